@@ -1,0 +1,329 @@
+/*
+ * koord_eval.h — C ABI of the MI355X-native koord-scheduler Filter/Score evaluator.
+ *
+ * This is the drop-in boundary for koord-scheduler's per-pod Filter/Score pass of
+ * LoadAwareScheduling, NodeNUMAResource (policy None, non-cpuset pods) and the framework's
+ * weighted-sum + selectHost step.  A Go scheduler binds it through cgo;
+ * the Python tests and bench bind it through ctypes.  No torch / HIP types cross it:
+ * plain structs, pointers and sizes only.
+ *
+ * What each entry point replaces in the reference (paths relative to haoyann/koordinator):
+ *   ke_create / ke_destroy        plugin factories  loadaware.New (pkg/scheduler/plugins/loadaware/load_aware.go:77-108),
+ *                                 nodenumaresource.NewWithOptions (pkg/scheduler/plugins/nodenumaresource/plugin.go:104-172),
+ *                                 registered through frameworkext.PluginFactoryProxy (pkg/scheduler/frameworkext/framework_extender_factory.go:325-343)
+ *   ke_node_upsert                NodeInfo snapshot + node annotations/labels read per call
+ *                                 (load_aware.go:155,160; plugin.go:408-442; estimator/default_estimator.go:124-143)
+ *   ke_nodemetric_upsert/_delete  nodeMetricLister.Get (load_aware.go:132,210) — NodeMetric informer events
+ *   ke_pod_assign / _unassign     podAssignCache.assign/unAssign (pkg/scheduler/plugins/loadaware/pod_assign_cache.go:89-136),
+ *                                 i.e. Reserve/Unreserve (load_aware.go:192-199) and pod informer OnAdd/OnUpdate/OnDelete (:138-181)
+ *   ke_node_set_requested         framework NodeInfo.Requested accounting (upstream assume/AddPod, k8s v1.28.7)
+ *   ke_node_set_cpuset_allocated  resourceManager.GetAvailableCPUs allocated count (nodenumaresource/resource_manager.go:130-164)
+ *   ke_eval                       per-node Filter + Score of all three plugins for a batch of pods
+ *                                 (load_aware.go:122-186,201-249; nodenumaresource/plugin.go:318-406; scoring.go:66-139);
+ *                                 parity mode returns the full pods x nodes status/score matrices
+ *   ke_schedule                   findNodesThatFitPod + RunScorePlugins + selectHost + Reserve for a queue of pods,
+ *                                 bit-exact with scheduling the pods one at a time (exact speculative batching)
+ *
+ * Conventions
+ *   - Return 0 on success, a negative KE_ERR_* on failure; ke_last_error() is thread-local.
+ *   - No pointer passed in is retained after the call returns (cgo rule).  All inputs are copied.
+ *   - A context is single-writer: the caller serialises calls on one context.
+ *   - Quantities are int64 in the unit the reference reads them in: cpu via Quantity.MilliValue(),
+ *     every other resource via Quantity.Value() (loadaware/helper.go:147-152).  Fractional quantities
+ *     must already be rounded up the way resource.Quantity does.
+ *   - Times are int64 unix nanoseconds; `now` is always passed explicitly.
+ *   - "absent" for an optional int64 is KE_ABSENT (-1) unless stated otherwise.
+ */
+#ifndef KOORD_EVAL_H
+#define KOORD_EVAL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KE_ABI_VERSION 1
+#define KE_ABSENT (-1)
+
+/* ---- error codes ---------------------------------------------------------------------------- */
+#define KE_OK 0
+#define KE_ERR_INVALID (-1)      /* bad argument / malformed object                              */
+#define KE_ERR_UNSUPPORTED (-2)  /* object uses a feature outside the implemented hot path      */
+#define KE_ERR_DEVICE (-3)       /* HIP runtime failure                                          */
+#define KE_ERR_NOT_FOUND (-4)    /* node / pod index not known                                   */
+#define KE_ERR_NO_DEVICE (-5)    /* evaluation requested but the HIP device/kernels are missing  */
+
+/* ---- framework status codes: k8s.io/kubernetes/pkg/scheduler/framework Code (v1.28.7) -------- */
+#define KE_CODE_SUCCESS 0
+#define KE_CODE_ERROR 1
+#define KE_CODE_UNSCHEDULABLE 2
+#define KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE 3
+#define KE_CODE_SKIP 5
+
+/* ---- filter failure reasons (which plugin / which message) ---------------------------------- */
+#define KE_REASON_NONE 0
+#define KE_REASON_LA_NODEMETRIC_EXPIRED 1    /* "node(s) nodeMetric expired"                 load_aware.go:46  */
+#define KE_REASON_LA_USAGE_CPU 2             /* "node(s) cpu usage exceed threshold"          load_aware.go:47  */
+#define KE_REASON_LA_USAGE_MEMORY 3          /* "node(s) memory usage exceed threshold"                         */
+#define KE_REASON_LA_AGG_USAGE_CPU 4         /* "node(s) cpu aggregated usage exceed threshold" load_aware.go:48 */
+#define KE_REASON_LA_AGG_USAGE_MEMORY 5
+#define KE_REASON_NUMA_INSUFFICIENT_AMPLIFIED_CPU 16 /* "Insufficient amplified cpu" nodenumaresource/plugin.go:57 */
+#define KE_REASON_NUMA_INVALID_AMPLIFICATION_RATIO 17 /* "node(s) invalid CPU amplification ratio" plugin.go:56 */
+#define KE_REASON_NUMA_INVALID_CPU_TOPOLOGY 18 /* "node(s) invalid CPU Topology" plugin.go:52 (GetAvailableCPUs) */
+
+/* ---- resources (index into per-resource arrays) ---------------------------------------------- */
+#define KE_RES_CPU 0          /* "cpu"                         MilliValue */
+#define KE_RES_MEMORY 1       /* "memory"                      Value      */
+#define KE_RES_BATCH_CPU 2    /* "kubernetes.io/batch-cpu"     Value      */
+#define KE_RES_BATCH_MEMORY 3 /* "kubernetes.io/batch-memory"  Value      */
+#define KE_RES_MID_CPU 4      /* "kubernetes.io/mid-cpu"       Value      */
+#define KE_RES_MID_MEMORY 5   /* "kubernetes.io/mid-memory"    Value      */
+#define KE_RES_COUNT 6
+#define KE_NRES 2             /* resources the LoadAware/NUMA scorers act on: cpu, memory */
+
+/* ---- koordinator priority / QoS classes (apis/extension/priority.go, qos.go) ----------------- */
+#define KE_PRIORITY_NONE 0
+#define KE_PRIORITY_PROD 1
+#define KE_PRIORITY_MID 2
+#define KE_PRIORITY_BATCH 3
+#define KE_PRIORITY_FREE 4
+
+#define KE_QOS_NONE 0
+#define KE_QOS_LSE 1
+#define KE_QOS_LSR 2
+#define KE_QOS_LS 3
+#define KE_QOS_BE 4
+#define KE_QOS_SYSTEM 5
+
+/* ---- NodeMetric aggregation types (apis/extension/constants.go:49-58) ------------------------ */
+#define KE_AGG_NONE 0 /* "" */
+#define KE_AGG_AVG 1
+#define KE_AGG_P50 2
+#define KE_AGG_P90 3
+#define KE_AGG_P95 4
+#define KE_AGG_P99 5
+#define KE_AGG_TYPES 6
+
+/* ---- scoring strategies (pkg/scheduler/apis/config/types.go:91-98) --------------------------- */
+#define KE_STRATEGY_LEAST_ALLOCATED 0
+#define KE_STRATEGY_MOST_ALLOCATED 1
+
+/* A resource map restricted to cpu/memory, with key presence (ResourceList semantics) and the
+ * total key count of the original map (len(ResourceList) matters in loadaware/helper.go:68,77,88). */
+typedef struct ke_resource_map {
+  int64_t value[KE_NRES];
+  uint8_t present[KE_NRES];
+  uint8_t pad[2];
+  int32_t n_keys; /* len() of the original ResourceList, including keys other than cpu/memory */
+} ke_resource_map; /* 24 bytes */
+
+/* LoadAwareSchedulingArgs after v1beta3 defaulting (pkg/scheduler/apis/config/types.go:31-87,
+ * v1beta3/defaults.go:89-114).  Threshold/weight/factor arrays are indexed by KE_RES_CPU/MEMORY,
+ * KE_ABSENT = key absent from the map.  Keys other than cpu/memory are not supported. */
+typedef struct ke_loadaware_args {
+  int64_t node_metric_expiration_seconds; /* KE_ABSENT = nil                       */
+  int64_t resource_weights[KE_NRES];
+  int64_t usage_thresholds[KE_NRES];
+  int64_t prod_usage_thresholds[KE_NRES];
+  int64_t estimated_scaling_factors[KE_NRES];
+  int64_t estimated_seconds_after_pod_scheduled; /* KE_ABSENT = nil */
+  int64_t estimated_seconds_after_initialized;   /* KE_ABSENT = nil */
+  /* Aggregated (nil when both types are KE_AGG_NONE and all thresholds absent) */
+  int64_t agg_usage_thresholds[KE_NRES];
+  int64_t agg_usage_duration_ns; /* 0 = "max non-empty duration" policy */
+  int64_t agg_score_duration_ns;
+  int32_t agg_usage_type;        /* KE_AGG_*  */
+  int32_t agg_score_type;        /* KE_AGG_*  */
+  uint8_t filter_expired_node_metrics;               /* *bool, default true  */
+  uint8_t enable_schedule_when_node_metrics_expired; /* *bool, default false */
+  uint8_t score_according_prod_usage;
+  uint8_t allow_customize_estimation;
+  uint8_t has_aggregated; /* args.Aggregated != nil */
+  uint8_t pad[3];
+} ke_loadaware_args;
+
+/* NodeNUMAResourceArgs.ScoringStrategy (types.go:114-125, v1beta3/defaults.go:118-153). */
+typedef struct ke_numa_args {
+  int64_t weights[KE_NRES]; /* KE_ABSENT = resource not in ScoringStrategy.Resources */
+  int32_t strategy;         /* KE_STRATEGY_*                                       */
+  int32_t pad;
+} ke_numa_args;
+
+/* Framework profile: score plugin weights (config/manager/scheduler-config.yaml:85-94). */
+typedef struct ke_config {
+  int32_t abi_version;    /* must be KE_ABI_VERSION                                      */
+  int32_t device_ordinal; /* HIP device used by this context (one process per GPU)      */
+  int64_t weight_loadaware;
+  int64_t weight_numa;
+  ke_loadaware_args loadaware;
+  ke_numa_args numa;
+  int32_t node_capacity;  /* max nodes this context will hold (device SoA is sized once) */
+  int32_t pod_batch;      /* B: pods evaluated per speculative batch in ke_schedule      */
+  int32_t global_node_offset; /* first global node index held by this shard (multi-GPU)  */
+  int32_t pad;
+} ke_config;
+
+/* A Node object (+ the NodeInfo aggregates the framework keeps for it). */
+typedef struct ke_node {
+  int64_t allocatable[KE_NRES];      /* node.Status.Allocatable == NodeInfo.Allocatable           */
+  int64_t raw_allocatable[KE_NRES];  /* annotation node.koordinator.sh/raw-allocatable, KE_ABSENT per key */
+  int64_t requested[KE_NRES];        /* NodeInfo.Requested (MilliCPU, Memory)                    */
+  double cpu_amplification_ratio;    /* annotation resource-amplification-ratio["cpu"]; -1 = not set */
+  int64_t cpuset_allocated_cpus;     /* CPUs held by cpuset pods (resourceManager allocated count)  */
+  /* annotation scheduling.koordinator.sh/usage-thresholds (apis/extension/load_aware.go:30-72) */
+  int64_t custom_usage_thresholds[KE_NRES];      /* KE_ABSENT per key */
+  int64_t custom_prod_usage_thresholds[KE_NRES]; /* KE_ABSENT per key */
+  int64_t custom_agg_thresholds[KE_NRES];        /* KE_ABSENT per key */
+  int64_t custom_agg_duration_ns;                /* 0 = nil / zero    */
+  /* TopologyOptions.AmplificationRatios["cpu"] as reported on the NodeResourceTopology
+   * (topology_options.go:150-162); Score prefers it over the node annotation (util.go:78-87).
+   * -2 = the NRT carries no ratio map (Score then reads the node annotation). */
+  double nrt_cpu_amplification_ratio;
+  int32_t custom_agg_type;                       /* KE_AGG_*           */
+  int32_t numa_topology_policy;    /* 0 = None; non-zero unsupported in ABI v1 */
+  int32_t cpu_bind_policy;         /* 0 = None; non-zero unsupported in ABI v1 */
+  uint8_t has_custom_thresholds;   /* annotation present and valid JSON  */
+  uint8_t custom_thresholds_error; /* annotation present but failed to unmarshal (helper.go:110) */
+  uint8_t has_custom_agg;          /* AggregatedUsage != nil in the annotation */
+  uint8_t amplification_error;     /* ratio annotation failed to unmarshal (plugin.go:421) */
+  uint8_t cpu_topology_invalid;    /* TopologyOptions.CPUTopology set but !IsValid() (resource_manager.go:502-504) */
+  uint8_t pad[7];
+} ke_node;
+
+/* One AggregatedUsage entry of NodeMetric.Status.NodeMetric.AggregatedNodeUsages. */
+typedef struct ke_aggregated_usage {
+  int64_t duration_ns;
+  ke_resource_map usage[KE_AGG_TYPES]; /* indexed by KE_AGG_*; n_keys == 0 means absent */
+} ke_aggregated_usage;
+
+/* One PodMetricInfo of NodeMetric.Status.PodsMetric. */
+typedef struct ke_pod_metric {
+  int64_t pod_key; /* interned namespace/name */
+  int32_t priority_class; /* PodMetricInfo.Priority as KE_PRIORITY_* */
+  int32_t pad;
+  ke_resource_map usage;
+} ke_pod_metric;
+
+/* NodeMetric header (slo/v1alpha1 nodemetric_types.go:38-136).  Pod metrics and aggregated usages
+ * are passed as separate arrays to ke_nodemetric_upsert. */
+typedef struct ke_node_metric {
+  int64_t update_time_ns;           /* valid if has_update_time */
+  int64_t report_interval_seconds;  /* Spec.CollectPolicy.ReportIntervalSeconds, KE_ABSENT = nil */
+  ke_resource_map node_usage;       /* Status.NodeMetric.NodeUsage */
+  uint8_t has_update_time;
+  uint8_t has_node_metric;          /* Status.NodeMetric != nil */
+  uint8_t pad[6];
+} ke_node_metric;
+
+/* A pod as the plugins see it.  Classes are resolved by the caller with the reference helpers
+ * GetPodPriorityClassWithDefault / GetPodQoSClassRaw (apis/extension/priority_utils.go:37-44,
+ * qos_utils.go:57-62); requests/limits are resourceapi.PodRequests/PodLimits. */
+typedef struct ke_pod {
+  int64_t pod_key; /* interned namespace/name (matches ke_pod_metric.pod_key) */
+  int64_t uid;
+  int64_t requests[KE_RES_COUNT];
+  int64_t limits[KE_RES_COUNT];
+  int64_t custom_scaling_factors[KE_NRES];      /* annotation load-estimated-scaling-factors, KE_ABSENT per key */
+  int64_t custom_seconds_after_scheduled;       /* KE_ABSENT = not set / unparsable */
+  int64_t custom_seconds_after_initialized;     /* KE_ABSENT */
+  int64_t scheduled_transition_ns;              /* PodScheduled=True LastTransitionTime, valid if has_scheduled */
+  int64_t initialized_transition_ns;            /* Initialized=True LastTransitionTime, valid if has_initialized */
+  int32_t priority_class; /* KE_PRIORITY_* (with default)  */
+  int32_t qos_class;      /* KE_QOS_* (raw label)          */
+  uint8_t is_daemonset;   /* an OwnerReference of Kind DaemonSet */
+  uint8_t has_custom_scaling_factors; /* annotation parsed into a non-empty map */
+  uint8_t has_scheduled;
+  uint8_t has_initialized;
+  uint8_t is_terminated;
+  uint8_t has_resource_spec;          /* cpuset annotations: unsupported in ABI v1 */
+  uint8_t has_other_requests;         /* PodRequests has a non-zero resource outside KE_RES_* */
+  uint8_t pad;
+} ke_pod;
+
+/* One candidate of a pod's speculative top-k list (device order: best first). */
+typedef struct ke_candidate {
+  int32_t node;  /* node index, -1 = none */
+  int32_t score; /* framework total score */
+} ke_candidate;
+
+typedef struct ke_ctx ke_ctx;
+
+/* ---- lifecycle ------------------------------------------------------------------------------- */
+int ke_create(const ke_config* cfg, ke_ctx** out);
+void ke_destroy(ke_ctx* ctx);
+const char* ke_last_error(void);
+int ke_abi_version(void);
+/* sizeof() of ke_config, ke_node, ke_node_metric, ke_pod_metric, ke_aggregated_usage, ke_pod,
+ * ke_resource_map, ke_loadaware_args, ke_numa_args (in that order) for binding-layout checks. */
+int ke_abi_struct_sizes(int32_t* sizes, int32_t n);
+/* 1 if this build has a usable HIP device and its gfx950 kernels loaded, else 0. */
+int ke_device_available(void);
+
+/* ---- state ingestion (informer events) ------------------------------------------------------- */
+/* Insert or replace node `node` (0 <= node < node_capacity).  Keeps its NodeMetric / assigned pods. */
+int ke_node_upsert(ke_ctx* ctx, int32_t node, const ke_node* n);
+/* Bulk load nodes [0, n): equivalent to n ke_node_upsert calls (initial informer list). */
+int ke_nodes_load(ke_ctx* ctx, int32_t n, const ke_node* nodes);
+int ke_node_set_requested(ke_ctx* ctx, int32_t node, int64_t milli_cpu, int64_t memory);
+int ke_node_set_cpuset_allocated(ke_ctx* ctx, int32_t node, int64_t cpus);
+/* Replace the NodeMetric of `node` (lister Get succeeds afterwards). */
+int ke_nodemetric_upsert(ke_ctx* ctx, int32_t node, const ke_node_metric* nm,
+                         int32_t n_pod_metrics, const ke_pod_metric* pod_metrics,
+                         int32_t n_aggregated, const ke_aggregated_usage* aggregated);
+/* Bulk NodeMetric load for nodes [0,n): pod metrics / aggregated usages are flattened, node i owns
+ * pod_metrics[pm_offsets[i] .. pm_offsets[i+1]) (offsets have n+1 entries). */
+int ke_nodemetrics_load(ke_ctx* ctx, int32_t n, const ke_node_metric* nms,
+                        const int64_t* pm_offsets, const ke_pod_metric* pod_metrics,
+                        const int64_t* agg_offsets, const ke_aggregated_usage* aggregated);
+int ke_nodemetric_delete(ke_ctx* ctx, int32_t node); /* lister Get -> NotFound */
+/* podAssignCache.assign(nodeName, pod): `timestamp_ns` is used when the pod has no PodScheduled
+ * condition (pod_assign_cache.go:99-122, timeNowFn fallback). */
+int ke_pod_assign(ke_ctx* ctx, int32_t node, const ke_pod* pod, int64_t timestamp_ns);
+int ke_pod_unassign(ke_ctx* ctx, int32_t node, int64_t uid);
+
+/* DefaultEstimator.EstimatePod (loadaware/estimator/default_estimator.go:59-122) under this
+ * context's args: est[KE_NRES] (cpu milli, memory bytes), KE_ABSENT for a resource without weight. */
+int ke_estimate_pod(ke_ctx* ctx, const ke_pod* pod, int64_t* est);
+
+/* ---- evaluation ------------------------------------------------------------------------------ */
+/* Parity mode: Filter + Score of `n_pods` pods against every node, no state change.
+ * Each output is optional (NULL) and laid out [pod][node]:
+ *   status   uint8  KE_CODE_* of the first failing filter (profile order LoadAware, NodeNUMAResource)
+ *   reason   uint8  KE_REASON_*
+ *   la_score int16  LoadAwareScheduling.Score (0 for filtered-out nodes)
+ *   numa_score int16 NodeNUMAResource.Score
+ *   total    int16  Σ weight·score over the plugins, -1 if the node is filtered out
+ * and `best[pod]` is selectHost's choice (-1 if no feasible node; ties -> lowest node index). */
+int ke_eval(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
+            uint8_t* status, uint8_t* reason, int16_t* la_score, int16_t* numa_score,
+            int16_t* total, int32_t* best);
+
+/* Schedule `n_pods` pods in queue order, each one seeing the Reserve of all pods before it
+ * (LoadAware podAssignCache.assign with timestamp now_ns, NodeInfo.Requested += pod requests).
+ * chosen[p] = node index or -1 (unschedulable), score[p] = its framework total (or -1).
+ * Bit-exact with one-pod-at-a-time scheduling (exact speculative batching). */
+int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
+                int32_t* chosen, int32_t* score);
+
+/* Timing of the last ke_schedule call: device milliseconds of the whole queue, and per-batch
+ * latency (pod dequeue -> node selected) in milliseconds, n_batches entries. */
+int ke_last_schedule_stats(ke_ctx* ctx, double* total_ms, int32_t* n_batches,
+                           double* batch_ms, int32_t batch_ms_cap);
+
+/* ---- introspection (tests, tools) ------------------------------------------------------------ */
+/* sizeof() of one node row of the device SoA in bytes (algorithmic bytes per node per pass). */
+int ke_row_bytes(void);
+/* Copy the device SoA rows of nodes [0,n) back to the host (n*ke_row_bytes() bytes) and, into
+ * `host_rows`, the rows the host derives from its object state; lets tests check the GPU-side
+ * patches against a from-scratch host derivation. */
+int ke_debug_rows(ke_ctx* ctx, int32_t n, int64_t now_ns, void* device_rows, void* host_rows);
+/* The folded LoadAware threshold U*(total, thr): the largest `used` with
+ * int64(math.Round(float64(used)/float64(total)*100)) <= thr (load_aware.go:299), |used| <= 2^53. */
+int64_t ke_debug_usage_bound(int64_t total, int64_t thr);
+int32_t ke_num_nodes(ke_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KOORD_EVAL_H */

@@ -1,0 +1,259 @@
+"""ctypes mirror of include/koord_eval.h (the C-ABI boundary) and the loader for libkoordeval.so.
+
+Only plain structs cross the boundary; this module is the Python-side equivalent of the cgo binding a
+Go koord-scheduler would use.  Struct layouts are checked against the library's own
+sizeof() values at load time (ke_abi_struct_sizes).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+ABI_VERSION = 1
+ABSENT = -1
+
+OK = 0
+ERR_INVALID, ERR_UNSUPPORTED, ERR_DEVICE, ERR_NOT_FOUND, ERR_NO_DEVICE = -1, -2, -3, -4, -5
+
+CODE_SUCCESS, CODE_ERROR, CODE_UNSCHEDULABLE, CODE_UNSCHEDULABLE_AND_UNRESOLVABLE, CODE_SKIP = 0, 1, 2, 3, 5
+
+REASON_NONE = 0
+REASON_LA_NODEMETRIC_EXPIRED = 1
+REASON_LA_USAGE_CPU = 2
+REASON_LA_USAGE_MEMORY = 3
+REASON_LA_AGG_USAGE_CPU = 4
+REASON_LA_AGG_USAGE_MEMORY = 5
+REASON_NUMA_INSUFFICIENT_AMPLIFIED_CPU = 16
+REASON_NUMA_INVALID_AMPLIFICATION_RATIO = 17
+REASON_NUMA_INVALID_CPU_TOPOLOGY = 18
+
+RES_CPU, RES_MEMORY, RES_BATCH_CPU, RES_BATCH_MEMORY, RES_MID_CPU, RES_MID_MEMORY = range(6)
+RES_COUNT = 6
+NRES = 2
+
+PRIORITY_NONE, PRIORITY_PROD, PRIORITY_MID, PRIORITY_BATCH, PRIORITY_FREE = range(5)
+QOS_NONE, QOS_LSE, QOS_LSR, QOS_LS, QOS_BE, QOS_SYSTEM = range(6)
+AGG_NONE, AGG_AVG, AGG_P50, AGG_P90, AGG_P95, AGG_P99 = range(6)
+AGG_TYPES = 6
+STRATEGY_LEAST_ALLOCATED, STRATEGY_MOST_ALLOCATED = 0, 1
+
+i64, i32, u8, f64 = C.c_int64, C.c_int32, C.c_uint8, C.c_double
+
+
+class ResourceMap(C.Structure):
+    _fields_ = [("value", i64 * NRES), ("present", u8 * NRES), ("pad", u8 * 2), ("n_keys", i32)]
+
+
+class LoadAwareArgs(C.Structure):
+    _fields_ = [
+        ("node_metric_expiration_seconds", i64),
+        ("resource_weights", i64 * NRES),
+        ("usage_thresholds", i64 * NRES),
+        ("prod_usage_thresholds", i64 * NRES),
+        ("estimated_scaling_factors", i64 * NRES),
+        ("estimated_seconds_after_pod_scheduled", i64),
+        ("estimated_seconds_after_initialized", i64),
+        ("agg_usage_thresholds", i64 * NRES),
+        ("agg_usage_duration_ns", i64),
+        ("agg_score_duration_ns", i64),
+        ("agg_usage_type", i32),
+        ("agg_score_type", i32),
+        ("filter_expired_node_metrics", u8),
+        ("enable_schedule_when_node_metrics_expired", u8),
+        ("score_according_prod_usage", u8),
+        ("allow_customize_estimation", u8),
+        ("has_aggregated", u8),
+        ("pad", u8 * 3),
+    ]
+
+
+class NumaArgs(C.Structure):
+    _fields_ = [("weights", i64 * NRES), ("strategy", i32), ("pad", i32)]
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("abi_version", i32),
+        ("device_ordinal", i32),
+        ("weight_loadaware", i64),
+        ("weight_numa", i64),
+        ("loadaware", LoadAwareArgs),
+        ("numa", NumaArgs),
+        ("node_capacity", i32),
+        ("pod_batch", i32),
+        ("global_node_offset", i32),
+        ("pad", i32),
+    ]
+
+
+class Node(C.Structure):
+    _fields_ = [
+        ("allocatable", i64 * NRES),
+        ("raw_allocatable", i64 * NRES),
+        ("requested", i64 * NRES),
+        ("cpu_amplification_ratio", f64),
+        ("cpuset_allocated_cpus", i64),
+        ("custom_usage_thresholds", i64 * NRES),
+        ("custom_prod_usage_thresholds", i64 * NRES),
+        ("custom_agg_thresholds", i64 * NRES),
+        ("custom_agg_duration_ns", i64),
+        ("nrt_cpu_amplification_ratio", f64),
+        ("custom_agg_type", i32),
+        ("numa_topology_policy", i32),
+        ("cpu_bind_policy", i32),
+        ("has_custom_thresholds", u8),
+        ("custom_thresholds_error", u8),
+        ("has_custom_agg", u8),
+        ("amplification_error", u8),
+        ("cpu_topology_invalid", u8),
+        ("pad", u8 * 7),
+    ]
+
+
+class AggregatedUsage(C.Structure):
+    _fields_ = [("duration_ns", i64), ("usage", ResourceMap * AGG_TYPES)]
+
+
+class PodMetric(C.Structure):
+    _fields_ = [("pod_key", i64), ("priority_class", i32), ("pad", i32), ("usage", ResourceMap)]
+
+
+class NodeMetric(C.Structure):
+    _fields_ = [
+        ("update_time_ns", i64),
+        ("report_interval_seconds", i64),
+        ("node_usage", ResourceMap),
+        ("has_update_time", u8),
+        ("has_node_metric", u8),
+        ("pad", u8 * 6),
+    ]
+
+
+class Pod(C.Structure):
+    _fields_ = [
+        ("pod_key", i64),
+        ("uid", i64),
+        ("requests", i64 * RES_COUNT),
+        ("limits", i64 * RES_COUNT),
+        ("custom_scaling_factors", i64 * NRES),
+        ("custom_seconds_after_scheduled", i64),
+        ("custom_seconds_after_initialized", i64),
+        ("scheduled_transition_ns", i64),
+        ("initialized_transition_ns", i64),
+        ("priority_class", i32),
+        ("qos_class", i32),
+        ("is_daemonset", u8),
+        ("has_custom_scaling_factors", u8),
+        ("has_scheduled", u8),
+        ("has_initialized", u8),
+        ("is_terminated", u8),
+        ("has_resource_spec", u8),
+        ("has_other_requests", u8),
+        ("pad", u8),
+    ]
+
+
+STRUCTS = [Config, Node, NodeMetric, PodMetric, AggregatedUsage, Pod, ResourceMap, LoadAwareArgs, NumaArgs]
+
+# numpy views of the same layouts (bulk loads)
+NODE_DTYPE = np.dtype(Node)
+NODE_METRIC_DTYPE = np.dtype(NodeMetric)
+POD_METRIC_DTYPE = np.dtype(PodMetric)
+AGG_DTYPE = np.dtype(AggregatedUsage)
+POD_DTYPE = np.dtype(Pod)
+
+ROW_DTYPE = np.dtype([("f", np.int64, (18,)), ("flags", np.uint32), ("pad", np.uint32)])
+
+
+def default_config(node_capacity, pod_batch=64, device_ordinal=0, global_node_offset=0):
+    """ke_config with v1beta3 defaults (pkg/scheduler/apis/config/v1beta3/defaults.go:89-153) and the
+    default profile's plugin weights 1/1 (config/manager/scheduler-config.yaml:85-94)."""
+    cfg = Config()
+    cfg.abi_version = ABI_VERSION
+    cfg.device_ordinal = device_ordinal
+    cfg.weight_loadaware = 1
+    cfg.weight_numa = 1
+    a = cfg.loadaware
+    a.node_metric_expiration_seconds = 180
+    a.resource_weights[:] = [1, 1]
+    a.usage_thresholds[:] = [65, 95]
+    a.prod_usage_thresholds[:] = [ABSENT, ABSENT]
+    a.estimated_scaling_factors[:] = [85, 70]
+    a.estimated_seconds_after_pod_scheduled = ABSENT
+    a.estimated_seconds_after_initialized = ABSENT
+    a.agg_usage_thresholds[:] = [ABSENT, ABSENT]
+    a.agg_usage_type = AGG_NONE
+    a.agg_score_type = AGG_NONE
+    a.filter_expired_node_metrics = 1
+    a.enable_schedule_when_node_metrics_expired = 0
+    cfg.numa.weights[:] = [1, 1]
+    cfg.numa.strategy = STRATEGY_LEAST_ALLOCATED
+    cfg.node_capacity = node_capacity
+    cfg.pod_batch = pod_batch
+    cfg.global_node_offset = global_node_offset
+    return cfg
+
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkoordeval.so")
+
+EXPORTS = {
+    # name: (restype, argtypes)
+    "ke_create": (C.c_int, [C.POINTER(Config), C.POINTER(C.c_void_p)]),
+    "ke_destroy": (None, [C.c_void_p]),
+    "ke_last_error": (C.c_char_p, []),
+    "ke_abi_version": (C.c_int, []),
+    "ke_abi_struct_sizes": (C.c_int, [C.POINTER(i32), i32]),
+    "ke_device_available": (C.c_int, []),
+    "ke_node_upsert": (C.c_int, [C.c_void_p, i32, C.POINTER(Node)]),
+    "ke_nodes_load": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
+    "ke_node_set_requested": (C.c_int, [C.c_void_p, i32, i64, i64]),
+    "ke_node_set_cpuset_allocated": (C.c_int, [C.c_void_p, i32, i64]),
+    "ke_nodemetric_upsert": (C.c_int, [C.c_void_p, i32, C.POINTER(NodeMetric), i32, C.c_void_p, i32, C.c_void_p]),
+    "ke_nodemetrics_load": (C.c_int, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "ke_nodemetric_delete": (C.c_int, [C.c_void_p, i32]),
+    "ke_pod_assign": (C.c_int, [C.c_void_p, i32, C.POINTER(Pod), i64]),
+    "ke_pod_unassign": (C.c_int, [C.c_void_p, i32, i64]),
+    "ke_estimate_pod": (C.c_int, [C.c_void_p, C.POINTER(Pod), C.c_void_p]),
+    "ke_eval": (C.c_int, [C.c_void_p, i32, C.c_void_p, i64] + [C.c_void_p] * 6),
+    "ke_schedule": (C.c_int, [C.c_void_p, i32, C.c_void_p, i64, C.c_void_p, C.c_void_p]),
+    "ke_last_schedule_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(i32), C.c_void_p, i32]),
+    "ke_row_bytes": (C.c_int, []),
+    "ke_debug_rows": (C.c_int, [C.c_void_p, i32, i64, C.c_void_p, C.c_void_p]),
+    "ke_debug_usage_bound": (i64, [i64, i64]),
+    "ke_num_nodes": (i32, [C.c_void_p]),
+}
+
+_lib = None
+
+
+def load_library(path=LIB_PATH):
+    """Load libkoordeval.so (built by __graft_entry__.build()).  Raises if missing: there is no
+    Python or CPU fallback for the evaluator."""
+    global _lib
+    if _lib is not None and path == LIB_PATH:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+    lib = C.CDLL(path)
+    for name, (res, args) in EXPORTS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.ke_abi_version() != ABI_VERSION:
+        raise RuntimeError("libkoordeval.so ABI version mismatch")
+    sizes = (i32 * len(STRUCTS))()
+    lib.ke_abi_struct_sizes(sizes, len(STRUCTS))
+    for s, n in zip(STRUCTS, sizes):
+        if C.sizeof(s) != n:
+            raise RuntimeError(f"ABI layout mismatch for {s.__name__}: python {C.sizeof(s)} != C {n}")
+    if path == LIB_PATH:
+        _lib = lib
+    return lib
+
+
+def ptr(arr):
+    """void* of a numpy array (or None)."""
+    if arr is None:
+        return None
+    return C.c_void_p(arr.ctypes.data)

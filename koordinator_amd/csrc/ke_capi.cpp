@@ -1,0 +1,290 @@
+// ke_capi.cpp — the extern "C" boundary (include/koord_eval.h) over the host state (ke_host.cpp)
+// and the device evaluator (ke_kernels.hip).
+#include <algorithm>
+#include <cstring>
+#include <new>
+
+#include "ke_host.h"
+
+namespace ke {
+const char* last_error_cstr();
+int device_available();
+int device_create(Context* ctx);
+void device_destroy(Context* ctx);
+int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, uint8_t* status, uint8_t* reason,
+                int16_t* la, int16_t* numa, int16_t* total, int32_t* best);
+int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t* chosen, int32_t* score);
+int device_debug_rows(Context* ctx, int32_t n, Row* out);
+}  // namespace ke
+
+using namespace ke;
+
+struct ke_ctx {
+  Context c;
+};
+
+static int check_node(ke_ctx* ctx, int32_t node) {
+  if (!ctx) return fail(KE_ERR_INVALID, "null context");
+  if (node < 0 || node >= ctx->c.cfg.node_capacity) return fail(KE_ERR_NOT_FOUND, "node index out of range");
+  return KE_OK;
+}
+
+static int check_pods(const ke_pod* pods, int32_t n) {
+  if (n < 0 || (n > 0 && !pods)) return fail(KE_ERR_INVALID, "pods");
+  for (int32_t p = 0; p < n; p++) {
+    int rc = validate_pod(pods[p]);
+    if (rc) return rc;
+  }
+  return KE_OK;
+}
+
+static int require_device(ke_ctx* ctx) {
+  if (!ctx->c.dev) return fail(KE_ERR_NO_DEVICE, "evaluation needs the gfx950 device; this context has none");
+  return KE_OK;
+}
+
+extern "C" {
+
+int ke_abi_version(void) { return KE_ABI_VERSION; }
+int ke_abi_struct_sizes(int32_t* sizes, int32_t n) {
+  const int32_t all[] = {(int32_t)sizeof(ke_config),       (int32_t)sizeof(ke_node),
+                         (int32_t)sizeof(ke_node_metric),  (int32_t)sizeof(ke_pod_metric),
+                         (int32_t)sizeof(ke_aggregated_usage), (int32_t)sizeof(ke_pod),
+                         (int32_t)sizeof(ke_resource_map), (int32_t)sizeof(ke_loadaware_args),
+                         (int32_t)sizeof(ke_numa_args)};
+  const int32_t m = (int32_t)(sizeof(all) / sizeof(all[0]));
+  for (int32_t i = 0; i < n && i < m; i++) sizes[i] = all[i];
+  return m;
+}
+const char* ke_last_error(void) { return last_error_cstr(); }
+int ke_device_available(void) { return device_available(); }
+int ke_row_bytes(void) { return ROW_BYTES; }
+
+int ke_create(const ke_config* cfg, ke_ctx** out) {
+  if (!cfg || !out) return fail(KE_ERR_INVALID, "null argument");
+  *out = nullptr;
+  int rc = validate_config(*cfg);
+  if (rc) return rc;
+  ke_ctx* ctx = new (std::nothrow) ke_ctx();
+  if (!ctx) return fail(KE_ERR_INVALID, "out of memory");
+  Context& c = ctx->c;
+  c.cfg = *cfg;
+  c.nodes.resize((size_t)cfg->node_capacity);
+  KArgs& k = c.kargs_template;
+  const ke_loadaware_args& a = cfg->loadaware;
+  k.exp_s = a.node_metric_expiration_seconds;
+  uint32_t f = 0;
+  if (a.filter_expired_node_metrics) f |= AF_FILTER_EXPIRED;
+  if (a.enable_schedule_when_node_metrics_expired) f |= AF_ENABLE_WHEN_EXPIRED;
+  if (a.node_metric_expiration_seconds != KE_ABSENT) f |= AF_EXP_PRESENT;
+  if (cfg->numa.strategy == KE_STRATEGY_MOST_ALLOCATED) f |= AF_NUMA_MOST;
+  k.flags = f;
+  k.wsum_la = k.wsum_numa = 0;
+  for (int r = 0; r < KE_NRES; r++) {
+    k.w_la[r] = a.resource_weights[r] == KE_ABSENT ? 0 : (int32_t)a.resource_weights[r];
+    k.w_numa[r] = cfg->numa.weights[r] == KE_ABSENT ? 0 : (int32_t)cfg->numa.weights[r];
+    k.wsum_la += k.w_la[r];
+    k.wsum_numa += k.w_numa[r];
+  }
+  k.wp_la = (int32_t)cfg->weight_loadaware;
+  k.wp_numa = (int32_t)cfg->weight_numa;
+  if (device_available()) {
+    rc = device_create(&c);
+    if (rc) {
+      device_destroy(&c);
+      delete ctx;
+      return rc;
+    }
+  }
+  *out = ctx;
+  return KE_OK;
+}
+
+void ke_destroy(ke_ctx* ctx) {
+  if (!ctx) return;
+  device_destroy(&ctx->c);
+  delete ctx;
+}
+
+int32_t ke_num_nodes(ke_ctx* ctx) { return ctx ? ctx->c.n_nodes : 0; }
+
+int ke_node_upsert(ke_ctx* ctx, int32_t node, const ke_node* n) {
+  int rc = check_node(ctx, node);
+  if (rc) return rc;
+  if (!n) return fail(KE_ERR_INVALID, "null node");
+  rc = validate_node(*n);
+  if (rc) return rc;
+  NodeState& ns = ctx->c.nodes[node];
+  ns.valid = true;
+  ns.node = *n;
+  ns.dirty = true;
+  ctx->c.n_nodes = std::max(ctx->c.n_nodes, node + 1);
+  return KE_OK;
+}
+
+int ke_nodes_load(ke_ctx* ctx, int32_t n, const ke_node* nodes) {
+  if (!ctx || n < 0 || (n > 0 && !nodes)) return fail(KE_ERR_INVALID, "ke_nodes_load arguments");
+  if (n > ctx->c.cfg.node_capacity) return fail(KE_ERR_INVALID, "more nodes than node_capacity");
+  for (int32_t i = 0; i < n; i++) {
+    int rc = ke_node_upsert(ctx, i, &nodes[i]);
+    if (rc) return rc;
+  }
+  return KE_OK;
+}
+
+int ke_node_set_requested(ke_ctx* ctx, int32_t node, int64_t milli_cpu, int64_t memory) {
+  int rc = check_node(ctx, node);
+  if (rc) return rc;
+  NodeState& ns = ctx->c.nodes[node];
+  ns.node.requested[KE_RES_CPU] = milli_cpu;
+  ns.node.requested[KE_RES_MEMORY] = memory;
+  ns.dirty = true;
+  return KE_OK;
+}
+
+int ke_node_set_cpuset_allocated(ke_ctx* ctx, int32_t node, int64_t cpus) {
+  int rc = check_node(ctx, node);
+  if (rc) return rc;
+  NodeState& ns = ctx->c.nodes[node];
+  ns.node.cpuset_allocated_cpus = cpus;
+  ns.dirty = true;
+  return KE_OK;
+}
+
+int ke_nodemetric_upsert(ke_ctx* ctx, int32_t node, const ke_node_metric* nm, int32_t n_pm, const ke_pod_metric* pm,
+                         int32_t n_agg, const ke_aggregated_usage* agg) {
+  int rc = check_node(ctx, node);
+  if (rc) return rc;
+  if (!nm || n_pm < 0 || n_agg < 0 || (n_pm && !pm) || (n_agg && !agg)) return fail(KE_ERR_INVALID, "nodemetric");
+  NodeState& ns = ctx->c.nodes[node];
+  ns.has_metric = true;
+  ns.nm = *nm;
+  ns.pm.assign(pm, pm + n_pm);
+  ns.agg.assign(agg, agg + n_agg);
+  ns.dirty = true;
+  return KE_OK;
+}
+
+int ke_nodemetrics_load(ke_ctx* ctx, int32_t n, const ke_node_metric* nms, const int64_t* pm_offsets,
+                        const ke_pod_metric* pod_metrics, const int64_t* agg_offsets, const ke_aggregated_usage* aggregated) {
+  if (!ctx || n < 0 || (n > 0 && (!nms || !pm_offsets || !agg_offsets))) return fail(KE_ERR_INVALID, "nodemetrics_load");
+  for (int32_t i = 0; i < n; i++) {
+    const int64_t p0 = pm_offsets[i], p1 = pm_offsets[i + 1], a0 = agg_offsets[i], a1 = agg_offsets[i + 1];
+    if (p1 < p0 || a1 < a0) return fail(KE_ERR_INVALID, "offsets must be non-decreasing");
+    int rc = ke_nodemetric_upsert(ctx, i, &nms[i], (int32_t)(p1 - p0), pod_metrics ? pod_metrics + p0 : nullptr,
+                                  (int32_t)(a1 - a0), aggregated ? aggregated + a0 : nullptr);
+    if (rc) return rc;
+  }
+  return KE_OK;
+}
+
+int ke_nodemetric_delete(ke_ctx* ctx, int32_t node) {
+  int rc = check_node(ctx, node);
+  if (rc) return rc;
+  NodeState& ns = ctx->c.nodes[node];
+  ns.has_metric = false;
+  ns.nm = ke_node_metric{};
+  ns.pm.clear();
+  ns.agg.clear();
+  ns.dirty = true;
+  return KE_OK;
+}
+
+int ke_pod_assign(ke_ctx* ctx, int32_t node, const ke_pod* pod, int64_t timestamp_ns) {
+  int rc = check_node(ctx, node);
+  if (rc) return rc;
+  if (!pod) return fail(KE_ERR_INVALID, "null pod");
+  host_assign(ctx->c.cfg, ctx->c.nodes[node], *pod, timestamp_ns);
+  return KE_OK;
+}
+
+int ke_pod_unassign(ke_ctx* ctx, int32_t node, int64_t uid) {
+  int rc = check_node(ctx, node);
+  if (rc) return rc;
+  auto& v = ctx->c.nodes[node].asg;
+  for (size_t i = 0; i < v.size(); i++) {
+    if (v[i].pod.uid == uid) {
+      v.erase(v.begin() + (long)i);
+      ctx->c.nodes[node].dirty = true;
+      break;
+    }
+  }
+  return KE_OK;
+}
+
+int ke_estimate_pod(ke_ctx* ctx, const ke_pod* pod, int64_t* est) {
+  if (!ctx || !pod || !est) return fail(KE_ERR_INVALID, "ke_estimate_pod arguments");
+  uint8_t present[KE_NRES];
+  estimate_pod(ctx->c.cfg.loadaware, *pod, est, present);
+  for (int r = 0; r < KE_NRES; r++)
+    if (!present[r]) est[r] = KE_ABSENT;
+  return KE_OK;
+}
+
+int ke_eval(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, uint8_t* status, uint8_t* reason,
+            int16_t* la_score, int16_t* numa_score, int16_t* total, int32_t* best) {
+  if (!ctx) return fail(KE_ERR_INVALID, "null context");
+  int rc = check_pods(pods, n_pods);
+  if (rc) return rc;
+  rc = require_device(ctx);
+  if (rc) return rc;
+  return device_eval(&ctx->c, n_pods, pods, now_ns, status, reason, la_score, numa_score, total, best);
+}
+
+int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int32_t* chosen, int32_t* score) {
+  if (!ctx || (n_pods > 0 && !chosen)) return fail(KE_ERR_INVALID, "ke_schedule arguments");
+  int rc = check_pods(pods, n_pods);
+  if (rc) return rc;
+  rc = require_device(ctx);
+  if (rc) return rc;
+  rc = device_schedule(&ctx->c, n_pods, pods, now_ns, chosen, score);
+  if (rc) return rc;
+  // Host mirror of the Reserves the device already applied to its rows: keep the object state
+  // (assign cache, NodeInfo.Requested) in step so later re-derivations include these pods.
+  const int32_t off = ctx->c.cfg.global_node_offset;
+  std::vector<int32_t> touched;
+  for (int32_t p = 0; p < n_pods; p++) {
+    const int32_t node = chosen[p] - off;
+    if (chosen[p] < 0 || node < 0 || node >= ctx->c.n_nodes) continue;
+    NodeState& ns = ctx->c.nodes[node];
+    const bool was_dirty = ns.dirty;
+    host_assign(ctx->c.cfg, ns, pods[p], now_ns);
+    ns.node.requested[KE_RES_CPU] += pods[p].requests[KE_RES_CPU];
+    ns.node.requested[KE_RES_MEMORY] += pods[p].requests[KE_RES_MEMORY];
+    ns.dirty = was_dirty;  // the device row already carries this Reserve
+  }
+  return KE_OK;
+}
+
+int ke_last_schedule_stats(ke_ctx* ctx, double* total_ms, int32_t* n_batches, double* batch_ms, int32_t batch_ms_cap) {
+  if (!ctx) return fail(KE_ERR_INVALID, "null context");
+  if (total_ms) *total_ms = ctx->c.last_total_ms;
+  if (n_batches) *n_batches = (int32_t)ctx->c.last_batch_ms.size();
+  if (batch_ms) {
+    const int32_t n = std::min<int32_t>(batch_ms_cap, (int32_t)ctx->c.last_batch_ms.size());
+    for (int32_t i = 0; i < n; i++) batch_ms[i] = ctx->c.last_batch_ms[i];
+  }
+  return KE_OK;
+}
+
+int64_t ke_debug_usage_bound(int64_t total, int64_t thr) { return total > 0 ? max_used_within(total, thr) : 0; }
+
+int ke_debug_rows(ke_ctx* ctx, int32_t n, int64_t now_ns, void* device_rows, void* host_rows) {
+  if (!ctx || n < 0 || n > ctx->c.n_nodes) return fail(KE_ERR_INVALID, "ke_debug_rows arguments");
+  if (device_rows) {
+    int rc = require_device(ctx);
+    if (rc) return rc;
+    rc = device_debug_rows(&ctx->c, n, (Row*)device_rows);
+    if (rc) return rc;
+  }
+  if (host_rows) {
+    Row* out = (Row*)host_rows;
+    for (int32_t i = 0; i < n; i++) {
+      int64_t vu;
+      derive_row(ctx->c.cfg, ctx->c.nodes[i], now_ns, &out[i], &vu);
+    }
+  }
+  return KE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,409 @@
+// ke_host.cpp — folding of the informer-fed object state into GPU node rows.
+//
+// The reference recomputes GetEstimatedUsed (load_aware.go:251-288) from the NodeMetric and the
+// podAssignCache on every Filter and every Score call.  Everything in it except the pod's own
+// estimate is a function of the node alone, so here it is computed once per node state change and
+// stored as a per-variant "term"; the pod enters the device arithmetic only through its estimate.
+#include "ke_host.h"
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <unordered_map>
+
+namespace ke {
+
+static thread_local std::string g_error;
+void set_error(const std::string& msg) { g_error = msg; }
+int fail(int code, const std::string& msg) {
+  g_error = msg;
+  return code;
+}
+const char* last_error_cstr() { return g_error.c_str(); }
+
+constexpr int64_t NS = 1000000000LL;
+constexpr int64_t DEFAULT_MILLI_CPU = 250;                 // default_estimator.go:36
+constexpr int64_t DEFAULT_MEMORY = 200LL * 1024 * 1024;    // default_estimator.go:38
+constexpr int64_t DEFAULT_REPORT_INTERVAL_NS = 60 * NS;    // load_aware.go:58
+constexpr int64_t USED_DOMAIN = 1LL << 53;                 // threshold folding is exact for |used| <= 2^53
+
+// ---------------------------------------------------------------------------------------------
+// validation
+// ---------------------------------------------------------------------------------------------
+int validate_config(const ke_config& cfg) {
+  if (cfg.abi_version != KE_ABI_VERSION) return fail(KE_ERR_INVALID, "ke_config.abi_version mismatch");
+  if (cfg.node_capacity <= 0 || cfg.node_capacity > MAX_SHARD_NODES)
+    return fail(KE_ERR_INVALID, "node_capacity out of range (1 .. 2^23-1 per shard)");
+  if (cfg.pod_batch < 1 || cfg.pod_batch > MAX_BATCH) return fail(KE_ERR_INVALID, "pod_batch out of range (1..64)");
+  if (cfg.weight_loadaware < 0 || cfg.weight_numa < 0 || (cfg.weight_loadaware + cfg.weight_numa) * 100 > MAX_TOTAL_SCORE)
+    return fail(KE_ERR_UNSUPPORTED, "plugin weights: (w_loadaware + w_numa) * 100 must be <= 510");
+  for (int r = 0; r < KE_NRES; r++) {
+    int64_t w = cfg.loadaware.resource_weights[r];
+    if (w != KE_ABSENT && (w < 0 || w > (1 << 20))) return fail(KE_ERR_UNSUPPORTED, "loadaware weight out of range");
+    w = cfg.numa.weights[r];
+    if (w != KE_ABSENT && (w < 0 || w > (1 << 20))) return fail(KE_ERR_UNSUPPORTED, "numa weight out of range");
+  }
+  if (cfg.numa.strategy != KE_STRATEGY_LEAST_ALLOCATED && cfg.numa.strategy != KE_STRATEGY_MOST_ALLOCATED)
+    return fail(KE_ERR_INVALID, "numa scoring strategy");
+  const auto& a = cfg.loadaware;
+  if (a.agg_usage_type < 0 || a.agg_usage_type >= KE_AGG_TYPES || a.agg_score_type < 0 || a.agg_score_type >= KE_AGG_TYPES)
+    return fail(KE_ERR_INVALID, "aggregation type");
+  return KE_OK;
+}
+
+int validate_node(const ke_node& n) {
+  for (int r = 0; r < KE_NRES; r++) {
+    if (n.allocatable[r] < 0 || (n.raw_allocatable[r] < 0 && n.raw_allocatable[r] != KE_ABSENT))
+      return fail(KE_ERR_INVALID, "negative allocatable");
+  }
+  if (n.numa_topology_policy != 0 || n.cpu_bind_policy != 0)
+    return fail(KE_ERR_UNSUPPORTED, "node NUMA topology / CPU bind policies are not implemented in ABI v1");
+  if (n.custom_agg_type < 0 || n.custom_agg_type >= KE_AGG_TYPES) return fail(KE_ERR_INVALID, "aggregation type");
+  return KE_OK;
+}
+
+int validate_pod(const ke_pod& p) {
+  // AllowUseCPUSet (nodenumaresource/util.go:49-56) with the default FullPCPUs bind policy makes the
+  // pod a cpuset pod (plugin.go:276-301): that path (cpu accumulator, NUMA hints) is a later §8 row.
+  const bool cpuset = (p.qos_class == KE_QOS_LSE || p.qos_class == KE_QOS_LSR) &&
+                      p.priority_class == KE_PRIORITY_PROD && p.requests[KE_RES_CPU] > 0;
+  if (cpuset || p.has_resource_spec)
+    return fail(KE_ERR_UNSUPPORTED, "cpuset (LSE/LSR koord-prod) pods are not implemented in ABI v1");
+  if (p.priority_class < 0 || p.priority_class > KE_PRIORITY_FREE) return fail(KE_ERR_INVALID, "priority class");
+  return KE_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// arithmetic helpers (IEEE double, no contraction: built with -ffp-contract=off)
+// ---------------------------------------------------------------------------------------------
+int64_t usage_percent(int64_t used, int64_t total) {
+  double q = (double)used / (double)total;  // float64(used) / float64(total)
+  double p = q * 100.0;                     // * 100
+  return (int64_t)std::round(p);            // int64(math.Round(...)): half away from zero
+}
+
+int64_t max_used_within(int64_t total, int64_t thr) {
+  // usage_percent is monotone non-decreasing in `used` (each of int64->float64, /total, *100, round
+  // is), so {used : pct(used) <= thr} is a prefix of the domain; binary-search its last element.
+  int64_t lo = -USED_DOMAIN, hi = USED_DOMAIN;
+  if (usage_percent(hi, total) <= thr) return hi;
+  if (usage_percent(lo, total) > thr) return lo - 1;
+  while (hi - lo > 1) {  // pct(lo) <= thr < pct(hi)
+    int64_t mid = lo + (hi - lo) / 2;
+    if (usage_percent(mid, total) <= thr) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+static int64_t amplify(int64_t origin, double ratio) {  // node_resource_amplification.go:170-175
+  if (ratio <= 1.0) return origin;
+  return (int64_t)std::ceil((double)origin * ratio);
+}
+
+// ---------------------------------------------------------------------------------------------
+// estimator
+// ---------------------------------------------------------------------------------------------
+static int translated_resource(int32_t priority, int r) {  // apis/extension/resource.go:53-58
+  if (priority == KE_PRIORITY_PROD || priority == KE_PRIORITY_NONE) return r;
+  if (priority == KE_PRIORITY_BATCH) return r == KE_RES_CPU ? KE_RES_BATCH_CPU : KE_RES_BATCH_MEMORY;
+  if (priority == KE_PRIORITY_MID) return r == KE_RES_CPU ? KE_RES_MID_CPU : KE_RES_MID_MEMORY;
+  return -1;  // koord-free: no translation entry -> empty resource name
+}
+
+static int64_t estimate_resource(const ke_pod& pod, int name, int64_t factor) {  // default_estimator.go:88-122
+  const int64_t lim = name >= 0 ? pod.limits[name] : 0;
+  const int64_t req = name >= 0 ? pod.requests[name] : 0;
+  const int64_t q = lim > req ? lim : req;
+  if (q == 0) {
+    if (name == KE_RES_CPU || name == KE_RES_BATCH_CPU) return DEFAULT_MILLI_CPU;
+    if (name == KE_RES_MEMORY || name == KE_RES_BATCH_MEMORY) return DEFAULT_MEMORY;
+    return 0;
+  }
+  const double prod = (double)q * (double)factor;
+  int64_t est = (int64_t)std::round(prod / 100.0);
+  if (lim > 0 && est > lim) est = lim;
+  return est;
+}
+
+void estimate_pod(const ke_loadaware_args& a, const ke_pod& pod, int64_t* est, uint8_t* present) {
+  const bool custom = a.allow_customize_estimation && pod.has_custom_scaling_factors;
+  for (int r = 0; r < KE_NRES; r++) {
+    int64_t f = custom ? pod.custom_scaling_factors[r] : KE_ABSENT;
+    if (f == KE_ABSENT) f = a.estimated_scaling_factors[r];
+    if (f == KE_ABSENT) f = 0;
+    present[r] = a.resource_weights[r] != KE_ABSENT;
+    est[r] = present[r] ? estimate_resource(pod, translated_resource(pod.priority_class, r), f) : 0;
+  }
+}
+
+DevPod make_dev_pod(const ke_config& cfg, const ke_pod& pod) {
+  DevPod d{};
+  uint8_t present[KE_NRES];
+  estimate_pod(cfg.loadaware, pod, d.est, present);
+  d.req[0] = pod.requests[KE_RES_CPU];
+  d.req[1] = pod.requests[KE_RES_MEMORY];
+  bool zero = !pod.has_other_requests;  // quotav1.IsZero(PodRequests)
+  for (int r = 0; r < KE_RES_COUNT; r++) zero = zero && pod.requests[r] == 0;
+  uint32_t f = 0;
+  if (pod.is_daemonset) f |= PF_DAEMONSET;
+  if (pod.priority_class == KE_PRIORITY_PROD) f |= PF_PROD;
+  if (zero) f |= PF_NUMA_SKIP;
+  if (pod.priority_class == KE_PRIORITY_PROD && cfg.loadaware.score_according_prod_usage) f |= PF_LA_SCORE_PROD;
+  d.flags = f;
+  return d;
+}
+
+// ---------------------------------------------------------------------------------------------
+// NodeMetric views (helper.go)
+// ---------------------------------------------------------------------------------------------
+static const ke_resource_map* target_aggregated(const NodeState& ns, int64_t dur, int32_t type) {  // helper.go:57-95
+  if (!ns.nm.has_node_metric || ns.agg.empty()) return nullptr;
+  if (dur == 0) {
+    int best = -1;
+    int64_t best_dur = 0;
+    for (size_t i = 0; i < ns.agg.size(); i++) {
+      if (ns.agg[i].usage[type].n_keys > 0 && ns.agg[i].duration_ns > best_dur) {
+        best_dur = ns.agg[i].duration_ns;
+        best = (int)i;
+      }
+    }
+    if (best >= 0) return &ns.agg[best].usage[type];
+    return ns.nm.node_usage.n_keys > 0 ? &ns.nm.node_usage : nullptr;
+  }
+  for (const auto& a : ns.agg)
+    if (a.duration_ns == dur && a.usage[type].n_keys > 0) return &a.usage[type];
+  return nullptr;
+}
+
+static bool any_present(const int64_t* v) { return v[0] != KE_ABSENT || v[1] != KE_ABSENT; }
+
+struct Profile {  // generateUsageThresholdsFilterProfile (helper.go:107-145)
+  int64_t usage[KE_NRES], prod[KE_NRES], agg_thr[KE_NRES];
+  bool has_agg = false;
+  int32_t agg_type = 0;
+  int64_t agg_dur = 0;
+};
+
+static Profile filter_profile(const ke_loadaware_args& a, const ke_node& n) {
+  Profile p;
+  const bool args_agg = a.has_aggregated && any_present(a.agg_usage_thresholds) && a.agg_usage_type != KE_AGG_NONE;
+  auto use_args_agg = [&]() {
+    p.has_agg = true;
+    std::memcpy(p.agg_thr, a.agg_usage_thresholds, sizeof p.agg_thr);
+    p.agg_type = a.agg_usage_type;
+    p.agg_dur = a.agg_usage_duration_ns;
+  };
+  if (n.custom_thresholds_error) {
+    std::memcpy(p.usage, a.usage_thresholds, sizeof p.usage);
+    std::memcpy(p.prod, a.prod_usage_thresholds, sizeof p.prod);
+    if (args_agg) use_args_agg();
+    return p;
+  }
+  const bool c = n.has_custom_thresholds;
+  if (c && any_present(n.custom_usage_thresholds)) std::memcpy(p.usage, n.custom_usage_thresholds, sizeof p.usage);
+  else std::memcpy(p.usage, a.usage_thresholds, sizeof p.usage);
+  if (c && any_present(n.custom_prod_usage_thresholds)) std::memcpy(p.prod, n.custom_prod_usage_thresholds, sizeof p.prod);
+  else std::memcpy(p.prod, a.prod_usage_thresholds, sizeof p.prod);
+  if (c && n.has_custom_agg && any_present(n.custom_agg_thresholds) && n.custom_agg_type != KE_AGG_NONE) {
+    p.has_agg = true;
+    std::memcpy(p.agg_thr, n.custom_agg_thresholds, sizeof p.agg_thr);
+    p.agg_type = n.custom_agg_type;
+    p.agg_dur = n.custom_agg_duration_ns;
+  } else if (args_agg) {
+    use_args_agg();
+  }
+  return p;
+}
+
+// ---------------------------------------------------------------------------------------------
+// per-variant node terms (GetEstimatedUsed without the pod's own estimate)
+// ---------------------------------------------------------------------------------------------
+struct Terms {
+  int64_t assigned[KE_NRES] = {0, 0};     // Σ max(est, actual) of estimated assigned pods
+  int64_t est_actual[KE_NRES] = {0, 0};   // Σ actual usage of estimated pods (pod metric map)
+  int64_t other_actual[KE_NRES] = {0, 0}; // Σ actual usage of the other pods in the metric map
+};
+
+// Time from which shouldEstimatePodByConfig (load_aware.go:360-385) flips for this pod, or INT64_MAX.
+static int64_t estimate_window_end(const ke_loadaware_args& a, const AssignedPod& info, int64_t now) {
+  int64_t after_sched = -1, after_init = -1;
+  if (a.allow_customize_estimation) {
+    after_sched = info.pod.custom_seconds_after_scheduled;
+    after_init = info.pod.custom_seconds_after_initialized;
+  }
+  if (a.estimated_seconds_after_pod_scheduled != KE_ABSENT && after_sched < 0) after_sched = a.estimated_seconds_after_pod_scheduled;
+  if (a.estimated_seconds_after_initialized != KE_ABSENT && after_init < 0) after_init = a.estimated_seconds_after_initialized;
+  if (after_init > 0 && info.pod.has_initialized) {
+    int64_t t = info.pod.initialized_transition_ns + after_init * NS;
+    return t > now ? t : INT64_MAX;
+  }
+  if (after_sched > 0) {
+    int64_t t = info.ts + after_sched * NS;
+    return t > now ? t : INT64_MAX;
+  }
+  return INT64_MAX;
+}
+
+static bool should_estimate(const ke_loadaware_args& a, const AssignedPod& info, int64_t now) {
+  int64_t after_sched = -1, after_init = -1;
+  if (a.allow_customize_estimation) {
+    after_sched = info.pod.custom_seconds_after_scheduled;
+    after_init = info.pod.custom_seconds_after_initialized;
+  }
+  if (a.estimated_seconds_after_pod_scheduled != KE_ABSENT && after_sched < 0) after_sched = a.estimated_seconds_after_pod_scheduled;
+  if (a.estimated_seconds_after_initialized != KE_ABSENT && after_init < 0) after_init = a.estimated_seconds_after_initialized;
+  if (after_init > 0 && info.pod.has_initialized) return info.pod.initialized_transition_ns + after_init * NS > now;
+  return after_sched > 0 && info.ts + after_sched * NS > now;
+}
+
+static Terms compute_terms(const ke_loadaware_args& a, const NodeState& ns, bool prod, int64_t now, int64_t* valid_until) {
+  Terms t;
+  // buildPodMetricMap(nodeMetric, prod): name -> last PodMetricInfo (helper.go:154-170)
+  std::unordered_map<int64_t, const ke_pod_metric*> metrics;
+  metrics.reserve(ns.pm.size() * 2 + 1);
+  for (const auto& m : ns.pm) {
+    if (prod && m.priority_class != KE_PRIORITY_PROD) continue;
+    metrics[m.pod_key] = &m;
+  }
+  const bool has_ut = ns.nm.has_update_time;
+  const int64_t ut = ns.nm.update_time_ns;
+  const int64_t interval = ns.nm.report_interval_seconds != KE_ABSENT ? ns.nm.report_interval_seconds * NS : DEFAULT_REPORT_INTERVAL_NS;
+  const bool score_agg = a.has_aggregated && a.agg_score_type != KE_AGG_NONE;
+  const bool score_agg_missing = score_agg && target_aggregated(ns, a.agg_score_duration_ns, a.agg_score_type) == nullptr;
+  std::unordered_map<int64_t, bool> estimated;  // estimatedPods set
+  for (const auto& info : ns.asg) {  // estimatedAssignedPodUsed (load_aware.go:315-358)
+    if (prod && info.pod.priority_class != KE_PRIORITY_PROD) continue;
+    auto it = metrics.find(info.pod.pod_key);
+    const ke_pod_metric* m = it == metrics.end() ? nullptr : it->second;
+    const bool static_cond = (m == nullptr || m->usage.n_keys == 0) || (has_ut ? info.ts > ut : true) ||
+                             (has_ut && info.ts < ut && ut - info.ts < interval) || score_agg_missing;
+    if (!static_cond) {
+      int64_t w = estimate_window_end(a, info, now);
+      if (w < *valid_until) *valid_until = w;
+    }
+    if (static_cond || should_estimate(a, info, now)) {
+      if (!info.has_est) continue;
+      for (int r = 0; r < KE_NRES; r++) {
+        if (!info.est_present[r]) continue;
+        int64_t v = info.est[r];
+        if (m && m->usage.present[r] && m->usage.value[r] > v) v = m->usage.value[r];
+        t.assigned[r] += v;
+      }
+      estimated[info.pod.pod_key] = true;
+    }
+  }
+  for (const auto& kv : metrics) {  // sumPodUsages (helper.go:172-186)
+    const bool is_est = estimated.count(kv.first) != 0;
+    for (int r = 0; r < KE_NRES; r++) {
+      if (!kv.second->usage.present[r]) continue;
+      (is_est ? t.est_actual : t.other_actual)[r] += kv.second->usage.value[r];
+    }
+  }
+  return t;
+}
+
+// non-prod usage contribution: nodeUsage minus the estimated pods' actual usage when covered
+// (load_aware.go:271-283)
+static void add_usage(const ke_resource_map* usage, const Terms& t, int64_t* term) {
+  if (!usage) return;
+  for (int r = 0; r < KE_NRES; r++) {
+    if (!usage->present[r]) continue;
+    int64_t q = usage->value[r];
+    if (t.est_actual[r] != 0 && q >= t.est_actual[r]) q -= t.est_actual[r];
+    term[r] += q;
+  }
+}
+
+void derive_row(const ke_config& cfg, const NodeState& ns, int64_t now, Row* row, int64_t* valid_until) {
+  std::memset(row, 0, sizeof(Row));
+  *valid_until = INT64_MAX;
+  if (!ns.valid) return;
+  const ke_loadaware_args& a = cfg.loadaware;
+  const ke_node& n = ns.node;
+  uint32_t flags = NF_VALID;
+
+  // ---- LoadAwareScheduling
+  int64_t cap[KE_NRES];  // EstimateNode (default_estimator.go:124-143)
+  for (int r = 0; r < KE_NRES; r++) cap[r] = n.raw_allocatable[r] != KE_ABSENT ? n.raw_allocatable[r] : n.allocatable[r];
+  for (int r = 0; r < KE_NRES; r++) row->f[F_CAP + r] = cap[r];
+  if (ns.has_metric) {
+    flags |= NF_HAS_METRIC;
+    if (ns.nm.has_update_time) flags |= NF_HAS_UT;
+    row->f[F_UT] = ns.nm.update_time_ns;
+    if (!ns.nm.has_node_metric) flags |= NF_NM_NIL;
+  }
+  if (ns.has_metric && ns.nm.has_node_metric) {
+    const Profile prof = filter_profile(a, n);
+    if (any_present(prof.prod)) flags |= NF_HAS_PROD_THR;
+    if (prof.has_agg) flags |= NF_FILTER_AGG;
+    const Terms tnp = compute_terms(a, ns, false, now, valid_until);
+    const Terms tp = compute_terms(a, ns, true, now, valid_until);
+    // filter terms
+    int64_t term_f[2][KE_NRES], term_s[2][KE_NRES];
+    for (int r = 0; r < KE_NRES; r++) {
+      term_f[0][r] = term_s[0][r] = tnp.assigned[r];
+      term_f[1][r] = term_s[1][r] = tp.assigned[r] + tp.other_actual[r];
+    }
+    add_usage(prof.has_agg ? target_aggregated(ns, prof.agg_dur, prof.agg_type) : &ns.nm.node_usage, tnp, term_f[0]);
+    const bool score_agg = a.has_aggregated && a.agg_score_type != KE_AGG_NONE;
+    add_usage(score_agg ? target_aggregated(ns, a.agg_score_duration_ns, a.agg_score_type) : &ns.nm.node_usage, tnp, term_s[0]);
+    const int64_t* thr[2] = {prof.has_agg ? prof.agg_thr : prof.usage, prof.prod};
+    for (int v = 0; v < 2; v++) {
+      for (int r = 0; r < KE_NRES; r++) {
+        const int64_t th = thr[v][r];
+        const bool on = th != KE_ABSENT && th != 0 && cap[r] != 0;
+        if (on) {
+          flags |= nf_fh_on(v, r);
+          row->f[F_FH + 2 * v + r] = max_used_within(cap[r], th) - term_f[v][r];
+        }
+        row->f[F_SA + 2 * v + r] = cap[r] - term_s[v][r];
+      }
+    }
+  }
+
+  // ---- NodeNUMAResource (policy None, non-cpuset pods)
+  for (int r = 0; r < KE_NRES; r++) {
+    row->f[F_NALLOC + r] = n.allocatable[r];
+    row->f[F_NREQ + r] = n.requested[r];
+  }
+  const int64_t cs_milli = n.cpuset_allocated_cpus * 1000;
+  row->f[F_CSM] = cs_milli;
+  if (n.amplification_error) flags |= NF_NUMA_AMP_ERR;
+  if (n.cpu_topology_invalid) flags |= NF_NUMA_TOPO_INVALID;
+  const double ratio_f = n.cpu_amplification_ratio;  // filterAmplifiedCPUs reads the annotation (plugin.go:420-427)
+  if (ratio_f > 1.0) flags |= NF_NUMA_RATIO_F;
+  row->f[F_CSAF] = amplify(cs_milli, ratio_f);
+  double ratio_s;  // Score: TopologyOptions ratios, else the annotation (util.go:78-87)
+  if (n.nrt_cpu_amplification_ratio > -1.5) {
+    ratio_s = n.nrt_cpu_amplification_ratio < 0 ? 0.0 : n.nrt_cpu_amplification_ratio;
+  } else {
+    if (n.amplification_error) flags |= NF_NUMA_SCORE_ZERO;
+    ratio_s = n.cpu_amplification_ratio < 0 ? 0.0 : n.cpu_amplification_ratio;
+  }
+  if (ratio_s > 1.0) flags |= NF_NUMA_RATIO_S;
+  row->f[F_CSAS] = amplify(cs_milli, ratio_s);
+  row->flags = flags;
+}
+
+void host_assign(const ke_config& cfg, NodeState& ns, const ke_pod& pod, int64_t timestamp_ns) {
+  if (pod.is_terminated) return;  // pod_assign_cache.go:90
+  AssignedPod info{};
+  info.pod = pod;
+  estimate_pod(cfg.loadaware, pod, info.est, info.est_present);
+  info.has_est = info.est_present[0] || info.est_present[1];
+  for (auto& e : ns.asg) {
+    if (e.pod.uid == pod.uid) {  // existing entry: refresh pod + estimate, keep timestamp
+      info.ts = e.ts;
+      e = info;
+      ns.dirty = true;
+      return;
+    }
+  }
+  info.ts = pod.has_scheduled ? pod.scheduled_transition_ns : timestamp_ns;
+  ns.asg.push_back(info);
+  ns.dirty = true;
+}
+
+}  // namespace ke

@@ -1,0 +1,74 @@
+// ke_host.h — host side of the evaluator: the informer-fed object state (what the reference keeps in
+// its listers, podAssignCache and NodeInfo snapshot) and its folding into GPU rows.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/koord_eval.h"
+#include "ke_types.h"
+
+namespace ke {
+
+// One podAssignCache entry (pkg/scheduler/plugins/loadaware/pod_assign_cache.go:45-49).
+struct AssignedPod {
+  ke_pod pod;
+  int64_t ts;
+  int64_t est[KE_NRES];
+  uint8_t est_present[KE_NRES];
+  bool has_est;
+};
+
+struct NodeState {
+  bool valid = false;
+  ke_node node{};
+  bool has_metric = false;
+  ke_node_metric nm{};
+  std::vector<ke_pod_metric> pm;
+  std::vector<ke_aggregated_usage> agg;
+  std::vector<AssignedPod> asg;
+  // derived
+  bool dirty = true;            // row must be re-derived and uploaded
+  int64_t valid_until = INT64_MAX;  // derived row is exact for now < valid_until
+  // LoadAware U*(total, thr) per [variant][res] (INT64_MAX = no constraint); cached by derive_row
+};
+
+struct DeviceState;  // ke_kernels.hip
+
+struct Context {
+  ke_config cfg{};
+  KArgs kargs_template{};
+  std::vector<NodeState> nodes;  // size = node_capacity
+  int32_t n_nodes = 0;           // 1 + highest populated index
+  DeviceState* dev = nullptr;
+  // last ke_schedule timing
+  double last_total_ms = 0.0;
+  std::vector<double> last_batch_ms;
+};
+
+// error plumbing (thread-local, read by ke_last_error)
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+
+// validation of objects against the implemented hot path
+int validate_config(const ke_config& cfg);
+int validate_node(const ke_node& n);
+int validate_pod(const ke_pod& p);
+
+// DefaultEstimator.EstimatePod (estimator/default_estimator.go:59-122)
+void estimate_pod(const ke_loadaware_args& a, const ke_pod& pod, int64_t* est, uint8_t* present);
+// pod -> device parameters
+DevPod make_dev_pod(const ke_config& cfg, const ke_pod& pod);
+
+// Fold a node's object state into its row for evaluation at `now` (valid until *valid_until).
+void derive_row(const ke_config& cfg, const NodeState& ns, int64_t now, Row* row, int64_t* valid_until);
+
+// U*(total, thr): the largest used with int64(math.Round(float64(used)/float64(total)*100)) <= thr,
+// searched over |used| <= 2^53 (load_aware.go:299).  total > 0.
+int64_t max_used_within(int64_t total, int64_t thr);
+int64_t usage_percent(int64_t used, int64_t total);
+
+// host mirror of Reserve (podAssignCache.assign + NodeInfo.Requested += requests)
+void host_assign(const ke_config& cfg, NodeState& ns, const ke_pod& pod, int64_t timestamp_ns);
+
+}  // namespace ke

@@ -1,0 +1,114 @@
+// ke_types.h — layout of the GPU-resident node state (struct of arrays) and of the per-pod
+// parameters, shared by the host-side derivation (ke_host.cpp) and the HIP kernels (ke_kernels.hip).
+//
+// One node row holds everything the fused LoadAware + NodeNUMAResource Filter/Score needs, already
+// folded on the host so that the per-(pod,node) work is pure int64 arithmetic:
+//   * LoadAware usage thresholds: int64(math.Round(float64(used)/float64(total)*100)) <= thr
+//     (load_aware.go:299) is monotone in `used`, so it is folded into the exact integer bound
+//     U*(total,thr) = max{used : round(used/total*100) <= thr}; the kernel tests
+//     pod_est <= fh = U* - node_term.  No float64 reaches the device for the filter.
+//   * node_term = GetEstimatedUsed minus the pod's own estimate (load_aware.go:251-288), per variant
+//     (non-prod / prod) — the assign cache and the NodeMetric enter only through it.
+//   * LoadAware score: leastUsedScore(est + term, cap) = (sa - est)*100/cap with sa = cap - term.
+//   * NodeNUMAResource: NodeInfo.Requested/Allocatable + the cpuset amplification pieces.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define KE_HD __host__ __device__
+#else
+#define KE_HD
+#endif
+
+namespace ke {
+
+// int64 SoA fields of a node row (index into the field table)
+enum RowField : int {
+  F_UT = 0,       // NodeMetric.Status.UpdateTime (ns)
+  F_FH = 1,       // 4 fields: filter headroom [variant][res]  (variant 0 = non-prod, 1 = prod)
+  F_SA = 5,       // 4 fields: score  sa = cap - term_score [variant][res]
+  F_CAP = 9,      // 2 fields: EstimateNode allocatable (cpu milli, memory)
+  F_NALLOC = 11,  // 2 fields: NodeInfo.Allocatable (cpu milli, memory)
+  F_NREQ = 13,    // 2 fields: NodeInfo.Requested
+  F_CSM = 15,     // allocated cpuset CPUs * 1000
+  F_CSAF = 16,    // Amplify(cpuset milli, filter ratio)
+  F_CSAS = 17,    // Amplify(cpuset milli, score ratio)
+  NUM_I64_FIELDS = 18
+};
+
+// node flags (u32 SoA field)
+enum NodeFlag : uint32_t {
+  NF_VALID = 1u << 0,          // slot holds a node
+  NF_HAS_METRIC = 1u << 1,     // nodeMetricLister.Get succeeded
+  NF_HAS_UT = 1u << 2,         // Status.UpdateTime != nil
+  NF_NM_NIL = 1u << 3,         // Status.NodeMetric == nil
+  NF_HAS_PROD_THR = 1u << 4,   // len(filterProfile.ProdUsageThresholds) > 0
+  NF_FILTER_AGG = 1u << 5,     // filterProfile.AggregatedUsage != nil (reason string)
+  NF_FH_ON0 = 1u << 6,         // 4 bits: threshold active for [variant][res] -> bit 6 + 2*v + r
+  NF_NUMA_AMP_ERR = 1u << 10,  // ratio annotation unparsable -> Filter UnschedulableAndUnresolvable
+  NF_NUMA_RATIO_F = 1u << 11,  // filter ratio > 1
+  NF_NUMA_TOPO_INVALID = 1u << 12,
+  NF_NUMA_RATIO_S = 1u << 13,  // score ratio > 1
+  NF_NUMA_SCORE_ZERO = 1u << 14,  // getResourceOptions error -> Score 0
+};
+KE_HD constexpr uint32_t nf_fh_on(int v, int r) { return NF_FH_ON0 << (2 * v + r); }
+
+// pod flags
+enum PodFlag : uint32_t {
+  PF_DAEMONSET = 1u << 0,
+  PF_PROD = 1u << 1,           // GetPodPriorityClassWithDefault == koord-prod
+  PF_NUMA_SKIP = 1u << 2,      // PodRequests all zero -> NodeNUMAResource skip
+  PF_LA_SCORE_PROD = 1u << 3,  // prod && ScoreAccordingProdUsage
+};
+
+// host-side packed row (staging for uploads, debug readback)
+struct Row {
+  int64_t f[NUM_I64_FIELDS];
+  uint32_t flags;
+  uint32_t pad;
+};
+static_assert(sizeof(Row) == 152, "Row layout");
+// Bytes of one node row the eval kernel reads per pass (18 int64 fields + u32 flags).
+constexpr int ROW_BYTES = NUM_I64_FIELDS * 8 + 4;
+
+struct DevPod {
+  int64_t est[2];  // LoadAware EstimatePod (cpu milli, memory); 0 for a resource without weight
+  int64_t req[2];  // PodRequests cpu milli, memory (NodeNUMAResource, NodeInfo.Requested patch)
+  uint32_t flags;
+  int32_t pad;
+};
+static_assert(sizeof(DevPod) == 40, "DevPod layout");
+
+// kernel-uniform arguments
+enum ArgFlag : uint32_t {
+  AF_FILTER_EXPIRED = 1u << 0,      // args.FilterExpiredNodeMetrics
+  AF_ENABLE_WHEN_EXPIRED = 1u << 1, // args.EnableScheduleWhenNodeMetricsExpired
+  AF_EXP_PRESENT = 1u << 2,         // args.NodeMetricExpirationSeconds != nil
+  AF_NUMA_MOST = 1u << 3,           // NodeNUMAResource MostAllocated
+};
+struct KArgs {
+  int64_t now;
+  int64_t exp_s;       // NodeMetricExpirationSeconds
+  int32_t w_la[2];     // LoadAware resourceWeights (0 = absent)
+  int32_t w_numa[2];   // NodeNUMAResource ScoringStrategy weights (0 = absent)
+  int32_t wsum_la, wsum_numa;
+  int32_t wp_la, wp_numa;  // plugin weights in the profile
+  uint32_t flags;
+  int32_t pad;
+};
+
+// Packed candidate key: higher is better.  (score+1) in the top 9 bits, inverted node index in the
+// low 23 bits, so max(key) == selectHost with ties resolved to the lowest node index.
+constexpr uint32_t KEY_IDX_BITS = 23;
+constexpr uint32_t KEY_IDX_MASK = (1u << KEY_IDX_BITS) - 1;
+constexpr int MAX_SHARD_NODES = (1 << KEY_IDX_BITS) - 1;
+constexpr int MAX_TOTAL_SCORE = 510;  // (score+1) must fit in 9 bits
+KE_HD inline uint32_t make_key(int32_t total, int32_t idx) {
+  return total < 0 ? 0u : ((uint32_t)(total + 1) << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)idx);
+}
+KE_HD inline int32_t key_node(uint32_t key) { return (int32_t)(KEY_IDX_MASK - (key & KEY_IDX_MASK)); }
+KE_HD inline int32_t key_score(uint32_t key) { return (int32_t)(key >> KEY_IDX_BITS) - 1; }
+
+constexpr int MAX_BATCH = 64;  // pods per speculative batch (== max candidates per pod)
+
+}  // namespace ke

@@ -1,0 +1,152 @@
+"""Python handle over the C ABI (libkoordeval.so): the same calls a Go koord-scheduler makes via cgo.
+
+`Evaluator` owns one ke_ctx (one GPU, one node shard).  State ingestion mirrors the informer events
+the reference plugins consume; `eval` is the parity-mode Filter/Score matrix and `schedule` the
+queue scheduler (findNodesThatFitPod + score + selectHost + Reserve per pod, exact speculative
+batching on the device).  There is no CPU fallback: evaluation without the HIP device raises.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+
+
+class KoordEvalError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"koord-eval error {code}: {msg}")
+        self.code = code
+
+
+def as_pod_array(pods):
+    """list[abi.Pod] | np.ndarray(POD_DTYPE) -> contiguous np.ndarray(POD_DTYPE)."""
+    if isinstance(pods, np.ndarray):
+        assert pods.dtype == abi.POD_DTYPE
+        return np.ascontiguousarray(pods)
+    arr = np.zeros(len(pods), dtype=abi.POD_DTYPE)
+    if len(pods):
+        buf = (abi.Pod * len(pods))(*pods)
+        arr[:] = np.frombuffer(buf, dtype=abi.POD_DTYPE, count=len(pods))
+    return arr
+
+
+class Evaluator:
+    def __init__(self, cfg, lib=None):
+        self.lib = lib or abi.load_library()
+        self.cfg = cfg
+        h = C.c_void_p()
+        self._check(self.lib.ke_create(C.byref(cfg), C.byref(h)))
+        self.h = h
+
+    # ---- plumbing --------------------------------------------------------------------------
+    def _check(self, rc):
+        if rc != abi.OK:
+            raise KoordEvalError(rc, self.lib.ke_last_error().decode())
+        return rc
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.ke_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def device(self):
+        return bool(self.lib.ke_device_available())
+
+    @property
+    def num_nodes(self):
+        return self.lib.ke_num_nodes(self.h)
+
+    # ---- state ingestion --------------------------------------------------------------------
+    def upsert_node(self, i, node):
+        self._check(self.lib.ke_node_upsert(self.h, i, C.byref(node)))
+
+    def nodes_load(self, nodes):
+        nodes = np.ascontiguousarray(nodes, dtype=abi.NODE_DTYPE)
+        self._check(self.lib.ke_nodes_load(self.h, len(nodes), abi.ptr(nodes)))
+
+    def set_requested(self, i, milli_cpu, memory):
+        self._check(self.lib.ke_node_set_requested(self.h, i, milli_cpu, memory))
+
+    def set_cpuset_allocated(self, i, cpus):
+        self._check(self.lib.ke_node_set_cpuset_allocated(self.h, i, cpus))
+
+    def set_nodemetric(self, i, nm):
+        """nm = model.make_node_metric(...) tuple."""
+        hdr, pms, n_pm, aggs, n_agg = nm
+        self._check(self.lib.ke_nodemetric_upsert(self.h, i, C.byref(hdr), n_pm, C.cast(pms, C.c_void_p), n_agg,
+                                                   C.cast(aggs, C.c_void_p)))
+
+    def nodemetrics_load(self, headers, pm_offsets, pod_metrics, agg_offsets, aggregated):
+        headers = np.ascontiguousarray(headers, dtype=abi.NODE_METRIC_DTYPE)
+        pm_offsets = np.ascontiguousarray(pm_offsets, dtype=np.int64)
+        agg_offsets = np.ascontiguousarray(agg_offsets, dtype=np.int64)
+        pod_metrics = np.ascontiguousarray(pod_metrics, dtype=abi.POD_METRIC_DTYPE)
+        aggregated = np.ascontiguousarray(aggregated, dtype=abi.AGG_DTYPE)
+        self._check(self.lib.ke_nodemetrics_load(self.h, len(headers), abi.ptr(headers), abi.ptr(pm_offsets),
+                                                 abi.ptr(pod_metrics), abi.ptr(agg_offsets), abi.ptr(aggregated)))
+
+    def delete_nodemetric(self, i):
+        self._check(self.lib.ke_nodemetric_delete(self.h, i))
+
+    def assign(self, i, pod, timestamp_ns):
+        self._check(self.lib.ke_pod_assign(self.h, i, C.byref(pod), int(timestamp_ns)))
+
+    def unassign(self, i, uid):
+        self._check(self.lib.ke_pod_unassign(self.h, i, uid))
+
+    def estimate_pod(self, pod):
+        est = np.zeros(2, np.int64)
+        self._check(self.lib.ke_estimate_pod(self.h, C.byref(pod), abi.ptr(est)))
+        return est
+
+    # ---- evaluation -------------------------------------------------------------------------
+    def eval(self, pods, now_ns):
+        pods = as_pod_array(pods)
+        P, N = len(pods), self.num_nodes
+        out = {
+            "status": np.zeros((P, N), np.uint8),
+            "reason": np.zeros((P, N), np.uint8),
+            "la": np.zeros((P, N), np.int16),
+            "numa": np.zeros((P, N), np.int16),
+            "total": np.zeros((P, N), np.int16),
+            "best": np.zeros(P, np.int32),
+        }
+        self._check(self.lib.ke_eval(self.h, P, abi.ptr(pods), int(now_ns), abi.ptr(out["status"]),
+                                     abi.ptr(out["reason"]), abi.ptr(out["la"]), abi.ptr(out["numa"]),
+                                     abi.ptr(out["total"]), abi.ptr(out["best"])))
+        return out
+
+    def schedule(self, pods, now_ns):
+        pods = as_pod_array(pods)
+        chosen = np.zeros(len(pods), np.int32)
+        score = np.zeros(len(pods), np.int32)
+        self._check(self.lib.ke_schedule(self.h, len(pods), abi.ptr(pods), int(now_ns), abi.ptr(chosen), abi.ptr(score)))
+        return chosen, score
+
+    def stats(self):
+        total = C.c_double()
+        nb = abi.i32()
+        self._check(self.lib.ke_last_schedule_stats(self.h, C.byref(total), C.byref(nb), None, 0))
+        per = np.zeros(max(nb.value, 1), np.float64)
+        self._check(self.lib.ke_last_schedule_stats(self.h, None, None, abi.ptr(per), len(per)))
+        return total.value, per[: nb.value]
+
+    def debug_rows(self, now_ns, device=True):
+        n = self.num_nodes
+        host = np.zeros(n, abi.ROW_DTYPE)
+        dev = np.zeros(n, abi.ROW_DTYPE) if device else None
+        self._check(self.lib.ke_debug_rows(self.h, n, int(now_ns), abi.ptr(dev), abi.ptr(host)))
+        return dev, host

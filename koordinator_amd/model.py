@@ -1,0 +1,308 @@
+"""Kubernetes-object helpers: build the boundary structs (abi.py) from pod/node/NodeMetric descriptions.
+
+This is what a Go caller gets from client-go and the reference's `apis/extension` helpers before it
+crosses the C ABI: quantity parsing (k8s.io/apimachinery resource.Quantity, rounding up), pod request
+aggregation (resourceapi.PodRequests/PodLimits), kube QoS and koordinator priority/QoS resolution
+(apis/extension/priority_utils.go:37-58, qos_utils.go:32-68).  Tests and the bench use it to state
+their inputs the way the reference's own tests do.
+"""
+import math
+from fractions import Fraction
+
+from . import abi
+
+NS = 1_000_000_000
+
+_SUFFIX = {
+    "n": Fraction(1, 10**9), "u": Fraction(1, 10**6), "m": Fraction(1, 1000), "": Fraction(1),
+    "k": Fraction(10**3), "M": Fraction(10**6), "G": Fraction(10**9), "T": Fraction(10**12),
+    "P": Fraction(10**15), "E": Fraction(10**18),
+    "Ki": Fraction(2**10), "Mi": Fraction(2**20), "Gi": Fraction(2**30), "Ti": Fraction(2**40),
+    "Pi": Fraction(2**50), "Ei": Fraction(2**60),
+}
+
+RESOURCE_INDEX = {
+    "cpu": abi.RES_CPU,
+    "memory": abi.RES_MEMORY,
+    "kubernetes.io/batch-cpu": abi.RES_BATCH_CPU,
+    "kubernetes.io/batch-memory": abi.RES_BATCH_MEMORY,
+    "kubernetes.io/mid-cpu": abi.RES_MID_CPU,
+    "kubernetes.io/mid-memory": abi.RES_MID_MEMORY,
+}
+
+PRIORITY_BY_NAME = {"koord-prod": abi.PRIORITY_PROD, "koord-mid": abi.PRIORITY_MID,
+                    "koord-batch": abi.PRIORITY_BATCH, "koord-free": abi.PRIORITY_FREE}
+QOS_BY_NAME = {"LSE": abi.QOS_LSE, "LSR": abi.QOS_LSR, "LS": abi.QOS_LS, "BE": abi.QOS_BE,
+               "SYSTEM": abi.QOS_SYSTEM}
+AGG_BY_NAME = {"": abi.AGG_NONE, "avg": abi.AGG_AVG, "p50": abi.AGG_P50, "p90": abi.AGG_P90,
+               "p95": abi.AGG_P95, "p99": abi.AGG_P99}
+
+PRIORITY_PROD_VALUE_MAX = 9999
+PRIORITY_MID_VALUE_MAX = 7999
+PRIORITY_BATCH_VALUE_MIN = 5000
+
+
+def parse_quantity(q):
+    """resource.MustParse -> exact rational (decimal/binary SI suffixes, decimal exponents)."""
+    if isinstance(q, (int, Fraction)):
+        return Fraction(q)
+    s = str(q).strip()
+    for suf in ("Ki", "Mi", "Gi", "Ti", "Pi", "Ei"):
+        if s.endswith(suf):
+            return Fraction(s[:-2]) * _SUFFIX[suf]
+    if "e" in s[1:] or "E" in s[1:]:
+        mant, exp = s.replace("E", "e").split("e")
+        return Fraction(mant) * Fraction(10) ** int(exp)
+    if s and s[-1] in "numkMGTPE":
+        return Fraction(s[:-1]) * _SUFFIX[s[-1]]
+    return Fraction(s)
+
+
+def value(q):  # Quantity.Value(): rounds up
+    return math.ceil(parse_quantity(q))
+
+
+def milli_value(q):  # Quantity.MilliValue(): rounds up
+    return math.ceil(parse_quantity(q) * 1000)
+
+
+def resource_value(name, q):
+    """getResourceValue (loadaware/helper.go:147-152): cpu -> MilliValue, else Value."""
+    return milli_value(q) if name == "cpu" else value(q)
+
+
+_keys = {}
+
+
+def pod_key(namespace, name):
+    """Interned NamespacedName -> int64 key (what a Go shim would keep in a map)."""
+    k = f"{namespace}/{name}"
+    if k not in _keys:
+        _keys[k] = len(_keys) + 1
+    return _keys[k]
+
+
+def _sum_lists(lists):
+    out = {}
+    for rl in lists:
+        for k, v in (rl or {}).items():
+            out[k] = out.get(k, Fraction(0)) + parse_quantity(v)
+    return out
+
+
+def pod_requests(containers, init_containers=(), overhead=None):
+    """resourceapi.PodRequests (k8s v1.28): max(Σ containers, max init container) + overhead."""
+    reqs = _sum_lists([c.get("requests") for c in containers])
+    for ic in init_containers:
+        for k, v in (ic.get("requests") or {}).items():
+            reqs[k] = max(reqs.get(k, Fraction(0)), parse_quantity(v))
+    for k, v in (overhead or {}).items():
+        reqs[k] = reqs.get(k, Fraction(0)) + parse_quantity(v)
+    return reqs
+
+
+def pod_limits(containers, init_containers=(), overhead=None):
+    lims = _sum_lists([c.get("limits") for c in containers])
+    for ic in init_containers:
+        for k, v in (ic.get("limits") or {}).items():
+            lims[k] = max(lims.get(k, Fraction(0)), parse_quantity(v))
+    for k, v in (overhead or {}).items():
+        if k in lims:
+            lims[k] = lims[k] + parse_quantity(v)
+    return lims
+
+
+def kube_qos(containers, init_containers=()):
+    """k8s GetPodQOS (pkg/apis/core/v1/helper/qos, v1.28) over cpu/memory."""
+    requests, limits = {}, {}
+    guaranteed = True
+    for c in list(containers) + list(init_containers):
+        for k, v in (c.get("requests") or {}).items():
+            if k in ("cpu", "memory") and parse_quantity(v) != 0:
+                requests[k] = requests.get(k, 0) + parse_quantity(v)
+        found = set()
+        for k, v in (c.get("limits") or {}).items():
+            if k in ("cpu", "memory") and parse_quantity(v) != 0:
+                found.add(k)
+                limits[k] = limits.get(k, 0) + parse_quantity(v)
+        if not {"cpu", "memory"} <= found:
+            guaranteed = False
+    if not requests and not limits:
+        return "BestEffort"
+    if guaranteed:
+        for k, v in requests.items():
+            if limits.get(k) != v:
+                guaranteed = False
+                break
+    if guaranteed and len(requests) == len(limits):
+        return "Guaranteed"
+    return "Burstable"
+
+
+def priority_class_raw(labels, spec_priority):
+    """GetPodPriorityClassRaw (apis/extension/priority.go:73-101)."""
+    if "koordinator.sh/priority-class" in labels:
+        return PRIORITY_BY_NAME.get(labels["koordinator.sh/priority-class"], abi.PRIORITY_NONE)
+    if spec_priority is None:
+        return abi.PRIORITY_NONE
+    p = spec_priority
+    if 9000 <= p <= 9999:
+        return abi.PRIORITY_PROD
+    if 7000 <= p <= 7999:
+        return abi.PRIORITY_MID
+    if 5000 <= p <= 5999:
+        return abi.PRIORITY_BATCH
+    if 3000 <= p <= 3999:
+        return abi.PRIORITY_FREE
+    return abi.PRIORITY_NONE
+
+
+def qos_raw(labels):
+    return QOS_BY_NAME.get(labels.get("koordinator.sh/qosClass"), abi.QOS_NONE)
+
+
+def priority_class_with_default(labels, spec_priority, containers, init_containers=()):
+    """GetPodPriorityClassWithDefault (priority_utils.go:37-58)."""
+    p = priority_class_raw(labels, spec_priority)
+    if p != abi.PRIORITY_NONE:
+        return p
+    q = qos_raw(labels)
+    if q == abi.QOS_NONE:  # GetPodQoSClassWithKubeQoS
+        q = {"Guaranteed": abi.QOS_LSR, "Burstable": abi.QOS_LS, "BestEffort": abi.QOS_BE}[
+            kube_qos(containers, init_containers)]
+    if q in (abi.QOS_SYSTEM, abi.QOS_LSE, abi.QOS_LSR, abi.QOS_LS):
+        return abi.PRIORITY_PROD
+    if q == abi.QOS_BE:
+        return abi.PRIORITY_BATCH
+    return abi.PRIORITY_NONE
+
+
+def _fill_resources(arr, rl):
+    other = False
+    for i in range(abi.RES_COUNT):
+        arr[i] = 0
+    for k, v in rl.items():
+        if k in RESOURCE_INDEX:
+            arr[RESOURCE_INDEX[k]] = milli_value(v) if k == "cpu" else value(v)
+        elif v != 0:
+            other = True
+    return other
+
+
+_uid = [0]
+
+
+def make_pod(name="pod", namespace="default", requests=None, limits=None, containers=None,
+             init_containers=(), overhead=None, priority=None, labels=None, owner_kind=None, uid=None,
+             scheduled_at=None, initialized_at=None, custom_factors=None,
+             custom_seconds_after_scheduled=None, custom_seconds_after_initialized=None,
+             terminated=False):
+    """A pod as the plugins see it.  `requests`/`limits` describe one container (MakePod().Req());
+    `containers` gives the full list.  Times are ns."""
+    labels = dict(labels or {})
+    if containers is None:
+        containers = [] if requests is None and limits is None else [{"requests": requests or {}, "limits": limits or {}}]
+    p = abi.Pod()
+    p.pod_key = pod_key(namespace, name)
+    if uid is None:
+        _uid[0] += 1
+        uid = _uid[0]
+    p.uid = uid
+    reqs = pod_requests(containers, init_containers, overhead)
+    lims = pod_limits(containers, init_containers, overhead)
+    other = _fill_resources(p.requests, reqs)
+    _fill_resources(p.limits, lims)
+    p.has_other_requests = 1 if other else 0
+    p.custom_scaling_factors[:] = [abi.ABSENT, abi.ABSENT]
+    if custom_factors:
+        p.has_custom_scaling_factors = 1
+        for k, v in custom_factors.items():
+            if k in ("cpu", "memory"):
+                p.custom_scaling_factors[RESOURCE_INDEX[k]] = int(v)
+    p.custom_seconds_after_scheduled = abi.ABSENT if custom_seconds_after_scheduled is None else custom_seconds_after_scheduled
+    p.custom_seconds_after_initialized = abi.ABSENT if custom_seconds_after_initialized is None else custom_seconds_after_initialized
+    if scheduled_at is not None:
+        p.has_scheduled = 1
+        p.scheduled_transition_ns = int(scheduled_at)
+    if initialized_at is not None:
+        p.has_initialized = 1
+        p.initialized_transition_ns = int(initialized_at)
+    p.priority_class = priority_class_with_default(labels, priority, containers, init_containers)
+    p.qos_class = qos_raw(labels)
+    p.is_daemonset = 1 if owner_kind == "DaemonSet" else 0
+    p.is_terminated = 1 if terminated else 0
+    return p
+
+
+def _thr(arr, m):
+    arr[:] = [abi.ABSENT, abi.ABSENT]
+    for k, v in (m or {}).items():
+        arr[RESOURCE_INDEX[k]] = int(v)
+
+
+def make_node(allocatable=None, requested=None, raw_allocatable=None, amplification_ratio=None,
+              nrt_amplification_ratio=None, cpuset_allocated_cpus=0, custom_usage_thresholds=None,
+              custom_prod_usage_thresholds=None, custom_aggregated=None, custom_thresholds_error=False,
+              amplification_error=False, cpu_topology_invalid=False):
+    """A Node (+ NodeInfo.Requested).  custom_* model the usage-thresholds annotation
+    (apis/extension/load_aware.go:30-72); custom_aggregated = dict(thresholds=, type=, duration_ns=)."""
+    n = abi.Node()
+    allocatable = allocatable or {}
+    n.allocatable[:] = [milli_value(allocatable.get("cpu", 0)), value(allocatable.get("memory", 0))]
+    n.raw_allocatable[:] = [abi.ABSENT, abi.ABSENT]
+    for k, v in (raw_allocatable or {}).items():
+        n.raw_allocatable[RESOURCE_INDEX[k]] = resource_value(k, v)
+    requested = requested or {}
+    n.requested[:] = [milli_value(requested.get("cpu", 0)), value(requested.get("memory", 0))]
+    n.cpu_amplification_ratio = -1.0 if amplification_ratio is None else float(amplification_ratio)
+    n.nrt_cpu_amplification_ratio = -2.0 if nrt_amplification_ratio is None else float(nrt_amplification_ratio)
+    n.cpuset_allocated_cpus = cpuset_allocated_cpus
+    has_custom = custom_usage_thresholds is not None or custom_prod_usage_thresholds is not None or custom_aggregated is not None
+    n.has_custom_thresholds = 1 if has_custom else 0
+    _thr(n.custom_usage_thresholds, custom_usage_thresholds)
+    _thr(n.custom_prod_usage_thresholds, custom_prod_usage_thresholds)
+    _thr(n.custom_agg_thresholds, (custom_aggregated or {}).get("thresholds"))
+    if custom_aggregated is not None:
+        n.has_custom_agg = 1
+        n.custom_agg_type = AGG_BY_NAME[custom_aggregated.get("type", "")]
+        n.custom_agg_duration_ns = int(custom_aggregated.get("duration_ns", 0))
+    n.custom_thresholds_error = 1 if custom_thresholds_error else 0
+    n.amplification_error = 1 if amplification_error else 0
+    n.cpu_topology_invalid = 1 if cpu_topology_invalid else 0
+    return n
+
+
+def resource_map(rl):
+    m = abi.ResourceMap()
+    rl = rl or {}
+    for k, v in rl.items():
+        if k in ("cpu", "memory"):
+            i = RESOURCE_INDEX[k]
+            m.value[i] = resource_value(k, v)
+            m.present[i] = 1
+    m.n_keys = len(rl)
+    return m
+
+
+def make_node_metric(update_time=None, report_interval_seconds=None, node_usage=None, has_node_metric=True,
+                     pods=(), aggregated=()):
+    """NodeMetric (slo/v1alpha1).  pods: [dict(namespace, name, priority('koord-prod'...), usage)];
+    aggregated: [dict(duration_ns, usage={'p95': {...}})].  Returns (header, pod_metrics, aggregated)."""
+    nm = abi.NodeMetric()
+    if update_time is not None:
+        nm.has_update_time = 1
+        nm.update_time_ns = int(update_time)
+    nm.report_interval_seconds = abi.ABSENT if report_interval_seconds is None else report_interval_seconds
+    nm.has_node_metric = 1 if has_node_metric else 0
+    nm.node_usage = resource_map(node_usage)
+    pms = (abi.PodMetric * max(len(pods), 1))()
+    for i, pm in enumerate(pods):
+        pms[i].pod_key = pod_key(pm.get("namespace", "default"), pm["name"])
+        pms[i].priority_class = PRIORITY_BY_NAME.get(pm.get("priority", ""), abi.PRIORITY_NONE)
+        pms[i].usage = resource_map(pm.get("usage"))
+    aggs = (abi.AggregatedUsage * max(len(aggregated), 1))()
+    for i, ag in enumerate(aggregated):
+        aggs[i].duration_ns = int(ag["duration_ns"])
+        for t, rl in ag.get("usage", {}).items():
+            aggs[i].usage[AGG_BY_NAME[t]] = resource_map(rl)
+    return nm, pms, len(pods), aggs, len(aggregated)

@@ -1,0 +1,174 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes handle over oracle/liboracle.so, the CPU restatement of the
+reference plugins (oracle.c).  Importable only by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg; same method names as koordinator_amd.evaluator.Evaluator so parity tests can drive
+both with identical calls.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from koordinator_amd import abi
+from koordinator_amd.evaluator import as_pod_array
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-C", HERE, "-s"], check=True)
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB):
+        build()
+    lib = C.CDLL(LIB)
+    V, i32, i64 = C.c_void_p, C.c_int32, C.c_int64
+    sig = {
+        "or_create": (V, [C.POINTER(abi.Config), i32]),
+        "or_destroy": (None, [V]),
+        "or_node_upsert": (C.c_int, [V, i32, C.POINTER(abi.Node)]),
+        "or_node_set_requested": (C.c_int, [V, i32, i64, i64]),
+        "or_node_set_cpuset_allocated": (C.c_int, [V, i32, i64]),
+        "or_nodemetric_upsert": (C.c_int, [V, i32, C.POINTER(abi.NodeMetric), i32, V, i32, V]),
+        "or_nodemetric_delete": (C.c_int, [V, i32]),
+        "or_pod_assign": (C.c_int, [V, i32, C.POINTER(abi.Pod), i64]),
+        "or_pod_unassign": (C.c_int, [V, i32, i64]),
+        "or_la_filter": (C.c_int, [V, C.POINTER(abi.Pod), i32, i64, C.POINTER(C.c_int)]),
+        "or_la_score": (i64, [V, C.POINTER(abi.Pod), i32, i64]),
+        "or_numa_filter": (C.c_int, [V, C.POINTER(abi.Pod), i32, C.POINTER(C.c_int)]),
+        "or_numa_score": (i64, [V, C.POINTER(abi.Pod), i32]),
+        "or_estimate_pod": (None, [V, C.POINTER(abi.Pod), V]),
+        "or_eval": (C.c_int, [V, i32, V, i64, V, V, V, V, V, V, C.c_int]),
+        "or_schedule": (C.c_int, [V, i32, V, i64, V, V, C.c_int]),
+        "or_usage_percent": (i64, [i64, i64]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+class Oracle:
+    def __init__(self, cfg, n_nodes):
+        self.lib = load()
+        self.cfg = cfg
+        self.n = n_nodes
+        self.h = self.lib.or_create(C.byref(cfg), n_nodes)
+
+    def close(self):
+        if self.h:
+            self.lib.or_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def num_nodes(self):
+        return self.n
+
+    def upsert_node(self, i, node):
+        assert self.lib.or_node_upsert(self.h, i, C.byref(node)) == 0
+
+    def nodes_load(self, nodes):
+        for i in range(len(nodes)):
+            node = abi.Node.from_buffer_copy(np.ascontiguousarray(nodes[i : i + 1]).tobytes())
+            self.upsert_node(i, node)
+
+    def set_requested(self, i, milli_cpu, memory):
+        assert self.lib.or_node_set_requested(self.h, i, milli_cpu, memory) == 0
+
+    def set_cpuset_allocated(self, i, cpus):
+        assert self.lib.or_node_set_cpuset_allocated(self.h, i, cpus) == 0
+
+    def set_nodemetric(self, i, nm):
+        hdr, pms, n_pm, aggs, n_agg = nm
+        assert self.lib.or_nodemetric_upsert(self.h, i, C.byref(hdr), n_pm, C.cast(pms, C.c_void_p), n_agg,
+                                             C.cast(aggs, C.c_void_p)) == 0
+
+    def nodemetrics_load(self, headers, pm_offsets, pod_metrics, agg_offsets, aggregated):
+        headers = np.ascontiguousarray(headers, dtype=abi.NODE_METRIC_DTYPE)
+        pod_metrics = np.ascontiguousarray(pod_metrics, dtype=abi.POD_METRIC_DTYPE)
+        aggregated = np.ascontiguousarray(aggregated, dtype=abi.AGG_DTYPE)
+        for i in range(len(headers)):
+            p0, p1 = int(pm_offsets[i]), int(pm_offsets[i + 1])
+            a0, a1 = int(agg_offsets[i]), int(agg_offsets[i + 1])
+            hdr = abi.NodeMetric.from_buffer_copy(headers[i : i + 1].tobytes())
+            pm_ptr = C.c_void_p(pod_metrics.ctypes.data + p0 * abi.POD_METRIC_DTYPE.itemsize) if p1 > p0 else None
+            ag_ptr = C.c_void_p(aggregated.ctypes.data + a0 * abi.AGG_DTYPE.itemsize) if a1 > a0 else None
+            assert self.lib.or_nodemetric_upsert(self.h, i, C.byref(hdr), p1 - p0, pm_ptr, a1 - a0, ag_ptr) == 0
+
+    def delete_nodemetric(self, i):
+        assert self.lib.or_nodemetric_delete(self.h, i) == 0
+
+    def assign(self, i, pod, timestamp_ns):
+        assert self.lib.or_pod_assign(self.h, i, C.byref(pod), int(timestamp_ns)) == 0
+
+    def unassign(self, i, uid):
+        assert self.lib.or_pod_unassign(self.h, i, uid) == 0
+
+    # per-plugin entry points (golden vectors)
+    def la_filter(self, pod, node, now_ns):
+        r = C.c_int()
+        code = self.lib.or_la_filter(self.h, C.byref(pod), node, int(now_ns), C.byref(r))
+        return code, r.value
+
+    def la_score(self, pod, node, now_ns):
+        return self.lib.or_la_score(self.h, C.byref(pod), node, int(now_ns))
+
+    def numa_filter(self, pod, node):
+        r = C.c_int()
+        code = self.lib.or_numa_filter(self.h, C.byref(pod), node, C.byref(r))
+        return code, r.value
+
+    def numa_score(self, pod, node):
+        return self.lib.or_numa_score(self.h, C.byref(pod), node)
+
+    def estimate_pod(self, pod):
+        est = np.zeros(2, np.int64)
+        self.lib.or_estimate_pod(self.h, C.byref(pod), abi.ptr(est))
+        return est
+
+    def eval(self, pods, now_ns, n_threads=0):
+        pods = as_pod_array(pods)
+        P, N = len(pods), self.n
+        out = {
+            "status": np.zeros((P, N), np.uint8),
+            "reason": np.zeros((P, N), np.uint8),
+            "la": np.zeros((P, N), np.int16),
+            "numa": np.zeros((P, N), np.int16),
+            "total": np.zeros((P, N), np.int16),
+            "best": np.zeros(P, np.int32),
+        }
+        rc = self.lib.or_eval(self.h, P, abi.ptr(pods), int(now_ns), abi.ptr(out["status"]), abi.ptr(out["reason"]),
+                              abi.ptr(out["la"]), abi.ptr(out["numa"]), abi.ptr(out["total"]), abi.ptr(out["best"]),
+                              n_threads)
+        if rc != 0:
+            raise RuntimeError(f"oracle eval rc={rc}")
+        return out
+
+    def schedule(self, pods, now_ns, n_threads=0):
+        pods = as_pod_array(pods)
+        chosen = np.zeros(len(pods), np.int32)
+        score = np.zeros(len(pods), np.int32)
+        rc = self.lib.or_schedule(self.h, len(pods), abi.ptr(pods), int(now_ns), abi.ptr(chosen), abi.ptr(score),
+                                  n_threads)
+        if rc != 0:
+            raise RuntimeError(f"oracle schedule rc={rc}")
+        return chosen, score
+
+
+def usage_percent(used, total):
+    return load().or_usage_percent(used, total)

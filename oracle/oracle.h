@@ -1,0 +1,56 @@
+/*
+ * oracle.h — TEST INFRASTRUCTURE ONLY.  CPU restatement of koord-scheduler's LoadAwareScheduling and
+ * NodeNUMAResource (policy None) Filter/Score and of the framework's weighted sum + selectHost.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library, and only
+ * as the checker / the timed CPU baseline.  The product (libkoordeval.so) never links or calls it.
+ *
+ * It works on the same object-level structs as the product boundary (include/koord_eval.h) but keeps
+ * its own state and recomputes every per-node quantity on every call, exactly like the Go plugins do.
+ */
+#ifndef KE_ORACLE_H
+#define KE_ORACLE_H
+#include <stdint.h>
+#include "koord_eval.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct or_cluster or_cluster;
+
+or_cluster* or_create(const ke_config* cfg, int32_t n_nodes);
+void or_destroy(or_cluster* c);
+int or_node_upsert(or_cluster* c, int32_t node, const ke_node* n);
+int or_node_set_requested(or_cluster* c, int32_t node, int64_t milli_cpu, int64_t memory);
+int or_node_set_cpuset_allocated(or_cluster* c, int32_t node, int64_t cpus);
+int or_nodemetric_upsert(or_cluster* c, int32_t node, const ke_node_metric* nm, int32_t n_pm,
+                         const ke_pod_metric* pm, int32_t n_agg, const ke_aggregated_usage* agg);
+int or_nodemetric_delete(or_cluster* c, int32_t node);
+int or_pod_assign(or_cluster* c, int32_t node, const ke_pod* pod, int64_t timestamp_ns);
+int or_pod_unassign(or_cluster* c, int32_t node, int64_t uid);
+
+/* Per-plugin entry points for one (pod, node) pair (golden-vector tests). */
+int or_la_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int64_t now_ns, int* reason);
+int64_t or_la_score(const or_cluster* c, const ke_pod* pod, int32_t node, int64_t now_ns);
+int or_numa_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* reason);
+int64_t or_numa_score(const or_cluster* c, const ke_pod* pod, int32_t node);
+/* DefaultEstimator.EstimatePod (estimator/default_estimator.go:59-85): est[KE_NRES], -1 = key absent */
+void or_estimate_pod(const or_cluster* c, const ke_pod* pod, int64_t* est);
+
+/* Matrix evaluation, same layout as ke_eval.  n_threads <= 0: all cores. */
+int or_eval(const or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now_ns, uint8_t* status,
+            uint8_t* reason, int16_t* la_score, int16_t* numa_score, int16_t* total, int32_t* best,
+            int n_threads);
+/* Sequential scheduling, same contract as ke_schedule (mutates the oracle's state). */
+int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int32_t* chosen,
+                int32_t* score, int n_threads);
+
+/* filterNodeUsage's usage percentage, exposed for the threshold-folding property tests:
+ * int64(math.Round(float64(used)/float64(total)*100)) (load_aware.go:299). */
+int64_t or_usage_percent(int64_t used, int64_t total);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

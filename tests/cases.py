@@ -1,0 +1,130 @@
+"""Turn the JSON golden fixtures (tests/golden/*.json) into calls on a cluster handle — the oracle
+(oracle.binding.Oracle) or the product (koordinator_amd.Evaluator); both expose the same methods."""
+import json
+import os
+
+from koordinator_amd import abi, model
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+NOW = 1_760_000_000 * model.NS  # the instant the plugin method runs (fixture offsets are relative)
+S = model.NS
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)["cases"]
+
+
+def t(offset_s):
+    return None if offset_s is None else NOW + int(round(offset_s * S))
+
+
+def make_cfg(case, n_nodes=1):
+    """v1beta3-defaulted args with the case's overrides (the Go tests call SetDefaults_* first)."""
+    cfg = abi.default_config(n_nodes)
+    a = cfg.loadaware
+    args = case.get("args", {})
+    if "filter_expired_node_metrics" in args:
+        a.filter_expired_node_metrics = int(args["filter_expired_node_metrics"])
+    if "enable_schedule_when_node_metrics_expired" in args:
+        a.enable_schedule_when_node_metrics_expired = int(args["enable_schedule_when_node_metrics_expired"])
+    if "score_according_prod_usage" in args:
+        a.score_according_prod_usage = int(args["score_according_prod_usage"])
+    if "allow_customize_estimation" in args:
+        a.allow_customize_estimation = int(args["allow_customize_estimation"])
+    if "usage_thresholds" in args:  # SetDefaults only fills an empty map
+        a.usage_thresholds[:] = [abi.ABSENT, abi.ABSENT]
+        for k, v in args["usage_thresholds"].items():
+            a.usage_thresholds[model.RESOURCE_INDEX[k]] = v
+    if "prod_usage_thresholds" in args:
+        for k, v in args["prod_usage_thresholds"].items():
+            a.prod_usage_thresholds[model.RESOURCE_INDEX[k]] = v
+    if "estimated_scaling_factors" in args:  # merged with the defaults (defaults.go:105-113)
+        for k, v in args["estimated_scaling_factors"].items():
+            a.estimated_scaling_factors[model.RESOURCE_INDEX[k]] = v
+    agg = args.get("aggregated")
+    if agg is not None:
+        a.has_aggregated = 1
+        for k, v in agg.get("usage_thresholds", {}).items():
+            a.agg_usage_thresholds[model.RESOURCE_INDEX[k]] = v
+        a.agg_usage_type = model.AGG_BY_NAME[agg.get("usage_aggregation_type", "")]
+        a.agg_usage_duration_ns = int(agg.get("usage_aggregated_duration_s", 0) * S)
+        a.agg_score_type = model.AGG_BY_NAME[agg.get("score_aggregation_type", "")]
+        a.agg_score_duration_ns = int(agg.get("score_aggregated_duration_s", 0) * S)
+    na = case.get("numa_args")
+    if na:
+        cfg.numa.strategy = abi.STRATEGY_MOST_ALLOCATED if na["strategy"] == "MostAllocated" else abi.STRATEGY_LEAST_ALLOCATED
+        cfg.numa.weights[:] = [abi.ABSENT, abi.ABSENT]
+        for k, v in na["weights"].items():
+            cfg.numa.weights[model.RESOURCE_INDEX[k]] = v
+    return cfg
+
+
+def make_pod(spec):
+    spec = dict(spec)
+    kw = {}
+    for k in ("name", "namespace", "requests", "limits", "containers", "priority", "labels", "owner_kind",
+              "custom_factors"):
+        if k in spec:
+            kw[k] = spec[k]
+    return model.make_pod(**kw)
+
+
+def make_la_node(spec):
+    ca = spec.get("custom_aggregated")
+    if ca is not None:
+        ca = {"thresholds": ca.get("thresholds"), "type": ca.get("type", ""),
+              "duration_ns": int(ca.get("duration_s", 0) * S)}
+    return model.make_node(allocatable=spec.get("allocatable"),
+                           custom_usage_thresholds=spec.get("custom_usage_thresholds"),
+                           custom_prod_usage_thresholds=spec.get("custom_prod_usage_thresholds"),
+                           custom_aggregated=ca)
+
+
+def make_nm(spec):
+    aggs = [{"duration_ns": int(a["duration_s"] * S), "usage": a["usage"]} for a in spec.get("aggregated", [])]
+    return model.make_node_metric(update_time=t(spec.get("update_time_s")),
+                                  report_interval_seconds=spec.get("report_interval_seconds"),
+                                  node_usage=spec.get("node_usage"), has_node_metric=spec.get("has_node_metric", True),
+                                  pods=spec.get("pods", []), aggregated=aggs)
+
+
+def setup_loadaware(handle, case):
+    """One-node cluster of a LoadAware case on `handle`; returns the pod under test."""
+    handle.upsert_node(0, make_la_node(case["node"]))
+    if case.get("node_metric") is not None:
+        handle.set_nodemetric(0, make_nm(case["node_metric"]))
+    for ap in case.get("assigned_pods", []):
+        spec = dict(ap["pod"])
+        pod = make_pod(spec)
+        if "scheduled_at_s" in ap:
+            pod.has_scheduled = 1
+            pod.scheduled_transition_ns = t(ap["scheduled_at_s"])
+        handle.assign(0, pod, t(ap.get("timestamp_s", -0.001)))
+    return make_pod(case.get("pod", {}))
+
+
+def make_numa_nodes(case):
+    """makeNode (plugin_test.go:123-129) + existing pods folded into NodeInfo.Requested and the
+    resource manager's cpuset allocation (only recorded on nodes with NRT)."""
+    nodes = []
+    nrt = case.get("nrt", [False] * len(case["nodes"]))
+    for i, spec in enumerate(case["nodes"]):
+        cpu_m = model.milli_value(spec["capacity_cpu"])
+        ratio = spec["amplification_ratio"]
+        amp_cpu = cpu_m if ratio <= 1 else int(-(-cpu_m * ratio // 1))
+        n = model.make_node(allocatable={"cpu": f"{amp_cpu}m", "memory": spec["memory"]},
+                            raw_allocatable={"cpu": spec["capacity_cpu"], "memory": spec["memory"]},
+                            amplification_ratio=ratio)
+        req_cpu = req_mem = cpus = 0
+        for e in case.get("existing", []):
+            if e["node"] != i:
+                continue
+            req_cpu += model.milli_value(e.get("cpu", "0"))
+            req_mem += model.value(e.get("memory", "0"))
+            if e.get("cpuset") and nrt[i]:
+                cpus += model.milli_value(e["cpu"]) // 1000
+        n.requested[:] = [req_cpu, req_mem]
+        n.cpuset_allocated_cpus = cpus
+        nodes.append(n)
+    return nodes
