@@ -1,0 +1,164 @@
+"""Benchmark: pod-node Filter+Score evaluations/s and p99 per-pod scheduling latency (BASELINE.json).
+
+Workload (BASELINE.json configs[2]): 50k synthetic nodes x 100k pending pods, LoadAwareScheduling +
+NodeNUMAResource with v1beta3 default args, every pod scheduled in queue order with Reserve between
+pods (bit-exact with one-pod-at-a-time scheduling).  One step = scheduling one slice of the queue
+(queue / steps pods) against all nodes; `value` = pods x nodes evaluated per second over the timed
+steps.  The node state is resident in HBM before the timed region starts.
+
+cpu_baseline: the oracle (C restatement of the Go plugins, oracle/) scheduling a prefix of the same
+queue on the host's cores (16 threads = the upstream scheduler's Parallelism) for ~10 s of work.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from koordinator_amd import Evaluator, abi, synth  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+DEVPOD_BYTES = 40
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--nodes", type=int, default=synth.CONFIGS[3]["nodes"])
+    ap.add_argument("--pods", type=int, default=synth.CONFIGS[3]["pods"])
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target host time of the CPU baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--stream-nodes", type=int, default=4_000_000,
+                    help="B=1 streaming sweep size (N*row > 512 MB, past the 256 MB Infinity Cache); 0 = skip")
+    return ap.parse_args()
+
+
+def eval_bytes(n_nodes, b):
+    """algorithmic bytes of one eval-kernel launch: the node SoA once, the pod batch, the score output"""
+    return n_nodes * abi.load_library().ke_row_bytes() + b * DEVPOD_BYTES + b * n_nodes * 2
+
+
+def cpu_baseline(cl, pods, cfg, seconds, threads):
+    from oracle.binding import Oracle  # checker / baseline only
+
+    o = Oracle(cfg, cl.n_nodes)
+    synth.load_into(o, cl)
+    # calibrate on a small prefix, then time a prefix worth ~`seconds`
+    t = time.perf_counter()
+    o.schedule(pods[:8], synth.T0, n_threads=threads)
+    per_pod = max((time.perf_counter() - t) / 8, 1e-6)
+    n = int(min(len(pods) - 8, max(16, seconds / per_pod)))
+    t = time.perf_counter()
+    o.schedule(pods[8:8 + n], synth.T0, n_threads=threads)
+    dt = time.perf_counter() - t
+    return {"value": n * cl.n_nodes / dt, "unit": "pod-node evals/s", "cores": threads, "kind": "port",
+            "sample": f"oracle (C restatement of the Go plugins) scheduling pods 8..{8 + n} of the same queue "
+                      f"against all {cl.n_nodes} nodes, {threads} threads, {dt:.1f} s"}
+
+
+def stream_sweep(n_nodes, cfg_batch):
+    """B=1 HBM streaming measurement of the eval kernel over a SoA far larger than the MALL."""
+    cl = synth.make_cluster(n_nodes, synth.BASE_SEED + 9, max_pods_per_node=0)
+    ev = Evaluator(synth.config(n_nodes, pod_batch=cfg_batch))
+    synth.load_into(ev, cl)
+    pod = synth.make_pods(1, synth.BASE_SEED + 99)
+    ms = ev.bench_eval_kernel(pod, synth.T0, iters=20)
+    by = eval_bytes(n_nodes, 1)
+    ev.close()
+    return {"nodes": n_nodes, "pods_per_launch": 1, "avg_ms": ms, "bytes_per_launch": by,
+            "achieved": by / ms / 1e6, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": by / ms / 1e6 / HBM_PEAK_GBS}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if a.gpus != 1 or world != 1:
+        raise SystemExit("multi-GPU node sharding: run bench_multi (not in this build)")
+    import torch
+
+    torch.cuda.set_device(0)
+    N, P, K, W = a.nodes, a.pods, a.steps, a.warmup
+    cl = synth.make_cluster(N, synth.BASE_SEED + 3)
+    pods = synth.make_pods(P, synth.BASE_SEED + 103)
+    cfg = synth.config(N, pod_batch=a.batch)
+    slice_len = P // K
+
+    # warmup on a throwaway context (same cluster, different pods) so the timed job starts pristine
+    if W > 0:
+        ew = Evaluator(cfg)
+        synth.load_into(ew, cl)
+        wp = synth.make_pods(W * slice_len, synth.BASE_SEED + 203)
+        for w in range(W):
+            ew.schedule(wp[w * slice_len:(w + 1) * slice_len], synth.T0)
+        ew.close()
+
+    ev = Evaluator(cfg)
+    synth.load_into(ev, cl)
+    ev.eval(pods[:0], synth.T0)  # derive + upload every node row: state resident in HBM
+    ev.set_profiling(8)
+    torch.cuda.synchronize()
+    lat, evm, sel, res, samples = [], [], [], [], 0
+    placed = 0
+    t0 = time.perf_counter()
+    for s in range(K):
+        chosen, _ = ev.schedule(pods[s * slice_len:(s + 1) * slice_len], synth.T0)
+        placed += int((chosen >= 0).sum())
+        _, per_batch = ev.stats()
+        lat.extend(per_batch.tolist())
+        ks = ev.kernel_stats()
+        evm.append(ks["eval_ms"] * ks["samples"])
+        sel.append(ks["select_ms"] * ks["samples"])
+        res.append(ks["resolve_ms"] * ks["samples"])
+        samples += ks["samples"]
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    evals = K * slice_len * N
+    eval_ms = sum(evm) / max(samples, 1)
+    by = eval_bytes(N, a.batch)
+    out = {
+        "metric": "pod-node Filter+Score evals/sec + p99 per-pod sched latency @50k nodes",
+        "value": evals / dt,
+        "unit": "pod-node evals/s",
+        "n_gpus": 1,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": dt / K * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (BASELINE.md generator, seed 20251015+3)",
+        "config": {"workload": synth.CONFIGS[3]["name"], "nodes": N, "pods": K * slice_len,
+                   "pods_per_batch": a.batch, "plugins": "LoadAwareScheduling+NodeNUMAResource",
+                   "args": "v1beta3 defaults, NodeMetricExpirationSeconds=3600", "parallelism": "node-shard x1"},
+        "p99_pod_latency_ms": float(np.percentile(lat, 99)) if lat else None,
+        "p50_pod_latency_ms": float(np.percentile(lat, 50)) if lat else None,
+        "pods_placed": placed,
+        "kernel_ms": {"eval": eval_ms, "select": sum(sel) / max(samples, 1), "resolve": sum(res) / max(samples, 1),
+                      "samples": samples},
+        "roofline": {"bound": "hbm", "kernel": "k_eval_batch", "achieved": by / eval_ms / 1e6 if eval_ms else None,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": (by / eval_ms / 1e6 / HBM_PEAK_GBS) if eval_ms else None, "traffic": None,
+                     "bytes_per_launch": by},
+    }
+    ev.close()
+    if a.stream_nodes > 0:
+        out["stream_roofline"] = stream_sweep(a.stream_nodes, a.batch)
+    if not a.no_cpu_baseline and rank == 0:
+        out["cpu_baseline"] = cpu_baseline(cl, pods, cfg, a.cpu_seconds, a.cpu_threads)
+        out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -281,6 +281,8 @@ int ke_nodemetric_delete(ke_ctx* ctx, int32_t node); /* lister Get -> NotFound *
  * condition (pod_assign_cache.go:99-122, timeNowFn fallback). */
 int ke_pod_assign(ke_ctx* ctx, int32_t node, const ke_pod* pod, int64_t timestamp_ns);
 int ke_pod_unassign(ke_ctx* ctx, int32_t node, int64_t uid);
+/* Bulk podAssignCache.assign for the initial informer list: pod i goes to nodes[i]. */
+int ke_pods_assign(ke_ctx* ctx, int32_t n, const int32_t* nodes, const ke_pod* pods, const int64_t* timestamps_ns);
 
 /* DefaultEstimator.EstimatePod (loadaware/estimator/default_estimator.go:59-122) under this
  * context's args: est[KE_NRES] (cpu milli, memory bytes), KE_ABSENT for a resource without weight. */
@@ -310,6 +312,17 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
  * latency (pod dequeue -> node selected) in milliseconds, n_batches entries. */
 int ke_last_schedule_stats(ke_ctx* ctx, double* total_ms, int32_t* n_batches,
                            double* batch_ms, int32_t batch_ms_cap);
+
+/* ---- measurement ----------------------------------------------------------------------------- */
+/* Sample every `sample_every`-th batch of ke_schedule with HIP event pairs around each of its
+ * kernels (0 = off).  ke_last_kernel_stats returns the average device milliseconds per launch of
+ * the eval / select / resolve kernels over the sampled batches of the last ke_schedule. */
+int ke_set_profiling(ke_ctx* ctx, int32_t sample_every);
+int ke_last_kernel_stats(ke_ctx* ctx, double* eval_ms, double* select_ms, double* resolve_ms, int32_t* samples);
+/* Launch the batch eval kernel `iters` times back to back over the current node SoA for `n_pods`
+ * (<= 64) pods and return the HIP-event average milliseconds per launch (roofline measurement). */
+int ke_bench_eval_kernel(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int32_t iters,
+                         double* avg_ms);
 
 /* ---- introspection (tests, tools) ------------------------------------------------------------ */
 /* sizeof() of one node row of the device SoA in bytes (algorithmic bytes per node per pass). */

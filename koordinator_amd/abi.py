@@ -214,10 +214,14 @@ EXPORTS = {
     "ke_nodemetric_delete": (C.c_int, [C.c_void_p, i32]),
     "ke_pod_assign": (C.c_int, [C.c_void_p, i32, C.POINTER(Pod), i64]),
     "ke_pod_unassign": (C.c_int, [C.c_void_p, i32, i64]),
+    "ke_pods_assign": (C.c_int, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "ke_estimate_pod": (C.c_int, [C.c_void_p, C.POINTER(Pod), C.c_void_p]),
     "ke_eval": (C.c_int, [C.c_void_p, i32, C.c_void_p, i64] + [C.c_void_p] * 6),
     "ke_schedule": (C.c_int, [C.c_void_p, i32, C.c_void_p, i64, C.c_void_p, C.c_void_p]),
     "ke_last_schedule_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(i32), C.c_void_p, i32]),
+    "ke_set_profiling": (C.c_int, [C.c_void_p, i32]),
+    "ke_last_kernel_stats": (C.c_int, [C.c_void_p] + [C.POINTER(C.c_double)] * 3 + [C.POINTER(i32)]),
+    "ke_bench_eval_kernel": (C.c_int, [C.c_void_p, i32, C.c_void_p, i64, i32, C.POINTER(C.c_double)]),
     "ke_row_bytes": (C.c_int, []),
     "ke_debug_rows": (C.c_int, [C.c_void_p, i32, i64, C.c_void_p, C.c_void_p]),
     "ke_debug_usage_bound": (i64, [i64, i64]),

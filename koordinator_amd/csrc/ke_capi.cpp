@@ -15,6 +15,8 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
                 int16_t* la, int16_t* numa, int16_t* total, int32_t* best);
 int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t* chosen, int32_t* score);
 int device_debug_rows(Context* ctx, int32_t n, Row* out);
+int device_set_profiling(Context* ctx, int32_t every);
+int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t iters, double* avg_ms);
 }  // namespace ke
 
 using namespace ke;
@@ -198,6 +200,16 @@ int ke_pod_assign(ke_ctx* ctx, int32_t node, const ke_pod* pod, int64_t timestam
   return KE_OK;
 }
 
+int ke_pods_assign(ke_ctx* ctx, int32_t n, const int32_t* nodes, const ke_pod* pods, const int64_t* timestamps_ns) {
+  if (!ctx || n < 0 || (n > 0 && (!nodes || !pods || !timestamps_ns))) return fail(KE_ERR_INVALID, "ke_pods_assign");
+  for (int32_t i = 0; i < n; i++) {
+    int rc = check_node(ctx, nodes[i]);
+    if (rc) return rc;
+    host_assign(ctx->c.cfg, ctx->c.nodes[nodes[i]], pods[i], timestamps_ns[i]);
+  }
+  return KE_OK;
+}
+
 int ke_pod_unassign(ke_ctx* ctx, int32_t node, int64_t uid) {
   int rc = check_node(ctx, node);
   if (rc) return rc;
@@ -265,6 +277,32 @@ int ke_last_schedule_stats(ke_ctx* ctx, double* total_ms, int32_t* n_batches, do
     for (int32_t i = 0; i < n; i++) batch_ms[i] = ctx->c.last_batch_ms[i];
   }
   return KE_OK;
+}
+
+int ke_set_profiling(ke_ctx* ctx, int32_t sample_every) {
+  if (!ctx) return fail(KE_ERR_INVALID, "null context");
+  int rc = require_device(ctx);
+  if (rc) return rc;
+  return device_set_profiling(&ctx->c, sample_every);
+}
+
+int ke_last_kernel_stats(ke_ctx* ctx, double* eval_ms, double* select_ms, double* resolve_ms, int32_t* samples) {
+  if (!ctx) return fail(KE_ERR_INVALID, "null context");
+  if (eval_ms) *eval_ms = ctx->c.kstat_eval_ms;
+  if (select_ms) *select_ms = ctx->c.kstat_select_ms;
+  if (resolve_ms) *resolve_ms = ctx->c.kstat_resolve_ms;
+  if (samples) *samples = ctx->c.kstat_samples;
+  return KE_OK;
+}
+
+int ke_bench_eval_kernel(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int32_t iters,
+                         double* avg_ms) {
+  if (!ctx || !avg_ms) return fail(KE_ERR_INVALID, "ke_bench_eval_kernel arguments");
+  int rc = check_pods(pods, n_pods);
+  if (rc) return rc;
+  rc = require_device(ctx);
+  if (rc) return rc;
+  return device_bench_eval(&ctx->c, n_pods, pods, now_ns, iters, avg_ms);
 }
 
 int64_t ke_debug_usage_bound(int64_t total, int64_t thr) { return total > 0 ? max_used_within(total, thr) : 0; }

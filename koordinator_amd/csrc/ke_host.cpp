@@ -260,6 +260,7 @@ static bool should_estimate(const ke_loadaware_args& a, const AssignedPod& info,
 
 static Terms compute_terms(const ke_loadaware_args& a, const NodeState& ns, bool prod, int64_t now, int64_t* valid_until) {
   Terms t;
+  if (ns.asg.empty() && ns.pm.empty()) return t;
   // buildPodMetricMap(nodeMetric, prod): name -> last PodMetricInfo (helper.go:154-170)
   std::unordered_map<int64_t, const ke_pod_metric*> metrics;
   metrics.reserve(ns.pm.size() * 2 + 1);

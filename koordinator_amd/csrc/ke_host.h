@@ -44,6 +44,8 @@ struct Context {
   // last ke_schedule timing
   double last_total_ms = 0.0;
   std::vector<double> last_batch_ms;
+  double kstat_eval_ms = 0, kstat_select_ms = 0, kstat_resolve_ms = 0;
+  int32_t kstat_samples = 0;
 };
 
 // error plumbing (thread-local, read by ke_last_error)

@@ -581,6 +581,7 @@ struct DeviceState {
   int64_t parity_cap = 0;
   uint32_t* d_best = nullptr;
   int64_t best_cap = 0;
+  int profile_every = 0;
 };
 
 static int ensure(void** p, int64_t* cap, int64_t bytes) {
@@ -759,20 +760,35 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   HIP_OK(hipEventCreate(&e1));
   HIP_OK(hipEventRecord(e0, d->stream));
   hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, d->stream, d->d_stamps);
+  // sampled per-kernel HIP event pairs (ke_set_profiling)
+  const int every = d->profile_every;
+  std::vector<hipEvent_t> ev;
+  if (every > 0) {
+    const int samples = (n_batches + every - 1) / every;
+    ev.resize((size_t)samples * 4);
+    for (auto& e : ev) HIP_OK(hipEventCreate(&e));
+  }
   for (int b = 0; b < n_batches; b++) {
     const int bp = std::min(B, n_pods - b * B);
+    const bool prof = every > 0 && b % every == 0;
+    hipEvent_t* pe = prof ? &ev[(size_t)(b / every) * 4] : nullptr;
+    if (prof) HIP_OK(hipEventRecord(pe[0], d->stream));
     if (N > 0) {
       dim3 grid((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((bp + ppb - 1) / ppb));
       hipLaunchKernelGGL(k_eval_batch, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, N, d->d_pods, d->d_batch_base, bp,
                          ppb, k, d->d_scores, d->capacity);
+      if (prof) HIP_OK(hipEventRecord(pe[1], d->stream));
       hipLaunchKernelGGL(k_select, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, d->stream, d->d_scores, d->capacity, N,
                          d->d_cand, d->d_cand_cnt);
     } else {
+      if (prof) HIP_OK(hipEventRecord(pe[1], d->stream));
       HIP_OK(hipMemsetAsync(d->d_cand_cnt, 0, sizeof(int32_t) * MAX_BATCH, d->stream));
     }
+    if (prof) HIP_OK(hipEventRecord(pe[2], d->stream));
     hipLaunchKernelGGL(k_resolve, dim3(1), dim3(64), 0, d->stream, d->soa, d->d_pods, d->d_batch_base, bp, k,
                        d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score, ctx->cfg.global_node_offset,
                        d->d_stamps, b);
+    if (prof) HIP_OK(hipEventRecord(pe[3], d->stream));
   }
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(e1, d->stream));
@@ -791,6 +807,63 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   const double ms_per_tick = span > 0 ? ms / span : 1e-5;
   ctx->last_batch_ms.resize(n_batches);
   for (int b = 0; b < n_batches; b++) ctx->last_batch_ms[b] = (double)(st[b + 1] - st[b]) * ms_per_tick;
+  ctx->kstat_samples = 0;
+  ctx->kstat_eval_ms = ctx->kstat_select_ms = ctx->kstat_resolve_ms = 0;
+  for (size_t s = 0; s + 3 < ev.size(); s += 4) {
+    float a = 0, b = 0, c = 0;
+    HIP_OK(hipEventElapsedTime(&a, ev[s], ev[s + 1]));
+    HIP_OK(hipEventElapsedTime(&b, ev[s + 1], ev[s + 2]));
+    HIP_OK(hipEventElapsedTime(&c, ev[s + 2], ev[s + 3]));
+    ctx->kstat_eval_ms += a;
+    ctx->kstat_select_ms += b;
+    ctx->kstat_resolve_ms += c;
+    ctx->kstat_samples++;
+  }
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  if (ctx->kstat_samples) {
+    ctx->kstat_eval_ms /= ctx->kstat_samples;
+    ctx->kstat_select_ms /= ctx->kstat_samples;
+    ctx->kstat_resolve_ms /= ctx->kstat_samples;
+  }
+  return KE_OK;
+}
+
+int device_set_profiling(Context* ctx, int32_t every) {
+  ctx->dev->profile_every = every < 0 ? 0 : every;
+  return KE_OK;
+}
+
+int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t iters, double* avg_ms) {
+  DeviceState* d = ctx->dev;
+  HIP_OK(hipSetDevice(d->device));
+  if (n_pods < 1 || n_pods > MAX_BATCH || iters < 1) return fail(KE_ERR_INVALID, "bench: 1 <= n_pods <= 64, iters >= 1");
+  int rc = device_refresh(ctx, now);
+  if (rc) return rc;
+  rc = upload_pods(ctx, n_pods, pods);
+  if (rc) return rc;
+  const int N = ctx->n_nodes;
+  if (N == 0) return fail(KE_ERR_INVALID, "bench: no nodes");
+  const KArgs k = make_kargs(ctx, now);
+  const int ppb = 8;
+  HIP_OK(hipMemsetAsync(d->d_batch_base, 0, sizeof(int32_t), d->stream));
+  dim3 grid((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((n_pods + ppb - 1) / ppb));
+  hipLaunchKernelGGL(k_eval_batch, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, N, d->d_pods, d->d_batch_base, n_pods,
+                     ppb, k, d->d_scores, d->capacity);  // warm
+  hipEvent_t e0, e1;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  HIP_OK(hipEventRecord(e0, d->stream));
+  for (int it = 0; it < iters; it++)
+    hipLaunchKernelGGL(k_eval_batch, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, N, d->d_pods, d->d_batch_base,
+                       n_pods, ppb, k, d->d_scores, d->capacity);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(e1, d->stream));
+  HIP_OK(hipEventSynchronize(e1));
+  float ms = 0;
+  HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  *avg_ms = ms / iters;
   return KE_OK;
 }
 

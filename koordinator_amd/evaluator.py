@@ -104,6 +104,12 @@ class Evaluator:
     def assign(self, i, pod, timestamp_ns):
         self._check(self.lib.ke_pod_assign(self.h, i, C.byref(pod), int(timestamp_ns)))
 
+    def assign_bulk(self, nodes, pods, timestamps_ns):
+        nodes = np.ascontiguousarray(nodes, dtype=np.int32)
+        pods = as_pod_array(pods)
+        ts = np.ascontiguousarray(timestamps_ns, dtype=np.int64)
+        self._check(self.lib.ke_pods_assign(self.h, len(nodes), abi.ptr(nodes), abi.ptr(pods), abi.ptr(ts)))
+
     def unassign(self, i, uid):
         self._check(self.lib.ke_pod_unassign(self.h, i, uid))
 
@@ -143,6 +149,21 @@ class Evaluator:
         per = np.zeros(max(nb.value, 1), np.float64)
         self._check(self.lib.ke_last_schedule_stats(self.h, None, None, abi.ptr(per), len(per)))
         return total.value, per[: nb.value]
+
+    def set_profiling(self, sample_every):
+        self._check(self.lib.ke_set_profiling(self.h, sample_every))
+
+    def kernel_stats(self):
+        v = [C.c_double() for _ in range(3)]
+        n = abi.i32()
+        self._check(self.lib.ke_last_kernel_stats(self.h, *[C.byref(x) for x in v], C.byref(n)))
+        return {"eval_ms": v[0].value, "select_ms": v[1].value, "resolve_ms": v[2].value, "samples": n.value}
+
+    def bench_eval_kernel(self, pods, now_ns, iters):
+        pods = as_pod_array(pods)
+        ms = C.c_double()
+        self._check(self.lib.ke_bench_eval_kernel(self.h, len(pods), abi.ptr(pods), int(now_ns), iters, C.byref(ms)))
+        return ms.value
 
     def debug_rows(self, now_ns, device=True):
         n = self.num_nodes

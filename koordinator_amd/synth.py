@@ -1,0 +1,211 @@
+"""Synthetic clusters for the bench and the parity tests (BASELINE.md "CPU baseline plan").
+
+Seeds: 20251015 + config id.  Quantities are exact integers (cpu in milli, memory a multiple of 1 MiB)
+so that resource.Quantity rounding never enters.  Node mix: allocatable cpu {32,64,96,128} cores,
+memory {128,256,512,1024} GiB; NodeMetric 96% fresh (t0-30s) / 2% expired (t0-1e6 s) / 2% absent with
+NodeMetricExpirationSeconds = 3600; NodeUsage cpu ~ U[0, .75 alloc], memory ~ U[.1, .9] alloc; 30% of
+nodes carry a 5-minute p95 AggregatedUsage; 10% carry custom usage thresholds; U{0..20} pre-existing
+pods per node with PodMetrics and PodScheduled at t0-3600s (never "estimated").  Pod queue: 60% LS
+koord-prod, 38% BE koord-batch, 2% DaemonSet-owned.
+"""
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import abi
+
+BASE_SEED = 20251015
+NS = 1_000_000_000
+GI = 1 << 30
+MI = 1 << 20
+T0 = 1_760_000_000 * NS  # "now" of the synthetic cluster
+
+CONFIGS = {
+    1: dict(nodes=1_000, pods=1_000, name="1k nodes x 1k pods, LoadAwareScheduling + NodeNUMAResource"),
+    2: dict(nodes=5_000, pods=10_000, name="5k nodes x 10k pods, mixed LS/BE with NodeMetric usage"),
+    3: dict(nodes=50_000, pods=100_000, name="50k nodes x 100k pods"),
+}
+
+
+@dataclass
+class Cluster:
+    n_nodes: int
+    nodes: np.ndarray          # NODE_DTYPE
+    nm: np.ndarray             # NODE_METRIC_DTYPE
+    has_nm: np.ndarray         # bool: NodeMetric exists (lister Get succeeds)
+    pm_offsets: np.ndarray
+    pod_metrics: np.ndarray    # POD_METRIC_DTYPE
+    agg_offsets: np.ndarray
+    aggregated: np.ndarray     # AGG_DTYPE
+    asg_nodes: np.ndarray      # int32
+    asg_pods: np.ndarray       # POD_DTYPE
+    asg_ts: np.ndarray         # int64
+    now: int = T0
+
+
+def config(node_capacity, pod_batch=64, global_node_offset=0, device_ordinal=0):
+    """bench args: v1beta3 defaults except NodeMetricExpirationSeconds = 3600."""
+    cfg = abi.default_config(node_capacity, pod_batch=pod_batch, device_ordinal=device_ordinal,
+                             global_node_offset=global_node_offset)
+    cfg.loadaware.node_metric_expiration_seconds = 3600
+    return cfg
+
+
+def _rmap_fill(arr, cpu, mem, n_keys=2):
+    arr["value"][:, 0] = cpu
+    arr["value"][:, 1] = mem
+    arr["present"][:, 0] = 1
+    arr["present"][:, 1] = 1
+    arr["n_keys"] = n_keys
+
+
+def make_cluster(n_nodes, seed, amplified_fraction=0.0, max_pods_per_node=20, key_base=1_000_000):
+    rng = np.random.default_rng(seed)
+    N = n_nodes
+    nodes = np.zeros(N, abi.NODE_DTYPE)
+    cpu_cores = rng.choice([32, 64, 96, 128], N)
+    mem_gib = rng.choice([128, 256, 512, 1024], N)
+    nodes["allocatable"][:, 0] = cpu_cores * 1000
+    nodes["allocatable"][:, 1] = mem_gib * GI
+    nodes["raw_allocatable"][:] = abi.ABSENT
+    nodes["cpu_amplification_ratio"] = -1.0
+    nodes["nrt_cpu_amplification_ratio"] = -2.0
+    for f in ("custom_usage_thresholds", "custom_prod_usage_thresholds", "custom_agg_thresholds"):
+        nodes[f][:] = abi.ABSENT
+    custom = rng.random(N) < 0.10
+    nodes["has_custom_thresholds"][custom] = 1
+    nodes["custom_usage_thresholds"][custom, 0] = rng.choice([50, 60, 70, 80], custom.sum())
+    nodes["custom_usage_thresholds"][custom, 1] = rng.choice([80, 90, 95], custom.sum())
+    if amplified_fraction > 0:
+        amp = rng.random(N) < amplified_fraction
+        ratio = rng.choice([1.5, 2.0, 2.5], amp.sum())
+        nodes["cpu_amplification_ratio"][amp] = ratio
+        nodes["raw_allocatable"][amp, 0] = nodes["allocatable"][amp, 0]
+        nodes["allocatable"][amp, 0] = np.ceil(nodes["allocatable"][amp, 0] * ratio).astype(np.int64)
+        nodes["cpuset_allocated_cpus"][amp] = rng.integers(0, 8, amp.sum()) * 2
+
+    # NodeMetric headers
+    kind = rng.random(N)
+    has_nm = kind < 0.98
+    expired = (kind >= 0.96) & has_nm
+    nm = np.zeros(N, abi.NODE_METRIC_DTYPE)
+    nm["has_update_time"] = 1
+    nm["update_time_ns"] = np.where(expired, T0 - 10**6 * NS, T0 - 30 * NS)
+    nm["report_interval_seconds"] = 60
+    nm["has_node_metric"] = 1
+    alloc_cpu = nodes["allocatable"][:, 0]
+    alloc_mem = nodes["allocatable"][:, 1]
+    use_cpu = (rng.random(N) * 0.75 * alloc_cpu).astype(np.int64)
+    use_mem = ((0.1 + 0.8 * rng.random(N)) * alloc_mem).astype(np.int64) // MI * MI
+    _rmap_fill(nm["node_usage"], use_cpu, use_mem)
+
+    # aggregated usages: 30% carry a 5-minute p95
+    has_agg = rng.random(N) < 0.30
+    n_agg = has_agg.astype(np.int64)
+    agg_offsets = np.zeros(N + 1, np.int64)
+    agg_offsets[1:] = np.cumsum(n_agg)
+    aggregated = np.zeros(int(agg_offsets[-1]), abi.AGG_DTYPE)
+    aggregated["duration_ns"] = 300 * NS
+    idx = np.nonzero(has_agg)[0]
+    p95 = aggregated["usage"][:, abi.AGG_P95]
+    _rmap_fill(p95, np.minimum(alloc_cpu[idx], (use_cpu[idx] * 1.1).astype(np.int64)),
+               np.minimum(alloc_mem[idx], use_mem[idx] + 4 * GI))
+    aggregated["usage"][:, abi.AGG_P95] = p95
+
+    # pre-existing pods + their pod metrics
+    per_node = rng.integers(0, max_pods_per_node + 1, N)
+    P0 = int(per_node.sum())
+    asg_nodes = np.repeat(np.arange(N, dtype=np.int32), per_node)
+    asg = np.zeros(P0, abi.POD_DTYPE)
+    asg["pod_key"] = key_base + np.arange(P0)
+    asg["uid"] = key_base + np.arange(P0)
+    prod = rng.random(P0) < 0.6
+    req_cpu = rng.choice([500, 1000, 2000, 4000], P0)
+    req_mem = rng.choice([1, 2, 4, 8], P0) * GI
+    asg["requests"][prod, abi.RES_CPU] = req_cpu[prod]
+    asg["requests"][prod, abi.RES_MEMORY] = req_mem[prod]
+    asg["limits"][prod, abi.RES_CPU] = req_cpu[prod]
+    asg["limits"][prod, abi.RES_MEMORY] = req_mem[prod]
+    asg["requests"][~prod, abi.RES_BATCH_CPU] = req_cpu[~prod]
+    asg["requests"][~prod, abi.RES_BATCH_MEMORY] = req_mem[~prod]
+    asg["priority_class"] = np.where(prod, abi.PRIORITY_PROD, abi.PRIORITY_BATCH)
+    asg["qos_class"] = np.where(prod, abi.QOS_LS, abi.QOS_BE)
+    asg["custom_scaling_factors"][:] = abi.ABSENT
+    asg["custom_seconds_after_scheduled"] = abi.ABSENT
+    asg["custom_seconds_after_initialized"] = abi.ABSENT
+    asg["has_scheduled"] = 1
+    asg["scheduled_transition_ns"] = T0 - 3600 * NS
+    asg_ts = np.full(P0, T0 - 3600 * NS, np.int64)
+    # NodeInfo.Requested = Σ requests of the pods on the node (cpu/memory)
+    np.add.at(nodes["requested"][:, 0], asg_nodes, asg["requests"][:, abi.RES_CPU])
+    np.add.at(nodes["requested"][:, 1], asg_nodes, asg["requests"][:, abi.RES_MEMORY])
+    # pod metrics (only nodes that have a NodeMetric)
+    pm_mask = has_nm[asg_nodes]
+    pm_per_node = np.bincount(asg_nodes[pm_mask], minlength=N)
+    pm_offsets = np.zeros(N + 1, np.int64)
+    pm_offsets[1:] = np.cumsum(pm_per_node)
+    pms = np.zeros(int(pm_mask.sum()), abi.POD_METRIC_DTYPE)
+    pms["pod_key"] = asg["pod_key"][pm_mask]
+    pms["priority_class"] = asg["priority_class"][pm_mask]
+    frac = rng.random(len(pms))
+    pcpu = np.where(prod[pm_mask], req_cpu[pm_mask], req_cpu[pm_mask])
+    _rmap_fill(pms["usage"], (pcpu * frac).astype(np.int64), (req_mem[pm_mask] * frac).astype(np.int64) // MI * MI)
+    return Cluster(N, nodes, nm, has_nm, pm_offsets, pms, agg_offsets, aggregated, asg_nodes, asg, asg_ts)
+
+
+def make_pods(n_pods, seed, key_base=1_000_000_000):
+    """The pending-pod queue: 60% LS koord-prod, 38% BE koord-batch, 2% DaemonSet-owned."""
+    rng = np.random.default_rng(seed)
+    P = n_pods
+    pods = np.zeros(P, abi.POD_DTYPE)
+    pods["pod_key"] = key_base + np.arange(P)
+    pods["uid"] = key_base + np.arange(P)
+    u = rng.random(P)
+    ls = u < 0.60
+    be = (u >= 0.60) & (u < 0.98)
+    ds = u >= 0.98
+    cpu = rng.choice([1, 2, 4, 8], P) * 1000
+    mem = rng.choice([2, 4, 8, 16], P) * GI
+    lim_mult = rng.choice([1, 2], P)
+    pods["requests"][ls | ds, abi.RES_CPU] = cpu[ls | ds]
+    pods["requests"][ls | ds, abi.RES_MEMORY] = mem[ls | ds]
+    pods["limits"][ls | ds, abi.RES_CPU] = (cpu * lim_mult)[ls | ds]
+    pods["limits"][ls | ds, abi.RES_MEMORY] = (mem * lim_mult)[ls | ds]
+    bcpu = rng.integers(1, 9, P) * 1000
+    bmem = rng.integers(1, 9, P) * GI
+    pods["requests"][be, abi.RES_BATCH_CPU] = bcpu[be]
+    pods["requests"][be, abi.RES_BATCH_MEMORY] = bmem[be]
+    pods["limits"][be, abi.RES_BATCH_CPU] = bcpu[be]
+    pods["limits"][be, abi.RES_BATCH_MEMORY] = bmem[be]
+    pods["priority_class"] = np.where(be, abi.PRIORITY_BATCH, abi.PRIORITY_PROD)
+    pods["qos_class"] = np.where(be, abi.QOS_BE, abi.QOS_LS)
+    pods["is_daemonset"] = ds.astype(np.uint8)
+    pods["custom_scaling_factors"][:] = abi.ABSENT
+    pods["custom_seconds_after_scheduled"] = abi.ABSENT
+    pods["custom_seconds_after_initialized"] = abi.ABSENT
+    return pods
+
+
+def load_into(handle, cl):
+    """Ingest a synthetic cluster into an Evaluator or an Oracle (same informer-event calls)."""
+    handle.nodes_load(cl.nodes)
+    hm = np.nonzero(cl.has_nm)[0]
+    # nodemetrics_load covers [0, N): load all, then delete the absent ones (lister NotFound)
+    handle.nodemetrics_load(cl.nm, cl.pm_offsets, cl.pod_metrics, cl.agg_offsets, cl.aggregated)
+    for i in np.nonzero(~cl.has_nm)[0]:
+        handle.delete_nodemetric(int(i))
+    handle.assign_bulk(cl.asg_nodes, cl.asg_pods, cl.asg_ts)
+    return len(hm)
+
+
+def shard(cl, rank, world):
+    """Contiguous node shard [rank*N/world, (rank+1)*N/world) of a cluster."""
+    N = cl.n_nodes
+    lo, hi = rank * N // world, (rank + 1) * N // world
+    pm0, pm1 = cl.pm_offsets[lo], cl.pm_offsets[hi]
+    ag0, ag1 = cl.agg_offsets[lo], cl.agg_offsets[hi]
+    am = (cl.asg_nodes >= lo) & (cl.asg_nodes < hi)
+    return lo, Cluster(hi - lo, cl.nodes[lo:hi].copy(), cl.nm[lo:hi].copy(), cl.has_nm[lo:hi].copy(),
+                       cl.pm_offsets[lo:hi + 1] - pm0, cl.pod_metrics[pm0:pm1].copy(),
+                       cl.agg_offsets[lo:hi + 1] - ag0, cl.aggregated[ag0:ag1].copy(),
+                       (cl.asg_nodes[am] - lo).astype(np.int32), cl.asg_pods[am].copy(), cl.asg_ts[am].copy(), cl.now)

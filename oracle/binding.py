@@ -40,6 +40,7 @@ def load():
         "or_nodemetric_delete": (C.c_int, [V, i32]),
         "or_pod_assign": (C.c_int, [V, i32, C.POINTER(abi.Pod), i64]),
         "or_pod_unassign": (C.c_int, [V, i32, i64]),
+        "or_pods_assign": (C.c_int, [V, i32, V, V, V]),
         "or_la_filter": (C.c_int, [V, C.POINTER(abi.Pod), i32, i64, C.POINTER(C.c_int)]),
         "or_la_score": (i64, [V, C.POINTER(abi.Pod), i32, i64]),
         "or_numa_filter": (C.c_int, [V, C.POINTER(abi.Pod), i32, C.POINTER(C.c_int)]),
@@ -115,6 +116,12 @@ class Oracle:
 
     def assign(self, i, pod, timestamp_ns):
         assert self.lib.or_pod_assign(self.h, i, C.byref(pod), int(timestamp_ns)) == 0
+
+    def assign_bulk(self, nodes, pods, timestamps_ns):
+        nodes = np.ascontiguousarray(nodes, dtype=np.int32)
+        pods = as_pod_array(pods)
+        ts = np.ascontiguousarray(timestamps_ns, dtype=np.int64)
+        assert self.lib.or_pods_assign(self.h, len(nodes), abi.ptr(nodes), abi.ptr(pods), abi.ptr(ts)) == 0
 
     def unassign(self, i, uid):
         assert self.lib.or_pod_unassign(self.h, i, uid) == 0

@@ -639,6 +639,14 @@ int or_pod_assign(or_cluster* c, int32_t node, const ke_pod* pod, int64_t timest
   return KE_OK;
 }
 
+int or_pods_assign(or_cluster* c, int32_t n, const int32_t* nodes, const ke_pod* pods, const int64_t* ts) {
+  for (int32_t i = 0; i < n; i++) {
+    int rc = or_pod_assign(c, nodes[i], &pods[i], ts[i]);
+    if (rc) return rc;
+  }
+  return KE_OK;
+}
+
 /* podAssignCache.unAssign  pod_assign_cache.go:126-136 */
 int or_pod_unassign(or_cluster* c, int32_t node, int64_t uid) {
   if (node < 0 || node >= c->n) return KE_ERR_NOT_FOUND;

@@ -29,6 +29,7 @@ int or_nodemetric_upsert(or_cluster* c, int32_t node, const ke_node_metric* nm, 
 int or_nodemetric_delete(or_cluster* c, int32_t node);
 int or_pod_assign(or_cluster* c, int32_t node, const ke_pod* pod, int64_t timestamp_ns);
 int or_pod_unassign(or_cluster* c, int32_t node, int64_t uid);
+int or_pods_assign(or_cluster* c, int32_t n, const int32_t* nodes, const ke_pod* pods, const int64_t* ts);
 
 /* Per-plugin entry points for one (pod, node) pair (golden-vector tests). */
 int or_la_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int64_t now_ns, int* reason);

@@ -1,0 +1,213 @@
+"""GPU parity: the gfx950 path (libkoordeval.so through the C ABI) against the oracle and the golden
+vectors.  Bit-exact on every status, reason, per-plugin score, framework total and selected node."""
+import numpy as np
+import pytest
+
+import cases
+from koordinator_amd import Evaluator, abi, model, synth
+from oracle.binding import Oracle
+
+pytestmark = pytest.mark.gpu
+
+LA_FILTER = cases.load("loadaware_filter.json")
+LA_SCORE = cases.load("loadaware_score.json")
+NUMA = cases.load("numa.json")
+
+
+# ---- golden vectors through the product ----------------------------------------------------------
+@pytest.mark.parametrize("case", LA_FILTER, ids=[c["name"] for c in LA_FILTER])
+def test_golden_loadaware_filter(gpu, case):
+    ev = Evaluator(cases.make_cfg(case))
+    pod = cases.setup_loadaware(ev, case)
+    r = ev.eval([pod], cases.NOW)
+    assert (int(r["status"][0, 0]), int(r["reason"][0, 0])) == (case["want"]["code"], case["want"]["reason"])
+
+
+@pytest.mark.parametrize("case", LA_SCORE, ids=[c["name"] for c in LA_SCORE])
+def test_golden_loadaware_score(gpu, case):
+    # Go's TestScore calls Score without Filter: disable the thresholds so every node reaches Score
+    cfg = cases.make_cfg(case)
+    cfg.loadaware.usage_thresholds[:] = [abi.ABSENT, abi.ABSENT]
+    cfg.loadaware.filter_expired_node_metrics = 0
+    ev = Evaluator(cfg)
+    pod = cases.setup_loadaware(ev, case)
+    r = ev.eval([pod], cases.NOW)
+    assert r["status"][0, 0] == abi.CODE_SUCCESS
+    assert int(r["la"][0, 0]) == case["want"]["score"], case["source"]
+
+
+@pytest.mark.parametrize("case", NUMA, ids=[c["name"] for c in NUMA])
+def test_golden_numa(gpu, case):
+    nodes = cases.make_numa_nodes(case)
+    ev = Evaluator(cases.make_cfg(case, len(nodes)))
+    for i, n in enumerate(nodes):
+        ev.upsert_node(i, n)
+    r = ev.eval([cases.make_pod(case["pod"])], cases.NOW)
+    if case["op"] == "score":
+        assert [int(x) for x in r["numa"][0]] == case["want"]["scores"], case["source"]
+    else:
+        assert (int(r["status"][0, 0]), int(r["reason"][0, 0])) == (case["want"]["code"], case["want"]["reason"])
+
+
+# ---- synthetic clusters: full matrices vs the oracle --------------------------------------------
+def both(cfg, cl):
+    ev, o = Evaluator(cfg), Oracle(cfg, cl.n_nodes)
+    synth.load_into(ev, cl)
+    synth.load_into(o, cl)
+    return ev, o
+
+
+def assert_eval_equal(a, b):
+    for k in ("status", "reason", "la", "numa", "total", "best"):
+        mism = np.argwhere(a[k] != b[k])
+        assert len(mism) == 0, f"{k}: {len(mism)} mismatches, first {mism[:5].tolist()}"
+
+
+VARIANTS = {
+    "default": dict(),
+    "amplified": dict(amplified=0.3),
+    "aggregated": dict(agg=True),
+    "prod-thresholds": dict(prod=True),
+    "most-allocated": dict(most=True),
+    "customize": dict(windows=True),
+}
+
+
+def variant_cfg(n, v, batch=64):
+    cfg = synth.config(n, pod_batch=batch)
+    a = cfg.loadaware
+    if v.get("agg"):
+        a.has_aggregated = 1
+        a.agg_usage_thresholds[:] = [60, 90]
+        a.agg_usage_type = abi.AGG_P95
+        a.agg_usage_duration_ns = 300 * synth.NS
+        a.agg_score_type = abi.AGG_P95
+        a.agg_score_duration_ns = 0
+    if v.get("prod"):
+        a.prod_usage_thresholds[:] = [55, 85]
+        a.score_according_prod_usage = 1
+    if v.get("most"):
+        cfg.numa.strategy = abi.STRATEGY_MOST_ALLOCATED
+    if v.get("windows"):
+        a.estimated_seconds_after_pod_scheduled = 7200  # pre-existing pods (t0-3600s) are re-estimated
+        a.allow_customize_estimation = 1
+    return cfg
+
+
+@pytest.mark.parametrize("name", list(VARIANTS))
+def test_eval_matrix_parity(gpu, name):
+    v = VARIANTS[name]
+    cl = synth.make_cluster(777, synth.BASE_SEED + 11, amplified_fraction=v.get("amplified", 0.0))
+    pods = synth.make_pods(96, synth.BASE_SEED + 12)
+    ev, o = both(variant_cfg(cl.n_nodes, v), cl)
+    assert_eval_equal(ev.eval(pods, synth.T0), o.eval(pods, synth.T0))
+
+
+def test_eval_zero_pods_and_single_node(gpu):
+    cl = synth.make_cluster(1, synth.BASE_SEED + 13)
+    ev, o = both(synth.config(1), cl)
+    assert ev.eval(synth.make_pods(0, 1), synth.T0)["best"].shape == (0,)
+    pods = synth.make_pods(5, synth.BASE_SEED + 14)
+    assert_eval_equal(ev.eval(pods, synth.T0), o.eval(pods, synth.T0))
+
+
+def test_eval_time_advances(gpu):
+    """now past NodeMetric expiry: the device recomputes expiry from `now` (no stale rows)."""
+    cl = synth.make_cluster(300, synth.BASE_SEED + 15)
+    ev, o = both(synth.config(300), cl)
+    pods = synth.make_pods(8, synth.BASE_SEED + 16)
+    for now in (synth.T0, synth.T0 + 3600 * synth.NS, synth.T0 + 10**7 * synth.NS):
+        assert_eval_equal(ev.eval(pods, now), o.eval(pods, now))
+
+
+# ---- schedule: sequential placements vs the oracle ------------------------------------------------
+def test_schedule_parity_config1(gpu):
+    """BASELINE config 1: 1k nodes x 1k pods, every placement identical to one-at-a-time scheduling."""
+    cl = synth.make_cluster(1000, synth.BASE_SEED + 1)
+    pods = synth.make_pods(1000, synth.BASE_SEED + 101)
+    ev, o = both(synth.config(1000), cl)
+    c1, s1 = ev.schedule(pods, synth.T0)
+    c0, s0 = o.schedule(pods, synth.T0)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5]
+    assert np.array_equal(s1, s0)
+    # the device's Reserve patches equal a from-scratch host derivation of the object state
+    dev, host = ev.debug_rows(synth.T0)
+    assert np.array_equal(dev["f"], host["f"]) and np.array_equal(dev["flags"], host["flags"])
+    # and the state after the queue evaluates identically
+    more = synth.make_pods(64, synth.BASE_SEED + 102)
+    assert_eval_equal(ev.eval(more, synth.T0), o.eval(more, synth.T0))
+
+
+@pytest.mark.parametrize("name", ["amplified", "prod-thresholds", "most-allocated", "aggregated", "customize"])
+def test_schedule_parity_variants(gpu, name):
+    v = VARIANTS[name]
+    cl = synth.make_cluster(640, synth.BASE_SEED + 21, amplified_fraction=v.get("amplified", 0.0))
+    pods = synth.make_pods(700, synth.BASE_SEED + 22)
+    ev, o = both(variant_cfg(cl.n_nodes, v), cl)
+    c1, s1 = ev.schedule(pods, synth.T0)
+    c0, s0 = o.schedule(pods, synth.T0)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5]
+    assert np.array_equal(s1, s0)
+
+
+def test_schedule_parity_config2_prefix(gpu):
+    """BASELINE config 2 cluster (5k nodes), first 1500 pods of its 10k queue."""
+    cl = synth.make_cluster(5000, synth.BASE_SEED + 2)
+    pods = synth.make_pods(1500, synth.BASE_SEED + 102)
+    ev, o = both(synth.config(5000), cl)
+    c1, s1 = ev.schedule(pods, synth.T0)
+    c0, s0 = o.schedule(pods, synth.T0)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+
+
+@pytest.mark.parametrize("batch", [1, 7, 64])
+def test_schedule_batch_size_invariance(gpu, batch):
+    """Exact speculative batching: any batch size gives the one-pod-at-a-time result (batch 1)."""
+    cl = synth.make_cluster(400, synth.BASE_SEED + 31)
+    pods = synth.make_pods(300, synth.BASE_SEED + 32)
+    ev1 = Evaluator(synth.config(400, pod_batch=1))
+    evb = Evaluator(synth.config(400, pod_batch=batch))
+    synth.load_into(ev1, cl)
+    synth.load_into(evb, cl)
+    a = ev1.schedule(pods, synth.T0)
+    b = evb.schedule(pods, synth.T0)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_schedule_split_queue_is_idempotent(gpu):
+    """Scheduling a queue in one call or in two consecutive calls gives the same placements."""
+    cl = synth.make_cluster(2000, synth.BASE_SEED + 41)
+    pods = synth.make_pods(900, synth.BASE_SEED + 42)
+    ev1 = Evaluator(synth.config(2000))
+    ev2 = Evaluator(synth.config(2000))
+    synth.load_into(ev1, cl)
+    synth.load_into(ev2, cl)
+    a, _ = ev1.schedule(pods, synth.T0)
+    b1, _ = ev2.schedule(pods[:333], synth.T0)
+    b2, _ = ev2.schedule(pods[333:], synth.T0)
+    assert np.array_equal(a, np.concatenate([b1, b2]))
+
+
+def test_schedule_unschedulable_pods(gpu):
+    """Pods that fit nowhere come back -1 and do not change any node."""
+    cl = synth.make_cluster(64, synth.BASE_SEED + 51)
+    ev, o = both(synth.config(64), cl)
+    huge = model.make_pod(requests={"cpu": "100000", "memory": "1Ti"}, limits={"cpu": "100000", "memory": "1Ti"})
+    pods = synth.make_pods(40, synth.BASE_SEED + 52)
+    seq = [huge] + [pods[i] for i in range(20)] + [huge] + [pods[i] for i in range(20, 40)]
+    seq_arr = np.concatenate([np.frombuffer(bytes(p), dtype=abi.POD_DTYPE) if isinstance(p, abi.Pod) else p[None]
+                              for p in seq])
+    c1, s1 = ev.schedule(seq_arr, synth.T0)
+    c0, s0 = o.schedule(seq_arr, synth.T0)
+    assert c1[0] == -1 and c1[21] == -1
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+
+
+def test_schedule_large_cluster_prefix(gpu):
+    """BASELINE config 3 cluster (50k nodes): first 400 pods vs the oracle, bit-exact."""
+    cl = synth.make_cluster(50_000, synth.BASE_SEED + 3)
+    pods = synth.make_pods(400, synth.BASE_SEED + 103)
+    ev, o = both(synth.config(50_000), cl)
+    c1, s1 = ev.schedule(pods, synth.T0)
+    c0, s0 = o.schedule(pods, synth.T0)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
