@@ -698,7 +698,7 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
   if (rc) return rc;
   const int64_t N = ctx->n_nodes, P = n_pods, M = N * P;
   // parity buffers: status u8, reason u8, la i16, numa i16, total i16 = 8 B per pair
-  rc = ensure(&d->d_parity, &d->parity_cap, std::max<int64_t>(M, 1) * 8);
+  rc = ensure(&d->d_parity, &d->parity_cap, std::max<int64_t>(M, 1) * 8 + 16);
   if (rc) return rc;
   rc = ensure((void**)&d->d_best, &d->best_cap, sizeof(uint32_t) * P);
   if (rc) return rc;
