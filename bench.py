@@ -107,7 +107,7 @@ def main():
     ev.eval(pods[:0], synth.T0)  # derive + upload every node row: state resident in HBM
     ev.set_profiling(8)
     torch.cuda.synchronize()
-    lat, evm, sel, res, samples = [], [], [], [], 0
+    lat, evm, sel, res, samples, rsplit = [], [], [], [], 0, []
     placed = 0
     t0 = time.perf_counter()
     for s in range(K):
@@ -120,6 +120,7 @@ def main():
         sel.append(ks["select_ms"] * ks["samples"])
         res.append(ks["resolve_ms"] * ks["samples"])
         samples += ks["samples"]
+        rsplit.append((ks["resolve_prologue_ms"], ks["resolve_replay_ms"]))
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     evals = K * slice_len * N
@@ -145,7 +146,8 @@ def main():
         "p50_pod_latency_ms": float(np.percentile(lat, 50)) if lat else None,
         "pods_placed": placed,
         "kernel_ms": {"eval": eval_ms, "select": sum(sel) / max(samples, 1), "resolve": sum(res) / max(samples, 1),
-                      "samples": samples},
+                      "resolve_prologue": float(np.mean([x[0] for x in rsplit])),
+                      "resolve_replay": float(np.mean([x[1] for x in rsplit])), "samples": samples},
         "roofline": {"bound": "hbm", "kernel": "k_eval_batch", "achieved": by / eval_ms / 1e6 if eval_ms else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (by / eval_ms / 1e6 / HBM_PEAK_GBS) if eval_ms else None, "traffic": None,

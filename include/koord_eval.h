@@ -319,6 +319,12 @@ int ke_last_schedule_stats(ke_ctx* ctx, double* total_ms, int32_t* n_batches,
  * the eval / select / resolve kernels over the sampled batches of the last ke_schedule. */
 int ke_set_profiling(ke_ctx* ctx, int32_t sample_every);
 int ke_last_kernel_stats(ke_ctx* ctx, double* eval_ms, double* select_ms, double* resolve_ms, int32_t* samples);
+/* Resolve kernel split of the last ke_schedule (in-kernel s_memrealtime stamps, every batch):
+ * average ms per batch of candidate/row staging (prologue) and of the sequential replay. */
+int ke_last_resolve_split(ke_ctx* ctx, double* prologue_ms, double* replay_ms);
+/* Finer split (6 entries, ms per batch): init, candidate copy, slot hashing, slot lookup, row
+ * gather, sequential replay. */
+int ke_debug_resolve_phases(ke_ctx* ctx, double* phases6);
 /* Launch the batch eval kernel `iters` times back to back over the current node SoA for `n_pods`
  * (<= 64) pods and return the HIP-event average milliseconds per launch (roofline measurement). */
 int ke_bench_eval_kernel(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int32_t iters,

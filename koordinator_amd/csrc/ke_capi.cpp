@@ -295,6 +295,19 @@ int ke_last_kernel_stats(ke_ctx* ctx, double* eval_ms, double* select_ms, double
   return KE_OK;
 }
 
+int ke_last_resolve_split(ke_ctx* ctx, double* prologue_ms, double* replay_ms) {
+  if (!ctx) return fail(KE_ERR_INVALID, "null context");
+  if (prologue_ms) *prologue_ms = ctx->c.kstat_resolve_prologue_ms;
+  if (replay_ms) *replay_ms = ctx->c.kstat_resolve_loop_ms;
+  return KE_OK;
+}
+
+int ke_debug_resolve_phases(ke_ctx* ctx, double* phases6) {
+  if (!ctx || !phases6) return fail(KE_ERR_INVALID, "ke_debug_resolve_phases arguments");
+  for (int i = 0; i < 6; i++) phases6[i] = ctx->c.kstat_resolve_phase_ms[i];
+  return KE_OK;
+}
+
 int ke_bench_eval_kernel(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int32_t iters,
                          double* avg_ms) {
   if (!ctx || !avg_ms) return fail(KE_ERR_INVALID, "ke_bench_eval_kernel arguments");

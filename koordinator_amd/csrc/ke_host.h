@@ -45,6 +45,8 @@ struct Context {
   double last_total_ms = 0.0;
   std::vector<double> last_batch_ms;
   double kstat_eval_ms = 0, kstat_select_ms = 0, kstat_resolve_ms = 0;
+  double kstat_resolve_prologue_ms = 0, kstat_resolve_loop_ms = 0;
+  double kstat_resolve_phase_ms[6] = {0, 0, 0, 0, 0, 0};
   int32_t kstat_samples = 0;
 };
 

@@ -49,7 +49,7 @@ struct SoA {
 struct NodeRegs {
   int64_t ut, fh[2][2], sa[2][2], cap[2], nalloc[2], nreq[2], csm, csaf, csas;
   uint32_t flags;
-  double rcap[2], ralloc[2];  // reciprocals for the exact score divisions
+  float rcap[2], ralloc[2];  // approximate reciprocals: estimates for the exact score divisions
 };
 
 __device__ __forceinline__ void load_row(const SoA& s, int64_t i, NodeRegs& r) {
@@ -75,18 +75,22 @@ __device__ __forceinline__ void load_row(const SoA& s, int64_t i, NodeRegs& r) {
   r.flags = s.flags[i];
 }
 
+__device__ __forceinline__ float i64_to_f32(int64_t x) {  // ~2 roundings, only feeds an estimate
+  return (float)(int32_t)(x >> 32) * 4294967296.0f + (float)(uint32_t)x;
+}
+
 __device__ __forceinline__ void prepare_row(NodeRegs& r) {
 #pragma unroll
   for (int q = 0; q < 2; q++) {
-    r.rcap[q] = r.cap[q] > 0 ? 1.0 / (double)r.cap[q] : 0.0;
-    r.ralloc[q] = r.nalloc[q] > 0 ? 1.0 / (double)r.nalloc[q] : 0.0;
+    r.rcap[q] = __builtin_amdgcn_rcpf(i64_to_f32(r.cap[q]));
+    r.ralloc[q] = __builtin_amdgcn_rcpf(i64_to_f32(r.nalloc[q]));
   }
 }
 
-// floor(num / den) for num >= 0, den > 0: double estimate from a reciprocal, then exact integer
-// correction (the estimate is within +-1 for the operand ranges of a scheduler score).
-__device__ __forceinline__ int64_t div_exact(int64_t num, int64_t den, double rden) {
-  int64_t q = (int64_t)((double)num * rden);
+// floor(num / den), num >= 0, den > 0, any magnitude: slow exact path (double estimate + integer
+// remainder correction), only reached for operands outside the fast path's range.
+__device__ __noinline__ int64_t div_exact_slow(int64_t num, int64_t den) {
+  int64_t q = (int64_t)((double)num / (double)den);
   int64_t rem = num - q * den;
   while (rem < 0) {
     q--;
@@ -96,6 +100,26 @@ __device__ __forceinline__ int64_t div_exact(int64_t num, int64_t den, double rd
     q++;
     rem -= den;
   }
+  return q;
+}
+
+// floor(x * 100 / c) for c > 0 — the framework.MaxNodeScore scaling of every least/most scorer.
+// Fast path (0 <= x <= 16c, i.e. a result <= 1600): f32 estimate from the node's reciprocal, off by at
+// most one (relative error < 2^-21), then one exact int64 correction in each direction.
+__device__ __forceinline__ int32_t div100(int64_t x, int64_t c, float rc) {
+  const int64_t x100 = x * 100;
+  if (x < 0 || x > 16 * c) return (int32_t)div_exact_slow(x100, c);
+  int32_t q = (int32_t)(i64_to_f32(x100) * rc);
+  q -= (int32_t)((int64_t)q * c > x100);
+  q += (int32_t)((int64_t)(q + 1) * c <= x100);
+  return q;
+}
+
+// floor(s / d) for 0 <= s < 2^22, d > 0 (weighted means of per-resource scores)
+__device__ __forceinline__ int32_t div_small(int32_t s, int32_t d) {
+  int32_t q = (int32_t)((float)s * __builtin_amdgcn_rcpf((float)d));
+  q -= (int32_t)(q * d > s);
+  q += (int32_t)((q + 1) * d <= s);
   return q;
 }
 
@@ -134,7 +158,8 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
       const int v = ((nf & NF_HAS_PROD_THR) && (p.flags & PF_PROD)) ? 1 : 0;
 #pragma unroll
       for (int q = 0; q < 2; q++) {
-        if (o.status == KE_CODE_SUCCESS && (nf & nf_fh_on(v, q)) && p.est[q] > n.fh[v][q]) {
+        const int64_t fh = v ? n.fh[1][q] : n.fh[0][q];  // select, not a runtime index (no scratch)
+        if (o.status == KE_CODE_SUCCESS && (nf & nf_fh_on(v, q)) && p.est[q] > fh) {
           o.status = KE_CODE_UNSCHEDULABLE;
           const bool agg = v == 0 && (nf & NF_FILTER_AGG);
           o.reason = (uint8_t)(agg ? KE_REASON_LA_AGG_USAGE_CPU + q : KE_REASON_LA_USAGE_CPU + q);
@@ -173,12 +198,11 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
 #pragma unroll
     for (int q = 0; q < 2; q++) {
       const int64_t cap = n.cap[q];
-      const int64_t room = n.sa[v][q] - p.est[q];  // cap - used
-      int32_t sc = 0;
-      if (cap != 0 && room >= 0) sc = (int32_t)div_exact(room * 100, cap, n.rcap[q]);
+      const int64_t room = (v ? n.sa[1][q] : n.sa[0][q]) - p.est[q];  // cap - used
+      const int32_t sc = (cap > 0 && room >= 0) ? div100(room, cap, n.rcap[q]) : 0;  // leastUsedScore
       s += sc * k.w_la[q];
     }
-    la = (int32_t)((uint32_t)s / (uint32_t)k.wsum_la);
+    la = div_small(s, k.wsum_la);
   }
   // ---- NodeNUMAResource.Score  scoring.go:66-139,210-249
   int32_t nu = 0;
@@ -198,16 +222,16 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
         if (w == 0 || alloc == 0) continue;
         const int64_t req = (q == 0 ? reqc : n.nreq[1]) + p.req[q];
         int32_t sc;
-        if (k.flags & AF_NUMA_MOST) {
+        if (k.flags & AF_NUMA_MOST) {  // mostRequestedScore  most_allocated.go:53-62
           const int64_t rq = req > alloc ? alloc : req;
-          sc = (int32_t)div_exact(rq * 100, alloc, n.ralloc[q]);
-        } else {
-          sc = req > alloc ? 0 : (int32_t)div_exact((alloc - req) * 100, alloc, n.ralloc[q]);
+          sc = alloc > 0 ? div100(rq, alloc, n.ralloc[q]) : (int32_t)((rq * 100) / alloc);
+        } else {  // leastRequestedScore  least_allocated.go:49-58
+          sc = req > alloc ? 0 : (alloc > 0 ? div100(alloc - req, alloc, n.ralloc[q]) : (int32_t)(((alloc - req) * 100) / alloc));
         }
         s += sc * w;
         ws += w;
       }
-      nu = ws > 0 ? (int32_t)((uint32_t)s / (uint32_t)ws) : 0;
+      nu = ws > 0 ? div_small(s, ws) : 0;
     }
   }
   o.la = (int16_t)la;
@@ -293,96 +317,212 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int n_nodes, c
   }
 }
 
-__device__ __forceinline__ int wave_popc(bool pred) { return __popcll(__ballot(pred)); }
+// ---- wave-wide primitives (DPP reductions from the device library, ballots) ---------------------
+extern "C" __device__ uint32_t __ockl_wfred_max_u32(uint32_t);
+extern "C" __device__ int32_t __ockl_wfred_add_i32(int32_t);
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) { return __ockl_wfred_max_u32(v); }
+__device__ __forceinline__ int wave_sum(int v) { return __ockl_wfred_add_i32(v); }
+__device__ __forceinline__ int lanes_below(uint64_t m) {  // popcount of m over lanes < this lane
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+// exclusive prefix over lanes of a small per-lane count c (0 <= c < 16) and the wave total
+__device__ __forceinline__ int lane_prefix16(int c, int* total) {
+  int pre = 0, tot = 0;
+#pragma unroll
+  for (int b = 0; b < 4; b++) {
+    const uint64_t m = __ballot((c >> b) & 1);
+    pre += lanes_below(m) << b;
+    tot += __popcll(m) << b;
+  }
+  *total = tot;
+  return pre;
+}
 
-// exact top-k_j per pod, k_j = min(j+1, KMAX), ordered by (score desc, node index asc)
+// 8 consecutive 9-bit scores of one pod starting at node i (i % 8 == 0), 0 beyond `end`
+__device__ __forceinline__ void load8(const uint16_t* sc, int i, int end, uint32_t v[8]) {
+  if (i + 8 <= end) {
+    const uint4 q = *reinterpret_cast<const uint4*>(sc + i);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      v[2 * t] = w[t] & 0xFFFFu;
+      v[2 * t + 1] = w[t] >> 16;
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 8; t++) v[t] = i + t < end ? sc[i + t] : 0u;
+  }
+}
+
+constexpr int SEL_WINDOW = 64;  // histogram window below the pod's best score
+
+// Exact top-k_j per pod, k_j = min(j+1, KMAX), in (score desc, node index asc) order.  One
+// workgroup per pod; each wave owns a contiguous node segment read 16 B per lane (8 scores).
+//   pass 1: best score M and the feasible count (DPP reductions)
+//   pass 2: per-wave histogram of the 64 scores below M in LDS -> threshold score and, per wave, the
+//           number of ties before it in node order (a generic binary search covers the rare case
+//           of fewer than k feasible nodes inside the window)
+//   pass 3: select score > thr, and the first need_ties nodes with score == thr by node index.
 __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restrict__ scores, int64_t score_stride,
                                                          int n_nodes, uint32_t* __restrict__ cand,
                                                          int32_t* __restrict__ cand_cnt) {
-  __shared__ int32_t s_cnt[SELECT_WAVES];
+  __shared__ int32_t s_hist[SELECT_WAVES][SEL_WINDOW];
+  __shared__ int32_t s_red[2][SELECT_WAVES];
+  __shared__ int32_t s_thr[2];
   __shared__ int32_t s_tie[SELECT_WAVES];
   __shared__ int32_t s_out;
   const int j = blockIdx.x;
   const int k = min(j + 1, KMAX);
   const uint16_t* sc = scores + (int64_t)j * score_stride;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int seg = ((n_nodes + SELECT_WAVES - 1) / SELECT_WAVES + 63) & ~63;
+  const int seg = ((n_nodes + SELECT_WAVES - 1) / SELECT_WAVES + 511) & ~511;
   const int w0 = wave * seg;
   const int w1 = min(n_nodes, w0 + seg);
-
-  auto count_ge = [&](int t) -> int {
-    int c = 0;
-    for (int b = w0; b < w1; b += 64) {
-      const int i = b + lane;
-      const int v = i < w1 ? sc[i] : 0;
-      c += wave_popc(v >= t);
-    }
-    if (lane == 0) s_cnt[wave] = c;
-    __syncthreads();
-    int tot = 0;
-#pragma unroll
-    for (int w = 0; w < SELECT_WAVES; w++) tot += s_cnt[w];
-    __syncthreads();
-    return tot;
-  };
-
-  const int feasible = count_ge(1);
-  int thr, need_ties;  // select all v > thr, plus the first `need_ties` with v == thr
-  if (feasible <= k) {
-    thr = 0;  // everything feasible, no tie selection at 0 (score 0 = filtered out)
-    need_ties = 0;
-  } else {
-    int lo = 1, hi = 512, cnt_hi = 0;  // count(>=lo) >= k > count(>=hi)
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      const int c = count_ge(mid);
-      if (c >= k) lo = mid;
-      else {
-        hi = mid;
-        cnt_hi = c;
-      }
-    }
-    thr = lo;
-    need_ties = k - cnt_hi;
-  }
-  // per-wave tie counts -> exclusive prefix over waves (index order)
-  int ties = 0;
-  if (need_ties > 0) {
-    for (int b = w0; b < w1; b += 64) {
-      const int i = b + lane;
-      const int v = i < w1 ? sc[i] : 0;
-      ties += wave_popc(v == thr);
-    }
-  }
-  if (lane == 0) s_tie[wave] = ties;
+  reinterpret_cast<int32_t*>(s_hist)[threadIdx.x] = 0;  // SELECT_WAVES * SEL_WINDOW == SELECT_BLOCK
   if (threadIdx.x == 0) s_out = 0;
-  __syncthreads();
-  int tie_base = 0;
-  for (int w = 0; w < wave; w++) tie_base += s_tie[w];
-  uint32_t* out = cand + (int64_t)j * KMAX;
-  int running = tie_base;
-  for (int b = w0; b < w1; b += 64) {
-    const int i = b + lane;
-    const int v = i < w1 ? sc[i] : 0;
-    bool sel = v > thr;
-    const bool tie = need_ties > 0 && v == thr && v > 0;
-    const uint64_t tmask = __ballot(tie);
-    if (tie) {
-      const int rank = running + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(tmask >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)tmask, 0));
-      sel = rank < need_ties;
+
+  // pass 1
+  uint32_t mx = 0;
+  int feas = 0;
+  for (int b = w0; b < w1; b += 512) {
+    uint32_t v[8];
+    load8(sc, b + lane * 8, w1, v);
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+      mx = max(mx, v[t]);
+      feas += v[t] > 0;
     }
-    running += __popcll(tmask);
-    const uint64_t smask = __ballot(sel);
-    if (smask) {
-      int wbase = 0;
-      if (lane == 0) wbase = atomicAdd(&s_out, __popcll(smask));
-      wbase = __shfl(wbase, 0, 64);
-      if (sel) {
-        const int pos = wbase + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(smask >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)smask, 0));
-        out[pos] = ((uint32_t)v << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)i);
+  }
+  mx = wave_max_u32(mx);
+  feas = wave_sum(feas);
+  if (lane == 0) {
+    s_red[0][wave] = (int)mx;
+    s_red[1][wave] = feas;
+  }
+  __syncthreads();
+  int M = 0, F = 0;
+#pragma unroll
+  for (int w = 0; w < SELECT_WAVES; w++) {
+    M = max(M, s_red[0][w]);
+    F += s_red[1][w];
+  }
+  int thr = 0, need_ties = 0;  // select v > thr, plus the first need_ties with v == thr
+  if (F > k) {
+    // pass 2: per-wave histogram of scores in (M - 64, M]
+    for (int b = w0; b < w1; b += 512) {
+      uint32_t v[8];
+      load8(sc, b + lane * 8, w1, v);
+#pragma unroll
+      for (int t = 0; t < 8; t++) {
+        const int d = M - (int)v[t];
+        if (v[t] > 0 && d < SEL_WINDOW) atomicAdd(&s_hist[wave][d], 1);
       }
+    }
+    __syncthreads();
+    if (wave == 0) {  // cumulative count from the top, lane d = window bin
+      int c = 0;
+#pragma unroll
+      for (int w = 0; w < SELECT_WAVES; w++) c += s_hist[w][lane];
+      int cum = c;  // inclusive prefix over lanes
+      for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(cum, off, 64);
+        if (lane >= off) cum += o;
+      }
+      const uint64_t reach = __ballot(cum >= k);
+      if (reach) {
+        const int d = __ffsll((unsigned long long)reach) - 1;
+        const int above = __shfl(cum - c, d, 64);
+        if (lane == 0) {
+          s_thr[0] = M - d;
+          s_thr[1] = k - above;
+        }
+      } else if (lane == 0) {
+        s_thr[0] = -1;  // fewer than k feasible nodes inside the window
+      }
+    }
+    __syncthreads();
+    thr = s_thr[0];
+    need_ties = s_thr[1];
+    if (thr < 0) {
+      // generic threshold search over [1, M - 64]: count(v >= lo) >= k > count(v >= hi)
+      auto count_ge = [&](int t) -> int {
+        int c = 0;
+        for (int b = w0; b < w1; b += 512) {
+          uint32_t v[8];
+          load8(sc, b + lane * 8, w1, v);
+#pragma unroll
+          for (int q = 0; q < 8; q++) c += v[q] >= (uint32_t)t;
+        }
+        c = wave_sum(c);
+        __syncthreads();
+        if (lane == 0) s_red[1][wave] = c;
+        __syncthreads();
+        int tot = 0;
+#pragma unroll
+        for (int w = 0; w < SELECT_WAVES; w++) tot += s_red[1][w];
+        return tot;
+      };
+      int lo = 1, hi = M - SEL_WINDOW + 1, cnt_hi = count_ge(hi);
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        const int c = count_ge(mid);
+        if (c >= k) lo = mid;
+        else {
+          hi = mid;
+          cnt_hi = c;
+        }
+      }
+      thr = lo;
+      need_ties = k - cnt_hi;
+      int ties = 0;
+      for (int b = w0; b < w1; b += 512) {
+        uint32_t v[8];
+        load8(sc, b + lane * 8, w1, v);
+#pragma unroll
+        for (int q = 0; q < 8; q++) ties += v[q] == (uint32_t)thr;
+      }
+      ties = wave_sum(ties);
+      if (lane == 0) s_tie[wave] = ties;
+    } else if (lane == 0) {
+      s_tie[wave] = s_hist[wave][M - thr];
+    }
+    __syncthreads();
+  }
+  // pass 3: select
+  int running = 0;  // ties of this wave before the current row
+  for (int w = 0; w < wave; w++) running += need_ties > 0 ? s_tie[w] : 0;
+  uint32_t* out = cand + (int64_t)j * KMAX;
+  for (int b = w0; b < w1; b += 512) {
+    const int i0 = b + lane * 8;
+    uint32_t v[8];
+    load8(sc, i0, w1, v);
+    int nt = 0;
+#pragma unroll
+    for (int t = 0; t < 8; t++) nt += (need_ties > 0 && v[t] == (uint32_t)thr && v[t] > 0);
+    int tie_tot;
+    int rank = running + lane_prefix16(nt, &tie_tot);
+    running += tie_tot;
+    uint32_t selm = 0;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+      bool sel = v[t] > (uint32_t)thr;
+      if (need_ties > 0 && v[t] == (uint32_t)thr && v[t] > 0) {
+        sel = rank < need_ties;
+        rank++;
+      }
+      selm |= (uint32_t)sel << t;
+    }
+    const int ns = __popc(selm);
+    int sel_tot;
+    const int pre = lane_prefix16(ns, &sel_tot);
+    if (sel_tot) {
+      int wbase = 0;
+      if (lane == 0) wbase = atomicAdd(&s_out, sel_tot);
+      wbase = __shfl(wbase, 0, 64);
+      int pos = wbase + pre;
+#pragma unroll
+      for (int t = 0; t < 8; t++)
+        if (selm & (1u << t)) out[pos++] = (v[t] << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)(i0 + t));
     }
   }
   __syncthreads();
@@ -417,132 +557,240 @@ __device__ __forceinline__ void regs_from_lds(const LdsRow& r, NodeRegs& n) {
   n.flags = r.flags;
 }
 
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-  for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off, 64));
-  return v;
+// LDS budget of the resolve workgroup (one wave, one CU): candidate keys + their row slots, a node
+// -> slot hash over every candidate, and the rows of the first RES_ROWS distinct candidates.
+constexpr int RES_ROWS = 448;                 // prefetched candidate rows
+constexpr int RES_OVF = MAX_BATCH;            // rows of chosen nodes that missed the prefetch
+constexpr int RES_SLOTS = RES_ROWS + RES_OVF;
+constexpr int HASH_SLOTS = 2 * MAX_BATCH * KMAX;  // load factor <= 1/2
+constexpr int HASH_EMPTY = -1;
+constexpr int RES_THREADS = 256;  // prologue width; the replay runs on wave 0 alone
+
+// Ordering point for LDS traffic between the lanes of ONE wavefront: LDS instructions of a wave
+// execute in issue order, so only the compiler must be kept from moving accesses across it
+// (a workgroup __syncthreads would also drain outstanding global stores).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
 }
 
-constexpr int HASH_SLOTS = 256;
+__device__ __forceinline__ int hash_of(int node) { return (int)(((uint32_t)node * 0x9E3779B1u) >> 19) & (HASH_SLOTS - 1); }
 
-__global__ __launch_bounds__(64) void k_resolve(SoA s, const DevPod* __restrict__ pods, int32_t* __restrict__ batch_base,
+__global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __restrict__ pods, int32_t* __restrict__ batch_base,
                                                 int batch_pods, KArgs k, const uint32_t* __restrict__ cand,
                                                 const int32_t* __restrict__ cand_cnt, int32_t* __restrict__ chosen,
                                                 int32_t* __restrict__ chosen_score, int32_t global_offset,
-                                                uint64_t* __restrict__ stamps, int batch_index) {
+                                                uint64_t* __restrict__ stamps, uint64_t* __restrict__ pstamps,
+                                                int batch_index) {
+  const int tid = threadIdx.x;
+  if (tid == 0) pstamps[8 * batch_index] = __builtin_amdgcn_s_memrealtime();
   __shared__ uint32_t s_cand[MAX_BATCH * KMAX];
-  __shared__ LdsRow s_chg[MAX_BATCH];
-  __shared__ LdsRow s_pref[MAX_BATCH];
-  __shared__ int32_t s_pref_node[MAX_BATCH];
-  __shared__ int32_t s_chg_node[MAX_BATCH];
-  __shared__ int32_t s_hash_key[HASH_SLOTS];
-  __shared__ int32_t s_hash_val[HASH_SLOTS];
+  __shared__ int16_t s_cand_slot[MAX_BATCH * KMAX];
+  __shared__ int32_t s_hkey[HASH_SLOTS];
+  __shared__ int16_t s_hval[HASH_SLOTS];
+  __shared__ LdsRow s_row[RES_SLOTS];
+  __shared__ int32_t s_slot_node[RES_SLOTS];
+  __shared__ uint8_t s_changed[RES_SLOTS];
   __shared__ DevPod s_pod[MAX_BATCH];
-  const int lane = threadIdx.x;
+  __shared__ int32_t s_cnt[MAX_BATCH];
+  __shared__ int32_t s_out[2][MAX_BATCH];
+  __shared__ int32_t s_nslots;
+  const int lane = tid & 63;
   const int base = *batch_base;
   const int B = batch_pods;
 
-  for (int t = lane; t < B * KMAX; t += 64) {
-    const int j = t / KMAX, c = t % KMAX;
-    s_cand[t] = c < cand_cnt[j] ? cand[t] : 0u;
+  // ---- prologue (all RES_THREADS threads): candidates, distinct-node slots, row prefetch ----
+  if (tid < B) {
+    s_cnt[tid] = cand_cnt[tid];
+    s_pod[tid] = pods[base + tid];
   }
-  for (int t = lane; t < HASH_SLOTS; t += 64) s_hash_key[t] = -1;
-  if (lane < B) s_pod[lane] = pods[base + lane];
+  for (int t = tid; t < HASH_SLOTS; t += RES_THREADS) s_hkey[t] = HASH_EMPTY;
+  for (int t = tid; t < RES_SLOTS; t += RES_THREADS) s_changed[t] = 0;
+  if (tid == 0) s_nslots = 0;
   __syncthreads();
-  // prefetch the row of each pod's best candidate (the most likely choice)
-  if (lane < B) {
-    uint32_t best = 0;
-    for (int c = 0; c < KMAX; c++) best = max(best, s_cand[lane * KMAX + c]);
-    const int node = best ? key_node(best) : -1;
-    s_pref_node[lane] = node;
-    if (node >= 0) {
+  if (tid == 0) pstamps[8 * batch_index + 1] = __builtin_amdgcn_s_memrealtime();
+  // candidate keys -> LDS: 16-byte loads, all issued before any use
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(cand);
+    uint4* dst = reinterpret_cast<uint4*>(s_cand);
+    const int n4 = B * KMAX / 4;
+    constexpr int U = MAX_BATCH * KMAX / 4 / RES_THREADS;
+    uint4 q[U];
 #pragma unroll
-      for (int f = 0; f < NUM_I64_FIELDS; f++) s_pref[lane].f[f] = s.f[f * s.stride + node];
-      s_pref[lane].flags = s.flags[node];
+    for (int u = 0; u < U; u++) q[u] = src[min(u * RES_THREADS + tid, n4 - 1)];  // unconditional
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int t = u * RES_THREADS + tid;
+      if (t < n4) {
+        const int j = (t * 4) / KMAX, c = (t * 4) % KMAX, cnt = s_cnt[j];
+        q[u].x = c + 0 < cnt ? q[u].x : 0u;
+        q[u].y = c + 1 < cnt ? q[u].y : 0u;
+        q[u].z = c + 2 < cnt ? q[u].z : 0u;
+        q[u].w = c + 3 < cnt ? q[u].w : 0u;
+        dst[t] = q[u];
+      }
     }
   }
   __syncthreads();
-
-  int n_chg = 0;
-  for (int j = 0; j < B; j++) {
-    const DevPod pod = s_pod[j];
-    // best snapshot candidate not changed earlier in this batch
-    const uint32_t ck = s_cand[j * KMAX + lane];
-    bool in_chg = false;
-    if (ck) {
-      const int node = key_node(ck);
-      int h = (node * 0x9E3779B1u) >> 24;
+  if (tid == 0) pstamps[8 * batch_index + 2] = __builtin_amdgcn_s_memrealtime();
+  for (int t = tid; t < B * KMAX; t += RES_THREADS) {
+    const uint32_t key = s_cand[t];
+    if (key) {  // insert the node; the first inserter of a node draws its row slot
+      const int node = key_node(key);
+      int h = hash_of(node);
       while (true) {
-        const int kk = s_hash_key[h];
-        if (kk < 0) break;
-        if (kk == node) {
-          in_chg = true;
+        const int prev = atomicCAS(&s_hkey[h], HASH_EMPTY, node);
+        if (prev == HASH_EMPTY) {
+          const int sl = atomicAdd(&s_nslots, 1);
+          s_hval[h] = (int16_t)(sl < RES_ROWS ? sl : -1);
+          if (sl < RES_ROWS) s_slot_node[sl] = node;
           break;
         }
+        if (prev == node) break;
         h = (h + 1) & (HASH_SLOTS - 1);
       }
     }
-    const uint32_t bu = wave_max_u32(in_chg ? 0u : ck);
-    // exact re-evaluation of the changed nodes against their patched rows
-    uint32_t kc = 0;
-    if (lane < n_chg) {
-      NodeRegs n;
-      regs_from_lds(s_chg[lane], n);
-      prepare_row(n);
-      const EvalOut o = eval_pair<false>(n, node_expired(n, k), pod, k);
-      kc = make_key(o.total, s_chg_node[lane]);
+  }
+  __syncthreads();
+  if (tid == 0) pstamps[8 * batch_index + 3] = __builtin_amdgcn_s_memrealtime();
+  const int n_pref = min(s_nslots, RES_ROWS);
+  for (int t = tid; t < B * KMAX; t += RES_THREADS) {  // candidate -> row slot
+    const uint32_t key = s_cand[t];
+    int16_t sl = -1;
+    if (key) {
+      const int node = key_node(key);
+      int h = hash_of(node);
+      while (s_hkey[h] != node) h = (h + 1) & (HASH_SLOTS - 1);
+      sl = s_hval[h];
     }
+    s_cand_slot[t] = sl;
+  }
+  if (tid == 0) pstamps[8 * batch_index + 5] = __builtin_amdgcn_s_memrealtime();
+  if (n_pref > 0) {  // rows of the distinct candidates: unconditional (clamped) gathers, 8 in flight
+    constexpr int W = NUM_I64_FIELDS + 1;
+    const int total = n_pref * W;
+    for (int t0 = 0; t0 < total; t0 += RES_THREADS * 8) {
+      int64_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int t = min(t0 + u * RES_THREADS + tid, total - 1);
+        const int sl = t / W, f = t % W;
+        const int node = s_slot_node[sl];
+        const int64_t a = s.f[(int64_t)min(f, NUM_I64_FIELDS - 1) * s.stride + node];
+        const uint32_t fl = s.flags[node];
+        v[u] = f < NUM_I64_FIELDS ? a : (int64_t)fl;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int t = t0 + u * RES_THREADS + tid;
+        if (t < total) {
+          const int sl = t / W, f = t % W;
+          if (f < NUM_I64_FIELDS) s_row[sl].f[f] = v[u];
+          else s_row[sl].flags = (uint32_t)v[u];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) pstamps[8 * batch_index + 4] = __builtin_amdgcn_s_memrealtime();
+  if (tid >= 64) return;  // the replay is one wavefront: wave-level ordering only from here on
+
+  // ---- sequential replay of the batch ----
+  // Lane c owns the c-th node changed in this batch: its row lives in that lane's registers, so the
+  // per-pod re-evaluation of every changed node is one register-only eval across the lanes.
+  int n_chg = 0, n_ovf = 0;
+  NodeRegs mine;
+  int my_node = -1;
+  bool my_expired = false;
+  for (int j = 0; j < B; j++) {
+    const DevPod pod = s_pod[j];
+    const uint32_t ck = s_cand[j * KMAX + lane];
+    int csl = s_cand_slot[j * KMAX + lane];
+    if (ck && csl < 0) {  // not prefetched: it has a row only if an earlier pod chose it (overflow slot)
+      const int node = key_node(ck);
+      int h = hash_of(node);
+      while (s_hkey[h] != node) h = (h + 1) & (HASH_SLOTS - 1);
+      csl = s_hval[h];
+    }
+    const bool in_chg = ck && csl >= 0 && s_changed[csl];
+    const uint32_t bu = wave_max_u32(in_chg ? 0u : ck);  // best unchanged snapshot candidate
+    uint32_t kc = 0;  // exact re-evaluation of the nodes changed earlier in this batch
+    if (lane < n_chg) kc = make_key(eval_pair<false>(mine, my_expired, pod, k).total, my_node);
     const uint32_t bc = wave_max_u32(kc);
     const uint32_t w = max(bu, bc);
-    int slot = -1;
     if (w != 0) {
-      const int node = key_node(w);
+      int owner;
       if (w == bc) {
-        const uint64_t m = __ballot(kc == w && lane < n_chg);
-        slot = __ffsll((unsigned long long)m) - 1;
+        owner = __ffsll((unsigned long long)__ballot(lane < n_chg && kc == w)) - 1;
       } else {
-        slot = n_chg;
-        if (lane == 0) s_chg_node[slot] = node;
-        if (s_pref_node[j] == node) {
-          if (lane < NUM_I64_FIELDS) s_chg[slot].f[lane] = s_pref[j].f[lane];
-          if (lane == 0) s_chg[slot].flags = s_pref[j].flags;
-        } else {
-          if (lane < NUM_I64_FIELDS) s_chg[slot].f[lane] = s.f[lane * s.stride + node];
-          if (lane == 0) s_chg[slot].flags = s.flags[node];
+        const int src = __ffsll((unsigned long long)__ballot(ck == w && !in_chg)) - 1;
+        int slot = __shfl(csl, src, 64);
+        const int node = key_node(w);
+        owner = n_chg++;
+        if (slot < 0) {  // chosen node missed the prefetch: overflow row from the SoA
+          slot = RES_ROWS + n_ovf++;
+          if (lane == owner) {
+            load_row(s, node, mine);
+            s_slot_node[slot] = node;
+            int h = hash_of(node);
+            while (s_hkey[h] != node) h = (h + 1) & (HASH_SLOTS - 1);
+            s_hval[h] = (int16_t)slot;
+          }
+        } else if (lane == owner) {
+          regs_from_lds(s_row[slot], mine);
         }
-        if (lane == 0) {
-          int h = (node * 0x9E3779B1u) >> 24;
-          while (s_hash_key[h] >= 0) h = (h + 1) & (HASH_SLOTS - 1);
-          s_hash_key[h] = node;
-          s_hash_val[h] = slot;
+        if (lane == owner) {
+          prepare_row(mine);
+          my_node = node;
+          my_expired = node_expired(mine, k);
+          s_changed[slot] = 1;
         }
-        n_chg++;
       }
-      __syncthreads();
       // Reserve: LoadAware assign (the new pod has no PodMetric -> counted at its estimate in every
       // non-prod term, and in the prod terms when it is prod), NodeInfo.Requested += requests.
-      if (lane == 0) {
-        LdsRow& r = s_chg[slot];
-        const int vmax = (r.flags & NF_HAS_METRIC) && !(r.flags & NF_NM_NIL) ? ((pod.flags & PF_PROD) ? 2 : 1) : 0;
-        for (int v = 0; v < vmax; v++)
+      if (lane == owner) {
+        if ((mine.flags & NF_HAS_METRIC) && !(mine.flags & NF_NM_NIL)) {
+#pragma unroll
           for (int q = 0; q < 2; q++) {
-            if (r.flags & nf_fh_on(v, q)) r.f[F_FH + 2 * v + q] -= pod.est[q];
-            r.f[F_SA + 2 * v + q] -= pod.est[q];
+            if (mine.flags & nf_fh_on(0, q)) mine.fh[0][q] -= pod.est[q];
+            mine.sa[0][q] -= pod.est[q];
+            if (pod.flags & PF_PROD) {
+              if (mine.flags & nf_fh_on(1, q)) mine.fh[1][q] -= pod.est[q];
+              mine.sa[1][q] -= pod.est[q];
+            }
           }
-        r.f[F_NREQ + 0] += pod.req[0];
-        r.f[F_NREQ + 1] += pod.req[1];
+        }
+        mine.nreq[0] += pod.req[0];
+        mine.nreq[1] += pod.req[1];
       }
+      if (lane == 0) {
+        s_out[0][j] = key_node(w) + global_offset;
+        s_out[1][j] = key_score(w);
+      }
+    } else if (lane == 0) {
+      s_out[0][j] = -1;
+      s_out[1][j] = -1;
     }
-    if (lane == 0) {
-      chosen[base + j] = w ? key_node(w) + global_offset : -1;
-      chosen_score[base + j] = w ? key_score(w) : -1;
-    }
-    __syncthreads();
+    wave_lds_sync();
+  }
+  if (lane < B) {
+    chosen[base + lane] = s_out[0][lane];
+    chosen_score[base + lane] = s_out[1][lane];
   }
   // write the patched rows back to the SoA
   if (lane < n_chg) {
-    const int node = s_chg_node[lane];
+    const int64_t st = s.stride;
+    int64_t* f = s.f + my_node;
 #pragma unroll
-    for (int f = 0; f < NUM_I64_FIELDS; f++) s.f[f * s.stride + node] = s_chg[lane].f[f];
+    for (int v = 0; v < 2; v++)
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        f[(F_FH + 2 * v + q) * st] = mine.fh[v][q];
+        f[(F_SA + 2 * v + q) * st] = mine.sa[v][q];
+      }
+    f[(F_NREQ + 0) * st] = mine.nreq[0];
+    f[(F_NREQ + 1) * st] = mine.nreq[1];
   }
   if (lane == 0) {
     *batch_base = base + B;
@@ -748,7 +996,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     if (d->d_stamps) HIP_OK(hipFree(d->d_stamps));
     HIP_OK(hipMalloc(&d->d_chosen, out_bytes));
     HIP_OK(hipMalloc(&d->d_chosen_score, out_bytes));
-    HIP_OK(hipMalloc(&d->d_stamps, sizeof(uint64_t) * ((int64_t)n_pods + 2)));
+    HIP_OK(hipMalloc(&d->d_stamps, sizeof(uint64_t) * 10 * ((int64_t)n_pods + 2)));
     d->out_cap = n_pods;
   }
   const KArgs k = make_kargs(ctx, now);
@@ -785,17 +1033,19 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       HIP_OK(hipMemsetAsync(d->d_cand_cnt, 0, sizeof(int32_t) * MAX_BATCH, d->stream));
     }
     if (prof) HIP_OK(hipEventRecord(pe[2], d->stream));
-    hipLaunchKernelGGL(k_resolve, dim3(1), dim3(64), 0, d->stream, d->soa, d->d_pods, d->d_batch_base, bp, k,
+    hipLaunchKernelGGL(k_resolve, dim3(1), dim3(RES_THREADS), 0, d->stream, d->soa, d->d_pods, d->d_batch_base, bp, k,
                        d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score, ctx->cfg.global_node_offset,
-                       d->d_stamps, b);
+                       d->d_stamps, d->d_stamps + (n_pods + 2), b);
     if (prof) HIP_OK(hipEventRecord(pe[3], d->stream));
   }
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(e1, d->stream));
   HIP_OK(hipMemcpyAsync(chosen, d->d_chosen, out_bytes, hipMemcpyDeviceToHost, d->stream));
   if (score) HIP_OK(hipMemcpyAsync(score, d->d_chosen_score, out_bytes, hipMemcpyDeviceToHost, d->stream));
-  std::vector<uint64_t> st((size_t)n_batches + 1);
+  std::vector<uint64_t> st((size_t)n_batches + 1), pst(8 * (size_t)n_batches);
   HIP_OK(hipMemcpyAsync(st.data(), d->d_stamps, sizeof(uint64_t) * (n_batches + 1), hipMemcpyDeviceToHost, d->stream));
+  HIP_OK(hipMemcpyAsync(pst.data(), d->d_stamps + (n_pods + 2), sizeof(uint64_t) * 8 * n_batches,
+                        hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipStreamSynchronize(d->stream));
   float ms = 0;
   HIP_OK(hipEventElapsedTime(&ms, e0, e1));
@@ -807,6 +1057,22 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   const double ms_per_tick = span > 0 ? ms / span : 1e-5;
   ctx->last_batch_ms.resize(n_batches);
   for (int b = 0; b < n_batches; b++) ctx->last_batch_ms[b] = (double)(st[b + 1] - st[b]) * ms_per_tick;
+  double pro = 0, loop = 0;  // resolve kernel: prologue (candidate/row staging) vs sequential replay
+  double ph[6] = {0, 0, 0, 0, 0, 0};  // init, cand copy, hash insert, slot lookup, row gather, replay
+  for (int b = 0; b < n_batches; b++) {
+    const uint64_t* p = &pst[8 * (size_t)b];
+    pro += (double)(p[4] - p[0]) * ms_per_tick;
+    loop += (double)(st[b + 1] - p[4]) * ms_per_tick;
+    ph[0] += (double)(p[1] - p[0]);
+    ph[1] += (double)(p[2] - p[1]);
+    ph[2] += (double)(p[3] - p[2]);
+    ph[3] += (double)(p[5] - p[3]);
+    ph[4] += (double)(p[4] - p[5]);
+    ph[5] += (double)(st[b + 1] - p[4]);
+  }
+  ctx->kstat_resolve_prologue_ms = pro / n_batches;
+  ctx->kstat_resolve_loop_ms = loop / n_batches;
+  for (int i = 0; i < 6; i++) ctx->kstat_resolve_phase_ms[i] = ph[i] * ms_per_tick / n_batches;
   ctx->kstat_samples = 0;
   ctx->kstat_eval_ms = ctx->kstat_select_ms = ctx->kstat_resolve_ms = 0;
   for (size_t s = 0; s + 3 < ev.size(); s += 4) {

@@ -157,7 +157,14 @@ class Evaluator:
         v = [C.c_double() for _ in range(3)]
         n = abi.i32()
         self._check(self.lib.ke_last_kernel_stats(self.h, *[C.byref(x) for x in v], C.byref(n)))
-        return {"eval_ms": v[0].value, "select_ms": v[1].value, "resolve_ms": v[2].value, "samples": n.value}
+        p, r = C.c_double(), C.c_double()
+        self._check(self.lib.ke_last_resolve_split(self.h, C.byref(p), C.byref(r)))
+        ph = np.zeros(6, np.float64)
+        self._check(self.lib.ke_debug_resolve_phases(self.h, abi.ptr(ph)))
+        return {"eval_ms": v[0].value, "select_ms": v[1].value, "resolve_ms": v[2].value, "samples": n.value,
+                "resolve_prologue_ms": p.value, "resolve_replay_ms": r.value,
+                "resolve_phases_ms": dict(zip(["init", "cand_copy", "hash", "lookup", "rows", "replay"],
+                                              ph.tolist()))}
 
     def bench_eval_kernel(self, pods, now_ns, iters):
         pods = as_pod_array(pods)
