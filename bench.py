@@ -34,7 +34,7 @@ def parse():
     ap.add_argument("--nodes", type=int, default=synth.CONFIGS[3]["nodes"])
     ap.add_argument("--pods", type=int, default=synth.CONFIGS[3]["pods"])
     ap.add_argument("--batch", type=int, default=64)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target host time of the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target host time of the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stream-nodes", type=int, default=4_000_000,
@@ -54,14 +54,14 @@ def cpu_baseline(cl, pods, cfg, seconds, threads):
     synth.load_into(o, cl)
     # calibrate on a small prefix, then time a prefix worth ~`seconds`
     t = time.perf_counter()
-    o.schedule(pods[:8], synth.T0, n_threads=threads)
-    per_pod = max((time.perf_counter() - t) / 8, 1e-6)
-    n = int(min(len(pods) - 8, max(16, seconds / per_pod)))
+    o.schedule(pods[:64], synth.T0, n_threads=threads)
+    per_pod = max((time.perf_counter() - t) / 64, 1e-6)
+    n = int(min(len(pods) - 64, max(16, seconds / per_pod)))
     t = time.perf_counter()
-    o.schedule(pods[8:8 + n], synth.T0, n_threads=threads)
+    o.schedule(pods[64:64 + n], synth.T0, n_threads=threads)
     dt = time.perf_counter() - t
     return {"value": n * cl.n_nodes / dt, "unit": "pod-node evals/s", "cores": threads, "kind": "port",
-            "sample": f"oracle (C restatement of the Go plugins) scheduling pods 8..{8 + n} of the same queue "
+            "sample": f"oracle (C restatement of the Go plugins) scheduling pods 64..{64 + n} of the same queue "
                       f"against all {cl.n_nodes} nodes, {threads} threads, {dt:.1f} s"}
 
 
@@ -82,21 +82,36 @@ def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if a.gpus != 1 or world != 1:
-        raise SystemExit("multi-GPU node sharding: run bench_multi (not in this build)")
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world:
+        raise SystemExit(f"--gpus {a.gpus} needs {a.gpus} ranks (torch.distributed.run --nproc-per-node {a.gpus}); "
+                         f"WORLD_SIZE={world}")
     import torch
+    import torch.distributed as dist
 
-    torch.cuda.set_device(0)
+    from koordinator_amd import shard
+
+    if world > 1:  # control plane only (RCCL id broadcast, barriers, max-over-ranks); data path = RCCL in libkoordeval
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local_rank)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
     N, P, K, W = a.nodes, a.pods, a.steps, a.warmup
     cl = synth.make_cluster(N, synth.BASE_SEED + 3)
     pods = synth.make_pods(P, synth.BASE_SEED + 103)
     cfg = synth.config(N, pod_batch=a.batch)
+    cfg.device_ordinal = local_rank
     slice_len = P // K
 
     # warmup on a throwaway context (same cluster, different pods) so the timed job starts pristine
     if W > 0:
         ew = Evaluator(cfg)
         synth.load_into(ew, cl)
+        shard.init_node_sharding(ew, rank, world)
         wp = synth.make_pods(W * slice_len, synth.BASE_SEED + 203)
         for w in range(W):
             ew.schedule(wp[w * slice_len:(w + 1) * slice_len], synth.T0)
@@ -104,11 +119,13 @@ def main():
 
     ev = Evaluator(cfg)
     synth.load_into(ev, cl)
+    shard.init_node_sharding(ev, rank, world)
+    lo, hi = ev.shard_range()
     ev.eval(pods[:0], synth.T0)  # derive + upload every node row: state resident in HBM
     ev.set_profiling(8)
-    torch.cuda.synchronize()
     lat, evm, sel, res, samples, rsplit = [], [], [], [], 0, []
     placed = 0
+    barrier()
     t0 = time.perf_counter()
     for s in range(K):
         chosen, _ = ev.schedule(pods[s * slice_len:(s + 1) * slice_len], synth.T0)
@@ -121,16 +138,20 @@ def main():
         res.append(ks["resolve_ms"] * ks["samples"])
         samples += ks["samples"]
         rsplit.append((ks["resolve_prologue_ms"], ks["resolve_replay_ms"]))
-    torch.cuda.synchronize()
+    barrier()
     dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
     evals = K * slice_len * N
     eval_ms = sum(evm) / max(samples, 1)
-    by = eval_bytes(N, a.batch)
+    by = eval_bytes(hi - lo, a.batch)
     out = {
         "metric": "pod-node Filter+Score evals/sec + p99 per-pod sched latency @50k nodes",
         "value": evals / dt,
         "unit": "pod-node evals/s",
-        "n_gpus": 1,
+        "n_gpus": world,
         "steps": K,
         "warmup": W,
         "ms_per_step": dt / K * 1e3,
@@ -141,25 +162,32 @@ def main():
         "data": "synthetic (BASELINE.md generator, seed 20251015+3)",
         "config": {"workload": synth.CONFIGS[3]["name"], "nodes": N, "pods": K * slice_len,
                    "pods_per_batch": a.batch, "plugins": "LoadAwareScheduling+NodeNUMAResource",
-                   "args": "v1beta3 defaults, NodeMetricExpirationSeconds=3600", "parallelism": "node-shard x1"},
+                   "args": "v1beta3 defaults, NodeMetricExpirationSeconds=3600",
+                   "parallelism": f"node-shard x{world}" + (" (RCCL all-gather of per-shard top-k)" if world > 1 else ""),
+                   "nodes_per_rank": hi - lo},
         "p99_pod_latency_ms": float(np.percentile(lat, 99)) if lat else None,
         "p50_pod_latency_ms": float(np.percentile(lat, 50)) if lat else None,
         "pods_placed": placed,
         "kernel_ms": {"eval": eval_ms, "select": sum(sel) / max(samples, 1), "resolve": sum(res) / max(samples, 1),
                       "resolve_prologue": float(np.mean([x[0] for x in rsplit])),
-                      "resolve_replay": float(np.mean([x[1] for x in rsplit])), "samples": samples},
+                      "resolve_replay": float(np.mean([x[1] for x in rsplit])), "samples": samples,
+                      "note": "per batch; 'select' includes the all-gather + merge when sharded"},
         "roofline": {"bound": "hbm", "kernel": "k_eval_batch", "achieved": by / eval_ms / 1e6 if eval_ms else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (by / eval_ms / 1e6 / HBM_PEAK_GBS) if eval_ms else None, "traffic": None,
                      "bytes_per_launch": by},
     }
     ev.close()
-    if a.stream_nodes > 0:
+    if world == 1 and a.stream_nodes > 0:
         out["stream_roofline"] = stream_sweep(a.stream_nodes, a.batch)
-    if not a.no_cpu_baseline and rank == 0:
+    if world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cl, pods, cfg, a.cpu_seconds, a.cpu_threads)
         out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
-    print(json.dumps(out))
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -313,6 +313,23 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
 int ke_last_schedule_stats(ke_ctx* ctx, double* total_ms, int32_t* n_batches,
                            double* batch_ms, int32_t batch_ms_cap);
 
+/* ---- node sharding across GPUs (one process per GPU) ------------------------------------------
+ * Replaces the upstream Parallelizer's fan-out of per-node Filter/Score over goroutines
+ * (cmd/koord-scheduler/app/server.go:417, Parallelism) with a fan-out of node ranges over GPUs.
+ * Every rank holds the full node state (same ingestion calls on every rank) and evaluates only its
+ * contiguous node range; per speculative batch the ranks exchange their per-pod top-k candidate
+ * lists with one RCCL all-gather and every rank resolves the batch identically, so the replicas
+ * stay bit-identical without exchanging rows.  Placements equal the unsharded ke_schedule. */
+#define KE_COMM_ID_BYTES 128
+/* RCCL unique id (ncclGetUniqueId), created once by rank 0 and broadcast to the others. */
+int ke_comm_unique_id(uint8_t* id, int32_t id_bytes);
+/* Collective: every rank calls it with the same id.  world in [1,8].  id == NULL with world > 1 is
+ * loopback mode: this context evaluates every shard itself and merges locally (single-GPU tests of
+ * the sharded path); world == 1 with an id runs the sharded path over a 1-rank communicator. */
+int ke_shard_init(ke_ctx* ctx, int32_t rank, int32_t world, const uint8_t* id);
+/* This rank's node range [lo, hi) for the current node count. */
+int ke_shard_range(ke_ctx* ctx, int32_t* lo, int32_t* hi);
+
 /* ---- measurement ----------------------------------------------------------------------------- */
 /* Sample every `sample_every`-th batch of ke_schedule with HIP event pairs around each of its
  * kernels (0 = off).  ke_last_kernel_stats returns the average device milliseconds per launch of

@@ -228,7 +228,11 @@ EXPORTS = {
     "ke_debug_rows": (C.c_int, [C.c_void_p, i32, i64, C.c_void_p, C.c_void_p]),
     "ke_debug_usage_bound": (i64, [i64, i64]),
     "ke_num_nodes": (i32, [C.c_void_p]),
+    "ke_comm_unique_id": (C.c_int, [C.c_void_p, i32]),
+    "ke_shard_init": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p]),
+    "ke_shard_range": (C.c_int, [C.c_void_p, C.POINTER(i32), C.POINTER(i32)]),
 }
+COMM_ID_BYTES = 128
 
 _lib = None
 

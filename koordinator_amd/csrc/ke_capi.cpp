@@ -17,6 +17,9 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
 int device_debug_rows(Context* ctx, int32_t n, Row* out);
 int device_set_profiling(Context* ctx, int32_t every);
 int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t iters, double* avg_ms);
+int device_comm_unique_id(uint8_t* id);
+int device_shard_init(Context* ctx, int rank, int world, const uint8_t* id);
+int device_shard_range(Context* ctx, int* lo, int* hi);
 }  // namespace ke
 
 using namespace ke;
@@ -316,6 +319,30 @@ int ke_bench_eval_kernel(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_
   rc = require_device(ctx);
   if (rc) return rc;
   return device_bench_eval(&ctx->c, n_pods, pods, now_ns, iters, avg_ms);
+}
+
+int ke_comm_unique_id(uint8_t* id, int32_t id_bytes) {
+  if (!id || id_bytes < KE_COMM_ID_BYTES) return fail(KE_ERR_INVALID, "ke_comm_unique_id: need a 128-byte buffer");
+  if (!device_available()) return fail(KE_ERR_NO_DEVICE, "ke_comm_unique_id: no HIP device");
+  return device_comm_unique_id(id);
+}
+
+int ke_shard_init(ke_ctx* ctx, int32_t rank, int32_t world, const uint8_t* id) {
+  if (!ctx) return fail(KE_ERR_INVALID, "null context");
+  int rc = require_device(ctx);
+  if (rc) return rc;
+  return device_shard_init(&ctx->c, rank, world, id);
+}
+
+int ke_shard_range(ke_ctx* ctx, int32_t* lo, int32_t* hi) {
+  if (!ctx || !lo || !hi) return fail(KE_ERR_INVALID, "ke_shard_range arguments");
+  int rc = require_device(ctx);
+  if (rc) return rc;
+  int l = 0, h = 0;
+  rc = device_shard_range(&ctx->c, &l, &h);
+  *lo = l;
+  *hi = h;
+  return rc;
 }
 
 int64_t ke_debug_usage_bound(int64_t total, int64_t thr) { return total > 0 ? max_used_within(total, thr) : 0; }

@@ -14,7 +14,9 @@
 //                 pods of the batch — then Reserve-patches the chosen rows in LDS and writes them back.
 // The three kernels are chained on one stream; nothing returns to the host between batches.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -298,12 +300,13 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_parity(SoA s, int n_nodes, 
 }
 
 // batch mode: 9-bit score per (pod,node): (total+1) or 0 when filtered out
-__global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int n_nodes, const DevPod* __restrict__ pods,
+// Nodes [lo, hi) of the SoA (this rank's shard); scores stay indexed by the global node index.
+__global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi, const DevPod* __restrict__ pods,
                                                            const int32_t* __restrict__ batch_base, int batch_pods,
                                                            int pods_per_block, KArgs k, uint16_t* __restrict__ scores,
                                                            int64_t score_stride) {
-  const int i = blockIdx.x * EVAL_BLOCK + threadIdx.x;
-  if (i >= n_nodes) return;
+  const int i = lo + blockIdx.x * EVAL_BLOCK + threadIdx.x;
+  if (i >= hi) return;
   NodeRegs n;
   load_row(s, i, n);
   prepare_row(n);
@@ -363,8 +366,10 @@ constexpr int SEL_WINDOW = 64;  // histogram window below the pod's best score
 //           number of ties before it in node order (a generic binary search covers the rare case
 //           of fewer than k feasible nodes inside the window)
 //   pass 3: select score > thr, and the first need_ties nodes with score == thr by node index.
+// Nodes [lo, hi) (lo % 512 == 0: the shard boundaries keep the 16-B loads aligned); keys carry the
+// global node index, so per-shard lists merge without translation (k_merge).
 __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restrict__ scores, int64_t score_stride,
-                                                         int n_nodes, uint32_t* __restrict__ cand,
+                                                         int lo, int hi, uint32_t* __restrict__ cand,
                                                          int32_t* __restrict__ cand_cnt) {
   __shared__ int32_t s_hist[SELECT_WAVES][SEL_WINDOW];
   __shared__ int32_t s_red[2][SELECT_WAVES];
@@ -375,9 +380,9 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
   const int k = min(j + 1, KMAX);
   const uint16_t* sc = scores + (int64_t)j * score_stride;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int seg = ((n_nodes + SELECT_WAVES - 1) / SELECT_WAVES + 511) & ~511;
-  const int w0 = wave * seg;
-  const int w1 = min(n_nodes, w0 + seg);
+  const int seg = ((hi - lo + SELECT_WAVES - 1) / SELECT_WAVES + 511) & ~511;
+  const int w0 = min(hi, lo + wave * seg);
+  const int w1 = min(hi, w0 + seg);
   reinterpret_cast<int32_t*>(s_hist)[threadIdx.x] = 0;  // SELECT_WAVES * SEL_WINDOW == SELECT_BLOCK
   if (threadIdx.x == 0) s_out = 0;
 
@@ -527,6 +532,40 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
   }
   __syncthreads();
   if (threadIdx.x == 0) cand_cnt[j] = s_out;
+}
+
+// --- node-sharded batches: merge of the per-shard candidate lists ---------------------------------
+// Rank r's k_select writes its block of the gather buffer: keys [MAX_BATCH][KMAX] then counts
+// [MAX_BATCH].  After the all-gather every rank holds all blocks and merges identically: the global
+// top-k_j of pod j is the top-k_j of the union of the per-shard top-k_j lists (each global top-k_j node
+// is also top-k_j inside its own shard).  Keys are unique (they embed the node index), so a key's
+// rank in the union is the number of larger keys; ranks < k_j are written in order.
+constexpr int GATH_WORDS = MAX_BATCH * KMAX + MAX_BATCH;
+constexpr int MAX_WORLD = 8;
+constexpr int MERGE_BLOCK = MAX_WORLD * KMAX;
+
+__global__ __launch_bounds__(MERGE_BLOCK) void k_merge(const uint32_t* __restrict__ gath, int world,
+                                                       uint32_t* __restrict__ cand, int32_t* __restrict__ cand_cnt) {
+  __shared__ uint4 s_k[MERGE_BLOCK / 4];
+  const int j = blockIdx.x, k = min(j + 1, KMAX);
+  const int t = threadIdx.x, r = t / KMAX, c = t % KMAX;
+  uint32_t key = 0;
+  if (r < world) {
+    const uint32_t* blk = gath + (int64_t)r * GATH_WORDS;
+    if (c < (int)blk[MAX_BATCH * KMAX + j]) key = blk[j * KMAX + c];
+  }
+  reinterpret_cast<uint32_t*>(s_k)[t] = key;
+  const int nz = __syncthreads_count(key != 0u);
+  if (key) {
+    int rank = 0;
+    const int n4 = world * KMAX / 4;
+    for (int u = 0; u < n4; u++) {
+      const uint4 q = s_k[u];
+      rank += (int)(q.x > key) + (int)(q.y > key) + (int)(q.z > key) + (int)(q.w > key);
+    }
+    if (rank < k) cand[j * KMAX + rank] = key;
+  }
+  if (t == 0) cand_cnt[j] = min(nz, k);
 }
 
 // --- resolve: one wavefront replays the batch sequentially -------------------------------------
@@ -830,7 +869,20 @@ struct DeviceState {
   uint32_t* d_best = nullptr;
   int64_t best_cap = 0;
   int profile_every = 0;
+  // node sharding (ke_shard_init): this rank evaluates/selects nodes shard_range(rank); the per-shard
+  // candidate lists meet in d_gath through an RCCL all-gather (or, loopback, all shards run here)
+  int world = 1, rank = 0;
+  bool loopback = false;
+  ncclComm_t comm = nullptr;
+  uint32_t* d_gath = nullptr;  // [world][GATH_WORDS]
 };
+
+// Contiguous node range of shard `rank`: 512-aligned chunks (k_select's 16-B loads stay aligned).
+void shard_range(int n_nodes, int rank, int world, int* lo, int* hi) {
+  const int chunk = ((n_nodes + world - 1) / world + 511) & ~511;
+  *lo = std::min(rank * chunk, n_nodes);
+  *hi = std::min(*lo + chunk, n_nodes);
+}
 
 static int ensure(void** p, int64_t* cap, int64_t bytes) {
   if (*cap >= bytes) return KE_OK;
@@ -874,13 +926,57 @@ void device_destroy(Context* ctx) {
   if (!d) return;
   (void)hipSetDevice(d->device);
   if (d->stream) (void)hipStreamSynchronize(d->stream);
+  if (d->comm) (void)ncclCommDestroy(d->comm);
   void* ptrs[] = {d->soa.f, d->soa.flags, d->d_rows, d->d_idx, d->d_pods, d->d_scores, d->d_cand, d->d_cand_cnt,
-                  d->d_batch_base, d->d_chosen, d->d_chosen_score, d->d_stamps, d->d_parity, d->d_best};
+                  d->d_batch_base, d->d_chosen, d->d_chosen_score, d->d_stamps, d->d_parity, d->d_best, d->d_gath};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (d->stream) (void)hipStreamDestroy(d->stream);
   delete d;
   ctx->dev = nullptr;
+}
+
+#define RCCL_OK(expr)                                                               \
+  do {                                                                              \
+    ncclResult_t _r = (expr);                                                       \
+    if (_r != ncclSuccess) return fail(KE_ERR_DEVICE, std::string(#expr ": ") + ncclGetErrorString(_r)); \
+  } while (0)
+
+int device_comm_unique_id(uint8_t* id) {
+  ncclUniqueId u;
+  RCCL_OK(ncclGetUniqueId(&u));
+  std::memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+  return KE_OK;
+}
+
+// Collective over `world` ranks (every rank calls it with the same id); id == nullptr = loopback.
+int device_shard_init(Context* ctx, int rank, int world, const uint8_t* id) {
+  DeviceState* d = ctx->dev;
+  HIP_OK(hipSetDevice(d->device));
+  if (world < 1 || world > MAX_WORLD || rank < 0 || rank >= world)
+    return fail(KE_ERR_INVALID, "ke_shard_init: need 1 <= world <= 8 and 0 <= rank < world");
+  if (d->comm) {
+    RCCL_OK(ncclCommDestroy(d->comm));
+    d->comm = nullptr;
+  }
+  if (!d->d_gath) HIP_OK(hipMalloc(&d->d_gath, sizeof(uint32_t) * GATH_WORDS * MAX_WORLD));
+  HIP_OK(hipMemsetAsync(d->d_gath, 0, sizeof(uint32_t) * GATH_WORDS * MAX_WORLD, d->stream));
+  HIP_OK(hipStreamSynchronize(d->stream));
+  d->world = world;
+  d->rank = rank;
+  d->loopback = id == nullptr && world > 1;
+  if (id) {  // world == 1 with an id: a 1-rank communicator through the sharded path (tests)
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+    RCCL_OK(ncclCommInitRank(&d->comm, world, u, rank));
+  }
+  return KE_OK;
+}
+
+int device_shard_range(Context* ctx, int* lo, int* hi) {
+  DeviceState* d = ctx->dev;
+  shard_range(ctx->n_nodes, d->rank, d->world, lo, hi);
+  return KE_OK;
 }
 
 static KArgs make_kargs(const Context* ctx, int64_t now) {
@@ -1021,13 +1117,37 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     const bool prof = every > 0 && b % every == 0;
     hipEvent_t* pe = prof ? &ev[(size_t)(b / every) * 4] : nullptr;
     if (prof) HIP_OK(hipEventRecord(pe[0], d->stream));
-    if (N > 0) {
+    if (N > 0 && d->world == 1 && !d->comm) {
       dim3 grid((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((bp + ppb - 1) / ppb));
-      hipLaunchKernelGGL(k_eval_batch, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, N, d->d_pods, d->d_batch_base, bp,
-                         ppb, k, d->d_scores, d->capacity);
+      hipLaunchKernelGGL(k_eval_batch, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base,
+                         bp, ppb, k, d->d_scores, d->capacity);
       if (prof) HIP_OK(hipEventRecord(pe[1], d->stream));
-      hipLaunchKernelGGL(k_select, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, d->stream, d->d_scores, d->capacity, N,
+      hipLaunchKernelGGL(k_select, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, d->stream, d->d_scores, d->capacity, 0, N,
                          d->d_cand, d->d_cand_cnt);
+    } else if (N > 0) {
+      // node-sharded: this rank's range (loopback: every range), per-shard top-k_j, all-gather, merge
+      int lo = 0, hi = N;
+      if (!d->loopback) shard_range(N, d->rank, d->world, &lo, &hi);
+      if (hi > lo) {
+        dim3 grid((unsigned)((hi - lo + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((bp + ppb - 1) / ppb));
+        hipLaunchKernelGGL(k_eval_batch, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, lo, hi, d->d_pods,
+                           d->d_batch_base, bp, ppb, k, d->d_scores, d->capacity);
+      }
+      if (prof) HIP_OK(hipEventRecord(pe[1], d->stream));
+      for (int r = 0; r < d->world; r++) {
+        if (!d->loopback && r != d->rank) continue;
+        int slo, shi;
+        shard_range(N, r, d->world, &slo, &shi);
+        uint32_t* blk = d->d_gath + (int64_t)r * GATH_WORDS;
+        hipLaunchKernelGGL(k_select, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, d->stream, d->d_scores, d->capacity,
+                           slo, shi, blk, reinterpret_cast<int32_t*>(blk + MAX_BATCH * KMAX));
+      }
+      if (!d->loopback) {
+        uint32_t* mine = d->d_gath + (int64_t)d->rank * GATH_WORDS;  // in place: send = own block of recv
+        RCCL_OK(ncclAllGather(mine, d->d_gath, GATH_WORDS, ncclUint32, d->comm, d->stream));
+      }
+      hipLaunchKernelGGL(k_merge, dim3((unsigned)bp), dim3(MERGE_BLOCK), 0, d->stream, d->d_gath, d->world, d->d_cand,
+                         d->d_cand_cnt);
     } else {
       if (prof) HIP_OK(hipEventRecord(pe[1], d->stream));
       HIP_OK(hipMemsetAsync(d->d_cand_cnt, 0, sizeof(int32_t) * MAX_BATCH, d->stream));
@@ -1113,14 +1233,14 @@ int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t 
   const int ppb = 8;
   HIP_OK(hipMemsetAsync(d->d_batch_base, 0, sizeof(int32_t), d->stream));
   dim3 grid((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((n_pods + ppb - 1) / ppb));
-  hipLaunchKernelGGL(k_eval_batch, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, N, d->d_pods, d->d_batch_base, n_pods,
+  hipLaunchKernelGGL(k_eval_batch, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base, n_pods,
                      ppb, k, d->d_scores, d->capacity);  // warm
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   HIP_OK(hipEventRecord(e0, d->stream));
   for (int it = 0; it < iters; it++)
-    hipLaunchKernelGGL(k_eval_batch, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, N, d->d_pods, d->d_batch_base,
+    hipLaunchKernelGGL(k_eval_batch, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base,
                        n_pods, ppb, k, d->d_scores, d->capacity);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(e1, d->stream));

@@ -118,6 +118,21 @@ class Evaluator:
         self._check(self.lib.ke_estimate_pod(self.h, C.byref(pod), abi.ptr(est)))
         return est
 
+    # ---- node sharding (one process per GPU) ------------------------------------------------
+    def shard_init(self, rank, world, unique_id=None):
+        """Collective over `world` ranks with the same RCCL `unique_id` (bytes from comm_unique_id on
+        rank 0); unique_id=None with world > 1 runs every shard in this context (loopback)."""
+        buf = None
+        if unique_id is not None:
+            assert len(unique_id) == abi.COMM_ID_BYTES
+            buf = C.create_string_buffer(bytes(unique_id), abi.COMM_ID_BYTES)
+        self._check(self.lib.ke_shard_init(self.h, rank, world, buf))
+
+    def shard_range(self):
+        lo, hi = abi.i32(), abi.i32()
+        self._check(self.lib.ke_shard_range(self.h, C.byref(lo), C.byref(hi)))
+        return lo.value, hi.value
+
     # ---- evaluation -------------------------------------------------------------------------
     def eval(self, pods, now_ns):
         pods = as_pod_array(pods)
@@ -178,3 +193,13 @@ class Evaluator:
         dev = np.zeros(n, abi.ROW_DTYPE) if device else None
         self._check(self.lib.ke_debug_rows(self.h, n, int(now_ns), abi.ptr(dev), abi.ptr(host)))
         return dev, host
+
+
+def comm_unique_id(lib=None):
+    """RCCL unique id for ke_shard_init, created on rank 0 (needs the HIP device)."""
+    lib = lib or abi.load_library()
+    buf = C.create_string_buffer(abi.COMM_ID_BYTES)
+    rc = lib.ke_comm_unique_id(buf, abi.COMM_ID_BYTES)
+    if rc != abi.OK:
+        raise KoordEvalError(rc, lib.ke_last_error().decode())
+    return buf.raw

@@ -211,3 +211,45 @@ def test_schedule_large_cluster_prefix(gpu):
     c1, s1 = ev.schedule(pods, synth.T0)
     c0, s0 = o.schedule(pods, synth.T0)
     assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+
+
+# ---- node sharding (loopback: every shard's eval/select + k_merge in one context) -----------------
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_schedule_sharded_loopback_parity(gpu, world):
+    """Per-shard top-k_j lists merged by k_merge give the unsharded placements (config-1 cluster)."""
+    cl = synth.make_cluster(3000, synth.BASE_SEED + 61)
+    pods = synth.make_pods(700, synth.BASE_SEED + 62)
+    ev, o = both(synth.config(3000), cl)
+    ev.shard_init(0, world, None)
+    c1, s1 = ev.schedule(pods, synth.T0)
+    c0, s0 = o.schedule(pods, synth.T0)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5]
+    assert np.array_equal(s1, s0)
+
+
+def test_shard_ranges_match_host_plan(gpu):
+    from koordinator_amd import shard
+    cl = synth.make_cluster(5000, synth.BASE_SEED + 63)
+    ev = Evaluator(synth.config(5000))
+    synth.load_into(ev, cl)
+    for world in (1, 2, 4, 8):
+        got = []
+        for r in range(world):
+            ev.shard_init(r, world, None)
+            got.append(ev.shard_range())
+        assert got == [shard.node_range(5000, r, world) for r in range(world)]
+
+
+def test_rccl_single_rank_communicator(gpu):
+    """The real RCCL path (unique id, ncclCommInitRank, in-place ncclAllGather, k_merge) with a
+    1-rank communicator: placements equal the oracle's."""
+    from koordinator_amd.evaluator import comm_unique_id
+    uid = comm_unique_id()
+    assert len(uid) == abi.COMM_ID_BYTES
+    cl = synth.make_cluster(2000, synth.BASE_SEED + 64)
+    pods = synth.make_pods(300, synth.BASE_SEED + 65)
+    ev, o = both(synth.config(2000), cl)
+    ev.shard_init(0, 1, uid)
+    c1, s1 = ev.schedule(pods, synth.T0)
+    c0, s0 = o.schedule(pods, synth.T0)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
