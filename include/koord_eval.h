@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define KE_ABI_VERSION 1
+#define KE_ABI_VERSION 2
 #define KE_ABSENT (-1)
 
 /* ---- error codes ---------------------------------------------------------------------------- */
@@ -71,6 +71,10 @@ extern "C" {
 #define KE_REASON_NUMA_INSUFFICIENT_AMPLIFIED_CPU 16 /* "Insufficient amplified cpu" nodenumaresource/plugin.go:57 */
 #define KE_REASON_NUMA_INVALID_AMPLIFICATION_RATIO 17 /* "node(s) invalid CPU amplification ratio" plugin.go:56 */
 #define KE_REASON_NUMA_INVALID_CPU_TOPOLOGY 18 /* "node(s) invalid CPU Topology" plugin.go:52 (GetAvailableCPUs) */
+#define KE_REASON_DS_INVALID_REQUEST 32      /* PreFilter: "invalid resource device requests" / unit (deviceshare/utils.go:304-327) */
+#define KE_REASON_DS_INSUFFICIENT_GPU 33     /* "Insufficient gpu devices"  (devicehandler_gpu.go:41, device_allocator.go:412) */
+#define KE_REASON_DS_INSUFFICIENT_RDMA 34    /* "Insufficient rdma devices" (devicehandler_default.go:46, device_allocator.go:412) */
+#define KE_REASON_DS_INSUFFICIENT_FPGA 35    /* "Insufficient fpga devices" */
 
 /* ---- resources (index into per-resource arrays) ---------------------------------------------- */
 #define KE_RES_CPU 0          /* "cpu"                         MilliValue */
@@ -150,14 +154,66 @@ typedef struct ke_numa_args {
   int32_t pad;
 } ke_numa_args;
 
+/* ---- DeviceShare (pkg/scheduler/plugins/deviceshare) ------------------------------------------ */
+#define KE_DEV_GPU 0  /* schedulingv1alpha1.GPU  */
+#define KE_DEV_RDMA 1 /* schedulingv1alpha1.RDMA */
+#define KE_DEV_FPGA 2 /* schedulingv1alpha1.FPGA */
+#define KE_DEV_TYPES 3
+#define KE_MAX_MINORS 16 /* device instances per type per node (minors 0..15) */
+/* Resource keys of one device instance.  GPU devices use all three, RDMA/FPGA devices key 0. */
+#define KE_DKEY_GPU_CORE 0         /* koordinator.sh/gpu-core          */
+#define KE_DKEY_GPU_MEMORY 1       /* koordinator.sh/gpu-memory (bytes) */
+#define KE_DKEY_GPU_MEMORY_RATIO 2 /* koordinator.sh/gpu-memory-ratio  */
+#define KE_DKEY_RDMA 0             /* koordinator.sh/rdma              */
+#define KE_DKEY_FPGA 0             /* koordinator.sh/fpga              */
+#define KE_DKEYS 3
+/* Pod device requests: PodRequests of the DeviceShare resource names (deviceshare/utils.go:54-69). */
+#define KE_PDR_NVIDIA_GPU 0       /* nvidia.com/gpu              */
+#define KE_PDR_AMD_GPU 1          /* amd.com/gpu                 */
+#define KE_PDR_KOORD_GPU 2        /* koordinator.sh/gpu          */
+#define KE_PDR_GPU_SHARED 3       /* koordinator.sh/gpu.shared   */
+#define KE_PDR_GPU_CORE 4         /* koordinator.sh/gpu-core     */
+#define KE_PDR_GPU_MEMORY 5       /* koordinator.sh/gpu-memory   */
+#define KE_PDR_GPU_MEMORY_RATIO 6 /* koordinator.sh/gpu-memory-ratio */
+#define KE_PDR_RDMA 7             /* koordinator.sh/rdma         */
+#define KE_PDR_FPGA 8             /* koordinator.sh/fpga         */
+#define KE_PDR_COUNT 9
+/* DeviceShareArgs.ScoringStrategy (types.go:263-275, v1beta3/defaults.go:218-242): weights indexed
+ * gpu-memory-ratio, gpu-memory, rdma, fpga; KE_ABSENT = not in Resources. */
+#define KE_DSW_GPU_MEMORY_RATIO 0
+#define KE_DSW_GPU_MEMORY 1
+#define KE_DSW_RDMA 2
+#define KE_DSW_FPGA 3
+typedef struct ke_deviceshare_args {
+  int64_t weights[4];
+  int32_t strategy; /* KE_STRATEGY_* */
+  int32_t pad;
+} ke_deviceshare_args;
+
+/* One device instance as koord-scheduler's nodeDeviceCache holds it (device_cache.go:518-568):
+ * `total` = DeviceInfo.Resources (left empty by the cache when !Health), `used` = Σ allocations of
+ * the pods already on it (updateCacheUsed).  has_* mark the keys present in each ResourceList. */
+typedef struct ke_device {
+  int32_t type;  /* KE_DEV_* */
+  int32_t minor; /* DeviceInfo.Minor, 0 .. KE_MAX_MINORS-1 */
+  uint8_t health;
+  uint8_t has_total[KE_DKEYS];
+  uint8_t has_used[KE_DKEYS];
+  uint8_t pad;
+  int64_t total[KE_DKEYS];
+  int64_t used[KE_DKEYS];
+} ke_device; /* 64 bytes */
+
 /* Framework profile: score plugin weights (config/manager/scheduler-config.yaml:85-94). */
 typedef struct ke_config {
   int32_t abi_version;    /* must be KE_ABI_VERSION                                      */
   int32_t device_ordinal; /* HIP device used by this context (one process per GPU)      */
   int64_t weight_loadaware;
   int64_t weight_numa;
+  int64_t weight_deviceshare;
   ke_loadaware_args loadaware;
   ke_numa_args numa;
+  ke_deviceshare_args deviceshare;
   int32_t node_capacity;  /* max nodes this context will hold (device SoA is sized once) */
   int32_t pod_batch;      /* B: pods evaluated per speculative batch in ke_schedule      */
   int32_t global_node_offset; /* first global node index held by this shard (multi-GPU)  */
@@ -238,7 +294,8 @@ typedef struct ke_pod {
   uint8_t is_terminated;
   uint8_t has_resource_spec;          /* cpuset annotations: unsupported in ABI v1 */
   uint8_t has_other_requests;         /* PodRequests has a non-zero resource outside KE_RES_* */
-  uint8_t pad;
+  uint8_t has_unsupported_device_requests; /* Huawei NPU / Hygon DCU device resources: unsupported */
+  int64_t device_requests[KE_PDR_COUNT]; /* PodRequests of the device resources (Value()), 0 = absent */
 } ke_pod;
 
 /* One candidate of a pod's speculative top-k list (device order: best first). */
@@ -255,7 +312,8 @@ void ke_destroy(ke_ctx* ctx);
 const char* ke_last_error(void);
 int ke_abi_version(void);
 /* sizeof() of ke_config, ke_node, ke_node_metric, ke_pod_metric, ke_aggregated_usage, ke_pod,
- * ke_resource_map, ke_loadaware_args, ke_numa_args (in that order) for binding-layout checks. */
+ * ke_resource_map, ke_loadaware_args, ke_numa_args, ke_deviceshare_args, ke_device (in that order)
+ * for binding-layout checks. */
 int ke_abi_struct_sizes(int32_t* sizes, int32_t n);
 /* 1 if this build has a usable HIP device and its gfx950 kernels loaded, else 0. */
 int ke_device_available(void);
@@ -288,6 +346,12 @@ int ke_pods_assign(ke_ctx* ctx, int32_t n, const int32_t* nodes, const ke_pod* p
  * context's args: est[KE_NRES] (cpu milli, memory bytes), KE_ABSENT for a resource without weight. */
 int ke_estimate_pod(ke_ctx* ctx, const ke_pod* pod, int64_t* est);
 
+/* DeviceShare node device cache (Device CRD informer, device_cache.go:518-568): replace the devices of
+ * `node` (n may be 0: a cache entry without devices).  At most KE_MAX_MINORS devices per type. */
+int ke_node_devices_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_device* devices);
+/* Drop the node's cache entry (getNodeDevice == nil: DeviceShare Filter passes, Score is 0). */
+int ke_node_devices_delete(ke_ctx* ctx, int32_t node);
+
 /* ---- evaluation ------------------------------------------------------------------------------ */
 /* Parity mode: Filter + Score of `n_pods` pods against every node, no state change.
  * Each output is optional (NULL) and laid out [pod][node]:
@@ -295,11 +359,13 @@ int ke_estimate_pod(ke_ctx* ctx, const ke_pod* pod, int64_t* est);
  *   reason   uint8  KE_REASON_*
  *   la_score int16  LoadAwareScheduling.Score (0 for filtered-out nodes)
  *   numa_score int16 NodeNUMAResource.Score
+ *   ds_score int16  DeviceShare.Score before NormalizeScore (the total uses the normalized score,
+ *                   DefaultNormalizeScore over the pod's feasible nodes, scoring.go:109-111)
  *   total    int16  Σ weight·score over the plugins, -1 if the node is filtered out
  * and `best[pod]` is selectHost's choice (-1 if no feasible node; ties -> lowest node index). */
 int ke_eval(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
             uint8_t* status, uint8_t* reason, int16_t* la_score, int16_t* numa_score,
-            int16_t* total, int32_t* best);
+            int16_t* ds_score, int16_t* total, int32_t* best);
 
 /* Schedule `n_pods` pods in queue order, each one seeing the Reserve of all pods before it
  * (LoadAware podAssignCache.assign with timestamp now_ns, NodeInfo.Requested += pod requests).
@@ -312,6 +378,9 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
  * latency (pod dequeue -> node selected) in milliseconds, n_batches entries. */
 int ke_last_schedule_stats(ke_ctx* ctx, double* total_ms, int32_t* n_batches,
                            double* batch_ms, int32_t batch_ms_cap);
+/* DeviceShare Reserve of the last ke_schedule (AutopilotAllocator.Allocate -> updateCacheUsed,
+ * plugin.go:426-492): per pod, bit 16*type + minor set for every device instance allocated. */
+int ke_last_device_allocations(ke_ctx* ctx, int32_t n, uint64_t* minors);
 
 /* ---- node sharding across GPUs (one process per GPU) ------------------------------------------
  * Replaces the upstream Parallelizer's fan-out of per-node Filter/Score over goroutines

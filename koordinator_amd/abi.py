@@ -9,7 +9,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 ABSENT = -1
 
 OK = 0
@@ -26,6 +26,24 @@ REASON_LA_AGG_USAGE_MEMORY = 5
 REASON_NUMA_INSUFFICIENT_AMPLIFIED_CPU = 16
 REASON_NUMA_INVALID_AMPLIFICATION_RATIO = 17
 REASON_NUMA_INVALID_CPU_TOPOLOGY = 18
+REASON_DS_INVALID_REQUEST = 32
+REASON_DS_INSUFFICIENT_GPU = 33
+REASON_DS_INSUFFICIENT_RDMA = 34
+REASON_DS_INSUFFICIENT_FPGA = 35
+
+DEV_GPU, DEV_RDMA, DEV_FPGA = 0, 1, 2
+DEV_TYPES = 3
+MAX_MINORS = 16
+DKEY_GPU_CORE, DKEY_GPU_MEMORY, DKEY_GPU_MEMORY_RATIO = 0, 1, 2
+DKEY_RDMA = DKEY_FPGA = 0
+DKEYS = 3
+PDR = {"nvidia.com/gpu": 0, "amd.com/gpu": 1, "koordinator.sh/gpu": 2, "koordinator.sh/gpu.shared": 3,
+       "koordinator.sh/gpu-core": 4, "koordinator.sh/gpu-memory": 5, "koordinator.sh/gpu-memory-ratio": 6,
+       "koordinator.sh/rdma": 7, "koordinator.sh/fpga": 8}
+PDR_COUNT = 9
+# device resources the DeviceShare ABI does not model (utils.go:38-52): Huawei NPU, Hygon DCU
+UNSUPPORTED_DEVICE_RESOURCES = {"huawei.com/npu-core", "huawei.com/npu-cpu", "huawei.com/npu-dvpp", "dcu.com/gpu"}
+DSW_GPU_MEMORY_RATIO, DSW_GPU_MEMORY, DSW_RDMA, DSW_FPGA = 0, 1, 2, 3
 
 RES_CPU, RES_MEMORY, RES_BATCH_CPU, RES_BATCH_MEMORY, RES_MID_CPU, RES_MID_MEMORY = range(6)
 RES_COUNT = 6
@@ -71,14 +89,33 @@ class NumaArgs(C.Structure):
     _fields_ = [("weights", i64 * NRES), ("strategy", i32), ("pad", i32)]
 
 
+class DeviceShareArgs(C.Structure):
+    _fields_ = [("weights", i64 * 4), ("strategy", i32), ("pad", i32)]
+
+
+class Device(C.Structure):
+    _fields_ = [
+        ("type", i32),
+        ("minor", i32),
+        ("health", u8),
+        ("has_total", u8 * DKEYS),
+        ("has_used", u8 * DKEYS),
+        ("pad", u8),
+        ("total", i64 * DKEYS),
+        ("used", i64 * DKEYS),
+    ]
+
+
 class Config(C.Structure):
     _fields_ = [
         ("abi_version", i32),
         ("device_ordinal", i32),
         ("weight_loadaware", i64),
         ("weight_numa", i64),
+        ("weight_deviceshare", i64),
         ("loadaware", LoadAwareArgs),
         ("numa", NumaArgs),
+        ("deviceshare", DeviceShareArgs),
         ("node_capacity", i32),
         ("pod_batch", i32),
         ("global_node_offset", i32),
@@ -149,11 +186,13 @@ class Pod(C.Structure):
         ("is_terminated", u8),
         ("has_resource_spec", u8),
         ("has_other_requests", u8),
-        ("pad", u8),
+        ("has_unsupported_device_requests", u8),
+        ("device_requests", i64 * PDR_COUNT),
     ]
 
 
-STRUCTS = [Config, Node, NodeMetric, PodMetric, AggregatedUsage, Pod, ResourceMap, LoadAwareArgs, NumaArgs]
+STRUCTS = [Config, Node, NodeMetric, PodMetric, AggregatedUsage, Pod, ResourceMap, LoadAwareArgs, NumaArgs,
+           DeviceShareArgs, Device]
 
 # numpy views of the same layouts (bulk loads)
 NODE_DTYPE = np.dtype(Node)
@@ -161,6 +200,7 @@ NODE_METRIC_DTYPE = np.dtype(NodeMetric)
 POD_METRIC_DTYPE = np.dtype(PodMetric)
 AGG_DTYPE = np.dtype(AggregatedUsage)
 POD_DTYPE = np.dtype(Pod)
+DEVICE_DTYPE = np.dtype(Device)
 
 ROW_DTYPE = np.dtype([("f", np.int64, (18,)), ("flags", np.uint32), ("pad", np.uint32)])
 
@@ -173,6 +213,7 @@ def default_config(node_capacity, pod_batch=64, device_ordinal=0, global_node_of
     cfg.device_ordinal = device_ordinal
     cfg.weight_loadaware = 1
     cfg.weight_numa = 1
+    cfg.weight_deviceshare = 1
     a = cfg.loadaware
     a.node_metric_expiration_seconds = 180
     a.resource_weights[:] = [1, 1]
@@ -188,6 +229,8 @@ def default_config(node_capacity, pod_batch=64, device_ordinal=0, global_node_of
     a.enable_schedule_when_node_metrics_expired = 0
     cfg.numa.weights[:] = [1, 1]
     cfg.numa.strategy = STRATEGY_LEAST_ALLOCATED
+    cfg.deviceshare.weights[:] = [1, 1, 1, 1]  # gpu-memory-ratio, gpu-memory, rdma, fpga (defaults.go:218-242)
+    cfg.deviceshare.strategy = STRATEGY_LEAST_ALLOCATED
     cfg.node_capacity = node_capacity
     cfg.pod_batch = pod_batch
     cfg.global_node_offset = global_node_offset
@@ -216,7 +259,10 @@ EXPORTS = {
     "ke_pod_unassign": (C.c_int, [C.c_void_p, i32, i64]),
     "ke_pods_assign": (C.c_int, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "ke_estimate_pod": (C.c_int, [C.c_void_p, C.POINTER(Pod), C.c_void_p]),
-    "ke_eval": (C.c_int, [C.c_void_p, i32, C.c_void_p, i64] + [C.c_void_p] * 6),
+    "ke_eval": (C.c_int, [C.c_void_p, i32, C.c_void_p, i64] + [C.c_void_p] * 7),
+    "ke_node_devices_set": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p]),
+    "ke_node_devices_delete": (C.c_int, [C.c_void_p, i32]),
+    "ke_last_device_allocations": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_schedule": (C.c_int, [C.c_void_p, i32, C.c_void_p, i64, C.c_void_p, C.c_void_p]),
     "ke_last_schedule_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(i32), C.c_void_p, i32]),
     "ke_set_profiling": (C.c_int, [C.c_void_p, i32]),

@@ -12,7 +12,7 @@ int device_available();
 int device_create(Context* ctx);
 void device_destroy(Context* ctx);
 int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, uint8_t* status, uint8_t* reason,
-                int16_t* la, int16_t* numa, int16_t* total, int32_t* best);
+                int16_t* la, int16_t* numa, int16_t* ds, int16_t* total, int32_t* best);
 int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t* chosen, int32_t* score);
 int device_debug_rows(Context* ctx, int32_t n, Row* out);
 int device_set_profiling(Context* ctx, int32_t every);
@@ -56,7 +56,8 @@ int ke_abi_struct_sizes(int32_t* sizes, int32_t n) {
                          (int32_t)sizeof(ke_node_metric),  (int32_t)sizeof(ke_pod_metric),
                          (int32_t)sizeof(ke_aggregated_usage), (int32_t)sizeof(ke_pod),
                          (int32_t)sizeof(ke_resource_map), (int32_t)sizeof(ke_loadaware_args),
-                         (int32_t)sizeof(ke_numa_args)};
+                         (int32_t)sizeof(ke_numa_args), (int32_t)sizeof(ke_deviceshare_args),
+                         (int32_t)sizeof(ke_device)};
   const int32_t m = (int32_t)(sizeof(all) / sizeof(all[0]));
   for (int32_t i = 0; i < n && i < m; i++) sizes[i] = all[i];
   return m;
@@ -83,6 +84,7 @@ int ke_create(const ke_config* cfg, ke_ctx** out) {
   if (a.enable_schedule_when_node_metrics_expired) f |= AF_ENABLE_WHEN_EXPIRED;
   if (a.node_metric_expiration_seconds != KE_ABSENT) f |= AF_EXP_PRESENT;
   if (cfg->numa.strategy == KE_STRATEGY_MOST_ALLOCATED) f |= AF_NUMA_MOST;
+  if (cfg->deviceshare.strategy == KE_STRATEGY_MOST_ALLOCATED) f |= AF_DS_MOST;
   k.flags = f;
   k.wsum_la = k.wsum_numa = 0;
   for (int r = 0; r < KE_NRES; r++) {
@@ -93,6 +95,9 @@ int ke_create(const ke_config* cfg, ke_ctx** out) {
   }
   k.wp_la = (int32_t)cfg->weight_loadaware;
   k.wp_numa = (int32_t)cfg->weight_numa;
+  k.wp_ds = (int32_t)cfg->weight_deviceshare;
+  for (int i = 0; i < 4; i++)
+    k.w_ds[i] = cfg->deviceshare.weights[i] == KE_ABSENT ? -1 : (int32_t)cfg->deviceshare.weights[i];
   if (device_available()) {
     rc = device_create(&c);
     if (rc) {
@@ -134,6 +139,36 @@ int ke_nodes_load(ke_ctx* ctx, int32_t n, const ke_node* nodes) {
     int rc = ke_node_upsert(ctx, i, &nodes[i]);
     if (rc) return rc;
   }
+  return KE_OK;
+}
+
+int ke_node_devices_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_device* devices) {
+  int rc = check_node(ctx, node);
+  if (rc) return rc;
+  rc = validate_devices(n, devices);
+  if (rc) return rc;
+  NodeState& ns = ctx->c.nodes[node];
+  ns.has_dev_cache = true;
+  ns.devs.assign(devices, devices + n);
+  ns.dirty = true;
+  ctx->c.ds_enabled = true;
+  return KE_OK;
+}
+
+int ke_node_devices_delete(ke_ctx* ctx, int32_t node) {
+  int rc = check_node(ctx, node);
+  if (rc) return rc;
+  NodeState& ns = ctx->c.nodes[node];
+  ns.has_dev_cache = false;
+  ns.devs.clear();
+  ns.dirty = true;
+  return KE_OK;
+}
+
+int ke_last_device_allocations(ke_ctx* ctx, int32_t n, uint64_t* minors) {
+  if (!ctx || n < 0 || (n > 0 && !minors)) return fail(KE_ERR_INVALID, "ke_last_device_allocations arguments");
+  const auto& a = ctx->c.last_dev_alloc;
+  for (int32_t i = 0; i < n; i++) minors[i] = i < (int32_t)a.size() ? a[i] : 0;
   return KE_OK;
 }
 
@@ -237,13 +272,13 @@ int ke_estimate_pod(ke_ctx* ctx, const ke_pod* pod, int64_t* est) {
 }
 
 int ke_eval(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, uint8_t* status, uint8_t* reason,
-            int16_t* la_score, int16_t* numa_score, int16_t* total, int32_t* best) {
+            int16_t* la_score, int16_t* numa_score, int16_t* ds_score, int16_t* total, int32_t* best) {
   if (!ctx) return fail(KE_ERR_INVALID, "null context");
   int rc = check_pods(pods, n_pods);
   if (rc) return rc;
   rc = require_device(ctx);
   if (rc) return rc;
-  return device_eval(&ctx->c, n_pods, pods, now_ns, status, reason, la_score, numa_score, total, best);
+  return device_eval(&ctx->c, n_pods, pods, now_ns, status, reason, la_score, numa_score, ds_score, total, best);
 }
 
 int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int32_t* chosen, int32_t* score) {
@@ -264,6 +299,8 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
     NodeState& ns = ctx->c.nodes[node];
     const bool was_dirty = ns.dirty;
     host_assign(ctx->c.cfg, ns, pods[p], now_ns);
+    if (p < (int32_t)ctx->c.last_dev_alloc.size() && ctx->c.last_dev_alloc[p])
+      host_ds_reserve(ctx->c.cfg, ns, make_dev_pod(ctx->c.cfg, pods[p]), ctx->c.last_dev_alloc[p]);
     ns.node.requested[KE_RES_CPU] += pods[p].requests[KE_RES_CPU];
     ns.node.requested[KE_RES_MEMORY] += pods[p].requests[KE_RES_MEMORY];
     ns.dirty = was_dirty;  // the device row already carries this Reserve

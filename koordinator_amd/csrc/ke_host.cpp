@@ -36,8 +36,15 @@ int validate_config(const ke_config& cfg) {
   if (cfg.node_capacity <= 0 || cfg.node_capacity > MAX_SHARD_NODES)
     return fail(KE_ERR_INVALID, "node_capacity out of range (1 .. 2^23-1 per shard)");
   if (cfg.pod_batch < 1 || cfg.pod_batch > MAX_BATCH) return fail(KE_ERR_INVALID, "pod_batch out of range (1..64)");
-  if (cfg.weight_loadaware < 0 || cfg.weight_numa < 0 || (cfg.weight_loadaware + cfg.weight_numa) * 100 > MAX_TOTAL_SCORE)
-    return fail(KE_ERR_UNSUPPORTED, "plugin weights: (w_loadaware + w_numa) * 100 must be <= 510");
+  if (cfg.weight_loadaware < 0 || cfg.weight_numa < 0 || cfg.weight_deviceshare < 0 ||
+      (cfg.weight_loadaware + cfg.weight_numa + cfg.weight_deviceshare) * 100 > MAX_TOTAL_SCORE)
+    return fail(KE_ERR_UNSUPPORTED, "plugin weights: (w_loadaware + w_numa + w_deviceshare) * 100 must be <= 510");
+  for (int i = 0; i < 4; i++) {
+    const int64_t w = cfg.deviceshare.weights[i];
+    if (w != KE_ABSENT && (w < 0 || w > (1 << 20))) return fail(KE_ERR_UNSUPPORTED, "deviceshare weight out of range");
+  }
+  if (cfg.deviceshare.strategy != KE_STRATEGY_LEAST_ALLOCATED && cfg.deviceshare.strategy != KE_STRATEGY_MOST_ALLOCATED)
+    return fail(KE_ERR_INVALID, "deviceshare scoring strategy");
   for (int r = 0; r < KE_NRES; r++) {
     int64_t w = cfg.loadaware.resource_weights[r];
     if (w != KE_ABSENT && (w < 0 || w > (1 << 20))) return fail(KE_ERR_UNSUPPORTED, "loadaware weight out of range");
@@ -63,6 +70,76 @@ int validate_node(const ke_node& n) {
   return KE_OK;
 }
 
+int validate_devices(int32_t n, const ke_device* devs) {
+  if (n < 0 || n > KE_DEV_TYPES * KE_MAX_MINORS || (n > 0 && !devs)) return fail(KE_ERR_INVALID, "device count");
+  uint64_t seen = 0;
+  for (int32_t i = 0; i < n; i++) {
+    const ke_device& d = devs[i];
+    if (d.type < 0 || d.type >= KE_DEV_TYPES || d.minor < 0 || d.minor >= KE_MAX_MINORS)
+      return fail(KE_ERR_INVALID, "device type / minor out of range");
+    const uint64_t bit = 1ull << (16 * d.type + d.minor);
+    if (seen & bit) return fail(KE_ERR_INVALID, "duplicate device minor");
+    seen |= bit;
+    for (int k = DS_NK[d.type]; k < KE_DKEYS; k++)
+      if (d.has_total[k] || d.has_used[k]) return fail(KE_ERR_UNSUPPORTED, "resource key outside the device type");
+    for (int k = 0; k < KE_DKEYS; k++)
+      if ((d.has_total[k] && d.total[k] < 0) || (d.has_used[k] && d.used[k] < 0))
+        return fail(KE_ERR_INVALID, "negative device quantity");
+    // fillGPUTotalMem divides by the instance's gpu-memory (devicehandler_gpu.go:110-125)
+    if (d.type == KE_DEV_GPU && d.health && !(d.has_total[KE_DKEY_GPU_MEMORY] && d.total[KE_DKEY_GPU_MEMORY] > 0))
+      return fail(KE_ERR_UNSUPPORTED, "healthy GPU device without a positive gpu-memory total");
+  }
+  return KE_OK;
+}
+
+void derive_ds_row(const NodeState& ns, int64_t* f, uint64_t* m) {
+  for (int i = 0; i < NUM_DS_FIELDS; i++) f[i] = 0;
+  for (int i = 0; i < NUM_DS_MASKS; i++) m[i] = 0;
+  if (!ns.has_dev_cache) return;
+  for (const ke_device& d : ns.devs) {
+    const int t = d.type, mi = d.minor;
+    m[DSM_EXISTS] |= 1ull << (16 * t + mi);
+    for (int k = 0; k < DS_NK[t]; k++) {
+      if (d.health && d.has_total[k]) {  // unhealthy: empty total (device_cache.go:558-560)
+        m[ds_ht_word(t)] |= 1ull << ds_ht_bit(t, mi, k);
+        f[DS_TBASE[t] + mi * DS_NK[t] + k] = d.total[k];
+      }
+      if (d.has_used[k]) {
+        m[ds_hu_word(t)] |= 1ull << ds_hu_bit(t, mi, k);
+        f[DS_UBASE[t] + mi * DS_NK[t] + k] = d.used[k];
+      }
+    }
+  }
+}
+
+void host_ds_reserve(const ke_config& cfg, NodeState& ns, const DevPod& dp, uint64_t mask) {
+  (void)cfg;
+  for (ke_device& d : ns.devs) {
+    if (!(mask & (1ull << (16 * d.type + d.minor)))) continue;
+    const int t = d.type;
+    int64_t alloc[KE_DKEYS] = {0, 0, 0};
+    bool has[KE_DKEYS] = {false, false, false};
+    if (t == KE_DEV_GPU) {
+      const int64_t tm = d.health && d.has_total[KE_DKEY_GPU_MEMORY] ? d.total[KE_DKEY_GPU_MEMORY] : 0;
+      if (dp.flags & PF_DS_H_CORE) has[0] = true, alloc[0] = dp.ds_req[0];
+      if (dp.flags & PF_DS_H_RATIO) {  // memoryRatioToBytes
+        has[2] = true, alloc[2] = dp.ds_req[2];
+        has[1] = true, alloc[1] = dp.ds_req[2] * tm / 100;
+      } else if (dp.flags & PF_DS_H_MEM) {  // memoryBytesToRatio
+        has[1] = true, alloc[1] = dp.ds_req[1];
+        has[2] = true, alloc[2] = (int64_t)((double)dp.ds_req[1] / (double)tm * 100.0);
+      }
+    } else {
+      has[0] = true, alloc[0] = dp.ds_req[2 + t];
+    }
+    for (int k = 0; k < DS_NK[t]; k++)
+      if (has[k]) {  // quotav1.Add
+        d.used[k] = (d.has_used[k] ? d.used[k] : 0) + alloc[k];
+        d.has_used[k] = 1;
+      }
+  }
+}
+
 int validate_pod(const ke_pod& p) {
   // AllowUseCPUSet (nodenumaresource/util.go:49-56) with the default FullPCPUs bind policy makes the
   // pod a cpuset pod (plugin.go:276-301): that path (cpu accumulator, NUMA hints) is a later §8 row.
@@ -71,6 +148,10 @@ int validate_pod(const ke_pod& p) {
   if (cpuset || p.has_resource_spec)
     return fail(KE_ERR_UNSUPPORTED, "cpuset (LSE/LSR koord-prod) pods are not implemented in ABI v1");
   if (p.priority_class < 0 || p.priority_class > KE_PRIORITY_FREE) return fail(KE_ERR_INVALID, "priority class");
+  if (p.has_unsupported_device_requests)
+    return fail(KE_ERR_UNSUPPORTED, "Huawei NPU / Hygon DCU device requests are not implemented");
+  for (int i = 0; i < KE_PDR_COUNT; i++)
+    if (p.device_requests[i] < 0) return fail(KE_ERR_INVALID, "negative device request");
   return KE_OK;
 }
 
@@ -138,6 +219,79 @@ void estimate_pod(const ke_loadaware_args& a, const ke_pod& pod, int64_t* est, u
   }
 }
 
+// DeviceShare PreFilter for one pod: GetPodDeviceRequests -> ValidateDeviceRequest ->
+// ConvertDeviceRequest (deviceshare/utils.go:304-342,392-412), calcDesiredRequestsAndCountForGPU
+// (devicehandler_gpu.go:53-96) and DefaultDeviceHandler.CalcDesiredRequestsAndCount
+// (devicehandler_default.go:44-93, no hint).  Returns false when the request is invalid.
+static bool percentage_ok(int64_t q) { return !(q > 100 && q % 100 != 0); }  // ValidatePercentageResource
+
+static bool ds_prepare(const ke_pod& pod, DevPod& d) {
+  const int64_t* q = pod.device_requests;
+  bool nv = q[KE_PDR_NVIDIA_GPU] > 0, amd = q[KE_PDR_AMD_GPU] > 0, kg = q[KE_PDR_KOORD_GPU] > 0;
+  bool sh = q[KE_PDR_GPU_SHARED] > 0, co = q[KE_PDR_GPU_CORE] > 0, me = q[KE_PDR_GPU_MEMORY] > 0,
+       ra = q[KE_PDR_GPU_MEMORY_RATIO] > 0;
+  const int kinds = nv + amd + kg + (sh || co || me || ra);
+  if (kinds > 1) return false;  // no ValidDeviceResourceCombinations entry mixes these
+  int64_t core = 0, mem = 0, ratio = 0;
+  bool h_core = false, h_mem = false, h_ratio = false, any_gpu = true;
+  int64_t n = 1;
+  if (nv || amd) {
+    core = ratio = 100 * q[nv ? KE_PDR_NVIDIA_GPU : KE_PDR_AMD_GPU];
+    h_core = h_ratio = true;
+  } else if (kg) {
+    if (!percentage_ok(q[KE_PDR_KOORD_GPU])) return false;
+    core = ratio = q[KE_PDR_KOORD_GPU];
+    h_core = h_ratio = true;
+  } else if (sh) {  // GPUShared | {GPUMemory | GPUMemoryRatio} [| GPUCore]
+    if (me == ra) return false;
+    const int64_t s = q[KE_PDR_GPU_SHARED];
+    if (co && (q[KE_PDR_GPU_CORE] % s != 0 || q[KE_PDR_GPU_CORE] / s > 100)) return false;
+    if (ra && (q[KE_PDR_GPU_MEMORY_RATIO] % s != 0 || q[KE_PDR_GPU_MEMORY_RATIO] / s > 100)) return false;
+    n = s;
+    core = q[KE_PDR_GPU_CORE], mem = q[KE_PDR_GPU_MEMORY], ratio = q[KE_PDR_GPU_MEMORY_RATIO];
+    h_core = co, h_mem = me, h_ratio = ra;
+  } else if (co || me || ra) {  // GPUMemory | GPUMemoryRatio | GPUCore+either (percentage checks)
+    if (me == ra) return false;
+    if (co && !percentage_ok(q[KE_PDR_GPU_CORE])) return false;
+    if (ra && !percentage_ok(q[KE_PDR_GPU_MEMORY_RATIO])) return false;
+    core = q[KE_PDR_GPU_CORE], mem = q[KE_PDR_GPU_MEMORY], ratio = q[KE_PDR_GPU_MEMORY_RATIO];
+    h_core = co, h_mem = me, h_ratio = ra;
+  } else {
+    any_gpu = false;
+  }
+  if (any_gpu) {
+    if (!sh && h_ratio && ratio > 100 && ratio % 100 == 0) n = ratio / 100;
+    if (n > 255) return false;
+    d.ds_cnt[KE_DEV_GPU] = (uint8_t)n;
+    if (h_core) {
+      d.flags |= PF_DS_H_CORE;
+      d.ds_req[0] = core / n;
+    }
+    if (h_ratio) {  // ratio wins over memory (devicehandler_gpu.go:83-92)
+      d.flags |= PF_DS_H_RATIO;
+      d.ds_req[2] = ratio / n;
+    } else if (h_mem) {
+      d.flags |= PF_DS_H_MEM;
+      d.ds_req[1] = mem / n;
+    }
+  }
+  const int pdr[2] = {KE_PDR_RDMA, KE_PDR_FPGA};
+  for (int i = 0; i < 2; i++) {
+    const int64_t v = q[pdr[i]];
+    if (v <= 0) continue;
+    if (!percentage_ok(v)) return false;
+    int64_t c = 1, per = v;
+    if (v > 100 && v % 100 == 0) {
+      c = v / 100;
+      per = v / c;
+    }
+    if (c > 255) return false;
+    d.ds_cnt[1 + i] = (uint8_t)c;
+    d.ds_req[3 + i] = per;
+  }
+  return true;
+}
+
 DevPod make_dev_pod(const ke_config& cfg, const ke_pod& pod) {
   DevPod d{};
   uint8_t present[KE_NRES];
@@ -152,6 +306,13 @@ DevPod make_dev_pod(const ke_config& cfg, const ke_pod& pod) {
   if (zero) f |= PF_NUMA_SKIP;
   if (pod.priority_class == KE_PRIORITY_PROD && cfg.loadaware.score_according_prod_usage) f |= PF_LA_SCORE_PROD;
   d.flags = f;
+  if (!ds_prepare(pod, d)) {
+    for (int t = 0; t < 3; t++) d.ds_cnt[t] = 0;
+    for (int i = 0; i < 5; i++) d.ds_req[i] = 0;
+    d.flags = f | PF_DS_INVALID;
+  } else if (d.ds_cnt[0] || d.ds_cnt[1] || d.ds_cnt[2]) {
+    d.flags |= PF_DS;
+  }
   return d;
 }
 
@@ -385,6 +546,7 @@ void derive_row(const ke_config& cfg, const NodeState& ns, int64_t now, Row* row
   }
   if (ratio_s > 1.0) flags |= NF_NUMA_RATIO_S;
   row->f[F_CSAS] = amplify(cs_milli, ratio_s);
+  if (ns.has_dev_cache) flags |= NF_DS_CACHE;
   row->flags = flags;
 }
 

@@ -27,6 +27,9 @@ struct NodeState {
   std::vector<ke_pod_metric> pm;
   std::vector<ke_aggregated_usage> agg;
   std::vector<AssignedPod> asg;
+  // DeviceShare node device cache entry (device_cache.go:518-568)
+  bool has_dev_cache = false;
+  std::vector<ke_device> devs;
   // derived
   bool dirty = true;            // row must be re-derived and uploaded
   int64_t valid_until = INT64_MAX;  // derived row is exact for now < valid_until
@@ -40,6 +43,8 @@ struct Context {
   KArgs kargs_template{};
   std::vector<NodeState> nodes;  // size = node_capacity
   int32_t n_nodes = 0;           // 1 + highest populated index
+  bool ds_enabled = false;       // some node has a device cache entry: the device SoA exists
+  std::vector<uint64_t> last_dev_alloc;  // per pod of the last ke_schedule
   DeviceState* dev = nullptr;
   // last ke_schedule timing
   double last_total_ms = 0.0;
@@ -74,5 +79,13 @@ int64_t usage_percent(int64_t used, int64_t total);
 
 // host mirror of Reserve (podAssignCache.assign + NodeInfo.Requested += requests)
 void host_assign(const ke_config& cfg, NodeState& ns, const ke_pod& pod, int64_t timestamp_ns);
+
+// DeviceShare
+int validate_devices(int32_t n, const ke_device* devs);
+// the device SoA row of a node: NUM_DS_FIELDS int64 + NUM_DS_MASKS uint64 (zero when no cache entry)
+void derive_ds_row(const NodeState& ns, int64_t* f, uint64_t* masks);
+// host mirror of DeviceShare Reserve: add the allocation of `pod` on the minors in `mask`
+// (bit 16*type+minor) to the node's device cache (fillGPUTotalMem + updateCacheUsed)
+void host_ds_reserve(const ke_config& cfg, NodeState& ns, const DevPod& dp, uint64_t mask);
 
 }  // namespace ke

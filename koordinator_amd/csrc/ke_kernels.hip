@@ -26,6 +26,10 @@
 
 namespace ke {
 
+// wave-wide reductions from the device library (DPP)
+extern "C" __device__ uint32_t __ockl_wfred_max_u32(uint32_t);
+extern "C" __device__ int32_t __ockl_wfred_add_i32(int32_t);
+
 #define HIP_OK(expr)                                                                 \
   do {                                                                               \
     hipError_t _e = (expr);                                                          \
@@ -43,6 +47,8 @@ struct SoA {
   int64_t* f;       // NUM_I64_FIELDS arrays of `stride` int64
   uint32_t* flags;  // `stride` u32
   int64_t stride;
+  int64_t* ds;      // DeviceShare: NUM_DS_FIELDS arrays of `stride` int64 (nullptr until a device cache appears)
+  uint64_t* dsm;    // DeviceShare: NUM_DS_MASKS arrays of `stride` uint64
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -132,20 +138,220 @@ __device__ __forceinline__ bool node_expired(const NodeRegs& r, const KArgs& k) 
 }
 
 struct EvalOut {
-  int32_t total;  // -1 = filtered out
+  int32_t total;  // -1 = filtered out; else Σ weight·score of LoadAware + NodeNUMAResource (DeviceShare
+                  // enters after NormalizeScore, once the pod's max over feasible nodes is known)
   uint8_t status, reason;
-  int16_t la, numa;
+  int16_t la, numa, ds;  // ds: DeviceShare.Score before NormalizeScore
 };
 
+// ---------------------------------------------------------------------------------------------
+// DeviceShare on one node (pkg/scheduler/plugins/deviceshare).  The device
+// cache of node i is read straight from the device SoA (L1/L2-resident across the pods of a block).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t dsf(const SoA& s, int field, int64_t i) { return s.ds[field * s.stride + i]; }
+__device__ __forceinline__ uint64_t dsmask(const SoA& s, int w, int64_t i) { return s.dsm[w * s.stride + i]; }
+
+__device__ __forceinline__ bool pod_req_has(const DevPod& p, int t, int k) {
+  if (t != KE_DEV_GPU) return true;
+  return (p.flags & (k == 0 ? PF_DS_H_CORE : (k == 1 ? PF_DS_H_MEM : PF_DS_H_RATIO))) != 0;
+}
+
+// One device instance as nodeDevice.filter leaves it (device_cache.go:360-415): free_orig =
+// SubtractWithNonNegativeResult(total, used); used' = total - free_orig (dropped when zero);
+// free' = used' zero ? total : total - used'.  Keys: presence bits.
+struct DsInst {
+  int64_t tv[3], fv[3];
+  uint32_t th, fh;  // key presence of total / free'
+};
+__device__ __forceinline__ void ds_instance(const SoA& s, int64_t i, int t, int m, const uint64_t msk[4], DsInst& d) {
+  const int nk = DS_NK[t];
+  int64_t up[3];
+  uint32_t uh = 0;
+  d.th = 0;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    d.tv[k] = 0;
+    up[k] = 0;
+    d.fv[k] = 0;
+    if (k >= nk) continue;
+    const bool ht = (msk[ds_ht_word(t)] >> ds_ht_bit(t, m, k)) & 1;
+    const bool hu = (msk[ds_hu_word(t)] >> ds_hu_bit(t, m, k)) & 1;
+    const int64_t tv = ht ? dsf(s, DS_TBASE[t] + m * nk + k, i) : 0;
+    const int64_t uv = hu ? dsf(s, DS_UBASE[t] + m * nk + k, i) : 0;
+    const int64_t fo = ht ? (tv - uv > 0 ? tv - uv : 0) : 0;  // free_orig (used-only keys: 0)
+    up[k] = ht ? (tv - fo > 0 ? tv - fo : 0) : 0;            // used' (keys of total U used)
+    d.tv[k] = tv;
+    d.th |= (uint32_t)ht << k;
+    uh |= (uint32_t)(ht || hu) << k;
+  }
+  bool up_zero = true;
+#pragma unroll
+  for (int k = 0; k < 3; k++) up_zero = up_zero && !(((uh >> k) & 1) && up[k] != 0);
+  d.fh = up_zero ? d.th : uh;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const bool ht = (d.th >> k) & 1;
+    d.fv[k] = up_zero ? d.tv[k] : (ht ? (d.tv[k] - up[k] > 0 ? d.tv[k] - up[k] : 0) : 0);
+  }
+}
+
+// quotav1.IsZero(free') false and quotav1.LessThanOrEqual(request, free')
+__device__ __forceinline__ bool ds_satisfied(const DsInst& d, const DevPod& p, int t) {
+  bool zero = true, leq = true;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const bool fh = (d.fh >> k) & 1;
+    zero = zero && !(fh && d.fv[k] != 0);
+    if (fh && k < DS_NK[t] && pod_req_has(p, t, k) && p.ds_req[ds_req_slot(t, k)] > d.fv[k]) leq = false;
+  }
+  return !zero && leq;
+}
+
+__device__ __forceinline__ int64_t ds_res_score(bool most, int64_t req, int64_t cap) {  // scoring.go:283-322
+  if (cap == 0) return 0;
+  if (most) return (req > cap ? cap : req) * 100 / cap;
+  return req > cap ? 0 : (cap - req) * 100 / cap;
+}
+
+// resourceAllocationScorer.scorer over per-key (requested, allocatable) with weights (scoring.go:268-297)
+__device__ __forceinline__ int64_t ds_weighted(const KArgs& k, int t, const int64_t* tot, const int64_t* fre,
+                                               const DevPod& p) {
+  int64_t sc = 0, ws = 0;
+  for (int key = 0; key < DS_NK[t]; key++) {
+    const int wi = ds_weight_index(t, key);
+    if (wi < 0 || k.w_ds[wi] < 0 || tot[key] == 0) continue;
+    const int64_t pr = pod_req_has(p, t, key) ? p.ds_req[ds_req_slot(t, key)] : 0;
+    const int64_t req = tot[key] >= fre[key] ? tot[key] - fre[key] + pr : tot[key];
+    sc += ds_res_score(k.flags & AF_DS_MOST, req, tot[key]) * k.w_ds[wi];
+    ws += k.w_ds[wi];
+  }
+  return ws ? sc / ws : 0;
+}
+
+// Filter (Prepare + per-type count of satisfiable instances) and raw Score of DeviceShare for a pod
+// with PF_DS on a node with a cache entry.  Types in the fixed order GPU, RDMA, FPGA.
+__device__ __noinline__ void ds_filter_score(const SoA& s, int64_t i, const DevPod& p, const KArgs& k, EvalOut& o) {
+  uint64_t msk[4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) msk[w] = dsmask(s, w, i);
+  for (int t = 0; t < 3; t++)  // AutopilotAllocator.Prepare: a requested type without devices
+    if (p.ds_cnt[t] && !((msk[DSM_EXISTS] >> (16 * t)) & 0xFFFF)) {
+      o.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+      o.reason = (uint8_t)(KE_REASON_DS_INSUFFICIENT_GPU + t);
+      return;
+    }
+  int64_t raw = 0;
+  for (int t = 0; t < 3; t++) {
+    if (!p.ds_cnt[t]) continue;
+    uint64_t ex = (msk[DSM_EXISTS] >> (16 * t)) & 0xFFFF;
+    int n_ok = 0;
+    int64_t tot[3] = {0, 0, 0}, fre[3] = {0, 0, 0};
+    while (ex) {
+      const int m = __builtin_ctzll(ex);
+      ex &= ex - 1;
+      DsInst d;
+      ds_instance(s, i, t, m, msk, d);
+      n_ok += ds_satisfied(d, p, t);
+#pragma unroll
+      for (int key = 0; key < 3; key++) {
+        tot[key] += ((d.th >> key) & 1) ? d.tv[key] : 0;
+        fre[key] += ((d.fh >> key) & 1) ? d.fv[key] : 0;
+      }
+    }
+    if (n_ok < p.ds_cnt[t]) {  // defaultAllocateDevices: "Insufficient <type> devices"
+      o.status = KE_CODE_UNSCHEDULABLE;
+      o.reason = (uint8_t)(KE_REASON_DS_INSUFFICIENT_GPU + t);
+      return;
+    }
+    raw += ds_weighted(k, t, tot, fre, p);  // resourceAllocationScorer.scoreNode
+  }
+  o.ds = (int16_t)raw;
+}
+
+// DeviceShare Reserve (plugin.go:426-492): per type, the instances in (scoreDevice desc, minor asc)
+// order (device_resources.go:171-208), the first ds_cnt that are satisfiable; the allocation
+// (request + fillGPUTotalMem, devicehandler_gpu.go:98-133) is added to `used` in the SoA
+// (updateCacheUsed).  Returns the minors mask (bit 16*type + minor).
+__device__ __noinline__ uint64_t ds_reserve(const SoA& s, int64_t i, const DevPod& p, const KArgs& k) {
+  uint64_t msk[4], out = 0;
+#pragma unroll
+  for (int w = 0; w < 4; w++) msk[w] = dsmask(s, w, i);
+  for (int t = 0; t < 3; t++) {
+    if (!p.ds_cnt[t]) continue;
+    const int nk = DS_NK[t];
+    int64_t score[DS_MINORS];
+    uint32_t ok = 0;
+    uint64_t ex = (msk[DSM_EXISTS] >> (16 * t)) & 0xFFFF;
+    while (ex) {
+      const int m = __builtin_ctzll(ex);
+      ex &= ex - 1;
+      DsInst d;
+      ds_instance(s, i, t, m, msk, d);
+      if (ds_satisfied(d, p, t)) ok |= 1u << m;
+      int64_t tot[3], fre[3];
+#pragma unroll
+      for (int key = 0; key < 3; key++) {
+        tot[key] = ((d.th >> key) & 1) ? d.tv[key] : 0;
+        fre[key] = ((d.fh >> key) & 1) ? d.fv[key] : 0;
+      }
+      score[m] = ds_weighted(k, t, tot, fre, p);  // scoreDevice
+    }
+    for (int c = 0; c < p.ds_cnt[t] && ok; c++) {
+      int best = -1;
+      for (uint32_t r = ok; r; r &= r - 1) {
+        const int m = __builtin_ctz(r);
+        if (best < 0 || score[m] > score[best]) best = m;  // ascending minors: ties keep the lower
+      }
+      ok &= ~(1u << best);
+      out |= 1ull << (16 * t + best);
+      int64_t alloc[3] = {0, 0, 0};
+      bool has[3] = {false, false, false};
+      if (t == KE_DEV_GPU) {
+        const bool htm = (msk[DSM_GPU_HT] >> ds_ht_bit(0, best, 1)) & 1;
+        const int64_t tm = htm ? dsf(s, DS_TBASE[0] + best * 3 + 1, i) : 0;
+        if (p.flags & PF_DS_H_CORE) has[0] = true, alloc[0] = p.ds_req[0];
+        if (p.flags & PF_DS_H_RATIO) {  // memoryRatioToBytes
+          has[2] = true, alloc[2] = p.ds_req[2];
+          has[1] = true, alloc[1] = p.ds_req[2] * tm / 100;
+        } else if (p.flags & PF_DS_H_MEM) {  // memoryBytesToRatio: int64(float64(b)/float64(total)*100)
+          has[1] = true, alloc[1] = p.ds_req[1];
+          has[2] = true, alloc[2] = (int64_t)((double)p.ds_req[1] / (double)tm * 100.0);
+        }
+      } else {
+        has[0] = true, alloc[0] = p.ds_req[2 + t];
+      }
+      for (int key = 0; key < nk; key++) {
+        if (!has[key]) continue;
+        const int w = ds_hu_word(t), b = ds_hu_bit(t, best, key);
+        const int field = DS_UBASE[t] + best * nk + key;
+        const int64_t prev = ((msk[w] >> b) & 1) ? dsf(s, field, i) : 0;
+        s.ds[field * s.stride + i] = prev + alloc[key];  // quotav1.Add
+        msk[w] |= 1ull << b;
+      }
+    }
+  }
+#pragma unroll
+  for (int w = 1; w < 4; w++) s.dsm[w * s.stride + i] = msk[w];
+  return out;
+}
+
+// `s`/`i` locate the node's DeviceShare state (read only for pods with PF_DS).
 template <bool FULL>
-__device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, const DevPod& p, const KArgs& k) {
+__device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, const DevPod& p, const KArgs& k,
+                                             const SoA& s, int64_t i) {
   EvalOut o;
   o.status = KE_CODE_SUCCESS;
   o.reason = KE_REASON_NONE;
-  o.la = o.numa = 0;
+  o.la = o.numa = o.ds = 0;
   const uint32_t nf = n.flags;
   if (!(nf & NF_VALID)) {
     o.status = KE_CODE_ERROR;
+    o.total = -1;
+    return o;
+  }
+  if (p.flags & PF_DS_INVALID) {  // DeviceShare PreFilter failed: the pod fits nowhere (utils.go:355-390)
+    o.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    o.reason = KE_REASON_DS_INVALID_REQUEST;
     o.total = -1;
     return o;
   }
@@ -188,8 +394,11 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
       }
     }
   }
+  // ---- DeviceShare.Filter + raw Score  plugin.go:311-365, scoring.go:45-103
+  if (o.status == KE_CODE_SUCCESS && (p.flags & PF_DS) && (nf & NF_DS_CACHE)) ds_filter_score(s, i, p, k, o);
   if (o.status != KE_CODE_SUCCESS) {
     o.total = -1;
+    o.ds = 0;
     return o;
   }
   // ---- LoadAwareScheduling.Score  load_aware.go:201-249,387-406
@@ -266,11 +475,14 @@ __global__ void k_gather_rows(SoA s, Row* __restrict__ rows, int n) {
   rows[i] = r;
 }
 
-// parity mode: full status / score matrices [pod][node] + selectHost per pod
+// parity mode: full status / score matrices [pod][node]; `total` holds the LoadAware + NUMA part
+// until k_parity_finalize adds the normalized DeviceShare score.  dsmax[p] = 1 + max raw DeviceShare
+// score over the pod's feasible nodes (DefaultNormalizeScore's maxCount).
 __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_parity(SoA s, int n_nodes, const DevPod* __restrict__ pods,
                                                             int n_pods, int pods_per_block, KArgs k,
                                                             uint8_t* status, uint8_t* reason, int16_t* la,
-                                                            int16_t* numa, int16_t* total, uint32_t* best_key) {
+                                                            int16_t* numa, int16_t* ds, int16_t* total,
+                                                            uint32_t* dsmax) {
   const int i = blockIdx.x * EVAL_BLOCK + threadIdx.x;
   const bool live = i < n_nodes;
   NodeRegs n;
@@ -282,29 +494,56 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_parity(SoA s, int n_nodes, 
   const int p0 = blockIdx.y * pods_per_block;
   const int p1 = min(n_pods, p0 + pods_per_block);
   for (int p = p0; p < p1; p++) {
-    uint32_t key = 0;
+    uint32_t m = 0;
     if (live) {
-      const EvalOut o = eval_pair<true>(n, expired, pods[p], k);
+      const EvalOut o = eval_pair<true>(n, expired, pods[p], k, s, i);
       const int64_t o_idx = (int64_t)p * n_nodes + i;
-      if (status) status[o_idx] = o.status;
-      if (reason) reason[o_idx] = o.reason;
-      if (la) la[o_idx] = o.la;
-      if (numa) numa[o_idx] = o.numa;
-      if (total) total[o_idx] = (int16_t)o.total;
-      key = make_key(o.total, i);
+      status[o_idx] = o.status;
+      reason[o_idx] = o.reason;
+      la[o_idx] = o.la;
+      numa[o_idx] = o.numa;
+      ds[o_idx] = o.ds;
+      total[o_idx] = (int16_t)o.total;
+      m = o.total >= 0 ? (uint32_t)o.ds + 1 : 0u;
     }
-    // wave max, one atomic per wave
-    for (int off = 32; off > 0; off >>= 1) key = max(key, (uint32_t)__shfl_xor((int)key, off, 64));
-    if ((threadIdx.x & 63) == 0 && key) atomicMax(&best_key[p], key);
+    m = __ockl_wfred_max_u32(m);
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(&dsmax[p], m);
   }
 }
 
-// batch mode: 9-bit score per (pod,node): (total+1) or 0 when filtered out
+// DeviceShare NormalizeScore (DefaultNormalizeScore(MaxNodeScore, false): score*100/max when max > 0)
+__device__ __forceinline__ int32_t ds_norm(int32_t raw, uint32_t dsmax1) {
+  const int32_t mx = dsmax1 > 0 ? (int32_t)dsmax1 - 1 : 0;
+  return mx > 0 ? raw * 100 / mx : raw;
+}
+
+// normalized DeviceShare score into the weighted sum, then selectHost's packed-key max per pod
+__global__ __launch_bounds__(EVAL_BLOCK) void k_parity_finalize(int n_nodes, KArgs k, const int16_t* ds,
+                                                                int16_t* total, const uint32_t* dsmax,
+                                                                uint32_t* best_key) {
+  const int i = blockIdx.x * EVAL_BLOCK + threadIdx.x;
+  const int p = blockIdx.y;
+  uint32_t key = 0;
+  if (i < n_nodes) {
+    const int64_t o = (int64_t)p * n_nodes + i;
+    int32_t t = total[o];
+    if (t >= 0) {
+      t += k.wp_ds * ds_norm(ds[o], dsmax[p]);
+      total[o] = (int16_t)t;
+    }
+    key = make_key(t, i);
+  }
+  key = __ockl_wfred_max_u32(key);
+  if ((threadIdx.x & 63) == 0 && key) atomicMax(&best_key[p], key);
+}
+
+// batch mode: 9-bit score per (pod,node): (total+1) or 0 when filtered out; for a DeviceShare pod
+// (always alone in its batch) also dsraw[node] = raw DeviceShare score + 1 (0 when filtered out).
 // Nodes [lo, hi) of the SoA (this rank's shard); scores stay indexed by the global node index.
 __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi, const DevPod* __restrict__ pods,
                                                            const int32_t* __restrict__ batch_base, int batch_pods,
                                                            int pods_per_block, KArgs k, uint16_t* __restrict__ scores,
-                                                           int64_t score_stride) {
+                                                           int64_t score_stride, uint16_t* __restrict__ dsraw) {
   const int i = lo + blockIdx.x * EVAL_BLOCK + threadIdx.x;
   if (i >= hi) return;
   NodeRegs n;
@@ -315,14 +554,14 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
   const int p0 = blockIdx.y * pods_per_block;
   const int p1 = min(batch_pods, p0 + pods_per_block);
   for (int p = p0; p < p1; p++) {
-    const EvalOut o = eval_pair<false>(n, expired, pods[base + p], k);
+    const DevPod& pod = pods[base + p];
+    const EvalOut o = eval_pair<false>(n, expired, pod, k, s, i);
     scores[(int64_t)p * score_stride + i] = (uint16_t)(o.total + 1);
+    if (pod.flags & PF_DS) dsraw[i] = o.total >= 0 ? (uint16_t)(o.ds + 1) : (uint16_t)0;
   }
 }
 
 // ---- wave-wide primitives (DPP reductions from the device library, ballots) ---------------------
-extern "C" __device__ uint32_t __ockl_wfred_max_u32(uint32_t);
-extern "C" __device__ int32_t __ockl_wfred_add_i32(int32_t);
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) { return __ockl_wfred_max_u32(v); }
 __device__ __forceinline__ int wave_sum(int v) { return __ockl_wfred_add_i32(v); }
 __device__ __forceinline__ int lanes_below(uint64_t m) {  // popcount of m over lanes < this lane
@@ -341,8 +580,8 @@ __device__ __forceinline__ int lane_prefix16(int c, int* total) {
   return pre;
 }
 
-// 8 consecutive 9-bit scores of one pod starting at node i (i % 8 == 0), 0 beyond `end`
-__device__ __forceinline__ void load8(const uint16_t* sc, int i, int end, uint32_t v[8]) {
+// 8 consecutive u16 values starting at node i (i % 8 == 0), 0 beyond `end`
+__device__ __forceinline__ void load8_raw(const uint16_t* sc, int i, int end, uint32_t v[8]) {
   if (i + 8 <= end) {
     const uint4 q = *reinterpret_cast<const uint4*>(sc + i);
     const uint32_t w[4] = {q.x, q.y, q.z, q.w};
@@ -357,6 +596,33 @@ __device__ __forceinline__ void load8(const uint16_t* sc, int i, int end, uint32
   }
 }
 
+// DeviceShare NormalizeScore folded into the select: lut[raw] = weight * normalized(raw)
+struct DsNorm {
+  const uint16_t* raw;  // raw DeviceShare score + 1 per node (0 = filtered out)
+  const int16_t* lut;   // LDS, MAX_DS_RAW + 1 entries
+};
+
+// 8 consecutive framework scores (total + 1, 0 = filtered out) of one pod starting at node i
+template <bool DS>
+__device__ __forceinline__ void load8(const uint16_t* sc, int i, int end, uint32_t v[8], const DsNorm& dn) {
+  load8_raw(sc, i, end, v);
+  if (DS) {
+    uint32_t r[8];
+    load8_raw(dn.raw, i, end, r);
+#pragma unroll
+    for (int t = 0; t < 8; t++) v[t] = v[t] ? v[t] + (uint32_t)dn.lut[r[t] - 1] : 0u;
+  }
+}
+
+// 1 + max raw DeviceShare score over the feasible nodes [lo, hi) of the batch's (single) pod
+__global__ __launch_bounds__(EVAL_BLOCK) void k_dsmax(const uint16_t* __restrict__ dsraw, int lo, int hi,
+                                                      uint32_t* __restrict__ dsmax1) {
+  const int i = lo + blockIdx.x * EVAL_BLOCK + threadIdx.x;
+  uint32_t m = i < hi ? dsraw[i] : 0u;
+  m = __ockl_wfred_max_u32(m);
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(dsmax1, m);
+}
+
 constexpr int SEL_WINDOW = 64;  // histogram window below the pod's best score
 
 // Exact top-k_j per pod, k_j = min(j+1, KMAX), in (score desc, node index asc) order.  One
@@ -368,9 +634,21 @@ constexpr int SEL_WINDOW = 64;  // histogram window below the pod's best score
 //   pass 3: select score > thr, and the first need_ties nodes with score == thr by node index.
 // Nodes [lo, hi) (lo % 512 == 0: the shard boundaries keep the 16-B loads aligned); keys carry the
 // global node index, so per-shard lists merge without translation (k_merge).
+// DS: the batch is one DeviceShare pod; its scores get the normalized DeviceShare term (dsmax1 =
+// 1 + the max raw score over all feasible nodes, after the all-reduce when node-sharded).
+template <bool DS>
 __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restrict__ scores, int64_t score_stride,
                                                          int lo, int hi, uint32_t* __restrict__ cand,
-                                                         int32_t* __restrict__ cand_cnt) {
+                                                         int32_t* __restrict__ cand_cnt,
+                                                         const uint16_t* __restrict__ dsraw,
+                                                         const uint32_t* __restrict__ dsmax1, int32_t wds) {
+  __shared__ int16_t s_lut[DS ? MAX_DS_RAW + 1 : 1];
+  DsNorm dn{dsraw, s_lut};
+  if (DS) {
+    const uint32_t m1 = *dsmax1;
+    for (int x = threadIdx.x; x <= MAX_DS_RAW; x += SELECT_BLOCK) s_lut[x] = (int16_t)(wds * ds_norm(x, m1));
+    __syncthreads();
+  }
   __shared__ int32_t s_hist[SELECT_WAVES][SEL_WINDOW];
   __shared__ int32_t s_red[2][SELECT_WAVES];
   __shared__ int32_t s_thr[2];
@@ -391,7 +669,7 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
   int feas = 0;
   for (int b = w0; b < w1; b += 512) {
     uint32_t v[8];
-    load8(sc, b + lane * 8, w1, v);
+    load8<DS>(sc, b + lane * 8, w1, v, dn);
 #pragma unroll
     for (int t = 0; t < 8; t++) {
       mx = max(mx, v[t]);
@@ -416,7 +694,7 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
     // pass 2: per-wave histogram of scores in (M - 64, M]
     for (int b = w0; b < w1; b += 512) {
       uint32_t v[8];
-      load8(sc, b + lane * 8, w1, v);
+      load8<DS>(sc, b + lane * 8, w1, v, dn);
 #pragma unroll
       for (int t = 0; t < 8; t++) {
         const int d = M - (int)v[t];
@@ -454,7 +732,7 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
         int c = 0;
         for (int b = w0; b < w1; b += 512) {
           uint32_t v[8];
-          load8(sc, b + lane * 8, w1, v);
+          load8<DS>(sc, b + lane * 8, w1, v, dn);
 #pragma unroll
           for (int q = 0; q < 8; q++) c += v[q] >= (uint32_t)t;
         }
@@ -482,7 +760,7 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
       int ties = 0;
       for (int b = w0; b < w1; b += 512) {
         uint32_t v[8];
-        load8(sc, b + lane * 8, w1, v);
+        load8<DS>(sc, b + lane * 8, w1, v, dn);
 #pragma unroll
         for (int q = 0; q < 8; q++) ties += v[q] == (uint32_t)thr;
       }
@@ -500,7 +778,7 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
   for (int b = w0; b < w1; b += 512) {
     const int i0 = b + lane * 8;
     uint32_t v[8];
-    load8(sc, i0, w1, v);
+    load8<DS>(sc, i0, w1, v, dn);
     int nt = 0;
 #pragma unroll
     for (int t = 0; t < 8; t++) nt += (need_ties > 0 && v[t] == (uint32_t)thr && v[t] > 0);
@@ -621,7 +899,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
                                                 const int32_t* __restrict__ cand_cnt, int32_t* __restrict__ chosen,
                                                 int32_t* __restrict__ chosen_score, int32_t global_offset,
                                                 uint64_t* __restrict__ stamps, uint64_t* __restrict__ pstamps,
-                                                int batch_index) {
+                                                int batch_index, uint64_t* __restrict__ dev_alloc) {
   const int tid = threadIdx.x;
   if (tid == 0) pstamps[8 * batch_index] = __builtin_amdgcn_s_memrealtime();
   __shared__ uint32_t s_cand[MAX_BATCH * KMAX];
@@ -634,6 +912,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
   __shared__ DevPod s_pod[MAX_BATCH];
   __shared__ int32_t s_cnt[MAX_BATCH];
   __shared__ int32_t s_out[2][MAX_BATCH];
+  __shared__ uint64_t s_alloc[MAX_BATCH];
   __shared__ int32_t s_nslots;
   const int lane = tid & 63;
   const int base = *batch_base;
@@ -755,7 +1034,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
     const bool in_chg = ck && csl >= 0 && s_changed[csl];
     const uint32_t bu = wave_max_u32(in_chg ? 0u : ck);  // best unchanged snapshot candidate
     uint32_t kc = 0;  // exact re-evaluation of the nodes changed earlier in this batch
-    if (lane < n_chg) kc = make_key(eval_pair<false>(mine, my_expired, pod, k).total, my_node);
+    if (lane < n_chg) kc = make_key(eval_pair<false>(mine, my_expired, pod, k, s, my_node).total, my_node);
     const uint32_t bc = wave_max_u32(kc);
     const uint32_t w = max(bu, bc);
     if (w != 0) {
@@ -802,6 +1081,9 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
         }
         mine.nreq[0] += pod.req[0];
         mine.nreq[1] += pod.req[1];
+        // DeviceShare Reserve (a DeviceShare pod is alone in its batch: no later pod of the batch
+        // reads the device state it patches)
+        s_alloc[j] = (pod.flags & PF_DS) && (mine.flags & NF_DS_CACHE) ? ds_reserve(s, my_node, pod, k) : 0ull;
       }
       if (lane == 0) {
         s_out[0][j] = key_node(w) + global_offset;
@@ -810,12 +1092,14 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
     } else if (lane == 0) {
       s_out[0][j] = -1;
       s_out[1][j] = -1;
+      s_alloc[j] = 0;
     }
     wave_lds_sync();
   }
   if (lane < B) {
     chosen[base + lane] = s_out[0][lane];
     chosen_score[base + lane] = s_out[1][lane];
+    dev_alloc[base + lane] = s_alloc[lane];
   }
   // write the patched rows back to the SoA
   if (lane < n_chg) {
@@ -875,6 +1159,14 @@ struct DeviceState {
   bool loopback = false;
   ncclComm_t comm = nullptr;
   uint32_t* d_gath = nullptr;  // [world][GATH_WORDS]
+  // DeviceShare
+  bool ds_alloc = false;         // soa.ds / soa.dsm allocated
+  uint16_t* d_dsraw = nullptr;   // [capacity] raw DeviceShare score + 1 of the batch's DeviceShare pod
+  uint32_t* d_dsmax = nullptr;   // 1 + max raw score over the feasible nodes of the batch's pod
+  uint64_t* d_devalloc = nullptr;  // [n_pods] device minors allocated per pod
+  int64_t* d_dsrows = nullptr;   // staging for DeviceShare row uploads
+  int64_t ds_staging_cap = 0;
+  std::vector<DevPod> host_pods;  // the last uploaded queue (batch segmentation)
 };
 
 // Contiguous node range of shard `rank`: 512-aligned chunks (k_select's 16-B loads stay aligned).
@@ -917,6 +1209,8 @@ int device_create(Context* ctx) {
   HIP_OK(hipMalloc(&d->d_cand, sizeof(uint32_t) * MAX_BATCH * KMAX));
   HIP_OK(hipMalloc(&d->d_cand_cnt, sizeof(int32_t) * MAX_BATCH));
   HIP_OK(hipMalloc(&d->d_batch_base, sizeof(int32_t)));
+  HIP_OK(hipMalloc(&d->d_dsraw, sizeof(uint16_t) * d->capacity));
+  HIP_OK(hipMalloc(&d->d_dsmax, sizeof(uint32_t) * MAX_BATCH));
   HIP_OK(hipStreamSynchronize(d->stream));
   return KE_OK;
 }
@@ -927,8 +1221,10 @@ void device_destroy(Context* ctx) {
   (void)hipSetDevice(d->device);
   if (d->stream) (void)hipStreamSynchronize(d->stream);
   if (d->comm) (void)ncclCommDestroy(d->comm);
-  void* ptrs[] = {d->soa.f, d->soa.flags, d->d_rows, d->d_idx, d->d_pods, d->d_scores, d->d_cand, d->d_cand_cnt,
-                  d->d_batch_base, d->d_chosen, d->d_chosen_score, d->d_stamps, d->d_parity, d->d_best, d->d_gath};
+  void* ptrs[] = {d->soa.f,     d->soa.flags, d->d_rows,      d->d_idx,          d->d_pods,   d->d_scores,
+                  d->d_cand,    d->d_cand_cnt, d->d_batch_base, d->d_chosen,     d->d_chosen_score,
+                  d->d_stamps,  d->d_parity, d->d_best,       d->d_gath,         d->soa.ds,   d->soa.dsm,
+                  d->d_dsraw,   d->d_dsmax,  d->d_devalloc,   d->d_dsrows};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (d->stream) (void)hipStreamDestroy(d->stream);
@@ -985,21 +1281,66 @@ static KArgs make_kargs(const Context* ctx, int64_t now) {
   return k;
 }
 
+__global__ void k_scatter_ds(SoA s, const int64_t* __restrict__ rows, const int32_t* __restrict__ idx, int n) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int64_t i = idx[t];
+  const int64_t* r = rows + (int64_t)t * (NUM_DS_FIELDS + NUM_DS_MASKS);
+  for (int f = 0; f < NUM_DS_FIELDS; f++) s.ds[f * s.stride + i] = r[f];
+  for (int w = 0; w < NUM_DS_MASKS; w++) s.dsm[w * s.stride + i] = (uint64_t)r[NUM_DS_FIELDS + w];
+}
+
+static int ensure_ds(Context* ctx) {
+  DeviceState* d = ctx->dev;
+  if (d->ds_alloc || !ctx->ds_enabled) return KE_OK;
+  HIP_OK(hipMalloc(&d->soa.ds, sizeof(int64_t) * NUM_DS_FIELDS * d->capacity));
+  HIP_OK(hipMalloc(&d->soa.dsm, sizeof(uint64_t) * NUM_DS_MASKS * d->capacity));
+  HIP_OK(hipMemsetAsync(d->soa.ds, 0, sizeof(int64_t) * NUM_DS_FIELDS * d->capacity, d->stream));
+  HIP_OK(hipMemsetAsync(d->soa.dsm, 0, sizeof(uint64_t) * NUM_DS_MASKS * d->capacity, d->stream));
+  d->ds_alloc = true;
+  return KE_OK;
+}
+
 // Re-derive rows of dirty / time-expired nodes and scatter them into the SoA.
 int device_refresh(Context* ctx, int64_t now) {
   DeviceState* d = ctx->dev;
+  int rc = ensure_ds(ctx);
+  if (rc) return rc;
   std::vector<Row> rows;
   std::vector<int32_t> idx;
+  std::vector<int64_t> dsrows;  // DeviceShare rows of the dirty nodes (the device state is not time-dependent)
+  std::vector<int32_t> dsidx;
   for (int32_t i = 0; i < ctx->n_nodes; i++) {
     NodeState& ns = ctx->nodes[i];
     if (!ns.dirty && now < ns.valid_until) continue;
     Row r;
     int64_t vu;
     derive_row(ctx->cfg, ns, now, &r, &vu);
+    if (ns.dirty && d->ds_alloc) {
+      const size_t o = dsrows.size();
+      dsrows.resize(o + NUM_DS_FIELDS + NUM_DS_MASKS);
+      derive_ds_row(ns, &dsrows[o], reinterpret_cast<uint64_t*>(&dsrows[o + NUM_DS_FIELDS]));
+      dsidx.push_back(i);
+    }
     ns.valid_until = vu;
     ns.dirty = false;
     rows.push_back(r);
     idx.push_back(i);
+  }
+  if (!dsidx.empty()) {
+    const int64_t n = (int64_t)dsidx.size();
+    if (d->ds_staging_cap < n) {
+      if (d->d_dsrows) HIP_OK(hipFree(d->d_dsrows));
+      HIP_OK(hipMalloc(&d->d_dsrows, sizeof(int64_t) * (NUM_DS_FIELDS + NUM_DS_MASKS) * n + sizeof(int32_t) * n));
+      d->ds_staging_cap = n;
+    }
+    int32_t* didx = reinterpret_cast<int32_t*>(d->d_dsrows + (NUM_DS_FIELDS + NUM_DS_MASKS) * n);
+    HIP_OK(hipMemcpyAsync(d->d_dsrows, dsrows.data(), sizeof(int64_t) * dsrows.size(), hipMemcpyHostToDevice, d->stream));
+    HIP_OK(hipMemcpyAsync(didx, dsidx.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, d->stream));
+    hipLaunchKernelGGL(k_scatter_ds, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, d->stream, d->soa, d->d_dsrows, didx,
+                       (int)n);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(d->stream));  // `dsrows` is a local host vector
   }
   if (rows.empty()) return KE_OK;
   HIP_OK(hipSetDevice(d->device));
@@ -1022,7 +1363,8 @@ int device_refresh(Context* ctx, int64_t now) {
 
 static int upload_pods(Context* ctx, int32_t n_pods, const ke_pod* pods) {
   DeviceState* d = ctx->dev;
-  std::vector<DevPod> dp((size_t)n_pods);
+  std::vector<DevPod>& dp = d->host_pods;
+  dp.resize((size_t)n_pods);
   for (int32_t p = 0; p < n_pods; p++) dp[p] = make_dev_pod(ctx->cfg, pods[p]);
   int rc = ensure((void**)&d->d_pods, &d->pods_cap, sizeof(DevPod) * (int64_t)std::max(n_pods, 1));
   if (rc) return rc;
@@ -1032,7 +1374,7 @@ static int upload_pods(Context* ctx, int32_t n_pods, const ke_pod* pods) {
 }
 
 int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, uint8_t* status, uint8_t* reason,
-                int16_t* la, int16_t* numa, int16_t* total, int32_t* best) {
+                int16_t* la, int16_t* numa, int16_t* ds, int16_t* total, int32_t* best) {
   DeviceState* d = ctx->dev;
   HIP_OK(hipSetDevice(d->device));
   int rc = device_refresh(ctx, now);
@@ -1041,29 +1383,36 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
   rc = upload_pods(ctx, n_pods, pods);
   if (rc) return rc;
   const int64_t N = ctx->n_nodes, P = n_pods, M = N * P;
-  // parity buffers: status u8, reason u8, la i16, numa i16, total i16 = 8 B per pair
-  rc = ensure(&d->d_parity, &d->parity_cap, std::max<int64_t>(M, 1) * 8 + 16);
+  // parity buffers: status u8, reason u8, la / numa / ds / total i16 = 10 B per pair
+  rc = ensure(&d->d_parity, &d->parity_cap, std::max<int64_t>(M, 1) * 10 + 16);
   if (rc) return rc;
-  rc = ensure((void**)&d->d_best, &d->best_cap, sizeof(uint32_t) * P);
+  rc = ensure((void**)&d->d_best, &d->best_cap, sizeof(uint32_t) * 2 * P);  // best key + dsmax per pod
   if (rc) return rc;
   uint8_t* d_status = (uint8_t*)d->d_parity;
   uint8_t* d_reason = d_status + M;
   int16_t* d_la = (int16_t*)(d_reason + M + (M & 1));
   int16_t* d_numa = d_la + M;
-  int16_t* d_total = d_numa + M;
-  HIP_OK(hipMemsetAsync(d->d_best, 0, sizeof(uint32_t) * P, d->stream));
+  int16_t* d_ds = d_numa + M;
+  int16_t* d_total = d_ds + M;
+  uint32_t* d_dsmax = d->d_best + P;
+  HIP_OK(hipMemsetAsync(d->d_best, 0, sizeof(uint32_t) * 2 * P, d->stream));
   const KArgs k = make_kargs(ctx, now);
   const int ppb = 8;
-  dim3 grid((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((P + ppb - 1) / ppb));
   if (N > 0) {
+    dim3 grid((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((P + ppb - 1) / ppb));
     hipLaunchKernelGGL(k_eval_parity, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, (int)N, d->d_pods, (int)P, ppb,
-                       k, d_status, d_reason, d_la, d_numa, d_total, d->d_best);
+                       k, d_status, d_reason, d_la, d_numa, d_ds, d_total, d_dsmax);
+    HIP_OK(hipGetLastError());
+    dim3 grid2((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)P);
+    hipLaunchKernelGGL(k_parity_finalize, grid2, dim3(EVAL_BLOCK), 0, d->stream, (int)N, k, d_ds, d_total, d_dsmax,
+                       d->d_best);
     HIP_OK(hipGetLastError());
   }
   if (status) HIP_OK(hipMemcpyAsync(status, d_status, M, hipMemcpyDeviceToHost, d->stream));
   if (reason) HIP_OK(hipMemcpyAsync(reason, d_reason, M, hipMemcpyDeviceToHost, d->stream));
   if (la) HIP_OK(hipMemcpyAsync(la, d_la, M * 2, hipMemcpyDeviceToHost, d->stream));
   if (numa) HIP_OK(hipMemcpyAsync(numa, d_numa, M * 2, hipMemcpyDeviceToHost, d->stream));
+  if (ds) HIP_OK(hipMemcpyAsync(ds, d_ds, M * 2, hipMemcpyDeviceToHost, d->stream));
   if (total) HIP_OK(hipMemcpyAsync(total, d_total, M * 2, hipMemcpyDeviceToHost, d->stream));
   std::vector<uint32_t> bk((size_t)P);
   HIP_OK(hipMemcpyAsync(bk.data(), d->d_best, sizeof(uint32_t) * P, hipMemcpyDeviceToHost, d->stream));
@@ -1079,20 +1428,38 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   int rc = device_refresh(ctx, now);
   if (rc) return rc;
   ctx->last_batch_ms.clear();
+  ctx->last_dev_alloc.clear();
   ctx->last_total_ms = 0;
   if (n_pods == 0) return KE_OK;
   rc = upload_pods(ctx, n_pods, pods);
   if (rc) return rc;
+  // Batches: runs of up to B pods without DeviceShare requests (exact speculative batching, DESIGN.md
+  // §4), and every DeviceShare pod alone: its NormalizeScore needs the max over all feasible nodes of
+  // the current state.
   const int B = ctx->cfg.pod_batch;
-  const int n_batches = (n_pods + B - 1) / B;
+  std::vector<std::pair<int, bool>> batches;  // (pods, DeviceShare singleton)
+  for (int32_t p = 0; p < n_pods;) {
+    if (d->host_pods[p].flags & PF_DS) {
+      batches.push_back({1, true});
+      p++;
+      continue;
+    }
+    int bp = 0;
+    while (p + bp < n_pods && bp < B && !(d->host_pods[p + bp].flags & PF_DS)) bp++;
+    batches.push_back({bp, false});
+    p += bp;
+  }
+  const int n_batches = (int)batches.size();
   const int64_t out_bytes = sizeof(int32_t) * (int64_t)n_pods;
   if (d->out_cap < n_pods) {
     if (d->d_chosen) HIP_OK(hipFree(d->d_chosen));
     if (d->d_chosen_score) HIP_OK(hipFree(d->d_chosen_score));
     if (d->d_stamps) HIP_OK(hipFree(d->d_stamps));
+    if (d->d_devalloc) HIP_OK(hipFree(d->d_devalloc));
     HIP_OK(hipMalloc(&d->d_chosen, out_bytes));
     HIP_OK(hipMalloc(&d->d_chosen_score, out_bytes));
     HIP_OK(hipMalloc(&d->d_stamps, sizeof(uint64_t) * 10 * ((int64_t)n_pods + 2)));
+    HIP_OK(hipMalloc(&d->d_devalloc, sizeof(uint64_t) * n_pods));
     d->out_cap = n_pods;
   }
   const KArgs k = make_kargs(ctx, now);
@@ -1112,42 +1479,57 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     ev.resize((size_t)samples * 4);
     for (auto& e : ev) HIP_OK(hipEventCreate(&e));
   }
+  const bool sharded = d->world > 1 || d->comm;
   for (int b = 0; b < n_batches; b++) {
-    const int bp = std::min(B, n_pods - b * B);
+    const int bp = batches[b].first;
+    const bool ds = batches[b].second;
     const bool prof = every > 0 && b % every == 0;
     hipEvent_t* pe = prof ? &ev[(size_t)(b / every) * 4] : nullptr;
     if (prof) HIP_OK(hipEventRecord(pe[0], d->stream));
-    if (N > 0 && d->world == 1 && !d->comm) {
-      dim3 grid((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((bp + ppb - 1) / ppb));
-      hipLaunchKernelGGL(k_eval_batch, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base,
-                         bp, ppb, k, d->d_scores, d->capacity);
-      if (prof) HIP_OK(hipEventRecord(pe[1], d->stream));
-      hipLaunchKernelGGL(k_select, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, d->stream, d->d_scores, d->capacity, 0, N,
-                         d->d_cand, d->d_cand_cnt);
-    } else if (N > 0) {
-      // node-sharded: this rank's range (loopback: every range), per-shard top-k_j, all-gather, merge
+    if (N > 0) {
+      // this rank's node range (unsharded and loopback: every node)
       int lo = 0, hi = N;
-      if (!d->loopback) shard_range(N, d->rank, d->world, &lo, &hi);
+      if (sharded && !d->loopback) shard_range(N, d->rank, d->world, &lo, &hi);
       if (hi > lo) {
         dim3 grid((unsigned)((hi - lo + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((bp + ppb - 1) / ppb));
         hipLaunchKernelGGL(k_eval_batch, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, lo, hi, d->d_pods,
-                           d->d_batch_base, bp, ppb, k, d->d_scores, d->capacity);
+                           d->d_batch_base, bp, ppb, k, d->d_scores, d->capacity, d->d_dsraw);
+      }
+      if (ds) {  // DefaultNormalizeScore's max over the feasible nodes (all ranks)
+        HIP_OK(hipMemsetAsync(d->d_dsmax, 0, sizeof(uint32_t), d->stream));
+        if (hi > lo)
+          hipLaunchKernelGGL(k_dsmax, dim3((unsigned)((hi - lo + EVAL_BLOCK - 1) / EVAL_BLOCK)), dim3(EVAL_BLOCK), 0,
+                             d->stream, d->d_dsraw, lo, hi, d->d_dsmax);
+        if (sharded && !d->loopback)
+          RCCL_OK(ncclAllReduce(d->d_dsmax, d->d_dsmax, 1, ncclUint32, ncclMax, d->comm, d->stream));
       }
       if (prof) HIP_OK(hipEventRecord(pe[1], d->stream));
-      for (int r = 0; r < d->world; r++) {
-        if (!d->loopback && r != d->rank) continue;
-        int slo, shi;
-        shard_range(N, r, d->world, &slo, &shi);
-        uint32_t* blk = d->d_gath + (int64_t)r * GATH_WORDS;
-        hipLaunchKernelGGL(k_select, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, d->stream, d->d_scores, d->capacity,
-                           slo, shi, blk, reinterpret_cast<int32_t*>(blk + MAX_BATCH * KMAX));
+      auto select = [&](int slo, int shi, uint32_t* cand, int32_t* cnt) {
+        if (ds)
+          hipLaunchKernelGGL(k_select<true>, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, d->stream, d->d_scores,
+                             d->capacity, slo, shi, cand, cnt, d->d_dsraw, d->d_dsmax, k.wp_ds);
+        else
+          hipLaunchKernelGGL(k_select<false>, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, d->stream, d->d_scores,
+                             d->capacity, slo, shi, cand, cnt, d->d_dsraw, d->d_dsmax, k.wp_ds);
+      };
+      if (!sharded) {
+        select(0, N, d->d_cand, d->d_cand_cnt);
+      } else {
+        // node-sharded: per-shard top-k_j, all-gather, merge
+        for (int r = 0; r < d->world; r++) {
+          if (!d->loopback && r != d->rank) continue;
+          int slo, shi;
+          shard_range(N, r, d->world, &slo, &shi);
+          uint32_t* blk = d->d_gath + (int64_t)r * GATH_WORDS;
+          select(slo, shi, blk, reinterpret_cast<int32_t*>(blk + MAX_BATCH * KMAX));
+        }
+        if (!d->loopback) {
+          uint32_t* mine = d->d_gath + (int64_t)d->rank * GATH_WORDS;  // in place: send = own block of recv
+          RCCL_OK(ncclAllGather(mine, d->d_gath, GATH_WORDS, ncclUint32, d->comm, d->stream));
+        }
+        hipLaunchKernelGGL(k_merge, dim3((unsigned)bp), dim3(MERGE_BLOCK), 0, d->stream, d->d_gath, d->world,
+                           d->d_cand, d->d_cand_cnt);
       }
-      if (!d->loopback) {
-        uint32_t* mine = d->d_gath + (int64_t)d->rank * GATH_WORDS;  // in place: send = own block of recv
-        RCCL_OK(ncclAllGather(mine, d->d_gath, GATH_WORDS, ncclUint32, d->comm, d->stream));
-      }
-      hipLaunchKernelGGL(k_merge, dim3((unsigned)bp), dim3(MERGE_BLOCK), 0, d->stream, d->d_gath, d->world, d->d_cand,
-                         d->d_cand_cnt);
     } else {
       if (prof) HIP_OK(hipEventRecord(pe[1], d->stream));
       HIP_OK(hipMemsetAsync(d->d_cand_cnt, 0, sizeof(int32_t) * MAX_BATCH, d->stream));
@@ -1155,13 +1537,16 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     if (prof) HIP_OK(hipEventRecord(pe[2], d->stream));
     hipLaunchKernelGGL(k_resolve, dim3(1), dim3(RES_THREADS), 0, d->stream, d->soa, d->d_pods, d->d_batch_base, bp, k,
                        d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score, ctx->cfg.global_node_offset,
-                       d->d_stamps, d->d_stamps + (n_pods + 2), b);
+                       d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc);
     if (prof) HIP_OK(hipEventRecord(pe[3], d->stream));
   }
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(e1, d->stream));
   HIP_OK(hipMemcpyAsync(chosen, d->d_chosen, out_bytes, hipMemcpyDeviceToHost, d->stream));
   if (score) HIP_OK(hipMemcpyAsync(score, d->d_chosen_score, out_bytes, hipMemcpyDeviceToHost, d->stream));
+  ctx->last_dev_alloc.assign((size_t)n_pods, 0);
+  HIP_OK(hipMemcpyAsync(ctx->last_dev_alloc.data(), d->d_devalloc, sizeof(uint64_t) * n_pods, hipMemcpyDeviceToHost,
+                        d->stream));
   std::vector<uint64_t> st((size_t)n_batches + 1), pst(8 * (size_t)n_batches);
   HIP_OK(hipMemcpyAsync(st.data(), d->d_stamps, sizeof(uint64_t) * (n_batches + 1), hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipMemcpyAsync(pst.data(), d->d_stamps + (n_pods + 2), sizeof(uint64_t) * 8 * n_batches,
@@ -1234,14 +1619,14 @@ int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t 
   HIP_OK(hipMemsetAsync(d->d_batch_base, 0, sizeof(int32_t), d->stream));
   dim3 grid((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((n_pods + ppb - 1) / ppb));
   hipLaunchKernelGGL(k_eval_batch, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base, n_pods,
-                     ppb, k, d->d_scores, d->capacity);  // warm
+                     ppb, k, d->d_scores, d->capacity, d->d_dsraw);  // warm
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   HIP_OK(hipEventRecord(e0, d->stream));
   for (int it = 0; it < iters; it++)
     hipLaunchKernelGGL(k_eval_batch, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base,
-                       n_pods, ppb, k, d->d_scores, d->capacity);
+                       n_pods, ppb, k, d->d_scores, d->capacity, d->d_dsraw);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(e1, d->stream));
   HIP_OK(hipEventSynchronize(e1));

@@ -50,6 +50,7 @@ enum NodeFlag : uint32_t {
   NF_NUMA_TOPO_INVALID = 1u << 12,
   NF_NUMA_RATIO_S = 1u << 13,  // score ratio > 1
   NF_NUMA_SCORE_ZERO = 1u << 14,  // getResourceOptions error -> Score 0
+  NF_DS_CACHE = 1u << 15,         // nodeDeviceCache has an entry for the node (DeviceShare runs)
 };
 KE_HD constexpr uint32_t nf_fh_on(int v, int r) { return NF_FH_ON0 << (2 * v + r); }
 
@@ -59,6 +60,11 @@ enum PodFlag : uint32_t {
   PF_PROD = 1u << 1,           // GetPodPriorityClassWithDefault == koord-prod
   PF_NUMA_SKIP = 1u << 2,      // PodRequests all zero -> NodeNUMAResource skip
   PF_LA_SCORE_PROD = 1u << 3,  // prod && ScoreAccordingProdUsage
+  PF_DS = 1u << 4,             // DeviceShare PreFilter succeeded and did not Skip: Filter/Score run
+  PF_DS_INVALID = 1u << 5,     // DeviceShare PreFilter failed (UnschedulableAndUnresolvable everywhere)
+  PF_DS_H_CORE = 1u << 6,      // per-GPU request has gpu-core
+  PF_DS_H_MEM = 1u << 7,       // per-GPU request has gpu-memory (fill: bytes -> ratio)
+  PF_DS_H_RATIO = 1u << 8,     // per-GPU request has gpu-memory-ratio (fill: ratio -> bytes)
 };
 
 // host-side packed row (staging for uploads, debug readback)
@@ -75,9 +81,35 @@ struct DevPod {
   int64_t est[2];  // LoadAware EstimatePod (cpu milli, memory); 0 for a resource without weight
   int64_t req[2];  // PodRequests cpu milli, memory (NodeNUMAResource, NodeInfo.Requested patch)
   uint32_t flags;
-  int32_t pad;
+  uint8_t ds_cnt[3];  // DeviceShare: desired device count per type (GPU, RDMA, FPGA), 0 = not requested
+  uint8_t pad;
+  int64_t ds_req[5];  // DeviceShare per-instance request: gpu-core, gpu-memory, gpu-memory-ratio, rdma, fpga
 };
-static_assert(sizeof(DevPod) == 40, "DevPod layout");
+static_assert(sizeof(DevPod) == 80, "DevPod layout");
+
+// ---- DeviceShare device state (a second SoA, allocated when the first node device cache appears) ----
+// int64 fields: total / used per (type, minor, key); key count 3 for GPU, 1 for RDMA/FPGA.
+constexpr int DS_MINORS = 16;  // == KE_MAX_MINORS
+constexpr int DS_NK[3] = {3, 1, 1};
+constexpr int DS_TBASE[3] = {0, 96, 128};  // total[t][m][k] = DS_TBASE[t] + m*DS_NK[t] + k
+constexpr int DS_UBASE[3] = {48, 112, 144};
+constexpr int NUM_DS_FIELDS = 160;
+// uint64 mask words: exists (bit 16t+m) and the key presence of total / used
+enum DsMask : int {
+  DSM_EXISTS = 0,  // device instance (t, m) is in the cache
+  DSM_GPU_HT = 1,  // GPU total has key k: bit 16k+m (empty for unhealthy devices)
+  DSM_GPU_HU = 2,  // GPU used has key k:  bit 16k+m
+  DSM_RF = 3,      // RDMA total 0-15, RDMA used 16-31, FPGA total 32-47, FPGA used 48-63
+  NUM_DS_MASKS = 4
+};
+KE_HD inline int ds_ht_word(int t) { return t == 0 ? DSM_GPU_HT : DSM_RF; }
+KE_HD inline int ds_hu_word(int t) { return t == 0 ? DSM_GPU_HU : DSM_RF; }
+KE_HD inline int ds_ht_bit(int t, int m, int k) { return t == 0 ? 16 * k + m : (t == 1 ? m : 32 + m); }
+KE_HD inline int ds_hu_bit(int t, int m, int k) { return t == 0 ? 16 * k + m : (t == 1 ? 16 + m : 48 + m); }
+// DeviceShare score weight index of (type, key) (KE_DSW_*), -1 = none
+KE_HD inline int ds_weight_index(int t, int k) { return t == 0 ? (k == 2 ? 0 : (k == 1 ? 1 : -1)) : (t == 1 ? 2 : 3); }
+// pod per-instance request slot of (type, key)
+KE_HD inline int ds_req_slot(int t, int k) { return t == 0 ? k : 2 + t; }
 
 // kernel-uniform arguments
 enum ArgFlag : uint32_t {
@@ -85,6 +117,7 @@ enum ArgFlag : uint32_t {
   AF_ENABLE_WHEN_EXPIRED = 1u << 1, // args.EnableScheduleWhenNodeMetricsExpired
   AF_EXP_PRESENT = 1u << 2,         // args.NodeMetricExpirationSeconds != nil
   AF_NUMA_MOST = 1u << 3,           // NodeNUMAResource MostAllocated
+  AF_DS_MOST = 1u << 4,             // DeviceShare MostAllocated
 };
 struct KArgs {
   int64_t now;
@@ -94,7 +127,8 @@ struct KArgs {
   int32_t wsum_la, wsum_numa;
   int32_t wp_la, wp_numa;  // plugin weights in the profile
   uint32_t flags;
-  int32_t pad;
+  int32_t wp_ds;           // DeviceShare plugin weight
+  int32_t w_ds[4];         // DeviceShare ScoringStrategy weights (KE_DSW_*), -1 = absent
 };
 
 // Packed candidate key: higher is better.  (score+1) in the top 9 bits, inverted node index in the
@@ -103,6 +137,7 @@ constexpr uint32_t KEY_IDX_BITS = 23;
 constexpr uint32_t KEY_IDX_MASK = (1u << KEY_IDX_BITS) - 1;
 constexpr int MAX_SHARD_NODES = (1 << KEY_IDX_BITS) - 1;
 constexpr int MAX_TOTAL_SCORE = 510;  // (score+1) must fit in 9 bits
+constexpr int MAX_DS_RAW = 300;       // DeviceShare raw score: <= 100 per device type
 KE_HD inline uint32_t make_key(int32_t total, int32_t idx) {
   return total < 0 ? 0u : ((uint32_t)(total + 1) << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)idx);
 }

@@ -113,6 +113,14 @@ class Evaluator:
     def unassign(self, i, uid):
         self._check(self.lib.ke_pod_unassign(self.h, i, uid))
 
+    def set_devices(self, i, devices):
+        """DeviceShare node device cache entry (model.make_devices(...))."""
+        devices = np.ascontiguousarray(devices, dtype=abi.DEVICE_DTYPE)
+        self._check(self.lib.ke_node_devices_set(self.h, i, len(devices), abi.ptr(devices)))
+
+    def delete_devices(self, i):
+        self._check(self.lib.ke_node_devices_delete(self.h, i))
+
     def estimate_pod(self, pod):
         est = np.zeros(2, np.int64)
         self._check(self.lib.ke_estimate_pod(self.h, C.byref(pod), abi.ptr(est)))
@@ -142,12 +150,13 @@ class Evaluator:
             "reason": np.zeros((P, N), np.uint8),
             "la": np.zeros((P, N), np.int16),
             "numa": np.zeros((P, N), np.int16),
+            "ds": np.zeros((P, N), np.int16),
             "total": np.zeros((P, N), np.int16),
             "best": np.zeros(P, np.int32),
         }
         self._check(self.lib.ke_eval(self.h, P, abi.ptr(pods), int(now_ns), abi.ptr(out["status"]),
                                      abi.ptr(out["reason"]), abi.ptr(out["la"]), abi.ptr(out["numa"]),
-                                     abi.ptr(out["total"]), abi.ptr(out["best"])))
+                                     abi.ptr(out["ds"]), abi.ptr(out["total"]), abi.ptr(out["best"])))
         return out
 
     def schedule(self, pods, now_ns):
@@ -155,6 +164,8 @@ class Evaluator:
         chosen = np.zeros(len(pods), np.int32)
         score = np.zeros(len(pods), np.int32)
         self._check(self.lib.ke_schedule(self.h, len(pods), abi.ptr(pods), int(now_ns), abi.ptr(chosen), abi.ptr(score)))
+        self.last_device_allocations = np.zeros(len(pods), np.uint64)
+        self._check(self.lib.ke_last_device_allocations(self.h, len(pods), abi.ptr(self.last_device_allocations)))
         return chosen, score
 
     def stats(self):

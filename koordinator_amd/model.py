@@ -9,6 +9,8 @@ their inputs the way the reference's own tests do.
 import math
 from fractions import Fraction
 
+import numpy as np
+
 from . import abi
 
 NS = 1_000_000_000
@@ -213,6 +215,11 @@ def make_pod(name="pod", namespace="default", requests=None, limits=None, contai
     other = _fill_resources(p.requests, reqs)
     _fill_resources(p.limits, lims)
     p.has_other_requests = 1 if other else 0
+    for k, v in reqs.items():  # DeviceShare reads PodRequests (utils.go:392-412), Value() of each
+        if k in abi.PDR and v != 0:
+            p.device_requests[abi.PDR[k]] = value(v)
+        elif k in abi.UNSUPPORTED_DEVICE_RESOURCES and v != 0:
+            p.has_unsupported_device_requests = 1
     p.custom_scaling_factors[:] = [abi.ABSENT, abi.ABSENT]
     if custom_factors:
         p.has_custom_scaling_factors = 1
@@ -306,3 +313,31 @@ def make_node_metric(update_time=None, report_interval_seconds=None, node_usage=
         for t, rl in ag.get("usage", {}).items():
             aggs[i].usage[AGG_BY_NAME[t]] = resource_map(rl)
     return nm, pms, len(pods), aggs, len(aggregated)
+
+
+DEVICE_TYPE_BY_NAME = {"gpu": abi.DEV_GPU, "rdma": abi.DEV_RDMA, "fpga": abi.DEV_FPGA}
+DEVICE_KEYS = {
+    abi.DEV_GPU: {"koordinator.sh/gpu-core": abi.DKEY_GPU_CORE, "koordinator.sh/gpu-memory": abi.DKEY_GPU_MEMORY,
+                  "koordinator.sh/gpu-memory-ratio": abi.DKEY_GPU_MEMORY_RATIO},
+    abi.DEV_RDMA: {"koordinator.sh/rdma": abi.DKEY_RDMA},
+    abi.DEV_FPGA: {"koordinator.sh/fpga": abi.DKEY_FPGA},
+}
+
+
+def make_devices(devices):
+    """DeviceShare node device cache entries: [dict(type='gpu'|'rdma'|'fpga', minor, health=True,
+    total={resource: quantity}, used={resource: quantity})] -> np.ndarray(DEVICE_DTYPE)."""
+    arr = np.zeros(len(devices), dtype=abi.DEVICE_DTYPE)
+    for i, d in enumerate(devices):
+        t = DEVICE_TYPE_BY_NAME[d["type"]]
+        dev = abi.Device()
+        dev.type = t
+        dev.minor = int(d["minor"])
+        dev.health = 1 if d.get("health", True) else 0
+        for field, hfield, rl in (("total", "has_total", d.get("total")), ("used", "has_used", d.get("used"))):
+            for k, q in (rl or {}).items():
+                key = DEVICE_KEYS[t][k]
+                getattr(dev, hfield)[key] = 1
+                getattr(dev, field)[key] = value(q)
+        arr[i] = np.frombuffer(bytes(dev), dtype=abi.DEVICE_DTYPE)[0]
+    return arr

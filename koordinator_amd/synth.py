@@ -24,6 +24,7 @@ CONFIGS = {
     1: dict(nodes=1_000, pods=1_000, name="1k nodes x 1k pods, LoadAwareScheduling + NodeNUMAResource"),
     2: dict(nodes=5_000, pods=10_000, name="5k nodes x 10k pods, mixed LS/BE with NodeMetric usage"),
     3: dict(nodes=50_000, pods=100_000, name="50k nodes x 100k pods"),
+    5: dict(nodes=20_000, pods=20_000, name="20k nodes x 8 GPU + 2 RDMA, DeviceShare partial-device pods"),
 }
 
 
@@ -209,3 +210,73 @@ def shard(cl, rank, world):
                        cl.pm_offsets[lo:hi + 1] - pm0, cl.pod_metrics[pm0:pm1].copy(),
                        cl.agg_offsets[lo:hi + 1] - ag0, cl.aggregated[ag0:ag1].copy(),
                        (cl.asg_nodes[am] - lo).astype(np.int32), cl.asg_pods[am].copy(), cl.asg_ts[am].copy(), cl.now)
+
+
+# ---- DeviceShare (BASELINE config 5) -------------------------------------------------------------
+GPU_MEM = 192 * GI
+
+
+def make_devices(n_nodes, seed, gpus=8, rdmas=2, no_cache_fraction=0.05, unhealthy_fraction=0.02):
+    """Per node a DeviceShare cache entry (or None): `gpus` GPUs (gpu-core 100, gpu-memory-ratio 100,
+    gpu-memory 192Gi) and `rdmas` RDMA NICs (rdma 100) with random partial usage."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n_nodes):
+        if rng.random() < no_cache_fraction:
+            out.append(None)
+            continue
+        devs = np.zeros(gpus + rdmas, abi.DEVICE_DTYPE)
+        frac = rng.choice([0, 0, 0, 25, 50, 75, 100], gpus)
+        for m in range(gpus):
+            d = devs[m]
+            d["type"], d["minor"] = abi.DEV_GPU, m
+            d["health"] = 0 if rng.random() < unhealthy_fraction else 1
+            d["has_total"][:] = 1
+            d["total"][:] = [100, GPU_MEM, 100]
+            if frac[m]:
+                d["has_used"][:] = 1
+                d["used"][:] = [frac[m], GPU_MEM * frac[m] // 100, frac[m]]
+        for r in range(rdmas):
+            d = devs[gpus + r]
+            d["type"], d["minor"] = abi.DEV_RDMA, r
+            d["health"] = 1
+            d["has_total"][0] = 1
+            d["total"][0] = 100
+            u = rng.choice([0, 25, 50, 100])
+            if u:
+                d["has_used"][0] = 1
+                d["used"][0] = u
+        out.append(devs)
+    return out
+
+
+def load_devices(handle, devices):
+    for i, d in enumerate(devices):
+        if d is not None:
+            handle.set_devices(i, d)
+
+
+def make_ds_pods(n_pods, seed, device_fraction=0.5, key_base=2_000_000_000):
+    """Queue for config 5: the config-2 mix, of which `device_fraction` also request devices:
+    gpu-core = gpu-memory-ratio in {25,50,100,200,400,800}, nvidia.com/gpu in {1,2}, or a shared
+    gpu-memory slice; 30% of them also RDMA {50,100}; 1% carry an invalid request."""
+    rng = np.random.default_rng(seed)
+    pods = make_pods(n_pods, seed + 1, key_base=key_base)
+    dev = rng.random(n_pods) < device_fraction
+    kind = rng.random(n_pods)
+    pct = rng.choice([25, 50, 100, 200, 400, 800], n_pods)
+    for i in np.nonzero(dev)[0]:
+        r = pods["device_requests"][i]
+        if kind[i] < 0.6:
+            r[abi.PDR["koordinator.sh/gpu-core"]] = pct[i]
+            r[abi.PDR["koordinator.sh/gpu-memory-ratio"]] = pct[i]
+        elif kind[i] < 0.8:
+            r[abi.PDR["nvidia.com/gpu"]] = rng.choice([1, 2])
+        elif kind[i] < 0.99:
+            r[abi.PDR["koordinator.sh/gpu-memory"]] = rng.choice([16, 48, 96]) * GI
+        else:
+            r[abi.PDR["koordinator.sh/gpu-memory-ratio"]] = 150  # invalid: > 100 and not a multiple
+        if rng.random() < 0.3:
+            r[abi.PDR["koordinator.sh/rdma"]] = rng.choice([50, 100])
+        pods["has_other_requests"][i] = 1
+    return pods

@@ -46,8 +46,16 @@ def load():
         "or_numa_filter": (C.c_int, [V, C.POINTER(abi.Pod), i32, C.POINTER(C.c_int)]),
         "or_numa_score": (i64, [V, C.POINTER(abi.Pod), i32]),
         "or_estimate_pod": (None, [V, C.POINTER(abi.Pod), V]),
-        "or_eval": (C.c_int, [V, i32, V, i64, V, V, V, V, V, V, C.c_int]),
-        "or_schedule": (C.c_int, [V, i32, V, i64, V, V, C.c_int]),
+        "or_eval": (C.c_int, [V, i32, V, i64, V, V, V, V, V, V, V, C.c_int]),
+        "or_schedule": (C.c_int, [V, i32, V, i64, V, V, V, C.c_int]),
+        "or_node_devices_set": (C.c_int, [V, i32, i32, V]),
+        "or_node_devices_delete": (C.c_int, [V, i32]),
+        "or_ds_prefilter": (C.c_int, [C.POINTER(abi.Pod), C.POINTER(C.c_int), V, V, V]),
+        "or_ds_score_device": (i64, [V, i32, V, V, V, V, V, V]),
+        "or_normalize_scores": (None, [V, i32]),
+        "or_ds_filter": (C.c_int, [V, C.POINTER(abi.Pod), i32, C.POINTER(C.c_int)]),
+        "or_ds_score": (i64, [V, C.POINTER(abi.Pod), i32]),
+        "or_ds_reserve": (C.c_uint64, [V, C.POINTER(abi.Pod), i32]),
         "or_usage_percent": (i64, [i64, i64]),
     }
     for name, (res, args) in sig.items():
@@ -126,6 +134,13 @@ class Oracle:
     def unassign(self, i, uid):
         assert self.lib.or_pod_unassign(self.h, i, uid) == 0
 
+    def set_devices(self, i, devices):
+        devices = np.ascontiguousarray(devices, dtype=abi.DEVICE_DTYPE)
+        assert self.lib.or_node_devices_set(self.h, i, len(devices), abi.ptr(devices)) == 0
+
+    def delete_devices(self, i):
+        assert self.lib.or_node_devices_delete(self.h, i) == 0
+
     # per-plugin entry points (golden vectors)
     def la_filter(self, pod, node, now_ns):
         r = C.c_int()
@@ -143,6 +158,32 @@ class Oracle:
     def numa_score(self, pod, node):
         return self.lib.or_numa_score(self.h, C.byref(pod), node)
 
+    def ds_prefilter(self, pod):
+        """(code, skip, count[3], req[3][3], req_has[3][3])"""
+        skip = C.c_int()
+        cnt = np.zeros(3, np.int32)
+        req = np.zeros((3, 3), np.int64)
+        has = np.zeros((3, 3), np.uint8)
+        code = self.lib.or_ds_prefilter(C.byref(pod), C.byref(skip), abi.ptr(cnt), abi.ptr(req), abi.ptr(has))
+        return code, bool(skip.value), cnt, req, has
+
+    def ds_score_device(self, dev_type, req, total, free):
+        """each argument: (values[3], has[3])"""
+        arrs = [np.ascontiguousarray(x, dtype) for pair in (req, total, free) for x, dtype in
+                zip(pair, (np.int64, np.uint8))]
+        return self.lib.or_ds_score_device(self.h, dev_type, *[abi.ptr(a) for a in arrs])
+
+    def ds_filter(self, pod, node):
+        r = C.c_int()
+        code = self.lib.or_ds_filter(self.h, C.byref(pod), node, C.byref(r))
+        return code, r.value
+
+    def ds_score(self, pod, node):
+        return self.lib.or_ds_score(self.h, C.byref(pod), node)
+
+    def ds_reserve(self, pod, node):
+        return self.lib.or_ds_reserve(self.h, C.byref(pod), node)
+
     def estimate_pod(self, pod):
         est = np.zeros(2, np.int64)
         self.lib.or_estimate_pod(self.h, C.byref(pod), abi.ptr(est))
@@ -156,12 +197,13 @@ class Oracle:
             "reason": np.zeros((P, N), np.uint8),
             "la": np.zeros((P, N), np.int16),
             "numa": np.zeros((P, N), np.int16),
+            "ds": np.zeros((P, N), np.int16),
             "total": np.zeros((P, N), np.int16),
             "best": np.zeros(P, np.int32),
         }
         rc = self.lib.or_eval(self.h, P, abi.ptr(pods), int(now_ns), abi.ptr(out["status"]), abi.ptr(out["reason"]),
-                              abi.ptr(out["la"]), abi.ptr(out["numa"]), abi.ptr(out["total"]), abi.ptr(out["best"]),
-                              n_threads)
+                              abi.ptr(out["la"]), abi.ptr(out["numa"]), abi.ptr(out["ds"]), abi.ptr(out["total"]),
+                              abi.ptr(out["best"]), n_threads)
         if rc != 0:
             raise RuntimeError(f"oracle eval rc={rc}")
         return out
@@ -170,11 +212,18 @@ class Oracle:
         pods = as_pod_array(pods)
         chosen = np.zeros(len(pods), np.int32)
         score = np.zeros(len(pods), np.int32)
+        self.last_device_allocations = np.zeros(len(pods), np.uint64)
         rc = self.lib.or_schedule(self.h, len(pods), abi.ptr(pods), int(now_ns), abi.ptr(chosen), abi.ptr(score),
-                                  n_threads)
+                                  abi.ptr(self.last_device_allocations), n_threads)
         if rc != 0:
             raise RuntimeError(f"oracle schedule rc={rc}")
         return chosen, score
+
+
+def normalize_scores(scores):
+    a = np.ascontiguousarray(scores, np.int64).copy()
+    load().or_normalize_scores(abi.ptr(a), len(a))
+    return a
 
 
 def usage_percent(used, total):

@@ -7,6 +7,9 @@
  *                        estimator/default_estimator.go, pod_assign_cache.go
  *   NodeNUMAResource     pkg/scheduler/plugins/nodenumaresource/plugin.go, scoring.go,
  *                        least_allocated.go, most_allocated.go, util.go
+ *   DeviceShare          pkg/scheduler/plugins/deviceshare/plugin.go, utils.go, scoring.go,
+ *                        device_allocator.go, allocator_gpu.go, device_cache.go, device_resources.go,
+ *                        devicehandler_gpu.go, devicehandler_default.go; k8s.io/apiserver quota/v1
  *   helpers              apis/extension/node_resource_amplification.go, resource.go, load_aware.go
  *   framework            k8s v1.28.7 weighted score sum + selectHost (tie -> lowest node index)
  *
@@ -46,6 +49,9 @@ typedef struct or_node {
   int32_t n_agg;
   or_asg* asg;
   int32_t n_asg, cap_asg;
+  int has_dev_cache; /* nodeDeviceCache.getNodeDevice != nil */
+  int32_t n_dev;
+  ke_device dev[KE_DEV_TYPES * KE_MAX_MINORS];
 } or_node;
 
 struct or_cluster {
@@ -354,7 +360,9 @@ static int pod_is_cpuset(const ke_pod* pod) {
   return (pod->qos_class == KE_QOS_LSE || pod->qos_class == KE_QOS_LSR) && pod->priority_class == KE_PRIORITY_PROD &&
          pod->requests[KE_RES_CPU] > 0;
 }
-static int pod_unsupported(const ke_pod* pod) { return pod_is_cpuset(pod) || pod->has_resource_spec; }
+static int pod_unsupported(const ke_pod* pod) {
+  return pod_is_cpuset(pod) || pod->has_resource_spec || pod->has_unsupported_device_requests;
+}
 static int node_unsupported(const ke_node* n) { return n->numa_topology_policy != 0 || n->cpu_bind_policy != 0; }
 
 /* ---------------------------------------------------------------------------------------------- */
@@ -535,6 +543,450 @@ int64_t or_numa_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
   return numa_resource_score(&c->cfg.numa, requested, n->node.allocatable, pod);
 }
 
+
+/* ---------------------------------------------------------------------------------------------- */
+/* DeviceShare (no reservations / preemption / NUMA affinity / hints / GPU topology tree)          */
+/* ---------------------------------------------------------------------------------------------- */
+
+/* A corev1.ResourceList restricted to one device type's keys (GPU: core, memory, memory-ratio;
+ * RDMA/FPGA: one key). */
+typedef struct rl {
+  uint8_t has[KE_DKEYS];
+  int64_t v[KE_DKEYS];
+} rl;
+
+static int nkeys(int t) { return t == KE_DEV_GPU ? 3 : 1; }
+static rl rl_empty(void) {
+  rl r;
+  memset(&r, 0, sizeof r);
+  return r;
+}
+/* quotav1.SubtractWithNonNegativeResult (k8s.io/apiserver v0.28.7 quota/v1/resources.go) */
+static rl rl_sub_nonneg(rl a, rl b, int nk) {
+  rl r = rl_empty();
+  for (int k = 0; k < nk; k++) {
+    if (a.has[k]) {
+      int64_t q = a.v[k] - (b.has[k] ? b.v[k] : 0);
+      r.has[k] = 1;
+      r.v[k] = q > 0 ? q : 0;
+    } else if (b.has[k]) {
+      r.has[k] = 1;
+      r.v[k] = -b.v[k] > 0 ? -b.v[k] : 0;
+    }
+  }
+  return r;
+}
+/* quotav1.IsZero */
+static int rl_is_zero(rl a, int nk) {
+  for (int k = 0; k < nk; k++)
+    if (a.has[k] && a.v[k] != 0) return 0;
+  return 1;
+}
+/* quotav1.LessThanOrEqual(a, b): only the keys of b that a also has are compared */
+static int rl_leq(rl a, rl b, int nk) {
+  for (int k = 0; k < nk; k++)
+    if (b.has[k] && a.has[k] && a.v[k] > b.v[k]) return 0;
+  return 1;
+}
+/* quotav1.Add */
+static rl rl_add(rl a, rl b, int nk) {
+  rl r = rl_empty();
+  for (int k = 0; k < nk; k++) {
+    r.has[k] = a.has[k] || b.has[k];
+    r.v[k] = (a.has[k] ? a.v[k] : 0) + (b.has[k] ? b.v[k] : 0);
+  }
+  return r;
+}
+
+/* the request of one device instance + how many, per type (preparePod + CalcDesiredRequestsAndCount) */
+typedef struct ds_pod {
+  int status; /* PreFilter status: 0 or UnschedulableAndUnresolvable (invalid device requests) */
+  int skip;   /* no device requests: PreFilter returns Skip */
+  int has[KE_DEV_TYPES];
+  int count[KE_DEV_TYPES];
+  rl req[KE_DEV_TYPES];
+} ds_pod;
+
+static int valid_percentage(int64_t q) { return !(q > 100 && q % 100 != 0); } /* utils.go:222-227 */
+
+/* GetPodDeviceRequests -> ValidateDeviceRequest -> ConvertDeviceRequest (utils.go:304-342,392-412),
+ * then calcDesiredRequestsAndCountForGPU (devicehandler_gpu.go:53-96) and
+ * DefaultDeviceHandler.CalcDesiredRequestsAndCount (devicehandler_default.go:44-93, no hint). */
+static void ds_prepare_pod(const ke_pod* pod, ds_pod* d) {
+  memset(d, 0, sizeof *d);
+  const int64_t* q = pod->device_requests;
+  /* GPU combination flags (utils.go:38-52) */
+  enum { NV = 1, AMD = 2, KGPU = 4, SHARED = 8, CORE = 16, MEM = 32, RATIO = 64 };
+  int comb = 0;
+  if (q[KE_PDR_NVIDIA_GPU] > 0) comb |= NV;
+  if (q[KE_PDR_AMD_GPU] > 0) comb |= AMD;
+  if (q[KE_PDR_KOORD_GPU] > 0) comb |= KGPU;
+  if (q[KE_PDR_GPU_SHARED] > 0) comb |= SHARED;
+  if (q[KE_PDR_GPU_CORE] > 0) comb |= CORE;
+  if (q[KE_PDR_GPU_MEMORY] > 0) comb |= MEM;
+  if (q[KE_PDR_GPU_MEMORY_RATIO] > 0) comb |= RATIO;
+  if (comb) {
+    int ok = 0;
+    const int64_t core = q[KE_PDR_GPU_CORE], ratio = q[KE_PDR_GPU_MEMORY_RATIO], shared = q[KE_PDR_GPU_SHARED];
+    if (comb == KGPU) ok = valid_percentage(q[KE_PDR_KOORD_GPU]);
+    else if (comb == NV || comb == AMD) ok = 1;
+    else if (comb == MEM || comb == RATIO || comb == (CORE | MEM) || comb == (CORE | RATIO))
+      ok = (!(comb & CORE) || valid_percentage(core)) && (!(comb & RATIO) || valid_percentage(ratio));
+    else if (comb == (SHARED | MEM) || comb == (SHARED | RATIO) || comb == (SHARED | CORE | MEM) ||
+             comb == (SHARED | CORE | RATIO))
+      ok = (!(comb & CORE) || (core % shared == 0 && core / shared <= 100)) &&
+           (!(comb & RATIO) || (ratio % shared == 0 && ratio / shared <= 100));
+    if (!ok) {
+      d->status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+      return;
+    }
+    /* ConvertDeviceRequest: converted keys */
+    int64_t c_core = 0, c_mem = 0, c_ratio = 0, c_shared = 0;
+    int h_core = 0, h_mem = 0, h_ratio = 0, h_shared = 0;
+    if (comb == NV || comb == AMD) {
+      const int64_t n = q[comb == NV ? KE_PDR_NVIDIA_GPU : KE_PDR_AMD_GPU];
+      c_core = c_ratio = n * 100;
+      h_core = h_ratio = 1;
+    } else if (comb == KGPU) {
+      c_core = c_ratio = q[KE_PDR_KOORD_GPU];
+      h_core = h_ratio = 1;
+    } else {
+      if (comb & SHARED) { c_shared = shared; h_shared = 1; }
+      if (comb & CORE) { c_core = core; h_core = 1; }
+      if (comb & MEM) { c_mem = q[KE_PDR_GPU_MEMORY]; h_mem = 1; }
+      if (comb & RATIO) { c_ratio = ratio; h_ratio = 1; }
+    }
+    /* calcDesiredRequestsAndCountForGPU */
+    int64_t n = 1;
+    if (h_shared && c_shared > 0) n = c_shared;
+    else if (h_ratio && c_ratio > 100 && c_ratio % 100 == 0) n = c_ratio / 100;
+    rl r = rl_empty();
+    if (h_core) { r.has[KE_DKEY_GPU_CORE] = 1; r.v[KE_DKEY_GPU_CORE] = c_core / n; }
+    if (h_ratio) { r.has[KE_DKEY_GPU_MEMORY_RATIO] = 1; r.v[KE_DKEY_GPU_MEMORY_RATIO] = c_ratio / n; }
+    else if (h_mem) { r.has[KE_DKEY_GPU_MEMORY] = 1; r.v[KE_DKEY_GPU_MEMORY] = c_mem / n; }
+    d->has[KE_DEV_GPU] = 1;
+    d->count[KE_DEV_GPU] = (int)n;
+    d->req[KE_DEV_GPU] = r;
+  }
+  const int pdr[2] = {KE_PDR_RDMA, KE_PDR_FPGA};
+  for (int i = 0; i < 2; i++) {
+    const int t = i == 0 ? KE_DEV_RDMA : KE_DEV_FPGA;
+    const int64_t v = q[pdr[i]];
+    if (v <= 0) continue;
+    if (!valid_percentage(v)) {
+      d->status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+      return;
+    }
+    int64_t n = 1, per = v;
+    if (v > 100 && v % 100 == 0) {
+      n = v / 100;
+      per = v / n;
+    }
+    d->has[t] = 1;
+    d->count[t] = (int)n;
+    d->req[t] = rl_empty();
+    d->req[t].has[0] = 1;
+    d->req[t].v[0] = per;
+  }
+  d->skip = !(d->has[0] || d->has[1] || d->has[2]);
+}
+
+/* one device type of a node's cache: minors in ascending order */
+typedef struct ds_view {
+  int n;
+  int minor[KE_MAX_MINORS];
+  rl total[KE_MAX_MINORS], used[KE_MAX_MINORS], free[KE_MAX_MINORS];
+  int present; /* the filtered nodeDevice kept this type (its free is not all zero) */
+} ds_view;
+
+static rl dev_total(const ke_device* d, int nk) {
+  rl r = rl_empty();
+  if (!d->health) return r; /* buildDeviceResources: unhealthy -> empty (device_cache.go:550-568) */
+  for (int k = 0; k < nk; k++) {
+    r.has[k] = d->has_total[k];
+    r.v[k] = d->has_total[k] ? d->total[k] : 0;
+  }
+  return r;
+}
+static rl dev_used(const ke_device* d, int nk) {
+  rl r = rl_empty();
+  for (int k = 0; k < nk; k++) {
+    r.has[k] = d->has_used[k];
+    r.v[k] = d->has_used[k] ? d->used[k] : 0;
+  }
+  return r;
+}
+
+/* The original cache view (resetDeviceFree, device_cache.go:165-182). */
+static void ds_orig_view(const or_node* nd, int t, ds_view* v) {
+  memset(v, 0, sizeof *v);
+  const int nk = nkeys(t);
+  for (int m = 0; m < KE_MAX_MINORS; m++)
+    for (int i = 0; i < nd->n_dev; i++)
+      if (nd->dev[i].type == t && nd->dev[i].minor == m) {
+        v->minor[v->n] = m;
+        v->total[v->n] = dev_total(&nd->dev[i], nk);
+        v->used[v->n] = dev_used(&nd->dev[i], nk);
+        v->free[v->n] = rl_sub_nonneg(v->total[v->n], v->used[v->n], nk);
+        v->n++;
+      }
+}
+
+/* AutopilotAllocator.filterNodeDevice -> nodeDevice.filter (device_allocator.go:137-166,
+ * device_cache.go:360-415) with no preemptible/required resources: the type is dropped when its free
+ * is all zero; otherwise used' = total - free (kept if non-zero) and free' = total - used'. */
+static void ds_filtered_view(const or_node* nd, int t, ds_view* v) {
+  ds_orig_view(nd, t, v);
+  const int nk = nkeys(t);
+  int all_zero = 1;
+  for (int i = 0; i < v->n; i++)
+    if (!rl_is_zero(v->free[i], nk)) all_zero = 0;
+  v->present = v->n > 0 && !all_zero;
+  if (!v->present) return;
+  for (int i = 0; i < v->n; i++) {
+    const rl u = rl_sub_nonneg(v->total[i], v->free[i], nk);
+    v->free[i] = rl_is_zero(u, nk) ? v->total[i] : rl_sub_nonneg(v->total[i], u, nk);
+  }
+}
+
+/* resourceAllocationScorer weights keyed by the device type's keys (scoring.go:142-197) */
+static int64_t ds_weight(const ke_deviceshare_args* a, int t, int k) {
+  if (t == KE_DEV_GPU) {
+    if (k == KE_DKEY_GPU_MEMORY_RATIO) return a->weights[KE_DSW_GPU_MEMORY_RATIO];
+    if (k == KE_DKEY_GPU_MEMORY) return a->weights[KE_DSW_GPU_MEMORY];
+    return KE_ABSENT;
+  }
+  return a->weights[t == KE_DEV_RDMA ? KE_DSW_RDMA : KE_DSW_FPGA];
+}
+
+/* leastRequestedScore / mostRequestedScore (scoring.go:283-322) */
+static int64_t ds_resource_score(int strategy, int64_t requested, int64_t capacity) {
+  if (capacity == 0) return 0;
+  if (strategy == KE_STRATEGY_MOST_ALLOCATED) {
+    if (requested > capacity) requested = capacity;
+    return requested * MAX_NODE_SCORE / capacity;
+  }
+  if (requested > capacity) return 0;
+  return (capacity - requested) * MAX_NODE_SCORE / capacity;
+}
+
+/* resourceAllocationScorer.scorer over (requested, allocatable) pairs of the keys with a weight and
+ * non-zero total: Σ w·score / Σ w (scoring.go:268-297) */
+static int64_t ds_weighted(const ke_deviceshare_args* a, int t, const int64_t* req, const int64_t* cap,
+                           const int* use, int nk) {
+  int64_t s = 0, ws = 0;
+  for (int k = 0; k < nk; k++) {
+    if (!use[k]) continue;
+    const int64_t w = ds_weight(a, t, k);
+    s += ds_resource_score(a->strategy, req[k], cap[k]) * w;
+    ws += w;
+  }
+  return ws == 0 ? 0 : s / ws;
+}
+
+/* resourceAllocationScorer.scoreNode (scoring.go:227-257) */
+static int64_t ds_score_node(const ke_deviceshare_args* a, int t, const rl* podreq, const ds_view* v) {
+  const int nk = nkeys(t);
+  int64_t req[KE_DKEYS] = {0}, cap[KE_DKEYS] = {0};
+  int use[KE_DKEYS] = {0};
+  for (int k = 0; k < nk; k++) {
+    if (ds_weight(a, t, k) == KE_ABSENT) continue;
+    int64_t total = 0, free = 0;
+    for (int i = 0; i < v->n; i++) {
+      total += v->total[i].has[k] ? v->total[i].v[k] : 0;
+      free += v->free[i].has[k] ? v->free[i].v[k] : 0;
+    }
+    if (total == 0) continue;
+    int64_t r = total;
+    if (total >= free) r = total - free + (podreq->has[k] ? podreq->v[k] : 0);
+    req[k] = r;
+    cap[k] = total;
+    use[k] = 1;
+  }
+  return ds_weighted(a, t, req, cap, use, nk);
+}
+
+/* resourceAllocationScorer.scoreDevice (scoring.go:200-225) */
+static int64_t ds_score_device(const ke_deviceshare_args* a, int t, const rl* podreq, const rl* total,
+                               const rl* free) {
+  const int nk = nkeys(t);
+  int64_t req[KE_DKEYS] = {0}, cap[KE_DKEYS] = {0};
+  int use[KE_DKEYS] = {0};
+  for (int k = 0; k < nk; k++) {
+    if (ds_weight(a, t, k) == KE_ABSENT) continue;
+    const int64_t tq = total->has[k] ? total->v[k] : 0;
+    if (tq == 0) continue;
+    const int64_t fq = free->has[k] ? free->v[k] : 0;
+    int64_t r = tq;
+    if (tq >= fq) r = tq - fq + (podreq->has[k] ? podreq->v[k] : 0);
+    req[k] = r;
+    cap[k] = tq;
+    use[k] = 1;
+  }
+  return ds_weighted(a, t, req, cap, use, nk);
+}
+
+/* defaultAllocateDevices (device_allocator.go:353-424) on the filtered view: devices in
+ * (score desc, minor asc) order (scoreDevices + sortDeviceResourcesByMinor, device_resources.go:171-208),
+ * the first `count` with a non-zero free that covers the request.  Returns the number chosen
+ * (picked[] = view indices).  scorer == NULL: Filter's allocator (every score 0). */
+static int ds_allocate(const ke_deviceshare_args* scorer, int t, const rl* req, int count, const ds_view* v,
+                       int* picked) {
+  const int nk = nkeys(t);
+  if (!v->present) return 0;
+  int order[KE_MAX_MINORS];
+  int64_t sc[KE_MAX_MINORS];
+  for (int i = 0; i < v->n; i++) {
+    order[i] = i;
+    sc[i] = scorer ? ds_score_device(scorer, t, req, &v->total[i], &v->free[i]) : 0;
+  }
+  for (int i = 1; i < v->n; i++) /* insertion sort: score desc, minor asc */
+    for (int j = i; j > 0; j--) {
+      const int a = order[j - 1], b = order[j];
+      if (sc[b] > sc[a] || (sc[b] == sc[a] && v->minor[b] < v->minor[a])) {
+        order[j - 1] = b;
+        order[j] = a;
+      } else {
+        break;
+      }
+    }
+  int n = 0;
+  for (int i = 0; i < v->n && n < count; i++) {
+    const int d = order[i];
+    if (rl_is_zero(v->free[d], nk)) continue;
+    if (!rl_leq(*req, v->free[d], nk)) continue;
+    picked[n++] = d;
+  }
+  return n;
+}
+
+static int ds_insufficient_reason(int t) {
+  return t == KE_DEV_GPU ? KE_REASON_DS_INSUFFICIENT_GPU
+                         : (t == KE_DEV_RDMA ? KE_REASON_DS_INSUFFICIENT_RDMA : KE_REASON_DS_INSUFFICIENT_FPGA);
+}
+
+/* DeviceShare Filter (plugin.go:311-365): AutopilotAllocator.Allocate (device_allocator.go:87-135).
+ * Device types are visited in the fixed order GPU, RDMA, FPGA (Go map order only changes the reason). */
+int or_ds_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* reason) {
+  ds_pod d;
+  ds_prepare_pod(pod, &d);
+  if (d.status) {
+    *reason = KE_REASON_DS_INVALID_REQUEST;
+    return d.status;
+  }
+  const or_node* nd = &c->nodes[node];
+  if (d.skip || !nd->has_dev_cache) return KE_CODE_SUCCESS;
+  ds_view v[KE_DEV_TYPES];
+  for (int t = 0; t < KE_DEV_TYPES; t++) { /* Prepare: a requested type without devices */
+    if (!d.has[t]) continue;
+    ds_orig_view(nd, t, &v[t]);
+    if (v[t].n == 0) {
+      *reason = ds_insufficient_reason(t);
+      return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    }
+  }
+  for (int t = 0; t < KE_DEV_TYPES; t++) {
+    if (!d.has[t]) continue;
+    ds_filtered_view(nd, t, &v[t]);
+    int picked[KE_MAX_MINORS];
+    if (ds_allocate(NULL, t, &d.req[t], d.count[t], &v[t], picked) < d.count[t]) {
+      *reason = ds_insufficient_reason(t);
+      return KE_CODE_UNSCHEDULABLE;
+    }
+  }
+  return KE_CODE_SUCCESS;
+}
+
+/* DeviceShare Score before NormalizeScore (scoring.go:45-103 -> AutopilotAllocator.score
+ * device_allocator.go:469-492) for a node that passed Filter. */
+int64_t or_ds_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
+  ds_pod d;
+  ds_prepare_pod(pod, &d);
+  const or_node* nd = &c->nodes[node];
+  if (d.status || d.skip || !nd->has_dev_cache) return 0;
+  int64_t s = 0;
+  for (int t = 0; t < KE_DEV_TYPES; t++) {
+    if (!d.has[t]) continue;
+    ds_view v;
+    ds_orig_view(nd, t, &v);
+    if (v.n == 0) return 0; /* Prepare error: Score returns 0 with an error status */
+    ds_filtered_view(nd, t, &v);
+    if (v.present && v.n > 0) s += ds_score_node(&c->cfg.deviceshare, t, &d.req[t], &v);
+  }
+  return s;
+}
+
+/* DeviceShare Reserve (plugin.go:426-492): allocate with the plugin's scorer, fillGPUTotalMem
+ * (devicehandler_gpu.go:98-125), updateCacheUsed (device_cache.go:127-141).  Returns the minor mask. */
+uint64_t or_ds_reserve(or_cluster* c, const ke_pod* pod, int32_t node) {
+  ds_pod d;
+  ds_prepare_pod(pod, &d);
+  or_node* nd = &c->nodes[node];
+  if (d.status || d.skip || !nd->has_dev_cache) return 0;
+  uint64_t mask = 0;
+  for (int t = 0; t < KE_DEV_TYPES; t++) {
+    if (!d.has[t]) continue;
+    const int nk = nkeys(t);
+    ds_view v;
+    ds_filtered_view(nd, t, &v);
+    int picked[KE_MAX_MINORS];
+    const int n = ds_allocate(&c->cfg.deviceshare, t, &d.req[t], d.count[t], &v, picked);
+    if (n < d.count[t]) return mask; /* not reached for a node that passed Filter */
+    for (int i = 0; i < n; i++) {
+      const int minor = v.minor[picked[i]];
+      rl alloc = d.req[t];
+      ke_device* dev = NULL;
+      for (int j = 0; j < nd->n_dev; j++)
+        if (nd->dev[j].type == t && nd->dev[j].minor == minor) dev = &nd->dev[j];
+      if (t == KE_DEV_GPU) {
+        const int64_t tm = dev->has_total[KE_DKEY_GPU_MEMORY] && dev->health ? dev->total[KE_DKEY_GPU_MEMORY] : 0;
+        if (alloc.has[KE_DKEY_GPU_MEMORY]) { /* memoryBytesToRatio */
+          alloc.has[KE_DKEY_GPU_MEMORY_RATIO] = 1;
+          alloc.v[KE_DKEY_GPU_MEMORY_RATIO] = (int64_t)((double)alloc.v[KE_DKEY_GPU_MEMORY] / (double)tm * 100.0);
+        } else { /* memoryRatioToBytes */
+          alloc.has[KE_DKEY_GPU_MEMORY] = 1;
+          alloc.v[KE_DKEY_GPU_MEMORY] = alloc.v[KE_DKEY_GPU_MEMORY_RATIO] * tm / 100;
+        }
+      }
+      const rl u = rl_add(dev_used(dev, nk), alloc, nk);
+      for (int k = 0; k < nk; k++) {
+        dev->has_used[k] = u.has[k];
+        dev->used[k] = u.v[k];
+      }
+      mask |= 1ull << (16 * t + minor);
+    }
+  }
+  return mask;
+}
+
+/* preparePod outcome: status, skip, and per type (count, per-instance request [key] / presence) */
+int or_ds_prefilter(const ke_pod* pod, int* skip, int32_t* count, int64_t* req, uint8_t* req_has) {
+  ds_pod d;
+  ds_prepare_pod(pod, &d);
+  *skip = d.skip;
+  for (int t = 0; t < KE_DEV_TYPES; t++) {
+    count[t] = d.has[t] ? d.count[t] : 0;
+    for (int k = 0; k < KE_DKEYS; k++) {
+      req[t * KE_DKEYS + k] = d.req[t].v[k];
+      req_has[t * KE_DKEYS + k] = d.has[t] ? d.req[t].has[k] : 0;
+    }
+  }
+  return d.status;
+}
+
+/* resourceAllocationScorer.scoreDevice for one instance (golden-vector entry point) */
+int64_t or_ds_score_device(const or_cluster* c, int32_t type, const int64_t* req, const uint8_t* req_has,
+                           const int64_t* total, const uint8_t* total_has, const int64_t* free,
+                           const uint8_t* free_has) {
+  rl r = rl_empty(), t = rl_empty(), f = rl_empty();
+  for (int k = 0; k < KE_DKEYS; k++) {
+    r.has[k] = req_has[k]; r.v[k] = req[k];
+    t.has[k] = total_has[k]; t.v[k] = total[k];
+    f.has[k] = free_has[k]; f.v[k] = free[k];
+  }
+  return ds_score_device(&c->cfg.deviceshare, type, &r, &t, &f);
+}
+
 /* ---------------------------------------------------------------------------------------------- */
 /* state                                                                                           */
 /* ---------------------------------------------------------------------------------------------- */
@@ -557,6 +1009,23 @@ void or_destroy(or_cluster* c) {
   }
   free(c->nodes);
   free(c);
+}
+
+int or_node_devices_set(or_cluster* c, int32_t node, int32_t n, const ke_device* devs) {
+  if (node < 0 || node >= c->n) return KE_ERR_NOT_FOUND;
+  if (n < 0 || n > KE_DEV_TYPES * KE_MAX_MINORS) return KE_ERR_INVALID;
+  or_node* nd = &c->nodes[node];
+  nd->has_dev_cache = 1;
+  nd->n_dev = n;
+  if (n) memcpy(nd->dev, devs, sizeof(ke_device) * (size_t)n);
+  return KE_OK;
+}
+
+int or_node_devices_delete(or_cluster* c, int32_t node) {
+  if (node < 0 || node >= c->n) return KE_ERR_NOT_FOUND;
+  c->nodes[node].has_dev_cache = 0;
+  c->nodes[node].n_dev = 0;
+  return KE_OK;
 }
 
 int or_node_upsert(or_cluster* c, int32_t node, const ke_node* n) {
@@ -667,27 +1136,48 @@ int or_pod_unassign(or_cluster* c, int32_t node, int64_t uid) {
 
 typedef struct eval_out {
   uint8_t status, reason;
-  int16_t la, numa, total;
+  int16_t la, numa, ds, total; /* ds: DeviceShare.Score before NormalizeScore */
 } eval_out;
 
-/* RunFilterPlugins in profile order (scheduler-config.yaml:68-73), then RunScorePlugins with
- * weights (:85-94) for a feasible node. */
+/* RunFilterPlugins in profile order LoadAware, NodeNUMAResource, DeviceShare
+ * (scheduler-config.yaml:68-73), then the raw Score of each plugin for a feasible node. */
 static void eval_pair(const or_cluster* c, const ke_pod* pod, int32_t node, int64_t now, eval_out* o) {
   int reason = 0;
   int code = or_la_filter(c, pod, node, now, &reason);
   if (code == KE_CODE_SUCCESS) code = or_numa_filter(c, pod, node, &reason);
+  if (code == KE_CODE_SUCCESS) code = or_ds_filter(c, pod, node, &reason);
   o->status = (uint8_t)code;
   o->reason = (uint8_t)reason;
-  if (code != KE_CODE_SUCCESS) {
-    o->la = o->numa = 0;
-    o->total = -1;
-    return;
+  o->la = o->numa = o->ds = 0;
+  o->total = -1;
+  if (code != KE_CODE_SUCCESS) return;
+  o->la = (int16_t)or_la_score(c, pod, node, now);
+  o->numa = (int16_t)or_numa_score(c, pod, node);
+  o->ds = (int16_t)or_ds_score(c, pod, node);
+}
+
+/* DeviceShare NormalizeScore = DefaultNormalizeScore(MaxNodeScore, false) over the feasible nodes
+ * (scoring.go:109-111; k8s pkg/scheduler/framework/plugins/helper/normalize_score.go), then the
+ * weighted sum (scheduler-config.yaml:85-94). */
+static void normalize_and_total(const or_cluster* c, eval_out* o, int64_t n) {
+  int64_t mx = 0;
+  for (int64_t i = 0; i < n; i++)
+    if (o[i].status == KE_CODE_SUCCESS && o[i].ds > mx) mx = o[i].ds;
+  for (int64_t i = 0; i < n; i++) {
+    if (o[i].status != KE_CODE_SUCCESS) continue;
+    const int64_t ds = mx > 0 ? MAX_NODE_SCORE * o[i].ds / mx : o[i].ds;
+    o[i].total = (int16_t)(c->cfg.weight_loadaware * o[i].la + c->cfg.weight_numa * o[i].numa +
+                           c->cfg.weight_deviceshare * ds);
   }
-  int64_t la = or_la_score(c, pod, node, now);
-  int64_t nu = or_numa_score(c, pod, node);
-  o->la = (int16_t)la;
-  o->numa = (int16_t)nu;
-  o->total = (int16_t)(c->cfg.weight_loadaware * la + c->cfg.weight_numa * nu);
+}
+
+/* DefaultNormalizeScore(MaxNodeScore, reverse=false) on a score list (golden-vector entry point) */
+void or_normalize_scores(int64_t* scores, int32_t n) {
+  int64_t mx = 0;
+  for (int32_t i = 0; i < n; i++)
+    if (scores[i] > mx) mx = scores[i];
+  if (mx == 0) return;
+  for (int32_t i = 0; i < n; i++) scores[i] = MAX_NODE_SCORE * scores[i] / mx;
 }
 
 static int check_supported(const or_cluster* c, int32_t n_pods, const ke_pod* pods) {
@@ -698,8 +1188,26 @@ static int check_supported(const or_cluster* c, int32_t n_pods, const ke_pod* po
   return KE_OK;
 }
 
+/* One pod against every node: filter + raw scores (parallel over nodes), normalize, selectHost
+ * (ties -> lowest node index).  Returns the chosen node or -1. */
+static int32_t eval_pod(const or_cluster* c, const ke_pod* pod, int64_t now, eval_out* o, int16_t* best_score) {
+  const int64_t N = c->n;
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < N; i++) eval_pair(c, pod, (int32_t)i, now, &o[i]);
+  normalize_and_total(c, o, N);
+  int32_t b = -1;
+  int16_t bs = -1;
+  for (int64_t i = 0; i < N; i++)
+    if (o[i].total > bs) {
+      bs = o[i].total;
+      b = (int32_t)i;
+    }
+  *best_score = bs;
+  return bs >= 0 ? b : -1;
+}
+
 int or_eval(const or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, uint8_t* status, uint8_t* reason,
-            int16_t* la_score, int16_t* numa_score, int16_t* total, int32_t* best, int n_threads) {
+            int16_t* la_score, int16_t* numa_score, int16_t* ds_score, int16_t* total, int32_t* best, int n_threads) {
   int rc = check_supported(c, n_pods, pods);
   if (rc) return rc;
   const int64_t N = c->n;
@@ -708,43 +1216,27 @@ int or_eval(const or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now
 #else
   (void)n_threads;
 #endif
+  eval_out* o = (eval_out*)malloc(sizeof(eval_out) * (size_t)(N > 0 ? N : 1));
   for (int p = 0; p < n_pods; p++) {
-    int32_t b = -1;
-    int16_t bs = -1;
-#pragma omp parallel
-    {
-      int32_t lb = -1;
-      int16_t ls = -1;
-#pragma omp for schedule(static)
-      for (int64_t i = 0; i < N; i++) {
-        eval_out o;
-        eval_pair(c, &pods[p], (int32_t)i, now, &o);
-        const int64_t k = (int64_t)p * N + i;
-        if (status) status[k] = o.status;
-        if (reason) reason[k] = o.reason;
-        if (la_score) la_score[k] = o.la;
-        if (numa_score) numa_score[k] = o.numa;
-        if (total) total[k] = o.total;
-        if (o.total > ls) { /* strict: keeps the lowest index of this thread's (ascending) chunk */
-          ls = o.total;
-          lb = (int32_t)i;
-        }
-      }
-#pragma omp critical
-      {
-        if (ls > bs || (ls == bs && ls >= 0 && lb < b)) {
-          bs = ls;
-          b = lb;
-        }
-      }
+    int16_t bs;
+    const int32_t b = eval_pod(c, &pods[p], now, o, &bs);
+    for (int64_t i = 0; i < N; i++) {
+      const int64_t k = (int64_t)p * N + i;
+      if (status) status[k] = o[i].status;
+      if (reason) reason[k] = o[i].reason;
+      if (la_score) la_score[k] = o[i].la;
+      if (numa_score) numa_score[k] = o[i].numa;
+      if (ds_score) ds_score[k] = o[i].ds;
+      if (total) total[k] = o[i].total;
     }
-    if (best) best[p] = bs >= 0 ? b : -1;
+    if (best) best[p] = b;
   }
+  free(o);
   return KE_OK;
 }
 
 int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t* chosen, int32_t* score,
-                int n_threads) {
+                uint64_t* dev_alloc, int n_threads) {
   int rc = check_supported(c, n_pods, pods);
   if (rc) return rc;
   const int64_t N = c->n;
@@ -753,40 +1245,23 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
 #else
   (void)n_threads;
 #endif
+  eval_out* o = (eval_out*)malloc(sizeof(eval_out) * (size_t)(N > 0 ? N : 1));
   for (int p = 0; p < n_pods; p++) {
-    int32_t b = -1;
-    int16_t bs = -1;
-#pragma omp parallel
-    {
-      int32_t lb = -1;
-      int16_t ls = -1;
-#pragma omp for schedule(static)
-      for (int64_t i = 0; i < N; i++) {
-        eval_out o;
-        eval_pair(c, &pods[p], (int32_t)i, now, &o);
-        if (o.total > ls) {
-          ls = o.total;
-          lb = (int32_t)i;
-        }
-      }
-#pragma omp critical
-      {
-        if (ls > bs || (ls == bs && ls >= 0 && lb < b)) {
-          bs = ls;
-          b = lb;
-        }
-      }
-    }
-    if (bs < 0) b = -1;
+    int16_t bs;
+    const int32_t b = eval_pod(c, &pods[p], now, o, &bs);
     chosen[p] = b;
-    if (score) score[p] = bs;
+    if (score) score[p] = b >= 0 ? bs : -1;
+    uint64_t mask = 0;
     if (b >= 0) {
-      /* Reserve: LoadAware podAssignCache.assign (load_aware.go:192-195) at `now`;
-       * framework assume: NodeInfo.Requested += pod requests. */
+      /* Reserve in profile order: LoadAware podAssignCache.assign (load_aware.go:192-195) at `now`,
+       * DeviceShare device allocation (plugin.go:426-492); framework assume: NodeInfo.Requested. */
       or_pod_assign(c, b, &pods[p], now);
+      mask = or_ds_reserve(c, &pods[p], b);
       c->nodes[b].node.requested[KE_RES_CPU] += pods[p].requests[KE_RES_CPU];
       c->nodes[b].node.requested[KE_RES_MEMORY] += pods[p].requests[KE_RES_MEMORY];
     }
+    if (dev_alloc) dev_alloc[p] = mask;
   }
+  free(o);
   return KE_OK;
 }

@@ -1,6 +1,7 @@
 /*
- * oracle.h — TEST INFRASTRUCTURE ONLY.  CPU restatement of koord-scheduler's LoadAwareScheduling and
- * NodeNUMAResource (policy None) Filter/Score and of the framework's weighted sum + selectHost.
+ * oracle.h — TEST INFRASTRUCTURE ONLY.  CPU restatement of koord-scheduler's LoadAwareScheduling,
+ * NodeNUMAResource (policy None) and DeviceShare Filter/Score/Reserve and of the framework's
+ * NormalizeScore + weighted sum + selectHost.
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library, and only
  * as the checker / the timed CPU baseline.  The product (libkoordeval.so) never links or calls it.
@@ -30,22 +31,35 @@ int or_nodemetric_delete(or_cluster* c, int32_t node);
 int or_pod_assign(or_cluster* c, int32_t node, const ke_pod* pod, int64_t timestamp_ns);
 int or_pod_unassign(or_cluster* c, int32_t node, int64_t uid);
 int or_pods_assign(or_cluster* c, int32_t n, const int32_t* nodes, const ke_pod* pods, const int64_t* ts);
+int or_node_devices_set(or_cluster* c, int32_t node, int32_t n, const ke_device* devs);
+int or_node_devices_delete(or_cluster* c, int32_t node);
 
 /* Per-plugin entry points for one (pod, node) pair (golden-vector tests). */
 int or_la_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int64_t now_ns, int* reason);
 int64_t or_la_score(const or_cluster* c, const ke_pod* pod, int32_t node, int64_t now_ns);
 int or_numa_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* reason);
 int64_t or_numa_score(const or_cluster* c, const ke_pod* pod, int32_t node);
+/* DeviceShare: PreFilter status (0 or UnschedulableAndUnresolvable) and skip; Filter; raw Score
+ * (before NormalizeScore); Reserve (mutates the device cache, returns the minor mask 1<<(16*type+minor)). */
+int or_ds_prefilter(const ke_pod* pod, int* skip, int32_t* count /*[3]*/, int64_t* req /*[3][3]*/,
+                    uint8_t* req_has /*[3][3]*/);
+int64_t or_ds_score_device(const or_cluster* c, int32_t type, const int64_t* req, const uint8_t* req_has,
+                           const int64_t* total, const uint8_t* total_has, const int64_t* free,
+                           const uint8_t* free_has);
+void or_normalize_scores(int64_t* scores, int32_t n);
+int or_ds_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* reason);
+int64_t or_ds_score(const or_cluster* c, const ke_pod* pod, int32_t node);
+uint64_t or_ds_reserve(or_cluster* c, const ke_pod* pod, int32_t node);
 /* DefaultEstimator.EstimatePod (estimator/default_estimator.go:59-85): est[KE_NRES], -1 = key absent */
 void or_estimate_pod(const or_cluster* c, const ke_pod* pod, int64_t* est);
 
 /* Matrix evaluation, same layout as ke_eval.  n_threads <= 0: all cores. */
 int or_eval(const or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now_ns, uint8_t* status,
-            uint8_t* reason, int16_t* la_score, int16_t* numa_score, int16_t* total, int32_t* best,
-            int n_threads);
+            uint8_t* reason, int16_t* la_score, int16_t* numa_score, int16_t* ds_score, int16_t* total,
+            int32_t* best, int n_threads);
 /* Sequential scheduling, same contract as ke_schedule (mutates the oracle's state). */
 int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int32_t* chosen,
-                int32_t* score, int n_threads);
+                int32_t* score, uint64_t* dev_alloc, int n_threads);
 
 /* filterNodeUsage's usage percentage, exposed for the threshold-folding property tests:
  * int64(math.Round(float64(used)/float64(total)*100)) (load_aware.go:299). */

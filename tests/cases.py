@@ -128,3 +128,35 @@ def make_numa_nodes(case):
         n.cpuset_allocated_cpus = cpus
         nodes.append(n)
     return nodes
+
+
+# ---- DeviceShare -----------------------------------------------------------------------------------
+def ds_cfg(case, n_nodes=1):
+    cfg = abi.default_config(n_nodes)
+    if case.get("strategy") == "MostAllocated":
+        cfg.deviceshare.strategy = abi.STRATEGY_MOST_ALLOCATED
+    return cfg
+
+
+def ds_pod(case):
+    """A pod whose only requests are the case's device requests (the Go tests build the pod from
+    preFilterState.podRequests, plugin_test.go:2614-2629)."""
+    return model.make_pod(requests=dict(case["pod"]["requests"]))
+
+
+def setup_ds(handle, case, node=0):
+    """Node `node` of `handle` gets the case's device cache (or none) and a big allocatable so that the
+    LoadAware / NodeNUMAResource filters pass; returns the pod."""
+    handle.upsert_node(node, model.make_node(allocatable={"cpu": "96", "memory": "512Gi"}))
+    if case.get("cache", True):
+        handle.set_devices(node, model.make_devices(case["devices"]))
+    return ds_pod(case)
+
+
+def rl3(dev_type, rl):
+    vals, has = [0, 0, 0], [0, 0, 0]
+    for k, v in rl.items():
+        key = model.DEVICE_KEYS[dev_type][k]
+        vals[key] = model.value(v)
+        has[key] = 1
+    return vals, has

@@ -253,3 +253,92 @@ def test_rccl_single_rank_communicator(gpu):
     c1, s1 = ev.schedule(pods, synth.T0)
     c0, s0 = o.schedule(pods, synth.T0)
     assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+
+
+# ---- DeviceShare ---------------------------------------------------------------------------------
+DS = [c for c in cases.load("deviceshare.json") if c["op"] in ("filter", "score")]
+
+
+@pytest.mark.parametrize("case", DS, ids=[c["name"] for c in DS])
+def test_golden_deviceshare(gpu, case):
+    ev = Evaluator(cases.ds_cfg(case))
+    pod = cases.setup_ds(ev, case)
+    r = ev.eval([pod], cases.NOW)
+    want = case["want"]
+    assert (int(r["status"][0, 0]), int(r["reason"][0, 0])) == (want["code"], want["reason"]), case["source"]
+    if case["op"] == "score":
+        assert int(r["ds"][0, 0]) == want["score"], case["source"]
+
+
+def ds_both(n_nodes, seed, strategy=abi.STRATEGY_LEAST_ALLOCATED, batch=64):
+    cl = synth.make_cluster(n_nodes, synth.BASE_SEED + seed)
+    dv = synth.make_devices(n_nodes, synth.BASE_SEED + seed + 50)
+    cfg = synth.config(n_nodes, pod_batch=batch)
+    cfg.deviceshare.strategy = strategy
+    ev, o = Evaluator(cfg), Oracle(cfg, n_nodes)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        synth.load_devices(h, dv)
+    return ev, o
+
+
+@pytest.mark.parametrize("strategy", [abi.STRATEGY_LEAST_ALLOCATED, abi.STRATEGY_MOST_ALLOCATED])
+def test_deviceshare_eval_matrix_parity(gpu, strategy):
+    ev, o = ds_both(700, 81, strategy)
+    pods = synth.make_ds_pods(48, synth.BASE_SEED + 82)
+    a, b = ev.eval(pods, synth.T0), o.eval(pods, synth.T0)
+    for k in ("status", "reason", "la", "numa", "ds", "total", "best"):
+        mism = np.argwhere(a[k] != b[k])
+        assert len(mism) == 0, f"{k}: {len(mism)} mismatches, first {mism[:5].tolist()}"
+
+
+@pytest.mark.parametrize("strategy", [abi.STRATEGY_LEAST_ALLOCATED, abi.STRATEGY_MOST_ALLOCATED])
+def test_deviceshare_schedule_parity(gpu, strategy):
+    """Mixed queue: DeviceShare pods (one per batch, NormalizeScore over all feasible nodes) between
+    batches of plain pods; placements, scores and the allocated device minors equal the oracle's."""
+    ev, o = ds_both(1500, 83, strategy)
+    pods = synth.make_ds_pods(600, synth.BASE_SEED + 84)
+    c1, s1 = ev.schedule(pods, synth.T0)
+    c0, s0 = o.schedule(pods, synth.T0)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5]
+    assert np.array_equal(s1, s0)
+    assert np.array_equal(ev.last_device_allocations, o.last_device_allocations)
+    # the device state after the queue evaluates identically (device cache patched by Reserve)
+    more = synth.make_ds_pods(32, synth.BASE_SEED + 85)
+    a, b = ev.eval(more, synth.T0), o.eval(more, synth.T0)
+    for k in ("status", "ds", "total", "best"):
+        assert np.array_equal(a[k], b[k]), k
+
+
+def test_deviceshare_sharded_loopback(gpu):
+    ev, o = ds_both(2000, 86)
+    pods = synth.make_ds_pods(300, synth.BASE_SEED + 87)
+    ev.shard_init(0, 3, None)
+    c1, s1 = ev.schedule(pods, synth.T0)
+    c0, s0 = o.schedule(pods, synth.T0)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    assert np.array_equal(ev.last_device_allocations, o.last_device_allocations)
+
+
+def test_deviceshare_rccl_single_rank(gpu):
+    from koordinator_amd.evaluator import comm_unique_id
+    ev, o = ds_both(1200, 88)
+    pods = synth.make_ds_pods(200, synth.BASE_SEED + 89)
+    ev.shard_init(0, 1, comm_unique_id())
+    c1, s1 = ev.schedule(pods, synth.T0)
+    c0, s0 = o.schedule(pods, synth.T0)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    assert np.array_equal(ev.last_device_allocations, o.last_device_allocations)
+
+
+def test_deviceshare_cache_delete_and_unhealthy(gpu):
+    """Dropping a node's device cache makes DeviceShare pass with score 0 there; unhealthy GPUs have
+    an empty total (device_cache.go:558-560)."""
+    ev, o = ds_both(300, 90)
+    for h in (ev, o):
+        for i in range(0, 300, 7):
+            h.delete_devices(i)
+    pods = synth.make_ds_pods(40, synth.BASE_SEED + 91)
+    a, b = ev.eval(pods, synth.T0), o.eval(pods, synth.T0)
+    for k in ("status", "reason", "ds", "total", "best"):
+        assert np.array_equal(a[k], b[k]), k

@@ -46,3 +46,42 @@ def test_numa(case):
     else:
         code, reason = o.numa_filter(pod, 0)
         assert (code, reason) == (case["want"]["code"], case["want"]["reason"]), case["source"]
+
+
+# ---- DeviceShare ---------------------------------------------------------------------------------
+DS = cases.load("deviceshare.json")
+TYPES = {"gpu": 0, "rdma": 1, "fpga": 2}
+
+
+@pytest.mark.parametrize("case", DS, ids=[c["name"] for c in DS])
+def test_deviceshare(case):
+    from koordinator_amd import abi
+    from oracle.binding import normalize_scores
+
+    op, want = case["op"], case["want"]
+    if op == "normalize":
+        assert list(normalize_scores(case["raw"])) == want["scores"], case["source"]
+        return
+    o = Oracle(cases.ds_cfg(case), 1)
+    if op == "score_device":
+        r = o.ds_score_device(abi.DEV_GPU, cases.rl3(abi.DEV_GPU, case["request"]),
+                              cases.rl3(abi.DEV_GPU, case["total"]), cases.rl3(abi.DEV_GPU, case["free"]))
+        assert r == want["score"], case["source"]
+        return
+    if op == "prefilter":
+        code, skip, cnt, req, has = o.ds_prefilter(cases.ds_pod(case))
+        assert (code, skip) == (want["code"], want["skip"]), case["source"]
+        for tname, t in TYPES.items():
+            exp = want["per"].get(tname)
+            assert cnt[t] == (exp[0] if exp else 0), (case["source"], tname)
+            if exp:
+                vals, hs = cases.rl3(t, exp[1])
+                assert list(has[t]) == hs and [int(v) for v, h in zip(req[t], hs) if h] == [v for v, h in zip(vals, hs) if h]
+        return
+    pod = cases.setup_ds(o, case)
+    code, reason = o.ds_filter(pod, 0)
+    if op == "filter":
+        assert (code, reason) == (want["code"], want["reason"]), case["source"]
+    else:  # Score (TestScore calls Score directly; a Prepare error shows up as Filter's status)
+        assert (code, reason) == (want["code"], want["reason"]), case["source"]
+        assert o.ds_score(pod, 0) == want["score"], case["source"]
