@@ -95,28 +95,13 @@ __device__ __forceinline__ void prepare_row(NodeRegs& r) {
   }
 }
 
-// floor(num / den), num >= 0, den > 0, any magnitude: slow exact path (double estimate + integer
-// remainder correction), only reached for operands outside the fast path's range.
-__device__ __noinline__ int64_t div_exact_slow(int64_t num, int64_t den) {
-  int64_t q = (int64_t)((double)num / (double)den);
-  int64_t rem = num - q * den;
-  while (rem < 0) {
-    q--;
-    rem += den;
-  }
-  while (rem >= den) {
-    q++;
-    rem -= den;
-  }
-  return q;
-}
-
-// floor(x * 100 / c) for c > 0 — the framework.MaxNodeScore scaling of every least/most scorer.
-// Fast path (0 <= x <= 16c, i.e. a result <= 1600): f32 estimate from the node's reciprocal, off by at
-// most one (relative error < 2^-21), then one exact int64 correction in each direction.
+// x * 100 / c for c > 0 (Go int64 division, truncating) — the framework.MaxNodeScore scaling of every
+// least/most scorer.  Fast path (0 <= x <= 16c, i.e. a result <= 1600): f32 estimate from the node's
+// reciprocal, off by at most one (relative error < 2^-21), then one exact int64 correction in each
+// direction.  Other operands take the native (inline, exec-masked) int64 division.
 __device__ __forceinline__ int32_t div100(int64_t x, int64_t c, float rc) {
   const int64_t x100 = x * 100;
-  if (x < 0 || x > 16 * c) return (int32_t)div_exact_slow(x100, c);
+  if (x < 0 || x > 16 * c) return (int32_t)(x100 / c);
   int32_t q = (int32_t)(i64_to_f32(x100) * rc);
   q -= (int32_t)((int64_t)q * c > x100);
   q += (int32_t)((int64_t)(q + 1) * c <= x100);
@@ -335,8 +320,9 @@ __device__ __noinline__ uint64_t ds_reserve(const SoA& s, int64_t i, const DevPo
   return out;
 }
 
-// `s`/`i` locate the node's DeviceShare state (read only for pods with PF_DS).
-template <bool FULL>
+// `s`/`i` locate the node's DeviceShare state (read only for pods with PF_DS, and only when DS: the
+// batch replay never evaluates a DeviceShare pod — such a pod is alone in its batch).
+template <bool DS>
 __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, const DevPod& p, const KArgs& k,
                                              const SoA& s, int64_t i) {
   EvalOut o;
@@ -395,7 +381,7 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
     }
   }
   // ---- DeviceShare.Filter + raw Score  plugin.go:311-365, scoring.go:45-103
-  if (o.status == KE_CODE_SUCCESS && (p.flags & PF_DS) && (nf & NF_DS_CACHE)) ds_filter_score(s, i, p, k, o);
+  if (DS && o.status == KE_CODE_SUCCESS && (p.flags & PF_DS) && (nf & NF_DS_CACHE)) ds_filter_score(s, i, p, k, o);
   if (o.status != KE_CODE_SUCCESS) {
     o.total = -1;
     o.ds = 0;
@@ -540,6 +526,8 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_parity_finalize(int n_nodes, KAr
 // batch mode: 9-bit score per (pod,node): (total+1) or 0 when filtered out; for a DeviceShare pod
 // (always alone in its batch) also dsraw[node] = raw DeviceShare score + 1 (0 when filtered out).
 // Nodes [lo, hi) of the SoA (this rank's shard); scores stay indexed by the global node index.
+// DS: the batch's pod is a DeviceShare pod (the DeviceShare path stays out of plain batches' code).
+template <bool DS>
 __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi, const DevPod* __restrict__ pods,
                                                            const int32_t* __restrict__ batch_base, int batch_pods,
                                                            int pods_per_block, KArgs k, uint16_t* __restrict__ scores,
@@ -555,9 +543,9 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
   const int p1 = min(batch_pods, p0 + pods_per_block);
   for (int p = p0; p < p1; p++) {
     const DevPod& pod = pods[base + p];
-    const EvalOut o = eval_pair<false>(n, expired, pod, k, s, i);
+    const EvalOut o = eval_pair<DS>(n, expired, pod, k, s, i);
     scores[(int64_t)p * score_stride + i] = (uint16_t)(o.total + 1);
-    if (pod.flags & PF_DS) dsraw[i] = o.total >= 0 ? (uint16_t)(o.ds + 1) : (uint16_t)0;
+    if (DS && (pod.flags & PF_DS)) dsraw[i] = o.total >= 0 ? (uint16_t)(o.ds + 1) : (uint16_t)0;
   }
 }
 
@@ -894,6 +882,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 __device__ __forceinline__ int hash_of(int node) { return (int)(((uint32_t)node * 0x9E3779B1u) >> 19) & (HASH_SLOTS - 1); }
 
+template <bool DS>
 __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __restrict__ pods, int32_t* __restrict__ batch_base,
                                                 int batch_pods, KArgs k, const uint32_t* __restrict__ cand,
                                                 const int32_t* __restrict__ cand_cnt, int32_t* __restrict__ chosen,
@@ -1083,7 +1072,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
         mine.nreq[1] += pod.req[1];
         // DeviceShare Reserve (a DeviceShare pod is alone in its batch: no later pod of the batch
         // reads the device state it patches)
-        s_alloc[j] = (pod.flags & PF_DS) && (mine.flags & NF_DS_CACHE) ? ds_reserve(s, my_node, pod, k) : 0ull;
+        s_alloc[j] = DS && (pod.flags & PF_DS) && (mine.flags & NF_DS_CACHE) ? ds_reserve(s, my_node, pod, k) : 0ull;
       }
       if (lane == 0) {
         s_out[0][j] = key_node(w) + global_offset;
@@ -1492,8 +1481,12 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       if (sharded && !d->loopback) shard_range(N, d->rank, d->world, &lo, &hi);
       if (hi > lo) {
         dim3 grid((unsigned)((hi - lo + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((bp + ppb - 1) / ppb));
-        hipLaunchKernelGGL(k_eval_batch, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, lo, hi, d->d_pods,
-                           d->d_batch_base, bp, ppb, k, d->d_scores, d->capacity, d->d_dsraw);
+        if (ds)
+          hipLaunchKernelGGL(k_eval_batch<true>, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, lo, hi, d->d_pods,
+                             d->d_batch_base, bp, ppb, k, d->d_scores, d->capacity, d->d_dsraw);
+        else
+          hipLaunchKernelGGL(k_eval_batch<false>, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, lo, hi, d->d_pods,
+                             d->d_batch_base, bp, ppb, k, d->d_scores, d->capacity, d->d_dsraw);
       }
       if (ds) {  // DefaultNormalizeScore's max over the feasible nodes (all ranks)
         HIP_OK(hipMemsetAsync(d->d_dsmax, 0, sizeof(uint32_t), d->stream));
@@ -1535,9 +1528,14 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       HIP_OK(hipMemsetAsync(d->d_cand_cnt, 0, sizeof(int32_t) * MAX_BATCH, d->stream));
     }
     if (prof) HIP_OK(hipEventRecord(pe[2], d->stream));
-    hipLaunchKernelGGL(k_resolve, dim3(1), dim3(RES_THREADS), 0, d->stream, d->soa, d->d_pods, d->d_batch_base, bp, k,
-                       d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score, ctx->cfg.global_node_offset,
-                       d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc);
+    if (ds)
+      hipLaunchKernelGGL(k_resolve<true>, dim3(1), dim3(RES_THREADS), 0, d->stream, d->soa, d->d_pods, d->d_batch_base,
+                         bp, k, d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score, ctx->cfg.global_node_offset,
+                         d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc);
+    else
+      hipLaunchKernelGGL(k_resolve<false>, dim3(1), dim3(RES_THREADS), 0, d->stream, d->soa, d->d_pods, d->d_batch_base,
+                         bp, k, d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score, ctx->cfg.global_node_offset,
+                         d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc);
     if (prof) HIP_OK(hipEventRecord(pe[3], d->stream));
   }
   HIP_OK(hipGetLastError());
@@ -1618,14 +1616,14 @@ int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t 
   const int ppb = 8;
   HIP_OK(hipMemsetAsync(d->d_batch_base, 0, sizeof(int32_t), d->stream));
   dim3 grid((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((n_pods + ppb - 1) / ppb));
-  hipLaunchKernelGGL(k_eval_batch, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base, n_pods,
+  hipLaunchKernelGGL(k_eval_batch<false>, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base, n_pods,
                      ppb, k, d->d_scores, d->capacity, d->d_dsraw);  // warm
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   HIP_OK(hipEventRecord(e0, d->stream));
   for (int it = 0; it < iters; it++)
-    hipLaunchKernelGGL(k_eval_batch, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base,
+    hipLaunchKernelGGL(k_eval_batch<false>, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base,
                        n_pods, ppb, k, d->d_scores, d->capacity, d->d_dsraw);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(e1, d->stream));
