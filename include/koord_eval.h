@@ -151,8 +151,34 @@ typedef struct ke_loadaware_args {
 typedef struct ke_numa_args {
   int64_t weights[KE_NRES]; /* KE_ABSENT = resource not in ScoringStrategy.Resources */
   int32_t strategy;         /* KE_STRATEGY_*                                       */
-  int32_t pad;
+  int32_t numa_strategy;    /* NUMAScoringStrategy.Type (KE_STRATEGY_*); its weights are the node-level
+                               ScoringStrategy.Resources (scoring.go:37-52, plugin.go:121-126) */
 } ke_numa_args;
+
+/* ---- NUMA topology (nodenumaresource + frameworkext/topologymanager) --------------------------- */
+/* NUMA topology policies (apis/extension/numa_aware.go): node label / NRT kubelet topology-manager policy */
+#define KE_NUMA_POLICY_NONE 0
+#define KE_NUMA_POLICY_BEST_EFFORT 1
+#define KE_NUMA_POLICY_RESTRICTED 2
+#define KE_NUMA_POLICY_SINGLE_NUMA_NODE 3
+#define KE_MAX_NUMA 8
+#define KE_REASON_NUMA_POLICY_CONFLICT 19 /* "node(s) NUMA Topology policy cannot match" (ErrNotMatchNUMATopology) */
+#define KE_REASON_NUMA_MISSING_RESOURCES 20 /* "node(s) missing NUMA resources" (topology_hint.go:35-37) */
+#define KE_REASON_NUMA_HINT_UNALIGNED 21 /* topologymanager Admit: "Unaligned NUMA Hint ..." / "Unsatisfied NUMA ..." */
+#define KE_REASON_NUMA_INSUFFICIENT_RESOURCES 22 /* Allocate: "Insufficient NUMA <resource>" (resource_manager.go:307) */
+
+/* One NUMA node of TopologyOptions.NUMANodeResources (topology_options.go:90-164; reserved CPUs already
+ * removed) with the resource manager's allocation on it (node_allocation.go:33-243). */
+typedef struct ke_numa_zone {
+  int32_t id;                  /* NUMA node id, 0 .. KE_MAX_NUMA-1; zones ascending by id */
+  uint8_t has[KE_NRES];        /* cpu / memory key present in the zone's resources */
+  uint8_t has_allocated;       /* allocatedResources has an entry for the zone */
+  uint8_t pad;
+  int64_t capacity[KE_NRES];   /* cpu milli, memory bytes (before amplification) */
+  int64_t allocated[KE_NRES];  /* Σ NUMANodeResources of the pods allocated on the zone */
+  int32_t cpuset_cpus;         /* cpuset CPUs allocated in the zone (allocatedCPUs.CPUsInNUMANodes) */
+  int32_t pad2;
+} ke_numa_zone; /* 48 bytes */
 
 /* ---- DeviceShare (pkg/scheduler/plugins/deviceshare) ------------------------------------------ */
 #define KE_DEV_GPU 0  /* schedulingv1alpha1.GPU  */
@@ -237,7 +263,7 @@ typedef struct ke_node {
    * -2 = the NRT carries no ratio map (Score then reads the node annotation). */
   double nrt_cpu_amplification_ratio;
   int32_t custom_agg_type;                       /* KE_AGG_*           */
-  int32_t numa_topology_policy;    /* 0 = None; non-zero unsupported in ABI v1 */
+  int32_t numa_topology_policy;    /* KE_NUMA_POLICY_*: getNUMATopologyPolicy (label, else NRT policy) */
   int32_t cpu_bind_policy;         /* 0 = None; non-zero unsupported in ABI v1 */
   uint8_t has_custom_thresholds;   /* annotation present and valid JSON  */
   uint8_t custom_thresholds_error; /* annotation present but failed to unmarshal (helper.go:110) */
@@ -312,8 +338,8 @@ void ke_destroy(ke_ctx* ctx);
 const char* ke_last_error(void);
 int ke_abi_version(void);
 /* sizeof() of ke_config, ke_node, ke_node_metric, ke_pod_metric, ke_aggregated_usage, ke_pod,
- * ke_resource_map, ke_loadaware_args, ke_numa_args, ke_deviceshare_args, ke_device (in that order)
- * for binding-layout checks. */
+ * ke_resource_map, ke_loadaware_args, ke_numa_args, ke_deviceshare_args, ke_device, ke_numa_zone (in
+ * that order) for binding-layout checks. */
 int ke_abi_struct_sizes(int32_t* sizes, int32_t n);
 /* 1 if this build has a usable HIP device and its gfx950 kernels loaded, else 0. */
 int ke_device_available(void);
@@ -351,6 +377,14 @@ int ke_estimate_pod(ke_ctx* ctx, const ke_pod* pod, int64_t* est);
 int ke_node_devices_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_device* devices);
 /* Drop the node's cache entry (getNodeDevice == nil: DeviceShare Filter passes, Score is 0). */
 int ke_node_devices_delete(ke_ctx* ctx, int32_t node);
+/* NodeResourceTopology informer + resource manager state of `node`: its NUMA zones (n <= KE_MAX_NUMA,
+ * n = 0: no NUMA resources).  Read when the node's NUMA topology policy is not None. */
+int ke_node_numa_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_numa_zone* zones);
+/* The NUMA allocation each pod of the last ke_schedule received on its node (NodeNUMAResource Reserve
+ * -> resourceManager.Update, resource_manager.go:194-258 / node_allocation.go:111-156): out[pod][2*id
+ * + r] for NUMA id and resource r (cpu milli, memory), all zero for a pod without one.  The context
+ * already applied them to its zones; a host keeping its own resource manager reads them here. */
+int ke_last_numa_allocations(ke_ctx* ctx, int32_t n, int64_t* out);
 
 /* ---- evaluation ------------------------------------------------------------------------------ */
 /* Parity mode: Filter + Score of `n_pods` pods against every node, no state change.

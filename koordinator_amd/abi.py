@@ -26,6 +26,12 @@ REASON_LA_AGG_USAGE_MEMORY = 5
 REASON_NUMA_INSUFFICIENT_AMPLIFIED_CPU = 16
 REASON_NUMA_INVALID_AMPLIFICATION_RATIO = 17
 REASON_NUMA_INVALID_CPU_TOPOLOGY = 18
+REASON_NUMA_POLICY_CONFLICT = 19
+REASON_NUMA_MISSING_RESOURCES = 20
+REASON_NUMA_HINT_UNALIGNED = 21
+REASON_NUMA_INSUFFICIENT_RESOURCES = 22
+NUMA_POLICY_NONE, NUMA_POLICY_BEST_EFFORT, NUMA_POLICY_RESTRICTED, NUMA_POLICY_SINGLE_NUMA_NODE = 0, 1, 2, 3
+MAX_NUMA = 8
 REASON_DS_INVALID_REQUEST = 32
 REASON_DS_INSUFFICIENT_GPU = 33
 REASON_DS_INSUFFICIENT_RDMA = 34
@@ -86,7 +92,20 @@ class LoadAwareArgs(C.Structure):
 
 
 class NumaArgs(C.Structure):
-    _fields_ = [("weights", i64 * NRES), ("strategy", i32), ("pad", i32)]
+    _fields_ = [("weights", i64 * NRES), ("strategy", i32), ("numa_strategy", i32)]
+
+
+class NumaZone(C.Structure):
+    _fields_ = [
+        ("id", i32),
+        ("has", u8 * NRES),
+        ("has_allocated", u8),
+        ("pad", u8),
+        ("capacity", i64 * NRES),
+        ("allocated", i64 * NRES),
+        ("cpuset_cpus", i32),
+        ("pad2", i32),
+    ]
 
 
 class DeviceShareArgs(C.Structure):
@@ -192,7 +211,7 @@ class Pod(C.Structure):
 
 
 STRUCTS = [Config, Node, NodeMetric, PodMetric, AggregatedUsage, Pod, ResourceMap, LoadAwareArgs, NumaArgs,
-           DeviceShareArgs, Device]
+           DeviceShareArgs, Device, NumaZone]
 
 # numpy views of the same layouts (bulk loads)
 NODE_DTYPE = np.dtype(Node)
@@ -201,6 +220,7 @@ POD_METRIC_DTYPE = np.dtype(PodMetric)
 AGG_DTYPE = np.dtype(AggregatedUsage)
 POD_DTYPE = np.dtype(Pod)
 DEVICE_DTYPE = np.dtype(Device)
+NUMA_ZONE_DTYPE = np.dtype(NumaZone)
 
 ROW_DTYPE = np.dtype([("f", np.int64, (18,)), ("flags", np.uint32), ("pad", np.uint32)])
 
@@ -262,7 +282,9 @@ EXPORTS = {
     "ke_eval": (C.c_int, [C.c_void_p, i32, C.c_void_p, i64] + [C.c_void_p] * 7),
     "ke_node_devices_set": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p]),
     "ke_node_devices_delete": (C.c_int, [C.c_void_p, i32]),
+    "ke_node_numa_set": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p]),
     "ke_last_device_allocations": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
+    "ke_last_numa_allocations": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_schedule": (C.c_int, [C.c_void_p, i32, C.c_void_p, i64, C.c_void_p, C.c_void_p]),
     "ke_last_schedule_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(i32), C.c_void_p, i32]),
     "ke_set_profiling": (C.c_int, [C.c_void_p, i32]),

@@ -48,6 +48,19 @@ static int require_device(ke_ctx* ctx) {
   return KE_OK;
 }
 
+// DeviceShare is a NUMA hint provider for pods with device requests (deviceshare/topology_hint.go);
+// that provider is not modelled, so such pods cannot meet nodes with a NUMA topology policy.
+static int check_numa_deviceshare(ke_ctx* ctx, const ke_pod* pods, int32_t n) {
+  if (!ctx->c.numa_enabled) return KE_OK;
+  bool ds = false;
+  for (int32_t p = 0; p < n && !ds; p++) ds = (make_dev_pod(ctx->c.cfg, pods[p]).flags & PF_DS) != 0;
+  if (!ds) return KE_OK;
+  for (int32_t i = 0; i < ctx->c.n_nodes; i++)
+    if (ctx->c.nodes[i].valid && ctx->c.nodes[i].node.numa_topology_policy != KE_NUMA_POLICY_NONE)
+      return fail(KE_ERR_UNSUPPORTED, "DeviceShare pods on nodes with a NUMA topology policy (DeviceShare NUMA hints)");
+  return KE_OK;
+}
+
 extern "C" {
 
 int ke_abi_version(void) { return KE_ABI_VERSION; }
@@ -57,7 +70,7 @@ int ke_abi_struct_sizes(int32_t* sizes, int32_t n) {
                          (int32_t)sizeof(ke_aggregated_usage), (int32_t)sizeof(ke_pod),
                          (int32_t)sizeof(ke_resource_map), (int32_t)sizeof(ke_loadaware_args),
                          (int32_t)sizeof(ke_numa_args), (int32_t)sizeof(ke_deviceshare_args),
-                         (int32_t)sizeof(ke_device)};
+                         (int32_t)sizeof(ke_device),       (int32_t)sizeof(ke_numa_zone)};
   const int32_t m = (int32_t)(sizeof(all) / sizeof(all[0]));
   for (int32_t i = 0; i < n && i < m; i++) sizes[i] = all[i];
   return m;
@@ -85,6 +98,7 @@ int ke_create(const ke_config* cfg, ke_ctx** out) {
   if (a.node_metric_expiration_seconds != KE_ABSENT) f |= AF_EXP_PRESENT;
   if (cfg->numa.strategy == KE_STRATEGY_MOST_ALLOCATED) f |= AF_NUMA_MOST;
   if (cfg->deviceshare.strategy == KE_STRATEGY_MOST_ALLOCATED) f |= AF_DS_MOST;
+  if (cfg->numa.numa_strategy == KE_STRATEGY_MOST_ALLOCATED) f |= AF_NUMA_HINT_MOST;
   k.flags = f;
   k.wsum_la = k.wsum_numa = 0;
   for (int r = 0; r < KE_NRES; r++) {
@@ -128,6 +142,7 @@ int ke_node_upsert(ke_ctx* ctx, int32_t node, const ke_node* n) {
   ns.valid = true;
   ns.node = *n;
   ns.dirty = true;
+  if (n->numa_topology_policy != KE_NUMA_POLICY_NONE) ctx->c.numa_enabled = true;
   ctx->c.n_nodes = std::max(ctx->c.n_nodes, node + 1);
   return KE_OK;
 }
@@ -162,6 +177,26 @@ int ke_node_devices_delete(ke_ctx* ctx, int32_t node) {
   ns.has_dev_cache = false;
   ns.devs.clear();
   ns.dirty = true;
+  return KE_OK;
+}
+
+int ke_node_numa_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_numa_zone* zones) {
+  int rc = check_node(ctx, node);
+  if (rc) return rc;
+  rc = validate_zones(n, zones);
+  if (rc) return rc;
+  NodeState& ns = ctx->c.nodes[node];
+  ns.zones.assign(zones, zones + n);
+  ns.dirty = true;
+  ctx->c.numa_enabled = true;
+  return KE_OK;
+}
+
+int ke_last_numa_allocations(ke_ctx* ctx, int32_t n, int64_t* out) {
+  if (!ctx || n < 0 || (n > 0 && !out)) return fail(KE_ERR_INVALID, "ke_last_numa_allocations arguments");
+  const auto& a = ctx->c.last_numa_alloc;
+  constexpr int W = KE_MAX_NUMA * KE_NRES;
+  for (int64_t i = 0; i < (int64_t)n * W; i++) out[i] = i < (int64_t)a.size() ? a[i] : 0;
   return KE_OK;
 }
 
@@ -276,6 +311,8 @@ int ke_eval(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, uin
   if (!ctx) return fail(KE_ERR_INVALID, "null context");
   int rc = check_pods(pods, n_pods);
   if (rc) return rc;
+  rc = check_numa_deviceshare(ctx, pods, n_pods);
+  if (rc) return rc;
   rc = require_device(ctx);
   if (rc) return rc;
   return device_eval(&ctx->c, n_pods, pods, now_ns, status, reason, la_score, numa_score, ds_score, total, best);
@@ -284,6 +321,8 @@ int ke_eval(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, uin
 int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int32_t* chosen, int32_t* score) {
   if (!ctx || (n_pods > 0 && !chosen)) return fail(KE_ERR_INVALID, "ke_schedule arguments");
   int rc = check_pods(pods, n_pods);
+  if (rc) return rc;
+  rc = check_numa_deviceshare(ctx, pods, n_pods);
   if (rc) return rc;
   rc = require_device(ctx);
   if (rc) return rc;
@@ -301,6 +340,8 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
     host_assign(ctx->c.cfg, ns, pods[p], now_ns);
     if (p < (int32_t)ctx->c.last_dev_alloc.size() && ctx->c.last_dev_alloc[p])
       host_ds_reserve(ctx->c.cfg, ns, make_dev_pod(ctx->c.cfg, pods[p]), ctx->c.last_dev_alloc[p]);
+    if ((int64_t)ctx->c.last_numa_alloc.size() >= (int64_t)(p + 1) * KE_MAX_NUMA * KE_NRES)
+      host_numa_reserve(ns, &ctx->c.last_numa_alloc[(size_t)p * KE_MAX_NUMA * KE_NRES]);
     ns.node.requested[KE_RES_CPU] += pods[p].requests[KE_RES_CPU];
     ns.node.requested[KE_RES_MEMORY] += pods[p].requests[KE_RES_MEMORY];
     ns.dirty = was_dirty;  // the device row already carries this Reserve

@@ -64,8 +64,10 @@ int validate_node(const ke_node& n) {
     if (n.allocatable[r] < 0 || (n.raw_allocatable[r] < 0 && n.raw_allocatable[r] != KE_ABSENT))
       return fail(KE_ERR_INVALID, "negative allocatable");
   }
-  if (n.numa_topology_policy != 0 || n.cpu_bind_policy != 0)
-    return fail(KE_ERR_UNSUPPORTED, "node NUMA topology / CPU bind policies are not implemented in ABI v1");
+  if (n.numa_topology_policy < KE_NUMA_POLICY_NONE || n.numa_topology_policy > KE_NUMA_POLICY_SINGLE_NUMA_NODE)
+    return fail(KE_ERR_INVALID, "NUMA topology policy");
+  if (n.cpu_bind_policy != 0)
+    return fail(KE_ERR_UNSUPPORTED, "node CPU bind policies (cpuset binding) are not implemented");
   if (n.custom_agg_type < 0 || n.custom_agg_type >= KE_AGG_TYPES) return fail(KE_ERR_INVALID, "aggregation type");
   return KE_OK;
 }
@@ -547,7 +549,71 @@ void derive_row(const ke_config& cfg, const NodeState& ns, int64_t now, Row* row
   if (ratio_s > 1.0) flags |= NF_NUMA_RATIO_S;
   row->f[F_CSAS] = amplify(cs_milli, ratio_s);
   if (ns.has_dev_cache) flags |= NF_DS_CACHE;
+  flags |= (uint32_t)n.numa_topology_policy * NF_NUMA_POLICY0;
+  if (n.nrt_cpu_amplification_ratio <= -1.5 && n.amplification_error) flags |= NF_NUMA_OPT_ERR;
   row->flags = flags;
+}
+
+int validate_zones(int32_t n, const ke_numa_zone* zones) {
+  if (n < 0 || n > KE_MAX_NUMA || (n > 0 && !zones)) return fail(KE_ERR_INVALID, "NUMA zone count");
+  for (int32_t i = 0; i < n; i++) {
+    if (zones[i].id < 0 || zones[i].id >= KE_MAX_NUMA) return fail(KE_ERR_INVALID, "NUMA zone id out of range");
+    if (i > 0 && zones[i].id <= zones[i - 1].id) return fail(KE_ERR_INVALID, "NUMA zones must ascend by id");
+    for (int r = 0; r < KE_NRES; r++)
+      if (zones[i].capacity[r] < 0 || zones[i].cpuset_cpus < 0) return fail(KE_ERR_INVALID, "negative NUMA quantity");
+    if (zones[i].cpuset_cpus > 0 && !zones[i].has_allocated)
+      return fail(KE_ERR_INVALID, "cpuset CPUs allocated in a zone without an allocation entry");
+  }
+  return KE_OK;
+}
+
+// getResourceOptions -> amplifyNUMANodeResources (util.go:78-98): the NUMA zones' cpu is amplified with
+// the node annotation's ratio unless the NRT reported ratios; getAvailableNUMANodeResources
+// (node_allocation.go:221-243) adjusts the allocated cpu of amplified cpusets.
+void derive_numa_row(const NodeState& ns, int64_t* f, uint32_t* mask) {
+  for (int i = 0; i < NUM_NUMA_FIELDS; i++) f[i] = 0;
+  *mask = 0;
+  const ke_node& n = ns.node;
+  double ratio;
+  bool amplify_caps = false;
+  if (n.nrt_cpu_amplification_ratio > -1.5) {
+    ratio = n.nrt_cpu_amplification_ratio < 0 ? 0.0 : n.nrt_cpu_amplification_ratio;
+  } else {
+    ratio = n.cpu_amplification_ratio < 0 ? 0.0 : n.cpu_amplification_ratio;
+    amplify_caps = true;
+  }
+  for (const ke_numa_zone& z : ns.zones) {
+    const int id = z.id;
+    *mask |= 1u << id;
+    for (int r = 0; r < KE_NRES; r++) {
+      if (z.has[r]) {
+        *mask |= 1u << (8 * (r + 1) + id);
+        int64_t c = z.capacity[r];
+        if (r == KE_RES_CPU && amplify_caps && ratio > 1.0 && c != 0) c = amplify(c, ratio);
+        f[NUMA_CAP + 2 * id + r] = c;
+      }
+    }
+    if (z.has_allocated) {
+      *mask |= 1u << (24 + id);
+      f[NUMA_AL + 2 * id + 0] = z.allocated[0];
+      f[NUMA_AL + 2 * id + 1] = z.allocated[1];
+      if (ratio > 1.0) {
+        const int64_t cs = (int64_t)z.cpuset_cpus * 1000;
+        f[NUMA_AL + 2 * id] = z.allocated[0] - cs + amplify(cs, ratio);
+      }
+    }
+  }
+}
+
+void host_numa_reserve(NodeState& ns, const int64_t* delta) {
+  for (ke_numa_zone& z : ns.zones) {
+    const int64_t d0 = delta[2 * z.id], d1 = delta[2 * z.id + 1];
+    if (d0 == 0 && d1 == 0) continue;
+    if (!z.has_allocated) z.allocated[0] = z.allocated[1] = 0;
+    z.has_allocated = 1;
+    z.allocated[0] += d0;
+    z.allocated[1] += d1;
+  }
 }
 
 void host_assign(const ke_config& cfg, NodeState& ns, const ke_pod& pod, int64_t timestamp_ns) {

@@ -27,6 +27,8 @@ struct NodeState {
   std::vector<ke_pod_metric> pm;
   std::vector<ke_aggregated_usage> agg;
   std::vector<AssignedPod> asg;
+  // NodeResourceTopology NUMA zones + the resource manager's allocation on them
+  std::vector<ke_numa_zone> zones;
   // DeviceShare node device cache entry (device_cache.go:518-568)
   bool has_dev_cache = false;
   std::vector<ke_device> devs;
@@ -44,6 +46,8 @@ struct Context {
   std::vector<NodeState> nodes;  // size = node_capacity
   int32_t n_nodes = 0;           // 1 + highest populated index
   bool ds_enabled = false;       // some node has a device cache entry: the device SoA exists
+  bool numa_enabled = false;     // some node has a NUMA topology policy: the NUMA SoA exists
+  std::vector<int64_t> last_numa_alloc;  // per pod of the last ke_schedule: [KE_MAX_NUMA*KE_NRES]
   std::vector<uint64_t> last_dev_alloc;  // per pod of the last ke_schedule
   DeviceState* dev = nullptr;
   // last ke_schedule timing
@@ -87,5 +91,12 @@ void derive_ds_row(const NodeState& ns, int64_t* f, uint64_t* masks);
 // host mirror of DeviceShare Reserve: add the allocation of `pod` on the minors in `mask`
 // (bit 16*type+minor) to the node's device cache (fillGPUTotalMem + updateCacheUsed)
 void host_ds_reserve(const ke_config& cfg, NodeState& ns, const DevPod& dp, uint64_t mask);
+
+// NUMA topology
+int validate_zones(int32_t n, const ke_numa_zone* zones);
+// the NUMA SoA row of a node: NUM_NUMA_FIELDS int64 + the uint32 mask
+void derive_numa_row(const NodeState& ns, int64_t* f, uint32_t* mask);
+// host mirror of the NUMA allocation the device Reserve made: delta[z][r] per zone id
+void host_numa_reserve(NodeState& ns, const int64_t* delta /*[KE_MAX_NUMA*KE_NRES]*/);
 
 }  // namespace ke

@@ -49,6 +49,8 @@ struct SoA {
   int64_t stride;
   int64_t* ds;      // DeviceShare: NUM_DS_FIELDS arrays of `stride` int64 (nullptr until a device cache appears)
   uint64_t* dsm;    // DeviceShare: NUM_DS_MASKS arrays of `stride` uint64
+  int64_t* nf;      // NUMA topology: NUM_NUMA_FIELDS arrays of `stride` int64 (nullptr until a NUMA node appears)
+  uint32_t* nm;     // NUMA topology: `stride` uint32 zone / key / allocation masks
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -320,11 +322,372 @@ __device__ __noinline__ uint64_t ds_reserve(const SoA& s, int64_t i, const DevPo
   return out;
 }
 
+// ---------------------------------------------------------------------------------------------
+// NodeNUMAResource under a NUMA topology policy, non-cpuset pods: hint generation
+// (resource_manager.go:525-622), topologymanager merge + admit (policy*.go), allocation by the merged
+// hint (tryBestToDistributeEvenly, resource_manager.go:260-314) and the NUMA-scope score
+// (scoring.go:101-119).  The zones of node i are read from the NUMA SoA once per lane into registers.
+// ---------------------------------------------------------------------------------------------
+// bitmask.IterateBitMasks order over NUMA ids 0..7: by popcount, then lexicographic on the ascending
+// id list.  Restricted to the subsets of a node's zones it is the order over those zones.
+__constant__ uint8_t NUMA_ORDER[255] = {
+    1, 2, 4, 8, 16, 32, 64, 128, 3, 5, 9, 17, 33, 65, 129, 6, 10, 18, 34, 66, 130, 12, 20, 36, 68, 132, 24,
+    40, 72, 136, 48, 80, 144, 96, 160, 192, 7, 11, 19, 35, 67, 131, 13, 21, 37, 69, 133, 25, 41, 73, 137,
+    49, 81, 145, 97, 161, 193, 14, 22, 38, 70, 134, 26, 42, 74, 138, 50, 82, 146, 98, 162, 194, 28, 44, 76,
+    140, 52, 84, 148, 100, 164, 196, 56, 88, 152, 104, 168, 200, 112, 176, 208, 224, 15, 23, 39, 71, 135,
+    27, 43, 75, 139, 51, 83, 147, 99, 163, 195, 29, 45, 77, 141, 53, 85, 149, 101, 165, 197, 57, 89, 153,
+    105, 169, 201, 113, 177, 209, 225, 30, 46, 78, 142, 54, 86, 150, 102, 166, 198, 58, 90, 154, 106, 170,
+    202, 114, 178, 210, 226, 60, 92, 156, 108, 172, 204, 116, 180, 212, 228, 120, 184, 216, 232, 240, 31,
+    47, 79, 143, 55, 87, 151, 103, 167, 199, 59, 91, 155, 107, 171, 203, 115, 179, 211, 227, 61, 93, 157,
+    109, 173, 205, 117, 181, 213, 229, 121, 185, 217, 233, 241, 62, 94, 158, 110, 174, 206, 118, 182, 214,
+    230, 122, 186, 218, 234, 242, 124, 188, 220, 236, 244, 248, 63, 95, 159, 111, 175, 207, 119, 183, 215,
+    231, 123, 187, 219, 235, 243, 125, 189, 221, 237, 245, 249, 126, 190, 222, 238, 246, 250, 252, 127, 191,
+    223, 239, 247, 251, 253, 254, 255};
+__constant__ uint8_t NUMA_OFF[10] = {0, 0, 8, 36, 92, 162, 218, 246, 254, 255};  // first entry of each size
+
+struct NumaNode {
+  uint32_t zm, ah, ch[2];  // zones present, allocation entries, cpu / memory capacity keys (bit = NUMA id)
+  int64_t av[2][8];        // totalAvailable[r][id] (0 for absent zones / keys)
+  uint32_t perm[2][8];     // perm[r][nb-1]: slot order of an nb-zone hint after the distribute sort
+};
+
+__device__ __forceinline__ int64_t pick8(const int64_t (&a)[8], int z) {
+  int64_t v = a[0];
+#pragma unroll
+  for (int t = 1; t < 8; t++) v = z == t ? a[t] : v;
+  return v;
+}
+__device__ __forceinline__ uint32_t pick8u(const uint32_t (&a)[8], int z) {
+  uint32_t v = a[0];
+#pragma unroll
+  for (int t = 1; t < 8; t++) v = z == t ? a[t] : v;
+  return v;
+}
+__device__ __forceinline__ int64_t numa_cap(const SoA& s, int64_t i, int z, int r) {
+  return s.nf[(NUMA_CAP + 2 * z + r) * s.stride + i];
+}
+__device__ __forceinline__ int64_t numa_al(const SoA& s, int64_t i, const NumaNode& v, int z, int r) {
+  const int64_t a = s.nf[(NUMA_AL + 2 * z + r) * s.stride + i];  // SubtractWithNonNegativeResult(allocated, {})
+  return ((v.ah >> z) & 1u) && a > 0 ? a : 0;
+}
+
+// getAvailableNUMANodeResources (node_allocation.go:221-243) and the sort order of
+// tryBestToDistributeEvenly: sort.Slice's insertion sort compares totalAvailable indexed by slice
+// POSITION (a reference quirk), so the permutation of an nb-zone hint depends only on av[r][0..nb-1]
+// and is the state after insertion passes 1..nb-1 — computed once for all hints.
+__device__ __forceinline__ void numa_load(const SoA& s, int64_t i, NumaNode& v) {
+  const uint32_t m = s.nm[i];
+  v.zm = m & 0xFFu;
+  v.ch[0] = (m >> 8) & 0xFFu;
+  v.ch[1] = (m >> 16) & 0xFFu;
+  v.ah = m >> 24;
+#pragma unroll
+  for (int z = 0; z < 8; z++)
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      const int64_t a = numa_cap(s, i, z, r) - numa_al(s, i, v, z, r);
+      v.av[r][z] = a > 0 ? a : 0;
+    }
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    uint32_t st = 0x76543210u;
+    v.perm[r][0] = st;
+#pragma unroll
+    for (int ii = 1; ii < 8; ii++) {
+      bool go = true;
+#pragma unroll
+      for (int j = ii; j > 0; j--) {
+        go = go && v.av[r][j] < v.av[r][j - 1];
+        if (go) {
+          const uint32_t a = (st >> (4 * j)) & 15u, b = (st >> (4 * (j - 1))) & 15u;
+          st = (st & ~(0xFFu << (4 * (j - 1)))) | (a << (4 * (j - 1))) | (b << (4 * j));
+        }
+      }
+      v.perm[r][ii] = st;
+    }
+  }
+}
+
+// q / d for 1 <= d <= 8 (Go int64 division): constant divisors become multiply-high sequences
+__device__ __forceinline__ int64_t div_upto8(int64_t q, int d) {
+  switch (d) {
+    case 1: return q;
+    case 2: return q / 2;
+    case 3: return q / 3;
+    case 4: return q / 4;
+    case 5: return q / 5;
+    case 6: return q / 6;
+    case 7: return q / 7;
+    default: return q / 8;
+  }
+}
+
+// tryBestToDistributeEvenly over the zones of mask m: true when every requested resource is fully
+// split; OUT: the zones that received a non-zero amount (bit) and the amounts (out[r][id]).
+template <bool OUT>
+__device__ __forceinline__ bool numa_distribute(const NumaNode& v, uint32_t m, const DevPod& p, uint32_t* got_mask,
+                                                int64_t (&out)[2][8]) {
+  const int nb = __popc(m);
+  uint32_t bl = 0;  // zone ids of m, ascending, one nibble each
+  for (uint32_t mm = m, t = 0; mm; mm &= mm - 1, t++) bl |= (uint32_t)(__ffs(mm) - 1) << (4 * t);
+  bool ok = true;
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    if (!OUT && !ok) break;
+    if (((v.ch[r] | v.ah) & v.zm) == 0 || p.req[r] == 0) continue;  // resourceNamesByNUMA x requests
+    const uint32_t perm = pick8u(v.perm[r], nb - 1);
+    int64_t q = p.req[r];
+    for (int t = 0; t < nb; t++) {
+      const int z = (int)((bl >> (4 * ((perm >> (4 * t)) & 15u))) & 15u);
+      const int64_t a = pick8(v.av[r], z);
+      const int64_t split = div_upto8(q, nb - t);  // splitQuantity
+      const int64_t got = a > split ? split : a;   // allocateRes
+      q -= got;
+      if (OUT && got != 0) {
+        *got_mask |= 1u << z;
+#pragma unroll
+        for (int zz = 0; zz < 8; zz++) out[r][zz] += zz == z ? got : 0;
+      }
+    }
+    if (q != 0) ok = false;
+  }
+  return ok;
+}
+
+// resourceAllocationScorer.score with least/mostResourceScorer (scoring.go:210-226) in plain int64
+__device__ __forceinline__ int32_t numa_scope_score(bool most, const int64_t (&req)[2], const int64_t (&alloc)[2],
+                                                    const DevPod& p, const KArgs& k) {
+  int64_t sc = 0, ws = 0;
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    const int64_t w = k.w_numa[r], a = alloc[r];
+    if (w == 0 || a == 0) continue;
+    const int64_t rq = req[r] + p.req[r];
+    int64_t x;
+    if (most) x = ((rq > a ? a : rq) * 100) / a;
+    else x = rq > a ? 0 : ((a - rq) * 100) / a;
+    sc += x * w;
+    ws += w;
+  }
+  return ws ? (int32_t)(sc / ws) : 0;
+}
+
+// the hint's score: numaScorer over requested = total - available of the hint's zones
+__device__ __forceinline__ int32_t numa_hint_score(const SoA& s, int64_t i, const NumaNode& v, uint32_t m,
+                                                   const DevPod& p, const KArgs& k) {
+  int64_t tot[2] = {0, 0}, av[2] = {0, 0}, req[2];
+#pragma unroll
+  for (int z = 0; z < 8; z++)
+    if ((m >> z) & 1u)
+#pragma unroll
+      for (int r = 0; r < 2; r++) {
+        tot[r] += numa_cap(s, i, z, r);
+        av[r] += v.av[r][z];
+      }
+#pragma unroll
+  for (int r = 0; r < 2; r++) req[r] = tot[r] - av[r] > 0 ? tot[r] - av[r] : 0;
+  return numa_scope_score((k.flags & AF_NUMA_HINT_MOST) != 0, req, tot, p, k);
+}
+
+__device__ __forceinline__ bool narrower(uint32_t a, uint32_t b) {  // bitmask.IsNarrowerThan
+  const int ca = __popc(a), cb = __popc(b);
+  return ca == cb ? a < b : ca < cb;
+}
+
+__device__ __forceinline__ bool in_list(const uint64_t (&l)[4], uint32_t m) {
+  const uint64_t w = m < 64 ? l[0] : m < 128 ? l[1] : m < 192 ? l[2] : l[3];
+  return (w >> (m & 63u)) & 1u;
+}
+
+struct NumaPick {
+  uint8_t status, reason;
+  uint32_t aff;  // merged NUMANodeAffinity, 0 = nil
+};
+
+// BestEffort without a preferred merged hint: mergeFilteredHints over the full provider lists
+// (policy.go:198-260); an unsatisfied result (or a resource without hints) -> any NUMA node.
+__device__ __forceinline__ uint32_t numa_best_effort_fallback(const SoA& s, int64_t i, const NumaNode& v, const DevPod& p,
+                                                           const KArgs& k, const bool (&present)[2],
+                                                           const uint32_t (&lack)[2]) {
+  uint64_t L[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+  int64_t dummy[2][8];
+  for (int e = 0; e < 255; e++) {
+    const uint32_t m = NUMA_ORDER[e];
+    if (m & ~v.zm) continue;
+    const bool in0 = present[0] && !(m & lack[0]), in1 = present[1] && !(m & lack[1]);
+    if (!in0 && !in1) continue;
+    if (!numa_distribute<false>(v, m, p, nullptr, dummy)) continue;
+    const uint64_t bit = 1ull << (m & 63u);
+    const int w = (int)(m >> 6);
+#pragma unroll
+    for (int ww = 0; ww < 4; ww++) {
+      if (in0 && w == ww) L[0][ww] |= bit;
+      if (in1 && w == ww) L[1][ww] |= bit;
+    }
+  }
+  const bool e0 = !(L[0][0] | L[0][1] | L[0][2] | L[0][3]), e1 = !(L[1][0] | L[1][1] | L[1][2] | L[1][3]);
+  if ((present[0] && e0) || (present[1] && e1)) return v.zm;  // filterProvidersHints reasons
+  if (!(present[0] && present[1])) return v.zm;  // unreachable: one list always has a preferred hint
+  uint32_t best = v.zm;
+  int32_t bsc = 0;
+  bool bun = false;
+  for (int e1i = 0; e1i < 255; e1i++) {
+    const uint32_t m1 = NUMA_ORDER[e1i];
+    if ((m1 & ~v.zm) || !in_list(L[0], m1)) continue;
+    int32_t s1 = -1;
+    for (int e2i = 0; e2i < 255; e2i++) {
+      const uint32_t m2 = NUMA_ORDER[e2i];
+      if ((m2 & ~v.zm) || !in_list(L[1], m2)) continue;
+      const uint32_t mg = m1 & m2;
+      if (!mg) continue;
+      const bool un = max(__popc(m1), __popc(m2)) != __popc(mg);
+      int32_t sc = 0;
+      if (m1 == mg) {
+        if (s1 < 0) s1 = numa_hint_score(s, i, v, m1, p, k);
+        sc += s1;
+      }
+      if (m2 == mg) sc += numa_hint_score(s, i, v, m2, p, k);
+      if (narrower(mg, best) || (__popc(mg) == __popc(best) && sc > bsc)) {
+        best = mg;
+        bsc = sc;
+        bun = un;
+      }
+    }
+  }
+  return bun ? v.zm : best;
+}
+
+// FilterByNUMANode + RunNUMATopologyManagerAdmit for a pod whose requests are not all zero.
+__device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t nf, const NumaNode& v,
+                                               const DevPod& p, const KArgs& k) {
+  NumaPick o{KE_CODE_SUCCESS, KE_REASON_NONE, 0u};
+  const int policy = nf_numa_policy(nf);
+  if (v.zm == 0) {  // topology_hint.go:31-41
+    o.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    o.reason = KE_REASON_NUMA_MISSING_RESOURCES;
+    return o;
+  }
+  if (nf & NF_NUMA_OPT_ERR) {  // GetPodTopologyHints error -> admit reasons
+    o.status = KE_CODE_UNSCHEDULABLE;
+    o.reason = KE_REASON_NUMA_HINT_UNALIGNED;
+    return o;
+  }
+  const uint32_t all = v.zm;
+  bool present[2];
+  uint32_t lack[2];
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    present[r] = p.req[r] != 0 && (v.ch[r] & all) != 0;
+    uint32_t l = 0;
+    if (v.ch[r] & all)
+#pragma unroll
+      for (int z = 0; z < 8; z++)
+        if (((all >> z) & 1u) && (!(((v.ch[r] | v.ah) >> z) & 1u) || v.av[r][z] == 0)) l |= 1u << z;
+    lack[r] = l;
+  }
+  const int R = (int)present[0] + (int)present[1];
+  int64_t dummy[2][8];
+  if (R == 0) {  // no hints: one preferred any-NUMA hint per provider -> merged = all zones
+    if (policy == KE_NUMA_POLICY_SINGLE_NUMA_NODE) return o;  // best == all -> nil affinity
+    o.aff = all;
+    if (!numa_distribute<false>(v, all, p, nullptr, dummy)) {
+      o.status = KE_CODE_UNSCHEDULABLE;
+      o.reason = KE_REASON_NUMA_INSUFFICIENT_RESOURCES;
+    }
+    return o;
+  }
+  // Preferred merged hints are the masks in every present list that are preferred in each (of the
+  // list's minimum size, or any size under Restricted); scanned in IterateBitMasks order with
+  // mergeFilteredHints' replacement rule (narrower, else same size and higher score).
+  int minr[2] = {0, 0};
+  uint32_t best = 0;
+  int32_t bsc = 0;
+  bool found = false, stop = false;
+  const int smax = policy == KE_NUMA_POLICY_SINGLE_NUMA_NODE ? 1 : __popc(all);
+  for (int sz = 1; sz <= smax && !stop; sz++) {
+    const bool first0 = minr[0] == 0, first1 = minr[1] == 0;
+    for (int e = NUMA_OFF[sz]; e < NUMA_OFF[sz + 1]; e++) {
+      const uint32_t m = NUMA_ORDER[e];
+      if (m & ~all) continue;
+      const bool in0 = present[0] && !(m & lack[0]), in1 = present[1] && !(m & lack[1]);
+      if (!in0 && !in1) continue;
+      if (!numa_distribute<false>(v, m, p, nullptr, dummy)) continue;
+      if (in0 && !minr[0]) minr[0] = sz;
+      if (in1 && !minr[1]) minr[1] = sz;
+      bool cand = (!present[0] || in0) && (!present[1] || in1);
+      if (policy != KE_NUMA_POLICY_RESTRICTED) cand = cand && (!present[0] || first0) && (!present[1] || first1);
+      if (!cand) continue;
+      const int32_t sc = R * numa_hint_score(s, i, v, m, p, k);
+      if (!found || narrower(m, best) || (__popc(m) == __popc(best) && sc > bsc)) {
+        best = m;
+        bsc = sc;
+        found = true;
+      }
+    }
+    stop = policy == KE_NUMA_POLICY_RESTRICTED ? found : ((!present[0] || minr[0]) && (!present[1] || minr[1]));
+  }
+  if (found) {
+    o.aff = (policy == KE_NUMA_POLICY_SINGLE_NUMA_NODE && best == all) ? 0u : best;
+    return o;
+  }
+  if (policy != KE_NUMA_POLICY_BEST_EFFORT) {
+    o.status = KE_CODE_UNSCHEDULABLE;
+    o.reason = KE_REASON_NUMA_HINT_UNALIGNED;
+    return o;
+  }
+  o.aff = numa_best_effort_fallback(s, i, v, p, k, present, lack);
+  if (!numa_distribute<false>(v, o.aff, p, nullptr, dummy)) {
+    o.status = KE_CODE_UNSCHEDULABLE;
+    o.reason = KE_REASON_NUMA_INSUFFICIENT_RESOURCES;
+  }
+  return o;
+}
+
+// Score under a NUMA policy (scoring.go:101-119): the allocation on the affinity, NUMA-scope
+// allocatable / requested of the zones it touches, else the node's.
+__device__ __forceinline__ int32_t numa_policy_score(const SoA& s, int64_t i, const NumaNode& v, uint32_t aff,
+                                                     const DevPod& p, const KArgs& k, const NodeRegs& n) {
+  int64_t out[2][8] = {{0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0, 0}};
+  uint32_t zs = 0;
+  if (aff) numa_distribute<true>(v, aff, p, &zs, out);
+  int64_t req[2] = {n.nreq[0], n.nreq[1]}, alloc[2] = {n.nalloc[0], n.nalloc[1]};
+  if (zs) {
+    req[0] = req[1] = alloc[0] = alloc[1] = 0;
+#pragma unroll
+    for (int z = 0; z < 8; z++)
+      if ((zs >> z) & 1u)
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+          alloc[r] += numa_cap(s, i, z, r);
+          req[r] += numa_al(s, i, v, z, r);
+        }
+  }
+  return numa_scope_score((k.flags & AF_NUMA_MOST) != 0, req, alloc, p, k);
+}
+
+// NodeNUMAResource Reserve of a non-cpuset pod under a NUMA policy: NodeAllocation.addPodAllocation
+// (node_allocation.go:111-156) adds the allocation on the affinity to the zones.  out16[2*id + r].
+__device__ __forceinline__ void numa_reserve(const SoA& s, int64_t i, const NumaNode& v, uint32_t aff,
+                                             const DevPod& p, int64_t* out16) {
+  int64_t out[2][8] = {{0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0, 0}};
+  uint32_t zs = 0;
+  if (aff) numa_distribute<true>(v, aff, p, &zs, out);
+#pragma unroll
+  for (int z = 0; z < 8; z++)
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      out16[2 * z + r] = out[r][z];
+      if ((zs >> z) & 1u) s.nf[(NUMA_AL + 2 * z + r) * s.stride + i] += out[r][z];
+    }
+  if (zs) s.nm[i] = s.nm[i] | (zs << 24);
+}
+
 // `s`/`i` locate the node's DeviceShare state (read only for pods with PF_DS, and only when DS: the
 // batch replay never evaluates a DeviceShare pod — such a pod is alone in its batch).
-template <bool DS>
+// NUMA: some node may carry a NUMA topology policy; `nv` holds node i's zones when its policy is set.
+template <bool DS, bool NUMA>
 __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, const DevPod& p, const KArgs& k,
-                                             const SoA& s, int64_t i) {
+                                             const SoA& s, int64_t i, const NumaNode& nv) {
   EvalOut o;
   o.status = KE_CODE_SUCCESS;
   o.reason = KE_REASON_NONE;
@@ -380,6 +743,18 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
       }
     }
   }
+  // ---- NodeNUMAResource.Filter under a NUMA topology policy: FilterByNUMANode + topologymanager Admit
+  const bool npol = NUMA && !(p.flags & PF_NUMA_SKIP) && nf_numa_policy(nf) != KE_NUMA_POLICY_NONE;
+  int32_t npol_score = 0;
+  if (npol && o.status == KE_CODE_SUCCESS) {
+    const NumaPick pk = numa_admit(s, i, nf, nv, p, k);
+    if (pk.status != KE_CODE_SUCCESS) {
+      o.status = pk.status;
+      o.reason = pk.reason;
+    } else {
+      npol_score = numa_policy_score(s, i, nv, pk.aff, p, k, n);
+    }
+  }
   // ---- DeviceShare.Filter + raw Score  plugin.go:311-365, scoring.go:45-103
   if (DS && o.status == KE_CODE_SUCCESS && (p.flags & PF_DS) && (nf & NF_DS_CACHE)) ds_filter_score(s, i, p, k, o);
   if (o.status != KE_CODE_SUCCESS) {
@@ -403,7 +778,9 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
   }
   // ---- NodeNUMAResource.Score  scoring.go:66-139,210-249
   int32_t nu = 0;
-  if (!(p.flags & PF_NUMA_SKIP) && !(nf & NF_NUMA_SCORE_ZERO)) {
+  if (npol) {
+    nu = npol_score;
+  } else if (!(p.flags & PF_NUMA_SKIP) && !(nf & NF_NUMA_SCORE_ZERO)) {
     bool zero = false;
     int64_t reqc = n.nreq[0];
     if (p.req[0] != 0 && (nf & NF_NUMA_RATIO_S)) {
@@ -464,6 +841,7 @@ __global__ void k_gather_rows(SoA s, Row* __restrict__ rows, int n) {
 // parity mode: full status / score matrices [pod][node]; `total` holds the LoadAware + NUMA part
 // until k_parity_finalize adds the normalized DeviceShare score.  dsmax[p] = 1 + max raw DeviceShare
 // score over the pod's feasible nodes (DefaultNormalizeScore's maxCount).
+template <bool NUMA>
 __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_parity(SoA s, int n_nodes, const DevPod* __restrict__ pods,
                                                             int n_pods, int pods_per_block, KArgs k,
                                                             uint8_t* status, uint8_t* reason, int16_t* la,
@@ -477,12 +855,14 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_parity(SoA s, int n_nodes, 
     prepare_row(n);
   }
   const bool expired = live ? node_expired(n, k) : false;
+  NumaNode nv;
+  if (NUMA && live && nf_numa_policy(n.flags) != KE_NUMA_POLICY_NONE) numa_load(s, i, nv);
   const int p0 = blockIdx.y * pods_per_block;
   const int p1 = min(n_pods, p0 + pods_per_block);
   for (int p = p0; p < p1; p++) {
     uint32_t m = 0;
     if (live) {
-      const EvalOut o = eval_pair<true>(n, expired, pods[p], k, s, i);
+      const EvalOut o = eval_pair<true, NUMA>(n, expired, pods[p], k, s, i, nv);
       const int64_t o_idx = (int64_t)p * n_nodes + i;
       status[o_idx] = o.status;
       reason[o_idx] = o.reason;
@@ -527,7 +907,7 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_parity_finalize(int n_nodes, KAr
 // (always alone in its batch) also dsraw[node] = raw DeviceShare score + 1 (0 when filtered out).
 // Nodes [lo, hi) of the SoA (this rank's shard); scores stay indexed by the global node index.
 // DS: the batch's pod is a DeviceShare pod (the DeviceShare path stays out of plain batches' code).
-template <bool DS>
+template <bool DS, bool NUMA>
 __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi, const DevPod* __restrict__ pods,
                                                            const int32_t* __restrict__ batch_base, int batch_pods,
                                                            int pods_per_block, KArgs k, uint16_t* __restrict__ scores,
@@ -538,12 +918,14 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
   load_row(s, i, n);
   prepare_row(n);
   const bool expired = node_expired(n, k);
+  NumaNode nv;
+  if (NUMA && nf_numa_policy(n.flags) != KE_NUMA_POLICY_NONE) numa_load(s, i, nv);
   const int base = *batch_base;
   const int p0 = blockIdx.y * pods_per_block;
   const int p1 = min(batch_pods, p0 + pods_per_block);
   for (int p = p0; p < p1; p++) {
     const DevPod& pod = pods[base + p];
-    const EvalOut o = eval_pair<DS>(n, expired, pod, k, s, i);
+    const EvalOut o = eval_pair<DS, NUMA>(n, expired, pod, k, s, i, nv);
     scores[(int64_t)p * score_stride + i] = (uint16_t)(o.total + 1);
     if (DS && (pod.flags & PF_DS)) dsraw[i] = o.total >= 0 ? (uint16_t)(o.ds + 1) : (uint16_t)0;
   }
@@ -882,13 +1264,16 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 __device__ __forceinline__ int hash_of(int node) { return (int)(((uint32_t)node * 0x9E3779B1u) >> 19) & (HASH_SLOTS - 1); }
 
-template <bool DS>
+// NUMA: nodes may carry NUMA topology policies — changed nodes re-read their zones (patched by this
+// replay's Reserves) from the NUMA SoA, and numa_alloc[pod][2*id + r] receives each pod's allocation.
+template <bool DS, bool NUMA>
 __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __restrict__ pods, int32_t* __restrict__ batch_base,
                                                 int batch_pods, KArgs k, const uint32_t* __restrict__ cand,
                                                 const int32_t* __restrict__ cand_cnt, int32_t* __restrict__ chosen,
                                                 int32_t* __restrict__ chosen_score, int32_t global_offset,
                                                 uint64_t* __restrict__ stamps, uint64_t* __restrict__ pstamps,
-                                                int batch_index, uint64_t* __restrict__ dev_alloc) {
+                                                int batch_index, uint64_t* __restrict__ dev_alloc,
+                                                int64_t* __restrict__ numa_alloc) {
   const int tid = threadIdx.x;
   if (tid == 0) pstamps[8 * batch_index] = __builtin_amdgcn_s_memrealtime();
   __shared__ uint32_t s_cand[MAX_BATCH * KMAX];
@@ -1023,7 +1408,11 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
     const bool in_chg = ck && csl >= 0 && s_changed[csl];
     const uint32_t bu = wave_max_u32(in_chg ? 0u : ck);  // best unchanged snapshot candidate
     uint32_t kc = 0;  // exact re-evaluation of the nodes changed earlier in this batch
-    if (lane < n_chg) kc = make_key(eval_pair<false>(mine, my_expired, pod, k, s, my_node).total, my_node);
+    if (lane < n_chg) {
+      NumaNode nv;
+      if (NUMA && nf_numa_policy(mine.flags) != KE_NUMA_POLICY_NONE) numa_load(s, my_node, nv);
+      kc = make_key(eval_pair<false, NUMA>(mine, my_expired, pod, k, s, my_node, nv).total, my_node);
+    }
     const uint32_t bc = wave_max_u32(kc);
     const uint32_t w = max(bu, bc);
     if (w != 0) {
@@ -1073,6 +1462,18 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
         // DeviceShare Reserve (a DeviceShare pod is alone in its batch: no later pod of the batch
         // reads the device state it patches)
         s_alloc[j] = DS && (pod.flags & PF_DS) && (mine.flags & NF_DS_CACHE) ? ds_reserve(s, my_node, pod, k) : 0ull;
+        if (NUMA) {  // NodeNUMAResource Reserve: the zones of a NUMA-policy node
+          int64_t* out16 = numa_alloc + (int64_t)(base + j) * 16;
+          if (!(pod.flags & PF_NUMA_SKIP) && nf_numa_policy(mine.flags) != KE_NUMA_POLICY_NONE) {
+            NumaNode nv;
+            numa_load(s, my_node, nv);
+            const NumaPick pk = numa_admit(s, my_node, mine.flags, nv, pod, k);
+            numa_reserve(s, my_node, nv, pk.status == KE_CODE_SUCCESS ? pk.aff : 0u, pod, out16);
+          } else {
+#pragma unroll
+            for (int t = 0; t < 16; t++) out16[t] = 0;
+          }
+        }
       }
       if (lane == 0) {
         s_out[0][j] = key_node(w) + global_offset;
@@ -1082,6 +1483,9 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
       s_out[0][j] = -1;
       s_out[1][j] = -1;
       s_alloc[j] = 0;
+      if (NUMA)
+#pragma unroll
+        for (int t = 0; t < 16; t++) numa_alloc[(int64_t)(base + j) * 16 + t] = 0;
     }
     wave_lds_sync();
   }
@@ -1156,6 +1560,11 @@ struct DeviceState {
   int64_t* d_dsrows = nullptr;   // staging for DeviceShare row uploads
   int64_t ds_staging_cap = 0;
   std::vector<DevPod> host_pods;  // the last uploaded queue (batch segmentation)
+  // NUMA topology
+  bool numa_alloc = false;         // soa.nf / soa.nm allocated
+  int64_t* d_numaalloc = nullptr;  // [n_pods][16] per-zone allocation of each pod (ke_schedule)
+  int64_t* d_numarows = nullptr;   // staging for NUMA row uploads
+  int64_t numa_staging_cap = 0;
 };
 
 // Contiguous node range of shard `rank`: 512-aligned chunks (k_select's 16-B loads stay aligned).
@@ -1213,7 +1622,8 @@ void device_destroy(Context* ctx) {
   void* ptrs[] = {d->soa.f,     d->soa.flags, d->d_rows,      d->d_idx,          d->d_pods,   d->d_scores,
                   d->d_cand,    d->d_cand_cnt, d->d_batch_base, d->d_chosen,     d->d_chosen_score,
                   d->d_stamps,  d->d_parity, d->d_best,       d->d_gath,         d->soa.ds,   d->soa.dsm,
-                  d->d_dsraw,   d->d_dsmax,  d->d_devalloc,   d->d_dsrows};
+                  d->d_dsraw,   d->d_dsmax,  d->d_devalloc,   d->d_dsrows,       d->soa.nf,   d->soa.nm,
+                  d->d_numaalloc, d->d_numarows};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (d->stream) (void)hipStreamDestroy(d->stream);
@@ -1290,15 +1700,43 @@ static int ensure_ds(Context* ctx) {
   return KE_OK;
 }
 
+constexpr int NUMA_ROW_WORDS = NUM_NUMA_FIELDS + 1;  // int64 fields + the mask word
+
+__global__ void k_scatter_numa(SoA s, const int64_t* __restrict__ rows, const int32_t* __restrict__ idx, int n) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int64_t i = idx[t];
+  const int64_t* r = rows + (int64_t)t * NUMA_ROW_WORDS;
+  for (int f = 0; f < NUM_NUMA_FIELDS; f++) s.nf[f * s.stride + i] = r[f];
+  s.nm[i] = (uint32_t)r[NUM_NUMA_FIELDS];
+}
+
+static int ensure_numa(Context* ctx) {
+  DeviceState* d = ctx->dev;
+  if (d->numa_alloc || !ctx->numa_enabled) return KE_OK;
+  HIP_OK(hipMalloc(&d->soa.nf, sizeof(int64_t) * NUM_NUMA_FIELDS * d->capacity));
+  HIP_OK(hipMalloc(&d->soa.nm, sizeof(uint32_t) * d->capacity));
+  HIP_OK(hipMemsetAsync(d->soa.nf, 0, sizeof(int64_t) * NUM_NUMA_FIELDS * d->capacity, d->stream));
+  HIP_OK(hipMemsetAsync(d->soa.nm, 0, sizeof(uint32_t) * d->capacity, d->stream));
+  d->numa_alloc = true;
+  for (int32_t i = 0; i < ctx->n_nodes; i++)  // rows derived before the NUMA SoA existed
+    if (!ctx->nodes[i].zones.empty()) ctx->nodes[i].dirty = true;
+  return KE_OK;
+}
+
 // Re-derive rows of dirty / time-expired nodes and scatter them into the SoA.
 int device_refresh(Context* ctx, int64_t now) {
   DeviceState* d = ctx->dev;
   int rc = ensure_ds(ctx);
   if (rc) return rc;
+  rc = ensure_numa(ctx);
+  if (rc) return rc;
   std::vector<Row> rows;
   std::vector<int32_t> idx;
   std::vector<int64_t> dsrows;  // DeviceShare rows of the dirty nodes (the device state is not time-dependent)
   std::vector<int32_t> dsidx;
+  std::vector<int64_t> nrows;  // NUMA rows of the dirty nodes
+  std::vector<int32_t> nidx;
   for (int32_t i = 0; i < ctx->n_nodes; i++) {
     NodeState& ns = ctx->nodes[i];
     if (!ns.dirty && now < ns.valid_until) continue;
@@ -1310,6 +1748,14 @@ int device_refresh(Context* ctx, int64_t now) {
       dsrows.resize(o + NUM_DS_FIELDS + NUM_DS_MASKS);
       derive_ds_row(ns, &dsrows[o], reinterpret_cast<uint64_t*>(&dsrows[o + NUM_DS_FIELDS]));
       dsidx.push_back(i);
+    }
+    if (ns.dirty && d->numa_alloc) {
+      const size_t o = nrows.size();
+      nrows.resize(o + NUMA_ROW_WORDS);
+      uint32_t mask;
+      derive_numa_row(ns, &nrows[o], &mask);
+      nrows[o + NUM_NUMA_FIELDS] = (int64_t)mask;
+      nidx.push_back(i);
     }
     ns.valid_until = vu;
     ns.dirty = false;
@@ -1330,6 +1776,21 @@ int device_refresh(Context* ctx, int64_t now) {
                        (int)n);
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(d->stream));  // `dsrows` is a local host vector
+  }
+  if (!nidx.empty()) {
+    const int64_t n = (int64_t)nidx.size();
+    if (d->numa_staging_cap < n) {
+      if (d->d_numarows) HIP_OK(hipFree(d->d_numarows));
+      HIP_OK(hipMalloc(&d->d_numarows, sizeof(int64_t) * NUMA_ROW_WORDS * n + sizeof(int32_t) * n));
+      d->numa_staging_cap = n;
+    }
+    int32_t* didx = reinterpret_cast<int32_t*>(d->d_numarows + NUMA_ROW_WORDS * n);
+    HIP_OK(hipMemcpyAsync(d->d_numarows, nrows.data(), sizeof(int64_t) * nrows.size(), hipMemcpyHostToDevice, d->stream));
+    HIP_OK(hipMemcpyAsync(didx, nidx.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, d->stream));
+    hipLaunchKernelGGL(k_scatter_numa, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, d->stream, d->soa, d->d_numarows,
+                       didx, (int)n);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(d->stream));  // `nrows` is a local host vector
   }
   if (rows.empty()) return KE_OK;
   HIP_OK(hipSetDevice(d->device));
@@ -1389,8 +1850,12 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
   const int ppb = 8;
   if (N > 0) {
     dim3 grid((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((P + ppb - 1) / ppb));
-    hipLaunchKernelGGL(k_eval_parity, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, (int)N, d->d_pods, (int)P, ppb,
-                       k, d_status, d_reason, d_la, d_numa, d_ds, d_total, d_dsmax);
+    if (d->numa_alloc)
+      hipLaunchKernelGGL(k_eval_parity<true>, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, (int)N, d->d_pods, (int)P,
+                         ppb, k, d_status, d_reason, d_la, d_numa, d_ds, d_total, d_dsmax);
+    else
+      hipLaunchKernelGGL(k_eval_parity<false>, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, (int)N, d->d_pods, (int)P,
+                         ppb, k, d_status, d_reason, d_la, d_numa, d_ds, d_total, d_dsmax);
     HIP_OK(hipGetLastError());
     dim3 grid2((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)P);
     hipLaunchKernelGGL(k_parity_finalize, grid2, dim3(EVAL_BLOCK), 0, d->stream, (int)N, k, d_ds, d_total, d_dsmax,
@@ -1445,12 +1910,16 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     if (d->d_chosen_score) HIP_OK(hipFree(d->d_chosen_score));
     if (d->d_stamps) HIP_OK(hipFree(d->d_stamps));
     if (d->d_devalloc) HIP_OK(hipFree(d->d_devalloc));
+    if (d->d_numaalloc) HIP_OK(hipFree(d->d_numaalloc));
+    d->d_numaalloc = nullptr;
     HIP_OK(hipMalloc(&d->d_chosen, out_bytes));
     HIP_OK(hipMalloc(&d->d_chosen_score, out_bytes));
     HIP_OK(hipMalloc(&d->d_stamps, sizeof(uint64_t) * 10 * ((int64_t)n_pods + 2)));
     HIP_OK(hipMalloc(&d->d_devalloc, sizeof(uint64_t) * n_pods));
     d->out_cap = n_pods;
   }
+  const bool numa = d->numa_alloc;
+  if (numa && !d->d_numaalloc) HIP_OK(hipMalloc(&d->d_numaalloc, sizeof(int64_t) * 16 * d->out_cap));
   const KArgs k = make_kargs(ctx, now);
   const int N = ctx->n_nodes;
   const int ppb = 8;
@@ -1481,12 +1950,10 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       if (sharded && !d->loopback) shard_range(N, d->rank, d->world, &lo, &hi);
       if (hi > lo) {
         dim3 grid((unsigned)((hi - lo + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((bp + ppb - 1) / ppb));
-        if (ds)
-          hipLaunchKernelGGL(k_eval_batch<true>, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, lo, hi, d->d_pods,
-                             d->d_batch_base, bp, ppb, k, d->d_scores, d->capacity, d->d_dsraw);
-        else
-          hipLaunchKernelGGL(k_eval_batch<false>, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, lo, hi, d->d_pods,
-                             d->d_batch_base, bp, ppb, k, d->d_scores, d->capacity, d->d_dsraw);
+        auto eval = ds ? (numa ? k_eval_batch<true, true> : k_eval_batch<true, false>)
+                       : (numa ? k_eval_batch<false, true> : k_eval_batch<false, false>);
+        hipLaunchKernelGGL(eval, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, lo, hi, d->d_pods, d->d_batch_base, bp,
+                           ppb, k, d->d_scores, d->capacity, d->d_dsraw);
       }
       if (ds) {  // DefaultNormalizeScore's max over the feasible nodes (all ranks)
         HIP_OK(hipMemsetAsync(d->d_dsmax, 0, sizeof(uint32_t), d->stream));
@@ -1528,14 +1995,13 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       HIP_OK(hipMemsetAsync(d->d_cand_cnt, 0, sizeof(int32_t) * MAX_BATCH, d->stream));
     }
     if (prof) HIP_OK(hipEventRecord(pe[2], d->stream));
-    if (ds)
-      hipLaunchKernelGGL(k_resolve<true>, dim3(1), dim3(RES_THREADS), 0, d->stream, d->soa, d->d_pods, d->d_batch_base,
-                         bp, k, d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score, ctx->cfg.global_node_offset,
-                         d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc);
-    else
-      hipLaunchKernelGGL(k_resolve<false>, dim3(1), dim3(RES_THREADS), 0, d->stream, d->soa, d->d_pods, d->d_batch_base,
-                         bp, k, d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score, ctx->cfg.global_node_offset,
-                         d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc);
+    {
+      auto resolve = ds ? (numa ? k_resolve<true, true> : k_resolve<true, false>)
+                        : (numa ? k_resolve<false, true> : k_resolve<false, false>);
+      hipLaunchKernelGGL(resolve, dim3(1), dim3(RES_THREADS), 0, d->stream, d->soa, d->d_pods, d->d_batch_base, bp, k,
+                         d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score, ctx->cfg.global_node_offset,
+                         d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc, d->d_numaalloc);
+    }
     if (prof) HIP_OK(hipEventRecord(pe[3], d->stream));
   }
   HIP_OK(hipGetLastError());
@@ -1545,6 +2011,12 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   ctx->last_dev_alloc.assign((size_t)n_pods, 0);
   HIP_OK(hipMemcpyAsync(ctx->last_dev_alloc.data(), d->d_devalloc, sizeof(uint64_t) * n_pods, hipMemcpyDeviceToHost,
                         d->stream));
+  ctx->last_numa_alloc.clear();
+  if (numa) {
+    ctx->last_numa_alloc.assign((size_t)n_pods * 16, 0);
+    HIP_OK(hipMemcpyAsync(ctx->last_numa_alloc.data(), d->d_numaalloc, sizeof(int64_t) * 16 * n_pods,
+                          hipMemcpyDeviceToHost, d->stream));
+  }
   std::vector<uint64_t> st((size_t)n_batches + 1), pst(8 * (size_t)n_batches);
   HIP_OK(hipMemcpyAsync(st.data(), d->d_stamps, sizeof(uint64_t) * (n_batches + 1), hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipMemcpyAsync(pst.data(), d->d_stamps + (n_pods + 2), sizeof(uint64_t) * 8 * n_batches,
@@ -1616,14 +2088,14 @@ int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t 
   const int ppb = 8;
   HIP_OK(hipMemsetAsync(d->d_batch_base, 0, sizeof(int32_t), d->stream));
   dim3 grid((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((n_pods + ppb - 1) / ppb));
-  hipLaunchKernelGGL(k_eval_batch<false>, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base, n_pods,
+  hipLaunchKernelGGL((k_eval_batch<false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base, n_pods,
                      ppb, k, d->d_scores, d->capacity, d->d_dsraw);  // warm
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   HIP_OK(hipEventRecord(e0, d->stream));
   for (int it = 0; it < iters; it++)
-    hipLaunchKernelGGL(k_eval_batch<false>, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base,
+    hipLaunchKernelGGL((k_eval_batch<false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base,
                        n_pods, ppb, k, d->d_scores, d->capacity, d->d_dsraw);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(e1, d->stream));

@@ -51,7 +51,20 @@ enum NodeFlag : uint32_t {
   NF_NUMA_RATIO_S = 1u << 13,  // score ratio > 1
   NF_NUMA_SCORE_ZERO = 1u << 14,  // getResourceOptions error -> Score 0
   NF_DS_CACHE = 1u << 15,         // nodeDeviceCache has an entry for the node (DeviceShare runs)
+  NF_NUMA_POLICY0 = 1u << 16,     // 2 bits: the node's NUMA topology policy (KE_NUMA_POLICY_*)
+  NF_NUMA_OPT_ERR = 1u << 18,     // getResourceOptions fails (amplification annotation unparsable)
 };
+KE_HD inline int nf_numa_policy(uint32_t f) { return (int)((f >> 16) & 3u); }
+
+// ---- NUMA topology state (a third SoA, allocated when the first node with a NUMA policy appears) ----
+// int64 fields indexed by NUMA id z (0..7) and resource r (cpu milli, memory):
+//   NUMA_CAP + 2z + r: TopologyOptions.NUMANodeResources after amplifyNUMANodeResources
+//   NUMA_AL  + 2z + r: the zone's allocated resources, cpu adjusted for amplified cpusets
+//                      (getAvailableNUMANodeResources before its non-negative clamp)
+// uint32 mask: zone present (bits 0-7), cpu key (8-15), memory key (16-23), allocation entry (24-31)
+constexpr int NUMA_CAP = 0;
+constexpr int NUMA_AL = 16;
+constexpr int NUM_NUMA_FIELDS = 32;
 KE_HD constexpr uint32_t nf_fh_on(int v, int r) { return NF_FH_ON0 << (2 * v + r); }
 
 // pod flags
@@ -118,6 +131,7 @@ enum ArgFlag : uint32_t {
   AF_EXP_PRESENT = 1u << 2,         // args.NodeMetricExpirationSeconds != nil
   AF_NUMA_MOST = 1u << 3,           // NodeNUMAResource MostAllocated
   AF_DS_MOST = 1u << 4,             // DeviceShare MostAllocated
+  AF_NUMA_HINT_MOST = 1u << 5,      // NodeNUMAResource NUMAScoringStrategy MostAllocated (hint scores)
 };
 struct KArgs {
   int64_t now;

@@ -121,6 +121,11 @@ class Evaluator:
     def delete_devices(self, i):
         self._check(self.lib.ke_node_devices_delete(self.h, i))
 
+    def set_numa(self, i, zones):
+        """NodeResourceTopology NUMA zones + their allocation (model.make_zones(...))."""
+        zones = np.ascontiguousarray(zones, dtype=abi.NUMA_ZONE_DTYPE)
+        self._check(self.lib.ke_node_numa_set(self.h, i, len(zones), abi.ptr(zones)))
+
     def estimate_pod(self, pod):
         est = np.zeros(2, np.int64)
         self._check(self.lib.ke_estimate_pod(self.h, C.byref(pod), abi.ptr(est)))
@@ -166,6 +171,8 @@ class Evaluator:
         self._check(self.lib.ke_schedule(self.h, len(pods), abi.ptr(pods), int(now_ns), abi.ptr(chosen), abi.ptr(score)))
         self.last_device_allocations = np.zeros(len(pods), np.uint64)
         self._check(self.lib.ke_last_device_allocations(self.h, len(pods), abi.ptr(self.last_device_allocations)))
+        self.last_numa_allocations = np.zeros((len(pods), 16), np.int64)
+        self._check(self.lib.ke_last_numa_allocations(self.h, len(pods), abi.ptr(self.last_numa_allocations)))
         return chosen, score
 
     def stats(self):

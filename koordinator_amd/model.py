@@ -341,3 +341,22 @@ def make_devices(devices):
                 getattr(dev, field)[key] = value(q)
         arr[i] = np.frombuffer(bytes(dev), dtype=abi.DEVICE_DTYPE)[0]
     return arr
+
+
+def make_zones(zones):
+    """NodeResourceTopology zones + the resource manager's allocation: [dict(id, cpu=quantity | None,
+    memory=quantity | None, allocated={'cpu':..., 'memory':...} | None, cpuset_cpus=0)] ->
+    np.ndarray(NUMA_ZONE_DTYPE).  A resource left out is absent from the zone's ResourceList."""
+    arr = np.zeros(len(zones), dtype=abi.NUMA_ZONE_DTYPE)
+    for i, z in enumerate(zones):
+        arr[i]["id"] = int(z["id"])
+        for r, name in ((0, "cpu"), (1, "memory")):
+            if z.get(name) is not None:
+                arr[i]["has"][r] = 1
+                arr[i]["capacity"][r] = resource_value(name, z[name])
+        al = z.get("allocated")
+        if al is not None:
+            arr[i]["has_allocated"] = 1
+            arr[i]["allocated"][:] = [milli_value(al.get("cpu", 0)), value(al.get("memory", 0))]
+        arr[i]["cpuset_cpus"] = int(z.get("cpuset_cpus", 0))
+    return arr

@@ -280,3 +280,49 @@ def make_ds_pods(n_pods, seed, device_fraction=0.5, key_base=2_000_000_000):
             r[abi.PDR["koordinator.sh/rdma"]] = rng.choice([50, 100])
         pods["has_other_requests"][i] = 1
     return pods
+
+
+# ---- NUMA topology policies (BASELINE config 4, non-cpuset part) ----------------------------------
+def make_numa(cl, seed, zone_counts=(8,), policy_weights=(0.1, 0.3, 0.3, 0.3), no_zone_fraction=0.02,
+              missing_memory_fraction=0.03, allocated_fraction=0.7):
+    """Give the nodes of cluster `cl` a NUMA topology policy (None / BestEffort / Restricted /
+    SingleNUMANode by `policy_weights`) and NodeResourceTopology zones: the node's allocatable split
+    evenly over `zone_counts` zones (cpu in whole cores), a few zones without a memory key, and a
+    random resource-manager allocation on most zones (cpuset CPUs on a quarter of the allocated zones
+    of amplified nodes).  Mutates cl.nodes; returns the per-node zone arrays (None = no NRT zones)."""
+    rng = np.random.default_rng(seed)
+    N = cl.n_nodes
+    pol = rng.choice(4, N, p=np.asarray(policy_weights) / np.sum(policy_weights))
+    cl.nodes["numa_topology_policy"] = pol
+    out = []
+    for i in range(N):
+        if rng.random() < no_zone_fraction:
+            out.append(None)
+            continue
+        nz = int(rng.choice(zone_counts))
+        cores = int(cl.nodes["allocatable"][i, 0]) // 1000
+        mem = int(cl.nodes["allocatable"][i, 1])
+        z = np.zeros(nz, abi.NUMA_ZONE_DTYPE)
+        amplified = cl.nodes["cpu_amplification_ratio"][i] > 1.0
+        for k in range(nz):
+            z[k]["id"] = k
+            z[k]["has"][0] = 1
+            z[k]["capacity"][0] = (cores // nz) * 1000
+            if rng.random() >= missing_memory_fraction:
+                z[k]["has"][1] = 1
+                z[k]["capacity"][1] = mem // nz // MI * MI
+            if rng.random() < allocated_fraction:
+                z[k]["has_allocated"] = 1
+                f = rng.choice([0.0, 0.25, 0.5, 0.75, 0.9, 1.0])
+                z[k]["allocated"][0] = int(z[k]["capacity"][0] * f) // 1000 * 1000
+                z[k]["allocated"][1] = int(z[k]["capacity"][1] * rng.choice([0.0, 0.3, 0.6, 0.95])) // MI * MI
+                if amplified and rng.random() < 0.25:
+                    z[k]["cpuset_cpus"] = int(rng.integers(1, 4))
+        out.append(z)
+    return out
+
+
+def load_numa(handle, zones):
+    for i, z in enumerate(zones):
+        if z is not None:
+            handle.set_numa(i, z)

@@ -47,12 +47,14 @@ def load():
         "or_numa_score": (i64, [V, C.POINTER(abi.Pod), i32]),
         "or_estimate_pod": (None, [V, C.POINTER(abi.Pod), V]),
         "or_eval": (C.c_int, [V, i32, V, i64, V, V, V, V, V, V, V, C.c_int]),
-        "or_schedule": (C.c_int, [V, i32, V, i64, V, V, V, C.c_int]),
+        "or_schedule": (C.c_int, [V, i32, V, i64, V, V, V, V, C.c_int]),
         "or_node_devices_set": (C.c_int, [V, i32, i32, V]),
         "or_node_devices_delete": (C.c_int, [V, i32]),
         "or_ds_prefilter": (C.c_int, [C.POINTER(abi.Pod), C.POINTER(C.c_int), V, V, V]),
         "or_ds_score_device": (i64, [V, i32, V, V, V, V, V, V]),
         "or_normalize_scores": (None, [V, i32]),
+        "or_topology_merge": (C.c_int, [i32, C.c_uint32, i32, V, V, V, V, V, V, V, V, V]),
+        "or_node_numa_set": (C.c_int, [V, i32, i32, V]),
         "or_ds_filter": (C.c_int, [V, C.POINTER(abi.Pod), i32, C.POINTER(C.c_int)]),
         "or_ds_score": (i64, [V, C.POINTER(abi.Pod), i32]),
         "or_ds_reserve": (C.c_uint64, [V, C.POINTER(abi.Pod), i32]),
@@ -138,6 +140,10 @@ class Oracle:
         devices = np.ascontiguousarray(devices, dtype=abi.DEVICE_DTYPE)
         assert self.lib.or_node_devices_set(self.h, i, len(devices), abi.ptr(devices)) == 0
 
+    def set_numa(self, i, zones):
+        zones = np.ascontiguousarray(zones, dtype=abi.NUMA_ZONE_DTYPE)
+        assert self.lib.or_node_numa_set(self.h, i, len(zones), abi.ptr(zones)) == 0
+
     def delete_devices(self, i):
         assert self.lib.or_node_devices_delete(self.h, i) == 0
 
@@ -213,8 +219,10 @@ class Oracle:
         chosen = np.zeros(len(pods), np.int32)
         score = np.zeros(len(pods), np.int32)
         self.last_device_allocations = np.zeros(len(pods), np.uint64)
+        self.last_numa_allocations = np.zeros((len(pods), 16), np.int64)
         rc = self.lib.or_schedule(self.h, len(pods), abi.ptr(pods), int(now_ns), abi.ptr(chosen), abi.ptr(score),
-                                  abi.ptr(self.last_device_allocations), n_threads)
+                                  abi.ptr(self.last_device_allocations), abi.ptr(self.last_numa_allocations),
+                                  n_threads)
         if rc != 0:
             raise RuntimeError(f"oracle schedule rc={rc}")
         return chosen, score
@@ -228,3 +236,20 @@ def normalize_scores(scores):
 
 def usage_percent(used, total):
     return load().or_usage_percent(used, total)
+
+
+def topology_merge(policy, all_mask, lists):
+    """Policy.Merge over raw lists: lists = [(kind, [(mask, preferred, score), ...])]; kind 0 list,
+    1 nil list (no preference), 2 empty list.  Returns (admit, mask, preferred, unsatisfied, score)."""
+    lib = load()
+    kinds = np.array([k for k, _ in lists] or [0], np.int32)
+    lens = np.array([len(h) for _, h in lists] or [0], np.int32)
+    flat = [x for _, h in lists for x in h]
+    masks = np.array([m for m, _, _ in flat] or [0], np.uint32)
+    pref = np.array([int(p) for _, p, _ in flat] or [0], np.uint8)
+    scores = np.array([s for _, _, s in flat] or [0], np.int64)
+    om, op, ou, os_ = C.c_uint32(), C.c_uint8(), C.c_uint8(), C.c_int64()
+    admit = lib.or_topology_merge(policy, all_mask, len(lists), abi.ptr(kinds), abi.ptr(lens), abi.ptr(masks),
+                                  abi.ptr(pref), abi.ptr(scores), C.byref(om), C.byref(op), C.byref(ou),
+                                  C.byref(os_))
+    return bool(admit), om.value, bool(op.value), bool(ou.value), os_.value

@@ -49,6 +49,8 @@ typedef struct or_node {
   int32_t n_agg;
   or_asg* asg;
   int32_t n_asg, cap_asg;
+  int32_t n_zone; /* TopologyOptions.NUMANodeResources + the resource manager's per-zone allocation */
+  ke_numa_zone zone[KE_MAX_NUMA];
   int has_dev_cache; /* nodeDeviceCache.getNodeDevice != nil */
   int32_t n_dev;
   ke_device dev[KE_DEV_TYPES * KE_MAX_MINORS];
@@ -363,7 +365,10 @@ static int pod_is_cpuset(const ke_pod* pod) {
 static int pod_unsupported(const ke_pod* pod) {
   return pod_is_cpuset(pod) || pod->has_resource_spec || pod->has_unsupported_device_requests;
 }
-static int node_unsupported(const ke_node* n) { return n->numa_topology_policy != 0 || n->cpu_bind_policy != 0; }
+static int node_unsupported(const ke_node* n) {
+  return n->numa_topology_policy < 0 || n->numa_topology_policy > KE_NUMA_POLICY_SINGLE_NUMA_NODE ||
+         n->cpu_bind_policy != 0;
+}
 
 /* ---------------------------------------------------------------------------------------------- */
 /* LoadAwareScheduling                                                                             */
@@ -468,10 +473,28 @@ static int pod_requests_zero(const ke_pod* pod) { /* quotav1.IsZero(PodRequests)
 }
 
 /* Plugin.Filter  plugin.go:318-406 -> filterAmplifiedCPUs :408-442 */
+static int numa_filter_amplified(const or_node* n, const ke_pod* pod, int* reason);
+static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod, int policy, uint32_t* affinity,
+                      int* reason);
+
 int or_numa_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* reason) {
   const or_node* n = &c->nodes[node];
   *reason = KE_REASON_NONE;
   if (pod_requests_zero(pod)) return KE_CODE_SUCCESS; /* state.skip */
+  const int code = numa_filter_amplified(n, pod, reason);
+  if (code != KE_CODE_SUCCESS) return code;
+  const int policy = n->node.numa_topology_policy; /* mergeTopologyPolicy: the pod sets none */
+  if (policy == KE_NUMA_POLICY_NONE) return KE_CODE_SUCCESS;
+  if (n->n_zone == 0) { /* FilterByNUMANode  topology_hint.go:31-41 */
+    *reason = KE_REASON_NUMA_MISSING_RESOURCES;
+    return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+  }
+  uint32_t aff;
+  return numa_admit(c, n, pod, policy, &aff, reason);
+}
+
+/* filterAmplifiedCPUs  plugin.go:408-442 */
+static int numa_filter_amplified(const or_node* n, const ke_pod* pod, int* reason) {
   const int64_t pod_cpu = pod->requests[KE_RES_CPU];
   if (pod_cpu == 0) return KE_CODE_SUCCESS;
   if (n->node.amplification_error) {
@@ -499,8 +522,8 @@ int or_numa_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* re
 
 /* resourceAllocationScorer.score (scoring.go:210-226) with least/mostResourceScorer
  * (least_allocated.go:30-58, most_allocated.go:30-62) over cpu and memory. */
-static int64_t numa_resource_score(const ke_numa_args* na, const int64_t* requested, const int64_t* allocatable,
-                                   const ke_pod* pod) {
+static int64_t numa_resource_score_as(const ke_numa_args* na, int strategy, const int64_t* requested,
+                                      const int64_t* allocatable, const ke_pod* pod) {
   int64_t score = 0, wsum = 0;
   for (int r = 0; r < KE_NRES; r++) {
     int64_t w = na->weights[r];
@@ -509,7 +532,7 @@ static int64_t numa_resource_score(const ke_numa_args* na, const int64_t* reques
     int64_t req = requested[r] + pod->requests[r];
     if (alloc == 0) continue; /* calculateResourceAllocatableRequest result dropped */
     int64_t s;
-    if (na->strategy == KE_STRATEGY_MOST_ALLOCATED) {
+    if (strategy == KE_STRATEGY_MOST_ALLOCATED) {
       int64_t rq = req > alloc ? alloc : req;
       s = (rq * MAX_NODE_SCORE) / alloc;
     } else {
@@ -520,11 +543,437 @@ static int64_t numa_resource_score(const ke_numa_args* na, const int64_t* reques
   }
   return wsum ? score / wsum : 0;
 }
+static int64_t numa_resource_score(const ke_numa_args* na, const int64_t* requested, const int64_t* allocatable,
+                                   const ke_pod* pod) {
+  return numa_resource_score_as(na, na->strategy, requested, allocatable, pod);
+}
+
+/* ---------------------------------------------------------------------------------------------- */
+/* NUMA topology policies for non-cpuset pods: GetPodTopologyHints (topology_hint.go:43-76,          */
+/* resource_manager.go:130-192,525-653), topologymanager Admit / Merge (manager.go:64-129,          */
+/* policy*.go), Allocate by hint (resource_manager.go:194-330), NUMA-scope Score (scoring.go:141-187) */
+/* ---------------------------------------------------------------------------------------------- */
+
+typedef struct numa_view {
+  int n;
+  int id[KE_MAX_NUMA];
+  uint8_t cap_has[KE_MAX_NUMA][KE_NRES];
+  int64_t cap[KE_MAX_NUMA][KE_NRES];     /* amplified NUMANodeResources (amplifyNUMANodeResources) */
+  uint8_t av_has[KE_MAX_NUMA][KE_NRES];
+  int64_t av[KE_MAX_NUMA][KE_NRES];      /* totalAvailable */
+  int has_alloc[KE_MAX_NUMA];
+  int64_t al[KE_MAX_NUMA][KE_NRES];      /* totalAllocated (cpu adjusted for amplified cpusets) */
+  uint8_t al_has[KE_MAX_NUMA][KE_NRES];
+} numa_view;
+
+/* getResourceOptions -> amplifyNUMANodeResources (util.go:78-98) + getAvailableNUMANodeResources
+ * (node_allocation.go:221-243).  Returns -1 on an amplification-ratio annotation error. */
+static int numa_view_build(const or_node* nd, numa_view* v) {
+  memset(v, 0, sizeof *v);
+  double ratio;
+  int amplify_caps = 0;
+  if (nd->node.nrt_cpu_amplification_ratio > -1.5) { /* TopologyOptions.AmplificationRatios != nil */
+    ratio = nd->node.nrt_cpu_amplification_ratio < 0 ? 0.0 : nd->node.nrt_cpu_amplification_ratio;
+  } else {
+    if (nd->node.amplification_error) return -1;
+    ratio = nd->node.cpu_amplification_ratio < 0 ? 0.0 : nd->node.cpu_amplification_ratio;
+    amplify_caps = 1;
+  }
+  v->n = nd->n_zone;
+  for (int z = 0; z < nd->n_zone; z++) {
+    const ke_numa_zone* zn = &nd->zone[z];
+    v->id[z] = zn->id;
+    for (int r = 0; r < KE_NRES; r++) {
+      v->cap_has[z][r] = zn->has[r];
+      v->cap[z][r] = zn->has[r] ? zn->capacity[r] : 0;
+    }
+    if (amplify_caps && ratio > 1.0 && v->cap_has[z][KE_RES_CPU] && v->cap[z][KE_RES_CPU] != 0)
+      v->cap[z][KE_RES_CPU] = amplify(v->cap[z][KE_RES_CPU], ratio);
+    v->has_alloc[z] = zn->has_allocated;
+    if (zn->has_allocated) {
+      int64_t al[KE_NRES] = {zn->allocated[0], zn->allocated[1]};
+      if (ratio > 1.0) {
+        const int64_t cs = (int64_t)zn->cpuset_cpus * 1000;
+        al[KE_RES_CPU] = al[KE_RES_CPU] - cs + amplify(cs, ratio);
+      }
+      for (int r = 0; r < KE_NRES; r++) { /* SubtractWithNonNegativeResult(allocated, reusable = {}) */
+        v->al_has[z][r] = 1;
+        v->al[z][r] = al[r] > 0 ? al[r] : 0;
+      }
+    }
+    for (int r = 0; r < KE_NRES; r++) { /* SubtractWithNonNegativeResult(capacity, allocated) */
+      const int64_t a = v->has_alloc[z] ? v->al[z][r] : 0;
+      v->av_has[z][r] = v->cap_has[z][r] || v->has_alloc[z];
+      const int64_t q = v->cap_has[z][r] ? v->cap[z][r] - a : -a;
+      v->av[z][r] = q > 0 ? q : 0;
+    }
+  }
+  return 0;
+}
+
+static int zone_of(const numa_view* v, int id) {
+  for (int z = 0; z < v->n; z++)
+    if (v->id[z] == id) return z;
+  return -1;
+}
+
+/* the pod's requests as options.requests sees them (PodRequests keys cpu / memory, non-zero) */
+static int pod_has_req(const ke_pod* pod, int r) { return pod->requests[r] != 0; }
+
+/* tryBestToDistributeEvenly (resource_manager.go:260-314) over the NUMA ids in `mask`.  The sort of the
+ * hint's nodes compares totalAvailable indexed by slice position (a reference quirk, reproduced):
+ * Go's sort.Slice on <= 12 elements is an insertion sort.  out[z][r]: allocated per zone. */
+static int numa_distribute(const numa_view* v, uint32_t mask, const ke_pod* pod, int64_t out[KE_MAX_NUMA][KE_NRES]) {
+  memset(out, 0, sizeof(int64_t) * KE_MAX_NUMA * KE_NRES);
+  int names[KE_NRES] = {0, 0}; /* resourceNamesByNUMA: keys of any totalAvailable entry */
+  for (int z = 0; z < v->n; z++)
+    for (int r = 0; r < KE_NRES; r++) names[r] |= v->av_has[z][r];
+  int bits[KE_MAX_NUMA], nb = 0;
+  for (int b = 0; b < KE_MAX_NUMA; b++)
+    if (mask & (1u << b)) bits[nb++] = b;
+  int ok = 1;
+  for (int r = 0; r < KE_NRES; r++) {
+    if (!names[r] || !pod_has_req(pod, r)) continue;
+    int sorted[KE_MAX_NUMA];
+    for (int i = 0; i < nb; i++) sorted[i] = bits[i];
+    for (int i = 1; i < nb; i++) /* insertionSortLessFunc with less(i,j) = avail[pos i] < avail[pos j] */
+      for (int j = i; j > 0; j--) {
+        const int zj = zone_of(v, j), zj1 = zone_of(v, j - 1);
+        const int64_t aj = zj >= 0 && v->av_has[zj][r] ? v->av[zj][r] : 0;
+        const int64_t aj1 = zj1 >= 0 && v->av_has[zj1][r] ? v->av[zj1][r] : 0;
+        if (!(aj < aj1)) break;
+        const int t = sorted[j];
+        sorted[j] = sorted[j - 1];
+        sorted[j - 1] = t;
+      }
+    int64_t q = pod->requests[r];
+    for (int i = 0; i < nb; i++) {
+      const int64_t split = q / (nb - i); /* splitQuantity: cpu milli / memory value */
+      const int z = zone_of(v, sorted[i]);
+      const int64_t avail = z >= 0 && v->av_has[z][r] ? v->av[z][r] : 0;
+      const int64_t got = avail > split ? split : avail; /* allocateRes */
+      if (got != 0) {
+        out[z][r] += got;
+        q -= got;
+      }
+    }
+    if (q != 0) ok = 0;
+  }
+  return ok;
+}
+
+typedef struct numa_hint {
+  uint32_t mask; /* 0 = nil NUMANodeAffinity */
+  int preferred, unsatisfied;
+  int64_t score;
+} numa_hint;
+
+/* generateResourceHints (resource_manager.go:525-622) for a non-cpuset pod.  Per resource (cpu,
+ * memory): the list of hints in IterateBitMasks order; present[r] = the resource has a list. */
+static void numa_generate_hints(const or_cluster* c, const numa_view* v, const ke_pod* pod, int policy,
+                                numa_hint* lists /*[KE_NRES][255]*/, int* counts, int* present) {
+  int names[KE_NRES] = {0, 0};
+  for (int z = 0; z < v->n; z++)
+    for (int r = 0; r < KE_NRES; r++) names[r] |= v->cap_has[z][r];
+  uint32_t lack[KE_NRES] = {0, 0}; /* numaNodesLackResource */
+  for (int r = 0; r < KE_NRES; r++)
+    if (names[r])
+      for (int z = 0; z < v->n; z++)
+        if (!v->av_has[z][r] || v->av[z][r] == 0) lack[r] |= 1u << v->id[z];
+  int min_size[KE_NRES] = {v->n, v->n};
+  int total_names[KE_NRES] = {0, 0};
+  for (int r = 0; r < KE_NRES; r++) counts[r] = 0;
+  /* IterateBitMasks: sizes 1..n, combinations of the zone ids in lexicographic order */
+  for (int size = 1; size <= v->n; size++) {
+    int idx[KE_MAX_NUMA];
+    for (int i = 0; i < size; i++) idx[i] = i;
+    for (;;) {
+      uint32_t mask = 0;
+      int64_t avail[KE_NRES] = {0, 0}, total[KE_NRES] = {0, 0};
+      int total_has[KE_NRES] = {0, 0};
+      for (int i = 0; i < size; i++) {
+        const int z = idx[i];
+        mask |= 1u << v->id[z];
+        for (int r = 0; r < KE_NRES; r++) {
+          avail[r] += v->av_has[z][r] ? v->av[z][r] : 0;
+          total[r] += v->cap_has[z][r] ? v->cap[z][r] : 0;
+          total_has[r] |= v->cap_has[z][r];
+        }
+      }
+      for (int r = 0; r < KE_NRES; r++)
+        if (pod_has_req(pod, r) && total_has[r]) total_names[r] = 1;
+      /* numaScorer.score(requested = total - available, total, pod) with the NUMA strategy */
+      int64_t req[KE_NRES];
+      for (int r = 0; r < KE_NRES; r++) req[r] = total[r] - avail[r] > 0 ? total[r] - avail[r] : 0;
+      const int64_t score = numa_resource_score_as(&c->cfg.numa, c->cfg.numa.numa_strategy, req, total, pod);
+      int64_t out[KE_MAX_NUMA][KE_NRES];
+      if (numa_distribute(v, mask, pod, out))
+        for (int r = 0; r < KE_NRES; r++) { /* generator.generateHints per resource */
+          if (!total_names[r]) continue;
+          if (mask & lack[r]) continue;
+          if (size < min_size[r]) min_size[r] = size;
+          numa_hint h = {mask, 0, 0, score};
+          lists[r * 255 + counts[r]++] = h;
+        }
+      int i = size - 1; /* next combination */
+      while (i >= 0 && idx[i] == v->n - size + i) i--;
+      if (i < 0) break;
+      idx[i]++;
+      for (int j = i + 1; j < size; j++) idx[j] = idx[j - 1] + 1;
+    }
+  }
+  for (int r = 0; r < KE_NRES; r++) {
+    present[r] = total_names[r] && pod_has_req(pod, r);
+    for (int i = 0; i < counts[r]; i++)
+      lists[r * 255 + i].preferred = __builtin_popcount(lists[r * 255 + i].mask) == min_size[r] ||
+                                     policy == KE_NUMA_POLICY_RESTRICTED;
+  }
+}
+
+/* mergePermutation (policy.go:98-137) */
+static numa_hint merge_permutation(uint32_t all, const numa_hint* perm, int n) {
+  int preferred = 1, satisfied = 1, maxn = 0, have = 0;
+  uint32_t first = 0, merged = all;
+  for (int i = 0; i < n; i++) {
+    if (perm[i].mask) {
+      if (!have) first = perm[i].mask, have = 1;
+      if (perm[i].mask != first) preferred = 0;
+      if (__builtin_popcount(perm[i].mask) > maxn) maxn = __builtin_popcount(perm[i].mask);
+      merged &= perm[i].mask;
+    }
+    if (!perm[i].preferred) preferred = 0;
+    if (perm[i].unsatisfied) satisfied = 0;
+  }
+  satisfied = (!have || maxn == __builtin_popcount(merged)) && satisfied;
+  numa_hint h = {merged, preferred, !satisfied, 0};
+  return h;
+}
+
+static int narrower(uint32_t a, uint32_t b) { /* bitmask.IsNarrowerThan */
+  const int ca = __builtin_popcount(a), cb = __builtin_popcount(b);
+  return ca == cb ? a < b : ca < cb;
+}
+
+/* mergeFilteredHints (policy.go:198-260) + iterateAllProviderTopologyHints (:282-299) */
+static numa_hint merge_filtered(uint32_t all, numa_hint* const* lists, const int* lens, int nl) {
+  numa_hint best = {all, 0, 0, 0};
+  int idx[4] = {0, 0, 0, 0};
+  for (int i = 0; i < nl; i++)
+    if (lens[i] == 0) return best; /* an empty list: no permutation */
+  for (;;) {
+    numa_hint perm[4];
+    for (int i = 0; i < nl; i++) perm[i] = lists[i][idx[i]];
+    numa_hint m = merge_permutation(all, perm, nl);
+    if (__builtin_popcount(m.mask) != 0) {
+      /* checkExclusivePolicy: the pod sets no NUMA exclusive policy -> always satisfied */
+      for (int i = 0; i < nl; i++)
+        if (perm[i].mask && perm[i].mask == m.mask) m.score += perm[i].score;
+      if (m.preferred && !best.preferred) {
+        best = m;
+      } else if (!(!m.preferred && best.preferred)) {
+        if (!narrower(m.mask, best.mask)) {
+          if (__builtin_popcount(m.mask) == __builtin_popcount(best.mask) && m.score > best.score) best = m;
+        } else {
+          best = m;
+        }
+      }
+    }
+    int i = nl - 1;
+    while (i >= 0 && ++idx[i] == lens[i]) idx[i--] = 0;
+    if (i < 0) break;
+  }
+  return best;
+}
+
+/* Policy.Merge after filterProvidersHints (policy_best_effort.go:48-60, policy_restricted.go:50-62,
+ * policy_single_numa_node.go:52-90).  `lists` are the filtered provider lists (for SingleNUMANode
+ * already reduced by filterSingleNumaHints); `reasons` = filterProvidersHints reported an empty list.
+ * Returns admit; *best = the merged hint (mask 0 = nil affinity). */
+static int policy_merge(int policy, uint32_t all, numa_hint* const* lists, const int* lens, int nl, int reasons,
+                        numa_hint* best) {
+  if (policy == KE_NUMA_POLICY_BEST_EFFORT) {
+    *best = merge_filtered(all, lists, lens, nl);
+    if (best->unsatisfied) *best = (numa_hint){all, 0, 0, 0};
+    return 1;
+  }
+  if (policy == KE_NUMA_POLICY_RESTRICTED) {
+    if (reasons) {
+      *best = (numa_hint){all, 0, 0, 0};
+      return 0;
+    }
+    *best = merge_filtered(all, lists, lens, nl);
+    return best->preferred;
+  }
+  if (reasons) { /* SingleNUMANode */
+    *best = (numa_hint){0, 0, 0, 0};
+    return 0;
+  }
+  *best = merge_filtered(all, lists, lens, nl);
+  if (best->mask == all) *best = (numa_hint){0, best->preferred, 0, 0};
+  return best->preferred;
+}
+
+/* Golden-vector entry point: Policy.Merge over raw provider hint lists.  kinds[i]: 0 = a hint list,
+ * 1 = nil list / provider without hints (one preferred any-NUMA hint), 2 = empty list (unsatisfied,
+ * reason).  Hints are flattened: masks (0 = nil affinity), preferred, scores; lens[i] per list. */
+int or_topology_merge(int32_t policy, uint32_t all, int32_t n_lists, const int32_t* kinds, const int32_t* lens,
+                      const uint32_t* masks, const uint8_t* preferred, const int64_t* scores, uint32_t* out_mask,
+                      uint8_t* out_preferred, uint8_t* out_unsatisfied, int64_t* out_score) {
+  static __thread numa_hint buf[16][64];
+  numa_hint* lists[16];
+  int ln[16], nl = 0, reasons = 0, off = 0;
+  if (n_lists > 15) return -1;
+  for (int i = 0; i < n_lists; i++) {
+    lists[nl] = buf[nl];
+    if (kinds[i] == 1) {
+      buf[nl][0] = (numa_hint){0, 1, 0, 0};
+      ln[nl++] = 1;
+      continue;
+    }
+    if (kinds[i] == 2) {
+      buf[nl][0] = (numa_hint){0, 0, 1, 0};
+      ln[nl] = policy == KE_NUMA_POLICY_SINGLE_NUMA_NODE ? 0 : 1;
+      nl++;
+      reasons = 1;
+      continue;
+    }
+    int n = 0;
+    for (int j = 0; j < lens[i] && j < 64; j++) {
+      numa_hint h = {masks[off + j], preferred[off + j], 0, scores[off + j]};
+      if (policy == KE_NUMA_POLICY_SINGLE_NUMA_NODE &&  /* filterSingleNumaHints */
+          !((h.mask == 0 && h.preferred) || (h.mask != 0 && __builtin_popcount(h.mask) == 1 && h.preferred)))
+        continue;
+      buf[nl][n++] = h;
+    }
+    off += lens[i];
+    ln[nl++] = n;
+  }
+  if (nl == 0) { /* no providers at all */
+    buf[0][0] = (numa_hint){0, 1, 0, 0};
+    lists[0] = buf[0];
+    ln[0] = 1;
+    nl = 1;
+  }
+  numa_hint best;
+  const int admit = policy_merge(policy, all, lists, ln, nl, reasons, &best);
+  *out_mask = best.mask;
+  *out_preferred = (uint8_t)best.preferred;
+  *out_unsatisfied = (uint8_t)best.unsatisfied;
+  *out_score = best.score;
+  return admit;
+}
+
+/* topologymanager Admit for the pod on the node (manager.go:64-129 with the NodeNUMAResource hint
+ * provider; DeviceShare provides no hints for a pod without device requests).  Returns the status
+ * code, *affinity (0 = nil) on success. */
+static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod, int policy, uint32_t* affinity,
+                      int* reason) {
+  numa_view v;
+  uint32_t all = 0;
+  for (int z = 0; z < nd->n_zone; z++) all |= 1u << nd->zone[z].id;
+  if (numa_view_build(nd, &v) != 0) { /* GetPodTopologyHints error -> reasons -> Unschedulable */
+    *reason = KE_REASON_NUMA_HINT_UNALIGNED;
+    return KE_CODE_UNSCHEDULABLE;
+  }
+  static __thread numa_hint store[KE_NRES * 255];
+  int counts[KE_NRES], present[KE_NRES];
+  numa_generate_hints(c, &v, pod, policy, store, counts, present);
+  /* filterProvidersHints: the NUMA provider's lists in sorted resource-name order (cpu, memory), then
+   * DeviceShare's nil hints -> one preferred any-NUMA hint */
+  static __thread numa_hint filt[KE_NRES + 1][255];
+  numa_hint* lists[KE_NRES + 1];
+  int lens[KE_NRES + 1], nl = 0, reasons = 0;
+  int any_present = present[0] || present[1];
+  for (int r = 0; r < KE_NRES; r++) {
+    if (!present[r]) continue;
+    if (counts[r] == 0) { /* no possible affinity for the resource */
+      if (policy == KE_NUMA_POLICY_SINGLE_NUMA_NODE) { /* filterSingleNumaHints drops the unsatisfied hint */
+        lists[nl] = filt[nl];
+        lens[nl++] = 0;
+        reasons = 1;
+        continue;
+      }
+      filt[nl][0] = (numa_hint){0, 0, 1, 0};
+      lists[nl] = filt[nl];
+      lens[nl++] = 1;
+      reasons = 1;
+      continue;
+    }
+    int n = 0;
+    for (int i = 0; i < counts[r]; i++) {
+      const numa_hint h = store[r * 255 + i];
+      if (policy == KE_NUMA_POLICY_SINGLE_NUMA_NODE && !(h.preferred && __builtin_popcount(h.mask) == 1)) continue;
+      filt[nl][n++] = h;
+    }
+    lists[nl] = filt[nl];
+    lens[nl++] = n;
+  }
+  if (!any_present) { /* the provider returned an empty map: one preferred any-NUMA hint */
+    filt[nl][0] = (numa_hint){0, 1, 0, 0};
+    lists[nl] = filt[nl];
+    lens[nl++] = 1;
+  }
+  filt[nl][0] = (numa_hint){0, 1, 0, 0}; /* DeviceShare: no preference */
+  lists[nl] = filt[nl];
+  lens[nl++] = 1;
+  numa_hint best;
+  const int admit = policy_merge(policy, all, lists, lens, nl, reasons, &best);
+  if (!admit) {
+    *reason = KE_REASON_NUMA_HINT_UNALIGNED;
+    return KE_CODE_UNSCHEDULABLE;
+  }
+  /* allocateResources -> NodeNUMAResource.Allocate -> tryAllocateFromNode with the hint */
+  if (best.mask) {
+    int64_t out[KE_MAX_NUMA][KE_NRES];
+    if (!numa_distribute(&v, best.mask, pod, out)) {
+      *reason = KE_REASON_NUMA_INSUFFICIENT_RESOURCES;
+      return KE_CODE_UNSCHEDULABLE;
+    }
+  }
+  *affinity = best.mask;
+  return KE_CODE_SUCCESS;
+}
+
+/* the pod's NUMA allocation on its affinity (resourceManager.Allocate -> allocateResourcesByHint) */
+static int numa_allocation(const or_node* nd, const ke_pod* pod, uint32_t affinity, numa_view* v,
+                           int64_t out[KE_MAX_NUMA][KE_NRES]) {
+  memset(out, 0, sizeof(int64_t) * KE_MAX_NUMA * KE_NRES);
+  if (numa_view_build(nd, v) != 0) return 0;
+  if (!affinity) return 1;
+  return numa_distribute(v, affinity, pod, out);
+}
 
 /* Plugin.Score  scoring.go:66-120 -> scoreWithAmplifiedCPUs :122-139 */
 int64_t or_numa_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
   const or_node* n = &c->nodes[node];
   if (pod_requests_zero(pod)) return 0; /* state.skip */
+  const int policy = n->node.numa_topology_policy;
+  if (policy != KE_NUMA_POLICY_NONE) {
+    /* the affinity the Filter's Admit stored, the allocation on it, calculateAllocatableAndRequested */
+    uint32_t aff = 0;
+    int reason;
+    if (n->n_zone == 0 || numa_admit(c, n, pod, policy, &aff, &reason) != KE_CODE_SUCCESS) return 0;
+    numa_view v;
+    int64_t out[KE_MAX_NUMA][KE_NRES];
+    if (!numa_allocation(n, pod, aff, &v, out)) return 0;
+    int64_t alloc[KE_NRES] = {0, 0}, req[KE_NRES] = {0, 0};
+    int any = 0;
+    for (int z = 0; z < v.n; z++) {
+      if (out[z][0] == 0 && out[z][1] == 0) continue; /* podAllocation.NUMANodeResources */
+      any = 1;
+      for (int r = 0; r < KE_NRES; r++) {
+        alloc[r] += v.cap_has[z][r] ? v.cap[z][r] : 0;
+        req[r] += v.has_alloc[z] ? v.al[z][r] : 0;
+      }
+    }
+    if (!any) {
+      req[0] = n->node.requested[KE_RES_CPU];
+      req[1] = n->node.requested[KE_RES_MEMORY];
+      alloc[0] = n->node.allocatable[KE_RES_CPU];
+      alloc[1] = n->node.allocatable[KE_RES_MEMORY];
+    }
+    return numa_resource_score(&c->cfg.numa, req, alloc, pod);
+  }
   /* getResourceOptions -> amplifyNUMANodeResources (util.go:78-87) */
   double ratio;
   if (n->node.nrt_cpu_amplification_ratio > -1.5) {
@@ -1011,6 +1460,41 @@ void or_destroy(or_cluster* c) {
   free(c);
 }
 
+int or_node_numa_set(or_cluster* c, int32_t node, int32_t n, const ke_numa_zone* zones) {
+  if (node < 0 || node >= c->n) return KE_ERR_NOT_FOUND;
+  if (n < 0 || n > KE_MAX_NUMA) return KE_ERR_INVALID;
+  for (int32_t i = 0; i < n; i++) { /* same validation as the product (ke_node_numa_set) */
+    if (zones[i].id < 0 || zones[i].id >= KE_MAX_NUMA || (i > 0 && zones[i].id <= zones[i - 1].id)) return KE_ERR_INVALID;
+    if (zones[i].capacity[0] < 0 || zones[i].capacity[1] < 0 || zones[i].cpuset_cpus < 0) return KE_ERR_INVALID;
+    if (zones[i].cpuset_cpus > 0 && !zones[i].has_allocated) return KE_ERR_INVALID;
+  }
+  c->nodes[node].n_zone = n;
+  if (n) memcpy(c->nodes[node].zone, zones, sizeof(ke_numa_zone) * (size_t)n);
+  return KE_OK;
+}
+
+/* NodeNUMAResource Reserve for a non-cpuset pod on a node with a NUMA policy: resourceManager.Update ->
+ * NodeAllocation.addPodAllocation (node_allocation.go:111-156) adds the NUMA allocation. */
+static void or_numa_reserve(or_cluster* c, const ke_pod* pod, int32_t node, int64_t* out16) {
+  or_node* n = &c->nodes[node];
+  if (pod_requests_zero(pod) || n->node.numa_topology_policy == KE_NUMA_POLICY_NONE || n->n_zone == 0) return;
+  uint32_t aff = 0;
+  int reason;
+  if (numa_admit(c, n, pod, n->node.numa_topology_policy, &aff, &reason) != KE_CODE_SUCCESS) return;
+  numa_view v;
+  int64_t out[KE_MAX_NUMA][KE_NRES];
+  if (!numa_allocation(n, pod, aff, &v, out)) return;
+  for (int z = 0; z < v.n; z++) {
+    if (out[z][0] == 0 && out[z][1] == 0) continue;
+    ke_numa_zone* zn = &n->zone[z];
+    if (out16)
+      for (int r = 0; r < KE_NRES; r++) out16[2 * zn->id + r] = out[z][r];
+    if (!zn->has_allocated) zn->allocated[0] = zn->allocated[1] = 0;
+    zn->has_allocated = 1;
+    for (int r = 0; r < KE_NRES; r++) zn->allocated[r] += out[z][r];
+  }
+}
+
 int or_node_devices_set(or_cluster* c, int32_t node, int32_t n, const ke_device* devs) {
   if (node < 0 || node >= c->n) return KE_ERR_NOT_FOUND;
   if (n < 0 || n > KE_DEV_TYPES * KE_MAX_MINORS) return KE_ERR_INVALID;
@@ -1181,10 +1665,19 @@ void or_normalize_scores(int64_t* scores, int32_t n) {
 }
 
 static int check_supported(const or_cluster* c, int32_t n_pods, const ke_pod* pods) {
-  for (int p = 0; p < n_pods; p++)
+  int ds = 0, numa = 0;
+  for (int p = 0; p < n_pods; p++) {
     if (pod_unsupported(&pods[p])) return KE_ERR_UNSUPPORTED;
-  for (int i = 0; i < c->n; i++)
+    ds_pod d;
+    ds_prepare_pod(&pods[p], &d);
+    if (!d.skip && d.status == KE_CODE_SUCCESS) ds = 1;
+  }
+  for (int i = 0; i < c->n; i++) {
     if (node_unsupported(&c->nodes[i].node)) return KE_ERR_UNSUPPORTED;
+    if (c->nodes[i].node.numa_topology_policy != KE_NUMA_POLICY_NONE) numa = 1;
+  }
+  /* DeviceShare's own NUMA hints (deviceshare/topology_hint.go) are not restated */
+  if (ds && numa) return KE_ERR_UNSUPPORTED;
   return KE_OK;
 }
 
@@ -1236,7 +1729,7 @@ int or_eval(const or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now
 }
 
 int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t* chosen, int32_t* score,
-                uint64_t* dev_alloc, int n_threads) {
+                uint64_t* dev_alloc, int64_t* numa_alloc, int n_threads) {
   int rc = check_supported(c, n_pods, pods);
   if (rc) return rc;
   const int64_t N = c->n;
@@ -1245,6 +1738,7 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
 #else
   (void)n_threads;
 #endif
+  if (numa_alloc) memset(numa_alloc, 0, sizeof(int64_t) * 16 * (size_t)n_pods);
   eval_out* o = (eval_out*)malloc(sizeof(eval_out) * (size_t)(N > 0 ? N : 1));
   for (int p = 0; p < n_pods; p++) {
     int16_t bs;
@@ -1256,6 +1750,7 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
       /* Reserve in profile order: LoadAware podAssignCache.assign (load_aware.go:192-195) at `now`,
        * DeviceShare device allocation (plugin.go:426-492); framework assume: NodeInfo.Requested. */
       or_pod_assign(c, b, &pods[p], now);
+      or_numa_reserve(c, &pods[p], b, numa_alloc ? numa_alloc + (int64_t)p * 16 : NULL);
       mask = or_ds_reserve(c, &pods[p], b);
       c->nodes[b].node.requested[KE_RES_CPU] += pods[p].requests[KE_RES_CPU];
       c->nodes[b].node.requested[KE_RES_MEMORY] += pods[p].requests[KE_RES_MEMORY];

@@ -32,6 +32,7 @@ int or_pod_assign(or_cluster* c, int32_t node, const ke_pod* pod, int64_t timest
 int or_pod_unassign(or_cluster* c, int32_t node, int64_t uid);
 int or_pods_assign(or_cluster* c, int32_t n, const int32_t* nodes, const ke_pod* pods, const int64_t* ts);
 int or_node_devices_set(or_cluster* c, int32_t node, int32_t n, const ke_device* devs);
+int or_node_numa_set(or_cluster* c, int32_t node, int32_t n, const ke_numa_zone* zones);
 int or_node_devices_delete(or_cluster* c, int32_t node);
 
 /* Per-plugin entry points for one (pod, node) pair (golden-vector tests). */
@@ -47,6 +48,10 @@ int64_t or_ds_score_device(const or_cluster* c, int32_t type, const int64_t* req
                            const int64_t* total, const uint8_t* total_has, const int64_t* free,
                            const uint8_t* free_has);
 void or_normalize_scores(int64_t* scores, int32_t n);
+/* topologymanager Policy.Merge over raw provider hint lists (see oracle.c). Returns admit. */
+int or_topology_merge(int32_t policy, uint32_t all, int32_t n_lists, const int32_t* kinds, const int32_t* lens,
+                      const uint32_t* masks, const uint8_t* preferred, const int64_t* scores, uint32_t* out_mask,
+                      uint8_t* out_preferred, uint8_t* out_unsatisfied, int64_t* out_score);
 int or_ds_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* reason);
 int64_t or_ds_score(const or_cluster* c, const ke_pod* pod, int32_t node);
 uint64_t or_ds_reserve(or_cluster* c, const ke_pod* pod, int32_t node);
@@ -59,7 +64,7 @@ int or_eval(const or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now
             int32_t* best, int n_threads);
 /* Sequential scheduling, same contract as ke_schedule (mutates the oracle's state). */
 int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int32_t* chosen,
-                int32_t* score, uint64_t* dev_alloc, int n_threads);
+                int32_t* score, uint64_t* dev_alloc, int64_t* numa_alloc, int n_threads);
 
 /* filterNodeUsage's usage percentage, exposed for the threshold-folding property tests:
  * int64(math.Round(float64(used)/float64(total)*100)) (load_aware.go:299). */

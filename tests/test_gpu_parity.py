@@ -342,3 +342,110 @@ def test_deviceshare_cache_delete_and_unhealthy(gpu):
     a, b = ev.eval(pods, synth.T0), o.eval(pods, synth.T0)
     for k in ("status", "reason", "ds", "total", "best"):
         assert np.array_equal(a[k], b[k]), k
+
+
+# ---- NUMA topology policies (non-cpuset pods) ------------------------------------------------------
+def numa_both(n_nodes, seed, zone_counts=(1, 2, 4, 8), batch=64, hint_most=False, most=False):
+    cl = synth.make_cluster(n_nodes, synth.BASE_SEED + seed, amplified_fraction=0.3)
+    zs = synth.make_numa(cl, synth.BASE_SEED + seed + 50, zone_counts=zone_counts)
+    cfg = synth.config(n_nodes, pod_batch=batch)
+    if hint_most:
+        cfg.numa.numa_strategy = abi.STRATEGY_MOST_ALLOCATED
+    if most:
+        cfg.numa.strategy = abi.STRATEGY_MOST_ALLOCATED
+    ev, o = Evaluator(cfg), Oracle(cfg, n_nodes)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        synth.load_numa(h, zs)
+    return ev, o
+
+
+@pytest.mark.parametrize("variant", ["least", "hint-most", "most"])
+def test_numa_policy_eval_matrix_parity(gpu, variant):
+    """Every policy, 1/2/4/8 zones: FilterByNUMANode, hint generation, merge + admit, allocation by the
+    hint and the NUMA-scope score equal the oracle's on every (pod, node)."""
+    ev, o = numa_both(400, 91, hint_most=variant == "hint-most", most=variant == "most")
+    pods = synth.make_pods(48, synth.BASE_SEED + 92)
+    assert_eval_equal(ev.eval(pods, synth.T0), o.eval(pods, synth.T0))
+
+
+def test_numa_policy_schedule_parity(gpu):
+    """Sequential placements with NUMA Reserve: batches re-evaluate nodes whose zones earlier pods of
+    the batch allocated; per-pod zone allocations equal the oracle's."""
+    ev, o = numa_both(400, 93, zone_counts=(1, 2, 4))
+    pods = synth.make_pods(320, synth.BASE_SEED + 94)
+    c1, s1 = ev.schedule(pods, synth.T0)
+    c0, s0 = o.schedule(pods, synth.T0)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5]
+    assert np.array_equal(s1, s0)
+    assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
+    assert np.any(ev.last_numa_allocations != 0)
+    more = synth.make_pods(32, synth.BASE_SEED + 95)
+    assert_eval_equal(ev.eval(more, synth.T0), o.eval(more, synth.T0))
+
+
+def test_numa_policy_sharded_loopback(gpu):
+    ev, o = numa_both(1100, 96, zone_counts=(2, 4))
+    pods = synth.make_pods(160, synth.BASE_SEED + 97)
+    ev.shard_init(0, 3, None)
+    c1, s1 = ev.schedule(pods, synth.T0)
+    c0, s0 = o.schedule(pods, synth.T0)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
+
+
+def test_numa_policy_edge_cases(gpu):
+    """Hand-built zones: no zones, a single zone (SingleNUMANode -> nil affinity), zones without a
+    memory key, exhausted zones, amplified cpu with NRT ratios, amplification errors; pods asking for
+    cpu only, memory only, both, or nothing NUMA-relevant."""
+    Z = model.make_zones
+    layouts = [
+        None,
+        Z([{"id": 0, "cpu": "16", "memory": "64Gi"}]),
+        Z([{"id": 0, "cpu": "8", "memory": "32Gi"}, {"id": 1, "cpu": "8", "memory": "32Gi"}]),
+        Z([{"id": 0, "cpu": "8", "memory": "32Gi", "allocated": {"cpu": "8", "memory": "1Gi"}},
+           {"id": 1, "cpu": "8", "memory": "32Gi", "allocated": {"cpu": "1", "memory": "32Gi"}}]),
+        Z([{"id": 0, "cpu": "4"}, {"id": 1, "cpu": "4", "memory": "16Gi"}, {"id": 3, "cpu": "4", "memory": "16Gi"}]),
+        Z([{"id": k, "cpu": "2", "memory": "8Gi", "allocated": {"cpu": str(k % 3), "memory": f"{k}Gi"}}
+           for k in range(8)]),
+        Z([{"id": 2, "cpu": "6", "memory": "6Gi", "allocated": {"cpu": "2"}, "cpuset_cpus": 1},
+           {"id": 5, "cpu": "6", "memory": "6Gi"}]),
+    ]
+    nodes, zones = [], []
+    for pol in range(4):
+        for li, lay in enumerate(layouts):
+            for amp in ("none", "annot", "nrt", "error"):
+                n = model.make_node(allocatable={"cpu": "16", "memory": "64Gi"}, requested={"cpu": "2"},
+                                    amplification_ratio=1.5 if amp == "annot" else None,
+                                    nrt_amplification_ratio=1.5 if amp == "nrt" else None,
+                                    amplification_error=amp == "error",
+                                    cpuset_allocated_cpus=1 if li == 6 and amp != "none" else 0)
+                n.numa_topology_policy = pol
+                nodes.append(n)
+                zones.append(lay)
+    cfg = abi.default_config(len(nodes))
+    cfg.numa.weights[:] = [1, 1]
+    ev, o = Evaluator(cfg), Oracle(cfg, len(nodes))
+    for h in (ev, o):
+        for i, (n, z) in enumerate(zip(nodes, zones)):
+            h.upsert_node(i, n)
+            if z is not None:
+                h.set_numa(i, z)
+    reqs = [{"cpu": "1"}, {"cpu": "3"}, {"cpu": "9"}, {"cpu": "17"}, {"memory": "8Gi"}, {"memory": "40Gi"},
+            {"cpu": "2", "memory": "20Gi"}, {"cpu": "7", "memory": "2Gi"}, {"cpu": "12", "memory": "48Gi"},
+            {}, {"kubernetes.io/batch-cpu": "1000"}]
+    pods = [model.make_pod(name=f"p{i}", requests=r) for i, r in enumerate(reqs)]
+    a, b = ev.eval(pods, cases.NOW), o.eval(pods, cases.NOW)
+    assert_eval_equal(a, b)
+    for code in (abi.CODE_UNSCHEDULABLE, abi.CODE_UNSCHEDULABLE_AND_UNRESOLVABLE):
+        assert np.any(a["status"] == code)
+    for reason in (abi.REASON_NUMA_MISSING_RESOURCES, abi.REASON_NUMA_HINT_UNALIGNED,
+                   abi.REASON_NUMA_INSUFFICIENT_RESOURCES):
+        assert np.any(a["reason"] == reason), reason
+    # and sequentially: the zones fill up as the queue is placed
+    queue = [model.make_pod(name=f"q{i}", requests=r) for i, r in enumerate(reqs * 4)]
+    c1, s1 = ev.schedule(queue, cases.NOW)
+    c0, s0 = o.schedule(queue, cases.NOW)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
+    assert_eval_equal(ev.eval(pods, cases.NOW), o.eval(pods, cases.NOW))

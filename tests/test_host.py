@@ -102,10 +102,31 @@ def test_unsupported_inputs_are_rejected():
         ev.eval([lsr], cases.NOW)
     assert e.value.code == abi.ERR_UNSUPPORTED
     n = model.make_node(allocatable={"cpu": "8"})
-    n.numa_topology_policy = 1
+    n.cpu_bind_policy = 1  # cpuset binding is not modelled
     with pytest.raises(KoordEvalError) as e:
         ev.upsert_node(1, n)
     assert e.value.code == abi.ERR_UNSUPPORTED
+    n.cpu_bind_policy = 0
+    n.numa_topology_policy = 7
+    with pytest.raises(KoordEvalError) as e:
+        ev.upsert_node(1, n)
+    assert e.value.code == abi.ERR_INVALID
+    # a NUMA-policy node is accepted; DeviceShare pods cannot meet it (DeviceShare NUMA hints)
+    n.numa_topology_policy = abi.NUMA_POLICY_RESTRICTED
+    ev.upsert_node(1, n)
+    gpu_pod = model.make_pod(requests={"cpu": "1", "koordinator.sh/gpu": "100"})
+    with pytest.raises(KoordEvalError) as e:
+        ev.eval([gpu_pod], cases.NOW)
+    assert e.value.code == abi.ERR_UNSUPPORTED
+    # zones: ids ascending, cpuset CPUs only inside an allocation entry
+    z = model.make_zones([{"id": 1, "cpu": "4"}, {"id": 0, "cpu": "4"}])
+    with pytest.raises(KoordEvalError) as e:
+        ev.set_numa(1, z)
+    assert e.value.code == abi.ERR_INVALID
+    z = model.make_zones([{"id": 0, "cpu": "4", "cpuset_cpus": 2}])
+    with pytest.raises(KoordEvalError) as e:
+        ev.set_numa(1, z)
+    assert e.value.code == abi.ERR_INVALID
     bad = abi.default_config(4)
     bad.abi_version = 99
     with pytest.raises(KoordEvalError):

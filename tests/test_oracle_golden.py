@@ -85,3 +85,39 @@ def test_deviceshare(case):
     else:  # Score (TestScore calls Score directly; a Prepare error shows up as Filter's status)
         assert (code, reason) == (want["code"], want["reason"]), case["source"]
         assert o.ds_score(pod, 0) == want["score"], case["source"]
+
+
+# ---- NUMA topology policies ----------------------------------------------------------------------
+NUMA_POLICY = cases.load("numa_policy.json")
+POLICY_ID = {"BestEffort": 1, "Restricted": 2, "SingleNUMANode": 3}
+
+
+def _mask(bits):
+    return 0 if bits is None else sum(1 << b for b in bits)
+
+
+def _lists(providers):
+    """filterProvidersHints input: the providers' maps in sorted resource order."""
+    out = []
+    for p in providers:
+        if p is None or len(p) == 0:
+            out.append((1, []))
+            continue
+        for res in sorted(p):
+            hints = p[res]
+            if hints is None:
+                out.append((1, []))
+            elif len(hints) == 0:
+                out.append((2, []))
+            else:
+                out.append((0, [(_mask(b), pref, 0) for b, pref in hints]))
+    return out
+
+
+@pytest.mark.parametrize("case", NUMA_POLICY, ids=[c["name"] for c in NUMA_POLICY])
+def test_numa_policy_merge(case):
+    from oracle.binding import topology_merge
+    admit, mask, pref, _, _ = topology_merge(POLICY_ID[case["policy"]], _mask(case["numa_nodes"]),
+                                             _lists(case["providers"]))
+    want = case["want"]
+    assert (mask, pref, admit) == (_mask(want["bits"]), want["preferred"], want["admit"]), case["source"]
