@@ -162,6 +162,9 @@ typedef struct ke_numa_args {
 #define KE_NUMA_POLICY_RESTRICTED 2
 #define KE_NUMA_POLICY_SINGLE_NUMA_NODE 3
 #define KE_MAX_NUMA 8
+#define KE_NUMA_ALLOC_ENTRY 1u  /* ke_numa_zone.has_allocated bits */
+#define KE_NUMA_ALLOC_CPU 2u
+#define KE_NUMA_ALLOC_MEMORY 4u
 #define KE_REASON_NUMA_POLICY_CONFLICT 19 /* "node(s) NUMA Topology policy cannot match" (ErrNotMatchNUMATopology) */
 #define KE_REASON_NUMA_MISSING_RESOURCES 20 /* "node(s) missing NUMA resources" (topology_hint.go:35-37) */
 #define KE_REASON_NUMA_HINT_UNALIGNED 21 /* topologymanager Admit: "Unaligned NUMA Hint ..." / "Unsatisfied NUMA ..." */
@@ -172,7 +175,9 @@ typedef struct ke_numa_args {
 typedef struct ke_numa_zone {
   int32_t id;                  /* NUMA node id, 0 .. KE_MAX_NUMA-1; zones ascending by id */
   uint8_t has[KE_NRES];        /* cpu / memory key present in the zone's resources */
-  uint8_t has_allocated;       /* allocatedResources has an entry for the zone */
+  uint8_t has_allocated;       /* the resource manager's allocatedResources entry of the zone:
+                                  KE_NUMA_ALLOC_ENTRY | KE_NUMA_ALLOC_CPU | KE_NUMA_ALLOC_MEMORY (the keys
+                                  its ResourceList holds; 0 = no entry) */
   uint8_t pad;
   int64_t capacity[KE_NRES];   /* cpu milli, memory bytes (before amplification) */
   int64_t allocated[KE_NRES];  /* Σ NUMANodeResources of the pods allocated on the zone */

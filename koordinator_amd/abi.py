@@ -31,6 +31,7 @@ REASON_NUMA_MISSING_RESOURCES = 20
 REASON_NUMA_HINT_UNALIGNED = 21
 REASON_NUMA_INSUFFICIENT_RESOURCES = 22
 NUMA_POLICY_NONE, NUMA_POLICY_BEST_EFFORT, NUMA_POLICY_RESTRICTED, NUMA_POLICY_SINGLE_NUMA_NODE = 0, 1, 2, 3
+NUMA_ALLOC_ENTRY, NUMA_ALLOC_CPU, NUMA_ALLOC_MEMORY = 1, 2, 4  # ke_numa_zone.has_allocated bits
 MAX_NUMA = 8
 REASON_DS_INVALID_REQUEST = 32
 REASON_DS_INSUFFICIENT_GPU = 33

@@ -551,6 +551,10 @@ void derive_row(const ke_config& cfg, const NodeState& ns, int64_t now, Row* row
   if (ns.has_dev_cache) flags |= NF_DS_CACHE;
   flags |= (uint32_t)n.numa_topology_policy * NF_NUMA_POLICY0;
   if (n.nrt_cpu_amplification_ratio <= -1.5 && n.amplification_error) flags |= NF_NUMA_OPT_ERR;
+  {  // TopologyOptions.AmplificationRatios[cpu]: the NRT's ratios, else the node annotation's
+    const double r = n.nrt_cpu_amplification_ratio > -1.5 ? n.nrt_cpu_amplification_ratio : n.cpu_amplification_ratio;
+    if (r > 1.0) flags |= NF_NUMA_AL_AMP;
+  }
   row->flags = flags;
 }
 
@@ -561,8 +565,10 @@ int validate_zones(int32_t n, const ke_numa_zone* zones) {
     if (i > 0 && zones[i].id <= zones[i - 1].id) return fail(KE_ERR_INVALID, "NUMA zones must ascend by id");
     for (int r = 0; r < KE_NRES; r++)
       if (zones[i].capacity[r] < 0 || zones[i].cpuset_cpus < 0) return fail(KE_ERR_INVALID, "negative NUMA quantity");
-    if (zones[i].cpuset_cpus > 0 && !zones[i].has_allocated)
+    if (zones[i].cpuset_cpus > 0 && !(zones[i].has_allocated & KE_NUMA_ALLOC_ENTRY))
       return fail(KE_ERR_INVALID, "cpuset CPUs allocated in a zone without an allocation entry");
+    if (zones[i].has_allocated > 7 || (zones[i].has_allocated && !(zones[i].has_allocated & KE_NUMA_ALLOC_ENTRY)))
+      return fail(KE_ERR_INVALID, "NUMA allocation keys without an allocation entry");
   }
   return KE_OK;
 }
@@ -570,7 +576,7 @@ int validate_zones(int32_t n, const ke_numa_zone* zones) {
 // getResourceOptions -> amplifyNUMANodeResources (util.go:78-98): the NUMA zones' cpu is amplified with
 // the node annotation's ratio unless the NRT reported ratios; getAvailableNUMANodeResources
 // (node_allocation.go:221-243) adjusts the allocated cpu of amplified cpusets.
-void derive_numa_row(const NodeState& ns, int64_t* f, uint32_t* mask) {
+void derive_numa_row(const NodeState& ns, int64_t* f, uint64_t* mask) {
   for (int i = 0; i < NUM_NUMA_FIELDS; i++) f[i] = 0;
   *mask = 0;
   const ke_node& n = ns.node;
@@ -584,22 +590,25 @@ void derive_numa_row(const NodeState& ns, int64_t* f, uint32_t* mask) {
   }
   for (const ke_numa_zone& z : ns.zones) {
     const int id = z.id;
-    *mask |= 1u << id;
+    *mask |= 1ull << id;
     for (int r = 0; r < KE_NRES; r++) {
       if (z.has[r]) {
-        *mask |= 1u << (8 * (r + 1) + id);
+        *mask |= 1ull << (NUMA_M_CAP + 8 * r + id);
         int64_t c = z.capacity[r];
         if (r == KE_RES_CPU && amplify_caps && ratio > 1.0 && c != 0) c = amplify(c, ratio);
         f[NUMA_CAP + 2 * id + r] = c;
       }
     }
-    if (z.has_allocated) {
-      *mask |= 1u << (24 + id);
-      f[NUMA_AL + 2 * id + 0] = z.allocated[0];
-      f[NUMA_AL + 2 * id + 1] = z.allocated[1];
-      if (ratio > 1.0) {
+    if (z.has_allocated & KE_NUMA_ALLOC_ENTRY) {
+      for (int r = 0; r < KE_NRES; r++)
+        if (z.has_allocated & (r == KE_RES_CPU ? KE_NUMA_ALLOC_CPU : KE_NUMA_ALLOC_MEMORY)) {
+          *mask |= 1ull << (NUMA_M_AL + 8 * r + id);
+          f[NUMA_AL + 2 * id + r] = z.allocated[r];
+        }
+      if (ratio > 1.0) {  // the cpu key is (re)written even when the entry had none
         const int64_t cs = (int64_t)z.cpuset_cpus * 1000;
-        f[NUMA_AL + 2 * id] = z.allocated[0] - cs + amplify(cs, ratio);
+        f[NUMA_AL + 2 * id] = f[NUMA_AL + 2 * id] - cs + amplify(cs, ratio);
+        *mask |= 1ull << (NUMA_M_AL + id);
       }
     }
   }
@@ -607,12 +616,15 @@ void derive_numa_row(const NodeState& ns, int64_t* f, uint32_t* mask) {
 
 void host_numa_reserve(NodeState& ns, const int64_t* delta) {
   for (ke_numa_zone& z : ns.zones) {
-    const int64_t d0 = delta[2 * z.id], d1 = delta[2 * z.id + 1];
-    if (d0 == 0 && d1 == 0) continue;
-    if (!z.has_allocated) z.allocated[0] = z.allocated[1] = 0;
-    z.has_allocated = 1;
-    z.allocated[0] += d0;
-    z.allocated[1] += d1;
+    const int64_t d[KE_NRES] = {delta[2 * z.id], delta[2 * z.id + 1]};
+    if (d[0] == 0 && d[1] == 0) continue;
+    for (int r = 0; r < KE_NRES; r++) {  // quotav1.Add(entry, allocation): keys with a non-zero amount
+      const uint8_t key = r == KE_RES_CPU ? KE_NUMA_ALLOC_CPU : KE_NUMA_ALLOC_MEMORY;
+      if (!(z.has_allocated & key)) z.allocated[r] = 0;
+      if (d[r] != 0) z.has_allocated |= key;
+      z.allocated[r] += d[r];
+    }
+    z.has_allocated |= KE_NUMA_ALLOC_ENTRY;
   }
 }
 

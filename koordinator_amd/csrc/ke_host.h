@@ -95,7 +95,7 @@ void host_ds_reserve(const ke_config& cfg, NodeState& ns, const DevPod& dp, uint
 // NUMA topology
 int validate_zones(int32_t n, const ke_numa_zone* zones);
 // the NUMA SoA row of a node: NUM_NUMA_FIELDS int64 + the uint32 mask
-void derive_numa_row(const NodeState& ns, int64_t* f, uint32_t* mask);
+void derive_numa_row(const NodeState& ns, int64_t* f, uint64_t* mask);
 // host mirror of the NUMA allocation the device Reserve made: delta[z][r] per zone id
 void host_numa_reserve(NodeState& ns, const int64_t* delta /*[KE_MAX_NUMA*KE_NRES]*/);
 

@@ -50,7 +50,7 @@ struct SoA {
   int64_t* ds;      // DeviceShare: NUM_DS_FIELDS arrays of `stride` int64 (nullptr until a device cache appears)
   uint64_t* dsm;    // DeviceShare: NUM_DS_MASKS arrays of `stride` uint64
   int64_t* nf;      // NUMA topology: NUM_NUMA_FIELDS arrays of `stride` int64 (nullptr until a NUMA node appears)
-  uint32_t* nm;     // NUMA topology: `stride` uint32 zone / key / allocation masks
+  uint64_t* nm;     // NUMA topology: `stride` uint64 zone / key masks (ke_types.h NUMA_M_*)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -346,7 +346,7 @@ __constant__ uint8_t NUMA_ORDER[255] = {
 __constant__ uint8_t NUMA_OFF[10] = {0, 0, 8, 36, 92, 162, 218, 246, 254, 255};  // first entry of each size
 
 struct NumaNode {
-  uint32_t zm, ah, ch[2];  // zones present, allocation entries, cpu / memory capacity keys (bit = NUMA id)
+  uint32_t zm, ch[2], ak[2];  // zones present, capacity keys, allocated keys per resource (bit = NUMA id)
   int64_t av[2][8];        // totalAvailable[r][id] (0 for absent zones / keys)
   uint32_t perm[2][8];     // perm[r][nb-1]: slot order of an nb-zone hint after the distribute sort
 };
@@ -368,7 +368,7 @@ __device__ __forceinline__ int64_t numa_cap(const SoA& s, int64_t i, int z, int 
 }
 __device__ __forceinline__ int64_t numa_al(const SoA& s, int64_t i, const NumaNode& v, int z, int r) {
   const int64_t a = s.nf[(NUMA_AL + 2 * z + r) * s.stride + i];  // SubtractWithNonNegativeResult(allocated, {})
-  return ((v.ah >> z) & 1u) && a > 0 ? a : 0;
+  return ((v.ak[r] >> z) & 1u) && a > 0 ? a : 0;
 }
 
 // getAvailableNUMANodeResources (node_allocation.go:221-243) and the sort order of
@@ -376,11 +376,13 @@ __device__ __forceinline__ int64_t numa_al(const SoA& s, int64_t i, const NumaNo
 // POSITION (a reference quirk), so the permutation of an nb-zone hint depends only on av[r][0..nb-1]
 // and is the state after insertion passes 1..nb-1 — computed once for all hints.
 __device__ __forceinline__ void numa_load(const SoA& s, int64_t i, NumaNode& v) {
-  const uint32_t m = s.nm[i];
-  v.zm = m & 0xFFu;
-  v.ch[0] = (m >> 8) & 0xFFu;
-  v.ch[1] = (m >> 16) & 0xFFu;
-  v.ah = m >> 24;
+  const uint64_t m = s.nm[i];
+  v.zm = (uint32_t)m & 0xFFu;
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    v.ch[r] = (uint32_t)(m >> (NUMA_M_CAP + 8 * r)) & 0xFFu;
+    v.ak[r] = (uint32_t)(m >> (NUMA_M_AL + 8 * r)) & 0xFFu;
+  }
 #pragma unroll
   for (int z = 0; z < 8; z++)
 #pragma unroll
@@ -434,7 +436,7 @@ __device__ __forceinline__ bool numa_distribute(const NumaNode& v, uint32_t m, c
 #pragma unroll
   for (int r = 0; r < 2; r++) {
     if (!OUT && !ok) break;
-    if (((v.ch[r] | v.ah) & v.zm) == 0 || p.req[r] == 0) continue;  // resourceNamesByNUMA x requests
+    if (((v.ch[r] | v.ak[r]) & v.zm) == 0 || p.req[r] == 0) continue;  // resourceNamesByNUMA x requests
     const uint32_t perm = pick8u(v.perm[r], nb - 1);
     int64_t q = p.req[r];
     for (int t = 0; t < nb; t++) {
@@ -444,7 +446,7 @@ __device__ __forceinline__ bool numa_distribute(const NumaNode& v, uint32_t m, c
       const int64_t got = a > split ? split : a;   // allocateRes
       q -= got;
       if (OUT && got != 0) {
-        *got_mask |= 1u << z;
+        got_mask[r] |= 1u << z;
 #pragma unroll
         for (int zz = 0; zz < 8; zz++) out[r][zz] += zz == z ? got : 0;
       }
@@ -582,7 +584,7 @@ __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t
     if (v.ch[r] & all)
 #pragma unroll
       for (int z = 0; z < 8; z++)
-        if (((all >> z) & 1u) && (!(((v.ch[r] | v.ah) >> z) & 1u) || v.av[r][z] == 0)) l |= 1u << z;
+        if (((all >> z) & 1u) && (!(((v.ch[r] | v.ak[r]) >> z) & 1u) || v.av[r][z] == 0)) l |= 1u << z;
     lack[r] = l;
   }
   const int R = (int)present[0] + (int)present[1];
@@ -648,8 +650,9 @@ __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t
 __device__ __forceinline__ int32_t numa_policy_score(const SoA& s, int64_t i, const NumaNode& v, uint32_t aff,
                                                      const DevPod& p, const KArgs& k, const NodeRegs& n) {
   int64_t out[2][8] = {{0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0, 0}};
-  uint32_t zs = 0;
-  if (aff) numa_distribute<true>(v, aff, p, &zs, out);
+  uint32_t got[2] = {0, 0};
+  if (aff) numa_distribute<true>(v, aff, p, got, out);
+  const uint32_t zs = got[0] | got[1];
   int64_t req[2] = {n.nreq[0], n.nreq[1]}, alloc[2] = {n.nalloc[0], n.nalloc[1]};
   if (zs) {
     req[0] = req[1] = alloc[0] = alloc[1] = 0;
@@ -666,20 +669,27 @@ __device__ __forceinline__ int32_t numa_policy_score(const SoA& s, int64_t i, co
 }
 
 // NodeNUMAResource Reserve of a non-cpuset pod under a NUMA policy: NodeAllocation.addPodAllocation
-// (node_allocation.go:111-156) adds the allocation on the affinity to the zones.  out16[2*id + r].
-__device__ __forceinline__ void numa_reserve(const SoA& s, int64_t i, const NumaNode& v, uint32_t aff,
+// (node_allocation.go:111-156) adds the allocation on the affinity to the zones (quotav1.Add: the
+// entry gains the keys allocated; with a ratio > 1 every entry carries cpu).  out16[2*id + r].
+__device__ __forceinline__ void numa_reserve(const SoA& s, int64_t i, uint32_t nf, const NumaNode& v, uint32_t aff,
                                              const DevPod& p, int64_t* out16) {
   int64_t out[2][8] = {{0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0, 0}};
-  uint32_t zs = 0;
-  if (aff) numa_distribute<true>(v, aff, p, &zs, out);
+  uint32_t got[2] = {0, 0};
+  if (aff) numa_distribute<true>(v, aff, p, got, out);
 #pragma unroll
   for (int z = 0; z < 8; z++)
 #pragma unroll
     for (int r = 0; r < 2; r++) {
       out16[2 * z + r] = out[r][z];
-      if ((zs >> z) & 1u) s.nf[(NUMA_AL + 2 * z + r) * s.stride + i] += out[r][z];
+      if ((got[r] >> z) & 1u) {
+        int64_t* f = s.nf + (NUMA_AL + 2 * z + r) * s.stride + i;
+        *f = (((v.ak[r] >> z) & 1u) ? *f : 0) + out[r][z];
+      }
     }
-  if (zs) s.nm[i] = s.nm[i] | (zs << 24);
+  uint32_t ak0 = v.ak[0] | got[0];
+  if (nf & NF_NUMA_AL_AMP) ak0 |= got[1];
+  const uint32_t ak1 = v.ak[1] | got[1];
+  s.nm[i] = s.nm[i] | ((uint64_t)ak0 << NUMA_M_AL) | ((uint64_t)ak1 << (NUMA_M_AL + 8));
 }
 
 // `s`/`i` locate the node's DeviceShare state (read only for pods with PF_DS, and only when DS: the
@@ -1468,7 +1478,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
             NumaNode nv;
             numa_load(s, my_node, nv);
             const NumaPick pk = numa_admit(s, my_node, mine.flags, nv, pod, k);
-            numa_reserve(s, my_node, nv, pk.status == KE_CODE_SUCCESS ? pk.aff : 0u, pod, out16);
+            numa_reserve(s, my_node, mine.flags, nv, pk.status == KE_CODE_SUCCESS ? pk.aff : 0u, pod, out16);
           } else {
 #pragma unroll
             for (int t = 0; t < 16; t++) out16[t] = 0;
@@ -1708,16 +1718,16 @@ __global__ void k_scatter_numa(SoA s, const int64_t* __restrict__ rows, const in
   const int64_t i = idx[t];
   const int64_t* r = rows + (int64_t)t * NUMA_ROW_WORDS;
   for (int f = 0; f < NUM_NUMA_FIELDS; f++) s.nf[f * s.stride + i] = r[f];
-  s.nm[i] = (uint32_t)r[NUM_NUMA_FIELDS];
+  s.nm[i] = (uint64_t)r[NUM_NUMA_FIELDS];
 }
 
 static int ensure_numa(Context* ctx) {
   DeviceState* d = ctx->dev;
   if (d->numa_alloc || !ctx->numa_enabled) return KE_OK;
   HIP_OK(hipMalloc(&d->soa.nf, sizeof(int64_t) * NUM_NUMA_FIELDS * d->capacity));
-  HIP_OK(hipMalloc(&d->soa.nm, sizeof(uint32_t) * d->capacity));
+  HIP_OK(hipMalloc(&d->soa.nm, sizeof(uint64_t) * d->capacity));
   HIP_OK(hipMemsetAsync(d->soa.nf, 0, sizeof(int64_t) * NUM_NUMA_FIELDS * d->capacity, d->stream));
-  HIP_OK(hipMemsetAsync(d->soa.nm, 0, sizeof(uint32_t) * d->capacity, d->stream));
+  HIP_OK(hipMemsetAsync(d->soa.nm, 0, sizeof(uint64_t) * d->capacity, d->stream));
   d->numa_alloc = true;
   for (int32_t i = 0; i < ctx->n_nodes; i++)  // rows derived before the NUMA SoA existed
     if (!ctx->nodes[i].zones.empty()) ctx->nodes[i].dirty = true;
@@ -1752,7 +1762,7 @@ int device_refresh(Context* ctx, int64_t now) {
     if (ns.dirty && d->numa_alloc) {
       const size_t o = nrows.size();
       nrows.resize(o + NUMA_ROW_WORDS);
-      uint32_t mask;
+      uint64_t mask;
       derive_numa_row(ns, &nrows[o], &mask);
       nrows[o + NUM_NUMA_FIELDS] = (int64_t)mask;
       nidx.push_back(i);

@@ -53,6 +53,7 @@ enum NodeFlag : uint32_t {
   NF_DS_CACHE = 1u << 15,         // nodeDeviceCache has an entry for the node (DeviceShare runs)
   NF_NUMA_POLICY0 = 1u << 16,     // 2 bits: the node's NUMA topology policy (KE_NUMA_POLICY_*)
   NF_NUMA_OPT_ERR = 1u << 18,     // getResourceOptions fails (amplification annotation unparsable)
+  NF_NUMA_AL_AMP = 1u << 19,      // the cpu amplification ratio in force is > 1: every allocation entry has a cpu key
 };
 KE_HD inline int nf_numa_policy(uint32_t f) { return (int)((f >> 16) & 3u); }
 
@@ -61,7 +62,10 @@ KE_HD inline int nf_numa_policy(uint32_t f) { return (int)((f >> 16) & 3u); }
 //   NUMA_CAP + 2z + r: TopologyOptions.NUMANodeResources after amplifyNUMANodeResources
 //   NUMA_AL  + 2z + r: the zone's allocated resources, cpu adjusted for amplified cpusets
 //                      (getAvailableNUMANodeResources before its non-negative clamp)
-// uint32 mask: zone present (bits 0-7), cpu key (8-15), memory key (16-23), allocation entry (24-31)
+// uint64 mask (bit = NUMA id): zone present (bits 0-7), capacity cpu / memory key (NUMA_M_CAP + 8r),
+// allocated cpu / memory key (NUMA_M_AL + 8r; cpu set for every entry when a ratio > 1 adjusts it)
+constexpr int NUMA_M_CAP = 8;
+constexpr int NUMA_M_AL = 24;
 constexpr int NUMA_CAP = 0;
 constexpr int NUMA_AL = 16;
 constexpr int NUM_NUMA_FIELDS = 32;

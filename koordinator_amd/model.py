@@ -346,7 +346,8 @@ def make_devices(devices):
 def make_zones(zones):
     """NodeResourceTopology zones + the resource manager's allocation: [dict(id, cpu=quantity | None,
     memory=quantity | None, allocated={'cpu':..., 'memory':...} | None, cpuset_cpus=0)] ->
-    np.ndarray(NUMA_ZONE_DTYPE).  A resource left out is absent from the zone's ResourceList."""
+    np.ndarray(NUMA_ZONE_DTYPE).  A resource left out is absent from the zone's ResourceList; the
+    allocation entry holds exactly the keys given in `allocated` ({} = an entry without keys)."""
     arr = np.zeros(len(zones), dtype=abi.NUMA_ZONE_DTYPE)
     for i, z in enumerate(zones):
         arr[i]["id"] = int(z["id"])
@@ -356,7 +357,8 @@ def make_zones(zones):
                 arr[i]["capacity"][r] = resource_value(name, z[name])
         al = z.get("allocated")
         if al is not None:
-            arr[i]["has_allocated"] = 1
+            arr[i]["has_allocated"] = (abi.NUMA_ALLOC_ENTRY | (abi.NUMA_ALLOC_CPU if "cpu" in al else 0)
+                                       | (abi.NUMA_ALLOC_MEMORY if "memory" in al else 0))
             arr[i]["allocated"][:] = [milli_value(al.get("cpu", 0)), value(al.get("memory", 0))]
         arr[i]["cpuset_cpus"] = int(z.get("cpuset_cpus", 0))
     return arr

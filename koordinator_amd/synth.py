@@ -312,10 +312,16 @@ def make_numa(cl, seed, zone_counts=(8,), policy_weights=(0.1, 0.3, 0.3, 0.3), n
                 z[k]["has"][1] = 1
                 z[k]["capacity"][1] = mem // nz // MI * MI
             if rng.random() < allocated_fraction:
-                z[k]["has_allocated"] = 1
                 f = rng.choice([0.0, 0.25, 0.5, 0.75, 0.9, 1.0])
                 z[k]["allocated"][0] = int(z[k]["capacity"][0] * f) // 1000 * 1000
                 z[k]["allocated"][1] = int(z[k]["capacity"][1] * rng.choice([0.0, 0.3, 0.6, 0.95])) // MI * MI
+                # the entry's keys: those allocated (zero amounts keep their key after a release)
+                keys = abi.NUMA_ALLOC_ENTRY
+                if z[k]["allocated"][0] or rng.random() < 0.5:
+                    keys |= abi.NUMA_ALLOC_CPU
+                if z[k]["allocated"][1] or rng.random() < 0.5:
+                    keys |= abi.NUMA_ALLOC_MEMORY
+                z[k]["has_allocated"] = keys
                 if amplified and rng.random() < 0.25:
                     z[k]["cpuset_cpus"] = int(rng.integers(1, 4))
         out.append(z)

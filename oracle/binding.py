@@ -55,6 +55,8 @@ def load():
         "or_normalize_scores": (None, [V, i32]),
         "or_topology_merge": (C.c_int, [i32, C.c_uint32, i32, V, V, V, V, V, V, V, V, V]),
         "or_node_numa_set": (C.c_int, [V, i32, i32, V]),
+        "or_numa_distribute": (C.c_int, [V, i32, V, C.c_uint32, V]),
+        "or_numa_hints": (C.c_int, [V, i32, V, i32, V, V, V, V, V]),
         "or_ds_filter": (C.c_int, [V, C.POINTER(abi.Pod), i32, C.POINTER(C.c_int)]),
         "or_ds_score": (i64, [V, C.POINTER(abi.Pod), i32]),
         "or_ds_reserve": (C.c_uint64, [V, C.POINTER(abi.Pod), i32]),
@@ -146,6 +148,26 @@ class Oracle:
 
     def delete_devices(self, i):
         assert self.lib.or_node_devices_delete(self.h, i) == 0
+
+    def numa_distribute(self, i, pod, mask):
+        """(ok, out[16]) of tryBestToDistributeEvenly on NUMA ids `mask` (None if options fail)."""
+        out = np.zeros(16, np.int64)
+        rc = self.lib.or_numa_distribute(self.h, i, C.byref(pod), mask, abi.ptr(out))
+        return None if rc < 0 else (bool(rc), out)
+
+    def numa_hints(self, i, pod, policy):
+        """{resource index: [(mask, preferred, score)]} for the resources that have a hint list."""
+        masks = np.zeros(2 * 255, np.uint32)
+        pref = np.zeros(2 * 255, np.uint8)
+        scores = np.zeros(2 * 255, np.int64)
+        counts = np.zeros(2, np.int32)
+        present = np.zeros(2, np.int32)
+        rc = self.lib.or_numa_hints(self.h, i, C.byref(pod), policy, abi.ptr(masks), abi.ptr(pref), abi.ptr(scores),
+                                    abi.ptr(counts), abi.ptr(present))
+        if rc < 0:
+            return None
+        return {r: [(int(masks[r * 255 + k]), bool(pref[r * 255 + k]), int(scores[r * 255 + k]))
+                    for k in range(counts[r])] for r in range(2) if present[r]}
 
     # per-plugin entry points (golden vectors)
     def la_filter(self, pod, node, now_ns):

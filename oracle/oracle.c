@@ -589,21 +589,27 @@ static int numa_view_build(const or_node* nd, numa_view* v) {
     }
     if (amplify_caps && ratio > 1.0 && v->cap_has[z][KE_RES_CPU] && v->cap[z][KE_RES_CPU] != 0)
       v->cap[z][KE_RES_CPU] = amplify(v->cap[z][KE_RES_CPU], ratio);
-    v->has_alloc[z] = zn->has_allocated;
-    if (zn->has_allocated) {
-      int64_t al[KE_NRES] = {zn->allocated[0], zn->allocated[1]};
-      if (ratio > 1.0) {
+    v->has_alloc[z] = (zn->has_allocated & KE_NUMA_ALLOC_ENTRY) != 0;
+    if (v->has_alloc[z]) {
+      int64_t al[KE_NRES];
+      uint8_t has[KE_NRES];
+      for (int r = 0; r < KE_NRES; r++) {
+        has[r] = (zn->has_allocated & (r == KE_RES_CPU ? KE_NUMA_ALLOC_CPU : KE_NUMA_ALLOC_MEMORY)) != 0;
+        al[r] = has[r] ? zn->allocated[r] : 0;
+      }
+      if (ratio > 1.0) { /* the cpu key is (re)written even when the entry had none */
         const int64_t cs = (int64_t)zn->cpuset_cpus * 1000;
         al[KE_RES_CPU] = al[KE_RES_CPU] - cs + amplify(cs, ratio);
+        has[KE_RES_CPU] = 1;
       }
       for (int r = 0; r < KE_NRES; r++) { /* SubtractWithNonNegativeResult(allocated, reusable = {}) */
-        v->al_has[z][r] = 1;
-        v->al[z][r] = al[r] > 0 ? al[r] : 0;
+        v->al_has[z][r] = has[r];
+        v->al[z][r] = has[r] && al[r] > 0 ? al[r] : 0;
       }
     }
     for (int r = 0; r < KE_NRES; r++) { /* SubtractWithNonNegativeResult(capacity, allocated) */
-      const int64_t a = v->has_alloc[z] ? v->al[z][r] : 0;
-      v->av_has[z][r] = v->cap_has[z][r] || v->has_alloc[z];
+      const int64_t a = v->al_has[z][r] ? v->al[z][r] : 0;
+      v->av_has[z][r] = v->cap_has[z][r] || v->al_has[z][r];
       const int64_t q = v->cap_has[z][r] ? v->cap[z][r] - a : -a;
       v->av[z][r] = q > 0 ? q : 0;
     }
@@ -932,6 +938,44 @@ static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod,
   }
   *affinity = best.mask;
   return KE_CODE_SUCCESS;
+}
+
+/* Golden-vector entry points.  tryBestToDistributeEvenly of `pod` on node `node` for the NUMA ids in
+ * `mask` (resource_manager.go:260-314): returns 1 when every requested NUMA resource was split;
+ * out16[2*id + r] = the amounts. */
+int or_numa_distribute(const or_cluster* c, int32_t node, const ke_pod* pod, uint32_t mask, int64_t* out16) {
+  const or_node* nd = &c->nodes[node];
+  numa_view v;
+  if (numa_view_build(nd, &v) != 0) return -1;
+  int64_t out[KE_MAX_NUMA][KE_NRES];
+  const int ok = numa_distribute(&v, mask, pod, out);
+  for (int i = 0; i < 2 * KE_MAX_NUMA; i++) out16[i] = 0;
+  for (int z = 0; z < v.n; z++)
+    for (int r = 0; r < KE_NRES; r++) out16[2 * v.id[z] + r] = out[z][r];
+  return ok;
+}
+
+/* generateResourceHints for `pod` on `node` under `policy` (resource_manager.go:525-622): per
+ * resource r (cpu, memory) present[r] = the resource has a hint list, counts[r] its length and
+ * masks / preferred / scores[r*255 + i] its hints in order. */
+int or_numa_hints(const or_cluster* c, int32_t node, const ke_pod* pod, int32_t policy, uint32_t* masks,
+                  uint8_t* preferred, int64_t* scores, int32_t* counts, int32_t* present) {
+  const or_node* nd = &c->nodes[node];
+  numa_view v;
+  if (numa_view_build(nd, &v) != 0) return -1;
+  static __thread numa_hint store[KE_NRES * 255];
+  int cnt[KE_NRES], pres[KE_NRES];
+  numa_generate_hints(c, &v, pod, policy, store, cnt, pres);
+  for (int r = 0; r < KE_NRES; r++) {
+    counts[r] = cnt[r];
+    present[r] = pres[r];
+    for (int i = 0; i < cnt[r]; i++) {
+      masks[r * 255 + i] = store[r * 255 + i].mask;
+      preferred[r * 255 + i] = (uint8_t)store[r * 255 + i].preferred;
+      scores[r * 255 + i] = store[r * 255 + i].score;
+    }
+  }
+  return 0;
 }
 
 /* the pod's NUMA allocation on its affinity (resourceManager.Allocate -> allocateResourcesByHint) */
@@ -1466,7 +1510,9 @@ int or_node_numa_set(or_cluster* c, int32_t node, int32_t n, const ke_numa_zone*
   for (int32_t i = 0; i < n; i++) { /* same validation as the product (ke_node_numa_set) */
     if (zones[i].id < 0 || zones[i].id >= KE_MAX_NUMA || (i > 0 && zones[i].id <= zones[i - 1].id)) return KE_ERR_INVALID;
     if (zones[i].capacity[0] < 0 || zones[i].capacity[1] < 0 || zones[i].cpuset_cpus < 0) return KE_ERR_INVALID;
-    if (zones[i].cpuset_cpus > 0 && !zones[i].has_allocated) return KE_ERR_INVALID;
+    if (zones[i].cpuset_cpus > 0 && !(zones[i].has_allocated & KE_NUMA_ALLOC_ENTRY)) return KE_ERR_INVALID;
+    if (zones[i].has_allocated > 7 || (zones[i].has_allocated && !(zones[i].has_allocated & KE_NUMA_ALLOC_ENTRY)))
+      return KE_ERR_INVALID;
   }
   c->nodes[node].n_zone = n;
   if (n) memcpy(c->nodes[node].zone, zones, sizeof(ke_numa_zone) * (size_t)n);
@@ -1489,9 +1535,14 @@ static void or_numa_reserve(or_cluster* c, const ke_pod* pod, int32_t node, int6
     ke_numa_zone* zn = &n->zone[z];
     if (out16)
       for (int r = 0; r < KE_NRES; r++) out16[2 * zn->id + r] = out[z][r];
-    if (!zn->has_allocated) zn->allocated[0] = zn->allocated[1] = 0;
-    zn->has_allocated = 1;
-    for (int r = 0; r < KE_NRES; r++) zn->allocated[r] += out[z][r];
+    /* quotav1.Add(entry, allocation): the allocation holds the keys with a non-zero amount */
+    for (int r = 0; r < KE_NRES; r++) {
+      const uint8_t key = r == KE_RES_CPU ? KE_NUMA_ALLOC_CPU : KE_NUMA_ALLOC_MEMORY;
+      if (!(zn->has_allocated & key)) zn->allocated[r] = 0;
+      if (out[z][r] != 0) zn->has_allocated |= key;
+      zn->allocated[r] += out[z][r];
+    }
+    zn->has_allocated |= KE_NUMA_ALLOC_ENTRY;
   }
 }
 

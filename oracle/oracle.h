@@ -58,6 +58,11 @@ uint64_t or_ds_reserve(or_cluster* c, const ke_pod* pod, int32_t node);
 /* DefaultEstimator.EstimatePod (estimator/default_estimator.go:59-85): est[KE_NRES], -1 = key absent */
 void or_estimate_pod(const or_cluster* c, const ke_pod* pod, int64_t* est);
 
+/* NUMA golden-vector entry points (tryBestToDistributeEvenly on a forced hint; generateResourceHints) */
+int or_numa_distribute(const or_cluster* c, int32_t node, const ke_pod* pod, uint32_t mask, int64_t* out16);
+int or_numa_hints(const or_cluster* c, int32_t node, const ke_pod* pod, int32_t policy, uint32_t* masks,
+                  uint8_t* preferred, int64_t* scores, int32_t* counts, int32_t* present);
+
 /* Matrix evaluation, same layout as ke_eval.  n_threads <= 0: all cores. */
 int or_eval(const or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now_ns, uint8_t* status,
             uint8_t* reason, int16_t* la_score, int16_t* numa_score, int16_t* ds_score, int16_t* total,

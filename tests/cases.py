@@ -160,3 +160,57 @@ def rl3(dev_type, rl):
         vals[key] = model.value(v)
         has[key] = 1
     return vals, has
+
+
+# ---- NodeNUMAResource non-cpuset NUMA vectors (numa_policy.json ops affinity/distribute/hints/available)
+NUMA_POLICY_ID = {"None": 0, "BestEffort": 1, "Restricted": 2, "SingleNUMANode": 3}
+
+
+def numa_case_cfg(case):
+    cfg = abi.default_config(1)
+    if case.get("numa_strategy") == "MostAllocated":
+        cfg.numa.numa_strategy = abi.STRATEGY_MOST_ALLOCATED
+    return cfg
+
+
+def numa_case_zones(case):
+    """The case's zones (+ allocation entries and cpusets) as model.make_zones input."""
+    if case["op"] == "affinity":
+        n = case["zones"]
+        cpu_m = model.milli_value(case["node"]["cpu"]) // n
+        mem = model.value(case["node"]["memory"]) // n
+        zones = []
+        for k in range(n):
+            z = {"id": k, "cpu": f"{cpu_m}m", "memory": str(mem)}
+            ex = case["existing"].get(str(k), case["existing"].get(k, []))
+            if ex:
+                z["allocated"] = {"cpu": f"{sum(model.milli_value(p['cpu']) for p in ex)}m",
+                                  "memory": str(sum(model.value(p["memory"]) for p in ex))}
+            zones.append(z)
+        return zones
+    zones = []
+    for k, z in enumerate(case["zones"]):
+        z = dict(z)
+        al = (case.get("allocated") or [None] * len(case["zones"]))[k]
+        if al is not None:
+            z["allocated"] = dict(al)
+        cs = (case.get("cpusets") or [0] * len(case["zones"]))[k]
+        if cs:
+            z["cpuset_cpus"] = cs
+        zones.append(z)
+    return zones
+
+
+def setup_numa_case(handle, case):
+    """Node 0 of `handle` with the case's policy, amplification ratio and zones; returns the pod."""
+    n = model.make_node(allocatable=case["node"], amplification_ratio=case.get("ratio"),
+                        nrt_amplification_ratio=case.get("nrt_ratio"))
+    n.numa_topology_policy = NUMA_POLICY_ID[case.get("policy", "BestEffort")]
+    handle.upsert_node(0, n)
+    handle.set_numa(0, model.make_zones(numa_case_zones(case)))
+    return model.make_pod(requests=dict(case.get("pod", {})))
+
+
+def quantity_vec(rl):
+    """{'cpu': q, 'memory': q} -> [cpu milli, memory bytes]"""
+    return [model.milli_value(rl.get("cpu", 0)), model.value(rl.get("memory", 0))]

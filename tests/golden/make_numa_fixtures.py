@@ -6,6 +6,10 @@ haoyann/koordinator).  Cases:
 * topologymanager Policy.Merge cases (frameworkext/topologymanager/policy_test.go): provider hint lists
   -> merged hint (NUMANodeAffinity, Preferred) and admit.  The Go tables leave `Unsatisfied` and `Score`
   unset in their expectations; only the affinity, Preferred and admit are compared.
+* NodeNUMAResource for pods without CPU binding: the NUMA affinity Filter stores under SingleNUMANode /
+  Restricted with NUMA-scope hint scoring (plugin_test.go), tryBestToDistributeEvenly on a fixed hint
+  and hint generation (resource_manager_test.go), getAvailableNUMANodeResources (node_allocation_test.go).
+  Cases that need CPU binding (cpusets), hugepages or reservations are not transcribed.
 
 Hint: [bits or None, preferred].  Provider: None (no hints) | {} (empty map) | {resource: None | [] | [hints]}.
 
@@ -128,6 +132,77 @@ for policy, numa_nodes, table, src_end in (
         cases.append({"name": f"{policy}: {name}", "source": f"{POLICY}:{line}", "op": "merge", "policy": policy,
                       "numa_nodes": numa_nodes, "providers": providers,
                       "want": {"bits": exp, "preferred": pref, "admit": admit}})
+
+# ---- NodeNUMAResource non-cpuset NUMA path ----------------------------------------------------------
+PLUGIN = "pkg/scheduler/plugins/nodenumaresource/plugin_test.go"
+RM = "pkg/scheduler/plugins/nodenumaresource/resource_manager_test.go"
+NA = "pkg/scheduler/plugins/nodenumaresource/node_allocation_test.go"
+
+# TestFilterWithNUMANodeScoring (plugin_test.go:1969-2190): node cpu 104 / memory 256Gi split evenly over
+# `zones` NUMA nodes, existing pods' requests allocated per zone (resourceManager.Update), the pod
+# requests cpu 4 / memory 40Gi; Filter succeeds and stores `want` as the NUMA affinity.
+def affinity(name, lines, policy, zones, existing, strategy, want):
+    cases.append({"name": f"{policy}: {name}", "source": f"{PLUGIN}:{lines}", "op": "affinity", "policy": policy,
+                  "numa_strategy": strategy, "node": {"cpu": "104", "memory": "256Gi"}, "zones": zones,
+                  "existing": existing, "pod": {"cpu": "4", "memory": "40Gi"}, "want": {"bits": want}})
+
+
+E2 = {0: [{"cpu": "4", "memory": "8Gi"}], 1: [{"cpu": "40", "memory": "8Gi"}]}
+E4 = {0: [{"cpu": "24", "memory": "8Gi"}], 1: [{"cpu": "23", "memory": "8Gi"}], 2: [{"cpu": "4", "memory": "8Gi"}],
+      3: [{"cpu": "8", "memory": "8Gi"}]}
+affinity("single numa nodes and select most allocated", "2006-2026", "SingleNUMANode", 2, E2, "MostAllocated", [1])
+affinity("single numa nodes and select least allocated", "2028-2048", "SingleNUMANode", 2, E2, "LeastAllocated", [0])
+affinity("single numa nodes and only one node can be used", "2050-2070", "SingleNUMANode", 2,
+         {0: [{"cpu": "4", "memory": "8Gi"}], 1: [{"cpu": "52", "memory": "8Gi"}]}, "LeastAllocated", [0])
+affinity("restricted numa nodes and select most allocated and preferred", "2072-2098", "Restricted", 4, E4,
+         "MostAllocated", [3])
+affinity("restricted numa nodes and select least allocated and preferred", "2100-2126", "Restricted", 4, E4,
+         "LeastAllocated", [2])
+
+# resource manager on buildCPUTopologyForTest(2, 1, 26, 2): NUMA 0 = CPUs 0-51, NUMA 1 = CPUs 52-103,
+# NUMANodeResources cpu 52 / memory 128Gi each (resource_manager_test.go:1213-1231, 1617-1637).
+RM_ZONES = [{"id": 0, "cpu": "52", "memory": "128Gi"}, {"id": 1, "cpu": "52", "memory": "128Gi"}]
+CPUSHARE_ALLOC = [{"cpu": "50"}, {"cpu": "50"}]  # PodAllocation CPUSet 0-49,52-101 + NUMANodeResources
+CPUSHARE_CPUSETS = [50, 50]
+
+
+def distribute(name, lines, requests, hint, want, ratio=None, allocated=None, cpusets=None):
+    """TestAllocateDistributeEvenly cases without CPU binding: Allocate with a fixed hint."""
+    cases.append({"name": name, "source": f"{RM}:{lines}", "op": "distribute", "node": {"cpu": "104", "memory": "256Gi"},
+                  "ratio": ratio, "zones": RM_ZONES, "allocated": allocated, "cpusets": cpusets,
+                  "pod": requests, "hint": hint, "want": want})
+
+
+distribute("allocate with non-existing resources in NUMA", "611-644", {"cpu": "4"}, [0, 1],
+           {"ok": True, "alloc": {"0": {"cpu": "2"}, "1": {"cpu": "2"}}})  # gpu-memory is not a NUMA resource
+distribute("allocate with insufficient resources", "645-662", {"cpu": "108"}, [0, 1], {"ok": False})
+distribute("allocate with CPU Share and allocated and amplified ratios", "1154-1210", {"cpu": "3.5"}, [0, 1],
+           {"ok": True, "alloc": {"0": {"cpu": "1.75"}, "1": {"cpu": "1.75"}}}, ratio=1.5,
+           allocated=CPUSHARE_ALLOC, cpusets=CPUSHARE_CPUSETS)
+
+# TestResourceManagerGetTopologyHint (resource_manager_test.go:1279-1668), BestEffort, no CPU binding
+cases.append({"name": "failed to allocate with CPU Share and allocated and amplified ratios",
+              "source": f"{RM}:1532-1580", "op": "hints", "policy": "BestEffort", "node": {"cpu": "104", "memory": "256Gi"},
+              "ratio": 1.5, "zones": RM_ZONES, "allocated": CPUSHARE_ALLOC, "cpusets": CPUSHARE_CPUSETS,
+              "pod": {"cpu": "4"}, "want": {"hints": {"cpu": [[[0, 1], True]]}}})
+
+# Test_getAvailableNUMANodeResources (node_allocation_test.go:171-300): CPU topology (2, 1, 8, 2), so
+# allocatedCPUSets = 4 are CPUs 0-3 on NUMA 0.  `nrt_ratio`: TopologyOptions.AmplificationRatios (the
+# NUMANodeResources are already amplified).
+R16 = {"cpu": "16", "memory": "32Gi"}
+R24 = {"cpu": "24", "memory": "32Gi"}
+for name, lines, res, ratio, alloc, cpusets, want in [
+    ("normal node", "190-205", R16, None, None, None, [R16, R16]),
+    ("normal node with amplification ratios", "206-223", R24, 1.5, None, None, [R24, R24]),
+    ("normal node with amplification ratios and allocated CPUSets", "224-256", R24, 1.5, [{"cpu": "4"}, None], [4, 0],
+     [{"cpu": "18", "memory": "32Gi"}, R24]),
+    ("normal node with amplification ratios and allocated CPUSets and CPU Shares", "257-289", R24, 1.5,
+     [{"cpu": "8"}, None], [4, 0], [{"cpu": "14", "memory": "32Gi"}, R24]),
+]:
+    cases.append({"name": name, "source": f"{NA}:{lines}", "op": "available", "node": {"cpu": "32", "memory": "64Gi"},
+                  "nrt_ratio": ratio, "zones": [dict(id=k, **res) for k in range(2)], "allocated": alloc,
+                  "cpusets": cpusets, "want": {"available": want}})
+
 
 def main():
     with open(os.path.join(HERE, "numa_policy.json"), "w") as f:

@@ -449,3 +449,29 @@ def test_numa_policy_edge_cases(gpu):
     assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
     assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
     assert_eval_equal(ev.eval(pods, cases.NOW), o.eval(pods, cases.NOW))
+
+
+NUMA_VEC = [c for c in cases.load("numa_policy.json") if c["op"] in ("affinity", "hints")
+            or c["name"] == "allocate with CPU Share and allocated and amplified ratios"]
+
+
+@pytest.mark.parametrize("case", NUMA_VEC, ids=[f'{c["op"]}: {c["name"]}' for c in NUMA_VEC])
+def test_golden_numa_policy_path(gpu, case):
+    """The reference's NUMA vectors observable through ke_schedule: the zones the pod's allocation
+    lands on (= the stored affinity) and the amounts, against the expectation and the oracle."""
+    ev, o = Evaluator(cases.numa_case_cfg(case)), Oracle(cases.numa_case_cfg(case), 1)
+    pod = cases.setup_numa_case(ev, case)
+    cases.setup_numa_case(o, case)
+    c1, s1 = ev.schedule([pod], cases.NOW)
+    c0, s0 = o.schedule([pod], cases.NOW)
+    assert c1[0] == 0 and (c1[0], s1[0]) == (c0[0], s0[0])
+    assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
+    alloc = ev.last_numa_allocations[0].reshape(8, 2)
+    zones = [z for z in range(8) if alloc[z].any()]
+    if case["op"] == "affinity":
+        assert zones == case["want"]["bits"], case["source"]
+    elif case["op"] == "hints":  # BestEffort admits the single preferred hint
+        assert zones == case["want"]["hints"]["cpu"][0][0], case["source"]
+    else:  # the single-zone hints do not fit: the merged hint is {0,1}, split 1.75 / 1.75
+        got = {str(z): alloc[z].tolist() for z in zones}
+        assert got == {z: cases.quantity_vec(rl) for z, rl in case["want"]["alloc"].items()}, case["source"]

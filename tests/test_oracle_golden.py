@@ -114,10 +114,47 @@ def _lists(providers):
     return out
 
 
-@pytest.mark.parametrize("case", NUMA_POLICY, ids=[c["name"] for c in NUMA_POLICY])
+NUMA_MERGE = [c for c in NUMA_POLICY if c["op"] == "merge"]
+
+
+@pytest.mark.parametrize("case", NUMA_MERGE, ids=[c["name"] for c in NUMA_MERGE])
 def test_numa_policy_merge(case):
     from oracle.binding import topology_merge
     admit, mask, pref, _, _ = topology_merge(POLICY_ID[case["policy"]], _mask(case["numa_nodes"]),
                                              _lists(case["providers"]))
     want = case["want"]
     assert (mask, pref, admit) == (_mask(want["bits"]), want["preferred"], want["admit"]), case["source"]
+
+
+NUMA_PATH = [c for c in NUMA_POLICY if c["op"] != "merge"]
+
+
+@pytest.mark.parametrize("case", NUMA_PATH, ids=[f'{c["op"]}: {c["name"]}' for c in NUMA_PATH])
+def test_numa_policy_path(case):
+    """Non-cpuset pods under a NUMA topology policy against the reference's own vectors."""
+    o = Oracle(cases.numa_case_cfg(case), 1)
+    pod = cases.setup_numa_case(o, case)
+    want = case["want"]
+    if case["op"] == "affinity":  # Filter succeeds; Reserve allocates on exactly the stored affinity
+        chosen, _ = o.schedule([pod], cases.NOW)
+        assert chosen[0] == 0
+        alloc = o.last_numa_allocations[0].reshape(8, 2)
+        assert [z for z in range(8) if alloc[z].any()] == want["bits"], case["source"]
+    elif case["op"] == "distribute":
+        ok, out = o.numa_distribute(0, pod, sum(1 << b for b in case["hint"]))
+        assert ok == want["ok"], case["source"]
+        if ok:
+            got = {str(z): out[2 * z: 2 * z + 2].tolist() for z in range(8) if out[2 * z: 2 * z + 2].any()}
+            assert got == {z: cases.quantity_vec(rl) for z, rl in want["alloc"].items()}, case["source"]
+    elif case["op"] == "hints":
+        hints = o.numa_hints(0, pod, cases.NUMA_POLICY_ID[case["policy"]])
+        names = {"cpu": 0, "memory": 1}
+        want_h = {names[k]: [(sum(1 << b for b in bits), pref) for bits, pref in v] for k, v in want["hints"].items()}
+        assert {r: [(m, p) for m, p, _ in h] for r, h in hints.items()} == want_h, case["source"]
+    else:  # available: the largest request a single zone can take (tryBestToDistributeEvenly on {zone})
+        for z, rl in enumerate(want["available"]):
+            for key, q in zip(("cpu", "memory"), cases.quantity_vec(rl)):
+                for amount, fits in ((q, True), (q + 1, False)):
+                    p = cases.make_pod({"requests": {key: f"{amount}m" if key == "cpu" else str(amount)}})
+                    ok, _ = o.numa_distribute(0, p, 1 << z)
+                    assert ok == fits, (case["source"], z, key, amount)
