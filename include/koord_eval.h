@@ -162,6 +162,12 @@ typedef struct ke_numa_args {
 #define KE_NUMA_POLICY_RESTRICTED 2
 #define KE_NUMA_POLICY_SINGLE_NUMA_NODE 3
 #define KE_MAX_NUMA 8
+#define KE_NUMA_EXCLUSIVE_NONE 0 /* ke_pod.numa_exclusive: unset (Required when the pod sets a policy) */
+#define KE_NUMA_EXCLUSIVE_PREFERRED 1
+#define KE_NUMA_EXCLUSIVE_REQUIRED 2
+#define KE_NUMA_STATUS_IDLE 0   /* ke_numa_zone.numa_status: NodeAllocation.NUMANodeSharedStatus */
+#define KE_NUMA_STATUS_SINGLE 1 /* only single-NUMA cpuset pods use the zone */
+#define KE_NUMA_STATUS_SHARED 2 /* some cpuset pod spans several zones including this one */
 #define KE_NUMA_ALLOC_ENTRY 1u  /* ke_numa_zone.has_allocated bits */
 #define KE_NUMA_ALLOC_CPU 2u
 #define KE_NUMA_ALLOC_MEMORY 4u
@@ -178,7 +184,7 @@ typedef struct ke_numa_zone {
   uint8_t has_allocated;       /* the resource manager's allocatedResources entry of the zone:
                                   KE_NUMA_ALLOC_ENTRY | KE_NUMA_ALLOC_CPU | KE_NUMA_ALLOC_MEMORY (the keys
                                   its ResourceList holds; 0 = no entry) */
-  uint8_t pad;
+  uint8_t numa_status;         /* KE_NUMA_STATUS_* (node_allocation.go:52-68), from the cpuset pods on it */
   int64_t capacity[KE_NRES];   /* cpu milli, memory bytes (before amplification) */
   int64_t allocated[KE_NRES];  /* Σ NUMANodeResources of the pods allocated on the zone */
   int32_t cpuset_cpus;         /* cpuset CPUs allocated in the zone (allocatedCPUs.CPUsInNUMANodes) */
@@ -327,6 +333,8 @@ typedef struct ke_pod {
   uint8_t has_other_requests;         /* PodRequests has a non-zero resource outside KE_RES_* */
   uint8_t has_unsupported_device_requests; /* Huawei NPU / Hygon DCU device resources: unsupported */
   int64_t device_requests[KE_PDR_COUNT]; /* PodRequests of the device resources (Value()), 0 = absent */
+  int32_t numa_topology_policy; /* NUMATopologySpec annotation: KE_NUMA_POLICY_* (NONE = unset) */
+  int32_t numa_exclusive;       /* NUMATopologySpec.SingleNUMANodeExclusive: KE_NUMA_EXCLUSIVE_* */
 } ke_pod;
 
 /* One candidate of a pod's speculative top-k list (device order: best first). */

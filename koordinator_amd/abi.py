@@ -32,6 +32,8 @@ REASON_NUMA_HINT_UNALIGNED = 21
 REASON_NUMA_INSUFFICIENT_RESOURCES = 22
 NUMA_POLICY_NONE, NUMA_POLICY_BEST_EFFORT, NUMA_POLICY_RESTRICTED, NUMA_POLICY_SINGLE_NUMA_NODE = 0, 1, 2, 3
 NUMA_ALLOC_ENTRY, NUMA_ALLOC_CPU, NUMA_ALLOC_MEMORY = 1, 2, 4  # ke_numa_zone.has_allocated bits
+NUMA_EXCLUSIVE_NONE, NUMA_EXCLUSIVE_PREFERRED, NUMA_EXCLUSIVE_REQUIRED = 0, 1, 2
+NUMA_STATUS_IDLE, NUMA_STATUS_SINGLE, NUMA_STATUS_SHARED = 0, 1, 2
 MAX_NUMA = 8
 REASON_DS_INVALID_REQUEST = 32
 REASON_DS_INSUFFICIENT_GPU = 33
@@ -101,7 +103,7 @@ class NumaZone(C.Structure):
         ("id", i32),
         ("has", u8 * NRES),
         ("has_allocated", u8),
-        ("pad", u8),
+        ("numa_status", u8),
         ("capacity", i64 * NRES),
         ("allocated", i64 * NRES),
         ("cpuset_cpus", i32),
@@ -208,6 +210,8 @@ class Pod(C.Structure):
         ("has_other_requests", u8),
         ("has_unsupported_device_requests", u8),
         ("device_requests", i64 * PDR_COUNT),
+        ("numa_topology_policy", i32),
+        ("numa_exclusive", i32),
     ]
 
 

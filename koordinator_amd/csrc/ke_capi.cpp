@@ -50,11 +50,18 @@ static int require_device(ke_ctx* ctx) {
 
 // DeviceShare is a NUMA hint provider for pods with device requests (deviceshare/topology_hint.go);
 // that provider is not modelled, so such pods cannot meet nodes with a NUMA topology policy.
+// A pod with its own NUMA topology policy switches the NUMA path on for every node.
 static int check_numa_deviceshare(ke_ctx* ctx, const ke_pod* pods, int32_t n) {
-  if (!ctx->c.numa_enabled) return KE_OK;
   bool ds = false;
-  for (int32_t p = 0; p < n && !ds; p++) ds = (make_dev_pod(ctx->c.cfg, pods[p]).flags & PF_DS) != 0;
-  if (!ds) return KE_OK;
+  for (int32_t p = 0; p < n; p++) {
+    if (pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE) ctx->c.numa_enabled = true;
+    if (make_dev_pod(ctx->c.cfg, pods[p]).flags & PF_DS) {
+      ds = true;
+      if (pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE)
+        return fail(KE_ERR_UNSUPPORTED, "DeviceShare pods with a NUMA topology policy (DeviceShare NUMA hints)");
+    }
+  }
+  if (!ds || !ctx->c.numa_enabled) return KE_OK;
   for (int32_t i = 0; i < ctx->c.n_nodes; i++)
     if (ctx->c.nodes[i].valid && ctx->c.nodes[i].node.numa_topology_policy != KE_NUMA_POLICY_NONE)
       return fail(KE_ERR_UNSUPPORTED, "DeviceShare pods on nodes with a NUMA topology policy (DeviceShare NUMA hints)");

@@ -154,6 +154,10 @@ int validate_pod(const ke_pod& p) {
     return fail(KE_ERR_UNSUPPORTED, "Huawei NPU / Hygon DCU device requests are not implemented");
   for (int i = 0; i < KE_PDR_COUNT; i++)
     if (p.device_requests[i] < 0) return fail(KE_ERR_INVALID, "negative device request");
+  if (p.numa_topology_policy < KE_NUMA_POLICY_NONE || p.numa_topology_policy > KE_NUMA_POLICY_SINGLE_NUMA_NODE)
+    return fail(KE_ERR_INVALID, "pod NUMA topology policy");
+  if (p.numa_exclusive < KE_NUMA_EXCLUSIVE_NONE || p.numa_exclusive > KE_NUMA_EXCLUSIVE_REQUIRED)
+    return fail(KE_ERR_INVALID, "pod NUMA exclusive policy");
   return KE_OK;
 }
 
@@ -307,6 +311,11 @@ DevPod make_dev_pod(const ke_config& cfg, const ke_pod& pod) {
   if (pod.priority_class == KE_PRIORITY_PROD) f |= PF_PROD;
   if (zero) f |= PF_NUMA_SKIP;
   if (pod.priority_class == KE_PRIORITY_PROD && cfg.loadaware.score_according_prod_usage) f |= PF_LA_SCORE_PROD;
+  // NUMATopologySpec: the pod's policy; SingleNUMANodeExclusive defaults to Required with a policy
+  f |= (uint32_t)pod.numa_topology_policy * PF_NUMA_POLICY0;
+  if (pod.numa_exclusive == KE_NUMA_EXCLUSIVE_REQUIRED ||
+      (pod.numa_exclusive == KE_NUMA_EXCLUSIVE_NONE && pod.numa_topology_policy != KE_NUMA_POLICY_NONE))
+    f |= PF_NUMA_EXCL_REQ;
   d.flags = f;
   if (!ds_prepare(pod, d)) {
     for (int t = 0; t < 3; t++) d.ds_cnt[t] = 0;
@@ -569,6 +578,7 @@ int validate_zones(int32_t n, const ke_numa_zone* zones) {
       return fail(KE_ERR_INVALID, "cpuset CPUs allocated in a zone without an allocation entry");
     if (zones[i].has_allocated > 7 || (zones[i].has_allocated && !(zones[i].has_allocated & KE_NUMA_ALLOC_ENTRY)))
       return fail(KE_ERR_INVALID, "NUMA allocation keys without an allocation entry");
+    if (zones[i].numa_status > KE_NUMA_STATUS_SHARED) return fail(KE_ERR_INVALID, "NUMA node status");
   }
   return KE_OK;
 }
@@ -591,6 +601,10 @@ void derive_numa_row(const NodeState& ns, int64_t* f, uint64_t* mask) {
   for (const ke_numa_zone& z : ns.zones) {
     const int id = z.id;
     *mask |= 1ull << id;
+    if (id < (int)ns.zones.size()) {  // GetAllNUMANodeStatus(len(numaNodes)) covers ids 0..n-1
+      if (z.numa_status == KE_NUMA_STATUS_SINGLE) *mask |= 1ull << (NUMA_M_ST + id);
+      if (z.numa_status == KE_NUMA_STATUS_SHARED) *mask |= 1ull << (NUMA_M_ST + 8 + id);
+    }
     for (int r = 0; r < KE_NRES; r++) {
       if (z.has[r]) {
         *mask |= 1ull << (NUMA_M_CAP + 8 * r + id);

@@ -347,6 +347,7 @@ __constant__ uint8_t NUMA_OFF[10] = {0, 0, 8, 36, 92, 162, 218, 246, 254, 255}; 
 
 struct NumaNode {
   uint32_t zm, ch[2], ak[2];  // zones present, capacity keys, allocated keys per resource (bit = NUMA id)
+  uint32_t single, shared;    // NUMANodeSharedStatus single / shared (ids < number of zones)
   int64_t av[2][8];        // totalAvailable[r][id] (0 for absent zones / keys)
   uint32_t perm[2][8];     // perm[r][nb-1]: slot order of an nb-zone hint after the distribute sort
 };
@@ -383,6 +384,8 @@ __device__ __forceinline__ void numa_load(const SoA& s, int64_t i, NumaNode& v) 
     v.ch[r] = (uint32_t)(m >> (NUMA_M_CAP + 8 * r)) & 0xFFu;
     v.ak[r] = (uint32_t)(m >> (NUMA_M_AL + 8 * r)) & 0xFFu;
   }
+  v.single = (uint32_t)(m >> NUMA_M_ST) & 0xFFu;
+  v.shared = (uint32_t)(m >> (NUMA_M_ST + 8)) & 0xFFu;
 #pragma unroll
   for (int z = 0; z < 8; z++)
 #pragma unroll
@@ -506,8 +509,17 @@ struct NumaPick {
   uint32_t aff;  // merged NUMANodeAffinity, 0 = nil
 };
 
+// checkExclusivePolicy (policy.go:73-93) for a non-empty mask: with SingleNUMANodeExclusive Required a
+// multi-zone hint may not touch a "single" zone and a one-zone hint may not be a "shared" zone.
+__device__ __forceinline__ bool exclusive_ok(const NumaNode& v, uint32_t m, bool required) {
+  if (!required) return true;
+  return __popc(m) > 1 ? (m & v.single) == 0 : (m & v.shared) == 0;
+}
+
 // BestEffort without a preferred merged hint: mergeFilteredHints over the full provider lists
-// (policy.go:198-260); an unsatisfied result (or a resource without hints) -> any NUMA node.
+// (policy.go:198-260), every merged hint non-preferred; an unsatisfied result (or a resource without
+// hints) -> any NUMA node.  Lists in resource-name order (cpu, memory): the reference ranges over a Go
+// map here, so its order — and with it this tie-break — is not deterministic.
 __device__ __forceinline__ uint32_t numa_best_effort_fallback(const SoA& s, int64_t i, const NumaNode& v, const DevPod& p,
                                                            const KArgs& k, const bool (&present)[2],
                                                            const uint32_t (&lack)[2]) {
@@ -529,10 +541,22 @@ __device__ __forceinline__ uint32_t numa_best_effort_fallback(const SoA& s, int6
   }
   const bool e0 = !(L[0][0] | L[0][1] | L[0][2] | L[0][3]), e1 = !(L[1][0] | L[1][1] | L[1][2] | L[1][3]);
   if ((present[0] && e0) || (present[1] && e1)) return v.zm;  // filterProvidersHints reasons
-  if (!(present[0] && present[1])) return v.zm;  // unreachable: one list always has a preferred hint
   uint32_t best = v.zm;
   int32_t bsc = 0;
   bool bun = false;
+  if (!(present[0] && present[1])) {  // one list (+ DeviceShare's any-NUMA hint): merged = the hint
+    const int r = present[0] ? 0 : 1;
+    for (int e = 0; e < 255; e++) {
+      const uint32_t m = NUMA_ORDER[e];
+      if ((m & ~v.zm) || !in_list(L[r], m)) continue;
+      const int32_t sc = numa_hint_score(s, i, v, m, p, k);
+      if (narrower(m, best) || (__popc(m) == __popc(best) && sc > bsc)) {
+        best = m;
+        bsc = sc;
+      }
+    }
+    return best;
+  }
   for (int e1i = 0; e1i < 255; e1i++) {
     const uint32_t m1 = NUMA_ORDER[e1i];
     if ((m1 & ~v.zm) || !in_list(L[0], m1)) continue;
@@ -559,11 +583,12 @@ __device__ __forceinline__ uint32_t numa_best_effort_fallback(const SoA& s, int6
   return bun ? v.zm : best;
 }
 
-// FilterByNUMANode + RunNUMATopologyManagerAdmit for a pod whose requests are not all zero.
-__device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t nf, const NumaNode& v,
+// FilterByNUMANode + RunNUMATopologyManagerAdmit for a pod whose requests are not all zero, under
+// the merged topology `policy` (node / pod, util.go:58-74).
+__device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t nf, int policy, const NumaNode& v,
                                                const DevPod& p, const KArgs& k) {
   NumaPick o{KE_CODE_SUCCESS, KE_REASON_NONE, 0u};
-  const int policy = nf_numa_policy(nf);
+  const bool excl = (p.flags & PF_NUMA_EXCL_REQ) != 0;
   if (v.zm == 0) {  // topology_hint.go:31-41
     o.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
     o.reason = KE_REASON_NUMA_MISSING_RESOURCES;
@@ -590,6 +615,11 @@ __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t
   const int R = (int)present[0] + (int)present[1];
   int64_t dummy[2][8];
   if (R == 0) {  // no hints: one preferred any-NUMA hint per provider -> merged = all zones
+    if (policy != KE_NUMA_POLICY_BEST_EFFORT && !exclusive_ok(v, all, excl)) {
+      o.status = KE_CODE_UNSCHEDULABLE;
+      o.reason = KE_REASON_NUMA_HINT_UNALIGNED;
+      return o;
+    }
     if (policy == KE_NUMA_POLICY_SINGLE_NUMA_NODE) return o;  // best == all -> nil affinity
     o.aff = all;
     if (!numa_distribute<false>(v, all, p, nullptr, dummy)) {
@@ -618,7 +648,7 @@ __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t
       if (in1 && !minr[1]) minr[1] = sz;
       bool cand = (!present[0] || in0) && (!present[1] || in1);
       if (policy != KE_NUMA_POLICY_RESTRICTED) cand = cand && (!present[0] || first0) && (!present[1] || first1);
-      if (!cand) continue;
+      if (!cand || !exclusive_ok(v, m, excl)) continue;
       const int32_t sc = R * numa_hint_score(s, i, v, m, p, k);
       if (!found || narrower(m, best) || (__popc(m) == __popc(best) && sc > bsc)) {
         best = m;
@@ -734,7 +764,13 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
       }
     }
   }
-  // ---- NodeNUMAResource.Filter -> filterAmplifiedCPUs  plugin.go:318-442
+  // ---- NodeNUMAResource.Filter: node / pod topology policy merge (plugin.go:337-341), then
+  // filterAmplifiedCPUs (plugin.go:408-442)
+  const int pod_pol = NUMA ? pf_numa_policy(p.flags) : 0, node_pol = nf_numa_policy(nf);
+  if (NUMA && o.status == KE_CODE_SUCCESS && !(p.flags & PF_NUMA_SKIP) && pod_pol && node_pol && pod_pol != node_pol) {
+    o.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    o.reason = KE_REASON_NUMA_POLICY_CONFLICT;
+  }
   if (o.status == KE_CODE_SUCCESS && !(p.flags & PF_NUMA_SKIP) && p.req[0] != 0) {
     if (nf & NF_NUMA_AMP_ERR) {
       o.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
@@ -754,10 +790,11 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
     }
   }
   // ---- NodeNUMAResource.Filter under a NUMA topology policy: FilterByNUMANode + topologymanager Admit
-  const bool npol = NUMA && !(p.flags & PF_NUMA_SKIP) && nf_numa_policy(nf) != KE_NUMA_POLICY_NONE;
+  const int eff_pol = pod_pol ? pod_pol : node_pol;
+  const bool npol = NUMA && !(p.flags & PF_NUMA_SKIP) && eff_pol != KE_NUMA_POLICY_NONE;
   int32_t npol_score = 0;
   if (npol && o.status == KE_CODE_SUCCESS) {
-    const NumaPick pk = numa_admit(s, i, nf, nv, p, k);
+    const NumaPick pk = numa_admit(s, i, nf, eff_pol, nv, p, k);
     if (pk.status != KE_CODE_SUCCESS) {
       o.status = pk.status;
       o.reason = pk.reason;
@@ -866,7 +903,7 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_parity(SoA s, int n_nodes, 
   }
   const bool expired = live ? node_expired(n, k) : false;
   NumaNode nv;
-  if (NUMA && live && nf_numa_policy(n.flags) != KE_NUMA_POLICY_NONE) numa_load(s, i, nv);
+  if (NUMA && live) numa_load(s, i, nv);  // a pod's own policy reaches nodes without one
   const int p0 = blockIdx.y * pods_per_block;
   const int p1 = min(n_pods, p0 + pods_per_block);
   for (int p = p0; p < p1; p++) {
@@ -929,7 +966,7 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
   prepare_row(n);
   const bool expired = node_expired(n, k);
   NumaNode nv;
-  if (NUMA && nf_numa_policy(n.flags) != KE_NUMA_POLICY_NONE) numa_load(s, i, nv);
+  if (NUMA) numa_load(s, i, nv);  // a pod's own policy reaches nodes without one
   const int base = *batch_base;
   const int p0 = blockIdx.y * pods_per_block;
   const int p1 = min(batch_pods, p0 + pods_per_block);
@@ -1420,7 +1457,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
     uint32_t kc = 0;  // exact re-evaluation of the nodes changed earlier in this batch
     if (lane < n_chg) {
       NumaNode nv;
-      if (NUMA && nf_numa_policy(mine.flags) != KE_NUMA_POLICY_NONE) numa_load(s, my_node, nv);
+      if (NUMA) numa_load(s, my_node, nv);
       kc = make_key(eval_pair<false, NUMA>(mine, my_expired, pod, k, s, my_node, nv).total, my_node);
     }
     const uint32_t bc = wave_max_u32(kc);
@@ -1474,10 +1511,11 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
         s_alloc[j] = DS && (pod.flags & PF_DS) && (mine.flags & NF_DS_CACHE) ? ds_reserve(s, my_node, pod, k) : 0ull;
         if (NUMA) {  // NodeNUMAResource Reserve: the zones of a NUMA-policy node
           int64_t* out16 = numa_alloc + (int64_t)(base + j) * 16;
-          if (!(pod.flags & PF_NUMA_SKIP) && nf_numa_policy(mine.flags) != KE_NUMA_POLICY_NONE) {
+          const int pol = pf_numa_policy(pod.flags) ? pf_numa_policy(pod.flags) : nf_numa_policy(mine.flags);
+          if (!(pod.flags & PF_NUMA_SKIP) && pol != KE_NUMA_POLICY_NONE) {
             NumaNode nv;
             numa_load(s, my_node, nv);
-            const NumaPick pk = numa_admit(s, my_node, mine.flags, nv, pod, k);
+            const NumaPick pk = numa_admit(s, my_node, mine.flags, pol, nv, pod, k);
             numa_reserve(s, my_node, mine.flags, nv, pk.status == KE_CODE_SUCCESS ? pk.aff : 0u, pod, out16);
           } else {
 #pragma unroll

@@ -56,6 +56,7 @@ enum NodeFlag : uint32_t {
   NF_NUMA_AL_AMP = 1u << 19,      // the cpu amplification ratio in force is > 1: every allocation entry has a cpu key
 };
 KE_HD inline int nf_numa_policy(uint32_t f) { return (int)((f >> 16) & 3u); }
+KE_HD inline int pf_numa_policy(uint32_t f) { return (int)((f >> 9) & 3u); }
 
 // ---- NUMA topology state (a third SoA, allocated when the first node with a NUMA policy appears) ----
 // int64 fields indexed by NUMA id z (0..7) and resource r (cpu milli, memory):
@@ -64,8 +65,11 @@ KE_HD inline int nf_numa_policy(uint32_t f) { return (int)((f >> 16) & 3u); }
 //                      (getAvailableNUMANodeResources before its non-negative clamp)
 // uint64 mask (bit = NUMA id): zone present (bits 0-7), capacity cpu / memory key (NUMA_M_CAP + 8r),
 // allocated cpu / memory key (NUMA_M_AL + 8r; cpu set for every entry when a ratio > 1 adjusts it)
+// NUMANodeSharedStatus of NUMA ids 0..n_zones-1 (GetAllNUMANodeStatus): single (NUMA_M_ST),
+// shared (NUMA_M_ST + 8)
 constexpr int NUMA_M_CAP = 8;
 constexpr int NUMA_M_AL = 24;
+constexpr int NUMA_M_ST = 40;
 constexpr int NUMA_CAP = 0;
 constexpr int NUMA_AL = 16;
 constexpr int NUM_NUMA_FIELDS = 32;
@@ -82,6 +86,8 @@ enum PodFlag : uint32_t {
   PF_DS_H_CORE = 1u << 6,      // per-GPU request has gpu-core
   PF_DS_H_MEM = 1u << 7,       // per-GPU request has gpu-memory (fill: bytes -> ratio)
   PF_DS_H_RATIO = 1u << 8,     // per-GPU request has gpu-memory-ratio (fill: ratio -> bytes)
+  PF_NUMA_POLICY0 = 1u << 9,   // 2 bits: the pod's NUMATopologySpec policy (KE_NUMA_POLICY_*)
+  PF_NUMA_EXCL_REQ = 1u << 11, // SingleNUMANodeExclusive Required (explicit, or defaulted by a pod policy)
 };
 
 // host-side packed row (staging for uploads, debug readback)

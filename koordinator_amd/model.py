@@ -198,9 +198,11 @@ def make_pod(name="pod", namespace="default", requests=None, limits=None, contai
              init_containers=(), overhead=None, priority=None, labels=None, owner_kind=None, uid=None,
              scheduled_at=None, initialized_at=None, custom_factors=None,
              custom_seconds_after_scheduled=None, custom_seconds_after_initialized=None,
-             terminated=False):
+             terminated=False, numa_policy=None, numa_exclusive=None):
     """A pod as the plugins see it.  `requests`/`limits` describe one container (MakePod().Req());
-    `containers` gives the full list.  Times are ns."""
+    `containers` gives the full list.  Times are ns.  numa_policy / numa_exclusive: the
+    scheduling.koordinator.sh/numa-topology-spec annotation ('BestEffort' | 'Restricted' |
+    'SingleNUMANode'; 'Required' | 'Preferred')."""
     labels = dict(labels or {})
     if containers is None:
         containers = [] if requests is None and limits is None else [{"requests": requests or {}, "limits": limits or {}}]
@@ -238,6 +240,8 @@ def make_pod(name="pod", namespace="default", requests=None, limits=None, contai
     p.qos_class = qos_raw(labels)
     p.is_daemonset = 1 if owner_kind == "DaemonSet" else 0
     p.is_terminated = 1 if terminated else 0
+    p.numa_topology_policy = {None: 0, "": 0, "BestEffort": 1, "Restricted": 2, "SingleNUMANode": 3}[numa_policy]
+    p.numa_exclusive = {None: 0, "": 0, "Preferred": 1, "Required": 2}[numa_exclusive]
     return p
 
 
@@ -361,4 +365,5 @@ def make_zones(zones):
                                        | (abi.NUMA_ALLOC_MEMORY if "memory" in al else 0))
             arr[i]["allocated"][:] = [milli_value(al.get("cpu", 0)), value(al.get("memory", 0))]
         arr[i]["cpuset_cpus"] = int(z.get("cpuset_cpus", 0))
+        arr[i]["numa_status"] = {"idle": 0, "single": 1, "shared": 2}[z.get("status", "idle")]
     return arr

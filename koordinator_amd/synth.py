@@ -284,7 +284,7 @@ def make_ds_pods(n_pods, seed, device_fraction=0.5, key_base=2_000_000_000):
 
 # ---- NUMA topology policies (BASELINE config 4, non-cpuset part) ----------------------------------
 def make_numa(cl, seed, zone_counts=(8,), policy_weights=(0.1, 0.3, 0.3, 0.3), no_zone_fraction=0.02,
-              missing_memory_fraction=0.03, allocated_fraction=0.7):
+              missing_memory_fraction=0.03, allocated_fraction=0.7, status_fraction=0.0):
     """Give the nodes of cluster `cl` a NUMA topology policy (None / BestEffort / Restricted /
     SingleNUMANode by `policy_weights`) and NodeResourceTopology zones: the node's allocatable split
     evenly over `zone_counts` zones (cpu in whole cores), a few zones without a memory key, and a
@@ -324,8 +324,23 @@ def make_numa(cl, seed, zone_counts=(8,), policy_weights=(0.1, 0.3, 0.3, 0.3), n
                 z[k]["has_allocated"] = keys
                 if amplified and rng.random() < 0.25:
                     z[k]["cpuset_cpus"] = int(rng.integers(1, 4))
+            # NUMANodeSharedStatus from cpuset pods already on the node (the Go path placed them)
+            if rng.random() < status_fraction:
+                z[k]["numa_status"] = rng.choice([abi.NUMA_STATUS_SINGLE, abi.NUMA_STATUS_SHARED])
         out.append(z)
     return out
+
+
+def make_numa_pods(n_pods, seed, policy_fraction=0.3, key_base=3_000_000_000):
+    """The config-2 queue where `policy_fraction` of the pods carry a numa-topology-spec annotation:
+    a policy (BestEffort / Restricted / SingleNUMANode) and SingleNUMANodeExclusive unset (Required by
+    default) / Preferred / Required."""
+    rng = np.random.default_rng(seed)
+    pods = make_pods(n_pods, seed + 1, key_base=key_base)
+    pol = rng.random(n_pods) < policy_fraction
+    pods["numa_topology_policy"] = np.where(pol, rng.integers(1, 4, n_pods), 0)
+    pods["numa_exclusive"] = np.where(pol, rng.integers(0, 3, n_pods), 0)
+    return pods
 
 
 def load_numa(handle, zones):

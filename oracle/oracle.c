@@ -474,23 +474,38 @@ static int pod_requests_zero(const ke_pod* pod) { /* quotav1.IsZero(PodRequests)
 
 /* Plugin.Filter  plugin.go:318-406 -> filterAmplifiedCPUs :408-442 */
 static int numa_filter_amplified(const or_node* n, const ke_pod* pod, int* reason);
-static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod, int policy, uint32_t* affinity,
-                      int* reason);
+static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod, int policy, int exclusive,
+                      uint32_t* affinity, int* reason);
+
+/* getNUMATopologyPolicy + mergeTopologyPolicy (util.go:58-74) and the exclusive default of
+ * Filter (plugin.go:330-336): -1 on a node / pod policy conflict. */
+static int effective_policy(const or_node* n, const ke_pod* pod, int* exclusive) {
+  const int np = n->node.numa_topology_policy, pp = pod->numa_topology_policy;
+  *exclusive = pod->numa_exclusive;
+  if (*exclusive == KE_NUMA_EXCLUSIVE_NONE && pp != KE_NUMA_POLICY_NONE) *exclusive = KE_NUMA_EXCLUSIVE_REQUIRED;
+  if (np != KE_NUMA_POLICY_NONE && pp != KE_NUMA_POLICY_NONE && pp != np) return -1;
+  return pp != KE_NUMA_POLICY_NONE ? pp : np;
+}
 
 int or_numa_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* reason) {
   const or_node* n = &c->nodes[node];
   *reason = KE_REASON_NONE;
   if (pod_requests_zero(pod)) return KE_CODE_SUCCESS; /* state.skip */
+  int exclusive;
+  const int policy = effective_policy(n, pod, &exclusive);
+  if (policy < 0) {
+    *reason = KE_REASON_NUMA_POLICY_CONFLICT;
+    return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+  }
   const int code = numa_filter_amplified(n, pod, reason);
   if (code != KE_CODE_SUCCESS) return code;
-  const int policy = n->node.numa_topology_policy; /* mergeTopologyPolicy: the pod sets none */
   if (policy == KE_NUMA_POLICY_NONE) return KE_CODE_SUCCESS;
   if (n->n_zone == 0) { /* FilterByNUMANode  topology_hint.go:31-41 */
     *reason = KE_REASON_NUMA_MISSING_RESOURCES;
     return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
   }
   uint32_t aff;
-  return numa_admit(c, n, pod, policy, &aff, reason);
+  return numa_admit(c, n, pod, policy, exclusive, &aff, reason);
 }
 
 /* filterAmplifiedCPUs  plugin.go:408-442 */
@@ -755,13 +770,28 @@ static numa_hint merge_permutation(uint32_t all, const numa_hint* perm, int n) {
   return h;
 }
 
+/* checkExclusivePolicy (policy.go:73-93); status[id] = NUMANodeSharedStatus of NUMA id `id` */
+static int exclusive_ok(uint32_t mask, int exclusive, const uint8_t* status) {
+  if (!mask) return 0;
+  if (exclusive == KE_NUMA_EXCLUSIVE_REQUIRED) {
+    if (__builtin_popcount(mask) > 1) {
+      for (int b = 0; b < KE_MAX_NUMA; b++)
+        if ((mask >> b & 1u) && status[b] == KE_NUMA_STATUS_SINGLE) return 0;
+    } else if (status[__builtin_ctz(mask)] == KE_NUMA_STATUS_SHARED) {
+      return 0;
+    }
+  }
+  return 1;
+}
+
 static int narrower(uint32_t a, uint32_t b) { /* bitmask.IsNarrowerThan */
   const int ca = __builtin_popcount(a), cb = __builtin_popcount(b);
   return ca == cb ? a < b : ca < cb;
 }
 
 /* mergeFilteredHints (policy.go:198-260) + iterateAllProviderTopologyHints (:282-299) */
-static numa_hint merge_filtered(uint32_t all, numa_hint* const* lists, const int* lens, int nl) {
+static numa_hint merge_filtered(uint32_t all, numa_hint* const* lists, const int* lens, int nl, int exclusive,
+                                const uint8_t* status) {
   numa_hint best = {all, 0, 0, 0};
   int idx[4] = {0, 0, 0, 0};
   for (int i = 0; i < nl; i++)
@@ -771,7 +801,7 @@ static numa_hint merge_filtered(uint32_t all, numa_hint* const* lists, const int
     for (int i = 0; i < nl; i++) perm[i] = lists[i][idx[i]];
     numa_hint m = merge_permutation(all, perm, nl);
     if (__builtin_popcount(m.mask) != 0) {
-      /* checkExclusivePolicy: the pod sets no NUMA exclusive policy -> always satisfied */
+      if (!exclusive_ok(m.mask, exclusive, status)) m.preferred = 0;
       for (int i = 0; i < nl; i++)
         if (perm[i].mask && perm[i].mask == m.mask) m.score += perm[i].score;
       if (m.preferred && !best.preferred) {
@@ -796,9 +826,9 @@ static numa_hint merge_filtered(uint32_t all, numa_hint* const* lists, const int
  * already reduced by filterSingleNumaHints); `reasons` = filterProvidersHints reported an empty list.
  * Returns admit; *best = the merged hint (mask 0 = nil affinity). */
 static int policy_merge(int policy, uint32_t all, numa_hint* const* lists, const int* lens, int nl, int reasons,
-                        numa_hint* best) {
+                        int exclusive, const uint8_t* status, numa_hint* best) {
   if (policy == KE_NUMA_POLICY_BEST_EFFORT) {
-    *best = merge_filtered(all, lists, lens, nl);
+    *best = merge_filtered(all, lists, lens, nl, exclusive, status);
     if (best->unsatisfied) *best = (numa_hint){all, 0, 0, 0};
     return 1;
   }
@@ -807,14 +837,14 @@ static int policy_merge(int policy, uint32_t all, numa_hint* const* lists, const
       *best = (numa_hint){all, 0, 0, 0};
       return 0;
     }
-    *best = merge_filtered(all, lists, lens, nl);
+    *best = merge_filtered(all, lists, lens, nl, exclusive, status);
     return best->preferred;
   }
   if (reasons) { /* SingleNUMANode */
     *best = (numa_hint){0, 0, 0, 0};
     return 0;
   }
-  *best = merge_filtered(all, lists, lens, nl);
+  *best = merge_filtered(all, lists, lens, nl, exclusive, status);
   if (best->mask == all) *best = (numa_hint){0, best->preferred, 0, 0};
   return best->preferred;
 }
@@ -861,7 +891,8 @@ int or_topology_merge(int32_t policy, uint32_t all, int32_t n_lists, const int32
     nl = 1;
   }
   numa_hint best;
-  const int admit = policy_merge(policy, all, lists, ln, nl, reasons, &best);
+  static const uint8_t idle[KE_MAX_NUMA] = {0};
+  const int admit = policy_merge(policy, all, lists, ln, nl, reasons, KE_NUMA_EXCLUSIVE_NONE, idle, &best);
   *out_mask = best.mask;
   *out_preferred = (uint8_t)best.preferred;
   *out_unsatisfied = (uint8_t)best.unsatisfied;
@@ -872,11 +903,16 @@ int or_topology_merge(int32_t policy, uint32_t all, int32_t n_lists, const int32
 /* topologymanager Admit for the pod on the node (manager.go:64-129 with the NodeNUMAResource hint
  * provider; DeviceShare provides no hints for a pod without device requests).  Returns the status
  * code, *affinity (0 = nil) on success. */
-static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod, int policy, uint32_t* affinity,
-                      int* reason) {
+static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod, int policy, int exclusive,
+                      uint32_t* affinity, int* reason) {
   numa_view v;
   uint32_t all = 0;
   for (int z = 0; z < nd->n_zone; z++) all |= 1u << nd->zone[z].id;
+  /* GetAllNUMANodeStatus(len(numaNodes)): the statuses of NUMA ids 0..n-1 (a zone id >= n would
+   * index past the reference's slice; read as idle here) */
+  uint8_t status[KE_MAX_NUMA] = {0};
+  for (int z = 0; z < nd->n_zone; z++)
+    if (nd->zone[z].id < nd->n_zone) status[nd->zone[z].id] = nd->zone[z].numa_status;
   if (numa_view_build(nd, &v) != 0) { /* GetPodTopologyHints error -> reasons -> Unschedulable */
     *reason = KE_REASON_NUMA_HINT_UNALIGNED;
     return KE_CODE_UNSCHEDULABLE;
@@ -923,7 +959,7 @@ static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod,
   lists[nl] = filt[nl];
   lens[nl++] = 1;
   numa_hint best;
-  const int admit = policy_merge(policy, all, lists, lens, nl, reasons, &best);
+  const int admit = policy_merge(policy, all, lists, lens, nl, reasons, exclusive, status, &best);
   if (!admit) {
     *reason = KE_REASON_NUMA_HINT_UNALIGNED;
     return KE_CODE_UNSCHEDULABLE;
@@ -978,6 +1014,13 @@ int or_numa_hints(const or_cluster* c, int32_t node, const ke_pod* pod, int32_t 
   return 0;
 }
 
+/* checkExclusivePolicy golden-vector entry point: status[i] for NUMA id i, n ids */
+int or_numa_exclusive_ok(uint32_t mask, int32_t exclusive, const uint8_t* status, int32_t n) {
+  uint8_t st[KE_MAX_NUMA] = {0};
+  for (int i = 0; i < n && i < KE_MAX_NUMA; i++) st[i] = status[i];
+  return exclusive_ok(mask, exclusive, st);
+}
+
 /* the pod's NUMA allocation on its affinity (resourceManager.Allocate -> allocateResourcesByHint) */
 static int numa_allocation(const or_node* nd, const ke_pod* pod, uint32_t affinity, numa_view* v,
                            int64_t out[KE_MAX_NUMA][KE_NRES]) {
@@ -991,12 +1034,14 @@ static int numa_allocation(const or_node* nd, const ke_pod* pod, uint32_t affini
 int64_t or_numa_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
   const or_node* n = &c->nodes[node];
   if (pod_requests_zero(pod)) return 0; /* state.skip */
-  const int policy = n->node.numa_topology_policy;
+  int exclusive;
+  const int policy = effective_policy(n, pod, &exclusive);
+  if (policy < 0) return 0;
   if (policy != KE_NUMA_POLICY_NONE) {
     /* the affinity the Filter's Admit stored, the allocation on it, calculateAllocatableAndRequested */
     uint32_t aff = 0;
     int reason;
-    if (n->n_zone == 0 || numa_admit(c, n, pod, policy, &aff, &reason) != KE_CODE_SUCCESS) return 0;
+    if (n->n_zone == 0 || numa_admit(c, n, pod, policy, exclusive, &aff, &reason) != KE_CODE_SUCCESS) return 0;
     numa_view v;
     int64_t out[KE_MAX_NUMA][KE_NRES];
     if (!numa_allocation(n, pod, aff, &v, out)) return 0;
@@ -1513,6 +1558,7 @@ int or_node_numa_set(or_cluster* c, int32_t node, int32_t n, const ke_numa_zone*
     if (zones[i].cpuset_cpus > 0 && !(zones[i].has_allocated & KE_NUMA_ALLOC_ENTRY)) return KE_ERR_INVALID;
     if (zones[i].has_allocated > 7 || (zones[i].has_allocated && !(zones[i].has_allocated & KE_NUMA_ALLOC_ENTRY)))
       return KE_ERR_INVALID;
+    if (zones[i].numa_status > KE_NUMA_STATUS_SHARED) return KE_ERR_INVALID;
   }
   c->nodes[node].n_zone = n;
   if (n) memcpy(c->nodes[node].zone, zones, sizeof(ke_numa_zone) * (size_t)n);
@@ -1523,10 +1569,12 @@ int or_node_numa_set(or_cluster* c, int32_t node, int32_t n, const ke_numa_zone*
  * NodeAllocation.addPodAllocation (node_allocation.go:111-156) adds the NUMA allocation. */
 static void or_numa_reserve(or_cluster* c, const ke_pod* pod, int32_t node, int64_t* out16) {
   or_node* n = &c->nodes[node];
-  if (pod_requests_zero(pod) || n->node.numa_topology_policy == KE_NUMA_POLICY_NONE || n->n_zone == 0) return;
+  int exclusive;
+  const int policy = effective_policy(n, pod, &exclusive);
+  if (pod_requests_zero(pod) || policy <= KE_NUMA_POLICY_NONE || n->n_zone == 0) return;
   uint32_t aff = 0;
   int reason;
-  if (numa_admit(c, n, pod, n->node.numa_topology_policy, &aff, &reason) != KE_CODE_SUCCESS) return;
+  if (numa_admit(c, n, pod, policy, exclusive, &aff, &reason) != KE_CODE_SUCCESS) return;
   numa_view v;
   int64_t out[KE_MAX_NUMA][KE_NRES];
   if (!numa_allocation(n, pod, aff, &v, out)) return;
@@ -1719,9 +1767,15 @@ static int check_supported(const or_cluster* c, int32_t n_pods, const ke_pod* po
   int ds = 0, numa = 0;
   for (int p = 0; p < n_pods; p++) {
     if (pod_unsupported(&pods[p])) return KE_ERR_UNSUPPORTED;
+    if (pods[p].numa_topology_policy < 0 || pods[p].numa_topology_policy > KE_NUMA_POLICY_SINGLE_NUMA_NODE ||
+        pods[p].numa_exclusive < 0 || pods[p].numa_exclusive > KE_NUMA_EXCLUSIVE_REQUIRED)
+      return KE_ERR_INVALID;
     ds_pod d;
     ds_prepare_pod(&pods[p], &d);
-    if (!d.skip && d.status == KE_CODE_SUCCESS) ds = 1;
+    if (!d.skip && d.status == KE_CODE_SUCCESS) {
+      ds = 1;
+      if (pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE) numa = 1;
+    }
   }
   for (int i = 0; i < c->n; i++) {
     if (node_unsupported(&c->nodes[i].node)) return KE_ERR_UNSUPPORTED;

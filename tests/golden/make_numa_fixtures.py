@@ -204,6 +204,25 @@ for name, lines, res, ratio, alloc, cpusets, want in [
                   "cpusets": cpusets, "want": {"available": want}})
 
 
+# Test_checkExclusivePolicy (frameworkext/topologymanager/policy_test.go:1278-1400)
+POLICY_T = "pkg/scheduler/frameworkext/topologymanager/policy_test.go"
+for name, line, bits, excl, status, want in [
+    ("preferred policy 1", 1291, [0], "Preferred", ["shared", "shared"], True),
+    ("preferred policy 2", 1300, [0, 1], "Preferred", ["shared", "shared"], True),
+    ("preferred policy 3", 1309, [0], "Preferred", ["idle", "single"], True),
+    ("preferred policy 4", 1318, [0, 1], "Preferred", ["idle", "single"], True),
+    ("required policy 1", 1327, [0], "Required", ["idle", "single"], True),
+    ("required policy 2", 1336, [0], "Required", ["shared", "single"], False),
+    ("required policy 3", 1345, [0], "Required", ["shared", "shared"], False),
+    ("required policy 4", 1354, [0], "Required", ["single", "shared"], True),
+    ("required policy 5", 1363, [0, 1], "Required", ["shared", "single"], False),
+    ("required policy 6", 1372, [0, 1], "Required", ["shared", "idle"], True),
+    ("required policy 7", 1381, [0, 1], "Required", ["shared", "shared"], True),
+]:
+    cases.append({"name": f"checkExclusivePolicy {name}", "source": f"{POLICY_T}:{line}", "op": "exclusive",
+                  "bits": bits, "exclusive": excl, "status": status, "want": {"ok": want}})
+
+
 def main():
     with open(os.path.join(HERE, "numa_policy.json"), "w") as f:
         json.dump({"source": "haoyann/koordinator topologymanager / nodenumaresource tests, transcribed by "

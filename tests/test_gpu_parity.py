@@ -345,9 +345,11 @@ def test_deviceshare_cache_delete_and_unhealthy(gpu):
 
 
 # ---- NUMA topology policies (non-cpuset pods) ------------------------------------------------------
-def numa_both(n_nodes, seed, zone_counts=(1, 2, 4, 8), batch=64, hint_most=False, most=False):
+def numa_both(n_nodes, seed, zone_counts=(1, 2, 4, 8), batch=64, hint_most=False, most=False, status_fraction=0.0,
+              policy_weights=(0.1, 0.3, 0.3, 0.3)):
     cl = synth.make_cluster(n_nodes, synth.BASE_SEED + seed, amplified_fraction=0.3)
-    zs = synth.make_numa(cl, synth.BASE_SEED + seed + 50, zone_counts=zone_counts)
+    zs = synth.make_numa(cl, synth.BASE_SEED + seed + 50, zone_counts=zone_counts, status_fraction=status_fraction,
+                         policy_weights=policy_weights)
     cfg = synth.config(n_nodes, pod_batch=batch)
     if hint_most:
         cfg.numa.numa_strategy = abi.STRATEGY_MOST_ALLOCATED
@@ -475,3 +477,26 @@ def test_golden_numa_policy_path(gpu, case):
     else:  # the single-zone hints do not fit: the merged hint is {0,1}, split 1.75 / 1.75
         got = {str(z): alloc[z].tolist() for z in zones}
         assert got == {z: cases.quantity_vec(rl) for z, rl in case["want"]["alloc"].items()}, case["source"]
+
+
+@pytest.mark.parametrize("nodes", ["node-policies", "no-node-policies"])
+def test_numa_pod_policy_eval_parity(gpu, nodes):
+    """Pods with their own numa-topology-spec: conflicts with the node's policy, the merged policy,
+    SingleNUMANodeExclusive against zones already single / shared."""
+    w = (0.1, 0.3, 0.3, 0.3) if nodes == "node-policies" else (1, 0, 0, 0)
+    ev, o = numa_both(400, 98, status_fraction=0.4, policy_weights=w)
+    pods = synth.make_numa_pods(48, synth.BASE_SEED + 99, policy_fraction=0.6)
+    a, b = ev.eval(pods, synth.T0), o.eval(pods, synth.T0)
+    assert_eval_equal(a, b)
+    if nodes == "node-policies":
+        assert np.any(a["reason"] == abi.REASON_NUMA_POLICY_CONFLICT)
+
+
+def test_numa_pod_policy_schedule_parity(gpu):
+    ev, o = numa_both(300, 100, zone_counts=(1, 2, 4), status_fraction=0.4)
+    pods = synth.make_numa_pods(256, synth.BASE_SEED + 101, policy_fraction=0.5)
+    c1, s1 = ev.schedule(pods, synth.T0)
+    c0, s0 = o.schedule(pods, synth.T0)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5]
+    assert np.array_equal(s1, s0)
+    assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)

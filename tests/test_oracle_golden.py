@@ -126,7 +126,19 @@ def test_numa_policy_merge(case):
     assert (mask, pref, admit) == (_mask(want["bits"]), want["preferred"], want["admit"]), case["source"]
 
 
-NUMA_PATH = [c for c in NUMA_POLICY if c["op"] != "merge"]
+NUMA_PATH = [c for c in NUMA_POLICY if c["op"] not in ("merge", "exclusive")]
+NUMA_EXCL = [c for c in NUMA_POLICY if c["op"] == "exclusive"]
+
+
+@pytest.mark.parametrize("case", NUMA_EXCL, ids=[c["name"] for c in NUMA_EXCL])
+def test_numa_exclusive_policy(case):
+    import numpy as np
+    from oracle.binding import load
+    from koordinator_amd import abi
+    st = np.array([{"idle": 0, "single": 1, "shared": 2}[x] for x in case["status"]], np.uint8)
+    excl = {"Preferred": abi.NUMA_EXCLUSIVE_PREFERRED, "Required": abi.NUMA_EXCLUSIVE_REQUIRED}[case["exclusive"]]
+    got = load().or_numa_exclusive_ok(sum(1 << b for b in case["bits"]), excl, abi.ptr(st), len(st))
+    assert bool(got) == case["want"]["ok"], case["source"]
 
 
 @pytest.mark.parametrize("case", NUMA_PATH, ids=[f'{c["op"]}: {c["name"]}' for c in NUMA_PATH])
