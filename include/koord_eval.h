@@ -457,6 +457,9 @@ int ke_last_kernel_stats(ke_ctx* ctx, double* eval_ms, double* select_ms, double
 int ke_last_resolve_split(ke_ctx* ctx, double* prologue_ms, double* replay_ms);
 /* Finer split (6 entries, ms per batch): init, candidate copy, slot hashing, slot lookup, row
  * gather, sequential replay. */
+/* BestEffort (pod, node) pairs the last ke_eval / ke_schedule evaluated in the compacted full-merge
+ * pass (no preferred merged hint). */
+int ke_debug_numa_deferred(ke_ctx* ctx, int64_t* n);
 int ke_debug_resolve_phases(ke_ctx* ctx, double* phases6);
 /* Launch the batch eval kernel `iters` times back to back over the current node SoA for `n_pods`
  * (<= 64) pods and return the HIP-event average milliseconds per launch (roofline measurement). */

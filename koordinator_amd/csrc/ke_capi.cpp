@@ -390,6 +390,12 @@ int ke_last_resolve_split(ke_ctx* ctx, double* prologue_ms, double* replay_ms) {
   return KE_OK;
 }
 
+int ke_debug_numa_deferred(ke_ctx* ctx, int64_t* n) {
+  if (!ctx || !n) return fail(KE_ERR_INVALID, "ke_debug_numa_deferred arguments");
+  *n = ctx->c.kstat_numa_deferred;
+  return KE_OK;
+}
+
 int ke_debug_resolve_phases(ke_ctx* ctx, double* phases6) {
   if (!ctx || !phases6) return fail(KE_ERR_INVALID, "ke_debug_resolve_phases arguments");
   for (int i = 0; i < 6; i++) phases6[i] = ctx->c.kstat_resolve_phase_ms[i];

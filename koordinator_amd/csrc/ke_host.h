@@ -56,6 +56,7 @@ struct Context {
   double kstat_eval_ms = 0, kstat_select_ms = 0, kstat_resolve_ms = 0;
   double kstat_resolve_prologue_ms = 0, kstat_resolve_loop_ms = 0;
   double kstat_resolve_phase_ms[6] = {0, 0, 0, 0, 0, 0};
+  int64_t kstat_numa_deferred = 0;  // BestEffort pairs the last ke_eval / ke_schedule left to k_numa_fallback
   int32_t kstat_samples = 0;
 };
 

@@ -427,11 +427,61 @@ __device__ __forceinline__ int64_t div_upto8(int64_t q, int d) {
   }
 }
 
+// the resources tryBestToDistributeEvenly splits: keys of some zone's totalAvailable, requested
+__device__ __forceinline__ bool numa_checked(const NumaNode& v, const DevPod& p, int r) {
+  return ((v.ch[r] | v.ak[r]) & v.zm) != 0 && p.req[r] != 0;
+}
+
+// Necessary condition of a successful split (allocateRes never takes more than a zone has): every
+// checked request fits in the summed availability of the mask's zones.
+__device__ __forceinline__ bool numa_sum_fits(const NumaNode& v, uint32_t m, const DevPod& p) {
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    if (!numa_checked(v, p, r)) continue;
+    int64_t sum = 0;
+#pragma unroll
+    for (int z = 0; z < 8; z++) sum += ((m >> z) & 1u) ? v.av[r][z] : 0;
+    if (sum < p.req[r]) return false;
+  }
+  return true;
+}
+
+// Smallest hint size that can pass numa_sum_fits (sum of the largest zones), 9 if none: the masks
+// below it are skipped without changing any hint list.
+__device__ __forceinline__ int numa_min_size(const NumaNode& v, const DevPod& p) {
+  int smin = 1;
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    if (!numa_checked(v, p, r) || p.req[r] <= 0) continue;
+    int64_t sum = 0;
+    uint32_t used = 0;
+    int s = 0;
+    while (sum < p.req[r] && s < 8) {
+      int64_t best = -1;
+      int bz = 0;
+#pragma unroll
+      for (int z = 0; z < 8; z++)
+        if (((v.zm & ~used) >> z & 1u) && v.av[r][z] > best) {
+          best = v.av[r][z];
+          bz = z;
+        }
+      if (best < 0) break;
+      used |= 1u << bz;
+      sum += best;
+      s++;
+    }
+    if (sum < p.req[r]) return 9;
+    smin = max(smin, s);
+  }
+  return smin;
+}
+
 // tryBestToDistributeEvenly over the zones of mask m: true when every requested resource is fully
-// split; OUT: the zones that received a non-zero amount (bit) and the amounts (out[r][id]).
+// split; OUT: per resource the zones that received a non-zero amount and the amounts (out[r][id]).
 template <bool OUT>
 __device__ __forceinline__ bool numa_distribute(const NumaNode& v, uint32_t m, const DevPod& p, uint32_t* got_mask,
                                                 int64_t (&out)[2][8]) {
+  if (!OUT && !numa_sum_fits(v, m, p)) return false;
   const int nb = __popc(m);
   uint32_t bl = 0;  // zone ids of m, ascending, one nibble each
   for (uint32_t mm = m, t = 0; mm; mm &= mm - 1, t++) bl |= (uint32_t)(__ffs(mm) - 1) << (4 * t);
@@ -439,7 +489,7 @@ __device__ __forceinline__ bool numa_distribute(const NumaNode& v, uint32_t m, c
 #pragma unroll
   for (int r = 0; r < 2; r++) {
     if (!OUT && !ok) break;
-    if (((v.ch[r] | v.ak[r]) & v.zm) == 0 || p.req[r] == 0) continue;  // resourceNamesByNUMA x requests
+    if (!numa_checked(v, p, r)) continue;  // resourceNamesByNUMA x requests
     const uint32_t perm = pick8u(v.perm[r], nb - 1);
     int64_t q = p.req[r];
     for (int t = 0; t < nb; t++) {
@@ -583,10 +633,32 @@ __device__ __forceinline__ uint32_t numa_best_effort_fallback(const SoA& s, int6
   return bun ? v.zm : best;
 }
 
+constexpr uint8_t STATUS_DEFERRED = 0xFF;  // BestEffort pair left to k_numa_fallback
+
+// generateResourceHints' resource lists: present[r] = the pod requests r and some zone has the key;
+// lack[r] = numaNodesLackResource (zones without r available)
+__device__ __forceinline__ void numa_present_lack(const NumaNode& v, const DevPod& p, bool (&present)[2],
+                                                  uint32_t (&lack)[2]) {
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    present[r] = p.req[r] != 0 && (v.ch[r] & v.zm) != 0;
+    uint32_t l = 0;
+    if (v.ch[r] & v.zm)
+#pragma unroll
+      for (int z = 0; z < 8; z++)
+        if (((v.zm >> z) & 1u) && (!(((v.ch[r] | v.ak[r]) >> z) & 1u) || v.av[r][z] == 0)) l |= 1u << z;
+    lack[r] = l;
+  }
+}
+
 // FilterByNUMANode + RunNUMATopologyManagerAdmit for a pod whose requests are not all zero, under
-// the merged topology `policy` (node / pod, util.go:58-74).
+// the merged topology `policy` (node / pod, util.go:58-74).  DEFER: a BestEffort pair without a
+// preferred merged hint returns STATUS_DEFERRED instead of running the full merge here (one lane
+// needing it would hold its whole wavefront; k_numa_fallback runs those pairs compacted).
+// FB_AFF: the BestEffort full-merge result was computed by the caller (k_numa_fallback) and is `fb_aff`.
+template <bool DEFER, bool FB_AFF = false>
 __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t nf, int policy, const NumaNode& v,
-                                               const DevPod& p, const KArgs& k) {
+                                               const DevPod& p, const KArgs& k, uint32_t fb_aff = 0) {
   NumaPick o{KE_CODE_SUCCESS, KE_REASON_NONE, 0u};
   const bool excl = (p.flags & PF_NUMA_EXCL_REQ) != 0;
   if (v.zm == 0) {  // topology_hint.go:31-41
@@ -602,16 +674,7 @@ __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t
   const uint32_t all = v.zm;
   bool present[2];
   uint32_t lack[2];
-#pragma unroll
-  for (int r = 0; r < 2; r++) {
-    present[r] = p.req[r] != 0 && (v.ch[r] & all) != 0;
-    uint32_t l = 0;
-    if (v.ch[r] & all)
-#pragma unroll
-      for (int z = 0; z < 8; z++)
-        if (((all >> z) & 1u) && (!(((v.ch[r] | v.ak[r]) >> z) & 1u) || v.av[r][z] == 0)) l |= 1u << z;
-    lack[r] = l;
-  }
+  numa_present_lack(v, p, present, lack);
   const int R = (int)present[0] + (int)present[1];
   int64_t dummy[2][8];
   if (R == 0) {  // no hints: one preferred any-NUMA hint per provider -> merged = all zones
@@ -636,7 +699,7 @@ __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t
   int32_t bsc = 0;
   bool found = false, stop = false;
   const int smax = policy == KE_NUMA_POLICY_SINGLE_NUMA_NODE ? 1 : __popc(all);
-  for (int sz = 1; sz <= smax && !stop; sz++) {
+  for (int sz = numa_min_size(v, p); sz <= smax && !stop; sz++) {
     const bool first0 = minr[0] == 0, first1 = minr[1] == 0;
     for (int e = NUMA_OFF[sz]; e < NUMA_OFF[sz + 1]; e++) {
       const uint32_t m = NUMA_ORDER[e];
@@ -667,7 +730,11 @@ __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t
     o.reason = KE_REASON_NUMA_HINT_UNALIGNED;
     return o;
   }
-  o.aff = numa_best_effort_fallback(s, i, v, p, k, present, lack);
+  if (DEFER) {
+    o.status = STATUS_DEFERRED;
+    return o;
+  }
+  o.aff = FB_AFF ? fb_aff : numa_best_effort_fallback(s, i, v, p, k, present, lack);
   if (!numa_distribute<false>(v, o.aff, p, nullptr, dummy)) {
     o.status = KE_CODE_UNSCHEDULABLE;
     o.reason = KE_REASON_NUMA_INSUFFICIENT_RESOURCES;
@@ -725,9 +792,9 @@ __device__ __forceinline__ void numa_reserve(const SoA& s, int64_t i, uint32_t n
 // `s`/`i` locate the node's DeviceShare state (read only for pods with PF_DS, and only when DS: the
 // batch replay never evaluates a DeviceShare pod — such a pod is alone in its batch).
 // NUMA: some node may carry a NUMA topology policy; `nv` holds node i's zones when its policy is set.
-template <bool DS, bool NUMA>
+template <bool DS, bool NUMA, bool DEFER = false, bool FB_AFF = false>
 __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, const DevPod& p, const KArgs& k,
-                                             const SoA& s, int64_t i, const NumaNode& nv) {
+                                             const SoA& s, int64_t i, const NumaNode& nv, uint32_t fb_aff = 0) {
   EvalOut o;
   o.status = KE_CODE_SUCCESS;
   o.reason = KE_REASON_NONE;
@@ -794,7 +861,12 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
   const bool npol = NUMA && !(p.flags & PF_NUMA_SKIP) && eff_pol != KE_NUMA_POLICY_NONE;
   int32_t npol_score = 0;
   if (npol && o.status == KE_CODE_SUCCESS) {
-    const NumaPick pk = numa_admit(s, i, nf, eff_pol, nv, p, k);
+    const NumaPick pk = numa_admit<DEFER, FB_AFF>(s, i, nf, eff_pol, nv, p, k, fb_aff);
+    if (DEFER && pk.status == STATUS_DEFERRED) {
+      o.status = STATUS_DEFERRED;
+      o.total = -1;
+      return o;
+    }
     if (pk.status != KE_CODE_SUCCESS) {
       o.status = pk.status;
       o.reason = pk.reason;
@@ -885,6 +957,21 @@ __global__ void k_gather_rows(SoA s, Row* __restrict__ rows, int n) {
   rows[i] = r;
 }
 
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v);
+__device__ __forceinline__ int lanes_below(uint64_t m);
+
+// Append `item` to a deferred-pair list (one atomic per wavefront).
+__device__ __forceinline__ void defer_push(bool want, uint64_t item, uint64_t* __restrict__ list, uint32_t* cnt) {
+  const uint64_t bal = __ballot(want);
+  if (!bal) return;
+  const int leader = __ffsll((unsigned long long)bal) - 1;
+  uint32_t base = 0;
+  if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(cnt, (uint32_t)__popcll(bal));
+  base = __shfl(base, leader, 64);
+  const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+  if (want) list[base + below] = item;
+}
+
 // parity mode: full status / score matrices [pod][node]; `total` holds the LoadAware + NUMA part
 // until k_parity_finalize adds the normalized DeviceShare score.  dsmax[p] = 1 + max raw DeviceShare
 // score over the pod's feasible nodes (DefaultNormalizeScore's maxCount).
@@ -893,7 +980,8 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_parity(SoA s, int n_nodes, 
                                                             int n_pods, int pods_per_block, KArgs k,
                                                             uint8_t* status, uint8_t* reason, int16_t* la,
                                                             int16_t* numa, int16_t* ds, int16_t* total,
-                                                            uint32_t* dsmax) {
+                                                            uint32_t* dsmax, uint64_t* defer_list,
+                                                            uint32_t* defer_cnt) {
   const int i = blockIdx.x * EVAL_BLOCK + threadIdx.x;
   const bool live = i < n_nodes;
   NodeRegs n;
@@ -908,8 +996,10 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_parity(SoA s, int n_nodes, 
   const int p1 = min(n_pods, p0 + pods_per_block);
   for (int p = p0; p < p1; p++) {
     uint32_t m = 0;
+    bool deferred = false;
     if (live) {
-      const EvalOut o = eval_pair<true, NUMA>(n, expired, pods[p], k, s, i, nv);
+      const EvalOut o = eval_pair<true, NUMA, NUMA>(n, expired, pods[p], k, s, i, nv);
+      deferred = NUMA && o.status == STATUS_DEFERRED;
       const int64_t o_idx = (int64_t)p * n_nodes + i;
       status[o_idx] = o.status;
       reason[o_idx] = o.reason;
@@ -919,6 +1009,7 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_parity(SoA s, int n_nodes, 
       total[o_idx] = (int16_t)o.total;
       m = o.total >= 0 ? (uint32_t)o.ds + 1 : 0u;
     }
+    if (NUMA) defer_push(deferred, ((uint64_t)p << 32) | (uint32_t)i, defer_list, defer_cnt);
     m = __ockl_wfred_max_u32(m);
     if ((threadIdx.x & 63) == 0 && m) atomicMax(&dsmax[p], m);
   }
@@ -958,7 +1049,8 @@ template <bool DS, bool NUMA>
 __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi, const DevPod* __restrict__ pods,
                                                            const int32_t* __restrict__ batch_base, int batch_pods,
                                                            int pods_per_block, KArgs k, uint16_t* __restrict__ scores,
-                                                           int64_t score_stride, uint16_t* __restrict__ dsraw) {
+                                                           int64_t score_stride, uint16_t* __restrict__ dsraw,
+                                                           uint64_t* __restrict__ defer_list, uint32_t* defer_cnt) {
   const int i = lo + blockIdx.x * EVAL_BLOCK + threadIdx.x;
   if (i >= hi) return;
   NodeRegs n;
@@ -972,9 +1064,152 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
   const int p1 = min(batch_pods, p0 + pods_per_block);
   for (int p = p0; p < p1; p++) {
     const DevPod& pod = pods[base + p];
-    const EvalOut o = eval_pair<DS, NUMA>(n, expired, pod, k, s, i, nv);
+    const EvalOut o = eval_pair<DS, NUMA, NUMA>(n, expired, pod, k, s, i, nv);
     scores[(int64_t)p * score_stride + i] = (uint16_t)(o.total + 1);
+    if (NUMA) defer_push(o.status == STATUS_DEFERRED, ((uint64_t)p << 32) | (uint32_t)i, defer_list, defer_cnt);
     if (DS && (pod.flags & PF_DS)) dsraw[i] = o.total >= 0 ? (uint16_t)(o.ds + 1) : (uint16_t)0;
+  }
+}
+
+// The deferred BestEffort pairs of an eval launch: one wavefront per pair computes mergeFilteredHints
+// over the full provider lists (numa_best_effort_fallback's result), then lane 0 evaluates the pair
+// with it.  Such a pair is never a DeviceShare pod (ke_capi rejects DeviceShare pods on NUMA-policy
+// nodes).  PARITY: write the parity matrices; else the batch score.
+//   1. lanes split the 255 masks: hint lists L_cpu / L_mem (IterateBitMasks order) and hint scores;
+//   2. c* = the smallest popcount of a non-empty merged mask m1 & m2: only merged hints of that size
+//      can end as the best (the first one is narrower than anything before it, larger ones never
+//      replace it), and between equal sizes the rule is "numerically smaller or higher score";
+//   3. 64 rows of L_cpu at a time, each lane lists its row's size-c* merged hints in L_mem order into
+//      LDS; lane 0 folds them in permutation order.
+constexpr int FALLBACK_BLOCKS = 1024;
+template <bool PARITY>
+__global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __restrict__ pods,
+                                                      const int32_t* __restrict__ batch_base, KArgs k,
+                                                      const uint64_t* __restrict__ list, const uint32_t* __restrict__ cnt,
+                                                      uint16_t* __restrict__ scores, int64_t score_stride, int n_nodes,
+                                                      uint8_t* status, uint8_t* reason, int16_t* la, int16_t* numa,
+                                                      int16_t* ds, int16_t* total, uint32_t* dsmax) {
+  __shared__ int32_t s_score[256];     // hint score by mask value
+  __shared__ uint8_t s_list[2][256];   // L_cpu / L_mem masks in order
+  __shared__ uint16_t s_buf[64][256];  // per-row merged hints of size c*: M | k << 8 | unsatisfied << 10
+  __shared__ int32_t s_cnt[64];
+  const int lane = threadIdx.x;
+  const uint32_t n = *cnt;
+  const int base = PARITY ? 0 : *batch_base;
+  for (uint32_t w = blockIdx.x; w < n; w += FALLBACK_BLOCKS) {
+    const uint64_t it = list[w];
+    const int p = (int)(it >> 32);
+    const int64_t i = (int64_t)(uint32_t)it;
+    const DevPod pod = pods[base + p];
+    NumaNode nv;
+    numa_load(s, i, nv);
+    bool present[2];
+    uint32_t lack[2];
+    numa_present_lack(nv, pod, present, lack);
+    // 1. lists and scores
+    int len[2] = {0, 0};
+    int64_t dummy[2][8];
+    for (int c = 0; c < 4; c++) {
+      const int e = c * 64 + lane;
+      const uint32_t m = e < 255 ? NUMA_ORDER[e] : 0u;
+      bool in[2] = {false, false};
+      if (m && !(m & ~nv.zm)) {
+        in[0] = present[0] && !(m & lack[0]);
+        in[1] = present[1] && !(m & lack[1]);
+        if ((in[0] || in[1]) && !numa_distribute<false>(nv, m, pod, nullptr, dummy)) in[0] = in[1] = false;
+        if (in[0] || in[1]) s_score[m] = numa_hint_score(s, i, nv, m, pod, k);
+      }
+#pragma unroll
+      for (int r = 0; r < 2; r++) {
+        const uint64_t bal = __ballot(in[r]);
+        if (in[r]) s_list[r][len[r] + lanes_below(bal)] = (uint8_t)m;
+        len[r] += __popcll(bal);
+      }
+    }
+    __syncthreads();
+    uint32_t aff;
+    if ((present[0] && !len[0]) || (present[1] && !len[1])) {
+      aff = nv.zm;  // filterProvidersHints reasons: unsatisfied -> any NUMA node
+    } else if (!(present[0] && present[1])) {  // one list: the merged hint is the list's hint
+      const int r = present[0] ? 0 : 1;
+      uint32_t best = nv.zm;
+      int32_t bsc = 0;
+      if (lane == 0)
+        for (int j = 0; j < len[r]; j++) {
+          const uint32_t m = s_list[r][j];
+          const int32_t sc = s_score[m];
+          if (narrower(m, best) || (__popc(m) == __popc(best) && sc > bsc)) {
+            best = m;
+            bsc = sc;
+          }
+        }
+      aff = best;
+    } else {
+      // 2. c*
+      int cmin = 9;
+      for (int j = lane; j < len[0]; j += 64) {
+        const uint32_t m1 = s_list[0][j];
+        for (int q = 0; q < len[1]; q++) {
+          const uint32_t mg = m1 & s_list[1][q];
+          if (mg) cmin = min(cmin, __popc(mg));
+        }
+      }
+      const int cs = 9 - (int)wave_max_u32((uint32_t)(9 - cmin));
+      // 3. fold the size-c* merged hints in permutation order
+      uint32_t best = nv.zm;
+      int32_t bsc = 0;
+      bool bun = false;
+      for (int r0 = 0; cs <= 8 && r0 < len[0]; r0 += 64) {
+        int c = 0;
+        if (r0 + lane < len[0]) {
+          const uint32_t m1 = s_list[0][r0 + lane];
+          for (int q = 0; q < len[1]; q++) {
+            const uint32_t m2 = s_list[1][q];
+            const uint32_t mg = m1 & m2;
+            if ((int)__popc(mg) != cs) continue;
+            const uint32_t kk = (uint32_t)(m1 == mg) + (uint32_t)(m2 == mg);
+            const uint32_t un = (int)max(__popc(m1), __popc(m2)) != cs;
+            s_buf[lane][c++] = (uint16_t)(mg | kk << 8 | un << 10);
+          }
+        }
+        s_cnt[lane] = c;
+        __syncthreads();
+        if (lane == 0)
+          for (int t = 0; t < 64; t++)
+            for (int q = 0; q < s_cnt[t]; q++) {
+              const uint32_t e = s_buf[t][q];
+              const uint32_t mg = e & 0xFFu;
+              const int32_t sc = (int32_t)((e >> 8) & 3u) * s_score[mg];
+              if (narrower(mg, best) || (__popc(mg) == __popc(best) && sc > bsc)) {
+                best = mg;
+                bsc = sc;
+                bun = (e >> 10) & 1u;
+              }
+            }
+        __syncthreads();
+      }
+      aff = bun ? nv.zm : best;
+    }
+    if (lane == 0) {
+      NodeRegs nr;
+      load_row(s, i, nr);
+      prepare_row(nr);
+      const bool expired = node_expired(nr, k);
+      const EvalOut o = eval_pair<false, true, false, true>(nr, expired, pod, k, s, i, nv, aff);
+      if (PARITY) {
+        const int64_t o_idx = (int64_t)p * n_nodes + i;
+        status[o_idx] = o.status;
+        reason[o_idx] = o.reason;
+        la[o_idx] = o.la;
+        numa[o_idx] = o.numa;
+        ds[o_idx] = o.ds;
+        total[o_idx] = (int16_t)o.total;
+        if (o.total >= 0) atomicMax(&dsmax[p], (uint32_t)o.ds + 1);
+      } else {
+        scores[(int64_t)p * score_stride + i] = (uint16_t)(o.total + 1);
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -1515,7 +1750,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
           if (!(pod.flags & PF_NUMA_SKIP) && pol != KE_NUMA_POLICY_NONE) {
             NumaNode nv;
             numa_load(s, my_node, nv);
-            const NumaPick pk = numa_admit(s, my_node, mine.flags, pol, nv, pod, k);
+            const NumaPick pk = numa_admit<false>(s, my_node, mine.flags, pol, nv, pod, k);
             numa_reserve(s, my_node, mine.flags, nv, pk.status == KE_CODE_SUCCESS ? pk.aff : 0u, pod, out16);
           } else {
 #pragma unroll
@@ -1613,6 +1848,10 @@ struct DeviceState {
   int64_t* d_numaalloc = nullptr;  // [n_pods][16] per-zone allocation of each pod (ke_schedule)
   int64_t* d_numarows = nullptr;   // staging for NUMA row uploads
   int64_t numa_staging_cap = 0;
+  uint64_t* d_defer = nullptr;     // deferred BestEffort pairs of one eval launch (k_numa_fallback)
+  int64_t defer_cap = 0;           // bytes
+  uint32_t* d_defer_cnt = nullptr; // one counter per batch of a ke_schedule (or the ke_eval launch)
+  int64_t defer_cnt_cap = 0;       // bytes
 };
 
 // Contiguous node range of shard `rank`: 512-aligned chunks (k_select's 16-B loads stay aligned).
@@ -1671,7 +1910,7 @@ void device_destroy(Context* ctx) {
                   d->d_cand,    d->d_cand_cnt, d->d_batch_base, d->d_chosen,     d->d_chosen_score,
                   d->d_stamps,  d->d_parity, d->d_best,       d->d_gath,         d->soa.ds,   d->soa.dsm,
                   d->d_dsraw,   d->d_dsmax,  d->d_devalloc,   d->d_dsrows,       d->soa.nf,   d->soa.nm,
-                  d->d_numaalloc, d->d_numarows};
+                  d->d_numaalloc, d->d_numarows, d->d_defer, d->d_defer_cnt};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (d->stream) (void)hipStreamDestroy(d->stream);
@@ -1898,12 +2137,22 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
   const int ppb = 8;
   if (N > 0) {
     dim3 grid((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((P + ppb - 1) / ppb));
-    if (d->numa_alloc)
+    if (d->numa_alloc) {
+      rc = ensure((void**)&d->d_defer, &d->defer_cap, sizeof(uint64_t) * M);
+      if (rc) return rc;
+      rc = ensure((void**)&d->d_defer_cnt, &d->defer_cnt_cap, sizeof(uint32_t));
+      if (rc) return rc;
+      HIP_OK(hipMemsetAsync(d->d_defer_cnt, 0, sizeof(uint32_t), d->stream));
       hipLaunchKernelGGL(k_eval_parity<true>, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, (int)N, d->d_pods, (int)P,
-                         ppb, k, d_status, d_reason, d_la, d_numa, d_ds, d_total, d_dsmax);
-    else
+                         ppb, k, d_status, d_reason, d_la, d_numa, d_ds, d_total, d_dsmax, d->d_defer, d->d_defer_cnt);
+      HIP_OK(hipGetLastError());
+      hipLaunchKernelGGL(k_numa_fallback<true>, dim3(FALLBACK_BLOCKS), dim3(64), 0, d->stream, d->soa, d->d_pods,
+                         d->d_batch_base, k, d->d_defer, d->d_defer_cnt, d->d_scores, d->capacity, (int)N, d_status,
+                         d_reason, d_la, d_numa, d_ds, d_total, d_dsmax);
+    } else {
       hipLaunchKernelGGL(k_eval_parity<false>, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, (int)N, d->d_pods, (int)P,
-                         ppb, k, d_status, d_reason, d_la, d_numa, d_ds, d_total, d_dsmax);
+                         ppb, k, d_status, d_reason, d_la, d_numa, d_ds, d_total, d_dsmax, nullptr, nullptr);
+    }
     HIP_OK(hipGetLastError());
     dim3 grid2((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)P);
     hipLaunchKernelGGL(k_parity_finalize, grid2, dim3(EVAL_BLOCK), 0, d->stream, (int)N, k, d_ds, d_total, d_dsmax,
@@ -1918,7 +2167,11 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
   if (total) HIP_OK(hipMemcpyAsync(total, d_total, M * 2, hipMemcpyDeviceToHost, d->stream));
   std::vector<uint32_t> bk((size_t)P);
   HIP_OK(hipMemcpyAsync(bk.data(), d->d_best, sizeof(uint32_t) * P, hipMemcpyDeviceToHost, d->stream));
+  uint32_t deferred = 0;
+  if (d->numa_alloc && N > 0)
+    HIP_OK(hipMemcpyAsync(&deferred, d->d_defer_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipStreamSynchronize(d->stream));
+  ctx->kstat_numa_deferred = deferred;
   if (best)
     for (int64_t p = 0; p < P; p++) best[p] = bk[p] ? key_node(bk[p]) + ctx->cfg.global_node_offset : -1;
   return KE_OK;
@@ -1968,6 +2221,13 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   }
   const bool numa = d->numa_alloc;
   if (numa && !d->d_numaalloc) HIP_OK(hipMalloc(&d->d_numaalloc, sizeof(int64_t) * 16 * d->out_cap));
+  if (numa) {  // deferred-pair list of one batch (reused) + a counter per batch
+    rc = ensure((void**)&d->d_defer, &d->defer_cap, sizeof(uint64_t) * MAX_BATCH * d->capacity);
+    if (rc) return rc;
+    rc = ensure((void**)&d->d_defer_cnt, &d->defer_cnt_cap, sizeof(uint32_t) * n_batches);
+    if (rc) return rc;
+    HIP_OK(hipMemsetAsync(d->d_defer_cnt, 0, sizeof(uint32_t) * n_batches, d->stream));
+  }
   const KArgs k = make_kargs(ctx, now);
   const int N = ctx->n_nodes;
   const int ppb = 8;
@@ -2000,8 +2260,13 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
         dim3 grid((unsigned)((hi - lo + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((bp + ppb - 1) / ppb));
         auto eval = ds ? (numa ? k_eval_batch<true, true> : k_eval_batch<true, false>)
                        : (numa ? k_eval_batch<false, true> : k_eval_batch<false, false>);
+        uint32_t* dcnt = numa ? d->d_defer_cnt + b : nullptr;
         hipLaunchKernelGGL(eval, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, lo, hi, d->d_pods, d->d_batch_base, bp,
-                           ppb, k, d->d_scores, d->capacity, d->d_dsraw);
+                           ppb, k, d->d_scores, d->capacity, d->d_dsraw, d->d_defer, dcnt);
+        if (numa && !ds)  // DeviceShare pods never meet a NUMA policy: nothing deferred in their batches
+          hipLaunchKernelGGL(k_numa_fallback<false>, dim3(FALLBACK_BLOCKS), dim3(64), 0, d->stream, d->soa, d->d_pods,
+                             d->d_batch_base, k, d->d_defer, dcnt, d->d_scores, d->capacity, 0, nullptr, nullptr,
+                             nullptr, nullptr, nullptr, nullptr, nullptr);
       }
       if (ds) {  // DefaultNormalizeScore's max over the feasible nodes (all ranks)
         HIP_OK(hipMemsetAsync(d->d_dsmax, 0, sizeof(uint32_t), d->stream));
@@ -2066,6 +2331,9 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                           hipMemcpyDeviceToHost, d->stream));
   }
   std::vector<uint64_t> st((size_t)n_batches + 1), pst(8 * (size_t)n_batches);
+  std::vector<uint32_t> dcnt(numa ? (size_t)n_batches : 0);
+  if (numa)
+    HIP_OK(hipMemcpyAsync(dcnt.data(), d->d_defer_cnt, sizeof(uint32_t) * n_batches, hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipMemcpyAsync(st.data(), d->d_stamps, sizeof(uint64_t) * (n_batches + 1), hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipMemcpyAsync(pst.data(), d->d_stamps + (n_pods + 2), sizeof(uint64_t) * 8 * n_batches,
                         hipMemcpyDeviceToHost, d->stream));
@@ -2096,6 +2364,8 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   ctx->kstat_resolve_prologue_ms = pro / n_batches;
   ctx->kstat_resolve_loop_ms = loop / n_batches;
   for (int i = 0; i < 6; i++) ctx->kstat_resolve_phase_ms[i] = ph[i] * ms_per_tick / n_batches;
+  ctx->kstat_numa_deferred = 0;
+  for (uint32_t c : dcnt) ctx->kstat_numa_deferred += c;
   ctx->kstat_samples = 0;
   ctx->kstat_eval_ms = ctx->kstat_select_ms = ctx->kstat_resolve_ms = 0;
   for (size_t s = 0; s + 3 < ev.size(); s += 4) {
@@ -2137,14 +2407,14 @@ int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t 
   HIP_OK(hipMemsetAsync(d->d_batch_base, 0, sizeof(int32_t), d->stream));
   dim3 grid((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((n_pods + ppb - 1) / ppb));
   hipLaunchKernelGGL((k_eval_batch<false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base, n_pods,
-                     ppb, k, d->d_scores, d->capacity, d->d_dsraw);  // warm
+                     ppb, k, d->d_scores, d->capacity, d->d_dsraw, nullptr, nullptr);  // warm
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   HIP_OK(hipEventRecord(e0, d->stream));
   for (int it = 0; it < iters; it++)
     hipLaunchKernelGGL((k_eval_batch<false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base,
-                       n_pods, ppb, k, d->d_scores, d->capacity, d->d_dsraw);
+                       n_pods, ppb, k, d->d_scores, d->capacity, d->d_dsraw, nullptr, nullptr);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(e1, d->stream));
   HIP_OK(hipEventSynchronize(e1));

@@ -186,6 +186,12 @@ class Evaluator:
     def set_profiling(self, sample_every):
         self._check(self.lib.ke_set_profiling(self.h, sample_every))
 
+    def numa_deferred(self):
+        """BestEffort pairs of the last eval / schedule that needed the compacted full NUMA merge."""
+        n = abi.i64()
+        self._check(self.lib.ke_debug_numa_deferred(self.h, C.byref(n)))
+        return n.value
+
     def kernel_stats(self):
         v = [C.c_double() for _ in range(3)]
         n = abi.i32()
