@@ -57,6 +57,8 @@ def load():
         "or_node_numa_set": (C.c_int, [V, i32, i32, V]),
         "or_numa_distribute": (C.c_int, [V, i32, V, C.c_uint32, V]),
         "or_numa_exclusive_ok": (C.c_int, [C.c_uint32, i32, V, i32]),
+        "or_take_cpus": (C.c_int, [V, i32, i32, V, V, V, i32, i32, i32, i32, V, V]),
+        "or_spread_order": (C.c_int, [V, i32, V, i32, V]),
         "or_numa_hints": (C.c_int, [V, i32, V, i32, V, V, V, V, V]),
         "or_ds_filter": (C.c_int, [V, C.POINTER(abi.Pod), i32, C.POINTER(C.c_int)]),
         "or_ds_score": (i64, [V, C.POINTER(abi.Pod), i32]),

@@ -17,6 +17,7 @@
  * assign cache on every Filter and every Score call, as the Go plugin does.
  */
 #include "oracle.h"
+#include "cpu_accumulator.h"
 
 #include <math.h>
 #include <stdlib.h>
@@ -1012,6 +1013,48 @@ int or_numa_hints(const or_cluster* c, int32_t node, const ke_pod* pod, int32_t 
     }
   }
   return 0;
+}
+
+/* CPU accumulator golden-vector entry point (cpu_accumulator_test.go): cpus[i] = {cpu id, core id,
+ * NUMA node id, socket id}; alloc_ref / alloc_excl per CPU id (-1 = not allocated); preferred may be
+ * NULL.  Returns 0 and `out` (CPU-id bitset) or -1. */
+int or_take_cpus(const int32_t* cpus, int32_t n, int32_t max_ref, const uint64_t* available, const int32_t* alloc_ref,
+                 const int32_t* alloc_excl, int32_t needed, int32_t bind, int32_t excl, int32_t numa_most,
+                 const uint64_t* preferred, uint64_t* out) {
+  static __thread acc_topo t;
+  static __thread acc_alloc al;
+  memset(&t, 0, sizeof t);
+  memset(&al, 0, sizeof al);
+  for (int i = 0; i < n; i++) {
+    const int c = cpus[4 * i];
+    if (c < 0 || c >= ACC_MAX_CPUS) return -2;
+    t.valid[c] = 1;
+    t.core[c] = cpus[4 * i + 1];
+    t.node[c] = cpus[4 * i + 2];
+    t.socket[c] = cpus[4 * i + 3];
+  }
+  acc_topo_finish(&t);
+  for (int c = 0; c < ACC_MAX_CPUS; c++)
+    if (alloc_ref && alloc_ref[c] >= 0) {
+      al.present[c] = 1;
+      al.ref[c] = alloc_ref[c];
+      al.excl[c] = alloc_excl ? alloc_excl[c] : 0;
+    }
+  return acc_take_preferred_cpus(&t, max_ref, available, preferred, &al, needed, bind, excl, numa_most, out);
+}
+
+int or_spread_order(const int32_t* cpus, int32_t n, const uint64_t* available, int32_t numa_most, int32_t* out) {
+  static __thread acc_topo t;
+  memset(&t, 0, sizeof t);
+  for (int i = 0; i < n; i++) {
+    const int c = cpus[4 * i];
+    t.valid[c] = 1;
+    t.core[c] = cpus[4 * i + 1];
+    t.node[c] = cpus[4 * i + 2];
+    t.socket[c] = cpus[4 * i + 3];
+  }
+  acc_topo_finish(&t);
+  return acc_spread_order(&t, available, numa_most, out);
 }
 
 /* checkExclusivePolicy golden-vector entry point: status[i] for NUMA id i, n ids */

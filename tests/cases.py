@@ -214,3 +214,46 @@ def setup_numa_case(handle, case):
 def quantity_vec(rl):
     """{'cpu': q, 'memory': q} -> [cpu milli, memory bytes]"""
     return [model.milli_value(rl.get("cpu", 0)), model.value(rl.get("memory", 0))]
+
+
+# ---- CPU accumulator vectors (cpu_accumulator.json) ---------------------------------------------
+BIND_ID = {"": 0, "None": 0, "FullPCPUs": 1, "SpreadByPCPUs": 2}
+CPU_EXCL_ID = {"": 0, "None": 0, "PCPULevel": 1, "NUMANodeLevel": 2}
+
+
+def test_topology(sockets, nodes_per_socket, cores_per_node, cpus_per_core, core_shift=False):
+    """buildCPUTopologyForTest (cpu_accumulator_test.go:30-57): rows [cpu, core, node, socket]."""
+    rows, node, core, cpu = [], 0, 0, 0
+    for s in range(sockets):
+        for _ in range(nodes_per_socket):
+            for _ in range(cores_per_node):
+                for _ in range(cpus_per_core):
+                    rows.append([cpu, (s << 16 | core) if core_shift else core, node, s])
+                    cpu += 1
+                core += 1
+            node += 1
+    return rows
+
+
+def parse_cpuset(s):
+    """cpuset.MustParse: '0-3,8' -> sorted list"""
+    out = []
+    for part in filter(None, (s or "").split(",")):
+        if "-" in part:
+            a, b = part.split("-")
+            out.extend(range(int(a), int(b) + 1))
+        else:
+            out.append(int(part))
+    return sorted(out)
+
+
+def cpu_bits(cpus):
+    import numpy as np
+    b = np.zeros(4, np.uint64)
+    for c in cpus:
+        b[c >> 6] |= np.uint64(1) << np.uint64(c & 63)
+    return b
+
+
+def bits_cpus(b):
+    return [c for c in range(256) if (int(b[c >> 6]) >> (c & 63)) & 1]

@@ -170,3 +170,62 @@ def test_numa_policy_path(case):
                     p = cases.make_pod({"requests": {key: f"{amount}m" if key == "cpu" else str(amount)}})
                     ok, _ = o.numa_distribute(0, p, 1 << z)
                     assert ok == fits, (case["source"], z, key, amount)
+
+
+# ---- CPU accumulator ---------------------------------------------------------------------------
+CPU_ACC = cases.load("cpu_accumulator.json")
+
+
+def _take(rows, max_ref, available, ref, excl_arr, needed, bind, excl, most, preferred):
+    import numpy as np
+    from oracle.binding import load
+    from koordinator_amd import abi
+    cpus = np.ascontiguousarray(rows, np.int32).ravel()
+    out = np.zeros(4, np.uint64)
+    pref = None if preferred is None else cases.cpu_bits(preferred)
+    rc = load().or_take_cpus(abi.ptr(cpus), len(rows), max_ref, abi.ptr(cases.cpu_bits(available)), abi.ptr(ref),
+                             abi.ptr(excl_arr), needed, bind, excl, most, None if pref is None else abi.ptr(pref),
+                             abi.ptr(out))
+    return rc, cases.bits_cpus(out)
+
+
+@pytest.mark.parametrize("case", CPU_ACC, ids=[c["name"] for c in CPU_ACC])
+def test_cpu_accumulator(case):
+    import numpy as np
+    rows = cases.test_topology(*case["topology"], core_shift=case.get("core_shift", False))
+    all_cpus = [r[0] for r in rows]
+    most = 1 if case["strategy"] == "MostAllocated" else 0
+    if case["op"] == "spread":
+        from oracle.binding import load
+        from koordinator_amd import abi
+        out = np.zeros(256, np.int32)
+        cpus = np.ascontiguousarray(rows, np.int32).ravel()
+        n = load().or_spread_order(abi.ptr(cpus), len(rows), abi.ptr(cases.cpu_bits(all_cpus)), most, abi.ptr(out))
+        assert out[:n].tolist() == case["want"], case["source"]
+        return
+    if case["op"] == "take":
+        allocated = cases.parse_cpuset(case["allocated"])
+        ref = np.full(256, -1, np.int32)
+        excl_arr = np.zeros(256, np.int32)
+        for c in allocated:
+            ref[c] = 0
+            excl_arr[c] = cases.CPU_EXCL_ID[case["alloc_excl"]]
+        available = [c for c in all_cpus if c not in allocated]
+        pref = None if case["preferred"] is None else cases.parse_cpuset(case["preferred"])
+        rc, got = _take(rows, case["max_ref"], available, ref, excl_arr, case["needed"], cases.BIND_ID[case["bind"]],
+                        cases.CPU_EXCL_ID[case["excl"]], most, pref)
+        assert rc == 0 and got == cases.parse_cpuset(case["want"]), (case["source"], got)
+        return
+    # sequence: NodeAllocation.getAvailableCPUs / addCPUs(PCPULevel) between the pods
+    ref = np.zeros(256, np.int32)
+    for needed, bind, want in case["steps"]:
+        available = [c for c in all_cpus if ref[c] < case["max_ref"]]
+        alloc_ref = np.where(ref > 0, ref, -1).astype(np.int32)
+        excl_arr = np.where(ref > 0, 1, 0).astype(np.int32)
+        rc, got = _take(rows, case["max_ref"], available, alloc_ref, excl_arr, needed, cases.BIND_ID[bind], 0, most,
+                        None)
+        assert rc == 0 and got == cases.parse_cpuset(want), (case["source"], needed, got)
+        for c in got:
+            ref[c] += 1
+    if "final_available" in case:
+        assert [c for c in all_cpus if ref[c] < case["max_ref"]] == cases.parse_cpuset(case["final_available"])
