@@ -153,7 +153,44 @@ typedef struct ke_numa_args {
   int32_t strategy;         /* KE_STRATEGY_*                                       */
   int32_t numa_strategy;    /* NUMAScoringStrategy.Type (KE_STRATEGY_*); its weights are the node-level
                                ScoringStrategy.Resources (scoring.go:37-52, plugin.go:121-126) */
+  int32_t default_cpu_bind_policy; /* DefaultCPUBindPolicy (KE_CPU_BIND_*, v1beta3 default FullPCPUs) */
+  int32_t pad;
 } ke_numa_args;
+
+/* ---- cpuset binding (nodenumaresource cpu accumulator) ----------------------------------------- */
+#define KE_CPU_BIND_UNSET 0 /* schedulingconfig.CPUBindPolicy: "" */
+#define KE_CPU_BIND_DEFAULT 1
+#define KE_CPU_BIND_FULL_PCPUS 2
+#define KE_CPU_BIND_SPREAD_BY_PCPUS 3
+#define KE_CPU_BIND_CONSTRAINED_BURST 4
+#define KE_CPU_EXCL_NONE 0 /* CPUExclusivePolicy */
+#define KE_CPU_EXCL_PCPU_LEVEL 1
+#define KE_CPU_EXCL_NUMA_NODE_LEVEL 2
+#define KE_NODE_CPU_BIND_NONE 0 /* node label / kubelet cpu manager policy (numa_aware.go:354-365) */
+#define KE_NODE_CPU_BIND_FULL_PCPUS_ONLY 1
+#define KE_NODE_CPU_BIND_SPREAD_BY_PCPUS 2
+#define KE_NUMA_ALLOCATE_DEFAULT 0 /* node label node.koordinator.sh/numa-allocate-strategy */
+#define KE_NUMA_ALLOCATE_MOST 1
+#define KE_NUMA_ALLOCATE_LEAST 2
+#define KE_MAX_CPUS 256 /* CPU ids 0..255 per node */
+#define KE_REASON_NUMA_INVALID_REQUESTED_CPUS 23 /* "the requested CPUs must be integer" (plugin.go:296-298, util.go:131-134) */
+#define KE_REASON_NUMA_CPU_BIND_POLICY_CONFLICT 24 /* ErrCPUBindPolicyConflict (plugin.go:365-367) */
+#define KE_REASON_NUMA_SMT_ALIGNMENT 25 /* ErrSMTAlignmentError (plugin.go:369-373) */
+#define KE_REASON_NUMA_INSUFFICIENT_CPUS 26 /* allocateCPUSet: "not enough cpus available to satisfy request" */
+
+/* One logical CPU of a node: CPUTopology.CPUDetails (cpu_topology.go:24-105, built from the NRT's
+ * CPU topology, topology_options.go:90-164) + NodeAllocation.allocatedCPUs (node_allocation.go:33-41)
+ * + TopologyOptions.ReservedCPUs. */
+typedef struct ke_cpu {
+  int32_t cpu_id;      /* 0 .. KE_MAX_CPUS-1 */
+  int32_t core_id;     /* as the topology holds it (socket<<16 | core for NRT topologies) */
+  int32_t numa_id;     /* NUMA node id */
+  int32_t socket_id;
+  int32_t ref_count;   /* allocatedCPUs[cpu].RefCount, 0 = not allocated */
+  uint8_t exclusive;   /* allocatedCPUs[cpu].ExclusivePolicy (KE_CPU_EXCL_*) */
+  uint8_t reserved;    /* in TopologyOptions.ReservedCPUs */
+  uint8_t pad[2];
+} ke_cpu; /* 24 bytes */
 
 /* ---- NUMA topology (nodenumaresource + frameworkext/topologymanager) --------------------------- */
 /* NUMA topology policies (apis/extension/numa_aware.go): node label / NRT kubelet topology-manager policy */
@@ -275,13 +312,14 @@ typedef struct ke_node {
   double nrt_cpu_amplification_ratio;
   int32_t custom_agg_type;                       /* KE_AGG_*           */
   int32_t numa_topology_policy;    /* KE_NUMA_POLICY_*: getNUMATopologyPolicy (label, else NRT policy) */
-  int32_t cpu_bind_policy;         /* 0 = None; non-zero unsupported in ABI v1 */
+  int32_t cpu_bind_policy;         /* KE_NODE_CPU_BIND_*: GetNodeCPUBindPolicy (label, else kubelet policy) */
   uint8_t has_custom_thresholds;   /* annotation present and valid JSON  */
   uint8_t custom_thresholds_error; /* annotation present but failed to unmarshal (helper.go:110) */
   uint8_t has_custom_agg;          /* AggregatedUsage != nil in the annotation */
   uint8_t amplification_error;     /* ratio annotation failed to unmarshal (plugin.go:421) */
   uint8_t cpu_topology_invalid;    /* TopologyOptions.CPUTopology set but !IsValid() (resource_manager.go:502-504) */
-  uint8_t pad[7];
+  uint8_t numa_allocate_strategy;  /* KE_NUMA_ALLOCATE_* (label overriding the args' NUMA allocate strategy) */
+  uint8_t pad[6];
 } ke_node;
 
 /* One AggregatedUsage entry of NodeMetric.Status.NodeMetric.AggregatedNodeUsages. */
@@ -329,12 +367,17 @@ typedef struct ke_pod {
   uint8_t has_scheduled;
   uint8_t has_initialized;
   uint8_t is_terminated;
-  uint8_t has_resource_spec;          /* cpuset annotations: unsupported in ABI v1 */
+  uint8_t has_resource_spec;          /* ResourceSpec annotation that failed to unmarshal (PreFilter Error) */
   uint8_t has_other_requests;         /* PodRequests has a non-zero resource outside KE_RES_* */
   uint8_t has_unsupported_device_requests; /* Huawei NPU / Hygon DCU device resources: unsupported */
   int64_t device_requests[KE_PDR_COUNT]; /* PodRequests of the device resources (Value()), 0 = absent */
   int32_t numa_topology_policy; /* NUMATopologySpec annotation: KE_NUMA_POLICY_* (NONE = unset) */
   int32_t numa_exclusive;       /* NUMATopologySpec.SingleNUMANodeExclusive: KE_NUMA_EXCLUSIVE_* */
+  /* ResourceSpec annotation (apis/extension/resource.go): KE_CPU_BIND_* / KE_CPU_EXCL_* */
+  int32_t cpu_bind_required;
+  int32_t cpu_bind_preferred;
+  int32_t cpu_exclusive;
+  int32_t pad2;
 } ke_pod;
 
 /* One candidate of a pod's speculative top-k list (device order: best first). */
@@ -351,7 +394,7 @@ void ke_destroy(ke_ctx* ctx);
 const char* ke_last_error(void);
 int ke_abi_version(void);
 /* sizeof() of ke_config, ke_node, ke_node_metric, ke_pod_metric, ke_aggregated_usage, ke_pod,
- * ke_resource_map, ke_loadaware_args, ke_numa_args, ke_deviceshare_args, ke_device, ke_numa_zone (in
+ * ke_resource_map, ke_loadaware_args, ke_numa_args, ke_deviceshare_args, ke_device, ke_numa_zone, ke_cpu (in
  * that order) for binding-layout checks. */
 int ke_abi_struct_sizes(int32_t* sizes, int32_t n);
 /* 1 if this build has a usable HIP device and its gfx950 kernels loaded, else 0. */
@@ -393,6 +436,14 @@ int ke_node_devices_delete(ke_ctx* ctx, int32_t node);
 /* NodeResourceTopology informer + resource manager state of `node`: its NUMA zones (n <= KE_MAX_NUMA,
  * n = 0: no NUMA resources).  Read when the node's NUMA topology policy is not None. */
 int ke_node_numa_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_numa_zone* zones);
+/* The node's CPU topology and cpuset allocation state (TopologyOptions.CPUTopology + ReservedCPUs +
+ * MaxRefCount, NodeAllocation.allocatedCPUs).  n = 0 clears it (no CPU topology).  With a CPU table the
+ * allocated-CPU count of the amplified-CPU filter / score and the zones' cpuset counts are derived from
+ * it (ke_node.cpuset_allocated_cpus and ke_numa_zone.cpuset_cpus are then ignored). */
+int ke_node_cpus_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_cpu* cpus, int32_t max_ref_count);
+/* The cpuset each pod of the last ke_schedule received (NodeNUMAResource Reserve -> PreBind
+ * resource-status annotation): out[pod][4] = a 256-bit CPU-id set, all zero without one. */
+int ke_last_cpusets(ke_ctx* ctx, int32_t n, uint64_t* out);
 /* The NUMA allocation each pod of the last ke_schedule received on its node (NodeNUMAResource Reserve
  * -> resourceManager.Update, resource_manager.go:194-258 / node_allocation.go:111-156): out[pod][2*id
  * + r] for NUMA id and resource r (cpu milli, memory), all zero for a pod without one.  The context

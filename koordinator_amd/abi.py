@@ -33,6 +33,12 @@ REASON_NUMA_INSUFFICIENT_RESOURCES = 22
 NUMA_POLICY_NONE, NUMA_POLICY_BEST_EFFORT, NUMA_POLICY_RESTRICTED, NUMA_POLICY_SINGLE_NUMA_NODE = 0, 1, 2, 3
 NUMA_ALLOC_ENTRY, NUMA_ALLOC_CPU, NUMA_ALLOC_MEMORY = 1, 2, 4  # ke_numa_zone.has_allocated bits
 NUMA_EXCLUSIVE_NONE, NUMA_EXCLUSIVE_PREFERRED, NUMA_EXCLUSIVE_REQUIRED = 0, 1, 2
+CPU_BIND_UNSET, CPU_BIND_DEFAULT, CPU_BIND_FULL_PCPUS, CPU_BIND_SPREAD_BY_PCPUS, CPU_BIND_CONSTRAINED_BURST = 0, 1, 2, 3, 4
+CPU_EXCL_NONE, CPU_EXCL_PCPU_LEVEL, CPU_EXCL_NUMA_NODE_LEVEL = 0, 1, 2
+NODE_CPU_BIND_NONE, NODE_CPU_BIND_FULL_PCPUS_ONLY, NODE_CPU_BIND_SPREAD_BY_PCPUS = 0, 1, 2
+NUMA_ALLOCATE_DEFAULT, NUMA_ALLOCATE_MOST, NUMA_ALLOCATE_LEAST = 0, 1, 2
+REASON_NUMA_INVALID_REQUESTED_CPUS, REASON_NUMA_CPU_BIND_POLICY_CONFLICT = 23, 24
+REASON_NUMA_SMT_ALIGNMENT, REASON_NUMA_INSUFFICIENT_CPUS = 25, 26
 NUMA_STATUS_IDLE, NUMA_STATUS_SINGLE, NUMA_STATUS_SHARED = 0, 1, 2
 MAX_NUMA = 8
 REASON_DS_INVALID_REQUEST = 32
@@ -95,7 +101,13 @@ class LoadAwareArgs(C.Structure):
 
 
 class NumaArgs(C.Structure):
-    _fields_ = [("weights", i64 * NRES), ("strategy", i32), ("numa_strategy", i32)]
+    _fields_ = [("weights", i64 * NRES), ("strategy", i32), ("numa_strategy", i32), ("default_cpu_bind_policy", i32),
+                ("pad", i32)]
+
+
+class Cpu(C.Structure):
+    _fields_ = [("cpu_id", i32), ("core_id", i32), ("numa_id", i32), ("socket_id", i32), ("ref_count", i32),
+                ("exclusive", u8), ("reserved", u8), ("pad", u8 * 2)]
 
 
 class NumaZone(C.Structure):
@@ -165,7 +177,8 @@ class Node(C.Structure):
         ("has_custom_agg", u8),
         ("amplification_error", u8),
         ("cpu_topology_invalid", u8),
-        ("pad", u8 * 7),
+        ("numa_allocate_strategy", u8),
+        ("pad", u8 * 6),
     ]
 
 
@@ -212,11 +225,15 @@ class Pod(C.Structure):
         ("device_requests", i64 * PDR_COUNT),
         ("numa_topology_policy", i32),
         ("numa_exclusive", i32),
+        ("cpu_bind_required", i32),
+        ("cpu_bind_preferred", i32),
+        ("cpu_exclusive", i32),
+        ("pad2", i32),
     ]
 
 
 STRUCTS = [Config, Node, NodeMetric, PodMetric, AggregatedUsage, Pod, ResourceMap, LoadAwareArgs, NumaArgs,
-           DeviceShareArgs, Device, NumaZone]
+           DeviceShareArgs, Device, NumaZone, Cpu]
 
 # numpy views of the same layouts (bulk loads)
 NODE_DTYPE = np.dtype(Node)
@@ -226,6 +243,7 @@ AGG_DTYPE = np.dtype(AggregatedUsage)
 POD_DTYPE = np.dtype(Pod)
 DEVICE_DTYPE = np.dtype(Device)
 NUMA_ZONE_DTYPE = np.dtype(NumaZone)
+CPU_DTYPE = np.dtype(Cpu)
 
 ROW_DTYPE = np.dtype([("f", np.int64, (18,)), ("flags", np.uint32), ("pad", np.uint32)])
 
@@ -254,6 +272,7 @@ def default_config(node_capacity, pod_batch=64, device_ordinal=0, global_node_of
     a.enable_schedule_when_node_metrics_expired = 0
     cfg.numa.weights[:] = [1, 1]
     cfg.numa.strategy = STRATEGY_LEAST_ALLOCATED
+    cfg.numa.default_cpu_bind_policy = CPU_BIND_FULL_PCPUS  # v1beta3/defaults.go:50
     cfg.deviceshare.weights[:] = [1, 1, 1, 1]  # gpu-memory-ratio, gpu-memory, rdma, fpga (defaults.go:218-242)
     cfg.deviceshare.strategy = STRATEGY_LEAST_ALLOCATED
     cfg.node_capacity = node_capacity
@@ -290,6 +309,8 @@ EXPORTS = {
     "ke_node_numa_set": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p]),
     "ke_last_device_allocations": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_last_numa_allocations": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
+    "ke_node_cpus_set": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p, i32]),
+    "ke_last_cpusets": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_schedule": (C.c_int, [C.c_void_p, i32, C.c_void_p, i64, C.c_void_p, C.c_void_p]),
     "ke_last_schedule_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(i32), C.c_void_p, i32]),
     "ke_set_profiling": (C.c_int, [C.c_void_p, i32]),

@@ -68,6 +68,25 @@ static int check_numa_deviceshare(ke_ctx* ctx, const ke_pod* pods, int32_t n) {
   return KE_OK;
 }
 
+// NodeNUMAResource under a NUMA topology policy hints and allocates cpusets through the NUMA hint
+// providers (resource_manager.go:525-622 with cpusets), which are not implemented: a pod that may bind
+// CPUs (a cpuset pod, or any cpu request while a node forces CPU binding) cannot meet NUMA policies.
+static int check_cpuset(ke_ctx* ctx, const ke_pod* pods, int32_t n) {
+  Context& c = ctx->c;
+  bool cpuset = false, policy = c.n_policy_nodes > 0;
+  for (int32_t p = 0; p < n; p++) {
+    const uint32_t f = make_dev_pod(c.cfg, pods[p]).flags;
+    const bool may_bind = (f & PF_CPU_RCB) || (c.n_bind_nodes > 0 && pods[p].requests[KE_RES_CPU] > 0);
+    if (may_bind || (f & PF_CPUSET)) c.cpu_enabled = true;  // the evaluation reads the CPU SoA
+    if (!may_bind) continue;
+    cpuset = true;
+    if (pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE) policy = true;
+  }
+  if (cpuset && policy)
+    return fail(KE_ERR_UNSUPPORTED, "cpuset pods with NUMA topology policies (NUMA hints of the CPU accumulator)");
+  return KE_OK;
+}
+
 extern "C" {
 
 int ke_abi_version(void) { return KE_ABI_VERSION; }
@@ -77,7 +96,8 @@ int ke_abi_struct_sizes(int32_t* sizes, int32_t n) {
                          (int32_t)sizeof(ke_aggregated_usage), (int32_t)sizeof(ke_pod),
                          (int32_t)sizeof(ke_resource_map), (int32_t)sizeof(ke_loadaware_args),
                          (int32_t)sizeof(ke_numa_args), (int32_t)sizeof(ke_deviceshare_args),
-                         (int32_t)sizeof(ke_device),       (int32_t)sizeof(ke_numa_zone)};
+                         (int32_t)sizeof(ke_device),       (int32_t)sizeof(ke_numa_zone),
+                         (int32_t)sizeof(ke_cpu)};
   const int32_t m = (int32_t)(sizeof(all) / sizeof(all[0]));
   for (int32_t i = 0; i < n && i < m; i++) sizes[i] = all[i];
   return m;
@@ -146,9 +166,15 @@ int ke_node_upsert(ke_ctx* ctx, int32_t node, const ke_node* n) {
   rc = validate_node(*n);
   if (rc) return rc;
   NodeState& ns = ctx->c.nodes[node];
+  if (ns.valid) {
+    ctx->c.n_bind_nodes -= ns.node.cpu_bind_policy != KE_NODE_CPU_BIND_NONE;
+    ctx->c.n_policy_nodes -= ns.node.numa_topology_policy != KE_NUMA_POLICY_NONE;
+  }
   ns.valid = true;
   ns.node = *n;
   ns.dirty = true;
+  ctx->c.n_bind_nodes += n->cpu_bind_policy != KE_NODE_CPU_BIND_NONE;
+  ctx->c.n_policy_nodes += n->numa_topology_policy != KE_NUMA_POLICY_NONE;
   if (n->numa_topology_policy != KE_NUMA_POLICY_NONE) ctx->c.numa_enabled = true;
   ctx->c.n_nodes = std::max(ctx->c.n_nodes, node + 1);
   return KE_OK;
@@ -196,6 +222,26 @@ int ke_node_numa_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_numa_zone* z
   ns.zones.assign(zones, zones + n);
   ns.dirty = true;
   ctx->c.numa_enabled = true;
+  return KE_OK;
+}
+
+int ke_node_cpus_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_cpu* cpus, int32_t max_ref_count) {
+  int rc = check_node(ctx, node);
+  if (rc) return rc;
+  rc = validate_cpus(n, cpus, max_ref_count);
+  if (rc) return rc;
+  NodeState& ns = ctx->c.nodes[node];
+  ns.cpus.assign(cpus, cpus + n);
+  ns.cpu_max_ref = n > 0 ? max_ref_count : 1;
+  ns.dirty = true;
+  if (n > 0) ctx->c.cpu_enabled = true;
+  return KE_OK;
+}
+
+int ke_last_cpusets(ke_ctx* ctx, int32_t n, uint64_t* out) {
+  if (!ctx || n < 0 || (n > 0 && !out)) return fail(KE_ERR_INVALID, "ke_last_cpusets arguments");
+  const auto& a = ctx->c.last_cpusets;
+  for (int64_t i = 0; i < (int64_t)n * 4; i++) out[i] = i < (int64_t)a.size() ? a[i] : 0;
   return KE_OK;
 }
 
@@ -320,6 +366,8 @@ int ke_eval(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, uin
   if (rc) return rc;
   rc = check_numa_deviceshare(ctx, pods, n_pods);
   if (rc) return rc;
+  rc = check_cpuset(ctx, pods, n_pods);
+  if (rc) return rc;
   rc = require_device(ctx);
   if (rc) return rc;
   return device_eval(&ctx->c, n_pods, pods, now_ns, status, reason, la_score, numa_score, ds_score, total, best);
@@ -330,6 +378,8 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
   int rc = check_pods(pods, n_pods);
   if (rc) return rc;
   rc = check_numa_deviceshare(ctx, pods, n_pods);
+  if (rc) return rc;
+  rc = check_cpuset(ctx, pods, n_pods);
   if (rc) return rc;
   rc = require_device(ctx);
   if (rc) return rc;
@@ -352,6 +402,10 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
     ns.node.requested[KE_RES_CPU] += pods[p].requests[KE_RES_CPU];
     ns.node.requested[KE_RES_MEMORY] += pods[p].requests[KE_RES_MEMORY];
     ns.dirty = was_dirty;  // the device row already carries this Reserve
+    // cpuset Reserve: the CPU table (the device one is patched too) and the zones' NUMA status (not
+    // patched on the device: re-derived from this mirror)
+    const uint64_t* cs = (int64_t)ctx->c.last_cpusets.size() >= (int64_t)(p + 1) * 4 ? &ctx->c.last_cpusets[(size_t)p * 4] : nullptr;
+    if (cs && (cs[0] | cs[1] | cs[2] | cs[3])) host_cpuset_reserve(ns, make_dev_pod(ctx->c.cfg, pods[p]), cs);
   }
   return KE_OK;
 }

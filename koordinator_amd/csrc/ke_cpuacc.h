@@ -1,0 +1,456 @@
+// ke_cpuacc.h — NodeNUMAResource's CPU accumulator on the device (one node, one thread, LDS-resident).
+//
+// Same algorithm as pkg/scheduler/plugins/nodenumaresource/cpu_accumulator.go (takeCPUs :87-232 and
+// the cpuAccumulator helpers :234-822).  Per node the CPU table lives in the CPU SoA as one 8-byte
+// record per CPU id (CpuRec); core and socket ids are the node's dense ranks of the reference ids (the
+// accumulator only compares them), NUMA ids are kept.  Go feeds every list through map iteration but
+// sorts each by a total order with the id last; the two length-only sorts in takeCPUs (:142-144,
+// :161-163) run on <= 12 sockets, where Go's sort.Slice is an insertion sort (stable) — the insertion
+// sorts here are stable too.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "ke_types.h"
+
+namespace ke {
+
+constexpr int ACC_CPUS = CPU_SLOTS;
+constexpr int ACC_TPC = 8;  // max logical CPUs per core (validated by ke_node_cpus_set)
+
+// topology counts (cpu_topology.go:45-105)
+struct AccTopo {
+  int num_cpus, num_cores, num_nodes, num_sockets;
+};
+
+struct AccLds {
+  CpuRec cpu[ACC_CPUS];
+  uint8_t alloc[ACC_CPUS];    // allocatableCPUs
+  uint8_t aref[ACC_CPUS];     // allocatableCPUs[c].RefCount (max_ref > 1)
+  uint8_t ex_core[ACC_CPUS];  // exclusiveInCores (core rank)
+  uint8_t ex_node[ACC_CPUS];  // exclusiveInNUMANodes (NUMA id)
+  uint8_t res[ACC_CPUS];      // result
+  // one grouping (cores / NUMA nodes / sockets): CPUs concatenated in group order
+  int16_t lst[ACC_CPUS];
+  int16_t goff[ACC_CPUS + 1];
+  int16_t gkey[ACC_CPUS];
+  int16_t gscore[ACC_CPUS];   // per group: the free score the sort used
+  int ng;
+  // a second grouping (takeCPUs keeps the unsatisfied sockets)
+  int16_t lst2[ACC_CPUS];
+  int16_t goff2[ACC_CPUS + 1];
+  int ng2;
+  // per core rank: its allocatable CPUs (kept by the current pass)
+  uint8_t core_n[ACC_CPUS];
+  uint8_t core_cpu[ACC_CPUS][ACC_TPC];
+  int16_t cref[ACC_CPUS];     // getCoreRefCount per core rank over the allocatable CPUs (max_ref > 1)
+  int16_t order[ACC_CPUS];
+  int16_t tmp[ACC_CPUS];
+  AccTopo t;
+  int max_ref, needed, excl_policy, exclusive, numa_most;
+};
+
+__device__ __forceinline__ int acc_cpc(const AccTopo& t) { return t.num_cores ? t.num_cpus / t.num_cores : 0; }
+__device__ __forceinline__ int acc_cps(const AccTopo& t) { return t.num_sockets ? t.num_cpus / t.num_sockets : 0; }
+__device__ __forceinline__ int acc_cpn(const AccTopo& t) { return t.num_nodes ? t.num_cpus / t.num_nodes : 0; }
+
+__device__ __forceinline__ bool strat_less(const AccLds& a, int si, int sj) { return a.numa_most ? si < sj : si > sj; }
+
+__device__ inline void acc_take(AccLds& a, const int16_t* cpus, int n) {  // :290-304
+  for (int i = 0; i < n; i++) {
+    const int c = cpus[i];
+    a.res[c] = 1;
+    a.alloc[c] = 0;
+    if (a.exclusive) {
+      if (a.excl_policy == 1) a.ex_core[a.cpu[c].core] = 1;
+      else if (a.excl_policy == 2) a.ex_node[a.cpu[c].numa] = 1;
+    }
+  }
+  a.needed -= n;
+}
+__device__ __forceinline__ int acc_count_alloc(const AccLds& a) {
+  int n = 0;
+  for (int c = 0; c < ACC_CPUS; c++) n += a.alloc[c];
+  return n;
+}
+__device__ __forceinline__ bool excl_pcpu(const AccLds& a, int c) { return a.excl_policy == 1 && a.ex_core[a.cpu[c].core]; }
+__device__ __forceinline__ bool excl_numa(const AccLds& a, int c) { return a.excl_policy == 2 && a.ex_node[a.cpu[c].numa]; }
+
+// getCoreRefCount (:776-783) over the allocatable CPUs: cached per core rank by collect_cores (the
+// allocatable set only changes in acc_take, between sorts)
+__device__ __forceinline__ int core_ref(const AccLds& a, int core) { return a.cref[core]; }
+
+__device__ inline void sort_i16(int16_t* v, int n) {
+  for (int i = 1; i < n; i++)
+    for (int j = i; j > 0 && v[j] < v[j - 1]; j--) {
+      const int16_t t = v[j];
+      v[j] = v[j - 1];
+      v[j - 1] = t;
+    }
+}
+__device__ inline void sort_by_ref(const AccLds& a, int16_t* v, int n) {  // sortCPUsByRefCount :785-796
+  for (int i = 1; i < n; i++)
+    for (int j = i; j > 0; j--) {
+      const int x = v[j], y = v[j - 1];
+      const bool less = a.aref[x] != a.aref[y] ? a.aref[x] < a.aref[y] : x < y;
+      if (!less) break;
+      v[j] = (int16_t)y;
+      v[j - 1] = (int16_t)x;
+    }
+}
+__device__ inline int extract_cpu(const AccLds& a, int16_t* v, int n) {  // :332-343
+  uint8_t seen[ACC_CPUS / 8] = {};
+  int m = 0;
+  for (int i = 0; i < n; i++) {
+    const int core = a.cpu[v[i]].core;
+    if (seen[core >> 3] >> (core & 7) & 1) continue;
+    seen[core >> 3] |= (uint8_t)(1u << (core & 7));
+    v[m++] = v[i];
+  }
+  return m;
+}
+
+// cores of the allocatable CPUs passing `keep` (per core rank, CPU ids ascending)
+template <typename Keep>
+__device__ inline void collect_cores(AccLds& a, Keep keep) {
+  for (int k = 0; k < ACC_CPUS; k++) a.core_n[k] = 0, a.cref[k] = 0;
+  if (a.max_ref > 1)
+    for (int c = 0; c < ACC_CPUS; c++)
+      if (a.alloc[c]) a.cref[a.cpu[c].core] += a.aref[c];
+  for (int c = 0; c < ACC_CPUS; c++)
+    if (a.alloc[c] && keep(c)) {
+      const int k = a.cpu[c].core;
+      if (a.core_n[k] < ACC_TPC) a.core_cpu[k][a.core_n[k]++] = (uint8_t)c;
+    }
+}
+
+// sortCores :345-368 on a list of core ranks
+__device__ inline bool cores_less(const AccLds& a, int ci, int cj) {
+  if (a.core_n[ci] != a.core_n[cj]) return a.core_n[ci] > a.core_n[cj];
+  if (a.max_ref > 1) {
+    const int ri = core_ref(a, ci), rj = core_ref(a, cj);
+    if (ri != rj) return ri < rj;
+  }
+  return ci < cj;
+}
+
+// Group the collected cores by NUMA node (by_socket = 0) or socket (1), full cores only if asked;
+// per group the cores sorted (sortCores) and their CPUs appended -> a.lst / a.goff / a.gkey.
+__device__ inline void group_cores(AccLds& a, bool by_socket, bool filter_full) {
+  const int cpc = acc_cpc(a.t);
+  // distinct group keys in ascending order (the final sort is a total order; start order is moot)
+  uint8_t has[ACC_CPUS] = {};
+  for (int k = 0; k < ACC_CPUS; k++) {
+    if (!a.core_n[k] || (filter_full && a.core_n[k] != cpc)) continue;
+    const int c0 = a.core_cpu[k][0];
+    has[by_socket ? a.cpu[c0].socket : a.cpu[c0].numa] = 1;
+  }
+  a.ng = 0;
+  int pos = 0;
+  for (int g = 0; g < ACC_CPUS; g++) {
+    if (!has[g]) continue;
+    int nc = 0;
+    for (int k = 0; k < ACC_CPUS; k++) {
+      if (!a.core_n[k] || (filter_full && a.core_n[k] != cpc)) continue;
+      const int c0 = a.core_cpu[k][0];
+      if ((by_socket ? a.cpu[c0].socket : a.cpu[c0].numa) == g) a.order[nc++] = (int16_t)k;
+    }
+    for (int i = 1; i < nc; i++)
+      for (int j = i; j > 0 && cores_less(a, a.order[j], a.order[j - 1]); j--) {
+        const int16_t t = a.order[j];
+        a.order[j] = a.order[j - 1];
+        a.order[j - 1] = t;
+      }
+    a.gkey[a.ng] = (int16_t)g;
+    a.goff[a.ng] = (int16_t)pos;
+    for (int i = 0; i < nc; i++) {
+      const int k = a.order[i];
+      for (int q = 0; q < a.core_n[k]; q++) a.tmp[q] = a.core_cpu[k][q];
+      sort_i16(a.tmp, a.core_n[k]);
+      for (int q = 0; q < a.core_n[k]; q++) a.lst[pos++] = a.tmp[q];
+    }
+    a.ng++;
+  }
+  a.goff[a.ng] = (int16_t)pos;
+}
+
+__device__ __forceinline__ int glen(const AccLds& a, int g) { return a.goff[g + 1] - a.goff[g]; }
+
+// reorder the groups of a.lst by a permutation a.order[0..ng)
+__device__ inline void permute_groups(AccLds& a) {
+  int pos = 0;
+  int16_t noff[ACC_CPUS + 1], nkey[ACC_CPUS], nsc[ACC_CPUS];
+  for (int i = 0; i < a.ng; i++) {
+    const int g = a.order[i];
+    noff[i] = (int16_t)pos;
+    nkey[i] = a.gkey[g];
+    nsc[i] = a.gscore[g];
+    for (int q = a.goff[g]; q < a.goff[g + 1]; q++) a.tmp[pos++] = a.lst[q];
+  }
+  noff[a.ng] = (int16_t)pos;
+  for (int q = 0; q < pos; q++) a.lst[q] = a.tmp[q];
+  for (int i = 0; i <= a.ng; i++) a.goff[i] = noff[i];
+  for (int i = 0; i < a.ng; i++) a.gkey[i] = nkey[i], a.gscore[i] = nsc[i];
+}
+
+// free-CPU count per socket / NUMA node of the allocatable CPUs passing `keep`
+template <typename Keep>
+__device__ inline void free_scores(const AccLds& a, Keep keep, int16_t* per_socket, int16_t* per_node) {
+  for (int k = 0; k < ACC_CPUS; k++) per_socket[k] = 0, per_node[k] = 0;
+  for (int c = 0; c < ACC_CPUS; c++)
+    if (a.alloc[c] && keep(c)) per_socket[a.cpu[c].socket]++, per_node[a.cpu[c].numa]++;
+}
+
+// freeCoresInNode :371-461
+__device__ inline void free_cores_in_node(AccLds& a, bool filter_full, bool filter_excl) {
+  auto keep = [&](int c) { return !(filter_excl && excl_numa(a, c)); };
+  int16_t sock[ACC_CPUS], node[ACC_CPUS];
+  free_scores(a, keep, sock, node);
+  collect_cores(a, keep);
+  group_cores(a, false, filter_full);
+  for (int g = 0; g < a.ng; g++) a.gscore[g] = (int16_t)glen(a, g), a.order[g] = (int16_t)g;
+  for (int i = 1; i < a.ng; i++)
+    for (int j = i; j > 0; j--) {
+      const int gi = a.order[j], gj = a.order[j - 1];
+      const int si = sock[a.cpu[a.lst[a.goff[gi]]].socket], sj = sock[a.cpu[a.lst[a.goff[gj]]].socket];
+      bool less;
+      if (a.gscore[gi] != a.gscore[gj]) less = strat_less(a, a.gscore[gi], a.gscore[gj]);
+      else if (si != sj) less = strat_less(a, si, sj);
+      else less = a.gkey[gi] < a.gkey[gj];
+      if (!less) break;
+      a.order[j] = (int16_t)gj;
+      a.order[j - 1] = (int16_t)gi;
+    }
+  permute_groups(a);
+}
+
+// freeCoresInSocket :464-527
+__device__ inline void free_cores_in_socket(AccLds& a, bool filter_full) {
+  collect_cores(a, [](int) { return true; });
+  group_cores(a, true, filter_full);
+  for (int g = 0; g < a.ng; g++) a.gscore[g] = (int16_t)glen(a, g), a.order[g] = (int16_t)g;
+  for (int i = 1; i < a.ng; i++)
+    for (int j = i; j > 0; j--) {
+      const int gi = a.order[j], gj = a.order[j - 1];
+      const bool less = a.gscore[gi] != a.gscore[gj] ? strat_less(a, a.gscore[gi], a.gscore[gj]) : a.gkey[gi] < a.gkey[gj];
+      if (!less) break;
+      a.order[j] = (int16_t)gj;
+      a.order[j - 1] = (int16_t)gi;
+    }
+  permute_groups(a);
+}
+
+// freeCPUsInNode (:530-605, by_socket = false) / freeCPUsInSocket (:608-656, by_socket = true)
+__device__ inline void free_cpus_in_group(AccLds& a, bool by_socket, bool filter_excl) {
+  auto keep = [&](int c) {
+    if (!filter_excl) return true;
+    return by_socket ? !excl_pcpu(a, c) : !(excl_pcpu(a, c) || excl_numa(a, c));
+  };
+  int16_t sock[ACC_CPUS], node[ACC_CPUS];
+  free_scores(a, keep, sock, node);
+  a.ng = 0;
+  int pos = 0;
+  for (int g = 0; g < ACC_CPUS; g++) {
+    const int start = pos;
+    for (int c = 0; c < ACC_CPUS; c++)
+      if (a.alloc[c] && keep(c) && (by_socket ? a.cpu[c].socket : a.cpu[c].numa) == g) a.lst[pos++] = (int16_t)c;
+    if (pos == start) continue;
+    int n = pos - start;  // ascending already; then by ref count, then one CPU per core
+    if (a.max_ref > 1) sort_by_ref(a, &a.lst[start], n);
+    if (filter_excl) n = extract_cpu(a, &a.lst[start], n);
+    pos = start + n;
+    a.gkey[a.ng] = (int16_t)g;
+    a.goff[a.ng] = (int16_t)start;
+    a.gscore[a.ng] = by_socket ? (int16_t)n : node[g];
+    a.ng++;
+  }
+  a.goff[a.ng] = (int16_t)pos;
+  for (int g = 0; g < a.ng; g++) a.order[g] = (int16_t)g;
+  for (int i = 1; i < a.ng; i++)
+    for (int j = i; j > 0; j--) {
+      const int gi = a.order[j], gj = a.order[j - 1];
+      bool less;
+      if (a.gscore[gi] != a.gscore[gj]) {
+        less = strat_less(a, a.gscore[gi], a.gscore[gj]);
+      } else if (!by_socket) {
+        const int si = sock[a.cpu[a.lst[a.goff[gi]]].socket], sj = sock[a.cpu[a.lst[a.goff[gj]]].socket];
+        less = si != sj ? strat_less(a, si, sj) : a.gkey[gi] < a.gkey[gj];
+      } else {
+        less = a.gkey[gi] < a.gkey[gj];
+      }
+      if (!less) break;
+      a.order[j] = (int16_t)gj;
+      a.order[j - 1] = (int16_t)gi;
+    }
+  permute_groups(a);
+}
+
+// freeCPUs :666-774 -> a.lst[0..n)
+__device__ inline int free_cpus(AccLds& a, bool filter_excl) {
+  auto keep = [&](int c) { return !(filter_excl && (excl_pcpu(a, c) || excl_numa(a, c))); };
+  int16_t sock[ACC_CPUS], node[ACC_CPUS], colo[ACC_CPUS];
+  free_scores(a, keep, sock, node);
+  for (int s = 0; s < ACC_CPUS; s++) colo[s] = 0;
+  for (int c = 0; c < ACC_CPUS; c++)
+    if ((a.cpu[c].flags & CR_VALID) && a.res[c]) colo[a.cpu[c].socket]++;
+  collect_cores(a, keep);
+  int nc = 0;
+  for (int k = 0; k < ACC_CPUS; k++)
+    if (a.core_n[k]) a.order[nc++] = (int16_t)k;
+  for (int i = 1; i < nc; i++)
+    for (int j = i; j > 0; j--) {
+      const int ki = a.order[j], kj = a.order[j - 1];
+      const int ci = a.core_cpu[ki][0], cj = a.core_cpu[kj][0];
+      const int si = a.cpu[ci].socket, sj = a.cpu[cj].socket, ni = a.cpu[ci].numa, nj = a.cpu[cj].numa;
+      bool less;
+      if (colo[si] != colo[sj]) less = colo[si] > colo[sj];
+      else if (sock[si] != sock[sj]) less = strat_less(a, sock[si], sock[sj]);
+      else if (node[ni] != node[nj]) less = strat_less(a, node[ni], node[nj]);
+      else if (a.core_n[ki] != a.core_n[kj]) less = a.core_n[ki] < a.core_n[kj];
+      else if (si != sj) less = si < sj;
+      else {
+        const int ri = a.max_ref > 1 ? core_ref(a, ki) : 0, rj = a.max_ref > 1 ? core_ref(a, kj) : 0;
+        less = ri != rj ? ri < rj : ki < kj;
+      }
+      if (!less) break;
+      a.order[j] = (int16_t)kj;
+      a.order[j - 1] = (int16_t)ki;
+    }
+  int n = 0;
+  for (int i = 0; i < nc; i++) {
+    const int k = a.order[i];
+    const int start = n;
+    for (int q = 0; q < a.core_n[k]; q++) a.lst[n++] = a.core_cpu[k][q];
+    sort_i16(&a.lst[start], a.core_n[k]);
+    if (a.max_ref > 1) sort_by_ref(a, &a.lst[start], a.core_n[k]);
+  }
+  return n;
+}
+
+// spreadCPUs :798-822 on v[0..n)
+__device__ inline void spread_cpus(AccLds& a, int16_t* v, int n) {
+  if (n <= acc_cpc(a.t)) return;
+  int16_t* prep = a.tmp;
+  for (int i = 0; i < n; i++) prep[i] = v[i];
+  int np = n, no = 0;
+  int16_t out[ACC_CPUS];
+  while (np > 0) {
+    uint8_t seen[ACC_CPUS / 8] = {};
+    int nr = 0;
+    for (int i = 0; i < np; i++) {
+      const int core = a.cpu[prep[i]].core;
+      if (seen[core >> 3] >> (core & 7) & 1) {
+        prep[nr++] = prep[i];  // reserved for the next pass (nr <= i: in place)
+        continue;
+      }
+      seen[core >> 3] |= (uint8_t)(1u << (core & 7));
+      out[no++] = prep[i];
+    }
+    np = nr;
+  }
+  for (int i = 0; i < n; i++) v[i] = out[i];
+}
+
+// takeCPUs :87-232 on the accumulator state prepared by the caller (alloc, aref, ex_*, res = 0,
+// needed, policies).  Returns true on success (a.res = the cpuset).
+__device__ inline bool acc_take_cpus(AccLds& a, int bind) {
+  if (a.needed < 1) return true;
+  if (a.needed > acc_count_alloc(a)) return false;
+  const bool full = bind == XB_FULL;
+  const int cpc = acc_cpc(a.t);
+  if (full || cpc == 1) {
+    if (a.needed <= acc_cpn(a.t))
+      for (int fe = 1; fe >= 0; fe--) {
+        free_cores_in_node(a, true, fe == 1);
+        for (int g = 0; g < a.ng; g++)
+          if (glen(a, g) >= a.needed) {
+            acc_take(a, &a.lst[a.goff[g]], a.needed);
+            return true;
+          }
+      }
+    if (a.needed <= acc_cps(a.t)) {
+      free_cores_in_socket(a, true);
+      for (int g = 0; g < a.ng; g++)
+        if (glen(a, g) >= a.needed) {
+          acc_take(a, &a.lst[a.goff[g]], a.needed);
+          return true;
+        }
+    }
+    free_cores_in_socket(a, true);
+    for (int g = 0; g < a.ng; g++) a.order[g] = (int16_t)g;
+    for (int i = 1; i < a.ng; i++)  // sort.Slice by length desc (stable on few sockets)
+      for (int j = i; j > 0 && glen(a, a.order[j]) > glen(a, a.order[j - 1]); j--) {
+        const int16_t t = a.order[j];
+        a.order[j] = a.order[j - 1];
+        a.order[j - 1] = t;
+      }
+    permute_groups(a);
+    a.ng2 = 0;
+    int pos2 = 0;
+    for (int g = 0; g < a.ng; g++) {
+      const int len = glen(a, g);
+      if (a.needed < len) {  // !needs(len): kept for the per-core pass
+        a.goff2[a.ng2++] = (int16_t)pos2;
+        for (int q = a.goff[g]; q < a.goff[g + 1]; q++) a.lst2[pos2++] = a.lst[q];
+      } else {
+        acc_take(a, &a.lst[a.goff[g]], len);
+        if (a.needed < 1) return true;
+      }
+    }
+    a.goff2[a.ng2] = (int16_t)pos2;
+    if (a.needed >= cpc) {
+      int16_t ord[ACC_CPUS];
+      for (int g = 0; g < a.ng2; g++) ord[g] = (int16_t)g;
+      for (int i = 1; i < a.ng2; i++)  // by length asc, stable
+        for (int j = i; j > 0; j--) {
+          const int li = a.goff2[ord[j] + 1] - a.goff2[ord[j]], lj = a.goff2[ord[j - 1] + 1] - a.goff2[ord[j - 1]];
+          if (!(li < lj)) break;
+          const int16_t t = ord[j];
+          ord[j] = ord[j - 1];
+          ord[j - 1] = t;
+        }
+      for (int i = 0; i < a.ng2; i++) {
+        const int g = ord[i];
+        for (int q = a.goff2[g]; q < a.goff2[g + 1]; q += cpc) {
+          acc_take(a, &a.lst2[q], cpc);
+          if (a.needed < 1) return true;
+          if (a.needed < cpc) break;
+        }
+      }
+    }
+  }
+  if (!full) {
+    if (a.needed <= acc_cpn(a.t))
+      for (int fe = 1; fe >= 0; fe--) {
+        free_cpus_in_group(a, false, fe == 1);
+        for (int g = 0; g < a.ng; g++)
+          if (glen(a, g) >= a.needed) {
+            spread_cpus(a, &a.lst[a.goff[g]], glen(a, g));
+            acc_take(a, &a.lst[a.goff[g]], a.needed);
+            return true;
+          }
+      }
+    if (a.needed <= acc_cps(a.t))
+      for (int fe = 1; fe >= 0; fe--) {
+        free_cpus_in_group(a, true, fe == 1);
+        for (int g = 0; g < a.ng; g++)
+          if (glen(a, g) >= a.needed) {
+            spread_cpus(a, &a.lst[a.goff[g]], glen(a, g));
+            acc_take(a, &a.lst[a.goff[g]], a.needed);
+            return true;
+          }
+      }
+  }
+  for (int fe = 1; fe >= 0; fe--) {
+    const int n = free_cpus(a, fe == 1);
+    spread_cpus(a, a.lst, n);
+    for (int i = 0; i < n; i++) {
+      if (a.needed >= 1) acc_take(a, &a.lst[i], 1);
+      if (a.needed < 1) return true;
+    }
+  }
+  return false;
+}
+
+}  // namespace ke

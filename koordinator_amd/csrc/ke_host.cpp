@@ -10,6 +10,7 @@
 #include <climits>
 #include <cmath>
 #include <cstring>
+#include <map>
 #include <unordered_map>
 
 namespace ke {
@@ -66,8 +67,9 @@ int validate_node(const ke_node& n) {
   }
   if (n.numa_topology_policy < KE_NUMA_POLICY_NONE || n.numa_topology_policy > KE_NUMA_POLICY_SINGLE_NUMA_NODE)
     return fail(KE_ERR_INVALID, "NUMA topology policy");
-  if (n.cpu_bind_policy != 0)
-    return fail(KE_ERR_UNSUPPORTED, "node CPU bind policies (cpuset binding) are not implemented");
+  if (n.cpu_bind_policy < KE_NODE_CPU_BIND_NONE || n.cpu_bind_policy > KE_NODE_CPU_BIND_SPREAD_BY_PCPUS)
+    return fail(KE_ERR_INVALID, "node CPU bind policy");
+  if (n.numa_allocate_strategy > KE_NUMA_ALLOCATE_LEAST) return fail(KE_ERR_INVALID, "NUMA allocate strategy");
   if (n.custom_agg_type < 0 || n.custom_agg_type >= KE_AGG_TYPES) return fail(KE_ERR_INVALID, "aggregation type");
   return KE_OK;
 }
@@ -143,12 +145,12 @@ void host_ds_reserve(const ke_config& cfg, NodeState& ns, const DevPod& dp, uint
 }
 
 int validate_pod(const ke_pod& p) {
-  // AllowUseCPUSet (nodenumaresource/util.go:49-56) with the default FullPCPUs bind policy makes the
-  // pod a cpuset pod (plugin.go:276-301): that path (cpu accumulator, NUMA hints) is a later §8 row.
-  const bool cpuset = (p.qos_class == KE_QOS_LSE || p.qos_class == KE_QOS_LSR) &&
-                      p.priority_class == KE_PRIORITY_PROD && p.requests[KE_RES_CPU] > 0;
-  if (cpuset || p.has_resource_spec)
-    return fail(KE_ERR_UNSUPPORTED, "cpuset (LSE/LSR koord-prod) pods are not implemented in ABI v1");
+  if (p.has_resource_spec)  // PreFilter returns the unmarshal error (plugin.go:276-280)
+    return fail(KE_ERR_UNSUPPORTED, "pods whose ResourceSpec annotation fails to unmarshal");
+  if (p.cpu_bind_required < KE_CPU_BIND_UNSET || p.cpu_bind_required > KE_CPU_BIND_CONSTRAINED_BURST ||
+      p.cpu_bind_preferred < KE_CPU_BIND_UNSET || p.cpu_bind_preferred > KE_CPU_BIND_CONSTRAINED_BURST ||
+      p.cpu_exclusive < KE_CPU_EXCL_NONE || p.cpu_exclusive > KE_CPU_EXCL_NUMA_NODE_LEVEL)
+    return fail(KE_ERR_INVALID, "pod CPU bind / exclusive policy");
   if (p.priority_class < 0 || p.priority_class > KE_PRIORITY_FREE) return fail(KE_ERR_INVALID, "priority class");
   if (p.has_unsupported_device_requests)
     return fail(KE_ERR_UNSUPPORTED, "Huawei NPU / Hygon DCU device requests are not implemented");
@@ -316,6 +318,30 @@ DevPod make_dev_pod(const ke_config& cfg, const ke_pod& pod) {
   if (pod.numa_exclusive == KE_NUMA_EXCLUSIVE_REQUIRED ||
       (pod.numa_exclusive == KE_NUMA_EXCLUSIVE_NONE && pod.numa_topology_policy != KE_NUMA_POLICY_NONE))
     f |= PF_NUMA_EXCL_REQ;
+  // NodeNUMAResource PreFilter (plugin.go:251-312): AllowUseCPUSet (util.go:49-56) and a FullPCPUs /
+  // SpreadByPCPUs bind policy from the ResourceSpec, the args' default standing in for "Default"
+  const int64_t cpu = pod.requests[KE_RES_CPU];
+  if (cpu % 1000 == 0) f |= PF_CPU_INT;
+  if ((pod.qos_class == KE_QOS_LSE || pod.qos_class == KE_QOS_LSR) && pod.priority_class == KE_PRIORITY_PROD) {
+    const int dflt = cfg.numa.default_cpu_bind_policy;
+    int bind = pod.cpu_bind_preferred;
+    if (bind == KE_CPU_BIND_UNSET || bind == KE_CPU_BIND_DEFAULT) bind = dflt;
+    int required = pod.cpu_bind_required;
+    if (required == KE_CPU_BIND_DEFAULT) required = dflt;
+    if (required != KE_CPU_BIND_UNSET) bind = required;
+    auto xb = [](int b) {
+      return b == KE_CPU_BIND_FULL_PCPUS ? XB_FULL : b == KE_CPU_BIND_SPREAD_BY_PCPUS ? XB_SPREAD : XB_NONE;
+    };
+    if (bind == KE_CPU_BIND_FULL_PCPUS || bind == KE_CPU_BIND_SPREAD_BY_PCPUS) {
+      if (cpu % 1000 != 0) {
+        f |= PF_CPU_INVALID | PF_CPUSET;  // "the requested CPUs must be integer"
+      } else if (cpu > 0) {
+        f |= PF_CPU_RCB | PF_CPUSET;
+        f |= (uint32_t)xb(required) * PF_CPU_REQ0 | (uint32_t)xb(bind) * PF_CPU_PREF0;
+        f |= (uint32_t)pod.cpu_exclusive * PF_CPU_EXCL0;
+      }
+    }
+  }
   d.flags = f;
   if (!ds_prepare(pod, d)) {
     for (int t = 0; t < 3; t++) d.ds_cnt[t] = 0;
@@ -541,7 +567,7 @@ void derive_row(const ke_config& cfg, const NodeState& ns, int64_t now, Row* row
     row->f[F_NALLOC + r] = n.allocatable[r];
     row->f[F_NREQ + r] = n.requested[r];
   }
-  const int64_t cs_milli = n.cpuset_allocated_cpus * 1000;
+  const int64_t cs_milli = cpus_allocated(ns) * 1000;
   row->f[F_CSM] = cs_milli;
   if (n.amplification_error) flags |= NF_NUMA_AMP_ERR;
   if (n.cpu_topology_invalid) flags |= NF_NUMA_TOPO_INVALID;
@@ -559,6 +585,12 @@ void derive_row(const ke_config& cfg, const NodeState& ns, int64_t now, Row* row
   row->f[F_CSAS] = amplify(cs_milli, ratio_s);
   if (ns.has_dev_cache) flags |= NF_DS_CACHE;
   flags |= (uint32_t)n.numa_topology_policy * NF_NUMA_POLICY0;
+  flags |= (uint32_t)n.cpu_bind_policy * NF_CPU_BIND0;
+  if (cpus_valid(ns)) flags |= NF_CPUS_VALID;
+  // GetNUMAAllocateStrategy (util.go:33-47): the node label, else NUMAScoringStrategy's type
+  if (n.numa_allocate_strategy == KE_NUMA_ALLOCATE_MOST ||
+      (n.numa_allocate_strategy == KE_NUMA_ALLOCATE_DEFAULT && cfg.numa.numa_strategy == KE_STRATEGY_MOST_ALLOCATED))
+    flags |= NF_CPU_NUMA_MOST;
   if (n.nrt_cpu_amplification_ratio <= -1.5 && n.amplification_error) flags |= NF_NUMA_OPT_ERR;
   {  // TopologyOptions.AmplificationRatios[cpu]: the NRT's ratios, else the node annotation's
     const double r = n.nrt_cpu_amplification_ratio > -1.5 ? n.nrt_cpu_amplification_ratio : n.cpu_amplification_ratio;
@@ -620,7 +652,11 @@ void derive_numa_row(const NodeState& ns, int64_t* f, uint64_t* mask) {
           f[NUMA_AL + 2 * id + r] = z.allocated[r];
         }
       if (ratio > 1.0) {  // the cpu key is (re)written even when the entry had none
-        const int64_t cs = (int64_t)z.cpuset_cpus * 1000;
+        int64_t cs = (int64_t)z.cpuset_cpus * 1000;  // allocatedCPUs.CPUsInNUMANodes(id).Size()
+        if (!ns.cpus.empty()) {
+          cs = 0;
+          for (const ke_cpu& c : ns.cpus) cs += (c.ref_count > 0 && c.numa_id == id) ? 1000 : 0;
+        }
         f[NUMA_AL + 2 * id] = f[NUMA_AL + 2 * id] - cs + amplify(cs, ratio);
         *mask |= 1ull << (NUMA_M_AL + id);
       }
@@ -640,6 +676,108 @@ void host_numa_reserve(NodeState& ns, const int64_t* delta) {
     }
     z.has_allocated |= KE_NUMA_ALLOC_ENTRY;
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// CPU topology (cpu_topology.go:24-105) and cpuset allocations (node_allocation.go:33-156)
+// ---------------------------------------------------------------------------------------------
+// The device accumulator keeps per CPU its core / socket rank and NUMA id in a byte each and reduces
+// the required-policy Filter to counts, which needs a regular topology: every core
+// in one socket and NUMA node with the same number (<= 8) of logical CPUs.
+int validate_cpus(int32_t n, const ke_cpu* cpus, int32_t max_ref) {
+  if (n < 0 || n > KE_MAX_CPUS || (n > 0 && !cpus)) return fail(KE_ERR_INVALID, "CPU count");
+  if (n == 0) return KE_OK;
+  if (max_ref < 1 || max_ref > 255) return fail(KE_ERR_INVALID, "MaxRefCount must be in 1..255");
+  bool seen[KE_MAX_CPUS] = {};
+  for (int32_t i = 0; i < n; i++) {
+    const ke_cpu& c = cpus[i];
+    if (c.cpu_id < 0 || c.cpu_id >= KE_MAX_CPUS || seen[c.cpu_id]) return fail(KE_ERR_INVALID, "CPU id out of range or repeated");
+    seen[c.cpu_id] = true;
+    if (c.core_id < 0 || c.socket_id < 0 || c.numa_id < 0 || c.numa_id > 255)
+      return fail(KE_ERR_INVALID, "CPU core / socket / NUMA id");
+    if (c.ref_count < 0 || c.ref_count > 255 || c.exclusive > KE_CPU_EXCL_NUMA_NODE_LEVEL || c.reserved > 1)
+      return fail(KE_ERR_INVALID, "CPU allocation state");
+  }
+  std::map<int32_t, std::pair<int32_t, int32_t>> where;  // core id -> (socket, NUMA node)
+  std::map<int32_t, int> per_core;
+  for (int32_t i = 0; i < n; i++) {
+    auto it = where.find(cpus[i].core_id);
+    if (it == where.end()) where[cpus[i].core_id] = {cpus[i].socket_id, cpus[i].numa_id};
+    else if (it->second != std::make_pair(cpus[i].socket_id, cpus[i].numa_id))
+      return fail(KE_ERR_UNSUPPORTED, "a core id spanning sockets / NUMA nodes");
+    per_core[cpus[i].core_id]++;
+  }
+  const int cpc = per_core.begin()->second;
+  for (const auto& kv : per_core)
+    if (kv.second != cpc) return fail(KE_ERR_UNSUPPORTED, "cores with different numbers of logical CPUs");
+  if (cpc > 8) return fail(KE_ERR_UNSUPPORTED, "more than 8 logical CPUs per core");
+  return KE_OK;
+}
+
+bool cpus_valid(const NodeState& ns) { return !ns.cpus.empty() && !ns.node.cpu_topology_invalid; }
+
+int64_t cpus_allocated(const NodeState& ns) {
+  if (ns.cpus.empty()) return ns.node.cpuset_allocated_cpus;
+  int64_t k = 0;
+  for (const ke_cpu& c : ns.cpus) k += c.ref_count > 0;
+  return k;
+}
+
+void derive_cpu_rows(const NodeState& ns, CpuRec* recs, int64_t* cs) {
+  std::memset(recs, 0, sizeof(CpuRec) * CPU_SLOTS);
+  const ke_node& n = ns.node;
+  const double ratio_f = n.cpu_amplification_ratio;
+  const double ratio_s = n.nrt_cpu_amplification_ratio > -1.5
+                             ? (n.nrt_cpu_amplification_ratio < 0 ? 0.0 : n.nrt_cpu_amplification_ratio)
+                             : (n.cpu_amplification_ratio < 0 ? 0.0 : n.cpu_amplification_ratio);
+  std::memcpy(&cs[CS_RF], &ratio_f, 8);
+  std::memcpy(&cs[CS_RS], &ratio_s, 8);
+  cs[CS_CNT] = 0;
+  if (ns.cpus.empty()) return;
+  std::vector<int32_t> cores, sockets;
+  for (const ke_cpu& c : ns.cpus) cores.push_back(c.core_id), sockets.push_back(c.socket_id);
+  std::sort(cores.begin(), cores.end());
+  cores.erase(std::unique(cores.begin(), cores.end()), cores.end());
+  std::sort(sockets.begin(), sockets.end());
+  sockets.erase(std::unique(sockets.begin(), sockets.end()), sockets.end());
+  for (const ke_cpu& c : ns.cpus) {
+    CpuRec& r = recs[c.cpu_id];
+    r.core = (uint8_t)(std::lower_bound(cores.begin(), cores.end(), c.core_id) - cores.begin());
+    r.socket = (uint8_t)(std::lower_bound(sockets.begin(), sockets.end(), c.socket_id) - sockets.begin());
+    r.numa = (uint8_t)c.numa_id;
+    r.ref = (uint8_t)c.ref_count;
+    r.excl = c.ref_count > 0 ? c.exclusive : 0;
+    r.flags = (uint8_t)(CR_VALID | (c.reserved ? CR_RESERVED : 0));
+  }
+  const int cpc = (int)(ns.cpus.size() / cores.size());
+  cs[CS_CNT] = cs_counts(recs, cpc, ns.cpu_max_ref);
+  std::vector<std::pair<int32_t, int32_t>> nodes;  // (socket, NUMA node) pairs
+  for (const ke_cpu& c : ns.cpus) nodes.push_back({c.socket_id, c.numa_id});
+  std::sort(nodes.begin(), nodes.end());
+  nodes.erase(std::unique(nodes.begin(), nodes.end()), nodes.end());
+  cs[CS_TOPO] = (int64_t)ns.cpus.size() | ((int64_t)cores.size() << 16) | ((int64_t)nodes.size() << 32) |
+                ((int64_t)sockets.size() << 48);
+}
+
+void host_cpuset_reserve(NodeState& ns, const DevPod& dp, const uint64_t* set) {
+  const int excl = (dp.flags & PF_CPU_RCB) ? pf_cpu_excl(dp.flags) : KE_CPU_EXCL_NONE;
+  uint32_t used = 0;  // NUMA ids < 32 of the new cpuset (zones carry ids < KE_MAX_NUMA)
+  int n_used = 0;
+  std::vector<int> ids;
+  for (ke_cpu& c : ns.cpus) {
+    if (!(set[c.cpu_id >> 6] >> (c.cpu_id & 63) & 1)) continue;
+    c.ref_count++;
+    c.exclusive = (uint8_t)excl;
+    if (std::find(ids.begin(), ids.end(), c.numa_id) == ids.end()) ids.push_back(c.numa_id);
+  }
+  n_used = (int)ids.size();
+  for (int id : ids)
+    if (id < 32) used |= 1u << id;
+  for (ke_numa_zone& z : ns.zones)  // NUMANodeSharedStatus after addPodAllocation
+    if (z.id < 32 && (used >> z.id & 1))
+      z.numa_status = (uint8_t)(n_used > 1 || z.numa_status == KE_NUMA_STATUS_SHARED ? KE_NUMA_STATUS_SHARED
+                                                                                    : KE_NUMA_STATUS_SINGLE);
+  ns.dirty = true;
 }
 
 void host_assign(const ke_config& cfg, NodeState& ns, const ke_pod& pod, int64_t timestamp_ns) {

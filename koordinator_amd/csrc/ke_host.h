@@ -29,6 +29,10 @@ struct NodeState {
   std::vector<AssignedPod> asg;
   // NodeResourceTopology NUMA zones + the resource manager's allocation on them
   std::vector<ke_numa_zone> zones;
+  // CPU topology + cpuset allocations (TopologyOptions.CPUTopology / ReservedCPUs / MaxRefCount,
+  // NodeAllocation.allocatedCPUs); empty = no CPU topology
+  std::vector<ke_cpu> cpus;
+  int32_t cpu_max_ref = 1;
   // DeviceShare node device cache entry (device_cache.go:518-568)
   bool has_dev_cache = false;
   std::vector<ke_device> devs;
@@ -47,6 +51,10 @@ struct Context {
   int32_t n_nodes = 0;           // 1 + highest populated index
   bool ds_enabled = false;       // some node has a device cache entry: the device SoA exists
   bool numa_enabled = false;     // some node has a NUMA topology policy: the NUMA SoA exists
+  bool cpu_enabled = false;      // some node has a CPU table: the CPU SoA exists
+  int32_t n_bind_nodes = 0;      // nodes with a CPU bind policy (a cpu request may bind CPUs there)
+  int32_t n_policy_nodes = 0;    // nodes with a NUMA topology policy
+  std::vector<uint64_t> last_cpusets;    // per pod of the last ke_schedule: 4 words (CPU-id bitset)
   std::vector<int64_t> last_numa_alloc;  // per pod of the last ke_schedule: [KE_MAX_NUMA*KE_NRES]
   std::vector<uint64_t> last_dev_alloc;  // per pod of the last ke_schedule
   DeviceState* dev = nullptr;
@@ -99,5 +107,15 @@ int validate_zones(int32_t n, const ke_numa_zone* zones);
 void derive_numa_row(const NodeState& ns, int64_t* f, uint64_t* mask);
 // host mirror of the NUMA allocation the device Reserve made: delta[z][r] per zone id
 void host_numa_reserve(NodeState& ns, const int64_t* delta /*[KE_MAX_NUMA*KE_NRES]*/);
+
+// CPU topology / cpuset binding (NodeNUMAResource with NUMA policy None)
+int validate_cpus(int32_t n, const ke_cpu* cpus, int32_t max_ref);
+bool cpus_valid(const NodeState& ns);  // a CPU table that CPUTopology.IsValid() accepts
+int64_t cpus_allocated(const NodeState& ns);  // allocatedCPUs.Size() (else ke_node.cpuset_allocated_cpus)
+// the node's CPU records (CPU_SLOTS, by CPU id) and its NUM_CS_FIELDS summary words
+void derive_cpu_rows(const NodeState& ns, CpuRec* recs, int64_t* cs);
+// host mirror of a cpuset Reserve: RefCount++ / exclusive policy on the CPUs of `set` (4 words), the
+// NUMA nodes' single / shared status (node_allocation.go:111-156)
+void host_cpuset_reserve(NodeState& ns, const DevPod& dp, const uint64_t* set);
 
 }  // namespace ke

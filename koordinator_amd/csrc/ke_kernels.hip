@@ -21,6 +21,7 @@
 #include <cstring>
 #include <vector>
 
+#include "ke_cpuacc.h"
 #include "ke_host.h"
 #include "ke_types.h"
 
@@ -51,7 +52,16 @@ struct SoA {
   uint64_t* dsm;    // DeviceShare: NUM_DS_MASKS arrays of `stride` uint64
   int64_t* nf;      // NUMA topology: NUM_NUMA_FIELDS arrays of `stride` int64 (nullptr until a NUMA node appears)
   uint64_t* nm;     // NUMA topology: `stride` uint64 zone / key masks (ke_types.h NUMA_M_*)
+  int64_t* cs;      // CPU tables: NUM_CS_FIELDS arrays of `stride` int64 (nullptr until a cpuset pod / CPU table)
+  CpuRec* cpu;      // CPU tables: CPU_SLOTS records per node, node-major
 };
+
+// Amplify (node_resource_amplification.go:170-175) with the ratio's IEEE bits from the CPU SoA
+__device__ __forceinline__ int64_t amplify_bits(int64_t q, int64_t ratio_bits) {
+  const double r = __longlong_as_double(ratio_bits);
+  if (r <= 1.0) return q;
+  return (int64_t)ceil((double)q * r);
+}
 
 // ---------------------------------------------------------------------------------------------
 // the fused per-(pod,node) evaluation
@@ -792,7 +802,9 @@ __device__ __forceinline__ void numa_reserve(const SoA& s, int64_t i, uint32_t n
 // `s`/`i` locate the node's DeviceShare state (read only for pods with PF_DS, and only when DS: the
 // batch replay never evaluates a DeviceShare pod — such a pod is alone in its batch).
 // NUMA: some node may carry a NUMA topology policy; `nv` holds node i's zones when its policy is set.
-template <bool DS, bool NUMA, bool DEFER = false, bool FB_AFF = false>
+// CPU: the pod may bind CPUs (PF_CPUSET: a singleton batch) — cpuset PreFilter state, requestCPUBind,
+// the amplified pod cpu and the required-bind-policy checks read the CPU SoA.
+template <bool DS, bool NUMA, bool DEFER = false, bool FB_AFF = false, bool CPU = false>
 __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, const DevPod& p, const KArgs& k,
                                              const SoA& s, int64_t i, const NumaNode& nv, uint32_t fb_aff = 0) {
   EvalOut o;
@@ -802,6 +814,12 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
   const uint32_t nf = n.flags;
   if (!(nf & NF_VALID)) {
     o.status = KE_CODE_ERROR;
+    o.total = -1;
+    return o;
+  }
+  if (CPU && (p.flags & PF_CPU_INVALID)) {  // NodeNUMAResource PreFilter failed (plugin.go:296-298)
+    o.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    o.reason = KE_REASON_NUMA_INVALID_REQUESTED_CPUS;
     o.total = -1;
     return o;
   }
@@ -838,6 +856,17 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
     o.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
     o.reason = KE_REASON_NUMA_POLICY_CONFLICT;
   }
+  // requestCPUBind (util.go:121-138): the pod's own cpuset state, else a node CPU bind policy binds
+  // any whole-CPU request (-1: a fractional one there is UnschedulableAndUnresolvable)
+  int rcb = 0;
+  if (CPU && !(p.flags & PF_NUMA_SKIP)) {
+    if (p.flags & PF_CPU_RCB) rcb = 1;
+    else if (p.req[0] != 0 && nf_cpu_bind(nf) != KE_NODE_CPU_BIND_NONE) rcb = (p.flags & PF_CPU_INT) ? 1 : -1;
+  }
+  if (CPU && o.status == KE_CODE_SUCCESS && rcb < 0) {
+    o.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    o.reason = KE_REASON_NUMA_INVALID_REQUESTED_CPUS;
+  }
   if (o.status == KE_CODE_SUCCESS && !(p.flags & PF_NUMA_SKIP) && p.req[0] != 0) {
     if (nf & NF_NUMA_AMP_ERR) {
       o.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
@@ -849,15 +878,40 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
       } else {
         int64_t req = n.nreq[0];
         if (req >= n.csm && n.csm > 0) req = req - n.csm + n.csaf;
-        if (p.req[0] > n.nalloc[0] - req) {
+        const int64_t pcpu = (CPU && rcb > 0) ? amplify_bits(p.req[0], s.cs[CS_RF * s.stride + i]) : p.req[0];
+        if (pcpu > n.nalloc[0] - req) {
           o.status = KE_CODE_UNSCHEDULABLE;
           o.reason = KE_REASON_NUMA_INSUFFICIENT_AMPLIFIED_CPU;
         }
       }
     }
   }
-  // ---- NodeNUMAResource.Filter under a NUMA topology policy: FilterByNUMANode + topologymanager Admit
   const int eff_pol = pod_pol ? pod_pol : node_pol;
+  // ---- cpuset binding (plugin.go:351-398): topology, bind-policy conflict, SMT alignment, and the
+  // required policies' trial allocation, which on a regular topology is a count check
+  if (CPU && rcb > 0 && o.status == KE_CODE_SUCCESS) {
+    if (!(nf & NF_CPUS_VALID)) {
+      o.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+      o.reason = KE_REASON_NUMA_INVALID_CPU_TOPOLOGY;
+    } else {
+      const int64_t cnt = s.cs[CS_CNT * s.stride + i];
+      const int preq = pf_cpu_required(p.flags), nb = nf_cpu_bind(nf);
+      const int req = nb == KE_NODE_CPU_BIND_FULL_PCPUS_ONLY ? XB_FULL : nb == KE_NODE_CPU_BIND_SPREAD_BY_PCPUS ? XB_SPREAD : preq;
+      const int64_t ncpu = p.req[0] / 1000;
+      if (preq != XB_NONE && preq != req) {
+        o.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+        o.reason = KE_REASON_NUMA_CPU_BIND_POLICY_CONFLICT;
+      } else if (req == XB_FULL && ncpu % cs_cpc(cnt) != 0) {
+        o.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+        o.reason = KE_REASON_NUMA_SMT_ALIGNMENT;
+      } else if (req != XB_NONE && eff_pol == KE_NUMA_POLICY_NONE &&
+                 ncpu > (req == XB_FULL ? cs_full(cnt) : cs_spread(cnt))) {
+        o.status = KE_CODE_UNSCHEDULABLE;
+        o.reason = KE_REASON_NUMA_INSUFFICIENT_CPUS;
+      }
+    }
+  }
+  // ---- NodeNUMAResource.Filter under a NUMA topology policy: FilterByNUMANode + topologymanager Admit
   const bool npol = NUMA && !(p.flags & PF_NUMA_SKIP) && eff_pol != KE_NUMA_POLICY_NONE;
   int32_t npol_score = 0;
   if (npol && o.status == KE_CODE_SUCCESS) {
@@ -901,10 +955,14 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
     nu = npol_score;
   } else if (!(p.flags & PF_NUMA_SKIP) && !(nf & NF_NUMA_SCORE_ZERO)) {
     bool zero = false;
-    int64_t reqc = n.nreq[0];
+    int64_t reqc = n.nreq[0], preq0 = p.req[0];
     if (p.req[0] != 0 && (nf & NF_NUMA_RATIO_S)) {
       if (nf & NF_NUMA_TOPO_INVALID) zero = true;
       else reqc = n.nreq[0] - n.csm + n.csas;
+    }
+    if (CPU && rcb != 0) {  // scoring.go:86-92: a binding pod scores its amplified cpu, 0 without a topology
+      if (rcb < 0 || !(nf & NF_CPUS_VALID)) zero = true;
+      else if (nf & NF_NUMA_RATIO_S) preq0 = amplify_bits(p.req[0], s.cs[CS_RS * s.stride + i]);
     }
     if (!zero) {
       int32_t s = 0, ws = 0;
@@ -913,7 +971,7 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
         const int32_t w = k.w_numa[q];
         const int64_t alloc = n.nalloc[q];
         if (w == 0 || alloc == 0) continue;
-        const int64_t req = (q == 0 ? reqc : n.nreq[1]) + p.req[q];
+        const int64_t req = (q == 0 ? reqc + preq0 : n.nreq[1] + p.req[1]);
         int32_t sc;
         if (k.flags & AF_NUMA_MOST) {  // mostRequestedScore  most_allocated.go:53-62
           const int64_t rq = req > alloc ? alloc : req;
@@ -975,7 +1033,7 @@ __device__ __forceinline__ void defer_push(bool want, uint64_t item, uint64_t* _
 // parity mode: full status / score matrices [pod][node]; `total` holds the LoadAware + NUMA part
 // until k_parity_finalize adds the normalized DeviceShare score.  dsmax[p] = 1 + max raw DeviceShare
 // score over the pod's feasible nodes (DefaultNormalizeScore's maxCount).
-template <bool NUMA>
+template <bool NUMA, bool CPU>
 __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_parity(SoA s, int n_nodes, const DevPod* __restrict__ pods,
                                                             int n_pods, int pods_per_block, KArgs k,
                                                             uint8_t* status, uint8_t* reason, int16_t* la,
@@ -998,7 +1056,7 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_parity(SoA s, int n_nodes, 
     uint32_t m = 0;
     bool deferred = false;
     if (live) {
-      const EvalOut o = eval_pair<true, NUMA, NUMA>(n, expired, pods[p], k, s, i, nv);
+      const EvalOut o = eval_pair<true, NUMA, NUMA, false, CPU>(n, expired, pods[p], k, s, i, nv);
       deferred = NUMA && o.status == STATUS_DEFERRED;
       const int64_t o_idx = (int64_t)p * n_nodes + i;
       status[o_idx] = o.status;
@@ -1045,7 +1103,7 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_parity_finalize(int n_nodes, KAr
 // (always alone in its batch) also dsraw[node] = raw DeviceShare score + 1 (0 when filtered out).
 // Nodes [lo, hi) of the SoA (this rank's shard); scores stay indexed by the global node index.
 // DS: the batch's pod is a DeviceShare pod (the DeviceShare path stays out of plain batches' code).
-template <bool DS, bool NUMA>
+template <bool DS, bool NUMA, bool CPU>
 __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi, const DevPod* __restrict__ pods,
                                                            const int32_t* __restrict__ batch_base, int batch_pods,
                                                            int pods_per_block, KArgs k, uint16_t* __restrict__ scores,
@@ -1064,7 +1122,7 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
   const int p1 = min(batch_pods, p0 + pods_per_block);
   for (int p = p0; p < p1; p++) {
     const DevPod& pod = pods[base + p];
-    const EvalOut o = eval_pair<DS, NUMA, NUMA>(n, expired, pod, k, s, i, nv);
+    const EvalOut o = eval_pair<DS, NUMA, NUMA, false, CPU>(n, expired, pod, k, s, i, nv);
     scores[(int64_t)p * score_stride + i] = (uint16_t)(o.total + 1);
     if (NUMA) defer_push(o.status == STATUS_DEFERRED, ((uint64_t)p << 32) | (uint32_t)i, defer_list, defer_cnt);
     if (DS && (pod.flags & PF_DS)) dsraw[i] = o.total >= 0 ? (uint16_t)(o.ds + 1) : (uint16_t)0;
@@ -1797,6 +1855,167 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
   }
 }
 
+// --- cpuset pods: Reserve with the CPU accumulator --------------------------------------------
+// LoadAware assign + NodeInfo.Requested on the SoA row of the chosen node (k_resolve's patch)
+__device__ void reserve_row(const SoA& s, int64_t node, uint32_t nf, const DevPod& pod) {
+  const int64_t st = s.stride;
+  int64_t* f = s.f + node;
+  if ((nf & NF_HAS_METRIC) && !(nf & NF_NM_NIL)) {
+    for (int q = 0; q < 2; q++) {
+      if (nf & nf_fh_on(0, q)) f[(F_FH + q) * st] -= pod.est[q];
+      f[(F_SA + q) * st] -= pod.est[q];
+      if (pod.flags & PF_PROD) {
+        if (nf & nf_fh_on(1, q)) f[(F_FH + 2 + q) * st] -= pod.est[q];
+        f[(F_SA + 2 + q) * st] -= pod.est[q];
+      }
+    }
+  }
+  f[F_NREQ * st] += pod.req[0];
+  f[(F_NREQ + 1) * st] += pod.req[1];
+}
+
+// allocateCPUSet without a NUMA hint (resource_manager.go:353-459): the node's CPU table into LDS,
+// getAvailableCPUs, filterCPUsByRequiredCPUBindPolicy (:655-695), takePreferredCPUs without preferred
+// CPUs (= takeCPUs), satisfiedRequiredCPUBindPolicy (:697-718).  Thread 0 only; a.res = the cpuset.
+__device__ bool cpuset_allocate(const SoA& s, int64_t node, uint32_t nf, const DevPod& pod, AccLds& a) {
+  const int64_t st = s.stride;
+  const CpuRec* recs = s.cpu + node * CPU_SLOTS;
+  const int64_t cnt = s.cs[CS_CNT * st + node], topo = s.cs[CS_TOPO * st + node];
+  const int max_ref = cs_max_ref(cnt), cpc = cs_cpc(cnt);
+  a.t.num_cpus = (int)(topo & 0xffff);
+  a.t.num_cores = (int)((topo >> 16) & 0xffff);
+  a.t.num_nodes = (int)((topo >> 32) & 0xffff);
+  a.t.num_sockets = (int)((topo >> 48) & 0xffff);
+  // getCPUBindPolicy (util.go:101-119)
+  const int preq = pf_cpu_required(pod.flags), nb = nf_cpu_bind(nf);
+  bool required = true;
+  int bind = preq;
+  if (preq == XB_NONE) {
+    if (nb == KE_NODE_CPU_BIND_SPREAD_BY_PCPUS) bind = XB_SPREAD;
+    else if (nb == KE_NODE_CPU_BIND_FULL_PCPUS_ONLY) bind = XB_FULL;
+    else required = false, bind = pf_cpu_preferred(pod.flags);
+  }
+  uint8_t navail_core[CPU_SLOTS];
+  for (int k = 0; k < CPU_SLOTS; k++) navail_core[k] = 0, a.ex_core[k] = 0, a.ex_node[k] = 0;
+  for (int c = 0; c < CPU_SLOTS; c++) {
+    const CpuRec r = recs[c];
+    a.cpu[c] = r;
+    a.res[c] = 0;
+    a.alloc[c] = cpu_available(r, max_ref) ? 1 : 0;
+    a.aref[c] = r.ref;
+    if (a.alloc[c]) navail_core[r.core]++;
+    if ((r.flags & CR_VALID) && r.ref > 0) {  // exclusiveInCores / exclusiveInNUMANodes of the allocated CPUs
+      if (r.excl == KE_CPU_EXCL_PCPU_LEVEL) a.ex_core[r.core] = 1;
+      else if (r.excl == KE_CPU_EXCL_NUMA_NODE_LEVEL) a.ex_node[r.numa] = 1;
+    }
+  }
+  if (required) {
+    uint8_t seen[CPU_SLOTS / 8] = {};
+    for (int c = 0; c < CPU_SLOTS; c++) {
+      if (!a.alloc[c]) continue;
+      const int k = a.cpu[c].core;
+      const bool lowest = !(seen[k >> 3] >> (k & 7) & 1);
+      seen[k >> 3] |= (uint8_t)(1u << (k & 7));
+      if ((bind == XB_FULL && navail_core[k] != cpc) || (bind == XB_SPREAD && !lowest)) a.alloc[c] = 0;
+    }
+  }
+  const int ncpu = (int)(pod.req[0] / 1000);
+  if (acc_count_alloc(a) < ncpu) return false;
+  a.max_ref = max_ref;
+  a.needed = ncpu;
+  a.excl_policy = (pod.flags & PF_CPU_RCB) ? pf_cpu_excl(pod.flags) : KE_CPU_EXCL_NONE;
+  a.exclusive = a.excl_policy == KE_CPU_EXCL_PCPU_LEVEL || a.excl_policy == KE_CPU_EXCL_NUMA_NODE_LEVEL;
+  a.numa_most = (nf & NF_CPU_NUMA_MOST) ? 1 : 0;
+  if (!acc_take_cpus(a, bind)) return false;
+  if (required) {
+    uint8_t seen[CPU_SLOTS / 8] = {};
+    int n = 0, ncore = 0;
+    for (int c = 0; c < CPU_SLOTS; c++) {
+      if (!a.res[c]) continue;
+      n++;
+      const int k = a.cpu[c].core;
+      if (!(seen[k >> 3] >> (k & 7) & 1)) ncore++;
+      seen[k >> 3] |= (uint8_t)(1u << (k & 7));
+    }
+    if (bind == XB_FULL && ncore * cpc != n) return false;
+    if (bind == XB_SPREAD && ncore != n) return false;
+  }
+  return true;
+}
+
+// resourceManager.Update -> addPodAllocation (node_allocation.go:111-156): RefCount++ and the pod's
+// exclusive policy on the new cpuset, the allocated-CPU count of the amplified cpu (row F_CS*) and the
+// availability counts.  The zones' NUMA status is left to the host mirror (re-derived rows).
+__device__ void cpuset_commit(const SoA& s, int64_t node, const DevPod& pod, AccLds& a, uint64_t* set) {
+  const int64_t st = s.stride;
+  CpuRec* recs = s.cpu + node * CPU_SLOTS;
+  const int excl = (pod.flags & PF_CPU_RCB) ? pf_cpu_excl(pod.flags) : KE_CPU_EXCL_NONE;
+  int64_t allocated = 0;
+  for (int c = 0; c < CPU_SLOTS; c++) {
+    if (a.res[c]) {
+      set[c >> 6] |= 1ull << (c & 63);
+      a.cpu[c].ref++;
+      a.cpu[c].excl = (uint8_t)excl;
+      recs[c] = a.cpu[c];
+    }
+    allocated += (a.cpu[c].flags & CR_VALID) && a.cpu[c].ref > 0;
+  }
+  int64_t* f = s.f + node;
+  const int64_t cs_milli = allocated * 1000;
+  f[F_CSM * st] = cs_milli;
+  f[F_CSAF * st] = amplify_bits(cs_milli, s.cs[CS_RF * st + node]);
+  f[F_CSAS * st] = amplify_bits(cs_milli, s.cs[CS_RS * st + node]);
+  const int64_t cnt = s.cs[CS_CNT * st + node];
+  s.cs[CS_CNT * st + node] = cs_counts(a.cpu, cs_cpc(cnt), cs_max_ref(cnt));
+}
+
+// A cpuset pod's singleton batch after k_select: selectHost's node, then Reserve in profile order —
+// LoadAware, NodeNUMAResource (the cpuset; failure = Reserve fails, the pod stays unplaced),
+// DeviceShare.  One thread: the accumulator is sequential (sorted lists, greedy takes).
+template <bool DS>
+__global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __restrict__ pods, int32_t* __restrict__ batch_base,
+                                                       KArgs k, const uint32_t* __restrict__ cand,
+                                                       const int32_t* __restrict__ cand_cnt, int32_t* __restrict__ chosen,
+                                                       int32_t* __restrict__ chosen_score, int32_t global_offset,
+                                                       uint64_t* __restrict__ stamps, uint64_t* __restrict__ pstamps,
+                                                       int batch_index, uint64_t* __restrict__ dev_alloc,
+                                                       int64_t* __restrict__ numa_alloc, uint64_t* __restrict__ cpusets) {
+  __shared__ AccLds a;
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const int base = *batch_base;
+  const DevPod pod = pods[base];
+  uint32_t w = 0;
+  const int cnt = min(cand_cnt[0], KMAX);
+  for (int c = 0; c < cnt; c++) w = max(w, cand[c]);
+  int32_t out_node = -1, out_score = -1;
+  uint64_t alloc = 0, set[4] = {0, 0, 0, 0};
+  if (w) {
+    const int64_t node = key_node(w);
+    const uint32_t nf = s.flags[node];
+    const bool rcb = !(pod.flags & PF_NUMA_SKIP) &&
+                     ((pod.flags & PF_CPU_RCB) ||
+                      (pod.req[0] != 0 && nf_cpu_bind(nf) != KE_NODE_CPU_BIND_NONE && (pod.flags & PF_CPU_INT)));
+    const bool ok = !rcb || ((nf & NF_CPUS_VALID) && cpuset_allocate(s, node, nf, pod, a));
+    if (ok) {
+      reserve_row(s, node, nf, pod);
+      if (rcb) cpuset_commit(s, node, pod, a, set);
+      if (DS && (pod.flags & PF_DS) && (nf & NF_DS_CACHE)) alloc = ds_reserve(s, node, pod, k);
+      out_node = (int32_t)node + global_offset;
+      out_score = key_score(w);
+    }
+  }
+  chosen[base] = out_node;
+  chosen_score[base] = out_score;
+  dev_alloc[base] = alloc;
+  for (int q = 0; q < 4; q++) cpusets[(int64_t)base * 4 + q] = set[q];
+  if (numa_alloc)
+    for (int t = 0; t < 16; t++) numa_alloc[(int64_t)base * 16 + t] = 0;
+  for (int u = 0; u < 6; u++) pstamps[8 * batch_index + u] = t0;  // no prologue: all "replay"
+  *batch_base = base + 1;
+  stamps[batch_index + 1] = __builtin_amdgcn_s_memrealtime();
+}
+
 __global__ void k_stamp(uint64_t* stamps) { stamps[0] = __builtin_amdgcn_s_memrealtime(); }
 
 // ---------------------------------------------------------------------------------------------
@@ -1852,6 +2071,12 @@ struct DeviceState {
   int64_t defer_cap = 0;           // bytes
   uint32_t* d_defer_cnt = nullptr; // one counter per batch of a ke_schedule (or the ke_eval launch)
   int64_t defer_cnt_cap = 0;       // bytes
+  // CPU tables (cpuset pods)
+  bool cpu_alloc = false;          // soa.cs / soa.cpu allocated
+  int64_t* d_cpurows = nullptr;    // staging for CPU table uploads
+  int64_t cpu_staging_cap = 0;     // nodes
+  uint64_t* d_cpusets = nullptr;   // [n_pods][4] cpuset of each pod (ke_schedule)
+  int64_t cpusets_cap = 0;         // bytes
 };
 
 // Contiguous node range of shard `rank`: 512-aligned chunks (k_select's 16-B loads stay aligned).
@@ -1910,7 +2135,8 @@ void device_destroy(Context* ctx) {
                   d->d_cand,    d->d_cand_cnt, d->d_batch_base, d->d_chosen,     d->d_chosen_score,
                   d->d_stamps,  d->d_parity, d->d_best,       d->d_gath,         d->soa.ds,   d->soa.dsm,
                   d->d_dsraw,   d->d_dsmax,  d->d_devalloc,   d->d_dsrows,       d->soa.nf,   d->soa.nm,
-                  d->d_numaalloc, d->d_numarows, d->d_defer, d->d_defer_cnt};
+                  d->d_numaalloc, d->d_numarows, d->d_defer, d->d_defer_cnt, d->soa.cs, d->soa.cpu,
+                  d->d_cpurows, d->d_cpusets};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (d->stream) (void)hipStreamDestroy(d->stream);
@@ -2011,6 +2237,32 @@ static int ensure_numa(Context* ctx) {
   return KE_OK;
 }
 
+constexpr int CPU_ROW_WORDS = CPU_SLOTS + NUM_CS_FIELDS;  // records (one int64 each) + summary
+
+__global__ void k_scatter_cpu(SoA s, const int64_t* __restrict__ rows, const int32_t* __restrict__ idx, int n) {
+  const int t = blockIdx.x;
+  if (t >= n) return;
+  const int64_t i = idx[t];
+  const int64_t* r = rows + (int64_t)t * CPU_ROW_WORDS;
+  reinterpret_cast<int64_t*>(s.cpu + i * CPU_SLOTS)[threadIdx.x] = r[threadIdx.x];
+  if (threadIdx.x < NUM_CS_FIELDS) s.cs[threadIdx.x * s.stride + i] = r[CPU_SLOTS + threadIdx.x];
+}
+
+// The CPU SoA: every node needs its summary words once a cpuset pod is evaluated (the amplified-cpu
+// filter of a binding pod reads the node's ratio even without a CPU table).
+static int ensure_cpu(Context* ctx) {
+  DeviceState* d = ctx->dev;
+  if (d->cpu_alloc || !ctx->cpu_enabled) return KE_OK;
+  HIP_OK(hipMalloc(&d->soa.cs, sizeof(int64_t) * NUM_CS_FIELDS * d->capacity));
+  HIP_OK(hipMalloc(&d->soa.cpu, sizeof(CpuRec) * CPU_SLOTS * d->capacity));
+  HIP_OK(hipMemsetAsync(d->soa.cs, 0, sizeof(int64_t) * NUM_CS_FIELDS * d->capacity, d->stream));
+  HIP_OK(hipMemsetAsync(d->soa.cpu, 0, sizeof(CpuRec) * CPU_SLOTS * d->capacity, d->stream));
+  d->cpu_alloc = true;
+  for (int32_t i = 0; i < ctx->n_nodes; i++)
+    if (ctx->nodes[i].valid) ctx->nodes[i].dirty = true;
+  return KE_OK;
+}
+
 // Re-derive rows of dirty / time-expired nodes and scatter them into the SoA.
 int device_refresh(Context* ctx, int64_t now) {
   DeviceState* d = ctx->dev;
@@ -2018,6 +2270,10 @@ int device_refresh(Context* ctx, int64_t now) {
   if (rc) return rc;
   rc = ensure_numa(ctx);
   if (rc) return rc;
+  rc = ensure_cpu(ctx);
+  if (rc) return rc;
+  std::vector<int64_t> crows;  // CPU tables + summaries of the dirty nodes
+  std::vector<int32_t> cidx;
   std::vector<Row> rows;
   std::vector<int32_t> idx;
   std::vector<int64_t> dsrows;  // DeviceShare rows of the dirty nodes (the device state is not time-dependent)
@@ -2043,6 +2299,12 @@ int device_refresh(Context* ctx, int64_t now) {
       derive_numa_row(ns, &nrows[o], &mask);
       nrows[o + NUM_NUMA_FIELDS] = (int64_t)mask;
       nidx.push_back(i);
+    }
+    if (ns.dirty && d->cpu_alloc) {
+      const size_t o = crows.size();
+      crows.resize(o + CPU_ROW_WORDS);
+      derive_cpu_rows(ns, reinterpret_cast<CpuRec*>(&crows[o]), &crows[o + CPU_SLOTS]);
+      cidx.push_back(i);
     }
     ns.valid_until = vu;
     ns.dirty = false;
@@ -2079,6 +2341,20 @@ int device_refresh(Context* ctx, int64_t now) {
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(d->stream));  // `nrows` is a local host vector
   }
+  if (!cidx.empty()) {
+    const int64_t n = (int64_t)cidx.size();
+    if (d->cpu_staging_cap < n) {
+      if (d->d_cpurows) HIP_OK(hipFree(d->d_cpurows));
+      HIP_OK(hipMalloc(&d->d_cpurows, sizeof(int64_t) * CPU_ROW_WORDS * n + sizeof(int32_t) * n));
+      d->cpu_staging_cap = n;
+    }
+    int32_t* didx = reinterpret_cast<int32_t*>(d->d_cpurows + CPU_ROW_WORDS * n);
+    HIP_OK(hipMemcpyAsync(d->d_cpurows, crows.data(), sizeof(int64_t) * crows.size(), hipMemcpyHostToDevice, d->stream));
+    HIP_OK(hipMemcpyAsync(didx, cidx.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, d->stream));
+    hipLaunchKernelGGL(k_scatter_cpu, dim3((unsigned)n), dim3(CPU_SLOTS), 0, d->stream, d->soa, d->d_cpurows, didx, (int)n);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(d->stream));  // `crows` is a local host vector
+  }
   if (rows.empty()) return KE_OK;
   HIP_OK(hipSetDevice(d->device));
   const int64_t n = (int64_t)rows.size();
@@ -2102,7 +2378,10 @@ static int upload_pods(Context* ctx, int32_t n_pods, const ke_pod* pods) {
   DeviceState* d = ctx->dev;
   std::vector<DevPod>& dp = d->host_pods;
   dp.resize((size_t)n_pods);
-  for (int32_t p = 0; p < n_pods; p++) dp[p] = make_dev_pod(ctx->cfg, pods[p]);
+  for (int32_t p = 0; p < n_pods; p++) {
+    dp[p] = make_dev_pod(ctx->cfg, pods[p]);
+    if (ctx->n_bind_nodes > 0 && dp[p].req[0] > 0) dp[p].flags |= PF_CPUSET;  // a node policy may bind it
+  }
   int rc = ensure((void**)&d->d_pods, &d->pods_cap, sizeof(DevPod) * (int64_t)std::max(n_pods, 1));
   if (rc) return rc;
   HIP_OK(hipMemcpyAsync(d->d_pods, dp.data(), sizeof(DevPod) * n_pods, hipMemcpyHostToDevice, d->stream));
@@ -2135,6 +2414,9 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
   HIP_OK(hipMemsetAsync(d->d_best, 0, sizeof(uint32_t) * 2 * P, d->stream));
   const KArgs k = make_kargs(ctx, now);
   const int ppb = 8;
+  bool cpu = false;
+  for (const DevPod& q : d->host_pods) cpu = cpu || (q.flags & PF_CPUSET);
+  if (cpu && !d->cpu_alloc) return fail(KE_ERR_DEVICE, "cpuset pod without the CPU SoA");
   if (N > 0) {
     dim3 grid((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((P + ppb - 1) / ppb));
     if (d->numa_alloc) {
@@ -2143,14 +2425,14 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
       rc = ensure((void**)&d->d_defer_cnt, &d->defer_cnt_cap, sizeof(uint32_t));
       if (rc) return rc;
       HIP_OK(hipMemsetAsync(d->d_defer_cnt, 0, sizeof(uint32_t), d->stream));
-      hipLaunchKernelGGL(k_eval_parity<true>, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, (int)N, d->d_pods, (int)P,
+      hipLaunchKernelGGL((cpu ? k_eval_parity<true, true> : k_eval_parity<true, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, (int)N, d->d_pods, (int)P,
                          ppb, k, d_status, d_reason, d_la, d_numa, d_ds, d_total, d_dsmax, d->d_defer, d->d_defer_cnt);
       HIP_OK(hipGetLastError());
       hipLaunchKernelGGL(k_numa_fallback<true>, dim3(FALLBACK_BLOCKS), dim3(64), 0, d->stream, d->soa, d->d_pods,
                          d->d_batch_base, k, d->d_defer, d->d_defer_cnt, d->d_scores, d->capacity, (int)N, d_status,
                          d_reason, d_la, d_numa, d_ds, d_total, d_dsmax);
     } else {
-      hipLaunchKernelGGL(k_eval_parity<false>, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, (int)N, d->d_pods, (int)P,
+      hipLaunchKernelGGL((cpu ? k_eval_parity<false, true> : k_eval_parity<false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, (int)N, d->d_pods, (int)P,
                          ppb, k, d_status, d_reason, d_la, d_numa, d_ds, d_total, d_dsmax, nullptr, nullptr);
     }
     HIP_OK(hipGetLastError());
@@ -2191,19 +2473,29 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   // Batches: runs of up to B pods without DeviceShare requests (exact speculative batching, DESIGN.md
   // §4), and every DeviceShare pod alone: its NormalizeScore needs the max over all feasible nodes of
   // the current state.
+  // A pod that may bind CPUs is alone in its batch too: its Reserve runs the CPU accumulator
+  // (k_cpuset_reserve) and may fail, and later pods read the CPU table it patches.
   const int B = ctx->cfg.pod_batch;
-  std::vector<std::pair<int, bool>> batches;  // (pods, DeviceShare singleton)
+  struct Batch {
+    int pods;
+    bool ds, cpu;  // singleton of a DeviceShare pod / of a pod that may bind CPUs
+  };
+  std::vector<Batch> batches;
   for (int32_t p = 0; p < n_pods;) {
-    if (d->host_pods[p].flags & PF_DS) {
-      batches.push_back({1, true});
+    const uint32_t f = d->host_pods[p].flags;
+    if (f & (PF_DS | PF_CPUSET)) {
+      batches.push_back({1, (f & PF_DS) != 0, (f & PF_CPUSET) != 0});
       p++;
       continue;
     }
     int bp = 0;
-    while (p + bp < n_pods && bp < B && !(d->host_pods[p + bp].flags & PF_DS)) bp++;
-    batches.push_back({bp, false});
+    while (p + bp < n_pods && bp < B && !(d->host_pods[p + bp].flags & (PF_DS | PF_CPUSET))) bp++;
+    batches.push_back({bp, false, false});
     p += bp;
   }
+  bool any_cpu = false;
+  for (const Batch& b : batches) any_cpu = any_cpu || b.cpu;
+  if (any_cpu && !d->cpu_alloc) return fail(KE_ERR_DEVICE, "cpuset pod without the CPU SoA");
   const int n_batches = (int)batches.size();
   const int64_t out_bytes = sizeof(int32_t) * (int64_t)n_pods;
   if (d->out_cap < n_pods) {
@@ -2219,6 +2511,9 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     HIP_OK(hipMalloc(&d->d_devalloc, sizeof(uint64_t) * n_pods));
     d->out_cap = n_pods;
   }
+  rc = ensure((void**)&d->d_cpusets, &d->cpusets_cap, sizeof(uint64_t) * 4 * (int64_t)n_pods);
+  if (rc) return rc;
+  HIP_OK(hipMemsetAsync(d->d_cpusets, 0, sizeof(uint64_t) * 4 * n_pods, d->stream));
   const bool numa = d->numa_alloc;
   if (numa && !d->d_numaalloc) HIP_OK(hipMalloc(&d->d_numaalloc, sizeof(int64_t) * 16 * d->out_cap));
   if (numa) {  // deferred-pair list of one batch (reused) + a counter per batch
@@ -2247,8 +2542,8 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   }
   const bool sharded = d->world > 1 || d->comm;
   for (int b = 0; b < n_batches; b++) {
-    const int bp = batches[b].first;
-    const bool ds = batches[b].second;
+    const int bp = batches[b].pods;
+    const bool ds = batches[b].ds, cpu = batches[b].cpu;
     const bool prof = every > 0 && b % every == 0;
     hipEvent_t* pe = prof ? &ev[(size_t)(b / every) * 4] : nullptr;
     if (prof) HIP_OK(hipEventRecord(pe[0], d->stream));
@@ -2258,12 +2553,14 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       if (sharded && !d->loopback) shard_range(N, d->rank, d->world, &lo, &hi);
       if (hi > lo) {
         dim3 grid((unsigned)((hi - lo + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((bp + ppb - 1) / ppb));
-        auto eval = ds ? (numa ? k_eval_batch<true, true> : k_eval_batch<true, false>)
-                       : (numa ? k_eval_batch<false, true> : k_eval_batch<false, false>);
+        // a binding pod never meets a NUMA policy (ke_capi check_cpuset): its batch skips the NUMA path
+        auto eval = cpu ? (ds ? k_eval_batch<true, false, true> : k_eval_batch<false, false, true>)
+                        : ds ? (numa ? k_eval_batch<true, true, false> : k_eval_batch<true, false, false>)
+                             : (numa ? k_eval_batch<false, true, false> : k_eval_batch<false, false, false>);
         uint32_t* dcnt = numa ? d->d_defer_cnt + b : nullptr;
         hipLaunchKernelGGL(eval, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, lo, hi, d->d_pods, d->d_batch_base, bp,
                            ppb, k, d->d_scores, d->capacity, d->d_dsraw, d->d_defer, dcnt);
-        if (numa && !ds)  // DeviceShare pods never meet a NUMA policy: nothing deferred in their batches
+        if (numa && !ds && !cpu)  // DeviceShare pods never meet a NUMA policy: nothing deferred in their batches
           hipLaunchKernelGGL(k_numa_fallback<false>, dim3(FALLBACK_BLOCKS), dim3(64), 0, d->stream, d->soa, d->d_pods,
                              d->d_batch_base, k, d->d_defer, dcnt, d->d_scores, d->capacity, 0, nullptr, nullptr,
                              nullptr, nullptr, nullptr, nullptr, nullptr);
@@ -2308,7 +2605,12 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       HIP_OK(hipMemsetAsync(d->d_cand_cnt, 0, sizeof(int32_t) * MAX_BATCH, d->stream));
     }
     if (prof) HIP_OK(hipEventRecord(pe[2], d->stream));
-    {
+    if (cpu) {
+      hipLaunchKernelGGL((ds ? k_cpuset_reserve<true> : k_cpuset_reserve<false>), dim3(1), dim3(64), 0, d->stream, d->soa,
+                         d->d_pods, d->d_batch_base, k, d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score,
+                         ctx->cfg.global_node_offset, d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc,
+                         numa ? d->d_numaalloc : nullptr, d->d_cpusets);
+    } else {
       auto resolve = ds ? (numa ? k_resolve<true, true> : k_resolve<true, false>)
                         : (numa ? k_resolve<false, true> : k_resolve<false, false>);
       hipLaunchKernelGGL(resolve, dim3(1), dim3(RES_THREADS), 0, d->stream, d->soa, d->d_pods, d->d_batch_base, bp, k,
@@ -2323,6 +2625,9 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   if (score) HIP_OK(hipMemcpyAsync(score, d->d_chosen_score, out_bytes, hipMemcpyDeviceToHost, d->stream));
   ctx->last_dev_alloc.assign((size_t)n_pods, 0);
   HIP_OK(hipMemcpyAsync(ctx->last_dev_alloc.data(), d->d_devalloc, sizeof(uint64_t) * n_pods, hipMemcpyDeviceToHost,
+                        d->stream));
+  ctx->last_cpusets.assign((size_t)n_pods * 4, 0);
+  HIP_OK(hipMemcpyAsync(ctx->last_cpusets.data(), d->d_cpusets, sizeof(uint64_t) * 4 * n_pods, hipMemcpyDeviceToHost,
                         d->stream));
   ctx->last_numa_alloc.clear();
   if (numa) {
@@ -2406,14 +2711,14 @@ int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t 
   const int ppb = 8;
   HIP_OK(hipMemsetAsync(d->d_batch_base, 0, sizeof(int32_t), d->stream));
   dim3 grid((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((n_pods + ppb - 1) / ppb));
-  hipLaunchKernelGGL((k_eval_batch<false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base, n_pods,
+  hipLaunchKernelGGL((k_eval_batch<false, false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base, n_pods,
                      ppb, k, d->d_scores, d->capacity, d->d_dsraw, nullptr, nullptr);  // warm
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   HIP_OK(hipEventRecord(e0, d->stream));
   for (int it = 0; it < iters; it++)
-    hipLaunchKernelGGL((k_eval_batch<false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base,
+    hipLaunchKernelGGL((k_eval_batch<false, false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base,
                        n_pods, ppb, k, d->d_scores, d->capacity, d->d_dsraw, nullptr, nullptr);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(e1, d->stream));

@@ -54,7 +54,11 @@ enum NodeFlag : uint32_t {
   NF_NUMA_POLICY0 = 1u << 16,     // 2 bits: the node's NUMA topology policy (KE_NUMA_POLICY_*)
   NF_NUMA_OPT_ERR = 1u << 18,     // getResourceOptions fails (amplification annotation unparsable)
   NF_NUMA_AL_AMP = 1u << 19,      // the cpu amplification ratio in force is > 1: every allocation entry has a cpu key
+  NF_CPU_BIND0 = 1u << 20,        // 2 bits: the node's CPU bind policy (KE_NODE_CPU_BIND_*)
+  NF_CPUS_VALID = 1u << 22,       // the node has a valid CPU topology table (cpuset pods can bind)
+  NF_CPU_NUMA_MOST = 1u << 23,    // GetNUMAAllocateStrategy == MostAllocated (cpu accumulator order)
 };
+KE_HD inline int nf_cpu_bind(uint32_t f) { return (int)((f >> 20) & 3u); }
 KE_HD inline int nf_numa_policy(uint32_t f) { return (int)((f >> 16) & 3u); }
 KE_HD inline int pf_numa_policy(uint32_t f) { return (int)((f >> 9) & 3u); }
 
@@ -88,7 +92,57 @@ enum PodFlag : uint32_t {
   PF_DS_H_RATIO = 1u << 8,     // per-GPU request has gpu-memory-ratio (fill: ratio -> bytes)
   PF_NUMA_POLICY0 = 1u << 9,   // 2 bits: the pod's NUMATopologySpec policy (KE_NUMA_POLICY_*)
   PF_NUMA_EXCL_REQ = 1u << 11, // SingleNUMANodeExclusive Required (explicit, or defaulted by a pod policy)
+  // NodeNUMAResource PreFilter cpuset state (plugin.go:251-312)
+  PF_CPU_INVALID = 1u << 12,   // non-integer cpuset request: UnschedulableAndUnresolvable everywhere
+  PF_CPU_RCB = 1u << 13,       // state.requestCPUBind
+  PF_CPU_INT = 1u << 14,       // cpu request is whole CPUs (a node CPU bind policy may force binding)
+  PF_CPU_REQ0 = 1u << 15,      // 2 bits: state.requiredCPUBindPolicy (XB_NONE / XB_FULL / XB_SPREAD)
+  PF_CPU_PREF0 = 1u << 17,     // 2 bits: state.preferredCPUBindPolicy
+  PF_CPU_EXCL0 = 1u << 19,     // 2 bits: state.preferredCPUExclusivePolicy (KE_CPU_EXCL_*)
+  PF_CPUSET = 1u << 21,        // the pod may bind CPUs on some node: singleton batch, cpuset Reserve
 };
+KE_HD inline int pf_cpu_required(uint32_t f) { return (int)((f >> 15) & 3u); }
+KE_HD inline int pf_cpu_preferred(uint32_t f) { return (int)((f >> 17) & 3u); }
+KE_HD inline int pf_cpu_excl(uint32_t f) { return (int)((f >> 19) & 3u); }
+
+// ---- CPU topology + cpuset allocation state (allocated when the first node CPU table appears) ----
+// Per node CPU_SLOTS records indexed by CPU id (node-major: 2 KiB per node), plus a summary SoA the
+// evaluation reads: CS_RF / CS_RS = the filter / score cpu amplification ratios (IEEE double bits),
+// CS_CNT = packed counts (cs_* accessors) of the CPUs available to a new cpuset.
+constexpr int CPU_SLOTS = 256;  // == KE_MAX_CPUS
+enum : uint8_t { CR_VALID = 1, CR_RESERVED = 2 };
+enum { XB_NONE = 0, XB_FULL = 1, XB_SPREAD = 2 };  // bind policies as the cpu accumulator sees them
+struct CpuRec {  // one logical CPU: ranks of the reference core / socket ids, the NUMA id as given
+  uint8_t core, numa, socket, ref, excl, flags, pad0, pad1;
+};
+static_assert(sizeof(CpuRec) == 8, "CpuRec layout");
+constexpr int CS_RF = 0, CS_RS = 1, CS_CNT = 2, CS_TOPO = 3, NUM_CS_FIELDS = 4;
+// CS_CNT: CPUs in fully available cores (bits 0-15), cores with an available CPU (16-31), CPUs per
+// core (32-39), MaxRefCount (40-47).  CS_TOPO: CPUTopology's NumCPUs / NumCores / NumNodes /
+// NumSockets (cpu_topology.go:45-105) in 16-bit lanes.
+KE_HD inline int64_t cs_pack(int full, int spread, int cpc, int max_ref) {
+  return (int64_t)full | ((int64_t)spread << 16) | ((int64_t)cpc << 32) | ((int64_t)max_ref << 40);
+}
+KE_HD inline int cs_full(int64_t c) { return (int)(c & 0xffff); }
+KE_HD inline int cs_spread(int64_t c) { return (int)((c >> 16) & 0xffff); }
+KE_HD inline int cs_cpc(int64_t c) { return (int)((c >> 32) & 0xff); }
+KE_HD inline int cs_max_ref(int64_t c) { return (int)((c >> 40) & 0xff); }
+// NodeAllocation.getAvailableCPUs (node_allocation.go:192-219): not reserved, RefCount < MaxRefCount
+KE_HD inline bool cpu_available(const CpuRec& r, int max_ref) {
+  return (r.flags & CR_VALID) && !(r.flags & CR_RESERVED) && !(r.ref > 0 && r.ref >= max_ref);
+}
+// the counts above over one node's records
+KE_HD inline int64_t cs_counts(const CpuRec* recs, int cpc, int max_ref) {
+  uint8_t a_core[CPU_SLOTS] = {};
+  for (int c = 0; c < CPU_SLOTS; c++)
+    if (cpu_available(recs[c], max_ref)) a_core[recs[c].core]++;
+  int full = 0, spread = 0;
+  for (int k = 0; k < CPU_SLOTS; k++) {
+    if (a_core[k] == cpc && cpc > 0) full += cpc;
+    if (a_core[k] > 0) spread++;
+  }
+  return cs_pack(full, spread, cpc, max_ref);
+}
 
 // host-side packed row (staging for uploads, debug readback)
 struct Row {

@@ -126,6 +126,11 @@ class Evaluator:
         zones = np.ascontiguousarray(zones, dtype=abi.NUMA_ZONE_DTYPE)
         self._check(self.lib.ke_node_numa_set(self.h, i, len(zones), abi.ptr(zones)))
 
+    def set_cpus(self, i, cpus, max_ref_count=1):
+        """CPU topology + cpuset allocation state (model.make_cpus(...)); an empty table clears it."""
+        cpus = np.ascontiguousarray(cpus, dtype=abi.CPU_DTYPE)
+        self._check(self.lib.ke_node_cpus_set(self.h, i, len(cpus), abi.ptr(cpus), max_ref_count))
+
     def estimate_pod(self, pod):
         est = np.zeros(2, np.int64)
         self._check(self.lib.ke_estimate_pod(self.h, C.byref(pod), abi.ptr(est)))
@@ -173,6 +178,8 @@ class Evaluator:
         self._check(self.lib.ke_last_device_allocations(self.h, len(pods), abi.ptr(self.last_device_allocations)))
         self.last_numa_allocations = np.zeros((len(pods), 16), np.int64)
         self._check(self.lib.ke_last_numa_allocations(self.h, len(pods), abi.ptr(self.last_numa_allocations)))
+        self.last_cpusets = np.zeros((len(pods), 4), np.uint64)
+        self._check(self.lib.ke_last_cpusets(self.h, len(pods), abi.ptr(self.last_cpusets)))
         return chosen, score
 
     def stats(self):

@@ -198,7 +198,8 @@ def make_pod(name="pod", namespace="default", requests=None, limits=None, contai
              init_containers=(), overhead=None, priority=None, labels=None, owner_kind=None, uid=None,
              scheduled_at=None, initialized_at=None, custom_factors=None,
              custom_seconds_after_scheduled=None, custom_seconds_after_initialized=None,
-             terminated=False, numa_policy=None, numa_exclusive=None):
+             terminated=False, numa_policy=None, numa_exclusive=None, cpu_bind_required=None,
+             cpu_bind_preferred=None, cpu_exclusive=None):
     """A pod as the plugins see it.  `requests`/`limits` describe one container (MakePod().Req());
     `containers` gives the full list.  Times are ns.  numa_policy / numa_exclusive: the
     scheduling.koordinator.sh/numa-topology-spec annotation ('BestEffort' | 'Restricted' |
@@ -242,7 +243,29 @@ def make_pod(name="pod", namespace="default", requests=None, limits=None, contai
     p.is_terminated = 1 if terminated else 0
     p.numa_topology_policy = {None: 0, "": 0, "BestEffort": 1, "Restricted": 2, "SingleNUMANode": 3}[numa_policy]
     p.numa_exclusive = {None: 0, "": 0, "Preferred": 1, "Required": 2}[numa_exclusive]
+    # scheduling.koordinator.sh/resource-spec: requiredCPUBindPolicy / preferredCPUBindPolicy /
+    # preferredCPUExclusivePolicy
+    p.cpu_bind_required = CPU_BIND_BY_NAME[cpu_bind_required]
+    p.cpu_bind_preferred = CPU_BIND_BY_NAME[cpu_bind_preferred]
+    p.cpu_exclusive = CPU_EXCL_BY_NAME[cpu_exclusive]
     return p
+
+
+CPU_BIND_BY_NAME = {None: 0, "": 0, "Default": 1, "FullPCPUs": 2, "SpreadByPCPUs": 3, "ConstrainedBurst": 4}
+CPU_EXCL_BY_NAME = {None: 0, "": 0, "None": 0, "PCPULevel": 1, "NUMANodeLevel": 2}
+NODE_CPU_BIND_BY_NAME = {None: 0, "": 0, "None": 0, "FullPCPUsOnly": 1, "SpreadByPCPUs": 2}
+
+
+def make_cpus(rows, allocated=None, reserved=()):
+    """A node's CPU table: rows [cpu, core, numa, socket]; allocated {cpu: (ref_count, exclusive name)}."""
+    arr = np.zeros(len(rows), dtype=abi.CPU_DTYPE)
+    for i, (cpu, core, numa, sock) in enumerate(rows):
+        arr[i]["cpu_id"], arr[i]["core_id"], arr[i]["numa_id"], arr[i]["socket_id"] = cpu, core, numa, sock
+        ref, excl = (allocated or {}).get(cpu, (0, None))
+        arr[i]["ref_count"] = ref
+        arr[i]["exclusive"] = CPU_EXCL_BY_NAME[excl]
+        arr[i]["reserved"] = 1 if cpu in reserved else 0
+    return arr
 
 
 def _thr(arr, m):

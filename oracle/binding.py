@@ -47,7 +47,7 @@ def load():
         "or_numa_score": (i64, [V, C.POINTER(abi.Pod), i32]),
         "or_estimate_pod": (None, [V, C.POINTER(abi.Pod), V]),
         "or_eval": (C.c_int, [V, i32, V, i64, V, V, V, V, V, V, V, C.c_int]),
-        "or_schedule": (C.c_int, [V, i32, V, i64, V, V, V, V, C.c_int]),
+        "or_schedule": (C.c_int, [V, i32, V, i64, V, V, V, V, V, C.c_int]),
         "or_node_devices_set": (C.c_int, [V, i32, i32, V]),
         "or_node_devices_delete": (C.c_int, [V, i32]),
         "or_ds_prefilter": (C.c_int, [C.POINTER(abi.Pod), C.POINTER(C.c_int), V, V, V]),
@@ -55,6 +55,7 @@ def load():
         "or_normalize_scores": (None, [V, i32]),
         "or_topology_merge": (C.c_int, [i32, C.c_uint32, i32, V, V, V, V, V, V, V, V, V]),
         "or_node_numa_set": (C.c_int, [V, i32, i32, V]),
+        "or_node_cpus_set": (C.c_int, [V, i32, i32, V, i32]),
         "or_numa_distribute": (C.c_int, [V, i32, V, C.c_uint32, V]),
         "or_numa_exclusive_ok": (C.c_int, [C.c_uint32, i32, V, i32]),
         "or_take_cpus": (C.c_int, [V, i32, i32, V, V, V, i32, i32, i32, i32, V, V]),
@@ -152,6 +153,10 @@ class Oracle:
     def delete_devices(self, i):
         assert self.lib.or_node_devices_delete(self.h, i) == 0
 
+    def set_cpus(self, i, cpus, max_ref_count=1):
+        cpus = np.ascontiguousarray(cpus, dtype=abi.CPU_DTYPE)
+        assert self.lib.or_node_cpus_set(self.h, i, len(cpus), abi.ptr(cpus), max_ref_count) == 0
+
     def numa_distribute(self, i, pod, mask):
         """(ok, out[16]) of tryBestToDistributeEvenly on NUMA ids `mask` (None if options fail)."""
         out = np.zeros(16, np.int64)
@@ -245,9 +250,10 @@ class Oracle:
         score = np.zeros(len(pods), np.int32)
         self.last_device_allocations = np.zeros(len(pods), np.uint64)
         self.last_numa_allocations = np.zeros((len(pods), 16), np.int64)
+        self.last_cpusets = np.zeros((len(pods), 4), np.uint64)
         rc = self.lib.or_schedule(self.h, len(pods), abi.ptr(pods), int(now_ns), abi.ptr(chosen), abi.ptr(score),
                                   abi.ptr(self.last_device_allocations), abi.ptr(self.last_numa_allocations),
-                                  n_threads)
+                                  abi.ptr(self.last_cpusets), n_threads)
         if rc != 0:
             raise RuntimeError(f"oracle schedule rc={rc}")
         return chosen, score

@@ -55,7 +55,16 @@ typedef struct or_node {
   int has_dev_cache; /* nodeDeviceCache.getNodeDevice != nil */
   int32_t n_dev;
   ke_device dev[KE_DEV_TYPES * KE_MAX_MINORS];
+  struct or_cpus* cpus; /* CPU topology + allocated CPUs (NULL: no CPU topology) */
 } or_node;
+
+/* TopologyOptions.CPUTopology / ReservedCPUs / MaxRefCount + NodeAllocation.allocatedCPUs */
+typedef struct or_cpus {
+  acc_topo t;
+  acc_alloc al; /* present = RefCount > 0 */
+  uint8_t reserved[ACC_MAX_CPUS];
+  int max_ref;
+} or_cpus;
 
 struct or_cluster {
   ke_config cfg;
@@ -364,11 +373,152 @@ static int pod_is_cpuset(const ke_pod* pod) {
          pod->requests[KE_RES_CPU] > 0;
 }
 static int pod_unsupported(const ke_pod* pod) {
-  return pod_is_cpuset(pod) || pod->has_resource_spec || pod->has_unsupported_device_requests;
+  return pod->has_resource_spec || pod->has_unsupported_device_requests;
 }
 static int node_unsupported(const ke_node* n) {
   return n->numa_topology_policy < 0 || n->numa_topology_policy > KE_NUMA_POLICY_SINGLE_NUMA_NODE ||
-         n->cpu_bind_policy != 0;
+         n->cpu_bind_policy < 0 || n->cpu_bind_policy > KE_NODE_CPU_BIND_SPREAD_BY_PCPUS;
+}
+
+/* ---- cpuset binding (PreFilter plugin.go:251-312, requestCPUBind util.go:121-138) ----------------- */
+typedef struct cpuset_state {
+  int rcb;        /* state.requestCPUBind */
+  int required;   /* state.requiredCPUBindPolicy */
+  int preferred;  /* state.preferredCPUBindPolicy */
+  int excl;       /* state.preferredCPUExclusivePolicy */
+  int num_cpus;   /* numCPUsNeeded */
+  int invalid;    /* PreFilter: non-integer cpuset request -> UnschedulableAndUnresolvable */
+} cpuset_state;
+
+static void cpuset_prefilter(const or_cluster* c, const ke_pod* pod, cpuset_state* st) {
+  memset(st, 0, sizeof *st);
+  const int64_t cpu = pod->requests[KE_RES_CPU];
+  st->num_cpus = (int)(cpu / 1000);
+  if (!pod_is_cpuset(pod) && !((pod->qos_class == KE_QOS_LSE || pod->qos_class == KE_QOS_LSR) &&
+                               pod->priority_class == KE_PRIORITY_PROD))
+    return; /* AllowUseCPUSet */
+  int bind = pod->cpu_bind_preferred;
+  if (bind == KE_CPU_BIND_UNSET || bind == KE_CPU_BIND_DEFAULT) bind = c->cfg.numa.default_cpu_bind_policy;
+  int required = pod->cpu_bind_required;
+  if (required == KE_CPU_BIND_DEFAULT) required = c->cfg.numa.default_cpu_bind_policy;
+  if (required != KE_CPU_BIND_UNSET) bind = required;
+  if (bind == KE_CPU_BIND_FULL_PCPUS || bind == KE_CPU_BIND_SPREAD_BY_PCPUS) {
+    if (cpu % 1000 != 0) {
+      st->invalid = 1;
+      return;
+    }
+    if (cpu > 0) {
+      st->rcb = 1;
+      st->required = required;
+      st->preferred = bind;
+      st->excl = pod->cpu_exclusive;
+    }
+  }
+}
+
+/* requestCPUBind (util.go:121-138): -1 = UnschedulableAndUnresolvable (non-integer cpus) */
+static int request_cpu_bind(const cpuset_state* st, const ke_pod* pod, int node_bind) {
+  if (st->rcb) return 1;
+  const int64_t cpu = pod->requests[KE_RES_CPU];
+  if (cpu == 0) return 0;
+  if (node_bind != KE_NODE_CPU_BIND_NONE) return cpu % 1000 != 0 ? -1 : 1;
+  return 0;
+}
+
+static int cpus_valid(const or_node* n) {
+  return n->cpus && !n->node.cpu_topology_invalid && n->cpus->t.num_sockets && n->cpus->t.num_nodes &&
+         n->cpus->t.num_cores && n->cpus->t.num_cpus;
+}
+
+/* GetAvailableCPUs(node) allocated.CPUs().Size() (resource_manager.go:497-511) */
+static int64_t cpus_allocated_count(const or_node* n) {
+  if (!n->cpus) return n->node.cpuset_allocated_cpus;
+  int64_t k = 0;
+  for (int c = 0; c < ACC_MAX_CPUS; c++) k += n->cpus->al.present[c];
+  return k;
+}
+
+/* NodeAllocation.getAvailableCPUs (node_allocation.go:192-219) without preferred CPUs */
+static void cpus_available(const or_cpus* x, uint64_t* avail) {
+  memset(avail, 0, sizeof(uint64_t) * ACC_WORDS);
+  for (int c = 0; c < ACC_MAX_CPUS; c++)
+    if (x->t.valid[c] && !x->reserved[c] && !(x->al.present[c] && x->al.ref[c] >= x->max_ref))
+      avail[c >> 6] |= 1ull << (c & 63);
+}
+
+/* getCPUBindPolicy (util.go:101-119): the policy and whether it is required */
+static int cpu_bind_policy_of(const cpuset_state* st, int node_bind, int* required) {
+  if (st->required != KE_CPU_BIND_UNSET) {
+    *required = 1;
+    return st->required;
+  }
+  *required = 0;
+  if (node_bind == KE_NODE_CPU_BIND_SPREAD_BY_PCPUS) {
+    *required = 1;
+    return KE_CPU_BIND_SPREAD_BY_PCPUS;
+  }
+  if (node_bind == KE_NODE_CPU_BIND_FULL_PCPUS_ONLY) {
+    *required = 1;
+    return KE_CPU_BIND_FULL_PCPUS;
+  }
+  return st->preferred;
+}
+
+static int acc_bind(int bind) {
+  return bind == KE_CPU_BIND_FULL_PCPUS ? ACC_BIND_FULL_PCPUS
+                                        : bind == KE_CPU_BIND_SPREAD_BY_PCPUS ? ACC_BIND_SPREAD_BY_PCPUS : ACC_BIND_NONE;
+}
+
+/* GetNUMAAllocateStrategy (util.go:33-47): 1 = NUMAMostAllocated */
+static int numa_most_allocated(const or_cluster* c, const or_node* n) {
+  if (n->node.numa_allocate_strategy == KE_NUMA_ALLOCATE_MOST) return 1;
+  if (n->node.numa_allocate_strategy == KE_NUMA_ALLOCATE_LEAST) return 0;
+  return c->cfg.numa.numa_strategy == KE_STRATEGY_MOST_ALLOCATED;
+}
+
+/* allocateCPUSet without NUMA hint (resource_manager.go:353-459): 0 and the cpuset, or -1 */
+static int cpuset_allocate(const or_cluster* c, const or_node* n, const cpuset_state* st, uint64_t* result) {
+  const or_cpus* x = n->cpus;
+  uint64_t avail[ACC_WORDS];
+  cpus_available(x, avail);
+  int required;
+  const int bind = cpu_bind_policy_of(st, n->node.cpu_bind_policy, &required);
+  const int cpc = acc_cpus_per_core(&x->t);
+  if (required) { /* filterCPUsByRequiredCPUBindPolicy (:655-695) */
+    uint64_t keep[ACC_WORDS] = {0};
+    for (int c1 = 0; c1 < ACC_MAX_CPUS; c1++) {
+      if (!(avail[c1 >> 6] >> (c1 & 63) & 1)) continue;
+      int in_core = 0, lowest = 1;
+      for (int c2 = 0; c2 < ACC_MAX_CPUS; c2++)
+        if ((avail[c2 >> 6] >> (c2 & 63) & 1) && x->t.core[c2] == x->t.core[c1]) {
+          in_core++;
+          if (c2 < c1) lowest = 0;
+        }
+      if ((bind == KE_CPU_BIND_FULL_PCPUS && in_core == cpc) || (bind == KE_CPU_BIND_SPREAD_BY_PCPUS && lowest) ||
+          (bind != KE_CPU_BIND_FULL_PCPUS && bind != KE_CPU_BIND_SPREAD_BY_PCPUS))
+        keep[c1 >> 6] |= 1ull << (c1 & 63);
+    }
+    memcpy(avail, keep, sizeof keep);
+  }
+  int navail = 0;
+  for (int w = 0; w < ACC_WORDS; w++) navail += __builtin_popcountll(avail[w]);
+  if (navail < st->num_cpus) return -1;
+  if (acc_take_preferred_cpus(&x->t, x->max_ref, avail, NULL, &x->al, st->num_cpus, acc_bind(bind), st->excl,
+                              numa_most_allocated(c, n), result) != 0)
+    return -1;
+  if (required) { /* satisfiedRequiredCPUBindPolicy (:697-718) */
+    int ncpu = 0, cores[ACC_MAX_CPUS], ncore = 0;
+    for (int c1 = 0; c1 < ACC_MAX_CPUS; c1++) {
+      if (!(result[c1 >> 6] >> (c1 & 63) & 1)) continue;
+      ncpu++;
+      int f = 0;
+      for (int k = 0; k < ncore && !f; k++) f = cores[k] == x->t.core[c1];
+      if (!f) cores[ncore++] = x->t.core[c1];
+    }
+    if (bind == KE_CPU_BIND_FULL_PCPUS && ncore * cpc != ncpu) return -1;
+    if (bind == KE_CPU_BIND_SPREAD_BY_PCPUS && ncore != ncpu) return -1;
+  }
+  return 0;
 }
 
 /* ---------------------------------------------------------------------------------------------- */
@@ -474,7 +624,7 @@ static int pod_requests_zero(const ke_pod* pod) { /* quotav1.IsZero(PodRequests)
 }
 
 /* Plugin.Filter  plugin.go:318-406 -> filterAmplifiedCPUs :408-442 */
-static int numa_filter_amplified(const or_node* n, const ke_pod* pod, int* reason);
+static int numa_filter_amplified(const or_node* n, const ke_pod* pod, int rcb, int* reason);
 static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod, int policy, int exclusive,
                       uint32_t* affinity, int* reason);
 
@@ -492,14 +642,50 @@ int or_numa_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* re
   const or_node* n = &c->nodes[node];
   *reason = KE_REASON_NONE;
   if (pod_requests_zero(pod)) return KE_CODE_SUCCESS; /* state.skip */
+  cpuset_state st;
+  cpuset_prefilter(c, pod, &st);
+  if (st.invalid) { /* PreFilter (plugin.go:296-298) */
+    *reason = KE_REASON_NUMA_INVALID_REQUESTED_CPUS;
+    return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+  }
   int exclusive;
   const int policy = effective_policy(n, pod, &exclusive);
   if (policy < 0) {
     *reason = KE_REASON_NUMA_POLICY_CONFLICT;
     return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
   }
-  const int code = numa_filter_amplified(n, pod, reason);
+  const int rcb = request_cpu_bind(&st, pod, n->node.cpu_bind_policy);
+  if (rcb < 0) {
+    *reason = KE_REASON_NUMA_INVALID_REQUESTED_CPUS;
+    return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+  }
+  const int code = numa_filter_amplified(n, pod, rcb, reason);
   if (code != KE_CODE_SUCCESS) return code;
+  if (rcb) { /* plugin.go:351-398 */
+    if (!cpus_valid(n)) {
+      *reason = KE_REASON_NUMA_INVALID_CPU_TOPOLOGY;
+      return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    }
+    int required = st.required;
+    if (n->node.cpu_bind_policy == KE_NODE_CPU_BIND_FULL_PCPUS_ONLY) required = KE_CPU_BIND_FULL_PCPUS;
+    else if (n->node.cpu_bind_policy == KE_NODE_CPU_BIND_SPREAD_BY_PCPUS) required = KE_CPU_BIND_SPREAD_BY_PCPUS;
+    if (st.required != KE_CPU_BIND_UNSET && st.required != required) {
+      *reason = KE_REASON_NUMA_CPU_BIND_POLICY_CONFLICT;
+      return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    }
+    if (required == KE_CPU_BIND_FULL_PCPUS && st.num_cpus % acc_cpus_per_core(&n->cpus->t) != 0) {
+      *reason = KE_REASON_NUMA_SMT_ALIGNMENT;
+      return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    }
+    if (required != KE_CPU_BIND_UNSET && policy == KE_NUMA_POLICY_NONE) { /* trial Allocate */
+      uint64_t cs[ACC_WORDS];
+      if (cpuset_allocate(c, n, &st, cs) != 0) {
+        *reason = KE_REASON_NUMA_INSUFFICIENT_CPUS;
+        return KE_CODE_UNSCHEDULABLE;
+      }
+      return KE_CODE_SUCCESS;
+    }
+  }
   if (policy == KE_NUMA_POLICY_NONE) return KE_CODE_SUCCESS;
   if (n->n_zone == 0) { /* FilterByNUMANode  topology_hint.go:31-41 */
     *reason = KE_REASON_NUMA_MISSING_RESOURCES;
@@ -510,8 +696,8 @@ int or_numa_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* re
 }
 
 /* filterAmplifiedCPUs  plugin.go:408-442 */
-static int numa_filter_amplified(const or_node* n, const ke_pod* pod, int* reason) {
-  const int64_t pod_cpu = pod->requests[KE_RES_CPU];
+static int numa_filter_amplified(const or_node* n, const ke_pod* pod, int rcb, int* reason) {
+  int64_t pod_cpu = pod->requests[KE_RES_CPU];
   if (pod_cpu == 0) return KE_CODE_SUCCESS;
   if (n->node.amplification_error) {
     *reason = KE_REASON_NUMA_INVALID_AMPLIFICATION_RATIO;
@@ -523,7 +709,8 @@ static int numa_filter_amplified(const or_node* n, const ke_pod* pod, int* reaso
     *reason = KE_REASON_NUMA_INVALID_CPU_TOPOLOGY;
     return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
   }
-  const int64_t allocated_milli = n->node.cpuset_allocated_cpus * 1000;
+  if (rcb) pod_cpu = amplify(pod_cpu, ratio);
+  const int64_t allocated_milli = cpus_allocated_count(n) * 1000;
   int64_t requested = n->node.requested[KE_RES_CPU];
   if (requested >= allocated_milli && allocated_milli > 0) {
     requested = requested - allocated_milli;
@@ -539,13 +726,13 @@ static int numa_filter_amplified(const or_node* n, const ke_pod* pod, int* reaso
 /* resourceAllocationScorer.score (scoring.go:210-226) with least/mostResourceScorer
  * (least_allocated.go:30-58, most_allocated.go:30-62) over cpu and memory. */
 static int64_t numa_resource_score_as(const ke_numa_args* na, int strategy, const int64_t* requested,
-                                      const int64_t* allocatable, const ke_pod* pod) {
+                                      const int64_t* allocatable, const int64_t* podreq) {
   int64_t score = 0, wsum = 0;
   for (int r = 0; r < KE_NRES; r++) {
     int64_t w = na->weights[r];
     if (w == KE_ABSENT) continue;
     int64_t alloc = allocatable[r];
-    int64_t req = requested[r] + pod->requests[r];
+    int64_t req = requested[r] + podreq[r];
     if (alloc == 0) continue; /* calculateResourceAllocatableRequest result dropped */
     int64_t s;
     if (strategy == KE_STRATEGY_MOST_ALLOCATED) {
@@ -560,8 +747,8 @@ static int64_t numa_resource_score_as(const ke_numa_args* na, int strategy, cons
   return wsum ? score / wsum : 0;
 }
 static int64_t numa_resource_score(const ke_numa_args* na, const int64_t* requested, const int64_t* allocatable,
-                                   const ke_pod* pod) {
-  return numa_resource_score_as(na, na->strategy, requested, allocatable, pod);
+                                   const int64_t* podreq) {
+  return numa_resource_score_as(na, na->strategy, requested, allocatable, podreq);
 }
 
 /* ---------------------------------------------------------------------------------------------- */
@@ -581,6 +768,14 @@ typedef struct numa_view {
   int64_t al[KE_MAX_NUMA][KE_NRES];      /* totalAllocated (cpu adjusted for amplified cpusets) */
   uint8_t al_has[KE_MAX_NUMA][KE_NRES];
 } numa_view;
+
+/* allocatedCPUs.CPUsInNUMANodes(id).Size(): from the CPU table when the node has one */
+static int zone_cpusets(const or_node* nd, int id, int given) {
+  if (!nd->cpus) return given;
+  int k = 0;
+  for (int c = 0; c < ACC_MAX_CPUS; c++) k += nd->cpus->al.present[c] && nd->cpus->t.node[c] == id;
+  return k;
+}
 
 /* getResourceOptions -> amplifyNUMANodeResources (util.go:78-98) + getAvailableNUMANodeResources
  * (node_allocation.go:221-243).  Returns -1 on an amplification-ratio annotation error. */
@@ -614,7 +809,7 @@ static int numa_view_build(const or_node* nd, numa_view* v) {
         al[r] = has[r] ? zn->allocated[r] : 0;
       }
       if (ratio > 1.0) { /* the cpu key is (re)written even when the entry had none */
-        const int64_t cs = (int64_t)zn->cpuset_cpus * 1000;
+        const int64_t cs = (int64_t)zone_cpusets(nd, zn->id, zn->cpuset_cpus) * 1000;
         al[KE_RES_CPU] = al[KE_RES_CPU] - cs + amplify(cs, ratio);
         has[KE_RES_CPU] = 1;
       }
@@ -727,7 +922,7 @@ static void numa_generate_hints(const or_cluster* c, const numa_view* v, const k
       /* numaScorer.score(requested = total - available, total, pod) with the NUMA strategy */
       int64_t req[KE_NRES];
       for (int r = 0; r < KE_NRES; r++) req[r] = total[r] - avail[r] > 0 ? total[r] - avail[r] : 0;
-      const int64_t score = numa_resource_score_as(&c->cfg.numa, c->cfg.numa.numa_strategy, req, total, pod);
+      const int64_t score = numa_resource_score_as(&c->cfg.numa, c->cfg.numa.numa_strategy, req, total, pod->requests);
       int64_t out[KE_MAX_NUMA][KE_NRES];
       if (numa_distribute(v, mask, pod, out))
         for (int r = 0; r < KE_NRES; r++) { /* generator.generateHints per resource */
@@ -1104,7 +1299,7 @@ int64_t or_numa_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
       alloc[0] = n->node.allocatable[KE_RES_CPU];
       alloc[1] = n->node.allocatable[KE_RES_MEMORY];
     }
-    return numa_resource_score(&c->cfg.numa, req, alloc, pod);
+    return numa_resource_score(&c->cfg.numa, req, alloc, pod->requests);
   }
   /* getResourceOptions -> amplifyNUMANodeResources (util.go:78-87) */
   double ratio;
@@ -1114,14 +1309,22 @@ int64_t or_numa_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
     if (n->node.amplification_error) return 0;
     ratio = n->node.cpu_amplification_ratio < 0 ? 0.0 : n->node.cpu_amplification_ratio;
   }
+  /* requestCPUBind (scoring.go:86-92): a cpuset pod scores 0 without a valid CPU topology, and its
+   * cpu request is amplified (getResourceOptions, plugin.go:634-640) */
+  cpuset_state st;
+  cpuset_prefilter(c, pod, &st);
+  const int rcb = request_cpu_bind(&st, pod, n->node.cpu_bind_policy);
+  if (rcb < 0 || (rcb && !cpus_valid(n))) return 0;
+  int64_t podreq[KE_NRES] = {pod->requests[KE_RES_CPU], pod->requests[KE_RES_MEMORY]};
+  if (rcb && ratio > 1.0) podreq[KE_RES_CPU] = amplify(podreq[KE_RES_CPU], ratio);
   int64_t requested[KE_NRES] = {n->node.requested[KE_RES_CPU], n->node.requested[KE_RES_MEMORY]};
   if (!(pod->requests[KE_RES_CPU] == 0 || ratio <= 1.0)) {
     if (n->node.cpu_topology_invalid) return 0;
-    const int64_t allocated_milli = n->node.cpuset_allocated_cpus * 1000;
+    const int64_t allocated_milli = cpus_allocated_count(n) * 1000;
     requested[KE_RES_CPU] -= allocated_milli;
     requested[KE_RES_CPU] += amplify(allocated_milli, ratio);
   }
-  return numa_resource_score(&c->cfg.numa, requested, n->node.allocatable, pod);
+  return numa_resource_score(&c->cfg.numa, requested, n->node.allocatable, podreq);
 }
 
 
@@ -1587,9 +1790,77 @@ void or_destroy(or_cluster* c) {
     free(c->nodes[i].pm);
     free(c->nodes[i].agg);
     free(c->nodes[i].asg);
+    free(c->nodes[i].cpus);
   }
   free(c->nodes);
   free(c);
+}
+
+int or_node_cpus_set(or_cluster* c, int32_t node, int32_t n, const ke_cpu* cpus, int32_t max_ref) {
+  if (node < 0 || node >= c->n) return KE_ERR_NOT_FOUND;
+  or_node* nd = &c->nodes[node];
+  if (n <= 0) {
+    free(nd->cpus);
+    nd->cpus = NULL;
+    return n < 0 ? KE_ERR_INVALID : KE_OK;
+  }
+  if (n > ACC_MAX_CPUS || max_ref < 1) return KE_ERR_INVALID;
+  or_cpus* x = (or_cpus*)calloc(1, sizeof(or_cpus));
+  for (int i = 0; i < n; i++) {
+    const int id = cpus[i].cpu_id;
+    if (id < 0 || id >= ACC_MAX_CPUS || x->t.valid[id] || cpus[i].ref_count < 0 || cpus[i].exclusive > 2) {
+      free(x);
+      return KE_ERR_INVALID;
+    }
+    x->t.valid[id] = 1;
+    x->t.core[id] = cpus[i].core_id;
+    x->t.node[id] = cpus[i].numa_id;
+    x->t.socket[id] = cpus[i].socket_id;
+    x->reserved[id] = cpus[i].reserved;
+    if (cpus[i].ref_count > 0) {
+      x->al.present[id] = 1;
+      x->al.ref[id] = cpus[i].ref_count;
+      x->al.excl[id] = cpus[i].exclusive;
+    }
+  }
+  acc_topo_finish(&x->t);
+  x->max_ref = max_ref;
+  free(nd->cpus);
+  nd->cpus = x;
+  return KE_OK;
+}
+
+/* NodeNUMAResource Reserve of a cpuset pod on a node without NUMA policy: the allocation
+ * (allocateCPUSet) and resourceManager.Update -> addPodAllocation (node_allocation.go:111-156):
+ * RefCount++ and the pod's exclusive policy per CPU, the NUMA nodes' single / shared status.
+ * Returns -1 when the allocation fails (Reserve fails: the pod is not placed). */
+static int or_cpuset_reserve(or_cluster* c, const ke_pod* pod, int32_t node, uint64_t* out) {
+  or_node* n = &c->nodes[node];
+  memset(out, 0, sizeof(uint64_t) * ACC_WORDS);
+  if (pod_requests_zero(pod)) return 0;
+  cpuset_state st;
+  cpuset_prefilter(c, pod, &st);
+  const int rcb = request_cpu_bind(&st, pod, n->node.cpu_bind_policy);
+  if (rcb <= 0) return 0;
+  if (!cpus_valid(n) || cpuset_allocate(c, n, &st, out) != 0) return -1;
+  or_cpus* x = n->cpus;
+  int used[KE_MAX_NUMA + 64], nu = 0;
+  for (int cpu = 0; cpu < ACC_MAX_CPUS; cpu++) {
+    if (!(out[cpu >> 6] >> (cpu & 63) & 1)) continue;
+    x->al.present[cpu] = 1;
+    x->al.ref[cpu]++;
+    x->al.excl[cpu] = st.excl;
+    int f = 0;
+    for (int k = 0; k < nu && !f; k++) f = used[k] == x->t.node[cpu];
+    if (!f && nu < KE_MAX_NUMA + 64) used[nu++] = x->t.node[cpu];
+  }
+  for (int k = 0; k < nu; k++) /* NUMANodeSharedStatus after adding the pod to sharedNode / singleNUMANode */
+    for (int z = 0; z < n->n_zone; z++)
+      if (n->zone[z].id == used[k])
+        n->zone[z].numa_status = (uint8_t)(nu > 1 || n->zone[z].numa_status == KE_NUMA_STATUS_SHARED
+                                               ? KE_NUMA_STATUS_SHARED
+                                               : KE_NUMA_STATUS_SINGLE);
+  return 0;
 }
 
 int or_node_numa_set(or_cluster* c, int32_t node, int32_t n, const ke_numa_zone* zones) {
@@ -1769,7 +2040,21 @@ typedef struct eval_out {
  * (scheduler-config.yaml:68-73), then the raw Score of each plugin for a feasible node. */
 static void eval_pair(const or_cluster* c, const ke_pod* pod, int32_t node, int64_t now, eval_out* o) {
   int reason = 0;
-  int code = or_la_filter(c, pod, node, now, &reason);
+  int code = KE_CODE_SUCCESS;
+  /* PreFilter failures fail the pod on every node before any Filter runs (profile order
+   * NodeNUMAResource, DeviceShare): a cpuset pod with a non-integer cpu request, invalid device requests */
+  cpuset_state st;
+  cpuset_prefilter(c, pod, &st);
+  ds_pod d;
+  ds_prepare_pod(pod, &d);
+  if (!pod_requests_zero(pod) && st.invalid) {
+    code = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    reason = KE_REASON_NUMA_INVALID_REQUESTED_CPUS;
+  } else if (d.status) {
+    code = d.status;
+    reason = KE_REASON_DS_INVALID_REQUEST;
+  }
+  if (code == KE_CODE_SUCCESS) code = or_la_filter(c, pod, node, now, &reason);
   if (code == KE_CODE_SUCCESS) code = or_numa_filter(c, pod, node, &reason);
   if (code == KE_CODE_SUCCESS) code = or_ds_filter(c, pod, node, &reason);
   o->status = (uint8_t)code;
@@ -1807,8 +2092,15 @@ void or_normalize_scores(int64_t* scores, int32_t n) {
 }
 
 static int check_supported(const or_cluster* c, int32_t n_pods, const ke_pod* pods) {
-  int ds = 0, numa = 0;
+  int ds = 0, numa = 0, cpuset = 0, node_bind = 0;
+  for (int i = 0; i < c->n; i++) node_bind |= c->nodes[i].node.cpu_bind_policy != KE_NODE_CPU_BIND_NONE;
   for (int p = 0; p < n_pods; p++) {
+    cpuset_state st;
+    cpuset_prefilter(c, &pods[p], &st);
+    if (st.rcb || (node_bind && pods[p].requests[KE_RES_CPU] > 0)) {
+      cpuset = 1;
+      if (pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE) numa = 1;
+    }
     if (pod_unsupported(&pods[p])) return KE_ERR_UNSUPPORTED;
     if (pods[p].numa_topology_policy < 0 || pods[p].numa_topology_policy > KE_NUMA_POLICY_SINGLE_NUMA_NODE ||
         pods[p].numa_exclusive < 0 || pods[p].numa_exclusive > KE_NUMA_EXCLUSIVE_REQUIRED)
@@ -1824,8 +2116,9 @@ static int check_supported(const or_cluster* c, int32_t n_pods, const ke_pod* po
     if (node_unsupported(&c->nodes[i].node)) return KE_ERR_UNSUPPORTED;
     if (c->nodes[i].node.numa_topology_policy != KE_NUMA_POLICY_NONE) numa = 1;
   }
-  /* DeviceShare's own NUMA hints (deviceshare/topology_hint.go) are not restated */
-  if (ds && numa) return KE_ERR_UNSUPPORTED;
+  /* DeviceShare's own NUMA hints (deviceshare/topology_hint.go) are not restated; neither are the cpuset
+   * hints and allocations under a NUMA topology policy */
+  if ((ds || cpuset) && numa) return KE_ERR_UNSUPPORTED;
   return KE_OK;
 }
 
@@ -1877,7 +2170,7 @@ int or_eval(const or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now
 }
 
 int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t* chosen, int32_t* score,
-                uint64_t* dev_alloc, int64_t* numa_alloc, int n_threads) {
+                uint64_t* dev_alloc, int64_t* numa_alloc, uint64_t* cpusets, int n_threads) {
   int rc = check_supported(c, n_pods, pods);
   if (rc) return rc;
   const int64_t N = c->n;
@@ -1890,10 +2183,17 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
   eval_out* o = (eval_out*)malloc(sizeof(eval_out) * (size_t)(N > 0 ? N : 1));
   for (int p = 0; p < n_pods; p++) {
     int16_t bs;
-    const int32_t b = eval_pod(c, &pods[p], now, o, &bs);
+    int32_t b = eval_pod(c, &pods[p], now, o, &bs);
     chosen[p] = b;
     if (score) score[p] = b >= 0 ? bs : -1;
     uint64_t mask = 0;
+    uint64_t cs[ACC_WORDS] = {0, 0, 0, 0};
+    if (b >= 0 && or_cpuset_reserve(c, &pods[p], b, cs) != 0) { /* Reserve failed: not placed */
+      chosen[p] = -1;
+      if (score) score[p] = -1;
+      b = -1;
+    }
+    if (cpusets) memcpy(cpusets + (int64_t)p * ACC_WORDS, cs, sizeof cs);
     if (b >= 0) {
       /* Reserve in profile order: LoadAware podAssignCache.assign (load_aware.go:192-195) at `now`,
        * DeviceShare device allocation (plugin.go:426-492); framework assume: NodeInfo.Requested. */

@@ -33,6 +33,7 @@ int or_pod_unassign(or_cluster* c, int32_t node, int64_t uid);
 int or_pods_assign(or_cluster* c, int32_t n, const int32_t* nodes, const ke_pod* pods, const int64_t* ts);
 int or_node_devices_set(or_cluster* c, int32_t node, int32_t n, const ke_device* devs);
 int or_node_numa_set(or_cluster* c, int32_t node, int32_t n, const ke_numa_zone* zones);
+int or_node_cpus_set(or_cluster* c, int32_t node, int32_t n, const ke_cpu* cpus, int32_t max_ref);
 int or_node_devices_delete(or_cluster* c, int32_t node);
 
 /* Per-plugin entry points for one (pod, node) pair (golden-vector tests). */
@@ -70,7 +71,7 @@ int or_eval(const or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now
             int32_t* best, int n_threads);
 /* Sequential scheduling, same contract as ke_schedule (mutates the oracle's state). */
 int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int32_t* chosen,
-                int32_t* score, uint64_t* dev_alloc, int64_t* numa_alloc, int n_threads);
+                int32_t* score, uint64_t* dev_alloc, int64_t* numa_alloc, uint64_t* cpusets, int n_threads);
 
 /* filterNodeUsage's usage percentage, exposed for the threshold-folding property tests:
  * int64(math.Round(float64(used)/float64(total)*100)) (load_aware.go:299). */

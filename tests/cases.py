@@ -257,3 +257,27 @@ def cpu_bits(cpus):
 
 def bits_cpus(b):
     return [c for c in range(256) if (int(b[c >> 6]) >> (c & 63)) & 1]
+
+
+# ---- cpuset Filter / Reserve vectors (cpuset.json) ------------------------------------------------
+def cpuset_pod(spec):
+    kind = spec["kind"]
+    if kind == "be":
+        return model.make_pod(requests={"kubernetes.io/batch-cpu": "4000"}, priority=5500)
+    labels = {"koordinator.sh/qosClass": "LSR" if kind == "cpuset" else "LS"}
+    return model.make_pod(requests={"cpu": spec["cpu"]}, labels=labels, priority=9500,
+                          cpu_bind_required=spec.get("required") or None,
+                          cpu_bind_preferred=spec.get("preferred") or None)
+
+
+def setup_cpuset_case(handle, case):
+    n = model.make_node(allocatable={"cpu": "96", "memory": "512Gi"}, amplification_ratio=case.get("ratio"),
+                        cpu_topology_invalid=case.get("invalid_topology", False))
+    n.cpu_bind_policy = model.NODE_CPU_BIND_BY_NAME[case["node_bind"]]
+    n.numa_allocate_strategy = {"": 0, "MostAllocated": 1, "LeastAllocated": 2}[case.get("numa_allocate_strategy", "")]
+    handle.upsert_node(0, n)
+    if not case.get("invalid_topology"):
+        rows = test_topology(*case["topology"])
+        allocated = {c: (1, None) for c in parse_cpuset(case.get("allocated", ""))}
+        handle.set_cpus(0, model.make_cpus(rows, allocated))
+    return cpuset_pod(case["pod"])

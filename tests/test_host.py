@@ -97,27 +97,49 @@ def test_eval_without_device_fails_loudly(lib):
 def test_unsupported_inputs_are_rejected():
     ev = Evaluator(abi.default_config(4))
     ev.upsert_node(0, model.make_node(allocatable={"cpu": "8", "memory": "8Gi"}))
-    lsr = model.make_pod(requests={"cpu": "2"}, labels={"koordinator.sh/qosClass": "LSR"}, priority=9500)
-    with pytest.raises(KoordEvalError) as e:
-        ev.eval([lsr], cases.NOW)
-    assert e.value.code == abi.ERR_UNSUPPORTED
     n = model.make_node(allocatable={"cpu": "8"})
-    n.cpu_bind_policy = 1  # cpuset binding is not modelled
+    n.cpu_bind_policy = 5
     with pytest.raises(KoordEvalError) as e:
         ev.upsert_node(1, n)
-    assert e.value.code == abi.ERR_UNSUPPORTED
+    assert e.value.code == abi.ERR_INVALID
+    n.cpu_bind_policy = abi.NODE_CPU_BIND_FULL_PCPUS_ONLY  # cpuset binding forced by the node: accepted
+    ev.upsert_node(1, n)
     n.cpu_bind_policy = 0
     n.numa_topology_policy = 7
     with pytest.raises(KoordEvalError) as e:
         ev.upsert_node(1, n)
     assert e.value.code == abi.ERR_INVALID
-    # a NUMA-policy node is accepted; DeviceShare pods cannot meet it (DeviceShare NUMA hints)
+    # a NUMA-policy node is accepted; DeviceShare pods cannot meet it (DeviceShare NUMA hints), nor
+    # can pods that bind CPUs (the CPU accumulator's NUMA hints)
     n.numa_topology_policy = abi.NUMA_POLICY_RESTRICTED
     ev.upsert_node(1, n)
     gpu_pod = model.make_pod(requests={"cpu": "1", "koordinator.sh/gpu": "100"})
     with pytest.raises(KoordEvalError) as e:
         ev.eval([gpu_pod], cases.NOW)
     assert e.value.code == abi.ERR_UNSUPPORTED
+    lsr = model.make_pod(requests={"cpu": "2"}, labels={"koordinator.sh/qosClass": "LSR"}, priority=9500)
+    with pytest.raises(KoordEvalError) as e:
+        ev.eval([lsr], cases.NOW)
+    assert e.value.code == abi.ERR_UNSUPPORTED
+    bad_spec = model.make_pod(requests={"cpu": "2"})
+    bad_spec.has_resource_spec = 1
+    with pytest.raises(KoordEvalError) as e:
+        ev.eval([bad_spec], cases.NOW)
+    assert e.value.code == abi.ERR_UNSUPPORTED
+    # CPU tables: ids unique and in range; a regular topology (same CPUs per core, one socket / NUMA
+    # node per core)
+    topo = [(c, c // 2, 0, 0) for c in range(8)]
+    ev.set_cpus(0, model.make_cpus(topo))
+    with pytest.raises(KoordEvalError) as e:
+        ev.set_cpus(0, model.make_cpus(topo + [(3, 1, 0, 0)]))
+    assert e.value.code == abi.ERR_INVALID
+    with pytest.raises(KoordEvalError) as e:
+        ev.set_cpus(0, model.make_cpus(topo + [(8, 4, 0, 0)]))
+    assert e.value.code == abi.ERR_UNSUPPORTED
+    with pytest.raises(KoordEvalError) as e:
+        ev.set_cpus(0, model.make_cpus([(0, 0, 0, 0), (1, 0, 1, 0)]))
+    assert e.value.code == abi.ERR_UNSUPPORTED
+    ev.set_cpus(0, model.make_cpus([]))
     # zones: ids ascending, cpuset CPUs only inside an allocation entry
     z = model.make_zones([{"id": 1, "cpu": "4"}, {"id": 0, "cpu": "4"}])
     with pytest.raises(KoordEvalError) as e:

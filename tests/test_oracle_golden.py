@@ -229,3 +229,25 @@ def test_cpu_accumulator(case):
             ref[c] += 1
     if "final_available" in case:
         assert [c for c in all_cpus if ref[c] < case["max_ref"]] == cases.parse_cpuset(case["final_available"])
+
+
+# ---- cpuset pods (NUMA policy None) --------------------------------------------------------------
+CPUSET = cases.load("cpuset.json")
+
+
+@pytest.mark.parametrize("case", CPUSET, ids=[f'{c["op"]}: {c["name"]}' for c in CPUSET])
+def test_cpuset_plugin(case):
+    from koordinator_amd import abi
+    o = Oracle(abi.default_config(1), 1)
+    pod = cases.setup_cpuset_case(o, case)
+    if case["op"] == "filter":
+        r = o.eval([pod], cases.NOW)
+        assert (int(r["status"][0, 0]), int(r["reason"][0, 0])) == (case["want"]["code"], case["want"]["reason"]), \
+            case["source"]
+        return
+    chosen, _ = o.schedule([pod], cases.NOW)
+    if case["want"]["fails"]:
+        assert chosen[0] == -1, case["source"]
+        return
+    assert chosen[0] == 0, case["source"]
+    assert cases.bits_cpus(o.last_cpusets[0]) == cases.parse_cpuset(case["want"]["cpuset"]), case["source"]
