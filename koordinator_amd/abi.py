@@ -41,6 +41,7 @@ REASON_NUMA_INVALID_REQUESTED_CPUS, REASON_NUMA_CPU_BIND_POLICY_CONFLICT = 23, 2
 REASON_NUMA_SMT_ALIGNMENT, REASON_NUMA_INSUFFICIENT_CPUS = 25, 26
 NUMA_STATUS_IDLE, NUMA_STATUS_SINGLE, NUMA_STATUS_SHARED = 0, 1, 2
 MAX_NUMA = 8
+MAX_CPUS = 256
 REASON_DS_INVALID_REQUEST = 32
 REASON_DS_INSUFFICIENT_GPU = 33
 REASON_DS_INSUFFICIENT_RDMA = 34

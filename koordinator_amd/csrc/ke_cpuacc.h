@@ -45,6 +45,12 @@ struct AccLds {
   uint8_t core_n[ACC_CPUS];
   uint8_t core_cpu[ACC_CPUS][ACC_TPC];
   int16_t cref[ACC_CPUS];     // getCoreRefCount per core rank over the allocatable CPUs (max_ref > 1)
+  // scratch of the list builders (kept in LDS: private arrays would spill to scratch memory)
+  int16_t sc_sock[ACC_CPUS], sc_node[ACC_CPUS], sc_colo[ACC_CPUS];  // free / co-located CPUs per socket / node
+  int16_t p_off[ACC_CPUS + 1], p_key[ACC_CPUS], p_sc[ACC_CPUS];     // permute_groups
+  int16_t sp_out[ACC_CPUS];                                         // spread_cpus
+  int16_t ord2[ACC_CPUS];
+  uint8_t mark[ACC_CPUS];
   int16_t order[ACC_CPUS];
   int16_t tmp[ACC_CPUS];
   AccTopo t;
@@ -99,13 +105,13 @@ __device__ inline void sort_by_ref(const AccLds& a, int16_t* v, int n) {  // sor
       v[j - 1] = (int16_t)x;
     }
 }
-__device__ inline int extract_cpu(const AccLds& a, int16_t* v, int n) {  // :332-343
-  uint8_t seen[ACC_CPUS / 8] = {};
+__device__ inline int extract_cpu(AccLds& a, int16_t* v, int n) {  // :332-343
+  for (int i = 0; i < n; i++) a.mark[a.cpu[v[i]].core] = 0;
   int m = 0;
   for (int i = 0; i < n; i++) {
     const int core = a.cpu[v[i]].core;
-    if (seen[core >> 3] >> (core & 7) & 1) continue;
-    seen[core >> 3] |= (uint8_t)(1u << (core & 7));
+    if (a.mark[core]) continue;
+    a.mark[core] = 1;
     v[m++] = v[i];
   }
   return m;
@@ -140,7 +146,8 @@ __device__ inline bool cores_less(const AccLds& a, int ci, int cj) {
 __device__ inline void group_cores(AccLds& a, bool by_socket, bool filter_full) {
   const int cpc = acc_cpc(a.t);
   // distinct group keys in ascending order (the final sort is a total order; start order is moot)
-  uint8_t has[ACC_CPUS] = {};
+  uint8_t* has = a.mark;
+  for (int k = 0; k < ACC_CPUS; k++) has[k] = 0;
   for (int k = 0; k < ACC_CPUS; k++) {
     if (!a.core_n[k] || (filter_full && a.core_n[k] != cpc)) continue;
     const int c0 = a.core_cpu[k][0];
@@ -180,7 +187,7 @@ __device__ __forceinline__ int glen(const AccLds& a, int g) { return a.goff[g + 
 // reorder the groups of a.lst by a permutation a.order[0..ng)
 __device__ inline void permute_groups(AccLds& a) {
   int pos = 0;
-  int16_t noff[ACC_CPUS + 1], nkey[ACC_CPUS], nsc[ACC_CPUS];
+  int16_t *noff = a.p_off, *nkey = a.p_key, *nsc = a.p_sc;
   for (int i = 0; i < a.ng; i++) {
     const int g = a.order[i];
     noff[i] = (int16_t)pos;
@@ -205,8 +212,8 @@ __device__ inline void free_scores(const AccLds& a, Keep keep, int16_t* per_sock
 // freeCoresInNode :371-461
 __device__ inline void free_cores_in_node(AccLds& a, bool filter_full, bool filter_excl) {
   auto keep = [&](int c) { return !(filter_excl && excl_numa(a, c)); };
-  int16_t sock[ACC_CPUS], node[ACC_CPUS];
-  free_scores(a, keep, sock, node);
+  const int16_t* sock = a.sc_sock;
+  free_scores(a, keep, a.sc_sock, a.sc_node);
   collect_cores(a, keep);
   group_cores(a, false, filter_full);
   for (int g = 0; g < a.ng; g++) a.gscore[g] = (int16_t)glen(a, g), a.order[g] = (int16_t)g;
@@ -247,8 +254,8 @@ __device__ inline void free_cpus_in_group(AccLds& a, bool by_socket, bool filter
     if (!filter_excl) return true;
     return by_socket ? !excl_pcpu(a, c) : !(excl_pcpu(a, c) || excl_numa(a, c));
   };
-  int16_t sock[ACC_CPUS], node[ACC_CPUS];
-  free_scores(a, keep, sock, node);
+  const int16_t *sock = a.sc_sock, *node = a.sc_node;
+  free_scores(a, keep, a.sc_sock, a.sc_node);
   a.ng = 0;
   int pos = 0;
   for (int g = 0; g < ACC_CPUS; g++) {
@@ -289,7 +296,7 @@ __device__ inline void free_cpus_in_group(AccLds& a, bool by_socket, bool filter
 // freeCPUs :666-774 -> a.lst[0..n)
 __device__ inline int free_cpus(AccLds& a, bool filter_excl) {
   auto keep = [&](int c) { return !(filter_excl && (excl_pcpu(a, c) || excl_numa(a, c))); };
-  int16_t sock[ACC_CPUS], node[ACC_CPUS], colo[ACC_CPUS];
+  int16_t *sock = a.sc_sock, *node = a.sc_node, *colo = a.sc_colo;
   free_scores(a, keep, sock, node);
   for (int s = 0; s < ACC_CPUS; s++) colo[s] = 0;
   for (int c = 0; c < ACC_CPUS; c++)
@@ -334,17 +341,17 @@ __device__ inline void spread_cpus(AccLds& a, int16_t* v, int n) {
   int16_t* prep = a.tmp;
   for (int i = 0; i < n; i++) prep[i] = v[i];
   int np = n, no = 0;
-  int16_t out[ACC_CPUS];
+  int16_t* out = a.sp_out;
   while (np > 0) {
-    uint8_t seen[ACC_CPUS / 8] = {};
+    for (int i = 0; i < np; i++) a.mark[a.cpu[prep[i]].core] = 0;
     int nr = 0;
     for (int i = 0; i < np; i++) {
       const int core = a.cpu[prep[i]].core;
-      if (seen[core >> 3] >> (core & 7) & 1) {
+      if (a.mark[core]) {
         prep[nr++] = prep[i];  // reserved for the next pass (nr <= i: in place)
         continue;
       }
-      seen[core >> 3] |= (uint8_t)(1u << (core & 7));
+      a.mark[core] = 1;
       out[no++] = prep[i];
     }
     np = nr;
@@ -400,7 +407,7 @@ __device__ inline bool acc_take_cpus(AccLds& a, int bind) {
     }
     a.goff2[a.ng2] = (int16_t)pos2;
     if (a.needed >= cpc) {
-      int16_t ord[ACC_CPUS];
+      int16_t* ord = a.ord2;
       for (int g = 0; g < a.ng2; g++) ord[g] = (int16_t)g;
       for (int i = 1; i < a.ng2; i++)  // by length asc, stable
         for (int j = i; j > 0; j--) {

@@ -1895,7 +1895,7 @@ __device__ bool cpuset_allocate(const SoA& s, int64_t node, uint32_t nf, const D
     else if (nb == KE_NODE_CPU_BIND_FULL_PCPUS_ONLY) bind = XB_FULL;
     else required = false, bind = pf_cpu_preferred(pod.flags);
   }
-  uint8_t navail_core[CPU_SLOTS];
+  uint8_t* navail_core = a.core_n;  // LDS scratch until the accumulator runs
   for (int k = 0; k < CPU_SLOTS; k++) navail_core[k] = 0, a.ex_core[k] = 0, a.ex_node[k] = 0;
   for (int c = 0; c < CPU_SLOTS; c++) {
     const CpuRec r = recs[c];
@@ -1910,12 +1910,12 @@ __device__ bool cpuset_allocate(const SoA& s, int64_t node, uint32_t nf, const D
     }
   }
   if (required) {
-    uint8_t seen[CPU_SLOTS / 8] = {};
+    for (int k = 0; k < CPU_SLOTS; k++) a.mark[k] = 0;
     for (int c = 0; c < CPU_SLOTS; c++) {
       if (!a.alloc[c]) continue;
       const int k = a.cpu[c].core;
-      const bool lowest = !(seen[k >> 3] >> (k & 7) & 1);
-      seen[k >> 3] |= (uint8_t)(1u << (k & 7));
+      const bool lowest = !a.mark[k];
+      a.mark[k] = 1;
       if ((bind == XB_FULL && navail_core[k] != cpc) || (bind == XB_SPREAD && !lowest)) a.alloc[c] = 0;
     }
   }
@@ -1928,14 +1928,14 @@ __device__ bool cpuset_allocate(const SoA& s, int64_t node, uint32_t nf, const D
   a.numa_most = (nf & NF_CPU_NUMA_MOST) ? 1 : 0;
   if (!acc_take_cpus(a, bind)) return false;
   if (required) {
-    uint8_t seen[CPU_SLOTS / 8] = {};
+    for (int k = 0; k < CPU_SLOTS; k++) a.mark[k] = 0;
     int n = 0, ncore = 0;
     for (int c = 0; c < CPU_SLOTS; c++) {
       if (!a.res[c]) continue;
       n++;
       const int k = a.cpu[c].core;
-      if (!(seen[k >> 3] >> (k & 7) & 1)) ncore++;
-      seen[k >> 3] |= (uint8_t)(1u << (k & 7));
+      if (!a.mark[k]) ncore++;
+      a.mark[k] = 1;
     }
     if (bind == XB_FULL && ncore * cpc != n) return false;
     if (bind == XB_SPREAD && ncore != n) return false;
@@ -1965,8 +1965,18 @@ __device__ void cpuset_commit(const SoA& s, int64_t node, const DevPod& pod, Acc
   f[F_CSM * st] = cs_milli;
   f[F_CSAF * st] = amplify_bits(cs_milli, s.cs[CS_RF * st + node]);
   f[F_CSAS * st] = amplify_bits(cs_milli, s.cs[CS_RS * st + node]);
+  // cs_counts with the per-core counter in LDS
   const int64_t cnt = s.cs[CS_CNT * st + node];
-  s.cs[CS_CNT * st + node] = cs_counts(a.cpu, cs_cpc(cnt), cs_max_ref(cnt));
+  const int cpc = cs_cpc(cnt), max_ref = cs_max_ref(cnt);
+  for (int k = 0; k < CPU_SLOTS; k++) a.core_n[k] = 0;
+  for (int c = 0; c < CPU_SLOTS; c++)
+    if (cpu_available(a.cpu[c], max_ref)) a.core_n[a.cpu[c].core]++;
+  int full = 0, spread = 0;
+  for (int k = 0; k < CPU_SLOTS; k++) {
+    if (a.core_n[k] == cpc && cpc > 0) full += cpc;
+    if (a.core_n[k] > 0) spread++;
+  }
+  s.cs[CS_CNT * st + node] = cs_pack(full, spread, cpc, max_ref);
 }
 
 // A cpuset pod's singleton batch after k_select: selectHost's node, then Reserve in profile order —

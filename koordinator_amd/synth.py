@@ -12,7 +12,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from . import abi
+from . import abi, model
 
 BASE_SEED = 20251015
 NS = 1_000_000_000
@@ -347,3 +347,87 @@ def load_numa(handle, zones):
     for i, z in enumerate(zones):
         if z is not None:
             handle.set_numa(i, z)
+
+
+# ---- CPU tables + cpuset pods (NodeNUMAResource, NUMA policy None) ----------------------------------
+def make_cpus(cl, seed, no_table_fraction=0.03, invalid_fraction=0.02, bind_weights=(0.7, 0.15, 0.15),
+              max_ref_choices=(1, 1, 1, 2), allocated_choices=(0.0, 0.1, 0.3, 0.6, 0.9), reserved_fraction=0.3):
+    """Give the nodes of `cl` a CPU topology table (kubelet-style: the node's logical CPUs over 1-2
+    sockets x 1-2 NUMA nodes, 1 or 2 threads per core, sibling ids adjacent or split by half), cpuset
+    allocations of earlier pods (RefCount up to MaxRefCount, PCPU / NUMA-level exclusivity), a few
+    reserved CPUs, a node CPU bind policy (None / FullPCPUsOnly / SpreadByPCPUs by `bind_weights`) and
+    a NUMA allocate strategy label.  Mutates cl.nodes; returns [(table or None, max_ref)] per node."""
+    rng = np.random.default_rng(seed)
+    N = cl.n_nodes
+    cl.nodes["cpu_bind_policy"] = rng.choice(3, N, p=np.asarray(bind_weights) / np.sum(bind_weights))
+    cl.nodes["numa_allocate_strategy"] = rng.choice(3, N)
+    out = []
+    for i in range(N):
+        u = rng.random()
+        if u < no_table_fraction:
+            out.append((None, 1))
+            continue
+        if u < no_table_fraction + invalid_fraction:
+            cl.nodes["cpu_topology_invalid"][i] = 1
+            out.append((None, 1))
+            continue
+        cap = cl.nodes["raw_allocatable"][i, 0]
+        ncpu = int((cap if cap != abi.ABSENT else cl.nodes["allocatable"][i, 0]) // 1000)
+        ncpu = min(ncpu, abi.MAX_CPUS)
+        sockets = int(rng.choice([1, 2]))
+        nps = int(rng.choice([1, 2]))
+        tpc = int(rng.choice([1, 2, 2]))
+        cores = ncpu // (sockets * nps * tpc)
+        n_all = sockets * nps * cores * tpc
+        split = rng.random() < 0.5  # Linux numbering: thread t of core k is cpu k + t*(n_all/tpc)
+        rows = []
+        core = 0
+        for s in range(sockets):
+            for q in range(nps):
+                for _ in range(cores):
+                    for t in range(tpc):
+                        cpu = core + t * (n_all // tpc) if split else core * tpc + t
+                        rows.append((cpu, 1000 + 7 * core, s * nps + q, 10 + s))
+                    core += 1
+        max_ref = int(rng.choice(max_ref_choices))
+        f = float(rng.choice(allocated_choices))
+        allocated = {}
+        for cpu, _, _, _ in rows:
+            if rng.random() < f:
+                excl = rng.choice([None, None, "PCPULevel", "NUMANodeLevel"])
+                allocated[cpu] = (int(rng.integers(1, max_ref + 1)), excl)
+        reserved = ()
+        if rng.random() < reserved_fraction:
+            reserved = tuple(int(c) for c in rng.choice([r[0] for r in rows], int(rng.integers(1, 5)), replace=False))
+        out.append((model.make_cpus(rows, allocated, reserved), max_ref))
+    return out
+
+
+def load_cpus(handle, tables):
+    for i, (t, max_ref) in enumerate(tables):
+        if t is not None:
+            handle.set_cpus(i, t, max_ref)
+
+
+def make_cpuset_pods(n_pods, seed, cpuset_fraction=0.5, key_base=4_000_000_000):
+    """The config-2 queue where `cpuset_fraction` of the pods are LSE/LSR koord-prod with whole-CPU
+    requests (a few fractional) and a ResourceSpec: required / preferred bind policy (unset, Default,
+    FullPCPUs, SpreadByPCPUs, ConstrainedBurst) and preferred CPU exclusivity."""
+    rng = np.random.default_rng(seed)
+    pods = make_pods(n_pods, seed + 1, key_base=key_base)
+    cs = rng.random(n_pods) < cpuset_fraction
+    k = int(cs.sum())
+    pods["priority_class"][cs] = abi.PRIORITY_PROD
+    pods["qos_class"][cs] = rng.choice([abi.QOS_LSE, abi.QOS_LSR], k)
+    cpu = rng.choice([1000, 2000, 3000, 4000, 6000, 8000, 16000, 1500], k, p=[.15, .2, .1, .2, .1, .1, .1, .05])
+    pods["requests"][cs, abi.RES_CPU] = cpu
+    pods["limits"][cs, abi.RES_CPU] = cpu
+    pods["requests"][cs, abi.RES_MEMORY] = rng.choice([2, 4, 8], k) * GI
+    pods["limits"][cs, abi.RES_MEMORY] = pods["requests"][cs, abi.RES_MEMORY]
+    pods["requests"][cs, abi.RES_BATCH_CPU] = 0
+    pods["requests"][cs, abi.RES_BATCH_MEMORY] = 0
+    pods["is_daemonset"][cs] = 0
+    pods["cpu_bind_required"][cs] = rng.choice(5, k, p=[.6, .1, .12, .12, .06])
+    pods["cpu_bind_preferred"][cs] = rng.choice(5, k, p=[.4, .15, .2, .2, .05])
+    pods["cpu_exclusive"][cs] = rng.choice(3, k, p=[.6, .2, .2])
+    return pods
