@@ -431,3 +431,73 @@ def make_cpuset_pods(n_pods, seed, cpuset_fraction=0.5, key_base=4_000_000_000):
     pods["cpu_bind_preferred"][cs] = rng.choice(5, k, p=[.4, .15, .2, .2, .05])
     pods["cpu_exclusive"][cs] = rng.choice(3, k, p=[.6, .2, .2])
     return pods
+
+
+def make_numa_cpus(cl, seed, zone_counts=(2, 4, 8), policy_weights=(0.1, 0.3, 0.3, 0.3), bind_weights=(0.8, 0.1, 0.1),
+                   cpuset_fraction=(0.0, 0.1, 0.3, 0.6), max_ref_choices=(1, 1, 2), status_mode="derived"):
+    """Config 4 (NUMA-aware cpuset binding, BASELINE.json configs[3]): per node a NUMA topology policy
+    (None / BestEffort / Restricted / SingleNUMANode by `policy_weights`), NRT zones over `zone_counts`
+    NUMA nodes with a CPU table consistent with them (1-2 sockets, 1-2 threads per core), cpusets of
+    earlier LSR/LSE pods (RefCount, exclusivity) whose CPUs also sit in the zones' allocation entries
+    (plus shared cpu / memory allocations), the zones' single / shared status from those cpusets, a
+    node CPU bind policy and a NUMA allocate strategy label.  Mutates cl.nodes; returns
+    (zones, tables) as make_numa / make_cpus do."""
+    rng = np.random.default_rng(seed)
+    N = cl.n_nodes
+    cl.nodes["numa_topology_policy"] = rng.choice(4, N, p=np.asarray(policy_weights) / np.sum(policy_weights))
+    cl.nodes["cpu_bind_policy"] = rng.choice(3, N, p=np.asarray(bind_weights) / np.sum(bind_weights))
+    cl.nodes["numa_allocate_strategy"] = rng.choice(3, N)
+    zones_out, tables = [], []
+    for i in range(N):
+        cap = cl.nodes["raw_allocatable"][i, 0]
+        ncpu = min(int((cap if cap != abi.ABSENT else cl.nodes["allocatable"][i, 0]) // 1000), abi.MAX_CPUS)
+        nz = int(rng.choice([z for z in zone_counts if ncpu % z == 0] or [1]))
+        cpz = ncpu // nz
+        tpc = int(rng.choice([1, 2])) if cpz % 2 == 0 else 1
+        sockets = 2 if nz % 2 == 0 and rng.random() < 0.7 else 1
+        split = rng.random() < 0.5
+        rows = []
+        core = 0
+        for z in range(nz):
+            for _ in range(cpz // tpc):
+                for t in range(tpc):
+                    cpu = core + t * (ncpu // tpc) if split else core * tpc + t
+                    rows.append((cpu, 500 + 3 * core, z, z * sockets // nz))
+                core += 1
+        max_ref = int(rng.choice(max_ref_choices))
+        frac = float(rng.choice(cpuset_fraction))
+        allocated, per_zone = {}, [0] * nz
+        for cpu, _, z, _ in rows:
+            if rng.random() < frac:
+                allocated[cpu] = (int(rng.integers(1, max_ref + 1)), rng.choice([None, None, "PCPULevel", "NUMANodeLevel"]))
+                per_zone[z] += 1
+        mem = int(cl.nodes["allocatable"][i, 1])
+        amplified = cl.nodes["cpu_amplification_ratio"][i] > 1.0
+        z_arr = np.zeros(nz, abi.NUMA_ZONE_DTYPE)
+        for z in range(nz):
+            z_arr[z]["id"] = z
+            z_arr[z]["has"][:] = 1
+            z_arr[z]["capacity"][0] = cpz * 1000
+            z_arr[z]["capacity"][1] = mem // nz // MI * MI
+            shared = int(rng.choice([0, 0, 1000, 2500, 4000])) if rng.random() < 0.6 else 0
+            mem_al = int(z_arr[z]["capacity"][1] * rng.choice([0.0, 0.2, 0.5, 0.8])) // MI * MI
+            if per_zone[z] or shared or mem_al or (amplified and rng.random() < 0.3):
+                z_arr[z]["has_allocated"] = abi.NUMA_ALLOC_ENTRY | abi.NUMA_ALLOC_CPU | abi.NUMA_ALLOC_MEMORY
+                z_arr[z]["allocated"][0] = per_zone[z] * 1000 + shared
+                z_arr[z]["allocated"][1] = mem_al
+            if per_zone[z]:
+                z_arr[z]["numa_status"] = abi.NUMA_STATUS_SINGLE if rng.random() < 0.7 else abi.NUMA_STATUS_SHARED
+        zones_out.append(z_arr)
+        tables.append((model.make_cpus(rows, allocated), max_ref))
+    return zones_out, tables
+
+
+def make_numa_cpuset_pods(n_pods, seed, cpuset_fraction=0.6, policy_fraction=0.2, key_base=6_000_000_000):
+    """Config 4's queue: make_cpuset_pods (LSR/LSE koord-prod binding pods, bind / exclusive policies)
+    where `policy_fraction` of the pods also carry a NUMA topology spec."""
+    rng = np.random.default_rng(seed)
+    pods = make_cpuset_pods(n_pods, seed + 1, cpuset_fraction=cpuset_fraction, key_base=key_base)
+    pol = rng.random(n_pods) < policy_fraction
+    pods["numa_topology_policy"] = np.where(pol, rng.integers(1, 4, n_pods), 0)
+    pods["numa_exclusive"] = np.where(pol, rng.integers(0, 3, n_pods), 0)
+    return pods

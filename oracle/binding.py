@@ -57,6 +57,8 @@ def load():
         "or_node_numa_set": (C.c_int, [V, i32, i32, V]),
         "or_node_cpus_set": (C.c_int, [V, i32, i32, V, i32]),
         "or_numa_distribute": (C.c_int, [V, i32, V, C.c_uint32, V]),
+        "or_numa_allocate": (C.c_int, [V, i32, V, C.c_uint32, V, V]),
+        "or_set_exact_cpusets": (None, [C.c_int]),
         "or_numa_exclusive_ok": (C.c_int, [C.c_uint32, i32, V, i32]),
         "or_take_cpus": (C.c_int, [V, i32, i32, V, V, V, i32, i32, i32, i32, V, V]),
         "or_spread_order": (C.c_int, [V, i32, V, i32, V]),
@@ -156,6 +158,17 @@ class Oracle:
     def set_cpus(self, i, cpus, max_ref_count=1):
         cpus = np.ascontiguousarray(cpus, dtype=abi.CPU_DTYPE)
         assert self.lib.or_node_cpus_set(self.h, i, len(cpus), abi.ptr(cpus), max_ref_count) == 0
+
+    def numa_allocate(self, i, pod, mask):
+        """resourceManager.Allocate with hint `mask` (0 = nil): None on error, else (out[16], cpuset words)."""
+        out = np.zeros(16, np.int64)
+        cpus = np.zeros(4, np.uint64)
+        rc = self.lib.or_numa_allocate(self.h, i, C.byref(pod), mask, abi.ptr(out), abi.ptr(cpus))
+        return None if rc < 0 else (out, cpus)
+
+    def set_exact_cpusets(self, on):
+        """Hints / admit run the CPU accumulator itself (the reference's shape) instead of its counts."""
+        self.lib.or_set_exact_cpusets(1 if on else 0)
 
     def numa_distribute(self, i, pod, mask):
         """(ok, out[16]) of tryBestToDistributeEvenly on NUMA ids `mask` (None if options fail)."""

@@ -476,49 +476,163 @@ static int numa_most_allocated(const or_cluster* c, const or_node* n) {
   return c->cfg.numa.numa_strategy == KE_STRATEGY_MOST_ALLOCATED;
 }
 
-/* allocateCPUSet without NUMA hint (resource_manager.go:353-459): 0 and the cpuset, or -1 */
-static int cpuset_allocate(const or_cluster* c, const or_node* n, const cpuset_state* st, uint64_t* result) {
-  const or_cpus* x = n->cpus;
+/* a node's NUMA zones as getResourceOptions / getAvailableNUMANodeResources see them */
+typedef struct numa_view {
+  int n;
+  int id[KE_MAX_NUMA];
+  uint8_t cap_has[KE_MAX_NUMA][KE_NRES];
+  int64_t cap[KE_MAX_NUMA][KE_NRES];     /* amplified NUMANodeResources (amplifyNUMANodeResources) */
+  uint8_t av_has[KE_MAX_NUMA][KE_NRES];
+  int64_t av[KE_MAX_NUMA][KE_NRES];      /* totalAvailable */
+  int has_alloc[KE_MAX_NUMA];
+  int64_t al[KE_MAX_NUMA][KE_NRES];      /* totalAllocated (cpu adjusted for amplified cpusets) */
+  uint8_t al_has[KE_MAX_NUMA][KE_NRES];
+  double ratio;                          /* TopologyOptions.AmplificationRatios[cpu] */
+} numa_view;
+
+/* The cpuset part of ResourceOptions for a pod that binds CPUs on the node (getResourceOptions
+ * plugin.go:629-668, getCPUBindPolicy util.go:101-119) and the CPUs allocateCPUSet may take:
+ * GetAvailableCPUs filtered by a required bind policy (resource_manager.go:353-377), per NUMA id. */
+typedef struct numa_cs {
+  int rcb;             /* requestCPUBind */
+  int valid;           /* the node's CPU topology is valid */
+  int required, bind;  /* requiredCPUBindPolicy, cpuBindPolicy (KE_CPU_BIND_*) */
+  int num_cpus, cpc, excl, numa_most;
+  int avail_total;
+  int zcnt[KE_MAX_NUMA];
   uint64_t avail[ACC_WORDS];
-  cpus_available(x, avail);
-  int required;
-  const int bind = cpu_bind_policy_of(st, n->node.cpu_bind_policy, &required);
-  const int cpc = acc_cpus_per_core(&x->t);
-  if (required) { /* filterCPUsByRequiredCPUBindPolicy (:655-695) */
+} numa_cs;
+
+static int exact_cpusets = 0; /* hints / admit run the CPU accumulator itself instead of its counts */
+void or_set_exact_cpusets(int on) { exact_cpusets = on; }
+
+static int popcount_set(const uint64_t* s) {
+  int n = 0;
+  for (int w = 0; w < ACC_WORDS; w++) n += __builtin_popcountll(s[w]);
+  return n;
+}
+
+static void numa_cs_build(const or_cluster* c, const or_node* n, const ke_pod* pod, numa_cs* cs) {
+  memset(cs, 0, sizeof *cs);
+  cpuset_state st;
+  cpuset_prefilter(c, pod, &st);
+  if (request_cpu_bind(&st, pod, n->node.cpu_bind_policy) <= 0) return;
+  cs->rcb = 1;
+  cs->valid = cpus_valid(n);
+  cs->num_cpus = st.num_cpus;
+  cs->excl = st.excl;
+  cs->bind = cpu_bind_policy_of(&st, n->node.cpu_bind_policy, &cs->required);
+  cs->numa_most = numa_most_allocated(c, n);
+  if (!cs->valid) return;
+  const or_cpus* x = n->cpus;
+  cs->cpc = acc_cpus_per_core(&x->t);
+  cpus_available(x, cs->avail);
+  if (cs->required) { /* filterCPUsByRequiredCPUBindPolicy (:655-695) */
     uint64_t keep[ACC_WORDS] = {0};
     for (int c1 = 0; c1 < ACC_MAX_CPUS; c1++) {
-      if (!(avail[c1 >> 6] >> (c1 & 63) & 1)) continue;
+      if (!(cs->avail[c1 >> 6] >> (c1 & 63) & 1)) continue;
       int in_core = 0, lowest = 1;
       for (int c2 = 0; c2 < ACC_MAX_CPUS; c2++)
-        if ((avail[c2 >> 6] >> (c2 & 63) & 1) && x->t.core[c2] == x->t.core[c1]) {
+        if ((cs->avail[c2 >> 6] >> (c2 & 63) & 1) && x->t.core[c2] == x->t.core[c1]) {
           in_core++;
           if (c2 < c1) lowest = 0;
         }
-      if ((bind == KE_CPU_BIND_FULL_PCPUS && in_core == cpc) || (bind == KE_CPU_BIND_SPREAD_BY_PCPUS && lowest) ||
-          (bind != KE_CPU_BIND_FULL_PCPUS && bind != KE_CPU_BIND_SPREAD_BY_PCPUS))
+      if ((cs->bind == KE_CPU_BIND_FULL_PCPUS && in_core == cs->cpc) || (cs->bind == KE_CPU_BIND_SPREAD_BY_PCPUS && lowest) ||
+          (cs->bind != KE_CPU_BIND_FULL_PCPUS && cs->bind != KE_CPU_BIND_SPREAD_BY_PCPUS))
         keep[c1 >> 6] |= 1ull << (c1 & 63);
     }
-    memcpy(avail, keep, sizeof keep);
+    memcpy(cs->avail, keep, sizeof keep);
   }
-  int navail = 0;
-  for (int w = 0; w < ACC_WORDS; w++) navail += __builtin_popcountll(avail[w]);
-  if (navail < st->num_cpus) return -1;
-  if (acc_take_preferred_cpus(&x->t, x->max_ref, avail, NULL, &x->al, st->num_cpus, acc_bind(bind), st->excl,
-                              numa_most_allocated(c, n), result) != 0)
-    return -1;
-  if (required) { /* satisfiedRequiredCPUBindPolicy (:697-718) */
-    int ncpu = 0, cores[ACC_MAX_CPUS], ncore = 0;
-    for (int c1 = 0; c1 < ACC_MAX_CPUS; c1++) {
-      if (!(result[c1 >> 6] >> (c1 & 63) & 1)) continue;
-      ncpu++;
-      int f = 0;
-      for (int k = 0; k < ncore && !f; k++) f = cores[k] == x->t.core[c1];
-      if (!f) cores[ncore++] = x->t.core[c1];
-    }
-    if (bind == KE_CPU_BIND_FULL_PCPUS && ncore * cpc != ncpu) return -1;
-    if (bind == KE_CPU_BIND_SPREAD_BY_PCPUS && ncore != ncpu) return -1;
+  cs->avail_total = popcount_set(cs->avail);
+  for (int c1 = 0; c1 < ACC_MAX_CPUS; c1++)
+    if ((cs->avail[c1 >> 6] >> (c1 & 63) & 1) && x->t.node[c1] >= 0 && x->t.node[c1] < KE_MAX_NUMA)
+      cs->zcnt[x->t.node[c1]]++;
+}
+
+/* satisfiedRequiredCPUBindPolicy (:697-718) */
+static int cpuset_satisfied(const numa_cs* cs, const or_cpus* x, const uint64_t* result) {
+  if (!cs->required) return 1;
+  int ncpu = 0, cores[ACC_MAX_CPUS], ncore = 0;
+  for (int c1 = 0; c1 < ACC_MAX_CPUS; c1++) {
+    if (!(result[c1 >> 6] >> (c1 & 63) & 1)) continue;
+    ncpu++;
+    int f = 0;
+    for (int k = 0; k < ncore && !f; k++) f = cores[k] == x->t.core[c1];
+    if (!f) cores[ncore++] = x->t.core[c1];
   }
-  return 0;
+  if (cs->bind == KE_CPU_BIND_FULL_PCPUS && ncore * cs->cpc != ncpu) return 0;
+  if (cs->bind == KE_CPU_BIND_SPREAD_BY_PCPUS && ncore != ncpu) return 0;
+  return 1;
+}
+
+/* allocateCPUSet (resource_manager.go:353-459): with the pod's NUMA allocation `dist` (zones of the
+ * view with a non-zero amount, ascending id) a takePreferredCPUs per zone over its available CPUs,
+ * then the remainder over the node.  0 and the cpuset, or -1. */
+static int cpuset_allocate_cs(const or_node* n, const numa_cs* cs, const numa_view* v,
+                              const int64_t (*dist)[KE_NRES], uint64_t* result) {
+  const or_cpus* x = n->cpus;
+  memset(result, 0, sizeof(uint64_t) * ACC_WORDS);
+  if (cs->avail_total < cs->num_cpus) return -1;
+  int needed = cs->num_cpus, any = 0;
+  for (int z = 0; dist && z < v->n; z++) {
+    if (dist[z][0] == 0 && dist[z][1] == 0) continue;
+    any = 1;
+    uint64_t az[ACC_WORDS] = {0}, got[ACC_WORDS];
+    for (int c1 = 0; c1 < ACC_MAX_CPUS; c1++)
+      if ((cs->avail[c1 >> 6] >> (c1 & 63) & 1) && x->t.node[c1] == v->id[z]) az[c1 >> 6] |= 1ull << (c1 & 63);
+    int k = popcount_set(az);
+    const int want = (int)(dist[z][KE_RES_CPU] / 1000);
+    if (want < k) k = want;
+    if (acc_take_preferred_cpus(&x->t, x->max_ref, az, NULL, &x->al, k, acc_bind(cs->bind), cs->excl, cs->numa_most, got) != 0)
+      return -1;
+    for (int w = 0; w < ACC_WORDS; w++) result[w] |= got[w];
+  }
+  if (any) {
+    needed -= popcount_set(result);
+    if (needed != 0) return -1;
+  }
+  if (needed > 0) {
+    uint64_t rest[ACC_WORDS], got[ACC_WORDS];
+    for (int w = 0; w < ACC_WORDS; w++) rest[w] = cs->avail[w] & ~result[w];
+    if (acc_take_preferred_cpus(&x->t, x->max_ref, rest, NULL, &x->al, needed, acc_bind(cs->bind), cs->excl, cs->numa_most,
+                                got) != 0)
+      return -1;
+    for (int w = 0; w < ACC_WORDS; w++) result[w] |= got[w];
+  }
+  return cpuset_satisfied(cs, x, result) ? 0 : -1;
+}
+
+/* The same outcome from counts: per zone takeCPUs over k <= |available| CPUs never
+ * fails and takes exactly k; a required FullPCPUs result is whole cores iff every zone's k is a
+ * multiple of CPUs per core (whole cores are all a zone offers then); SpreadByPCPUs offers one CPU per
+ * core.  Verified against cpuset_allocate_cs by tests/test_oracle_cpuset_numa.py. */
+static int cpuset_fits_cs(const or_node* n, const numa_cs* cs, const numa_view* v, const int64_t (*dist)[KE_NRES]) {
+  if (exact_cpusets) {
+    uint64_t r[ACC_WORDS];
+    return cpuset_allocate_cs(n, cs, v, dist, r) == 0;
+  }
+  if (cs->avail_total < cs->num_cpus) return 0;
+  int taken = 0, any = 0, aligned = 1;
+  for (int z = 0; dist && z < v->n; z++) {
+    if (dist[z][0] == 0 && dist[z][1] == 0) continue;
+    any = 1;
+    int k = v->id[z] < KE_MAX_NUMA ? cs->zcnt[v->id[z]] : 0;
+    const int want = (int)(dist[z][KE_RES_CPU] / 1000);
+    if (want < k) k = want;
+    if (k <= 0) continue;
+    taken += k;
+    if (k % cs->cpc) aligned = 0;
+  }
+  if (!any) return 1; /* the whole-node take: FullPCPUs is SMT-aligned after Filter */
+  if (taken != cs->num_cpus) return 0;
+  return !(cs->required && cs->bind == KE_CPU_BIND_FULL_PCPUS && !aligned);
+}
+
+/* allocateCPUSet without a NUMA allocation (policy None) */
+static int cpuset_allocate(const or_cluster* c, const or_node* n, const ke_pod* pod, uint64_t* result) {
+  numa_cs cs;
+  numa_cs_build(c, n, pod, &cs);
+  return cpuset_allocate_cs(n, &cs, NULL, NULL, result);
 }
 
 /* ---------------------------------------------------------------------------------------------- */
@@ -626,7 +740,7 @@ static int pod_requests_zero(const ke_pod* pod) { /* quotav1.IsZero(PodRequests)
 /* Plugin.Filter  plugin.go:318-406 -> filterAmplifiedCPUs :408-442 */
 static int numa_filter_amplified(const or_node* n, const ke_pod* pod, int rcb, int* reason);
 static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod, int policy, int exclusive,
-                      uint32_t* affinity, int* reason);
+                      uint32_t* affinity, int* reason, const numa_cs* cs);
 
 /* getNUMATopologyPolicy + mergeTopologyPolicy (util.go:58-74) and the exclusive default of
  * Filter (plugin.go:330-336): -1 on a node / pod policy conflict. */
@@ -679,7 +793,7 @@ int or_numa_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* re
     }
     if (required != KE_CPU_BIND_UNSET && policy == KE_NUMA_POLICY_NONE) { /* trial Allocate */
       uint64_t cs[ACC_WORDS];
-      if (cpuset_allocate(c, n, &st, cs) != 0) {
+      if (cpuset_allocate(c, n, pod, cs) != 0) {
         *reason = KE_REASON_NUMA_INSUFFICIENT_CPUS;
         return KE_CODE_UNSCHEDULABLE;
       }
@@ -692,7 +806,9 @@ int or_numa_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* re
     return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
   }
   uint32_t aff;
-  return numa_admit(c, n, pod, policy, exclusive, &aff, reason);
+  numa_cs cs;
+  numa_cs_build(c, n, pod, &cs);
+  return numa_admit(c, n, pod, policy, exclusive, &aff, reason, &cs);
 }
 
 /* filterAmplifiedCPUs  plugin.go:408-442 */
@@ -757,17 +873,8 @@ static int64_t numa_resource_score(const ke_numa_args* na, const int64_t* reques
 /* policy*.go), Allocate by hint (resource_manager.go:194-330), NUMA-scope Score (scoring.go:141-187) */
 /* ---------------------------------------------------------------------------------------------- */
 
-typedef struct numa_view {
-  int n;
-  int id[KE_MAX_NUMA];
-  uint8_t cap_has[KE_MAX_NUMA][KE_NRES];
-  int64_t cap[KE_MAX_NUMA][KE_NRES];     /* amplified NUMANodeResources (amplifyNUMANodeResources) */
-  uint8_t av_has[KE_MAX_NUMA][KE_NRES];
-  int64_t av[KE_MAX_NUMA][KE_NRES];      /* totalAvailable */
-  int has_alloc[KE_MAX_NUMA];
-  int64_t al[KE_MAX_NUMA][KE_NRES];      /* totalAllocated (cpu adjusted for amplified cpusets) */
-  uint8_t al_has[KE_MAX_NUMA][KE_NRES];
-} numa_view;
+
+
 
 /* allocatedCPUs.CPUsInNUMANodes(id).Size(): from the CPU table when the node has one */
 static int zone_cpusets(const or_node* nd, int id, int given) {
@@ -779,7 +886,7 @@ static int zone_cpusets(const or_node* nd, int id, int given) {
 
 /* getResourceOptions -> amplifyNUMANodeResources (util.go:78-98) + getAvailableNUMANodeResources
  * (node_allocation.go:221-243).  Returns -1 on an amplification-ratio annotation error. */
-static int numa_view_build(const or_node* nd, numa_view* v) {
+static int numa_view_build(const or_node* nd, numa_view* v, const numa_cs* cs) {
   memset(v, 0, sizeof *v);
   double ratio;
   int amplify_caps = 0;
@@ -790,6 +897,7 @@ static int numa_view_build(const or_node* nd, numa_view* v) {
     ratio = nd->node.cpu_amplification_ratio < 0 ? 0.0 : nd->node.cpu_amplification_ratio;
     amplify_caps = 1;
   }
+  v->ratio = ratio;
   v->n = nd->n_zone;
   for (int z = 0; z < nd->n_zone; z++) {
     const ke_numa_zone* zn = &nd->zone[z];
@@ -824,6 +932,11 @@ static int numa_view_build(const or_node* nd, numa_view* v) {
       const int64_t q = v->cap_has[z][r] ? v->cap[z][r] - a : -a;
       v->av[z][r] = q > 0 ? q : 0;
     }
+    /* trimNUMANodeResources (resource_manager.go:166-192): a required bind policy caps a zone's cpu
+     * at its CPUs that the policy leaves available */
+    if (cs && cs->rcb && cs->required && v->av[z][KE_RES_CPU] != 0 && zn->id < KE_MAX_NUMA &&
+        (int64_t)cs->zcnt[zn->id] * 1000 < v->av[z][KE_RES_CPU])
+      v->av[z][KE_RES_CPU] = (int64_t)cs->zcnt[zn->id] * 1000;
   }
   return 0;
 }
@@ -840,7 +953,11 @@ static int pod_has_req(const ke_pod* pod, int r) { return pod->requests[r] != 0;
 /* tryBestToDistributeEvenly (resource_manager.go:260-314) over the NUMA ids in `mask`.  The sort of the
  * hint's nodes compares totalAvailable indexed by slice position (a reference quirk, reproduced):
  * Go's sort.Slice on <= 12 elements is an insertion sort.  out[z][r]: allocated per zone. */
-static int numa_distribute(const numa_view* v, uint32_t mask, const ke_pod* pod, int64_t out[KE_MAX_NUMA][KE_NRES]) {
+/* resource.Quantity.Value() of a cpu amount in milli: rounded up, away from zero */
+static int64_t qty_value(int64_t milli) { return milli >= 0 ? (milli + 999) / 1000 : -((-milli + 999) / 1000); }
+
+static int numa_distribute(const numa_view* v, uint32_t mask, const ke_pod* pod, int64_t out[KE_MAX_NUMA][KE_NRES],
+                           const numa_cs* cs) {
   memset(out, 0, sizeof(int64_t) * KE_MAX_NUMA * KE_NRES);
   int names[KE_NRES] = {0, 0}; /* resourceNamesByNUMA: keys of any totalAvailable entry */
   for (int z = 0; z < v->n; z++)
@@ -863,9 +980,15 @@ static int numa_distribute(const numa_view* v, uint32_t mask, const ke_pod* pod,
         sorted[j] = sorted[j - 1];
         sorted[j - 1] = t;
       }
-    int64_t q = pod->requests[r];
+    int64_t q = pod->requests[r]; /* requestCPUBind: originalRequests (never amplified) */
     for (int i = 0; i < nb; i++) {
-      const int64_t split = q / (nb - i); /* splitQuantity: cpu milli / memory value */
+      int64_t split = q / (nb - i); /* splitQuantity (:316-330): cpu milli / memory value */
+      if (r == KE_RES_CPU && cs && cs->rcb) { /* whole CPUs; whole cores under a required FullPCPUs */
+        if (cs->required && cs->bind == KE_CPU_BIND_FULL_PCPUS)
+          split = qty_value(q) / cs->cpc / (nb - i) * cs->cpc * 1000;
+        else
+          split = qty_value(q) / (nb - i) * 1000;
+      }
       const int z = zone_of(v, sorted[i]);
       const int64_t avail = z >= 0 && v->av_has[z][r] ? v->av[z][r] : 0;
       const int64_t got = avail > split ? split : avail; /* allocateRes */
@@ -887,8 +1010,12 @@ typedef struct numa_hint {
 
 /* generateResourceHints (resource_manager.go:525-622) for a non-cpuset pod.  Per resource (cpu,
  * memory): the list of hints in IterateBitMasks order; present[r] = the resource has a list. */
-static void numa_generate_hints(const or_cluster* c, const numa_view* v, const ke_pod* pod, int policy,
-                                numa_hint* lists /*[KE_NRES][255]*/, int* counts, int* present) {
+static void numa_generate_hints(const or_cluster* c, const or_node* nd, const numa_view* v, const ke_pod* pod,
+                                int policy, numa_hint* lists /*[KE_NRES][255]*/, int* counts, int* present,
+                                const numa_cs* cs) {
+  /* options.requests: a binding pod's cpu amplified (getResourceOptions, plugin.go:634-640) */
+  int64_t podreq[KE_NRES] = {pod->requests[KE_RES_CPU], pod->requests[KE_RES_MEMORY]};
+  if (cs && cs->rcb && v->ratio > 1.0) podreq[KE_RES_CPU] = amplify(podreq[KE_RES_CPU], v->ratio);
   int names[KE_NRES] = {0, 0};
   for (int z = 0; z < v->n; z++)
     for (int r = 0; r < KE_NRES; r++) names[r] |= v->cap_has[z][r];
@@ -922,9 +1049,10 @@ static void numa_generate_hints(const or_cluster* c, const numa_view* v, const k
       /* numaScorer.score(requested = total - available, total, pod) with the NUMA strategy */
       int64_t req[KE_NRES];
       for (int r = 0; r < KE_NRES; r++) req[r] = total[r] - avail[r] > 0 ? total[r] - avail[r] : 0;
-      const int64_t score = numa_resource_score_as(&c->cfg.numa, c->cfg.numa.numa_strategy, req, total, pod->requests);
+      const int64_t score = numa_resource_score_as(&c->cfg.numa, c->cfg.numa.numa_strategy, req, total, podreq);
       int64_t out[KE_MAX_NUMA][KE_NRES];
-      if (numa_distribute(v, mask, pod, out))
+      /* tryAllocateFromNode with the mask: allocateResourcesByHint, then allocateCPUSet */
+      if (numa_distribute(v, mask, pod, out, cs) && (!cs || !cs->rcb || cpuset_fits_cs(nd, cs, v, (const int64_t(*)[KE_NRES])out)))
         for (int r = 0; r < KE_NRES; r++) { /* generator.generateHints per resource */
           if (!total_names[r]) continue;
           if (mask & lack[r]) continue;
@@ -1100,7 +1228,7 @@ int or_topology_merge(int32_t policy, uint32_t all, int32_t n_lists, const int32
  * provider; DeviceShare provides no hints for a pod without device requests).  Returns the status
  * code, *affinity (0 = nil) on success. */
 static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod, int policy, int exclusive,
-                      uint32_t* affinity, int* reason) {
+                      uint32_t* affinity, int* reason, const numa_cs* cs) {
   numa_view v;
   uint32_t all = 0;
   for (int z = 0; z < nd->n_zone; z++) all |= 1u << nd->zone[z].id;
@@ -1109,13 +1237,13 @@ static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod,
   uint8_t status[KE_MAX_NUMA] = {0};
   for (int z = 0; z < nd->n_zone; z++)
     if (nd->zone[z].id < nd->n_zone) status[nd->zone[z].id] = nd->zone[z].numa_status;
-  if (numa_view_build(nd, &v) != 0) { /* GetPodTopologyHints error -> reasons -> Unschedulable */
+  if (numa_view_build(nd, &v, cs) != 0) { /* GetPodTopologyHints error -> reasons -> Unschedulable */
     *reason = KE_REASON_NUMA_HINT_UNALIGNED;
     return KE_CODE_UNSCHEDULABLE;
   }
   static __thread numa_hint store[KE_NRES * 255];
   int counts[KE_NRES], present[KE_NRES];
-  numa_generate_hints(c, &v, pod, policy, store, counts, present);
+  numa_generate_hints(c, nd, &v, pod, policy, store, counts, present, cs);
   /* filterProvidersHints: the NUMA provider's lists in sorted resource-name order (cpu, memory), then
    * DeviceShare's nil hints -> one preferred any-NUMA hint */
   static __thread numa_hint filt[KE_NRES + 1][255];
@@ -1161,12 +1289,15 @@ static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod,
     return KE_CODE_UNSCHEDULABLE;
   }
   /* allocateResources -> NodeNUMAResource.Allocate -> tryAllocateFromNode with the hint */
-  if (best.mask) {
-    int64_t out[KE_MAX_NUMA][KE_NRES];
-    if (!numa_distribute(&v, best.mask, pod, out)) {
-      *reason = KE_REASON_NUMA_INSUFFICIENT_RESOURCES;
-      return KE_CODE_UNSCHEDULABLE;
-    }
+  int64_t out[KE_MAX_NUMA][KE_NRES];
+  memset(out, 0, sizeof out);
+  if (best.mask && !numa_distribute(&v, best.mask, pod, out, cs)) {
+    *reason = KE_REASON_NUMA_INSUFFICIENT_RESOURCES;
+    return KE_CODE_UNSCHEDULABLE;
+  }
+  if (cs && cs->rcb && !cpuset_fits_cs(nd, cs, &v, (const int64_t(*)[KE_NRES])out)) {
+    *reason = KE_REASON_NUMA_INSUFFICIENT_CPUS; /* "not enough cpus available to satisfy request" */
+    return KE_CODE_UNSCHEDULABLE;
   }
   *affinity = best.mask;
   return KE_CODE_SUCCESS;
@@ -1178,9 +1309,11 @@ static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod,
 int or_numa_distribute(const or_cluster* c, int32_t node, const ke_pod* pod, uint32_t mask, int64_t* out16) {
   const or_node* nd = &c->nodes[node];
   numa_view v;
-  if (numa_view_build(nd, &v) != 0) return -1;
+  numa_cs cs;
+  numa_cs_build(c, nd, pod, &cs);
+  if (numa_view_build(nd, &v, &cs) != 0) return -1;
   int64_t out[KE_MAX_NUMA][KE_NRES];
-  const int ok = numa_distribute(&v, mask, pod, out);
+  const int ok = numa_distribute(&v, mask, pod, out, &cs);
   for (int i = 0; i < 2 * KE_MAX_NUMA; i++) out16[i] = 0;
   for (int z = 0; z < v.n; z++)
     for (int r = 0; r < KE_NRES; r++) out16[2 * v.id[z] + r] = out[z][r];
@@ -1194,10 +1327,12 @@ int or_numa_hints(const or_cluster* c, int32_t node, const ke_pod* pod, int32_t 
                   uint8_t* preferred, int64_t* scores, int32_t* counts, int32_t* present) {
   const or_node* nd = &c->nodes[node];
   numa_view v;
-  if (numa_view_build(nd, &v) != 0) return -1;
+  numa_cs cs;
+  numa_cs_build(c, nd, pod, &cs);
+  if (numa_view_build(nd, &v, &cs) != 0) return -1;
   static __thread numa_hint store[KE_NRES * 255];
   int cnt[KE_NRES], pres[KE_NRES];
-  numa_generate_hints(c, &v, pod, policy, store, cnt, pres);
+  numa_generate_hints(c, nd, &v, pod, policy, store, cnt, pres, &cs);
   for (int r = 0; r < KE_NRES; r++) {
     counts[r] = cnt[r];
     present[r] = pres[r];
@@ -1261,11 +1396,11 @@ int or_numa_exclusive_ok(uint32_t mask, int32_t exclusive, const uint8_t* status
 
 /* the pod's NUMA allocation on its affinity (resourceManager.Allocate -> allocateResourcesByHint) */
 static int numa_allocation(const or_node* nd, const ke_pod* pod, uint32_t affinity, numa_view* v,
-                           int64_t out[KE_MAX_NUMA][KE_NRES]) {
+                           int64_t out[KE_MAX_NUMA][KE_NRES], const numa_cs* cs) {
   memset(out, 0, sizeof(int64_t) * KE_MAX_NUMA * KE_NRES);
-  if (numa_view_build(nd, v) != 0) return 0;
+  if (numa_view_build(nd, v, cs) != 0) return 0;
   if (!affinity) return 1;
-  return numa_distribute(v, affinity, pod, out);
+  return numa_distribute(v, affinity, pod, out, cs);
 }
 
 /* Plugin.Score  scoring.go:66-120 -> scoreWithAmplifiedCPUs :122-139 */
@@ -1279,10 +1414,13 @@ int64_t or_numa_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
     /* the affinity the Filter's Admit stored, the allocation on it, calculateAllocatableAndRequested */
     uint32_t aff = 0;
     int reason;
-    if (n->n_zone == 0 || numa_admit(c, n, pod, policy, exclusive, &aff, &reason) != KE_CODE_SUCCESS) return 0;
+    numa_cs cs;
+    numa_cs_build(c, n, pod, &cs);
+    if (cs.rcb && !cs.valid) return 0; /* scoring.go:93-95 */
+    if (n->n_zone == 0 || numa_admit(c, n, pod, policy, exclusive, &aff, &reason, &cs) != KE_CODE_SUCCESS) return 0;
     numa_view v;
     int64_t out[KE_MAX_NUMA][KE_NRES];
-    if (!numa_allocation(n, pod, aff, &v, out)) return 0;
+    if (!numa_allocation(n, pod, aff, &v, out, &cs)) return 0;
     int64_t alloc[KE_NRES] = {0, 0}, req[KE_NRES] = {0, 0};
     int any = 0;
     for (int z = 0; z < v.n; z++) {
@@ -1299,7 +1437,14 @@ int64_t or_numa_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
       alloc[0] = n->node.allocatable[KE_RES_CPU];
       alloc[1] = n->node.allocatable[KE_RES_MEMORY];
     }
-    return numa_resource_score(&c->cfg.numa, req, alloc, pod->requests);
+    int64_t podreq[KE_NRES] = {pod->requests[KE_RES_CPU], pod->requests[KE_RES_MEMORY]};
+    if (cs.rcb) {
+      /* a non-empty pod cpuset: requested cpu = Amplify(all allocated CPUs of the node * 1000)
+       * (scoring.go:179-185); options.requests carries the amplified cpu */
+      req[0] = amplify(cpus_allocated_count(n) * 1000, v.ratio);
+      if (v.ratio > 1.0) podreq[KE_RES_CPU] = amplify(podreq[KE_RES_CPU], v.ratio);
+    }
+    return numa_resource_score(&c->cfg.numa, req, alloc, podreq);
   }
   /* getResourceOptions -> amplifyNUMANodeResources (util.go:78-87) */
   double ratio;
@@ -1830,36 +1975,98 @@ int or_node_cpus_set(or_cluster* c, int32_t node, int32_t n, const ke_cpu* cpus,
   return KE_OK;
 }
 
-/* NodeNUMAResource Reserve of a cpuset pod on a node without NUMA policy: the allocation
- * (allocateCPUSet) and resourceManager.Update -> addPodAllocation (node_allocation.go:111-156):
- * RefCount++ and the pod's exclusive policy per CPU, the NUMA nodes' single / shared status.
- * Returns -1 when the allocation fails (Reserve fails: the pod is not placed). */
-static int or_cpuset_reserve(or_cluster* c, const ke_pod* pod, int32_t node, uint64_t* out) {
-  or_node* n = &c->nodes[node];
-  memset(out, 0, sizeof(uint64_t) * ACC_WORDS);
+/* NodeNUMAResource Reserve (resourceManager.Allocate with the affinity the Filter stored,
+ * resource_manager.go:194-225): the NUMA allocation on a NUMA-policy node and the cpuset of a binding
+ * pod, both from the state before the pod.  Returns -1 when Allocate fails (Reserve fails: the pod is
+ * not placed). */
+typedef struct reserve_plan {
+  int64_t dist[KE_MAX_NUMA][KE_NRES]; /* per zone of the node (zone order) */
+  uint64_t cpus[ACC_WORDS];
+  int excl;
+} reserve_plan;
+
+static int or_reserve_plan(const or_cluster* c, const ke_pod* pod, int32_t node, reserve_plan* rp) {
+  const or_node* n = &c->nodes[node];
+  memset(rp, 0, sizeof *rp);
   if (pod_requests_zero(pod)) return 0;
-  cpuset_state st;
-  cpuset_prefilter(c, pod, &st);
-  const int rcb = request_cpu_bind(&st, pod, n->node.cpu_bind_policy);
-  if (rcb <= 0) return 0;
-  if (!cpus_valid(n) || cpuset_allocate(c, n, &st, out) != 0) return -1;
-  or_cpus* x = n->cpus;
-  int used[KE_MAX_NUMA + 64], nu = 0;
-  for (int cpu = 0; cpu < ACC_MAX_CPUS; cpu++) {
-    if (!(out[cpu >> 6] >> (cpu & 63) & 1)) continue;
-    x->al.present[cpu] = 1;
-    x->al.ref[cpu]++;
-    x->al.excl[cpu] = st.excl;
-    int f = 0;
-    for (int k = 0; k < nu && !f; k++) f = used[k] == x->t.node[cpu];
-    if (!f && nu < KE_MAX_NUMA + 64) used[nu++] = x->t.node[cpu];
+  int exclusive;
+  const int policy = effective_policy(n, pod, &exclusive);
+  numa_cs cs;
+  numa_cs_build(c, n, pod, &cs);
+  rp->excl = cs.excl;
+  if (cs.rcb && !cs.valid) return -1;
+  numa_view v;
+  int have = 0;
+  if (policy > KE_NUMA_POLICY_NONE && n->n_zone > 0) {
+    uint32_t aff = 0;
+    int reason;
+    if (numa_admit(c, n, pod, policy, exclusive, &aff, &reason, &cs) != KE_CODE_SUCCESS) return cs.rcb ? -1 : 0;
+    if (!numa_allocation(n, pod, aff, &v, rp->dist, &cs)) return cs.rcb ? -1 : 0;
+    have = 1;
   }
-  for (int k = 0; k < nu; k++) /* NUMANodeSharedStatus after adding the pod to sharedNode / singleNUMANode */
-    for (int z = 0; z < n->n_zone; z++)
-      if (n->zone[z].id == used[k])
-        n->zone[z].numa_status = (uint8_t)(nu > 1 || n->zone[z].numa_status == KE_NUMA_STATUS_SHARED
-                                               ? KE_NUMA_STATUS_SHARED
-                                               : KE_NUMA_STATUS_SINGLE);
+  if (cs.rcb &&
+      cpuset_allocate_cs(n, &cs, have ? &v : NULL, have ? (const int64_t(*)[KE_NRES])rp->dist : NULL, rp->cpus) != 0)
+    return -1;
+  return 0;
+}
+
+/* resourceManager.Update -> NodeAllocation.addPodAllocation (node_allocation.go:111-156): RefCount++
+ * and the pod's exclusive policy per CPU, the NUMA nodes' single / shared status, the NUMA allocation
+ * added to the zones' entries (quotav1.Add keys). */
+static void or_reserve_apply(or_cluster* c, int32_t node, const reserve_plan* rp, int64_t* out16) {
+  or_node* n = &c->nodes[node];
+  if (n->cpus) {
+    or_cpus* x = n->cpus;
+    int used[ACC_MAX_CPUS], nu = 0;
+    for (int cpu = 0; cpu < ACC_MAX_CPUS; cpu++) {
+      if (!(rp->cpus[cpu >> 6] >> (cpu & 63) & 1)) continue;
+      x->al.present[cpu] = 1;
+      x->al.ref[cpu]++;
+      x->al.excl[cpu] = rp->excl;
+      int f = 0;
+      for (int k = 0; k < nu && !f; k++) f = used[k] == x->t.node[cpu];
+      if (!f) used[nu++] = x->t.node[cpu];
+    }
+    for (int k = 0; k < nu; k++) /* NUMANodeSharedStatus after adding the pod to sharedNode / singleNUMANode */
+      for (int z = 0; z < n->n_zone; z++)
+        if (n->zone[z].id == used[k])
+          n->zone[z].numa_status = (uint8_t)(nu > 1 || n->zone[z].numa_status == KE_NUMA_STATUS_SHARED
+                                                 ? KE_NUMA_STATUS_SHARED
+                                                 : KE_NUMA_STATUS_SINGLE);
+  }
+  for (int z = 0; z < n->n_zone; z++) {
+    if (rp->dist[z][0] == 0 && rp->dist[z][1] == 0) continue;
+    ke_numa_zone* zn = &n->zone[z];
+    if (out16)
+      for (int r = 0; r < KE_NRES; r++) out16[2 * zn->id + r] = rp->dist[z][r];
+    for (int r = 0; r < KE_NRES; r++) {
+      const uint8_t key = r == KE_RES_CPU ? KE_NUMA_ALLOC_CPU : KE_NUMA_ALLOC_MEMORY;
+      if (!(zn->has_allocated & key)) zn->allocated[r] = 0;
+      if (rp->dist[z][r] != 0) zn->has_allocated |= key;
+      zn->allocated[r] += rp->dist[z][r];
+    }
+    zn->has_allocated |= KE_NUMA_ALLOC_ENTRY;
+  }
+}
+
+/* Golden-vector entry point: resourceManager.Allocate for `pod` on `node` with the hint `mask` (0 =
+ * nil NUMANodeAffinity), resource_manager.go:194-225.  0 and out16[2*id + r] / cpus, or -1. */
+int or_numa_allocate(const or_cluster* c, int32_t node, const ke_pod* pod, uint32_t mask, int64_t* out16,
+                     uint64_t* cpus) {
+  const or_node* nd = &c->nodes[node];
+  numa_cs cs;
+  numa_cs_build(c, nd, pod, &cs);
+  numa_view v;
+  int64_t dist[KE_MAX_NUMA][KE_NRES];
+  memset(dist, 0, sizeof dist);
+  memset(cpus, 0, sizeof(uint64_t) * ACC_WORDS);
+  for (int i = 0; i < 2 * KE_MAX_NUMA; i++) out16[i] = 0;
+  if (numa_view_build(nd, &v, &cs) != 0) return -1;
+  if (mask && !numa_distribute(&v, mask, pod, dist, &cs)) return -1;
+  if (cs.rcb && (!cs.valid || cpuset_allocate_cs(nd, &cs, &v, mask ? (const int64_t(*)[KE_NRES])dist : NULL, cpus) != 0))
+    return -1;
+  for (int z = 0; z < v.n; z++)
+    for (int r = 0; r < KE_NRES; r++) out16[2 * v.id[z] + r] = dist[z][r];
   return 0;
 }
 
@@ -1877,35 +2084,6 @@ int or_node_numa_set(or_cluster* c, int32_t node, int32_t n, const ke_numa_zone*
   c->nodes[node].n_zone = n;
   if (n) memcpy(c->nodes[node].zone, zones, sizeof(ke_numa_zone) * (size_t)n);
   return KE_OK;
-}
-
-/* NodeNUMAResource Reserve for a non-cpuset pod on a node with a NUMA policy: resourceManager.Update ->
- * NodeAllocation.addPodAllocation (node_allocation.go:111-156) adds the NUMA allocation. */
-static void or_numa_reserve(or_cluster* c, const ke_pod* pod, int32_t node, int64_t* out16) {
-  or_node* n = &c->nodes[node];
-  int exclusive;
-  const int policy = effective_policy(n, pod, &exclusive);
-  if (pod_requests_zero(pod) || policy <= KE_NUMA_POLICY_NONE || n->n_zone == 0) return;
-  uint32_t aff = 0;
-  int reason;
-  if (numa_admit(c, n, pod, policy, exclusive, &aff, &reason) != KE_CODE_SUCCESS) return;
-  numa_view v;
-  int64_t out[KE_MAX_NUMA][KE_NRES];
-  if (!numa_allocation(n, pod, aff, &v, out)) return;
-  for (int z = 0; z < v.n; z++) {
-    if (out[z][0] == 0 && out[z][1] == 0) continue;
-    ke_numa_zone* zn = &n->zone[z];
-    if (out16)
-      for (int r = 0; r < KE_NRES; r++) out16[2 * zn->id + r] = out[z][r];
-    /* quotav1.Add(entry, allocation): the allocation holds the keys with a non-zero amount */
-    for (int r = 0; r < KE_NRES; r++) {
-      const uint8_t key = r == KE_RES_CPU ? KE_NUMA_ALLOC_CPU : KE_NUMA_ALLOC_MEMORY;
-      if (!(zn->has_allocated & key)) zn->allocated[r] = 0;
-      if (out[z][r] != 0) zn->has_allocated |= key;
-      zn->allocated[r] += out[z][r];
-    }
-    zn->has_allocated |= KE_NUMA_ALLOC_ENTRY;
-  }
 }
 
 int or_node_devices_set(or_cluster* c, int32_t node, int32_t n, const ke_device* devs) {
@@ -2116,9 +2294,9 @@ static int check_supported(const or_cluster* c, int32_t n_pods, const ke_pod* po
     if (node_unsupported(&c->nodes[i].node)) return KE_ERR_UNSUPPORTED;
     if (c->nodes[i].node.numa_topology_policy != KE_NUMA_POLICY_NONE) numa = 1;
   }
-  /* DeviceShare's own NUMA hints (deviceshare/topology_hint.go) are not restated; neither are the cpuset
-   * hints and allocations under a NUMA topology policy */
-  if ((ds || cpuset) && numa) return KE_ERR_UNSUPPORTED;
+  /* DeviceShare's own NUMA hints (deviceshare/topology_hint.go) are not restated */
+  (void)cpuset;
+  if (ds && numa) return KE_ERR_UNSUPPORTED;
   return KE_OK;
 }
 
@@ -2187,18 +2365,21 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
     chosen[p] = b;
     if (score) score[p] = b >= 0 ? bs : -1;
     uint64_t mask = 0;
-    uint64_t cs[ACC_WORDS] = {0, 0, 0, 0};
-    if (b >= 0 && or_cpuset_reserve(c, &pods[p], b, cs) != 0) { /* Reserve failed: not placed */
+    reserve_plan rp;
+    memset(&rp, 0, sizeof rp);
+    if (b >= 0 && or_reserve_plan(c, &pods[p], b, &rp) != 0) { /* Reserve failed: not placed */
       chosen[p] = -1;
       if (score) score[p] = -1;
       b = -1;
+      memset(&rp, 0, sizeof rp);
     }
-    if (cpusets) memcpy(cpusets + (int64_t)p * ACC_WORDS, cs, sizeof cs);
+    if (cpusets) memcpy(cpusets + (int64_t)p * ACC_WORDS, rp.cpus, sizeof rp.cpus);
     if (b >= 0) {
       /* Reserve in profile order: LoadAware podAssignCache.assign (load_aware.go:192-195) at `now`,
-       * DeviceShare device allocation (plugin.go:426-492); framework assume: NodeInfo.Requested. */
+       * NodeNUMAResource (NUMA allocation + cpuset), DeviceShare device allocation (plugin.go:426-492);
+       * framework assume: NodeInfo.Requested. */
       or_pod_assign(c, b, &pods[p], now);
-      or_numa_reserve(c, &pods[p], b, numa_alloc ? numa_alloc + (int64_t)p * 16 : NULL);
+      or_reserve_apply(c, b, &rp, numa_alloc ? numa_alloc + (int64_t)p * 16 : NULL);
       mask = or_ds_reserve(c, &pods[p], b);
       c->nodes[b].node.requested[KE_RES_CPU] += pods[p].requests[KE_RES_CPU];
       c->nodes[b].node.requested[KE_RES_MEMORY] += pods[p].requests[KE_RES_MEMORY];

@@ -61,6 +61,9 @@ void or_estimate_pod(const or_cluster* c, const ke_pod* pod, int64_t* est);
 
 /* NUMA golden-vector entry points (tryBestToDistributeEvenly on a forced hint; generateResourceHints) */
 int or_numa_distribute(const or_cluster* c, int32_t node, const ke_pod* pod, uint32_t mask, int64_t* out16);
+int or_numa_allocate(const or_cluster* c, int32_t node, const ke_pod* pod, uint32_t mask, int64_t* out16,
+                     uint64_t* cpus);
+void or_set_exact_cpusets(int on);
 int or_numa_exclusive_ok(uint32_t mask, int32_t exclusive, const uint8_t* status, int32_t n);
 int or_numa_hints(const or_cluster* c, int32_t node, const ke_pod* pod, int32_t policy, uint32_t* masks,
                   uint8_t* preferred, int64_t* scores, int32_t* counts, int32_t* present);

@@ -281,3 +281,61 @@ def setup_cpuset_case(handle, case):
         allocated = {c: (1, None) for c in parse_cpuset(case.get("allocated", ""))}
         handle.set_cpus(0, model.make_cpus(rows, allocated))
     return cpuset_pod(case["pod"])
+
+
+# ---- cpusets under NUMA policies (numa_cpuset.json) ----------------------------------------------
+def numa_cpuset_pod(spec):
+    """A binding pod (LSR koord-prod with a required bind policy) or a plain cpu pod."""
+    if spec.get("bind"):
+        return cpuset_pod({"kind": "cpuset", "cpu": spec["cpu"], "required": spec["bind"]})
+    p = model.make_pod(requests={"cpu": spec["cpu"]})
+    if spec.get("other"):
+        p.has_other_requests = 1
+    return p
+
+
+def setup_numa_cpuset_case(handle, case):
+    """Node 0: the resource-manager tests' node, zones with the case's allocation entries, CPU table
+    with the allocated CPUs (RefCount 1)."""
+    n = model.make_node(allocatable=case["node"], amplification_ratio=case.get("ratio"))
+    handle.upsert_node(0, n)
+    zones = [dict(z) for z in case["zones"]]
+    allocated = case.get("allocated")
+    if allocated:
+        for e in allocated["numa"]:
+            zones[e["id"]]["allocated"] = {"cpu": e["cpu"]}
+    handle.set_numa(0, model.make_zones(zones))
+    busy = {c: (1, None) for c in parse_cpuset(allocated["cpuset"])} if allocated else {}
+    handle.set_cpus(0, model.make_cpus(test_topology(*case["topology"]), busy))
+    return numa_cpuset_pod(case["pod"])
+
+
+def setup_numa_score_case(handle, case):
+    """TestNUMANodeScore nodes: zones = allocatable / count, existing pods' requests on NUMA 0, their
+    cpusets 0..cpu-1 for LSR koord-prod pods; returns the pod."""
+    for i, nd in enumerate(case["nodes"]):
+        n = model.make_node(allocatable={"cpu": nd["cpu"], "memory": nd["memory"]})
+        n.numa_topology_policy = NUMA_POLICY_ID[nd["policy"]]
+        handle.upsert_node(i, n)
+        cnt = nd["numa"]
+        cpu_m, mem = model.milli_value(nd["cpu"]), model.value(nd["memory"])
+        zones = [{"id": k, "cpu": f"{cpu_m // cnt}m", "memory": str(mem // cnt)} for k in range(cnt)]
+        ex = [e for e in case["existing"] if e["node"] == i]
+        if ex:
+            zones[0]["allocated"] = {"cpu": f"{sum(model.milli_value(e['cpu']) for e in ex)}m",
+                                     "memory": str(sum(model.value(e["memory"]) for e in ex))}
+        refs = {}
+        for e in ex:
+            if e["lsr"]:
+                for c in range(model.milli_value(e["cpu"]) // 1000):
+                    refs[c] = refs.get(c, 0) + 1
+        if refs:  # addPodAllocation: the LSR pods' CPUs (NUMA 0) make it a single-NUMA node
+            zones[0]["status"] = "single"
+        handle.set_numa(i, model.make_zones(zones))
+        rows = test_topology(cnt, 1, cpu_m // 1000 // 2 // cnt, 2)
+        handle.set_cpus(i, model.make_cpus(rows, {c: (r, None) for c, r in refs.items()}), max(refs.values(), default=1))
+    p = case["pod"]
+    if p["lsr"]:
+        return model.make_pod(requests={"cpu": p["cpu"], "memory": p["memory"]},
+                              labels={"koordinator.sh/qosClass": "LSR"}, priority=9500)
+    return model.make_pod(requests={"cpu": p["cpu"], "memory": p["memory"]})

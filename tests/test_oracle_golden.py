@@ -1,5 +1,6 @@
 """Pin the oracle: every known-answer vector transcribed from the reference's Go tests
 (tests/golden/) must come out of the CPU restatement unchanged."""
+import numpy as np
 import pytest
 
 import cases
@@ -55,7 +56,7 @@ TYPES = {"gpu": 0, "rdma": 1, "fpga": 2}
 
 @pytest.mark.parametrize("case", DS, ids=[c["name"] for c in DS])
 def test_deviceshare(case):
-    from koordinator_amd import abi
+    from koordinator_amd import abi, model
     from oracle.binding import normalize_scores
 
     op, want = case["op"], case["want"]
@@ -134,7 +135,7 @@ NUMA_EXCL = [c for c in NUMA_POLICY if c["op"] == "exclusive"]
 def test_numa_exclusive_policy(case):
     import numpy as np
     from oracle.binding import load
-    from koordinator_amd import abi
+    from koordinator_amd import abi, model
     st = np.array([{"idle": 0, "single": 1, "shared": 2}[x] for x in case["status"]], np.uint8)
     excl = {"Preferred": abi.NUMA_EXCLUSIVE_PREFERRED, "Required": abi.NUMA_EXCLUSIVE_REQUIRED}[case["exclusive"]]
     got = load().or_numa_exclusive_ok(sum(1 << b for b in case["bits"]), excl, abi.ptr(st), len(st))
@@ -179,7 +180,7 @@ CPU_ACC = cases.load("cpu_accumulator.json")
 def _take(rows, max_ref, available, ref, excl_arr, needed, bind, excl, most, preferred):
     import numpy as np
     from oracle.binding import load
-    from koordinator_amd import abi
+    from koordinator_amd import abi, model
     cpus = np.ascontiguousarray(rows, np.int32).ravel()
     out = np.zeros(4, np.uint64)
     pref = None if preferred is None else cases.cpu_bits(preferred)
@@ -237,7 +238,7 @@ CPUSET = cases.load("cpuset.json")
 
 @pytest.mark.parametrize("case", CPUSET, ids=[f'{c["op"]}: {c["name"]}' for c in CPUSET])
 def test_cpuset_plugin(case):
-    from koordinator_amd import abi
+    from koordinator_amd import abi, model
     o = Oracle(abi.default_config(1), 1)
     pod = cases.setup_cpuset_case(o, case)
     if case["op"] == "filter":
@@ -251,3 +252,47 @@ def test_cpuset_plugin(case):
         return
     assert chosen[0] == 0, case["source"]
     assert cases.bits_cpus(o.last_cpusets[0]) == cases.parse_cpuset(case["want"]["cpuset"]), case["source"]
+
+
+# ---- cpusets under NUMA topology policies ----------------------------------------------------------
+NUMA_CPUSET = cases.load("numa_cpuset.json")
+
+
+@pytest.mark.parametrize("exact", [False, True], ids=["counts", "accumulator"])
+@pytest.mark.parametrize("case", NUMA_CPUSET, ids=[f'{c["op"]}: {c["name"]}' for c in NUMA_CPUSET])
+def test_numa_cpuset(case, exact):
+    """Allocate with a hint, BestEffort hint lists and Filter + Score of binding pods against the
+    reference's vectors; `exact` runs hints / admit through the CPU accumulator itself instead of the
+    count reduction (both must agree with the reference)."""
+    from koordinator_amd import abi, model
+    if case["op"] == "node_score":
+        cfg = abi.default_config(len(case["nodes"]))
+        cfg.numa.strategy = abi.STRATEGY_MOST_ALLOCATED
+        o = Oracle(cfg, len(case["nodes"]))
+        o.set_exact_cpusets(exact)
+        pod = cases.setup_numa_score_case(o, case)
+        r = o.eval([pod], cases.NOW)
+        assert list(r["status"][0]) == [abi.CODE_SUCCESS] * len(case["nodes"]), case["source"]
+        assert [int(x) for x in r["numa"][0]] == case["want"]["scores"], case["source"]
+        return
+    o = Oracle(abi.default_config(1), 1)
+    o.set_exact_cpusets(exact)
+    pod = cases.setup_numa_cpuset_case(o, case)
+    if case["op"] == "allocate":
+        mask = sum(1 << b for b in case["hint"])
+        got = o.numa_allocate(0, pod, mask)
+        if case["want"]["error"]:
+            assert got is None, case["source"]
+            return
+        assert got is not None, case["source"]
+        out, cpus = got
+        assert cases.bits_cpus(cpus) == cases.parse_cpuset(case["want"]["cpuset"]), case["source"]
+        want = np.zeros(16, np.int64)
+        for zid, res in case["want"]["numa"].items():
+            want[2 * int(zid)] = model.milli_value(res["cpu"])
+        assert list(out) == list(want), case["source"]
+        return
+    hints = o.numa_hints(0, pod, abi.NUMA_POLICY_BEST_EFFORT)
+    want = [(sum(1 << b for b in h["bits"]), h["preferred"]) for h in case["want"]["cpu"]]
+    assert [(m, p) for m, p, _ in hints.get(0, [])] == want, case["source"]
+    assert 1 not in hints, case["source"]
