@@ -68,22 +68,14 @@ static int check_numa_deviceshare(ke_ctx* ctx, const ke_pod* pods, int32_t n) {
   return KE_OK;
 }
 
-// NodeNUMAResource under a NUMA topology policy hints and allocates cpusets through the NUMA hint
-// providers (resource_manager.go:525-622 with cpusets), which are not implemented: a pod that may bind
-// CPUs (a cpuset pod, or any cpu request while a node forces CPU binding) cannot meet NUMA policies.
+// A pod that may bind CPUs (a cpuset pod, or any cpu request while a node forces CPU binding) reads the
+// CPU SoA during evaluation: make sure it exists.
 static int check_cpuset(ke_ctx* ctx, const ke_pod* pods, int32_t n) {
   Context& c = ctx->c;
-  bool cpuset = false, policy = c.n_policy_nodes > 0;
   for (int32_t p = 0; p < n; p++) {
     const uint32_t f = make_dev_pod(c.cfg, pods[p]).flags;
-    const bool may_bind = (f & PF_CPU_RCB) || (c.n_bind_nodes > 0 && pods[p].requests[KE_RES_CPU] > 0);
-    if (may_bind || (f & PF_CPUSET)) c.cpu_enabled = true;  // the evaluation reads the CPU SoA
-    if (!may_bind) continue;
-    cpuset = true;
-    if (pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE) policy = true;
+    if ((f & PF_CPUSET) || (c.n_bind_nodes > 0 && pods[p].requests[KE_RES_CPU] > 0)) c.cpu_enabled = true;
   }
-  if (cpuset && policy)
-    return fail(KE_ERR_UNSUPPORTED, "cpuset pods with NUMA topology policies (NUMA hints of the CPU accumulator)");
   return KE_OK;
 }
 

@@ -51,6 +51,10 @@ struct AccLds {
   int16_t sp_out[ACC_CPUS];                                         // spread_cpus
   int16_t ord2[ACC_CPUS];
   uint8_t mark[ACC_CPUS];
+  // allocateCPUSet around the accumulator: the CPUs it may take, the exclusivity of the allocated
+  // CPUs before the pod, the union of its per-NUMA takes, the recomputed availability words
+  uint8_t base[ACC_CPUS], ex_core0[ACC_CPUS], ex_node0[ACC_CPUS], uni[ACC_CPUS];
+  int64_t z6[6];
   int16_t order[ACC_CPUS];
   int16_t tmp[ACC_CPUS];
   AccTopo t;

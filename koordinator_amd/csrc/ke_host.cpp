@@ -732,7 +732,7 @@ void derive_cpu_rows(const NodeState& ns, CpuRec* recs, int64_t* cs) {
                              : (n.cpu_amplification_ratio < 0 ? 0.0 : n.cpu_amplification_ratio);
   std::memcpy(&cs[CS_RF], &ratio_f, 8);
   std::memcpy(&cs[CS_RS], &ratio_s, 8);
-  cs[CS_CNT] = 0;
+  for (int f = CS_CNT; f < NUM_CS_FIELDS; f++) cs[f] = 0;
   if (ns.cpus.empty()) return;
   std::vector<int32_t> cores, sockets;
   for (const ke_cpu& c : ns.cpus) cores.push_back(c.core_id), sockets.push_back(c.socket_id);
@@ -750,7 +750,8 @@ void derive_cpu_rows(const NodeState& ns, CpuRec* recs, int64_t* cs) {
     r.flags = (uint8_t)(CR_VALID | (c.reserved ? CR_RESERVED : 0));
   }
   const int cpc = (int)(ns.cpus.size() / cores.size());
-  cs[CS_CNT] = cs_counts(recs, cpc, ns.cpu_max_ref);
+  uint8_t scratch[CPU_SLOTS];
+  cs_fill(recs, cpc, ns.cpu_max_ref, scratch, &cs[CS_CNT], &cs[CS_ZALL]);
   std::vector<std::pair<int32_t, int32_t>> nodes;  // (socket, NUMA node) pairs
   for (const ke_cpu& c : ns.cpus) nodes.push_back({c.socket_id, c.numa_id});
   std::sort(nodes.begin(), nodes.end());

@@ -382,6 +382,26 @@ __device__ __forceinline__ int64_t numa_al(const SoA& s, int64_t i, const NumaNo
   return ((v.ak[r] >> z) & 1u) && a > 0 ? a : 0;
 }
 
+// The sort order of tryBestToDistributeEvenly for resource r: perm[r][nb-1] after insertion passes
+// 1..nb-1 over av[r][0..7] (positions, the reference quirk below).
+__device__ __forceinline__ void numa_perm(NumaNode& v, int r) {
+  uint32_t st = 0x76543210u;
+  v.perm[r][0] = st;
+#pragma unroll
+  for (int ii = 1; ii < 8; ii++) {
+    bool go = true;
+#pragma unroll
+    for (int j = ii; j > 0; j--) {
+      go = go && v.av[r][j] < v.av[r][j - 1];
+      if (go) {
+        const uint32_t a = (st >> (4 * j)) & 15u, b = (st >> (4 * (j - 1))) & 15u;
+        st = (st & ~(0xFFu << (4 * (j - 1)))) | (a << (4 * (j - 1))) | (b << (4 * j));
+      }
+    }
+    v.perm[r][ii] = st;
+  }
+}
+
 // getAvailableNUMANodeResources (node_allocation.go:221-243) and the sort order of
 // tryBestToDistributeEvenly: sort.Slice's insertion sort compares totalAvailable indexed by slice
 // POSITION (a reference quirk), so the permutation of an nb-zone hint depends only on av[r][0..nb-1]
@@ -404,23 +424,51 @@ __device__ __forceinline__ void numa_load(const SoA& s, int64_t i, NumaNode& v) 
       v.av[r][z] = a > 0 ? a : 0;
     }
 #pragma unroll
-  for (int r = 0; r < 2; r++) {
-    uint32_t st = 0x76543210u;
-    v.perm[r][0] = st;
-#pragma unroll
-    for (int ii = 1; ii < 8; ii++) {
-      bool go = true;
-#pragma unroll
-      for (int j = ii; j > 0; j--) {
-        go = go && v.av[r][j] < v.av[r][j - 1];
-        if (go) {
-          const uint32_t a = (st >> (4 * j)) & 15u, b = (st >> (4 * (j - 1))) & 15u;
-          st = (st & ~(0xFFu << (4 * (j - 1)))) | (a << (4 * (j - 1))) | (b << (4 * j));
-        }
-      }
-      v.perm[r][ii] = st;
-    }
+  for (int r = 0; r < 2; r++) numa_perm(v, r);
+}
+
+// A pod that binds CPUs on the node (requestCPUBind): the cpuset part of ResourceOptions
+// (getResourceOptions plugin.go:629-668, getCPUBindPolicy util.go:101-119) and, per NUMA id, the CPUs
+// allocateCPUSet may take there (GetAvailableCPUs after a required policy's filter, CS_Z* words).
+struct NumaCs {
+  bool rcb, req, full;  // binding; required policy; required FullPCPUs
+  int num, cpc, total;  // numCPUsNeeded, CPUs per core, the node's CPUs allocateCPUSet may take
+  int64_t zlo, zhi;     // per NUMA id (16 bits each) the same in the zone
+};
+__device__ __forceinline__ int cs_zc(const NumaCs& c, int z) { return cs_zone(c.zlo, c.zhi, z); }
+
+__device__ __forceinline__ NumaCs numa_cs_load(const SoA& s, int64_t i, uint32_t nf, const DevPod& p) {
+  NumaCs c;
+  const int64_t cnt = s.cs[CS_CNT * s.stride + i];
+  const int preq = pf_cpu_required(p.flags), nb = nf_cpu_bind(nf);
+  int bind = preq;
+  c.req = true;
+  if (preq == XB_NONE) {
+    if (nb == KE_NODE_CPU_BIND_SPREAD_BY_PCPUS) bind = XB_SPREAD;
+    else if (nb == KE_NODE_CPU_BIND_FULL_PCPUS_ONLY) bind = XB_FULL;
+    else c.req = false, bind = pf_cpu_preferred(p.flags);
   }
+  c.rcb = true;
+  c.full = c.req && bind == XB_FULL;
+  c.num = (int)(p.req[0] / 1000);
+  c.cpc = cs_cpc(cnt);
+  const int zw = !c.req ? CS_ZALL : (bind == XB_FULL ? CS_ZFULL : CS_ZSPREAD);
+  c.total = !c.req ? cs_all(cnt) : (bind == XB_FULL ? cs_full(cnt) : cs_spread(cnt));
+  c.zlo = s.cs[zw * s.stride + i];
+  c.zhi = s.cs[(zw + 1) * s.stride + i];
+  return c;
+}
+
+// trimNUMANodeResources (resource_manager.go:166-192): a required policy caps a zone's available cpu at
+// its CPUs the policy leaves; the distribute order follows the trimmed availability.
+__device__ __forceinline__ void numa_trim(NumaNode& v, const NumaCs& c) {
+  if (!c.req) return;
+#pragma unroll
+  for (int z = 0; z < 8; z++) {
+    const int64_t cap = (int64_t)cs_zc(c, z) * 1000;
+    if (v.av[0][z] != 0 && cap < v.av[0][z]) v.av[0][z] = cap;
+  }
+  numa_perm(v, 0);
 }
 
 // q / d for 1 <= d <= 8 (Go int64 division): constant divisors become multiply-high sequences
@@ -488,14 +536,24 @@ __device__ __forceinline__ int numa_min_size(const NumaNode& v, const DevPod& p)
 
 // tryBestToDistributeEvenly over the zones of mask m: true when every requested resource is fully
 // split; OUT: per resource the zones that received a non-zero amount and the amounts (out[r][id]).
-template <bool OUT>
+// CS: the pod may bind CPUs (`cs` non-null): a binding pod splits whole CPUs (whole cores under a
+// required FullPCPUs, splitQuantity :316-330) and its allocateCPUSet must then take numCPUsNeeded CPUs
+// from the zones that received resources — per zone min(cpu/1000, its CPUs), whole cores each under a
+// required FullPCPUs — or from the node when none did.  *split_ok: the split alone.
+template <bool OUT, bool CS = false>
 __device__ __forceinline__ bool numa_distribute(const NumaNode& v, uint32_t m, const DevPod& p, uint32_t* got_mask,
-                                                int64_t (&out)[2][8]) {
-  if (!OUT && !numa_sum_fits(v, m, p)) return false;
+                                                int64_t (&out)[2][8], const NumaCs* cs = nullptr,
+                                                bool* split_ok = nullptr) {
+  if (!OUT && !numa_sum_fits(v, m, p)) {
+    if (split_ok) *split_ok = false;
+    return false;
+  }
+  const bool bind = CS && cs->rcb;
   const int nb = __popc(m);
   uint32_t bl = 0;  // zone ids of m, ascending, one nibble each
   for (uint32_t mm = m, t = 0; mm; mm &= mm - 1, t++) bl |= (uint32_t)(__ffs(mm) - 1) << (4 * t);
-  bool ok = true;
+  bool ok = true, any = false, aligned = true;
+  int taken = 0;
 #pragma unroll
   for (int r = 0; r < 2; r++) {
     if (!OUT && !ok) break;
@@ -505,9 +563,23 @@ __device__ __forceinline__ bool numa_distribute(const NumaNode& v, uint32_t m, c
     for (int t = 0; t < nb; t++) {
       const int z = (int)((bl >> (4 * ((perm >> (4 * t)) & 15u))) & 15u);
       const int64_t a = pick8(v.av[r], z);
-      const int64_t split = div_upto8(q, nb - t);  // splitQuantity
-      const int64_t got = a > split ? split : a;   // allocateRes
+      int64_t split = div_upto8(q, nb - t);  // splitQuantity
+      if (bind && r == 0) {
+        const int64_t val = q >= 0 ? (q + 999) / 1000 : -((-q + 999) / 1000);  // Quantity.Value()
+        split = cs->full ? div_upto8(div_upto8(val, cs->cpc), nb - t) * cs->cpc * 1000 : div_upto8(val, nb - t) * 1000;
+      }
+      const int64_t got = a > split ? split : a;  // allocateRes
       q -= got;
+      if (got != 0) {
+        any = true;
+        if (bind && r == 0) {
+          const int k = min((int)(got / 1000), cs_zc(*cs, z));
+          if (k > 0) {
+            taken += k;
+            if (k % cs->cpc) aligned = false;
+          }
+        }
+      }
       if (OUT && got != 0) {
         got_mask[r] |= 1u << z;
 #pragma unroll
@@ -516,6 +588,8 @@ __device__ __forceinline__ bool numa_distribute(const NumaNode& v, uint32_t m, c
     }
     if (q != 0) ok = false;
   }
+  if (split_ok) *split_ok = ok;
+  if (bind) ok = ok && cs->total >= cs->num && (!any || (taken == cs->num && (!cs->full || aligned)));
   return ok;
 }
 
@@ -580,9 +654,13 @@ __device__ __forceinline__ bool exclusive_ok(const NumaNode& v, uint32_t m, bool
 // (policy.go:198-260), every merged hint non-preferred; an unsatisfied result (or a resource without
 // hints) -> any NUMA node.  Lists in resource-name order (cpu, memory): the reference ranges over a Go
 // map here, so its order — and with it this tie-break — is not deterministic.
+// ps: the requests the hint scores see (options.requests; a binding pod's cpu amplified)
+template <bool CS = false>
 __device__ __forceinline__ uint32_t numa_best_effort_fallback(const SoA& s, int64_t i, const NumaNode& v, const DevPod& p,
                                                            const KArgs& k, const bool (&present)[2],
-                                                           const uint32_t (&lack)[2]) {
+                                                           const uint32_t (&lack)[2], const NumaCs* cs = nullptr,
+                                                           const DevPod* ps = nullptr) {
+  const DevPod& sp = CS ? *ps : p;
   uint64_t L[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
   int64_t dummy[2][8];
   for (int e = 0; e < 255; e++) {
@@ -590,7 +668,7 @@ __device__ __forceinline__ uint32_t numa_best_effort_fallback(const SoA& s, int6
     if (m & ~v.zm) continue;
     const bool in0 = present[0] && !(m & lack[0]), in1 = present[1] && !(m & lack[1]);
     if (!in0 && !in1) continue;
-    if (!numa_distribute<false>(v, m, p, nullptr, dummy)) continue;
+    if (!numa_distribute<false, CS>(v, m, p, nullptr, dummy, cs)) continue;
     const uint64_t bit = 1ull << (m & 63u);
     const int w = (int)(m >> 6);
 #pragma unroll
@@ -609,7 +687,7 @@ __device__ __forceinline__ uint32_t numa_best_effort_fallback(const SoA& s, int6
     for (int e = 0; e < 255; e++) {
       const uint32_t m = NUMA_ORDER[e];
       if ((m & ~v.zm) || !in_list(L[r], m)) continue;
-      const int32_t sc = numa_hint_score(s, i, v, m, p, k);
+      const int32_t sc = numa_hint_score(s, i, v, m, sp, k);
       if (narrower(m, best) || (__popc(m) == __popc(best) && sc > bsc)) {
         best = m;
         bsc = sc;
@@ -629,10 +707,10 @@ __device__ __forceinline__ uint32_t numa_best_effort_fallback(const SoA& s, int6
       const bool un = max(__popc(m1), __popc(m2)) != __popc(mg);
       int32_t sc = 0;
       if (m1 == mg) {
-        if (s1 < 0) s1 = numa_hint_score(s, i, v, m1, p, k);
+        if (s1 < 0) s1 = numa_hint_score(s, i, v, m1, sp, k);
         sc += s1;
       }
-      if (m2 == mg) sc += numa_hint_score(s, i, v, m2, p, k);
+      if (m2 == mg) sc += numa_hint_score(s, i, v, m2, sp, k);
       if (narrower(mg, best) || (__popc(mg) == __popc(best) && sc > bsc)) {
         best = mg;
         bsc = sc;
@@ -666,10 +744,25 @@ __device__ __forceinline__ void numa_present_lack(const NumaNode& v, const DevPo
 // preferred merged hint returns STATUS_DEFERRED instead of running the full merge here (one lane
 // needing it would hold its whole wavefront; k_numa_fallback runs those pairs compacted).
 // FB_AFF: the BestEffort full-merge result was computed by the caller (k_numa_fallback) and is `fb_aff`.
-template <bool DEFER, bool FB_AFF = false>
+// CS: a binding pod (`cs`, `ps` = its amplified requests for the hint scores): never deferred; every
+// allocation check includes allocateCPUSet's take, a nil affinity the node-wide one.
+template <bool DEFER, bool FB_AFF = false, bool CS = false>
 __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t nf, int policy, const NumaNode& v,
-                                               const DevPod& p, const KArgs& k, uint32_t fb_aff = 0) {
+                                               const DevPod& p, const KArgs& k, uint32_t fb_aff = 0,
+                                               const NumaCs* cs = nullptr, const DevPod* ps = nullptr) {
   NumaPick o{KE_CODE_SUCCESS, KE_REASON_NONE, 0u};
+  const DevPod& sp = CS ? *ps : p;
+  // Allocate on the chosen affinity (topologymanager allocateResources -> tryAllocateFromNode)
+  auto allocate_on = [&](uint32_t aff) {
+    int64_t dummy2[2][8];
+    bool split = true;
+    const bool fits = aff ? numa_distribute<false, CS>(v, aff, p, nullptr, dummy2, cs, &split)
+                          : (!CS || cs->total >= cs->num);
+    if (!fits) {
+      o.status = KE_CODE_UNSCHEDULABLE;
+      o.reason = split ? KE_REASON_NUMA_INSUFFICIENT_CPUS : KE_REASON_NUMA_INSUFFICIENT_RESOURCES;
+    }
+  };
   const bool excl = (p.flags & PF_NUMA_EXCL_REQ) != 0;
   if (v.zm == 0) {  // topology_hint.go:31-41
     o.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
@@ -693,12 +786,8 @@ __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t
       o.reason = KE_REASON_NUMA_HINT_UNALIGNED;
       return o;
     }
-    if (policy == KE_NUMA_POLICY_SINGLE_NUMA_NODE) return o;  // best == all -> nil affinity
-    o.aff = all;
-    if (!numa_distribute<false>(v, all, p, nullptr, dummy)) {
-      o.status = KE_CODE_UNSCHEDULABLE;
-      o.reason = KE_REASON_NUMA_INSUFFICIENT_RESOURCES;
-    }
+    o.aff = policy == KE_NUMA_POLICY_SINGLE_NUMA_NODE ? 0u : all;  // best == all -> nil affinity
+    allocate_on(o.aff);
     return o;
   }
   // Preferred merged hints are the masks in every present list that are preferred in each (of the
@@ -716,13 +805,13 @@ __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t
       if (m & ~all) continue;
       const bool in0 = present[0] && !(m & lack[0]), in1 = present[1] && !(m & lack[1]);
       if (!in0 && !in1) continue;
-      if (!numa_distribute<false>(v, m, p, nullptr, dummy)) continue;
+      if (!numa_distribute<false, CS>(v, m, p, nullptr, dummy, cs)) continue;
       if (in0 && !minr[0]) minr[0] = sz;
       if (in1 && !minr[1]) minr[1] = sz;
       bool cand = (!present[0] || in0) && (!present[1] || in1);
       if (policy != KE_NUMA_POLICY_RESTRICTED) cand = cand && (!present[0] || first0) && (!present[1] || first1);
       if (!cand || !exclusive_ok(v, m, excl)) continue;
-      const int32_t sc = R * numa_hint_score(s, i, v, m, p, k);
+      const int32_t sc = R * numa_hint_score(s, i, v, m, sp, k);
       if (!found || narrower(m, best) || (__popc(m) == __popc(best) && sc > bsc)) {
         best = m;
         bsc = sc;
@@ -733,6 +822,7 @@ __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t
   }
   if (found) {
     o.aff = (policy == KE_NUMA_POLICY_SINGLE_NUMA_NODE && best == all) ? 0u : best;
+    if (CS && !o.aff) allocate_on(0u);  // a hint passed its allocation already
     return o;
   }
   if (policy != KE_NUMA_POLICY_BEST_EFFORT) {
@@ -740,25 +830,26 @@ __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t
     o.reason = KE_REASON_NUMA_HINT_UNALIGNED;
     return o;
   }
-  if (DEFER) {
+  if (DEFER && !CS) {
     o.status = STATUS_DEFERRED;
     return o;
   }
-  o.aff = FB_AFF ? fb_aff : numa_best_effort_fallback(s, i, v, p, k, present, lack);
-  if (!numa_distribute<false>(v, o.aff, p, nullptr, dummy)) {
-    o.status = KE_CODE_UNSCHEDULABLE;
-    o.reason = KE_REASON_NUMA_INSUFFICIENT_RESOURCES;
-  }
+  o.aff = FB_AFF ? fb_aff : numa_best_effort_fallback<CS>(s, i, v, p, k, present, lack, cs, ps);
+  allocate_on(o.aff);
   return o;
 }
 
 // Score under a NUMA policy (scoring.go:101-119): the allocation on the affinity, NUMA-scope
 // allocatable / requested of the zones it touches, else the node's.
+// CS: a binding pod's requested cpu is Amplify(the node's allocated CPUs * 1000) (scoring.go:179-185),
+// scored with its amplified requests `ps`.
+template <bool CS = false>
 __device__ __forceinline__ int32_t numa_policy_score(const SoA& s, int64_t i, const NumaNode& v, uint32_t aff,
-                                                     const DevPod& p, const KArgs& k, const NodeRegs& n) {
+                                                     const DevPod& p, const KArgs& k, const NodeRegs& n,
+                                                     const NumaCs* cs = nullptr, const DevPod* ps = nullptr) {
   int64_t out[2][8] = {{0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0, 0}};
   uint32_t got[2] = {0, 0};
-  if (aff) numa_distribute<true>(v, aff, p, got, out);
+  if (aff) numa_distribute<true, CS>(v, aff, p, got, out, cs);
   const uint32_t zs = got[0] | got[1];
   int64_t req[2] = {n.nreq[0], n.nreq[1]}, alloc[2] = {n.nalloc[0], n.nalloc[1]};
   if (zs) {
@@ -772,7 +863,8 @@ __device__ __forceinline__ int32_t numa_policy_score(const SoA& s, int64_t i, co
           req[r] += numa_al(s, i, v, z, r);
         }
   }
-  return numa_scope_score((k.flags & AF_NUMA_MOST) != 0, req, alloc, p, k);
+  if (CS) req[0] = amplify_bits(n.csm, s.cs[CS_RS * s.stride + i]);
+  return numa_scope_score((k.flags & AF_NUMA_MOST) != 0, req, alloc, CS ? *ps : p, k);
 }
 
 // NodeNUMAResource Reserve of a non-cpuset pod under a NUMA policy: NodeAllocation.addPodAllocation
@@ -915,17 +1007,32 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
   const bool npol = NUMA && !(p.flags & PF_NUMA_SKIP) && eff_pol != KE_NUMA_POLICY_NONE;
   int32_t npol_score = 0;
   if (npol && o.status == KE_CODE_SUCCESS) {
-    const NumaPick pk = numa_admit<DEFER, FB_AFF>(s, i, nf, eff_pol, nv, p, k, fb_aff);
-    if (DEFER && pk.status == STATUS_DEFERRED) {
-      o.status = STATUS_DEFERRED;
-      o.total = -1;
-      return o;
-    }
-    if (pk.status != KE_CODE_SUCCESS) {
-      o.status = pk.status;
-      o.reason = pk.reason;
+    if (CPU && rcb > 0) {  // a binding pod: cpuset hints and allocation (resource_manager.go:166-192,353-459)
+      const NumaCs cs = numa_cs_load(s, i, nf, p);
+      DevPod ps = p;  // options.requests: cpu amplified (plugin.go:634-640)
+      ps.req[0] = amplify_bits(p.req[0], s.cs[CS_RS * s.stride + i]);
+      NumaNode tv = nv;
+      numa_trim(tv, cs);
+      const NumaPick pk = numa_admit<false, false, true>(s, i, nf, eff_pol, tv, p, k, 0u, &cs, &ps);
+      if (pk.status != KE_CODE_SUCCESS) {
+        o.status = pk.status;
+        o.reason = pk.reason;
+      } else {
+        npol_score = numa_policy_score<true>(s, i, tv, pk.aff, p, k, n, &cs, &ps);
+      }
     } else {
-      npol_score = numa_policy_score(s, i, nv, pk.aff, p, k, n);
+      const NumaPick pk = numa_admit<DEFER, FB_AFF>(s, i, nf, eff_pol, nv, p, k, fb_aff);
+      if (DEFER && pk.status == STATUS_DEFERRED) {
+        o.status = STATUS_DEFERRED;
+        o.total = -1;
+        return o;
+      }
+      if (pk.status != KE_CODE_SUCCESS) {
+        o.status = pk.status;
+        o.reason = pk.reason;
+      } else {
+        npol_score = numa_policy_score(s, i, nv, pk.aff, p, k, n);
+      }
     }
   }
   // ---- DeviceShare.Filter + raw Score  plugin.go:311-365, scoring.go:45-103
@@ -1122,7 +1229,7 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
   const int p1 = min(batch_pods, p0 + pods_per_block);
   for (int p = p0; p < p1; p++) {
     const DevPod& pod = pods[base + p];
-    const EvalOut o = eval_pair<DS, NUMA, NUMA, false, CPU>(n, expired, pod, k, s, i, nv);
+    const EvalOut o = eval_pair<DS, NUMA, NUMA && !CPU, false, CPU>(n, expired, pod, k, s, i, nv);
     scores[(int64_t)p * score_stride + i] = (uint16_t)(o.total + 1);
     if (NUMA) defer_push(o.status == STATUS_DEFERRED, ((uint64_t)p << 32) | (uint32_t)i, defer_list, defer_cnt);
     if (DS && (pod.flags & PF_DS)) dsraw[i] = o.total >= 0 ? (uint16_t)(o.ds + 1) : (uint16_t)0;
@@ -1874,10 +1981,30 @@ __device__ void reserve_row(const SoA& s, int64_t node, uint32_t nf, const DevPo
   f[(F_NREQ + 1) * st] += pod.req[1];
 }
 
-// allocateCPUSet without a NUMA hint (resource_manager.go:353-459): the node's CPU table into LDS,
-// getAvailableCPUs, filterCPUsByRequiredCPUBindPolicy (:655-695), takePreferredCPUs without preferred
-// CPUs (= takeCPUs), satisfiedRequiredCPUBindPolicy (:697-718).  Thread 0 only; a.res = the cpuset.
-__device__ bool cpuset_allocate(const SoA& s, int64_t node, uint32_t nf, const DevPod& pod, AccLds& a) {
+// One takePreferredCPUs call (no preferred CPUs = takeCPUs, cpu_accumulator.go:29-85) over the CPUs of
+// `a.base` in NUMA id `zone` (-1 = all) not yet in `a.uni`, from the pre-pod exclusivity; adds the
+// result to a.uni.  needed <= 0 takes nothing.
+__device__ bool cpuset_take(AccLds& a, int zone, int needed, int bind) {
+  if (needed <= 0) return true;
+  for (int c = 0; c < CPU_SLOTS; c++) {
+    a.alloc[c] = a.base[c] && !a.uni[c] && (zone < 0 || a.cpu[c].numa == zone);
+    a.res[c] = 0;
+    a.ex_core[c] = a.ex_core0[c];
+    a.ex_node[c] = a.ex_node0[c];
+  }
+  a.needed = needed;
+  if (!acc_take_cpus(a, bind)) return false;
+  for (int c = 0; c < CPU_SLOTS; c++) a.uni[c] |= a.res[c];
+  return true;
+}
+
+// allocateCPUSet (resource_manager.go:353-459): the node's CPU table into LDS, getAvailableCPUs, the
+// required-policy filter (filterCPUsByRequiredCPUBindPolicy :655-695); with a NUMA allocation (zones
+// `zmask`, cpu milli `zcpu[id]`) one take per zone in id order of min(cpu/1000, its CPUs) CPUs, which
+// must add up to numCPUsNeeded; else one take over the node; then satisfiedRequiredCPUBindPolicy
+// (:697-718).  Thread 0 only; a.res = the cpuset.
+__device__ bool cpuset_allocate(const SoA& s, int64_t node, uint32_t nf, const DevPod& pod, AccLds& a, uint32_t zmask,
+                                const int64_t (&zcpu)[8]) {
   const int64_t st = s.stride;
   const CpuRec* recs = s.cpu + node * CPU_SLOTS;
   const int64_t cnt = s.cs[CS_CNT * st + node], topo = s.cs[CS_TOPO * st + node];
@@ -1896,37 +2023,51 @@ __device__ bool cpuset_allocate(const SoA& s, int64_t node, uint32_t nf, const D
     else required = false, bind = pf_cpu_preferred(pod.flags);
   }
   uint8_t* navail_core = a.core_n;  // LDS scratch until the accumulator runs
-  for (int k = 0; k < CPU_SLOTS; k++) navail_core[k] = 0, a.ex_core[k] = 0, a.ex_node[k] = 0;
+  for (int k = 0; k < CPU_SLOTS; k++) navail_core[k] = 0, a.ex_core0[k] = 0, a.ex_node0[k] = 0, a.uni[k] = 0;
   for (int c = 0; c < CPU_SLOTS; c++) {
     const CpuRec r = recs[c];
     a.cpu[c] = r;
-    a.res[c] = 0;
-    a.alloc[c] = cpu_available(r, max_ref) ? 1 : 0;
+    a.base[c] = cpu_available(r, max_ref) ? 1 : 0;
     a.aref[c] = r.ref;
-    if (a.alloc[c]) navail_core[r.core]++;
+    if (a.base[c]) navail_core[r.core]++;
     if ((r.flags & CR_VALID) && r.ref > 0) {  // exclusiveInCores / exclusiveInNUMANodes of the allocated CPUs
-      if (r.excl == KE_CPU_EXCL_PCPU_LEVEL) a.ex_core[r.core] = 1;
-      else if (r.excl == KE_CPU_EXCL_NUMA_NODE_LEVEL) a.ex_node[r.numa] = 1;
+      if (r.excl == KE_CPU_EXCL_PCPU_LEVEL) a.ex_core0[r.core] = 1;
+      else if (r.excl == KE_CPU_EXCL_NUMA_NODE_LEVEL) a.ex_node0[r.numa] = 1;
     }
   }
   if (required) {
     for (int k = 0; k < CPU_SLOTS; k++) a.mark[k] = 0;
     for (int c = 0; c < CPU_SLOTS; c++) {
-      if (!a.alloc[c]) continue;
+      if (!a.base[c]) continue;
       const int k = a.cpu[c].core;
       const bool lowest = !a.mark[k];
       a.mark[k] = 1;
-      if ((bind == XB_FULL && navail_core[k] != cpc) || (bind == XB_SPREAD && !lowest)) a.alloc[c] = 0;
+      if ((bind == XB_FULL && navail_core[k] != cpc) || (bind == XB_SPREAD && !lowest)) a.base[c] = 0;
     }
   }
+  int navail = 0;
+  for (int c = 0; c < CPU_SLOTS; c++) navail += a.base[c];
   const int ncpu = (int)(pod.req[0] / 1000);
-  if (acc_count_alloc(a) < ncpu) return false;
+  if (navail < ncpu) return false;
   a.max_ref = max_ref;
-  a.needed = ncpu;
   a.excl_policy = (pod.flags & PF_CPU_RCB) ? pf_cpu_excl(pod.flags) : KE_CPU_EXCL_NONE;
   a.exclusive = a.excl_policy == KE_CPU_EXCL_PCPU_LEVEL || a.excl_policy == KE_CPU_EXCL_NUMA_NODE_LEVEL;
   a.numa_most = (nf & NF_CPU_NUMA_MOST) ? 1 : 0;
-  if (!acc_take_cpus(a, bind)) return false;
+  int needed = ncpu;
+  if (zmask) {
+    for (int z = 0; z < 8; z++) {
+      if (!((zmask >> z) & 1u)) continue;
+      int inzone = 0;
+      for (int c = 0; c < CPU_SLOTS; c++) inzone += a.base[c] && a.cpu[c].numa == z;
+      if (!cpuset_take(a, z, min((int)(zcpu[z] / 1000), inzone), bind)) return false;
+    }
+    int got = 0;
+    for (int c = 0; c < CPU_SLOTS; c++) got += a.uni[c];
+    needed -= got;
+    if (needed != 0) return false;
+  }
+  if (needed > 0 && !cpuset_take(a, -1, needed, bind)) return false;
+  for (int c = 0; c < CPU_SLOTS; c++) a.res[c] = a.uni[c];
   if (required) {
     for (int k = 0; k < CPU_SLOTS; k++) a.mark[k] = 0;
     int n = 0, ncore = 0;
@@ -1965,24 +2106,60 @@ __device__ void cpuset_commit(const SoA& s, int64_t node, const DevPod& pod, Acc
   f[F_CSM * st] = cs_milli;
   f[F_CSAF * st] = amplify_bits(cs_milli, s.cs[CS_RF * st + node]);
   f[F_CSAS * st] = amplify_bits(cs_milli, s.cs[CS_RS * st + node]);
-  // cs_counts with the per-core counter in LDS
+  // the availability counts, per-core counter in LDS
   const int64_t cnt = s.cs[CS_CNT * st + node];
-  const int cpc = cs_cpc(cnt), max_ref = cs_max_ref(cnt);
-  for (int k = 0; k < CPU_SLOTS; k++) a.core_n[k] = 0;
-  for (int c = 0; c < CPU_SLOTS; c++)
-    if (cpu_available(a.cpu[c], max_ref)) a.core_n[a.cpu[c].core]++;
-  int full = 0, spread = 0;
-  for (int k = 0; k < CPU_SLOTS; k++) {
-    if (a.core_n[k] == cpc && cpc > 0) full += cpc;
-    if (a.core_n[k] > 0) spread++;
-  }
-  s.cs[CS_CNT * st + node] = cs_pack(full, spread, cpc, max_ref);
+  int64_t ncnt;
+  cs_fill(a.cpu, cs_cpc(cnt), cs_max_ref(cnt), a.core_n, &ncnt, a.z6);
+  s.cs[CS_CNT * st + node] = ncnt;
+  for (int w = 0; w < 6; w++) s.cs[(CS_ZALL + w) * st + node] = a.z6[w];
 }
 
-// A cpuset pod's singleton batch after k_select: selectHost's node, then Reserve in profile order —
-// LoadAware, NodeNUMAResource (the cpuset; failure = Reserve fails, the pod stays unplaced),
-// DeviceShare.  One thread: the accumulator is sequential (sorted lists, greedy takes).
-template <bool DS>
+// NodeNUMAResource Reserve of a pod in a CPU batch on a NUMA-policy node: the allocation (`dist`) joins
+// the zones' entries (quotav1.Add keys, numa_reserve); under a cpu ratio > 1 an entry's cpu is the
+// allocated cpu - cpusets + Amplify(cpusets) of its zone (node_allocation.go:221-243), re-adjusted for
+// the zones whose cpuset count changed (`cs_old` -> `cs_new`, CPUs per NUMA id); the cpuset's NUMA ids
+// become single / shared (node_allocation.go:111-156 and GetAllNUMANodeStatus).
+__device__ void numa_reserve_cs(const SoA& s, int64_t i, uint32_t nf, const NumaNode& v, const uint32_t (&got)[2],
+                                const int64_t (&dist)[2][8], const int (&cs_old)[8], const int (&cs_new)[8],
+                                uint32_t used, int n_used, int64_t* out16) {
+  const int64_t ratio = s.cs[CS_RS * s.stride + i];
+  for (int z = 0; z < 8; z++) {
+    for (int r = 0; r < 2; r++) {
+      if (out16) out16[2 * z + r] = dist[r][z];
+      int64_t* f = s.nf + (NUMA_AL + 2 * z + r) * s.stride + i;
+      const bool entry_before = (v.ak[0] >> z) & 1u, entry_after = entry_before || (((got[0] | got[1]) >> z) & 1u);
+      if (r == 0 && (nf & NF_NUMA_AL_AMP)) {
+        if (!entry_after) continue;
+        const int64_t o = (int64_t)cs_old[z] * 1000, n = (int64_t)cs_new[z] * 1000;
+        const int64_t raw = entry_before ? *f + o - amplify_bits(o, ratio) : 0;
+        *f = raw + dist[0][z] - n + amplify_bits(n, ratio);
+      } else if ((got[r] >> z) & 1u) {
+        *f = (((v.ak[r] >> z) & 1u) ? *f : 0) + dist[r][z];
+      }
+    }
+  }
+  uint32_t ak0 = v.ak[0] | got[0];
+  if (nf & NF_NUMA_AL_AMP) ak0 |= got[1];
+  const uint32_t ak1 = v.ak[1] | got[1];
+  uint32_t single = v.single, shared = v.shared;
+  const uint32_t tracked = v.zm & ((1u << __popc(v.zm)) - 1u);  // ids < len(numaNodes) with a zone
+  for (int z = 0; z < 8; z++) {
+    if (!((used >> z) & 1u) || !((tracked >> z) & 1u)) continue;
+    if (n_used > 1 || ((shared >> z) & 1u)) shared |= 1u << z, single &= ~(1u << z);
+    else single |= 1u << z;
+  }
+  uint64_t m = s.nm[i];
+  m |= ((uint64_t)ak0 << NUMA_M_AL) | ((uint64_t)ak1 << (NUMA_M_AL + 8));
+  m &= ~((uint64_t)0xFFFF << NUMA_M_ST);
+  m |= ((uint64_t)single << NUMA_M_ST) | ((uint64_t)shared << (NUMA_M_ST + 8));
+  s.nm[i] = m;
+}
+
+// A singleton batch of a pod that may bind CPUs, after k_select: selectHost's node, then Reserve in
+// profile order — LoadAware, NodeNUMAResource (the NUMA allocation on the affinity Admit picks and the
+// cpuset; a failed Allocate fails Reserve and the pod stays unplaced), DeviceShare.  One thread: the
+// accumulator is sequential (sorted lists, greedy takes).  NUMA: nodes may carry NUMA policies.
+template <bool DS, bool NUMA>
 __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __restrict__ pods, int32_t* __restrict__ batch_base,
                                                        KArgs k, const uint32_t* __restrict__ cand,
                                                        const int32_t* __restrict__ cand_cnt, int32_t* __restrict__ chosen,
@@ -2000,16 +2177,69 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
   for (int c = 0; c < cnt; c++) w = max(w, cand[c]);
   int32_t out_node = -1, out_score = -1;
   uint64_t alloc = 0, set[4] = {0, 0, 0, 0};
+  int64_t* out16 = numa_alloc ? numa_alloc + (int64_t)base * 16 : nullptr;
+  if (out16)
+    for (int t = 0; t < 16; t++) out16[t] = 0;
   if (w) {
     const int64_t node = key_node(w);
     const uint32_t nf = s.flags[node];
     const bool rcb = !(pod.flags & PF_NUMA_SKIP) &&
                      ((pod.flags & PF_CPU_RCB) ||
                       (pod.req[0] != 0 && nf_cpu_bind(nf) != KE_NODE_CPU_BIND_NONE && (pod.flags & PF_CPU_INT)));
-    const bool ok = !rcb || ((nf & NF_CPUS_VALID) && cpuset_allocate(s, node, nf, pod, a));
+    const int pol = pf_numa_policy(pod.flags) ? pf_numa_policy(pod.flags) : nf_numa_policy(nf);
+    const bool nsoa = NUMA && s.nm != nullptr;  // the node's zones (if any) live in the NUMA SoA
+    const bool npol = nsoa && !(pod.flags & PF_NUMA_SKIP) && pol != KE_NUMA_POLICY_NONE;
+    bool ok = !rcb || (nf & NF_CPUS_VALID);
+    NumaNode v;
+    if (nsoa) numa_load(s, node, v);
+    uint32_t got[2] = {0, 0};
+    int64_t dist[2][8] = {{0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0, 0}};
+    if (ok && npol) {  // the affinity the Filter's Admit stored and the allocation on it
+      NumaPick pk;
+      if (rcb) {
+        const NumaCs cs = numa_cs_load(s, node, nf, pod);
+        DevPod ps = pod;
+        ps.req[0] = amplify_bits(pod.req[0], s.cs[CS_RS * s.stride + node]);
+        NumaNode tv = v;
+        numa_trim(tv, cs);
+        pk = numa_admit<false, false, true>(s, node, nf, pol, tv, pod, k, 0u, &cs, &ps);
+        if (pk.status == KE_CODE_SUCCESS && pk.aff) numa_distribute<true, true>(tv, pk.aff, pod, got, dist, &cs);
+        ok = pk.status == KE_CODE_SUCCESS;
+      } else {
+        pk = numa_admit<false>(s, node, nf, pol, v, pod, k);
+        if (pk.status == KE_CODE_SUCCESS && pk.aff) numa_distribute<true>(v, pk.aff, pod, got, dist);
+      }
+    }
+    int cs_old[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // allocated CPUs per NUMA id before the pod
+    if (nsoa && v.zm) {
+      const CpuRec* recs = s.cpu + node * CPU_SLOTS;
+      for (int c = 0; c < CPU_SLOTS; c++) {
+        const CpuRec r = recs[c];
+        if ((r.flags & CR_VALID) && r.ref > 0 && r.numa < 8) cs_old[r.numa]++;
+      }
+    }
+    if (ok && rcb) {
+      const int64_t zcpu[8] = {dist[0][0], dist[0][1], dist[0][2], dist[0][3],
+                               dist[0][4], dist[0][5], dist[0][6], dist[0][7]};
+      ok = cpuset_allocate(s, node, nf, pod, a, got[0] | got[1], zcpu);
+    }
     if (ok) {
       reserve_row(s, node, nf, pod);
-      if (rcb) cpuset_commit(s, node, pod, a, set);
+      uint32_t used = 0;
+      int n_used = 0;
+      int cs_new[8] = {cs_old[0], cs_old[1], cs_old[2], cs_old[3], cs_old[4], cs_old[5], cs_old[6], cs_old[7]};
+      if (rcb) {
+        cpuset_commit(s, node, pod, a, set);
+        for (int c = 0; c < CPU_SLOTS; c++) a.mark[c] = 0;
+        for (int c = 0; c < CPU_SLOTS; c++) {
+          if (!a.res[c]) continue;
+          const int z = a.cpu[c].numa;
+          if (!a.mark[z]) n_used++;
+          a.mark[z] = 1;
+          if (z < 8) used |= 1u << z, cs_new[z] += a.cpu[c].ref == 1;  // a CPU newly allocated
+        }
+      }
+      if (nsoa && v.zm) numa_reserve_cs(s, node, nf, v, got, dist, cs_old, cs_new, used, n_used, out16);
       if (DS && (pod.flags & PF_DS) && (nf & NF_DS_CACHE)) alloc = ds_reserve(s, node, pod, k);
       out_node = (int32_t)node + global_offset;
       out_score = key_score(w);
@@ -2019,8 +2249,6 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
   chosen_score[base] = out_score;
   dev_alloc[base] = alloc;
   for (int q = 0; q < 4; q++) cpusets[(int64_t)base * 4 + q] = set[q];
-  if (numa_alloc)
-    for (int t = 0; t < 16; t++) numa_alloc[(int64_t)base * 16 + t] = 0;
   for (int u = 0; u < 6; u++) pstamps[8 * batch_index + u] = t0;  // no prologue: all "replay"
   *batch_base = base + 1;
   stamps[batch_index + 1] = __builtin_amdgcn_s_memrealtime();
@@ -2564,7 +2792,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       if (hi > lo) {
         dim3 grid((unsigned)((hi - lo + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((bp + ppb - 1) / ppb));
         // a binding pod never meets a NUMA policy (ke_capi check_cpuset): its batch skips the NUMA path
-        auto eval = cpu ? (ds ? k_eval_batch<true, false, true> : k_eval_batch<false, false, true>)
+        auto eval = cpu ? (ds ? k_eval_batch<true, false, true> : numa ? k_eval_batch<false, true, true> : k_eval_batch<false, false, true>)
                         : ds ? (numa ? k_eval_batch<true, true, false> : k_eval_batch<true, false, false>)
                              : (numa ? k_eval_batch<false, true, false> : k_eval_batch<false, false, false>);
         uint32_t* dcnt = numa ? d->d_defer_cnt + b : nullptr;
@@ -2616,7 +2844,9 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     }
     if (prof) HIP_OK(hipEventRecord(pe[2], d->stream));
     if (cpu) {
-      hipLaunchKernelGGL((ds ? k_cpuset_reserve<true> : k_cpuset_reserve<false>), dim3(1), dim3(64), 0, d->stream, d->soa,
+      hipLaunchKernelGGL((ds ? (numa ? k_cpuset_reserve<true, true> : k_cpuset_reserve<true, false>)
+                             : (numa ? k_cpuset_reserve<false, true> : k_cpuset_reserve<false, false>)),
+                         dim3(1), dim3(64), 0, d->stream, d->soa,
                          d->d_pods, d->d_batch_base, k, d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score,
                          ctx->cfg.global_node_offset, d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc,
                          numa ? d->d_numaalloc : nullptr, d->d_cpusets);

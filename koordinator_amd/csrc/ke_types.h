@@ -116,32 +116,49 @@ struct CpuRec {  // one logical CPU: ranks of the reference core / socket ids, t
   uint8_t core, numa, socket, ref, excl, flags, pad0, pad1;
 };
 static_assert(sizeof(CpuRec) == 8, "CpuRec layout");
-constexpr int CS_RF = 0, CS_RS = 1, CS_CNT = 2, CS_TOPO = 3, NUM_CS_FIELDS = 4;
+constexpr int CS_RF = 0, CS_RS = 1, CS_CNT = 2, CS_TOPO = 3;
+constexpr int CS_ZALL = 4, CS_ZFULL = 6, CS_ZSPREAD = 8;  // 2 words each: 16-bit counts per NUMA id 0..7
+constexpr int NUM_CS_FIELDS = 10;
 // CS_CNT: CPUs in fully available cores (bits 0-15), cores with an available CPU (16-31), CPUs per
-// core (32-39), MaxRefCount (40-47).  CS_TOPO: CPUTopology's NumCPUs / NumCores / NumNodes /
-// NumSockets (cpu_topology.go:45-105) in 16-bit lanes.
-KE_HD inline int64_t cs_pack(int full, int spread, int cpc, int max_ref) {
-  return (int64_t)full | ((int64_t)spread << 16) | ((int64_t)cpc << 32) | ((int64_t)max_ref << 40);
+// core (32-39), MaxRefCount (40-47), available CPUs (48-63).  CS_TOPO: CPUTopology's NumCPUs /
+// NumCores / NumNodes / NumSockets (cpu_topology.go:45-105) in 16-bit lanes.  CS_Z*: the same three
+// availabilities per NUMA id (the CPUs allocateCPUSet may take in a zone without / under a required
+// FullPCPUs / SpreadByPCPUs policy).
+KE_HD inline int64_t cs_pack(int full, int spread, int cpc, int max_ref, int all) {
+  return (int64_t)full | ((int64_t)spread << 16) | ((int64_t)cpc << 32) | ((int64_t)max_ref << 40) |
+         ((int64_t)all << 48);
 }
 KE_HD inline int cs_full(int64_t c) { return (int)(c & 0xffff); }
 KE_HD inline int cs_spread(int64_t c) { return (int)((c >> 16) & 0xffff); }
 KE_HD inline int cs_cpc(int64_t c) { return (int)((c >> 32) & 0xff); }
 KE_HD inline int cs_max_ref(int64_t c) { return (int)((c >> 40) & 0xff); }
+KE_HD inline int cs_all(int64_t c) { return (int)((c >> 48) & 0xffff); }
+KE_HD inline int cs_zone(int64_t lo, int64_t hi, int z) { return (int)(((z < 4 ? lo : hi) >> (16 * (z & 3))) & 0xffff); }
 // NodeAllocation.getAvailableCPUs (node_allocation.go:192-219): not reserved, RefCount < MaxRefCount
 KE_HD inline bool cpu_available(const CpuRec& r, int max_ref) {
   return (r.flags & CR_VALID) && !(r.flags & CR_RESERVED) && !(r.ref > 0 && r.ref >= max_ref);
 }
-// the counts above over one node's records
-KE_HD inline int64_t cs_counts(const CpuRec* recs, int cpc, int max_ref) {
-  uint8_t a_core[CPU_SLOTS] = {};
+// CS_CNT and the six CS_Z* words over one node's records; `core_n` is CPU_SLOTS bytes of scratch
+KE_HD inline void cs_fill(const CpuRec* recs, int cpc, int max_ref, uint8_t* core_n, int64_t* cnt, int64_t* z6) {
+  for (int k = 0; k < CPU_SLOTS; k++) core_n[k] = 0;
+  int all = 0;
   for (int c = 0; c < CPU_SLOTS; c++)
-    if (cpu_available(recs[c], max_ref)) a_core[recs[c].core]++;
+    if (cpu_available(recs[c], max_ref)) core_n[recs[c].core]++, all++;
   int full = 0, spread = 0;
   for (int k = 0; k < CPU_SLOTS; k++) {
-    if (a_core[k] == cpc && cpc > 0) full += cpc;
-    if (a_core[k] > 0) spread++;
+    if (core_n[k] == cpc && cpc > 0) full += cpc;
+    if (core_n[k] > 0) spread++;
   }
-  return cs_pack(full, spread, cpc, max_ref);
+  *cnt = cs_pack(full, spread, cpc, max_ref, all);
+  for (int w = 0; w < 6; w++) z6[w] = 0;
+  for (int c = 0; c < CPU_SLOTS; c++) {  // ascending ids: a core's first available CPU is its lowest
+    if (!cpu_available(recs[c], max_ref) || recs[c].numa >= 8) continue;
+    const int z = recs[c].numa, sh = 16 * (z & 3), hi = z >> 2;
+    uint8_t& n = core_n[recs[c].core];
+    z6[0 + hi] += (int64_t)1 << sh;                                  // available
+    if ((n & 0x7f) == cpc) z6[2 + hi] += (int64_t)1 << sh;          // in a fully available core
+    if (!(n & 0x80)) z6[4 + hi] += (int64_t)1 << sh, n |= 0x80;     // the core's lowest available CPU
+  }
 }
 
 // host-side packed row (staging for uploads, debug readback)

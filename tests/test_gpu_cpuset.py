@@ -134,3 +134,85 @@ def test_cpuset_edge_cases(gpu):
     for h in (ev, o):
         h.set_cpus(1, model.make_cpus([]))
     assert_eval_equal(ev.eval(pods, cases.NOW), o.eval(pods, cases.NOW))
+
+
+# ---- cpusets under NUMA topology policies (config 4) ----------------------------------------------
+NUMA_CPUSET = [c for c in cases.load("numa_cpuset.json") if c["op"] == "node_score"]
+
+
+@pytest.mark.parametrize("case", NUMA_CPUSET, ids=[c["name"] for c in NUMA_CPUSET])
+def test_golden_numa_node_score(gpu, case):
+    """TestNUMANodeScore through the product: Filter + Score under SingleNUMANode / Restricted, incl. an
+    LSR pod whose requested cpu is the node's cpuset count (scoring.go:179-185)."""
+    cfg = abi.default_config(len(case["nodes"]))
+    cfg.numa.strategy = abi.STRATEGY_MOST_ALLOCATED
+    ev = Evaluator(cfg)
+    pod = cases.setup_numa_score_case(ev, case)
+    r = ev.eval([pod], cases.NOW)
+    assert list(r["status"][0]) == [abi.CODE_SUCCESS] * len(case["nodes"]), case["source"]
+    assert [int(x) for x in r["numa"][0]] == case["want"]["scores"], case["source"]
+
+
+def numa_cpuset_both(n_nodes, seed, no_la=True, batch=64, numa_most=False, **kw):
+    cl = synth.make_cluster(n_nodes, synth.BASE_SEED + seed, amplified_fraction=0.3)
+    zs, tabs = synth.make_numa_cpus(cl, synth.BASE_SEED + seed + 1, **kw)
+    cfg = synth.config(n_nodes, pod_batch=batch)
+    if no_la:
+        cfg.loadaware.usage_thresholds[:] = [abi.ABSENT, abi.ABSENT]
+    if numa_most:
+        cfg.numa.numa_strategy = abi.STRATEGY_MOST_ALLOCATED
+    ev, o = Evaluator(cfg), Oracle(cfg, n_nodes)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        synth.load_numa(h, zs)
+        synth.load_cpus(h, tabs)
+    return ev, o
+
+
+NUMA_VARIANTS = {
+    "mixed": dict(),
+    "eight-zones-shared": dict(zone_counts=(8,), max_ref_choices=(2, 3)),
+    "forced-binding": dict(bind_weights=(0.2, 0.4, 0.4), policy_weights=(0, 1, 1, 1)),
+    "hint-most": dict(numa_most=True, zone_counts=(2, 4)),
+}
+
+
+@pytest.mark.parametrize("name", list(NUMA_VARIANTS))
+def test_numa_cpuset_eval_matrix_parity(gpu, name):
+    """Binding pods under every policy: trimmed availability, whole-CPU splits, per-zone CPU counts,
+    nil affinities, the cpuset NUMA-scope score — every (pod, node) equal to the oracle."""
+    ev, o = numa_cpuset_both(240, 401, **NUMA_VARIANTS[name])
+    pods = synth.make_numa_cpuset_pods(72, synth.BASE_SEED + 403)
+    a, b = ev.eval(pods, synth.T0), o.eval(pods, synth.T0)
+    assert_eval_equal(a, b)
+    assert np.any(a["status"] == abi.CODE_SUCCESS)
+
+
+@pytest.mark.parametrize("name", ["mixed", "eight-zones-shared", "forced-binding"])
+def test_numa_cpuset_schedule_parity(gpu, name):
+    """Sequential placements: per-zone accumulator takes, NUMA allocations and cpusets, the zones'
+    entries / statuses patched for later pods of the queue, then a second queue and an eval."""
+    ev, o = numa_cpuset_both(240, 411, **NUMA_VARIANTS[name])
+    pods = synth.make_numa_cpuset_pods(160, synth.BASE_SEED + 413)
+    c = assert_schedule_equal(ev, o, pods, synth.T0)
+    assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
+    assert (c >= 0).sum() > 80
+    more = synth.make_numa_cpuset_pods(40, synth.BASE_SEED + 414, key_base=7_000_000_000)
+    assert_eval_equal(ev.eval(more, synth.T0), o.eval(more, synth.T0))
+    assert_schedule_equal(ev, o, more, synth.T0)
+    assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
+
+
+def test_numa_cpuset_with_load_aware(gpu):
+    ev, o = numa_cpuset_both(240, 421, no_la=False)
+    pods = synth.make_numa_cpuset_pods(96, synth.BASE_SEED + 423)
+    assert_eval_equal(ev.eval(pods, synth.T0), o.eval(pods, synth.T0))
+    assert_schedule_equal(ev, o, pods, synth.T0)
+
+
+def test_numa_cpuset_sharded_loopback(gpu):
+    ev, o = numa_cpuset_both(1100, 431)
+    pods = synth.make_numa_cpuset_pods(96, synth.BASE_SEED + 433)
+    ev.shard_init(0, 3, None)
+    assert_schedule_equal(ev, o, pods, synth.T0)
+    assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)

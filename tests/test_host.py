@@ -109,17 +109,12 @@ def test_unsupported_inputs_are_rejected():
     with pytest.raises(KoordEvalError) as e:
         ev.upsert_node(1, n)
     assert e.value.code == abi.ERR_INVALID
-    # a NUMA-policy node is accepted; DeviceShare pods cannot meet it (DeviceShare NUMA hints), nor
-    # can pods that bind CPUs (the CPU accumulator's NUMA hints)
+    # a NUMA-policy node is accepted; DeviceShare pods cannot meet it (DeviceShare NUMA hints)
     n.numa_topology_policy = abi.NUMA_POLICY_RESTRICTED
     ev.upsert_node(1, n)
     gpu_pod = model.make_pod(requests={"cpu": "1", "koordinator.sh/gpu": "100"})
     with pytest.raises(KoordEvalError) as e:
         ev.eval([gpu_pod], cases.NOW)
-    assert e.value.code == abi.ERR_UNSUPPORTED
-    lsr = model.make_pod(requests={"cpu": "2"}, labels={"koordinator.sh/qosClass": "LSR"}, priority=9500)
-    with pytest.raises(KoordEvalError) as e:
-        ev.eval([lsr], cases.NOW)
     assert e.value.code == abi.ERR_UNSUPPORTED
     bad_spec = model.make_pod(requests={"cpu": "2"})
     bad_spec.has_resource_spec = 1
