@@ -744,8 +744,8 @@ __device__ __forceinline__ void numa_present_lack(const NumaNode& v, const DevPo
 // preferred merged hint returns STATUS_DEFERRED instead of running the full merge here (one lane
 // needing it would hold its whole wavefront; k_numa_fallback runs those pairs compacted).
 // FB_AFF: the BestEffort full-merge result was computed by the caller (k_numa_fallback) and is `fb_aff`.
-// CS: a binding pod (`cs`, `ps` = its amplified requests for the hint scores): never deferred; every
-// allocation check includes allocateCPUSet's take, a nil affinity the node-wide one.
+// CS: a binding pod (`cs`, `ps` = its amplified requests for the hint scores): every allocation check
+// includes allocateCPUSet's take, a nil affinity the node-wide one.
 template <bool DEFER, bool FB_AFF = false, bool CS = false>
 __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t nf, int policy, const NumaNode& v,
                                                const DevPod& p, const KArgs& k, uint32_t fb_aff = 0,
@@ -830,7 +830,7 @@ __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t
     o.reason = KE_REASON_NUMA_HINT_UNALIGNED;
     return o;
   }
-  if (DEFER && !CS) {
+  if (DEFER) {
     o.status = STATUS_DEFERRED;
     return o;
   }
@@ -1013,7 +1013,12 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
       ps.req[0] = amplify_bits(p.req[0], s.cs[CS_RS * s.stride + i]);
       NumaNode tv = nv;
       numa_trim(tv, cs);
-      const NumaPick pk = numa_admit<false, false, true>(s, i, nf, eff_pol, tv, p, k, 0u, &cs, &ps);
+      const NumaPick pk = numa_admit<DEFER, FB_AFF, true>(s, i, nf, eff_pol, tv, p, k, fb_aff, &cs, &ps);
+      if (DEFER && pk.status == STATUS_DEFERRED) {
+        o.status = STATUS_DEFERRED;
+        o.total = -1;
+        return o;
+      }
       if (pk.status != KE_CODE_SUCCESS) {
         o.status = pk.status;
         o.reason = pk.reason;
@@ -1229,7 +1234,7 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
   const int p1 = min(batch_pods, p0 + pods_per_block);
   for (int p = p0; p < p1; p++) {
     const DevPod& pod = pods[base + p];
-    const EvalOut o = eval_pair<DS, NUMA, NUMA && !CPU, false, CPU>(n, expired, pod, k, s, i, nv);
+    const EvalOut o = eval_pair<DS, NUMA, NUMA, false, CPU>(n, expired, pod, k, s, i, nv);
     scores[(int64_t)p * score_stride + i] = (uint16_t)(o.total + 1);
     if (NUMA) defer_push(o.status == STATUS_DEFERRED, ((uint64_t)p << 32) | (uint32_t)i, defer_list, defer_cnt);
     if (DS && (pod.flags & PF_DS)) dsraw[i] = o.total >= 0 ? (uint16_t)(o.ds + 1) : (uint16_t)0;
@@ -1247,7 +1252,9 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
 //   3. 64 rows of L_cpu at a time, each lane lists its row's size-c* merged hints in L_mem order into
 //      LDS; lane 0 folds them in permutation order.
 constexpr int FALLBACK_BLOCKS = 1024;
-template <bool PARITY>
+// CS: pods of the launch may bind CPUs — such a pair's lists come from the trimmed zones with the
+// cpuset-aware split, its hint scores from the amplified requests (eval_pair's binding branch).
+template <bool PARITY, bool CS = false>
 __global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __restrict__ pods,
                                                       const int32_t* __restrict__ batch_base, KArgs k,
                                                       const uint64_t* __restrict__ list, const uint32_t* __restrict__ cnt,
@@ -1268,6 +1275,20 @@ __global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __res
     const DevPod pod = pods[base + p];
     NumaNode nv;
     numa_load(s, i, nv);
+    NumaCs cs;
+    cs.rcb = false;
+    DevPod ps = pod;
+    if (CS) {
+      const uint32_t nf = s.flags[i];
+      const bool rcb = !(pod.flags & PF_NUMA_SKIP) &&
+                       ((pod.flags & PF_CPU_RCB) || (pod.req[0] != 0 && nf_cpu_bind(nf) != KE_NODE_CPU_BIND_NONE &&
+                                                     (pod.flags & PF_CPU_INT)));
+      if (rcb) {
+        cs = numa_cs_load(s, i, nf, pod);
+        ps.req[0] = amplify_bits(pod.req[0], s.cs[CS_RS * s.stride + i]);
+        numa_trim(nv, cs);
+      }
+    }
     bool present[2];
     uint32_t lack[2];
     numa_present_lack(nv, pod, present, lack);
@@ -1281,8 +1302,8 @@ __global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __res
       if (m && !(m & ~nv.zm)) {
         in[0] = present[0] && !(m & lack[0]);
         in[1] = present[1] && !(m & lack[1]);
-        if ((in[0] || in[1]) && !numa_distribute<false>(nv, m, pod, nullptr, dummy)) in[0] = in[1] = false;
-        if (in[0] || in[1]) s_score[m] = numa_hint_score(s, i, nv, m, pod, k);
+        if ((in[0] || in[1]) && !numa_distribute<false, CS>(nv, m, pod, nullptr, dummy, &cs)) in[0] = in[1] = false;
+        if (in[0] || in[1]) s_score[m] = numa_hint_score(s, i, nv, m, ps, k);
       }
 #pragma unroll
       for (int r = 0; r < 2; r++) {
@@ -1360,7 +1381,7 @@ __global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __res
       load_row(s, i, nr);
       prepare_row(nr);
       const bool expired = node_expired(nr, k);
-      const EvalOut o = eval_pair<false, true, false, true>(nr, expired, pod, k, s, i, nv, aff);
+      const EvalOut o = eval_pair<false, true, false, true, CS>(nr, expired, pod, k, s, i, nv, aff);
       if (PARITY) {
         const int64_t o_idx = (int64_t)p * n_nodes + i;
         status[o_idx] = o.status;
@@ -2666,7 +2687,8 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
       hipLaunchKernelGGL((cpu ? k_eval_parity<true, true> : k_eval_parity<true, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, (int)N, d->d_pods, (int)P,
                          ppb, k, d_status, d_reason, d_la, d_numa, d_ds, d_total, d_dsmax, d->d_defer, d->d_defer_cnt);
       HIP_OK(hipGetLastError());
-      hipLaunchKernelGGL(k_numa_fallback<true>, dim3(FALLBACK_BLOCKS), dim3(64), 0, d->stream, d->soa, d->d_pods,
+      hipLaunchKernelGGL((cpu ? k_numa_fallback<true, true> : k_numa_fallback<true, false>), dim3(FALLBACK_BLOCKS),
+                         dim3(64), 0, d->stream, d->soa, d->d_pods,
                          d->d_batch_base, k, d->d_defer, d->d_defer_cnt, d->d_scores, d->capacity, (int)N, d_status,
                          d_reason, d_la, d_numa, d_ds, d_total, d_dsmax);
     } else {
@@ -2798,8 +2820,9 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
         uint32_t* dcnt = numa ? d->d_defer_cnt + b : nullptr;
         hipLaunchKernelGGL(eval, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, lo, hi, d->d_pods, d->d_batch_base, bp,
                            ppb, k, d->d_scores, d->capacity, d->d_dsraw, d->d_defer, dcnt);
-        if (numa && !ds && !cpu)  // DeviceShare pods never meet a NUMA policy: nothing deferred in their batches
-          hipLaunchKernelGGL(k_numa_fallback<false>, dim3(FALLBACK_BLOCKS), dim3(64), 0, d->stream, d->soa, d->d_pods,
+        if (numa && !ds)  // DeviceShare pods never meet a NUMA policy: nothing deferred in their batches
+          hipLaunchKernelGGL((cpu ? k_numa_fallback<false, true> : k_numa_fallback<false, false>), dim3(FALLBACK_BLOCKS),
+                             dim3(64), 0, d->stream, d->soa, d->d_pods,
                              d->d_batch_base, k, d->d_defer, dcnt, d->d_scores, d->capacity, 0, nullptr, nullptr,
                              nullptr, nullptr, nullptr, nullptr, nullptr);
       }

@@ -448,6 +448,7 @@ def make_numa_cpus(cl, seed, zone_counts=(2, 4, 8), policy_weights=(0.1, 0.3, 0.
     cl.nodes["cpu_bind_policy"] = rng.choice(3, N, p=np.asarray(bind_weights) / np.sum(bind_weights))
     cl.nodes["numa_allocate_strategy"] = rng.choice(3, N)
     zones_out, tables = [], []
+    excl_codes = np.array([abi.CPU_EXCL_NONE, abi.CPU_EXCL_NONE, abi.CPU_EXCL_PCPU_LEVEL, abi.CPU_EXCL_NUMA_NODE_LEVEL])
     for i in range(N):
         cap = cl.nodes["raw_allocatable"][i, 0]
         ncpu = min(int((cap if cap != abi.ABSENT else cl.nodes["allocatable"][i, 0]) // 1000), abi.MAX_CPUS)
@@ -456,39 +457,38 @@ def make_numa_cpus(cl, seed, zone_counts=(2, 4, 8), policy_weights=(0.1, 0.3, 0.
         tpc = int(rng.choice([1, 2])) if cpz % 2 == 0 else 1
         sockets = 2 if nz % 2 == 0 and rng.random() < 0.7 else 1
         split = rng.random() < 0.5
-        rows = []
-        core = 0
-        for z in range(nz):
-            for _ in range(cpz // tpc):
-                for t in range(tpc):
-                    cpu = core + t * (ncpu // tpc) if split else core * tpc + t
-                    rows.append((cpu, 500 + 3 * core, z, z * sockets // nz))
-                core += 1
+        # CPU rows in (zone, core, thread) order: core k of the node, thread t
+        core = np.repeat(np.arange(ncpu // tpc), tpc)
+        thread = np.tile(np.arange(tpc), ncpu // tpc)
+        zone = core // (cpz // tpc)
+        t = np.zeros(ncpu, abi.CPU_DTYPE)
+        t["cpu_id"] = core + thread * (ncpu // tpc) if split else core * tpc + thread
+        t["core_id"] = 500 + 3 * core
+        t["numa_id"] = zone
+        t["socket_id"] = zone * sockets // nz
         max_ref = int(rng.choice(max_ref_choices))
         frac = float(rng.choice(cpuset_fraction))
-        allocated, per_zone = {}, [0] * nz
-        for cpu, _, z, _ in rows:
-            if rng.random() < frac:
-                allocated[cpu] = (int(rng.integers(1, max_ref + 1)), rng.choice([None, None, "PCPULevel", "NUMANodeLevel"]))
-                per_zone[z] += 1
+        busy = rng.random(ncpu) < frac
+        t["ref_count"] = np.where(busy, rng.integers(1, max_ref + 1, ncpu), 0)
+        t["exclusive"] = np.where(busy, excl_codes[rng.integers(0, 4, ncpu)], 0)
+        per_zone = np.bincount(zone[busy], minlength=nz)
         mem = int(cl.nodes["allocatable"][i, 1])
         amplified = cl.nodes["cpu_amplification_ratio"][i] > 1.0
         z_arr = np.zeros(nz, abi.NUMA_ZONE_DTYPE)
-        for z in range(nz):
-            z_arr[z]["id"] = z
-            z_arr[z]["has"][:] = 1
-            z_arr[z]["capacity"][0] = cpz * 1000
-            z_arr[z]["capacity"][1] = mem // nz // MI * MI
-            shared = int(rng.choice([0, 0, 1000, 2500, 4000])) if rng.random() < 0.6 else 0
-            mem_al = int(z_arr[z]["capacity"][1] * rng.choice([0.0, 0.2, 0.5, 0.8])) // MI * MI
-            if per_zone[z] or shared or mem_al or (amplified and rng.random() < 0.3):
-                z_arr[z]["has_allocated"] = abi.NUMA_ALLOC_ENTRY | abi.NUMA_ALLOC_CPU | abi.NUMA_ALLOC_MEMORY
-                z_arr[z]["allocated"][0] = per_zone[z] * 1000 + shared
-                z_arr[z]["allocated"][1] = mem_al
-            if per_zone[z]:
-                z_arr[z]["numa_status"] = abi.NUMA_STATUS_SINGLE if rng.random() < 0.7 else abi.NUMA_STATUS_SHARED
+        z_arr["id"] = np.arange(nz)
+        z_arr["has"][:] = 1
+        z_arr["capacity"][:, 0] = cpz * 1000
+        z_arr["capacity"][:, 1] = mem // nz // MI * MI
+        shared = np.where(rng.random(nz) < 0.6, rng.choice([0, 0, 1000, 2500, 4000], nz), 0)
+        mem_al = (z_arr["capacity"][:, 1] * rng.choice([0.0, 0.2, 0.5, 0.8], nz)).astype(np.int64) // MI * MI
+        entry = (per_zone > 0) | (shared > 0) | (mem_al > 0) | (amplified & (rng.random(nz) < 0.3))
+        z_arr["has_allocated"] = np.where(entry, abi.NUMA_ALLOC_ENTRY | abi.NUMA_ALLOC_CPU | abi.NUMA_ALLOC_MEMORY, 0)
+        z_arr["allocated"][:, 0] = np.where(entry, per_zone * 1000 + shared, 0)
+        z_arr["allocated"][:, 1] = np.where(entry, mem_al, 0)
+        z_arr["numa_status"] = np.where(per_zone > 0, np.where(rng.random(nz) < 0.7, abi.NUMA_STATUS_SINGLE,
+                                                                   abi.NUMA_STATUS_SHARED), 0)
         zones_out.append(z_arr)
-        tables.append((model.make_cpus(rows, allocated), max_ref))
+        tables.append((t, max_ref))
     return zones_out, tables
 
 
