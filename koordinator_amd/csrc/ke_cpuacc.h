@@ -146,37 +146,45 @@ __device__ inline bool cores_less(const AccLds& a, int ci, int cj) {
 }
 
 // Group the collected cores by NUMA node (by_socket = 0) or socket (1), full cores only if asked;
-// per group the cores sorted (sortCores) and their CPUs appended -> a.lst / a.goff / a.gkey.
+// per group the cores sorted (sortCores) and their CPUs appended -> a.lst / a.goff / a.gkey.  Groups
+// in ascending key order (the caller's sort is total), cores bucketed by a counting sort.
 __device__ inline void group_cores(AccLds& a, bool by_socket, bool filter_full) {
   const int cpc = acc_cpc(a.t);
-  // distinct group keys in ascending order (the final sort is a total order; start order is moot)
-  uint8_t* has = a.mark;
-  for (int k = 0; k < ACC_CPUS; k++) has[k] = 0;
+  int16_t* cnt = a.p_key;  // per group key: cores, then the bucket's next slot
+  for (int g = 0; g < ACC_CPUS; g++) cnt[g] = 0;
   for (int k = 0; k < ACC_CPUS; k++) {
     if (!a.core_n[k] || (filter_full && a.core_n[k] != cpc)) continue;
     const int c0 = a.core_cpu[k][0];
-    has[by_socket ? a.cpu[c0].socket : a.cpu[c0].numa] = 1;
+    cnt[by_socket ? a.cpu[c0].socket : a.cpu[c0].numa]++;
+  }
+  int16_t* start = a.p_sc;
+  int acc = 0;
+  for (int g = 0; g < ACC_CPUS; g++) {
+    start[g] = (int16_t)acc;
+    acc += cnt[g];
+    cnt[g] = start[g];
+  }
+  for (int k = 0; k < ACC_CPUS; k++) {  // ascending core rank within a bucket
+    if (!a.core_n[k] || (filter_full && a.core_n[k] != cpc)) continue;
+    const int c0 = a.core_cpu[k][0];
+    a.order[cnt[by_socket ? a.cpu[c0].socket : a.cpu[c0].numa]++] = (int16_t)k;
   }
   a.ng = 0;
   int pos = 0;
   for (int g = 0; g < ACC_CPUS; g++) {
-    if (!has[g]) continue;
-    int nc = 0;
-    for (int k = 0; k < ACC_CPUS; k++) {
-      if (!a.core_n[k] || (filter_full && a.core_n[k] != cpc)) continue;
-      const int c0 = a.core_cpu[k][0];
-      if ((by_socket ? a.cpu[c0].socket : a.cpu[c0].numa) == g) a.order[nc++] = (int16_t)k;
-    }
+    const int b = start[g], nc = cnt[g] - b;
+    if (nc == 0) continue;
+    int16_t* o = &a.order[b];
     for (int i = 1; i < nc; i++)
-      for (int j = i; j > 0 && cores_less(a, a.order[j], a.order[j - 1]); j--) {
-        const int16_t t = a.order[j];
-        a.order[j] = a.order[j - 1];
-        a.order[j - 1] = t;
+      for (int j = i; j > 0 && cores_less(a, o[j], o[j - 1]); j--) {
+        const int16_t t = o[j];
+        o[j] = o[j - 1];
+        o[j - 1] = t;
       }
     a.gkey[a.ng] = (int16_t)g;
     a.goff[a.ng] = (int16_t)pos;
     for (int i = 0; i < nc; i++) {
-      const int k = a.order[i];
+      const int k = o[i];
       for (int q = 0; q < a.core_n[k]; q++) a.tmp[q] = a.core_cpu[k][q];
       sort_i16(a.tmp, a.core_n[k]);
       for (int q = 0; q < a.core_n[k]; q++) a.lst[pos++] = a.tmp[q];
@@ -260,14 +268,28 @@ __device__ inline void free_cpus_in_group(AccLds& a, bool by_socket, bool filter
   };
   const int16_t *sock = a.sc_sock, *node = a.sc_node;
   free_scores(a, keep, a.sc_sock, a.sc_node);
+  // CPUs bucketed by group key (counting sort, ascending ids within a bucket)
+  int16_t* cnt = a.p_key;
+  int16_t* first = a.p_sc;
+  for (int g = 0; g < ACC_CPUS; g++) cnt[g] = 0;
+  for (int c = 0; c < ACC_CPUS; c++)
+    if (a.alloc[c] && keep(c)) cnt[by_socket ? a.cpu[c].socket : a.cpu[c].numa]++;
+  int acc = 0;
+  for (int g = 0; g < ACC_CPUS; g++) {
+    first[g] = (int16_t)acc;
+    acc += cnt[g];
+    cnt[g] = first[g];
+  }
+  for (int c = 0; c < ACC_CPUS; c++)
+    if (a.alloc[c] && keep(c)) a.tmp[cnt[by_socket ? a.cpu[c].socket : a.cpu[c].numa]++] = (int16_t)c;
   a.ng = 0;
   int pos = 0;
   for (int g = 0; g < ACC_CPUS; g++) {
+    const int b = first[g], m = cnt[g] - b;
+    if (m == 0) continue;
     const int start = pos;
-    for (int c = 0; c < ACC_CPUS; c++)
-      if (a.alloc[c] && keep(c) && (by_socket ? a.cpu[c].socket : a.cpu[c].numa) == g) a.lst[pos++] = (int16_t)c;
-    if (pos == start) continue;
-    int n = pos - start;  // ascending already; then by ref count, then one CPU per core
+    for (int q = 0; q < m; q++) a.lst[pos++] = a.tmp[b + q];
+    int n = m;  // ascending already; then by ref count, then one CPU per core
     if (a.max_ref > 1) sort_by_ref(a, &a.lst[start], n);
     if (filter_excl) n = extract_cpu(a, &a.lst[start], n);
     pos = start + n;

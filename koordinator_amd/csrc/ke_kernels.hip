@@ -138,6 +138,7 @@ struct EvalOut {
   int32_t total;  // -1 = filtered out; else Σ weight·score of LoadAware + NodeNUMAResource (DeviceShare
                   // enters after NormalizeScore, once the pod's max over feasible nodes is known)
   uint8_t status, reason;
+  uint8_t aff;           // NUMA policy: the affinity Admit stored for the node (0 = nil)
   int16_t la, numa, ds;  // ds: DeviceShare.Score before NormalizeScore
 };
 
@@ -902,6 +903,7 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
   EvalOut o;
   o.status = KE_CODE_SUCCESS;
   o.reason = KE_REASON_NONE;
+  o.aff = 0;
   o.la = o.numa = o.ds = 0;
   const uint32_t nf = n.flags;
   if (!(nf & NF_VALID)) {
@@ -1023,6 +1025,7 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
         o.status = pk.status;
         o.reason = pk.reason;
       } else {
+        o.aff = (uint8_t)pk.aff;
         npol_score = numa_policy_score<true>(s, i, tv, pk.aff, p, k, n, &cs, &ps);
       }
     } else {
@@ -1036,6 +1039,7 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
         o.status = pk.status;
         o.reason = pk.reason;
       } else {
+        o.aff = (uint8_t)pk.aff;
         npol_score = numa_policy_score(s, i, nv, pk.aff, p, k, n);
       }
     }
@@ -1220,8 +1224,9 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
                                                            const int32_t* __restrict__ batch_base, int batch_pods,
                                                            int pods_per_block, KArgs k, uint16_t* __restrict__ scores,
                                                            int64_t score_stride, uint16_t* __restrict__ dsraw,
-                                                           uint64_t* __restrict__ defer_list, uint32_t* defer_cnt) {
-  const int i = lo + blockIdx.x * EVAL_BLOCK + threadIdx.x;
+                                                           uint64_t* __restrict__ defer_list, uint32_t* defer_cnt,
+                                                           uint8_t* __restrict__ aff_out) {
+  const int i = lo + blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= hi) return;
   NodeRegs n;
   load_row(s, i, n);
@@ -1238,6 +1243,7 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
     scores[(int64_t)p * score_stride + i] = (uint16_t)(o.total + 1);
     if (NUMA) defer_push(o.status == STATUS_DEFERRED, ((uint64_t)p << 32) | (uint32_t)i, defer_list, defer_cnt);
     if (DS && (pod.flags & PF_DS)) dsraw[i] = o.total >= 0 ? (uint16_t)(o.ds + 1) : (uint16_t)0;
+    if (CPU && NUMA) aff_out[i] = o.aff;  // singleton batch: the affinity its Reserve allocates on
   }
 }
 
@@ -1260,7 +1266,8 @@ __global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __res
                                                       const uint64_t* __restrict__ list, const uint32_t* __restrict__ cnt,
                                                       uint16_t* __restrict__ scores, int64_t score_stride, int n_nodes,
                                                       uint8_t* status, uint8_t* reason, int16_t* la, int16_t* numa,
-                                                      int16_t* ds, int16_t* total, uint32_t* dsmax) {
+                                                      int16_t* ds, int16_t* total, uint32_t* dsmax,
+                                                      uint8_t* __restrict__ aff_out) {
   __shared__ int32_t s_score[256];     // hint score by mask value
   __shared__ uint8_t s_list[2][256];   // L_cpu / L_mem masks in order
   __shared__ uint16_t s_buf[64][256];  // per-row merged hints of size c*: M | k << 8 | unsatisfied << 10
@@ -1393,6 +1400,7 @@ __global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __res
         if (o.total >= 0) atomicMax(&dsmax[p], (uint32_t)o.ds + 1);
       } else {
         scores[(int64_t)p * score_stride + i] = (uint16_t)(o.total + 1);
+        if (CS && aff_out) aff_out[i] = o.aff;
       }
     }
     __syncthreads();
@@ -2019,7 +2027,7 @@ __device__ bool cpuset_take(AccLds& a, int zone, int needed, int bind) {
   return true;
 }
 
-// allocateCPUSet (resource_manager.go:353-459): the node's CPU table into LDS, getAvailableCPUs, the
+// allocateCPUSet (resource_manager.go:353-459) over the node's CPU table in LDS: getAvailableCPUs, the
 // required-policy filter (filterCPUsByRequiredCPUBindPolicy :655-695); with a NUMA allocation (zones
 // `zmask`, cpu milli `zcpu[id]`) one take per zone in id order of min(cpu/1000, its CPUs) CPUs, which
 // must add up to numCPUsNeeded; else one take over the node; then satisfiedRequiredCPUBindPolicy
@@ -2027,7 +2035,6 @@ __device__ bool cpuset_take(AccLds& a, int zone, int needed, int bind) {
 __device__ bool cpuset_allocate(const SoA& s, int64_t node, uint32_t nf, const DevPod& pod, AccLds& a, uint32_t zmask,
                                 const int64_t (&zcpu)[8]) {
   const int64_t st = s.stride;
-  const CpuRec* recs = s.cpu + node * CPU_SLOTS;
   const int64_t cnt = s.cs[CS_CNT * st + node], topo = s.cs[CS_TOPO * st + node];
   const int max_ref = cs_max_ref(cnt), cpc = cs_cpc(cnt);
   a.t.num_cpus = (int)(topo & 0xffff);
@@ -2045,9 +2052,8 @@ __device__ bool cpuset_allocate(const SoA& s, int64_t node, uint32_t nf, const D
   }
   uint8_t* navail_core = a.core_n;  // LDS scratch until the accumulator runs
   for (int k = 0; k < CPU_SLOTS; k++) navail_core[k] = 0, a.ex_core0[k] = 0, a.ex_node0[k] = 0, a.uni[k] = 0;
-  for (int c = 0; c < CPU_SLOTS; c++) {
-    const CpuRec r = recs[c];
-    a.cpu[c] = r;
+  for (int c = 0; c < CPU_SLOTS; c++) {  // a.cpu: the node's records (k_cpuset_reserve loaded them)
+    const CpuRec r = a.cpu[c];
     a.base[c] = cpu_available(r, max_ref) ? 1 : 0;
     a.aref[c] = r.ref;
     if (a.base[c]) navail_core[r.core]++;
@@ -2187,15 +2193,27 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
                                                        int32_t* __restrict__ chosen_score, int32_t global_offset,
                                                        uint64_t* __restrict__ stamps, uint64_t* __restrict__ pstamps,
                                                        int batch_index, uint64_t* __restrict__ dev_alloc,
-                                                       int64_t* __restrict__ numa_alloc, uint64_t* __restrict__ cpusets) {
+                                                       int64_t* __restrict__ numa_alloc, uint64_t* __restrict__ cpusets,
+                                                       const uint8_t* __restrict__ aff_in, int eval_lo, int eval_hi) {
   __shared__ AccLds a;
-  if (threadIdx.x != 0) return;
+  __shared__ uint32_t s_w;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const int base = *batch_base;
+  {  // selectHost's key (wave max over the candidates), then the node's CPU records into LDS (all lanes)
+    const int cnt = min(cand_cnt[0], KMAX);
+    const uint32_t mine = (int)threadIdx.x < cnt ? cand[threadIdx.x] : 0u;
+    const uint32_t wmax = wave_max_u32(mine);
+    if (threadIdx.x == 0) s_w = wmax;
+    __syncthreads();
+    if (s_w && s.cpu) {
+      const CpuRec* recs = s.cpu + (int64_t)key_node(s_w) * CPU_SLOTS;
+      for (int c = threadIdx.x; c < CPU_SLOTS; c += 64) a.cpu[c] = recs[c];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
   const DevPod pod = pods[base];
-  uint32_t w = 0;
-  const int cnt = min(cand_cnt[0], KMAX);
-  for (int c = 0; c < cnt; c++) w = max(w, cand[c]);
+  const uint32_t w = s_w;
   int32_t out_node = -1, out_score = -1;
   uint64_t alloc = 0, set[4] = {0, 0, 0, 0};
   int64_t* out16 = numa_alloc ? numa_alloc + (int64_t)base * 16 : nullptr;
@@ -2216,29 +2234,30 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
     uint32_t got[2] = {0, 0};
     int64_t dist[2][8] = {{0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0, 0}};
     if (ok && npol) {  // the affinity the Filter's Admit stored and the allocation on it
-      NumaPick pk;
+      // this rank evaluated the node: its eval stored the affinity (a feasible node admitted); else
+      // (a node of another shard) Admit runs here
+      const bool have = node >= eval_lo && node < eval_hi;
+      NumaPick pk{KE_CODE_SUCCESS, KE_REASON_NONE, have ? (uint32_t)aff_in[node] : 0u};
       if (rcb) {
         const NumaCs cs = numa_cs_load(s, node, nf, pod);
         DevPod ps = pod;
         ps.req[0] = amplify_bits(pod.req[0], s.cs[CS_RS * s.stride + node]);
         NumaNode tv = v;
         numa_trim(tv, cs);
-        pk = numa_admit<false, false, true>(s, node, nf, pol, tv, pod, k, 0u, &cs, &ps);
+        if (!have) pk = numa_admit<false, false, true>(s, node, nf, pol, tv, pod, k, 0u, &cs, &ps);
         if (pk.status == KE_CODE_SUCCESS && pk.aff) numa_distribute<true, true>(tv, pk.aff, pod, got, dist, &cs);
         ok = pk.status == KE_CODE_SUCCESS;
       } else {
-        pk = numa_admit<false>(s, node, nf, pol, v, pod, k);
+        if (!have) pk = numa_admit<false>(s, node, nf, pol, v, pod, k);
         if (pk.status == KE_CODE_SUCCESS && pk.aff) numa_distribute<true>(v, pk.aff, pod, got, dist);
       }
     }
     int cs_old[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // allocated CPUs per NUMA id before the pod
-    if (nsoa && v.zm) {
-      const CpuRec* recs = s.cpu + node * CPU_SLOTS;
+    if (nsoa && v.zm && s.cpu)
       for (int c = 0; c < CPU_SLOTS; c++) {
-        const CpuRec r = recs[c];
+        const CpuRec r = a.cpu[c];
         if ((r.flags & CR_VALID) && r.ref > 0 && r.numa < 8) cs_old[r.numa]++;
       }
-    }
     if (ok && rcb) {
       const int64_t zcpu[8] = {dist[0][0], dist[0][1], dist[0][2], dist[0][3],
                                dist[0][4], dist[0][5], dist[0][6], dist[0][7]};
@@ -2336,6 +2355,7 @@ struct DeviceState {
   int64_t cpu_staging_cap = 0;     // nodes
   uint64_t* d_cpusets = nullptr;   // [n_pods][4] cpuset of each pod (ke_schedule)
   int64_t cpusets_cap = 0;         // bytes
+  uint8_t* d_aff = nullptr;        // [capacity] NUMA affinity per node of a singleton batch's eval
 };
 
 // Contiguous node range of shard `rank`: 512-aligned chunks (k_select's 16-B loads stay aligned).
@@ -2380,6 +2400,7 @@ int device_create(Context* ctx) {
   HIP_OK(hipMalloc(&d->d_batch_base, sizeof(int32_t)));
   HIP_OK(hipMalloc(&d->d_dsraw, sizeof(uint16_t) * d->capacity));
   HIP_OK(hipMalloc(&d->d_dsmax, sizeof(uint32_t) * MAX_BATCH));
+  HIP_OK(hipMalloc(&d->d_aff, d->capacity));
   HIP_OK(hipStreamSynchronize(d->stream));
   return KE_OK;
 }
@@ -2395,7 +2416,7 @@ void device_destroy(Context* ctx) {
                   d->d_stamps,  d->d_parity, d->d_best,       d->d_gath,         d->soa.ds,   d->soa.dsm,
                   d->d_dsraw,   d->d_dsmax,  d->d_devalloc,   d->d_dsrows,       d->soa.nf,   d->soa.nm,
                   d->d_numaalloc, d->d_numarows, d->d_defer, d->d_defer_cnt, d->soa.cs, d->soa.cpu,
-                  d->d_cpurows, d->d_cpusets};
+                  d->d_cpurows, d->d_cpusets, d->d_aff};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (d->stream) (void)hipStreamDestroy(d->stream);
@@ -2690,7 +2711,7 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
       hipLaunchKernelGGL((cpu ? k_numa_fallback<true, true> : k_numa_fallback<true, false>), dim3(FALLBACK_BLOCKS),
                          dim3(64), 0, d->stream, d->soa, d->d_pods,
                          d->d_batch_base, k, d->d_defer, d->d_defer_cnt, d->d_scores, d->capacity, (int)N, d_status,
-                         d_reason, d_la, d_numa, d_ds, d_total, d_dsmax);
+                         d_reason, d_la, d_numa, d_ds, d_total, d_dsmax, nullptr);
     } else {
       hipLaunchKernelGGL((cpu ? k_eval_parity<false, true> : k_eval_parity<false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, (int)N, d->d_pods, (int)P,
                          ppb, k, d_status, d_reason, d_la, d_numa, d_ds, d_total, d_dsmax, nullptr, nullptr);
@@ -2812,19 +2833,21 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       int lo = 0, hi = N;
       if (sharded && !d->loopback) shard_range(N, d->rank, d->world, &lo, &hi);
       if (hi > lo) {
-        dim3 grid((unsigned)((hi - lo + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((bp + ppb - 1) / ppb));
+        // a singleton batch has one pod's worth of lanes: single-wave blocks spread it over every CU
+        const int eb = (bp == 1) ? 64 : EVAL_BLOCK;
+        dim3 grid((unsigned)((hi - lo + eb - 1) / eb), (unsigned)((bp + ppb - 1) / ppb));
         // a binding pod never meets a NUMA policy (ke_capi check_cpuset): its batch skips the NUMA path
         auto eval = cpu ? (ds ? k_eval_batch<true, false, true> : numa ? k_eval_batch<false, true, true> : k_eval_batch<false, false, true>)
                         : ds ? (numa ? k_eval_batch<true, true, false> : k_eval_batch<true, false, false>)
                              : (numa ? k_eval_batch<false, true, false> : k_eval_batch<false, false, false>);
         uint32_t* dcnt = numa ? d->d_defer_cnt + b : nullptr;
-        hipLaunchKernelGGL(eval, grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, lo, hi, d->d_pods, d->d_batch_base, bp,
-                           ppb, k, d->d_scores, d->capacity, d->d_dsraw, d->d_defer, dcnt);
+        hipLaunchKernelGGL(eval, grid, dim3(eb), 0, d->stream, d->soa, lo, hi, d->d_pods, d->d_batch_base, bp,
+                           ppb, k, d->d_scores, d->capacity, d->d_dsraw, d->d_defer, dcnt, d->d_aff);
         if (numa && !ds)  // DeviceShare pods never meet a NUMA policy: nothing deferred in their batches
           hipLaunchKernelGGL((cpu ? k_numa_fallback<false, true> : k_numa_fallback<false, false>), dim3(FALLBACK_BLOCKS),
                              dim3(64), 0, d->stream, d->soa, d->d_pods,
                              d->d_batch_base, k, d->d_defer, dcnt, d->d_scores, d->capacity, 0, nullptr, nullptr,
-                             nullptr, nullptr, nullptr, nullptr, nullptr);
+                             nullptr, nullptr, nullptr, nullptr, nullptr, cpu ? d->d_aff : nullptr);
       }
       if (ds) {  // DefaultNormalizeScore's max over the feasible nodes (all ranks)
         HIP_OK(hipMemsetAsync(d->d_dsmax, 0, sizeof(uint32_t), d->stream));
@@ -2867,12 +2890,15 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     }
     if (prof) HIP_OK(hipEventRecord(pe[2], d->stream));
     if (cpu) {
+      int elo = 0, ehi = N;  // nodes this rank's eval covered (their affinities are in d_aff)
+      if (sharded && !d->loopback) shard_range(N, d->rank, d->world, &elo, &ehi);
       hipLaunchKernelGGL((ds ? (numa ? k_cpuset_reserve<true, true> : k_cpuset_reserve<true, false>)
                              : (numa ? k_cpuset_reserve<false, true> : k_cpuset_reserve<false, false>)),
                          dim3(1), dim3(64), 0, d->stream, d->soa,
                          d->d_pods, d->d_batch_base, k, d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score,
                          ctx->cfg.global_node_offset, d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc,
-                         numa ? d->d_numaalloc : nullptr, d->d_cpusets);
+                         numa ? d->d_numaalloc : nullptr, d->d_cpusets,
+                         d->d_aff, elo, ehi);
     } else {
       auto resolve = ds ? (numa ? k_resolve<true, true> : k_resolve<true, false>)
                         : (numa ? k_resolve<false, true> : k_resolve<false, false>);
@@ -2975,14 +3001,14 @@ int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t 
   HIP_OK(hipMemsetAsync(d->d_batch_base, 0, sizeof(int32_t), d->stream));
   dim3 grid((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((n_pods + ppb - 1) / ppb));
   hipLaunchKernelGGL((k_eval_batch<false, false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base, n_pods,
-                     ppb, k, d->d_scores, d->capacity, d->d_dsraw, nullptr, nullptr);  // warm
+                     ppb, k, d->d_scores, d->capacity, d->d_dsraw, nullptr, nullptr, nullptr);  // warm
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   HIP_OK(hipEventRecord(e0, d->stream));
   for (int it = 0; it < iters; it++)
     hipLaunchKernelGGL((k_eval_batch<false, false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base,
-                       n_pods, ppb, k, d->d_scores, d->capacity, d->d_dsraw, nullptr, nullptr);
+                       n_pods, ppb, k, d->d_scores, d->capacity, d->d_dsraw, nullptr, nullptr, nullptr);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(e1, d->stream));
   HIP_OK(hipEventSynchronize(e1));

@@ -57,7 +57,7 @@ def main():
     ev.eval(pods[:0], synth.T0)  # rows, NUMA rows and CPU tables resident in HBM
     ev.set_profiling(8)
     sl = P // K
-    lat, ks_acc, samples, placed, cpusets = [], {"eval_ms": 0.0, "select_ms": 0.0, "resolve_ms": 0.0}, 0, 0, 0
+    lat, ks_acc, samples, placed, cpusets, deferred = [], {"eval_ms": 0.0, "select_ms": 0.0, "resolve_ms": 0.0}, 0, 0, 0, 0
     t0 = time.perf_counter()
     for s in range(K):
         chosen, _ = ev.schedule(pods[s * sl:(s + 1) * sl], synth.T0)
@@ -69,6 +69,7 @@ def main():
         for key in ks_acc:
             ks_acc[key] += ks[key] * ks["samples"]
         samples += ks["samples"]
+        deferred += ev.numa_deferred()
     dt = time.perf_counter() - t0
     ev.close()
     out = {"workload": f"{N} nodes x {a.zones} NUMA zones with CPU tables, {K * sl} pods "
@@ -77,7 +78,7 @@ def main():
            "ms_per_pod": dt / (K * sl) * 1e3, "batches": len(lat),
            "p99_batch_latency_ms": float(np.percentile(lat, 99)), "p50_batch_latency_ms": float(np.percentile(lat, 50)),
            "kernel_ms_per_batch": {k: v / max(samples, 1) for k, v in ks_acc.items()},
-           "placed": placed, "cpusets": cpusets}
+           "placed": placed, "cpusets": cpusets, "deferred_pairs": deferred}
     if not a.no_cpu_baseline:
         from oracle.binding import Oracle  # checker / baseline only
 
