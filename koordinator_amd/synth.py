@@ -434,7 +434,7 @@ def make_cpuset_pods(n_pods, seed, cpuset_fraction=0.5, key_base=4_000_000_000):
 
 
 def make_numa_cpus(cl, seed, zone_counts=(2, 4, 8), policy_weights=(0.1, 0.3, 0.3, 0.3), bind_weights=(0.8, 0.1, 0.1),
-                   cpuset_fraction=(0.0, 0.1, 0.3, 0.6), max_ref_choices=(1, 1, 2), status_mode="derived"):
+                   cpuset_fraction=(0.0, 0.1, 0.3, 0.6), max_ref_choices=(1, 1, 2), threads=None, sockets=None):
     """Config 4 (NUMA-aware cpuset binding, BASELINE.json configs[3]): per node a NUMA topology policy
     (None / BestEffort / Restricted / SingleNUMANode by `policy_weights`), NRT zones over `zone_counts`
     NUMA nodes with a CPU table consistent with them (1-2 sockets, 1-2 threads per core), cpusets of
@@ -454,8 +454,8 @@ def make_numa_cpus(cl, seed, zone_counts=(2, 4, 8), policy_weights=(0.1, 0.3, 0.
         ncpu = min(int((cap if cap != abi.ABSENT else cl.nodes["allocatable"][i, 0]) // 1000), abi.MAX_CPUS)
         nz = int(rng.choice([z for z in zone_counts if ncpu % z == 0] or [1]))
         cpz = ncpu // nz
-        tpc = int(rng.choice([1, 2])) if cpz % 2 == 0 else 1
-        sockets = 2 if nz % 2 == 0 and rng.random() < 0.7 else 1
+        tpc = threads if threads else (int(rng.choice([1, 2])) if cpz % 2 == 0 else 1)
+        n_sock = sockets if sockets else (2 if nz % 2 == 0 and rng.random() < 0.7 else 1)
         split = rng.random() < 0.5
         # CPU rows in (zone, core, thread) order: core k of the node, thread t
         core = np.repeat(np.arange(ncpu // tpc), tpc)
@@ -465,7 +465,7 @@ def make_numa_cpus(cl, seed, zone_counts=(2, 4, 8), policy_weights=(0.1, 0.3, 0.
         t["cpu_id"] = core + thread * (ncpu // tpc) if split else core * tpc + thread
         t["core_id"] = 500 + 3 * core
         t["numa_id"] = zone
-        t["socket_id"] = zone * sockets // nz
+        t["socket_id"] = zone * n_sock // nz
         max_ref = int(rng.choice(max_ref_choices))
         frac = float(rng.choice(cpuset_fraction))
         busy = rng.random(ncpu) < frac
@@ -490,6 +490,35 @@ def make_numa_cpus(cl, seed, zone_counts=(2, 4, 8), policy_weights=(0.1, 0.3, 0.
         zones_out.append(z_arr)
         tables.append((t, max_ref))
     return zones_out, tables
+
+
+def make_c4_cluster(n_nodes, seed):
+    """128-CPU hosts (2 sockets x 4 NUMA x 8 cores x 2 threads), NUMA policy labels
+    SingleNUMANode / Restricted / BestEffort 40/30/30, earlier cpusets on part of the CPUs."""
+    cl = make_cluster(n_nodes, seed)
+    cl.nodes["allocatable"][:, 0] = 128_000
+    zones, tables = make_numa_cpus(cl, seed + 1, zone_counts=(8,), policy_weights=(0.0, 0.3, 0.3, 0.4),
+                                   bind_weights=(1.0, 0.0, 0.0), threads=2, sockets=2)
+    return cl, zones, tables
+
+
+def make_c4_pods(n_pods, seed, key_base=8_000_000_000):
+    """SURVEY.md §8d C4 queue: LSR/LSE koord-prod pods, cpu in {2,4,8,16} cores, the FullPCPUs default
+    (no ResourceSpec annotation)."""
+    rng = np.random.default_rng(seed)
+    pods = make_pods(n_pods, seed + 1, key_base=key_base)
+    cpu = rng.choice([2, 4, 8, 16], n_pods) * 1000
+    pods["priority_class"] = abi.PRIORITY_PROD
+    pods["qos_class"] = rng.choice([abi.QOS_LSE, abi.QOS_LSR], n_pods)
+    pods["is_daemonset"] = 0
+    pods["requests"][:] = 0
+    pods["limits"][:] = 0
+    pods["requests"][:, abi.RES_CPU] = cpu
+    pods["limits"][:, abi.RES_CPU] = cpu
+    mem = rng.choice([4, 8, 16, 32], n_pods) * GI
+    pods["requests"][:, abi.RES_MEMORY] = mem
+    pods["limits"][:, abi.RES_MEMORY] = mem
+    return pods
 
 
 def make_numa_cpuset_pods(n_pods, seed, cpuset_fraction=0.6, policy_fraction=0.2, key_base=6_000_000_000):

@@ -35,12 +35,18 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--survey", action="store_true", help="SURVEY.md §8d C4 spec: 128-CPU 2x4x8x2 hosts, "
+                    "policies 40/30/30, LSR/LSE pods cpu {2,4,8,16} with the FullPCPUs default")
     a = ap.parse_args()
     N, P, K = a.nodes, a.pods, a.steps
-    cl = synth.make_cluster(N, synth.BASE_SEED + 6, amplified_fraction=0.3)
-    zones, tables = synth.make_numa_cpus(cl, synth.BASE_SEED + 66, zone_counts=(a.zones,))
-    pods = synth.make_numa_cpuset_pods(P, synth.BASE_SEED + 106, cpuset_fraction=a.cpuset,
-                                       policy_fraction=a.pod_policy)
+    if a.survey:
+        cl, zones, tables = synth.make_c4_cluster(N, synth.BASE_SEED + 4)
+        pods = synth.make_c4_pods(P, synth.BASE_SEED + 104)
+    else:
+        cl = synth.make_cluster(N, synth.BASE_SEED + 6, amplified_fraction=0.3)
+        zones, tables = synth.make_numa_cpus(cl, synth.BASE_SEED + 66, zone_counts=(a.zones,))
+        pods = synth.make_numa_cpuset_pods(P, synth.BASE_SEED + 106, cpuset_fraction=a.cpuset,
+                                           policy_fraction=a.pod_policy)
     cfg = synth.config(N)
 
     def load(h):
@@ -50,8 +56,7 @@ def main():
         return h
 
     ew = load(Evaluator(cfg))  # warm-up context: kernels loaded, code paths exercised
-    ew.schedule(synth.make_numa_cpuset_pods(128, synth.BASE_SEED + 206, cpuset_fraction=a.cpuset,
-                                            policy_fraction=a.pod_policy), synth.T0)
+    ew.schedule(pods[:64], synth.T0)
     ew.close()
     ev = load(Evaluator(cfg))
     ev.eval(pods[:0], synth.T0)  # rows, NUMA rows and CPU tables resident in HBM
@@ -72,8 +77,10 @@ def main():
         deferred += ev.numa_deferred()
     dt = time.perf_counter() - t0
     ev.close()
-    out = {"workload": f"{N} nodes x {a.zones} NUMA zones with CPU tables, {K * sl} pods "
-                       f"({a.cpuset:.0%} LSR/LSE binding, {a.pod_policy:.0%} with a pod NUMA policy)",
+    wl = (f"C4 (SURVEY.md §8d): {N} nodes x 128 CPUs (2 sockets x 4 NUMA x 8 cores x 2 threads), {K * sl} LSR/LSE pods"
+          if a.survey else f"{N} nodes x {a.zones} NUMA zones with CPU tables, {K * sl} pods "
+                           f"({a.cpuset:.0%} LSR/LSE binding, {a.pod_policy:.0%} with a pod NUMA policy)")
+    out = {"workload": wl,
            "value": K * sl * N / dt, "unit": "pod-node evals/s", "pods_per_s": K * sl / dt,
            "ms_per_pod": dt / (K * sl) * 1e3, "batches": len(lat),
            "p99_batch_latency_ms": float(np.percentile(lat, 99)), "p50_batch_latency_ms": float(np.percentile(lat, 50)),
