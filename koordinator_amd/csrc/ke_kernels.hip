@@ -868,28 +868,72 @@ __device__ __forceinline__ int32_t numa_policy_score(const SoA& s, int64_t i, co
   return numa_scope_score((k.flags & AF_NUMA_MOST) != 0, req, alloc, CS ? *ps : p, k);
 }
 
+// NodeNUMAResource Reserve of a pod in a CPU batch on a NUMA-policy node: the allocation (`dist`) joins
+// the zones' entries (quotav1.Add keys, numa_reserve); under a cpu ratio > 1 an entry's cpu is the
+// allocated cpu - cpusets + Amplify(cpusets) of its zone (node_allocation.go:221-243), re-adjusted for
+// the zones whose cpuset count changed (`cs_old` -> `cs_new`, CPUs per NUMA id); the cpuset's NUMA ids
+// become single / shared (node_allocation.go:111-156 and GetAllNUMANodeStatus).
+__device__ void numa_reserve_cs(const SoA& s, int64_t i, uint32_t nf, const NumaNode& v, const uint32_t (&got)[2],
+                                const int64_t (&dist)[2][8], const int (&cs_old)[8], const int (&cs_new)[8],
+                                uint32_t used, int n_used, int64_t* out16) {
+  // the cpuset counts come from CPU tables; without the CPU SoA they are zero (a zone without an
+  // allocation entry holds no cpusets, ke_node_numa_set) and the ratio is never read
+  const int64_t ratio = s.cs ? s.cs[CS_RS * s.stride + i] : 0;
+  for (int z = 0; z < 8; z++) {
+    for (int r = 0; r < 2; r++) {
+      if (out16) out16[2 * z + r] = dist[r][z];
+      int64_t* f = s.nf + (NUMA_AL + 2 * z + r) * s.stride + i;
+      const bool entry_before = (v.ak[0] >> z) & 1u, entry_after = entry_before || (((got[0] | got[1]) >> z) & 1u);
+      if (r == 0 && (nf & NF_NUMA_AL_AMP)) {
+        if (!entry_after) continue;
+        const int64_t o = (int64_t)cs_old[z] * 1000, n = (int64_t)cs_new[z] * 1000;
+        const int64_t raw = entry_before ? *f + o - amplify_bits(o, ratio) : 0;
+        *f = raw + dist[0][z] - n + amplify_bits(n, ratio);
+      } else if ((got[r] >> z) & 1u) {
+        *f = (((v.ak[r] >> z) & 1u) ? *f : 0) + dist[r][z];
+      }
+    }
+  }
+  uint32_t ak0 = v.ak[0] | got[0];
+  if (nf & NF_NUMA_AL_AMP) ak0 |= got[1];
+  const uint32_t ak1 = v.ak[1] | got[1];
+  uint32_t single = v.single, shared = v.shared;
+  const uint32_t tracked = v.zm & ((1u << __popc(v.zm)) - 1u);  // ids < len(numaNodes) with a zone
+  for (int z = 0; z < 8; z++) {
+    if (!((used >> z) & 1u) || !((tracked >> z) & 1u)) continue;
+    if (n_used > 1 || ((shared >> z) & 1u)) shared |= 1u << z, single &= ~(1u << z);
+    else single |= 1u << z;
+  }
+  uint64_t m = s.nm[i];
+  m |= ((uint64_t)ak0 << NUMA_M_AL) | ((uint64_t)ak1 << (NUMA_M_AL + 8));
+  m &= ~((uint64_t)0xFFFF << NUMA_M_ST);
+  m |= ((uint64_t)single << NUMA_M_ST) | ((uint64_t)shared << (NUMA_M_ST + 8));
+  s.nm[i] = m;
+}
+
+// allocated CPUs per NUMA id of node i from its CPU table (zeros without the CPU SoA)
+__device__ __forceinline__ void zone_cpusets(const SoA& s, int64_t i, int (&cs)[8]) {
+#pragma unroll
+  for (int z = 0; z < 8; z++) cs[z] = 0;
+  if (!s.cpu) return;
+  const CpuRec* recs = s.cpu + i * CPU_SLOTS;
+  for (int c = 0; c < CPU_SLOTS; c++) {
+    const CpuRec r = recs[c];
+    if ((r.flags & CR_VALID) && r.ref > 0 && r.numa < 8) cs[r.numa]++;
+  }
+}
+
 // NodeNUMAResource Reserve of a non-cpuset pod under a NUMA policy: NodeAllocation.addPodAllocation
-// (node_allocation.go:111-156) adds the allocation on the affinity to the zones (quotav1.Add: the
-// entry gains the keys allocated; with a ratio > 1 every entry carries cpu).  out16[2*id + r].
+// (node_allocation.go:111-156) adds the allocation on the affinity to the zones (numa_reserve_cs with
+// unchanged cpusets; a new entry under a cpu ratio > 1 carries its zone's cpuset adjustment).
 __device__ __forceinline__ void numa_reserve(const SoA& s, int64_t i, uint32_t nf, const NumaNode& v, uint32_t aff,
                                              const DevPod& p, int64_t* out16) {
   int64_t out[2][8] = {{0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0, 0}};
   uint32_t got[2] = {0, 0};
   if (aff) numa_distribute<true>(v, aff, p, got, out);
-#pragma unroll
-  for (int z = 0; z < 8; z++)
-#pragma unroll
-    for (int r = 0; r < 2; r++) {
-      out16[2 * z + r] = out[r][z];
-      if ((got[r] >> z) & 1u) {
-        int64_t* f = s.nf + (NUMA_AL + 2 * z + r) * s.stride + i;
-        *f = (((v.ak[r] >> z) & 1u) ? *f : 0) + out[r][z];
-      }
-    }
-  uint32_t ak0 = v.ak[0] | got[0];
-  if (nf & NF_NUMA_AL_AMP) ak0 |= got[1];
-  const uint32_t ak1 = v.ak[1] | got[1];
-  s.nm[i] = s.nm[i] | ((uint64_t)ak0 << NUMA_M_AL) | ((uint64_t)ak1 << (NUMA_M_AL + 8));
+  int cs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if ((nf & NF_NUMA_AL_AMP) && ((got[0] | got[1]) & ~v.ak[0])) zone_cpusets(s, i, cs);  // a new entry
+  numa_reserve_cs(s, i, nf, v, got, out, cs, cs, 0u, 0, out16);
 }
 
 // `s`/`i` locate the node's DeviceShare state (read only for pods with PF_DS, and only when DS: the
@@ -1225,7 +1269,7 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
                                                            int pods_per_block, KArgs k, uint16_t* __restrict__ scores,
                                                            int64_t score_stride, uint16_t* __restrict__ dsraw,
                                                            uint64_t* __restrict__ defer_list, uint32_t* defer_cnt,
-                                                           uint8_t* __restrict__ aff_out) {
+                                                           uint8_t* __restrict__ aff_out, uint32_t* __restrict__ dsmax1) {
   const int i = lo + blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= hi) return;
   NodeRegs n;
@@ -1242,9 +1286,32 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
     const EvalOut o = eval_pair<DS, NUMA, NUMA, false, CPU>(n, expired, pod, k, s, i, nv);
     scores[(int64_t)p * score_stride + i] = (uint16_t)(o.total + 1);
     if (NUMA) defer_push(o.status == STATUS_DEFERRED, ((uint64_t)p << 32) | (uint32_t)i, defer_list, defer_cnt);
-    if (DS && (pod.flags & PF_DS)) dsraw[i] = o.total >= 0 ? (uint16_t)(o.ds + 1) : (uint16_t)0;
+    if (DS && (pod.flags & PF_DS)) {  // DefaultNormalizeScore's max: 1 + max raw score over feasible nodes
+      const uint32_t r = o.total >= 0 ? (uint32_t)(o.ds + 1) : 0u;
+      dsraw[i] = (uint16_t)r;
+      const uint32_t m = __ockl_wfred_max_u32(r);
+      if ((threadIdx.x & 63) == 0 && m) atomicMax(dsmax1, m);
+    }
     if (CPU && NUMA) aff_out[i] = o.aff;  // singleton batch: the affinity its Reserve allocates on
   }
+}
+
+// selectHost for a singleton batch: the best packed key over nodes [lo, hi) (ties to the lowest node
+// index), one atomicMax per wave; cand[0] must be zero on entry, cand_cnt[0] becomes 1.
+template <bool DS>
+__global__ __launch_bounds__(256) void k_argmax1(const uint16_t* __restrict__ scores, int lo, int hi,
+                                                 const uint16_t* __restrict__ dsraw, const uint32_t* __restrict__ dsmax1,
+                                                 int32_t wds, uint32_t* __restrict__ cand, int32_t* __restrict__ cand_cnt) {
+  const int i = lo + blockIdx.x * 256 + threadIdx.x;
+  uint32_t key = 0;
+  if (i < hi) {
+    uint32_t v = scores[i];  // total + 1, 0 = filtered out
+    if (DS && v) v += (uint32_t)(wds * ds_norm((int32_t)dsraw[i] - 1, *dsmax1));
+    key = v ? (v << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)i) : 0u;
+  }
+  key = __ockl_wfred_max_u32(key);
+  if ((threadIdx.x & 63) == 0 && key) atomicMax(cand, key);
+  if (blockIdx.x == 0 && threadIdx.x == 0) cand_cnt[0] = 1;
 }
 
 // The deferred BestEffort pairs of an eval launch: one wavefront per pair computes mergeFilteredHints
@@ -1458,15 +1525,6 @@ __device__ __forceinline__ void load8(const uint16_t* sc, int i, int end, uint32
 #pragma unroll
     for (int t = 0; t < 8; t++) v[t] = v[t] ? v[t] + (uint32_t)dn.lut[r[t] - 1] : 0u;
   }
-}
-
-// 1 + max raw DeviceShare score over the feasible nodes [lo, hi) of the batch's (single) pod
-__global__ __launch_bounds__(EVAL_BLOCK) void k_dsmax(const uint16_t* __restrict__ dsraw, int lo, int hi,
-                                                      uint32_t* __restrict__ dsmax1) {
-  const int i = lo + blockIdx.x * EVAL_BLOCK + threadIdx.x;
-  uint32_t m = i < hi ? dsraw[i] : 0u;
-  m = __ockl_wfred_max_u32(m);
-  if ((threadIdx.x & 63) == 0 && m) atomicMax(dsmax1, m);
 }
 
 constexpr int SEL_WINDOW = 64;  // histogram window below the pod's best score
@@ -2141,47 +2199,6 @@ __device__ void cpuset_commit(const SoA& s, int64_t node, const DevPod& pod, Acc
   for (int w = 0; w < 6; w++) s.cs[(CS_ZALL + w) * st + node] = a.z6[w];
 }
 
-// NodeNUMAResource Reserve of a pod in a CPU batch on a NUMA-policy node: the allocation (`dist`) joins
-// the zones' entries (quotav1.Add keys, numa_reserve); under a cpu ratio > 1 an entry's cpu is the
-// allocated cpu - cpusets + Amplify(cpusets) of its zone (node_allocation.go:221-243), re-adjusted for
-// the zones whose cpuset count changed (`cs_old` -> `cs_new`, CPUs per NUMA id); the cpuset's NUMA ids
-// become single / shared (node_allocation.go:111-156 and GetAllNUMANodeStatus).
-__device__ void numa_reserve_cs(const SoA& s, int64_t i, uint32_t nf, const NumaNode& v, const uint32_t (&got)[2],
-                                const int64_t (&dist)[2][8], const int (&cs_old)[8], const int (&cs_new)[8],
-                                uint32_t used, int n_used, int64_t* out16) {
-  const int64_t ratio = s.cs[CS_RS * s.stride + i];
-  for (int z = 0; z < 8; z++) {
-    for (int r = 0; r < 2; r++) {
-      if (out16) out16[2 * z + r] = dist[r][z];
-      int64_t* f = s.nf + (NUMA_AL + 2 * z + r) * s.stride + i;
-      const bool entry_before = (v.ak[0] >> z) & 1u, entry_after = entry_before || (((got[0] | got[1]) >> z) & 1u);
-      if (r == 0 && (nf & NF_NUMA_AL_AMP)) {
-        if (!entry_after) continue;
-        const int64_t o = (int64_t)cs_old[z] * 1000, n = (int64_t)cs_new[z] * 1000;
-        const int64_t raw = entry_before ? *f + o - amplify_bits(o, ratio) : 0;
-        *f = raw + dist[0][z] - n + amplify_bits(n, ratio);
-      } else if ((got[r] >> z) & 1u) {
-        *f = (((v.ak[r] >> z) & 1u) ? *f : 0) + dist[r][z];
-      }
-    }
-  }
-  uint32_t ak0 = v.ak[0] | got[0];
-  if (nf & NF_NUMA_AL_AMP) ak0 |= got[1];
-  const uint32_t ak1 = v.ak[1] | got[1];
-  uint32_t single = v.single, shared = v.shared;
-  const uint32_t tracked = v.zm & ((1u << __popc(v.zm)) - 1u);  // ids < len(numaNodes) with a zone
-  for (int z = 0; z < 8; z++) {
-    if (!((used >> z) & 1u) || !((tracked >> z) & 1u)) continue;
-    if (n_used > 1 || ((shared >> z) & 1u)) shared |= 1u << z, single &= ~(1u << z);
-    else single |= 1u << z;
-  }
-  uint64_t m = s.nm[i];
-  m |= ((uint64_t)ak0 << NUMA_M_AL) | ((uint64_t)ak1 << (NUMA_M_AL + 8));
-  m &= ~((uint64_t)0xFFFF << NUMA_M_ST);
-  m |= ((uint64_t)single << NUMA_M_ST) | ((uint64_t)shared << (NUMA_M_ST + 8));
-  s.nm[i] = m;
-}
-
 // A singleton batch of a pod that may bind CPUs, after k_select: selectHost's node, then Reserve in
 // profile order — LoadAware, NodeNUMAResource (the NUMA allocation on the affinity Admit picks and the
 // cpuset; a failed Allocate fails Reserve and the pod stays unplaced), DeviceShare.  One thread: the
@@ -2832,31 +2849,27 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       // this rank's node range (unsharded and loopback: every node)
       int lo = 0, hi = N;
       if (sharded && !d->loopback) shard_range(N, d->rank, d->world, &lo, &hi);
+      const bool single = bp == 1;
+      if (ds) HIP_OK(hipMemsetAsync(d->d_dsmax, 0, sizeof(uint32_t), d->stream));  // the eval's atomicMax target
       if (hi > lo) {
         // a singleton batch has one pod's worth of lanes: single-wave blocks spread it over every CU
-        const int eb = (bp == 1) ? 64 : EVAL_BLOCK;
+        const int eb = single ? 64 : EVAL_BLOCK;
         dim3 grid((unsigned)((hi - lo + eb - 1) / eb), (unsigned)((bp + ppb - 1) / ppb));
-        // a binding pod never meets a NUMA policy (ke_capi check_cpuset): its batch skips the NUMA path
+        // a DeviceShare pod never meets a NUMA policy (ke_capi check_numa_deviceshare): no NUMA path there
         auto eval = cpu ? (ds ? k_eval_batch<true, false, true> : numa ? k_eval_batch<false, true, true> : k_eval_batch<false, false, true>)
                         : ds ? (numa ? k_eval_batch<true, true, false> : k_eval_batch<true, false, false>)
                              : (numa ? k_eval_batch<false, true, false> : k_eval_batch<false, false, false>);
         uint32_t* dcnt = numa ? d->d_defer_cnt + b : nullptr;
         hipLaunchKernelGGL(eval, grid, dim3(eb), 0, d->stream, d->soa, lo, hi, d->d_pods, d->d_batch_base, bp,
-                           ppb, k, d->d_scores, d->capacity, d->d_dsraw, d->d_defer, dcnt, d->d_aff);
+                           ppb, k, d->d_scores, d->capacity, d->d_dsraw, d->d_defer, dcnt, d->d_aff, d->d_dsmax);
         if (numa && !ds)  // DeviceShare pods never meet a NUMA policy: nothing deferred in their batches
           hipLaunchKernelGGL((cpu ? k_numa_fallback<false, true> : k_numa_fallback<false, false>), dim3(FALLBACK_BLOCKS),
                              dim3(64), 0, d->stream, d->soa, d->d_pods,
                              d->d_batch_base, k, d->d_defer, dcnt, d->d_scores, d->capacity, 0, nullptr, nullptr,
                              nullptr, nullptr, nullptr, nullptr, nullptr, cpu ? d->d_aff : nullptr);
       }
-      if (ds) {  // DefaultNormalizeScore's max over the feasible nodes (all ranks)
-        HIP_OK(hipMemsetAsync(d->d_dsmax, 0, sizeof(uint32_t), d->stream));
-        if (hi > lo)
-          hipLaunchKernelGGL(k_dsmax, dim3((unsigned)((hi - lo + EVAL_BLOCK - 1) / EVAL_BLOCK)), dim3(EVAL_BLOCK), 0,
-                             d->stream, d->d_dsraw, lo, hi, d->d_dsmax);
-        if (sharded && !d->loopback)
-          RCCL_OK(ncclAllReduce(d->d_dsmax, d->d_dsmax, 1, ncclUint32, ncclMax, d->comm, d->stream));
-      }
+      if (ds && sharded && !d->loopback)  // DefaultNormalizeScore's max over the feasible nodes of all ranks
+        RCCL_OK(ncclAllReduce(d->d_dsmax, d->d_dsmax, 1, ncclUint32, ncclMax, d->comm, d->stream));
       if (prof) HIP_OK(hipEventRecord(pe[1], d->stream));
       auto select = [&](int slo, int shi, uint32_t* cand, int32_t* cnt) {
         if (ds)
@@ -2866,7 +2879,11 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
           hipLaunchKernelGGL(k_select<false>, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, d->stream, d->d_scores,
                              d->capacity, slo, shi, cand, cnt, d->d_dsraw, d->d_dsmax, k.wp_ds);
       };
-      if (!sharded) {
+      if (!sharded && single) {  // selectHost of one pod: a grid-wide argmax
+        HIP_OK(hipMemsetAsync(d->d_cand, 0, sizeof(uint32_t), d->stream));
+        hipLaunchKernelGGL((ds ? k_argmax1<true> : k_argmax1<false>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
+                           d->stream, d->d_scores, 0, N, d->d_dsraw, d->d_dsmax, k.wp_ds, d->d_cand, d->d_cand_cnt);
+      } else if (!sharded) {
         select(0, N, d->d_cand, d->d_cand_cnt);
       } else {
         // node-sharded: per-shard top-k_j, all-gather, merge
@@ -2889,9 +2906,12 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       HIP_OK(hipMemsetAsync(d->d_cand_cnt, 0, sizeof(int32_t) * MAX_BATCH, d->stream));
     }
     if (prof) HIP_OK(hipEventRecord(pe[2], d->stream));
-    if (cpu) {
-      int elo = 0, ehi = N;  // nodes this rank's eval covered (their affinities are in d_aff)
-      if (sharded && !d->loopback) shard_range(N, d->rank, d->world, &elo, &ehi);
+    if (bp == 1) {  // one pod: the single-node Reserve (cpuset accumulator when it binds)
+      int elo = 0, ehi = 0;  // nodes whose affinities this batch's eval stored in d_aff (binding batches)
+      if (cpu && numa) {
+        ehi = N;
+        if (sharded && !d->loopback) shard_range(N, d->rank, d->world, &elo, &ehi);
+      }
       hipLaunchKernelGGL((ds ? (numa ? k_cpuset_reserve<true, true> : k_cpuset_reserve<true, false>)
                              : (numa ? k_cpuset_reserve<false, true> : k_cpuset_reserve<false, false>)),
                          dim3(1), dim3(64), 0, d->stream, d->soa,
@@ -3001,14 +3021,14 @@ int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t 
   HIP_OK(hipMemsetAsync(d->d_batch_base, 0, sizeof(int32_t), d->stream));
   dim3 grid((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((n_pods + ppb - 1) / ppb));
   hipLaunchKernelGGL((k_eval_batch<false, false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base, n_pods,
-                     ppb, k, d->d_scores, d->capacity, d->d_dsraw, nullptr, nullptr, nullptr);  // warm
+                     ppb, k, d->d_scores, d->capacity, d->d_dsraw, nullptr, nullptr, nullptr, nullptr);  // warm
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   HIP_OK(hipEventRecord(e0, d->stream));
   for (int it = 0; it < iters; it++)
     hipLaunchKernelGGL((k_eval_batch<false, false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base,
-                       n_pods, ppb, k, d->d_scores, d->capacity, d->d_dsraw, nullptr, nullptr, nullptr);
+                       n_pods, ppb, k, d->d_scores, d->capacity, d->d_dsraw, nullptr, nullptr, nullptr, nullptr);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(e1, d->stream));
   HIP_OK(hipEventSynchronize(e1));

@@ -203,6 +203,18 @@ def test_numa_cpuset_schedule_parity(gpu, name):
     assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
 
 
+def test_numa_cpuset_pod_policies_on_policy_none_nodes(gpu):
+    """Nodes without a policy: binding pods take CPUs node-wide (zones without an allocation entry
+    gain cpusets), later pods with their own policy create entries there — under a cpu ratio > 1 an
+    entry's cpu carries its zone's cpuset adjustment (node_allocation.go:221-243)."""
+    ev, o = numa_cpuset_both(240, 441, policy_weights=(1, 0, 0, 0), cpuset_fraction=(0.0, 0.1))
+    pods = synth.make_numa_cpuset_pods(200, synth.BASE_SEED + 443, policy_fraction=0.5)
+    assert_schedule_equal(ev, o, pods, synth.T0)
+    assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
+    more = synth.make_numa_cpuset_pods(40, synth.BASE_SEED + 444, policy_fraction=0.5, key_base=7_500_000_000)
+    assert_eval_equal(ev.eval(more, synth.T0), o.eval(more, synth.T0))
+
+
 def test_numa_cpuset_with_load_aware(gpu):
     ev, o = numa_cpuset_both(240, 421, no_la=False)
     pods = synth.make_numa_cpuset_pods(96, synth.BASE_SEED + 423)
