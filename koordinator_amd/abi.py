@@ -283,7 +283,7 @@ def default_config(node_capacity, pod_batch=64, device_ordinal=0, global_node_of
 
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkoordeval.so")
+LIB_PATH = os.environ.get("KOORDEVAL_LIB") or os.path.join(_HERE, "libkoordeval.so")  # override: A/B builds
 
 EXPORTS = {
     # name: (restype, argtypes)

@@ -69,7 +69,7 @@ __device__ __forceinline__ int64_t amplify_bits(int64_t q, int64_t ratio_bits) {
 struct NodeRegs {
   int64_t ut, fh[2][2], sa[2][2], cap[2], nalloc[2], nreq[2], csm, csaf, csas;
   uint32_t flags;
-  float rcap[2], ralloc[2];  // approximate reciprocals: estimates for the exact score divisions
+  double dcap[2], rcap[2], dalloc[2], ralloc[2];  // cap/alloc as double and approximate reciprocals
 };
 
 __device__ __forceinline__ void load_row(const SoA& s, int64_t i, NodeRegs& r) {
@@ -95,36 +95,40 @@ __device__ __forceinline__ void load_row(const SoA& s, int64_t i, NodeRegs& r) {
   r.flags = s.flags[i];
 }
 
-__device__ __forceinline__ float i64_to_f32(int64_t x) {  // ~2 roundings, only feeds an estimate
-  return (float)(int32_t)(x >> 32) * 4294967296.0f + (float)(uint32_t)x;
-}
-
 __device__ __forceinline__ void prepare_row(NodeRegs& r) {
 #pragma unroll
   for (int q = 0; q < 2; q++) {
-    r.rcap[q] = __builtin_amdgcn_rcpf(i64_to_f32(r.cap[q]));
-    r.ralloc[q] = __builtin_amdgcn_rcpf(i64_to_f32(r.nalloc[q]));
+    r.dcap[q] = (double)r.cap[q];
+    r.rcap[q] = __builtin_amdgcn_rcp(r.dcap[q]);
+    r.dalloc[q] = (double)r.nalloc[q];
+    r.ralloc[q] = __builtin_amdgcn_rcp(r.dalloc[q]);
   }
 }
 
-// x * 100 / c for c > 0 (Go int64 division, truncating) — the framework.MaxNodeScore scaling of every
-// least/most scorer.  Fast path (0 <= x <= 16c, i.e. a result <= 1600): f32 estimate from the node's
-// reciprocal, off by at most one (relative error < 2^-21), then one exact int64 correction in each
-// direction.  Other operands take the native (inline, exec-masked) int64 division.
-__device__ __forceinline__ int32_t div100(int64_t x, int64_t c, float rc) {
-  const int64_t x100 = x * 100;
-  if (x < 0 || x > 16 * c) return (int32_t)(x100 / c);
-  int32_t q = (int32_t)(i64_to_f32(x100) * rc);
-  q -= (int32_t)((int64_t)q * c > x100);
-  q += (int32_t)((int64_t)(q + 1) * c <= x100);
-  return q;
+// x * 100 / c for 0 < c < 2^42 and 0 <= x <= 16c (Go int64 division, truncating) — the
+// framework.MaxNodeScore scaling of every least/most scorer.  On that range x, c, x*100 and every
+// q*c below are integers < 2^53, so each double product and comparison is exact: the reciprocal
+// estimate is off by at most one (q <= 1600, relative error << 2^-12) and one exact test in each
+// direction fixes it.  No 64-bit integer multiply (quarter-rate on the VALU).
+constexpr int64_t DIV_FAST_CAP = 1LL << 42;
+__device__ __forceinline__ bool div100_fast_ok(int64_t x, int64_t c) { return c > 0 && c < DIV_FAST_CAP && x >= 0 && x <= 16 * c; }
+__device__ __forceinline__ int32_t div100_f(int64_t x, double dc, double rc) {
+  const double dx = (double)x * 100.0;
+  const int32_t q = (int32_t)(dx * rc);
+  const double t = (double)q * dc;
+  return q - (int32_t)(t > dx) + (int32_t)(t + dc <= dx);
+}
+__device__ __forceinline__ int32_t div100(int64_t x, int64_t c, double dc, double rc) {
+  if (!div100_fast_ok(x, c)) return (int32_t)(x * 100 / c);
+  return div100_f(x, dc, rc);
 }
 
-// floor(s / d) for 0 <= s < 2^22, d > 0 (weighted means of per-resource scores)
+// floor(s / d) for 0 <= s < 2^22, 0 < d < 2^22 (weighted means of per-resource scores); 24-bit
+// multiplies are full rate
 __device__ __forceinline__ int32_t div_small(int32_t s, int32_t d) {
   int32_t q = (int32_t)((float)s * __builtin_amdgcn_rcpf((float)d));
-  q -= (int32_t)(q * d > s);
-  q += (int32_t)((q + 1) * d <= s);
+  q -= (int32_t)(__mul24(q, d) > s);
+  q += (int32_t)(__mul24(q + 1, d) <= s);
   return q;
 }
 
@@ -1104,7 +1108,7 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
     for (int q = 0; q < 2; q++) {
       const int64_t cap = n.cap[q];
       const int64_t room = (v ? n.sa[1][q] : n.sa[0][q]) - p.est[q];  // cap - used
-      const int32_t sc = (cap > 0 && room >= 0) ? div100(room, cap, n.rcap[q]) : 0;  // leastUsedScore
+      const int32_t sc = (cap > 0 && room >= 0) ? div100(room, cap, n.dcap[q], n.rcap[q]) : 0;  // leastUsedScore
       s += sc * k.w_la[q];
     }
     la = div_small(s, k.wsum_la);
@@ -1135,9 +1139,9 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
         int32_t sc;
         if (k.flags & AF_NUMA_MOST) {  // mostRequestedScore  most_allocated.go:53-62
           const int64_t rq = req > alloc ? alloc : req;
-          sc = alloc > 0 ? div100(rq, alloc, n.ralloc[q]) : (int32_t)((rq * 100) / alloc);
+          sc = alloc > 0 ? div100(rq, alloc, n.dalloc[q], n.ralloc[q]) : (int32_t)((rq * 100) / alloc);
         } else {  // leastRequestedScore  least_allocated.go:49-58
-          sc = req > alloc ? 0 : (alloc > 0 ? div100(alloc - req, alloc, n.ralloc[q]) : (int32_t)(((alloc - req) * 100) / alloc));
+          sc = req > alloc ? 0 : (alloc > 0 ? div100(alloc - req, alloc, n.dalloc[q], n.ralloc[q]) : (int32_t)(((alloc - req) * 100) / alloc));
         }
         s += sc * w;
         ws += w;
@@ -1149,6 +1153,73 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
   o.numa = (int16_t)nu;
   o.total = k.wp_la * la + k.wp_numa * nu;
   return o;
+}
+
+// use ? x*100/c : 0 (Go int64 division) as straight-line code: div100's estimate + corrections always,
+// the native division only for lanes outside the estimate's range (exec-masked, skipped when none).
+__device__ __forceinline__ int32_t div100_sel(bool use, int64_t x, int64_t c, double dc, double rc) {
+  int32_t q = div100_f(x, dc, rc);
+  if (use && !div100_fast_ok(x, c)) q = (int32_t)(x * 100 / c);
+  return use ? q : 0;
+}
+
+// eval_pair<false, false>(...).total without exec-mask branches: every predicate is a lane boolean and
+// every score term is computed and selected.  Plain pods on nodes seen through the LoadAware +
+// NodeNUMAResource (policy None) path — k_resolve's replay re-evaluation and k_eval_batch's plain
+// batches.  Same arithmetic as eval_pair (load_aware.go:122-249,387-406; plugin.go:408-442;
+// scoring.go:66-139,210-249); a failing filter gives -1 whatever the reason.
+__device__ __forceinline__ int32_t lite_total(const NodeRegs& n, bool expired, const DevPod& p, const KArgs& k) {
+  const uint32_t nf = n.flags, pf = p.flags, af = k.flags;
+  bool fail = !(nf & NF_VALID) || (pf & PF_DS_INVALID);
+  // LoadAwareScheduling.Filter
+  const bool la_on = !(pf & PF_DAEMONSET) && (nf & NF_HAS_METRIC);
+  const bool exp_f = (af & AF_FILTER_EXPIRED) && (af & AF_EXP_PRESENT) && expired;
+  fail |= la_on && exp_f && !(af & AF_ENABLE_WHEN_EXPIRED);
+  const bool thr_on = la_on && !exp_f && !(nf & NF_NM_NIL);
+  const bool v = (nf & NF_HAS_PROD_THR) && (pf & PF_PROD);
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const int64_t fh = v ? n.fh[1][q] : n.fh[0][q];
+    const bool on = (nf & (v ? nf_fh_on(1, q) : nf_fh_on(0, q))) != 0;
+    fail |= thr_on && on && p.est[q] > fh;
+  }
+  // filterAmplifiedCPUs
+  const bool amp = !(pf & PF_NUMA_SKIP) && p.req[0] != 0;
+  fail |= amp && (nf & NF_NUMA_AMP_ERR);
+  const bool rf = amp && !(nf & NF_NUMA_AMP_ERR) && (nf & NF_NUMA_RATIO_F);
+  fail |= rf && (nf & NF_NUMA_TOPO_INVALID);
+  const int64_t areq = (n.nreq[0] >= n.csm && n.csm > 0) ? n.nreq[0] - n.csm + n.csaf : n.nreq[0];
+  fail |= rf && !(nf & NF_NUMA_TOPO_INVALID) && p.req[0] > n.nalloc[0] - areq;
+  // LoadAwareScheduling.Score
+  const bool las = (nf & NF_HAS_METRIC) && !((af & AF_EXP_PRESENT) && expired) && !(nf & NF_NM_NIL) && k.wsum_la > 0;
+  const bool vs = (pf & PF_LA_SCORE_PROD) != 0;
+  int32_t sl = 0;
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const int64_t cap = n.cap[q];
+    const int64_t room = (vs ? n.sa[1][q] : n.sa[0][q]) - p.est[q];
+    sl += div100_sel(las && cap > 0 && room >= 0, room, cap, n.dcap[q], n.rcap[q]) * k.w_la[q];
+  }
+  const int32_t la = las ? div_small(sl, k.wsum_la) : 0;
+  // NodeNUMAResource.Score (policy None)
+  const bool rs = p.req[0] != 0 && (nf & NF_NUMA_RATIO_S);
+  const bool zero = (pf & PF_NUMA_SKIP) || (nf & NF_NUMA_SCORE_ZERO) || (rs && (nf & NF_NUMA_TOPO_INVALID));
+  const int64_t reqc = rs ? n.nreq[0] - n.csm + n.csas : n.nreq[0];
+  const bool most = (af & AF_NUMA_MOST) != 0;
+  int32_t sn = 0, ws = 0;
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const int32_t w = k.w_numa[q];
+    const int64_t alloc = n.nalloc[q];
+    const bool on = !zero && w != 0 && alloc != 0;
+    const int64_t req = q == 0 ? reqc + p.req[0] : n.nreq[1] + p.req[1];
+    const int64_t x = most ? (req > alloc ? alloc : req) : alloc - req;
+    const int32_t sc = div100_sel(on && (most || req <= alloc), x, alloc, n.dalloc[q], n.ralloc[q]);
+    sn += on ? sc * w : 0;
+    ws += on ? w : 0;
+  }
+  const int32_t nu = ws > 0 ? div_small(sn, ws) : 0;
+  return fail ? -1 : k.wp_la * la + k.wp_numa * nu;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1283,6 +1354,10 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
   const int p1 = min(batch_pods, p0 + pods_per_block);
   for (int p = p0; p < p1; p++) {
     const DevPod& pod = pods[base + p];
+    if constexpr (!DS && !NUMA && !CPU) {  // plain batch: straight-line evaluation
+      scores[(int64_t)p * score_stride + i] = (uint16_t)(lite_total(n, expired, pod, k) + 1);
+      continue;
+    }
     const EvalOut o = eval_pair<DS, NUMA, NUMA, false, CPU>(n, expired, pod, k, s, i, nv);
     scores[(int64_t)p * score_stride + i] = (uint16_t)(o.total + 1);
     if (NUMA) defer_push(o.status == STATUS_DEFERRED, ((uint64_t)p << 32) | (uint32_t)i, defer_list, defer_cnt);
@@ -1819,8 +1894,6 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
   __shared__ uint8_t s_changed[RES_SLOTS];
   __shared__ DevPod s_pod[MAX_BATCH];
   __shared__ int32_t s_cnt[MAX_BATCH];
-  __shared__ int32_t s_out[2][MAX_BATCH];
-  __shared__ uint64_t s_alloc[MAX_BATCH];
   __shared__ int32_t s_nslots;
   const int lane = tid & 63;
   const int base = *batch_base;
@@ -1925,27 +1998,41 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
   // ---- sequential replay of the batch ----
   // Lane c owns the c-th node changed in this batch: its row lives in that lane's registers, so the
   // per-pod re-evaluation of every changed node is one register-only eval across the lanes.
+  // Software-pipelined so that no LDS round trip sits on the per-pod critical path: pod j+1's record,
+  // candidates and row slots are read while pod j is replayed, its changed flags right after pod j's
+  // Reserve (consumed one iteration later), and the row of pod j's best unchanged candidate is
+  // fetched into spare registers before the re-evaluation, for the owner lane to take if it wins.
   int n_chg = 0, n_ovf = 0;
   NodeRegs mine;
   int my_node = -1;
   bool my_expired = false;
+  int32_t o_node = -1, o_score = -1;  // lane j: pod j's placement
+  uint64_t o_alloc = 0;
+  DevPod pod = s_pod[0];
+  uint32_t ck = s_cand[lane];
+  int csl = s_cand_slot[lane];
+  bool chg = false;  // prefetched changed flag of this lane's candidate (pods < j)
   for (int j = 0; j < B; j++) {
-    const DevPod pod = s_pod[j];
-    const uint32_t ck = s_cand[j * KMAX + lane];
-    int csl = s_cand_slot[j * KMAX + lane];
-    if (ck && csl < 0) {  // not prefetched: it has a row only if an earlier pod chose it (overflow slot)
-      const int node = key_node(ck);
-      int h = hash_of(node);
-      while (s_hkey[h] != node) h = (h + 1) & (HASH_SLOTS - 1);
-      csl = s_hval[h];
-    }
-    const bool in_chg = ck && csl >= 0 && s_changed[csl];
+    const bool more = j + 1 < B;
+    const DevPod pod_n = s_pod[more ? j + 1 : j];
+    const uint32_t ck_n = more ? s_cand[(j + 1) * KMAX + lane] : 0u;
+    int csl_n = s_cand_slot[(more ? j + 1 : j) * KMAX + lane];
+    const bool in_chg = chg;
     const uint32_t bu = wave_max_u32(in_chg ? 0u : ck);  // best unchanged snapshot candidate
+    int slot = -1;
+    LdsRow nxt;
+    if (bu != 0) {
+      const int src = __ffsll((unsigned long long)__ballot(ck == bu && !in_chg)) - 1;
+      slot = __builtin_amdgcn_readlane(csl, src);
+      if (slot >= 0) nxt = s_row[slot];  // wave-uniform address: a broadcast read
+    }
     uint32_t kc = 0;  // exact re-evaluation of the nodes changed earlier in this batch
     if (lane < n_chg) {
       NumaNode nv;
       if (NUMA) numa_load(s, my_node, nv);
-      kc = make_key(eval_pair<false, NUMA>(mine, my_expired, pod, k, s, my_node, nv).total, my_node);
+      const int32_t tot = NUMA ? eval_pair<false, NUMA>(mine, my_expired, pod, k, s, my_node, nv).total
+                               : lite_total(mine, my_expired, pod, k);
+      kc = make_key(tot, my_node);
     }
     const uint32_t bc = wave_max_u32(kc);
     const uint32_t w = max(bu, bc);
@@ -1954,8 +2041,6 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
       if (w == bc) {
         owner = __ffsll((unsigned long long)__ballot(lane < n_chg && kc == w)) - 1;
       } else {
-        const int src = __ffsll((unsigned long long)__ballot(ck == w && !in_chg)) - 1;
-        int slot = __shfl(csl, src, 64);
         const int node = key_node(w);
         owner = n_chg++;
         if (slot < 0) {  // chosen node missed the prefetch: overflow row from the SoA
@@ -1968,7 +2053,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
             s_hval[h] = (int16_t)slot;
           }
         } else if (lane == owner) {
-          regs_from_lds(s_row[slot], mine);
+          regs_from_lds(nxt, mine);
         }
         if (lane == owner) {
           prepare_row(mine);
@@ -1979,6 +2064,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
       }
       // Reserve: LoadAware assign (the new pod has no PodMetric -> counted at its estimate in every
       // non-prod term, and in the prod terms when it is prod), NodeInfo.Requested += requests.
+      uint64_t al = 0;
       if (lane == owner) {
         if ((mine.flags & NF_HAS_METRIC) && !(mine.flags & NF_NM_NIL)) {
 #pragma unroll
@@ -1995,7 +2081,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
         mine.nreq[1] += pod.req[1];
         // DeviceShare Reserve (a DeviceShare pod is alone in its batch: no later pod of the batch
         // reads the device state it patches)
-        s_alloc[j] = DS && (pod.flags & PF_DS) && (mine.flags & NF_DS_CACHE) ? ds_reserve(s, my_node, pod, k) : 0ull;
+        al = DS && (pod.flags & PF_DS) && (mine.flags & NF_DS_CACHE) ? ds_reserve(s, my_node, pod, k) : 0ull;
         if (NUMA) {  // NodeNUMAResource Reserve: the zones of a NUMA-policy node
           int64_t* out16 = numa_alloc + (int64_t)(base + j) * 16;
           const int pol = pf_numa_policy(pod.flags) ? pf_numa_policy(pod.flags) : nf_numa_policy(mine.flags);
@@ -2010,24 +2096,42 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
           }
         }
       }
-      if (lane == 0) {
-        s_out[0][j] = key_node(w) + global_offset;
-        s_out[1][j] = key_score(w);
+      if (DS) {
+        const uint64_t a = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(al >> 32), owner) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)al, owner);
+        if (lane == j) o_alloc = a;
       }
-    } else if (lane == 0) {
-      s_out[0][j] = -1;
-      s_out[1][j] = -1;
-      s_alloc[j] = 0;
-      if (NUMA)
+      if (lane == j) {
+        o_node = key_node(w) + global_offset;
+        o_score = key_score(w);
+      }
+    } else if (NUMA && lane == 0) {
 #pragma unroll
-        for (int t = 0; t < 16; t++) numa_alloc[(int64_t)(base + j) * 16 + t] = 0;
+      for (int t = 0; t < 16; t++) numa_alloc[(int64_t)(base + j) * 16 + t] = 0;
     }
-    wave_lds_sync();
+    // pod j+1's changed flags (row slots of unprefetched candidates: overflow hash), read after this
+    // Reserve's own LDS writes (in order within the wave), so they already include pod j's new node
+    bool chg_n = false;
+    if (ck_n) {
+      if (csl_n < 0) {
+        const int node = key_node(ck_n);
+        int h = hash_of(node);
+        while (s_hkey[h] != node) h = (h + 1) & (HASH_SLOTS - 1);
+        csl_n = s_hval[h];
+      }
+      chg_n = csl_n >= 0 && s_changed[csl_n];
+    }
+    if (NUMA) wave_lds_sync();  // the next re-evaluation reads the zones this Reserve patched
+    else __atomic_signal_fence(__ATOMIC_SEQ_CST);  // LDS ops of one wave execute in order
+    pod = pod_n;
+    ck = ck_n;
+    csl = csl_n;
+    chg = chg_n;
   }
   if (lane < B) {
-    chosen[base + lane] = s_out[0][lane];
-    chosen_score[base + lane] = s_out[1][lane];
-    dev_alloc[base + lane] = s_alloc[lane];
+    chosen[base + lane] = o_node;
+    chosen_score[base + lane] = o_score;
+    dev_alloc[base + lane] = o_alloc;
   }
   // write the patched rows back to the SoA
   if (lane < n_chg) {
