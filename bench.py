@@ -47,6 +47,17 @@ def eval_bytes(n_nodes, b):
     return n_nodes * abi.load_library().ke_row_bytes() + b * DEVPOD_BYTES + b * n_nodes * 2
 
 
+def pmc_traffic(n_nodes, b):
+    """HBM bytes per k_eval_batch launch from the committed rocprofv3 PMC passes (tools/pmc_summary.py)
+    for this exact workload shape; None when no pass covers it."""
+    f = os.path.join(ROOT, "profiles", "r01", "pmc_eval_traffic.json")
+    if not os.path.exists(f):
+        return None, None
+    d = json.load(open(f))
+    e = d["shapes"].get(f"nodes{n_nodes}pods{b}", {})
+    return e.get("traffic_bytes"), d["source"] if "traffic_bytes" in e else None
+
+
 def cpu_baseline(cl, pods, cfg, seconds, threads):
     from oracle.binding import Oracle  # checker / baseline only
 
@@ -147,6 +158,7 @@ def main():
     evals = K * slice_len * N
     eval_ms = sum(evm) / max(samples, 1)
     by = eval_bytes(hi - lo, a.batch)
+    traffic, traffic_src = pmc_traffic(hi - lo, a.batch)
     out = {
         "metric": "pod-node Filter+Score evals/sec + p99 per-pod sched latency @50k nodes",
         "value": evals / dt,
@@ -174,8 +186,8 @@ def main():
                       "note": "per batch; 'select' includes the all-gather + merge when sharded"},
         "roofline": {"bound": "hbm", "kernel": "k_eval_batch", "achieved": by / eval_ms / 1e6 if eval_ms else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": (by / eval_ms / 1e6 / HBM_PEAK_GBS) if eval_ms else None, "traffic": None,
-                     "bytes_per_launch": by},
+                     "frac": (by / eval_ms / 1e6 / HBM_PEAK_GBS) if eval_ms else None, "traffic": traffic,
+                     "traffic_source": traffic_src, "bytes_per_launch": by},
     }
     ev.close()
     if world == 1 and a.stream_nodes > 0:

@@ -40,6 +40,11 @@ extern "C" __device__ int32_t __ockl_wfred_add_i32(int32_t);
   } while (0)
 
 constexpr int EVAL_BLOCK = 256;
+// k_eval_batch grid: node tiles padded to a multiple of the 8 XCDs (x) x pod groups (y)
+inline dim3 eval_grid(int n_nodes, int block, int pods, int ppb) {
+  const int tiles = (n_nodes + block - 1) / block;
+  return dim3((unsigned)((tiles + 7) / 8 * 8), (unsigned)((pods + ppb - 1) / ppb));
+}
 constexpr int SELECT_BLOCK = 1024;
 constexpr int SELECT_WAVES = SELECT_BLOCK / 64;
 constexpr int KMAX = MAX_BATCH;
@@ -1159,7 +1164,7 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
 // the native division only for lanes outside the estimate's range (exec-masked, skipped when none).
 __device__ __forceinline__ int32_t div100_sel(bool use, int64_t x, int64_t c, double dc, double rc) {
   int32_t q = div100_f(x, dc, rc);
-  if (use && !div100_fast_ok(x, c)) q = (int32_t)(x * 100 / c);
+  if (use & !div100_fast_ok(x, c)) q = (int32_t)(x * 100 / c);
   return use ? q : 0;
 }
 
@@ -1170,40 +1175,40 @@ __device__ __forceinline__ int32_t div100_sel(bool use, int64_t x, int64_t c, do
 // scoring.go:66-139,210-249); a failing filter gives -1 whatever the reason.
 __device__ __forceinline__ int32_t lite_total(const NodeRegs& n, bool expired, const DevPod& p, const KArgs& k) {
   const uint32_t nf = n.flags, pf = p.flags, af = k.flags;
-  bool fail = !(nf & NF_VALID) || (pf & PF_DS_INVALID);
+  bool fail = !(nf & NF_VALID) | ((pf & PF_DS_INVALID) != 0);
   // LoadAwareScheduling.Filter
-  const bool la_on = !(pf & PF_DAEMONSET) && (nf & NF_HAS_METRIC);
-  const bool exp_f = (af & AF_FILTER_EXPIRED) && (af & AF_EXP_PRESENT) && expired;
-  fail |= la_on && exp_f && !(af & AF_ENABLE_WHEN_EXPIRED);
-  const bool thr_on = la_on && !exp_f && !(nf & NF_NM_NIL);
-  const bool v = (nf & NF_HAS_PROD_THR) && (pf & PF_PROD);
+  const bool la_on = !(pf & PF_DAEMONSET) & ((nf & NF_HAS_METRIC) != 0);
+  const bool exp_f = ((af & AF_FILTER_EXPIRED) != 0) & ((af & AF_EXP_PRESENT) != 0) & expired;
+  fail |= la_on & exp_f & !(af & AF_ENABLE_WHEN_EXPIRED);
+  const bool thr_on = la_on & !exp_f & !(nf & NF_NM_NIL);
+  const bool v = ((nf & NF_HAS_PROD_THR) != 0) & ((pf & PF_PROD) != 0);
 #pragma unroll
   for (int q = 0; q < 2; q++) {
     const int64_t fh = v ? n.fh[1][q] : n.fh[0][q];
     const bool on = (nf & (v ? nf_fh_on(1, q) : nf_fh_on(0, q))) != 0;
-    fail |= thr_on && on && p.est[q] > fh;
+    fail |= thr_on & on & (p.est[q] > fh);
   }
   // filterAmplifiedCPUs
-  const bool amp = !(pf & PF_NUMA_SKIP) && p.req[0] != 0;
-  fail |= amp && (nf & NF_NUMA_AMP_ERR);
-  const bool rf = amp && !(nf & NF_NUMA_AMP_ERR) && (nf & NF_NUMA_RATIO_F);
-  fail |= rf && (nf & NF_NUMA_TOPO_INVALID);
-  const int64_t areq = (n.nreq[0] >= n.csm && n.csm > 0) ? n.nreq[0] - n.csm + n.csaf : n.nreq[0];
-  fail |= rf && !(nf & NF_NUMA_TOPO_INVALID) && p.req[0] > n.nalloc[0] - areq;
+  const bool amp = !(pf & PF_NUMA_SKIP) & (p.req[0] != 0);
+  fail |= amp & ((nf & NF_NUMA_AMP_ERR) != 0);
+  const bool rf = amp & !(nf & NF_NUMA_AMP_ERR) & ((nf & NF_NUMA_RATIO_F) != 0);
+  fail |= rf & ((nf & NF_NUMA_TOPO_INVALID) != 0);
+  const int64_t areq = ((n.nreq[0] >= n.csm) & (n.csm > 0)) ? n.nreq[0] - n.csm + n.csaf : n.nreq[0];
+  fail |= rf & !(nf & NF_NUMA_TOPO_INVALID) & (p.req[0] > n.nalloc[0] - areq);
   // LoadAwareScheduling.Score
-  const bool las = (nf & NF_HAS_METRIC) && !((af & AF_EXP_PRESENT) && expired) && !(nf & NF_NM_NIL) && k.wsum_la > 0;
+  const bool las = ((nf & NF_HAS_METRIC) != 0) & !(((af & AF_EXP_PRESENT) != 0) & expired) & !(nf & NF_NM_NIL) & (k.wsum_la > 0);
   const bool vs = (pf & PF_LA_SCORE_PROD) != 0;
   int32_t sl = 0;
 #pragma unroll
   for (int q = 0; q < 2; q++) {
     const int64_t cap = n.cap[q];
     const int64_t room = (vs ? n.sa[1][q] : n.sa[0][q]) - p.est[q];
-    sl += div100_sel(las && cap > 0 && room >= 0, room, cap, n.dcap[q], n.rcap[q]) * k.w_la[q];
+    sl += div100_sel(las & (cap > 0) & (room >= 0), room, cap, n.dcap[q], n.rcap[q]) * k.w_la[q];
   }
   const int32_t la = las ? div_small(sl, k.wsum_la) : 0;
   // NodeNUMAResource.Score (policy None)
-  const bool rs = p.req[0] != 0 && (nf & NF_NUMA_RATIO_S);
-  const bool zero = (pf & PF_NUMA_SKIP) || (nf & NF_NUMA_SCORE_ZERO) || (rs && (nf & NF_NUMA_TOPO_INVALID));
+  const bool rs = (p.req[0] != 0) & ((nf & NF_NUMA_RATIO_S) != 0);
+  const bool zero = ((pf & PF_NUMA_SKIP) != 0) | ((nf & NF_NUMA_SCORE_ZERO) != 0) | (rs & ((nf & NF_NUMA_TOPO_INVALID) != 0));
   const int64_t reqc = rs ? n.nreq[0] - n.csm + n.csas : n.nreq[0];
   const bool most = (af & AF_NUMA_MOST) != 0;
   int32_t sn = 0, ws = 0;
@@ -1211,10 +1216,10 @@ __device__ __forceinline__ int32_t lite_total(const NodeRegs& n, bool expired, c
   for (int q = 0; q < 2; q++) {
     const int32_t w = k.w_numa[q];
     const int64_t alloc = n.nalloc[q];
-    const bool on = !zero && w != 0 && alloc != 0;
+    const bool on = !zero & (w != 0) & (alloc != 0);
     const int64_t req = q == 0 ? reqc + p.req[0] : n.nreq[1] + p.req[1];
     const int64_t x = most ? (req > alloc ? alloc : req) : alloc - req;
-    const int32_t sc = div100_sel(on && (most || req <= alloc), x, alloc, n.dalloc[q], n.ralloc[q]);
+    const int32_t sc = div100_sel(on & (most | (req <= alloc)), x, alloc, n.dalloc[q], n.ralloc[q]);
     sn += on ? sc * w : 0;
     ws += on ? w : 0;
   }
@@ -1341,7 +1346,13 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
                                                            int64_t score_stride, uint16_t* __restrict__ dsraw,
                                                            uint64_t* __restrict__ defer_list, uint32_t* defer_cnt,
                                                            uint8_t* __restrict__ aff_out, uint32_t* __restrict__ dsmax1) {
-  const int i = lo + blockIdx.x * blockDim.x + threadIdx.x;
+  // XCD-aware block mapping (eval_grid): workgroups are dealt to the 8 XCDs round-robin by linear id,
+  // so every pod group of one node tile is given ids of the same residue mod 8 — the tile's rows are
+  // fetched into one XCD's L2 once instead of once per pod group.
+  const int G = (int)gridDim.y;
+  const int b = (int)(blockIdx.x + blockIdx.y * gridDim.x), r = b >> 3;
+  const int tile = (r / G) * 8 + (b & 7), group = r % G;
+  const int i = lo + tile * blockDim.x + threadIdx.x;
   if (i >= hi) return;
   NodeRegs n;
   load_row(s, i, n);
@@ -1350,7 +1361,7 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
   NumaNode nv;
   if (NUMA) numa_load(s, i, nv);  // a pod's own policy reaches nodes without one
   const int base = *batch_base;
-  const int p0 = blockIdx.y * pods_per_block;
+  const int p0 = group * pods_per_block;
   const int p1 = min(batch_pods, p0 + pods_per_block);
   for (int p = p0; p < p1; p++) {
     const DevPod& pod = pods[base + p];
@@ -2958,7 +2969,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       if (hi > lo) {
         // a singleton batch has one pod's worth of lanes: single-wave blocks spread it over every CU
         const int eb = single ? 64 : EVAL_BLOCK;
-        dim3 grid((unsigned)((hi - lo + eb - 1) / eb), (unsigned)((bp + ppb - 1) / ppb));
+        const dim3 grid = eval_grid(hi - lo, eb, bp, ppb);
         // a DeviceShare pod never meets a NUMA policy (ke_capi check_numa_deviceshare): no NUMA path there
         auto eval = cpu ? (ds ? k_eval_batch<true, false, true> : numa ? k_eval_batch<false, true, true> : k_eval_batch<false, false, true>)
                         : ds ? (numa ? k_eval_batch<true, true, false> : k_eval_batch<true, false, false>)
@@ -3123,7 +3134,7 @@ int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t 
   const KArgs k = make_kargs(ctx, now);
   const int ppb = 8;
   HIP_OK(hipMemsetAsync(d->d_batch_base, 0, sizeof(int32_t), d->stream));
-  dim3 grid((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((n_pods + ppb - 1) / ppb));
+  const dim3 grid = eval_grid(N, EVAL_BLOCK, n_pods, ppb);
   hipLaunchKernelGGL((k_eval_batch<false, false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base, n_pods,
                      ppb, k, d->d_scores, d->capacity, d->d_dsraw, nullptr, nullptr, nullptr, nullptr);  // warm
   hipEvent_t e0, e1;
