@@ -31,8 +31,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--nodes", type=int, default=synth.CONFIGS[3]["nodes"])
-    ap.add_argument("--pods", type=int, default=synth.CONFIGS[3]["pods"])
+    ap.add_argument("--config", type=int, default=3, choices=(2, 3),
+                    help="BASELINE.json config: 3 = 50k x 100k (the metric's workload), 2 = 5k x 10k")
+    ap.add_argument("--nodes", type=int, default=None)
+    ap.add_argument("--pods", type=int, default=None)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target host time of the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -111,9 +113,11 @@ def main():
         if world > 1:
             dist.barrier()
 
-    N, P, K, W = a.nodes, a.pods, a.steps, a.warmup
-    cl = synth.make_cluster(N, synth.BASE_SEED + 3)
-    pods = synth.make_pods(P, synth.BASE_SEED + 103)
+    N = a.nodes or synth.CONFIGS[a.config]["nodes"]
+    P = a.pods or synth.CONFIGS[a.config]["pods"]
+    K, W = a.steps, a.warmup
+    cl = synth.make_cluster(N, synth.BASE_SEED + a.config)
+    pods = synth.make_pods(P, synth.BASE_SEED + 100 + a.config)
     cfg = synth.config(N, pod_batch=a.batch)
     cfg.device_ordinal = local_rank
     slice_len = P // K
@@ -171,8 +175,8 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "int64",
-        "data": "synthetic (BASELINE.md generator, seed 20251015+3)",
-        "config": {"workload": synth.CONFIGS[3]["name"], "nodes": N, "pods": K * slice_len,
+        "data": f"synthetic (BASELINE.md generator, seed 20251015+{a.config})",
+        "config": {"workload": synth.CONFIGS[a.config]["name"], "baseline_config": a.config, "nodes": N, "pods": K * slice_len,
                    "pods_per_batch": a.batch, "plugins": "LoadAwareScheduling+NodeNUMAResource",
                    "args": "v1beta3 defaults, NodeMetricExpirationSeconds=3600",
                    "parallelism": f"node-shard x{world}" + (" (RCCL all-gather of per-shard top-k)" if world > 1 else ""),
