@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define KE_ABI_VERSION 2
+#define KE_ABI_VERSION 3
 #define KE_ABSENT (-1)
 
 /* ---- error codes ---------------------------------------------------------------------------- */
@@ -377,7 +377,11 @@ typedef struct ke_pod {
   int32_t cpu_bind_required;
   int32_t cpu_bind_preferred;
   int32_t cpu_exclusive;
-  int32_t pad2;
+  /* ElasticQuota (elasticquota/plugin_helper.go:64-82 getPodAssociateQuotaNameAndTreeID): 0 = no quota
+   * (PreFilter Skip), else 1 + the index of the pod's quota in the last ke_quotas_load table. */
+  int16_t quota;
+  uint8_t quota_non_preemptible; /* extension.IsPodNonPreemptible (label preemptible=false) */
+  uint8_t pad2;
 } ke_pod;
 
 /* One candidate of a pod's speculative top-k list (device order: best first). */
@@ -479,6 +483,47 @@ int ke_last_schedule_stats(ke_ctx* ctx, double* total_ms, int32_t* n_batches,
 /* DeviceShare Reserve of the last ke_schedule (AutopilotAllocator.Allocate -> updateCacheUsed,
  * plugin.go:426-492): per pod, bit 16*type + minor set for every device instance allocated. */
 int ke_last_device_allocations(ke_ctx* ctx, int32_t n, uint64_t* minors);
+
+/* ---- ElasticQuota admission (pkg/scheduler/plugins/elasticquota) ----------
+ * One quota tree.  Replaces GroupQuotaManager's runtime calculation and the plugin's PreFilter /
+ * Reserve for the pods of a ke_schedule call:
+ *  - runtime: RuntimeQuotaCalculator (core/runtime_quota_calculator.go:117-189) over the tree, fed by
+ *    the limited requests of recursiveUpdateGroupTreeWithDeltaRequest (core/group_quota_manager.go:196-239)
+ *    and refreshed top-down as refreshRuntimeNoLock (:286-353); requests are fixed for the call;
+ *  - PreFilter (plugin.go:223-275): used + Mask(PodRequests, Max names) <= usedLimit (runtime on the
+ *    tree's resource keys, or Max with EnableRuntimeQuota false / for system and default quotas), non-preemptible
+ *    pods also against Min, EnableCheckParentQuota walks the ancestors (plugin_helper.go:281-301);
+ *    a refused pod is unschedulable (chosen -1) and reserves nothing;
+ *  - Reserve (core/group_quota_manager.go:700-760, ReservePod :943-963): the masked request is added
+ *    to used (and non-preemptible used) of the quota and every ancestor.
+ * Not modelled: scale-min, guaranteed usage, hook plugins, quota-overuse revocation, preemption.
+ * Resources: cpu (milli, getQuantityValue) and memory (bytes).  Values >= 0. */
+#define KE_MAX_QUOTAS 255 /* ke_pod.quota - 1 fits a byte on the device */
+typedef struct ke_quota_args {
+  int64_t total[KE_NRES];            /* totalResourceExceptSystemAndDefaultUsed of the tree */
+  uint8_t enable_runtime_quota;      /* ElasticQuotaArgs.EnableRuntimeQuota (v1beta3 default true) */
+  uint8_t enable_check_parent_quota; /* ElasticQuotaArgs.EnableCheckParentQuota (default false) */
+  uint8_t pad[6];
+} ke_quota_args;
+typedef struct ke_quota {
+  int32_t parent;                 /* index of the parent quota; -1 = koordinator-root-quota */
+  uint8_t has_max[KE_NRES];       /* keys of Spec.Max */
+  uint8_t has_min[KE_NRES];       /* keys of Spec.Min */
+  uint8_t allow_lent_resource;    /* AllowLentResource (label allow-lent-resource, default true) */
+  uint8_t limit_is_max;           /* system / default quota: used limit = Max (group_quota_manager.go:297) */
+  uint8_t pad[2];
+  int64_t max[KE_NRES];
+  int64_t min[KE_NRES];
+  int64_t shared_weight[KE_NRES]; /* extension.GetSharedWeight: annotation, else Max */
+  int64_t self_request[KE_NRES];  /* Σ Mask(PodRequests, Max) of the quota's own pods, pending and assigned */
+  int64_t used[KE_NRES];          /* Used: assigned pods of the quota and of its descendants */
+  int64_t non_preemptible_used[KE_NRES];
+} ke_quota;
+/* Load (replace) the tree, quotas in any order with parents by index; n <= KE_MAX_QUOTAS. */
+int ke_quotas_load(ke_ctx* ctx, const ke_quota_args* args, const ke_quota* quotas, int32_t n);
+/* The used limit PreFilter compares against (runtime, or Max) with its keys, and the quota's
+ * current used / non-preemptible used (after the Reserves of the last ke_schedule). */
+int ke_quota_state(ke_ctx* ctx, int32_t q, int64_t* limit, uint8_t* limit_has, int64_t* used, int64_t* np_used);
 
 /* ---- node sharding across GPUs (one process per GPU) ------------------------------------------
  * Replaces the upstream Parallelizer's fan-out of per-node Filter/Score over goroutines

@@ -9,7 +9,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 ABSENT = -1
 
 OK = 0
@@ -229,12 +229,40 @@ class Pod(C.Structure):
         ("cpu_bind_required", i32),
         ("cpu_bind_preferred", i32),
         ("cpu_exclusive", i32),
-        ("pad2", i32),
+        ("quota", C.c_int16),
+        ("quota_non_preemptible", u8),
+        ("pad2", u8),
+    ]
+
+
+MAX_QUOTAS = 255
+
+
+class QuotaArgs(C.Structure):
+    _fields_ = [("total", i64 * NRES), ("enable_runtime_quota", u8), ("enable_check_parent_quota", u8),
+                ("pad", u8 * 6)]
+
+
+class Quota(C.Structure):
+    _fields_ = [
+        ("parent", i32),
+        ("has_max", u8 * NRES),
+        ("has_min", u8 * NRES),
+        ("allow_lent_resource", u8),
+        ("limit_is_max", u8),
+        ("pad", u8 * 2),
+        ("max", i64 * NRES),
+        ("min", i64 * NRES),
+        ("shared_weight", i64 * NRES),
+        ("self_request", i64 * NRES),
+        ("used", i64 * NRES),
+        ("non_preemptible_used", i64 * NRES),
     ]
 
 
 STRUCTS = [Config, Node, NodeMetric, PodMetric, AggregatedUsage, Pod, ResourceMap, LoadAwareArgs, NumaArgs,
-           DeviceShareArgs, Device, NumaZone, Cpu]
+           DeviceShareArgs, Device, NumaZone, Cpu, QuotaArgs, Quota]
+QUOTA_DTYPE = np.dtype(Quota)
 
 # numpy views of the same layouts (bulk loads)
 NODE_DTYPE = np.dtype(Node)
@@ -312,6 +340,8 @@ EXPORTS = {
     "ke_last_numa_allocations": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_node_cpus_set": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p, i32]),
     "ke_last_cpusets": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
+    "ke_quotas_load": (C.c_int, [C.c_void_p, C.POINTER(QuotaArgs), C.c_void_p, i32]),
+    "ke_quota_state": (C.c_int, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "ke_schedule": (C.c_int, [C.c_void_p, i32, C.c_void_p, i64, C.c_void_p, C.c_void_p]),
     "ke_last_schedule_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(i32), C.c_void_p, i32]),
     "ke_set_profiling": (C.c_int, [C.c_void_p, i32]),

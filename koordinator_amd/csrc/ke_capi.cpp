@@ -14,6 +14,7 @@ void device_destroy(Context* ctx);
 int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, uint8_t* status, uint8_t* reason,
                 int16_t* la, int16_t* numa, int16_t* ds, int16_t* total, int32_t* best);
 int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t* chosen, int32_t* score);
+int device_quota_sync(Context* ctx);
 int device_debug_rows(Context* ctx, int32_t n, Row* out);
 int device_set_profiling(Context* ctx, int32_t every);
 int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t iters, double* avg_ms);
@@ -89,7 +90,8 @@ int ke_abi_struct_sizes(int32_t* sizes, int32_t n) {
                          (int32_t)sizeof(ke_resource_map), (int32_t)sizeof(ke_loadaware_args),
                          (int32_t)sizeof(ke_numa_args), (int32_t)sizeof(ke_deviceshare_args),
                          (int32_t)sizeof(ke_device),       (int32_t)sizeof(ke_numa_zone),
-                         (int32_t)sizeof(ke_cpu)};
+                         (int32_t)sizeof(ke_cpu),          (int32_t)sizeof(ke_quota_args),
+                         (int32_t)sizeof(ke_quota)};
   const int32_t m = (int32_t)(sizeof(all) / sizeof(all[0]));
   for (int32_t i = 0; i < n && i < m; i++) sizes[i] = all[i];
   return m;
@@ -227,6 +229,44 @@ int ke_node_cpus_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_cpu* cpus, i
   ns.cpu_max_ref = n > 0 ? max_ref_count : 1;
   ns.dirty = true;
   if (n > 0) ctx->c.cpu_enabled = true;
+  return KE_OK;
+}
+
+int ke_quotas_load(ke_ctx* ctx, const ke_quota_args* args, const ke_quota* quotas, int32_t n) {
+  if (!ctx || !args || n < 0 || n > KE_MAX_QUOTAS || (n > 0 && !quotas)) return fail(KE_ERR_INVALID, "ke_quotas_load arguments");
+  for (int r = 0; r < KE_NRES; r++)
+    if (args->total[r] < 0) return fail(KE_ERR_INVALID, "ke_quota_args.total must be >= 0");
+  std::vector<ke_quota> q(quotas, quotas + n);
+  for (const ke_quota& x : q)
+    for (int r = 0; r < KE_NRES; r++)
+      if (x.max[r] < 0 || x.min[r] < 0 || x.shared_weight[r] < 0 || x.self_request[r] < 0 || x.used[r] < 0 ||
+          x.non_preemptible_used[r] < 0)
+        return fail(KE_ERR_INVALID, "ke_quota values must be >= 0");
+  std::vector<int64_t> lim;
+  std::vector<uint8_t> has;
+  const int rc = quota_compute_limits(*args, q, lim, has);
+  if (rc) return rc;
+  Context& c = ctx->c;
+  c.qargs = *args;
+  c.quotas.swap(q);
+  c.qlimit.swap(lim);
+  c.qlimit_has.swap(has);
+  c.quota_dirty = true;
+  c.quota_on_device = false;
+  return KE_OK;
+}
+
+int ke_quota_state(ke_ctx* ctx, int32_t q, int64_t* limit, uint8_t* limit_has, int64_t* used, int64_t* np_used) {
+  if (!ctx || q < 0 || q >= (int32_t)ctx->c.quotas.size()) return fail(KE_ERR_NOT_FOUND, "ke_quota_state: no such quota");
+  const int rc = device_quota_sync(&ctx->c);
+  if (rc) return rc;
+  const ke_quota& x = ctx->c.quotas[q];
+  for (int r = 0; r < KE_NRES; r++) {
+    if (limit) limit[r] = ctx->c.qlimit[(size_t)q * KE_NRES + r];
+    if (limit_has) limit_has[r] = ctx->c.qlimit_has[(size_t)q * KE_NRES + r];
+    if (used) used[r] = x.used[r];
+    if (np_used) np_used[r] = x.non_preemptible_used[r];
+  }
   return KE_OK;
 }
 
@@ -373,6 +413,9 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
   if (rc) return rc;
   rc = check_cpuset(ctx, pods, n_pods);
   if (rc) return rc;
+  for (int32_t p = 0; p < n_pods; p++)
+    if (pods[p].quota < 0 || pods[p].quota > (int32_t)ctx->c.quotas.size())
+      return fail(KE_ERR_INVALID, "ke_pod.quota outside the loaded ElasticQuota tree");
   rc = require_device(ctx);
   if (rc) return rc;
   rc = device_schedule(&ctx->c, n_pods, pods, now_ns, chosen, score);

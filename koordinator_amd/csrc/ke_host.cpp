@@ -302,6 +302,7 @@ static bool ds_prepare(const ke_pod& pod, DevPod& d) {
 
 DevPod make_dev_pod(const ke_config& cfg, const ke_pod& pod) {
   DevPod d{};
+  d.quota = (uint8_t)pod.quota;  // range-checked against the loaded tree by ke_schedule
   uint8_t present[KE_NRES];
   estimate_pod(cfg.loadaware, pod, d.est, present);
   d.req[0] = pod.requests[KE_RES_CPU];
@@ -350,6 +351,7 @@ DevPod make_dev_pod(const ke_config& cfg, const ke_pod& pod) {
   } else if (d.ds_cnt[0] || d.ds_cnt[1] || d.ds_cnt[2]) {
     d.flags |= PF_DS;
   }
+  if (pod.quota_non_preemptible) d.flags |= PF_QUOTA_NP;
   return d;
 }
 
@@ -798,6 +800,114 @@ void host_assign(const ke_config& cfg, NodeState& ns, const ke_pod& pod, int64_t
   info.ts = pod.has_scheduled ? pod.scheduled_transition_ns : timestamp_ns;
   ns.asg.push_back(info);
   ns.dirty = true;
+}
+
+}  // namespace ke
+
+namespace ke {
+
+// ---------------------------------------------------------------------------------------------
+// ElasticQuota runtime (pkg/scheduler/plugins/elasticquota/core).  Requests are fixed for a
+// ke_schedule call, so the incremental GroupQuotaManager state reduces to one pass per resource:
+// limited requests bottom-up (recursiveUpdateGroupTreeWithDeltaRequest, group_quota_manager.go:196-239;
+// getLimitRequestNoLock, quota_info.go:217-228), then each parent's RuntimeQuotaCalculator shares its
+// runtime among its children top-down (refreshRuntimeNoLock :286-353; quotaTree.redistribution /
+// iterationForRedistribution, runtime_quota_calculator.go:117-189).  System / default quotas
+// (limit_is_max) stay out of the sharing; their limit is Max.
+// ---------------------------------------------------------------------------------------------
+namespace {
+struct QuotaShare {
+  int64_t weight, request, min;
+  bool lent;
+  int64_t runtime;
+};
+
+// one calculator: `total` shared among `kids` (min first, then sharedWeight water-filling)
+void share_runtime(int64_t total, std::vector<QuotaShare*>& kids) {
+  std::vector<QuotaShare*> open;
+  int64_t left = total, wsum = 0;
+  for (QuotaShare* c : kids) {
+    if (c->request > c->min) {  // wants more than its min: starts at min, joins the sharing
+      c->runtime = c->min;
+      open.push_back(c);
+      wsum += c->weight;
+    } else {
+      c->runtime = c->lent ? c->request : c->min;
+    }
+    left -= c->runtime;
+  }
+  if (left <= 0) return;
+  while (wsum > 0 && !open.empty()) {
+    std::vector<QuotaShare*> still;
+    int64_t spare = 0, still_w = 0;
+    for (QuotaShare* c : open) {
+      // int64(float64(sharedWeight)*float64(totalRes)/float64(totalSharedWeight) + 0.5)
+      const double share = static_cast<double>(c->weight) * static_cast<double>(left) / static_cast<double>(wsum) + 0.5;
+      c->runtime += static_cast<int64_t>(share);
+      if (c->runtime < c->request) {
+        still.push_back(c);
+        still_w += c->weight;
+      } else {
+        spare += c->runtime - c->request;
+        c->runtime = c->request;
+      }
+    }
+    if (spare <= 0) break;
+    open.swap(still);
+    left = spare;
+    wsum = still_w;
+  }
+}
+}  // namespace
+
+int quota_compute_limits(const ke_quota_args& args, const std::vector<ke_quota>& q, std::vector<int64_t>& limit,
+                         std::vector<uint8_t>& has) {
+  const int n = (int)q.size();
+  std::vector<std::vector<int>> kids(n + 1);  // kids[n] = children of the root quota
+  std::vector<int> order;                     // parents before children
+  for (int i = 0; i < n; i++) {
+    if (q[i].parent < -1 || q[i].parent >= n) return fail(KE_ERR_INVALID, "ke_quota.parent out of range");
+    kids[q[i].parent < 0 ? n : q[i].parent].push_back(i);
+  }
+  std::vector<int> stack{n};
+  while (!stack.empty()) {
+    const int p = stack.back();
+    stack.pop_back();
+    if (p != n) order.push_back(p);
+    for (int c : kids[p]) stack.push_back(c);
+  }
+  if ((int)order.size() != n) return fail(KE_ERR_INVALID, "ke_quota parents form a cycle");
+  limit.assign((size_t)n * KE_NRES, 0);
+  has.assign((size_t)n * KE_NRES, 0);
+  for (int r = 0; r < KE_NRES; r++) {
+    std::vector<QuotaShare> sh(n);
+    std::vector<int64_t> child_req(n, 0);
+    bool tree_key = false;
+    for (int i = 0; i < n; i++) tree_key = tree_key || q[i].has_max[r];
+    for (int t = n - 1; t >= 0; t--) {  // children before parents
+      const int i = order[t];
+      const ke_quota& x = q[i];
+      int64_t req = child_req[i] + x.self_request[r];
+      if (!x.allow_lent_resource && x.has_min[r] && x.min[r] > req) req = x.min[r];
+      const int64_t lim = (x.has_max[r] && req > x.max[r]) ? x.max[r] : req;
+      sh[i] = QuotaShare{x.shared_weight[r], lim, x.has_min[r] ? x.min[r] : 0, x.allow_lent_resource != 0, 0};
+      if (x.parent >= 0) child_req[x.parent] += lim;
+    }
+    auto share_children = [&](int p, int64_t total) {
+      std::vector<QuotaShare*> ks;
+      for (int c : kids[p])
+        if (!q[c].limit_is_max) ks.push_back(&sh[c]);
+      if (!ks.empty()) share_runtime(total, ks);
+    };
+    share_children(n, args.total[r]);
+    for (int i : order) share_children(i, sh[i].runtime);
+    for (int i = 0; i < n; i++) {
+      const bool use_max = !args.enable_runtime_quota || q[i].limit_is_max;
+      has[(size_t)i * KE_NRES + r] = use_max ? q[i].has_max[r] : (uint8_t)tree_key;
+      limit[(size_t)i * KE_NRES + r] = use_max ? q[i].max[r] : sh[i].runtime;
+    }
+  }
+  return KE_OK;
 }
 
 }  // namespace ke

@@ -66,7 +66,19 @@ struct Context {
   double kstat_resolve_phase_ms[6] = {0, 0, 0, 0, 0, 0};
   int64_t kstat_numa_deferred = 0;  // BestEffort pairs the last ke_eval / ke_schedule left to k_numa_fallback
   int32_t kstat_samples = 0;
+  // ElasticQuota tree (ke_quotas_load): objects, the used limits computed on the host, and whether the
+  // device copy of the table is stale
+  ke_quota_args qargs{};
+  std::vector<ke_quota> quotas;
+  std::vector<int64_t> qlimit;     // [q * KE_NRES + r]
+  std::vector<uint8_t> qlimit_has; // [q * KE_NRES + r]
+  bool quota_dirty = false;        // host table newer than the device table
+  bool quota_on_device = false;    // the device table holds the current used (after a ke_schedule)
 };
+
+// ElasticQuota used limits of every quota (RuntimeQuotaCalculator over the tree, or Max)
+int quota_compute_limits(const ke_quota_args& args, const std::vector<ke_quota>& q, std::vector<int64_t>& limit,
+                         std::vector<uint8_t>& has);
 
 // error plumbing (thread-local, read by ke_last_error)
 void set_error(const std::string& msg);

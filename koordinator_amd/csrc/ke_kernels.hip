@@ -59,7 +59,85 @@ struct SoA {
   uint64_t* nm;     // NUMA topology: `stride` uint64 zone / key masks (ke_types.h NUMA_M_*)
   int64_t* cs;      // CPU tables: NUM_CS_FIELDS arrays of `stride` int64 (nullptr until a cpuset pod / CPU table)
   CpuRec* cpu;      // CPU tables: CPU_SLOTS records per node, node-major
+  int64_t* qt;      // ElasticQuota: NUM_QF arrays of QT_STRIDE int64 (nullptr until a tree is loaded)
+  int32_t* qm;      // ElasticQuota: QT_STRIDE meta words (ke_types.h qm_*)
 };
+
+// ---------------------------------------------------------------------------------------------
+// ElasticQuota PreFilter / Reserve (elasticquota/plugin.go:223-275,345-359; plugin_helper.go:281-301;
+// core/group_quota_manager.go:700-760,943-963).  Used limits come from the host (ke_host.cpp
+// quota_compute_limits); the request is Mask(PodRequests, Max names of the pod's quota).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t qtf(const SoA& s, int f, int q) { return s.qt[f * QT_STRIDE + q]; }
+
+// one thread, global memory (singleton batches)
+__device__ bool quota_admit_g(const SoA& s, const DevPod& p, const KArgs& k, int64_t req[2]) {
+  const int qi = (int)p.quota - 1;
+  const int32_t m = s.qm[qi];
+  for (int r = 0; r < 2; r++) req[r] = qm_max(m, r) ? p.req[r] : 0;
+  for (int r = 0; r < 2; r++)
+    if (qm_lim(m, r) && qtf(s, QF_USED + r, qi) + req[r] > qtf(s, QF_LIM + r, qi)) return false;
+  if (p.flags & PF_QUOTA_NP)
+    for (int r = 0; r < 2; r++)
+      if (qm_min(m, r) && qtf(s, QF_NP + r, qi) + req[r] > qtf(s, QF_MIN + r, qi)) return false;
+  if (k.flags & AF_QUOTA_PARENT)
+    for (int a = qm_parent(m); a >= 0; a = qm_parent(s.qm[a]))
+      for (int r = 0; r < 2; r++)
+        if (req[r] != 0 && qm_lim(s.qm[a], r) && qtf(s, QF_USED + r, a) + req[r] > qtf(s, QF_LIM + r, a)) return false;
+  return true;
+}
+__device__ void quota_reserve_g(const SoA& s, const DevPod& p, const int64_t req[2]) {
+  for (int a = (int)p.quota - 1; a >= 0; a = qm_parent(s.qm[a]))
+    for (int r = 0; r < 2; r++) {
+      s.qt[(QF_USED + r) * QT_STRIDE + a] += req[r];
+      if (p.flags & PF_QUOTA_NP) s.qt[(QF_NP + r) * QT_STRIDE + a] += req[r];
+    }
+}
+
+// the replay's copy: lane l holds used / non-preemptible used of quotas l, 64+l, 128+l, 192+l
+struct QuotaRegs {
+  int64_t u[4][2], n[4][2];
+};
+__device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int64_t qreg_get(const int64_t (&a)[4][2], int q, int r) {  // q wave-uniform
+  const int b = q >> 6;
+  const int64_t v = b == 0 ? a[0][r] : b == 1 ? a[1][r] : b == 2 ? a[2][r] : a[3][r];
+  return readlane64(v, q & 63);
+}
+__device__ bool quota_admit_r(const SoA& s, const DevPod& p, const KArgs& k, const QuotaRegs& Q, int64_t req[2]) {
+  const int qi = (int)p.quota - 1;
+  const int32_t m = s.qm[qi];
+  for (int r = 0; r < 2; r++) req[r] = qm_max(m, r) ? p.req[r] : 0;
+  bool ok = true;
+  for (int r = 0; r < 2; r++)
+    ok = ok && !(qm_lim(m, r) && qreg_get(Q.u, qi, r) + req[r] > qtf(s, QF_LIM + r, qi));
+  if (p.flags & PF_QUOTA_NP)
+    for (int r = 0; r < 2; r++)
+      ok = ok && !(qm_min(m, r) && qreg_get(Q.n, qi, r) + req[r] > qtf(s, QF_MIN + r, qi));
+  if (ok && (k.flags & AF_QUOTA_PARENT))
+    for (int a = qm_parent(m); a >= 0 && ok; a = qm_parent(s.qm[a]))
+      for (int r = 0; r < 2; r++)
+        ok = ok && !(req[r] != 0 && qm_lim(s.qm[a], r) && qreg_get(Q.u, a, r) + req[r] > qtf(s, QF_LIM + r, a));
+  return ok;
+}
+__device__ void quota_reserve_r(const SoA& s, const DevPod& p, QuotaRegs& Q, const int64_t req[2], int lane) {
+  const bool np = (p.flags & PF_QUOTA_NP) != 0;
+  for (int a = (int)p.quota - 1; a >= 0; a = qm_parent(s.qm[a])) {
+    if (lane != (a & 63)) continue;
+#pragma unroll
+    for (int b = 0; b < 4; b++)
+      if (b == (a >> 6))
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+          Q.u[b][r] += req[r];
+          if (np) Q.n[b][r] += req[r];
+        }
+  }
+}
 
 // Amplify (node_resource_amplification.go:170-175) with the ratio's IEEE bits from the CPU SoA
 __device__ __forceinline__ int64_t amplify_bits(int64_t q, int64_t ratio_bits) {
@@ -1886,7 +1964,7 @@ __device__ __forceinline__ int hash_of(int node) { return (int)(((uint32_t)node 
 
 // NUMA: nodes may carry NUMA topology policies — changed nodes re-read their zones (patched by this
 // replay's Reserves) from the NUMA SoA, and numa_alloc[pod][2*id + r] receives each pod's allocation.
-template <bool DS, bool NUMA>
+template <bool DS, bool NUMA, bool QUOTA>
 __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __restrict__ pods, int32_t* __restrict__ batch_base,
                                                 int batch_pods, KArgs k, const uint32_t* __restrict__ cand,
                                                 const int32_t* __restrict__ cand_cnt, int32_t* __restrict__ chosen,
@@ -2019,6 +2097,15 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
   bool my_expired = false;
   int32_t o_node = -1, o_score = -1;  // lane j: pod j's placement
   uint64_t o_alloc = 0;
+  QuotaRegs Q;  // ElasticQuota used / non-preemptible used, lane-distributed (QUOTA only)
+  if (QUOTA)
+#pragma unroll
+    for (int b = 0; b < 4; b++)
+#pragma unroll
+      for (int r = 0; r < 2; r++) {
+        Q.u[b][r] = qtf(s, QF_USED + r, 64 * b + lane);
+        Q.n[b][r] = qtf(s, QF_NP + r, 64 * b + lane);
+      }
   DevPod pod = s_pod[0];
   uint32_t ck = s_cand[lane];
   int csl = s_cand_slot[lane];
@@ -2046,7 +2133,10 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
       kc = make_key(tot, my_node);
     }
     const uint32_t bc = wave_max_u32(kc);
-    const uint32_t w = max(bu, bc);
+    // ElasticQuota PreFilter: a refused pod is placed nowhere
+    int64_t qreq[2] = {0, 0};
+    const bool adm = !QUOTA || !pod.quota || quota_admit_r(s, pod, k, Q, qreq);
+    const uint32_t w = adm ? max(bu, bc) : 0u;
     if (w != 0) {
       int owner;
       if (w == bc) {
@@ -2107,6 +2197,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
           }
         }
       }
+      if (QUOTA && pod.quota) quota_reserve_r(s, pod, Q, qreq, lane);  // ElasticQuota Reserve
       if (DS) {
         const uint64_t a = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(al >> 32), owner) << 32) |
                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)al, owner);
@@ -2144,6 +2235,14 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
     chosen_score[base + lane] = o_score;
     dev_alloc[base + lane] = o_alloc;
   }
+  if (QUOTA)
+#pragma unroll
+    for (int b = 0; b < 4; b++)
+#pragma unroll
+      for (int r = 0; r < 2; r++) {
+        s.qt[(QF_USED + r) * QT_STRIDE + 64 * b + lane] = Q.u[b][r];
+        s.qt[(QF_NP + r) * QT_STRIDE + 64 * b + lane] = Q.n[b][r];
+      }
   // write the patched rows back to the SoA
   if (lane < n_chg) {
     const int64_t st = s.stride;
@@ -2345,7 +2444,9 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
   }
   if (threadIdx.x != 0) return;
   const DevPod pod = pods[base];
-  const uint32_t w = s_w;
+  int64_t qreq[2] = {0, 0};  // ElasticQuota PreFilter: a refused pod is placed nowhere
+  const bool quota = (k.flags & AF_QUOTA) && pod.quota;
+  const uint32_t w = (!quota || quota_admit_g(s, pod, k, qreq)) ? s_w : 0u;
   int32_t out_node = -1, out_score = -1;
   uint64_t alloc = 0, set[4] = {0, 0, 0, 0};
   int64_t* out16 = numa_alloc ? numa_alloc + (int64_t)base * 16 : nullptr;
@@ -2415,6 +2516,7 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
       if (DS && (pod.flags & PF_DS) && (nf & NF_DS_CACHE)) alloc = ds_reserve(s, node, pod, k);
       out_node = (int32_t)node + global_offset;
       out_score = key_score(w);
+      if (quota) quota_reserve_g(s, pod, qreq);  // ElasticQuota Reserve
     }
   }
   chosen[base] = out_node;
@@ -2548,12 +2650,59 @@ void device_destroy(Context* ctx) {
                   d->d_stamps,  d->d_parity, d->d_best,       d->d_gath,         d->soa.ds,   d->soa.dsm,
                   d->d_dsraw,   d->d_dsmax,  d->d_devalloc,   d->d_dsrows,       d->soa.nf,   d->soa.nm,
                   d->d_numaalloc, d->d_numarows, d->d_defer, d->d_defer_cnt, d->soa.cs, d->soa.cpu,
-                  d->d_cpurows, d->d_cpusets, d->d_aff};
+                  d->d_cpurows, d->d_cpusets, d->d_aff, d->soa.qt, d->soa.qm};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (d->stream) (void)hipStreamDestroy(d->stream);
   delete d;
   ctx->dev = nullptr;
+}
+
+// ElasticQuota table -> device (when the host tree changed since the last upload)
+static int device_quota_upload(Context* ctx) {
+  DeviceState* d = ctx->dev;
+  if (!d->soa.qt) {
+    HIP_OK(hipMalloc(&d->soa.qt, sizeof(int64_t) * NUM_QF * QT_STRIDE));
+    HIP_OK(hipMalloc(&d->soa.qm, sizeof(int32_t) * QT_STRIDE));
+  }
+  std::vector<int64_t> t((size_t)NUM_QF * QT_STRIDE, 0);
+  std::vector<int32_t> m(QT_STRIDE, 0xFFFF);  // parent -1, no keys
+  for (size_t i = 0; i < ctx->quotas.size(); i++) {
+    const ke_quota& q = ctx->quotas[i];
+    uint32_t w = (uint32_t)(uint16_t)(int16_t)q.parent;
+    for (int r = 0; r < KE_NRES; r++) {
+      t[(QF_LIM + r) * QT_STRIDE + i] = ctx->qlimit[i * KE_NRES + r];
+      t[(QF_MIN + r) * QT_STRIDE + i] = q.has_min[r] ? q.min[r] : 0;
+      t[(QF_USED + r) * QT_STRIDE + i] = q.used[r];
+      t[(QF_NP + r) * QT_STRIDE + i] = q.non_preemptible_used[r];
+      w |= (uint32_t)(ctx->qlimit_has[i * KE_NRES + r] != 0) << (16 + r);
+      w |= (uint32_t)(q.has_min[r] != 0) << (18 + r);
+      w |= (uint32_t)(q.has_max[r] != 0) << (20 + r);
+    }
+    m[i] = (int32_t)w;
+  }
+  HIP_OK(hipStreamSynchronize(d->stream));
+  HIP_OK(hipMemcpy(d->soa.qt, t.data(), sizeof(int64_t) * t.size(), hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(d->soa.qm, m.data(), sizeof(int32_t) * m.size(), hipMemcpyHostToDevice));
+  ctx->quota_dirty = false;
+  ctx->quota_on_device = true;
+  return KE_OK;
+}
+
+// device used / non-preemptible used -> the host objects (ke_quota_state)
+int device_quota_sync(Context* ctx) {
+  DeviceState* d = ctx->dev;
+  if (!ctx->quota_on_device || !d || !d->soa.qt) return KE_OK;
+  HIP_OK(hipSetDevice(d->device));
+  std::vector<int64_t> t((size_t)4 * QT_STRIDE);
+  HIP_OK(hipStreamSynchronize(d->stream));
+  HIP_OK(hipMemcpy(t.data(), d->soa.qt + (size_t)QF_USED * QT_STRIDE, sizeof(int64_t) * t.size(), hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < ctx->quotas.size(); i++)
+    for (int r = 0; r < KE_NRES; r++) {
+      ctx->quotas[i].used[r] = t[(size_t)r * QT_STRIDE + i];
+      ctx->quotas[i].non_preemptible_used[r] = t[(size_t)(2 + r) * QT_STRIDE + i];
+    }
+  return KE_OK;
 }
 
 #define RCCL_OK(expr)                                                               \
@@ -2936,7 +3085,15 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     if (rc) return rc;
     HIP_OK(hipMemsetAsync(d->d_defer_cnt, 0, sizeof(uint32_t) * n_batches, d->stream));
   }
-  const KArgs k = make_kargs(ctx, now);
+  KArgs k = make_kargs(ctx, now);
+  const bool quota = !ctx->quotas.empty();  // ElasticQuota admission + Reserve in the Reserve kernels
+  if (quota) {
+    if (ctx->quota_dirty) {
+      rc = device_quota_upload(ctx);
+      if (rc) return rc;
+    }
+    k.flags |= AF_QUOTA | (ctx->qargs.enable_check_parent_quota ? AF_QUOTA_PARENT : 0u);
+  }
   const int N = ctx->n_nodes;
   const int ppb = 8;
   HIP_OK(hipMemsetAsync(d->d_batch_base, 0, sizeof(int32_t), d->stream));
@@ -3035,8 +3192,10 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                          numa ? d->d_numaalloc : nullptr, d->d_cpusets,
                          d->d_aff, elo, ehi);
     } else {
-      auto resolve = ds ? (numa ? k_resolve<true, true> : k_resolve<true, false>)
-                        : (numa ? k_resolve<false, true> : k_resolve<false, false>);
+      auto resolve = quota ? (ds ? (numa ? k_resolve<true, true, true> : k_resolve<true, false, true>)
+                                 : (numa ? k_resolve<false, true, true> : k_resolve<false, false, true>))
+                           : (ds ? (numa ? k_resolve<true, true, false> : k_resolve<true, false, false>)
+                                 : (numa ? k_resolve<false, true, false> : k_resolve<false, false, false>));
       hipLaunchKernelGGL(resolve, dim3(1), dim3(RES_THREADS), 0, d->stream, d->soa, d->d_pods, d->d_batch_base, bp, k,
                          d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score, ctx->cfg.global_node_offset,
                          d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc, d->d_numaalloc);

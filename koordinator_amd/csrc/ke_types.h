@@ -100,6 +100,7 @@ enum PodFlag : uint32_t {
   PF_CPU_PREF0 = 1u << 17,     // 2 bits: state.preferredCPUBindPolicy
   PF_CPU_EXCL0 = 1u << 19,     // 2 bits: state.preferredCPUExclusivePolicy (KE_CPU_EXCL_*)
   PF_CPUSET = 1u << 21,        // the pod may bind CPUs on some node: singleton batch, cpuset Reserve
+  PF_QUOTA_NP = 1u << 22,      // ElasticQuota: IsPodNonPreemptible (checked against Min, counted in non-preemptible used)
 };
 KE_HD inline int pf_cpu_required(uint32_t f) { return (int)((f >> 15) & 3u); }
 KE_HD inline int pf_cpu_preferred(uint32_t f) { return (int)((f >> 17) & 3u); }
@@ -171,12 +172,21 @@ static_assert(sizeof(Row) == 152, "Row layout");
 // Bytes of one node row the eval kernel reads per pass (18 int64 fields + u32 flags).
 constexpr int ROW_BYTES = NUM_I64_FIELDS * 8 + 4;
 
+// ElasticQuota device table: int64 fields x QT_STRIDE quotas, and a meta word per quota
+constexpr int QT_STRIDE = 256;
+enum QuotaField : int { QF_LIM = 0, QF_MIN = 2, QF_USED = 4, QF_NP = 6, NUM_QF = 8 };  // + resource
+// meta: parent index (int16, -1 = root) | used-limit keys << 16 | Min keys << 18 | Max keys << 20
+KE_HD inline int qm_parent(int32_t m) { return (int)(int16_t)(m & 0xFFFF); }
+KE_HD inline bool qm_lim(int32_t m, int r) { return (m >> (16 + r)) & 1; }
+KE_HD inline bool qm_min(int32_t m, int r) { return (m >> (18 + r)) & 1; }
+KE_HD inline bool qm_max(int32_t m, int r) { return (m >> (20 + r)) & 1; }
+
 struct DevPod {
   int64_t est[2];  // LoadAware EstimatePod (cpu milli, memory); 0 for a resource without weight
   int64_t req[2];  // PodRequests cpu milli, memory (NodeNUMAResource, NodeInfo.Requested patch)
   uint32_t flags;
   uint8_t ds_cnt[3];  // DeviceShare: desired device count per type (GPU, RDMA, FPGA), 0 = not requested
-  uint8_t pad;
+  uint8_t quota;      // ElasticQuota: 0 = none, else 1 + quota index (ke_pod.quota)
   int64_t ds_req[5];  // DeviceShare per-instance request: gpu-core, gpu-memory, gpu-memory-ratio, rdma, fpga
 };
 static_assert(sizeof(DevPod) == 80, "DevPod layout");
@@ -213,6 +223,8 @@ enum ArgFlag : uint32_t {
   AF_NUMA_MOST = 1u << 3,           // NodeNUMAResource MostAllocated
   AF_DS_MOST = 1u << 4,             // DeviceShare MostAllocated
   AF_NUMA_HINT_MOST = 1u << 5,      // NodeNUMAResource NUMAScoringStrategy MostAllocated (hint scores)
+  AF_QUOTA = 1u << 6,               // an ElasticQuota tree is loaded: PreFilter admission + Reserve
+  AF_QUOTA_PARENT = 1u << 7,        // ElasticQuotaArgs.EnableCheckParentQuota
 };
 struct KArgs {
   int64_t now;

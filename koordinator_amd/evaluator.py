@@ -182,6 +182,18 @@ class Evaluator:
         self._check(self.lib.ke_last_cpusets(self.h, len(pods), abi.ptr(self.last_cpusets)))
         return chosen, score
 
+    def quotas_load(self, args, quotas):
+        """ElasticQuota tree (include/koord_eval.h ke_quotas_load): runtime computed on the host,
+        admission and Reserve applied inside schedule()."""
+        quotas = np.ascontiguousarray(quotas, abi.QUOTA_DTYPE)
+        self._check(self.lib.ke_quotas_load(self.h, C.byref(args), abi.ptr(quotas), len(quotas)))
+
+    def quota_state(self, q):
+        limit, used, npu = np.zeros(2, np.int64), np.zeros(2, np.int64), np.zeros(2, np.int64)
+        has = np.zeros(2, np.uint8)
+        self._check(self.lib.ke_quota_state(self.h, int(q), abi.ptr(limit), abi.ptr(has), abi.ptr(used), abi.ptr(npu)))
+        return {"limit": limit, "limit_has": has.astype(bool), "used": used, "np_used": npu}
+
     def stats(self):
         total = C.c_double()
         nb = abi.i32()

@@ -530,3 +530,60 @@ def make_numa_cpuset_pods(n_pods, seed, cpuset_fraction=0.6, policy_fraction=0.2
     pods["numa_topology_policy"] = np.where(pol, rng.integers(1, 4, n_pods), 0)
     pods["numa_exclusive"] = np.where(pol, rng.integers(0, 3, n_pods), 0)
     return pods
+
+
+# ---- ElasticQuota (config 5: "ElasticQuota tree of 64 leaves") ----------------------------------
+def make_quota_tree(seed, n_leaves=64, fanout=8, total_cpu=None, total_mem=None, lent_fraction=0.8):
+    """A 3-level tree: root children (n_leaves / fanout parents) -> leaves.  Max / Min / shared weight
+    in cpu milli and memory bytes; about a fifth of the quotas do not lend (allow-lent-resource
+    false).  Returns the ke_quota array; leaves are the last n_leaves entries."""
+    rng = np.random.default_rng(seed)
+    n_par = max(1, n_leaves // fanout)
+    q = np.zeros(n_par + n_leaves, abi.QUOTA_DTYPE)
+    total_cpu = total_cpu or 1_000_000 * 1000
+    total_mem = total_mem or 4_000_000 * GI
+
+    def fill(i, parent, scale):
+        q[i]["parent"] = parent
+        cpu_max = int(rng.integers(1, 4) * scale[0])
+        mem_max = int(rng.integers(1, 4) * scale[1])
+        q[i]["has_max"] = (1, 1)
+        q[i]["max"] = (cpu_max, mem_max)
+        q[i]["has_min"] = (1, 1)
+        q[i]["min"] = (int(cpu_max * rng.uniform(0.1, 0.6)) // 1000 * 1000, int(mem_max * rng.uniform(0.1, 0.6)) // MI * MI)
+        q[i]["shared_weight"] = q[i]["max"]
+        q[i]["allow_lent_resource"] = 1 if rng.random() < lent_fraction else 0
+
+    for p in range(n_par):
+        fill(p, -1, (total_cpu // n_par, total_mem // n_par))
+    for l in range(n_leaves):
+        fill(n_par + l, l // fanout if n_par > 1 else 0, (total_cpu // n_leaves, total_mem // n_leaves))
+    return q
+
+
+def quota_args(total_cpu, total_mem, runtime=True, check_parent=False):
+    a = abi.QuotaArgs()
+    a.total[0], a.total[1] = total_cpu, total_mem
+    a.enable_runtime_quota = 1 if runtime else 0
+    a.enable_check_parent_quota = 1 if check_parent else 0
+    return a
+
+
+def assign_quotas(pods, quotas, seed, no_quota_fraction=0.1, non_preemptible_fraction=0.2):
+    """Pods -> leaf quotas (ke_pod.quota = 1 + index); the quotas' self requests are the masked
+    requests of their pods (the whole queue is pending: GroupQuotaManager counts pending pods)."""
+    rng = np.random.default_rng(seed)
+    parents = set(int(x) for x in quotas["parent"] if x >= 0)
+    leaves = np.array([i for i in range(len(quotas)) if i not in parents], np.int64)
+    pods = pods.copy()
+    for p in range(len(pods)):
+        if rng.random() < no_quota_fraction:
+            pods[p]["quota"] = 0
+            continue
+        qi = int(leaves[rng.integers(0, len(leaves))])
+        pods[p]["quota"] = qi + 1
+        pods[p]["quota_non_preemptible"] = 1 if rng.random() < non_preemptible_fraction else 0
+        for r, res in enumerate((abi.RES_CPU, abi.RES_MEMORY)):
+            if quotas[qi]["has_max"][r]:
+                quotas[qi]["self_request"][r] += pods[p]["requests"][res]
+    return pods

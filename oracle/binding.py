@@ -67,6 +67,8 @@ def load():
         "or_ds_score": (i64, [V, C.POINTER(abi.Pod), i32]),
         "or_ds_reserve": (C.c_uint64, [V, C.POINTER(abi.Pod), i32]),
         "or_usage_percent": (i64, [i64, i64]),
+        "or_quotas_load": (C.c_int, [V, C.POINTER(abi.QuotaArgs), V, i32]),
+        "or_quota_state": (C.c_int, [V, i32, V, V, V, V]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -270,6 +272,24 @@ class Oracle:
         if rc != 0:
             raise RuntimeError(f"oracle schedule rc={rc}")
         return chosen, score
+
+    def quotas_load(self, args, quotas):
+        quotas = np.ascontiguousarray(quotas, abi.QUOTA_DTYPE)
+        rc = self.lib.or_quotas_load(self.h, C.byref(args), abi.ptr(quotas), len(quotas))
+        if rc != 0:
+            raise RuntimeError(f"oracle quotas_load rc={rc}")
+
+    def quota_state(self, q):
+        return _quota_state(self.lib.or_quota_state, self.h, q)
+
+
+def _quota_state(fn, h, q):
+    limit, used, npu = np.zeros(2, np.int64), np.zeros(2, np.int64), np.zeros(2, np.int64)
+    has = np.zeros(2, np.uint8)
+    rc = fn(h, int(q), abi.ptr(limit), abi.ptr(has), abi.ptr(used), abi.ptr(npu))
+    if rc != 0:
+        raise RuntimeError(f"quota state rc={rc}")
+    return {"limit": limit, "limit_has": has.astype(bool), "used": used, "np_used": npu}
 
 
 def normalize_scores(scores):

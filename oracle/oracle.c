@@ -17,6 +17,7 @@
  * assign cache on every Filter and every Score call, as the Go plugin does.
  */
 #include "oracle.h"
+#include "quota.h"
 #include "cpu_accumulator.h"
 
 #include <math.h>
@@ -70,6 +71,7 @@ struct or_cluster {
   ke_config cfg;
   int32_t n;
   or_node* nodes;
+  or_quotas* quotas; /* ElasticQuota tree (quota.c), NULL until loaded */
 };
 
 /* ---------------------------------------------------------------------------------------------- */
@@ -1938,7 +1940,26 @@ void or_destroy(or_cluster* c) {
     free(c->nodes[i].cpus);
   }
   free(c->nodes);
+  free(c->quotas);
   free(c);
+}
+
+int or_quotas_load(or_cluster* c, const ke_quota_args* args, const ke_quota* q, int32_t n) {
+  if (!c->quotas) c->quotas = (or_quotas*)calloc(1, sizeof(or_quotas));
+  if (!c->quotas) return KE_ERR_INVALID;
+  return orq_load(c->quotas, args, q, n);
+}
+
+int or_quota_state(const or_cluster* c, int32_t q, int64_t* limit, uint8_t* limit_has, int64_t* used,
+                   int64_t* np_used) {
+  if (!c->quotas || q < 0 || q >= c->quotas->n) return KE_ERR_NOT_FOUND;
+  for (int r = 0; r < KE_NRES; r++) {
+    if (limit) limit[r] = c->quotas->limit[q][r];
+    if (limit_has) limit_has[r] = c->quotas->limit_has[q][r];
+    if (used) used[r] = c->quotas->q[q].used[r];
+    if (np_used) np_used[r] = c->quotas->q[q].non_preemptible_used[r];
+  }
+  return KE_OK;
 }
 
 int or_node_cpus_set(or_cluster* c, int32_t node, int32_t n, const ke_cpu* cpus, int32_t max_ref) {
@@ -2360,6 +2381,14 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
   if (numa_alloc) memset(numa_alloc, 0, sizeof(int64_t) * 16 * (size_t)n_pods);
   eval_out* o = (eval_out*)malloc(sizeof(eval_out) * (size_t)(N > 0 ? N : 1));
   for (int p = 0; p < n_pods; p++) {
+    /* ElasticQuota PreFilter (plugin.go:223-275): a refused pod is evaluated nowhere */
+    if (c->quotas && orq_admit(c->quotas, &pods[p]) == 0) {
+      chosen[p] = -1;
+      if (score) score[p] = -1;
+      if (cpusets) memset(cpusets + (int64_t)p * ACC_WORDS, 0, sizeof(uint64_t) * ACC_WORDS);
+      if (dev_alloc) dev_alloc[p] = 0;
+      continue;
+    }
     int16_t bs;
     int32_t b = eval_pod(c, &pods[p], now, o, &bs);
     chosen[p] = b;
@@ -2383,6 +2412,7 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
       mask = or_ds_reserve(c, &pods[p], b);
       c->nodes[b].node.requested[KE_RES_CPU] += pods[p].requests[KE_RES_CPU];
       c->nodes[b].node.requested[KE_RES_MEMORY] += pods[p].requests[KE_RES_MEMORY];
+      if (c->quotas) orq_reserve(c->quotas, &pods[p]); /* ElasticQuota Reserve */
     }
     if (dev_alloc) dev_alloc[p] = mask;
   }

@@ -79,6 +79,10 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now_n
 /* filterNodeUsage's usage percentage, exposed for the threshold-folding property tests:
  * int64(math.Round(float64(used)/float64(total)*100)) (load_aware.go:299). */
 int64_t or_usage_percent(int64_t used, int64_t total);
+/* ElasticQuota (quota.c): tree load (runtime computed) and per-quota used limit / used state */
+int or_quotas_load(or_cluster* c, const ke_quota_args* args, const ke_quota* q, int32_t n);
+int or_quota_state(const or_cluster* c, int32_t q, int64_t* limit, uint8_t* limit_has, int64_t* used,
+                   int64_t* np_used);
 
 #ifdef __cplusplus
 }
