@@ -1,5 +1,7 @@
-"""BASELINE config 5 — DeviceShare GPU/RDMA partial-device Filter + Score over 20k nodes: throughput
-and per-pod latency (ElasticQuota admission is out of the hot path's scope).
+"""BASELINE config 5 — DeviceShare GPU/RDMA partial-device Filter + Score + ElasticQuota admission over
+20k nodes: throughput and per-pod latency.  `--quota` (default on) loads a 64-leaf ElasticQuota tree
+(synth.make_quota_tree) whose total is `--quota-frac` of the queue's requests; every pod with a quota
+is admitted (PreFilter) and reserved (used += request) on the GPU, in queue order.
 
 N synthetic nodes (synth.make_cluster + synth.make_devices: 8 GPUs with gpu-core 100 / ratio 100 /
 192Gi and 2 RDMA NICs each, random partial usage, 5 % without a device cache entry, 2 % unhealthy
@@ -33,16 +35,27 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-quota", action="store_true")
+    ap.add_argument("--quota-frac", type=float, default=0.6)
     a = ap.parse_args()
     N, P, K = a.nodes, a.pods, a.steps
     cl = synth.make_cluster(N, synth.BASE_SEED + 5)
     devices = synth.make_devices(N, synth.BASE_SEED + 55)
     pods = synth.make_ds_pods(P, synth.BASE_SEED + 105, device_fraction=a.device)
     cfg = synth.config(N)
+    quotas = None
+    if not a.no_quota:
+        tc = int(pods["requests"][:, 0].sum() * a.quota_frac)
+        tm = int(pods["requests"][:, 1].sum() * a.quota_frac)
+        quotas = synth.make_quota_tree(synth.BASE_SEED + 305, 64, 8, tc, tm)
+        pods = synth.assign_quotas(pods, quotas, synth.BASE_SEED + 306)
+        qargs = synth.quota_args(tc, tm)
 
     def load(h):
         synth.load_into(h, cl)
         synth.load_devices(h, devices)
+        if quotas is not None:
+            h.quotas_load(qargs, quotas)
         return h
 
     ew = load(Evaluator(cfg))  # warm-up context
@@ -66,7 +79,8 @@ def main():
         samples += ks["samples"]
     dt = time.perf_counter() - t0
     ev.close()
-    out = {"workload": f"{N} nodes x (8 GPU + 2 RDMA), {K * sl} pods ({a.device:.0%} with device requests)",
+    out = {"workload": f"{N} nodes x (8 GPU + 2 RDMA), {K * sl} pods ({a.device:.0%} with device requests)"
+                       + ("" if quotas is None else f", ElasticQuota tree of 64 leaves (total {a.quota_frac:.0%} of requests)"),
            "value": K * sl * N / dt, "unit": "pod-node evals/s", "pods_per_s": K * sl / dt,
            "ms_per_pod": dt / (K * sl) * 1e3, "batches": len(lat),
            "p99_batch_latency_ms": float(np.percentile(lat, 99)), "p50_batch_latency_ms": float(np.percentile(lat, 50)),
