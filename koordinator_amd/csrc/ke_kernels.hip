@@ -108,23 +108,29 @@ __device__ __forceinline__ int64_t qreg_get(const int64_t (&a)[4][2], int q, int
   const int64_t v = b == 0 ? a[0][r] : b == 1 ? a[1][r] : b == 2 ? a[2][r] : a[3][r];
   return readlane64(v, q & 63);
 }
-__device__ bool quota_admit_r(const SoA& s, const DevPod& p, const KArgs& k, const QuotaRegs& Q, int64_t req[2]) {
+__device__ __forceinline__ bool quota_admit_r(const SoA& s, const DevPod& p, const KArgs& k, const QuotaRegs& Q,
+                                              int64_t req[2]) {
   const int qi = (int)p.quota - 1;
   const int32_t m = s.qm[qi];
+#pragma unroll
   for (int r = 0; r < 2; r++) req[r] = qm_max(m, r) ? p.req[r] : 0;
   bool ok = true;
+#pragma unroll
   for (int r = 0; r < 2; r++)
     ok = ok && !(qm_lim(m, r) && qreg_get(Q.u, qi, r) + req[r] > qtf(s, QF_LIM + r, qi));
   if (p.flags & PF_QUOTA_NP)
+#pragma unroll
     for (int r = 0; r < 2; r++)
       ok = ok && !(qm_min(m, r) && qreg_get(Q.n, qi, r) + req[r] > qtf(s, QF_MIN + r, qi));
   if (ok && (k.flags & AF_QUOTA_PARENT))
     for (int a = qm_parent(m); a >= 0 && ok; a = qm_parent(s.qm[a]))
+#pragma unroll
       for (int r = 0; r < 2; r++)
         ok = ok && !(req[r] != 0 && qm_lim(s.qm[a], r) && qreg_get(Q.u, a, r) + req[r] > qtf(s, QF_LIM + r, a));
   return ok;
 }
-__device__ void quota_reserve_r(const SoA& s, const DevPod& p, QuotaRegs& Q, const int64_t req[2], int lane) {
+__device__ __forceinline__ void quota_reserve_r(const SoA& s, const DevPod& p, QuotaRegs& Q, const int64_t req[2],
+                                                int lane) {
   const bool np = (p.flags & PF_QUOTA_NP) != 0;
   for (int a = (int)p.quota - 1; a >= 0; a = qm_parent(s.qm[a])) {
     if (lane != (a & 63)) continue;
@@ -1949,7 +1955,9 @@ constexpr int RES_OVF = MAX_BATCH;            // rows of chosen nodes that misse
 constexpr int RES_SLOTS = RES_ROWS + RES_OVF;
 constexpr int HASH_SLOTS = 2 * MAX_BATCH * KMAX;  // load factor <= 1/2
 constexpr int HASH_EMPTY = -1;
-constexpr int RES_THREADS = 256;  // prologue width; the replay runs on wave 0 alone
+// prologue width (the replay runs on wave 0 alone): 8 waves keep 2x the row gathers in flight; the
+// NUMA variants stay at 4 waves (their replay wave needs up to 256 VGPRs, 2 waves per SIMD would cap it)
+template <bool NUMA> constexpr int res_threads() { return NUMA ? 256 : 512; }
 
 // Ordering point for LDS traffic between the lanes of ONE wavefront: LDS instructions of a wave
 // execute in issue order, so only the compiler must be kept from moving accesses across it
@@ -1965,7 +1973,7 @@ __device__ __forceinline__ int hash_of(int node) { return (int)(((uint32_t)node 
 // NUMA: nodes may carry NUMA topology policies — changed nodes re-read their zones (patched by this
 // replay's Reserves) from the NUMA SoA, and numa_alloc[pod][2*id + r] receives each pod's allocation.
 template <bool DS, bool NUMA, bool QUOTA>
-__global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __restrict__ pods, int32_t* __restrict__ batch_base,
+__global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(SoA s, const DevPod* __restrict__ pods, int32_t* __restrict__ batch_base,
                                                 int batch_pods, KArgs k, const uint32_t* __restrict__ cand,
                                                 const int32_t* __restrict__ cand_cnt, int32_t* __restrict__ chosen,
                                                 int32_t* __restrict__ chosen_score, int32_t global_offset,
@@ -1989,6 +1997,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_resolve(SoA s, const DevPod* __
   const int B = batch_pods;
 
   // ---- prologue (all RES_THREADS threads): candidates, distinct-node slots, row prefetch ----
+  constexpr int RES_THREADS = res_threads<NUMA>();
   if (tid < B) {
     s_cnt[tid] = cand_cnt[tid];
     s_pod[tid] = pods[base + tid];
@@ -3196,7 +3205,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                                  : (numa ? k_resolve<false, true, true> : k_resolve<false, false, true>))
                            : (ds ? (numa ? k_resolve<true, true, false> : k_resolve<true, false, false>)
                                  : (numa ? k_resolve<false, true, false> : k_resolve<false, false, false>));
-      hipLaunchKernelGGL(resolve, dim3(1), dim3(RES_THREADS), 0, d->stream, d->soa, d->d_pods, d->d_batch_base, bp, k,
+      hipLaunchKernelGGL(resolve, dim3(1), dim3(numa ? res_threads<true>() : res_threads<false>()), 0, d->stream, d->soa, d->d_pods, d->d_batch_base, bp, k,
                          d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score, ctx->cfg.global_node_offset,
                          d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc, d->d_numaalloc);
     }
