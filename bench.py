@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target host time of the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true", help="one-stream schedule (A/B of the pipelined one)")
+    ap.add_argument("--profile-every", type=int, default=8, help="HIP-event-sample every n-th batch (0 = off)")
     ap.add_argument("--stream-nodes", type=int, default=4_000_000,
                     help="B=1 streaming sweep size (N*row > 512 MB, past the 256 MB Infinity Cache); 0 = skip")
     return ap.parse_args()
@@ -137,8 +139,9 @@ def main():
     shard.init_node_sharding(ev, rank, world)
     lo, hi = ev.shard_range()
     ev.eval(pods[:0], synth.T0)  # derive + upload every node row: state resident in HBM
-    ev.set_profiling(8)
-    lat, evm, sel, res, samples, rsplit = [], [], [], [], 0, []
+    ev.set_profiling(a.profile_every)
+    ev.set_pipeline(not a.no_pipeline)
+    lat, evm, sel, fix, res, samples, rsplit, npipe, enq, hof = [], [], [], [], [], 0, [], 0, [], []
     placed = 0
     barrier()
     t0 = time.perf_counter()
@@ -150,7 +153,11 @@ def main():
         ks = ev.kernel_stats()
         evm.append(ks["eval_ms"] * ks["samples"])
         sel.append(ks["select_ms"] * ks["samples"])
-        res.append(ks["resolve_ms"] * ks["samples"])
+        res.append(ks["resolve_ms"])
+        fix.append(ks["fixup_ms"])
+        npipe += ks["pipelined_batches"]
+        enq.append(ks["enqueue_ms"])
+        hof.append(ks["handoff_ms"])
         samples += ks["samples"]
         rsplit.append((ks["resolve_prologue_ms"], ks["resolve_replay_ms"]))
     barrier()
@@ -184,7 +191,9 @@ def main():
         "p99_pod_latency_ms": float(np.percentile(lat, 99)) if lat else None,
         "p50_pod_latency_ms": float(np.percentile(lat, 50)) if lat else None,
         "pods_placed": placed,
-        "kernel_ms": {"eval": eval_ms, "select": sum(sel) / max(samples, 1), "resolve": sum(res) / max(samples, 1),
+        "kernel_ms": {"eval": eval_ms, "select": sum(sel) / max(samples, 1), "fixup": float(np.mean(fix)), "handoff": float(np.mean(hof)),
+                      "resolve": float(np.mean(res)), "pipelined_batches": npipe,
+                      "host_enqueue_ms_per_step": float(np.mean(enq)),
                       "resolve_prologue": float(np.mean([x[0] for x in rsplit])),
                       "resolve_replay": float(np.mean([x[1] for x in rsplit])), "samples": samples,
                       "note": "per batch; 'select' includes the all-gather + merge when sharded"},

@@ -548,6 +548,16 @@ int ke_shard_range(ke_ctx* ctx, int32_t* lo, int32_t* hi);
  * the eval / select / resolve kernels over the sampled batches of the last ke_schedule. */
 int ke_set_profiling(ke_ctx* ctx, int32_t sample_every);
 int ke_last_kernel_stats(ke_ctx* ctx, double* eval_ms, double* select_ms, double* resolve_ms, int32_t* samples);
+/* Per-batch timing of the last ke_schedule, ms: ms6 = {eval, select (HIP-event samples on the eval
+ * stream), fixup (k_fixup after its wait, pipelined batches), Reserve (in-kernel stamps: prologue +
+ * replay, every batch), host enqueue time of the whole call, hand-off (end of a pipelined batch's
+ * replay -> start of the next one's)}, the number of event samples, and how many batches ran
+ * pipelined. */
+int ke_last_kernel_stats_ex(ke_ctx* ctx, double* ms6, int32_t* samples, int32_t* pipelined_batches);
+/* Pipelined schedule (default on): batch b's eval + select overlap batch b-1's Reserve replay on a
+ * second stream.  Off = one stream, every batch waits for the previous Reserve.  The
+ * placements are identical either way. */
+int ke_set_pipeline(ke_ctx* ctx, int32_t on);
 /* Resolve kernel split of the last ke_schedule (in-kernel s_memrealtime stamps, every batch):
  * average ms per batch of candidate/row staging (prologue) and of the sequential replay. */
 int ke_last_resolve_split(ke_ctx* ctx, double* prologue_ms, double* replay_ms);

@@ -346,6 +346,8 @@ EXPORTS = {
     "ke_last_schedule_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(i32), C.c_void_p, i32]),
     "ke_set_profiling": (C.c_int, [C.c_void_p, i32]),
     "ke_last_kernel_stats": (C.c_int, [C.c_void_p] + [C.POINTER(C.c_double)] * 3 + [C.POINTER(i32)]),
+    "ke_last_kernel_stats_ex": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(i32), C.POINTER(i32)]),
+    "ke_set_pipeline": (C.c_int, [C.c_void_p, i32]),
     "ke_last_resolve_split": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "ke_debug_resolve_phases": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ke_debug_numa_deferred": (C.c_int, [C.c_void_p, C.POINTER(i64)]),

@@ -17,6 +17,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
 int device_quota_sync(Context* ctx);
 int device_debug_rows(Context* ctx, int32_t n, Row* out);
 int device_set_profiling(Context* ctx, int32_t every);
+int device_set_pipeline(Context* ctx, int32_t on);
 int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t iters, double* avg_ms);
 int device_comm_unique_id(uint8_t* id);
 int device_shard_init(Context* ctx, int rank, int world, const uint8_t* id);
@@ -470,6 +471,26 @@ int ke_last_kernel_stats(ke_ctx* ctx, double* eval_ms, double* select_ms, double
   if (resolve_ms) *resolve_ms = ctx->c.kstat_resolve_ms;
   if (samples) *samples = ctx->c.kstat_samples;
   return KE_OK;
+}
+
+int ke_last_kernel_stats_ex(ke_ctx* ctx, double* ms4 /* [6] */, int32_t* samples, int32_t* pipelined_batches) {
+  if (!ctx || !ms4) return fail(KE_ERR_INVALID, "ke_last_kernel_stats_ex arguments");
+  ms4[0] = ctx->c.kstat_eval_ms;
+  ms4[1] = ctx->c.kstat_select_ms;
+  ms4[2] = ctx->c.kstat_fixup_ms;
+  ms4[3] = ctx->c.kstat_resolve_ms;
+  if (samples) *samples = ctx->c.kstat_samples;
+  if (pipelined_batches) *pipelined_batches = ctx->c.last_pipelined;
+  ms4[4] = ctx->c.last_enqueue_ms;
+  ms4[5] = ctx->c.kstat_handoff_ms;
+  return KE_OK;
+}
+
+int ke_set_pipeline(ke_ctx* ctx, int32_t on) {
+  if (!ctx) return fail(KE_ERR_INVALID, "null context");
+  int rc = require_device(ctx);
+  if (rc) return rc;
+  return device_set_pipeline(&ctx->c, on);
 }
 
 int ke_last_resolve_split(ke_ctx* ctx, double* prologue_ms, double* replay_ms) {

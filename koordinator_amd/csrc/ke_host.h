@@ -61,7 +61,9 @@ struct Context {
   // last ke_schedule timing
   double last_total_ms = 0.0;
   std::vector<double> last_batch_ms;
-  double kstat_eval_ms = 0, kstat_select_ms = 0, kstat_resolve_ms = 0;
+  double kstat_eval_ms = 0, kstat_select_ms = 0, kstat_resolve_ms = 0, kstat_fixup_ms = 0, kstat_handoff_ms = 0;
+  int32_t last_pipelined = 0;
+  double last_enqueue_ms = 0;  // host time spent enqueueing the last ke_schedule's launches  // batches of the last ke_schedule that ran pipelined (two streams)
   double kstat_resolve_prologue_ms = 0, kstat_resolve_loop_ms = 0;
   double kstat_resolve_phase_ms[6] = {0, 0, 0, 0, 0, 0};
   int64_t kstat_numa_deferred = 0;  // BestEffort pairs the last ke_eval / ke_schedule left to k_numa_fallback

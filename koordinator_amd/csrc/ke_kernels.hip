@@ -17,6 +17,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -1710,12 +1711,15 @@ constexpr int SEL_WINDOW = 64;  // histogram window below the pod's best score
 // global node index, so per-shard lists merge without translation (k_merge).
 // DS: the batch is one DeviceShare pod; its scores get the normalized DeviceShare term (dsmax1 =
 // 1 + the max raw score over all feasible nodes, after the all-reduce when node-sharded).
+// kext / ostride: the pipelined schedule selects top-(k_j + KMAX) lists of a stale snapshot into
+// rows of `ostride` keys (pipelining); otherwise kext = 0, ostride = KMAX.
 template <bool DS>
 __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restrict__ scores, int64_t score_stride,
                                                          int lo, int hi, uint32_t* __restrict__ cand,
                                                          int32_t* __restrict__ cand_cnt,
                                                          const uint16_t* __restrict__ dsraw,
-                                                         const uint32_t* __restrict__ dsmax1, int32_t wds) {
+                                                         const uint32_t* __restrict__ dsmax1, int32_t wds, int kext,
+                                                         int ostride) {
   __shared__ int16_t s_lut[DS ? MAX_DS_RAW + 1 : 1];
   DsNorm dn{dsraw, s_lut};
   if (DS) {
@@ -1729,7 +1733,7 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
   __shared__ int32_t s_tie[SELECT_WAVES];
   __shared__ int32_t s_out;
   const int j = blockIdx.x;
-  const int k = min(j + 1, KMAX);
+  const int k = min(j + 1, KMAX) + kext;
   const uint16_t* sc = scores + (int64_t)j * score_stride;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int seg = ((hi - lo + SELECT_WAVES - 1) / SELECT_WAVES + 511) & ~511;
@@ -1848,7 +1852,7 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
   // pass 3: select
   int running = 0;  // ties of this wave before the current row
   for (int w = 0; w < wave; w++) running += need_ties > 0 ? s_tie[w] : 0;
-  uint32_t* out = cand + (int64_t)j * KMAX;
+  uint32_t* out = cand + (int64_t)j * ostride;
   for (int b = w0; b < w1; b += 512) {
     const int i0 = b + lane * 8;
     uint32_t v[8];
@@ -1892,32 +1896,129 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
 // top-k_j of pod j is the top-k_j of the union of the per-shard top-k_j lists (each global top-k_j node
 // is also top-k_j inside its own shard).  Keys are unique (they embed the node index), so a key's
 // rank in the union is the number of larger keys; ranks < k_j are written in order.
-constexpr int GATH_WORDS = MAX_BATCH * KMAX + MAX_BATCH;
+// L = list length (KMAX, or KSTALE for the pipelined schedule's stale lists); outputs use stride L.
+constexpr int KSTALE = 2 * KMAX;  // stale-snapshot list length of the pipelined schedule
+constexpr int gath_words(int L) { return MAX_BATCH * L + MAX_BATCH; }
+constexpr int GATH_WORDS_MAX = MAX_BATCH * KSTALE + MAX_BATCH;
 constexpr int MAX_WORLD = 8;
-constexpr int MERGE_BLOCK = MAX_WORLD * KMAX;
+constexpr int MERGE_BLOCK = MAX_WORLD * KSTALE;
 
-__global__ __launch_bounds__(MERGE_BLOCK) void k_merge(const uint32_t* __restrict__ gath, int world,
+__global__ __launch_bounds__(MERGE_BLOCK) void k_merge(const uint32_t* __restrict__ gath, int world, int L, int kext,
                                                        uint32_t* __restrict__ cand, int32_t* __restrict__ cand_cnt) {
   __shared__ uint4 s_k[MERGE_BLOCK / 4];
-  const int j = blockIdx.x, k = min(j + 1, KMAX);
-  const int t = threadIdx.x, r = t / KMAX, c = t % KMAX;
+  const int j = blockIdx.x, k = min(j + 1, KMAX) + kext;
+  const int t = threadIdx.x, r = t / L, c = t % L;
   uint32_t key = 0;
   if (r < world) {
-    const uint32_t* blk = gath + (int64_t)r * GATH_WORDS;
-    if (c < (int)blk[MAX_BATCH * KMAX + j]) key = blk[j * KMAX + c];
+    const uint32_t* blk = gath + (int64_t)r * gath_words(L);
+    if (c < (int)blk[MAX_BATCH * L + j]) key = blk[j * L + c];
   }
   reinterpret_cast<uint32_t*>(s_k)[t] = key;
   const int nz = __syncthreads_count(key != 0u);
   if (key) {
     int rank = 0;
-    const int n4 = world * KMAX / 4;
+    const int n4 = world * L / 4;
     for (int u = 0; u < n4; u++) {
       const uint4 q = s_k[u];
       rank += (int)(q.x > key) + (int)(q.y > key) + (int)(q.z > key) + (int)(q.w > key);
     }
-    if (rank < k) cand[j * KMAX + rank] = key;
+    if (rank < k) cand[j * L + rank] = key;
   }
   if (t == 0) cand_cnt[j] = min(nz, k);
+}
+
+// --- pipelined schedule: exact candidate lists from a stale snapshot ------------------------------
+// Batch b's eval + select run while batch b-1 is still being resolved (pipelining): they
+// see every Reserve of batches <= b-2, and arbitrary (possibly half-written) rows for the <= 64 nodes
+// batch b-1 chose ("touched").  Every other row equals the exact pre-b state S.  The select keeps the
+// stale top-(k_j + KMAX) per pod.  An untouched node in the exact top-k_j under S has at most k_j - 1
+// untouched and T <= KMAX touched nodes above it in the stale order, so it is in the stale list; the
+// touched nodes are re-evaluated here against their rows in S (this kernel runs after batch b-1's
+// resolve).  The top-k_j of (stale list minus touched) + (touched, fresh keys) is therefore the exact
+// top-k_j under S that k_resolve expects.  One workgroup per pod.
+constexpr int FIX_BLOCK = KSTALE + KMAX;  // stale keys, then fresh keys of the touched nodes
+// Device-side hand-off between the eval stream and the persistent Reserve kernel (k_resolve_run):
+// flags in global memory, agent-scope release / acquire (MI355X_MICROARCH.md, inter-workgroup
+// visibility), every wait bounded in time and abandoned when the run's error word is set.
+constexpr uint64_t HANDOFF_TIMEOUT_TICKS = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
+__device__ __forceinline__ bool wait_at_least(const int32_t* flag, int32_t want, int32_t* err) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < want) {
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > HANDOFF_TIMEOUT_TICKS) {
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return true;
+}
+
+// wait_b >= 0: the lists need the Reserves of batch wait_b (the touched nodes' rows): wait for its flag
+// in `done` first.  When the list is written the workgroup adds 1 to *ready (the Reserve kernel waits
+// for all of the batch's pods).
+__global__ __launch_bounds__(FIX_BLOCK) void k_fixup(SoA s, const DevPod* __restrict__ pods,
+                                                     const int32_t* __restrict__ batch_base, KArgs k,
+                                                     const uint32_t* __restrict__ stale,
+                                                     const int32_t* __restrict__ stale_cnt,
+                                                     const int32_t* __restrict__ touched, int n_touched,
+                                                     int32_t global_offset, uint32_t* __restrict__ cand,
+                                                     int32_t* __restrict__ cand_cnt, const int32_t* __restrict__ done,
+                                                     int wait_b, int32_t* __restrict__ ready, int32_t* __restrict__ err,
+                                                     uint64_t* __restrict__ fstamp) {
+  __shared__ int32_t s_tn[KMAX];
+  __shared__ uint4 s_k[FIX_BLOCK / 4];
+  __shared__ int32_t s_ok;
+  const int j = blockIdx.x, kj = min(j + 1, KMAX);
+  const int t = threadIdx.x;
+  if (t == 0) {
+    s_ok = wait_b < 0 || wait_at_least(done + wait_b, 1, err);
+    if (j == 0 && fstamp) fstamp[0] = __builtin_amdgcn_s_memrealtime();
+  }
+  __syncthreads();
+  if (!s_ok) return;
+  if (t < KMAX) s_tn[t] = t < n_touched ? touched[t] - global_offset : -1;  // chosen: -1 = unplaced
+  __syncthreads();
+  uint32_t key = 0;
+  if (t < KSTALE) {
+    if (t < stale_cnt[j]) key = stale[j * KSTALE + t];
+    if (key) {
+      const int node = key_node(key);
+#pragma unroll 8
+      for (int u = 0; u < KMAX; u++) key = s_tn[u] == node ? 0u : key;  // broadcast reads
+    }
+  } else {
+    const int u = t - KSTALE;
+    const int node = s_tn[u];
+    bool first = node >= 0;
+    for (int v = 0; v < u; v++) first = first && s_tn[v] != node;
+    if (first) {
+      NodeRegs n;
+      load_row(s, node, n);
+      prepare_row(n);
+      const DevPod& pod = pods[*batch_base + j];
+      key = make_key(lite_total(n, node_expired(n, k), pod, k), node);
+    }
+  }
+  reinterpret_cast<uint32_t*>(s_k)[t] = key;
+  const int nz = __syncthreads_count(key != 0u);
+  if (key) {
+    int rank = 0;
+#pragma unroll 4
+    for (int u = 0; u < FIX_BLOCK / 4; u++) {
+      const uint4 q = s_k[u];
+      rank += (int)(q.x > key) + (int)(q.y > key) + (int)(q.z > key) + (int)(q.w > key);
+    }
+    if (rank < kj) cand[j * KMAX + rank] = key;
+  }
+  if (t == 0) cand_cnt[j] = min(nz, kj);
+  if (ready) {  // publish: every wave's stores drained at the barrier, then one agent-scope release
+    __syncthreads();
+    if (t == 0) {
+      __hip_atomic_fetch_add(ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      if (j == 0 && fstamp) fstamp[1] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
 }
 
 // --- resolve: one wavefront replays the batch sequentially -------------------------------------
@@ -1972,28 +2073,46 @@ __device__ __forceinline__ int hash_of(int node) { return (int)(((uint32_t)node 
 
 // NUMA: nodes may carry NUMA topology policies — changed nodes re-read their zones (patched by this
 // replay's Reserves) from the NUMA SoA, and numa_alloc[pod][2*id + r] receives each pod's allocation.
+struct ResLds {
+  uint32_t cand[MAX_BATCH * KMAX];
+  int16_t cand_slot[MAX_BATCH * KMAX];
+  int32_t hkey[HASH_SLOTS];
+  int16_t hval[HASH_SLOTS];
+  LdsRow row[RES_SLOTS];
+  int32_t slot_node[RES_SLOTS];
+  uint8_t changed[RES_SLOTS];
+  DevPod pod[MAX_BATCH];
+  int32_t cnt[MAX_BATCH];
+  int32_t nslots;
+};
+
 template <bool DS, bool NUMA, bool QUOTA>
-__global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(SoA s, const DevPod* __restrict__ pods, int32_t* __restrict__ batch_base,
-                                                int batch_pods, KArgs k, const uint32_t* __restrict__ cand,
-                                                const int32_t* __restrict__ cand_cnt, int32_t* __restrict__ chosen,
-                                                int32_t* __restrict__ chosen_score, int32_t global_offset,
-                                                uint64_t* __restrict__ stamps, uint64_t* __restrict__ pstamps,
-                                                int batch_index, uint64_t* __restrict__ dev_alloc,
-                                                int64_t* __restrict__ numa_alloc) {
+__device__ __forceinline__ void replay_batch(ResLds& L, const SoA& s, const int base, const int B, const KArgs& k,
+                                             int32_t* __restrict__ chosen, int32_t* __restrict__ chosen_score,
+                                             int32_t global_offset, uint64_t* __restrict__ stamps, int batch_index,
+                                             uint64_t* __restrict__ dev_alloc, int64_t* __restrict__ numa_alloc);
+
+// One batch: prologue on every thread of the workgroup, replay on wave 0 (the other waves skip it).
+template <bool DS, bool NUMA, bool QUOTA>
+__device__ __forceinline__ void resolve_batch(ResLds& L, const SoA& s, const DevPod* __restrict__ pods, const int base,
+                                              const int batch_pods, const KArgs& k, const uint32_t* __restrict__ cand,
+                                              const int32_t* __restrict__ cand_cnt, int32_t* __restrict__ chosen,
+                                              int32_t* __restrict__ chosen_score, int32_t global_offset,
+                                              uint64_t* __restrict__ stamps, uint64_t* __restrict__ pstamps,
+                                              int batch_index, uint64_t* __restrict__ dev_alloc,
+                                              int64_t* __restrict__ numa_alloc) {
   const int tid = threadIdx.x;
   if (tid == 0) pstamps[8 * batch_index] = __builtin_amdgcn_s_memrealtime();
-  __shared__ uint32_t s_cand[MAX_BATCH * KMAX];
-  __shared__ int16_t s_cand_slot[MAX_BATCH * KMAX];
-  __shared__ int32_t s_hkey[HASH_SLOTS];
-  __shared__ int16_t s_hval[HASH_SLOTS];
-  __shared__ LdsRow s_row[RES_SLOTS];
-  __shared__ int32_t s_slot_node[RES_SLOTS];
-  __shared__ uint8_t s_changed[RES_SLOTS];
-  __shared__ DevPod s_pod[MAX_BATCH];
-  __shared__ int32_t s_cnt[MAX_BATCH];
-  __shared__ int32_t s_nslots;
-  const int lane = tid & 63;
-  const int base = *batch_base;
+  uint32_t* const s_cand = L.cand;
+  int16_t* const s_cand_slot = L.cand_slot;
+  int32_t* const s_hkey = L.hkey;
+  int16_t* const s_hval = L.hval;
+  LdsRow* const s_row = L.row;
+  int32_t* const s_slot_node = L.slot_node;
+  uint8_t* const s_changed = L.changed;
+  DevPod* const s_pod = L.pod;
+  int32_t* const s_cnt = L.cnt;
+  int32_t& s_nslots = L.nslots;
   const int B = batch_pods;
 
   // ---- prologue (all RES_THREADS threads): candidates, distinct-node slots, row prefetch ----
@@ -2092,6 +2211,28 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(SoA s, const De
   __syncthreads();
   if (tid == 0) pstamps[8 * batch_index + 4] = __builtin_amdgcn_s_memrealtime();
   if (tid >= 64) return;  // the replay is one wavefront: wave-level ordering only from here on
+  // the next batch's eval waves may share this SIMD (pipelined schedule): the replay issues first
+  __builtin_amdgcn_s_setprio(3);
+  replay_batch<DS, NUMA, QUOTA>(L, s, base, B, k, chosen, chosen_score, global_offset, stamps, batch_index, dev_alloc,
+                                numa_alloc);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+// The sequential replay of one batch (wave 0).
+template <bool DS, bool NUMA, bool QUOTA>
+__device__ __forceinline__ void replay_batch(ResLds& L, const SoA& s, const int base, const int B, const KArgs& k,
+                                             int32_t* __restrict__ chosen, int32_t* __restrict__ chosen_score,
+                                             int32_t global_offset, uint64_t* __restrict__ stamps, int batch_index,
+                                             uint64_t* __restrict__ dev_alloc, int64_t* __restrict__ numa_alloc) {
+  const uint32_t* const s_cand = L.cand;
+  const int16_t* const s_cand_slot = L.cand_slot;
+  int32_t* const s_hkey = L.hkey;
+  int16_t* const s_hval = L.hval;
+  const LdsRow* const s_row = L.row;
+  int32_t* const s_slot_node = L.slot_node;
+  uint8_t* const s_changed = L.changed;
+  const DevPod* const s_pod = L.pod;
+  const int lane = threadIdx.x & 63;
 
   // ---- sequential replay of the batch ----
   // Lane c owns the c-th node changed in this batch: its row lives in that lane's registers, so the
@@ -2266,9 +2407,51 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(SoA s, const De
     f[(F_NREQ + 0) * st] = mine.nreq[0];
     f[(F_NREQ + 1) * st] = mine.nreq[1];
   }
-  if (lane == 0) {
-    *batch_base = base + B;
-    stamps[batch_index + 1] = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0) stamps[batch_index + 1] = __builtin_amdgcn_s_memrealtime();
+}
+
+template <bool DS, bool NUMA, bool QUOTA>
+__global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(SoA s, const DevPod* __restrict__ pods, const int32_t* __restrict__ batch_base,
+                                                int batch_pods, KArgs k, const uint32_t* __restrict__ cand,
+                                                const int32_t* __restrict__ cand_cnt, int32_t* __restrict__ chosen,
+                                                int32_t* __restrict__ chosen_score, int32_t global_offset,
+                                                uint64_t* __restrict__ stamps, uint64_t* __restrict__ pstamps,
+                                                int batch_index, uint64_t* __restrict__ dev_alloc,
+                                                int64_t* __restrict__ numa_alloc) {
+  __shared__ ResLds L;
+  resolve_batch<DS, NUMA, QUOTA>(L, s, pods, *batch_base, batch_pods, k, cand, cand_cnt, chosen, chosen_score,
+                                 global_offset, stamps, pstamps, batch_index, dev_alloc, numa_alloc);
+}
+
+// Persistent Reserve chain of a run of pipelined plain batches [b0, b0 + nb): one
+// workgroup for the whole run, so no kernel boundary or cross-stream event sits between two batches.
+// Per batch: wait until k_fixup published every pod's exact list (ready[b] == pods of b), resolve it,
+// then publish done[b] (rows, placements) with an agent-scope release for the fixup of batch b+1 and
+// the eval of batch b+2.  Every wait is bounded (wait_at_least); on a timeout the run stops and the
+// error word tells the host.
+template <bool QUOTA>
+__global__ __launch_bounds__(res_threads<false>()) void k_resolve_run(SoA s, const DevPod* __restrict__ pods,
+                                                                      const int32_t* __restrict__ bases, int b0, int nb,
+                                                                      KArgs k, const uint32_t* __restrict__ cand,
+                                                                      const int32_t* __restrict__ cand_cnt,
+                                                                      int32_t* __restrict__ chosen,
+                                                                      int32_t* __restrict__ chosen_score, int32_t global_offset,
+                                                                      uint64_t* __restrict__ stamps,
+                                                                      uint64_t* __restrict__ pstamps,
+                                                                      uint64_t* __restrict__ dev_alloc,
+                                                                      const int32_t* __restrict__ ready,
+                                                                      int32_t* __restrict__ done, int32_t* __restrict__ err) {
+  __shared__ ResLds L;
+  __shared__ int32_t s_ok;
+  for (int b = b0; b < b0 + nb; b++) {
+    const int base = bases[b], B = bases[b + 1] - bases[b];
+    if (threadIdx.x == 0) s_ok = wait_at_least(ready + b, B, err);
+    __syncthreads();
+    if (!s_ok) return;
+    resolve_batch<false, false, QUOTA>(L, s, pods, base, B, k, cand, cand_cnt, chosen, chosen_score, global_offset,
+                                       stamps, pstamps, b, dev_alloc, nullptr);
+    __syncthreads();  // wave 0's replay, row write-back and placements are done (drained at the barrier)
+    if (threadIdx.x == 0) __hip_atomic_store(done + b, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -2427,7 +2610,7 @@ __device__ void cpuset_commit(const SoA& s, int64_t node, const DevPod& pod, Acc
 // cpuset; a failed Allocate fails Reserve and the pod stays unplaced), DeviceShare.  One thread: the
 // accumulator is sequential (sorted lists, greedy takes).  NUMA: nodes may carry NUMA policies.
 template <bool DS, bool NUMA>
-__global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __restrict__ pods, int32_t* __restrict__ batch_base,
+__global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __restrict__ pods, const int32_t* __restrict__ batch_base,
                                                        KArgs k, const uint32_t* __restrict__ cand,
                                                        const int32_t* __restrict__ cand_cnt, int32_t* __restrict__ chosen,
                                                        int32_t* __restrict__ chosen_score, int32_t global_offset,
@@ -2533,7 +2716,6 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
   dev_alloc[base] = alloc;
   for (int q = 0; q < 4; q++) cpusets[(int64_t)base * 4 + q] = set[q];
   for (int u = 0; u < 6; u++) pstamps[8 * batch_index + u] = t0;  // no prologue: all "replay"
-  *batch_base = base + 1;
   stamps[batch_index + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -2558,7 +2740,9 @@ struct DeviceState {
   uint16_t* d_scores = nullptr;  // [MAX_BATCH][capacity]
   uint32_t* d_cand = nullptr;    // [MAX_BATCH][KMAX]
   int32_t* d_cand_cnt = nullptr;
-  int32_t* d_batch_base = nullptr;
+  int32_t* d_batch_base = nullptr;  // a zero word (batch base of the parity / bench launches)
+  int32_t* d_sched = nullptr;       // ke_schedule bookkeeping: batch bases, hand-off flags, fixup stamps
+  int64_t sched_cap = 0;            // bytes
   int32_t* d_chosen = nullptr;
   int32_t* d_chosen_score = nullptr;
   uint64_t* d_stamps = nullptr;
@@ -2599,6 +2783,15 @@ struct DeviceState {
   uint64_t* d_cpusets = nullptr;   // [n_pods][4] cpuset of each pod (ke_schedule)
   int64_t cpusets_cap = 0;         // bytes
   uint8_t* d_aff = nullptr;        // [capacity] NUMA affinity per node of a singleton batch's eval
+  // pipelined schedule: eval + select run on `estream` one batch ahead of the Reserve chain on `stream`
+  hipStream_t estream = nullptr;
+  uint32_t* d_stale = nullptr;      // [2][MAX_BATCH][KSTALE] stale-snapshot candidate lists
+  int32_t* d_stale_cnt = nullptr;   // [2][MAX_BATCH]
+  static constexpr int EV_RING = 8;
+  hipEvent_t ev_res[EV_RING] = {};  // a batch's Reserve done (stream)
+  hipEvent_t ev_sel[EV_RING] = {};  // a batch's candidate lists done (estream)
+  hipEvent_t ev_start = nullptr;
+  bool pipeline = true;             // ke_set_pipeline
 };
 
 // Contiguous node range of shard `rank`: 512-aligned chunks (k_select's 16-B loads stay aligned).
@@ -2630,7 +2823,15 @@ int device_create(Context* ctx) {
   ctx->dev = d;
   d->device = ctx->cfg.device_ordinal;
   HIP_OK(hipSetDevice(d->device));
-  HIP_OK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+  int prio_lo = 0, prio_hi = 0;  // the Reserve chain gets the higher queue priority
+  HIP_OK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+  HIP_OK(hipStreamCreateWithPriority(&d->stream, hipStreamNonBlocking, prio_hi));
+  HIP_OK(hipStreamCreateWithPriority(&d->estream, hipStreamNonBlocking, prio_lo));
+  for (int e = 0; e < DeviceState::EV_RING; e++) {
+    HIP_OK(hipEventCreateWithFlags(&d->ev_res[e], hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&d->ev_sel[e], hipEventDisableTiming));
+  }
+  HIP_OK(hipEventCreateWithFlags(&d->ev_start, hipEventDisableTiming));
   d->capacity = ((int64_t)ctx->cfg.node_capacity + 255) & ~255LL;
   d->soa.stride = d->capacity;
   HIP_OK(hipMalloc(&d->soa.f, sizeof(int64_t) * NUM_I64_FIELDS * d->capacity));
@@ -2641,6 +2842,9 @@ int device_create(Context* ctx) {
   HIP_OK(hipMalloc(&d->d_cand, sizeof(uint32_t) * MAX_BATCH * KMAX));
   HIP_OK(hipMalloc(&d->d_cand_cnt, sizeof(int32_t) * MAX_BATCH));
   HIP_OK(hipMalloc(&d->d_batch_base, sizeof(int32_t)));
+  HIP_OK(hipMemsetAsync(d->d_batch_base, 0, sizeof(int32_t), d->stream));
+  HIP_OK(hipMalloc(&d->d_stale, sizeof(uint32_t) * 2 * MAX_BATCH * KSTALE));
+  HIP_OK(hipMalloc(&d->d_stale_cnt, sizeof(int32_t) * 2 * MAX_BATCH));
   HIP_OK(hipMalloc(&d->d_dsraw, sizeof(uint16_t) * d->capacity));
   HIP_OK(hipMalloc(&d->d_dsmax, sizeof(uint32_t) * MAX_BATCH));
   HIP_OK(hipMalloc(&d->d_aff, d->capacity));
@@ -2659,9 +2863,17 @@ void device_destroy(Context* ctx) {
                   d->d_stamps,  d->d_parity, d->d_best,       d->d_gath,         d->soa.ds,   d->soa.dsm,
                   d->d_dsraw,   d->d_dsmax,  d->d_devalloc,   d->d_dsrows,       d->soa.nf,   d->soa.nm,
                   d->d_numaalloc, d->d_numarows, d->d_defer, d->d_defer_cnt, d->soa.cs, d->soa.cpu,
-                  d->d_cpurows, d->d_cpusets, d->d_aff, d->soa.qt, d->soa.qm};
+                  d->d_cpurows, d->d_cpusets, d->d_aff, d->soa.qt, d->soa.qm, d->d_sched, d->d_stale,
+                  d->d_stale_cnt};
+  if (d->estream) (void)hipStreamSynchronize(d->estream);
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  for (int e = 0; e < DeviceState::EV_RING; e++) {
+    if (d->ev_res[e]) (void)hipEventDestroy(d->ev_res[e]);
+    if (d->ev_sel[e]) (void)hipEventDestroy(d->ev_sel[e]);
+  }
+  if (d->ev_start) (void)hipEventDestroy(d->ev_start);
+  if (d->estream) (void)hipStreamDestroy(d->estream);
   if (d->stream) (void)hipStreamDestroy(d->stream);
   delete d;
   ctx->dev = nullptr;
@@ -2737,8 +2949,8 @@ int device_shard_init(Context* ctx, int rank, int world, const uint8_t* id) {
     RCCL_OK(ncclCommDestroy(d->comm));
     d->comm = nullptr;
   }
-  if (!d->d_gath) HIP_OK(hipMalloc(&d->d_gath, sizeof(uint32_t) * GATH_WORDS * MAX_WORLD));
-  HIP_OK(hipMemsetAsync(d->d_gath, 0, sizeof(uint32_t) * GATH_WORDS * MAX_WORLD, d->stream));
+  if (!d->d_gath) HIP_OK(hipMalloc(&d->d_gath, sizeof(uint32_t) * GATH_WORDS_MAX * MAX_WORLD));
+  HIP_OK(hipMemsetAsync(d->d_gath, 0, sizeof(uint32_t) * GATH_WORDS_MAX * MAX_WORLD, d->stream));
   HIP_OK(hipStreamSynchronize(d->stream));
   d->world = world;
   d->rank = rank;
@@ -3105,33 +3317,77 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   }
   const int N = ctx->n_nodes;
   const int ppb = 8;
-  HIP_OK(hipMemsetAsync(d->d_batch_base, 0, sizeof(int32_t), d->stream));
+  // first pod of every batch and the end (the kernels' batch base pointer is d_bases + b)
+  std::vector<int32_t> bases((size_t)n_batches + 1);
+  for (int b = 0, p = 0; b <= n_batches; b++) {
+    bases[b] = p;
+    if (b < n_batches) p += batches[b].pods;
+  }
+  // pipelined runs: maximal stretches of plain batches (no DeviceShare / cpuset pod) in a
+  // context without NUMA policies; run_end[b] > 0 marks the first batch of a run and holds its end
+  auto eligible = [&](int b) { return d->pipeline && N > 0 && !numa && !batches[b].ds && !batches[b].cpu; };
+  std::vector<int> run_end((size_t)n_batches, 0);
+  for (int b = 0; b < n_batches;) {
+    if (!eligible(b)) {
+      b++;
+      continue;
+    }
+    int e = b;
+    while (e < n_batches && eligible(e)) e++;
+    run_end[b] = e;
+    b = e;
+  }
+  // device: bases [n+1], ready [n], done [n], error word; fixup stamps [2n]
+  const int64_t sched_words = 3 * ((int64_t)n_batches + 1) + 1;
+  rc = ensure((void**)&d->d_sched, &d->sched_cap, sizeof(int32_t) * sched_words + sizeof(uint64_t) * 2 * n_batches + 8);
+  if (rc) return rc;
+  int32_t* d_bases = d->d_sched;
+  int32_t* d_ready = d_bases + n_batches + 1;
+  int32_t* d_done = d_ready + n_batches + 1;
+  int32_t* d_err = d_done + n_batches + 1;
+  uint64_t* d_fst = reinterpret_cast<uint64_t*>(d->d_sched + ((sched_words + 1) & ~1LL));
+  HIP_OK(hipMemcpyAsync(d_bases, bases.data(), sizeof(int32_t) * (n_batches + 1), hipMemcpyHostToDevice, d->stream));
+  HIP_OK(hipMemsetAsync(d_ready, 0, sizeof(int32_t) * (sched_words - n_batches - 1), d->stream));
+  HIP_OK(hipMemsetAsync(d_fst, 0, sizeof(uint64_t) * 2 * n_batches, d->stream));
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   HIP_OK(hipEventRecord(e0, d->stream));
   hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, d->stream, d->d_stamps);
-  // sampled per-kernel HIP event pairs (ke_set_profiling)
+  HIP_OK(hipEventRecord(d->ev_start, d->stream));
+  HIP_OK(hipStreamWaitEvent(d->estream, d->ev_start, 0));
+  // sampled per-kernel HIP event pairs (ke_set_profiling) on the eval stream: eval, select
+  constexpr int PE = 3;
   const int every = d->profile_every;
   std::vector<hipEvent_t> ev;
   if (every > 0) {
     const int samples = (n_batches + every - 1) / every;
-    ev.resize((size_t)samples * 4);
+    ev.resize((size_t)samples * PE);
     for (auto& e : ev) HIP_OK(hipEventCreate(&e));
   }
   const bool sharded = d->world > 1 || d->comm;
-  for (int b = 0; b < n_batches; b++) {
+  uint64_t* estamps = d->d_stamps + 9 * ((int64_t)n_pods + 2);  // eval start of each batch
+  constexpr int R = DeviceState::EV_RING;
+  int n_pipelined = 0;
+  // Batch b's eval + candidate lists on estream.  pipe: stale top-(k_j + KMAX) lists into the run's
+  // stale buffer (k_fixup makes them exact); else the exact top-k_j lists straight into d_cand.
+  auto eval_select = [&](int b, bool pipe) -> int {
     const int bp = batches[b].pods;
     const bool ds = batches[b].ds, cpu = batches[b].cpu;
     const bool prof = every > 0 && b % every == 0;
-    hipEvent_t* pe = prof ? &ev[(size_t)(b / every) * 4] : nullptr;
-    if (prof) HIP_OK(hipEventRecord(pe[0], d->stream));
+    hipEvent_t* pe = prof ? &ev[(size_t)(b / every) * PE] : nullptr;
+    const int32_t* bbase = d_bases + b;
+    hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, d->estream, estamps + b);
+    if (prof) HIP_OK(hipEventRecord(pe[0], d->estream));
+    const int L = pipe ? KSTALE : KMAX, kext = pipe ? KMAX : 0;
+    uint32_t* lists = pipe ? d->d_stale + (size_t)(b & 1) * MAX_BATCH * KSTALE : d->d_cand;
+    int32_t* lists_cnt = pipe ? d->d_stale_cnt + (b & 1) * MAX_BATCH : d->d_cand_cnt;
     if (N > 0) {
       // this rank's node range (unsharded and loopback: every node)
       int lo = 0, hi = N;
       if (sharded && !d->loopback) shard_range(N, d->rank, d->world, &lo, &hi);
       const bool single = bp == 1;
-      if (ds) HIP_OK(hipMemsetAsync(d->d_dsmax, 0, sizeof(uint32_t), d->stream));  // the eval's atomicMax target
+      if (ds) HIP_OK(hipMemsetAsync(d->d_dsmax, 0, sizeof(uint32_t), d->estream));  // the eval's atomicMax target
       if (hi > lo) {
         // a singleton batch has one pod's worth of lanes: single-wave blocks spread it over every CU
         const int eb = single ? 64 : EVAL_BLOCK;
@@ -3141,52 +3397,93 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                         : ds ? (numa ? k_eval_batch<true, true, false> : k_eval_batch<true, false, false>)
                              : (numa ? k_eval_batch<false, true, false> : k_eval_batch<false, false, false>);
         uint32_t* dcnt = numa ? d->d_defer_cnt + b : nullptr;
-        hipLaunchKernelGGL(eval, grid, dim3(eb), 0, d->stream, d->soa, lo, hi, d->d_pods, d->d_batch_base, bp,
+        hipLaunchKernelGGL(eval, grid, dim3(eb), 0, d->estream, d->soa, lo, hi, d->d_pods, bbase, bp,
                            ppb, k, d->d_scores, d->capacity, d->d_dsraw, d->d_defer, dcnt, d->d_aff, d->d_dsmax);
         if (numa && !ds)  // DeviceShare pods never meet a NUMA policy: nothing deferred in their batches
           hipLaunchKernelGGL((cpu ? k_numa_fallback<false, true> : k_numa_fallback<false, false>), dim3(FALLBACK_BLOCKS),
-                             dim3(64), 0, d->stream, d->soa, d->d_pods,
-                             d->d_batch_base, k, d->d_defer, dcnt, d->d_scores, d->capacity, 0, nullptr, nullptr,
+                             dim3(64), 0, d->estream, d->soa, d->d_pods,
+                             bbase, k, d->d_defer, dcnt, d->d_scores, d->capacity, 0, nullptr, nullptr,
                              nullptr, nullptr, nullptr, nullptr, nullptr, cpu ? d->d_aff : nullptr);
       }
       if (ds && sharded && !d->loopback)  // DefaultNormalizeScore's max over the feasible nodes of all ranks
-        RCCL_OK(ncclAllReduce(d->d_dsmax, d->d_dsmax, 1, ncclUint32, ncclMax, d->comm, d->stream));
-      if (prof) HIP_OK(hipEventRecord(pe[1], d->stream));
+        RCCL_OK(ncclAllReduce(d->d_dsmax, d->d_dsmax, 1, ncclUint32, ncclMax, d->comm, d->estream));
+      if (prof) HIP_OK(hipEventRecord(pe[1], d->estream));
       auto select = [&](int slo, int shi, uint32_t* cand, int32_t* cnt) {
         if (ds)
-          hipLaunchKernelGGL(k_select<true>, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, d->stream, d->d_scores,
-                             d->capacity, slo, shi, cand, cnt, d->d_dsraw, d->d_dsmax, k.wp_ds);
+          hipLaunchKernelGGL(k_select<true>, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, d->estream, d->d_scores,
+                             d->capacity, slo, shi, cand, cnt, d->d_dsraw, d->d_dsmax, k.wp_ds, kext, L);
         else
-          hipLaunchKernelGGL(k_select<false>, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, d->stream, d->d_scores,
-                             d->capacity, slo, shi, cand, cnt, d->d_dsraw, d->d_dsmax, k.wp_ds);
+          hipLaunchKernelGGL(k_select<false>, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, d->estream, d->d_scores,
+                             d->capacity, slo, shi, cand, cnt, d->d_dsraw, d->d_dsmax, k.wp_ds, kext, L);
       };
-      if (!sharded && single) {  // selectHost of one pod: a grid-wide argmax
-        HIP_OK(hipMemsetAsync(d->d_cand, 0, sizeof(uint32_t), d->stream));
+      if (!sharded && single && !pipe) {  // selectHost of one pod: a grid-wide argmax
+        HIP_OK(hipMemsetAsync(d->d_cand, 0, sizeof(uint32_t), d->estream));
         hipLaunchKernelGGL((ds ? k_argmax1<true> : k_argmax1<false>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
-                           d->stream, d->d_scores, 0, N, d->d_dsraw, d->d_dsmax, k.wp_ds, d->d_cand, d->d_cand_cnt);
+                           d->estream, d->d_scores, 0, N, d->d_dsraw, d->d_dsmax, k.wp_ds, d->d_cand, d->d_cand_cnt);
       } else if (!sharded) {
-        select(0, N, d->d_cand, d->d_cand_cnt);
+        select(0, N, lists, lists_cnt);
       } else {
         // node-sharded: per-shard top-k_j, all-gather, merge
+        const int gw = gath_words(L);
         for (int r = 0; r < d->world; r++) {
           if (!d->loopback && r != d->rank) continue;
           int slo, shi;
           shard_range(N, r, d->world, &slo, &shi);
-          uint32_t* blk = d->d_gath + (int64_t)r * GATH_WORDS;
-          select(slo, shi, blk, reinterpret_cast<int32_t*>(blk + MAX_BATCH * KMAX));
+          uint32_t* blk = d->d_gath + (int64_t)r * gw;
+          select(slo, shi, blk, reinterpret_cast<int32_t*>(blk + MAX_BATCH * L));
         }
         if (!d->loopback) {
-          uint32_t* mine = d->d_gath + (int64_t)d->rank * GATH_WORDS;  // in place: send = own block of recv
-          RCCL_OK(ncclAllGather(mine, d->d_gath, GATH_WORDS, ncclUint32, d->comm, d->stream));
+          uint32_t* mine = d->d_gath + (int64_t)d->rank * gw;  // in place: send = own block of recv
+          RCCL_OK(ncclAllGather(mine, d->d_gath, gw, ncclUint32, d->comm, d->estream));
         }
-        hipLaunchKernelGGL(k_merge, dim3((unsigned)bp), dim3(MERGE_BLOCK), 0, d->stream, d->d_gath, d->world,
-                           d->d_cand, d->d_cand_cnt);
+        hipLaunchKernelGGL(k_merge, dim3((unsigned)bp), dim3(MERGE_BLOCK), 0, d->estream, d->d_gath, d->world, L, kext,
+                           lists, lists_cnt);
       }
     } else {
-      if (prof) HIP_OK(hipEventRecord(pe[1], d->stream));
-      HIP_OK(hipMemsetAsync(d->d_cand_cnt, 0, sizeof(int32_t) * MAX_BATCH, d->stream));
+      if (prof) HIP_OK(hipEventRecord(pe[1], d->estream));
+      HIP_OK(hipMemsetAsync(lists_cnt, 0, sizeof(int32_t) * MAX_BATCH, d->estream));
     }
-    if (prof) HIP_OK(hipEventRecord(pe[2], d->stream));
+    if (prof) HIP_OK(hipEventRecord(pe[2], d->estream));
+    return KE_OK;
+  };
+  // Two streams (pipelining).  A run of plain batches: one persistent k_resolve_run on
+  // `stream` resolves them all; on `estream` batch b's eval + select run while batch b-1 is being
+  // resolved (they see the Reserves of batches <= b-2), and k_fixup waits for batch b-1's done flag,
+  // re-evaluates the nodes it chose and publishes the exact lists.  Any other batch (DeviceShare /
+  // cpuset singletons, NUMA-policy contexts, pipeline off) is serial: its eval waits for the previous
+  // batch's Reserve (HIP events), its lists are exact, its Reserve kernel waits for its lists.
+  const auto host_t0 = std::chrono::steady_clock::now();
+  for (int b = 0; b < n_batches;) {
+    if (run_end[b] > 0) {
+      const int r0 = b, e = run_end[b];
+      hipLaunchKernelGGL((quota ? k_resolve_run<true> : k_resolve_run<false>), dim3(1), dim3(res_threads<false>()), 0,
+                         d->stream, d->soa, d->d_pods, d_bases, r0, e - r0, k, d->d_cand, d->d_cand_cnt, d->d_chosen,
+                         d->d_chosen_score, ctx->cfg.global_node_offset, d->d_stamps, d->d_stamps + (n_pods + 2),
+                         d->d_devalloc, d_ready, d_done, d_err);
+      if (r0 > 0) HIP_OK(hipStreamWaitEvent(d->estream, d->ev_res[(r0 - 1) % R], 0));
+      for (int q = r0; q < e; q++) {
+        rc = eval_select(q, true);
+        if (rc) return rc;
+        const bool first = q == r0;
+        hipLaunchKernelGGL(k_fixup, dim3((unsigned)batches[q].pods), dim3(FIX_BLOCK), 0, d->estream, d->soa, d->d_pods,
+                           d_bases + q, k, d->d_stale + (size_t)(q & 1) * MAX_BATCH * KSTALE,
+                           d->d_stale_cnt + (q & 1) * MAX_BATCH, first ? nullptr : d->d_chosen + bases[q - 1],
+                           first ? 0 : batches[q - 1].pods, ctx->cfg.global_node_offset, d->d_cand, d->d_cand_cnt,
+                           d_done, first ? -1 : q - 1, d_ready + q, d_err, d_fst + 2 * q);
+      }
+      HIP_OK(hipEventRecord(d->ev_res[(e - 1) % R], d->stream));
+      n_pipelined += e - r0;
+      b = e;
+      continue;
+    }
+    const int bp = batches[b].pods;
+    const bool ds = batches[b].ds, cpu = batches[b].cpu;
+    const int32_t* bbase = d_bases + b;
+    if (b > 0) HIP_OK(hipStreamWaitEvent(d->estream, d->ev_res[(b - 1) % R], 0));
+    rc = eval_select(b, false);
+    if (rc) return rc;
+    HIP_OK(hipEventRecord(d->ev_sel[b % R], d->estream));
+    HIP_OK(hipStreamWaitEvent(d->stream, d->ev_sel[b % R], 0));
     if (bp == 1) {  // one pod: the single-node Reserve (cpuset accumulator when it binds)
       int elo = 0, ehi = 0;  // nodes whose affinities this batch's eval stored in d_aff (binding batches)
       if (cpu && numa) {
@@ -3196,7 +3493,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       hipLaunchKernelGGL((ds ? (numa ? k_cpuset_reserve<true, true> : k_cpuset_reserve<true, false>)
                              : (numa ? k_cpuset_reserve<false, true> : k_cpuset_reserve<false, false>)),
                          dim3(1), dim3(64), 0, d->stream, d->soa,
-                         d->d_pods, d->d_batch_base, k, d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score,
+                         d->d_pods, bbase, k, d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score,
                          ctx->cfg.global_node_offset, d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc,
                          numa ? d->d_numaalloc : nullptr, d->d_cpusets,
                          d->d_aff, elo, ehi);
@@ -3205,13 +3502,15 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                                  : (numa ? k_resolve<false, true, true> : k_resolve<false, false, true>))
                            : (ds ? (numa ? k_resolve<true, true, false> : k_resolve<true, false, false>)
                                  : (numa ? k_resolve<false, true, false> : k_resolve<false, false, false>));
-      hipLaunchKernelGGL(resolve, dim3(1), dim3(numa ? res_threads<true>() : res_threads<false>()), 0, d->stream, d->soa, d->d_pods, d->d_batch_base, bp, k,
+      hipLaunchKernelGGL(resolve, dim3(1), dim3(numa ? res_threads<true>() : res_threads<false>()), 0, d->stream, d->soa, d->d_pods, bbase, bp, k,
                          d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score, ctx->cfg.global_node_offset,
                          d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc, d->d_numaalloc);
     }
-    if (prof) HIP_OK(hipEventRecord(pe[3], d->stream));
+    HIP_OK(hipEventRecord(d->ev_res[b % R], d->stream));
+    b++;
   }
   HIP_OK(hipGetLastError());
+  ctx->last_enqueue_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - host_t0).count();
   HIP_OK(hipEventRecord(e1, d->stream));
   HIP_OK(hipMemcpyAsync(chosen, d->d_chosen, out_bytes, hipMemcpyDeviceToHost, d->stream));
   if (score) HIP_OK(hipMemcpyAsync(score, d->d_chosen_score, out_bytes, hipMemcpyDeviceToHost, d->stream));
@@ -3227,24 +3526,41 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     HIP_OK(hipMemcpyAsync(ctx->last_numa_alloc.data(), d->d_numaalloc, sizeof(int64_t) * 16 * n_pods,
                           hipMemcpyDeviceToHost, d->stream));
   }
-  std::vector<uint64_t> st((size_t)n_batches + 1), pst(8 * (size_t)n_batches);
+  std::vector<uint64_t> st((size_t)n_batches + 1), pst(8 * (size_t)n_batches), est((size_t)n_batches),
+      fst(2 * (size_t)n_batches);
+  int32_t herr = 0;
+  HIP_OK(hipMemcpyAsync(&herr, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, d->stream));
+  HIP_OK(hipMemcpyAsync(fst.data(), d_fst, sizeof(uint64_t) * 2 * n_batches, hipMemcpyDeviceToHost, d->stream));
   std::vector<uint32_t> dcnt(numa ? (size_t)n_batches : 0);
   if (numa)
     HIP_OK(hipMemcpyAsync(dcnt.data(), d->d_defer_cnt, sizeof(uint32_t) * n_batches, hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipMemcpyAsync(st.data(), d->d_stamps, sizeof(uint64_t) * (n_batches + 1), hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipMemcpyAsync(pst.data(), d->d_stamps + (n_pods + 2), sizeof(uint64_t) * 8 * n_batches,
                         hipMemcpyDeviceToHost, d->stream));
+  HIP_OK(hipMemcpyAsync(est.data(), estamps, sizeof(uint64_t) * n_batches, hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipStreamSynchronize(d->stream));
+  HIP_OK(hipStreamSynchronize(d->estream));
+  if (herr) {
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    return fail(KE_ERR_DEVICE, "pipelined schedule: a device-side hand-off timed out (placements invalid)");
+  }
   float ms = 0;
   HIP_OK(hipEventElapsedTime(&ms, e0, e1));
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   ctx->last_total_ms = ms;
+  ctx->last_pipelined = n_pipelined;
   // s_memrealtime ticks -> ms, calibrated against the event-timed span of the whole queue
   const double span = (double)(st[n_batches] - st[0]);
   const double ms_per_tick = span > 0 ? ms / span : 1e-5;
+  // a pod's latency: from its batch's eval start (dequeue) to the end of its batch's Reserve
   ctx->last_batch_ms.resize(n_batches);
-  for (int b = 0; b < n_batches; b++) ctx->last_batch_ms[b] = (double)(st[b + 1] - st[b]) * ms_per_tick;
+  for (int b = 0; b < n_batches; b++) {
+    const uint64_t t0 = std::max(std::min(est[b], st[b + 1]), st[0]);
+    ctx->last_batch_ms[b] = (double)(st[b + 1] - t0) * ms_per_tick;
+  }
   double pro = 0, loop = 0;  // resolve kernel: prologue (candidate/row staging) vs sequential replay
   double ph[6] = {0, 0, 0, 0, 0, 0};  // init, cand copy, hash insert, slot lookup, row gather, replay
   for (int b = 0; b < n_batches; b++) {
@@ -3263,24 +3579,45 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   for (int i = 0; i < 6; i++) ctx->kstat_resolve_phase_ms[i] = ph[i] * ms_per_tick / n_batches;
   ctx->kstat_numa_deferred = 0;
   for (uint32_t c : dcnt) ctx->kstat_numa_deferred += c;
+  // per-batch Reserve time from the in-kernel stamps (start of the batch's prologue -> end of its
+  // replay); hand-off = end of batch b-1's replay -> start of batch b (run batches after the first);
+  // fixup = k_fixup's workgroup 0 from its wait to its publish
+  double res_sum = 0, ho_sum = 0, fx_sum = 0;
+  int ho_n = 0, fx_n = 0;
+  for (int b = 0; b < n_batches; b++) {
+    res_sum += (double)(st[b + 1] - pst[8 * (size_t)b]) * ms_per_tick;
+    if (fst[2 * b + 1] > fst[2 * b]) {
+      fx_sum += (double)(fst[2 * b + 1] - fst[2 * b]) * ms_per_tick;
+      fx_n++;
+      if (run_end[b] == 0 && b > 0) {
+        ho_sum += (double)(pst[8 * (size_t)b] - st[b]) * ms_per_tick;
+        ho_n++;
+      }
+    }
+  }
+  ctx->kstat_resolve_ms = n_batches ? res_sum / n_batches : 0;
+  ctx->kstat_fixup_ms = fx_n ? fx_sum / fx_n : 0;
+  ctx->kstat_handoff_ms = ho_n ? ho_sum / ho_n : 0;
   ctx->kstat_samples = 0;
-  ctx->kstat_eval_ms = ctx->kstat_select_ms = ctx->kstat_resolve_ms = 0;
-  for (size_t s = 0; s + 3 < ev.size(); s += 4) {
-    float a = 0, b = 0, c = 0;
+  ctx->kstat_eval_ms = ctx->kstat_select_ms = 0;
+  for (size_t s = 0; s + PE - 1 < ev.size(); s += PE) {
+    float a = 0, b = 0;
     HIP_OK(hipEventElapsedTime(&a, ev[s], ev[s + 1]));
     HIP_OK(hipEventElapsedTime(&b, ev[s + 1], ev[s + 2]));
-    HIP_OK(hipEventElapsedTime(&c, ev[s + 2], ev[s + 3]));
     ctx->kstat_eval_ms += a;
     ctx->kstat_select_ms += b;
-    ctx->kstat_resolve_ms += c;
     ctx->kstat_samples++;
   }
   for (auto& e : ev) (void)hipEventDestroy(e);
   if (ctx->kstat_samples) {
     ctx->kstat_eval_ms /= ctx->kstat_samples;
     ctx->kstat_select_ms /= ctx->kstat_samples;
-    ctx->kstat_resolve_ms /= ctx->kstat_samples;
   }
+  return KE_OK;
+}
+
+int device_set_pipeline(Context* ctx, int32_t on) {
+  ctx->dev->pipeline = on != 0;
   return KE_OK;
 }
 

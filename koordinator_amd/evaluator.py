@@ -211,15 +211,20 @@ class Evaluator:
         self._check(self.lib.ke_debug_numa_deferred(self.h, C.byref(n)))
         return n.value
 
+    def set_pipeline(self, on):
+        """Pipelined schedule (default): batch b's eval + select overlap batch b-1's Reserve replay."""
+        self._check(self.lib.ke_set_pipeline(self.h, 1 if on else 0))
+
     def kernel_stats(self):
-        v = [C.c_double() for _ in range(3)]
-        n = abi.i32()
-        self._check(self.lib.ke_last_kernel_stats(self.h, *[C.byref(x) for x in v], C.byref(n)))
+        ms4 = np.zeros(6, np.float64)
+        n, npipe = abi.i32(), abi.i32()
+        self._check(self.lib.ke_last_kernel_stats_ex(self.h, abi.ptr(ms4), C.byref(n), C.byref(npipe)))
         p, r = C.c_double(), C.c_double()
         self._check(self.lib.ke_last_resolve_split(self.h, C.byref(p), C.byref(r)))
         ph = np.zeros(6, np.float64)
         self._check(self.lib.ke_debug_resolve_phases(self.h, abi.ptr(ph)))
-        return {"eval_ms": v[0].value, "select_ms": v[1].value, "resolve_ms": v[2].value, "samples": n.value,
+        return {"eval_ms": ms4[0], "select_ms": ms4[1], "fixup_ms": ms4[2], "resolve_ms": ms4[3], "samples": n.value,
+                "pipelined_batches": npipe.value, "enqueue_ms": ms4[4], "handoff_ms": ms4[5],
                 "resolve_prologue_ms": p.value, "resolve_replay_ms": r.value,
                 "resolve_phases_ms": dict(zip(["init", "cand_copy", "hash", "lookup", "rows", "replay"],
                                               ph.tolist()))}

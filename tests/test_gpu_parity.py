@@ -204,13 +204,57 @@ def test_schedule_unschedulable_pods(gpu):
 
 
 def test_schedule_large_cluster_prefix(gpu):
-    """BASELINE config 3 cluster (50k nodes): first 400 pods vs the oracle, bit-exact."""
+    """BASELINE config 3 cluster (50k nodes) and queue: first 2048 pods (32 pipelined 64-pod batches)
+    vs the oracle, bit-exact, then the rows the device patched vs a from-scratch host derivation."""
     cl = synth.make_cluster(50_000, synth.BASE_SEED + 3)
-    pods = synth.make_pods(400, synth.BASE_SEED + 103)
+    pods = synth.make_pods(2048, synth.BASE_SEED + 103)
     ev, o = both(synth.config(50_000), cl)
     c1, s1 = ev.schedule(pods, synth.T0)
+    assert ev.kernel_stats()["pipelined_batches"] == 32
     c0, s0 = o.schedule(pods, synth.T0)
     assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    dev, host = ev.debug_rows(synth.T0)
+    assert np.array_equal(dev, host)
+
+
+# ---- pipelined schedule (two streams, stale lists + k_fixup) ---------------------------------------
+@pytest.mark.parametrize("n_nodes,n_pods,seed", [(20_000, 3000, 71), (150, 2500, 72), (40, 1200, 73)])
+def test_pipeline_matches_serial_and_oracle(gpu, n_nodes, n_pods, seed):
+    """Batch b's eval/select against the stale snapshot (batch b-1 still resolving) + k_fixup give the
+    same placements as the serial one-stream schedule and the oracle.  The small clusters make every
+    batch touch most candidate lists (k_fixup's drop-and-re-evaluate path on nearly every pod)."""
+    cl = synth.make_cluster(n_nodes, synth.BASE_SEED + seed)
+    pods = synth.make_pods(n_pods, synth.BASE_SEED + 100 + seed)
+    ev, o = both(synth.config(n_nodes), cl)
+    es = Evaluator(synth.config(n_nodes))
+    synth.load_into(es, cl)
+    es.set_pipeline(False)
+    c1, s1 = ev.schedule(pods, synth.T0)
+    assert ev.kernel_stats()["pipelined_batches"] > 0
+    c2, s2 = es.schedule(pods, synth.T0)
+    assert es.kernel_stats()["pipelined_batches"] == 0
+    assert np.array_equal(c1, c2) and np.array_equal(s1, s2)
+    c0, s0 = o.schedule(pods, synth.T0)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    es.close()
+
+
+@pytest.mark.parametrize("name", ["prod-thresholds", "most-allocated", "amplified"])
+def test_pipeline_with_unschedulable_and_variants(gpu, name):
+    """Pipelined batches whose predecessor placed nothing (chosen -1); MostAllocated scores rise on the
+    touched nodes (nothing in the exactness argument assumes they fall)."""
+    v = VARIANTS[name]
+    cl = synth.make_cluster(64, synth.BASE_SEED + 51, amplified_fraction=v.get("amplified", 0.0))
+    cfg = variant_cfg(64, v)
+    ev, o = both(cfg, cl)
+    huge = model.make_pod(requests={"cpu": "100000", "memory": "1Ti"}, limits={"cpu": "100000", "memory": "1Ti"})
+    pods = synth.make_pods(600, synth.BASE_SEED + 75)
+    hp = np.frombuffer(bytes(huge), dtype=abi.POD_DTYPE)
+    seq = np.concatenate([np.repeat(hp, 64), pods[:200], np.repeat(hp, 70), pods[200:]])
+    c1, s1 = ev.schedule(seq, synth.T0)
+    c0, s0 = o.schedule(seq, synth.T0)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    assert (c1 == -1).sum() >= 64 and ev.kernel_stats()["pipelined_batches"] > 0
 
 
 # ---- node sharding (loopback: every shard's eval/select + k_merge in one context) -----------------
