@@ -6,8 +6,14 @@ pods (bit-exact with one-pod-at-a-time scheduling).  One step = scheduling one s
 (queue / steps pods) against all nodes; `value` = pods x nodes evaluated per second over the timed
 steps.  The node state is resident in HBM before the timed region starts.
 
+roofline: the per-batch pipeline.  The critical path is the Reserve chain (k_resolve_run,
+one workgroup, per-batch time from in-kernel s_memrealtime stamps); eval, select and fixup run beside it
+on the second stream.  `roofline` describes that dominant kernel, `roofline.kernels` every kernel of a
+batch and `roofline.end_to_end` the whole step, each as algorithmic bytes / time against 8 TB/s.
+`traffic` = HBM bytes from a prior rocprofv3 PMC pass of this workload (profiles/r02/pmc_bench.json).
+
 cpu_baseline: the oracle (C restatement of the Go plugins, oracle/) scheduling a prefix of the same
-queue on the host's cores (16 threads = the upstream scheduler's Parallelism) for ~10 s of work.
+queue on the host's cores at 1 thread, 16 threads (upstream Parallelism) and every usable core.
 """
 import argparse
 import json
@@ -23,7 +29,11 @@ sys.path.insert(0, ROOT)
 from koordinator_amd import Evaluator, abi, synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
-DEVPOD_BYTES = 40
+KMAX, KSTALE = 64, 128  # candidate list lengths (ke_kernels.hip)
+CAND_BYTES = 4
+ROW_RECORD = 152  # bytes of a full node row record (ke_types.h Row) staged / published by the Reserve chain
+ROW_PATCH = 10 * 8  # int64 fields a Reserve writes back (fh 4, sa 4, NodeInfo.Requested 2)
+OUT_BYTES = 4 + 4 + 8  # chosen, score, device allocation per pod
 
 
 def parse():
@@ -36,8 +46,7 @@ def parse():
     ap.add_argument("--nodes", type=int, default=None)
     ap.add_argument("--pods", type=int, default=None)
     ap.add_argument("--batch", type=int, default=64)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target host time of the CPU baseline sample")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="host time of each CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true", help="one-stream schedule (A/B of the pipelined one)")
     ap.add_argument("--profile-every", type=int, default=8, help="HIP-event-sample every n-th batch (0 = off)")
@@ -46,38 +55,106 @@ def parse():
     return ap.parse_args()
 
 
+def sizes():
+    lib = abi.load_library()
+    return lib.ke_row_bytes(), lib.ke_pod_record_bytes()
+
+
 def eval_bytes(n_nodes, b):
     """algorithmic bytes of one eval-kernel launch: the node SoA once, the pod batch, the score output"""
-    return n_nodes * abi.load_library().ke_row_bytes() + b * DEVPOD_BYTES + b * n_nodes * 2
+    row, pod = sizes()
+    return n_nodes * row + b * pod + b * n_nodes * 2
 
 
-def pmc_traffic(n_nodes, b):
-    """HBM bytes per k_eval_batch launch from the committed rocprofv3 PMC passes (tools/pmc_summary.py)
-    for this exact workload shape; None when no pass covers it."""
-    f = os.path.join(ROOT, "profiles", "r01", "pmc_eval_traffic.json")
+def batch_bytes(n_nodes, b, staged, changed, pipelined):
+    """algorithmic bytes per batch of each kernel"""
+    row, pod = sizes()
+    L = KSTALE if pipelined else KMAX
+    return {
+        "k_eval_batch": eval_bytes(n_nodes, b),
+        "k_select": b * n_nodes * 2 + b * (L + 1) * CAND_BYTES,
+        "k_fixup": (b * ((L + 1) * CAND_BYTES + pod + (KMAX + 1) * CAND_BYTES) + changed * ROW_RECORD) if pipelined else 0,
+        "k_resolve": b * ((KMAX + 1) * CAND_BYTES + pod + OUT_BYTES) + staged * row + changed * (ROW_PATCH + ROW_RECORD),
+    }
+
+
+def pmc_traffic(tag):
+    """HBM bytes per batch by kernel from the committed PMC pass (tools/pmc_bench.sh) of this workload."""
+    f = os.path.join(ROOT, "profiles", "r02", "pmc_bench.json")
     if not os.path.exists(f):
-        return None, None
+        return {}, None
     d = json.load(open(f))
-    e = d["shapes"].get(f"nodes{n_nodes}pods{b}", {})
-    return e.get("traffic_bytes"), d["source"] if "traffic_bytes" in e else None
+    e = d.get("workloads", {}).get(tag)
+    return (e or {}), (f"prior PMC pass: {d.get('source')}" if e else None)
 
 
-def cpu_baseline(cl, pods, cfg, seconds, threads):
+def host_info():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return {"nproc": usable, "cpu_count": os.cpu_count(), "model": model}
+
+
+def cpu_baseline(cl, pods, cfg, seconds):
+    """The oracle scheduling consecutive prefixes of the queue at 1, 16 and every usable thread."""
     from oracle.binding import Oracle  # checker / baseline only
 
+    info = host_info()
     o = Oracle(cfg, cl.n_nodes)
     synth.load_into(o, cl)
-    # calibrate on a small prefix, then time a prefix worth ~`seconds`
-    t = time.perf_counter()
-    o.schedule(pods[:64], synth.T0, n_threads=threads)
-    per_pod = max((time.perf_counter() - t) / 64, 1e-6)
-    n = int(min(len(pods) - 64, max(16, seconds / per_pod)))
-    t = time.perf_counter()
-    o.schedule(pods[64:64 + n], synth.T0, n_threads=threads)
-    dt = time.perf_counter() - t
-    return {"value": n * cl.n_nodes / dt, "unit": "pod-node evals/s", "cores": threads, "kind": "port",
-            "sample": f"oracle (C restatement of the Go plugins) scheduling pods 64..{64 + n} of the same queue "
-                      f"against all {cl.n_nodes} nodes, {threads} threads, {dt:.1f} s"}
+    rates, pos = {}, 0
+    for threads in sorted({1, 16, max(1, info["nproc"])}):
+        o.schedule(pods[pos:pos + 4], synth.T0, n_threads=threads)  # thread pool warm-up
+        pos += 4
+        p0, dt, chunk = pos, 0.0, 8  # doubling chunks of the queue until ~`seconds` of work
+        while dt < seconds and pos < len(pods):
+            n = min(chunk, len(pods) - pos)
+            t = time.perf_counter()
+            o.schedule(pods[pos:pos + n], synth.T0, n_threads=threads)
+            dt += time.perf_counter() - t
+            pos += n
+            chunk *= 2
+        rates[str(threads)] = {"value": (pos - p0) * cl.n_nodes / dt, "pods": [p0, pos], "seconds": dt}
+    best = max(rates, key=lambda k: rates[k]["value"])
+    return {"value": rates[best]["value"], "unit": "pod-node evals/s", "cores": int(best), "kind": "port",
+            "host": info, "rates_by_threads": rates,
+            "sample": f"oracle (C restatement of the Go plugins) scheduling consecutive prefixes of the same queue "
+                      f"against all {cl.n_nodes} nodes at 1 / 16 / {info['nproc']} threads (~{seconds:.0f} s each); "
+                      f"value = the fastest ({best} threads)"}
+
+
+def roofline(n_nodes, b, ks, dt_step, batches_per_step, pipelined, tag):
+    """The dominant kernel's roofline (the Reserve chain) with the per-kernel and end-to-end fractions."""
+    by = batch_bytes(n_nodes, b, ks["rows_staged"], ks["rows_changed"], pipelined)
+    ms = {"k_eval_batch": ks["eval_ms"], "k_select": ks["select_ms"], "k_fixup": ks["fixup_ms"],
+          "k_resolve": ks["resolve_ms"]}
+    traffic, src = pmc_traffic(tag)
+    kern = {}
+    for k in by:
+        t = ms[k]
+        ach = by[k] / t / 1e6 if t else None
+        kern[k] = {"bytes_per_batch": by[k], "ms_per_batch": t, "achieved": ach,
+                   "frac": ach / HBM_PEAK_GBS if ach else None, "traffic": traffic.get(k)}
+    step_bytes = sum(by.values()) * batches_per_step
+    dom = kern["k_resolve"]
+    return {"bound": "hbm", "kernel": "k_resolve_run (per 64-pod batch: prologue + sequential replay)",
+            "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": dom["frac"],
+            "traffic": dom["traffic"], "traffic_source": src, "bytes_per_launch": dom["bytes_per_batch"],
+            "launch_ms": dom["ms_per_batch"],
+            "timing": "k_resolve / k_fixup: in-kernel s_memrealtime per batch (one persistent launch per run); "
+                      "k_eval_batch / k_select: HIP events on the eval stream",
+            "kernels": kern,
+            "end_to_end": {"bytes_per_step": step_bytes, "ms_per_step": dt_step * 1e3,
+                           "achieved": step_bytes / dt_step / 1e9, "frac": step_bytes / dt_step / 1e9 / HBM_PEAK_GBS},
+            "note": "the Reserve replay is sequential (pod j sees pods < j) and latency-bound on one wave; "
+                    "its HBM fraction is small by nature. The HBM gate is stream_roofline (eval kernel, B=1, "
+                    "SoA past the 256 MB Infinity Cache)."}
 
 
 def stream_sweep(n_nodes, cfg_batch):
@@ -141,8 +218,9 @@ def main():
     ev.eval(pods[:0], synth.T0)  # derive + upload every node row: state resident in HBM
     ev.set_profiling(a.profile_every)
     ev.set_pipeline(not a.no_pipeline)
-    lat, evm, sel, fix, res, samples, rsplit, npipe, enq, hof = [], [], [], [], [], 0, [], 0, [], []
+    lat, evm, sel, samples, rsplit, npipe, hs, kss = [], [], [], 0, [], 0, [], []
     placed = 0
+    n_batches = 0
     barrier()
     t0 = time.perf_counter()
     for s in range(K):
@@ -150,14 +228,13 @@ def main():
         placed += int((chosen >= 0).sum())
         _, per_batch = ev.stats()
         lat.extend(per_batch.tolist())
+        n_batches += len(per_batch)
         ks = ev.kernel_stats()
+        kss.append(ks)
         evm.append(ks["eval_ms"] * ks["samples"])
         sel.append(ks["select_ms"] * ks["samples"])
-        res.append(ks["resolve_ms"])
-        fix.append(ks["fixup_ms"])
         npipe += ks["pipelined_batches"]
-        enq.append(ks["enqueue_ms"])
-        hof.append(ks["handoff_ms"])
+        hs.append(ev.host_stats())
         samples += ks["samples"]
         rsplit.append((ks["resolve_prologue_ms"], ks["resolve_replay_ms"]))
     barrier()
@@ -167,9 +244,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     evals = K * slice_len * N
-    eval_ms = sum(evm) / max(samples, 1)
-    by = eval_bytes(hi - lo, a.batch)
-    traffic, traffic_src = pmc_traffic(hi - lo, a.batch)
+    mean = lambda key: float(np.mean([k[key] for k in kss]))  # noqa: E731
+    kagg = {"eval_ms": sum(evm) / max(samples, 1), "select_ms": sum(sel) / max(samples, 1),
+            "fixup_ms": mean("fixup_ms"), "resolve_ms": mean("resolve_ms"), "handoff_ms": mean("handoff_ms"),
+            "rows_staged": mean("rows_staged"), "rows_changed": mean("rows_changed")}
+    tag = f"config{a.config}_nodes{hi - lo}_batch{a.batch}_world{world}" + ("" if not a.no_pipeline else "_serial")
     out = {
         "metric": "pod-node Filter+Score evals/sec + p99 per-pod sched latency @50k nodes",
         "value": evals / dt,
@@ -187,26 +266,25 @@ def main():
                    "pods_per_batch": a.batch, "plugins": "LoadAwareScheduling+NodeNUMAResource",
                    "args": "v1beta3 defaults, NodeMetricExpirationSeconds=3600",
                    "parallelism": f"node-shard x{world}" + (" (RCCL all-gather of per-shard top-k)" if world > 1 else ""),
-                   "nodes_per_rank": hi - lo},
+                   "nodes_per_rank": hi - lo, "pipelined": not a.no_pipeline},
         "p99_pod_latency_ms": float(np.percentile(lat, 99)) if lat else None,
         "p50_pod_latency_ms": float(np.percentile(lat, 50)) if lat else None,
         "pods_placed": placed,
-        "kernel_ms": {"eval": eval_ms, "select": sum(sel) / max(samples, 1), "fixup": float(np.mean(fix)), "handoff": float(np.mean(hof)),
-                      "resolve": float(np.mean(res)), "pipelined_batches": npipe,
-                      "host_enqueue_ms_per_step": float(np.mean(enq)),
+        "kernel_ms": {"eval": kagg["eval_ms"], "select": kagg["select_ms"], "fixup": kagg["fixup_ms"],
+                      "handoff": kagg["handoff_ms"], "resolve": kagg["resolve_ms"],
                       "resolve_prologue": float(np.mean([x[0] for x in rsplit])),
-                      "resolve_replay": float(np.mean([x[1] for x in rsplit])), "samples": samples,
+                      "resolve_replay": float(np.mean([x[1] for x in rsplit])),
+                      "pipelined_batches": npipe, "batches": n_batches, "event_samples": samples,
+                      "rows_staged_per_batch": kagg["rows_staged"], "rows_changed_per_batch": kagg["rows_changed"],
                       "note": "per batch; 'select' includes the all-gather + merge when sharded"},
-        "roofline": {"bound": "hbm", "kernel": "k_eval_batch", "achieved": by / eval_ms / 1e6 if eval_ms else None,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": (by / eval_ms / 1e6 / HBM_PEAK_GBS) if eval_ms else None, "traffic": traffic,
-                     "traffic_source": traffic_src, "bytes_per_launch": by},
+        "host_ms_per_step": {k: float(np.mean([h[k] for h in hs])) for k in hs[0]} if hs else None,
+        "roofline": roofline(hi - lo, a.batch, kagg, dt / K, n_batches / K, not a.no_pipeline, tag),
     }
     ev.close()
     if world == 1 and a.stream_nodes > 0:
         out["stream_roofline"] = stream_sweep(a.stream_nodes, a.batch)
     if world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cl, pods, cfg, a.cpu_seconds, a.cpu_threads)
+        out["cpu_baseline"] = cpu_baseline(cl, pods, cfg, a.cpu_seconds)
         out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(out), flush=True)

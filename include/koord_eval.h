@@ -548,16 +548,19 @@ int ke_shard_range(ke_ctx* ctx, int32_t* lo, int32_t* hi);
  * the eval / select / resolve kernels over the sampled batches of the last ke_schedule. */
 int ke_set_profiling(ke_ctx* ctx, int32_t sample_every);
 int ke_last_kernel_stats(ke_ctx* ctx, double* eval_ms, double* select_ms, double* resolve_ms, int32_t* samples);
-/* Per-batch timing of the last ke_schedule, ms: ms6 = {eval, select (HIP-event samples on the eval
- * stream), fixup (k_fixup after its wait, pipelined batches), Reserve (in-kernel stamps: prologue +
- * replay, every batch), host enqueue time of the whole call, hand-off (end of a pipelined batch's
- * replay -> start of the next one's)}, the number of event samples, and how many batches ran
- * pipelined. */
-int ke_last_kernel_stats_ex(ke_ctx* ctx, double* ms6, int32_t* samples, int32_t* pipelined_batches);
+/* Per-batch statistics of the last ke_schedule: v8 = {eval ms, select ms (HIP-event samples on the eval
+ * stream), fixup ms (k_fixup after its wait, pipelined batches), Reserve ms (in-kernel stamps: prologue +
+ * replay, every batch), host enqueue ms of the whole call, hand-off ms (end of a pipelined batch's replay
+ * -> start of the next one's), distinct candidate rows staged per batch, rows changed per batch}, the
+ * number of event samples, and how many batches ran pipelined. */
+int ke_last_kernel_stats_ex(ke_ctx* ctx, double* v8, int32_t* samples, int32_t* pipelined_batches);
 /* Pipelined schedule (default on): batch b's eval + select overlap batch b-1's Reserve replay on a
  * second stream.  Off = one stream, every batch waits for the previous Reserve.  The
  * placements are identical either way. */
 int ke_set_pipeline(ke_ctx* ctx, int32_t on);
+/* Host wall milliseconds of the last ke_schedule by phase: argument checks, row refresh, pod upload,
+ * launch setup, enqueue, wait for the device, statistics readback, host mirror of the Reserves. */
+int ke_last_host_stats(ke_ctx* ctx, double* ms8);
 /* Resolve kernel split of the last ke_schedule (in-kernel s_memrealtime stamps, every batch):
  * average ms per batch of candidate/row staging (prologue) and of the sequential replay. */
 int ke_last_resolve_split(ke_ctx* ctx, double* prologue_ms, double* replay_ms);
@@ -575,6 +578,8 @@ int ke_bench_eval_kernel(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_
 /* ---- introspection (tests, tools) ------------------------------------------------------------ */
 /* sizeof() of one node row of the device SoA in bytes (algorithmic bytes per node per pass). */
 int ke_row_bytes(void);
+/* sizeof() of the per-pod record the kernels read (the device form of a ke_pod). */
+int ke_pod_record_bytes(void);
 /* Copy the device SoA rows of nodes [0,n) back to the host (n*ke_row_bytes() bytes) and, into
  * `host_rows`, the rows the host derives from its object state; lets tests check the GPU-side
  * patches against a from-scratch host derivation. */

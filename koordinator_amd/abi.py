@@ -348,11 +348,13 @@ EXPORTS = {
     "ke_last_kernel_stats": (C.c_int, [C.c_void_p] + [C.POINTER(C.c_double)] * 3 + [C.POINTER(i32)]),
     "ke_last_kernel_stats_ex": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(i32), C.POINTER(i32)]),
     "ke_set_pipeline": (C.c_int, [C.c_void_p, i32]),
+    "ke_last_host_stats": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ke_last_resolve_split": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "ke_debug_resolve_phases": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ke_debug_numa_deferred": (C.c_int, [C.c_void_p, C.POINTER(i64)]),
     "ke_bench_eval_kernel": (C.c_int, [C.c_void_p, i32, C.c_void_p, i64, i32, C.POINTER(C.c_double)]),
     "ke_row_bytes": (C.c_int, []),
+    "ke_pod_record_bytes": (C.c_int, []),
     "ke_debug_rows": (C.c_int, [C.c_void_p, i32, i64, C.c_void_p, C.c_void_p]),
     "ke_debug_usage_bound": (i64, [i64, i64]),
     "ke_num_nodes": (i32, [C.c_void_p]),

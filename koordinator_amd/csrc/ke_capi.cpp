@@ -1,6 +1,7 @@
 // ke_capi.cpp — the extern "C" boundary (include/koord_eval.h) over the host state (ke_host.cpp)
 // and the device evaluator (ke_kernels.hip).
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <new>
 
@@ -100,6 +101,7 @@ int ke_abi_struct_sizes(int32_t* sizes, int32_t n) {
 const char* ke_last_error(void) { return last_error_cstr(); }
 int ke_device_available(void) { return device_available(); }
 int ke_row_bytes(void) { return ROW_BYTES; }
+int ke_pod_record_bytes(void) { return (int)sizeof(DevPod); }
 
 int ke_create(const ke_config* cfg, ke_ctx** out) {
   if (!cfg || !out) return fail(KE_ERR_INVALID, "null argument");
@@ -156,6 +158,7 @@ int32_t ke_num_nodes(ke_ctx* ctx) { return ctx ? ctx->c.n_nodes : 0; }
 
 int ke_node_upsert(ke_ctx* ctx, int32_t node, const ke_node* n) {
   int rc = check_node(ctx, node);
+  if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
   if (!n) return fail(KE_ERR_INVALID, "null node");
   rc = validate_node(*n);
@@ -177,6 +180,7 @@ int ke_node_upsert(ke_ctx* ctx, int32_t node, const ke_node* n) {
 
 int ke_nodes_load(ke_ctx* ctx, int32_t n, const ke_node* nodes) {
   if (!ctx || n < 0 || (n > 0 && !nodes)) return fail(KE_ERR_INVALID, "ke_nodes_load arguments");
+  if (ctx) flush_mirror(ctx->c);
   if (n > ctx->c.cfg.node_capacity) return fail(KE_ERR_INVALID, "more nodes than node_capacity");
   for (int32_t i = 0; i < n; i++) {
     int rc = ke_node_upsert(ctx, i, &nodes[i]);
@@ -187,6 +191,7 @@ int ke_nodes_load(ke_ctx* ctx, int32_t n, const ke_node* nodes) {
 
 int ke_node_devices_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_device* devices) {
   int rc = check_node(ctx, node);
+  if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
   rc = validate_devices(n, devices);
   if (rc) return rc;
@@ -200,6 +205,7 @@ int ke_node_devices_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_device* d
 
 int ke_node_devices_delete(ke_ctx* ctx, int32_t node) {
   int rc = check_node(ctx, node);
+  if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
   NodeState& ns = ctx->c.nodes[node];
   ns.has_dev_cache = false;
@@ -210,6 +216,7 @@ int ke_node_devices_delete(ke_ctx* ctx, int32_t node) {
 
 int ke_node_numa_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_numa_zone* zones) {
   int rc = check_node(ctx, node);
+  if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
   rc = validate_zones(n, zones);
   if (rc) return rc;
@@ -222,6 +229,7 @@ int ke_node_numa_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_numa_zone* z
 
 int ke_node_cpus_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_cpu* cpus, int32_t max_ref_count) {
   int rc = check_node(ctx, node);
+  if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
   rc = validate_cpus(n, cpus, max_ref_count);
   if (rc) return rc;
@@ -295,6 +303,7 @@ int ke_last_device_allocations(ke_ctx* ctx, int32_t n, uint64_t* minors) {
 
 int ke_node_set_requested(ke_ctx* ctx, int32_t node, int64_t milli_cpu, int64_t memory) {
   int rc = check_node(ctx, node);
+  if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
   NodeState& ns = ctx->c.nodes[node];
   ns.node.requested[KE_RES_CPU] = milli_cpu;
@@ -305,6 +314,7 @@ int ke_node_set_requested(ke_ctx* ctx, int32_t node, int64_t milli_cpu, int64_t 
 
 int ke_node_set_cpuset_allocated(ke_ctx* ctx, int32_t node, int64_t cpus) {
   int rc = check_node(ctx, node);
+  if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
   NodeState& ns = ctx->c.nodes[node];
   ns.node.cpuset_allocated_cpus = cpus;
@@ -315,6 +325,7 @@ int ke_node_set_cpuset_allocated(ke_ctx* ctx, int32_t node, int64_t cpus) {
 int ke_nodemetric_upsert(ke_ctx* ctx, int32_t node, const ke_node_metric* nm, int32_t n_pm, const ke_pod_metric* pm,
                          int32_t n_agg, const ke_aggregated_usage* agg) {
   int rc = check_node(ctx, node);
+  if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
   if (!nm || n_pm < 0 || n_agg < 0 || (n_pm && !pm) || (n_agg && !agg)) return fail(KE_ERR_INVALID, "nodemetric");
   NodeState& ns = ctx->c.nodes[node];
@@ -329,6 +340,7 @@ int ke_nodemetric_upsert(ke_ctx* ctx, int32_t node, const ke_node_metric* nm, in
 int ke_nodemetrics_load(ke_ctx* ctx, int32_t n, const ke_node_metric* nms, const int64_t* pm_offsets,
                         const ke_pod_metric* pod_metrics, const int64_t* agg_offsets, const ke_aggregated_usage* aggregated) {
   if (!ctx || n < 0 || (n > 0 && (!nms || !pm_offsets || !agg_offsets))) return fail(KE_ERR_INVALID, "nodemetrics_load");
+  if (ctx) flush_mirror(ctx->c);
   for (int32_t i = 0; i < n; i++) {
     const int64_t p0 = pm_offsets[i], p1 = pm_offsets[i + 1], a0 = agg_offsets[i], a1 = agg_offsets[i + 1];
     if (p1 < p0 || a1 < a0) return fail(KE_ERR_INVALID, "offsets must be non-decreasing");
@@ -341,6 +353,7 @@ int ke_nodemetrics_load(ke_ctx* ctx, int32_t n, const ke_node_metric* nms, const
 
 int ke_nodemetric_delete(ke_ctx* ctx, int32_t node) {
   int rc = check_node(ctx, node);
+  if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
   NodeState& ns = ctx->c.nodes[node];
   ns.has_metric = false;
@@ -353,6 +366,7 @@ int ke_nodemetric_delete(ke_ctx* ctx, int32_t node) {
 
 int ke_pod_assign(ke_ctx* ctx, int32_t node, const ke_pod* pod, int64_t timestamp_ns) {
   int rc = check_node(ctx, node);
+  if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
   if (!pod) return fail(KE_ERR_INVALID, "null pod");
   host_assign(ctx->c.cfg, ctx->c.nodes[node], *pod, timestamp_ns);
@@ -361,6 +375,7 @@ int ke_pod_assign(ke_ctx* ctx, int32_t node, const ke_pod* pod, int64_t timestam
 
 int ke_pods_assign(ke_ctx* ctx, int32_t n, const int32_t* nodes, const ke_pod* pods, const int64_t* timestamps_ns) {
   if (!ctx || n < 0 || (n > 0 && (!nodes || !pods || !timestamps_ns))) return fail(KE_ERR_INVALID, "ke_pods_assign");
+  if (ctx) flush_mirror(ctx->c);
   for (int32_t i = 0; i < n; i++) {
     int rc = check_node(ctx, nodes[i]);
     if (rc) return rc;
@@ -371,6 +386,7 @@ int ke_pods_assign(ke_ctx* ctx, int32_t n, const int32_t* nodes, const ke_pod* p
 
 int ke_pod_unassign(ke_ctx* ctx, int32_t node, int64_t uid) {
   int rc = check_node(ctx, node);
+  if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
   auto& v = ctx->c.nodes[node].asg;
   for (size_t i = 0; i < v.size(); i++) {
@@ -395,6 +411,7 @@ int ke_estimate_pod(ke_ctx* ctx, const ke_pod* pod, int64_t* est) {
 int ke_eval(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, uint8_t* status, uint8_t* reason,
             int16_t* la_score, int16_t* numa_score, int16_t* ds_score, int16_t* total, int32_t* best) {
   if (!ctx) return fail(KE_ERR_INVALID, "null context");
+  if (ctx) flush_mirror(ctx->c);
   int rc = check_pods(pods, n_pods);
   if (rc) return rc;
   rc = check_numa_deviceshare(ctx, pods, n_pods);
@@ -408,6 +425,8 @@ int ke_eval(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, uin
 
 int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int32_t* chosen, int32_t* score) {
   if (!ctx || (n_pods > 0 && !chosen)) return fail(KE_ERR_INVALID, "ke_schedule arguments");
+  using clk = std::chrono::steady_clock;
+  auto tp = clk::now();
   int rc = check_pods(pods, n_pods);
   if (rc) return rc;
   rc = check_numa_deviceshare(ctx, pods, n_pods);
@@ -419,30 +438,39 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
       return fail(KE_ERR_INVALID, "ke_pod.quota outside the loaded ElasticQuota tree");
   rc = require_device(ctx);
   if (rc) return rc;
+  ctx->c.host_ms[0] = std::chrono::duration<double, std::milli>(clk::now() - tp).count();
   rc = device_schedule(&ctx->c, n_pods, pods, now_ns, chosen, score);
   if (rc) return rc;
+  tp = clk::now();
   // Host mirror of the Reserves the device already applied to its rows: keep the object state
   // (assign cache, NodeInfo.Requested) in step so later re-derivations include these pods.
   const int32_t off = ctx->c.cfg.global_node_offset;
   std::vector<int32_t> touched;
+  ctx->c.pending.reserve(ctx->c.pending.size() + (size_t)n_pods);
   for (int32_t p = 0; p < n_pods; p++) {
     const int32_t node = chosen[p] - off;
     if (chosen[p] < 0 || node < 0 || node >= ctx->c.n_nodes) continue;
     NodeState& ns = ctx->c.nodes[node];
+    // LoadAware assign + NodeInfo.Requested: deferred (flush_mirror), the device rows carry them
+    ctx->c.pending.push_back({node, now_ns, pods[p]});
     const bool was_dirty = ns.dirty;
-    host_assign(ctx->c.cfg, ns, pods[p], now_ns);
     if (p < (int32_t)ctx->c.last_dev_alloc.size() && ctx->c.last_dev_alloc[p])
       host_ds_reserve(ctx->c.cfg, ns, make_dev_pod(ctx->c.cfg, pods[p]), ctx->c.last_dev_alloc[p]);
     if ((int64_t)ctx->c.last_numa_alloc.size() >= (int64_t)(p + 1) * KE_MAX_NUMA * KE_NRES)
       host_numa_reserve(ns, &ctx->c.last_numa_alloc[(size_t)p * KE_MAX_NUMA * KE_NRES]);
-    ns.node.requested[KE_RES_CPU] += pods[p].requests[KE_RES_CPU];
-    ns.node.requested[KE_RES_MEMORY] += pods[p].requests[KE_RES_MEMORY];
-    ns.dirty = was_dirty;  // the device row already carries this Reserve
+    ns.dirty = was_dirty;  // the device rows already carry these Reserves
     // cpuset Reserve: the CPU table (the device one is patched too) and the zones' NUMA status (not
     // patched on the device: re-derived from this mirror)
     const uint64_t* cs = (int64_t)ctx->c.last_cpusets.size() >= (int64_t)(p + 1) * 4 ? &ctx->c.last_cpusets[(size_t)p * 4] : nullptr;
     if (cs && (cs[0] | cs[1] | cs[2] | cs[3])) host_cpuset_reserve(ns, make_dev_pod(ctx->c.cfg, pods[p]), cs);
   }
+  ctx->c.host_ms[7] = std::chrono::duration<double, std::milli>(clk::now() - tp).count();
+  return KE_OK;
+}
+
+int ke_last_host_stats(ke_ctx* ctx, double* ms8) {
+  if (!ctx || !ms8) return fail(KE_ERR_INVALID, "ke_last_host_stats arguments");
+  for (int i = 0; i < 8; i++) ms8[i] = ctx->c.host_ms[i];
   return KE_OK;
 }
 
@@ -473,7 +501,7 @@ int ke_last_kernel_stats(ke_ctx* ctx, double* eval_ms, double* select_ms, double
   return KE_OK;
 }
 
-int ke_last_kernel_stats_ex(ke_ctx* ctx, double* ms4 /* [6] */, int32_t* samples, int32_t* pipelined_batches) {
+int ke_last_kernel_stats_ex(ke_ctx* ctx, double* ms4 /* [8] */, int32_t* samples, int32_t* pipelined_batches) {
   if (!ctx || !ms4) return fail(KE_ERR_INVALID, "ke_last_kernel_stats_ex arguments");
   ms4[0] = ctx->c.kstat_eval_ms;
   ms4[1] = ctx->c.kstat_select_ms;
@@ -483,6 +511,8 @@ int ke_last_kernel_stats_ex(ke_ctx* ctx, double* ms4 /* [6] */, int32_t* samples
   if (pipelined_batches) *pipelined_batches = ctx->c.last_pipelined;
   ms4[4] = ctx->c.last_enqueue_ms;
   ms4[5] = ctx->c.kstat_handoff_ms;
+  ms4[6] = ctx->c.kstat_rows_staged;
+  ms4[7] = ctx->c.kstat_rows_changed;
   return KE_OK;
 }
 
@@ -515,6 +545,7 @@ int ke_debug_resolve_phases(ke_ctx* ctx, double* phases6) {
 int ke_bench_eval_kernel(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int32_t iters,
                          double* avg_ms) {
   if (!ctx || !avg_ms) return fail(KE_ERR_INVALID, "ke_bench_eval_kernel arguments");
+  if (ctx) flush_mirror(ctx->c);
   int rc = check_pods(pods, n_pods);
   if (rc) return rc;
   rc = require_device(ctx);
@@ -550,6 +581,7 @@ int64_t ke_debug_usage_bound(int64_t total, int64_t thr) { return total > 0 ? ma
 
 int ke_debug_rows(ke_ctx* ctx, int32_t n, int64_t now_ns, void* device_rows, void* host_rows) {
   if (!ctx || n < 0 || n > ctx->c.n_nodes) return fail(KE_ERR_INVALID, "ke_debug_rows arguments");
+  if (ctx) flush_mirror(ctx->c);
   if (device_rows) {
     int rc = require_device(ctx);
     if (rc) return rc;

@@ -783,6 +783,18 @@ void host_cpuset_reserve(NodeState& ns, const DevPod& dp, const uint64_t* set) {
   ns.dirty = true;
 }
 
+void flush_mirror(Context& c) {
+  for (const Context::PendingAssign& a : c.pending) {
+    NodeState& ns = c.nodes[a.node];
+    const bool was_dirty = ns.dirty;
+    host_assign(c.cfg, ns, a.pod, a.ts);
+    ns.node.requested[KE_RES_CPU] += a.pod.requests[KE_RES_CPU];
+    ns.node.requested[KE_RES_MEMORY] += a.pod.requests[KE_RES_MEMORY];
+    ns.dirty = was_dirty;  // the device row already carries this Reserve
+  }
+  c.pending.clear();
+}
+
 void host_assign(const ke_config& cfg, NodeState& ns, const ke_pod& pod, int64_t timestamp_ns) {
   if (pod.is_terminated) return;  // pod_assign_cache.go:90
   AssignedPod info{};

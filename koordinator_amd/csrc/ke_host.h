@@ -63,11 +63,24 @@ struct Context {
   std::vector<double> last_batch_ms;
   double kstat_eval_ms = 0, kstat_select_ms = 0, kstat_resolve_ms = 0, kstat_fixup_ms = 0, kstat_handoff_ms = 0;
   int32_t last_pipelined = 0;
-  double last_enqueue_ms = 0;  // host time spent enqueueing the last ke_schedule's launches  // batches of the last ke_schedule that ran pipelined (two streams)
+  double kstat_rows_staged = 0, kstat_rows_changed = 0;  // per batch: distinct candidate rows, changed rows
+  double last_enqueue_ms = 0;  // host time spent enqueueing the last ke_schedule's launches
+  // host wall ms of the last ke_schedule by phase: argument checks, row refresh, pod upload, launch
+  // setup, enqueue, wait for the device, statistics readback, host mirror of the Reserves
+  double host_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // batches of the last ke_schedule that ran pipelined (two streams)
   double kstat_resolve_prologue_ms = 0, kstat_resolve_loop_ms = 0;
   double kstat_resolve_phase_ms[6] = {0, 0, 0, 0, 0, 0};
   int64_t kstat_numa_deferred = 0;  // BestEffort pairs the last ke_eval / ke_schedule left to k_numa_fallback
   int32_t kstat_samples = 0;
+  // Host mirror of the LoadAware / NodeInfo part of the last ke_schedule's Reserves (the device rows
+  // already carry them), applied lazily: by the next call that reads or changes host node state, or
+  // while the next ke_schedule's launches run (flush_mirror).
+  struct PendingAssign {
+    int32_t node;
+    int64_t ts;
+    ke_pod pod;
+  };
+  std::vector<PendingAssign> pending;
   // ElasticQuota tree (ke_quotas_load): objects, the used limits computed on the host, and whether the
   // device copy of the table is stale
   ke_quota_args qargs{};
@@ -106,6 +119,8 @@ int64_t usage_percent(int64_t used, int64_t total);
 
 // host mirror of Reserve (podAssignCache.assign + NodeInfo.Requested += requests)
 void host_assign(const ke_config& cfg, NodeState& ns, const ke_pod& pod, int64_t timestamp_ns);
+// apply Context::pending (placements whose device rows are already patched: dirty flags unchanged)
+void flush_mirror(Context& c);
 
 // DeviceShare
 int validate_devices(int32_t n, const ke_device* devs);

@@ -1937,13 +1937,34 @@ __global__ __launch_bounds__(MERGE_BLOCK) void k_merge(const uint32_t* __restric
 // resolve).  The top-k_j of (stale list minus touched) + (touched, fresh keys) is therefore the exact
 // top-k_j under S that k_resolve expects.  One workgroup per pod.
 constexpr int FIX_BLOCK = KSTALE + KMAX;  // stale keys, then fresh keys of the touched nodes
+// Words one workgroup hands to another while both run (k_fixup -> k_resolve_run: the exact lists;
+// k_resolve_run -> k_fixup: the changed rows; -> later eval launches: the patched SoA rows) are
+// written and read with sc1 (relaxed agent-scope atomics: global_store / global_load ... sc1), i.e.
+// write-through past the storing CU and read past the reading CU's L1: no release (L2 write-back) and
+// no acquire (L1/L2 invalidate) fence on the hand-off path (MI355X_MICROARCH.md § visibility,
+// cdna_hip_programming.md Guideline 16).  The storing wave drains (vmcnt(0)) before the flag.
+__device__ __forceinline__ int64_t ld_sc1(const int64_t* p) {
+  return __hip_atomic_load(const_cast<int64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
+  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int32_t ld_sc1(const int32_t* p) {
+  return __hip_atomic_load(const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drain_stores() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
+
 // Device-side hand-off between the eval stream and the persistent Reserve kernel (k_resolve_run):
-// flags in global memory, agent-scope release / acquire (MI355X_MICROARCH.md, inter-workgroup
-// visibility), every wait bounded in time and abandoned when the run's error word is set.
+// counters / flags in global memory polled with relaxed sc1 loads, payloads sc1 (above), every wait
+// bounded in time and abandoned when the run's error word is set.
 constexpr uint64_t HANDOFF_TIMEOUT_TICKS = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
 __device__ __forceinline__ bool wait_at_least(const int32_t* flag, int32_t want, int32_t* err) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < want) {
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
     if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
     if (__builtin_amdgcn_s_memrealtime() - t0 > HANDOFF_TIMEOUT_TICKS) {
       __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1951,84 +1972,18 @@ __device__ __forceinline__ bool wait_at_least(const int32_t* flag, int32_t want,
     }
     __builtin_amdgcn_s_sleep(2);
   }
+  // the hand-off's words are read with sc1 loads from here on: no acquire fence, only a compiler
+  // ordering point (cdna_hip_programming.md Guideline 16)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   return true;
 }
 
 // wait_b >= 0: the lists need the Reserves of batch wait_b (the touched nodes' rows): wait for its flag
 // in `done` first.  When the list is written the workgroup adds 1 to *ready (the Reserve kernel waits
 // for all of the batch's pods).
-__global__ __launch_bounds__(FIX_BLOCK) void k_fixup(SoA s, const DevPod* __restrict__ pods,
-                                                     const int32_t* __restrict__ batch_base, KArgs k,
-                                                     const uint32_t* __restrict__ stale,
-                                                     const int32_t* __restrict__ stale_cnt,
-                                                     const int32_t* __restrict__ touched, int n_touched,
-                                                     int32_t global_offset, uint32_t* __restrict__ cand,
-                                                     int32_t* __restrict__ cand_cnt, const int32_t* __restrict__ done,
-                                                     int wait_b, int32_t* __restrict__ ready, int32_t* __restrict__ err,
-                                                     uint64_t* __restrict__ fstamp) {
-  __shared__ int32_t s_tn[KMAX];
-  __shared__ uint4 s_k[FIX_BLOCK / 4];
-  __shared__ int32_t s_ok;
-  const int j = blockIdx.x, kj = min(j + 1, KMAX);
-  const int t = threadIdx.x;
-  if (t == 0) {
-    s_ok = wait_b < 0 || wait_at_least(done + wait_b, 1, err);
-    if (j == 0 && fstamp) fstamp[0] = __builtin_amdgcn_s_memrealtime();
-  }
-  __syncthreads();
-  if (!s_ok) return;
-  if (t < KMAX) s_tn[t] = t < n_touched ? touched[t] - global_offset : -1;  // chosen: -1 = unplaced
-  __syncthreads();
-  uint32_t key = 0;
-  if (t < KSTALE) {
-    if (t < stale_cnt[j]) key = stale[j * KSTALE + t];
-    if (key) {
-      const int node = key_node(key);
-#pragma unroll 8
-      for (int u = 0; u < KMAX; u++) key = s_tn[u] == node ? 0u : key;  // broadcast reads
-    }
-  } else {
-    const int u = t - KSTALE;
-    const int node = s_tn[u];
-    bool first = node >= 0;
-    for (int v = 0; v < u; v++) first = first && s_tn[v] != node;
-    if (first) {
-      NodeRegs n;
-      load_row(s, node, n);
-      prepare_row(n);
-      const DevPod& pod = pods[*batch_base + j];
-      key = make_key(lite_total(n, node_expired(n, k), pod, k), node);
-    }
-  }
-  reinterpret_cast<uint32_t*>(s_k)[t] = key;
-  const int nz = __syncthreads_count(key != 0u);
-  if (key) {
-    int rank = 0;
-#pragma unroll 4
-    for (int u = 0; u < FIX_BLOCK / 4; u++) {
-      const uint4 q = s_k[u];
-      rank += (int)(q.x > key) + (int)(q.y > key) + (int)(q.z > key) + (int)(q.w > key);
-    }
-    if (rank < kj) cand[j * KMAX + rank] = key;
-  }
-  if (t == 0) cand_cnt[j] = min(nz, kj);
-  if (ready) {  // publish: every wave's stores drained at the barrier, then one agent-scope release
-    __syncthreads();
-    if (t == 0) {
-      __hip_atomic_fetch_add(ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      if (j == 0 && fstamp) fstamp[1] = __builtin_amdgcn_s_memrealtime();
-    }
-  }
-}
-
-// --- resolve: one wavefront replays the batch sequentially -------------------------------------
-struct LdsRow {
-  int64_t f[NUM_I64_FIELDS];
-  uint32_t flags;
-  uint32_t pad;
-};
-
-__device__ __forceinline__ void regs_from_lds(const LdsRow& r, NodeRegs& n) {
+// The touched nodes come as the Reserve kernel's compact list of the rows batch b-1 changed (distinct
+// nodes, the node index in Row.pad), so no row gather depends on a node id read after the wait.
+__device__ __forceinline__ void regs_from_row(const Row& r, NodeRegs& n) {
   n.ut = r.f[F_UT];
 #pragma unroll
   for (int v = 0; v < 2; v++)
@@ -2049,16 +2004,115 @@ __device__ __forceinline__ void regs_from_lds(const LdsRow& r, NodeRegs& n) {
   n.flags = r.flags;
 }
 
-// LDS budget of the resolve workgroup (one wave, one CU): candidate keys + their row slots, a node
-// -> slot hash over every candidate, and the rows of the first RES_ROWS distinct candidates.
-constexpr int RES_ROWS = 448;                 // prefetched candidate rows
-constexpr int RES_OVF = MAX_BATCH;            // rows of chosen nodes that missed the prefetch
-constexpr int RES_SLOTS = RES_ROWS + RES_OVF;
-constexpr int HASH_SLOTS = 2 * MAX_BATCH * KMAX;  // load factor <= 1/2
-constexpr int HASH_EMPTY = -1;
-// prologue width (the replay runs on wave 0 alone): 8 waves keep 2x the row gathers in flight; the
-// NUMA variants stay at 4 waves (their replay wave needs up to 256 VGPRs, 2 waves per SIMD would cap it)
-template <bool NUMA> constexpr int res_threads() { return NUMA ? 256 : 512; }
+__global__ __launch_bounds__(FIX_BLOCK) void k_fixup(const DevPod* __restrict__ pods,
+                                                     const int32_t* __restrict__ batch_base, KArgs k,
+                                                     const uint32_t* __restrict__ stale,
+                                                     const int32_t* __restrict__ stale_cnt,
+                                                     const Row* __restrict__ trows, const int32_t* __restrict__ tcnt,
+                                                     uint32_t* __restrict__ cand, int32_t* __restrict__ cand_cnt,
+                                                     const int32_t* __restrict__ done, int wait_b,
+                                                     int32_t* __restrict__ ready, int32_t* __restrict__ err,
+                                                     uint64_t* __restrict__ fstamp) {
+  __shared__ int32_t s_tn[KMAX];
+  __shared__ uint4 s_k[FIX_BLOCK / 4];
+  __shared__ int32_t s_ok, s_nt;
+  const int j = blockIdx.x, kj = min(j + 1, KMAX);
+  const int t = threadIdx.x;
+  // everything that does not depend on batch b-1 is read before the wait
+  uint32_t key = 0;
+  if (t < KSTALE && t < stale_cnt[j]) key = stale[j * KSTALE + t];
+  DevPod pod;
+  if (t >= KSTALE) pod = pods[*batch_base + j];
+  if (t == 0) {
+    s_ok = wait_b < 0 || wait_at_least(done + wait_b, 1, err);
+    s_nt = wait_b < 0 ? 0 : ld_sc1(tcnt);
+    if (j == 0 && fstamp) fstamp[0] = __builtin_amdgcn_s_memrealtime();
+  }
+  __syncthreads();
+  if (!s_ok) return;
+  const int nt = s_nt;
+  NodeRegs n;
+  int node = -1;
+  if (t >= KSTALE && t - KSTALE < nt) {  // sc1: the Reserve kernel wrote them while running
+    const int64_t* rp = reinterpret_cast<const int64_t*>(trows + (t - KSTALE));
+    Row r;
+#pragma unroll
+    for (int f = 0; f < NUM_I64_FIELDS; f++) r.f[f] = ld_sc1(rp + f);
+    const uint64_t fl = (uint64_t)ld_sc1(rp + NUM_I64_FIELDS);
+    r.flags = (uint32_t)fl;
+    r.pad = (uint32_t)(fl >> 32);
+    regs_from_row(r, n);
+    node = (int)r.pad;
+    s_tn[t - KSTALE] = node;
+  }
+  __syncthreads();
+  if (t < KSTALE) {
+    if (key) {
+      const int kn = key_node(key);
+      for (int u = 0; u < nt; u++) key = s_tn[u] == kn ? 0u : key;  // broadcast reads
+    }
+  } else if (node >= 0) {
+    prepare_row(n);
+    key = make_key(lite_total(n, node_expired(n, k), pod, k), node);
+  }
+  reinterpret_cast<uint32_t*>(s_k)[t] = key;
+  const int nz = __syncthreads_count(key != 0u);
+  if (key) {
+    int rank = 0;
+#pragma unroll 4
+    for (int u = 0; u < FIX_BLOCK / 4; u++) {
+      const uint4 q = s_k[u];
+      rank += (int)(q.x > key) + (int)(q.y > key) + (int)(q.z > key) + (int)(q.w > key);
+    }
+    if (rank < kj) st_sc1(cand + j * KMAX + rank, key);  // sc1: read by the running Reserve kernel
+  }
+  if (t == 0) st_sc1(cand_cnt + j, min(nz, kj));
+  if (ready) {  // publish: every wave drains its sc1 stores before the barrier, then one counter add
+    drain_stores();
+    __syncthreads();
+    if (t == 0) {
+      __hip_atomic_fetch_add(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (j == 0 && fstamp) fstamp[1] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+}
+
+// --- resolve: one wavefront replays the batch sequentially -------------------------------------
+// one node row straight from the SoA, past this CU's L1 (rows this workgroup patched earlier)
+__device__ __forceinline__ void load_row_sc1(const SoA& s, int64_t i, Row& r) {
+  const int64_t st = s.stride;
+#pragma unroll
+  for (int f = 0; f < NUM_I64_FIELDS; f++) r.f[f] = ld_sc1(s.f + f * st + i);
+  r.flags = ld_sc1(s.flags + i);
+  r.pad = 0;
+}
+
+// Changed-node set of the batch being replayed: a bitmap over node ids, in LDS for ids < 2^20 (else a
+// zeroed device bitmap in global memory, sc1-accessed).  Only the replay wave touches it; the bits of a
+// batch are cleared when it ends, so it is zero between batches.
+constexpr int CHG_LDS_WORDS = 32768;
+struct ChgSet {
+  uint32_t* lds;
+  uint32_t* glb;  // non-null: node ids beyond the LDS bitmap
+};
+__device__ __forceinline__ bool chg_test(const ChgSet& c, int node) {
+  const uint32_t w = c.glb ? ld_sc1(c.glb + (node >> 5)) : c.lds[node >> 5];
+  return (w >> (node & 31)) & 1u;
+}
+__device__ __forceinline__ void chg_set(const ChgSet& c, int node) {  // one lane
+  if (c.glb) __hip_atomic_fetch_or(c.glb + (node >> 5), 1u << (node & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else c.lds[node >> 5] |= 1u << (node & 31);
+}
+// at the end of a batch every set bit belongs to a changed node: each changed lane zeroes its word
+// (lanes sharing a word all store zero)
+__device__ __forceinline__ void chg_clear_word(const ChgSet& c, int node) {
+  if (c.glb) st_sc1(c.glb + (node >> 5), 0u);
+  else c.lds[node >> 5] = 0u;
+}
+
+// prologue width (the replay runs on wave 0 alone): 4 waves, one per SIMD, so the replay wave may use
+// every register of its SIMD (no scratch spills in any variant)
+template <bool NUMA> constexpr int res_threads() { return 256; }
 
 // Ordering point for LDS traffic between the lanes of ONE wavefront: LDS instructions of a wave
 // execute in issue order, so only the compiler must be kept from moving accesses across it
@@ -2069,180 +2123,95 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ int hash_of(int node) { return (int)(((uint32_t)node * 0x9E3779B1u) >> 19) & (HASH_SLOTS - 1); }
-
-// NUMA: nodes may carry NUMA topology policies — changed nodes re-read their zones (patched by this
-// replay's Reserves) from the NUMA SoA, and numa_alloc[pod][2*id + r] receives each pod's allocation.
 struct ResLds {
   uint32_t cand[MAX_BATCH * KMAX];
-  int16_t cand_slot[MAX_BATCH * KMAX];
-  int32_t hkey[HASH_SLOTS];
-  int16_t hval[HASH_SLOTS];
-  LdsRow row[RES_SLOTS];
-  int32_t slot_node[RES_SLOTS];
-  uint8_t changed[RES_SLOTS];
   DevPod pod[MAX_BATCH];
   int32_t cnt[MAX_BATCH];
-  int32_t nslots;
+  uint32_t chg[CHG_LDS_WORDS];
 };
 
-template <bool DS, bool NUMA, bool QUOTA>
-__device__ __forceinline__ void replay_batch(ResLds& L, const SoA& s, const int base, const int B, const KArgs& k,
-                                             int32_t* __restrict__ chosen, int32_t* __restrict__ chosen_score,
-                                             int32_t global_offset, uint64_t* __restrict__ stamps, int batch_index,
-                                             uint64_t* __restrict__ dev_alloc, int64_t* __restrict__ numa_alloc);
+// zero the LDS bitmap words of node ids [0, n_nodes) (all threads; once per launch)
+__device__ __forceinline__ ChgSet chg_init(ResLds& L, uint32_t* glb, int n_nodes) {
+  const int words = glb ? 0 : (n_nodes + 31) >> 5;
+  for (int t = threadIdx.x; t < words; t += blockDim.x) L.chg[t] = 0u;
+  return ChgSet{L.chg, glb};
+}
 
-// One batch: prologue on every thread of the workgroup, replay on wave 0 (the other waves skip it).
 template <bool DS, bool NUMA, bool QUOTA>
-__device__ __forceinline__ void resolve_batch(ResLds& L, const SoA& s, const DevPod* __restrict__ pods, const int base,
-                                              const int batch_pods, const KArgs& k, const uint32_t* __restrict__ cand,
-                                              const int32_t* __restrict__ cand_cnt, int32_t* __restrict__ chosen,
-                                              int32_t* __restrict__ chosen_score, int32_t global_offset,
-                                              uint64_t* __restrict__ stamps, uint64_t* __restrict__ pstamps,
-                                              int batch_index, uint64_t* __restrict__ dev_alloc,
-                                              int64_t* __restrict__ numa_alloc) {
+__device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const SoA& s, const int base, const int B,
+                                             const KArgs& k, int32_t* __restrict__ chosen,
+                                             int32_t* __restrict__ chosen_score, int32_t global_offset,
+                                             uint64_t* __restrict__ stamps, int batch_index,
+                                             uint64_t* __restrict__ dev_alloc, int64_t* __restrict__ numa_alloc,
+                                             Row* __restrict__ touched_out, int32_t* __restrict__ touched_cnt,
+                                             uint64_t* __restrict__ pst);
+
+// One batch: prologue on every thread of the workgroup (the batch's pods and exact candidate lists
+// into LDS), replay on wave 0 (the other waves skip it).
+template <bool DS, bool NUMA, bool QUOTA>
+__device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const SoA& s, const DevPod* __restrict__ pods,
+                                              const int base, const int B, const KArgs& k,
+                                              const uint32_t* __restrict__ cand, const int32_t* __restrict__ cand_cnt,
+                                              int32_t* __restrict__ chosen, int32_t* __restrict__ chosen_score,
+                                              int32_t global_offset, uint64_t* __restrict__ stamps,
+                                              uint64_t* __restrict__ pstamps, int batch_index,
+                                              uint64_t* __restrict__ dev_alloc, int64_t* __restrict__ numa_alloc,
+                                              Row* __restrict__ touched_out = nullptr,
+                                              int32_t* __restrict__ touched_cnt = nullptr) {
   const int tid = threadIdx.x;
-  if (tid == 0) pstamps[8 * batch_index] = __builtin_amdgcn_s_memrealtime();
-  uint32_t* const s_cand = L.cand;
-  int16_t* const s_cand_slot = L.cand_slot;
-  int32_t* const s_hkey = L.hkey;
-  int16_t* const s_hval = L.hval;
-  LdsRow* const s_row = L.row;
-  int32_t* const s_slot_node = L.slot_node;
-  uint8_t* const s_changed = L.changed;
-  DevPod* const s_pod = L.pod;
-  int32_t* const s_cnt = L.cnt;
-  int32_t& s_nslots = L.nslots;
-  const int B = batch_pods;
-
-  // ---- prologue (all RES_THREADS threads): candidates, distinct-node slots, row prefetch ----
   constexpr int RES_THREADS = res_threads<NUMA>();
+  if (tid == 0) pstamps[8 * batch_index] = __builtin_amdgcn_s_memrealtime();
   if (tid < B) {
-    s_cnt[tid] = cand_cnt[tid];
-    s_pod[tid] = pods[base + tid];
+    L.cnt[tid] = ld_sc1(cand_cnt + tid);
+    L.pod[tid] = pods[base + tid];
   }
-  for (int t = tid; t < HASH_SLOTS; t += RES_THREADS) s_hkey[t] = HASH_EMPTY;
-  for (int t = tid; t < RES_SLOTS; t += RES_THREADS) s_changed[t] = 0;
-  if (tid == 0) s_nslots = 0;
   __syncthreads();
-  if (tid == 0) pstamps[8 * batch_index + 1] = __builtin_amdgcn_s_memrealtime();
-  // candidate keys -> LDS: 16-byte loads, all issued before any use
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(cand);
-    uint4* dst = reinterpret_cast<uint4*>(s_cand);
-    const int n4 = B * KMAX / 4;
-    constexpr int U = MAX_BATCH * KMAX / 4 / RES_THREADS;
-    uint4 q[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) q[u] = src[min(u * RES_THREADS + tid, n4 - 1)];  // unconditional
+  {  // candidate keys (sc1: k_fixup of a concurrent launch wrote them), unused slots zeroed
+    constexpr int U = MAX_BATCH * KMAX / RES_THREADS;
+    uint32_t q[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int t = u * RES_THREADS + tid;
-      if (t < n4) {
-        const int j = (t * 4) / KMAX, c = (t * 4) % KMAX, cnt = s_cnt[j];
-        q[u].x = c + 0 < cnt ? q[u].x : 0u;
-        q[u].y = c + 1 < cnt ? q[u].y : 0u;
-        q[u].z = c + 2 < cnt ? q[u].z : 0u;
-        q[u].w = c + 3 < cnt ? q[u].w : 0u;
-        dst[t] = q[u];
-      }
+      const int t = u * RES_THREADS + tid, j = t / KMAX, c = t % KMAX;
+      q[u] = (j < B && c < L.cnt[j]) ? ld_sc1(cand + t) : 0u;
     }
-  }
-  __syncthreads();
-  if (tid == 0) pstamps[8 * batch_index + 2] = __builtin_amdgcn_s_memrealtime();
-  for (int t = tid; t < B * KMAX; t += RES_THREADS) {
-    const uint32_t key = s_cand[t];
-    if (key) {  // insert the node; the first inserter of a node draws its row slot
-      const int node = key_node(key);
-      int h = hash_of(node);
-      while (true) {
-        const int prev = atomicCAS(&s_hkey[h], HASH_EMPTY, node);
-        if (prev == HASH_EMPTY) {
-          const int sl = atomicAdd(&s_nslots, 1);
-          s_hval[h] = (int16_t)(sl < RES_ROWS ? sl : -1);
-          if (sl < RES_ROWS) s_slot_node[sl] = node;
-          break;
-        }
-        if (prev == node) break;
-        h = (h + 1) & (HASH_SLOTS - 1);
-      }
-    }
-  }
-  __syncthreads();
-  if (tid == 0) pstamps[8 * batch_index + 3] = __builtin_amdgcn_s_memrealtime();
-  const int n_pref = min(s_nslots, RES_ROWS);
-  for (int t = tid; t < B * KMAX; t += RES_THREADS) {  // candidate -> row slot
-    const uint32_t key = s_cand[t];
-    int16_t sl = -1;
-    if (key) {
-      const int node = key_node(key);
-      int h = hash_of(node);
-      while (s_hkey[h] != node) h = (h + 1) & (HASH_SLOTS - 1);
-      sl = s_hval[h];
-    }
-    s_cand_slot[t] = sl;
-  }
-  if (tid == 0) pstamps[8 * batch_index + 5] = __builtin_amdgcn_s_memrealtime();
-  if (n_pref > 0) {  // rows of the distinct candidates: unconditional (clamped) gathers, 8 in flight
-    constexpr int W = NUM_I64_FIELDS + 1;
-    const int total = n_pref * W;
-    for (int t0 = 0; t0 < total; t0 += RES_THREADS * 8) {
-      int64_t v[8];
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int t = min(t0 + u * RES_THREADS + tid, total - 1);
-        const int sl = t / W, f = t % W;
-        const int node = s_slot_node[sl];
-        const int64_t a = s.f[(int64_t)min(f, NUM_I64_FIELDS - 1) * s.stride + node];
-        const uint32_t fl = s.flags[node];
-        v[u] = f < NUM_I64_FIELDS ? a : (int64_t)fl;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int t = t0 + u * RES_THREADS + tid;
-        if (t < total) {
-          const int sl = t / W, f = t % W;
-          if (f < NUM_I64_FIELDS) s_row[sl].f[f] = v[u];
-          else s_row[sl].flags = (uint32_t)v[u];
-        }
-      }
-    }
+    for (int u = 0; u < U; u++) L.cand[u * RES_THREADS + tid] = q[u];
   }
   __syncthreads();
-  if (tid == 0) pstamps[8 * batch_index + 4] = __builtin_amdgcn_s_memrealtime();
+  if (tid == 0) {
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    for (int u = 1; u < 6; u++) pstamps[8 * batch_index + u] = t;
+  }
   if (tid >= 64) return;  // the replay is one wavefront: wave-level ordering only from here on
   // the next batch's eval waves may share this SIMD (pipelined schedule): the replay issues first
   __builtin_amdgcn_s_setprio(3);
-  replay_batch<DS, NUMA, QUOTA>(L, s, base, B, k, chosen, chosen_score, global_offset, stamps, batch_index, dev_alloc,
-                                numa_alloc);
+  replay_batch<DS, NUMA, QUOTA>(L, C, s, base, B, k, chosen, chosen_score, global_offset, stamps, batch_index,
+                                dev_alloc, numa_alloc, touched_out, touched_cnt, pstamps + 8 * batch_index);
   __builtin_amdgcn_s_setprio(0);
 }
 
 // The sequential replay of one batch (wave 0).
+//   Lane c owns the c-th node changed in this batch: its row lives in that lane's registers, so the
+//   per-pod re-evaluation of every changed node is one register-only eval across the lanes.  Per pod j:
+//   the best unchanged candidate bu (wave max over its list minus the changed nodes), the exact score
+//   of every changed node, the better of the two, Reserve on the owner lane.  The row of bu's node is
+//   fetched from the SoA by the next free lane at the start of the pod, into spare registers, so its
+//   latency hides under the re-evaluation; it becomes that lane's row if bu wins.  Pod j+1's record
+//   and candidates are read during pod j, its changed flags right after pod j's Reserve.
 template <bool DS, bool NUMA, bool QUOTA>
-__device__ __forceinline__ void replay_batch(ResLds& L, const SoA& s, const int base, const int B, const KArgs& k,
-                                             int32_t* __restrict__ chosen, int32_t* __restrict__ chosen_score,
-                                             int32_t global_offset, uint64_t* __restrict__ stamps, int batch_index,
-                                             uint64_t* __restrict__ dev_alloc, int64_t* __restrict__ numa_alloc) {
+__device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const SoA& s, const int base, const int B,
+                                             const KArgs& k, int32_t* __restrict__ chosen,
+                                             int32_t* __restrict__ chosen_score, int32_t global_offset,
+                                             uint64_t* __restrict__ stamps, int batch_index,
+                                             uint64_t* __restrict__ dev_alloc, int64_t* __restrict__ numa_alloc,
+                                             Row* __restrict__ touched_out, int32_t* __restrict__ touched_cnt,
+                                             uint64_t* __restrict__ pst) {
   const uint32_t* const s_cand = L.cand;
-  const int16_t* const s_cand_slot = L.cand_slot;
-  int32_t* const s_hkey = L.hkey;
-  int16_t* const s_hval = L.hval;
-  const LdsRow* const s_row = L.row;
-  int32_t* const s_slot_node = L.slot_node;
-  uint8_t* const s_changed = L.changed;
   const DevPod* const s_pod = L.pod;
   const int lane = threadIdx.x & 63;
-
-  // ---- sequential replay of the batch ----
-  // Lane c owns the c-th node changed in this batch: its row lives in that lane's registers, so the
-  // per-pod re-evaluation of every changed node is one register-only eval across the lanes.
-  // Software-pipelined so that no LDS round trip sits on the per-pod critical path: pod j+1's record,
-  // candidates and row slots are read while pod j is replayed, its changed flags right after pod j's
-  // Reserve (consumed one iteration later), and the row of pod j's best unchanged candidate is
-  // fetched into spare registers before the re-evaluation, for the owner lane to take if it wins.
-  int n_chg = 0, n_ovf = 0;
+  int n_chg = 0, n_fetch = 0;
   NodeRegs mine;
+  Row spare;  // lane n_chg: the row of the pod's best unchanged candidate
   int my_node = -1;
   bool my_expired = false;
   int32_t o_node = -1, o_score = -1;  // lane j: pod j's placement
@@ -2258,22 +2227,14 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const SoA& s, const int 
       }
   DevPod pod = s_pod[0];
   uint32_t ck = s_cand[lane];
-  int csl = s_cand_slot[lane];
-  bool chg = false;  // prefetched changed flag of this lane's candidate (pods < j)
+  bool chg = false;  // changed flag of this lane's candidate (pods < j); nothing is changed at j = 0
   for (int j = 0; j < B; j++) {
     const bool more = j + 1 < B;
     const DevPod pod_n = s_pod[more ? j + 1 : j];
     const uint32_t ck_n = more ? s_cand[(j + 1) * KMAX + lane] : 0u;
-    int csl_n = s_cand_slot[(more ? j + 1 : j) * KMAX + lane];
-    const bool in_chg = chg;
-    const uint32_t bu = wave_max_u32(in_chg ? 0u : ck);  // best unchanged snapshot candidate
-    int slot = -1;
-    LdsRow nxt;
-    if (bu != 0) {
-      const int src = __ffsll((unsigned long long)__ballot(ck == bu && !in_chg)) - 1;
-      slot = __builtin_amdgcn_readlane(csl, src);
-      if (slot >= 0) nxt = s_row[slot];  // wave-uniform address: a broadcast read
-    }
+    const uint32_t bu = wave_max_u32(chg ? 0u : ck);  // best unchanged snapshot candidate
+    if (bu != 0 && lane == n_chg) load_row_sc1(s, key_node(bu), spare);
+    n_fetch += bu != 0;
     uint32_t kc = 0;  // exact re-evaluation of the nodes changed earlier in this batch
     if (lane < n_chg) {
       NumaNode nv;
@@ -2292,25 +2253,13 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const SoA& s, const int 
       if (w == bc) {
         owner = __ffsll((unsigned long long)__ballot(lane < n_chg && kc == w)) - 1;
       } else {
-        const int node = key_node(w);
         owner = n_chg++;
-        if (slot < 0) {  // chosen node missed the prefetch: overflow row from the SoA
-          slot = RES_ROWS + n_ovf++;
-          if (lane == owner) {
-            load_row(s, node, mine);
-            s_slot_node[slot] = node;
-            int h = hash_of(node);
-            while (s_hkey[h] != node) h = (h + 1) & (HASH_SLOTS - 1);
-            s_hval[h] = (int16_t)slot;
-          }
-        } else if (lane == owner) {
-          regs_from_lds(nxt, mine);
-        }
         if (lane == owner) {
+          regs_from_row(spare, mine);
           prepare_row(mine);
-          my_node = node;
+          my_node = key_node(w);
           my_expired = node_expired(mine, k);
-          s_changed[slot] = 1;
+          chg_set(C, my_node);
         }
       }
       // Reserve: LoadAware assign (the new pod has no PodMetric -> counted at its estimate in every
@@ -2361,23 +2310,13 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const SoA& s, const int 
 #pragma unroll
       for (int t = 0; t < 16; t++) numa_alloc[(int64_t)(base + j) * 16 + t] = 0;
     }
-    // pod j+1's changed flags (row slots of unprefetched candidates: overflow hash), read after this
-    // Reserve's own LDS writes (in order within the wave), so they already include pod j's new node
-    bool chg_n = false;
-    if (ck_n) {
-      if (csl_n < 0) {
-        const int node = key_node(ck_n);
-        int h = hash_of(node);
-        while (s_hkey[h] != node) h = (h + 1) & (HASH_SLOTS - 1);
-        csl_n = s_hval[h];
-      }
-      chg_n = csl_n >= 0 && s_changed[csl_n];
-    }
+    // pod j+1's changed flags, read after this Reserve's bitmap update (LDS ops of a wave execute in
+    // order), so they already include pod j's new node
+    const bool chg_n = ck_n != 0 && chg_test(C, key_node(ck_n));
     if (NUMA) wave_lds_sync();  // the next re-evaluation reads the zones this Reserve patched
-    else __atomic_signal_fence(__ATOMIC_SEQ_CST);  // LDS ops of one wave execute in order
+    else __atomic_signal_fence(__ATOMIC_SEQ_CST);
     pod = pod_n;
     ck = ck_n;
-    csl = csl_n;
     chg = chg_n;
   }
   if (lane < B) {
@@ -2393,21 +2332,50 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const SoA& s, const int 
         s.qt[(QF_USED + r) * QT_STRIDE + 64 * b + lane] = Q.u[b][r];
         s.qt[(QF_NP + r) * QT_STRIDE + 64 * b + lane] = Q.n[b][r];
       }
-  // write the patched rows back to the SoA
   if (lane < n_chg) {
+    // the patched rows back to the SoA (sc1: read by the next batches' evals on other CUs), and the
+    // compact list of them for the next batch's k_fixup (pipelined runs)
     const int64_t st = s.stride;
     int64_t* f = s.f + my_node;
 #pragma unroll
     for (int v = 0; v < 2; v++)
 #pragma unroll
       for (int q = 0; q < 2; q++) {
-        f[(F_FH + 2 * v + q) * st] = mine.fh[v][q];
-        f[(F_SA + 2 * v + q) * st] = mine.sa[v][q];
+        st_sc1(f + (F_FH + 2 * v + q) * st, mine.fh[v][q]);
+        st_sc1(f + (F_SA + 2 * v + q) * st, mine.sa[v][q]);
       }
-    f[(F_NREQ + 0) * st] = mine.nreq[0];
-    f[(F_NREQ + 1) * st] = mine.nreq[1];
+    st_sc1(f + (F_NREQ + 0) * st, mine.nreq[0]);
+    st_sc1(f + (F_NREQ + 1) * st, mine.nreq[1]);
+    if (touched_out) {
+      int64_t* r = reinterpret_cast<int64_t*>(touched_out + lane);
+      st_sc1(r + F_UT, mine.ut);
+#pragma unroll
+      for (int v = 0; v < 2; v++)
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+          st_sc1(r + F_FH + 2 * v + q, mine.fh[v][q]);
+          st_sc1(r + F_SA + 2 * v + q, mine.sa[v][q]);
+        }
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        st_sc1(r + F_CAP + q, mine.cap[q]);
+        st_sc1(r + F_NALLOC + q, mine.nalloc[q]);
+        st_sc1(r + F_NREQ + q, mine.nreq[q]);
+      }
+      st_sc1(r + F_CSM, mine.csm);
+      st_sc1(r + F_CSAF, mine.csaf);
+      st_sc1(r + F_CSAS, mine.csas);
+      st_sc1(r + NUM_I64_FIELDS, (int64_t)(((uint64_t)(uint32_t)my_node << 32) | mine.flags));
+    }
+    chg_clear_word(C, my_node);  // the bitmap is zero again for the next batch
   }
-  if (lane == 0) stamps[batch_index + 1] = __builtin_amdgcn_s_memrealtime();
+  if (touched_out && lane == 0) st_sc1(touched_cnt, (int32_t)n_chg);
+  if (lane == 0) {
+    stamps[batch_index + 1] = __builtin_amdgcn_s_memrealtime();
+    pst[6] = (uint64_t)n_fetch;  // candidate rows fetched from the SoA
+    pst[7] = (uint64_t)n_chg;    // rows changed (written back)
+  }
+  drain_stores();  // every hand-off store is performed before the workgroup publishes the batch
 }
 
 template <bool DS, bool NUMA, bool QUOTA>
@@ -2417,18 +2385,19 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(SoA s, const De
                                                 int32_t* __restrict__ chosen_score, int32_t global_offset,
                                                 uint64_t* __restrict__ stamps, uint64_t* __restrict__ pstamps,
                                                 int batch_index, uint64_t* __restrict__ dev_alloc,
-                                                int64_t* __restrict__ numa_alloc) {
+                                                int64_t* __restrict__ numa_alloc, uint32_t* __restrict__ chg_glb,
+                                                int n_nodes) {
   __shared__ ResLds L;
-  resolve_batch<DS, NUMA, QUOTA>(L, s, pods, *batch_base, batch_pods, k, cand, cand_cnt, chosen, chosen_score,
+  const ChgSet C = chg_init(L, chg_glb, n_nodes);
+  resolve_batch<DS, NUMA, QUOTA>(L, C, s, pods, *batch_base, batch_pods, k, cand, cand_cnt, chosen, chosen_score,
                                  global_offset, stamps, pstamps, batch_index, dev_alloc, numa_alloc);
 }
 
 // Persistent Reserve chain of a run of pipelined plain batches [b0, b0 + nb): one
 // workgroup for the whole run, so no kernel boundary or cross-stream event sits between two batches.
 // Per batch: wait until k_fixup published every pod's exact list (ready[b] == pods of b), resolve it,
-// then publish done[b] (rows, placements) with an agent-scope release for the fixup of batch b+1 and
-// the eval of batch b+2.  Every wait is bounded (wait_at_least); on a timeout the run stops and the
-// error word tells the host.
+// then publish done[b] (rows, placements, the changed-row list).  Every wait is bounded
+// (wait_at_least); on a timeout the run stops and the error word tells the host.
 template <bool QUOTA>
 __global__ __launch_bounds__(res_threads<false>()) void k_resolve_run(SoA s, const DevPod* __restrict__ pods,
                                                                       const int32_t* __restrict__ bases, int b0, int nb,
@@ -2440,18 +2409,22 @@ __global__ __launch_bounds__(res_threads<false>()) void k_resolve_run(SoA s, con
                                                                       uint64_t* __restrict__ pstamps,
                                                                       uint64_t* __restrict__ dev_alloc,
                                                                       const int32_t* __restrict__ ready,
-                                                                      int32_t* __restrict__ done, int32_t* __restrict__ err) {
+                                                                      int32_t* __restrict__ done, int32_t* __restrict__ err,
+                                                                      Row* __restrict__ touched_out,
+                                                                      int32_t* __restrict__ touched_cnt,
+                                                                      uint32_t* __restrict__ chg_glb, int n_nodes) {
   __shared__ ResLds L;
   __shared__ int32_t s_ok;
+  const ChgSet C = chg_init(L, chg_glb, n_nodes);
   for (int b = b0; b < b0 + nb; b++) {
     const int base = bases[b], B = bases[b + 1] - bases[b];
     if (threadIdx.x == 0) s_ok = wait_at_least(ready + b, B, err);
     __syncthreads();
     if (!s_ok) return;
-    resolve_batch<false, false, QUOTA>(L, s, pods, base, B, k, cand, cand_cnt, chosen, chosen_score, global_offset,
-                                       stamps, pstamps, b, dev_alloc, nullptr);
-    __syncthreads();  // wave 0's replay, row write-back and placements are done (drained at the barrier)
-    if (threadIdx.x == 0) __hip_atomic_store(done + b, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    resolve_batch<false, false, QUOTA>(L, C, s, pods, base, B, k, cand, cand_cnt, chosen, chosen_score, global_offset,
+                                       stamps, pstamps, b, dev_alloc, nullptr, touched_out, touched_cnt);
+    __syncthreads();  // wave 0 drained its stores (replay_batch), so they are performed
+    if (threadIdx.x == 0) st_sc1(done + b, 1);
   }
 }
 
@@ -2716,6 +2689,8 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
   dev_alloc[base] = alloc;
   for (int q = 0; q < 4; q++) cpusets[(int64_t)base * 4 + q] = set[q];
   for (int u = 0; u < 6; u++) pstamps[8 * batch_index + u] = t0;  // no prologue: all "replay"
+  pstamps[8 * batch_index + 6] = 1;
+  pstamps[8 * batch_index + 7] = out_node >= 0;
   stamps[batch_index + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -2786,6 +2761,9 @@ struct DeviceState {
   // pipelined schedule: eval + select run on `estream` one batch ahead of the Reserve chain on `stream`
   hipStream_t estream = nullptr;
   uint32_t* d_stale = nullptr;      // [2][MAX_BATCH][KSTALE] stale-snapshot candidate lists
+  uint32_t* d_chg = nullptr;        // changed-node bitmap of the replay when node ids exceed its LDS copy
+  Row* d_trows = nullptr;           // [MAX_BATCH] rows the last resolved batch changed (node in .pad)
+  int32_t* d_tcnt = nullptr;        // their count
   int32_t* d_stale_cnt = nullptr;   // [2][MAX_BATCH]
   static constexpr int EV_RING = 8;
   hipEvent_t ev_res[EV_RING] = {};  // a batch's Reserve done (stream)
@@ -2845,6 +2823,12 @@ int device_create(Context* ctx) {
   HIP_OK(hipMemsetAsync(d->d_batch_base, 0, sizeof(int32_t), d->stream));
   HIP_OK(hipMalloc(&d->d_stale, sizeof(uint32_t) * 2 * MAX_BATCH * KSTALE));
   HIP_OK(hipMalloc(&d->d_stale_cnt, sizeof(int32_t) * 2 * MAX_BATCH));
+  HIP_OK(hipMalloc(&d->d_trows, sizeof(Row) * MAX_BATCH));
+  HIP_OK(hipMalloc(&d->d_tcnt, sizeof(int32_t)));
+  if (d->capacity > (int64_t)CHG_LDS_WORDS * 32) {  // zero between batches (each replay clears its bits)
+    HIP_OK(hipMalloc(&d->d_chg, sizeof(uint32_t) * (d->capacity + 31) / 32));
+    HIP_OK(hipMemsetAsync(d->d_chg, 0, sizeof(uint32_t) * (d->capacity + 31) / 32, d->stream));
+  }
   HIP_OK(hipMalloc(&d->d_dsraw, sizeof(uint16_t) * d->capacity));
   HIP_OK(hipMalloc(&d->d_dsmax, sizeof(uint32_t) * MAX_BATCH));
   HIP_OK(hipMalloc(&d->d_aff, d->capacity));
@@ -2864,7 +2848,7 @@ void device_destroy(Context* ctx) {
                   d->d_dsraw,   d->d_dsmax,  d->d_devalloc,   d->d_dsrows,       d->soa.nf,   d->soa.nm,
                   d->d_numaalloc, d->d_numarows, d->d_defer, d->d_defer_cnt, d->soa.cs, d->soa.cpu,
                   d->d_cpurows, d->d_cpusets, d->d_aff, d->soa.qt, d->soa.qm, d->d_sched, d->d_stale,
-                  d->d_stale_cnt};
+                  d->d_stale_cnt, d->d_trows, d->d_tcnt, d->d_chg};
   if (d->estream) (void)hipStreamSynchronize(d->estream);
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -3048,6 +3032,12 @@ static int ensure_cpu(Context* ctx) {
 // Re-derive rows of dirty / time-expired nodes and scatter them into the SoA.
 int device_refresh(Context* ctx, int64_t now) {
   DeviceState* d = ctx->dev;
+  if (!ctx->pending.empty())  // a row to derive needs the deferred host mirror first
+    for (int32_t i = 0; i < ctx->n_nodes; i++)
+      if (ctx->nodes[i].dirty || now >= ctx->nodes[i].valid_until) {
+        flush_mirror(*ctx);
+        break;
+      }
   int rc = ensure_ds(ctx);
   if (rc) return rc;
   rc = ensure_numa(ctx);
@@ -3244,15 +3234,22 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
 
 int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t* chosen, int32_t* score) {
   DeviceState* d = ctx->dev;
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
+  auto tp = clk::now();
   HIP_OK(hipSetDevice(d->device));
   int rc = device_refresh(ctx, now);
   if (rc) return rc;
+  ctx->host_ms[1] = ms_since(tp);
   ctx->last_batch_ms.clear();
   ctx->last_dev_alloc.clear();
   ctx->last_total_ms = 0;
   if (n_pods == 0) return KE_OK;
+  tp = clk::now();
   rc = upload_pods(ctx, n_pods, pods);
   if (rc) return rc;
+  ctx->host_ms[2] = ms_since(tp);
+  tp = clk::now();
   // Batches: runs of up to B pods without DeviceShare requests (exact speculative batching, DESIGN.md
   // §4), and every DeviceShare pod alone: its NormalizeScore needs the max over all feasible nodes of
   // the current state.
@@ -3452,6 +3449,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   // re-evaluates the nodes it chose and publishes the exact lists.  Any other batch (DeviceShare /
   // cpuset singletons, NUMA-policy contexts, pipeline off) is serial: its eval waits for the previous
   // batch's Reserve (HIP events), its lists are exact, its Reserve kernel waits for its lists.
+  ctx->host_ms[3] = ms_since(tp);
   const auto host_t0 = std::chrono::steady_clock::now();
   for (int b = 0; b < n_batches;) {
     if (run_end[b] > 0) {
@@ -3459,16 +3457,15 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       hipLaunchKernelGGL((quota ? k_resolve_run<true> : k_resolve_run<false>), dim3(1), dim3(res_threads<false>()), 0,
                          d->stream, d->soa, d->d_pods, d_bases, r0, e - r0, k, d->d_cand, d->d_cand_cnt, d->d_chosen,
                          d->d_chosen_score, ctx->cfg.global_node_offset, d->d_stamps, d->d_stamps + (n_pods + 2),
-                         d->d_devalloc, d_ready, d_done, d_err);
+                         d->d_devalloc, d_ready, d_done, d_err, d->d_trows, d->d_tcnt, d->d_chg, N);
       if (r0 > 0) HIP_OK(hipStreamWaitEvent(d->estream, d->ev_res[(r0 - 1) % R], 0));
       for (int q = r0; q < e; q++) {
         rc = eval_select(q, true);
         if (rc) return rc;
         const bool first = q == r0;
-        hipLaunchKernelGGL(k_fixup, dim3((unsigned)batches[q].pods), dim3(FIX_BLOCK), 0, d->estream, d->soa, d->d_pods,
+        hipLaunchKernelGGL(k_fixup, dim3((unsigned)batches[q].pods), dim3(FIX_BLOCK), 0, d->estream, d->d_pods,
                            d_bases + q, k, d->d_stale + (size_t)(q & 1) * MAX_BATCH * KSTALE,
-                           d->d_stale_cnt + (q & 1) * MAX_BATCH, first ? nullptr : d->d_chosen + bases[q - 1],
-                           first ? 0 : batches[q - 1].pods, ctx->cfg.global_node_offset, d->d_cand, d->d_cand_cnt,
+                           d->d_stale_cnt + (q & 1) * MAX_BATCH, d->d_trows, d->d_tcnt, d->d_cand, d->d_cand_cnt,
                            d_done, first ? -1 : q - 1, d_ready + q, d_err, d_fst + 2 * q);
       }
       HIP_OK(hipEventRecord(d->ev_res[(e - 1) % R], d->stream));
@@ -3504,13 +3501,15 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                                  : (numa ? k_resolve<false, true, false> : k_resolve<false, false, false>));
       hipLaunchKernelGGL(resolve, dim3(1), dim3(numa ? res_threads<true>() : res_threads<false>()), 0, d->stream, d->soa, d->d_pods, bbase, bp, k,
                          d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score, ctx->cfg.global_node_offset,
-                         d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc, d->d_numaalloc);
+                         d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc, d->d_numaalloc, d->d_chg, N);
     }
     HIP_OK(hipEventRecord(d->ev_res[b % R], d->stream));
     b++;
   }
   HIP_OK(hipGetLastError());
-  ctx->last_enqueue_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - host_t0).count();
+  ctx->last_enqueue_ms = ctx->host_ms[4] = ms_since(host_t0);
+  tp = clk::now();
+  flush_mirror(*ctx);  // the previous call's deferred host mirror, while the device works
   HIP_OK(hipEventRecord(e1, d->stream));
   HIP_OK(hipMemcpyAsync(chosen, d->d_chosen, out_bytes, hipMemcpyDeviceToHost, d->stream));
   if (score) HIP_OK(hipMemcpyAsync(score, d->d_chosen_score, out_bytes, hipMemcpyDeviceToHost, d->stream));
@@ -3540,7 +3539,11 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   HIP_OK(hipMemcpyAsync(est.data(), estamps, sizeof(uint64_t) * n_batches, hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipStreamSynchronize(d->stream));
   HIP_OK(hipStreamSynchronize(d->estream));
+  ctx->host_ms[5] = ms_since(tp);
+  tp = clk::now();
   if (herr) {
+    if (d->d_chg)  // an abandoned replay may have left bits set
+      (void)hipMemset(d->d_chg, 0, sizeof(uint32_t) * (d->capacity + 31) / 32);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     for (auto& e : ev) (void)hipEventDestroy(e);
@@ -3596,6 +3599,13 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     }
   }
   ctx->kstat_resolve_ms = n_batches ? res_sum / n_batches : 0;
+  double rows_staged = 0, rows_changed = 0;
+  for (int b = 0; b < n_batches; b++) {
+    rows_staged += (double)pst[8 * (size_t)b + 6];
+    rows_changed += (double)pst[8 * (size_t)b + 7];
+  }
+  ctx->kstat_rows_staged = n_batches ? rows_staged / n_batches : 0;
+  ctx->kstat_rows_changed = n_batches ? rows_changed / n_batches : 0;
   ctx->kstat_fixup_ms = fx_n ? fx_sum / fx_n : 0;
   ctx->kstat_handoff_ms = ho_n ? ho_sum / ho_n : 0;
   ctx->kstat_samples = 0;
@@ -3613,6 +3623,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     ctx->kstat_eval_ms /= ctx->kstat_samples;
     ctx->kstat_select_ms /= ctx->kstat_samples;
   }
+  ctx->host_ms[6] = ms_since(tp);
   return KE_OK;
 }
 

@@ -215,8 +215,16 @@ class Evaluator:
         """Pipelined schedule (default): batch b's eval + select overlap batch b-1's Reserve replay."""
         self._check(self.lib.ke_set_pipeline(self.h, 1 if on else 0))
 
+    HOST_PHASES = ("checks", "refresh", "upload", "setup", "enqueue", "wait", "stats", "mirror")
+
+    def host_stats(self):
+        """Host wall ms of the last schedule() by phase (ke_last_host_stats)."""
+        ms = np.zeros(8, np.float64)
+        self._check(self.lib.ke_last_host_stats(self.h, abi.ptr(ms)))
+        return dict(zip(self.HOST_PHASES, ms.tolist()))
+
     def kernel_stats(self):
-        ms4 = np.zeros(6, np.float64)
+        ms4 = np.zeros(8, np.float64)
         n, npipe = abi.i32(), abi.i32()
         self._check(self.lib.ke_last_kernel_stats_ex(self.h, abi.ptr(ms4), C.byref(n), C.byref(npipe)))
         p, r = C.c_double(), C.c_double()
@@ -225,6 +233,7 @@ class Evaluator:
         self._check(self.lib.ke_debug_resolve_phases(self.h, abi.ptr(ph)))
         return {"eval_ms": ms4[0], "select_ms": ms4[1], "fixup_ms": ms4[2], "resolve_ms": ms4[3], "samples": n.value,
                 "pipelined_batches": npipe.value, "enqueue_ms": ms4[4], "handoff_ms": ms4[5],
+                "rows_staged": ms4[6], "rows_changed": ms4[7],
                 "resolve_prologue_ms": p.value, "resolve_replay_ms": r.value,
                 "resolve_phases_ms": dict(zip(["init", "cand_copy", "hash", "lookup", "rows", "replay"],
                                               ph.tolist()))}
