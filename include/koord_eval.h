@@ -570,6 +570,13 @@ int ke_last_resolve_split(ke_ctx* ctx, double* prologue_ms, double* replay_ms);
  * pass (no preferred merged hint). */
 int ke_debug_numa_deferred(ke_ctx* ctx, int64_t* n);
 int ke_debug_resolve_phases(ke_ctx* ctx, double* phases6);
+/* Diagnostic build only (-DKE_PROF_REPLAY): shader cycles per pod of the replay loop's phases since the
+ * last call — best unchanged candidate, row fetch issue, re-evaluation, its wave max, decision / adoption,
+ * Reserve, next pod's changed flags — and the pod count (cyc8[7]); zeros in the product build. */
+int ke_debug_replay_phases(ke_ctx* ctx, double* cyc8);
+/* Number of nodes whose replay record (the Reserve replay's row-major copy of the node-only terms)
+ * differs from one derived from the node's current device row (0 = consistent). */
+int ke_debug_check_records(ke_ctx* ctx, int64_t now_ns, int64_t* mismatched_nodes);
 /* Launch the batch eval kernel `iters` times back to back over the current node SoA for `n_pods`
  * (<= 64) pods and return the HIP-event average milliseconds per launch (roofline measurement). */
 int ke_bench_eval_kernel(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int32_t iters,

@@ -19,6 +19,8 @@ int device_quota_sync(Context* ctx);
 int device_debug_rows(Context* ctx, int32_t n, Row* out);
 int device_set_profiling(Context* ctx, int32_t every);
 int device_set_pipeline(Context* ctx, int32_t on);
+int device_replay_phases(Context* ctx, double* cyc8);
+int device_check_records(Context* ctx, int64_t now, int64_t* bad);
 int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t iters, double* avg_ms);
 int device_comm_unique_id(uint8_t* id);
 int device_shard_init(Context* ctx, int rank, int world, const uint8_t* id);
@@ -514,6 +516,21 @@ int ke_last_kernel_stats_ex(ke_ctx* ctx, double* ms4 /* [8] */, int32_t* samples
   ms4[6] = ctx->c.kstat_rows_staged;
   ms4[7] = ctx->c.kstat_rows_changed;
   return KE_OK;
+}
+
+int ke_debug_replay_phases(ke_ctx* ctx, double* cyc8) {
+  if (!ctx || !cyc8) return fail(KE_ERR_INVALID, "ke_debug_replay_phases arguments");
+  int rc = require_device(ctx);
+  if (rc) return rc;
+  return device_replay_phases(&ctx->c, cyc8);
+}
+
+int ke_debug_check_records(ke_ctx* ctx, int64_t now_ns, int64_t* mismatched_nodes) {
+  if (!ctx || !mismatched_nodes) return fail(KE_ERR_INVALID, "ke_debug_check_records arguments");
+  flush_mirror(ctx->c);
+  int rc = require_device(ctx);
+  if (rc) return rc;
+  return device_check_records(&ctx->c, now_ns, mismatched_nodes);
 }
 
 int ke_set_pipeline(ke_ctx* ctx, int32_t on) {

@@ -62,6 +62,7 @@ struct SoA {
   CpuRec* cpu;      // CPU tables: CPU_SLOTS records per node, node-major
   int64_t* qt;      // ElasticQuota: NUM_QF arrays of QT_STRIDE int64 (nullptr until a tree is loaded)
   int32_t* qm;      // ElasticQuota: QT_STRIDE meta words (ke_types.h qm_*)
+  int64_t* rec;     // replay records: NUM_RW int64 words per node, row-major (RecWord)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -1312,10 +1313,342 @@ __device__ __forceinline__ int32_t lite_total(const NodeRegs& n, bool expired, c
   return fail ? -1 : k.wp_la * la + k.wp_numa * nu;
 }
 
+// a packed row into registers
+__device__ __forceinline__ void regs_from_row(const Row& r, NodeRegs& n) {
+  n.ut = r.f[F_UT];
+#pragma unroll
+  for (int v = 0; v < 2; v++)
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      n.fh[v][q] = r.f[F_FH + 2 * v + q];
+      n.sa[v][q] = r.f[F_SA + 2 * v + q];
+    }
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    n.cap[q] = r.f[F_CAP + q];
+    n.nalloc[q] = r.f[F_NALLOC + q];
+    n.nreq[q] = r.f[F_NREQ + q];
+  }
+  n.csm = r.f[F_CSM];
+  n.csaf = r.f[F_CSAF];
+  n.csas = r.f[F_CSAS];
+  n.flags = r.flags;
+}
+
+// Words one workgroup hands to another while both run (k_fixup -> k_resolve_run: the exact lists;
+// k_resolve_run -> k_fixup: the changed rows; -> later eval launches: the patched SoA rows) are
+// written and read with sc1 (relaxed agent-scope atomics: global_store / global_load ... sc1), i.e.
+// write-through past the storing CU and read past the reading CU's L1: no release (L2 write-back) and
+// no acquire (L1/L2 invalidate) fence on the hand-off path (MI355X_MICROARCH.md § visibility,
+// cdna_hip_programming.md Guideline 16).  The storing wave drains (vmcnt(0)) before the flag.
+__device__ __forceinline__ int64_t ld_sc1(const int64_t* p) {
+  return __hip_atomic_load(const_cast<int64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
+  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int32_t ld_sc1(const int32_t* p) {
+  return __hip_atomic_load(const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drain_stores() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
+
+// ---- the replay's fast path: per-node records with the node-only terms precomputed --------------
+// In the replay a changed node is re-evaluated for every later pod of its batch, while its row changes
+// only at its own Reserves; and almost every pod adopts a node it has not touched yet.  Each node
+// therefore has a row-major replay record (NUM_RW words, RecWord) next to the SoA: the static node-only
+// terms of lite_total (KArgs weights, capacities as doubles with their reciprocals, flag bits) and the
+// Reserve-dependent ones (the LoadAware filter headrooms, score bases and NodeInfo.Requested as exact
+// doubles).  k_scatter_rows derives it with the row, every Reserve rewrites it.  Adopting a node is 13
+// contiguous 16-byte loads plus the `now`-dependent bits; re-evaluating it (fast_total) is a handful of
+// compares and four exact x*100/c divisions.  Doubles are exact: every value is an integer below 2^53
+// (ingestion rejects larger quantities) and only sums / differences of them are formed.
+constexpr int64_t THR_NONE = INT64_MAX;
+enum : uint32_t {
+  FB_FAIL = 1u,       // not a valid node
+  FB_EXP_FAIL = 2u,   // LoadAware: NodeMetric expired and FilterExpiredNodeMetrics (non-DaemonSet pods)
+  FB_AMP_BAD = 4u,    // filterAmplifiedCPUs fails for any cpu request (unparsable ratio / invalid topology)
+  FB_LAS = 8u,        // LoadAware Score computes (metric present, not expired, NodeMetric set, weights)
+  FB_NZERO = 16u,     // NodeNUMAResource Score is 0 (getResourceOptions error)
+  FB_RSZERO = 32u,    // ... when the pod requests cpu (score ratio > 1 with an invalid topology)
+  FB_CAP0 = 64u,      // 2 bits: EstimateNode allocatable > 0 per resource
+  FB_AL0 = 256u,      // 2 bits: NodeInfo.Allocatable != 0 per resource
+  FB_SLOW = 1024u,    // a capacity >= 2^42: x*100/c in int64 (outside the reciprocal estimate's range)
+  FB_RF = 2048u,      // filterAmplifiedCPUs checks the amplified room (ratio > 1, parsable, valid topology)
+};
+// record words (int64 / double)
+enum RecWord : int {
+  RW_FH = 0,       // 4: LoadAware filter headroom fh[variant][res] (int64)
+  RW_SA = 4,       // 4: LoadAware score base sa[variant][res] (double)
+  RW_CAP = 8,      // 2: EstimateNode allocatable (double)
+  RW_RCAP = 10,    // 2: its approximate reciprocal
+  RW_AL = 12,      // 2: NodeInfo.Allocatable (double)
+  RW_RAL = 14,     // 2: its approximate reciprocal
+  RW_NREQ = 16,    // 2: NodeInfo.Requested (double)
+  RW_NREQ0S = 18,  // cpu requested, cpuset CPUs at the score amplification (double)
+  RW_NALLOC0 = 19, // cpu allocatable (int64), RW_CSM / RW_CSAF: cpuset milli and its filter amplification
+  RW_CSM = 20,
+  RW_CSAF = 21,
+  RW_UT = 22,      // NodeMetric UpdateTime
+  RW_FLAGS = 23,   // node flags (low 32) | static FB_* bits (high 32)
+  RW_NWS = 24,     // Σ NUMA score weights over resources with allocatable != 0
+  RW_PAD = 25,
+  NUM_RW = 26
+};
+static_assert(NUM_RW % 2 == 0, "records are 16-byte granules");
+
+struct NodeFast {
+  int64_t fh[2][2];
+  double sa[2][2];
+  double cap[2], rcap[2], al[2], ral[2];
+  double nreq[2], nreq0s;
+  int64_t nalloc0, csm, csaf, ut;
+  uint32_t nflags, sbits;  // node flags, static FB bits
+  int32_t nws;
+  // derived at adoption / after each Reserve
+  int64_t thr[2][2];  // [pod is prod][res]: LoadAware filter passes iff est <= thr (THR_NONE = no check)
+  int64_t amp_room;   // filterAmplifiedCPUs passes iff req0 <= amp_room (THR_NONE = no check)
+  uint32_t bits;      // sbits + the `now`-dependent FB bits
+  bool thr_node;      // the LoadAware filter thresholds apply (metric, not expired-filtered, NodeMetric set)
+};
+
+// the record of a prepared row (rcap / ralloc set), static bits from the args
+__device__ __forceinline__ void rec_from_regs(const NodeRegs& n, const KArgs& k, int64_t (&w)[NUM_RW]) {
+  const uint32_t nf = n.flags;
+  uint32_t b = 0;
+  b |= !(nf & NF_VALID) ? FB_FAIL : 0u;
+  b |= ((nf & NF_NUMA_AMP_ERR) || ((nf & NF_NUMA_RATIO_F) && (nf & NF_NUMA_TOPO_INVALID))) ? FB_AMP_BAD : 0u;
+  b |= (!(nf & NF_NUMA_AMP_ERR) && (nf & NF_NUMA_RATIO_F) && !(nf & NF_NUMA_TOPO_INVALID)) ? FB_RF : 0u;
+  b |= (nf & NF_NUMA_SCORE_ZERO) ? FB_NZERO : 0u;
+  b |= ((nf & NF_NUMA_RATIO_S) && (nf & NF_NUMA_TOPO_INVALID)) ? FB_RSZERO : 0u;
+  int32_t nws = 0;
+  for (int q = 0; q < 2; q++) {
+    b |= n.cap[q] > 0 ? (FB_CAP0 << q) : 0u;
+    b |= n.nalloc[q] != 0 ? (FB_AL0 << q) : 0u;
+    nws += (n.nalloc[q] != 0 && k.w_numa[q] != 0) ? k.w_numa[q] : 0;
+    // the reciprocal division's range: 0 < c < 2^42 (x <= 16c holds: x <= sa <= cap for LoadAware,
+    // x <= alloc for the NUMA scorers)
+    if ((n.cap[q] > 0 && n.cap[q] >= DIV_FAST_CAP) || n.nalloc[q] < 0 || n.nalloc[q] >= DIV_FAST_CAP) b |= FB_SLOW;
+  }
+  for (int v = 0; v < 2; v++)
+    for (int q = 0; q < 2; q++) {
+      w[RW_FH + 2 * v + q] = n.fh[v][q];
+      w[RW_SA + 2 * v + q] = __double_as_longlong((double)n.sa[v][q]);
+    }
+  for (int q = 0; q < 2; q++) {
+    w[RW_CAP + q] = __double_as_longlong(n.dcap[q]);
+    w[RW_RCAP + q] = __double_as_longlong(n.rcap[q]);
+    w[RW_AL + q] = __double_as_longlong(n.dalloc[q]);
+    w[RW_RAL + q] = __double_as_longlong(n.ralloc[q]);
+    w[RW_NREQ + q] = __double_as_longlong((double)n.nreq[q]);
+  }
+  w[RW_NREQ0S] = __double_as_longlong((nf & NF_NUMA_RATIO_S) ? (double)(n.nreq[0] - n.csm + n.csas) : (double)n.nreq[0]);
+  w[RW_NALLOC0] = n.nalloc[0];
+  w[RW_CSM] = n.csm;
+  w[RW_CSAF] = n.csaf;
+  w[RW_UT] = n.ut;
+  w[RW_FLAGS] = (int64_t)(((uint64_t)b << 32) | nf);
+  w[RW_NWS] = nws;
+  w[RW_PAD] = 0;
+}
+
+// the LoadAware filter bounds and the amplified room from the current headrooms / requested
+__device__ __forceinline__ void fast_bounds(NodeFast& f) {
+  const uint32_t nf = f.nflags;
+  const bool v1 = (nf & NF_HAS_PROD_THR) != 0;  // the prod pods' profile (register selects, no indexing)
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    f.thr[0][q] = (f.thr_node & ((nf & nf_fh_on(0, q)) != 0)) ? f.fh[0][q] : THR_NONE;
+    const bool on1 = v1 ? (nf & nf_fh_on(1, q)) != 0 : (nf & nf_fh_on(0, q)) != 0;
+    f.thr[1][q] = (f.thr_node & on1) ? (v1 ? f.fh[1][q] : f.fh[0][q]) : THR_NONE;
+  }
+  const int64_t nreq0 = (int64_t)f.nreq[0];
+  const int64_t areq = ((nreq0 >= f.csm) & (f.csm > 0)) ? nreq0 - f.csm + f.csaf : nreq0;
+  f.amp_room = (f.sbits & FB_RF) ? f.nalloc0 - areq : THR_NONE;
+}
+
+// the `now`-dependent parts after loading a record (isNodeMetricExpired, helper.go:35-40)
+__device__ __forceinline__ void fast_adopt(NodeFast& f, const KArgs& k) {
+  const uint32_t nf = f.nflags, af = k.flags;
+  const bool expired = !(nf & NF_HAS_UT) || (k.exp_s > 0 && (k.now - f.ut) >= k.exp_s * 1000000000LL);
+  const bool exp_f = ((af & AF_FILTER_EXPIRED) != 0) & ((af & AF_EXP_PRESENT) != 0) & expired;
+  uint32_t b = f.sbits;
+  b |= (((nf & NF_HAS_METRIC) != 0) & exp_f & !(af & AF_ENABLE_WHEN_EXPIRED)) ? FB_EXP_FAIL : 0u;
+  const bool las = ((nf & NF_HAS_METRIC) != 0) & !(((af & AF_EXP_PRESENT) != 0) & expired) & !(nf & NF_NM_NIL) &
+                   (k.wsum_la > 0);
+  b |= las ? FB_LAS : 0u;
+  f.bits = b;
+  f.thr_node = ((nf & NF_HAS_METRIC) != 0) & !exp_f & !(nf & NF_NM_NIL);
+  fast_bounds(f);
+}
+
+// a record from the replay's record array (workgroup-scope loads: this workgroup may have rewritten it
+// in an earlier batch; another launch wrote it before this one started)
+template <int SCOPE = __HIP_MEMORY_SCOPE_WORKGROUP>
+__device__ __forceinline__ void rec_load(const int64_t* __restrict__ rec, NodeFast& f) {
+  int64_t w[NUM_RW];
+  // every loaded word is consumed (a dead load's register would be reused while the load is in flight,
+  // and the reuse would wait for it)
+#pragma unroll
+  for (int u = 0; u < RW_PAD; u++) w[u] = __hip_atomic_load(const_cast<int64_t*>(rec + u), __ATOMIC_RELAXED, SCOPE);
+#pragma unroll
+  for (int v = 0; v < 2; v++)
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      f.fh[v][q] = w[RW_FH + 2 * v + q];
+      f.sa[v][q] = __longlong_as_double(w[RW_SA + 2 * v + q]);
+    }
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    f.cap[q] = __longlong_as_double(w[RW_CAP + q]);
+    f.rcap[q] = __longlong_as_double(w[RW_RCAP + q]);
+    f.al[q] = __longlong_as_double(w[RW_AL + q]);
+    f.ral[q] = __longlong_as_double(w[RW_RAL + q]);
+    f.nreq[q] = __longlong_as_double(w[RW_NREQ + q]);
+  }
+  f.nreq0s = __longlong_as_double(w[RW_NREQ0S]);
+  f.nalloc0 = w[RW_NALLOC0];
+  f.csm = w[RW_CSM];
+  f.csaf = w[RW_CSAF];
+  f.ut = w[RW_UT];
+  f.nflags = (uint32_t)w[RW_FLAGS];
+  f.sbits = (uint32_t)((uint64_t)w[RW_FLAGS] >> 32);
+  f.nws = (int32_t)w[RW_NWS];
+}
+
+// write a record back (the Reserve-dependent words; the static ones never change)
+template <int SCOPE>
+__device__ __forceinline__ void rec_store_dyn(int64_t* rec, const NodeFast& f) {
+#pragma unroll
+  for (int v = 0; v < 2; v++)
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      __hip_atomic_store(rec + RW_FH + 2 * v + q, f.fh[v][q], __ATOMIC_RELAXED, SCOPE);
+      __hip_atomic_store(rec + RW_SA + 2 * v + q, (int64_t)__double_as_longlong(f.sa[v][q]), __ATOMIC_RELAXED, SCOPE);
+    }
+#pragma unroll
+  for (int q = 0; q < 2; q++)
+    __hip_atomic_store(rec + RW_NREQ + q, (int64_t)__double_as_longlong(f.nreq[q]), __ATOMIC_RELAXED, SCOPE);
+  __hip_atomic_store(rec + RW_NREQ0S, (int64_t)__double_as_longlong(f.nreq0s), __ATOMIC_RELAXED, SCOPE);
+}
+
+// a full record (sc1) with the node index in RW_PAD: the compact changed list k_fixup reads
+__device__ __forceinline__ void rec_store_full(int64_t* r, const NodeFast& f, int node) {
+  int64_t w[NUM_RW];
+#pragma unroll
+  for (int v = 0; v < 2; v++)
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      w[RW_FH + 2 * v + q] = f.fh[v][q];
+      w[RW_SA + 2 * v + q] = __double_as_longlong(f.sa[v][q]);
+    }
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    w[RW_CAP + q] = __double_as_longlong(f.cap[q]);
+    w[RW_RCAP + q] = __double_as_longlong(f.rcap[q]);
+    w[RW_AL + q] = __double_as_longlong(f.al[q]);
+    w[RW_RAL + q] = __double_as_longlong(f.ral[q]);
+    w[RW_NREQ + q] = __double_as_longlong(f.nreq[q]);
+  }
+  w[RW_NREQ0S] = __double_as_longlong(f.nreq0s);
+  w[RW_NALLOC0] = f.nalloc0;
+  w[RW_CSM] = f.csm;
+  w[RW_CSAF] = f.csaf;
+  w[RW_UT] = f.ut;
+  w[RW_FLAGS] = (int64_t)(((uint64_t)f.sbits << 32) | f.nflags);
+  w[RW_NWS] = f.nws;
+  w[RW_PAD] = node;
+#pragma unroll
+  for (int u = 0; u < NUM_RW; u++) st_sc1(r + u, w[u]);
+}
+
+// the owner lane's Reserve of pod p (load_aware.go:192-195, NodeInfo.Requested += requests): the same
+// updates k_resolve's int64 path makes, the doubles moved by the same exact amounts
+__device__ __forceinline__ void fast_reserve(NodeFast& f, const DevPod& p, const double (&estd)[2],
+                                             const double (&reqd)[2]) {
+  const uint32_t nf = f.nflags;
+  if ((nf & NF_HAS_METRIC) && !(nf & NF_NM_NIL)) {
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      if (nf & nf_fh_on(0, q)) f.fh[0][q] -= p.est[q];
+      f.sa[0][q] -= estd[q];
+      if (p.flags & PF_PROD) {
+        if (nf & nf_fh_on(1, q)) f.fh[1][q] -= p.est[q];
+        f.sa[1][q] -= estd[q];
+      }
+    }
+  }
+  f.nreq[0] += reqd[0];
+  f.nreq[1] += reqd[1];
+  f.nreq0s += reqd[0];
+  fast_bounds(f);
+}
+
+// x * 100 / c on the fast range, x and c exact doubles (div100_f without the int64 -> double step)
+__device__ __forceinline__ int32_t div100_d(double x, double dc, double rc) {
+  const double dx = x * 100.0;
+  const int32_t q = (int32_t)(dx * rc);
+  const double t = (double)q * dc;
+  return q - (int32_t)(t > dx) + (int32_t)(t + dc <= dx);
+}
+
+// lite_total(n, expired, p, k) from the node's record (fast_adopt'ed, current).  `estd` / `reqd`: the
+// pod's estimate / requests as doubles.
+__device__ __forceinline__ int32_t fast_total(const NodeFast& f, const DevPod& p, const double (&estd)[2],
+                                              const double (&reqd)[2], const KArgs& k) {
+  const uint32_t b = f.bits, pf = p.flags;
+  bool fail = (b & FB_FAIL) | ((pf & PF_DS_INVALID) != 0);
+  const bool pp = (pf & PF_PROD) != 0;  // pod-uniform: scalar selects
+  if (!(pf & PF_DAEMONSET))
+    fail |= ((b & FB_EXP_FAIL) != 0) | (p.est[0] > (pp ? f.thr[1][0] : f.thr[0][0])) |
+            (p.est[1] > (pp ? f.thr[1][1] : f.thr[0][1]));
+  if (!(pf & PF_NUMA_SKIP) & (p.req[0] != 0)) fail |= ((b & FB_AMP_BAD) != 0) | (p.req[0] > f.amp_room);
+  // LoadAwareScheduling.Score
+  const bool vs = (pf & PF_LA_SCORE_PROD) != 0;
+  int32_t sl = 0;
+  double xs[4];
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const double room = (vs ? f.sa[1][q] : f.sa[0][q]) - estd[q];
+    xs[q] = room;
+    const bool use = ((b & (FB_CAP0 << q)) != 0) & (room >= 0.0);
+    sl += (use ? div100_d(room, f.cap[q], f.rcap[q]) : 0) * k.w_la[q];
+  }
+  // NodeNUMAResource.Score (policy None)
+  const bool rs = p.req[0] != 0;
+  const bool zero = ((pf & PF_NUMA_SKIP) != 0) | ((b & FB_NZERO) != 0) | (rs & ((b & FB_RSZERO) != 0));
+  const bool most = (k.flags & AF_NUMA_MOST) != 0;
+  const double rq[2] = {(rs ? f.nreq0s : f.nreq[0]) + reqd[0], f.nreq[1] + reqd[1]};
+  int32_t sn = 0;
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const bool on = ((b & (FB_AL0 << q)) != 0) & (k.w_numa[q] != 0);
+    const double x = most ? fmin(rq[q], f.al[q]) : f.al[q] - rq[q];
+    xs[2 + q] = x;
+    sn += (on & (most | (rq[q] <= f.al[q]))) ? div100_d(x, f.al[q], f.ral[q]) * k.w_numa[q] : 0;
+  }
+  if (b & FB_SLOW) {  // exec-masked, rare: capacities >= 2^42, the int64 division (as lite_total)
+    sl = sn = 0;
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const bool use = ((b & (FB_CAP0 << q)) != 0) & (xs[q] >= 0.0);
+      sl += (use ? (int32_t)((int64_t)xs[q] * 100 / (int64_t)f.cap[q]) : 0) * k.w_la[q];
+      const bool on = ((b & (FB_AL0 << q)) != 0) & (k.w_numa[q] != 0);
+      sn += (on & (most | (rq[q] <= f.al[q]))) ? (int32_t)((int64_t)xs[2 + q] * 100 / (int64_t)f.al[q]) * k.w_numa[q] : 0;
+    }
+  }
+  const int32_t la = (b & FB_LAS) ? div_small(sl, k.wsum_la) : 0;
+  const int32_t nu = (!zero & (f.nws > 0)) ? div_small(sn, f.nws) : 0;
+  return fail ? -1 : k.wp_la * la + k.wp_numa * nu;
+}
+
 // ---------------------------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------------------------
-__global__ void k_scatter_rows(SoA s, const Row* __restrict__ rows, const int32_t* __restrict__ idx, int n) {
+__global__ void k_scatter_rows(SoA s, const Row* __restrict__ rows, const int32_t* __restrict__ idx, int n, KArgs k) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   const int64_t i = idx[t];
@@ -1323,6 +1656,13 @@ __global__ void k_scatter_rows(SoA s, const Row* __restrict__ rows, const int32_
 #pragma unroll
   for (int f = 0; f < NUM_I64_FIELDS; f++) s.f[f * s.stride + i] = r.f[f];
   s.flags[i] = r.flags;
+  NodeRegs nr;  // the node's replay record
+  regs_from_row(r, nr);
+  prepare_row(nr);
+  int64_t w[NUM_RW];
+  rec_from_regs(nr, k, w);
+#pragma unroll
+  for (int u = 0; u < NUM_RW; u++) s.rec[i * NUM_RW + u] = w[u];
 }
 
 __global__ void k_gather_rows(SoA s, Row* __restrict__ rows, int n) {
@@ -1937,26 +2277,6 @@ __global__ __launch_bounds__(MERGE_BLOCK) void k_merge(const uint32_t* __restric
 // resolve).  The top-k_j of (stale list minus touched) + (touched, fresh keys) is therefore the exact
 // top-k_j under S that k_resolve expects.  One workgroup per pod.
 constexpr int FIX_BLOCK = KSTALE + KMAX;  // stale keys, then fresh keys of the touched nodes
-// Words one workgroup hands to another while both run (k_fixup -> k_resolve_run: the exact lists;
-// k_resolve_run -> k_fixup: the changed rows; -> later eval launches: the patched SoA rows) are
-// written and read with sc1 (relaxed agent-scope atomics: global_store / global_load ... sc1), i.e.
-// write-through past the storing CU and read past the reading CU's L1: no release (L2 write-back) and
-// no acquire (L1/L2 invalidate) fence on the hand-off path (MI355X_MICROARCH.md § visibility,
-// cdna_hip_programming.md Guideline 16).  The storing wave drains (vmcnt(0)) before the flag.
-__device__ __forceinline__ int64_t ld_sc1(const int64_t* p) {
-  return __hip_atomic_load(const_cast<int64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
-  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int32_t ld_sc1(const int32_t* p) {
-  return __hip_atomic_load(const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename T>
-__device__ __forceinline__ void st_sc1(T* p, T v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void drain_stores() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
 
 // Device-side hand-off between the eval stream and the persistent Reserve kernel (k_resolve_run):
 // counters / flags in global memory polled with relaxed sc1 loads, payloads sc1 (above), every wait
@@ -1983,32 +2303,12 @@ __device__ __forceinline__ bool wait_at_least(const int32_t* flag, int32_t want,
 // for all of the batch's pods).
 // The touched nodes come as the Reserve kernel's compact list of the rows batch b-1 changed (distinct
 // nodes, the node index in Row.pad), so no row gather depends on a node id read after the wait.
-__device__ __forceinline__ void regs_from_row(const Row& r, NodeRegs& n) {
-  n.ut = r.f[F_UT];
-#pragma unroll
-  for (int v = 0; v < 2; v++)
-#pragma unroll
-    for (int q = 0; q < 2; q++) {
-      n.fh[v][q] = r.f[F_FH + 2 * v + q];
-      n.sa[v][q] = r.f[F_SA + 2 * v + q];
-    }
-#pragma unroll
-  for (int q = 0; q < 2; q++) {
-    n.cap[q] = r.f[F_CAP + q];
-    n.nalloc[q] = r.f[F_NALLOC + q];
-    n.nreq[q] = r.f[F_NREQ + q];
-  }
-  n.csm = r.f[F_CSM];
-  n.csaf = r.f[F_CSAF];
-  n.csas = r.f[F_CSAS];
-  n.flags = r.flags;
-}
 
 __global__ __launch_bounds__(FIX_BLOCK) void k_fixup(const DevPod* __restrict__ pods,
                                                      const int32_t* __restrict__ batch_base, KArgs k,
                                                      const uint32_t* __restrict__ stale,
                                                      const int32_t* __restrict__ stale_cnt,
-                                                     const Row* __restrict__ trows, const int32_t* __restrict__ tcnt,
+                                                     const int64_t* __restrict__ trows, const int32_t* __restrict__ tcnt,
                                                      uint32_t* __restrict__ cand, int32_t* __restrict__ cand_cnt,
                                                      const int32_t* __restrict__ done, int wait_b,
                                                      int32_t* __restrict__ ready, int32_t* __restrict__ err,
@@ -2031,18 +2331,12 @@ __global__ __launch_bounds__(FIX_BLOCK) void k_fixup(const DevPod* __restrict__ 
   __syncthreads();
   if (!s_ok) return;
   const int nt = s_nt;
-  NodeRegs n;
+  NodeFast n;
   int node = -1;
-  if (t >= KSTALE && t - KSTALE < nt) {  // sc1: the Reserve kernel wrote them while running
-    const int64_t* rp = reinterpret_cast<const int64_t*>(trows + (t - KSTALE));
-    Row r;
-#pragma unroll
-    for (int f = 0; f < NUM_I64_FIELDS; f++) r.f[f] = ld_sc1(rp + f);
-    const uint64_t fl = (uint64_t)ld_sc1(rp + NUM_I64_FIELDS);
-    r.flags = (uint32_t)fl;
-    r.pad = (uint32_t)(fl >> 32);
-    regs_from_row(r, n);
-    node = (int)r.pad;
+  if (t >= KSTALE && t - KSTALE < nt) {  // sc1: the Reserve kernel wrote the records while running
+    const int64_t* rp = trows + (int64_t)(t - KSTALE) * NUM_RW;
+    rec_load<__HIP_MEMORY_SCOPE_AGENT>(rp, n);
+    node = (int)ld_sc1(rp + RW_PAD);
     s_tn[t - KSTALE] = node;
   }
   __syncthreads();
@@ -2052,8 +2346,9 @@ __global__ __launch_bounds__(FIX_BLOCK) void k_fixup(const DevPod* __restrict__ 
       for (int u = 0; u < nt; u++) key = s_tn[u] == kn ? 0u : key;  // broadcast reads
     }
   } else if (node >= 0) {
-    prepare_row(n);
-    key = make_key(lite_total(n, node_expired(n, k), pod, k), node);
+    fast_adopt(n, k);
+    const double estd[2] = {(double)pod.est[0], (double)pod.est[1]}, reqd[2] = {(double)pod.req[0], (double)pod.req[1]};
+    key = make_key(fast_total(n, pod, estd, reqd, k), node);
   }
   reinterpret_cast<uint32_t*>(s_k)[t] = key;
   const int nz = __syncthreads_count(key != 0u);
@@ -2126,6 +2421,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 struct ResLds {
   uint32_t cand[MAX_BATCH * KMAX];
   DevPod pod[MAX_BATCH];
+  double pd[MAX_BATCH][4];  // the pod's estimate and requests (cpu, memory) as doubles
   int32_t cnt[MAX_BATCH];
   uint32_t chg[CHG_LDS_WORDS];
 };
@@ -2143,7 +2439,7 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
                                              int32_t* __restrict__ chosen_score, int32_t global_offset,
                                              uint64_t* __restrict__ stamps, int batch_index,
                                              uint64_t* __restrict__ dev_alloc, int64_t* __restrict__ numa_alloc,
-                                             Row* __restrict__ touched_out, int32_t* __restrict__ touched_cnt,
+                                             int64_t* __restrict__ touched_out, int32_t* __restrict__ touched_cnt,
                                              uint64_t* __restrict__ pst);
 
 // One batch: prologue on every thread of the workgroup (the batch's pods and exact candidate lists
@@ -2156,14 +2452,19 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
                                               int32_t global_offset, uint64_t* __restrict__ stamps,
                                               uint64_t* __restrict__ pstamps, int batch_index,
                                               uint64_t* __restrict__ dev_alloc, int64_t* __restrict__ numa_alloc,
-                                              Row* __restrict__ touched_out = nullptr,
+                                              int64_t* __restrict__ touched_out = nullptr,
                                               int32_t* __restrict__ touched_cnt = nullptr) {
   const int tid = threadIdx.x;
   constexpr int RES_THREADS = res_threads<NUMA>();
   if (tid == 0) pstamps[8 * batch_index] = __builtin_amdgcn_s_memrealtime();
   if (tid < B) {
     L.cnt[tid] = ld_sc1(cand_cnt + tid);
-    L.pod[tid] = pods[base + tid];
+    const DevPod pd = pods[base + tid];
+    L.pod[tid] = pd;
+    L.pd[tid][0] = (double)pd.est[0];
+    L.pd[tid][1] = (double)pd.est[1];
+    L.pd[tid][2] = (double)pd.req[0];
+    L.pd[tid][3] = (double)pd.req[1];
   }
   __syncthreads();
   {  // candidate keys (sc1: k_fixup of a concurrent launch wrote them), unused slots zeroed
@@ -2190,6 +2491,29 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
   __builtin_amdgcn_s_setprio(0);
 }
 
+// Diagnostic build (-DKE_PROF_REPLAY, tools/replay_phases.sh): shader-clock cycles of each phase of
+// the per-pod replay loop, summed over every pod into g_rprof (ke_debug_replay_phases).  Off in the
+// product build (the macro expands to nothing).
+#ifdef KE_PROF_REPLAY
+__device__ unsigned long long g_rprof[8];
+#define RPROF_DECL uint64_t rp_[7] = {0, 0, 0, 0, 0, 0, 0}, rp_t = __builtin_amdgcn_s_memtime();
+#define RPROF(i)                                         \
+  {                                                      \
+    const uint64_t rp_n = __builtin_amdgcn_s_memtime(); \
+    rp_[i] += rp_n - rp_t;                               \
+    rp_t = rp_n;                                         \
+  }
+#define RPROF_FLUSH(npods)                                                           \
+  if (lane == 0) {                                                                   \
+    for (int u_ = 0; u_ < 7; u_++) atomicAdd(&g_rprof[u_], (unsigned long long)rp_[u_]); \
+    atomicAdd(&g_rprof[7], (unsigned long long)(npods));                             \
+  }
+#else
+#define RPROF_DECL
+#define RPROF(i)
+#define RPROF_FLUSH(npods)
+#endif
+
 // The sequential replay of one batch (wave 0).
 //   Lane c owns the c-th node changed in this batch: its row lives in that lane's registers, so the
 //   per-pod re-evaluation of every changed node is one register-only eval across the lanes.  Per pod j:
@@ -2204,14 +2528,17 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
                                              int32_t* __restrict__ chosen_score, int32_t global_offset,
                                              uint64_t* __restrict__ stamps, int batch_index,
                                              uint64_t* __restrict__ dev_alloc, int64_t* __restrict__ numa_alloc,
-                                             Row* __restrict__ touched_out, int32_t* __restrict__ touched_cnt,
+                                             int64_t* __restrict__ touched_out, int32_t* __restrict__ touched_cnt,
                                              uint64_t* __restrict__ pst) {
   const uint32_t* const s_cand = L.cand;
   const DevPod* const s_pod = L.pod;
   const int lane = threadIdx.x & 63;
   int n_chg = 0, n_fetch = 0;
-  NodeRegs mine;
-  Row spare;  // lane n_chg: the row of the pod's best unchanged candidate
+  constexpr bool FAST = !NUMA;  // changed nodes as replay records (fast_total); NUMA: full rows + zones
+  NodeRegs mine;   // NUMA: the changed node's row
+  Row spare;       // NUMA, lane n_chg: the row of the pod's best unchanged candidate
+  NodeFast fast;   // FAST: the changed node's record
+  NodeFast sparef; // FAST, lane n_chg: the record of the pod's best unchanged candidate
   int my_node = -1;
   bool my_expired = false;
   int32_t o_node = -1, o_score = -1;  // lane j: pod j's placement
@@ -2226,24 +2553,40 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
         Q.n[b][r] = qtf(s, QF_NP + r, 64 * b + lane);
       }
   DevPod pod = s_pod[0];
+  double pdd[4] = {L.pd[0][0], L.pd[0][1], L.pd[0][2], L.pd[0][3]};
   uint32_t ck = s_cand[lane];
   bool chg = false;  // changed flag of this lane's candidate (pods < j); nothing is changed at j = 0
+  RPROF_DECL
   for (int j = 0; j < B; j++) {
     const bool more = j + 1 < B;
     const DevPod pod_n = s_pod[more ? j + 1 : j];
+    const int jn = more ? j + 1 : j;
+    const double pdd_n[4] = {L.pd[jn][0], L.pd[jn][1], L.pd[jn][2], L.pd[jn][3]};
+    const double estd[2] = {pdd[0], pdd[1]}, reqd[2] = {pdd[2], pdd[3]};
     const uint32_t ck_n = more ? s_cand[(j + 1) * KMAX + lane] : 0u;
     const uint32_t bu = wave_max_u32(chg ? 0u : ck);  // best unchanged snapshot candidate
-    if (bu != 0 && lane == n_chg) load_row_sc1(s, key_node(bu), spare);
+    RPROF(0)
+    if (bu != 0 && lane == n_chg) {
+      if constexpr (FAST) rec_load(s.rec + (int64_t)key_node(bu) * NUM_RW, sparef);
+      else load_row_sc1(s, key_node(bu), spare);
+    }
     n_fetch += bu != 0;
+    RPROF(1)
     uint32_t kc = 0;  // exact re-evaluation of the nodes changed earlier in this batch
     if (lane < n_chg) {
-      NumaNode nv;
-      if (NUMA) numa_load(s, my_node, nv);
-      const int32_t tot = NUMA ? eval_pair<false, NUMA>(mine, my_expired, pod, k, s, my_node, nv).total
-                               : lite_total(mine, my_expired, pod, k);
+      int32_t tot;
+      if constexpr (NUMA) {
+        NumaNode nv;
+        numa_load(s, my_node, nv);
+        tot = eval_pair<false, NUMA>(mine, my_expired, pod, k, s, my_node, nv).total;
+      } else {
+        tot = fast_total(fast, pod, estd, reqd, k);
+      }
       kc = make_key(tot, my_node);
     }
+    RPROF(2)
     const uint32_t bc = wave_max_u32(kc);
+    RPROF(3)
     // ElasticQuota PreFilter: a refused pod is placed nowhere
     int64_t qreq[2] = {0, 0};
     const bool adm = !QUOTA || !pod.quota || quota_admit_r(s, pod, k, Q, qreq);
@@ -2255,33 +2598,44 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
       } else {
         owner = n_chg++;
         if (lane == owner) {
-          regs_from_row(spare, mine);
-          prepare_row(mine);
           my_node = key_node(w);
-          my_expired = node_expired(mine, k);
+          if constexpr (FAST) {
+            fast = sparef;
+            fast_adopt(fast, k);
+          } else {
+            regs_from_row(spare, mine);
+            prepare_row(mine);
+            my_expired = node_expired(mine, k);
+          }
           chg_set(C, my_node);
         }
       }
+      RPROF(4)
       // Reserve: LoadAware assign (the new pod has no PodMetric -> counted at its estimate in every
       // non-prod term, and in the prod terms when it is prod), NodeInfo.Requested += requests.
       uint64_t al = 0;
       if (lane == owner) {
-        if ((mine.flags & NF_HAS_METRIC) && !(mine.flags & NF_NM_NIL)) {
+        if constexpr (FAST) {
+          fast_reserve(fast, pod, estd, reqd);
+        } else {
+          if ((mine.flags & NF_HAS_METRIC) && !(mine.flags & NF_NM_NIL)) {
 #pragma unroll
-          for (int q = 0; q < 2; q++) {
-            if (mine.flags & nf_fh_on(0, q)) mine.fh[0][q] -= pod.est[q];
-            mine.sa[0][q] -= pod.est[q];
-            if (pod.flags & PF_PROD) {
-              if (mine.flags & nf_fh_on(1, q)) mine.fh[1][q] -= pod.est[q];
-              mine.sa[1][q] -= pod.est[q];
+            for (int q = 0; q < 2; q++) {
+              if (mine.flags & nf_fh_on(0, q)) mine.fh[0][q] -= pod.est[q];
+              mine.sa[0][q] -= pod.est[q];
+              if (pod.flags & PF_PROD) {
+                if (mine.flags & nf_fh_on(1, q)) mine.fh[1][q] -= pod.est[q];
+                mine.sa[1][q] -= pod.est[q];
+              }
             }
           }
+          mine.nreq[0] += pod.req[0];
+          mine.nreq[1] += pod.req[1];
         }
-        mine.nreq[0] += pod.req[0];
-        mine.nreq[1] += pod.req[1];
         // DeviceShare Reserve (a DeviceShare pod is alone in its batch: no later pod of the batch
         // reads the device state it patches)
-        al = DS && (pod.flags & PF_DS) && (mine.flags & NF_DS_CACHE) ? ds_reserve(s, my_node, pod, k) : 0ull;
+        const uint32_t nfl = FAST ? fast.nflags : mine.flags;
+        al = DS && (pod.flags & PF_DS) && (nfl & NF_DS_CACHE) ? ds_reserve(s, my_node, pod, k) : 0ull;
         if (NUMA) {  // NodeNUMAResource Reserve: the zones of a NUMA-policy node
           int64_t* out16 = numa_alloc + (int64_t)(base + j) * 16;
           const int pol = pf_numa_policy(pod.flags) ? pf_numa_policy(pod.flags) : nf_numa_policy(mine.flags);
@@ -2310,15 +2664,20 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
 #pragma unroll
       for (int t = 0; t < 16; t++) numa_alloc[(int64_t)(base + j) * 16 + t] = 0;
     }
+    RPROF(5)
     // pod j+1's changed flags, read after this Reserve's bitmap update (LDS ops of a wave execute in
     // order), so they already include pod j's new node
     const bool chg_n = ck_n != 0 && chg_test(C, key_node(ck_n));
     if (NUMA) wave_lds_sync();  // the next re-evaluation reads the zones this Reserve patched
     else __atomic_signal_fence(__ATOMIC_SEQ_CST);
     pod = pod_n;
+#pragma unroll
+    for (int u = 0; u < 4; u++) pdd[u] = pdd_n[u];
     ck = ck_n;
     chg = chg_n;
+    RPROF(6)
   }
+  RPROF_FLUSH(B)
   if (lane < B) {
     chosen[base + lane] = o_node;
     chosen_score[base + lane] = o_score;
@@ -2333,39 +2692,38 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
         s.qt[(QF_NP + r) * QT_STRIDE + 64 * b + lane] = Q.n[b][r];
       }
   if (lane < n_chg) {
-    // the patched rows back to the SoA (sc1: read by the next batches' evals on other CUs), and the
-    // compact list of them for the next batch's k_fixup (pipelined runs)
+    // the patched rows back to the SoA (sc1: read by the next batches' evals on other CUs), the replay
+    // records (this workgroup's later batches, later launches), and the compact list of the changed
+    // records for the next batch's k_fixup (pipelined runs; sc1, read by a concurrent launch)
     const int64_t st = s.stride;
     int64_t* f = s.f + my_node;
-#pragma unroll
-    for (int v = 0; v < 2; v++)
-#pragma unroll
-      for (int q = 0; q < 2; q++) {
-        st_sc1(f + (F_FH + 2 * v + q) * st, mine.fh[v][q]);
-        st_sc1(f + (F_SA + 2 * v + q) * st, mine.sa[v][q]);
-      }
-    st_sc1(f + (F_NREQ + 0) * st, mine.nreq[0]);
-    st_sc1(f + (F_NREQ + 1) * st, mine.nreq[1]);
-    if (touched_out) {
-      int64_t* r = reinterpret_cast<int64_t*>(touched_out + lane);
-      st_sc1(r + F_UT, mine.ut);
+    int64_t* rec = s.rec + (int64_t)my_node * NUM_RW;
+    if constexpr (FAST) {
 #pragma unroll
       for (int v = 0; v < 2; v++)
 #pragma unroll
         for (int q = 0; q < 2; q++) {
-          st_sc1(r + F_FH + 2 * v + q, mine.fh[v][q]);
-          st_sc1(r + F_SA + 2 * v + q, mine.sa[v][q]);
+          st_sc1(f + (F_FH + 2 * v + q) * st, fast.fh[v][q]);
+          st_sc1(f + (F_SA + 2 * v + q) * st, (int64_t)fast.sa[v][q]);
         }
+      st_sc1(f + (F_NREQ + 0) * st, (int64_t)fast.nreq[0]);
+      st_sc1(f + (F_NREQ + 1) * st, (int64_t)fast.nreq[1]);
+      rec_store_dyn<__HIP_MEMORY_SCOPE_WORKGROUP>(rec, fast);
+      if (touched_out) rec_store_full(touched_out + (int64_t)lane * NUM_RW, fast, my_node);
+    } else {
 #pragma unroll
-      for (int q = 0; q < 2; q++) {
-        st_sc1(r + F_CAP + q, mine.cap[q]);
-        st_sc1(r + F_NALLOC + q, mine.nalloc[q]);
-        st_sc1(r + F_NREQ + q, mine.nreq[q]);
-      }
-      st_sc1(r + F_CSM, mine.csm);
-      st_sc1(r + F_CSAF, mine.csaf);
-      st_sc1(r + F_CSAS, mine.csas);
-      st_sc1(r + NUM_I64_FIELDS, (int64_t)(((uint64_t)(uint32_t)my_node << 32) | mine.flags));
+      for (int v = 0; v < 2; v++)
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+          st_sc1(f + (F_FH + 2 * v + q) * st, mine.fh[v][q]);
+          st_sc1(f + (F_SA + 2 * v + q) * st, mine.sa[v][q]);
+        }
+      st_sc1(f + (F_NREQ + 0) * st, mine.nreq[0]);
+      st_sc1(f + (F_NREQ + 1) * st, mine.nreq[1]);
+      int64_t w[NUM_RW];
+      rec_from_regs(mine, k, w);
+#pragma unroll
+      for (int u = 0; u < NUM_RW; u++) __hip_atomic_store(rec + u, w[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     chg_clear_word(C, my_node);  // the bitmap is zero again for the next batch
   }
@@ -2410,7 +2768,7 @@ __global__ __launch_bounds__(res_threads<false>()) void k_resolve_run(SoA s, con
                                                                       uint64_t* __restrict__ dev_alloc,
                                                                       const int32_t* __restrict__ ready,
                                                                       int32_t* __restrict__ done, int32_t* __restrict__ err,
-                                                                      Row* __restrict__ touched_out,
+                                                                      int64_t* __restrict__ touched_out,
                                                                       int32_t* __restrict__ touched_cnt,
                                                                       uint32_t* __restrict__ chg_glb, int n_nodes) {
   __shared__ ResLds L;
@@ -2663,6 +3021,14 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
     }
     if (ok) {
       reserve_row(s, node, nf, pod);
+      {  // the node's replay record follows its patched row
+        NodeRegs nr;
+        load_row(s, node, nr);
+        prepare_row(nr);
+        int64_t w[NUM_RW];
+        rec_from_regs(nr, k, w);
+        for (int u = 0; u < NUM_RW; u++) s.rec[node * NUM_RW + u] = w[u];
+      }
       uint32_t used = 0;
       int n_used = 0;
       int cs_new[8] = {cs_old[0], cs_old[1], cs_old[2], cs_old[3], cs_old[4], cs_old[5], cs_old[6], cs_old[7]};
@@ -2762,7 +3128,7 @@ struct DeviceState {
   hipStream_t estream = nullptr;
   uint32_t* d_stale = nullptr;      // [2][MAX_BATCH][KSTALE] stale-snapshot candidate lists
   uint32_t* d_chg = nullptr;        // changed-node bitmap of the replay when node ids exceed its LDS copy
-  Row* d_trows = nullptr;           // [MAX_BATCH] rows the last resolved batch changed (node in .pad)
+  int64_t* d_trows = nullptr;       // [MAX_BATCH][NUM_RW] records the last resolved batch changed (node in RW_PAD)
   int32_t* d_tcnt = nullptr;        // their count
   int32_t* d_stale_cnt = nullptr;   // [2][MAX_BATCH]
   static constexpr int EV_RING = 8;
@@ -2823,7 +3189,9 @@ int device_create(Context* ctx) {
   HIP_OK(hipMemsetAsync(d->d_batch_base, 0, sizeof(int32_t), d->stream));
   HIP_OK(hipMalloc(&d->d_stale, sizeof(uint32_t) * 2 * MAX_BATCH * KSTALE));
   HIP_OK(hipMalloc(&d->d_stale_cnt, sizeof(int32_t) * 2 * MAX_BATCH));
-  HIP_OK(hipMalloc(&d->d_trows, sizeof(Row) * MAX_BATCH));
+  HIP_OK(hipMalloc(&d->d_trows, sizeof(int64_t) * MAX_BATCH * NUM_RW));
+  HIP_OK(hipMalloc(&d->soa.rec, sizeof(int64_t) * NUM_RW * d->capacity));
+  HIP_OK(hipMemsetAsync(d->soa.rec, 0, sizeof(int64_t) * NUM_RW * d->capacity, d->stream));
   HIP_OK(hipMalloc(&d->d_tcnt, sizeof(int32_t)));
   if (d->capacity > (int64_t)CHG_LDS_WORDS * 32) {  // zero between batches (each replay clears its bits)
     HIP_OK(hipMalloc(&d->d_chg, sizeof(uint32_t) * (d->capacity + 31) / 32));
@@ -2848,7 +3216,7 @@ void device_destroy(Context* ctx) {
                   d->d_dsraw,   d->d_dsmax,  d->d_devalloc,   d->d_dsrows,       d->soa.nf,   d->soa.nm,
                   d->d_numaalloc, d->d_numarows, d->d_defer, d->d_defer_cnt, d->soa.cs, d->soa.cpu,
                   d->d_cpurows, d->d_cpusets, d->d_aff, d->soa.qt, d->soa.qm, d->d_sched, d->d_stale,
-                  d->d_stale_cnt, d->d_trows, d->d_tcnt, d->d_chg};
+                  d->d_stale_cnt, d->d_trows, d->d_tcnt, d->d_chg, d->soa.rec};
   if (d->estream) (void)hipStreamSynchronize(d->estream);
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -3140,7 +3508,7 @@ int device_refresh(Context* ctx, int64_t now) {
   HIP_OK(hipMemcpyAsync(d->d_rows, rows.data(), sizeof(Row) * n, hipMemcpyHostToDevice, d->stream));
   HIP_OK(hipMemcpyAsync(d->d_idx, idx.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, d->stream));
   hipLaunchKernelGGL(k_scatter_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, d->stream, d->soa, d->d_rows,
-                     d->d_idx, (int)n);
+                     d->d_idx, (int)n, make_kargs(ctx, now));
   HIP_OK(hipGetLastError());
   HIP_OK(hipStreamSynchronize(d->stream));  // `rows` is a local host vector
   return KE_OK;
@@ -3627,6 +3995,25 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   return KE_OK;
 }
 
+// cycles per pod of each replay phase since the last call (diagnostic build only; zeros otherwise)
+int device_replay_phases(Context* ctx, double* cyc8) {
+#ifdef KE_PROF_REPLAY
+  DeviceState* d = ctx->dev;
+  HIP_OK(hipSetDevice(d->device));
+  HIP_OK(hipDeviceSynchronize());
+  unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  HIP_OK(hipMemcpyFromSymbol(v, HIP_SYMBOL(g_rprof), sizeof(v)));
+  const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_rprof), z, sizeof(z)));
+  for (int i = 0; i < 7; i++) cyc8[i] = v[7] ? (double)v[i] / (double)v[7] : 0.0;
+  cyc8[7] = (double)v[7];
+#else
+  (void)ctx;
+  for (int i = 0; i < 8; i++) cyc8[i] = 0.0;
+#endif
+  return KE_OK;
+}
+
 int device_set_pipeline(Context* ctx, int32_t on) {
   ctx->dev->pipeline = on != 0;
   return KE_OK;
@@ -3668,6 +4055,40 @@ int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t 
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   *avg_ms = ms / iters;
+  return KE_OK;
+}
+
+// every node's replay record against one derived from its current SoA row (test of the record upkeep)
+__global__ void k_check_records(SoA s, int n, KArgs k, unsigned long long* bad) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  NodeRegs nr;
+  load_row(s, i, nr);
+  prepare_row(nr);
+  int64_t w[NUM_RW];
+  rec_from_regs(nr, k, w);
+  int miss = 0;
+  for (int u = 0; u < NUM_RW; u++) miss += (u != RW_PAD) & (s.rec[(int64_t)i * NUM_RW + u] != w[u]);
+  if (miss) atomicAdd(bad, 1ull);
+}
+
+int device_check_records(Context* ctx, int64_t now, int64_t* bad) {
+  DeviceState* d = ctx->dev;
+  HIP_OK(hipSetDevice(d->device));
+  int rc = device_refresh(ctx, now);
+  if (rc) return rc;
+  unsigned long long* dbad = nullptr;
+  HIP_OK(hipMalloc(&dbad, sizeof(unsigned long long)));
+  HIP_OK(hipMemsetAsync(dbad, 0, sizeof(unsigned long long), d->stream));
+  const int N = ctx->n_nodes;
+  if (N > 0)
+    hipLaunchKernelGGL(k_check_records, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, d->stream, d->soa, N,
+                       make_kargs(ctx, now), dbad);
+  unsigned long long h = 0;
+  HIP_OK(hipMemcpyAsync(&h, dbad, sizeof(h), hipMemcpyDeviceToHost, d->stream));
+  HIP_OK(hipStreamSynchronize(d->stream));
+  HIP_OK(hipFree(dbad));
+  *bad = (int64_t)h;
   return KE_OK;
 }
 

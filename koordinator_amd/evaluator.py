@@ -211,6 +211,12 @@ class Evaluator:
         self._check(self.lib.ke_debug_numa_deferred(self.h, C.byref(n)))
         return n.value
 
+    def check_records(self, now_ns):
+        """Nodes whose replay record differs from one derived from their device row (0 = consistent)."""
+        n = abi.i64()
+        self._check(self.lib.ke_debug_check_records(self.h, int(now_ns), C.byref(n)))
+        return n.value
+
     def set_pipeline(self, on):
         """Pipelined schedule (default): batch b's eval + select overlap batch b-1's Reserve replay."""
         self._check(self.lib.ke_set_pipeline(self.h, 1 if on else 0))

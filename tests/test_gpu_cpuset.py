@@ -90,6 +90,7 @@ def test_cpuset_schedule_parity(gpu, variant):
     more = synth.make_cpuset_pods(40, synth.BASE_SEED + 214, key_base=5_000_000_000)
     assert_eval_equal(ev.eval(more, synth.T0), o.eval(more, synth.T0))
     assert_schedule_equal(ev, o, more, synth.T0)
+    assert ev.check_records(synth.T0) == 0  # cpuset Reserves keep the replay records current
 
 
 def test_cpuset_schedule_shared_cpus(gpu):

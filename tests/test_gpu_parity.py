@@ -215,6 +215,7 @@ def test_schedule_large_cluster_prefix(gpu):
     assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
     dev, host = ev.debug_rows(synth.T0)
     assert np.array_equal(dev, host)
+    assert ev.check_records(synth.T0) == 0
 
 
 # ---- pipelined schedule (two streams, stale lists + k_fixup) ---------------------------------------
@@ -236,6 +237,7 @@ def test_pipeline_matches_serial_and_oracle(gpu, n_nodes, n_pods, seed):
     assert np.array_equal(c1, c2) and np.array_equal(s1, s2)
     c0, s0 = o.schedule(pods, synth.T0)
     assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    assert ev.check_records(synth.T0) == 0 and es.check_records(synth.T0) == 0
     es.close()
 
 
@@ -352,6 +354,7 @@ def test_deviceshare_schedule_parity(gpu, strategy):
     a, b = ev.eval(more, synth.T0), o.eval(more, synth.T0)
     for k in ("status", "ds", "total", "best"):
         assert np.array_equal(a[k], b[k]), k
+    assert ev.check_records(synth.T0) == 0
 
 
 def test_deviceshare_sharded_loopback(gpu):
@@ -428,6 +431,7 @@ def test_numa_policy_schedule_parity(gpu):
     assert np.any(ev.last_numa_allocations != 0)
     more = synth.make_pods(32, synth.BASE_SEED + 95)
     assert_eval_equal(ev.eval(more, synth.T0), o.eval(more, synth.T0))
+    assert ev.check_records(synth.T0) == 0
 
 
 def test_numa_policy_sharded_loopback(gpu):
