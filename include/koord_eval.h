@@ -496,7 +496,13 @@ int ke_last_device_allocations(ke_ctx* ctx, int32_t n, uint64_t* minors);
  *    a refused pod is unschedulable (chosen -1) and reserves nothing;
  *  - Reserve (core/group_quota_manager.go:700-760, ReservePod :943-963): the masked request is added
  *    to used (and non-preemptible used) of the quota and every ancestor.
- * Not modelled: scale-min, guaranteed usage, hook plugins, quota-overuse revocation, preemption.
+ *  - system / default quotas (limit_is_max): used limit = Max; a Reserve into one with runtime quota on
+ *    shrinks totalResourceExceptSystemAndDefaultUsed (updateClusterTotalResourceNoLock,
+ *    group_quota_manager.go:127-151,268-271) and every later pod of the call sees runtime limits
+ *    refreshed from the smaller total.
+ * Not modelled: scale-min, guaranteed usage, hook plugins, quota-overuse revocation, preemption
+ * (PostFilter); a zero-valued pod request counts as an absent key (checkQuotaRecursive masks on
+ * ResourceNames(PodRequests), which keeps explicit zeros — ke_pod carries values, not key sets).
  * Resources: cpu (milli, getQuantityValue) and memory (bytes).  Values >= 0. */
 #define KE_MAX_QUOTAS 255 /* ke_pod.quota - 1 fits a byte on the device */
 typedef struct ke_quota_args {

@@ -441,32 +441,80 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
   rc = require_device(ctx);
   if (rc) return rc;
   ctx->c.host_ms[0] = std::chrono::duration<double, std::milli>(clk::now() - tp).count();
-  rc = device_schedule(&ctx->c, n_pods, pods, now_ns, chosen, score);
-  if (rc) return rc;
-  tp = clk::now();
-  // Host mirror of the Reserves the device already applied to its rows: keep the object state
-  // (assign cache, NodeInfo.Requested) in step so later re-derivations include these pods.
-  const int32_t off = ctx->c.cfg.global_node_offset;
-  std::vector<int32_t> touched;
-  ctx->c.pending.reserve(ctx->c.pending.size() + (size_t)n_pods);
-  for (int32_t p = 0; p < n_pods; p++) {
-    const int32_t node = chosen[p] - off;
-    if (chosen[p] < 0 || node < 0 || node >= ctx->c.n_nodes) continue;
-    NodeState& ns = ctx->c.nodes[node];
-    // LoadAware assign + NodeInfo.Requested: deferred (flush_mirror), the device rows carry them
-    ctx->c.pending.push_back({node, now_ns, pods[p]});
-    const bool was_dirty = ns.dirty;
-    if (p < (int32_t)ctx->c.last_dev_alloc.size() && ctx->c.last_dev_alloc[p])
-      host_ds_reserve(ctx->c.cfg, ns, make_dev_pod(ctx->c.cfg, pods[p]), ctx->c.last_dev_alloc[p]);
-    if ((int64_t)ctx->c.last_numa_alloc.size() >= (int64_t)(p + 1) * KE_MAX_NUMA * KE_NRES)
-      host_numa_reserve(ns, &ctx->c.last_numa_alloc[(size_t)p * KE_MAX_NUMA * KE_NRES]);
-    ns.dirty = was_dirty;  // the device rows already carry these Reserves
-    // cpuset Reserve: the CPU table (the device one is patched too) and the zones' NUMA status (not
-    // patched on the device: re-derived from this mirror)
-    const uint64_t* cs = (int64_t)ctx->c.last_cpusets.size() >= (int64_t)(p + 1) * 4 ? &ctx->c.last_cpusets[(size_t)p * 4] : nullptr;
-    if (cs && (cs[0] | cs[1] | cs[2] | cs[3])) host_cpuset_reserve(ns, make_dev_pod(ctx->c.cfg, pods[p]), cs);
+  Context& c = ctx->c;
+  // ElasticQuota: a Reserve into the system / default quota (limit_is_max) with runtime quota on
+  // shrinks totalResourceExceptSystemAndDefaultUsed (updateClusterTotalResourceNoLock,
+  // group_quota_manager.go:268-271, 127-151), and every later pod sees runtime limits refreshed from it.
+  // The queue is cut after each such pod; between the segments the host takes the device's used,
+  // shrinks the total by the pod's masked request and recomputes the limits (uploaded by the next
+  // segment).  Without such pods the queue is one segment.
+  auto barrier = [&](int32_t p) {
+    if (c.quotas.empty() || !c.qargs.enable_runtime_quota || pods[p].quota <= 0) return false;
+    return c.quotas[(size_t)pods[p].quota - 1].limit_is_max != 0;
+  };
+  std::vector<uint64_t> all_dev, all_cs;
+  std::vector<int64_t> all_numa;
+  std::vector<double> all_batch_ms;
+  double all_ms = 0;
+  bool numa_out = false;
+  const int32_t off = c.cfg.global_node_offset;
+  for (int32_t s0 = 0; s0 < n_pods || (n_pods == 0 && s0 == 0);) {
+    int32_t s1 = s0;
+    while (s1 < n_pods && !barrier(s1)) s1++;
+    if (s1 < n_pods) s1++;  // the barrier pod ends its segment
+    const int32_t len = s1 - s0;
+    rc = device_schedule(&c, len, pods + s0, now_ns, chosen + (n_pods ? s0 : 0), score ? score + s0 : nullptr);
+    if (rc) return rc;
+    if (n_pods == 0) break;
+    tp = clk::now();
+    // Host mirror of the Reserves the device already applied to its rows: keep the object state
+    // (assign cache, NodeInfo.Requested) in step so later re-derivations include these pods.
+    c.pending.reserve(c.pending.size() + (size_t)len);
+    for (int32_t i = 0; i < len; i++) {
+      const int32_t p = s0 + i;
+      const int32_t node = chosen[p] - off;
+      if (chosen[p] < 0 || node < 0 || node >= c.n_nodes) continue;
+      NodeState& ns = c.nodes[node];
+      // LoadAware assign + NodeInfo.Requested: deferred (flush_mirror), the device rows carry them
+      c.pending.push_back({node, now_ns, pods[p]});
+      const bool was_dirty = ns.dirty;
+      if (i < (int32_t)c.last_dev_alloc.size() && c.last_dev_alloc[i])
+        host_ds_reserve(c.cfg, ns, make_dev_pod(c.cfg, pods[p]), c.last_dev_alloc[i]);
+      if ((int64_t)c.last_numa_alloc.size() >= (int64_t)(i + 1) * KE_MAX_NUMA * KE_NRES)
+        host_numa_reserve(ns, &c.last_numa_alloc[(size_t)i * KE_MAX_NUMA * KE_NRES]);
+      ns.dirty = was_dirty;  // the device rows already carry these Reserves
+      // cpuset Reserve: the CPU table (the device one is patched too) and the zones' NUMA status (not
+      // patched on the device: re-derived from this mirror)
+      const uint64_t* cs = (int64_t)c.last_cpusets.size() >= (int64_t)(i + 1) * 4 ? &c.last_cpusets[(size_t)i * 4] : nullptr;
+      if (cs && (cs[0] | cs[1] | cs[2] | cs[3])) host_cpuset_reserve(ns, make_dev_pod(c.cfg, pods[p]), cs);
+    }
+    c.host_ms[7] = std::chrono::duration<double, std::milli>(clk::now() - tp).count();
+    if (s0 == 0 && s1 == n_pods) return KE_OK;  // one segment: the last_* outputs are already whole
+    all_dev.insert(all_dev.end(), c.last_dev_alloc.begin(), c.last_dev_alloc.end());
+    all_cs.insert(all_cs.end(), c.last_cpusets.begin(), c.last_cpusets.end());
+    numa_out = numa_out || !c.last_numa_alloc.empty();
+    if (c.last_numa_alloc.empty()) all_numa.resize(all_numa.size() + (size_t)len * KE_MAX_NUMA * KE_NRES, 0);
+    else all_numa.insert(all_numa.end(), c.last_numa_alloc.begin(), c.last_numa_alloc.end());
+    all_batch_ms.insert(all_batch_ms.end(), c.last_batch_ms.begin(), c.last_batch_ms.end());
+    all_ms += c.last_total_ms;
+    if (barrier(s1 - 1) && chosen[s1 - 1] >= 0) {  // the placed system / default pod: refresh the runtime
+      rc = device_quota_sync(&c);
+      if (rc) return rc;
+      const ke_quota& q = c.quotas[(size_t)pods[s1 - 1].quota - 1];
+      c.qargs.total[0] -= q.has_max[0] ? pods[s1 - 1].requests[KE_RES_CPU] : 0;
+      c.qargs.total[1] -= q.has_max[1] ? pods[s1 - 1].requests[KE_RES_MEMORY] : 0;
+      rc = quota_compute_limits(c.qargs, c.quotas, c.qlimit, c.qlimit_has);
+      if (rc) return rc;
+      c.quota_dirty = true;
+    }
+    s0 = s1;
   }
-  ctx->c.host_ms[7] = std::chrono::duration<double, std::milli>(clk::now() - tp).count();
+  c.last_dev_alloc.swap(all_dev);
+  c.last_cpusets.swap(all_cs);
+  if (numa_out) c.last_numa_alloc.swap(all_numa);
+  else c.last_numa_alloc.clear();
+  c.last_batch_ms.swap(all_batch_ms);
+  c.last_total_ms = all_ms;
   return KE_OK;
 }
 

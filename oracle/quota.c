@@ -12,7 +12,8 @@
  *                   the quota and every ancestor)
  * quotav1.LessThanOrEqual(a, b) compares only keys of b also present in a (k8s.io/apiserver v0.28.7
  * quota/v1); with non-negative values a key absent from a compares as 0.  A zero pod request counts
- * as an absent key (ke_pod carries no key set). */
+ * as an absent key (ke_pod carries no key set).  A Reserve into the system / default quota (limit_is_max)
+ * with runtime quota on shrinks the tree total and refreshes every runtime limit (orq_reserve). */
 #include "quota.h"
 
 #include <string.h>
@@ -159,4 +160,14 @@ void orq_reserve(or_quotas* Q, const ke_pod* pod) {
       Q->q[a].used[r] += req[r];
       if (pod->quota_non_preemptible) Q->q[a].non_preemptible_used[r] += req[r];
     }
+  /* the system / default quota's used changed: updateClusterTotalResourceNoLock (group_quota_manager.go:
+   * 268-271, 127-151) shrinks totalResourceExceptSystemAndDefaultUsed by it, the root's
+   * RuntimeQuotaCalculator takes the new total and every runtime quota is refreshed from it */
+  if (Q->q[qi].limit_is_max && Q->args.enable_runtime_quota) {
+    ke_quota_args args = Q->args;
+    for (int r = 0; r < KE_NRES; r++) args.total[r] -= req[r];
+    ke_quota q[KE_MAX_QUOTAS];
+    memcpy(q, Q->q, sizeof(ke_quota) * (size_t)Q->n);
+    orq_load(Q, &args, q, Q->n);
+  }
 }

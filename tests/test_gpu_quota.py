@@ -79,3 +79,28 @@ def test_quota_used_carries_across_calls(gpu):
         h.quotas_load(synth.quota_args(tc, tm), q)
     check_same(ev, o, len(q), pods[:450])
     check_same(ev, o, len(q), pods[450:])
+
+
+@pytest.mark.parametrize("runtime", [True, False])
+def test_quota_default_quota_pods(gpu, runtime):
+    """Pods of the default quota (limit_is_max) between batched and singleton pods: with runtime quota
+    each placed one shrinks the tree total and refreshes every runtime limit (the call is cut after it,
+    group_quota_manager.go:268-271); placements and every quota's limit / used equal the oracle's."""
+    from test_quota import with_default_quota
+    n = 1500
+    cl = synth.make_cluster(n, synth.BASE_SEED + 96)
+    dv = synth.make_devices(n, synth.BASE_SEED + 146)
+    pods = synth.make_ds_pods(900, synth.BASE_SEED + 196, device_fraction=0.2)
+    q, pods, tc, tm = tight_tree(pods, 306, 0.5)
+    q = with_default_quota(q, tc // 2, tm // 2)
+    pods["quota"][3::37] = len(q)
+    cfg = synth.config(n)
+    ev, o = Evaluator(cfg), Oracle(cfg, n)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        synth.load_devices(h, dv)
+        h.quotas_load(synth.quota_args(tc, tm, runtime, True), q)
+    c = check_same(ev, o, len(q), pods)
+    assert ((c >= 0) & (pods["quota"] == len(q))).sum() > 5
+    assert np.array_equal(ev.last_device_allocations, o.last_device_allocations)
+    assert len(ev.stats()[1]) > 0

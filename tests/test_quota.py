@@ -120,3 +120,47 @@ def test_oracle_admission_and_reserve():
         placed = sum(1 for c, p in zip(chosen, pods) if c >= 0 and p["quota"])
         assert o.quota_state(1)["used"][0] == placed * 4 * M
         assert o.quota_state(0)["used"][0] == placed * 4 * M  # ancestors count the leaf's pods
+
+
+def with_default_quota(q, max_cpu, max_mem):
+    """Append a default quota (koordinator-default-quota: limit_is_max, child of the root)."""
+    d = np.zeros(1, abi.QUOTA_DTYPE)
+    d[0]["parent"] = -1
+    d[0]["has_max"] = (1, 1)
+    d[0]["max"] = (max_cpu, max_mem)
+    d[0]["shared_weight"] = (max_cpu, max_mem)
+    d[0]["allow_lent_resource"] = 1
+    d[0]["limit_is_max"] = 1
+    return np.concatenate([q, d])
+
+
+def test_default_quota_reserve_shrinks_runtime_total():
+    """group_quota_manager.go:268-271,127-151: a pod reserved into the default quota lowers
+    totalResourceExceptSystemAndDefaultUsed, so the runtime limits after the queue are those of the
+    tree total minus the default pods' placed requests."""
+    n = 40
+    cl = synth.make_cluster(n, synth.BASE_SEED + 501)
+    pods = synth.make_pods(120, synth.BASE_SEED + 502)
+    tc = int(pods["requests"][:, abi.RES_CPU].sum() * 0.5)
+    tm = int(pods["requests"][:, abi.RES_MEMORY].sum() * 0.5)
+    q = synth.make_quota_tree(synth.BASE_SEED + 503, 16, 4, tc, tm)
+    pods = synth.assign_quotas(pods, q, synth.BASE_SEED + 504)
+    q = with_default_quota(q, tc, tm)
+    dq = len(q)  # ke_pod.quota of the default quota
+    pods["quota"][::5] = dq
+    o = Oracle(synth.config(n), n)
+    synth.load_into(o, cl)
+    o.quotas_load(synth.quota_args(tc, tm), q)
+    before = [o.quota_state(i)["limit"].copy() for i in range(len(q))]
+    chosen, _ = o.schedule(pods, synth.T0)
+    placed_default = (chosen >= 0) & (pods["quota"] == dq)
+    assert placed_default.sum() > 5
+    shrink = pods["requests"][placed_default][:, [abi.RES_CPU, abi.RES_MEMORY]].sum(axis=0)
+    ref = Oracle(synth.config(n), n)
+    ref.quotas_load(synth.quota_args(tc - int(shrink[0]), tm - int(shrink[1])), q)
+    changed = 0
+    for i in range(len(q)):
+        got = o.quota_state(i)["limit"]
+        assert np.array_equal(got, ref.quota_state(i)["limit"]), i
+        changed += not np.array_equal(got, before[i])
+    assert changed > 0
