@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define KE_ABI_VERSION 3
+#define KE_ABI_VERSION 4
 #define KE_ABSENT (-1)
 
 /* ---- error codes ---------------------------------------------------------------------------- */
@@ -75,6 +75,14 @@ extern "C" {
 #define KE_REASON_DS_INSUFFICIENT_GPU 33     /* "Insufficient gpu devices"  (devicehandler_gpu.go:41, device_allocator.go:412) */
 #define KE_REASON_DS_INSUFFICIENT_RDMA 34    /* "Insufficient rdma devices" (devicehandler_default.go:46, device_allocator.go:412) */
 #define KE_REASON_DS_INSUFFICIENT_FPGA 35    /* "Insufficient fpga devices" */
+/* GPUAllocator.Allocate (deviceshare/allocator_gpu.go:72-133): partition and topology-scope outcomes */
+#define KE_REASON_DS_MISSING_PARTITION_TABLE 36   /* ErrNodeMissingGPUPartitionTable "node(s) missing GPU Partition Table" */
+#define KE_REASON_DS_UNSUPPORTED_GPU_REQUESTS 37  /* ErrUnsupportedGPURequests "node(s) Unsupported number of GPU requests" */
+#define KE_REASON_DS_INSUFFICIENT_PARTITIONED 38  /* ErrInsufficientPartitionedDevice "Insufficient Partitioned GPU Devices" */
+#define KE_REASON_DS_MISSING_TOPOLOGY_TREE 39     /* ErrNodeMissingGPUDeviceTopologyTree (required scope only) */
+#define KE_REASON_DS_MULTI_SHARED_GPU 40          /* ErrUnsupportedMultiSharedGPU (required scope only) */
+#define KE_REASON_DS_INSUFFICIENT_TOPOLOGY_SCOPED 41 /* ErrInsufficientTopologyScopedGPUDevices */
+#define KE_REASON_DS_INSUFFICIENT_GPU_TOPOLOGY 42 /* ErrInsufficientGPUDevices "Insufficient GPU Devices" (topology tree) */
 
 /* ---- resources (index into per-resource arrays) ---------------------------------------------- */
 #define KE_RES_CPU 0          /* "cpu"                         MilliValue */
@@ -144,7 +152,10 @@ typedef struct ke_loadaware_args {
   uint8_t score_according_prod_usage;
   uint8_t allow_customize_estimation;
   uint8_t has_aggregated; /* args.Aggregated != nil */
-  uint8_t pad[3];
+  /* Some map of the args (ResourceWeights, UsageThresholds, ProdUsageThresholds, EstimatedScalingFactors,
+   * Aggregated.UsageThresholds) has a key other than cpu/memory: not supported (KE_ERR_UNSUPPORTED). */
+  uint8_t has_other_keys;
+  uint8_t pad[2];
 } ke_loadaware_args;
 
 /* NodeNUMAResourceArgs.ScoringStrategy (types.go:114-125, v1beta3/defaults.go:118-153). */
@@ -154,7 +165,9 @@ typedef struct ke_numa_args {
   int32_t numa_strategy;    /* NUMAScoringStrategy.Type (KE_STRATEGY_*); its weights are the node-level
                                ScoringStrategy.Resources (scoring.go:37-52, plugin.go:121-126) */
   int32_t default_cpu_bind_policy; /* DefaultCPUBindPolicy (KE_CPU_BIND_*, v1beta3 default FullPCPUs) */
-  int32_t pad;
+  uint8_t has_other_keys;  /* ScoringStrategy.Resources names a resource other than cpu/memory (scoring.go
+                              217-262 scores scalar resources too): not supported (KE_ERR_UNSUPPORTED) */
+  uint8_t pad[3];
 } ke_numa_args;
 
 /* ---- cpuset binding (nodenumaresource cpu accumulator) ----------------------------------------- */
@@ -258,10 +271,19 @@ typedef struct ke_numa_zone {
 #define KE_DSW_GPU_MEMORY 1
 #define KE_DSW_RDMA 2
 #define KE_DSW_FPGA 3
+/* KE_DKEY_* bits of DeviceShareArgs.GPUSharedResourceTemplatesMatchedResources (types.go:277-283) */
+#define KE_TEMPLATE_KEY_CORE 1u
+#define KE_TEMPLATE_KEY_MEMORY 2u
+#define KE_TEMPLATE_KEY_MEMORY_RATIO 4u
 typedef struct ke_deviceshare_args {
   int64_t weights[4];
   int32_t strategy; /* KE_STRATEGY_* */
-  int32_t pad;
+  /* GPUSharedResourceTemplatesMatchedResources restricted to the GPU keys (KE_TEMPLATE_KEY_*): a shared-GPU
+   * pod whose per-GPU request names one of them would be allocated by template (allocator_gpu.go:135-159,
+   * utils.go:508-515), which is not implemented: ke_eval / ke_schedule return KE_ERR_UNSUPPORTED for it. */
+  uint8_t template_matched_keys;
+  uint8_t has_other_keys; /* ScoringStrategy.Resources names a resource outside KE_DSW_*: not supported */
+  uint8_t pad[2];
 } ke_deviceshare_args;
 
 /* One device instance as koord-scheduler's nodeDeviceCache holds it (device_cache.go:518-568):
@@ -273,10 +295,27 @@ typedef struct ke_device {
   uint8_t health;
   uint8_t has_total[KE_DKEYS];
   uint8_t has_used[KE_DKEYS];
-  uint8_t pad;
+  uint8_t has_topology; /* DeviceInfo.Topology != nil */
   int64_t total[KE_DKEYS];
   int64_t used[KE_DKEYS];
-} ke_device; /* 64 bytes */
+  /* DeviceInfo.Topology: NodeID, and the rank of PCIEID among the node's distinct PCIEID strings in Go string
+   * order (0 = smallest).  GetGPUTopologyScope (allocator_gpu_helper.go:202-263) builds the GPU scope tree
+   * Node > NUMANode (by NodeID) > PCIe (by PCIEID) from them when every GPU device has a topology. */
+  int32_t numa_node;
+  int32_t pcie_rank;
+} ke_device; /* 72 bytes */
+
+/* One GPUPartition of a node's GPUPartitionTable (apis/extension/device_share.go:196-226): the table is the
+ * Device annotation scheduling.koordinator.sh/gpu-partitions, or, when the Device has none, the designated
+ * table of the node's GPU model (GetDesignatedGPUPartitionIndexer, allocator_gpu_helper.go:146-162). */
+typedef struct ke_gpu_partition {
+  uint32_t minors;          /* bit m = minor m (Minors; minors 0 .. KE_MAX_MINORS-1, non-empty)          */
+  int32_t number_of_gpus;   /* the table key the partition is listed under                               */
+  int32_t allocation_score; /* AllocationScore                                                           */
+  int32_t pad;
+  int64_t ring_bus_bandwidth; /* RingBusBandwidth.Value(), KE_ABSENT = nil                               */
+} ke_gpu_partition; /* 24 bytes */
+#define KE_MAX_GPU_PARTITIONS 64 /* partitions per node table */
 
 /* Framework profile: score plugin weights (config/manager/scheduler-config.yaml:85-94). */
 typedef struct ke_config {
@@ -382,7 +421,29 @@ typedef struct ke_pod {
   int16_t quota;
   uint8_t quota_non_preemptible; /* extension.IsPodNonPreemptible (label preemptible=false) */
   uint8_t pad2;
+  /* DeviceShare allocation annotations (apis/extension/device_share.go; parsed by utils.go:355-513) */
+  int64_t gpu_ring_bus_bandwidth;      /* GPUPartitionSpec.RingBusBandwidth.Value(), KE_ABSENT = nil       */
+  int32_t gpu_required_topology_scope; /* DeviceAllocateHints[gpu].RequiredTopologyScope: KE_SCOPE_*       */
+  uint8_t gpu_partition_spec;          /* annotation GPUPartitionSpec present (honorGPUPartition)         */
+  uint8_t gpu_partition_restricted;    /* GPUPartitionSpec.AllocatePolicy == Restricted                   */
+  uint8_t device_joint_allocate;       /* DeviceJointAllocate annotation that keeps >= 1 requested device type:
+                                          tryJointAllocate (device_allocator.go:205-300) is not implemented */
+  uint8_t device_hints;                /* KE_DHINT_* bits of DeviceAllocateHints this evaluator does not model */
 } ke_pod;
+
+/* ke_pod.gpu_required_topology_scope: apiext.DeviceTopologyScope and its DeviceTopologyScopeLevel */
+#define KE_SCOPE_NONE 0     /* ""                                                  */
+#define KE_SCOPE_NODE 1     /* "Node"      level 1                                 */
+#define KE_SCOPE_NUMA 2     /* "NUMANode"  level 2                                 */
+#define KE_SCOPE_PCIE 3     /* "PCIe"      level 3                                 */
+#define KE_SCOPE_DEVICE 4   /* "Device"    level 4                                 */
+#define KE_SCOPE_UNKNOWN 5  /* any other non-empty string: required, level 0       */
+/* ke_pod.device_hints: fields of the DeviceAllocateHints annotation (any device type) outside the modelled
+ * path -> KE_ERR_UNSUPPORTED.  A hint with none of them set changes nothing (devicehandler_default.go:44-93). */
+#define KE_DHINT_SELECTOR 1u        /* DeviceHint.Selector (filterNodeDevice by device labels)          */
+#define KE_DHINT_VF 2u              /* DeviceHint.VFSelector: mustAllocateVF (device_allocator.go:396-460) */
+#define KE_DHINT_STRATEGY 4u        /* DeviceHint.AllocateStrategy (ApplyForAll / RequestsAsCount)       */
+#define KE_DHINT_EXCLUSIVE 8u       /* DeviceHint.ExclusivePolicy (PCIe-level exclusive)                  */
 
 /* One candidate of a pod's speculative top-k list (device order: best first). */
 typedef struct ke_candidate {
@@ -437,6 +498,14 @@ int ke_estimate_pod(ke_ctx* ctx, const ke_pod* pod, int64_t* est);
 int ke_node_devices_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_device* devices);
 /* Drop the node's cache entry (getNodeDevice == nil: DeviceShare Filter passes, Score is 0). */
 int ke_node_devices_delete(ke_ctx* ctx, int32_t node);
+/* The node's GPU partition indexer and policy as GPUAllocator.Allocate resolves them (allocator_gpu.go:77-82,
+ * device_cache.go:532-545): has_table = the indexer is not nil (the Device's gpu-partitions annotation, else
+ * the designated table of the node's GPU model), honor = the matching GPUPartitionPolicy label is Honor.
+ * Partitions with the same (number_of_gpus, allocation_score) keep their table order; such a group may hold
+ * at most 12 partitions (selectPartitionByBinPack's sort.Slice is stable only up to 12 elements), else
+ * KE_ERR_UNSUPPORTED.  Kept across ke_node_devices_set; dropped with ke_node_devices_delete. */
+int ke_node_gpu_partitions(ke_ctx* ctx, int32_t node, int32_t has_table, int32_t honor, int32_t n,
+                           const ke_gpu_partition* partitions);
 /* NodeResourceTopology informer + resource manager state of `node`: its NUMA zones (n <= KE_MAX_NUMA,
  * n = 0: no NUMA resources).  Read when the node's NUMA topology policy is not None. */
 int ke_node_numa_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_numa_zone* zones);

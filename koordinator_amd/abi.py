@@ -9,7 +9,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 ABSENT = -1
 
 OK = 0
@@ -46,6 +46,20 @@ REASON_DS_INVALID_REQUEST = 32
 REASON_DS_INSUFFICIENT_GPU = 33
 REASON_DS_INSUFFICIENT_RDMA = 34
 REASON_DS_INSUFFICIENT_FPGA = 35
+REASON_DS_MISSING_PARTITION_TABLE = 36
+REASON_DS_UNSUPPORTED_GPU_REQUESTS = 37
+REASON_DS_INSUFFICIENT_PARTITIONED = 38
+REASON_DS_MISSING_TOPOLOGY_TREE = 39
+REASON_DS_MULTI_SHARED_GPU = 40
+REASON_DS_INSUFFICIENT_TOPOLOGY_SCOPED = 41
+REASON_DS_INSUFFICIENT_GPU_TOPOLOGY = 42
+# ke_pod.gpu_required_topology_scope (apiext.DeviceTopologyScope -> level)
+SCOPE_NONE, SCOPE_NODE, SCOPE_NUMA, SCOPE_PCIE, SCOPE_DEVICE, SCOPE_UNKNOWN = range(6)
+SCOPES = {"": SCOPE_NONE, "Node": SCOPE_NODE, "NUMANode": SCOPE_NUMA, "PCIe": SCOPE_PCIE, "Device": SCOPE_DEVICE}
+# ke_pod.device_hints bits (DeviceAllocateHints fields the evaluator does not model)
+DHINT_SELECTOR, DHINT_VF, DHINT_STRATEGY, DHINT_EXCLUSIVE = 1, 2, 4, 8
+TEMPLATE_KEY_CORE, TEMPLATE_KEY_MEMORY, TEMPLATE_KEY_MEMORY_RATIO = 1, 2, 4
+MAX_GPU_PARTITIONS = 64
 
 DEV_GPU, DEV_RDMA, DEV_FPGA = 0, 1, 2
 DEV_TYPES = 3
@@ -97,13 +111,14 @@ class LoadAwareArgs(C.Structure):
         ("score_according_prod_usage", u8),
         ("allow_customize_estimation", u8),
         ("has_aggregated", u8),
-        ("pad", u8 * 3),
+        ("has_other_keys", u8),
+        ("pad", u8 * 2),
     ]
 
 
 class NumaArgs(C.Structure):
     _fields_ = [("weights", i64 * NRES), ("strategy", i32), ("numa_strategy", i32), ("default_cpu_bind_policy", i32),
-                ("pad", i32)]
+                ("has_other_keys", u8), ("pad", u8 * 3)]
 
 
 class Cpu(C.Structure):
@@ -125,7 +140,8 @@ class NumaZone(C.Structure):
 
 
 class DeviceShareArgs(C.Structure):
-    _fields_ = [("weights", i64 * 4), ("strategy", i32), ("pad", i32)]
+    _fields_ = [("weights", i64 * 4), ("strategy", i32), ("template_matched_keys", u8), ("has_other_keys", u8),
+                ("pad", u8 * 2)]
 
 
 class Device(C.Structure):
@@ -135,10 +151,17 @@ class Device(C.Structure):
         ("health", u8),
         ("has_total", u8 * DKEYS),
         ("has_used", u8 * DKEYS),
-        ("pad", u8),
+        ("has_topology", u8),
         ("total", i64 * DKEYS),
         ("used", i64 * DKEYS),
+        ("numa_node", i32),
+        ("pcie_rank", i32),
     ]
+
+
+class GpuPartition(C.Structure):
+    _fields_ = [("minors", C.c_uint32), ("number_of_gpus", i32), ("allocation_score", i32), ("pad", i32),
+                ("ring_bus_bandwidth", i64)]
 
 
 class Config(C.Structure):
@@ -232,6 +255,12 @@ class Pod(C.Structure):
         ("quota", C.c_int16),
         ("quota_non_preemptible", u8),
         ("pad2", u8),
+        ("gpu_ring_bus_bandwidth", i64),
+        ("gpu_required_topology_scope", i32),
+        ("gpu_partition_spec", u8),
+        ("gpu_partition_restricted", u8),
+        ("device_joint_allocate", u8),
+        ("device_hints", u8),
     ]
 
 
@@ -261,7 +290,7 @@ class Quota(C.Structure):
 
 
 STRUCTS = [Config, Node, NodeMetric, PodMetric, AggregatedUsage, Pod, ResourceMap, LoadAwareArgs, NumaArgs,
-           DeviceShareArgs, Device, NumaZone, Cpu, QuotaArgs, Quota]
+           DeviceShareArgs, Device, NumaZone, Cpu, QuotaArgs, Quota, GpuPartition]
 QUOTA_DTYPE = np.dtype(Quota)
 
 # numpy views of the same layouts (bulk loads)
@@ -271,6 +300,7 @@ POD_METRIC_DTYPE = np.dtype(PodMetric)
 AGG_DTYPE = np.dtype(AggregatedUsage)
 POD_DTYPE = np.dtype(Pod)
 DEVICE_DTYPE = np.dtype(Device)
+GPU_PARTITION_DTYPE = np.dtype(GpuPartition)
 NUMA_ZONE_DTYPE = np.dtype(NumaZone)
 CPU_DTYPE = np.dtype(Cpu)
 
@@ -334,6 +364,7 @@ EXPORTS = {
     "ke_estimate_pod": (C.c_int, [C.c_void_p, C.POINTER(Pod), C.c_void_p]),
     "ke_eval": (C.c_int, [C.c_void_p, i32, C.c_void_p, i64] + [C.c_void_p] * 7),
     "ke_node_devices_set": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p]),
+    "ke_node_gpu_partitions": (C.c_int, [C.c_void_p, i32, i32, i32, i32, C.c_void_p]),
     "ke_node_devices_delete": (C.c_int, [C.c_void_p, i32]),
     "ke_node_numa_set": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p]),
     "ke_last_device_allocations": (C.c_int, [C.c_void_p, i32, C.c_void_p]),

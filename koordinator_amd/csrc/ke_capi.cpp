@@ -73,6 +73,23 @@ static int check_numa_deviceshare(ke_ctx* ctx, const ke_pod* pods, int32_t n) {
   return KE_OK;
 }
 
+// allocateByTemplate (allocator_gpu.go:135-159): a shared-GPU pod whose per-GPU request names one of
+// GPUSharedResourceTemplatesMatchedResources enforces a template (utils.go:508-515); not implemented.
+static int check_gpu_templates(ke_ctx* ctx, const ke_pod* pods, int32_t n) {
+  const uint32_t keys = ctx->c.cfg.deviceshare.template_matched_keys;
+  if (!keys) return KE_OK;
+  for (int32_t p = 0; p < n; p++) {
+    const DevPod d = make_dev_pod(ctx->c.cfg, pods[p]);
+    if (!(d.flags & PF_DS) || !d.ds_cnt[KE_DEV_GPU] || !(d.flags & PF_GPU_SHARED)) continue;
+    uint32_t req = 0;
+    if (d.flags & PF_DS_H_CORE) req |= KE_TEMPLATE_KEY_CORE;
+    if (d.flags & PF_DS_H_RATIO) req |= KE_TEMPLATE_KEY_MEMORY_RATIO;
+    else if (d.flags & PF_DS_H_MEM) req |= KE_TEMPLATE_KEY_MEMORY;
+    if (req & keys) return fail(KE_ERR_UNSUPPORTED, "shared-GPU pods allocated by GPU shared resource template");
+  }
+  return KE_OK;
+}
+
 // A pod that may bind CPUs (a cpuset pod, or any cpu request while a node forces CPU binding) reads the
 // CPU SoA during evaluation: make sure it exists.
 static int check_cpuset(ke_ctx* ctx, const ke_pod* pods, int32_t n) {
@@ -95,7 +112,7 @@ int ke_abi_struct_sizes(int32_t* sizes, int32_t n) {
                          (int32_t)sizeof(ke_numa_args), (int32_t)sizeof(ke_deviceshare_args),
                          (int32_t)sizeof(ke_device),       (int32_t)sizeof(ke_numa_zone),
                          (int32_t)sizeof(ke_cpu),          (int32_t)sizeof(ke_quota_args),
-                         (int32_t)sizeof(ke_quota)};
+                         (int32_t)sizeof(ke_quota),        (int32_t)sizeof(ke_gpu_partition)};
   const int32_t m = (int32_t)(sizeof(all) / sizeof(all[0]));
   for (int32_t i = 0; i < n && i < m; i++) sizes[i] = all[i];
   return m;
@@ -205,6 +222,24 @@ int ke_node_devices_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_device* d
   return KE_OK;
 }
 
+int ke_node_gpu_partitions(ke_ctx* ctx, int32_t node, int32_t has_table, int32_t honor, int32_t n,
+                           const ke_gpu_partition* partitions) {
+  int rc = check_node(ctx, node);
+  if (ctx) flush_mirror(ctx->c);
+  if (rc) return rc;
+  if (n > 0 && !has_table) return fail(KE_ERR_INVALID, "partitions without a table");
+  int id = -1;
+  if (has_table) {
+    id = ptable_intern(ctx->c, n, partitions);
+    if (id < 0) return id;
+  }
+  NodeState& ns = ctx->c.nodes[node];
+  ns.ptable = id;
+  ns.gpu_honor = honor != 0;
+  ns.dirty = true;
+  return KE_OK;
+}
+
 int ke_node_devices_delete(ke_ctx* ctx, int32_t node) {
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);
@@ -212,6 +247,8 @@ int ke_node_devices_delete(ke_ctx* ctx, int32_t node) {
   NodeState& ns = ctx->c.nodes[node];
   ns.has_dev_cache = false;
   ns.devs.clear();
+  ns.ptable = -1;
+  ns.gpu_honor = false;
   ns.dirty = true;
   return KE_OK;
 }
@@ -418,6 +455,8 @@ int ke_eval(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, uin
   if (rc) return rc;
   rc = check_numa_deviceshare(ctx, pods, n_pods);
   if (rc) return rc;
+  rc = check_gpu_templates(ctx, pods, n_pods);
+  if (rc) return rc;
   rc = check_cpuset(ctx, pods, n_pods);
   if (rc) return rc;
   rc = require_device(ctx);
@@ -432,6 +471,8 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
   int rc = check_pods(pods, n_pods);
   if (rc) return rc;
   rc = check_numa_deviceshare(ctx, pods, n_pods);
+  if (rc) return rc;
+  rc = check_gpu_templates(ctx, pods, n_pods);
   if (rc) return rc;
   rc = check_cpuset(ctx, pods, n_pods);
   if (rc) return rc;

@@ -54,6 +54,13 @@ int validate_config(const ke_config& cfg) {
   }
   if (cfg.numa.strategy != KE_STRATEGY_LEAST_ALLOCATED && cfg.numa.strategy != KE_STRATEGY_MOST_ALLOCATED)
     return fail(KE_ERR_INVALID, "numa scoring strategy");
+  if (cfg.loadaware.has_other_keys)
+    return fail(KE_ERR_UNSUPPORTED, "LoadAwareSchedulingArgs maps with keys other than cpu/memory");
+  if (cfg.numa.has_other_keys)
+    return fail(KE_ERR_UNSUPPORTED, "NodeNUMAResource ScoringStrategy resources other than cpu/memory");
+  if (cfg.deviceshare.has_other_keys)
+    return fail(KE_ERR_UNSUPPORTED, "DeviceShare ScoringStrategy resources other than gpu-memory(-ratio)/rdma/fpga");
+  if (cfg.deviceshare.template_matched_keys & ~7u) return fail(KE_ERR_INVALID, "template_matched_keys");
   const auto& a = cfg.loadaware;
   if (a.agg_usage_type < 0 || a.agg_usage_type >= KE_AGG_TYPES || a.agg_score_type < 0 || a.agg_score_type >= KE_AGG_TYPES)
     return fail(KE_ERR_INVALID, "aggregation type");
@@ -89,6 +96,8 @@ int validate_devices(int32_t n, const ke_device* devs) {
     for (int k = 0; k < KE_DKEYS; k++)
       if ((d.has_total[k] && d.total[k] < 0) || (d.has_used[k] && d.used[k] < 0))
         return fail(KE_ERR_INVALID, "negative device quantity");
+    if (d.has_topology && (d.pcie_rank < 0 || d.pcie_rank >= KE_DEV_TYPES * KE_MAX_MINORS))
+      return fail(KE_ERR_INVALID, "device pcie_rank out of range");
     // fillGPUTotalMem divides by the instance's gpu-memory (devicehandler_gpu.go:110-125)
     if (d.type == KE_DEV_GPU && d.health && !(d.has_total[KE_DKEY_GPU_MEMORY] && d.total[KE_DKEY_GPU_MEMORY] > 0))
       return fail(KE_ERR_UNSUPPORTED, "healthy GPU device without a positive gpu-memory total");
@@ -96,10 +105,44 @@ int validate_devices(int32_t n, const ke_device* devs) {
   return KE_OK;
 }
 
+// GetGPUTopologyScope (allocator_gpu_helper.go:202-263) as per-minor scope ranks: NUMA scopes ascending by
+// NodeID, PCIe scopes in depth-first order (NUMA rank, then PCIEID).  Returns false for a nil tree.
+static bool gpu_topology_ranks(const NodeState& ns, uint64_t* topo, uint64_t* pcie) {
+  std::vector<int32_t> numa;
+  std::vector<std::pair<int32_t, int32_t>> pc;  // (numa rank, pcie rank)
+  int n_gpu = 0;
+  for (const ke_device& d : ns.devs) {
+    if (d.type != KE_DEV_GPU) continue;
+    if (!d.has_topology) return false;
+    n_gpu++;
+    numa.push_back(d.numa_node);
+  }
+  if (n_gpu == 0) return false;
+  std::sort(numa.begin(), numa.end());
+  numa.erase(std::unique(numa.begin(), numa.end()), numa.end());
+  auto numa_rank = [&](int32_t id) { return (int32_t)(std::lower_bound(numa.begin(), numa.end(), id) - numa.begin()); };
+  for (const ke_device& d : ns.devs)
+    if (d.type == KE_DEV_GPU) pc.emplace_back(numa_rank(d.numa_node), d.pcie_rank);
+  std::sort(pc.begin(), pc.end());
+  pc.erase(std::unique(pc.begin(), pc.end()), pc.end());
+  *topo = *pcie = 0;
+  for (const ke_device& d : ns.devs) {
+    if (d.type != KE_DEV_GPU) continue;
+    const int32_t nr = numa_rank(d.numa_node);
+    const int32_t pr = (int32_t)(std::lower_bound(pc.begin(), pc.end(), std::make_pair(nr, d.pcie_rank)) - pc.begin());
+    *topo |= (uint64_t)nr << (4 * d.minor);
+    *pcie |= (uint64_t)pr << (4 * d.minor);
+  }
+  return true;
+}
+
 void derive_ds_row(const NodeState& ns, int64_t* f, uint64_t* m) {
   for (int i = 0; i < NUM_DS_FIELDS; i++) f[i] = 0;
   for (int i = 0; i < NUM_DS_MASKS; i++) m[i] = 0;
   if (!ns.has_dev_cache) return;
+  if (gpu_topology_ranks(ns, &m[DSM_TOPO], &m[DSM_PCIE])) m[DSM_EXISTS] |= DSX_TOPO;
+  if (ns.gpu_honor) m[DSM_EXISTS] |= DSX_HONOR;
+  if (ns.ptable >= 0) m[DSM_EXISTS] |= DSX_TABLE | ((uint64_t)ns.ptable << DSX_TABLE_SHIFT);
   for (const ke_device& d : ns.devs) {
     const int t = d.type, mi = d.minor;
     m[DSM_EXISTS] |= 1ull << (16 * t + mi);
@@ -114,6 +157,49 @@ void derive_ds_row(const NodeState& ns, int64_t* f, uint64_t* m) {
       }
     }
   }
+}
+
+int ptable_intern(Context& c, int32_t n, const ke_gpu_partition* parts) {
+  if (n < 0 || n > KE_MAX_GPU_PARTITIONS || (n > 0 && !parts)) return fail(KE_ERR_INVALID, "partition count");
+  std::vector<int> order((size_t)n);
+  for (int i = 0; i < n; i++) {
+    const ke_gpu_partition& q = parts[i];
+    if (q.minors == 0 || (q.minors >> KE_MAX_MINORS)) return fail(KE_ERR_INVALID, "partition minors (non-empty, 0..15)");
+    if (q.number_of_gpus < 1 || q.number_of_gpus > 255) return fail(KE_ERR_INVALID, "partition number_of_gpus");
+    if (q.ring_bus_bandwidth < 0 && q.ring_bus_bandwidth != KE_ABSENT) return fail(KE_ERR_INVALID, "ring bus bandwidth");
+    order[(size_t)i] = i;
+  }
+  // GetGPUPartitionIndexer (allocator_gpu_helper.go:165-200): per number of GPUs, groups of equal
+  // AllocationScore ascending, table order inside a group
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+    if (parts[a].number_of_gpus != parts[b].number_of_gpus) return parts[a].number_of_gpus < parts[b].number_of_gpus;
+    return parts[a].allocation_score < parts[b].allocation_score;
+  });
+  std::vector<uint64_t> t((size_t)PT_WORDS, 0);
+  int group = -1, in_group = 0;
+  for (int k = 0; k < n; k++) {
+    const ke_gpu_partition& q = parts[order[(size_t)k]];
+    const bool same_n = k > 0 && parts[order[(size_t)k - 1]].number_of_gpus == q.number_of_gpus;
+    if (!same_n) group = -1;
+    if (!same_n || parts[order[(size_t)k - 1]].allocation_score != q.allocation_score) {
+      group++;
+      in_group = 0;
+    }
+    // selectPartitionByBinPack sorts the feasible partitions of one group with sort.Slice, which is a
+    // stable insertion sort only up to 12 elements (Go pdqsort)
+    if (++in_group > 12) return fail(KE_ERR_UNSUPPORTED, "more than 12 GPU partitions with one (number_of_gpus, allocation_score)");
+    if (group > 255) return fail(KE_ERR_UNSUPPORTED, "partition groups");
+    t[(size_t)k] = (uint64_t)q.minors | (uint64_t)q.number_of_gpus << 16 | (uint64_t)group << 24 |
+                   (uint64_t)(uint32_t)q.allocation_score << 32;
+    t[(size_t)(PT_SLOTS + k)] = (uint64_t)q.ring_bus_bandwidth;
+  }
+  const size_t n_tab = c.ptab.size() / PT_WORDS;
+  for (size_t id = 0; id < n_tab; id++)
+    if (std::equal(t.begin(), t.end(), c.ptab.begin() + (ptrdiff_t)(id * PT_WORDS))) return (int)id;
+  if (n_tab >= (size_t)MAX_PTABLES) return fail(KE_ERR_UNSUPPORTED, "more than 4096 distinct GPU partition tables");
+  c.ptab.insert(c.ptab.end(), t.begin(), t.end());
+  c.ptab_dirty = true;
+  return (int)n_tab;
 }
 
 void host_ds_reserve(const ke_config& cfg, NodeState& ns, const DevPod& dp, uint64_t mask) {
@@ -160,6 +246,19 @@ int validate_pod(const ke_pod& p) {
     return fail(KE_ERR_INVALID, "pod NUMA topology policy");
   if (p.numa_exclusive < KE_NUMA_EXCLUSIVE_NONE || p.numa_exclusive > KE_NUMA_EXCLUSIVE_REQUIRED)
     return fail(KE_ERR_INVALID, "pod NUMA exclusive policy");
+  if (p.gpu_required_topology_scope < KE_SCOPE_NONE || p.gpu_required_topology_scope > KE_SCOPE_UNKNOWN)
+    return fail(KE_ERR_INVALID, "pod GPU required topology scope");
+  if (p.device_joint_allocate)  // tryJointAllocate / validateJointAllocation (device_allocator.go:205-300)
+    return fail(KE_ERR_UNSUPPORTED, "DeviceJointAllocate annotation (joint GPU/RDMA allocation) is not implemented");
+  if (p.device_hints & KE_DHINT_VF)  // mustAllocateVF -> allocateVF (device_allocator.go:87-92,396-460)
+    return fail(KE_ERR_UNSUPPORTED, "DeviceHint VFSelector (virtual function allocation) is not implemented");
+  if (p.device_hints & KE_DHINT_SELECTOR)  // filterNodeDevice by device labels (device_allocator.go:137-166)
+    return fail(KE_ERR_UNSUPPORTED, "DeviceHint Selector is not implemented");
+  if (p.device_hints & KE_DHINT_STRATEGY)  // ApplyForAll / RequestsAsCount (devicehandler_default.go:58-90)
+    return fail(KE_ERR_UNSUPPORTED, "DeviceHint AllocateStrategy is not implemented");
+  if (p.device_hints & KE_DHINT_EXCLUSIVE)  // filterFreeDevicesByPCIe (device_cache.go:372-376,417-440)
+    return fail(KE_ERR_UNSUPPORTED, "DeviceHint ExclusivePolicy is not implemented");
+  if (p.device_hints) return fail(KE_ERR_INVALID, "unknown device hint bits");
   return KE_OK;
 }
 
@@ -278,8 +377,9 @@ static bool ds_prepare(const ke_pod& pod, DevPod& d) {
     if (h_ratio) {  // ratio wins over memory (devicehandler_gpu.go:83-92)
       d.flags |= PF_DS_H_RATIO;
       d.ds_req[2] = ratio / n;
+      if (ratio / n < 100) d.flags |= PF_GPU_SHARED;  // isShared
     } else if (h_mem) {
-      d.flags |= PF_DS_H_MEM;
+      d.flags |= PF_DS_H_MEM | PF_GPU_SHARED;
       d.ds_req[1] = mem / n;
     }
   }
@@ -352,6 +452,17 @@ DevPod make_dev_pod(const ke_config& cfg, const ke_pod& pod) {
     d.flags |= PF_DS;
   }
   if (pod.quota_non_preemptible) d.flags |= PF_QUOTA_NP;
+  // parseGPURequirements (utils.go:487-513): GPUPartitionSpec and the GPU hint's required topology scope
+  d.flags |= (uint32_t)pod.gpu_required_topology_scope * PF_GPU_SCOPE0;
+  d.ring_bw = KE_ABSENT;
+  if (pod.gpu_partition_spec) {
+    d.flags |= PF_GPU_PART_SPEC;
+    if (pod.gpu_partition_restricted) d.flags |= PF_GPU_PART_RESTRICTED;
+    if (pod.gpu_ring_bus_bandwidth != KE_ABSENT) {
+      d.flags |= PF_GPU_RING_BW;
+      d.ring_bw = pod.gpu_ring_bus_bandwidth;
+    }
+  }
   return d;
 }
 

@@ -36,6 +36,9 @@ struct NodeState {
   // DeviceShare node device cache entry (device_cache.go:518-568)
   bool has_dev_cache = false;
   std::vector<ke_device> devs;
+  // GPU partition indexer / policy (ke_node_gpu_partitions): table id in Context::ptab, -1 = nil indexer
+  int32_t ptable = -1;
+  bool gpu_honor = false;
   // derived
   bool dirty = true;            // row must be re-derived and uploaded
   int64_t valid_until = INT64_MAX;  // derived row is exact for now < valid_until
@@ -89,7 +92,13 @@ struct Context {
   std::vector<uint8_t> qlimit_has; // [q * KE_NRES + r]
   bool quota_dirty = false;        // host table newer than the device table
   bool quota_on_device = false;    // the device table holds the current used (after a ke_schedule)
+  // GPU partition tables, deduplicated: PT_WORDS words per table (ke_types.h), uploaded when ptab_dirty
+  std::vector<uint64_t> ptab;
+  bool ptab_dirty = false;
 };
+
+// Encode a node's partition table (validated) into the pool; returns its id or a negative KE_ERR_*.
+int ptable_intern(Context& c, int32_t n, const ke_gpu_partition* parts);
 
 // ElasticQuota used limits of every quota (RuntimeQuotaCalculator over the tree, or Max)
 int quota_compute_limits(const ke_quota_args& args, const std::vector<ke_quota>& q, std::vector<int64_t>& limit,

@@ -63,6 +63,7 @@ struct SoA {
   int64_t* qt;      // ElasticQuota: NUM_QF arrays of QT_STRIDE int64 (nullptr until a tree is loaded)
   int32_t* qm;      // ElasticQuota: QT_STRIDE meta words (ke_types.h qm_*)
   int64_t* rec;     // replay records: NUM_RW int64 words per node, row-major (RecWord)
+  uint64_t* pt;     // GPU partition tables: PT_WORDS words per table (ke_types.h), nullptr until one is set
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -255,6 +256,7 @@ __device__ __forceinline__ bool pod_req_has(const DevPod& p, int t, int k) {
 struct DsInst {
   int64_t tv[3], fv[3];
   uint32_t th, fh;  // key presence of total / free'
+  bool used_nz;     // used' kept (non-zero): the minor is in getRealUsed (allocator_gpu.go:59-70)
 };
 __device__ __forceinline__ void ds_instance(const SoA& s, int64_t i, int t, int m, const uint64_t msk[4], DsInst& d) {
   const int nk = DS_NK[t];
@@ -280,6 +282,7 @@ __device__ __forceinline__ void ds_instance(const SoA& s, int64_t i, int t, int 
   bool up_zero = true;
 #pragma unroll
   for (int k = 0; k < 3; k++) up_zero = up_zero && !(((uh >> k) & 1) && up[k] != 0);
+  d.used_nz = !up_zero;
   d.fh = up_zero ? d.th : uh;
 #pragma unroll
   for (int k = 0; k < 3; k++) {
@@ -288,16 +291,33 @@ __device__ __forceinline__ void ds_instance(const SoA& s, int64_t i, int t, int 
   }
 }
 
-// quotav1.IsZero(free') false and quotav1.LessThanOrEqual(request, free')
-__device__ __forceinline__ bool ds_satisfied(const DsInst& d, const DevPod& p, int t) {
-  bool zero = true, leq = true;
+// quotav1.IsZero(free')
+__device__ __forceinline__ bool ds_free_zero(const DsInst& d) {
+  bool zero = true;
+#pragma unroll
+  for (int k = 0; k < 3; k++) zero = zero && !(((d.fh >> k) & 1) && d.fv[k] != 0);
+  return zero;
+}
+// quotav1.LessThanOrEqual(request, free'): the keys of free' the request also has
+__device__ __forceinline__ bool ds_leq(const DsInst& d, const DevPod& p, int t) {
+  bool leq = true;
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     const bool fh = (d.fh >> k) & 1;
-    zero = zero && !(fh && d.fv[k] != 0);
     if (fh && k < DS_NK[t] && pod_req_has(p, t, k) && p.ds_req[ds_req_slot(t, k)] > d.fv[k]) leq = false;
   }
-  return !zero && leq;
+  return leq;
+}
+// defaultAllocateDevices' test: !IsZero(free') && LessThanOrEqual(request, free')
+__device__ __forceinline__ bool ds_satisfied(const DsInst& d, const DevPod& p, int t) {
+  return !ds_free_zero(d) && ds_leq(d, p, t);
+}
+// removeZeroDevice: the instance's total is not zero
+__device__ __forceinline__ bool ds_total_nz(const DsInst& d) {
+  bool nz = false;
+#pragma unroll
+  for (int k = 0; k < 3; k++) nz = nz || (((d.th >> k) & 1) && d.tv[k] != 0);
+  return nz;
 }
 
 __device__ __forceinline__ int64_t ds_res_score(bool most, int64_t req, int64_t cap) {  // scoring.go:283-322
@@ -321,8 +341,215 @@ __device__ __forceinline__ int64_t ds_weighted(const KArgs& k, int t, const int6
   return ws ? sc / ws : 0;
 }
 
-// Filter (Prepare + per-type count of satisfiable instances) and raw Score of DeviceShare for a pod
-// with PF_DS on a node with a cache entry.  Types in the fixed order GPU, RDMA, FPGA.
+// ---- GPUAllocator.Allocate (allocator_gpu.go:72-451) ------------------------------------------------
+// The node's GPUs as AllocateContext sees them, as minor masks.
+struct GpuMasks {
+  uint32_t minors;  // every GPU device (DeviceInfos; the scope tree's minors)
+  uint32_t total;   // removeZeroDevice(deviceTotal[GPU]); 0 when the filtered view dropped the type
+  uint32_t used;    // deviceUsedMinorsHash
+  uint32_t sat;     // allocateFromScope: LessThanOrEqual(request, deviceFree) && in deviceTotal
+  uint32_t dflt;    // defaultAllocateDevices: !IsZero(free') && LessThanOrEqual(request, free')
+};
+
+// minors whose 4-bit rank in `w` equals r (SWAR nibble compare)
+__device__ __forceinline__ uint32_t rank_mask(uint64_t w, int r) {
+  const uint64_t x = w ^ ((uint64_t)(uint32_t)r * 0x1111111111111111ull);
+  const uint64_t lo = 0x7777777777777777ull;
+  const uint64_t t = ~(((x & lo) + lo) | x | lo);  // bit 4k+3 set iff nibble k == 0
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) m |= (uint32_t)((t >> (4 * k + 3)) & 1) << k;
+  return m;
+}
+
+enum GpuSt : int { GS_OK = 0, GS_NONE = 1 };  // a stage allocated / fell through
+
+// allocateByPartition (allocator_gpu.go:177-237) + selectPartitionByBinPack (:261-296) over the node's table.
+// Returns the chosen minors, 0 = none; *why = the failure reason (MISSING/UNSUPPORTED/INSUFFICIENT).
+__device__ uint32_t gpu_partition(const SoA& s, uint64_t ex0, const DevPod& p, int want, const GpuMasks& g,
+                                  bool select, int* why) {
+  if (!(ex0 & DSX_TABLE)) {
+    *why = KE_REASON_DS_MISSING_PARTITION_TABLE;
+    return 0;
+  }
+  const uint64_t* tab = s.pt + (int64_t)(ex0 >> DSX_TABLE_SHIFT) * PT_WORDS;
+  const bool restricted = p.flags & PF_GPU_PART_RESTRICTED;
+  int group = -1, nf = 0;
+  uint32_t best = 0;
+  int64_t best_score = 0;
+  for (int e = 0; e < PT_SLOTS; e++) {
+    const uint64_t w = tab[e];
+    if (pt_gpus(w) == 0) break;
+    if (pt_gpus(w) != want) continue;
+    if (pt_group(w) != group) {
+      if (nf > 0 || (restricted && group >= 0)) break;  // the first group with a feasible partition
+      group = pt_group(w);
+    }
+    const uint32_t pm = pt_minors(w);
+    if (pm & g.used) continue;
+    if ((g.total & pm) != pm) continue;
+    if (p.flags & PF_GPU_RING_BW) {
+      const int64_t bw = (int64_t)tab[PT_SLOTS + e];
+      if (bw == KE_ABSENT || p.ring_bw > bw) continue;
+    }
+    nf++;
+    if (!select) return pm;
+    // BinPackScore: the 8/4/2-GPU partitions of each lowest-score group that stay free
+    const uint32_t alloc = g.used | pm;
+    int64_t score = 0;
+    for (int f = 0; f < PT_SLOTS; f++) {
+      const uint64_t q = tab[f];
+      const int c = pt_gpus(q);
+      if (c == 0) break;
+      if ((c != 8 && c != 4 && c != 2) || c < want || pt_group(q) != 0 || (pt_minors(q) & alloc)) continue;
+      score += (int64_t)(c == 8 ? 10000 : c == 4 ? 100 : 1) * pt_score(q);
+    }
+    if (nf == 1 || score > best_score) {  // stable descending sort: first of the maxima
+      best = pm;
+      best_score = score;
+    }
+  }
+  *why = group < 0 ? KE_REASON_DS_UNSUPPORTED_GPU_REQUESTS : KE_REASON_DS_INSUFFICIENT_PARTITIONED;
+  return best;
+}
+
+// One scope's own candidates (allocator_gpu.go:393-450): the first `want` satisfied minors ascending, or
+// for a shared GPU the satisfied minor of the highest scoreDevice (first on ties).
+struct ScopeRes {
+  uint32_t minors;  // 0 = no result
+  int depth, cum;
+  int64_t score;
+};
+__device__ __forceinline__ void scope_take(uint32_t mask, int level, int depth, int cum, int req_level, int want,
+                                           bool shared, const GpuMasks& g, const int64_t* dscore, ScopeRes& r) {
+  r.minors = 0;
+  if (req_level > level) return;
+  const uint32_t sm = g.sat & mask;
+  if (!shared) {
+    if (__builtin_popcount(sm) < want) return;
+    uint32_t c = 0, rest = sm;
+    for (int n = 0; n < want; n++) {
+      c |= rest & (0u - rest);
+      rest &= rest - 1;
+    }
+    r.minors = c;
+    r.score = -1;
+  } else {
+    if (!sm) return;
+    int bm = -1;
+    int64_t bs = -1;
+    for (uint32_t rest = sm; rest; rest &= rest - 1) {
+      const int m = __builtin_ctz(rest);
+      if (dscore[m] > bs) bm = m, bs = dscore[m];
+    }
+    r.minors = 1u << bm;
+    r.score = bs;
+  }
+  r.depth = depth;
+  r.cum = cum;
+}
+__device__ __forceinline__ bool scope_better(const ScopeRes& best, const ScopeRes& r, bool shared) {
+  if (!best.minors) return true;
+  if (best.depth < r.depth || (best.depth == r.depth && best.cum < r.cum)) return true;
+  return shared && best.depth == r.depth && best.cum == r.cum && best.score < r.score;
+}
+
+// allocateFromScope over the tree Node > NUMANode > PCIe (allocator_gpu.go:357-451; tree from
+// GetGPUTopologyScope, allocator_gpu_helper.go:202-263).  dscore: per-minor scoreDevice (shared GPUs).
+__device__ uint32_t gpu_topology(const SoA& s, int64_t i, const DevPod& p, int want, const GpuMasks& g,
+                                 const int64_t* dscore) {
+  const bool shared = p.flags & PF_GPU_SHARED;
+  const int req_level = scope_level(pod_scope(p.flags));
+  if (__builtin_popcount(g.minors) < want) return 0;
+  const uint64_t topo = dsmask(s, DSM_TOPO, i), pcie = dsmask(s, DSM_PCIE, i);
+  const int cum0 = (g.minors & g.used) ? 1 : 0;
+  ScopeRes best;
+  best.minors = 0;
+  for (int a = 0; a < DS_MINORS; a++) {  // NUMA scopes by NodeID
+    const uint32_t nm = rank_mask(topo, a) & g.minors;
+    if (!nm) break;
+    if (__builtin_popcount(nm) < want) continue;
+    const int cum1 = cum0 + ((nm & g.used) ? 1 : 0);
+    int lo = DS_MINORS, hi = -1;  // this NUMA node's PCIe scope ranks
+    for (uint32_t rest = nm; rest; rest &= rest - 1) {
+      const int r = (int)((pcie >> (4 * __builtin_ctz(rest))) & 15u);
+      lo = r < lo ? r : lo;
+      hi = r > hi ? r : hi;
+    }
+    ScopeRes nb;
+    nb.minors = 0;
+    for (int b = lo; b <= hi; b++) {
+      const uint32_t pm = rank_mask(pcie, b) & nm;
+      if (__builtin_popcount(pm) < want) continue;
+      ScopeRes r;
+      scope_take(pm, 3, 3, cum1 + ((pm & g.used) ? 1 : 0), req_level, want, shared, g, dscore, r);
+      if (r.minors && scope_better(nb, r, shared)) nb = r;
+    }
+    if (!nb.minors) scope_take(nm, 2, 2, cum1, req_level, want, shared, g, dscore, nb);
+    if (nb.minors && scope_better(best, nb, shared)) best = nb;
+  }
+  if (!best.minors) scope_take(g.minors, 1, 1, cum0, req_level, want, shared, g, dscore, best);
+  return best.minors;
+}
+
+// Filter feasibility of allocateFromScope: some scope at or below the required level has enough
+// satisfied minors (a deeper result always exists when a shallower one does, so no tree search).
+__device__ bool gpu_topology_feasible(const SoA& s, int64_t i, const DevPod& p, int want, const GpuMasks& g) {
+  const bool shared = p.flags & PF_GPU_SHARED;
+  const int need = shared ? 1 : want;
+  const int req_level = scope_level(pod_scope(p.flags));
+  if (__builtin_popcount(g.minors) < want) return false;
+  if (req_level <= 1) return __builtin_popcount(g.sat) >= need;
+  if (req_level > 3) return false;
+  const uint64_t w = dsmask(s, req_level == 2 ? DSM_TOPO : DSM_PCIE, i);
+  for (int r = 0; r < DS_MINORS; r++) {
+    const uint32_t m = rank_mask(w, r) & g.minors;
+    if (!m) break;
+    if (__builtin_popcount(m) >= want && __builtin_popcount(g.sat & m) >= need) return true;
+  }
+  return false;
+}
+
+// GPUAllocator.Allocate after allocateByTemplate (refused at the boundary).  Returns the framework code
+// (0 = allocated); *minors = the chosen minors when select (Reserve), else only feasibility is decided.
+__device__ int gpu_allocate(const SoA& s, int64_t i, uint64_t ex0, const DevPod& p, const GpuMasks& g, bool select,
+                            const int64_t* dscore, uint32_t* minors, int* reason) {
+  const int want = p.ds_cnt[KE_DEV_GPU];
+  const bool shared = p.flags & PF_GPU_SHARED;
+  const bool honor = (p.flags & PF_GPU_PART_SPEC) || (ex0 & DSX_HONOR);
+  *minors = 0;
+  if (!shared) {  // allocateByPartition
+    int why = 0;
+    const uint32_t pm = gpu_partition(s, ex0, p, want, g, select, &why);
+    if (pm) {
+      *minors = pm;
+      return 0;
+    }
+    if (honor) {
+      *reason = why;
+      return why == KE_REASON_DS_INSUFFICIENT_PARTITIONED ? KE_CODE_UNSCHEDULABLE : KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    }
+  }
+  const bool required = pod_scope(p.flags) != KE_SCOPE_NONE;  // generalAllocate -> allocateByDeviceTopology
+  if (!(ex0 & DSX_TOPO) || (shared && want > 1)) {
+    if (required) {
+      *reason = (ex0 & DSX_TOPO) ? KE_REASON_DS_MULTI_SHARED_GPU : KE_REASON_DS_MISSING_TOPOLOGY_TREE;
+      return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    }
+  } else {
+    const bool ok = select ? (*minors = gpu_topology(s, i, p, want, g, dscore)) != 0
+                           : gpu_topology_feasible(s, i, p, want, g);
+    if (ok) return 0;
+    *reason = required ? KE_REASON_DS_INSUFFICIENT_TOPOLOGY_SCOPED : KE_REASON_DS_INSUFFICIENT_GPU_TOPOLOGY;
+    return KE_CODE_UNSCHEDULABLE;
+  }
+  if (__builtin_popcount(g.dflt) >= want) return 0;  // defaultAllocateDevices (minors picked by the caller)
+  *reason = KE_REASON_DS_INSUFFICIENT_GPU;
+  return KE_CODE_UNSCHEDULABLE;
+}
+
+// Filter (Prepare + per-type allocation feasibility) and raw Score of DeviceShare for a pod with PF_DS on
+// a node with a cache entry.  Types in the fixed order GPU, RDMA, FPGA.
 __device__ __noinline__ void ds_filter_score(const SoA& s, int64_t i, const DevPod& p, const KArgs& k, EvalOut& o) {
   uint64_t msk[4];
 #pragma unroll
@@ -337,23 +564,39 @@ __device__ __noinline__ void ds_filter_score(const SoA& s, int64_t i, const DevP
   for (int t = 0; t < 3; t++) {
     if (!p.ds_cnt[t]) continue;
     uint64_t ex = (msk[DSM_EXISTS] >> (16 * t)) & 0xFFFF;
-    int n_ok = 0;
+    GpuMasks g;
+    g.minors = (uint32_t)ex;
+    g.total = g.used = g.sat = g.dflt = 0;
+    bool present = false;
     int64_t tot[3] = {0, 0, 0}, fre[3] = {0, 0, 0};
     while (ex) {
       const int m = __builtin_ctzll(ex);
       ex &= ex - 1;
       DsInst d;
       ds_instance(s, i, t, m, msk, d);
-      n_ok += ds_satisfied(d, p, t);
+      const bool leq = ds_leq(d, p, t), fz = ds_free_zero(d);
+      present = present || !fz;
+      g.dflt |= (uint32_t)(!fz && leq) << m;
+      g.sat |= (uint32_t)(leq && ds_total_nz(d)) << m;
+      g.total |= (uint32_t)ds_total_nz(d) << m;
+      g.used |= (uint32_t)d.used_nz << m;
 #pragma unroll
       for (int key = 0; key < 3; key++) {
         tot[key] += ((d.th >> key) & 1) ? d.tv[key] : 0;
         fre[key] += ((d.fh >> key) & 1) ? d.fv[key] : 0;
       }
     }
-    if (n_ok < p.ds_cnt[t]) {  // defaultAllocateDevices: "Insufficient <type> devices"
-      o.status = KE_CODE_UNSCHEDULABLE;
-      o.reason = (uint8_t)(KE_REASON_DS_INSUFFICIENT_GPU + t);
+    if (!present) g.total = g.sat = 0;  // the filtered nodeDevice dropped the type
+    int st = 0, reason = KE_REASON_DS_INSUFFICIENT_GPU + t;
+    if (t == KE_DEV_GPU) {
+      uint32_t unused;
+      st = gpu_allocate(s, i, msk[DSM_EXISTS], p, g, false, nullptr, &unused, &reason);
+    } else if (__builtin_popcount(g.dflt) < p.ds_cnt[t]) {  // defaultAllocateDevices: "Insufficient <type> devices"
+      st = KE_CODE_UNSCHEDULABLE;
+    }
+    if (st) {
+      o.status = (uint8_t)st;
+      o.reason = (uint8_t)reason;
       return;
     }
     raw += ds_weighted(k, t, tot, fre, p);  // resourceAllocationScorer.scoreNode
@@ -361,9 +604,10 @@ __device__ __noinline__ void ds_filter_score(const SoA& s, int64_t i, const DevP
   o.ds = (int16_t)raw;
 }
 
-// DeviceShare Reserve (plugin.go:426-492): per type, the instances in (scoreDevice desc, minor asc)
-// order (device_resources.go:171-208), the first ds_cnt that are satisfiable; the allocation
-// (request + fillGPUTotalMem, devicehandler_gpu.go:98-133) is added to `used` in the SoA
+// DeviceShare Reserve (plugin.go:426-492): per type the allocator's minors -- GPUs through GPUAllocator
+// (partition, topology scope, then default), other types defaultAllocateDevices: instances in
+// (scoreDevice desc, minor asc) order (device_resources.go:171-208), the first ds_cnt satisfiable.  The
+// allocation (request + fillGPUTotalMem, devicehandler_gpu.go:98-133) is added to `used` in the SoA
 // (updateCacheUsed).  Returns the minors mask (bit 16*type + minor).
 __device__ __noinline__ uint64_t ds_reserve(const SoA& s, int64_t i, const DevPod& p, const KArgs& k) {
   uint64_t msk[4], out = 0;
@@ -373,29 +617,52 @@ __device__ __noinline__ uint64_t ds_reserve(const SoA& s, int64_t i, const DevPo
     if (!p.ds_cnt[t]) continue;
     const int nk = DS_NK[t];
     int64_t score[DS_MINORS];
-    uint32_t ok = 0;
+    GpuMasks g;
+    g.minors = g.total = g.used = g.sat = g.dflt = 0;
+    bool present = false;
     uint64_t ex = (msk[DSM_EXISTS] >> (16 * t)) & 0xFFFF;
+    g.minors = (uint32_t)ex;
     while (ex) {
       const int m = __builtin_ctzll(ex);
       ex &= ex - 1;
       DsInst d;
       ds_instance(s, i, t, m, msk, d);
-      if (ds_satisfied(d, p, t)) ok |= 1u << m;
+      const bool leq = ds_leq(d, p, t), fz = ds_free_zero(d);
+      present = present || !fz;
+      g.dflt |= (uint32_t)(!fz && leq) << m;
+      g.sat |= (uint32_t)(leq && ds_total_nz(d)) << m;
+      g.total |= (uint32_t)ds_total_nz(d) << m;
+      g.used |= (uint32_t)d.used_nz << m;
       int64_t tot[3], fre[3];
 #pragma unroll
       for (int key = 0; key < 3; key++) {
         tot[key] = ((d.th >> key) & 1) ? d.tv[key] : 0;
         fre[key] = ((d.fh >> key) & 1) ? d.fv[key] : 0;
       }
-      score[m] = ds_weighted(k, t, tot, fre, p);  // scoreDevice
+      score[m] = ds_weighted(k, t, tot, fre, p);  // scoreDevice (total = the cache total of the minor)
     }
-    for (int c = 0; c < p.ds_cnt[t] && ok; c++) {
-      int best = -1;
-      for (uint32_t r = ok; r; r &= r - 1) {
-        const int m = __builtin_ctz(r);
-        if (best < 0 || score[m] > score[best]) best = m;  // ascending minors: ties keep the lower
+    if (!present) g.total = g.sat = 0;
+    uint32_t take = 0;
+    bool by_default = true;
+    if (t == KE_DEV_GPU) {
+      int reason = 0;
+      if (gpu_allocate(s, i, msk[DSM_EXISTS], p, g, true, score, &take, &reason) != 0) take = 0;
+      by_default = take == 0;  // passed Filter: only the default stage leaves the minors to pick here
+    }
+    if (by_default) {
+      uint32_t ok = g.dflt;
+      for (int c = 0; c < p.ds_cnt[t] && ok; c++) {
+        int best = -1;
+        for (uint32_t r = ok; r; r &= r - 1) {
+          const int m = __builtin_ctz(r);
+          if (best < 0 || score[m] > score[best]) best = m;  // ascending minors: ties keep the lower
+        }
+        ok &= ~(1u << best);
+        take |= 1u << best;
       }
-      ok &= ~(1u << best);
+    }
+    for (uint32_t rest = take; rest; rest &= rest - 1) {
+      const int best = __builtin_ctz(rest);
       out |= 1ull << (16 * t + best);
       int64_t alloc[3] = {0, 0, 0};
       bool has[3] = {false, false, false};
@@ -3102,6 +3369,7 @@ struct DeviceState {
   uint32_t* d_gath = nullptr;  // [world][GATH_WORDS]
   // DeviceShare
   bool ds_alloc = false;         // soa.ds / soa.dsm allocated
+  size_t pt_words = 0;           // soa.pt capacity (uint64 words)
   uint16_t* d_dsraw = nullptr;   // [capacity] raw DeviceShare score + 1 of the batch's DeviceShare pod
   uint32_t* d_dsmax = nullptr;   // 1 + max raw score over the feasible nodes of the batch's pod
   uint64_t* d_devalloc = nullptr;  // [n_pods] device minors allocated per pod
@@ -3216,7 +3484,7 @@ void device_destroy(Context* ctx) {
                   d->d_dsraw,   d->d_dsmax,  d->d_devalloc,   d->d_dsrows,       d->soa.nf,   d->soa.nm,
                   d->d_numaalloc, d->d_numarows, d->d_defer, d->d_defer_cnt, d->soa.cs, d->soa.cpu,
                   d->d_cpurows, d->d_cpusets, d->d_aff, d->soa.qt, d->soa.qm, d->d_sched, d->d_stale,
-                  d->d_stale_cnt, d->d_trows, d->d_tcnt, d->d_chg, d->soa.rec};
+                  d->d_stale_cnt, d->d_trows, d->d_tcnt, d->d_chg, d->soa.rec, d->soa.pt};
   if (d->estream) (void)hipStreamSynchronize(d->estream);
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -3412,6 +3680,18 @@ int device_refresh(Context* ctx, int64_t now) {
   if (rc) return rc;
   rc = ensure_cpu(ctx);
   if (rc) return rc;
+  if (ctx->ptab_dirty) {  // GPU partition tables (ke_node_gpu_partitions); the pool only grows
+    if (d->pt_words < ctx->ptab.size()) {
+      if (d->soa.pt) HIP_OK(hipFree(d->soa.pt));
+      const size_t cap = std::max(ctx->ptab.size(), (size_t)16 * PT_WORDS);
+      HIP_OK(hipMalloc(&d->soa.pt, sizeof(uint64_t) * cap));
+      d->pt_words = cap;
+    }
+    HIP_OK(hipMemcpyAsync(d->soa.pt, ctx->ptab.data(), sizeof(uint64_t) * ctx->ptab.size(), hipMemcpyHostToDevice,
+                          d->stream));
+    HIP_OK(hipStreamSynchronize(d->stream));
+    ctx->ptab_dirty = false;
+  }
   std::vector<int64_t> crows;  // CPU tables + summaries of the dirty nodes
   std::vector<int32_t> cidx;
   std::vector<Row> rows;

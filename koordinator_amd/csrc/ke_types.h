@@ -101,6 +101,11 @@ enum PodFlag : uint32_t {
   PF_CPU_EXCL0 = 1u << 19,     // 2 bits: state.preferredCPUExclusivePolicy (KE_CPU_EXCL_*)
   PF_CPUSET = 1u << 21,        // the pod may bind CPUs on some node: singleton batch, cpuset Reserve
   PF_QUOTA_NP = 1u << 22,      // ElasticQuota: IsPodNonPreemptible (checked against Min, counted in non-preemptible used)
+  PF_GPU_SHARED = 1u << 23,    // GPURequirements.gpuShared (devicehandler_gpu.go:84-93)
+  PF_GPU_SCOPE0 = 1u << 24,    // 3 bits: requiredTopologyScope (KE_SCOPE_*)
+  PF_GPU_PART_SPEC = 1u << 27, // GPUPartitionSpec present: honorGPUPartition
+  PF_GPU_PART_RESTRICTED = 1u << 28,  // GPUPartitionSpec.AllocatePolicy Restricted
+  PF_GPU_RING_BW = 1u << 29,   // GPUPartitionSpec.RingBusBandwidth set (DevPod::ring_bw)
 };
 KE_HD inline int pf_cpu_required(uint32_t f) { return (int)((f >> 15) & 3u); }
 KE_HD inline int pf_cpu_preferred(uint32_t f) { return (int)((f >> 17) & 3u); }
@@ -188,8 +193,11 @@ struct DevPod {
   uint8_t ds_cnt[3];  // DeviceShare: desired device count per type (GPU, RDMA, FPGA), 0 = not requested
   uint8_t quota;      // ElasticQuota: 0 = none, else 1 + quota index (ke_pod.quota)
   int64_t ds_req[5];  // DeviceShare per-instance request: gpu-core, gpu-memory, gpu-memory-ratio, rdma, fpga
+  int64_t ring_bw;    // GPUPartitionSpec.RingBusBandwidth (PF_GPU_RING_BW)
 };
-static_assert(sizeof(DevPod) == 80, "DevPod layout");
+static_assert(sizeof(DevPod) == 88, "DevPod layout");
+KE_HD inline int pod_scope(uint32_t flags) { return (int)((flags >> 24) & 7u); }
+KE_HD inline int scope_level(int scope) { return scope >= 1 && scope <= 4 ? scope : 0; }
 
 // ---- DeviceShare device state (a second SoA, allocated when the first node device cache appears) ----
 // int64 fields: total / used per (type, minor, key); key count 3 for GPU, 1 for RDMA/FPGA.
@@ -200,12 +208,29 @@ constexpr int DS_UBASE[3] = {48, 112, 144};
 constexpr int NUM_DS_FIELDS = 160;
 // uint64 mask words: exists (bit 16t+m) and the key presence of total / used
 enum DsMask : int {
-  DSM_EXISTS = 0,  // device instance (t, m) is in the cache
+  DSM_EXISTS = 0,  // device instance (t, m) is in the cache (bits 0-47); node GPU flags DSX_* (48-63)
   DSM_GPU_HT = 1,  // GPU total has key k: bit 16k+m (empty for unhealthy devices)
   DSM_GPU_HU = 2,  // GPU used has key k:  bit 16k+m
   DSM_RF = 3,      // RDMA total 0-15, RDMA used 16-31, FPGA total 32-47, FPGA used 48-63
-  NUM_DS_MASKS = 4
+  DSM_TOPO = 4,    // GPU topology tree: 4 bits per minor m at 4m = NUMA scope rank (scopes ascending by NodeID)
+  DSM_PCIE = 5,    // 4 bits per minor m at 4m = PCIe scope rank (DFS order: NUMA rank, then PCIEID)
+  NUM_DS_MASKS = 6
 };
+// DSM_EXISTS high bits: GPU allocator state of the node (allocator_gpu.go:72-133)
+constexpr uint64_t DSX_TOPO = 1ull << 48;   // GetGPUTopologyScope != nil
+constexpr uint64_t DSX_HONOR = 1ull << 49;  // nodeHonorGPUPartition
+constexpr uint64_t DSX_TABLE = 1ull << 50;  // gpuPartitionIndexer != nil
+constexpr int DSX_TABLE_SHIFT = 52;         // 12 bits: partition table id in the table pool
+constexpr int MAX_PTABLES = 4096;
+// One partition table in the pool: PT_SLOTS entries ordered by (number_of_gpus, allocation score group, table
+// order), then the ring bus bandwidths.  Entry: minors (bits 0-15) | number_of_gpus << 16 | group << 24 |
+// (uint32)allocation_score << 32; number_of_gpus 0 ends the table.
+constexpr int PT_SLOTS = 64;                // == KE_MAX_GPU_PARTITIONS
+constexpr int PT_WORDS = 2 * PT_SLOTS;      // entries + ring bandwidths (int64, KE_ABSENT = nil)
+KE_HD inline uint32_t pt_minors(uint64_t e) { return (uint32_t)(e & 0xFFFFu); }
+KE_HD inline int pt_gpus(uint64_t e) { return (int)((e >> 16) & 0xFFu); }
+KE_HD inline int pt_group(uint64_t e) { return (int)((e >> 24) & 0xFFu); }
+KE_HD inline int32_t pt_score(uint64_t e) { return (int32_t)(uint32_t)(e >> 32); }
 KE_HD inline int ds_ht_word(int t) { return t == 0 ? DSM_GPU_HT : DSM_RF; }
 KE_HD inline int ds_hu_word(int t) { return t == 0 ? DSM_GPU_HU : DSM_RF; }
 KE_HD inline int ds_ht_bit(int t, int m, int k) { return t == 0 ? 16 * k + m : (t == 1 ? m : 32 + m); }

@@ -121,6 +121,13 @@ class Evaluator:
     def delete_devices(self, i):
         self._check(self.lib.ke_node_devices_delete(self.h, i))
 
+    def set_gpu_partitions(self, i, has_table, honor, partitions=None):
+        """The node's GPU partition indexer + policy (model.gpu_partition_state(...))."""
+        parts = np.ascontiguousarray(partitions if partitions is not None else np.zeros(0, abi.GPU_PARTITION_DTYPE),
+                                     dtype=abi.GPU_PARTITION_DTYPE)
+        self._check(self.lib.ke_node_gpu_partitions(self.h, i, int(bool(has_table)), int(bool(honor)), len(parts),
+                                                    abi.ptr(parts)))
+
     def set_numa(self, i, zones):
         """NodeResourceTopology NUMA zones + their allocation (model.make_zones(...))."""
         zones = np.ascontiguousarray(zones, dtype=abi.NUMA_ZONE_DTYPE)

@@ -199,7 +199,8 @@ def make_pod(name="pod", namespace="default", requests=None, limits=None, contai
              scheduled_at=None, initialized_at=None, custom_factors=None,
              custom_seconds_after_scheduled=None, custom_seconds_after_initialized=None,
              terminated=False, numa_policy=None, numa_exclusive=None, cpu_bind_required=None,
-             cpu_bind_preferred=None, cpu_exclusive=None):
+             cpu_bind_preferred=None, cpu_exclusive=None, gpu_partition_spec=None, device_hints=None,
+             device_joint_allocate=None):
     """A pod as the plugins see it.  `requests`/`limits` describe one container (MakePod().Req());
     `containers` gives the full list.  Times are ns.  numa_policy / numa_exclusive: the
     scheduling.koordinator.sh/numa-topology-spec annotation ('BestEffort' | 'Restricted' |
@@ -248,7 +249,78 @@ def make_pod(name="pod", namespace="default", requests=None, limits=None, contai
     p.cpu_bind_required = CPU_BIND_BY_NAME[cpu_bind_required]
     p.cpu_bind_preferred = CPU_BIND_BY_NAME[cpu_bind_preferred]
     p.cpu_exclusive = CPU_EXCL_BY_NAME[cpu_exclusive]
+    _device_annotations(p, gpu_partition_spec, device_hints, device_joint_allocate)
     return p
+
+
+def _device_annotations(p, spec, hints, joint):
+    """DeviceShare annotations (apis/extension/device_share.go) as utils.go:355-513 parses them:
+    spec = GPUPartitionSpec {'allocatePolicy': 'BestEffort'|'Restricted', 'ringBusBandwidth': quantity};
+    hints = DeviceAllocateHints {type: {'selector', 'vfSelector', 'allocateStrategy', 'requiredTopologyScope',
+    'exclusivePolicy'}}; joint = DeviceJointAllocate {'deviceTypes': [...], 'requiredScope': ...}."""
+    p.gpu_ring_bus_bandwidth = abi.ABSENT
+    if spec is not None:
+        p.gpu_partition_spec = 1
+        p.gpu_partition_restricted = 1 if spec.get("allocatePolicy") == "Restricted" else 0
+        if spec.get("ringBusBandwidth") is not None:
+            p.gpu_ring_bus_bandwidth = value(spec["ringBusBandwidth"])
+    bits = 0
+    for t, h in (hints or {}).items():
+        if h is None:
+            continue
+        if h.get("selector") is not None:
+            bits |= abi.DHINT_SELECTOR
+        if h.get("vfSelector") is not None:
+            bits |= abi.DHINT_VF
+        if h.get("allocateStrategy"):
+            bits |= abi.DHINT_STRATEGY
+        if h.get("exclusivePolicy"):
+            bits |= abi.DHINT_EXCLUSIVE
+        if t == "gpu" and h.get("requiredTopologyScope"):
+            p.gpu_required_topology_scope = abi.SCOPES.get(h["requiredTopologyScope"], abi.SCOPE_UNKNOWN)
+    p.device_hints = bits
+    if joint:  # parsePodDeviceShareExtensions: keep the requested types without an ApplyForAll hint
+        req = {"gpu": any(p.device_requests[i] for i in range(7)), "rdma": p.device_requests[abi.PDR["koordinator.sh/rdma"]] > 0,
+               "fpga": p.device_requests[abi.PDR["koordinator.sh/fpga"]] > 0}
+        kept = [t for t in joint.get("deviceTypes", [])
+                if req.get(t) and ((hints or {}).get(t) or {}).get("allocateStrategy") != "ApplyForAll"]
+        p.device_joint_allocate = 1 if kept else 0
+
+
+# GPUPartitionIndexOfNVIDIAHopper (allocator_gpu_helper.go:28-144): {number of GPUs: [minors, ...]}, score 1
+HOPPER_PARTITIONS = {1: [[m] for m in range(8)], 2: [[0, 1], [2, 3], [4, 5], [6, 7]],
+                     4: [[0, 1, 2, 3], [4, 5, 6, 7]], 8: [list(range(8))]}
+
+
+def make_gpu_partitions(table):
+    """GPUPartitionTable {number_of_gpus: [{'minors': [...], 'allocationScore': s, 'ringBusBandwidth': q}
+    or [minors...]]} -> np.ndarray(GPU_PARTITION_DTYPE) in table order (allocationScore defaults to 0, as
+    an omitted JSON field; the designated Hopper table gives 1)."""
+    rows = []
+    for n, parts in table.items():
+        for q in parts:
+            if not isinstance(q, dict):
+                q = {"minors": q}
+            rows.append((sum(1 << m for m in q["minors"]), int(n), int(q.get("allocationScore", 0)), 0,
+                         abi.ABSENT if q.get("ringBusBandwidth") is None else value(q["ringBusBandwidth"])))
+    return np.array(rows, dtype=abi.GPU_PARTITION_DTYPE)
+
+
+def gpu_partition_state(device_table=None, device_labels=None, node_labels=None):
+    """(has_table, honor, partitions) as GPUAllocator.Allocate resolves them (allocator_gpu.go:77-82):
+    the Device's table (annotation scheduling.koordinator.sh/gpu-partitions) with the Device's
+    partition-policy label, else the designated table of the node's GPU vendor/model labels with the
+    node's label (GetDesignatedGPUPartitionIndexer, allocator_gpu_helper.go:146-162)."""
+    policy_key, vendor_key, model_key = ("node.koordinator.sh/gpu-partition-policy", "node.koordinator.sh/gpu-vendor",
+                                         "node.koordinator.sh/gpu-model")
+    if device_table is not None:
+        return True, (device_labels or {}).get(policy_key) == "Honor", make_gpu_partitions(device_table)
+    labels = node_labels or {}
+    honor = labels.get(policy_key) == "Honor"
+    if labels.get(vendor_key, "") in ("", "nvidia") and labels.get(model_key) in ("H100", "H800", "H20"):
+        table = {n: [{"minors": m, "allocationScore": 1} for m in ms] for n, ms in HOPPER_PARTITIONS.items()}
+        return True, honor, make_gpu_partitions(table)
+    return False, honor, None
 
 
 CPU_BIND_BY_NAME = {None: 0, "": 0, "Default": 1, "FullPCPUs": 2, "SpreadByPCPUs": 3, "ConstrainedBurst": 4}
@@ -353,14 +425,22 @@ DEVICE_KEYS = {
 
 def make_devices(devices):
     """DeviceShare node device cache entries: [dict(type='gpu'|'rdma'|'fpga', minor, health=True,
-    total={resource: quantity}, used={resource: quantity})] -> np.ndarray(DEVICE_DTYPE)."""
+    total={resource: quantity}, used={resource: quantity}, topology={'nodeID': n, 'pcieID': str} | None)]
+    -> np.ndarray(DEVICE_DTYPE)."""
     arr = np.zeros(len(devices), dtype=abi.DEVICE_DTYPE)
+    pcie_ids = sorted({str(d["topology"].get("pcieID", "")) for d in devices if d.get("topology") is not None},
+                      key=lambda x: x.encode())
     for i, d in enumerate(devices):
         t = DEVICE_TYPE_BY_NAME[d["type"]]
         dev = abi.Device()
         dev.type = t
         dev.minor = int(d["minor"])
         dev.health = 1 if d.get("health", True) else 0
+        topo = d.get("topology")
+        if topo is not None:  # DeviceInfo.Topology: NodeID + the PCIEID's rank in Go string order
+            dev.has_topology = 1
+            dev.numa_node = int(topo.get("nodeID", 0))
+            dev.pcie_rank = pcie_ids.index(str(topo.get("pcieID", "")))
         for field, hfield, rl in (("total", "has_total", d.get("total")), ("used", "has_used", d.get("used"))):
             for k, q in (rl or {}).items():
                 key = DEVICE_KEYS[t][k]

@@ -183,6 +183,7 @@ def make_pods(n_pods, seed, key_base=1_000_000_000):
     pods["is_daemonset"] = ds.astype(np.uint8)
     pods["custom_scaling_factors"][:] = abi.ABSENT
     pods["custom_seconds_after_scheduled"] = abi.ABSENT
+    pods["gpu_ring_bus_bandwidth"] = abi.ABSENT
     pods["custom_seconds_after_initialized"] = abi.ABSENT
     return pods
 
@@ -254,6 +255,106 @@ def load_devices(handle, devices):
     for i, d in enumerate(devices):
         if d is not None:
             handle.set_devices(i, d)
+
+
+def add_gpu_topology(devices, seed, nil_fraction=0.05):
+    """Give the GPUs of each device cache entry a DeviceInfo.Topology (in place): NUMA nodes of 2-4 GPUs
+    (NodeID possibly non-contiguous), PCIe switches of 1-2 GPUs, PCIEID strings whose Go order differs from
+    their numeric order ("10" < "9").  A `nil_fraction` of the entries leave one GPU without topology
+    (GetGPUTopologyScope -> nil).  RDMA NICs get topologies too (unused by the GPU tree)."""
+    rng = np.random.default_rng(seed)
+    for devs in devices:
+        if devs is None:
+            continue
+        g = np.nonzero(devs["type"] == abi.DEV_GPU)[0]
+        per_numa = int(rng.choice([2, 4, 4, 8]))
+        per_pcie = int(rng.choice([1, 2, 2]))
+        numa_ids = rng.permutation(4)[: (len(g) + per_numa - 1) // per_numa] if len(g) else []
+        names = []
+        for j, i in enumerate(g):
+            m = int(devs[i]["minor"])
+            devs[i]["has_topology"] = 1
+            devs[i]["numa_node"] = int(numa_ids[j // per_numa])
+            names.append((i, str(7 + m // per_pcie)))  # "7", "8", "9", "10", ...
+        for i in np.nonzero(devs["type"] != abi.DEV_GPU)[0]:
+            devs[i]["has_topology"] = 1
+            devs[i]["numa_node"] = int(numa_ids[0]) if len(numa_ids) else 0
+            names.append((i, str(7 + int(devs[i]["minor"]))))
+        order = sorted({n for _, n in names}, key=lambda x: x.encode())
+        for i, n in names:
+            devs[i]["pcie_rank"] = order.index(n)
+        if len(g) and rng.random() < nil_fraction:
+            devs[g[rng.integers(len(g))]]["has_topology"] = 0
+    return devices
+
+
+def make_partition_states(n_nodes, seed, gpus=8):
+    """Per node (has_table, honor, partitions) for ke_node_gpu_partitions: the designated Hopper table
+    (40 %), a custom table with two allocation-score groups and ring bus bandwidths (15 %), an empty table
+    (5 %), or none; Honor on half of the nodes."""
+    from . import model
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n_nodes):
+        u, honor = rng.random(), bool(rng.random() < 0.5)
+        if u < 0.40:
+            out.append((True, honor, model.gpu_partition_state(
+                node_labels={"node.koordinator.sh/gpu-model": "H800"})[2]))
+        elif u < 0.55:
+            table = {}
+            for n in (1, 2, 4):
+                parts = []
+                for start in range(0, gpus - n + 1, n):
+                    parts.append({"minors": list(range(start, start + n)), "allocationScore": int(rng.choice([1, 2])),
+                                  "ringBusBandwidth": None if rng.random() < 0.2 else int(rng.choice([100, 200, 400]))})
+                table[n] = parts
+            table[3] = [{"minors": [0, 1, 2], "allocationScore": 1}, {"minors": [4, 5, 6], "allocationScore": 1}]
+            out.append((True, honor, model.make_gpu_partitions(table)))
+        elif u < 0.60:
+            out.append((True, honor, None))
+        else:
+            out.append((False, honor, None))
+    return out
+
+
+def load_partition_states(handle, states):
+    for i, (has, honor, parts) in enumerate(states):
+        if has or honor:
+            handle.set_gpu_partitions(i, has, honor, parts)
+
+
+def make_gpu_alloc_pods(n_pods, seed, key_base=5_000_000_000):
+    """Pods exercising GPUAllocator.Allocate: whole GPUs (1, 2, 3, 4, 8), shared slices (gpu.shared 1 or 2),
+    GPU hints with a required topology scope, GPUPartitionSpec (Restricted, ring bus bandwidth)."""
+    rng = np.random.default_rng(seed)
+    pods = make_pods(n_pods, seed + 1, key_base=key_base)
+    for i in range(n_pods):
+        r = pods["device_requests"][i]
+        k = rng.random()
+        if k < 0.55:
+            r[abi.PDR["nvidia.com/gpu"]] = rng.choice([1, 1, 2, 2, 3, 4, 8])
+        elif k < 0.8:
+            r[abi.PDR["koordinator.sh/gpu.shared"]] = 1
+            r[abi.PDR["koordinator.sh/gpu-core"]] = rng.choice([25, 50])
+            r[abi.PDR["koordinator.sh/gpu-memory-ratio"]] = rng.choice([25, 50])
+        elif k < 0.9:
+            sh = int(rng.choice([1, 2]))
+            r[abi.PDR["koordinator.sh/gpu.shared"]] = sh
+            r[abi.PDR["koordinator.sh/gpu-memory-ratio"]] = 50 * sh
+        else:
+            r[abi.PDR["koordinator.sh/gpu-core"]] = 200
+            r[abi.PDR["koordinator.sh/gpu-memory-ratio"]] = 200
+        pods["has_other_requests"][i] = 1
+        pods["gpu_ring_bus_bandwidth"][i] = abi.ABSENT
+        if rng.random() < 0.3:
+            pods["gpu_required_topology_scope"][i] = rng.choice([abi.SCOPE_NODE, abi.SCOPE_NUMA, abi.SCOPE_PCIE,
+                                                                 abi.SCOPE_PCIE, abi.SCOPE_DEVICE, abi.SCOPE_UNKNOWN])
+        if rng.random() < 0.25:
+            pods["gpu_partition_spec"][i] = 1
+            pods["gpu_partition_restricted"][i] = int(rng.random() < 0.4)
+            if rng.random() < 0.5:
+                pods["gpu_ring_bus_bandwidth"][i] = rng.choice([50, 200, 300])
+    return pods
 
 
 def make_ds_pods(n_pods, seed, device_fraction=0.5, key_base=2_000_000_000):

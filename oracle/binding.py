@@ -50,6 +50,7 @@ def load():
         "or_schedule": (C.c_int, [V, i32, V, i64, V, V, V, V, V, C.c_int]),
         "or_node_devices_set": (C.c_int, [V, i32, i32, V]),
         "or_node_devices_delete": (C.c_int, [V, i32]),
+        "or_node_gpu_partitions": (C.c_int, [V, i32, i32, i32, i32, V]),
         "or_ds_prefilter": (C.c_int, [C.POINTER(abi.Pod), C.POINTER(C.c_int), V, V, V]),
         "or_ds_score_device": (i64, [V, i32, V, V, V, V, V, V]),
         "or_normalize_scores": (None, [V, i32]),
@@ -149,6 +150,12 @@ class Oracle:
     def set_devices(self, i, devices):
         devices = np.ascontiguousarray(devices, dtype=abi.DEVICE_DTYPE)
         assert self.lib.or_node_devices_set(self.h, i, len(devices), abi.ptr(devices)) == 0
+
+    def set_gpu_partitions(self, i, has_table, honor, partitions=None):
+        parts = np.ascontiguousarray(partitions if partitions is not None else np.zeros(0, abi.GPU_PARTITION_DTYPE),
+                                     dtype=abi.GPU_PARTITION_DTYPE)
+        assert self.lib.or_node_gpu_partitions(self.h, i, int(bool(has_table)), int(bool(honor)), len(parts),
+                                               abi.ptr(parts)) == 0
 
     def set_numa(self, i, zones):
         zones = np.ascontiguousarray(zones, dtype=abi.NUMA_ZONE_DTYPE)

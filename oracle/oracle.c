@@ -56,6 +56,10 @@ typedef struct or_node {
   int has_dev_cache; /* nodeDeviceCache.getNodeDevice != nil */
   int32_t n_dev;
   ke_device dev[KE_DEV_TYPES * KE_MAX_MINORS];
+  /* GPU partition indexer + policy as GPUAllocator.Allocate resolves them (allocator_gpu.go:77-82) */
+  int gpu_has_table, gpu_honor;
+  int32_t n_part;
+  ke_gpu_partition part[KE_MAX_GPU_PARTITIONS];
   struct or_cpus* cpus; /* CPU topology + allocated CPUs (NULL: no CPU topology) */
 } or_node;
 
@@ -1476,7 +1480,7 @@ int64_t or_numa_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
 
 
 /* ---------------------------------------------------------------------------------------------- */
-/* DeviceShare (no reservations / preemption / NUMA affinity / hints / GPU topology tree)          */
+/* DeviceShare (no reservations / preemption / NUMA affinity / hints / joint allocation / templates)  */
 /* ---------------------------------------------------------------------------------------------- */
 
 /* A corev1.ResourceList restricted to one device type's keys (GPU: core, memory, memory-ratio;
@@ -1536,6 +1540,13 @@ typedef struct ds_pod {
   int has[KE_DEV_TYPES];
   int count[KE_DEV_TYPES];
   rl req[KE_DEV_TYPES];
+  /* GPURequirements (utils.go:487-513) */
+  int gpu_shared;       /* calcDesiredRequestsAndCountForGPU isShared */
+  int scope;            /* requiredTopologyScope: KE_SCOPE_* */
+  int scope_level;      /* DeviceTopologyScopeLevel[requiredTopologyScope] (0 for "" / unknown) */
+  int part_spec;        /* honorGPUPartition from the pod's GPUPartitionSpec */
+  int part_restricted;  /* restrictedGPUPartition */
+  int64_t ring_bw;      /* rindBusBandwidth, KE_ABSENT = nil */
 } ds_pod;
 
 static int valid_percentage(int64_t q) { return !(q > 100 && q % 100 != 0); } /* utils.go:222-227 */
@@ -1595,6 +1606,7 @@ static void ds_prepare_pod(const ke_pod* pod, ds_pod* d) {
     if (h_core) { r.has[KE_DKEY_GPU_CORE] = 1; r.v[KE_DKEY_GPU_CORE] = c_core / n; }
     if (h_ratio) { r.has[KE_DKEY_GPU_MEMORY_RATIO] = 1; r.v[KE_DKEY_GPU_MEMORY_RATIO] = c_ratio / n; }
     else if (h_mem) { r.has[KE_DKEY_GPU_MEMORY] = 1; r.v[KE_DKEY_GPU_MEMORY] = c_mem / n; }
+    d->gpu_shared = h_ratio ? (c_ratio / n < 100) : h_mem; /* isShared (devicehandler_gpu.go:84-93) */
     d->has[KE_DEV_GPU] = 1;
     d->count[KE_DEV_GPU] = (int)n;
     d->req[KE_DEV_GPU] = r;
@@ -1620,6 +1632,12 @@ static void ds_prepare_pod(const ke_pod* pod, ds_pod* d) {
     d->req[t].v[0] = per;
   }
   d->skip = !(d->has[0] || d->has[1] || d->has[2]);
+  /* parseGPURequirements (utils.go:487-513): the pod's GPUPartitionSpec and GPU hint */
+  d->scope = pod->gpu_required_topology_scope;
+  d->scope_level = d->scope >= KE_SCOPE_NODE && d->scope <= KE_SCOPE_DEVICE ? d->scope : 0;
+  d->part_spec = pod->gpu_partition_spec != 0;
+  d->part_restricted = d->part_spec && pod->gpu_partition_restricted;
+  d->ring_bw = d->part_spec ? pod->gpu_ring_bus_bandwidth : KE_ABSENT;
 }
 
 /* one device type of a node's cache: minors in ascending order */
@@ -1791,6 +1809,316 @@ static int ds_allocate(const ke_deviceshare_args* scorer, int t, const rl* req, 
   return n;
 }
 
+/* ---- GPUAllocator (allocator_gpu.go) --------------------------------------------------------- */
+static int popcount16(uint32_t x) { return __builtin_popcount(x & 0xFFFFu); }
+
+/* AllocateContext (allocator_gpu.go:52-57,83-89) over the filtered view of the node's GPUs */
+typedef struct gpu_ctx {
+  uint32_t used;   /* deviceUsedMinorsHash = hashDevices(getRealUsed(...)) (:59-70, :239-254) */
+  uint32_t total;  /* minors of removeZeroDevice(deviceTotal) (:114-122) */
+  int present;     /* the filtered nodeDevice kept the GPU type: deviceFree[GPU] exists */
+  rl free[KE_MAX_MINORS];
+  rl crd_total[KE_MAX_MINORS]; /* GPUTopologyScope.minorsResources: the cache total of each GPU */
+  uint32_t minors; /* every GPU device of the node (DeviceInfos) */
+} gpu_ctx;
+
+static void gpu_ctx_init(const or_node* nd, const ds_view* v, gpu_ctx* g) {
+  memset(g, 0, sizeof *g);
+  g->present = v->present;
+  for (int i = 0; i < nd->n_dev; i++) {
+    const ke_device* dv = &nd->dev[i];
+    if (dv->type != KE_DEV_GPU) continue;
+    g->minors |= 1u << dv->minor;
+    g->crd_total[dv->minor] = dev_total(dv, 3);
+    /* original used minors not in the refined total: all of them when the GPU type was dropped */
+    if (!v->present && (dv->has_used[0] || dv->has_used[1] || dv->has_used[2])) g->used |= 1u << dv->minor;
+  }
+  if (!v->present) return;
+  for (int i = 0; i < v->n; i++) {
+    const int m = v->minor[i];
+    g->free[m] = v->free[i];
+    if (!rl_is_zero(v->total[i], 3)) g->total |= 1u << m;
+    /* refined used: total - free' non-zero (nodeDevice.filter keeps used' only when non-zero) */
+    if (!rl_is_zero(rl_sub_nonneg(v->total[i], v->free[i], 3), 3)) g->used |= 1u << m;
+  }
+}
+
+/* selectPartitionByBinPack (allocator_gpu.go:261-296): for each feasible partition, Σ over the 8/4/2-GPU
+ * partitions of the lowest allocation-score group that stay free after it, weight 10000/100/1 x their
+ * AllocationScore; sort.Slice descending (stable for <= 12 elements, enforced at the boundary). */
+static int gpu_binpack(const or_node* nd, uint32_t used, const int* feas, int nf, int want) {
+  if (nf == 1) return feas[0];
+  static const int cnts[3] = {8, 4, 2}, wts[3] = {10000, 100, 1};
+  int best = -1;
+  int64_t best_score = 0;
+  for (int f = 0; f < nf; f++) {
+    const uint32_t alloc = used | nd->part[feas[f]].minors;
+    int64_t score = 0;
+    for (int c = 0; c < 3; c++) {
+      if (cnts[c] < want) continue;
+      int lo = -1; /* indexerOfGPUNumber[0]: the lowest allocation score listed for cnts[c] */
+      for (int i = 0; i < nd->n_part; i++)
+        if (nd->part[i].number_of_gpus == cnts[c] && (lo < 0 || nd->part[i].allocation_score < nd->part[lo].allocation_score))
+          lo = i;
+      if (lo < 0) continue;
+      for (int i = 0; i < nd->n_part; i++) {
+        const ke_gpu_partition* q = &nd->part[i];
+        if (q->number_of_gpus != cnts[c] || q->allocation_score != nd->part[lo].allocation_score) continue;
+        if (q->minors & alloc) continue;
+        score += (int64_t)wts[c] * q->allocation_score;
+      }
+    }
+    if (best < 0 || score > best_score) { /* stable descending sort: first of the maxima */
+      best = feas[f];
+      best_score = score;
+    }
+  }
+  return best;
+}
+
+/* allocateByPartition (allocator_gpu.go:177-237).  Returns the status (0 also when !honor swallows a
+ * failure); *out = the chosen partition's minors, 0 = none. */
+static int gpu_by_partition(const or_node* nd, const ds_pod* d, const gpu_ctx* g, int honor, uint32_t* out,
+                            int* reason) {
+  *out = 0;
+  if (d->gpu_shared) return 0;
+  int st = 0;
+  const int want = d->count[KE_DEV_GPU];
+  if (!nd->gpu_has_table) {
+    st = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    *reason = KE_REASON_DS_MISSING_PARTITION_TABLE;
+  } else {
+    /* indexer[numberOfGPUs]: groups of equal AllocationScore, ascending (GetGPUPartitionIndexer :165-200) */
+    int scores[KE_MAX_GPU_PARTITIONS], ng = 0;
+    for (int i = 0; i < nd->n_part; i++) {
+      if (nd->part[i].number_of_gpus != want) continue;
+      const int sc = nd->part[i].allocation_score;
+      int j = 0;
+      while (j < ng && scores[j] < sc) j++;
+      if (j < ng && scores[j] == sc) continue;
+      for (int k = ng; k > j; k--) scores[k] = scores[k - 1];
+      scores[j] = sc;
+      ng++;
+    }
+    if (ng == 0) {
+      st = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+      *reason = KE_REASON_DS_UNSUPPORTED_GPU_REQUESTS;
+    } else {
+      int feas[KE_MAX_GPU_PARTITIONS], nf = 0;
+      for (int gi = 0; gi < ng; gi++) {
+        for (int i = 0; i < nd->n_part; i++) {
+          const ke_gpu_partition* q = &nd->part[i];
+          if (q->number_of_gpus != want || q->allocation_score != scores[gi]) continue;
+          if (q->minors & g->used) continue;
+          if ((g->total & q->minors) != q->minors) continue;
+          if (d->ring_bw != KE_ABSENT) {
+            if (q->ring_bus_bandwidth == KE_ABSENT) continue;
+            if (d->ring_bw > q->ring_bus_bandwidth) continue;
+          }
+          feas[nf++] = i;
+        }
+        if (nf > 0 || d->part_restricted) break;
+      }
+      if (nf == 0) {
+        st = KE_CODE_UNSCHEDULABLE;
+        *reason = KE_REASON_DS_INSUFFICIENT_PARTITIONED;
+      } else {
+        *out = nd->part[gpu_binpack(nd, g->used, feas, nf, want)].minors;
+        return 0;
+      }
+    }
+  }
+  return honor ? st : 0;
+}
+
+/* GPUTopologyScope (allocator_gpu.go:298-309) as GetGPUTopologyScope builds it (allocator_gpu_helper.go:202-263) */
+typedef struct gscope {
+  int level; /* DeviceTopologyScopeLevel: Node 1, NUMANode 2, PCIe 3 */
+  uint32_t minors;
+  int n_child;
+  int child[KE_MAX_MINORS];
+} gscope;
+
+/* Scope tree in an array: [0] = Node, then NUMANode scopes by NodeID, each followed by nothing; PCIe
+ * scopes after all NUMA scopes.  Returns the scope count, 0 = nil tree. */
+static int gpu_scope_tree(const or_node* nd, gscope* sc) {
+  int n_gpu = 0;
+  for (int i = 0; i < nd->n_dev; i++) {
+    if (nd->dev[i].type != KE_DEV_GPU) continue;
+    if (!nd->dev[i].has_topology) return 0; /* info.Topology == nil -> nil */
+    n_gpu++;
+  }
+  if (n_gpu == 0) return 0;
+  int numa_ids[KE_MAX_MINORS], nn = 0;
+  for (int i = 0; i < nd->n_dev; i++) { /* NUMA ids ascending */
+    if (nd->dev[i].type != KE_DEV_GPU) continue;
+    const int id = nd->dev[i].numa_node;
+    int j = 0;
+    while (j < nn && numa_ids[j] < id) j++;
+    if (j < nn && numa_ids[j] == id) continue;
+    for (int k = nn; k > j; k--) numa_ids[k] = numa_ids[k - 1];
+    numa_ids[j] = id;
+    nn++;
+  }
+  int ns = 1;
+  memset(&sc[0], 0, sizeof sc[0]);
+  sc[0].level = 1;
+  for (int i = 0; i < nd->n_dev; i++)
+    if (nd->dev[i].type == KE_DEV_GPU) sc[0].minors |= 1u << nd->dev[i].minor;
+  for (int a = 0; a < nn; a++) {
+    const int ni = ns++;
+    memset(&sc[ni], 0, sizeof sc[ni]);
+    sc[ni].level = 2;
+    sc[0].child[sc[0].n_child++] = ni;
+    int pcie[KE_MAX_MINORS], np = 0; /* PCIe ranks of this NUMA node, ascending */
+    for (int i = 0; i < nd->n_dev; i++) {
+      const ke_device* dv = &nd->dev[i];
+      if (dv->type != KE_DEV_GPU || dv->numa_node != numa_ids[a]) continue;
+      sc[ni].minors |= 1u << dv->minor;
+      int j = 0;
+      while (j < np && pcie[j] < dv->pcie_rank) j++;
+      if (j < np && pcie[j] == dv->pcie_rank) continue;
+      for (int k = np; k > j; k--) pcie[k] = pcie[k - 1];
+      pcie[j] = dv->pcie_rank;
+      np++;
+    }
+    for (int b = 0; b < np; b++) {
+      const int pi = ns++;
+      memset(&sc[pi], 0, sizeof sc[pi]);
+      sc[pi].level = 3;
+      sc[ni].child[sc[ni].n_child++] = pi;
+      for (int i = 0; i < nd->n_dev; i++) {
+        const ke_device* dv = &nd->dev[i];
+        if (dv->type == KE_DEV_GPU && dv->numa_node == numa_ids[a] && dv->pcie_rank == pcie[b])
+          sc[pi].minors |= 1u << dv->minor;
+      }
+    }
+  }
+  return ns;
+}
+
+typedef struct sres { /* ScopeLevelAllocateResult */
+  int ok;
+  uint32_t minors;
+  int cum, depth;
+  int64_t score;
+} sres;
+
+typedef struct dctx { /* DeviceLevelContext cache, filled on first visit */
+  int seen[KE_MAX_MINORS], sat[KE_MAX_MINORS];
+  int64_t score[KE_MAX_MINORS];
+} dctx;
+
+/* allocateFromScope (allocator_gpu.go:357-451) */
+static sres gpu_from_scope(const gscope* sc, int s, const ds_pod* d, const gpu_ctx* g,
+                           const ke_deviceshare_args* scorer, int cum, int depth, dctx* dc) {
+  sres none;
+  memset(&none, 0, sizeof none);
+  const int want = d->count[KE_DEV_GPU];
+  if (popcount16(sc[s].minors) < want) return none;
+  depth++;
+  if (sc[s].minors & g->used) cum++;
+  sres best = none;
+  for (int c = 0; c < sc[s].n_child; c++) {
+    const int ch = sc[s].child[c];
+    if (popcount16(sc[ch].minors) < want) continue;
+    const sres r = gpu_from_scope(sc, ch, d, g, scorer, cum, depth, dc);
+    if (!r.ok) continue;
+    if (!best.ok) {
+      best = r;
+      continue;
+    }
+    if (best.depth < r.depth || (best.depth == r.depth && best.cum < r.cum)) best = r;
+    if (d->gpu_shared && best.depth == r.depth && best.cum == r.cum && best.score < r.score) best = r;
+  }
+  if (best.ok) return best;
+  if (d->scope_level > sc[s].level) return none;
+  uint32_t cand = 0;
+  int n_cand = 0, satisfied = 0, best_minor = -1;
+  int64_t best_score = -1;
+  for (int m = 0; m < KE_MAX_MINORS; m++) {
+    if (!(sc[s].minors & (1u << m))) continue;
+    if (!dc->seen[m]) {
+      dc->seen[m] = 1;
+      const rl empty = rl_empty();
+      const rl* fr = g->present ? &g->free[m] : &empty; /* deviceFree[minor] (nil -> empty) */
+      dc->sat[m] = rl_leq(d->req[KE_DEV_GPU], *fr, 3) && (g->total & (1u << m));
+      dc->score[m] = 0;
+      if (dc->sat[m] && d->gpu_shared && scorer)
+        dc->score[m] = ds_score_device(scorer, KE_DEV_GPU, &d->req[KE_DEV_GPU], &g->crd_total[m], fr);
+    }
+    if (!dc->sat[m]) continue;
+    if (!d->gpu_shared) {
+      cand |= 1u << m;
+      if (++n_cand == want) {
+        satisfied = 1;
+        break;
+      }
+      continue;
+    }
+    satisfied = 1;
+    if (dc->score[m] > best_score) {
+      best_minor = m;
+      best_score = dc->score[m];
+    }
+  }
+  if (!satisfied) return none;
+  sres r;
+  r.ok = 1;
+  r.cum = cum;
+  r.depth = depth;
+  r.score = best_score;
+  r.minors = d->gpu_shared ? (1u << best_minor) : cand;
+  return r;
+}
+
+/* allocateByDeviceTopology (allocator_gpu.go:312-341) */
+static int gpu_by_topology(const or_node* nd, const ds_pod* d, const gpu_ctx* g, const ke_deviceshare_args* scorer,
+                           uint32_t* out, int* reason) {
+  *out = 0;
+  const int required = d->scope != KE_SCOPE_NONE;
+  gscope sc[1 + 2 * KE_MAX_MINORS];
+  const int ns = gpu_scope_tree(nd, sc);
+  if (ns == 0) { /* UnschedulableAndUnresolvable, swallowed when not required */
+    *reason = KE_REASON_DS_MISSING_TOPOLOGY_TREE;
+    return required ? KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE : 0;
+  }
+  if (d->gpu_shared && d->count[KE_DEV_GPU] > 1) {
+    *reason = KE_REASON_DS_MULTI_SHARED_GPU;
+    return required ? KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE : 0;
+  }
+  dctx dc;
+  memset(&dc, 0, sizeof dc);
+  const sres r = gpu_from_scope(sc, 0, d, g, scorer, 0, 0, &dc);
+  if (!r.ok) {
+    *reason = required ? KE_REASON_DS_INSUFFICIENT_TOPOLOGY_SCOPED : KE_REASON_DS_INSUFFICIENT_GPU_TOPOLOGY;
+    return KE_CODE_UNSCHEDULABLE;
+  }
+  *out = r.minors;
+  return 0;
+}
+
+/* GPUAllocator.Allocate (allocator_gpu.go:72-112; allocateByTemplate is refused at the boundary) on the
+ * filtered view.  Returns the status; *mask = the minors chosen. */
+static int ds_gpu_allocate(const or_node* nd, const ds_pod* d, const ds_view* v, const ke_deviceshare_args* scorer,
+                           uint32_t* mask, int* reason) {
+  gpu_ctx g;
+  gpu_ctx_init(nd, v, &g);
+  const int honor = d->part_spec || nd->gpu_honor;
+  int st = gpu_by_partition(nd, d, &g, honor, mask, reason);
+  if (st || *mask) return st;
+  st = gpu_by_topology(nd, d, &g, scorer, mask, reason); /* generalAllocate (:114-126) */
+  if (st || *mask) return st;
+  int picked[KE_MAX_MINORS];
+  const int n = ds_allocate(scorer, KE_DEV_GPU, &d->req[KE_DEV_GPU], d->count[KE_DEV_GPU], v, picked);
+  if (n < d->count[KE_DEV_GPU]) {
+    *reason = KE_REASON_DS_INSUFFICIENT_GPU;
+    return KE_CODE_UNSCHEDULABLE;
+  }
+  for (int i = 0; i < n; i++) *mask |= 1u << v->minor[picked[i]];
+  return 0;
+}
+
 static int ds_insufficient_reason(int t) {
   return t == KE_DEV_GPU ? KE_REASON_DS_INSUFFICIENT_GPU
                          : (t == KE_DEV_RDMA ? KE_REASON_DS_INSUFFICIENT_RDMA : KE_REASON_DS_INSUFFICIENT_FPGA);
@@ -1819,6 +2147,16 @@ int or_ds_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* reas
   for (int t = 0; t < KE_DEV_TYPES; t++) {
     if (!d.has[t]) continue;
     ds_filtered_view(nd, t, &v[t]);
+    if (t == KE_DEV_GPU) { /* Filter's allocator carries no scorer */
+      uint32_t mask;
+      int why = 0;
+      const int st = ds_gpu_allocate(nd, &d, &v[t], NULL, &mask, &why);
+      if (st) {
+        *reason = why;
+        return st;
+      }
+      continue;
+    }
     int picked[KE_MAX_MINORS];
     if (ds_allocate(NULL, t, &d.req[t], d.count[t], &v[t], picked) < d.count[t]) {
       *reason = ds_insufficient_reason(t);
@@ -1861,10 +2199,20 @@ uint64_t or_ds_reserve(or_cluster* c, const ke_pod* pod, int32_t node) {
     ds_view v;
     ds_filtered_view(nd, t, &v);
     int picked[KE_MAX_MINORS];
-    const int n = ds_allocate(&c->cfg.deviceshare, t, &d.req[t], d.count[t], &v, picked);
-    if (n < d.count[t]) return mask; /* not reached for a node that passed Filter */
+    int n = 0;
+    if (t == KE_DEV_GPU) {
+      uint32_t gm = 0;
+      int reason = 0;
+      if (ds_gpu_allocate(nd, &d, &v, &c->cfg.deviceshare, &gm, &reason)) return mask; /* passed Filter */
+      for (int m = 0; m < KE_MAX_MINORS; m++) /* fillGPUTotalMem reads each allocated minor's own total */
+        if (gm & (1u << m)) picked[n++] = m;
+    } else {
+      n = ds_allocate(&c->cfg.deviceshare, t, &d.req[t], d.count[t], &v, picked);
+      if (n < d.count[t]) return mask; /* not reached for a node that passed Filter */
+      for (int i = 0; i < n; i++) picked[i] = v.minor[picked[i]];
+    }
     for (int i = 0; i < n; i++) {
-      const int minor = v.minor[picked[i]];
+      const int minor = picked[i];
       rl alloc = d.req[t];
       ke_device* dev = NULL;
       for (int j = 0; j < nd->n_dev; j++)
@@ -2121,6 +2469,20 @@ int or_node_devices_delete(or_cluster* c, int32_t node) {
   if (node < 0 || node >= c->n) return KE_ERR_NOT_FOUND;
   c->nodes[node].has_dev_cache = 0;
   c->nodes[node].n_dev = 0;
+  c->nodes[node].gpu_has_table = c->nodes[node].gpu_honor = 0;
+  c->nodes[node].n_part = 0;
+  return KE_OK;
+}
+
+int or_node_gpu_partitions(or_cluster* c, int32_t node, int32_t has_table, int32_t honor, int32_t n,
+                           const ke_gpu_partition* parts) {
+  if (node < 0 || node >= c->n) return KE_ERR_NOT_FOUND;
+  if (n < 0 || n > KE_MAX_GPU_PARTITIONS || (n > 0 && !has_table)) return KE_ERR_INVALID;
+  or_node* nd = &c->nodes[node];
+  nd->gpu_has_table = has_table != 0;
+  nd->gpu_honor = honor != 0;
+  nd->n_part = n;
+  if (n) memcpy(nd->part, parts, sizeof(ke_gpu_partition) * (size_t)n);
   return KE_OK;
 }
 

@@ -150,6 +150,84 @@ def test_unsupported_inputs_are_rejected():
         Evaluator(bad)
 
 
+def _unsupported(fn, *args):
+    with pytest.raises(KoordEvalError) as e:
+        fn(*args)
+    assert e.value.code == abi.ERR_UNSUPPORTED, str(e.value)
+
+
+GPU2 = {"nvidia.com/gpu": "2"}
+
+
+@pytest.mark.parametrize("kind", ["joint", "vf", "selector", "strategy", "exclusive"])
+def test_unmodelled_device_annotations_are_refused(kind):
+    """annotations whose allocation path is not implemented fail loudly instead of being
+    evaluated on the default path (device_allocator.go:74-138,205-300,396-460; devicehandler_default.go:58-90)."""
+    ev = Evaluator(abi.default_config(4))
+    ev.upsert_node(0, model.make_node(allocatable={"cpu": "8", "memory": "8Gi"}))
+    req = dict(GPU2, **{"koordinator.sh/rdma": "1"})
+    pod = {
+        "joint": lambda: model.make_pod(requests=req, device_joint_allocate={"deviceTypes": ["gpu", "rdma"]}),
+        "vf": lambda: model.make_pod(requests=req, device_hints={"rdma": {"vfSelector": {"matchLabels": {"t": "a"}}}}),
+        "selector": lambda: model.make_pod(requests=GPU2, device_hints={"gpu": {"selector": {"matchLabels": {}}}}),
+        "strategy": lambda: model.make_pod(requests=req, device_hints={"rdma": {"allocateStrategy": "ApplyForAll"}}),
+        "exclusive": lambda: model.make_pod(requests=req,
+                                            device_hints={"rdma": {"exclusivePolicy": "PCIeLevel"}}),
+    }[kind]()
+    _unsupported(ev.eval, [pod], cases.NOW)
+    _unsupported(ev.schedule, [pod], cases.NOW)
+
+
+def test_joint_allocate_of_one_requested_type_is_dropped():
+    """parsePodDeviceShareExtensions keeps only requested types without an ApplyForAll hint (utils.go:428-441):
+    a joint spec naming only unrequested types carries nothing."""
+    pod = model.make_pod(requests=GPU2, device_joint_allocate={"deviceTypes": ["rdma"]})
+    assert pod.device_joint_allocate == 0
+    pod = model.make_pod(requests=GPU2, device_hints={"gpu": {"requiredTopologyScope": "PCIe"}})
+    assert pod.device_hints == 0 and pod.gpu_required_topology_scope == abi.SCOPE_PCIE
+
+
+def test_gpu_shared_templates_are_refused():
+    """allocateByTemplate (allocator_gpu.go:135-159): a shared-GPU pod naming a template-matched resource."""
+    cfg = abi.default_config(4)
+    cfg.deviceshare.template_matched_keys = abi.TEMPLATE_KEY_CORE
+    ev = Evaluator(cfg)
+    ev.upsert_node(0, model.make_node(allocatable={"cpu": "8", "memory": "8Gi"}))
+    shared = model.make_pod(requests={"koordinator.sh/gpu.shared": "1", "koordinator.sh/gpu-core": "50",
+                                      "koordinator.sh/gpu-memory-ratio": "50"})
+    _unsupported(ev.eval, [shared], cases.NOW)
+    _unsupported(ev.schedule, [shared], cases.NOW)
+    whole = model.make_pod(requests=GPU2)  # not shared: no template enforced
+    with pytest.raises(KoordEvalError) as e:
+        ev.eval([whole], cases.NOW)
+    assert e.value.code in (abi.ERR_NO_DEVICE, abi.OK)
+
+
+@pytest.mark.parametrize("which", ["loadaware", "numa", "deviceshare"])
+def test_args_with_other_resource_keys_are_refused(which):
+    """pkg/scheduler/apis/config/types.go:31-125: the args are maps; keys beyond the modelled ones fail."""
+    cfg = abi.default_config(4)
+    getattr(cfg, which).has_other_keys = 1
+    _unsupported(Evaluator, cfg)
+
+
+def test_gpu_partition_tables_validated():
+    ev = Evaluator(abi.default_config(4))
+    ev.upsert_node(0, model.make_node(allocatable={"cpu": "8", "memory": "8Gi"}))
+    has, honor, parts = model.gpu_partition_state(node_labels={"node.koordinator.sh/gpu-model": "H800"})
+    assert has and not honor and len(parts) == 15
+    ev.set_gpu_partitions(0, has, honor, parts)
+    ev.set_gpu_partitions(1, has, True, parts)  # same table: interned once
+    ev.set_gpu_partitions(2, True, False, None)  # empty table: indexer present, every count unsupported
+    big = model.make_gpu_partitions({1: [[m] for m in range(13)]})  # 13 in one group: Go's sort is unstable
+    _unsupported(ev.set_gpu_partitions, 0, True, False, big)
+    bad = model.make_gpu_partitions({1: [[16]]})
+    with pytest.raises(KoordEvalError) as e:
+        ev.set_gpu_partitions(0, True, False, bad)
+    assert e.value.code == abi.ERR_INVALID
+    assert model.gpu_partition_state(node_labels={"node.koordinator.sh/gpu-model": "A100"})[0] is False
+
+
 def test_host_rows_fold_loadaware_terms():
     """The row the host derives for a golden case reproduces the Go score arithmetic."""
     case = [c for c in cases.load("loadaware_score.json") if c["name"] == "score load node"][0]

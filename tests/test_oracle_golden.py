@@ -296,3 +296,36 @@ def test_numa_cpuset(case, exact):
     want = [(sum(1 << b for b in h["bits"]), h["preferred"]) for h in case["want"]["cpu"]]
     assert [(m, p) for m, p, _ in hints.get(0, [])] == want, case["source"]
     assert 1 not in hints, case["source"]
+
+
+# ---- DeviceShare GPUAllocator: partitions, topology scopes, shared GPUs -------------------------------
+GPU_ALLOC = cases.load("gpu_allocator.json")
+
+
+def gpu_alloc_setup(handle, case, node=0):
+    """Node `node` gets the case's GPUs and partition state; returns the pod (cases.py conventions)."""
+    from koordinator_amd import model
+    handle.upsert_node(node, model.make_node(allocatable={"cpu": "96", "memory": "512Gi"}))
+    handle.set_devices(node, model.make_devices(case["devices"]))
+    has_table, honor, parts = model.gpu_partition_state(node_labels=case["node_labels"])
+    handle.set_gpu_partitions(node, has_table, honor, parts)
+    return model.make_pod(requests=dict(case["pod"]["requests"]), device_hints=case["pod"]["device_hints"])
+
+
+def gpu_alloc_cfg(case, n_nodes=1):
+    from koordinator_amd import abi
+    cfg = cases.ds_cfg(case, n_nodes)
+    if case.get("weights"):
+        cfg.deviceshare.weights[:] = [abi.ABSENT if w is None else w for w in case["weights"]]
+    return cfg
+
+
+@pytest.mark.parametrize("case", GPU_ALLOC, ids=[c["name"] for c in GPU_ALLOC])
+def test_gpu_allocator(case):
+    o = Oracle(gpu_alloc_cfg(case), 1)
+    pod = gpu_alloc_setup(o, case)
+    want = case["want"]
+    assert o.ds_filter(pod, 0) == (want["code"], want["reason"]), case["source"]
+    if want["code"] == 0:
+        mask = o.ds_reserve(pod, 0)
+        assert [m for m in range(16) if mask >> m & 1] == want["minors"], case["source"]
