@@ -31,8 +31,11 @@ from koordinator_amd import Evaluator, abi, synth  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 KMAX, KSTALE = 64, 128  # candidate list lengths (ke_kernels.hip)
 CAND_BYTES = 4
-ROW_RECORD = 152  # bytes of a full node row record (ke_types.h Row) staged / published by the Reserve chain
-ROW_PATCH = 10 * 8  # int64 fields a Reserve writes back (fh 4, sa 4, NodeInfo.Requested 2)
+# replay records (ke_kernels.hip RecWord, NUM_RW = 26 int64 words per node)
+REC_READ = 25 * 8   # words a fetch loads (all but RW_PAD)
+REC_DYN = 11 * 8    # Reserve-dependent words a changed node writes back (rec_store_dyn)
+REC_FULL = 26 * 8   # the full record of a changed node in the hand-off list k_fixup reads
+ROW_PATCH = 10 * 8  # SoA int64 fields a Reserve writes back (fh 4, sa 4, NodeInfo.Requested 2)
 OUT_BYTES = 4 + 4 + 8  # chosen, score, device allocation per pod
 
 
@@ -66,29 +69,41 @@ def eval_bytes(n_nodes, b):
     return n_nodes * row + b * pod + b * n_nodes * 2
 
 
-def batch_bytes(n_nodes, b, staged, changed, pipelined):
-    """algorithmic bytes per batch of each kernel"""
+def batch_bytes(n_nodes, b, fetched, changed, pipelined):
+    """algorithmic bytes per batch of each kernel: every input read once, every output
+    written once; `fetched` = replay records of best unchanged candidates, `changed` = nodes a batch Reserved"""
     row, pod = sizes()
     L = KSTALE if pipelined else KMAX
     return {
         "k_eval_batch": eval_bytes(n_nodes, b),
         "k_select": b * n_nodes * 2 + b * (L + 1) * CAND_BYTES,
-        "k_fixup": (b * ((L + 1) * CAND_BYTES + pod + (KMAX + 1) * CAND_BYTES) + changed * ROW_RECORD) if pipelined else 0,
-        "k_resolve": b * ((KMAX + 1) * CAND_BYTES + pod + OUT_BYTES) + staged * row + changed * (ROW_PATCH + ROW_RECORD),
+        "k_fixup": (b * ((L + 1) * CAND_BYTES + pod + (KMAX + 1) * CAND_BYTES) + changed * REC_FULL) if pipelined else 0,
+        "k_resolve": b * ((KMAX + 1) * CAND_BYTES + pod + OUT_BYTES) + fetched * REC_READ
+                     + changed * (ROW_PATCH + REC_DYN + (REC_FULL if pipelined else 0)),
     }
 
 
 def pmc_traffic(tag):
-    """HBM bytes per batch by kernel from the committed PMC pass (tools/pmc_bench.sh) of this workload."""
+    """HBM bytes per launch by kernel from the committed PMC passes (tools/pmc_bench.sh, summarised by
+    tools/pmc_summary.py into profiles/r02/pmc_bench.json) of this workload.  Counter collection serialises
+    dispatches, which the persistent Reserve chain cannot run under, so the passes run the one-stream
+    schedule (tag suffix _serial): its k_eval_batch / k_select / k_resolve launches do the same work per batch."""
     f = os.path.join(ROOT, "profiles", "r02", "pmc_bench.json")
     if not os.path.exists(f):
         return {}, None
     d = json.load(open(f))
-    e = d.get("workloads", {}).get(tag)
-    return (e or {}), (f"prior PMC pass: {d.get('source')}" if e else None)
+    w = d.get("workloads", {})
+    key = tag if tag in w else (tag + "_serial" if tag + "_serial" in w else None)
+    if key is None:
+        return {}, None
+    e = {k: {x: v[x] for x in ("traffic_bytes", "valu_busy", "wave_issue_stall_share", "wave_wait_share") if x in v}
+         for k, v in w[key].items() if isinstance(v, dict) and "traffic_bytes" in v}
+    return e, f"PMC passes {key} ({d.get('source')})"
 
 
 def host_info():
+    """CPU model, the affinity mask and the cgroup CPU quota (cpu.max) -- the box shares its host, so the
+    quota, not nproc, is the number of cores a process can keep busy."""
     model = None
     try:
         for line in open("/proc/cpuinfo"):
@@ -97,8 +112,16 @@ def host_info():
                 break
     except OSError:
         pass
-    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    return {"nproc": usable, "cpu_count": os.cpu_count(), "model": model}
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    usable = affinity if quota is None else max(1, min(affinity, int(quota)))
+    return {"nproc": affinity, "cpu_count": os.cpu_count(), "cgroup_cpus": quota, "usable": usable, "model": model}
 
 
 def cpu_baseline(cl, pods, cfg, seconds):
@@ -109,7 +132,7 @@ def cpu_baseline(cl, pods, cfg, seconds):
     o = Oracle(cfg, cl.n_nodes)
     synth.load_into(o, cl)
     rates, pos = {}, 0
-    for threads in sorted({1, 16, max(1, info["nproc"])}):
+    for threads in sorted({1, 16, info["usable"]}):
         o.schedule(pods[pos:pos + 4], synth.T0, n_threads=threads)  # thread pool warm-up
         pos += 4
         p0, dt, chunk = pos, 0.0, 8  # doubling chunks of the queue until ~`seconds` of work
@@ -125,13 +148,14 @@ def cpu_baseline(cl, pods, cfg, seconds):
     return {"value": rates[best]["value"], "unit": "pod-node evals/s", "cores": int(best), "kind": "port",
             "host": info, "rates_by_threads": rates,
             "sample": f"oracle (C restatement of the Go plugins) scheduling consecutive prefixes of the same queue "
-                      f"against all {cl.n_nodes} nodes at 1 / 16 / {info['nproc']} threads (~{seconds:.0f} s each); "
+                      f"against all {cl.n_nodes} nodes at 1 / 16 / {info['usable']} threads (all usable cores: "
+                      f"cgroup quota {info['cgroup_cpus']}, affinity {info['nproc']}) (~{seconds:.0f} s each); "
                       f"value = the fastest ({best} threads)"}
 
 
 def roofline(n_nodes, b, ks, dt_step, batches_per_step, pipelined, tag):
     """The dominant kernel's roofline (the Reserve chain) with the per-kernel and end-to-end fractions."""
-    by = batch_bytes(n_nodes, b, ks["rows_staged"], ks["rows_changed"], pipelined)
+    by = batch_bytes(n_nodes, b, ks["rows_fetched"], ks["rows_changed"], pipelined)
     ms = {"k_eval_batch": ks["eval_ms"], "k_select": ks["select_ms"], "k_fixup": ks["fixup_ms"],
           "k_resolve": ks["resolve_ms"]}
     traffic, src = pmc_traffic(tag)
@@ -139,8 +163,10 @@ def roofline(n_nodes, b, ks, dt_step, batches_per_step, pipelined, tag):
     for k in by:
         t = ms[k]
         ach = by[k] / t / 1e6 if t else None
+        pmc = traffic.get(k, {})
         kern[k] = {"bytes_per_batch": by[k], "ms_per_batch": t, "achieved": ach,
-                   "frac": ach / HBM_PEAK_GBS if ach else None, "traffic": traffic.get(k)}
+                   "frac": ach / HBM_PEAK_GBS if ach else None, "traffic": pmc.get("traffic_bytes"),
+                   "valu_busy": pmc.get("valu_busy"), "issue_stall_share": pmc.get("wave_issue_stall_share")}
     step_bytes = sum(by.values()) * batches_per_step
     dom = kern["k_resolve"]
     return {"bound": "hbm", "kernel": "k_resolve_run (per 64-pod batch: prologue + sequential replay)",
@@ -247,7 +273,7 @@ def main():
     mean = lambda key: float(np.mean([k[key] for k in kss]))  # noqa: E731
     kagg = {"eval_ms": sum(evm) / max(samples, 1), "select_ms": sum(sel) / max(samples, 1),
             "fixup_ms": mean("fixup_ms"), "resolve_ms": mean("resolve_ms"), "handoff_ms": mean("handoff_ms"),
-            "rows_staged": mean("rows_staged"), "rows_changed": mean("rows_changed")}
+            "rows_fetched": mean("rows_fetched"), "rows_changed": mean("rows_changed")}
     tag = f"config{a.config}_nodes{hi - lo}_batch{a.batch}_world{world}" + ("" if not a.no_pipeline else "_serial")
     out = {
         "metric": "pod-node Filter+Score evals/sec + p99 per-pod sched latency @50k nodes",
@@ -275,7 +301,7 @@ def main():
                       "resolve_prologue": float(np.mean([x[0] for x in rsplit])),
                       "resolve_replay": float(np.mean([x[1] for x in rsplit])),
                       "pipelined_batches": npipe, "batches": n_batches, "event_samples": samples,
-                      "rows_staged_per_batch": kagg["rows_staged"], "rows_changed_per_batch": kagg["rows_changed"],
+                      "records_fetched_per_batch": kagg["rows_fetched"], "rows_changed_per_batch": kagg["rows_changed"],
                       "note": "per batch; 'select' includes the all-gather + merge when sharded"},
         "host_ms_per_step": {k: float(np.mean([h[k] for h in hs])) for k in hs[0]} if hs else None,
         "roofline": roofline(hi - lo, a.batch, kagg, dt / K, n_batches / K, not a.no_pipeline, tag),

@@ -626,8 +626,8 @@ int ke_last_kernel_stats(ke_ctx* ctx, double* eval_ms, double* select_ms, double
 /* Per-batch statistics of the last ke_schedule: v8 = {eval ms, select ms (HIP-event samples on the eval
  * stream), fixup ms (k_fixup after its wait, pipelined batches), Reserve ms (in-kernel stamps: prologue +
  * replay, every batch), host enqueue ms of the whole call, hand-off ms (end of a pipelined batch's replay
- * -> start of the next one's), distinct candidate rows staged per batch, rows changed per batch}, the
- * number of event samples, and how many batches ran pipelined. */
+ * -> start of the next one's), replay records fetched per batch (best unchanged candidates), rows changed
+ * per batch}, the number of event samples, and how many batches ran pipelined. */
 int ke_last_kernel_stats_ex(ke_ctx* ctx, double* v8, int32_t* samples, int32_t* pipelined_batches);
 /* Pipelined schedule (default on): batch b's eval + select overlap batch b-1's Reserve replay on a
  * second stream.  Off = one stream, every batch waits for the previous Reserve.  The

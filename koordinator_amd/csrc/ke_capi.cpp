@@ -602,7 +602,7 @@ int ke_last_kernel_stats_ex(ke_ctx* ctx, double* ms4 /* [8] */, int32_t* samples
   if (pipelined_batches) *pipelined_batches = ctx->c.last_pipelined;
   ms4[4] = ctx->c.last_enqueue_ms;
   ms4[5] = ctx->c.kstat_handoff_ms;
-  ms4[6] = ctx->c.kstat_rows_staged;
+  ms4[6] = ctx->c.kstat_rows_fetched;
   ms4[7] = ctx->c.kstat_rows_changed;
   return KE_OK;
 }

@@ -561,9 +561,14 @@ __device__ __noinline__ void ds_filter_score(const SoA& s, int64_t i, const DevP
       return;
     }
   int64_t raw = 0;
+  // GPUs on a node without partition table / honor policy / topology tree, for a pod without a partition
+  // spec or required scope, go straight to defaultAllocateDevices: only its count is needed
+  const bool gpu_default = !(msk[DSM_EXISTS] & (DSX_TOPO | DSX_TABLE | DSX_HONOR)) &&
+                           !(p.flags & (PF_GPU_PART_SPEC | 7u * PF_GPU_SCOPE0));
   for (int t = 0; t < 3; t++) {
     if (!p.ds_cnt[t]) continue;
     uint64_t ex = (msk[DSM_EXISTS] >> (16 * t)) & 0xFFFF;
+    const bool masks = t == KE_DEV_GPU && !gpu_default;
     GpuMasks g;
     g.minors = (uint32_t)ex;
     g.total = g.used = g.sat = g.dflt = 0;
@@ -575,11 +580,13 @@ __device__ __noinline__ void ds_filter_score(const SoA& s, int64_t i, const DevP
       DsInst d;
       ds_instance(s, i, t, m, msk, d);
       const bool leq = ds_leq(d, p, t), fz = ds_free_zero(d);
-      present = present || !fz;
       g.dflt |= (uint32_t)(!fz && leq) << m;
-      g.sat |= (uint32_t)(leq && ds_total_nz(d)) << m;
-      g.total |= (uint32_t)ds_total_nz(d) << m;
-      g.used |= (uint32_t)d.used_nz << m;
+      if (masks) {
+        present = present || !fz;
+        g.sat |= (uint32_t)(leq && ds_total_nz(d)) << m;
+        g.total |= (uint32_t)ds_total_nz(d) << m;
+        g.used |= (uint32_t)d.used_nz << m;
+      }
 #pragma unroll
       for (int key = 0; key < 3; key++) {
         tot[key] += ((d.th >> key) & 1) ? d.tv[key] : 0;
@@ -588,7 +595,7 @@ __device__ __noinline__ void ds_filter_score(const SoA& s, int64_t i, const DevP
     }
     if (!present) g.total = g.sat = 0;  // the filtered nodeDevice dropped the type
     int st = 0, reason = KE_REASON_DS_INSUFFICIENT_GPU + t;
-    if (t == KE_DEV_GPU) {
+    if (masks) {
       uint32_t unused;
       st = gpu_allocate(s, i, msk[DSM_EXISTS], p, g, false, nullptr, &unused, &reason);
     } else if (__builtin_popcount(g.dflt) < p.ds_cnt[t]) {  // defaultAllocateDevices: "Insufficient <type> devices"
@@ -3328,6 +3335,13 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
 }
 
 __global__ void k_stamp(uint64_t* stamps) { stamps[0] = __builtin_amdgcn_s_memrealtime(); }
+// start of a batch on its eval stream: the eval-start stamp, and the zeroed atomicMax targets of a
+// DeviceShare batch (NormalizeScore's max) and of a one-pod argmax (one launch instead of three)
+__global__ void k_batch_begin(uint64_t* stamp, uint32_t* dsmax, uint32_t* argmax) {
+  stamp[0] = __builtin_amdgcn_s_memrealtime();
+  if (dsmax) dsmax[0] = 0;
+  if (argmax) argmax[0] = 0;
+}
 
 // ---------------------------------------------------------------------------------------------
 // device state
@@ -3970,6 +3984,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   }
   // pipelined runs: maximal stretches of plain batches (no DeviceShare / cpuset pod) in a
   // context without NUMA policies; run_end[b] > 0 marks the first batch of a run and holds its end
+  // (a lone plain batch between singletons gains nothing from the second stream: it runs serially)
   auto eligible = [&](int b) { return d->pipeline && N > 0 && !numa && !batches[b].ds && !batches[b].cpu; };
   std::vector<int> run_end((size_t)n_batches, 0);
   for (int b = 0; b < n_batches;) {
@@ -3979,7 +3994,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     }
     int e = b;
     while (e < n_batches && eligible(e)) e++;
-    run_end[b] = e;
+    if (e - b >= 2) run_end[b] = e;
     b = e;
   }
   // device: bases [n+1], ready [n], done [n], error word; fixup stamps [2n]
@@ -4014,16 +4029,18 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   uint64_t* estamps = d->d_stamps + 9 * ((int64_t)n_pods + 2);  // eval start of each batch
   constexpr int R = DeviceState::EV_RING;
   int n_pipelined = 0;
-  // Batch b's eval + candidate lists on estream.  pipe: stale top-(k_j + KMAX) lists into the run's
+  // Batch b's eval + candidate lists on stream `es`.  pipe: stale top-(k_j + KMAX) lists into the run's
   // stale buffer (k_fixup makes them exact); else the exact top-k_j lists straight into d_cand.
-  auto eval_select = [&](int b, bool pipe) -> int {
+  auto eval_select = [&](int b, bool pipe, hipStream_t es) -> int {
     const int bp = batches[b].pods;
     const bool ds = batches[b].ds, cpu = batches[b].cpu;
     const bool prof = every > 0 && b % every == 0;
     hipEvent_t* pe = prof ? &ev[(size_t)(b / every) * PE] : nullptr;
     const int32_t* bbase = d_bases + b;
-    hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, d->estream, estamps + b);
-    if (prof) HIP_OK(hipEventRecord(pe[0], d->estream));
+    const bool argmax1 = !sharded && bp == 1 && !pipe && N > 0;  // selectHost of one pod: a grid-wide argmax
+    hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(1), 0, es, estamps + b, ds ? d->d_dsmax : nullptr,
+                       argmax1 ? d->d_cand : nullptr);
+    if (prof) HIP_OK(hipEventRecord(pe[0], es));
     const int L = pipe ? KSTALE : KMAX, kext = pipe ? KMAX : 0;
     uint32_t* lists = pipe ? d->d_stale + (size_t)(b & 1) * MAX_BATCH * KSTALE : d->d_cand;
     int32_t* lists_cnt = pipe ? d->d_stale_cnt + (b & 1) * MAX_BATCH : d->d_cand_cnt;
@@ -4032,7 +4049,6 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       int lo = 0, hi = N;
       if (sharded && !d->loopback) shard_range(N, d->rank, d->world, &lo, &hi);
       const bool single = bp == 1;
-      if (ds) HIP_OK(hipMemsetAsync(d->d_dsmax, 0, sizeof(uint32_t), d->estream));  // the eval's atomicMax target
       if (hi > lo) {
         // a singleton batch has one pod's worth of lanes: single-wave blocks spread it over every CU
         const int eb = single ? 64 : EVAL_BLOCK;
@@ -4042,29 +4058,28 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                         : ds ? (numa ? k_eval_batch<true, true, false> : k_eval_batch<true, false, false>)
                              : (numa ? k_eval_batch<false, true, false> : k_eval_batch<false, false, false>);
         uint32_t* dcnt = numa ? d->d_defer_cnt + b : nullptr;
-        hipLaunchKernelGGL(eval, grid, dim3(eb), 0, d->estream, d->soa, lo, hi, d->d_pods, bbase, bp,
+        hipLaunchKernelGGL(eval, grid, dim3(eb), 0, es, d->soa, lo, hi, d->d_pods, bbase, bp,
                            ppb, k, d->d_scores, d->capacity, d->d_dsraw, d->d_defer, dcnt, d->d_aff, d->d_dsmax);
         if (numa && !ds)  // DeviceShare pods never meet a NUMA policy: nothing deferred in their batches
           hipLaunchKernelGGL((cpu ? k_numa_fallback<false, true> : k_numa_fallback<false, false>), dim3(FALLBACK_BLOCKS),
-                             dim3(64), 0, d->estream, d->soa, d->d_pods,
+                             dim3(64), 0, es, d->soa, d->d_pods,
                              bbase, k, d->d_defer, dcnt, d->d_scores, d->capacity, 0, nullptr, nullptr,
                              nullptr, nullptr, nullptr, nullptr, nullptr, cpu ? d->d_aff : nullptr);
       }
       if (ds && sharded && !d->loopback)  // DefaultNormalizeScore's max over the feasible nodes of all ranks
-        RCCL_OK(ncclAllReduce(d->d_dsmax, d->d_dsmax, 1, ncclUint32, ncclMax, d->comm, d->estream));
-      if (prof) HIP_OK(hipEventRecord(pe[1], d->estream));
+        RCCL_OK(ncclAllReduce(d->d_dsmax, d->d_dsmax, 1, ncclUint32, ncclMax, d->comm, es));
+      if (prof) HIP_OK(hipEventRecord(pe[1], es));
       auto select = [&](int slo, int shi, uint32_t* cand, int32_t* cnt) {
         if (ds)
-          hipLaunchKernelGGL(k_select<true>, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, d->estream, d->d_scores,
+          hipLaunchKernelGGL(k_select<true>, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, es, d->d_scores,
                              d->capacity, slo, shi, cand, cnt, d->d_dsraw, d->d_dsmax, k.wp_ds, kext, L);
         else
-          hipLaunchKernelGGL(k_select<false>, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, d->estream, d->d_scores,
+          hipLaunchKernelGGL(k_select<false>, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, es, d->d_scores,
                              d->capacity, slo, shi, cand, cnt, d->d_dsraw, d->d_dsmax, k.wp_ds, kext, L);
       };
-      if (!sharded && single && !pipe) {  // selectHost of one pod: a grid-wide argmax
-        HIP_OK(hipMemsetAsync(d->d_cand, 0, sizeof(uint32_t), d->estream));
+      if (argmax1) {  // d_cand[0] zeroed by k_batch_begin
         hipLaunchKernelGGL((ds ? k_argmax1<true> : k_argmax1<false>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
-                           d->estream, d->d_scores, 0, N, d->d_dsraw, d->d_dsmax, k.wp_ds, d->d_cand, d->d_cand_cnt);
+                           es, d->d_scores, 0, N, d->d_dsraw, d->d_dsmax, k.wp_ds, d->d_cand, d->d_cand_cnt);
       } else if (!sharded) {
         select(0, N, lists, lists_cnt);
       } else {
@@ -4079,16 +4094,16 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
         }
         if (!d->loopback) {
           uint32_t* mine = d->d_gath + (int64_t)d->rank * gw;  // in place: send = own block of recv
-          RCCL_OK(ncclAllGather(mine, d->d_gath, gw, ncclUint32, d->comm, d->estream));
+          RCCL_OK(ncclAllGather(mine, d->d_gath, gw, ncclUint32, d->comm, es));
         }
-        hipLaunchKernelGGL(k_merge, dim3((unsigned)bp), dim3(MERGE_BLOCK), 0, d->estream, d->d_gath, d->world, L, kext,
+        hipLaunchKernelGGL(k_merge, dim3((unsigned)bp), dim3(MERGE_BLOCK), 0, es, d->d_gath, d->world, L, kext,
                            lists, lists_cnt);
       }
     } else {
-      if (prof) HIP_OK(hipEventRecord(pe[1], d->estream));
-      HIP_OK(hipMemsetAsync(lists_cnt, 0, sizeof(int32_t) * MAX_BATCH, d->estream));
+      if (prof) HIP_OK(hipEventRecord(pe[1], es));
+      HIP_OK(hipMemsetAsync(lists_cnt, 0, sizeof(int32_t) * MAX_BATCH, es));
     }
-    if (prof) HIP_OK(hipEventRecord(pe[2], d->estream));
+    if (prof) HIP_OK(hipEventRecord(pe[2], es));
     return KE_OK;
   };
   // Two streams (pipelining).  A run of plain batches: one persistent k_resolve_run on
@@ -4108,7 +4123,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                          d->d_devalloc, d_ready, d_done, d_err, d->d_trows, d->d_tcnt, d->d_chg, N);
       if (r0 > 0) HIP_OK(hipStreamWaitEvent(d->estream, d->ev_res[(r0 - 1) % R], 0));
       for (int q = r0; q < e; q++) {
-        rc = eval_select(q, true);
+        rc = eval_select(q, true, d->estream);
         if (rc) return rc;
         const bool first = q == r0;
         hipLaunchKernelGGL(k_fixup, dim3((unsigned)batches[q].pods), dim3(FIX_BLOCK), 0, d->estream, d->d_pods,
@@ -4117,18 +4132,19 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                            d_done, first ? -1 : q - 1, d_ready + q, d_err, d_fst + 2 * q);
       }
       HIP_OK(hipEventRecord(d->ev_res[(e - 1) % R], d->stream));
+      HIP_OK(hipEventRecord(d->ev_sel[(e - 1) % R], d->estream));
       n_pipelined += e - r0;
       b = e;
+      if (b < n_batches && run_end[b] == 0)  // a serial batch next: the run's eval stream drains first
+        HIP_OK(hipStreamWaitEvent(d->stream, d->ev_sel[(e - 1) % R], 0));
       continue;
     }
+    // serial batch: eval, select and Reserve in order on one stream (no cross-stream hand-off)
     const int bp = batches[b].pods;
     const bool ds = batches[b].ds, cpu = batches[b].cpu;
     const int32_t* bbase = d_bases + b;
-    if (b > 0) HIP_OK(hipStreamWaitEvent(d->estream, d->ev_res[(b - 1) % R], 0));
-    rc = eval_select(b, false);
+    rc = eval_select(b, false, d->stream);
     if (rc) return rc;
-    HIP_OK(hipEventRecord(d->ev_sel[b % R], d->estream));
-    HIP_OK(hipStreamWaitEvent(d->stream, d->ev_sel[b % R], 0));
     if (bp == 1) {  // one pod: the single-node Reserve (cpuset accumulator when it binds)
       int elo = 0, ehi = 0;  // nodes whose affinities this batch's eval stored in d_aff (binding batches)
       if (cpu && numa) {
@@ -4151,7 +4167,8 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                          d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score, ctx->cfg.global_node_offset,
                          d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc, d->d_numaalloc, d->d_chg, N);
     }
-    HIP_OK(hipEventRecord(d->ev_res[b % R], d->stream));
+    if (b + 1 < n_batches && run_end[b + 1] > 0)  // the next run's eval stream waits for this Reserve
+      HIP_OK(hipEventRecord(d->ev_res[b % R], d->stream));
     b++;
   }
   HIP_OK(hipGetLastError());
@@ -4247,12 +4264,12 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     }
   }
   ctx->kstat_resolve_ms = n_batches ? res_sum / n_batches : 0;
-  double rows_staged = 0, rows_changed = 0;
+  double rows_fetched = 0, rows_changed = 0;
   for (int b = 0; b < n_batches; b++) {
-    rows_staged += (double)pst[8 * (size_t)b + 6];
+    rows_fetched += (double)pst[8 * (size_t)b + 6];
     rows_changed += (double)pst[8 * (size_t)b + 7];
   }
-  ctx->kstat_rows_staged = n_batches ? rows_staged / n_batches : 0;
+  ctx->kstat_rows_fetched = n_batches ? rows_fetched / n_batches : 0;
   ctx->kstat_rows_changed = n_batches ? rows_changed / n_batches : 0;
   ctx->kstat_fixup_ms = fx_n ? fx_sum / fx_n : 0;
   ctx->kstat_handoff_ms = ho_n ? ho_sum / ho_n : 0;

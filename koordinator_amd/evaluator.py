@@ -246,7 +246,7 @@ class Evaluator:
         self._check(self.lib.ke_debug_resolve_phases(self.h, abi.ptr(ph)))
         return {"eval_ms": ms4[0], "select_ms": ms4[1], "fixup_ms": ms4[2], "resolve_ms": ms4[3], "samples": n.value,
                 "pipelined_batches": npipe.value, "enqueue_ms": ms4[4], "handoff_ms": ms4[5],
-                "rows_staged": ms4[6], "rows_changed": ms4[7],
+                "rows_fetched": ms4[6], "rows_changed": ms4[7],
                 "resolve_prologue_ms": p.value, "resolve_replay_ms": r.value,
                 "resolve_phases_ms": dict(zip(["init", "cand_copy", "hash", "lookup", "rows", "replay"],
                                               ph.tolist()))}

@@ -66,6 +66,7 @@ def main():
     ev.set_profiling(8)
     sl = P // K
     lat, ks_acc, samples, placed, with_dev = [], {"eval_ms": 0.0, "select_ms": 0.0, "resolve_ms": 0.0}, 0, 0, 0
+    hs = []
     t0 = time.perf_counter()
     for s in range(K):
         chosen, _ = ev.schedule(pods[s * sl:(s + 1) * sl], synth.T0)
@@ -74,9 +75,11 @@ def main():
         _, per_batch = ev.stats()
         lat.extend(per_batch.tolist())
         ks = ev.kernel_stats()
-        for key in ks_acc:
+        for key in ("eval_ms", "select_ms"):  # HIP-event samples
             ks_acc[key] += ks[key] * ks["samples"]
+        ks_acc["resolve_ms"] += ks["resolve_ms"] * len(per_batch)  # in-kernel stamps: mean over every batch
         samples += ks["samples"]
+        hs.append(ev.host_stats())
     dt = time.perf_counter() - t0
     ev.close()
     out = {"workload": f"{N} nodes x (8 GPU + 2 RDMA), {K * sl} pods ({a.device:.0%} with device requests)"
@@ -84,8 +87,11 @@ def main():
            "value": K * sl * N / dt, "unit": "pod-node evals/s", "pods_per_s": K * sl / dt,
            "ms_per_pod": dt / (K * sl) * 1e3, "batches": len(lat),
            "p99_batch_latency_ms": float(np.percentile(lat, 99)), "p50_batch_latency_ms": float(np.percentile(lat, 50)),
-           "kernel_ms_per_batch": {k: v / max(samples, 1) for k, v in ks_acc.items()},
-           "placed": placed, "device_allocations": with_dev}
+           "kernel_ms_per_batch": {"eval_ms": ks_acc["eval_ms"] / max(samples, 1),
+                                   "select_ms": ks_acc["select_ms"] / max(samples, 1),
+                                   "resolve_ms": ks_acc["resolve_ms"] / max(len(lat), 1)},
+           "placed": placed, "device_allocations": with_dev,
+           "host_ms_per_step": {k: float(np.mean([h[k] for h in hs])) for k in hs[0]} if hs else None}
     if not a.no_cpu_baseline:
         from oracle.binding import Oracle  # checker / baseline only
 
