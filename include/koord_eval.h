@@ -83,6 +83,7 @@ extern "C" {
 #define KE_REASON_DS_MULTI_SHARED_GPU 40          /* ErrUnsupportedMultiSharedGPU (required scope only) */
 #define KE_REASON_DS_INSUFFICIENT_TOPOLOGY_SCOPED 41 /* ErrInsufficientTopologyScopedGPUDevices */
 #define KE_REASON_DS_INSUFFICIENT_GPU_TOPOLOGY 42 /* ErrInsufficientGPUDevices "Insufficient GPU Devices" (topology tree) */
+#define KE_REASON_DS_INSUFFICIENT_NUMA_SCOPED 43  /* ErrInsufficientNUMAScopedDevices (topology_hint.go:32), via Admit */
 
 /* ---- resources (index into per-resource arrays) ---------------------------------------------- */
 #define KE_RES_CPU 0          /* "cpu"                         MilliValue */
@@ -283,7 +284,9 @@ typedef struct ke_deviceshare_args {
    * utils.go:508-515), which is not implemented: ke_eval / ke_schedule return KE_ERR_UNSUPPORTED for it. */
   uint8_t template_matched_keys;
   uint8_t has_other_keys; /* ScoringStrategy.Resources names a resource outside KE_DSW_*: not supported */
-  uint8_t pad[2];
+  uint8_t disable_numa_alignment; /* DisableDeviceNUMATopologyAlignment (types.go:271-272): no device NUMA
+                                     hints, no device Allocate in Admit, Reserve ignores the affinity */
+  uint8_t pad;
 } ke_deviceshare_args;
 
 /* One device instance as koord-scheduler's nodeDeviceCache holds it (device_cache.go:518-568):
@@ -298,9 +301,10 @@ typedef struct ke_device {
   uint8_t has_topology; /* DeviceInfo.Topology != nil */
   int64_t total[KE_DKEYS];
   int64_t used[KE_DKEYS];
-  /* DeviceInfo.Topology: NodeID, and the rank of PCIEID among the node's distinct PCIEID strings in Go string
-   * order (0 = smallest).  GetGPUTopologyScope (allocator_gpu_helper.go:202-263) builds the GPU scope tree
-   * Node > NUMANode (by NodeID) > PCIe (by PCIEID) from them when every GPU device has a topology. */
+  /* DeviceInfo.Topology: NodeID (-1 .. KE_MAX_NUMA-1), and the rank of PCIEID among the node's distinct PCIEID
+   * strings in Go string order (0 = smallest).  GetGPUTopologyScope (allocator_gpu_helper.go:202-263) builds
+   * the GPU scope tree Node > NUMANode (by NodeID) > PCIe (by PCIEID) from them when every GPU device has a
+   * topology; DeviceShare's NUMA hints (topology_hint.go) group the devices by NodeID (-1: any NUMA node). */
   int32_t numa_node;
   int32_t pcie_rank;
 } ke_device; /* 72 bytes */

@@ -53,6 +53,7 @@ REASON_DS_MISSING_TOPOLOGY_TREE = 39
 REASON_DS_MULTI_SHARED_GPU = 40
 REASON_DS_INSUFFICIENT_TOPOLOGY_SCOPED = 41
 REASON_DS_INSUFFICIENT_GPU_TOPOLOGY = 42
+REASON_DS_INSUFFICIENT_NUMA_SCOPED = 43
 # ke_pod.gpu_required_topology_scope (apiext.DeviceTopologyScope -> level)
 SCOPE_NONE, SCOPE_NODE, SCOPE_NUMA, SCOPE_PCIE, SCOPE_DEVICE, SCOPE_UNKNOWN = range(6)
 SCOPES = {"": SCOPE_NONE, "Node": SCOPE_NODE, "NUMANode": SCOPE_NUMA, "PCIe": SCOPE_PCIE, "Device": SCOPE_DEVICE}
@@ -141,7 +142,7 @@ class NumaZone(C.Structure):
 
 class DeviceShareArgs(C.Structure):
     _fields_ = [("weights", i64 * 4), ("strategy", i32), ("template_matched_keys", u8), ("has_other_keys", u8),
-                ("pad", u8 * 2)]
+                ("disable_numa_alignment", u8), ("pad", u8)]
 
 
 class Device(C.Structure):

@@ -53,23 +53,11 @@ static int require_device(ke_ctx* ctx) {
   return KE_OK;
 }
 
-// DeviceShare is a NUMA hint provider for pods with device requests (deviceshare/topology_hint.go);
-// that provider is not modelled, so such pods cannot meet nodes with a NUMA topology policy.
-// A pod with its own NUMA topology policy switches the NUMA path on for every node.
+// A pod with its own NUMA topology policy switches the NUMA path on for every node (DeviceShare pods on
+// NUMA-policy nodes take part in the topology manager's Admit as a second hint provider).
 static int check_numa_deviceshare(ke_ctx* ctx, const ke_pod* pods, int32_t n) {
-  bool ds = false;
-  for (int32_t p = 0; p < n; p++) {
+  for (int32_t p = 0; p < n; p++)
     if (pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE) ctx->c.numa_enabled = true;
-    if (make_dev_pod(ctx->c.cfg, pods[p]).flags & PF_DS) {
-      ds = true;
-      if (pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE)
-        return fail(KE_ERR_UNSUPPORTED, "DeviceShare pods with a NUMA topology policy (DeviceShare NUMA hints)");
-    }
-  }
-  if (!ds || !ctx->c.numa_enabled) return KE_OK;
-  for (int32_t i = 0; i < ctx->c.n_nodes; i++)
-    if (ctx->c.nodes[i].valid && ctx->c.nodes[i].node.numa_topology_policy != KE_NUMA_POLICY_NONE)
-      return fail(KE_ERR_UNSUPPORTED, "DeviceShare pods on nodes with a NUMA topology policy (DeviceShare NUMA hints)");
   return KE_OK;
 }
 
@@ -141,6 +129,7 @@ int ke_create(const ke_config* cfg, ke_ctx** out) {
   if (a.node_metric_expiration_seconds != KE_ABSENT) f |= AF_EXP_PRESENT;
   if (cfg->numa.strategy == KE_STRATEGY_MOST_ALLOCATED) f |= AF_NUMA_MOST;
   if (cfg->deviceshare.strategy == KE_STRATEGY_MOST_ALLOCATED) f |= AF_DS_MOST;
+  if (cfg->deviceshare.disable_numa_alignment) f |= AF_DS_NO_NUMA;
   if (cfg->numa.numa_strategy == KE_STRATEGY_MOST_ALLOCATED) f |= AF_NUMA_HINT_MOST;
   k.flags = f;
   k.wsum_la = k.wsum_numa = 0;

@@ -98,6 +98,8 @@ int validate_devices(int32_t n, const ke_device* devs) {
         return fail(KE_ERR_INVALID, "negative device quantity");
     if (d.has_topology && (d.pcie_rank < 0 || d.pcie_rank >= KE_DEV_TYPES * KE_MAX_MINORS))
       return fail(KE_ERR_INVALID, "device pcie_rank out of range");
+    if (d.has_topology && (d.numa_node < -1 || d.numa_node >= KE_MAX_NUMA))
+      return fail(KE_ERR_UNSUPPORTED, "device NUMA node outside -1 .. KE_MAX_NUMA-1");
     // fillGPUTotalMem divides by the instance's gpu-memory (devicehandler_gpu.go:110-125)
     if (d.type == KE_DEV_GPU && d.health && !(d.has_total[KE_DKEY_GPU_MEMORY] && d.total[KE_DKEY_GPU_MEMORY] > 0))
       return fail(KE_ERR_UNSUPPORTED, "healthy GPU device without a positive gpu-memory total");
@@ -141,6 +143,9 @@ void derive_ds_row(const NodeState& ns, int64_t* f, uint64_t* m) {
   for (int i = 0; i < NUM_DS_MASKS; i++) m[i] = 0;
   if (!ns.has_dev_cache) return;
   if (gpu_topology_ranks(ns, &m[DSM_TOPO], &m[DSM_PCIE])) m[DSM_EXISTS] |= DSX_TOPO;
+  for (const ke_device& d : ns.devs)  // DeviceShare's NUMA hints group devices by Topology.NodeID
+    if (d.has_topology)
+      m[DSM_DNUMA + d.type] |= (uint64_t)(d.numa_node < 0 ? DN_ANY : 1u + (uint32_t)d.numa_node) << (4 * d.minor);
   if (ns.gpu_honor) m[DSM_EXISTS] |= DSX_HONOR;
   if (ns.ptable >= 0) m[DSM_EXISTS] |= DSX_TABLE | ((uint64_t)ns.ptable << DSX_TABLE_SHIFT);
   for (const ke_device& d : ns.devs) {

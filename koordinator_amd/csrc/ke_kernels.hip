@@ -64,7 +64,10 @@ struct SoA {
   int32_t* qm;      // ElasticQuota: QT_STRIDE meta words (ke_types.h qm_*)
   int64_t* rec;     // replay records: NUM_RW int64 words per node, row-major (RecWord)
   uint64_t* pt;     // GPU partition tables: PT_WORDS words per table (ke_types.h), nullptr until one is set
+  int32_t* kerr;    // device error word of the context (KERR_* bits; the host reads it after a call)
 };
+// kerr bits: an input the kernels refuse mid-call (the call returns KE_ERR_UNSUPPORTED)
+constexpr int32_t KERR_DS_MERGE = 1;  // a DeviceShare BestEffort merge beyond the permutation budget
 
 // ---------------------------------------------------------------------------------------------
 // ElasticQuota PreFilter / Reserve (elasticquota/plugin.go:223-275,345-359; plugin_helper.go:281-301;
@@ -341,6 +344,23 @@ __device__ __forceinline__ int64_t ds_weighted(const KArgs& k, int t, const int6
   return ws ? sc / ws : 0;
 }
 
+// bitmask.IterateBitMasks order over NUMA ids 0..7: by popcount, then lexicographic on the ascending
+// id list.  Restricted to the subsets of a node's zones it is the order over those zones.
+__constant__ uint8_t NUMA_ORDER[255] = {
+    1, 2, 4, 8, 16, 32, 64, 128, 3, 5, 9, 17, 33, 65, 129, 6, 10, 18, 34, 66, 130, 12, 20, 36, 68, 132, 24,
+    40, 72, 136, 48, 80, 144, 96, 160, 192, 7, 11, 19, 35, 67, 131, 13, 21, 37, 69, 133, 25, 41, 73, 137,
+    49, 81, 145, 97, 161, 193, 14, 22, 38, 70, 134, 26, 42, 74, 138, 50, 82, 146, 98, 162, 194, 28, 44, 76,
+    140, 52, 84, 148, 100, 164, 196, 56, 88, 152, 104, 168, 200, 112, 176, 208, 224, 15, 23, 39, 71, 135,
+    27, 43, 75, 139, 51, 83, 147, 99, 163, 195, 29, 45, 77, 141, 53, 85, 149, 101, 165, 197, 57, 89, 153,
+    105, 169, 201, 113, 177, 209, 225, 30, 46, 78, 142, 54, 86, 150, 102, 166, 198, 58, 90, 154, 106, 170,
+    202, 114, 178, 210, 226, 60, 92, 156, 108, 172, 204, 116, 180, 212, 228, 120, 184, 216, 232, 240, 31,
+    47, 79, 143, 55, 87, 151, 103, 167, 199, 59, 91, 155, 107, 171, 203, 115, 179, 211, 227, 61, 93, 157,
+    109, 173, 205, 117, 181, 213, 229, 121, 185, 217, 233, 241, 62, 94, 158, 110, 174, 206, 118, 182, 214,
+    230, 122, 186, 218, 234, 242, 124, 188, 220, 236, 244, 248, 63, 95, 159, 111, 175, 207, 119, 183, 215,
+    231, 123, 187, 219, 235, 243, 125, 189, 221, 237, 245, 249, 126, 190, 222, 238, 246, 250, 252, 127, 191,
+    223, 239, 247, 251, 253, 254, 255};
+__constant__ uint8_t NUMA_OFF[10] = {0, 0, 8, 36, 92, 162, 218, 246, 254, 255};  // first entry of each size
+
 // ---- GPUAllocator.Allocate (allocator_gpu.go:72-451) ------------------------------------------------
 // The node's GPUs as AllocateContext sees them, as minor masks.
 struct GpuMasks {
@@ -440,7 +460,8 @@ __device__ __forceinline__ void scope_take(uint32_t mask, int level, int depth, 
     int64_t bs = -1;
     for (uint32_t rest = sm; rest; rest &= rest - 1) {
       const int m = __builtin_ctz(rest);
-      if (dscore[m] > bs) bm = m, bs = dscore[m];
+      const int64_t sc = dscore ? dscore[m] : 0;  // no scorer (Filter, hints): every score 0
+      if (sc > bs) bm = m, bs = sc;
     }
     r.minors = 1u << bm;
     r.score = bs;
@@ -510,8 +531,25 @@ __device__ bool gpu_topology_feasible(const SoA& s, int64_t i, const DevPod& p, 
   return false;
 }
 
+// defaultAllocateDevices' choice among the satisfiable instances `ok`: (scoreDevice desc, minor asc)
+// (device_resources.go:171-208), the first `want`; without a scorer the lowest minors.
+__device__ __forceinline__ uint32_t default_pick(uint32_t ok, int want, const int64_t* score) {
+  uint32_t take = 0;
+  for (int c = 0; c < want && ok; c++) {
+    int best = -1;
+    for (uint32_t r = ok; r; r &= r - 1) {
+      const int m = __builtin_ctz(r);
+      if (best < 0 || (score && score[m] > score[best])) best = m;  // ascending minors: ties keep the lower
+    }
+    ok &= ~(1u << best);
+    take |= 1u << best;
+  }
+  return take;
+}
+
 // GPUAllocator.Allocate after allocateByTemplate (refused at the boundary).  Returns the framework code
-// (0 = allocated); *minors = the chosen minors when select (Reserve), else only feasibility is decided.
+// (0 = allocated); with `select` *minors = the chosen minors (dscore: scoreDevice per minor, nullptr = no
+// scorer), else only feasibility is decided.
 __device__ int gpu_allocate(const SoA& s, int64_t i, uint64_t ex0, const DevPod& p, const GpuMasks& g, bool select,
                             const int64_t* dscore, uint32_t* minors, int* reason) {
   const int want = p.ds_cnt[KE_DEV_GPU];
@@ -543,22 +581,141 @@ __device__ int gpu_allocate(const SoA& s, int64_t i, uint64_t ex0, const DevPod&
     *reason = required ? KE_REASON_DS_INSUFFICIENT_TOPOLOGY_SCOPED : KE_REASON_DS_INSUFFICIENT_GPU_TOPOLOGY;
     return KE_CODE_UNSCHEDULABLE;
   }
-  if (__builtin_popcount(g.dflt) >= want) return 0;  // defaultAllocateDevices (minors picked by the caller)
+  if (__builtin_popcount(g.dflt) >= want) {  // defaultAllocateDevices
+    if (select) *minors = default_pick(g.dflt, want, dscore);
+    return 0;
+  }
   *reason = KE_REASON_DS_INSUFFICIENT_GPU;
   return KE_CODE_UNSCHEDULABLE;
 }
 
+// AutopilotAllocator.numaNodes (nil = off): the NUMA affinity the devices are restricted to
+struct DsAff {
+  bool on;
+  uint32_t mask;  // NUMA ids
+};
+// filterNodeDevice's device choice (device_allocator.go:137-166): with numaNodes set, a device needs a
+// topology whose NodeID is -1 or in the affinity (DSM_DNUMA codes: 0 none, 1 + NodeID, 9 = -1)
+__device__ __forceinline__ uint32_t ds_allowed(const SoA& s, int64_t i, int t, DsAff a) {
+  if (!a.on) return 0xFFFFu;
+  const uint64_t w = dsmask(s, DSM_DNUMA + t, i);
+  uint32_t m = 0;
+#pragma unroll
+  for (int q = 0; q < 16; q++) {
+    const uint32_t c = (uint32_t)(w >> (4 * q)) & 15u;
+    const bool ok = c == DN_ANY || (c >= 1 && c <= 8 && ((a.mask >> (c - 1)) & 1u));
+    m |= (uint32_t)ok << q;
+  }
+  return m;
+}
+
+// One device type of the filtered nodeDevice (nodeDevice.filter, device_cache.go:360-415): the type is kept
+// when some instance has a free (over every instance) and some instance passes the affinity; the masks of
+// the passing instances, their summed total / free' (scoreNode), scoreDevice per minor (`score`, optional),
+// and the used hash over realUsed (allocator_gpu.go:59-70: the original used minors outside the refined
+// total, the refined used' inside).
+__device__ __forceinline__ bool ds_type_view(const SoA& s, int64_t i, int t, const uint64_t msk[4], const DevPod& p,
+                                             const KArgs& k, DsAff a, GpuMasks& g, int64_t (&tot)[3],
+                                             int64_t (&fre)[3], int64_t* score) {
+  const int nk = DS_NK[t];
+  uint64_t ex = (msk[DSM_EXISTS] >> (16 * t)) & 0xFFFF;
+  const uint32_t allowed = (uint32_t)ex & ds_allowed(s, i, t, a);
+  g.minors = (uint32_t)ex;
+  g.total = g.used = g.sat = g.dflt = 0;
+  uint32_t orig_used = 0, used_p = 0, tot_m = 0, sat = 0, dflt = 0;
+  bool present = false;
+#pragma unroll
+  for (int q = 0; q < 3; q++) tot[q] = fre[q] = 0;
+  while (ex) {
+    const int m = __builtin_ctzll(ex);
+    ex &= ex - 1;
+    bool hu = false;
+#pragma unroll
+    for (int q = 0; q < 3; q++) hu = hu || (q < nk && ((msk[ds_hu_word(t)] >> ds_hu_bit(t, m, q)) & 1));
+    orig_used |= (uint32_t)hu << m;
+    DsInst d;
+    ds_instance(s, i, t, m, msk, d);
+    const bool fz = ds_free_zero(d);
+    present = present || !fz;
+    if (!((allowed >> m) & 1u)) continue;
+    const bool leq = ds_leq(d, p, t), tnz = ds_total_nz(d);
+    dflt |= (uint32_t)(!fz && leq) << m;
+    sat |= (uint32_t)(leq && tnz) << m;
+    tot_m |= (uint32_t)tnz << m;
+    used_p |= (uint32_t)d.used_nz << m;
+    int64_t tv[3], fv[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      tv[q] = ((d.th >> q) & 1) ? d.tv[q] : 0;
+      fv[q] = ((d.fh >> q) & 1) ? d.fv[q] : 0;
+      tot[q] += tv[q];
+      fre[q] += fv[q];
+    }
+    if (score) score[m] = ds_weighted(k, t, tv, fv, p);  // scoreDevice
+  }
+  present = present && allowed != 0;
+  if (present) {
+    g.dflt = dflt;
+    g.sat = sat;
+    g.total = tot_m;
+    g.used = (orig_used & ~allowed) | used_p;
+  } else {
+    g.used = orig_used;
+  }
+  return present;
+}
+
+// AutopilotAllocator.Allocate (device_allocator.go:87-135) on the devices the affinity leaves: Prepare (a
+// requested type without devices in the cache), then every requested type in the fixed order GPU, RDMA,
+// FPGA.  *gpu = the GPU minors (no scorer) when `gpu` is given.
+__device__ int ds_try_allocate(const SoA& s, int64_t i, const DevPod& p, const KArgs& k, DsAff a, uint32_t* gpu,
+                               int* reason) {
+  uint64_t msk[4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) msk[w] = dsmask(s, w, i);
+  for (int t = 0; t < 3; t++)
+    if (p.ds_cnt[t] && !((msk[DSM_EXISTS] >> (16 * t)) & 0xFFFF)) {
+      *reason = KE_REASON_DS_INSUFFICIENT_GPU + t;
+      return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    }
+  if (gpu) *gpu = 0;
+  for (int t = 0; t < 3; t++) {
+    if (!p.ds_cnt[t]) continue;
+    GpuMasks g;
+    int64_t tot[3], fre[3];
+    ds_type_view(s, i, t, msk, p, k, a, g, tot, fre, nullptr);
+    if (t == KE_DEV_GPU) {
+      uint32_t take = 0;
+      int why = 0;
+      const int st = gpu_allocate(s, i, msk[DSM_EXISTS], p, g, gpu != nullptr, nullptr, &take, &why);
+      if (st) {
+        *reason = why;
+        return st;
+      }
+      if (gpu) *gpu = take;
+    } else if (__builtin_popcount(g.dflt) < p.ds_cnt[t]) {
+      *reason = KE_REASON_DS_INSUFFICIENT_GPU + t;
+      return KE_CODE_UNSCHEDULABLE;
+    }
+  }
+  return 0;
+}
+
 // Filter (Prepare + per-type allocation feasibility) and raw Score of DeviceShare for a pod with PF_DS on
-// a node with a cache entry.  Types in the fixed order GPU, RDMA, FPGA.
-__device__ __noinline__ void ds_filter_score(const SoA& s, int64_t i, const DevPod& p, const KArgs& k, EvalOut& o) {
+// a node with a cache entry.  `a`: the affinity the topology manager stored (Score and Reserve read it;
+// Filter then passes: topology_hint.go Allocate already ran).  Types in the fixed order GPU, RDMA, FPGA.
+__device__ __noinline__ void ds_filter_score(const SoA& s, int64_t i, const DevPod& p, const KArgs& k, EvalOut& o,
+                                             bool stored, DsAff a) {
   uint64_t msk[4];
 #pragma unroll
   for (int w = 0; w < 4; w++) msk[w] = dsmask(s, w, i);
   for (int t = 0; t < 3; t++)  // AutopilotAllocator.Prepare: a requested type without devices
     if (p.ds_cnt[t] && !((msk[DSM_EXISTS] >> (16 * t)) & 0xFFFF)) {
-      o.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
-      o.reason = (uint8_t)(KE_REASON_DS_INSUFFICIENT_GPU + t);
-      return;
+      if (!stored) {
+        o.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+        o.reason = (uint8_t)(KE_REASON_DS_INSUFFICIENT_GPU + t);
+      }
+      return;  // Score: 0 with an error status
     }
   int64_t raw = 0;
   // GPUs on a node without partition table / honor policy / topology tree, for a pod without a partition
@@ -567,56 +724,34 @@ __device__ __noinline__ void ds_filter_score(const SoA& s, int64_t i, const DevP
                            !(p.flags & (PF_GPU_PART_SPEC | 7u * PF_GPU_SCOPE0));
   for (int t = 0; t < 3; t++) {
     if (!p.ds_cnt[t]) continue;
-    uint64_t ex = (msk[DSM_EXISTS] >> (16 * t)) & 0xFFFF;
-    const bool masks = t == KE_DEV_GPU && !gpu_default;
     GpuMasks g;
-    g.minors = (uint32_t)ex;
-    g.total = g.used = g.sat = g.dflt = 0;
-    bool present = false;
-    int64_t tot[3] = {0, 0, 0}, fre[3] = {0, 0, 0};
-    while (ex) {
-      const int m = __builtin_ctzll(ex);
-      ex &= ex - 1;
-      DsInst d;
-      ds_instance(s, i, t, m, msk, d);
-      const bool leq = ds_leq(d, p, t), fz = ds_free_zero(d);
-      g.dflt |= (uint32_t)(!fz && leq) << m;
-      if (masks) {
-        present = present || !fz;
-        g.sat |= (uint32_t)(leq && ds_total_nz(d)) << m;
-        g.total |= (uint32_t)ds_total_nz(d) << m;
-        g.used |= (uint32_t)d.used_nz << m;
+    int64_t tot[3], fre[3];
+    const bool present = ds_type_view(s, i, t, msk, p, k, a, g, tot, fre, nullptr);
+    if (!stored) {
+      int st = 0, reason = KE_REASON_DS_INSUFFICIENT_GPU + t;
+      if (t == KE_DEV_GPU && !gpu_default) {
+        uint32_t unused;
+        st = gpu_allocate(s, i, msk[DSM_EXISTS], p, g, false, nullptr, &unused, &reason);
+      } else if (__builtin_popcount(g.dflt) < p.ds_cnt[t]) {  // defaultAllocateDevices: "Insufficient <type> devices"
+        st = KE_CODE_UNSCHEDULABLE;
       }
-#pragma unroll
-      for (int key = 0; key < 3; key++) {
-        tot[key] += ((d.th >> key) & 1) ? d.tv[key] : 0;
-        fre[key] += ((d.fh >> key) & 1) ? d.fv[key] : 0;
+      if (st) {
+        o.status = (uint8_t)st;
+        o.reason = (uint8_t)reason;
+        return;
       }
     }
-    if (!present) g.total = g.sat = 0;  // the filtered nodeDevice dropped the type
-    int st = 0, reason = KE_REASON_DS_INSUFFICIENT_GPU + t;
-    if (masks) {
-      uint32_t unused;
-      st = gpu_allocate(s, i, msk[DSM_EXISTS], p, g, false, nullptr, &unused, &reason);
-    } else if (__builtin_popcount(g.dflt) < p.ds_cnt[t]) {  // defaultAllocateDevices: "Insufficient <type> devices"
-      st = KE_CODE_UNSCHEDULABLE;
-    }
-    if (st) {
-      o.status = (uint8_t)st;
-      o.reason = (uint8_t)reason;
-      return;
-    }
-    raw += ds_weighted(k, t, tot, fre, p);  // resourceAllocationScorer.scoreNode
+    if (present) raw += ds_weighted(k, t, tot, fre, p);  // resourceAllocationScorer.scoreNode
   }
   o.ds = (int16_t)raw;
 }
 
-// DeviceShare Reserve (plugin.go:426-492): per type the allocator's minors -- GPUs through GPUAllocator
-// (partition, topology scope, then default), other types defaultAllocateDevices: instances in
-// (scoreDevice desc, minor asc) order (device_resources.go:171-208), the first ds_cnt satisfiable.  The
-// allocation (request + fillGPUTotalMem, devicehandler_gpu.go:98-133) is added to `used` in the SoA
-// (updateCacheUsed).  Returns the minors mask (bit 16*type + minor).
-__device__ __noinline__ uint64_t ds_reserve(const SoA& s, int64_t i, const DevPod& p, const KArgs& k) {
+// DeviceShare Reserve (plugin.go:426-492) on the devices the affinity leaves: per type the allocator's
+// minors -- GPUs through GPUAllocator (partition, topology scope, then default), other types
+// defaultAllocateDevices -- with the plugin's scorer.  The allocation (request + fillGPUTotalMem,
+// devicehandler_gpu.go:98-133) is added to `used` in the SoA (updateCacheUsed).  Returns the minors mask
+// (bit 16*type + minor).
+__device__ __noinline__ uint64_t ds_reserve(const SoA& s, int64_t i, const DevPod& p, const KArgs& k, DsAff a) {
   uint64_t msk[4], out = 0;
 #pragma unroll
   for (int w = 0; w < 4; w++) msk[w] = dsmask(s, w, i);
@@ -625,48 +760,14 @@ __device__ __noinline__ uint64_t ds_reserve(const SoA& s, int64_t i, const DevPo
     const int nk = DS_NK[t];
     int64_t score[DS_MINORS];
     GpuMasks g;
-    g.minors = g.total = g.used = g.sat = g.dflt = 0;
-    bool present = false;
-    uint64_t ex = (msk[DSM_EXISTS] >> (16 * t)) & 0xFFFF;
-    g.minors = (uint32_t)ex;
-    while (ex) {
-      const int m = __builtin_ctzll(ex);
-      ex &= ex - 1;
-      DsInst d;
-      ds_instance(s, i, t, m, msk, d);
-      const bool leq = ds_leq(d, p, t), fz = ds_free_zero(d);
-      present = present || !fz;
-      g.dflt |= (uint32_t)(!fz && leq) << m;
-      g.sat |= (uint32_t)(leq && ds_total_nz(d)) << m;
-      g.total |= (uint32_t)ds_total_nz(d) << m;
-      g.used |= (uint32_t)d.used_nz << m;
-      int64_t tot[3], fre[3];
-#pragma unroll
-      for (int key = 0; key < 3; key++) {
-        tot[key] = ((d.th >> key) & 1) ? d.tv[key] : 0;
-        fre[key] = ((d.fh >> key) & 1) ? d.fv[key] : 0;
-      }
-      score[m] = ds_weighted(k, t, tot, fre, p);  // scoreDevice (total = the cache total of the minor)
-    }
-    if (!present) g.total = g.sat = 0;
+    int64_t tot[3], fre[3];
+    ds_type_view(s, i, t, msk, p, k, a, g, tot, fre, score);
     uint32_t take = 0;
-    bool by_default = true;
     if (t == KE_DEV_GPU) {
       int reason = 0;
-      if (gpu_allocate(s, i, msk[DSM_EXISTS], p, g, true, score, &take, &reason) != 0) take = 0;
-      by_default = take == 0;  // passed Filter: only the default stage leaves the minors to pick here
-    }
-    if (by_default) {
-      uint32_t ok = g.dflt;
-      for (int c = 0; c < p.ds_cnt[t] && ok; c++) {
-        int best = -1;
-        for (uint32_t r = ok; r; r &= r - 1) {
-          const int m = __builtin_ctz(r);
-          if (best < 0 || score[m] > score[best]) best = m;  // ascending minors: ties keep the lower
-        }
-        ok &= ~(1u << best);
-        take |= 1u << best;
-      }
+      if (gpu_allocate(s, i, msk[DSM_EXISTS], p, g, true, score, &take, &reason) != 0) take = 0;  // passed Filter
+    } else {
+      take = default_pick(g.dflt, p.ds_cnt[t], score);
     }
     for (uint32_t rest = take; rest; rest &= rest - 1) {
       const int best = __builtin_ctz(rest);
@@ -702,28 +803,100 @@ __device__ __noinline__ uint64_t ds_reserve(const SoA& s, int64_t i, const DevPo
   return out;
 }
 
+// ---- DeviceShare as a NUMA topology hint provider (topology_hint.go:38-236) ----------------------------
+// The hints of one pod on one node, as sets over mask values of the device NUMA ids: F = the feasible
+// masks, S = those whose GPU allocation equals the one on every device NUMA node (score 500); preferred =
+// popcount == dmin; one identical list per requested device type (`copies`).
+struct DsHints {
+  uint8_t status, reason;  // a provider error (Admit reason)
+  bool none;               // no preference (nil hints)
+  uint8_t copies, dmin;
+  uint64_t F[4], S[4];
+};
+__device__ __forceinline__ bool bit256(const uint64_t (&b)[4], uint32_t m) {
+  const uint64_t w = m < 64 ? b[0] : m < 128 ? b[1] : m < 192 ? b[2] : b[3];
+  return (w >> (m & 63u)) & 1u;
+}
+__device__ __forceinline__ void set256(uint64_t (&b)[4], uint32_t m) {
+  const uint64_t bit = 1ull << (m & 63u);
+  const int w = (int)(m >> 6);
+#pragma unroll
+  for (int q = 0; q < 4; q++) b[q] |= q == w ? bit : 0ull;
+}
+
+// generateTopologyHints (topology_hint.go:119-212) for a pod with PF_DS on a node with a device cache
+__device__ __noinline__ void ds_numa_hints(const SoA& s, int64_t i, const DevPod& p, const KArgs& k, DsHints& h) {
+  h.status = h.reason = 0;
+  h.none = true;
+  h.copies = h.dmin = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) h.F[q] = h.S[q] = 0;
+  if (k.flags & AF_DS_NO_NUMA) return;
+  uint32_t ids = 0;  // numaTopology.nodes: NodeIDs of devices with a topology, -1 excluded
+#pragma unroll
+  for (int t = 0; t < 3; t++) {
+    const uint64_t w = dsmask(s, DSM_DNUMA + t, i);
+    for (int q = 0; q < 16; q++) {
+      const uint32_t c = (uint32_t)(w >> (4 * q)) & 15u;
+      if (c >= 1 && c <= 8) ids |= 1u << (c - 1);
+    }
+  }
+  if (!ids) return;  // an empty hint map
+  const uint64_t ex = dsmask(s, DSM_EXISTS, i);
+  for (int t = 0; t < 3; t++)  // Prepare fails on every mask alike
+    if (p.ds_cnt[t] && !((ex >> (16 * t)) & 0xFFFF)) {
+      h.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+      h.reason = (uint8_t)(KE_REASON_DS_INSUFFICIENT_GPU + t);
+      return;
+    }
+  // one mask: calcTotalDevicesByNUMA's count check, then the trial allocation
+  auto try_mask = [&](uint32_t m, uint32_t* gpu, int* why) -> int {
+#pragma unroll
+    for (int t = 0; t < 3; t++) {
+      if (!p.ds_cnt[t]) continue;
+      const uint64_t w = dsmask(s, DSM_DNUMA + t, i);
+      int cnt = 0;
+      for (int q = 0; q < 16; q++) {
+        const uint32_t c = (uint32_t)(w >> (4 * q)) & 15u;
+        cnt += (c >= 1 && c <= 8 && ((m >> (c - 1)) & 1u)) ? 1 : 0;
+      }
+      if (cnt > 0 && cnt < p.ds_cnt[t]) {
+        *why = KE_REASON_DS_INSUFFICIENT_NUMA_SCOPED;
+        return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+      }
+    }
+    return ds_try_allocate(s, i, p, k, DsAff{true, m}, gpu, why);
+  };
+  uint32_t best_gpu = 0;
+  int why = 0;
+  const int full = try_mask(ids, &best_gpu, &why);  // statusUnsatisfied / bestAllocationResult
+  if (full) {
+    h.status = (uint8_t)full;
+    h.reason = (uint8_t)why;
+    return;
+  }
+  int dmin = 9;
+  for (int e = 0; e < 255; e++) {
+    const uint32_t m = NUMA_ORDER[e];
+    if (m & ~ids) continue;
+    uint32_t gpu = 0;
+    int w2 = 0;
+    if (try_mask(m, &gpu, &w2)) continue;
+    set256(h.F, m);
+    if (gpu == best_gpu) set256(h.S, m);
+    dmin = min(dmin, __popc(m));
+  }
+  h.none = false;
+  h.dmin = (uint8_t)dmin;
+  h.copies = (uint8_t)((p.ds_cnt[0] != 0) + (p.ds_cnt[1] != 0) + (p.ds_cnt[2] != 0));
+}
+
 // ---------------------------------------------------------------------------------------------
 // NodeNUMAResource under a NUMA topology policy, non-cpuset pods: hint generation
 // (resource_manager.go:525-622), topologymanager merge + admit (policy*.go), allocation by the merged
 // hint (tryBestToDistributeEvenly, resource_manager.go:260-314) and the NUMA-scope score
 // (scoring.go:101-119).  The zones of node i are read from the NUMA SoA once per lane into registers.
 // ---------------------------------------------------------------------------------------------
-// bitmask.IterateBitMasks order over NUMA ids 0..7: by popcount, then lexicographic on the ascending
-// id list.  Restricted to the subsets of a node's zones it is the order over those zones.
-__constant__ uint8_t NUMA_ORDER[255] = {
-    1, 2, 4, 8, 16, 32, 64, 128, 3, 5, 9, 17, 33, 65, 129, 6, 10, 18, 34, 66, 130, 12, 20, 36, 68, 132, 24,
-    40, 72, 136, 48, 80, 144, 96, 160, 192, 7, 11, 19, 35, 67, 131, 13, 21, 37, 69, 133, 25, 41, 73, 137,
-    49, 81, 145, 97, 161, 193, 14, 22, 38, 70, 134, 26, 42, 74, 138, 50, 82, 146, 98, 162, 194, 28, 44, 76,
-    140, 52, 84, 148, 100, 164, 196, 56, 88, 152, 104, 168, 200, 112, 176, 208, 224, 15, 23, 39, 71, 135,
-    27, 43, 75, 139, 51, 83, 147, 99, 163, 195, 29, 45, 77, 141, 53, 85, 149, 101, 165, 197, 57, 89, 153,
-    105, 169, 201, 113, 177, 209, 225, 30, 46, 78, 142, 54, 86, 150, 102, 166, 198, 58, 90, 154, 106, 170,
-    202, 114, 178, 210, 226, 60, 92, 156, 108, 172, 204, 116, 180, 212, 228, 120, 184, 216, 232, 240, 31,
-    47, 79, 143, 55, 87, 151, 103, 167, 199, 59, 91, 155, 107, 171, 203, 115, 179, 211, 227, 61, 93, 157,
-    109, 173, 205, 117, 181, 213, 229, 121, 185, 217, 233, 241, 62, 94, 158, 110, 174, 206, 118, 182, 214,
-    230, 122, 186, 218, 234, 242, 124, 188, 220, 236, 244, 248, 63, 95, 159, 111, 175, 207, 119, 183, 215,
-    231, 123, 187, 219, 235, 243, 125, 189, 221, 237, 245, 249, 126, 190, 222, 238, 246, 250, 252, 127, 191,
-    223, 239, 247, 251, 253, 254, 255};
-__constant__ uint8_t NUMA_OFF[10] = {0, 0, 8, 36, 92, 162, 218, 246, 254, 255};  // first entry of each size
 
 struct NumaNode {
   uint32_t zm, ch[2], ak[2];  // zones present, capacity keys, allocated keys per resource (bit = NUMA id)
@@ -1109,6 +1282,175 @@ __device__ __forceinline__ void numa_present_lack(const NumaNode& v, const DevPo
   }
 }
 
+// mergeFilteredHints over every permutation of the provider lists (policy.go:198-299) when no merged hint
+// is preferred: lists[l][0..len[l]) hold masks in order (0 = a nil-affinity entry, `unsat` bit: the
+// unsatisfied entry of a resource without hints); DeviceShare lists carry their hint scores via `dsS`.
+// Exact fold in permutation order; more than DS_MERGE_BUDGET permutations sets KERR_DS_MERGE.
+constexpr int64_t DS_MERGE_BUDGET = 1 << 20;
+struct MergeLists {
+  uint8_t m[5][255];
+  uint8_t ds[5];      // the list is a DeviceShare list (scores from S)
+  uint8_t unsat[5];   // the list is the unsatisfied nil entry
+  int len[5];
+  int n;
+};
+__device__ __noinline__ uint32_t merge_all_permutations(const SoA& s, int64_t i, const NumaNode& v, const DevPod& sp,
+                                                         const KArgs& k, const MergeLists& L, const DsHints& dh,
+                                                         bool excl) {
+  int64_t total = 1;
+  for (int l = 0; l < L.n; l++) total *= L.len[l];
+  if (total > DS_MERGE_BUDGET) {
+    __hip_atomic_fetch_or(s.kerr, KERR_DS_MERGE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v.zm;
+  }
+  const uint32_t all = v.zm;
+  uint32_t best = all;
+  int32_t bsc = 0;
+  bool bun = false;
+  int idx[5] = {0, 0, 0, 0, 0};
+  for (int64_t it = 0; it < total; it++) {
+    uint32_t mg = all;
+    int maxn = 0;
+    bool have = false, un = false;
+    for (int l = 0; l < L.n; l++) {
+      const uint32_t m = L.m[l][idx[l]];
+      un = un || L.unsat[l];
+      if (m) {
+        have = true;
+        mg &= m;
+        maxn = max(maxn, __popc(m));
+      }
+    }
+    un = un || (have && maxn != __popc(mg));
+    if (mg) {
+      (void)excl;  // every merged hint is non-preferred here: the exclusive check changes nothing
+      int32_t sc = 0;
+      for (int l = 0; l < L.n; l++) {
+        const uint32_t m = L.m[l][idx[l]];
+        if (!m || m != mg) continue;
+        sc += L.ds[l] ? (bit256(dh.S, m) ? 500 : 0) : numa_hint_score(s, i, v, m, sp, k);
+      }
+      if (narrower(mg, best) || (__popc(mg) == __popc(best) && sc > bsc)) {
+        best = mg;
+        bsc = sc;
+        bun = un;
+      }
+    }
+    for (int l = L.n - 1; l >= 0; l--) {  // next permutation (last list fastest)
+      if (++idx[l] < L.len[l]) break;
+      idx[l] = 0;
+    }
+  }
+  return bun ? all : best;
+}
+
+// topologymanager Admit with DeviceShare's hint lists (topology_hint.go:38-212, manager.go:64-129): the
+// provider lists in order [cpu, memory] (NodeNUMAResource; one preferred any-NUMA hint when it has none),
+// then `copies` identical DeviceShare lists.  A merged hint is preferred only on the diagonal (every list
+// holds the mask, preferred), so the preferred candidates are scanned in IterateBitMasks order with
+// mergeFilteredHints' replacement rule; without one, BestEffort folds every permutation.  The NUMA
+// allocation on the result follows; DeviceShare's Allocate is the caller's.
+template <bool CS>
+__device__ __noinline__ NumaPick numa_admit_ds(const SoA& s, int64_t i, int policy, const NumaNode& v, const DevPod& p,
+                                               const KArgs& k, const NumaCs* cs, const DevPod* ps, const DsHints& dh) {
+  NumaPick o{KE_CODE_SUCCESS, KE_REASON_NONE, 0u};
+  const DevPod& sp = CS ? *ps : p;
+  if (dh.status) {  // the provider's error is an Admit reason (manager.go:110-125)
+    o.status = KE_CODE_UNSCHEDULABLE;
+    o.reason = dh.reason;
+    return o;
+  }
+  const bool excl = (p.flags & PF_NUMA_EXCL_REQ) != 0;
+  const uint32_t all = v.zm;
+  bool present[2];
+  uint32_t lack[2];
+  numa_present_lack(v, p, present, lack);
+  const int R = (int)present[0] + (int)present[1];
+  uint64_t L[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+  int minr[2] = {9, 9};
+  int64_t dummy[2][8];
+  for (int e = 0; e < 255; e++) {  // generateResourceHints: the feasible masks per resource
+    const uint32_t m = NUMA_ORDER[e];
+    if (m & ~all) continue;
+    const bool in0 = present[0] && !(m & lack[0]), in1 = present[1] && !(m & lack[1]);
+    if (!in0 && !in1) continue;
+    if (!numa_distribute<false, CS>(v, m, p, nullptr, dummy, cs)) continue;
+    if (in0) set256(L[0], m), minr[0] = min(minr[0], __popc(m));
+    if (in1) set256(L[1], m), minr[1] = min(minr[1], __popc(m));
+  }
+  const bool single = policy == KE_NUMA_POLICY_SINGLE_NUMA_NODE, restricted = policy == KE_NUMA_POLICY_RESTRICTED;
+  const bool empty0 = present[0] && minr[0] == 9, empty1 = present[1] && minr[1] == 9;  // filterProvidersHints reasons
+  const int copies = dh.copies;
+  uint32_t best = all;
+  int32_t bsc = 0;
+  bool found = false, bun = false;  // bun: the best merged hint is narrower than its masks (unsatisfied)
+  if (!empty0 && !empty1) {
+    for (int e = 0; e < 255; e++) {
+      const uint32_t m = NUMA_ORDER[e];
+      if (!bit256(dh.F, m) || __popc(m) != dh.dmin) continue;  // DeviceShare: preferred = the minimal size
+      if (single && __popc(m) != 1) continue;                   // filterSingleNumaHints
+      bool cand = true;
+#pragma unroll
+      for (int r = 0; r < 2; r++)
+        if (present[r]) cand = cand && !(m & ~all) && bit256(L[r], m) && (restricted || __popc(m) == minr[r]);
+      if (!cand) continue;
+      const uint32_t mg = m & all;  // mergePermutation ANDs the default affinity
+      if (!mg || !exclusive_ok(v, mg, excl)) continue;
+      const int32_t sc = (R ? R * numa_hint_score(s, i, v, m, sp, k) : 0) + (mg == m && bit256(dh.S, m) ? 500 * copies : 0);
+      if (!found || narrower(mg, best) || (__popc(mg) == __popc(best) && sc > bsc)) {
+        best = mg;
+        bsc = sc;
+        found = true;
+        bun = mg != m;  // a hint on NUMA ids without a zone: maxNUMANodeNum != merged count
+      }
+    }
+  }
+  if (found && bun && policy == KE_NUMA_POLICY_BEST_EFFORT) best = all;  // policy_best_effort.go: unsatisfied -> any
+  if (!found) {
+    if (policy != KE_NUMA_POLICY_BEST_EFFORT) {
+      o.status = KE_CODE_UNSCHEDULABLE;
+      o.reason = KE_REASON_NUMA_HINT_UNALIGNED;
+      return o;
+    }
+    MergeLists ml;
+    ml.n = 0;
+    auto add_set = [&](const uint64_t (&b)[4], bool ds) {
+      int n = 0;
+      for (int e = 0; e < 255; e++)
+        if (bit256(b, NUMA_ORDER[e])) ml.m[ml.n][n++] = NUMA_ORDER[e];
+      ml.len[ml.n] = n;
+      ml.ds[ml.n] = ds;
+      ml.unsat[ml.n] = 0;
+      ml.n++;
+    };
+    if (R == 0) {
+      ml.m[0][0] = 0, ml.len[0] = 1, ml.ds[0] = 0, ml.unsat[0] = 0, ml.n = 1;
+    } else {
+      for (int r = 0; r < 2; r++) {
+        if (!present[r]) continue;
+        if (r == 0 ? empty0 : empty1) {
+          ml.m[ml.n][0] = 0, ml.len[ml.n] = 1, ml.ds[ml.n] = 0, ml.unsat[ml.n] = 1, ml.n++;
+        } else {
+          add_set(L[r], false);
+        }
+      }
+    }
+    for (int c = 0; c < copies; c++) add_set(dh.F, true);
+    best = merge_all_permutations(s, i, v, sp, k, ml, dh, excl);
+  }
+  o.aff = (single && best == all) ? 0u : best;
+  // topologymanager allocateResources -> NodeNUMAResource.Allocate (tryAllocateFromNode with the hint)
+  int64_t dummy2[2][8];
+  bool split = true;
+  const bool fits = o.aff ? numa_distribute<false, CS>(v, o.aff, p, nullptr, dummy2, cs, &split)
+                          : (!CS || cs->total >= cs->num);
+  if (!fits) {
+    o.status = KE_CODE_UNSCHEDULABLE;
+    o.reason = split ? KE_REASON_NUMA_INSUFFICIENT_CPUS : KE_REASON_NUMA_INSUFFICIENT_RESOURCES;
+  }
+  return o;
+}
+
 // FilterByNUMANode + RunNUMATopologyManagerAdmit for a pod whose requests are not all zero, under
 // the merged topology `policy` (node / pod, util.go:58-74).  DEFER: a BestEffort pair without a
 // preferred merged hint returns STATUS_DEFERRED instead of running the full merge here (one lane
@@ -1119,7 +1461,8 @@ __device__ __forceinline__ void numa_present_lack(const NumaNode& v, const DevPo
 template <bool DEFER, bool FB_AFF = false, bool CS = false>
 __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t nf, int policy, const NumaNode& v,
                                                const DevPod& p, const KArgs& k, uint32_t fb_aff = 0,
-                                               const NumaCs* cs = nullptr, const DevPod* ps = nullptr) {
+                                               const NumaCs* cs = nullptr, const DevPod* ps = nullptr,
+                                               const DsHints* dh = nullptr) {
   NumaPick o{KE_CODE_SUCCESS, KE_REASON_NONE, 0u};
   const DevPod& sp = CS ? *ps : p;
   // Allocate on the chosen affinity (topologymanager allocateResources -> tryAllocateFromNode)
@@ -1144,6 +1487,7 @@ __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t
     o.reason = KE_REASON_NUMA_HINT_UNALIGNED;
     return o;
   }
+  if (dh && (dh->status || !dh->none)) return numa_admit_ds<CS>(s, i, policy, v, p, k, cs, ps, *dh);
   const uint32_t all = v.zm;
   bool present[2];
   uint32_t lack[2];
@@ -1421,44 +1765,57 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
   // ---- NodeNUMAResource.Filter under a NUMA topology policy: FilterByNUMANode + topologymanager Admit
   const bool npol = NUMA && !(p.flags & PF_NUMA_SKIP) && eff_pol != KE_NUMA_POLICY_NONE;
   int32_t npol_score = 0;
+  // DeviceShare is a second hint provider for a pod with device requests on a node with a device cache
+  // (topology_hint.go:38-58); such a pair is never deferred (its batch runs no k_numa_fallback)
+  const bool ds_here = DS && (p.flags & PF_DS) && (nf & NF_DS_CACHE);
+  bool stored = false;  // the topology manager stored an affinity for the node
   if (npol && o.status == KE_CODE_SUCCESS) {
+    DsHints dh;
+    dh.status = 0;
+    dh.none = true;
+    if (ds_here) ds_numa_hints(s, i, p, k, dh);
+    const DsHints* dhp = ds_here ? &dh : nullptr;
+    NumaPick pk;
     if (CPU && rcb > 0) {  // a binding pod: cpuset hints and allocation (resource_manager.go:166-192,353-459)
       const NumaCs cs = numa_cs_load(s, i, nf, p);
       DevPod ps = p;  // options.requests: cpu amplified (plugin.go:634-640)
       ps.req[0] = amplify_bits(p.req[0], s.cs[CS_RS * s.stride + i]);
       NumaNode tv = nv;
       numa_trim(tv, cs);
-      const NumaPick pk = numa_admit<DEFER, FB_AFF, true>(s, i, nf, eff_pol, tv, p, k, fb_aff, &cs, &ps);
+      pk = ds_here ? numa_admit<false, false, true>(s, i, nf, eff_pol, tv, p, k, 0u, &cs, &ps, dhp)
+                   : numa_admit<DEFER, FB_AFF, true>(s, i, nf, eff_pol, tv, p, k, fb_aff, &cs, &ps);
       if (DEFER && pk.status == STATUS_DEFERRED) {
         o.status = STATUS_DEFERRED;
         o.total = -1;
         return o;
       }
-      if (pk.status != KE_CODE_SUCCESS) {
-        o.status = pk.status;
-        o.reason = pk.reason;
-      } else {
-        o.aff = (uint8_t)pk.aff;
-        npol_score = numa_policy_score<true>(s, i, tv, pk.aff, p, k, n, &cs, &ps);
-      }
+      if (pk.status == KE_CODE_SUCCESS) npol_score = numa_policy_score<true>(s, i, tv, pk.aff, p, k, n, &cs, &ps);
     } else {
-      const NumaPick pk = numa_admit<DEFER, FB_AFF>(s, i, nf, eff_pol, nv, p, k, fb_aff);
+      pk = ds_here ? numa_admit<false>(s, i, nf, eff_pol, nv, p, k, 0u, nullptr, nullptr, dhp)
+                   : numa_admit<DEFER, FB_AFF>(s, i, nf, eff_pol, nv, p, k, fb_aff);
       if (DEFER && pk.status == STATUS_DEFERRED) {
         o.status = STATUS_DEFERRED;
         o.total = -1;
         return o;
       }
-      if (pk.status != KE_CODE_SUCCESS) {
-        o.status = pk.status;
-        o.reason = pk.reason;
-      } else {
-        o.aff = (uint8_t)pk.aff;
-        npol_score = numa_policy_score(s, i, nv, pk.aff, p, k, n);
-      }
+      if (pk.status == KE_CODE_SUCCESS) npol_score = numa_policy_score(s, i, nv, pk.aff, p, k, n);
+    }
+    if (pk.status == KE_CODE_SUCCESS && ds_here && !(k.flags & AF_DS_NO_NUMA)) {
+      int why = 0;  // allocateResources -> DeviceShare.Allocate on the affinity (topology_hint.go:60-117)
+      const int st = ds_try_allocate(s, i, p, k, DsAff{pk.aff != 0, pk.aff}, nullptr, &why);
+      if (st) pk.status = (uint8_t)st, pk.reason = (uint8_t)why;
+    }
+    if (pk.status != KE_CODE_SUCCESS) {
+      o.status = pk.status;
+      o.reason = pk.reason;
+    } else {
+      o.aff = (uint8_t)pk.aff;
+      stored = true;
     }
   }
-  // ---- DeviceShare.Filter + raw Score  plugin.go:311-365, scoring.go:45-103
-  if (DS && o.status == KE_CODE_SUCCESS && (p.flags & PF_DS) && (nf & NF_DS_CACHE)) ds_filter_score(s, i, p, k, o);
+  // ---- DeviceShare.Filter + raw Score  plugin.go:311-365, scoring.go:45-103 (Filter passes and Score
+  // reads the devices of the affinity when the topology manager stored one)
+  if (ds_here && o.status == KE_CODE_SUCCESS) ds_filter_score(s, i, p, k, o, stored, DsAff{stored && o.aff != 0, o.aff});
   if (o.status != KE_CODE_SUCCESS) {
     o.total = -1;
     o.ds = 0;
@@ -2101,8 +2458,9 @@ __global__ __launch_bounds__(256) void k_argmax1(const uint16_t* __restrict__ sc
 
 // The deferred BestEffort pairs of an eval launch: one wavefront per pair computes mergeFilteredHints
 // over the full provider lists (numa_best_effort_fallback's result), then lane 0 evaluates the pair
-// with it.  Such a pair is never a DeviceShare pod (ke_capi rejects DeviceShare pods on NUMA-policy
-// nodes).  PARITY: write the parity matrices; else the batch score.
+// with it.  A DeviceShare pod's pair is deferred only on a node without a device cache (DeviceShare has
+// no hints there, Filter passes, Score is 0).  PARITY: write the parity matrices; else the batch score
+// (and for a DeviceShare singleton its raw score + 1 into `dsraw`, the max into `dsmax`).
 //   1. lanes split the 255 masks: hint lists L_cpu / L_mem (IterateBitMasks order) and hint scores;
 //   2. c* = the smallest popcount of a non-empty merged mask m1 & m2: only merged hints of that size
 //      can end as the best (the first one is narrower than anything before it, larger ones never
@@ -2119,7 +2477,7 @@ __global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __res
                                                       uint16_t* __restrict__ scores, int64_t score_stride, int n_nodes,
                                                       uint8_t* status, uint8_t* reason, int16_t* la, int16_t* numa,
                                                       int16_t* ds, int16_t* total, uint32_t* dsmax,
-                                                      uint8_t* __restrict__ aff_out) {
+                                                      uint8_t* __restrict__ aff_out, uint16_t* __restrict__ dsraw) {
   __shared__ int32_t s_score[256];     // hint score by mask value
   __shared__ uint8_t s_list[2][256];   // L_cpu / L_mem masks in order
   __shared__ uint16_t s_buf[64][256];  // per-row merged hints of size c*: M | k << 8 | unsatisfied << 10
@@ -2253,6 +2611,10 @@ __global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __res
       } else {
         scores[(int64_t)p * score_stride + i] = (uint16_t)(o.total + 1);
         if (CS && aff_out) aff_out[i] = o.aff;
+        if (dsraw && (pod.flags & PF_DS)) {  // a DeviceShare singleton: its raw score (0 here) for the normalisation
+          dsraw[i] = o.total >= 0 ? (uint16_t)(o.ds + 1) : (uint16_t)0;
+          if (o.total >= 0) atomicMax(dsmax, (uint32_t)o.ds + 1);
+        }
       }
     }
     __syncthreads();
@@ -2909,7 +3271,7 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
         // DeviceShare Reserve (a DeviceShare pod is alone in its batch: no later pod of the batch
         // reads the device state it patches)
         const uint32_t nfl = FAST ? fast.nflags : mine.flags;
-        al = DS && (pod.flags & PF_DS) && (nfl & NF_DS_CACHE) ? ds_reserve(s, my_node, pod, k) : 0ull;
+        al = DS && (pod.flags & PF_DS) && (nfl & NF_DS_CACHE) ? ds_reserve(s, my_node, pod, k, DsAff{false, 0u}) : 0ull;
         if (NUMA) {  // NodeNUMAResource Reserve: the zones of a NUMA-policy node
           int64_t* out16 = numa_alloc + (int64_t)(base + j) * 16;
           const int pol = pf_numa_policy(pod.flags) ? pf_numa_policy(pod.flags) : nf_numa_policy(mine.flags);
@@ -3263,24 +3625,35 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
     if (nsoa) numa_load(s, node, v);
     uint32_t got[2] = {0, 0};
     int64_t dist[2][8] = {{0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0, 0}};
+    // DeviceShare's hints join the Admit of a pod with device requests (topology_hint.go:38-58)
+    const bool ds_here = DS && (pod.flags & PF_DS) && (nf & NF_DS_CACHE);
+    bool stored = false;
+    uint32_t aff = 0;
     if (ok && npol) {  // the affinity the Filter's Admit stored and the allocation on it
-      // this rank evaluated the node: its eval stored the affinity (a feasible node admitted); else
-      // (a node of another shard) Admit runs here
-      const bool have = node >= eval_lo && node < eval_hi;
+      // this rank evaluated the node: its eval stored the affinity (a feasible node admitted, binding pods);
+      // else (a node of another shard, a DeviceShare pod) Admit runs here
+      const bool have = node >= eval_lo && node < eval_hi && !ds_here;
       NumaPick pk{KE_CODE_SUCCESS, KE_REASON_NONE, have ? (uint32_t)aff_in[node] : 0u};
+      DsHints dh;
+      dh.status = 0;
+      dh.none = true;
+      if (ds_here) ds_numa_hints(s, node, pod, k, dh);
+      const DsHints* dhp = ds_here ? &dh : nullptr;
       if (rcb) {
         const NumaCs cs = numa_cs_load(s, node, nf, pod);
         DevPod ps = pod;
         ps.req[0] = amplify_bits(pod.req[0], s.cs[CS_RS * s.stride + node]);
         NumaNode tv = v;
         numa_trim(tv, cs);
-        if (!have) pk = numa_admit<false, false, true>(s, node, nf, pol, tv, pod, k, 0u, &cs, &ps);
+        if (!have) pk = numa_admit<false, false, true>(s, node, nf, pol, tv, pod, k, 0u, &cs, &ps, dhp);
         if (pk.status == KE_CODE_SUCCESS && pk.aff) numa_distribute<true, true>(tv, pk.aff, pod, got, dist, &cs);
         ok = pk.status == KE_CODE_SUCCESS;
       } else {
-        if (!have) pk = numa_admit<false>(s, node, nf, pol, v, pod, k);
+        if (!have) pk = numa_admit<false>(s, node, nf, pol, v, pod, k, 0u, nullptr, nullptr, dhp);
         if (pk.status == KE_CODE_SUCCESS && pk.aff) numa_distribute<true>(v, pk.aff, pod, got, dist);
       }
+      stored = pk.status == KE_CODE_SUCCESS;
+      aff = pk.aff;
     }
     int cs_old[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // allocated CPUs per NUMA id before the pod
     if (nsoa && v.zm && s.cpu)
@@ -3288,6 +3661,14 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
         const CpuRec r = a.cpu[c];
         if ((r.flags & CR_VALID) && r.ref > 0 && r.numa < 8) cs_old[r.numa]++;
       }
+    // DeviceShare Reserve allocates on the stored affinity unless the alignment is disabled (plugin.go:452-466);
+    // with the alignment disabled nothing checked the devices of a NUMA-admitted node (Filter skipped,
+    // Allocate a no-op), so the allocation may fail: Reserve fails and every Reserve of the pod is undone
+    const DsAff da{stored && aff != 0 && !(k.flags & AF_DS_NO_NUMA), aff};
+    if (ok && ds_here && stored && (k.flags & AF_DS_NO_NUMA)) {  // elsewhere the Filter / Admit checked it
+      int why = 0;
+      ok = ds_try_allocate(s, node, pod, k, da, nullptr, &why) == KE_CODE_SUCCESS;
+    }
     if (ok && rcb) {
       const int64_t zcpu[8] = {dist[0][0], dist[0][1], dist[0][2], dist[0][3],
                                dist[0][4], dist[0][5], dist[0][6], dist[0][7]};
@@ -3318,7 +3699,7 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
         }
       }
       if (nsoa && v.zm) numa_reserve_cs(s, node, nf, v, got, dist, cs_old, cs_new, used, n_used, out16);
-      if (DS && (pod.flags & PF_DS) && (nf & NF_DS_CACHE)) alloc = ds_reserve(s, node, pod, k);
+      if (ds_here) alloc = ds_reserve(s, node, pod, k, da);
       out_node = (int32_t)node + global_offset;
       out_score = key_score(w);
       if (quota) quota_reserve_g(s, pod, qreq);  // ElasticQuota Reserve
@@ -3473,6 +3854,8 @@ int device_create(Context* ctx) {
   HIP_OK(hipMalloc(&d->d_stale_cnt, sizeof(int32_t) * 2 * MAX_BATCH));
   HIP_OK(hipMalloc(&d->d_trows, sizeof(int64_t) * MAX_BATCH * NUM_RW));
   HIP_OK(hipMalloc(&d->soa.rec, sizeof(int64_t) * NUM_RW * d->capacity));
+  HIP_OK(hipMalloc(&d->soa.kerr, sizeof(int32_t)));
+  HIP_OK(hipMemsetAsync(d->soa.kerr, 0, sizeof(int32_t), d->stream));
   HIP_OK(hipMemsetAsync(d->soa.rec, 0, sizeof(int64_t) * NUM_RW * d->capacity, d->stream));
   HIP_OK(hipMalloc(&d->d_tcnt, sizeof(int32_t)));
   if (d->capacity > (int64_t)CHG_LDS_WORDS * 32) {  // zero between batches (each replay clears its bits)
@@ -3498,7 +3881,7 @@ void device_destroy(Context* ctx) {
                   d->d_dsraw,   d->d_dsmax,  d->d_devalloc,   d->d_dsrows,       d->soa.nf,   d->soa.nm,
                   d->d_numaalloc, d->d_numarows, d->d_defer, d->d_defer_cnt, d->soa.cs, d->soa.cpu,
                   d->d_cpurows, d->d_cpusets, d->d_aff, d->soa.qt, d->soa.qm, d->d_sched, d->d_stale,
-                  d->d_stale_cnt, d->d_trows, d->d_tcnt, d->d_chg, d->soa.rec, d->soa.pt};
+                  d->d_stale_cnt, d->d_trows, d->d_tcnt, d->d_chg, d->soa.rec, d->soa.pt, d->soa.kerr};
   if (d->estream) (void)hipStreamSynchronize(d->estream);
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -3846,6 +4229,7 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
   int16_t* d_total = d_ds + M;
   uint32_t* d_dsmax = d->d_best + P;
   HIP_OK(hipMemsetAsync(d->d_best, 0, sizeof(uint32_t) * 2 * P, d->stream));
+  HIP_OK(hipMemsetAsync(d->soa.kerr, 0, sizeof(int32_t), d->stream));
   const KArgs k = make_kargs(ctx, now);
   const int ppb = 8;
   bool cpu = false;
@@ -3865,7 +4249,7 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
       hipLaunchKernelGGL((cpu ? k_numa_fallback<true, true> : k_numa_fallback<true, false>), dim3(FALLBACK_BLOCKS),
                          dim3(64), 0, d->stream, d->soa, d->d_pods,
                          d->d_batch_base, k, d->d_defer, d->d_defer_cnt, d->d_scores, d->capacity, (int)N, d_status,
-                         d_reason, d_la, d_numa, d_ds, d_total, d_dsmax, nullptr);
+                         d_reason, d_la, d_numa, d_ds, d_total, d_dsmax, nullptr, nullptr);
     } else {
       hipLaunchKernelGGL((cpu ? k_eval_parity<false, true> : k_eval_parity<false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, (int)N, d->d_pods, (int)P,
                          ppb, k, d_status, d_reason, d_la, d_numa, d_ds, d_total, d_dsmax, nullptr, nullptr);
@@ -3887,7 +4271,11 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
   uint32_t deferred = 0;
   if (d->numa_alloc && N > 0)
     HIP_OK(hipMemcpyAsync(&deferred, d->d_defer_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, d->stream));
+  int32_t kerr = 0;
+  HIP_OK(hipMemcpyAsync(&kerr, d->soa.kerr, sizeof(int32_t), hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipStreamSynchronize(d->stream));
+  if (kerr & KERR_DS_MERGE)
+    return fail(KE_ERR_UNSUPPORTED, "a DeviceShare BestEffort NUMA merge beyond 2^20 hint permutations");
   ctx->kstat_numa_deferred = deferred;
   if (best)
     for (int64_t p = 0; p < P; p++) best[p] = bk[p] ? key_node(bk[p]) + ctx->cfg.global_node_offset : -1;
@@ -4009,6 +4397,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   HIP_OK(hipMemcpyAsync(d_bases, bases.data(), sizeof(int32_t) * (n_batches + 1), hipMemcpyHostToDevice, d->stream));
   HIP_OK(hipMemsetAsync(d_ready, 0, sizeof(int32_t) * (sched_words - n_batches - 1), d->stream));
   HIP_OK(hipMemsetAsync(d_fst, 0, sizeof(uint64_t) * 2 * n_batches, d->stream));
+  HIP_OK(hipMemsetAsync(d->soa.kerr, 0, sizeof(int32_t), d->stream));
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
@@ -4053,18 +4442,19 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
         // a singleton batch has one pod's worth of lanes: single-wave blocks spread it over every CU
         const int eb = single ? 64 : EVAL_BLOCK;
         const dim3 grid = eval_grid(hi - lo, eb, bp, ppb);
-        // a DeviceShare pod never meets a NUMA policy (ke_capi check_numa_deviceshare): no NUMA path there
-        auto eval = cpu ? (ds ? k_eval_batch<true, false, true> : numa ? k_eval_batch<false, true, true> : k_eval_batch<false, false, true>)
+        auto eval = cpu ? (ds ? (numa ? k_eval_batch<true, true, true> : k_eval_batch<true, false, true>)
+                              : (numa ? k_eval_batch<false, true, true> : k_eval_batch<false, false, true>))
                         : ds ? (numa ? k_eval_batch<true, true, false> : k_eval_batch<true, false, false>)
                              : (numa ? k_eval_batch<false, true, false> : k_eval_batch<false, false, false>);
         uint32_t* dcnt = numa ? d->d_defer_cnt + b : nullptr;
         hipLaunchKernelGGL(eval, grid, dim3(eb), 0, es, d->soa, lo, hi, d->d_pods, bbase, bp,
                            ppb, k, d->d_scores, d->capacity, d->d_dsraw, d->d_defer, dcnt, d->d_aff, d->d_dsmax);
-        if (numa && !ds)  // DeviceShare pods never meet a NUMA policy: nothing deferred in their batches
+        if (numa)  // a DeviceShare pod defers only on nodes without a device cache (no DeviceShare hints there)
           hipLaunchKernelGGL((cpu ? k_numa_fallback<false, true> : k_numa_fallback<false, false>), dim3(FALLBACK_BLOCKS),
                              dim3(64), 0, es, d->soa, d->d_pods,
                              bbase, k, d->d_defer, dcnt, d->d_scores, d->capacity, 0, nullptr, nullptr,
-                             nullptr, nullptr, nullptr, nullptr, nullptr, cpu ? d->d_aff : nullptr);
+                             nullptr, nullptr, nullptr, nullptr, ds ? d->d_dsmax : nullptr, cpu ? d->d_aff : nullptr,
+                             ds ? d->d_dsraw : nullptr);
       }
       if (ds && sharded && !d->loopback)  // DefaultNormalizeScore's max over the feasible nodes of all ranks
         RCCL_OK(ncclAllReduce(d->d_dsmax, d->d_dsmax, 1, ncclUint32, ncclMax, d->comm, es));
@@ -4192,8 +4582,9 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   }
   std::vector<uint64_t> st((size_t)n_batches + 1), pst(8 * (size_t)n_batches), est((size_t)n_batches),
       fst(2 * (size_t)n_batches);
-  int32_t herr = 0;
+  int32_t herr = 0, kerr = 0;
   HIP_OK(hipMemcpyAsync(&herr, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, d->stream));
+  HIP_OK(hipMemcpyAsync(&kerr, d->soa.kerr, sizeof(int32_t), hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipMemcpyAsync(fst.data(), d_fst, sizeof(uint64_t) * 2 * n_batches, hipMemcpyDeviceToHost, d->stream));
   std::vector<uint32_t> dcnt(numa ? (size_t)n_batches : 0);
   if (numa)
@@ -4213,6 +4604,12 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     (void)hipEventDestroy(e1);
     for (auto& e : ev) (void)hipEventDestroy(e);
     return fail(KE_ERR_DEVICE, "pipelined schedule: a device-side hand-off timed out (placements invalid)");
+  }
+  if (kerr & KERR_DS_MERGE) {  // placements past the refused pair are not the reference's
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    return fail(KE_ERR_UNSUPPORTED, "a DeviceShare BestEffort NUMA merge beyond 2^20 hint permutations");
   }
   float ms = 0;
   HIP_OK(hipEventElapsedTime(&ms, e0, e1));

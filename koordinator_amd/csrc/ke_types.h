@@ -214,8 +214,11 @@ enum DsMask : int {
   DSM_RF = 3,      // RDMA total 0-15, RDMA used 16-31, FPGA total 32-47, FPGA used 48-63
   DSM_TOPO = 4,    // GPU topology tree: 4 bits per minor m at 4m = NUMA scope rank (scopes ascending by NodeID)
   DSM_PCIE = 5,    // 4 bits per minor m at 4m = PCIe scope rank (DFS order: NUMA rank, then PCIEID)
-  NUM_DS_MASKS = 6
+  DSM_DNUMA = 6,   // 3 words (per type): 4 bits per minor m at 4m = the device's NUMA code (DN_*)
+  NUM_DS_MASKS = 9
 };
+// device NUMA codes (DeviceInfo.Topology): 0 = no topology, 1 + NodeID for NodeID 0..7, DN_ANY = NodeID -1
+constexpr uint32_t DN_ANY = 9;
 // DSM_EXISTS high bits: GPU allocator state of the node (allocator_gpu.go:72-133)
 constexpr uint64_t DSX_TOPO = 1ull << 48;   // GetGPUTopologyScope != nil
 constexpr uint64_t DSX_HONOR = 1ull << 49;  // nodeHonorGPUPartition
@@ -250,6 +253,7 @@ enum ArgFlag : uint32_t {
   AF_NUMA_HINT_MOST = 1u << 5,      // NodeNUMAResource NUMAScoringStrategy MostAllocated (hint scores)
   AF_QUOTA = 1u << 6,               // an ElasticQuota tree is loaded: PreFilter admission + Reserve
   AF_QUOTA_PARENT = 1u << 7,        // ElasticQuotaArgs.EnableCheckParentQuota
+  AF_DS_NO_NUMA = 1u << 8,          // DeviceShareArgs.DisableDeviceNUMATopologyAlignment
 };
 struct KArgs {
   int64_t now;

@@ -288,6 +288,49 @@ def add_gpu_topology(devices, seed, nil_fraction=0.05):
     return devices
 
 
+def add_device_numa(devices, zones, seed, off_zone_fraction=0.05, no_topology_fraction=0.05):
+    """Give each device cache entry NUMA node ids consistent with the node's NRT zones (in place), for
+    DeviceShare's NUMA hints: 8 GPUs over the zones (2 or 4 zones: spread evenly; 8 zones: two zones,
+    so a BestEffort merge stays within the permutation budget), the RDMA NICs on the GPUs' zones.  An
+    `off_zone_fraction` of the entries put a GPU on a NUMA id the node has no zone for, a
+    `no_topology_fraction` leave one GPU without topology (filtered out under an affinity)."""
+    rng = np.random.default_rng(seed)
+    for devs, z in zip(devices, zones):
+        if devs is None:
+            continue
+        nz = len(z) if z is not None else 2
+        ids = list(range(nz)) if nz <= 4 else sorted(rng.choice(nz, 2, replace=False).tolist())
+        g = np.nonzero(devs["type"] == abi.DEV_GPU)[0]
+        r = np.nonzero(devs["type"] != abi.DEV_GPU)[0]
+        for j, i in enumerate(g):
+            devs[i]["has_topology"] = 1
+            devs[i]["numa_node"] = ids[j * len(ids) // len(g)]
+            devs[i]["pcie_rank"] = j // 2
+        for j, i in enumerate(r):
+            devs[i]["has_topology"] = 1
+            devs[i]["numa_node"] = ids[j * len(ids) // len(r)]
+            devs[i]["pcie_rank"] = (len(g) + 1) // 2 + j
+        if len(g) and rng.random() < off_zone_fraction:
+            devs[g[-1]]["numa_node"] = min(nz, 7)
+        if len(g) and rng.random() < no_topology_fraction:
+            k = g[rng.integers(len(g))]
+            devs[k]["has_topology"] = 0
+            devs[k]["numa_node"] = -1
+    return devices
+
+
+def make_ds_numa_pods(n_pods, seed, policy_fraction=0.3, key_base=2_500_000_000):
+    """make_ds_pods (device requests on half of the queue) where `policy_fraction` of the pods also carry a
+    NUMA topology spec (BestEffort / Restricted / SingleNUMANode, SingleNUMANodeExclusive unset /
+    Preferred / Required)."""
+    rng = np.random.default_rng(seed)
+    pods = make_ds_pods(n_pods, seed + 1, key_base=key_base)
+    pol = rng.random(n_pods) < policy_fraction
+    pods["numa_topology_policy"] = np.where(pol, rng.integers(1, 4, n_pods), 0)
+    pods["numa_exclusive"] = np.where(pol, rng.integers(0, 3, n_pods), 0)
+    return pods
+
+
 def make_partition_states(n_nodes, seed, gpus=8):
     """Per node (has_table, honor, partitions) for ke_node_gpu_partitions: the designated Hopper table
     (40 %), a custom table with two allocation-score groups and ring bus bandwidths (15 %), an empty table

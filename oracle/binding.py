@@ -67,6 +67,8 @@ def load():
         "or_ds_filter": (C.c_int, [V, C.POINTER(abi.Pod), i32, C.POINTER(C.c_int)]),
         "or_ds_score": (i64, [V, C.POINTER(abi.Pod), i32]),
         "or_ds_reserve": (C.c_uint64, [V, C.POINTER(abi.Pod), i32]),
+        "or_ds_numa_hints": (C.c_int, [V, i32, C.POINTER(abi.Pod), V, V, V, V, V, V, V]),
+        "or_ds_numa_allocate": (C.c_int, [V, i32, C.POINTER(abi.Pod), C.c_uint32, V]),
         "or_usage_percent": (i64, [i64, i64]),
         "or_quotas_load": (C.c_int, [V, C.POINTER(abi.QuotaArgs), V, i32]),
         "or_quota_state": (C.c_int, [V, i32, V, V, V, V]),
@@ -241,6 +243,20 @@ class Oracle:
 
     def ds_reserve(self, pod, node):
         return self.lib.or_ds_reserve(self.h, C.byref(pod), node)
+
+    def ds_numa_hints(self, pod, node):
+        """DeviceShare's NUMA hints: (status, reason, none, copies, [(mask, preferred, score)])"""
+        masks, pref, sc = np.zeros(255, np.uint32), np.zeros(255, np.uint8), np.zeros(255, np.int64)
+        n, copies, none, reason = (np.zeros(1, np.int32) for _ in range(4))
+        st = self.lib.or_ds_numa_hints(self.h, node, C.byref(pod), abi.ptr(masks), abi.ptr(pref), abi.ptr(sc),
+                                       abi.ptr(n), abi.ptr(copies), abi.ptr(none), abi.ptr(reason))
+        hints = [(int(masks[i]), bool(pref[i]), int(sc[i])) for i in range(int(n[0]))]
+        return st, int(reason[0]), bool(none[0]), int(copies[0]), hints
+
+    def ds_numa_allocate(self, pod, node, affinity):
+        reason = np.zeros(1, np.int32)
+        st = self.lib.or_ds_numa_allocate(self.h, node, C.byref(pod), affinity, abi.ptr(reason))
+        return st, int(reason[0])
 
     def estimate_pod(self, pod):
         est = np.zeros(2, np.int64)

@@ -745,6 +745,12 @@ static int pod_requests_zero(const ke_pod* pod) { /* quotav1.IsZero(PodRequests)
 
 /* Plugin.Filter  plugin.go:318-406 -> filterAmplifiedCPUs :408-442 */
 static int numa_filter_amplified(const or_node* n, const ke_pod* pod, int rcb, int* reason);
+/* DeviceShare as a NUMA hint provider (defined with DeviceShare below) */
+struct numa_hint;
+static int ds_numa_hints(const or_cluster* c, const or_node* nd, const ke_pod* pod, struct numa_hint* list, int* n,
+                         int* copies, int* none, int* reason);
+static int ds_numa_allocate(const or_cluster* c, const or_node* nd, const ke_pod* pod, uint32_t affinity, int* reason);
+static int numa_stored_affinity(const or_cluster* c, const ke_pod* pod, int32_t node, uint32_t* aff);
 static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod, int policy, int exclusive,
                       uint32_t* affinity, int* reason, const numa_cs* cs);
 
@@ -758,9 +764,29 @@ static int effective_policy(const or_node* n, const ke_pod* pod, int* exclusive)
   return pp != KE_NUMA_POLICY_NONE ? pp : np;
 }
 
+/* Filter's path; *stored = topologymanager Admit ran and stored *aff (0 = nil NUMANodeAffinity) */
+static int numa_filter_aff(const or_cluster* c, const ke_pod* pod, int32_t node, int* reason, int* stored,
+                           uint32_t* aff_out);
 int or_numa_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* reason) {
+  int stored;
+  uint32_t aff;
+  return numa_filter_aff(c, pod, node, reason, &stored, &aff);
+}
+
+/* The affinity NodeNUMAResource's Filter stores for the pod on the node (topologymanager Store,
+ * manager.go:64-95): 1 when its Filter passes through Admit, *aff = the NUMANodeAffinity (0 = nil). */
+static int numa_stored_affinity(const or_cluster* c, const ke_pod* pod, int32_t node, uint32_t* aff) {
+  int reason, stored;
+  const int code = numa_filter_aff(c, pod, node, &reason, &stored, aff);
+  return code == KE_CODE_SUCCESS && stored;
+}
+
+static int numa_filter_aff(const or_cluster* c, const ke_pod* pod, int32_t node, int* reason, int* stored,
+                           uint32_t* aff_out) {
   const or_node* n = &c->nodes[node];
   *reason = KE_REASON_NONE;
+  *stored = 0;
+  *aff_out = 0;
   if (pod_requests_zero(pod)) return KE_CODE_SUCCESS; /* state.skip */
   cpuset_state st;
   cpuset_prefilter(c, pod, &st);
@@ -814,7 +840,12 @@ int or_numa_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* re
   uint32_t aff;
   numa_cs cs;
   numa_cs_build(c, n, pod, &cs);
-  return numa_admit(c, n, pod, policy, exclusive, &aff, reason, &cs);
+  const int admit_code = numa_admit(c, n, pod, policy, exclusive, &aff, reason, &cs);
+  if (admit_code == KE_CODE_SUCCESS) {
+    *stored = 1;
+    *aff_out = aff;
+  }
+  return admit_code;
 }
 
 /* filterAmplifiedCPUs  plugin.go:408-442 */
@@ -1123,11 +1154,11 @@ static int narrower(uint32_t a, uint32_t b) { /* bitmask.IsNarrowerThan */
 static numa_hint merge_filtered(uint32_t all, numa_hint* const* lists, const int* lens, int nl, int exclusive,
                                 const uint8_t* status) {
   numa_hint best = {all, 0, 0, 0};
-  int idx[4] = {0, 0, 0, 0};
+  int idx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int i = 0; i < nl; i++)
     if (lens[i] == 0) return best; /* an empty list: no permutation */
   for (;;) {
-    numa_hint perm[4];
+    numa_hint perm[8];
     for (int i = 0; i < nl; i++) perm[i] = lists[i][idx[i]];
     numa_hint m = merge_permutation(all, perm, nl);
     if (__builtin_popcount(m.mask) != 0) {
@@ -1250,11 +1281,19 @@ static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod,
   static __thread numa_hint store[KE_NRES * 255];
   int counts[KE_NRES], present[KE_NRES];
   numa_generate_hints(c, nd, &v, pod, policy, store, counts, present, cs);
+  /* DeviceShare's hints (topology_hint.go:38-58): a provider error is an Admit reason
+   * (accumulateProvidersHints, manager.go:110-125) */
+  static __thread numa_hint ds_list[255];
+  int ds_n = 0, ds_copies = 0, ds_none = 1;
+  const int ds_st = ds_numa_hints(c, nd, pod, ds_list, &ds_n, &ds_copies, &ds_none, reason);
+  if (ds_st) return KE_CODE_UNSCHEDULABLE;
   /* filterProvidersHints: the NUMA provider's lists in sorted resource-name order (cpu, memory), then
-   * DeviceShare's nil hints -> one preferred any-NUMA hint */
-  static __thread numa_hint filt[KE_NRES + 1][255];
-  numa_hint* lists[KE_NRES + 1];
-  int lens[KE_NRES + 1], nl = 0, reasons = 0;
+   * DeviceShare's: nil hints -> one preferred any-NUMA hint, else one (identical) list per requested device
+   * type.  Providers in profile order (NodeNUMAResource, DeviceShare); the reference creates plugins from a
+   * Go map, so this order is a convention. */
+  static __thread numa_hint filt[KE_NRES + 4][255];
+  numa_hint* lists[KE_NRES + 4];
+  int lens[KE_NRES + 4], nl = 0, reasons = 0;
   int any_present = present[0] || present[1];
   for (int r = 0; r < KE_NRES; r++) {
     if (!present[r]) continue;
@@ -1285,9 +1324,22 @@ static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod,
     lists[nl] = filt[nl];
     lens[nl++] = 1;
   }
-  filt[nl][0] = (numa_hint){0, 1, 0, 0}; /* DeviceShare: no preference */
-  lists[nl] = filt[nl];
-  lens[nl++] = 1;
+  if (ds_none) {
+    filt[nl][0] = (numa_hint){0, 1, 0, 0}; /* DeviceShare: no preference */
+    lists[nl] = filt[nl];
+    lens[nl++] = 1;
+  } else {
+    for (int t = 0; t < ds_copies; t++) {
+      int n = 0;
+      for (int i = 0; i < ds_n; i++) {
+        const numa_hint h = ds_list[i];
+        if (policy == KE_NUMA_POLICY_SINGLE_NUMA_NODE && !(h.preferred && __builtin_popcount(h.mask) == 1)) continue;
+        filt[nl][n++] = h;
+      }
+      lists[nl] = filt[nl];
+      lens[nl++] = n;
+    }
+  }
   numa_hint best;
   const int admit = policy_merge(policy, all, lists, lens, nl, reasons, exclusive, status, &best);
   if (!admit) {
@@ -1305,6 +1357,9 @@ static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod,
     *reason = KE_REASON_NUMA_INSUFFICIENT_CPUS; /* "not enough cpus available to satisfy request" */
     return KE_CODE_UNSCHEDULABLE;
   }
+  /* -> DeviceShare.Allocate with the affinity (topology_hint.go:60-117) */
+  const int ds_code = ds_numa_allocate(c, nd, pod, best.mask, reason);
+  if (ds_code) return ds_code;
   *affinity = best.mask;
   return KE_CODE_SUCCESS;
 }
@@ -1681,15 +1736,48 @@ static void ds_orig_view(const or_node* nd, int t, ds_view* v) {
       }
 }
 
+/* AutopilotAllocator.numaNodes (nil = off): the NUMA affinity the devices are restricted to */
+typedef struct ds_aff {
+  int on;
+  uint32_t mask;
+} ds_aff;
+static const ds_aff NO_AFF = {0, 0};
+
+/* filterNodeDevice's device choice (device_allocator.go:137-166): with numaNodes set, a device needs a
+ * topology whose NodeID is -1 or in the affinity */
+static int dev_allowed(const ke_device* dv, ds_aff a) {
+  if (!a.on) return 1;
+  if (!dv->has_topology) return 0;
+  if (dv->numa_node == -1) return 1;
+  return dv->numa_node >= 0 && dv->numa_node < 32 && ((a.mask >> dv->numa_node) & 1u);
+}
+
 /* AutopilotAllocator.filterNodeDevice -> nodeDevice.filter (device_allocator.go:137-166,
- * device_cache.go:360-415) with no preemptible/required resources: the type is dropped when its free
- * is all zero; otherwise used' = total - free (kept if non-zero) and free' = total - used'. */
-static void ds_filtered_view(const or_node* nd, int t, ds_view* v) {
+ * device_cache.go:360-415) with no required resources and an empty preemptible map: the type is dropped
+ * when its free is all zero (over every instance) or no instance passes the NUMA affinity; otherwise the
+ * passing instances with used' = total - free (kept if non-zero) and free' = total - used'. */
+static void ds_filtered_view_aff(const or_node* nd, int t, ds_aff a, ds_view* v) {
   ds_orig_view(nd, t, v);
   const int nk = nkeys(t);
   int all_zero = 1;
   for (int i = 0; i < v->n; i++)
     if (!rl_is_zero(v->free[i], nk)) all_zero = 0;
+  if (a.on) { /* the instances of the type that pass the affinity, ascending minors */
+    int n = 0;
+    for (int i = 0; i < v->n; i++) {
+      const ke_device* dv = NULL;
+      for (int j = 0; j < nd->n_dev; j++)
+        if (nd->dev[j].type == t && nd->dev[j].minor == v->minor[i]) dv = &nd->dev[j];
+      if (!dev_allowed(dv, a)) continue;
+      v->minor[n] = v->minor[i];
+      v->total[n] = v->total[i];
+      v->used[n] = v->used[i];
+      v->free[n] = v->free[i];
+      n++;
+    }
+    if (n == 0) all_zero = 1; /* devices[type] not set: the type is absent */
+    v->n = n;
+  }
   v->present = v->n > 0 && !all_zero;
   if (!v->present) return;
   for (int i = 0; i < v->n; i++) {
@@ -1825,13 +1913,17 @@ typedef struct gpu_ctx {
 static void gpu_ctx_init(const or_node* nd, const ds_view* v, gpu_ctx* g) {
   memset(g, 0, sizeof *g);
   g->present = v->present;
+  uint32_t refined = 0; /* the refined deviceTotal's minors */
+  if (v->present)
+    for (int i = 0; i < v->n; i++) refined |= 1u << v->minor[i];
   for (int i = 0; i < nd->n_dev; i++) {
     const ke_device* dv = &nd->dev[i];
     if (dv->type != KE_DEV_GPU) continue;
     g->minors |= 1u << dv->minor;
     g->crd_total[dv->minor] = dev_total(dv, 3);
-    /* original used minors not in the refined total: all of them when the GPU type was dropped */
-    if (!v->present && (dv->has_used[0] || dv->has_used[1] || dv->has_used[2])) g->used |= 1u << dv->minor;
+    /* original used minors not in the refined total (outside the affinity, or the type dropped) */
+    if (!(refined >> dv->minor & 1u) && (dv->has_used[0] || dv->has_used[1] || dv->has_used[2]))
+      g->used |= 1u << dv->minor;
   }
   if (!v->present) return;
   for (int i = 0; i < v->n; i++) {
@@ -2124,8 +2216,44 @@ static int ds_insufficient_reason(int t) {
                          : (t == KE_DEV_RDMA ? KE_REASON_DS_INSUFFICIENT_RDMA : KE_REASON_DS_INSUFFICIENT_FPGA);
 }
 
-/* DeviceShare Filter (plugin.go:311-365): AutopilotAllocator.Allocate (device_allocator.go:87-135).
- * Device types are visited in the fixed order GPU, RDMA, FPGA (Go map order only changes the reason). */
+/* AutopilotAllocator.Allocate (device_allocator.go:87-135) without a scorer, on the devices the NUMA
+ * affinity leaves: Prepare (a requested type without devices in the cache), then every requested type in
+ * the fixed order GPU, RDMA, FPGA (Go map order only changes the reason).  *gpu = the GPU minors. */
+static int ds_try_allocate(const or_node* nd, const ds_pod* d, ds_aff a, uint32_t* gpu, int* reason) {
+  *gpu = 0;
+  for (int t = 0; t < KE_DEV_TYPES; t++) {
+    if (!d->has[t]) continue;
+    ds_view v;
+    ds_orig_view(nd, t, &v);
+    if (v.n == 0) {
+      *reason = ds_insufficient_reason(t);
+      return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    }
+  }
+  for (int t = 0; t < KE_DEV_TYPES; t++) {
+    if (!d->has[t]) continue;
+    ds_view v;
+    ds_filtered_view_aff(nd, t, a, &v);
+    if (t == KE_DEV_GPU) {
+      int why = 0;
+      const int st = ds_gpu_allocate(nd, d, &v, NULL, gpu, &why);
+      if (st) {
+        *reason = why;
+        return st;
+      }
+      continue;
+    }
+    int picked[KE_MAX_MINORS];
+    if (ds_allocate(NULL, t, &d->req[t], d->count[t], &v, picked) < d->count[t]) {
+      *reason = ds_insufficient_reason(t);
+      return KE_CODE_UNSCHEDULABLE;
+    }
+  }
+  return KE_CODE_SUCCESS;
+}
+
+/* DeviceShare Filter (plugin.go:311-365): skipped when the topology manager stored an affinity for the
+ * node (Admit ran DeviceShare.Allocate on it), else AutopilotAllocator.Allocate. */
 int or_ds_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* reason) {
   ds_pod d;
   ds_prepare_pod(pod, &d);
@@ -2134,36 +2262,144 @@ int or_ds_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* reas
     return d.status;
   }
   const or_node* nd = &c->nodes[node];
-  if (d.skip || !nd->has_dev_cache) return KE_CODE_SUCCESS;
-  ds_view v[KE_DEV_TYPES];
-  for (int t = 0; t < KE_DEV_TYPES; t++) { /* Prepare: a requested type without devices */
-    if (!d.has[t]) continue;
-    ds_orig_view(nd, t, &v[t]);
-    if (v[t].n == 0) {
-      *reason = ds_insufficient_reason(t);
-      return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
-    }
+  if (d.skip) return KE_CODE_SUCCESS;
+  uint32_t aff;
+  if (numa_stored_affinity(c, pod, node, &aff)) return KE_CODE_SUCCESS;
+  if (!nd->has_dev_cache) return KE_CODE_SUCCESS;
+  uint32_t gpu;
+  int why = 0;
+  const int st = ds_try_allocate(nd, &d, NO_AFF, &gpu, &why);
+  if (st) *reason = why;
+  return st;
+}
+
+/* The DeviceShare NUMA hint provider (topology_hint.go:38-58,119-212).  Returns a provider error status
+ * (+ *reason) or 0 with: *none = no preference (the provider returned no hints), else the hint list over
+ * the device NUMA ids (IterateBitMasks order, preferred = the minimal affinity size, score 500 when the
+ * hint's GPU allocation equals the one on all device NUMA nodes) and *copies = one list per requested
+ * device type. */
+static int ds_numa_hints(const or_cluster* c, const or_node* nd, const ke_pod* pod, numa_hint* list, int* n,
+                         int* copies, int* none, int* reason) {
+  *n = 0;
+  *copies = 0;
+  *none = 1;
+  ds_pod d;
+  ds_prepare_pod(pod, &d);
+  if (d.status || d.skip || !nd->has_dev_cache || c->cfg.deviceshare.disable_numa_alignment) return 0;
+  int ids[KE_MAX_NUMA], k = 0; /* numaTopology.nodes: the NodeIDs of devices with a topology, -1 excluded */
+  for (int i = 0; i < nd->n_dev; i++) {
+    const ke_device* dv = &nd->dev[i];
+    if (!dv->has_topology || dv->numa_node < 0) continue;
+    int j = 0;
+    while (j < k && ids[j] < dv->numa_node) j++;
+    if (j < k && ids[j] == dv->numa_node) continue;
+    for (int q = k; q > j; q--) ids[q] = ids[q - 1];
+    ids[j] = dv->numa_node;
+    k++;
   }
-  for (int t = 0; t < KE_DEV_TYPES; t++) {
+  if (k == 0) return 0; /* no mask to iterate: an empty hint map */
+  int prep = 0, prep_reason = 0; /* Prepare fails on every mask alike */
+  for (int t = 0; t < KE_DEV_TYPES && !prep; t++) {
     if (!d.has[t]) continue;
-    ds_filtered_view(nd, t, &v[t]);
-    if (t == KE_DEV_GPU) { /* Filter's allocator carries no scorer */
-      uint32_t mask;
-      int why = 0;
-      const int st = ds_gpu_allocate(nd, &d, &v[t], NULL, &mask, &why);
-      if (st) {
-        *reason = why;
-        return st;
+    ds_view v;
+    ds_orig_view(nd, t, &v);
+    if (v.n == 0) prep = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE, prep_reason = ds_insufficient_reason(t);
+  }
+  static __thread uint32_t fmask[255], fgpu[255];
+  int nf = 0, min_size = -1, full_st = 0, full_reason = 0;
+  uint32_t best_gpu = 0;
+  for (int size = 1; size <= k; size++) { /* bitmask.IterateBitMasks(numaNodes) */
+    int idx[KE_MAX_NUMA];
+    for (int i = 0; i < size; i++) idx[i] = i;
+    for (;;) {
+      uint32_t mask = 0;
+      for (int i = 0; i < size; i++) mask |= 1u << ids[idx[i]];
+      int st = prep, why = prep_reason;
+      uint32_t gpu = 0;
+      if (!st) { /* calcTotalDevicesByNUMA: a requested type with devices there but too few */
+        for (int t = 0; t < KE_DEV_TYPES && !st; t++) {
+          if (!d.has[t]) continue;
+          int cnt = 0;
+          for (int i = 0; i < nd->n_dev; i++) {
+            const ke_device* dv = &nd->dev[i];
+            if (dv->type == t && dv->has_topology && dv->numa_node >= 0 && ((mask >> dv->numa_node) & 1u)) cnt++;
+          }
+          if (cnt > 0 && cnt < d.count[t]) st = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE, why = KE_REASON_DS_INSUFFICIENT_NUMA_SCOPED;
+        }
       }
-      continue;
-    }
-    int picked[KE_MAX_MINORS];
-    if (ds_allocate(NULL, t, &d.req[t], d.count[t], &v[t], picked) < d.count[t]) {
-      *reason = ds_insufficient_reason(t);
-      return KE_CODE_UNSCHEDULABLE;
+      if (!st) {
+        if (min_size < 0) min_size = k;
+        st = ds_try_allocate(nd, &d, (ds_aff){1, mask}, &gpu, &why);
+        if (!st) {
+          fmask[nf] = mask;
+          fgpu[nf] = gpu;
+          nf++;
+          if (size < min_size) min_size = size;
+        }
+      }
+      if (size == k) { /* the mask of every device NUMA node: statusUnsatisfied, bestAllocationResult */
+        full_st = st;
+        full_reason = why;
+        best_gpu = st ? 0 : gpu;
+      }
+      int i = size - 1;
+      while (i >= 0 && idx[i] == k - size + i) i--;
+      if (i < 0) break;
+      idx[i]++;
+      for (int j = i + 1; j < size; j++) idx[j] = idx[j - 1] + 1;
     }
   }
-  return KE_CODE_SUCCESS;
+  if (full_st) {
+    *reason = full_reason;
+    return full_st;
+  }
+  *none = 0;
+  for (int t = 0; t < KE_DEV_TYPES; t++) *copies += d.has[t];
+  for (int i = 0; i < nf; i++) {
+    numa_hint h = {fmask[i], __builtin_popcount(fmask[i]) == min_size, 0, fgpu[i] == best_gpu ? 500 : 0};
+    list[(*n)++] = h;
+  }
+  return 0;
+}
+
+/* DeviceShare.Allocate during Admit (topology_hint.go:60-117): the allocation on the affinity's NUMA
+ * nodes (nil affinity: every device) must succeed. */
+static int ds_numa_allocate(const or_cluster* c, const or_node* nd, const ke_pod* pod, uint32_t affinity, int* reason) {
+  ds_pod d;
+  ds_prepare_pod(pod, &d);
+  if (d.status || d.skip || !nd->has_dev_cache || c->cfg.deviceshare.disable_numa_alignment) return KE_CODE_SUCCESS;
+  uint32_t gpu;
+  int why = 0;
+  const int st = ds_try_allocate(nd, &d, (ds_aff){affinity != 0, affinity}, &gpu, &why);
+  if (st) *reason = why;
+  return st;
+}
+
+/* Golden-vector entry points for the DeviceShare NUMA hint provider: the hint list (masks, preferred,
+ * scores; *copies lists of it, *none = no preference) or the provider's error status; and
+ * DeviceShare.Allocate on an affinity (0 = nil). */
+int or_ds_numa_hints(const or_cluster* c, int32_t node, const ke_pod* pod, uint32_t* masks, uint8_t* preferred,
+                     int64_t* scores, int32_t* n, int32_t* copies, int32_t* none, int32_t* reason) {
+  static __thread numa_hint list[255];
+  int nn = 0, cp = 0, no = 1, why = 0;
+  const int st = ds_numa_hints(c, &c->nodes[node], pod, list, &nn, &cp, &no, &why);
+  for (int i = 0; i < nn; i++) {
+    masks[i] = list[i].mask;
+    preferred[i] = (uint8_t)list[i].preferred;
+    scores[i] = list[i].score;
+  }
+  *n = nn;
+  *copies = cp;
+  *none = no;
+  *reason = why;
+  return st;
+}
+
+int or_ds_numa_allocate(const or_cluster* c, int32_t node, const ke_pod* pod, uint32_t affinity, int32_t* reason) {
+  int why = 0;
+  const int st = ds_numa_allocate(c, &c->nodes[node], pod, affinity, &why);
+  *reason = why;
+  return st;
 }
 
 /* DeviceShare Score before NormalizeScore (scoring.go:45-103 -> AutopilotAllocator.score
@@ -2173,13 +2409,15 @@ int64_t or_ds_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
   ds_prepare_pod(pod, &d);
   const or_node* nd = &c->nodes[node];
   if (d.status || d.skip || !nd->has_dev_cache) return 0;
+  uint32_t aff = 0; /* the stored affinity restricts the devices scored (scoring.go:63-73) */
+  const ds_aff a = numa_stored_affinity(c, pod, node, &aff) ? (ds_aff){aff != 0, aff} : NO_AFF;
   int64_t s = 0;
   for (int t = 0; t < KE_DEV_TYPES; t++) {
     if (!d.has[t]) continue;
     ds_view v;
     ds_orig_view(nd, t, &v);
     if (v.n == 0) return 0; /* Prepare error: Score returns 0 with an error status */
-    ds_filtered_view(nd, t, &v);
+    ds_filtered_view_aff(nd, t, a, &v);
     if (v.present && v.n > 0) s += ds_score_node(&c->cfg.deviceshare, t, &d.req[t], &v);
   }
   return s;
@@ -2187,7 +2425,33 @@ int64_t or_ds_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
 
 /* DeviceShare Reserve (plugin.go:426-492): allocate with the plugin's scorer, fillGPUTotalMem
  * (devicehandler_gpu.go:98-125), updateCacheUsed (device_cache.go:127-141).  Returns the minor mask. */
+/* the affinity DeviceShare's Reserve allocates on: the one the Filter's Admit stored (taken before any
+ * Reserve of the pod changes the node), none when the alignment is disabled (plugin.go:452-466) */
+static ds_aff ds_reserve_affinity(const or_cluster* c, const ke_pod* pod, int32_t node) {
+  uint32_t aff = 0;
+  return !c->cfg.deviceshare.disable_numa_alignment && numa_stored_affinity(c, pod, node, &aff)
+             ? (ds_aff){aff != 0, aff} : NO_AFF;
+}
+
+static uint64_t ds_reserve_on(or_cluster* c, const ke_pod* pod, int32_t node, ds_aff a);
+
+/* AutopilotAllocator.Allocate in Reserve (plugin.go:459-486) succeeds: with the alignment disabled nothing
+ * checked the devices of a node whose NUMA Admit stored an affinity (Filter skipped, Allocate a no-op) */
+static int ds_reserve_feasible(const or_cluster* c, const ke_pod* pod, int32_t node, ds_aff a) {
+  ds_pod d;
+  ds_prepare_pod(pod, &d);
+  const or_node* nd = &c->nodes[node];
+  if (d.status || d.skip || !nd->has_dev_cache) return 1;
+  uint32_t gpu;
+  int why = 0;
+  return ds_try_allocate(nd, &d, a, &gpu, &why) == KE_CODE_SUCCESS;
+}
+
 uint64_t or_ds_reserve(or_cluster* c, const ke_pod* pod, int32_t node) {
+  return ds_reserve_on(c, pod, node, ds_reserve_affinity(c, pod, node));
+}
+
+static uint64_t ds_reserve_on(or_cluster* c, const ke_pod* pod, int32_t node, ds_aff a) {
   ds_pod d;
   ds_prepare_pod(pod, &d);
   or_node* nd = &c->nodes[node];
@@ -2197,7 +2461,7 @@ uint64_t or_ds_reserve(or_cluster* c, const ke_pod* pod, int32_t node) {
     if (!d.has[t]) continue;
     const int nk = nkeys(t);
     ds_view v;
-    ds_filtered_view(nd, t, &v);
+    ds_filtered_view_aff(nd, t, a, &v);
     int picked[KE_MAX_MINORS];
     int n = 0;
     if (t == KE_DEV_GPU) {
@@ -2677,9 +2941,9 @@ static int check_supported(const or_cluster* c, int32_t n_pods, const ke_pod* po
     if (node_unsupported(&c->nodes[i].node)) return KE_ERR_UNSUPPORTED;
     if (c->nodes[i].node.numa_topology_policy != KE_NUMA_POLICY_NONE) numa = 1;
   }
-  /* DeviceShare's own NUMA hints (deviceshare/topology_hint.go) are not restated */
   (void)cpuset;
-  if (ds && numa) return KE_ERR_UNSUPPORTED;
+  (void)ds;
+  (void)numa;
   return KE_OK;
 }
 
@@ -2758,7 +3022,10 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
     uint64_t mask = 0;
     reserve_plan rp;
     memset(&rp, 0, sizeof rp);
-    if (b >= 0 && or_reserve_plan(c, &pods[p], b, &rp) != 0) { /* Reserve failed: not placed */
+    ds_aff da = NO_AFF; /* the affinity the Filter stored, for DeviceShare's Reserve */
+    if (b >= 0) da = ds_reserve_affinity(c, &pods[p], b);
+    if (b >= 0 && (or_reserve_plan(c, &pods[p], b, &rp) != 0 || !ds_reserve_feasible(c, &pods[p], b, da))) {
+      /* Reserve failed (Unreserve undoes the others): not placed */
       chosen[p] = -1;
       if (score) score[p] = -1;
       b = -1;
@@ -2771,7 +3038,7 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
        * framework assume: NodeInfo.Requested. */
       or_pod_assign(c, b, &pods[p], now);
       or_reserve_apply(c, b, &rp, numa_alloc ? numa_alloc + (int64_t)p * 16 : NULL);
-      mask = or_ds_reserve(c, &pods[p], b);
+      mask = ds_reserve_on(c, &pods[p], b, da);
       c->nodes[b].node.requested[KE_RES_CPU] += pods[p].requests[KE_RES_CPU];
       c->nodes[b].node.requested[KE_RES_MEMORY] += pods[p].requests[KE_RES_MEMORY];
       if (c->quotas) orq_reserve(c->quotas, &pods[p]); /* ElasticQuota Reserve */

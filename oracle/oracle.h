@@ -58,6 +58,9 @@ int or_topology_merge(int32_t policy, uint32_t all, int32_t n_lists, const int32
 int or_ds_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* reason);
 int64_t or_ds_score(const or_cluster* c, const ke_pod* pod, int32_t node);
 uint64_t or_ds_reserve(or_cluster* c, const ke_pod* pod, int32_t node);
+int or_ds_numa_hints(const or_cluster* c, int32_t node, const ke_pod* pod, uint32_t* masks /*[255]*/, uint8_t* preferred,
+                     int64_t* scores, int32_t* n, int32_t* copies, int32_t* none, int32_t* reason);
+int or_ds_numa_allocate(const or_cluster* c, int32_t node, const ke_pod* pod, uint32_t affinity, int32_t* reason);
 /* DefaultEstimator.EstimatePod (estimator/default_estimator.go:59-85): est[KE_NRES], -1 = key absent */
 void or_estimate_pod(const or_cluster* c, const ke_pod* pod, int64_t* est);
 

@@ -109,13 +109,9 @@ def test_unsupported_inputs_are_rejected():
     with pytest.raises(KoordEvalError) as e:
         ev.upsert_node(1, n)
     assert e.value.code == abi.ERR_INVALID
-    # a NUMA-policy node is accepted; DeviceShare pods cannot meet it (DeviceShare NUMA hints)
+    # a NUMA-policy node is accepted (DeviceShare pods meet it as a second NUMA hint provider)
     n.numa_topology_policy = abi.NUMA_POLICY_RESTRICTED
     ev.upsert_node(1, n)
-    gpu_pod = model.make_pod(requests={"cpu": "1", "koordinator.sh/gpu": "100"})
-    with pytest.raises(KoordEvalError) as e:
-        ev.eval([gpu_pod], cases.NOW)
-    assert e.value.code == abi.ERR_UNSUPPORTED
     bad_spec = model.make_pod(requests={"cpu": "2"})
     bad_spec.has_resource_spec = 1
     with pytest.raises(KoordEvalError) as e:

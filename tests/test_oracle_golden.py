@@ -329,3 +329,26 @@ def test_gpu_allocator(case):
     if want["code"] == 0:
         mask = o.ds_reserve(pod, 0)
         assert [m for m in range(16) if mask >> m & 1] == want["minors"], case["source"]
+
+
+# ---- DeviceShare as a NUMA hint provider (topology_hint.go) --------------------------------------------
+DS_NUMA = cases.load("ds_numa.json")
+
+
+@pytest.mark.parametrize("case", DS_NUMA, ids=[c["name"] for c in DS_NUMA])
+def test_ds_numa_hints(case):
+    from koordinator_amd import abi, model
+    o = Oracle(abi.default_config(1), 1)
+    o.upsert_node(0, model.make_node(allocatable={"cpu": "96", "memory": "512Gi"}))
+    o.set_devices(0, model.make_devices(case["devices"]))
+    pod = model.make_pod(requests=dict(case["pod"]["requests"]))
+    want = case["want"]
+    if case["op"] == "allocate":
+        st, _ = o.ds_numa_allocate(pod, 0, case["affinity"])
+        assert st == want["code"], case["source"]
+        return
+    st, reason, none, copies, hints = o.ds_numa_hints(pod, 0)
+    assert (st, reason if st else 0) == (want["code"], want["reason"]), case["source"]
+    if not st:
+        assert not none and copies == want["copies"], case["source"]
+        assert [list(h) for h in hints] == want["hints"], case["source"]
