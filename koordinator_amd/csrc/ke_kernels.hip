@@ -1136,6 +1136,80 @@ __device__ __forceinline__ bool numa_distribute(const NumaNode& v, uint32_t m, c
   return ok;
 }
 
+// numa_distribute<false, CS>'s result (the hint loops' feasibility test).  A one-zone mask (the common
+// case: hint sizes are tried smallest first) takes the split in one step — splitQuantity by 1, one zone,
+// no sort — as straight-line code on its uniform zone id; larger masks run the general split.
+// A binding pod whose cpu is split (requested, some zone keyed) must take numCPUsNeeded CPUs from the
+// zones that received cpu (taken == num): the mask's zones need that many CPUs allocateCPUSet may take.
+template <bool CS>
+__device__ __forceinline__ bool numa_cs_counts_ok(const NumaNode& v, uint32_t m, const DevPod& p, const NumaCs* cs) {
+  if (!CS || !cs->rcb || cs->num <= 0 || p.req[0] <= 0 || !numa_checked(v, p, 0)) return true;
+  int n = 0;
+#pragma unroll
+  for (int z = 0; z < 8; z++) n += ((m >> z) & 1u) ? cs_zc(*cs, z) : 0;
+  return n >= cs->num;
+}
+
+// The smallest mask size whose zones can hold numCPUsNeeded such CPUs (1 when the bound does not apply).
+template <bool CS>
+__device__ __forceinline__ int numa_cs_min_size(const NumaNode& v, const DevPod& p, const NumaCs* cs) {
+  if (!CS || !cs->rcb || cs->num <= 0 || p.req[0] <= 0 || !numa_checked(v, p, 0)) return 1;
+  int c[8];
+#pragma unroll
+  for (int z = 0; z < 8; z++) c[z] = ((v.zm >> z) & 1u) ? cs_zc(*cs, z) : 0;
+  int sum = 0, k = 0;
+  uint32_t used = 0;
+  while (sum < cs->num && k < 8) {  // the largest counts first
+    int best = -1, bz = 0;
+#pragma unroll
+    for (int z = 0; z < 8; z++)
+      if (!((used >> z) & 1u) && c[z] > best) best = c[z], bz = z;
+    used |= 1u << bz;
+    sum += best;
+    k++;
+  }
+  return sum >= cs->num ? k : 9;
+}
+
+template <bool CS = false>
+__device__ __forceinline__ bool numa_fits(const NumaNode& v, uint32_t m, const DevPod& p, const NumaCs* cs = nullptr) {
+  if (!numa_cs_counts_ok<CS>(v, m, p, cs)) return false;
+  if (__popc(m) != 1) {
+    int64_t dummy[2][8];
+    return numa_distribute<false, CS>(v, m, p, nullptr, dummy, cs);
+  }
+  const int z = __ffs(m) - 1;
+  const bool bind = CS && cs->rcb;
+  bool ok = true, any = false, aligned = true;
+  int taken = 0;
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    if (!ok) break;
+    if (!numa_checked(v, p, r)) continue;
+    const int64_t q = p.req[r];
+    const int64_t a = pick8(v.av[r], z);
+    int64_t split = q;
+    if (bind && r == 0) {
+      const int64_t val = q >= 0 ? (q + 999) / 1000 : -((-q + 999) / 1000);  // Quantity.Value()
+      split = cs->full ? (val / cs->cpc) * cs->cpc * 1000 : val * 1000;
+    }
+    const int64_t got = a > split ? split : a;
+    if (got != 0) {
+      any = true;
+      if (bind && r == 0) {
+        const int k = min((int)(got / 1000), cs_zc(*cs, z));
+        if (k > 0) {
+          taken = k;
+          if (k % cs->cpc) aligned = false;
+        }
+      }
+    }
+    if (q - got != 0) ok = false;
+  }
+  if (bind) ok = ok && cs->total >= cs->num && (!any || (taken == cs->num && (!cs->full || aligned)));
+  return ok;
+}
+
 // resourceAllocationScorer.score with least/mostResourceScorer (scoring.go:210-226) in plain int64
 __device__ __forceinline__ int32_t numa_scope_score(bool most, const int64_t (&req)[2], const int64_t (&alloc)[2],
                                                     const DevPod& p, const KArgs& k) {
@@ -1211,7 +1285,7 @@ __device__ __forceinline__ uint32_t numa_best_effort_fallback(const SoA& s, int6
     if (m & ~v.zm) continue;
     const bool in0 = present[0] && !(m & lack[0]), in1 = present[1] && !(m & lack[1]);
     if (!in0 && !in1) continue;
-    if (!numa_distribute<false, CS>(v, m, p, nullptr, dummy, cs)) continue;
+    if (!numa_fits<CS>(v, m, p, cs)) continue;
     const uint64_t bit = 1ull << (m & 63u);
     const int w = (int)(m >> 6);
 #pragma unroll
@@ -1264,7 +1338,9 @@ __device__ __forceinline__ uint32_t numa_best_effort_fallback(const SoA& s, int6
   return bun ? v.zm : best;
 }
 
-constexpr uint8_t STATUS_DEFERRED = 0xFF;  // BestEffort pair left to k_numa_fallback
+constexpr uint8_t STATUS_DEFERRED = 0xFF;  // pair left to k_numa_fallback
+constexpr int NUMA_DEFER_SIZE = 1;         // largest hint size the batch eval's lanes search
+constexpr uint32_t NFB_FOUND = 1, NFB_FAIL = 2, NFB_BEST_EFFORT = 3;  // k_numa_fallback's merge outcome
 
 // generateResourceHints' resource lists: present[r] = the pod requests r and some zone has the key;
 // lack[r] = numaNodesLackResource (zones without r available)
@@ -1374,7 +1450,7 @@ __device__ __noinline__ NumaPick numa_admit_ds(const SoA& s, int64_t i, int poli
     if (m & ~all) continue;
     const bool in0 = present[0] && !(m & lack[0]), in1 = present[1] && !(m & lack[1]);
     if (!in0 && !in1) continue;
-    if (!numa_distribute<false, CS>(v, m, p, nullptr, dummy, cs)) continue;
+    if (!numa_fits<CS>(v, m, p, cs)) continue;
     if (in0) set256(L[0], m), minr[0] = min(minr[0], __popc(m));
     if (in1) set256(L[1], m), minr[1] = min(minr[1], __popc(m));
   }
@@ -1455,7 +1531,10 @@ __device__ __noinline__ NumaPick numa_admit_ds(const SoA& s, int64_t i, int poli
 // the merged topology `policy` (node / pod, util.go:58-74).  DEFER: a BestEffort pair without a
 // preferred merged hint returns STATUS_DEFERRED instead of running the full merge here (one lane
 // needing it would hold its whole wavefront; k_numa_fallback runs those pairs compacted).
-// FB_AFF: the BestEffort full-merge result was computed by the caller (k_numa_fallback) and is `fb_aff`.
+// The deferral also caps the in-lane search at hints of NUMA_DEFER_SIZE zones: a pair whose lists need
+// larger hints (a few per wave, but the wave waits for its slowest lane) goes to k_numa_fallback, whose
+// wave lists every mask of the pair at once.
+// FB_AFF: k_numa_fallback computed the Admit's merge for the pair: `fb_aff` = FB_* kind << 8 | affinity.
 // CS: a binding pod (`cs`, `ps` = its amplified requests for the hint scores): every allocation check
 // includes allocateCPUSet's take, a nil affinity the node-wide one.
 template <bool DEFER, bool FB_AFF = false, bool CS = false>
@@ -1504,6 +1583,21 @@ __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t
     allocate_on(o.aff);
     return o;
   }
+  if (FB_AFF) {  // the merge k_numa_fallback ran over the pair's full lists
+    const uint32_t kind = fb_aff >> 8, aff = fb_aff & 0xFFu;
+    if (kind == NFB_FAIL) {
+      o.status = KE_CODE_UNSCHEDULABLE;
+      o.reason = KE_REASON_NUMA_HINT_UNALIGNED;
+      return o;
+    }
+    o.aff = aff;
+    if (kind == NFB_FOUND) {
+      if (CS && !o.aff) allocate_on(0u);
+    } else {
+      allocate_on(o.aff);
+    }
+    return o;
+  }
   // Preferred merged hints are the masks in every present list that are preferred in each (of the
   // list's minimum size, or any size under Restricted); scanned in IterateBitMasks order with
   // mergeFilteredHints' replacement rule (narrower, else same size and higher score).
@@ -1512,14 +1606,18 @@ __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t
   int32_t bsc = 0;
   bool found = false, stop = false;
   const int smax = policy == KE_NUMA_POLICY_SINGLE_NUMA_NODE ? 1 : __popc(all);
-  for (int sz = numa_min_size(v, p); sz <= smax && !stop; sz++) {
+  for (int sz = max(numa_min_size(v, p), numa_cs_min_size<CS>(v, p, cs)); sz <= smax && !stop; sz++) {
+    if (DEFER && sz > NUMA_DEFER_SIZE) {
+      o.status = STATUS_DEFERRED;
+      return o;
+    }
     const bool first0 = minr[0] == 0, first1 = minr[1] == 0;
     for (int e = NUMA_OFF[sz]; e < NUMA_OFF[sz + 1]; e++) {
       const uint32_t m = NUMA_ORDER[e];
       if (m & ~all) continue;
       const bool in0 = present[0] && !(m & lack[0]), in1 = present[1] && !(m & lack[1]);
       if (!in0 && !in1) continue;
-      if (!numa_distribute<false, CS>(v, m, p, nullptr, dummy, cs)) continue;
+      if (!numa_fits<CS>(v, m, p, cs)) continue;
       if (in0 && !minr[0]) minr[0] = sz;
       if (in1 && !minr[1]) minr[1] = sz;
       bool cand = (!present[0] || in0) && (!present[1] || in1);
@@ -1548,7 +1646,7 @@ __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t
     o.status = STATUS_DEFERRED;
     return o;
   }
-  o.aff = FB_AFF ? fb_aff : numa_best_effort_fallback<CS>(s, i, v, p, k, present, lack, cs, ps);
+  o.aff = numa_best_effort_fallback<CS>(s, i, v, p, k, present, lack, cs, ps);
   allocate_on(o.aff);
   return o;
 }
@@ -2465,9 +2563,10 @@ __global__ __launch_bounds__(256) void k_argmax1(const uint16_t* __restrict__ sc
 //   2. c* = the smallest popcount of a non-empty merged mask m1 & m2: only merged hints of that size
 //      can end as the best (the first one is narrower than anything before it, larger ones never
 //      replace it), and between equal sizes the rule is "numerically smaller or higher score";
-//   3. 64 rows of L_cpu at a time, each lane lists its row's size-c* merged hints in L_mem order into
-//      LDS; lane 0 folds them in permutation order.
-constexpr int FALLBACK_BLOCKS = 1024;
+//   3. FB_ROWS rows of L_cpu at a time, each lane lists its row's size-c* merged hints in L_mem order
+//      into LDS; lane 0 folds them in permutation order.
+constexpr int FALLBACK_BLOCKS = 4096;
+constexpr int FB_ROWS = 16;  // rows of L_cpu per fold chunk (LDS: several pair-waves per CU)
 // CS: pods of the launch may bind CPUs — such a pair's lists come from the trimmed zones with the
 // cpuset-aware split, its hint scores from the amplified requests (eval_pair's binding branch).
 template <bool PARITY, bool CS = false>
@@ -2480,8 +2579,8 @@ __global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __res
                                                       uint8_t* __restrict__ aff_out, uint16_t* __restrict__ dsraw) {
   __shared__ int32_t s_score[256];     // hint score by mask value
   __shared__ uint8_t s_list[2][256];   // L_cpu / L_mem masks in order
-  __shared__ uint16_t s_buf[64][256];  // per-row merged hints of size c*: M | k << 8 | unsatisfied << 10
-  __shared__ int32_t s_cnt[64];
+  __shared__ uint16_t s_buf[FB_ROWS][256];  // per-row merged hints of size c*: M | k << 8 | unsatisfied << 10
+  __shared__ int32_t s_cnt[FB_ROWS];
   const int lane = threadIdx.x;
   const uint32_t n = *cnt;
   const int base = PARITY ? 0 : *batch_base;
@@ -2509,29 +2608,69 @@ __global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __res
     bool present[2];
     uint32_t lack[2];
     numa_present_lack(nv, pod, present, lack);
-    // 1. lists and scores
+    // 1. lists and scores, 64 masks (in IterateBitMasks order) per step; E[r][c]: the list membership of
+    // NUMA_ORDER[64c + lane].  2. after each step lane 0 runs numa_admit's search for the preferred merged
+    // hint over the hint sizes listed completely so far (same scan order and replacement rule, same lists):
+    // the lists' minimum sizes, candidates in both present lists (of those sizes unless Restricted),
+    // SingleNUMANode one-zone hints only.  A hint found there ends the listing.
     int len[2] = {0, 0};
-    int64_t dummy[2][8];
-    for (int c = 0; c < 4; c++) {
+    uint64_t E[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+    const int pol = pf_numa_policy(pod.flags) ? pf_numa_policy(pod.flags) : nf_numa_policy(s.flags[i]);
+    uint32_t fb = 0;
+    for (int c = 0; c < 4 && !fb; c++) {
       const int e = c * 64 + lane;
       const uint32_t m = e < 255 ? NUMA_ORDER[e] : 0u;
       bool in[2] = {false, false};
       if (m && !(m & ~nv.zm)) {
         in[0] = present[0] && !(m & lack[0]);
         in[1] = present[1] && !(m & lack[1]);
-        if ((in[0] || in[1]) && !numa_distribute<false, CS>(nv, m, pod, nullptr, dummy, &cs)) in[0] = in[1] = false;
+        if ((in[0] || in[1]) && !numa_fits<CS>(nv, m, pod, &cs)) in[0] = in[1] = false;
         if (in[0] || in[1]) s_score[m] = numa_hint_score(s, i, nv, m, ps, k);
       }
 #pragma unroll
       for (int r = 0; r < 2; r++) {
         const uint64_t bal = __ballot(in[r]);
+        E[r][c] = bal;
         if (in[r]) s_list[r][len[r] + lanes_below(bal)] = (uint8_t)m;
         len[r] += __popcll(bal);
       }
+      __syncthreads();
+      int covered = 0;  // hint sizes whose masks are all listed
+      while (covered < 8 && NUMA_OFF[covered + 2] <= 64 * (c + 1)) covered++;
+      if (lane == 0) {
+        const bool single = pol == KE_NUMA_POLICY_SINGLE_NUMA_NODE, restricted = pol == KE_NUMA_POLICY_RESTRICTED;
+        const bool excl = (pod.flags & PF_NUMA_EXCL_REQ) != 0;
+        const int R = (int)present[0] + (int)present[1];
+        const int minr0 = len[0] ? __popc(s_list[0][0]) : 9, minr1 = len[1] ? __popc(s_list[1][0]) : 9;
+        uint32_t best = 0;
+        int32_t bsc = 0;
+        bool found = false;
+        for (int sz = 1; sz <= (single ? 1 : covered) && !found; sz++) {
+          for (int q = NUMA_OFF[sz]; q < NUMA_OFF[sz + 1]; q++) {
+            const bool in0 = (E[0][q >> 6] >> (q & 63)) & 1u, in1 = (E[1][q >> 6] >> (q & 63)) & 1u;
+            if (!in0 && !in1) continue;
+            bool cand = (!present[0] || in0) && (!present[1] || in1);
+            if (!restricted) cand = cand && (!present[0] || minr0 == sz) && (!present[1] || minr1 == sz);
+            const uint32_t mm = NUMA_ORDER[q];
+            if (!cand || !exclusive_ok(nv, mm, excl)) continue;
+            const int32_t sc = R * s_score[mm];
+            if (!found || narrower(mm, best) || (__popc(mm) == __popc(best) && sc > bsc)) {
+              best = mm;
+              bsc = sc;
+              found = true;
+            }
+          }
+          if (!restricted && (!present[0] || minr0 <= sz) && (!present[1] || minr1 <= sz)) break;
+        }
+        if (found) fb = NFB_FOUND << 8 | ((single && best == nv.zm) ? 0u : best);
+        else if (c == 3 && pol != KE_NUMA_POLICY_BEST_EFFORT) fb = NFB_FAIL << 8;
+      }
+      fb = __shfl(fb, 0);
     }
-    __syncthreads();
-    uint32_t aff;
-    if ((present[0] && !len[0]) || (present[1] && !len[1])) {
+    uint32_t aff = 0;
+    if (fb) {
+      // the search decided
+    } else if ((present[0] && !len[0]) || (present[1] && !len[1])) {
       aff = nv.zm;  // filterProvidersHints reasons: unsatisfied -> any NUMA node
     } else if (!(present[0] && present[1])) {  // one list: the merged hint is the list's hint
       const int r = present[0] ? 0 : 1;
@@ -2562,9 +2701,9 @@ __global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __res
       uint32_t best = nv.zm;
       int32_t bsc = 0;
       bool bun = false;
-      for (int r0 = 0; cs <= 8 && r0 < len[0]; r0 += 64) {
+      for (int r0 = 0; cs <= 8 && r0 < len[0]; r0 += FB_ROWS) {
         int c = 0;
-        if (r0 + lane < len[0]) {
+        if (lane < FB_ROWS && r0 + lane < len[0]) {
           const uint32_t m1 = s_list[0][r0 + lane];
           for (int q = 0; q < len[1]; q++) {
             const uint32_t m2 = s_list[1][q];
@@ -2575,10 +2714,10 @@ __global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __res
             s_buf[lane][c++] = (uint16_t)(mg | kk << 8 | un << 10);
           }
         }
-        s_cnt[lane] = c;
+        if (lane < FB_ROWS) s_cnt[lane] = c;
         __syncthreads();
         if (lane == 0)
-          for (int t = 0; t < 64; t++)
+          for (int t = 0; t < FB_ROWS; t++)
             for (int q = 0; q < s_cnt[t]; q++) {
               const uint32_t e = s_buf[t][q];
               const uint32_t mg = e & 0xFFu;
@@ -2593,12 +2732,13 @@ __global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __res
       }
       aff = bun ? nv.zm : best;
     }
+    if (!fb) fb = NFB_BEST_EFFORT << 8 | aff;
     if (lane == 0) {
       NodeRegs nr;
       load_row(s, i, nr);
       prepare_row(nr);
       const bool expired = node_expired(nr, k);
-      const EvalOut o = eval_pair<false, true, false, true, CS>(nr, expired, pod, k, s, i, nv, aff);
+      const EvalOut o = eval_pair<false, true, false, true, CS>(nr, expired, pod, k, s, i, nv, fb);
       if (PARITY) {
         const int64_t o_idx = (int64_t)p * n_nodes + i;
         status[o_idx] = o.status;

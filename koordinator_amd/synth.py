@@ -636,12 +636,12 @@ def make_numa_cpus(cl, seed, zone_counts=(2, 4, 8), policy_weights=(0.1, 0.3, 0.
     return zones_out, tables
 
 
-def make_c4_cluster(n_nodes, seed):
+def make_c4_cluster(n_nodes, seed, policy_weights=(0.0, 0.3, 0.3, 0.4)):
     """128-CPU hosts (2 sockets x 4 NUMA x 8 cores x 2 threads), NUMA policy labels
     SingleNUMANode / Restricted / BestEffort 40/30/30, earlier cpusets on part of the CPUs."""
     cl = make_cluster(n_nodes, seed)
     cl.nodes["allocatable"][:, 0] = 128_000
-    zones, tables = make_numa_cpus(cl, seed + 1, zone_counts=(8,), policy_weights=(0.0, 0.3, 0.3, 0.4),
+    zones, tables = make_numa_cpus(cl, seed + 1, zone_counts=(8,), policy_weights=policy_weights,
                                    bind_weights=(1.0, 0.0, 0.0), threads=2, sockets=2)
     return cl, zones, tables
 

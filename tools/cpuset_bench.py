@@ -37,10 +37,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--survey", action="store_true", help="SURVEY.md §8d C4 spec: 128-CPU 2x4x8x2 hosts, "
                     "policies 40/30/30, LSR/LSE pods cpu {2,4,8,16} with the FullPCPUs default")
+    ap.add_argument("--policy-weights", default="", help="with --survey: None,BestEffort,Restricted,SingleNUMANode "
+                    "weights (default 0,0.3,0.3,0.4)")
     a = ap.parse_args()
     N, P, K = a.nodes, a.pods, a.steps
     if a.survey:
-        cl, zones, tables = synth.make_c4_cluster(N, synth.BASE_SEED + 4)
+        pw = tuple(float(x) for x in a.policy_weights.split(",")) if a.policy_weights else (0.0, 0.3, 0.3, 0.4)
+        cl, zones, tables = synth.make_c4_cluster(N, synth.BASE_SEED + 4, policy_weights=pw)
         pods = synth.make_c4_pods(P, synth.BASE_SEED + 104)
     else:
         cl = synth.make_cluster(N, synth.BASE_SEED + 6, amplified_fraction=0.3)
