@@ -59,7 +59,12 @@ struct AccLds {
   int16_t tmp[ACC_CPUS];
   AccTopo t;
   int max_ref, needed, excl_policy, exclusive, numa_most;
+  // loop bounds of the node's table: CPU ids < n_cpu, core ranks < n_core, socket ranks < n_sock, NUMA
+  // ids < n_numa (the byte arrays are zero past them)
+  int n_cpu, n_core, n_sock, n_numa;
 };
+
+__device__ __forceinline__ int acc_nkey(const AccLds& a, bool by_socket) { return by_socket ? a.n_sock : a.n_numa; }
 
 __device__ __forceinline__ int acc_cpc(const AccTopo& t) { return t.num_cores ? t.num_cpus / t.num_cores : 0; }
 __device__ __forceinline__ int acc_cps(const AccTopo& t) { return t.num_sockets ? t.num_cpus / t.num_sockets : 0; }
@@ -81,7 +86,7 @@ __device__ inline void acc_take(AccLds& a, const int16_t* cpus, int n) {  // :29
 }
 __device__ __forceinline__ int acc_count_alloc(const AccLds& a) {
   int n = 0;
-  for (int c = 0; c < ACC_CPUS; c++) n += a.alloc[c];
+  for (int c = 0; c < a.n_cpu; c++) n += a.alloc[c];
   return n;
 }
 __device__ __forceinline__ bool excl_pcpu(const AccLds& a, int c) { return a.excl_policy == 1 && a.ex_core[a.cpu[c].core]; }
@@ -124,11 +129,11 @@ __device__ inline int extract_cpu(AccLds& a, int16_t* v, int n) {  // :332-343
 // cores of the allocatable CPUs passing `keep` (per core rank, CPU ids ascending)
 template <typename Keep>
 __device__ inline void collect_cores(AccLds& a, Keep keep) {
-  for (int k = 0; k < ACC_CPUS; k++) a.core_n[k] = 0, a.cref[k] = 0;
+  for (int k = 0; k < a.n_core; k++) a.core_n[k] = 0, a.cref[k] = 0;
   if (a.max_ref > 1)
-    for (int c = 0; c < ACC_CPUS; c++)
+    for (int c = 0; c < a.n_cpu; c++)
       if (a.alloc[c]) a.cref[a.cpu[c].core] += a.aref[c];
-  for (int c = 0; c < ACC_CPUS; c++)
+  for (int c = 0; c < a.n_cpu; c++)
     if (a.alloc[c] && keep(c)) {
       const int k = a.cpu[c].core;
       if (a.core_n[k] < ACC_TPC) a.core_cpu[k][a.core_n[k]++] = (uint8_t)c;
@@ -151,27 +156,28 @@ __device__ inline bool cores_less(const AccLds& a, int ci, int cj) {
 __device__ inline void group_cores(AccLds& a, bool by_socket, bool filter_full) {
   const int cpc = acc_cpc(a.t);
   int16_t* cnt = a.p_key;  // per group key: cores, then the bucket's next slot
-  for (int g = 0; g < ACC_CPUS; g++) cnt[g] = 0;
-  for (int k = 0; k < ACC_CPUS; k++) {
+  const int nkey = acc_nkey(a, by_socket);
+  for (int g = 0; g < nkey; g++) cnt[g] = 0;
+  for (int k = 0; k < a.n_core; k++) {
     if (!a.core_n[k] || (filter_full && a.core_n[k] != cpc)) continue;
     const int c0 = a.core_cpu[k][0];
     cnt[by_socket ? a.cpu[c0].socket : a.cpu[c0].numa]++;
   }
   int16_t* start = a.p_sc;
   int acc = 0;
-  for (int g = 0; g < ACC_CPUS; g++) {
+  for (int g = 0; g < nkey; g++) {
     start[g] = (int16_t)acc;
     acc += cnt[g];
     cnt[g] = start[g];
   }
-  for (int k = 0; k < ACC_CPUS; k++) {  // ascending core rank within a bucket
+  for (int k = 0; k < a.n_core; k++) {  // ascending core rank within a bucket
     if (!a.core_n[k] || (filter_full && a.core_n[k] != cpc)) continue;
     const int c0 = a.core_cpu[k][0];
     a.order[cnt[by_socket ? a.cpu[c0].socket : a.cpu[c0].numa]++] = (int16_t)k;
   }
   a.ng = 0;
   int pos = 0;
-  for (int g = 0; g < ACC_CPUS; g++) {
+  for (int g = 0; g < nkey; g++) {
     const int b = start[g], nc = cnt[g] - b;
     if (nc == 0) continue;
     int16_t* o = &a.order[b];
@@ -216,8 +222,9 @@ __device__ inline void permute_groups(AccLds& a) {
 // free-CPU count per socket / NUMA node of the allocatable CPUs passing `keep`
 template <typename Keep>
 __device__ inline void free_scores(const AccLds& a, Keep keep, int16_t* per_socket, int16_t* per_node) {
-  for (int k = 0; k < ACC_CPUS; k++) per_socket[k] = 0, per_node[k] = 0;
-  for (int c = 0; c < ACC_CPUS; c++)
+  for (int k = 0; k < a.n_sock; k++) per_socket[k] = 0;
+  for (int k = 0; k < a.n_numa; k++) per_node[k] = 0;
+  for (int c = 0; c < a.n_cpu; c++)
     if (a.alloc[c] && keep(c)) per_socket[a.cpu[c].socket]++, per_node[a.cpu[c].numa]++;
 }
 
@@ -271,20 +278,21 @@ __device__ inline void free_cpus_in_group(AccLds& a, bool by_socket, bool filter
   // CPUs bucketed by group key (counting sort, ascending ids within a bucket)
   int16_t* cnt = a.p_key;
   int16_t* first = a.p_sc;
-  for (int g = 0; g < ACC_CPUS; g++) cnt[g] = 0;
-  for (int c = 0; c < ACC_CPUS; c++)
+  const int nkey = acc_nkey(a, by_socket);
+  for (int g = 0; g < nkey; g++) cnt[g] = 0;
+  for (int c = 0; c < a.n_cpu; c++)
     if (a.alloc[c] && keep(c)) cnt[by_socket ? a.cpu[c].socket : a.cpu[c].numa]++;
   int acc = 0;
-  for (int g = 0; g < ACC_CPUS; g++) {
+  for (int g = 0; g < nkey; g++) {
     first[g] = (int16_t)acc;
     acc += cnt[g];
     cnt[g] = first[g];
   }
-  for (int c = 0; c < ACC_CPUS; c++)
+  for (int c = 0; c < a.n_cpu; c++)
     if (a.alloc[c] && keep(c)) a.tmp[cnt[by_socket ? a.cpu[c].socket : a.cpu[c].numa]++] = (int16_t)c;
   a.ng = 0;
   int pos = 0;
-  for (int g = 0; g < ACC_CPUS; g++) {
+  for (int g = 0; g < nkey; g++) {
     const int b = first[g], m = cnt[g] - b;
     if (m == 0) continue;
     const int start = pos;
@@ -324,12 +332,12 @@ __device__ inline int free_cpus(AccLds& a, bool filter_excl) {
   auto keep = [&](int c) { return !(filter_excl && (excl_pcpu(a, c) || excl_numa(a, c))); };
   int16_t *sock = a.sc_sock, *node = a.sc_node, *colo = a.sc_colo;
   free_scores(a, keep, sock, node);
-  for (int s = 0; s < ACC_CPUS; s++) colo[s] = 0;
-  for (int c = 0; c < ACC_CPUS; c++)
+  for (int s = 0; s < a.n_sock; s++) colo[s] = 0;
+  for (int c = 0; c < a.n_cpu; c++)
     if ((a.cpu[c].flags & CR_VALID) && a.res[c]) colo[a.cpu[c].socket]++;
   collect_cores(a, keep);
   int nc = 0;
-  for (int k = 0; k < ACC_CPUS; k++)
+  for (int k = 0; k < a.n_core; k++)
     if (a.core_n[k]) a.order[nc++] = (int16_t)k;
   for (int i = 1; i < nc; i++)
     for (int j = i; j > 0; j--) {

@@ -3586,15 +3586,15 @@ __device__ void reserve_row(const SoA& s, int64_t node, uint32_t nf, const DevPo
 // result to a.uni.  needed <= 0 takes nothing.
 __device__ bool cpuset_take(AccLds& a, int zone, int needed, int bind) {
   if (needed <= 0) return true;
-  for (int c = 0; c < CPU_SLOTS; c++) {
+  for (int c = 0; c < a.n_cpu; c++) {
     a.alloc[c] = a.base[c] && !a.uni[c] && (zone < 0 || a.cpu[c].numa == zone);
     a.res[c] = 0;
-    a.ex_core[c] = a.ex_core0[c];
-    a.ex_node[c] = a.ex_node0[c];
   }
+  for (int k = 0; k < a.n_core; k++) a.ex_core[k] = a.ex_core0[k];
+  for (int z = 0; z < a.n_numa; z++) a.ex_node[z] = a.ex_node0[z];
   a.needed = needed;
   if (!acc_take_cpus(a, bind)) return false;
-  for (int c = 0; c < CPU_SLOTS; c++) a.uni[c] |= a.res[c];
+  for (int c = 0; c < a.n_cpu; c++) a.uni[c] |= a.res[c];
   return true;
 }
 
@@ -3612,6 +3612,8 @@ __device__ bool cpuset_allocate(const SoA& s, int64_t node, uint32_t nf, const D
   a.t.num_cores = (int)((topo >> 16) & 0xffff);
   a.t.num_nodes = (int)((topo >> 32) & 0xffff);
   a.t.num_sockets = (int)((topo >> 48) & 0xffff);
+  a.n_core = a.t.num_cores;  // dense ranks
+  a.n_sock = a.t.num_sockets;
   // getCPUBindPolicy (util.go:101-119)
   const int preq = pf_cpu_required(pod.flags), nb = nf_cpu_bind(nf);
   bool required = true;
@@ -3622,8 +3624,10 @@ __device__ bool cpuset_allocate(const SoA& s, int64_t node, uint32_t nf, const D
     else required = false, bind = pf_cpu_preferred(pod.flags);
   }
   uint8_t* navail_core = a.core_n;  // LDS scratch until the accumulator runs
-  for (int k = 0; k < CPU_SLOTS; k++) navail_core[k] = 0, a.ex_core0[k] = 0, a.ex_node0[k] = 0, a.uni[k] = 0;
-  for (int c = 0; c < CPU_SLOTS; c++) {  // a.cpu: the node's records (k_cpuset_reserve loaded them)
+  for (int k = 0; k < a.n_core; k++) navail_core[k] = 0, a.ex_core0[k] = 0;
+  for (int z = 0; z < a.n_numa; z++) a.ex_node0[z] = 0;
+  for (int c = 0; c < a.n_cpu; c++) a.uni[c] = 0;
+  for (int c = 0; c < a.n_cpu; c++) {  // a.cpu: the node's records (k_cpuset_reserve loaded them)
     const CpuRec r = a.cpu[c];
     a.base[c] = cpu_available(r, max_ref) ? 1 : 0;
     a.aref[c] = r.ref;
@@ -3634,8 +3638,8 @@ __device__ bool cpuset_allocate(const SoA& s, int64_t node, uint32_t nf, const D
     }
   }
   if (required) {
-    for (int k = 0; k < CPU_SLOTS; k++) a.mark[k] = 0;
-    for (int c = 0; c < CPU_SLOTS; c++) {
+    for (int k = 0; k < a.n_core; k++) a.mark[k] = 0;
+    for (int c = 0; c < a.n_cpu; c++) {
       if (!a.base[c]) continue;
       const int k = a.cpu[c].core;
       const bool lowest = !a.mark[k];
@@ -3644,7 +3648,7 @@ __device__ bool cpuset_allocate(const SoA& s, int64_t node, uint32_t nf, const D
     }
   }
   int navail = 0;
-  for (int c = 0; c < CPU_SLOTS; c++) navail += a.base[c];
+  for (int c = 0; c < a.n_cpu; c++) navail += a.base[c];
   const int ncpu = (int)(pod.req[0] / 1000);
   if (navail < ncpu) return false;
   a.max_ref = max_ref;
@@ -3656,20 +3660,20 @@ __device__ bool cpuset_allocate(const SoA& s, int64_t node, uint32_t nf, const D
     for (int z = 0; z < 8; z++) {
       if (!((zmask >> z) & 1u)) continue;
       int inzone = 0;
-      for (int c = 0; c < CPU_SLOTS; c++) inzone += a.base[c] && a.cpu[c].numa == z;
+      for (int c = 0; c < a.n_cpu; c++) inzone += a.base[c] && a.cpu[c].numa == z;
       if (!cpuset_take(a, z, min((int)(zcpu[z] / 1000), inzone), bind)) return false;
     }
     int got = 0;
-    for (int c = 0; c < CPU_SLOTS; c++) got += a.uni[c];
+    for (int c = 0; c < a.n_cpu; c++) got += a.uni[c];
     needed -= got;
     if (needed != 0) return false;
   }
   if (needed > 0 && !cpuset_take(a, -1, needed, bind)) return false;
-  for (int c = 0; c < CPU_SLOTS; c++) a.res[c] = a.uni[c];
+  for (int c = 0; c < a.n_cpu; c++) a.res[c] = a.uni[c];
   if (required) {
-    for (int k = 0; k < CPU_SLOTS; k++) a.mark[k] = 0;
+    for (int k = 0; k < a.n_core; k++) a.mark[k] = 0;
     int n = 0, ncore = 0;
-    for (int c = 0; c < CPU_SLOTS; c++) {
+    for (int c = 0; c < a.n_cpu; c++) {
       if (!a.res[c]) continue;
       n++;
       const int k = a.cpu[c].core;
@@ -3682,34 +3686,80 @@ __device__ bool cpuset_allocate(const SoA& s, int64_t node, uint32_t nf, const D
   return true;
 }
 
+// k_cpuset_reserve's hand-off from thread 0 to the wave, and the wave's sums
+struct CsrShared {
+  int64_t node;
+  int cs_pass, commit, excl, cpc, max_ref;
+  int cs_old[8], cs_add[8];  // allocated CPUs per NUMA id before the pod; newly allocated ones
+  uint32_t used[8];          // NUMA ids (0..255) of the cpuset
+  int zc[24];                // cs_fill's per-NUMA-id counts: available, in full cores, cores' lowest
+  int allocated, all;
+  unsigned long long set[4];
+  int core_cnt[CPU_SLOTS], core_min[CPU_SLOTS];
+};
+
 // resourceManager.Update -> addPodAllocation (node_allocation.go:111-156): RefCount++ and the pod's
 // exclusive policy on the new cpuset, the allocated-CPU count of the amplified cpu (row F_CS*) and the
-// availability counts.  The zones' NUMA status is left to the host mirror (re-derived rows).
-__device__ void cpuset_commit(const SoA& s, int64_t node, const DevPod& pod, AccLds& a, uint64_t* set) {
-  const int64_t st = s.stride;
+// availability counts (cs_fill's words, one CPU per lane step).  The zones' NUMA status is left to the
+// host mirror (re-derived rows).  Every lane of the wave; a.res = the cpuset.
+__device__ void cpuset_commit_wave(const SoA& s, AccLds& a, CsrShared& sh, int lane) {
+  const int64_t st = s.stride, node = sh.node;
   CpuRec* recs = s.cpu + node * CPU_SLOTS;
-  const int excl = (pod.flags & PF_CPU_RCB) ? pf_cpu_excl(pod.flags) : KE_CPU_EXCL_NONE;
-  int64_t allocated = 0;
-  for (int c = 0; c < CPU_SLOTS; c++) {
+  int allocated = 0, all = 0;
+  for (int c = lane; c < CPU_SLOTS; c += 64) {
     if (a.res[c]) {
-      set[c >> 6] |= 1ull << (c & 63);
-      a.cpu[c].ref++;
-      a.cpu[c].excl = (uint8_t)excl;
-      recs[c] = a.cpu[c];
+      atomicOr(&sh.set[c >> 6], 1ull << (c & 63));
+      CpuRec r = a.cpu[c];
+      r.ref++;
+      r.excl = (uint8_t)sh.excl;
+      a.cpu[c] = r;
+      recs[c] = r;
+      atomicOr(&sh.used[r.numa >> 5], 1u << (r.numa & 31));
+      if (r.numa < 8 && r.ref == 1) atomicAdd(&sh.cs_add[r.numa], 1);  // a CPU newly allocated
     }
     allocated += (a.cpu[c].flags & CR_VALID) && a.cpu[c].ref > 0;
+    sh.core_cnt[c] = 0;
+    sh.core_min[c] = CPU_SLOTS;
   }
-  int64_t* f = s.f + node;
-  const int64_t cs_milli = allocated * 1000;
-  f[F_CSM * st] = cs_milli;
-  f[F_CSAF * st] = amplify_bits(cs_milli, s.cs[CS_RF * st + node]);
-  f[F_CSAS * st] = amplify_bits(cs_milli, s.cs[CS_RS * st + node]);
-  // the availability counts, per-core counter in LDS
-  const int64_t cnt = s.cs[CS_CNT * st + node];
-  int64_t ncnt;
-  cs_fill(a.cpu, cs_cpc(cnt), cs_max_ref(cnt), a.core_n, &ncnt, a.z6);
-  s.cs[CS_CNT * st + node] = ncnt;
-  for (int w = 0; w < 6; w++) s.cs[(CS_ZALL + w) * st + node] = a.z6[w];
+  allocated = wave_sum(allocated);
+  __syncthreads();
+  for (int c = lane; c < CPU_SLOTS; c += 64)  // available CPUs per core, its lowest available id
+    if (cpu_available(a.cpu[c], sh.max_ref)) {
+      atomicAdd(&sh.core_cnt[a.cpu[c].core], 1);
+      atomicMin(&sh.core_min[a.cpu[c].core], c);
+      all++;
+    }
+  all = wave_sum(all);
+  __syncthreads();
+  const int cpc = sh.cpc;
+  int full = 0, spread = 0;
+  for (int kk = lane; kk < CPU_SLOTS; kk += 64) {
+    if (sh.core_cnt[kk] == cpc && cpc > 0) full += cpc;
+    if (sh.core_cnt[kk] > 0) spread++;
+  }
+  full = wave_sum(full);
+  spread = wave_sum(spread);
+  for (int c = lane; c < CPU_SLOTS; c += 64) {
+    const CpuRec r = a.cpu[c];
+    if (!cpu_available(r, sh.max_ref) || r.numa >= 8) continue;
+    atomicAdd(&sh.zc[r.numa], 1);                                     // available
+    if (sh.core_cnt[r.core] == cpc) atomicAdd(&sh.zc[8 + r.numa], 1);  // in a fully available core
+    if (sh.core_min[r.core] == c) atomicAdd(&sh.zc[16 + r.numa], 1);  // the core's lowest available CPU
+  }
+  __syncthreads();
+  if (lane == 0) {
+    int64_t* f = s.f + node;
+    const int64_t cs_milli = (int64_t)allocated * 1000;
+    f[F_CSM * st] = cs_milli;
+    f[F_CSAF * st] = amplify_bits(cs_milli, s.cs[CS_RF * st + node]);
+    f[F_CSAS * st] = amplify_bits(cs_milli, s.cs[CS_RS * st + node]);
+    s.cs[CS_CNT * st + node] = cs_pack(full, spread, cpc, sh.max_ref, all);
+    for (int w = 0; w < 6; w++) {  // CS_Z* words: 16-bit counts of NUMA ids 4 (w & 1) .. 4 (w & 1) + 3
+      int64_t word = 0;
+      for (int q = 0; q < 4; q++) word |= (int64_t)sh.zc[8 * (w >> 1) + 4 * (w & 1) + q] << (16 * q);
+      s.cs[(CS_ZALL + w) * st + node] = word;
+    }
+  }
 }
 
 // A singleton batch of a pod that may bind CPUs, after k_select: selectHost's node, then Reserve in
@@ -3736,39 +3786,64 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
     if (threadIdx.x == 0) s_w = wmax;
     __syncthreads();
     if (s_w && s.cpu) {
+      // the records, the table's bounds (highest CPU id / NUMA id + 1) and the zeroed per-CPU byte
+      // arrays the accumulator's loops stop short of
       const CpuRec* recs = s.cpu + (int64_t)key_node(s_w) * CPU_SLOTS;
-      for (int c = threadIdx.x; c < CPU_SLOTS; c += 64) a.cpu[c] = recs[c];
+      int top_cpu = 0, top_numa = 0;
+      for (int c = threadIdx.x; c < CPU_SLOTS; c += 64) {
+        const CpuRec r = recs[c];
+        a.cpu[c] = r;
+        a.alloc[c] = a.res[c] = a.base[c] = a.uni[c] = a.mark[c] = 0;
+        if (r.flags & CR_VALID) top_cpu = c + 1, top_numa = max(top_numa, (int)r.numa + 1);
+      }
+      top_cpu = (int)wave_max_u32((uint32_t)top_cpu);
+      top_numa = (int)wave_max_u32((uint32_t)top_numa);
+      if (threadIdx.x == 0) a.n_cpu = top_cpu, a.n_numa = top_numa;
     }
     __syncthreads();
   }
-  if (threadIdx.x != 0) return;
+  // Thread 0 selects, admits and runs the accumulator; the wave commits the cpuset and re-derives the
+  // node's availability words (cs_fill) in parallel; thread 0 then patches the NUMA zones and devices.
+  __shared__ CsrShared sh;
+  const int lane = threadIdx.x;
+  RPROF_DECL
   const DevPod pod = pods[base];
   int64_t qreq[2] = {0, 0};  // ElasticQuota PreFilter: a refused pod is placed nowhere
   const bool quota = (k.flags & AF_QUOTA) && pod.quota;
-  const uint32_t w = (!quota || quota_admit_g(s, pod, k, qreq)) ? s_w : 0u;
+  uint32_t w = 0;
   int32_t out_node = -1, out_score = -1;
-  uint64_t alloc = 0, set[4] = {0, 0, 0, 0};
+  uint64_t alloc = 0;
   int64_t* out16 = numa_alloc ? numa_alloc + (int64_t)base * 16 : nullptr;
-  if (out16)
-    for (int t = 0; t < 16; t++) out16[t] = 0;
-  if (w) {
-    const int64_t node = key_node(w);
-    const uint32_t nf = s.flags[node];
-    const bool rcb = !(pod.flags & PF_NUMA_SKIP) &&
-                     ((pod.flags & PF_CPU_RCB) ||
-                      (pod.req[0] != 0 && nf_cpu_bind(nf) != KE_NODE_CPU_BIND_NONE && (pod.flags & PF_CPU_INT)));
+  int64_t node = 0;
+  uint32_t nf = 0;
+  bool rcb = false, nsoa = false, ok = false, ds_here = false, stored = false;
+  NumaNode v;
+  v.zm = 0;
+  uint32_t got[2] = {0, 0}, aff = 0;
+  int64_t dist[2][8] = {{0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0, 0}};
+  if (lane == 0) {
+    sh.cs_pass = 0;
+    sh.commit = 0;
+    for (int q = 0; q < 4; q++) sh.set[q] = 0;
+    for (int z = 0; z < 8; z++) sh.cs_old[z] = sh.cs_add[z] = sh.used[z] = 0;
+    for (int z = 0; z < 24; z++) sh.zc[z] = 0;
+    sh.allocated = sh.all = 0;
+    w = (!quota || quota_admit_g(s, pod, k, qreq)) ? s_w : 0u;
+    if (out16)
+      for (int t = 0; t < 16; t++) out16[t] = 0;
+  }
+  if (lane == 0 && w) {
+    node = key_node(w);
+    nf = s.flags[node];
+    rcb = !(pod.flags & PF_NUMA_SKIP) &&
+          ((pod.flags & PF_CPU_RCB) || (pod.req[0] != 0 && nf_cpu_bind(nf) != KE_NODE_CPU_BIND_NONE && (pod.flags & PF_CPU_INT)));
     const int pol = pf_numa_policy(pod.flags) ? pf_numa_policy(pod.flags) : nf_numa_policy(nf);
-    const bool nsoa = NUMA && s.nm != nullptr;  // the node's zones (if any) live in the NUMA SoA
+    nsoa = NUMA && s.nm != nullptr;  // the node's zones (if any) live in the NUMA SoA
     const bool npol = nsoa && !(pod.flags & PF_NUMA_SKIP) && pol != KE_NUMA_POLICY_NONE;
-    bool ok = !rcb || (nf & NF_CPUS_VALID);
-    NumaNode v;
+    ok = !rcb || (nf & NF_CPUS_VALID);
     if (nsoa) numa_load(s, node, v);
-    uint32_t got[2] = {0, 0};
-    int64_t dist[2][8] = {{0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0, 0}};
     // DeviceShare's hints join the Admit of a pod with device requests (topology_hint.go:38-58)
-    const bool ds_here = DS && (pod.flags & PF_DS) && (nf & NF_DS_CACHE);
-    bool stored = false;
-    uint32_t aff = 0;
+    ds_here = DS && (pod.flags & PF_DS) && (nf & NF_DS_CACHE);
     if (ok && npol) {  // the affinity the Filter's Admit stored and the allocation on it
       // this rank evaluated the node: its eval stored the affinity (a feasible node admitted, binding pods);
       // else (a node of another shard, a DeviceShare pod) Admit runs here
@@ -3795,64 +3870,78 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
       stored = pk.status == KE_CODE_SUCCESS;
       aff = pk.aff;
     }
-    int cs_old[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // allocated CPUs per NUMA id before the pod
-    if (nsoa && v.zm && s.cpu)
-      for (int c = 0; c < CPU_SLOTS; c++) {
-        const CpuRec r = a.cpu[c];
-        if ((r.flags & CR_VALID) && r.ref > 0 && r.numa < 8) cs_old[r.numa]++;
-      }
+    RPROF(0)
     // DeviceShare Reserve allocates on the stored affinity unless the alignment is disabled (plugin.go:452-466);
     // with the alignment disabled nothing checked the devices of a NUMA-admitted node (Filter skipped,
     // Allocate a no-op), so the allocation may fail: Reserve fails and every Reserve of the pod is undone
-    const DsAff da{stored && aff != 0 && !(k.flags & AF_DS_NO_NUMA), aff};
     if (ok && ds_here && stored && (k.flags & AF_DS_NO_NUMA)) {  // elsewhere the Filter / Admit checked it
       int why = 0;
-      ok = ds_try_allocate(s, node, pod, k, da, nullptr, &why) == KE_CODE_SUCCESS;
+      ok = ds_try_allocate(s, node, pod, k, DsAff{false, 0u}, nullptr, &why) == KE_CODE_SUCCESS;  // Reserve: no affinity
     }
+    RPROF(1)
     if (ok && rcb) {
       const int64_t zcpu[8] = {dist[0][0], dist[0][1], dist[0][2], dist[0][3],
                                dist[0][4], dist[0][5], dist[0][6], dist[0][7]};
       ok = cpuset_allocate(s, node, nf, pod, a, got[0] | got[1], zcpu);
     }
+    RPROF(2)
     if (ok) {
       reserve_row(s, node, nf, pod);
       {  // the node's replay record follows its patched row
         NodeRegs nr;
         load_row(s, node, nr);
         prepare_row(nr);
-        int64_t w[NUM_RW];
-        rec_from_regs(nr, k, w);
-        for (int u = 0; u < NUM_RW; u++) s.rec[node * NUM_RW + u] = w[u];
+        int64_t wr[NUM_RW];
+        rec_from_regs(nr, k, wr);
+        for (int u = 0; u < NUM_RW; u++) s.rec[node * NUM_RW + u] = wr[u];
       }
-      uint32_t used = 0;
-      int n_used = 0;
-      int cs_new[8] = {cs_old[0], cs_old[1], cs_old[2], cs_old[3], cs_old[4], cs_old[5], cs_old[6], cs_old[7]};
+      sh.cs_pass = nsoa && v.zm && s.cpu;  // allocated CPUs per NUMA id before the pod
+      sh.commit = rcb;
       if (rcb) {
-        cpuset_commit(s, node, pod, a, set);
-        for (int c = 0; c < CPU_SLOTS; c++) a.mark[c] = 0;
-        for (int c = 0; c < CPU_SLOTS; c++) {
-          if (!a.res[c]) continue;
-          const int z = a.cpu[c].numa;
-          if (!a.mark[z]) n_used++;
-          a.mark[z] = 1;
-          if (z < 8) used |= 1u << z, cs_new[z] += a.cpu[c].ref == 1;  // a CPU newly allocated
-        }
+        const int64_t cnt = s.cs[CS_CNT * s.stride + node];
+        sh.node = node;
+        sh.excl = (pod.flags & PF_CPU_RCB) ? pf_cpu_excl(pod.flags) : KE_CPU_EXCL_NONE;
+        sh.cpc = cs_cpc(cnt);
+        sh.max_ref = cs_max_ref(cnt);
       }
+    }
+    RPROF(3)
+  }
+  __syncthreads();
+  if (sh.cs_pass) {
+    for (int c = lane; c < CPU_SLOTS; c += 64) {
+      const CpuRec r = a.cpu[c];
+      if ((r.flags & CR_VALID) && r.ref > 0 && r.numa < 8) atomicAdd(&sh.cs_old[r.numa], 1);
+    }
+    __syncthreads();
+  }
+  if (sh.commit) cpuset_commit_wave(s, a, sh, lane);
+  if (lane == 0) {
+    RPROF(4)
+    if (ok) {
+      uint32_t used = sh.used[0] & 0xFFu;
+      int n_used = 0;
+      for (int q = 0; q < 8; q++) n_used += __popc(sh.used[q]);
+      int cs_old[8], cs_new[8];
+      for (int z = 0; z < 8; z++) cs_old[z] = sh.cs_old[z], cs_new[z] = sh.cs_old[z] + sh.cs_add[z];
       if (nsoa && v.zm) numa_reserve_cs(s, node, nf, v, got, dist, cs_old, cs_new, used, n_used, out16);
-      if (ds_here) alloc = ds_reserve(s, node, pod, k, da);
+      RPROF(5)
+      if (ds_here) alloc = ds_reserve(s, node, pod, k, DsAff{stored && aff != 0 && !(k.flags & AF_DS_NO_NUMA), aff});
       out_node = (int32_t)node + global_offset;
       out_score = key_score(w);
       if (quota) quota_reserve_g(s, pod, qreq);  // ElasticQuota Reserve
     }
+    RPROF(6)
+    RPROF_FLUSH(1)
+    chosen[base] = out_node;
+    chosen_score[base] = out_score;
+    dev_alloc[base] = alloc;
+    for (int q = 0; q < 4; q++) cpusets[(int64_t)base * 4 + q] = sh.set[q];
+    for (int u = 0; u < 6; u++) pstamps[8 * batch_index + u] = t0;  // no prologue: all "replay"
+    pstamps[8 * batch_index + 6] = 1;
+    pstamps[8 * batch_index + 7] = out_node >= 0;
+    stamps[batch_index + 1] = __builtin_amdgcn_s_memrealtime();
   }
-  chosen[base] = out_node;
-  chosen_score[base] = out_score;
-  dev_alloc[base] = alloc;
-  for (int q = 0; q < 4; q++) cpusets[(int64_t)base * 4 + q] = set[q];
-  for (int u = 0; u < 6; u++) pstamps[8 * batch_index + u] = t0;  // no prologue: all "replay"
-  pstamps[8 * batch_index + 6] = 1;
-  pstamps[8 * batch_index + 7] = out_node >= 0;
-  stamps[batch_index + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
 __global__ void k_stamp(uint64_t* stamps) { stamps[0] = __builtin_amdgcn_s_memrealtime(); }
