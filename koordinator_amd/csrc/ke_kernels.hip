@@ -3583,18 +3583,21 @@ __device__ void reserve_row(const SoA& s, int64_t node, uint32_t nf, const DevPo
 
 // One takePreferredCPUs call (no preferred CPUs = takeCPUs, cpu_accumulator.go:29-85) over the CPUs of
 // `a.base` in NUMA id `zone` (-1 = all) not yet in `a.uni`, from the pre-pod exclusivity; adds the
-// result to a.uni.  needed <= 0 takes nothing.
+// result to a.uni.  needed <= 0 takes nothing.  All lanes (ke_cpuacc.h).
 __device__ bool cpuset_take(AccLds& a, int zone, int needed, int bind) {
   if (needed <= 0) return true;
-  for (int c = 0; c < a.n_cpu; c++) {
+  const int L = threadIdx.x;
+  for (int c = L; c < a.n_cpu; c += 64) {
     a.alloc[c] = a.base[c] && !a.uni[c] && (zone < 0 || a.cpu[c].numa == zone);
     a.res[c] = 0;
   }
-  for (int k = 0; k < a.n_core; k++) a.ex_core[k] = a.ex_core0[k];
-  for (int z = 0; z < a.n_numa; z++) a.ex_node[z] = a.ex_node0[z];
-  a.needed = needed;
+  for (int k = L; k < a.n_core; k += 64) a.ex_core[k] = a.ex_core0[k];
+  for (int z = L; z < a.n_numa; z += 64) a.ex_node[z] = a.ex_node0[z];
+  if (L == 0) a.needed = needed;
+  __syncthreads();
   if (!acc_take_cpus(a, bind)) return false;
-  for (int c = 0; c < a.n_cpu; c++) a.uni[c] |= a.res[c];
+  for (int c = L; c < a.n_cpu; c += 64) a.uni[c] |= a.res[c];
+  __syncthreads();
   return true;
 }
 
@@ -3602,18 +3605,13 @@ __device__ bool cpuset_take(AccLds& a, int zone, int needed, int bind) {
 // required-policy filter (filterCPUsByRequiredCPUBindPolicy :655-695); with a NUMA allocation (zones
 // `zmask`, cpu milli `zcpu[id]`) one take per zone in id order of min(cpu/1000, its CPUs) CPUs, which
 // must add up to numCPUsNeeded; else one take over the node; then satisfiedRequiredCPUBindPolicy
-// (:697-718).  Thread 0 only; a.res = the cpuset.
+// (:697-718).  All lanes of the workgroup, same arguments; a.res = the cpuset.
 __device__ bool cpuset_allocate(const SoA& s, int64_t node, uint32_t nf, const DevPod& pod, AccLds& a, uint32_t zmask,
-                                const int64_t (&zcpu)[8]) {
+                                const int64_t* zcpu) {
+  const int L = threadIdx.x;
   const int64_t st = s.stride;
   const int64_t cnt = s.cs[CS_CNT * st + node], topo = s.cs[CS_TOPO * st + node];
   const int max_ref = cs_max_ref(cnt), cpc = cs_cpc(cnt);
-  a.t.num_cpus = (int)(topo & 0xffff);
-  a.t.num_cores = (int)((topo >> 16) & 0xffff);
-  a.t.num_nodes = (int)((topo >> 32) & 0xffff);
-  a.t.num_sockets = (int)((topo >> 48) & 0xffff);
-  a.n_core = a.t.num_cores;  // dense ranks
-  a.n_sock = a.t.num_sockets;
   // getCPUBindPolicy (util.go:101-119)
   const int preq = pf_cpu_required(pod.flags), nb = nf_cpu_bind(nf);
   bool required = true;
@@ -3623,65 +3621,85 @@ __device__ bool cpuset_allocate(const SoA& s, int64_t node, uint32_t nf, const D
     else if (nb == KE_NODE_CPU_BIND_FULL_PCPUS_ONLY) bind = XB_FULL;
     else required = false, bind = pf_cpu_preferred(pod.flags);
   }
-  uint8_t* navail_core = a.core_n;  // LDS scratch until the accumulator runs
-  for (int k = 0; k < a.n_core; k++) navail_core[k] = 0, a.ex_core0[k] = 0;
-  for (int z = 0; z < a.n_numa; z++) a.ex_node0[z] = 0;
-  for (int c = 0; c < a.n_cpu; c++) a.uni[c] = 0;
-  for (int c = 0; c < a.n_cpu; c++) {  // a.cpu: the node's records (k_cpuset_reserve loaded them)
+  if (L == 0) {
+    a.t.num_cpus = (int)(topo & 0xffff);
+    a.t.num_cores = (int)((topo >> 16) & 0xffff);
+    a.t.num_nodes = (int)((topo >> 32) & 0xffff);
+    a.t.num_sockets = (int)((topo >> 48) & 0xffff);
+    a.n_core = a.t.num_cores;  // dense ranks
+    a.n_sock = a.t.num_sockets;
+    a.max_ref = max_ref;
+    a.excl_policy = (pod.flags & PF_CPU_RCB) ? pf_cpu_excl(pod.flags) : KE_CPU_EXCL_NONE;
+    a.exclusive = a.excl_policy == KE_CPU_EXCL_PCPU_LEVEL || a.excl_policy == KE_CPU_EXCL_NUMA_NODE_LEVEL;
+    a.numa_most = (nf & NF_CPU_NUMA_MOST) ? 1 : 0;
+  }
+  __syncthreads();
+  int32_t* navail_core = a.core_n;  // LDS scratch until the accumulator runs
+  for (int k = L; k < a.n_core; k += 64) navail_core[k] = 0, a.ex_core0[k] = 0;
+  for (int z = L; z < a.n_numa; z += 64) a.ex_node0[z] = 0;
+  for (int c = L; c < a.n_cpu; c += 64) a.uni[c] = 0;
+  __syncthreads();
+  for (int c = L; c < a.n_cpu; c += 64) {  // a.cpu: the node's records (k_cpuset_reserve loaded them)
     const CpuRec r = a.cpu[c];
     a.base[c] = cpu_available(r, max_ref) ? 1 : 0;
     a.aref[c] = r.ref;
-    if (a.base[c]) navail_core[r.core]++;
+    if (a.base[c]) atomicAdd(&navail_core[r.core], 1);
     if ((r.flags & CR_VALID) && r.ref > 0) {  // exclusiveInCores / exclusiveInNUMANodes of the allocated CPUs
       if (r.excl == KE_CPU_EXCL_PCPU_LEVEL) a.ex_core0[r.core] = 1;
       else if (r.excl == KE_CPU_EXCL_NUMA_NODE_LEVEL) a.ex_node0[r.numa] = 1;
     }
   }
-  if (required) {
-    for (int k = 0; k < a.n_core; k++) a.mark[k] = 0;
-    for (int c = 0; c < a.n_cpu; c++) {
-      if (!a.base[c]) continue;
-      const int k = a.cpu[c].core;
-      const bool lowest = !a.mark[k];
-      a.mark[k] = 1;
-      if ((bind == XB_FULL && navail_core[k] != cpc) || (bind == XB_SPREAD && !lowest)) a.base[c] = 0;
+  __syncthreads();
+  if (required) {  // FullPCPUs: CPUs of fully available cores; SpreadByPCPUs: each core's lowest CPU
+    if (L == 0) {
+      for (int k = 0; k < a.n_core; k++) a.mark[k] = 0;
+      for (int c = 0; c < a.n_cpu; c++) {
+        if (!a.base[c]) continue;
+        const int k = a.cpu[c].core;
+        const bool lowest = !a.mark[k];
+        a.mark[k] = 1;
+        if ((bind == XB_FULL && navail_core[k] != cpc) || (bind == XB_SPREAD && !lowest)) a.base[c] = 0;
+      }
     }
+    __syncthreads();
   }
   int navail = 0;
-  for (int c = 0; c < a.n_cpu; c++) navail += a.base[c];
+  for (int c = L; c < a.n_cpu; c += 64) navail += a.base[c];
+  navail = acc_wave_sum(navail);
   const int ncpu = (int)(pod.req[0] / 1000);
   if (navail < ncpu) return false;
-  a.max_ref = max_ref;
-  a.excl_policy = (pod.flags & PF_CPU_RCB) ? pf_cpu_excl(pod.flags) : KE_CPU_EXCL_NONE;
-  a.exclusive = a.excl_policy == KE_CPU_EXCL_PCPU_LEVEL || a.excl_policy == KE_CPU_EXCL_NUMA_NODE_LEVEL;
-  a.numa_most = (nf & NF_CPU_NUMA_MOST) ? 1 : 0;
   int needed = ncpu;
   if (zmask) {
     for (int z = 0; z < 8; z++) {
       if (!((zmask >> z) & 1u)) continue;
       int inzone = 0;
-      for (int c = 0; c < a.n_cpu; c++) inzone += a.base[c] && a.cpu[c].numa == z;
+      for (int c = L; c < a.n_cpu; c += 64) inzone += a.base[c] && a.cpu[c].numa == z;
+      inzone = acc_wave_sum(inzone);
       if (!cpuset_take(a, z, min((int)(zcpu[z] / 1000), inzone), bind)) return false;
     }
     int got = 0;
-    for (int c = 0; c < a.n_cpu; c++) got += a.uni[c];
-    needed -= got;
+    for (int c = L; c < a.n_cpu; c += 64) got += a.uni[c];
+    needed -= acc_wave_sum(got);
     if (needed != 0) return false;
   }
   if (needed > 0 && !cpuset_take(a, -1, needed, bind)) return false;
-  for (int c = 0; c < a.n_cpu; c++) a.res[c] = a.uni[c];
+  for (int c = L; c < a.n_cpu; c += 64) a.res[c] = a.uni[c];
+  __syncthreads();
   if (required) {
-    for (int k = 0; k < a.n_core; k++) a.mark[k] = 0;
-    int n = 0, ncore = 0;
-    for (int c = 0; c < a.n_cpu; c++) {
-      if (!a.res[c]) continue;
-      n++;
-      const int k = a.cpu[c].core;
-      if (!a.mark[k]) ncore++;
-      a.mark[k] = 1;
+    if (L == 0) {
+      for (int k = 0; k < a.n_core; k++) a.mark[k] = 0;
+      int n = 0, ncore = 0;
+      for (int c = 0; c < a.n_cpu; c++) {
+        if (!a.res[c]) continue;
+        n++;
+        const int k = a.cpu[c].core;
+        if (!a.mark[k]) ncore++;
+        a.mark[k] = 1;
+      }
+      a.bcast = !((bind == XB_FULL && ncore * cpc != n) || (bind == XB_SPREAD && ncore != n));
     }
-    if (bind == XB_FULL && ncore * cpc != n) return false;
-    if (bind == XB_SPREAD && ncore != n) return false;
+    __syncthreads();
+    if (!a.bcast) return false;
   }
   return true;
 }
@@ -3689,7 +3707,9 @@ __device__ bool cpuset_allocate(const SoA& s, int64_t node, uint32_t nf, const D
 // k_cpuset_reserve's hand-off from thread 0 to the wave, and the wave's sums
 struct CsrShared {
   int64_t node;
-  int cs_pass, commit, excl, cpc, max_ref;
+  int64_t zcpu[8];  // the NUMA allocation's cpu per id (cpuset_allocate's zones)
+  uint32_t nf, zmask;
+  int take, cs_pass, commit, excl, cpc, max_ref;
   int cs_old[8], cs_add[8];  // allocated CPUs per NUMA id before the pod; newly allocated ones
   uint32_t used[8];          // NUMA ids (0..255) of the cpuset
   int zc[24];                // cs_fill's per-NUMA-id counts: available, in full cores, cores' lowest
@@ -3824,6 +3844,7 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
   if (lane == 0) {
     sh.cs_pass = 0;
     sh.commit = 0;
+    sh.take = 0;
     for (int q = 0; q < 4; q++) sh.set[q] = 0;
     for (int z = 0; z < 8; z++) sh.cs_old[z] = sh.cs_add[z] = sh.used[z] = 0;
     for (int z = 0; z < 24; z++) sh.zc[z] = 0;
@@ -3879,11 +3900,20 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
       ok = ds_try_allocate(s, node, pod, k, DsAff{false, 0u}, nullptr, &why) == KE_CODE_SUCCESS;  // Reserve: no affinity
     }
     RPROF(1)
-    if (ok && rcb) {
-      const int64_t zcpu[8] = {dist[0][0], dist[0][1], dist[0][2], dist[0][3],
-                               dist[0][4], dist[0][5], dist[0][6], dist[0][7]};
-      ok = cpuset_allocate(s, node, nf, pod, a, got[0] | got[1], zcpu);
+    sh.take = ok && rcb;
+    if (sh.take) {
+      sh.node = node;
+      sh.nf = nf;
+      sh.zmask = got[0] | got[1];
+      for (int z = 0; z < 8; z++) sh.zcpu[z] = dist[0][z];
     }
+  }
+  __syncthreads();
+  if (sh.take) {  // the accumulator on the whole wave
+    const bool took = cpuset_allocate(s, sh.node, sh.nf, pod, a, sh.zmask, sh.zcpu);
+    if (lane == 0) ok = took;
+  }
+  if (lane == 0 && w) {
     RPROF(2)
     if (ok) {
       reserve_row(s, node, nf, pod);
