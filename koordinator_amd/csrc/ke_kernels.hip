@@ -361,6 +361,29 @@ __constant__ uint8_t NUMA_ORDER[255] = {
     223, 239, 247, 251, 253, 254, 255};
 __constant__ uint8_t NUMA_OFF[10] = {0, 0, 8, 36, 92, 162, 218, 246, 254, 255};  // first entry of each size
 
+// Diagnostic build (-DKE_PROF_REPLAY, tools/replay_phases.sh): shader-clock cycles of each phase of
+// the per-pod replay loop, summed over every pod into g_rprof (ke_debug_replay_phases).  Off in the
+// product build (the macro expands to nothing).
+#ifdef KE_PROF_REPLAY
+__device__ unsigned long long g_rprof[8];
+#define RPROF_DECL uint64_t rp_[7] = {0, 0, 0, 0, 0, 0, 0}, rp_t = __builtin_amdgcn_s_memtime();
+#define RPROF(i)                                         \
+  {                                                      \
+    const uint64_t rp_n = __builtin_amdgcn_s_memtime(); \
+    rp_[i] += rp_n - rp_t;                               \
+    rp_t = rp_n;                                         \
+  }
+#define RPROF_FLUSH(npods)                                                           \
+  if (lane == 0) {                                                                   \
+    for (int u_ = 0; u_ < 7; u_++) atomicAdd(&g_rprof[u_], (unsigned long long)rp_[u_]); \
+    atomicAdd(&g_rprof[7], (unsigned long long)(npods));                             \
+  }
+#else
+#define RPROF_DECL
+#define RPROF(i)
+#define RPROF_FLUSH(npods)
+#endif
+
 // ---- GPUAllocator.Allocate (allocator_gpu.go:72-451) ------------------------------------------------
 // The node's GPUs as AllocateContext sees them, as minor masks.
 struct GpuMasks {
@@ -1171,10 +1194,57 @@ __device__ __forceinline__ int numa_cs_min_size(const NumaNode& v, const DevPod&
   return sum >= cs->num ? k : 9;
 }
 
+// numa_distribute<false, CS> for a two-zone mask: the two split steps unrolled; the zones' availability
+// read at their uniform ids, the distribute order (per lane) picks between them.
+template <bool CS>
+__device__ __forceinline__ bool numa_fits2(const NumaNode& v, uint32_t m, const DevPod& p, const NumaCs* cs) {
+  if (!numa_sum_fits(v, m, p)) return false;
+  const int za = __ffs(m) - 1, zb = 31 - __clz(m);
+  const bool bind = CS && cs->rcb;
+  bool ok = true, any = false, aligned = true;
+  int taken = 0;
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    if (!ok) break;
+    if (!numa_checked(v, p, r)) continue;
+    const uint32_t perm = v.perm[r][1];  // slots 0, 1 hold positions 0 / 1 of the mask's zones
+    const int64_t aa = pick8(v.av[r], za), ab = pick8(v.av[r], zb);
+    int64_t q = p.req[r];
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      const bool first_zone = ((perm >> (4 * t)) & 15u) == 0;
+      const int z = first_zone ? za : zb;
+      const int64_t a = first_zone ? aa : ab;
+      int64_t split = t == 0 ? q / 2 : q;  // splitQuantity
+      if (bind && r == 0) {
+        const int val = (int)(q >= 0 ? (q + 999) / 1000 : -((-q + 999) / 1000));  // Quantity.Value()
+        split = cs->full ? (int64_t)((val / cs->cpc) / (2 - t)) * cs->cpc * 1000 : (int64_t)(val / (2 - t)) * 1000;
+      }
+      const int64_t got = a > split ? split : a;  // allocateRes
+      q -= got;
+      if (got != 0) {
+        any = true;
+        if (bind && r == 0) {
+          const int kk = min((int)(got / 1000), cs_zc(*cs, z));
+          if (kk > 0) {
+            taken += kk;
+            if (kk % cs->cpc) aligned = false;
+          }
+        }
+      }
+    }
+    if (q != 0) ok = false;
+  }
+  if (bind) ok = ok && cs->total >= cs->num && (!any || (taken == cs->num && (!cs->full || aligned)));
+  return ok;
+}
+
 template <bool CS = false>
 __device__ __forceinline__ bool numa_fits(const NumaNode& v, uint32_t m, const DevPod& p, const NumaCs* cs = nullptr) {
   if (!numa_cs_counts_ok<CS>(v, m, p, cs)) return false;
-  if (__popc(m) != 1) {
+  const int nb = __popc(m);
+  if (nb == 2 && (!CS || !cs->rcb || (p.req[0] >= 0 && p.req[0] < (1ll << 40)))) return numa_fits2<CS>(v, m, p, cs);
+  if (nb != 1) {
     int64_t dummy[2][8];
     return numa_distribute<false, CS>(v, m, p, nullptr, dummy, cs);
   }
@@ -1279,7 +1349,6 @@ __device__ __forceinline__ uint32_t numa_best_effort_fallback(const SoA& s, int6
                                                            const DevPod* ps = nullptr) {
   const DevPod& sp = CS ? *ps : p;
   uint64_t L[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-  int64_t dummy[2][8];
   for (int e = 0; e < 255; e++) {
     const uint32_t m = NUMA_ORDER[e];
     if (m & ~v.zm) continue;
@@ -1444,7 +1513,6 @@ __device__ __noinline__ NumaPick numa_admit_ds(const SoA& s, int64_t i, int poli
   const int R = (int)present[0] + (int)present[1];
   uint64_t L[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
   int minr[2] = {9, 9};
-  int64_t dummy[2][8];
   for (int e = 0; e < 255; e++) {  // generateResourceHints: the feasible masks per resource
     const uint32_t m = NUMA_ORDER[e];
     if (m & ~all) continue;
@@ -1572,7 +1640,6 @@ __device__ __forceinline__ NumaPick numa_admit(const SoA& s, int64_t i, uint32_t
   uint32_t lack[2];
   numa_present_lack(v, p, present, lack);
   const int R = (int)present[0] + (int)present[1];
-  int64_t dummy[2][8];
   if (R == 0) {  // no hints: one preferred any-NUMA hint per provider -> merged = all zones
     if (policy != KE_NUMA_POLICY_BEST_EFFORT && !exclusive_ok(v, all, excl)) {
       o.status = KE_CODE_UNSCHEDULABLE;
@@ -2576,11 +2643,13 @@ __global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __res
                                                       uint16_t* __restrict__ scores, int64_t score_stride, int n_nodes,
                                                       uint8_t* status, uint8_t* reason, int16_t* la, int16_t* numa,
                                                       int16_t* ds, int16_t* total, uint32_t* dsmax,
-                                                      uint8_t* __restrict__ aff_out, uint16_t* __restrict__ dsraw) {
+                                                      uint8_t* __restrict__ aff_out, uint16_t* __restrict__ dsraw,
+                                                      uint32_t* __restrict__ fb_out) {
   __shared__ int32_t s_score[256];     // hint score by mask value
   __shared__ uint8_t s_list[2][256];   // L_cpu / L_mem masks in order
   __shared__ uint16_t s_buf[FB_ROWS][256];  // per-row merged hints of size c*: M | k << 8 | unsatisfied << 10
   __shared__ int32_t s_cnt[FB_ROWS];
+  __shared__ uint64_t s_E[2][4];       // list membership by NUMA_ORDER index (LDS: read at runtime indices)
   const int lane = threadIdx.x;
   const uint32_t n = *cnt;
   const int base = PARITY ? 0 : *batch_base;
@@ -2588,6 +2657,7 @@ __global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __res
     const uint64_t it = list[w];
     const int p = (int)(it >> 32);
     const int64_t i = (int64_t)(uint32_t)it;
+    RPROF_DECL
     const DevPod pod = pods[base + p];
     NumaNode nv;
     numa_load(s, i, nv);
@@ -2608,18 +2678,28 @@ __global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __res
     bool present[2];
     uint32_t lack[2];
     numa_present_lack(nv, pod, present, lack);
+    RPROF(3)
     // 1. lists and scores, 64 masks (in IterateBitMasks order) per step; E[r][c]: the list membership of
     // NUMA_ORDER[64c + lane].  2. after each step lane 0 runs numa_admit's search for the preferred merged
     // hint over the hint sizes listed completely so far (same scan order and replacement rule, same lists):
     // the lists' minimum sizes, candidates in both present lists (of those sizes unless Restricted),
     // SingleNUMANode one-zone hints only.  A hint found there ends the listing.
     int len[2] = {0, 0};
-    uint64_t E[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+    if (lane < 8) s_E[lane >> 2][lane & 3] = 0;
     const int pol = pf_numa_policy(pod.flags) ? pf_numa_policy(pod.flags) : nf_numa_policy(s.flags[i]);
     uint32_t fb = 0;
-    for (int c = 0; c < 4 && !fb; c++) {
-      const int e = c * 64 + lane;
-      const uint32_t m = e < 255 ? NUMA_ORDER[e] : 0u;
+    const bool single = pol == KE_NUMA_POLICY_SINGLE_NUMA_NODE, restricted = pol == KE_NUMA_POLICY_RESTRICTED;
+    const bool excl = (pod.flags & PF_NUMA_EXCL_REQ) != 0;
+    const int R = (int)present[0] + (int)present[1];
+    int cov_done = 0;  // hint sizes folded
+    uint32_t best = 0;
+    int32_t bsc = 0;
+    bool found = false;
+    // steps: the one- and two-zone hints (most searches end there), then 64 masks at a time
+    for (int c = 0, e0 = 0; e0 < 255 && !fb; c++) {
+      const int e1 = c == 0 ? NUMA_OFF[3] : min(e0 + 64, 255);
+      const int e = e0 + lane;
+      const uint32_t m = e < e1 ? NUMA_ORDER[e] : 0u;
       bool in[2] = {false, false};
       if (m && !(m & ~nv.zm)) {
         in[0] = present[0] && !(m & lack[0]);
@@ -2630,42 +2710,61 @@ __global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __res
 #pragma unroll
       for (int r = 0; r < 2; r++) {
         const uint64_t bal = __ballot(in[r]);
-        E[r][c] = bal;
+        const int sh = e0 & 63;  // lane l's mask is NUMA_ORDER[e0 + l]
+        if (lane == 0) {
+          s_E[r][e0 >> 6] |= bal << sh;
+          if (sh && (e0 >> 6) < 3) s_E[r][(e0 >> 6) + 1] |= bal >> (64 - sh);
+        }
         if (in[r]) s_list[r][len[r] + lanes_below(bal)] = (uint8_t)m;
         len[r] += __popcll(bal);
       }
       __syncthreads();
+      if (c == 0) {
+        RPROF(4)
+      }
       int covered = 0;  // hint sizes whose masks are all listed
-      while (covered < 8 && NUMA_OFF[covered + 2] <= 64 * (c + 1)) covered++;
-      if (lane == 0) {
-        const bool single = pol == KE_NUMA_POLICY_SINGLE_NUMA_NODE, restricted = pol == KE_NUMA_POLICY_RESTRICTED;
-        const bool excl = (pod.flags & PF_NUMA_EXCL_REQ) != 0;
-        const int R = (int)present[0] + (int)present[1];
+      while (covered < 8 && NUMA_OFF[covered + 2] <= e1) covered++;
+      e0 = e1;
+      // fold the candidates of the sizes listed completely since the last step, in IterateBitMasks order
+      // (lanes test 64 masks at a time; the fold reads the candidate lanes' registers): a larger hint
+      // never replaces a smaller one, so folding every candidate equals the search's early stops
+      const int top = single ? min(covered, 1) : covered;
+      if (top > cov_done) {
         const int minr0 = len[0] ? __popc(s_list[0][0]) : 9, minr1 = len[1] ? __popc(s_list[1][0]) : 9;
-        uint32_t best = 0;
-        int32_t bsc = 0;
-        bool found = false;
-        for (int sz = 1; sz <= (single ? 1 : covered) && !found; sz++) {
-          for (int q = NUMA_OFF[sz]; q < NUMA_OFF[sz + 1]; q++) {
-            const bool in0 = (E[0][q >> 6] >> (q & 63)) & 1u, in1 = (E[1][q >> 6] >> (q & 63)) & 1u;
-            if (!in0 && !in1) continue;
-            bool cand = (!present[0] || in0) && (!present[1] || in1);
+        for (int q0 = NUMA_OFF[cov_done + 1]; q0 < NUMA_OFF[top + 1]; q0 += 64) {
+          const int q = q0 + lane;
+          bool cand = false;
+          uint32_t mq = 0;
+          int32_t sc = 0;
+          if (q < NUMA_OFF[top + 1]) {
+            mq = NUMA_ORDER[q];
+            const int sz = __popc(mq);
+            const bool in0 = (s_E[0][q >> 6] >> (q & 63)) & 1u, in1 = (s_E[1][q >> 6] >> (q & 63)) & 1u;
+            cand = (in0 || in1) && (!present[0] || in0) && (!present[1] || in1);
             if (!restricted) cand = cand && (!present[0] || minr0 == sz) && (!present[1] || minr1 == sz);
-            const uint32_t mm = NUMA_ORDER[q];
-            if (!cand || !exclusive_ok(nv, mm, excl)) continue;
-            const int32_t sc = R * s_score[mm];
-            if (!found || narrower(mm, best) || (__popc(mm) == __popc(best) && sc > bsc)) {
+            cand = cand && exclusive_ok(nv, mq, excl);
+            if (cand) sc = R * s_score[mq];
+          }
+          for (uint64_t cb = __ballot(cand); cb; cb &= cb - 1) {
+            const int l = __ffsll((long long)cb) - 1;
+            const uint32_t mm = (uint32_t)__builtin_amdgcn_readlane((int)mq, l);
+            const int32_t ss = __builtin_amdgcn_readlane(sc, l);
+            if (!found || narrower(mm, best) || (__popc(mm) == __popc(best) && ss > bsc)) {
               best = mm;
-              bsc = sc;
+              bsc = ss;
               found = true;
             }
           }
-          if (!restricted && (!present[0] || minr0 <= sz) && (!present[1] || minr1 <= sz)) break;
         }
-        if (found) fb = NFB_FOUND << 8 | ((single && best == nv.zm) ? 0u : best);
-        else if (c == 3 && pol != KE_NUMA_POLICY_BEST_EFFORT) fb = NFB_FAIL << 8;
+        cov_done = top;
       }
-      fb = __shfl(fb, 0);
+      if (found) fb = NFB_FOUND << 8 | ((single && best == nv.zm) ? 0u : best);
+      else if (e1 >= 255 && pol != KE_NUMA_POLICY_BEST_EFFORT) fb = NFB_FAIL << 8;
+      if (c == 0) {
+        RPROF(0)
+      } else {
+        RPROF(1)
+      }
     }
     uint32_t aff = 0;
     if (fb) {
@@ -2732,32 +2831,58 @@ __global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __res
       }
       aff = bun ? nv.zm : best;
     }
+    RPROF(2)
     if (!fb) fb = NFB_BEST_EFFORT << 8 | aff;
-    if (lane == 0) {
-      NodeRegs nr;
-      load_row(s, i, nr);
-      prepare_row(nr);
-      const bool expired = node_expired(nr, k);
-      const EvalOut o = eval_pair<false, true, false, true, CS>(nr, expired, pod, k, s, i, nv, fb);
-      if (PARITY) {
-        const int64_t o_idx = (int64_t)p * n_nodes + i;
-        status[o_idx] = o.status;
-        reason[o_idx] = o.reason;
-        la[o_idx] = o.la;
-        numa[o_idx] = o.numa;
-        ds[o_idx] = o.ds;
-        total[o_idx] = (int16_t)o.total;
-        if (o.total >= 0) atomicMax(&dsmax[p], (uint32_t)o.ds + 1);
-      } else {
-        scores[(int64_t)p * score_stride + i] = (uint16_t)(o.total + 1);
-        if (CS && aff_out) aff_out[i] = o.aff;
-        if (dsraw && (pod.flags & PF_DS)) {  // a DeviceShare singleton: its raw score (0 here) for the normalisation
-          dsraw[i] = o.total >= 0 ? (uint16_t)(o.ds + 1) : (uint16_t)0;
-          if (o.total >= 0) atomicMax(dsmax, (uint32_t)o.ds + 1);
-        }
+    if (lane == 0) fb_out[w] = fb;
+    RPROF_FLUSH(1)
+    __syncthreads();
+  }
+}
+
+// The deferred pairs evaluated with their merges (k_numa_fallback's fb_in), one lane per pair: the
+// Filter / Score of eval_pair with the Admit's outcome given.  PARITY: the parity matrices; else the
+// batch score (and for a binding batch the affinity, for a DeviceShare singleton its raw score).
+constexpr int FINISH_BLOCKS = 256;
+template <bool PARITY, bool CS = false>
+__global__ __launch_bounds__(64) void k_numa_finish(SoA s, const DevPod* __restrict__ pods,
+                                                    const int32_t* __restrict__ batch_base, KArgs k,
+                                                    const uint64_t* __restrict__ list, const uint32_t* __restrict__ cnt,
+                                                    uint16_t* __restrict__ scores, int64_t score_stride, int n_nodes,
+                                                    uint8_t* status, uint8_t* reason, int16_t* la, int16_t* numa,
+                                                    int16_t* ds, int16_t* total, uint32_t* dsmax,
+                                                    uint8_t* __restrict__ aff_out, uint16_t* __restrict__ dsraw,
+                                                    const uint32_t* __restrict__ fb_in) {
+  const uint32_t n = *cnt;
+  const int base = PARITY ? 0 : *batch_base;
+  for (uint32_t w = blockIdx.x * 64 + threadIdx.x; w < n; w += FINISH_BLOCKS * 64) {
+    const uint64_t it = list[w];
+    const int p = (int)(it >> 32);
+    const int64_t i = (int64_t)(uint32_t)it;
+    const DevPod pod = pods[base + p];
+    NumaNode nv;
+    numa_load(s, i, nv);
+    NodeRegs nr;
+    load_row(s, i, nr);
+    prepare_row(nr);
+    const bool expired = node_expired(nr, k);
+    const EvalOut o = eval_pair<false, true, false, true, CS>(nr, expired, pod, k, s, i, nv, fb_in[w]);
+    if (PARITY) {
+      const int64_t o_idx = (int64_t)p * n_nodes + i;
+      status[o_idx] = o.status;
+      reason[o_idx] = o.reason;
+      la[o_idx] = o.la;
+      numa[o_idx] = o.numa;
+      ds[o_idx] = o.ds;
+      total[o_idx] = (int16_t)o.total;
+      if (o.total >= 0) atomicMax(&dsmax[p], (uint32_t)o.ds + 1);
+    } else {
+      scores[(int64_t)p * score_stride + i] = (uint16_t)(o.total + 1);
+      if (CS && aff_out) aff_out[i] = o.aff;
+      if (dsraw && (pod.flags & PF_DS)) {  // a DeviceShare singleton: its raw score (0 here) for the normalisation
+        dsraw[i] = o.total >= 0 ? (uint16_t)(o.ds + 1) : (uint16_t)0;
+        if (o.total >= 0) atomicMax(dsmax, (uint32_t)o.ds + 1);
       }
     }
-    __syncthreads();
   }
 }
 
@@ -3267,28 +3392,6 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
   __builtin_amdgcn_s_setprio(0);
 }
 
-// Diagnostic build (-DKE_PROF_REPLAY, tools/replay_phases.sh): shader-clock cycles of each phase of
-// the per-pod replay loop, summed over every pod into g_rprof (ke_debug_replay_phases).  Off in the
-// product build (the macro expands to nothing).
-#ifdef KE_PROF_REPLAY
-__device__ unsigned long long g_rprof[8];
-#define RPROF_DECL uint64_t rp_[7] = {0, 0, 0, 0, 0, 0, 0}, rp_t = __builtin_amdgcn_s_memtime();
-#define RPROF(i)                                         \
-  {                                                      \
-    const uint64_t rp_n = __builtin_amdgcn_s_memtime(); \
-    rp_[i] += rp_n - rp_t;                               \
-    rp_t = rp_n;                                         \
-  }
-#define RPROF_FLUSH(npods)                                                           \
-  if (lane == 0) {                                                                   \
-    for (int u_ = 0; u_ < 7; u_++) atomicAdd(&g_rprof[u_], (unsigned long long)rp_[u_]); \
-    atomicAdd(&g_rprof[7], (unsigned long long)(npods));                             \
-  }
-#else
-#define RPROF_DECL
-#define RPROF(i)
-#define RPROF_FLUSH(npods)
-#endif
 
 // The sequential replay of one batch (wave 0).
 //   Lane c owns the c-th node changed in this batch: its row lives in that lane's registers, so the
@@ -4497,7 +4600,7 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
   if (N > 0) {
     dim3 grid((unsigned)((N + EVAL_BLOCK - 1) / EVAL_BLOCK), (unsigned)((P + ppb - 1) / ppb));
     if (d->numa_alloc) {
-      rc = ensure((void**)&d->d_defer, &d->defer_cap, sizeof(uint64_t) * M);
+      rc = ensure((void**)&d->d_defer, &d->defer_cap, (sizeof(uint64_t) + sizeof(uint32_t)) * M);  // pairs, merges
       if (rc) return rc;
       rc = ensure((void**)&d->d_defer_cnt, &d->defer_cnt_cap, sizeof(uint32_t));
       if (rc) return rc;
@@ -4505,10 +4608,15 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
       hipLaunchKernelGGL((cpu ? k_eval_parity<true, true> : k_eval_parity<true, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, (int)N, d->d_pods, (int)P,
                          ppb, k, d_status, d_reason, d_la, d_numa, d_ds, d_total, d_dsmax, d->d_defer, d->d_defer_cnt);
       HIP_OK(hipGetLastError());
+      uint32_t* fb = reinterpret_cast<uint32_t*>(d->d_defer + M);
       hipLaunchKernelGGL((cpu ? k_numa_fallback<true, true> : k_numa_fallback<true, false>), dim3(FALLBACK_BLOCKS),
                          dim3(64), 0, d->stream, d->soa, d->d_pods,
                          d->d_batch_base, k, d->d_defer, d->d_defer_cnt, d->d_scores, d->capacity, (int)N, d_status,
-                         d_reason, d_la, d_numa, d_ds, d_total, d_dsmax, nullptr, nullptr);
+                         d_reason, d_la, d_numa, d_ds, d_total, d_dsmax, nullptr, nullptr, fb);
+      hipLaunchKernelGGL((cpu ? k_numa_finish<true, true> : k_numa_finish<true, false>), dim3(FINISH_BLOCKS),
+                         dim3(64), 0, d->stream, d->soa, d->d_pods,
+                         d->d_batch_base, k, d->d_defer, d->d_defer_cnt, d->d_scores, d->capacity, (int)N, d_status,
+                         d_reason, d_la, d_numa, d_ds, d_total, d_dsmax, nullptr, nullptr, fb);
     } else {
       hipLaunchKernelGGL((cpu ? k_eval_parity<false, true> : k_eval_parity<false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, (int)N, d->d_pods, (int)P,
                          ppb, k, d_status, d_reason, d_la, d_numa, d_ds, d_total, d_dsmax, nullptr, nullptr);
@@ -4606,7 +4714,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   const bool numa = d->numa_alloc;
   if (numa && !d->d_numaalloc) HIP_OK(hipMalloc(&d->d_numaalloc, sizeof(int64_t) * 16 * d->out_cap));
   if (numa) {  // deferred-pair list of one batch (reused) + a counter per batch
-    rc = ensure((void**)&d->d_defer, &d->defer_cap, sizeof(uint64_t) * MAX_BATCH * d->capacity);
+    rc = ensure((void**)&d->d_defer, &d->defer_cap, (sizeof(uint64_t) + sizeof(uint32_t)) * MAX_BATCH * d->capacity);
     if (rc) return rc;
     rc = ensure((void**)&d->d_defer_cnt, &d->defer_cnt_cap, sizeof(uint32_t) * n_batches);
     if (rc) return rc;
@@ -4708,12 +4816,19 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
         uint32_t* dcnt = numa ? d->d_defer_cnt + b : nullptr;
         hipLaunchKernelGGL(eval, grid, dim3(eb), 0, es, d->soa, lo, hi, d->d_pods, bbase, bp,
                            ppb, k, d->d_scores, d->capacity, d->d_dsraw, d->d_defer, dcnt, d->d_aff, d->d_dsmax);
-        if (numa)  // a DeviceShare pod defers only on nodes without a device cache (no DeviceShare hints there)
+        if (numa) {  // a DeviceShare pod defers only on nodes without a device cache (no DeviceShare hints there)
+          uint32_t* fb = reinterpret_cast<uint32_t*>(d->d_defer + (int64_t)MAX_BATCH * d->capacity);
           hipLaunchKernelGGL((cpu ? k_numa_fallback<false, true> : k_numa_fallback<false, false>), dim3(FALLBACK_BLOCKS),
                              dim3(64), 0, es, d->soa, d->d_pods,
                              bbase, k, d->d_defer, dcnt, d->d_scores, d->capacity, 0, nullptr, nullptr,
                              nullptr, nullptr, nullptr, nullptr, ds ? d->d_dsmax : nullptr, cpu ? d->d_aff : nullptr,
-                             ds ? d->d_dsraw : nullptr);
+                             ds ? d->d_dsraw : nullptr, fb);
+          hipLaunchKernelGGL((cpu ? k_numa_finish<false, true> : k_numa_finish<false, false>), dim3(FINISH_BLOCKS),
+                             dim3(64), 0, es, d->soa, d->d_pods,
+                             bbase, k, d->d_defer, dcnt, d->d_scores, d->capacity, 0, nullptr, nullptr,
+                             nullptr, nullptr, nullptr, nullptr, ds ? d->d_dsmax : nullptr, cpu ? d->d_aff : nullptr,
+                             ds ? d->d_dsraw : nullptr, fb);
+        }
       }
       if (ds && sharded && !d->loopback)  // DefaultNormalizeScore's max over the feasible nodes of all ranks
         RCCL_OK(ncclAllReduce(d->d_dsmax, d->d_dsmax, 1, ncclUint32, ncclMax, d->comm, es));
