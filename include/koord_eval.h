@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define KE_ABI_VERSION 4
+#define KE_ABI_VERSION 5
 #define KE_ABSENT (-1)
 
 /* ---- error codes ---------------------------------------------------------------------------- */
@@ -321,6 +321,36 @@ typedef struct ke_gpu_partition {
 } ke_gpu_partition; /* 24 bytes */
 #define KE_MAX_GPU_PARTITIONS 64 /* partitions per node table */
 
+/* ---- NodeResourcesFitPlus / ScarceResourceAvoidance -------------------------
+ * Two Score plugins without Filter or NormalizeScore, fused into the same per-(pod, node) pass:
+ *  - NodeResourcesFitPlus (pkg/scheduler/plugins/noderesourcefitplus/node_resources_fit_plus.go:75-93,
+ *    node_resource_fit_plus_utils.go:35-89): over the pod's requested resources (PodRequests > 0) that the
+ *    args name, Σ weight·{least,most}RequestedScore(NodeInfo (NonZero)Requested + pod request, Allocatable)
+ *    / Σ weight, MaxNodeScore when the weight sum is 0;
+ *  - ScarceResourceAvoidance (scarceresourceavoidance/scarce_resource_avoidance.go:70-160): diff = the node's
+ *    allocatable resource names (> 0) minus the pod's requested names, n = |diff ∩ args.Resources|:
+ *    MaxNodeScore when diff or n is empty, else (|diff| - n)·100/|diff|.
+ * Resource names are interned by the caller into ids 0 .. KE_MAX_XRES-1 (one table per context, every name
+ * a node advertises must have an id); cpu and memory have fixed ids.  Plugin weight 0 = not in the profile. */
+#define KE_MAX_XRES 64
+#define KE_XRES_CPU 0
+#define KE_XRES_MEMORY 1
+#define KE_MAX_FITPLUS 4 /* NodeResourcesFitPlusArgs.Resources entries */
+#define KE_MAX_POD_XRES 8 /* ke_pod.xres_id / xres_value entries */
+typedef struct ke_fitplus_resource {
+  int32_t id;     /* resource id */
+  int32_t type;   /* KE_STRATEGY_* (ResourcesType.Type: LeastAllocated / MostAllocated) */
+  int64_t weight; /* ResourcesType.Weight, >= 0 */
+} ke_fitplus_resource; /* 16 bytes */
+typedef struct ke_ext_args {
+  int64_t weight_fitplus;      /* profile Score weight of NodeResourcesFitPlus (0 = disabled) */
+  int64_t weight_sra;          /* profile Score weight of ScarceResourceAvoidance (0 = disabled) */
+  uint64_t sra_resources;      /* ScarceResourceAvoidanceArgs.Resources as a mask of resource ids */
+  int32_t n_fitplus;           /* entries of NodeResourcesFitPlusArgs.Resources (distinct ids) */
+  int32_t pad;
+  ke_fitplus_resource fitplus[KE_MAX_FITPLUS];
+} ke_ext_args; /* 96 bytes */
+
 /* Framework profile: score plugin weights (config/manager/scheduler-config.yaml:85-94). */
 typedef struct ke_config {
   int32_t abi_version;    /* must be KE_ABI_VERSION                                      */
@@ -335,6 +365,7 @@ typedef struct ke_config {
   int32_t pod_batch;      /* B: pods evaluated per speculative batch in ke_schedule      */
   int32_t global_node_offset; /* first global node index held by this shard (multi-GPU)  */
   int32_t pad;
+  ke_ext_args ext;        /* NodeResourcesFitPlus / ScarceResourceAvoidance (all zero = disabled) */
 } ke_config;
 
 /* A Node object (+ the NodeInfo aggregates the framework keeps for it). */
@@ -433,6 +464,16 @@ typedef struct ke_pod {
   uint8_t device_joint_allocate;       /* DeviceJointAllocate annotation that keeps >= 1 requested device type:
                                           tryJointAllocate (device_allocator.go:205-300) is not implemented */
   uint8_t device_hints;                /* KE_DHINT_* bits of DeviceAllocateHints this evaluator does not model */
+  /* NodeResourcesFitPlus / ScarceResourceAvoidance PreScore (computePodResourceRequest): the resource ids
+   * whose PodRequests value is > 0 (fitsPodRequestName / fitsRequest, scarce_resource_avoidance.go:109-150),
+   * and per id calculatePodResourceRequest (node_resource_fit_plus_utils.go:138-203: containers' requests
+   * with the 100m cpu / 200Mi memory defaults for a container without one, init containers' max); ids
+   * not listed count 0.  Only the ids of NodeResourcesFitPlusArgs.Resources are read. */
+  uint64_t xres_request_mask;
+  int32_t n_xres;
+  int32_t xres_id[KE_MAX_POD_XRES];
+  int32_t pad3;
+  int64_t xres_value[KE_MAX_POD_XRES];
 } ke_pod;
 
 /* ke_pod.gpu_required_topology_scope: apiext.DeviceTopologyScope and its DeviceTopologyScopeLevel */
@@ -463,8 +504,9 @@ void ke_destroy(ke_ctx* ctx);
 const char* ke_last_error(void);
 int ke_abi_version(void);
 /* sizeof() of ke_config, ke_node, ke_node_metric, ke_pod_metric, ke_aggregated_usage, ke_pod,
- * ke_resource_map, ke_loadaware_args, ke_numa_args, ke_deviceshare_args, ke_device, ke_numa_zone, ke_cpu (in
- * that order) for binding-layout checks. */
+ * ke_resource_map, ke_loadaware_args, ke_numa_args, ke_deviceshare_args, ke_device, ke_numa_zone, ke_cpu,
+ * ke_quota_args, ke_quota, ke_gpu_partition, ke_ext_args, ke_node_resource (in that order) for binding-layout
+ * checks. */
 int ke_abi_struct_sizes(int32_t* sizes, int32_t n);
 /* 1 if this build has a usable HIP device and its gfx950 kernels loaded, else 0. */
 int ke_device_available(void);
@@ -500,6 +542,21 @@ int ke_estimate_pod(ke_ctx* ctx, const ke_pod* pod, int64_t* est);
 /* DeviceShare node device cache (Device CRD informer, device_cache.go:518-568): replace the devices of
  * `node` (n may be 0: a cache entry without devices).  At most KE_MAX_MINORS devices per type. */
 int ke_node_devices_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_device* devices);
+/* NodeInfo.Allocatable / Requested of the node by resource id for NodeResourcesFitPlus and
+ * ScarceResourceAvoidance (replaces the node's table; n = 0: none).  `requested` is what
+ * calculateResourceAllocatableRequest reads (node_resource_fit_plus_utils.go:110-133): NonZeroRequested
+ * for cpu / memory, Requested for every other resource.  Every resource the node advertises (allocatable
+ * > 0, "pods" excluded: framework.Resource keeps it apart) must be listed for ScarceResourceAvoidance.
+ * ke_schedule adds each placed pod's xres_value to its node's requested. */
+typedef struct ke_node_resource {
+  int32_t id;
+  int32_t pad;
+  int64_t allocatable;
+  int64_t requested;
+} ke_node_resource; /* 24 bytes */
+int ke_node_resources_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_node_resource* res);
+/* The node's current table (after the Reserves of past ke_schedule calls): up to cap entries, *n = count. */
+int ke_node_resources_get(ke_ctx* ctx, int32_t node, int32_t cap, ke_node_resource* res, int32_t* n);
 /* Drop the node's cache entry (getNodeDevice == nil: DeviceShare Filter passes, Score is 0). */
 int ke_node_devices_delete(ke_ctx* ctx, int32_t node);
 /* The node's GPU partition indexer and policy as GPUAllocator.Allocate resolves them (allocator_gpu.go:77-82,

@@ -9,7 +9,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 ABSENT = -1
 
 OK = 0
@@ -165,6 +165,27 @@ class GpuPartition(C.Structure):
                 ("ring_bus_bandwidth", i64)]
 
 
+MAX_XRES = 64
+XRES_CPU = 0
+XRES_MEMORY = 1
+MAX_FITPLUS = 4
+MAX_POD_XRES = 8
+
+
+class FitPlusResource(C.Structure):
+    _fields_ = [("id", i32), ("type", i32), ("weight", i64)]
+
+
+class ExtArgs(C.Structure):
+    """NodeResourcesFitPlus / ScarceResourceAvoidance args + profile weights (koord_eval.h ke_ext_args)."""
+    _fields_ = [("weight_fitplus", i64), ("weight_sra", i64), ("sra_resources", C.c_uint64), ("n_fitplus", i32),
+                ("pad", i32), ("fitplus", FitPlusResource * MAX_FITPLUS)]
+
+
+class NodeResource(C.Structure):
+    _fields_ = [("id", i32), ("pad", i32), ("allocatable", i64), ("requested", i64)]
+
+
 class Config(C.Structure):
     _fields_ = [
         ("abi_version", i32),
@@ -179,6 +200,7 @@ class Config(C.Structure):
         ("pod_batch", i32),
         ("global_node_offset", i32),
         ("pad", i32),
+        ("ext", ExtArgs),
     ]
 
 
@@ -262,6 +284,11 @@ class Pod(C.Structure):
         ("gpu_partition_restricted", u8),
         ("device_joint_allocate", u8),
         ("device_hints", u8),
+        ("xres_request_mask", C.c_uint64),
+        ("n_xres", i32),
+        ("xres_id", i32 * MAX_POD_XRES),
+        ("pad3", i32),
+        ("xres_value", i64 * MAX_POD_XRES),
     ]
 
 
@@ -291,7 +318,7 @@ class Quota(C.Structure):
 
 
 STRUCTS = [Config, Node, NodeMetric, PodMetric, AggregatedUsage, Pod, ResourceMap, LoadAwareArgs, NumaArgs,
-           DeviceShareArgs, Device, NumaZone, Cpu, QuotaArgs, Quota, GpuPartition]
+           DeviceShareArgs, Device, NumaZone, Cpu, QuotaArgs, Quota, GpuPartition, ExtArgs, NodeResource]
 QUOTA_DTYPE = np.dtype(Quota)
 
 # numpy views of the same layouts (bulk loads)
@@ -304,6 +331,7 @@ DEVICE_DTYPE = np.dtype(Device)
 GPU_PARTITION_DTYPE = np.dtype(GpuPartition)
 NUMA_ZONE_DTYPE = np.dtype(NumaZone)
 CPU_DTYPE = np.dtype(Cpu)
+NODE_RESOURCE_DTYPE = np.dtype(NodeResource)
 
 ROW_DTYPE = np.dtype([("f", np.int64, (18,)), ("flags", np.uint32), ("pad", np.uint32)])
 
@@ -368,6 +396,8 @@ EXPORTS = {
     "ke_node_gpu_partitions": (C.c_int, [C.c_void_p, i32, i32, i32, i32, C.c_void_p]),
     "ke_node_devices_delete": (C.c_int, [C.c_void_p, i32]),
     "ke_node_numa_set": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p]),
+    "ke_node_resources_set": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p]),
+    "ke_node_resources_get": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p, C.POINTER(i32)]),
     "ke_last_device_allocations": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_last_numa_allocations": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_node_cpus_set": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p, i32]),

@@ -100,7 +100,8 @@ int ke_abi_struct_sizes(int32_t* sizes, int32_t n) {
                          (int32_t)sizeof(ke_numa_args), (int32_t)sizeof(ke_deviceshare_args),
                          (int32_t)sizeof(ke_device),       (int32_t)sizeof(ke_numa_zone),
                          (int32_t)sizeof(ke_cpu),          (int32_t)sizeof(ke_quota_args),
-                         (int32_t)sizeof(ke_quota),        (int32_t)sizeof(ke_gpu_partition)};
+                         (int32_t)sizeof(ke_quota),        (int32_t)sizeof(ke_gpu_partition),
+                         (int32_t)sizeof(ke_ext_args),     (int32_t)sizeof(ke_node_resource)};
   const int32_t m = (int32_t)(sizeof(all) / sizeof(all[0]));
   for (int32_t i = 0; i < n && i < m; i++) sizes[i] = all[i];
   return m;
@@ -144,6 +145,24 @@ int ke_create(const ke_config* cfg, ke_ctx** out) {
   k.wp_ds = (int32_t)cfg->weight_deviceshare;
   for (int i = 0; i < 4; i++)
     k.w_ds[i] = cfg->deviceshare.weights[i] == KE_ABSENT ? -1 : (int32_t)cfg->deviceshare.weights[i];
+  // NodeResourcesFitPlus / ScarceResourceAvoidance: their Score runs in the NUMA-path kernels (eval_pair and
+  // the zone-aware Reserve), so a context with either plugin keeps the NUMA SoA and the serial schedule
+  const ke_ext_args& x = cfg->ext;
+  k.wp_fp = (int32_t)x.weight_fitplus;
+  k.wp_sra = (int32_t)x.weight_sra;
+  k.fp_n = x.n_fitplus;
+  k.fp_most = 0;
+  k.sra_mask = x.sra_resources;
+  for (int q = 0; q < 4; q++) {
+    k.fp_id[q] = q < x.n_fitplus ? x.fitplus[q].id : 0;
+    k.fp_w[q] = q < x.n_fitplus ? x.fitplus[q].weight : 0;
+    if (q < x.n_fitplus && x.fitplus[q].type == KE_STRATEGY_MOST_ALLOCATED) k.fp_most |= 1u << q;
+  }
+  if (x.weight_fitplus > 0 || x.weight_sra > 0) {
+    k.flags |= AF_EXT;
+    c.ext_enabled = true;
+    c.numa_enabled = true;
+  }
   if (device_available()) {
     rc = device_create(&c);
     if (rc) {
@@ -163,6 +182,30 @@ void ke_destroy(ke_ctx* ctx) {
 }
 
 int32_t ke_num_nodes(ke_ctx* ctx) { return ctx ? ctx->c.n_nodes : 0; }
+
+int ke_node_resources_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_node_resource* res) {
+  int rc = check_node(ctx, node);
+  if (ctx) flush_mirror(ctx->c);
+  if (rc) return rc;
+  rc = validate_node_resources(n, res);
+  if (rc) return rc;
+  NodeState& ns = ctx->c.nodes[node];
+  ns.xres.assign(res, res + n);
+  ns.dirty = true;
+  ctx->c.n_nodes = std::max(ctx->c.n_nodes, node + 1);
+  return KE_OK;
+}
+
+int ke_node_resources_get(ke_ctx* ctx, int32_t node, int32_t cap, ke_node_resource* res, int32_t* n) {
+  int rc = check_node(ctx, node);
+  if (ctx) flush_mirror(ctx->c);
+  if (rc) return rc;
+  if (!n || cap < 0 || (cap > 0 && !res)) return fail(KE_ERR_INVALID, "ke_node_resources_get arguments");
+  const NodeState& ns = ctx->c.nodes[node];
+  *n = (int32_t)ns.xres.size();
+  for (int32_t e = 0; e < cap && e < *n; e++) res[e] = ns.xres[e];
+  return KE_OK;
+}
 
 int ke_node_upsert(ke_ctx* ctx, int32_t node, const ke_node* n) {
   int rc = check_node(ctx, node);

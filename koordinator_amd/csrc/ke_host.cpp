@@ -37,9 +37,23 @@ int validate_config(const ke_config& cfg) {
   if (cfg.node_capacity <= 0 || cfg.node_capacity > MAX_SHARD_NODES)
     return fail(KE_ERR_INVALID, "node_capacity out of range (1 .. 2^23-1 per shard)");
   if (cfg.pod_batch < 1 || cfg.pod_batch > MAX_BATCH) return fail(KE_ERR_INVALID, "pod_batch out of range (1..64)");
-  if (cfg.weight_loadaware < 0 || cfg.weight_numa < 0 || cfg.weight_deviceshare < 0 ||
-      (cfg.weight_loadaware + cfg.weight_numa + cfg.weight_deviceshare) * 100 > MAX_TOTAL_SCORE)
-    return fail(KE_ERR_UNSUPPORTED, "plugin weights: (w_loadaware + w_numa + w_deviceshare) * 100 must be <= 510");
+  const ke_ext_args& x = cfg.ext;
+  if (cfg.weight_loadaware < 0 || cfg.weight_numa < 0 || cfg.weight_deviceshare < 0 || x.weight_fitplus < 0 ||
+      x.weight_sra < 0 ||
+      (cfg.weight_loadaware + cfg.weight_numa + cfg.weight_deviceshare + x.weight_fitplus + x.weight_sra) * 100 >
+          MAX_TOTAL_SCORE)
+    return fail(KE_ERR_UNSUPPORTED, "plugin weights: (sum of the Score plugin weights) * 100 must be <= 510");
+  if (x.n_fitplus < 0 || x.n_fitplus > KE_MAX_FITPLUS)
+    return fail(KE_ERR_UNSUPPORTED, "NodeResourcesFitPlusArgs.Resources: at most 4 resources");
+  for (int q = 0; q < x.n_fitplus; q++) {
+    const ke_fitplus_resource& e = x.fitplus[q];
+    if (e.id < 0 || e.id >= KE_MAX_XRES) return fail(KE_ERR_INVALID, "NodeResourcesFitPlus resource id out of range");
+    if (e.type != KE_STRATEGY_LEAST_ALLOCATED && e.type != KE_STRATEGY_MOST_ALLOCATED)
+      return fail(KE_ERR_INVALID, "NodeResourcesFitPlus resource type");
+    if (e.weight < 0 || e.weight > (1 << 20)) return fail(KE_ERR_UNSUPPORTED, "NodeResourcesFitPlus weight out of range");
+    for (int r = 0; r < q; r++)
+      if (x.fitplus[r].id == e.id) return fail(KE_ERR_INVALID, "NodeResourcesFitPlus resource listed twice");
+  }
   for (int i = 0; i < 4; i++) {
     const int64_t w = cfg.deviceshare.weights[i];
     if (w != KE_ABSENT && (w < 0 || w > (1 << 20))) return fail(KE_ERR_UNSUPPORTED, "deviceshare weight out of range");
@@ -264,7 +278,49 @@ int validate_pod(const ke_pod& p) {
   if (p.device_hints & KE_DHINT_EXCLUSIVE)  // filterFreeDevicesByPCIe (device_cache.go:372-376,417-440)
     return fail(KE_ERR_UNSUPPORTED, "DeviceHint ExclusivePolicy is not implemented");
   if (p.device_hints) return fail(KE_ERR_INVALID, "unknown device hint bits");
+  if (p.n_xres < 0 || p.n_xres > KE_MAX_POD_XRES) return fail(KE_ERR_INVALID, "pod n_xres out of range (0..8)");
+  for (int e = 0; e < p.n_xres; e++) {
+    if (p.xres_id[e] < 0 || p.xres_id[e] >= KE_MAX_XRES) return fail(KE_ERR_INVALID, "pod xres id out of range");
+    if (p.xres_value[e] < 0) return fail(KE_ERR_INVALID, "negative pod xres value");
+    for (int f = 0; f < e; f++)
+      if (p.xres_id[f] == p.xres_id[e]) return fail(KE_ERR_INVALID, "pod xres id listed twice");
+  }
   return KE_OK;
+}
+
+int validate_node_resources(int32_t n, const ke_node_resource* r) {
+  if (n < 0 || n > KE_MAX_XRES || (n > 0 && !r)) return fail(KE_ERR_INVALID, "node resources: n out of range (0..64)");
+  uint64_t seen = 0;
+  for (int32_t e = 0; e < n; e++) {
+    if (r[e].id < 0 || r[e].id >= KE_MAX_XRES) return fail(KE_ERR_INVALID, "node resource id out of range");
+    if (seen >> r[e].id & 1) return fail(KE_ERR_INVALID, "node resource id listed twice");
+    seen |= 1ull << r[e].id;
+    if (r[e].allocatable < 0 || r[e].requested < 0) return fail(KE_ERR_INVALID, "negative node resource quantity");
+  }
+  return KE_OK;
+}
+
+// NodeResourcesFitPlus / ScarceResourceAvoidance ext row: Allocatable / (NonZero)Requested of the FitPlus
+// slots (0 for a resource the node does not list) and the mask of ids with Allocatable > 0
+void derive_ext_row(const ke_config& cfg, const NodeState& ns, int64_t* f, uint64_t* mask) {
+  for (int w = 0; w < NUM_XF; w++) f[w] = 0;
+  uint64_t m = 0;
+  for (const ke_node_resource& r : ns.xres) {
+    if (r.allocatable > 0) m |= 1ull << r.id;
+    for (int q = 0; q < cfg.ext.n_fitplus && q < 4; q++)
+      if (cfg.ext.fitplus[q].id == r.id) f[XF_ALLOC + q] = r.allocatable, f[XF_REQ + q] = r.requested;
+  }
+  *mask = m;
+}
+
+// host mirror of a placement's ext Reserve: NodeInfo (NonZero)Requested += the pod's requests by id
+void host_ext_reserve(NodeState& ns, const ke_pod& pod) {
+  for (int e = 0; e < pod.n_xres; e++) {
+    bool found = false;
+    for (ke_node_resource& r : ns.xres)
+      if (r.id == pod.xres_id[e]) r.requested += pod.xres_value[e], found = true;
+    if (!found && pod.xres_value[e] != 0) ns.xres.push_back(ke_node_resource{pod.xres_id[e], 0, 0, pod.xres_value[e]});
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -457,6 +513,13 @@ DevPod make_dev_pod(const ke_config& cfg, const ke_pod& pod) {
     d.flags |= PF_DS;
   }
   if (pod.quota_non_preemptible) d.flags |= PF_QUOTA_NP;
+  // NodeResourcesFitPlus / ScarceResourceAvoidance PreScore: requested names and the FitPlus requests by slot
+  d.xmask = pod.xres_request_mask;
+  for (int q = 0; q < cfg.ext.n_fitplus && q < 4; q++) {
+    d.xreq[q] = 0;
+    for (int e = 0; e < pod.n_xres; e++)
+      if (pod.xres_id[e] == cfg.ext.fitplus[q].id) d.xreq[q] = pod.xres_value[e];
+  }
   // parseGPURequirements (utils.go:487-513): GPUPartitionSpec and the GPU hint's required topology scope
   d.flags |= (uint32_t)pod.gpu_required_topology_scope * PF_GPU_SCOPE0;
   d.ring_bw = KE_ABSENT;
@@ -906,6 +969,7 @@ void flush_mirror(Context& c) {
     host_assign(c.cfg, ns, a.pod, a.ts);
     ns.node.requested[KE_RES_CPU] += a.pod.requests[KE_RES_CPU];
     ns.node.requested[KE_RES_MEMORY] += a.pod.requests[KE_RES_MEMORY];
+    if (c.ext_enabled) host_ext_reserve(ns, a.pod);
     ns.dirty = was_dirty;  // the device row already carries this Reserve
   }
   c.pending.clear();

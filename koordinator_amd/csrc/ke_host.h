@@ -39,6 +39,8 @@ struct NodeState {
   // GPU partition indexer / policy (ke_node_gpu_partitions): table id in Context::ptab, -1 = nil indexer
   int32_t ptable = -1;
   bool gpu_honor = false;
+  // NodeResourcesFitPlus / ScarceResourceAvoidance: NodeInfo Allocatable / (NonZero)Requested by resource id
+  std::vector<ke_node_resource> xres;
   // derived
   bool dirty = true;            // row must be re-derived and uploaded
   int64_t valid_until = INT64_MAX;  // derived row is exact for now < valid_until
@@ -55,6 +57,7 @@ struct Context {
   bool ds_enabled = false;       // some node has a device cache entry: the device SoA exists
   bool numa_enabled = false;     // some node has a NUMA topology policy: the NUMA SoA exists
   bool cpu_enabled = false;      // some node has a CPU table: the CPU SoA exists
+  bool ext_enabled = false;      // NodeResourcesFitPlus / ScarceResourceAvoidance in the profile: the ext SoA exists
   int32_t n_bind_nodes = 0;      // nodes with a CPU bind policy (a cpu request may bind CPUs there)
   int32_t n_policy_nodes = 0;    // nodes with a NUMA topology policy
   std::vector<uint64_t> last_cpusets;    // per pod of the last ke_schedule: 4 words (CPU-id bitset)
@@ -145,6 +148,12 @@ int validate_zones(int32_t n, const ke_numa_zone* zones);
 void derive_numa_row(const NodeState& ns, int64_t* f, uint64_t* mask);
 // host mirror of the NUMA allocation the device Reserve made: delta[z][r] per zone id
 void host_numa_reserve(NodeState& ns, const int64_t* delta /*[KE_MAX_NUMA*KE_NRES]*/);
+
+// NodeResourcesFitPlus / ScarceResourceAvoidance
+int validate_node_resources(int32_t n, const ke_node_resource* r);
+// the ext SoA row of a node: NUM_XF int64 + the uint64 mask of resource ids with Allocatable > 0
+void derive_ext_row(const ke_config& cfg, const NodeState& ns, int64_t* f, uint64_t* mask);
+void host_ext_reserve(NodeState& ns, const ke_pod& pod);
 
 // CPU topology / cpuset binding (NodeNUMAResource with NUMA policy None)
 int validate_cpus(int32_t n, const ke_cpu* cpus, int32_t max_ref);

@@ -65,6 +65,8 @@ struct SoA {
   int64_t* rec;     // replay records: NUM_RW int64 words per node, row-major (RecWord)
   uint64_t* pt;     // GPU partition tables: PT_WORDS words per table (ke_types.h), nullptr until one is set
   int32_t* kerr;    // device error word of the context (KERR_* bits; the host reads it after a call)
+  int64_t* xf;      // NodeResourcesFitPlus / ScarceResourceAvoidance: NUM_XF arrays of `stride` int64 (XF_*)
+  uint64_t* xm;     //   and `stride` uint64 masks of the resource ids with Allocatable > 0 (nullptr when off)
 };
 // kerr bits: an input the kernels refuse mid-call (the call returns KE_ERR_UNSUPPORTED)
 constexpr int32_t KERR_DS_MERGE = 1;  // a DeviceShare BestEffort merge beyond the permutation budget
@@ -1819,6 +1821,43 @@ __device__ __forceinline__ void numa_reserve(const SoA& s, int64_t i, uint32_t n
 // NUMA: some node may carry a NUMA topology policy; `nv` holds node i's zones when its policy is set.
 // CPU: the pod may bind CPUs (PF_CPUSET: a singleton batch) — cpuset PreFilter state, requestCPUBind,
 // the amplified pod cpu and the required-bind-policy checks read the CPU SoA.
+// ---- NodeResourcesFitPlus + ScarceResourceAvoidance Score ------------------------
+// Weighted framework contribution of the two plugins for a feasible (pod, node).  Go int64 arithmetic
+// (wrapping products, truncating division) on the ext SoA.
+__device__ __forceinline__ int64_t mul100_wrap(int64_t x) { return (int64_t)((uint64_t)x * 100u); }
+__device__ __forceinline__ int32_t ext_score(const SoA& s, int64_t i, const DevPod& p, const KArgs& k) {
+  int32_t t = 0;
+  if (k.wp_fp) {  // resourceScorer (node_resource_fit_plus_utils.go:57-89) over the pod's requested names
+    int64_t ns = 0, ws = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      if (q >= k.fp_n || !((p.xmask >> k.fp_id[q]) & 1)) continue;
+      const int64_t cap = s.xf[(XF_ALLOC + q) * s.stride + i];
+      int64_t req = s.xf[(XF_REQ + q) * s.stride + i] + p.xreq[q];
+      int64_t sc = 0;
+      if ((k.fp_most >> q) & 1) {  // mostRequestedScore (:35-44)
+        if (req > cap) req = cap;
+        sc = cap == 0 ? 0 : mul100_wrap(req) / cap;
+      } else {  // leastRequestedScore (:46-55)
+        sc = (cap == 0 || req > cap) ? 0 : mul100_wrap(cap - req) / cap;
+      }
+      ns += sc * k.fp_w[q];
+      ws += k.fp_w[q];
+    }
+    t += k.wp_fp * (int32_t)(ws == 0 ? 100 : ns / ws);
+  }
+  if (k.wp_sra) {  // scarce_resource_avoidance.go:70-90,159-161
+    const uint64_t diff = s.xm[i] & ~p.xmask;
+    const int nd = __popcll(diff), ni = __popcll(diff & k.sra_mask);
+    t += k.wp_sra * ((nd == 0 || ni == 0) ? 100 : (nd - ni) * 100 / nd);
+  }
+  return t;
+}
+// Reserve: NodeInfo (NonZero)Requested += the pod's requests of the FitPlus resources
+__device__ __forceinline__ void ext_reserve(const SoA& s, int64_t i, const DevPod& p, const KArgs& k) {
+  for (int q = 0; q < k.fp_n && q < 4; q++) s.xf[(XF_REQ + q) * s.stride + i] += p.xreq[q];
+}
+
 template <bool DS, bool NUMA, bool DEFER = false, bool FB_AFF = false, bool CPU = false>
 __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, const DevPod& p, const KArgs& k,
                                              const SoA& s, int64_t i, const NumaNode& nv, uint32_t fb_aff = 0) {
@@ -2039,6 +2078,7 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
   o.la = (int16_t)la;
   o.numa = (int16_t)nu;
   o.total = k.wp_la * la + k.wp_numa * nu;
+  if (k.flags & AF_EXT) o.total += ext_score(s, i, p, k);
   return o;
 }
 
@@ -3511,6 +3551,7 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
           mine.nreq[0] += pod.req[0];
           mine.nreq[1] += pod.req[1];
         }
+        if (!FAST && (k.flags & AF_EXT)) ext_reserve(s, my_node, pod, k);  // read back by the next re-evaluations
         // DeviceShare Reserve (a DeviceShare pod is alone in its batch: no later pod of the batch
         // reads the device state it patches)
         const uint32_t nfl = FAST ? fast.nflags : mine.flags;
@@ -4020,6 +4061,7 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
     RPROF(2)
     if (ok) {
       reserve_row(s, node, nf, pod);
+      if (k.flags & AF_EXT) ext_reserve(s, node, pod, k);
       {  // the node's replay record follows its patched row
         NodeRegs nr;
         load_row(s, node, nr);
@@ -4138,6 +4180,9 @@ struct DeviceState {
   int64_t* d_numaalloc = nullptr;  // [n_pods][16] per-zone allocation of each pod (ke_schedule)
   int64_t* d_numarows = nullptr;   // staging for NUMA row uploads
   int64_t numa_staging_cap = 0;
+  bool ext_alloc = false;          // soa.xf / soa.xm allocated (NodeResourcesFitPlus / ScarceResourceAvoidance)
+  int64_t* d_xrows = nullptr;      // staging for ext row uploads
+  int64_t ext_staging_cap = 0;
   uint64_t* d_defer = nullptr;     // deferred BestEffort pairs of one eval launch (k_numa_fallback)
   int64_t defer_cap = 0;           // bytes
   uint32_t* d_defer_cnt = nullptr; // one counter per batch of a ke_schedule (or the ke_eval launch)
@@ -4243,7 +4288,8 @@ void device_destroy(Context* ctx) {
                   d->d_dsraw,   d->d_dsmax,  d->d_devalloc,   d->d_dsrows,       d->soa.nf,   d->soa.nm,
                   d->d_numaalloc, d->d_numarows, d->d_defer, d->d_defer_cnt, d->soa.cs, d->soa.cpu,
                   d->d_cpurows, d->d_cpusets, d->d_aff, d->soa.qt, d->soa.qm, d->d_sched, d->d_stale,
-                  d->d_stale_cnt, d->d_trows, d->d_tcnt, d->d_chg, d->soa.rec, d->soa.pt, d->soa.kerr};
+                  d->d_stale_cnt, d->d_trows, d->d_tcnt, d->d_chg, d->soa.rec, d->soa.pt, d->soa.kerr,
+                  d->soa.xf, d->soa.xm, d->d_xrows};
   if (d->estream) (void)hipStreamSynchronize(d->estream);
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -4398,6 +4444,29 @@ static int ensure_numa(Context* ctx) {
   return KE_OK;
 }
 
+constexpr int XROW_WORDS = NUM_XF + 1;  // ext row: NUM_XF int64 + the mask
+
+__global__ void k_scatter_ext(SoA s, const int64_t* __restrict__ rows, const int32_t* __restrict__ idx, int n) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int64_t i = idx[t];
+  const int64_t* r = rows + (int64_t)t * XROW_WORDS;
+  for (int f = 0; f < NUM_XF; f++) s.xf[f * s.stride + i] = r[f];
+  s.xm[i] = (uint64_t)r[NUM_XF];
+}
+
+static int ensure_ext(Context* ctx) {
+  DeviceState* d = ctx->dev;
+  if (d->ext_alloc || !ctx->ext_enabled) return KE_OK;
+  HIP_OK(hipMalloc(&d->soa.xf, sizeof(int64_t) * NUM_XF * d->capacity));
+  HIP_OK(hipMalloc(&d->soa.xm, sizeof(uint64_t) * d->capacity));
+  HIP_OK(hipMemsetAsync(d->soa.xf, 0, sizeof(int64_t) * NUM_XF * d->capacity, d->stream));
+  HIP_OK(hipMemsetAsync(d->soa.xm, 0, sizeof(uint64_t) * d->capacity, d->stream));
+  d->ext_alloc = true;
+  for (int32_t i = 0; i < ctx->n_nodes; i++) ctx->nodes[i].dirty = true;
+  return KE_OK;
+}
+
 constexpr int CPU_ROW_WORDS = CPU_SLOTS + NUM_CS_FIELDS;  // records (one int64 each) + summary
 
 __global__ void k_scatter_cpu(SoA s, const int64_t* __restrict__ rows, const int32_t* __restrict__ idx, int n) {
@@ -4439,6 +4508,8 @@ int device_refresh(Context* ctx, int64_t now) {
   if (rc) return rc;
   rc = ensure_cpu(ctx);
   if (rc) return rc;
+  rc = ensure_ext(ctx);
+  if (rc) return rc;
   if (ctx->ptab_dirty) {  // GPU partition tables (ke_node_gpu_partitions); the pool only grows
     if (d->pt_words < ctx->ptab.size()) {
       if (d->soa.pt) HIP_OK(hipFree(d->soa.pt));
@@ -4459,6 +4530,8 @@ int device_refresh(Context* ctx, int64_t now) {
   std::vector<int32_t> dsidx;
   std::vector<int64_t> nrows;  // NUMA rows of the dirty nodes
   std::vector<int32_t> nidx;
+  std::vector<int64_t> xrows;  // ext rows of the dirty nodes
+  std::vector<int32_t> xidx;
   for (int32_t i = 0; i < ctx->n_nodes; i++) {
     NodeState& ns = ctx->nodes[i];
     if (!ns.dirty && now < ns.valid_until) continue;
@@ -4478,6 +4551,14 @@ int device_refresh(Context* ctx, int64_t now) {
       derive_numa_row(ns, &nrows[o], &mask);
       nrows[o + NUM_NUMA_FIELDS] = (int64_t)mask;
       nidx.push_back(i);
+    }
+    if (ns.dirty && d->ext_alloc) {
+      const size_t o = xrows.size();
+      xrows.resize(o + XROW_WORDS);
+      uint64_t mask;
+      derive_ext_row(ctx->cfg, ns, &xrows[o], &mask);
+      xrows[o + NUM_XF] = (int64_t)mask;
+      xidx.push_back(i);
     }
     if (ns.dirty && d->cpu_alloc) {
       const size_t o = crows.size();
@@ -4519,6 +4600,21 @@ int device_refresh(Context* ctx, int64_t now) {
                        didx, (int)n);
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(d->stream));  // `nrows` is a local host vector
+  }
+  if (!xidx.empty()) {
+    const int64_t n = (int64_t)xidx.size();
+    if (d->ext_staging_cap < n) {
+      if (d->d_xrows) HIP_OK(hipFree(d->d_xrows));
+      HIP_OK(hipMalloc(&d->d_xrows, sizeof(int64_t) * XROW_WORDS * n + sizeof(int32_t) * n));
+      d->ext_staging_cap = n;
+    }
+    int32_t* didx = reinterpret_cast<int32_t*>(d->d_xrows + XROW_WORDS * n);
+    HIP_OK(hipMemcpyAsync(d->d_xrows, xrows.data(), sizeof(int64_t) * xrows.size(), hipMemcpyHostToDevice, d->stream));
+    HIP_OK(hipMemcpyAsync(didx, xidx.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, d->stream));
+    hipLaunchKernelGGL(k_scatter_ext, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, d->stream, d->soa, d->d_xrows,
+                       didx, (int)n);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(d->stream));  // `xrows` is a local host vector
   }
   if (!cidx.empty()) {
     const int64_t n = (int64_t)cidx.size();

@@ -194,8 +194,12 @@ struct DevPod {
   uint8_t quota;      // ElasticQuota: 0 = none, else 1 + quota index (ke_pod.quota)
   int64_t ds_req[5];  // DeviceShare per-instance request: gpu-core, gpu-memory, gpu-memory-ratio, rdma, fpga
   int64_t ring_bw;    // GPUPartitionSpec.RingBusBandwidth (PF_GPU_RING_BW)
+  // NodeResourcesFitPlus / ScarceResourceAvoidance: the pod's request of each FitPlus resource (slot order of
+  // KArgs::fp_id, calculatePodResourceRequest), and the ids of its requested resource names (PodRequests > 0)
+  int64_t xreq[4];
+  uint64_t xmask;
 };
-static_assert(sizeof(DevPod) == 88, "DevPod layout");
+static_assert(sizeof(DevPod) == 128, "DevPod layout");
 KE_HD inline int pod_scope(uint32_t flags) { return (int)((flags >> 24) & 7u); }
 KE_HD inline int scope_level(int scope) { return scope >= 1 && scope <= 4 ? scope : 0; }
 
@@ -254,6 +258,7 @@ enum ArgFlag : uint32_t {
   AF_QUOTA = 1u << 6,               // an ElasticQuota tree is loaded: PreFilter admission + Reserve
   AF_QUOTA_PARENT = 1u << 7,        // ElasticQuotaArgs.EnableCheckParentQuota
   AF_DS_NO_NUMA = 1u << 8,          // DeviceShareArgs.DisableDeviceNUMATopologyAlignment
+  AF_EXT = 1u << 9,                 // NodeResourcesFitPlus / ScarceResourceAvoidance in the profile (ext SoA)
 };
 struct KArgs {
   int64_t now;
@@ -265,14 +270,24 @@ struct KArgs {
   uint32_t flags;
   int32_t wp_ds;           // DeviceShare plugin weight
   int32_t w_ds[4];         // DeviceShare ScoringStrategy weights (KE_DSW_*), -1 = absent
+  // NodeResourcesFitPlus (fp_n resources: id, weight, MostAllocated bit) and ScarceResourceAvoidance
+  int32_t wp_fp, wp_sra;   // plugin weights (0 = not in the profile)
+  int32_t fp_n;
+  uint32_t fp_most;        // bit q: slot q scores MostAllocated
+  int32_t fp_id[4];
+  int64_t fp_w[4];
+  uint64_t sra_mask;       // ScarceResourceAvoidanceArgs.Resources (resource ids)
 };
+// ext SoA (NodeResourcesFitPlus / ScarceResourceAvoidance): XF_ALLOC + q / XF_REQ + q = NodeInfo.Allocatable /
+// (NonZero)Requested of FitPlus slot q, plus a uint64 mask per node of the resource ids with Allocatable > 0
+constexpr int XF_ALLOC = 0, XF_REQ = 4, NUM_XF = 8;
 
 // Packed candidate key: higher is better.  (score+1) in the top 9 bits, inverted node index in the
 // low 23 bits, so max(key) == selectHost with ties resolved to the lowest node index.
 constexpr uint32_t KEY_IDX_BITS = 23;
 constexpr uint32_t KEY_IDX_MASK = (1u << KEY_IDX_BITS) - 1;
 constexpr int MAX_SHARD_NODES = (1 << KEY_IDX_BITS) - 1;
-constexpr int MAX_TOTAL_SCORE = 510;  // (score+1) must fit in 9 bits
+constexpr int MAX_TOTAL_SCORE = 510;  // (score+1) must fit in 9 bits: Σ plugin weight * 100 <= 510
 constexpr int MAX_DS_RAW = 300;       // DeviceShare raw score: <= 100 per device type
 KE_HD inline uint32_t make_key(int32_t total, int32_t idx) {
   return total < 0 ? 0u : ((uint32_t)(total + 1) << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)idx);

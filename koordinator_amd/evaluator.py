@@ -133,6 +133,17 @@ class Evaluator:
         zones = np.ascontiguousarray(zones, dtype=abi.NUMA_ZONE_DTYPE)
         self._check(self.lib.ke_node_numa_set(self.h, i, len(zones), abi.ptr(zones)))
 
+    def set_resources(self, i, resources):
+        """NodeResourcesFitPlus / ScarceResourceAvoidance table of node i (np.ndarray NODE_RESOURCE_DTYPE)."""
+        res = np.ascontiguousarray(resources, dtype=abi.NODE_RESOURCE_DTYPE)
+        self._check(self.lib.ke_node_resources_set(self.h, i, len(res), abi.ptr(res)))
+
+    def get_resources(self, i):
+        out = np.zeros(abi.MAX_XRES, abi.NODE_RESOURCE_DTYPE)
+        n = abi.i32()
+        self._check(self.lib.ke_node_resources_get(self.h, i, abi.MAX_XRES, abi.ptr(out), C.byref(n)))
+        return out[:n.value]
+
     def set_cpus(self, i, cpus, max_ref_count=1):
         """CPU topology + cpuset allocation state (model.make_cpus(...)); an empty table clears it."""
         cpus = np.ascontiguousarray(cpus, dtype=abi.CPU_DTYPE)

@@ -191,6 +191,67 @@ def _fill_resources(arr, rl):
     return other
 
 
+# Resource-name ids of NodeResourcesFitPlus / ScarceResourceAvoidance (koord_eval.h KE_XRES_*): cpu and memory
+# fixed, every other name interned on first use (a Go shim keeps the same table per context).
+XRES_IDS = {"cpu": abi.XRES_CPU, "memory": abi.XRES_MEMORY}
+DEFAULT_MILLI_CPU_REQUEST = 100                 # schedutil.DefaultMilliCPURequest
+DEFAULT_MEMORY_REQUEST = 200 * 1024 * 1024      # schedutil.DefaultMemoryRequest
+
+
+def xres_id(name):
+    if name not in XRES_IDS:
+        if len(XRES_IDS) >= abi.MAX_XRES:
+            raise ValueError("more than 64 resource names")
+        XRES_IDS[name] = len(XRES_IDS)
+    return XRES_IDS[name]
+
+
+def _nonzero_request(name, requests):
+    """GetNonzeroRequestForResource (node_resource_fit_plus_utils.go:167-203)."""
+    requests = requests or {}
+    if name == "cpu":
+        return milli_value(requests["cpu"]) if "cpu" in requests else DEFAULT_MILLI_CPU_REQUEST
+    if name == "memory":
+        return value(requests["memory"]) if "memory" in requests else DEFAULT_MEMORY_REQUEST
+    return value(requests[name]) if name in requests else 0
+
+
+def fitplus_pod_request(name, containers, init_containers=()):
+    """calculatePodResourceRequest (node_resource_fit_plus_utils.go:138-165), without pod Overhead."""
+    r = sum(_nonzero_request(name, c.get("requests")) for c in containers)
+    for ic in init_containers:
+        r = max(r, _nonzero_request(name, ic.get("requests")))
+    return r
+
+
+def _fill_xres(p, reqs, containers, init_containers):
+    """ke_pod.xres_*: the ids of the names PodRequests holds > 0 and their calculatePodResourceRequest."""
+    names = [k for k, v in reqs.items() if v > 0]
+    mask = 0
+    for k in names:
+        mask |= 1 << xres_id(k)
+    p.xres_request_mask = mask
+    if len(names) > abi.MAX_POD_XRES:
+        raise ValueError("more than 8 requested resource names")
+    p.n_xres = len(names)
+    for e, k in enumerate(names):
+        p.xres_id[e] = xres_id(k)
+        p.xres_value[e] = fitplus_pod_request(k, containers, init_containers)
+
+
+def make_node_resources(allocatable, requested=None):
+    """NodeInfo Allocatable / (NonZero)Requested by resource id (ke_node_resource table).  `requested` is what
+    calculateResourceAllocatableRequest reads: NonZeroRequested for cpu/memory, Requested otherwise."""
+    requested = requested or {}
+    names = list(dict.fromkeys(list(allocatable) + list(requested)))
+    arr = np.zeros(len(names), abi.NODE_RESOURCE_DTYPE)
+    for e, k in enumerate(names):
+        arr[e]["id"] = xres_id(k)
+        arr[e]["allocatable"] = resource_value(k, allocatable.get(k, 0))
+        arr[e]["requested"] = resource_value(k, requested.get(k, 0))
+    return arr
+
+
 _uid = [0]
 
 
@@ -219,6 +280,7 @@ def make_pod(name="pod", namespace="default", requests=None, limits=None, contai
     other = _fill_resources(p.requests, reqs)
     _fill_resources(p.limits, lims)
     p.has_other_requests = 1 if other else 0
+    _fill_xres(p, reqs, containers, init_containers)
     for k, v in reqs.items():  # DeviceShare reads PodRequests (utils.go:392-412), Value() of each
         if k in abi.PDR and v != 0:
             p.device_requests[abi.PDR[k]] = value(v)

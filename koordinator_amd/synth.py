@@ -731,3 +731,90 @@ def assign_quotas(pods, quotas, seed, no_quota_fraction=0.1, non_preemptible_fra
             if quotas[qi]["has_max"][r]:
                 quotas[qi]["self_request"][r] += pods[p]["requests"][res]
     return pods
+
+
+# ---- NodeResourcesFitPlus / ScarceResourceAvoidance -------------------------------
+# Resource ids of the synthetic profile: the KE_RES_* names plus ephemeral storage and two extended resources
+# (a GPU count and a scarce device that most pods never request).
+XRES = {"cpu": abi.XRES_CPU, "memory": abi.XRES_MEMORY, "kubernetes.io/batch-cpu": 2, "kubernetes.io/batch-memory": 3,
+        "ephemeral-storage": 4, "nvidia.com/gpu": 5, "example.com/scarce": 6}
+_POD_RES = ((abi.RES_CPU, 0), (abi.RES_MEMORY, 1), (abi.RES_BATCH_CPU, 2), (abi.RES_BATCH_MEMORY, 3))
+
+
+def ext_config(cfg, w_fitplus=1, w_sra=1, fitplus=None, sra=("nvidia.com/gpu", "example.com/scarce")):
+    """The profile of config/manager/scheduler-config.yaml's resource scorer (cpu, memory, batch-cpu,
+    batch-memory at weight 1) as NodeResourcesFitPlus args, GPUs MostAllocated, plus ScarceResourceAvoidance."""
+    x = cfg.ext
+    x.weight_fitplus, x.weight_sra = w_fitplus, w_sra
+    fitplus = fitplus if fitplus is not None else [("cpu", abi.STRATEGY_LEAST_ALLOCATED, 1),
+                                                   ("memory", abi.STRATEGY_LEAST_ALLOCATED, 1),
+                                                   ("kubernetes.io/batch-cpu", abi.STRATEGY_LEAST_ALLOCATED, 1),
+                                                   ("nvidia.com/gpu", abi.STRATEGY_MOST_ALLOCATED, 2)]
+    x.n_fitplus = len(fitplus)
+    for q, (name, typ, w) in enumerate(fitplus):
+        x.fitplus[q].id, x.fitplus[q].type, x.fitplus[q].weight = XRES[name], typ, w
+    x.sra_resources = sum(1 << XRES[n] for n in sra)
+    return cfg
+
+
+def make_node_resources(cl, seed, gpu_fraction=0.3, scarce_fraction=0.15):
+    """Per node a ke_node_resource table consistent with the cluster: Allocatable cpu / memory of the node,
+    NonZeroRequested = Requested (+ the 100m / 200Mi defaults of a few zero-request pods), batch resources,
+    ephemeral storage, and on some nodes GPUs / a scarce device with random usage."""
+    rng = np.random.default_rng(seed)
+    tables = []
+    for i in range(cl.n_nodes):
+        n = cl.nodes[i]
+        rows = [(XRES["cpu"], int(n["allocatable"][0]), int(n["requested"][0]) + 100 * int(rng.integers(0, 3))),
+                (XRES["memory"], int(n["allocatable"][1]), int(n["requested"][1]) + 200 * 2**20 * int(rng.integers(0, 3)))]
+        if rng.random() < 0.8:
+            bc = int(rng.integers(8, 65)) * 1000
+            rows.append((2, bc, int(rng.integers(0, bc // 1000 + 8)) * 1000))
+            bm = int(rng.integers(32, 257)) * GI
+            rows.append((3, bm, int(rng.integers(0, bm // GI + 8)) * GI))
+        if rng.random() < 0.9:
+            rows.append((4, int(rng.integers(100, 1000)) * GI, int(rng.integers(0, 100)) * GI))
+        if rng.random() < gpu_fraction:
+            g = int(rng.choice([4, 8]))
+            rows.append((5, g, int(rng.integers(0, g + 1))))
+        if rng.random() < scarce_fraction:
+            rows.append((6, int(rng.integers(1, 4)), 0))
+        if rng.random() < 0.03:  # a listed resource with zero allocatable: not a name of the node
+            rows.append((6 if rows[-1][0] != 6 else 5, 0, 0))
+        t = np.zeros(len(rows), abi.NODE_RESOURCE_DTYPE)
+        for e, (rid, a, r) in enumerate(rows):
+            t[e]["id"], t[e]["allocatable"], t[e]["requested"] = rid, a, r
+        tables.append(t)
+    return tables
+
+
+def load_node_resources(handle, tables):
+    for i, t in enumerate(tables):
+        handle.set_resources(i, t)
+
+
+def add_pod_xres(pods, seed, gpu_fraction=0.2, storage_fraction=0.5, scarce_fraction=0.03):
+    """ke_pod.xres_*: the requested names of each pod (PodRequests > 0) and calculatePodResourceRequest; a few
+    pods request GPUs, ephemeral storage or the scarce device, a few have a container without a cpu / memory
+    request (the 100m / 200Mi nonzero defaults)."""
+    rng = np.random.default_rng(seed)
+    for p in range(len(pods)):
+        mask, ids, vals = 0, [], []
+        for r, rid in _POD_RES:
+            v = int(pods["requests"][p, r])
+            if v > 0:
+                mask |= 1 << rid
+                extra = 0
+                if rid in (0, 1) and rng.random() < 0.1:  # a second container without this request
+                    extra = 100 if rid == 0 else 200 * 2**20
+                ids.append(rid), vals.append(v + extra)
+        for rid, frac, lo, hi in ((5, gpu_fraction, 1, 5), (4, storage_fraction, 1, 50), (6, scarce_fraction, 1, 2)):
+            if rng.random() < frac:
+                v = int(rng.integers(lo, hi)) * (GI if rid == 4 else 1)
+                mask |= 1 << rid
+                ids.append(rid), vals.append(v)
+        pods["xres_request_mask"][p] = mask
+        pods["n_xres"][p] = len(ids)
+        pods["xres_id"][p, :len(ids)] = ids
+        pods["xres_value"][p, :len(ids)] = vals
+    return pods

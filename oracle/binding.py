@@ -57,6 +57,9 @@ def load():
         "or_topology_merge": (C.c_int, [i32, C.c_uint32, i32, V, V, V, V, V, V, V, V, V]),
         "or_node_numa_set": (C.c_int, [V, i32, i32, V]),
         "or_node_cpus_set": (C.c_int, [V, i32, i32, V, i32]),
+        "or_node_resources_set": (C.c_int, [V, i32, i32, V]),
+        "or_fitplus_score": (i64, [V, C.POINTER(abi.Pod), i32]),
+        "or_sra_score": (i64, [V, C.POINTER(abi.Pod), i32]),
         "or_numa_distribute": (C.c_int, [V, i32, V, C.c_uint32, V]),
         "or_numa_allocate": (C.c_int, [V, i32, V, C.c_uint32, V, V]),
         "or_set_exact_cpusets": (None, [C.c_int]),
@@ -165,6 +168,16 @@ class Oracle:
 
     def delete_devices(self, i):
         assert self.lib.or_node_devices_delete(self.h, i) == 0
+
+    def set_resources(self, i, resources):
+        res = np.ascontiguousarray(resources, dtype=abi.NODE_RESOURCE_DTYPE)
+        assert self.lib.or_node_resources_set(self.h, i, len(res), abi.ptr(res)) == 0
+
+    def fitplus_score(self, pod, i):
+        return self.lib.or_fitplus_score(self.h, C.byref(pod), i)
+
+    def sra_score(self, pod, i):
+        return self.lib.or_sra_score(self.h, C.byref(pod), i)
 
     def set_cpus(self, i, cpus, max_ref_count=1):
         cpus = np.ascontiguousarray(cpus, dtype=abi.CPU_DTYPE)

@@ -61,6 +61,9 @@ typedef struct or_node {
   int32_t n_part;
   ke_gpu_partition part[KE_MAX_GPU_PARTITIONS];
   struct or_cpus* cpus; /* CPU topology + allocated CPUs (NULL: no CPU topology) */
+  /* NodeInfo Allocatable / (NonZero)Requested by resource id (NodeResourcesFitPlus, ScarceResourceAvoidance) */
+  int32_t n_xres;
+  ke_node_resource xres[KE_MAX_XRES];
 } or_node;
 
 /* TopologyOptions.CPUTopology / ReservedCPUs / MaxRefCount + NodeAllocation.allocatedCPUs */
@@ -2703,6 +2706,88 @@ int or_numa_allocate(const or_cluster* c, int32_t node, const ke_pod* pod, uint3
   return 0;
 }
 
+/* ---------------------------------------------------------------------------------------------- */
+/* NodeResourcesFitPlus / ScarceResourceAvoidance                            */
+/* ---------------------------------------------------------------------------------------------- */
+
+int or_node_resources_set(or_cluster* c, int32_t node, int32_t n, const ke_node_resource* res) {
+  if (node < 0 || node >= c->n) return KE_ERR_NOT_FOUND;
+  if (n < 0 || n > KE_MAX_XRES) return KE_ERR_INVALID;
+  c->nodes[node].n_xres = n;
+  if (n) memcpy(c->nodes[node].xres, res, sizeof(ke_node_resource) * (size_t)n);
+  return KE_OK;
+}
+
+static const ke_node_resource* node_xres(const or_node* nd, int32_t id) {
+  for (int32_t e = 0; e < nd->n_xres; e++)
+    if (nd->xres[e].id == id) return &nd->xres[e];
+  return NULL;
+}
+
+/* calculatePodResourceRequest (node_resource_fit_plus_utils.go:138-165) as the caller computed it */
+static int64_t pod_xres(const ke_pod* pod, int32_t id) {
+  for (int32_t e = 0; e < pod->n_xres; e++)
+    if (pod->xres_id[e] == id) return pod->xres_value[e];
+  return 0;
+}
+
+/* Go int64 multiply (wraps) */
+static int64_t mul_wrap(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }
+
+/* mostRequestedScore / leastRequestedScore (node_resource_fit_plus_utils.go:35-55) */
+static int64_t fp_most(int64_t requested, int64_t capacity) {
+  if (capacity == 0) return 0;
+  if (requested > capacity) requested = capacity;
+  return mul_wrap(requested, MAX_NODE_SCORE) / capacity;
+}
+static int64_t fp_least(int64_t requested, int64_t capacity) {
+  if (capacity == 0) return 0;
+  if (requested > capacity) return 0;
+  return mul_wrap(capacity - requested, MAX_NODE_SCORE) / capacity;
+}
+
+/* NodeResourcesFitPlus Score (node_resources_fit_plus.go:75-93 -> getResourceScore -> resourceScorer,
+ * node_resource_fit_plus_utils.go:57-103): for every resource name the pod requests (PodRequests > 0,
+ * fitsPodRequestName) that the args list, calculateResourceAllocatableRequest gives allocatable and
+ * NodeInfo (NonZero)Requested + the pod's request; score = Σ score·weight / Σ weight (MaxNodeScore for a
+ * zero weight sum).  The map's iteration order does not matter: integer sums. */
+int64_t or_fitplus_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
+  const or_node* nd = &c->nodes[node];
+  const ke_ext_args* x = &c->cfg.ext;
+  int64_t node_score = 0, weight_sum = 0;
+  for (int32_t id = 0; id < KE_MAX_XRES; id++) {
+    if (!((pod->xres_request_mask >> id) & 1)) continue;
+    const ke_fitplus_resource* ra = NULL;
+    for (int q = 0; q < x->n_fitplus; q++)
+      if (x->fitplus[q].id == id) ra = &x->fitplus[q];
+    if (!ra) continue;
+    const ke_node_resource* r = node_xres(nd, id);
+    const int64_t alloc = r ? r->allocatable : 0;
+    const int64_t req = (r ? r->requested : 0) + pod_xres(pod, id);
+    const int64_t rs = ra->type == KE_STRATEGY_MOST_ALLOCATED ? fp_most(req, alloc) : fp_least(req, alloc);
+    node_score += rs * ra->weight;
+    weight_sum += ra->weight;
+  }
+  if (weight_sum == 0) return MAX_NODE_SCORE;
+  return node_score / weight_sum;
+}
+
+/* ScarceResourceAvoidance Score (scarce_resource_avoidance.go:70-90): the node's allocatable names (> 0)
+ * minus the pod's requested names (quotav1.Difference), intersected with args.Resources; resourceTypesScore
+ * (:159-161). */
+int64_t or_sra_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
+  const or_node* nd = &c->nodes[node];
+  int64_t n_diff = 0, n_inter = 0;
+  for (int32_t e = 0; e < nd->n_xres; e++) {
+    const int32_t id = nd->xres[e].id;
+    if (nd->xres[e].allocatable <= 0 || ((pod->xres_request_mask >> id) & 1)) continue;
+    n_diff++;
+    if ((c->cfg.ext.sra_resources >> id) & 1) n_inter++;
+  }
+  if (n_diff == 0 || n_inter == 0) return MAX_NODE_SCORE;
+  return (n_diff - n_inter) * MAX_NODE_SCORE / n_diff;
+}
+
 int or_node_numa_set(or_cluster* c, int32_t node, int32_t n, const ke_numa_zone* zones) {
   if (node < 0 || node >= c->n) return KE_ERR_NOT_FOUND;
   if (n < 0 || n > KE_MAX_NUMA) return KE_ERR_INVALID;
@@ -2859,6 +2944,7 @@ int or_pod_unassign(or_cluster* c, int32_t node, int64_t uid) {
 typedef struct eval_out {
   uint8_t status, reason;
   int16_t la, numa, ds, total; /* ds: DeviceShare.Score before NormalizeScore */
+  int16_t fp, sra;              /* NodeResourcesFitPlus, ScarceResourceAvoidance */
 } eval_out;
 
 /* RunFilterPlugins in profile order LoadAware, NodeNUMAResource, DeviceShare
@@ -2884,9 +2970,11 @@ static void eval_pair(const or_cluster* c, const ke_pod* pod, int32_t node, int6
   if (code == KE_CODE_SUCCESS) code = or_ds_filter(c, pod, node, &reason);
   o->status = (uint8_t)code;
   o->reason = (uint8_t)reason;
-  o->la = o->numa = o->ds = 0;
+  o->la = o->numa = o->ds = o->fp = o->sra = 0;
   o->total = -1;
   if (code != KE_CODE_SUCCESS) return;
+  if (c->cfg.ext.weight_fitplus) o->fp = (int16_t)or_fitplus_score(c, pod, node);
+  if (c->cfg.ext.weight_sra) o->sra = (int16_t)or_sra_score(c, pod, node);
   o->la = (int16_t)or_la_score(c, pod, node, now);
   o->numa = (int16_t)or_numa_score(c, pod, node);
   o->ds = (int16_t)or_ds_score(c, pod, node);
@@ -2903,7 +2991,8 @@ static void normalize_and_total(const or_cluster* c, eval_out* o, int64_t n) {
     if (o[i].status != KE_CODE_SUCCESS) continue;
     const int64_t ds = mx > 0 ? MAX_NODE_SCORE * o[i].ds / mx : o[i].ds;
     o[i].total = (int16_t)(c->cfg.weight_loadaware * o[i].la + c->cfg.weight_numa * o[i].numa +
-                           c->cfg.weight_deviceshare * ds);
+                           c->cfg.weight_deviceshare * ds + c->cfg.ext.weight_fitplus * o[i].fp +
+                           c->cfg.ext.weight_sra * o[i].sra);
   }
 }
 
@@ -3041,6 +3130,16 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
       mask = ds_reserve_on(c, &pods[p], b, da);
       c->nodes[b].node.requested[KE_RES_CPU] += pods[p].requests[KE_RES_CPU];
       c->nodes[b].node.requested[KE_RES_MEMORY] += pods[p].requests[KE_RES_MEMORY];
+      /* NodeInfo (NonZero)Requested of every resource the pod requests (NodeResourcesFitPlus reads them) */
+      or_node* nb = &c->nodes[b];
+      for (int32_t e = 0; e < pods[p].n_xres; e++) {
+        ke_node_resource* r = (ke_node_resource*)node_xres(nb, pods[p].xres_id[e]);
+        if (r) r->requested += pods[p].xres_value[e];
+        else if (pods[p].xres_value[e] != 0 && nb->n_xres < KE_MAX_XRES) {
+          ke_node_resource z = {pods[p].xres_id[e], 0, 0, pods[p].xres_value[e]};
+          nb->xres[nb->n_xres++] = z;
+        }
+      }
       if (c->quotas) orq_reserve(c->quotas, &pods[p]); /* ElasticQuota Reserve */
     }
     if (dev_alloc) dev_alloc[p] = mask;

@@ -35,6 +35,10 @@ int or_node_devices_set(or_cluster* c, int32_t node, int32_t n, const ke_device*
 int or_node_numa_set(or_cluster* c, int32_t node, int32_t n, const ke_numa_zone* zones);
 int or_node_cpus_set(or_cluster* c, int32_t node, int32_t n, const ke_cpu* cpus, int32_t max_ref);
 int or_node_devices_delete(or_cluster* c, int32_t node);
+/* NodeResourcesFitPlus / ScarceResourceAvoidance: the node's resources by id, and the two raw scores */
+int or_node_resources_set(or_cluster* c, int32_t node, int32_t n, const ke_node_resource* res);
+int64_t or_fitplus_score(const or_cluster* c, const ke_pod* pod, int32_t node);
+int64_t or_sra_score(const or_cluster* c, const ke_pod* pod, int32_t node);
 int or_node_gpu_partitions(or_cluster* c, int32_t node, int32_t has_table, int32_t honor, int32_t n,
                            const ke_gpu_partition* parts);
 
