@@ -79,7 +79,7 @@ def test_ext_eval_matrix_parity(gpu):
     assert_eval_equal(ev.eval(pods, synth.T0), o.eval(pods, synth.T0))
 
 
-@pytest.mark.parametrize("ext", [dict(), dict(w_sra=0), dict(w_fitplus=0), dict(w_fitplus=2, w_sra=1)],
+@pytest.mark.parametrize("ext", [dict(), dict(w_sra=0), dict(w_fitplus=0), dict(w_fitplus=2, w_sra=0)],
                          ids=["both", "fitplus", "sra", "fitplus-w2"])
 def test_ext_schedule_parity(gpu, ext):
     ev, o, tables = _cluster(600, 311, **ext)
