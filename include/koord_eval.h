@@ -661,6 +661,42 @@ int ke_quotas_load(ke_ctx* ctx, const ke_quota_args* args, const ke_quota* quota
  * current used / non-preemptible used (after the Reserves of the last ke_schedule). */
 int ke_quota_state(ke_ctx* ctx, int32_t q, int64_t* limit, uint8_t* limit_has, int64_t* used, int64_t* np_used);
 
+/* ---- wire-format decoders ------------------------------------------------
+ * The informer objects as the apiserver serves them (JSON) -> the structs above, the way the reference's
+ * listers and apis/extension helpers read them per call.  Context-free, host-only, thread-safe.  Malformed
+ * objects -> KE_ERR_INVALID; values the structs cannot carry (a policy string outside the known ones,
+ * thresholds on other resources, quantities beyond int64, ...) -> KE_ERR_UNSUPPORTED.
+ *   ke_quantity_parse     resource.ParseQuantity + Value() / MilliValue() (both round up)
+ *   ke_pod_key            the interned key ke_pod.pod_key / ke_pod_metric.pod_key use: FNV-1a 64 of
+ *                         "namespace/name" (top bit cleared); ke_decode_pod / ke_decode_node_metric use it
+ *   ke_decode_node        Node: status.allocatable; annotations node.koordinator.sh/raw-allocatable,
+ *                         node.koordinator.sh/resource-amplification-ratio, scheduling.koordinator.sh/usage-thresholds
+ *                         (node_resource_amplification.go:45-124, load_aware.go:42-72, default_estimator.go:124-143);
+ *                         labels node.koordinator.sh/numa-topology-policy, cpu-bind-policy, numa-allocate-strategy
+ *                         (numa_aware.go:54-59,354-369, nodenumaresource/util.go:41-47).  NodeInfo.Requested, the
+ *                         cpuset count and the NodeResourceTopology-side fields (kubelet policies, NRT ratios,
+ *                         CPU topology validity) are not in a Node object: left 0 / "no NRT".
+ *   ke_decode_node_metric NodeMetric (slo/v1alpha1/nodemetric_types.go:38-136): header, up to pm_cap pod metrics
+ *                         (nil entries skipped) and agg_cap aggregated usages.
+ *   ke_decode_pod         Pod: PodRequests / PodLimits (k8s v1.28; restartable init containers -> UNSUPPORTED),
+ *                         classes (priority_utils.go:37-58, qos_utils.go:32-68), DaemonSet owner, phase, the
+ *                         PodScheduled / Initialized conditions, the LoadAware estimation annotations
+ *                         (load_aware.go:75-100), ResourceSpec / NUMATopologySpec, the preemptible label, the
+ *                         DeviceShare annotations; xres_names[id] = the resource name of id (NodeResourcesFitPlus /
+ *                         ScarceResourceAvoidance, n_names <= KE_MAX_XRES).  ke_pod.quota is left 0: the caller
+ *                         maps the quota label to its ke_quotas_load index.
+ *   ke_decode_device      Device (scheduling/v1alpha1/device_types.go:32-67) as nodeDeviceCache builds it
+ *                         (device_cache.go:518-568; `used` is the pods' business: 0), the gpu-partitions annotation
+ *                         (table in ascending key order) and the gpu-partition-policy label. */
+int ke_quantity_parse(const char* s, int64_t* value, int64_t* milli_value);
+int64_t ke_pod_key(const char* ns, const char* name);
+int ke_decode_node(const char* json, int64_t len, ke_node* out);
+int ke_decode_node_metric(const char* json, int64_t len, ke_node_metric* nm, int32_t pm_cap, ke_pod_metric* pm,
+                          int32_t* n_pm, int32_t agg_cap, ke_aggregated_usage* agg, int32_t* n_agg);
+int ke_decode_pod(const char* json, int64_t len, int32_t n_names, const char* const* xres_names, ke_pod* out);
+int ke_decode_device(const char* json, int64_t len, int32_t cap, ke_device* out, int32_t* n, int32_t part_cap,
+                     ke_gpu_partition* parts, int32_t* n_parts, int32_t* has_table, int32_t* honor);
+
 /* ---- node sharding across GPUs (one process per GPU) ------------------------------------------
  * Replaces the upstream Parallelizer's fan-out of per-node Filter/Score over goroutines
  * (cmd/koord-scheduler/app/server.go:417, Parallelism) with a fan-out of node ranges over GPUs.

@@ -397,6 +397,14 @@ EXPORTS = {
     "ke_node_devices_delete": (C.c_int, [C.c_void_p, i32]),
     "ke_node_numa_set": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p]),
     "ke_node_resources_set": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p]),
+    "ke_quantity_parse": (C.c_int, [C.c_char_p, C.POINTER(i64), C.POINTER(i64)]),
+    "ke_pod_key": (i64, [C.c_char_p, C.c_char_p]),
+    "ke_decode_node": (C.c_int, [C.c_char_p, i64, C.POINTER(Node)]),
+    "ke_decode_node_metric": (C.c_int, [C.c_char_p, i64, C.POINTER(NodeMetric), i32, C.c_void_p, C.POINTER(i32), i32,
+                                        C.c_void_p, C.POINTER(i32)]),
+    "ke_decode_pod": (C.c_int, [C.c_char_p, i64, i32, C.c_void_p, C.POINTER(Pod)]),
+    "ke_decode_device": (C.c_int, [C.c_char_p, i64, i32, C.c_void_p, C.POINTER(i32), i32, C.c_void_p, C.POINTER(i32),
+                                   C.POINTER(i32), C.POINTER(i32)]),
     "ke_node_resources_get": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p, C.POINTER(i32)]),
     "ke_last_device_allocations": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_last_numa_allocations": (C.c_int, [C.c_void_p, i32, C.c_void_p]),

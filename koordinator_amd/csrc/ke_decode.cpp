@@ -1,0 +1,812 @@
+// ke_decode.cpp — SURVEY.md §8f rank 1: the informer objects' wire format (the JSON the apiserver serves) to
+// the boundary structs, as the reference's listers and apis/extension helpers read them per call.  Host-only
+// C++; a Go caller would instead fill the structs from its typed objects.
+//
+//   ke_decode_node         Node: status.allocatable, the raw-allocatable / amplification-ratio / usage-thresholds
+//                          annotations (apis/extension/node_resource_amplification.go:45-124, load_aware.go:42-72)
+//                          and the NUMA / CPU bind / NUMA allocate labels (numa_aware.go:54-59,354-369;
+//                          nodenumaresource/util.go:41-47)
+//   ke_decode_node_metric  NodeMetric CRD (apis/slo/v1alpha1/nodemetric_types.go:38-136)
+//   ke_decode_pod          Pod: resourceapi.PodRequests / PodLimits (k8s v1.28), priority / QoS classes
+//                          (apis/extension/priority_utils.go:37-58, qos_utils.go:32-68), the LoadAware estimation
+//                          annotations (load_aware.go:75-100), conditions (loadaware/pod_assign_cache.go:89-124,
+//                          load_aware.go:360-385), ResourceSpec / NUMATopologySpec (numa_aware.go:62-80,217-243),
+//                          the DeviceShare annotations (device_share.go:32-40) and the FitPlus / SRA request names
+//   ke_decode_device       Device CRD (apis/scheduling/v1alpha1/device_types.go:32-67) as nodeDeviceCache builds
+//                          it (deviceshare/device_cache.go:518-568), plus its GPU partition table and policy
+//                          (device_share.go:196-226,355-380)
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/koord_eval.h"
+#include "ke_host.h"
+#include "ke_json.h"
+
+using namespace ke;
+using json::Value;
+
+namespace {
+
+int bad(const std::string& m) { return fail(KE_ERR_INVALID, m); }
+int unsup(const std::string& m) { return fail(KE_ERR_UNSUPPORTED, m); }
+
+int parse_doc(const char* js, int64_t len, Value& v, const char* what) {
+  if (!js || len < 0) return bad(std::string(what) + ": null input");
+  std::string err;
+  if (!json::parse(js, (size_t)len, v, err)) return bad(std::string(what) + ": malformed JSON: " + err);
+  if (!v.is_obj()) return bad(std::string(what) + ": not a JSON object");
+  return KE_OK;
+}
+
+// map[string]string (labels / annotations): a non-string value is a malformed object
+int string_map(const Value* m, std::map<std::string, std::string>& out, const char* what) {
+  out.clear();
+  if (!m || m->is_null()) return KE_OK;
+  if (!m->is_obj()) return bad(std::string(what) + " is not an object");
+  for (const auto& kv : m->o) {
+    if (kv.second.t != Value::STR) return bad(std::string(what) + " value is not a string");
+    out[kv.first] = kv.second.s;
+  }
+  return KE_OK;
+}
+
+const std::string* lookup(const std::map<std::string, std::string>& m, const char* k) {
+  auto it = m.find(k);
+  return it == m.end() ? nullptr : &it->second;
+}
+
+// corev1.ResourceList: name -> exact quantity (nanos); false on a malformed list / quantity
+struct RL {
+  std::map<std::string, __int128> q;
+  bool overflow = false;
+};
+bool resource_list(const Value* v, RL& out) {
+  out.q.clear();
+  out.overflow = false;
+  if (!v || v->is_null()) return true;
+  if (!v->is_obj()) return false;
+  for (const auto& kv : v->o) {
+    __int128 n;
+    bool ov;
+    if (!quantity_json_nanos(kv.second, &n, &ov)) {
+      out.overflow |= ov;
+      return false;
+    }
+    out.q[kv.first] = n;
+  }
+  return true;
+}
+// getResourceValue (loadaware/helper.go:147-152): cpu MilliValue, everything else Value
+bool rl_value(const RL& rl, const std::string& name, int64_t* out) {
+  auto it = rl.q.find(name);
+  if (it == rl.q.end()) return false;
+  int64_t v, m;
+  if (!nanos_value(it->second, &v, &m)) return false;
+  *out = name == "cpu" ? m : v;
+  return true;
+}
+
+// map[ResourceName]int64 of cpu / memory (thresholds, scaling factors); other keys -> *other
+bool int_map(const Value* v, int64_t (&out)[KE_NRES], bool* other, size_t* n_keys) {
+  out[0] = out[1] = KE_ABSENT;
+  *other = false;
+  if (n_keys) *n_keys = 0;
+  if (!v || v->is_null()) return true;
+  if (!v->is_obj()) return false;
+  bool ok = true;
+  std::map<std::string, int64_t> m;
+  for (const auto& kv : v->o) {
+    int64_t x;
+    if (!json::as_int64(kv.second, &x)) ok = false;
+    else m[kv.first] = x;
+  }
+  if (!ok) return false;
+  for (const auto& kv : m) {
+    if (kv.first == "cpu") out[0] = kv.second;
+    else if (kv.first == "memory") out[1] = kv.second;
+    else *other = true;
+  }
+  if (n_keys) *n_keys = m.size();
+  return true;
+}
+
+const char* str_or_empty(const Value* v) { return v && v->t == Value::STR ? v->s.c_str() : ""; }
+
+int agg_type(const std::string& s, int32_t* out) {
+  static const char* names[] = {"", "avg", "p50", "p90", "p95", "p99"};
+  for (int i = 0; i < KE_AGG_TYPES; i++)
+    if (s == names[i]) {
+      *out = i;
+      return KE_OK;
+    }
+  return unsup("aggregation type \"" + s + "\" outside avg/p50/p90/p95/p99");
+}
+
+uint64_t fnv1a(const std::string& s) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+  return h;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ke_quantity_parse(const char* s, int64_t* value, int64_t* milli_value) {
+  if (!s || !value || !milli_value) return bad("ke_quantity_parse arguments");
+  bool ov;
+  if (!parse_quantity(s, value, milli_value, &ov))
+    return ov ? unsup(std::string("quantity out of the int64 range: ") + s) : bad(std::string("malformed quantity: ") + s);
+  return KE_OK;
+}
+
+int64_t ke_pod_key(const char* ns, const char* name) {
+  return (int64_t)(fnv1a(std::string(ns ? ns : "") + "/" + (name ? name : "")) & (uint64_t)INT64_MAX);
+}
+
+int ke_decode_node(const char* js, int64_t len, ke_node* out) {
+  if (!out) return bad("ke_decode_node: null output");
+  Value doc;
+  int rc = parse_doc(js, len, doc, "Node");
+  if (rc) return rc;
+  ke_node n{};
+  n.raw_allocatable[0] = n.raw_allocatable[1] = KE_ABSENT;
+  for (int r = 0; r < KE_NRES; r++)
+    n.custom_usage_thresholds[r] = n.custom_prod_usage_thresholds[r] = n.custom_agg_thresholds[r] = KE_ABSENT;
+  n.cpu_amplification_ratio = -1.0;
+  n.nrt_cpu_amplification_ratio = -2.0;  // no NodeResourceTopology in this object
+  const Value* meta = doc.field("metadata");
+  const Value* status = doc.field("status");
+  std::map<std::string, std::string> ann, lab;
+  if ((rc = string_map(meta ? meta->field("annotations") : nullptr, ann, "metadata.annotations"))) return rc;
+  if ((rc = string_map(meta ? meta->field("labels") : nullptr, lab, "metadata.labels"))) return rc;
+  RL alloc;
+  if (!resource_list(status ? status->field("allocatable") : nullptr, alloc))
+    return alloc.overflow ? unsup("Node allocatable out of range") : bad("Node status.allocatable");
+  rl_value(alloc, "cpu", &n.allocatable[0]);
+  rl_value(alloc, "memory", &n.allocatable[1]);
+  // raw allocatable (EstimateNode, default_estimator.go:124-143): an unmarshal error falls back to Allocatable
+  if (const std::string* s = lookup(ann, "node.koordinator.sh/raw-allocatable")) {
+    Value v;
+    std::string err;
+    RL raw;
+    if (json::parse(s->data(), s->size(), v, err) && resource_list(&v, raw)) {
+      int64_t x;
+      if (rl_value(raw, "cpu", &x)) n.raw_allocatable[0] = x;
+      if (rl_value(raw, "memory", &x)) n.raw_allocatable[1] = x;
+    }
+  }
+  // GetNodeResourceAmplificationRatio(annotations, cpu): -1 when unset, an error when unparsable
+  if (const std::string* s = lookup(ann, "node.koordinator.sh/resource-amplification-ratio")) {
+    Value v;
+    std::string err;
+    bool ok = json::parse(s->data(), s->size(), v, err) && (v.is_null() || v.is_obj());
+    double cpu = -1.0;
+    if (ok && v.is_obj())
+      for (const auto& kv : v.o) {
+        double d;
+        if (!json::as_float64(kv.second, &d)) ok = false;
+        else if (kv.first == "cpu") cpu = d;
+      }
+    if (ok) n.cpu_amplification_ratio = cpu;
+    else n.amplification_error = 1;
+  }
+  // CustomUsageThresholds (GetCustomUsageThresholds): present + valid, or present + unmarshal error
+  if (const std::string* s = lookup(ann, "scheduling.koordinator.sh/usage-thresholds")) {
+    Value v;
+    std::string err;
+    bool ok = json::parse(s->data(), s->size(), v, err) && (v.is_null() || v.is_obj());
+    bool other = false, o2;
+    int64_t u[KE_NRES], pu[KE_NRES], au[KE_NRES];
+    u[0] = u[1] = pu[0] = pu[1] = au[0] = au[1] = KE_ABSENT;
+    bool has_agg = false;
+    int32_t atype = KE_AGG_NONE;
+    int64_t adur = 0;
+    if (ok && v.is_obj()) {
+      ok = int_map(v.field("usageThresholds"), u, &o2, nullptr);
+      other |= o2;
+      ok = int_map(v.field("prodUsageThresholds"), pu, &o2, nullptr) && ok;
+      other |= o2;
+      const Value* ag = v.field("aggregatedUsage");
+      if (ag && !ag->is_null()) {
+        if (!ag->is_obj()) {
+          ok = false;
+        } else {
+          has_agg = true;
+          ok = int_map(ag->field("usageThresholds"), au, &o2, nullptr) && ok;
+          other |= o2;
+          const Value* t = ag->field("usageAggregationType");
+          if (t && !t->is_null()) {
+            if (t->t != Value::STR) ok = false;
+            else if ((rc = agg_type(t->s, &atype))) return rc;
+          }
+          const Value* d = ag->field("usageAggregatedDuration");
+          if (d && !d->is_null() && (d->t != Value::STR || !parse_duration(d->s, &adur))) ok = false;
+        }
+      }
+    }
+    if (!ok) {
+      n.custom_thresholds_error = 1;
+    } else {
+      if (other) return unsup("usage-thresholds annotation with resources other than cpu/memory");
+      n.has_custom_thresholds = 1;
+      for (int r = 0; r < KE_NRES; r++) {
+        n.custom_usage_thresholds[r] = u[r];
+        n.custom_prod_usage_thresholds[r] = pu[r];
+        n.custom_agg_thresholds[r] = au[r];
+      }
+      n.has_custom_agg = has_agg;
+      n.custom_agg_type = atype;
+      n.custom_agg_duration_ns = adur;
+    }
+  }
+  // labels
+  if (const std::string* s = lookup(lab, "node.koordinator.sh/numa-topology-policy")) {
+    if (*s == "") n.numa_topology_policy = KE_NUMA_POLICY_NONE;
+    else if (*s == "BestEffort") n.numa_topology_policy = KE_NUMA_POLICY_BEST_EFFORT;
+    else if (*s == "Restricted") n.numa_topology_policy = KE_NUMA_POLICY_RESTRICTED;
+    else if (*s == "SingleNUMANode") n.numa_topology_policy = KE_NUMA_POLICY_SINGLE_NUMA_NODE;
+    else return unsup("NUMA topology policy label \"" + *s + "\"");
+  }
+  if (const std::string* s = lookup(lab, "node.koordinator.sh/cpu-bind-policy")) {
+    if (*s == "FullPCPUsOnly") n.cpu_bind_policy = KE_NODE_CPU_BIND_FULL_PCPUS_ONLY;
+    else if (*s == "SpreadByPCPUs") n.cpu_bind_policy = KE_NODE_CPU_BIND_SPREAD_BY_PCPUS;
+  }
+  if (const std::string* s = lookup(lab, "node.koordinator.sh/numa-allocate-strategy")) {
+    if (*s == "MostAllocated") n.numa_allocate_strategy = KE_NUMA_ALLOCATE_MOST;
+    else if (*s == "LeastAllocated") n.numa_allocate_strategy = KE_NUMA_ALLOCATE_LEAST;
+    else if (*s != "") return unsup("NUMA allocate strategy label \"" + *s + "\"");
+  }
+  *out = n;
+  return KE_OK;
+}
+
+// slo/v1alpha1 ResourceMap {resources: ResourceList} -> ke_resource_map (len() of the list kept)
+static bool resource_map(const Value* rm, ke_resource_map* out) {
+  std::memset(out, 0, sizeof *out);
+  if (!rm || rm->is_null()) return true;
+  if (!rm->is_obj()) return false;
+  RL rl;
+  if (!resource_list(rm->field("resources"), rl)) return false;
+  for (int r = 0; r < KE_NRES; r++) {
+    int64_t x;
+    if (rl_value(rl, r == 0 ? "cpu" : "memory", &x)) out->value[r] = x, out->present[r] = 1;
+  }
+  out->n_keys = (int32_t)rl.q.size();
+  return true;
+}
+
+int ke_decode_node_metric(const char* js, int64_t len, ke_node_metric* nm, int32_t pm_cap, ke_pod_metric* pm,
+                          int32_t* n_pm, int32_t agg_cap, ke_aggregated_usage* agg, int32_t* n_agg) {
+  if (!nm || !n_pm || !n_agg || pm_cap < 0 || agg_cap < 0 || (pm_cap && !pm) || (agg_cap && !agg))
+    return bad("ke_decode_node_metric arguments");
+  Value doc;
+  int rc = parse_doc(js, len, doc, "NodeMetric");
+  if (rc) return rc;
+  ke_node_metric h{};
+  h.report_interval_seconds = KE_ABSENT;
+  const Value* spec = doc.field("spec");
+  const Value* cp = spec ? spec->field("metricCollectPolicy") : nullptr;
+  const Value* ri = cp ? cp->field("reportIntervalSeconds") : nullptr;
+  if (ri && !ri->is_null() && !json::as_int64(*ri, &h.report_interval_seconds)) return bad("reportIntervalSeconds");
+  const Value* st = doc.field("status");
+  const Value* ut = st ? st->field("updateTime") : nullptr;
+  if (ut && !ut->is_null()) {
+    if (ut->t != Value::STR || !parse_rfc3339(ut->s, &h.update_time_ns)) return bad("status.updateTime");
+    h.has_update_time = 1;
+  }
+  const Value* info = st ? st->field("nodeMetric") : nullptr;
+  *n_pm = *n_agg = 0;
+  if (info && !info->is_null()) {
+    h.has_node_metric = 1;
+    if (!resource_map(info->field("nodeUsage"), &h.node_usage)) return bad("nodeMetric.nodeUsage");
+    const Value* aggs = info->field("aggregatedNodeUsages");
+    if (aggs && !aggs->is_null()) {
+      if (aggs->t != Value::ARR) return bad("aggregatedNodeUsages");
+      if ((int64_t)aggs->a.size() > agg_cap) return bad("aggregatedNodeUsages: more entries than agg_cap");
+      for (const Value& a : aggs->a) {
+        ke_aggregated_usage u{};
+        const Value* d = a.field("duration");
+        if (d && !d->is_null() && (d->t != Value::STR || !parse_duration(d->s, &u.duration_ns))) return bad("duration");
+        const Value* usage = a.field("usage");
+        if (usage && !usage->is_null()) {
+          if (!usage->is_obj()) return bad("aggregated usage");
+          for (const auto& kv : usage->o) {
+            int32_t t;
+            if ((rc = agg_type(kv.first, &t))) return rc;
+            if (!resource_map(&kv.second, &u.usage[t])) return bad("aggregated usage resources");
+          }
+        }
+        agg[(*n_agg)++] = u;
+      }
+    }
+  }
+  const Value* pods = st ? st->field("podsMetric") : nullptr;
+  if (pods && !pods->is_null()) {
+    if (pods->t != Value::ARR) return bad("podsMetric");
+    if ((int64_t)pods->a.size() > pm_cap) return bad("podsMetric: more entries than pm_cap");
+    for (const Value& p : pods->a) {
+      if (p.is_null()) continue;  // []*PodMetricInfo: a nil entry
+      ke_pod_metric m{};
+      m.pod_key = ke_pod_key(str_or_empty(p.field("namespace")), str_or_empty(p.field("name")));
+      const std::string pr = str_or_empty(p.field("priority"));
+      m.priority_class = pr == "koord-prod"    ? KE_PRIORITY_PROD
+                         : pr == "koord-mid"   ? KE_PRIORITY_MID
+                         : pr == "koord-batch" ? KE_PRIORITY_BATCH
+                         : pr == "koord-free"  ? KE_PRIORITY_FREE
+                                               : KE_PRIORITY_NONE;
+      if (!resource_map(p.field("podUsage"), &m.usage)) return bad("podUsage");
+      pm[(*n_pm)++] = m;
+    }
+  }
+  *nm = h;
+  return KE_OK;
+}
+
+}  // extern "C"
+
+// ---- Pod ---------------------------------------------------------------------------------------------------
+namespace {
+const char* const KE_RES_NAMES[KE_RES_COUNT] = {"cpu", "memory", "kubernetes.io/batch-cpu", "kubernetes.io/batch-memory",
+                                                "kubernetes.io/mid-cpu", "kubernetes.io/mid-memory"};
+const char* const PDR_NAMES[KE_PDR_COUNT] = {"nvidia.com/gpu", "amd.com/gpu", "koordinator.sh/gpu",
+                                             "koordinator.sh/gpu.shared", "koordinator.sh/gpu-core",
+                                             "koordinator.sh/gpu-memory", "koordinator.sh/gpu-memory-ratio",
+                                             "koordinator.sh/rdma", "koordinator.sh/fpga"};
+const char* const UNSUPPORTED_DEVICE[] = {"huawei.com/npu-core", "huawei.com/npu-cpu", "huawei.com/npu-dvpp",
+                                          "dcu.com/gpu"};
+
+struct Container {
+  RL req, lim;
+};
+
+int containers(const Value* arr, std::vector<Container>& out, const char* what) {
+  out.clear();
+  if (!arr || arr->is_null()) return KE_OK;
+  if (arr->t != Value::ARR) return bad(std::string(what) + " is not an array");
+  for (const Value& c : arr->a) {
+    Container k;
+    const Value* res = c.field("resources");
+    if (!resource_list(res ? res->field("requests") : nullptr, k.req) ||
+        !resource_list(res ? res->field("limits") : nullptr, k.lim))
+      return k.req.overflow || k.lim.overflow ? unsup(std::string(what) + " quantity out of range")
+                                              : bad(std::string(what) + " resources");
+    const Value* rp = c.field("restartPolicy");
+    if (rp && rp->t == Value::STR && rp->s == "Always")
+      return unsup("restartable init containers (sidecars) in PodRequests are not modelled");
+    out.push_back(std::move(k));
+  }
+  return KE_OK;
+}
+
+// resourceapi.PodRequests / PodLimits (k8s v1.28): Σ containers, max with each init container, + overhead
+// (PodLimits adds the overhead only to the resources that already have a limit)
+std::map<std::string, __int128> pod_total(const std::vector<Container>& cs, const std::vector<Container>& ics,
+                                          const RL& overhead, bool limits) {
+  std::map<std::string, __int128> t;
+  for (const Container& c : cs)
+    for (const auto& kv : (limits ? c.lim : c.req).q) t[kv.first] += kv.second;
+  for (const Container& c : ics)
+    for (const auto& kv : (limits ? c.lim : c.req).q) t[kv.first] = std::max(t[kv.first], kv.second);
+  for (const auto& kv : overhead.q)
+    if (!limits || t.count(kv.first)) t[kv.first] += kv.second;
+  return t;
+}
+
+bool total_value(const std::map<std::string, __int128>& t, const std::string& name, int64_t* out) {
+  auto it = t.find(name);
+  if (it == t.end()) return false;
+  int64_t v, m;
+  if (!nanos_value(it->second, &v, &m)) return false;
+  *out = name == "cpu" ? m : v;
+  return true;
+}
+
+// k8s GetPodQOS (pkg/apis/core/v1/helper/qos, v1.28) over cpu / memory of containers + init containers
+int kube_qos(const std::vector<Container>& cs, const std::vector<Container>& ics) {  // 0 Guaranteed 1 Burstable 2 BE
+  std::map<std::string, __int128> req, lim;
+  bool guaranteed = true;
+  auto scan = [&](const Container& c) {
+    for (const auto& kv : c.req.q)
+      if ((kv.first == "cpu" || kv.first == "memory") && kv.second != 0) req[kv.first] += kv.second;
+    int found = 0;
+    for (const auto& kv : c.lim.q)
+      if ((kv.first == "cpu" || kv.first == "memory") && kv.second != 0) lim[kv.first] += kv.second, found++;
+    if (found < 2) guaranteed = false;
+  };
+  for (const Container& c : cs) scan(c);
+  for (const Container& c : ics) scan(c);
+  if (req.empty() && lim.empty()) return 2;
+  if (guaranteed)
+    for (const auto& kv : req)
+      if (!lim.count(kv.first) || lim[kv.first] != kv.second) guaranteed = false;
+  return guaranteed && req.size() == lim.size() ? 0 : 1;
+}
+
+int cpu_bind(const Value* v, int32_t* out) {
+  const std::string s = str_or_empty(v);
+  if (s == "") *out = KE_CPU_BIND_UNSET;
+  else if (s == "Default") *out = KE_CPU_BIND_DEFAULT;
+  else if (s == "FullPCPUs") *out = KE_CPU_BIND_FULL_PCPUS;
+  else if (s == "SpreadByPCPUs") *out = KE_CPU_BIND_SPREAD_BY_PCPUS;
+  else if (s == "ConstrainedBurst") *out = KE_CPU_BIND_CONSTRAINED_BURST;
+  else return unsup("CPU bind policy \"" + s + "\"");
+  return KE_OK;
+}
+
+// time of the first condition of `type` with status True (podutil.GetPodCondition); false if none / zero time
+bool condition_time(const Value* conds, const char* type, int64_t* ns, int* rc) {
+  *rc = KE_OK;
+  if (!conds || conds->t != Value::ARR) return false;
+  for (const Value& c : conds->a) {
+    if (std::string(str_or_empty(c.field("type"))) != type) continue;
+    if (std::string(str_or_empty(c.field("status"))) != "True") return false;
+    const Value* t = c.field("lastTransitionTime");
+    if (!t || t->is_null()) return false;
+    if (t->t != Value::STR || !parse_rfc3339(t->s, ns)) {
+      *rc = bad(std::string(type) + " lastTransitionTime");
+      return false;
+    }
+    return true;
+  }
+  return false;
+}
+}  // namespace
+
+extern "C" {
+
+int ke_decode_pod(const char* js, int64_t len, int32_t n_names, const char* const* xres_names, ke_pod* out) {
+  if (!out || n_names < 0 || n_names > KE_MAX_XRES || (n_names && !xres_names)) return bad("ke_decode_pod arguments");
+  Value doc;
+  int rc = parse_doc(js, len, doc, "Pod");
+  if (rc) return rc;
+  ke_pod p{};
+  const Value* meta = doc.field("metadata");
+  const Value* spec = doc.field("spec");
+  const Value* status = doc.field("status");
+  std::map<std::string, std::string> ann, lab;
+  if ((rc = string_map(meta ? meta->field("annotations") : nullptr, ann, "metadata.annotations"))) return rc;
+  if ((rc = string_map(meta ? meta->field("labels") : nullptr, lab, "metadata.labels"))) return rc;
+  const std::string ns = str_or_empty(meta ? meta->field("namespace") : nullptr),
+                    name = str_or_empty(meta ? meta->field("name") : nullptr),
+                    uid = str_or_empty(meta ? meta->field("uid") : nullptr);
+  p.pod_key = ke_pod_key(ns.c_str(), name.c_str());
+  p.uid = uid.empty() ? p.pod_key : (int64_t)(fnv1a(uid) & (uint64_t)INT64_MAX);
+  // requests / limits
+  std::vector<Container> cs, ics;
+  if ((rc = containers(spec ? spec->field("containers") : nullptr, cs, "spec.containers"))) return rc;
+  if ((rc = containers(spec ? spec->field("initContainers") : nullptr, ics, "spec.initContainers"))) return rc;
+  RL overhead;
+  if (!resource_list(spec ? spec->field("overhead") : nullptr, overhead)) return bad("spec.overhead");
+  const auto reqs = pod_total(cs, ics, overhead, false), lims = pod_total(cs, ics, overhead, true);
+  for (int r = 0; r < KE_RES_COUNT; r++) {
+    if (reqs.count(KE_RES_NAMES[r]) && !total_value(reqs, KE_RES_NAMES[r], &p.requests[r]))
+      return unsup("pod request out of range");
+    if (lims.count(KE_RES_NAMES[r]) && !total_value(lims, KE_RES_NAMES[r], &p.limits[r]))
+      return unsup("pod limit out of range");
+  }
+  for (const auto& kv : reqs) {
+    if (kv.second == 0) continue;
+    bool known = false;
+    for (const char* n : KE_RES_NAMES) known |= kv.first == n;
+    if (!known) p.has_other_requests = 1;
+    for (int d = 0; d < KE_PDR_COUNT; d++)
+      if (kv.first == PDR_NAMES[d] && !total_value(reqs, kv.first, &p.device_requests[d]))
+        return unsup("device request out of range");
+    for (const char* u : UNSUPPORTED_DEVICE)
+      if (kv.first == u) p.has_unsupported_device_requests = 1;
+  }
+  // NodeResourcesFitPlus / ScarceResourceAvoidance: requested names (> 0) and calculatePodResourceRequest
+  p.xres_request_mask = 0;
+  for (int32_t id = 0; id < n_names; id++) {
+    const std::string nm = xres_names[id] ? xres_names[id] : "";
+    auto it = reqs.find(nm);
+    if (it == reqs.end() || it->second <= 0) continue;
+    p.xres_request_mask |= 1ull << id;
+    if (p.n_xres >= KE_MAX_POD_XRES) return unsup("more than 8 requested resource names");
+    // GetNonzeroRequestForResource per container (100m cpu / 200Mi memory when the key is missing)
+    auto nz = [&](const Container& c) -> __int128 {
+      auto f = c.req.q.find(nm);
+      if (f != c.req.q.end()) return f->second;
+      if (nm == "cpu") return (__int128)100 * 1000000;                    // 100m in nanos
+      if (nm == "memory") return (__int128)200 * 1048576 * 1000000000;    // 200Mi in nanos
+      return 0;
+    };
+    __int128 s = 0;
+    for (const Container& c : cs) s += nz(c);
+    for (const Container& c : ics) s = std::max(s, nz(c));
+    int64_t v, m;
+    if (!nanos_value(s, &v, &m)) return unsup("pod request out of range");
+    p.xres_id[p.n_xres] = id;
+    p.xres_value[p.n_xres++] = nm == "cpu" ? m : v;
+  }
+  // classes (GetPodPriorityClassWithDefault, GetPodQoSClassRaw)
+  static const char* QOS[] = {"", "LSE", "LSR", "LS", "BE", "SYSTEM"};
+  if (const std::string* q = lookup(lab, "koordinator.sh/qosClass"))
+    for (int i = 1; i < 6; i++)
+      if (*q == QOS[i]) p.qos_class = i;
+  int pc = KE_PRIORITY_NONE;
+  if (const std::string* s = lookup(lab, "koordinator.sh/priority-class")) {
+    pc = *s == "koord-prod" ? KE_PRIORITY_PROD : *s == "koord-mid" ? KE_PRIORITY_MID : *s == "koord-batch" ? KE_PRIORITY_BATCH
+         : *s == "koord-free" ? KE_PRIORITY_FREE : KE_PRIORITY_NONE;
+  } else if (const Value* pr = spec ? spec->field("priority") : nullptr; pr && !pr->is_null()) {
+    int64_t v;
+    if (!json::as_int64(*pr, &v)) return bad("spec.priority");
+    pc = (v >= 9000 && v <= 9999) ? KE_PRIORITY_PROD : (v >= 7000 && v <= 7999) ? KE_PRIORITY_MID
+         : (v >= 5000 && v <= 5999) ? KE_PRIORITY_BATCH : (v >= 3000 && v <= 3999) ? KE_PRIORITY_FREE : KE_PRIORITY_NONE;
+  }
+  if (pc == KE_PRIORITY_NONE) {  // GetPodQoSClassWithKubeQoS -> priority by QoS
+    int q = p.qos_class;
+    static const int BY_KUBE_QOS[3] = {KE_QOS_LSR, KE_QOS_LS, KE_QOS_BE};  // Guaranteed / Burstable / BestEffort
+    if (q == KE_QOS_NONE) q = BY_KUBE_QOS[kube_qos(cs, ics)];
+    pc = (q == KE_QOS_SYSTEM || q == KE_QOS_LSE || q == KE_QOS_LSR || q == KE_QOS_LS) ? KE_PRIORITY_PROD
+         : q == KE_QOS_BE ? KE_PRIORITY_BATCH : KE_PRIORITY_NONE;
+  }
+  p.priority_class = pc;
+  // owner, phase, conditions
+  const Value* owners = meta ? meta->field("ownerReferences") : nullptr;
+  if (owners && owners->t == Value::ARR)
+    for (const Value& o : owners->a)
+      if (std::string(str_or_empty(o.field("kind"))) == "DaemonSet") p.is_daemonset = 1;
+  const std::string phase = str_or_empty(status ? status->field("phase") : nullptr);
+  p.is_terminated = phase == "Succeeded" || phase == "Failed";
+  const Value* conds = status ? status->field("conditions") : nullptr;
+  p.has_scheduled = condition_time(conds, "PodScheduled", &p.scheduled_transition_ns, &rc);
+  if (rc) return rc;
+  p.has_initialized = condition_time(conds, "Initialized", &p.initialized_transition_ns, &rc);
+  if (rc) return rc;
+  // LoadAware estimation annotations (load_aware.go:75-100)
+  p.custom_scaling_factors[0] = p.custom_scaling_factors[1] = KE_ABSENT;
+  if (const std::string* s = lookup(ann, "scheduling.koordinator.sh/load-estimated-scaling-factors"); s && !s->empty()) {
+    Value v;
+    std::string err;
+    int64_t f[KE_NRES];
+    bool other;
+    size_t nk = 0;
+    if (json::parse(s->data(), s->size(), v, err) && int_map(&v, f, &other, &nk) && nk > 0) {
+      p.has_custom_scaling_factors = 1;
+      p.custom_scaling_factors[0] = f[0];
+      p.custom_scaling_factors[1] = f[1];
+    }
+  }
+  p.custom_seconds_after_scheduled = p.custom_seconds_after_initialized = KE_ABSENT;
+  if (const std::string* s = lookup(ann, "scheduling.koordinator.sh/load-estimated-seconds-after-pod-scheduled"))
+    if (!parse_int64(*s, &p.custom_seconds_after_scheduled)) p.custom_seconds_after_scheduled = KE_ABSENT;
+  if (const std::string* s = lookup(ann, "scheduling.koordinator.sh/load-estimated-seconds-after-initialized"))
+    if (!parse_int64(*s, &p.custom_seconds_after_initialized)) p.custom_seconds_after_initialized = KE_ABSENT;
+  // ResourceSpec (an unmarshal error is PreFilter's error: has_resource_spec)
+  if (const std::string* s = lookup(ann, "scheduling.koordinator.sh/resource-spec")) {
+    Value v;
+    std::string err;
+    const bool ok = json::parse(s->data(), s->size(), v, err) && (v.is_null() || v.is_obj());
+    const Value *rq = ok ? v.field("requiredCPUBindPolicy") : nullptr, *pf = ok ? v.field("preferredCPUBindPolicy") : nullptr,
+                *ex = ok ? v.field("preferredCPUExclusivePolicy") : nullptr;
+    auto strish = [](const Value* x) { return !x || x->is_null() || x->t == Value::STR; };
+    if (!ok || !strish(rq) || !strish(pf) || !strish(ex)) {
+      p.has_resource_spec = 1;
+    } else {
+      if ((rc = cpu_bind(rq, &p.cpu_bind_required)) || (rc = cpu_bind(pf, &p.cpu_bind_preferred))) return rc;
+      const std::string e = str_or_empty(ex);
+      if (e == "" || e == "None") p.cpu_exclusive = KE_CPU_EXCL_NONE;
+      else if (e == "PCPULevel") p.cpu_exclusive = KE_CPU_EXCL_PCPU_LEVEL;
+      else if (e == "NUMANodeLevel") p.cpu_exclusive = KE_CPU_EXCL_NUMA_NODE_LEVEL;
+      else return unsup("CPU exclusive policy \"" + e + "\"");
+    }
+  }
+  if (const std::string* s = lookup(ann, "scheduling.koordinator.sh/numa-topology-spec")) {
+    Value v;
+    std::string err;
+    if (!json::parse(s->data(), s->size(), v, err) || !(v.is_null() || v.is_obj()))
+      return unsup("numa-topology-spec annotation that fails to unmarshal");
+    const std::string pol = str_or_empty(v.field("numaTopologyPolicy")), ex = str_or_empty(v.field("singleNUMANodeExclusive"));
+    if (pol == "") p.numa_topology_policy = KE_NUMA_POLICY_NONE;
+    else if (pol == "BestEffort") p.numa_topology_policy = KE_NUMA_POLICY_BEST_EFFORT;
+    else if (pol == "Restricted") p.numa_topology_policy = KE_NUMA_POLICY_RESTRICTED;
+    else if (pol == "SingleNUMANode") p.numa_topology_policy = KE_NUMA_POLICY_SINGLE_NUMA_NODE;
+    else return unsup("NUMA topology policy \"" + pol + "\"");
+    if (ex == "") p.numa_exclusive = KE_NUMA_EXCLUSIVE_NONE;
+    else if (ex == "Preferred") p.numa_exclusive = KE_NUMA_EXCLUSIVE_PREFERRED;
+    else if (ex == "Required") p.numa_exclusive = KE_NUMA_EXCLUSIVE_REQUIRED;
+    else return unsup("SingleNUMANodeExclusive \"" + ex + "\"");
+  }
+  // ElasticQuota: the quota name -> index mapping is the caller's (ke_quotas_load order); preemptible label
+  const std::string* pre = lookup(lab, "quota.scheduling.koordinator.sh/preemptible");
+  p.quota_non_preemptible = pre && *pre == "false";
+  // DeviceShare annotations (utils.go:355-513)
+  p.gpu_ring_bus_bandwidth = KE_ABSENT;
+  if (const std::string* s = lookup(ann, "scheduling.koordinator.sh/gpu-partition-spec")) {
+    Value v;
+    std::string err;
+    if (!json::parse(s->data(), s->size(), v, err) || !(v.is_null() || v.is_obj()))
+      return unsup("gpu-partition-spec annotation that fails to unmarshal");
+    p.gpu_partition_spec = 1;
+    p.gpu_partition_restricted = std::string(str_or_empty(v.field("allocatePolicy"))) == "Restricted";
+    const Value* bw = v.field("ringBusBandwidth");
+    if (bw && !bw->is_null()) {
+      int64_t val, milli;
+      bool ov;
+      if (!quantity_json(*bw, &val, &milli, &ov)) return unsup("ringBusBandwidth");
+      p.gpu_ring_bus_bandwidth = val;
+    }
+  }
+  if (const std::string* s = lookup(ann, "scheduling.koordinator.sh/device-allocate-hint")) {
+    Value v;
+    std::string err;
+    if (!json::parse(s->data(), s->size(), v, err) || !(v.is_null() || v.is_obj()))
+      return unsup("device-allocate-hint annotation that fails to unmarshal");
+    uint8_t bits = 0;
+    if (v.is_obj())
+      for (const auto& kv : v.o) {
+        const Value& h = kv.second;
+        if (!h.is_obj()) continue;
+        auto set = [&](const char* f) { const Value* x = h.field(f); return x && !x->is_null(); };
+        if (set("selector")) bits |= KE_DHINT_SELECTOR;
+        if (set("vfSelector")) bits |= KE_DHINT_VF;
+        if (*str_or_empty(h.field("allocateStrategy"))) bits |= KE_DHINT_STRATEGY;
+        if (*str_or_empty(h.field("exclusivePolicy"))) bits |= KE_DHINT_EXCLUSIVE;
+        const std::string sc = str_or_empty(h.field("requiredTopologyScope"));
+        if (kv.first == "gpu" && !sc.empty())
+          p.gpu_required_topology_scope = sc == "Node" ? KE_SCOPE_NODE : sc == "NUMANode" ? KE_SCOPE_NUMA
+                                          : sc == "PCIe" ? KE_SCOPE_PCIE : sc == "Device" ? KE_SCOPE_DEVICE : KE_SCOPE_UNKNOWN;
+      }
+    p.device_hints = bits;
+  }
+  if (const std::string* s = lookup(ann, "scheduling.koordinator.sh/device-joint-allocate")) {
+    Value v, hints;
+    std::string err;
+    if (!json::parse(s->data(), s->size(), v, err) || !(v.is_null() || v.is_obj()))
+      return unsup("device-joint-allocate annotation that fails to unmarshal");
+    const std::string* hs = lookup(ann, "scheduling.koordinator.sh/device-allocate-hint");
+    if (hs) json::parse(hs->data(), hs->size(), hints, err);
+    bool gpu = false;
+    for (int d = 0; d < 7; d++) gpu |= p.device_requests[d] > 0;
+    const Value* types = v.field("deviceTypes");
+    if (types && types->t == Value::ARR)
+      for (const Value& t : types->a) {
+        const std::string ty = t.t == Value::STR ? t.s : "";
+        const bool req = (ty == "gpu" && gpu) || (ty == "rdma" && p.device_requests[KE_PDR_RDMA] > 0) ||
+                         (ty == "fpga" && p.device_requests[KE_PDR_FPGA] > 0);
+        const Value* h = hints.is_obj() ? hints.key(ty.c_str()) : nullptr;
+        const bool apply_all = h && std::string(str_or_empty(h->field("allocateStrategy"))) == "ApplyForAll";
+        if (req && !apply_all) p.device_joint_allocate = 1;
+      }
+  }
+  *out = p;
+  return KE_OK;
+}
+
+// ---- Device ------------------------------------------------------------------------------------------------
+int ke_decode_device(const char* js, int64_t len, int32_t cap, ke_device* out, int32_t* n, int32_t part_cap,
+                     ke_gpu_partition* parts, int32_t* n_parts, int32_t* has_table, int32_t* honor) {
+  if (!n || cap < 0 || (cap && !out) || part_cap < 0 || (part_cap && !parts) || !n_parts || !has_table || !honor)
+    return bad("ke_decode_device arguments");
+  Value doc;
+  int rc = parse_doc(js, len, doc, "Device");
+  if (rc) return rc;
+  const Value* meta = doc.field("metadata");
+  const Value* spec = doc.field("spec");
+  std::map<std::string, std::string> ann, lab;
+  if ((rc = string_map(meta ? meta->field("annotations") : nullptr, ann, "metadata.annotations"))) return rc;
+  if ((rc = string_map(meta ? meta->field("labels") : nullptr, lab, "metadata.labels"))) return rc;
+  const Value* devs = spec ? spec->field("devices") : nullptr;
+  std::vector<ke_device> out_v;
+  std::vector<std::string> pcie;  // per output device: its PCIe id ("" without a topology)
+  if (devs && !devs->is_null()) {
+    if (devs->t != Value::ARR) return bad("spec.devices");
+    for (const Value& d : devs->a) {
+      const std::string type = str_or_empty(d.field("type"));
+      ke_device k{};
+      if (type == "gpu") k.type = KE_DEV_GPU;
+      else if (type == "rdma") k.type = KE_DEV_RDMA;
+      else if (type == "fpga") k.type = KE_DEV_FPGA;
+      else return unsup("device type \"" + type + "\" (not gpu / rdma / fpga)");
+      const Value* mi = d.field("minor");
+      int64_t minor;
+      if (!mi || mi->is_null() || !json::as_int64(*mi, &minor)) return bad("device without a minor");
+      if (minor < 0 || minor >= KE_MAX_MINORS) return unsup("device minor outside 0..15");
+      k.minor = (int32_t)minor;
+      const Value* h = d.field("health");
+      k.health = h && h->t == Value::BOOL && h->b;
+      RL res;
+      if (!resource_list(d.field("resources"), res)) return bad("device resources");
+      if (k.health) {  // buildDeviceResources: an unhealthy device has an empty ResourceList
+        static const char* GPU_KEYS[KE_DKEYS] = {"koordinator.sh/gpu-core", "koordinator.sh/gpu-memory",
+                                                 "koordinator.sh/gpu-memory-ratio"};
+        const char* key0 = k.type == KE_DEV_GPU ? nullptr : (k.type == KE_DEV_RDMA ? "koordinator.sh/rdma" : "koordinator.sh/fpga");
+        for (const auto& kv : res.q) {
+          int slot = -1;
+          if (k.type == KE_DEV_GPU) {
+            for (int s = 0; s < KE_DKEYS; s++)
+              if (kv.first == GPU_KEYS[s]) slot = s;
+          } else if (kv.first == key0) {
+            slot = 0;
+          }
+          if (slot < 0) return unsup("device resource \"" + kv.first + "\" outside the device type's keys");
+          int64_t v, m;
+          if (!nanos_value(kv.second, &v, &m)) return unsup("device resource out of range");
+          k.has_total[slot] = 1;
+          k.total[slot] = v;
+        }
+      }
+      const Value* topo = d.field("topology");
+      std::string pid;
+      if (topo && !topo->is_null()) {
+        int64_t node = 0;
+        const Value* nid = topo->field("nodeID");
+        if (nid && !nid->is_null() && !json::as_int64(*nid, &node)) return bad("topology.nodeID");
+        k.has_topology = 1;
+        k.numa_node = (int32_t)node;
+        pid = str_or_empty(topo->field("pcieID"));
+      }
+      out_v.push_back(k);
+      pcie.push_back(pid);
+    }
+  }
+  // PCIe id rank among the node's distinct ids in Go string order (bytewise)
+  std::vector<std::string> ids;
+  for (size_t i = 0; i < out_v.size(); i++)
+    if (out_v[i].has_topology) ids.push_back(pcie[i]);
+  std::sort(ids.begin(), ids.end());
+  ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+  for (size_t i = 0; i < out_v.size(); i++)
+    if (out_v[i].has_topology)
+      out_v[i].pcie_rank = (int32_t)(std::lower_bound(ids.begin(), ids.end(), pcie[i]) - ids.begin());
+  if ((int64_t)out_v.size() > cap) return bad("more devices than cap");
+  std::copy(out_v.begin(), out_v.end(), out);
+  *n = (int32_t)out_v.size();
+  // GPU partition table (GetGPUPartitionTable) and policy label (GetGPUPartitionPolicy)
+  *n_parts = 0;
+  *has_table = 0;
+  const std::string* pol = lookup(lab, "node.koordinator.sh/gpu-partition-policy");
+  *honor = pol && *pol == "Honor";
+  if (const std::string* s = lookup(ann, "scheduling.koordinator.sh/gpu-partitions"); s && !s->empty()) {
+    Value v;
+    std::string err;
+    if (!json::parse(s->data(), s->size(), v, err) || !(v.is_null() || v.is_obj()))
+      return unsup("gpu-partitions annotation that fails to unmarshal (the cache keeps a nil indexer)");
+    if (v.is_obj()) {
+      *has_table = 1;
+      std::vector<std::pair<int64_t, const Value*>> keys;  // map[int][]GPUPartition: ascending by key
+      for (const auto& kv : v.o) {
+        int64_t k;
+        if (!parse_int64(kv.first, &k)) return unsup("gpu-partitions key");
+        keys.emplace_back(k, &kv.second);
+      }
+      std::stable_sort(keys.begin(), keys.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+      for (const auto& kv : keys) {
+        if (kv.second->t != Value::ARR) return unsup("gpu-partitions entry");
+        for (const Value& g : kv.second->a) {
+          ke_gpu_partition q{};
+          q.number_of_gpus = (int32_t)kv.first;
+          q.ring_bus_bandwidth = KE_ABSENT;
+          const Value* mn = g.field("minors");
+          if (!mn || mn->t != Value::ARR) return unsup("gpu partition without minors");
+          for (const Value& m : mn->a) {
+            int64_t x;
+            if (!json::as_int64(m, &x) || x < 0 || x >= KE_MAX_MINORS) return unsup("gpu partition minor");
+            q.minors |= 1u << x;
+          }
+          int64_t sc = 0;
+          const Value* as = g.field("allocationScore");
+          if (as && !as->is_null() && !json::as_int64(*as, &sc)) return unsup("allocationScore");
+          q.allocation_score = (int32_t)sc;
+          const Value* bw = g.field("ringBusBandwidth");
+          if (bw && !bw->is_null()) {
+            int64_t val, milli;
+            bool ov;
+            if (!quantity_json(*bw, &val, &milli, &ov)) return unsup("ringBusBandwidth");
+            q.ring_bus_bandwidth = val;
+          }
+          if (*n_parts >= part_cap) return bad("more partitions than part_cap");
+          parts[(*n_parts)++] = q;
+        }
+      }
+    }
+  }
+  return KE_OK;
+}
+
+}  // extern "C"

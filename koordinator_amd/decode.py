@@ -1,0 +1,87 @@
+"""Wire-format decoders: Kubernetes objects as the apiserver serves them (JSON) into the
+boundary structs, through the C ABI (ke_decode_* in libkoordeval.so; no Python re-implementation runs here).
+
+    node = decode_node(node_json)                  -> abi.Node
+    nm, pms, n_pm, aggs, n_agg = decode_node_metric(nodemetric_json)   (the Evaluator.set_nodemetric layout)
+    pod = decode_pod(pod_json, xres_names)         -> abi.Pod
+    devices, (has_table, honor, partitions) = decode_device(device_json)
+Objects may be given as dicts (serialised with json.dumps) or JSON text.
+"""
+import ctypes as C
+import json
+
+import numpy as np
+
+from . import abi
+
+
+class DecodeError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"koord-eval decode error {code}: {msg}")
+        self.code = code
+
+
+def _lib():
+    return abi.load_library()
+
+
+def _text(obj):
+    s = obj if isinstance(obj, (str, bytes)) else json.dumps(obj)
+    return s.encode() if isinstance(s, str) else s
+
+
+def _check(lib, rc):
+    if rc != abi.OK:
+        raise DecodeError(rc, lib.ke_last_error().decode())
+
+
+def parse_quantity(s):
+    """(Value(), MilliValue()) of a resource.Quantity string."""
+    lib = _lib()
+    v, m = abi.i64(), abi.i64()
+    _check(lib, lib.ke_quantity_parse(s.encode(), C.byref(v), C.byref(m)))
+    return v.value, m.value
+
+
+def pod_key(namespace, name):
+    return _lib().ke_pod_key(namespace.encode(), name.encode())
+
+
+def decode_node(obj):
+    lib = _lib()
+    t = _text(obj)
+    n = abi.Node()
+    _check(lib, lib.ke_decode_node(t, len(t), C.byref(n)))
+    return n
+
+
+def decode_node_metric(obj, pm_cap=4096, agg_cap=16):
+    lib = _lib()
+    t = _text(obj)
+    nm = abi.NodeMetric()
+    pms = (abi.PodMetric * max(pm_cap, 1))()
+    aggs = (abi.AggregatedUsage * max(agg_cap, 1))()
+    n_pm, n_agg = abi.i32(), abi.i32()
+    _check(lib, lib.ke_decode_node_metric(t, len(t), C.byref(nm), pm_cap, pms, C.byref(n_pm), agg_cap, aggs,
+                                          C.byref(n_agg)))
+    return nm, pms, n_pm.value, aggs, n_agg.value
+
+
+def decode_pod(obj, xres_names=()):
+    lib = _lib()
+    t = _text(obj)
+    names = (C.c_char_p * max(len(xres_names), 1))(*[n.encode() for n in xres_names])
+    p = abi.Pod()
+    _check(lib, lib.ke_decode_pod(t, len(t), len(xres_names), names, C.byref(p)))
+    return p
+
+
+def decode_device(obj, cap=3 * abi.MAX_MINORS, part_cap=abi.MAX_GPU_PARTITIONS):
+    lib = _lib()
+    t = _text(obj)
+    devs = np.zeros(cap, abi.DEVICE_DTYPE)
+    parts = np.zeros(part_cap, abi.GPU_PARTITION_DTYPE)
+    n, n_parts, has_table, honor = abi.i32(), abi.i32(), abi.i32(), abi.i32()
+    _check(lib, lib.ke_decode_device(t, len(t), cap, abi.ptr(devs), C.byref(n), part_cap, abi.ptr(parts),
+                                     C.byref(n_parts), C.byref(has_table), C.byref(honor)))
+    return devs[:n.value], (bool(has_table.value), bool(honor.value), parts[:n_parts.value])
