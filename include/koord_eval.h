@@ -687,7 +687,8 @@ int ke_quota_state(ke_ctx* ctx, int32_t q, int64_t* limit, uint8_t* limit_has, i
  *                         maps the quota label to its ke_quotas_load index.
  *   ke_decode_device      Device (scheduling/v1alpha1/device_types.go:32-67) as nodeDeviceCache builds it
  *                         (device_cache.go:518-568; `used` is the pods' business: 0), the gpu-partitions annotation
- *                         (table in ascending key order) and the gpu-partition-policy label. */
+ *                         (table in ascending key order) and the gpu-partition-policy label.
+ *   ke_decode_nrt         NodeResourceTopology (below). */
 int ke_quantity_parse(const char* s, int64_t* value, int64_t* milli_value);
 int64_t ke_pod_key(const char* ns, const char* name);
 int ke_decode_node(const char* json, int64_t len, ke_node* out);
@@ -696,6 +697,16 @@ int ke_decode_node_metric(const char* json, int64_t len, ke_node_metric* nm, int
 int ke_decode_pod(const char* json, int64_t len, int32_t n_names, const char* const* xres_names, ke_pod* out);
 int ke_decode_device(const char* json, int64_t len, int32_t cap, ke_device* out, int32_t* n, int32_t part_cap,
                      ke_gpu_partition* parts, int32_t* n_parts, int32_t* has_table, int32_t* honor);
+/* NodeResourceTopology (NewTopologyOptions, nodenumaresource/topology_options.go:90-236): the zones of type
+ * "Node" named node-<id> with their Allocatable cpu / memory (cpu less 1000 per reserved CPU of the zone), the CPU
+ * table of the cpu-topology annotation (core id = socket << 16 | core) with the reserved CPUs (kubelet-managed
+ * pod-cpu-allocs, kubelet reservedCPUs, the node-reservation reservedCPUs, an exclusive system-QoS cpuset) flagged,
+ * and the node-level fields an NRT supplies, patched into *node (decode the Node first): the topology-manager
+ * policy when the Node has no policy label, FullPCPUsOnly from a static kubelet with full-pcpus-only=true, the
+ * NRT's cpu amplification ratio (-2 without a ratio map), and cpu_topology_invalid when no CPU is reported.  The
+ * resource manager's allocation state (zone allocations, RefCounts, NUMA status) is the scheduler's own: 0. */
+int ke_decode_nrt(const char* json, int64_t len, ke_node* node, int32_t zone_cap, ke_numa_zone* zones, int32_t* n_zones,
+                  int32_t cpu_cap, ke_cpu* cpus, int32_t* n_cpus);
 
 /* ---- node sharding across GPUs (one process per GPU) ------------------------------------------
  * Replaces the upstream Parallelizer's fan-out of per-node Filter/Score over goroutines

@@ -403,6 +403,8 @@ EXPORTS = {
     "ke_decode_node_metric": (C.c_int, [C.c_char_p, i64, C.POINTER(NodeMetric), i32, C.c_void_p, C.POINTER(i32), i32,
                                         C.c_void_p, C.POINTER(i32)]),
     "ke_decode_pod": (C.c_int, [C.c_char_p, i64, i32, C.c_void_p, C.POINTER(Pod)]),
+    "ke_decode_nrt": (C.c_int, [C.c_char_p, i64, C.POINTER(Node), i32, C.c_void_p, C.POINTER(i32), i32, C.c_void_p,
+                                C.POINTER(i32)]),
     "ke_decode_device": (C.c_int, [C.c_char_p, i64, i32, C.c_void_p, C.POINTER(i32), i32, C.c_void_p, C.POINTER(i32),
                                    C.POINTER(i32), C.POINTER(i32)]),
     "ke_node_resources_get": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p, C.POINTER(i32)]),

@@ -810,3 +810,184 @@ int ke_decode_device(const char* js, int64_t len, int32_t cap, ke_device* out, i
 }
 
 }  // extern "C"
+
+// ---- NodeResourceTopology (nodenumaresource/topology_options.go:90-236) -----------------------------------
+namespace {
+// k8s cpuset.Parse ("0-3,8"); false on a malformed list (the reference then logs and uses the empty set)
+bool parse_cpuset(const std::string& s, std::vector<int>& out) {
+  out.clear();
+  if (s.empty()) return true;
+  size_t i = 0;
+  while (i <= s.size()) {
+    size_t j = s.find(',', i);
+    if (j == std::string::npos) j = s.size();
+    const std::string part = s.substr(i, j - i);
+    const size_t dash = part.find('-');
+    int64_t a, b;
+    if (dash == std::string::npos) {
+      if (!parse_int64(part, &a) || a < 0) return false;
+      b = a;
+    } else if (!parse_int64(part.substr(0, dash), &a) || !parse_int64(part.substr(dash + 1), &b) || a < 0 || b < a) {
+      return false;
+    }
+    if (b - a > 4096) return false;
+    for (int64_t c = a; c <= b; c++) out.push_back((int)c);
+    i = j + 1;
+  }
+  return true;
+}
+}  // namespace
+
+extern "C" {
+
+int ke_decode_nrt(const char* js, int64_t len, ke_node* node, int32_t zone_cap, ke_numa_zone* zones, int32_t* n_zones,
+                  int32_t cpu_cap, ke_cpu* cpus, int32_t* n_cpus) {
+  if (!node || !n_zones || !n_cpus || zone_cap < 0 || cpu_cap < 0 || (zone_cap && !zones) || (cpu_cap && !cpus))
+    return bad("ke_decode_nrt arguments");
+  Value doc;
+  int rc = parse_doc(js, len, doc, "NodeResourceTopology");
+  if (rc) return rc;
+  const Value* meta = doc.field("metadata");
+  std::map<std::string, std::string> ann;
+  if ((rc = string_map(meta ? meta->field("annotations") : nullptr, ann, "metadata.annotations"))) return rc;
+  auto parse_ann = [&](const char* key, Value& v) {  // the annotation's JSON, false when absent / unparsable
+    const std::string* s = lookup(ann, key);
+    std::string err;
+    return s && json::parse(s->data(), s->size(), v, err);
+  };
+  // CPU topology (GetCPUTopology + convertCPUTopology: core id = socket << 16 | core)
+  struct Cpu {
+    int id, core, node, socket;
+  };
+  std::map<int, Cpu> topo;
+  Value v;
+  if (lookup(ann, "node.koordinator.sh/cpu-topology")) {
+    if (!parse_ann("node.koordinator.sh/cpu-topology", v) || !(v.is_null() || v.is_obj()))
+      return unsup("cpu-topology annotation that fails to unmarshal");
+    const Value* det = v.is_obj() ? v.field("detail") : nullptr;
+    if (det && det->t == Value::ARR)
+      for (const Value& c : det->a) {
+        int64_t id = 0, core = 0, sock = 0, nd = 0;
+        for (auto f : {std::make_pair("id", &id), std::make_pair("core", &core), std::make_pair("socket", &sock),
+                       std::make_pair("node", &nd)}) {
+          const Value* x = c.field(f.first);
+          if (x && !x->is_null() && !json::as_int64(*x, f.second)) return unsup("cpu-topology entry");
+        }
+        if (id < 0 || id >= KE_MAX_CPUS || core < 0 || core > 0xFFFF || sock < 0 || nd < 0)
+          return unsup("cpu-topology ids outside the modelled range (CPU ids 0..255)");
+        topo[(int)id] = Cpu{(int)id, (int)(sock << 16 | core), (int)nd, (int)sock};
+      }
+  }
+  // reserved CPUs = pod-cpu-allocs (kubelet-managed) + kubelet reserved + node reservation + exclusive system QoS
+  std::vector<int> reserved, tmp;
+  if (parse_ann("node.koordinator.sh/pod-cpu-allocs", v) && v.t == Value::ARR)
+    for (const Value& a : v.a) {
+      const Value* mk = a.field("managedByKubelet");
+      if (!(mk && mk->t == Value::BOOL && mk->b) || !*str_or_empty(a.field("uid"))) continue;
+      if (parse_cpuset(str_or_empty(a.field("cpuset")), tmp)) reserved.insert(reserved.end(), tmp.begin(), tmp.end());
+    }
+  bool kubelet_full = false;
+  if (parse_ann("kubelet.koordinator.sh/cpu-manager-policy", v) && v.is_obj()) {
+    if (parse_cpuset(str_or_empty(v.field("reservedCPUs")), tmp)) reserved.insert(reserved.end(), tmp.begin(), tmp.end());
+    const Value* opts = v.field("options");
+    const Value* full = opts && opts->is_obj() ? opts->key("full-pcpus-only") : nullptr;
+    kubelet_full = std::string(str_or_empty(v.field("policy"))) == "static" && full && full->t == Value::STR &&
+                   full->s == "true";
+  }
+  if (const std::string* s = lookup(ann, "node.koordinator.sh/reservation"); s && !s->empty()) {
+    std::string err;
+    if (json::parse(s->data(), s->size(), v, err) && v.is_obj() &&
+        parse_cpuset(str_or_empty(v.field("reservedCPUs")), tmp))
+      reserved.insert(reserved.end(), tmp.begin(), tmp.end());
+  }
+  if (parse_ann("node.koordinator.sh/system-qos-resource", v) && v.is_obj()) {
+    const Value* ex = v.field("cpusetExclusive");
+    const bool exclusive = !ex || ex->is_null() || (ex->t == Value::BOOL && ex->b);
+    if (exclusive && parse_cpuset(str_or_empty(v.field("cpuset")), tmp))
+      reserved.insert(reserved.end(), tmp.begin(), tmp.end());
+  }
+  std::sort(reserved.begin(), reserved.end());
+  reserved.erase(std::unique(reserved.begin(), reserved.end()), reserved.end());
+  auto is_reserved = [&](int c) { return std::binary_search(reserved.begin(), reserved.end(), c); };
+  // zones: type Node, name node-<id>, Allocatable per resource; cpu minus 1000 per reserved CPU of the NUMA node
+  std::vector<ke_numa_zone> zs;
+  const Value* zarr = doc.field("zones");
+  if (zarr && zarr->t == Value::ARR)
+    for (const Value& z : zarr->a) {
+      if (std::string(str_or_empty(z.field("type"))) != "Node") continue;
+      const std::string name = str_or_empty(z.field("name"));
+      if (name.compare(0, 5, "node-") != 0 || name.find("node-", 5) != std::string::npos) continue;
+      int64_t id;
+      if (!parse_int64(name.substr(5), &id)) continue;  // strconv.Atoi error: the zone is skipped
+      if (id < 0 || id >= KE_MAX_NUMA) return unsup("NUMA node id outside 0..7");
+      ke_numa_zone k{};
+      k.id = (int32_t)id;
+      const Value* res = z.field("resources");
+      if (res && res->t == Value::ARR)
+        for (const Value& r : res->a) {
+          const std::string rn = str_or_empty(r.field("name"));
+          const int slot = rn == "cpu" ? 0 : rn == "memory" ? 1 : -1;
+          if (slot < 0) continue;
+          const Value* al = r.field("allocatable");
+          int64_t val = 0, milli = 0;
+          bool ov;
+          if (al && !al->is_null() && !quantity_json(*al, &val, &milli, &ov)) return bad("zone allocatable");
+          k.has[slot] = 1;
+          k.capacity[slot] = slot == 0 ? milli : val;
+        }
+      if (k.has[0] && k.capacity[0] != 0) {
+        int in_node = 0;
+        for (const auto& kv : topo) in_node += kv.second.node == id && is_reserved(kv.first);
+        k.capacity[0] -= 1000LL * in_node;
+      }
+      zs.push_back(k);
+    }
+  std::stable_sort(zs.begin(), zs.end(), [](const ke_numa_zone& a, const ke_numa_zone& b) { return a.id < b.id; });
+  for (size_t i = 1; i < zs.size(); i++)
+    if (zs[i].id == zs[i - 1].id) return unsup("two zones with one NUMA node id");
+  if ((int64_t)zs.size() > zone_cap || (int64_t)topo.size() > cpu_cap) return bad("zone_cap / cpu_cap too small");
+  std::copy(zs.begin(), zs.end(), zones);
+  *n_zones = (int32_t)zs.size();
+  int32_t nc = 0;
+  for (const auto& kv : topo) {
+    ke_cpu c{};
+    c.cpu_id = kv.second.id;
+    c.core_id = kv.second.core;
+    c.numa_id = kv.second.node;
+    c.socket_id = kv.second.socket;
+    c.reserved = is_reserved(kv.first);
+    cpus[nc++] = c;
+  }
+  *n_cpus = nc;
+  // node-level fields the NRT carries (getNUMATopologyPolicy, GetNodeCPUBindPolicy, TopologyOptions ratios)
+  if (node->numa_topology_policy == KE_NUMA_POLICY_NONE) {
+    const Value* pols = doc.field("topologyPolicies");
+    if (pols && pols->t == Value::ARR)
+      for (const Value& p : pols->a) {
+        const std::string s = p.t == Value::STR ? p.s : "";
+        const int pol = s == "BestEffort" ? KE_NUMA_POLICY_BEST_EFFORT : s == "Restricted" ? KE_NUMA_POLICY_RESTRICTED
+                        : s == "SingleNUMANodePodLevel" ? KE_NUMA_POLICY_SINGLE_NUMA_NODE : KE_NUMA_POLICY_NONE;
+        if (pol != KE_NUMA_POLICY_NONE) {
+          node->numa_topology_policy = pol;
+          break;
+        }
+      }
+  }
+  if (kubelet_full) node->cpu_bind_policy = KE_NODE_CPU_BIND_FULL_PCPUS_ONLY;
+  node->nrt_cpu_amplification_ratio = -2.0;
+  if (lookup(ann, "node.koordinator.sh/resource-amplification-ratio")) {
+    bool ok = parse_ann("node.koordinator.sh/resource-amplification-ratio", v) && (v.is_null() || v.is_obj());
+    double cpu = 0.0;  // a ratio map without cpu: the Go zero value (no amplification)
+    if (ok && v.is_obj())
+      for (const auto& kv : v.o) {
+        double d;
+        if (!json::as_float64(kv.second, &d)) ok = false;
+        else if (kv.first == "cpu") cpu = d;
+      }
+    if (ok && v.is_obj()) node->nrt_cpu_amplification_ratio = cpu;
+  }
+  node->cpu_topology_invalid = topo.empty();  // convertCPUTopology of no detail: !IsValid()
+  return KE_OK;
+}
+
+}  // extern "C"

@@ -5,6 +5,7 @@ boundary structs, through the C ABI (ke_decode_* in libkoordeval.so; no Python r
     nm, pms, n_pm, aggs, n_agg = decode_node_metric(nodemetric_json)   (the Evaluator.set_nodemetric layout)
     pod = decode_pod(pod_json, xres_names)         -> abi.Pod
     devices, (has_table, honor, partitions) = decode_device(device_json)
+    zones, cpus = decode_nrt(nrt_json, node)       (patches the NRT-side fields of `node`)
 Objects may be given as dicts (serialised with json.dumps) or JSON text.
 """
 import ctypes as C
@@ -85,3 +86,15 @@ def decode_device(obj, cap=3 * abi.MAX_MINORS, part_cap=abi.MAX_GPU_PARTITIONS):
     _check(lib, lib.ke_decode_device(t, len(t), cap, abi.ptr(devs), C.byref(n), part_cap, abi.ptr(parts),
                                      C.byref(n_parts), C.byref(has_table), C.byref(honor)))
     return devs[:n.value], (bool(has_table.value), bool(honor.value), parts[:n_parts.value])
+
+
+def decode_nrt(obj, node):
+    """NodeResourceTopology -> (zones NUMA_ZONE_DTYPE, cpus CPU_DTYPE); patches the NRT-side fields of `node`."""
+    lib = _lib()
+    t = _text(obj)
+    zones = np.zeros(abi.MAX_NUMA, abi.NUMA_ZONE_DTYPE)
+    cpus = np.zeros(abi.MAX_CPUS, abi.CPU_DTYPE)
+    nz, nc = abi.i32(), abi.i32()
+    _check(lib, lib.ke_decode_nrt(t, len(t), C.byref(node), abi.MAX_NUMA, abi.ptr(zones), C.byref(nz), abi.MAX_CPUS,
+                                  abi.ptr(cpus), C.byref(nc)))
+    return zones[:nz.value], cpus[:nc.value]

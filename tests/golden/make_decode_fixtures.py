@@ -8,6 +8,8 @@ object and expected result by hand.  Only data is written.
     (-1 unset, 1.22 set, error on an unparsable annotation)
   * priority_utils_test.go:86-196  GetPodPriorityClassWithDefault (spec.priority ranges, the priority-class label,
     QoS labels, kube QoS of the containers)
+  * nodenumaresource/topology_options_test.go:36-176  NewTopologyOptions from a NodeResourceTopology (CPU topology,
+    reserved CPUs from four annotations, zone cpu less the reserved CPUs)
 
 Run:  python tests/golden/make_decode_fixtures.py
 """
@@ -57,6 +59,40 @@ for i, (obj, want) in enumerate((
         (pod(containers=[{"name": "abc"}]), BATCH))):
     cases.append({"name": f"priority_with_default_{i}", "source": f"{PRI}:86-196", "kind": "pod", "object": obj,
                   "want": {"priority_class": want}})
+
+# TestTopologyOptionsManager (nodenumaresource/topology_options_test.go:36-185): buildCPUTopologyForTest(2, 1, 4, 2)
+# reported as the cpu-topology annotation (raw core ids), kubelet static policy with reservedCPUs 0-1, a kubelet-managed
+# pod-cpu-alloc 0-3, system QoS cpuset 4-5 (exclusive by default), node reservation 6-7; zones node-0 / node-1 with
+# 8 cpus each.  Expected: reserved 0-7, zone cpu 0 and 8000 milli, core ids socket<<16|core; after the pod allocs
+# are removed the reserved set is 0-1,4-7 (zone node-0: 8000 - 6000).
+NRT_SRC = "pkg/scheduler/plugins/nodenumaresource/topology_options_test.go"
+rows, core, cpu = [], 0, 0
+for sock in range(2):
+    for _ in range(4):
+        for _ in range(2):
+            rows.append({"id": cpu, "core": core, "socket": sock, "node": sock})
+            cpu += 1
+        core += 1
+nrt_ann = {
+    "node.koordinator.sh/cpu-topology": json.dumps({"detail": rows}),
+    "kubelet.koordinator.sh/cpu-manager-policy": json.dumps({"policy": "static", "options": {"static": "true"},
+                                                             "reservedCPUs": "0-1"}),
+    "node.koordinator.sh/pod-cpu-allocs": json.dumps([{"namespace": "default", "name": "pod-1", "uid": "0b6a3c5e",
+                                                       "cpuset": "0-3", "managedByKubelet": True}]),
+    "node.koordinator.sh/system-qos-resource": json.dumps({"cpuset": "4-5"}),
+    "node.koordinator.sh/reservation": json.dumps({"reservedCPUs": "6-7"}),
+}
+zone = lambda n: {"name": f"node-{n}", "type": "Node", "resources": [{"name": "cpu", "capacity": "8", "allocatable": "8",
+                                                                      "available": "8"}]}
+nrt = {"metadata": {"name": "test-node-1", "annotations": nrt_ann}, "zones": [zone(0), zone(1)]}
+want_cpus = [[r["id"], r["socket"] << 16 | r["core"], r["node"], r["socket"]] for r in rows]
+cases.append({"name": "nrt_topology_options", "source": f"{NRT_SRC}:36-167", "kind": "nrt", "object": nrt,
+              "want": {"reserved": list(range(8)), "zone_cpu": [[0, 0], [1, 8000]], "cpus": want_cpus}})
+nrt2 = json.loads(json.dumps(nrt))
+del nrt2["metadata"]["annotations"]["node.koordinator.sh/pod-cpu-allocs"]
+cases.append({"name": "nrt_topology_options_no_pod_allocs", "source": f"{NRT_SRC}:169-176", "kind": "nrt",
+              "object": nrt2, "want": {"reserved": [0, 1, 4, 5, 6, 7], "zone_cpu": [[0, 2000], [1, 8000]],
+                                       "cpus": want_cpus}})
 
 if __name__ == "__main__":
     with open(os.path.join(HERE, "decode.json"), "w") as f:

@@ -15,7 +15,41 @@ from koordinator_amd import abi, decode, model
 DEC = cases.load("decode.json")
 
 
-@pytest.mark.parametrize("case", DEC, ids=[c["name"] for c in DEC])
+@pytest.mark.parametrize("case", [c for c in DEC if c["kind"] == "nrt"], ids=lambda c: c["name"])
+def test_decode_nrt_golden(lib, case):
+    node = decode.decode_node({"metadata": {"name": "n"}})
+    zones, cpus = decode.decode_nrt(case["object"], node)
+    w = case["want"]
+    assert [[int(z["id"]), int(z["capacity"][0])] for z in zones] == w["zone_cpu"], case["source"]
+    assert all(z["has"][0] == 1 and z["has"][1] == 0 for z in zones)
+    assert [[int(c["cpu_id"]), int(c["core_id"]), int(c["numa_id"]), int(c["socket_id"])] for c in cpus] == w["cpus"]
+    assert [int(c["cpu_id"]) for c in cpus if c["reserved"]] == w["reserved"]
+    assert node.cpu_topology_invalid == 0 and node.nrt_cpu_amplification_ratio == -2.0
+    # options {"static": "true"} is not full-pcpus-only: the node keeps no CPU bind policy
+    assert node.cpu_bind_policy == 0
+
+
+def test_decode_nrt_policy_and_kubelet(lib):
+    node = decode.decode_node({"metadata": {"name": "n"}})
+    nrt = {"topologyPolicies": ["None", "SingleNUMANodePodLevel"],
+           "metadata": {"annotations": {"kubelet.koordinator.sh/cpu-manager-policy":
+                                        '{"policy":"static","options":{"full-pcpus-only":"true"}}',
+                                        "node.koordinator.sh/resource-amplification-ratio": '{"memory":1.5}'}},
+           "zones": [{"name": "node-1", "type": "Node", "resources": [{"name": "memory", "allocatable": "64Gi"}]},
+                     {"name": "node-0", "type": "Node", "resources": [{"name": "memory", "allocatable": "64Gi"}]},
+                     {"name": "socket-0", "type": "Socket"}, {"name": "node-x", "type": "Node"}]}
+    zones, cpus = decode.decode_nrt(nrt, node)
+    assert [int(z["id"]) for z in zones] == [0, 1] and len(cpus) == 0
+    assert int(zones[0]["capacity"][1]) == 64 * 2**30 and zones[0]["has"][0] == 0
+    assert node.numa_topology_policy == abi.NUMA_POLICY_SINGLE_NUMA_NODE
+    assert node.cpu_bind_policy == 1 and node.cpu_topology_invalid == 1
+    assert node.nrt_cpu_amplification_ratio == 0.0  # a ratio map without cpu: Go's zero value
+    labelled = decode.decode_node({"metadata": {"labels": {"node.koordinator.sh/numa-topology-policy": "Restricted"}}})
+    decode.decode_nrt(nrt, labelled)
+    assert labelled.numa_topology_policy == abi.NUMA_POLICY_RESTRICTED  # the label wins (getNUMATopologyPolicy)
+
+
+@pytest.mark.parametrize("case", [c for c in DEC if c["kind"] != "nrt"], ids=lambda c: c["name"])
 def test_decode_golden(lib, case):
     obj = decode.decode_node(case["object"]) if case["kind"] == "node" else decode.decode_pod(case["object"])
     for k, v in case["want"].items():
