@@ -752,6 +752,9 @@ int ke_last_resolve_split(ke_ctx* ctx, double* prologue_ms, double* replay_ms);
 /* BestEffort (pod, node) pairs the last ke_eval / ke_schedule evaluated in the compacted full-merge
  * pass (no preferred merged hint). */
 int ke_debug_numa_deferred(ke_ctx* ctx, int64_t* n);
+/* DeviceShare batches of the last ke_schedule that stopped early because a pod's NormalizeScore max may have
+ * moved (their remaining pods were re-run as a new batch). */
+int ke_debug_ds_cuts(ke_ctx* ctx, int32_t* cuts);
 int ke_debug_resolve_phases(ke_ctx* ctx, double* phases6);
 /* Diagnostic build only (-DKE_PROF_REPLAY): shader cycles per pod of the replay loop's phases since the
  * last call — best unchanged candidate, row fetch issue, re-evaluation, its wave max, decision / adoption,

@@ -207,6 +207,12 @@ int ke_node_resources_get(ke_ctx* ctx, int32_t node, int32_t cap, ke_node_resour
   return KE_OK;
 }
 
+int ke_debug_ds_cuts(ke_ctx* ctx, int32_t* cuts) {
+  if (!ctx || !cuts) return fail(KE_ERR_INVALID, "ke_debug_ds_cuts arguments");
+  *cuts = ctx->c.last_ds_cuts;
+  return KE_OK;
+}
+
 int ke_node_upsert(ke_ctx* ctx, int32_t node, const ke_node* n) {
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);

@@ -67,7 +67,13 @@ struct SoA {
   int32_t* kerr;    // device error word of the context (KERR_* bits; the host reads it after a call)
   int64_t* xf;      // NodeResourcesFitPlus / ScarceResourceAvoidance: NUM_XF arrays of `stride` int64 (XF_*)
   uint64_t* xm;     //   and `stride` uint64 masks of the resource ids with Allocatable > 0 (nullptr when off)
+  // DeviceShare batches (nullptr until a device cache appears): per pod of the batch 1 + the snapshot max raw
+  // score over its feasible nodes (DSB_MAX), how many feasible nodes attain it (DSB_CNT), and the replay's cut
+  // word (DSB_CUT: the first pod it left unplaced, -1 = none)
+  uint32_t* dsb;
+  uint16_t* dsraw;  // DeviceShare batch: per pod, 1 + each node's raw score in the batch's snapshot (0 = infeasible)
 };
+constexpr int DSB_MAX = 0, DSB_CNT = 64, DSB_CUT = 128, DSB_WORDS = 129;
 // kerr bits: an input the kernels refuse mid-call (the call returns KE_ERR_UNSUPPORTED)
 constexpr int32_t KERR_DS_MERGE = 1;  // a DeviceShare BestEffort merge beyond the permutation budget
 
@@ -2635,9 +2641,11 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
     if (NUMA) defer_push(o.status == STATUS_DEFERRED, ((uint64_t)p << 32) | (uint32_t)i, defer_list, defer_cnt);
     if (DS && (pod.flags & PF_DS)) {  // DefaultNormalizeScore's max: 1 + max raw score over feasible nodes
       const uint32_t r = o.total >= 0 ? (uint32_t)(o.ds + 1) : 0u;
-      dsraw[i] = (uint16_t)r;
+      dsraw[(int64_t)p * score_stride + i] = (uint16_t)r;
       const uint32_t m = __ockl_wfred_max_u32(r);
-      if ((threadIdx.x & 63) == 0 && m) atomicMax(dsmax1, m);
+      if ((threadIdx.x & 63) == 0 && m) atomicMax(dsmax1 + p, m);
+    } else if (DS) {  // a plain pod of a DeviceShare batch: raw 0, no normalisation
+      dsraw[(int64_t)p * score_stride + i] = (uint16_t)(o.total >= 0 ? 1u : 0u);
     }
     if (CPU && NUMA) aff_out[i] = o.aff;  // singleton batch: the affinity its Reserve allocates on
   }
@@ -2999,12 +3007,15 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
                                                          int lo, int hi, uint32_t* __restrict__ cand,
                                                          int32_t* __restrict__ cand_cnt,
                                                          const uint16_t* __restrict__ dsraw,
-                                                         const uint32_t* __restrict__ dsmax1, int32_t wds, int kext,
+                                                         uint32_t* __restrict__ dsmax1, int32_t wds, int kext,
                                                          int ostride) {
   __shared__ int16_t s_lut[DS ? MAX_DS_RAW + 1 : 1];
-  DsNorm dn{dsraw, s_lut};
+  __shared__ int32_t s_dscnt;
+  DsNorm dn{DS ? dsraw + (int64_t)blockIdx.x * score_stride : dsraw, s_lut};
+  uint32_t m1 = 0;
   if (DS) {
-    const uint32_t m1 = *dsmax1;
+    m1 = dsmax1[blockIdx.x];
+    if (threadIdx.x == 0) s_dscnt = 0;
     for (int x = threadIdx.x; x <= MAX_DS_RAW; x += SELECT_BLOCK) s_lut[x] = (int16_t)(wds * ds_norm(x, m1));
     __syncthreads();
   }
@@ -3025,7 +3036,7 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
 
   // pass 1
   uint32_t mx = 0;
-  int feas = 0;
+  int feas = 0, at_max = 0;  // DS: feasible nodes whose raw score attains the normalisation max
   for (int b = w0; b < w1; b += 512) {
     uint32_t v[8];
     load8<DS>(sc, b + lane * 8, w1, v, dn);
@@ -3034,6 +3045,16 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
       mx = max(mx, v[t]);
       feas += v[t] > 0;
     }
+    if (DS && m1) {
+      uint32_t r[8];
+      load8_raw(dn.raw, b + lane * 8, w1, r);
+#pragma unroll
+      for (int t = 0; t < 8; t++) at_max += r[t] == m1;
+    }
+  }
+  if (DS && m1) {
+    at_max = wave_sum(at_max);
+    if (lane == 0 && at_max) atomicAdd(&s_dscnt, at_max);
   }
   mx = wave_max_u32(mx);
   feas = wave_sum(feas);
@@ -3168,7 +3189,10 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) cand_cnt[j] = s_out;
+  if (threadIdx.x == 0) {
+    cand_cnt[j] = s_out;
+    if (DS) dsmax1[DSB_CNT + j] = (uint32_t)s_dscnt;
+  }
 }
 
 // --- node-sharded batches: merge of the per-shard candidate lists ---------------------------------
@@ -3364,6 +3388,8 @@ struct ResLds {
   DevPod pod[MAX_BATCH];
   double pd[MAX_BATCH][4];  // the pod's estimate and requests (cpu, memory) as doubles
   int32_t cnt[MAX_BATCH];
+  uint32_t dsm[MAX_BATCH];  // DeviceShare batch: 1 + snapshot max raw score of each pod (0: none / not DS)
+  int32_t dsc[MAX_BATCH];   // ... and the number of its feasible nodes attaining it
   uint32_t chg[CHG_LDS_WORDS];
 };
 
@@ -3406,6 +3432,10 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
     L.pd[tid][1] = (double)pd.est[1];
     L.pd[tid][2] = (double)pd.req[0];
     L.pd[tid][3] = (double)pd.req[1];
+    if (DS) {  // written by this batch's eval / select, earlier on the same stream
+      L.dsm[tid] = s.dsb[DSB_MAX + tid];
+      L.dsc[tid] = (int32_t)s.dsb[DSB_CNT + tid];
+    }
   }
   __syncthreads();
   {  // candidate keys (sc1: k_fixup of a concurrent launch wrote them), unused slots zeroed
@@ -3453,7 +3483,8 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
   const DevPod* const s_pod = L.pod;
   const int lane = threadIdx.x & 63;
   int n_chg = 0, n_fetch = 0;
-  constexpr bool FAST = !NUMA;  // changed nodes as replay records (fast_total); NUMA: full rows + zones
+  // changed nodes as replay records (fast_total); NUMA / DeviceShare batches: full rows (+ zones / devices)
+  constexpr bool FAST = !NUMA && !DS;
   NodeRegs mine;   // NUMA: the changed node's row
   Row spare;       // NUMA, lane n_chg: the row of the pod's best unchanged candidate
   NodeFast fast;   // FAST: the changed node's record
@@ -3492,12 +3523,24 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
     n_fetch += bu != 0;
     RPROF(1)
     uint32_t kc = 0;  // exact re-evaluation of the nodes changed earlier in this batch
+    uint32_t craw = 0;  // DeviceShare batch: 1 + the changed node's current raw DeviceShare score (0 = infeasible)
+    const uint32_t m0 = DS ? L.dsm[j] : 0u;  // the snapshot's normalisation max of pod j (DeviceShare pods)
+    uint32_t snap = 0;  // DeviceShare batch: 1 + the changed node's raw score for pod j in the snapshot
+    if (DS && (pod.flags & PF_DS) && lane < n_chg) snap = s.dsraw[(int64_t)(j) * s.stride + my_node];
     if (lane < n_chg) {
       int32_t tot;
       if constexpr (NUMA) {
         NumaNode nv;
         numa_load(s, my_node, nv);
         tot = eval_pair<false, NUMA>(mine, my_expired, pod, k, s, my_node, nv).total;
+      } else if constexpr (DS) {
+        NumaNode nv;  // unused without NUMA policies
+        const EvalOut o = eval_pair<true, false>(mine, my_expired, pod, k, s, my_node, nv);
+        tot = o.total;
+        if (tot >= 0) {
+          craw = (uint32_t)o.ds + 1;
+          tot += k.wp_ds * ds_norm(o.ds, m0);
+        }
       } else {
         tot = fast_total(fast, pod, estd, reqd, k);
       }
@@ -3506,6 +3549,21 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
     RPROF(2)
     const uint32_t bc = wave_max_u32(kc);
     RPROF(3)
+    // DeviceShare batch: pod j's candidate keys used the snapshot max m0.  It still is the max over the
+    // feasible nodes when some node that attained it in the snapshot is unchanged (it still does) and no
+    // changed node now exceeds it; otherwise the batch stops here and the host re-runs pods j..
+    if constexpr (DS) {
+      if (pod.flags & PF_DS) {
+        const uint32_t cmax = wave_max_u32(craw);
+        // snapshot max-attaining nodes that changed since: the rest still attain m0
+        const int lost = __popcll(__ballot(lane < n_chg && snap == m0));
+        const bool safe = m0 == 0 ? cmax == 0 : (cmax <= m0 && L.dsc[j] > lost);
+        if (!safe) {
+          if (lane == 0) s.dsb[DSB_CUT] = (uint32_t)(base + j);
+          break;
+        }
+      }
+    }
     // ElasticQuota PreFilter: a refused pod is placed nowhere
     int64_t qreq[2] = {0, 0};
     const bool adm = !QUOTA || !pod.quota || quota_admit_r(s, pod, k, Q, qreq);
@@ -3552,8 +3610,8 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
           mine.nreq[1] += pod.req[1];
         }
         if (!FAST && (k.flags & AF_EXT)) ext_reserve(s, my_node, pod, k);  // read back by the next re-evaluations
-        // DeviceShare Reserve (a DeviceShare pod is alone in its batch: no later pod of the batch
-        // reads the device state it patches)
+        // DeviceShare Reserve (the device SoA is global: a later pod of the batch re-evaluating this node
+        // reads it back, wave_lds_sync below)
         const uint32_t nfl = FAST ? fast.nflags : mine.flags;
         al = DS && (pod.flags & PF_DS) && (nfl & NF_DS_CACHE) ? ds_reserve(s, my_node, pod, k, DsAff{false, 0u}) : 0ull;
         if (NUMA) {  // NodeNUMAResource Reserve: the zones of a NUMA-policy node
@@ -3588,7 +3646,7 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
     // pod j+1's changed flags, read after this Reserve's bitmap update (LDS ops of a wave execute in
     // order), so they already include pod j's new node
     const bool chg_n = ck_n != 0 && chg_test(C, key_node(ck_n));
-    if (NUMA) wave_lds_sync();  // the next re-evaluation reads the zones this Reserve patched
+    if (NUMA || DS) wave_lds_sync();  // the next re-evaluation reads the zones / devices this Reserve patched
     else __atomic_signal_fence(__ATOMIC_SEQ_CST);
     pod = pod_n;
 #pragma unroll
@@ -4122,10 +4180,15 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
 __global__ void k_stamp(uint64_t* stamps) { stamps[0] = __builtin_amdgcn_s_memrealtime(); }
 // start of a batch on its eval stream: the eval-start stamp, and the zeroed atomicMax targets of a
 // DeviceShare batch (NormalizeScore's max) and of a one-pod argmax (one launch instead of three)
-__global__ void k_batch_begin(uint64_t* stamp, uint32_t* dsmax, uint32_t* argmax) {
-  stamp[0] = __builtin_amdgcn_s_memrealtime();
-  if (dsmax) dsmax[0] = 0;
-  if (argmax) argmax[0] = 0;
+__global__ void k_batch_begin(uint64_t* stamp, uint32_t* dsb, uint32_t* argmax) {  // 64 threads
+  const int t = threadIdx.x;
+  if (t == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
+  if (dsb) {
+    dsb[DSB_MAX + t] = 0;
+    dsb[DSB_CNT + t] = 0;
+    if (t == 0) dsb[DSB_CUT] = 0xFFFFFFFFu;
+  }
+  if (argmax && t == 0) argmax[0] = 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -4269,8 +4332,10 @@ int device_create(Context* ctx) {
     HIP_OK(hipMalloc(&d->d_chg, sizeof(uint32_t) * (d->capacity + 31) / 32));
     HIP_OK(hipMemsetAsync(d->d_chg, 0, sizeof(uint32_t) * (d->capacity + 31) / 32, d->stream));
   }
-  HIP_OK(hipMalloc(&d->d_dsraw, sizeof(uint16_t) * d->capacity));
-  HIP_OK(hipMalloc(&d->d_dsmax, sizeof(uint32_t) * MAX_BATCH));
+  HIP_OK(hipMalloc(&d->d_dsraw, sizeof(uint16_t) * MAX_BATCH * d->capacity));  // per pod of a DeviceShare batch
+  HIP_OK(hipMalloc(&d->d_dsmax, sizeof(uint32_t) * DSB_WORDS));
+  d->soa.dsb = d->d_dsmax;
+  d->soa.dsraw = d->d_dsraw;
   HIP_OK(hipMalloc(&d->d_aff, d->capacity));
   HIP_OK(hipStreamSynchronize(d->stream));
   return KE_OK;
@@ -4774,16 +4839,27 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     bool ds, cpu;  // singleton of a DeviceShare pod / of a pod that may bind CPUs
   };
   std::vector<Batch> batches;
+  // DeviceShare pods share batches (exact: the replay checks each pod's normalisation max and stops the
+  // batch where it may have moved) unless the nodes are sharded or carry NUMA policies (then
+  // each is a singleton batch)
+  const bool ds_batch = !(d->world > 1 || d->comm) && !d->numa_alloc && ctx->n_nodes > 0;
+  ctx->last_ds_cuts = 0;
   for (int32_t p = 0; p < n_pods;) {
     const uint32_t f = d->host_pods[p].flags;
-    if (f & (PF_DS | PF_CPUSET)) {
+    if ((f & PF_CPUSET) || ((f & PF_DS) && !ds_batch)) {
       batches.push_back({1, (f & PF_DS) != 0, (f & PF_CPUSET) != 0});
       p++;
       continue;
     }
     int bp = 0;
-    while (p + bp < n_pods && bp < B && !(d->host_pods[p + bp].flags & (PF_DS | PF_CPUSET))) bp++;
-    batches.push_back({bp, false, false});
+    bool has_ds = false;
+    while (p + bp < n_pods && bp < B) {
+      const uint32_t g = d->host_pods[p + bp].flags;
+      if ((g & PF_CPUSET) || ((g & PF_DS) && !ds_batch)) break;
+      has_ds = has_ds || (g & PF_DS);
+      bp++;
+    }
+    batches.push_back({bp, has_ds, false});
     p += bp;
   }
   bool any_cpu = false;
@@ -4883,6 +4959,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   int n_pipelined = 0;
   // Batch b's eval + candidate lists on stream `es`.  pipe: stale top-(k_j + KMAX) lists into the run's
   // stale buffer (k_fixup makes them exact); else the exact top-k_j lists straight into d_cand.
+  bool rerun = false;  // the current serial batch is the remainder of a DeviceShare batch that stopped early
   auto eval_select = [&](int b, bool pipe, hipStream_t es) -> int {
     const int bp = batches[b].pods;
     const bool ds = batches[b].ds, cpu = batches[b].cpu;
@@ -4890,7 +4967,8 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     hipEvent_t* pe = prof ? &ev[(size_t)(b / every) * PE] : nullptr;
     const int32_t* bbase = d_bases + b;
     const bool argmax1 = !sharded && bp == 1 && !pipe && N > 0;  // selectHost of one pod: a grid-wide argmax
-    hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(1), 0, es, estamps + b, ds ? d->d_dsmax : nullptr,
+    // a re-run remainder keeps its batch's first dequeue stamp (latency counts from there)
+    hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(MAX_BATCH), 0, es, estamps + (rerun ? n_pods + 1 : b), ds ? d->d_dsmax : nullptr,
                        argmax1 ? d->d_cand : nullptr);
     if (prof) HIP_OK(hipEventRecord(pe[0], es));
     const int L = pipe ? KSTALE : KMAX, kext = pipe ? KMAX : 0;
@@ -5026,6 +5104,21 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       hipLaunchKernelGGL(resolve, dim3(1), dim3(numa ? res_threads<true>() : res_threads<false>()), 0, d->stream, d->soa, d->d_pods, bbase, bp, k,
                          d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score, ctx->cfg.global_node_offset,
                          d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc, d->d_numaalloc, d->d_chg, N);
+      if (ds) {  // a DeviceShare batch may stop early: re-run its remaining pods as batch b
+        int32_t cut = -1;
+        HIP_OK(hipMemcpyAsync(&cut, d->d_dsmax + DSB_CUT, sizeof(int32_t), hipMemcpyDeviceToHost, d->stream));
+        HIP_OK(hipStreamSynchronize(d->stream));
+        if (cut >= 0) {
+          if (cut <= bases[b] || cut >= bases[b] + bp) return fail(KE_ERR_DEVICE, "DeviceShare batch cut out of range");
+          batches[b].pods = bases[b] + bp - cut;
+          bases[b] = cut;
+          HIP_OK(hipMemcpyAsync(d_bases + b, &bases[b], sizeof(int32_t), hipMemcpyHostToDevice, d->stream));
+          ctx->last_ds_cuts++;
+          rerun = true;
+          continue;
+        }
+      }
+      rerun = false;
     }
     if (b + 1 < n_batches && run_end[b + 1] > 0)  // the next run's eval stream waits for this Reserve
       HIP_OK(hipEventRecord(d->ev_res[b % R], d->stream));

@@ -223,6 +223,12 @@ class Evaluator:
     def set_profiling(self, sample_every):
         self._check(self.lib.ke_set_profiling(self.h, sample_every))
 
+    def ds_cuts(self):
+        """DeviceShare batches of the last schedule that stopped early (NormalizeScore max may have moved)."""
+        n = abi.i32()
+        self._check(self.lib.ke_debug_ds_cuts(self.h, C.byref(n)))
+        return n.value
+
     def numa_deferred(self):
         """BestEffort pairs of the last eval / schedule that needed the compacted full NUMA merge."""
         n = abi.i64()

@@ -340,8 +340,8 @@ def test_deviceshare_eval_matrix_parity(gpu, strategy):
 
 @pytest.mark.parametrize("strategy", [abi.STRATEGY_LEAST_ALLOCATED, abi.STRATEGY_MOST_ALLOCATED])
 def test_deviceshare_schedule_parity(gpu, strategy):
-    """Mixed queue: DeviceShare pods (one per batch, NormalizeScore over all feasible nodes) between
-    batches of plain pods; placements, scores and the allocated device minors equal the oracle's."""
+    """Mixed queue: DeviceShare pods (batched with the plain pods, NormalizeScore over all feasible nodes);
+    placements, scores and the allocated device minors equal the oracle's."""
     ev, o = ds_both(1500, 83, strategy)
     pods = synth.make_ds_pods(600, synth.BASE_SEED + 84)
     c1, s1 = ev.schedule(pods, synth.T0)
@@ -355,6 +355,27 @@ def test_deviceshare_schedule_parity(gpu, strategy):
     for k in ("status", "ds", "total", "best"):
         assert np.array_equal(a[k], b[k]), k
     assert ev.check_records(synth.T0) == 0
+
+
+@pytest.mark.parametrize("strategy", [abi.STRATEGY_LEAST_ALLOCATED, abi.STRATEGY_MOST_ALLOCATED])
+def test_deviceshare_batches_exact(gpu, strategy):
+    """DeviceShare pods share speculative batches: each pod's NormalizeScore max is checked in the replay and
+    the batch stops where it may have moved (MostAllocated moves it often).  Every batch size gives the
+    oracle's placements, scores and device minors."""
+    pods = synth.make_ds_pods(400, synth.BASE_SEED + 94, device_fraction=0.7)
+    ref = None
+    for b in (1, 7, 64):
+        ev, o = ds_both(900, 93, strategy, batch=b)
+        c1, s1 = ev.schedule(pods, synth.T0)
+        if ref is None:
+            c0, s0 = o.schedule(pods, synth.T0)
+            ref = (c0, s0, o.last_device_allocations.copy())
+        assert np.array_equal(c1, ref[0]), (b, np.argwhere(c1 != ref[0])[:5].ravel().tolist())
+        assert np.array_equal(s1, ref[1]), b
+        assert np.array_equal(ev.last_device_allocations, ref[2]), b
+        assert ev.check_records(synth.T0) == 0
+        if b == 64 and strategy == abi.STRATEGY_MOST_ALLOCATED:
+            assert ev.ds_cuts() > 0  # the max moves under MostAllocated: the cut path ran
 
 
 def test_deviceshare_sharded_loopback(gpu):

@@ -67,6 +67,7 @@ def main():
     sl = P // K
     lat, ks_acc, samples, placed, with_dev = [], {"eval_ms": 0.0, "select_ms": 0.0, "resolve_ms": 0.0}, 0, 0, 0
     hs = []
+    cuts = 0
     t0 = time.perf_counter()
     for s in range(K):
         chosen, _ = ev.schedule(pods[s * sl:(s + 1) * sl], synth.T0)
@@ -80,6 +81,7 @@ def main():
         ks_acc["resolve_ms"] += ks["resolve_ms"] * len(per_batch)  # in-kernel stamps: mean over every batch
         samples += ks["samples"]
         hs.append(ev.host_stats())
+        cuts += ev.ds_cuts()
     dt = time.perf_counter() - t0
     ev.close()
     out = {"workload": f"{N} nodes x (8 GPU + 2 RDMA), {K * sl} pods ({a.device:.0%} with device requests)"
@@ -90,7 +92,7 @@ def main():
            "kernel_ms_per_batch": {"eval_ms": ks_acc["eval_ms"] / max(samples, 1),
                                    "select_ms": ks_acc["select_ms"] / max(samples, 1),
                                    "resolve_ms": ks_acc["resolve_ms"] / max(len(lat), 1)},
-           "placed": placed, "device_allocations": with_dev,
+           "placed": placed, "device_allocations": with_dev, "ds_batch_cuts": cuts,
            "host_ms_per_step": {k: float(np.mean([h[k] for h in hs])) for k in hs[0]} if hs else None}
     if not a.no_cpu_baseline:
         from oracle.binding import Oracle  # checker / baseline only
