@@ -269,7 +269,22 @@ struct DsInst {
   uint32_t th, fh;  // key presence of total / free'
   bool used_nz;     // used' kept (non-zero): the minor is in getRealUsed (allocator_gpu.go:59-70)
 };
-__device__ __forceinline__ void ds_instance(const SoA& s, int64_t i, int t, int m, const uint64_t msk[4], DsInst& d) {
+// the instance's total / used words (0 for absent keys), loaded ahead of their use (ds_type_view issues a
+// group of instances' loads together: one memory round trip per group instead of per instance)
+struct DsRaw {
+  int64_t tv[3], uv[3];
+};
+__device__ __forceinline__ void ds_load(const SoA& s, int64_t i, int t, int m, const uint64_t msk[4], DsRaw& r) {
+  const int nk = DS_NK[t];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const bool ht = k < nk && ((msk[ds_ht_word(t)] >> ds_ht_bit(t, m, k)) & 1);
+    const bool hu = k < nk && ((msk[ds_hu_word(t)] >> ds_hu_bit(t, m, k)) & 1);
+    r.tv[k] = ht ? dsf(s, DS_TBASE[t] + m * nk + k, i) : 0;
+    r.uv[k] = hu ? dsf(s, DS_UBASE[t] + m * nk + k, i) : 0;
+  }
+}
+__device__ __forceinline__ void ds_instance_from(const DsRaw& r, int t, int m, const uint64_t msk[4], DsInst& d) {
   const int nk = DS_NK[t];
   int64_t up[3];
   uint32_t uh = 0;
@@ -282,8 +297,8 @@ __device__ __forceinline__ void ds_instance(const SoA& s, int64_t i, int t, int 
     if (k >= nk) continue;
     const bool ht = (msk[ds_ht_word(t)] >> ds_ht_bit(t, m, k)) & 1;
     const bool hu = (msk[ds_hu_word(t)] >> ds_hu_bit(t, m, k)) & 1;
-    const int64_t tv = ht ? dsf(s, DS_TBASE[t] + m * nk + k, i) : 0;
-    const int64_t uv = hu ? dsf(s, DS_UBASE[t] + m * nk + k, i) : 0;
+    const int64_t tv = r.tv[k];
+    const int64_t uv = r.uv[k];
     const int64_t fo = ht ? (tv - uv > 0 ? tv - uv : 0) : 0;  // free_orig (used-only keys: 0)
     up[k] = ht ? (tv - fo > 0 ? tv - fo : 0) : 0;            // used' (keys of total U used)
     d.tv[k] = tv;
@@ -331,10 +346,15 @@ __device__ __forceinline__ bool ds_total_nz(const DsInst& d) {
   return nz;
 }
 
+// x*100/cap exactly (Go int64 division) without the 64-bit division routine on the usual range (div100)
+__device__ __forceinline__ int64_t ds_div100(int64_t x, int64_t cap) {
+  const double dc = (double)cap;
+  return div100(x, cap, dc, __builtin_amdgcn_rcp(dc));
+}
 __device__ __forceinline__ int64_t ds_res_score(bool most, int64_t req, int64_t cap) {  // scoring.go:283-322
   if (cap == 0) return 0;
-  if (most) return (req > cap ? cap : req) * 100 / cap;
-  return req > cap ? 0 : (cap - req) * 100 / cap;
+  if (most) return ds_div100(req > cap ? cap : req, cap);
+  return req > cap ? 0 : ds_div100(cap - req, cap);
 }
 
 // resourceAllocationScorer.scorer over per-key (requested, allocatable) with weights (scoring.go:268-297)
@@ -349,7 +369,8 @@ __device__ __forceinline__ int64_t ds_weighted(const KArgs& k, int t, const int6
     sc += ds_res_score(k.flags & AF_DS_MOST, req, tot[key]) * k.w_ds[wi];
     ws += k.w_ds[wi];
   }
-  return ws ? sc / ws : 0;
+  if (!ws) return 0;
+  return (sc >= 0 && sc < (1 << 22) && ws < (1 << 22)) ? div_small((int32_t)sc, (int32_t)ws) : sc / ws;
 }
 
 // bitmask.IterateBitMasks order over NUMA ids 0..7: by popcount, then lexicographic on the ascending
@@ -657,32 +678,46 @@ __device__ __forceinline__ bool ds_type_view(const SoA& s, int64_t i, int t, con
   bool present = false;
 #pragma unroll
   for (int q = 0; q < 3; q++) tot[q] = fre[q] = 0;
+  constexpr int GRP = 2;  // instances whose words are loaded together
   while (ex) {
-    const int m = __builtin_ctzll(ex);
-    ex &= ex - 1;
-    bool hu = false;
+    int ms[GRP];
+    DsRaw raw[GRP];
 #pragma unroll
-    for (int q = 0; q < 3; q++) hu = hu || (q < nk && ((msk[ds_hu_word(t)] >> ds_hu_bit(t, m, q)) & 1));
-    orig_used |= (uint32_t)hu << m;
-    DsInst d;
-    ds_instance(s, i, t, m, msk, d);
-    const bool fz = ds_free_zero(d);
-    present = present || !fz;
-    if (!((allowed >> m) & 1u)) continue;
-    const bool leq = ds_leq(d, p, t), tnz = ds_total_nz(d);
-    dflt |= (uint32_t)(!fz && leq) << m;
-    sat |= (uint32_t)(leq && tnz) << m;
-    tot_m |= (uint32_t)tnz << m;
-    used_p |= (uint32_t)d.used_nz << m;
-    int64_t tv[3], fv[3];
-#pragma unroll
-    for (int q = 0; q < 3; q++) {
-      tv[q] = ((d.th >> q) & 1) ? d.tv[q] : 0;
-      fv[q] = ((d.fh >> q) & 1) ? d.fv[q] : 0;
-      tot[q] += tv[q];
-      fre[q] += fv[q];
+    for (int u = 0; u < GRP; u++) {
+      ms[u] = ex ? __builtin_ctzll(ex) : -1;
+      ex &= ex ? ex - 1 : 0;
     }
-    if (score) score[m] = ds_weighted(k, t, tv, fv, p);  // scoreDevice
+#pragma unroll
+    for (int u = 0; u < GRP; u++)
+      if (ms[u] >= 0) ds_load(s, i, t, ms[u], msk, raw[u]);
+#pragma unroll
+    for (int u = 0; u < GRP; u++) {
+      const int m = ms[u];
+      if (m < 0) continue;
+      bool hu = false;
+#pragma unroll
+      for (int q = 0; q < 3; q++) hu = hu || (q < nk && ((msk[ds_hu_word(t)] >> ds_hu_bit(t, m, q)) & 1));
+      orig_used |= (uint32_t)hu << m;
+      DsInst d;
+      ds_instance_from(raw[u], t, m, msk, d);
+      const bool fz = ds_free_zero(d);
+      present = present || !fz;
+      if (!((allowed >> m) & 1u)) continue;
+      const bool leq = ds_leq(d, p, t), tnz = ds_total_nz(d);
+      dflt |= (uint32_t)(!fz && leq) << m;
+      sat |= (uint32_t)(leq && tnz) << m;
+      tot_m |= (uint32_t)tnz << m;
+      used_p |= (uint32_t)d.used_nz << m;
+      int64_t tv[3], fv[3];
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        tv[q] = ((d.th >> q) & 1) ? d.tv[q] : 0;
+        fv[q] = ((d.fh >> q) & 1) ? d.fv[q] : 0;
+        tot[q] += tv[q];
+        fre[q] += fv[q];
+      }
+      if (score) score[m] = ds_weighted(k, t, tv, fv, p);  // scoreDevice
+    }
   }
   present = present && allowed != 0;
   if (present) {

@@ -23,11 +23,15 @@ def main():
     ap.add_argument("--nodes", type=int, default=50_000)
     ap.add_argument("--pods", type=int, default=5_000)
     ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--ds", type=float, default=0.0, help="C5 shape: DeviceShare pods (this fraction) on 8 GPU + 2 RDMA nodes")
     a = ap.parse_args()
     cl = synth.make_cluster(a.nodes, synth.BASE_SEED + a.config)
     pods = synth.make_pods(a.pods, synth.BASE_SEED + 100 + a.config)
     ev = Evaluator(synth.config(a.nodes))
     synth.load_into(ev, cl)
+    if a.ds > 0:
+        pods = synth.make_ds_pods(a.pods, synth.BASE_SEED + 105, device_fraction=a.ds)
+        synth.load_devices(ev, synth.make_devices(a.nodes, synth.BASE_SEED + 55))
     ev.eval(pods[:0], synth.T0)
     cyc = np.zeros(8)
     ev.lib.ke_debug_replay_phases(ev.h, cyc.ctypes.data_as(C.c_void_p))  # reset
