@@ -4871,7 +4871,8 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   const int B = ctx->cfg.pod_batch;
   struct Batch {
     int pods;
-    bool ds, cpu;  // singleton of a DeviceShare pod / of a pod that may bind CPUs
+    bool ds, cpu;  // DeviceShare-capable batch (its pods' NormalizeScore) / singleton of a pod that may bind CPUs
+    bool cut;      // a DeviceShare batch with DeviceShare pods: the replay may stop early
   };
   std::vector<Batch> batches;
   // DeviceShare pods share batches (exact: the replay checks each pod's normalisation max and stops the
@@ -4882,19 +4883,20 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   for (int32_t p = 0; p < n_pods;) {
     const uint32_t f = d->host_pods[p].flags;
     if ((f & PF_CPUSET) || ((f & PF_DS) && !ds_batch)) {
-      batches.push_back({1, (f & PF_DS) != 0, (f & PF_CPUSET) != 0});
+      batches.push_back({1, (f & PF_DS) != 0, (f & PF_CPUSET) != 0, false});
       p++;
       continue;
     }
     int bp = 0;
-    bool has_ds = false;
+    bool has_ds = false, ds_pods = false;
     while (p + bp < n_pods && bp < B) {
       const uint32_t g = d->host_pods[p + bp].flags;
       if ((g & PF_CPUSET) || ((g & PF_DS) && !ds_batch)) break;
-      has_ds = has_ds || (g & PF_DS);
+      has_ds = has_ds || (g & PF_DS) || (ctx->ext_enabled && ds_batch);  // FitPlus / SRA: the record-free replay
+      ds_pods = ds_pods || (g & PF_DS);
       bp++;
     }
-    batches.push_back({bp, has_ds, false});
+    batches.push_back({bp, has_ds, false, ds_pods && bp > 1});
     p += bp;
   }
   bool any_cpu = false;
@@ -5139,7 +5141,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       hipLaunchKernelGGL(resolve, dim3(1), dim3(numa ? res_threads<true>() : res_threads<false>()), 0, d->stream, d->soa, d->d_pods, bbase, bp, k,
                          d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score, ctx->cfg.global_node_offset,
                          d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc, d->d_numaalloc, d->d_chg, N);
-      if (ds) {  // a DeviceShare batch may stop early: re-run its remaining pods as batch b
+      if (batches[b].cut) {  // a DeviceShare batch may stop early: re-run its remaining pods as batch b
         int32_t cut = -1;
         HIP_OK(hipMemcpyAsync(&cut, d->d_dsmax + DSB_CUT, sizeof(int32_t), hipMemcpyDeviceToHost, d->stream));
         HIP_OK(hipStreamSynchronize(d->stream));

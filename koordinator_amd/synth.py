@@ -780,7 +780,9 @@ def make_node_resources(cl, seed, gpu_fraction=0.3, scarce_fraction=0.15):
         if rng.random() < scarce_fraction:
             rows.append((6, int(rng.integers(1, 4)), 0))
         if rng.random() < 0.03:  # a listed resource with zero allocatable: not a name of the node
-            rows.append((6 if rows[-1][0] != 6 else 5, 0, 0))
+            free = [r for r in (6, 5) if r not in {x[0] for x in rows}]
+            if free:
+                rows.append((free[0], 0, 0))
         t = np.zeros(len(rows), abi.NODE_RESOURCE_DTYPE)
         for e, (rid, a, r) in enumerate(rows):
             t[e]["id"], t[e]["allocatable"], t[e]["requested"] = rid, a, r
