@@ -145,9 +145,8 @@ int ke_create(const ke_config* cfg, ke_ctx** out) {
   k.wp_ds = (int32_t)cfg->weight_deviceshare;
   for (int i = 0; i < 4; i++)
     k.w_ds[i] = cfg->deviceshare.weights[i] == KE_ABSENT ? -1 : (int32_t)cfg->deviceshare.weights[i];
-  // NodeResourcesFitPlus / ScarceResourceAvoidance: their Score runs in eval_pair and the record-free replays
-  // (the DeviceShare batches' path, or the zone-aware one of NUMA / sharded contexts), never in the records of
-  // the pipelined fast replay
+  // NodeResourcesFitPlus / ScarceResourceAvoidance: their Score joins every evaluation path (eval_pair,
+  // lite_total, and the fast replay's fast_total from the node's ext words)
   const ke_ext_args& x = cfg->ext;
   k.wp_fp = (int32_t)x.weight_fitplus;
   k.wp_sra = (int32_t)x.weight_sra;
@@ -707,8 +706,6 @@ int ke_shard_init(ke_ctx* ctx, int32_t rank, int32_t world, const uint8_t* id) {
   if (!ctx) return fail(KE_ERR_INVALID, "null context");
   int rc = require_device(ctx);
   if (rc) return rc;
-  // sharded contexts keep one DeviceShare pod per batch: FitPlus / SRA then run on the zone-aware path
-  if (ctx->c.ext_enabled && (world > 1 || id)) ctx->c.numa_enabled = true;
   return device_shard_init(&ctx->c, rank, world, id);
 }
 

@@ -1866,15 +1866,17 @@ __device__ __forceinline__ void numa_reserve(const SoA& s, int64_t i, uint32_t n
 // Weighted framework contribution of the two plugins for a feasible (pod, node).  Go int64 arithmetic
 // (wrapping products, truncating division) on the ext SoA.
 __device__ __forceinline__ int64_t mul100_wrap(int64_t x) { return (int64_t)((uint64_t)x * 100u); }
-__device__ __forceinline__ int32_t ext_score(const SoA& s, int64_t i, const DevPod& p, const KArgs& k) {
+// from the node's words: xm = ids with Allocatable > 0, xa / xr = FitPlus slots' Allocatable / (NonZero)Requested
+__device__ __forceinline__ int32_t ext_score_vals(uint64_t xm, const int64_t (&xa)[4], const int64_t (&xr)[4],
+                                                  const DevPod& p, const KArgs& k) {
   int32_t t = 0;
   if (k.wp_fp) {  // resourceScorer (node_resource_fit_plus_utils.go:57-89) over the pod's requested names
     int64_t ns = 0, ws = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       if (q >= k.fp_n || !((p.xmask >> k.fp_id[q]) & 1)) continue;
-      const int64_t cap = s.xf[(XF_ALLOC + q) * s.stride + i];
-      int64_t req = s.xf[(XF_REQ + q) * s.stride + i] + p.xreq[q];
+      const int64_t cap = xa[q];
+      int64_t req = xr[q] + p.xreq[q];
       int64_t sc = 0;
       if ((k.fp_most >> q) & 1) {  // mostRequestedScore (:35-44)
         if (req > cap) req = cap;
@@ -1888,15 +1890,26 @@ __device__ __forceinline__ int32_t ext_score(const SoA& s, int64_t i, const DevP
     t += k.wp_fp * (int32_t)(ws == 0 ? 100 : ns / ws);
   }
   if (k.wp_sra) {  // scarce_resource_avoidance.go:70-90,159-161
-    const uint64_t diff = s.xm[i] & ~p.xmask;
+    const uint64_t diff = xm & ~p.xmask;
     const int nd = __popcll(diff), ni = __popcll(diff & k.sra_mask);
     t += k.wp_sra * ((nd == 0 || ni == 0) ? 100 : (nd - ni) * 100 / nd);
   }
   return t;
 }
+__device__ __forceinline__ int32_t ext_score(const SoA& s, int64_t i, const DevPod& p, const KArgs& k) {
+  int64_t xa[4], xr[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    xa[q] = q < k.fp_n ? s.xf[(XF_ALLOC + q) * s.stride + i] : 0;
+    xr[q] = q < k.fp_n ? s.xf[(XF_REQ + q) * s.stride + i] : 0;
+  }
+  return ext_score_vals(s.xm[i], xa, xr, p, k);
+}
 // Reserve: NodeInfo (NonZero)Requested += the pod's requests of the FitPlus resources
 __device__ __forceinline__ void ext_reserve(const SoA& s, int64_t i, const DevPod& p, const KArgs& k) {
-  for (int q = 0; q < k.fp_n && q < 4; q++) s.xf[(XF_REQ + q) * s.stride + i] += p.xreq[q];
+#pragma unroll
+  for (int q = 0; q < 4; q++)
+    if (q < k.fp_n) s.xf[(XF_REQ + q) * s.stride + i] += p.xreq[q];
 }
 
 template <bool DS, bool NUMA, bool DEFER = false, bool FB_AFF = false, bool CPU = false>
@@ -2290,7 +2303,20 @@ struct NodeFast {
   int64_t amp_room;   // filterAmplifiedCPUs passes iff req0 <= amp_room (THR_NONE = no check)
   uint32_t bits;      // sbits + the `now`-dependent FB bits
   bool thr_node;      // the LoadAware filter thresholds apply (metric, not expired-filtered, NodeMetric set)
+  // NodeResourcesFitPlus / ScarceResourceAvoidance (AF_EXT): the node's ext SoA words (ext_load)
+  uint64_t xm;
+  int64_t xa[4], xr[4];
 };
+
+// the node's ext words (sc1: a Reserve kernel of this or a concurrent launch may have written them)
+__device__ __forceinline__ void ext_load(const SoA& s, int64_t node, const KArgs& k, NodeFast& f) {
+  f.xm = (uint64_t)ld_sc1(reinterpret_cast<const int64_t*>(s.xm) + node);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    f.xa[q] = q < k.fp_n ? ld_sc1(s.xf + (XF_ALLOC + q) * s.stride + node) : 0;
+    f.xr[q] = q < k.fp_n ? ld_sc1(s.xf + (XF_REQ + q) * s.stride + node) : 0;
+  }
+}
 
 // the record of a prepared row (rcap / ralloc set), static bits from the args
 __device__ __forceinline__ void rec_from_regs(const NodeRegs& n, const KArgs& k, int64_t (&w)[NUM_RW]) {
@@ -2474,6 +2500,7 @@ __device__ __forceinline__ int32_t div100_d(double x, double dc, double rc) {
 
 // lite_total(n, expired, p, k) from the node's record (fast_adopt'ed, current).  `estd` / `reqd`: the
 // pod's estimate / requests as doubles.
+template <bool EXT = true>
 __device__ __forceinline__ int32_t fast_total(const NodeFast& f, const DevPod& p, const double (&estd)[2],
                                               const double (&reqd)[2], const KArgs& k) {
   const uint32_t b = f.bits, pf = p.flags;
@@ -2519,7 +2546,10 @@ __device__ __forceinline__ int32_t fast_total(const NodeFast& f, const DevPod& p
   }
   const int32_t la = (b & FB_LAS) ? div_small(sl, k.wsum_la) : 0;
   const int32_t nu = (!zero & (f.nws > 0)) ? div_small(sn, f.nws) : 0;
-  return fail ? -1 : k.wp_la * la + k.wp_numa * nu;
+  if (fail) return -1;
+  int32_t tot = k.wp_la * la + k.wp_numa * nu;
+  if (EXT && (k.flags & AF_EXT)) tot += ext_score_vals(f.xm, f.xa, f.xr, p, k);
+  return tot;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2641,7 +2671,7 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_parity_finalize(int n_nodes, KAr
 // (always alone in its batch) also dsraw[node] = raw DeviceShare score + 1 (0 when filtered out).
 // Nodes [lo, hi) of the SoA (this rank's shard); scores stay indexed by the global node index.
 // DS: the batch's pod is a DeviceShare pod (the DeviceShare path stays out of plain batches' code).
-template <bool DS, bool NUMA, bool CPU>
+template <bool DS, bool NUMA, bool CPU, bool EXT = false>
 __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi, const DevPod* __restrict__ pods,
                                                            const int32_t* __restrict__ batch_base, int batch_pods,
                                                            int pods_per_block, KArgs k, uint16_t* __restrict__ scores,
@@ -2668,7 +2698,9 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
   for (int p = p0; p < p1; p++) {
     const DevPod& pod = pods[base + p];
     if constexpr (!DS && !NUMA && !CPU) {  // plain batch: straight-line evaluation
-      scores[(int64_t)p * score_stride + i] = (uint16_t)(lite_total(n, expired, pod, k) + 1);
+      int32_t tot = lite_total(n, expired, pod, k);
+      if (EXT && tot >= 0) tot += ext_score(s, i, pod, k);  // FitPlus / SRA: its own variant
+      scores[(int64_t)p * score_stride + i] = (uint16_t)(tot + 1);
       continue;
     }
     const EvalOut o = eval_pair<DS, NUMA, NUMA, false, CPU>(n, expired, pod, k, s, i, nv);
@@ -3304,7 +3336,8 @@ __device__ __forceinline__ bool wait_at_least(const int32_t* flag, int32_t want,
 // The touched nodes come as the Reserve kernel's compact list of the rows batch b-1 changed (distinct
 // nodes, the node index in Row.pad), so no row gather depends on a node id read after the wait.
 
-__global__ __launch_bounds__(FIX_BLOCK) void k_fixup(const DevPod* __restrict__ pods,
+template <bool EXT>
+__global__ __launch_bounds__(FIX_BLOCK) void k_fixup(SoA s, const DevPod* __restrict__ pods,
                                                      const int32_t* __restrict__ batch_base, KArgs k,
                                                      const uint32_t* __restrict__ stale,
                                                      const int32_t* __restrict__ stale_cnt,
@@ -3337,6 +3370,7 @@ __global__ __launch_bounds__(FIX_BLOCK) void k_fixup(const DevPod* __restrict__ 
     const int64_t* rp = trows + (int64_t)(t - KSTALE) * NUM_RW;
     rec_load<__HIP_MEMORY_SCOPE_AGENT>(rp, n);
     node = (int)ld_sc1(rp + RW_PAD);
+    if (EXT && (k.flags & AF_EXT)) ext_load(s, node, k, n);  // written by batch b-1's Reserve before its done flag
     s_tn[t - KSTALE] = node;
   }
   __syncthreads();
@@ -3348,7 +3382,7 @@ __global__ __launch_bounds__(FIX_BLOCK) void k_fixup(const DevPod* __restrict__ 
   } else if (node >= 0) {
     fast_adopt(n, k);
     const double estd[2] = {(double)pod.est[0], (double)pod.est[1]}, reqd[2] = {(double)pod.req[0], (double)pod.req[1]};
-    key = make_key(fast_total(n, pod, estd, reqd, k), node);
+    key = make_key(fast_total<EXT>(n, pod, estd, reqd, k), node);
   }
   reinterpret_cast<uint32_t*>(s_k)[t] = key;
   const int nz = __syncthreads_count(key != 0u);
@@ -3435,7 +3469,7 @@ __device__ __forceinline__ ChgSet chg_init(ResLds& L, uint32_t* glb, int n_nodes
   return ChgSet{L.chg, glb};
 }
 
-template <bool DS, bool NUMA, bool QUOTA>
+template <bool DS, bool NUMA, bool QUOTA, bool EXT>
 __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const SoA& s, const int base, const int B,
                                              const KArgs& k, int32_t* __restrict__ chosen,
                                              int32_t* __restrict__ chosen_score, int32_t global_offset,
@@ -3446,7 +3480,7 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
 
 // One batch: prologue on every thread of the workgroup (the batch's pods and exact candidate lists
 // into LDS), replay on wave 0 (the other waves skip it).
-template <bool DS, bool NUMA, bool QUOTA>
+template <bool DS, bool NUMA, bool QUOTA, bool EXT = true>
 __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const SoA& s, const DevPod* __restrict__ pods,
                                               const int base, const int B, const KArgs& k,
                                               const uint32_t* __restrict__ cand, const int32_t* __restrict__ cand_cnt,
@@ -3492,7 +3526,7 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
   if (tid >= 64) return;  // the replay is one wavefront: wave-level ordering only from here on
   // the next batch's eval waves may share this SIMD (pipelined schedule): the replay issues first
   __builtin_amdgcn_s_setprio(3);
-  replay_batch<DS, NUMA, QUOTA>(L, C, s, base, B, k, chosen, chosen_score, global_offset, stamps, batch_index,
+  replay_batch<DS, NUMA, QUOTA, EXT>(L, C, s, base, B, k, chosen, chosen_score, global_offset, stamps, batch_index,
                                 dev_alloc, numa_alloc, touched_out, touched_cnt, pstamps + 8 * batch_index);
   __builtin_amdgcn_s_setprio(0);
 }
@@ -3506,7 +3540,7 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
 //   fetched from the SoA by the next free lane at the start of the pod, into spare registers, so its
 //   latency hides under the re-evaluation; it becomes that lane's row if bu wins.  Pod j+1's record
 //   and candidates are read during pod j, its changed flags right after pod j's Reserve.
-template <bool DS, bool NUMA, bool QUOTA>
+template <bool DS, bool NUMA, bool QUOTA, bool EXT>
 __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const SoA& s, const int base, const int B,
                                              const KArgs& k, int32_t* __restrict__ chosen,
                                              int32_t* __restrict__ chosen_score, int32_t global_offset,
@@ -3552,7 +3586,10 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
     const uint32_t bu = wave_max_u32(chg ? 0u : ck);  // best unchanged snapshot candidate
     RPROF(0)
     if (bu != 0 && lane == n_chg) {
-      if constexpr (FAST) rec_load(s.rec + (int64_t)key_node(bu) * NUM_RW, sparef);
+      if constexpr (FAST) {
+        rec_load(s.rec + (int64_t)key_node(bu) * NUM_RW, sparef);
+        if (EXT && (k.flags & AF_EXT)) ext_load(s, key_node(bu), k, sparef);
+      }
       else load_row_sc1(s, key_node(bu), spare);
     }
     n_fetch += bu != 0;
@@ -3577,7 +3614,7 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
           tot += k.wp_ds * ds_norm(o.ds, m0);
         }
       } else {
-        tot = fast_total(fast, pod, estd, reqd, k);
+        tot = fast_total<EXT>(fast, pod, estd, reqd, k);
       }
       kc = make_key(tot, my_node);
     }
@@ -3629,6 +3666,9 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
       if (lane == owner) {
         if constexpr (FAST) {
           fast_reserve(fast, pod, estd, reqd);
+          if (EXT && (k.flags & AF_EXT))  // NodeInfo (NonZero)Requested of the FitPlus resources
+#pragma unroll
+            for (int q = 0; q < 4; q++) fast.xr[q] += q < k.fp_n ? pod.xreq[q] : 0;
         } else {
           if ((mine.flags & NF_HAS_METRIC) && !(mine.flags & NF_NM_NIL)) {
 #pragma unroll
@@ -3722,6 +3762,10 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
       st_sc1(f + (F_NREQ + 0) * st, (int64_t)fast.nreq[0]);
       st_sc1(f + (F_NREQ + 1) * st, (int64_t)fast.nreq[1]);
       rec_store_dyn<__HIP_MEMORY_SCOPE_WORKGROUP>(rec, fast);
+      if (EXT && (k.flags & AF_EXT))
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+          if (q < k.fp_n) st_sc1(s.xf + (XF_REQ + q) * st + my_node, fast.xr[q]);
       if (touched_out) rec_store_full(touched_out + (int64_t)lane * NUM_RW, fast, my_node);
     } else {
 #pragma unroll
@@ -3769,7 +3813,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(SoA s, const De
 // Per batch: wait until k_fixup published every pod's exact list (ready[b] == pods of b), resolve it,
 // then publish done[b] (rows, placements, the changed-row list).  Every wait is bounded
 // (wait_at_least); on a timeout the run stops and the error word tells the host.
-template <bool QUOTA>
+template <bool QUOTA, bool EXT>
 __global__ __launch_bounds__(res_threads<false>()) void k_resolve_run(SoA s, const DevPod* __restrict__ pods,
                                                                       const int32_t* __restrict__ bases, int b0, int nb,
                                                                       KArgs k, const uint32_t* __restrict__ cand,
@@ -3792,7 +3836,7 @@ __global__ __launch_bounds__(res_threads<false>()) void k_resolve_run(SoA s, con
     if (threadIdx.x == 0) s_ok = wait_at_least(ready + b, B, err);
     __syncthreads();
     if (!s_ok) return;
-    resolve_batch<false, false, QUOTA>(L, C, s, pods, base, B, k, cand, cand_cnt, chosen, chosen_score, global_offset,
+    resolve_batch<false, false, QUOTA, EXT>(L, C, s, pods, base, B, k, cand, cand_cnt, chosen, chosen_score, global_offset,
                                        stamps, pstamps, b, dev_alloc, nullptr, touched_out, touched_cnt);
     __syncthreads();  // wave 0 drained its stores (replay_batch), so they are performed
     if (threadIdx.x == 0) st_sc1(done + b, 1);
@@ -4892,7 +4936,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     while (p + bp < n_pods && bp < B) {
       const uint32_t g = d->host_pods[p + bp].flags;
       if ((g & PF_CPUSET) || ((g & PF_DS) && !ds_batch)) break;
-      has_ds = has_ds || (g & PF_DS) || (ctx->ext_enabled && ds_batch);  // FitPlus / SRA: the record-free replay
+      has_ds = has_ds || (g & PF_DS);
       ds_pods = ds_pods || (g & PF_DS);
       bp++;
     }
@@ -5023,7 +5067,9 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
         auto eval = cpu ? (ds ? (numa ? k_eval_batch<true, true, true> : k_eval_batch<true, false, true>)
                               : (numa ? k_eval_batch<false, true, true> : k_eval_batch<false, false, true>))
                         : ds ? (numa ? k_eval_batch<true, true, false> : k_eval_batch<true, false, false>)
-                             : (numa ? k_eval_batch<false, true, false> : k_eval_batch<false, false, false>);
+                             : (numa ? k_eval_batch<false, true, false>
+                                     : ((k.flags & AF_EXT) ? k_eval_batch<false, false, false, true>
+                                                           : k_eval_batch<false, false, false>));
         uint32_t* dcnt = numa ? d->d_defer_cnt + b : nullptr;
         hipLaunchKernelGGL(eval, grid, dim3(eb), 0, es, d->soa, lo, hi, d->d_pods, bbase, bp,
                            ppb, k, d->d_scores, d->capacity, d->d_dsraw, d->d_defer, dcnt, d->d_aff, d->d_dsmax);
@@ -5092,7 +5138,9 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   for (int b = 0; b < n_batches;) {
     if (run_end[b] > 0) {
       const int r0 = b, e = run_end[b];
-      hipLaunchKernelGGL((quota ? k_resolve_run<true> : k_resolve_run<false>), dim3(1), dim3(res_threads<false>()), 0,
+      const bool ext = (k.flags & AF_EXT) != 0;
+      hipLaunchKernelGGL((quota ? (ext ? k_resolve_run<true, true> : k_resolve_run<true, false>)
+                                : (ext ? k_resolve_run<false, true> : k_resolve_run<false, false>)), dim3(1), dim3(res_threads<false>()), 0,
                          d->stream, d->soa, d->d_pods, d_bases, r0, e - r0, k, d->d_cand, d->d_cand_cnt, d->d_chosen,
                          d->d_chosen_score, ctx->cfg.global_node_offset, d->d_stamps, d->d_stamps + (n_pods + 2),
                          d->d_devalloc, d_ready, d_done, d_err, d->d_trows, d->d_tcnt, d->d_chg, N);
@@ -5101,7 +5149,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
         rc = eval_select(q, true, d->estream);
         if (rc) return rc;
         const bool first = q == r0;
-        hipLaunchKernelGGL(k_fixup, dim3((unsigned)batches[q].pods), dim3(FIX_BLOCK), 0, d->estream, d->d_pods,
+        hipLaunchKernelGGL((ext ? k_fixup<true> : k_fixup<false>), dim3((unsigned)batches[q].pods), dim3(FIX_BLOCK), 0, d->estream, d->soa, d->d_pods,
                            d_bases + q, k, d->d_stale + (size_t)(q & 1) * MAX_BATCH * KSTALE,
                            d->d_stale_cnt + (q & 1) * MAX_BATCH, d->d_trows, d->d_tcnt, d->d_cand, d->d_cand_cnt,
                            d_done, first ? -1 : q - 1, d_ready + q, d_err, d_fst + 2 * q);
