@@ -630,7 +630,7 @@ int ke_last_device_allocations(ke_ctx* ctx, int32_t n, uint64_t* minors);
  *    shrinks totalResourceExceptSystemAndDefaultUsed (updateClusterTotalResourceNoLock,
  *    group_quota_manager.go:127-151,268-271) and every later pod of the call sees runtime limits
  *    refreshed from the smaller total.
- * Not modelled: scale-min, guaranteed usage, hook plugins, quota-overuse revocation, preemption
+ * Not modelled: guaranteed usage (feature gate ElasticQuotaGuaranteeUsage, default off), hook plugins, quota-overuse revocation, preemption
  * (PostFilter); a zero-valued pod request counts as an absent key (checkQuotaRecursive masks on
  * ResourceNames(PodRequests), which keeps explicit zeros — ke_pod carries values, not key sets).
  * Resources: cpu (milli, getQuantityValue) and memory (bytes).  Values >= 0. */
@@ -639,7 +639,21 @@ typedef struct ke_quota_args {
   int64_t total[KE_NRES];            /* totalResourceExceptSystemAndDefaultUsed of the tree */
   uint8_t enable_runtime_quota;      /* ElasticQuotaArgs.EnableRuntimeQuota (v1beta3 default true) */
   uint8_t enable_check_parent_quota; /* ElasticQuotaArgs.EnableCheckParentQuota (default false) */
-  uint8_t pad[6];
+  /* 0 (the scheduler's NewGroupQuotaManager: scaleMinQuotaEnabled = true): when the Min of a parent's
+   * children sums above the parent's runtime (the tree total for the root's children) on a resource,
+   * the calculator shares with every child's Min scaled to int64(float64(total) * float64(Min) /
+   * float64(ΣMin)) (ScaleMinQuotaManager.getScaledMinQuota, scale_minquota_when_over_root_res.go:129-184;
+   * refreshRuntimeNoLock :320-328) — the state once every quota has been refreshed at the current
+   * total.  System / default quotas (limit_is_max) stay out of the sums as they stay out of the
+   * sharing.  1: the core package's test manager (Min unscaled). */
+  uint8_t disable_scale_min_quota;
+  /* Not on this path -> ke_quotas_load returns KE_ERR_UNSUPPORTED when set: the number of
+   * ElasticQuotaArgs.HookPlugins (QuotaHookPlugin callbacks, core/hook_plugin.go), and the
+   * ElasticQuotaGuaranteeUsage feature gate (Guaranteed raising the calculator's Min,
+   * group_quota_manager.go:257,1074-1106). */
+  uint8_t n_hook_plugins;
+  uint8_t enable_guarantee_usage;
+  uint8_t pad[3];
 } ke_quota_args;
 typedef struct ke_quota {
   int32_t parent;                 /* index of the parent quota; -1 = koordinator-root-quota */

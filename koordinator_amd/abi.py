@@ -297,7 +297,8 @@ MAX_QUOTAS = 255
 
 class QuotaArgs(C.Structure):
     _fields_ = [("total", i64 * NRES), ("enable_runtime_quota", u8), ("enable_check_parent_quota", u8),
-                ("pad", u8 * 6)]
+                ("disable_scale_min_quota", u8), ("n_hook_plugins", u8),
+                ("enable_guarantee_usage", u8), ("pad", u8 * 3)]
 
 
 class Quota(C.Structure):

@@ -319,6 +319,8 @@ int ke_node_cpus_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_cpu* cpus, i
 
 int ke_quotas_load(ke_ctx* ctx, const ke_quota_args* args, const ke_quota* quotas, int32_t n) {
   if (!ctx || !args || n < 0 || n > KE_MAX_QUOTAS || (n > 0 && !quotas)) return fail(KE_ERR_INVALID, "ke_quotas_load arguments");
+  if (args->n_hook_plugins) return fail(KE_ERR_UNSUPPORTED, "ElasticQuotaArgs.HookPlugins are not supported");
+  if (args->enable_guarantee_usage) return fail(KE_ERR_UNSUPPORTED, "ElasticQuotaGuaranteeUsage is not supported");
   for (int r = 0; r < KE_NRES; r++)
     if (args->total[r] < 0) return fail(KE_ERR_INVALID, "ke_quota_args.total must be >= 0");
   std::vector<ke_quota> q(quotas, quotas + n);

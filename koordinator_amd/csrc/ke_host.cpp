@@ -1087,9 +1087,21 @@ int quota_compute_limits(const ke_quota_args& args, const std::vector<ke_quota>&
     }
     auto share_children = [&](int p, int64_t total) {
       std::vector<QuotaShare*> ks;
+      int64_t min_sum = 0;
       for (int c : kids[p])
-        if (!q[c].limit_is_max) ks.push_back(&sh[c]);
-      if (!ks.empty()) share_runtime(total, ks);
+        if (!q[c].limit_is_max) {
+          ks.push_back(&sh[c]);
+          min_sum += sh[c].min;
+        }
+      if (ks.empty()) return;
+      // scale-min (scale_minquota_when_over_root_res.go:129-184): the children's Min sum exceeds what
+      // the parent shares -> the calculator's AutoScaleMin is each Min's share of `total`
+      if (!args.disable_scale_min_quota && total < min_sum)
+        for (QuotaShare* c : ks)
+          c->min = total <= 0 ? 0
+                              : static_cast<int64_t>(static_cast<double>(total) * static_cast<double>(c->min) /
+                                                     static_cast<double>(min_sum));
+      share_runtime(total, ks);
     };
     share_children(n, args.total[r]);
     for (int i : order) share_children(i, sh[i].runtime);

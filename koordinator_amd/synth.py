@@ -705,11 +705,12 @@ def make_quota_tree(seed, n_leaves=64, fanout=8, total_cpu=None, total_mem=None,
     return q
 
 
-def quota_args(total_cpu, total_mem, runtime=True, check_parent=False):
+def quota_args(total_cpu, total_mem, runtime=True, check_parent=False, scale_min=True):
     a = abi.QuotaArgs()
     a.total[0], a.total[1] = total_cpu, total_mem
     a.enable_runtime_quota = 1 if runtime else 0
     a.enable_check_parent_quota = 1 if check_parent else 0
+    a.disable_scale_min_quota = 0 if scale_min else 1
     return a
 
 

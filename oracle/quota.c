@@ -93,7 +93,7 @@ int orq_load(or_quotas* Q, const ke_quota_args* args, const ke_quota* q, int32_t
     for (int i = 0; i < n; i++) {
       child[i] = q[i].self_request[r];
       w[i] = q[i].shared_weight[r];
-      mn[i] = q[i].has_min[r] ? q[i].min[r] : 0; /* AutoScaleMin = Min (no scale-min), guarantee 0 */
+      mn[i] = q[i].has_min[r] ? q[i].min[r] : 0; /* AutoScaleMin = Min until scaled below; guarantee 0 */
       lent[i] = q[i].allow_lent_resource;
       rt[i] = 0;
     }
@@ -113,10 +113,22 @@ int orq_load(or_quotas* Q, const ke_quota_args* args, const ke_quota* q, int32_t
       for (int p = -1; p < n; p++) {
         if ((p < 0 ? 0 : depth[p] + 1) != d) continue;
         int k = 0;
+        int64_t min_sum = 0;
         for (int i = 0; i < n; i++)
-          if (q[i].parent == p && !q[i].limit_is_max) ids[k++] = i;
+          if (q[i].parent == p && !q[i].limit_is_max) {
+            ids[k++] = i;
+            min_sum += mn[i];
+          }
         if (k == 0) continue;
-        redistribute(p < 0 ? args->total[r] : rt[p], ids, k, w, limreq, mn, lent, rt);
+        const int64_t total = p < 0 ? args->total[r] : rt[p];
+        /* ScaleMinQuotaManager.getScaledMinQuota (scale_minquota_when_over_root_res.go:129-184), every
+         * child scale-enabled (UpdateQuota passes scaleMinQuotaEnabled, group_quota_manager.go:604):
+         * total < ΣMin -> AutoScaleMin = int64(float64(total) * float64(Min) / float64(ΣMin)), 0 when
+         * total <= 0; refreshRuntimeNoLock applies it before the parent's calculator shares (:320-333) */
+        if (!args->disable_scale_min_quota && total < min_sum)
+          for (int j = 0; j < k; j++)
+            mn[ids[j]] = total <= 0 ? 0 : (int64_t)((double)total * (double)mn[ids[j]] / (double)min_sum);
+        redistribute(total, ids, k, w, limreq, mn, lent, rt);
       }
     }
     /* Runtime carries every resource key of the tree (updateOneGroupRuntimeQuota over resourceKeys =

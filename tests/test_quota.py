@@ -32,6 +32,24 @@ def limits(handle, qs, total_cpu, runtime=True, check_parent=False):
     return [int(handle.quota_state(i)["limit"][0]) for i in range(len(qs))]
 
 
+GB = 1024 * 1048576  # group_quota_manager_test.go:43 GigaByte
+
+
+def quota2(parent, max_c, max_gb, min_c, min_gb, req_c=0, req_gb=0, lent=True):
+    """AddQuotaToManager (group_quota_manager_test.go:1144-1169): cpu in cores, memory in GiB; shared
+    weight = Max; self request in cores / GiB."""
+    q = np.zeros(1, abi.QUOTA_DTYPE)[0]
+    q["parent"] = parent
+    q["has_max"] = (1, 1)
+    q["max"] = (max_c * M, max_gb * GB)
+    q["has_min"] = (1, 1)
+    q["min"] = (min_c * M, min_gb * GB)
+    q["shared_weight"] = q["max"]
+    q["self_request"] = (req_c * M, req_gb * GB)
+    q["allow_lent_resource"] = 1 if lent else 0
+    return q
+
+
 def handles():
     cfg = abi.default_config(4)
     return [Oracle(cfg, 4), Evaluator(cfg)]
@@ -68,6 +86,29 @@ def test_not_allow_lent_tree_golden(root_lent, child2_lent, phases):
             assert limits(h, qs, 100 * M) == [w * M for w in want], (req, type(h).__name__)
 
 
+# group_quota_manager_test.go:794-862 TestGroupQuotaManager_MultiUpdateQuotaRequest_WithScaledMinQuota1 and
+# :866-912 _WithScaledMinQuota2 (gqm.scaleMinQuotaEnabled = true, as NewGroupQuotaManager sets it): parent p
+# (min 300 cores / 300 GiB) under the root, children a, b, c (min 100 / 100 each) requesting 200 / 200 (b 0 in
+# _2); the runtimes once every quota was refreshed at the cluster total, [p, a, b, c] as (milli-cpu, bytes)
+@pytest.mark.parametrize("b_req,total,want", [
+    (200, 200, [(200 * M, 200 * GB)] + [(66667, 200 * GB // 3 + 1)] * 3),
+    (200, 600, [(600 * M, 600 * GB)] + [(200 * M, 200 * GB)] * 3),
+    (0, 200, [(200 * M, 200 * GB), (100 * M, 100 * GB), (0, 0), (100 * M, 100 * GB)]),
+], ids=["scaled_min_1", "scaled_min_1_large", "scaled_min_2"])
+def test_scaled_min_quota_golden(b_req, total, want):
+    qs = np.array([quota2(-1, 1000, 1000, 300, 300), quota2(0, 1000, 1000, 100, 100, 200, 200),
+                   quota2(0, 1000, 1000, 100, 100, b_req, b_req), quota2(0, 1000, 1000, 100, 100, 200, 200)],
+                  abi.QUOTA_DTYPE)
+    for h in handles():
+        h.quotas_load(synth.quota_args(total * M, total * GB), qs)
+        got = [tuple(int(v) for v in h.quota_state(i)["limit"]) for i in range(4)]
+        assert got == want, type(h).__name__
+        # the core package's test manager (scale-min off): a, b, c keep Min 100 and the 200 are not enough
+        h.quotas_load(synth.quota_args(total * M, total * GB, scale_min=False), qs)
+        if total == 200 and b_req:
+            assert [int(h.quota_state(i)["limit"][0]) for i in range(1, 4)] == [100 * M] * 3
+
+
 def test_host_runtime_matches_oracle_random_trees():
     """The product's C++ runtime (ke_quotas_load) equals the oracle's restatement on random trees."""
     rng = np.random.default_rng(7)
@@ -87,7 +128,7 @@ def test_host_runtime_matches_oracle_random_trees():
             q[i]["allow_lent_resource"] = rng.random() < 0.7
             q[i]["limit_is_max"] = rng.random() < 0.05
         args = synth.quota_args(int(rng.integers(0, 100_000)), int(rng.integers(0, 100_000)),
-                                runtime=rng.random() < 0.9)
+                                runtime=rng.random() < 0.9, scale_min=rng.random() < 0.7)
         o.quotas_load(args, q)
         ev.quotas_load(args, q)
         for i in range(n):
@@ -164,3 +205,18 @@ def test_default_quota_reserve_shrinks_runtime_total():
         assert np.array_equal(got, ref.quota_state(i)["limit"]), i
         changed += not np.array_equal(got, before[i])
     assert changed > 0
+
+
+@pytest.mark.parametrize("field", ["n_hook_plugins", "enable_guarantee_usage"])
+def test_quota_args_outside_the_path_refused(field):
+    """ElasticQuotaArgs.HookPlugins and the ElasticQuotaGuaranteeUsage gate change the runtime the reference
+    computes; the boundary refuses them instead of ignoring them."""
+    from koordinator_amd.evaluator import KoordEvalError
+
+    args = synth.quota_args(100 * M, 100 * GB)
+    setattr(args, field, 1)
+    ev = Evaluator(abi.default_config(4))
+    with pytest.raises(KoordEvalError) as e:
+        ev.quotas_load(args, np.array([quota(-1, 10 * M)], abi.QUOTA_DTYPE))
+    assert e.value.code == abi.ERR_UNSUPPORTED
+    ev.close()
