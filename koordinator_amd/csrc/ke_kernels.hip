@@ -269,6 +269,9 @@ struct DsInst {
   uint32_t th, fh;  // key presence of total / free'
   bool used_nz;     // used' kept (non-zero): the minor is in getRealUsed (allocator_gpu.go:59-70)
 };
+#ifndef KE_DS_GRP
+#define KE_DS_GRP 2
+#endif
 // the instance's total / used words (0 for absent keys), loaded ahead of their use (ds_type_view issues a
 // group of instances' loads together: one memory round trip per group instead of per instance)
 struct DsRaw {
@@ -678,7 +681,7 @@ __device__ __forceinline__ bool ds_type_view(const SoA& s, int64_t i, int t, con
   bool present = false;
 #pragma unroll
   for (int q = 0; q < 3; q++) tot[q] = fre[q] = 0;
-  constexpr int GRP = 2;  // instances whose words are loaded together
+  constexpr int GRP = KE_DS_GRP;  // instances whose words are loaded together
   while (ex) {
     int ms[GRP];
     DsRaw raw[GRP];
