@@ -3455,6 +3455,93 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// DeviceShare Reserve of node i on the whole wave, lane m = minor m (ds_reserve spreads nothing: one lane
+// walks every instance, scores it and updates it in turn).  The default-allocation case: a node without
+// partition table / honor policy / topology tree and a pod without partition spec or required scope, no NUMA
+// affinity -- GPUAllocator.Allocate then reduces to defaultAllocateDevices on the instances that fit
+// (allocator_gpu.go; device_allocator.go:237-300), other types too.  The same instance views, scores,
+// picks (highest scoreDevice, ties to the lower minor) and quotav1.Add of the allocation as ds_reserve;
+// anything else goes to ds_reserve on lane 0.  Wave-uniform i / p; returns the minors mask on every lane.
+__device__ __forceinline__ uint64_t ds_reserve_wave(const SoA& s, int64_t i, const DevPod& p, const KArgs& k,
+                                                    int lane) {
+  uint64_t msk[4], out = 0;
+#pragma unroll
+  for (int w = 0; w < 4; w++) msk[w] = dsmask(s, w, i);
+  if ((msk[DSM_EXISTS] & (DSX_TOPO | DSX_TABLE | DSX_HONOR)) || (p.flags & (PF_GPU_PART_SPEC | 7u * PF_GPU_SCOPE0))) {
+    if (lane == 0) out = ds_reserve(s, i, p, k, DsAff{false, 0u});
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(out >> 32), 0) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)out, 0);
+  }
+  const int m = lane & (DS_MINORS - 1);
+  for (int t = 0; t < 3; t++) {
+    if (!p.ds_cnt[t]) continue;
+    const int nk = DS_NK[t];
+    const uint32_t ex = (uint32_t)(msk[DSM_EXISTS] >> (16 * t)) & 0xFFFFu;
+    const bool inst = lane < DS_MINORS && ((ex >> m) & 1u);
+    DsRaw raw;
+    bool fit = false;
+    uint32_t key = 0;  // 1 + (scoreDevice << 4 | 15 - m) for an instance defaultAllocateDevices may take
+    if (inst) {
+      ds_load(s, i, t, m, msk, raw);
+      DsInst d;
+      ds_instance_from(raw, t, m, msk, d);
+      fit = !ds_free_zero(d) && ds_leq(d, p, t);
+      if (fit) {
+        int64_t tv[3], fv[3];
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+          tv[q] = ((d.th >> q) & 1) ? d.tv[q] : 0;
+          fv[q] = ((d.fh >> q) & 1) ? d.fv[q] : 0;
+        }
+        const int64_t sc = ds_weighted(k, t, tv, fv, p);  // in [0, MaxNodeScore]
+        key = 1u + (((uint32_t)sc << 4) | (uint32_t)(DS_MINORS - 1 - m));
+      }
+    }
+    const uint32_t ok = (uint32_t)__ballot(fit) & 0xFFFFu;
+    const int want = p.ds_cnt[t];
+    uint32_t take = 0;
+    // GPUAllocator: "Insufficient GPU devices" takes nothing (Reserve follows a passed Filter); other types
+    // take what fits, up to the count
+    if (t != KE_DEV_GPU || __builtin_popcount(ok) >= want)
+      for (int c = 0; c < want && (ok & ~take); c++) {
+        const uint32_t best = wave_max_u32(((take >> m) & 1u) ? 0u : key);
+        take |= 1u << (DS_MINORS - 1 - (int)((best - 1u) & 15u));
+      }
+    out |= (uint64_t)take << (16 * t);
+    const bool mine = inst && ((take >> m) & 1u);
+    int64_t alloc[3] = {0, 0, 0};
+    bool has[3] = {false, false, false};
+    if (t == KE_DEV_GPU) {
+      const int64_t tm = raw.tv[1];  // the instance's total memory (0 without the key)
+      if (p.flags & PF_DS_H_CORE) has[0] = true, alloc[0] = p.ds_req[0];
+      if (p.flags & PF_DS_H_RATIO) {  // memoryRatioToBytes
+        has[2] = true, alloc[2] = p.ds_req[2];
+        has[1] = true, alloc[1] = mine ? p.ds_req[2] * tm / 100 : 0;
+      } else if (p.flags & PF_DS_H_MEM) {  // memoryBytesToRatio: int64(float64(b)/float64(total)*100)
+        has[1] = true, alloc[1] = p.ds_req[1];
+        has[2] = true, alloc[2] = mine ? (int64_t)((double)p.ds_req[1] / (double)tm * 100.0) : 0;
+      }
+    } else {
+      has[0] = true, alloc[0] = p.ds_req[2 + t];
+    }
+    const int w = ds_hu_word(t);
+#pragma unroll
+    for (int key_i = 0; key_i < 3; key_i++) {
+      if (key_i >= nk || !has[key_i]) continue;
+      if (mine) {
+        const int field = DS_UBASE[t] + m * nk + key_i;
+        s.ds[field * s.stride + i] = raw.uv[key_i] + alloc[key_i];  // quotav1.Add (absent used key: 0)
+      }
+      msk[w] |= (uint64_t)take << ds_hu_bit(t, 0, key_i);
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int w = 1; w < 4; w++) s.dsm[w * s.stride + i] = msk[w];
+  }
+  return out;
+}
+
 struct ResLds {
   uint32_t cand[MAX_BATCH * KMAX];
   DevPod pod[MAX_BATCH];
@@ -3666,6 +3753,13 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
       // Reserve: LoadAware assign (the new pod has no PodMetric -> counted at its estimate in every
       // non-prod term, and in the prod terms when it is prod), NodeInfo.Requested += requests.
       uint64_t al = 0;
+      if (DS && (pod.flags & PF_DS)) {  // DeviceShare Reserve (wave-uniform branch), before NodeNUMAResource's
+        const uint32_t nfl = (uint32_t)__builtin_amdgcn_readlane((int)(FAST ? fast.nflags : mine.flags), owner);
+        const int node = (int)key_node(w);  // the chosen node (my_node of the owner lane)
+        // the device SoA is global: a later pod of the batch re-evaluating this node reads it back
+        // (wave_lds_sync below)
+        if (nfl & NF_DS_CACHE) al = ds_reserve_wave(s, node, pod, k, lane);
+      }
       if (lane == owner) {
         if constexpr (FAST) {
           fast_reserve(fast, pod, estd, reqd);
@@ -3690,8 +3784,6 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
         if (!FAST && (k.flags & AF_EXT)) ext_reserve(s, my_node, pod, k);  // read back by the next re-evaluations
         // DeviceShare Reserve (the device SoA is global: a later pod of the batch re-evaluating this node
         // reads it back, wave_lds_sync below)
-        const uint32_t nfl = FAST ? fast.nflags : mine.flags;
-        al = DS && (pod.flags & PF_DS) && (nfl & NF_DS_CACHE) ? ds_reserve(s, my_node, pod, k, DsAff{false, 0u}) : 0ull;
         if (NUMA) {  // NodeNUMAResource Reserve: the zones of a NUMA-policy node
           int64_t* out16 = numa_alloc + (int64_t)(base + j) * 16;
           const int pol = pf_numa_policy(pod.flags) ? pf_numa_policy(pod.flags) : nf_numa_policy(mine.flags);
