@@ -748,6 +748,7 @@ __device__ int ds_try_allocate(const SoA& s, int64_t i, const DevPod& p, const K
       return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
     }
   if (gpu) *gpu = 0;
+#pragma unroll
   for (int t = 0; t < 3; t++) {
     if (!p.ds_cnt[t]) continue;
     GpuMasks g;
@@ -791,6 +792,7 @@ __device__ __noinline__ void ds_filter_score(const SoA& s, int64_t i, const DevP
   // spec or required scope, go straight to defaultAllocateDevices: only its count is needed
   const bool gpu_default = !(msk[DSM_EXISTS] & (DSX_TOPO | DSX_TABLE | DSX_HONOR)) &&
                            !(p.flags & (PF_GPU_PART_SPEC | 7u * PF_GPU_SCOPE0));
+#pragma unroll  // the type as a constant: key counts, field bases and mask bits fold per instance
   for (int t = 0; t < 3; t++) {
     if (!p.ds_cnt[t]) continue;
     GpuMasks g;
@@ -3473,6 +3475,7 @@ __device__ __forceinline__ uint64_t ds_reserve_wave(const SoA& s, int64_t i, con
            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)out, 0);
   }
   const int m = lane & (DS_MINORS - 1);
+#pragma unroll
   for (int t = 0; t < 3; t++) {
     if (!p.ds_cnt[t]) continue;
     const int nk = DS_NK[t];
