@@ -774,7 +774,7 @@ __device__ int ds_try_allocate(const SoA& s, int64_t i, const DevPod& p, const K
 // Filter (Prepare + per-type allocation feasibility) and raw Score of DeviceShare for a pod with PF_DS on
 // a node with a cache entry.  `a`: the affinity the topology manager stored (Score and Reserve read it;
 // Filter then passes: topology_hint.go Allocate already ran).  Types in the fixed order GPU, RDMA, FPGA.
-__device__ __noinline__ void ds_filter_score(const SoA& s, int64_t i, const DevPod& p, const KArgs& k, EvalOut& o,
+__device__ __forceinline__ void ds_filter_score(const SoA& s, int64_t i, const DevPod& p, const KArgs& k, EvalOut& o,
                                              bool stored, DsAff a) {
   uint64_t msk[4];
 #pragma unroll
