@@ -283,12 +283,8 @@ __device__ __forceinline__ void ds_load(const SoA& s, int64_t i, int t, int m, c
   for (int k = 0; k < 3; k++) {
     const bool ht = k < nk && ((msk[ds_ht_word(t)] >> ds_ht_bit(t, m, k)) & 1);
     const bool hu = k < nk && ((msk[ds_hu_word(t)] >> ds_hu_bit(t, m, k)) & 1);
-    // unconditional loads (every field of the node's device SoA column exists), the key bits select after:
-    // no exec-mask split per load, and the group's loads issue back to back
-    const int64_t tv = k < nk ? dsf(s, DS_TBASE[t] + m * nk + k, i) : 0;
-    const int64_t uv = k < nk ? dsf(s, DS_UBASE[t] + m * nk + k, i) : 0;
-    r.tv[k] = ht ? tv : 0;
-    r.uv[k] = hu ? uv : 0;
+    r.tv[k] = ht ? dsf(s, DS_TBASE[t] + m * nk + k, i) : 0;
+    r.uv[k] = hu ? dsf(s, DS_UBASE[t] + m * nk + k, i) : 0;
   }
 }
 __device__ __forceinline__ void ds_instance_from(const DsRaw& r, int t, int m, const uint64_t msk[4], DsInst& d) {
