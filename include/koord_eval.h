@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define KE_ABI_VERSION 5
+#define KE_ABI_VERSION 6
 #define KE_ABSENT (-1)
 
 /* ---- error codes ---------------------------------------------------------------------------- */
@@ -239,7 +239,12 @@ typedef struct ke_numa_zone {
   int64_t capacity[KE_NRES];   /* cpu milli, memory bytes (before amplification) */
   int64_t allocated[KE_NRES];  /* Σ NUMANodeResources of the pods allocated on the zone */
   int32_t cpuset_cpus;         /* cpuset CPUs allocated in the zone (allocatedCPUs.CPUsInNUMANodes) */
-  int32_t pad2;
+  /* len(NodeAllocation.singleNUMANode[id]) / len(sharedNode[id]): the cpuset pods whose CPUs lie only in
+   * this zone / in several zones including it.  The status is Shared when shared_pods > 0, else Single
+   * when single_pods > 0, else Idle (NUMANodeSharedStatus).  Both 0 with numa_status Single / Shared
+   * counts as one such pod.  A release (ke_pod_release) of a cpuset pod removes it from these sets. */
+  int16_t single_pods;
+  int16_t shared_pods;
 } ke_numa_zone; /* 48 bytes */
 
 /* ---- DeviceShare (pkg/scheduler/plugins/deviceshare) ------------------------------------------ */
@@ -505,7 +510,7 @@ const char* ke_last_error(void);
 int ke_abi_version(void);
 /* sizeof() of ke_config, ke_node, ke_node_metric, ke_pod_metric, ke_aggregated_usage, ke_pod,
  * ke_resource_map, ke_loadaware_args, ke_numa_args, ke_deviceshare_args, ke_device, ke_numa_zone, ke_cpu,
- * ke_quota_args, ke_quota, ke_gpu_partition, ke_ext_args, ke_node_resource (in that order) for binding-layout
+ * ke_quota_args, ke_quota, ke_gpu_partition, ke_ext_args, ke_node_resource, ke_pod_allocation (in that order) for binding-layout
  * checks. */
 int ke_abi_struct_sizes(int32_t* sizes, int32_t n);
 /* 1 if this build has a usable HIP device and its gfx950 kernels loaded, else 0. */
@@ -613,6 +618,48 @@ int ke_last_schedule_stats(ke_ctx* ctx, double* total_ms, int32_t* n_batches,
 /* DeviceShare Reserve of the last ke_schedule (AutopilotAllocator.Allocate -> updateCacheUsed,
  * plugin.go:426-492): per pod, bit 16*type + minor set for every device instance allocated. */
 int ke_last_device_allocations(ke_ctx* ctx, int32_t n, uint64_t* minors);
+
+/* ---- Unreserve and pod release (ReservePlugin.Unreserve, pod informer deletes) -------------------
+ * What one placement reserved, as the plugins keep it in CycleState / their caches:
+ *   cpuset, numa     NodeNUMAResource PodAllocation.CPUSet / NUMANodeResources (state.allocation,
+ *                    nodenumaresource/plugin.go:564-565; node_allocation.go:42-49)
+ *   device_minors    DeviceShare state.allocationResult (deviceshare/plugin.go:491): the instances; the
+ *                    amounts are the pod's per-instance request (what Reserve added, fillGPUTotalMem)
+ *   quota_assigned   ElasticQuota: the pod's request is counted in its quota's used (ReservePod ran)
+ * node = the node index ke_schedule returned (global index when sharded), -1 = not placed. */
+typedef struct ke_pod_allocation {
+  int32_t node;
+  uint8_t quota_assigned;
+  uint8_t pad[3];
+  uint64_t cpuset[4];                   /* bit c = CPU id c (ke_last_cpusets)                 */
+  int64_t numa[KE_MAX_NUMA * KE_NRES];  /* [2*id + r] per NUMA id (ke_last_numa_allocations) */
+  uint64_t device_minors;               /* bit 16*type + minor (ke_last_device_allocations)   */
+} ke_pod_allocation; /* 176 bytes */
+/* ke_pod_release modes */
+#define KE_RELEASE_UNRESERVE 0 /* the framework's Unreserve of every Reserve plugin + ForgetPod:
+                                  loadaware podAssignCache.unAssign (load_aware.go:197-199),
+                                  nodenumaresource resourceManager.Release (plugin.go:569-577,
+                                  node_allocation.go:158-190), deviceshare updateCacheUsed(..., false)
+                                  (plugin.go:498-516, device_cache.go:132-209), elasticquota UnreservePod
+                                  (plugin.go:361, group_quota_manager.go:965-981), NodeInfo.RemovePod */
+#define KE_RELEASE_DELETE 1    /* informer delete of an assigned pod: the same, and the quota also drops the
+                                  pod's request (OnPodDelete, group_quota_manager.go:922-941;
+                                  nodenumaresource pod_eventhandler.go:99-144, deviceshare
+                                  eventhandler_pod.go:89-131) */
+/* Each placement of the last ke_schedule as a release record (node -1 for an unplaced pod). */
+int ke_last_allocations(ke_ctx* ctx, int32_t n, ke_pod_allocation* out);
+/* Release `pod` from alloc->node: every plugin's state and the node's NodeInfo.Requested (and the
+ * NodeResourcesFitPlus requested of its resources) lose exactly what its Reserve added, with the
+ * reference's non-negative subtraction (quotav1.SubtractWithNonNegativeResult for NUMA zones and device
+ * used, a device whose used becomes zero drops its used keys; RefCount-- per CPU, the CPU leaving the
+ * allocation at 0; the zones' single / shared pod sets; quota used / non-preemptible used of the quota
+ * and every ancestor clamped at 0, a system / default quota growing the tree total back).  Release each
+ * placement at most once.  alloc->node == -1 with KE_RELEASE_DELETE removes only the quota request. */
+int ke_pod_release(ke_ctx* ctx, const ke_pod* pod, const ke_pod_allocation* alloc, int32_t mode);
+/* Unreserve of the pod at `queue_pos` of the last ke_schedule call (pod->uid must match): ke_pod_release
+ * with the record ke_last_allocations reports, KE_RELEASE_UNRESERVE.  A second call for the same
+ * position, or for an unplaced pod, is a no-op. */
+int ke_unreserve(ke_ctx* ctx, const ke_pod* pod, int32_t queue_pos);
 
 /* ---- ElasticQuota admission (pkg/scheduler/plugins/elasticquota) ----------
  * One quota tree.  Replaces GroupQuotaManager's runtime calculation and the plugin's PreFilter /
@@ -795,6 +842,12 @@ int ke_debug_rows(ke_ctx* ctx, int32_t n, int64_t now_ns, void* device_rows, voi
  * int64(math.Round(float64(used)/float64(total)*100)) <= thr (load_aware.go:299), |used| <= 2^53. */
 int64_t ke_debug_usage_bound(int64_t total, int64_t thr);
 int32_t ke_num_nodes(ke_ctx* ctx);
+/* The host object state of `node` after every Reserve / release so far: the Node (NodeInfo.Requested), its
+ * CPU table (RefCount / ExclusivePolicy), NUMA zones (allocations, single / shared pod counts) and device
+ * cache entry (used).  Up to *_cap entries each, counts in *n_*.  Tests compare it with the oracle's. */
+int ke_debug_node_state(ke_ctx* ctx, int32_t node, ke_node* out, int32_t cpu_cap, ke_cpu* cpus, int32_t* n_cpus,
+                        int32_t zone_cap, ke_numa_zone* zones, int32_t* n_zones, int32_t dev_cap, ke_device* devs,
+                        int32_t* n_devs);
 
 #ifdef __cplusplus
 }

@@ -9,7 +9,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 ABSENT = -1
 
 OK = 0
@@ -136,7 +136,8 @@ class NumaZone(C.Structure):
         ("capacity", i64 * NRES),
         ("allocated", i64 * NRES),
         ("cpuset_cpus", i32),
-        ("pad2", i32),
+        ("single_pods", C.c_int16),
+        ("shared_pods", C.c_int16),
     ]
 
 
@@ -318,8 +319,18 @@ class Quota(C.Structure):
     ]
 
 
+RELEASE_UNRESERVE, RELEASE_DELETE = 0, 1  # ke_pod_release modes
+
+
+class PodAllocation(C.Structure):
+    """ke_pod_allocation: what one placement reserved (Unreserve / informer-delete record)."""
+    _fields_ = [("node", i32), ("quota_assigned", u8), ("pad", u8 * 3), ("cpuset", C.c_uint64 * 4),
+                ("numa", i64 * (MAX_NUMA * NRES)), ("device_minors", C.c_uint64)]
+
+
 STRUCTS = [Config, Node, NodeMetric, PodMetric, AggregatedUsage, Pod, ResourceMap, LoadAwareArgs, NumaArgs,
-           DeviceShareArgs, Device, NumaZone, Cpu, QuotaArgs, Quota, GpuPartition, ExtArgs, NodeResource]
+           DeviceShareArgs, Device, NumaZone, Cpu, QuotaArgs, Quota, GpuPartition, ExtArgs, NodeResource,
+           PodAllocation]
 QUOTA_DTYPE = np.dtype(Quota)
 
 # numpy views of the same layouts (bulk loads)
@@ -333,6 +344,7 @@ GPU_PARTITION_DTYPE = np.dtype(GpuPartition)
 NUMA_ZONE_DTYPE = np.dtype(NumaZone)
 CPU_DTYPE = np.dtype(Cpu)
 NODE_RESOURCE_DTYPE = np.dtype(NodeResource)
+POD_ALLOCATION_DTYPE = np.dtype(PodAllocation)
 
 ROW_DTYPE = np.dtype([("f", np.int64, (18,)), ("flags", np.uint32), ("pad", np.uint32)])
 
@@ -413,6 +425,9 @@ EXPORTS = {
     "ke_last_numa_allocations": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_node_cpus_set": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p, i32]),
     "ke_last_cpusets": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
+    "ke_last_allocations": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
+    "ke_pod_release": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, i32]),
+    "ke_unreserve": (C.c_int, [C.c_void_p, C.c_void_p, i32]),
     "ke_quotas_load": (C.c_int, [C.c_void_p, C.POINTER(QuotaArgs), C.c_void_p, i32]),
     "ke_quota_state": (C.c_int, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "ke_schedule": (C.c_int, [C.c_void_p, i32, C.c_void_p, i64, C.c_void_p, C.c_void_p]),
@@ -434,6 +449,8 @@ EXPORTS = {
     "ke_debug_rows": (C.c_int, [C.c_void_p, i32, i64, C.c_void_p, C.c_void_p]),
     "ke_debug_usage_bound": (i64, [i64, i64]),
     "ke_num_nodes": (i32, [C.c_void_p]),
+    "ke_debug_node_state": (C.c_int, [C.c_void_p, i32, C.c_void_p, i32, C.c_void_p, C.c_void_p, i32, C.c_void_p,
+                                      C.c_void_p, i32, C.c_void_p, C.c_void_p]),
     "ke_comm_unique_id": (C.c_int, [C.c_void_p, i32]),
     "ke_shard_init": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p]),
     "ke_shard_range": (C.c_int, [C.c_void_p, C.POINTER(i32), C.POINTER(i32)]),
@@ -473,3 +490,17 @@ def ptr(arr):
     if arr is None:
         return None
     return C.c_void_p(arr.ctypes.data)
+
+
+def node_state(fn, h, i):
+    """(Node, cpus, zones, devices) of node i from a ke_debug_node_state-shaped call (product or oracle)."""
+    node = Node()
+    cpus = np.zeros(MAX_CPUS, CPU_DTYPE)
+    zones = np.zeros(MAX_NUMA, NUMA_ZONE_DTYPE)
+    devs = np.zeros(DEV_TYPES * MAX_MINORS, DEVICE_DTYPE)
+    nc, nz, nd = i32(), i32(), i32()
+    rc = fn(h, int(i), C.byref(node), MAX_CPUS, ptr(cpus), C.byref(nc), MAX_NUMA, ptr(zones), C.byref(nz),
+            len(devs), ptr(devs), C.byref(nd))
+    if rc != OK:
+        raise RuntimeError(f"node state rc={rc}")
+    return node, cpus[:nc.value], zones[:nz.value], devs[:nd.value]

@@ -101,7 +101,8 @@ int ke_abi_struct_sizes(int32_t* sizes, int32_t n) {
                          (int32_t)sizeof(ke_device),       (int32_t)sizeof(ke_numa_zone),
                          (int32_t)sizeof(ke_cpu),          (int32_t)sizeof(ke_quota_args),
                          (int32_t)sizeof(ke_quota),        (int32_t)sizeof(ke_gpu_partition),
-                         (int32_t)sizeof(ke_ext_args),     (int32_t)sizeof(ke_node_resource)};
+                         (int32_t)sizeof(ke_ext_args),     (int32_t)sizeof(ke_node_resource),
+                         (int32_t)sizeof(ke_pod_allocation)};
   const int32_t m = (int32_t)(sizeof(all) / sizeof(all[0]));
   for (int32_t i = 0; i < n && i < m; i++) sizes[i] = all[i];
   return m;
@@ -298,6 +299,7 @@ int ke_node_numa_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_numa_zone* z
   if (rc) return rc;
   NodeState& ns = ctx->c.nodes[node];
   ns.zones.assign(zones, zones + n);
+  for (ke_numa_zone& z : ns.zones) normalize_zone(z);
   ns.dirty = true;
   ctx->c.numa_enabled = true;
   return KE_OK;
@@ -536,7 +538,7 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
   std::vector<int64_t> all_numa;
   std::vector<double> all_batch_ms;
   double all_ms = 0;
-  bool numa_out = false;
+  bool numa_out = false, multi = false;
   const int32_t off = c.cfg.global_node_offset;
   for (int32_t s0 = 0; s0 < n_pods || (n_pods == 0 && s0 == 0);) {
     int32_t s1 = s0;
@@ -569,15 +571,18 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
       if (cs && (cs[0] | cs[1] | cs[2] | cs[3])) host_cpuset_reserve(ns, make_dev_pod(c.cfg, pods[p]), cs);
     }
     c.host_ms[7] = std::chrono::duration<double, std::milli>(clk::now() - tp).count();
-    if (s0 == 0 && s1 == n_pods) return KE_OK;  // one segment: the last_* outputs are already whole
-    all_dev.insert(all_dev.end(), c.last_dev_alloc.begin(), c.last_dev_alloc.end());
-    all_cs.insert(all_cs.end(), c.last_cpusets.begin(), c.last_cpusets.end());
-    numa_out = numa_out || !c.last_numa_alloc.empty();
-    if (c.last_numa_alloc.empty()) all_numa.resize(all_numa.size() + (size_t)len * KE_MAX_NUMA * KE_NRES, 0);
-    else all_numa.insert(all_numa.end(), c.last_numa_alloc.begin(), c.last_numa_alloc.end());
-    all_batch_ms.insert(all_batch_ms.end(), c.last_batch_ms.begin(), c.last_batch_ms.end());
-    all_ms += c.last_total_ms;
-    if (barrier(s1 - 1) && chosen[s1 - 1] >= 0) {  // the placed system / default pod: refresh the runtime
+    const bool whole = s0 == 0 && s1 == n_pods;  // one segment: the last_* outputs are already whole
+    if (!whole) {
+      all_dev.insert(all_dev.end(), c.last_dev_alloc.begin(), c.last_dev_alloc.end());
+      all_cs.insert(all_cs.end(), c.last_cpusets.begin(), c.last_cpusets.end());
+      numa_out = numa_out || !c.last_numa_alloc.empty();
+      if (c.last_numa_alloc.empty()) all_numa.resize(all_numa.size() + (size_t)len * KE_MAX_NUMA * KE_NRES, 0);
+      else all_numa.insert(all_numa.end(), c.last_numa_alloc.begin(), c.last_numa_alloc.end());
+      all_batch_ms.insert(all_batch_ms.end(), c.last_batch_ms.begin(), c.last_batch_ms.end());
+      all_ms += c.last_total_ms;
+    }
+    // the placed system / default pod (also when it ends the only segment): refresh the runtime
+    if (barrier(s1 - 1) && chosen[s1 - 1] >= 0) {
       rc = device_quota_sync(&c);
       if (rc) return rc;
       const ke_quota& q = c.quotas[(size_t)pods[s1 - 1].quota - 1];
@@ -587,14 +592,86 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
       if (rc) return rc;
       c.quota_dirty = true;
     }
+    if (whole) break;
     s0 = s1;
+    multi = true;
   }
-  c.last_dev_alloc.swap(all_dev);
-  c.last_cpusets.swap(all_cs);
-  if (numa_out) c.last_numa_alloc.swap(all_numa);
-  else c.last_numa_alloc.clear();
-  c.last_batch_ms.swap(all_batch_ms);
-  c.last_total_ms = all_ms;
+  if (multi) {
+    c.last_dev_alloc.swap(all_dev);
+    c.last_cpusets.swap(all_cs);
+    if (numa_out) c.last_numa_alloc.swap(all_numa);
+    else c.last_numa_alloc.clear();
+    c.last_batch_ms.swap(all_batch_ms);
+    c.last_total_ms = all_ms;
+  }
+  // release records of this call (ke_last_allocations / ke_unreserve)
+  c.last_chosen.assign(chosen, chosen + n_pods);
+  c.last_uid.resize((size_t)n_pods);
+  c.last_quota.resize((size_t)n_pods);
+  for (int32_t p = 0; p < n_pods; p++) {
+    c.last_uid[(size_t)p] = pods[p].uid;
+    c.last_quota[(size_t)p] = chosen[p] >= 0 && pods[p].quota > 0 && !c.quotas.empty();
+  }
+  return KE_OK;
+}
+
+// the release record of position p of the last ke_schedule
+static ke_pod_allocation last_allocation(const Context& c, int32_t p) {
+  ke_pod_allocation a{};
+  a.node = p < (int32_t)c.last_chosen.size() ? c.last_chosen[(size_t)p] : -1;
+  if (a.node < 0) return a;
+  a.quota_assigned = c.last_quota[(size_t)p];
+  constexpr int W = KE_MAX_NUMA * KE_NRES;
+  for (int q = 0; q < 4; q++)
+    a.cpuset[q] = (int64_t)c.last_cpusets.size() >= (int64_t)(p + 1) * 4 ? c.last_cpusets[(size_t)p * 4 + q] : 0;
+  for (int w = 0; w < W; w++)
+    a.numa[w] = (int64_t)c.last_numa_alloc.size() >= (int64_t)(p + 1) * W ? c.last_numa_alloc[(size_t)p * W + w] : 0;
+  a.device_minors = p < (int32_t)c.last_dev_alloc.size() ? c.last_dev_alloc[(size_t)p] : 0;
+  return a;
+}
+
+int ke_last_allocations(ke_ctx* ctx, int32_t n, ke_pod_allocation* out) {
+  if (!ctx || n < 0 || (n > 0 && !out)) return fail(KE_ERR_INVALID, "ke_last_allocations arguments");
+  for (int32_t p = 0; p < n; p++) out[p] = last_allocation(ctx->c, p);
+  return KE_OK;
+}
+
+int ke_pod_release(ke_ctx* ctx, const ke_pod* pod, const ke_pod_allocation* alloc, int32_t mode) {
+  if (!ctx || !pod || !alloc) return fail(KE_ERR_INVALID, "ke_pod_release arguments");
+  if (mode != KE_RELEASE_UNRESERVE && mode != KE_RELEASE_DELETE) return fail(KE_ERR_INVALID, "ke_pod_release mode");
+  int rc = validate_pod(*pod);
+  if (rc) return rc;
+  Context& c = ctx->c;
+  flush_mirror(c);  // the pod's own deferred Reserve mirror first
+  if (pod->quota < 0 || pod->quota > (int32_t)c.quotas.size())
+    return fail(KE_ERR_INVALID, "ke_pod.quota outside the loaded ElasticQuota tree");
+  const int32_t node = alloc->node < 0 ? -1 : alloc->node - c.cfg.global_node_offset;
+  if (node >= c.cfg.node_capacity) return fail(KE_ERR_NOT_FOUND, "ke_pod_release: node index out of range");
+  if (node >= 0 && c.nodes[(size_t)node].valid)  // (a node of another context's range: only the quota part)
+    host_release_node(c.cfg, c.ext_enabled, c.nodes[(size_t)node], *pod, *alloc);
+  const bool assigned = alloc->node >= 0 && alloc->quota_assigned;
+  if (pod->quota > 0 && (assigned || mode == KE_RELEASE_DELETE)) {
+    if (c.dev) {
+      rc = device_quota_sync(&c);  // the device holds the current used after a ke_schedule
+      if (rc) return rc;
+    }
+    rc = host_quota_release(c, *pod, assigned, mode == KE_RELEASE_DELETE);
+    if (rc) return rc;
+  }
+  return KE_OK;
+}
+
+int ke_unreserve(ke_ctx* ctx, const ke_pod* pod, int32_t queue_pos) {
+  if (!ctx || !pod) return fail(KE_ERR_INVALID, "ke_unreserve arguments");
+  Context& c = ctx->c;
+  if (queue_pos < 0 || queue_pos >= (int32_t)c.last_chosen.size())
+    return fail(KE_ERR_NOT_FOUND, "ke_unreserve: no such position in the last ke_schedule");
+  if (c.last_uid[(size_t)queue_pos] != pod->uid) return fail(KE_ERR_INVALID, "ke_unreserve: pod uid differs from the queue's");
+  if (c.last_chosen[(size_t)queue_pos] < 0) return KE_OK;  // not placed, or already unreserved
+  const ke_pod_allocation a = last_allocation(c, queue_pos);
+  const int rc = ke_pod_release(ctx, pod, &a, KE_RELEASE_UNRESERVE);
+  if (rc) return rc;
+  c.last_chosen[(size_t)queue_pos] = -1;
   return KE_OK;
 }
 
@@ -720,6 +797,23 @@ int ke_shard_range(ke_ctx* ctx, int32_t* lo, int32_t* hi) {
   *lo = l;
   *hi = h;
   return rc;
+}
+
+int ke_debug_node_state(ke_ctx* ctx, int32_t node, ke_node* out, int32_t cpu_cap, ke_cpu* cpus, int32_t* n_cpus,
+                        int32_t zone_cap, ke_numa_zone* zones, int32_t* n_zones, int32_t dev_cap, ke_device* devs,
+                        int32_t* n_devs) {
+  int rc = check_node(ctx, node);
+  if (ctx) flush_mirror(ctx->c);
+  if (rc) return rc;
+  const NodeState& ns = ctx->c.nodes[(size_t)node];
+  if (out) *out = ns.node;
+  if (n_cpus) *n_cpus = (int32_t)ns.cpus.size();
+  for (int32_t i = 0; cpus && i < cpu_cap && i < (int32_t)ns.cpus.size(); i++) cpus[i] = ns.cpus[(size_t)i];
+  if (n_zones) *n_zones = (int32_t)ns.zones.size();
+  for (int32_t i = 0; zones && i < zone_cap && i < (int32_t)ns.zones.size(); i++) zones[i] = ns.zones[(size_t)i];
+  if (n_devs) *n_devs = (int32_t)ns.devs.size();
+  for (int32_t i = 0; devs && i < dev_cap && i < (int32_t)ns.devs.size(); i++) devs[i] = ns.devs[(size_t)i];
+  return KE_OK;
 }
 
 int64_t ke_debug_usage_bound(int64_t total, int64_t thr) { return total > 0 ? max_used_within(total, thr) : 0; }

@@ -792,8 +792,22 @@ int validate_zones(int32_t n, const ke_numa_zone* zones) {
     if (zones[i].has_allocated > 7 || (zones[i].has_allocated && !(zones[i].has_allocated & KE_NUMA_ALLOC_ENTRY)))
       return fail(KE_ERR_INVALID, "NUMA allocation keys without an allocation entry");
     if (zones[i].numa_status > KE_NUMA_STATUS_SHARED) return fail(KE_ERR_INVALID, "NUMA node status");
+    if (zones[i].single_pods < 0 || zones[i].shared_pods < 0) return fail(KE_ERR_INVALID, "negative NUMA pod count");
+    if ((zones[i].single_pods || zones[i].shared_pods) && zones[i].numa_status != zone_status(zones[i]))
+      return fail(KE_ERR_INVALID, "NUMA node status disagrees with its single / shared pod counts");
   }
   return KE_OK;
+}
+
+uint8_t zone_status(const ke_numa_zone& z) {
+  if (z.shared_pods > 0) return KE_NUMA_STATUS_SHARED;
+  return z.single_pods > 0 ? KE_NUMA_STATUS_SINGLE : KE_NUMA_STATUS_IDLE;
+}
+
+void normalize_zone(ke_numa_zone& z) {
+  if (z.single_pods || z.shared_pods) return;
+  if (z.numa_status == KE_NUMA_STATUS_SINGLE) z.single_pods = 1;
+  if (z.numa_status == KE_NUMA_STATUS_SHARED) z.shared_pods = 1;
 }
 
 // getResourceOptions -> amplifyNUMANodeResources (util.go:78-98): the NUMA zones' cpu is amplified with
@@ -815,8 +829,8 @@ void derive_numa_row(const NodeState& ns, int64_t* f, uint64_t* mask) {
     const int id = z.id;
     *mask |= 1ull << id;
     if (id < (int)ns.zones.size()) {  // GetAllNUMANodeStatus(len(numaNodes)) covers ids 0..n-1
-      if (z.numa_status == KE_NUMA_STATUS_SINGLE) *mask |= 1ull << (NUMA_M_ST + id);
-      if (z.numa_status == KE_NUMA_STATUS_SHARED) *mask |= 1ull << (NUMA_M_ST + 8 + id);
+      if (zone_status(z) == KE_NUMA_STATUS_SINGLE) *mask |= 1ull << (NUMA_M_ST + id);
+      if (zone_status(z) == KE_NUMA_STATUS_SHARED) *mask |= 1ull << (NUMA_M_ST + 8 + id);
     }
     for (int r = 0; r < KE_NRES; r++) {
       if (z.has[r]) {
@@ -846,6 +860,8 @@ void derive_numa_row(const NodeState& ns, int64_t* f, uint64_t* mask) {
 }
 
 void host_numa_reserve(NodeState& ns, const int64_t* delta) {
+  // resourceManager.Update records nothing on a node without a valid CPU topology (resource_manager.go:461-466)
+  if (!cpus_valid(ns)) return;
   for (ke_numa_zone& z : ns.zones) {
     const int64_t d[KE_NRES] = {delta[2 * z.id], delta[2 * z.id + 1]};
     if (d[0] == 0 && d[1] == 0) continue;
@@ -955,10 +971,91 @@ void host_cpuset_reserve(NodeState& ns, const DevPod& dp, const uint64_t* set) {
   n_used = (int)ids.size();
   for (int id : ids)
     if (id < 32) used |= 1u << id;
-  for (ke_numa_zone& z : ns.zones)  // NUMANodeSharedStatus after addPodAllocation
-    if (z.id < 32 && (used >> z.id & 1))
-      z.numa_status = (uint8_t)(n_used > 1 || z.numa_status == KE_NUMA_STATUS_SHARED ? KE_NUMA_STATUS_SHARED
-                                                                                    : KE_NUMA_STATUS_SINGLE);
+  for (ke_numa_zone& z : ns.zones)  // sharedNode / singleNUMANode after addPodAllocation
+    if (z.id < 32 && (used >> z.id & 1)) {
+      if (n_used > 1) z.shared_pods++;
+      else z.single_pods++;
+      z.numa_status = zone_status(z);
+    }
+  ns.dirty = true;
+}
+
+void host_release_node(const ke_config& cfg, bool ext, NodeState& ns, const ke_pod& pod, const ke_pod_allocation& a) {
+  // LoadAware podAssignCache.unAssign (pod_assign_cache.go:126-136)
+  for (size_t i = 0; i < ns.asg.size(); i++)
+    if (ns.asg[i].pod.uid == pod.uid) {
+      ns.asg.erase(ns.asg.begin() + (long)i);
+      break;
+    }
+  // framework NodeInfo.RemovePod: Requested (and the FitPlus (NonZero)Requested by resource id)
+  ns.node.requested[KE_RES_CPU] -= pod.requests[KE_RES_CPU];
+  ns.node.requested[KE_RES_MEMORY] -= pod.requests[KE_RES_MEMORY];
+  if (ext)
+    for (int e = 0; e < pod.n_xres; e++)
+      for (ke_node_resource& r : ns.xres)
+        if (r.id == pod.xres_id[e]) r.requested -= pod.xres_value[e];
+  // NodeNUMAResource resourceManager.Release -> NodeAllocation.release (node_allocation.go:158-190); only a
+  // node with a valid CPU topology recorded the allocation (Update, resource_manager.go:461-466)
+  if (cpus_valid(ns)) {
+    std::vector<int> ids;
+    for (ke_cpu& c : ns.cpus) {
+      if (!(a.cpuset[c.cpu_id >> 6] >> (c.cpu_id & 63) & 1) || c.ref_count <= 0) continue;
+      if (--c.ref_count == 0) c.exclusive = KE_CPU_EXCL_NONE;  // the CPU leaves allocatedCPUs
+      if (std::find(ids.begin(), ids.end(), c.numa_id) == ids.end()) ids.push_back(c.numa_id);
+    }
+    for (ke_numa_zone& z : ns.zones) {
+      if (std::find(ids.begin(), ids.end(), z.id) != ids.end()) {  // delete(sharedNode / singleNUMANode[id], uid)
+        int16_t& k = ids.size() > 1 ? z.shared_pods : z.single_pods;
+        if (k > 0) k--;
+        z.numa_status = zone_status(z);
+      }
+      if (!(z.has_allocated & KE_NUMA_ALLOC_ENTRY)) continue;  // allocatedResources[id] == nil
+      for (int r = 0; r < KE_NRES; r++) {  // quotav1.SubtractWithNonNegativeResult: keys of both, floor 0
+        const int64_t b = a.numa[2 * z.id + r];
+        if (b == 0) continue;
+        const uint8_t key = r == KE_RES_CPU ? KE_NUMA_ALLOC_CPU : KE_NUMA_ALLOC_MEMORY;
+        const int64_t v = ((z.has_allocated & key) ? z.allocated[r] : 0) - b;
+        z.allocated[r] = v > 0 ? v : 0;
+        z.has_allocated |= key;
+      }
+    }
+  }
+  // DeviceShare updateCacheUsed(allocation, pod, false) -> updateDeviceUsed (device_cache.go:184-209)
+  if (ns.has_dev_cache && a.device_minors) {
+    const DevPod dp = make_dev_pod(cfg, pod);
+    for (ke_device& d : ns.devs) {
+      if (!(a.device_minors & (1ull << (16 * d.type + d.minor)))) continue;
+      const int t = d.type;
+      int64_t alloc[KE_DKEYS] = {0, 0, 0};
+      bool has[KE_DKEYS] = {false, false, false};
+      if (t == KE_DEV_GPU) {  // the amounts Reserve added (fillGPUTotalMem, host_ds_reserve)
+        const int64_t tm = d.health && d.has_total[KE_DKEY_GPU_MEMORY] ? d.total[KE_DKEY_GPU_MEMORY] : 0;
+        if (dp.flags & PF_DS_H_CORE) has[0] = true, alloc[0] = dp.ds_req[0];
+        if (dp.flags & PF_DS_H_RATIO) {
+          has[2] = true, alloc[2] = dp.ds_req[2];
+          has[1] = true, alloc[1] = dp.ds_req[2] * tm / 100;
+        } else if (dp.flags & PF_DS_H_MEM) {
+          has[1] = true, alloc[1] = dp.ds_req[1];
+          has[2] = true, alloc[2] = (int64_t)((double)dp.ds_req[1] / (double)tm * 100.0);
+        }
+      } else {
+        has[0] = true, alloc[0] = dp.ds_req[2 + t];
+      }
+      bool zero = true;
+      for (int k = 0; k < DS_NK[t]; k++) {  // SubtractWithNonNegativeResult over the keys of both
+        if (has[k]) {
+          const int64_t v = (d.has_used[k] ? d.used[k] : 0) - alloc[k];
+          d.used[k] = v > 0 ? v : 0;
+          d.has_used[k] = 1;
+        } else if (d.has_used[k] && d.used[k] < 0) {
+          d.used[k] = 0;
+        }
+        zero = zero && (!d.has_used[k] || d.used[k] == 0);
+      }
+      if (zero)  // quotav1.IsZero(used): the minor's used entry is deleted
+        for (int k = 0; k < KE_DKEYS; k++) d.has_used[k] = 0, d.used[k] = 0;
+    }
+  }
   ns.dirty = true;
 }
 
@@ -1051,6 +1148,43 @@ void share_runtime(int64_t total, std::vector<QuotaShare*>& kids) {
   }
 }
 }  // namespace
+
+int host_quota_release(Context& c, const ke_pod& pod, bool assigned, bool del) {
+  if (pod.quota <= 0 || pod.quota > (int32_t)c.quotas.size()) return KE_OK;
+  const int qi = pod.quota - 1;
+  int64_t req[KE_NRES];  // quotav1.Mask(PodRequests, ResourceNames(Max)) of the pod's own quota
+  for (int r = 0; r < KE_NRES; r++)
+    req[r] = c.quotas[(size_t)qi].has_max[r] ? pod.requests[r == 0 ? KE_RES_CPU : KE_RES_MEMORY] : 0;
+  bool refresh = false;
+  if (assigned) {  // updateGroupDeltaUsedNoLock with -request: the quota and every ancestor, floor 0 each
+    int64_t before[KE_NRES];
+    for (int r = 0; r < KE_NRES; r++) before[r] = c.quotas[(size_t)qi].used[r];
+    for (int q = qi; q >= 0; q = c.quotas[(size_t)q].parent)
+      for (int r = 0; r < KE_NRES; r++) {
+        ke_quota& x = c.quotas[(size_t)q];
+        x.used[r] = std::max<int64_t>(0, x.used[r] - req[r]);
+        if (pod.quota_non_preemptible) x.non_preemptible_used[r] = std::max<int64_t>(0, x.non_preemptible_used[r] - req[r]);
+      }
+    // a system / default quota's used shrank: totalResourceExceptSystemAndDefaultUsed grows by as much
+    // (updateClusterTotalResourceNoLock, group_quota_manager.go:127-151,268-271)
+    if (c.quotas[(size_t)qi].limit_is_max && c.qargs.enable_runtime_quota) {
+      for (int r = 0; r < KE_NRES; r++) c.qargs.total[r] += before[r] - c.quotas[(size_t)qi].used[r];
+      refresh = true;
+    }
+  }
+  if (del) {  // updatePodRequestNoLock(quota, pod, nil): SelfRequest, floor 0 (quota_info.go:238-258)
+    for (int r = 0; r < KE_NRES; r++)
+      c.quotas[(size_t)qi].self_request[r] = std::max<int64_t>(0, c.quotas[(size_t)qi].self_request[r] - req[r]);
+    refresh = true;
+  }
+  if (refresh) {
+    const int rc = quota_compute_limits(c.qargs, c.quotas, c.qlimit, c.qlimit_has);
+    if (rc) return rc;
+  }
+  c.quota_dirty = true;
+  c.quota_on_device = false;  // the host tree is now the current one
+  return KE_OK;
+}
 
 int quota_compute_limits(const ke_quota_args& args, const std::vector<ke_quota>& q, std::vector<int64_t>& limit,
                          std::vector<uint8_t>& has) {

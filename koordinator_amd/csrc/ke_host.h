@@ -63,6 +63,11 @@ struct Context {
   std::vector<uint64_t> last_cpusets;    // per pod of the last ke_schedule: 4 words (CPU-id bitset)
   std::vector<int64_t> last_numa_alloc;  // per pod of the last ke_schedule: [KE_MAX_NUMA*KE_NRES]
   std::vector<uint64_t> last_dev_alloc;  // per pod of the last ke_schedule
+  // per pod of the last ke_schedule: the chosen node (-1 once unreserved), the pod uid and whether its
+  // ElasticQuota Reserve ran (ke_last_allocations / ke_unreserve)
+  std::vector<int32_t> last_chosen;
+  std::vector<int64_t> last_uid;
+  std::vector<uint8_t> last_quota;
   DeviceState* dev = nullptr;
   // last ke_schedule timing
   double last_total_ms = 0.0;
@@ -145,6 +150,10 @@ void host_ds_reserve(const ke_config& cfg, NodeState& ns, const DevPod& dp, uint
 
 // NUMA topology
 int validate_zones(int32_t n, const ke_numa_zone* zones);
+// NUMANodeSharedStatus (node_allocation.go:60-68) from the zone's single / shared pod counts
+uint8_t zone_status(const ke_numa_zone& z);
+// a status given without counts stands for one pod of that kind
+void normalize_zone(ke_numa_zone& z);
 // the NUMA SoA row of a node: NUM_NUMA_FIELDS int64 + the uint32 mask
 void derive_numa_row(const NodeState& ns, int64_t* f, uint64_t* mask);
 // host mirror of the NUMA allocation the device Reserve made: delta[z][r] per zone id
@@ -165,5 +174,12 @@ void derive_cpu_rows(const NodeState& ns, CpuRec* recs, int64_t* cs);
 // host mirror of a cpuset Reserve: RefCount++ / exclusive policy on the CPUs of `set` (4 words), the
 // NUMA nodes' single / shared status (node_allocation.go:111-156)
 void host_cpuset_reserve(NodeState& ns, const DevPod& dp, const uint64_t* set);
+
+// Release of one placement from its node (ke_pod_release): podAssignCache.unAssign, NodeInfo.RemovePod
+// (Requested, the FitPlus requested when `ext`), resourceManager.Release, DeviceShare updateCacheUsed(false)
+void host_release_node(const ke_config& cfg, bool ext, NodeState& ns, const ke_pod& pod, const ke_pod_allocation& a);
+// ElasticQuota UnreservePod (assigned) / OnPodDelete (del) on the host tree (used already synced from the
+// device); recomputes the runtime limits when the tree total or a request moved
+int host_quota_release(Context& c, const ke_pod& pod, bool assigned, bool del);
 
 }  // namespace ke

@@ -1804,10 +1804,15 @@ __device__ void numa_reserve_cs(const SoA& s, int64_t i, uint32_t nf, const Numa
                                 uint32_t used, int n_used, int64_t* out16) {
   // the cpuset counts come from CPU tables; without the CPU SoA they are zero (a zone without an
   // allocation entry holds no cpusets, ke_node_numa_set) and the ratio is never read
+  if (out16)
+    for (int z = 0; z < 8; z++)
+      for (int r = 0; r < 2; r++) out16[2 * z + r] = dist[r][z];
+  // resourceManager.Update records the allocation only on a node with a valid CPU topology
+  // (resource_manager.go:461-466); the pod still carries it (state.allocation -> PreBind)
+  if (!(nf & NF_CPUS_VALID)) return;
   const int64_t ratio = s.cs ? s.cs[CS_RS * s.stride + i] : 0;
   for (int z = 0; z < 8; z++) {
     for (int r = 0; r < 2; r++) {
-      if (out16) out16[2 * z + r] = dist[r][z];
       int64_t* f = s.nf + (NUMA_AL + 2 * z + r) * s.stride + i;
       const bool entry_before = (v.ak[0] >> z) & 1u, entry_after = entry_before || (((got[0] | got[1]) >> z) & 1u);
       if (r == 0 && (nf & NF_NUMA_AL_AMP)) {

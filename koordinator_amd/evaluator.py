@@ -200,6 +200,25 @@ class Evaluator:
         self._check(self.lib.ke_last_cpusets(self.h, len(pods), abi.ptr(self.last_cpusets)))
         return chosen, score
 
+    def last_allocations(self, n=None):
+        """Release records (np.ndarray POD_ALLOCATION_DTYPE) of the pods of the last schedule()."""
+        n = len(self.last_device_allocations) if n is None else n
+        out = np.zeros(n, abi.POD_ALLOCATION_DTYPE)
+        self._check(self.lib.ke_last_allocations(self.h, n, abi.ptr(out)))
+        return out
+
+    def release(self, pod, alloc, mode=abi.RELEASE_UNRESERVE):
+        """ke_pod_release: Unreserve (or informer delete) of one placement; `pod` abi.Pod or a POD_DTYPE
+        record, `alloc` a POD_ALLOCATION_DTYPE record."""
+        p = as_pod_array([pod] if isinstance(pod, abi.Pod) else np.asarray(pod).reshape(1))
+        a = np.ascontiguousarray(np.asarray(alloc, abi.POD_ALLOCATION_DTYPE).reshape(1))
+        self._check(self.lib.ke_pod_release(self.h, abi.ptr(p), abi.ptr(a), int(mode)))
+
+    def unreserve(self, pod, queue_pos):
+        """ke_unreserve: Unreserve of the pod at `queue_pos` of the last schedule()."""
+        p = as_pod_array([pod] if isinstance(pod, abi.Pod) else np.asarray(pod).reshape(1))
+        self._check(self.lib.ke_unreserve(self.h, abi.ptr(p), int(queue_pos)))
+
     def quotas_load(self, args, quotas):
         """ElasticQuota tree (include/koord_eval.h ke_quotas_load): runtime computed on the host,
         admission and Reserve applied inside schedule()."""
@@ -273,6 +292,10 @@ class Evaluator:
         ms = C.c_double()
         self._check(self.lib.ke_bench_eval_kernel(self.h, len(pods), abi.ptr(pods), int(now_ns), iters, C.byref(ms)))
         return ms.value
+
+    def node_state(self, i):
+        """Host object state of node i: (Node, cpus, zones, devices) (ke_debug_node_state)."""
+        return abi.node_state(self.lib.ke_debug_node_state, self.h, i)
 
     def debug_rows(self, now_ns, device=True):
         n = self.num_nodes

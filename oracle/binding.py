@@ -75,6 +75,8 @@ def load():
         "or_usage_percent": (i64, [i64, i64]),
         "or_quotas_load": (C.c_int, [V, C.POINTER(abi.QuotaArgs), V, i32]),
         "or_quota_state": (C.c_int, [V, i32, V, V, V, V]),
+        "or_pod_release": (C.c_int, [V, V, V, i32]),
+        "or_debug_node_state": (C.c_int, [V, i32, V, i32, V, V, i32, V, V, i32, V, V]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -307,13 +309,38 @@ class Oracle:
                                   abi.ptr(self.last_cpusets), n_threads)
         if rc != 0:
             raise RuntimeError(f"oracle schedule rc={rc}")
+        self._last = (pods, chosen)
         return chosen, score
+
+    def last_allocations(self, n=None):
+        """Release records of the last schedule() (same layout as Evaluator.last_allocations)."""
+        pods, chosen = self._last
+        n = len(chosen) if n is None else n
+        out = np.zeros(n, abi.POD_ALLOCATION_DTYPE)
+        out["node"] = chosen[:n]
+        placed = chosen[:n] >= 0
+        out["quota_assigned"] = placed & (pods["quota"][:n] > 0) & getattr(self, "_has_quotas", False)
+        out["cpuset"] = np.where(placed[:, None], self.last_cpusets[:n], 0)
+        out["numa"] = np.where(placed[:, None], self.last_numa_allocations[:n], 0)
+        out["device_minors"] = np.where(placed, self.last_device_allocations[:n], 0)
+        return out
+
+    def node_state(self, i):
+        return abi.node_state(self.lib.or_debug_node_state, self.h, i)
+
+    def release(self, pod, alloc, mode=abi.RELEASE_UNRESERVE):
+        p = as_pod_array([pod] if isinstance(pod, abi.Pod) else np.asarray(pod).reshape(1))
+        a = np.ascontiguousarray(np.asarray(alloc, abi.POD_ALLOCATION_DTYPE).reshape(1))
+        rc = self.lib.or_pod_release(self.h, abi.ptr(p), abi.ptr(a), int(mode))
+        if rc != 0:
+            raise RuntimeError(f"oracle release rc={rc}")
 
     def quotas_load(self, args, quotas):
         quotas = np.ascontiguousarray(quotas, abi.QUOTA_DTYPE)
         rc = self.lib.or_quotas_load(self.h, C.byref(args), abi.ptr(quotas), len(quotas))
         if rc != 0:
             raise RuntimeError(f"oracle quotas_load rc={rc}")
+        self._has_quotas = True
 
     def quota_state(self, q):
         return _quota_state(self.lib.or_quota_state, self.h, q)

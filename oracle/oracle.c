@@ -439,6 +439,13 @@ static int cpus_valid(const or_node* n) {
          n->cpus->t.num_cores && n->cpus->t.num_cpus;
 }
 
+/* NodeAllocation.NUMANodeSharedStatus (node_allocation.go:60-68) from the sizes of the zone's
+ * singleNUMANode / sharedNode pod sets */
+static uint8_t zone_status_of(const ke_numa_zone* z) {
+  if (z->shared_pods > 0) return KE_NUMA_STATUS_SHARED;
+  return z->single_pods > 0 ? KE_NUMA_STATUS_SINGLE : KE_NUMA_STATUS_IDLE;
+}
+
 /* GetAvailableCPUs(node) allocated.CPUs().Size() (resource_manager.go:497-511) */
 static int64_t cpus_allocated_count(const or_node* n) {
   if (!n->cpus) return n->node.cpuset_allocated_cpus;
@@ -2438,6 +2445,19 @@ static ds_aff ds_reserve_affinity(const or_cluster* c, const ke_pod* pod, int32_
 
 static uint64_t ds_reserve_on(or_cluster* c, const ke_pod* pod, int32_t node, ds_aff a);
 
+/* fillGPUTotalMem (devicehandler_gpu.go:98-125): the allocated instance's memory / memory ratio from the other
+ * and the device's own gpu-memory total */
+static void fill_gpu_total_mem(const ke_device* dev, rl* alloc) {
+  const int64_t tm = dev->has_total[KE_DKEY_GPU_MEMORY] && dev->health ? dev->total[KE_DKEY_GPU_MEMORY] : 0;
+  if (alloc->has[KE_DKEY_GPU_MEMORY]) { /* memoryBytesToRatio */
+    alloc->has[KE_DKEY_GPU_MEMORY_RATIO] = 1;
+    alloc->v[KE_DKEY_GPU_MEMORY_RATIO] = (int64_t)((double)alloc->v[KE_DKEY_GPU_MEMORY] / (double)tm * 100.0);
+  } else { /* memoryRatioToBytes */
+    alloc->has[KE_DKEY_GPU_MEMORY] = 1;
+    alloc->v[KE_DKEY_GPU_MEMORY] = alloc->v[KE_DKEY_GPU_MEMORY_RATIO] * tm / 100;
+  }
+}
+
 /* AutopilotAllocator.Allocate in Reserve (plugin.go:459-486) succeeds: with the alignment disabled nothing
  * checked the devices of a node whose NUMA Admit stored an affinity (Filter skipped, Allocate a no-op) */
 static int ds_reserve_feasible(const or_cluster* c, const ke_pod* pod, int32_t node, ds_aff a) {
@@ -2484,16 +2504,7 @@ static uint64_t ds_reserve_on(or_cluster* c, const ke_pod* pod, int32_t node, ds
       ke_device* dev = NULL;
       for (int j = 0; j < nd->n_dev; j++)
         if (nd->dev[j].type == t && nd->dev[j].minor == minor) dev = &nd->dev[j];
-      if (t == KE_DEV_GPU) {
-        const int64_t tm = dev->has_total[KE_DKEY_GPU_MEMORY] && dev->health ? dev->total[KE_DKEY_GPU_MEMORY] : 0;
-        if (alloc.has[KE_DKEY_GPU_MEMORY]) { /* memoryBytesToRatio */
-          alloc.has[KE_DKEY_GPU_MEMORY_RATIO] = 1;
-          alloc.v[KE_DKEY_GPU_MEMORY_RATIO] = (int64_t)((double)alloc.v[KE_DKEY_GPU_MEMORY] / (double)tm * 100.0);
-        } else { /* memoryRatioToBytes */
-          alloc.has[KE_DKEY_GPU_MEMORY] = 1;
-          alloc.v[KE_DKEY_GPU_MEMORY] = alloc.v[KE_DKEY_GPU_MEMORY_RATIO] * tm / 100;
-        }
-      }
+      if (t == KE_DEV_GPU) fill_gpu_total_mem(dev, &alloc);
       const rl u = rl_add(dev_used(dev, nk), alloc, nk);
       for (int k = 0; k < nk; k++) {
         dev->has_used[k] = u.has[k];
@@ -2651,6 +2662,12 @@ static int or_reserve_plan(const or_cluster* c, const ke_pod* pod, int32_t node,
  * added to the zones' entries (quotav1.Add keys). */
 static void or_reserve_apply(or_cluster* c, int32_t node, const reserve_plan* rp, int64_t* out16) {
   or_node* n = &c->nodes[node];
+  for (int z = 0; z < n->n_zone; z++) /* state.allocation: the pod carries it whatever Update records */
+    if (out16)
+      for (int r = 0; r < KE_NRES; r++) out16[2 * n->zone[z].id + r] = rp->dist[z][r];
+  /* resourceManager.Update returns before recording anything when !CPUTopology.IsValid()
+   * (resource_manager.go:461-466) */
+  if (!cpus_valid(n)) return;
   if (n->cpus) {
     or_cpus* x = n->cpus;
     int used[ACC_MAX_CPUS], nu = 0;
@@ -2663,18 +2680,17 @@ static void or_reserve_apply(or_cluster* c, int32_t node, const reserve_plan* rp
       for (int k = 0; k < nu && !f; k++) f = used[k] == x->t.node[cpu];
       if (!f) used[nu++] = x->t.node[cpu];
     }
-    for (int k = 0; k < nu; k++) /* NUMANodeSharedStatus after adding the pod to sharedNode / singleNUMANode */
+    for (int k = 0; k < nu; k++) /* the pod joins sharedNode[id] (several NUMA ids) or singleNUMANode[id] */
       for (int z = 0; z < n->n_zone; z++)
-        if (n->zone[z].id == used[k])
-          n->zone[z].numa_status = (uint8_t)(nu > 1 || n->zone[z].numa_status == KE_NUMA_STATUS_SHARED
-                                                 ? KE_NUMA_STATUS_SHARED
-                                                 : KE_NUMA_STATUS_SINGLE);
+        if (n->zone[z].id == used[k]) {
+          if (nu > 1) n->zone[z].shared_pods++;
+          else n->zone[z].single_pods++;
+          n->zone[z].numa_status = zone_status_of(&n->zone[z]);
+        }
   }
   for (int z = 0; z < n->n_zone; z++) {
     if (rp->dist[z][0] == 0 && rp->dist[z][1] == 0) continue;
     ke_numa_zone* zn = &n->zone[z];
-    if (out16)
-      for (int r = 0; r < KE_NRES; r++) out16[2 * zn->id + r] = rp->dist[z][r];
     for (int r = 0; r < KE_NRES; r++) {
       const uint8_t key = r == KE_RES_CPU ? KE_NUMA_ALLOC_CPU : KE_NUMA_ALLOC_MEMORY;
       if (!(zn->has_allocated & key)) zn->allocated[r] = 0;
@@ -2797,10 +2813,20 @@ int or_node_numa_set(or_cluster* c, int32_t node, int32_t n, const ke_numa_zone*
     if (zones[i].cpuset_cpus > 0 && !(zones[i].has_allocated & KE_NUMA_ALLOC_ENTRY)) return KE_ERR_INVALID;
     if (zones[i].has_allocated > 7 || (zones[i].has_allocated && !(zones[i].has_allocated & KE_NUMA_ALLOC_ENTRY)))
       return KE_ERR_INVALID;
-    if (zones[i].numa_status > KE_NUMA_STATUS_SHARED) return KE_ERR_INVALID;
+    if (zones[i].numa_status > KE_NUMA_STATUS_SHARED || zones[i].single_pods < 0 || zones[i].shared_pods < 0)
+      return KE_ERR_INVALID;
+    if ((zones[i].single_pods || zones[i].shared_pods) && zones[i].numa_status != zone_status_of(&zones[i]))
+      return KE_ERR_INVALID;
   }
   c->nodes[node].n_zone = n;
   if (n) memcpy(c->nodes[node].zone, zones, sizeof(ke_numa_zone) * (size_t)n);
+  for (int32_t i = 0; i < n; i++) { /* a status without counts: one pod in that set */
+    ke_numa_zone* z = &c->nodes[node].zone[i];
+    if (!z->single_pods && !z->shared_pods) {
+      if (z->numa_status == KE_NUMA_STATUS_SINGLE) z->single_pods = 1;
+      if (z->numa_status == KE_NUMA_STATUS_SHARED) z->shared_pods = 1;
+    }
+  }
   return KE_OK;
 }
 
@@ -3145,5 +3171,121 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
     if (dev_alloc) dev_alloc[p] = mask;
   }
   free(o);
+  return KE_OK;
+}
+
+/* ---------------------------------------------------------------------------------------------- */
+/* Unreserve / pod delete (ReservePlugin.Unreserve of every plugin, framework ForgetPod)             */
+/* ---------------------------------------------------------------------------------------------- */
+
+/* The release of one placement recorded in `a` (see ke_pod_release in koord_eval.h):
+ *  - loadaware Unreserve: podAssignCache.unAssign (load_aware.go:197-199, pod_assign_cache.go:126-136)
+ *  - framework RemovePod: NodeInfo.Requested and the per-resource requested NodeResourcesFitPlus reads
+ *  - nodenumaresource Unreserve: resourceManager.Release -> NodeAllocation.release (plugin.go:569-577,
+ *    node_allocation.go:158-190): RefCount-- per CPU (deleted at 0), the pod leaves sharedNode /
+ *    singleNUMANode of its CPUs' NUMA ids, allocatedResources[id] = SubtractWithNonNegativeResult;
+ *    nothing was recorded on a node without a valid CPU topology (Update, resource_manager.go:461-466)
+ *  - deviceshare Unreserve: updateCacheUsed(allocationResult, pod, false) (plugin.go:498-516,
+ *    device_cache.go:184-209): used = SubtractWithNonNegativeResult(used, allocation), deleted when zero
+ *  - elasticquota Unreserve: UnreservePod (plugin.go:361, group_quota_manager.go:965-981), or OnPodDelete
+ *    (:922-941) for an informer delete (quota.c orq_release) */
+int or_pod_release(or_cluster* c, const ke_pod* pod, const ke_pod_allocation* a, int32_t mode) {
+  const int32_t node = a->node;
+  if (node >= c->n) return KE_ERR_NOT_FOUND;
+  if (node >= 0) {
+    or_node* n = &c->nodes[node];
+    or_pod_unassign(c, node, pod->uid);
+    n->node.requested[KE_RES_CPU] -= pod->requests[KE_RES_CPU];
+    n->node.requested[KE_RES_MEMORY] -= pod->requests[KE_RES_MEMORY];
+    if (c->cfg.ext.weight_fitplus > 0 || c->cfg.ext.weight_sra > 0)
+      for (int32_t e = 0; e < pod->n_xres; e++) {
+        ke_node_resource* r = (ke_node_resource*)node_xres(n, pod->xres_id[e]);
+        if (r) r->requested -= pod->xres_value[e];
+      }
+    if (cpus_valid(n)) {
+      or_cpus* x = n->cpus;
+      int used[ACC_MAX_CPUS], nu = 0;
+      for (int cpu = 0; cpu < ACC_MAX_CPUS; cpu++) {
+        if (!(a->cpuset[cpu >> 6] >> (cpu & 63) & 1) || !x->al.present[cpu]) continue;
+        if (--x->al.ref[cpu] == 0) {
+          x->al.present[cpu] = 0;
+          x->al.excl[cpu] = 0;
+        }
+        int f = 0;
+        for (int k = 0; k < nu && !f; k++) f = used[k] == x->t.node[cpu];
+        if (!f) used[nu++] = x->t.node[cpu];
+      }
+      for (int z = 0; z < n->n_zone; z++) {
+        ke_numa_zone* zn = &n->zone[z];
+        for (int k = 0; k < nu; k++)
+          if (used[k] == zn->id) {
+            int16_t* cnt = nu > 1 ? &zn->shared_pods : &zn->single_pods;
+            if (*cnt > 0) (*cnt)--;
+            zn->numa_status = zone_status_of(zn);
+          }
+        if (!(zn->has_allocated & KE_NUMA_ALLOC_ENTRY)) continue;
+        for (int r = 0; r < KE_NRES; r++) {
+          const int64_t b = a->numa[2 * zn->id + r];
+          if (b == 0) continue; /* a key of the pod's allocation carries a non-zero amount */
+          const uint8_t key = r == KE_RES_CPU ? KE_NUMA_ALLOC_CPU : KE_NUMA_ALLOC_MEMORY;
+          const int64_t v = ((zn->has_allocated & key) ? zn->allocated[r] : 0) - b;
+          zn->allocated[r] = v > 0 ? v : 0;
+          zn->has_allocated |= key;
+        }
+      }
+    }
+    if (n->has_dev_cache && a->device_minors) {
+      ds_pod d;
+      ds_prepare_pod(pod, &d);
+      for (int i = 0; i < n->n_dev; i++) {
+        ke_device* dv = &n->dev[i];
+        if (!(a->device_minors >> (16 * dv->type + dv->minor) & 1)) continue;
+        const int t = dv->type, nk = nkeys(t);
+        rl alloc = d.req[t];
+        if (t == KE_DEV_GPU) fill_gpu_total_mem(dv, &alloc);
+        rl used = rl_sub_nonneg(dev_used(dv, nk), alloc, nk);
+        if (rl_is_zero(used, nk)) used = rl_empty();
+        for (int k = 0; k < nk; k++) {
+          dv->has_used[k] = used.has[k];
+          dv->used[k] = used.has[k] ? used.v[k] : 0;
+        }
+      }
+    }
+  }
+  if (c->quotas && pod->quota > 0)
+    orq_release(c->quotas, pod, node >= 0 && a->quota_assigned, mode == KE_RELEASE_DELETE);
+  return KE_OK;
+}
+
+/* The oracle's object state of `node` in the product's introspection layout (ke_debug_node_state). */
+int or_debug_node_state(const or_cluster* c, int32_t node, ke_node* out, int32_t cpu_cap, ke_cpu* cpus,
+                        int32_t* n_cpus, int32_t zone_cap, ke_numa_zone* zones, int32_t* n_zones, int32_t dev_cap,
+                        ke_device* devs, int32_t* n_devs) {
+  if (node < 0 || node >= c->n) return KE_ERR_NOT_FOUND;
+  const or_node* n = &c->nodes[node];
+  if (out) *out = n->node;
+  int32_t k = 0;
+  if (n->cpus)
+    for (int id = 0; id < ACC_MAX_CPUS; id++) {
+      if (!n->cpus->t.valid[id]) continue;
+      if (cpus && k < cpu_cap) {
+        ke_cpu e;
+        memset(&e, 0, sizeof e);
+        e.cpu_id = id;
+        e.core_id = n->cpus->t.core[id];
+        e.numa_id = n->cpus->t.node[id];
+        e.socket_id = n->cpus->t.socket[id];
+        e.ref_count = n->cpus->al.present[id] ? n->cpus->al.ref[id] : 0;
+        e.exclusive = (uint8_t)(n->cpus->al.present[id] ? n->cpus->al.excl[id] : 0);
+        e.reserved = n->cpus->reserved[id];
+        cpus[k] = e;
+      }
+      k++;
+    }
+  if (n_cpus) *n_cpus = k;
+  if (n_zones) *n_zones = n->n_zone;
+  for (int32_t i = 0; zones && i < zone_cap && i < n->n_zone; i++) zones[i] = n->zone[i];
+  if (n_devs) *n_devs = n->n_dev;
+  for (int32_t i = 0; devs && i < dev_cap && i < n->n_dev; i++) devs[i] = n->dev[i];
   return KE_OK;
 }

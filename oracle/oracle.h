@@ -92,6 +92,11 @@ int64_t or_usage_percent(int64_t used, int64_t total);
 int or_quotas_load(or_cluster* c, const ke_quota_args* args, const ke_quota* q, int32_t n);
 int or_quota_state(const or_cluster* c, int32_t q, int64_t* limit, uint8_t* limit_has, int64_t* used,
                    int64_t* np_used);
+/* Unreserve / informer delete of one placement (same contract as ke_pod_release) */
+int or_pod_release(or_cluster* c, const ke_pod* pod, const ke_pod_allocation* a, int32_t mode);
+int or_debug_node_state(const or_cluster* c, int32_t node, ke_node* out, int32_t cpu_cap, ke_cpu* cpus,
+                        int32_t* n_cpus, int32_t zone_cap, ke_numa_zone* zones, int32_t* n_zones, int32_t dev_cap,
+                        ke_device* devs, int32_t* n_devs);
 
 #ifdef __cplusplus
 }

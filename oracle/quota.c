@@ -183,3 +183,45 @@ void orq_reserve(or_quotas* Q, const ke_pod* pod) {
     orq_load(Q, &args, q, Q->n);
   }
 }
+
+/* Unreserve (UnreservePod, group_quota_manager.go:965-981) of an assigned pod: used / non-preemptible used
+ * minus Mask(PodRequests, Max) on the quota and every ancestor, each floored at 0 (addUsedNonNegativeNoLock,
+ * quota_info.go:279-299); a system / default quota's smaller used grows the tree total back
+ * (updateClusterTotalResourceNoLock, :127-151).  `del` (OnPodDelete, :922-941): the pod's request leaves
+ * the quota's SelfRequest too (addRequestNonNegativeNoLock, quota_info.go:238-258) and the runtime is
+ * recomputed. */
+void orq_release(or_quotas* Q, const ke_pod* pod, int assigned, int del) {
+  if (pod->quota <= 0 || pod->quota > Q->n) return;
+  const int qi = pod->quota - 1;
+  int64_t req[KE_NRES], before[KE_NRES];
+  for (int r = 0; r < KE_NRES; r++) req[r] = pod_req(&Q->q[qi], pod, r), before[r] = Q->q[qi].used[r];
+  ke_quota_args args = Q->args;
+  int refresh = 0;
+  if (assigned) {
+    for (int a = qi; a >= 0; a = Q->q[a].parent)
+      for (int r = 0; r < KE_NRES; r++) {
+        int64_t u = Q->q[a].used[r] - req[r];
+        Q->q[a].used[r] = u > 0 ? u : 0;
+        if (pod->quota_non_preemptible) {
+          u = Q->q[a].non_preemptible_used[r] - req[r];
+          Q->q[a].non_preemptible_used[r] = u > 0 ? u : 0;
+        }
+      }
+    if (Q->q[qi].limit_is_max && Q->args.enable_runtime_quota) {
+      for (int r = 0; r < KE_NRES; r++) args.total[r] += before[r] - Q->q[qi].used[r];
+      refresh = 1;
+    }
+  }
+  if (del) {
+    for (int r = 0; r < KE_NRES; r++) {
+      const int64_t v = Q->q[qi].self_request[r] - req[r];
+      Q->q[qi].self_request[r] = v > 0 ? v : 0;
+    }
+    refresh = 1;
+  }
+  if (refresh) {
+    ke_quota q[KE_MAX_QUOTAS];
+    memcpy(q, Q->q, sizeof(ke_quota) * (size_t)Q->n);
+    orq_load(Q, &args, q, Q->n);
+  }
+}

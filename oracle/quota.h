@@ -16,4 +16,6 @@ int orq_load(or_quotas* Q, const ke_quota_args* args, const ke_quota* q, int32_t
 /* PreFilter: -1 = Skip (no quota), 1 = admitted, 0 = Unschedulable */
 int orq_admit(const or_quotas* Q, const ke_pod* pod);
 void orq_reserve(or_quotas* Q, const ke_pod* pod);
+/* Unreserve of an assigned pod (assigned) and/or its request leaving the tree (del, informer delete) */
+void orq_release(or_quotas* Q, const ke_pod* pod, int assigned, int del);
 #endif
