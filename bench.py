@@ -8,8 +8,9 @@ steps.  The node state is resident in HBM before the timed region starts.
 
 roofline: the per-batch pipeline.  The critical path is the Reserve chain (k_resolve_run,
 one workgroup, per-batch time from in-kernel s_memrealtime stamps); eval, select and fixup run beside it
-on the second stream.  `roofline` describes that dominant kernel, `roofline.kernels` every kernel of a
-batch and `roofline.end_to_end` the whole step, each as algorithmic bytes / time against 8 TB/s.
+on the second stream.  `roofline.achieved` = SURVEY.md §8(d)'s algorithmic bytes of a batch (N*S_row +
+B*S_pod + B*k*12) over that critical path; `roofline.replay` the replay's own bytes, `roofline.kernels`
+every kernel of a batch and `roofline.end_to_end` the whole step, each against 8 TB/s.
 `traffic` = HBM bytes from a prior rocprofv3 PMC pass of this workload (profiles/r02/pmc_bench.json).
 
 cpu_baseline: the oracle (C restatement of the Go plugins, oracle/) scheduling a prefix of the same
@@ -153,8 +154,16 @@ def cpu_baseline(cl, pods, cfg, seconds):
                       f"value = the fastest ({best} threads)"}
 
 
+def alg_batch_bytes(n_nodes, b):
+    """SURVEY.md §8(d) algorithmic bytes of one B-pod batch: the node SoA row once (S_row = ke_row_bytes()),
+    the pod records (S_pod = ke_pod_record_bytes()) and the top-k out (B * k * 12 B, k = KMAX)."""
+    row, pod = sizes()
+    return n_nodes * row + b * pod + b * KMAX * 12
+
+
 def roofline(n_nodes, b, ks, dt_step, batches_per_step, pipelined, tag):
-    """The dominant kernel's roofline (the Reserve chain) with the per-kernel and end-to-end fractions."""
+    """§8(d) roofline of a batch over its critical path (the Reserve chain: replay + hand-off per batch), with
+    the replay's own bytes, the per-kernel and the end-to-end fractions as sub-fields."""
     by = batch_bytes(n_nodes, b, ks["rows_fetched"], ks["rows_changed"], pipelined)
     ms = {"k_eval_batch": ks["eval_ms"], "k_select": ks["select_ms"], "k_fixup": ks["fixup_ms"],
           "k_resolve": ks["resolve_ms"]}
@@ -169,10 +178,18 @@ def roofline(n_nodes, b, ks, dt_step, batches_per_step, pipelined, tag):
                    "valu_busy": pmc.get("valu_busy"), "issue_stall_share": pmc.get("wave_issue_stall_share")}
     step_bytes = sum(by.values()) * batches_per_step
     dom = kern["k_resolve"]
-    return {"bound": "hbm", "kernel": "k_resolve_run (per 64-pod batch: prologue + sequential replay)",
-            "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": dom["frac"],
-            "traffic": dom["traffic"], "traffic_source": src, "bytes_per_launch": dom["bytes_per_batch"],
-            "launch_ms": dom["ms_per_batch"],
+    alg = alg_batch_bytes(n_nodes, b)
+    crit_ms = ks["resolve_ms"] + (ks["handoff_ms"] if pipelined else 0.0)
+    ach = alg / crit_ms / 1e6 if crit_ms else None
+    pmc_sum = sum(v["traffic"] for v in kern.values() if v.get("traffic")) or None
+    return {"bound": "hbm", "kernel": "k_resolve_run (the Reserve chain: the batch's critical path)",
+            "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS if ach else None,
+            "traffic": pmc_sum, "traffic_source": src, "bytes_per_launch": alg, "launch_ms": crit_ms,
+            "bytes_definition": "SURVEY.md §8(d) per B-pod batch: N*S_row + B*S_pod + B*k*12 "
+                                f"(S_row {sizes()[0]}, S_pod {sizes()[1]}, k {KMAX}); time = replay + hand-off per batch "
+                                "(in-kernel s_memrealtime); traffic = PMC HBM bytes of every kernel of a batch",
+            "replay": {"bytes_per_batch": dom["bytes_per_batch"], "ms_per_batch": dom["ms_per_batch"],
+                       "achieved": dom["achieved"], "frac": dom["frac"], "traffic": dom["traffic"]},
             "timing": "k_resolve / k_fixup: in-kernel s_memrealtime per batch (one persistent launch per run); "
                       "k_eval_batch / k_select: HIP events on the eval stream",
             "kernels": kern,

@@ -821,6 +821,9 @@ int ke_debug_resolve_phases(ke_ctx* ctx, double* phases6);
  * last call — best unchanged candidate, row fetch issue, re-evaluation, its wave max, decision / adoption,
  * Reserve, next pod's changed flags — and the pod count (cyc8[7]); zeros in the product build. */
 int ke_debug_replay_phases(ke_ctx* ctx, double* cyc8);
+/* Speculative replay of plain batches: rounds per batch of the last ke_schedule that ended at a
+ * failed prediction (0 = every pod of the batch took its best candidate not taken before). */
+int ke_debug_spec_failed(ke_ctx* ctx, double* per_batch);
 /* Number of nodes whose replay record (the Reserve replay's row-major copy of the node-only terms)
  * differs from one derived from the node's current device row (0 = consistent). */
 int ke_debug_check_records(ke_ctx* ctx, int64_t now_ns, int64_t* mismatched_nodes);

@@ -730,6 +730,12 @@ int ke_debug_replay_phases(ke_ctx* ctx, double* cyc8) {
   return device_replay_phases(&ctx->c, cyc8);
 }
 
+int ke_debug_spec_failed(ke_ctx* ctx, double* per_batch) {
+  if (!ctx || !per_batch) return fail(KE_ERR_INVALID, "ke_debug_spec_failed arguments");
+  *per_batch = ctx->c.kstat_spec_failed;
+  return KE_OK;
+}
+
 int ke_debug_check_records(ke_ctx* ctx, int64_t now_ns, int64_t* mismatched_nodes) {
   if (!ctx || !mismatched_nodes) return fail(KE_ERR_INVALID, "ke_debug_check_records arguments");
   flush_mirror(ctx->c);

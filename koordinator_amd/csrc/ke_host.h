@@ -75,6 +75,7 @@ struct Context {
   double kstat_eval_ms = 0, kstat_select_ms = 0, kstat_resolve_ms = 0, kstat_fixup_ms = 0, kstat_handoff_ms = 0;
   int32_t last_pipelined = 0;
   int32_t last_ds_cuts = 0;  // DeviceShare batches of the last ke_schedule that stopped early (re-run remainders)
+  double kstat_spec_failed = 0;  // per batch: speculative-replay rounds that ended at a failed prediction
   double kstat_rows_fetched = 0, kstat_rows_changed = 0;  // per batch: replay records fetched (best unchanged candidates), rows changed
   double last_enqueue_ms = 0;  // host time spent enqueueing the last ke_schedule's launches
   // host wall ms of the last ke_schedule by phase: argument checks, row refresh, pod upload, launch

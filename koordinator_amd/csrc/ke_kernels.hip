@@ -3550,6 +3550,15 @@ __device__ __forceinline__ uint64_t ds_reserve_wave(const SoA& s, int64_t i, con
   return out;
 }
 
+// The speculative replay's round state (replay_spec): per pod its predicted node / snapshot key, the best
+// current key among the nodes earlier pods of the batch took, and the round's first failing pod.
+struct SpecLds {
+  int32_t xnode[MAX_BATCH];  // pod j's predicted (then committed) node, -1 = none
+  uint32_t xkey[MAX_BATCH];  // its snapshot candidate key (the best unchanged candidate), 0 = none
+  uint32_t mrow[MAX_BATCH];  // max key of pod j over the nodes pods < j took, in their current state
+  int32_t jf;                // first pod of the round whose prediction failed (end of round: none)
+};
+
 struct ResLds {
   uint32_t cand[MAX_BATCH * KMAX];
   DevPod pod[MAX_BATCH];
@@ -3557,8 +3566,175 @@ struct ResLds {
   int32_t cnt[MAX_BATCH];
   uint32_t dsm[MAX_BATCH];  // DeviceShare batch: 1 + snapshot max raw score of each pod (0: none / not DS)
   int32_t dsc[MAX_BATCH];   // ... and the number of its feasible nodes attaining it
+  SpecLds sp;
   uint32_t chg[CHG_LDS_WORDS];
 };
+
+// a changed-set bit that a failed prediction set (several lanes may share a word)
+__device__ __forceinline__ void chg_unset(const ChgSet& c, int node) {
+  if (c.glb) __hip_atomic_fetch_and(c.glb + (node >> 5), ~(1u << (node & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else __hip_atomic_fetch_and(c.lds + (node >> 5), ~(1u << (node & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Speculative replay of a plain batch (LoadAware + NodeNUMAResource (+ FitPlus / SRA) pods, no quota) on
+// every wave of the workgroup ("speculative replay").  The sequential replay decides pod j as
+// max(bu_j, bc_j): bu_j its best candidate no earlier pod of the batch took (exact: its snapshot key), bc_j
+// the best current key among the nodes earlier pods took.  Almost every pod takes its bu_j, so a round
+//   P  predicts that every pod of a window does (wave 0: bu_j from its sorted list minus the nodes of the
+//      earlier predictions -- a ballot per pod),
+//   R  builds in lane c of every wave the record of pod c's predicted node after pod c's Reserve,
+//   S  evaluates every pod j of the window against the slots c < j in parallel (rows spread over the waves;
+//      one fast_total pass per row, wave max -> mrow[j]),
+//   V  checks the predictions in order: pod j's holds iff xkey[j] > mrow[j] (keys are unique per node; both
+//      0: unschedulable).  Up to the first failing pod jf every prediction is the sequential decision (its
+//      state is the predicted one); pod jf takes the changed node of mrow[jf] (Reserve on that slot), the
+//      predictions after it are dropped, and the next round starts at jf + 1 with a smaller window.
+// Lane c of every wave holds slot c: the node pod c took (valid when pod c took a node no earlier pod had),
+// in its current state -- every wave applies the same Reserves, so no slot crosses waves.
+template <bool EXT>
+__device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const SoA& s, const int base, const int B,
+                                            const KArgs& k, int32_t* __restrict__ chosen,
+                                            int32_t* __restrict__ chosen_score, int32_t global_offset,
+                                            uint64_t* __restrict__ stamps, int batch_index,
+                                            uint64_t* __restrict__ dev_alloc, int64_t* __restrict__ touched_out,
+                                            int32_t* __restrict__ touched_cnt, uint64_t* __restrict__ pst) {
+  constexpr int NW = res_threads<false>() / 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool ext = EXT && (k.flags & AF_EXT);
+  NodeFast slot;  // lane c: the node pod c took, after every Reserve on it so far
+  bool sv = false;
+  int snode = -1;
+  int32_t o_node = -1, o_score = -1;  // wave 0, lane j: pod j's placement
+  int start = 0, win = B, rounds = 0, fetched = 0;
+  while (start < B) {
+    const int end = min(B, start + win);
+    // ---- P (wave 0): pods [start, end) each take their best candidate not taken before
+    if (wave == 0) {
+      uint32_t ck = L.cand[start * KMAX + lane];
+      bool fl = ck != 0 && chg_test(C, key_node(ck));
+      for (int j = start; j < end; j++) {
+        // pod j+1's list and flags (the bits of pods < j are set: LDS operations of a wave run in order);
+        // pod j's own prediction is compared below
+        const uint32_t ckn = j + 1 < end ? L.cand[(j + 1) * KMAX + lane] : 0u;
+        const bool fln = ckn != 0 && chg_test(C, key_node(ckn));
+        const uint64_t m = __ballot(ck != 0 && !fl);
+        const uint32_t bu = m ? (uint32_t)__builtin_amdgcn_readlane((int)ck, __ffsll((unsigned long long)m) - 1) : 0u;
+        const int xn = bu ? key_node(bu) : -1;
+        if (lane == 0) {
+          L.sp.xnode[j] = xn;
+          L.sp.xkey[j] = bu;
+          if (xn >= 0) chg_set(C, xn);
+        }
+        ck = ckn;
+        fl = fln || (ckn != 0 && xn >= 0 && key_node(ckn) == xn);
+      }
+    }
+    __syncthreads();
+    // ---- R (every wave): lane c in [start, end) adopts pod c's predicted node and reserves pod c on it
+    if (lane >= start && lane < end) {
+      snode = L.sp.xnode[lane];
+      sv = snode >= 0;
+      if (sv) {
+        rec_load(s.rec + (int64_t)snode * NUM_RW, slot);
+        if (ext) ext_load(s, snode, k, slot);
+        fast_adopt(slot, k);
+        const DevPod pc = L.pod[lane];
+        const double ed[2] = {L.pd[lane][0], L.pd[lane][1]}, rd[2] = {L.pd[lane][2], L.pd[lane][3]};
+        fast_reserve(slot, pc, ed, rd);
+        if (ext)
+#pragma unroll
+          for (int q = 0; q < 4; q++) slot.xr[q] += q < k.fp_n ? pc.xreq[q] : 0;
+      }
+    }
+    if (wave == 0) fetched += __popcll(__ballot(lane >= start && lane < end && sv));
+    // ---- S (rows over the waves): pod j against every slot c < j
+    for (int j = start + wave; j < end; j += NW) {
+      const DevPod p = L.pod[j];
+      const double ed[2] = {L.pd[j][0], L.pd[j][1]}, rd[2] = {L.pd[j][2], L.pd[j][3]};
+      uint32_t kc = 0;
+      if (sv && lane < j) kc = make_key(fast_total<EXT>(slot, p, ed, rd, k), snode);
+      const uint32_t mx = wave_max_u32(kc);
+      if (lane == 0) L.sp.mrow[j] = mx;
+    }
+    __syncthreads();
+    // ---- V (wave 0): the first pod whose best changed node beats its prediction
+    if (wave == 0) {
+      const bool in = lane >= start && lane < end;
+      const uint32_t xk = in ? L.sp.xkey[lane] : 0u, mk = in ? L.sp.mrow[lane] : 0u;
+      const uint64_t bad = __ballot(in && mk > xk);
+      const int jf = bad ? __ffsll((unsigned long long)bad) - 1 : end;
+      if (lane >= start && lane < jf) {
+        const int xn = L.sp.xnode[lane];
+        o_node = xn >= 0 ? xn + global_offset : -1;
+        o_score = xk ? key_score(xk) : -1;
+      }
+      if (lane == jf && jf < end) {  // pod jf takes the changed node of its best current key
+        o_node = key_node(mk) + global_offset;
+        o_score = key_score(mk);
+      }
+      if (lane >= jf && lane < end) {  // predictions that did not happen leave the changed set
+        const int xn = L.sp.xnode[lane];
+        if (xn >= 0) chg_unset(C, xn);
+      }
+      if (lane == 0) L.sp.jf = jf;
+    }
+    __syncthreads();
+    const int jf = L.sp.jf;
+    if (jf < end) {
+      if (lane >= jf && lane < end) sv = false;
+      const int wn = key_node(L.sp.mrow[jf]);
+      if (sv && snode == wn) {  // pod jf's Reserve on that slot (every wave keeps its copy)
+        const DevPod pc = L.pod[jf];
+        const double ed[2] = {L.pd[jf][0], L.pd[jf][1]}, rd[2] = {L.pd[jf][2], L.pd[jf][3]};
+        fast_reserve(slot, pc, ed, rd);
+        if (ext)
+#pragma unroll
+          for (int q = 0; q < 4; q++) slot.xr[q] += q < k.fp_n ? pc.xreq[q] : 0;
+      }
+      win = max(8, 2 * (jf - start + 1));
+      start = jf + 1;
+      rounds++;
+    } else {
+      start = end;
+      win = min(MAX_BATCH, 2 * win);
+    }
+  }
+  if (wave != 0) return;
+  if (lane < B) {
+    chosen[base + lane] = o_node;
+    chosen_score[base + lane] = o_score;
+    dev_alloc[base + lane] = 0;
+  }
+  // the changed nodes' rows back to the SoA, their replay records, the compact list for the next k_fixup
+  const uint64_t vm = __ballot(sv);
+  if (sv) {
+    const int64_t st = s.stride;
+    int64_t* f = s.f + snode;
+#pragma unroll
+    for (int v = 0; v < 2; v++)
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        st_sc1(f + (F_FH + 2 * v + q) * st, slot.fh[v][q]);
+        st_sc1(f + (F_SA + 2 * v + q) * st, (int64_t)slot.sa[v][q]);
+      }
+    st_sc1(f + (F_NREQ + 0) * st, (int64_t)slot.nreq[0]);
+    st_sc1(f + (F_NREQ + 1) * st, (int64_t)slot.nreq[1]);
+    rec_store_dyn<__HIP_MEMORY_SCOPE_WORKGROUP>(s.rec + (int64_t)snode * NUM_RW, slot);
+    if (ext)
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if (q < k.fp_n) st_sc1(s.xf + (XF_REQ + q) * st + snode, slot.xr[q]);
+    if (touched_out) rec_store_full(touched_out + (int64_t)lanes_below(vm) * NUM_RW, slot, snode);
+    chg_clear_word(C, snode);  // every bit still set belongs to a taken node
+  }
+  if (touched_out && lane == 0) st_sc1(touched_cnt, (int32_t)__popcll(vm));
+  if (lane == 0) {
+    stamps[batch_index + 1] = __builtin_amdgcn_s_memrealtime();
+    pst[6] = (uint64_t)(uint32_t)fetched | ((uint64_t)rounds << 32);  // records fetched | failed rounds
+    pst[7] = (uint64_t)__popcll(vm);
+  }
+  drain_stores();
+}
 
 // zero the LDS bitmap words of node ids [0, n_nodes) (all threads; once per launch)
 __device__ __forceinline__ ChgSet chg_init(ResLds& L, uint32_t* glb, int n_nodes) {
@@ -3620,6 +3796,13 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
   if (tid == 0) {
     const uint64_t t = __builtin_amdgcn_s_memrealtime();
     for (int u = 1; u < 6; u++) pstamps[8 * batch_index + u] = t;
+  }
+  if constexpr (!DS && !NUMA && !QUOTA) {  // plain batch: the speculative replay on every wave
+    __builtin_amdgcn_s_setprio(3);
+    replay_spec<EXT>(L, C, s, base, B, k, chosen, chosen_score, global_offset, stamps, batch_index, dev_alloc,
+                     touched_out, touched_cnt, pstamps + 8 * batch_index);
+    __builtin_amdgcn_s_setprio(0);
+    return;
   }
   if (tid >= 64) return;  // the replay is one wavefront: wave-level ordering only from here on
   // the next batch's eval waves may share this SIMD (pipelined schedule): the replay issues first
@@ -5413,10 +5596,13 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   }
   ctx->kstat_resolve_ms = n_batches ? res_sum / n_batches : 0;
   double rows_fetched = 0, rows_changed = 0;
+  double spec_rounds = 0;
   for (int b = 0; b < n_batches; b++) {
-    rows_fetched += (double)pst[8 * (size_t)b + 6];
+    rows_fetched += (double)(pst[8 * (size_t)b + 6] & 0xFFFFFFFFull);
+    spec_rounds += (double)(pst[8 * (size_t)b + 6] >> 32);
     rows_changed += (double)pst[8 * (size_t)b + 7];
   }
+  ctx->kstat_spec_failed = n_batches ? spec_rounds / n_batches : 0;
   ctx->kstat_rows_fetched = n_batches ? rows_fetched / n_batches : 0;
   ctx->kstat_rows_changed = n_batches ? rows_changed / n_batches : 0;
   ctx->kstat_fixup_ms = fx_n ? fx_sum / fx_n : 0;

@@ -278,11 +278,13 @@ class Evaluator:
         self._check(self.lib.ke_last_kernel_stats_ex(self.h, abi.ptr(ms4), C.byref(n), C.byref(npipe)))
         p, r = C.c_double(), C.c_double()
         self._check(self.lib.ke_last_resolve_split(self.h, C.byref(p), C.byref(r)))
+        sf = C.c_double()
+        self._check(self.lib.ke_debug_spec_failed(self.h, C.byref(sf)))
         ph = np.zeros(6, np.float64)
         self._check(self.lib.ke_debug_resolve_phases(self.h, abi.ptr(ph)))
         return {"eval_ms": ms4[0], "select_ms": ms4[1], "fixup_ms": ms4[2], "resolve_ms": ms4[3], "samples": n.value,
                 "pipelined_batches": npipe.value, "enqueue_ms": ms4[4], "handoff_ms": ms4[5],
-                "rows_fetched": ms4[6], "rows_changed": ms4[7],
+                "rows_fetched": ms4[6], "rows_changed": ms4[7], "spec_failed_rounds": sf.value,
                 "resolve_prologue_ms": p.value, "resolve_replay_ms": r.value,
                 "resolve_phases_ms": dict(zip(["init", "cand_copy", "hash", "lookup", "rows", "replay"],
                                               ph.tolist()))}

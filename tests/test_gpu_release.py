@@ -177,21 +177,24 @@ def test_default_quota_pod_last_and_alone(gpu):
     calls = [np.concatenate([rest[:60], sys_pods[:1]]),  # the system pod ends the queue
              sys_pods[1:2],                              # alone: n_pods == 1
              rest[60:120], rest[120:], sys_pods[2:3]]
+    def same_quotas():
+        for i in range(len(quotas)):
+            a, b = ev.quota_state(i), o.quota_state(i)
+            for k in ("limit", "used", "np_used"):
+                assert np.array_equal(a[k], b[k]), (i, k)
+
+    unreserved = 0
     for idx in calls:
         q = pods[idx]
         c1, s1 = ev.schedule(q, synth.T0)
         c0, s0 = o.schedule(q, synth.T0)
         assert np.array_equal(c1, c0) and np.array_equal(s1, s0), np.argwhere(c1 != c0)[:5].ravel().tolist()
-        for i in range(len(quotas)):
-            a, b = ev.quota_state(i), o.quota_state(i)
-            for k in ("limit", "used", "np_used"):
-                assert np.array_equal(a[k], b[k]), (i, k)
-    # and the system pod's Unreserve grows the total back
-    a0 = o.last_allocations()
-    assert c1[0] >= 0 and a0[0]["quota_assigned"]
-    ev.unreserve(pods[calls[-1][0]], 0)
-    o.release(pods[calls[-1][0]], a0[0])
-    for i in range(len(quotas)):
-        a, b = ev.quota_state(i), o.quota_state(i)
-        for k in ("limit", "used", "np_used"):
-            assert np.array_equal(a[k], b[k]), (i, k)
+        same_quotas()
+        if len(idx) == 1 and c1[0] >= 0:  # the placed system pod's Unreserve grows the total back
+            a0 = o.last_allocations()
+            assert a0[0]["quota_assigned"]
+            ev.unreserve(pods[idx[0]], 0)
+            o.release(pods[idx[0]], a0[0])
+            same_quotas()
+            unreserved += 1
+    assert unreserved >= 1
