@@ -405,6 +405,16 @@ bool total_value(const std::map<std::string, __int128>& t, const std::string& na
   return true;
 }
 
+// schedutil.IsScalarResourceName (k8s v1.28 pkg/apis/core/v1/helper): an extended resource (a qualified name
+// with a domain outside kubernetes.io, not "requests."-prefixed), a hugepages-* resource, a kubernetes.io/
+// prefixed native resource or an attachable-volumes-* resource
+bool scalar_resource_name(const std::string& n) {
+  if (n.rfind("hugepages-", 0) == 0 || n.rfind("attachable-volumes-", 0) == 0) return true;
+  if (n.find("kubernetes.io/") != std::string::npos) return true;
+  const size_t slash = n.find('/');
+  return slash != std::string::npos && slash > 0 && slash + 1 < n.size() && n.rfind("requests.", 0) != 0;
+}
+
 // k8s GetPodQOS (pkg/apis/core/v1/helper/qos, v1.28) over cpu / memory of containers + init containers
 int kube_qos(const std::vector<Container>& cs, const std::vector<Container>& ics) {  // 0 Guaranteed 1 Burstable 2 BE
   std::map<std::string, __int128> req, lim;
@@ -507,21 +517,30 @@ int ke_decode_pod(const char* js, int64_t len, int32_t n_names, const char* cons
     if (it == reqs.end() || it->second <= 0) continue;
     p.xres_request_mask |= 1ull << id;
     if (p.n_xres >= KE_MAX_POD_XRES) return unsup("more than 8 requested resource names");
-    // GetNonzeroRequestForResource per container (100m cpu / 200Mi memory when the key is missing)
-    auto nz = [&](const Container& c) -> __int128 {
+    // calculatePodResourceRequest adds Spec.Overhead[name].Value() behind the PodOverhead feature gate
+    // (node_resource_fit_plus_utils.go:157-162), which k8s v1.28 no longer registers: not modelled
+    if (overhead.q.count(nm)) return unsup("spec.overhead on a NodeResourcesFitPlus / ScarceResourceAvoidance resource");
+    // GetNonzeroRequestForResource per container, each rounded as Quantity.MilliValue() (cpu) / Value() before
+    // the sum (node_resource_fit_plus_utils.go:140-203): 100m cpu / 200Mi memory for a container without the
+    // key, 0 for a name that is not a scalar resource (schedutil.IsScalarResourceName)
+    const bool scalar = nm == "cpu" || nm == "memory" || nm == "ephemeral-storage" || scalar_resource_name(nm);
+    bool range_ok = true;
+    auto nz = [&](const Container& c) -> int64_t {
       auto f = c.req.q.find(nm);
-      if (f != c.req.q.end()) return f->second;
-      if (nm == "cpu") return (__int128)100 * 1000000;                    // 100m in nanos
-      if (nm == "memory") return (__int128)200 * 1048576 * 1000000000;    // 200Mi in nanos
-      return 0;
+      if (f == c.req.q.end()) return nm == "cpu" ? 100 : nm == "memory" ? 200LL * 1048576 : 0;
+      int64_t v, m;
+      if (!nanos_value(f->second, &v, &m)) range_ok = false;
+      return nm == "cpu" ? m : v;
     };
-    __int128 s = 0;
-    for (const Container& c : cs) s += nz(c);
-    for (const Container& c : ics) s = std::max(s, nz(c));
-    int64_t v, m;
-    if (!nanos_value(s, &v, &m)) return unsup("pod request out of range");
+    int64_t s = 0;
+    if (scalar) {
+      for (const Container& c : cs)
+        if (__builtin_add_overflow(s, nz(c), &s)) range_ok = false;
+      for (const Container& c : ics) s = std::max(s, nz(c));
+    }
+    if (!range_ok) return unsup("pod request out of range");
     p.xres_id[p.n_xres] = id;
-    p.xres_value[p.n_xres++] = nm == "cpu" ? m : v;
+    p.xres_value[p.n_xres++] = s;
   }
   // classes (GetPodPriorityClassWithDefault, GetPodQoSClassRaw)
   static const char* QOS[] = {"", "LSE", "LSR", "LS", "BE", "SYSTEM"};
@@ -541,7 +560,15 @@ int ke_decode_pod(const char* js, int64_t len, int32_t n_names, const char* cons
   if (pc == KE_PRIORITY_NONE) {  // GetPodQoSClassWithKubeQoS -> priority by QoS
     int q = p.qos_class;
     static const int BY_KUBE_QOS[3] = {KE_QOS_LSR, KE_QOS_LS, KE_QOS_BE};  // Guaranteed / Burstable / BestEffort
-    if (q == KE_QOS_NONE) q = BY_KUBE_QOS[kube_qos(cs, ics)];
+    if (q == KE_QOS_NONE) {  // GetKubeQosClass: Status.QOSClass when set, else computed (qos_utils.go:72-78)
+      const std::string sq = str_or_empty(status ? status->field("qosClass") : nullptr);
+      int kq = -1;
+      if (sq == "Guaranteed") kq = 0;
+      else if (sq == "Burstable") kq = 1;
+      else if (sq == "BestEffort") kq = 2;
+      else if (!sq.empty()) return unsup("status.qosClass \"" + sq + "\"");
+      q = BY_KUBE_QOS[kq >= 0 ? kq : kube_qos(cs, ics)];
+    }
     pc = (q == KE_QOS_SYSTEM || q == KE_QOS_LSE || q == KE_QOS_LSR || q == KE_QOS_LS) ? KE_PRIORITY_PROD
          : q == KE_QOS_BE ? KE_PRIORITY_BATCH : KE_PRIORITY_NONE;
   }

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstddef>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -214,7 +215,7 @@ int ptable_intern(Context& c, int32_t n, const ke_gpu_partition* parts) {
   }
   const size_t n_tab = c.ptab.size() / PT_WORDS;
   for (size_t id = 0; id < n_tab; id++)
-    if (std::equal(t.begin(), t.end(), c.ptab.begin() + (ptrdiff_t)(id * PT_WORDS))) return (int)id;
+    if (std::equal(t.begin(), t.end(), c.ptab.begin() + (std::ptrdiff_t)(id * PT_WORDS))) return (int)id;
   if (n_tab >= (size_t)MAX_PTABLES) return fail(KE_ERR_UNSUPPORTED, "more than 4096 distinct GPU partition tables");
   c.ptab.insert(c.ptab.end(), t.begin(), t.end());
   c.ptab_dirty = true;

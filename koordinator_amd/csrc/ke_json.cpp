@@ -592,7 +592,11 @@ bool parse_rfc3339(const std::string& s, int64_t* ns) {
   }
   if (i != s.size()) return false;
   const int64_t secs = days_from_civil(Y, (unsigned)M, (unsigned)D) * 86400 + h * 3600 + m * 60 + sec - off;
-  *ns = secs * 1000000000LL + frac;
+  // int64 unix nanoseconds cover 1677-09-21 .. 2262-04-11 (Go: UnixNano undefined outside); later times are
+  // not representable here
+  int64_t t;
+  if (__builtin_mul_overflow(secs, (int64_t)1000000000, &t) || __builtin_add_overflow(t, frac, &t)) return false;
+  *ns = t;
   return true;
 }
 

@@ -3580,8 +3580,8 @@ __device__ __forceinline__ void chg_unset(const ChgSet& c, int node) {
 // every wave of the workgroup ("speculative replay").  The sequential replay decides pod j as
 // max(bu_j, bc_j): bu_j its best candidate no earlier pod of the batch took (exact: its snapshot key), bc_j
 // the best current key among the nodes earlier pods took.  Almost every pod takes its bu_j, so a round
-//   P  predicts that every pod of a window does (wave 0: bu_j from its sorted list minus the nodes of the
-//      earlier predictions -- a ballot per pod),
+//   P  predicts that every pod of a window does (wave 0: bu_j = the max of its list minus the nodes of the
+//      earlier predictions -- one wave max per pod),
 //   R  builds in lane c of every wave the record of pod c's predicted node after pod c's Reserve,
 //   S  evaluates every pod j of the window against the slots c < j in parallel (rows spread over the waves;
 //      one fast_total pass per row, wave max -> mrow[j]),
@@ -3617,8 +3617,7 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
         // pod j's own prediction is compared below
         const uint32_t ckn = j + 1 < end ? L.cand[(j + 1) * KMAX + lane] : 0u;
         const bool fln = ckn != 0 && chg_test(C, key_node(ckn));
-        const uint64_t m = __ballot(ck != 0 && !fl);
-        const uint32_t bu = m ? (uint32_t)__builtin_amdgcn_readlane((int)ck, __ffsll((unsigned long long)m) - 1) : 0u;
+        const uint32_t bu = wave_max_u32(fl ? 0u : ck);  // lists from k_select are unordered
         const int xn = bu ? key_node(bu) : -1;
         if (lane == 0) {
           L.sp.xnode[j] = xn;

@@ -163,15 +163,16 @@ def qos_raw(labels):
     return QOS_BY_NAME.get(labels.get("koordinator.sh/qosClass"), abi.QOS_NONE)
 
 
-def priority_class_with_default(labels, spec_priority, containers, init_containers=()):
-    """GetPodPriorityClassWithDefault (priority_utils.go:37-58)."""
+def priority_class_with_default(labels, spec_priority, containers, init_containers=(), status_qos=None):
+    """GetPodPriorityClassWithDefault (priority_utils.go:37-58); the kube QoS class is Status.QOSClass when set
+    (GetKubeQosClass, qos_utils.go:72-78)."""
     p = priority_class_raw(labels, spec_priority)
     if p != abi.PRIORITY_NONE:
         return p
     q = qos_raw(labels)
     if q == abi.QOS_NONE:  # GetPodQoSClassWithKubeQoS
         q = {"Guaranteed": abi.QOS_LSR, "Burstable": abi.QOS_LS, "BestEffort": abi.QOS_BE}[
-            kube_qos(containers, init_containers)]
+            status_qos or kube_qos(containers, init_containers)]
     if q in (abi.QOS_SYSTEM, abi.QOS_LSE, abi.QOS_LSR, abi.QOS_LS):
         return abi.PRIORITY_PROD
     if q == abi.QOS_BE:
@@ -206,13 +207,25 @@ def xres_id(name):
     return XRES_IDS[name]
 
 
+def is_scalar_resource_name(name):
+    """schedutil.IsScalarResourceName (k8s v1.28): extended (qualified, domain outside kubernetes.io, not
+    "requests."-prefixed), hugepages-*, kubernetes.io/-prefixed native or attachable-volumes-* resources."""
+    if name.startswith(("hugepages-", "attachable-volumes-")) or "kubernetes.io/" in name:
+        return True
+    i = name.find("/")
+    return 0 < i < len(name) - 1 and not name.startswith("requests.")
+
+
 def _nonzero_request(name, requests):
-    """GetNonzeroRequestForResource (node_resource_fit_plus_utils.go:167-203)."""
+    """GetNonzeroRequestForResource (node_resource_fit_plus_utils.go:167-203): one container's request, rounded
+    as Quantity.MilliValue() / Value()."""
     requests = requests or {}
     if name == "cpu":
         return milli_value(requests["cpu"]) if "cpu" in requests else DEFAULT_MILLI_CPU_REQUEST
     if name == "memory":
         return value(requests["memory"]) if "memory" in requests else DEFAULT_MEMORY_REQUEST
+    if name != "ephemeral-storage" and not is_scalar_resource_name(name):
+        return 0
     return value(requests[name]) if name in requests else 0
 
 
@@ -261,7 +274,7 @@ def make_pod(name="pod", namespace="default", requests=None, limits=None, contai
              custom_seconds_after_scheduled=None, custom_seconds_after_initialized=None,
              terminated=False, numa_policy=None, numa_exclusive=None, cpu_bind_required=None,
              cpu_bind_preferred=None, cpu_exclusive=None, gpu_partition_spec=None, device_hints=None,
-             device_joint_allocate=None):
+             device_joint_allocate=None, status_qos=None):
     """A pod as the plugins see it.  `requests`/`limits` describe one container (MakePod().Req());
     `containers` gives the full list.  Times are ns.  numa_policy / numa_exclusive: the
     scheduling.koordinator.sh/numa-topology-spec annotation ('BestEffort' | 'Restricted' |
@@ -300,7 +313,7 @@ def make_pod(name="pod", namespace="default", requests=None, limits=None, contai
     if initialized_at is not None:
         p.has_initialized = 1
         p.initialized_transition_ns = int(initialized_at)
-    p.priority_class = priority_class_with_default(labels, priority, containers, init_containers)
+    p.priority_class = priority_class_with_default(labels, priority, containers, init_containers, status_qos)
     p.qos_class = qos_raw(labels)
     p.is_daemonset = 1 if owner_kind == "DaemonSet" else 0
     p.is_terminated = 1 if terminated else 0

@@ -252,6 +252,9 @@ def random_pod(rng, i):
     if rng.random() < 0.1:
         overhead = {"cpu": "100m", "memory": "64Mi"}
         spec["overhead"] = overhead
+    status_qos = None
+    if rng.random() < 0.3:  # Status.QOSClass as the apiserver reports it (may disagree with the containers)
+        status_qos = str(rng.choice(["Guaranteed", "Burstable", "BestEffort"]))
     owner = "DaemonSet" if rng.random() < 0.1 else "ReplicaSet"
     sched = 1_700_000_000 * 10**9 + i * 10**9
     doc = {"metadata": {"name": f"p{i}", "namespace": "ns", "uid": f"uid-{i}", "labels": labels, "annotations": ann,
@@ -259,10 +262,12 @@ def random_pod(rng, i):
            "spec": spec,
            "status": {"phase": "Running", "conditions": [{"type": "PodScheduled", "status": "True",
                                                           "lastTransitionTime": "2023-11-14T22:13:%02dZ" % (20 + i % 40)}]}}
+    if status_qos:
+        doc["status"]["qosClass"] = status_qos
     kw = dict(containers=[{"requests": c["resources"]["requests"], "limits": c["resources"]["limits"]} for c in cs],
               init_containers=[{"requests": c["resources"]["requests"]} for c in ics], overhead=overhead,
               priority=prio, labels=labels, owner_kind=owner, custom_factors=factors, numa_policy=numa,
-              cpu_bind_preferred=bind, cpu_exclusive=excl)
+              cpu_bind_preferred=bind, cpu_exclusive=excl, status_qos=status_qos)
     return doc, kw
 
 
@@ -275,6 +280,11 @@ def test_pod_random_vs_model(lib):
     table = sorted(model.XRES_IDS, key=model.XRES_IDS.get)
     for i in range(300):
         doc, kw = random_pod(rng, i)
+        if kw["overhead"]:  # calculatePodResourceRequest's Overhead term (PodOverhead gate): refused
+            with pytest.raises(decode.DecodeError) as e:
+                decode.decode_pod(doc, table)
+            assert e.value.code == abi.ERR_UNSUPPORTED
+            continue
         got = decode.decode_pod(doc, table)
         want = model.make_pod(**kw)
         want.quota_non_preemptible = 1 if kw["labels"].get("quota.scheduling.koordinator.sh/preemptible") == "false" else 0
@@ -342,4 +352,39 @@ def test_device_vs_model(lib):
     assert parts.tobytes() == wt.tobytes()
     with pytest.raises(decode.DecodeError) as e:
         decode.decode_device({"spec": {"devices": [{"type": "npu", "minor": 0, "health": True}]}})
+    assert e.value.code == abi.ERR_UNSUPPORTED
+
+
+def test_pod_status_qos_class_first(lib):
+    """GetKubeQosClass reads Status.QOSClass before computing it (qos_utils.go:72-78): a Burstable-looking pod
+    reported Guaranteed defaults to LSR -> koord-prod; reported BestEffort -> koord-batch."""
+    base = {"metadata": {"name": "q", "namespace": "n"},
+            "spec": {"containers": [{"resources": {"requests": {"cpu": "1"}}}]}}
+    assert decode.decode_pod(base).priority_class == abi.PRIORITY_PROD  # computed Burstable -> LS -> prod
+    doc = dict(base, status={"qosClass": "BestEffort"})
+    assert decode.decode_pod(doc).priority_class == abi.PRIORITY_BATCH
+    with pytest.raises(decode.DecodeError):
+        decode.decode_pod(dict(base, status={"qosClass": "Platinum"}))
+
+
+def test_pod_fitplus_request_rounding_and_names(lib):
+    """calculatePodResourceRequest (node_resource_fit_plus_utils.go:140-203): each container's value is
+    rounded (MilliValue / Value) before the sum; a name that is not a scalar resource counts 0."""
+    names = ["cpu", "memory", "pods", "example.com/dev", "ephemeral-storage"]
+    doc = {"metadata": {"name": "r", "namespace": "n"}, "spec": {"containers": [
+        {"resources": {"requests": {"cpu": "100100u", "memory": "1500m", "pods": "1", "example.com/dev": "1"}}},
+        {"resources": {"requests": {"cpu": "100100u", "memory": "1500m", "example.com/dev": "2"}}}]}}
+    p = decode.decode_pod(doc, names)
+    got = dict(zip(p.xres_id[:p.n_xres], p.xres_value[:p.n_xres]))
+    assert got[0] == 202  # ceil(100.1m) = 101m per container (the PodRequests total would round to 201m)
+    assert got[1] == 4    # ceil(1.5) = 2 bytes per container
+    assert got[2] == 0    # "pods" is not a scalar resource
+    assert got[3] == 3
+    assert p.xres_request_mask == 0b1111
+    want = model.make_pod(containers=[{"requests": {"cpu": "100100u", "memory": "1500m", "pods": "1", "example.com/dev": "1"}},
+                                      {"requests": {"cpu": "100100u", "memory": "1500m", "example.com/dev": "2"}}])
+    assert sorted(want.xres_value[:want.n_xres]) == sorted(got.values())
+    with pytest.raises(decode.DecodeError) as e:  # overhead on a requested name: refused
+        decode.decode_pod({"spec": {"containers": [{"resources": {"requests": {"cpu": "1"}}}],
+                                    "overhead": {"cpu": "100m"}}}, names)
     assert e.value.code == abi.ERR_UNSUPPORTED
