@@ -2400,6 +2400,7 @@ __device__ __forceinline__ void fast_adopt(NodeFast& f, const KArgs& k) {
 
 // a record from the replay's record array (workgroup-scope loads: this workgroup may have rewritten it
 // in an earlier batch; another launch wrote it before this one started)
+__device__ __forceinline__ void rec_unpack(const int64_t (&w)[NUM_RW], NodeFast& f);
 template <int SCOPE = __HIP_MEMORY_SCOPE_WORKGROUP>
 __device__ __forceinline__ void rec_load(const int64_t* __restrict__ rec, NodeFast& f) {
   int64_t w[NUM_RW];
@@ -2407,6 +2408,22 @@ __device__ __forceinline__ void rec_load(const int64_t* __restrict__ rec, NodeFa
   // and the reuse would wait for it)
 #pragma unroll
   for (int u = 0; u < RW_PAD; u++) w[u] = __hip_atomic_load(const_cast<int64_t*>(rec + u), __ATOMIC_RELAXED, SCOPE);
+  w[RW_PAD] = 0;
+  rec_unpack(w, f);
+}
+// a record no running kernel writes (k_eval_plain): 13 plain 16-byte loads
+__device__ __forceinline__ void rec_load_plain(const int64_t* __restrict__ rec, NodeFast& f) {
+  int64_t w[NUM_RW];
+  const int4* r4 = reinterpret_cast<const int4*>(rec);
+#pragma unroll
+  for (int u = 0; u < NUM_RW / 2; u++) {
+    const int4 q = r4[u];
+    w[2 * u] = (int64_t)(((uint64_t)(uint32_t)q.y << 32) | (uint32_t)q.x);
+    w[2 * u + 1] = (int64_t)(((uint64_t)(uint32_t)q.w << 32) | (uint32_t)q.z);
+  }
+  rec_unpack(w, f);
+}
+__device__ __forceinline__ void rec_unpack(const int64_t (&w)[NUM_RW], NodeFast& f) {
 #pragma unroll
   for (int v = 0; v < 2; v++)
 #pragma unroll
@@ -2687,7 +2704,10 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
                                                            int pods_per_block, KArgs k, uint16_t* __restrict__ scores,
                                                            int64_t score_stride, uint16_t* __restrict__ dsraw,
                                                            uint64_t* __restrict__ defer_list, uint32_t* defer_cnt,
-                                                           uint8_t* __restrict__ aff_out, uint32_t* __restrict__ dsmax1) {
+                                                           uint8_t* __restrict__ aff_out, uint32_t* __restrict__ dsmax1,
+                                                           uint64_t* __restrict__ stamp) {
+  // a plain batch's eval-start stamp (per-pod latency counts from here; else k_batch_begin wrote it)
+  if (stamp && (blockIdx.x | blockIdx.y | threadIdx.x) == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
   // XCD-aware block mapping (eval_grid): workgroups are dealt to the 8 XCDs round-robin by linear id,
   // so every pod group of one node tile is given ids of the same residue mod 8 — the tile's rows are
   // fetched into one XCD's L2 once instead of once per pod group.
@@ -2725,6 +2745,45 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
       dsraw[(int64_t)p * score_stride + i] = (uint16_t)(o.total >= 0 ? 1u : 0u);
     }
     if (CPU && NUMA) aff_out[i] = o.aff;  // singleton batch: the affinity its Reserve allocates on
+  }
+}
+
+// Plain batches (LoadAware + NodeNUMAResource policy None, FitPlus / SRA when EXT): each lane adopts its
+// node's replay record (13 16-byte loads + fast_adopt, once per pod group) and scores the group's pods
+// with fast_total — k_resolve's exact re-evaluation, equal to lite_total (+ ext_score): the Reserve-
+// dependent words are exact doubles, so no int64 -> double conversion or 64-bit subtraction is left per
+// (pod, node).  The pods' estimates / requests as doubles are converted once per block into LDS.
+// Records are written sc1 by the Reserve kernels, so a pipelined eval sees them like the SoA rows.
+constexpr int EVAL_PPB = 8;  // pods per block (eval_grid's pod groups)
+template <bool EXT>
+__global__ __launch_bounds__(EVAL_BLOCK) void k_eval_plain(SoA s, int lo, int hi, const DevPod* __restrict__ pods,
+                                                           const int32_t* __restrict__ batch_base, int batch_pods,
+                                                           KArgs k, uint16_t* __restrict__ scores, int64_t score_stride,
+                                                           uint64_t* __restrict__ stamp) {
+  if (stamp && (blockIdx.x | blockIdx.y | threadIdx.x) == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
+  const int G = (int)gridDim.y;
+  const int b = (int)(blockIdx.x + blockIdx.y * gridDim.x), r = b >> 3;
+  const int tile = (r / G) * 8 + (b & 7), group = r % G;  // XCD-aware, as k_eval_batch
+  const int i = lo + tile * blockDim.x + threadIdx.x;
+  const int base = *batch_base;
+  const int p0 = group * EVAL_PPB;
+  const int np = min(batch_pods, p0 + EVAL_PPB) - p0;
+  __shared__ double s_pd[EVAL_PPB][4];
+  if ((int)threadIdx.x < 4 * np) {
+    const int q = threadIdx.x >> 2, c = threadIdx.x & 3;
+    const DevPod& pp = pods[base + p0 + q];
+    s_pd[q][c] = (double)(c < 2 ? pp.est[c] : pp.req[c - 2]);
+  }
+  __syncthreads();
+  if (i >= hi) return;
+  NodeFast f;
+  rec_load_plain(s.rec + (int64_t)i * NUM_RW, f);
+  if (EXT && (k.flags & AF_EXT)) ext_load(s, i, k, f);
+  fast_adopt(f, k);
+  for (int q = 0; q < np; q++) {
+    const DevPod& pod = pods[base + p0 + q];
+    const double ed[2] = {s_pd[q][0], s_pd[q][1]}, rd[2] = {s_pd[q][2], s_pd[q][3]};
+    scores[(int64_t)(p0 + q) * score_stride + i] = (uint16_t)(fast_total<EXT>(f, pod, ed, rd, k) + 1);
   }
 }
 
@@ -3065,6 +3124,39 @@ __device__ __forceinline__ void load8(const uint16_t* sc, int i, int end, uint32
 }
 
 constexpr int SEL_WINDOW = 64;  // histogram window below the pod's best score
+constexpr int SEL_RC = 8;       // register-resident select: up to SEL_RC * 512 nodes per wave (65,536 per pod)
+constexpr int SEL_COPIES = 8;   // histogram copies per wave (pass 2)
+
+// per-wave node segment of k_select over [lo, hi): a multiple of 512 (one 16-B load per lane per step)
+__host__ __device__ inline int select_seg(int lo, int hi) { return ((hi - lo + SELECT_WAVES - 1) / SELECT_WAVES + 511) & ~511; }
+
+// it = 0 .. iters-1 over a wave's 512-node steps; RC > 0: a constant trip count (registers indexed by it)
+template <int RC, typename F>
+__device__ __forceinline__ void sel_each(int iters, F&& f) {
+  if constexpr (RC > 0) {
+#pragma unroll
+    for (int it = 0; it < RC; it++)
+      if (it < iters) f(it);
+  } else {
+    for (int it = 0; it < iters; it++) f(it);
+  }
+}
+
+// two u16 scores per dword (low half = the lower node index): packed VALU, two scores per instruction
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t w) { return __builtin_bit_cast(u16x2, w); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 w) { return __builtin_bit_cast(uint32_t, w); }
+__device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
+  return as_u32(__builtin_elementwise_max(as_u16x2(a), as_u16x2(b)));
+}
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {  // kept one instruction (no compare rewrite)
+  uint32_t r;
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) { return as_u32(as_u16x2(a) + as_u16x2(b)); }
+__device__ __forceinline__ uint32_t pk_sub_u16(uint32_t a, uint32_t b) { return as_u32(as_u16x2(a) - as_u16x2(b)); }
+__device__ __forceinline__ uint32_t max_halves(uint32_t w) { return max(w & 0xFFFFu, w >> 16); }
 
 // Exact top-k_j per pod, k_j = min(j+1, KMAX), in (score desc, node index asc) order.  One
 // workgroup per pod; each wave owns a contiguous node segment read 16 B per lane (8 scores).
@@ -3073,13 +3165,19 @@ constexpr int SEL_WINDOW = 64;  // histogram window below the pod's best score
 //           number of ties before it in node order (a generic binary search covers the rare case
 //           of fewer than k feasible nodes inside the window)
 //   pass 3: select score > thr, and the first need_ties nodes with score == thr by node index.
+// Every pass works on the scores two per dword with packed u16 instructions; a step whose lanes hold no
+// score in the window (pass 2) or none that can be selected (pass 3) is skipped by one ballot, so pass 3
+// — k of N nodes selected — costs a max and a ballot per step.
+// RC > 0 (segments of <= RC * 512 nodes): pass 1 issues every load of the wave's segment at once and
+// keeps the (normalized) scores in registers, so passes 2 and 3 read no memory.  RC = 0 streams the
+// segment in every pass.
 // Nodes [lo, hi) (lo % 512 == 0: the shard boundaries keep the 16-B loads aligned); keys carry the
 // global node index, so per-shard lists merge without translation (k_merge).
 // DS: the batch is one DeviceShare pod; its scores get the normalized DeviceShare term (dsmax1 =
 // 1 + the max raw score over all feasible nodes, after the all-reduce when node-sharded).
 // kext / ostride: the pipelined schedule selects top-(k_j + KMAX) lists of a stale snapshot into
 // rows of `ostride` keys (pipelining); otherwise kext = 0, ostride = KMAX.
-template <bool DS>
+template <bool DS, int RC>
 __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restrict__ scores, int64_t score_stride,
                                                          int lo, int hi, uint32_t* __restrict__ cand,
                                                          int32_t* __restrict__ cand_cnt,
@@ -3096,7 +3194,9 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
     for (int x = threadIdx.x; x <= MAX_DS_RAW; x += SELECT_BLOCK) s_lut[x] = (int16_t)(wds * ds_norm(x, m1));
     __syncthreads();
   }
-  __shared__ int32_t s_hist[SELECT_WAVES][SEL_WINDOW];
+  // per wave SEL_COPIES histograms (lane & 7 picks one), rows padded to 65 words: lanes of one LDS lane group
+  // that count the same score go to different copies in different banks instead of one address
+  __shared__ int32_t s_hist[SELECT_WAVES][SEL_COPIES][SEL_WINDOW + 1];
   __shared__ int32_t s_red[2][SELECT_WAVES];
   __shared__ int32_t s_thr[2];
   __shared__ int32_t s_tie[SELECT_WAVES];
@@ -3105,36 +3205,69 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
   const int k = min(j + 1, KMAX) + kext;
   const uint16_t* sc = scores + (int64_t)j * score_stride;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int seg = ((hi - lo + SELECT_WAVES - 1) / SELECT_WAVES + 511) & ~511;
+  const int seg = select_seg(lo, hi);
   const int w0 = min(hi, lo + wave * seg);
   const int w1 = min(hi, w0 + seg);
-  reinterpret_cast<int32_t*>(s_hist)[threadIdx.x] = 0;  // SELECT_WAVES * SEL_WINDOW == SELECT_BLOCK
+  const int iters = (w1 - w0 + 511) >> 9;  // wave-uniform; <= RC when RC > 0 (the host picks RC by select_seg)
+  for (int x = threadIdx.x; x < SELECT_WAVES * SEL_COPIES * (SEL_WINDOW + 1); x += SELECT_BLOCK)
+    reinterpret_cast<int32_t*>(s_hist)[x] = 0;
+  int32_t* my_hist = &s_hist[wave][lane & (SEL_COPIES - 1)][0];
   if (threadIdx.x == 0) s_out = 0;
-
-  // pass 1
-  uint32_t mx = 0;
-  int feas = 0, at_max = 0;  // DS: feasible nodes whose raw score attains the normalisation max
-  for (int b = w0; b < w1; b += 512) {
-    uint32_t v[8];
-    load8<DS>(sc, b + lane * 8, w1, v, dn);
+  uint4 cache[RC > 0 ? RC : 1];
+  // the 8 scores of this lane at step it (nodes w0 + it*512 + lane*8 ...) as 4 packed dwords, 0 beyond w1
+  auto load4 = [&](int it, uint32_t w[4]) {
+    const int i = w0 + it * 512 + lane * 8;
+    if (!DS && i + 8 <= w1) {
+      const uint4 q = *reinterpret_cast<const uint4*>(sc + i);
+      w[0] = q.x, w[1] = q.y, w[2] = q.z, w[3] = q.w;
+    } else {
+      uint32_t v[8];
+      load8<DS>(sc, i, w1, v, dn);
 #pragma unroll
-    for (int t = 0; t < 8; t++) {
-      mx = max(mx, v[t]);
-      feas += v[t] > 0;
+      for (int t = 0; t < 4; t++) w[t] = v[2 * t] | (v[2 * t + 1] << 16);
+    }
+  };
+  auto get4 = [&](int it, uint32_t w[4]) {
+    if constexpr (RC > 0) {
+      w[0] = cache[it].x, w[1] = cache[it].y, w[2] = cache[it].z, w[3] = cache[it].w;
+    } else {
+      load4(it, w);
+    }
+  };
+  auto unpack = [](const uint32_t w[4], uint32_t v[8]) {
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      v[2 * t] = w[t] & 0xFFFFu;
+      v[2 * t + 1] = w[t] >> 16;
+    }
+  };
+  auto lane_max = [](const uint32_t w[4]) { return max_halves(pk_max_u16(pk_max_u16(w[0], w[1]), pk_max_u16(w[2], w[3]))); };
+
+  // pass 1 (RC > 0: the only pass that reads memory)
+  uint32_t mx2 = 0, cnt2 = 0;  // packed: per half, the max and the feasible count
+  int at_max = 0;              // DS: feasible nodes whose raw score attains the normalisation max
+  sel_each<RC>(iters, [&](int it) {
+    uint32_t w[4];
+    load4(it, w);
+    if constexpr (RC > 0) cache[it] = make_uint4(w[0], w[1], w[2], w[3]);
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      mx2 = pk_max_u16(mx2, w[t]);
+      cnt2 = pk_add_u16(cnt2, pk_min_u16(w[t], 0x00010001u));
     }
     if (DS && m1) {
       uint32_t r[8];
-      load8_raw(dn.raw, b + lane * 8, w1, r);
+      load8_raw(dn.raw, w0 + it * 512 + lane * 8, w1, r);
 #pragma unroll
       for (int t = 0; t < 8; t++) at_max += r[t] == m1;
     }
-  }
+  });
   if (DS && m1) {
     at_max = wave_sum(at_max);
     if (lane == 0 && at_max) atomicAdd(&s_dscnt, at_max);
   }
-  mx = wave_max_u32(mx);
-  feas = wave_sum(feas);
+  const uint32_t mx = wave_max_u32(max_halves(mx2));
+  const int feas = wave_sum((int)((cnt2 & 0xFFFFu) + (cnt2 >> 16)));
   if (lane == 0) {
     s_red[0][wave] = (int)mx;
     s_red[1][wave] = feas;
@@ -3148,21 +3281,34 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
   }
   int thr = 0, need_ties = 0;  // select v > thr, plus the first need_ties with v == thr
   if (F > k) {
-    // pass 2: per-wave histogram of scores in (M - 64, M]
-    for (int b = w0; b < w1; b += 512) {
-      uint32_t v[8];
-      load8<DS>(sc, b + lane * 8, w1, v, dn);
+    // pass 2: per-wave histogram of d = M - v over the window d < 64.  An infeasible node (v = 0) has
+    // d = M exactly, so bins d < M are exact and the scan below ignores the rest.
+    const uint32_t MM = (uint32_t)M * 0x00010001u;
+    sel_each<RC>(iters, [&](int it) {
+      uint32_t w[4];
+      get4(it, w);
+      if (!__ballot(lane_max(w) + SEL_WINDOW > (uint32_t)M)) return;  // no score of the step in the window
 #pragma unroll
-      for (int t = 0; t < 8; t++) {
-        const int d = M - (int)v[t];
-        if (v[t] > 0 && d < SEL_WINDOW) atomicAdd(&s_hist[wave][d], 1);
+      for (int t = 0; t < 4; t++) {
+        const uint32_t d2 = pk_sub_u16(MM, w[t]);
+        const uint32_t dl = d2 & 0xFFFFu, dh = d2 >> 16;
+        if (dl < SEL_WINDOW) atomicAdd(my_hist + dl, 1);
+        if (dh < SEL_WINDOW) atomicAdd(my_hist + dh, 1);
       }
+    });
+    __syncthreads();
+    {  // each wave folds its copies into copy 0, lane d = window bin
+      int c = 0;
+#pragma unroll
+      for (int y = 0; y < SEL_COPIES; y++) c += s_hist[wave][y][lane];
+      s_hist[wave][0][lane] = c;  // the wave's own row: no other wave reads it before the barrier
     }
     __syncthreads();
     if (wave == 0) {  // cumulative count from the top, lane d = window bin
       int c = 0;
 #pragma unroll
-      for (int w = 0; w < SELECT_WAVES; w++) c += s_hist[w][lane];
+      for (int w = 0; w < SELECT_WAVES; w++) c += s_hist[w][0][lane];
+      if (lane >= M) c = 0;  // d >= M: score <= 0, infeasible
       int cum = c;  // inclusive prefix over lanes
       for (int off = 1; off < 64; off <<= 1) {
         const int o = __shfl_up(cum, off, 64);
@@ -3187,12 +3333,13 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
       // generic threshold search over [1, M - 64]: count(v >= lo) >= k > count(v >= hi)
       auto count_ge = [&](int t) -> int {
         int c = 0;
-        for (int b = w0; b < w1; b += 512) {
-          uint32_t v[8];
-          load8<DS>(sc, b + lane * 8, w1, v, dn);
+        sel_each<RC>(iters, [&](int it) {
+          uint32_t w[4], v[8];
+          get4(it, w);
+          unpack(w, v);
 #pragma unroll
           for (int q = 0; q < 8; q++) c += v[q] >= (uint32_t)t;
-        }
+        });
         c = wave_sum(c);
         __syncthreads();
         if (lane == 0) s_red[1][wave] = c;
@@ -3215,27 +3362,32 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
       thr = lo;
       need_ties = k - cnt_hi;
       int ties = 0;
-      for (int b = w0; b < w1; b += 512) {
-        uint32_t v[8];
-        load8<DS>(sc, b + lane * 8, w1, v, dn);
+      sel_each<RC>(iters, [&](int it) {
+        uint32_t w[4], v[8];
+        get4(it, w);
+        unpack(w, v);
 #pragma unroll
         for (int q = 0; q < 8; q++) ties += v[q] == (uint32_t)thr;
-      }
+      });
       ties = wave_sum(ties);
       if (lane == 0) s_tie[wave] = ties;
     } else if (lane == 0) {
-      s_tie[wave] = s_hist[wave][M - thr];
+      s_tie[wave] = s_hist[wave][0][M - thr];
     }
     __syncthreads();
   }
-  // pass 3: select
+  // pass 3: select (a step none of whose scores reaches vmin holds no selected node and no tie)
+  const uint32_t vmin = (uint32_t)max(1, need_ties > 0 ? thr : thr + 1);
   int running = 0;  // ties of this wave before the current row
   for (int w = 0; w < wave; w++) running += need_ties > 0 ? s_tie[w] : 0;
   uint32_t* out = cand + (int64_t)j * ostride;
-  for (int b = w0; b < w1; b += 512) {
-    const int i0 = b + lane * 8;
+  sel_each<RC>(iters, [&](int it) {
+    uint32_t w[4];
+    get4(it, w);
+    if (!__ballot(lane_max(w) >= vmin)) return;
+    const int i0 = w0 + it * 512 + lane * 8;
     uint32_t v[8];
-    load8<DS>(sc, i0, w1, v, dn);
+    unpack(w, v);
     int nt = 0;
 #pragma unroll
     for (int t = 0; t < 8; t++) nt += (need_ties > 0 && v[t] == (uint32_t)thr && v[t] > 0);
@@ -3264,7 +3416,7 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
       for (int t = 0; t < 8; t++)
         if (selm & (1u << t)) out[pos++] = (v[t] << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)(i0 + t));
     }
-  }
+  });
   __syncthreads();
   if (threadIdx.x == 0) {
     cand_cnt[j] = s_out;
@@ -3718,7 +3870,7 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
       }
     st_sc1(f + (F_NREQ + 0) * st, (int64_t)slot.nreq[0]);
     st_sc1(f + (F_NREQ + 1) * st, (int64_t)slot.nreq[1]);
-    rec_store_dyn<__HIP_MEMORY_SCOPE_WORKGROUP>(s.rec + (int64_t)snode * NUM_RW, slot);
+    rec_store_dyn<__HIP_MEMORY_SCOPE_AGENT>(s.rec + (int64_t)snode * NUM_RW, slot);  // sc1: read by k_eval_plain
     if (ext)
 #pragma unroll
       for (int q = 0; q < 4; q++)
@@ -4046,7 +4198,7 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
         }
       st_sc1(f + (F_NREQ + 0) * st, (int64_t)fast.nreq[0]);
       st_sc1(f + (F_NREQ + 1) * st, (int64_t)fast.nreq[1]);
-      rec_store_dyn<__HIP_MEMORY_SCOPE_WORKGROUP>(rec, fast);
+      rec_store_dyn<__HIP_MEMORY_SCOPE_AGENT>(rec, fast);
       if (EXT && (k.flags & AF_EXT))
 #pragma unroll
         for (int q = 0; q < 4; q++)
@@ -4065,7 +4217,7 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
       int64_t w[NUM_RW];
       rec_from_regs(mine, k, w);
 #pragma unroll
-      for (int u = 0; u < NUM_RW; u++) __hip_atomic_store(rec + u, w[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (int u = 0; u < NUM_RW; u++) __hip_atomic_store(rec + u, w[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     chg_clear_word(C, my_node);  // the bitmap is zero again for the next batch
   }
@@ -5118,7 +5270,7 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
   HIP_OK(hipMemsetAsync(d->d_best, 0, sizeof(uint32_t) * 2 * P, d->stream));
   HIP_OK(hipMemsetAsync(d->soa.kerr, 0, sizeof(int32_t), d->stream));
   const KArgs k = make_kargs(ctx, now);
-  const int ppb = 8;
+  const int ppb = EVAL_PPB;
   bool cpu = false;
   for (const DevPod& q : d->host_pods) cpu = cpu || (q.flags & PF_CPUSET);
   if (cpu && !d->cpu_alloc) return fail(KE_ERR_DEVICE, "cpuset pod without the CPU SoA");
@@ -5268,7 +5420,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     k.flags |= AF_QUOTA | (ctx->qargs.enable_check_parent_quota ? AF_QUOTA_PARENT : 0u);
   }
   const int N = ctx->n_nodes;
-  const int ppb = 8;
+  const int ppb = EVAL_PPB;
   // first pod of every batch and the end (the kernels' batch base pointer is d_bases + b)
   std::vector<int32_t> bases((size_t)n_batches + 1);
   for (int b = 0, p = 0; b <= n_batches; b++) {
@@ -5333,17 +5485,21 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     hipEvent_t* pe = prof ? &ev[(size_t)(b / every) * PE] : nullptr;
     const int32_t* bbase = d_bases + b;
     const bool argmax1 = !sharded && bp == 1 && !pipe && N > 0;  // selectHost of one pod: a grid-wide argmax
-    // a re-run remainder keeps its batch's first dequeue stamp (latency counts from there)
-    hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(MAX_BATCH), 0, es, estamps + (rerun ? n_pods + 1 : b), ds ? d->d_dsmax : nullptr,
-                       argmax1 ? d->d_cand : nullptr);
+    // this rank's node range (unsharded and loopback: every node)
+    int lo = 0, hi = N;
+    if (N > 0 && sharded && !d->loopback) shard_range(N, d->rank, d->world, &lo, &hi);
+    // a plain batch with nodes to evaluate: k_eval_batch writes the eval-start stamp itself (one launch
+    // less on the eval stream); else k_batch_begin — a re-run remainder keeps its batch's first dequeue
+    // stamp (latency counts from there)
+    const bool fold_begin = !ds && !argmax1 && !rerun && hi > lo;
+    if (!fold_begin)
+      hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(MAX_BATCH), 0, es, estamps + (rerun ? n_pods + 1 : b), ds ? d->d_dsmax : nullptr,
+                         argmax1 ? d->d_cand : nullptr);
     if (prof) HIP_OK(hipEventRecord(pe[0], es));
     const int L = pipe ? KSTALE : KMAX, kext = pipe ? KMAX : 0;
     uint32_t* lists = pipe ? d->d_stale + (size_t)(b & 1) * MAX_BATCH * KSTALE : d->d_cand;
     int32_t* lists_cnt = pipe ? d->d_stale_cnt + (b & 1) * MAX_BATCH : d->d_cand_cnt;
     if (N > 0) {
-      // this rank's node range (unsharded and loopback: every node)
-      int lo = 0, hi = N;
-      if (sharded && !d->loopback) shard_range(N, d->rank, d->world, &lo, &hi);
       const bool single = bp == 1;
       if (hi > lo) {
         // a singleton batch has one pod's worth of lanes: single-wave blocks spread it over every CU
@@ -5356,8 +5512,13 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                                      : ((k.flags & AF_EXT) ? k_eval_batch<false, false, false, true>
                                                            : k_eval_batch<false, false, false>));
         uint32_t* dcnt = numa ? d->d_defer_cnt + b : nullptr;
-        hipLaunchKernelGGL(eval, grid, dim3(eb), 0, es, d->soa, lo, hi, d->d_pods, bbase, bp,
-                           ppb, k, d->d_scores, d->capacity, d->d_dsraw, d->d_defer, dcnt, d->d_aff, d->d_dsmax);
+        if (!cpu && !ds && !numa)  // plain batch: the record-based evaluation
+          hipLaunchKernelGGL(((k.flags & AF_EXT) ? k_eval_plain<true> : k_eval_plain<false>), grid, dim3(eb), 0, es, d->soa,
+                             lo, hi, d->d_pods, bbase, bp, k, d->d_scores, d->capacity, fold_begin ? estamps + b : nullptr);
+        else
+          hipLaunchKernelGGL(eval, grid, dim3(eb), 0, es, d->soa, lo, hi, d->d_pods, bbase, bp,
+                             ppb, k, d->d_scores, d->capacity, d->d_dsraw, d->d_defer, dcnt, d->d_aff, d->d_dsmax,
+                             fold_begin ? estamps + b : nullptr);
         if (numa) {  // a DeviceShare pod defers only on nodes without a device cache (no DeviceShare hints there)
           uint32_t* fb = reinterpret_cast<uint32_t*>(d->d_defer + (int64_t)MAX_BATCH * d->capacity);
           hipLaunchKernelGGL((cpu ? k_numa_fallback<false, true> : k_numa_fallback<false, false>), dim3(FALLBACK_BLOCKS),
@@ -5376,12 +5537,11 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
         RCCL_OK(ncclAllReduce(d->d_dsmax, d->d_dsmax, 1, ncclUint32, ncclMax, d->comm, es));
       if (prof) HIP_OK(hipEventRecord(pe[1], es));
       auto select = [&](int slo, int shi, uint32_t* cand, int32_t* cnt) {
-        if (ds)
-          hipLaunchKernelGGL(k_select<true>, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, es, d->d_scores,
-                             d->capacity, slo, shi, cand, cnt, d->d_dsraw, d->d_dsmax, k.wp_ds, kext, L);
-        else
-          hipLaunchKernelGGL(k_select<false>, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, es, d->d_scores,
-                             d->capacity, slo, shi, cand, cnt, d->d_dsraw, d->d_dsmax, k.wp_ds, kext, L);
+        // register-resident when a wave's segment fits SEL_RC steps, else streamed
+        const bool rc = select_seg(slo, shi) <= SEL_RC * 512;
+        auto sel = ds ? (rc ? k_select<true, SEL_RC> : k_select<true, 0>) : (rc ? k_select<false, SEL_RC> : k_select<false, 0>);
+        hipLaunchKernelGGL(sel, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, es, d->d_scores, d->capacity, slo, shi, cand,
+                           cnt, d->d_dsraw, d->d_dsmax, k.wp_ds, kext, L);
       };
       if (argmax1) {  // d_cand[0] zeroed by k_batch_begin
         hipLaunchKernelGGL((ds ? k_argmax1<true> : k_argmax1<false>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
@@ -5665,18 +5825,18 @@ int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t 
   const int N = ctx->n_nodes;
   if (N == 0) return fail(KE_ERR_INVALID, "bench: no nodes");
   const KArgs k = make_kargs(ctx, now);
-  const int ppb = 8;
+  const int ppb = EVAL_PPB;
   HIP_OK(hipMemsetAsync(d->d_batch_base, 0, sizeof(int32_t), d->stream));
   const dim3 grid = eval_grid(N, EVAL_BLOCK, n_pods, ppb);
-  hipLaunchKernelGGL((k_eval_batch<false, false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base, n_pods,
-                     ppb, k, d->d_scores, d->capacity, d->d_dsraw, nullptr, nullptr, nullptr, nullptr);  // warm
+  hipLaunchKernelGGL((k_eval_plain<false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base, n_pods,
+                     k, d->d_scores, d->capacity, nullptr);  // warm
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   HIP_OK(hipEventRecord(e0, d->stream));
   for (int it = 0; it < iters; it++)
-    hipLaunchKernelGGL((k_eval_batch<false, false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base,
-                       n_pods, ppb, k, d->d_scores, d->capacity, d->d_dsraw, nullptr, nullptr, nullptr, nullptr);
+    hipLaunchKernelGGL((k_eval_plain<false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base,
+                       n_pods, k, d->d_scores, d->capacity, nullptr);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(e1, d->stream));
   HIP_OK(hipEventSynchronize(e1));
