@@ -900,7 +900,7 @@ int ke_decode_nrt(const char* js, int64_t len, ke_node* node, int32_t zone_cap, 
           const Value* x = c.field(f.first);
           if (x && !x->is_null() && !json::as_int64(*x, f.second)) return unsup("cpu-topology entry");
         }
-        if (id < 0 || id >= KE_MAX_CPUS || core < 0 || core > 0xFFFF || sock < 0 || nd < 0)
+        if (id < 0 || id >= KE_MAX_CPUS || core < 0 || core > 0xFFFF || sock < 0 || sock > 0x7FFF || nd < 0 || nd > 0x7FFF)
           return unsup("cpu-topology ids outside the modelled range (CPU ids 0..255)");
         topo[(int)id] = Cpu{(int)id, (int)(sock << 16 | core), (int)nd, (int)sock};
       }

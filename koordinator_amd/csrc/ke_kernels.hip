@@ -2755,6 +2755,10 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
 // (pod, node).  The pods' estimates / requests as doubles are converted once per block into LDS.
 // Records are written sc1 by the Reserve kernels, so a pipelined eval sees them like the SoA rows.
 constexpr int EVAL_PPB = 8;  // pods per block (eval_grid's pod groups)
+// A plain batch of more than 2 pods is evaluated from the 208-B replay records (k_eval_plain: no int64 ->
+// double work per pair, the record read once per 8 pods); 1-2 pods stream the 148-B SoA rows
+// (k_eval_batch), the smaller read when the pass is bandwidth-bound.
+__host__ __device__ constexpr bool use_record_eval(int pods) { return pods > 2; }
 template <bool EXT>
 __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_plain(SoA s, int lo, int hi, const DevPod* __restrict__ pods,
                                                            const int32_t* __restrict__ batch_base, int batch_pods,
@@ -5512,7 +5516,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                                      : ((k.flags & AF_EXT) ? k_eval_batch<false, false, false, true>
                                                            : k_eval_batch<false, false, false>));
         uint32_t* dcnt = numa ? d->d_defer_cnt + b : nullptr;
-        if (!cpu && !ds && !numa)  // plain batch: the record-based evaluation
+        if (!cpu && !ds && !numa && use_record_eval(bp))  // plain batch: the record-based evaluation
           hipLaunchKernelGGL(((k.flags & AF_EXT) ? k_eval_plain<true> : k_eval_plain<false>), grid, dim3(eb), 0, es, d->soa,
                              lo, hi, d->d_pods, bbase, bp, k, d->d_scores, d->capacity, fold_begin ? estamps + b : nullptr);
         else
@@ -5828,15 +5832,22 @@ int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t 
   const int ppb = EVAL_PPB;
   HIP_OK(hipMemsetAsync(d->d_batch_base, 0, sizeof(int32_t), d->stream));
   const dim3 grid = eval_grid(N, EVAL_BLOCK, n_pods, ppb);
-  hipLaunchKernelGGL((k_eval_plain<false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base, n_pods,
-                     k, d->d_scores, d->capacity, nullptr);  // warm
+  // the kernel ke_schedule runs for a plain batch of n_pods
+  auto launch = [&]() {
+    if (use_record_eval(n_pods))
+      hipLaunchKernelGGL((k_eval_plain<false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods,
+                         d->d_batch_base, n_pods, k, d->d_scores, d->capacity, nullptr);
+    else
+      hipLaunchKernelGGL((k_eval_batch<false, false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N,
+                         d->d_pods, d->d_batch_base, n_pods, ppb, k, d->d_scores, d->capacity, d->d_dsraw, d->d_defer,
+                         nullptr, d->d_aff, d->d_dsmax, nullptr);
+  };
+  launch();  // warm
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   HIP_OK(hipEventRecord(e0, d->stream));
-  for (int it = 0; it < iters; it++)
-    hipLaunchKernelGGL((k_eval_plain<false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods, d->d_batch_base,
-                       n_pods, k, d->d_scores, d->capacity, nullptr);
+  for (int it = 0; it < iters; it++) launch();
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(e1, d->stream));
   HIP_OK(hipEventSynchronize(e1));

@@ -11,6 +11,16 @@ object and expected result by hand.  Only data is written.
   * nodenumaresource/topology_options_test.go:36-176  NewTopologyOptions from a NodeResourceTopology (CPU topology,
     reserved CPUs from four annotations, zone cpu less the reserved CPUs)
 
+  * device_share_test.go:174-251  GetGPUPartitionSpec (pod annotation gpu-partition-spec: absent, {}, BestEffort,
+    Restricted, Restricted + ringBusBandwidth 200Gi)
+  * device_share_test.go:253-311  GetGPUPartitionTable (Device annotation gpu-partitions: a valid table, none,
+    invalid JSON -> error)
+  * device_share_test.go:313-359  GetGPUPartitionPolicy (Device label gpu-partition-policy Honor / Prefer / none)
+  * qos_utils_test.go:27-111  GetPodQoSClassRaw / GetQoSClassByAttrs (the koordinator.sh/qosClass label)
+  * node_reservation_test.go:37-153  GetReservedCPUs: the node.koordinator.sh/reservation annotation's reservedCPUs
+    (the string NewTopologyOptions parses with cpuset.Parse, topology_options.go:108-112), observed as the
+    NodeResourceTopology's reserved CPUs ("-1" does not parse: nothing reserved)
+
 Run:  python tests/golden/make_decode_fixtures.py
 """
 import json
@@ -93,6 +103,77 @@ del nrt2["metadata"]["annotations"]["node.koordinator.sh/pod-cpu-allocs"]
 cases.append({"name": "nrt_topology_options_no_pod_allocs", "source": f"{NRT_SRC}:169-176", "kind": "nrt",
               "object": nrt2, "want": {"reserved": [0, 1, 4, 5, 6, 7], "zone_cpu": [[0, 2000], [1, 8000]],
                                        "cpus": want_cpus}})
+
+# ---- apis/extension/device_share_test.go -------------------------------------------------------------------
+DS = "apis/extension/device_share_test.go"
+SPEC = "scheduling.koordinator.sh/gpu-partition-spec"
+ABSENT = -1
+for name, lines, ann, want in (
+        ("gpu_partition_spec_nil", "185-192", None, (0, 0, ABSENT)),
+        ("gpu_partition_spec_empty", "193-203", "{}", (1, 0, ABSENT)),
+        ("gpu_partition_spec_best_effort", "204-214", '{"allocatePolicy":"BestEffort"}', (1, 0, ABSENT)),
+        ("gpu_partition_spec_restricted", "215-225", '{"allocatePolicy":"Restricted"}', (1, 1, ABSENT)),
+        ("gpu_partition_spec_restricted_bw", "226-237", '{"allocatePolicy":"Restricted", "ringBusBandwidth":"200Gi"}',
+         (1, 1, 200 * 2**30))):
+    obj = {"metadata": {"name": "p", "namespace": "default", "annotations": {SPEC: ann} if ann else {}},
+           "spec": {"containers": []}}
+    cases.append({"name": name, "source": f"{DS}:{lines}", "kind": "pod", "object": obj,
+                  "want": {"gpu_partition_spec": want[0], "gpu_partition_restricted": want[1],
+                           "gpu_ring_bus_bandwidth": want[2]}})
+PARTS = "scheduling.koordinator.sh/gpu-partitions"
+cases.append({"name": "gpu_partition_table_valid", "source": f"{DS}:259-279", "kind": "device",
+              "object": {"metadata": {"annotations": {PARTS: '{"0": [{"minors": [0,1], "gpuLinkType": "NVLink",'
+                                                             '"ringBusBandwidth": "200Gi", "allocationScore": 10}]}'}},
+                         "spec": {"devices": []}},
+              "want": {"has_table": 1, "partitions": [[0b11, 0, 10, 200 * 2**30]]}})
+cases.append({"name": "gpu_partition_table_none", "source": f"{DS}:280-285", "kind": "device",
+              "object": {"spec": {"devices": []}}, "want": {"has_table": 0, "partitions": []}})
+cases.append({"name": "gpu_partition_table_invalid_json", "source": f"{DS}:286-296", "kind": "device",
+              "object": {"metadata": {"annotations": {PARTS: "Invalid JSON format"}}, "spec": {"devices": []}},
+              "want": {"error": True}})
+POLICY = "node.koordinator.sh/gpu-partition-policy"
+for name, lines, labels, honor in (("gpu_partition_policy_honor", "321-331", {POLICY: "Honor"}, 1),
+                                   ("gpu_partition_policy_prefer", "332-342", {POLICY: "Prefer"}, 0),
+                                   ("gpu_partition_policy_unset", "343-351", {}, 0)):
+    cases.append({"name": name, "source": f"{DS}:{lines}", "kind": "device",
+                  "object": {"metadata": {"labels": labels}, "spec": {"devices": []}}, "want": {"honor": honor}})
+
+# ---- apis/extension/qos_utils_test.go ----------------------------------------------------------------------
+QU = "apis/extension/qos_utils_test.go"
+QOS_NONE, QOS_LS, QOS_BE = 0, 3, 4  # KE_QOS_*
+for name, lines, labels, want in (("qos_not_specified", "33-37", None, QOS_NONE),
+                                  ("qos_not_specified_1", "38-46", {}, QOS_NONE),
+                                  ("qos_ls", "47-56", {QOS: "LS"}, QOS_LS),
+                                  ("qos_be", "57-66", {QOS: "BE"}, QOS_BE),
+                                  ("qos_by_attrs_not_specified", "88-94", {}, QOS_NONE),
+                                  ("qos_by_attrs_be", "95-103", {QOS: "BE"}, QOS_BE)):
+    obj = {"metadata": {"name": "p", "namespace": "default"}, "spec": {}}
+    if labels is not None:
+        obj["metadata"]["labels"] = labels
+    cases.append({"name": name, "source": f"{QU}:{lines}", "kind": "pod", "object": obj, "want": {"qos_class": want}})
+
+# ---- apis/extension/node_reservation_test.go ---------------------------------------------------------------
+NR = "apis/extension/node_reservation_test.go"
+small_rows = [{"id": c, "core": c // 2, "socket": 0, "node": c // 4} for c in range(8)]
+small_zone = lambda n: {"name": f"node-{n}", "type": "Node", "resources": [
+    {"name": "cpu", "capacity": "4", "allocatable": "4", "available": "4"}]}
+for name, lines, reservation, reserved in (
+        ("reserved_cpus_nil_annotation", "47-54", None, []),
+        ("reserved_cpus_empty", "55-66", {}, []),
+        ("reserved_cpus_quantity_only", "67-77", {"resources": {"cpu": "10"}}, []),
+        ("reserved_cpus_quantity_not_integer", "78-88", {"resources": {"cpu": "2500m"}}, []),
+        ("reserved_cpus_quantity_negative", "89-99", {"resources": {"cpu": "-2"}}, []),
+        ("reserved_cpus_specific", "100-110", {"reservedCPUs": "0-1"}, [0, 1]),
+        ("reserved_cpus_unavailable_id", "111-121", {"reservedCPUs": "-1"}, []),
+        ("reserved_cpus_specific_and_quantity", "122-133", {"resources": {"cpu": "10"}, "reservedCPUs": "0-1"}, [0, 1])):
+    ann = {"node.koordinator.sh/cpu-topology": json.dumps({"detail": small_rows})}
+    if reservation is not None:
+        ann["node.koordinator.sh/reservation"] = json.dumps(reservation)
+    zone_cpu = [[z, 4000 - 1000 * sum(1 for c in reserved if c // 4 == z)] for z in range(2)]
+    cases.append({"name": name, "source": f"{NR}:{lines}", "kind": "nrt",
+                  "object": {"metadata": {"name": "n", "annotations": ann}, "zones": [small_zone(0), small_zone(1)]},
+                  "want": {"reserved": reserved, "zone_cpu": zone_cpu,
+                           "cpus": [[r["id"], r["socket"] << 16 | r["core"], r["node"], r["socket"]] for r in small_rows]}})
 
 if __name__ == "__main__":
     with open(os.path.join(HERE, "decode.json"), "w") as f:

@@ -49,7 +49,24 @@ def test_decode_nrt_policy_and_kubelet(lib):
     assert labelled.numa_topology_policy == abi.NUMA_POLICY_RESTRICTED  # the label wins (getNUMATopologyPolicy)
 
 
-@pytest.mark.parametrize("case", [c for c in DEC if c["kind"] != "nrt"], ids=lambda c: c["name"])
+@pytest.mark.parametrize("case", [c for c in DEC if c["kind"] == "device"], ids=lambda c: c["name"])
+def test_decode_device_golden(lib, case):
+    w = case["want"]
+    if w.get("error"):
+        with pytest.raises(decode.DecodeError):
+            decode.decode_device(case["object"])
+        return
+    _, (has_table, honor, parts) = decode.decode_device(case["object"])
+    if "has_table" in w:
+        assert int(has_table) == w["has_table"], case["source"]
+        got = [[int(p["minors"]), int(p["number_of_gpus"]), int(p["allocation_score"]), int(p["ring_bus_bandwidth"])]
+               for p in parts]
+        assert got == w["partitions"], case["source"]
+    if "honor" in w:
+        assert int(honor) == w["honor"], case["source"]
+
+
+@pytest.mark.parametrize("case", [c for c in DEC if c["kind"] in ("node", "pod")], ids=lambda c: c["name"])
 def test_decode_golden(lib, case):
     obj = decode.decode_node(case["object"]) if case["kind"] == "node" else decode.decode_pod(case["object"])
     for k, v in case["want"].items():
