@@ -43,8 +43,10 @@
 extern "C" {
 #endif
 
-#define KE_ABI_VERSION 6
+#define KE_ABI_VERSION 7
 #define KE_ABSENT (-1)
+
+typedef struct ke_ctx ke_ctx; /* one evaluator context (ke_create) */
 
 /* ---- error codes ---------------------------------------------------------------------------- */
 #define KE_OK 0
@@ -84,6 +86,12 @@ extern "C" {
 #define KE_REASON_DS_INSUFFICIENT_TOPOLOGY_SCOPED 41 /* ErrInsufficientTopologyScopedGPUDevices */
 #define KE_REASON_DS_INSUFFICIENT_GPU_TOPOLOGY 42 /* ErrInsufficientGPUDevices "Insufficient GPU Devices" (topology tree) */
 #define KE_REASON_DS_INSUFFICIENT_NUMA_SCOPED 43  /* ErrInsufficientNUMAScopedDevices (topology_hint.go:32), via Admit */
+#define KE_REASON_DS_INVALID_HINT 44              /* PreFilter: "invalid Selector / VFSelector of DeviceHint" (utils.go:457-482) */
+#define KE_REASON_DS_INSUFFICIENT_RDMA_VF 45      /* "Insufficient rdma VirtualFunctions" (device_allocator.go:85-89) */
+#define KE_REASON_DS_INSUFFICIENT_FPGA_VF 46      /* "Insufficient fpga VirtualFunctions" */
+#define KE_REASON_DS_INSUFFICIENT_PRIMARY 47      /* "node(s) Insufficient primary device" (device_allocator.go:264-266) */
+#define KE_REASON_DS_JOINT_VIOLATION 48           /* "node(s) Device Joint-Allocate rules violation" (:247-249) */
+#define KE_REASON_DS_NO_MATCHED_TEMPLATE 49       /* ErrNoMatchedGPUSharedResourceTemplate (allocator_gpu.go:141-143, utils.go:512-514) */
 
 /* ---- resources (index into per-resource arrays) ---------------------------------------------- */
 #define KE_RES_CPU 0          /* "cpu"                         MilliValue */
@@ -294,6 +302,46 @@ typedef struct ke_deviceshare_args {
   uint8_t pad;
 } ke_deviceshare_args;
 
+/* ---- labels and label selectors (DeviceShare hints: apis/extension/device_share.go:151-195) ---------
+ * Label keys and values are ids of one process-wide string table (ke_label_id; 0 = no string), so a label
+ * set is KE_MAX_LABELS (key, value) id pairs and a selector is metav1.LabelSelector after
+ * LabelSelectorAsSelector (util.GetFastLabelSelector, pkg/util/selector.go:24-32): every matchLabels entry is
+ * an In requirement with one value; a present selector without requirements matches everything. */
+#define KE_MAX_LABELS 8
+#define KE_MAX_SEL_REQS 4
+#define KE_MAX_SEL_VALUES 4
+int32_t ke_label_id(const char* s); /* intern (stable for the process); NULL / "" -> 0 */
+typedef struct ke_labels {
+  int32_t n;
+  int32_t key[KE_MAX_LABELS];
+  int32_t value[KE_MAX_LABELS];
+} ke_labels; /* 68 bytes */
+#define KE_SEL_IN 0             /* also matchLabels k: v */
+#define KE_SEL_NOT_IN 1         /* key absent, or its value not listed */
+#define KE_SEL_EXISTS 2
+#define KE_SEL_DOES_NOT_EXIST 3
+typedef struct ke_label_requirement {
+  int32_t key;
+  int32_t op; /* KE_SEL_* */
+  int32_t n_values;
+  int32_t values[KE_MAX_SEL_VALUES];
+} ke_label_requirement; /* 28 bytes */
+typedef struct ke_label_selector {
+  int32_t present; /* the *metav1.LabelSelector is not nil */
+  int32_t n;
+  ke_label_requirement req[KE_MAX_SEL_REQS];
+} ke_label_selector; /* 120 bytes */
+
+/* A device's SR-IOV virtual function group (DeviceInfo.VFGroups, apis/scheduling/v1alpha1/device_types.go):
+ * its labels and its VFs as a mask over the device's VF ranks (rank r = the r-th VF of the device in BusID
+ * string order over all its groups; at most 64 VFs per device). */
+#define KE_MAX_VF_GROUPS 4
+typedef struct ke_vf_group {
+  ke_labels labels;
+  int32_t pad;
+  uint64_t vfs;
+} ke_vf_group; /* 80 bytes */
+
 /* One device instance as koord-scheduler's nodeDeviceCache holds it (device_cache.go:518-568):
  * `total` = DeviceInfo.Resources (left empty by the cache when !Health), `used` = Σ allocations of
  * the pods already on it (updateCacheUsed).  has_* mark the keys present in each ResourceList. */
@@ -312,7 +360,11 @@ typedef struct ke_device {
    * topology; DeviceShare's NUMA hints (topology_hint.go) group the devices by NodeID (-1: any NUMA node). */
   int32_t numa_node;
   int32_t pcie_rank;
-} ke_device; /* 72 bytes */
+  ke_labels labels;          /* DeviceInfo.Labels (Selector / ApplyForAll matching)                        */
+  int32_t n_vf_groups;       /* DeviceInfo.VFGroups (hasVirtualFunctions, allocateVF); RDMA / FPGA only     */
+  ke_vf_group vf_groups[KE_MAX_VF_GROUPS];
+  uint64_t vf_allocated;     /* VF ranks held by pods on the node (nodeDevice.vfAllocations[type][minor])   */
+} ke_device; /* 472 bytes */
 
 /* One GPUPartition of a node's GPUPartitionTable (apis/extension/device_share.go:196-226): the table is the
  * Device annotation scheduling.koordinator.sh/gpu-partitions, or, when the Device has none, the designated
@@ -466,8 +518,8 @@ typedef struct ke_pod {
   int32_t gpu_required_topology_scope; /* DeviceAllocateHints[gpu].RequiredTopologyScope: KE_SCOPE_*       */
   uint8_t gpu_partition_spec;          /* annotation GPUPartitionSpec present (honorGPUPartition)         */
   uint8_t gpu_partition_restricted;    /* GPUPartitionSpec.AllocatePolicy == Restricted                   */
-  uint8_t device_joint_allocate;       /* DeviceJointAllocate annotation that keeps >= 1 requested device type:
-                                          tryJointAllocate (device_allocator.go:205-300) is not implemented */
+  uint8_t device_joint_allocate;       /* DeviceJointAllocate annotation present (informational; the modelled
+                                          joint allocation is ke_pod_device_hints.joint_*) */
   uint8_t device_hints;                /* KE_DHINT_* bits of DeviceAllocateHints this evaluator does not model */
   /* NodeResourcesFitPlus / ScarceResourceAvoidance PreScore (computePodResourceRequest): the resource ids
    * whose PodRequests value is > 0 (fitsPodRequestName / fitsRequest, scarce_resource_avoidance.go:109-150),
@@ -477,9 +529,56 @@ typedef struct ke_pod {
   uint64_t xres_request_mask;
   int32_t n_xres;
   int32_t xres_id[KE_MAX_POD_XRES];
-  int32_t pad3;
+  int32_t device_hint; /* 1 + index into the ke_set_pod_device_hints table, 0 = no hints / joint allocation */
   int64_t xres_value[KE_MAX_POD_XRES];
 } ke_pod;
+
+/* DeviceAllocateHints[type] (apis/extension/device_share.go:151-195) + DeviceJointAllocate (:135-147) of one pod,
+ * as parsePodDeviceShareExtensions reads them (deviceshare/utils.go:414-482).  Passed apart from ke_pod (most
+ * pods have none): ke_set_pod_device_hints stores a table, ke_pod.device_hint = 1 + an index into it. */
+#define KE_DSTRATEGY_NONE 0
+#define KE_DSTRATEGY_APPLY_FOR_ALL 1     /* desired count = the node's devices of the type (matching the Selector) */
+#define KE_DSTRATEGY_REQUESTS_AS_COUNT 2 /* desired count = the request, 1 (100 with DeviceLevel) per instance */
+#define KE_DEXCL_NONE 0
+#define KE_DEXCL_DEVICE_LEVEL 1          /* RequestsAsCount asks 100 per instance (devicehandler_default.go:84-86) */
+#define KE_DEXCL_PCIE_LEVEL 2            /* nodeDevice.filter's PCIe intersection, whose result the reference
+                                            discards (device_cache.go:382-385): no effect */
+typedef struct ke_device_hint {
+  ke_label_selector selector;    /* Selector: filterNodeDevice keeps the matching devices (device_allocator.go:140-169) */
+  ke_label_selector vf_selector; /* VFSelector: mustAllocateVF, allocateVF over matching VF groups (:396-455)   */
+  int32_t strategy;  /* KE_DSTRATEGY_* (DefaultDeviceHandler; the GPU handler ignores it) */
+  int32_t exclusive; /* KE_DEXCL_* */
+} ke_device_hint; /* 248 bytes */
+typedef struct ke_pod_device_hints {
+  ke_device_hint hint[KE_DEV_TYPES];
+  int32_t invalid;        /* a Selector / VFSelector LabelSelectorAsSelector rejects: PreFilter UnschedulableAndUnresolvable */
+  int32_t has_selectors;  /* state.hasSelectors: some hint of any device type has a Selector (utils.go:446-452) */
+  /* DeviceJointAllocate.DeviceTypes after parsePodDeviceShareExtensions: the requested, non-ApplyForAll types in
+   * annotation order (joint_n = 0: no joint allocation); RequiredScope SamePCIe */
+  int32_t joint_n;
+  int32_t joint_types[KE_DEV_TYPES];
+  int32_t joint_same_pcie;
+  int32_t pad;
+} ke_pod_device_hints; /* 768 bytes */
+/* The hint table ke_pod.device_hint indexes for the following ke_eval / ke_schedule / ke_pod_release calls
+ * (copied; replaces the previous table). */
+int ke_set_pod_device_hints(ke_ctx* ctx, int32_t n, const ke_pod_device_hints* hints);
+
+/* GPU shared resource templates (GPUSharedResourceTemplates ConfigMap, gpu_shared_resource_templates_cache.go):
+ * per node GPU model key (node labels gpu vendor / model -> "<vendor>-<model>", an id of ke_label_id) the named
+ * per-GPU resource lists.  A shared-GPU pod whose per-GPU request names a key of
+ * ke_deviceshare_args.template_matched_keys is allocated by template (allocateByTemplate, allocator_gpu.go:135-159). */
+typedef struct ke_gpu_template {
+  int32_t model_key; /* ke_label_id("<vendor>-<model>") */
+  int32_t name;      /* ke_label_id(template name) */
+  uint8_t has[KE_DKEYS];
+  uint8_t pad[5];
+  int64_t value[KE_DKEYS]; /* gpu-core, gpu-memory, gpu-memory-ratio (KE_DKEY_*) */
+} ke_gpu_template; /* 40 bytes */
+int ke_gpu_templates_load(ke_ctx* ctx, int32_t n, const ke_gpu_template* templates);
+/* The node's device-level labels the allocator reads: secondaryDeviceWellPlanned (Device label,
+ * apis/extension IsSecondaryDeviceWellPlanned) and the GPU template key of the node (0 = none). */
+int ke_node_device_flags(ke_ctx* ctx, int32_t node, int32_t secondary_well_planned, int32_t gpu_model_key);
 
 /* ke_pod.gpu_required_topology_scope: apiext.DeviceTopologyScope and its DeviceTopologyScopeLevel */
 #define KE_SCOPE_NONE 0     /* ""                                                  */
@@ -488,12 +587,8 @@ typedef struct ke_pod {
 #define KE_SCOPE_PCIE 3     /* "PCIe"      level 3                                 */
 #define KE_SCOPE_DEVICE 4   /* "Device"    level 4                                 */
 #define KE_SCOPE_UNKNOWN 5  /* any other non-empty string: required, level 0       */
-/* ke_pod.device_hints: fields of the DeviceAllocateHints annotation (any device type) outside the modelled
- * path -> KE_ERR_UNSUPPORTED.  A hint with none of them set changes nothing (devicehandler_default.go:44-93). */
-#define KE_DHINT_SELECTOR 1u        /* DeviceHint.Selector (filterNodeDevice by device labels)          */
-#define KE_DHINT_VF 2u              /* DeviceHint.VFSelector: mustAllocateVF (device_allocator.go:396-460) */
-#define KE_DHINT_STRATEGY 4u        /* DeviceHint.AllocateStrategy (ApplyForAll / RequestsAsCount)       */
-#define KE_DHINT_EXCLUSIVE 8u       /* DeviceHint.ExclusivePolicy (PCIe-level exclusive)                  */
+/* ke_pod.device_hints: parts of the DeviceAllocateHints annotation outside the modelled path -> KE_ERR_UNSUPPORTED */
+#define KE_DHINT_GPU_VF 2u          /* DeviceHint.VFSelector on the gpu type (defaultAllocateDevices' VF path for GPUs) */
 
 /* One candidate of a pod's speculative top-k list (device order: best first). */
 typedef struct ke_candidate {
@@ -501,7 +596,6 @@ typedef struct ke_candidate {
   int32_t score; /* framework total score */
 } ke_candidate;
 
-typedef struct ke_ctx ke_ctx;
 
 /* ---- lifecycle ------------------------------------------------------------------------------- */
 int ke_create(const ke_config* cfg, ke_ctx** out);
@@ -510,8 +604,8 @@ const char* ke_last_error(void);
 int ke_abi_version(void);
 /* sizeof() of ke_config, ke_node, ke_node_metric, ke_pod_metric, ke_aggregated_usage, ke_pod,
  * ke_resource_map, ke_loadaware_args, ke_numa_args, ke_deviceshare_args, ke_device, ke_numa_zone, ke_cpu,
- * ke_quota_args, ke_quota, ke_gpu_partition, ke_ext_args, ke_node_resource, ke_pod_allocation (in that order) for binding-layout
- * checks. */
+ * ke_quota_args, ke_quota, ke_gpu_partition, ke_ext_args, ke_node_resource, ke_pod_allocation, ke_pod_device_hints,
+ * ke_gpu_template (in that order) for binding-layout checks. */
 int ke_abi_struct_sizes(int32_t* sizes, int32_t n);
 /* 1 if this build has a usable HIP device and its gfx950 kernels loaded, else 0. */
 int ke_device_available(void);
@@ -634,7 +728,9 @@ typedef struct ke_pod_allocation {
   uint64_t cpuset[4];                   /* bit c = CPU id c (ke_last_cpusets)                 */
   int64_t numa[KE_MAX_NUMA * KE_NRES];  /* [2*id + r] per NUMA id (ke_last_numa_allocations) */
   uint64_t device_minors;               /* bit 16*type + minor (ke_last_device_allocations)   */
-} ke_pod_allocation; /* 176 bytes */
+  /* allocateVF: the VF rank taken on each allocated RDMA / FPGA minor, -1 = none ([type - 1][minor]) */
+  int8_t vf_rank[2][KE_MAX_MINORS];
+} ke_pod_allocation; /* 208 bytes */
 /* ke_pod_release modes */
 #define KE_RELEASE_UNRESERVE 0 /* the framework's Unreserve of every Reserve plugin + ForgetPod:
                                   loadaware podAssignCache.unAssign (load_aware.go:197-199),
@@ -758,6 +854,14 @@ int ke_decode_node_metric(const char* json, int64_t len, ke_node_metric* nm, int
 int ke_decode_pod(const char* json, int64_t len, int32_t n_names, const char* const* xres_names, ke_pod* out);
 int ke_decode_device(const char* json, int64_t len, int32_t cap, ke_device* out, int32_t* n, int32_t part_cap,
                      ke_gpu_partition* parts, int32_t* n_parts, int32_t* has_table, int32_t* honor);
+/* A pod's DeviceAllocateHints + DeviceJointAllocate annotations (parsePodDeviceShareExtensions,
+ * deviceshare/utils.go:414-482; selectors through GetFastLabelSelector); *present = 0 when neither annotation
+ * is set (the pod needs no hint entry).  Label strings are interned with ke_label_id. */
+int ke_decode_pod_device_hints(const char* json, int64_t len, ke_pod_device_hints* out, int32_t* present);
+/* The node-level device flags ke_node_device_flags takes: the Device's secondary-device-well-planned label and the
+ * GPU template key of the Node ("<gpu vendor label>-<gpu model label>" interned; 0 without both labels). */
+int ke_decode_device_flags(const char* device_json, int64_t device_len, const char* node_json, int64_t node_len,
+                           int32_t* secondary_well_planned, int32_t* gpu_model_key);
 /* NodeResourceTopology (NewTopologyOptions, nodenumaresource/topology_options.go:90-236): the zones of type
  * "Node" named node-<id> with their Allocatable cpu / memory (cpu less 1000 per reserved CPU of the zone), the CPU
  * table of the cpu-topology annotation (core id = socket << 16 | core) with the reserved CPUs (kubelet-managed

@@ -9,7 +9,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 ABSENT = -1
 
 OK = 0
@@ -54,11 +54,21 @@ REASON_DS_MULTI_SHARED_GPU = 40
 REASON_DS_INSUFFICIENT_TOPOLOGY_SCOPED = 41
 REASON_DS_INSUFFICIENT_GPU_TOPOLOGY = 42
 REASON_DS_INSUFFICIENT_NUMA_SCOPED = 43
+REASON_DS_INVALID_HINT = 44
+REASON_DS_INSUFFICIENT_RDMA_VF = 45
+REASON_DS_INSUFFICIENT_FPGA_VF = 46
+REASON_DS_INSUFFICIENT_PRIMARY = 47
+REASON_DS_JOINT_VIOLATION = 48
+REASON_DS_NO_MATCHED_TEMPLATE = 49
 # ke_pod.gpu_required_topology_scope (apiext.DeviceTopologyScope -> level)
 SCOPE_NONE, SCOPE_NODE, SCOPE_NUMA, SCOPE_PCIE, SCOPE_DEVICE, SCOPE_UNKNOWN = range(6)
 SCOPES = {"": SCOPE_NONE, "Node": SCOPE_NODE, "NUMANode": SCOPE_NUMA, "PCIe": SCOPE_PCIE, "Device": SCOPE_DEVICE}
 # ke_pod.device_hints bits (DeviceAllocateHints fields the evaluator does not model)
-DHINT_SELECTOR, DHINT_VF, DHINT_STRATEGY, DHINT_EXCLUSIVE = 1, 2, 4, 8
+DHINT_GPU_VF = 2
+DSTRATEGY_NONE, DSTRATEGY_APPLY_FOR_ALL, DSTRATEGY_REQUESTS_AS_COUNT = 0, 1, 2
+DEXCL_NONE, DEXCL_DEVICE_LEVEL, DEXCL_PCIE_LEVEL = 0, 1, 2
+SEL_IN, SEL_NOT_IN, SEL_EXISTS, SEL_DOES_NOT_EXIST = 0, 1, 2, 3
+MAX_LABELS, MAX_SEL_REQS, MAX_SEL_VALUES, MAX_VF_GROUPS = 8, 4, 4, 4
 TEMPLATE_KEY_CORE, TEMPLATE_KEY_MEMORY, TEMPLATE_KEY_MEMORY_RATIO = 1, 2, 4
 MAX_GPU_PARTITIONS = 64
 
@@ -146,6 +156,22 @@ class DeviceShareArgs(C.Structure):
                 ("disable_numa_alignment", u8), ("pad", u8)]
 
 
+class Labels(C.Structure):
+    _fields_ = [("n", i32), ("key", i32 * MAX_LABELS), ("value", i32 * MAX_LABELS)]
+
+
+class LabelRequirement(C.Structure):
+    _fields_ = [("key", i32), ("op", i32), ("n_values", i32), ("values", i32 * MAX_SEL_VALUES)]
+
+
+class LabelSelector(C.Structure):
+    _fields_ = [("present", i32), ("n", i32), ("req", LabelRequirement * MAX_SEL_REQS)]
+
+
+class VfGroup(C.Structure):
+    _fields_ = [("labels", Labels), ("pad", i32), ("vfs", C.c_uint64)]
+
+
 class Device(C.Structure):
     _fields_ = [
         ("type", i32),
@@ -158,7 +184,24 @@ class Device(C.Structure):
         ("used", i64 * DKEYS),
         ("numa_node", i32),
         ("pcie_rank", i32),
+        ("labels", Labels),
+        ("n_vf_groups", i32),
+        ("vf_groups", VfGroup * MAX_VF_GROUPS),
+        ("vf_allocated", C.c_uint64),
     ]
+
+
+class DeviceHint(C.Structure):
+    _fields_ = [("selector", LabelSelector), ("vf_selector", LabelSelector), ("strategy", i32), ("exclusive", i32)]
+
+
+class PodDeviceHints(C.Structure):
+    _fields_ = [("hint", DeviceHint * DEV_TYPES), ("invalid", i32), ("has_selectors", i32), ("joint_n", i32),
+                ("joint_types", i32 * DEV_TYPES), ("joint_same_pcie", i32), ("pad", i32)]
+
+
+class GpuTemplate(C.Structure):
+    _fields_ = [("model_key", i32), ("name", i32), ("has", u8 * DKEYS), ("pad", u8 * 5), ("value", i64 * DKEYS)]
 
 
 class GpuPartition(C.Structure):
@@ -288,7 +331,7 @@ class Pod(C.Structure):
         ("xres_request_mask", C.c_uint64),
         ("n_xres", i32),
         ("xres_id", i32 * MAX_POD_XRES),
-        ("pad3", i32),
+        ("device_hint", i32),
         ("xres_value", i64 * MAX_POD_XRES),
     ]
 
@@ -325,12 +368,15 @@ RELEASE_UNRESERVE, RELEASE_DELETE = 0, 1  # ke_pod_release modes
 class PodAllocation(C.Structure):
     """ke_pod_allocation: what one placement reserved (Unreserve / informer-delete record)."""
     _fields_ = [("node", i32), ("quota_assigned", u8), ("pad", u8 * 3), ("cpuset", C.c_uint64 * 4),
-                ("numa", i64 * (MAX_NUMA * NRES)), ("device_minors", C.c_uint64)]
+                ("numa", i64 * (MAX_NUMA * NRES)), ("device_minors", C.c_uint64),
+                ("vf_rank", C.c_int8 * (2 * MAX_MINORS))]
 
 
 STRUCTS = [Config, Node, NodeMetric, PodMetric, AggregatedUsage, Pod, ResourceMap, LoadAwareArgs, NumaArgs,
            DeviceShareArgs, Device, NumaZone, Cpu, QuotaArgs, Quota, GpuPartition, ExtArgs, NodeResource,
-           PodAllocation]
+           PodAllocation, PodDeviceHints, GpuTemplate]
+POD_DEVICE_HINTS_DTYPE = np.dtype(PodDeviceHints)
+GPU_TEMPLATE_DTYPE = np.dtype(GpuTemplate)
 QUOTA_DTYPE = np.dtype(Quota)
 
 # numpy views of the same layouts (bulk loads)
@@ -347,6 +393,18 @@ NODE_RESOURCE_DTYPE = np.dtype(NodeResource)
 POD_ALLOCATION_DTYPE = np.dtype(PodAllocation)
 
 ROW_DTYPE = np.dtype([("f", np.int64, (18,)), ("flags", np.uint32), ("pad", np.uint32)])
+
+
+def struct_array(items, ctype):
+    """list of ctypes `ctype` structures | numpy array of np.dtype(ctype) -> contiguous numpy array"""
+    dt = np.dtype(ctype)
+    if isinstance(items, np.ndarray):
+        return np.ascontiguousarray(items, dt)
+    arr = np.zeros(len(items), dt)
+    if len(items):
+        buf = (ctype * len(items))(*items)
+        arr[:] = np.frombuffer(buf, dtype=dt, count=len(items))
+    return arr
 
 
 def default_config(node_capacity, pod_batch=64, device_ordinal=0, global_node_offset=0):
@@ -421,6 +479,12 @@ EXPORTS = {
     "ke_decode_device": (C.c_int, [C.c_char_p, i64, i32, C.c_void_p, C.POINTER(i32), i32, C.c_void_p, C.POINTER(i32),
                                    C.POINTER(i32), C.POINTER(i32)]),
     "ke_node_resources_get": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p, C.POINTER(i32)]),
+    "ke_label_id": (i32, [C.c_char_p]),
+    "ke_set_pod_device_hints": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
+    "ke_gpu_templates_load": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
+    "ke_node_device_flags": (C.c_int, [C.c_void_p, i32, i32, i32]),
+    "ke_decode_pod_device_hints": (C.c_int, [C.c_char_p, i64, C.POINTER(PodDeviceHints), C.POINTER(i32)]),
+    "ke_decode_device_flags": (C.c_int, [C.c_char_p, i64, C.c_char_p, i64, C.POINTER(i32), C.POINTER(i32)]),
     "ke_last_device_allocations": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_last_numa_allocations": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_node_cpus_set": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p, i32]),

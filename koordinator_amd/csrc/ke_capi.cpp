@@ -39,10 +39,13 @@ static int check_node(ke_ctx* ctx, int32_t node) {
   return KE_OK;
 }
 
-static int check_pods(const ke_pod* pods, int32_t n) {
+static int check_pods(const ke_pod* pods, int32_t n, const Context* c = nullptr) {
   if (n < 0 || (n > 0 && !pods)) return fail(KE_ERR_INVALID, "pods");
   for (int32_t p = 0; p < n; p++) {
     int rc = validate_pod(pods[p]);
+    if (rc) return rc;
+    if (c) rc = validate_pod_hints(*c, pods[p]);
+    else if (pods[p].device_hint) rc = fail(KE_ERR_INVALID, "ke_pod.device_hint without a context");
     if (rc) return rc;
   }
   return KE_OK;
@@ -61,29 +64,12 @@ static int check_numa_deviceshare(ke_ctx* ctx, const ke_pod* pods, int32_t n) {
   return KE_OK;
 }
 
-// allocateByTemplate (allocator_gpu.go:135-159): a shared-GPU pod whose per-GPU request names one of
-// GPUSharedResourceTemplatesMatchedResources enforces a template (utils.go:508-515); not implemented.
-static int check_gpu_templates(ke_ctx* ctx, const ke_pod* pods, int32_t n) {
-  const uint32_t keys = ctx->c.cfg.deviceshare.template_matched_keys;
-  if (!keys) return KE_OK;
-  for (int32_t p = 0; p < n; p++) {
-    const DevPod d = make_dev_pod(ctx->c.cfg, pods[p]);
-    if (!(d.flags & PF_DS) || !d.ds_cnt[KE_DEV_GPU] || !(d.flags & PF_GPU_SHARED)) continue;
-    uint32_t req = 0;
-    if (d.flags & PF_DS_H_CORE) req |= KE_TEMPLATE_KEY_CORE;
-    if (d.flags & PF_DS_H_RATIO) req |= KE_TEMPLATE_KEY_MEMORY_RATIO;
-    else if (d.flags & PF_DS_H_MEM) req |= KE_TEMPLATE_KEY_MEMORY;
-    if (req & keys) return fail(KE_ERR_UNSUPPORTED, "shared-GPU pods allocated by GPU shared resource template");
-  }
-  return KE_OK;
-}
-
 // A pod that may bind CPUs (a cpuset pod, or any cpu request while a node forces CPU binding) reads the
 // CPU SoA during evaluation: make sure it exists.
 static int check_cpuset(ke_ctx* ctx, const ke_pod* pods, int32_t n) {
   Context& c = ctx->c;
   for (int32_t p = 0; p < n; p++) {
-    const uint32_t f = make_dev_pod(c.cfg, pods[p]).flags;
+    const uint32_t f = make_dev_pod(c.cfg, pods[p], pod_hints(c, pods[p]), &c.tmpl).flags;
     if ((f & PF_CPUSET) || (c.n_bind_nodes > 0 && pods[p].requests[KE_RES_CPU] > 0)) c.cpu_enabled = true;
   }
   return KE_OK;
@@ -102,7 +88,8 @@ int ke_abi_struct_sizes(int32_t* sizes, int32_t n) {
                          (int32_t)sizeof(ke_cpu),          (int32_t)sizeof(ke_quota_args),
                          (int32_t)sizeof(ke_quota),        (int32_t)sizeof(ke_gpu_partition),
                          (int32_t)sizeof(ke_ext_args),     (int32_t)sizeof(ke_node_resource),
-                         (int32_t)sizeof(ke_pod_allocation)};
+                         (int32_t)sizeof(ke_pod_allocation), (int32_t)sizeof(ke_pod_device_hints),
+                         (int32_t)sizeof(ke_gpu_template)};
   const int32_t m = (int32_t)(sizeof(all) / sizeof(all[0]));
   for (int32_t i = 0; i < n && i < m; i++) sizes[i] = all[i];
   return m;
@@ -255,8 +242,39 @@ int ke_node_devices_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_device* d
   NodeState& ns = ctx->c.nodes[node];
   ns.has_dev_cache = true;
   ns.devs.assign(devices, devices + n);
+  rc = intern_device_labels(ctx->c, ns);
+  if (rc) return rc;
   ns.dirty = true;
   ctx->c.ds_enabled = true;
+  return KE_OK;
+}
+
+int ke_node_device_flags(ke_ctx* ctx, int32_t node, int32_t secondary_well_planned, int32_t gpu_model_key) {
+  int rc = check_node(ctx, node);
+  if (ctx) flush_mirror(ctx->c);
+  if (rc) return rc;
+  const int id = intern_model_key(ctx->c, gpu_model_key);
+  if (id < 0) return id;
+  NodeState& ns = ctx->c.nodes[node];
+  ns.secondary_well_planned = secondary_well_planned != 0;
+  ns.gpu_model_id = id;
+  ns.dirty = true;
+  return KE_OK;
+}
+
+int ke_set_pod_device_hints(ke_ctx* ctx, int32_t n, const ke_pod_device_hints* hints) {
+  if (!ctx || n < 0 || (n > 0 && !hints)) return fail(KE_ERR_INVALID, "ke_set_pod_device_hints arguments");
+  ctx->c.hints.assign(hints, hints + n);
+  return KE_OK;
+}
+
+int ke_gpu_templates_load(ke_ctx* ctx, int32_t n, const ke_gpu_template* templates) {
+  if (!ctx || n < 0 || (n > 0 && !templates)) return fail(KE_ERR_INVALID, "ke_gpu_templates_load arguments");
+  for (int32_t i = 0; i < n; i++) {
+    const int id = intern_model_key(ctx->c, templates[i].model_key);
+    if (id < 0) return id;
+  }
+  ctx->c.tmpl.assign(templates, templates + n);
   return KE_OK;
 }
 
@@ -492,11 +510,9 @@ int ke_eval(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, uin
             int16_t* la_score, int16_t* numa_score, int16_t* ds_score, int16_t* total, int32_t* best) {
   if (!ctx) return fail(KE_ERR_INVALID, "null context");
   if (ctx) flush_mirror(ctx->c);
-  int rc = check_pods(pods, n_pods);
+  int rc = check_pods(pods, n_pods, &ctx->c);
   if (rc) return rc;
   rc = check_numa_deviceshare(ctx, pods, n_pods);
-  if (rc) return rc;
-  rc = check_gpu_templates(ctx, pods, n_pods);
   if (rc) return rc;
   rc = check_cpuset(ctx, pods, n_pods);
   if (rc) return rc;
@@ -509,11 +525,9 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
   if (!ctx || (n_pods > 0 && !chosen)) return fail(KE_ERR_INVALID, "ke_schedule arguments");
   using clk = std::chrono::steady_clock;
   auto tp = clk::now();
-  int rc = check_pods(pods, n_pods);
+  int rc = check_pods(pods, n_pods, &ctx->c);
   if (rc) return rc;
   rc = check_numa_deviceshare(ctx, pods, n_pods);
-  if (rc) return rc;
-  rc = check_gpu_templates(ctx, pods, n_pods);
   if (rc) return rc;
   rc = check_cpuset(ctx, pods, n_pods);
   if (rc) return rc;
@@ -535,6 +549,7 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
     return c.quotas[(size_t)pods[p].quota - 1].limit_is_max != 0;
   };
   std::vector<uint64_t> all_dev, all_cs;
+  std::vector<int8_t> all_vf;
   std::vector<int64_t> all_numa;
   std::vector<double> all_batch_ms;
   double all_ms = 0;
@@ -561,7 +576,8 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
       c.pending.push_back({node, now_ns, pods[p]});
       const bool was_dirty = ns.dirty;
       if (i < (int32_t)c.last_dev_alloc.size() && c.last_dev_alloc[i])
-        host_ds_reserve(c.cfg, ns, make_dev_pod(c.cfg, pods[p]), c.last_dev_alloc[i]);
+        host_ds_reserve(c.cfg, ns, make_dev_pod(c.cfg, pods[p], pod_hints(c, pods[p]), &c.tmpl), c.last_dev_alloc[i],
+                        (int64_t)c.last_vf.size() >= (int64_t)(i + 1) * 2 * KE_MAX_MINORS ? &c.last_vf[(size_t)i * 2 * KE_MAX_MINORS] : nullptr);
       if ((int64_t)c.last_numa_alloc.size() >= (int64_t)(i + 1) * KE_MAX_NUMA * KE_NRES)
         host_numa_reserve(ns, &c.last_numa_alloc[(size_t)i * KE_MAX_NUMA * KE_NRES]);
       ns.dirty = was_dirty;  // the device rows already carry these Reserves
@@ -574,6 +590,8 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
     const bool whole = s0 == 0 && s1 == n_pods;  // one segment: the last_* outputs are already whole
     if (!whole) {
       all_dev.insert(all_dev.end(), c.last_dev_alloc.begin(), c.last_dev_alloc.end());
+      if (c.last_vf.empty()) all_vf.resize(all_vf.size() + (size_t)len * 2 * KE_MAX_MINORS, -1);
+      else all_vf.insert(all_vf.end(), c.last_vf.begin(), c.last_vf.end());
       all_cs.insert(all_cs.end(), c.last_cpusets.begin(), c.last_cpusets.end());
       numa_out = numa_out || !c.last_numa_alloc.empty();
       if (c.last_numa_alloc.empty()) all_numa.resize(all_numa.size() + (size_t)len * KE_MAX_NUMA * KE_NRES, 0);
@@ -598,6 +616,7 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
   }
   if (multi) {
     c.last_dev_alloc.swap(all_dev);
+    c.last_vf.swap(all_vf);
     c.last_cpusets.swap(all_cs);
     if (numa_out) c.last_numa_alloc.swap(all_numa);
     else c.last_numa_alloc.clear();
@@ -618,6 +637,7 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
 // the release record of position p of the last ke_schedule
 static ke_pod_allocation last_allocation(const Context& c, int32_t p) {
   ke_pod_allocation a{};
+  memset(a.vf_rank, -1, sizeof a.vf_rank);
   a.node = p < (int32_t)c.last_chosen.size() ? c.last_chosen[(size_t)p] : -1;
   if (a.node < 0) return a;
   a.quota_assigned = c.last_quota[(size_t)p];
@@ -627,6 +647,9 @@ static ke_pod_allocation last_allocation(const Context& c, int32_t p) {
   for (int w = 0; w < W; w++)
     a.numa[w] = (int64_t)c.last_numa_alloc.size() >= (int64_t)(p + 1) * W ? c.last_numa_alloc[(size_t)p * W + w] : 0;
   a.device_minors = p < (int32_t)c.last_dev_alloc.size() ? c.last_dev_alloc[(size_t)p] : 0;
+  for (int k = 0; k < 2 * KE_MAX_MINORS; k++)
+    a.vf_rank[k / KE_MAX_MINORS][k % KE_MAX_MINORS] =
+        (int64_t)c.last_vf.size() >= (int64_t)(p + 1) * 2 * KE_MAX_MINORS ? c.last_vf[(size_t)p * 2 * KE_MAX_MINORS + k] : (int8_t)-1;
   return a;
 }
 
@@ -642,13 +665,15 @@ int ke_pod_release(ke_ctx* ctx, const ke_pod* pod, const ke_pod_allocation* allo
   int rc = validate_pod(*pod);
   if (rc) return rc;
   Context& c = ctx->c;
+  rc = validate_pod_hints(c, *pod);
+  if (rc) return rc;
   flush_mirror(c);  // the pod's own deferred Reserve mirror first
   if (pod->quota < 0 || pod->quota > (int32_t)c.quotas.size())
     return fail(KE_ERR_INVALID, "ke_pod.quota outside the loaded ElasticQuota tree");
   const int32_t node = alloc->node < 0 ? -1 : alloc->node - c.cfg.global_node_offset;
   if (node >= c.cfg.node_capacity) return fail(KE_ERR_NOT_FOUND, "ke_pod_release: node index out of range");
   if (node >= 0 && c.nodes[(size_t)node].valid)  // (a node of another context's range: only the quota part)
-    host_release_node(c.cfg, c.ext_enabled, c.nodes[(size_t)node], *pod, *alloc);
+    host_release_node(c.cfg, c.ext_enabled, c.nodes[(size_t)node], *pod, *alloc, pod_hints(c, *pod));
   const bool assigned = alloc->node >= 0 && alloc->quota_assigned;
   if (pod->quota > 0 && (assigned || mode == KE_RELEASE_DELETE)) {
     if (c.dev) {

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -141,6 +142,19 @@ int ke_quantity_parse(const char* s, int64_t* value, int64_t* milli_value) {
   if (!parse_quantity(s, value, milli_value, &ov))
     return ov ? unsup(std::string("quantity out of the int64 range: ") + s) : bad(std::string("malformed quantity: ") + s);
   return KE_OK;
+}
+
+// the process-wide label string table (ke_label_id): ids from 1, stable for the process
+int32_t ke_label_id(const char* str) {
+  if (!str || !*str) return 0;
+  static std::mutex mu;
+  static std::map<std::string, int32_t> ids;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = ids.find(str);
+  if (it != ids.end()) return it->second;
+  const int32_t id = (int32_t)ids.size() + 1;
+  ids.emplace(str, id);
+  return id;
 }
 
 int64_t ke_pod_key(const char* ns, const char* name) {
@@ -670,10 +684,8 @@ int ke_decode_pod(const char* js, int64_t len, int32_t n_names, const char* cons
         const Value& h = kv.second;
         if (!h.is_obj()) continue;
         auto set = [&](const char* f) { const Value* x = h.field(f); return x && !x->is_null(); };
-        if (set("selector")) bits |= KE_DHINT_SELECTOR;
-        if (set("vfSelector")) bits |= KE_DHINT_VF;
-        if (*str_or_empty(h.field("allocateStrategy"))) bits |= KE_DHINT_STRATEGY;
-        if (*str_or_empty(h.field("exclusivePolicy"))) bits |= KE_DHINT_EXCLUSIVE;
+        // the hints themselves come from ke_decode_pod_device_hints; a gpu VFSelector is not modelled
+        if (kv.first == "gpu" && set("vfSelector")) bits |= KE_DHINT_GPU_VF;
         const std::string sc = str_or_empty(h.field("requiredTopologyScope"));
         if (kv.first == "gpu" && !sc.empty())
           p.gpu_required_topology_scope = sc == "Node" ? KE_SCOPE_NODE : sc == "NUMANode" ? KE_SCOPE_NUMA
@@ -703,6 +715,66 @@ int ke_decode_pod(const char* js, int64_t len, int32_t n_names, const char* cons
   }
   *out = p;
   return KE_OK;
+}
+
+// a string map of labels into (key, value) ids (Go map order is irrelevant: matching is by key)
+static bool labels_of(const Value* v, ke_labels& out) {
+  out = ke_labels{};
+  if (!v || v->is_null()) return true;
+  if (!v->is_obj()) return false;
+  for (const auto& kv : v->o) {
+    if (kv.second.t != Value::STR || out.n >= KE_MAX_LABELS) return false;
+    out.key[out.n] = ke_label_id(kv.first.c_str());
+    out.value[out.n] = ke_label_id(kv.second.s.c_str());
+    out.n++;
+  }
+  return true;
+}
+
+// metav1.LabelSelector -> labels.Selector (util.GetFastLabelSelector, pkg/util/selector.go:24-32; apimachinery
+// LabelSelectorAsSelector): matchLabels entries become In requirements with one value, matchExpressions keep
+// their operator (In / NotIn need values, Exists / DoesNotExist take none; anything else is an error)
+static bool selector_of(const Value* v, ke_label_selector& out, bool* invalid) {
+  out = ke_label_selector{};
+  if (!v || v->is_null()) return true;
+  if (!v->is_obj()) return false;
+  out.present = 1;
+  const Value* ml = v->field("matchLabels");
+  if (ml && ml->is_obj())
+    for (const auto& kv : ml->o) {
+      if (kv.second.t != Value::STR || out.n >= KE_MAX_SEL_REQS) return false;
+      ke_label_requirement& r = out.req[out.n++];
+      r.key = ke_label_id(kv.first.c_str());
+      r.op = KE_SEL_IN;
+      r.n_values = 1;
+      r.values[0] = ke_label_id(kv.second.s.c_str());
+    }
+  const Value* me = v->field("matchExpressions");
+  if (me && me->t == Value::ARR)
+    for (const Value& e : me->a) {
+      if (out.n >= KE_MAX_SEL_REQS) return false;
+      ke_label_requirement& r = out.req[out.n++];
+      r.key = ke_label_id(str_or_empty(e.field("key")));
+      const std::string op = str_or_empty(e.field("operator"));
+      const Value* vals = e.field("values");
+      const size_t nv = vals && vals->t == Value::ARR ? vals->a.size() : 0;
+      if (nv > KE_MAX_SEL_VALUES) return false;
+      for (size_t q = 0; q < nv; q++) {
+        if (vals->a[q].t != Value::STR) return false;
+        r.values[q] = ke_label_id(vals->a[q].s.c_str());
+      }
+      r.n_values = (int32_t)nv;
+      if (op == "In" || op == "NotIn") {
+        r.op = op == "In" ? KE_SEL_IN : KE_SEL_NOT_IN;
+        if (nv == 0) *invalid = true;
+      } else if (op == "Exists" || op == "DoesNotExist") {
+        r.op = op == "Exists" ? KE_SEL_EXISTS : KE_SEL_DOES_NOT_EXIST;
+        if (nv != 0) *invalid = true;
+      } else {
+        *invalid = true;
+      }
+    }
+  return true;
 }
 
 // ---- Device ------------------------------------------------------------------------------------------------
@@ -757,6 +829,26 @@ int ke_decode_device(const char* js, int64_t len, int32_t cap, ke_device* out, i
           k.has_total[slot] = 1;
           k.total[slot] = v;
         }
+      }
+      // DeviceInfo.Labels and VFGroups (VF ranks: the device's VFs in BusID string order over all its groups)
+      if (!labels_of(d.field("labels"), k.labels)) return unsup("device labels (more than 8, or not strings)");
+      const Value* vg = d.field("vfGroups");
+      if (vg && !vg->is_null()) {
+        if (vg->t != Value::ARR) return bad("vfGroups");
+        if (vg->a.size() > KE_MAX_VF_GROUPS) return unsup("more than 4 VF groups on a device");
+        std::vector<std::pair<std::string, int>> vfs;  // (BusID, group)
+        for (size_t g = 0; g < vg->a.size(); g++) {
+          const Value& grp = vg->a[g];
+          if (!labels_of(grp.field("labels"), k.vf_groups[g].labels)) return unsup("VF group labels");
+          const Value* list = grp.field("vfs");
+          if (list && list->t == Value::ARR)
+            for (const Value& vf : list->a) vfs.emplace_back(str_or_empty(vf.field("busID")), (int)g);
+        }
+        if (vfs.size() > 64) return unsup("more than 64 VFs on a device");
+        std::stable_sort(vfs.begin(), vfs.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+        for (size_t r = 0; r < vfs.size(); r++) k.vf_groups[vfs[r].second].vfs |= 1ull << r;
+        k.n_vf_groups = (int32_t)vg->a.size();
+        if (k.type == KE_DEV_GPU) k.n_vf_groups = 0;  // GPU VFs are not modelled (a GPU VFSelector is refused)
       }
       const Value* topo = d.field("topology");
       std::string pid;
@@ -837,6 +929,97 @@ int ke_decode_device(const char* js, int64_t len, int32_t cap, ke_device* out, i
 }
 
 }  // extern "C"
+
+// ---- DeviceShare pod hints (parsePodDeviceShareExtensions, deviceshare/utils.go:414-482) ---------------------
+int ke_decode_pod_device_hints(const char* js, int64_t len, ke_pod_device_hints* out, int32_t* present) {
+  if (!out || !present) return bad("ke_decode_pod_device_hints arguments");
+  Value doc;
+  int rc = parse_doc(js, len, doc, "Pod");
+  if (rc) return rc;
+  ke_pod_device_hints h{};
+  *present = 0;
+  const Value* meta = doc.field("metadata");
+  std::map<std::string, std::string> ann;
+  if ((rc = string_map(meta ? meta->field("annotations") : nullptr, ann, "metadata.annotations"))) return rc;
+  auto type_of = [](const std::string& t) { return t == "gpu" ? KE_DEV_GPU : t == "rdma" ? KE_DEV_RDMA : t == "fpga" ? KE_DEV_FPGA : -1; };
+  Value hints;
+  std::string err;
+  if (const std::string* s = lookup(ann, "scheduling.koordinator.sh/device-allocate-hint")) {
+    if (!json::parse(s->data(), s->size(), hints, err) || !(hints.is_null() || hints.is_obj()))
+      return unsup("device-allocate-hint annotation that fails to unmarshal");
+    *present = 1;
+    if (hints.is_obj())
+      for (const auto& kv : hints.o) {
+        const Value& hv = kv.second;
+        if (!hv.is_obj()) continue;
+        bool invalid = false;
+        ke_label_selector sel, vfsel;
+        if (!selector_of(hv.field("selector"), sel, &invalid) || !selector_of(hv.field("vfSelector"), vfsel, &invalid))
+          return unsup("a device hint selector beyond 4 requirements / 4 values");
+        if (invalid) h.invalid = 1;
+        if (sel.present) h.has_selectors = 1;  // any device type, modelled or not (utils.go:446-452)
+        const int t = type_of(kv.first);
+        if (t < 0) continue;
+        ke_device_hint& d = h.hint[t];
+        d.selector = sel;
+        d.vf_selector = vfsel;
+        const std::string st = str_or_empty(hv.field("allocateStrategy"));
+        d.strategy = st == "ApplyForAll" ? KE_DSTRATEGY_APPLY_FOR_ALL
+                     : st == "RequestsAsCount" ? KE_DSTRATEGY_REQUESTS_AS_COUNT : KE_DSTRATEGY_NONE;
+        const std::string ex = str_or_empty(hv.field("exclusivePolicy"));
+        d.exclusive = ex == "DeviceLevel" ? KE_DEXCL_DEVICE_LEVEL : ex == "PCIeLevel" ? KE_DEXCL_PCIE_LEVEL : KE_DEXCL_NONE;
+      }
+  }
+  if (const std::string* s = lookup(ann, "scheduling.koordinator.sh/device-joint-allocate")) {
+    Value v;
+    if (!json::parse(s->data(), s->size(), v, err) || !(v.is_null() || v.is_obj()))
+      return unsup("device-joint-allocate annotation that fails to unmarshal");
+    *present = 1;
+    // the requested, non-ApplyForAll types in annotation order (utils.go:430-442): the caller's ke_pod tells
+    // which types are requested; here every listed gpu / rdma / fpga type is kept and ke_schedule's PreFilter
+    // drops the unrequested ones (decode the pod with ke_decode_pod for them)
+    const Value* types = v.field("deviceTypes");
+    if (types && types->t == Value::ARR)
+      for (const Value& tv : types->a) {
+        const int t = type_of(tv.t == Value::STR ? tv.s : "");
+        if (t < 0 || h.hint[t].strategy == KE_DSTRATEGY_APPLY_FOR_ALL) continue;
+        bool dup = false;
+        for (int j = 0; j < h.joint_n; j++) dup = dup || h.joint_types[j] == t;
+        if (!dup && h.joint_n < KE_DEV_TYPES) h.joint_types[h.joint_n++] = t;
+      }
+    h.joint_same_pcie = std::string(str_or_empty(v.field("requiredScope"))) == "SamePCIe";
+  }
+  *out = h;
+  return KE_OK;
+}
+
+int ke_decode_device_flags(const char* device_json, int64_t device_len, const char* node_json, int64_t node_len,
+                           int32_t* secondary_well_planned, int32_t* gpu_model_key) {
+  if (!secondary_well_planned || !gpu_model_key) return bad("ke_decode_device_flags arguments");
+  *secondary_well_planned = 0;
+  *gpu_model_key = 0;
+  Value doc;
+  int rc;
+  if (device_json) {
+    if ((rc = parse_doc(device_json, device_len, doc, "Device"))) return rc;
+    const Value* meta = doc.field("metadata");
+    std::map<std::string, std::string> lab;
+    if ((rc = string_map(meta ? meta->field("labels") : nullptr, lab, "metadata.labels"))) return rc;
+    const std::string* w = lookup(lab, "node.koordinator.sh/secondary-device-well-planned");
+    *secondary_well_planned = w && *w == "true";
+  }
+  if (node_json) {
+    if ((rc = parse_doc(node_json, node_len, doc, "Node"))) return rc;
+    const Value* meta = doc.field("metadata");
+    std::map<std::string, std::string> lab;
+    if ((rc = string_map(meta ? meta->field("labels") : nullptr, lab, "metadata.labels"))) return rc;
+    const std::string* vendor = lookup(lab, "node.koordinator.sh/gpu-vendor");
+    const std::string* model = lookup(lab, "node.koordinator.sh/gpu-model");
+    const std::string key = (vendor ? *vendor : std::string()) + "-" + (model ? *model : std::string());  // buildGPUSharedResourceTemplatesKey
+    *gpu_model_key = ke_label_id(key.c_str());
+  }
+  return KE_OK;
+}
 
 // ---- NodeResourceTopology (nodenumaresource/topology_options.go:90-236) -----------------------------------
 namespace {

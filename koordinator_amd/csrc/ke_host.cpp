@@ -118,8 +118,193 @@ int validate_devices(int32_t n, const ke_device* devs) {
     // fillGPUTotalMem divides by the instance's gpu-memory (devicehandler_gpu.go:110-125)
     if (d.type == KE_DEV_GPU && d.health && !(d.has_total[KE_DKEY_GPU_MEMORY] && d.total[KE_DKEY_GPU_MEMORY] > 0))
       return fail(KE_ERR_UNSUPPORTED, "healthy GPU device without a positive gpu-memory total");
+    if (d.labels.n < 0 || d.labels.n > KE_MAX_LABELS || d.n_vf_groups < 0 || d.n_vf_groups > KE_MAX_VF_GROUPS)
+      return fail(KE_ERR_INVALID, "device label / VF group count");
+    for (int g = 0; g < d.n_vf_groups; g++)
+      if (d.vf_groups[g].labels.n < 0 || d.vf_groups[g].labels.n > KE_MAX_LABELS)
+        return fail(KE_ERR_INVALID, "VF group label count");
   }
   return KE_OK;
+}
+
+// ---- DeviceShare hints -------------------------------------------------------------
+static std::vector<std::pair<int32_t, int32_t>> label_pairs(const ke_labels& l) {
+  std::vector<std::pair<int32_t, int32_t>> v;
+  for (int k = 0; k < l.n && k < KE_MAX_LABELS; k++) v.emplace_back(l.key[k], l.value[k]);
+  std::sort(v.begin(), v.end());
+  return v;
+}
+static int intern_set(Context& c, const ke_labels& l) {
+  auto v = label_pairs(l);
+  auto it = c.label_set_ids.find(v);
+  if (it != c.label_set_ids.end()) return it->second;
+  if (c.label_sets.size() >= 256) return fail(KE_ERR_UNSUPPORTED, "more than 256 distinct device / VF-group label sets");
+  const int id = (int)c.label_sets.size();
+  c.label_sets.push_back(v);
+  c.label_set_ids.emplace(std::move(v), id);
+  return id;
+}
+int intern_device_labels(Context& c, NodeState& ns) {
+  ns.dev_lbl.assign(ns.devs.size() * 5, 0);
+  for (size_t i = 0; i < ns.devs.size(); i++) {
+    const ke_device& d = ns.devs[i];
+    int id = intern_set(c, d.labels);
+    if (id < 0) return id;
+    ns.dev_lbl[i * 5] = (uint8_t)id;
+    for (int g = 0; g < d.n_vf_groups && g < KE_MAX_VF_GROUPS; g++) {
+      id = intern_set(c, d.vf_groups[g].labels);
+      if (id < 0) return id;
+      ns.dev_lbl[i * 5 + 1 + g] = (uint8_t)id;
+    }
+  }
+  return KE_OK;
+}
+int intern_model_key(Context& c, int32_t key) {
+  if (key == 0) return 0;
+  for (size_t i = 1; i < c.model_keys.size(); i++)
+    if (c.model_keys[i] == key) return (int)i;
+  if (c.model_keys.size() >= 256) return fail(KE_ERR_UNSUPPORTED, "more than 255 GPU template model keys");
+  c.model_keys.push_back(key);
+  return (int)c.model_keys.size() - 1;
+}
+
+bool selector_matches(const ke_label_selector& sel, const std::vector<std::pair<int32_t, int32_t>>& labels) {
+  for (int r = 0; r < sel.n && r < KE_MAX_SEL_REQS; r++) {  // apimachinery labels.Requirement.Matches
+    const ke_label_requirement& q = sel.req[r];
+    const auto it = std::find_if(labels.begin(), labels.end(), [&](const auto& kv) { return kv.first == q.key; });
+    const bool has = it != labels.end();
+    bool listed = false;
+    for (int v = 0; v < q.n_values && v < KE_MAX_SEL_VALUES; v++) listed = listed || (has && q.values[v] == it->second);
+    bool ok;
+    switch (q.op) {
+      case KE_SEL_IN: ok = has && listed; break;
+      case KE_SEL_NOT_IN: ok = !has || !listed; break;
+      case KE_SEL_EXISTS: ok = has; break;
+      default: ok = !has; break;
+    }
+    if (!ok) return false;
+  }
+  return true;
+}
+
+// DeviceJointAllocate.DeviceTypes as parsePodDeviceShareExtensions keeps them (utils.go:430-442): the requested
+// types without an ApplyForAll hint, in annotation order
+static int joint_list(const ke_pod_device_hints& h, const ke_pod& p, int* out) {
+  bool req[KE_DEV_TYPES] = {false, p.device_requests[KE_PDR_RDMA] > 0, p.device_requests[KE_PDR_FPGA] > 0};
+  for (int i = 0; i < KE_PDR_RDMA; i++) req[KE_DEV_GPU] = req[KE_DEV_GPU] || p.device_requests[i] > 0;
+  int n = 0;
+  for (int j = 0; j < h.joint_n && j < KE_DEV_TYPES; j++) {
+    const int t = h.joint_types[j];
+    if (t < 0 || t >= KE_DEV_TYPES || !req[t] || h.hint[t].strategy == KE_DSTRATEGY_APPLY_FOR_ALL) continue;
+    bool dup = false;
+    for (int q = 0; q < n; q++) dup = dup || out[q] == t;
+    if (!dup) out[n++] = t;
+  }
+  return n;
+}
+
+const ke_pod_device_hints* pod_hints(const Context& c, const ke_pod& p) {
+  return p.device_hint > 0 && p.device_hint <= (int32_t)c.hints.size() ? &c.hints[(size_t)p.device_hint - 1] : nullptr;
+}
+
+int validate_pod_hints(const Context& c, const ke_pod& p) {
+  if (p.device_hint < 0 || p.device_hint > (int32_t)c.hints.size())
+    return fail(KE_ERR_INVALID, "ke_pod.device_hint outside the ke_set_pod_device_hints table");
+  const ke_pod_device_hints* h = pod_hints(c, p);
+  if (!h) return KE_OK;
+  if (h->hint[KE_DEV_GPU].vf_selector.present)  // generalAllocate's defaultAllocateDevices with GPU VFs
+    return fail(KE_ERR_UNSUPPORTED, "a VFSelector on the gpu device type is not implemented");
+  if (h->joint_n < 0 || h->joint_n > KE_DEV_TYPES) return fail(KE_ERR_INVALID, "joint_n");
+  for (int j = 0; j < h->joint_n; j++)
+    if (h->joint_types[j] < 0 || h->joint_types[j] >= KE_DEV_TYPES) return fail(KE_ERR_INVALID, "joint device type");
+  int jl[KE_DEV_TYPES];
+  const int jn = joint_list(*h, p, jl);
+  for (int j = 1; j < jn; j++)
+    if (jl[j] == KE_DEV_GPU)  // GPUAllocator with a preferred PCIe set / maxDesiredCount
+      return fail(KE_ERR_UNSUPPORTED, "DeviceJointAllocate with the gpu type after the primary is not implemented");
+  if (jn == 3)  // a secondary type outside requestsPerInstance allocates a nil request
+    return fail(KE_ERR_UNSUPPORTED, "DeviceJointAllocate over three device types is not implemented");
+  for (int t = 0; t < KE_DEV_TYPES; t++)
+    for (const ke_label_selector* sel : {&h->hint[t].selector, &h->hint[t].vf_selector})
+      if (sel->n < 0 || sel->n > KE_MAX_SEL_REQS) return fail(KE_ERR_INVALID, "selector requirement count");
+  return KE_OK;
+}
+
+static void set256(uint64_t (&b)[4], int x) { b[x >> 6] |= 1ull << (x & 63); }
+
+DevPodHint make_pod_hint(const Context& c, const ke_pod& pod, const DevPod& dp, const ke_pod_device_hints& h) {
+  DevPodHint r{};
+  r.ring_bw = (dp.flags & PF_GPU_RING_BW) ? pod.gpu_ring_bus_bandwidth : KE_ABSENT;
+  if (h.has_selectors) r.flags |= PH_FILTER;
+  for (int t = 0; t < KE_DEV_TYPES; t++) {
+    const ke_device_hint& dh = h.hint[t];
+    for (int w = 0; w < 4; w++) r.sel[t][w] = ~0ull;
+    if (dh.selector.present) {
+      r.flags |= PH_SEL0 << t;
+      for (int w = 0; w < 4; w++) r.sel[t][w] = 0;
+      for (size_t id = 0; id < c.label_sets.size(); id++)
+        if (selector_matches(dh.selector, c.label_sets[id])) set256(r.sel[t], (int)id);
+    }
+    if (dh.vf_selector.present) {
+      r.flags |= PH_VF0 << t;
+      for (size_t id = 0; id < c.label_sets.size(); id++)
+        if (selector_matches(dh.vf_selector, c.label_sets[id])) set256(r.vfsel[t], (int)id);
+    }
+  }
+  int jl[KE_DEV_TYPES];
+  const int jn = joint_list(h, pod, jl);
+  r.joint_n = (uint8_t)jn;
+  for (int j = 0; j < KE_DEV_TYPES; j++) r.joint[j] = (int8_t)(j < jn ? jl[j] : -1);
+  if (h.joint_same_pcie) r.flags |= PH_JOINT_PCIE;
+  if (dp.ds_cnt[KE_DEV_GPU] && !(dp.flags & PF_GPU_SHARED)) r.flags |= PH_FITS_WELL_PLANNED;
+  // enforceGPUSharedResourceTemplate: candidates per model key (gpu_shared_resource_templates_cache.go:41-62)
+  const uint32_t keys = c.cfg.deviceshare.template_matched_keys;
+  uint32_t named = 0;
+  if (dp.flags & PF_DS_H_CORE) named |= KE_TEMPLATE_KEY_CORE;
+  if (dp.flags & PF_DS_H_RATIO) named |= KE_TEMPLATE_KEY_MEMORY_RATIO;
+  else if (dp.flags & PF_DS_H_MEM) named |= KE_TEMPLATE_KEY_MEMORY;
+  if (dp.ds_cnt[KE_DEV_GPU] && (dp.flags & PF_GPU_SHARED) && (named & keys)) {
+    r.flags |= PH_TMPL;
+    for (size_t id = 1; id < c.model_keys.size(); id++) {
+      int n = 0;
+      for (const ke_gpu_template& t : c.tmpl)
+        if (t.model_key == c.model_keys[id] && t.has[0] == ((named & KE_TEMPLATE_KEY_CORE) != 0) &&
+            t.has[1] == ((named & KE_TEMPLATE_KEY_MEMORY) != 0) && t.has[2] == ((named & KE_TEMPLATE_KEY_MEMORY_RATIO) != 0) &&
+            (!t.has[0] || t.value[0] == dp.ds_req[0]) && (!t.has[1] || t.value[1] == dp.ds_req[1]) &&
+            (!t.has[2] || t.value[2] == dp.ds_req[2]))
+          n++;
+      if (n == 1) set256(r.tmpl1, (int)id);
+      if (n >= 2) set256(r.tmplm, (int)id);
+    }
+  }
+  return r;
+}
+
+void derive_dsx_row(const NodeState& ns, int64_t* w) {
+  for (int i = 0; i < NUM_DSX; i++) w[i] = 0;
+  for (int i = DSX_PCIE; i < DSX_PCIE + 6; i++) w[i] = -1;  // 0xFF: no topology
+  uint64_t node = ns.secondary_well_planned ? 1u : 0u;
+  node |= (uint64_t)(ns.gpu_model_id & 0xFF) << 8;
+  for (size_t x = 0; x < ns.devs.size(); x++) {
+    const ke_device& d = ns.devs[x];
+    const int t = d.type, m = d.minor, sh = 8 * (m & 7);
+    const uint64_t lbl = x * 5 < ns.dev_lbl.size() ? ns.dev_lbl[x * 5] : 0;
+    w[DSX_LBL + 2 * t + (m >> 3)] |= (int64_t)(lbl << sh);
+    if (d.has_topology)
+      w[DSX_PCIE + 2 * t + (m >> 3)] &= (int64_t)~((uint64_t)(0xFFu & ~(uint32_t)d.pcie_rank) << sh);
+    if (t == KE_DEV_GPU || d.n_vf_groups <= 0) continue;
+    node |= 1ull << t;  // hasVirtualFunctions
+    const int dv = 16 * (t - 1) + m;
+    uint64_t all = 0;
+    for (int g = 0; g < d.n_vf_groups && g < KE_MAX_VF_GROUPS; g++) {
+      w[DSX_VFG + 4 * dv + g] = (int64_t)d.vf_groups[g].vfs;
+      all |= d.vf_groups[g].vfs;
+      const uint64_t gl = x * 5 + 1 + (size_t)g < ns.dev_lbl.size() ? ns.dev_lbl[x * 5 + 1 + (size_t)g] : 0;
+      w[DSX_VFL + (dv >> 1)] |= (int64_t)(gl << (32 * (dv & 1) + 8 * g));
+    }
+    w[DSX_VFFREE + dv] = (int64_t)(all & ~d.vf_allocated);
+  }
+  w[DSX_NODE] = (int64_t)node;
 }
 
 // GetGPUTopologyScope (allocator_gpu_helper.go:202-263) as per-minor scope ranks: NUMA scopes ascending by
@@ -222,11 +407,13 @@ int ptable_intern(Context& c, int32_t n, const ke_gpu_partition* parts) {
   return (int)n_tab;
 }
 
-void host_ds_reserve(const ke_config& cfg, NodeState& ns, const DevPod& dp, uint64_t mask) {
+void host_ds_reserve(const ke_config& cfg, NodeState& ns, const DevPod& dp, uint64_t mask, const int8_t* vf) {
   (void)cfg;
   for (ke_device& d : ns.devs) {
     if (!(mask & (1ull << (16 * d.type + d.minor)))) continue;
     const int t = d.type;
+    if (vf && t > 0 && vf[(t - 1) * KE_MAX_MINORS + d.minor] >= 0)  // updateVFAllocations
+      d.vf_allocated |= 1ull << vf[(t - 1) * KE_MAX_MINORS + d.minor];
     int64_t alloc[KE_DKEYS] = {0, 0, 0};
     bool has[KE_DKEYS] = {false, false, false};
     if (t == KE_DEV_GPU) {
@@ -268,16 +455,8 @@ int validate_pod(const ke_pod& p) {
     return fail(KE_ERR_INVALID, "pod NUMA exclusive policy");
   if (p.gpu_required_topology_scope < KE_SCOPE_NONE || p.gpu_required_topology_scope > KE_SCOPE_UNKNOWN)
     return fail(KE_ERR_INVALID, "pod GPU required topology scope");
-  if (p.device_joint_allocate)  // tryJointAllocate / validateJointAllocation (device_allocator.go:205-300)
-    return fail(KE_ERR_UNSUPPORTED, "DeviceJointAllocate annotation (joint GPU/RDMA allocation) is not implemented");
-  if (p.device_hints & KE_DHINT_VF)  // mustAllocateVF -> allocateVF (device_allocator.go:87-92,396-460)
-    return fail(KE_ERR_UNSUPPORTED, "DeviceHint VFSelector (virtual function allocation) is not implemented");
-  if (p.device_hints & KE_DHINT_SELECTOR)  // filterNodeDevice by device labels (device_allocator.go:137-166)
-    return fail(KE_ERR_UNSUPPORTED, "DeviceHint Selector is not implemented");
-  if (p.device_hints & KE_DHINT_STRATEGY)  // ApplyForAll / RequestsAsCount (devicehandler_default.go:58-90)
-    return fail(KE_ERR_UNSUPPORTED, "DeviceHint AllocateStrategy is not implemented");
-  if (p.device_hints & KE_DHINT_EXCLUSIVE)  // filterFreeDevicesByPCIe (device_cache.go:372-376,417-440)
-    return fail(KE_ERR_UNSUPPORTED, "DeviceHint ExclusivePolicy is not implemented");
+  if (p.device_hints & KE_DHINT_GPU_VF)  // generalAllocate's defaultAllocateDevices with GPU VFs
+    return fail(KE_ERR_UNSUPPORTED, "a VFSelector on the gpu device type is not implemented");
   if (p.device_hints) return fail(KE_ERR_INVALID, "unknown device hint bits");
   if (p.n_xres < 0 || p.n_xres > KE_MAX_POD_XRES) return fail(KE_ERR_INVALID, "pod n_xres out of range (0..8)");
   for (int e = 0; e < p.n_xres; e++) {
@@ -394,7 +573,7 @@ void estimate_pod(const ke_loadaware_args& a, const ke_pod& pod, int64_t* est, u
 // (devicehandler_default.go:44-93, no hint).  Returns false when the request is invalid.
 static bool percentage_ok(int64_t q) { return !(q > 100 && q % 100 != 0); }  // ValidatePercentageResource
 
-static bool ds_prepare(const ke_pod& pod, DevPod& d) {
+static bool ds_prepare(const ke_pod& pod, DevPod& d, const ke_pod_device_hints* h) {
   const int64_t* q = pod.device_requests;
   bool nv = q[KE_PDR_NVIDIA_GPU] > 0, amd = q[KE_PDR_AMD_GPU] > 0, kg = q[KE_PDR_KOORD_GPU] > 0;
   bool sh = q[KE_PDR_GPU_SHARED] > 0, co = q[KE_PDR_GPU_CORE] > 0, me = q[KE_PDR_GPU_MEMORY] > 0,
@@ -451,9 +630,15 @@ static bool ds_prepare(const ke_pod& pod, DevPod& d) {
     if (v <= 0) continue;
     if (!percentage_ok(v)) return false;
     int64_t c = 1, per = v;
+    const ke_device_hint* ht = h ? &h->hint[1 + i] : nullptr;  // DefaultDeviceHandler (devicehandler_default.go:53-91)
     if (v > 100 && v % 100 == 0) {
       c = v / 100;
       per = v / c;
+    } else if (ht && ht->strategy == KE_DSTRATEGY_APPLY_FOR_ALL) {
+      c = DS_CNT_ALL;  // the node's devices (matching the Selector): decided per node
+    } else if (ht && ht->strategy == KE_DSTRATEGY_REQUESTS_AS_COUNT) {
+      c = v < DS_CNT_ALL ? v : DS_CNT_ALL - 1;  // more than KE_MAX_MINORS never fits: the cap keeps that
+      per = ht->exclusive == KE_DEXCL_DEVICE_LEVEL ? 100 : 1;
     }
     if (c > 255) return false;
     d.ds_cnt[1 + i] = (uint8_t)c;
@@ -462,7 +647,8 @@ static bool ds_prepare(const ke_pod& pod, DevPod& d) {
   return true;
 }
 
-DevPod make_dev_pod(const ke_config& cfg, const ke_pod& pod) {
+DevPod make_dev_pod(const ke_config& cfg, const ke_pod& pod, const ke_pod_device_hints* hints,
+                    const std::vector<ke_gpu_template>* tmpl) {
   DevPod d{};
   d.quota = (uint8_t)pod.quota;  // range-checked against the loaded tree by ke_schedule
   uint8_t present[KE_NRES];
@@ -506,12 +692,34 @@ DevPod make_dev_pod(const ke_config& cfg, const ke_pod& pod) {
     }
   }
   d.flags = f;
-  if (!ds_prepare(pod, d)) {
+  int invalid = 0;  // the PreFilter failure's reason (PF_DS_INVALID; DevPod::ds_req[0] carries it)
+  if (!ds_prepare(pod, d, hints)) invalid = KE_REASON_DS_INVALID_REQUEST;
+  const bool requests = d.ds_cnt[0] || d.ds_cnt[1] || d.ds_cnt[2];
+  if (!invalid && requests && hints) {
+    if (hints->invalid) invalid = KE_REASON_DS_INVALID_HINT;  // newHintSelectors (utils.go:420-423)
+    // parseGPURequirements: no template of any GPU model equal to the request (utils.go:508-515)
+    const uint32_t keys = cfg.deviceshare.template_matched_keys;
+    uint32_t named = 0;
+    if (d.flags & PF_DS_H_CORE) named |= KE_TEMPLATE_KEY_CORE;
+    if (d.flags & PF_DS_H_RATIO) named |= KE_TEMPLATE_KEY_MEMORY_RATIO;
+    else if (d.flags & PF_DS_H_MEM) named |= KE_TEMPLATE_KEY_MEMORY;
+    if (!invalid && d.ds_cnt[KE_DEV_GPU] && (d.flags & PF_GPU_SHARED) && (named & keys)) {
+      bool any = false;
+      for (const ke_gpu_template& t : tmpl ? *tmpl : std::vector<ke_gpu_template>{})
+        any = any || (t.has[0] == ((named & KE_TEMPLATE_KEY_CORE) != 0) && t.has[1] == ((named & KE_TEMPLATE_KEY_MEMORY) != 0) &&
+                      t.has[2] == ((named & KE_TEMPLATE_KEY_MEMORY_RATIO) != 0) && (!t.has[0] || t.value[0] == d.ds_req[0]) &&
+                      (!t.has[1] || t.value[1] == d.ds_req[1]) && (!t.has[2] || t.value[2] == d.ds_req[2]));
+      if (!any) invalid = KE_REASON_DS_NO_MATCHED_TEMPLATE;
+    }
+  }
+  if (invalid) {
     for (int t = 0; t < 3; t++) d.ds_cnt[t] = 0;
     for (int i = 0; i < 5; i++) d.ds_req[i] = 0;
+    d.ds_req[0] = invalid;
     d.flags = f | PF_DS_INVALID;
-  } else if (d.ds_cnt[0] || d.ds_cnt[1] || d.ds_cnt[2]) {
+  } else if (requests) {
     d.flags |= PF_DS;
+    if (hints) d.flags |= PF_DS_HINT;  // DevPod::ring_bw becomes the hint slot at upload
   }
   if (pod.quota_non_preemptible) d.flags |= PF_QUOTA_NP;
   // NodeResourcesFitPlus / ScarceResourceAvoidance PreScore: requested names and the FitPlus requests by slot
@@ -981,7 +1189,8 @@ void host_cpuset_reserve(NodeState& ns, const DevPod& dp, const uint64_t* set) {
   ns.dirty = true;
 }
 
-void host_release_node(const ke_config& cfg, bool ext, NodeState& ns, const ke_pod& pod, const ke_pod_allocation& a) {
+void host_release_node(const ke_config& cfg, bool ext, NodeState& ns, const ke_pod& pod, const ke_pod_allocation& a,
+                       const ke_pod_device_hints* h) {
   // LoadAware podAssignCache.unAssign (pod_assign_cache.go:126-136)
   for (size_t i = 0; i < ns.asg.size(); i++)
     if (ns.asg[i].pod.uid == pod.uid) {
@@ -1023,9 +1232,11 @@ void host_release_node(const ke_config& cfg, bool ext, NodeState& ns, const ke_p
   }
   // DeviceShare updateCacheUsed(allocation, pod, false) -> updateDeviceUsed (device_cache.go:184-209)
   if (ns.has_dev_cache && a.device_minors) {
-    const DevPod dp = make_dev_pod(cfg, pod);
+    const DevPod dp = make_dev_pod(cfg, pod, h);
     for (ke_device& d : ns.devs) {
       if (!(a.device_minors & (1ull << (16 * d.type + d.minor)))) continue;
+      if (d.type > 0 && a.vf_rank[d.type - 1][d.minor] >= 0)  // removeVFAllocations (device_cache.go:283-300)
+        d.vf_allocated &= ~(1ull << a.vf_rank[d.type - 1][d.minor]);
       const int t = d.type;
       int64_t alloc[KE_DKEYS] = {0, 0, 0};
       bool has[KE_DKEYS] = {false, false, false};

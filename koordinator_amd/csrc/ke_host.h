@@ -2,7 +2,9 @@
 // its listers, podAssignCache and NodeInfo snapshot) and its folding into GPU rows.
 #pragma once
 #include <cstdint>
+#include <map>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/koord_eval.h"
@@ -39,6 +41,11 @@ struct NodeState {
   // GPU partition indexer / policy (ke_node_gpu_partitions): table id in Context::ptab, -1 = nil indexer
   int32_t ptable = -1;
   bool gpu_honor = false;
+  // DeviceShare hints: interned label-set ids per device (5 per device: its labels, then its 4 VF groups'),
+  // the Device's secondary-well-planned label and the node's GPU template model key id (0 = none)
+  std::vector<uint8_t> dev_lbl;
+  bool secondary_well_planned = false;
+  int32_t gpu_model_id = 0;
   // NodeResourcesFitPlus / ScarceResourceAvoidance: NodeInfo Allocatable / (NonZero)Requested by resource id
   std::vector<ke_node_resource> xres;
   // derived
@@ -105,7 +112,28 @@ struct Context {
   // GPU partition tables, deduplicated: PT_WORDS words per table (ke_types.h), uploaded when ptab_dirty
   std::vector<uint64_t> ptab;
   bool ptab_dirty = false;
+  // DeviceShare hints (ke_set_pod_device_hints), GPU shared resource templates (ke_gpu_templates_load), the
+  // interned device / VF-group label sets (id -> sorted (key, value) pairs; id 0 = no labels) and template
+  // model keys (id -> ke_label_id of "<vendor>-<model>", id 0 = none); the VF ranks of the last ke_schedule
+  std::vector<ke_pod_device_hints> hints;
+  std::vector<ke_gpu_template> tmpl;
+  std::vector<std::vector<std::pair<int32_t, int32_t>>> label_sets{{}};
+  std::map<std::vector<std::pair<int32_t, int32_t>>, int> label_set_ids{{{}, 0}};
+  std::vector<int32_t> model_keys{0};
+  std::vector<int8_t> last_vf;  // [pod][2][KE_MAX_MINORS]
 };
+
+// the hint record of a pod (nullptr: none); the index was validated by validate_pod_hints
+const ke_pod_device_hints* pod_hints(const Context& c, const ke_pod& p);
+int validate_pod_hints(const Context& c, const ke_pod& p);
+// intern the label sets of a node's devices into ns.dev_lbl (KE_ERR_UNSUPPORTED beyond 256 distinct sets)
+int intern_device_labels(Context& c, NodeState& ns);
+int intern_model_key(Context& c, int32_t key);  // id 1..255, or a negative KE_ERR_*
+// labels.Selector.Matches of a converted LabelSelector against an interned label set
+bool selector_matches(const ke_label_selector& sel, const std::vector<std::pair<int32_t, int32_t>>& labels);
+// the device-side record of a hinted pod: the Selector / VFSelector / template candidate sets over the
+// current interned ids, flags and the joint types
+DevPodHint make_pod_hint(const Context& c, const ke_pod& pod, const DevPod& dp, const ke_pod_device_hints& h);
 
 // Encode a node's partition table (validated) into the pool; returns its id or a negative KE_ERR_*.
 int ptable_intern(Context& c, int32_t n, const ke_gpu_partition* parts);
@@ -126,7 +154,8 @@ int validate_pod(const ke_pod& p);
 // DefaultEstimator.EstimatePod (estimator/default_estimator.go:59-122)
 void estimate_pod(const ke_loadaware_args& a, const ke_pod& pod, int64_t* est, uint8_t* present);
 // pod -> device parameters
-DevPod make_dev_pod(const ke_config& cfg, const ke_pod& pod);
+DevPod make_dev_pod(const ke_config& cfg, const ke_pod& pod, const ke_pod_device_hints* hints = nullptr,
+                    const std::vector<ke_gpu_template>* tmpl = nullptr);
 
 // Fold a node's object state into its row for evaluation at `now` (valid until *valid_until).
 void derive_row(const ke_config& cfg, const NodeState& ns, int64_t now, Row* row, int64_t* valid_until);
@@ -145,9 +174,11 @@ void flush_mirror(Context& c);
 int validate_devices(int32_t n, const ke_device* devs);
 // the device SoA row of a node: NUM_DS_FIELDS int64 + NUM_DS_MASKS uint64 (zero when no cache entry)
 void derive_ds_row(const NodeState& ns, int64_t* f, uint64_t* masks);
+// its NUM_DSX hint words (DSX_*: label-set ids, PCIe ranks, node flags, VF state)
+void derive_dsx_row(const NodeState& ns, int64_t* w);
 // host mirror of DeviceShare Reserve: add the allocation of `pod` on the minors in `mask`
 // (bit 16*type+minor) to the node's device cache (fillGPUTotalMem + updateCacheUsed)
-void host_ds_reserve(const ke_config& cfg, NodeState& ns, const DevPod& dp, uint64_t mask);
+void host_ds_reserve(const ke_config& cfg, NodeState& ns, const DevPod& dp, uint64_t mask, const int8_t* vf = nullptr);
 
 // NUMA topology
 int validate_zones(int32_t n, const ke_numa_zone* zones);
@@ -178,7 +209,8 @@ void host_cpuset_reserve(NodeState& ns, const DevPod& dp, const uint64_t* set);
 
 // Release of one placement from its node (ke_pod_release): podAssignCache.unAssign, NodeInfo.RemovePod
 // (Requested, the FitPlus requested when `ext`), resourceManager.Release, DeviceShare updateCacheUsed(false)
-void host_release_node(const ke_config& cfg, bool ext, NodeState& ns, const ke_pod& pod, const ke_pod_allocation& a);
+void host_release_node(const ke_config& cfg, bool ext, NodeState& ns, const ke_pod& pod, const ke_pod_allocation& a,
+                       const ke_pod_device_hints* h = nullptr);
 // ElasticQuota UnreservePod (assigned) / OnPodDelete (del) on the host tree (used already synced from the
 // device); recomputes the runtime limits when the tree total or a request moved
 int host_quota_release(Context& c, const ke_pod& pod, bool assigned, bool del);

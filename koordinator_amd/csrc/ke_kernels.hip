@@ -72,6 +72,12 @@ struct SoA {
   // word (DSB_CUT: the first pod it left unplaced, -1 = none)
   uint32_t* dsb;
   uint16_t* dsraw;  // DeviceShare batch: per pod, 1 + each node's raw score in the batch's snapshot (0 = infeasible)
+  // DeviceShare hints: per node NUM_DSX words (DSX_*, field-major, allocated with the device
+  // SoA), the hinted pods' records of the current call (DevPod::ring_bw = slot), and per pod of the call the VF
+  // ranks its Reserve took ([pod][type - 1][minor], -1 = none)
+  int64_t* dsx;
+  const DevPodHint* ph;
+  int8_t* vfo;
 };
 constexpr int DSB_MAX = 0, DSB_CNT = 64, DSB_CUT = 128, DSB_WORDS = 129;
 // kerr bits: an input the kernels refuse mid-call (the call returns KE_ERR_UNSUPPORTED)
@@ -606,12 +612,16 @@ __device__ __forceinline__ uint32_t default_pick(uint32_t ok, int want, const in
 // (0 = allocated); with `select` *minors = the chosen minors (dscore: scoreDevice per minor, nullptr = no
 // scorer), else only feasibility is decided.
 __device__ int gpu_allocate(const SoA& s, int64_t i, uint64_t ex0, const DevPod& p, const GpuMasks& g, bool select,
-                            const int64_t* dscore, uint32_t* minors, int* reason) {
+                            const int64_t* dscore, uint32_t* minors, int* reason, int tmode = 0) {
   const int want = p.ds_cnt[KE_DEV_GPU];
   const bool shared = p.flags & PF_GPU_SHARED;
   const bool honor = (p.flags & PF_GPU_PART_SPEC) || (ex0 & DSX_HONOR);
   *minors = 0;
-  if (!shared) {  // allocateByPartition
+  if (tmode == 2) {  // allocateByTemplate: no candidate template of the node's GPU model (allocator_gpu.go:141-143)
+    *reason = KE_REASON_DS_NO_MATCHED_TEMPLATE;
+    return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+  }
+  if (!shared && tmode == 0) {  // allocateByPartition (one candidate template: generalAllocate only, :144-154)
     int why = 0;
     const uint32_t pm = gpu_partition(s, ex0, p, want, g, select, &why);
     if (pm) {
@@ -671,10 +681,10 @@ __device__ __forceinline__ uint32_t ds_allowed(const SoA& s, int64_t i, int t, D
 // total, the refined used' inside).
 __device__ __forceinline__ bool ds_type_view(const SoA& s, int64_t i, int t, const uint64_t msk[4], const DevPod& p,
                                              const KArgs& k, DsAff a, GpuMasks& g, int64_t (&tot)[3],
-                                             int64_t (&fre)[3], int64_t* score) {
+                                             int64_t (&fre)[3], int64_t* score, uint32_t sel = 0xFFFFu) {
   const int nk = DS_NK[t];
   uint64_t ex = (msk[DSM_EXISTS] >> (16 * t)) & 0xFFFF;
-  const uint32_t allowed = (uint32_t)ex & ds_allowed(s, i, t, a);
+  const uint32_t allowed = (uint32_t)ex & ds_allowed(s, i, t, a) & sel;  // sel: a hint Selector's devices
   g.minors = (uint32_t)ex;
   g.total = g.used = g.sat = g.dflt = 0;
   uint32_t orig_used = 0, used_p = 0, tot_m = 0, sat = 0, dflt = 0;
@@ -734,11 +744,23 @@ __device__ __forceinline__ bool ds_type_view(const SoA& s, int64_t i, int t, con
   return present;
 }
 
+__device__ int hint_allocate(const SoA& s, int64_t i, const DevPod& p0, const KArgs& k, DsAff a, bool reserve,
+                             bool scored, uint32_t* out, int8_t (*vf)[DS_MINORS], int* reason);
+__device__ bool hint_score(const SoA& s, int64_t i, const DevPod& p0, const KArgs& k, DsAff a, int64_t* raw);
+__device__ __forceinline__ uint64_t dsxw(const SoA& s, int w, int64_t i);
+
 // AutopilotAllocator.Allocate (device_allocator.go:87-135) on the devices the affinity leaves: Prepare (a
 // requested type without devices in the cache), then every requested type in the fixed order GPU, RDMA,
 // FPGA.  *gpu = the GPU minors (no scorer) when `gpu` is given.
 __device__ int ds_try_allocate(const SoA& s, int64_t i, const DevPod& p, const KArgs& k, DsAff a, uint32_t* gpu,
                                int* reason) {
+  if (p.flags & PF_DS_HINT) {  // Filter's trial allocation (no scorer, Prepare outside Reserve)
+    uint32_t out[3];
+    int8_t vf[2][DS_MINORS];
+    const int st = hint_allocate(s, i, p, k, a, false, false, out, vf, reason);
+    if (gpu) *gpu = st ? 0u : out[KE_DEV_GPU];
+    return st;
+  }
   uint64_t msk[4];
 #pragma unroll
   for (int w = 0; w < 4; w++) msk[w] = dsmask(s, w, i);
@@ -776,6 +798,21 @@ __device__ int ds_try_allocate(const SoA& s, int64_t i, const DevPod& p, const K
 // Filter then passes: topology_hint.go Allocate already ran).  Types in the fixed order GPU, RDMA, FPGA.
 __device__ __forceinline__ void ds_filter_score(const SoA& s, int64_t i, const DevPod& p, const KArgs& k, EvalOut& o,
                                              bool stored, DsAff a) {
+  if (p.flags & PF_DS_HINT) {
+    if (!stored) {
+      int why = 0;
+      const int st = ds_try_allocate(s, i, p, k, DsAff{false, 0u}, nullptr, &why);
+      if (st) {
+        o.status = (uint8_t)st;
+        o.reason = (uint8_t)why;
+        return;
+      }
+    }
+    int64_t raw = 0;
+    hint_score(s, i, p, k, a, &raw);
+    o.ds = (int16_t)raw;
+    return;
+  }
   uint64_t msk[4];
 #pragma unroll
   for (int w = 0; w < 4; w++) msk[w] = dsmask(s, w, i);
@@ -822,23 +859,46 @@ __device__ __forceinline__ void ds_filter_score(const SoA& s, int64_t i, const D
 // defaultAllocateDevices -- with the plugin's scorer.  The allocation (request + fillGPUTotalMem,
 // devicehandler_gpu.go:98-133) is added to `used` in the SoA (updateCacheUsed).  Returns the minors mask
 // (bit 16*type + minor).
-__device__ __noinline__ uint64_t ds_reserve(const SoA& s, int64_t i, const DevPod& p, const KArgs& k, DsAff a) {
+__device__ __noinline__ uint64_t ds_reserve(const SoA& s, int64_t i, const DevPod& p, const KArgs& k, DsAff a,
+                                            int8_t* vf_out = nullptr) {
   uint64_t msk[4], out = 0;
 #pragma unroll
   for (int w = 0; w < 4; w++) msk[w] = dsmask(s, w, i);
+  uint32_t hout[3] = {0, 0, 0};
+  int8_t hvf[2][DS_MINORS];
+  const bool hinted = (p.flags & PF_DS_HINT) != 0;
+  if (hinted) {  // the hinted allocation with the scorer in the Reserve phase (feasibility checked by the caller)
+    for (int t = 0; t < 2; t++)
+      for (int m = 0; m < DS_MINORS; m++) hvf[t][m] = -1;
+    int why = 0;
+    if (hint_allocate(s, i, p, k, a, true, true, hout, hvf, &why)) hout[0] = hout[1] = hout[2] = 0;
+    if (vf_out)
+      for (int t = 0; t < 2; t++)
+        for (int m = 0; m < DS_MINORS; m++) vf_out[t * DS_MINORS + m] = ((hout[t + 1] >> m) & 1u) ? hvf[t][m] : (int8_t)-1;
+  }
   for (int t = 0; t < 3; t++) {
     if (!p.ds_cnt[t]) continue;
     const int nk = DS_NK[t];
-    int64_t score[DS_MINORS];
-    GpuMasks g;
-    int64_t tot[3], fre[3];
-    ds_type_view(s, i, t, msk, p, k, a, g, tot, fre, score);
     uint32_t take = 0;
-    if (t == KE_DEV_GPU) {
-      int reason = 0;
-      if (gpu_allocate(s, i, msk[DSM_EXISTS], p, g, true, score, &take, &reason) != 0) take = 0;  // passed Filter
+    if (hinted) {
+      take = hout[t];
+      for (uint32_t rest = take; t > 0 && rest; rest &= rest - 1) {  // updateVFAllocations: the VF is held
+        const int m = __builtin_ctz(rest);
+        if (hvf[t - 1][m] < 0) continue;
+        const int w = DSX_VFFREE + 16 * (t - 1) + m;
+        s.dsx[w * s.stride + i] = (int64_t)(dsxw(s, w, i) & ~(1ull << hvf[t - 1][m]));
+      }
     } else {
-      take = default_pick(g.dflt, p.ds_cnt[t], score);
+      int64_t score[DS_MINORS];
+      GpuMasks g;
+      int64_t tot[3], fre[3];
+      ds_type_view(s, i, t, msk, p, k, a, g, tot, fre, score);
+      if (t == KE_DEV_GPU) {
+        int reason = 0;
+        if (gpu_allocate(s, i, msk[DSM_EXISTS], p, g, true, score, &take, &reason) != 0) take = 0;  // passed Filter
+      } else {
+        take = default_pick(g.dflt, p.ds_cnt[t], score);
+      }
     }
     for (uint32_t rest = take; rest; rest &= rest - 1) {
       const int best = __builtin_ctz(rest);
@@ -872,6 +932,220 @@ __device__ __noinline__ uint64_t ds_reserve(const SoA& s, int64_t i, const DevPo
 #pragma unroll
   for (int w = 1; w < 4; w++) s.dsm[w * s.stride + i] = msk[w];
   return out;
+}
+
+// ---- DeviceShare hints (deviceshare/utils.go:414-482, device_allocator.go:74-455) --------------
+// Pods with DeviceAllocateHints / DeviceJointAllocate (PF_DS_HINT) are singleton batches; their DeviceShare
+// Filter / Score / Reserve / NUMA hints run these functions on one lane.  The node's label-set ids, PCIe ranks,
+// VF state and template model key live in the DSX SoA; the pod's Selector / VFSelector / template candidates
+// are 256-bit sets over the context's interned ids (the host evaluates the selectors once per call).
+__device__ __forceinline__ uint64_t dsxw(const SoA& s, int w, int64_t i) { return (uint64_t)s.dsx[w * s.stride + i]; }
+__device__ __forceinline__ bool in256(const uint64_t* b, uint32_t x) { return (b[x >> 6] >> (x & 63u)) & 1u; }
+__device__ __forceinline__ uint32_t dsx_byte(const SoA& s, int base, int64_t i, int t, int m) {
+  return (uint32_t)(dsxw(s, base + 2 * t + (m >> 3), i) >> (8 * (m & 7))) & 0xFFu;
+}
+// filterNodeDevice's Selector (device_allocator.go:150-161): minors of type t whose labels it matches
+__device__ uint32_t hint_sel_minors(const SoA& s, int64_t i, const DevPodHint& h, int t) {
+  if (!(h.flags & (PH_SEL0 << t))) return 0xFFFFu;
+  uint32_t m = 0;
+  for (int q = 0; q < DS_MINORS; q++) m |= (uint32_t)in256(h.sel[t], dsx_byte(s, DSX_LBL, i, t, q)) << q;
+  return m;
+}
+// allocateVF (device_allocator.go:426-455): the VF ranks of minor m (type 1..2) free and in a group the
+// VFSelector matches; the lowest rank is the lowest BusID
+__device__ uint64_t hint_vf_cand(const SoA& s, int64_t i, const DevPodHint& h, int t, int m) {
+  const int d = 16 * (t - 1) + m;
+  const uint64_t lw = dsxw(s, DSX_VFL + (d >> 1), i) >> (32 * (d & 1));
+  uint64_t c = 0;
+  for (int g = 0; g < KE_MAX_VF_GROUPS; g++) {
+    const uint64_t vfs = dsxw(s, DSX_VFG + 4 * d + g, i);
+    if (vfs && in256(h.vfsel[t], (uint32_t)(lw >> (8 * g)) & 0xFFu)) c |= vfs;
+  }
+  return c & dsxw(s, DSX_VFFREE + d, i);
+}
+// newPreferredPCIes (device_allocator.go:456-467): the PCIe ranks of `minors` (devices with a topology)
+__device__ uint64_t hint_pcie_set(const SoA& s, int64_t i, int t, uint32_t minors) {
+  uint64_t r = 0;
+  for (uint32_t rest = minors; rest; rest &= rest - 1) {
+    const uint32_t pr = dsx_byte(s, DSX_PCIE, i, t, __builtin_ctz(rest));
+    if (pr < 64) r |= 1ull << pr;
+  }
+  return r;
+}
+
+// AutopilotAllocator.Prepare (device_allocator.go:74-94, calcRequestsAndCountByDeviceType :171-203): the types
+// of requestsPerInstance (a joint pod's secondary types are left out outside Reserve on a node with well-planned
+// secondary devices) and their desired counts (ApplyForAll: the node's devices matching the Selector,
+// devicehandler_default.go:62-80), then mustAllocateVF's hasVirtualFunctions.  Types in the order GPU, RDMA, FPGA.
+struct DsPrep {
+  uint32_t inc;
+  int want[3];
+};
+__device__ int hint_prepare(const SoA& s, int64_t i, const DevPod& p, const DevPodHint& h, uint64_t ex0, bool reserve,
+                            DsPrep& pr, int* reason) {
+  const uint64_t node = dsxw(s, DSX_NODE, i);
+  pr.inc = 0;
+  for (int t = 0; t < 3; t++) {
+    pr.want[t] = 0;
+    if (!p.ds_cnt[t]) continue;
+    if (h.joint_n && t != h.joint[0] && (h.flags & PH_FITS_WELL_PLANNED) && (node & 1u) && !reserve) continue;
+    const uint32_t ex = (uint32_t)(ex0 >> (16 * t)) & 0xFFFFu;
+    int w = p.ds_cnt[t];
+    if (w == DS_CNT_ALL) w = __builtin_popcount(ex & hint_sel_minors(s, i, h, t));
+    if (!ex || w == 0) {
+      *reason = KE_REASON_DS_INSUFFICIENT_GPU + t;
+      return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    }
+    pr.want[t] = w;
+    pr.inc |= 1u << t;
+  }
+  for (int t = 1; t < 3; t++)
+    if (((pr.inc >> t) & 1u) && (h.flags & (PH_VF0 << t)) && !((node >> t) & 1u)) {
+      *reason = t == KE_DEV_RDMA ? KE_REASON_DS_INSUFFICIENT_RDMA_VF : KE_REASON_DS_INSUFFICIENT_FPGA_VF;
+      return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    }
+  return 0;
+}
+
+// defaultAllocateDevices (device_allocator.go:352-424) with sortDeviceResourcesByPreferredPCIe (preferred PCIe
+// first, then scoreDevice desc, minor asc) and one VF per device for a VF pod: up to max_count of `ok`.
+__device__ int hint_default_pick(const SoA& s, int64_t i, const DevPodHint& h, int t, uint32_t ok, int max_count,
+                                 uint64_t pref, const int64_t* score, uint32_t* take, int8_t* vf) {
+  int8_t rank[DS_MINORS];
+  uint32_t pf = 0;
+  for (uint32_t rest = ok; rest; rest &= rest - 1) {
+    const int m = __builtin_ctz(rest);
+    rank[m] = -1;
+    if (t > 0 && (h.flags & (PH_VF0 << t))) {
+      const uint64_t c = hint_vf_cand(s, i, h, t, m);
+      if (!c) {
+        ok &= ~(1u << m);
+        continue;
+      }
+      rank[m] = (int8_t)__builtin_ctzll(c);
+    }
+    const uint32_t pr = dsx_byte(s, DSX_PCIE, i, t, m);
+    if (pr < 64 && ((pref >> pr) & 1u)) pf |= 1u << m;
+  }
+  *take = 0;
+  int n = 0;
+  for (; n < max_count && ok; n++) {
+    int best = -1;
+    for (uint32_t rest = ok; rest; rest &= rest - 1) {
+      const int m = __builtin_ctz(rest);
+      if (best < 0) {
+        best = m;
+        continue;
+      }
+      const bool pm = (pf >> m) & 1u, pb = (pf >> best) & 1u;
+      const int64_t sm = score ? score[m] : 0, sb = score ? score[best] : 0;
+      if (pm != pb ? pm : sm > sb) best = m;  // ascending minors: ties keep the lower
+    }
+    ok &= ~(1u << best);
+    *take |= 1u << best;
+    if (vf) vf[best] = rank[best];
+  }
+  return n;
+}
+
+// AutopilotAllocator.Allocate (device_allocator.go:96-138) for a hinted pod on the devices the NUMA affinity and
+// the Selectors leave: Prepare, tryJointAllocate (:205-299: the primary type, then the secondary types preferring
+// the primary's PCIe switches, SamePCIe validated) when more than one type is requested, then the other types.
+// `scored`: the plugin's scorer (Reserve), else every score 0.  out[type] = minors, vf[type-1][minor] = VF ranks.
+__device__ __noinline__ int hint_allocate(const SoA& s, int64_t i, const DevPod& p0, const KArgs& k, DsAff a,
+                                          bool reserve, bool scored, uint32_t* out, int8_t (*vf)[DS_MINORS],
+                                          int* reason) {
+  const DevPodHint& h = s.ph[p0.ring_bw];
+  DevPod p = p0;
+  p.ring_bw = h.ring_bw;
+  uint64_t msk[4];
+  for (int w = 0; w < 4; w++) msk[w] = dsmask(s, w, i);
+  for (int t = 0; t < 3; t++) out[t] = 0;
+  DsPrep pr;
+  int st = hint_prepare(s, i, p, h, msk[DSM_EXISTS], reserve, pr, reason);
+  if (st) return st;
+  int tmode = 0;
+  if (h.flags & PH_TMPL) {
+    const uint32_t key = (uint32_t)(dsxw(s, DSX_NODE, i) >> 8) & 0xFFu;
+    tmode = in256(h.tmpl1, key) ? 1 : in256(h.tmplm, key) ? 0 : 2;
+  }
+  // allocateDevices (:320-350) of one type with its desired count and preferred PCIe ranks
+  auto alloc_type = [&](int t, int desired, uint64_t pref) -> int {
+    int max_count = desired;
+    const int np = __builtin_popcountll(pref);
+    if (np > max_count) max_count = np;
+    if (desired == 0) desired = 1;
+    if (max_count < desired) max_count = desired;
+    GpuMasks g;
+    int64_t tot[3], fre[3], score[DS_MINORS];
+    ds_type_view(s, i, t, msk, p, k, a, g, tot, fre, scored ? score : nullptr, hint_sel_minors(s, i, h, t));
+    if (t == KE_DEV_GPU) {
+      DevPod q = p;
+      q.ds_cnt[KE_DEV_GPU] = (uint8_t)desired;
+      return gpu_allocate(s, i, msk[DSM_EXISTS], q, g, true, scored ? score : nullptr, &out[t], reason, tmode);
+    }
+    const int n = hint_default_pick(s, i, h, t, g.dflt, max_count, pref, scored ? score : nullptr, &out[t], vf[t - 1]);
+    if (n < desired) {
+      out[t] = 0;
+      *reason = KE_REASON_DS_INSUFFICIENT_GPU + t;
+      return KE_CODE_UNSCHEDULABLE;
+    }
+    return 0;
+  };
+  uint32_t done = 0;
+  if (__builtin_popcount(pr.inc) > 1 && h.joint_n) {
+    const int pt = h.joint[0];
+    st = alloc_type(pt, pr.want[pt], 0);
+    if (st) return st;
+    if (!out[pt]) {
+      *reason = KE_REASON_DS_INSUFFICIENT_PRIMARY;
+      return KE_CODE_UNSCHEDULABLE;
+    }
+    done |= 1u << pt;
+    const uint64_t pcie = hint_pcie_set(s, i, pt, out[pt]);
+    const int npcie = __builtin_popcountll(pcie);
+    for (int j = 1; j < h.joint_n; j++) {
+      const int t = h.joint[j];
+      int desired = pr.want[t];
+      if ((h.flags & PH_JOINT_PCIE) && desired < npcie) desired = npcie;
+      st = alloc_type(t, desired, pcie);
+      if (st) return st;
+      if (out[t]) done |= 1u << t;
+    }
+    if (h.flags & PH_JOINT_PCIE)
+      for (int j = 1; j < h.joint_n; j++)
+        if (hint_pcie_set(s, i, h.joint[j], out[h.joint[j]]) != pcie) {  // validateJointAllocation (:223-252)
+          *reason = KE_REASON_DS_JOINT_VIOLATION;
+          return KE_CODE_UNSCHEDULABLE;
+        }
+  }
+  for (int t = 0; t < 3; t++) {
+    if (!((pr.inc >> t) & 1u) || ((done >> t) & 1u)) continue;
+    st = alloc_type(t, pr.want[t], 0);
+    if (st) return st;
+  }
+  return 0;
+}
+
+// DeviceShare Score of a hinted pod (AutopilotAllocator.score, device_allocator.go:469-492): scoreNode over the
+// types of requestsPerInstance on the Selector-filtered view; false when Prepare fails (Score 0 with an error)
+__device__ __noinline__ bool hint_score(const SoA& s, int64_t i, const DevPod& p0, const KArgs& k, DsAff a,
+                                        int64_t* raw) {
+  const DevPodHint& h = s.ph[p0.ring_bw];
+  uint64_t msk[4];
+  for (int w = 0; w < 4; w++) msk[w] = dsmask(s, w, i);
+  DsPrep pr;
+  int why = 0;
+  *raw = 0;
+  if (hint_prepare(s, i, p0, h, msk[DSM_EXISTS], false, pr, &why)) return false;
+  for (int t = 0; t < 3; t++) {
+    if (!((pr.inc >> t) & 1u)) continue;
+    GpuMasks g;
+    int64_t tot[3], fre[3];
+    if (ds_type_view(s, i, t, msk, p0, k, a, g, tot, fre, nullptr, hint_sel_minors(s, i, h, t)))
+      *raw += ds_weighted(k, t, tot, fre, p0);
+  }
+  return true;
 }
 
 // ---- DeviceShare as a NUMA topology hint provider (topology_hint.go:38-236) ----------------------------
@@ -914,7 +1188,23 @@ __device__ __noinline__ void ds_numa_hints(const SoA& s, int64_t i, const DevPod
   }
   if (!ids) return;  // an empty hint map
   const uint64_t ex = dsmask(s, DSM_EXISTS, i);
-  for (int t = 0; t < 3; t++)  // Prepare fails on every mask alike
+  // Prepare fails on every mask alike; a hinted pod's requestsPerInstance / desired counts (hint_prepare)
+  DsPrep pr;
+  pr.inc = 0;
+  for (int t = 0; t < 3; t++) {
+    pr.want[t] = p.ds_cnt[t];
+    pr.inc |= p.ds_cnt[t] ? 1u << t : 0u;
+  }
+  if (p.flags & PF_DS_HINT) {
+    int why = 0;
+    const int st = hint_prepare(s, i, p, s.ph[p.ring_bw], ex, false, pr, &why);
+    if (st) {
+      h.status = (uint8_t)st;
+      h.reason = (uint8_t)why;
+      return;
+    }
+  }
+  for (int t = 0; t < 3; t++)
     if (p.ds_cnt[t] && !((ex >> (16 * t)) & 0xFFFF)) {
       h.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
       h.reason = (uint8_t)(KE_REASON_DS_INSUFFICIENT_GPU + t);
@@ -924,14 +1214,14 @@ __device__ __noinline__ void ds_numa_hints(const SoA& s, int64_t i, const DevPod
   auto try_mask = [&](uint32_t m, uint32_t* gpu, int* why) -> int {
 #pragma unroll
     for (int t = 0; t < 3; t++) {
-      if (!p.ds_cnt[t]) continue;
+      if (!((pr.inc >> t) & 1u)) continue;
       const uint64_t w = dsmask(s, DSM_DNUMA + t, i);
       int cnt = 0;
       for (int q = 0; q < 16; q++) {
         const uint32_t c = (uint32_t)(w >> (4 * q)) & 15u;
         cnt += (c >= 1 && c <= 8 && ((m >> (c - 1)) & 1u)) ? 1 : 0;
       }
-      if (cnt > 0 && cnt < p.ds_cnt[t]) {
+      if (cnt > 0 && cnt < pr.want[t]) {
         *why = KE_REASON_DS_INSUFFICIENT_NUMA_SCOPED;
         return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
       }
@@ -959,7 +1249,7 @@ __device__ __noinline__ void ds_numa_hints(const SoA& s, int64_t i, const DevPod
   }
   h.none = false;
   h.dmin = (uint8_t)dmin;
-  h.copies = (uint8_t)((p.ds_cnt[0] != 0) + (p.ds_cnt[1] != 0) + (p.ds_cnt[2] != 0));
+  h.copies = (uint8_t)__builtin_popcount(pr.inc);  // minAffinitySize: the types of requestsPerInstance
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1944,7 +2234,7 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
   }
   if (p.flags & PF_DS_INVALID) {  // DeviceShare PreFilter failed: the pod fits nowhere (utils.go:355-390)
     o.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
-    o.reason = KE_REASON_DS_INVALID_REQUEST;
+    o.reason = p.ds_req[0] ? (uint8_t)p.ds_req[0] : (uint8_t)KE_REASON_DS_INVALID_REQUEST;  // the host's reason
     o.total = -1;
     return o;
   }
@@ -4622,6 +4912,13 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
       ok = ds_try_allocate(s, node, pod, k, DsAff{false, 0u}, nullptr, &why) == KE_CODE_SUCCESS;  // Reserve: no affinity
     }
     RPROF(1)
+    if (ok && ds_here && (pod.flags & PF_DS_HINT)) {  // a hinted pod's Reserve-phase allocation must succeed
+      int why = 0;
+      uint32_t o3[3];
+      int8_t v2[2][DS_MINORS];
+      ok = hint_allocate(s, node, pod, k, DsAff{stored && aff != 0 && !(k.flags & AF_DS_NO_NUMA), aff}, true, true, o3, v2,
+                         &why) == KE_CODE_SUCCESS;
+    }
     sh.take = ok && rcb;
     if (sh.take) {
       sh.node = node;
@@ -4679,7 +4976,9 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
       for (int z = 0; z < 8; z++) cs_old[z] = sh.cs_old[z], cs_new[z] = sh.cs_old[z] + sh.cs_add[z];
       if (nsoa && v.zm) numa_reserve_cs(s, node, nf, v, got, dist, cs_old, cs_new, used, n_used, out16);
       RPROF(5)
-      if (ds_here) alloc = ds_reserve(s, node, pod, k, DsAff{stored && aff != 0 && !(k.flags & AF_DS_NO_NUMA), aff});
+      if (ds_here)
+        alloc = ds_reserve(s, node, pod, k, DsAff{stored && aff != 0 && !(k.flags & AF_DS_NO_NUMA), aff},
+                           s.vfo ? s.vfo + (int64_t)base * 2 * DS_MINORS : nullptr);
       out_node = (int32_t)node + global_offset;
       out_score = key_score(w);
       if (quota) quota_reserve_g(s, pod, qreq);  // ElasticQuota Reserve
@@ -4726,6 +5025,10 @@ struct DeviceState {
   // pods
   DevPod* d_pods = nullptr;
   int64_t pods_cap = 0;
+  DevPodHint* d_ph = nullptr;  // the hinted pods' records of the current call
+  int64_t ph_cap = 0;
+  int8_t* d_vfo = nullptr;     // [n_pods][2][DS_MINORS] VF ranks of the Reserves
+  int64_t vfo_cap = 0;
   // batch buffers
   uint16_t* d_scores = nullptr;  // [MAX_BATCH][capacity]
   uint32_t* d_cand = nullptr;    // [MAX_BATCH][KMAX]
@@ -4874,7 +5177,7 @@ void device_destroy(Context* ctx) {
                   d->d_numaalloc, d->d_numarows, d->d_defer, d->d_defer_cnt, d->soa.cs, d->soa.cpu,
                   d->d_cpurows, d->d_cpusets, d->d_aff, d->soa.qt, d->soa.qm, d->d_sched, d->d_stale,
                   d->d_stale_cnt, d->d_trows, d->d_tcnt, d->d_chg, d->soa.rec, d->soa.pt, d->soa.kerr,
-                  d->soa.xf, d->soa.xm, d->d_xrows};
+                  d->soa.xf, d->soa.xm, d->d_xrows, d->soa.dsx, d->d_ph, d->d_vfo};
   if (d->estream) (void)hipStreamSynchronize(d->estream);
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -4985,13 +5288,15 @@ static KArgs make_kargs(const Context* ctx, int64_t now) {
   return k;
 }
 
+constexpr int DS_ROW_WORDS = NUM_DS_FIELDS + NUM_DS_MASKS + NUM_DSX;  // device fields, masks, hint words
 __global__ void k_scatter_ds(SoA s, const int64_t* __restrict__ rows, const int32_t* __restrict__ idx, int n) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   const int64_t i = idx[t];
-  const int64_t* r = rows + (int64_t)t * (NUM_DS_FIELDS + NUM_DS_MASKS);
+  const int64_t* r = rows + (int64_t)t * DS_ROW_WORDS;
   for (int f = 0; f < NUM_DS_FIELDS; f++) s.ds[f * s.stride + i] = r[f];
   for (int w = 0; w < NUM_DS_MASKS; w++) s.dsm[w * s.stride + i] = (uint64_t)r[NUM_DS_FIELDS + w];
+  for (int w = 0; w < NUM_DSX; w++) s.dsx[w * s.stride + i] = r[NUM_DS_FIELDS + NUM_DS_MASKS + w];
 }
 
 static int ensure_ds(Context* ctx) {
@@ -5001,6 +5306,8 @@ static int ensure_ds(Context* ctx) {
   HIP_OK(hipMalloc(&d->soa.dsm, sizeof(uint64_t) * NUM_DS_MASKS * d->capacity));
   HIP_OK(hipMemsetAsync(d->soa.ds, 0, sizeof(int64_t) * NUM_DS_FIELDS * d->capacity, d->stream));
   HIP_OK(hipMemsetAsync(d->soa.dsm, 0, sizeof(uint64_t) * NUM_DS_MASKS * d->capacity, d->stream));
+  HIP_OK(hipMalloc(&d->soa.dsx, sizeof(int64_t) * NUM_DSX * d->capacity));
+  HIP_OK(hipMemsetAsync(d->soa.dsx, 0, sizeof(int64_t) * NUM_DSX * d->capacity, d->stream));
   d->ds_alloc = true;
   return KE_OK;
 }
@@ -5125,8 +5432,9 @@ int device_refresh(Context* ctx, int64_t now) {
     derive_row(ctx->cfg, ns, now, &r, &vu);
     if (ns.dirty && d->ds_alloc) {
       const size_t o = dsrows.size();
-      dsrows.resize(o + NUM_DS_FIELDS + NUM_DS_MASKS);
+      dsrows.resize(o + DS_ROW_WORDS);
       derive_ds_row(ns, &dsrows[o], reinterpret_cast<uint64_t*>(&dsrows[o + NUM_DS_FIELDS]));
+      derive_dsx_row(ns, &dsrows[o + NUM_DS_FIELDS + NUM_DS_MASKS]);
       dsidx.push_back(i);
     }
     if (ns.dirty && d->numa_alloc) {
@@ -5160,10 +5468,10 @@ int device_refresh(Context* ctx, int64_t now) {
     const int64_t n = (int64_t)dsidx.size();
     if (d->ds_staging_cap < n) {
       if (d->d_dsrows) HIP_OK(hipFree(d->d_dsrows));
-      HIP_OK(hipMalloc(&d->d_dsrows, sizeof(int64_t) * (NUM_DS_FIELDS + NUM_DS_MASKS) * n + sizeof(int32_t) * n));
+      HIP_OK(hipMalloc(&d->d_dsrows, sizeof(int64_t) * DS_ROW_WORDS * n + sizeof(int32_t) * n));
       d->ds_staging_cap = n;
     }
-    int32_t* didx = reinterpret_cast<int32_t*>(d->d_dsrows + (NUM_DS_FIELDS + NUM_DS_MASKS) * n);
+    int32_t* didx = reinterpret_cast<int32_t*>(d->d_dsrows + DS_ROW_WORDS * n);
     HIP_OK(hipMemcpyAsync(d->d_dsrows, dsrows.data(), sizeof(int64_t) * dsrows.size(), hipMemcpyHostToDevice, d->stream));
     HIP_OK(hipMemcpyAsync(didx, dsidx.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, d->stream));
     hipLaunchKernelGGL(k_scatter_ds, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, d->stream, d->soa, d->d_dsrows, didx,
@@ -5238,13 +5546,25 @@ static int upload_pods(Context* ctx, int32_t n_pods, const ke_pod* pods) {
   DeviceState* d = ctx->dev;
   std::vector<DevPod>& dp = d->host_pods;
   dp.resize((size_t)n_pods);
+  std::vector<DevPodHint> ph;  // the hinted pods' records; DevPod::ring_bw = slot
   for (int32_t p = 0; p < n_pods; p++) {
-    dp[p] = make_dev_pod(ctx->cfg, pods[p]);
+    const ke_pod_device_hints* h = pod_hints(*ctx, pods[p]);
+    dp[p] = make_dev_pod(ctx->cfg, pods[p], h, &ctx->tmpl);
     if (ctx->n_bind_nodes > 0 && dp[p].req[0] > 0) dp[p].flags |= PF_CPUSET;  // a node policy may bind it
+    if (dp[p].flags & PF_DS_HINT) {
+      ph.push_back(make_pod_hint(*ctx, pods[p], dp[p], *h));
+      dp[p].ring_bw = (int64_t)ph.size() - 1;
+    }
   }
   int rc = ensure((void**)&d->d_pods, &d->pods_cap, sizeof(DevPod) * (int64_t)std::max(n_pods, 1));
   if (rc) return rc;
   HIP_OK(hipMemcpyAsync(d->d_pods, dp.data(), sizeof(DevPod) * n_pods, hipMemcpyHostToDevice, d->stream));
+  if (!ph.empty()) {
+    rc = ensure((void**)&d->d_ph, &d->ph_cap, sizeof(DevPodHint) * (int64_t)ph.size());
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(d->d_ph, ph.data(), sizeof(DevPodHint) * ph.size(), hipMemcpyHostToDevice, d->stream));
+  }
+  d->soa.ph = d->d_ph;
   HIP_OK(hipStreamSynchronize(d->stream));
   return KE_OK;
 }
@@ -5367,7 +5687,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   ctx->last_ds_cuts = 0;
   for (int32_t p = 0; p < n_pods;) {
     const uint32_t f = d->host_pods[p].flags;
-    if ((f & PF_CPUSET) || ((f & PF_DS) && !ds_batch)) {
+    if ((f & PF_CPUSET) || ((f & PF_DS) && !ds_batch) || (f & PF_DS_HINT)) {  // hinted pods: singletons
       batches.push_back({1, (f & PF_DS) != 0, (f & PF_CPUSET) != 0, false});
       p++;
       continue;
@@ -5376,7 +5696,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     bool has_ds = false, ds_pods = false;
     while (p + bp < n_pods && bp < B) {
       const uint32_t g = d->host_pods[p + bp].flags;
-      if ((g & PF_CPUSET) || ((g & PF_DS) && !ds_batch)) break;
+      if ((g & PF_CPUSET) || ((g & PF_DS) && !ds_batch) || (g & PF_DS_HINT)) break;
       has_ds = has_ds || (g & PF_DS);
       ds_pods = ds_pods || (g & PF_DS);
       bp++;
@@ -5405,6 +5725,15 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   rc = ensure((void**)&d->d_cpusets, &d->cpusets_cap, sizeof(uint64_t) * 4 * (int64_t)n_pods);
   if (rc) return rc;
   HIP_OK(hipMemsetAsync(d->d_cpusets, 0, sizeof(uint64_t) * 4 * n_pods, d->stream));
+  bool any_hint = false;
+  for (const DevPod& q : d->host_pods) any_hint = any_hint || (q.flags & PF_DS_HINT);
+  d->soa.vfo = nullptr;
+  if (any_hint) {  // the VF ranks the hinted pods' Reserves take
+    rc = ensure((void**)&d->d_vfo, &d->vfo_cap, 2 * DS_MINORS * (int64_t)n_pods);
+    if (rc) return rc;
+    HIP_OK(hipMemsetAsync(d->d_vfo, 0xFF, 2 * DS_MINORS * (size_t)n_pods, d->stream));
+    d->soa.vfo = d->d_vfo;
+  }
   const bool numa = d->numa_alloc;
   if (numa && !d->d_numaalloc) HIP_OK(hipMalloc(&d->d_numaalloc, sizeof(int64_t) * 16 * d->out_cap));
   if (numa) {  // deferred-pair list of one batch (reused) + a counter per batch
@@ -5671,6 +6000,9 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   ctx->last_cpusets.assign((size_t)n_pods * 4, 0);
   HIP_OK(hipMemcpyAsync(ctx->last_cpusets.data(), d->d_cpusets, sizeof(uint64_t) * 4 * n_pods, hipMemcpyDeviceToHost,
                         d->stream));
+  ctx->last_vf.assign(d->soa.vfo ? (size_t)n_pods * 2 * DS_MINORS : 0, -1);
+  if (d->soa.vfo)
+    HIP_OK(hipMemcpyAsync(ctx->last_vf.data(), d->d_vfo, 2 * DS_MINORS * (size_t)n_pods, hipMemcpyDeviceToHost, d->stream));
   ctx->last_numa_alloc.clear();
   if (numa) {
     ctx->last_numa_alloc.assign((size_t)n_pods * 16, 0);

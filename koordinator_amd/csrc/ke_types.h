@@ -106,6 +106,7 @@ enum PodFlag : uint32_t {
   PF_GPU_PART_SPEC = 1u << 27, // GPUPartitionSpec present: honorGPUPartition
   PF_GPU_PART_RESTRICTED = 1u << 28,  // GPUPartitionSpec.AllocatePolicy Restricted
   PF_GPU_RING_BW = 1u << 29,   // GPUPartitionSpec.RingBusBandwidth set (DevPod::ring_bw)
+  PF_DS_HINT = 1u << 30,       // DeviceAllocateHints / DeviceJointAllocate: DevPod::ring_bw = the DevPodHint slot
 };
 KE_HD inline int pf_cpu_required(uint32_t f) { return (int)((f >> 15) & 3u); }
 KE_HD inline int pf_cpu_preferred(uint32_t f) { return (int)((f >> 17) & 3u); }
@@ -200,6 +201,40 @@ struct DevPod {
   uint64_t xmask;
 };
 static_assert(sizeof(DevPod) == 128, "DevPod layout");
+// DevPod::ds_cnt of an ApplyForAll type: the desired count is the node's devices of the type matching the Selector
+constexpr uint8_t DS_CNT_ALL = 255;
+
+// ---- DeviceShare hints: one record per hinted pod of a call, indexed by DevPod::ring_bw --------
+// Label sets (of devices and VF groups) are interned per context into ids 0..255 (0 = no labels); a selector
+// becomes the 256-bit set of label-set ids it matches.  GPU template model keys likewise (ids 1..255).
+enum PodHintFlag : uint32_t {
+  PH_SEL0 = 1u << 0,     // 3 bits: the type has a Selector (filterNodeDevice keeps the matching devices)
+  PH_FILTER = 1u << 3,   // state.hasSelectors: the filtered nodeDevice view
+  PH_VF0 = 1u << 4,      // 3 bits: mustAllocateVF for the type
+  PH_TMPL = 1u << 8,     // enforceGPUSharedResourceTemplate
+  PH_JOINT_PCIE = 1u << 9,      // DeviceJointAllocate RequiredScope SamePCIe
+  PH_FITS_WELL_PLANNED = 1u << 10,  // podFitsSecondaryDeviceWellPlanned
+};
+struct DevPodHint {
+  uint64_t sel[3][4];    // label-set ids the type's Selector matches (all ones without one)
+  uint64_t vfsel[3][4];  // label-set ids the type's VFSelector matches
+  uint64_t tmpl1[4];     // model key ids with exactly one candidate template
+  uint64_t tmplm[4];     // model key ids with two or more
+  int64_t ring_bw;       // GPUPartitionSpec.RingBusBandwidth (PF_GPU_RING_BW)
+  uint32_t flags;        // PH_*
+  uint8_t joint_n;       // DeviceJointAllocate types (primary first)
+  int8_t joint[3];
+};
+static_assert(sizeof(DevPodHint) == 272, "DevPodHint layout");
+// Per node DeviceShare hint state (a third device SoA, field-major, allocated with the device SoA):
+constexpr int DSX_LBL = 0;     // 6 words: label-set id of (type, minor), 8 bits, word 2*type + minor/8
+constexpr int DSX_PCIE = 6;    // 6 words: PCIe rank of (type, minor) (ke_device.pcie_rank), 0xFF = no topology
+constexpr int DSX_NODE = 12;   // bit 0 secondary well planned, bits 1-2: the node has VFs of RDMA / FPGA,
+                               // bits 8-15: GPU template model key id (0 = none)
+constexpr int DSX_VFFREE = 13; // 32 words: VF ranks not held, of (type 1..2, minor): word 16*(type-1) + minor
+constexpr int DSX_VFG = 45;    // 128 words: group g's VF ranks of (type, minor): DSX_VFG + 4*(16*(type-1)+minor) + g
+constexpr int DSX_VFL = 173;   // 16 words: the 4 groups' label-set ids of (type, minor), 8 bits each, 2 devices a word
+constexpr int NUM_DSX = 189;
 KE_HD inline int pod_scope(uint32_t flags) { return (int)((flags >> 24) & 7u); }
 KE_HD inline int scope_level(int scope) { return scope >= 1 && scope <= 4 ? scope : 0; }
 

@@ -6,6 +6,8 @@ boundary structs, through the C ABI (ke_decode_* in libkoordeval.so; no Python r
     pod = decode_pod(pod_json, xres_names)         -> abi.Pod
     devices, (has_table, honor, partitions) = decode_device(device_json)
     zones, cpus = decode_nrt(nrt_json, node)       (patches the NRT-side fields of `node`)
+    hints = decode_pod_device_hints(pod_json)       -> abi.PodDeviceHints or None (no hint annotations)
+    well_planned, model_key = decode_device_flags(device_json, node_json)
 Objects may be given as dicts (serialised with json.dumps) or JSON text.
 """
 import ctypes as C
@@ -98,3 +100,26 @@ def decode_nrt(obj, node):
     _check(lib, lib.ke_decode_nrt(t, len(t), C.byref(node), abi.MAX_NUMA, abi.ptr(zones), C.byref(nz), abi.MAX_CPUS,
                                   abi.ptr(cpus), C.byref(nc)))
     return zones[:nz.value], cpus[:nc.value]
+
+
+def label_id(text):
+    """ke_label_id: the process-wide id of a label key / value string (0 for an empty one)."""
+    return _lib().ke_label_id(text.encode())
+
+
+def decode_pod_device_hints(obj):
+    lib = _lib()
+    t = _text(obj)
+    h = abi.PodDeviceHints()
+    present = abi.i32()
+    _check(lib, lib.ke_decode_pod_device_hints(t, len(t), C.byref(h), C.byref(present)))
+    return h if present.value else None
+
+
+def decode_device_flags(device_obj=None, node_obj=None):
+    lib = _lib()
+    dt = _text(device_obj) if device_obj is not None else None
+    nt = _text(node_obj) if node_obj is not None else None
+    w, k = abi.i32(), abi.i32()
+    _check(lib, lib.ke_decode_device_flags(dt, len(dt) if dt else 0, nt, len(nt) if nt else 0, C.byref(w), C.byref(k)))
+    return bool(w.value), k.value

@@ -121,6 +121,21 @@ class Evaluator:
     def delete_devices(self, i):
         self._check(self.lib.ke_node_devices_delete(self.h, i))
 
+    def set_pod_device_hints(self, hints):
+        """ke_set_pod_device_hints: the DeviceAllocateHints / DeviceJointAllocate table (POD_DEVICE_HINTS_DTYPE)
+        ke_pod.device_hint indexes (1 + index)."""
+        h = abi.struct_array(hints, abi.PodDeviceHints)
+        self._check(self.lib.ke_set_pod_device_hints(self.h, len(h), abi.ptr(h)))
+
+    def gpu_templates_load(self, templates):
+        """ke_gpu_templates_load: GPU shared resource templates (GPU_TEMPLATE_DTYPE)."""
+        t = abi.struct_array(templates, abi.GpuTemplate)
+        self._check(self.lib.ke_gpu_templates_load(self.h, len(t), abi.ptr(t)))
+
+    def set_device_flags(self, i, secondary_well_planned, gpu_model_key):
+        """ke_node_device_flags: the Device's secondary-well-planned label and the node's GPU template key."""
+        self._check(self.lib.ke_node_device_flags(self.h, i, int(secondary_well_planned), int(gpu_model_key)))
+
     def set_gpu_partitions(self, i, has_table, honor, partitions=None):
         """The node's GPU partition indexer + policy (model.gpu_partition_state(...))."""
         parts = np.ascontiguousarray(partitions if partitions is not None else np.zeros(0, abi.GPU_PARTITION_DTYPE),

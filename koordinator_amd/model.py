@@ -343,14 +343,8 @@ def _device_annotations(p, spec, hints, joint):
     for t, h in (hints or {}).items():
         if h is None:
             continue
-        if h.get("selector") is not None:
-            bits |= abi.DHINT_SELECTOR
-        if h.get("vfSelector") is not None:
-            bits |= abi.DHINT_VF
-        if h.get("allocateStrategy"):
-            bits |= abi.DHINT_STRATEGY
-        if h.get("exclusivePolicy"):
-            bits |= abi.DHINT_EXCLUSIVE
+        if t == "gpu" and h.get("vfSelector") is not None:  # a GPU VFSelector is not modelled
+            bits |= abi.DHINT_GPU_VF
         if t == "gpu" and h.get("requiredTopologyScope"):
             p.gpu_required_topology_scope = abi.SCOPES.get(h["requiredTopologyScope"], abi.SCOPE_UNKNOWN)
     p.device_hints = bits
@@ -360,6 +354,92 @@ def _device_annotations(p, spec, hints, joint):
         kept = [t for t in joint.get("deviceTypes", [])
                 if req.get(t) and ((hints or {}).get(t) or {}).get("allocateStrategy") != "ApplyForAll"]
         p.device_joint_allocate = 1 if kept else 0
+
+
+DEV_TYPE_IDS = {"gpu": abi.DEV_GPU, "rdma": abi.DEV_RDMA, "fpga": abi.DEV_FPGA}
+SEL_OPS = {"In": abi.SEL_IN, "NotIn": abi.SEL_NOT_IN, "Exists": abi.SEL_EXISTS, "DoesNotExist": abi.SEL_DOES_NOT_EXIST}
+
+
+def label_id(text):
+    from . import decode  # the process-wide string table lives in the library (ke_label_id)
+    return decode.label_id(text) if text else 0
+
+
+def make_labels(labels):
+    """abi.Labels from a {key: value} dict"""
+    out = abi.Labels()
+    for k, v in (labels or {}).items():
+        out.key[out.n] = label_id(k)
+        out.value[out.n] = label_id(v)
+        out.n += 1
+    return out
+
+
+def _selector(sel, out):
+    """metav1.LabelSelector dict -> abi.LabelSelector (GetFastLabelSelector / LabelSelectorAsSelector);
+    returns False when the conversion fails (an invalid operator / value count)"""
+    if sel is None:
+        return True
+    out.present = 1
+    ok = True
+    for k, v in (sel.get("matchLabels") or {}).items():
+        r = out.req[out.n]
+        r.key, r.op, r.n_values = label_id(k), abi.SEL_IN, 1
+        r.values[0] = label_id(v)
+        out.n += 1
+    for e in sel.get("matchExpressions") or []:
+        r = out.req[out.n]
+        r.key = label_id(e["key"])
+        vals = e.get("values") or []
+        r.n_values = len(vals)
+        for i, v in enumerate(vals):
+            r.values[i] = label_id(v)
+        op = e.get("operator")
+        r.op = SEL_OPS.get(op, abi.SEL_DOES_NOT_EXIST)
+        if op not in SEL_OPS or (op in ("In", "NotIn")) != bool(vals):
+            ok = False
+        out.n += 1
+    return ok
+
+
+def make_device_hints(hints=None, joint=None):
+    """ke_pod_device_hints from DeviceAllocateHints {type: {'selector', 'vfSelector', 'allocateStrategy',
+    'exclusivePolicy'}} and DeviceJointAllocate {'deviceTypes', 'requiredScope'} dicts (utils.go:414-482)."""
+    h = abi.PodDeviceHints()
+    for t, d in (hints or {}).items():
+        d = d or {}
+        ok = _selector(d.get("selector"), abi.LabelSelector()) and _selector(d.get("vfSelector"), abi.LabelSelector())
+        h.invalid |= 0 if ok else 1
+        if d.get("selector") is not None:
+            h.has_selectors = 1
+        if t not in DEV_TYPE_IDS:
+            continue
+        x = h.hint[DEV_TYPE_IDS[t]]
+        _selector(d.get("selector"), x.selector)
+        _selector(d.get("vfSelector"), x.vf_selector)
+        x.strategy = {"ApplyForAll": abi.DSTRATEGY_APPLY_FOR_ALL,
+                      "RequestsAsCount": abi.DSTRATEGY_REQUESTS_AS_COUNT}.get(d.get("allocateStrategy"), 0)
+        x.exclusive = {"DeviceLevel": abi.DEXCL_DEVICE_LEVEL, "PCIeLevel": abi.DEXCL_PCIE_LEVEL}.get(d.get("exclusivePolicy"), 0)
+    if joint is not None:
+        for t in joint.get("deviceTypes") or []:
+            tid = DEV_TYPE_IDS.get(t)
+            if tid is None or h.hint[tid].strategy == abi.DSTRATEGY_APPLY_FOR_ALL:
+                continue
+            if tid not in list(h.joint_types[:h.joint_n]):
+                h.joint_types[h.joint_n] = tid
+                h.joint_n += 1
+        h.joint_same_pcie = 1 if joint.get("requiredScope") == "SamePCIe" else 0
+    return h
+
+
+def make_gpu_template(model_key, name, resources):
+    t = abi.GpuTemplate()
+    t.model_key, t.name = label_id(model_key), label_id(name)
+    for k, v in resources.items():
+        slot = {"koordinator.sh/gpu-core": 0, "koordinator.sh/gpu-memory": 1, "koordinator.sh/gpu-memory-ratio": 2}[k]
+        t.has[slot] = 1
+        t.value[slot] = value(v)
+    return t
 
 
 # GPUPartitionIndexOfNVIDIAHopper (allocator_gpu_helper.go:28-144): {number of GPUs: [minors, ...]}, score 1
@@ -521,6 +601,18 @@ def make_devices(devices):
                 key = DEVICE_KEYS[t][k]
                 getattr(dev, hfield)[key] = 1
                 getattr(dev, field)[key] = value(q)
+        dev.labels = make_labels(d.get("labels"))
+        # VFGroups: VF rank = position of its BusID among the device's VFs in string order
+        groups = d.get("vf_groups") or []
+        bus = sorted((vf, g) for g, grp in enumerate(groups) for vf in grp.get("vfs", []))
+        if t != abi.DEV_GPU:
+            dev.n_vf_groups = len(groups)
+            for g, grp in enumerate(groups):
+                dev.vf_groups[g].labels = make_labels(grp.get("labels"))
+            for r, (vf, g) in enumerate(bus):
+                dev.vf_groups[g].vfs |= 1 << r
+                if vf in (d.get("vf_allocated") or ()):
+                    dev.vf_allocated |= 1 << r
         arr[i] = np.frombuffer(bytes(dev), dtype=abi.DEVICE_DTYPE)[0]
     return arr
 

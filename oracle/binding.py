@@ -51,7 +51,12 @@ def load():
         "or_node_devices_set": (C.c_int, [V, i32, i32, V]),
         "or_node_devices_delete": (C.c_int, [V, i32]),
         "or_node_gpu_partitions": (C.c_int, [V, i32, i32, i32, i32, V]),
-        "or_ds_prefilter": (C.c_int, [C.POINTER(abi.Pod), C.POINTER(C.c_int), V, V, V]),
+        "or_ds_prefilter": (C.c_int, [V, C.POINTER(abi.Pod), C.POINTER(C.c_int), V, V, V]),
+        "or_set_pod_device_hints": (C.c_int, [V, i32, V]),
+        "or_gpu_templates_load": (C.c_int, [V, i32, V]),
+        "or_node_device_flags": (C.c_int, [V, i32, i32, i32]),
+        "or_last_vf_ranks": (C.c_int, [V, i32, V]),
+        "or_ds_allocate": (C.c_int, [V, C.POINTER(abi.Pod), i32, i32, i32, V, V, V]),
         "or_ds_score_device": (i64, [V, i32, V, V, V, V, V, V]),
         "or_normalize_scores": (None, [V, i32]),
         "or_topology_merge": (C.c_int, [i32, C.c_uint32, i32, V, V, V, V, V, V, V, V, V]),
@@ -239,8 +244,29 @@ class Oracle:
         cnt = np.zeros(3, np.int32)
         req = np.zeros((3, 3), np.int64)
         has = np.zeros((3, 3), np.uint8)
-        code = self.lib.or_ds_prefilter(C.byref(pod), C.byref(skip), abi.ptr(cnt), abi.ptr(req), abi.ptr(has))
+        code = self.lib.or_ds_prefilter(self.h, C.byref(pod), C.byref(skip), abi.ptr(cnt), abi.ptr(req), abi.ptr(has))
         return code, bool(skip.value), cnt, req, has
+
+    def set_pod_device_hints(self, hints):
+        """the ke_set_pod_device_hints table (POD_DEVICE_HINTS_DTYPE array); ke_pod.device_hint = 1 + index"""
+        h = abi.struct_array(hints, abi.PodDeviceHints)
+        assert self.lib.or_set_pod_device_hints(self.h, len(h), abi.ptr(h)) == 0
+
+    def gpu_templates_load(self, templates):
+        t = abi.struct_array(templates, abi.GpuTemplate)
+        assert self.lib.or_gpu_templates_load(self.h, len(t), abi.ptr(t)) == 0
+
+    def set_device_flags(self, i, secondary_well_planned, gpu_model_key):
+        assert self.lib.or_node_device_flags(self.h, i, int(secondary_well_planned), int(gpu_model_key)) == 0
+
+    def ds_allocate(self, pod, node, reserve=False, scored=False):
+        """AutopilotAllocator.Allocate: (status, reason, minors[3], vf_ranks[2][16])"""
+        out = np.zeros(3, np.uint32)
+        vf = np.zeros((2, abi.MAX_MINORS), np.int8)
+        reason = np.zeros(1, np.int32)
+        st = self.lib.or_ds_allocate(self.h, C.byref(pod), node, int(reserve), int(scored), abi.ptr(out), abi.ptr(vf),
+                                     abi.ptr(reason))
+        return st, int(reason[0]), out, vf
 
     def ds_score_device(self, dev_type, req, total, free):
         """each argument: (values[3], has[3])"""
@@ -323,6 +349,9 @@ class Oracle:
         out["cpuset"] = np.where(placed[:, None], self.last_cpusets[:n], 0)
         out["numa"] = np.where(placed[:, None], self.last_numa_allocations[:n], 0)
         out["device_minors"] = np.where(placed, self.last_device_allocations[:n], 0)
+        vf = np.full((len(chosen), 2 * abi.MAX_MINORS), -1, np.int8)
+        self.lib.or_last_vf_ranks(self.h, len(chosen), abi.ptr(vf))
+        out["vf_rank"] = np.where(placed[:, None], vf[:n], -1)
         return out
 
     def node_state(self, i):

@@ -58,6 +58,8 @@ typedef struct or_node {
   ke_device dev[KE_DEV_TYPES * KE_MAX_MINORS];
   /* GPU partition indexer + policy as GPUAllocator.Allocate resolves them (allocator_gpu.go:77-82) */
   int gpu_has_table, gpu_honor;
+  int secondary_well_planned; /* Device label: IsSecondaryDeviceWellPlanned (device_cache.go:546) */
+  int32_t gpu_model_key;      /* "<vendor>-<model>" of the node's GPU labels (allocator_gpu.go:140), 0 = none */
   int32_t n_part;
   ke_gpu_partition part[KE_MAX_GPU_PARTITIONS];
   struct or_cpus* cpus; /* CPU topology + allocated CPUs (NULL: no CPU topology) */
@@ -79,6 +81,13 @@ struct or_cluster {
   int32_t n;
   or_node* nodes;
   or_quotas* quotas; /* ElasticQuota tree (quota.c), NULL until loaded */
+  /* ke_set_pod_device_hints table (ke_pod.device_hint = 1 + index) and the GPU shared resource templates */
+  ke_pod_device_hints* hints;
+  int32_t n_hints;
+  ke_gpu_template* tmpl;
+  int32_t n_tmpl;
+  int8_t* last_vf; /* VF ranks of the last or_schedule: [pod][2][KE_MAX_MINORS] */
+  int32_t last_vf_n;
 };
 
 /* ---------------------------------------------------------------------------------------------- */
@@ -1588,6 +1597,14 @@ static int rl_leq(rl a, rl b, int nk) {
     if (b.has[k] && a.has[k] && a.v[k] > b.v[k]) return 0;
   return 1;
 }
+/* quotav1.Equals: the same keys with equal values */
+static int rl_equal(rl a, rl b, int nk) {
+  for (int k = 0; k < nk; k++) {
+    if (a.has[k] != b.has[k]) return 0;
+    if (a.has[k] && a.v[k] != b.v[k]) return 0;
+  }
+  return 1;
+}
 /* quotav1.Add */
 static rl rl_add(rl a, rl b, int nk) {
   rl r = rl_empty();
@@ -1601,6 +1618,7 @@ static rl rl_add(rl a, rl b, int nk) {
 /* the request of one device instance + how many, per type (preparePod + CalcDesiredRequestsAndCount) */
 typedef struct ds_pod {
   int status; /* PreFilter status: 0 or UnschedulableAndUnresolvable (invalid device requests) */
+  int status_reason; /* its reason: KE_REASON_DS_INVALID_REQUEST (0 here) / _INVALID_HINT / _NO_MATCHED_TEMPLATE */
   int skip;   /* no device requests: PreFilter returns Skip */
   int has[KE_DEV_TYPES];
   int count[KE_DEV_TYPES];
@@ -1612,6 +1630,15 @@ typedef struct ds_pod {
   int part_spec;        /* honorGPUPartition from the pod's GPUPartitionSpec */
   int part_restricted;  /* restrictedGPUPartition */
   int64_t ring_bw;      /* rindBusBandwidth, KE_ABSENT = nil */
+  /* parsePodDeviceShareExtensions (utils.go:414-455): the hints (NULL = none) */
+  const ke_pod_device_hints* h;
+  int apply_all[KE_DEV_TYPES]; /* ApplyForAll: the desired count is the node's (matching) devices */
+  int vf[KE_DEV_TYPES];        /* mustAllocateVF */
+  int sel[KE_DEV_TYPES];       /* a Selector for the type */
+  int has_selectors;           /* state.hasSelectors: filterNodeDevice runs */
+  int joint_n, joint[KE_DEV_TYPES], joint_pcie; /* DeviceJointAllocate after parsing; RequiredScope SamePCIe */
+  int fits_well_planned;       /* podFitsSecondaryDeviceWellPlanned (utils.go:381) */
+  int tmpl;                    /* enforceGPUSharedResourceTemplate (utils.go:508-515) */
 } ds_pod;
 
 static int valid_percentage(int64_t q) { return !(q > 100 && q % 100 != 0); } /* utils.go:222-227 */
@@ -1619,8 +1646,12 @@ static int valid_percentage(int64_t q) { return !(q > 100 && q % 100 != 0); } /*
 /* GetPodDeviceRequests -> ValidateDeviceRequest -> ConvertDeviceRequest (utils.go:304-342,392-412),
  * then calcDesiredRequestsAndCountForGPU (devicehandler_gpu.go:53-96) and
  * DefaultDeviceHandler.CalcDesiredRequestsAndCount (devicehandler_default.go:44-93, no hint). */
-static void ds_prepare_pod(const ke_pod* pod, ds_pod* d) {
+static int rl_equal(rl a, rl b, int nk);
+static int tmpl_candidates(const or_cluster* c, const ds_pod* d, int32_t key);
+static void ds_prepare_pod(const or_cluster* c, const ke_pod* pod, ds_pod* d) {
   memset(d, 0, sizeof *d);
+  const ke_pod_device_hints* h = NULL;
+  if (pod->device_hint > 0 && c && pod->device_hint <= c->n_hints) h = &c->hints[pod->device_hint - 1];
   const int64_t* q = pod->device_requests;
   /* GPU combination flags (utils.go:38-52) */
   enum { NV = 1, AMD = 2, KGPU = 4, SHARED = 8, CORE = 16, MEM = 32, RATIO = 64 };
@@ -1686,9 +1717,15 @@ static void ds_prepare_pod(const ke_pod* pod, ds_pod* d) {
       return;
     }
     int64_t n = 1, per = v;
+    const ke_device_hint* ht = h ? &h->hint[t] : NULL;
     if (v > 100 && v % 100 == 0) {
       n = v / 100;
       per = v / n;
+    } else if (ht && ht->strategy == KE_DSTRATEGY_APPLY_FOR_ALL) { /* devicehandler_default.go:62-80 */
+      d->apply_all[t] = 1;
+    } else if (ht && ht->strategy == KE_DSTRATEGY_REQUESTS_AS_COUNT) { /* :81-90 */
+      n = v;
+      per = ht->exclusive == KE_DEXCL_DEVICE_LEVEL ? 100 : 1;
     }
     d->has[t] = 1;
     d->count[t] = (int)n;
@@ -1703,6 +1740,91 @@ static void ds_prepare_pod(const ke_pod* pod, ds_pod* d) {
   d->part_spec = pod->gpu_partition_spec != 0;
   d->part_restricted = d->part_spec && pod->gpu_partition_restricted;
   d->ring_bw = d->part_spec ? pod->gpu_ring_bus_bandwidth : KE_ABSENT;
+  d->fits_well_planned = d->has[KE_DEV_GPU] && !d->gpu_shared;
+  if (d->skip) return;
+  d->h = h;
+  if (h) {
+    if (h->invalid) { /* newHintSelectors error: PreFilter UnschedulableAndUnresolvable */
+      d->status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+      d->status_reason = KE_REASON_DS_INVALID_HINT;
+      return;
+    }
+    d->has_selectors = h->has_selectors;
+    for (int t = 0; t < KE_DEV_TYPES; t++) {
+      d->vf[t] = h->hint[t].vf_selector.present != 0;
+      d->sel[t] = h->hint[t].selector.present != 0;
+    }
+    /* DeviceJointAllocate.DeviceTypes kept by parsePodDeviceShareExtensions (utils.go:430-442): requested, no
+     * ApplyForAll hint, annotation order */
+    for (int i = 0; i < h->joint_n && i < KE_DEV_TYPES; i++) {
+      const int t = h->joint_types[i];
+      if (t < 0 || t >= KE_DEV_TYPES || !d->has[t] || h->hint[t].strategy == KE_DSTRATEGY_APPLY_FOR_ALL) continue;
+      int dup = 0;
+      for (int q = 0; q < d->joint_n; q++) dup |= d->joint[q] == t;
+      if (!dup) d->joint[d->joint_n++] = t;
+    }
+    d->joint_pcie = h->joint_same_pcie;
+  }
+  /* parseGPURequirements: a shared GPU whose per-GPU request names a template-matched resource is allocated by
+   * template; no template of any GPU model equal to the request fails PreFilter (utils.go:508-515) */
+  if (d->has[KE_DEV_GPU] && d->gpu_shared && c) {
+    const uint32_t keys = c->cfg.deviceshare.template_matched_keys;
+    int named = 0;
+    for (int k = 0; k < KE_DKEYS; k++) named |= d->req[KE_DEV_GPU].has[k] && ((keys >> k) & 1u);
+    if (named) {
+      d->tmpl = 1;
+      if (tmpl_candidates(c, d, -1) == 0) {
+        d->status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+        d->status_reason = KE_REASON_DS_NO_MATCHED_TEMPLATE;
+      }
+    }
+  }
+}
+
+/* findMatchedTemplates(requestsPerGPU, strict) (gpu_shared_resource_templates_cache.go:41-62): templates whose
+ * resources equal the per-GPU request, of GPU model `key` (-1: any model) */
+static int tmpl_candidates(const or_cluster* c, const ds_pod* d, int32_t key) {
+  int n = 0;
+  for (int i = 0; i < c->n_tmpl; i++) {
+    const ke_gpu_template* t = &c->tmpl[i];
+    if (key >= 0 && t->model_key != key) continue;
+    rl r = rl_empty();
+    for (int k = 0; k < KE_DKEYS; k++) {
+      r.has[k] = t->has[k];
+      r.v[k] = t->has[k] ? t->value[k] : 0;
+    }
+    if (rl_equal(r, d->req[KE_DEV_GPU], KE_DKEYS)) n++;
+  }
+  return n;
+}
+
+/* labels.Selector.Matches for a converted metav1.LabelSelector (apimachinery labels/selector.go Requirement.Matches):
+ * In: the key is present with a listed value; NotIn: absent, or its value not listed; Exists / DoesNotExist. */
+static int label_get(const ke_labels* l, int32_t key, int32_t* value) {
+  for (int i = 0; i < l->n && i < KE_MAX_LABELS; i++)
+    if (l->key[i] == key) {
+      *value = l->value[i];
+      return 1;
+    }
+  return 0;
+}
+static int sel_matches(const ke_label_selector* s, const ke_labels* l) {
+  for (int r = 0; r < s->n && r < KE_MAX_SEL_REQS; r++) {
+    const ke_label_requirement* q = &s->req[r];
+    int32_t v = 0;
+    const int has = label_get(l, q->key, &v);
+    int listed = 0;
+    for (int i = 0; i < q->n_values && i < KE_MAX_SEL_VALUES; i++) listed |= q->values[i] == v;
+    int ok = 0;
+    switch (q->op) {
+      case KE_SEL_IN: ok = has && listed; break;
+      case KE_SEL_NOT_IN: ok = !has || !listed; break;
+      case KE_SEL_EXISTS: ok = has; break;
+      default: ok = !has; break;
+    }
+    if (!ok) return 0;
+  }
+  return 1;
 }
 
 /* one device type of a node's cache: minors in ascending order */
@@ -1766,19 +1888,26 @@ static int dev_allowed(const ke_device* dv, ds_aff a) {
  * device_cache.go:360-415) with no required resources and an empty preemptible map: the type is dropped
  * when its free is all zero (over every instance) or no instance passes the NUMA affinity; otherwise the
  * passing instances with used' = total - free (kept if non-zero) and free' = total - used'. */
-static void ds_filtered_view_aff(const or_node* nd, int t, ds_aff a, ds_view* v) {
+static const ke_device* dev_of(const or_node* nd, int t, int minor) {
+  for (int j = 0; j < nd->n_dev; j++)
+    if (nd->dev[j].type == t && nd->dev[j].minor == minor) return &nd->dev[j];
+  return NULL;
+}
+/* filterNodeDevice's Selector (device_allocator.go:150-161) */
+static int dev_selected(const ds_pod* d, int t, const ke_device* dv) {
+  return !d || !d->sel[t] || sel_matches(&d->h->hint[t].selector, &dv->labels);
+}
+static void ds_filtered_view_aff(const or_node* nd, const ds_pod* d, int t, ds_aff a, ds_view* v) {
   ds_orig_view(nd, t, v);
   const int nk = nkeys(t);
   int all_zero = 1;
   for (int i = 0; i < v->n; i++)
     if (!rl_is_zero(v->free[i], nk)) all_zero = 0;
-  if (a.on) { /* the instances of the type that pass the affinity, ascending minors */
+  if (a.on || (d && d->has_selectors)) { /* the instances that pass the affinity and the Selector, ascending minors */
     int n = 0;
     for (int i = 0; i < v->n; i++) {
-      const ke_device* dv = NULL;
-      for (int j = 0; j < nd->n_dev; j++)
-        if (nd->dev[j].type == t && nd->dev[j].minor == v->minor[i]) dv = &nd->dev[j];
-      if (!dev_allowed(dv, a)) continue;
+      const ke_device* dv = dev_of(nd, t, v->minor[i]);
+      if (!dev_allowed(dv, a) || !dev_selected(d, t, dv)) continue;
       v->minor[n] = v->minor[i];
       v->total[n] = v->total[i];
       v->used[n] = v->used[i];
@@ -1877,34 +2006,60 @@ static int64_t ds_score_device(const ke_deviceshare_args* a, int t, const rl* po
  * (score desc, minor asc) order (scoreDevices + sortDeviceResourcesByMinor, device_resources.go:171-208),
  * the first `count` with a non-zero free that covers the request.  Returns the number chosen
  * (picked[] = view indices).  scorer == NULL: Filter's allocator (every score 0). */
-static int ds_allocate(const ke_deviceshare_args* scorer, int t, const rl* req, int count, const ds_view* v,
-                       int* picked) {
+/* allocateVF (device_allocator.go:426-455): the lowest-BusID VF (rank) of the groups the VFSelector matches that
+ * the node's pods do not hold; -1 = none */
+static int vf_pick(const ke_device* dv, const ke_label_selector* vsel) {
+  if (!dv) return -1;
+  uint64_t cand = 0;
+  for (int g = 0; g < dv->n_vf_groups && g < KE_MAX_VF_GROUPS; g++)
+    if (sel_matches(vsel, &dv->vf_groups[g].labels)) cand |= dv->vf_groups[g].vfs;
+  cand &= ~dv->vf_allocated;
+  return cand ? __builtin_ctzll(cand) : -1;
+}
+
+/* defaultAllocateDevices with the joint-allocation extras: `pref` = preferred PCIe ranks
+ * (sortDeviceResourcesByPreferredPCIe, device_resources.go:211-220: preferred first, then score desc, minor
+ * asc), up to max_count devices (maxDesiredCount), and for a pod that must allocate VFs one VF per device
+ * (vf_out[i] = its rank; nd / d give the device infos and the VFSelector). */
+static int ds_allocate_x(const or_node* nd, const ds_pod* d, const ke_deviceshare_args* scorer, int t, const rl* req,
+                         int max_count, uint64_t pref, const ds_view* v, int* picked, int* vf_out) {
   const int nk = nkeys(t);
   if (!v->present) return 0;
-  int order[KE_MAX_MINORS];
+  int order[KE_MAX_MINORS], pf[KE_MAX_MINORS];
   int64_t sc[KE_MAX_MINORS];
   for (int i = 0; i < v->n; i++) {
     order[i] = i;
     sc[i] = scorer ? ds_score_device(scorer, t, req, &v->total[i], &v->free[i]) : 0;
+    const ke_device* dv = nd ? dev_of(nd, t, v->minor[i]) : NULL;
+    pf[i] = pref && dv && dv->has_topology && dv->pcie_rank >= 0 && dv->pcie_rank < 64 && ((pref >> dv->pcie_rank) & 1);
   }
-  for (int i = 1; i < v->n; i++) /* insertion sort: score desc, minor asc */
+  for (int i = 1; i < v->n; i++) /* insertion sort: preferred, score desc, minor asc */
     for (int j = i; j > 0; j--) {
       const int a = order[j - 1], b = order[j];
-      if (sc[b] > sc[a] || (sc[b] == sc[a] && v->minor[b] < v->minor[a])) {
-        order[j - 1] = b;
-        order[j] = a;
-      } else {
-        break;
-      }
+      const int before = pf[b] != pf[a] ? pf[b] > pf[a] : (sc[b] > sc[a] || (sc[b] == sc[a] && v->minor[b] < v->minor[a]));
+      if (!before) break;
+      order[j - 1] = b;
+      order[j] = a;
     }
+  const int vf = d && d->vf[t];
   int n = 0;
-  for (int i = 0; i < v->n && n < count; i++) {
-    const int d = order[i];
-    if (rl_is_zero(v->free[d], nk)) continue;
-    if (!rl_leq(*req, v->free[d], nk)) continue;
-    picked[n++] = d;
+  for (int i = 0; i < v->n && n < max_count; i++) {
+    const int k = order[i];
+    if (rl_is_zero(v->free[k], nk)) continue;
+    if (!rl_leq(*req, v->free[k], nk)) continue;
+    int r = -1;
+    if (vf) {
+      r = vf_pick(dev_of(nd, t, v->minor[k]), &d->h->hint[t].vf_selector);
+      if (r < 0) continue;
+    }
+    if (vf_out) vf_out[n] = r;
+    picked[n++] = k;
   }
   return n;
+}
+static int ds_allocate(const ke_deviceshare_args* scorer, int t, const rl* req, int count, const ds_view* v,
+                       int* picked) {
+  return ds_allocate_x(NULL, NULL, scorer, t, req, count, 0, v, picked, NULL);
 }
 
 /* ---- GPUAllocator (allocator_gpu.go) --------------------------------------------------------- */
@@ -2202,12 +2357,22 @@ static int gpu_by_topology(const or_node* nd, const ds_pod* d, const gpu_ctx* g,
 
 /* GPUAllocator.Allocate (allocator_gpu.go:72-112; allocateByTemplate is refused at the boundary) on the
  * filtered view.  Returns the status; *mask = the minors chosen. */
-static int ds_gpu_allocate(const or_node* nd, const ds_pod* d, const ds_view* v, const ke_deviceshare_args* scorer,
-                           uint32_t* mask, int* reason) {
+static int ds_gpu_allocate(const or_cluster* c, const or_node* nd, const ds_pod* d, const ds_view* v,
+                           const ke_deviceshare_args* scorer, uint32_t* mask, int* reason) {
   gpu_ctx g;
   gpu_ctx_init(nd, v, &g);
+  *mask = 0;
+  int general = 0; /* allocateByTemplate (:135-159): one candidate template of the node's GPU model -> generalAllocate */
+  if (d->tmpl) {
+    const int nc = tmpl_candidates(c, d, nd->gpu_model_key);
+    if (nc == 0) {
+      *reason = KE_REASON_DS_NO_MATCHED_TEMPLATE;
+      return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    }
+    general = nc == 1;
+  }
   const int honor = d->part_spec || nd->gpu_honor;
-  int st = gpu_by_partition(nd, d, &g, honor, mask, reason);
+  int st = general ? 0 : gpu_by_partition(nd, d, &g, honor, mask, reason);
   if (st || *mask) return st;
   st = gpu_by_topology(nd, d, &g, scorer, mask, reason); /* generalAllocate (:114-126) */
   if (st || *mask) return st;
@@ -2226,49 +2391,153 @@ static int ds_insufficient_reason(int t) {
                          : (t == KE_DEV_RDMA ? KE_REASON_DS_INSUFFICIENT_RDMA : KE_REASON_DS_INSUFFICIENT_FPGA);
 }
 
-/* AutopilotAllocator.Allocate (device_allocator.go:87-135) without a scorer, on the devices the NUMA
- * affinity leaves: Prepare (a requested type without devices in the cache), then every requested type in
- * the fixed order GPU, RDMA, FPGA (Go map order only changes the reason).  *gpu = the GPU minors. */
-static int ds_try_allocate(const or_node* nd, const ds_pod* d, ds_aff a, uint32_t* gpu, int* reason) {
-  *gpu = 0;
+/* AutopilotAllocator.Prepare (device_allocator.go:74-94) on node nd: per requested type whether it is in
+ * requestsPerInstance (a secondary type of a joint pod is left out outside Reserve on a node whose secondary
+ * devices are well planned, :188-190) and its desired count (ApplyForAll: the node's devices of the type
+ * matching the Selector, devicehandler_default.go:62-80); a type without devices, an ApplyForAll matching none,
+ * or a VF pod on a node without VFs of the type fail UnschedulableAndUnresolvable (fixed type order GPU, RDMA, FPGA). */
+static int ds_node_prepare(const or_node* nd, const ds_pod* d, int reserve, int* inc, int* count, int* reason) {
   for (int t = 0; t < KE_DEV_TYPES; t++) {
+    inc[t] = 0;
+    count[t] = 0;
     if (!d->has[t]) continue;
-    ds_view v;
-    ds_orig_view(nd, t, &v);
-    if (v.n == 0) {
+    if (d->joint_n > 0 && t != d->joint[0] && d->fits_well_planned && nd->secondary_well_planned && !reserve) continue;
+    int n = 0, matched = 0, vfs = 0;
+    for (int i = 0; i < nd->n_dev; i++) {
+      const ke_device* dv = &nd->dev[i];
+      if (dv->type != t) continue;
+      n++;
+      matched += dev_selected(d, t, dv);
+      vfs |= dv->n_vf_groups > 0;
+    }
+    if (n == 0) {
       *reason = ds_insufficient_reason(t);
       return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
     }
+    count[t] = d->apply_all[t] ? (d->sel[t] ? matched : n) : d->count[t];
+    if (count[t] == 0) {
+      *reason = ds_insufficient_reason(t);
+      return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    }
+    inc[t] = 1;
+    (void)vfs;
   }
   for (int t = 0; t < KE_DEV_TYPES; t++) {
-    if (!d->has[t]) continue;
-    ds_view v;
-    ds_filtered_view_aff(nd, t, a, &v);
-    if (t == KE_DEV_GPU) {
-      int why = 0;
-      const int st = ds_gpu_allocate(nd, d, &v, NULL, gpu, &why);
-      if (st) {
-        *reason = why;
-        return st;
-      }
-      continue;
-    }
-    int picked[KE_MAX_MINORS];
-    if (ds_allocate(NULL, t, &d->req[t], d->count[t], &v, picked) < d->count[t]) {
-      *reason = ds_insufficient_reason(t);
-      return KE_CODE_UNSCHEDULABLE;
+    if (!inc[t] || !d->vf[t]) continue;
+    int vfs = 0;
+    for (int i = 0; i < nd->n_dev; i++) vfs |= nd->dev[i].type == t && nd->dev[i].n_vf_groups > 0;
+    if (!vfs) { /* hasVirtualFunctions */
+      *reason = t == KE_DEV_RDMA ? KE_REASON_DS_INSUFFICIENT_RDMA_VF : KE_REASON_DS_INSUFFICIENT_FPGA_VF;
+      return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
     }
   }
-  return KE_CODE_SUCCESS;
+  return 0;
+}
+
+/* allocateDevices (device_allocator.go:320-350) of one type: GPUs through GPUAllocator, other types
+ * defaultAllocateDevices; desired / maxDesired as that function derives them from the count and the preferred
+ * PCIe set.  out = minors, vf[minor] = VF ranks. */
+static int ds_alloc_type(const or_cluster* c, const or_node* nd, const ds_pod* d, int t, const rl* req, int desired,
+                         uint64_t pref, ds_aff a, const ke_deviceshare_args* scorer, uint32_t* out, int8_t* vf,
+                         int* reason) {
+  int max_count = desired;
+  const int np = __builtin_popcountll(pref);
+  if (np > max_count) max_count = np;
+  if (desired == 0) desired = 1;
+  if (max_count < desired) max_count = desired;
+  ds_view v;
+  ds_filtered_view_aff(nd, d, t, a, &v);
+  *out = 0;
+  if (t == KE_DEV_GPU) return ds_gpu_allocate(c, nd, d, &v, scorer, out, reason);
+  int picked[KE_MAX_MINORS], vr[KE_MAX_MINORS];
+  const int n = ds_allocate_x(nd, d, scorer, t, req, max_count, pref, &v, picked, vr);
+  if (n < desired) {
+    *reason = ds_insufficient_reason(t);
+    return KE_CODE_UNSCHEDULABLE;
+  }
+  for (int i = 0; i < n; i++) {
+    *out |= 1u << v.minor[picked[i]];
+    if (vf) vf[v.minor[picked[i]]] = (int8_t)vr[i];
+  }
+  return 0;
+}
+
+/* the PCIe ranks of the devices in `minors` that have a topology (newPreferredPCIes, :456-467) */
+static uint64_t pcie_set(const or_node* nd, int t, uint32_t minors) {
+  uint64_t r = 0;
+  for (int m = 0; m < KE_MAX_MINORS; m++) {
+    if (!((minors >> m) & 1u)) continue;
+    const ke_device* dv = dev_of(nd, t, m);
+    if (dv && dv->has_topology && dv->pcie_rank >= 0 && dv->pcie_rank < 64) r |= 1ull << dv->pcie_rank;
+  }
+  return r;
+}
+
+/* AutopilotAllocator.Allocate (device_allocator.go:96-138) on the devices the NUMA affinity / Selector leave:
+ * Prepare, tryJointAllocate (:205-299; primary type first, the secondary types preferring the primary's PCIe
+ * switches, SamePCIe validated) when more than one type is requested, then every other requested type in the
+ * fixed order GPU, RDMA, FPGA.  scorer NULL: Filter's allocator.  out[type] = minors, vf[type-1][minor] = VF
+ * ranks (optional). */
+static int ds_autopilot(const or_cluster* c, const or_node* nd, const ds_pod* d, ds_aff a,
+                        const ke_deviceshare_args* scorer, int reserve, uint32_t* out, int8_t (*vf)[KE_MAX_MINORS],
+                        int* reason) {
+  int inc[KE_DEV_TYPES], count[KE_DEV_TYPES], done[KE_DEV_TYPES] = {0, 0, 0};
+  for (int t = 0; t < KE_DEV_TYPES; t++) out[t] = 0;
+  int st = ds_node_prepare(nd, d, reserve, inc, count, reason);
+  if (st) return st;
+  const int n_inc = inc[0] + inc[1] + inc[2];
+  if (n_inc > 1 && d->joint_n > 0) {
+    const int p = d->joint[0];
+    st = ds_alloc_type(c, nd, d, p, &d->req[p], count[p], 0, a, scorer, &out[p], p ? vf[p - 1] : NULL, reason);
+    if (st) return st;
+    if (!out[p]) {
+      *reason = KE_REASON_DS_INSUFFICIENT_PRIMARY;
+      return KE_CODE_UNSCHEDULABLE;
+    }
+    done[p] = 1;
+    const uint64_t pcie = pcie_set(nd, p, out[p]);
+    for (int j = 1; j < d->joint_n; j++) {
+      const int t = d->joint[j];
+      int desired = count[t];
+      if (d->joint_pcie && desired < __builtin_popcountll(pcie)) desired = __builtin_popcountll(pcie);
+      const rl empty = rl_empty();
+      st = ds_alloc_type(c, nd, d, t, inc[t] ? &d->req[t] : &empty, desired, pcie, a, scorer, &out[t],
+                         t ? vf[t - 1] : NULL, reason);
+      if (st) return st;
+      done[t] = out[t] != 0;
+    }
+    if (d->joint_pcie)
+      for (int j = 1; j < d->joint_n; j++)
+        if (pcie_set(nd, d->joint[j], out[d->joint[j]]) != pcie) { /* validateJointAllocation */
+          *reason = KE_REASON_DS_JOINT_VIOLATION;
+          return KE_CODE_UNSCHEDULABLE;
+        }
+  }
+  for (int t = 0; t < KE_DEV_TYPES; t++) {
+    if (!inc[t] || done[t]) continue;
+    st = ds_alloc_type(c, nd, d, t, &d->req[t], count[t], 0, a, scorer, &out[t], t ? vf[t - 1] : NULL, reason);
+    if (st) return st;
+  }
+  return 0;
+}
+
+/* Filter's trial allocation: *gpu = the GPU minors */
+static int ds_try_allocate(const or_cluster* c, const or_node* nd, const ds_pod* d, ds_aff a, uint32_t* gpu,
+                           int* reason) {
+  uint32_t out[KE_DEV_TYPES];
+  int8_t vf[2][KE_MAX_MINORS];
+  const int st = ds_autopilot(c, nd, d, a, NULL, 0, out, vf, reason);
+  *gpu = st ? 0 : out[KE_DEV_GPU];
+  return st;
 }
 
 /* DeviceShare Filter (plugin.go:311-365): skipped when the topology manager stored an affinity for the
  * node (Admit ran DeviceShare.Allocate on it), else AutopilotAllocator.Allocate. */
 int or_ds_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* reason) {
   ds_pod d;
-  ds_prepare_pod(pod, &d);
+  ds_prepare_pod(c, pod, &d);
   if (d.status) {
-    *reason = KE_REASON_DS_INVALID_REQUEST;
+    *reason = d.status_reason ? d.status_reason : KE_REASON_DS_INVALID_REQUEST;
     return d.status;
   }
   const or_node* nd = &c->nodes[node];
@@ -2278,7 +2547,7 @@ int or_ds_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* reas
   if (!nd->has_dev_cache) return KE_CODE_SUCCESS;
   uint32_t gpu;
   int why = 0;
-  const int st = ds_try_allocate(nd, &d, NO_AFF, &gpu, &why);
+  const int st = ds_try_allocate(c, nd, &d, NO_AFF, &gpu, &why);
   if (st) *reason = why;
   return st;
 }
@@ -2294,7 +2563,7 @@ static int ds_numa_hints(const or_cluster* c, const or_node* nd, const ke_pod* p
   *copies = 0;
   *none = 1;
   ds_pod d;
-  ds_prepare_pod(pod, &d);
+  ds_prepare_pod(c, pod, &d);
   if (d.status || d.skip || !nd->has_dev_cache || c->cfg.deviceshare.disable_numa_alignment) return 0;
   int ids[KE_MAX_NUMA], k = 0; /* numaTopology.nodes: the NodeIDs of devices with a topology, -1 excluded */
   for (int i = 0; i < nd->n_dev; i++) {
@@ -2308,13 +2577,8 @@ static int ds_numa_hints(const or_cluster* c, const or_node* nd, const ke_pod* p
     k++;
   }
   if (k == 0) return 0; /* no mask to iterate: an empty hint map */
-  int prep = 0, prep_reason = 0; /* Prepare fails on every mask alike */
-  for (int t = 0; t < KE_DEV_TYPES && !prep; t++) {
-    if (!d.has[t]) continue;
-    ds_view v;
-    ds_orig_view(nd, t, &v);
-    if (v.n == 0) prep = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE, prep_reason = ds_insufficient_reason(t);
-  }
+  int prep_reason = 0, inc[KE_DEV_TYPES], cnt_t[KE_DEV_TYPES]; /* Prepare fails on every mask alike */
+  const int prep = ds_node_prepare(nd, &d, 0, inc, cnt_t, &prep_reason);
   static __thread uint32_t fmask[255], fgpu[255];
   int nf = 0, min_size = -1, full_st = 0, full_reason = 0;
   uint32_t best_gpu = 0;
@@ -2328,18 +2592,18 @@ static int ds_numa_hints(const or_cluster* c, const or_node* nd, const ke_pod* p
       uint32_t gpu = 0;
       if (!st) { /* calcTotalDevicesByNUMA: a requested type with devices there but too few */
         for (int t = 0; t < KE_DEV_TYPES && !st; t++) {
-          if (!d.has[t]) continue;
+          if (!inc[t]) continue;
           int cnt = 0;
           for (int i = 0; i < nd->n_dev; i++) {
             const ke_device* dv = &nd->dev[i];
             if (dv->type == t && dv->has_topology && dv->numa_node >= 0 && ((mask >> dv->numa_node) & 1u)) cnt++;
           }
-          if (cnt > 0 && cnt < d.count[t]) st = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE, why = KE_REASON_DS_INSUFFICIENT_NUMA_SCOPED;
+          if (cnt > 0 && cnt < cnt_t[t]) st = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE, why = KE_REASON_DS_INSUFFICIENT_NUMA_SCOPED;
         }
       }
       if (!st) {
         if (min_size < 0) min_size = k;
-        st = ds_try_allocate(nd, &d, (ds_aff){1, mask}, &gpu, &why);
+        st = ds_try_allocate(c, nd, &d, (ds_aff){1, mask}, &gpu, &why);
         if (!st) {
           fmask[nf] = mask;
           fgpu[nf] = gpu;
@@ -2364,7 +2628,7 @@ static int ds_numa_hints(const or_cluster* c, const or_node* nd, const ke_pod* p
     return full_st;
   }
   *none = 0;
-  for (int t = 0; t < KE_DEV_TYPES; t++) *copies += d.has[t];
+  for (int t = 0; t < KE_DEV_TYPES; t++) *copies += inc[t]; /* minAffinitySize: the types of requestsPerInstance */
   for (int i = 0; i < nf; i++) {
     numa_hint h = {fmask[i], __builtin_popcount(fmask[i]) == min_size, 0, fgpu[i] == best_gpu ? 500 : 0};
     list[(*n)++] = h;
@@ -2376,11 +2640,11 @@ static int ds_numa_hints(const or_cluster* c, const or_node* nd, const ke_pod* p
  * nodes (nil affinity: every device) must succeed. */
 static int ds_numa_allocate(const or_cluster* c, const or_node* nd, const ke_pod* pod, uint32_t affinity, int* reason) {
   ds_pod d;
-  ds_prepare_pod(pod, &d);
+  ds_prepare_pod(c, pod, &d);
   if (d.status || d.skip || !nd->has_dev_cache || c->cfg.deviceshare.disable_numa_alignment) return KE_CODE_SUCCESS;
   uint32_t gpu;
   int why = 0;
-  const int st = ds_try_allocate(nd, &d, (ds_aff){affinity != 0, affinity}, &gpu, &why);
+  const int st = ds_try_allocate(c, nd, &d, (ds_aff){affinity != 0, affinity}, &gpu, &why);
   if (st) *reason = why;
   return st;
 }
@@ -2416,18 +2680,18 @@ int or_ds_numa_allocate(const or_cluster* c, int32_t node, const ke_pod* pod, ui
  * device_allocator.go:469-492) for a node that passed Filter. */
 int64_t or_ds_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
   ds_pod d;
-  ds_prepare_pod(pod, &d);
+  ds_prepare_pod(c, pod, &d);
   const or_node* nd = &c->nodes[node];
   if (d.status || d.skip || !nd->has_dev_cache) return 0;
   uint32_t aff = 0; /* the stored affinity restricts the devices scored (scoring.go:63-73) */
   const ds_aff a = numa_stored_affinity(c, pod, node, &aff) ? (ds_aff){aff != 0, aff} : NO_AFF;
+  int inc[KE_DEV_TYPES], cnt[KE_DEV_TYPES], why = 0;
+  if (ds_node_prepare(nd, &d, 0, inc, cnt, &why)) return 0; /* Prepare error: Score returns 0 with an error status */
   int64_t s = 0;
   for (int t = 0; t < KE_DEV_TYPES; t++) {
-    if (!d.has[t]) continue;
+    if (!inc[t]) continue;
     ds_view v;
-    ds_orig_view(nd, t, &v);
-    if (v.n == 0) return 0; /* Prepare error: Score returns 0 with an error status */
-    ds_filtered_view_aff(nd, t, a, &v);
+    ds_filtered_view_aff(nd, &d, t, a, &v);
     if (v.present && v.n > 0) s += ds_score_node(&c->cfg.deviceshare, t, &d.req[t], &v);
   }
   return s;
@@ -2443,7 +2707,7 @@ static ds_aff ds_reserve_affinity(const or_cluster* c, const ke_pod* pod, int32_
              ? (ds_aff){aff != 0, aff} : NO_AFF;
 }
 
-static uint64_t ds_reserve_on(or_cluster* c, const ke_pod* pod, int32_t node, ds_aff a);
+static uint64_t ds_reserve_on(or_cluster* c, const ke_pod* pod, int32_t node, ds_aff a, int8_t (*vf_out)[KE_MAX_MINORS]);
 
 /* fillGPUTotalMem (devicehandler_gpu.go:98-125): the allocated instance's memory / memory ratio from the other
  * and the device's own gpu-memory total */
@@ -2462,64 +2726,79 @@ static void fill_gpu_total_mem(const ke_device* dev, rl* alloc) {
  * checked the devices of a node whose NUMA Admit stored an affinity (Filter skipped, Allocate a no-op) */
 static int ds_reserve_feasible(const or_cluster* c, const ke_pod* pod, int32_t node, ds_aff a) {
   ds_pod d;
-  ds_prepare_pod(pod, &d);
+  ds_prepare_pod(c, pod, &d);
   const or_node* nd = &c->nodes[node];
   if (d.status || d.skip || !nd->has_dev_cache) return 1;
-  uint32_t gpu;
+  uint32_t out[KE_DEV_TYPES];
+  int8_t vf[2][KE_MAX_MINORS];
   int why = 0;
-  return ds_try_allocate(nd, &d, a, &gpu, &why) == KE_CODE_SUCCESS;
+  return ds_autopilot(c, nd, &d, a, &c->cfg.deviceshare, 1, out, vf, &why) == KE_CODE_SUCCESS;
 }
 
 uint64_t or_ds_reserve(or_cluster* c, const ke_pod* pod, int32_t node) {
-  return ds_reserve_on(c, pod, node, ds_reserve_affinity(c, pod, node));
+  return ds_reserve_on(c, pod, node, ds_reserve_affinity(c, pod, node), NULL);
 }
 
-static uint64_t ds_reserve_on(or_cluster* c, const ke_pod* pod, int32_t node, ds_aff a) {
+/* Reserve: AutopilotAllocator.Allocate with the plugin's scorer in the Reserve phase, then updateCacheUsed
+ * (device_cache.go:132-209; VF allocations recorded per minor).  vf_out[type-1][minor] = the VF ranks. */
+static uint64_t ds_reserve_on(or_cluster* c, const ke_pod* pod, int32_t node, ds_aff a, int8_t (*vf_out)[KE_MAX_MINORS]) {
   ds_pod d;
-  ds_prepare_pod(pod, &d);
+  ds_prepare_pod(c, pod, &d);
   or_node* nd = &c->nodes[node];
   if (d.status || d.skip || !nd->has_dev_cache) return 0;
+  uint32_t out[KE_DEV_TYPES];
+  int8_t vf[2][KE_MAX_MINORS];
+  memset(vf, -1, sizeof vf);
+  int why = 0;
+  if (ds_autopilot(c, nd, &d, a, &c->cfg.deviceshare, 1, out, vf, &why)) return 0; /* passed Filter */
   uint64_t mask = 0;
   for (int t = 0; t < KE_DEV_TYPES; t++) {
-    if (!d.has[t]) continue;
     const int nk = nkeys(t);
-    ds_view v;
-    ds_filtered_view_aff(nd, t, a, &v);
-    int picked[KE_MAX_MINORS];
-    int n = 0;
-    if (t == KE_DEV_GPU) {
-      uint32_t gm = 0;
-      int reason = 0;
-      if (ds_gpu_allocate(nd, &d, &v, &c->cfg.deviceshare, &gm, &reason)) return mask; /* passed Filter */
-      for (int m = 0; m < KE_MAX_MINORS; m++) /* fillGPUTotalMem reads each allocated minor's own total */
-        if (gm & (1u << m)) picked[n++] = m;
-    } else {
-      n = ds_allocate(&c->cfg.deviceshare, t, &d.req[t], d.count[t], &v, picked);
-      if (n < d.count[t]) return mask; /* not reached for a node that passed Filter */
-      for (int i = 0; i < n; i++) picked[i] = v.minor[picked[i]];
-    }
-    for (int i = 0; i < n; i++) {
-      const int minor = picked[i];
-      rl alloc = d.req[t];
-      ke_device* dev = NULL;
-      for (int j = 0; j < nd->n_dev; j++)
-        if (nd->dev[j].type == t && nd->dev[j].minor == minor) dev = &nd->dev[j];
+    for (int minor = 0; minor < KE_MAX_MINORS; minor++) {
+      if (!((out[t] >> minor) & 1u)) continue;
+      /* the allocation's resources: the per-instance request (jointAllocate's secondary type outside
+       * requestsPerInstance allocates its nil request) */
+      rl alloc = d.has[t] ? d.req[t] : rl_empty();
+      ke_device* dev = (ke_device*)dev_of(nd, t, minor);
       if (t == KE_DEV_GPU) fill_gpu_total_mem(dev, &alloc);
       const rl u = rl_add(dev_used(dev, nk), alloc, nk);
       for (int k = 0; k < nk; k++) {
         dev->has_used[k] = u.has[k];
         dev->used[k] = u.v[k];
       }
+      if (t > 0 && vf[t - 1][minor] >= 0) dev->vf_allocated |= 1ull << vf[t - 1][minor];
       mask |= 1ull << (16 * t + minor);
     }
   }
+  if (vf_out) memcpy(vf_out, vf, sizeof vf);
   return mask;
 }
 
-/* preparePod outcome: status, skip, and per type (count, per-instance request [key] / presence) */
-int or_ds_prefilter(const ke_pod* pod, int* skip, int32_t* count, int64_t* req, uint8_t* req_has) {
+/* AutopilotAllocator.Allocate on `node` (golden-vector entry point: TestAutopilotAllocator calls it outside
+ * Reserve without a scorer): the status, the minors per type and the VF ranks ([type-1][minor]) */
+int or_ds_allocate(const or_cluster* c, const ke_pod* pod, int32_t node, int32_t reserve, int32_t scored,
+                   uint32_t* out3, int8_t* vf32, int32_t* reason) {
   ds_pod d;
-  ds_prepare_pod(pod, &d);
+  ds_prepare_pod(c, pod, &d);
+  *reason = 0;
+  for (int t = 0; t < KE_DEV_TYPES; t++) out3[t] = 0;
+  memset(vf32, -1, 2 * KE_MAX_MINORS);
+  if (d.status) {
+    *reason = d.status_reason ? d.status_reason : KE_REASON_DS_INVALID_REQUEST;
+    return d.status;
+  }
+  if (d.skip) return 0;
+  int why = 0;
+  const int st = ds_autopilot(c, &c->nodes[node], &d, NO_AFF, scored ? &c->cfg.deviceshare : NULL, reserve, out3,
+                              (int8_t(*)[KE_MAX_MINORS])vf32, &why);
+  *reason = why;
+  return st;
+}
+
+/* preparePod outcome: status, skip, and per type (count, per-instance request [key] / presence) */
+int or_ds_prefilter(const or_cluster* c, const ke_pod* pod, int* skip, int32_t* count, int64_t* req, uint8_t* req_has) {
+  ds_pod d;
+  ds_prepare_pod(c, pod, &d);
   *skip = d.skip;
   for (int t = 0; t < KE_DEV_TYPES; t++) {
     count[t] = d.has[t] ? d.count[t] : 0;
@@ -2567,7 +2846,42 @@ void or_destroy(or_cluster* c) {
   }
   free(c->nodes);
   free(c->quotas);
+  free(c->hints);
+  free(c->tmpl);
+  free(c->last_vf);
   free(c);
+}
+
+int or_set_pod_device_hints(or_cluster* c, int32_t n, const ke_pod_device_hints* hints) {
+  if (n < 0 || (n > 0 && !hints)) return KE_ERR_INVALID;
+  free(c->hints);
+  c->hints = (ke_pod_device_hints*)malloc(sizeof(ke_pod_device_hints) * (size_t)(n > 0 ? n : 1));
+  if (n) memcpy(c->hints, hints, sizeof(ke_pod_device_hints) * (size_t)n);
+  c->n_hints = n;
+  return KE_OK;
+}
+
+int or_gpu_templates_load(or_cluster* c, int32_t n, const ke_gpu_template* t) {
+  if (n < 0 || (n > 0 && !t)) return KE_ERR_INVALID;
+  free(c->tmpl);
+  c->tmpl = (ke_gpu_template*)malloc(sizeof(ke_gpu_template) * (size_t)(n > 0 ? n : 1));
+  if (n) memcpy(c->tmpl, t, sizeof(ke_gpu_template) * (size_t)n);
+  c->n_tmpl = n;
+  return KE_OK;
+}
+
+int or_node_device_flags(or_cluster* c, int32_t node, int32_t secondary_well_planned, int32_t gpu_model_key) {
+  if (node < 0 || node >= c->n) return KE_ERR_NOT_FOUND;
+  c->nodes[node].secondary_well_planned = secondary_well_planned != 0;
+  c->nodes[node].gpu_model_key = gpu_model_key;
+  return KE_OK;
+}
+
+int or_last_vf_ranks(const or_cluster* c, int32_t n, int8_t* out) {
+  for (int32_t p = 0; p < n; p++)
+    for (int k = 0; k < 2 * KE_MAX_MINORS; k++)
+      out[(int64_t)p * 2 * KE_MAX_MINORS + k] = p < c->last_vf_n && c->last_vf ? c->last_vf[(int64_t)p * 2 * KE_MAX_MINORS + k] : -1;
+  return KE_OK;
 }
 
 int or_quotas_load(or_cluster* c, const ke_quota_args* args, const ke_quota* q, int32_t n) {
@@ -2983,13 +3297,13 @@ static void eval_pair(const or_cluster* c, const ke_pod* pod, int32_t node, int6
   cpuset_state st;
   cpuset_prefilter(c, pod, &st);
   ds_pod d;
-  ds_prepare_pod(pod, &d);
+  ds_prepare_pod(c, pod, &d);
   if (!pod_requests_zero(pod) && st.invalid) {
     code = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
     reason = KE_REASON_NUMA_INVALID_REQUESTED_CPUS;
   } else if (d.status) {
     code = d.status;
-    reason = KE_REASON_DS_INVALID_REQUEST;
+    reason = d.status_reason ? d.status_reason : KE_REASON_DS_INVALID_REQUEST;
   }
   if (code == KE_CODE_SUCCESS) code = or_la_filter(c, pod, node, now, &reason);
   if (code == KE_CODE_SUCCESS) code = or_numa_filter(c, pod, node, &reason);
@@ -3046,7 +3360,7 @@ static int check_supported(const or_cluster* c, int32_t n_pods, const ke_pod* po
         pods[p].numa_exclusive < 0 || pods[p].numa_exclusive > KE_NUMA_EXCLUSIVE_REQUIRED)
       return KE_ERR_INVALID;
     ds_pod d;
-    ds_prepare_pod(&pods[p], &d);
+    ds_prepare_pod(c, &pods[p], &d);
     if (!d.skip && d.status == KE_CODE_SUCCESS) {
       ds = 1;
       if (pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE) numa = 1;
@@ -3120,6 +3434,10 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
   (void)n_threads;
 #endif
   if (numa_alloc) memset(numa_alloc, 0, sizeof(int64_t) * 16 * (size_t)n_pods);
+  free(c->last_vf);
+  c->last_vf = (int8_t*)malloc((size_t)(n_pods > 0 ? n_pods : 1) * 2 * KE_MAX_MINORS);
+  memset(c->last_vf, -1, (size_t)(n_pods > 0 ? n_pods : 1) * 2 * KE_MAX_MINORS);
+  c->last_vf_n = n_pods;
   eval_out* o = (eval_out*)malloc(sizeof(eval_out) * (size_t)(N > 0 ? N : 1));
   for (int p = 0; p < n_pods; p++) {
     /* ElasticQuota PreFilter (plugin.go:223-275): a refused pod is evaluated nowhere */
@@ -3153,7 +3471,7 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
        * framework assume: NodeInfo.Requested. */
       or_pod_assign(c, b, &pods[p], now);
       or_reserve_apply(c, b, &rp, numa_alloc ? numa_alloc + (int64_t)p * 16 : NULL);
-      mask = ds_reserve_on(c, &pods[p], b, da);
+      mask = ds_reserve_on(c, &pods[p], b, da, (int8_t(*)[KE_MAX_MINORS])(c->last_vf + (int64_t)p * 2 * KE_MAX_MINORS));
       c->nodes[b].node.requested[KE_RES_CPU] += pods[p].requests[KE_RES_CPU];
       c->nodes[b].node.requested[KE_RES_MEMORY] += pods[p].requests[KE_RES_MEMORY];
       /* NodeInfo (NonZero)Requested of every resource the pod requests (NodeResourcesFitPlus reads them) */
@@ -3236,12 +3554,14 @@ int or_pod_release(or_cluster* c, const ke_pod* pod, const ke_pod_allocation* a,
     }
     if (n->has_dev_cache && a->device_minors) {
       ds_pod d;
-      ds_prepare_pod(pod, &d);
+      ds_prepare_pod(c, pod, &d);
       for (int i = 0; i < n->n_dev; i++) {
         ke_device* dv = &n->dev[i];
         if (!(a->device_minors >> (16 * dv->type + dv->minor) & 1)) continue;
         const int t = dv->type, nk = nkeys(t);
-        rl alloc = d.req[t];
+        if (t > 0 && a->vf_rank[t - 1][dv->minor] >= 0) /* removeVFAllocations */
+          dv->vf_allocated &= ~(1ull << a->vf_rank[t - 1][dv->minor]);
+        rl alloc = d.has[t] ? d.req[t] : rl_empty();
         if (t == KE_DEV_GPU) fill_gpu_total_mem(dv, &alloc);
         rl used = rl_sub_nonneg(dev_used(dv, nk), alloc, nk);
         if (rl_is_zero(used, nk)) used = rl_empty();

@@ -39,6 +39,14 @@ int or_node_devices_delete(or_cluster* c, int32_t node);
 int or_node_resources_set(or_cluster* c, int32_t node, int32_t n, const ke_node_resource* res);
 int64_t or_fitplus_score(const or_cluster* c, const ke_pod* pod, int32_t node);
 int64_t or_sra_score(const or_cluster* c, const ke_pod* pod, int32_t node);
+/* DeviceShare hints / templates / node device flags / VF ranks of the last or_schedule (ke_set_pod_device_hints,
+ * ke_gpu_templates_load, ke_node_device_flags, ke_pod_allocation.vf_rank) */
+int or_set_pod_device_hints(or_cluster* c, int32_t n, const ke_pod_device_hints* hints);
+int or_gpu_templates_load(or_cluster* c, int32_t n, const ke_gpu_template* t);
+int or_node_device_flags(or_cluster* c, int32_t node, int32_t secondary_well_planned, int32_t gpu_model_key);
+int or_ds_allocate(const or_cluster* c, const ke_pod* pod, int32_t node, int32_t reserve, int32_t scored,
+                   uint32_t* out3, int8_t* vf32, int32_t* reason);
+int or_last_vf_ranks(const or_cluster* c, int32_t n, int8_t* out /* [n][2][KE_MAX_MINORS] */);
 int or_node_gpu_partitions(or_cluster* c, int32_t node, int32_t has_table, int32_t honor, int32_t n,
                            const ke_gpu_partition* parts);
 
@@ -49,7 +57,7 @@ int or_numa_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* re
 int64_t or_numa_score(const or_cluster* c, const ke_pod* pod, int32_t node);
 /* DeviceShare: PreFilter status (0 or UnschedulableAndUnresolvable) and skip; Filter; raw Score
  * (before NormalizeScore); Reserve (mutates the device cache, returns the minor mask 1<<(16*type+minor)). */
-int or_ds_prefilter(const ke_pod* pod, int* skip, int32_t* count /*[3]*/, int64_t* req /*[3][3]*/,
+int or_ds_prefilter(const or_cluster* c, const ke_pod* pod, int* skip, int32_t* count /*[3]*/, int64_t* req /*[3][3]*/,
                     uint8_t* req_has /*[3][3]*/);
 int64_t or_ds_score_device(const or_cluster* c, int32_t type, const int64_t* req, const uint8_t* req_has,
                            const int64_t* total, const uint8_t* total_has, const int64_t* free,

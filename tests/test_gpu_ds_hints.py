@@ -1,0 +1,129 @@
+"""DeviceShare hints on the GPU path against the oracle: the reference's hint vectors
+(tests/golden/ds_hints.json) and randomized clusters with device labels, SR-IOV VF groups, well-planned
+secondary devices and pods with Selectors, VFSelectors, ApplyForAll / RequestsAsCount (DeviceLevel), joint
+GPU+RDMA allocation (SamePCIe) — eval matrices, placements, device minors, VF ranks, every node's device state,
+and Unreserve of a part of the queue followed by more scheduling."""
+import numpy as np
+import pytest
+
+import cases
+import ds_hint_cases as dh
+from koordinator_amd import Evaluator, abi, decode, synth
+from oracle.binding import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def same_devices(ev, o, n):
+    for i in range(n):
+        d1, d0 = ev.node_state(i)[3], o.node_state(i)[3]
+        for k in ("has_used", "used", "vf_allocated"):
+            assert np.array_equal(d1[k], d0[k]), (i, k)
+
+
+@pytest.mark.parametrize("case", dh.HINTS, ids=lambda c: c["name"])
+def test_golden_hint_cases(gpu, case):
+    cfg = abi.default_config(2)
+    ev, o = Evaluator(cfg), Oracle(cfg, 2)
+    pod, hint = dh.pod_and_hints(case)
+    for h in (ev, o):
+        dh.node_cluster(h, 2)
+        dh.build(h, case, 0)
+        dh.build(h, case, 1)
+        h.set_pod_device_hints([hint])
+    a, b = ev.eval([pod], cases.NOW), o.eval([pod], cases.NOW)
+    for k in ("status", "reason", "ds", "total", "best"):
+        assert np.array_equal(a[k], b[k]), k
+    c1, s1 = ev.schedule([pod, pod], cases.NOW)
+    c0, s0 = o.schedule([pod, pod], cases.NOW)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    a1, a0 = ev.last_allocations(), o.last_allocations()
+    assert np.array_equal(a1["device_minors"], a0["device_minors"])
+    assert np.array_equal(a1["vf_rank"], a0["vf_rank"])
+    same_devices(ev, o, 2)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_hint_queue(gpu, seed):
+    rng = np.random.default_rng(synth.BASE_SEED + 900 + seed)
+    n = 60
+    cl = synth.make_cluster(n, synth.BASE_SEED + 910 + seed)
+    cfg = synth.config(n)
+    ev, o = Evaluator(cfg), Oracle(cfg, n)
+    crs = [dh.random_device_cr(rng) for _ in range(n)]
+    planned = rng.random(n) < 0.3
+    pods, table = dh.random_hint_queue(rng, 160, 70_000_000 + 1000 * seed)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        for i in range(n):
+            devs, (ht, hon, parts) = decode.decode_device(crs[i])
+            h.set_devices(i, devs)
+            h.set_gpu_partitions(i, ht, hon, parts)
+            h.set_device_flags(i, bool(planned[i]), 0)
+        h.set_pod_device_hints(table)
+    a, b = ev.eval(pods[:24], synth.T0), o.eval(pods[:24], synth.T0)
+    for k in ("status", "reason", "ds", "total", "best"):
+        assert np.array_equal(a[k], b[k]), k
+    first, more = pods[:100], pods[100:]
+    c1, s1 = ev.schedule(first, synth.T0)
+    c0, s0 = o.schedule(first, synth.T0)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5].ravel().tolist()
+    assert np.array_equal(s1, s0)
+    a1, a0 = ev.last_allocations(), o.last_allocations()
+    for k in ("device_minors", "vf_rank"):
+        assert np.array_equal(a1[k], a0[k]), k
+    assert (a1["vf_rank"] >= 0).any() and (c1 >= 0).sum() > 30
+    same_devices(ev, o, n)
+    for p in np.nonzero(c1 >= 0)[0][::4]:  # Unreserve a quarter: used and VFs return
+        ev.unreserve(first[p], int(p))
+        o.release(first[p], a0[p])
+    same_devices(ev, o, n)
+    c1, s1 = ev.schedule(more, synth.T0)
+    c0, s0 = o.schedule(more, synth.T0)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    same_devices(ev, o, n)
+    assert ev.check_records(synth.T0) == 0
+
+
+def test_gpu_templates(gpu):
+    """allocateByTemplate (allocator_gpu.go:135-159): one candidate template of the node's GPU model ->
+    generalAllocate, none -> UnschedulableAndUnresolvable, several -> the partition path; no template of any
+    model -> PreFilter fails (utils.go:508-515)."""
+    from koordinator_amd import model
+    n = 6
+    cfg = abi.default_config(n)
+    cfg.deviceshare.template_matched_keys = abi.TEMPLATE_KEY_CORE | abi.TEMPLATE_KEY_MEMORY_RATIO
+    ev, o = Evaluator(cfg), Oracle(cfg, n)
+    rng = np.random.default_rng(5)
+    tmpl = [model.make_gpu_template("nvidia-A100", "half", {"koordinator.sh/gpu-core": "50",
+                                                            "koordinator.sh/gpu-memory-ratio": "50"}),
+            model.make_gpu_template("nvidia-H100", "half", {"koordinator.sh/gpu-core": "50",
+                                                            "koordinator.sh/gpu-memory-ratio": "50"}),
+            model.make_gpu_template("nvidia-H100", "half-b", {"koordinator.sh/gpu-core": "50",
+                                                              "koordinator.sh/gpu-memory-ratio": "50"}),
+            model.make_gpu_template("nvidia-A100", "quarter", {"koordinator.sh/gpu-core": "25",
+                                                               "koordinator.sh/gpu-memory-ratio": "25"})]
+    keys = [decode.label_id(k) for k in ("nvidia-A100", "nvidia-H100", "nvidia-L4")]
+    for h in (ev, o):
+        dh.node_cluster(h, n)
+        h.gpu_templates_load(tmpl)
+        for i in range(n):
+            devs, (ht, hon, parts) = decode.decode_device(dh.random_device_cr(rng, vf_fraction=0))
+            h.set_devices(i, devs)
+            h.set_gpu_partitions(i, True, i % 2 == 0, model.make_gpu_partitions(model.HOPPER_PARTITIONS))
+            h.set_device_flags(i, False, keys[i % 3])
+    pods = []
+    for i, (core, ratio) in enumerate([(50, 50), (25, 25), (50, 50), (30, 30), (25, 25), (50, 50)] * 3):
+        p = model.make_pod(name=f"t{i}", requests={"koordinator.sh/gpu-core": str(core),
+                                                   "koordinator.sh/gpu-memory-ratio": str(ratio), "cpu": "1"})
+        p.uid = 80_000_000 + i
+        pods.append(p)
+    a, b = ev.eval(pods, cases.NOW), o.eval(pods, cases.NOW)
+    for k in ("status", "reason", "ds", "total", "best"):
+        assert np.array_equal(a[k], b[k]), k
+    assert (a["reason"] == abi.REASON_DS_NO_MATCHED_TEMPLATE).any()
+    c1, s1 = ev.schedule(pods, cases.NOW)
+    c0, s0 = o.schedule(pods, cases.NOW)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    assert np.array_equal(ev.last_device_allocations, o.last_device_allocations)
+    same_devices(ev, o, n)

@@ -155,23 +155,28 @@ def _unsupported(fn, *args):
 GPU2 = {"nvidia.com/gpu": "2"}
 
 
-@pytest.mark.parametrize("kind", ["joint", "vf", "selector", "strategy", "exclusive"])
-def test_unmodelled_device_annotations_are_refused(kind):
-    """annotations whose allocation path is not implemented fail loudly instead of being
-    evaluated on the default path (device_allocator.go:74-138,205-300,396-460; devicehandler_default.go:58-90)."""
+@pytest.mark.parametrize("kind", ["gpu_vf", "gpu_secondary", "three_types", "bad_index"])
+def test_unmodelled_device_hints_are_refused(kind):
+    """The DeviceShare hint paths outside the modelled allocator fail loudly: a VFSelector on the gpu type
+    (defaultAllocateDevices' GPU VFs), a joint allocation with the gpu type after the primary or over three
+    types (device_allocator.go:205-300), and a hint index outside the table."""
     ev = Evaluator(abi.default_config(4))
     ev.upsert_node(0, model.make_node(allocatable={"cpu": "8", "memory": "8Gi"}))
     req = dict(GPU2, **{"koordinator.sh/rdma": "1"})
-    pod = {
-        "joint": lambda: model.make_pod(requests=req, device_joint_allocate={"deviceTypes": ["gpu", "rdma"]}),
-        "vf": lambda: model.make_pod(requests=req, device_hints={"rdma": {"vfSelector": {"matchLabels": {"t": "a"}}}}),
-        "selector": lambda: model.make_pod(requests=GPU2, device_hints={"gpu": {"selector": {"matchLabels": {}}}}),
-        "strategy": lambda: model.make_pod(requests=req, device_hints={"rdma": {"allocateStrategy": "ApplyForAll"}}),
-        "exclusive": lambda: model.make_pod(requests=req,
-                                            device_hints={"rdma": {"exclusivePolicy": "PCIeLevel"}}),
-    }[kind]()
-    _unsupported(ev.eval, [pod], cases.NOW)
-    _unsupported(ev.schedule, [pod], cases.NOW)
+    hints, joint = {}, None
+    if kind == "gpu_vf":
+        hints = {"gpu": {"vfSelector": {}}}
+    elif kind == "gpu_secondary":
+        joint = {"deviceTypes": ["rdma", "gpu"]}
+    elif kind == "three_types":
+        req["koordinator.sh/fpga"] = "1"
+        joint = {"deviceTypes": ["gpu", "rdma", "fpga"]}
+    pod = model.make_pod(requests=req, device_hints=hints)
+    ev.set_pod_device_hints([model.make_device_hints(hints, joint)])
+    pod.device_hint = 5 if kind == "bad_index" else 1
+    with pytest.raises(KoordEvalError) as e:
+        ev.schedule([pod], cases.NOW)
+    assert e.value.code == (abi.ERR_INVALID if kind == "bad_index" else abi.ERR_UNSUPPORTED), str(e.value)
 
 
 def test_joint_allocate_of_one_requested_type_is_dropped():
@@ -181,22 +186,6 @@ def test_joint_allocate_of_one_requested_type_is_dropped():
     assert pod.device_joint_allocate == 0
     pod = model.make_pod(requests=GPU2, device_hints={"gpu": {"requiredTopologyScope": "PCIe"}})
     assert pod.device_hints == 0 and pod.gpu_required_topology_scope == abi.SCOPE_PCIE
-
-
-def test_gpu_shared_templates_are_refused():
-    """allocateByTemplate (allocator_gpu.go:135-159): a shared-GPU pod naming a template-matched resource."""
-    cfg = abi.default_config(4)
-    cfg.deviceshare.template_matched_keys = abi.TEMPLATE_KEY_CORE
-    ev = Evaluator(cfg)
-    ev.upsert_node(0, model.make_node(allocatable={"cpu": "8", "memory": "8Gi"}))
-    shared = model.make_pod(requests={"koordinator.sh/gpu.shared": "1", "koordinator.sh/gpu-core": "50",
-                                      "koordinator.sh/gpu-memory-ratio": "50"})
-    _unsupported(ev.eval, [shared], cases.NOW)
-    _unsupported(ev.schedule, [shared], cases.NOW)
-    whole = model.make_pod(requests=GPU2)  # not shared: no template enforced
-    with pytest.raises(KoordEvalError) as e:
-        ev.eval([whole], cases.NOW)
-    assert e.value.code in (abi.ERR_NO_DEVICE, abi.OK)
 
 
 @pytest.mark.parametrize("which", ["loadaware", "numa", "deviceshare"])
