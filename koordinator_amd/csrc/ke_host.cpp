@@ -695,8 +695,9 @@ DevPod make_dev_pod(const ke_config& cfg, const ke_pod& pod, const ke_pod_device
   int invalid = 0;  // the PreFilter failure's reason (PF_DS_INVALID; DevPod::ds_req[0] carries it)
   if (!ds_prepare(pod, d, hints)) invalid = KE_REASON_DS_INVALID_REQUEST;
   const bool requests = d.ds_cnt[0] || d.ds_cnt[1] || d.ds_cnt[2];
-  if (!invalid && requests && hints) {
-    if (hints->invalid) invalid = KE_REASON_DS_INVALID_HINT;  // newHintSelectors (utils.go:420-423)
+  bool tmpl_pod = false;  // enforceGPUSharedResourceTemplate: the hinted path allocates it (DevPodHint PH_TMPL)
+  if (!invalid && requests) {
+    if (hints && hints->invalid) invalid = KE_REASON_DS_INVALID_HINT;  // newHintSelectors (utils.go:420-423)
     // parseGPURequirements: no template of any GPU model equal to the request (utils.go:508-515)
     const uint32_t keys = cfg.deviceshare.template_matched_keys;
     uint32_t named = 0;
@@ -704,12 +705,13 @@ DevPod make_dev_pod(const ke_config& cfg, const ke_pod& pod, const ke_pod_device
     if (d.flags & PF_DS_H_RATIO) named |= KE_TEMPLATE_KEY_MEMORY_RATIO;
     else if (d.flags & PF_DS_H_MEM) named |= KE_TEMPLATE_KEY_MEMORY;
     if (!invalid && d.ds_cnt[KE_DEV_GPU] && (d.flags & PF_GPU_SHARED) && (named & keys)) {
+      tmpl_pod = true;
       bool any = false;
       for (const ke_gpu_template& t : tmpl ? *tmpl : std::vector<ke_gpu_template>{})
         any = any || (t.has[0] == ((named & KE_TEMPLATE_KEY_CORE) != 0) && t.has[1] == ((named & KE_TEMPLATE_KEY_MEMORY) != 0) &&
                       t.has[2] == ((named & KE_TEMPLATE_KEY_MEMORY_RATIO) != 0) && (!t.has[0] || t.value[0] == d.ds_req[0]) &&
                       (!t.has[1] || t.value[1] == d.ds_req[1]) && (!t.has[2] || t.value[2] == d.ds_req[2]));
-      if (!any) invalid = KE_REASON_DS_NO_MATCHED_TEMPLATE;
+      if (tmpl && !any) invalid = KE_REASON_DS_NO_MATCHED_TEMPLATE;  // (release records: no check)
     }
   }
   if (invalid) {
@@ -719,7 +721,7 @@ DevPod make_dev_pod(const ke_config& cfg, const ke_pod& pod, const ke_pod_device
     d.flags = f | PF_DS_INVALID;
   } else if (requests) {
     d.flags |= PF_DS;
-    if (hints) d.flags |= PF_DS_HINT;  // DevPod::ring_bw becomes the hint slot at upload
+    if (hints || tmpl_pod) d.flags |= PF_DS_HINT;  // DevPod::ring_bw becomes the hint slot at upload
   }
   if (pod.quota_non_preemptible) d.flags |= PF_QUOTA_NP;
   // NodeResourcesFitPlus / ScarceResourceAvoidance PreScore: requested names and the FitPlus requests by slot

@@ -5551,8 +5551,9 @@ static int upload_pods(Context* ctx, int32_t n_pods, const ke_pod* pods) {
     const ke_pod_device_hints* h = pod_hints(*ctx, pods[p]);
     dp[p] = make_dev_pod(ctx->cfg, pods[p], h, &ctx->tmpl);
     if (ctx->n_bind_nodes > 0 && dp[p].req[0] > 0) dp[p].flags |= PF_CPUSET;  // a node policy may bind it
-    if (dp[p].flags & PF_DS_HINT) {
-      ph.push_back(make_pod_hint(*ctx, pods[p], dp[p], *h));
+    if (dp[p].flags & PF_DS_HINT) {  // hints, or a pod allocated by GPU shared resource template
+      static const ke_pod_device_hints none{};
+      ph.push_back(make_pod_hint(*ctx, pods[p], dp[p], h ? *h : none));
       dp[p].ring_bw = (int64_t)ph.size() - 1;
     }
   }

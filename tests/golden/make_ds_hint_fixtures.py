@@ -113,6 +113,25 @@ for name, lines, q, hint, want_count, want_per, ok in (
                   "requests": {"koordinator.sh/rdma": q}, "hints": {"rdma": hint} if hint else None,
                   "want": {"count": want_count, "per_device": want_per, "ok": ok}})
 
+# DeviceShare's NUMA hints (topology_hint_test.go:128-212, fakeDeviceCR): [mask, preferred, score] per hint,
+# one list per requested type (copies); GPU requests gpu-core 100 + gpu-memory-ratio 100, RDMA requests rdma 2
+TH = "pkg/scheduler/plugins/deviceshare/topology_hint_test.go"
+ONE, TWO, BOTH = 1, 2, 3
+for name, lines, req, hint, joint, copies, want in (
+        ("numa_hints_2_rdma", "128-145", {"koordinator.sh/rdma": "2"}, {"rdma": {"allocateStrategy": "RequestsAsCount"}},
+         None, 1, [[ONE, True, 500], [TWO, True, 500], [BOTH, False, 500]]),
+        ("numa_hints_rdma_2_vf", "146-164", {"koordinator.sh/rdma": "2"},
+         {"rdma": {"vfSelector": {}, "allocateStrategy": "RequestsAsCount"}}, None, 1,
+         [[ONE, True, 500], [TWO, True, 500], [BOTH, False, 500]]),
+        ("numa_hints_rdma_4_vf", "165-183", {"koordinator.sh/rdma": "4"},
+         {"rdma": {"vfSelector": {}, "allocateStrategy": "RequestsAsCount"}}, None, 1, [[BOTH, True, 500]]),
+        ("numa_hints_joint_gpu_rdma", "184-208", {"koordinator.sh/rdma": "2", "koordinator.sh/gpu-core": "100",
+                                                  "koordinator.sh/gpu-memory-ratio": "100"},
+         {"rdma": {"vfSelector": {}}}, {"deviceTypes": ["gpu", "rdma"]}, 2,
+         [[ONE, True, 500], [TWO, True, 0], [BOTH, False, 500]])):
+    cases.append({"name": name, "source": f"{TH}:{lines}", "kind": "numa_hints", "device": fake_device_cr(),
+                  "requests": req, "hints": hint, "joint": joint, "want": {"copies": copies, "hints": want}})
+
 if __name__ == "__main__":
     with open(os.path.join(HERE, "ds_hints.json"), "w") as f:
         json.dump({"source": "make_ds_hint_fixtures.py", "cases": cases}, f, indent=1)

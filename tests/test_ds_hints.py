@@ -72,3 +72,16 @@ def test_hints_decode_like_the_model(lib):
                                       {"metadata": {"labels": {"node.koordinator.sh/gpu-vendor": "nvidia",
                                                                "node.koordinator.sh/gpu-model": "A100"}}})
     assert w and k == decode.label_id("nvidia-A100")
+
+
+@pytest.mark.parametrize("case", [c for c in dh.HINTS if c["kind"] == "numa_hints"], ids=lambda c: c["name"])
+def test_numa_hints_with_device_hints(lib, case):
+    o = Oracle(abi.default_config(1), 1)
+    dh.node_cluster(o)
+    dh.build(o, case)
+    pod, hint = dh.pod_and_hints(case)
+    o.set_pod_device_hints([hint])
+    st, reason, none, copies, hints = o.ds_numa_hints(pod, 0)
+    assert st == 0 and not none, (case["source"], reason)
+    assert copies == case["want"]["copies"], case["source"]
+    assert [list(h) for h in hints] == case["want"]["hints"], case["source"]

@@ -127,3 +127,38 @@ def test_gpu_templates(gpu):
     assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
     assert np.array_equal(ev.last_device_allocations, o.last_device_allocations)
     same_devices(ev, o, n)
+
+
+@pytest.mark.parametrize("policy", [abi.NUMA_POLICY_BEST_EFFORT, abi.NUMA_POLICY_RESTRICTED,
+                                    abi.NUMA_POLICY_SINGLE_NUMA_NODE])
+def test_hinted_pods_under_numa_policies(gpu, policy):
+    """DeviceShare with hints as the second NUMA hint provider (topology_hint.go:38-236): RequestsAsCount / VF /
+    joint pods on 2-zone nodes under each policy — Admit, the stored affinity's allocation, Reserve."""
+    from koordinator_amd import model
+    n = 8
+    cfg = abi.default_config(n)
+    ev, o = Evaluator(cfg), Oracle(cfg, n)
+    rng = np.random.default_rng(11 + policy)
+    crs = [dh.random_device_cr(rng) for _ in range(n)]
+    zones = model.make_zones([{"id": z, "cpu": "48", "memory": "256Gi"} for z in range(2)])
+    pods, table = dh.random_hint_queue(rng, 40, 90_000_000 + 100 * policy)
+    for h in (ev, o):
+        for i in range(n):
+            node = model.make_node(allocatable={"cpu": "96", "memory": "512Gi"})
+            node.numa_topology_policy = policy
+            h.upsert_node(i, node)
+            h.set_numa(i, zones)
+            devs, (ht, hon, parts) = decode.decode_device(crs[i])
+            h.set_devices(i, devs)
+            h.set_gpu_partitions(i, ht, hon, parts)
+        h.set_pod_device_hints(table)
+    a, b = ev.eval(pods[:16], cases.NOW), o.eval(pods[:16], cases.NOW)
+    for k in ("status", "reason", "ds", "numa", "total", "best"):
+        assert np.array_equal(a[k], b[k]), k
+    c1, s1 = ev.schedule(pods, cases.NOW)
+    c0, s0 = o.schedule(pods, cases.NOW)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    a1, a0 = ev.last_allocations(), o.last_allocations()
+    for k in ("device_minors", "vf_rank", "numa"):
+        assert np.array_equal(a1[k], a0[k]), k
+    same_devices(ev, o, n)
