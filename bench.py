@@ -11,7 +11,7 @@ one workgroup, per-batch time from in-kernel s_memrealtime stamps); eval, select
 on the second stream.  `roofline.achieved` = SURVEY.md §8(d)'s algorithmic bytes of a batch (N*S_row +
 B*S_pod + B*k*12) over that critical path; `roofline.replay` the replay's own bytes, `roofline.kernels`
 every kernel of a batch and `roofline.end_to_end` the whole step, each against 8 TB/s.
-`traffic` = HBM bytes from a prior rocprofv3 PMC pass of this workload (profiles/r02/pmc_bench.json).
+`traffic` = HBM bytes from a prior rocprofv3 PMC pass of this workload (profiles/r03/pmc_bench.json).
 
 cpu_baseline: the oracle (C restatement of the Go plugins, oracle/) scheduling a prefix of the same
 queue on the host's cores at 1 thread, 16 threads (upstream Parallelism) and every usable core.
@@ -64,10 +64,19 @@ def sizes():
     return lib.ke_row_bytes(), lib.ke_pod_record_bytes()
 
 
+REC_EVAL = 13 * 16  # the replay record k_eval_plain reads per node (13 16-byte loads)
+
+
+def eval_kernel(b):
+    """the eval kernel a plain batch of b pods launches (ke_kernels.hip use_record_eval)"""
+    return "k_eval_plain" if b > 2 else "k_eval_batch"
+
+
 def eval_bytes(n_nodes, b):
-    """algorithmic bytes of one eval-kernel launch: the node SoA once, the pod batch, the score output"""
+    """algorithmic bytes of one eval-kernel launch: per node the SoA row (k_eval_batch) or the replay record
+    (k_eval_plain), the pod batch, the score output"""
     row, pod = sizes()
-    return n_nodes * row + b * pod + b * n_nodes * 2
+    return n_nodes * (REC_EVAL if b > 2 else row) + b * pod + b * n_nodes * 2
 
 
 def batch_bytes(n_nodes, b, fetched, changed, pipelined):
@@ -76,7 +85,7 @@ def batch_bytes(n_nodes, b, fetched, changed, pipelined):
     row, pod = sizes()
     L = KSTALE if pipelined else KMAX
     return {
-        "k_eval_batch": eval_bytes(n_nodes, b),
+        eval_kernel(b): eval_bytes(n_nodes, b),
         "k_select": b * n_nodes * 2 + b * (L + 1) * CAND_BYTES,
         "k_fixup": (b * ((L + 1) * CAND_BYTES + pod + (KMAX + 1) * CAND_BYTES) + changed * REC_FULL) if pipelined else 0,
         "k_resolve": b * ((KMAX + 1) * CAND_BYTES + pod + OUT_BYTES) + fetched * REC_READ
@@ -86,10 +95,10 @@ def batch_bytes(n_nodes, b, fetched, changed, pipelined):
 
 def pmc_traffic(tag):
     """HBM bytes per launch by kernel from the committed PMC passes (tools/pmc_bench.sh, summarised by
-    tools/pmc_summary.py into profiles/r02/pmc_bench.json) of this workload.  Counter collection serialises
+    tools/pmc_summary.py into profiles/r03/pmc_bench.json) of this workload.  Counter collection serialises
     dispatches, which the persistent Reserve chain cannot run under, so the passes run the one-stream
     schedule (tag suffix _serial): its k_eval_batch / k_select / k_resolve launches do the same work per batch."""
-    f = os.path.join(ROOT, "profiles", "r02", "pmc_bench.json")
+    f = os.path.join(ROOT, "profiles", "r03", "pmc_bench.json")
     if not os.path.exists(f):
         return {}, None
     d = json.load(open(f))
@@ -165,7 +174,7 @@ def roofline(n_nodes, b, ks, dt_step, batches_per_step, pipelined, tag):
     """§8(d) roofline of a batch over its critical path (the Reserve chain: replay + hand-off per batch), with
     the replay's own bytes, the per-kernel and the end-to-end fractions as sub-fields."""
     by = batch_bytes(n_nodes, b, ks["rows_fetched"], ks["rows_changed"], pipelined)
-    ms = {"k_eval_batch": ks["eval_ms"], "k_select": ks["select_ms"], "k_fixup": ks["fixup_ms"],
+    ms = {eval_kernel(b): ks["eval_ms"], "k_select": ks["select_ms"], "k_fixup": ks["fixup_ms"],
           "k_resolve": ks["resolve_ms"]}
     traffic, src = pmc_traffic(tag)
     kern = {}
@@ -191,7 +200,7 @@ def roofline(n_nodes, b, ks, dt_step, batches_per_step, pipelined, tag):
             "replay": {"bytes_per_batch": dom["bytes_per_batch"], "ms_per_batch": dom["ms_per_batch"],
                        "achieved": dom["achieved"], "frac": dom["frac"], "traffic": dom["traffic"]},
             "timing": "k_resolve / k_fixup: in-kernel s_memrealtime per batch (one persistent launch per run); "
-                      "k_eval_batch / k_select: HIP events on the eval stream",
+                      "k_eval_plain / k_eval_batch / k_select: HIP events on the eval stream",
             "kernels": kern,
             "end_to_end": {"bytes_per_step": step_bytes, "ms_per_step": dt_step * 1e3,
                            "achieved": step_bytes / dt_step / 1e9, "frac": step_bytes / dt_step / 1e9 / HBM_PEAK_GBS},

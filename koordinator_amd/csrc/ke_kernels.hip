@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "ke_cpuacc.h"
+#include "ke_merge.h"
 #include "ke_host.h"
 #include "ke_types.h"
 
@@ -81,7 +82,7 @@ struct SoA {
 };
 constexpr int DSB_MAX = 0, DSB_CNT = 64, DSB_CUT = 128, DSB_WORDS = 129;
 // kerr bits: an input the kernels refuse mid-call (the call returns KE_ERR_UNSUPPORTED)
-constexpr int32_t KERR_DS_MERGE = 1;  // a DeviceShare BestEffort merge beyond the permutation budget
+constexpr int32_t KERR_HINT_ROUTE = 2;  // a hinted pod reached a kernel instantiated without the hint path (H)
 
 // ---------------------------------------------------------------------------------------------
 // ElasticQuota PreFilter / Reserve (elasticquota/plugin.go:223-275,345-359; plugin_helper.go:281-301;
@@ -752,14 +753,28 @@ __device__ __forceinline__ uint64_t dsxw(const SoA& s, int w, int64_t i);
 // AutopilotAllocator.Allocate (device_allocator.go:87-135) on the devices the affinity leaves: Prepare (a
 // requested type without devices in the cache), then every requested type in the fixed order GPU, RDMA,
 // FPGA.  *gpu = the GPU minors (no scorer) when `gpu` is given.
+// H: the hint path is compiled in (hinted pods run only in kernels instantiated with H; elsewhere a hinted pod
+// is an internal routing error: KERR_HINT_ROUTE, the call fails loudly).  Keeping hint_allocate / hint_score
+// out of the batch kernels keeps them free of call frames and scratch.
+__device__ __forceinline__ bool hint_misrouted(const SoA& s, const DevPod& p) {
+  if (!(p.flags & PF_DS_HINT)) return false;
+  __hip_atomic_fetch_or(s.kerr, KERR_HINT_ROUTE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+template <bool H = true>
 __device__ int ds_try_allocate(const SoA& s, int64_t i, const DevPod& p, const KArgs& k, DsAff a, uint32_t* gpu,
                                int* reason) {
-  if (p.flags & PF_DS_HINT) {  // Filter's trial allocation (no scorer, Prepare outside Reserve)
-    uint32_t out[3];
-    int8_t vf[2][DS_MINORS];
-    const int st = hint_allocate(s, i, p, k, a, false, false, out, vf, reason);
-    if (gpu) *gpu = st ? 0u : out[KE_DEV_GPU];
-    return st;
+  if constexpr (H) {
+    if (p.flags & PF_DS_HINT) {  // Filter's trial allocation (no scorer, Prepare outside Reserve)
+      uint32_t out[3];
+      int8_t vf[2][DS_MINORS];
+      const int st = hint_allocate(s, i, p, k, a, false, false, out, vf, reason);
+      if (gpu) *gpu = st ? 0u : out[KE_DEV_GPU];
+      return st;
+    }
+  } else if (hint_misrouted(s, p)) {
+    *reason = KE_REASON_DS_INSUFFICIENT_GPU;
+    return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
   }
   uint64_t msk[4];
 #pragma unroll
@@ -796,21 +811,28 @@ __device__ int ds_try_allocate(const SoA& s, int64_t i, const DevPod& p, const K
 // Filter (Prepare + per-type allocation feasibility) and raw Score of DeviceShare for a pod with PF_DS on
 // a node with a cache entry.  `a`: the affinity the topology manager stored (Score and Reserve read it;
 // Filter then passes: topology_hint.go Allocate already ran).  Types in the fixed order GPU, RDMA, FPGA.
+template <bool H>
 __device__ __forceinline__ void ds_filter_score(const SoA& s, int64_t i, const DevPod& p, const KArgs& k, EvalOut& o,
                                              bool stored, DsAff a) {
-  if (p.flags & PF_DS_HINT) {
-    if (!stored) {
-      int why = 0;
-      const int st = ds_try_allocate(s, i, p, k, DsAff{false, 0u}, nullptr, &why);
-      if (st) {
-        o.status = (uint8_t)st;
-        o.reason = (uint8_t)why;
-        return;
+  if constexpr (H) {
+    if (p.flags & PF_DS_HINT) {
+      if (!stored) {
+        int why = 0;
+        const int st = ds_try_allocate<true>(s, i, p, k, DsAff{false, 0u}, nullptr, &why);
+        if (st) {
+          o.status = (uint8_t)st;
+          o.reason = (uint8_t)why;
+          return;
+        }
       }
+      int64_t raw = 0;
+      hint_score(s, i, p, k, a, &raw);
+      o.ds = (int16_t)raw;
+      return;
     }
-    int64_t raw = 0;
-    hint_score(s, i, p, k, a, &raw);
-    o.ds = (int16_t)raw;
+  } else if (hint_misrouted(s, p)) {
+    o.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    o.reason = KE_REASON_DS_INSUFFICIENT_GPU;
     return;
   }
   uint64_t msk[4];
@@ -859,6 +881,7 @@ __device__ __forceinline__ void ds_filter_score(const SoA& s, int64_t i, const D
 // defaultAllocateDevices -- with the plugin's scorer.  The allocation (request + fillGPUTotalMem,
 // devicehandler_gpu.go:98-133) is added to `used` in the SoA (updateCacheUsed).  Returns the minors mask
 // (bit 16*type + minor).
+template <bool H>
 __device__ __noinline__ uint64_t ds_reserve(const SoA& s, int64_t i, const DevPod& p, const KArgs& k, DsAff a,
                                             int8_t* vf_out = nullptr) {
   uint64_t msk[4], out = 0;
@@ -866,7 +889,10 @@ __device__ __noinline__ uint64_t ds_reserve(const SoA& s, int64_t i, const DevPo
   for (int w = 0; w < 4; w++) msk[w] = dsmask(s, w, i);
   uint32_t hout[3] = {0, 0, 0};
   int8_t hvf[2][DS_MINORS];
-  const bool hinted = (p.flags & PF_DS_HINT) != 0;
+  const bool hinted = H && (p.flags & PF_DS_HINT) != 0;
+  if constexpr (!H) {
+    if (hint_misrouted(s, p)) return 0;
+  }
   if (hinted) {  // the hinted allocation with the scorer in the Reserve phase (feasibility checked by the caller)
     for (int t = 0; t < 2; t++)
       for (int m = 0; m < DS_MINORS; m++) hvf[t][m] = -1;
@@ -1170,6 +1196,7 @@ __device__ __forceinline__ void set256(uint64_t (&b)[4], uint32_t m) {
 }
 
 // generateTopologyHints (topology_hint.go:119-212) for a pod with PF_DS on a node with a device cache
+template <bool H>
 __device__ __noinline__ void ds_numa_hints(const SoA& s, int64_t i, const DevPod& p, const KArgs& k, DsHints& h) {
   h.status = h.reason = 0;
   h.none = true;
@@ -1195,14 +1222,20 @@ __device__ __noinline__ void ds_numa_hints(const SoA& s, int64_t i, const DevPod
     pr.want[t] = p.ds_cnt[t];
     pr.inc |= p.ds_cnt[t] ? 1u << t : 0u;
   }
-  if (p.flags & PF_DS_HINT) {
-    int why = 0;
-    const int st = hint_prepare(s, i, p, s.ph[p.ring_bw], ex, false, pr, &why);
-    if (st) {
-      h.status = (uint8_t)st;
-      h.reason = (uint8_t)why;
-      return;
+  if constexpr (H) {
+    if (p.flags & PF_DS_HINT) {
+      int why = 0;
+      const int st = hint_prepare(s, i, p, s.ph[p.ring_bw], ex, false, pr, &why);
+      if (st) {
+        h.status = (uint8_t)st;
+        h.reason = (uint8_t)why;
+        return;
+      }
     }
+  } else if (hint_misrouted(s, p)) {
+    h.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+    h.reason = KE_REASON_DS_INSUFFICIENT_GPU;
+    return;
   }
   for (int t = 0; t < 3; t++)
     if (p.ds_cnt[t] && !((ex >> (16 * t)) & 0xFFFF)) {
@@ -1226,7 +1259,7 @@ __device__ __noinline__ void ds_numa_hints(const SoA& s, int64_t i, const DevPod
         return KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
       }
     }
-    return ds_try_allocate(s, i, p, k, DsAff{true, m}, gpu, why);
+    return ds_try_allocate<H>(s, i, p, k, DsAff{true, m}, gpu, why);
   };
   uint32_t best_gpu = 0;
   int why = 0;
@@ -1766,65 +1799,20 @@ __device__ __forceinline__ void numa_present_lack(const NumaNode& v, const DevPo
 }
 
 // mergeFilteredHints over every permutation of the provider lists (policy.go:198-299) when no merged hint
-// is preferred: lists[l][0..len[l]) hold masks in order (0 = a nil-affinity entry, `unsat` bit: the
-// unsatisfied entry of a resource without hints); DeviceShare lists carry their hint scores via `dsS`.
-// Exact fold in permutation order; more than DS_MERGE_BUDGET permutations sets KERR_DS_MERGE.
-constexpr int64_t DS_MERGE_BUDGET = 1 << 20;
-struct MergeLists {
-  uint8_t m[5][255];
-  uint8_t ds[5];      // the list is a DeviceShare list (scores from S)
-  uint8_t unsat[5];   // the list is the unsatisfied nil entry
-  int len[5];
-  int n;
-};
+// is preferred (ke_merge.h): up to MERGE_BUDGET permutations are walked in order, beyond it merge_exact
+// computes the same fold without enumerating them.  DeviceShare lists score 500 where their hint carries it
+// (dh.S), the NodeNUMAResource lists numa_hint_score.
 __device__ __noinline__ uint32_t merge_all_permutations(const SoA& s, int64_t i, const NumaNode& v, const DevPod& sp,
                                                          const KArgs& k, const MergeLists& L, const DsHints& dh,
                                                          bool excl) {
+  (void)excl;  // every merged hint is non-preferred here: the exclusive check changes nothing
   int64_t total = 1;
   for (int l = 0; l < L.n; l++) total *= L.len[l];
-  if (total > DS_MERGE_BUDGET) {
-    __hip_atomic_fetch_or(s.kerr, KERR_DS_MERGE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return v.zm;
-  }
-  const uint32_t all = v.zm;
-  uint32_t best = all;
-  int32_t bsc = 0;
-  bool bun = false;
-  int idx[5] = {0, 0, 0, 0, 0};
-  for (int64_t it = 0; it < total; it++) {
-    uint32_t mg = all;
-    int maxn = 0;
-    bool have = false, un = false;
-    for (int l = 0; l < L.n; l++) {
-      const uint32_t m = L.m[l][idx[l]];
-      un = un || L.unsat[l];
-      if (m) {
-        have = true;
-        mg &= m;
-        maxn = max(maxn, __popc(m));
-      }
-    }
-    un = un || (have && maxn != __popc(mg));
-    if (mg) {
-      (void)excl;  // every merged hint is non-preferred here: the exclusive check changes nothing
-      int32_t sc = 0;
-      for (int l = 0; l < L.n; l++) {
-        const uint32_t m = L.m[l][idx[l]];
-        if (!m || m != mg) continue;
-        sc += L.ds[l] ? (bit256(dh.S, m) ? 500 : 0) : numa_hint_score(s, i, v, m, sp, k);
-      }
-      if (narrower(mg, best) || (__popc(mg) == __popc(best) && sc > bsc)) {
-        best = mg;
-        bsc = sc;
-        bun = un;
-      }
-    }
-    for (int l = L.n - 1; l >= 0; l--) {  // next permutation (last list fastest)
-      if (++idx[l] < L.len[l]) break;
-      idx[l] = 0;
-    }
-  }
-  return bun ? all : best;
+  auto sc = [&](int l, uint32_t m) -> int32_t {
+    return L.ds[l] ? (bit256(dh.S, m) ? 500 : 0) : numa_hint_score(s, i, v, m, sp, k);
+  };
+  if (total <= MERGE_BUDGET) return merge_walk(L, v.zm, total, sc);
+  return merge_exact(L, v.zm, sc);
 }
 
 // topologymanager Admit with DeviceShare's hint lists (topology_hint.go:38-212, manager.go:64-129): the
@@ -1874,7 +1862,7 @@ __device__ __noinline__ NumaPick numa_admit_ds(const SoA& s, int64_t i, int poli
       bool cand = true;
 #pragma unroll
       for (int r = 0; r < 2; r++)
-        if (present[r]) cand = cand && !(m & ~all) && bit256(L[r], m) && (restricted || __popc(m) == minr[r]);
+        if (present[r]) cand = cand && !(m & ~all) && bit256(L[r], m) && (restricted || (int)__popc(m) == minr[r]);
       if (!cand) continue;
       const uint32_t mg = m & all;  // mergePermutation ANDs the default affinity
       if (!mg || !exclusive_ok(v, mg, excl)) continue;
@@ -2212,7 +2200,7 @@ __device__ __forceinline__ void ext_reserve(const SoA& s, int64_t i, const DevPo
     if (q < k.fp_n) s.xf[(XF_REQ + q) * s.stride + i] += p.xreq[q];
 }
 
-template <bool DS, bool NUMA, bool DEFER = false, bool FB_AFF = false, bool CPU = false>
+template <bool DS, bool NUMA, bool DEFER = false, bool FB_AFF = false, bool CPU = false, bool H = false>
 __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, const DevPod& p, const KArgs& k,
                                              const SoA& s, int64_t i, const NumaNode& nv, uint32_t fb_aff = 0) {
   EvalOut o;
@@ -2331,7 +2319,7 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
     DsHints dh;
     dh.status = 0;
     dh.none = true;
-    if (ds_here) ds_numa_hints(s, i, p, k, dh);
+    if (ds_here) ds_numa_hints<H>(s, i, p, k, dh);
     const DsHints* dhp = ds_here ? &dh : nullptr;
     NumaPick pk;
     if (CPU && rcb > 0) {  // a binding pod: cpuset hints and allocation (resource_manager.go:166-192,353-459)
@@ -2360,7 +2348,7 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
     }
     if (pk.status == KE_CODE_SUCCESS && ds_here && !(k.flags & AF_DS_NO_NUMA)) {
       int why = 0;  // allocateResources -> DeviceShare.Allocate on the affinity (topology_hint.go:60-117)
-      const int st = ds_try_allocate(s, i, p, k, DsAff{pk.aff != 0, pk.aff}, nullptr, &why);
+      const int st = ds_try_allocate<H>(s, i, p, k, DsAff{pk.aff != 0, pk.aff}, nullptr, &why);
       if (st) pk.status = (uint8_t)st, pk.reason = (uint8_t)why;
     }
     if (pk.status != KE_CODE_SUCCESS) {
@@ -2373,7 +2361,7 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
   }
   // ---- DeviceShare.Filter + raw Score  plugin.go:311-365, scoring.go:45-103 (Filter passes and Score
   // reads the devices of the affinity when the topology manager stored one)
-  if (ds_here && o.status == KE_CODE_SUCCESS) ds_filter_score(s, i, p, k, o, stored, DsAff{stored && o.aff != 0, o.aff});
+  if (ds_here && o.status == KE_CODE_SUCCESS) ds_filter_score<H>(s, i, p, k, o, stored, DsAff{stored && o.aff != 0, o.aff});
   if (o.status != KE_CODE_SUCCESS) {
     o.total = -1;
     o.ds = 0;
@@ -2941,7 +2929,7 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_parity(SoA s, int n_nodes, 
     uint32_t m = 0;
     bool deferred = false;
     if (live) {
-      const EvalOut o = eval_pair<true, NUMA, NUMA, false, CPU>(n, expired, pods[p], k, s, i, nv);
+      const EvalOut o = eval_pair<true, NUMA, NUMA, false, CPU, true>(n, expired, pods[p], k, s, i, nv);
       deferred = NUMA && o.status == STATUS_DEFERRED;
       const int64_t o_idx = (int64_t)p * n_nodes + i;
       status[o_idx] = o.status;
@@ -2988,7 +2976,7 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_parity_finalize(int n_nodes, KAr
 // (always alone in its batch) also dsraw[node] = raw DeviceShare score + 1 (0 when filtered out).
 // Nodes [lo, hi) of the SoA (this rank's shard); scores stay indexed by the global node index.
 // DS: the batch's pod is a DeviceShare pod (the DeviceShare path stays out of plain batches' code).
-template <bool DS, bool NUMA, bool CPU, bool EXT = false>
+template <bool DS, bool NUMA, bool CPU, bool EXT = false, bool H = false>
 __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi, const DevPod* __restrict__ pods,
                                                            const int32_t* __restrict__ batch_base, int batch_pods,
                                                            int pods_per_block, KArgs k, uint16_t* __restrict__ scores,
@@ -3023,7 +3011,7 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
       scores[(int64_t)p * score_stride + i] = (uint16_t)(tot + 1);
       continue;
     }
-    const EvalOut o = eval_pair<DS, NUMA, NUMA, false, CPU>(n, expired, pod, k, s, i, nv);
+    const EvalOut o = eval_pair<DS, NUMA, NUMA, false, CPU, H>(n, expired, pod, k, s, i, nv);
     scores[(int64_t)p * score_stride + i] = (uint16_t)(o.total + 1);
     if (NUMA) defer_push(o.status == STATUS_DEFERRED, ((uint64_t)p << 32) | (uint32_t)i, defer_list, defer_cnt);
     if (DS && (pod.flags & PF_DS)) {  // DefaultNormalizeScore's max: 1 + max raw score over feasible nodes
@@ -3921,7 +3909,7 @@ __device__ __forceinline__ uint64_t ds_reserve_wave(const SoA& s, int64_t i, con
 #pragma unroll
   for (int w = 0; w < 4; w++) msk[w] = dsmask(s, w, i);
   if ((msk[DSM_EXISTS] & (DSX_TOPO | DSX_TABLE | DSX_HONOR)) || (p.flags & (PF_GPU_PART_SPEC | 7u * PF_GPU_SCOPE0))) {
-    if (lane == 0) out = ds_reserve(s, i, p, k, DsAff{false, 0u});
+    if (lane == 0) out = ds_reserve<false>(s, i, p, k, DsAff{false, 0u});
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(out >> 32), 0) << 32) |
            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)out, 0);
   }
@@ -4885,7 +4873,7 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
       DsHints dh;
       dh.status = 0;
       dh.none = true;
-      if (ds_here) ds_numa_hints(s, node, pod, k, dh);
+      if (ds_here) ds_numa_hints<true>(s, node, pod, k, dh);
       const DsHints* dhp = ds_here ? &dh : nullptr;
       if (rcb) {
         const NumaCs cs = numa_cs_load(s, node, nf, pod);
@@ -4909,7 +4897,7 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
     // Allocate a no-op), so the allocation may fail: Reserve fails and every Reserve of the pod is undone
     if (ok && ds_here && stored && (k.flags & AF_DS_NO_NUMA)) {  // elsewhere the Filter / Admit checked it
       int why = 0;
-      ok = ds_try_allocate(s, node, pod, k, DsAff{false, 0u}, nullptr, &why) == KE_CODE_SUCCESS;  // Reserve: no affinity
+      ok = ds_try_allocate<true>(s, node, pod, k, DsAff{false, 0u}, nullptr, &why) == KE_CODE_SUCCESS;  // Reserve: no affinity
     }
     RPROF(1)
     if (ok && ds_here && (pod.flags & PF_DS_HINT)) {  // a hinted pod's Reserve-phase allocation must succeed
@@ -4977,7 +4965,7 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
       if (nsoa && v.zm) numa_reserve_cs(s, node, nf, v, got, dist, cs_old, cs_new, used, n_used, out16);
       RPROF(5)
       if (ds_here)
-        alloc = ds_reserve(s, node, pod, k, DsAff{stored && aff != 0 && !(k.flags & AF_DS_NO_NUMA), aff},
+        alloc = ds_reserve<true>(s, node, pod, k, DsAff{stored && aff != 0 && !(k.flags & AF_DS_NO_NUMA), aff},
                            s.vfo ? s.vfo + (int64_t)base * 2 * DS_MINORS : nullptr);
       out_node = (int32_t)node + global_offset;
       out_score = key_score(w);
@@ -5643,8 +5631,7 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
   int32_t kerr = 0;
   HIP_OK(hipMemcpyAsync(&kerr, d->soa.kerr, sizeof(int32_t), hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipStreamSynchronize(d->stream));
-  if (kerr & KERR_DS_MERGE)
-    return fail(KE_ERR_UNSUPPORTED, "a DeviceShare BestEffort NUMA merge beyond 2^20 hint permutations");
+  if (kerr & KERR_HINT_ROUTE) return fail(KE_ERR_DEVICE, "internal: a hinted pod reached a kernel without the hint path");
   ctx->kstat_numa_deferred = deferred;
   if (best)
     for (int64_t p = 0; p < P; p++) best[p] = bk[p] ? key_node(bk[p]) + ctx->cfg.global_node_offset : -1;
@@ -5679,6 +5666,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     int pods;
     bool ds, cpu;  // DeviceShare-capable batch (its pods' NormalizeScore) / singleton of a pod that may bind CPUs
     bool cut;      // a DeviceShare batch with DeviceShare pods: the replay may stop early
+    bool hint;     // singleton of a pod with device hints: its eval kernel carries the hint path (H)
   };
   std::vector<Batch> batches;
   // DeviceShare pods share batches (exact: the replay checks each pod's normalisation max and stops the
@@ -5689,7 +5677,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   for (int32_t p = 0; p < n_pods;) {
     const uint32_t f = d->host_pods[p].flags;
     if ((f & PF_CPUSET) || ((f & PF_DS) && !ds_batch) || (f & PF_DS_HINT)) {  // hinted pods: singletons
-      batches.push_back({1, (f & PF_DS) != 0, (f & PF_CPUSET) != 0, false});
+      batches.push_back({1, (f & PF_DS) != 0, (f & PF_CPUSET) != 0, false, (f & PF_DS_HINT) != 0});
       p++;
       continue;
     }
@@ -5702,7 +5690,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       ds_pods = ds_pods || (g & PF_DS);
       bp++;
     }
-    batches.push_back({bp, has_ds, false, ds_pods && bp > 1});
+    batches.push_back({bp, has_ds, false, ds_pods && bp > 1, false});
     p += bp;
   }
   bool any_cpu = false;
@@ -5839,7 +5827,10 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
         // a singleton batch has one pod's worth of lanes: single-wave blocks spread it over every CU
         const int eb = single ? 64 : EVAL_BLOCK;
         const dim3 grid = eval_grid(hi - lo, eb, bp, ppb);
-        auto eval = cpu ? (ds ? (numa ? k_eval_batch<true, true, true> : k_eval_batch<true, false, true>)
+        auto eval = (ds && batches[b].hint)
+                        ? (cpu ? (numa ? k_eval_batch<true, true, true, false, true> : k_eval_batch<true, false, true, false, true>)
+                               : (numa ? k_eval_batch<true, true, false, false, true> : k_eval_batch<true, false, false, false, true>))
+                  : cpu ? (ds ? (numa ? k_eval_batch<true, true, true> : k_eval_batch<true, false, true>)
                               : (numa ? k_eval_batch<false, true, true> : k_eval_batch<false, false, true>))
                         : ds ? (numa ? k_eval_batch<true, true, false> : k_eval_batch<true, false, false>)
                              : (numa ? k_eval_batch<false, true, false>
@@ -6035,11 +6026,11 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     for (auto& e : ev) (void)hipEventDestroy(e);
     return fail(KE_ERR_DEVICE, "pipelined schedule: a device-side hand-off timed out (placements invalid)");
   }
-  if (kerr & KERR_DS_MERGE) {  // placements past the refused pair are not the reference's
+  if (kerr & KERR_HINT_ROUTE) {  // an internal routing error: the placements are not the reference's
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     for (auto& e : ev) (void)hipEventDestroy(e);
-    return fail(KE_ERR_UNSUPPORTED, "a DeviceShare BestEffort NUMA merge beyond 2^20 hint permutations");
+    return fail(KE_ERR_DEVICE, "internal: a hinted pod reached a kernel without the hint path");
   }
   float ms = 0;
   HIP_OK(hipEventElapsedTime(&ms, e0, e1));

@@ -94,3 +94,50 @@ def test_ds_numa_cpuset_pods(gpu):
     c = _schedule_equal(ev, o, pods)
     assert np.array_equal(ev.last_cpusets, o.last_cpusets)
     assert (c >= 0).sum() > 60
+
+
+def test_ds_numa_merge_beyond_walk(gpu):
+    """A BestEffort merge over more than MERGE_BUDGET (2^20) hint permutations runs merge_exact (ke_merge.h)
+    instead of the permutation walk: 6-zone BestEffort nodes with one GPU and one RDMA NIC per zone, pods
+    asking 4 whole GPUs + an RDMA NIC.  NodeNUMAResource's cpu / memory lists hold up to 63 masks each and
+    DeviceShare's two copies the 22 masks of >= 4 zones (no preferred merged hint: DeviceShare's minimal size
+    is 4, the resources' 1), so a pair folds up to 63 x 63 x 22 x 22 = 1.9M permutations; the oracle walks
+    every one of them (policy.go:198-299)."""
+    n = 6
+    cl = synth.make_cluster(n, synth.BASE_SEED + 731)
+    zones = synth.make_numa(cl, synth.BASE_SEED + 732, zone_counts=(6,), policy_weights=(0, 1, 0, 0),
+                            no_zone_fraction=0.0, missing_memory_fraction=0.0, allocated_fraction=0.2)
+    devs = []
+    for i in range(n):
+        d = np.zeros(12, abi.DEVICE_DTYPE)
+        for z in range(6):
+            g, r = d[z], d[6 + z]
+            g["type"], g["minor"], g["health"] = abi.DEV_GPU, z, 1
+            g["has_total"][:] = 1
+            g["total"][:] = [100, synth.GPU_MEM, 100]
+            r["type"], r["minor"], r["health"] = abi.DEV_RDMA, z, 1
+            r["has_total"][0] = 1
+            r["total"][0] = 100
+            for x in (g, r):
+                x["has_topology"], x["numa_node"], x["pcie_rank"] = 1, z, z
+        if i % 3 == 1:  # a used GPU: fewer feasible masks on this node
+            d[2]["has_used"][:] = 1
+            d[2]["used"][:] = [100, synth.GPU_MEM, 100]
+        devs.append(d)
+    cfg = synth.config(n)
+    ev, o = Evaluator(cfg), Oracle(cfg, n)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        synth.load_numa(h, zones)
+        synth.load_devices(h, devs)
+    pods = synth.make_pods(6, synth.BASE_SEED + 733, key_base=9_800_000_000)
+    for j in range(len(pods)):
+        r = pods["device_requests"][j]
+        r[abi.PDR["koordinator.sh/gpu-core"]] = 400
+        r[abi.PDR["koordinator.sh/gpu-memory-ratio"]] = 400
+        r[abi.PDR["koordinator.sh/rdma"]] = 100 if j % 2 == 0 else 50
+        pods["has_other_requests"][j] = 1
+    a, b = ev.eval(pods, synth.T0), o.eval(pods, synth.T0)
+    assert_eval_equal(a, b)
+    assert (a["status"] == 0).sum() >= 6
+    _schedule_equal(ev, o, pods)
