@@ -66,10 +66,14 @@ static int check_numa_deviceshare(ke_ctx* ctx, const ke_pod* pods, int32_t n) {
 
 // A pod that may bind CPUs (a cpuset pod, or any cpu request while a node forces CPU binding) reads the
 // CPU SoA during evaluation: make sure it exists.
+// The pods' DevPod records are staged for upload_pods (built once per call).
 static int check_cpuset(ke_ctx* ctx, const ke_pod* pods, int32_t n) {
   Context& c = ctx->c;
+  c.staged.resize((size_t)n);
+  c.staged_src = pods;
   for (int32_t p = 0; p < n; p++) {
-    const uint32_t f = make_dev_pod(c.cfg, pods[p], pod_hints(c, pods[p]), &c.tmpl).flags;
+    c.staged[p] = make_dev_pod(c.cfg, pods[p], pod_hints(c, pods[p]), &c.tmpl);
+    const uint32_t f = c.staged[p].flags;
     if ((f & PF_CPUSET) || (c.n_bind_nodes > 0 && pods[p].requests[KE_RES_CPU] > 0)) c.cpu_enabled = true;
   }
   return KE_OK;
@@ -567,13 +571,14 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
     // Host mirror of the Reserves the device already applied to its rows: keep the object state
     // (assign cache, NodeInfo.Requested) in step so later re-derivations include these pods.
     c.pending.reserve(c.pending.size() + (size_t)len);
+    const int64_t base = c.pending_base;  // device_schedule copied pods[s0 .. s1) there during its wait
     for (int32_t i = 0; i < len; i++) {
       const int32_t p = s0 + i;
       const int32_t node = chosen[p] - off;
       if (chosen[p] < 0 || node < 0 || node >= c.n_nodes) continue;
       NodeState& ns = c.nodes[node];
       // LoadAware assign + NodeInfo.Requested: deferred (flush_mirror), the device rows carry them
-      c.pending.push_back({node, now_ns, pods[p]});
+      c.pending.push_back({node, now_ns, base + i});
       const bool was_dirty = ns.dirty;
       if (i < (int32_t)c.last_dev_alloc.size() && c.last_dev_alloc[i])
         host_ds_reserve(c.cfg, ns, make_dev_pod(c.cfg, pods[p], pod_hints(c, pods[p]), &c.tmpl), c.last_dev_alloc[i],

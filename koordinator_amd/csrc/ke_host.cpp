@@ -1276,14 +1276,16 @@ void host_release_node(const ke_config& cfg, bool ext, NodeState& ns, const ke_p
 void flush_mirror(Context& c) {
   for (const Context::PendingAssign& a : c.pending) {
     NodeState& ns = c.nodes[a.node];
+    const ke_pod& pod = c.pending_pods[(size_t)a.idx];
     const bool was_dirty = ns.dirty;
-    host_assign(c.cfg, ns, a.pod, a.ts);
-    ns.node.requested[KE_RES_CPU] += a.pod.requests[KE_RES_CPU];
-    ns.node.requested[KE_RES_MEMORY] += a.pod.requests[KE_RES_MEMORY];
-    if (c.ext_enabled) host_ext_reserve(ns, a.pod);
+    host_assign(c.cfg, ns, pod, a.ts);
+    ns.node.requested[KE_RES_CPU] += pod.requests[KE_RES_CPU];
+    ns.node.requested[KE_RES_MEMORY] += pod.requests[KE_RES_MEMORY];
+    if (c.ext_enabled) host_ext_reserve(ns, pod);
     ns.dirty = was_dirty;  // the device row already carries this Reserve
   }
   c.pending.clear();
+  c.pending_pods.clear();
 }
 
 void host_assign(const ke_config& cfg, NodeState& ns, const ke_pod& pod, int64_t timestamp_ns) {

@@ -98,9 +98,15 @@ struct Context {
   struct PendingAssign {
     int32_t node;
     int64_t ts;
-    ke_pod pod;
+    int64_t idx;  // the pod: pending_pods[idx]
   };
   std::vector<PendingAssign> pending;
+  std::vector<ke_pod> pending_pods;  // copies of scheduled pods, taken while the device runs the call
+  int64_t pending_base = 0;          // pending_pods index of the current device_schedule segment's first pod
+  // The DevPod records of the current call's pods, built once by the argument checks (check_cpuset) and
+  // reused by upload_pods
+  std::vector<DevPod> staged;
+  const ke_pod* staged_src = nullptr;
   // ElasticQuota tree (ke_quotas_load): objects, the used limits computed on the host, and whether the
   // device copy of the table is stale
   ke_quota_args qargs{};

@@ -3411,6 +3411,8 @@ constexpr int SEL_COPIES = 8;   // histogram copies per wave (pass 2)
 
 // per-wave node segment of k_select over [lo, hi): a multiple of 512 (one 16-B load per lane per step)
 __host__ __device__ inline int select_seg(int lo, int hi) { return ((hi - lo + SELECT_WAVES - 1) / SELECT_WAVES + 511) & ~511; }
+// node part of one of `parts` workgroups of a split k_select (512-aligned, like the shard ranges)
+__host__ __device__ inline int select_part(int lo, int hi, int parts) { return ((hi - lo + parts - 1) / parts + 511) & ~511; }
 
 // it = 0 .. iters-1 over a wave's 512-node steps; RC > 0: a constant trip count (registers indexed by it)
 template <int RC, typename F>
@@ -3459,13 +3461,23 @@ __device__ __forceinline__ uint32_t max_halves(uint32_t w) { return max(w & 0xFF
 // 1 + the max raw score over all feasible nodes, after the all-reduce when node-sharded).
 // kext / ostride: the pipelined schedule selects top-(k_j + KMAX) lists of a stale snapshot into
 // rows of `ostride` keys (pipelining); otherwise kext = 0, ostride = KMAX.
+// gridDim.y > 1 (plain batches): the pod's nodes are split into gridDim.y 512-aligned parts, one workgroup
+// each, every part's top-k_j list in its own block of a gather buffer (`ystride` words apart) for k_merge --
+// the per-shard lists of the node-sharded path, on one GPU (a batch of 64 pods then fills every CU).
 template <bool DS, int RC>
 __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restrict__ scores, int64_t score_stride,
                                                          int lo, int hi, uint32_t* __restrict__ cand,
                                                          int32_t* __restrict__ cand_cnt,
                                                          const uint16_t* __restrict__ dsraw,
                                                          uint32_t* __restrict__ dsmax1, int32_t wds, int kext,
-                                                         int ostride) {
+                                                         int ostride, int64_t ystride) {
+  if (!DS && gridDim.y > 1) {
+    const int part = select_part(lo, hi, gridDim.y);
+    lo = min(hi, lo + (int)blockIdx.y * part);
+    hi = min(hi, lo + part);
+    cand += (int64_t)blockIdx.y * ystride;
+    cand_cnt += (int64_t)blockIdx.y * ystride;
+  }
   __shared__ int16_t s_lut[DS ? MAX_DS_RAW + 1 : 1];
   __shared__ int32_t s_dscnt;
   DsNorm dn{DS ? dsraw + (int64_t)blockIdx.x * score_stride : dsraw, s_lut};
@@ -5040,6 +5052,7 @@ struct DeviceState {
   bool loopback = false;
   ncclComm_t comm = nullptr;
   uint32_t* d_gath = nullptr;  // [world][GATH_WORDS]
+  uint32_t* d_split = nullptr; // [MAX_WORLD][GATH_WORDS]: the part lists of a split k_select (unsharded)
   // DeviceShare
   bool ds_alloc = false;         // soa.ds / soa.dsm allocated
   size_t pt_words = 0;           // soa.pt capacity (uint64 words)
@@ -5049,6 +5062,7 @@ struct DeviceState {
   int64_t* d_dsrows = nullptr;   // staging for DeviceShare row uploads
   int64_t ds_staging_cap = 0;
   std::vector<DevPod> host_pods;  // the last uploaded queue (batch segmentation)
+  std::vector<DevPodHint> host_ph;  // its hinted pods' records (the async upload reads them)
   // NUMA topology
   bool numa_alloc = false;         // soa.nf / soa.nm allocated
   int64_t* d_numaalloc = nullptr;  // [n_pods][16] per-zone allocation of each pod (ke_schedule)
@@ -5148,6 +5162,7 @@ int device_create(Context* ctx) {
   d->soa.dsb = d->d_dsmax;
   d->soa.dsraw = d->d_dsraw;
   HIP_OK(hipMalloc(&d->d_aff, d->capacity));
+  HIP_OK(hipMalloc(&d->d_split, sizeof(uint32_t) * GATH_WORDS_MAX * MAX_WORLD));
   HIP_OK(hipStreamSynchronize(d->stream));
   return KE_OK;
 }
@@ -5160,7 +5175,7 @@ void device_destroy(Context* ctx) {
   if (d->comm) (void)ncclCommDestroy(d->comm);
   void* ptrs[] = {d->soa.f,     d->soa.flags, d->d_rows,      d->d_idx,          d->d_pods,   d->d_scores,
                   d->d_cand,    d->d_cand_cnt, d->d_batch_base, d->d_chosen,     d->d_chosen_score,
-                  d->d_stamps,  d->d_parity, d->d_best,       d->d_gath,         d->soa.ds,   d->soa.dsm,
+                  d->d_stamps,  d->d_parity, d->d_best,       d->d_gath,    d->d_split,         d->soa.ds,   d->soa.dsm,
                   d->d_dsraw,   d->d_dsmax,  d->d_devalloc,   d->d_dsrows,       d->soa.nf,   d->soa.nm,
                   d->d_numaalloc, d->d_numarows, d->d_defer, d->d_defer_cnt, d->soa.cs, d->soa.cpu,
                   d->d_cpurows, d->d_cpusets, d->d_aff, d->soa.qt, d->soa.qm, d->d_sched, d->d_stale,
@@ -5534,10 +5549,15 @@ static int upload_pods(Context* ctx, int32_t n_pods, const ke_pod* pods) {
   DeviceState* d = ctx->dev;
   std::vector<DevPod>& dp = d->host_pods;
   dp.resize((size_t)n_pods);
-  std::vector<DevPodHint> ph;  // the hinted pods' records; DevPod::ring_bw = slot
+  std::vector<DevPodHint>& ph = d->host_ph;  // the hinted pods' records; DevPod::ring_bw = slot
+  ph.clear();
+  // the argument checks of this call staged the records (check_cpuset); pods may be a segment of them
+  const bool staged = ctx->staged_src && pods >= ctx->staged_src &&
+                      pods + n_pods <= ctx->staged_src + (int64_t)ctx->staged.size();
+  const DevPod* st = staged ? ctx->staged.data() + (pods - ctx->staged_src) : nullptr;
   for (int32_t p = 0; p < n_pods; p++) {
     const ke_pod_device_hints* h = pod_hints(*ctx, pods[p]);
-    dp[p] = make_dev_pod(ctx->cfg, pods[p], h, &ctx->tmpl);
+    dp[p] = st ? st[p] : make_dev_pod(ctx->cfg, pods[p], h, &ctx->tmpl);
     if (ctx->n_bind_nodes > 0 && dp[p].req[0] > 0) dp[p].flags |= PF_CPUSET;  // a node policy may bind it
     if (dp[p].flags & PF_DS_HINT) {  // hints, or a pod allocated by GPU shared resource template
       static const ke_pod_device_hints none{};
@@ -5554,7 +5574,8 @@ static int upload_pods(Context* ctx, int32_t n_pods, const ke_pod* pods) {
     HIP_OK(hipMemcpyAsync(d->d_ph, ph.data(), sizeof(DevPodHint) * ph.size(), hipMemcpyHostToDevice, d->stream));
   }
   d->soa.ph = d->d_ph;
-  HIP_OK(hipStreamSynchronize(d->stream));
+  // no host wait: the kernels run on d->stream after the copies, and the eval stream waits for ev_start,
+  // recorded on d->stream after them; dp / ph stay untouched until the call's final synchronisation
   return KE_OK;
 }
 
@@ -5866,11 +5887,23 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
         const bool rc = select_seg(slo, shi) <= SEL_RC * 512;
         auto sel = ds ? (rc ? k_select<true, SEL_RC> : k_select<true, 0>) : (rc ? k_select<false, SEL_RC> : k_select<false, 0>);
         hipLaunchKernelGGL(sel, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, es, d->d_scores, d->capacity, slo, shi, cand,
-                           cnt, d->d_dsraw, d->d_dsmax, k.wp_ds, kext, L);
+                           cnt, d->d_dsraw, d->d_dsmax, k.wp_ds, kext, L, (int64_t)0);
       };
+      // a plain batch over many nodes: its pods' selections split over several workgroups each (>= 256
+      // workgroups in all, parts of >= 4096 nodes), merged by k_merge
+      const int parts = ds ? 1 : std::max(1, std::min({MAX_WORLD, (255 + bp) / bp, (int)(N / 4096)}));
       if (argmax1) {  // d_cand[0] zeroed by k_batch_begin
         hipLaunchKernelGGL((ds ? k_argmax1<true> : k_argmax1<false>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
                            es, d->d_scores, 0, N, d->d_dsraw, d->d_dsmax, k.wp_ds, d->d_cand, d->d_cand_cnt);
+      } else if (!sharded && parts > 1) {
+        const int gw = gath_words(L);
+        const bool rc = select_seg(0, select_part(0, N, parts)) <= SEL_RC * 512;
+        hipLaunchKernelGGL((rc ? k_select<false, SEL_RC> : k_select<false, 0>), dim3((unsigned)bp, (unsigned)parts),
+                           dim3(SELECT_BLOCK), 0, es, d->d_scores, d->capacity, 0, (int)N, d->d_split,
+                           reinterpret_cast<int32_t*>(d->d_split + MAX_BATCH * L), d->d_dsraw, d->d_dsmax, k.wp_ds,
+                           kext, L, (int64_t)gw);
+        hipLaunchKernelGGL(k_merge, dim3((unsigned)bp), dim3(MERGE_BLOCK), 0, es, d->d_split, parts, L, kext, lists,
+                           lists_cnt);
       } else if (!sharded) {
         select(0, N, lists, lists_cnt);
       } else {
@@ -6014,6 +6047,10 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   HIP_OK(hipMemcpyAsync(pst.data(), d->d_stamps + (n_pods + 2), sizeof(uint64_t) * 8 * n_batches,
                         hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipMemcpyAsync(est.data(), estamps, sizeof(uint64_t) * n_batches, hipMemcpyDeviceToHost, d->stream));
+  // while the device runs: the host copies of the segment's pods for the deferred mirror (flush_mirror;
+  // ke_schedule records which of them were placed)
+  ctx->pending_base = (int64_t)ctx->pending_pods.size();
+  ctx->pending_pods.insert(ctx->pending_pods.end(), pods, pods + n_pods);
   HIP_OK(hipStreamSynchronize(d->stream));
   HIP_OK(hipStreamSynchronize(d->estream));
   ctx->host_ms[5] = ms_since(tp);
