@@ -44,6 +44,28 @@ def test_c4_generator_schedule_parity(gpu):
     assert ev.check_records(synth.T0) == 0
 
 
+def test_c4_full_cluster_prefix(gpu):
+    """C4 at its own 50k-node size: the first 12 pods of the bench queue (tools/cpuset_bench.py
+    --survey) bit-exact with the oracle -- placements, scores, cpusets, NUMA allocations.  The oracle takes
+    about 2.3 s per pod here at 16 threads, so the prefix is short."""
+    n, p = 50_000, 12
+    cl, zones, tables = synth.make_c4_cluster(n, synth.BASE_SEED + 4)
+    pods = synth.make_c4_pods(p, synth.BASE_SEED + 104)
+    cfg = synth.config(n)
+    ev, o = Evaluator(cfg), Oracle(cfg, n)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        synth.load_numa(h, zones)
+        synth.load_cpus(h, tables)
+    c1, s1 = ev.schedule(pods, synth.T0)
+    c0, s0 = o.schedule(pods, synth.T0)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5].ravel().tolist()
+    assert np.array_equal(s1, s0)
+    assert np.array_equal(ev.last_cpusets, o.last_cpusets)
+    assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
+    assert (c1 >= 0).all() and np.any(ev.last_cpusets != 0)
+
+
 def test_c5_full_cluster_quota_prefix(gpu):
     n, p = 20_000, 640
     cl = synth.make_cluster(n, synth.BASE_SEED + 5)
