@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define KE_ABI_VERSION 7
+#define KE_ABI_VERSION 8
 #define KE_ABSENT (-1)
 
 typedef struct ke_ctx ke_ctx; /* one evaluator context (ke_create) */
@@ -512,7 +512,9 @@ typedef struct ke_pod {
    * (PreFilter Skip), else 1 + the index of the pod's quota in the last ke_quotas_load table. */
   int16_t quota;
   uint8_t quota_non_preemptible; /* extension.IsPodNonPreemptible (label preemptible=false) */
-  uint8_t pad2;
+  uint8_t reservation_matched;   /* the pod matches or ignores a reservation (BeforePreFilter's matchedOrIgnored is
+                                    not empty for some node, transformer.go:93-145): the nominated-reservation path
+                                    is not modelled -> KE_ERR_UNSUPPORTED (see ke_reservations_load) */
   /* DeviceShare allocation annotations (apis/extension/device_share.go; parsed by utils.go:355-513) */
   int64_t gpu_ring_bus_bandwidth;      /* GPUPartitionSpec.RingBusBandwidth.Value(), KE_ABSENT = nil       */
   int32_t gpu_required_topology_scope; /* DeviceAllocateHints[gpu].RequiredTopologyScope: KE_SCOPE_*       */
@@ -605,7 +607,7 @@ int ke_abi_version(void);
 /* sizeof() of ke_config, ke_node, ke_node_metric, ke_pod_metric, ke_aggregated_usage, ke_pod,
  * ke_resource_map, ke_loadaware_args, ke_numa_args, ke_deviceshare_args, ke_device, ke_numa_zone, ke_cpu,
  * ke_quota_args, ke_quota, ke_gpu_partition, ke_ext_args, ke_node_resource, ke_pod_allocation, ke_pod_device_hints,
- * ke_gpu_template (in that order) for binding-layout checks. */
+ * ke_gpu_template, ke_reservation (in that order) for binding-layout checks. */
 int ke_abi_struct_sizes(int32_t* sizes, int32_t n);
 /* 1 if this build has a usable HIP device and its gfx950 kernels loaded, else 0. */
 int ke_device_available(void);
@@ -658,6 +660,34 @@ int ke_node_resources_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_node_re
 int ke_node_resources_get(ke_ctx* ctx, int32_t node, int32_t cap, ke_node_resource* res, int32_t* n);
 /* Drop the node's cache entry (getNodeDevice == nil: DeviceShare Filter passes, Score is 0). */
 int ke_node_devices_delete(ke_ctx* ctx, int32_t node);
+
+/* ---- Reservations (pkg/scheduler/plugins/reservation) -----------------------
+ * The reservation cache as the scheduler's BeforePreFilter reads it (reservation/cache.go,
+ * transformer.go:147-300).  Every pod sees each node's NodeInfo restored: a reservation that is available
+ * (IsAvailable, no ParseError), not (AllocateOnce with allocated pods), has allocated pods and is not
+ * matched by the pod gives back the part its owner pods already hold twice (restoreUnmatchedReservations,
+ * transformer.go:447-473): Requested -= allocatable, += SubtractWithNonNegativeResult(allocatable, allocated),
+ * NonZeroRequested likewise with the 100m / 200Mi defaults of a zero request.  `NodeInfo.Requested` passed
+ * with ke_node_upsert / ke_node_set_requested (and the cpu / memory rows of ke_node_resources_set) must
+ * include the reserve pods' requests, as the scheduler's NodeInfo does.  The restored values feed every
+ * plugin that reads NodeInfo: NodeNUMAResource's amplified-cpu Filter and Score, NodeResourcesFitPlus.
+ * A pod that matches a reservation (ke_pod.reservation_matched) is refused: its restore, the Reservation
+ * plugin's Filter / Score / Reserve and the NUMA / DeviceShare reservation restores are not modelled. */
+typedef struct ke_reservation {
+  int32_t node;           /* status.nodeName as a node index                                     */
+  uint8_t available;      /* IsAvailable() and no ParseError                                     */
+  uint8_t allocate_once;  /* spec.allocateOnce                                                   */
+  uint8_t pad[2];
+  int32_t allocated_pods; /* GetAllocatedPods(): owner pods assigned to it                         */
+  int32_t pad2;
+  int64_t allocatable[KE_NRES]; /* status.allocatable = the reserve pod's requests: MilliCPU, Memory */
+  int64_t allocated[KE_NRES];   /* status.allocated: the owner pods' requests                     */
+} ke_reservation; /* 48 bytes */
+/* Replace the reservation set (n = 0: none). */
+int ke_reservations_load(ke_ctx* ctx, int32_t n, const ke_reservation* reservations);
+/* NodeInfo.Requested / NonZeroRequested (MilliCPU, Memory) of `node` as the plugins see it for a pod that
+ * matches no reservation (after the restore above and the Reserves of past ke_schedule calls). */
+int ke_node_info_requested(ke_ctx* ctx, int32_t node, int64_t* requested /*[2]*/, int64_t* non_zero /*[2]*/);
 /* The node's GPU partition indexer and policy as GPUAllocator.Allocate resolves them (allocator_gpu.go:77-82,
  * device_cache.go:532-545): has_table = the indexer is not nil (the Device's gpu-partitions annotation, else
  * the designated table of the node's GPU model), honor = the matching GPUPartitionPolicy label is Honor.

@@ -9,7 +9,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 ABSENT = -1
 
 OK = 0
@@ -321,7 +321,7 @@ class Pod(C.Structure):
         ("cpu_exclusive", i32),
         ("quota", C.c_int16),
         ("quota_non_preemptible", u8),
-        ("pad2", u8),
+        ("reservation_matched", u8),
         ("gpu_ring_bus_bandwidth", i64),
         ("gpu_required_topology_scope", i32),
         ("gpu_partition_spec", u8),
@@ -372,9 +372,15 @@ class PodAllocation(C.Structure):
                 ("vf_rank", C.c_int8 * (2 * MAX_MINORS))]
 
 
+class Reservation(C.Structure):  # ke_reservation
+    _fields_ = [("node", i32), ("available", u8), ("allocate_once", u8), ("pad", u8 * 2), ("allocated_pods", i32),
+                ("pad2", i32), ("allocatable", i64 * NRES), ("allocated", i64 * NRES)]
+
+
 STRUCTS = [Config, Node, NodeMetric, PodMetric, AggregatedUsage, Pod, ResourceMap, LoadAwareArgs, NumaArgs,
            DeviceShareArgs, Device, NumaZone, Cpu, QuotaArgs, Quota, GpuPartition, ExtArgs, NodeResource,
-           PodAllocation, PodDeviceHints, GpuTemplate]
+           PodAllocation, PodDeviceHints, GpuTemplate, Reservation]
+RESERVATION_DTYPE = np.dtype(Reservation)
 POD_DEVICE_HINTS_DTYPE = np.dtype(PodDeviceHints)
 GPU_TEMPLATE_DTYPE = np.dtype(GpuTemplate)
 QUOTA_DTYPE = np.dtype(Quota)
@@ -483,6 +489,8 @@ EXPORTS = {
     "ke_set_pod_device_hints": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_gpu_templates_load": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_node_device_flags": (C.c_int, [C.c_void_p, i32, i32, i32]),
+    "ke_reservations_load": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
+    "ke_node_info_requested": (C.c_int, [C.c_void_p, i32, C.POINTER(i64), C.POINTER(i64)]),
     "ke_decode_pod_device_hints": (C.c_int, [C.c_char_p, i64, C.POINTER(PodDeviceHints), C.POINTER(i32)]),
     "ke_decode_device_flags": (C.c_int, [C.c_char_p, i64, C.c_char_p, i64, C.POINTER(i32), C.POINTER(i32)]),
     "ke_last_device_allocations": (C.c_int, [C.c_void_p, i32, C.c_void_p]),

@@ -44,6 +44,8 @@ static int check_pods(const ke_pod* pods, int32_t n, const Context* c = nullptr)
   for (int32_t p = 0; p < n; p++) {
     int rc = validate_pod(pods[p]);
     if (rc) return rc;
+    if (pods[p].reservation_matched)
+      return fail(KE_ERR_UNSUPPORTED, "a pod matching a reservation (the nominated-reservation path is not modelled)");
     if (c) rc = validate_pod_hints(*c, pods[p]);
     else if (pods[p].device_hint) rc = fail(KE_ERR_INVALID, "ke_pod.device_hint without a context");
     if (rc) return rc;
@@ -93,7 +95,7 @@ int ke_abi_struct_sizes(int32_t* sizes, int32_t n) {
                          (int32_t)sizeof(ke_quota),        (int32_t)sizeof(ke_gpu_partition),
                          (int32_t)sizeof(ke_ext_args),     (int32_t)sizeof(ke_node_resource),
                          (int32_t)sizeof(ke_pod_allocation), (int32_t)sizeof(ke_pod_device_hints),
-                         (int32_t)sizeof(ke_gpu_template)};
+                         (int32_t)sizeof(ke_gpu_template),   (int32_t)sizeof(ke_reservation)};
   const int32_t m = (int32_t)(sizeof(all) / sizeof(all[0]));
   for (int32_t i = 0; i < n && i < m; i++) sizes[i] = all[i];
   return m;
@@ -279,6 +281,27 @@ int ke_gpu_templates_load(ke_ctx* ctx, int32_t n, const ke_gpu_template* templat
     if (id < 0) return id;
   }
   ctx->c.tmpl.assign(templates, templates + n);
+  return KE_OK;
+}
+
+int ke_reservations_load(ke_ctx* ctx, int32_t n, const ke_reservation* reservations) {
+  if (!ctx) return fail(KE_ERR_INVALID, "null context");
+  flush_mirror(ctx->c);
+  return load_reservations(ctx->c, n, reservations);
+}
+
+int ke_node_info_requested(ke_ctx* ctx, int32_t node, int64_t* requested, int64_t* non_zero) {
+  int rc = check_node(ctx, node);
+  if (rc) return rc;
+  if (!requested || !non_zero) return fail(KE_ERR_INVALID, "ke_node_info_requested outputs");
+  flush_mirror(ctx->c);
+  const NodeState& ns = ctx->c.nodes[node];
+  for (int k = 0; k < KE_NRES; k++) {
+    requested[k] = ns.node.requested[k] + ns.rv_req[k];
+    non_zero[k] = KE_ABSENT;  // NonZeroRequested is known from the node's ke_node_resources_set rows
+    for (const ke_node_resource& r : ns.xres)
+      if (r.id == k) non_zero[k] = xres_requested(ns, r);
+  }
   return KE_OK;
 }
 

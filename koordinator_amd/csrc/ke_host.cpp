@@ -488,9 +488,54 @@ void derive_ext_row(const ke_config& cfg, const NodeState& ns, int64_t* f, uint6
   for (const ke_node_resource& r : ns.xres) {
     if (r.allocatable > 0) m |= 1ull << r.id;
     for (int q = 0; q < cfg.ext.n_fitplus && q < 4; q++)
-      if (cfg.ext.fitplus[q].id == r.id) f[XF_ALLOC + q] = r.allocatable, f[XF_REQ + q] = r.requested;
+      if (cfg.ext.fitplus[q].id == r.id) f[XF_ALLOC + q] = r.allocatable, f[XF_REQ + q] = xres_requested(ns, r);
   }
   *mask = m;
+}
+
+int64_t xres_requested(const NodeState& ns, const ke_node_resource& r) {
+  // cpu / memory rows carry NonZeroRequested: the reservation restore moves it too
+  return r.requested + (r.id == KE_RES_CPU || r.id == KE_RES_MEMORY ? ns.rv_nz[r.id] : 0);
+}
+
+// The reservation cache's NodeInfo restore for a pod that matches no reservation (BeforePreFilter,
+// transformer.go:147-300): an available reservation (not AllocateOnce with allocated pods) that has
+// allocated pods is "unmatched", and restoreUnmatchedReservations (transformer.go:447-473) removes its reserve
+// pod (requests = allocatable) from NodeInfo and adds back a pod requesting SubtractWithNonNegativeResult(
+// allocatable, allocated) when that is not zero; updateNodeInfoRequested's NonZeroRequested uses the 100m /
+// 200Mi defaults of a zero cpu / memory request (the reserve pod taken as one container).
+int load_reservations(Context& c, int32_t n, const ke_reservation* rs) {
+  if (n < 0 || (n > 0 && !rs)) return fail(KE_ERR_INVALID, "reservations");
+  for (int32_t i = 0; i < n; i++) {
+    const ke_reservation& r = rs[i];
+    if (r.node < 0 || r.node >= c.n_nodes) return fail(KE_ERR_NOT_FOUND, "reservation node index");
+    if (r.allocated_pods < 0) return fail(KE_ERR_INVALID, "negative reservation allocated pods");
+    for (int k = 0; k < KE_NRES; k++)
+      if (r.allocatable[k] < 0 || r.allocated[k] < 0) return fail(KE_ERR_INVALID, "negative reservation quantity");
+  }
+  for (const ke_reservation& r : c.resv) {  // the old restore leaves
+    NodeState& ns = c.nodes[r.node];
+    for (int k = 0; k < KE_NRES; k++) ns.rv_req[k] = ns.rv_nz[k] = 0;
+    ns.dirty = true;
+  }
+  c.resv.assign(rs, rs + n);
+  auto non0 = [](int k, int64_t v) { return v != 0 ? v : (k == KE_RES_CPU ? 100 : 200LL << 20); };
+  for (const ke_reservation& r : c.resv) {
+    NodeState& ns = c.nodes[r.node];
+    ns.dirty = true;
+    if (!r.available || (r.allocate_once && r.allocated_pods > 0) || r.allocated_pods == 0) continue;
+    int64_t rem[KE_NRES];
+    bool rem_nz = false;
+    for (int k = 0; k < KE_NRES; k++) {
+      rem[k] = r.allocatable[k] > r.allocated[k] ? r.allocatable[k] - r.allocated[k] : 0;
+      rem_nz = rem_nz || rem[k] != 0;
+    }
+    for (int k = 0; k < KE_NRES; k++) {
+      ns.rv_req[k] += -r.allocatable[k] + rem[k];
+      ns.rv_nz[k] += -non0(k, r.allocatable[k]) + (rem_nz ? non0(k, rem[k]) : 0);
+    }
+  }
+  return KE_OK;
 }
 
 // host mirror of a placement's ext Reserve: NodeInfo (NonZero)Requested += the pod's requests by id
@@ -957,7 +1002,7 @@ void derive_row(const ke_config& cfg, const NodeState& ns, int64_t now, Row* row
   // ---- NodeNUMAResource (policy None, non-cpuset pods)
   for (int r = 0; r < KE_NRES; r++) {
     row->f[F_NALLOC + r] = n.allocatable[r];
-    row->f[F_NREQ + r] = n.requested[r];
+    row->f[F_NREQ + r] = n.requested[r] + ns.rv_req[r];  // NodeInfo.Requested after the reservation restore
   }
   const int64_t cs_milli = cpus_allocated(ns) * 1000;
   row->f[F_CSM] = cs_milli;

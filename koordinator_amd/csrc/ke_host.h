@@ -48,6 +48,9 @@ struct NodeState {
   int32_t gpu_model_id = 0;
   // NodeResourcesFitPlus / ScarceResourceAvoidance: NodeInfo Allocatable / (NonZero)Requested by resource id
   std::vector<ke_node_resource> xres;
+  // Reservations: the NodeInfo restore every pod sees (restoreUnmatchedReservations), added to
+  // Requested / NonZeroRequested (MilliCPU, Memory) when the rows are derived (load_reservations)
+  int64_t rv_req[KE_NRES] = {0, 0}, rv_nz[KE_NRES] = {0, 0};
   // derived
   bool dirty = true;            // row must be re-derived and uploaded
   int64_t valid_until = INT64_MAX;  // derived row is exact for now < valid_until
@@ -123,6 +126,7 @@ struct Context {
   // model keys (id -> ke_label_id of "<vendor>-<model>", id 0 = none); the VF ranks of the last ke_schedule
   std::vector<ke_pod_device_hints> hints;
   std::vector<ke_gpu_template> tmpl;
+  std::vector<ke_reservation> resv;  // ke_reservations_load
   std::vector<std::vector<std::pair<int32_t, int32_t>>> label_sets{{}};
   std::map<std::vector<std::pair<int32_t, int32_t>>, int> label_set_ids{{{}, 0}};
   std::vector<int32_t> model_keys{0};
@@ -201,6 +205,9 @@ void host_numa_reserve(NodeState& ns, const int64_t* delta /*[KE_MAX_NUMA*KE_NRE
 int validate_node_resources(int32_t n, const ke_node_resource* r);
 // the ext SoA row of a node: NUM_XF int64 + the uint64 mask of resource ids with Allocatable > 0
 void derive_ext_row(const ke_config& cfg, const NodeState& ns, int64_t* f, uint64_t* mask);
+int load_reservations(Context& c, int32_t n, const ke_reservation* r);
+// NodeResourcesFitPlus' (NonZero)Requested of resource `id` on the node, with the reservation restore
+int64_t xres_requested(const NodeState& ns, const ke_node_resource& r);
 void host_ext_reserve(NodeState& ns, const ke_pod& pod);
 
 // CPU topology / cpuset binding (NodeNUMAResource with NUMA policy None)

@@ -132,6 +132,17 @@ class Evaluator:
         t = abi.struct_array(templates, abi.GpuTemplate)
         self._check(self.lib.ke_gpu_templates_load(self.h, len(t), abi.ptr(t)))
 
+    def reservations_load(self, reservations):
+        """ke_reservations_load: the reservation cache (RESERVATION_DTYPE array)."""
+        r = abi.struct_array(reservations, abi.Reservation)
+        self._check(self.lib.ke_reservations_load(self.h, len(r), abi.ptr(r)))
+
+    def node_info_requested(self, i):
+        """ke_node_info_requested: NodeInfo Requested / NonZeroRequested (MilliCPU, Memory) after the restore."""
+        req, nz = (C.c_int64 * 2)(), (C.c_int64 * 2)()
+        self._check(self.lib.ke_node_info_requested(self.h, i, req, nz))
+        return list(req), list(nz)
+
     def set_device_flags(self, i, secondary_well_planned, gpu_model_key):
         """ke_node_device_flags: the Device's secondary-well-planned label and the node's GPU template key."""
         self._check(self.lib.ke_node_device_flags(self.h, i, int(secondary_well_planned), int(gpu_model_key)))

@@ -54,6 +54,8 @@ def load():
         "or_ds_prefilter": (C.c_int, [V, C.POINTER(abi.Pod), C.POINTER(C.c_int), V, V, V]),
         "or_set_pod_device_hints": (C.c_int, [V, i32, V]),
         "or_gpu_templates_load": (C.c_int, [V, i32, V]),
+        "or_reservations_load": (C.c_int, [V, i32, V]),
+        "or_node_info_requested": (C.c_int, [V, i32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
         "or_node_device_flags": (C.c_int, [V, i32, i32, i32]),
         "or_last_vf_ranks": (C.c_int, [V, i32, V]),
         "or_ds_allocate": (C.c_int, [V, C.POINTER(abi.Pod), i32, i32, i32, V, V, V]),
@@ -255,6 +257,15 @@ class Oracle:
     def gpu_templates_load(self, templates):
         t = abi.struct_array(templates, abi.GpuTemplate)
         assert self.lib.or_gpu_templates_load(self.h, len(t), abi.ptr(t)) == 0
+
+    def reservations_load(self, reservations):
+        r = abi.struct_array(reservations, abi.Reservation)
+        assert self.lib.or_reservations_load(self.h, len(r), abi.ptr(r)) == 0
+
+    def node_info_requested(self, i):
+        req, nz = (C.c_int64 * 2)(), (C.c_int64 * 2)()
+        assert self.lib.or_node_info_requested(self.h, i, req, nz) == 0
+        return list(req), list(nz)
 
     def set_device_flags(self, i, secondary_well_planned, gpu_model_key):
         assert self.lib.or_node_device_flags(self.h, i, int(secondary_well_planned), int(gpu_model_key)) == 0

@@ -66,6 +66,8 @@ typedef struct or_node {
   /* NodeInfo Allocatable / (NonZero)Requested by resource id (NodeResourcesFitPlus, ScarceResourceAvoidance) */
   int32_t n_xres;
   ke_node_resource xres[KE_MAX_XRES];
+  /* the reservation cache's NodeInfo restore for a pod that matches no reservation (or_reservations_load) */
+  int64_t rv_req[KE_NRES], rv_nz[KE_NRES];
 } or_node;
 
 /* TopologyOptions.CPUTopology / ReservedCPUs / MaxRefCount + NodeAllocation.allocatedCPUs */
@@ -391,7 +393,7 @@ static int pod_is_cpuset(const ke_pod* pod) {
          pod->requests[KE_RES_CPU] > 0;
 }
 static int pod_unsupported(const ke_pod* pod) {
-  return pod->has_resource_spec || pod->has_unsupported_device_requests;
+  return pod->has_resource_spec || pod->has_unsupported_device_requests || pod->reservation_matched;
 }
 static int node_unsupported(const ke_node* n) {
   return n->numa_topology_policy < 0 || n->numa_topology_policy > KE_NUMA_POLICY_SINGLE_NUMA_NODE ||
@@ -883,7 +885,7 @@ static int numa_filter_amplified(const or_node* n, const ke_pod* pod, int rcb, i
   }
   if (rcb) pod_cpu = amplify(pod_cpu, ratio);
   const int64_t allocated_milli = cpus_allocated_count(n) * 1000;
-  int64_t requested = n->node.requested[KE_RES_CPU];
+  int64_t requested = n->node.requested[KE_RES_CPU] + n->rv_req[KE_RES_CPU]; /* NodeInfo after the restore */
   if (requested >= allocated_milli && allocated_milli > 0) {
     requested = requested - allocated_milli;
     requested += amplify(allocated_milli, ratio);
@@ -1512,8 +1514,8 @@ int64_t or_numa_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
       }
     }
     if (!any) {
-      req[0] = n->node.requested[KE_RES_CPU];
-      req[1] = n->node.requested[KE_RES_MEMORY];
+      req[0] = n->node.requested[KE_RES_CPU] + n->rv_req[KE_RES_CPU];
+      req[1] = n->node.requested[KE_RES_MEMORY] + n->rv_req[KE_RES_MEMORY];
       alloc[0] = n->node.allocatable[KE_RES_CPU];
       alloc[1] = n->node.allocatable[KE_RES_MEMORY];
     }
@@ -1542,7 +1544,8 @@ int64_t or_numa_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
   if (rcb < 0 || (rcb && !cpus_valid(n))) return 0;
   int64_t podreq[KE_NRES] = {pod->requests[KE_RES_CPU], pod->requests[KE_RES_MEMORY]};
   if (rcb && ratio > 1.0) podreq[KE_RES_CPU] = amplify(podreq[KE_RES_CPU], ratio);
-  int64_t requested[KE_NRES] = {n->node.requested[KE_RES_CPU], n->node.requested[KE_RES_MEMORY]};
+  int64_t requested[KE_NRES] = {n->node.requested[KE_RES_CPU] + n->rv_req[KE_RES_CPU],
+                                 n->node.requested[KE_RES_MEMORY] + n->rv_req[KE_RES_MEMORY]};
   if (!(pod->requests[KE_RES_CPU] == 0 || ratio <= 1.0)) {
     if (n->node.cpu_topology_invalid) return 0;
     const int64_t allocated_milli = cpus_allocated_count(n) * 1000;
@@ -2870,6 +2873,46 @@ int or_gpu_templates_load(or_cluster* c, int32_t n, const ke_gpu_template* t) {
   return KE_OK;
 }
 
+/* BeforePreFilter's NodeInfo restore for a pod matching no reservation (transformer.go:147-300): an available
+ * reservation, not AllocateOnce with allocated pods, with allocated pods is unmatched; restoreUnmatchedReservations
+ * (transformer.go:447-473) removes its reserve pod (requests = allocatable) and adds a pod requesting
+ * SubtractWithNonNegativeResult(allocatable, allocated) unless that is zero (updateNodeInfoRequested,
+ * :491-504: NonZeroRequested with the 100m / 200Mi defaults of a zero request). */
+static const ke_node_resource* node_xres(const or_node* nd, int32_t id);
+static int64_t or_non0(int k, int64_t v) { return v != 0 ? v : (k == KE_RES_CPU ? 100 : 200LL << 20); }
+int or_reservations_load(or_cluster* c, int32_t n, const ke_reservation* rs) {
+  for (int32_t i = 0; i < n; i++)
+    if (rs[i].node < 0 || rs[i].node >= c->n) return KE_ERR_NOT_FOUND;
+  for (int32_t i = 0; i < c->n; i++)
+    for (int k = 0; k < KE_NRES; k++) c->nodes[i].rv_req[k] = c->nodes[i].rv_nz[k] = 0;
+  for (int32_t i = 0; i < n; i++) {
+    const ke_reservation* r = &rs[i];
+    if (!r->available || (r->allocate_once && r->allocated_pods > 0) || r->allocated_pods == 0) continue;
+    or_node* nd = &c->nodes[r->node];
+    int64_t rem[KE_NRES];
+    int rem_nz = 0;
+    for (int k = 0; k < KE_NRES; k++) {
+      rem[k] = r->allocatable[k] - r->allocated[k] > 0 ? r->allocatable[k] - r->allocated[k] : 0;
+      rem_nz |= rem[k] != 0;
+    }
+    for (int k = 0; k < KE_NRES; k++) {
+      nd->rv_req[k] += -r->allocatable[k] + rem[k];
+      nd->rv_nz[k] += -or_non0(k, r->allocatable[k]) + (rem_nz ? or_non0(k, rem[k]) : 0);
+    }
+  }
+  return KE_OK;
+}
+int or_node_info_requested(const or_cluster* c, int32_t node, int64_t* requested, int64_t* non_zero) {
+  if (node < 0 || node >= c->n) return KE_ERR_NOT_FOUND;
+  const or_node* nd = &c->nodes[node];
+  for (int k = 0; k < KE_NRES; k++) {
+    requested[k] = nd->node.requested[k] + nd->rv_req[k];
+    const ke_node_resource* r = node_xres(nd, k);
+    non_zero[k] = r ? r->requested + nd->rv_nz[k] : KE_ABSENT;
+  }
+  return KE_OK;
+}
+
 int or_node_device_flags(or_cluster* c, int32_t node, int32_t secondary_well_planned, int32_t gpu_model_key) {
   if (node < 0 || node >= c->n) return KE_ERR_NOT_FOUND;
   c->nodes[node].secondary_well_planned = secondary_well_planned != 0;
@@ -3093,7 +3136,9 @@ int64_t or_fitplus_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
     if (!ra) continue;
     const ke_node_resource* r = node_xres(nd, id);
     const int64_t alloc = r ? r->allocatable : 0;
-    const int64_t req = (r ? r->requested : 0) + pod_xres(pod, id);
+    /* NonZeroRequested of cpu / memory after the reservation restore */
+    const int64_t rv = r && (id == KE_RES_CPU || id == KE_RES_MEMORY) ? nd->rv_nz[id] : 0;
+    const int64_t req = (r ? r->requested + rv : 0) + pod_xres(pod, id);
     const int64_t rs = ra->type == KE_STRATEGY_MOST_ALLOCATED ? fp_most(req, alloc) : fp_least(req, alloc);
     node_score += rs * ra->weight;
     weight_sum += ra->weight;

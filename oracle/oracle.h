@@ -44,6 +44,8 @@ int64_t or_sra_score(const or_cluster* c, const ke_pod* pod, int32_t node);
 int or_set_pod_device_hints(or_cluster* c, int32_t n, const ke_pod_device_hints* hints);
 int or_gpu_templates_load(or_cluster* c, int32_t n, const ke_gpu_template* t);
 int or_node_device_flags(or_cluster* c, int32_t node, int32_t secondary_well_planned, int32_t gpu_model_key);
+int or_reservations_load(or_cluster* c, int32_t n, const ke_reservation* r);
+int or_node_info_requested(const or_cluster* c, int32_t node, int64_t* requested, int64_t* non_zero);
 int or_ds_allocate(const or_cluster* c, const ke_pod* pod, int32_t node, int32_t reserve, int32_t scored,
                    uint32_t* out3, int8_t* vf32, int32_t* reason);
 int or_last_vf_ranks(const or_cluster* c, int32_t n, int8_t* out /* [n][2][KE_MAX_MINORS] */);
