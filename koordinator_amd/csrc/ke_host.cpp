@@ -493,6 +493,8 @@ void derive_ext_row(const ke_config& cfg, const NodeState& ns, int64_t* f, uint6
   *mask = m;
 }
 
+std::atomic<uint64_t> g_dirty_epoch{0};
+
 int64_t xres_requested(const NodeState& ns, const ke_node_resource& r) {
   // cpu / memory rows carry NonZeroRequested: the reservation restore moves it too
   return r.requested + (r.id == KE_RES_CPU || r.id == KE_RES_MEMORY ? ns.rv_nz[r.id] : 0);

@@ -1,6 +1,7 @@
 // ke_host.h — host side of the evaluator: the informer-fed object state (what the reference keeps in
 // its listers, podAssignCache and NodeInfo snapshot) and its folding into GPU rows.
 #pragma once
+#include <atomic>
 #include <cstdint>
 #include <map>
 #include <string>
@@ -19,6 +20,22 @@ struct AssignedPod {
   int64_t est[KE_NRES];
   uint8_t est_present[KE_NRES];
   bool has_est;
+};
+
+// A node's "row must be re-derived" flag.  Setting it bumps a process-wide epoch, so device_refresh can skip its
+// scan over every node when no flag was set since it last cleaned them all (conservative across contexts).
+extern std::atomic<uint64_t> g_dirty_epoch;
+struct DirtyFlag {
+  bool v = true;
+  DirtyFlag() { g_dirty_epoch.fetch_add(1, std::memory_order_relaxed); }  // a new node starts dirty
+  DirtyFlag(const DirtyFlag& o) : v(o.v) { g_dirty_epoch.fetch_add(1, std::memory_order_relaxed); }
+  DirtyFlag& operator=(const DirtyFlag& o) { return *this = o.v; }
+  DirtyFlag& operator=(bool x) {
+    v = x;
+    if (x) g_dirty_epoch.fetch_add(1, std::memory_order_relaxed);
+    return *this;
+  }
+  operator bool() const { return v; }
 };
 
 struct NodeState {
@@ -52,7 +69,7 @@ struct NodeState {
   // Requested / NonZeroRequested (MilliCPU, Memory) when the rows are derived (load_reservations)
   int64_t rv_req[KE_NRES] = {0, 0}, rv_nz[KE_NRES] = {0, 0};
   // derived
-  bool dirty = true;            // row must be re-derived and uploaded
+  DirtyFlag dirty;              // row must be re-derived and uploaded
   int64_t valid_until = INT64_MAX;  // derived row is exact for now < valid_until
   // LoadAware U*(total, thr) per [variant][res] (INT64_MAX = no constraint); cached by derive_row
 };
@@ -127,6 +144,9 @@ struct Context {
   std::vector<ke_pod_device_hints> hints;
   std::vector<ke_gpu_template> tmpl;
   std::vector<ke_reservation> resv;  // ke_reservations_load
+  // device_refresh: g_dirty_epoch when every row was last clean, and the earliest valid_until then
+  uint64_t clean_epoch = UINT64_MAX;
+  int64_t min_valid_until = INT64_MIN;
   std::vector<std::vector<std::pair<int32_t, int32_t>>> label_sets{{}};
   std::map<std::vector<std::pair<int32_t, int32_t>>, int> label_set_ids{{{}, 0}};
   std::vector<int32_t> model_keys{0};

@@ -5391,13 +5391,7 @@ static int ensure_cpu(Context* ctx) {
 // Re-derive rows of dirty / time-expired nodes and scatter them into the SoA.
 int device_refresh(Context* ctx, int64_t now) {
   DeviceState* d = ctx->dev;
-  if (!ctx->pending.empty())  // a row to derive needs the deferred host mirror first
-    for (int32_t i = 0; i < ctx->n_nodes; i++)
-      if (ctx->nodes[i].dirty || now >= ctx->nodes[i].valid_until) {
-        flush_mirror(*ctx);
-        break;
-      }
-  int rc = ensure_ds(ctx);
+  int rc = ensure_ds(ctx);  // (first use marks the nodes dirty: before the checks below)
   if (rc) return rc;
   rc = ensure_numa(ctx);
   if (rc) return rc;
@@ -5405,6 +5399,14 @@ int device_refresh(Context* ctx, int64_t now) {
   if (rc) return rc;
   rc = ensure_ext(ctx);
   if (rc) return rc;
+  // nothing marked dirty since every row was last clean, and no row expired: no scan over the nodes
+  const bool all_clean = g_dirty_epoch.load(std::memory_order_relaxed) == ctx->clean_epoch && now < ctx->min_valid_until;
+  if (!all_clean && !ctx->pending.empty())  // a row to derive needs the deferred host mirror first
+    for (int32_t i = 0; i < ctx->n_nodes; i++)
+      if (ctx->nodes[i].dirty || now >= ctx->nodes[i].valid_until) {
+        flush_mirror(*ctx);
+        break;
+      }
   if (ctx->ptab_dirty) {  // GPU partition tables (ke_node_gpu_partitions); the pool only grows
     if (d->pt_words < ctx->ptab.size()) {
       if (d->soa.pt) HIP_OK(hipFree(d->soa.pt));
@@ -5427,9 +5429,13 @@ int device_refresh(Context* ctx, int64_t now) {
   std::vector<int32_t> nidx;
   std::vector<int64_t> xrows;  // ext rows of the dirty nodes
   std::vector<int32_t> xidx;
-  for (int32_t i = 0; i < ctx->n_nodes; i++) {
+  int64_t mvu = INT64_MAX;
+  for (int32_t i = 0; i < ctx->n_nodes && !all_clean; i++) {
     NodeState& ns = ctx->nodes[i];
-    if (!ns.dirty && now < ns.valid_until) continue;
+    if (!ns.dirty && now < ns.valid_until) {
+      mvu = std::min(mvu, ns.valid_until);
+      continue;
+    }
     Row r;
     int64_t vu;
     derive_row(ctx->cfg, ns, now, &r, &vu);
@@ -5464,8 +5470,13 @@ int device_refresh(Context* ctx, int64_t now) {
     }
     ns.valid_until = vu;
     ns.dirty = false;
+    mvu = std::min(mvu, vu);
     rows.push_back(r);
     idx.push_back(i);
+  }
+  if (!all_clean) {
+    ctx->clean_epoch = g_dirty_epoch.load(std::memory_order_relaxed);
+    ctx->min_valid_until = mvu;
   }
   if (!dsidx.empty()) {
     const int64_t n = (int64_t)dsidx.size();

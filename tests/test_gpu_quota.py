@@ -104,3 +104,12 @@ def test_quota_default_quota_pods(gpu, runtime):
     assert ((c >= 0) & (pods["quota"] == len(q))).sum() > 5
     assert np.array_equal(ev.last_device_allocations, o.last_device_allocations)
     assert len(ev.stats()[1]) > 0
+    # a call whose only (or last) pod is a default-quota pod refreshes the runtime total too; the
+    # calls after it admit against the refreshed limits
+    extra = synth.make_pods(12, synth.BASE_SEED + 197, key_base=9_950_000_000)
+    extra["quota"] = pods["quota"][:12]
+    extra["quota"][[0, 3, 7, 11]] = len(q)
+    placed = 0
+    for lo, hi in ((0, 1), (1, 4), (4, 8), (8, 12)):  # alone, then three calls ending in a default-quota pod
+        placed += int((check_same(ev, o, len(q), extra[lo:hi]) >= 0).sum())
+    assert placed > 0
