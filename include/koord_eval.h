@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define KE_ABI_VERSION 8
+#define KE_ABI_VERSION 9
 #define KE_ABSENT (-1)
 
 typedef struct ke_ctx ke_ctx; /* one evaluator context (ke_create) */
@@ -421,7 +421,8 @@ typedef struct ke_config {
   int32_t node_capacity;  /* max nodes this context will hold (device SoA is sized once) */
   int32_t pod_batch;      /* B: pods evaluated per speculative batch in ke_schedule      */
   int32_t global_node_offset; /* first global node index held by this shard (multi-GPU)  */
-  int32_t pad;
+  int32_t weight_reservation; /* profile Score weight of the Reservation plugin (scheduler-config.yaml:91-92:
+                                 5000); scores only pods with matched reservations (ke_pod_reservations) */
   ke_ext_args ext;        /* NodeResourcesFitPlus / ScarceResourceAvoidance (all zero = disabled) */
 } ke_config;
 
@@ -512,9 +513,8 @@ typedef struct ke_pod {
    * (PreFilter Skip), else 1 + the index of the pod's quota in the last ke_quotas_load table. */
   int16_t quota;
   uint8_t quota_non_preemptible; /* extension.IsPodNonPreemptible (label preemptible=false) */
-  uint8_t reservation_matched;   /* the pod matches or ignores a reservation (BeforePreFilter's matchedOrIgnored is
-                                    not empty for some node, transformer.go:93-145): the nominated-reservation path
-                                    is not modelled -> KE_ERR_UNSUPPORTED (see ke_reservations_load) */
+  uint8_t reservation_matched;   /* KE_RSV_*: how BeforePreFilter's matchedOrIgnored sets of this pod come about
+                                    (transformer.go:93-145); KE_RSV_MATCHED pods list theirs with ke_pod_reservations */
   /* DeviceShare allocation annotations (apis/extension/device_share.go; parsed by utils.go:355-513) */
   int64_t gpu_ring_bus_bandwidth;      /* GPUPartitionSpec.RingBusBandwidth.Value(), KE_ABSENT = nil       */
   int32_t gpu_required_topology_scope; /* DeviceAllocateHints[gpu].RequiredTopologyScope: KE_SCOPE_*       */
@@ -673,18 +673,57 @@ int ke_node_devices_delete(ke_ctx* ctx, int32_t node);
  * plugin that reads NodeInfo: NodeNUMAResource's amplified-cpu Filter and Score, NodeResourcesFitPlus.
  * A pod that matches a reservation (ke_pod.reservation_matched) is refused: its restore, the Reservation
  * plugin's Filter / Score / Reserve and the NUMA / DeviceShare reservation restores are not modelled. */
+#define KE_RSV_POLICY_DEFAULT 0    /* spec.allocatePolicy "" */
+#define KE_RSV_POLICY_ALIGNED 1    /* Aligned */
+#define KE_RSV_POLICY_RESTRICTED 2 /* Restricted (ResourceNames = the allocatable's names) */
 typedef struct ke_reservation {
   int32_t node;           /* status.nodeName as a node index                                     */
   uint8_t available;      /* IsAvailable() and no ParseError                                     */
   uint8_t allocate_once;  /* spec.allocateOnce                                                   */
-  uint8_t pad[2];
+  uint8_t allocate_policy; /* KE_RSV_POLICY_*                                                     */
+  uint8_t pad;
   int32_t allocated_pods; /* GetAllocatedPods(): owner pods assigned to it                         */
   int32_t pad2;
-  int64_t allocatable[KE_NRES]; /* status.allocatable = the reserve pod's requests: MilliCPU, Memory */
+  int64_t allocatable[KE_NRES]; /* status.allocatable = the reserve pod's requests: MilliCPU, Memory; a zero
+                                   quantity is an absent resource name */
   int64_t allocated[KE_NRES];   /* status.allocated: the owner pods' requests                     */
-} ke_reservation; /* 48 bytes */
-/* Replace the reservation set (n = 0: none). */
+  int64_t order;          /* label scheduling.koordinator.sh/reservation-order parsed (ParseInt), 0 = none */
+} ke_reservation; /* 56 bytes */
+/* Replace the reservation set (n = 0: none).  A pod placed into a reservation (below) updates its
+ * allocated / allocated_pods here (ke_reservations_get reads them back). */
 int ke_reservations_load(ke_ctx* ctx, int32_t n, const ke_reservation* reservations);
+int ke_reservations_get(ke_ctx* ctx, int32_t n, ke_reservation* out);
+
+/* Pods that match reservations (the nominated-reservation path).  ke_pod.reservation_matched: */
+#define KE_RSV_NONE 0     /* matches no reservation: the restore above only                             */
+#define KE_RSV_MATCHED 1  /* owner-matched reservations (MatchOwners, not unschedulable, taints tolerated,
+                             ReservationAffinity / exact-match spec satisfied: the integrator's label logic,
+                             transformer.go:97-146) listed with ke_pod_reservations                          */
+#define KE_RSV_AFFINITY 2 /* a required reservation affinity (Filter only on reserved resources): refused  */
+#define KE_RSV_IGNORED 3  /* reservation-ignored pod: refused                                               */
+/* For each pod of the next ke_schedule call, the reservations (indices into the loaded set) it matches,
+ * ids[offsets[p] .. offsets[p+1]).  Only KE_RSV_MATCHED pods may list any; the call consumes the lists.
+ * For a KE_RSV_MATCHED pod the evaluator runs, as the Reservation plugin and the transformer do:
+ *  - BeforePreFilter: of its listed reservations the available ones that are not AllocateOnce with
+ *    allocated pods are "matched" on their nodes; restoreMatchedReservation (transformer.go:422-445)
+ *    removes each one's reserve pod from NodeInfo (Requested and NonZeroRequested -= allocatable), the
+ *    other reservations restore as for any pod;
+ *  - Filter passes (no reservation affinity, plugin.go:351-354);
+ *  - PreScore / NominateReservation (scoring.go:42-109, nominator.go:207-278): per node the matched
+ *    reservations passing FilterNominateReservation (plugin.go:707-738: resource names shared with the pod,
+ *    fitsNode over the restored NodeInfo, fitsReservation for Restricted) are nominated by the smallest
+ *    order, else by ScoreReservation (ties -> the lowest reservation index); the feasible node holding the
+ *    smallest order (ties -> lowest node index) is preferredNode;
+ *  - Score (scoring.go:111-139): 1000 for preferredNode, else ScoreReservation of the nominated one
+ *    (MostAllocated over the reservation's allocatable, scoring.go:191-210), 0 without; DefaultNormalizeScore
+ *    over the feasible nodes; weighted by ke_config.weight_reservation into the total;
+ *  - Reserve (plugin.go:740-793, reservation_info.go:458-468): the nominated reservation of the chosen node
+ *    takes Mask(pod requests, names) into allocated and one allocated pod (ke_pod_allocation.reservation); ke_pod_release gives it back (forgetPod,
+ *    reservation_info.go:470-482).
+ * Refused (KE_ERR_UNSUPPORTED): such a pod with DeviceShare requests, cpuset binding or a NUMA topology
+ * policy, a matched reservation on a node with a NUMA topology policy, ke_eval of such a pod, a sharded
+ * context.  NodeInfo's pod-count check of fitsNode is not modelled (allowedPodNumber taken as not binding). */
+int ke_pod_reservations(ke_ctx* ctx, int32_t n_pods, const int32_t* offsets, const int32_t* ids);
 /* NodeInfo.Requested / NonZeroRequested (MilliCPU, Memory) of `node` as the plugins see it for a pod that
  * matches no reservation (after the restore above and the Reserves of past ke_schedule calls). */
 int ke_node_info_requested(ke_ctx* ctx, int32_t node, int64_t* requested /*[2]*/, int64_t* non_zero /*[2]*/);
@@ -760,7 +799,10 @@ typedef struct ke_pod_allocation {
   uint64_t device_minors;               /* bit 16*type + minor (ke_last_device_allocations)   */
   /* allocateVF: the VF rank taken on each allocated RDMA / FPGA minor, -1 = none ([type - 1][minor]) */
   int8_t vf_rank[2][KE_MAX_MINORS];
-} ke_pod_allocation; /* 208 bytes */
+  int32_t reservation;                  /* 1 + the index of the reservation the pod was assumed into (Reserve),
+                                           0 = none */
+  int32_t pad2;
+} ke_pod_allocation; /* 216 bytes */
 /* ke_pod_release modes */
 #define KE_RELEASE_UNRESERVE 0 /* the framework's Unreserve of every Reserve plugin + ForgetPod:
                                   loadaware podAssignCache.unAssign (load_aware.go:197-199),

@@ -9,7 +9,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 ABSENT = -1
 
 OK = 0
@@ -243,7 +243,7 @@ class Config(C.Structure):
         ("node_capacity", i32),
         ("pod_batch", i32),
         ("global_node_offset", i32),
-        ("pad", i32),
+        ("weight_reservation", i32),
         ("ext", ExtArgs),
     ]
 
@@ -369,12 +369,17 @@ class PodAllocation(C.Structure):
     """ke_pod_allocation: what one placement reserved (Unreserve / informer-delete record)."""
     _fields_ = [("node", i32), ("quota_assigned", u8), ("pad", u8 * 3), ("cpuset", C.c_uint64 * 4),
                 ("numa", i64 * (MAX_NUMA * NRES)), ("device_minors", C.c_uint64),
-                ("vf_rank", C.c_int8 * (2 * MAX_MINORS))]
+                ("vf_rank", C.c_int8 * (2 * MAX_MINORS)), ("reservation", i32), ("pad2", i32)]
+
+
+RSV_NONE, RSV_MATCHED, RSV_AFFINITY, RSV_IGNORED = 0, 1, 2, 3  # ke_pod.reservation_matched
+RSV_POLICY_DEFAULT, RSV_POLICY_ALIGNED, RSV_POLICY_RESTRICTED = 0, 1, 2
 
 
 class Reservation(C.Structure):  # ke_reservation
-    _fields_ = [("node", i32), ("available", u8), ("allocate_once", u8), ("pad", u8 * 2), ("allocated_pods", i32),
-                ("pad2", i32), ("allocatable", i64 * NRES), ("allocated", i64 * NRES)]
+    _fields_ = [("node", i32), ("available", u8), ("allocate_once", u8), ("allocate_policy", u8), ("pad", u8),
+                ("allocated_pods", i32), ("pad2", i32), ("allocatable", i64 * NRES), ("allocated", i64 * NRES),
+                ("order", i64)]
 
 
 STRUCTS = [Config, Node, NodeMetric, PodMetric, AggregatedUsage, Pod, ResourceMap, LoadAwareArgs, NumaArgs,
@@ -422,6 +427,7 @@ def default_config(node_capacity, pod_batch=64, device_ordinal=0, global_node_of
     cfg.weight_loadaware = 1
     cfg.weight_numa = 1
     cfg.weight_deviceshare = 1
+    cfg.weight_reservation = 5000  # config/manager/scheduler-config.yaml:91-92
     a = cfg.loadaware
     a.node_metric_expiration_seconds = 180
     a.resource_weights[:] = [1, 1]
@@ -490,6 +496,8 @@ EXPORTS = {
     "ke_gpu_templates_load": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_node_device_flags": (C.c_int, [C.c_void_p, i32, i32, i32]),
     "ke_reservations_load": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
+    "ke_reservations_get": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
+    "ke_pod_reservations": (C.c_int, [C.c_void_p, i32, C.c_void_p, C.c_void_p]),
     "ke_node_info_requested": (C.c_int, [C.c_void_p, i32, C.POINTER(i64), C.POINTER(i64)]),
     "ke_decode_pod_device_hints": (C.c_int, [C.c_char_p, i64, C.POINTER(PodDeviceHints), C.POINTER(i32)]),
     "ke_decode_device_flags": (C.c_int, [C.c_char_p, i64, C.c_char_p, i64, C.POINTER(i32), C.POINTER(i32)]),

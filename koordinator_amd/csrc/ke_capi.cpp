@@ -15,6 +15,7 @@ void device_destroy(Context* ctx);
 int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, uint8_t* status, uint8_t* reason,
                 int16_t* la, int16_t* numa, int16_t* ds, int16_t* total, int32_t* best);
 int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t* chosen, int32_t* score);
+int device_rsv_result(Context* ctx, int32_t* out4);
 int device_quota_sync(Context* ctx);
 int device_debug_rows(Context* ctx, int32_t n, Row* out);
 int device_set_profiling(Context* ctx, int32_t every);
@@ -39,13 +40,17 @@ static int check_node(ke_ctx* ctx, int32_t node) {
   return KE_OK;
 }
 
-static int check_pods(const ke_pod* pods, int32_t n, const Context* c = nullptr) {
+static int check_pods(const ke_pod* pods, int32_t n, const Context* c = nullptr, bool matched_ok = false) {
   if (n < 0 || (n > 0 && !pods)) return fail(KE_ERR_INVALID, "pods");
   for (int32_t p = 0; p < n; p++) {
     int rc = validate_pod(pods[p]);
     if (rc) return rc;
-    if (pods[p].reservation_matched)
-      return fail(KE_ERR_UNSUPPORTED, "a pod matching a reservation (the nominated-reservation path is not modelled)");
+    const uint8_t rm = pods[p].reservation_matched;
+    if (rm > KE_RSV_IGNORED) return fail(KE_ERR_INVALID, "ke_pod.reservation_matched");
+    if (rm == KE_RSV_AFFINITY) return fail(KE_ERR_UNSUPPORTED, "a pod with a required reservation affinity");
+    if (rm == KE_RSV_IGNORED) return fail(KE_ERR_UNSUPPORTED, "a reservation-ignored pod");
+    if (rm == KE_RSV_MATCHED && !matched_ok)
+      return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations outside ke_schedule");
     if (c) rc = validate_pod_hints(*c, pods[p]);
     else if (pods[p].device_hint) rc = fail(KE_ERR_INVALID, "ke_pod.device_hint without a context");
     if (rc) return rc;
@@ -77,6 +82,34 @@ static int check_cpuset(ke_ctx* ctx, const ke_pod* pods, int32_t n) {
     c.staged[p] = make_dev_pod(c.cfg, pods[p], pod_hints(c, pods[p]), &c.tmpl);
     const uint32_t f = c.staged[p].flags;
     if ((f & PF_CPUSET) || (c.n_bind_nodes > 0 && pods[p].requests[KE_RES_CPU] > 0)) c.cpu_enabled = true;
+  }
+  return KE_OK;
+}
+
+// ke_pod_reservations lists of a ke_schedule call (consumed by it): shape, and the KE_RSV_MATCHED pods the
+// nominated-reservation path supports
+static int check_matches(Context& c, const ke_pod* pods, int32_t n) {
+  const bool staged = !c.match_off.empty();
+  if (staged && (int32_t)c.match_off.size() != n + 1) {
+    c.match_off.clear();
+    c.match_ids.clear();
+    return fail(KE_ERR_INVALID, "ke_pod_reservations lists for a different number of pods");
+  }
+  for (int32_t p = 0; p < n; p++) {
+    const int32_t cnt = staged ? c.match_off[(size_t)p + 1] - c.match_off[(size_t)p] : 0;
+    if (pods[p].reservation_matched != KE_RSV_MATCHED) {
+      if (cnt) return fail(KE_ERR_INVALID, "reservations listed for a pod that is not KE_RSV_MATCHED");
+      continue;
+    }
+    if (!staged) return fail(KE_ERR_INVALID, "a KE_RSV_MATCHED pod without ke_pod_reservations");
+    const uint32_t f = c.staged[(size_t)p].flags;
+    bool scalar = pods[p].has_other_requests || pods[p].has_unsupported_device_requests;
+    for (int r = KE_NRES; r < KE_RES_COUNT; r++) scalar = scalar || pods[p].requests[r] != 0;
+    for (int r = 0; r < KE_PDR_COUNT; r++) scalar = scalar || pods[p].device_requests[r] != 0;
+    if ((f & (PF_DS | PF_DS_HINT | PF_CPUSET)) || scalar)
+      return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations with device, cpuset or scalar requests");
+    if (pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE || (c.n_bind_nodes > 0 && pods[p].requests[KE_RES_CPU] > 0))
+      return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations with a NUMA policy or that may bind CPUs");
   }
   return KE_OK;
 }
@@ -288,6 +321,26 @@ int ke_reservations_load(ke_ctx* ctx, int32_t n, const ke_reservation* reservati
   if (!ctx) return fail(KE_ERR_INVALID, "null context");
   flush_mirror(ctx->c);
   return load_reservations(ctx->c, n, reservations);
+}
+
+int ke_reservations_get(ke_ctx* ctx, int32_t n, ke_reservation* out) {
+  if (!ctx || n < 0 || (n > 0 && !out) || n > (int32_t)ctx->c.resv.size()) return fail(KE_ERR_INVALID, "ke_reservations_get arguments");
+  std::copy(ctx->c.resv.begin(), ctx->c.resv.begin() + n, out);
+  return KE_OK;
+}
+
+int ke_pod_reservations(ke_ctx* ctx, int32_t n_pods, const int32_t* offsets, const int32_t* ids) {
+  if (!ctx || n_pods < 0 || !offsets) return fail(KE_ERR_INVALID, "ke_pod_reservations arguments");
+  Context& c = ctx->c;
+  if (offsets[0] != 0) return fail(KE_ERR_INVALID, "ke_pod_reservations offsets[0] != 0");
+  for (int32_t p = 0; p < n_pods; p++)
+    if (offsets[p + 1] < offsets[p]) return fail(KE_ERR_INVALID, "ke_pod_reservations offsets decrease");
+  if (offsets[n_pods] > 0 && !ids) return fail(KE_ERR_INVALID, "ke_pod_reservations ids");
+  for (int32_t j = 0; j < offsets[n_pods]; j++)
+    if (ids[j] < 0 || ids[j] >= (int32_t)c.resv.size()) return fail(KE_ERR_NOT_FOUND, "ke_pod_reservations: reservation index");
+  c.match_off.assign(offsets, offsets + n_pods + 1);
+  c.match_ids.assign(ids, ids + offsets[n_pods]);
+  return KE_OK;
 }
 
 int ke_node_info_requested(ke_ctx* ctx, int32_t node, int64_t* requested, int64_t* non_zero) {
@@ -552,7 +605,7 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
   if (!ctx || (n_pods > 0 && !chosen)) return fail(KE_ERR_INVALID, "ke_schedule arguments");
   using clk = std::chrono::steady_clock;
   auto tp = clk::now();
-  int rc = check_pods(pods, n_pods, &ctx->c);
+  int rc = check_pods(pods, n_pods, &ctx->c, true);
   if (rc) return rc;
   rc = check_numa_deviceshare(ctx, pods, n_pods);
   if (rc) return rc;
@@ -561,6 +614,8 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
   for (int32_t p = 0; p < n_pods; p++)
     if (pods[p].quota < 0 || pods[p].quota > (int32_t)ctx->c.quotas.size())
       return fail(KE_ERR_INVALID, "ke_pod.quota outside the loaded ElasticQuota tree");
+  rc = check_matches(ctx->c, pods, n_pods);
+  if (rc) return rc;
   rc = require_device(ctx);
   if (rc) return rc;
   ctx->c.host_ms[0] = std::chrono::duration<double, std::milli>(clk::now() - tp).count();
@@ -582,13 +637,34 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
   double all_ms = 0;
   bool numa_out = false, multi = false;
   const int32_t off = c.cfg.global_node_offset;
+  // A pod with matched reservations (KE_RSV_MATCHED with a non-empty list) is a segment of its own: its
+  // rows carry its matched restore and k_rsv_pick adds the Reservation score (resv_prepare / resv_finish).
+  std::vector<int32_t> moff, mids;
+  moff.swap(c.match_off);  // consumed by this call
+  mids.swap(c.match_ids);
+  auto matched = [&](int32_t p) { return !moff.empty() && moff[(size_t)p + 1] > moff[(size_t)p]; };
+  std::vector<int32_t> assumed((size_t)n_pods, 0);
   for (int32_t s0 = 0; s0 < n_pods || (n_pods == 0 && s0 == 0);) {
     int32_t s1 = s0;
-    while (s1 < n_pods && !barrier(s1)) s1++;
-    if (s1 < n_pods) s1++;  // the barrier pod ends its segment
+    while (s1 < n_pods && !barrier(s1) && !matched(s1)) s1++;
+    if (s1 < n_pods && (s1 == s0 || !matched(s1))) s1++;  // a barrier pod ends its segment; a matched one is alone
     const int32_t len = s1 - s0;
+    const bool rsv = len == 1 && matched(s0);
+    if (rsv) {
+      rc = resv_prepare(c, pods[s0], mids.data() + moff[(size_t)s0], moff[(size_t)s0 + 1] - moff[(size_t)s0]);
+      if (rc) return rc;
+    }
     rc = device_schedule(&c, len, pods + s0, now_ns, chosen + (n_pods ? s0 : 0), score ? score + s0 : nullptr);
     if (rc) return rc;
+    if (rsv) {
+      const int32_t local = chosen[s0] < 0 ? -1 : chosen[s0] - off;
+      int32_t pick[4] = {local, 0, 0, -1};  // no usable matched reservation: no Reservation score
+      if (!c.rsv_pairs.empty()) rc = device_rsv_result(&c, pick);
+      if (rc) return rc;
+      if (local >= 0 && local != pick[0]) return fail(KE_ERR_DEVICE, "k_rsv_pick winner differs from the placement");
+      if (local >= 0 && score) score[s0] += (int32_t)c.cfg.weight_reservation * pick[1];
+      resv_finish(c, local, pods[s0], &assumed[(size_t)s0]);
+    }
     if (n_pods == 0) break;
     tp = clk::now();
     // Host mirror of the Reserves the device already applied to its rows: keep the object state
@@ -655,6 +731,7 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
   c.last_chosen.assign(chosen, chosen + n_pods);
   c.last_uid.resize((size_t)n_pods);
   c.last_quota.resize((size_t)n_pods);
+  c.last_resv.swap(assumed);
   for (int32_t p = 0; p < n_pods; p++) {
     c.last_uid[(size_t)p] = pods[p].uid;
     c.last_quota[(size_t)p] = chosen[p] >= 0 && pods[p].quota > 0 && !c.quotas.empty();
@@ -668,6 +745,7 @@ static ke_pod_allocation last_allocation(const Context& c, int32_t p) {
   memset(a.vf_rank, -1, sizeof a.vf_rank);
   a.node = p < (int32_t)c.last_chosen.size() ? c.last_chosen[(size_t)p] : -1;
   if (a.node < 0) return a;
+  a.reservation = p < (int32_t)c.last_resv.size() ? c.last_resv[(size_t)p] : 0;
   a.quota_assigned = c.last_quota[(size_t)p];
   constexpr int W = KE_MAX_NUMA * KE_NRES;
   for (int q = 0; q < 4; q++)
@@ -700,8 +778,11 @@ int ke_pod_release(ke_ctx* ctx, const ke_pod* pod, const ke_pod_allocation* allo
     return fail(KE_ERR_INVALID, "ke_pod.quota outside the loaded ElasticQuota tree");
   const int32_t node = alloc->node < 0 ? -1 : alloc->node - c.cfg.global_node_offset;
   if (node >= c.cfg.node_capacity) return fail(KE_ERR_NOT_FOUND, "ke_pod_release: node index out of range");
+  if (alloc->reservation < 0 || alloc->reservation > (int32_t)c.resv.size())
+    return fail(KE_ERR_NOT_FOUND, "ke_pod_release: reservation index");
   if (node >= 0 && c.nodes[(size_t)node].valid)  // (a node of another context's range: only the quota part)
     host_release_node(c.cfg, c.ext_enabled, c.nodes[(size_t)node], *pod, *alloc, pod_hints(c, *pod));
+  if (node >= 0 && alloc->reservation > 0) resv_forget(c, alloc->reservation - 1, *pod);
   const bool assigned = alloc->node >= 0 && alloc->quota_assigned;
   if (pod->quota > 0 && (assigned || mode == KE_RELEASE_DELETE)) {
     if (c.dev) {

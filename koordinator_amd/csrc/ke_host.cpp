@@ -39,6 +39,7 @@ int validate_config(const ke_config& cfg) {
     return fail(KE_ERR_INVALID, "node_capacity out of range (1 .. 2^23-1 per shard)");
   if (cfg.pod_batch < 1 || cfg.pod_batch > MAX_BATCH) return fail(KE_ERR_INVALID, "pod_batch out of range (1..64)");
   const ke_ext_args& x = cfg.ext;
+  if (cfg.weight_reservation < 0) return fail(KE_ERR_INVALID, "negative Reservation weight");
   if (cfg.weight_loadaware < 0 || cfg.weight_numa < 0 || cfg.weight_deviceshare < 0 || x.weight_fitplus < 0 ||
       x.weight_sra < 0 ||
       (cfg.weight_loadaware + cfg.weight_numa + cfg.weight_deviceshare + x.weight_fitplus + x.weight_sra) * 100 >
@@ -500,32 +501,33 @@ int64_t xres_requested(const NodeState& ns, const ke_node_resource& r) {
   return r.requested + (r.id == KE_RES_CPU || r.id == KE_RES_MEMORY ? ns.rv_nz[r.id] : 0);
 }
 
-// The reservation cache's NodeInfo restore for a pod that matches no reservation (BeforePreFilter,
-// transformer.go:147-300): an available reservation (not AllocateOnce with allocated pods) that has
-// allocated pods is "unmatched", and restoreUnmatchedReservations (transformer.go:447-473) removes its reserve
-// pod (requests = allocatable) from NodeInfo and adds back a pod requesting SubtractWithNonNegativeResult(
-// allocatable, allocated) when that is not zero; updateNodeInfoRequested's NonZeroRequested uses the 100m /
-// 200Mi defaults of a zero cpu / memory request (the reserve pod taken as one container).
-int load_reservations(Context& c, int32_t n, const ke_reservation* rs) {
-  if (n < 0 || (n > 0 && !rs)) return fail(KE_ERR_INVALID, "reservations");
-  for (int32_t i = 0; i < n; i++) {
-    const ke_reservation& r = rs[i];
-    if (r.node < 0 || r.node >= c.n_nodes) return fail(KE_ERR_NOT_FOUND, "reservation node index");
-    if (r.allocated_pods < 0) return fail(KE_ERR_INVALID, "negative reservation allocated pods");
-    for (int k = 0; k < KE_NRES; k++)
-      if (r.allocatable[k] < 0 || r.allocated[k] < 0) return fail(KE_ERR_INVALID, "negative reservation quantity");
-  }
-  for (const ke_reservation& r : c.resv) {  // the old restore leaves
-    NodeState& ns = c.nodes[r.node];
-    for (int k = 0; k < KE_NRES; k++) ns.rv_req[k] = ns.rv_nz[k] = 0;
-    ns.dirty = true;
-  }
-  c.resv.assign(rs, rs + n);
-  auto non0 = [](int k, int64_t v) { return v != 0 ? v : (k == KE_RES_CPU ? 100 : 200LL << 20); };
-  for (const ke_reservation& r : c.resv) {
-    NodeState& ns = c.nodes[r.node];
-    ns.dirty = true;
-    if (!r.available || (r.allocate_once && r.allocated_pods > 0) || r.allocated_pods == 0) continue;
+// The reservation cache's NodeInfo restore (BeforePreFilter, transformer.go:147-300).  A reservation that is
+// available and not AllocateOnce with allocated pods takes part (transformer.go:181-190); for a pod that does
+// not match it, it is "unmatched" when it has allocated pods and restoreUnmatchedReservations
+// (transformer.go:447-473) removes its reserve pod (requests = allocatable) from NodeInfo and adds back a pod
+// requesting SubtractWithNonNegativeResult(allocatable, allocated) when that is not zero; for a pod that
+// matches it, restoreMatchedReservation (:422-445) removes the reserve pod.  updateNodeInfoRequested /
+// NodeInfo.RemovePod move NonZeroRequested with the 100m / 200Mi defaults of a zero cpu / memory request
+// (the reserve pod taken as one container).
+static int64_t resv_non0(int k, int64_t v) { return v != 0 ? v : (k == KE_RES_CPU ? 100 : 200LL << 20); }
+bool resv_usable(const ke_reservation& r) { return r.available && !(r.allocate_once && r.allocated_pods > 0); }
+
+// node's Requested / NonZeroRequested deltas with `matched` (by reservation index, nullptr = none) matched
+static void resv_delta(const Context& c, int32_t node, const std::vector<char>* matched, bool with_matched,
+                       int64_t* req, int64_t* nz) {
+  for (int k = 0; k < KE_NRES; k++) req[k] = nz[k] = 0;
+  for (int32_t i : c.resv_by_node[(size_t)node]) {
+    const ke_reservation& r = c.resv[(size_t)i];
+    if (!resv_usable(r)) continue;
+    if (matched && (*matched)[(size_t)i]) {
+      if (!with_matched) continue;
+      for (int k = 0; k < KE_NRES; k++) {
+        req[k] -= r.allocatable[k];
+        nz[k] -= resv_non0(k, r.allocatable[k]);
+      }
+      continue;
+    }
+    if (r.allocated_pods == 0) continue;
     int64_t rem[KE_NRES];
     bool rem_nz = false;
     for (int k = 0; k < KE_NRES; k++) {
@@ -533,11 +535,170 @@ int load_reservations(Context& c, int32_t n, const ke_reservation* rs) {
       rem_nz = rem_nz || rem[k] != 0;
     }
     for (int k = 0; k < KE_NRES; k++) {
-      ns.rv_req[k] += -r.allocatable[k] + rem[k];
-      ns.rv_nz[k] += -non0(k, r.allocatable[k]) + (rem_nz ? non0(k, rem[k]) : 0);
+      req[k] += -r.allocatable[k] + rem[k];
+      nz[k] += -resv_non0(k, r.allocatable[k]) + (rem_nz ? resv_non0(k, rem[k]) : 0);
     }
   }
+}
+
+void resv_node_restore(Context& c, int32_t node) {
+  NodeState& ns = c.nodes[(size_t)node];
+  resv_delta(c, node, nullptr, false, ns.rv_req, ns.rv_nz);
+  ns.dirty = true;
+}
+
+int load_reservations(Context& c, int32_t n, const ke_reservation* rs) {
+  if (n < 0 || (n > 0 && !rs)) return fail(KE_ERR_INVALID, "reservations");
+  for (int32_t i = 0; i < n; i++) {
+    const ke_reservation& r = rs[i];
+    if (r.node < 0 || r.node >= c.n_nodes) return fail(KE_ERR_NOT_FOUND, "reservation node index");
+    if (r.allocated_pods < 0) return fail(KE_ERR_INVALID, "negative reservation allocated pods");
+    if (r.allocate_policy > KE_RSV_POLICY_RESTRICTED) return fail(KE_ERR_INVALID, "reservation allocate policy");
+    for (int k = 0; k < KE_NRES; k++)
+      if (r.allocatable[k] < 0 || r.allocated[k] < 0) return fail(KE_ERR_INVALID, "negative reservation quantity");
+  }
+  std::vector<int32_t> old;
+  for (const ke_reservation& r : c.resv) old.push_back(r.node);
+  c.resv.assign(rs, rs + n);
+  c.resv_by_node.assign(c.nodes.size(), {});
+  for (int32_t i = 0; i < n; i++) c.resv_by_node[(size_t)rs[i].node].push_back(i);
+  for (int32_t node : old) resv_node_restore(c, node);  // the old restore leaves
+  for (const ke_reservation& r : c.resv) resv_node_restore(c, r.node);
+  c.last_resv.clear();  // release records of earlier calls no longer name these reservations
   return KE_OK;
+}
+
+// FilterNominateReservation -> filterWithReservations(..., requiredFromReservation = true) for one matched
+// reservation (plugin.go:351-442, 707-738): a resource name shared with the pod, fitsNode over the restored
+// NodeInfo (plugin.go:447-497; preemptible empty; the pod-count check not modelled) and, for Restricted,
+// fitsReservation (plugin.go:499-569).  podRequested = Requested after the unmatched restore only,
+// allRAllocated = Σ allocated of the node's matched reservations.
+static bool resv_nominable(const ke_reservation& r, const ke_pod& pod, const int64_t* alloc, const int64_t* pod_requested,
+                           const int64_t* all_allocated) {
+  bool shared = false;
+  for (int k = 0; k < KE_NRES; k++) shared = shared || (r.allocatable[k] != 0 && pod.requests[k] != 0);
+  if (!shared) return false;
+  bool node_fits = true;
+  if (pod.requests[KE_RES_CPU] != 0 || pod.requests[KE_RES_MEMORY] != 0)
+    for (int k = 0; k < KE_NRES; k++) {
+      const int64_t remained = r.allocatable[k] > r.allocated[k] ? r.allocatable[k] - r.allocated[k] : 0;  // GetAvailable
+      if (pod.requests[k] > alloc[k] - (pod_requested[k] - remained - all_allocated[k])) node_fits = false;
+    }
+  bool resv_fits = node_fits;
+  if (r.allocate_policy == KE_RSV_POLICY_RESTRICTED) {
+    resv_fits = true;
+    for (int k = 0; k < KE_NRES; k++)  // requests masked to the reservation's names; zero requests skipped
+      if (r.allocatable[k] != 0 && pod.requests[k] != 0 && pod.requests[k] > r.allocatable[k] - r.allocated[k])
+        resv_fits = false;
+  }
+  return node_fits && resv_fits;
+}
+
+// scoreReservation (scoring.go:191-210): MostAllocated of (pod requests + allocated) over the reservation's
+// non-zero allocatable, 100 * req / capacity per resource that fits, averaged
+int32_t resv_score(const ke_reservation& r, const ke_pod& pod) {
+  int64_t s = 0, w = 0;
+  for (int k = 0; k < KE_NRES; k++) {
+    if (r.allocatable[k] == 0) continue;
+    w++;
+    const int64_t req = pod.requests[k] + r.allocated[k];
+    if (req <= r.allocatable[k]) s += 100 * req / r.allocatable[k];  // MilliValue ratio: the same quotient
+  }
+  return w ? (int32_t)(s / w) : 0;
+}
+
+int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids) {
+  c.rsv_pairs.clear();
+  c.rsv_nominated.clear();
+  c.rsv_nodes.clear();
+  std::vector<char> m(c.resv.size(), 0);
+  for (int32_t j = 0; j < n_ids; j++) {
+    if (ids[j] < 0 || ids[j] >= (int32_t)c.resv.size()) return fail(KE_ERR_NOT_FOUND, "matched reservation index");
+    if (resv_usable(c.resv[(size_t)ids[j]])) m[(size_t)ids[j]] = 1;
+  }
+  for (int32_t j = 0; j < n_ids; j++)
+    if (m[(size_t)ids[j]]) c.rsv_nodes.push_back(c.resv[(size_t)ids[j]].node);
+  std::sort(c.rsv_nodes.begin(), c.rsv_nodes.end());
+  c.rsv_nodes.erase(std::unique(c.rsv_nodes.begin(), c.rsv_nodes.end()), c.rsv_nodes.end());
+  for (int32_t node : c.rsv_nodes)
+    if (c.nodes[(size_t)node].node.numa_topology_policy != KE_NUMA_POLICY_NONE)
+      return fail(KE_ERR_UNSUPPORTED, "a matched reservation on a node with a NUMA topology policy");
+  flush_mirror(c);  // NodeInfo.Requested with every earlier placement
+  for (int32_t node : c.rsv_nodes) {
+    NodeState& ns = c.nodes[(size_t)node];
+    int64_t ureq[KE_NRES], unz[KE_NRES], pod_requested[KE_NRES], all_alloc[KE_NRES] = {0, 0};
+    resv_delta(c, node, &m, false, ureq, unz);
+    for (int k = 0; k < KE_NRES; k++) pod_requested[k] = ns.node.requested[k] + ureq[k];
+    std::vector<int32_t> mine;
+    int64_t order = 0;  // findMostPreferredReservationByOrder over all matched (scoring.go:170-189)
+    for (int32_t i : c.resv_by_node[(size_t)node])
+      if (m[(size_t)i]) {
+        mine.push_back(i);
+        for (int k = 0; k < KE_NRES; k++) all_alloc[k] += c.resv[(size_t)i].allocated[k];
+        const int64_t o = c.resv[(size_t)i].order;
+        if (o != 0 && (order == 0 || o < order)) order = o;
+      }
+    std::vector<int32_t> ok;
+    for (int32_t i : mine)
+      if (resv_nominable(c.resv[(size_t)i], pod, ns.node.allocatable, pod_requested, all_alloc)) ok.push_back(i);
+    // NominateReservation (nominator.go:237-277): the only one, else the smallest order, else the best
+    // ScoreReservation (ties -> lowest index: sort.Slice's insertion sort keeps them below 13 elements)
+    int32_t nom = -1;
+    if (ok.size() == 1) nom = ok[0];
+    if (ok.size() > 1) {
+      int64_t bo = 0;
+      for (int32_t i : ok) {
+        const int64_t o = c.resv[(size_t)i].order;
+        if (o != 0 && (bo == 0 || o < bo)) {
+          bo = o;
+          nom = i;
+        }
+      }
+      if (nom < 0) {
+        int32_t bs = -1;
+        for (int32_t i : ok) {
+          const int32_t sc = resv_score(c.resv[(size_t)i], pod);
+          if (sc > bs) {
+            bs = sc;
+            nom = i;
+          }
+        }
+      }
+    }
+    c.rsv_pairs.push_back({node, nom >= 0 ? resv_score(c.resv[(size_t)nom], pod) : 0, order});
+    c.rsv_nominated.push_back(nom);
+    // the rows this pod sees: its matched reservations restored too
+    resv_delta(c, node, &m, true, ns.rv_req, ns.rv_nz);
+    ns.dirty = true;
+  }
+  return KE_OK;
+}
+
+void resv_finish(Context& c, int32_t chosen_local, const ke_pod& pod, int32_t* assumed) {
+  *assumed = 0;
+  for (size_t j = 0; j < c.rsv_nodes.size(); j++)
+    if (c.rsv_nodes[j] == chosen_local && c.rsv_nominated[j] >= 0) {
+      // assumePod -> AddAssignedPod (reservation_info.go:458-468): Mask(requests, ResourceNames)
+      ke_reservation& r = c.resv[(size_t)c.rsv_nominated[j]];
+      for (int k = 0; k < KE_NRES; k++)
+        if (r.allocatable[k] != 0) r.allocated[k] += pod.requests[k];
+      r.allocated_pods++;
+      *assumed = 1 + c.rsv_nominated[j];
+    }
+  for (int32_t node : c.rsv_nodes) resv_node_restore(c, node);
+  c.rsv_pairs.clear();
+  c.rsv_nominated.clear();
+  c.rsv_nodes.clear();
+}
+
+// forgetPod -> RemoveAssignedPod (reservation_info.go:470-482)
+void resv_forget(Context& c, int32_t idx, const ke_pod& pod) {
+  if (idx < 0 || idx >= (int32_t)c.resv.size()) return;
+  ke_reservation& r = c.resv[(size_t)idx];
+  for (int k = 0; k < KE_NRES; k++)
+    if (r.allocatable[k] != 0) r.allocated[k] = std::max<int64_t>(0, r.allocated[k] - pod.requests[k]);
+  if (r.allocated_pods > 0) r.allocated_pods--;
+  resv_node_restore(c, r.node);
 }
 
 // host mirror of a placement's ext Reserve: NodeInfo (NonZero)Requested += the pod's requests by id

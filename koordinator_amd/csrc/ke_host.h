@@ -38,6 +38,13 @@ struct DirtyFlag {
   operator bool() const { return v; }
 };
 
+// one node holding reservations a pod matches (k_rsv_pick)
+struct RsvPair {
+  int32_t node;   // local node index
+  int32_t raw;    // ScoreReservation of the nominated reservation (0 = none)
+  int64_t order;  // smallest reservation-order label of the matched reservations (0 = none)
+};
+
 struct NodeState {
   bool valid = false;
   ke_node node{};
@@ -143,7 +150,16 @@ struct Context {
   // model keys (id -> ke_label_id of "<vendor>-<model>", id 0 = none); the VF ranks of the last ke_schedule
   std::vector<ke_pod_device_hints> hints;
   std::vector<ke_gpu_template> tmpl;
-  std::vector<ke_reservation> resv;  // ke_reservations_load
+  std::vector<ke_reservation> resv;  // ke_reservations_load (allocated / allocated_pods kept by Reserve)
+  std::vector<std::vector<int32_t>> resv_by_node;  // reservation indices per node
+  // ke_pod_reservations staging for the next ke_schedule: CSR over its pods
+  std::vector<int32_t> match_off, match_ids;
+  // the KE_RSV_MATCHED pod of the current segment: its nodes with matched reservations, their
+  // (node, ScoreReservation of the nominated one, smallest order) for the device pick, the nominated index
+  std::vector<int32_t> rsv_nodes;
+  std::vector<RsvPair> rsv_pairs;
+  std::vector<int32_t> rsv_nominated;
+  std::vector<int32_t> last_resv;  // per pod of the last ke_schedule: 1 + the reservation assumed, 0 = none
   // device_refresh: g_dirty_epoch when every row was last clean, and the earliest valid_until then
   uint64_t clean_epoch = UINT64_MAX;
   int64_t min_valid_until = INT64_MIN;
@@ -226,6 +242,14 @@ int validate_node_resources(int32_t n, const ke_node_resource* r);
 // the ext SoA row of a node: NUM_XF int64 + the uint64 mask of resource ids with Allocatable > 0
 void derive_ext_row(const ke_config& cfg, const NodeState& ns, int64_t* f, uint64_t* mask);
 int load_reservations(Context& c, int32_t n, const ke_reservation* r);
+bool resv_usable(const ke_reservation& r);
+void resv_node_restore(Context& c, int32_t node);  // the restore every non-matching pod sees
+int32_t resv_score(const ke_reservation& r, const ke_pod& pod);
+// the nominated-reservation path of one KE_RSV_MATCHED pod: rows with its matched restore, rsv_pairs /
+// rsv_nominated; resv_finish assumes the pod into the chosen node's nominated reservation (1 + index, 0)
+int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids);
+void resv_finish(Context& c, int32_t chosen_local, const ke_pod& pod, int32_t* assumed);
+void resv_forget(Context& c, int32_t idx, const ke_pod& pod);
 // NodeResourcesFitPlus' (NonZero)Requested of resource `id` on the node, with the reservation restore
 int64_t xres_requested(const NodeState& ns, const ke_node_resource& r);
 void host_ext_reserve(NodeState& ns, const ke_pod& pod);

@@ -3087,6 +3087,73 @@ __global__ __launch_bounds__(256) void k_argmax1(const uint16_t* __restrict__ sc
   if (blockIdx.x == 0 && threadIdx.x == 0) cand_cnt[0] = 1;
 }
 
+// The Reservation plugin for a singleton batch whose pod matches reservations, after
+// k_argmax1: one wave over the K nodes holding matched reservations (the other nodes score 0).
+//   1. PreScore's preferredNode (reservation/scoring.go:97-107): the feasible node with the smallest
+//      reservation order != 0, ties -> lowest node index; it scores mostPreferredScore 1000 (:118-120);
+//   2. DefaultNormalizeScore (:134-139): n = 100 * raw / max over the feasible nodes (all 0 when max is 0);
+//   3. selectHost over total + w * n: a 64-bit key over the K nodes against k_argmax1's winner (n = 0).
+// cand[0] becomes the winner's 32-bit key (its plugin total without the Reservation part); out = {winner
+// node or -1, its n, max, preferredNode or -1}.
+__global__ __launch_bounds__(64) void k_rsv_pick(const uint16_t* __restrict__ scores, const RsvPair* __restrict__ pr,
+                                                 int K, int64_t w, uint32_t* __restrict__ cand, int32_t* __restrict__ out) {
+  const int l = (int)threadIdx.x;
+  int64_t bo = INT64_MAX;
+  int32_t bn = INT32_MAX;
+  for (int i = l; i < K; i += 64) {
+    const RsvPair q = pr[i];
+    if (q.order != 0 && scores[q.node] && (q.order < bo || (q.order == bo && q.node < bn))) {
+      bo = q.order;
+      bn = q.node;
+    }
+  }
+  for (int m = 32; m; m >>= 1) {
+    const int64_t o2 = __shfl_xor(bo, m);
+    const int32_t n2 = __shfl_xor(bn, m);
+    if (o2 < bo || (o2 == bo && n2 < bn)) {
+      bo = o2;
+      bn = n2;
+    }
+  }
+  const int32_t pref = bo == INT64_MAX ? -1 : bn;
+  int32_t mx = 0;
+  for (int i = l; i < K; i += 64) {
+    const RsvPair q = pr[i];
+    if (scores[q.node]) mx = max(mx, q.node == pref ? 1000 : q.raw);
+  }
+  for (int m = 32; m; m >>= 1) mx = max(mx, __shfl_xor(mx, m));
+  const uint32_t g = cand[0];  // k_argmax1's key: (total + 1) << KEY_IDX_BITS | (mask - node), 0 = none
+  uint64_t best = g;
+  if (mx > 0)
+    for (int i = l; i < K; i += 64) {
+      const RsvPair q = pr[i];
+      const uint32_t v = scores[q.node];
+      if (!v) continue;
+      const int64_t n = 100 * (int64_t)(q.node == pref ? 1000 : q.raw) / mx;
+      const uint64_t key = ((uint64_t)(v + w * n) << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)q.node);
+      best = key > best ? key : best;
+    }
+  for (int m = 32; m; m >>= 1) {
+    const uint64_t o = __shfl_xor(best, m);
+    best = o > best ? o : best;
+  }
+  const int32_t win = best ? (int32_t)(KEY_IDX_MASK - (uint32_t)(best & KEY_IDX_MASK)) : -1;
+  int32_t nw = 0;  // the winner's n (0 unless it holds matched reservations)
+  if (win >= 0 && mx > 0)
+    for (int i = l; i < K; i += 64) {
+      const RsvPair q = pr[i];
+      if (q.node == win) nw = (int32_t)(100 * (int64_t)(q.node == pref ? 1000 : q.raw) / mx);
+    }
+  for (int m = 32; m; m >>= 1) nw = max(nw, __shfl_xor(nw, m));
+  if (l == 0) {
+    if (win >= 0) cand[0] = ((uint32_t)scores[win] << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)win);
+    out[0] = win;
+    out[1] = nw;
+    out[2] = mx;
+    out[3] = pref;
+  }
+}
+
 // The deferred BestEffort pairs of an eval launch: one wavefront per pair computes mergeFilteredHints
 // over the full provider lists (numa_best_effort_fallback's result), then lane 0 evaluates the pair
 // with it.  A DeviceShare pod's pair is deferred only on a node without a device cache (DeviceShare has
@@ -5094,6 +5161,10 @@ struct DeviceState {
   hipEvent_t ev_sel[EV_RING] = {};  // a batch's candidate lists done (estream)
   hipEvent_t ev_start = nullptr;
   bool pipeline = true;             // ke_set_pipeline
+  // the Reservation plugin of a singleton batch (k_rsv_pick): its pairs and result words
+  RsvPair* d_rsv = nullptr;
+  int64_t rsv_cap = 0;              // bytes
+  int32_t* d_rsv_out = nullptr;     // [4]
 };
 
 // Contiguous node range of shard `rank`: 512-aligned chunks (k_select's 16-B loads stay aligned).
@@ -5163,6 +5234,15 @@ int device_create(Context* ctx) {
   d->soa.dsraw = d->d_dsraw;
   HIP_OK(hipMalloc(&d->d_aff, d->capacity));
   HIP_OK(hipMalloc(&d->d_split, sizeof(uint32_t) * GATH_WORDS_MAX * MAX_WORLD));
+  HIP_OK(hipMalloc(&d->d_rsv_out, sizeof(int32_t) * 4));
+  HIP_OK(hipStreamSynchronize(d->stream));
+  return KE_OK;
+}
+
+// k_rsv_pick's result of the last device_schedule (a segment of one KE_RSV_MATCHED pod)
+int device_rsv_result(Context* ctx, int32_t* out4) {
+  DeviceState* d = ctx->dev;
+  HIP_OK(hipMemcpyAsync(out4, d->d_rsv_out, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipStreamSynchronize(d->stream));
   return KE_OK;
 }
@@ -5180,7 +5260,7 @@ void device_destroy(Context* ctx) {
                   d->d_numaalloc, d->d_numarows, d->d_defer, d->d_defer_cnt, d->soa.cs, d->soa.cpu,
                   d->d_cpurows, d->d_cpusets, d->d_aff, d->soa.qt, d->soa.qm, d->d_sched, d->d_stale,
                   d->d_stale_cnt, d->d_trows, d->d_tcnt, d->d_chg, d->soa.rec, d->soa.pt, d->soa.kerr,
-                  d->soa.xf, d->soa.xm, d->d_xrows, d->soa.dsx, d->d_ph, d->d_vfo};
+                  d->soa.xf, d->soa.xm, d->d_xrows, d->soa.dsx, d->d_ph, d->d_vfo, d->d_rsv, d->d_rsv_out};
   if (d->estream) (void)hipStreamSynchronize(d->estream);
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -5765,6 +5845,16 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     HIP_OK(hipMemsetAsync(d->d_defer_cnt, 0, sizeof(uint32_t) * n_batches, d->stream));
   }
   KArgs k = make_kargs(ctx, now);
+  if (!ctx->rsv_pairs.empty()) {  // one KE_RSV_MATCHED pod (ke_schedule's segment of its own)
+    if (n_pods != 1 || d->world > 1 || d->comm) return fail(KE_ERR_UNSUPPORTED, "matched reservations need an unsharded singleton");
+    for (const RsvPair& q : ctx->rsv_pairs)
+      if (q.node < 0 || q.node >= ctx->n_nodes) return fail(KE_ERR_DEVICE, "reservation pair node out of range");
+    rc = ensure((void**)&d->d_rsv, &d->rsv_cap, (int64_t)sizeof(RsvPair) * (int64_t)ctx->rsv_pairs.size());
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(d->d_rsv, ctx->rsv_pairs.data(), sizeof(RsvPair) * ctx->rsv_pairs.size(), hipMemcpyHostToDevice,
+                          d->stream));
+    HIP_OK(hipMemsetAsync(d->d_rsv_out, 0xFF, sizeof(int32_t) * 4, d->stream));
+  }
   const bool quota = !ctx->quotas.empty();  // ElasticQuota admission + Reserve in the Reserve kernels
   if (quota) {
     if (ctx->quota_dirty) {
@@ -5906,6 +5996,9 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       if (argmax1) {  // d_cand[0] zeroed by k_batch_begin
         hipLaunchKernelGGL((ds ? k_argmax1<true> : k_argmax1<false>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
                            es, d->d_scores, 0, N, d->d_dsraw, d->d_dsmax, k.wp_ds, d->d_cand, d->d_cand_cnt);
+        if (!ctx->rsv_pairs.empty())  // the pod's matched reservations: the Reservation plugin's score
+          hipLaunchKernelGGL(k_rsv_pick, dim3(1), dim3(64), 0, es, d->d_scores, d->d_rsv, (int)ctx->rsv_pairs.size(),
+                             (int64_t)ctx->cfg.weight_reservation, d->d_cand, d->d_rsv_out);
       } else if (!sharded && parts > 1) {
         const int gw = gath_words(L);
         const bool rc = select_seg(0, select_part(0, N, parts)) <= SEL_RC * 512;

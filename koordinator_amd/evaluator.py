@@ -136,6 +136,21 @@ class Evaluator:
         """ke_reservations_load: the reservation cache (RESERVATION_DTYPE array)."""
         r = abi.struct_array(reservations, abi.Reservation)
         self._check(self.lib.ke_reservations_load(self.h, len(r), abi.ptr(r)))
+        self._n_resv = len(r)
+
+    def reservations_get(self):
+        """ke_reservations_get: the reservation cache as Reserve / Unreserve left it."""
+        out = np.zeros(getattr(self, "_n_resv", 0), abi.RESERVATION_DTYPE)
+        self._check(self.lib.ke_reservations_get(self.h, len(out), abi.ptr(out)))
+        return out
+
+    def pod_reservations(self, matches):
+        """ke_pod_reservations: per pod of the next schedule() the reservation indices it matches."""
+        off = np.zeros(len(matches) + 1, np.int32)
+        off[1:] = np.cumsum([len(m) for m in matches])
+        ids = np.ascontiguousarray(np.concatenate([np.asarray(m, np.int32) for m in matches]) if len(matches)
+                                   else np.zeros(0, np.int32), np.int32)
+        self._check(self.lib.ke_pod_reservations(self.h, len(matches), abi.ptr(off), abi.ptr(ids)))
 
     def node_info_requested(self, i):
         """ke_node_info_requested: NodeInfo Requested / NonZeroRequested (MilliCPU, Memory) after the restore."""
@@ -213,8 +228,11 @@ class Evaluator:
                                      abi.ptr(out["ds"]), abi.ptr(out["total"]), abi.ptr(out["best"])))
         return out
 
-    def schedule(self, pods, now_ns):
+    def schedule(self, pods, now_ns, matches=None):
+        """ke_schedule; `matches` (optional): per pod the reservation indices it matches (KE_RSV_MATCHED pods)."""
         pods = as_pod_array(pods)
+        if matches is not None:
+            self.pod_reservations(matches)
         chosen = np.zeros(len(pods), np.int32)
         score = np.zeros(len(pods), np.int32)
         self._check(self.lib.ke_schedule(self.h, len(pods), abi.ptr(pods), int(now_ns), abi.ptr(chosen), abi.ptr(score)))

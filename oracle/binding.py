@@ -55,6 +55,11 @@ def load():
         "or_set_pod_device_hints": (C.c_int, [V, i32, V]),
         "or_gpu_templates_load": (C.c_int, [V, i32, V]),
         "or_reservations_load": (C.c_int, [V, i32, V]),
+        "or_reservations_get": (C.c_int, [V, i32, V]),
+        "or_pod_reservations": (C.c_int, [V, i32, V, V]),
+        "or_last_reservations": (C.c_int, [V, i32, V]),
+        "or_reservation_score": (C.c_int64, [V, V]),
+        "or_reservation_prescore": (i32, [V, V, V, i32, V, V]),
         "or_node_info_requested": (C.c_int, [V, i32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
         "or_node_device_flags": (C.c_int, [V, i32, i32, i32]),
         "or_last_vf_ranks": (C.c_int, [V, i32, V]),
@@ -261,6 +266,35 @@ class Oracle:
     def reservations_load(self, reservations):
         r = abi.struct_array(reservations, abi.Reservation)
         assert self.lib.or_reservations_load(self.h, len(r), abi.ptr(r)) == 0
+        self._n_resv = len(r)
+
+    def reservations_get(self):
+        out = np.zeros(getattr(self, "_n_resv", 0), abi.RESERVATION_DTYPE)
+        assert self.lib.or_reservations_get(self.h, len(out), abi.ptr(out)) == 0
+        return out
+
+    def pod_reservations(self, matches):
+        off = np.zeros(len(matches) + 1, np.int32)
+        off[1:] = np.cumsum([len(m) for m in matches])
+        ids = np.ascontiguousarray(np.concatenate([np.asarray(m, np.int32) for m in matches]) if len(matches)
+                                   else np.zeros(0, np.int32), np.int32)
+        assert self.lib.or_pod_reservations(self.h, len(matches), abi.ptr(off), abi.ptr(ids)) == 0
+
+    def reservation_prescore(self, pod, ids):
+        """Reservation plugin PreScore + Score of `pod` matching reservations `ids` on every node:
+        (preferredNode or -1, raw Score per node, nominated reservation per node)."""
+        p = as_pod_array([pod] if isinstance(pod, abi.Pod) else np.asarray(pod).reshape(1))
+        ids = np.ascontiguousarray(ids, np.int32)
+        raw = np.zeros(self.n, np.int64)
+        nom = np.zeros(self.n, np.int32)
+        pref = self.lib.or_reservation_prescore(self.h, abi.ptr(p), abi.ptr(ids), len(ids), abi.ptr(raw), abi.ptr(nom))
+        return int(pref), raw, nom
+
+    def reservation_score(self, reservation, pod):
+        """scoreReservation of one reservation record for one pod (golden-vector entry point)."""
+        r = abi.struct_array([reservation] if isinstance(reservation, abi.Reservation) else reservation, abi.Reservation)
+        p = as_pod_array([pod] if isinstance(pod, abi.Pod) else np.asarray(pod).reshape(1))
+        return int(self.lib.or_reservation_score(abi.ptr(r), abi.ptr(p)))
 
     def node_info_requested(self, i):
         req, nz = (C.c_int64 * 2)(), (C.c_int64 * 2)()
@@ -334,8 +368,10 @@ class Oracle:
             raise RuntimeError(f"oracle eval rc={rc}")
         return out
 
-    def schedule(self, pods, now_ns, n_threads=0):
+    def schedule(self, pods, now_ns, n_threads=0, matches=None):
         pods = as_pod_array(pods)
+        if matches is not None:
+            self.pod_reservations(matches)
         chosen = np.zeros(len(pods), np.int32)
         score = np.zeros(len(pods), np.int32)
         self.last_device_allocations = np.zeros(len(pods), np.uint64)
@@ -363,6 +399,9 @@ class Oracle:
         vf = np.full((len(chosen), 2 * abi.MAX_MINORS), -1, np.int8)
         self.lib.or_last_vf_ranks(self.h, len(chosen), abi.ptr(vf))
         out["vf_rank"] = np.where(placed[:, None], vf[:n], -1)
+        rv = np.zeros(len(chosen), np.int32)
+        self.lib.or_last_reservations(self.h, len(chosen), abi.ptr(rv))
+        out["reservation"] = np.where(placed, rv[:n], 0)
         return out
 
     def node_state(self, i):

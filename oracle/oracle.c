@@ -90,6 +90,16 @@ struct or_cluster {
   int32_t n_tmpl;
   int8_t* last_vf; /* VF ranks of the last or_schedule: [pod][2][KE_MAX_MINORS] */
   int32_t last_vf_n;
+  /* the reservation cache (or_reservations_load; allocated / allocated pods kept by Reserve), the matched
+   * lists of the next or_schedule (or_pod_reservations) and 1 + the reservation each pod of the last
+   * or_schedule was assumed into */
+  ke_reservation* resv;
+  int32_t n_resv;
+  int32_t* moff;
+  int32_t* mids;
+  int32_t m_pods;
+  int32_t* last_resv;
+  int32_t last_resv_n;
 };
 
 /* ---------------------------------------------------------------------------------------------- */
@@ -393,7 +403,8 @@ static int pod_is_cpuset(const ke_pod* pod) {
          pod->requests[KE_RES_CPU] > 0;
 }
 static int pod_unsupported(const ke_pod* pod) {
-  return pod->has_resource_spec || pod->has_unsupported_device_requests || pod->reservation_matched;
+  /* KE_RSV_MATCHED pods are checked by or_schedule (or_resv_supported); affinity / ignored are refused */
+  return pod->has_resource_spec || pod->has_unsupported_device_requests || pod->reservation_matched > KE_RSV_MATCHED;
 }
 static int node_unsupported(const ke_node* n) {
   return n->numa_topology_policy < 0 || n->numa_topology_policy > KE_NUMA_POLICY_SINGLE_NUMA_NODE ||
@@ -2841,6 +2852,10 @@ or_cluster* or_create(const ke_config* cfg, int32_t n_nodes) {
 
 void or_destroy(or_cluster* c) {
   if (!c) return;
+  free(c->resv);
+  free(c->moff);
+  free(c->mids);
+  free(c->last_resv);
   for (int i = 0; i < c->n; i++) {
     free(c->nodes[i].pm);
     free(c->nodes[i].agg);
@@ -2873,22 +2888,33 @@ int or_gpu_templates_load(or_cluster* c, int32_t n, const ke_gpu_template* t) {
   return KE_OK;
 }
 
-/* BeforePreFilter's NodeInfo restore for a pod matching no reservation (transformer.go:147-300): an available
- * reservation, not AllocateOnce with allocated pods, with allocated pods is unmatched; restoreUnmatchedReservations
- * (transformer.go:447-473) removes its reserve pod (requests = allocatable) and adds a pod requesting
- * SubtractWithNonNegativeResult(allocatable, allocated) unless that is zero (updateNodeInfoRequested,
- * :491-504: NonZeroRequested with the 100m / 200Mi defaults of a zero request). */
+/* BeforePreFilter's NodeInfo restore (transformer.go:147-300).  forEachAvailableReservationOnNode skips a
+ * reservation that is not available or is AllocateOnce with allocated pods (:181-190).  For the scheduling pod
+ * the others are matched (checkReservationMatchedOrIgnored) or, with allocated pods, unmatched (:195-199):
+ *  - restoreUnmatchedReservations (:447-473) removes the reserve pod (requests = allocatable) and adds a pod
+ *    requesting SubtractWithNonNegativeResult(allocatable, allocated) unless that is zero;
+ *  - restoreMatchedReservation (:422-445) removes the reserve pod (NodeInfo.RemovePod).
+ * updateNodeInfoRequested / RemovePod move NonZeroRequested with the 100m / 200Mi defaults of a zero request
+ * (:491-504).  `matched` (by reservation index) may be NULL; with_matched = 0 leaves the matched ones out. */
 static const ke_node_resource* node_xres(const or_node* nd, int32_t id);
 static int64_t or_non0(int k, int64_t v) { return v != 0 ? v : (k == KE_RES_CPU ? 100 : 200LL << 20); }
-int or_reservations_load(or_cluster* c, int32_t n, const ke_reservation* rs) {
-  for (int32_t i = 0; i < n; i++)
-    if (rs[i].node < 0 || rs[i].node >= c->n) return KE_ERR_NOT_FOUND;
+static int or_resv_usable(const ke_reservation* r) { return r->available && !(r->allocate_once && r->allocated_pods > 0); }
+static void or_restore(or_cluster* c, const char* matched, int with_matched) {
   for (int32_t i = 0; i < c->n; i++)
     for (int k = 0; k < KE_NRES; k++) c->nodes[i].rv_req[k] = c->nodes[i].rv_nz[k] = 0;
-  for (int32_t i = 0; i < n; i++) {
-    const ke_reservation* r = &rs[i];
-    if (!r->available || (r->allocate_once && r->allocated_pods > 0) || r->allocated_pods == 0) continue;
+  for (int32_t i = 0; i < c->n_resv; i++) {
+    const ke_reservation* r = &c->resv[i];
+    if (!or_resv_usable(r)) continue;
     or_node* nd = &c->nodes[r->node];
+    if (matched && matched[i]) {
+      if (with_matched)
+        for (int k = 0; k < KE_NRES; k++) {
+          nd->rv_req[k] -= r->allocatable[k];
+          nd->rv_nz[k] -= or_non0(k, r->allocatable[k]);
+        }
+      continue;
+    }
+    if (r->allocated_pods == 0) continue;
     int64_t rem[KE_NRES];
     int rem_nz = 0;
     for (int k = 0; k < KE_NRES; k++) {
@@ -2900,8 +2926,83 @@ int or_reservations_load(or_cluster* c, int32_t n, const ke_reservation* rs) {
       nd->rv_nz[k] += -or_non0(k, r->allocatable[k]) + (rem_nz ? or_non0(k, rem[k]) : 0);
     }
   }
+}
+int or_reservations_load(or_cluster* c, int32_t n, const ke_reservation* rs) {
+  for (int32_t i = 0; i < n; i++)
+    if (rs[i].node < 0 || rs[i].node >= c->n) return KE_ERR_NOT_FOUND;
+  free(c->resv);
+  c->resv = (ke_reservation*)malloc(sizeof(ke_reservation) * (size_t)(n > 0 ? n : 1));
+  if (n > 0) memcpy(c->resv, rs, sizeof(ke_reservation) * (size_t)n);
+  c->n_resv = n;
+  or_restore(c, NULL, 0);
   return KE_OK;
 }
+int or_reservations_get(const or_cluster* c, int32_t n, ke_reservation* out) {
+  if (n < 0 || n > c->n_resv) return KE_ERR_INVALID;
+  if (n > 0) memcpy(out, c->resv, sizeof(ke_reservation) * (size_t)n);
+  return KE_OK;
+}
+int or_pod_reservations(or_cluster* c, int32_t n_pods, const int32_t* offsets, const int32_t* ids) {
+  free(c->moff);
+  free(c->mids);
+  c->moff = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n_pods + 1));
+  memcpy(c->moff, offsets, sizeof(int32_t) * (size_t)(n_pods + 1));
+  const int32_t m = offsets[n_pods];
+  c->mids = (int32_t*)malloc(sizeof(int32_t) * (size_t)(m > 0 ? m : 1));
+  if (m > 0) memcpy(c->mids, ids, sizeof(int32_t) * (size_t)m);
+  c->m_pods = n_pods;
+  for (int32_t j = 0; j < m; j++)
+    if (ids[j] < 0 || ids[j] >= c->n_resv) return KE_ERR_NOT_FOUND;
+  return KE_OK;
+}
+
+/* ScoreReservation -> scoreReservation (reservation/scoring.go:141-164, 191-210): requested = PodRequests +
+ * allocated; over RemoveZeros(allocatable): MaxNodeScore * req.MilliValue() / capacity.MilliValue() for each
+ * resource with req <= capacity, summed, divided by the number of resources */
+int64_t or_reservation_score(const ke_reservation* r, const ke_pod* pod) {
+  int64_t s = 0, w = 0;
+  for (int k = 0; k < KE_NRES; k++) {
+    if (r->allocatable[k] == 0) continue;
+    w++;
+    const int64_t req = pod->requests[k] + r->allocated[k];
+    const int64_t milli = k == KE_RES_CPU ? 1 : 1000; /* memory: Value() * 1000 */
+    if (req <= r->allocatable[k]) s += MAX_NODE_SCORE * (req * milli) / (r->allocatable[k] * milli);
+  }
+  return w ? s / w : 0;
+}
+
+/* FilterNominateReservation (reservation/plugin.go:707-738) -> filterWithReservations(..., true) on one
+ * reservation (:351-442): skipped (not nominable) without a resource name shared with the pod (:369-375);
+ * fitsNode (:447-497: pods count not modelled; preemptible empty) with podRequested = Requested after the
+ * unmatched restore, rRemained = GetAvailable (allocatable - allocated, >= 0), allRAllocated = Σ allocated
+ * of the node's matched reservations; fitsReservation (:499-569) for the Restricted policy, else the node fit.
+ * The NUMA / DeviceShare FilterNominateReservation pass for pods without cpuset, NUMA policy or devices. */
+static int or_resv_nominable(const or_cluster* c, const ke_reservation* r, const ke_pod* pod, int32_t node,
+                             const int64_t* pod_requested, const int64_t* all_allocated) {
+  int shared = 0;
+  for (int k = 0; k < KE_NRES; k++)
+    if (r->allocatable[k] != 0 && pod->requests[k] != 0) shared = 1;
+  if (!shared) return 0;
+  int node_fits = 1;
+  if (!(pod->requests[KE_RES_CPU] == 0 && pod->requests[KE_RES_MEMORY] == 0)) {
+    for (int k = 0; k < KE_NRES; k++) {
+      int64_t remained = r->allocatable[k] - r->allocated[k];
+      if (remained < 0) remained = 0;
+      const int64_t avail = c->nodes[node].node.allocatable[k] - (pod_requested[k] - remained - all_allocated[k]);
+      if (pod->requests[k] > avail) node_fits = 0;
+    }
+  }
+  int resv_fits = node_fits;
+  if (r->allocate_policy == KE_RSV_POLICY_RESTRICTED) {
+    resv_fits = 1;
+    for (int k = 0; k < KE_NRES; k++) {
+      if (r->allocatable[k] == 0 || pod->requests[k] == 0) continue; /* Mask(requests, names); zero skipped */
+      if (pod->requests[k] > r->allocatable[k] - r->allocated[k]) resv_fits = 0;
+    }
+  }
+  return node_fits && resv_fits;
+}
+
 int or_node_info_requested(const or_cluster* c, int32_t node, int64_t* requested, int64_t* non_zero) {
   if (node < 0 || node >= c->n) return KE_ERR_NOT_FOUND;
   const or_node* nd = &c->nodes[node];
@@ -3443,6 +3544,8 @@ int or_eval(const or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now
             int16_t* la_score, int16_t* numa_score, int16_t* ds_score, int16_t* total, int32_t* best, int n_threads) {
   int rc = check_supported(c, n_pods, pods);
   if (rc) return rc;
+  for (int32_t p = 0; p < n_pods; p++)
+    if (pods[p].reservation_matched) return KE_ERR_UNSUPPORTED;
   const int64_t N = c->n;
 #ifdef _OPENMP
   if (n_threads > 0) omp_set_num_threads(n_threads);
@@ -3468,9 +3571,156 @@ int or_eval(const or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now
   return KE_OK;
 }
 
+/* The Reservation plugin's PreScore + Score for a pod whose matched reservations are flagged in m[]
+ * (reservation/scoring.go:42-128, nominator.go:207-278): per node the matched reservations in index order, their
+ * smallest order, the nominated one (NominateReservation: the FilterNominateReservation survivors; the only one,
+ * else the smallest order, else the best ScoreReservation) and its ScoreReservation; preferredNode = the node
+ * of `nodes` (feasible[i] != 0, NULL = every node) with the smallest order (first in node order) scores 1000.
+ * pod_requested[i*KE_NRES + k]: NodeInfo Requested after the unmatched restore.  raw[i] = Score (before
+ * NormalizeScore), nom[i] = the nominated reservation or -1.  Returns preferredNode or -1. */
+static int32_t or_resv_prescore(const or_cluster* c, const ke_pod* pod, const char* m, const int64_t* pod_requested,
+                                const uint8_t* feasible, int64_t* raw, int32_t* nom) {
+  const int32_t N = c->n;
+  int32_t pref = -1;
+  int64_t po = 0;
+  for (int32_t i = 0; i < N; i++) {
+    nom[i] = -1;
+    raw[i] = 0;
+    int64_t all_alloc[KE_NRES] = {0, 0}, order = 0;
+    int any = 0;
+    for (int32_t r = 0; r < c->n_resv; r++)
+      if (m[r] && c->resv[r].node == i) {
+        any = 1;
+        for (int k = 0; k < KE_NRES; k++) all_alloc[k] += c->resv[r].allocated[k];
+        if (c->resv[r].order != 0 && (order == 0 || c->resv[r].order < order)) order = c->resv[r].order;
+      }
+    if (!any) continue;
+    int32_t n_ok = 0, first = -1, by_order = -1, by_score = -1;
+    int64_t bo = 0, bsc = -1;
+    for (int32_t r = 0; r < c->n_resv; r++) {
+      if (!m[r] || c->resv[r].node != i) continue;
+      if (!or_resv_nominable(c, &c->resv[r], pod, i, &pod_requested[i * KE_NRES], all_alloc)) continue;
+      n_ok++;
+      if (first < 0) first = r;
+      if (c->resv[r].order != 0 && (bo == 0 || c->resv[r].order < bo)) {
+        bo = c->resv[r].order;
+        by_order = r;
+      }
+      const int64_t sc = or_reservation_score(&c->resv[r], pod);
+      if (sc > bsc) { /* sort.Slice by score desc; equal scores keep list order (insertion sort below 13) */
+        bsc = sc;
+        by_score = r;
+      }
+    }
+    nom[i] = n_ok == 0 ? -1 : n_ok == 1 ? first : by_order >= 0 ? by_order : by_score;
+    raw[i] = nom[i] >= 0 ? or_reservation_score(&c->resv[nom[i]], pod) : 0;
+    if ((!feasible || feasible[i]) && order != 0 && (pref < 0 || order < po)) {
+      po = order;
+      pref = i;
+    }
+  }
+  if (pref >= 0) raw[pref] = 1000; /* mostPreferredScore */
+  return pref;
+}
+
+/* matched flags + fitsNode's podRequested for the listed reservations of a pod; the rows left restored with
+ * the matched ones (with_matched) */
+static char* or_resv_begin(or_cluster* c, const int32_t* ids, int32_t n_ids, int64_t** pod_requested) {
+  const int32_t N = c->n;
+  char* m = (char*)calloc((size_t)(c->n_resv > 0 ? c->n_resv : 1), 1);
+  for (int32_t j = 0; j < n_ids; j++)
+    if (or_resv_usable(&c->resv[ids[j]])) m[ids[j]] = 1;
+  or_restore(c, m, 0);
+  *pod_requested = (int64_t*)malloc(sizeof(int64_t) * KE_NRES * (size_t)(N > 0 ? N : 1));
+  for (int32_t i = 0; i < N; i++)
+    for (int k = 0; k < KE_NRES; k++) (*pod_requested)[i * KE_NRES + k] = c->nodes[i].node.requested[k] + c->nodes[i].rv_req[k];
+  or_restore(c, m, 1);
+  return m;
+}
+
+/* golden-vector entry point: the Reservation plugin's Score per node (every node in PreScore's list) */
+int32_t or_reservation_prescore(or_cluster* c, const ke_pod* pod, const int32_t* ids, int32_t n_ids, int64_t* raw,
+                                int32_t* nom) {
+  int64_t* pr;
+  char* m = or_resv_begin(c, ids, n_ids, &pr);
+  const int32_t pref = or_resv_prescore(c, pod, m, pr, NULL, raw, nom);
+  or_restore(c, NULL, 0);
+  free(m);
+  free(pr);
+  return pref;
+}
+
+/* A KE_RSV_MATCHED pod: BeforePreFilter restore with its matched reservations, Filter / Score of the plugins
+ * (eval_pod), the Reservation plugin's PreScore / Score, NormalizeScore (DefaultNormalizeScore over the
+ * feasible nodes, scoring.go:134-139) and selectHost over the total with weight_reservation.  Returns the
+ * chosen node (-1), its total in *best and the nominated reservation of every node in nom[]. */
+static int32_t or_resv_eval(or_cluster* c, const ke_pod* pod, int64_t now, eval_out* o, const int32_t* ids, int32_t n_ids,
+                            int32_t* best, int32_t* nom) {
+  const int32_t N = c->n;
+  int64_t* pr;
+  char* m = or_resv_begin(c, ids, n_ids, &pr);
+  int16_t bs16;
+  (void)eval_pod(c, pod, now, o, &bs16);
+  or_restore(c, NULL, 0);
+  uint8_t* feasible = (uint8_t*)malloc((size_t)(N > 0 ? N : 1));
+  for (int32_t i = 0; i < N; i++) feasible[i] = o[i].status == KE_CODE_SUCCESS;
+  int64_t* raw = (int64_t*)malloc(sizeof(int64_t) * (size_t)(N > 0 ? N : 1));
+  (void)or_resv_prescore(c, pod, m, pr, feasible, raw, nom);
+  int64_t mx = 0;
+  for (int32_t i = 0; i < N; i++)
+    if (feasible[i] && raw[i] > mx) mx = raw[i];
+  int32_t b = -1;
+  int64_t bt = -1;
+  for (int32_t i = 0; i < N; i++) {
+    if (!feasible[i]) continue;
+    const int64_t n = mx > 0 ? MAX_NODE_SCORE * raw[i] / mx : 0;
+    const int64_t t = o[i].total + c->cfg.weight_reservation * n;
+    if (t > bt) {
+      bt = t;
+      b = i;
+    }
+  }
+  *best = b >= 0 ? (int32_t)bt : -1;
+  free(m);
+  free(pr);
+  free(feasible);
+  free(raw);
+  return b;
+}
+
+/* the KE_RSV_MATCHED pods this restatement covers (koord_eval.h ke_pod_reservations) */
+static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* pods) {
+  int node_bind = 0;
+  for (int i = 0; i < c->n; i++) node_bind |= c->nodes[i].node.cpu_bind_policy != KE_NODE_CPU_BIND_NONE;
+  for (int32_t p = 0; p < n_pods; p++) {
+    const int32_t n_ids = c->moff && c->m_pods == n_pods ? c->moff[p + 1] - c->moff[p] : 0;
+    if (pods[p].reservation_matched != KE_RSV_MATCHED) {
+      if (n_ids) return KE_ERR_INVALID;
+      continue;
+    }
+    if (!(c->moff && c->m_pods == n_pods)) return KE_ERR_INVALID;
+    cpuset_state st;
+    cpuset_prefilter(c, &pods[p], &st);
+    ds_pod d;
+    ds_prepare_pod(c, &pods[p], &d);
+    int scalar = pods[p].has_other_requests || !d.skip || st.rcb || (node_bind && pods[p].requests[KE_RES_CPU] > 0) ||
+                 pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE;
+    for (int r = KE_NRES; r < KE_RES_COUNT; r++) scalar |= pods[p].requests[r] != 0;
+    for (int r = 0; r < KE_PDR_COUNT; r++) scalar |= pods[p].device_requests[r] != 0;
+    if (scalar) return KE_ERR_UNSUPPORTED;
+    for (int32_t j = c->moff[p]; j < c->moff[p + 1]; j++)
+      if (or_resv_usable(&c->resv[c->mids[j]]) &&
+          c->nodes[c->resv[c->mids[j]].node].node.numa_topology_policy != KE_NUMA_POLICY_NONE)
+        return KE_ERR_UNSUPPORTED;
+  }
+  return KE_OK;
+}
+
 int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t* chosen, int32_t* score,
                 uint64_t* dev_alloc, int64_t* numa_alloc, uint64_t* cpusets, int n_threads) {
   int rc = check_supported(c, n_pods, pods);
+  if (rc) return rc;
+  rc = or_resv_supported(c, n_pods, pods);
   if (rc) return rc;
   const int64_t N = c->n;
 #ifdef _OPENMP
@@ -3484,6 +3734,11 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
   memset(c->last_vf, -1, (size_t)(n_pods > 0 ? n_pods : 1) * 2 * KE_MAX_MINORS);
   c->last_vf_n = n_pods;
   eval_out* o = (eval_out*)malloc(sizeof(eval_out) * (size_t)(N > 0 ? N : 1));
+  int32_t* nom = (int32_t*)malloc(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
+  if (c->moff && c->m_pods != n_pods) c->moff = (free(c->moff), NULL); /* lists for another queue: none */
+  free(c->last_resv);
+  c->last_resv = (int32_t*)calloc((size_t)(n_pods > 0 ? n_pods : 1), sizeof(int32_t));
+  c->last_resv_n = n_pods;
   for (int p = 0; p < n_pods; p++) {
     /* ElasticQuota PreFilter (plugin.go:223-275): a refused pod is evaluated nowhere */
     if (c->quotas && orq_admit(c->quotas, &pods[p]) == 0) {
@@ -3493,8 +3748,15 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
       if (dev_alloc) dev_alloc[p] = 0;
       continue;
     }
-    int16_t bs;
-    int32_t b = eval_pod(c, &pods[p], now, o, &bs);
+    int16_t bs16;
+    int32_t bs, b;
+    const int32_t n_ids = c->moff && pods[p].reservation_matched == KE_RSV_MATCHED ? c->moff[p + 1] - c->moff[p] : 0;
+    if (n_ids > 0) {
+      b = or_resv_eval(c, &pods[p], now, o, c->mids + c->moff[p], n_ids, &bs, nom);
+    } else {
+      b = eval_pod(c, &pods[p], now, o, &bs16);
+      bs = bs16;
+    }
     chosen[p] = b;
     if (score) score[p] = b >= 0 ? bs : -1;
     uint64_t mask = 0;
@@ -3530,10 +3792,27 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
         }
       }
       if (c->quotas) orq_reserve(c->quotas, &pods[p]); /* ElasticQuota Reserve */
+      if (n_ids > 0 && nom[b] >= 0) {
+        /* Reservation Reserve: assumePod -> AddAssignedPod (reservation/plugin.go:783,
+         * reservation_info.go:458-468): allocated += Mask(requests, ResourceNames), one more allocated pod */
+        ke_reservation* r = &c->resv[nom[b]];
+        for (int k = 0; k < KE_NRES; k++)
+          if (r->allocatable[k] != 0) r->allocated[k] += pods[p].requests[k];
+        r->allocated_pods++;
+        c->last_resv[p] = 1 + nom[b];
+        or_restore(c, NULL, 0);
+      }
     }
     if (dev_alloc) dev_alloc[p] = mask;
   }
   free(o);
+  free(nom);
+  free(c->moff); /* the lists were for this call */
+  c->moff = NULL;
+  return KE_OK;
+}
+int or_last_reservations(const or_cluster* c, int32_t n, int32_t* out) {
+  for (int32_t p = 0; p < n; p++) out[p] = p < c->last_resv_n ? c->last_resv[p] : 0;
   return KE_OK;
 }
 
@@ -3555,6 +3834,16 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
 int or_pod_release(or_cluster* c, const ke_pod* pod, const ke_pod_allocation* a, int32_t mode) {
   const int32_t node = a->node;
   if (node >= c->n) return KE_ERR_NOT_FOUND;
+  if (a->reservation < 0 || a->reservation > c->n_resv) return KE_ERR_NOT_FOUND;
+  if (node >= 0 && a->reservation > 0) {
+    /* reservation forgetPod -> RemoveAssignedPod (reservation/plugin.go:815-819, reservation_info.go:470-482):
+     * allocated = SubtractWithNonNegativeResult(allocated, Mask(requests, ResourceNames)) */
+    ke_reservation* r = &c->resv[a->reservation - 1];
+    for (int k = 0; k < KE_NRES; k++)
+      if (r->allocatable[k] != 0) r->allocated[k] = r->allocated[k] - pod->requests[k] > 0 ? r->allocated[k] - pod->requests[k] : 0;
+    if (r->allocated_pods > 0) r->allocated_pods--;
+    or_restore(c, NULL, 0);
+  }
   if (node >= 0) {
     or_node* n = &c->nodes[node];
     or_pod_unassign(c, node, pod->uid);

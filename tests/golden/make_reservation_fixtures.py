@@ -9,6 +9,16 @@ restates one test's objects and expectations by hand.  Only data is written.
     the unmatched restore, podRequested = 32C/64Gi (:330-333) -- what every pod matching no reservation sees:
     restoreUnmatchedReservations (transformer.go:447-473) swaps the 12C24G reserve pod for an 8C16Gi one.
 
+  * pkg/scheduler/plugins/reservation/scoring_test.go:40-284 TestScore: one 16C/128Gi node, the pod's matched
+    reservations reservation4C8G / reservation2C4G (optionally with allocated resources); PreScore + Score
+    (before NormalizeScore): no reservation 0, a zero-request pod 0 (no shared resource name: not nominated), 2C4Gi
+    into 4C8G 50, into a 2C4G holding 2C3Gi 0, both reservations 100 (the better ScoreReservation is nominated).
+  * scoring_test.go:286-461 TestScoreWithOrder: four nodes without allocatable, a 4C8G reservation on each, the
+    one on test-node-4 labelled reservation-order 123456; a 4C8Gi pod: test-node-4 is preferredNode and scores
+    mostPreferredScore 1000, the others MaxNodeScore.
+  Both tests write the cycle state by hand (no restore ran): NodeInfo holds no reserve pods and fitsNode's
+  podRequested / rAllocated are empty, so the cases' nodes have requested 0; nodes are indexed in test order.
+
 Run:  python tests/golden/make_reservation_fixtures.py
 """
 import json
@@ -31,7 +41,34 @@ cases = [{
     "want_requested": [32000, 64 * GI],
 }]
 
+SC = "pkg/scheduler/plugins/reservation/scoring_test.go"
+R4C8G = {"allocatable": [4000, 8 * GI], "allocated": [0, 0], "order": 0}
+R2C4G = {"allocatable": [2000, 4 * GI], "allocated": [0, 0], "order": 0}
+
+
+def score_case(name, lines, pod, resv, want, nodes=1, alloc=(16000, 128 * GI)):
+    """resv: [(node, reservation)]; want: the Score of each node"""
+    requested = [[0, 0] for _ in range(nodes)]  # the tests build the state by hand: no reserve pods in NodeInfo
+    return {"name": name, "source": f"{SC}:{lines}", "nodes": [{"allocatable": list(alloc), "requested": q}
+                                                              for q in requested],
+            "reservations": [dict(r, node=n) for n, r in resv], "pod": pod, "want_score": want}
+
+
+score_cases = [
+    score_case("no_reservation_matched", "136-139", [0, 0], [], [0]),
+    score_case("matched_zero_request_pod", "140-148", [0, 0], [(0, R2C4G)], [0]),
+    score_case("matched_4c8g_pod_2c4g", "149-172", [2000, 4 * GI], [(0, R4C8G)], [50]),
+    score_case("allocated_2c4g_pod_2c4g", "173-202", [2000, 4 * GI],
+               [(0, dict(R2C4G, allocated=[2000, 3 * GI]))], [0]),
+    score_case("multi_matched_pod_2c4g", "203-226", [2000, 4 * GI], [(0, R4C8G), (0, R2C4G)], [100]),
+    score_case("preferred_by_order", "286-461", [4000, 8 * GI],
+               [(0, R4C8G), (1, R4C8G), (2, R4C8G), (3, dict(R4C8G, order=123456))], [100, 100, 100, 1000],
+               nodes=4, alloc=(0, 0)),
+]
+
 if __name__ == "__main__":
+    with open(os.path.join(HERE, "reservation_scores.json"), "w") as f:
+        json.dump({"source": "make_reservation_fixtures.py", "cases": score_cases}, f, indent=1)
     with open(os.path.join(HERE, "reservations.json"), "w") as f:
         json.dump({"source": "make_reservation_fixtures.py", "cases": cases}, f, indent=1)
     print(len(cases), "cases")

@@ -1,11 +1,13 @@
-"""Reservations on the GPU (first part): with a reservation cache loaded, every pod that
-matches no reservation is evaluated against the restored NodeInfo (restoreUnmatchedReservations,
-transformer.go:447-473) -- NodeNUMAResource's amplified-cpu Filter and Score and NodeResourcesFitPlus read it --
-bit-exact with the oracle on eval matrices and schedules, and again after the reservation set changes."""
+"""Reservations on the GPU: with a reservation cache loaded, every pod that matches no
+reservation is evaluated against the restored NodeInfo (restoreUnmatchedReservations, transformer.go:447-473) --
+NodeNUMAResource's amplified-cpu Filter and Score and NodeResourcesFitPlus read it -- and pods that match
+reservations take the nominated-reservation path (restoreMatchedReservation, the Reservation plugin's Score and
+Reserve, k_rsv_pick), bit-exact with the oracle."""
 import numpy as np
 import pytest
 
-from koordinator_amd import abi, synth
+from koordinator_amd import Evaluator, abi, synth
+from oracle.binding import Oracle
 from test_gpu_cpuset import assert_eval_equal
 from test_gpu_ext import _cluster, _schedule_equal
 
@@ -54,4 +56,115 @@ def test_reservation_restore_schedule_parity(gpu):
     c1, s1 = ev.schedule(more, synth.T0)
     c0, s0 = o.schedule(more, synth.T0)
     assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    assert ev.check_records(synth.T0) == 0
+
+
+def _matched_setup(n, seed, n_pods, quota=False):
+    """A FitPlus + amplified-cpu cluster whose NodeInfo holds the reserve pods of owner-grouped reservations
+    (Default / Aligned / Restricted, AllocateOnce, orders, some already allocated), and a queue in which
+    about 40 % of the eligible pods match one owner group's reservations (KE_RSV_MATCHED)."""
+    rng = np.random.default_rng(seed)
+    cl = synth.make_cluster(n, synth.BASE_SEED + seed, amplified_fraction=0.2)
+    rs, grp = [], []
+    for g in range(10):
+        for _ in range(int(rng.integers(2, 7))):
+            r = abi.Reservation(node=int(rng.integers(0, n)), available=int(rng.random() < 0.95),
+                                allocate_once=int(rng.random() < 0.25), allocate_policy=int(rng.integers(0, 3)),
+                                allocated_pods=int(rng.choice([0, 0, 1, 2])), order=int(rng.choice([0, 0, 0, 7, 3, 11])))
+            r.allocatable[0] = int(rng.choice([0, 2000, 4000, 8000, 16000]))
+            r.allocatable[1] = int(rng.choice([0, 4, 8, 16, 32])) * 2**30
+            if r.allocated_pods:
+                r.allocated[0], r.allocated[1] = r.allocatable[0] // 2, r.allocatable[1] // 4
+            cl.nodes["requested"][r.node, 0] += r.allocatable[0]  # the reserve pod is in NodeInfo
+            cl.nodes["requested"][r.node, 1] += r.allocatable[1]
+            rs.append(r)
+            grp.append(g)
+    cfg = synth.ext_config(synth.config(n))
+    ev, o = Evaluator(cfg), Oracle(cfg, n)
+    tables = synth.make_node_resources(cl, synth.BASE_SEED + seed + 1)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        synth.load_node_resources(h, tables)
+        h.reservations_load(rs)
+    pods = synth.add_pod_xres(synth.make_pods(n_pods, synth.BASE_SEED + seed + 2), synth.BASE_SEED + seed + 3)
+    cpuset = np.isin(pods["qos_class"], [abi.QOS_LSE, abi.QOS_LSR]) & (pods["priority_class"] == abi.PRIORITY_PROD)
+    elig = ((pods["numa_topology_policy"] == 0) & (pods["requests"][:, 2:] == 0).all(1) & (pods["has_other_requests"] == 0)
+            & (pods["device_requests"] == 0).all(1) & ~cpuset)
+    grp = np.asarray(grp)
+    matches = [[] for _ in range(n_pods)]
+    for p in np.flatnonzero(elig & (rng.random(n_pods) < 0.4)):
+        pods["reservation_matched"][p] = abi.RSV_MATCHED
+        matches[p] = np.flatnonzero(grp == rng.integers(0, 10)).tolist()
+    return ev, o, pods, matches
+
+
+def _resv_equal(ev, o):
+    a, b = ev.reservations_get(), o.reservations_get()
+    assert np.array_equal(a["allocated"], b["allocated"]) and np.array_equal(a["allocated_pods"], b["allocated_pods"])
+    return a
+
+
+def test_matched_reservations_schedule_parity(gpu):
+    """The nominated-reservation path: KE_RSV_MATCHED pods between plain ones in one queue --
+    their matched restore, the Reservation plugin's preferredNode / nomination / normalized Score at weight 5000,
+    Reserve into the nominated reservation -- bit-exact with the oracle on placements, totals, reservation
+    state and release records; then Unreserve of a third of the matched placements and a second queue."""
+    ev, o, pods, matches = _matched_setup(300, 961, 260)
+    before = ev.reservations_get()
+    c1, s1 = ev.schedule(pods, synth.T0, matches=matches)
+    c0, s0 = o.schedule(pods, synth.T0, matches=matches)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5].ravel().tolist()
+    assert np.array_equal(s1, s0)
+    after = _resv_equal(ev, o)
+    a1, a0 = ev.last_allocations(), o.last_allocations()
+    assert np.array_equal(a1["reservation"], a0["reservation"])
+    assert (a1["reservation"] > 0).sum() >= 5  # pods went into reservations
+    assert (s1 >= 5000).sum() >= 5  # and carried the Reservation score
+    assert (after["allocated_pods"] > before["allocated_pods"]).any()
+    assert ev.check_records(synth.T0) == 0
+    into = np.flatnonzero(a1["reservation"] > 0)
+    for p in into[::3]:
+        ev.unreserve(pods[p], int(p))
+        o.release(pods[p], a0[p], abi.RELEASE_UNRESERVE)
+    _resv_equal(ev, o)
+    ev2, o2, more, m2 = _matched_setup(300, 961, 260)  # the same generator: a second queue of the same shape
+    ev2.close()
+    more["pod_key"] += 7_000_000_000
+    more["uid"] += 7_000_000_000
+    c1, s1 = ev.schedule(more, synth.T0, matches=m2)
+    c0, s0 = o.schedule(more, synth.T0, matches=m2)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    _resv_equal(ev, o)
+    assert ev.check_records(synth.T0) == 0
+
+
+def test_matched_reservations_weight_one(gpu):
+    """weight_reservation 1: the Reservation score mixes with the other plugins' totals instead of dominating;
+    every matched pod matches all 40 reservations (several per node compete in NominateReservation)."""
+    ev, o, pods, matches = _matched_setup(200, 971, 150)
+    ev.close()
+    n = 200
+    rng = np.random.default_rng(972)
+    cl = synth.make_cluster(n, synth.BASE_SEED + 971, amplified_fraction=0.2)
+    cfg = synth.ext_config(synth.config(n))
+    cfg.weight_reservation = 1
+    ev, o = Evaluator(cfg), Oracle(cfg, n)
+    tables = synth.make_node_resources(cl, synth.BASE_SEED + 972)
+    rs = []
+    for i in rng.choice(n, 40, replace=False):
+        r = abi.Reservation(node=int(i), available=1, order=int(rng.choice([0, 0, 4])))
+        r.allocatable[0], r.allocatable[1] = 8000, 16 * 2**30
+        cl.nodes["requested"][i, 0] += 8000
+        cl.nodes["requested"][i, 1] += 16 * 2**30
+        rs.append(r)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        synth.load_node_resources(h, tables)
+        h.reservations_load(rs)
+    ids = list(range(len(rs)))
+    matches = [ids if pods["reservation_matched"][p] else [] for p in range(len(pods))]
+    c1, s1 = ev.schedule(pods, synth.T0, matches=matches)
+    c0, s0 = o.schedule(pods, synth.T0, matches=matches)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    _resv_equal(ev, o)
     assert ev.check_records(synth.T0) == 0

@@ -92,12 +92,73 @@ def test_restore_rules_product_equals_oracle():
     ev.close()
 
 
-def test_matched_pod_refused():
+def test_matched_pod_checks():
+    """KE_RSV_MATCHED needs ke_pod_reservations lists; affinity / ignored pods and ke_eval of a matched pod are
+    refused; lists for other pods or of another length are invalid (host checks, no device call)."""
     cfg = synth.config(4)
     ev = Evaluator(cfg)
+    synth.load_into(ev, synth.make_cluster(4, synth.BASE_SEED + 903))
+    ev.reservations_load([abi.Reservation(node=0, available=1)])
     pods = synth.make_pods(2, synth.BASE_SEED + 902)
-    pods["reservation_matched"][1] = 1
+    pods["reservation_matched"][1] = abi.RSV_MATCHED
     with pytest.raises(KoordEvalError) as e:
         ev.schedule(pods, synth.T0)
+    assert e.value.code == abi.ERR_INVALID
+    with pytest.raises(KoordEvalError) as e:
+        ev.schedule(pods, synth.T0, matches=[[0], []])  # listed for a pod that is not KE_RSV_MATCHED
+    assert e.value.code == abi.ERR_INVALID
+    with pytest.raises(KoordEvalError) as e:
+        ev.schedule(pods, synth.T0, matches=[[]])  # another queue length
+    assert e.value.code == abi.ERR_INVALID
+    with pytest.raises(KoordEvalError) as e:
+        ev.pod_reservations([[], [1]])  # no such reservation
+    assert e.value.code == abi.ERR_NOT_FOUND
+    for v in (abi.RSV_AFFINITY, abi.RSV_IGNORED):
+        pods["reservation_matched"][1] = v
+        with pytest.raises(KoordEvalError) as e:
+            ev.schedule(pods, synth.T0)
+        assert e.value.code == abi.ERR_UNSUPPORTED
+    pods["reservation_matched"][1] = abi.RSV_MATCHED
+    pods["requests"][1][abi.RES_BATCH_CPU] = 1000  # a scalar request
+    with pytest.raises(KoordEvalError) as e:
+        ev.schedule(pods, synth.T0, matches=[[], [0]])
+    assert e.value.code == abi.ERR_UNSUPPORTED
+    with pytest.raises(KoordEvalError) as e:
+        ev.eval(pods, synth.T0)
     assert e.value.code == abi.ERR_UNSUPPORTED
     ev.close()
+
+
+SCORE_CASES = json.load(open(os.path.join(HERE, "golden", "reservation_scores.json")))["cases"]
+
+
+@pytest.mark.parametrize("case", SCORE_CASES, ids=[c["name"] for c in SCORE_CASES])
+def test_reservation_score_golden(case):
+    """The oracle's Reservation PreScore / NominateReservation / Score against TestScore and TestScoreWithOrder."""
+    n = len(case["nodes"])
+    cfg = synth.config(n)
+    o = Oracle(cfg, n)
+    for i, nd in enumerate(case["nodes"]):
+        node = abi.Node()
+        for k in range(abi.NRES):
+            node.allocatable[k] = nd["allocatable"][k]
+            node.raw_allocatable[k] = abi.ABSENT
+            node.requested[k] = nd["requested"][k]
+            node.custom_usage_thresholds[k] = node.custom_prod_usage_thresholds[k] = abi.ABSENT
+            node.custom_agg_thresholds[k] = abi.ABSENT
+        node.cpu_amplification_ratio = -1.0
+        node.nrt_cpu_amplification_ratio = -2.0
+        o.upsert_node(i, node)
+    rs = []
+    for d in case["reservations"]:
+        r = abi.Reservation(node=d["node"], available=1, order=d["order"])
+        for k in range(abi.NRES):
+            r.allocatable[k], r.allocated[k] = d["allocatable"][k], d["allocated"][k]
+        rs.append(r)
+    o.reservations_load(rs)
+    pod = synth.make_pods(1, synth.BASE_SEED + 904)
+    pod["requests"][0][:] = 0
+    pod["requests"][0][:2] = case["pod"]
+    pod["reservation_matched"][0] = abi.RSV_MATCHED
+    pref, raw, nom = o.reservation_prescore(pod[0], list(range(len(rs))))
+    assert list(raw) == case["want_score"]
