@@ -699,16 +699,20 @@ int ke_reservations_get(ke_ctx* ctx, int32_t n, ke_reservation* out);
 #define KE_RSV_MATCHED 1  /* owner-matched reservations (MatchOwners, not unschedulable, taints tolerated,
                              ReservationAffinity / exact-match spec satisfied: the integrator's label logic,
                              transformer.go:97-146) listed with ke_pod_reservations                          */
-#define KE_RSV_AFFINITY 2 /* a required reservation affinity (Filter only on reserved resources): refused  */
+#define KE_RSV_AFFINITY 2 /* a required reservation affinity: as KE_RSV_MATCHED, and the Reservation Filter
+                             passes only nodes where a listed reservation fits (an empty list: unschedulable) */
 #define KE_RSV_IGNORED 3  /* reservation-ignored pod: refused                                               */
 /* For each pod of the next ke_schedule call, the reservations (indices into the loaded set) it matches,
- * ids[offsets[p] .. offsets[p+1]).  Only KE_RSV_MATCHED pods may list any; the call consumes the lists.
+ * ids[offsets[p] .. offsets[p+1]) (with a reservation name in the affinity: only that one).  Only KE_RSV_MATCHED /
+ * KE_RSV_AFFINITY pods may list any; the call consumes the lists.
  * For a KE_RSV_MATCHED pod the evaluator runs, as the Reservation plugin and the transformer do:
  *  - BeforePreFilter: of its listed reservations the available ones that are not AllocateOnce with
  *    allocated pods are "matched" on their nodes; restoreMatchedReservation (transformer.go:422-445)
  *    removes each one's reserve pod from NodeInfo (Requested and NonZeroRequested -= allocatable), the
  *    other reservations restore as for any pod;
- *  - Filter passes (no reservation affinity, plugin.go:351-354);
+ *  - Filter passes without a reservation affinity (plugin.go:351-354); with one (KE_RSV_AFFINITY) only nodes
+ *    holding a matched reservation that fits (fitsNode, and fitsReservation for Restricted) pass
+ *    (plugin.go:316-318, 368-441), and NominateReservation takes a node's only matched one unfiltered (:223-225);
  *  - PreScore / NominateReservation (scoring.go:42-109, nominator.go:207-278): per node the matched
  *    reservations passing FilterNominateReservation (plugin.go:707-738: resource names shared with the pod,
  *    fitsNode over the restored NodeInfo, fitsReservation for Restricted) are nominated by the smallest

@@ -47,9 +47,8 @@ static int check_pods(const ke_pod* pods, int32_t n, const Context* c = nullptr,
     if (rc) return rc;
     const uint8_t rm = pods[p].reservation_matched;
     if (rm > KE_RSV_IGNORED) return fail(KE_ERR_INVALID, "ke_pod.reservation_matched");
-    if (rm == KE_RSV_AFFINITY) return fail(KE_ERR_UNSUPPORTED, "a pod with a required reservation affinity");
     if (rm == KE_RSV_IGNORED) return fail(KE_ERR_UNSUPPORTED, "a reservation-ignored pod");
-    if (rm == KE_RSV_MATCHED && !matched_ok)
+    if ((rm == KE_RSV_MATCHED || rm == KE_RSV_AFFINITY) && !matched_ok)
       return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations outside ke_schedule");
     if (c) rc = validate_pod_hints(*c, pods[p]);
     else if (pods[p].device_hint) rc = fail(KE_ERR_INVALID, "ke_pod.device_hint without a context");
@@ -97,11 +96,12 @@ static int check_matches(Context& c, const ke_pod* pods, int32_t n) {
   }
   for (int32_t p = 0; p < n; p++) {
     const int32_t cnt = staged ? c.match_off[(size_t)p + 1] - c.match_off[(size_t)p] : 0;
-    if (pods[p].reservation_matched != KE_RSV_MATCHED) {
-      if (cnt) return fail(KE_ERR_INVALID, "reservations listed for a pod that is not KE_RSV_MATCHED");
+    const uint8_t rm = pods[p].reservation_matched;
+    if (rm != KE_RSV_MATCHED && rm != KE_RSV_AFFINITY) {
+      if (cnt) return fail(KE_ERR_INVALID, "reservations listed for a pod that is not KE_RSV_MATCHED / AFFINITY");
       continue;
     }
-    if (!staged) return fail(KE_ERR_INVALID, "a KE_RSV_MATCHED pod without ke_pod_reservations");
+    if (!staged) return fail(KE_ERR_INVALID, "a KE_RSV_MATCHED / AFFINITY pod without ke_pod_reservations");
     const uint32_t f = c.staged[(size_t)p].flags;
     bool scalar = pods[p].has_other_requests || pods[p].has_unsupported_device_requests;
     for (int r = KE_NRES; r < KE_RES_COUNT; r++) scalar = scalar || pods[p].requests[r] != 0;
@@ -642,7 +642,10 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
   std::vector<int32_t> moff, mids;
   moff.swap(c.match_off);  // consumed by this call
   mids.swap(c.match_ids);
-  auto matched = [&](int32_t p) { return !moff.empty() && moff[(size_t)p + 1] > moff[(size_t)p]; };
+  auto matched = [&](int32_t p) {
+    return pods[p].reservation_matched == KE_RSV_AFFINITY ||
+           (!moff.empty() && moff[(size_t)p + 1] > moff[(size_t)p]);
+  };
   std::vector<int32_t> assumed((size_t)n_pods, 0);
   for (int32_t s0 = 0; s0 < n_pods || (n_pods == 0 && s0 == 0);) {
     int32_t s1 = s0;
@@ -651,7 +654,8 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
     const int32_t len = s1 - s0;
     const bool rsv = len == 1 && matched(s0);
     if (rsv) {
-      rc = resv_prepare(c, pods[s0], mids.data() + moff[(size_t)s0], moff[(size_t)s0 + 1] - moff[(size_t)s0]);
+      rc = resv_prepare(c, pods[s0], mids.data() + moff[(size_t)s0], moff[(size_t)s0 + 1] - moff[(size_t)s0],
+                        pods[s0].reservation_matched == KE_RSV_AFFINITY);
       if (rc) return rc;
     }
     rc = device_schedule(&c, len, pods + s0, now_ns, chosen + (n_pods ? s0 : 0), score ? score + s0 : nullptr);
@@ -659,7 +663,7 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
     if (rsv) {
       const int32_t local = chosen[s0] < 0 ? -1 : chosen[s0] - off;
       int32_t pick[4] = {local, 0, 0, -1};  // no usable matched reservation: no Reservation score
-      if (!c.rsv_pairs.empty()) rc = device_rsv_result(&c, pick);
+      if (!c.rsv_pairs.empty() || c.rsv_affinity) rc = device_rsv_result(&c, pick);
       if (rc) return rc;
       if (local >= 0 && local != pick[0]) return fail(KE_ERR_DEVICE, "k_rsv_pick winner differs from the placement");
       if (local >= 0 && score) score[s0] += (int32_t)c.cfg.weight_reservation * pick[1];

@@ -573,11 +573,12 @@ int load_reservations(Context& c, int32_t n, const ke_reservation* rs) {
 // NodeInfo (plugin.go:447-497; preemptible empty; the pod-count check not modelled) and, for Restricted,
 // fitsReservation (plugin.go:499-569).  podRequested = Requested after the unmatched restore only,
 // allRAllocated = Σ allocated of the node's matched reservations.
+// With a reservation affinity the name check is skipped (the pod may use any matched reservation, :373).
 static bool resv_nominable(const ke_reservation& r, const ke_pod& pod, const int64_t* alloc, const int64_t* pod_requested,
-                           const int64_t* all_allocated) {
+                           const int64_t* all_allocated, bool affinity) {
   bool shared = false;
   for (int k = 0; k < KE_NRES; k++) shared = shared || (r.allocatable[k] != 0 && pod.requests[k] != 0);
-  if (!shared) return false;
+  if (!shared && !affinity) return false;
   bool node_fits = true;
   if (pod.requests[KE_RES_CPU] != 0 || pod.requests[KE_RES_MEMORY] != 0)
     for (int k = 0; k < KE_NRES; k++) {
@@ -607,7 +608,8 @@ int32_t resv_score(const ke_reservation& r, const ke_pod& pod) {
   return w ? (int32_t)(s / w) : 0;
 }
 
-int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids) {
+int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids, bool affinity) {
+  c.rsv_affinity = affinity;
   c.rsv_pairs.clear();
   c.rsv_nominated.clear();
   c.rsv_nodes.clear();
@@ -640,10 +642,15 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
       }
     std::vector<int32_t> ok;
     for (int32_t i : mine)
-      if (resv_nominable(c.resv[(size_t)i], pod, ns.node.allocatable, pod_requested, all_alloc)) ok.push_back(i);
-    // NominateReservation (nominator.go:237-277): the only one, else the smallest order, else the best
-    // ScoreReservation (ties -> lowest index: sort.Slice's insertion sort keeps them below 13 elements)
+      if (resv_nominable(c.resv[(size_t)i], pod, ns.node.allocatable, pod_requested, all_alloc, affinity)) ok.push_back(i);
+    // the Reservation Filter with a reservation affinity (plugin.go:316-318, 351-442): a node without matched
+    // reservations fails, one with them passes when one of them fits (the same checks as the nomination's)
+    const bool allowed = !affinity || !ok.empty();
+    // NominateReservation (nominator.go:223-277): with an affinity and one matched reservation that one, else
+    // the survivors: the only one, else the smallest order, else the best ScoreReservation (ties -> lowest
+    // index: sort.Slice's insertion sort keeps them below 13 elements)
     int32_t nom = -1;
+    if (affinity && mine.size() == 1) ok.assign(1, mine[0]);
     if (ok.size() == 1) nom = ok[0];
     if (ok.size() > 1) {
       int64_t bo = 0;
@@ -665,7 +672,7 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
         }
       }
     }
-    c.rsv_pairs.push_back({node, nom >= 0 ? resv_score(c.resv[(size_t)nom], pod) : 0, order});
+    c.rsv_pairs.push_back({node, (int16_t)(nom >= 0 ? resv_score(c.resv[(size_t)nom], pod) : 0), (int16_t)allowed, order});
     c.rsv_nominated.push_back(nom);
     // the rows this pod sees: its matched reservations restored too
     resv_delta(c, node, &m, true, ns.rv_req, ns.rv_nz);
@@ -686,6 +693,7 @@ void resv_finish(Context& c, int32_t chosen_local, const ke_pod& pod, int32_t* a
       *assumed = 1 + c.rsv_nominated[j];
     }
   for (int32_t node : c.rsv_nodes) resv_node_restore(c, node);
+  c.rsv_affinity = false;
   c.rsv_pairs.clear();
   c.rsv_nominated.clear();
   c.rsv_nodes.clear();

@@ -40,9 +40,10 @@ struct DirtyFlag {
 
 // one node holding reservations a pod matches (k_rsv_pick)
 struct RsvPair {
-  int32_t node;   // local node index
-  int32_t raw;    // ScoreReservation of the nominated reservation (0 = none)
-  int64_t order;  // smallest reservation-order label of the matched reservations (0 = none)
+  int32_t node;     // local node index
+  int16_t raw;      // ScoreReservation of the nominated reservation (0 = none)
+  int16_t allowed;  // the Reservation plugin's Filter passes (always without a reservation affinity)
+  int64_t order;    // smallest reservation-order label of the matched reservations (0 = none)
 };
 
 struct NodeState {
@@ -159,6 +160,7 @@ struct Context {
   std::vector<int32_t> rsv_nodes;
   std::vector<RsvPair> rsv_pairs;
   std::vector<int32_t> rsv_nominated;
+  bool rsv_affinity = false;  // the segment's pod has a required reservation affinity
   std::vector<int32_t> last_resv;  // per pod of the last ke_schedule: 1 + the reservation assumed, 0 = none
   // device_refresh: g_dirty_epoch when every row was last clean, and the earliest valid_until then
   uint64_t clean_epoch = UINT64_MAX;
@@ -247,7 +249,7 @@ void resv_node_restore(Context& c, int32_t node);  // the restore every non-matc
 int32_t resv_score(const ke_reservation& r, const ke_pod& pod);
 // the nominated-reservation path of one KE_RSV_MATCHED pod: rows with its matched restore, rsv_pairs /
 // rsv_nominated; resv_finish assumes the pod into the chosen node's nominated reservation (1 + index, 0)
-int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids);
+int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids, bool affinity);
 void resv_finish(Context& c, int32_t chosen_local, const ke_pod& pod, int32_t* assumed);
 void resv_forget(Context& c, int32_t idx, const ke_pod& pod);
 // NodeResourcesFitPlus' (NonZero)Requested of resource `id` on the node, with the reservation restore

@@ -3095,14 +3095,18 @@ __global__ __launch_bounds__(256) void k_argmax1(const uint16_t* __restrict__ sc
 //   3. selectHost over total + w * n: a 64-bit key over the K nodes against k_argmax1's winner (n = 0).
 // cand[0] becomes the winner's 32-bit key (its plugin total without the Reservation part); out = {winner
 // node or -1, its n, max, preferredNode or -1}.
+// With a reservation affinity only the pairs' allowed nodes pass the Reservation Filter: k_argmax1's winner
+// does not count and the others are infeasible.
 __global__ __launch_bounds__(64) void k_rsv_pick(const uint16_t* __restrict__ scores, const RsvPair* __restrict__ pr,
-                                                 int K, int64_t w, uint32_t* __restrict__ cand, int32_t* __restrict__ out) {
+                                                 int K, int64_t w, int affinity, uint32_t* __restrict__ cand,
+                                                 int32_t* __restrict__ out) {
   const int l = (int)threadIdx.x;
+  auto feasible = [&](const RsvPair& q) { return scores[q.node] != 0 && q.allowed != 0; };
   int64_t bo = INT64_MAX;
   int32_t bn = INT32_MAX;
   for (int i = l; i < K; i += 64) {
     const RsvPair q = pr[i];
-    if (q.order != 0 && scores[q.node] && (q.order < bo || (q.order == bo && q.node < bn))) {
+    if (q.order != 0 && feasible(q) && (q.order < bo || (q.order == bo && q.node < bn))) {
       bo = q.order;
       bn = q.node;
     }
@@ -3119,17 +3123,17 @@ __global__ __launch_bounds__(64) void k_rsv_pick(const uint16_t* __restrict__ sc
   int32_t mx = 0;
   for (int i = l; i < K; i += 64) {
     const RsvPair q = pr[i];
-    if (scores[q.node]) mx = max(mx, q.node == pref ? 1000 : q.raw);
+    if (feasible(q)) mx = max(mx, q.node == pref ? 1000 : (int32_t)q.raw);
   }
   for (int m = 32; m; m >>= 1) mx = max(mx, __shfl_xor(mx, m));
-  const uint32_t g = cand[0];  // k_argmax1's key: (total + 1) << KEY_IDX_BITS | (mask - node), 0 = none
+  const uint32_t g = affinity ? 0u : cand[0];  // k_argmax1's key: (total + 1) << KEY_IDX_BITS | (mask - node)
   uint64_t best = g;
-  if (mx > 0)
+  if (mx > 0 || affinity)
     for (int i = l; i < K; i += 64) {
       const RsvPair q = pr[i];
       const uint32_t v = scores[q.node];
-      if (!v) continue;
-      const int64_t n = 100 * (int64_t)(q.node == pref ? 1000 : q.raw) / mx;
+      if (!feasible(q)) continue;
+      const int64_t n = mx > 0 ? 100 * (int64_t)(q.node == pref ? 1000 : q.raw) / mx : 0;
       const uint64_t key = ((uint64_t)(v + w * n) << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)q.node);
       best = key > best ? key : best;
     }
@@ -3146,7 +3150,7 @@ __global__ __launch_bounds__(64) void k_rsv_pick(const uint16_t* __restrict__ sc
     }
   for (int m = 32; m; m >>= 1) nw = max(nw, __shfl_xor(nw, m));
   if (l == 0) {
-    if (win >= 0) cand[0] = ((uint32_t)scores[win] << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)win);
+    cand[0] = win >= 0 ? ((uint32_t)scores[win] << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)win) : 0u;
     out[0] = win;
     out[1] = nw;
     out[2] = mx;
@@ -5845,14 +5849,15 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     HIP_OK(hipMemsetAsync(d->d_defer_cnt, 0, sizeof(uint32_t) * n_batches, d->stream));
   }
   KArgs k = make_kargs(ctx, now);
-  if (!ctx->rsv_pairs.empty()) {  // one KE_RSV_MATCHED pod (ke_schedule's segment of its own)
+  if (!ctx->rsv_pairs.empty() || ctx->rsv_affinity) {  // one matched pod (ke_schedule's segment of its own)
     if (n_pods != 1 || d->world > 1 || d->comm) return fail(KE_ERR_UNSUPPORTED, "matched reservations need an unsharded singleton");
     for (const RsvPair& q : ctx->rsv_pairs)
       if (q.node < 0 || q.node >= ctx->n_nodes) return fail(KE_ERR_DEVICE, "reservation pair node out of range");
     rc = ensure((void**)&d->d_rsv, &d->rsv_cap, (int64_t)sizeof(RsvPair) * (int64_t)ctx->rsv_pairs.size());
     if (rc) return rc;
-    HIP_OK(hipMemcpyAsync(d->d_rsv, ctx->rsv_pairs.data(), sizeof(RsvPair) * ctx->rsv_pairs.size(), hipMemcpyHostToDevice,
-                          d->stream));
+    if (!ctx->rsv_pairs.empty())
+      HIP_OK(hipMemcpyAsync(d->d_rsv, ctx->rsv_pairs.data(), sizeof(RsvPair) * ctx->rsv_pairs.size(),
+                            hipMemcpyHostToDevice, d->stream));
     HIP_OK(hipMemsetAsync(d->d_rsv_out, 0xFF, sizeof(int32_t) * 4, d->stream));
   }
   const bool quota = !ctx->quotas.empty();  // ElasticQuota admission + Reserve in the Reserve kernels
@@ -5996,9 +6001,9 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       if (argmax1) {  // d_cand[0] zeroed by k_batch_begin
         hipLaunchKernelGGL((ds ? k_argmax1<true> : k_argmax1<false>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
                            es, d->d_scores, 0, N, d->d_dsraw, d->d_dsmax, k.wp_ds, d->d_cand, d->d_cand_cnt);
-        if (!ctx->rsv_pairs.empty())  // the pod's matched reservations: the Reservation plugin's score
+        if (!ctx->rsv_pairs.empty() || ctx->rsv_affinity)  // the pod's matched reservations: the Reservation plugin
           hipLaunchKernelGGL(k_rsv_pick, dim3(1), dim3(64), 0, es, d->d_scores, d->d_rsv, (int)ctx->rsv_pairs.size(),
-                             (int64_t)ctx->cfg.weight_reservation, d->d_cand, d->d_rsv_out);
+                             (int64_t)ctx->cfg.weight_reservation, (int)ctx->rsv_affinity, d->d_cand, d->d_rsv_out);
       } else if (!sharded && parts > 1) {
         const int gw = gath_words(L);
         const bool rc = select_seg(0, select_part(0, N, parts)) <= SEL_RC * 512;

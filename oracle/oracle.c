@@ -404,7 +404,7 @@ static int pod_is_cpuset(const ke_pod* pod) {
 }
 static int pod_unsupported(const ke_pod* pod) {
   /* KE_RSV_MATCHED pods are checked by or_schedule (or_resv_supported); affinity / ignored are refused */
-  return pod->has_resource_spec || pod->has_unsupported_device_requests || pod->reservation_matched > KE_RSV_MATCHED;
+  return pod->has_resource_spec || pod->has_unsupported_device_requests || pod->reservation_matched > KE_RSV_AFFINITY;
 }
 static int node_unsupported(const ke_node* n) {
   return n->numa_topology_policy < 0 || n->numa_topology_policy > KE_NUMA_POLICY_SINGLE_NUMA_NODE ||
@@ -2978,11 +2978,11 @@ int64_t or_reservation_score(const ke_reservation* r, const ke_pod* pod) {
  * of the node's matched reservations; fitsReservation (:499-569) for the Restricted policy, else the node fit.
  * The NUMA / DeviceShare FilterNominateReservation pass for pods without cpuset, NUMA policy or devices. */
 static int or_resv_nominable(const or_cluster* c, const ke_reservation* r, const ke_pod* pod, int32_t node,
-                             const int64_t* pod_requested, const int64_t* all_allocated) {
+                             const int64_t* pod_requested, const int64_t* all_allocated, int affinity) {
   int shared = 0;
   for (int k = 0; k < KE_NRES; k++)
     if (r->allocatable[k] != 0 && pod->requests[k] != 0) shared = 1;
-  if (!shared) return 0;
+  if (!shared && !affinity) return 0; /* plugin.go:373: skipped only without a reservation affinity */
   int node_fits = 1;
   if (!(pod->requests[KE_RES_CPU] == 0 && pod->requests[KE_RES_MEMORY] == 0)) {
     for (int k = 0; k < KE_NRES; k++) {
@@ -3579,7 +3579,7 @@ int or_eval(const or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now
  * pod_requested[i*KE_NRES + k]: NodeInfo Requested after the unmatched restore.  raw[i] = Score (before
  * NormalizeScore), nom[i] = the nominated reservation or -1.  Returns preferredNode or -1. */
 static int32_t or_resv_prescore(const or_cluster* c, const ke_pod* pod, const char* m, const int64_t* pod_requested,
-                                const uint8_t* feasible, int64_t* raw, int32_t* nom) {
+                                const uint8_t* feasible, int affinity, int64_t* raw, int32_t* nom) {
   const int32_t N = c->n;
   int32_t pref = -1;
   int64_t po = 0;
@@ -3595,11 +3595,13 @@ static int32_t or_resv_prescore(const or_cluster* c, const ke_pod* pod, const ch
         if (c->resv[r].order != 0 && (order == 0 || c->resv[r].order < order)) order = c->resv[r].order;
       }
     if (!any) continue;
-    int32_t n_ok = 0, first = -1, by_order = -1, by_score = -1;
+    int32_t n_ok = 0, first = -1, by_order = -1, by_score = -1, n_matched = 0, only = -1;
     int64_t bo = 0, bsc = -1;
     for (int32_t r = 0; r < c->n_resv; r++) {
       if (!m[r] || c->resv[r].node != i) continue;
-      if (!or_resv_nominable(c, &c->resv[r], pod, i, &pod_requested[i * KE_NRES], all_alloc)) continue;
+      n_matched++;
+      only = r;
+      if (!or_resv_nominable(c, &c->resv[r], pod, i, &pod_requested[i * KE_NRES], all_alloc, affinity)) continue;
       n_ok++;
       if (first < 0) first = r;
       if (c->resv[r].order != 0 && (bo == 0 || c->resv[r].order < bo)) {
@@ -3613,6 +3615,7 @@ static int32_t or_resv_prescore(const or_cluster* c, const ke_pod* pod, const ch
       }
     }
     nom[i] = n_ok == 0 ? -1 : n_ok == 1 ? first : by_order >= 0 ? by_order : by_score;
+    if (affinity && n_matched == 1) nom[i] = only; /* nominator.go:223-225 */
     raw[i] = nom[i] >= 0 ? or_reservation_score(&c->resv[nom[i]], pod) : 0;
     if ((!feasible || feasible[i]) && order != 0 && (pref < 0 || order < po)) {
       po = order;
@@ -3643,7 +3646,7 @@ int32_t or_reservation_prescore(or_cluster* c, const ke_pod* pod, const int32_t*
                                 int32_t* nom) {
   int64_t* pr;
   char* m = or_resv_begin(c, ids, n_ids, &pr);
-  const int32_t pref = or_resv_prescore(c, pod, m, pr, NULL, raw, nom);
+  const int32_t pref = or_resv_prescore(c, pod, m, pr, NULL, 0, raw, nom);
   or_restore(c, NULL, 0);
   free(m);
   free(pr);
@@ -3655,7 +3658,7 @@ int32_t or_reservation_prescore(or_cluster* c, const ke_pod* pod, const int32_t*
  * feasible nodes, scoring.go:134-139) and selectHost over the total with weight_reservation.  Returns the
  * chosen node (-1), its total in *best and the nominated reservation of every node in nom[]. */
 static int32_t or_resv_eval(or_cluster* c, const ke_pod* pod, int64_t now, eval_out* o, const int32_t* ids, int32_t n_ids,
-                            int32_t* best, int32_t* nom) {
+                            int affinity, int32_t* best, int32_t* nom) {
   const int32_t N = c->n;
   int64_t* pr;
   char* m = or_resv_begin(c, ids, n_ids, &pr);
@@ -3664,8 +3667,24 @@ static int32_t or_resv_eval(or_cluster* c, const ke_pod* pod, int64_t now, eval_
   or_restore(c, NULL, 0);
   uint8_t* feasible = (uint8_t*)malloc((size_t)(N > 0 ? N : 1));
   for (int32_t i = 0; i < N; i++) feasible[i] = o[i].status == KE_CODE_SUCCESS;
+  if (affinity) {
+    /* the Reservation Filter with a reservation affinity (plugin.go:316-318, 351-442): only nodes with a matched
+     * reservation that fits (fitsNode, and fitsReservation for Restricted) pass */
+    for (int32_t i = 0; i < N; i++) {
+      if (!feasible[i]) continue;
+      int64_t all_alloc[KE_NRES] = {0, 0};
+      for (int32_t r = 0; r < c->n_resv; r++)
+        if (m[r] && c->resv[r].node == i)
+          for (int k = 0; k < KE_NRES; k++) all_alloc[k] += c->resv[r].allocated[k];
+      int fit = 0;
+      for (int32_t r = 0; r < c->n_resv && !fit; r++)
+        if (m[r] && c->resv[r].node == i)
+          fit = or_resv_nominable(c, &c->resv[r], pod, i, &pr[i * KE_NRES], all_alloc, 1);
+      feasible[i] = (uint8_t)fit;
+    }
+  }
   int64_t* raw = (int64_t*)malloc(sizeof(int64_t) * (size_t)(N > 0 ? N : 1));
-  (void)or_resv_prescore(c, pod, m, pr, feasible, raw, nom);
+  (void)or_resv_prescore(c, pod, m, pr, feasible, affinity, raw, nom);
   int64_t mx = 0;
   for (int32_t i = 0; i < N; i++)
     if (feasible[i] && raw[i] > mx) mx = raw[i];
@@ -3694,7 +3713,7 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
   for (int i = 0; i < c->n; i++) node_bind |= c->nodes[i].node.cpu_bind_policy != KE_NODE_CPU_BIND_NONE;
   for (int32_t p = 0; p < n_pods; p++) {
     const int32_t n_ids = c->moff && c->m_pods == n_pods ? c->moff[p + 1] - c->moff[p] : 0;
-    if (pods[p].reservation_matched != KE_RSV_MATCHED) {
+    if (pods[p].reservation_matched != KE_RSV_MATCHED && pods[p].reservation_matched != KE_RSV_AFFINITY) {
       if (n_ids) return KE_ERR_INVALID;
       continue;
     }
@@ -3750,9 +3769,10 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
     }
     int16_t bs16;
     int32_t bs, b;
-    const int32_t n_ids = c->moff && pods[p].reservation_matched == KE_RSV_MATCHED ? c->moff[p + 1] - c->moff[p] : 0;
-    if (n_ids > 0) {
-      b = or_resv_eval(c, &pods[p], now, o, c->mids + c->moff[p], n_ids, &bs, nom);
+    const int affinity = pods[p].reservation_matched == KE_RSV_AFFINITY;
+    const int32_t n_ids = c->moff && pods[p].reservation_matched ? c->moff[p + 1] - c->moff[p] : 0;
+    if (n_ids > 0 || affinity) {
+      b = or_resv_eval(c, &pods[p], now, o, c->moff ? c->mids + c->moff[p] : NULL, n_ids, affinity, &bs, nom);
     } else {
       b = eval_pod(c, &pods[p], now, o, &bs16);
       bs = bs16;
@@ -3792,7 +3812,7 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
         }
       }
       if (c->quotas) orq_reserve(c->quotas, &pods[p]); /* ElasticQuota Reserve */
-      if (n_ids > 0 && nom[b] >= 0) {
+      if ((n_ids > 0 || affinity) && nom[b] >= 0) {
         /* Reservation Reserve: assumePod -> AddAssignedPod (reservation/plugin.go:783,
          * reservation_info.go:458-468): allocated += Mask(requests, ResourceNames), one more allocated pod */
         ke_reservation* r = &c->resv[nom[b]];

@@ -59,7 +59,7 @@ def test_reservation_restore_schedule_parity(gpu):
     assert ev.check_records(synth.T0) == 0
 
 
-def _matched_setup(n, seed, n_pods, quota=False):
+def _matched_setup(n, seed, n_pods, affinity=0.0):
     """A FitPlus + amplified-cpu cluster whose NodeInfo holds the reserve pods of owner-grouped reservations
     (Default / Aligned / Restricted, AllocateOnce, orders, some already allocated), and a queue in which
     about 40 % of the eligible pods match one owner group's reservations (KE_RSV_MATCHED)."""
@@ -93,8 +93,10 @@ def _matched_setup(n, seed, n_pods, quota=False):
     grp = np.asarray(grp)
     matches = [[] for _ in range(n_pods)]
     for p in np.flatnonzero(elig & (rng.random(n_pods) < 0.4)):
-        pods["reservation_matched"][p] = abi.RSV_MATCHED
+        pods["reservation_matched"][p] = abi.RSV_AFFINITY if rng.random() < affinity else abi.RSV_MATCHED
         matches[p] = np.flatnonzero(grp == rng.integers(0, 10)).tolist()
+        if pods["reservation_matched"][p] == abi.RSV_AFFINITY and rng.random() < 0.2:
+            matches[p] = matches[p][:1] if rng.random() < 0.5 else []  # by name / no reservation left
     return ev, o, pods, matches
 
 
@@ -167,4 +169,24 @@ def test_matched_reservations_weight_one(gpu):
     c0, s0 = o.schedule(pods, synth.T0, matches=matches)
     assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
     _resv_equal(ev, o)
+    assert ev.check_records(synth.T0) == 0
+
+
+def test_reservation_affinity_schedule_parity(gpu):
+    """Required reservation affinity (KE_RSV_AFFINITY): the Reservation Filter keeps only nodes where a listed
+    reservation fits, a one-reservation node nominates it unfiltered, an empty list leaves the pod unschedulable;
+    mixed with KE_RSV_MATCHED and plain pods, bit-exact with the oracle."""
+    ev, o, pods, matches = _matched_setup(300, 981, 260, affinity=0.5)
+    aff = pods["reservation_matched"] == abi.RSV_AFFINITY
+    assert aff.sum() >= 10
+    c1, s1 = ev.schedule(pods, synth.T0, matches=matches)
+    c0, s0 = o.schedule(pods, synth.T0, matches=matches)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5].ravel().tolist()
+    assert np.array_equal(s1, s0)
+    _resv_equal(ev, o)
+    a1 = ev.last_allocations()
+    assert np.array_equal(a1["reservation"], o.last_allocations()["reservation"])
+    placed_aff = aff & (c1 >= 0)
+    assert (a1["reservation"][placed_aff] > 0).all()  # an affinity pod is placed only into a reservation
+    assert (c1[aff & np.array([len(m) == 0 for m in matches])] == -1).all()
     assert ev.check_records(synth.T0) == 0

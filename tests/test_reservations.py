@@ -113,11 +113,14 @@ def test_matched_pod_checks():
     with pytest.raises(KoordEvalError) as e:
         ev.pod_reservations([[], [1]])  # no such reservation
     assert e.value.code == abi.ERR_NOT_FOUND
-    for v in (abi.RSV_AFFINITY, abi.RSV_IGNORED):
-        pods["reservation_matched"][1] = v
-        with pytest.raises(KoordEvalError) as e:
-            ev.schedule(pods, synth.T0)
-        assert e.value.code == abi.ERR_UNSUPPORTED
+    pods["reservation_matched"][1] = abi.RSV_IGNORED
+    with pytest.raises(KoordEvalError) as e:
+        ev.schedule(pods, synth.T0)
+    assert e.value.code == abi.ERR_UNSUPPORTED
+    pods["reservation_matched"][1] = abi.RSV_AFFINITY
+    with pytest.raises(KoordEvalError) as e:
+        ev.schedule(pods, synth.T0)  # an affinity pod needs its (possibly empty) list staged
+    assert e.value.code == abi.ERR_INVALID
     pods["reservation_matched"][1] = abi.RSV_MATCHED
     pods["requests"][1][abi.RES_BATCH_CPU] = 1000  # a scalar request
     with pytest.raises(KoordEvalError) as e:
