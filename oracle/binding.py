@@ -60,6 +60,7 @@ def load():
         "or_last_reservations": (C.c_int, [V, i32, V]),
         "or_reservation_score": (C.c_int64, [V, V]),
         "or_reservation_prescore": (i32, [V, V, V, i32, V, V]),
+        "or_reservation_filter": (i32, [V, V, V, i32, i32]),
         "or_node_info_requested": (C.c_int, [V, i32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
         "or_node_device_flags": (C.c_int, [V, i32, i32, i32]),
         "or_last_vf_ranks": (C.c_int, [V, i32, V]),
@@ -289,6 +290,12 @@ class Oracle:
         nom = np.zeros(self.n, np.int32)
         pref = self.lib.or_reservation_prescore(self.h, abi.ptr(p), abi.ptr(ids), len(ids), abi.ptr(raw), abi.ptr(nom))
         return int(pref), raw, nom
+
+    def reservation_filter(self, pod, ids, node):
+        """The Reservation Filter of `pod` with a required reservation affinity over reservations `ids` on `node`."""
+        p = as_pod_array([pod] if isinstance(pod, abi.Pod) else np.asarray(pod).reshape(1))
+        ids = np.ascontiguousarray(ids, np.int32)
+        return bool(self.lib.or_reservation_filter(self.h, abi.ptr(p), abi.ptr(ids), len(ids), int(node)))
 
     def reservation_score(self, reservation, pod):
         """scoreReservation of one reservation record for one pod (golden-vector entry point)."""

@@ -3626,6 +3626,21 @@ static int32_t or_resv_prescore(const or_cluster* c, const ke_pod* pod, const ch
   return pref;
 }
 
+/* The Reservation Filter of a pod with a reservation affinity on node i (plugin.go:316-318, 351-442): a node
+ * without matched reservations fails, one with them passes when one fits (fitsNode, and fitsReservation for
+ * Restricted; resource names are not required to overlap with an affinity) */
+static int or_resv_filter_node(const or_cluster* c, const ke_pod* pod, const char* m, const int64_t* pod_requested,
+                               int32_t i) {
+  int64_t all_alloc[KE_NRES] = {0, 0};
+  for (int32_t r = 0; r < c->n_resv; r++)
+    if (m[r] && c->resv[r].node == i)
+      for (int k = 0; k < KE_NRES; k++) all_alloc[k] += c->resv[r].allocated[k];
+  for (int32_t r = 0; r < c->n_resv; r++)
+    if (m[r] && c->resv[r].node == i && or_resv_nominable(c, &c->resv[r], pod, i, &pod_requested[i * KE_NRES], all_alloc, 1))
+      return 1;
+  return 0;
+}
+
 /* matched flags + fitsNode's podRequested for the listed reservations of a pod; the rows left restored with
  * the matched ones (with_matched) */
 static char* or_resv_begin(or_cluster* c, const int32_t* ids, int32_t n_ids, int64_t** pod_requested) {
@@ -3653,6 +3668,17 @@ int32_t or_reservation_prescore(or_cluster* c, const ke_pod* pod, const int32_t*
   return pref;
 }
 
+/* golden-vector entry point: the Reservation Filter with a reservation affinity on `node` (1 = passes) */
+int32_t or_reservation_filter(or_cluster* c, const ke_pod* pod, const int32_t* ids, int32_t n_ids, int32_t node) {
+  int64_t* pr;
+  char* m = or_resv_begin(c, ids, n_ids, &pr);
+  const int32_t ok = or_resv_filter_node(c, pod, m, pr, node);
+  or_restore(c, NULL, 0);
+  free(m);
+  free(pr);
+  return ok;
+}
+
 /* A KE_RSV_MATCHED pod: BeforePreFilter restore with its matched reservations, Filter / Score of the plugins
  * (eval_pod), the Reservation plugin's PreScore / Score, NormalizeScore (DefaultNormalizeScore over the
  * feasible nodes, scoring.go:134-139) and selectHost over the total with weight_reservation.  Returns the
@@ -3667,22 +3693,9 @@ static int32_t or_resv_eval(or_cluster* c, const ke_pod* pod, int64_t now, eval_
   or_restore(c, NULL, 0);
   uint8_t* feasible = (uint8_t*)malloc((size_t)(N > 0 ? N : 1));
   for (int32_t i = 0; i < N; i++) feasible[i] = o[i].status == KE_CODE_SUCCESS;
-  if (affinity) {
-    /* the Reservation Filter with a reservation affinity (plugin.go:316-318, 351-442): only nodes with a matched
-     * reservation that fits (fitsNode, and fitsReservation for Restricted) pass */
-    for (int32_t i = 0; i < N; i++) {
-      if (!feasible[i]) continue;
-      int64_t all_alloc[KE_NRES] = {0, 0};
-      for (int32_t r = 0; r < c->n_resv; r++)
-        if (m[r] && c->resv[r].node == i)
-          for (int k = 0; k < KE_NRES; k++) all_alloc[k] += c->resv[r].allocated[k];
-      int fit = 0;
-      for (int32_t r = 0; r < c->n_resv && !fit; r++)
-        if (m[r] && c->resv[r].node == i)
-          fit = or_resv_nominable(c, &c->resv[r], pod, i, &pr[i * KE_NRES], all_alloc, 1);
-      feasible[i] = (uint8_t)fit;
-    }
-  }
+  if (affinity)
+    for (int32_t i = 0; i < N; i++)
+      if (feasible[i]) feasible[i] = (uint8_t)or_resv_filter_node(c, pod, m, pr, i);
   int64_t* raw = (int64_t*)malloc(sizeof(int64_t) * (size_t)(N > 0 ? N : 1));
   (void)or_resv_prescore(c, pod, m, pr, feasible, affinity, raw, nom);
   int64_t mx = 0;

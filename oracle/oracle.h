@@ -49,6 +49,7 @@ int or_reservations_get(const or_cluster* c, int32_t n, ke_reservation* out);
 int or_pod_reservations(or_cluster* c, int32_t n_pods, const int32_t* offsets, const int32_t* ids);
 int or_last_reservations(const or_cluster* c, int32_t n, int32_t* out);
 int64_t or_reservation_score(const ke_reservation* r, const ke_pod* pod);
+int32_t or_reservation_filter(or_cluster* c, const ke_pod* pod, const int32_t* ids, int32_t n_ids, int32_t node);
 int32_t or_reservation_prescore(or_cluster* c, const ke_pod* pod, const int32_t* ids, int32_t n_ids, int64_t* raw,
                                 int32_t* nom);
 int or_node_info_requested(const or_cluster* c, int32_t node, int64_t* requested, int64_t* non_zero);

@@ -137,7 +137,8 @@ SCORE_CASES = json.load(open(os.path.join(HERE, "golden", "reservation_scores.js
 
 @pytest.mark.parametrize("case", SCORE_CASES, ids=[c["name"] for c in SCORE_CASES])
 def test_reservation_score_golden(case):
-    """The oracle's Reservation PreScore / NominateReservation / Score against TestScore and TestScoreWithOrder."""
+    """The oracle's Reservation PreScore / NominateReservation / Score against TestScore, TestScoreWithOrder and
+    TestNominateReservation."""
     n = len(case["nodes"])
     cfg = synth.config(n)
     o = Oracle(cfg, n)
@@ -164,4 +165,38 @@ def test_reservation_score_golden(case):
     pod["requests"][0][:2] = case["pod"]
     pod["reservation_matched"][0] = abi.RSV_MATCHED
     pref, raw, nom = o.reservation_prescore(pod[0], list(range(len(rs))))
-    assert list(raw) == case["want_score"]
+    if case["want_score"] is not None:
+        assert list(raw) == case["want_score"]
+    if case["want_nominated"] is not None:
+        assert list(nom) == case["want_nominated"]
+
+
+FILTER_CASES = json.load(open(os.path.join(HERE, "golden", "reservation_filters.json")))["cases"]
+
+
+@pytest.mark.parametrize("case", FILTER_CASES, ids=[c["name"] for c in FILTER_CASES])
+def test_reservation_filter_golden(case):
+    """The oracle's Reservation Filter with a reservation affinity (fitsNode / fitsReservation) against
+    Test_filterWithReservations."""
+    cfg = synth.config(1)
+    o = Oracle(cfg, 1)
+    node = abi.Node()
+    for k in range(abi.NRES):
+        node.allocatable[k] = case["node"]["allocatable"][k]
+        node.raw_allocatable[k] = abi.ABSENT
+        node.requested[k] = case["node"]["requested"][k]
+        node.custom_usage_thresholds[k] = node.custom_prod_usage_thresholds[k] = abi.ABSENT
+        node.custom_agg_thresholds[k] = abi.ABSENT
+    node.cpu_amplification_ratio = -1.0
+    node.nrt_cpu_amplification_ratio = -2.0
+    o.upsert_node(0, node)
+    d = case["reservation"]
+    r = abi.Reservation(node=0, available=1, allocate_policy=d["allocate_policy"])
+    for k in range(abi.NRES):
+        r.allocatable[k], r.allocated[k] = d["allocatable"][k], d["allocated"][k]
+    o.reservations_load([r])
+    pod = synth.make_pods(1, synth.BASE_SEED + 905)
+    pod["requests"][0][:] = 0
+    pod["requests"][0][:2] = case["pod"]
+    pod["reservation_matched"][0] = abi.RSV_AFFINITY
+    assert o.reservation_filter(pod[0], [0], 0) == case["want"]
