@@ -3583,9 +3583,13 @@ static int32_t or_resv_prescore(const or_cluster* c, const ke_pod* pod, const ch
   const int32_t N = c->n;
   int32_t pref = -1;
   int64_t po = 0;
+  char* has = (char*)calloc((size_t)(N > 0 ? N : 1), 1); /* nodes holding a matched reservation */
+  for (int32_t r = 0; r < c->n_resv; r++)
+    if (m[r]) has[c->resv[r].node] = 1;
   for (int32_t i = 0; i < N; i++) {
     nom[i] = -1;
     raw[i] = 0;
+    if (!has[i]) continue;
     int64_t all_alloc[KE_NRES] = {0, 0}, order = 0;
     int any = 0;
     for (int32_t r = 0; r < c->n_resv; r++)
@@ -3623,6 +3627,7 @@ static int32_t or_resv_prescore(const or_cluster* c, const ke_pod* pod, const ch
     }
   }
   if (pref >= 0) raw[pref] = 1000; /* mostPreferredScore */
+  free(has);
   return pref;
 }
 
@@ -3693,9 +3698,14 @@ static int32_t or_resv_eval(or_cluster* c, const ke_pod* pod, int64_t now, eval_
   or_restore(c, NULL, 0);
   uint8_t* feasible = (uint8_t*)malloc((size_t)(N > 0 ? N : 1));
   for (int32_t i = 0; i < N; i++) feasible[i] = o[i].status == KE_CODE_SUCCESS;
-  if (affinity)
+  if (affinity) {
+    char* has = (char*)calloc((size_t)(N > 0 ? N : 1), 1);
+    for (int32_t r = 0; r < c->n_resv; r++)
+      if (m[r]) has[c->resv[r].node] = 1;
     for (int32_t i = 0; i < N; i++)
-      if (feasible[i]) feasible[i] = (uint8_t)or_resv_filter_node(c, pod, m, pr, i);
+      if (feasible[i]) feasible[i] = (uint8_t)(has[i] && or_resv_filter_node(c, pod, m, pr, i));
+    free(has);
+  }
   int64_t* raw = (int64_t*)malloc(sizeof(int64_t) * (size_t)(N > 0 ? N : 1));
   (void)or_resv_prescore(c, pod, m, pr, feasible, affinity, raw, nom);
   int64_t mx = 0;

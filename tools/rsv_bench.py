@@ -1,0 +1,110 @@
+"""Reservation workload: throughput of a queue in which a fraction of the pods match
+reservations (the nominated-reservation path) against the same queue with none matched.
+
+N synthetic nodes (the config-3 generator) hold `--resv-nodes` x N reservations in owner groups of ~25 (Default /
+Aligned / Restricted, AllocateOnce, orders, partly allocated; the reserve pods counted in NodeInfo.Requested);
+`--matched` of the pods match one owner group's reservations.  Each matched pod is a segment of its own in
+ke_schedule (host nomination + k_rsv_pick), every other pod keeps the batched path.  Prints one JSON line:
+evals/s with and without matched pods, the added cost per matched pod, and an oracle-checked prefix.
+Usage: python tools/rsv_bench.py [--nodes 50000] [--pods 12800] [--matched 0.05] ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from koordinator_amd import Evaluator, abi, synth  # noqa: E402
+
+
+def reservations(cl, frac, seed):
+    rng = np.random.default_rng(seed)
+    n = cl.n_nodes
+    nodes = rng.choice(n, int(n * frac), replace=False)
+    rs = []
+    for i in nodes:
+        r = abi.Reservation(node=int(i), available=int(rng.random() < 0.97), allocate_once=int(rng.random() < 0.2),
+                            allocate_policy=int(rng.integers(0, 3)), allocated_pods=int(rng.choice([0, 0, 1])),
+                            order=int(rng.choice([0, 0, 0, 0, 5, 9])))
+        r.allocatable[0] = int(rng.choice([2000, 4000, 8000]))
+        r.allocatable[1] = int(rng.choice([4, 8, 16])) * 2**30
+        if r.allocated_pods:
+            r.allocated[0], r.allocated[1] = r.allocatable[0] // 2, r.allocatable[1] // 4
+        cl.nodes["requested"][i, 0] += r.allocatable[0]
+        cl.nodes["requested"][i, 1] += r.allocatable[1]
+        rs.append(r)
+    return rs
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nodes", type=int, default=50_000)
+    ap.add_argument("--pods", type=int, default=12_800)
+    ap.add_argument("--resv-nodes", type=float, default=0.1)
+    ap.add_argument("--matched", type=float, default=0.05)
+    ap.add_argument("--check", type=int, default=384, help="queue prefix checked against the oracle (0 = none)")
+    a = ap.parse_args()
+    N, P = a.nodes, a.pods
+    cl = synth.make_cluster(N, synth.BASE_SEED + 3)
+    rs = reservations(cl, a.resv_nodes, synth.BASE_SEED + 61)
+    groups = np.arange(len(rs)) // 25
+    pods = synth.make_pods(P, synth.BASE_SEED + 62)
+    rng = np.random.default_rng(synth.BASE_SEED + 63)
+    cpuset = np.isin(pods["qos_class"], [abi.QOS_LSE, abi.QOS_LSR]) & (pods["priority_class"] == abi.PRIORITY_PROD)
+    elig = ((pods["numa_topology_policy"] == 0) & (pods["requests"][:, 2:] == 0).all(1) & (pods["has_other_requests"] == 0)
+            & (pods["device_requests"] == 0).all(1) & ~cpuset)
+    matched_pods = pods.copy()
+    matches = [[] for _ in range(P)]
+    for p in np.flatnonzero(elig & (rng.random(P) < a.matched)):
+        matched_pods["reservation_matched"][p] = abi.RSV_MATCHED
+        matches[p] = np.flatnonzero(groups == rng.integers(0, groups.max() + 1)).tolist()
+    n_matched = int((matched_pods["reservation_matched"] == abi.RSV_MATCHED).sum())
+    cfg = synth.config(N)
+
+    def run(q, m):
+        ev = Evaluator(cfg)
+        synth.load_into(ev, cl)
+        ev.reservations_load(rs)
+        ev.schedule(q[:0], synth.T0)  # rows resident
+        t0 = time.perf_counter()
+        c, s = ev.schedule(q, synth.T0, matches=m)
+        dt = time.perf_counter() - t0
+        into = int((ev.last_allocations()["reservation"] > 0).sum())
+        ev.close()
+        return dt, c, s, into
+
+    warm = Evaluator(cfg)  # kernels loaded, code paths exercised
+    synth.load_into(warm, cl)
+    warm.reservations_load(rs)
+    warm.schedule(matched_pods[:64], synth.T0, matches=matches[:64])
+    warm.close()
+    t_plain, _, _, _ = run(pods, None)
+    t_rsv, c1, s1, into = run(matched_pods, matches)
+    out = {"workload": f"{N} nodes x {P} pods, {len(rs)} reservations, {n_matched} matched pods",
+           "evals_per_s_plain": P * N / t_plain, "evals_per_s_matched": P * N / t_rsv,
+           "s_plain": t_plain, "s_matched": t_rsv,
+           "ms_per_matched_pod": (t_rsv - t_plain) * 1e3 / max(n_matched, 1), "placed_into_reservations": into}
+    if a.check:
+        from oracle.binding import Oracle
+        o = Oracle(cfg, N)
+        synth.load_into(o, cl)
+        o.reservations_load(rs)
+        k = a.check
+        c0, s0 = o.schedule(matched_pods[:k], synth.T0, n_threads=16, matches=matches[:k])
+        ev = Evaluator(cfg)
+        synth.load_into(ev, cl)
+        ev.reservations_load(rs)
+        c2, s2 = ev.schedule(matched_pods[:k], synth.T0, matches=matches[:k])
+        ev.close()
+        out["oracle_prefix"] = {"pods": k, "matched": int((matched_pods["reservation_matched"][:k] == 1).sum()),
+                                "bit_exact": bool(np.array_equal(c0, c2) and np.array_equal(s0, s2))}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
