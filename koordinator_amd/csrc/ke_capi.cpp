@@ -148,6 +148,7 @@ int ke_create(const ke_config* cfg, ke_ctx** out) {
   Context& c = ctx->c;
   c.cfg = *cfg;
   c.nodes.resize((size_t)cfg->node_capacity);
+  for (int32_t i = 0; i < cfg->node_capacity; i++) c.nodes[(size_t)i].dirty.bind(i, &c.dirty_list);
   KArgs& k = c.kargs_template;
   const ke_loadaware_args& a = cfg->loadaware;
   k.exp_s = a.node_metric_expiration_seconds;

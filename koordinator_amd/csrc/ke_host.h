@@ -23,17 +23,29 @@ struct AssignedPod {
 };
 
 // A node's "row must be re-derived" flag.  Setting it bumps a process-wide epoch, so device_refresh can skip its
-// scan over every node when no flag was set since it last cleaned them all (conservative across contexts).
+// scan over every node when no flag was set since it last cleaned them all (conservative across contexts), and
+// a bound flag (its context's nodes) appends its node to the context's dirty list on a clean -> dirty change, so
+// the refresh can visit only those nodes while no row has expired.
 extern std::atomic<uint64_t> g_dirty_epoch;
 struct DirtyFlag {
   bool v = true;
+  int32_t idx = -1;
+  std::vector<int32_t>* list = nullptr;
   DirtyFlag() { g_dirty_epoch.fetch_add(1, std::memory_order_relaxed); }  // a new node starts dirty
   DirtyFlag(const DirtyFlag& o) : v(o.v) { g_dirty_epoch.fetch_add(1, std::memory_order_relaxed); }
   DirtyFlag& operator=(const DirtyFlag& o) { return *this = o.v; }
   DirtyFlag& operator=(bool x) {
+    if (x) {
+      g_dirty_epoch.fetch_add(1, std::memory_order_relaxed);
+      if (!v && list) list->push_back(idx);
+    }
     v = x;
-    if (x) g_dirty_epoch.fetch_add(1, std::memory_order_relaxed);
     return *this;
+  }
+  void bind(int32_t i, std::vector<int32_t>* l) {
+    idx = i;
+    list = l;
+    if (v) l->push_back(i);
   }
   operator bool() const { return v; }
 };
@@ -165,6 +177,8 @@ struct Context {
   // device_refresh: g_dirty_epoch when every row was last clean, and the earliest valid_until then
   uint64_t clean_epoch = UINT64_MAX;
   int64_t min_valid_until = INT64_MIN;
+  int32_t clean_n_nodes = -1;         // n_nodes at that scan
+  std::vector<int32_t> dirty_list;    // nodes that became dirty since (may repeat or be clean again)
   std::vector<std::vector<std::pair<int32_t, int32_t>>> label_sets{{}};
   std::map<std::vector<std::pair<int32_t, int32_t>>, int> label_set_ids{{{}, 0}};
   std::vector<int32_t> model_keys{0};

@@ -5483,14 +5483,19 @@ int device_refresh(Context* ctx, int64_t now) {
   if (rc) return rc;
   rc = ensure_ext(ctx);
   if (rc) return rc;
-  // nothing marked dirty since every row was last clean, and no row expired: no scan over the nodes
-  const bool all_clean = g_dirty_epoch.load(std::memory_order_relaxed) == ctx->clean_epoch && now < ctx->min_valid_until;
-  if (!all_clean && !ctx->pending.empty())  // a row to derive needs the deferred host mirror first
-    for (int32_t i = 0; i < ctx->n_nodes; i++)
-      if (ctx->nodes[i].dirty || now >= ctx->nodes[i].valid_until) {
-        flush_mirror(*ctx);
-        break;
-      }
+  // nothing marked dirty since every row was last clean, and no row expired: no scan over the nodes; no row
+  // expired and the same nodes: only the dirty list (the nodes marked since)
+  const bool no_expiry = now < ctx->min_valid_until && ctx->n_nodes == ctx->clean_n_nodes;
+  const bool all_clean = no_expiry && g_dirty_epoch.load(std::memory_order_relaxed) == ctx->clean_epoch;
+  const bool incremental = !all_clean && no_expiry;
+  if (!all_clean && !ctx->pending.empty()) {  // a row to derive needs the deferred host mirror first
+    bool any = false;
+    if (incremental)
+      for (int32_t i : ctx->dirty_list) any = any || (i < ctx->n_nodes && ctx->nodes[i].dirty);
+    else
+      for (int32_t i = 0; i < ctx->n_nodes && !any; i++) any = ctx->nodes[i].dirty || now >= ctx->nodes[i].valid_until;
+    if (any) flush_mirror(*ctx);
+  }
   if (ctx->ptab_dirty) {  // GPU partition tables (ke_node_gpu_partitions); the pool only grows
     if (d->pt_words < ctx->ptab.size()) {
       if (d->soa.pt) HIP_OK(hipFree(d->soa.pt));
@@ -5513,8 +5518,17 @@ int device_refresh(Context* ctx, int64_t now) {
   std::vector<int32_t> nidx;
   std::vector<int64_t> xrows;  // ext rows of the dirty nodes
   std::vector<int32_t> xidx;
-  int64_t mvu = INT64_MAX;
-  for (int32_t i = 0; i < ctx->n_nodes && !all_clean; i++) {
+  int64_t mvu = incremental ? ctx->min_valid_until : INT64_MAX;
+  std::vector<int32_t> visit;
+  if (incremental) {
+    visit.swap(ctx->dirty_list);  // (flush_mirror above may have appended; rows marked below append anew)
+    std::sort(visit.begin(), visit.end());
+    visit.erase(std::unique(visit.begin(), visit.end()), visit.end());
+  }
+  const int32_t n_visit = all_clean ? 0 : incremental ? (int32_t)visit.size() : ctx->n_nodes;
+  for (int32_t v = 0; v < n_visit; v++) {
+    const int32_t i = incremental ? visit[(size_t)v] : v;
+    if (i >= ctx->n_nodes) continue;
     NodeState& ns = ctx->nodes[i];
     if (!ns.dirty && now < ns.valid_until) {
       mvu = std::min(mvu, ns.valid_until);
@@ -5561,6 +5575,8 @@ int device_refresh(Context* ctx, int64_t now) {
   if (!all_clean) {
     ctx->clean_epoch = g_dirty_epoch.load(std::memory_order_relaxed);
     ctx->min_valid_until = mvu;
+    ctx->clean_n_nodes = ctx->n_nodes;
+    ctx->dirty_list.clear();  // every node < n_nodes is clean now
   }
   if (!dsidx.empty()) {
     const int64_t n = (int64_t)dsidx.size();
