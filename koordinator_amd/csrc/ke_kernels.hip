@@ -5521,9 +5521,7 @@ int device_refresh(Context* ctx, int64_t now) {
   int64_t mvu = incremental ? ctx->min_valid_until : INT64_MAX;
   std::vector<int32_t> visit;
   if (incremental) {
-    visit.swap(ctx->dirty_list);  // (flush_mirror above may have appended; rows marked below append anew)
-    std::sort(visit.begin(), visit.end());
-    visit.erase(std::unique(visit.begin(), visit.end()), visit.end());
+    visit.swap(ctx->dirty_list);  // (flush_mirror above may have appended; a repeated node is clean the 2nd time)
   }
   const int32_t n_visit = all_clean ? 0 : incremental ? (int32_t)visit.size() : ctx->n_nodes;
   for (int32_t v = 0; v < n_visit; v++) {

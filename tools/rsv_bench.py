@@ -89,6 +89,21 @@ def main():
            "evals_per_s_plain": P * N / t_plain, "evals_per_s_matched": P * N / t_rsv,
            "s_plain": t_plain, "s_matched": t_rsv,
            "ms_per_matched_pod": (t_rsv - t_plain) * 1e3 / max(n_matched, 1), "placed_into_reservations": into}
+    # one matched pod per ke_schedule call: the fixed cost of its segment, by host phase
+    ev = Evaluator(cfg)
+    synth.load_into(ev, cl)
+    ev.reservations_load(rs)
+    ev.schedule(pods[:0], synth.T0)
+    one = np.flatnonzero(matched_pods["reservation_matched"] == abi.RSV_MATCHED)[:64]
+    phases = np.zeros(8)
+    t0 = time.perf_counter()
+    for p in one:
+        ev.schedule(matched_pods[p:p + 1], synth.T0, matches=[matches[p]])
+        phases += np.asarray(list(ev.host_stats().values()))
+    out["ms_per_single_matched_call"] = (time.perf_counter() - t0) * 1e3 / len(one)
+    out["single_call_host_ms"] = dict(zip(["checks", "refresh", "upload", "setup", "enqueue", "wait", "stats", "mirror"],
+                                          (phases / len(one)).round(4).tolist()))
+    ev.close()
     if a.check:
         from oracle.binding import Oracle
         o = Oracle(cfg, N)
