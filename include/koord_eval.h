@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define KE_ABI_VERSION 9
+#define KE_ABI_VERSION 10
 #define KE_ABSENT (-1)
 
 typedef struct ke_ctx ke_ctx; /* one evaluator context (ke_create) */
@@ -422,7 +422,7 @@ typedef struct ke_config {
   int32_t pod_batch;      /* B: pods evaluated per speculative batch in ke_schedule      */
   int32_t global_node_offset; /* first global node index held by this shard (multi-GPU)  */
   int32_t weight_reservation; /* profile Score weight of the Reservation plugin (scheduler-config.yaml:91-92:
-                                 5000); scores only pods with matched reservations (ke_pod_reservations) */
+                                 5000), 0 .. 2^20; scores only pods with matched reservations (ke_pod_reservations) */
   ke_ext_args ext;        /* NodeResourcesFitPlus / ScarceResourceAvoidance (all zero = disabled) */
 } ke_config;
 
@@ -615,6 +615,18 @@ int ke_device_available(void);
 /* ---- state ingestion (informer events) ------------------------------------------------------- */
 /* Insert or replace node `node` (0 <= node < node_capacity).  Keeps its NodeMetric / assigned pods. */
 int ke_node_upsert(ke_ctx* ctx, int32_t node, const ke_node* n);
+/* Node informer delete (the scheduler cache's RemoveNode, k8s v1.28.7): the node leaves the snapshot, so no
+ * pod is evaluated against it (ke_eval reports KE_CODE_ERROR for it, ke_schedule never chooses it).  The state of
+ * the other informers stays until their own events remove it — as the scheduler's caches keep it: the NodeMetric
+ * (ke_nodemetric_delete), the podAssignCache (ke_pod_unassign / ke_pod_release), NodeInfo.Requested of pods still
+ * bound there, the NRT topology (ke_node_topology_delete), the device cache (ke_node_devices_delete), the
+ * node's reservations (ke_reservations_load).  ke_node_upsert brings the node back with that state. */
+int ke_node_delete(ke_ctx* ctx, int32_t node);
+/* NodeResourceTopology informer delete (topology_eventhandler.go:82-99 -> TopologyOptionsManager.Delete): the
+ * node's TopologyOptions go away — no NUMA zones, no CPU topology (GetAvailableCPUs then sees no allocated CPUs),
+ * no NRT amplification ratios (nrt_cpu_amplification_ratio -2).  Node fields the caller derived from the NRT
+ * (kubelet topology / CPU manager policies without node labels) are the caller's to re-upsert. */
+int ke_node_topology_delete(ke_ctx* ctx, int32_t node);
 /* Bulk load nodes [0, n): equivalent to n ke_node_upsert calls (initial informer list). */
 int ke_nodes_load(ke_ctx* ctx, int32_t n, const ke_node* nodes);
 int ke_node_set_requested(ke_ctx* ctx, int32_t node, int64_t milli_cpu, int64_t memory);
@@ -671,24 +683,37 @@ int ke_node_devices_delete(ke_ctx* ctx, int32_t node);
  * with ke_node_upsert / ke_node_set_requested (and the cpu / memory rows of ke_node_resources_set) must
  * include the reserve pods' requests, as the scheduler's NodeInfo does.  The restored values feed every
  * plugin that reads NodeInfo: NodeNUMAResource's amplified-cpu Filter and Score, NodeResourcesFitPlus.
- * A pod that matches a reservation (ke_pod.reservation_matched) is refused: its restore, the Reservation
- * plugin's Filter / Score / Reserve and the NUMA / DeviceShare reservation restores are not modelled. */
+ * Pods that match reservations take the nominated-reservation path below (ke_pod_reservations).
+ * What a reservation's reserve pod holds beyond NodeInfo — a NUMA allocation or a cpuset in the resource manager
+ * (nodenumaresource/reservation.go:185-259), device instances in the device cache (deviceshare/reservation.go:
+ * 136-195) — and allocatable names other than cpu / memory are flagged in `holds`; such a reservation is refused
+ * (KE_ERR_UNSUPPORTED from ke_reservations_load) rather than scheduled without its restore. */
 #define KE_RSV_POLICY_DEFAULT 0    /* spec.allocatePolicy "" */
 #define KE_RSV_POLICY_ALIGNED 1    /* Aligned */
 #define KE_RSV_POLICY_RESTRICTED 2 /* Restricted (ResourceNames = the allocatable's names) */
+/* ke_reservation.holds bits */
+#define KE_RSV_HOLDS_NUMA 1u     /* the reserve pod has NUMANodeResources in the resource manager            */
+#define KE_RSV_HOLDS_CPUSET 2u   /* the reserve pod has a CPUSet in the resource manager                     */
+#define KE_RSV_HOLDS_DEVICES 4u  /* the reserve pod has device instances in the DeviceShare device cache     */
+#define KE_RSV_OTHER_ALLOCATABLE 8u /* status.allocatable names a resource other than cpu / memory (pods, GPU,
+                                       scalars): scoreReservation / fitsReservation read them (scoring.go:191-210,
+                                       plugin.go:499-569) */
 typedef struct ke_reservation {
   int32_t node;           /* status.nodeName as a node index                                     */
   uint8_t available;      /* IsAvailable() and no ParseError                                     */
   uint8_t allocate_once;  /* spec.allocateOnce                                                   */
   uint8_t allocate_policy; /* KE_RSV_POLICY_*                                                     */
-  uint8_t pad;
+  uint8_t holds;          /* KE_RSV_HOLDS_* / KE_RSV_OTHER_ALLOCATABLE; any bit -> KE_ERR_UNSUPPORTED */
   int32_t allocated_pods; /* GetAllocatedPods(): owner pods assigned to it                         */
   int32_t pad2;
   int64_t allocatable[KE_NRES]; /* status.allocatable = the reserve pod's requests: MilliCPU, Memory; a zero
                                    quantity is an absent resource name */
   int64_t allocated[KE_NRES];   /* status.allocated: the owner pods' requests                     */
   int64_t order;          /* label scheduling.koordinator.sh/reservation-order parsed (ParseInt), 0 = none */
-} ke_reservation; /* 56 bytes */
+  int64_t uid;            /* the Reservation's UID interned by the caller (release records find it by this; 0 = none) */
+} ke_reservation; /* 64 bytes */
+/* Generation of the loaded reservation set: bumped by every ke_reservations_load. */
+int32_t ke_reservations_generation(ke_ctx* ctx);
 /* Replace the reservation set (n = 0: none).  A pod placed into a reservation (below) updates its
  * allocated / allocated_pods here (ke_reservations_get reads them back). */
 int ke_reservations_load(ke_ctx* ctx, int32_t n, const ke_reservation* reservations);
@@ -724,9 +749,10 @@ int ke_reservations_get(ke_ctx* ctx, int32_t n, ke_reservation* out);
  *  - Reserve (plugin.go:740-793, reservation_info.go:458-468): the nominated reservation of the chosen node
  *    takes Mask(pod requests, names) into allocated and one allocated pod (ke_pod_allocation.reservation); ke_pod_release gives it back (forgetPod,
  *    reservation_info.go:470-482).
- * Refused (KE_ERR_UNSUPPORTED): such a pod with DeviceShare requests, cpuset binding or a NUMA topology
- * policy, a matched reservation on a node with a NUMA topology policy, ke_eval of such a pod, a sharded
- * context.  NodeInfo's pod-count check of fitsNode is not modelled (allowedPodNumber taken as not binding). */
+ * Refused (KE_ERR_UNSUPPORTED, by ke_schedule's argument checks before any pod of the call is scheduled): such a
+ * pod with DeviceShare requests, cpuset binding or a NUMA topology policy, a usable matched reservation on a node
+ * with a NUMA topology policy, a sharded context; ke_eval of such a pod.  NodeInfo's pod-count check of fitsNode
+ * is not modelled (allowedPodNumber taken as not binding). */
 int ke_pod_reservations(ke_ctx* ctx, int32_t n_pods, const int32_t* offsets, const int32_t* ids);
 /* NodeInfo.Requested / NonZeroRequested (MilliCPU, Memory) of `node` as the plugins see it for a pod that
  * matches no reservation (after the restore above and the Reserves of past ke_schedule calls). */
@@ -779,9 +805,15 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
                 int32_t* chosen, int32_t* score);
 
 /* Timing of the last ke_schedule call: device milliseconds of the whole queue, and per-batch
- * latency (pod dequeue -> node selected) in milliseconds, n_batches entries. */
+ * device service time (the batch's eval start -> its Reserve end) in milliseconds, n_batches entries. */
 int ke_last_schedule_stats(ke_ctx* ctx, double* total_ms, int32_t* n_batches,
                            double* batch_ms, int32_t batch_ms_cap);
+/* Per-pod scheduling latency of the last ke_schedule (pod dequeue -> node selected), in
+ * milliseconds: from the ke_schedule call's entry (every pod of the call is dequeued then) to the end of its
+ * batch's Reserve on the device, mapped onto the host clock through the call's device-side stamps aligned at
+ * the host's return from the final stream synchronisation (an upper bound).  Includes the argument checks, row
+ * refresh, pod upload, launch setup and the wait behind earlier batches of the same call. */
+int ke_last_pod_latencies(ke_ctx* ctx, int32_t n, double* ms);
 /* DeviceShare Reserve of the last ke_schedule (AutopilotAllocator.Allocate -> updateCacheUsed,
  * plugin.go:426-492): per pod, bit 16*type + minor set for every device instance allocated. */
 int ke_last_device_allocations(ke_ctx* ctx, int32_t n, uint64_t* minors);
@@ -805,8 +837,11 @@ typedef struct ke_pod_allocation {
   int8_t vf_rank[2][KE_MAX_MINORS];
   int32_t reservation;                  /* 1 + the index of the reservation the pod was assumed into (Reserve),
                                            0 = none */
-  int32_t pad2;
-} ke_pod_allocation; /* 216 bytes */
+  int32_t reservation_generation;       /* ke_reservations_generation() when the record was taken */
+  int64_t reservation_uid;              /* that reservation's uid: a release finds it by uid when non-zero (a
+                                           reservation no longer loaded forgets nothing), else by index, which
+                                           must belong to the current generation (KE_ERR_INVALID otherwise) */
+} ke_pod_allocation; /* 224 bytes */
 /* ke_pod_release modes */
 #define KE_RELEASE_UNRESERVE 0 /* the framework's Unreserve of every Reserve plugin + ForgetPod:
                                   loadaware podAssignCache.unAssign (load_aware.go:197-199),

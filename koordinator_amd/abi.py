@@ -9,7 +9,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 ABSENT = -1
 
 OK = 0
@@ -369,17 +369,19 @@ class PodAllocation(C.Structure):
     """ke_pod_allocation: what one placement reserved (Unreserve / informer-delete record)."""
     _fields_ = [("node", i32), ("quota_assigned", u8), ("pad", u8 * 3), ("cpuset", C.c_uint64 * 4),
                 ("numa", i64 * (MAX_NUMA * NRES)), ("device_minors", C.c_uint64),
-                ("vf_rank", C.c_int8 * (2 * MAX_MINORS)), ("reservation", i32), ("pad2", i32)]
+                ("vf_rank", C.c_int8 * (2 * MAX_MINORS)), ("reservation", i32), ("reservation_generation", i32),
+                ("reservation_uid", i64)]
 
 
 RSV_NONE, RSV_MATCHED, RSV_AFFINITY, RSV_IGNORED = 0, 1, 2, 3  # ke_pod.reservation_matched
 RSV_POLICY_DEFAULT, RSV_POLICY_ALIGNED, RSV_POLICY_RESTRICTED = 0, 1, 2
+RSV_HOLDS_NUMA, RSV_HOLDS_CPUSET, RSV_HOLDS_DEVICES, RSV_OTHER_ALLOCATABLE = 1, 2, 4, 8  # ke_reservation.holds
 
 
 class Reservation(C.Structure):  # ke_reservation
-    _fields_ = [("node", i32), ("available", u8), ("allocate_once", u8), ("allocate_policy", u8), ("pad", u8),
+    _fields_ = [("node", i32), ("available", u8), ("allocate_once", u8), ("allocate_policy", u8), ("holds", u8),
                 ("allocated_pods", i32), ("pad2", i32), ("allocatable", i64 * NRES), ("allocated", i64 * NRES),
-                ("order", i64)]
+                ("order", i64), ("uid", i64)]
 
 
 STRUCTS = [Config, Node, NodeMetric, PodMetric, AggregatedUsage, Pod, ResourceMap, LoadAwareArgs, NumaArgs,
@@ -465,6 +467,10 @@ EXPORTS = {
     "ke_device_available": (C.c_int, []),
     "ke_node_upsert": (C.c_int, [C.c_void_p, i32, C.POINTER(Node)]),
     "ke_nodes_load": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
+    "ke_node_delete": (C.c_int, [C.c_void_p, i32]),
+    "ke_node_topology_delete": (C.c_int, [C.c_void_p, i32]),
+    "ke_reservations_generation": (i32, [C.c_void_p]),
+    "ke_last_pod_latencies": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_node_set_requested": (C.c_int, [C.c_void_p, i32, i64, i64]),
     "ke_node_set_cpuset_allocated": (C.c_int, [C.c_void_p, i32, i64]),
     "ke_nodemetric_upsert": (C.c_int, [C.c_void_p, i32, C.POINTER(NodeMetric), i32, C.c_void_p, i32, C.c_void_p]),

@@ -26,6 +26,7 @@ int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t 
 int device_comm_unique_id(uint8_t* id);
 int device_shard_init(Context* ctx, int rank, int world, const uint8_t* id);
 int device_shard_range(Context* ctx, int* lo, int* hi);
+bool device_sharded(const Context* ctx);
 }  // namespace ke
 
 using namespace ke;
@@ -86,7 +87,8 @@ static int check_cpuset(ke_ctx* ctx, const ke_pod* pods, int32_t n) {
 }
 
 // ke_pod_reservations lists of a ke_schedule call (consumed by it): shape, and the KE_RSV_MATCHED pods the
-// nominated-reservation path supports
+// nominated-reservation path supports.  Every refusal of that path is raised here, before the
+// call schedules any pod: a refusal after earlier segments ran would leave their Reserves applied.
 static int check_matches(Context& c, const ke_pod* pods, int32_t n) {
   const bool staged = !c.match_off.empty();
   if (staged && (int32_t)c.match_off.size() != n + 1) {
@@ -110,6 +112,9 @@ static int check_matches(Context& c, const ke_pod* pods, int32_t n) {
       return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations with device, cpuset or scalar requests");
     if (pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE || (c.n_bind_nodes > 0 && pods[p].requests[KE_RES_CPU] > 0))
       return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations with a NUMA policy or that may bind CPUs");
+    if (c.dev && device_sharded(&c)) return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations in a sharded context");
+    const int rc = resv_check(c, c.match_ids.data() + c.match_off[(size_t)p], cnt);
+    if (rc) return rc;
   }
   return KE_OK;
 }
@@ -253,12 +258,41 @@ int ke_node_upsert(ke_ctx* ctx, int32_t node, const ke_node* n) {
     ctx->c.n_policy_nodes -= ns.node.numa_topology_policy != KE_NUMA_POLICY_NONE;
   }
   ns.valid = true;
+  ns.known = true;
   ns.node = *n;
   ns.dirty = true;
   ctx->c.n_bind_nodes += n->cpu_bind_policy != KE_NODE_CPU_BIND_NONE;
   ctx->c.n_policy_nodes += n->numa_topology_policy != KE_NUMA_POLICY_NONE;
   if (n->numa_topology_policy != KE_NUMA_POLICY_NONE) ctx->c.numa_enabled = true;
   ctx->c.n_nodes = std::max(ctx->c.n_nodes, node + 1);
+  return KE_OK;
+}
+
+int ke_node_delete(ke_ctx* ctx, int32_t node) {
+  int rc = check_node(ctx, node);
+  if (ctx) flush_mirror(ctx->c);  // pending Reserves on it first: the object state stays (koord_eval.h)
+  if (rc) return rc;
+  NodeState& ns = ctx->c.nodes[node];
+  if (!ns.valid) return KE_OK;
+  ctx->c.n_bind_nodes -= ns.node.cpu_bind_policy != KE_NODE_CPU_BIND_NONE;
+  ctx->c.n_policy_nodes -= ns.node.numa_topology_policy != KE_NUMA_POLICY_NONE;
+  ns.valid = false;  // derive_row: no NF_VALID -> every Filter path fails the node
+  ns.dirty = true;
+  return KE_OK;
+}
+
+int ke_node_topology_delete(ke_ctx* ctx, int32_t node) {
+  int rc = check_node(ctx, node);
+  if (ctx) flush_mirror(ctx->c);
+  if (rc) return rc;
+  NodeState& ns = ctx->c.nodes[node];
+  ns.zones.clear();
+  ns.cpus.clear();
+  ns.cpu_max_ref = 1;
+  ns.node.cpuset_allocated_cpus = 0;        // GetAvailableCPUs without a CPU topology: no allocated CPUs
+  ns.node.nrt_cpu_amplification_ratio = -2;  // no NRT ratio map
+  ns.node.cpu_topology_invalid = 0;
+  ns.dirty = true;
   return KE_OK;
 }
 
@@ -323,6 +357,8 @@ int ke_reservations_load(ke_ctx* ctx, int32_t n, const ke_reservation* reservati
   flush_mirror(ctx->c);
   return load_reservations(ctx->c, n, reservations);
 }
+
+int32_t ke_reservations_generation(ke_ctx* ctx) { return ctx ? ctx->c.resv_gen : 0; }
 
 int ke_reservations_get(ke_ctx* ctx, int32_t n, ke_reservation* out) {
   if (!ctx || n < 0 || (n > 0 && !out) || n > (int32_t)ctx->c.resv.size()) return fail(KE_ERR_INVALID, "ke_reservations_get arguments");
@@ -606,6 +642,7 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
   if (!ctx || (n_pods > 0 && !chosen)) return fail(KE_ERR_INVALID, "ke_schedule arguments");
   using clk = std::chrono::steady_clock;
   auto tp = clk::now();
+  ctx->c.call_entry = tp;  // every pod of the call is dequeued now (ke_last_pod_latencies)
   int rc = check_pods(pods, n_pods, &ctx->c, true);
   if (rc) return rc;
   rc = check_numa_deviceshare(ctx, pods, n_pods);
@@ -634,7 +671,7 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
   std::vector<uint64_t> all_dev, all_cs;
   std::vector<int8_t> all_vf;
   std::vector<int64_t> all_numa;
-  std::vector<double> all_batch_ms;
+  std::vector<double> all_batch_ms, all_lat;
   double all_ms = 0;
   bool numa_out = false, multi = false;
   const int32_t off = c.cfg.global_node_offset;
@@ -659,15 +696,23 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
                         pods[s0].reservation_matched == KE_RSV_AFFINITY);
       if (rc) return rc;
     }
+    // a device failure leaves the pods of earlier segments Reserved on the device and the context's state
+    // undefined (KE_ERR_DEVICE: rebuild the context); the matched-restore state is still undone so the
+    // reservation's capacity does not stay visible to later calls
+    auto undo_rsv = [&]() {
+      int32_t dummy = 0;
+      if (rsv) resv_finish(c, -1, pods[s0], &dummy);
+    };
     rc = device_schedule(&c, len, pods + s0, now_ns, chosen + (n_pods ? s0 : 0), score ? score + s0 : nullptr);
-    if (rc) return rc;
+    if (rc) return undo_rsv(), rc;
     if (rsv) {
       const int32_t local = chosen[s0] < 0 ? -1 : chosen[s0] - off;
       int32_t pick[4] = {local, 0, 0, -1};  // no usable matched reservation: no Reservation score
       if (!c.rsv_pairs.empty() || c.rsv_affinity) rc = device_rsv_result(&c, pick);
-      if (rc) return rc;
-      if (local >= 0 && local != pick[0]) return fail(KE_ERR_DEVICE, "k_rsv_pick winner differs from the placement");
-      if (local >= 0 && score) score[s0] += (int32_t)c.cfg.weight_reservation * pick[1];
+      if (rc) return undo_rsv(), rc;
+      if (local >= 0 && local != pick[0])
+        return undo_rsv(), fail(KE_ERR_DEVICE, "k_rsv_pick winner differs from the placement");
+      if (local >= 0 && score) score[s0] = (int32_t)((int64_t)score[s0] + c.cfg.weight_reservation * (int64_t)pick[1]);
       resv_finish(c, local, pods[s0], &assumed[(size_t)s0]);
     }
     if (n_pods == 0) break;
@@ -706,6 +751,7 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
       if (c.last_numa_alloc.empty()) all_numa.resize(all_numa.size() + (size_t)len * KE_MAX_NUMA * KE_NRES, 0);
       else all_numa.insert(all_numa.end(), c.last_numa_alloc.begin(), c.last_numa_alloc.end());
       all_batch_ms.insert(all_batch_ms.end(), c.last_batch_ms.begin(), c.last_batch_ms.end());
+      all_lat.insert(all_lat.end(), c.last_pod_lat.begin(), c.last_pod_lat.end());
       all_ms += c.last_total_ms;
     }
     // the placed system / default pod (also when it ends the only segment): refresh the runtime
@@ -730,6 +776,7 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
     if (numa_out) c.last_numa_alloc.swap(all_numa);
     else c.last_numa_alloc.clear();
     c.last_batch_ms.swap(all_batch_ms);
+    c.last_pod_lat.swap(all_lat);
     c.last_total_ms = all_ms;
   }
   // release records of this call (ke_last_allocations / ke_unreserve)
@@ -751,6 +798,8 @@ static ke_pod_allocation last_allocation(const Context& c, int32_t p) {
   a.node = p < (int32_t)c.last_chosen.size() ? c.last_chosen[(size_t)p] : -1;
   if (a.node < 0) return a;
   a.reservation = p < (int32_t)c.last_resv.size() ? c.last_resv[(size_t)p] : 0;
+  a.reservation_generation = c.resv_gen;
+  a.reservation_uid = a.reservation > 0 ? c.resv[(size_t)a.reservation - 1].uid : 0;
   a.quota_assigned = c.last_quota[(size_t)p];
   constexpr int W = KE_MAX_NUMA * KE_NRES;
   for (int q = 0; q < 4; q++)
@@ -783,11 +832,23 @@ int ke_pod_release(ke_ctx* ctx, const ke_pod* pod, const ke_pod_allocation* allo
     return fail(KE_ERR_INVALID, "ke_pod.quota outside the loaded ElasticQuota tree");
   const int32_t node = alloc->node < 0 ? -1 : alloc->node - c.cfg.global_node_offset;
   if (node >= c.cfg.node_capacity) return fail(KE_ERR_NOT_FOUND, "ke_pod_release: node index out of range");
-  if (alloc->reservation < 0 || alloc->reservation > (int32_t)c.resv.size())
+  // the reservation the pod was assumed into: by uid (the set may have been reloaded since), else by an index of
+  // the current set
+  int32_t ridx = -1;
+  if (alloc->reservation > 0 && alloc->reservation_uid != 0) {
+    for (size_t i = 0; i < c.resv.size() && ridx < 0; i++)
+      if (c.resv[i].uid == alloc->reservation_uid) ridx = (int32_t)i;
+  } else if (alloc->reservation > 0) {
+    if (alloc->reservation > (int32_t)c.resv.size()) return fail(KE_ERR_NOT_FOUND, "ke_pod_release: reservation index");
+    if (alloc->reservation_generation != c.resv_gen)
+      return fail(KE_ERR_INVALID, "ke_pod_release: a reservation index of an earlier reservation set (no uid)");
+    ridx = alloc->reservation - 1;
+  } else if (alloc->reservation < 0) {
     return fail(KE_ERR_NOT_FOUND, "ke_pod_release: reservation index");
-  if (node >= 0 && c.nodes[(size_t)node].valid)  // (a node of another context's range: only the quota part)
+  }
+  if (node >= 0 && c.nodes[(size_t)node].known)  // (also a deleted node: its caches keep the pod until released)
     host_release_node(c.cfg, c.ext_enabled, c.nodes[(size_t)node], *pod, *alloc, pod_hints(c, *pod));
-  if (node >= 0 && alloc->reservation > 0) resv_forget(c, alloc->reservation - 1, *pod);
+  if (node >= 0 && ridx >= 0) resv_forget(c, ridx, *pod);
   const bool assigned = alloc->node >= 0 && alloc->quota_assigned;
   if (pod->quota > 0 && (assigned || mode == KE_RELEASE_DELETE)) {
     if (c.dev) {
@@ -811,6 +872,13 @@ int ke_unreserve(ke_ctx* ctx, const ke_pod* pod, int32_t queue_pos) {
   const int rc = ke_pod_release(ctx, pod, &a, KE_RELEASE_UNRESERVE);
   if (rc) return rc;
   c.last_chosen[(size_t)queue_pos] = -1;
+  return KE_OK;
+}
+
+int ke_last_pod_latencies(ke_ctx* ctx, int32_t n, double* ms) {
+  if (!ctx || n < 0 || (n > 0 && !ms)) return fail(KE_ERR_INVALID, "ke_last_pod_latencies arguments");
+  const auto& v = ctx->c.last_pod_lat;
+  for (int32_t i = 0; i < n; i++) ms[i] = i < (int32_t)v.size() ? v[(size_t)i] : 0.0;
   return KE_OK;
 }
 

@@ -40,6 +40,7 @@ int validate_config(const ke_config& cfg) {
   if (cfg.pod_batch < 1 || cfg.pod_batch > MAX_BATCH) return fail(KE_ERR_INVALID, "pod_batch out of range (1..64)");
   const ke_ext_args& x = cfg.ext;
   if (cfg.weight_reservation < 0) return fail(KE_ERR_INVALID, "negative Reservation weight");
+  if (cfg.weight_reservation > (1 << 20)) return fail(KE_ERR_UNSUPPORTED, "Reservation weight above 2^20");
   if (cfg.weight_loadaware < 0 || cfg.weight_numa < 0 || cfg.weight_deviceshare < 0 || x.weight_fitplus < 0 ||
       x.weight_sra < 0 ||
       (cfg.weight_loadaware + cfg.weight_numa + cfg.weight_deviceshare + x.weight_fitplus + x.weight_sra) * 100 >
@@ -556,6 +557,15 @@ int load_reservations(Context& c, int32_t n, const ke_reservation* rs) {
     if (r.allocate_policy > KE_RSV_POLICY_RESTRICTED) return fail(KE_ERR_INVALID, "reservation allocate policy");
     for (int k = 0; k < KE_NRES; k++)
       if (r.allocatable[k] < 0 || r.allocated[k] < 0) return fail(KE_ERR_INVALID, "negative reservation quantity");
+    // what the restore of such a reservation needs is not carried by ke_reservation: refuse rather than
+    // schedule every pod on its node without the NUMA / cpuset / device restore (koord_eval.h)
+    if (r.holds & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET))
+      return fail(KE_ERR_UNSUPPORTED, "a reservation holding a NUMA allocation or a cpuset (nodenumaresource/reservation.go)");
+    if (r.holds & KE_RSV_HOLDS_DEVICES)
+      return fail(KE_ERR_UNSUPPORTED, "a reservation holding device instances (deviceshare/reservation.go)");
+    if (r.holds & KE_RSV_OTHER_ALLOCATABLE)
+      return fail(KE_ERR_UNSUPPORTED, "a reservation whose allocatable names resources other than cpu / memory");
+    if (r.holds & ~15u) return fail(KE_ERR_INVALID, "unknown ke_reservation.holds bits");
   }
   std::vector<int32_t> old;
   for (const ke_reservation& r : c.resv) old.push_back(r.node);
@@ -565,6 +575,7 @@ int load_reservations(Context& c, int32_t n, const ke_reservation* rs) {
   for (int32_t node : old) resv_node_restore(c, node);  // the old restore leaves
   for (const ke_reservation& r : c.resv) resv_node_restore(c, r.node);
   c.last_resv.clear();  // release records of earlier calls no longer name these reservations
+  c.resv_gen++;
   return KE_OK;
 }
 
@@ -608,23 +619,30 @@ int32_t resv_score(const ke_reservation& r, const ke_pod& pod) {
   return w ? (int32_t)(s / w) : 0;
 }
 
+int resv_check(const Context& c, const int32_t* ids, int32_t n_ids) {
+  for (int32_t j = 0; j < n_ids; j++) {
+    if (ids[j] < 0 || ids[j] >= (int32_t)c.resv.size()) return fail(KE_ERR_NOT_FOUND, "matched reservation index");
+    const ke_reservation& r = c.resv[(size_t)ids[j]];
+    if (resv_usable(r) && c.nodes[(size_t)r.node].node.numa_topology_policy != KE_NUMA_POLICY_NONE)
+      return fail(KE_ERR_UNSUPPORTED, "a matched reservation on a node with a NUMA topology policy");
+  }
+  return KE_OK;
+}
+
 int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids, bool affinity) {
+  int rc = resv_check(c, ids, n_ids);  // (ke_schedule's argument checks ran it already: nothing below fails)
+  if (rc) return rc;
   c.rsv_affinity = affinity;
   c.rsv_pairs.clear();
   c.rsv_nominated.clear();
   c.rsv_nodes.clear();
   std::vector<char> m(c.resv.size(), 0);
-  for (int32_t j = 0; j < n_ids; j++) {
-    if (ids[j] < 0 || ids[j] >= (int32_t)c.resv.size()) return fail(KE_ERR_NOT_FOUND, "matched reservation index");
+  for (int32_t j = 0; j < n_ids; j++)
     if (resv_usable(c.resv[(size_t)ids[j]])) m[(size_t)ids[j]] = 1;
-  }
   for (int32_t j = 0; j < n_ids; j++)
     if (m[(size_t)ids[j]]) c.rsv_nodes.push_back(c.resv[(size_t)ids[j]].node);
   std::sort(c.rsv_nodes.begin(), c.rsv_nodes.end());
   c.rsv_nodes.erase(std::unique(c.rsv_nodes.begin(), c.rsv_nodes.end()), c.rsv_nodes.end());
-  for (int32_t node : c.rsv_nodes)
-    if (c.nodes[(size_t)node].node.numa_topology_policy != KE_NUMA_POLICY_NONE)
-      return fail(KE_ERR_UNSUPPORTED, "a matched reservation on a node with a NUMA topology policy");
   flush_mirror(c);  // NodeInfo.Requested with every earlier placement
   for (int32_t node : c.rsv_nodes) {
     NodeState& ns = c.nodes[(size_t)node];

@@ -2,6 +2,7 @@
 // its listers, podAssignCache and NodeInfo snapshot) and its folding into GPU rows.
 #pragma once
 #include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <map>
 #include <string>
@@ -32,7 +33,9 @@ struct DirtyFlag {
   int32_t idx = -1;
   std::vector<int32_t>* list = nullptr;
   DirtyFlag() { g_dirty_epoch.fetch_add(1, std::memory_order_relaxed); }  // a new node starts dirty
-  DirtyFlag(const DirtyFlag& o) : v(o.v) { g_dirty_epoch.fetch_add(1, std::memory_order_relaxed); }
+  // a copy keeps the binding: Context::nodes elements moved by a reallocation still feed their context's dirty
+  // list under the same node index (a stray copy pushing its index only costs the refresh one more visit)
+  DirtyFlag(const DirtyFlag& o) : v(o.v), idx(o.idx), list(o.list) { g_dirty_epoch.fetch_add(1, std::memory_order_relaxed); }
   DirtyFlag& operator=(const DirtyFlag& o) { return *this = o.v; }
   DirtyFlag& operator=(bool x) {
     if (x) {
@@ -59,7 +62,8 @@ struct RsvPair {
 };
 
 struct NodeState {
-  bool valid = false;
+  bool valid = false;  // in the snapshot (ke_node_upsert .. ke_node_delete)
+  bool known = false;  // upserted at least once: the object state below belongs to a node
   ke_node node{};
   bool has_metric = false;
   ke_node_metric nm{};
@@ -174,6 +178,11 @@ struct Context {
   std::vector<int32_t> rsv_nominated;
   bool rsv_affinity = false;  // the segment's pod has a required reservation affinity
   std::vector<int32_t> last_resv;  // per pod of the last ke_schedule: 1 + the reservation assumed, 0 = none
+  int32_t resv_gen = 0;            // ke_reservations_generation: bumped by every load_reservations
+  // per-pod latency of the last ke_schedule (ke_last_pod_latencies): the call's entry on the host clock, and
+  // per pod the ms from it to its batch's Reserve end
+  std::chrono::steady_clock::time_point call_entry{};
+  std::vector<double> last_pod_lat;
   // device_refresh: g_dirty_epoch when every row was last clean, and the earliest valid_until then
   uint64_t clean_epoch = UINT64_MAX;
   int64_t min_valid_until = INT64_MIN;
@@ -264,6 +273,8 @@ int32_t resv_score(const ke_reservation& r, const ke_pod& pod);
 // the nominated-reservation path of one KE_RSV_MATCHED pod: rows with its matched restore, rsv_pairs /
 // rsv_nominated; resv_finish assumes the pod into the chosen node's nominated reservation (1 + index, 0)
 int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids, bool affinity);
+// the refusals of resv_prepare, checked for every pod before a ke_schedule call schedules any
+int resv_check(const Context& c, const int32_t* ids, int32_t n_ids);
 void resv_finish(Context& c, int32_t chosen_local, const ke_pod& pod, int32_t* assumed);
 void resv_forget(Context& c, int32_t idx, const ke_pod& pod);
 // NodeResourcesFitPlus' (NonZero)Requested of resource `id` on the node, with the reservation restore

@@ -5363,6 +5363,8 @@ int device_shard_init(Context* ctx, int rank, int world, const uint8_t* id) {
   return KE_OK;
 }
 
+bool device_sharded(const Context* ctx) { return ctx->dev && (ctx->dev->world > 1 || ctx->dev->comm); }
+
 int device_shard_range(Context* ctx, int* lo, int* hi) {
   DeviceState* d = ctx->dev;
   shard_range(ctx->n_nodes, d->rank, d->world, lo, hi);
@@ -5780,6 +5782,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   ctx->last_batch_ms.clear();
   ctx->last_dev_alloc.clear();
   ctx->last_total_ms = 0;
+  ctx->last_pod_lat.clear();
   if (n_pods == 0) return KE_OK;
   tp = clk::now();
   rc = upload_pods(ctx, n_pods, pods);
@@ -6176,6 +6179,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   ctx->pending_pods.insert(ctx->pending_pods.end(), pods, pods + n_pods);
   HIP_OK(hipStreamSynchronize(d->stream));
   HIP_OK(hipStreamSynchronize(d->estream));
+  const auto t_sync = clk::now();
   ctx->host_ms[5] = ms_since(tp);
   tp = clk::now();
   if (herr) {
@@ -6201,11 +6205,24 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   // s_memrealtime ticks -> ms, calibrated against the event-timed span of the whole queue
   const double span = (double)(st[n_batches] - st[0]);
   const double ms_per_tick = span > 0 ? ms / span : 1e-5;
-  // a pod's latency: from its batch's eval start (dequeue) to the end of its batch's Reserve
+  // a batch's device service time: from its eval start to the end of its Reserve
   ctx->last_batch_ms.resize(n_batches);
   for (int b = 0; b < n_batches; b++) {
     const uint64_t t0 = std::max(std::min(est[b], st[b + 1]), st[0]);
     ctx->last_batch_ms[b] = (double)(st[b + 1] - t0) * ms_per_tick;
+  }
+  // a pod's latency: from the ke_schedule call's entry (its dequeue) to its batch's Reserve end,
+  // the device stamps placed on the host clock by aligning the last one with the return of the final
+  // synchronisation (later than the true end: an upper bound)
+  {
+    const double sync_ms = std::chrono::duration<double, std::milli>(t_sync - ctx->call_entry).count();
+    ctx->last_pod_lat.resize((size_t)n_pods);
+    for (int b = 0, p0 = 0; b < n_batches; b++) {  // (a DeviceShare batch cut and re-run covers its first part too)
+      const double lat = sync_ms - (double)(st[n_batches] - st[b + 1]) * ms_per_tick;
+      const int p1 = bases[b] + batches[b].pods;
+      for (int p = p0; p < p1; p++) ctx->last_pod_lat[(size_t)p] = lat;
+      p0 = p1;
+    }
   }
   double pro = 0, loop = 0;  // resolve kernel: prologue (candidate/row staging) vs sequential replay
   double ph[6] = {0, 0, 0, 0, 0, 0};  // init, cand copy, hash insert, slot lookup, row gather, replay

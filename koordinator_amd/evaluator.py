@@ -101,6 +101,14 @@ class Evaluator:
     def delete_nodemetric(self, i):
         self._check(self.lib.ke_nodemetric_delete(self.h, i))
 
+    def delete_node(self, i):
+        """Node informer delete (ke_node_delete): out of the snapshot, other caches kept."""
+        self._check(self.lib.ke_node_delete(self.h, i))
+
+    def delete_topology(self, i):
+        """NodeResourceTopology delete (ke_node_topology_delete)."""
+        self._check(self.lib.ke_node_topology_delete(self.h, i))
+
     def assign(self, i, pod, timestamp_ns):
         self._check(self.lib.ke_pod_assign(self.h, i, C.byref(pod), int(timestamp_ns)))
 
@@ -282,6 +290,12 @@ class Evaluator:
         per = np.zeros(max(nb.value, 1), np.float64)
         self._check(self.lib.ke_last_schedule_stats(self.h, None, None, abi.ptr(per), len(per)))
         return total.value, per[: nb.value]
+
+    def pod_latencies(self, n):
+        """per-pod latency (ms, ke_last_pod_latencies) of the n pods of the last schedule()"""
+        out = np.zeros(n, np.float64)
+        self._check(self.lib.ke_last_pod_latencies(self.h, n, abi.ptr(out)))
+        return out
 
     def set_profiling(self, sample_every):
         self._check(self.lib.ke_set_profiling(self.h, sample_every))

@@ -50,6 +50,8 @@ def load():
         "or_schedule": (C.c_int, [V, i32, V, i64, V, V, V, V, V, C.c_int]),
         "or_node_devices_set": (C.c_int, [V, i32, i32, V]),
         "or_node_devices_delete": (C.c_int, [V, i32]),
+        "or_node_delete": (C.c_int, [V, i32]),
+        "or_node_topology_delete": (C.c_int, [V, i32]),
         "or_node_gpu_partitions": (C.c_int, [V, i32, i32, i32, i32, V]),
         "or_ds_prefilter": (C.c_int, [V, C.POINTER(abi.Pod), C.POINTER(C.c_int), V, V, V]),
         "or_set_pod_device_hints": (C.c_int, [V, i32, V]),
@@ -184,6 +186,12 @@ class Oracle:
     def delete_devices(self, i):
         assert self.lib.or_node_devices_delete(self.h, i) == 0
 
+    def delete_node(self, i):
+        assert self.lib.or_node_delete(self.h, i) == 0
+
+    def delete_topology(self, i):
+        assert self.lib.or_node_topology_delete(self.h, i) == 0
+
     def set_resources(self, i, resources):
         res = np.ascontiguousarray(resources, dtype=abi.NODE_RESOURCE_DTYPE)
         assert self.lib.or_node_resources_set(self.h, i, len(res), abi.ptr(res)) == 0
@@ -266,7 +274,9 @@ class Oracle:
 
     def reservations_load(self, reservations):
         r = abi.struct_array(reservations, abi.Reservation)
-        assert self.lib.or_reservations_load(self.h, len(r), abi.ptr(r)) == 0
+        rc = self.lib.or_reservations_load(self.h, len(r), abi.ptr(r))
+        if rc != 0:
+            raise RuntimeError(f"oracle reservations_load rc={rc}")
         self._n_resv = len(r)
 
     def reservations_get(self):
@@ -409,6 +419,8 @@ class Oracle:
         rv = np.zeros(len(chosen), np.int32)
         self.lib.or_last_reservations(self.h, len(chosen), abi.ptr(rv))
         out["reservation"] = np.where(placed, rv[:n], 0)
+        uids = self.reservations_get()["uid"]
+        out["reservation_uid"] = [uids[r - 1] if r > 0 else 0 for r in out["reservation"]]
         return out
 
     def node_state(self, i):

@@ -68,6 +68,7 @@ typedef struct or_node {
   ke_node_resource xres[KE_MAX_XRES];
   /* the reservation cache's NodeInfo restore for a pod that matches no reservation (or_reservations_load) */
   int64_t rv_req[KE_NRES], rv_nz[KE_NRES];
+  int deleted; /* Node informer delete: out of the snapshot (every other cache keeps its state) */
 } or_node;
 
 /* TopologyOptions.CPUTopology / ReservedCPUs / MaxRefCount + NodeAllocation.allocatedCPUs */
@@ -2928,8 +2929,10 @@ static void or_restore(or_cluster* c, const char* matched, int with_matched) {
   }
 }
 int or_reservations_load(or_cluster* c, int32_t n, const ke_reservation* rs) {
-  for (int32_t i = 0; i < n; i++)
+  for (int32_t i = 0; i < n; i++) {
     if (rs[i].node < 0 || rs[i].node >= c->n) return KE_ERR_NOT_FOUND;
+    if (rs[i].holds) return KE_ERR_UNSUPPORTED; /* NUMA / cpuset / device holdings: not restated */
+  }
   free(c->resv);
   c->resv = (ke_reservation*)malloc(sizeof(ke_reservation) * (size_t)(n > 0 ? n : 1));
   if (n > 0) memcpy(c->resv, rs, sizeof(ke_reservation) * (size_t)n);
@@ -3324,6 +3327,29 @@ int or_node_gpu_partitions(or_cluster* c, int32_t node, int32_t has_table, int32
 int or_node_upsert(or_cluster* c, int32_t node, const ke_node* n) {
   if (node < 0 || node >= c->n) return KE_ERR_NOT_FOUND;
   c->nodes[node].node = *n;
+  c->nodes[node].deleted = 0;
+  return KE_OK;
+}
+
+/* Node informer delete: the scheduler cache's RemoveNode leaves the NodeInfo out of the snapshot (k8s v1.28.7);
+ * NodeMetric, podAssignCache, resource manager, device cache and reservation cache keep their entries */
+int or_node_delete(or_cluster* c, int32_t node) {
+  if (node < 0 || node >= c->n) return KE_ERR_NOT_FOUND;
+  c->nodes[node].deleted = 1;
+  return KE_OK;
+}
+
+/* NodeResourceTopology delete (topology_eventhandler.go:82-99): TopologyOptions gone -- no NUMA node resources,
+ * no CPU topology (GetAvailableCPUs: nothing allocated), no NRT amplification ratios */
+int or_node_topology_delete(or_cluster* c, int32_t node) {
+  if (node < 0 || node >= c->n) return KE_ERR_NOT_FOUND;
+  or_node* nd = &c->nodes[node];
+  nd->n_zone = 0;
+  free(nd->cpus);
+  nd->cpus = NULL;
+  nd->node.cpuset_allocated_cpus = 0;
+  nd->node.nrt_cpu_amplification_ratio = -2;
+  nd->node.cpu_topology_invalid = 0;
   return KE_OK;
 }
 
@@ -3438,6 +3464,13 @@ typedef struct eval_out {
 static void eval_pair(const or_cluster* c, const ke_pod* pod, int32_t node, int64_t now, eval_out* o) {
   int reason = 0;
   int code = KE_CODE_SUCCESS;
+  if (c->nodes[node].deleted) { /* not in the snapshot: evaluated nowhere (KE_CODE_ERROR, as the product) */
+    o->status = KE_CODE_ERROR;
+    o->reason = 0;
+    o->la = o->numa = o->ds = o->fp = o->sra = 0;
+    o->total = -1;
+    return;
+  }
   /* PreFilter failures fail the pod on every node before any Filter runs (profile order
    * NodeNUMAResource, DeviceShare): a cpuset pod with a non-integer cpu request, invalid device requests */
   cpuset_state st;
@@ -3877,11 +3910,18 @@ int or_last_reservations(const or_cluster* c, int32_t n, int32_t* out) {
 int or_pod_release(or_cluster* c, const ke_pod* pod, const ke_pod_allocation* a, int32_t mode) {
   const int32_t node = a->node;
   if (node >= c->n) return KE_ERR_NOT_FOUND;
-  if (a->reservation < 0 || a->reservation > c->n_resv) return KE_ERR_NOT_FOUND;
-  if (node >= 0 && a->reservation > 0) {
+  int32_t ridx = -1; /* the reservation the pod was assumed into: by uid when the record has one */
+  if (a->reservation > 0 && a->reservation_uid != 0) {
+    for (int32_t i = 0; i < c->n_resv && ridx < 0; i++)
+      if (c->resv[i].uid == a->reservation_uid) ridx = i;
+  } else if (a->reservation != 0) {
+    if (a->reservation < 0 || a->reservation > c->n_resv) return KE_ERR_NOT_FOUND;
+    ridx = a->reservation - 1;
+  }
+  if (node >= 0 && ridx >= 0) {
     /* reservation forgetPod -> RemoveAssignedPod (reservation/plugin.go:815-819, reservation_info.go:470-482):
      * allocated = SubtractWithNonNegativeResult(allocated, Mask(requests, ResourceNames)) */
-    ke_reservation* r = &c->resv[a->reservation - 1];
+    ke_reservation* r = &c->resv[ridx];
     for (int k = 0; k < KE_NRES; k++)
       if (r->allocatable[k] != 0) r->allocated[k] = r->allocated[k] - pod->requests[k] > 0 ? r->allocated[k] - pod->requests[k] : 0;
     if (r->allocated_pods > 0) r->allocated_pods--;

@@ -23,6 +23,8 @@ typedef struct or_cluster or_cluster;
 or_cluster* or_create(const ke_config* cfg, int32_t n_nodes);
 void or_destroy(or_cluster* c);
 int or_node_upsert(or_cluster* c, int32_t node, const ke_node* n);
+int or_node_delete(or_cluster* c, int32_t node);          /* Node informer delete (ke_node_delete) */
+int or_node_topology_delete(or_cluster* c, int32_t node); /* NRT delete (ke_node_topology_delete) */
 int or_node_set_requested(or_cluster* c, int32_t node, int64_t milli_cpu, int64_t memory);
 int or_node_set_cpuset_allocated(or_cluster* c, int32_t node, int64_t cpus);
 int or_nodemetric_upsert(or_cluster* c, int32_t node, const ke_node_metric* nm, int32_t n_pm,

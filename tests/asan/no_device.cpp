@@ -23,4 +23,5 @@ int device_bench_eval(Context*, int32_t, const ke_pod*, int64_t, int32_t, double
 int device_comm_unique_id(uint8_t*) { return none(); }
 int device_shard_init(Context*, int, int, const uint8_t*) { return none(); }
 int device_shard_range(Context*, int*, int*) { return none(); }
+bool device_sharded(const Context*) { return false; }
 }  // namespace ke
