@@ -301,7 +301,8 @@ def main():
     kagg = {"eval_ms": sum(evm) / max(samples, 1), "select_ms": sum(sel) / max(samples, 1),
             "fixup_ms": mean("fixup_ms"), "resolve_ms": mean("resolve_ms"), "handoff_ms": mean("handoff_ms"),
             "rows_fetched": mean("rows_fetched"), "rows_changed": mean("rows_changed"),
-            "spec_failed": mean("spec_failed_rounds")}
+            "spec_failed": mean("spec_failed_rounds"),
+            "resolve_phases": {k: float(np.mean([x["resolve_phases_ms"][k] for x in kss])) for k in kss[0]["resolve_phases_ms"]}}
     tag = f"config{a.config}_nodes{hi - lo}_batch{a.batch}_world{world}" + ("" if not a.no_pipeline else "_serial")
     out = {
         "metric": "pod-node Filter+Score evals/sec + p99 per-pod sched latency @50k nodes",
@@ -336,6 +337,7 @@ def main():
                       "pipelined_batches": npipe, "batches": n_batches, "event_samples": samples,
                       "records_fetched_per_batch": kagg["rows_fetched"], "rows_changed_per_batch": kagg["rows_changed"],
                       "spec_failed_rounds_per_batch": kagg["spec_failed"],
+                      "resolve_phases": kagg["resolve_phases"],
                       "note": "per batch; 'select' includes the all-gather + merge when sharded"},
         "host_ms_per_step": {k: float(np.mean([h[k] for h in hs])) for k in hs[0]} if hs else None,
         "roofline": roofline(hi - lo, a.batch, kagg, dt / K, n_batches / K, not a.no_pipeline, tag),

@@ -92,6 +92,13 @@ typedef struct ke_ctx ke_ctx; /* one evaluator context (ke_create) */
 #define KE_REASON_DS_INSUFFICIENT_PRIMARY 47      /* "node(s) Insufficient primary device" (device_allocator.go:264-266) */
 #define KE_REASON_DS_JOINT_VIOLATION 48           /* "node(s) Device Joint-Allocate rules violation" (:247-249) */
 #define KE_REASON_DS_NO_MATCHED_TEMPLATE 49       /* ErrNoMatchedGPUSharedResourceTemplate (allocator_gpu.go:141-143, utils.go:512-514) */
+/* NodeResourcesFit's Filter (upstream k8s v1.28.7 noderesources/fit.go fitsRequest): the first insufficiency in
+ * fitsRequest's order (pods, cpu, memory, then the scalar resources -- ranged over a Go map there, here in ext
+ * slot order) */
+#define KE_REASON_FIT_TOO_MANY_PODS 64            /* "Too many pods" */
+#define KE_REASON_FIT_INSUFFICIENT_CPU 65         /* "Insufficient cpu" */
+#define KE_REASON_FIT_INSUFFICIENT_MEMORY 66      /* "Insufficient memory" */
+#define KE_REASON_FIT_INSUFFICIENT_SCALAR 67      /* "Insufficient <resource name>" */
 
 /* ---- resources (index into per-resource arrays) ---------------------------------------------- */
 #define KE_RES_CPU 0          /* "cpu"                         MilliValue */
@@ -408,6 +415,37 @@ typedef struct ke_ext_args {
   ke_fitplus_resource fitplus[KE_MAX_FITPLUS];
 } ke_ext_args; /* 96 bytes */
 
+/* ---- NodeResourcesFit (upstream kube-scheduler v1.28.7 pkg/scheduler/framework/plugins/noderesources: fit.go,
+ * resource_allocation.go, least_allocated.go, most_allocated.go -- not in the reference tree, go.mod:60; restated
+ * from the published algorithm, parity unpinned).  The shipped profile runs it by default with LeastAllocated over
+ * cpu, memory, kubernetes.io/batch-cpu and kubernetes.io/batch-memory at weight 1 (config/manager/
+ * scheduler-config.yaml:17-31):
+ *  - Filter (fitsRequest), before every koordinator Filter (default plugins precede the profile's): len(Pods) + 1 >
+ *    AllowedPodNumber fails; a pod requesting nothing passes; else cpu / memory requests > 0 above Allocatable -
+ *    Requested fail, and so does a scalar request above Allocatable - Requested of its resource.
+ *  - Score: per configured resource, alloc / req = calculateResourceAllocatableRequest (cpu / memory: Allocatable,
+ *    NonZeroRequested + the pod's request with the 100m / 200Mi container defaults; a scalar the pod does not
+ *    request is skipped, else Allocatable, Requested + request), resources with alloc 0 skipped, then
+ *    Σ weight·{least,most}RequestedScore / Σ weight (0 when no weight counts).
+ * Resource ids as for NodeResourcesFitPlus; cpu / memory come from ke_node (Allocatable, Requested) and from the
+ * node's ke_node_resources_set rows (NonZeroRequested), scalars from those rows, the pod's requests from ke_pod.requests
+ * (cpu / memory) and ke_pod.xres (scalars; cpu / memory with the defaults for the Score).  Every scalar a pod may
+ * request must be listed in `scalars` (a pod listing another scalar id with a non-zero value is refused). */
+typedef struct ke_fit_args {
+  int64_t weight;          /* profile Score weight (0 = the Score is not in the profile) */
+  int32_t strategy;        /* ScoringStrategy.Type: KE_STRATEGY_LEAST_ALLOCATED / MOST_ALLOCATED */
+  int32_t n_resources;     /* ScoringStrategy.Resources (<= KE_MAX_FITPLUS; the type field of an entry is unused) */
+  ke_fitplus_resource resources[KE_MAX_FITPLUS];
+  int32_t n_scalars;       /* scalar resource ids (not cpu / memory) the Filter checks, <= 8 */
+  int32_t scalars[8];
+  uint8_t filter;          /* the Filter is in the profile */
+  uint8_t has_ignored;     /* IgnoredResources / IgnoredResourceGroups set, or RequestedToCapacityRatio:
+                              KE_ERR_UNSUPPORTED */
+  uint8_t pad[2];
+} ke_fit_args; /* 120 bytes */
+/* The ext slots NodeResourcesFitPlus and NodeResourcesFit read (their resources and the Filter's scalars,
+ * FitPlus's first) are at most 8 distinct ids (KE_ERR_UNSUPPORTED beyond). */
+
 /* Framework profile: score plugin weights (config/manager/scheduler-config.yaml:85-94). */
 typedef struct ke_config {
   int32_t abi_version;    /* must be KE_ABI_VERSION                                      */
@@ -418,12 +456,13 @@ typedef struct ke_config {
   ke_loadaware_args loadaware;
   ke_numa_args numa;
   ke_deviceshare_args deviceshare;
-  int32_t node_capacity;  /* max nodes this context will hold (device SoA is sized once) */
+  int32_t node_capacity;  /* max nodes this context will hold (device SoA is sized once), <= 2^22 - 1 */
   int32_t pod_batch;      /* B: pods evaluated per speculative batch in ke_schedule      */
   int32_t global_node_offset; /* first global node index held by this shard (multi-GPU)  */
   int32_t weight_reservation; /* profile Score weight of the Reservation plugin (scheduler-config.yaml:91-92:
                                  5000), 0 .. 2^20; scores only pods with matched reservations (ke_pod_reservations) */
   ke_ext_args ext;        /* NodeResourcesFitPlus / ScarceResourceAvoidance (all zero = disabled) */
+  ke_fit_args fit;        /* NodeResourcesFit (all zero = not in the profile) */
 } ke_config;
 
 /* A Node object (+ the NodeInfo aggregates the framework keeps for it). */
@@ -452,6 +491,8 @@ typedef struct ke_node {
   uint8_t cpu_topology_invalid;    /* TopologyOptions.CPUTopology set but !IsValid() (resource_manager.go:502-504) */
   uint8_t numa_allocate_strategy;  /* KE_NUMA_ALLOCATE_* (label overriding the args' NUMA allocate strategy) */
   uint8_t pad[6];
+  int32_t allowed_pods;            /* NodeInfo.Allocatable.AllowedPodNumber (status.allocatable pods) */
+  int32_t pod_count;               /* len(NodeInfo.Pods), reserve pods included; ke_schedule adds each placed pod */
 } ke_node;
 
 /* One AggregatedUsage entry of NodeMetric.Status.NodeMetric.AggregatedNodeUsages. */
@@ -1023,15 +1064,16 @@ int ke_last_host_stats(ke_ctx* ctx, double* ms8);
 /* Resolve kernel split of the last ke_schedule (in-kernel s_memrealtime stamps, every batch):
  * average ms per batch of candidate/row staging (prologue) and of the sequential replay. */
 int ke_last_resolve_split(ke_ctx* ctx, double* prologue_ms, double* replay_ms);
-/* Finer split (6 entries, ms per batch): init, candidate copy, slot hashing, slot lookup, row
- * gather, sequential replay. */
+/* Finer split (6 entries, ms per batch): prologue, the speculative replay's first round — predict (P),
+ * reserve + evaluate the slots (R + S), verify (V) —, its later rounds, and the write-back (all of a one-wave
+ * replay). */
+int ke_debug_resolve_phases(ke_ctx* ctx, double* phases6);
 /* BestEffort (pod, node) pairs the last ke_eval / ke_schedule evaluated in the compacted full-merge
  * pass (no preferred merged hint). */
 int ke_debug_numa_deferred(ke_ctx* ctx, int64_t* n);
 /* DeviceShare batches of the last ke_schedule that stopped early because a pod's NormalizeScore max may have
  * moved (their remaining pods were re-run as a new batch). */
 int ke_debug_ds_cuts(ke_ctx* ctx, int32_t* cuts);
-int ke_debug_resolve_phases(ke_ctx* ctx, double* phases6);
 /* Diagnostic build only (-DKE_PROF_REPLAY): shader cycles per pod of the replay loop's phases since the
  * last call — best unchanged candidate, row fetch issue, re-evaluation, its wave max, decision / adoption,
  * Reserve, next pod's changed flags — and the pod count (cyc8[7]); zeros in the product build. */

@@ -60,6 +60,8 @@ REASON_DS_INSUFFICIENT_FPGA_VF = 46
 REASON_DS_INSUFFICIENT_PRIMARY = 47
 REASON_DS_JOINT_VIOLATION = 48
 REASON_DS_NO_MATCHED_TEMPLATE = 49
+REASON_FIT_TOO_MANY_PODS, REASON_FIT_INSUFFICIENT_CPU, REASON_FIT_INSUFFICIENT_MEMORY = 64, 65, 66
+REASON_FIT_INSUFFICIENT_SCALAR = 67
 # ke_pod.gpu_required_topology_scope (apiext.DeviceTopologyScope -> level)
 SCOPE_NONE, SCOPE_NODE, SCOPE_NUMA, SCOPE_PCIE, SCOPE_DEVICE, SCOPE_UNKNOWN = range(6)
 SCOPES = {"": SCOPE_NONE, "Node": SCOPE_NODE, "NUMANode": SCOPE_NUMA, "PCIe": SCOPE_PCIE, "Device": SCOPE_DEVICE}
@@ -226,6 +228,12 @@ class ExtArgs(C.Structure):
                 ("pad", i32), ("fitplus", FitPlusResource * MAX_FITPLUS)]
 
 
+class FitArgs(C.Structure):
+    """NodeResourcesFit args + profile weight (koord_eval.h ke_fit_args; upstream k8s, parity unpinned)."""
+    _fields_ = [("weight", i64), ("strategy", i32), ("n_resources", i32), ("resources", FitPlusResource * MAX_FITPLUS),
+                ("n_scalars", i32), ("scalars", i32 * 8), ("filter", u8), ("has_ignored", u8), ("pad", u8 * 2)]
+
+
 class NodeResource(C.Structure):
     _fields_ = [("id", i32), ("pad", i32), ("allocatable", i64), ("requested", i64)]
 
@@ -245,6 +253,7 @@ class Config(C.Structure):
         ("global_node_offset", i32),
         ("weight_reservation", i32),
         ("ext", ExtArgs),
+        ("fit", FitArgs),
     ]
 
 
@@ -270,6 +279,8 @@ class Node(C.Structure):
         ("cpu_topology_invalid", u8),
         ("numa_allocate_strategy", u8),
         ("pad", u8 * 6),
+        ("allowed_pods", i32),
+        ("pod_count", i32),
     ]
 
 

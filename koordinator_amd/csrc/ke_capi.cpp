@@ -54,6 +54,13 @@ static int check_pods(const ke_pod* pods, int32_t n, const Context* c = nullptr,
     if (c) rc = validate_pod_hints(*c, pods[p]);
     else if (pods[p].device_hint) rc = fail(KE_ERR_INVALID, "ke_pod.device_hint without a context");
     if (rc) return rc;
+    if (c && c->cfg.fit.filter)  // NodeResourcesFit's Filter checks every requested scalar: it must have a slot
+      for (int e = 0; e < pods[p].n_xres; e++) {
+        const int32_t id = pods[p].xres_id[e];
+        bool known = id == KE_XRES_CPU || id == KE_XRES_MEMORY || pods[p].xres_value[e] == 0;
+        for (int q = 0; q < c->cfg.fit.n_scalars && !known; q++) known = c->cfg.fit.scalars[q] == id;
+        if (!known) return fail(KE_ERR_UNSUPPORTED, "a pod requesting a scalar resource outside ke_fit_args.scalars");
+      }
   }
   return KE_OK;
 }
@@ -180,18 +187,34 @@ int ke_create(const ke_config* cfg, ke_ctx** out) {
     k.w_ds[i] = cfg->deviceshare.weights[i] == KE_ABSENT ? -1 : (int32_t)cfg->deviceshare.weights[i];
   // NodeResourcesFitPlus / ScarceResourceAvoidance: their Score joins every evaluation path (eval_pair,
   // lite_total, and the fast replay's fast_total from the node's ext words)
+  // and NodeResourcesFit: ext slots (ext_slots: FitPlus resources first, then Fit's resources and scalars)
   const ke_ext_args& x = cfg->ext;
+  const ke_fit_args& fa = cfg->fit;
   k.wp_fp = (int32_t)x.weight_fitplus;
   k.wp_sra = (int32_t)x.weight_sra;
-  k.fp_n = x.n_fitplus;
-  k.fp_most = 0;
+  k.wp_fit = (int32_t)fa.weight;
   k.sra_mask = x.sra_resources;
-  for (int q = 0; q < 4; q++) {
-    k.fp_id[q] = q < x.n_fitplus ? x.fitplus[q].id : 0;
-    k.fp_w[q] = q < x.n_fitplus ? x.fitplus[q].weight : 0;
-    if (q < x.n_fitplus && x.fitplus[q].type == KE_STRATEGY_MOST_ALLOCATED) k.fp_most |= 1u << q;
+  int32_t ids[2 * NUM_XS + KE_MAX_FITPLUS];
+  k.xs_n = ext_slots(*cfg, ids);
+  k.fp_mask = k.fp_most = k.fit_mask = k.fit_scalar = 0;
+  for (int q = 0; q < NUM_XS; q++) {
+    k.xs_id[q] = q < k.xs_n ? ids[q] : 0;
+    k.fp_w[q] = k.fit_w[q] = 0;
   }
-  if (x.weight_fitplus > 0 || x.weight_sra > 0) {
+  for (int q = 0; q < x.n_fitplus; q++) {  // FitPlus resource q is slot q
+    k.fp_mask |= 1u << q;
+    k.fp_w[q] = x.fitplus[q].weight;
+    if (x.fitplus[q].type == KE_STRATEGY_MOST_ALLOCATED) k.fp_most |= 1u << q;
+  }
+  for (int q = 0; q < k.xs_n; q++) {
+    for (int r = 0; r < fa.n_resources; r++)
+      if (fa.resources[r].id == k.xs_id[q]) k.fit_mask |= 1u << q, k.fit_w[q] = fa.resources[r].weight;
+    for (int r = 0; r < fa.n_scalars; r++)
+      if (fa.scalars[r] == k.xs_id[q]) k.fit_scalar |= 1u << q;
+  }
+  if (fa.filter) k.flags |= AF_FIT_FILTER;
+  if (fa.strategy == KE_STRATEGY_MOST_ALLOCATED) k.flags |= AF_FIT_MOST;
+  if (x.weight_fitplus > 0 || x.weight_sra > 0 || fa.weight > 0 || fa.filter) {
     k.flags |= AF_EXT;
     c.ext_enabled = true;
   }

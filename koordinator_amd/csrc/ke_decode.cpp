@@ -16,6 +16,7 @@
 //                          it (deviceshare/device_cache.go:518-568), plus its GPU partition table and policy
 //                          (device_share.go:196-226,355-380)
 #include <algorithm>
+#include <climits>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -182,6 +183,10 @@ int ke_decode_node(const char* js, int64_t len, ke_node* out) {
     return alloc.overflow ? unsup("Node allocatable out of range") : bad("Node status.allocatable");
   rl_value(alloc, "cpu", &n.allocatable[0]);
   rl_value(alloc, "memory", &n.allocatable[1]);
+  {  // NodeInfo.Allocatable.AllowedPodNumber = int(pods.Value()) (framework.Resource.Add, k8s v1.28.7)
+    int64_t pods = 0;
+    if (rl_value(alloc, "pods", &pods)) n.allowed_pods = pods > INT32_MAX ? INT32_MAX : (int32_t)pods;
+  }
   // raw allocatable (EstimateNode, default_estimator.go:124-143): an unmarshal error falls back to Allocatable
   if (const std::string* s = lookup(ann, "node.koordinator.sh/raw-allocatable")) {
     Value v;

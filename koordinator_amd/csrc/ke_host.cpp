@@ -42,12 +42,35 @@ int validate_config(const ke_config& cfg) {
   if (cfg.weight_reservation < 0) return fail(KE_ERR_INVALID, "negative Reservation weight");
   if (cfg.weight_reservation > (1 << 20)) return fail(KE_ERR_UNSUPPORTED, "Reservation weight above 2^20");
   if (cfg.weight_loadaware < 0 || cfg.weight_numa < 0 || cfg.weight_deviceshare < 0 || x.weight_fitplus < 0 ||
-      x.weight_sra < 0 ||
-      (cfg.weight_loadaware + cfg.weight_numa + cfg.weight_deviceshare + x.weight_fitplus + x.weight_sra) * 100 >
-          MAX_TOTAL_SCORE)
-    return fail(KE_ERR_UNSUPPORTED, "plugin weights: (sum of the Score plugin weights) * 100 must be <= 510");
+      x.weight_sra < 0 || cfg.fit.weight < 0 ||
+      (cfg.weight_loadaware + cfg.weight_numa + cfg.weight_deviceshare + x.weight_fitplus + x.weight_sra +
+       cfg.fit.weight) * 100 > MAX_TOTAL_SCORE)
+    return fail(KE_ERR_UNSUPPORTED, "plugin weights: (sum of the Score plugin weights) * 100 must be <= 1022");
   if (x.n_fitplus < 0 || x.n_fitplus > KE_MAX_FITPLUS)
     return fail(KE_ERR_UNSUPPORTED, "NodeResourcesFitPlusArgs.Resources: at most 4 resources");
+  const ke_fit_args& fa = cfg.fit;
+  if (fa.weight < 0 || fa.weight > (1 << 20)) return fail(KE_ERR_UNSUPPORTED, "NodeResourcesFit weight out of range");
+  if (fa.has_ignored)
+    return fail(KE_ERR_UNSUPPORTED, "NodeResourcesFit ignored resources / groups or RequestedToCapacityRatio");
+  if (fa.strategy != KE_STRATEGY_LEAST_ALLOCATED && fa.strategy != KE_STRATEGY_MOST_ALLOCATED)
+    return fail(KE_ERR_INVALID, "NodeResourcesFit scoring strategy");
+  if (fa.n_resources < 0 || fa.n_resources > KE_MAX_FITPLUS || fa.n_scalars < 0 || fa.n_scalars > 8)
+    return fail(KE_ERR_UNSUPPORTED, "NodeResourcesFit: at most 4 scored resources and 8 filtered scalars");
+  for (int q = 0; q < fa.n_resources; q++) {
+    const ke_fitplus_resource& e = fa.resources[q];
+    if (e.id < 0 || e.id >= KE_MAX_XRES) return fail(KE_ERR_INVALID, "NodeResourcesFit resource id out of range");
+    if (e.weight < 0 || e.weight > (1 << 20)) return fail(KE_ERR_UNSUPPORTED, "NodeResourcesFit resource weight out of range");
+    for (int r = 0; r < q; r++)
+      if (fa.resources[r].id == e.id) return fail(KE_ERR_INVALID, "NodeResourcesFit resource listed twice");
+  }
+  for (int q = 0; q < fa.n_scalars; q++)
+    if (fa.scalars[q] < 2 || fa.scalars[q] >= KE_MAX_XRES)
+      return fail(KE_ERR_INVALID, "NodeResourcesFit scalar id out of range (cpu / memory are not scalars)");
+  {
+    int32_t ids[2 * NUM_XS + KE_MAX_FITPLUS];
+    if (ext_slots(cfg, ids) > NUM_XS)
+      return fail(KE_ERR_UNSUPPORTED, "NodeResourcesFitPlus + NodeResourcesFit read more than 8 distinct resources");
+  }
   for (int q = 0; q < x.n_fitplus; q++) {
     const ke_fitplus_resource& e = x.fitplus[q];
     if (e.id < 0 || e.id >= KE_MAX_XRES) return fail(KE_ERR_INVALID, "NodeResourcesFitPlus resource id out of range");
@@ -482,16 +505,33 @@ int validate_node_resources(int32_t n, const ke_node_resource* r) {
   return KE_OK;
 }
 
-// NodeResourcesFitPlus / ScarceResourceAvoidance ext row: Allocatable / (NonZero)Requested of the FitPlus
-// slots (0 for a resource the node does not list) and the mask of ids with Allocatable > 0
+int ext_slots(const ke_config& cfg, int32_t* ids) {
+  int n = 0;
+  auto add = [&](int32_t id) {
+    for (int q = 0; q < n; q++)
+      if (ids[q] == id) return;
+    ids[n++] = id;
+  };
+  for (int q = 0; q < cfg.ext.n_fitplus && q < KE_MAX_FITPLUS; q++) ids[n++] = cfg.ext.fitplus[q].id;  // slot q = FitPlus q
+  for (int q = 0; q < cfg.fit.n_resources && q < KE_MAX_FITPLUS; q++) add(cfg.fit.resources[q].id);
+  for (int q = 0; q < cfg.fit.n_scalars && q < 8; q++) add(cfg.fit.scalars[q]);
+  return n;
+}
+
+// ext row: per slot Allocatable / (NonZero)Requested (0 for a resource the node does not list), the pod room of
+// NodeResourcesFit's Filter (AllowedPodNumber - len(Pods), the matched reservations' reserve pods removed), and the
+// mask of ids with Allocatable > 0
 void derive_ext_row(const ke_config& cfg, const NodeState& ns, int64_t* f, uint64_t* mask) {
   for (int w = 0; w < NUM_XF; w++) f[w] = 0;
+  int32_t ids[2 * NUM_XS + KE_MAX_FITPLUS];
+  const int nxs = std::min(ext_slots(cfg, ids), NUM_XS);
   uint64_t m = 0;
   for (const ke_node_resource& r : ns.xres) {
     if (r.allocatable > 0) m |= 1ull << r.id;
-    for (int q = 0; q < cfg.ext.n_fitplus && q < 4; q++)
-      if (cfg.ext.fitplus[q].id == r.id) f[XF_ALLOC + q] = r.allocatable, f[XF_REQ + q] = xres_requested(ns, r);
+    for (int q = 0; q < nxs; q++)
+      if (ids[q] == r.id) f[XF_ALLOC + q] = r.allocatable, f[XF_REQ + q] = xres_requested(ns, r);
   }
+  f[XF_PODS] = (int64_t)ns.node.allowed_pods - ((int64_t)ns.node.pod_count + ns.rv_pods);
   *mask = m;
 }
 
@@ -515,13 +555,15 @@ bool resv_usable(const ke_reservation& r) { return r.available && !(r.allocate_o
 
 // node's Requested / NonZeroRequested deltas with `matched` (by reservation index, nullptr = none) matched
 static void resv_delta(const Context& c, int32_t node, const std::vector<char>* matched, bool with_matched,
-                       int64_t* req, int64_t* nz) {
+                       int64_t* req, int64_t* nz, int32_t* pods = nullptr) {
   for (int k = 0; k < KE_NRES; k++) req[k] = nz[k] = 0;
+  if (pods) *pods = 0;
   for (int32_t i : c.resv_by_node[(size_t)node]) {
     const ke_reservation& r = c.resv[(size_t)i];
     if (!resv_usable(r)) continue;
     if (matched && (*matched)[(size_t)i]) {
       if (!with_matched) continue;
+      if (pods) --*pods;  // NodeInfo.RemovePod(reservePod)
       for (int k = 0; k < KE_NRES; k++) {
         req[k] -= r.allocatable[k];
         nz[k] -= resv_non0(k, r.allocatable[k]);
@@ -544,7 +586,7 @@ static void resv_delta(const Context& c, int32_t node, const std::vector<char>* 
 
 void resv_node_restore(Context& c, int32_t node) {
   NodeState& ns = c.nodes[(size_t)node];
-  resv_delta(c, node, nullptr, false, ns.rv_req, ns.rv_nz);
+  resv_delta(c, node, nullptr, false, ns.rv_req, ns.rv_nz, &ns.rv_pods);
   ns.dirty = true;
 }
 
@@ -693,7 +735,7 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
     c.rsv_pairs.push_back({node, (int16_t)(nom >= 0 ? resv_score(c.resv[(size_t)nom], pod) : 0), (int16_t)allowed, order});
     c.rsv_nominated.push_back(nom);
     // the rows this pod sees: its matched reservations restored too
-    resv_delta(c, node, &m, true, ns.rv_req, ns.rv_nz);
+    resv_delta(c, node, &m, true, ns.rv_req, ns.rv_nz, &ns.rv_pods);
     ns.dirty = true;
   }
   return KE_OK;
@@ -960,10 +1002,12 @@ DevPod make_dev_pod(const ke_config& cfg, const ke_pod& pod, const ke_pod_device
   if (pod.quota_non_preemptible) d.flags |= PF_QUOTA_NP;
   // NodeResourcesFitPlus / ScarceResourceAvoidance PreScore: requested names and the FitPlus requests by slot
   d.xmask = pod.xres_request_mask;
-  for (int q = 0; q < cfg.ext.n_fitplus && q < 4; q++) {
+  int32_t ids[2 * NUM_XS + KE_MAX_FITPLUS];
+  const int nxs = std::min(ext_slots(cfg, ids), NUM_XS);
+  for (int q = 0; q < NUM_XS; q++) {
     d.xreq[q] = 0;
-    for (int e = 0; e < pod.n_xres; e++)
-      if (pod.xres_id[e] == cfg.ext.fitplus[q].id) d.xreq[q] = pod.xres_value[e];
+    for (int e = 0; q < nxs && e < pod.n_xres; e++)
+      if (pod.xres_id[e] == ids[q]) d.xreq[q] = pod.xres_value[e];
   }
   // parseGPURequirements (utils.go:487-513): GPUPartitionSpec and the GPU hint's required topology scope
   d.flags |= (uint32_t)pod.gpu_required_topology_scope * PF_GPU_SCOPE0;
@@ -1436,6 +1480,7 @@ void host_release_node(const ke_config& cfg, bool ext, NodeState& ns, const ke_p
   // framework NodeInfo.RemovePod: Requested (and the FitPlus (NonZero)Requested by resource id)
   ns.node.requested[KE_RES_CPU] -= pod.requests[KE_RES_CPU];
   ns.node.requested[KE_RES_MEMORY] -= pod.requests[KE_RES_MEMORY];
+  ns.node.pod_count--;
   if (ext)
     for (int e = 0; e < pod.n_xres; e++)
       for (ke_node_resource& r : ns.xres)
@@ -1515,6 +1560,7 @@ void flush_mirror(Context& c) {
     host_assign(c.cfg, ns, pod, a.ts);
     ns.node.requested[KE_RES_CPU] += pod.requests[KE_RES_CPU];
     ns.node.requested[KE_RES_MEMORY] += pod.requests[KE_RES_MEMORY];
+    ns.node.pod_count++;  // NodeInfo.AddPod
     if (c.ext_enabled) host_ext_reserve(ns, pod);
     ns.dirty = was_dirty;  // the device row already carries this Reserve
   }

@@ -92,6 +92,7 @@ struct NodeState {
   // Reservations: the NodeInfo restore every pod sees (restoreUnmatchedReservations), added to
   // Requested / NonZeroRequested (MilliCPU, Memory) when the rows are derived (load_reservations)
   int64_t rv_req[KE_NRES] = {0, 0}, rv_nz[KE_NRES] = {0, 0};
+  int32_t rv_pods = 0;  // len(NodeInfo.Pods) delta of the restore (matched reserve pods removed)
   // derived
   DirtyFlag dirty;              // row must be re-derived and uploaded
   int64_t valid_until = INT64_MAX;  // derived row is exact for now < valid_until
@@ -264,6 +265,9 @@ void host_numa_reserve(NodeState& ns, const int64_t* delta /*[KE_MAX_NUMA*KE_NRE
 
 // NodeResourcesFitPlus / ScarceResourceAvoidance
 int validate_node_resources(int32_t n, const ke_node_resource* r);
+// the ext slots' resource ids (FitPlus resources, then NodeResourcesFit's other resources and filtered scalars);
+// returns their count (> NUM_XS: refused by validate_config).  `ids` holds 2 * NUM_XS + KE_MAX_FITPLUS entries.
+int ext_slots(const ke_config& cfg, int32_t* ids);
 // the ext SoA row of a node: NUM_XF int64 + the uint64 mask of resource ids with Allocatable > 0
 void derive_ext_row(const ke_config& cfg, const NodeState& ns, int64_t* f, uint64_t* mask);
 int load_reservations(Context& c, int32_t n, const ke_reservation* r);

@@ -2150,19 +2150,20 @@ __device__ __forceinline__ void numa_reserve(const SoA& s, int64_t i, uint32_t n
 // NUMA: some node may carry a NUMA topology policy; `nv` holds node i's zones when its policy is set.
 // CPU: the pod may bind CPUs (PF_CPUSET: a singleton batch) — cpuset PreFilter state, requestCPUBind,
 // the amplified pod cpu and the required-bind-policy checks read the CPU SoA.
-// ---- NodeResourcesFitPlus + ScarceResourceAvoidance Score ------------------------
-// Weighted framework contribution of the two plugins for a feasible (pod, node).  Go int64 arithmetic
-// (wrapping products, truncating division) on the ext SoA.
+// ---- NodeResourcesFitPlus + ScarceResourceAvoidance + NodeResourcesFit -----------
+// Weighted framework contribution of the Score plugins that read NodeInfo by resource id, for a feasible (pod,
+// node), and NodeResourcesFit's Filter.  Go int64 arithmetic (wrapping products, truncating division) on the ext
+// slots (KArgs::xs_id): xa / xr = the node's Allocatable / (NonZero)Requested of slot q, xm = its ids with
+// Allocatable > 0.
 __device__ __forceinline__ int64_t mul100_wrap(int64_t x) { return (int64_t)((uint64_t)x * 100u); }
-// from the node's words: xm = ids with Allocatable > 0, xa / xr = FitPlus slots' Allocatable / (NonZero)Requested
-__device__ __forceinline__ int32_t ext_score_vals(uint64_t xm, const int64_t (&xa)[4], const int64_t (&xr)[4],
+__device__ __forceinline__ int32_t ext_score_vals(uint64_t xm, const int64_t (&xa)[NUM_XS], const int64_t (&xr)[NUM_XS],
                                                   const DevPod& p, const KArgs& k) {
   int32_t t = 0;
   if (k.wp_fp) {  // resourceScorer (node_resource_fit_plus_utils.go:57-89) over the pod's requested names
     int64_t ns = 0, ws = 0;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      if (q >= k.fp_n || !((p.xmask >> k.fp_id[q]) & 1)) continue;
+    for (int q = 0; q < NUM_XS; q++) {
+      if (!((k.fp_mask >> q) & 1) || !((p.xmask >> k.xs_id[q]) & 1)) continue;
       const int64_t cap = xa[q];
       int64_t req = xr[q] + p.xreq[q];
       int64_t sc = 0;
@@ -2182,22 +2183,74 @@ __device__ __forceinline__ int32_t ext_score_vals(uint64_t xm, const int64_t (&x
     const int nd = __popcll(diff), ni = __popcll(diff & k.sra_mask);
     t += k.wp_sra * ((nd == 0 || ni == 0) ? 100 : (nd - ni) * 100 / nd);
   }
+  if (k.wp_fit) {  // NodeResourcesFit Score (k8s v1.28.7 resource_allocation.go score, least/most_allocated.go)
+    int64_t ns = 0, ws = 0;
+    const bool most = (k.flags & AF_FIT_MOST) != 0;
+#pragma unroll
+    for (int q = 0; q < NUM_XS; q++) {
+      if (!((k.fit_mask >> q) & 1)) continue;
+      const int64_t preq = p.xreq[q];
+      if (k.xs_id[q] >= 2 && preq == 0) continue;  // a scalar the pod does not request: (0, 0)
+      const int64_t cap = xa[q];
+      if (cap == 0) continue;
+      int64_t req = xr[q] + preq;
+      int64_t sc;
+      if (most) {
+        if (req > cap) req = cap;
+        sc = mul100_wrap(req) / cap;
+      } else {
+        sc = req > cap ? 0 : mul100_wrap(cap - req) / cap;
+      }
+      ns += sc * k.fit_w[q];
+      ws += k.fit_w[q];
+    }
+    t += k.wp_fit * (int32_t)(ws == 0 ? 0 : ns / ws);
+  }
   return t;
 }
-__device__ __forceinline__ int32_t ext_score(const SoA& s, int64_t i, const DevPod& p, const KArgs& k) {
-  int64_t xa[4], xr[4];
+// NodeResourcesFit Filter (k8s v1.28.7 fit.go fitsRequest): the pod room, then cpu / memory requests > 0 against
+// Allocatable - Requested (the row's NodeInfo), then the scalar slots; returns the reason (0 = fits)
+__device__ __forceinline__ uint8_t fit_filter(int64_t room, const int64_t (&xa)[NUM_XS], const int64_t (&xr)[NUM_XS],
+                                              bool cpu_over, bool mem_over, const DevPod& p, const KArgs& k) {
+  if (room < 1) return KE_REASON_FIT_TOO_MANY_PODS;
+  if (cpu_over) return KE_REASON_FIT_INSUFFICIENT_CPU;
+  if (mem_over) return KE_REASON_FIT_INSUFFICIENT_MEMORY;
+  bool sc = false;
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
-    xa[q] = q < k.fp_n ? s.xf[(XF_ALLOC + q) * s.stride + i] : 0;
-    xr[q] = q < k.fp_n ? s.xf[(XF_REQ + q) * s.stride + i] : 0;
+  for (int q = 0; q < NUM_XS; q++)
+    sc |= ((k.fit_scalar >> q) & 1) && p.xreq[q] > 0 && p.xreq[q] > xa[q] - xr[q];
+  return sc ? KE_REASON_FIT_INSUFFICIENT_SCALAR : 0;
+}
+// the node's ext words from the SoA (plain loads: no kernel writes them while this one runs)
+__device__ __forceinline__ void ext_words(const SoA& s, int64_t i, const KArgs& k, int64_t (&xa)[NUM_XS],
+                                          int64_t (&xr)[NUM_XS], int64_t& room) {
+#pragma unroll
+  for (int q = 0; q < NUM_XS; q++) {
+    xa[q] = q < k.xs_n ? s.xf[(XF_ALLOC + q) * s.stride + i] : 0;
+    xr[q] = q < k.xs_n ? s.xf[(XF_REQ + q) * s.stride + i] : 0;
   }
+  room = s.xf[XF_PODS * s.stride + i];
+}
+// NodeResourcesFit's Filter reason on a row (eval_pair / lite_total)
+__device__ __forceinline__ uint8_t fit_filter_row(const SoA& s, int64_t i, const NodeRegs& n, const DevPod& p,
+                                                  const KArgs& k) {
+  int64_t xa[NUM_XS], xr[NUM_XS], room;
+  ext_words(s, i, k, xa, xr, room);
+  const bool co = p.req[0] > 0 && p.req[0] > n.nalloc[0] - n.nreq[0];
+  const bool mo = p.req[1] > 0 && p.req[1] > n.nalloc[1] - n.nreq[1];
+  return fit_filter(room, xa, xr, co, mo, p, k);
+}
+__device__ __forceinline__ int32_t ext_score(const SoA& s, int64_t i, const DevPod& p, const KArgs& k) {
+  int64_t xa[NUM_XS], xr[NUM_XS], room;
+  ext_words(s, i, k, xa, xr, room);
   return ext_score_vals(s.xm[i], xa, xr, p, k);
 }
-// Reserve: NodeInfo (NonZero)Requested += the pod's requests of the FitPlus resources
+// Reserve: NodeInfo (NonZero)Requested += the pod's requests of the slots' resources, one pod more
 __device__ __forceinline__ void ext_reserve(const SoA& s, int64_t i, const DevPod& p, const KArgs& k) {
 #pragma unroll
-  for (int q = 0; q < 4; q++)
-    if (q < k.fp_n) s.xf[(XF_REQ + q) * s.stride + i] += p.xreq[q];
+  for (int q = 0; q < NUM_XS; q++)
+    if (q < k.xs_n) s.xf[(XF_REQ + q) * s.stride + i] += p.xreq[q];
+  s.xf[XF_PODS * s.stride + i] -= 1;
 }
 
 template <bool DS, bool NUMA, bool DEFER = false, bool FB_AFF = false, bool CPU = false, bool H = false>
@@ -2225,6 +2278,16 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
     o.reason = p.ds_req[0] ? (uint8_t)p.ds_req[0] : (uint8_t)KE_REASON_DS_INVALID_REQUEST;  // the host's reason
     o.total = -1;
     return o;
+  }
+  // ---- NodeResourcesFit.Filter (a default plugin: before the profile's own Filters)
+  if (k.flags & AF_FIT_FILTER) {
+    const uint8_t why = fit_filter_row(s, i, n, p, k);
+    if (why) {
+      o.status = KE_CODE_UNSCHEDULABLE;
+      o.reason = why;
+      o.total = -1;
+      return o;
+    }
   }
   // ---- LoadAwareScheduling.Filter  load_aware.go:122-186
   if (!(p.flags & PF_DAEMONSET) && (nf & NF_HAS_METRIC)) {
@@ -2591,19 +2654,33 @@ struct NodeFast {
   int64_t amp_room;   // filterAmplifiedCPUs passes iff req0 <= amp_room (THR_NONE = no check)
   uint32_t bits;      // sbits + the `now`-dependent FB bits
   bool thr_node;      // the LoadAware filter thresholds apply (metric, not expired-filtered, NodeMetric set)
-  // NodeResourcesFitPlus / ScarceResourceAvoidance (AF_EXT): the node's ext SoA words (ext_load)
+  // NodeResourcesFitPlus / ScarceResourceAvoidance / NodeResourcesFit (AF_EXT): the node's ext SoA words (ext_load)
   uint64_t xm;
-  int64_t xa[4], xr[4];
+  int64_t xa[NUM_XS], xr[NUM_XS];
+  int64_t room;  // AllowedPodNumber - len(Pods)
 };
 
 // the node's ext words (sc1: a Reserve kernel of this or a concurrent launch may have written them)
 __device__ __forceinline__ void ext_load(const SoA& s, int64_t node, const KArgs& k, NodeFast& f) {
   f.xm = (uint64_t)ld_sc1(reinterpret_cast<const int64_t*>(s.xm) + node);
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
-    f.xa[q] = q < k.fp_n ? ld_sc1(s.xf + (XF_ALLOC + q) * s.stride + node) : 0;
-    f.xr[q] = q < k.fp_n ? ld_sc1(s.xf + (XF_REQ + q) * s.stride + node) : 0;
+  for (int q = 0; q < NUM_XS; q++) {
+    f.xa[q] = q < k.xs_n ? ld_sc1(s.xf + (XF_ALLOC + q) * s.stride + node) : 0;
+    f.xr[q] = q < k.xs_n ? ld_sc1(s.xf + (XF_REQ + q) * s.stride + node) : 0;
   }
+  f.room = ld_sc1(s.xf + XF_PODS * s.stride + node);
+}
+// a Reserve on the node's ext words in registers, and their write-back (sc1: read by later launches)
+__device__ __forceinline__ void ext_fast_reserve(NodeFast& f, const DevPod& p, const KArgs& k) {
+#pragma unroll
+  for (int q = 0; q < NUM_XS; q++) f.xr[q] += q < k.xs_n ? p.xreq[q] : 0;
+  f.room -= 1;
+}
+__device__ __forceinline__ void ext_store(const SoA& s, int64_t node, const NodeFast& f, const KArgs& k) {
+#pragma unroll
+  for (int q = 0; q < NUM_XS; q++)
+    if (q < k.xs_n) st_sc1(s.xf + (XF_REQ + q) * s.stride + node, f.xr[q]);
+  st_sc1(s.xf + XF_PODS * s.stride + node, f.room);
 }
 
 // the record of a prepared row (rcap / ralloc set), static bits from the args
@@ -2815,6 +2892,11 @@ __device__ __forceinline__ int32_t fast_total(const NodeFast& f, const DevPod& p
     fail |= ((b & FB_EXP_FAIL) != 0) | (p.est[0] > (pp ? f.thr[1][0] : f.thr[0][0])) |
             (p.est[1] > (pp ? f.thr[1][1] : f.thr[0][1]));
   if (!(pf & PF_NUMA_SKIP) & (p.req[0] != 0)) fail |= ((b & FB_AMP_BAD) != 0) | (p.req[0] > f.amp_room);
+  if (EXT && (k.flags & AF_FIT_FILTER)) {  // NodeResourcesFit.Filter on the record's exact doubles
+    const bool co = (p.req[0] > 0) & (reqd[0] > f.al[0] - f.nreq[0]);
+    const bool mo = (p.req[1] > 0) & (reqd[1] > f.al[1] - f.nreq[1]);
+    fail |= fit_filter(f.room, f.xa, f.xr, co, mo, p, k) != 0;
+  }
   // LoadAwareScheduling.Score
   const bool vs = (pf & PF_LA_SCORE_PROD) != 0;
   int32_t sl = 0;
@@ -3007,7 +3089,8 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_batch(SoA s, int lo, int hi
     const DevPod& pod = pods[base + p];
     if constexpr (!DS && !NUMA && !CPU) {  // plain batch: straight-line evaluation
       int32_t tot = lite_total(n, expired, pod, k);
-      if (EXT && tot >= 0) tot += ext_score(s, i, pod, k);  // FitPlus / SRA: its own variant
+      if (EXT && tot >= 0 && (k.flags & AF_FIT_FILTER) && fit_filter_row(s, i, n, pod, k)) tot = -1;
+      if (EXT && tot >= 0) tot += ext_score(s, i, pod, k);  // FitPlus / SRA / Fit: its own variant
       scores[(int64_t)p * score_stride + i] = (uint16_t)(tot + 1);
       continue;
     }
@@ -4123,6 +4206,8 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
   int snode = -1;
   int32_t o_node = -1, o_score = -1;  // wave 0, lane j: pod j's placement
   int start = 0, win = B, rounds = 0, fetched = 0;
+  const bool stamp = wave == 0 && lane == 0;  // phase stamps of the first round (ke_debug_resolve_phases)
+  bool first = true;
   while (start < B) {
     const int end = min(B, start + win);
     // ---- P (wave 0): pods [start, end) each take their best candidate not taken before
@@ -4146,6 +4231,7 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
       }
     }
     __syncthreads();
+    if (stamp && first) pst[1] = __builtin_amdgcn_s_memrealtime();
     // ---- R (every wave): lane c in [start, end) adopts pod c's predicted node and reserves pod c on it
     if (lane >= start && lane < end) {
       snode = L.sp.xnode[lane];
@@ -4157,9 +4243,7 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
         const DevPod pc = L.pod[lane];
         const double ed[2] = {L.pd[lane][0], L.pd[lane][1]}, rd[2] = {L.pd[lane][2], L.pd[lane][3]};
         fast_reserve(slot, pc, ed, rd);
-        if (ext)
-#pragma unroll
-          for (int q = 0; q < 4; q++) slot.xr[q] += q < k.fp_n ? pc.xreq[q] : 0;
+        if (ext) ext_fast_reserve(slot, pc, k);
       }
     }
     if (wave == 0) fetched += __popcll(__ballot(lane >= start && lane < end && sv));
@@ -4173,6 +4257,7 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
       if (lane == 0) L.sp.mrow[j] = mx;
     }
     __syncthreads();
+    if (stamp && first) pst[2] = __builtin_amdgcn_s_memrealtime();
     // ---- V (wave 0): the first pod whose best changed node beats its prediction
     if (wave == 0) {
       const bool in = lane >= start && lane < end;
@@ -4195,6 +4280,8 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
       if (lane == 0) L.sp.jf = jf;
     }
     __syncthreads();
+    if (stamp && first) pst[3] = __builtin_amdgcn_s_memrealtime();
+    first = false;
     const int jf = L.sp.jf;
     if (jf < end) {
       if (lane >= jf && lane < end) sv = false;
@@ -4203,9 +4290,7 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
         const DevPod pc = L.pod[jf];
         const double ed[2] = {L.pd[jf][0], L.pd[jf][1]}, rd[2] = {L.pd[jf][2], L.pd[jf][3]};
         fast_reserve(slot, pc, ed, rd);
-        if (ext)
-#pragma unroll
-          for (int q = 0; q < 4; q++) slot.xr[q] += q < k.fp_n ? pc.xreq[q] : 0;
+        if (ext) ext_fast_reserve(slot, pc, k);
       }
       win = max(8, 2 * (jf - start + 1));
       start = jf + 1;
@@ -4216,6 +4301,7 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
     }
   }
   if (wave != 0) return;
+  if (lane == 0) pst[5] = __builtin_amdgcn_s_memrealtime();
   if (lane < B) {
     chosen[base + lane] = o_node;
     chosen_score[base + lane] = o_score;
@@ -4236,10 +4322,7 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
     st_sc1(f + (F_NREQ + 0) * st, (int64_t)slot.nreq[0]);
     st_sc1(f + (F_NREQ + 1) * st, (int64_t)slot.nreq[1]);
     rec_store_dyn<__HIP_MEMORY_SCOPE_AGENT>(s.rec + (int64_t)snode * NUM_RW, slot);  // sc1: read by k_eval_plain
-    if (ext)
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-        if (q < k.fp_n) st_sc1(s.xf + (XF_REQ + q) * st + snode, slot.xr[q]);
+    if (ext) ext_store(s, snode, slot, k);
     if (touched_out) rec_store_full(touched_out + (int64_t)lanes_below(vm) * NUM_RW, slot, snode);
     chg_clear_word(C, snode);  // every bit still set belongs to a taken node
   }
@@ -4470,9 +4553,7 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
       if (lane == owner) {
         if constexpr (FAST) {
           fast_reserve(fast, pod, estd, reqd);
-          if (EXT && (k.flags & AF_EXT))  // NodeInfo (NonZero)Requested of the FitPlus resources
-#pragma unroll
-            for (int q = 0; q < 4; q++) fast.xr[q] += q < k.fp_n ? pod.xreq[q] : 0;
+          if (EXT && (k.flags & AF_EXT)) ext_fast_reserve(fast, pod, k);  // NodeInfo (NonZero)Requested, Pods
         } else {
           if ((mine.flags & NF_HAS_METRIC) && !(mine.flags & NF_NM_NIL)) {
 #pragma unroll
@@ -4564,10 +4645,7 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
       st_sc1(f + (F_NREQ + 0) * st, (int64_t)fast.nreq[0]);
       st_sc1(f + (F_NREQ + 1) * st, (int64_t)fast.nreq[1]);
       rec_store_dyn<__HIP_MEMORY_SCOPE_AGENT>(rec, fast);
-      if (EXT && (k.flags & AF_EXT))
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-          if (q < k.fp_n) st_sc1(s.xf + (XF_REQ + q) * st + my_node, fast.xr[q]);
+      if (EXT && (k.flags & AF_EXT)) ext_store(s, my_node, fast, k);
       if (touched_out) rec_store_full(touched_out + (int64_t)lane * NUM_RW, fast, my_node);
     } else {
 #pragma unroll
@@ -6225,17 +6303,20 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     }
   }
   double pro = 0, loop = 0;  // resolve kernel: prologue (candidate/row staging) vs sequential replay
-  double ph[6] = {0, 0, 0, 0, 0, 0};  // init, cand copy, hash insert, slot lookup, row gather, replay
+  // phases: prologue, then the speculative replay's first round (P, R + S, V), its later rounds, and the
+  // write-back (the one-wave replay of other batches counts entirely as write-back)
+  double ph[6] = {0, 0, 0, 0, 0, 0};
   for (int b = 0; b < n_batches; b++) {
     const uint64_t* p = &pst[8 * (size_t)b];
     pro += (double)(p[4] - p[0]) * ms_per_tick;
     loop += (double)(st[b + 1] - p[4]) * ms_per_tick;
-    ph[0] += (double)(p[1] - p[0]);
-    ph[1] += (double)(p[2] - p[1]);
-    ph[2] += (double)(p[3] - p[2]);
-    ph[3] += (double)(p[5] - p[3]);
-    ph[4] += (double)(p[4] - p[5]);
-    ph[5] += (double)(st[b + 1] - p[4]);
+    const bool spec = p[1] > p[4];
+    ph[0] += (double)(p[4] - p[0]);
+    ph[1] += spec ? (double)(p[1] - p[4]) : 0.0;
+    ph[2] += spec ? (double)(p[2] - p[1]) : 0.0;
+    ph[3] += spec ? (double)(p[3] - p[2]) : 0.0;
+    ph[4] += spec ? (double)(p[5] - p[3]) : 0.0;
+    ph[5] += (double)(st[b + 1] - (spec ? p[5] : p[4]));
   }
   ctx->kstat_resolve_prologue_ms = pro / n_batches;
   ctx->kstat_resolve_loop_ms = loop / n_batches;

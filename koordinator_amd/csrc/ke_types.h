@@ -195,12 +195,13 @@ struct DevPod {
   uint8_t quota;      // ElasticQuota: 0 = none, else 1 + quota index (ke_pod.quota)
   int64_t ds_req[5];  // DeviceShare per-instance request: gpu-core, gpu-memory, gpu-memory-ratio, rdma, fpga
   int64_t ring_bw;    // GPUPartitionSpec.RingBusBandwidth (PF_GPU_RING_BW)
-  // NodeResourcesFitPlus / ScarceResourceAvoidance: the pod's request of each FitPlus resource (slot order of
-  // KArgs::fp_id, calculatePodResourceRequest), and the ids of its requested resource names (PodRequests > 0)
-  int64_t xreq[4];
+  // ext slots (KArgs::xs_id: NodeResourcesFitPlus / NodeResourcesFit resources): the pod's request of each slot's
+  // resource (ke_pod.xres_value: calculatePodResourceRequest -- cpu / memory with the non-zero defaults --, a
+  // scalar's PodRequests), and the ids of its requested resource names (PodRequests > 0)
+  int64_t xreq[8];
   uint64_t xmask;
 };
-static_assert(sizeof(DevPod) == 128, "DevPod layout");
+static_assert(sizeof(DevPod) == 160, "DevPod layout");
 // DevPod::ds_cnt of an ApplyForAll type: the desired count is the node's devices of the type matching the Selector
 constexpr uint8_t DS_CNT_ALL = 255;
 
@@ -293,8 +294,11 @@ enum ArgFlag : uint32_t {
   AF_QUOTA = 1u << 6,               // an ElasticQuota tree is loaded: PreFilter admission + Reserve
   AF_QUOTA_PARENT = 1u << 7,        // ElasticQuotaArgs.EnableCheckParentQuota
   AF_DS_NO_NUMA = 1u << 8,          // DeviceShareArgs.DisableDeviceNUMATopologyAlignment
-  AF_EXT = 1u << 9,                 // NodeResourcesFitPlus / ScarceResourceAvoidance in the profile (ext SoA)
+  AF_EXT = 1u << 9,                 // NodeResourcesFitPlus / ScarceResourceAvoidance / NodeResourcesFit (ext SoA)
+  AF_FIT_FILTER = 1u << 10,         // NodeResourcesFit's Filter in the profile
+  AF_FIT_MOST = 1u << 11,           // NodeResourcesFit ScoringStrategy MostAllocated
 };
+constexpr int NUM_XS = 8;  // ext slots: the resource ids NodeResourcesFitPlus / NodeResourcesFit read
 struct KArgs {
   int64_t now;
   int64_t exp_s;       // NodeMetricExpirationSeconds
@@ -305,24 +309,28 @@ struct KArgs {
   uint32_t flags;
   int32_t wp_ds;           // DeviceShare plugin weight
   int32_t w_ds[4];         // DeviceShare ScoringStrategy weights (KE_DSW_*), -1 = absent
-  // NodeResourcesFitPlus (fp_n resources: id, weight, MostAllocated bit) and ScarceResourceAvoidance
-  int32_t wp_fp, wp_sra;   // plugin weights (0 = not in the profile)
-  int32_t fp_n;
-  uint32_t fp_most;        // bit q: slot q scores MostAllocated
-  int32_t fp_id[4];
-  int64_t fp_w[4];
+  // ext slots q < xs_n (resource id xs_id[q]): NodeResourcesFitPlus scores the slots of fp_mask (weight fp_w[q],
+  // MostAllocated bit in fp_most), NodeResourcesFit scores those of fit_mask (weight fit_w[q]) and its Filter
+  // checks the scalar slots of fit_scalar; ScarceResourceAvoidance reads the id masks
+  int32_t wp_fp, wp_sra, wp_fit;  // plugin weights (0 = not in the profile)
+  int32_t xs_n;
+  uint32_t fp_mask, fp_most, fit_mask, fit_scalar;
+  int32_t xs_id[NUM_XS];
+  int64_t fp_w[NUM_XS];
+  int64_t fit_w[NUM_XS];
   uint64_t sra_mask;       // ScarceResourceAvoidanceArgs.Resources (resource ids)
 };
-// ext SoA (NodeResourcesFitPlus / ScarceResourceAvoidance): XF_ALLOC + q / XF_REQ + q = NodeInfo.Allocatable /
-// (NonZero)Requested of FitPlus slot q, plus a uint64 mask per node of the resource ids with Allocatable > 0
-constexpr int XF_ALLOC = 0, XF_REQ = 4, NUM_XF = 8;
+// ext SoA: XF_ALLOC + q / XF_REQ + q = NodeInfo.Allocatable / what calculateResourceAllocatableRequest reads
+// (NonZeroRequested for cpu / memory, Requested for a scalar) of slot q; XF_PODS = AllowedPodNumber - len(Pods);
+// plus a uint64 mask per node of the resource ids with Allocatable > 0
+constexpr int XF_ALLOC = 0, XF_REQ = NUM_XS, XF_PODS = 2 * NUM_XS, NUM_XF = 2 * NUM_XS + 1;
 
-// Packed candidate key: higher is better.  (score+1) in the top 9 bits, inverted node index in the
-// low 23 bits, so max(key) == selectHost with ties resolved to the lowest node index.
-constexpr uint32_t KEY_IDX_BITS = 23;
+// Packed candidate key: higher is better.  (score+1) in the top 10 bits, inverted node index in the
+// low 22 bits, so max(key) == selectHost with ties resolved to the lowest node index.
+constexpr uint32_t KEY_IDX_BITS = 22;
 constexpr uint32_t KEY_IDX_MASK = (1u << KEY_IDX_BITS) - 1;
 constexpr int MAX_SHARD_NODES = (1 << KEY_IDX_BITS) - 1;
-constexpr int MAX_TOTAL_SCORE = 510;  // (score+1) must fit in 9 bits: Σ plugin weight * 100 <= 510
+constexpr int MAX_TOTAL_SCORE = 1022;  // (score+1) must fit in 10 bits: Σ plugin weight * 100 <= 1022
 constexpr int MAX_DS_RAW = 300;       // DeviceShare raw score: <= 100 per device type
 KE_HD inline uint32_t make_key(int32_t total, int32_t idx) {
   return total < 0 ? 0u : ((uint32_t)(total + 1) << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)idx);

@@ -344,7 +344,7 @@ class Evaluator:
                 "pipelined_batches": npipe.value, "enqueue_ms": ms4[4], "handoff_ms": ms4[5],
                 "rows_fetched": ms4[6], "rows_changed": ms4[7], "spec_failed_rounds": sf.value,
                 "resolve_prologue_ms": p.value, "resolve_replay_ms": r.value,
-                "resolve_phases_ms": dict(zip(["init", "cand_copy", "hash", "lookup", "rows", "replay"],
+                "resolve_phases_ms": dict(zip(["prologue", "spec_predict", "spec_reserve_eval", "spec_verify", "spec_later_rounds", "writeback"],
                                               ph.tolist()))}
 
     def bench_eval_kernel(self, pods, now_ns, iters):

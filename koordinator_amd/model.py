@@ -510,6 +510,8 @@ def make_node(allocatable=None, requested=None, raw_allocatable=None, amplificat
     n = abi.Node()
     allocatable = allocatable or {}
     n.allocatable[:] = [milli_value(allocatable.get("cpu", 0)), value(allocatable.get("memory", 0))]
+    if "pods" in allocatable:  # NodeInfo.Allocatable.AllowedPodNumber
+        n.allowed_pods = min(value(allocatable["pods"]), 2**31 - 1)
     n.raw_allocatable[:] = [abi.ABSENT, abi.ABSENT]
     for k, v in (raw_allocatable or {}).items():
         n.raw_allocatable[RESOURCE_INDEX[k]] = resource_value(k, v)

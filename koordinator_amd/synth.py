@@ -137,7 +137,10 @@ def make_cluster(n_nodes, seed, amplified_fraction=0.0, max_pods_per_node=20, ke
     asg["has_scheduled"] = 1
     asg["scheduled_transition_ns"] = T0 - 3600 * NS
     asg_ts = np.full(P0, T0 - 3600 * NS, np.int64)
-    # NodeInfo.Requested = Σ requests of the pods on the node (cpu/memory)
+    # NodeInfo.Requested = Σ requests of the pods on the node (cpu/memory); len(NodeInfo.Pods); kubelet's
+    # default max-pods as AllowedPodNumber (NodeResourcesFit's Filter)
+    nodes["pod_count"] = per_node
+    nodes["allowed_pods"] = 110
     np.add.at(nodes["requested"][:, 0], asg_nodes, asg["requests"][:, abi.RES_CPU])
     np.add.at(nodes["requested"][:, 1], asg_nodes, asg["requests"][:, abi.RES_MEMORY])
     # pod metrics (only nodes that have a NodeMetric)
@@ -756,6 +759,37 @@ def ext_config(cfg, w_fitplus=1, w_sra=1, fitplus=None, sra=("nvidia.com/gpu", "
         x.fitplus[q].id, x.fitplus[q].type, x.fitplus[q].weight = XRES[name], typ, w
     x.sra_resources = sum(1 << XRES[n] for n in sra)
     return cfg
+
+
+def fit_config(cfg, weight=1, filter=True, strategy=abi.STRATEGY_LEAST_ALLOCATED,
+               resources=(("cpu", 1), ("memory", 1), ("kubernetes.io/batch-cpu", 1), ("kubernetes.io/batch-memory", 1)),
+               scalars=("kubernetes.io/batch-cpu", "kubernetes.io/batch-memory", "ephemeral-storage", "nvidia.com/gpu",
+                        "example.com/scarce")):
+    """NodeResourcesFit as the shipped profile configures it (config/manager/scheduler-config.yaml:17-31: LeastAllocated
+    over cpu, memory, batch-cpu, batch-memory at weight 1) with its Filter over the synthetic scalar resources."""
+    f = cfg.fit
+    f.weight, f.filter, f.strategy = weight, int(filter), strategy
+    f.n_resources = len(resources)
+    for q, (name, w) in enumerate(resources):
+        f.resources[q].id, f.resources[q].weight = XRES[name], w
+    f.n_scalars = len(scalars)
+    for q, name in enumerate(scalars):
+        f.scalars[q] = XRES[name]
+    return cfg
+
+
+def add_fit_defaults(pods):
+    """calculatePodResourceRequest's 100m / 200Mi container defaults for pods whose containers request no cpu /
+    memory (one container): xres entries for ids 0 / 1 without a requested-name bit."""
+    for p in range(len(pods)):
+        n = int(pods["n_xres"][p])
+        have = set(pods["xres_id"][p, :n].tolist())
+        for rid, v in ((abi.XRES_CPU, 100), (abi.XRES_MEMORY, 200 * 2**20)):
+            if rid not in have and n < abi.MAX_POD_XRES:
+                pods["xres_id"][p, n], pods["xres_value"][p, n] = rid, v
+                n += 1
+        pods["n_xres"][p] = n
+    return pods
 
 
 def make_node_resources(cl, seed, gpu_fraction=0.3, scarce_fraction=0.15):

@@ -68,6 +68,7 @@ typedef struct or_node {
   ke_node_resource xres[KE_MAX_XRES];
   /* the reservation cache's NodeInfo restore for a pod that matches no reservation (or_reservations_load) */
   int64_t rv_req[KE_NRES], rv_nz[KE_NRES];
+  int32_t rv_pods; /* len(NodeInfo.Pods) delta of the restore: a matched reservation's reserve pod is removed */
   int deleted; /* Node informer delete: out of the snapshot (every other cache keeps its state) */
 } or_node;
 
@@ -2901,13 +2902,16 @@ static const ke_node_resource* node_xres(const or_node* nd, int32_t id);
 static int64_t or_non0(int k, int64_t v) { return v != 0 ? v : (k == KE_RES_CPU ? 100 : 200LL << 20); }
 static int or_resv_usable(const ke_reservation* r) { return r->available && !(r->allocate_once && r->allocated_pods > 0); }
 static void or_restore(or_cluster* c, const char* matched, int with_matched) {
-  for (int32_t i = 0; i < c->n; i++)
+  for (int32_t i = 0; i < c->n; i++) {
     for (int k = 0; k < KE_NRES; k++) c->nodes[i].rv_req[k] = c->nodes[i].rv_nz[k] = 0;
+    c->nodes[i].rv_pods = 0;
+  }
   for (int32_t i = 0; i < c->n_resv; i++) {
     const ke_reservation* r = &c->resv[i];
     if (!or_resv_usable(r)) continue;
     or_node* nd = &c->nodes[r->node];
     if (matched && matched[i]) {
+      if (with_matched) nd->rv_pods--; /* restoreMatchedReservation: NodeInfo.RemovePod(reservePod) */
       if (with_matched)
         for (int k = 0; k < KE_NRES; k++) {
           nd->rv_req[k] -= r->allocatable[k];
@@ -3251,6 +3255,53 @@ int64_t or_fitplus_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
   return node_score / weight_sum;
 }
 
+/* NodeResourcesFit (upstream kube-scheduler v1.28.7, pkg/scheduler/framework/plugins/noderesources; not in the
+ * reference tree, go.mod:60): PARITY UNPINNED -- restated from the published algorithm, no reference test vector.
+ * Filter (fit.go fitsRequest): len(NodeInfo.Pods) + 1 > AllowedPodNumber ("Too many pods"); a pod requesting
+ * nothing passes; cpu / memory requests > 0 above Allocatable - Requested; scalar requests > 0 above the scalar's
+ * Allocatable - Requested (the first insufficiency in that order; the scalars in args order).  Returns the reason,
+ * 0 = fits. */
+static int or_fit_filter(const or_cluster* c, const ke_pod* pod, int32_t node) {
+  const or_node* nd = &c->nodes[node];
+  if ((int64_t)nd->node.pod_count + nd->rv_pods + 1 > nd->node.allowed_pods) return KE_REASON_FIT_TOO_MANY_PODS;
+  for (int r = 0; r < KE_NRES; r++) {
+    const int64_t q = pod->requests[r];
+    if (q > 0 && q > nd->node.allocatable[r] - (nd->node.requested[r] + nd->rv_req[r]))
+      return r == KE_RES_CPU ? KE_REASON_FIT_INSUFFICIENT_CPU : KE_REASON_FIT_INSUFFICIENT_MEMORY;
+  }
+  for (int q = 0; q < c->cfg.fit.n_scalars; q++) {
+    const int32_t id = c->cfg.fit.scalars[q];
+    const int64_t v = pod_xres(pod, id);
+    const ke_node_resource* r = node_xres(nd, id);
+    if (v > 0 && v > (r ? r->allocatable : 0) - (r ? r->requested : 0)) return KE_REASON_FIT_INSUFFICIENT_SCALAR;
+  }
+  return 0;
+}
+
+/* NodeResourcesFit Score (resource_allocation.go score + calculateResourceAllocatableRequest, least_allocated.go /
+ * most_allocated.go): per configured resource, cpu / memory: (Allocatable, NonZeroRequested + the pod's request
+ * with the container defaults); a scalar the pod does not request: skipped; else (Allocatable, Requested +
+ * request); alloc 0: skipped; Σ weight·score / Σ weight, 0 for a zero weight sum. */
+static int64_t or_fit_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
+  const or_node* nd = &c->nodes[node];
+  const ke_fit_args* a = &c->cfg.fit;
+  int64_t node_score = 0, weight_sum = 0;
+  for (int q = 0; q < a->n_resources; q++) {
+    const int32_t id = a->resources[q].id;
+    const int64_t preq = pod_xres(pod, id);
+    if (id >= 2 && preq == 0) continue;
+    const ke_node_resource* r = node_xres(nd, id);
+    const int64_t alloc = r ? r->allocatable : 0;
+    if (alloc == 0) continue;
+    const int64_t rv = id == KE_RES_CPU || id == KE_RES_MEMORY ? nd->rv_nz[id] : 0;
+    const int64_t req = r->requested + rv + preq;
+    const int64_t rs = a->strategy == KE_STRATEGY_MOST_ALLOCATED ? fp_most(req, alloc) : fp_least(req, alloc);
+    node_score += rs * a->resources[q].weight;
+    weight_sum += a->resources[q].weight;
+  }
+  return weight_sum == 0 ? 0 : node_score / weight_sum;
+}
+
 /* ScarceResourceAvoidance Score (scarce_resource_avoidance.go:70-90): the node's allocatable names (> 0)
  * minus the pod's requested names (quotav1.Difference), intersected with args.Resources; resourceTypesScore
  * (:159-161). */
@@ -3456,7 +3507,7 @@ int or_pod_unassign(or_cluster* c, int32_t node, int64_t uid) {
 typedef struct eval_out {
   uint8_t status, reason;
   int16_t la, numa, ds, total; /* ds: DeviceShare.Score before NormalizeScore */
-  int16_t fp, sra;              /* NodeResourcesFitPlus, ScarceResourceAvoidance */
+  int16_t fp, sra, fit;         /* NodeResourcesFitPlus, ScarceResourceAvoidance, NodeResourcesFit */
 } eval_out;
 
 /* RunFilterPlugins in profile order LoadAware, NodeNUMAResource, DeviceShare
@@ -3467,7 +3518,7 @@ static void eval_pair(const or_cluster* c, const ke_pod* pod, int32_t node, int6
   if (c->nodes[node].deleted) { /* not in the snapshot: evaluated nowhere (KE_CODE_ERROR, as the product) */
     o->status = KE_CODE_ERROR;
     o->reason = 0;
-    o->la = o->numa = o->ds = o->fp = o->sra = 0;
+    o->la = o->numa = o->ds = o->fp = o->sra = o->fit = 0;
     o->total = -1;
     return;
   }
@@ -3484,14 +3535,18 @@ static void eval_pair(const or_cluster* c, const ke_pod* pod, int32_t node, int6
     code = d.status;
     reason = d.status_reason ? d.status_reason : KE_REASON_DS_INVALID_REQUEST;
   }
+  /* NodeResourcesFit's Filter: a default plugin, ahead of the profile's own Filters */
+  if (code == KE_CODE_SUCCESS && c->cfg.fit.filter && (reason = or_fit_filter(c, pod, node)) != 0)
+    code = KE_CODE_UNSCHEDULABLE;
   if (code == KE_CODE_SUCCESS) code = or_la_filter(c, pod, node, now, &reason);
   if (code == KE_CODE_SUCCESS) code = or_numa_filter(c, pod, node, &reason);
   if (code == KE_CODE_SUCCESS) code = or_ds_filter(c, pod, node, &reason);
   o->status = (uint8_t)code;
   o->reason = (uint8_t)reason;
-  o->la = o->numa = o->ds = o->fp = o->sra = 0;
+  o->la = o->numa = o->ds = o->fp = o->sra = o->fit = 0;
   o->total = -1;
   if (code != KE_CODE_SUCCESS) return;
+  if (c->cfg.fit.weight) o->fit = (int16_t)or_fit_score(c, pod, node);
   if (c->cfg.ext.weight_fitplus) o->fp = (int16_t)or_fitplus_score(c, pod, node);
   if (c->cfg.ext.weight_sra) o->sra = (int16_t)or_sra_score(c, pod, node);
   o->la = (int16_t)or_la_score(c, pod, node, now);
@@ -3511,7 +3566,7 @@ static void normalize_and_total(const or_cluster* c, eval_out* o, int64_t n) {
     const int64_t ds = mx > 0 ? MAX_NODE_SCORE * o[i].ds / mx : o[i].ds;
     o[i].total = (int16_t)(c->cfg.weight_loadaware * o[i].la + c->cfg.weight_numa * o[i].numa +
                            c->cfg.weight_deviceshare * ds + c->cfg.ext.weight_fitplus * o[i].fp +
-                           c->cfg.ext.weight_sra * o[i].sra);
+                           c->cfg.ext.weight_sra * o[i].sra + c->cfg.fit.weight * o[i].fit);
   }
 }
 
@@ -3857,6 +3912,7 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
       mask = ds_reserve_on(c, &pods[p], b, da, (int8_t(*)[KE_MAX_MINORS])(c->last_vf + (int64_t)p * 2 * KE_MAX_MINORS));
       c->nodes[b].node.requested[KE_RES_CPU] += pods[p].requests[KE_RES_CPU];
       c->nodes[b].node.requested[KE_RES_MEMORY] += pods[p].requests[KE_RES_MEMORY];
+      c->nodes[b].node.pod_count++; /* NodeInfo.AddPod */
       /* NodeInfo (NonZero)Requested of every resource the pod requests (NodeResourcesFitPlus reads them) */
       or_node* nb = &c->nodes[b];
       for (int32_t e = 0; e < pods[p].n_xres; e++) {
@@ -3932,7 +3988,8 @@ int or_pod_release(or_cluster* c, const ke_pod* pod, const ke_pod_allocation* a,
     or_pod_unassign(c, node, pod->uid);
     n->node.requested[KE_RES_CPU] -= pod->requests[KE_RES_CPU];
     n->node.requested[KE_RES_MEMORY] -= pod->requests[KE_RES_MEMORY];
-    if (c->cfg.ext.weight_fitplus > 0 || c->cfg.ext.weight_sra > 0)
+    n->node.pod_count--; /* NodeInfo.RemovePod */
+    if (c->cfg.ext.weight_fitplus > 0 || c->cfg.ext.weight_sra > 0 || c->cfg.fit.weight > 0 || c->cfg.fit.filter)
       for (int32_t e = 0; e < pod->n_xres; e++) {
         ke_node_resource* r = (ke_node_resource*)node_xres(n, pod->xres_id[e]);
         if (r) r->requested -= pod->xres_value[e];

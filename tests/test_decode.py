@@ -149,7 +149,8 @@ def test_node_thresholds_ratio_raw_labels(lib):
                     "node.koordinator.sh/cpu-bind-policy": "FullPCPUsOnly",
                     "node.koordinator.sh/numa-allocate-strategy": "MostAllocated"})
     got = decode.decode_node(doc)
-    want = model.make_node(allocatable={"cpu": "96", "memory": "512Gi"}, raw_allocatable={"cpu": "64", "memory": "500Gi"},
+    want = model.make_node(allocatable={"cpu": "96", "memory": "512Gi", "pods": "110"},
+                           raw_allocatable={"cpu": "64", "memory": "500Gi"},
                            amplification_ratio=1.5, custom_usage_thresholds={"cpu": 60, "memory": 80},
                            custom_prod_usage_thresholds={"cpu": 50},
                            custom_aggregated=dict(thresholds={"memory": 70}, type="p95", duration_ns=300 * 10**9))

@@ -74,9 +74,11 @@ def test_ext_config_validation(lib):
     cfg = synth.ext_config(synth.config(4))
     ev = Evaluator(cfg)
     ev.close()
-    bad = synth.ext_config(synth.config(4), w_fitplus=3)  # (1 + 1 + 1 + 3 + 1) * 100 > 510
+    bad = synth.ext_config(synth.config(4), w_fitplus=8)  # (1 + 1 + 1 + 8 + 1) * 100 > 1022 (10-bit key score)
     with pytest.raises(Exception, match="weights"):
         Evaluator(bad)
+    # the shipped profile's six Score plugins at weight 1 (600) fit the widened key
+    Evaluator(synth.fit_config(synth.ext_config(synth.config(4)))).close()
     bad = synth.ext_config(synth.config(4))
     bad.ext.fitplus[1].id = bad.ext.fitplus[0].id
     with pytest.raises(Exception, match="twice"):
