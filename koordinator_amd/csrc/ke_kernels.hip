@@ -2156,16 +2156,29 @@ __device__ __forceinline__ void numa_reserve(const SoA& s, int64_t i, uint32_t n
 // slots (KArgs::xs_id): xa / xr = the node's Allocatable / (NonZero)Requested of slot q, xm = its ids with
 // Allocatable > 0.
 __device__ __forceinline__ int64_t mul100_wrap(int64_t x) { return (int64_t)((uint64_t)x * 100u); }
-__device__ __forceinline__ int32_t ext_score_vals(uint64_t xm, const int64_t (&xa)[NUM_XS], const int64_t (&xr)[NUM_XS],
-                                                  const DevPod& p, const KArgs& k) {
+// `get(q, a, r)` yields slot q's Allocatable / (NonZero)Requested: from registers (NodeFast: unrolled, constant
+// indices) or straight from the SoA one slot at a time (ROLLED: a loop, so the row-path kernels -- whose registers
+// the DeviceShare / NUMA evaluation already fills -- keep one slot's int64 division live, not eight)
+template <bool ROLLED, typename F>
+__device__ __forceinline__ void for_slots(F&& f) {
+  if constexpr (ROLLED) {
+#pragma unroll 1
+    for (int q = 0; q < NUM_XS; q++) f(q);
+  } else {
+#pragma unroll
+    for (int q = 0; q < NUM_XS; q++) f(q);
+  }
+}
+template <bool ROLLED = false, typename G>
+__device__ __forceinline__ int32_t ext_score_gen(uint64_t xm, G&& get, const DevPod& p, const KArgs& k) {
   int32_t t = 0;
   if (k.wp_fp) {  // resourceScorer (node_resource_fit_plus_utils.go:57-89) over the pod's requested names
     int64_t ns = 0, ws = 0;
-#pragma unroll
-    for (int q = 0; q < NUM_XS; q++) {
-      if (!((k.fp_mask >> q) & 1) || !((p.xmask >> k.xs_id[q]) & 1)) continue;
-      const int64_t cap = xa[q];
-      int64_t req = xr[q] + p.xreq[q];
+    for_slots<ROLLED>([&](int q) {
+      if (!((k.fp_mask >> q) & 1) || !((p.xmask >> k.xs_id[q]) & 1)) return;
+      int64_t cap, req;
+      get(q, cap, req);
+      req += p.xreq[q];
       int64_t sc = 0;
       if ((k.fp_most >> q) & 1) {  // mostRequestedScore (:35-44)
         if (req > cap) req = cap;
@@ -2175,7 +2188,7 @@ __device__ __forceinline__ int32_t ext_score_vals(uint64_t xm, const int64_t (&x
       }
       ns += sc * k.fp_w[q];
       ws += k.fp_w[q];
-    }
+    });
     t += k.wp_fp * (int32_t)(ws == 0 ? 100 : ns / ws);
   }
   if (k.wp_sra) {  // scarce_resource_avoidance.go:70-90,159-161
@@ -2186,14 +2199,14 @@ __device__ __forceinline__ int32_t ext_score_vals(uint64_t xm, const int64_t (&x
   if (k.wp_fit) {  // NodeResourcesFit Score (k8s v1.28.7 resource_allocation.go score, least/most_allocated.go)
     int64_t ns = 0, ws = 0;
     const bool most = (k.flags & AF_FIT_MOST) != 0;
-#pragma unroll
-    for (int q = 0; q < NUM_XS; q++) {
-      if (!((k.fit_mask >> q) & 1)) continue;
+    for_slots<ROLLED>([&](int q) {
+      if (!((k.fit_mask >> q) & 1)) return;
       const int64_t preq = p.xreq[q];
-      if (k.xs_id[q] >= 2 && preq == 0) continue;  // a scalar the pod does not request: (0, 0)
-      const int64_t cap = xa[q];
-      if (cap == 0) continue;
-      int64_t req = xr[q] + preq;
+      if (k.xs_id[q] >= 2 && preq == 0) return;  // a scalar the pod does not request: (0, 0)
+      int64_t cap, req;
+      get(q, cap, req);
+      if (cap == 0) return;
+      req += preq;
       int64_t sc;
       if (most) {
         if (req > cap) req = cap;
@@ -2203,47 +2216,54 @@ __device__ __forceinline__ int32_t ext_score_vals(uint64_t xm, const int64_t (&x
       }
       ns += sc * k.fit_w[q];
       ws += k.fit_w[q];
-    }
+    });
     t += k.wp_fit * (int32_t)(ws == 0 ? 0 : ns / ws);
   }
   return t;
 }
+__device__ __forceinline__ int32_t ext_score_vals(uint64_t xm, const int64_t (&xa)[NUM_XS], const int64_t (&xr)[NUM_XS],
+                                                  const DevPod& p, const KArgs& k) {
+  return ext_score_gen(xm, [&](int q, int64_t& a, int64_t& r) { a = xa[q], r = xr[q]; }, p, k);
+}
 // NodeResourcesFit Filter (k8s v1.28.7 fit.go fitsRequest): the pod room, then cpu / memory requests > 0 against
 // Allocatable - Requested (the row's NodeInfo), then the scalar slots; returns the reason (0 = fits)
-__device__ __forceinline__ uint8_t fit_filter(int64_t room, const int64_t (&xa)[NUM_XS], const int64_t (&xr)[NUM_XS],
-                                              bool cpu_over, bool mem_over, const DevPod& p, const KArgs& k) {
+template <bool ROLLED = false, typename G>
+__device__ __forceinline__ uint8_t fit_filter_gen(int64_t room, G&& get, bool cpu_over, bool mem_over, const DevPod& p,
+                                                  const KArgs& k) {
   if (room < 1) return KE_REASON_FIT_TOO_MANY_PODS;
   if (cpu_over) return KE_REASON_FIT_INSUFFICIENT_CPU;
   if (mem_over) return KE_REASON_FIT_INSUFFICIENT_MEMORY;
   bool sc = false;
-#pragma unroll
-  for (int q = 0; q < NUM_XS; q++)
-    sc |= ((k.fit_scalar >> q) & 1) && p.xreq[q] > 0 && p.xreq[q] > xa[q] - xr[q];
+  for_slots<ROLLED>([&](int q) {
+    if (!((k.fit_scalar >> q) & 1) || p.xreq[q] <= 0) return;
+    int64_t a, r;
+    get(q, a, r);
+    sc |= p.xreq[q] > a - r;
+  });
   return sc ? KE_REASON_FIT_INSUFFICIENT_SCALAR : 0;
 }
-// the node's ext words from the SoA (plain loads: no kernel writes them while this one runs)
-__device__ __forceinline__ void ext_words(const SoA& s, int64_t i, const KArgs& k, int64_t (&xa)[NUM_XS],
-                                          int64_t (&xr)[NUM_XS], int64_t& room) {
-#pragma unroll
-  for (int q = 0; q < NUM_XS; q++) {
-    xa[q] = q < k.xs_n ? s.xf[(XF_ALLOC + q) * s.stride + i] : 0;
-    xr[q] = q < k.xs_n ? s.xf[(XF_REQ + q) * s.stride + i] : 0;
-  }
-  room = s.xf[XF_PODS * s.stride + i];
+__device__ __forceinline__ uint8_t fit_filter(int64_t room, const int64_t (&xa)[NUM_XS], const int64_t (&xr)[NUM_XS],
+                                              bool cpu_over, bool mem_over, const DevPod& p, const KArgs& k) {
+  return fit_filter_gen(room, [&](int q, int64_t& a, int64_t& r) { a = xa[q], r = xr[q]; }, cpu_over, mem_over, p, k);
 }
+// slot q's words from the SoA (plain loads: no kernel writes them while this one runs)
+struct ExtSoaGet {
+  const SoA& s;
+  int64_t i;
+  __device__ __forceinline__ void operator()(int q, int64_t& a, int64_t& r) const {
+    a = s.xf[(XF_ALLOC + q) * s.stride + i];
+    r = s.xf[(XF_REQ + q) * s.stride + i];
+  }
+};
 // NodeResourcesFit's Filter reason on a row (eval_pair / lite_total)
 __device__ __forceinline__ uint8_t fit_filter_row(const SoA& s, int64_t i, const NodeRegs& n, const DevPod& p,
                                                   const KArgs& k) {
-  int64_t xa[NUM_XS], xr[NUM_XS], room;
-  ext_words(s, i, k, xa, xr, room);
   const bool co = p.req[0] > 0 && p.req[0] > n.nalloc[0] - n.nreq[0];
   const bool mo = p.req[1] > 0 && p.req[1] > n.nalloc[1] - n.nreq[1];
-  return fit_filter(room, xa, xr, co, mo, p, k);
+  return fit_filter_gen<true>(s.xf[XF_PODS * s.stride + i], ExtSoaGet{s, i}, co, mo, p, k);
 }
 __device__ __forceinline__ int32_t ext_score(const SoA& s, int64_t i, const DevPod& p, const KArgs& k) {
-  int64_t xa[NUM_XS], xr[NUM_XS], room;
-  ext_words(s, i, k, xa, xr, room);
-  return ext_score_vals(s.xm[i], xa, xr, p, k);
+  return ext_score_gen<true>(s.xm[i], ExtSoaGet{s, i}, p, k);
 }
 // Reserve: NodeInfo (NonZero)Requested += the pod's requests of the slots' resources, one pod more
 __device__ __forceinline__ void ext_reserve(const SoA& s, int64_t i, const DevPod& p, const KArgs& k) {
