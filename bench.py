@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="host time of each CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true", help="one-stream schedule (A/B of the pipelined one)")
+    ap.add_argument("--pipeline-fixup", action="store_true",
+                    help="pipelined with exact lists from k_fixup (ke_set_pipeline 2, the round-3 schedule)")
     ap.add_argument("--profile-every", type=int, default=8, help="HIP-event-sample every n-th batch (0 = off)")
     ap.add_argument("--stream-nodes", type=int, default=4_000_000,
                     help="B=1 streaming sweep size (N*row > 512 MB, past the 256 MB Infinity Cache); 0 = skip")
@@ -269,7 +271,7 @@ def main():
     lo, hi = ev.shard_range()
     ev.eval(pods[:0], synth.T0)  # derive + upload every node row: state resident in HBM
     ev.set_profiling(a.profile_every)
-    ev.set_pipeline(not a.no_pipeline)
+    ev.set_pipeline(False if a.no_pipeline else ("fixup" if a.pipeline_fixup else True))
     lat, plat, evm, sel, samples, rsplit, npipe, hs, kss = [], [], [], [], 0, [], 0, [], []
     placed = 0
     n_batches = 0

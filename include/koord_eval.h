@@ -793,7 +793,8 @@ int ke_reservations_get(ke_ctx* ctx, int32_t n, ke_reservation* out);
  * Refused (KE_ERR_UNSUPPORTED, by ke_schedule's argument checks before any pod of the call is scheduled): such a
  * pod with DeviceShare requests, cpuset binding or a NUMA topology policy, a usable matched reservation on a node
  * with a NUMA topology policy, a sharded context; ke_eval of such a pod.  NodeInfo's pod-count check of fitsNode
- * is not modelled (allowedPodNumber taken as not binding). */
+ * is not modelled (allowedPodNumber taken as not binding).  The lists are consumed by the next ke_schedule call,
+ * a refused one included. */
 int ke_pod_reservations(ke_ctx* ctx, int32_t n_pods, const int32_t* offsets, const int32_t* ids);
 /* NodeInfo.Requested / NonZeroRequested (MilliCPU, Memory) of `node` as the plugins see it for a pod that
  * matches no reservation (after the restore above and the Reserves of past ke_schedule calls). */
@@ -1054,9 +1055,11 @@ int ke_last_kernel_stats(ke_ctx* ctx, double* eval_ms, double* select_ms, double
  * -> start of the next one's), replay records fetched per batch (best unchanged candidates), rows changed
  * per batch}, the number of event samples, and how many batches ran pipelined. */
 int ke_last_kernel_stats_ex(ke_ctx* ctx, double* v8, int32_t* samples, int32_t* pipelined_batches);
-/* Pipelined schedule (default on): batch b's eval + select overlap batch b-1's Reserve replay on a
- * second stream.  Off = one stream, every batch waits for the previous Reserve.  The
- * placements are identical either way. */
+/* Pipelined schedule (default 1): batch b's eval + select overlap batch b-1's Reserve replay on a
+ * second stream; the replay takes the stale candidate lists with batch b-1's changed nodes as
+ * slots.  2 = pipelined with the lists made exact by a fixup kernel first (the round-3 schedule; ElasticQuota
+ * runs always take it).  0 = one stream, every batch waits for the previous Reserve.  The placements are
+ * identical in every mode. */
 int ke_set_pipeline(ke_ctx* ctx, int32_t on);
 /* Host wall milliseconds of the last ke_schedule by phase: argument checks, row refresh, pod upload,
  * launch setup, enqueue, wait for the device, statistics readback, host mirror of the Reserves. */

@@ -666,19 +666,25 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
   using clk = std::chrono::steady_clock;
   auto tp = clk::now();
   ctx->c.call_entry = tp;  // every pod of the call is dequeued now (ke_last_pod_latencies)
+  // the staged ke_pod_reservations lists belong to this call, refused or not
+  auto refuse = [&](int r) {
+    ctx->c.match_off.clear();
+    ctx->c.match_ids.clear();
+    return r;
+  };
   int rc = check_pods(pods, n_pods, &ctx->c, true);
-  if (rc) return rc;
+  if (rc) return refuse(rc);
   rc = check_numa_deviceshare(ctx, pods, n_pods);
-  if (rc) return rc;
+  if (rc) return refuse(rc);
   rc = check_cpuset(ctx, pods, n_pods);
-  if (rc) return rc;
+  if (rc) return refuse(rc);
   for (int32_t p = 0; p < n_pods; p++)
     if (pods[p].quota < 0 || pods[p].quota > (int32_t)ctx->c.quotas.size())
-      return fail(KE_ERR_INVALID, "ke_pod.quota outside the loaded ElasticQuota tree");
+      return refuse(fail(KE_ERR_INVALID, "ke_pod.quota outside the loaded ElasticQuota tree"));
   rc = check_matches(ctx->c, pods, n_pods);
-  if (rc) return rc;
+  if (rc) return refuse(rc);
   rc = require_device(ctx);
-  if (rc) return rc;
+  if (rc) return refuse(rc);
   ctx->c.host_ms[0] = std::chrono::duration<double, std::milli>(clk::now() - tp).count();
   Context& c = ctx->c;
   // ElasticQuota: a Reserve into the system / default quota (limit_is_max) with runtime quota on

@@ -3585,6 +3585,11 @@ constexpr int SEL_COPIES = 8;   // histogram copies per wave (pass 2)
 
 // per-wave node segment of k_select over [lo, hi): a multiple of 512 (one 16-B load per lane per step)
 __host__ __device__ inline int select_seg(int lo, int hi) { return ((hi - lo + SELECT_WAVES - 1) / SELECT_WAVES + 511) & ~511; }
+// workgroups per pod of a plain batch's split k_select over n nodes: >= 256 workgroups in all, parts of
+// >= 4096 nodes, at most MAX_WORLD (k_merge's fan-in)
+inline int select_parts(int64_t n, int bp) {
+  return std::max(1, std::min({8, (255 + bp) / bp, (int)(n / 4096)}));
+}
 // node part of one of `parts` workgroups of a split k_select (512-aligned, like the shard ranges)
 __host__ __device__ inline int select_part(int lo, int hi, int parts) { return ((hi - lo + parts - 1) / parts + 511) & ~511; }
 
@@ -3638,13 +3643,31 @@ __device__ __forceinline__ uint32_t max_halves(uint32_t w) { return max(w & 0xFF
 // gridDim.y > 1 (plain batches): the pod's nodes are split into gridDim.y 512-aligned parts, one workgroup
 // each, every part's top-k_j list in its own block of a gather buffer (`ystride` words apart) for k_merge --
 // the per-shard lists of the node-sharded path, on one GPU (a batch of 64 pods then fills every CU).
+// L = list length (KMAX, or KSTALE for the pipelined schedule's stale lists); outputs use stride L.
+constexpr int KSTALE = 2 * KMAX;  // stale-snapshot list length of the pipelined schedule
+constexpr int gath_words(int L) { return MAX_BATCH * L + MAX_BATCH; }
+constexpr int GATH_WORDS_MAX = MAX_BATCH * KSTALE + MAX_BATCH;
+constexpr int MAX_WORLD = 8;
+static_assert(MAX_WORLD == 8, "select_parts caps the parts at 8");
+constexpr int MERGE_BLOCK = MAX_WORLD * KSTALE;
+
+template <bool SC1>
+__device__ __forceinline__ void merge_lists(const uint32_t* __restrict__ gath, int64_t gw, int world, int L, int kext,
+                                            int j, uint4* s_k, uint32_t* __restrict__ cand,
+                                            int32_t* __restrict__ cand_cnt);
+static_assert(SELECT_BLOCK == MERGE_BLOCK, "the last part's workgroup of a split k_select merges");
+
 template <bool DS, int RC>
 __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restrict__ scores, int64_t score_stride,
                                                          int lo, int hi, uint32_t* __restrict__ cand,
                                                          int32_t* __restrict__ cand_cnt,
                                                          const uint16_t* __restrict__ dsraw,
                                                          uint32_t* __restrict__ dsmax1, int32_t wds, int kext,
-                                                         int ostride, int64_t ystride) {
+                                                         int ostride, int64_t ystride,
+                                                         uint32_t* __restrict__ mcand = nullptr,
+                                                         int32_t* __restrict__ mcnt = nullptr,
+                                                         int32_t* __restrict__ parts_done = nullptr) {
+  uint32_t* const gath = cand;
   if (!DS && gridDim.y > 1) {
     const int part = select_part(lo, hi, gridDim.y);
     lo = min(hi, lo + (int)blockIdx.y * part);
@@ -3664,7 +3687,7 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
   }
   // per wave SEL_COPIES histograms (lane & 7 picks one), rows padded to 65 words: lanes of one LDS lane group
   // that count the same score go to different copies in different banks instead of one address
-  __shared__ int32_t s_hist[SELECT_WAVES][SEL_COPIES][SEL_WINDOW + 1];
+  __shared__ __attribute__((aligned(16))) int32_t s_hist[SELECT_WAVES][SEL_COPIES][SEL_WINDOW + 1];
   __shared__ int32_t s_red[2][SELECT_WAVES];
   __shared__ int32_t s_thr[2];
   __shared__ int32_t s_tie[SELECT_WAVES];
@@ -3882,14 +3905,37 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
       int pos = wbase + pre;
 #pragma unroll
       for (int t = 0; t < 8; t++)
-        if (selm & (1u << t)) out[pos++] = (v[t] << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)(i0 + t));
+        if (selm & (1u << t)) {
+          const uint32_t key = (v[t] << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)(i0 + t));
+          if (mcand) st_sc1(out + pos, key);  // (fused merge: read by another workgroup of this launch)
+          else out[pos] = key;
+          pos++;
+        }
     }
   });
   __syncthreads();
   if (threadIdx.x == 0) {
-    cand_cnt[j] = s_out;
+    if (mcand) st_sc1(cand_cnt + j, (int32_t)s_out);
+    else cand_cnt[j] = s_out;
     if (DS) dsmax1[DSB_CNT + j] = (uint32_t)s_dscnt;
   }
+  if (DS || !mcand) return;
+  // split select with the merge fused: the workgroup finishing pod j's last part merges the parts (k_merge's
+  // work without its launch).  The lists went out as sc1 stores; every wave drains them before the barrier,
+  // then one relaxed count (no agent-scope fence: on this part it would write back the XCD's L2,
+  // cdna_hip_programming.md Guideline 16); the merging workgroup reads them with sc1 loads.
+  drain_stores();
+  __syncthreads();
+  __shared__ int32_t s_last;
+  if (threadIdx.x == 0) {
+    const int prev = __hip_atomic_fetch_add(parts_done + j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == (int)gridDim.y - 1;
+    if (s_last) parts_done[j] = 0;  // the next batch's count (stream order; no other workgroup touches it now)
+  }
+  __syncthreads();
+  if (!s_last) return;
+  merge_lists<true>(gath, ystride, (int)gridDim.y, ostride, kext, j, reinterpret_cast<uint4*>(&s_hist[0][0][0]),
+                    mcand, mcnt);
 }
 
 // --- node-sharded batches: merge of the per-shard candidate lists ---------------------------------
@@ -3898,22 +3944,20 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
 // top-k_j of pod j is the top-k_j of the union of the per-shard top-k_j lists (each global top-k_j node
 // is also top-k_j inside its own shard).  Keys are unique (they embed the node index), so a key's
 // rank in the union is the number of larger keys; ranks < k_j are written in order.
-// L = list length (KMAX, or KSTALE for the pipelined schedule's stale lists); outputs use stride L.
-constexpr int KSTALE = 2 * KMAX;  // stale-snapshot list length of the pipelined schedule
-constexpr int gath_words(int L) { return MAX_BATCH * L + MAX_BATCH; }
-constexpr int GATH_WORDS_MAX = MAX_BATCH * KSTALE + MAX_BATCH;
-constexpr int MAX_WORLD = 8;
-constexpr int MERGE_BLOCK = MAX_WORLD * KSTALE;
 
-__global__ __launch_bounds__(MERGE_BLOCK) void k_merge(const uint32_t* __restrict__ gath, int world, int L, int kext,
-                                                       uint32_t* __restrict__ cand, int32_t* __restrict__ cand_cnt) {
-  __shared__ uint4 s_k[MERGE_BLOCK / 4];
-  const int j = blockIdx.x, k = min(j + 1, KMAX) + kext;
+// pod j's merged list from `world` blocks `gw` words apart (all MERGE_BLOCK threads of the workgroup; s_k:
+// MERGE_BLOCK keys of LDS).  SC1: the blocks were written by other workgroups of the running launch.
+template <bool SC1>
+__device__ __forceinline__ void merge_lists(const uint32_t* __restrict__ gath, int64_t gw, int world, int L, int kext,
+                                            int j, uint4* s_k, uint32_t* __restrict__ cand,
+                                            int32_t* __restrict__ cand_cnt) {
+  const int k = min(j + 1, KMAX) + kext;
   const int t = threadIdx.x, r = t / L, c = t % L;
   uint32_t key = 0;
   if (r < world) {
-    const uint32_t* blk = gath + (int64_t)r * gath_words(L);
-    if (c < (int)blk[MAX_BATCH * L + j]) key = blk[j * L + c];
+    const uint32_t* blk = gath + (int64_t)r * gw;
+    const int n = SC1 ? ld_sc1(reinterpret_cast<const int32_t*>(blk + MAX_BATCH * L + j)) : (int)blk[MAX_BATCH * L + j];
+    if (c < n) key = SC1 ? (uint32_t)ld_sc1(reinterpret_cast<const int32_t*>(blk + j * L + c)) : blk[j * L + c];
   }
   reinterpret_cast<uint32_t*>(s_k)[t] = key;
   const int nz = __syncthreads_count(key != 0u);
@@ -3927,6 +3971,12 @@ __global__ __launch_bounds__(MERGE_BLOCK) void k_merge(const uint32_t* __restric
     if (rank < k) cand[j * L + rank] = key;
   }
   if (t == 0) cand_cnt[j] = min(nz, k);
+}
+
+__global__ __launch_bounds__(MERGE_BLOCK) void k_merge(const uint32_t* __restrict__ gath, int world, int L, int kext,
+                                                       uint32_t* __restrict__ cand, int32_t* __restrict__ cand_cnt) {
+  __shared__ uint4 s_k[MERGE_BLOCK / 4];
+  merge_lists<false>(gath, gath_words(L), world, L, kext, (int)blockIdx.x, s_k, cand, cand_cnt);
 }
 
 // --- pipelined schedule: exact candidate lists from a stale snapshot ------------------------------
@@ -4036,6 +4086,23 @@ __global__ __launch_bounds__(FIX_BLOCK) void k_fixup(SoA s, const DevPod* __rest
   }
 }
 
+// Pipelined schedule without k_fixup (k_resolve_run's stale-list mode): publish batch q's lists to the
+// running Reserve kernel (ready = its pods; the select / merge kernels before this one on the same stream
+// wrote them), then hold the eval stream until batch q-1's Reserve is done (done_wait), so that batch q+1's
+// eval sees every Reserve of batches <= q-1 -- its stale keys differ from the exact ones only on the nodes
+// batch q changes -- and its lists may reuse batch q-1's half of the double buffer.
+__global__ void k_handoff(int32_t* __restrict__ ready, int32_t n, const int32_t* __restrict__ done_wait,
+                          int32_t* __restrict__ err, uint64_t* __restrict__ fstamp) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  __hip_atomic_store(ready, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (fstamp) {
+    fstamp[0] = t0;
+    fstamp[1] = t0 + 1;
+  }
+  if (done_wait) (void)wait_at_least(done_wait, 1, err);  // a timeout sets *err: the host discards the queue
+}
+
 // --- resolve: one wavefront replays the batch sequentially -------------------------------------
 // one node row straight from the SoA, past this CU's L1 (rows this workgroup patched earlier)
 __device__ __forceinline__ void load_row_sc1(const SoA& s, int64_t i, Row& r) {
@@ -4046,10 +4113,10 @@ __device__ __forceinline__ void load_row_sc1(const SoA& s, int64_t i, Row& r) {
   r.pad = 0;
 }
 
-// Changed-node set of the batch being replayed: a bitmap over node ids, in LDS for ids < 2^20 (else a
+// Changed-node set of the batch being replayed: a bitmap over node ids, in LDS for ids < 917,504 (else a
 // zeroed device bitmap in global memory, sc1-accessed).  Only the replay wave touches it; the bits of a
 // batch are cleared when it ends, so it is zero between batches.
-constexpr int CHG_LDS_WORDS = 32768;
+constexpr int CHG_LDS_WORDS = 28672;  // node ids < 917,504 (else the global bitmap)
 struct ChgSet {
   uint32_t* lds;
   uint32_t* glb;  // non-null: node ids beyond the LDS bitmap
@@ -4061,6 +4128,22 @@ __device__ __forceinline__ bool chg_test(const ChgSet& c, int node) {
 __device__ __forceinline__ void chg_set(const ChgSet& c, int node) {  // one lane
   if (c.glb) __hip_atomic_fetch_or(c.glb + (node >> 5), 1u << (node & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else c.lds[node >> 5] |= 1u << (node & 31);
+}
+// several lanes at once (words may be shared)
+__device__ __forceinline__ void chg_set_atomic(const ChgSet& c, int node) {
+  if (c.glb) __hip_atomic_fetch_or(c.glb + (node >> 5), 1u << (node & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else __hip_atomic_fetch_or(c.lds + (node >> 5), 1u << (node & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// compile-time placement of the bitmap (the speculative prediction loop: no branch, no vmcnt wait on the
+// LDS path); GLB: one lane's atomic is drained before later loads of other lanes may depend on it
+template <bool GLB>
+__device__ __forceinline__ void chg_or(const ChgSet& c, int node) {
+  if (GLB) {
+    __hip_atomic_fetch_or(c.glb + (node >> 5), 1u << (node & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    drain_stores();
+  } else {
+    __hip_atomic_fetch_or(c.lds + (node >> 5), 1u << (node & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
 }
 // at the end of a batch every set bit belongs to a changed node: each changed lane zeroes its word
 // (lanes sharing a word all store zero)
@@ -4177,10 +4260,12 @@ struct SpecLds {
   uint32_t xkey[MAX_BATCH];  // its snapshot candidate key (the best unchanged candidate), 0 = none
   uint32_t mrow[MAX_BATCH];  // max key of pod j over the nodes pods < j took, in their current state
   int32_t jf;                // first pod of the round whose prediction failed (end of round: none)
+  uint32_t tmx[MAX_BATCH];   // stale lists: max key of pod j over the previous batch's changed nodes T ...
+  int32_t tver[MAX_BATCH];   // ... valid while no pod of the batch reserved a T node since (-1: never computed)
 };
 
-struct ResLds {
-  uint32_t cand[MAX_BATCH * KMAX];
+struct ResLdsCore {
+  uint32_t cand[MAX_BATCH * KSTALE];  // exact lists at stride KMAX, or the pipelined schedule's stale lists at KSTALE
   DevPod pod[MAX_BATCH];
   double pd[MAX_BATCH][4];  // the pod's estimate and requests (cpu, memory) as doubles
   int32_t cnt[MAX_BATCH];
@@ -4189,6 +4274,14 @@ struct ResLds {
   SpecLds sp;
   uint32_t chg[CHG_LDS_WORDS];
 };
+// The Reserve kernels take the CU's whole LDS (160 KB, less 64 B for a kernel's own words): no workgroup of
+// the eval / select kernels (all of which use LDS) is co-resident, so the latency-bound replay waves issue on
+// SIMDs of their own instead of queueing behind a concurrent eval's FP64 instructions (pipelined schedule).
+constexpr int CU_LDS_BYTES = 163840;
+struct ResLds : ResLdsCore {
+  uint8_t cu_fill[CU_LDS_BYTES - 64 - sizeof(ResLdsCore)];
+};
+static_assert(sizeof(ResLds) == CU_LDS_BYTES - 64, "ResLds fills the CU's LDS");
 
 // a changed-set bit that a failed prediction set (several lanes may share a word)
 __device__ __forceinline__ void chg_unset(const ChgSet& c, int node) {
@@ -4196,7 +4289,76 @@ __device__ __forceinline__ void chg_unset(const ChgSet& c, int node) {
   else __hip_atomic_fetch_and(c.lds + (node >> 5), ~(1u << (node & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// Speculative replay of a plain batch (LoadAware + NodeNUMAResource (+ FitPlus / SRA) pods, no quota) on
+// The P phase of the speculative replay (wave 0): pods [start, end) each predict their best candidate whose
+// node is not in the changed set, nor predicted by an earlier pod of the round.  A software pipeline keeps
+// every LDS access off the per-pod chain: while pod j reduces, pod j+1's changed-set words are read (after
+// the set updates of pods < j: a wave's LDS operations execute in order; pod j's own prediction is compared
+// in registers) and pod j+2's keys are read; each is consumed one step later.  The three register sets
+// rotate by hand (step A, B, C -> B, C, A), so no loop-carried copy of a pending load forces an early wait.
+// Lane j keeps pod j's prediction (xn, xk); the caller stores them.
+template <bool GLB>
+__device__ __forceinline__ uint32_t chg_load_word(const ChgSet& c, uint32_t key) {
+  const int node = key ? key_node(key) : 0;  // (key 0: any word, its bit is masked below)
+  return GLB ? ld_sc1(c.glb + (node >> 5)) : c.lds[node >> 5];
+}
+__device__ __forceinline__ bool chg_word_bit(uint32_t w, uint32_t key) {
+  return key != 0 && ((w >> (key_node(key) & 31)) & 1u);
+}
+// SORTED: every list is in descending key order (the merged lists of a split / sharded select, k_fixup's):
+// the prediction is the first unflagged key -- a ballot and a lane read instead of a wave max.
+template <bool GLB, bool SORTED>
+__device__ __forceinline__ void spec_predict(const ResLds& L, const ChgSet& C, int start, int end, int LS, bool two,
+                                             int lane, int32_t& my_xn, uint32_t& my_xk) {
+  auto keys = [&](int j, uint32_t& k0, uint32_t& k1) {
+    k0 = j < end ? L.cand[j * LS + lane] : 0u;
+    k1 = two && j < end ? L.cand[j * LS + 64 + lane] : 0u;
+  };
+  // set X: keys k0/k1 of one pod, its changed-set words w0/w1, its keys' matches m0/m1 of the previous pod's
+  // prediction (not yet in the words)
+  uint32_t ka0, ka1, kb0, kb1, kc0 = 0, kc1 = 0, wa0, wa1, wb0 = 0, wb1 = 0, wc0 = 0, wc1 = 0;
+  bool ma0 = false, ma1 = false, mb0 = false, mb1 = false, mc0 = false, mc1 = false;
+  keys(start, ka0, ka1);
+  keys(start + 1, kb0, kb1);
+  wa0 = chg_load_word<GLB>(C, ka0);
+  wa1 = chg_load_word<GLB>(C, ka1);
+  // pod j on set A; set B = pod j+1 (words read here); set C = pod j+2 (keys read here)
+  auto step = [&](int j, uint32_t& kA0, uint32_t& kA1, uint32_t& wA0, uint32_t& wA1, bool& mA0, bool& mA1,
+                  uint32_t& kB0, uint32_t& kB1, uint32_t& wB0, uint32_t& wB1, bool& mB0, bool& mB1,
+                  uint32_t& kC0, uint32_t& kC1, bool& mC0, bool& mC1) {
+    wB0 = chg_load_word<GLB>(C, kB0);
+    wB1 = chg_load_word<GLB>(C, kB1);
+    keys(j + 2, kC0, kC1);
+    mC0 = mC1 = false;
+    const bool f0 = mA0 || chg_word_bit(wA0, kA0), f1 = mA1 || chg_word_bit(wA1, kA1);
+    uint32_t bu;
+    if constexpr (SORTED) {
+      const uint64_t u0 = __ballot(kA0 != 0 && !f0);
+      if (u0) {
+        bu = (uint32_t)__builtin_amdgcn_readlane((int)kA0, __builtin_ctzll(u0));
+      } else {
+        const uint64_t u1 = __ballot(kA1 != 0 && !f1);
+        bu = u1 ? (uint32_t)__builtin_amdgcn_readlane((int)kA1, __builtin_ctzll(u1)) : 0u;
+      }
+    } else {
+      bu = wave_max_u32(max(f0 ? 0u : kA0, f1 ? 0u : kA1));
+    }
+    const int xn = bu ? key_node(bu) : -1;
+    my_xn = lane == j ? xn : my_xn;
+    my_xk = lane == j ? bu : my_xk;
+    if (xn >= 0 && lane == 0) chg_or<GLB>(C, xn);
+    mB0 = kB0 != 0 && xn >= 0 && key_node(kB0) == xn;
+    mB1 = kB1 != 0 && xn >= 0 && key_node(kB1) == xn;
+  };
+  for (int j = start; j < end; j += 3) {
+    step(j, ka0, ka1, wa0, wa1, ma0, ma1, kb0, kb1, wb0, wb1, mb0, mb1, kc0, kc1, mc0, mc1);
+    if (j + 1 >= end) break;
+    step(j + 1, kb0, kb1, wb0, wb1, mb0, mb1, kc0, kc1, wc0, wc1, mc0, mc1, ka0, ka1, ma0, ma1);
+    if (j + 2 >= end) break;
+    step(j + 2, kc0, kc1, wc0, wc1, mc0, mc1, ka0, ka1, wa0, wa1, ma0, ma1, kb0, kb1, mb0, mb1);
+  }
+}
+
+// Speculative replay of a plain batch (LoadAware + NodeNUMAResource (+ FitPlus / SRA / Fit) pods, no quota) on
 // every wave of the workgroup ("speculative replay").  The sequential replay decides pod j as
 // max(bu_j, bc_j): bu_j its best candidate no earlier pod of the batch took (exact: its snapshot key), bc_j
 // the best current key among the nodes earlier pods took.  Almost every pod takes its bu_j, so a round
@@ -4211,44 +4373,81 @@ __device__ __forceinline__ void chg_unset(const ChgSet& c, int node) {
 //      predictions after it are dropped, and the next round starts at jf + 1 with a smaller window.
 // Lane c of every wave holds slot c: the node pod c took (valid when pod c took a node no earlier pod had),
 // in its current state -- every wave applies the same Reserves, so no slot crosses waves.
+//
+// Stale lists (`tin`, the pipelined schedule without k_fixup): the lists were selected from a
+// snapshot that lacks the Reserves of the previous batch, whose changed nodes T (<= 64, their current records in
+// `tin`, node index in RW_PAD) are the only nodes whose snapshot keys are stale; each pod's list holds its top-
+// (k_j + 64) of that snapshot (LS = KSTALE keys a pod, two a lane).  Lane t of every wave then also holds T's
+// node t as a second slot: T's bits are set in the changed set before P, so a prediction never takes a T node
+// (every node outside T and the batch's own slots keeps its exact key, and at most 64 + j of them can precede pod
+// j's best such node in its stale list); S evaluates every pod against all of T besides its own slots c < j; a
+// pod whose best current key is a T node takes it in V (Reserve on the T slot).  The batch's changed nodes --
+// its own slots and the T slots it reserved -- are written back and become the next batch's T.
 template <bool EXT>
 __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const SoA& s, const int base, const int B,
                                             const KArgs& k, int32_t* __restrict__ chosen,
                                             int32_t* __restrict__ chosen_score, int32_t global_offset,
                                             uint64_t* __restrict__ stamps, int batch_index,
                                             uint64_t* __restrict__ dev_alloc, int64_t* __restrict__ touched_out,
-                                            int32_t* __restrict__ touched_cnt, uint64_t* __restrict__ pst) {
+                                            int32_t* __restrict__ touched_cnt, uint64_t* __restrict__ pst,
+                                            const int64_t* __restrict__ tin, int tin_n, int LS, bool sorted) {
   constexpr int NW = res_threads<false>() / 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const bool ext = EXT && (k.flags & AF_EXT);
+  const bool two = LS > KMAX;  // stale lists: two keys a lane
   NodeFast slot;  // lane c: the node pod c took, after every Reserve on it so far
   bool sv = false;
   int snode = -1;
+  NodeFast tslot;  // lane t: node t of the previous batch's changed set T (stale lists only)
+  bool tv = false, tdirty = false;
+  int tnode = -1;
+  if (tin && lane < tin_n) {  // T's current records (this workgroup wrote them at the end of the last batch)
+    rec_load<__HIP_MEMORY_SCOPE_AGENT>(tin + (int64_t)lane * NUM_RW, tslot);
+    tnode = (int)ld_sc1(tin + (int64_t)lane * NUM_RW + RW_PAD);
+    if (ext) ext_load(s, tnode, k, tslot);
+    fast_adopt(tslot, k);
+    tv = true;
+    if (wave == 0) chg_set_atomic(C, tnode);
+  }
+  int tres = 0;  // Reserves of this batch's pods on T nodes so far (the version of L.sp.tmx)
+  if (tin) {
+    if ((int)threadIdx.x < B) L.sp.tver[threadIdx.x] = -1;
+    __syncthreads();  // T's changed bits before P
+  }
+  // pod j's max key over T in its current state, cached in L.sp.tmx until a pod reserves on a T node
+  auto t_row = [&](int j) {
+    if (L.sp.tver[j] == tres) return;
+    const DevPod p = L.pod[j];
+    const double ed[2] = {L.pd[j][0], L.pd[j][1]}, rd[2] = {L.pd[j][2], L.pd[j][3]};
+    uint32_t tk = tv ? make_key(fast_total<EXT>(tslot, p, ed, rd, k), tnode) : 0u;
+    tk = wave_max_u32(tk);
+    if (lane == 0) L.sp.tmx[j] = tk, L.sp.tver[j] = tres;
+  };
   int32_t o_node = -1, o_score = -1;  // wave 0, lane j: pod j's placement
   int start = 0, win = B, rounds = 0, fetched = 0;
   const bool stamp = wave == 0 && lane == 0;  // phase stamps of the first round (ke_debug_resolve_phases)
   bool first = true;
   while (start < B) {
     const int end = min(B, start + win);
-    // ---- P (wave 0): pods [start, end) each take their best candidate not taken before
+    // ---- P (wave 0): pods [start, end) each take their best candidate not taken before.  Meanwhile the other
+    // waves evaluate the rows' T maxima the S phase would compute (stale lists: the first round, or after a
+    // Reserve on a T node).
     if (wave == 0) {
-      uint32_t ck = L.cand[start * KMAX + lane];
-      bool fl = ck != 0 && chg_test(C, key_node(ck));
-      for (int j = start; j < end; j++) {
-        // pod j+1's list and flags (the bits of pods < j are set: LDS operations of a wave run in order);
-        // pod j's own prediction is compared below
-        const uint32_t ckn = j + 1 < end ? L.cand[(j + 1) * KMAX + lane] : 0u;
-        const bool fln = ckn != 0 && chg_test(C, key_node(ckn));
-        const uint32_t bu = wave_max_u32(fl ? 0u : ck);  // lists from k_select are unordered
-        const int xn = bu ? key_node(bu) : -1;
-        if (lane == 0) {
-          L.sp.xnode[j] = xn;
-          L.sp.xkey[j] = bu;
-          if (xn >= 0) chg_set(C, xn);
-        }
-        ck = ckn;
-        fl = fln || (ckn != 0 && xn >= 0 && key_node(ckn) == xn);
+      int32_t xn = -1;
+      uint32_t xk = 0;
+      if (C.glb) {
+        if (sorted) spec_predict<true, true>(L, C, start, end, LS, two, lane, xn, xk);
+        else spec_predict<true, false>(L, C, start, end, LS, two, lane, xn, xk);
+      } else {
+        if (sorted) spec_predict<false, true>(L, C, start, end, LS, two, lane, xn, xk);
+        else spec_predict<false, false>(L, C, start, end, LS, two, lane, xn, xk);
       }
+      if (lane >= start && lane < end) {
+        L.sp.xnode[lane] = xn;
+        L.sp.xkey[lane] = xk;
+      }
+    } else if (tin) {
+      for (int j = start + wave - 1; j < end; j += NW - 1) t_row(j);
     }
     __syncthreads();
     if (stamp && first) pst[1] = __builtin_amdgcn_s_memrealtime();
@@ -4267,13 +4466,18 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
       }
     }
     if (wave == 0) fetched += __popcll(__ballot(lane >= start && lane < end && sv));
-    // ---- S (rows over the waves): pod j against every slot c < j
+    // ---- S (rows over the waves): pod j against every slot c < j (and every T slot)
     for (int j = start + wave; j < end; j += NW) {
       const DevPod p = L.pod[j];
       const double ed[2] = {L.pd[j][0], L.pd[j][1]}, rd[2] = {L.pd[j][2], L.pd[j][3]};
       uint32_t kc = 0;
       if (sv && lane < j) kc = make_key(fast_total<EXT>(slot, p, ed, rd, k), snode);
-      const uint32_t mx = wave_max_u32(kc);
+      uint32_t tk = 0;
+      if (tin) {  // T changes only when a pod of the batch reserves on it: pod j's T max is cached meanwhile
+        t_row(j);  // (this wave's own LDS writes: in order)
+        tk = L.sp.tmx[j];
+      }
+      const uint32_t mx = max(wave_max_u32(kc), tk);
       if (lane == 0) L.sp.mrow[j] = mx;
     }
     __syncthreads();
@@ -4306,12 +4510,20 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
     if (jf < end) {
       if (lane >= jf && lane < end) sv = false;
       const int wn = key_node(L.sp.mrow[jf]);
-      if (sv && snode == wn) {  // pod jf's Reserve on that slot (every wave keeps its copy)
+      const bool on_c = sv && snode == wn, on_t = tv && tnode == wn;
+      if (on_c || on_t) {  // pod jf's Reserve on that slot (every wave keeps its copy)
         const DevPod pc = L.pod[jf];
         const double ed[2] = {L.pd[jf][0], L.pd[jf][1]}, rd[2] = {L.pd[jf][2], L.pd[jf][3]};
-        fast_reserve(slot, pc, ed, rd);
-        if (ext) ext_fast_reserve(slot, pc, k);
+        if (on_c) {
+          fast_reserve(slot, pc, ed, rd);
+          if (ext) ext_fast_reserve(slot, pc, k);
+        } else {
+          fast_reserve(tslot, pc, ed, rd);
+          if (ext) ext_fast_reserve(tslot, pc, k);
+          tdirty = true;
+        }
       }
+      if (tin && __ballot(on_t)) tres++;  // same T slots on every wave: uniform
       win = max(8, 2 * (jf - start + 1));
       start = jf + 1;
       rounds++;
@@ -4320,37 +4532,41 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
       win = min(MAX_BATCH, 2 * win);
     }
   }
-  if (wave != 0) return;
+  if (wave != 0) return;  // (T came from `tin` into registers the S phases consumed: the write-back may replace it)
   if (lane == 0) pst[5] = __builtin_amdgcn_s_memrealtime();
   if (lane < B) {
     chosen[base + lane] = o_node;
     chosen_score[base + lane] = o_score;
     dev_alloc[base + lane] = 0;
   }
-  // the changed nodes' rows back to the SoA, their replay records, the compact list for the next k_fixup
-  const uint64_t vm = __ballot(sv);
-  if (sv) {
+  // the changed nodes' rows back to the SoA, their replay records, the compact list for the next batch (T of a
+  // stale-list batch, or k_fixup's touched rows)
+  const uint64_t vm = __ballot(sv), tm = __ballot(tdirty);
+  auto write_back = [&](const NodeFast& f, int node, int pos) {
     const int64_t st = s.stride;
-    int64_t* f = s.f + snode;
+    int64_t* fr = s.f + node;
 #pragma unroll
     for (int v = 0; v < 2; v++)
 #pragma unroll
       for (int q = 0; q < 2; q++) {
-        st_sc1(f + (F_FH + 2 * v + q) * st, slot.fh[v][q]);
-        st_sc1(f + (F_SA + 2 * v + q) * st, (int64_t)slot.sa[v][q]);
+        st_sc1(fr + (F_FH + 2 * v + q) * st, f.fh[v][q]);
+        st_sc1(fr + (F_SA + 2 * v + q) * st, (int64_t)f.sa[v][q]);
       }
-    st_sc1(f + (F_NREQ + 0) * st, (int64_t)slot.nreq[0]);
-    st_sc1(f + (F_NREQ + 1) * st, (int64_t)slot.nreq[1]);
-    rec_store_dyn<__HIP_MEMORY_SCOPE_AGENT>(s.rec + (int64_t)snode * NUM_RW, slot);  // sc1: read by k_eval_plain
-    if (ext) ext_store(s, snode, slot, k);
-    if (touched_out) rec_store_full(touched_out + (int64_t)lanes_below(vm) * NUM_RW, slot, snode);
-    chg_clear_word(C, snode);  // every bit still set belongs to a taken node
-  }
-  if (touched_out && lane == 0) st_sc1(touched_cnt, (int32_t)__popcll(vm));
+    st_sc1(fr + (F_NREQ + 0) * st, (int64_t)f.nreq[0]);
+    st_sc1(fr + (F_NREQ + 1) * st, (int64_t)f.nreq[1]);
+    rec_store_dyn<__HIP_MEMORY_SCOPE_AGENT>(s.rec + (int64_t)node * NUM_RW, f);  // sc1: read by k_eval_plain
+    if (ext) ext_store(s, node, f, k);
+    if (touched_out) rec_store_full(touched_out + (int64_t)pos * NUM_RW, f, node);
+  };
+  if (sv) write_back(slot, snode, lanes_below(vm));
+  if (tdirty) write_back(tslot, tnode, __popcll(vm) + lanes_below(tm));
+  if (sv) chg_clear_word(C, snode);  // every bit still set belongs to a taken node or to T
+  if (tv) chg_clear_word(C, tnode);
+  if (touched_out && lane == 0) st_sc1(touched_cnt, (int32_t)(__popcll(vm) + __popcll(tm)));
   if (lane == 0) {
     stamps[batch_index + 1] = __builtin_amdgcn_s_memrealtime();
     pst[6] = (uint64_t)(uint32_t)fetched | ((uint64_t)rounds << 32);  // records fetched | failed rounds
-    pst[7] = (uint64_t)__popcll(vm);
+    pst[7] = (uint64_t)(__popcll(vm) + __popcll(tm));
   }
   drain_stores();
 }
@@ -4382,7 +4598,9 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
                                               uint64_t* __restrict__ pstamps, int batch_index,
                                               uint64_t* __restrict__ dev_alloc, int64_t* __restrict__ numa_alloc,
                                               int64_t* __restrict__ touched_out = nullptr,
-                                              int32_t* __restrict__ touched_cnt = nullptr) {
+                                              int32_t* __restrict__ touched_cnt = nullptr,
+                                              const int64_t* __restrict__ tin = nullptr, int tin_n = 0,
+                                              int LS = KMAX, bool sorted = false) {
   const int tid = threadIdx.x;
   constexpr int RES_THREADS = res_threads<NUMA>();
   if (tid == 0) pstamps[8 * batch_index] = __builtin_amdgcn_s_memrealtime();
@@ -4400,16 +4618,18 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
     }
   }
   __syncthreads();
-  {  // candidate keys (sc1: k_fixup of a concurrent launch wrote them), unused slots zeroed
-    constexpr int U = MAX_BATCH * KMAX / RES_THREADS;
+  {  // candidate keys at stride LS (sc1: a concurrent launch wrote them), unused slots zeroed
+    constexpr int U = MAX_BATCH * KSTALE / RES_THREADS;
+    const int lsh = LS == KSTALE ? 7 : 6, n = MAX_BATCH * LS;
     uint32_t q[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int t = u * RES_THREADS + tid, j = t / KMAX, c = t % KMAX;
-      q[u] = (j < B && c < L.cnt[j]) ? ld_sc1(cand + t) : 0u;
+      const int t = u * RES_THREADS + tid, j = t >> lsh, c = t & (LS - 1);
+      q[u] = (t < n && j < B && c < L.cnt[j]) ? ld_sc1(cand + t) : 0u;
     }
 #pragma unroll
-    for (int u = 0; u < U; u++) L.cand[u * RES_THREADS + tid] = q[u];
+    for (int u = 0; u < U; u++)
+      if (u * RES_THREADS + tid < n) L.cand[u * RES_THREADS + tid] = q[u];
   }
   __syncthreads();
   if (tid == 0) {
@@ -4419,7 +4639,7 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
   if constexpr (!DS && !NUMA && !QUOTA) {  // plain batch: the speculative replay on every wave
     __builtin_amdgcn_s_setprio(3);
     replay_spec<EXT>(L, C, s, base, B, k, chosen, chosen_score, global_offset, stamps, batch_index, dev_alloc,
-                     touched_out, touched_cnt, pstamps + 8 * batch_index);
+                     touched_out, touched_cnt, pstamps + 8 * batch_index, tin, tin_n, LS, sorted);
     __builtin_amdgcn_s_setprio(0);
     return;
   }
@@ -4701,18 +4921,23 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(SoA s, const De
                                                 uint64_t* __restrict__ stamps, uint64_t* __restrict__ pstamps,
                                                 int batch_index, uint64_t* __restrict__ dev_alloc,
                                                 int64_t* __restrict__ numa_alloc, uint32_t* __restrict__ chg_glb,
-                                                int n_nodes) {
+                                                int n_nodes, int sorted) {
   __shared__ ResLds L;
   const ChgSet C = chg_init(L, chg_glb, n_nodes);
   resolve_batch<DS, NUMA, QUOTA>(L, C, s, pods, *batch_base, batch_pods, k, cand, cand_cnt, chosen, chosen_score,
-                                 global_offset, stamps, pstamps, batch_index, dev_alloc, numa_alloc);
+                                 global_offset, stamps, pstamps, batch_index, dev_alloc, numa_alloc, nullptr, nullptr,
+                                 nullptr, 0, KMAX, sorted != 0);
 }
 
 // Persistent Reserve chain of a run of pipelined plain batches [b0, b0 + nb): one
 // workgroup for the whole run, so no kernel boundary or cross-stream event sits between two batches.
-// Per batch: wait until k_fixup published every pod's exact list (ready[b] == pods of b), resolve it,
-// then publish done[b] (rows, placements, the changed-row list).  Every wait is bounded
-// (wait_at_least); on a timeout the run stops and the error word tells the host.
+// Per batch: wait until its lists are published (ready[b] == pods of b), resolve it, then publish
+// done[b] (rows, placements, the changed-row list).  Every wait is bounded (wait_at_least); on a
+// timeout the run stops and the error word tells the host.
+//   stale == nullptr (quota runs): k_fixup made the lists exact (cand, stride KMAX).
+//   else: the stale top-(k_j + KMAX) lists of the double buffer `stale` (stride KSTALE) go straight to the
+//   speculative replay, with the previous batch's changed rows (touched_out, this workgroup wrote them) as
+//   its T slots -- no fixup kernel and no hand-off back to the eval stream on the critical path.
 template <bool QUOTA, bool EXT>
 __global__ __launch_bounds__(res_threads<false>()) void k_resolve_run(SoA s, const DevPod* __restrict__ pods,
                                                                       const int32_t* __restrict__ bases, int b0, int nb,
@@ -4727,17 +4952,25 @@ __global__ __launch_bounds__(res_threads<false>()) void k_resolve_run(SoA s, con
                                                                       int32_t* __restrict__ done, int32_t* __restrict__ err,
                                                                       int64_t* __restrict__ touched_out,
                                                                       int32_t* __restrict__ touched_cnt,
-                                                                      uint32_t* __restrict__ chg_glb, int n_nodes) {
+                                                                      uint32_t* __restrict__ chg_glb, int n_nodes,
+                                                                      const uint32_t* __restrict__ stale,
+                                                                      const int32_t* __restrict__ stale_cnt, int sorted) {
   __shared__ ResLds L;
   __shared__ int32_t s_ok;
   const ChgSet C = chg_init(L, chg_glb, n_nodes);
+  const bool nofix = !QUOTA && stale != nullptr;
   for (int b = b0; b < b0 + nb; b++) {
     const int base = bases[b], B = bases[b + 1] - bases[b];
     if (threadIdx.x == 0) s_ok = wait_at_least(ready + b, B, err);
     __syncthreads();
     if (!s_ok) return;
-    resolve_batch<false, false, QUOTA, EXT>(L, C, s, pods, base, B, k, cand, cand_cnt, chosen, chosen_score, global_offset,
-                                       stamps, pstamps, b, dev_alloc, nullptr, touched_out, touched_cnt);
+    const int par = b & 1;
+    const int64_t* tin = nofix && b > b0 ? touched_out : nullptr;
+    const int tin_n = tin ? ld_sc1(touched_cnt) : 0;  // the previous batch's wave 0 wrote it (drained, barrier)
+    resolve_batch<false, false, QUOTA, EXT>(L, C, s, pods, base, B, k, nofix ? stale + (int64_t)par * MAX_BATCH * KSTALE : cand,
+                                       nofix ? stale_cnt + par * MAX_BATCH : cand_cnt, chosen, chosen_score, global_offset,
+                                       stamps, pstamps, b, dev_alloc, nullptr, touched_out, touched_cnt, tin, tin_n,
+                                       nofix ? KSTALE : KMAX, !nofix || sorted != 0);  // (k_fixup's lists: by rank)
     __syncthreads();  // wave 0 drained its stores (replay_batch), so they are performed
     if (threadIdx.x == 0) st_sc1(done + b, 1);
   }
@@ -5257,12 +5490,14 @@ struct DeviceState {
   uint32_t* d_chg = nullptr;        // changed-node bitmap of the replay when node ids exceed its LDS copy
   int64_t* d_trows = nullptr;       // [MAX_BATCH][NUM_RW] records the last resolved batch changed (node in RW_PAD)
   int32_t* d_tcnt = nullptr;        // their count
+  int32_t* d_parts_done = nullptr;  // [MAX_BATCH] parts of each pod a split k_select finished (zero between launches)
   int32_t* d_stale_cnt = nullptr;   // [2][MAX_BATCH]
   static constexpr int EV_RING = 8;
   hipEvent_t ev_res[EV_RING] = {};  // a batch's Reserve done (stream)
   hipEvent_t ev_sel[EV_RING] = {};  // a batch's candidate lists done (estream)
   hipEvent_t ev_start = nullptr;
   bool pipeline = true;             // ke_set_pipeline
+  bool pipe_fixup = false;          // ke_set_pipeline(2): exact lists from k_fixup for every run (else quota runs only)
   // the Reservation plugin of a singleton batch (k_rsv_pick): its pairs and result words
   RsvPair* d_rsv = nullptr;
   int64_t rsv_cap = 0;              // bytes
@@ -5326,6 +5561,8 @@ int device_create(Context* ctx) {
   HIP_OK(hipMemsetAsync(d->soa.kerr, 0, sizeof(int32_t), d->stream));
   HIP_OK(hipMemsetAsync(d->soa.rec, 0, sizeof(int64_t) * NUM_RW * d->capacity, d->stream));
   HIP_OK(hipMalloc(&d->d_tcnt, sizeof(int32_t)));
+  HIP_OK(hipMalloc(&d->d_parts_done, sizeof(int32_t) * MAX_BATCH));
+  HIP_OK(hipMemset(d->d_parts_done, 0, sizeof(int32_t) * MAX_BATCH));
   if (d->capacity > (int64_t)CHG_LDS_WORDS * 32) {  // zero between batches (each replay clears its bits)
     HIP_OK(hipMalloc(&d->d_chg, sizeof(uint32_t) * (d->capacity + 31) / 32));
     HIP_OK(hipMemsetAsync(d->d_chg, 0, sizeof(uint32_t) * (d->capacity + 31) / 32, d->stream));
@@ -5361,7 +5598,7 @@ void device_destroy(Context* ctx) {
                   d->d_dsraw,   d->d_dsmax,  d->d_devalloc,   d->d_dsrows,       d->soa.nf,   d->soa.nm,
                   d->d_numaalloc, d->d_numarows, d->d_defer, d->d_defer_cnt, d->soa.cs, d->soa.cpu,
                   d->d_cpurows, d->d_cpusets, d->d_aff, d->soa.qt, d->soa.qm, d->d_sched, d->d_stale,
-                  d->d_stale_cnt, d->d_trows, d->d_tcnt, d->d_chg, d->soa.rec, d->soa.pt, d->soa.kerr,
+                  d->d_stale_cnt, d->d_trows, d->d_tcnt, d->d_parts_done, d->d_chg, d->soa.rec, d->soa.pt, d->soa.kerr,
                   d->soa.xf, d->soa.xm, d->d_xrows, d->soa.dsx, d->d_ph, d->d_vfo, d->d_rsv, d->d_rsv_out};
   if (d->estream) (void)hipStreamSynchronize(d->estream);
   for (void* p : ptrs)
@@ -6019,6 +6256,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   HIP_OK(hipMemsetAsync(d_ready, 0, sizeof(int32_t) * (sched_words - n_batches - 1), d->stream));
   HIP_OK(hipMemsetAsync(d_fst, 0, sizeof(uint64_t) * 2 * n_batches, d->stream));
   HIP_OK(hipMemsetAsync(d->soa.kerr, 0, sizeof(int32_t), d->stream));
+  HIP_OK(hipMemsetAsync(d->d_parts_done, 0, sizeof(int32_t) * MAX_BATCH, d->stream));  // (an aborted launch's counts)
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
@@ -6108,11 +6346,11 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
         const bool rc = select_seg(slo, shi) <= SEL_RC * 512;
         auto sel = ds ? (rc ? k_select<true, SEL_RC> : k_select<true, 0>) : (rc ? k_select<false, SEL_RC> : k_select<false, 0>);
         hipLaunchKernelGGL(sel, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, es, d->d_scores, d->capacity, slo, shi, cand,
-                           cnt, d->d_dsraw, d->d_dsmax, k.wp_ds, kext, L, (int64_t)0);
+                           cnt, d->d_dsraw, d->d_dsmax, k.wp_ds, kext, L, (int64_t)0, nullptr, nullptr, nullptr);
       };
       // a plain batch over many nodes: its pods' selections split over several workgroups each (>= 256
       // workgroups in all, parts of >= 4096 nodes), merged by k_merge
-      const int parts = ds ? 1 : std::max(1, std::min({MAX_WORLD, (255 + bp) / bp, (int)(N / 4096)}));
+      const int parts = ds ? 1 : select_parts(N, bp);
       if (argmax1) {  // d_cand[0] zeroed by k_batch_begin
         hipLaunchKernelGGL((ds ? k_argmax1<true> : k_argmax1<false>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
                            es, d->d_scores, 0, N, d->d_dsraw, d->d_dsmax, k.wp_ds, d->d_cand, d->d_cand_cnt);
@@ -6125,9 +6363,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
         hipLaunchKernelGGL((rc ? k_select<false, SEL_RC> : k_select<false, 0>), dim3((unsigned)bp, (unsigned)parts),
                            dim3(SELECT_BLOCK), 0, es, d->d_scores, d->capacity, 0, (int)N, d->d_split,
                            reinterpret_cast<int32_t*>(d->d_split + MAX_BATCH * L), d->d_dsraw, d->d_dsmax, k.wp_ds,
-                           kext, L, (int64_t)gw);
-        hipLaunchKernelGGL(k_merge, dim3((unsigned)bp), dim3(MERGE_BLOCK), 0, es, d->d_split, parts, L, kext, lists,
-                           lists_cnt);
+                           kext, L, (int64_t)gw, lists, lists_cnt, d->d_parts_done);  // the last part merges
       } else if (!sharded) {
         select(0, N, lists, lists_cnt);
       } else {
@@ -6160,22 +6396,40 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   // re-evaluates the nodes it chose and publishes the exact lists.  Any other batch (DeviceShare /
   // cpuset singletons, NUMA-policy contexts, pipeline off) is serial: its eval waits for the previous
   // batch's Reserve (HIP events), its lists are exact, its Reserve kernel waits for its lists.
+  // the candidate lists of batches [b0, e) are in descending key order: they come out of a merge (split or
+  // node-sharded select), not straight out of one k_select workgroup (unordered)
+  auto run_sorted = [&](int b0, int e) {
+    for (int b = b0; b < e; b++) {
+      const int bp = batches[b].pods;
+      if (N <= 0 || batches[b].ds) return false;
+      if (sharded) continue;
+      if (select_parts(N, bp) <= 1) return false;
+    }
+    return true;
+  };
   ctx->host_ms[3] = ms_since(tp);
   const auto host_t0 = std::chrono::steady_clock::now();
   for (int b = 0; b < n_batches;) {
     if (run_end[b] > 0) {
       const int r0 = b, e = run_end[b];
       const bool ext = (k.flags & AF_EXT) != 0;
+      const bool fixup = quota || d->pipe_fixup;  // the replay_batch path (quota) needs exact lists
       hipLaunchKernelGGL((quota ? (ext ? k_resolve_run<true, true> : k_resolve_run<true, false>)
                                 : (ext ? k_resolve_run<false, true> : k_resolve_run<false, false>)), dim3(1), dim3(res_threads<false>()), 0,
                          d->stream, d->soa, d->d_pods, d_bases, r0, e - r0, k, d->d_cand, d->d_cand_cnt, d->d_chosen,
                          d->d_chosen_score, ctx->cfg.global_node_offset, d->d_stamps, d->d_stamps + (n_pods + 2),
-                         d->d_devalloc, d_ready, d_done, d_err, d->d_trows, d->d_tcnt, d->d_chg, N);
+                         d->d_devalloc, d_ready, d_done, d_err, d->d_trows, d->d_tcnt, d->d_chg, N,
+                         fixup ? nullptr : d->d_stale, fixup ? nullptr : d->d_stale_cnt, (int)run_sorted(r0, e));
       if (r0 > 0) HIP_OK(hipStreamWaitEvent(d->estream, d->ev_res[(r0 - 1) % R], 0));
       for (int q = r0; q < e; q++) {
         rc = eval_select(q, true, d->estream);
         if (rc) return rc;
         const bool first = q == r0;
+        if (!fixup) {  // the stale lists go to the replay as they are; batch q+1's eval waits for batch q-1
+          hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), 0, d->estream, d_ready + q, (int32_t)batches[q].pods,
+                             first ? nullptr : d_done + (q - 1), d_err, d_fst + 2 * q);
+          continue;
+        }
         hipLaunchKernelGGL((ext ? k_fixup<true> : k_fixup<false>), dim3((unsigned)batches[q].pods), dim3(FIX_BLOCK), 0, d->estream, d->soa, d->d_pods,
                            d_bases + q, k, d->d_stale + (size_t)(q & 1) * MAX_BATCH * KSTALE,
                            d->d_stale_cnt + (q & 1) * MAX_BATCH, d->d_trows, d->d_tcnt, d->d_cand, d->d_cand_cnt,
@@ -6215,7 +6469,8 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                                  : (numa ? k_resolve<false, true, false> : k_resolve<false, false, false>));
       hipLaunchKernelGGL(resolve, dim3(1), dim3(numa ? res_threads<true>() : res_threads<false>()), 0, d->stream, d->soa, d->d_pods, bbase, bp, k,
                          d->d_cand, d->d_cand_cnt, d->d_chosen, d->d_chosen_score, ctx->cfg.global_node_offset,
-                         d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc, d->d_numaalloc, d->d_chg, N);
+                         d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc, d->d_numaalloc, d->d_chg, N,
+                         (int)run_sorted(b, b + 1));
       if (batches[b].cut) {  // a DeviceShare batch may stop early: re-run its remaining pods as batch b
         int32_t cut = -1;
         HIP_OK(hipMemcpyAsync(&cut, d->d_dsmax + DSB_CUT, sizeof(int32_t), hipMemcpyDeviceToHost, d->stream));
@@ -6411,7 +6666,9 @@ int device_replay_phases(Context* ctx, double* cyc8) {
 }
 
 int device_set_pipeline(Context* ctx, int32_t on) {
+  if (on < 0 || on > 2) return fail(KE_ERR_INVALID, "ke_set_pipeline: 0, 1 or 2");
   ctx->dev->pipeline = on != 0;
+  ctx->dev->pipe_fixup = on == 2;
   return KE_OK;
 }
 

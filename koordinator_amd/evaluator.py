@@ -319,8 +319,9 @@ class Evaluator:
         return n.value
 
     def set_pipeline(self, on):
-        """Pipelined schedule (default): batch b's eval + select overlap batch b-1's Reserve replay."""
-        self._check(self.lib.ke_set_pipeline(self.h, 1 if on else 0))
+        """Pipelined schedule (default): batch b's eval + select overlap batch b-1's Reserve replay.
+        on: False / True, or "fixup" (pipelined with exact lists from the fixup kernel, ke_set_pipeline 2)."""
+        self._check(self.lib.ke_set_pipeline(self.h, 2 if on == "fixup" else (1 if on else 0)))
 
     HOST_PHASES = ("checks", "refresh", "upload", "setup", "enqueue", "wait", "stats", "mirror")
 

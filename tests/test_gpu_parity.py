@@ -218,15 +218,18 @@ def test_schedule_large_cluster_prefix(gpu):
     assert ev.check_records(synth.T0) == 0
 
 
-# ---- pipelined schedule (two streams, stale lists + k_fixup) ---------------------------------------
+# ---- pipelined schedule (two streams, stale lists -> the replay's T slots, or k_fixup) ---------------
+@pytest.mark.parametrize("mode", [True, "fixup"], ids=["stale-slots", "fixup"])
 @pytest.mark.parametrize("n_nodes,n_pods,seed", [(20_000, 3000, 71), (150, 2500, 72), (40, 1200, 73)])
-def test_pipeline_matches_serial_and_oracle(gpu, n_nodes, n_pods, seed):
-    """Batch b's eval/select against the stale snapshot (batch b-1 still resolving) + k_fixup give the
-    same placements as the serial one-stream schedule and the oracle.  The small clusters make every
-    batch touch most candidate lists (k_fixup's drop-and-re-evaluate path on nearly every pod)."""
+def test_pipeline_matches_serial_and_oracle(gpu, n_nodes, n_pods, seed, mode):
+    """Batch b's eval/select against the stale snapshot (batch b-1 still resolving) give the same placements
+    as the serial one-stream schedule and the oracle, whether the replay takes the stale lists with batch
+    b-1's changed nodes as slots or k_fixup makes them exact first.  The small clusters make every batch
+    touch most candidate lists (most pods take a node the previous batch changed)."""
     cl = synth.make_cluster(n_nodes, synth.BASE_SEED + seed)
     pods = synth.make_pods(n_pods, synth.BASE_SEED + 100 + seed)
     ev, o = both(synth.config(n_nodes), cl)
+    ev.set_pipeline(mode)
     es = Evaluator(synth.config(n_nodes))
     synth.load_into(es, cl)
     es.set_pipeline(False)

@@ -110,6 +110,11 @@ def test_matched_refusals_precede_every_segment():
         ev.schedule(pods, synth.T0, matches=[[], [], [], [], [0, 1], []])
     assert e.value.code == abi.ERR_UNSUPPORTED
     if not ev.device:
+        plain = synth.make_pods(9, synth.BASE_SEED + 1207)
+        plain["reservation_matched"] = 0
+        with pytest.raises(KoordEvalError) as e:  # the refused call consumed its lists: no shape error here
+            ev.schedule(plain, synth.T0)
+        assert e.value.code == abi.ERR_NO_DEVICE
         with pytest.raises(KoordEvalError) as e:  # without the NUMA-policy node: past the checks, no device here
             ev.schedule(pods, synth.T0, matches=[[], [], [], [], [1], []])
         assert e.value.code == abi.ERR_NO_DEVICE
