@@ -538,6 +538,7 @@ EXPORTS = {
     "ke_last_host_stats": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ke_last_resolve_split": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "ke_debug_resolve_phases": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "ke_debug_resolve_subphases": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ke_debug_numa_deferred": (C.c_int, [C.c_void_p, C.POINTER(i64)]),
     "ke_debug_ds_cuts": (C.c_int, [C.c_void_p, C.POINTER(i32)]),
     "ke_debug_spec_failed": (C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),

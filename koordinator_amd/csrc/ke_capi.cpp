@@ -772,6 +772,8 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
     c.host_ms[7] = std::chrono::duration<double, std::milli>(clk::now() - tp).count();
     const bool whole = s0 == 0 && s1 == n_pods;  // one segment: the last_* outputs are already whole
     if (!whole) {
+      c.last_dev_alloc.resize((size_t)len, 0);  // (a segment without DeviceShare batches reads none back)
+      c.last_cpusets.resize((size_t)len * 4, 0);
       all_dev.insert(all_dev.end(), c.last_dev_alloc.begin(), c.last_dev_alloc.end());
       if (c.last_vf.empty()) all_vf.resize(all_vf.size() + (size_t)len * 2 * KE_MAX_MINORS, -1);
       else all_vf.insert(all_vf.end(), c.last_vf.begin(), c.last_vf.end());
@@ -1003,6 +1005,12 @@ int ke_debug_numa_deferred(ke_ctx* ctx, int64_t* n) {
 int ke_debug_resolve_phases(ke_ctx* ctx, double* phases6) {
   if (!ctx || !phases6) return fail(KE_ERR_INVALID, "ke_debug_resolve_phases arguments");
   for (int i = 0; i < 6; i++) phases6[i] = ctx->c.kstat_resolve_phase_ms[i];
+  return KE_OK;
+}
+
+int ke_debug_resolve_subphases(ke_ctx* ctx, double* sub4) {
+  if (!ctx || !sub4) return fail(KE_ERR_INVALID, "ke_debug_resolve_subphases arguments");
+  for (int i = 0; i < 4; i++) sub4[i] = ctx->c.kstat_resolve_sub_ms[i];
   return KE_OK;
 }
 

@@ -42,6 +42,7 @@ extern "C" __device__ int32_t __ockl_wfred_add_i32(int32_t);
   } while (0)
 
 constexpr int EVAL_BLOCK = 256;
+constexpr int PST = 16;  // replay stamps / counters per batch (ke_debug_resolve_phases)
 // k_eval_batch grid: node tiles padded to a multiple of the 8 XCDs (x) x pod groups (y)
 inline dim3 eval_grid(int n_nodes, int block, int pods, int ppb) {
   const int tiles = (n_nodes + block - 1) / block;
@@ -2617,6 +2618,27 @@ __device__ __forceinline__ void st_sc1(T* p, T v) {
 }
 __device__ __forceinline__ void drain_stores() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
 
+// Device-side hand-off between the eval stream and the persistent Reserve kernel (k_resolve_run):
+// counters / flags in global memory polled with relaxed sc1 loads, payloads sc1 (above), every wait
+// bounded in time and abandoned when the run's error word is set.
+constexpr uint64_t HANDOFF_TIMEOUT_TICKS = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
+__device__ __forceinline__ bool wait_at_least(const int32_t* flag, int32_t want, int32_t* err) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > HANDOFF_TIMEOUT_TICKS) {
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  // the hand-off's words are read with sc1 loads from here on: no acquire fence, only a compiler
+  // ordering point (cdna_hip_programming.md Guideline 16)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return true;
+}
+
+
 // ---- the replay's fast path: per-node records with the node-only terms precomputed --------------
 // In the replay a changed node is re-evaluated for every later pod of its batch, while its row changes
 // only at its own Reserves; and almost every pod adopts a node it has not touched yet.  Each node
@@ -3144,7 +3166,14 @@ template <bool EXT>
 __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_plain(SoA s, int lo, int hi, const DevPod* __restrict__ pods,
                                                            const int32_t* __restrict__ batch_base, int batch_pods,
                                                            KArgs k, uint16_t* __restrict__ scores, int64_t score_stride,
-                                                           uint64_t* __restrict__ stamp) {
+                                                           uint64_t* __restrict__ stamp, const int32_t* __restrict__ done_wait,
+                                                           int32_t* __restrict__ err) {
+  if (done_wait) {  // pipelined: the Reserves of batch b-2 first (every workgroup sees the flag itself)
+    __shared__ int32_t s_go;
+    if (threadIdx.x == 0) s_go = wait_at_least(done_wait, 1, err);
+    __syncthreads();
+    if (!s_go) return;  // (a timed-out hand-off: the host discards the queue)
+  }
   if (stamp && (blockIdx.x | blockIdx.y | threadIdx.x) == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
   const int G = (int)gridDim.y;
   const int b = (int)(blockIdx.x + blockIdx.y * gridDim.x), r = b >> 3;
@@ -3651,10 +3680,10 @@ constexpr int MAX_WORLD = 8;
 static_assert(MAX_WORLD == 8, "select_parts caps the parts at 8");
 constexpr int MERGE_BLOCK = MAX_WORLD * KSTALE;
 
-template <bool SC1>
+template <bool SC1, bool SORTED = false>
 __device__ __forceinline__ void merge_lists(const uint32_t* __restrict__ gath, int64_t gw, int world, int L, int kext,
                                             int j, uint4* s_k, uint32_t* __restrict__ cand,
-                                            int32_t* __restrict__ cand_cnt);
+                                            int32_t* __restrict__ cand_cnt, bool sc1_out = false);
 static_assert(SELECT_BLOCK == MERGE_BLOCK, "the last part's workgroup of a split k_select merges");
 
 template <bool DS, int RC>
@@ -3666,7 +3695,8 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
                                                          int ostride, int64_t ystride,
                                                          uint32_t* __restrict__ mcand = nullptr,
                                                          int32_t* __restrict__ mcnt = nullptr,
-                                                         int32_t* __restrict__ parts_done = nullptr) {
+                                                         int32_t* __restrict__ parts_done = nullptr,
+                                                         int32_t* __restrict__ ready = nullptr) {
   uint32_t* const gath = cand;
   if (!DS && gridDim.y > 1) {
     const int part = select_part(lo, hi, gridDim.y);
@@ -3869,6 +3899,7 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
   }
   // pass 3: select (a step none of whose scores reaches vmin holds no selected node and no tie)
   const uint32_t vmin = (uint32_t)max(1, need_ties > 0 ? thr : thr + 1);
+  uint32_t* const stage = reinterpret_cast<uint32_t*>(&s_hist[0][0][0]);  // (pass 3 reads no histogram)
   int running = 0;  // ties of this wave before the current row
   for (int w = 0; w < wave; w++) running += need_ties > 0 ? s_tie[w] : 0;
   uint32_t* out = cand + (int64_t)j * ostride;
@@ -3907,17 +3938,32 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
       for (int t = 0; t < 8; t++)
         if (selm & (1u << t)) {
           const uint32_t key = (v[t] << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)(i0 + t));
-          if (mcand) st_sc1(out + pos, key);  // (fused merge: read by another workgroup of this launch)
+          if (mcand) stage[pos] = key;  // (fused merge: sorted below)
+          else if (ready) st_sc1(out + pos, key);  // (read by the running Reserve kernel)
           else out[pos] = key;
           pos++;
         }
     }
   });
   __syncthreads();
+  if (mcand && !DS) {  // the part's list in descending order (the merge ranks by binary search)
+    const int n = s_out;
+    if ((int)threadIdx.x < n) {
+      const uint32_t key = stage[threadIdx.x];
+      int rank = 0;
+      for (int x = 0; x < n; x++) rank += stage[x] > key;
+      st_sc1(out + rank, key);  // (read by another workgroup of this launch)
+    }
+  }
   if (threadIdx.x == 0) {
-    if (mcand) st_sc1(cand_cnt + j, (int32_t)s_out);
+    if (mcand || ready) st_sc1(cand_cnt + j, (int32_t)s_out);
     else cand_cnt[j] = s_out;
     if (DS) dsmax1[DSB_CNT + j] = (uint32_t)s_dscnt;
+  }
+  if (!DS && !mcand && ready) {  // one workgroup per pod: publish its list to the running Reserve kernel
+    drain_stores();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (DS || !mcand) return;
   // split select with the merge fused: the workgroup finishing pod j's last part merges the parts (k_merge's
@@ -3934,8 +3980,14 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
   }
   __syncthreads();
   if (!s_last) return;
-  merge_lists<true>(gath, ystride, (int)gridDim.y, ostride, kext, j, reinterpret_cast<uint4*>(&s_hist[0][0][0]),
-                    mcand, mcnt);
+  __syncthreads();  // (the staging reads above, before the merge reuses the words)
+  merge_lists<true, true>(gath, ystride, (int)gridDim.y, ostride, kext, j, reinterpret_cast<uint4*>(&s_hist[0][0][0]),
+                          mcand, mcnt, ready != nullptr);
+  if (ready) {  // publish the merged list to the running Reserve kernel
+    drain_stores();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // --- node-sharded batches: merge of the per-shard candidate lists ---------------------------------
@@ -3947,20 +3999,49 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
 
 // pod j's merged list from `world` blocks `gw` words apart (all MERGE_BLOCK threads of the workgroup; s_k:
 // MERGE_BLOCK keys of LDS).  SC1: the blocks were written by other workgroups of the running launch.
-template <bool SC1>
+// SORTED: every block's list is in descending order, so a key's rank in another block is the length of
+// that block's prefix of larger keys (a binary search) instead of a count over all of its keys.
+template <bool SC1, bool SORTED>
 __device__ __forceinline__ void merge_lists(const uint32_t* __restrict__ gath, int64_t gw, int world, int L, int kext,
                                             int j, uint4* s_k, uint32_t* __restrict__ cand,
-                                            int32_t* __restrict__ cand_cnt) {
+                                            int32_t* __restrict__ cand_cnt, bool sc1_out) {
   const int k = min(j + 1, KMAX) + kext;
   const int t = threadIdx.x, r = t / L, c = t % L;
   uint32_t key = 0;
+  int n = 0;
   if (r < world) {
     const uint32_t* blk = gath + (int64_t)r * gw;
-    const int n = SC1 ? ld_sc1(reinterpret_cast<const int32_t*>(blk + MAX_BATCH * L + j)) : (int)blk[MAX_BATCH * L + j];
+    n = SC1 ? ld_sc1(reinterpret_cast<const int32_t*>(blk + MAX_BATCH * L + j)) : (int)blk[MAX_BATCH * L + j];
     if (c < n) key = SC1 ? (uint32_t)ld_sc1(reinterpret_cast<const int32_t*>(blk + j * L + c)) : blk[j * L + c];
   }
-  reinterpret_cast<uint32_t*>(s_k)[t] = key;
+  uint32_t* const sk = reinterpret_cast<uint32_t*>(s_k);
+  sk[t] = key;
   const int nz = __syncthreads_count(key != 0u);
+  if (SORTED) {
+    if (key) {
+      int rank = c;  // the larger keys of its own block come first
+      for (int q = 0; q < world; q++) {
+        if (q == r) continue;
+        const uint32_t* b = sk + q * L;  // descending, zeros after the block's count
+        int lo = 0, hi = L;              // the first position holding a key < key
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (b[mid] > key) lo = mid + 1;
+          else hi = mid;
+        }
+        rank += lo;
+      }
+      if (rank < k) {
+        if (sc1_out) st_sc1(cand + j * L + rank, key);
+        else cand[j * L + rank] = key;
+      }
+    }
+    if (t == 0) {
+      if (sc1_out) st_sc1(cand_cnt + j, min(nz, k));
+      else cand_cnt[j] = min(nz, k);
+    }
+    return;
+  }
   if (key) {
     int rank = 0;
     const int n4 = world * L / 4;
@@ -3989,26 +4070,6 @@ __global__ __launch_bounds__(MERGE_BLOCK) void k_merge(const uint32_t* __restric
 // resolve).  The top-k_j of (stale list minus touched) + (touched, fresh keys) is therefore the exact
 // top-k_j under S that k_resolve expects.  One workgroup per pod.
 constexpr int FIX_BLOCK = KSTALE + KMAX;  // stale keys, then fresh keys of the touched nodes
-
-// Device-side hand-off between the eval stream and the persistent Reserve kernel (k_resolve_run):
-// counters / flags in global memory polled with relaxed sc1 loads, payloads sc1 (above), every wait
-// bounded in time and abandoned when the run's error word is set.
-constexpr uint64_t HANDOFF_TIMEOUT_TICKS = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
-__device__ __forceinline__ bool wait_at_least(const int32_t* flag, int32_t want, int32_t* err) {
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > HANDOFF_TIMEOUT_TICKS) {
-      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-  // the hand-off's words are read with sc1 loads from here on: no acquire fence, only a compiler
-  // ordering point (cdna_hip_programming.md Guideline 16)
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  return true;
-}
 
 // wait_b >= 0: the lists need the Reserves of batch wait_b (the touched nodes' rows): wait for its flag
 // in `done` first.  When the list is written the workgroup adds 1 to *ready (the Reserve kernel waits
@@ -4086,16 +4147,17 @@ __global__ __launch_bounds__(FIX_BLOCK) void k_fixup(SoA s, const DevPod* __rest
   }
 }
 
-// Pipelined schedule without k_fixup (k_resolve_run's stale-list mode): publish batch q's lists to the
-// running Reserve kernel (ready = its pods; the select / merge kernels before this one on the same stream
-// wrote them), then hold the eval stream until batch q-1's Reserve is done (done_wait), so that batch q+1's
-// eval sees every Reserve of batches <= q-1 -- its stale keys differ from the exact ones only on the nodes
-// batch q changes -- and its lists may reuse batch q-1's half of the double buffer.
+// Pipelined schedule without k_fixup (k_resolve_run's stale-list mode), where the eval / select kernels do not
+// do it themselves (node-sharded selects, 1-2-pod batches): publish batch q's lists to the running Reserve
+// kernel (ready = its pods; the select / merge kernels before this one on the same stream wrote them), and /
+// or hold the eval stream until batch q-1's Reserve is done (done_wait), so that batch q+1's eval sees every
+// Reserve of batches <= q-1 -- its stale keys differ from the exact ones only on the nodes batch q changes --
+// and its lists may reuse batch q-1's half of the double buffer.
 __global__ void k_handoff(int32_t* __restrict__ ready, int32_t n, const int32_t* __restrict__ done_wait,
                           int32_t* __restrict__ err, uint64_t* __restrict__ fstamp) {
   if (threadIdx.x != 0) return;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  __hip_atomic_store(ready, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (ready) __hip_atomic_store(ready, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (fstamp) {
     fstamp[0] = t0;
     fstamp[1] = t0 + 1;
@@ -4262,6 +4324,8 @@ struct SpecLds {
   int32_t jf;                // first pod of the round whose prediction failed (end of round: none)
   uint32_t tmx[MAX_BATCH];   // stale lists: max key of pod j over the previous batch's changed nodes T ...
   int32_t tver[MAX_BATCH];   // ... valid while no pod of the batch reserved a T node since (-1: never computed)
+  int32_t tnext[MAX_BATCH];  // the batch's changed nodes (the next batch's T), in touched-list order
+  int32_t tnext_n;
 };
 
 struct ResLdsCore {
@@ -4295,7 +4359,7 @@ __device__ __forceinline__ void chg_unset(const ChgSet& c, int node) {
 // the set updates of pods < j: a wave's LDS operations execute in order; pod j's own prediction is compared
 // in registers) and pod j+2's keys are read; each is consumed one step later.  The three register sets
 // rotate by hand (step A, B, C -> B, C, A), so no loop-carried copy of a pending load forces an early wait.
-// Lane j keeps pod j's prediction (xn, xk); the caller stores them.
+// Lane 0 stores pod j's prediction (L.sp.xnode / xkey) with its changed-set bit.
 template <bool GLB>
 __device__ __forceinline__ uint32_t chg_load_word(const ChgSet& c, uint32_t key) {
   const int node = key ? key_node(key) : 0;  // (key 0: any word, its bit is masked below)
@@ -4307,11 +4371,14 @@ __device__ __forceinline__ bool chg_word_bit(uint32_t w, uint32_t key) {
 // SORTED: every list is in descending key order (the merged lists of a split / sharded select, k_fixup's):
 // the prediction is the first unflagged key -- a ballot and a lane read instead of a wave max.
 template <bool GLB, bool SORTED>
-__device__ __forceinline__ void spec_predict(const ResLds& L, const ChgSet& C, int start, int end, int LS, bool two,
-                                             int lane, int32_t& my_xn, uint32_t& my_xk) {
+__device__ __forceinline__ void spec_predict(ResLds& L, const ChgSet& C, int start, int end, int LS, bool two,
+                                             int lane) {
+  // SORTED: only the first 64 keys of a list are pipelined; the rest are read (with their words, which by then
+  // hold every earlier prediction) when those 64 are all taken -- j + |T| of them at most, so rarely
+  const bool two_p = two && !SORTED;
   auto keys = [&](int j, uint32_t& k0, uint32_t& k1) {
     k0 = j < end ? L.cand[j * LS + lane] : 0u;
-    k1 = two && j < end ? L.cand[j * LS + 64 + lane] : 0u;
+    k1 = two_p && j < end ? L.cand[j * LS + 64 + lane] : 0u;
   };
   // set X: keys k0/k1 of one pod, its changed-set words w0/w1, its keys' matches m0/m1 of the previous pod's
   // prediction (not yet in the words)
@@ -4320,34 +4387,41 @@ __device__ __forceinline__ void spec_predict(const ResLds& L, const ChgSet& C, i
   keys(start, ka0, ka1);
   keys(start + 1, kb0, kb1);
   wa0 = chg_load_word<GLB>(C, ka0);
-  wa1 = chg_load_word<GLB>(C, ka1);
+  wa1 = two_p ? chg_load_word<GLB>(C, ka1) : 0u;
   // pod j on set A; set B = pod j+1 (words read here); set C = pod j+2 (keys read here)
   auto step = [&](int j, uint32_t& kA0, uint32_t& kA1, uint32_t& wA0, uint32_t& wA1, bool& mA0, bool& mA1,
                   uint32_t& kB0, uint32_t& kB1, uint32_t& wB0, uint32_t& wB1, bool& mB0, bool& mB1,
                   uint32_t& kC0, uint32_t& kC1, bool& mC0, bool& mC1) {
     wB0 = chg_load_word<GLB>(C, kB0);
-    wB1 = chg_load_word<GLB>(C, kB1);
+    if (two_p) wB1 = chg_load_word<GLB>(C, kB1);
     keys(j + 2, kC0, kC1);
     mC0 = mC1 = false;
-    const bool f0 = mA0 || chg_word_bit(wA0, kA0), f1 = mA1 || chg_word_bit(wA1, kA1);
+    const bool f0 = mA0 || chg_word_bit(wA0, kA0);
     uint32_t bu;
     if constexpr (SORTED) {
       const uint64_t u0 = __ballot(kA0 != 0 && !f0);
       if (u0) {
         bu = (uint32_t)__builtin_amdgcn_readlane((int)kA0, __builtin_ctzll(u0));
+      } else if (two) {  // the list's second half, read now
+        const uint32_t k1 = j < end ? L.cand[j * LS + 64 + lane] : 0u;
+        const uint32_t w1 = chg_load_word<GLB>(C, k1);
+        const uint64_t u1 = __ballot(k1 != 0 && !chg_word_bit(w1, k1));
+        bu = u1 ? (uint32_t)__builtin_amdgcn_readlane((int)k1, __builtin_ctzll(u1)) : 0u;
       } else {
-        const uint64_t u1 = __ballot(kA1 != 0 && !f1);
-        bu = u1 ? (uint32_t)__builtin_amdgcn_readlane((int)kA1, __builtin_ctzll(u1)) : 0u;
+        bu = 0u;
       }
     } else {
-      bu = wave_max_u32(max(f0 ? 0u : kA0, f1 ? 0u : kA1));
+      const bool f1 = mA1 || chg_word_bit(wA1, kA1);
+      bu = wave_max_u32(max(f0 ? 0u : kA0, two_p && !f1 ? kA1 : 0u));
     }
     const int xn = bu ? key_node(bu) : -1;
-    my_xn = lane == j ? xn : my_xn;
-    my_xk = lane == j ? bu : my_xk;
-    if (xn >= 0 && lane == 0) chg_or<GLB>(C, xn);
+    if (lane == 0) {  // pod j's prediction, and its node into the changed set
+      L.sp.xnode[j] = xn;
+      L.sp.xkey[j] = bu;
+      if (xn >= 0) chg_or<GLB>(C, xn);
+    }
     mB0 = kB0 != 0 && xn >= 0 && key_node(kB0) == xn;
-    mB1 = kB1 != 0 && xn >= 0 && key_node(kB1) == xn;
+    if (two_p) mB1 = kB1 != 0 && xn >= 0 && key_node(kB1) == xn;
   };
   for (int j = start; j < end; j += 3) {
     step(j, ka0, ka1, wa0, wa1, ma0, ma1, kb0, kb1, wb0, wb1, mb0, mb1, kc0, kc1, mc0, mc1);
@@ -4390,7 +4464,7 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
                                             uint64_t* __restrict__ stamps, int batch_index,
                                             uint64_t* __restrict__ dev_alloc, int64_t* __restrict__ touched_out,
                                             int32_t* __restrict__ touched_cnt, uint64_t* __restrict__ pst,
-                                            const int64_t* __restrict__ tin, int tin_n, int LS, bool sorted) {
+                                            const int64_t* __restrict__ tin, bool keep, int LS, bool sorted) {
   constexpr int NW = res_threads<false>() / 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const bool ext = EXT && (k.flags & AF_EXT);
@@ -4401,19 +4475,25 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
   NodeFast tslot;  // lane t: node t of the previous batch's changed set T (stale lists only)
   bool tv = false, tdirty = false;
   int tnode = -1;
-  if (tin && lane < tin_n) {  // T's current records (this workgroup wrote them at the end of the last batch)
+  // T: the previous batch of the run left its changed nodes' bits set in the changed set and their ids in
+  // L.sp.tnext; their current records are in `tin` (loaded now, adopted at first use: they land during P)
+  const int tin_n = tin ? L.sp.tnext_n : 0;
+  if (lane < tin_n) {
+    tnode = L.sp.tnext[lane];
     rec_load<__HIP_MEMORY_SCOPE_AGENT>(tin + (int64_t)lane * NUM_RW, tslot);
-    tnode = (int)ld_sc1(tin + (int64_t)lane * NUM_RW + RW_PAD);
-    if (ext) ext_load(s, tnode, k, tslot);
-    fast_adopt(tslot, k);
     tv = true;
-    if (wave == 0) chg_set_atomic(C, tnode);
   }
-  int tres = 0;  // Reserves of this batch's pods on T nodes so far (the version of L.sp.tmx)
-  if (tin) {
-    if ((int)threadIdx.x < B) L.sp.tver[threadIdx.x] = -1;
-    __syncthreads();  // T's changed bits before P
-  }
+  bool t_adopted = false;
+  auto adopt_t = [&]() {  // first use of the T slots (wave-uniform)
+    if (t_adopted) return;
+    t_adopted = true;
+    if (tv) {
+      if (ext) ext_load(s, tnode, k, tslot);
+      fast_adopt(tslot, k);
+    }
+  };
+  int tres = 0;  // Reserves of this batch's pods on T nodes so far (the version of L.sp.tmx, reset in the prologue)
+  if (wave == 0 && lane == 0) pst[8] = __builtin_amdgcn_s_memrealtime();  // T set up
   // pod j's max key over T in its current state, cached in L.sp.tmx until a pod reserves on a T node
   auto t_row = [&](int j) {
     if (L.sp.tver[j] == tres) return;
@@ -4422,6 +4502,32 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
     uint32_t tk = tv ? make_key(fast_total<EXT>(tslot, p, ed, rd, k), tnode) : 0u;
     tk = wave_max_u32(tk);
     if (lane == 0) L.sp.tmx[j] = tk, L.sp.tver[j] = tres;
+  };
+  // two rows at once (j1 < 0: none), independent chains (the P phase's idle waves)
+  auto t_row2 = [&](int j, int j1) {
+    const bool need0 = L.sp.tver[j] != tres, need1 = j1 >= 0 && L.sp.tver[j1] != tres;
+    if (!need1) {
+      t_row(j);
+      return;
+    }
+    if (!need0) {
+      t_row(j1);
+      return;
+    }
+    const DevPod p = L.pod[j], p1 = L.pod[j1];
+    const double ed[2] = {L.pd[j][0], L.pd[j][1]}, rd[2] = {L.pd[j][2], L.pd[j][3]};
+    const double ed1[2] = {L.pd[j1][0], L.pd[j1][1]}, rd1[2] = {L.pd[j1][2], L.pd[j1][3]};
+    uint32_t tk = 0, tk1 = 0;
+    if (tv) {
+      tk = make_key(fast_total<EXT>(tslot, p, ed, rd, k), tnode);
+      tk1 = make_key(fast_total<EXT>(tslot, p1, ed1, rd1, k), tnode);
+    }
+    tk = wave_max_u32(tk);
+    tk1 = wave_max_u32(tk1);
+    if (lane == 0) {
+      L.sp.tmx[j] = tk, L.sp.tver[j] = tres;
+      L.sp.tmx[j1] = tk1, L.sp.tver[j1] = tres;
+    }
   };
   int32_t o_node = -1, o_score = -1;  // wave 0, lane j: pod j's placement
   int start = 0, win = B, rounds = 0, fetched = 0;
@@ -4433,21 +4539,20 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
     // waves evaluate the rows' T maxima the S phase would compute (stale lists: the first round, or after a
     // Reserve on a T node).
     if (wave == 0) {
-      int32_t xn = -1;
-      uint32_t xk = 0;
       if (C.glb) {
-        if (sorted) spec_predict<true, true>(L, C, start, end, LS, two, lane, xn, xk);
-        else spec_predict<true, false>(L, C, start, end, LS, two, lane, xn, xk);
+        if (sorted) spec_predict<true, true>(L, C, start, end, LS, two, lane);
+        else spec_predict<true, false>(L, C, start, end, LS, two, lane);
       } else {
-        if (sorted) spec_predict<false, true>(L, C, start, end, LS, two, lane, xn, xk);
-        else spec_predict<false, false>(L, C, start, end, LS, two, lane, xn, xk);
+        if (sorted) spec_predict<false, true>(L, C, start, end, LS, two, lane);
+        else spec_predict<false, false>(L, C, start, end, LS, two, lane);
       }
-      if (lane >= start && lane < end) {
-        L.sp.xnode[lane] = xn;
-        L.sp.xkey[lane] = xk;
-      }
+      if (first && lane == 0) pst[9] = __builtin_amdgcn_s_memrealtime();  // the prediction loop's end
+      adopt_t();  // (its loads landed during the prediction)
     } else if (tin) {
-      for (int j = start + wave - 1; j < end; j += NW - 1) t_row(j);
+      adopt_t();
+      constexpr int RT = EXT ? 1 : 2;
+      for (int j = start + wave - 1; j < end; j += RT * (NW - 1)) t_row2(j, RT == 2 && j + NW - 1 < end ? j + NW - 1 : -1);
+      if (first && wave == 1 && lane == 0) pst[10] = __builtin_amdgcn_s_memrealtime();  // wave 1's T rows
     }
     __syncthreads();
     if (stamp && first) pst[1] = __builtin_amdgcn_s_memrealtime();
@@ -4466,19 +4571,40 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
       }
     }
     if (wave == 0) fetched += __popcll(__ballot(lane >= start && lane < end && sv));
+    if (stamp && first) pst[11] = __builtin_amdgcn_s_memrealtime();  // wave 0's slots reserved (R)
     // ---- S (rows over the waves): pod j against every slot c < j (and every T slot)
-    for (int j = start + wave; j < end; j += NW) {
+    // Two rows a pass (j and j + NW): two independent evaluation chains for the latency-bound wave (one with
+    // the ext slots: their registers would spill).
+    constexpr int RS = EXT ? 1 : 2;
+    for (int j = start + wave; j < end; j += RS * NW) {
+      const int j1 = j + NW;
+      const bool has1 = RS == 2 && j1 < end;  // (wave-uniform)
       const DevPod p = L.pod[j];
       const double ed[2] = {L.pd[j][0], L.pd[j][1]}, rd[2] = {L.pd[j][2], L.pd[j][3]};
-      uint32_t kc = 0;
-      if (sv && lane < j) kc = make_key(fast_total<EXT>(slot, p, ed, rd, k), snode);
-      uint32_t tk = 0;
+      uint32_t kc = 0, kc1 = 0;
+      if (has1) {
+        const DevPod p1 = L.pod[j1];
+        const double ed1[2] = {L.pd[j1][0], L.pd[j1][1]}, rd1[2] = {L.pd[j1][2], L.pd[j1][3]};
+        if (sv && lane < j) kc = make_key(fast_total<EXT>(slot, p, ed, rd, k), snode);
+        if (sv && lane < j1) kc1 = make_key(fast_total<EXT>(slot, p1, ed1, rd1, k), snode);
+      } else if (sv && lane < j) {
+        kc = make_key(fast_total<EXT>(slot, p, ed, rd, k), snode);
+      }
+      uint32_t tk = 0, tk1 = 0;
       if (tin) {  // T changes only when a pod of the batch reserves on it: pod j's T max is cached meanwhile
         t_row(j);  // (this wave's own LDS writes: in order)
         tk = L.sp.tmx[j];
+        if (has1) {
+          t_row(j1);
+          tk1 = L.sp.tmx[j1];
+        }
       }
       const uint32_t mx = max(wave_max_u32(kc), tk);
-      if (lane == 0) L.sp.mrow[j] = mx;
+      const uint32_t mx1 = has1 ? max(wave_max_u32(kc1), tk1) : 0u;
+      if (lane == 0) {
+        L.sp.mrow[j] = mx;
+        if (has1) L.sp.mrow[j1] = mx1;
+      }
     }
     __syncthreads();
     if (stamp && first) pst[2] = __builtin_amdgcn_s_memrealtime();
@@ -4560,8 +4686,15 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
   };
   if (sv) write_back(slot, snode, lanes_below(vm));
   if (tdirty) write_back(tslot, tnode, __popcll(vm) + lanes_below(tm));
-  if (sv) chg_clear_word(C, snode);  // every bit still set belongs to a taken node or to T
-  if (tv) chg_clear_word(C, tnode);
+  if (keep) {  // the changed nodes stay in the set as the next batch's T; T nodes no pod reserved leave it
+    if (sv) L.sp.tnext[lanes_below(vm)] = snode;
+    if (tdirty) L.sp.tnext[__popcll(vm) + lanes_below(tm)] = tnode;
+    if (lane == 0) L.sp.tnext_n = __popcll(vm) + __popcll(tm);
+    if (tv && !tdirty) chg_unset(C, tnode);
+  } else {  // every bit still set belongs to a taken node or to T
+    if (sv) chg_clear_word(C, snode);
+    if (tv) chg_clear_word(C, tnode);
+  }
   if (touched_out && lane == 0) st_sc1(touched_cnt, (int32_t)(__popcll(vm) + __popcll(tm)));
   if (lane == 0) {
     stamps[batch_index + 1] = __builtin_amdgcn_s_memrealtime();
@@ -4599,11 +4732,21 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
                                               uint64_t* __restrict__ dev_alloc, int64_t* __restrict__ numa_alloc,
                                               int64_t* __restrict__ touched_out = nullptr,
                                               int32_t* __restrict__ touched_cnt = nullptr,
-                                              const int64_t* __restrict__ tin = nullptr, int tin_n = 0,
+                                              const int64_t* __restrict__ tin = nullptr, bool keep = false,
                                               int LS = KMAX, bool sorted = false) {
   const int tid = threadIdx.x;
   constexpr int RES_THREADS = res_threads<NUMA>();
-  if (tid == 0) pstamps[8 * batch_index] = __builtin_amdgcn_s_memrealtime();
+  if (tid == 0) pstamps[PST * batch_index] = __builtin_amdgcn_s_memrealtime();
+  // candidate keys at stride LS, issued together with their counts and the pods' loads (one round trip;
+  // sc1: a concurrent launch wrote them), then the slots past a list's count zeroed
+  constexpr int U = MAX_BATCH * KSTALE / RES_THREADS;
+  const int lsh = LS == KSTALE ? 7 : 6, nk = MAX_BATCH * LS;
+  uint32_t q[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const int t = u * RES_THREADS + tid, j = t >> lsh;
+    q[u] = (t < nk && j < B) ? ld_sc1(cand + t) : 0u;
+  }
   if (tid < B) {
     L.cnt[tid] = ld_sc1(cand_cnt + tid);
     const DevPod pd = pods[base + tid];
@@ -4617,29 +4760,23 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
       L.dsc[tid] = (int32_t)s.dsb[DSB_CNT + tid];
     }
   }
-  __syncthreads();
-  {  // candidate keys at stride LS (sc1: a concurrent launch wrote them), unused slots zeroed
-    constexpr int U = MAX_BATCH * KSTALE / RES_THREADS;
-    const int lsh = LS == KSTALE ? 7 : 6, n = MAX_BATCH * LS;
-    uint32_t q[U];
+  if (tin && tid < B) L.sp.tver[tid] = -1;  // no pod's T max computed yet (replay_spec)
+  __syncthreads();  // the counts
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const int t = u * RES_THREADS + tid, j = t >> lsh, c = t & (LS - 1);
-      q[u] = (t < n && j < B && c < L.cnt[j]) ? ld_sc1(cand + t) : 0u;
-    }
-#pragma unroll
-    for (int u = 0; u < U; u++)
-      if (u * RES_THREADS + tid < n) L.cand[u * RES_THREADS + tid] = q[u];
+  for (int u = 0; u < U; u++) {
+    const int t = u * RES_THREADS + tid, j = t >> lsh, c = t & (LS - 1);
+    if (t < nk) L.cand[t] = (j < B && c < L.cnt[j]) ? q[u] : 0u;
   }
   __syncthreads();
   if (tid == 0) {
     const uint64_t t = __builtin_amdgcn_s_memrealtime();
-    for (int u = 1; u < 6; u++) pstamps[8 * batch_index + u] = t;
+    for (int u = 1; u < 6; u++) pstamps[PST * batch_index + u] = t;
+    for (int u = 8; u < 12; u++) pstamps[PST * batch_index + u] = t;
   }
   if constexpr (!DS && !NUMA && !QUOTA) {  // plain batch: the speculative replay on every wave
     __builtin_amdgcn_s_setprio(3);
     replay_spec<EXT>(L, C, s, base, B, k, chosen, chosen_score, global_offset, stamps, batch_index, dev_alloc,
-                     touched_out, touched_cnt, pstamps + 8 * batch_index, tin, tin_n, LS, sorted);
+                     touched_out, touched_cnt, pstamps + PST * batch_index, tin, keep, LS, sorted);
     __builtin_amdgcn_s_setprio(0);
     return;
   }
@@ -4647,7 +4784,7 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
   // the next batch's eval waves may share this SIMD (pipelined schedule): the replay issues first
   __builtin_amdgcn_s_setprio(3);
   replay_batch<DS, NUMA, QUOTA, EXT>(L, C, s, base, B, k, chosen, chosen_score, global_offset, stamps, batch_index,
-                                dev_alloc, numa_alloc, touched_out, touched_cnt, pstamps + 8 * batch_index);
+                                dev_alloc, numa_alloc, touched_out, touched_cnt, pstamps + PST * batch_index);
   __builtin_amdgcn_s_setprio(0);
 }
 
@@ -4926,7 +5063,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(SoA s, const De
   const ChgSet C = chg_init(L, chg_glb, n_nodes);
   resolve_batch<DS, NUMA, QUOTA>(L, C, s, pods, *batch_base, batch_pods, k, cand, cand_cnt, chosen, chosen_score,
                                  global_offset, stamps, pstamps, batch_index, dev_alloc, numa_alloc, nullptr, nullptr,
-                                 nullptr, 0, KMAX, sorted != 0);
+                                 nullptr, false, KMAX, sorted != 0);
 }
 
 // Persistent Reserve chain of a run of pipelined plain batches [b0, b0 + nb): one
@@ -4965,11 +5102,11 @@ __global__ __launch_bounds__(res_threads<false>()) void k_resolve_run(SoA s, con
     __syncthreads();
     if (!s_ok) return;
     const int par = b & 1;
-    const int64_t* tin = nofix && b > b0 ? touched_out : nullptr;
-    const int tin_n = tin ? ld_sc1(touched_cnt) : 0;  // the previous batch's wave 0 wrote it (drained, barrier)
+    const int64_t* tin = nofix && b > b0 ? touched_out : nullptr;  // the previous batch's changed records
+    const bool keep = nofix && b + 1 < b0 + nb;                     // this batch's are the next one's T
     resolve_batch<false, false, QUOTA, EXT>(L, C, s, pods, base, B, k, nofix ? stale + (int64_t)par * MAX_BATCH * KSTALE : cand,
                                        nofix ? stale_cnt + par * MAX_BATCH : cand_cnt, chosen, chosen_score, global_offset,
-                                       stamps, pstamps, b, dev_alloc, nullptr, touched_out, touched_cnt, tin, tin_n,
+                                       stamps, pstamps, b, dev_alloc, nullptr, touched_out, touched_cnt, tin, keep,
                                        nofix ? KSTALE : KMAX, !nofix || sorted != 0);  // (k_fixup's lists: by rank)
     __syncthreads();  // wave 0 drained its stores (replay_batch), so they are performed
     if (threadIdx.x == 0) st_sc1(done + b, 1);
@@ -5391,9 +5528,9 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
     chosen_score[base] = out_score;
     dev_alloc[base] = alloc;
     for (int q = 0; q < 4; q++) cpusets[(int64_t)base * 4 + q] = sh.set[q];
-    for (int u = 0; u < 6; u++) pstamps[8 * batch_index + u] = t0;  // no prologue: all "replay"
-    pstamps[8 * batch_index + 6] = 1;
-    pstamps[8 * batch_index + 7] = out_node >= 0;
+    for (int u = 0; u < 6; u++) pstamps[PST * batch_index + u] = t0;  // no prologue: all "replay"
+    pstamps[PST * batch_index + 6] = 1;
+    pstamps[PST * batch_index + 7] = out_node >= 0;
     stamps[batch_index + 1] = __builtin_amdgcn_s_memrealtime();
   }
 }
@@ -5415,6 +5552,45 @@ __global__ void k_batch_begin(uint64_t* stamp, uint32_t* dsb, uint32_t* argmax) 
 // ---------------------------------------------------------------------------------------------
 // device state
 // ---------------------------------------------------------------------------------------------
+// Page-locked host array: the async copies of a ke_schedule call to / from it neither stage nor block the
+// host thread (a pageable destination makes hipMemcpyAsync wait for the stream: every readback copy of a call
+// would then sit on its critical path one after another).
+template <typename T>
+struct PinnedVec {
+  T* p = nullptr;
+  size_t n = 0, cap = 0;
+  PinnedVec() = default;
+  PinnedVec(const PinnedVec&) = delete;
+  PinnedVec& operator=(const PinnedVec&) = delete;
+  ~PinnedVec() {
+    if (p) (void)hipHostFree(p);
+  }
+  bool resize(size_t m) {  // contents not kept when it grows
+    if (m > cap) {
+      if (p) (void)hipHostFree(p);
+      p = nullptr;
+      cap = 0;
+      if (hipHostMalloc((void**)&p, sizeof(T) * std::max<size_t>(m, 1), hipHostMallocDefault) != hipSuccess) {
+        p = nullptr;
+        n = 0;
+        return false;
+      }
+      cap = m;
+    }
+    n = m;
+    return true;
+  }
+  T* data() { return p; }
+  const T* data() const { return p; }
+  size_t size() const { return n; }
+  T& operator[](size_t i) { return p[i]; }
+  const T& operator[](size_t i) const { return p[i]; }
+  T* begin() { return p; }
+  T* end() { return p + n; }
+  const T* begin() const { return p; }
+  const T* end() const { return p + n; }
+};
+
 struct DeviceState {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -5463,7 +5639,8 @@ struct DeviceState {
   uint64_t* d_devalloc = nullptr;  // [n_pods] device minors allocated per pod
   int64_t* d_dsrows = nullptr;   // staging for DeviceShare row uploads
   int64_t ds_staging_cap = 0;
-  std::vector<DevPod> host_pods;  // the last uploaded queue (batch segmentation)
+  PinnedVec<DevPod> host_pods;    // the last uploaded queue (batch segmentation), page-locked
+  PinnedVec<uint8_t> h_out;       // ke_schedule's readback staging (placements, allocations, stamps)
   std::vector<DevPodHint> host_ph;  // its hinted pods' records (the async upload reads them)
   // NUMA topology
   bool numa_alloc = false;         // soa.nf / soa.nm allocated
@@ -5993,8 +6170,8 @@ int device_refresh(Context* ctx, int64_t now) {
 
 static int upload_pods(Context* ctx, int32_t n_pods, const ke_pod* pods) {
   DeviceState* d = ctx->dev;
-  std::vector<DevPod>& dp = d->host_pods;
-  dp.resize((size_t)n_pods);
+  PinnedVec<DevPod>& dp = d->host_pods;
+  if (!dp.resize((size_t)n_pods)) return fail(KE_ERR_DEVICE, "hipHostMalloc of the pod staging buffer");
   std::vector<DevPodHint>& ph = d->host_ph;  // the hinted pods' records; DevPod::ring_bw = slot
   ph.clear();
   // the argument checks of this call staged the records (check_cpuset); pods may be a segment of them
@@ -6175,7 +6352,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     d->d_numaalloc = nullptr;
     HIP_OK(hipMalloc(&d->d_chosen, out_bytes));
     HIP_OK(hipMalloc(&d->d_chosen_score, out_bytes));
-    HIP_OK(hipMalloc(&d->d_stamps, sizeof(uint64_t) * 10 * ((int64_t)n_pods + 2)));
+    HIP_OK(hipMalloc(&d->d_stamps, sizeof(uint64_t) * (PST + 2) * ((int64_t)n_pods + 2)));
     HIP_OK(hipMalloc(&d->d_devalloc, sizeof(uint64_t) * n_pods));
     d->out_cap = n_pods;
   }
@@ -6274,13 +6451,19 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     for (auto& e : ev) HIP_OK(hipEventCreate(&e));
   }
   const bool sharded = d->world > 1 || d->comm;
-  uint64_t* estamps = d->d_stamps + 9 * ((int64_t)n_pods + 2);  // eval start of each batch
+  uint64_t* estamps = d->d_stamps + (PST + 1) * ((int64_t)n_pods + 2);  // eval start of each batch
   constexpr int R = DeviceState::EV_RING;
   int n_pipelined = 0;
   // Batch b's eval + candidate lists on stream `es`.  pipe: stale top-(k_j + KMAX) lists into the run's
   // stale buffer (k_fixup makes them exact); else the exact top-k_j lists straight into d_cand.
   bool rerun = false;  // the current serial batch is the remainder of a DeviceShare batch that stopped early
-  auto eval_select = [&](int b, bool pipe, hipStream_t es) -> int {
+  // dwait (pipelined, stale lists): the eval first waits for that done flag -- in k_eval_plain itself, else a
+  // k_handoff ahead of it; rpub: the select publishes the lists to the running Reserve kernel itself when it
+  // can (split or one-workgroup select, unsharded) -- *published tells the caller
+  bool published = false;
+  auto eval_select = [&](int b, bool pipe, hipStream_t es, const int32_t* dwait = nullptr,
+                         int32_t* rpub = nullptr) -> int {
+    published = false;
     const int bp = batches[b].pods;
     const bool ds = batches[b].ds, cpu = batches[b].cpu;
     const bool prof = every > 0 && b % every == 0;
@@ -6317,9 +6500,13 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                                      : ((k.flags & AF_EXT) ? k_eval_batch<false, false, false, true>
                                                            : k_eval_batch<false, false, false>));
         uint32_t* dcnt = numa ? d->d_defer_cnt + b : nullptr;
-        if (!cpu && !ds && !numa && use_record_eval(bp))  // plain batch: the record-based evaluation
+        const bool plain_rec = !cpu && !ds && !numa && use_record_eval(bp);
+        if (dwait && !plain_rec)
+          hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), 0, es, nullptr, 0, dwait, d_err, nullptr);
+        if (plain_rec)  // plain batch: the record-based evaluation
           hipLaunchKernelGGL(((k.flags & AF_EXT) ? k_eval_plain<true> : k_eval_plain<false>), grid, dim3(eb), 0, es, d->soa,
-                             lo, hi, d->d_pods, bbase, bp, k, d->d_scores, d->capacity, fold_begin ? estamps + b : nullptr);
+                             lo, hi, d->d_pods, bbase, bp, k, d->d_scores, d->capacity, fold_begin ? estamps + b : nullptr,
+                             dwait, d_err);
         else
           hipLaunchKernelGGL(eval, grid, dim3(eb), 0, es, d->soa, lo, hi, d->d_pods, bbase, bp,
                              ppb, k, d->d_scores, d->capacity, d->d_dsraw, d->d_defer, dcnt, d->d_aff, d->d_dsmax,
@@ -6341,12 +6528,12 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       if (ds && sharded && !d->loopback)  // DefaultNormalizeScore's max over the feasible nodes of all ranks
         RCCL_OK(ncclAllReduce(d->d_dsmax, d->d_dsmax, 1, ncclUint32, ncclMax, d->comm, es));
       if (prof) HIP_OK(hipEventRecord(pe[1], es));
-      auto select = [&](int slo, int shi, uint32_t* cand, int32_t* cnt) {
+      auto select = [&](int slo, int shi, uint32_t* cand, int32_t* cnt, int32_t* pub) {
         // register-resident when a wave's segment fits SEL_RC steps, else streamed
         const bool rc = select_seg(slo, shi) <= SEL_RC * 512;
         auto sel = ds ? (rc ? k_select<true, SEL_RC> : k_select<true, 0>) : (rc ? k_select<false, SEL_RC> : k_select<false, 0>);
         hipLaunchKernelGGL(sel, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, es, d->d_scores, d->capacity, slo, shi, cand,
-                           cnt, d->d_dsraw, d->d_dsmax, k.wp_ds, kext, L, (int64_t)0, nullptr, nullptr, nullptr);
+                           cnt, d->d_dsraw, d->d_dsmax, k.wp_ds, kext, L, (int64_t)0, nullptr, nullptr, nullptr, pub);
       };
       // a plain batch over many nodes: its pods' selections split over several workgroups each (>= 256
       // workgroups in all, parts of >= 4096 nodes), merged by k_merge
@@ -6363,9 +6550,11 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
         hipLaunchKernelGGL((rc ? k_select<false, SEL_RC> : k_select<false, 0>), dim3((unsigned)bp, (unsigned)parts),
                            dim3(SELECT_BLOCK), 0, es, d->d_scores, d->capacity, 0, (int)N, d->d_split,
                            reinterpret_cast<int32_t*>(d->d_split + MAX_BATCH * L), d->d_dsraw, d->d_dsmax, k.wp_ds,
-                           kext, L, (int64_t)gw, lists, lists_cnt, d->d_parts_done);  // the last part merges
+                           kext, L, (int64_t)gw, lists, lists_cnt, d->d_parts_done, rpub);  // the last part merges
+        published = rpub != nullptr;
       } else if (!sharded) {
-        select(0, N, lists, lists_cnt);
+        select(0, N, lists, lists_cnt, ds ? nullptr : rpub);
+        published = rpub != nullptr && !ds;
       } else {
         // node-sharded: per-shard top-k_j, all-gather, merge
         const int gw = gath_words(L);
@@ -6374,7 +6563,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
           int slo, shi;
           shard_range(N, r, d->world, &slo, &shi);
           uint32_t* blk = d->d_gath + (int64_t)r * gw;
-          select(slo, shi, blk, reinterpret_cast<int32_t*>(blk + MAX_BATCH * L));
+          select(slo, shi, blk, reinterpret_cast<int32_t*>(blk + MAX_BATCH * L), nullptr);
         }
         if (!d->loopback) {
           uint32_t* mine = d->d_gath + (int64_t)d->rank * gw;  // in place: send = own block of recv
@@ -6422,14 +6611,17 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                          fixup ? nullptr : d->d_stale, fixup ? nullptr : d->d_stale_cnt, (int)run_sorted(r0, e));
       if (r0 > 0) HIP_OK(hipStreamWaitEvent(d->estream, d->ev_res[(r0 - 1) % R], 0));
       for (int q = r0; q < e; q++) {
-        rc = eval_select(q, true, d->estream);
-        if (rc) return rc;
         const bool first = q == r0;
-        if (!fixup) {  // the stale lists go to the replay as they are; batch q+1's eval waits for batch q-1
-          hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), 0, d->estream, d_ready + q, (int32_t)batches[q].pods,
-                             first ? nullptr : d_done + (q - 1), d_err, d_fst + 2 * q);
+        if (!fixup) {  // the stale lists go to the replay as they are; batch q's eval waits for batch q-2's done
+          rc = eval_select(q, true, d->estream, q - 2 >= r0 ? d_done + (q - 2) : nullptr, d_ready + q);
+          if (rc) return rc;
+          if (!published)
+            hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), 0, d->estream, d_ready + q, (int32_t)batches[q].pods, nullptr,
+                               d_err, nullptr);
           continue;
         }
+        rc = eval_select(q, true, d->estream);
+        if (rc) return rc;
         hipLaunchKernelGGL((ext ? k_fixup<true> : k_fixup<false>), dim3((unsigned)batches[q].pods), dim3(FIX_BLOCK), 0, d->estream, d->soa, d->d_pods,
                            d_bases + q, k, d->d_stale + (size_t)(q & 1) * MAX_BATCH * KSTALE,
                            d->d_stale_cnt + (q & 1) * MAX_BATCH, d->d_trows, d->d_tcnt, d->d_cand, d->d_cand_cnt,
@@ -6496,36 +6688,44 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   tp = clk::now();
   flush_mirror(*ctx);  // the previous call's deferred host mirror, while the device works
   HIP_OK(hipEventRecord(e1, d->stream));
-  HIP_OK(hipMemcpyAsync(chosen, d->d_chosen, out_bytes, hipMemcpyDeviceToHost, d->stream));
-  if (score) HIP_OK(hipMemcpyAsync(score, d->d_chosen_score, out_bytes, hipMemcpyDeviceToHost, d->stream));
-  ctx->last_dev_alloc.assign((size_t)n_pods, 0);
-  HIP_OK(hipMemcpyAsync(ctx->last_dev_alloc.data(), d->d_devalloc, sizeof(uint64_t) * n_pods, hipMemcpyDeviceToHost,
-                        d->stream));
-  ctx->last_cpusets.assign((size_t)n_pods * 4, 0);
-  HIP_OK(hipMemcpyAsync(ctx->last_cpusets.data(), d->d_cpusets, sizeof(uint64_t) * 4 * n_pods, hipMemcpyDeviceToHost,
-                        d->stream));
-  ctx->last_vf.assign(d->soa.vfo ? (size_t)n_pods * 2 * DS_MINORS : 0, -1);
-  if (d->soa.vfo)
-    HIP_OK(hipMemcpyAsync(ctx->last_vf.data(), d->d_vfo, 2 * DS_MINORS * (size_t)n_pods, hipMemcpyDeviceToHost, d->stream));
-  ctx->last_numa_alloc.clear();
-  if (numa) {
-    ctx->last_numa_alloc.assign((size_t)n_pods * 16, 0);
-    HIP_OK(hipMemcpyAsync(ctx->last_numa_alloc.data(), d->d_numaalloc, sizeof(int64_t) * 16 * n_pods,
-                          hipMemcpyDeviceToHost, d->stream));
-  }
-  std::vector<uint64_t> st((size_t)n_batches + 1), pst(8 * (size_t)n_batches), est((size_t)n_batches),
-      fst(2 * (size_t)n_batches);
+  // The call's outputs go to one page-locked staging area (async copies, no host wait) and are copied out after
+  // the synchronisation; allocations none of the call's batches can make are not read back (zero).
+  bool any_ds = false;
+  for (const Batch& bt : batches) any_ds = any_ds || bt.ds || bt.hint;
+  const bool vf_out = d->soa.vfo != nullptr;
+  const size_t np = (size_t)n_pods, nb = (size_t)n_batches;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off = (off + bytes + 15) & ~(size_t)15;
+    return o;
+  };
+  const size_t o_chosen = take((size_t)out_bytes), o_score = take(score ? (size_t)out_bytes : 0),
+               o_dev = take(any_ds ? 8 * np : 0), o_cs = take(any_cpu ? 32 * np : 0),
+               o_vf = take(vf_out ? 2 * DS_MINORS * np : 0), o_numa = take(numa ? 8 * 16 * np : 0), o_err = take(8),
+               o_fst = take(16 * nb), o_dcnt = take(numa ? 4 * nb : 0), o_st = take(8 * (nb + 1)),
+               o_pst = take(8 * PST * nb), o_est = take(8 * nb);
+  if (!d->h_out.resize(off)) return fail(KE_ERR_DEVICE, "hipHostMalloc of the readback staging buffer");
+  uint8_t* const h = d->h_out.data();
+  auto d2h = [&](size_t o, const void* src, size_t bytes) -> int {
+    if (bytes) HIP_OK(hipMemcpyAsync(h + o, src, bytes, hipMemcpyDeviceToHost, d->stream));
+    return KE_OK;
+  };
+  if ((rc = d2h(o_chosen, d->d_chosen, (size_t)out_bytes))) return rc;
+  if (score && (rc = d2h(o_score, d->d_chosen_score, (size_t)out_bytes))) return rc;
+  if (any_ds && (rc = d2h(o_dev, d->d_devalloc, 8 * np))) return rc;
+  if (any_cpu && (rc = d2h(o_cs, d->d_cpusets, 32 * np))) return rc;
+  if (vf_out && (rc = d2h(o_vf, d->d_vfo, 2 * DS_MINORS * np))) return rc;
+  if (numa && (rc = d2h(o_numa, d->d_numaalloc, 8 * 16 * np))) return rc;
+  if ((rc = d2h(o_err, d_err, 4)) || (rc = d2h(o_err + 4, d->soa.kerr, 4))) return rc;
+  if ((rc = d2h(o_fst, d_fst, 16 * nb))) return rc;
+  if (numa && (rc = d2h(o_dcnt, d->d_defer_cnt, 4 * nb))) return rc;
+  if ((rc = d2h(o_st, d->d_stamps, 8 * (nb + 1))) || (rc = d2h(o_pst, d->d_stamps + (n_pods + 2), 8 * PST * nb)) ||
+      (rc = d2h(o_est, estamps, 8 * nb)))
+    return rc;
+  std::vector<uint64_t> st(nb + 1), pst(PST * nb), est(nb), fst(2 * nb);
+  std::vector<uint32_t> dcnt(numa ? nb : 0);
   int32_t herr = 0, kerr = 0;
-  HIP_OK(hipMemcpyAsync(&herr, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, d->stream));
-  HIP_OK(hipMemcpyAsync(&kerr, d->soa.kerr, sizeof(int32_t), hipMemcpyDeviceToHost, d->stream));
-  HIP_OK(hipMemcpyAsync(fst.data(), d_fst, sizeof(uint64_t) * 2 * n_batches, hipMemcpyDeviceToHost, d->stream));
-  std::vector<uint32_t> dcnt(numa ? (size_t)n_batches : 0);
-  if (numa)
-    HIP_OK(hipMemcpyAsync(dcnt.data(), d->d_defer_cnt, sizeof(uint32_t) * n_batches, hipMemcpyDeviceToHost, d->stream));
-  HIP_OK(hipMemcpyAsync(st.data(), d->d_stamps, sizeof(uint64_t) * (n_batches + 1), hipMemcpyDeviceToHost, d->stream));
-  HIP_OK(hipMemcpyAsync(pst.data(), d->d_stamps + (n_pods + 2), sizeof(uint64_t) * 8 * n_batches,
-                        hipMemcpyDeviceToHost, d->stream));
-  HIP_OK(hipMemcpyAsync(est.data(), estamps, sizeof(uint64_t) * n_batches, hipMemcpyDeviceToHost, d->stream));
   // while the device runs: the host copies of the segment's pods for the deferred mirror (flush_mirror;
   // ke_schedule records which of them were placed)
   ctx->pending_base = (int64_t)ctx->pending_pods.size();
@@ -6533,6 +6733,37 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   HIP_OK(hipStreamSynchronize(d->stream));
   HIP_OK(hipStreamSynchronize(d->estream));
   const auto t_sync = clk::now();
+  std::memcpy(chosen, h + o_chosen, (size_t)out_bytes);
+  if (score) std::memcpy(score, h + o_score, (size_t)out_bytes);
+  if (any_ds) {
+    ctx->last_dev_alloc.resize(np);
+    std::memcpy(ctx->last_dev_alloc.data(), h + o_dev, 8 * np);
+  } else {
+    ctx->last_dev_alloc.clear();  // (readers take absent entries as zero)
+  }
+  if (any_cpu) {
+    ctx->last_cpusets.resize(4 * np);
+    std::memcpy(ctx->last_cpusets.data(), h + o_cs, 32 * np);
+  } else {
+    ctx->last_cpusets.clear();
+  }
+  ctx->last_vf.clear();
+  if (vf_out) {
+    ctx->last_vf.resize(2 * DS_MINORS * np);
+    std::memcpy(ctx->last_vf.data(), h + o_vf, 2 * DS_MINORS * np);
+  }
+  ctx->last_numa_alloc.clear();
+  if (numa) {
+    ctx->last_numa_alloc.resize(16 * np);
+    std::memcpy(ctx->last_numa_alloc.data(), h + o_numa, 8 * 16 * np);
+    std::memcpy(dcnt.data(), h + o_dcnt, 4 * nb);
+  }
+  std::memcpy(&herr, h + o_err, 4);
+  std::memcpy(&kerr, h + o_err + 4, 4);
+  std::memcpy(fst.data(), h + o_fst, 16 * nb);
+  std::memcpy(st.data(), h + o_st, 8 * (nb + 1));
+  std::memcpy(pst.data(), h + o_pst, 8 * PST * nb);
+  std::memcpy(est.data(), h + o_est, 8 * nb);
   ctx->host_ms[5] = ms_since(tp);
   tp = clk::now();
   if (herr) {
@@ -6582,7 +6813,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   // write-back (the one-wave replay of other batches counts entirely as write-back)
   double ph[6] = {0, 0, 0, 0, 0, 0};
   for (int b = 0; b < n_batches; b++) {
-    const uint64_t* p = &pst[8 * (size_t)b];
+    const uint64_t* p = &pst[PST * (size_t)b];
     pro += (double)(p[4] - p[0]) * ms_per_tick;
     loop += (double)(st[b + 1] - p[4]) * ms_per_tick;
     const bool spec = p[1] > p[4];
@@ -6596,6 +6827,21 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   ctx->kstat_resolve_prologue_ms = pro / n_batches;
   ctx->kstat_resolve_loop_ms = loop / n_batches;
   for (int i = 0; i < 6; i++) ctx->kstat_resolve_phase_ms[i] = ph[i] * ms_per_tick / n_batches;
+  {  // the speculative replay's first round in detail: T set-up, the prediction loop, wave 1's T
+     // rows (concurrent with the loop), wave 0's R
+    double sub[4] = {0, 0, 0, 0};
+    int ns = 0;
+    for (int b = 0; b < n_batches; b++) {
+      const uint64_t* p = &pst[PST * (size_t)b];
+      if (!(p[1] > p[4])) continue;
+      ns++;
+      sub[0] += (double)(p[8] - p[4]);
+      sub[1] += (double)(p[9] > p[8] ? p[9] - p[8] : 0);
+      sub[2] += (double)(p[10] > p[8] ? p[10] - p[8] : 0);
+      sub[3] += (double)(p[11] > p[1] ? p[11] - p[1] : 0);
+    }
+    for (int i = 0; i < 4; i++) ctx->kstat_resolve_sub_ms[i] = ns ? sub[i] * ms_per_tick / ns : 0;
+  }
   ctx->kstat_numa_deferred = 0;
   for (uint32_t c : dcnt) ctx->kstat_numa_deferred += c;
   // per-batch Reserve time from the in-kernel stamps (start of the batch's prologue -> end of its
@@ -6603,24 +6849,28 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   // fixup = k_fixup's workgroup 0 from its wait to its publish
   double res_sum = 0, ho_sum = 0, fx_sum = 0;
   int ho_n = 0, fx_n = 0;
+  std::vector<char> in_run((size_t)n_batches, 0);  // a pipelined batch after the first of its run
+  for (int b = 0; b < n_batches; b++)
+    if (run_end[b] > 0)
+      for (int q = b + 1; q < run_end[b]; q++) in_run[(size_t)q] = 1;
   for (int b = 0; b < n_batches; b++) {
-    res_sum += (double)(st[b + 1] - pst[8 * (size_t)b]) * ms_per_tick;
+    res_sum += (double)(st[b + 1] - pst[PST * (size_t)b]) * ms_per_tick;
     if (fst[2 * b + 1] > fst[2 * b]) {
       fx_sum += (double)(fst[2 * b + 1] - fst[2 * b]) * ms_per_tick;
       fx_n++;
-      if (run_end[b] == 0 && b > 0) {
-        ho_sum += (double)(pst[8 * (size_t)b] - st[b]) * ms_per_tick;
-        ho_n++;
-      }
+    }
+    if (in_run[(size_t)b] && pst[PST * (size_t)b] > st[b]) {
+      ho_sum += (double)(pst[PST * (size_t)b] - st[b]) * ms_per_tick;
+      ho_n++;
     }
   }
   ctx->kstat_resolve_ms = n_batches ? res_sum / n_batches : 0;
   double rows_fetched = 0, rows_changed = 0;
   double spec_rounds = 0;
   for (int b = 0; b < n_batches; b++) {
-    rows_fetched += (double)(pst[8 * (size_t)b + 6] & 0xFFFFFFFFull);
-    spec_rounds += (double)(pst[8 * (size_t)b + 6] >> 32);
-    rows_changed += (double)pst[8 * (size_t)b + 7];
+    rows_fetched += (double)(pst[PST * (size_t)b + 6] & 0xFFFFFFFFull);
+    spec_rounds += (double)(pst[PST * (size_t)b + 6] >> 32);
+    rows_changed += (double)pst[PST * (size_t)b + 7];
   }
   ctx->kstat_spec_failed = n_batches ? spec_rounds / n_batches : 0;
   ctx->kstat_rows_fetched = n_batches ? rows_fetched / n_batches : 0;
@@ -6695,7 +6945,7 @@ int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t 
   auto launch = [&]() {
     if (use_record_eval(n_pods))
       hipLaunchKernelGGL((k_eval_plain<false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N, d->d_pods,
-                         d->d_batch_base, n_pods, k, d->d_scores, d->capacity, nullptr);
+                         d->d_batch_base, n_pods, k, d->d_scores, d->capacity, nullptr, nullptr, nullptr);
     else
       hipLaunchKernelGGL((k_eval_batch<false, false, false>), grid, dim3(EVAL_BLOCK), 0, d->stream, d->soa, 0, N,
                          d->d_pods, d->d_batch_base, n_pods, ppb, k, d->d_scores, d->capacity, d->d_dsraw, d->d_defer,

@@ -37,6 +37,7 @@ class Evaluator:
         h = C.c_void_p()
         self._check(self.lib.ke_create(C.byref(cfg), C.byref(h)))
         self.h = h
+        self._last_n, self._last_out = 0, {}
 
     # ---- plumbing --------------------------------------------------------------------------
     def _check(self, rc):
@@ -244,17 +245,34 @@ class Evaluator:
         chosen = np.zeros(len(pods), np.int32)
         score = np.zeros(len(pods), np.int32)
         self._check(self.lib.ke_schedule(self.h, len(pods), abi.ptr(pods), int(now_ns), abi.ptr(chosen), abi.ptr(score)))
-        self.last_device_allocations = np.zeros(len(pods), np.uint64)
-        self._check(self.lib.ke_last_device_allocations(self.h, len(pods), abi.ptr(self.last_device_allocations)))
-        self.last_numa_allocations = np.zeros((len(pods), 16), np.int64)
-        self._check(self.lib.ke_last_numa_allocations(self.h, len(pods), abi.ptr(self.last_numa_allocations)))
-        self.last_cpusets = np.zeros((len(pods), 4), np.uint64)
-        self._check(self.lib.ke_last_cpusets(self.h, len(pods), abi.ptr(self.last_cpusets)))
+        self._last_n, self._last_out = len(pods), {}  # the per-pod allocations are read on first access
         return chosen, score
+
+    def _last(self, name, shape, dtype, fn):
+        if name not in self._last_out:
+            a = np.zeros(shape, dtype)
+            self._check(getattr(self.lib, fn)(self.h, self._last_n, abi.ptr(a)))
+            self._last_out[name] = a
+        return self._last_out[name]
+
+    @property
+    def last_device_allocations(self):
+        """ke_last_device_allocations of the last schedule(): allocated minors per pod."""
+        return self._last("dev", self._last_n, np.uint64, "ke_last_device_allocations")
+
+    @property
+    def last_numa_allocations(self):
+        """ke_last_numa_allocations of the last schedule(): [pod][NUMA id * 2 + resource]."""
+        return self._last("numa", (self._last_n, 16), np.int64, "ke_last_numa_allocations")
+
+    @property
+    def last_cpusets(self):
+        """ke_last_cpusets of the last schedule(): 256-bit CPU-id set per pod."""
+        return self._last("cpus", (self._last_n, 4), np.uint64, "ke_last_cpusets")
 
     def last_allocations(self, n=None):
         """Release records (np.ndarray POD_ALLOCATION_DTYPE) of the pods of the last schedule()."""
-        n = len(self.last_device_allocations) if n is None else n
+        n = self._last_n if n is None else n
         out = np.zeros(n, abi.POD_ALLOCATION_DTYPE)
         self._check(self.lib.ke_last_allocations(self.h, n, abi.ptr(out)))
         return out
@@ -341,12 +359,15 @@ class Evaluator:
         self._check(self.lib.ke_debug_spec_failed(self.h, C.byref(sf)))
         ph = np.zeros(6, np.float64)
         self._check(self.lib.ke_debug_resolve_phases(self.h, abi.ptr(ph)))
+        sub = np.zeros(4, np.float64)
+        self._check(self.lib.ke_debug_resolve_subphases(self.h, abi.ptr(sub)))
         return {"eval_ms": ms4[0], "select_ms": ms4[1], "fixup_ms": ms4[2], "resolve_ms": ms4[3], "samples": n.value,
                 "pipelined_batches": npipe.value, "enqueue_ms": ms4[4], "handoff_ms": ms4[5],
                 "rows_fetched": ms4[6], "rows_changed": ms4[7], "spec_failed_rounds": sf.value,
                 "resolve_prologue_ms": p.value, "resolve_replay_ms": r.value,
-                "resolve_phases_ms": dict(zip(["prologue", "spec_predict", "spec_reserve_eval", "spec_verify", "spec_later_rounds", "writeback"],
-                                              ph.tolist()))}
+                "resolve_phases_ms": dict(zip(["prologue", "spec_predict", "spec_reserve_eval", "spec_verify", "spec_later_rounds", "writeback",
+                                               "sub_t_setup", "sub_predict_loop", "sub_t_rows_wave1", "sub_reserve_R"],
+                                              ph.tolist() + sub.tolist()))}
 
     def bench_eval_kernel(self, pods, now_ns, iters):
         pods = as_pod_array(pods)
