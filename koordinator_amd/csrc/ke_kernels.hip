@@ -2862,9 +2862,9 @@ __device__ __forceinline__ void rec_store_dyn(int64_t* rec, const NodeFast& f) {
   __hip_atomic_store(rec + RW_NREQ0S, (int64_t)__double_as_longlong(f.nreq0s), __ATOMIC_RELAXED, SCOPE);
 }
 
-// a full record (sc1) with the node index in RW_PAD: the compact changed list k_fixup reads
-__device__ __forceinline__ void rec_store_full(int64_t* r, const NodeFast& f, int node) {
-  int64_t w[NUM_RW];
+// a full record with the node index in RW_PAD
+template <typename W>
+__device__ __forceinline__ void rec_to_words(const NodeFast& f, int node, W& w) {
 #pragma unroll
   for (int v = 0; v < 2; v++)
 #pragma unroll
@@ -2888,6 +2888,11 @@ __device__ __forceinline__ void rec_store_full(int64_t* r, const NodeFast& f, in
   w[RW_FLAGS] = (int64_t)(((uint64_t)f.sbits << 32) | f.nflags);
   w[RW_NWS] = f.nws;
   w[RW_PAD] = node;
+}
+// ... stored sc1: the compact changed list k_fixup reads
+__device__ __forceinline__ void rec_store_full(int64_t* r, const NodeFast& f, int node) {
+  int64_t w[NUM_RW];
+  rec_to_words(f, node, w);
 #pragma unroll
   for (int u = 0; u < NUM_RW; u++) st_sc1(r + u, w[u]);
 }
@@ -4175,10 +4180,10 @@ __device__ __forceinline__ void load_row_sc1(const SoA& s, int64_t i, Row& r) {
   r.pad = 0;
 }
 
-// Changed-node set of the batch being replayed: a bitmap over node ids, in LDS for ids < 917,504 (else a
+// Changed-node set of the batch being replayed: a bitmap over node ids, in LDS for ids < 811,008 (else a
 // zeroed device bitmap in global memory, sc1-accessed).  Only the replay wave touches it; the bits of a
 // batch are cleared when it ends, so it is zero between batches.
-constexpr int CHG_LDS_WORDS = 28672;  // node ids < 917,504 (else the global bitmap)
+constexpr int CHG_LDS_WORDS = 25344;  // node ids < 811,008 (else the global bitmap)
 struct ChgSet {
   uint32_t* lds;
   uint32_t* glb;  // non-null: node ids beyond the LDS bitmap
@@ -4336,6 +4341,7 @@ struct ResLdsCore {
   uint32_t dsm[MAX_BATCH];  // DeviceShare batch: 1 + snapshot max raw score of each pod (0: none / not DS)
   int32_t dsc[MAX_BATCH];   // ... and the number of its feasible nodes attaining it
   SpecLds sp;
+  int64_t trec[MAX_BATCH][NUM_RW];  // the last batch's changed records (stale lists: the next batch's T slots)
   uint32_t chg[CHG_LDS_WORDS];
 };
 // The Reserve kernels take the CU's whole LDS (160 KB, less 64 B for a kernel's own words): no workgroup of
@@ -4464,7 +4470,7 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
                                             uint64_t* __restrict__ stamps, int batch_index,
                                             uint64_t* __restrict__ dev_alloc, int64_t* __restrict__ touched_out,
                                             int32_t* __restrict__ touched_cnt, uint64_t* __restrict__ pst,
-                                            const int64_t* __restrict__ tin, bool keep, int LS, bool sorted) {
+                                            bool has_t, bool keep, int LS, bool sorted) {
   constexpr int NW = res_threads<false>() / 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const bool ext = EXT && (k.flags & AF_EXT);
@@ -4475,12 +4481,16 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
   NodeFast tslot;  // lane t: node t of the previous batch's changed set T (stale lists only)
   bool tv = false, tdirty = false;
   int tnode = -1;
-  // T: the previous batch of the run left its changed nodes' bits set in the changed set and their ids in
-  // L.sp.tnext; their current records are in `tin` (loaded now, adopted at first use: they land during P)
-  const int tin_n = tin ? L.sp.tnext_n : 0;
+  // T: the previous batch of the run left its changed nodes' bits set in the changed set, their ids in
+  // L.sp.tnext and their current records in L.trec
+  const int64_t* const tin = has_t ? &L.trec[0][0] : nullptr;  // (non-null: T present)
+  const int tin_n = has_t ? L.sp.tnext_n : 0;
   if (lane < tin_n) {
     tnode = L.sp.tnext[lane];
-    rec_load<__HIP_MEMORY_SCOPE_AGENT>(tin + (int64_t)lane * NUM_RW, tslot);
+    int64_t w[NUM_RW];
+#pragma unroll
+    for (int u = 0; u < NUM_RW; u++) w[u] = L.trec[lane][u];
+    rec_unpack(w, tslot);
     tv = true;
   }
   bool t_adopted = false;
@@ -4682,7 +4692,8 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
     st_sc1(fr + (F_NREQ + 1) * st, (int64_t)f.nreq[1]);
     rec_store_dyn<__HIP_MEMORY_SCOPE_AGENT>(s.rec + (int64_t)node * NUM_RW, f);  // sc1: read by k_eval_plain
     if (ext) ext_store(s, node, f, k);
-    if (touched_out) rec_store_full(touched_out + (int64_t)pos * NUM_RW, f, node);
+    if (keep) rec_to_words(f, node, L.trec[pos]);  // the next batch's T slot
+    else if (touched_out) rec_store_full(touched_out + (int64_t)pos * NUM_RW, f, node);
   };
   if (sv) write_back(slot, snode, lanes_below(vm));
   if (tdirty) write_back(tslot, tnode, __popcll(vm) + lanes_below(tm));
@@ -4732,8 +4743,8 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
                                               uint64_t* __restrict__ dev_alloc, int64_t* __restrict__ numa_alloc,
                                               int64_t* __restrict__ touched_out = nullptr,
                                               int32_t* __restrict__ touched_cnt = nullptr,
-                                              const int64_t* __restrict__ tin = nullptr, bool keep = false,
-                                              int LS = KMAX, bool sorted = false) {
+                                              bool has_t = false, bool keep = false, int LS = KMAX,
+                                              bool sorted = false) {
   const int tid = threadIdx.x;
   constexpr int RES_THREADS = res_threads<NUMA>();
   if (tid == 0) pstamps[PST * batch_index] = __builtin_amdgcn_s_memrealtime();
@@ -4760,7 +4771,7 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
       L.dsc[tid] = (int32_t)s.dsb[DSB_CNT + tid];
     }
   }
-  if (tin && tid < B) L.sp.tver[tid] = -1;  // no pod's T max computed yet (replay_spec)
+  if (has_t && tid < B) L.sp.tver[tid] = -1;  // no pod's T max computed yet (replay_spec)
   __syncthreads();  // the counts
 #pragma unroll
   for (int u = 0; u < U; u++) {
@@ -4776,7 +4787,7 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
   if constexpr (!DS && !NUMA && !QUOTA) {  // plain batch: the speculative replay on every wave
     __builtin_amdgcn_s_setprio(3);
     replay_spec<EXT>(L, C, s, base, B, k, chosen, chosen_score, global_offset, stamps, batch_index, dev_alloc,
-                     touched_out, touched_cnt, pstamps + PST * batch_index, tin, keep, LS, sorted);
+                     touched_out, touched_cnt, pstamps + PST * batch_index, has_t, keep, LS, sorted);
     __builtin_amdgcn_s_setprio(0);
     return;
   }
@@ -5063,7 +5074,7 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(SoA s, const De
   const ChgSet C = chg_init(L, chg_glb, n_nodes);
   resolve_batch<DS, NUMA, QUOTA>(L, C, s, pods, *batch_base, batch_pods, k, cand, cand_cnt, chosen, chosen_score,
                                  global_offset, stamps, pstamps, batch_index, dev_alloc, numa_alloc, nullptr, nullptr,
-                                 nullptr, false, KMAX, sorted != 0);
+                                 false, false, KMAX, sorted != 0);
 }
 
 // Persistent Reserve chain of a run of pipelined plain batches [b0, b0 + nb): one
@@ -5102,11 +5113,11 @@ __global__ __launch_bounds__(res_threads<false>()) void k_resolve_run(SoA s, con
     __syncthreads();
     if (!s_ok) return;
     const int par = b & 1;
-    const int64_t* tin = nofix && b > b0 ? touched_out : nullptr;  // the previous batch's changed records
-    const bool keep = nofix && b + 1 < b0 + nb;                     // this batch's are the next one's T
+    const bool has_t = nofix && b > b0;       // the previous batch's changed nodes (L.trec)
+    const bool keep = nofix && b + 1 < b0 + nb;  // this batch's are the next one's T
     resolve_batch<false, false, QUOTA, EXT>(L, C, s, pods, base, B, k, nofix ? stale + (int64_t)par * MAX_BATCH * KSTALE : cand,
                                        nofix ? stale_cnt + par * MAX_BATCH : cand_cnt, chosen, chosen_score, global_offset,
-                                       stamps, pstamps, b, dev_alloc, nullptr, touched_out, touched_cnt, tin, keep,
+                                       stamps, pstamps, b, dev_alloc, nullptr, touched_out, touched_cnt, has_t, keep,
                                        nofix ? KSTALE : KMAX, !nofix || sorted != 0);  // (k_fixup's lists: by rank)
     __syncthreads();  // wave 0 drained its stores (replay_batch), so they are performed
     if (threadIdx.x == 0) st_sc1(done + b, 1);
