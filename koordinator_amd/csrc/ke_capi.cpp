@@ -754,20 +754,25 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
       const int32_t p = s0 + i;
       const int32_t node = chosen[p] - off;
       if (chosen[p] < 0 || node < 0 || node >= c.n_nodes) continue;
-      NodeState& ns = c.nodes[node];
       // LoadAware assign + NodeInfo.Requested: deferred (flush_mirror), the device rows carry them
       c.pending.push_back({node, now_ns, base + i});
+      // the allocations (read back only when the call's batches could make them): the node's state is touched
+      // only for a pod that has one
+      const bool dev = i < (int32_t)c.last_dev_alloc.size() && c.last_dev_alloc[i];
+      const bool numa = (int64_t)c.last_numa_alloc.size() >= (int64_t)(i + 1) * KE_MAX_NUMA * KE_NRES;
+      const uint64_t* cs = (int64_t)c.last_cpusets.size() >= (int64_t)(i + 1) * 4 ? &c.last_cpusets[(size_t)i * 4] : nullptr;
+      const bool cpus = cs && (cs[0] | cs[1] | cs[2] | cs[3]);
+      if (!dev && !numa && !cpus) continue;
+      NodeState& ns = c.nodes[node];
       const bool was_dirty = ns.dirty;
-      if (i < (int32_t)c.last_dev_alloc.size() && c.last_dev_alloc[i])
+      if (dev)
         host_ds_reserve(c.cfg, ns, make_dev_pod(c.cfg, pods[p], pod_hints(c, pods[p]), &c.tmpl), c.last_dev_alloc[i],
                         (int64_t)c.last_vf.size() >= (int64_t)(i + 1) * 2 * KE_MAX_MINORS ? &c.last_vf[(size_t)i * 2 * KE_MAX_MINORS] : nullptr);
-      if ((int64_t)c.last_numa_alloc.size() >= (int64_t)(i + 1) * KE_MAX_NUMA * KE_NRES)
-        host_numa_reserve(ns, &c.last_numa_alloc[(size_t)i * KE_MAX_NUMA * KE_NRES]);
+      if (numa) host_numa_reserve(ns, &c.last_numa_alloc[(size_t)i * KE_MAX_NUMA * KE_NRES]);
       ns.dirty = was_dirty;  // the device rows already carry these Reserves
       // cpuset Reserve: the CPU table (the device one is patched too) and the zones' NUMA status (not
       // patched on the device: re-derived from this mirror)
-      const uint64_t* cs = (int64_t)c.last_cpusets.size() >= (int64_t)(i + 1) * 4 ? &c.last_cpusets[(size_t)i * 4] : nullptr;
-      if (cs && (cs[0] | cs[1] | cs[2] | cs[3])) host_cpuset_reserve(ns, make_dev_pod(c.cfg, pods[p]), cs);
+      if (cpus) host_cpuset_reserve(ns, make_dev_pod(c.cfg, pods[p]), cs);
     }
     c.host_ms[7] = std::chrono::duration<double, std::milli>(clk::now() - tp).count();
     const bool whole = s0 == 0 && s1 == n_pods;  // one segment: the last_* outputs are already whole

@@ -5674,6 +5674,13 @@ struct DeviceState {
   uint8_t* d_aff = nullptr;        // [capacity] NUMA affinity per node of a singleton batch's eval
   // pipelined schedule: eval + select run on `estream` one batch ahead of the Reserve chain on `stream`
   hipStream_t estream = nullptr;
+  // a second eval stream with its own score matrix / part lists: consecutive batches of a stale-list run
+  // alternate between the two, so batch b+1's eval overlaps batch b's select (nullptr: clusters too large to
+  // double the score matrix)
+  hipStream_t estream2 = nullptr;
+  hipEvent_t ev_sel2 = nullptr;
+  uint16_t* d_scores2 = nullptr;
+  uint32_t* d_split2 = nullptr;
   uint32_t* d_stale = nullptr;      // [2][MAX_BATCH][KSTALE] stale-snapshot candidate lists
   uint32_t* d_chg = nullptr;        // changed-node bitmap of the replay when node ids exceed its LDS copy
   int64_t* d_trows = nullptr;       // [MAX_BATCH][NUM_RW] records the last resolved batch changed (node in RW_PAD)
@@ -5737,6 +5744,12 @@ int device_create(Context* ctx) {
   HIP_OK(hipMemsetAsync(d->soa.f, 0, sizeof(int64_t) * NUM_I64_FIELDS * d->capacity, d->stream));
   HIP_OK(hipMemsetAsync(d->soa.flags, 0, sizeof(uint32_t) * d->capacity, d->stream));
   HIP_OK(hipMalloc(&d->d_scores, sizeof(uint16_t) * MAX_BATCH * d->capacity));
+  if (d->capacity <= (1 << 20)) {  // <= 128 MB for the second score matrix
+    HIP_OK(hipStreamCreateWithPriority(&d->estream2, hipStreamNonBlocking, prio_lo));
+    HIP_OK(hipEventCreateWithFlags(&d->ev_sel2, hipEventDisableTiming));
+    HIP_OK(hipMalloc(&d->d_scores2, sizeof(uint16_t) * MAX_BATCH * d->capacity));
+    HIP_OK(hipMalloc(&d->d_split2, sizeof(uint32_t) * GATH_WORDS_MAX * MAX_WORLD));
+  }
   HIP_OK(hipMalloc(&d->d_cand, sizeof(uint32_t) * MAX_BATCH * KMAX));
   HIP_OK(hipMalloc(&d->d_cand_cnt, sizeof(int32_t) * MAX_BATCH));
   HIP_OK(hipMalloc(&d->d_batch_base, sizeof(int32_t)));
@@ -5749,8 +5762,8 @@ int device_create(Context* ctx) {
   HIP_OK(hipMemsetAsync(d->soa.kerr, 0, sizeof(int32_t), d->stream));
   HIP_OK(hipMemsetAsync(d->soa.rec, 0, sizeof(int64_t) * NUM_RW * d->capacity, d->stream));
   HIP_OK(hipMalloc(&d->d_tcnt, sizeof(int32_t)));
-  HIP_OK(hipMalloc(&d->d_parts_done, sizeof(int32_t) * MAX_BATCH));
-  HIP_OK(hipMemset(d->d_parts_done, 0, sizeof(int32_t) * MAX_BATCH));
+  HIP_OK(hipMalloc(&d->d_parts_done, sizeof(int32_t) * 2 * MAX_BATCH));  // (one half per eval stream)
+  HIP_OK(hipMemset(d->d_parts_done, 0, sizeof(int32_t) * 2 * MAX_BATCH));
   if (d->capacity > (int64_t)CHG_LDS_WORDS * 32) {  // zero between batches (each replay clears its bits)
     HIP_OK(hipMalloc(&d->d_chg, sizeof(uint32_t) * (d->capacity + 31) / 32));
     HIP_OK(hipMemsetAsync(d->d_chg, 0, sizeof(uint32_t) * (d->capacity + 31) / 32, d->stream));
@@ -5786,9 +5799,10 @@ void device_destroy(Context* ctx) {
                   d->d_dsraw,   d->d_dsmax,  d->d_devalloc,   d->d_dsrows,       d->soa.nf,   d->soa.nm,
                   d->d_numaalloc, d->d_numarows, d->d_defer, d->d_defer_cnt, d->soa.cs, d->soa.cpu,
                   d->d_cpurows, d->d_cpusets, d->d_aff, d->soa.qt, d->soa.qm, d->d_sched, d->d_stale,
-                  d->d_stale_cnt, d->d_trows, d->d_tcnt, d->d_parts_done, d->d_chg, d->soa.rec, d->soa.pt, d->soa.kerr,
+                  d->d_stale_cnt, d->d_trows, d->d_tcnt, d->d_parts_done, d->d_scores2, d->d_split2, d->d_chg, d->soa.rec, d->soa.pt, d->soa.kerr,
                   d->soa.xf, d->soa.xm, d->d_xrows, d->soa.dsx, d->d_ph, d->d_vfo, d->d_rsv, d->d_rsv_out};
   if (d->estream) (void)hipStreamSynchronize(d->estream);
+  if (d->estream2) (void)hipStreamSynchronize(d->estream2);
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (int e = 0; e < DeviceState::EV_RING; e++) {
@@ -5797,6 +5811,8 @@ void device_destroy(Context* ctx) {
   }
   if (d->ev_start) (void)hipEventDestroy(d->ev_start);
   if (d->estream) (void)hipStreamDestroy(d->estream);
+  if (d->estream2) (void)hipStreamDestroy(d->estream2);
+  if (d->ev_sel2) (void)hipEventDestroy(d->ev_sel2);
   if (d->stream) (void)hipStreamDestroy(d->stream);
   delete d;
   ctx->dev = nullptr;
@@ -6444,7 +6460,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   HIP_OK(hipMemsetAsync(d_ready, 0, sizeof(int32_t) * (sched_words - n_batches - 1), d->stream));
   HIP_OK(hipMemsetAsync(d_fst, 0, sizeof(uint64_t) * 2 * n_batches, d->stream));
   HIP_OK(hipMemsetAsync(d->soa.kerr, 0, sizeof(int32_t), d->stream));
-  HIP_OK(hipMemsetAsync(d->d_parts_done, 0, sizeof(int32_t) * MAX_BATCH, d->stream));  // (an aborted launch's counts)
+  HIP_OK(hipMemsetAsync(d->d_parts_done, 0, sizeof(int32_t) * 2 * MAX_BATCH, d->stream));  // (an aborted launch's counts)
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
@@ -6473,8 +6489,11 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   // can (split or one-workgroup select, unsharded) -- *published tells the caller
   bool published = false;
   auto eval_select = [&](int b, bool pipe, hipStream_t es, const int32_t* dwait = nullptr,
-                         int32_t* rpub = nullptr) -> int {
+                         int32_t* rpub = nullptr, bool alt = false) -> int {
     published = false;
+    uint16_t* const scores = alt ? d->d_scores2 : d->d_scores;  // (the second eval stream's buffers)
+    uint32_t* const split = alt ? d->d_split2 : d->d_split;
+    int32_t* const pdone = d->d_parts_done + (alt ? MAX_BATCH : 0);
     const int bp = batches[b].pods;
     const bool ds = batches[b].ds, cpu = batches[b].cpu;
     const bool prof = every > 0 && b % every == 0;
@@ -6511,27 +6530,30 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                                      : ((k.flags & AF_EXT) ? k_eval_batch<false, false, false, true>
                                                            : k_eval_batch<false, false, false>));
         uint32_t* dcnt = numa ? d->d_defer_cnt + b : nullptr;
+        // (with two eval streams the wait is a one-wave kernel: an eval grid spinning on the flag would hold the
+        // CUs the other stream's select needs)
         const bool plain_rec = !cpu && !ds && !numa && use_record_eval(bp);
-        if (dwait && !plain_rec)
+        const bool wait_kernel = dwait && (!plain_rec || alt || d->estream2 != nullptr);
+        if (wait_kernel)
           hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), 0, es, nullptr, 0, dwait, d_err, nullptr);
         if (plain_rec)  // plain batch: the record-based evaluation
           hipLaunchKernelGGL(((k.flags & AF_EXT) ? k_eval_plain<true> : k_eval_plain<false>), grid, dim3(eb), 0, es, d->soa,
-                             lo, hi, d->d_pods, bbase, bp, k, d->d_scores, d->capacity, fold_begin ? estamps + b : nullptr,
-                             dwait, d_err);
+                             lo, hi, d->d_pods, bbase, bp, k, scores, d->capacity, fold_begin ? estamps + b : nullptr,
+                             wait_kernel ? nullptr : dwait, d_err);
         else
           hipLaunchKernelGGL(eval, grid, dim3(eb), 0, es, d->soa, lo, hi, d->d_pods, bbase, bp,
-                             ppb, k, d->d_scores, d->capacity, d->d_dsraw, d->d_defer, dcnt, d->d_aff, d->d_dsmax,
+                             ppb, k, scores, d->capacity, d->d_dsraw, d->d_defer, dcnt, d->d_aff, d->d_dsmax,
                              fold_begin ? estamps + b : nullptr);
         if (numa) {  // a DeviceShare pod defers only on nodes without a device cache (no DeviceShare hints there)
           uint32_t* fb = reinterpret_cast<uint32_t*>(d->d_defer + (int64_t)MAX_BATCH * d->capacity);
           hipLaunchKernelGGL((cpu ? k_numa_fallback<false, true> : k_numa_fallback<false, false>), dim3(FALLBACK_BLOCKS),
                              dim3(64), 0, es, d->soa, d->d_pods,
-                             bbase, k, d->d_defer, dcnt, d->d_scores, d->capacity, 0, nullptr, nullptr,
+                             bbase, k, d->d_defer, dcnt, scores, d->capacity, 0, nullptr, nullptr,
                              nullptr, nullptr, nullptr, nullptr, ds ? d->d_dsmax : nullptr, cpu ? d->d_aff : nullptr,
                              ds ? d->d_dsraw : nullptr, fb);
           hipLaunchKernelGGL((cpu ? k_numa_finish<false, true> : k_numa_finish<false, false>), dim3(FINISH_BLOCKS),
                              dim3(64), 0, es, d->soa, d->d_pods,
-                             bbase, k, d->d_defer, dcnt, d->d_scores, d->capacity, 0, nullptr, nullptr,
+                             bbase, k, d->d_defer, dcnt, scores, d->capacity, 0, nullptr, nullptr,
                              nullptr, nullptr, nullptr, nullptr, ds ? d->d_dsmax : nullptr, cpu ? d->d_aff : nullptr,
                              ds ? d->d_dsraw : nullptr, fb);
         }
@@ -6543,7 +6565,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
         // register-resident when a wave's segment fits SEL_RC steps, else streamed
         const bool rc = select_seg(slo, shi) <= SEL_RC * 512;
         auto sel = ds ? (rc ? k_select<true, SEL_RC> : k_select<true, 0>) : (rc ? k_select<false, SEL_RC> : k_select<false, 0>);
-        hipLaunchKernelGGL(sel, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, es, d->d_scores, d->capacity, slo, shi, cand,
+        hipLaunchKernelGGL(sel, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, es, scores, d->capacity, slo, shi, cand,
                            cnt, d->d_dsraw, d->d_dsmax, k.wp_ds, kext, L, (int64_t)0, nullptr, nullptr, nullptr, pub);
       };
       // a plain batch over many nodes: its pods' selections split over several workgroups each (>= 256
@@ -6551,17 +6573,17 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       const int parts = ds ? 1 : select_parts(N, bp);
       if (argmax1) {  // d_cand[0] zeroed by k_batch_begin
         hipLaunchKernelGGL((ds ? k_argmax1<true> : k_argmax1<false>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
-                           es, d->d_scores, 0, N, d->d_dsraw, d->d_dsmax, k.wp_ds, d->d_cand, d->d_cand_cnt);
+                           es, scores, 0, N, d->d_dsraw, d->d_dsmax, k.wp_ds, d->d_cand, d->d_cand_cnt);
         if (!ctx->rsv_pairs.empty() || ctx->rsv_affinity)  // the pod's matched reservations: the Reservation plugin
-          hipLaunchKernelGGL(k_rsv_pick, dim3(1), dim3(64), 0, es, d->d_scores, d->d_rsv, (int)ctx->rsv_pairs.size(),
+          hipLaunchKernelGGL(k_rsv_pick, dim3(1), dim3(64), 0, es, scores, d->d_rsv, (int)ctx->rsv_pairs.size(),
                              (int64_t)ctx->cfg.weight_reservation, (int)ctx->rsv_affinity, d->d_cand, d->d_rsv_out);
       } else if (!sharded && parts > 1) {
         const int gw = gath_words(L);
         const bool rc = select_seg(0, select_part(0, N, parts)) <= SEL_RC * 512;
         hipLaunchKernelGGL((rc ? k_select<false, SEL_RC> : k_select<false, 0>), dim3((unsigned)bp, (unsigned)parts),
-                           dim3(SELECT_BLOCK), 0, es, d->d_scores, d->capacity, 0, (int)N, d->d_split,
-                           reinterpret_cast<int32_t*>(d->d_split + MAX_BATCH * L), d->d_dsraw, d->d_dsmax, k.wp_ds,
-                           kext, L, (int64_t)gw, lists, lists_cnt, d->d_parts_done, rpub);  // the last part merges
+                           dim3(SELECT_BLOCK), 0, es, scores, d->capacity, 0, (int)N, split,
+                           reinterpret_cast<int32_t*>(split + MAX_BATCH * L), d->d_dsraw, d->d_dsmax, k.wp_ds,
+                           kext, L, (int64_t)gw, lists, lists_cnt, pdone, rpub);  // the last part merges
         published = rpub != nullptr;
       } else if (!sharded) {
         select(0, N, lists, lists_cnt, ds ? nullptr : rpub);
@@ -6620,14 +6642,18 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                          d->d_chosen_score, ctx->cfg.global_node_offset, d->d_stamps, d->d_stamps + (n_pods + 2),
                          d->d_devalloc, d_ready, d_done, d_err, d->d_trows, d->d_tcnt, d->d_chg, N,
                          fixup ? nullptr : d->d_stale, fixup ? nullptr : d->d_stale_cnt, (int)run_sorted(r0, e));
+      const bool two_es = !fixup && d->estream2 != nullptr;  // batches alternate between the eval streams
       if (r0 > 0) HIP_OK(hipStreamWaitEvent(d->estream, d->ev_res[(r0 - 1) % R], 0));
+      if (two_es) HIP_OK(hipStreamWaitEvent(d->estream2, r0 > 0 ? d->ev_res[(r0 - 1) % R] : d->ev_start, 0));
       for (int q = r0; q < e; q++) {
         const bool first = q == r0;
         if (!fixup) {  // the stale lists go to the replay as they are; batch q's eval waits for batch q-2's done
-          rc = eval_select(q, true, d->estream, q - 2 >= r0 ? d_done + (q - 2) : nullptr, d_ready + q);
+          const bool alt = two_es && ((q - r0) & 1);
+          hipStream_t es = alt ? d->estream2 : d->estream;
+          rc = eval_select(q, true, es, q - 2 >= r0 ? d_done + (q - 2) : nullptr, d_ready + q, alt);
           if (rc) return rc;
           if (!published)
-            hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), 0, d->estream, d_ready + q, (int32_t)batches[q].pods, nullptr,
+            hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), 0, es, d_ready + q, (int32_t)batches[q].pods, nullptr,
                                d_err, nullptr);
           continue;
         }
@@ -6640,10 +6666,13 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       }
       HIP_OK(hipEventRecord(d->ev_res[(e - 1) % R], d->stream));
       HIP_OK(hipEventRecord(d->ev_sel[(e - 1) % R], d->estream));
+      if (two_es) HIP_OK(hipEventRecord(d->ev_sel2, d->estream2));
       n_pipelined += e - r0;
       b = e;
-      if (b < n_batches && run_end[b] == 0)  // a serial batch next: the run's eval stream drains first
+      if (b < n_batches && run_end[b] == 0) {  // a serial batch next: the run's eval streams drain first
         HIP_OK(hipStreamWaitEvent(d->stream, d->ev_sel[(e - 1) % R], 0));
+        if (two_es) HIP_OK(hipStreamWaitEvent(d->stream, d->ev_sel2, 0));
+      }
       continue;
     }
     // serial batch: eval, select and Reserve in order on one stream (no cross-stream hand-off)
@@ -6743,6 +6772,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   ctx->pending_pods.insert(ctx->pending_pods.end(), pods, pods + n_pods);
   HIP_OK(hipStreamSynchronize(d->stream));
   HIP_OK(hipStreamSynchronize(d->estream));
+  if (d->estream2) HIP_OK(hipStreamSynchronize(d->estream2));
   const auto t_sync = clk::now();
   std::memcpy(chosen, h + o_chosen, (size_t)out_bytes);
   if (score) std::memcpy(score, h + o_score, (size_t)out_bytes);
