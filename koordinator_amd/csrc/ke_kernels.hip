@@ -4366,17 +4366,10 @@ __device__ __forceinline__ void chg_unset(const ChgSet& c, int node) {
 // in registers) and pod j+2's keys are read; each is consumed one step later.  The three register sets
 // rotate by hand (step A, B, C -> B, C, A), so no loop-carried copy of a pending load forces an early wait.
 // Lane 0 stores pod j's prediction (L.sp.xnode / xkey) with its changed-set bit.
-#ifndef KE_EXP
-#define KE_EXP 0
-#endif
 template <bool GLB>
 __device__ __forceinline__ uint32_t chg_load_word(const ChgSet& c, uint32_t key) {
-#if KE_EXP == 1
-  return 0u;
-#else
   const int node = key ? key_node(key) : 0;  // (key 0: any word, its bit is masked below)
   return GLB ? ld_sc1(c.glb + (node >> 5)) : c.lds[node >> 5];
-#endif
 }
 __device__ __forceinline__ bool chg_word_bit(uint32_t w, uint32_t key) {
   return key != 0 && ((w >> (key_node(key) & 31)) & 1u);
@@ -4442,81 +4435,6 @@ __device__ __forceinline__ void spec_predict(ResLds& L, const ChgSet& C, int sta
     step(j + 1, kb0, kb1, wb0, wb1, mb0, mb1, kc0, kc1, wc0, wc1, mc0, mc1, ka0, ka1, ma0, ma1);
     if (j + 2 >= end) break;
     step(j + 2, kc0, kc1, wc0, wc1, mc0, mc1, ka0, ka1, wa0, wa1, ma0, ma1, kb0, kb1, mb0, mb1);
-  }
-}
-
-// Sorted lists, two pods a step: pod j's prediction is its first key outside the changed set and the pair
-// before's predictions; pod j+1's is its first such key unless that is pod j's prediction, then its second --
-// both from words read one step earlier, so the serial chain per pair is two ballots and a compare (a pod with
-// too few untaken keys among its first 64 takes the slow path: its whole list against the set as it is then).
-template <bool GLB>
-__device__ __forceinline__ void spec_predict_pairs(ResLds& L, const ChgSet& C, int start, int end, int LS, bool two,
-                                                   int lane) {
-#if KE_EXP == 3
-  auto key = [&](int j) -> uint32_t { return j < end ? ((uint32_t)(1000 - lane) << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)(lane * 64 + j)) : 0u; };
-#else
-  auto key = [&](int j) -> uint32_t { return j < end ? L.cand[j * LS + lane] : 0u; };
-#endif
-  auto slow = [&](int j) -> uint32_t {  // the changed set holds every earlier prediction (LDS order)
-    const uint32_t k0 = key(j), w0 = chg_load_word<GLB>(C, k0);
-    const uint64_t u0 = __ballot(k0 != 0 && !chg_word_bit(w0, k0));
-    if (u0) return (uint32_t)__builtin_amdgcn_readlane((int)k0, __builtin_ctzll(u0));
-    if (!two || j >= end) return 0u;
-    const uint32_t k1 = L.cand[j * LS + 64 + lane], w1 = chg_load_word<GLB>(C, k1);
-    const uint64_t u1 = __ballot(k1 != 0 && !chg_word_bit(w1, k1));
-    return u1 ? (uint32_t)__builtin_amdgcn_readlane((int)k1, __builtin_ctzll(u1)) : 0u;
-  };
-  auto record = [&](int j, uint32_t bu) {  // lane 0: the prediction, and its node into the changed set
-    const int xn = bu ? key_node(bu) : -1;
-    if (KE_EXP == 2) return;
-    if (lane == 0) {
-      L.sp.xnode[j] = xn;
-      L.sp.xkey[j] = bu;
-      if (xn >= 0) chg_or<GLB>(C, xn);
-    }
-  };
-  // pair sets: keys (a: pod j, b: pod j+1) and their words; the pair two steps ahead: keys only
-  uint32_t a0 = key(start), b0 = key(start + 1), a1 = key(start + 2), b1 = key(start + 3), a2 = 0, b2 = 0;
-  uint32_t wa0 = chg_load_word<GLB>(C, a0), wb0 = chg_load_word<GLB>(C, b0), wa1 = 0, wb1 = 0, wa2 = 0, wb2 = 0;
-  int px0 = -1, px1 = -1;  // the previous pair's predicted nodes (not in the words of this pair)
-  auto step = [&](int j, uint32_t& ka, uint32_t& kb, uint32_t& wa, uint32_t& wb, uint32_t& na, uint32_t& nb,
-                  uint32_t& wna, uint32_t& wnb, uint32_t& fa, uint32_t& fb) {
-    wna = chg_load_word<GLB>(C, na);  // the next pair: after the set updates of pods < j
-    wnb = chg_load_word<GLB>(C, nb);
-    fa = key(j + 4);                  // the pair after it: keys
-    fb = key(j + 5);
-    auto untaken = [&](uint32_t k, uint32_t w) {  // (a node's key differs between pods: compare nodes)
-      return k != 0 && !chg_word_bit(w, k) && key_node(k) != px0 && key_node(k) != px1;
-    };
-    const uint64_t ua = __ballot(untaken(ka, wa)), ub = __ballot(untaken(kb, wb));
-    uint32_t xa = ua ? (uint32_t)__builtin_amdgcn_readlane((int)ka, __builtin_ctzll(ua)) : slow(j);
-    record(j, xa);
-    if (j + 1 < end) {
-      uint32_t xb = 0;
-      bool done = false;
-      if (ub) {
-        const uint32_t c1 = (uint32_t)__builtin_amdgcn_readlane((int)kb, __builtin_ctzll(ub));
-        if (xa == 0 || key_node(c1) != key_node(xa)) {
-          xb = c1, done = true;
-        } else {
-          const uint64_t ub2 = ub & (ub - 1);
-          if (ub2) xb = (uint32_t)__builtin_amdgcn_readlane((int)kb, __builtin_ctzll(ub2)), done = true;
-        }
-      }
-      if (!done) xb = slow(j + 1);
-      record(j + 1, xb);
-      px1 = xb ? key_node(xb) : -1;
-    } else {
-      px1 = -1;
-    }
-    px0 = xa ? key_node(xa) : -1;
-  };
-  for (int j = start; j < end; j += 6) {
-    step(j, a0, b0, wa0, wb0, a1, b1, wa1, wb1, a2, b2);
-    if (j + 2 >= end) break;
-    step(j + 2, a1, b1, wa1, wb1, a2, b2, wa2, wb2, a0, b0);
-    if (j + 4 >= end) break;
-    step(j + 4, a2, b2, wa2, wb2, a0, b0, wa0, wb0, a1, b1);
   }
 }
 
@@ -4632,10 +4550,10 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
     // Reserve on a T node).
     if (wave == 0) {
       if (C.glb) {
-        if (sorted) spec_predict_pairs<true>(L, C, start, end, LS, two, lane);
+        if (sorted) spec_predict<true, true>(L, C, start, end, LS, two, lane);
         else spec_predict<true, false>(L, C, start, end, LS, two, lane);
       } else {
-        if (sorted) spec_predict_pairs<false>(L, C, start, end, LS, two, lane);
+        if (sorted) spec_predict<false, true>(L, C, start, end, LS, two, lane);
         else spec_predict<false, false>(L, C, start, end, LS, two, lane);
       }
       if (first && lane == 0) pst[9] = __builtin_amdgcn_s_memrealtime();  // the prediction loop's end
@@ -4830,15 +4748,22 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
   const int tid = threadIdx.x;
   constexpr int RES_THREADS = res_threads<NUMA>();
   if (tid == 0) pstamps[PST * batch_index] = __builtin_amdgcn_s_memrealtime();
-  // candidate keys at stride LS, issued together with their counts and the pods' loads (one round trip;
-  // sc1: a concurrent launch wrote them), then the slots past a list's count zeroed
-  constexpr int U = MAX_BATCH * KSTALE / RES_THREADS;
+  // candidate keys at stride LS, 16 B a load, issued together with their counts and the pods' loads (one round
+  // trip; sc1 buffer loads: a concurrent launch wrote them), then the slots past a list's count zeroed
+  constexpr int U = MAX_BATCH * KSTALE / 4 / RES_THREADS;  // 16-B chunks per thread
   const int lsh = LS == KSTALE ? 7 : 6, nk = MAX_BATCH * LS;
-  uint32_t q[U];
+  const __amdgpu_buffer_rsrc_t crs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(cand), 0, nk * 4, 0x00020000);
+  uint4 q[U];
 #pragma unroll
   for (int u = 0; u < U; u++) {
-    const int t = u * RES_THREADS + tid, j = t >> lsh;
-    q[u] = (t < nk && j < B) ? ld_sc1(cand + t) : 0u;
+    const int t = 4 * (u * RES_THREADS + tid), j = t >> lsh;
+    if (t < nk && j < B) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(crs, t * 4, 0, 16);  // aux 16: sc1
+      q[u] = make_uint4(v[0], v[1], v[2], v[3]);
+    } else {
+      q[u] = make_uint4(0u, 0u, 0u, 0u);
+    }
   }
   if (tid < B) {
     L.cnt[tid] = ld_sc1(cand_cnt + tid);
@@ -4857,8 +4782,16 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
   __syncthreads();  // the counts
 #pragma unroll
   for (int u = 0; u < U; u++) {
-    const int t = u * RES_THREADS + tid, j = t >> lsh, c = t & (LS - 1);
-    if (t < nk) L.cand[t] = (j < B && c < L.cnt[j]) ? q[u] : 0u;
+    const int t = 4 * (u * RES_THREADS + tid), j = t >> lsh, c = t & (LS - 1);
+    if (t < nk) {
+      const int n = j < B ? L.cnt[j] : 0;
+      uint4 w = q[u];
+      w.x = c < n ? w.x : 0u;
+      w.y = c + 1 < n ? w.y : 0u;
+      w.z = c + 2 < n ? w.z : 0u;
+      w.w = c + 3 < n ? w.w : 0u;
+      *reinterpret_cast<uint4*>(&L.cand[t]) = w;
+    }
   }
   __syncthreads();
   if (tid == 0) {
