@@ -4571,7 +4571,8 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
       snode = L.sp.xnode[lane];
       sv = snode >= 0;
       if (sv) {
-        rec_load(s.rec + (int64_t)snode * NUM_RW, slot);
+        rec_load_plain(s.rec + (int64_t)snode * NUM_RW, slot);  // 16-B loads (this workgroup wrote it sc1, or a
+                                                                 // launch before this one)
         if (ext) ext_load(s, snode, k, slot);
         fast_adopt(slot, k);
         const DevPod pc = L.pod[lane];
