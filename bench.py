@@ -7,11 +7,11 @@ pods (bit-exact with one-pod-at-a-time scheduling).  One step = scheduling one s
 steps.  The node state is resident in HBM before the timed region starts.
 
 roofline: the per-batch pipeline.  The critical path is the Reserve chain (k_resolve_run,
-one workgroup, per-batch time from in-kernel s_memrealtime stamps); eval, select and fixup run beside it
-on the second stream.  `roofline.achieved` = SURVEY.md §8(d)'s algorithmic bytes of a batch (N*S_row +
+one workgroup, per-batch time from in-kernel s_memrealtime stamps); eval and select run beside it on two
+alternating eval streams (k_fixup too with --pipeline-fixup).  `roofline.achieved` = SURVEY.md §8(d)'s algorithmic bytes of a batch (N*S_row +
 B*S_pod + B*k*12) over that critical path; `roofline.replay` the replay's own bytes, `roofline.kernels`
 every kernel of a batch and `roofline.end_to_end` the whole step, each against 8 TB/s.
-`traffic` = HBM bytes from a prior rocprofv3 PMC pass of this workload (profiles/r03/pmc_bench.json).
+`traffic` = HBM bytes from a prior rocprofv3 PMC pass of this workload (profiles/r04/pmc_bench.json).
 
 cpu_baseline: the oracle (C restatement of the Go plugins, oracle/) scheduling a prefix of the same
 queue on the host's cores at 1 thread, 16 threads (upstream Parallelism) and every usable core.
@@ -81,7 +81,7 @@ def eval_bytes(n_nodes, b):
     return n_nodes * (REC_EVAL if b > 2 else row) + b * pod + b * n_nodes * 2
 
 
-def batch_bytes(n_nodes, b, fetched, changed, pipelined):
+def batch_bytes(n_nodes, b, fetched, changed, pipelined, fixup=False):
     """algorithmic bytes per batch of each kernel: every input read once, every output
     written once; `fetched` = replay records of best unchanged candidates, `changed` = nodes a batch Reserved"""
     row, pod = sizes()
@@ -89,18 +89,18 @@ def batch_bytes(n_nodes, b, fetched, changed, pipelined):
     return {
         eval_kernel(b): eval_bytes(n_nodes, b),
         "k_select": b * n_nodes * 2 + b * (L + 1) * CAND_BYTES,
-        "k_fixup": (b * ((L + 1) * CAND_BYTES + pod + (KMAX + 1) * CAND_BYTES) + changed * REC_FULL) if pipelined else 0,
+        "k_fixup": (b * ((L + 1) * CAND_BYTES + pod + (KMAX + 1) * CAND_BYTES) + changed * REC_FULL) if fixup else 0,
         "k_resolve": b * ((KMAX + 1) * CAND_BYTES + pod + OUT_BYTES) + fetched * REC_READ
-                     + changed * (ROW_PATCH + REC_DYN + (REC_FULL if pipelined else 0)),
+                     + changed * (ROW_PATCH + REC_DYN + (REC_FULL if fixup else 0)),
     }
 
 
 def pmc_traffic(tag):
     """HBM bytes per launch by kernel from the committed PMC passes (tools/pmc_bench.sh, summarised by
-    tools/pmc_summary.py into profiles/r03/pmc_bench.json) of this workload.  Counter collection serialises
+    tools/pmc_summary.py into profiles/r04/pmc_bench.json) of this workload.  Counter collection serialises
     dispatches, which the persistent Reserve chain cannot run under, so the passes run the one-stream
     schedule (tag suffix _serial): its k_eval_batch / k_select / k_resolve launches do the same work per batch."""
-    f = os.path.join(ROOT, "profiles", "r03", "pmc_bench.json")
+    f = os.path.join(ROOT, "profiles", "r04", "pmc_bench.json")
     if not os.path.exists(f):
         return {}, None
     d = json.load(open(f))
@@ -172,10 +172,10 @@ def alg_batch_bytes(n_nodes, b):
     return n_nodes * row + b * pod + b * KMAX * 12
 
 
-def roofline(n_nodes, b, ks, dt_step, batches_per_step, pipelined, tag):
+def roofline(n_nodes, b, ks, dt_step, batches_per_step, pipelined, tag, fixup=False):
     """§8(d) roofline of a batch over its critical path (the Reserve chain: replay + hand-off per batch), with
     the replay's own bytes, the per-kernel and the end-to-end fractions as sub-fields."""
-    by = batch_bytes(n_nodes, b, ks["rows_fetched"], ks["rows_changed"], pipelined)
+    by = batch_bytes(n_nodes, b, ks["rows_fetched"], ks["rows_changed"], pipelined, fixup)
     ms = {eval_kernel(b): ks["eval_ms"], "k_select": ks["select_ms"], "k_fixup": ks["fixup_ms"],
           "k_resolve": ks["resolve_ms"]}
     traffic, src = pmc_traffic(tag)
@@ -342,7 +342,8 @@ def main():
                       "resolve_phases": kagg["resolve_phases"],
                       "note": "per batch; 'select' includes the all-gather + merge when sharded"},
         "host_ms_per_step": {k: float(np.mean([h[k] for h in hs])) for k in hs[0]} if hs else None,
-        "roofline": roofline(hi - lo, a.batch, kagg, dt / K, n_batches / K, not a.no_pipeline, tag),
+        "roofline": roofline(hi - lo, a.batch, kagg, dt / K, n_batches / K, not a.no_pipeline, tag,
+                             a.pipeline_fixup and not a.no_pipeline),
     }
     ev.close()
     if world == 1 and a.stream_nodes > 0:

@@ -6526,6 +6526,11 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     if (!fold_begin)
       hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(MAX_BATCH), 0, es, estamps + (rerun ? n_pods + 1 : b), ds ? d->d_dsmax : nullptr,
                          argmax1 ? d->d_cand : nullptr);
+    // (with two eval streams the wait is a one-wave kernel ahead of the eval, outside its timing: an eval grid
+    // spinning on the flag would hold the CUs the other stream's select needs)
+    const bool plain_rec = !cpu && !ds && !numa && use_record_eval(bp);
+    const bool wait_kernel = dwait && (!plain_rec || alt || d->estream2 != nullptr || hi <= lo);
+    if (wait_kernel) hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), 0, es, nullptr, 0, dwait, d_err, nullptr);
     if (prof) HIP_OK(hipEventRecord(pe[0], es));
     const int L = pipe ? KSTALE : KMAX, kext = pipe ? KMAX : 0;
     uint32_t* lists = pipe ? d->d_stale + (size_t)(b & 1) * MAX_BATCH * KSTALE : d->d_cand;
@@ -6546,12 +6551,6 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                                      : ((k.flags & AF_EXT) ? k_eval_batch<false, false, false, true>
                                                            : k_eval_batch<false, false, false>));
         uint32_t* dcnt = numa ? d->d_defer_cnt + b : nullptr;
-        // (with two eval streams the wait is a one-wave kernel: an eval grid spinning on the flag would hold the
-        // CUs the other stream's select needs)
-        const bool plain_rec = !cpu && !ds && !numa && use_record_eval(bp);
-        const bool wait_kernel = dwait && (!plain_rec || alt || d->estream2 != nullptr);
-        if (wait_kernel)
-          hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), 0, es, nullptr, 0, dwait, d_err, nullptr);
         if (plain_rec)  // plain batch: the record-based evaluation
           hipLaunchKernelGGL(((k.flags & AF_EXT) ? k_eval_plain<true> : k_eval_plain<false>), grid, dim3(eb), 0, es, d->soa,
                              lo, hi, d->d_pods, bbase, bp, k, scores, d->capacity, fold_begin ? estamps + b : nullptr,
