@@ -6529,7 +6529,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     // (with two eval streams the wait is a one-wave kernel ahead of the eval, outside its timing: an eval grid
     // spinning on the flag would hold the CUs the other stream's select needs)
     const bool plain_rec = !cpu && !ds && !numa && use_record_eval(bp);
-    const bool wait_kernel = dwait && (!plain_rec || alt || d->estream2 != nullptr || hi <= lo);
+    const bool wait_kernel = dwait && (!plain_rec || alt || (d->estream2 != nullptr && !sharded) || hi <= lo);
     if (wait_kernel) hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), 0, es, nullptr, 0, dwait, d_err, nullptr);
     if (prof) HIP_OK(hipEventRecord(pe[0], es));
     const int L = pipe ? KSTALE : KMAX, kext = pipe ? KMAX : 0;
@@ -6657,7 +6657,9 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                          d->d_chosen_score, ctx->cfg.global_node_offset, d->d_stamps, d->d_stamps + (n_pods + 2),
                          d->d_devalloc, d_ready, d_done, d_err, d->d_trows, d->d_tcnt, d->d_chg, N,
                          fixup ? nullptr : d->d_stale, fixup ? nullptr : d->d_stale_cnt, (int)run_sorted(r0, e));
-      const bool two_es = !fixup && d->estream2 != nullptr;  // batches alternate between the eval streams
+      // batches alternate between the eval streams -- unsharded only: a node-sharded batch's all-gather must run
+      // in the same order on every rank's communicator, which two streams of one rank would not guarantee
+      const bool two_es = !fixup && d->estream2 != nullptr && !sharded;
       if (r0 > 0) HIP_OK(hipStreamWaitEvent(d->estream, d->ev_res[(r0 - 1) % R], 0));
       if (two_es) HIP_OK(hipStreamWaitEvent(d->estream2, r0 > 0 ? d->ev_res[(r0 - 1) % R] : d->ev_start, 0));
       for (int q = r0; q < e; q++) {
