@@ -1071,9 +1071,10 @@ int ke_last_resolve_split(ke_ctx* ctx, double* prologue_ms, double* replay_ms);
  * reserve + evaluate the slots (R + S), verify (V) —, its later rounds, and the write-back (all of a one-wave
  * replay). */
 int ke_debug_resolve_phases(ke_ctx* ctx, double* phases6);
-/* The speculative replay's first round in detail (4 entries, ms per batch): T's set-up, the prediction loop
- * (wave 0), the T rows of wave 1 (concurrent with the loop), wave 0's R. */
-int ke_debug_resolve_subphases(ke_ctx* ctx, double* sub4);
+/* The speculative replay's first round in detail (5 entries; the first four ms per batch): T's set-up, the
+ * prediction loop (wave 0), the T maxima on wave 1 (its own rows or the T-row helpers' hand-off, concurrent with
+ * the loop), wave 0's R; then the fraction of T batches whose maxima came from the helpers. */
+int ke_debug_resolve_subphases(ke_ctx* ctx, double* sub5);
 /* BestEffort (pod, node) pairs the last ke_eval / ke_schedule evaluated in the compacted full-merge
  * pass (no preferred merged hint). */
 int ke_debug_numa_deferred(ke_ctx* ctx, int64_t* n);

@@ -1013,9 +1013,9 @@ int ke_debug_resolve_phases(ke_ctx* ctx, double* phases6) {
   return KE_OK;
 }
 
-int ke_debug_resolve_subphases(ke_ctx* ctx, double* sub4) {
-  if (!ctx || !sub4) return fail(KE_ERR_INVALID, "ke_debug_resolve_subphases arguments");
-  for (int i = 0; i < 4; i++) sub4[i] = ctx->c.kstat_resolve_sub_ms[i];
+int ke_debug_resolve_subphases(ke_ctx* ctx, double* sub5) {
+  if (!ctx || !sub5) return fail(KE_ERR_INVALID, "ke_debug_resolve_subphases arguments");
+  for (int i = 0; i < 5; i++) sub5[i] = ctx->c.kstat_resolve_sub_ms[i];
   return KE_OK;
 }
 

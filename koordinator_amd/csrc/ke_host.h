@@ -135,7 +135,7 @@ struct Context {
   double host_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // batches of the last ke_schedule that ran pipelined (two streams)
   double kstat_resolve_prologue_ms = 0, kstat_resolve_loop_ms = 0;
   double kstat_resolve_phase_ms[6] = {0, 0, 0, 0, 0, 0};
-  double kstat_resolve_sub_ms[4] = {0, 0, 0, 0};  // ke_debug_resolve_subphases
+  double kstat_resolve_sub_ms[5] = {0, 0, 0, 0, 0};  // ke_debug_resolve_subphases
   int64_t kstat_numa_deferred = 0;  // BestEffort pairs the last ke_eval / ke_schedule left to k_numa_fallback
   int32_t kstat_samples = 0;
   // Host mirror of the LoadAware / NodeInfo part of the last ke_schedule's Reserves (the device rows

@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -3206,6 +3207,27 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_plain(SoA s, int lo, int hi
   }
 }
 
+// Batch b's scores of the nodes batch b-2 changed (stale-list runs on two eval streams): batch
+// b's eval waited only for batch b-3's done flag; once done[b-2] is published (a k_handoff ahead of this kernel)
+// lane t of workgroup j re-evaluates node t of batch b-2's changed list (written with its rows, drained before
+// the flag) for pod j from its record, as k_eval_plain does -- the lists then see every Reserve of batches <= b-2.
+template <bool EXT>
+__global__ __launch_bounds__(64) void k_patch(SoA s, const DevPod* __restrict__ pods, const int32_t* __restrict__ batch_base,
+                                              KArgs k, const int32_t* __restrict__ tlist, uint16_t* __restrict__ scores,
+                                              int64_t score_stride) {
+  const int j = blockIdx.x, t = threadIdx.x;
+  const int n = ld_sc1(tlist);
+  if (t >= n) return;
+  const int node = ld_sc1(tlist + 1 + t);
+  NodeFast f;
+  rec_load<__HIP_MEMORY_SCOPE_AGENT>(s.rec + (int64_t)node * NUM_RW, f);
+  if (EXT && (k.flags & AF_EXT)) ext_load(s, node, k, f);
+  fast_adopt(f, k);
+  const DevPod pod = pods[*batch_base + j];
+  const double ed[2] = {(double)pod.est[0], (double)pod.est[1]}, rd[2] = {(double)pod.req[0], (double)pod.req[1]};
+  scores[(int64_t)j * score_stride + node] = (uint16_t)(fast_total<EXT>(f, pod, ed, rd, k) + 1);
+}
+
 // selectHost for a singleton batch: the best packed key over nodes [lo, hi) (ties to the lowest node
 // index), one atomicMax per wave; cand[0] must be zero on entry, cand_cnt[0] becomes 1.
 template <bool DS>
@@ -4333,6 +4355,19 @@ struct SpecLds {
   int32_t tnext_n;
 };
 
+constexpr int32_t XN_PENDING = INT32_MIN;  // L.sp.xnode: not predicted yet (the progressive S polls it)
+constexpr int PCH = 16;                    // the progressive S: pods a chunk
+constexpr uint64_t T_HELP_WAIT_TICKS = 2000;  // wave 0's wait for the helpers' T maxima (20 us), then its own rows
+// The T-row helpers of a stale-list run (k_resolve_run workgroups 1..H): batch b's T maxima
+// (every pod against the previous batch's changed nodes) evaluated on other CUs while the Reserve workgroup
+// predicts, instead of on its own waves.  Global hand-off words, double-buffered by batch parity.
+struct THelp {
+  int32_t* tlist;   // [2][1 + MAX_BATCH]: a batch's changed nodes (count first; the Reserve workgroup writes them)
+  uint32_t* tmx;    // [2][MAX_BATCH]: the T maxima of a batch's pods (the helpers write them)
+  int32_t* tready;  // [batch]: helpers done with the batch (relaxed agent adds)
+  int H;            // helper workgroups (0: none)
+};
+
 struct ResLdsCore {
   uint32_t cand[MAX_BATCH * KSTALE];  // exact lists at stride KMAX, or the pipelined schedule's stale lists at KSTALE
   DevPod pod[MAX_BATCH];
@@ -4422,7 +4457,7 @@ __device__ __forceinline__ void spec_predict(ResLds& L, const ChgSet& C, int sta
     }
     const int xn = bu ? key_node(bu) : -1;
     if (lane == 0) {  // pod j's prediction, and its node into the changed set
-      L.sp.xnode[j] = xn;
+      ((volatile int32_t*)L.sp.xnode)[j] = xn;  // (in order: the progressive S polls it)
       L.sp.xkey[j] = bu;
       if (xn >= 0) chg_or<GLB>(C, xn);
     }
@@ -4470,7 +4505,7 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
                                             uint64_t* __restrict__ stamps, int batch_index,
                                             uint64_t* __restrict__ dev_alloc, int64_t* __restrict__ touched_out,
                                             int32_t* __restrict__ touched_cnt, uint64_t* __restrict__ pst,
-                                            bool has_t, bool keep, int LS, bool sorted) {
+                                            bool has_t, bool keep, int LS, bool sorted, const THelp th) {
   constexpr int NW = res_threads<false>() / 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const bool ext = EXT && (k.flags & AF_EXT);
@@ -4539,12 +4574,59 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
       L.sp.tmx[j1] = tk1, L.sp.tver[j1] = tres;
     }
   };
+  // lane c in [lo, hi) adopts pod c's predicted node and reserves pod c on it (vol: read while wave 0 predicts)
+  auto reserve_lanes = [&](int lo, int hi, bool vol) {
+    if (lane >= lo && lane < hi) {
+      snode = vol ? ((volatile int32_t*)L.sp.xnode)[lane] : L.sp.xnode[lane];
+      sv = snode >= 0;
+      if (sv) {
+        rec_load_plain(s.rec + (int64_t)snode * NUM_RW, slot);  // 16-B loads (this workgroup wrote it sc1, or a
+                                                                 // launch before this one)
+        if (ext) ext_load(s, snode, k, slot);
+        fast_adopt(slot, k);
+        const DevPod pc = L.pod[lane];
+        const double ed[2] = {L.pd[lane][0], L.pd[lane][1]}, rd[2] = {L.pd[lane][2], L.pd[lane][3]};
+        fast_reserve(slot, pc, ed, rd);
+        if (ext) ext_fast_reserve(slot, pc, k);
+      }
+    }
+  };
+  // rows j and j1 (j1 < 0: none) against the slots c < j: mrow without T (the progressive S)
+  auto s_rows = [&](int j, int j1) {
+    const bool has1 = !EXT && j1 >= 0;
+    const DevPod p = L.pod[j];
+    const double ed[2] = {L.pd[j][0], L.pd[j][1]}, rd[2] = {L.pd[j][2], L.pd[j][3]};
+    uint32_t kc = 0, kc1 = 0;
+    if (has1) {
+      const DevPod p1 = L.pod[j1];
+      const double ed1[2] = {L.pd[j1][0], L.pd[j1][1]}, rd1[2] = {L.pd[j1][2], L.pd[j1][3]};
+      if (sv && lane < j) kc = make_key(fast_total<EXT>(slot, p, ed, rd, k), snode);
+      if (sv && lane < j1) kc1 = make_key(fast_total<EXT>(slot, p1, ed1, rd1, k), snode);
+    } else if (sv && lane < j) {
+      kc = make_key(fast_total<EXT>(slot, p, ed, rd, k), snode);
+    }
+    kc = wave_max_u32(kc);
+    kc1 = has1 ? wave_max_u32(kc1) : 0u;
+    if (lane == 0) {
+      L.sp.mrow[j] = kc;
+      if (has1) L.sp.mrow[j1] = kc1;
+    }
+    if (EXT && j1 >= 0) {  // (the ext slots: one chain a pass)
+      const DevPod p1 = L.pod[j1];
+      const double ed1[2] = {L.pd[j1][0], L.pd[j1][1]}, rd1[2] = {L.pd[j1][2], L.pd[j1][3]};
+      uint32_t k1 = (sv && lane < j1) ? make_key(fast_total<EXT>(slot, p1, ed1, rd1, k), snode) : 0u;
+      k1 = wave_max_u32(k1);
+      if (lane == 0) L.sp.mrow[j1] = k1;
+    }
+  };
   int32_t o_node = -1, o_score = -1;  // wave 0, lane j: pod j's placement
   int start = 0, win = B, rounds = 0, fetched = 0;
   const bool stamp = wave == 0 && lane == 0;  // phase stamps of the first round (ke_debug_resolve_phases)
   bool first = true;
   while (start < B) {
     const int end = min(B, start + win);
+    // the first round of a batch with T whose maxima the helpers evaluate: R + S follow the prediction
+    const bool prog = first && tin && th.H > 0;
     // ---- P (wave 0): pods [start, end) each take their best candidate not taken before.  Meanwhile the other
     // waves evaluate the rows' T maxima the S phase would compute (stale lists: the first round, or after a
     // Reserve on a T node).
@@ -4558,6 +4640,46 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
       }
       if (first && lane == 0) pst[9] = __builtin_amdgcn_s_memrealtime();  // the prediction loop's end
       adopt_t();  // (its loads landed during the prediction)
+      if (prog) {
+        reserve_lanes(start, end, false);  // wave 0's own slots (V, write-back)
+        fetched += __popcll(__ballot(lane >= start && lane < end && sv));
+        if (lane == 0) pst[11] = __builtin_amdgcn_s_memrealtime();
+        // the helpers' T maxima of this batch (a bounded wait: rows whose maximum did not arrive are evaluated
+        // after the barrier)
+        int ok = 0;
+        if (lane == 0) {
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          while (true) {
+            if (ld_sc1(th.tready + batch_index) >= th.H) {
+              ok = 1;
+              break;
+            }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > T_HELP_WAIT_TICKS) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        ok = __builtin_amdgcn_readfirstlane(ok);
+        if (ok && lane >= start && lane < end) {
+          L.sp.tmx[lane] = ld_sc1(th.tmx + (batch_index & 1) * MAX_BATCH + lane);
+          L.sp.tver[lane] = 0;  // (tres == 0: the first round)
+        }
+        if (lane == 0) {
+          pst[10] = __builtin_amdgcn_s_memrealtime();
+          pst[12] = ok;
+        }
+      }
+    } else if (prog) {
+      // ---- progressive R + S (waves 1..NW-1): once pod hi-1 of a chunk [lo, hi) is predicted, its slots are
+      // reserved and the rows (prev, hi] -- pods whose slots c < j are all known -- evaluated against them
+      adopt_t();
+      for (int lo = start; lo < end; lo += PCH) {
+        const int hi = min(end, lo + PCH);
+        if (lane == 0)
+          while (((volatile int32_t*)L.sp.xnode)[hi - 1] == XN_PENDING) __builtin_amdgcn_s_sleep(1);
+        reserve_lanes(lo, hi, true);
+        const int r0 = lo == start ? start : lo + 1, r1 = min(hi + 1, end);  // rows [r0, r1)
+        for (int j = r0 + wave - 1; j < r1; j += 2 * (NW - 1)) s_rows(j, j + NW - 1 < r1 ? j + NW - 1 : -1);
+      }
     } else if (tin) {
       adopt_t();
       constexpr int RT = EXT ? 1 : 2;
@@ -4566,55 +4688,50 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
     }
     __syncthreads();
     if (stamp && first) pst[1] = __builtin_amdgcn_s_memrealtime();
-    // ---- R (every wave): lane c in [start, end) adopts pod c's predicted node and reserves pod c on it
-    if (lane >= start && lane < end) {
-      snode = L.sp.xnode[lane];
-      sv = snode >= 0;
-      if (sv) {
-        rec_load_plain(s.rec + (int64_t)snode * NUM_RW, slot);  // 16-B loads (this workgroup wrote it sc1, or a
-                                                                 // launch before this one)
-        if (ext) ext_load(s, snode, k, slot);
-        fast_adopt(slot, k);
-        const DevPod pc = L.pod[lane];
-        const double ed[2] = {L.pd[lane][0], L.pd[lane][1]}, rd[2] = {L.pd[lane][2], L.pd[lane][3]};
-        fast_reserve(slot, pc, ed, rd);
-        if (ext) ext_fast_reserve(slot, pc, k);
+    if (prog) {
+      // the T maxima into the rows: the helpers' (wave 0 polled them), else evaluated here
+      for (int j = start + wave; j < end; j += NW) {
+        t_row(j);
+        if (lane == 0) L.sp.mrow[j] = max(L.sp.mrow[j], L.sp.tmx[j]);
       }
-    }
-    if (wave == 0) fetched += __popcll(__ballot(lane >= start && lane < end && sv));
-    if (stamp && first) pst[11] = __builtin_amdgcn_s_memrealtime();  // wave 0's slots reserved (R)
-    // ---- S (rows over the waves): pod j against every slot c < j (and every T slot)
-    // Two rows a pass (j and j + NW): two independent evaluation chains for the latency-bound wave (one with
-    // the ext slots: their registers would spill).
-    constexpr int RS = EXT ? 1 : 2;
-    for (int j = start + wave; j < end; j += RS * NW) {
-      const int j1 = j + NW;
-      const bool has1 = RS == 2 && j1 < end;  // (wave-uniform)
-      const DevPod p = L.pod[j];
-      const double ed[2] = {L.pd[j][0], L.pd[j][1]}, rd[2] = {L.pd[j][2], L.pd[j][3]};
-      uint32_t kc = 0, kc1 = 0;
-      if (has1) {
-        const DevPod p1 = L.pod[j1];
-        const double ed1[2] = {L.pd[j1][0], L.pd[j1][1]}, rd1[2] = {L.pd[j1][2], L.pd[j1][3]};
-        if (sv && lane < j) kc = make_key(fast_total<EXT>(slot, p, ed, rd, k), snode);
-        if (sv && lane < j1) kc1 = make_key(fast_total<EXT>(slot, p1, ed1, rd1, k), snode);
-      } else if (sv && lane < j) {
-        kc = make_key(fast_total<EXT>(slot, p, ed, rd, k), snode);
-      }
-      uint32_t tk = 0, tk1 = 0;
-      if (tin) {  // T changes only when a pod of the batch reserves on it: pod j's T max is cached meanwhile
-        t_row(j);  // (this wave's own LDS writes: in order)
-        tk = L.sp.tmx[j];
+    } else {
+      // ---- R (every wave): lane c in [start, end) adopts pod c's predicted node and reserves pod c on it
+      reserve_lanes(start, end, false);
+      if (wave == 0) fetched += __popcll(__ballot(lane >= start && lane < end && sv));
+      if (stamp && first) pst[11] = __builtin_amdgcn_s_memrealtime();  // wave 0's slots reserved (R)
+      // ---- S (rows over the waves): pod j against every slot c < j (and every T slot)
+      // Two rows a pass (j and j + NW): two independent evaluation chains for the latency-bound wave (one with
+      // the ext slots: their registers would spill).
+      constexpr int RS = EXT ? 1 : 2;
+      for (int j = start + wave; j < end; j += RS * NW) {
+        const int j1 = j + NW;
+        const bool has1 = RS == 2 && j1 < end;  // (wave-uniform)
+        const DevPod p = L.pod[j];
+        const double ed[2] = {L.pd[j][0], L.pd[j][1]}, rd[2] = {L.pd[j][2], L.pd[j][3]};
+        uint32_t kc = 0, kc1 = 0;
         if (has1) {
-          t_row(j1);
-          tk1 = L.sp.tmx[j1];
+          const DevPod p1 = L.pod[j1];
+          const double ed1[2] = {L.pd[j1][0], L.pd[j1][1]}, rd1[2] = {L.pd[j1][2], L.pd[j1][3]};
+          if (sv && lane < j) kc = make_key(fast_total<EXT>(slot, p, ed, rd, k), snode);
+          if (sv && lane < j1) kc1 = make_key(fast_total<EXT>(slot, p1, ed1, rd1, k), snode);
+        } else if (sv && lane < j) {
+          kc = make_key(fast_total<EXT>(slot, p, ed, rd, k), snode);
         }
-      }
-      const uint32_t mx = max(wave_max_u32(kc), tk);
-      const uint32_t mx1 = has1 ? max(wave_max_u32(kc1), tk1) : 0u;
-      if (lane == 0) {
-        L.sp.mrow[j] = mx;
-        if (has1) L.sp.mrow[j1] = mx1;
+        uint32_t tk = 0, tk1 = 0;
+        if (tin) {  // T changes only when a pod of the batch reserves on it: pod j's T max is cached meanwhile
+          t_row(j);  // (this wave's own LDS writes: in order)
+          tk = L.sp.tmx[j];
+          if (has1) {
+            t_row(j1);
+            tk1 = L.sp.tmx[j1];
+          }
+        }
+        const uint32_t mx = max(wave_max_u32(kc), tk);
+        const uint32_t mx1 = has1 ? max(wave_max_u32(kc1), tk1) : 0u;
+        if (lane == 0) {
+          L.sp.mrow[j] = mx;
+          if (has1) L.sp.mrow[j1] = mx1;
+        }
       }
     }
     __syncthreads();
@@ -4702,6 +4819,12 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
     if (sv) L.sp.tnext[lanes_below(vm)] = snode;
     if (tdirty) L.sp.tnext[__popcll(vm) + lanes_below(tm)] = tnode;
     if (lane == 0) L.sp.tnext_n = __popcll(vm) + __popcll(tm);
+    if (th.tlist) {  // ... and for the helpers / k_patch (drained before done[batch_index] is published)
+      int32_t* tl = th.tlist + (batch_index & 1) * (1 + MAX_BATCH);
+      if (sv) st_sc1(tl + 1 + lanes_below(vm), (int32_t)snode);
+      if (tdirty) st_sc1(tl + 1 + __popcll(vm) + lanes_below(tm), (int32_t)tnode);
+      if (lane == 0) st_sc1(tl, (int32_t)(__popcll(vm) + __popcll(tm)));
+    }
     if (tv && !tdirty) chg_unset(C, tnode);
   } else {  // every bit still set belongs to a taken node or to T
     if (sv) chg_clear_word(C, snode);
@@ -4713,7 +4836,7 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
     pst[6] = (uint64_t)(uint32_t)fetched | ((uint64_t)rounds << 32);  // records fetched | failed rounds
     pst[7] = (uint64_t)(__popcll(vm) + __popcll(tm));
   }
-  drain_stores();
+  if (!keep) drain_stores();  // (keep: the next batch's prologue drains them behind its loads, then publishes)
 }
 
 // zero the LDS bitmap words of node ids [0, n_nodes) (all threads; once per launch)
@@ -4745,10 +4868,13 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
                                               int64_t* __restrict__ touched_out = nullptr,
                                               int32_t* __restrict__ touched_cnt = nullptr,
                                               bool has_t = false, bool keep = false, int LS = KMAX,
-                                              bool sorted = false) {
+                                              bool sorted = false, int32_t* __restrict__ pub_done = nullptr,
+                                              const THelp th = THelp{nullptr, nullptr, nullptr, 0}) {
   const int tid = threadIdx.x;
   constexpr int RES_THREADS = res_threads<NUMA>();
   if (tid == 0) pstamps[PST * batch_index] = __builtin_amdgcn_s_memrealtime();
+  // `pub_done` (stale-list runs): the previous batch's done flag, published once wave 0's stores of it have
+  // drained -- here, behind this batch's loads, rather than before them
   // candidate keys at stride LS, 16 B a load, issued together with their counts and the pods' loads (one round
   // trip; sc1 buffer loads: a concurrent launch wrote them), then the slots past a list's count zeroed
   constexpr int U = MAX_BATCH * KSTALE / 4 / RES_THREADS;  // 16-B chunks per thread
@@ -4780,6 +4906,11 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
     }
   }
   if (has_t && tid < B) L.sp.tver[tid] = -1;  // no pod's T max computed yet (replay_spec)
+  if (tid < B) L.sp.xnode[tid] = XN_PENDING;
+  if (pub_done && tid == 0) {  // (wave 0 issued every store of the previous batch)
+    drain_stores();
+    st_sc1(pub_done, 1);
+  }
   __syncthreads();  // the counts
 #pragma unroll
   for (int u = 0; u < U; u++) {
@@ -4799,11 +4930,12 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
     const uint64_t t = __builtin_amdgcn_s_memrealtime();
     for (int u = 1; u < 6; u++) pstamps[PST * batch_index + u] = t;
     for (int u = 8; u < 12; u++) pstamps[PST * batch_index + u] = t;
+    pstamps[PST * batch_index + 12] = 0;
   }
   if constexpr (!DS && !NUMA && !QUOTA) {  // plain batch: the speculative replay on every wave
     __builtin_amdgcn_s_setprio(3);
     replay_spec<EXT>(L, C, s, base, B, k, chosen, chosen_score, global_offset, stamps, batch_index, dev_alloc,
-                     touched_out, touched_cnt, pstamps + PST * batch_index, has_t, keep, LS, sorted);
+                     touched_out, touched_cnt, pstamps + PST * batch_index, has_t, keep, LS, sorted, th);
     __builtin_amdgcn_s_setprio(0);
     return;
   }
@@ -5093,6 +5225,87 @@ __global__ __launch_bounds__(res_threads<NUMA>()) void k_resolve(SoA s, const De
                                  false, false, KMAX, sorted != 0);
 }
 
+// A T-row helper workgroup (THelp; helper h of H): for every batch b > b0 of the run, once the Reserve
+// workgroup has published done[b-1] (the changed nodes' records and list drained), the T slots in registers
+// (lane t: changed node t of batch b-1, as replay_spec's tslot) and the T maximum of every pod j of batch b
+// whose pair index (j / 2) falls to this helper: max_t key(fast_total(T node t, pod j)).  Published to tmx with
+// one relaxed add on tready[b] per helper.  A batch the Reserve workgroup has already finished (done[b]) is
+// skipped; the Reserve workgroup falls back to its own rows for any batch whose maxima arrive late, so no
+// wait of the run depends on a helper being resident.
+template <bool EXT>
+__device__ __noinline__ void t_helper(ResLds& L, const SoA& s, const DevPod* __restrict__ pods,
+                                      const int32_t* __restrict__ bases, int b0, int nb, const KArgs& k,
+                                      const int32_t* __restrict__ done, int32_t* __restrict__ err, const THelp th,
+                                      int h, int32_t* s_go) {
+  constexpr int NW = res_threads<false>() / 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool ext = EXT && (k.flags & AF_EXT);
+  for (int b = b0 + 1; b < b0 + nb; b++) {
+    const int base = bases[b], B = bases[b + 1] - base;
+    if ((int)threadIdx.x < B) {  // the batch's pods (uploaded before the launch): before the wait
+      const DevPod pd = pods[base + threadIdx.x];
+      L.pod[threadIdx.x] = pd;
+      L.pd[threadIdx.x][0] = (double)pd.est[0];
+      L.pd[threadIdx.x][1] = (double)pd.est[1];
+      L.pd[threadIdx.x][2] = (double)pd.req[0];
+      L.pd[threadIdx.x][3] = (double)pd.req[1];
+    }
+    if (threadIdx.x == 0) {
+      int go = -1;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (true) {  // (no error word of its own: a stuck run is the Reserve workgroup's to report)
+        if (ld_sc1(done + (b - 1)) != 0) {
+          go = ld_sc1(done + b) != 0 ? 0 : 1;
+          break;
+        }
+        if (ld_sc1(err) != 0 || __builtin_amdgcn_s_memrealtime() - t0 > HANDOFF_TIMEOUT_TICKS) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      *s_go = go;
+    }
+    __syncthreads();
+    const int go = *s_go;
+    if (go < 0) return;
+    if (go > 0) {
+      // T of batch b: the changed nodes of batch b-1 (count and ids in one round trip, then the records)
+      const int32_t* tl = th.tlist + ((b - 1) & 1) * (1 + MAX_BATCH);
+      const int tn = ld_sc1(tl);
+      const int32_t tid_node = ld_sc1(tl + 1 + lane);
+      const bool tv = lane < tn;
+      NodeFast tslot;
+      const int tnode = tv ? tid_node : -1;
+      if (tv) {
+        rec_load<__HIP_MEMORY_SCOPE_AGENT>(s.rec + (int64_t)tnode * NUM_RW, tslot);
+        if (ext) ext_load(s, tnode, k, tslot);
+        fast_adopt(tslot, k);
+      }
+      uint32_t* out = th.tmx + (b & 1) * MAX_BATCH;
+      // pairs of rows (two independent chains a pass): pair q to helper q % H, wave (q / H) % NW
+      for (int q = h + th.H * wave; 2 * q < B; q += th.H * NW) {
+        const int j = 2 * q, j1 = j + 1;
+        const bool has1 = j1 < B;
+        const DevPod p = L.pod[j];
+        const double ed[2] = {L.pd[j][0], L.pd[j][1]}, rd[2] = {L.pd[j][2], L.pd[j][3]};
+        uint32_t tk = tv ? make_key(fast_total<EXT>(tslot, p, ed, rd, k), tnode) : 0u, tk1 = 0u;
+        if (has1) {
+          const DevPod p1 = L.pod[j1];
+          const double ed1[2] = {L.pd[j1][0], L.pd[j1][1]}, rd1[2] = {L.pd[j1][2], L.pd[j1][3]};
+          tk1 = tv ? make_key(fast_total<EXT>(tslot, p1, ed1, rd1, k), tnode) : 0u;
+        }
+        tk = wave_max_u32(tk);
+        tk1 = wave_max_u32(tk1);
+        if (lane == 0) {
+          st_sc1(out + j, tk);
+          if (has1) st_sc1(out + j1, tk1);
+        }
+      }
+      drain_stores();
+    }
+    __syncthreads();  // (every wave's maxima drained; s_go and the pods are rewritten next batch)
+    if (go > 0 && threadIdx.x == 0) __hip_atomic_fetch_add(th.tready + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // Persistent Reserve chain of a run of pipelined plain batches [b0, b0 + nb): one
 // workgroup for the whole run, so no kernel boundary or cross-stream event sits between two batches.
 // Per batch: wait until its lists are published (ready[b] == pods of b), resolve it, then publish
@@ -5118,25 +5331,40 @@ __global__ __launch_bounds__(res_threads<false>()) void k_resolve_run(SoA s, con
                                                                       int32_t* __restrict__ touched_cnt,
                                                                       uint32_t* __restrict__ chg_glb, int n_nodes,
                                                                       const uint32_t* __restrict__ stale,
-                                                                      const int32_t* __restrict__ stale_cnt, int sorted) {
+                                                                      const int32_t* __restrict__ stale_cnt, int sorted,
+                                                                      THelp th) {
   __shared__ ResLds L;
   __shared__ int32_t s_ok;
-  const ChgSet C = chg_init(L, chg_glb, n_nodes);
   const bool nofix = !QUOTA && stale != nullptr;
+  if (blockIdx.x > 0) {  // a T-row helper
+    if (nofix) t_helper<EXT>(L, s, pods, bases, b0, nb, k, done, err, th, (int)blockIdx.x - 1, &s_ok);
+    return;
+  }
+  if (!nofix) th.H = 0, th.tlist = nullptr;
+  const ChgSet C = chg_init(L, chg_glb, n_nodes);
   for (int b = b0; b < b0 + nb; b++) {
     const int base = bases[b], B = bases[b + 1] - bases[b];
-    if (threadIdx.x == 0) s_ok = wait_at_least(ready + b, B, err);
-    __syncthreads();
-    if (!s_ok) return;
+    if (!nofix || b == b0) {  // (a stale-list batch after the first: polled while its predecessor wrote back)
+      if (threadIdx.x == 0) s_ok = wait_at_least(ready + b, B, err);
+      __syncthreads();
+      if (!s_ok) return;
+    }
     const int par = b & 1;
     const bool has_t = nofix && b > b0;       // the previous batch's changed nodes (L.trec)
     const bool keep = nofix && b + 1 < b0 + nb;  // this batch's are the next one's T
     resolve_batch<false, false, QUOTA, EXT>(L, C, s, pods, base, B, k, nofix ? stale + (int64_t)par * MAX_BATCH * KSTALE : cand,
                                        nofix ? stale_cnt + par * MAX_BATCH : cand_cnt, chosen, chosen_score, global_offset,
                                        stamps, pstamps, b, dev_alloc, nullptr, touched_out, touched_cnt, has_t, keep,
-                                       nofix ? KSTALE : KMAX, !nofix || sorted != 0);  // (k_fixup's lists: by rank)
-    __syncthreads();  // wave 0 drained its stores (replay_batch), so they are performed
-    if (threadIdx.x == 0) st_sc1(done + b, 1);
+                                       nofix ? KSTALE : KMAX, !nofix || sorted != 0,  // (k_fixup's lists: by rank)
+                                       has_t ? done + (b - 1) : nullptr, th);
+    // the next stale-list batch's lists: wave 1 waits for them while wave 0 writes this batch back (every load
+    // of them comes after the barrier below, so after the flag was seen)
+    if (keep && threadIdx.x == 64) s_ok = wait_at_least(ready + b + 1, bases[b + 2] - bases[b + 1], err);
+    __syncthreads();
+    if (keep && !s_ok) return;
+    // wave 0 drained its stores (replay_batch / a batch without a successor), so they are performed; a stale-list
+    // batch with a successor is published by that successor's prologue
+    if (threadIdx.x == 0 && !keep) st_sc1(done + b, 1);
   }
 }
 
@@ -5709,6 +5937,8 @@ struct DeviceState {
   hipEvent_t ev_start = nullptr;
   bool pipeline = true;             // ke_set_pipeline
   bool pipe_fixup = false;          // ke_set_pipeline(2): exact lists from k_fixup for every run (else quota runs only)
+  bool eval_patch = true;           // two eval streams: evals wait for batch b-3, k_patch adds b-2 (KOORDEVAL_EVAL_PATCH)
+  int t_helpers = 4;                // T-row helper workgroups of a stale-list run (THelp; KOORDEVAL_T_HELPERS)
   // the Reservation plugin of a singleton batch (k_rsv_pick): its pairs and result words
   RsvPair* d_rsv = nullptr;
   int64_t rsv_cap = 0;              // bytes
@@ -5746,6 +5976,8 @@ int device_create(Context* ctx) {
   HIP_OK(hipSetDevice(d->device));
   int prio_lo = 0, prio_hi = 0;  // the Reserve chain gets the higher queue priority
   HIP_OK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+  if (const char* e = std::getenv("KOORDEVAL_T_HELPERS")) d->t_helpers = std::max(0, std::min(8, std::atoi(e)));
+  if (const char* e = std::getenv("KOORDEVAL_EVAL_PATCH")) d->eval_patch = std::atoi(e) != 0;
   HIP_OK(hipStreamCreateWithPriority(&d->stream, hipStreamNonBlocking, prio_hi));
   HIP_OK(hipStreamCreateWithPriority(&d->estream, hipStreamNonBlocking, prio_lo));
   for (int e = 0; e < DeviceState::EV_RING; e++) {
@@ -6463,15 +6695,21 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     if (e - b >= 2) run_end[b] = e;
     b = e;
   }
-  // device: bases [n+1], ready [n], done [n], error word; fixup stamps [2n]
-  const int64_t sched_words = 3 * ((int64_t)n_batches + 1) + 1;
-  rc = ensure((void**)&d->d_sched, &d->sched_cap, sizeof(int32_t) * sched_words + sizeof(uint64_t) * 2 * n_batches + 8);
+  // device: bases [n+1], ready [n], done [n], error word, T-helper counts [n]; fixup stamps [2n]; the T
+  // helpers' lists and maxima (THelp)
+  const int64_t sched_words = 4 * ((int64_t)n_batches + 1) + 1;
+  constexpr int64_t THELP_WORDS = 2 * (1 + MAX_BATCH) + 2 * MAX_BATCH;
+  rc = ensure((void**)&d->d_sched, &d->sched_cap,
+              sizeof(int32_t) * sched_words + sizeof(uint64_t) * 2 * n_batches + 8 + sizeof(int32_t) * THELP_WORDS);
   if (rc) return rc;
   int32_t* d_bases = d->d_sched;
   int32_t* d_ready = d_bases + n_batches + 1;
   int32_t* d_done = d_ready + n_batches + 1;
   int32_t* d_err = d_done + n_batches + 1;
+  int32_t* d_tready = d_err + 1;
   uint64_t* d_fst = reinterpret_cast<uint64_t*>(d->d_sched + ((sched_words + 1) & ~1LL));
+  int32_t* d_tlist = reinterpret_cast<int32_t*>(d_fst + 2 * n_batches);
+  uint32_t* d_tmx = reinterpret_cast<uint32_t*>(d_tlist + 2 * (1 + MAX_BATCH));
   HIP_OK(hipMemcpyAsync(d_bases, bases.data(), sizeof(int32_t) * (n_batches + 1), hipMemcpyHostToDevice, d->stream));
   HIP_OK(hipMemsetAsync(d_ready, 0, sizeof(int32_t) * (sched_words - n_batches - 1), d->stream));
   HIP_OK(hipMemsetAsync(d_fst, 0, sizeof(uint64_t) * 2 * n_batches, d->stream));
@@ -6505,7 +6743,8 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   // can (split or one-workgroup select, unsharded) -- *published tells the caller
   bool published = false;
   auto eval_select = [&](int b, bool pipe, hipStream_t es, const int32_t* dwait = nullptr,
-                         int32_t* rpub = nullptr, bool alt = false) -> int {
+                         int32_t* rpub = nullptr, bool alt = false, const int32_t* pwait = nullptr,
+                         const int32_t* ptl = nullptr) -> int {
     published = false;
     uint16_t* const scores = alt ? d->d_scores2 : d->d_scores;  // (the second eval stream's buffers)
     uint32_t* const split = alt ? d->d_split2 : d->d_split;
@@ -6572,6 +6811,11 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                              nullptr, nullptr, nullptr, nullptr, ds ? d->d_dsmax : nullptr, cpu ? d->d_aff : nullptr,
                              ds ? d->d_dsraw : nullptr, fb);
         }
+      }
+      if (pwait) {  // the nodes batch b-2 changed, once it is done (k_patch)
+        hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), 0, es, nullptr, 0, pwait, d_err, nullptr);
+        hipLaunchKernelGGL(((k.flags & AF_EXT) ? k_patch<true> : k_patch<false>), dim3((unsigned)bp), dim3(64), 0, es,
+                           d->soa, d->d_pods, bbase, k, ptl, scores, d->capacity);
       }
       if (ds && sharded && !d->loopback)  // DefaultNormalizeScore's max over the feasible nodes of all ranks
         RCCL_OK(ncclAllReduce(d->d_dsmax, d->d_dsmax, 1, ncclUint32, ncclMax, d->comm, es));
@@ -6651,12 +6895,13 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       const int r0 = b, e = run_end[b];
       const bool ext = (k.flags & AF_EXT) != 0;
       const bool fixup = quota || d->pipe_fixup;  // the replay_batch path (quota) needs exact lists
+      const THelp th{d_tlist, d_tmx, d_tready, fixup ? 0 : d->t_helpers};
       hipLaunchKernelGGL((quota ? (ext ? k_resolve_run<true, true> : k_resolve_run<true, false>)
-                                : (ext ? k_resolve_run<false, true> : k_resolve_run<false, false>)), dim3(1), dim3(res_threads<false>()), 0,
+                                : (ext ? k_resolve_run<false, true> : k_resolve_run<false, false>)), dim3(1 + th.H), dim3(res_threads<false>()), 0,
                          d->stream, d->soa, d->d_pods, d_bases, r0, e - r0, k, d->d_cand, d->d_cand_cnt, d->d_chosen,
                          d->d_chosen_score, ctx->cfg.global_node_offset, d->d_stamps, d->d_stamps + (n_pods + 2),
                          d->d_devalloc, d_ready, d_done, d_err, d->d_trows, d->d_tcnt, d->d_chg, N,
-                         fixup ? nullptr : d->d_stale, fixup ? nullptr : d->d_stale_cnt, (int)run_sorted(r0, e));
+                         fixup ? nullptr : d->d_stale, fixup ? nullptr : d->d_stale_cnt, (int)run_sorted(r0, e), th);
       // batches alternate between the eval streams -- unsharded only: a node-sharded batch's all-gather must run
       // in the same order on every rank's communicator, which two streams of one rank would not guarantee
       const bool two_es = !fixup && d->estream2 != nullptr && !sharded;
@@ -6667,7 +6912,10 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
         if (!fixup) {  // the stale lists go to the replay as they are; batch q's eval waits for batch q-2's done
           const bool alt = two_es && ((q - r0) & 1);
           hipStream_t es = alt ? d->estream2 : d->estream;
-          rc = eval_select(q, true, es, q - 2 >= r0 ? d_done + (q - 2) : nullptr, d_ready + q, alt);
+          // two eval streams: batch q's eval waits only for batch q-3, k_patch brings in batch q-2's changed nodes
+          const bool patch = two_es && d->eval_patch && q - 2 >= r0;
+          rc = eval_select(q, true, es, q - (patch ? 3 : 2) >= r0 ? d_done + (q - (patch ? 3 : 2)) : nullptr, d_ready + q,
+                           alt, patch ? d_done + (q - 2) : nullptr, d_tlist + ((q - 2) & 1) * (1 + MAX_BATCH));
           if (rc) return rc;
           if (!published)
             hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), 0, es, d_ready + q, (int32_t)batches[q].pods, nullptr,
@@ -6885,10 +7133,16 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   ctx->kstat_resolve_prologue_ms = pro / n_batches;
   ctx->kstat_resolve_loop_ms = loop / n_batches;
   for (int i = 0; i < 6; i++) ctx->kstat_resolve_phase_ms[i] = ph[i] * ms_per_tick / n_batches;
+  std::vector<char> in_run((size_t)n_batches, 0);  // a pipelined batch after the first of its run
+  for (int b = 0; b < n_batches; b++)
+    if (run_end[b] > 0)
+      for (int q = b + 1; q < run_end[b]; q++) in_run[(size_t)q] = 1;
+  std::vector<char> in_run_t(in_run);  // ... with T maxima the helpers may deliver
+  if (quota || d->pipe_fixup || d->t_helpers == 0) std::fill(in_run_t.begin(), in_run_t.end(), 0);
   {  // the speculative replay's first round in detail: T set-up, the prediction loop, wave 1's T
      // rows (concurrent with the loop), wave 0's R
     double sub[4] = {0, 0, 0, 0};
-    int ns = 0;
+    int ns = 0, nt = 0, hits = 0;
     for (int b = 0; b < n_batches; b++) {
       const uint64_t* p = &pst[PST * (size_t)b];
       if (!(p[1] > p[4])) continue;
@@ -6897,8 +7151,10 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       sub[1] += (double)(p[9] > p[8] ? p[9] - p[8] : 0);
       sub[2] += (double)(p[10] > p[8] ? p[10] - p[8] : 0);
       sub[3] += (double)(p[11] > p[1] ? p[11] - p[1] : 0);
+      if (in_run_t[(size_t)b]) nt++, hits += p[12] == 1;
     }
     for (int i = 0; i < 4; i++) ctx->kstat_resolve_sub_ms[i] = ns ? sub[i] * ms_per_tick / ns : 0;
+    ctx->kstat_resolve_sub_ms[4] = nt ? (double)hits / nt : 0;
   }
   ctx->kstat_numa_deferred = 0;
   for (uint32_t c : dcnt) ctx->kstat_numa_deferred += c;
@@ -6907,10 +7163,6 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   // fixup = k_fixup's workgroup 0 from its wait to its publish
   double res_sum = 0, ho_sum = 0, fx_sum = 0;
   int ho_n = 0, fx_n = 0;
-  std::vector<char> in_run((size_t)n_batches, 0);  // a pipelined batch after the first of its run
-  for (int b = 0; b < n_batches; b++)
-    if (run_end[b] > 0)
-      for (int q = b + 1; q < run_end[b]; q++) in_run[(size_t)q] = 1;
   for (int b = 0; b < n_batches; b++) {
     res_sum += (double)(st[b + 1] - pst[PST * (size_t)b]) * ms_per_tick;
     if (fst[2 * b + 1] > fst[2 * b]) {

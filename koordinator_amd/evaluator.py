@@ -359,14 +359,15 @@ class Evaluator:
         self._check(self.lib.ke_debug_spec_failed(self.h, C.byref(sf)))
         ph = np.zeros(6, np.float64)
         self._check(self.lib.ke_debug_resolve_phases(self.h, abi.ptr(ph)))
-        sub = np.zeros(4, np.float64)
+        sub = np.zeros(5, np.float64)
         self._check(self.lib.ke_debug_resolve_subphases(self.h, abi.ptr(sub)))
         return {"eval_ms": ms4[0], "select_ms": ms4[1], "fixup_ms": ms4[2], "resolve_ms": ms4[3], "samples": n.value,
                 "pipelined_batches": npipe.value, "enqueue_ms": ms4[4], "handoff_ms": ms4[5],
                 "rows_fetched": ms4[6], "rows_changed": ms4[7], "spec_failed_rounds": sf.value,
                 "resolve_prologue_ms": p.value, "resolve_replay_ms": r.value,
                 "resolve_phases_ms": dict(zip(["prologue", "spec_predict", "spec_reserve_eval", "spec_verify", "spec_later_rounds", "writeback",
-                                               "sub_t_setup", "sub_predict_loop", "sub_t_rows_wave1", "sub_reserve_R"],
+                                               "sub_t_setup", "sub_predict_loop", "sub_t_rows_wave1", "sub_reserve_R",
+                                               "t_helper_hit"],
                                               ph.tolist() + sub.tolist()))}
 
     def bench_eval_kernel(self, pods, now_ns, iters):
