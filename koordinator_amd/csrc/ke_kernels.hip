@@ -4366,6 +4366,7 @@ struct THelp {
   uint32_t* tmx;    // [2][MAX_BATCH]: the T maxima of a batch's pods (the helpers write them)
   int32_t* tready;  // [batch]: helpers done with the batch (relaxed agent adds)
   int H;            // helper workgroups (0: none)
+  int ign;          // test hook: the Reserve workgroup ignores the helpers' maxima (its own rows after the barrier)
 };
 
 struct ResLdsCore {
@@ -4647,7 +4648,7 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
         // the helpers' T maxima of this batch (a bounded wait: rows whose maximum did not arrive are evaluated
         // after the barrier)
         int ok = 0;
-        if (lane == 0) {
+        if (lane == 0 && !th.ign) {
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
           while (true) {
             if (ld_sc1(th.tready + batch_index) >= th.H) {
@@ -4869,7 +4870,7 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
                                               int32_t* __restrict__ touched_cnt = nullptr,
                                               bool has_t = false, bool keep = false, int LS = KMAX,
                                               bool sorted = false, int32_t* __restrict__ pub_done = nullptr,
-                                              const THelp th = THelp{nullptr, nullptr, nullptr, 0}) {
+                                              const THelp th = THelp{nullptr, nullptr, nullptr, 0, 0}) {
   const int tid = threadIdx.x;
   constexpr int RES_THREADS = res_threads<NUMA>();
   if (tid == 0) pstamps[PST * batch_index] = __builtin_amdgcn_s_memrealtime();
@@ -5939,6 +5940,7 @@ struct DeviceState {
   bool pipe_fixup = false;          // ke_set_pipeline(2): exact lists from k_fixup for every run (else quota runs only)
   bool eval_patch = true;           // two eval streams: evals wait for batch b-3, k_patch adds b-2 (KOORDEVAL_EVAL_PATCH)
   int t_helpers = 4;                // T-row helper workgroups of a stale-list run (THelp; KOORDEVAL_T_HELPERS)
+  int t_help_ignore = 0;            // test hook (KOORDEVAL_T_HELPERS_IGNORE): the replay's own T rows every batch
   // the Reservation plugin of a singleton batch (k_rsv_pick): its pairs and result words
   RsvPair* d_rsv = nullptr;
   int64_t rsv_cap = 0;              // bytes
@@ -5978,6 +5980,7 @@ int device_create(Context* ctx) {
   HIP_OK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
   if (const char* e = std::getenv("KOORDEVAL_T_HELPERS")) d->t_helpers = std::max(0, std::min(8, std::atoi(e)));
   if (const char* e = std::getenv("KOORDEVAL_EVAL_PATCH")) d->eval_patch = std::atoi(e) != 0;
+  if (const char* e = std::getenv("KOORDEVAL_T_HELPERS_IGNORE")) d->t_help_ignore = std::atoi(e) != 0;
   HIP_OK(hipStreamCreateWithPriority(&d->stream, hipStreamNonBlocking, prio_hi));
   HIP_OK(hipStreamCreateWithPriority(&d->estream, hipStreamNonBlocking, prio_lo));
   for (int e = 0; e < DeviceState::EV_RING; e++) {
@@ -6895,7 +6898,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       const int r0 = b, e = run_end[b];
       const bool ext = (k.flags & AF_EXT) != 0;
       const bool fixup = quota || d->pipe_fixup;  // the replay_batch path (quota) needs exact lists
-      const THelp th{d_tlist, d_tmx, d_tready, fixup ? 0 : d->t_helpers};
+      const THelp th{d_tlist, d_tmx, d_tready, fixup ? 0 : d->t_helpers, d->t_help_ignore};
       hipLaunchKernelGGL((quota ? (ext ? k_resolve_run<true, true> : k_resolve_run<true, false>)
                                 : (ext ? k_resolve_run<false, true> : k_resolve_run<false, false>)), dim3(1 + th.H), dim3(res_threads<false>()), 0,
                          d->stream, d->soa, d->d_pods, d_bases, r0, e - r0, k, d->d_cand, d->d_cand_cnt, d->d_chosen,

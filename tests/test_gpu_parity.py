@@ -218,6 +218,32 @@ def test_schedule_large_cluster_prefix(gpu):
     assert ev.check_records(synth.T0) == 0
 
 
+# ---- the stale-list run's options: T-row helpers, progressive R+S, patched early eval -----------------
+@pytest.mark.parametrize("helpers,patch,ignore", [("0", "1", "0"), ("4", "0", "0"), ("4", "1", "1"), ("8", "1", "0")],
+                         ids=["no-helpers", "no-patch", "helpers-ignored", "8-helpers"])
+@pytest.mark.parametrize("n_nodes,n_pods,seed", [(20_000, 3000, 71), (150, 2500, 72)])
+def test_stale_run_options_match_oracle(gpu, monkeypatch, n_nodes, n_pods, seed, helpers, patch, ignore):
+    """The stale-list run with its helper workgroups off / on (progressive R+S) / on but ignored (the replay's
+    own T rows after the barrier), and with the eval waiting for batch b-2 instead of k_patch: every variant
+    places exactly as the oracle and leaves exact rows and records (KOORDEVAL_* are read per device context)."""
+    monkeypatch.setenv("KOORDEVAL_T_HELPERS", helpers)
+    monkeypatch.setenv("KOORDEVAL_EVAL_PATCH", patch)
+    monkeypatch.setenv("KOORDEVAL_T_HELPERS_IGNORE", ignore)
+    cl = synth.make_cluster(n_nodes, synth.BASE_SEED + seed)
+    pods = synth.make_pods(n_pods, synth.BASE_SEED + 100 + seed)
+    ev, o = both(synth.config(n_nodes), cl)
+    c1, s1 = ev.schedule(pods, synth.T0)
+    ks = ev.kernel_stats()
+    assert ks["pipelined_batches"] > 0
+    hit = ks["resolve_phases_ms"]["t_helper_hit"]
+    assert hit == 0 if helpers == "0" or ignore == "1" else hit > 0
+    c0, s0 = o.schedule(pods, synth.T0)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    dev, host = ev.debug_rows(synth.T0)
+    assert np.array_equal(dev, host)
+    assert ev.check_records(synth.T0) == 0
+
+
 # ---- pipelined schedule (two streams, stale lists -> the replay's T slots, or k_fixup) ---------------
 @pytest.mark.parametrize("mode", [True, "fixup"], ids=["stale-slots", "fixup"])
 @pytest.mark.parametrize("n_nodes,n_pods,seed", [(20_000, 3000, 71), (150, 2500, 72), (40, 1200, 73)])
