@@ -4180,6 +4180,10 @@ __global__ __launch_bounds__(FIX_BLOCK) void k_fixup(SoA s, const DevPod* __rest
 // or hold the eval stream until batch q-1's Reserve is done (done_wait), so that batch q+1's eval sees every
 // Reserve of batches <= q-1 -- its stale keys differ from the exact ones only on the nodes batch q changes --
 // and its lists may reuse batch q-1's half of the double buffer.
+// Dynamic LDS of the eval streams' LDS-free kernels (k_handoff, k_patch): a workgroup holding any LDS cannot
+// share a CU with a Reserve workgroup (which leaves 64 B of the CU's LDS), so their waves never take issue
+// slots from the replay's latency-bound waves.
+constexpr unsigned EXCL_LDS = 1024;
 __global__ void k_handoff(int32_t* __restrict__ ready, int32_t n, const int32_t* __restrict__ done_wait,
                           int32_t* __restrict__ err, uint64_t* __restrict__ fstamp) {
   if (threadIdx.x != 0) return;
@@ -4474,6 +4478,62 @@ __device__ __forceinline__ void spec_predict(ResLds& L, const ChgSet& C, int sta
   }
 }
 
+// The prediction loop for sorted lists and the LDS changed set, shortened to the per-pod instructions the chain
+// needs (the loop is issue-bound: one wave per SIMD, ~11 cycles per dependent instruction): pod j's key word is
+// read a step ahead (it misses only pod j-1's prediction, compared as a node), the untaken test is one bit
+// extract and two compares, the prediction one ballot / find-first / lane read, and lane 0's stores (prediction,
+// key, changed-set bit) are one exec-masked group without a branch.  A pod whose first 64 keys are all taken
+// reads the second half of its list (rare: j + |T| keys at most precede its prediction).
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
+__device__ __forceinline__ void lane0_record(uint32_t pa, uint32_t xn, uint32_t xk, uint32_t ca, uint32_t cm) {
+  uint64_t sv;
+  asm volatile(
+      "s_mov_b64 %0, exec\n\t"
+      "s_mov_b64 exec, 1\n\t"
+      "ds_write2_b32 %1, %2, %3 offset1:64\n\t"
+      "ds_or_b32 %4, %5\n\t"
+      "s_mov_b64 exec, %0"
+      : "=&s"(sv)
+      : "v"(pa), "v"(xn), "v"(xk), "v"(ca), "v"(cm)
+      : "memory");
+}
+__device__ __forceinline__ void spec_predict_lean(ResLds& L, const ChgSet& C, int start, int end, int LS, bool two,
+                                                  int lane) {
+  const uint32_t cbase = lds_addr(C.lds), pbase = lds_addr(&L.sp.xnode[0]);
+  auto node_of = [](uint32_t k) { return (int32_t)(KEY_IDX_MASK - (k & KEY_IDX_MASK)); };
+  auto key_at = [&](int j) -> uint32_t { return j < end ? L.cand[j * LS + lane] : 0u; };
+  auto word_of = [&](int n) -> uint32_t { return C.lds[(uint32_t)n >> 5]; };
+  auto node_of0 = [&](uint32_t k) { return k ? node_of(k) : 0; };  // (key 0: word 0, masked by the key test)
+  uint32_t kA = key_at(start), kB = key_at(start + 1);
+  int32_t nA = node_of0(kA);
+  uint32_t wA = word_of(nA);
+  int32_t xprev = -1;
+  for (int j = start; j < end; j++) {
+    const int32_t nB = node_of0(kB);
+    const uint32_t wB = word_of(nB);     // after the set updates of pods < j (LDS order); misses pod j's
+    const uint32_t kC = key_at(j + 2);
+    const bool untaken = (kA != 0u) & (((wA >> (nA & 31)) & 1u) == 0u) & (nA != xprev);
+    const uint64_t u = __ballot(untaken);
+    uint32_t bu;
+    int32_t xn;
+    if (__builtin_expect(u != 0, 1)) {
+      const int l = __builtin_ctzll(u);
+      bu = (uint32_t)__builtin_amdgcn_readlane((int)kA, l);
+      xn = __builtin_amdgcn_readlane(nA, l);
+    } else {  // every one of the first 64 keys taken: the second half, against the set as it is now
+      const uint32_t k1 = two && j < end ? L.cand[j * LS + 64 + lane] : 0u;
+      const int32_t n1 = node_of0(k1);
+      const uint64_t u1 = __ballot(k1 != 0u && !((word_of(n1) >> (n1 & 31)) & 1u) && n1 != xprev);
+      bu = u1 ? (uint32_t)__builtin_amdgcn_readlane((int)k1, __builtin_ctzll(u1)) : 0u;
+      xn = bu ? node_of(bu) : -1;
+    }
+    const uint32_t ca = cbase + (xn >= 0 ? ((uint32_t)xn >> 5) << 2 : 0u), cm = xn >= 0 ? 1u << (xn & 31) : 0u;
+    lane0_record(pbase + 4u * (uint32_t)j, (uint32_t)xn, bu, ca, cm);
+    xprev = xn;
+    kA = kB, nA = nB, wA = wB, kB = kC;
+  }
+}
+
 // Speculative replay of a plain batch (LoadAware + NodeNUMAResource (+ FitPlus / SRA / Fit) pods, no quota) on
 // every wave of the workgroup ("speculative replay").  The sequential replay decides pod j as
 // max(bu_j, bc_j): bu_j its best candidate no earlier pod of the batch took (exact: its snapshot key), bc_j
@@ -4636,7 +4696,7 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
         if (sorted) spec_predict<true, true>(L, C, start, end, LS, two, lane);
         else spec_predict<true, false>(L, C, start, end, LS, two, lane);
       } else {
-        if (sorted) spec_predict<false, true>(L, C, start, end, LS, two, lane);
+        if (sorted) spec_predict_lean(L, C, start, end, LS, two, lane);
         else spec_predict<false, false>(L, C, start, end, LS, two, lane);
       }
       if (first && lane == 0) pst[9] = __builtin_amdgcn_s_memrealtime();  // the prediction loop's end
@@ -6772,7 +6832,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     // spinning on the flag would hold the CUs the other stream's select needs)
     const bool plain_rec = !cpu && !ds && !numa && use_record_eval(bp);
     const bool wait_kernel = dwait && (!plain_rec || alt || (d->estream2 != nullptr && !sharded) || hi <= lo);
-    if (wait_kernel) hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), 0, es, nullptr, 0, dwait, d_err, nullptr);
+    if (wait_kernel) hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), EXCL_LDS, es, nullptr, 0, dwait, d_err, nullptr);
     if (prof) HIP_OK(hipEventRecord(pe[0], es));
     const int L = pipe ? KSTALE : KMAX, kext = pipe ? KMAX : 0;
     uint32_t* lists = pipe ? d->d_stale + (size_t)(b & 1) * MAX_BATCH * KSTALE : d->d_cand;
@@ -6816,8 +6876,8 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
         }
       }
       if (pwait) {  // the nodes batch b-2 changed, once it is done (k_patch)
-        hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), 0, es, nullptr, 0, pwait, d_err, nullptr);
-        hipLaunchKernelGGL(((k.flags & AF_EXT) ? k_patch<true> : k_patch<false>), dim3((unsigned)bp), dim3(64), 0, es,
+        hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), EXCL_LDS, es, nullptr, 0, pwait, d_err, nullptr);
+        hipLaunchKernelGGL(((k.flags & AF_EXT) ? k_patch<true> : k_patch<false>), dim3((unsigned)bp), dim3(64), EXCL_LDS, es,
                            d->soa, d->d_pods, bbase, k, ptl, scores, d->capacity);
       }
       if (ds && sharded && !d->loopback)  // DefaultNormalizeScore's max over the feasible nodes of all ranks
@@ -6921,7 +6981,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                            alt, patch ? d_done + (q - 2) : nullptr, d_tlist + ((q - 2) & 1) * (1 + MAX_BATCH));
           if (rc) return rc;
           if (!published)
-            hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), 0, es, d_ready + q, (int32_t)batches[q].pods, nullptr,
+            hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), EXCL_LDS, es, d_ready + q, (int32_t)batches[q].pods, nullptr,
                                d_err, nullptr);
           continue;
         }
