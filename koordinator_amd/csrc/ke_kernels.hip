@@ -6786,7 +6786,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   HIP_OK(hipEventRecord(d->ev_start, d->stream));
   HIP_OK(hipStreamWaitEvent(d->estream, d->ev_start, 0));
   // sampled per-kernel HIP event pairs (ke_set_profiling) on the eval stream: eval, select
-  constexpr int PE = 3;
+  constexpr int PE = 4;  // eval start, eval end, select end, select start (after k_patch and its wait)
   const int every = d->profile_every;
   std::vector<hipEvent_t> ev;
   if (every > 0) {
@@ -6875,6 +6875,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                              ds ? d->d_dsraw : nullptr, fb);
         }
       }
+      if (prof) HIP_OK(hipEventRecord(pe[1], es));
       if (pwait) {  // the nodes batch b-2 changed, once it is done (k_patch)
         hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), EXCL_LDS, es, nullptr, 0, pwait, d_err, nullptr);
         hipLaunchKernelGGL(((k.flags & AF_EXT) ? k_patch<true> : k_patch<false>), dim3((unsigned)bp), dim3(64), EXCL_LDS, es,
@@ -6882,7 +6883,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       }
       if (ds && sharded && !d->loopback)  // DefaultNormalizeScore's max over the feasible nodes of all ranks
         RCCL_OK(ncclAllReduce(d->d_dsmax, d->d_dsmax, 1, ncclUint32, ncclMax, d->comm, es));
-      if (prof) HIP_OK(hipEventRecord(pe[1], es));
+      if (prof) HIP_OK(hipEventRecord(pe[3], es));
       auto select = [&](int slo, int shi, uint32_t* cand, int32_t* cnt, int32_t* pub) {
         // register-resident when a wave's segment fits SEL_RC steps, else streamed
         const bool rc = select_seg(slo, shi) <= SEL_RC * 512;
@@ -6929,6 +6930,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       }
     } else {
       if (prof) HIP_OK(hipEventRecord(pe[1], es));
+      if (prof) HIP_OK(hipEventRecord(pe[3], es));
       HIP_OK(hipMemsetAsync(lists_cnt, 0, sizeof(int32_t) * MAX_BATCH, es));
     }
     if (prof) HIP_OK(hipEventRecord(pe[2], es));
@@ -7255,7 +7257,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   for (size_t s = 0; s + PE - 1 < ev.size(); s += PE) {
     float a = 0, b = 0;
     HIP_OK(hipEventElapsedTime(&a, ev[s], ev[s + 1]));
-    HIP_OK(hipEventElapsedTime(&b, ev[s + 1], ev[s + 2]));
+    HIP_OK(hipEventElapsedTime(&b, ev[s + 3], ev[s + 2]));
     ctx->kstat_eval_ms += a;
     ctx->kstat_select_ms += b;
     ctx->kstat_samples++;
