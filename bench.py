@@ -165,6 +165,24 @@ def cpu_baseline(cl, pods, cfg, seconds):
                       f"value = the fastest ({best} threads)"}
 
 
+def c3_parity(chosen, score, n_nodes, n_pods, config):
+    """The timed run's placements and scores against the oracle's full-queue fixture (tests/golden/
+    make_c3_fixture.py: the oracle scheduled the same 100k-pod queue on the same 50k-node cluster), compared after
+    the timed region.  Only for the default config-3 workload (other sizes have no fixture)."""
+    f = os.path.join(ROOT, "tests", "golden", "c3_placements.npz")
+    if config != 3 or not os.path.exists(f):
+        return "unchecked (no fixture for this workload)"
+    g = np.load(f)
+    if int(g["nodes"]) != n_nodes:
+        return "unchecked (no fixture for this workload)"
+    m = min(n_pods, int(g["pods"]))
+    ok = (chosen[:m] == g["chosen"][:m]) & (score[:m] == g["score"][:m].astype(np.int32))
+    if ok.all():
+        return f"bit-exact {m}/{int(g['pods'])} (placements + scores vs the oracle fixture)"
+    bad = np.flatnonzero(~ok)
+    return f"MISMATCH {len(bad)}/{m} (first at pod {int(bad[0])})"
+
+
 def alg_batch_bytes(n_nodes, b):
     """SURVEY.md §8(d) algorithmic bytes of one B-pod batch: the node SoA row once (S_row = ke_row_bytes()),
     the pod records (S_pod = ke_pod_record_bytes()) and the top-k out (B * k * 12 B, k = KMAX)."""
@@ -275,10 +293,13 @@ def main():
     lat, plat, evm, sel, samples, rsplit, npipe, hs, kss = [], [], [], [], 0, [], 0, [], []
     placed = 0
     n_batches = 0
+    got_c, got_s = [], []
     barrier()
     t0 = time.perf_counter()
     for s in range(K):
-        chosen, _ = ev.schedule(pods[s * slice_len:(s + 1) * slice_len], synth.T0)
+        chosen, score = ev.schedule(pods[s * slice_len:(s + 1) * slice_len], synth.T0)
+        got_c.append(chosen)
+        got_s.append(score)
         placed += int((chosen >= 0).sum())
         _, per_batch = ev.stats()
         lat.extend(per_batch.tolist())
@@ -346,6 +367,7 @@ def main():
                              a.pipeline_fixup and not a.no_pipeline),
     }
     ev.close()
+    out["parity"] = c3_parity(np.concatenate(got_c), np.concatenate(got_s), N, K * slice_len, a.config)
     if world == 1 and a.stream_nodes > 0:
         out["stream_roofline"] = stream_sweep(a.stream_nodes, a.batch)
     if world == 1 and not a.no_cpu_baseline:

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define KE_ABI_VERSION 10
+#define KE_ABI_VERSION 11
 #define KE_ABSENT (-1)
 
 typedef struct ke_ctx ke_ctx; /* one evaluator context (ke_create) */
@@ -648,7 +648,7 @@ int ke_abi_version(void);
 /* sizeof() of ke_config, ke_node, ke_node_metric, ke_pod_metric, ke_aggregated_usage, ke_pod,
  * ke_resource_map, ke_loadaware_args, ke_numa_args, ke_deviceshare_args, ke_device, ke_numa_zone, ke_cpu,
  * ke_quota_args, ke_quota, ke_gpu_partition, ke_ext_args, ke_node_resource, ke_pod_allocation, ke_pod_device_hints,
- * ke_gpu_template, ke_reservation (in that order) for binding-layout checks. */
+ * ke_gpu_template, ke_reservation, ke_reservation_alloc (in that order) for binding-layout checks. */
 int ke_abi_struct_sizes(int32_t* sizes, int32_t n);
 /* 1 if this build has a usable HIP device and its gfx950 kernels loaded, else 0. */
 int ke_device_available(void);
@@ -727,8 +727,8 @@ int ke_node_devices_delete(ke_ctx* ctx, int32_t node);
  * Pods that match reservations take the nominated-reservation path below (ke_pod_reservations).
  * What a reservation's reserve pod holds beyond NodeInfo — a NUMA allocation or a cpuset in the resource manager
  * (nodenumaresource/reservation.go:185-259), device instances in the device cache (deviceshare/reservation.go:
- * 136-195) — and allocatable names other than cpu / memory are flagged in `holds`; such a reservation is refused
- * (KE_ERR_UNSUPPORTED from ke_reservations_load) rather than scheduled without its restore. */
+ * 136-195) — comes with ke_reservations_load_ex (ke_reservation_alloc); `holds` states which (the records decide).
+ * Allocatable names other than cpu / memory (KE_RSV_OTHER_ALLOCATABLE) are refused (KE_ERR_UNSUPPORTED). */
 #define KE_RSV_POLICY_DEFAULT 0    /* spec.allocatePolicy "" */
 #define KE_RSV_POLICY_ALIGNED 1    /* Aligned */
 #define KE_RSV_POLICY_RESTRICTED 2 /* Restricted (ResourceNames = the allocatable's names) */
@@ -744,7 +744,8 @@ typedef struct ke_reservation {
   uint8_t available;      /* IsAvailable() and no ParseError                                     */
   uint8_t allocate_once;  /* spec.allocateOnce                                                   */
   uint8_t allocate_policy; /* KE_RSV_POLICY_*                                                     */
-  uint8_t holds;          /* KE_RSV_HOLDS_* / KE_RSV_OTHER_ALLOCATABLE; any bit -> KE_ERR_UNSUPPORTED */
+  uint8_t holds;          /* KE_RSV_HOLDS_*: must agree with the ke_reservation_alloc record (without one:
+                             KE_ERR_UNSUPPORTED); KE_RSV_OTHER_ALLOCATABLE: KE_ERR_UNSUPPORTED                 */
   int32_t allocated_pods; /* GetAllocatedPods(): owner pods assigned to it                         */
   int32_t pad2;
   int64_t allocatable[KE_NRES]; /* status.allocatable = the reserve pod's requests: MilliCPU, Memory; a zero
@@ -753,6 +754,40 @@ typedef struct ke_reservation {
   int64_t order;          /* label scheduling.koordinator.sh/reservation-order parsed (ParseInt), 0 = none */
   int64_t uid;            /* the Reservation's UID interned by the caller (release records find it by this; 0 = none) */
 } ke_reservation; /* 64 bytes */
+/* What a reservation's reserve pod holds beyond NodeInfo, and what its owner pods (rInfo.AssignedPods) hold:
+ * the resource manager's NUMANodeResources / CPUSet of the reserve pod and of its owners
+ * (resourceManager.GetAllocatedNUMAResource / GetAllocatedCPUSet, nodenumaresource/reservation.go:185-227), and
+ * the device cache's allocations of both (nodeDevice.getUsed, deviceshare/reservation.go:148-180).  These
+ * allocations must also be part of the node state given with ke_node_numa_set / ke_node_cpus_set /
+ * ke_node_devices_set (the reserve pod and its owners are pods on the node, as the resource manager and the device
+ * cache count them).  From them the evaluator derives, per pod and node, the plugins' reservation restore states:
+ *  - every pod: the unmatched reservations with allocated pods give back what their owners hold twice --
+ *    mergedUnmatchedUsed as reusableResources of the NUMA zones (getAvailableNUMANodeResources,
+ *    node_allocation.go:221-243) and as DeviceShare's preemptible (calcFreeWithPreemptible,
+ *    device_cache.go:322-365);
+ *  - a KE_RSV_MATCHED pod: its matched reservations' NUMA / cpuset / device holdings are allocated from first
+ *    (tryAllocateFromReservation, nodenumaresource/reservation.go:270-424, deviceshare/reservation.go:207-287)
+ *    with the Aligned / Restricted policy of each, in the Filter, the nomination's FilterNominateReservation,
+ *    Score and Reserve.
+ * A placement into a reservation adds the pod's cpuset / NUMA allocation / device minors to the owners' part
+ * (ke_reservation_allocs_get reads them back); its release removes them. */
+typedef struct ke_reservation_alloc {
+  int64_t numa[KE_MAX_NUMA * KE_NRES];       /* the reserve pod's NUMANodeResources: [2*id + r], 0 = none    */
+  int64_t owner_numa[KE_MAX_NUMA * KE_NRES]; /* Σ the owner pods' NUMANodeResources                            */
+  uint64_t cpuset[4];                        /* the reserve pod's CPUSet (bit c = CPU id c)                    */
+  uint64_t owner_cpuset[4];                  /* ∪ the owner pods' CPUSets                                      */
+  uint64_t device_minors;                    /* bit 16*type + minor: instances the reserve pod holds           */
+  uint64_t owner_device_minors;              /* bit 16*type + minor: instances an owner pod holds              */
+  int64_t device[KE_DEV_TYPES][KE_MAX_MINORS][KE_DKEYS];       /* the reserve pod's used per instance, 0 = none */
+  int64_t owner_device[KE_DEV_TYPES][KE_MAX_MINORS][KE_DKEYS]; /* Σ the owner pods' used per instance          */
+} ke_reservation_alloc; /* 2,640 bytes */
+/* ke_reservations_load with the holdings of each reservation (allocs[i] belongs to reservations[i]; NULL = none
+ * holds anything).  The holds bits NUMA / CPUSET / DEVICES must agree with the records (else KE_ERR_INVALID);
+ * the evaluator takes the holdings from the records. */
+int ke_reservations_load_ex(ke_ctx* ctx, int32_t n, const ke_reservation* reservations,
+                            const ke_reservation_alloc* allocs);
+/* The holdings as they stand (owner parts after the Reserves / releases of this context). */
+int ke_reservation_allocs_get(ke_ctx* ctx, int32_t n, ke_reservation_alloc* out);
 /* Generation of the loaded reservation set: bumped by every ke_reservations_load. */
 int32_t ke_reservations_generation(ke_ctx* ctx);
 /* Replace the reservation set (n = 0: none).  A pod placed into a reservation (below) updates its
@@ -790,11 +825,13 @@ int ke_reservations_get(ke_ctx* ctx, int32_t n, ke_reservation* out);
  *  - Reserve (plugin.go:740-793, reservation_info.go:458-468): the nominated reservation of the chosen node
  *    takes Mask(pod requests, names) into allocated and one allocated pod (ke_pod_allocation.reservation); ke_pod_release gives it back (forgetPod,
  *    reservation_info.go:470-482).
+ * fitsNode's pod-count check (plugin.go:450-453) is part of the nomination and the affinity Filter: len(Pods) of
+ * the restored NodeInfo (ke_node.pod_count with the matched reserve pods removed) minus the node's matched
+ * reservations, plus one, within ke_node.allowed_pods.
  * Refused (KE_ERR_UNSUPPORTED, by ke_schedule's argument checks before any pod of the call is scheduled): such a
- * pod with DeviceShare requests, cpuset binding or a NUMA topology policy, a usable matched reservation on a node
- * with a NUMA topology policy, a sharded context; ke_eval of such a pod.  NodeInfo's pod-count check of fitsNode
- * is not modelled (allowedPodNumber taken as not binding).  The lists are consumed by the next ke_schedule call,
- * a refused one included. */
+ * pod with DeviceShare requests, cpuset binding or a NUMA topology policy, a usable matched reservation holding NUMA
+ * resources or a cpuset on a node with a NUMA topology policy, a sharded context; ke_eval of such a pod.  The lists
+ * are consumed by the next ke_schedule call, a refused one included. */
 int ke_pod_reservations(ke_ctx* ctx, int32_t n_pods, const int32_t* offsets, const int32_t* ids);
 /* NodeInfo.Requested / NonZeroRequested (MilliCPU, Memory) of `node` as the plugins see it for a pod that
  * matches no reservation (after the restore above and the Reserves of past ke_schedule calls). */

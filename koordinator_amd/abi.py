@@ -9,7 +9,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 ABSENT = -1
 
 OK = 0
@@ -395,10 +395,18 @@ class Reservation(C.Structure):  # ke_reservation
                 ("order", i64), ("uid", i64)]
 
 
+class ReservationAlloc(C.Structure):  # ke_reservation_alloc
+    _fields_ = [("numa", i64 * (MAX_NUMA * NRES)), ("owner_numa", i64 * (MAX_NUMA * NRES)),
+                ("cpuset", C.c_uint64 * 4), ("owner_cpuset", C.c_uint64 * 4),
+                ("device_minors", C.c_uint64), ("owner_device_minors", C.c_uint64),
+                ("device", ((i64 * 3) * MAX_MINORS) * 3), ("owner_device", ((i64 * 3) * MAX_MINORS) * 3)]
+
+
 STRUCTS = [Config, Node, NodeMetric, PodMetric, AggregatedUsage, Pod, ResourceMap, LoadAwareArgs, NumaArgs,
            DeviceShareArgs, Device, NumaZone, Cpu, QuotaArgs, Quota, GpuPartition, ExtArgs, NodeResource,
-           PodAllocation, PodDeviceHints, GpuTemplate, Reservation]
+           PodAllocation, PodDeviceHints, GpuTemplate, Reservation, ReservationAlloc]
 RESERVATION_DTYPE = np.dtype(Reservation)
+RESERVATION_ALLOC_DTYPE = np.dtype(ReservationAlloc)
 POD_DEVICE_HINTS_DTYPE = np.dtype(PodDeviceHints)
 GPU_TEMPLATE_DTYPE = np.dtype(GpuTemplate)
 QUOTA_DTYPE = np.dtype(Quota)
@@ -513,6 +521,8 @@ EXPORTS = {
     "ke_gpu_templates_load": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_node_device_flags": (C.c_int, [C.c_void_p, i32, i32, i32]),
     "ke_reservations_load": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
+    "ke_reservations_load_ex": (C.c_int, [C.c_void_p, i32, C.c_void_p, C.c_void_p]),
+    "ke_reservation_allocs_get": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_reservations_get": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_pod_reservations": (C.c_int, [C.c_void_p, i32, C.c_void_p, C.c_void_p]),
     "ke_node_info_requested": (C.c_int, [C.c_void_p, i32, C.POINTER(i64), C.POINTER(i64)]),

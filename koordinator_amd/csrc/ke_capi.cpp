@@ -140,7 +140,8 @@ int ke_abi_struct_sizes(int32_t* sizes, int32_t n) {
                          (int32_t)sizeof(ke_quota),        (int32_t)sizeof(ke_gpu_partition),
                          (int32_t)sizeof(ke_ext_args),     (int32_t)sizeof(ke_node_resource),
                          (int32_t)sizeof(ke_pod_allocation), (int32_t)sizeof(ke_pod_device_hints),
-                         (int32_t)sizeof(ke_gpu_template),   (int32_t)sizeof(ke_reservation)};
+                         (int32_t)sizeof(ke_gpu_template),   (int32_t)sizeof(ke_reservation),
+                         (int32_t)sizeof(ke_reservation_alloc)};
   const int32_t m = (int32_t)(sizeof(all) / sizeof(all[0]));
   for (int32_t i = 0; i < n && i < m; i++) sizes[i] = all[i];
   return m;
@@ -309,6 +310,9 @@ int ke_node_topology_delete(ke_ctx* ctx, int32_t node) {
   if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
   NodeState& ns = ctx->c.nodes[node];
+  // the NodeAllocation stays (resource_manager.go keeps nodeAllocations[node] until the Node itself goes)
+  if (!ns.cpus.empty()) ns.kept_cpus = ns.cpus;
+  if (!ns.zones.empty()) ns.kept_zones = ns.zones;
   ns.zones.clear();
   ns.cpus.clear();
   ns.cpu_max_ref = 1;
@@ -379,6 +383,21 @@ int ke_reservations_load(ke_ctx* ctx, int32_t n, const ke_reservation* reservati
   if (!ctx) return fail(KE_ERR_INVALID, "null context");
   flush_mirror(ctx->c);
   return load_reservations(ctx->c, n, reservations);
+}
+
+int ke_reservations_load_ex(ke_ctx* ctx, int32_t n, const ke_reservation* reservations,
+                            const ke_reservation_alloc* allocs) {
+  if (!ctx) return fail(KE_ERR_INVALID, "null context");
+  flush_mirror(ctx->c);
+  return load_reservations(ctx->c, n, reservations, allocs);
+}
+
+int ke_reservation_allocs_get(ke_ctx* ctx, int32_t n, ke_reservation_alloc* out) {
+  if (!ctx || n < 0 || (n > 0 && !out) || n > (int32_t)ctx->c.resv.size())
+    return fail(KE_ERR_INVALID, "ke_reservation_allocs_get arguments");
+  for (int32_t i = 0; i < n; i++)
+    out[i] = ctx->c.resv_alloc.empty() ? ke_reservation_alloc{} : ctx->c.resv_alloc[(size_t)i];
+  return KE_OK;
 }
 
 int32_t ke_reservations_generation(ke_ctx* ctx) { return ctx ? ctx->c.resv_gen : 0; }
@@ -458,6 +477,21 @@ int ke_node_numa_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_numa_zone* z
   NodeState& ns = ctx->c.nodes[node];
   ns.zones.assign(zones, zones + n);
   for (ke_numa_zone& z : ns.zones) normalize_zone(z);
+  bool bare = true;  // an NRT without the resource manager's allocation: the parked one comes back
+  for (const ke_numa_zone& z : ns.zones)
+    bare = bare && !z.has_allocated && !z.single_pods && !z.shared_pods && !z.cpuset_cpus;
+  if (bare)
+    for (ke_numa_zone& z : ns.zones)
+      for (const ke_numa_zone& k : ns.kept_zones)
+        if (k.id == z.id) {
+          z.has_allocated = k.has_allocated;
+          for (int r = 0; r < KE_NRES; r++) z.allocated[r] = k.allocated[r];
+          z.cpuset_cpus = k.cpuset_cpus;
+          z.single_pods = k.single_pods;
+          z.shared_pods = k.shared_pods;
+          z.numa_status = zone_status(z);
+        }
+  if (n > 0) ns.kept_zones.clear();
   ns.dirty = true;
   ctx->c.numa_enabled = true;
   return KE_OK;
@@ -472,6 +506,13 @@ int ke_node_cpus_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_cpu* cpus, i
   NodeState& ns = ctx->c.nodes[node];
   ns.cpus.assign(cpus, cpus + n);
   ns.cpu_max_ref = n > 0 ? max_ref_count : 1;
+  bool bare = true;  // a topology without allocatedCPUs: the parked NodeAllocation comes back by CPU id
+  for (const ke_cpu& c : ns.cpus) bare = bare && c.ref_count == 0;
+  if (bare)
+    for (ke_cpu& c : ns.cpus)
+      for (const ke_cpu& k : ns.kept_cpus)
+        if (k.cpu_id == c.cpu_id) c.ref_count = k.ref_count, c.exclusive = k.exclusive;
+  if (n > 0) ns.kept_cpus.clear();
   ns.dirty = true;
   if (n > 0) ctx->c.cpu_enabled = true;
   return KE_OK;
@@ -742,7 +783,9 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
       if (local >= 0 && local != pick[0])
         return undo_rsv(), fail(KE_ERR_DEVICE, "k_rsv_pick winner differs from the placement");
       if (local >= 0 && score) score[s0] = (int32_t)((int64_t)score[s0] + c.cfg.weight_reservation * (int64_t)pick[1]);
-      resv_finish(c, local, pods[s0], &assumed[(size_t)s0]);
+      resv_finish(c, local, pods[s0], &assumed[(size_t)s0], c.last_cpusets.size() >= 4 ? c.last_cpusets.data() : nullptr,
+                  c.last_numa_alloc.size() >= (size_t)(KE_MAX_NUMA * KE_NRES) ? c.last_numa_alloc.data() : nullptr,
+                  c.last_dev_alloc.empty() ? 0 : c.last_dev_alloc[0]);
     }
     if (n_pods == 0) break;
     tp = clk::now();
@@ -884,7 +927,7 @@ int ke_pod_release(ke_ctx* ctx, const ke_pod* pod, const ke_pod_allocation* allo
   }
   if (node >= 0 && c.nodes[(size_t)node].known)  // (also a deleted node: its caches keep the pod until released)
     host_release_node(c.cfg, c.ext_enabled, c.nodes[(size_t)node], *pod, *alloc, pod_hints(c, *pod));
-  if (node >= 0 && ridx >= 0) resv_forget(c, ridx, *pod);
+  if (node >= 0 && ridx >= 0) resv_forget(c, ridx, *pod, alloc);
   const bool assigned = alloc->node >= 0 && alloc->quota_assigned;
   if (pod->quota > 0 && (assigned || mode == KE_RELEASE_DELETE)) {
     if (c.dev) {

@@ -36,7 +36,7 @@ constexpr int64_t USED_DOMAIN = 1LL << 53;                 // threshold folding 
 int validate_config(const ke_config& cfg) {
   if (cfg.abi_version != KE_ABI_VERSION) return fail(KE_ERR_INVALID, "ke_config.abi_version mismatch");
   if (cfg.node_capacity <= 0 || cfg.node_capacity > MAX_SHARD_NODES)
-    return fail(KE_ERR_INVALID, "node_capacity out of range (1 .. 2^23-1 per shard)");
+    return fail(KE_ERR_INVALID, "node_capacity out of range (1 .. 2^22-1 per shard)");
   if (cfg.pod_batch < 1 || cfg.pod_batch > MAX_BATCH) return fail(KE_ERR_INVALID, "pod_batch out of range (1..64)");
   const ke_ext_args& x = cfg.ext;
   if (cfg.weight_reservation < 0) return fail(KE_ERR_INVALID, "negative Reservation weight");
@@ -381,9 +381,16 @@ void derive_ds_row(const NodeState& ns, int64_t* f, uint64_t* m) {
         m[ds_ht_word(t)] |= 1ull << ds_ht_bit(t, mi, k);
         f[DS_TBASE[t] + mi * DS_NK[t] + k] = d.total[k];
       }
-      if (d.has_used[k]) {
+      // calcFreeWithPreemptible (device_cache.go:327-336) with the unmatched reservations' owners' part
+      // (resv_plugin_restore) as preemptible: used = SubtractWithNonNegativeResult(used, preemptible[minor]) --
+      // the free it leaves is the filtered view's (an instance left with nothing free is free of nothing either way)
+      const uint64_t rbit = 1ull << (16 * t + mi);
+      const bool rv = (ns.rv_dev_minors & rbit) != 0;
+      if (d.has_used[k] || (rv && (ns.rv_dev_keys[k] & rbit))) {
         m[ds_hu_word(t)] |= 1ull << ds_hu_bit(t, mi, k);
-        f[DS_UBASE[t] + mi * DS_NK[t] + k] = d.used[k];
+        int64_t u = d.has_used[k] ? d.used[k] : 0;
+        if (rv) u = std::max<int64_t>(0, u - ns.rv_dev[t][mi][k]);
+        f[DS_UBASE[t] + mi * DS_NK[t] + k] = u;
       }
     }
   }
@@ -432,6 +439,25 @@ int ptable_intern(Context& c, int32_t n, const ke_gpu_partition* parts) {
   return (int)n_tab;
 }
 
+// the amounts a pod's Reserve puts on one of its instances (fillGPUTotalMem + the per-instance request)
+void ds_instance_amounts(const ke_device& d, const DevPod& dp, int64_t* alloc, bool* has) {
+  const int t = d.type;
+  for (int k = 0; k < KE_DKEYS; k++) alloc[k] = 0, has[k] = false;
+  if (t == KE_DEV_GPU) {
+    const int64_t tm = d.health && d.has_total[KE_DKEY_GPU_MEMORY] ? d.total[KE_DKEY_GPU_MEMORY] : 0;
+    if (dp.flags & PF_DS_H_CORE) has[0] = true, alloc[0] = dp.ds_req[0];
+    if (dp.flags & PF_DS_H_RATIO) {  // memoryRatioToBytes
+      has[2] = true, alloc[2] = dp.ds_req[2];
+      has[1] = true, alloc[1] = dp.ds_req[2] * tm / 100;
+    } else if (dp.flags & PF_DS_H_MEM) {  // memoryBytesToRatio
+      has[1] = true, alloc[1] = dp.ds_req[1];
+      has[2] = true, alloc[2] = (int64_t)((double)dp.ds_req[1] / (double)tm * 100.0);
+    }
+  } else {
+    has[0] = true, alloc[0] = dp.ds_req[2 + t];
+  }
+}
+
 void host_ds_reserve(const ke_config& cfg, NodeState& ns, const DevPod& dp, uint64_t mask, const int8_t* vf) {
   (void)cfg;
   for (ke_device& d : ns.devs) {
@@ -439,21 +465,9 @@ void host_ds_reserve(const ke_config& cfg, NodeState& ns, const DevPod& dp, uint
     const int t = d.type;
     if (vf && t > 0 && vf[(t - 1) * KE_MAX_MINORS + d.minor] >= 0)  // updateVFAllocations
       d.vf_allocated |= 1ull << vf[(t - 1) * KE_MAX_MINORS + d.minor];
-    int64_t alloc[KE_DKEYS] = {0, 0, 0};
-    bool has[KE_DKEYS] = {false, false, false};
-    if (t == KE_DEV_GPU) {
-      const int64_t tm = d.health && d.has_total[KE_DKEY_GPU_MEMORY] ? d.total[KE_DKEY_GPU_MEMORY] : 0;
-      if (dp.flags & PF_DS_H_CORE) has[0] = true, alloc[0] = dp.ds_req[0];
-      if (dp.flags & PF_DS_H_RATIO) {  // memoryRatioToBytes
-        has[2] = true, alloc[2] = dp.ds_req[2];
-        has[1] = true, alloc[1] = dp.ds_req[2] * tm / 100;
-      } else if (dp.flags & PF_DS_H_MEM) {  // memoryBytesToRatio
-        has[1] = true, alloc[1] = dp.ds_req[1];
-        has[2] = true, alloc[2] = (int64_t)((double)dp.ds_req[1] / (double)tm * 100.0);
-      }
-    } else {
-      has[0] = true, alloc[0] = dp.ds_req[2 + t];
-    }
+    int64_t alloc[KE_DKEYS];
+    bool has[KE_DKEYS];
+    ds_instance_amounts(d, dp, alloc, has);
     for (int k = 0; k < DS_NK[t]; k++)
       if (has[k]) {  // quotav1.Add
         d.used[k] = (d.has_used[k] ? d.used[k] : 0) + alloc[k];
@@ -584,13 +598,76 @@ static void resv_delta(const Context& c, int32_t node, const std::vector<char>* 
   }
 }
 
+// The NodeNUMAResource / DeviceShare restore states of the reservations holding allocations that a pod does not
+// match: mergedUnmatchedUsed (nodenumaresource/reservation.go:111-120, deviceshare/reservation.go:99-108) over the
+// node's unmatched reservations with allocated pods (transformer.go:195-199), each one's
+//   used = subtractAllocated(copy(allocatable), remained, true),  remained = allocatable - allocated
+// which per NUMA id / device instance and key is the owners' amount where the reserve pod holds that key (keys of
+// both lists kept, the ResourceList arithmetic of quotav1) -- the part the node allocation counts twice.
+static void resv_plugin_restore(const Context& c, int32_t node, const std::vector<char>* matched, NodeState& ns) {
+  std::memset(ns.rv_numa, 0, sizeof ns.rv_numa);
+  std::memset(ns.rv_dev, 0, sizeof ns.rv_dev);
+  ns.rv_numa_keys = 0;
+  ns.rv_numa_zones = 0;
+  ns.rv_dev_minors = 0;
+  for (int k = 0; k < KE_DKEYS; k++) ns.rv_dev_keys[k] = 0;
+  if (c.resv_alloc.empty()) return;
+  for (int32_t i : c.resv_by_node[(size_t)node]) {
+    const ke_reservation& r = c.resv[(size_t)i];
+    if (!resv_usable(r) || (matched && (*matched)[(size_t)i]) || r.allocated_pods == 0) continue;
+    const ke_reservation_alloc& a = c.resv_alloc[(size_t)i];
+    // NodeNUMAResource (RestoreReservation, reservation.go:196-209): only with the reserve pod's NUMA resources
+    bool any = false;
+    for (int j = 0; j < KE_MAX_NUMA * KE_NRES; j++) any = any || a.numa[j] != 0;
+    if (any)
+      for (int id = 0; id < KE_MAX_NUMA; id++) {
+        const bool in_a = a.numa[2 * id] != 0 || a.numa[2 * id + 1] != 0;
+        const bool in_b = a.owner_numa[2 * id] != 0 || a.owner_numa[2 * id + 1] != 0;
+        if (!in_a && !in_b) continue;
+        ns.rv_numa_zones |= (uint8_t)(1u << id);
+        for (int r = 0; r < KE_NRES; r++) {
+          const int j = 2 * id + r;
+          if (a.numa[j] == 0 && a.owner_numa[j] == 0) continue;
+          ns.rv_numa_keys |= 1u << j;
+          if (a.numa[j] != 0 && a.owner_numa[j] > 0) ns.rv_numa[j] += a.owner_numa[j];
+        }
+      }
+    // DeviceShare (RestoreReservation, deviceshare/reservation.go:157-172): the owners' usage on the reserve pod's
+    // instances (appendAllocatedByHints); an instance whose used is zero leaves the map (deviceResources.subtract)
+    for (int t = 0; t < KE_DEV_TYPES; t++)
+      for (int m = 0; m < KE_MAX_MINORS; m++) {
+        const uint64_t bit = 1ull << (16 * t + m);
+        if (!(a.device_minors & bit)) continue;
+        bool nz = false;
+        for (int k = 0; k < KE_DKEYS; k++) nz = nz || (a.device[t][m][k] != 0 && a.owner_device[t][m][k] > 0);
+        if (!nz) continue;
+        ns.rv_dev_minors |= bit;
+        for (int k = 0; k < KE_DKEYS; k++) {
+          if (a.device[t][m][k] == 0 && a.owner_device[t][m][k] == 0) continue;
+          ns.rv_dev_keys[k] |= bit;
+          if (a.device[t][m][k] != 0 && a.owner_device[t][m][k] > 0) ns.rv_dev[t][m][k] += a.owner_device[t][m][k];
+        }
+      }
+  }
+}
+
 void resv_node_restore(Context& c, int32_t node) {
   NodeState& ns = c.nodes[(size_t)node];
   resv_delta(c, node, nullptr, false, ns.rv_req, ns.rv_nz, &ns.rv_pods);
+  resv_plugin_restore(c, node, nullptr, ns);
   ns.dirty = true;
 }
 
-int load_reservations(Context& c, int32_t n, const ke_reservation* rs) {
+// KE_RSV_HOLDS_* of a holdings record
+uint8_t resv_holds_of(const ke_reservation_alloc& a) {
+  uint8_t h = 0;
+  for (int j = 0; j < KE_MAX_NUMA * KE_NRES; j++) h |= a.numa[j] != 0 ? KE_RSV_HOLDS_NUMA : 0;
+  for (int w = 0; w < 4; w++) h |= a.cpuset[w] ? KE_RSV_HOLDS_CPUSET : 0;
+  if (a.device_minors) h |= KE_RSV_HOLDS_DEVICES;
+  return h;
+}
+
+int load_reservations(Context& c, int32_t n, const ke_reservation* rs, const ke_reservation_alloc* allocs) {
   if (n < 0 || (n > 0 && !rs)) return fail(KE_ERR_INVALID, "reservations");
   for (int32_t i = 0; i < n; i++) {
     const ke_reservation& r = rs[i];
@@ -599,12 +676,31 @@ int load_reservations(Context& c, int32_t n, const ke_reservation* rs) {
     if (r.allocate_policy > KE_RSV_POLICY_RESTRICTED) return fail(KE_ERR_INVALID, "reservation allocate policy");
     for (int k = 0; k < KE_NRES; k++)
       if (r.allocatable[k] < 0 || r.allocated[k] < 0) return fail(KE_ERR_INVALID, "negative reservation quantity");
-    // what the restore of such a reservation needs is not carried by ke_reservation: refuse rather than
-    // schedule every pod on its node without the NUMA / cpuset / device restore (koord_eval.h)
-    if (r.holds & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET))
-      return fail(KE_ERR_UNSUPPORTED, "a reservation holding a NUMA allocation or a cpuset (nodenumaresource/reservation.go)");
-    if (r.holds & KE_RSV_HOLDS_DEVICES)
-      return fail(KE_ERR_UNSUPPORTED, "a reservation holding device instances (deviceshare/reservation.go)");
+    // the holdings come with the record (ke_reservations_load_ex); a holds bit without one has nothing to restore
+    // from: refused rather than scheduled around without the NUMA / cpuset / device restore (koord_eval.h)
+    const uint8_t held = allocs ? resv_holds_of(allocs[i]) : 0;
+    const uint8_t said = r.holds & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET | KE_RSV_HOLDS_DEVICES);
+    if (!allocs && said)
+      return fail(KE_ERR_UNSUPPORTED, "a reservation holding NUMA / cpuset / device allocations without its "
+                                      "ke_reservation_alloc (ke_reservations_load_ex)");
+    if (allocs && said != held) return fail(KE_ERR_INVALID, "ke_reservation.holds disagrees with its ke_reservation_alloc");
+    if (allocs) {
+      const ke_reservation_alloc& a = allocs[i];
+      for (int j = 0; j < KE_MAX_NUMA * KE_NRES; j++)
+        if (a.numa[j] < 0 || a.owner_numa[j] < 0) return fail(KE_ERR_INVALID, "negative reservation NUMA amount");
+      for (int t = 0; t < KE_DEV_TYPES; t++)
+        for (int m = 0; m < KE_MAX_MINORS; m++)
+          for (int k = 0; k < KE_DKEYS; k++) {
+            const int64_t v = a.device[t][m][k], o = a.owner_device[t][m][k];
+            if (v < 0 || o < 0) return fail(KE_ERR_INVALID, "negative reservation device amount");
+            if (k >= (t == KE_DEV_GPU ? 3 : 1) && (v || o)) return fail(KE_ERR_INVALID, "reservation device key of another type");
+            if (v && !(a.device_minors >> (16 * t + m) & 1)) return fail(KE_ERR_INVALID, "reservation device amount off its minors");
+            if (o && !(a.owner_device_minors >> (16 * t + m) & 1))
+              return fail(KE_ERR_INVALID, "reservation owner device amount off its minors");
+          }
+      if ((a.device_minors | a.owner_device_minors) & ~0x0000FFFFFFFFFFFFull)
+        return fail(KE_ERR_INVALID, "reservation device minors beyond the three types");
+    }
     if (r.holds & KE_RSV_OTHER_ALLOCATABLE)
       return fail(KE_ERR_UNSUPPORTED, "a reservation whose allocatable names resources other than cpu / memory");
     if (r.holds & ~15u) return fail(KE_ERR_INVALID, "unknown ke_reservation.holds bits");
@@ -612,6 +708,11 @@ int load_reservations(Context& c, int32_t n, const ke_reservation* rs) {
   std::vector<int32_t> old;
   for (const ke_reservation& r : c.resv) old.push_back(r.node);
   c.resv.assign(rs, rs + n);
+  if (allocs) c.resv_alloc.assign(allocs, allocs + n);
+  else c.resv_alloc.clear();
+  c.resv_cpu_cnt.clear();
+  c.resv_holds.assign((size_t)n, 0);
+  for (int32_t i = 0; allocs && i < n; i++) c.resv_holds[(size_t)i] = resv_holds_of(allocs[i]);
   c.resv_by_node.assign(c.nodes.size(), {});
   for (int32_t i = 0; i < n; i++) c.resv_by_node[(size_t)rs[i].node].push_back(i);
   for (int32_t node : old) resv_node_restore(c, node);  // the old restore leaves
@@ -627,12 +728,16 @@ int load_reservations(Context& c, int32_t n, const ke_reservation* rs) {
 // fitsReservation (plugin.go:499-569).  podRequested = Requested after the unmatched restore only,
 // allRAllocated = Σ allocated of the node's matched reservations.
 // With a reservation affinity the name check is skipped (the pod may use any matched reservation, :373).
+// The pod-count check of fitsNode (plugin.go:450-453) reads len(NodeInfo.Pods) of the snapshot NodeInfo, which
+// the BeforePreFilter restore already left without the matched reserve pods (restoreMatchedReservation ->
+// RemovePod, transformer.go:440), and subtracts len(matchedOrIgnored) once more: `pods_restored` is the former.
 static bool resv_nominable(const ke_reservation& r, const ke_pod& pod, const int64_t* alloc, const int64_t* pod_requested,
-                           const int64_t* all_allocated, bool affinity) {
+                           const int64_t* all_allocated, bool affinity, int64_t pods_restored, int64_t n_matched,
+                           int64_t allowed_pods) {
   bool shared = false;
   for (int k = 0; k < KE_NRES; k++) shared = shared || (r.allocatable[k] != 0 && pod.requests[k] != 0);
   if (!shared && !affinity) return false;
-  bool node_fits = true;
+  bool node_fits = pods_restored - n_matched + 1 <= allowed_pods;
   if (pod.requests[KE_RES_CPU] != 0 || pod.requests[KE_RES_MEMORY] != 0)
     for (int k = 0; k < KE_NRES; k++) {
       const int64_t remained = r.allocatable[k] > r.allocated[k] ? r.allocatable[k] - r.allocated[k] : 0;  // GetAvailable
@@ -665,8 +770,10 @@ int resv_check(const Context& c, const int32_t* ids, int32_t n_ids) {
   for (int32_t j = 0; j < n_ids; j++) {
     if (ids[j] < 0 || ids[j] >= (int32_t)c.resv.size()) return fail(KE_ERR_NOT_FOUND, "matched reservation index");
     const ke_reservation& r = c.resv[(size_t)ids[j]];
-    if (resv_usable(r) && c.nodes[(size_t)r.node].node.numa_topology_policy != KE_NUMA_POLICY_NONE)
-      return fail(KE_ERR_UNSUPPORTED, "a matched reservation on a node with a NUMA topology policy");
+    if (resv_usable(r) && c.nodes[(size_t)r.node].node.numa_topology_policy != KE_NUMA_POLICY_NONE &&
+        !c.resv_holds.empty() && (c.resv_holds[(size_t)ids[j]] & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)))
+      return fail(KE_ERR_UNSUPPORTED, "a matched reservation holding NUMA resources / a cpuset on a node with a NUMA "
+                                      "topology policy");
   }
   return KE_OK;
 }
@@ -700,9 +807,15 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
         const int64_t o = c.resv[(size_t)i].order;
         if (o != 0 && (order == 0 || o < order)) order = o;
       }
+    int64_t mreq[KE_NRES], mnz[KE_NRES];
+    int32_t mpods = 0;  // the snapshot's len(Pods) delta with this pod's matched reserve pods removed
+    resv_delta(c, node, &m, true, mreq, mnz, &mpods);
+    const int64_t pods_restored = (int64_t)ns.node.pod_count + mpods;
     std::vector<int32_t> ok;
     for (int32_t i : mine)
-      if (resv_nominable(c.resv[(size_t)i], pod, ns.node.allocatable, pod_requested, all_alloc, affinity)) ok.push_back(i);
+      if (resv_nominable(c.resv[(size_t)i], pod, ns.node.allocatable, pod_requested, all_alloc, affinity, pods_restored,
+                         (int64_t)mine.size(), ns.node.allowed_pods))
+        ok.push_back(i);
     // the Reservation Filter with a reservation affinity (plugin.go:316-318, 351-442): a node without matched
     // reservations fails, one with them passes when one of them fits (the same checks as the nomination's)
     const bool allowed = !affinity || !ok.empty();
@@ -734,14 +847,60 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
     }
     c.rsv_pairs.push_back({node, (int16_t)(nom >= 0 ? resv_score(c.resv[(size_t)nom], pod) : 0), (int16_t)allowed, order});
     c.rsv_nominated.push_back(nom);
-    // the rows this pod sees: its matched reservations restored too
+    // the rows this pod sees: its matched reservations restored too, and left out of the plugins' unmatched states
     resv_delta(c, node, &m, true, ns.rv_req, ns.rv_nz, &ns.rv_pods);
+    resv_plugin_restore(c, node, &m, ns);
     ns.dirty = true;
   }
   return KE_OK;
 }
 
-void resv_finish(Context& c, int32_t chosen_local, const ke_pod& pod, int32_t* assumed) {
+// An owner pod's allocations enter (sign +1) or leave (-1) its reservation's owner part: the resource manager /
+// device cache entries RestoreReservation reads by the reservation's AssignedPods (reservation.go:201-226,
+// deviceshare/reservation.go:165-170).  CPUs are counted per owner (the owners' union is what the record shows).
+void resv_owner_update(Context& c, int32_t idx, const ke_pod& pod, const uint64_t* cpuset, const int64_t* numa,
+                       uint64_t dev_minors, int sign) {
+  if (c.resv_alloc.empty() || idx < 0 || idx >= (int32_t)c.resv_alloc.size()) return;
+  ke_reservation_alloc& a = c.resv_alloc[(size_t)idx];
+  if (c.resv_cpu_cnt.size() != c.resv_alloc.size()) c.resv_cpu_cnt.assign(c.resv_alloc.size(), {});
+  std::vector<uint8_t>& cnt = c.resv_cpu_cnt[(size_t)idx];
+  if (cnt.empty()) {
+    cnt.assign(KE_MAX_CPUS, 0);
+    for (int cpu = 0; cpu < KE_MAX_CPUS; cpu++) cnt[(size_t)cpu] = a.owner_cpuset[cpu >> 6] >> (cpu & 63) & 1;
+  }
+  for (int cpu = 0; cpuset && cpu < KE_MAX_CPUS; cpu++)
+    if (cpuset[cpu >> 6] >> (cpu & 63) & 1) {
+      uint8_t& k = cnt[(size_t)cpu];
+      k = (uint8_t)(sign > 0 ? std::min(255, k + 1) : std::max(0, k - 1));
+      if (k) a.owner_cpuset[cpu >> 6] |= 1ull << (cpu & 63);
+      else a.owner_cpuset[cpu >> 6] &= ~(1ull << (cpu & 63));
+    }
+  for (int j = 0; numa && j < KE_MAX_NUMA * KE_NRES; j++)
+    a.owner_numa[j] = std::max<int64_t>(0, a.owner_numa[j] + sign * numa[j]);
+  if (dev_minors) {
+    const NodeState& ns = c.nodes[(size_t)c.resv[(size_t)idx].node];
+    const DevPod dp = make_dev_pod(c.cfg, pod, pod_hints(c, pod), &c.tmpl);
+    for (const ke_device& d : ns.devs) {
+      const uint64_t bit = 1ull << (16 * d.type + d.minor);
+      if (!(dev_minors & bit)) continue;
+      int64_t amt[KE_DKEYS];
+      bool has[KE_DKEYS];
+      ds_instance_amounts(d, dp, amt, has);
+      bool any = false;
+      for (int k = 0; k < KE_DKEYS; k++) {
+        int64_t& o = a.owner_device[d.type][d.minor][k];
+        if (has[k]) o = std::max<int64_t>(0, o + sign * amt[k]);
+        any = any || o != 0;
+      }
+      if (any) a.owner_device_minors |= bit;
+      else a.owner_device_minors &= ~bit;
+    }
+  }
+  c.resv_holds[(size_t)idx] = resv_holds_of(a);
+}
+
+void resv_finish(Context& c, int32_t chosen_local, const ke_pod& pod, int32_t* assumed, const uint64_t* cpuset,
+                 const int64_t* numa, uint64_t dev_minors) {
   *assumed = 0;
   for (size_t j = 0; j < c.rsv_nodes.size(); j++)
     if (c.rsv_nodes[j] == chosen_local && c.rsv_nominated[j] >= 0) {
@@ -751,6 +910,7 @@ void resv_finish(Context& c, int32_t chosen_local, const ke_pod& pod, int32_t* a
         if (r.allocatable[k] != 0) r.allocated[k] += pod.requests[k];
       r.allocated_pods++;
       *assumed = 1 + c.rsv_nominated[j];
+      resv_owner_update(c, c.rsv_nominated[j], pod, cpuset, numa, dev_minors, +1);
     }
   for (int32_t node : c.rsv_nodes) resv_node_restore(c, node);
   c.rsv_affinity = false;
@@ -760,12 +920,13 @@ void resv_finish(Context& c, int32_t chosen_local, const ke_pod& pod, int32_t* a
 }
 
 // forgetPod -> RemoveAssignedPod (reservation_info.go:470-482)
-void resv_forget(Context& c, int32_t idx, const ke_pod& pod) {
+void resv_forget(Context& c, int32_t idx, const ke_pod& pod, const ke_pod_allocation* a) {
   if (idx < 0 || idx >= (int32_t)c.resv.size()) return;
   ke_reservation& r = c.resv[(size_t)idx];
   for (int k = 0; k < KE_NRES; k++)
     if (r.allocatable[k] != 0) r.allocated[k] = std::max<int64_t>(0, r.allocated[k] - pod.requests[k]);
   if (r.allocated_pods > 0) r.allocated_pods--;
+  if (a) resv_owner_update(c, idx, pod, a->cpuset, a->numa, a->device_minors, -1);
   resv_node_restore(c, r.node);
 }
 
@@ -1344,6 +1505,17 @@ void derive_numa_row(const NodeState& ns, int64_t* f, uint64_t* mask) {
         f[NUMA_AL + 2 * id] = f[NUMA_AL + 2 * id] - cs + amplify(cs, ratio);
         *mask |= 1ull << (NUMA_M_AL + id);
       }
+      // allocatedRes = SubtractWithNonNegativeResult(allocatedRes, reusableResources[id]) (node_allocation.go:237):
+      // the unmatched reservations' owners' part (resv_plugin_restore); keys of both lists
+      if (ns.rv_numa_zones >> id & 1)
+        for (int r = 0; r < KE_NRES; r++) {
+          const bool key = ns.rv_numa_keys >> (2 * id + r) & 1;
+          const bool had = *mask >> (NUMA_M_AL + 8 * r + id) & 1;
+          if (!key && !had) continue;
+          const int64_t v = (had ? f[NUMA_AL + 2 * id + r] : 0) - ns.rv_numa[2 * id + r];
+          f[NUMA_AL + 2 * id + r] = v > 0 ? v : 0;
+          *mask |= 1ull << (NUMA_M_AL + 8 * r + id);
+        }
     }
   }
 }
@@ -1486,15 +1658,19 @@ void host_release_node(const ke_config& cfg, bool ext, NodeState& ns, const ke_p
       for (ke_node_resource& r : ns.xres)
         if (r.id == pod.xres_id[e]) r.requested -= pod.xres_value[e];
   // NodeNUMAResource resourceManager.Release -> NodeAllocation.release (node_allocation.go:158-190); only a
-  // node with a valid CPU topology recorded the allocation (Update, resource_manager.go:461-466)
-  if (cpus_valid(ns)) {
+  // node with a valid CPU topology recorded the allocation (Update, resource_manager.go:461-466).  While the
+  // NRT is deleted the NodeAllocation lives on in the parked tables (ke_node_topology_delete).
+  const bool parked = ns.cpus.empty() && !ns.kept_cpus.empty();
+  if (cpus_valid(ns) || parked) {
+    std::vector<ke_cpu>& cpus = parked ? ns.kept_cpus : ns.cpus;
+    std::vector<ke_numa_zone>& zones = parked ? ns.kept_zones : ns.zones;
     std::vector<int> ids;
-    for (ke_cpu& c : ns.cpus) {
+    for (ke_cpu& c : cpus) {
       if (!(a.cpuset[c.cpu_id >> 6] >> (c.cpu_id & 63) & 1) || c.ref_count <= 0) continue;
       if (--c.ref_count == 0) c.exclusive = KE_CPU_EXCL_NONE;  // the CPU leaves allocatedCPUs
       if (std::find(ids.begin(), ids.end(), c.numa_id) == ids.end()) ids.push_back(c.numa_id);
     }
-    for (ke_numa_zone& z : ns.zones) {
+    for (ke_numa_zone& z : zones) {
       if (std::find(ids.begin(), ids.end(), z.id) != ids.end()) {  // delete(sharedNode / singleNUMANode[id], uid)
         int16_t& k = ids.size() > 1 ? z.shared_pods : z.single_pods;
         if (k > 0) k--;

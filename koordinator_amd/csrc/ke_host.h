@@ -76,6 +76,12 @@ struct NodeState {
   // NodeAllocation.allocatedCPUs); empty = no CPU topology
   std::vector<ke_cpu> cpus;
   int32_t cpu_max_ref = 1;
+  // The resource manager's NodeAllocation outlives the NRT (topologyManager.Delete drops only the
+  // TopologyOptions, topology_options.go:84-88): ke_node_topology_delete parks the CPU records and zones here
+  // (releases keep applying to them) and the next ke_node_cpus_set / ke_node_numa_set that carries no
+  // allocation of its own takes the parked ref counts / zone allocations back by CPU / NUMA id.
+  std::vector<ke_cpu> kept_cpus;
+  std::vector<ke_numa_zone> kept_zones;
   // DeviceShare node device cache entry (device_cache.go:518-568)
   bool has_dev_cache = false;
   std::vector<ke_device> devs;
@@ -93,6 +99,16 @@ struct NodeState {
   // Requested / NonZeroRequested (MilliCPU, Memory) when the rows are derived (load_reservations)
   int64_t rv_req[KE_NRES] = {0, 0}, rv_nz[KE_NRES] = {0, 0};
   int32_t rv_pods = 0;  // len(NodeInfo.Pods) delta of the restore (matched reserve pods removed)
+  // ... and the plugins' restore states of the reservations holding NUMA / cpuset / device allocations
+  // (ke_reservations_load_ex): NodeNUMAResource's reusableResources per zone (mergedUnmatchedUsed; key bits
+  // 2*id + r of the ResourceList keys present) and DeviceShare's preemptible per instance
+  // (mergedUnmatchedUsed[type][minor]; bit 16*type + minor present), folded into the NUMA / device rows
+  int64_t rv_numa[KE_MAX_NUMA * KE_NRES] = {};
+  uint32_t rv_numa_keys = 0;
+  uint8_t rv_numa_zones = 0;  // NUMA ids with a reusable entry
+  int64_t rv_dev[KE_DEV_TYPES][KE_MAX_MINORS][KE_DKEYS] = {};
+  uint64_t rv_dev_keys[KE_DKEYS] = {0, 0, 0};  // bit 16*type + minor per key present
+  uint64_t rv_dev_minors = 0;
   // derived
   DirtyFlag dirty;              // row must be re-derived and uploaded
   int64_t valid_until = INT64_MAX;  // derived row is exact for now < valid_until
@@ -170,6 +186,9 @@ struct Context {
   std::vector<ke_pod_device_hints> hints;
   std::vector<ke_gpu_template> tmpl;
   std::vector<ke_reservation> resv;  // ke_reservations_load (allocated / allocated_pods kept by Reserve)
+  std::vector<ke_reservation_alloc> resv_alloc;  // their NUMA / cpuset / device holdings (owner parts kept by Reserve)
+  std::vector<uint8_t> resv_holds;   // derived from resv_alloc: KE_RSV_HOLDS_* bits
+  std::vector<std::vector<uint8_t>> resv_cpu_cnt;  // per reservation: owners per CPU id (lazily from owner_cpuset)
   std::vector<std::vector<int32_t>> resv_by_node;  // reservation indices per node
   // ke_pod_reservations staging for the next ke_schedule: CSR over its pods
   std::vector<int32_t> match_off, match_ids;
@@ -271,7 +290,7 @@ int validate_node_resources(int32_t n, const ke_node_resource* r);
 int ext_slots(const ke_config& cfg, int32_t* ids);
 // the ext SoA row of a node: NUM_XF int64 + the uint64 mask of resource ids with Allocatable > 0
 void derive_ext_row(const ke_config& cfg, const NodeState& ns, int64_t* f, uint64_t* mask);
-int load_reservations(Context& c, int32_t n, const ke_reservation* r);
+int load_reservations(Context& c, int32_t n, const ke_reservation* r, const ke_reservation_alloc* allocs = nullptr);
 bool resv_usable(const ke_reservation& r);
 void resv_node_restore(Context& c, int32_t node);  // the restore every non-matching pod sees
 int32_t resv_score(const ke_reservation& r, const ke_pod& pod);
@@ -280,8 +299,11 @@ int32_t resv_score(const ke_reservation& r, const ke_pod& pod);
 int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids, bool affinity);
 // the refusals of resv_prepare, checked for every pod before a ke_schedule call schedules any
 int resv_check(const Context& c, const int32_t* ids, int32_t n_ids);
-void resv_finish(Context& c, int32_t chosen_local, const ke_pod& pod, int32_t* assumed);
-void resv_forget(Context& c, int32_t idx, const ke_pod& pod);
+void resv_finish(Context& c, int32_t chosen_local, const ke_pod& pod, int32_t* assumed, const uint64_t* cpuset = nullptr,
+                 const int64_t* numa = nullptr, uint64_t dev_minors = 0);
+void resv_forget(Context& c, int32_t idx, const ke_pod& pod, const ke_pod_allocation* a = nullptr);
+uint8_t resv_holds_of(const ke_reservation_alloc& a);
+void ds_instance_amounts(const ke_device& d, const DevPod& dp, int64_t* alloc, bool* has);
 // NodeResourcesFitPlus' (NonZero)Requested of resource `id` on the node, with the reservation restore
 int64_t xres_requested(const NodeState& ns, const ke_node_resource& r);
 void host_ext_reserve(NodeState& ns, const ke_pod& pod);

@@ -85,6 +85,7 @@ struct SoA {
 constexpr int DSB_MAX = 0, DSB_CNT = 64, DSB_CUT = 128, DSB_WORDS = 129;
 // kerr bits: an input the kernels refuse mid-call (the call returns KE_ERR_UNSUPPORTED)
 constexpr int32_t KERR_HINT_ROUTE = 2;  // a hinted pod reached a kernel instantiated without the hint path (H)
+constexpr int32_t KERR_LDS_WAIT = 4;    // a bounded intra-workgroup LDS wait of the replay expired (internal)
 
 // ---------------------------------------------------------------------------------------------
 // ElasticQuota PreFilter / Reserve (elasticquota/plugin.go:223-275,345-359; plugin_helper.go:281-301;
@@ -4365,6 +4366,15 @@ constexpr uint64_t T_HELP_WAIT_TICKS = 2000;  // wave 0's wait for the helpers' 
 // The T-row helpers of a stale-list run (k_resolve_run workgroups 1..H): batch b's T maxima
 // (every pod against the previous batch's changed nodes) evaluated on other CUs while the Reserve workgroup
 // predicts, instead of on its own waves.  Global hand-off words, double-buffered by batch parity.
+// Co-residency: nothing waits for a helper.  The Reserve workgroup (workgroup 0) waits for tready[b] at most
+// T_HELP_WAIT_TICKS and then evaluates the missing T maxima itself, so a helper that is not resident (the grid is
+// 1 + H workgroups of one CU each; other launches may hold the CUs) only costs that wait; a helper waits only for
+// done[b-1], which workgroup 0 publishes whether or not any helper ran (bounded by HANDOFF_TIMEOUT_TICKS and the
+// error word).  Within a workgroup every wait on LDS (the progressive S polling xnode) is on wave 0's prediction
+// loop, which writes every xnode of its window before any barrier.  An unbounded LDS wait on a wave that may sit
+// at a barrier is the one wait shape the bounded global hand-offs do not cover -- the most likely cause of the
+// round-4 hang under per-chunk row claiming (reverted before commit) -- so the xnode poll is
+// bounded too (KERR_LDS_WAIT fails the call).
 struct THelp {
   int32_t* tlist;   // [2][1 + MAX_BATCH]: a batch's changed nodes (count first; the Reserve workgroup writes them)
   uint32_t* tmx;    // [2][MAX_BATCH]: the T maxima of a batch's pods (the helpers write them)
@@ -4735,8 +4745,18 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
       adopt_t();
       for (int lo = start; lo < end; lo += PCH) {
         const int hi = min(end, lo + PCH);
-        if (lane == 0)
-          while (((volatile int32_t*)L.sp.xnode)[hi - 1] == XN_PENDING) __builtin_amdgcn_s_sleep(1);
+        if (lane == 0) {  // an LDS wait on wave 0 of the same workgroup (co-resident by construction), bounded
+                          // all the same: wave 0 never reaches a barrier before every xnode of [start, end) is
+                          // written, and a wait past 2 s fails the call (KERR_LDS_WAIT) instead of hanging it
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          while (((volatile int32_t*)L.sp.xnode)[hi - 1] == XN_PENDING) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > HANDOFF_TIMEOUT_TICKS) {
+              __hip_atomic_fetch_or(s.kerr, KERR_LDS_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
         reserve_lanes(lo, hi, true);
         const int r0 = lo == start ? start : lo + 1, r1 = min(hi + 1, end);  // rows [r0, r1)
         for (int j = r0 + wave - 1; j < r1; j += 2 * (NW - 1)) s_rows(j, j + NW - 1 < r1 ? j + NW - 1 : -1);
@@ -5998,6 +6018,9 @@ struct DeviceState {
   hipEvent_t ev_start = nullptr;
   bool pipeline = true;             // ke_set_pipeline
   bool pipe_fixup = false;          // ke_set_pipeline(2): exact lists from k_fixup for every run (else quota runs only)
+  // dynamic LDS of the eval streams' LDS-free kernels: more than what a Reserve workgroup (ResLds) leaves free of
+  // the CU's LDS, from the device's per-CU LDS at device_create (EXCL_LDS at the 160 KB of gfx950)
+  unsigned excl_lds = EXCL_LDS;
   bool eval_patch = true;           // two eval streams: evals wait for batch b-3, k_patch adds b-2 (KOORDEVAL_EVAL_PATCH)
   int t_helpers = 4;                // T-row helper workgroups of a stale-list run (THelp; KOORDEVAL_T_HELPERS)
   int t_help_ignore = 0;            // test hook (KOORDEVAL_T_HELPERS_IGNORE): the replay's own T rows every batch
@@ -6036,6 +6059,11 @@ int device_create(Context* ctx) {
   ctx->dev = d;
   d->device = ctx->cfg.device_ordinal;
   HIP_OK(hipSetDevice(d->device));
+  int cu_lds = 0;  // the Reserve kernels' ResLds fills a CU_LDS_BYTES CU; the exclusion of co-resident eval waves
+  HIP_OK(hipDeviceGetAttribute(&cu_lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, d->device));
+  if (cu_lds < (int)sizeof(ResLds))
+    return fail(KE_ERR_UNSUPPORTED, "device LDS per CU below the Reserve kernels' ResLds (built for gfx950's 160 KB)");
+  d->excl_lds = std::max<unsigned>(EXCL_LDS, (unsigned)(cu_lds - (int)sizeof(ResLds)) + 1024u);
   int prio_lo = 0, prio_hi = 0;  // the Reserve chain gets the higher queue priority
   HIP_OK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
   if (const char* e = std::getenv("KOORDEVAL_T_HELPERS")) d->t_helpers = std::max(0, std::min(8, std::atoi(e)));
@@ -6832,7 +6860,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     // spinning on the flag would hold the CUs the other stream's select needs)
     const bool plain_rec = !cpu && !ds && !numa && use_record_eval(bp);
     const bool wait_kernel = dwait && (!plain_rec || alt || (d->estream2 != nullptr && !sharded) || hi <= lo);
-    if (wait_kernel) hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), EXCL_LDS, es, nullptr, 0, dwait, d_err, nullptr);
+    if (wait_kernel) hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), d->excl_lds, es, nullptr, 0, dwait, d_err, nullptr);
     if (prof) HIP_OK(hipEventRecord(pe[0], es));
     const int L = pipe ? KSTALE : KMAX, kext = pipe ? KMAX : 0;
     uint32_t* lists = pipe ? d->d_stale + (size_t)(b & 1) * MAX_BATCH * KSTALE : d->d_cand;
@@ -6877,8 +6905,8 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       }
       if (prof) HIP_OK(hipEventRecord(pe[1], es));
       if (pwait) {  // the nodes batch b-2 changed, once it is done (k_patch)
-        hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), EXCL_LDS, es, nullptr, 0, pwait, d_err, nullptr);
-        hipLaunchKernelGGL(((k.flags & AF_EXT) ? k_patch<true> : k_patch<false>), dim3((unsigned)bp), dim3(64), EXCL_LDS, es,
+        hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), d->excl_lds, es, nullptr, 0, pwait, d_err, nullptr);
+        hipLaunchKernelGGL(((k.flags & AF_EXT) ? k_patch<true> : k_patch<false>), dim3((unsigned)bp), dim3(64), d->excl_lds, es,
                            d->soa, d->d_pods, bbase, k, ptl, scores, d->capacity);
       }
       if (ds && sharded && !d->loopback)  // DefaultNormalizeScore's max over the feasible nodes of all ranks
@@ -6983,7 +7011,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
                            alt, patch ? d_done + (q - 2) : nullptr, d_tlist + ((q - 2) & 1) * (1 + MAX_BATCH));
           if (rc) return rc;
           if (!published)
-            hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), EXCL_LDS, es, d_ready + q, (int32_t)batches[q].pods, nullptr,
+            hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), d->excl_lds, es, d_ready + q, (int32_t)batches[q].pods, nullptr,
                                d_err, nullptr);
           continue;
         }
@@ -7145,11 +7173,12 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     for (auto& e : ev) (void)hipEventDestroy(e);
     return fail(KE_ERR_DEVICE, "pipelined schedule: a device-side hand-off timed out (placements invalid)");
   }
-  if (kerr & KERR_HINT_ROUTE) {  // an internal routing error: the placements are not the reference's
+  if (kerr & (KERR_HINT_ROUTE | KERR_LDS_WAIT)) {  // internal errors: the placements are not the reference's
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     for (auto& e : ev) (void)hipEventDestroy(e);
-    return fail(KE_ERR_DEVICE, "internal: a hinted pod reached a kernel without the hint path");
+    return fail(KE_ERR_DEVICE, (kerr & KERR_LDS_WAIT) ? "internal: a replay LDS wait expired (placements invalid)"
+                                                      : "internal: a hinted pod reached a kernel without the hint path");
   }
   float ms = 0;
   HIP_OK(hipEventElapsedTime(&ms, e0, e1));

@@ -141,11 +141,23 @@ class Evaluator:
         t = abi.struct_array(templates, abi.GpuTemplate)
         self._check(self.lib.ke_gpu_templates_load(self.h, len(t), abi.ptr(t)))
 
-    def reservations_load(self, reservations):
-        """ke_reservations_load: the reservation cache (RESERVATION_DTYPE array)."""
+    def reservations_load(self, reservations, allocs=None):
+        """ke_reservations_load(_ex): the reservation cache (RESERVATION_DTYPE array) and, optionally, each one's
+        NUMA / cpuset / device holdings (RESERVATION_ALLOC_DTYPE array, one per reservation)."""
         r = abi.struct_array(reservations, abi.Reservation)
-        self._check(self.lib.ke_reservations_load(self.h, len(r), abi.ptr(r)))
+        if allocs is None:
+            self._check(self.lib.ke_reservations_load(self.h, len(r), abi.ptr(r)))
+        else:
+            a = abi.struct_array(allocs, abi.ReservationAlloc)
+            assert len(a) == len(r)
+            self._check(self.lib.ke_reservations_load_ex(self.h, len(r), abi.ptr(r), abi.ptr(a)))
         self._n_resv = len(r)
+
+    def reservation_allocs_get(self):
+        """ke_reservation_allocs_get: the holdings with the owner parts as Reserve / release left them."""
+        out = np.zeros(getattr(self, "_n_resv", 0), abi.RESERVATION_ALLOC_DTYPE)
+        self._check(self.lib.ke_reservation_allocs_get(self.h, len(out), abi.ptr(out)))
+        return out
 
     def reservations_get(self):
         """ke_reservations_get: the reservation cache as Reserve / Unreserve left it."""

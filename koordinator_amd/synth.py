@@ -855,3 +855,120 @@ def add_pod_xres(pods, seed, gpu_fraction=0.2, storage_fraction=0.5, scarce_frac
         pods["xres_id"][p, :len(ids)] = ids
         pods["xres_value"][p, :len(ids)] = vals
     return pods
+
+
+# ---- reservations whose reserve pods hold NUMA resources, cpusets and devices ------------------------------------
+def make_reservation_holdings(cl, seed, zones=None, tabs=None, devices=None, frac=0.3, owner_fraction=0.6,
+                              policies=(0, 1, 2)):
+    """Reservations on a `frac` of the nodes whose reserve pods hold, where the node has them, a NUMA allocation on
+    one or two zones, a cpuset out of the zones' free CPUs and a share of one GPU / RDMA instance, with owner pods
+    (allocated_pods > 0 for `owner_fraction` of them) holding part of each.  Both are added to the node state the way
+    the resource manager and the device cache count them (zone allocation, CPU ref counts, device used, NodeInfo
+    Requested / pod count).  Mutates cl.nodes, zones, tabs and devices; returns (RESERVATION_DTYPE array,
+    RESERVATION_ALLOC_DTYPE array)."""
+    rng = np.random.default_rng(seed)
+    rs, al = [], []
+    for i in range(cl.n_nodes):
+        if rng.random() >= frac:
+            continue
+        for _ in range(int(rng.integers(1, 3))):
+            r = np.zeros((), abi.RESERVATION_DTYPE)
+            a = np.zeros((), abi.RESERVATION_ALLOC_DTYPE)
+            r["node"], r["available"] = i, int(rng.random() < 0.95)
+            r["allocate_policy"] = int(rng.choice(policies))
+            r["order"] = int(rng.choice([0, 0, 0, 5, 9]))
+            owners = rng.random() < owner_fraction
+            r["allocated_pods"] = int(rng.integers(1, 3)) if owners else 0
+            holds = 0
+            cpu_total = mem_total = cpu_owned = mem_owned = 0
+            z = zones[i] if zones is not None else None
+            t = tabs[i][0] if tabs is not None and tabs[i] is not None else None
+            if z is not None and len(z):
+                picked = rng.choice(len(z), int(min(len(z), rng.integers(1, 3))), replace=False)
+                for zi in picked:
+                    zid = int(z["id"][zi])
+                    ko = 0
+                    if t is not None and rng.random() < 0.6:  # a cpuset on this zone
+                        free = np.flatnonzero((t["numa_id"] == zid) & (t["ref_count"] == 0) & (t["reserved"] == 0))
+                        k = int(min(len(free), rng.choice([2, 4, 6])))
+                        if k == 0:
+                            continue
+                        cpus = t["cpu_id"][free[:k]]
+                        t["ref_count"][free[:k]] += 1
+                        for c in cpus:
+                            a["cpuset"][c >> 6] |= np.uint64(1) << np.uint64(c & 63)
+                        cpu = k * 1000
+                        if z["single_pods"][zi] == 0 and z["shared_pods"][zi] == 0:  # a status without counts: one pod
+                            z["single_pods"][zi] = int(z["numa_status"][zi] == abi.NUMA_STATUS_SINGLE)
+                            z["shared_pods"][zi] = int(z["numa_status"][zi] == abi.NUMA_STATUS_SHARED)
+                        z["single_pods"][zi] += 1
+                        z["numa_status"][zi] = abi.NUMA_STATUS_SHARED if z["shared_pods"][zi] else abi.NUMA_STATUS_SINGLE
+                        if owners:
+                            ko = int(rng.integers(1, k + 1))
+                            t["ref_count"][free[:ko]] += 1
+                            for c in cpus[:ko]:
+                                a["owner_cpuset"][c >> 6] |= np.uint64(1) << np.uint64(c & 63)
+                            a["owner_numa"][2 * zid] += ko * 1000
+                            z["allocated"][zi, 0] += ko * 1000
+                            cpu_owned += ko * 1000
+                            z["single_pods"][zi] += 1
+                    else:
+                        cpu = int(rng.choice([1000, 2000, 2500, 4000]))
+                    mem = int(rng.choice([1, 2, 4])) * GI
+                    a["numa"][2 * zid] += cpu
+                    a["numa"][2 * zid + 1] += mem
+                    cpu_total += cpu
+                    mem_total += mem
+                    z["has_allocated"][zi] = abi.NUMA_ALLOC_ENTRY | abi.NUMA_ALLOC_CPU | abi.NUMA_ALLOC_MEMORY
+                    z["allocated"][zi, 0] += cpu
+                    z["allocated"][zi, 1] += mem
+                    if owners:
+                        oc = 0 if ko else cpu // 2 // 1000 * 1000  # (a cpuset zone's owners hold CPUs above)
+                        om = mem // 2
+                        a["owner_numa"][2 * zid] += oc
+                        a["owner_numa"][2 * zid + 1] += om
+                        z["allocated"][zi, 0] += oc
+                        z["allocated"][zi, 1] += om
+                        cpu_owned += oc
+                        mem_owned += om
+                if a["numa"].any():
+                    holds |= abi.RSV_HOLDS_NUMA
+                if a["cpuset"].any():
+                    holds |= abi.RSV_HOLDS_CPUSET
+            d = devices[i] if devices is not None else None
+            if d is not None and len(d) and rng.random() < 0.7:
+                cand = [j for j in range(len(d)) if d["health"][j] and
+                        (d["used"][j, 0] if d["has_used"][j, 0] else 0) <= d["total"][j, 0] - 50]
+                if cand:
+                    j = int(rng.choice(cand))
+                    ty, mi = int(d["type"][j]), int(d["minor"][j])
+                    nk = 3 if ty == abi.DEV_GPU else 1
+                    share = 50
+                    amt = [share, int(d["total"][j, 1]) * share // 100, share][:nk] if ty == abi.DEV_GPU else [share]
+                    a["device_minors"] |= np.uint64(1) << np.uint64(16 * ty + mi)
+                    for k in range(nk):
+                        a["device"][ty, mi, k] = amt[k]
+                        d["used"][j, k] = (d["used"][j, k] if d["has_used"][j, k] else 0) + amt[k]
+                        d["has_used"][j, k] = 1
+                    if owners:
+                        a["owner_device_minors"] |= np.uint64(1) << np.uint64(16 * ty + mi)
+                        for k in range(nk):
+                            o = amt[k] // 2
+                            a["owner_device"][ty, mi, k] = o
+                            d["used"][j, k] += o
+                    holds |= abi.RSV_HOLDS_DEVICES
+            if holds == 0 and rng.random() < 0.5:
+                continue
+            cpu_total = cpu_total or int(rng.choice([2000, 4000]))
+            mem_total = mem_total or int(rng.choice([2, 4])) * GI
+            r["holds"] = holds
+            r["allocatable"][:] = [cpu_total, mem_total]
+            if owners:
+                r["allocated"][:] = [max(cpu_owned, 1000), max(mem_owned, GI)]
+            # the reserve pod and its owners are pods of the node (NodeInfo.Requested / Pods)
+            cl.nodes["requested"][i, 0] += cpu_total + (r["allocated"][0] if owners else 0)
+            cl.nodes["requested"][i, 1] += mem_total + (r["allocated"][1] if owners else 0)
+            cl.nodes["pod_count"][i] += 1 + int(r["allocated_pods"])
+            rs.append(r)
+            al.append(a)
+    return np.array(rs, abi.RESERVATION_DTYPE), np.array(al, abi.RESERVATION_ALLOC_DTYPE)

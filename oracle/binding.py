@@ -12,6 +12,16 @@ import numpy as np
 from koordinator_amd import abi
 from koordinator_amd.evaluator import as_pod_array
 
+# or_rsv_state (oracle.h): RestoreReservation's matched state of one reservation
+RSV_STATE_DTYPE = np.dtype([
+    ("allocatable_cpus", np.uint64, (4,)), ("allocated_cpus", np.uint64, (4,)), ("remained_cpus", np.uint64, (4,)),
+    ("numa_in", np.int32), ("pad", np.int32),
+    ("numa_allocatable", np.int64, (16,)), ("numa_allocated", np.int64, (16,)), ("numa_remained", np.int64, (16,)),
+    ("numa_remained_has", np.uint8, (16,)),
+    ("dev_allocatable_minors", np.uint64), ("dev_allocated_minors", np.uint64), ("dev_remained_minors", np.uint64),
+    ("dev_allocatable", np.int64, (3, 16, 3)), ("dev_allocated", np.int64, (3, 16, 3)),
+    ("dev_remained", np.int64, (3, 16, 3))], align=True)
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle.so")
 
@@ -58,6 +68,9 @@ def load():
         "or_gpu_templates_load": (C.c_int, [V, i32, V]),
         "or_reservations_load": (C.c_int, [V, i32, V]),
         "or_reservations_get": (C.c_int, [V, i32, V]),
+        "or_reservations_load_ex": (C.c_int, [V, i32, V, V]),
+        "or_restore_state": (C.c_int, [V, i32, V]),
+        "or_reservation_allocs_get": (C.c_int, [V, i32, V]),
         "or_pod_reservations": (C.c_int, [V, i32, V, V]),
         "or_last_reservations": (C.c_int, [V, i32, V]),
         "or_reservation_score": (C.c_int64, [V, V]),
@@ -272,12 +285,28 @@ class Oracle:
         t = abi.struct_array(templates, abi.GpuTemplate)
         assert self.lib.or_gpu_templates_load(self.h, len(t), abi.ptr(t)) == 0
 
-    def reservations_load(self, reservations):
+    def reservations_load(self, reservations, allocs=None):
         r = abi.struct_array(reservations, abi.Reservation)
-        rc = self.lib.or_reservations_load(self.h, len(r), abi.ptr(r))
+        if allocs is None:
+            rc = self.lib.or_reservations_load(self.h, len(r), abi.ptr(r))
+        else:
+            a = abi.struct_array(allocs, abi.ReservationAlloc)
+            assert len(a) == len(r)
+            rc = self.lib.or_reservations_load_ex(self.h, len(r), abi.ptr(r), abi.ptr(a))
         if rc != 0:
             raise RuntimeError(f"oracle reservations_load rc={rc}")
         self._n_resv = len(r)
+
+    def restore_state(self, r):
+        """RestoreReservation's matched state of reservation r (or_restore_state): a RSV_STATE_DTYPE record."""
+        out = np.zeros(1, RSV_STATE_DTYPE)
+        assert self.lib.or_restore_state(self.h, int(r), abi.ptr(out)) == 0
+        return out[0]
+
+    def reservation_allocs_get(self):
+        out = np.zeros(getattr(self, "_n_resv", 0), abi.RESERVATION_ALLOC_DTYPE)
+        assert self.lib.or_reservation_allocs_get(self.h, len(out), abi.ptr(out)) == 0
+        return out
 
     def reservations_get(self):
         out = np.zeros(getattr(self, "_n_resv", 0), abi.RESERVATION_DTYPE)

@@ -63,12 +63,25 @@ typedef struct or_node {
   int32_t n_part;
   ke_gpu_partition part[KE_MAX_GPU_PARTITIONS];
   struct or_cpus* cpus; /* CPU topology + allocated CPUs (NULL: no CPU topology) */
+  /* the NodeAllocation while the NRT is deleted (topology_options.go:84-88 drops only the TopologyOptions):
+   * or_node_topology_delete parks the CPU table / zones, releases apply to them, a bare re-add takes them back */
+  struct or_cpus* kept_cpus;
+  int32_t n_kept_zone;
+  ke_numa_zone kept_zone[KE_MAX_NUMA];
   /* NodeInfo Allocatable / (NonZero)Requested by resource id (NodeResourcesFitPlus, ScarceResourceAvoidance) */
   int32_t n_xres;
   ke_node_resource xres[KE_MAX_XRES];
   /* the reservation cache's NodeInfo restore for a pod that matches no reservation (or_reservations_load) */
   int64_t rv_req[KE_NRES], rv_nz[KE_NRES];
   int32_t rv_pods; /* len(NodeInfo.Pods) delta of the restore: a matched reservation's reserve pod is removed */
+  /* the plugins' RestoreReservation states of the pod being evaluated (or_restore): NodeNUMAResource's
+   * mergedUnmatchedUsed per NUMA id (ResourceList keys tracked) and DeviceShare's per (type, minor) */
+  int rs_numa_has[KE_MAX_NUMA];
+  uint8_t rs_numa_key[KE_MAX_NUMA][KE_NRES];
+  int64_t rs_numa[KE_MAX_NUMA][KE_NRES];
+  int rs_dev_has[KE_DEV_TYPES][KE_MAX_MINORS];
+  uint8_t rs_dev_key[KE_DEV_TYPES][KE_MAX_MINORS][KE_DKEYS];
+  int64_t rs_dev[KE_DEV_TYPES][KE_MAX_MINORS][KE_DKEYS];
   int deleted; /* Node informer delete: out of the snapshot (every other cache keeps its state) */
 } or_node;
 
@@ -96,6 +109,9 @@ struct or_cluster {
    * lists of the next or_schedule (or_pod_reservations) and 1 + the reservation each pod of the last
    * or_schedule was assumed into */
   ke_reservation* resv;
+  ke_reservation_alloc* ralloc; /* the reservations' NUMA / cpuset / device holdings (NULL: none) */
+  const char* resv_m;           /* the matched flags of the pod being evaluated (or_resv_begin), NULL = none */
+  uint8_t* rcpu;                /* [reservation][cpu] owner counts (or_owner_update), NULL until first needed */
   int32_t n_resv;
   int32_t* moff;
   int32_t* mids;
@@ -992,9 +1008,14 @@ static int numa_view_build(const or_node* nd, numa_view* v, const numa_cs* cs) {
         al[KE_RES_CPU] = al[KE_RES_CPU] - cs + amplify(cs, ratio);
         has[KE_RES_CPU] = 1;
       }
-      for (int r = 0; r < KE_NRES; r++) { /* SubtractWithNonNegativeResult(allocated, reusable = {}) */
-        v->al_has[z][r] = has[r];
-        v->al[z][r] = has[r] && al[r] > 0 ? al[r] : 0;
+      /* SubtractWithNonNegativeResult(allocated, reusableResources[id]) (node_allocation.go:237): the pod's
+       * restore state (or_restore) -- keys of both, floor 0 */
+      const int zid = zn->id >= 0 && zn->id < KE_MAX_NUMA ? zn->id : -1;
+      for (int r = 0; r < KE_NRES; r++) {
+        const int rk = zid >= 0 && nd->rs_numa_has[zid] && nd->rs_numa_key[zid][r];
+        const int64_t q = (has[r] ? al[r] : 0) - (rk ? nd->rs_numa[zid][r] : 0);
+        v->al_has[z][r] = has[r] || rk;
+        v->al[z][r] = v->al_has[z][r] && q > 0 ? q : 0;
       }
     }
     for (int r = 0; r < KE_NRES; r++) { /* SubtractWithNonNegativeResult(capacity, allocated) */
@@ -1916,6 +1937,20 @@ static int dev_selected(const ds_pod* d, int t, const ke_device* dv) {
 static void ds_filtered_view_aff(const or_node* nd, const ds_pod* d, int t, ds_aff a, ds_view* v) {
   ds_orig_view(nd, t, v);
   const int nk = nkeys(t);
+  /* calcFreeWithPreemptible (device_cache.go:322-348) with the pod's restore state as preemptible: an instance
+   * with a preemptible entry and a non-zero remaining = total - (used - preemptible) frees that instead
+   * (mergedFreeDevices; the others keep deviceFree) */
+  for (int i = 0; i < v->n; i++) {
+    const int m = v->minor[i];
+    if (!nd->rs_dev_has[t][m]) continue;
+    rl pre = rl_empty();
+    for (int k = 0; k < nk; k++) {
+      pre.has[k] = nd->rs_dev_key[t][m][k];
+      pre.v[k] = nd->rs_dev[t][m][k];
+    }
+    const rl remaining = rl_sub_nonneg(v->total[i], rl_sub_nonneg(v->used[i], pre, nk), nk);
+    if (!rl_is_zero(remaining, nk)) v->free[i] = remaining;
+  }
   int all_zero = 1;
   for (int i = 0; i < v->n; i++)
     if (!rl_is_zero(v->free[i], nk)) all_zero = 0;
@@ -2855,6 +2890,8 @@ or_cluster* or_create(const ke_config* cfg, int32_t n_nodes) {
 void or_destroy(or_cluster* c) {
   if (!c) return;
   free(c->resv);
+  free(c->ralloc);
+  free(c->rcpu);
   free(c->moff);
   free(c->mids);
   free(c->last_resv);
@@ -2863,6 +2900,7 @@ void or_destroy(or_cluster* c) {
     free(c->nodes[i].agg);
     free(c->nodes[i].asg);
     free(c->nodes[i].cpus);
+    free(c->nodes[i].kept_cpus);
   }
   free(c->nodes);
   free(c->quotas);
@@ -2901,10 +2939,100 @@ int or_gpu_templates_load(or_cluster* c, int32_t n, const ke_gpu_template* t) {
 static const ke_node_resource* node_xres(const or_node* nd, int32_t id);
 static int64_t or_non0(int k, int64_t v) { return v != 0 ? v : (k == KE_RES_CPU ? 100 : 200LL << 20); }
 static int or_resv_usable(const ke_reservation* r) { return r->available && !(r->allocate_once && r->allocated_pods > 0); }
+/* NodeNUMAResource RestoreReservation for one unmatched reservation (nodenumaresource/reservation.go:196-209) and
+ * its share of mergeReservationAllocations (:111-120): allocatable = the reserve pod's NUMANodeResources,
+ * allocated = Σ owners', remained = subtractAllocated(copy(allocatable), allocated, false) over allocated's NUMA ids
+ * (quotav1.Subtract: keys of both), used = subtractAllocated(copy(allocatable), remained, true) over remained's ids
+ * (SubtractWithNonNegativeResult: keys of both, floor 0), added into the node's map (quotav1.Add).  A zero
+ * amount in ke_reservation_alloc is an absent key. */
+static void or_numa_unmatched_used(or_node* nd, const ke_reservation_alloc* a) {
+  int any = 0;
+  for (int j = 0; j < KE_MAX_NUMA * KE_NRES; j++) any |= a->numa[j] != 0;
+  if (!any) return; /* GetAllocatedNUMAResource(reservePod) empty: no allocatable, nothing restored */
+  for (int id = 0; id < KE_MAX_NUMA; id++) {
+    const int in_alloc = a->numa[2 * id] != 0 || a->numa[2 * id + 1] != 0;
+    const int in_owned = a->owner_numa[2 * id] != 0 || a->owner_numa[2 * id + 1] != 0;
+    /* remained[id]: allocatable (copy) minus allocated where the owners hold the id */
+    int rem_has[KE_NRES] = {0, 0}, rem_in = in_alloc || in_owned;
+    int64_t rem[KE_NRES] = {0, 0};
+    for (int r = 0; r < KE_NRES; r++) {
+      const int ha = a->numa[2 * id + r] != 0, hb = in_owned && a->owner_numa[2 * id + r] != 0;
+      rem_has[r] = ha || hb;
+      rem[r] = (ha ? a->numa[2 * id + r] : 0) - (hb ? a->owner_numa[2 * id + r] : 0);
+    }
+    if (!rem_in) continue;
+    /* used[id] = SubtractWithNonNegativeResult(allocatable[id], remained[id]) */
+    nd->rs_numa_has[id] = 1;
+    for (int r = 0; r < KE_NRES; r++) {
+      const int ha = a->numa[2 * id + r] != 0;
+      if (!ha && !rem_has[r]) continue;
+      const int64_t u = (ha ? a->numa[2 * id + r] : 0) - (rem_has[r] ? rem[r] : 0);
+      nd->rs_numa_key[id][r] = 1;
+      nd->rs_numa[id][r] += u > 0 ? u : 0;
+    }
+  }
+}
+
+/* DeviceShare RestoreReservation for one unmatched reservation (deviceshare/reservation.go:157-178): allocatable =
+ * nd.getUsed(reservePod), allocated = appendAllocatedByHints(the reserve pod's minors, owners' usage),
+ * remained = subtractAllocated(copy(allocatable), allocated, false), used = subtractAllocated(copy(allocatable),
+ * remained, true) -- deviceResources.subtract drops an instance whose result IsZero -- then appendAllocated. */
+static void or_dev_unmatched_used(or_node* nd, const ke_reservation_alloc* a) {
+  for (int t = 0; t < KE_DEV_TYPES; t++) {
+    const int nk = t == KE_DEV_GPU ? 3 : 1;
+    for (int m = 0; m < KE_MAX_MINORS; m++) {
+      if (!(a->device_minors >> (16 * t + m) & 1)) continue;
+      rl al = rl_empty(), ow = rl_empty(), rem;
+      for (int k = 0; k < nk; k++) {
+        al.has[k] = a->device[t][m][k] != 0;
+        al.v[k] = a->device[t][m][k];
+        ow.has[k] = a->owner_device[t][m][k] != 0;
+        ow.v[k] = a->owner_device[t][m][k];
+      }
+      const int owned = (a->owner_device_minors >> (16 * t + m) & 1) && !rl_is_zero(ow, nk);
+      int rem_in = 1;
+      if (owned) { /* quotav1.Subtract, deleted when IsZero */
+        rem = rl_empty();
+        for (int k = 0; k < nk; k++) {
+          rem.has[k] = al.has[k] || ow.has[k];
+          rem.v[k] = al.v[k] - ow.v[k];
+        }
+        rem_in = !rl_is_zero(rem, nk);
+      } else {
+        rem = al;
+      }
+      rl used = al; /* an instance absent from remained keeps allocatable's list in used */
+      if (rem_in) used = rl_sub_nonneg(al, rem, nk);
+      if (rl_is_zero(used, nk)) continue; /* deleted */
+      nd->rs_dev_has[t][m] = 1;
+      for (int k = 0; k < nk; k++)
+        if (used.has[k]) {
+          nd->rs_dev_key[t][m][k] = 1;
+          nd->rs_dev[t][m][k] += used.v[k];
+        }
+    }
+  }
+}
+
 static void or_restore(or_cluster* c, const char* matched, int with_matched) {
   for (int32_t i = 0; i < c->n; i++) {
-    for (int k = 0; k < KE_NRES; k++) c->nodes[i].rv_req[k] = c->nodes[i].rv_nz[k] = 0;
-    c->nodes[i].rv_pods = 0;
+    or_node* nd = &c->nodes[i];
+    for (int k = 0; k < KE_NRES; k++) nd->rv_req[k] = nd->rv_nz[k] = 0;
+    nd->rv_pods = 0;
+    memset(nd->rs_numa_has, 0, sizeof nd->rs_numa_has);
+    memset(nd->rs_numa_key, 0, sizeof nd->rs_numa_key);
+    memset(nd->rs_numa, 0, sizeof nd->rs_numa);
+    memset(nd->rs_dev_has, 0, sizeof nd->rs_dev_has);
+    memset(nd->rs_dev_key, 0, sizeof nd->rs_dev_key);
+    memset(nd->rs_dev, 0, sizeof nd->rs_dev);
+  }
+  /* the plugins' unmatched restore states: the node's unmatched reservations with allocated pods
+   * (transformer.go:195-199) */
+  for (int32_t i = 0; c->ralloc && i < c->n_resv; i++) {
+    const ke_reservation* r = &c->resv[i];
+    if (!or_resv_usable(r) || (matched && matched[i]) || r->allocated_pods == 0) continue;
+    or_numa_unmatched_used(&c->nodes[r->node], &c->ralloc[i]);
+    or_dev_unmatched_used(&c->nodes[r->node], &c->ralloc[i]);
   }
   for (int32_t i = 0; i < c->n_resv; i++) {
     const ke_reservation* r = &c->resv[i];
@@ -2932,16 +3060,145 @@ static void or_restore(or_cluster* c, const char* matched, int with_matched) {
     }
   }
 }
-int or_reservations_load(or_cluster* c, int32_t n, const ke_reservation* rs) {
+/* An owner pod enters (+1) / leaves (-1) the reservation's AssignedPods: its resource manager / device cache entries
+ * are what RestoreReservation sums as the owners' (reservation.go:201-226, deviceshare/reservation.go:165-170).
+ * CPUs are counted per owner (c->rcpu), the owners' union is the record's owner_cpuset. */
+static void or_owner_update(or_cluster* c, int32_t idx, const ke_pod* pod, const uint64_t* cpuset, const int64_t* numa,
+                            uint64_t dev_minors, int sign) {
+  if (!c->ralloc || idx < 0 || idx >= c->n_resv) return;
+  ke_reservation_alloc* a = &c->ralloc[idx];
+  if (!c->rcpu) {
+    c->rcpu = (uint8_t*)calloc((size_t)c->n_resv * KE_MAX_CPUS, 1);
+    for (int32_t i = 0; i < c->n_resv; i++)
+      for (int cpu = 0; cpu < KE_MAX_CPUS; cpu++)
+        c->rcpu[(size_t)i * KE_MAX_CPUS + cpu] = (uint8_t)(c->ralloc[i].owner_cpuset[cpu >> 6] >> (cpu & 63) & 1);
+  }
+  uint8_t* cnt = c->rcpu + (size_t)idx * KE_MAX_CPUS;
+  for (int cpu = 0; cpuset && cpu < KE_MAX_CPUS; cpu++) {
+    if (!(cpuset[cpu >> 6] >> (cpu & 63) & 1)) continue;
+    if (sign > 0 && cnt[cpu] < 255) cnt[cpu]++;
+    if (sign < 0 && cnt[cpu] > 0) cnt[cpu]--;
+    if (cnt[cpu]) a->owner_cpuset[cpu >> 6] |= 1ull << (cpu & 63);
+    else a->owner_cpuset[cpu >> 6] &= ~(1ull << (cpu & 63));
+  }
+  for (int j = 0; numa && j < KE_MAX_NUMA * KE_NRES; j++) {
+    const int64_t v = a->owner_numa[j] + sign * numa[j];
+    a->owner_numa[j] = v > 0 ? v : 0;
+  }
+  if (dev_minors) {
+    const or_node* nd = &c->nodes[c->resv[idx].node];
+    ds_pod d;
+    ds_prepare_pod(c, pod, &d);
+    for (int i = 0; i < nd->n_dev; i++) {
+      const ke_device* dv = &nd->dev[i];
+      const uint64_t bit = 1ull << (16 * dv->type + dv->minor);
+      if (!(dev_minors & bit)) continue;
+      rl amt = d.has[dv->type] ? d.req[dv->type] : rl_empty();
+      if (dv->type == KE_DEV_GPU) fill_gpu_total_mem(dv, &amt);
+      int any = 0;
+      for (int k = 0; k < KE_DKEYS; k++) {
+        int64_t* o = &a->owner_device[dv->type][dv->minor][k];
+        if (amt.has[k]) {
+          const int64_t v = *o + sign * amt.v[k];
+          *o = v > 0 ? v : 0;
+        }
+        any |= *o != 0;
+      }
+      if (any) a->owner_device_minors |= bit;
+      else a->owner_device_minors &= ~bit;
+    }
+  }
+}
+
+/* RestoreReservation's per-reservation state of a matched reservation (nodenumaresource/reservation.go:187-239,
+ * deviceshare/reservation.go:148-180), as the allocate-from-reservation paths read it:
+ *  - CPUs: allocatableCPUs = the reserve pod's cpuset; allocatedCPUs starts as that same set and only grows by
+ *    allocatable ∩ owner CPUs, so it equals allocatableCPUs (the reference's own construction, pinned by
+ *    TestRestoreReservation); remainedCPUs = allocatable minus the owners' CPUs;
+ *  - NUMA (only with the reserve pod's NUMA resources): allocatable, allocated = Σ owners', remained =
+ *    subtractAllocated(copy(allocatable), allocated, false) -- quotav1.Subtract, may go negative;
+ *  - devices (only with the reserve pod's instances): allocatable, allocated = the owners' usage on those instances,
+ *    remained = subtractAllocated(copy(allocatable), allocated, false) dropping all-zero instances.
+ * A zero amount is an absent ResourceList key. */
+int or_restore_state(const or_cluster* c, int32_t r, or_rsv_state* out) {
+  if (!c->ralloc || r < 0 || r >= c->n_resv) return KE_ERR_NOT_FOUND;
+  const ke_reservation_alloc* a = &c->ralloc[r];
+  memset(out, 0, sizeof *out);
+  for (int w = 0; w < 4; w++) {
+    out->allocatable_cpus[w] = a->cpuset[w];
+    out->allocated_cpus[w] = a->cpuset[w];
+    out->remained_cpus[w] = a->cpuset[w] & ~a->owner_cpuset[w];
+  }
+  for (int j = 0; j < KE_MAX_NUMA * KE_NRES; j++) out->numa_in |= a->numa[j] != 0;
+  if (out->numa_in)
+    for (int j = 0; j < KE_MAX_NUMA * KE_NRES; j++) {
+      out->numa_allocatable[j] = a->numa[j];
+      out->numa_allocated[j] = a->owner_numa[j];
+      out->numa_remained[j] = a->numa[j] - a->owner_numa[j];
+      out->numa_remained_has[j] = a->numa[j] != 0 || a->owner_numa[j] != 0;
+    }
+  for (int t = 0; t < KE_DEV_TYPES; t++) {
+    const int nk = t == KE_DEV_GPU ? 3 : 1;
+    for (int m = 0; m < KE_MAX_MINORS; m++) {
+      const uint64_t bit = 1ull << (16 * t + m);
+      if (!(a->device_minors & bit)) continue;
+      out->dev_allocatable_minors |= bit;
+      int owned = 0, rem_nz = 0;
+      for (int k = 0; k < nk; k++) owned |= (a->owner_device_minors & bit) && a->owner_device[t][m][k] != 0;
+      for (int k = 0; k < nk; k++) {
+        out->dev_allocatable[t][m][k] = a->device[t][m][k];
+        out->dev_allocated[t][m][k] = owned ? a->owner_device[t][m][k] : 0;
+        out->dev_remained[t][m][k] = a->device[t][m][k] - out->dev_allocated[t][m][k];
+        rem_nz |= out->dev_remained[t][m][k] != 0;
+      }
+      if (owned) out->dev_allocated_minors |= bit;
+      if (rem_nz) out->dev_remained_minors |= bit;
+    }
+  }
+  return KE_OK;
+}
+
+static uint8_t or_holds_of(const ke_reservation_alloc* a) {
+  uint8_t h = 0;
+  for (int j = 0; j < KE_MAX_NUMA * KE_NRES; j++)
+    if (a->numa[j]) h |= KE_RSV_HOLDS_NUMA;
+  for (int w = 0; w < 4; w++)
+    if (a->cpuset[w]) h |= KE_RSV_HOLDS_CPUSET;
+  if (a->device_minors) h |= KE_RSV_HOLDS_DEVICES;
+  return h;
+}
+int or_reservations_load_ex(or_cluster* c, int32_t n, const ke_reservation* rs, const ke_reservation_alloc* allocs) {
   for (int32_t i = 0; i < n; i++) {
     if (rs[i].node < 0 || rs[i].node >= c->n) return KE_ERR_NOT_FOUND;
-    if (rs[i].holds) return KE_ERR_UNSUPPORTED; /* NUMA / cpuset / device holdings: not restated */
+    const uint8_t said = rs[i].holds & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET | KE_RSV_HOLDS_DEVICES);
+    if (rs[i].holds & KE_RSV_OTHER_ALLOCATABLE) return KE_ERR_UNSUPPORTED; /* other allocatable names */
+    if (!allocs && said) return KE_ERR_UNSUPPORTED;                      /* holdings without their record */
+    if (allocs && or_holds_of(&allocs[i]) != said) return KE_ERR_INVALID;
   }
   free(c->resv);
   c->resv = (ke_reservation*)malloc(sizeof(ke_reservation) * (size_t)(n > 0 ? n : 1));
   if (n > 0) memcpy(c->resv, rs, sizeof(ke_reservation) * (size_t)n);
+  free(c->ralloc);
+  c->ralloc = NULL;
+  free(c->rcpu);
+  c->rcpu = NULL;
+  if (allocs && n > 0) {
+    c->ralloc = (ke_reservation_alloc*)malloc(sizeof(ke_reservation_alloc) * (size_t)n);
+    memcpy(c->ralloc, allocs, sizeof(ke_reservation_alloc) * (size_t)n);
+  }
   c->n_resv = n;
   or_restore(c, NULL, 0);
+  return KE_OK;
+}
+int or_reservations_load(or_cluster* c, int32_t n, const ke_reservation* rs) {
+  return or_reservations_load_ex(c, n, rs, NULL);
+}
+int or_reservation_allocs_get(const or_cluster* c, int32_t n, ke_reservation_alloc* out) {
+  if (n < 0 || n > c->n_resv) return KE_ERR_INVALID;
+  for (int32_t i = 0; i < n; i++) {
+    if (c->ralloc) out[i] = c->ralloc[i];
+    else memset(&out[i], 0, sizeof out[i]);
+  }
   return KE_OK;
 }
 int or_reservations_get(const or_cluster* c, int32_t n, ke_reservation* out) {
@@ -2990,7 +3247,13 @@ static int or_resv_nominable(const or_cluster* c, const ke_reservation* r, const
   for (int k = 0; k < KE_NRES; k++)
     if (r->allocatable[k] != 0 && pod->requests[k] != 0) shared = 1;
   if (!shared && !affinity) return 0; /* plugin.go:373: skipped only without a reservation affinity */
-  int node_fits = 1;
+  /* fitsNode's pod count (plugin.go:450-453): len(nodeInfo.Pods) of the snapshot NodeInfo the BeforePreFilter
+   * restore left (the matched reserve pods removed: rv_pods after or_restore(m, 1)) minus len(matchedOrIgnored) */
+  int32_t n_matched = 0;
+  for (int32_t i = 0; i < c->n_resv; i++)
+    if (c->resv[i].node == node && or_resv_usable(&c->resv[i]) && c->resv_m && c->resv_m[i]) n_matched++;
+  int node_fits = (int64_t)c->nodes[node].node.pod_count + c->nodes[node].rv_pods - n_matched + 1 <=
+                  (int64_t)c->nodes[node].node.allowed_pods;
   if (!(pod->requests[KE_RES_CPU] == 0 && pod->requests[KE_RES_MEMORY] == 0)) {
     for (int k = 0; k < KE_NRES; k++) {
       int64_t remained = r->allocatable[k] - r->allocated[k];
@@ -3082,6 +3345,17 @@ int or_node_cpus_set(or_cluster* c, int32_t node, int32_t n, const ke_cpu* cpus,
   }
   acc_topo_finish(&x->t);
   x->max_ref = max_ref;
+  int bare = 1; /* no allocatedCPUs given: the parked NodeAllocation comes back by CPU id */
+  for (int i = 0; i < ACC_MAX_CPUS; i++) bare = bare && !x->al.present[i];
+  if (bare && nd->kept_cpus)
+    for (int i = 0; i < ACC_MAX_CPUS; i++)
+      if (x->t.valid[i] && nd->kept_cpus->al.present[i]) {
+        x->al.present[i] = 1;
+        x->al.ref[i] = nd->kept_cpus->al.ref[i];
+        x->al.excl[i] = nd->kept_cpus->al.excl[i];
+      }
+  free(nd->kept_cpus);
+  nd->kept_cpus = NULL;
   free(nd->cpus);
   nd->cpus = x;
   return KE_OK;
@@ -3341,6 +3615,25 @@ int or_node_numa_set(or_cluster* c, int32_t node, int32_t n, const ke_numa_zone*
       if (z->numa_status == KE_NUMA_STATUS_SHARED) z->shared_pods = 1;
     }
   }
+  or_node* nd = &c->nodes[node];
+  int bare = 1; /* an NRT without the resource manager's allocation: the parked zones' allocation comes back */
+  for (int32_t i = 0; i < n; i++)
+    bare = bare && !nd->zone[i].has_allocated && !nd->zone[i].single_pods && !nd->zone[i].shared_pods &&
+           !nd->zone[i].cpuset_cpus;
+  if (bare)
+    for (int32_t i = 0; i < n; i++)
+      for (int32_t k = 0; k < nd->n_kept_zone; k++)
+        if (nd->kept_zone[k].id == nd->zone[i].id) {
+          ke_numa_zone* z = &nd->zone[i];
+          const ke_numa_zone* kz = &nd->kept_zone[k];
+          z->has_allocated = kz->has_allocated;
+          for (int r = 0; r < KE_NRES; r++) z->allocated[r] = kz->allocated[r];
+          z->cpuset_cpus = kz->cpuset_cpus;
+          z->single_pods = kz->single_pods;
+          z->shared_pods = kz->shared_pods;
+          z->numa_status = zone_status_of(z);
+        }
+  if (n > 0) nd->n_kept_zone = 0;
   return KE_OK;
 }
 
@@ -3395,8 +3688,15 @@ int or_node_delete(or_cluster* c, int32_t node) {
 int or_node_topology_delete(or_cluster* c, int32_t node) {
   if (node < 0 || node >= c->n) return KE_ERR_NOT_FOUND;
   or_node* nd = &c->nodes[node];
+  if (nd->n_zone) {
+    nd->n_kept_zone = nd->n_zone;
+    memcpy(nd->kept_zone, nd->zone, sizeof(ke_numa_zone) * (size_t)nd->n_zone);
+  }
   nd->n_zone = 0;
-  free(nd->cpus);
+  if (nd->cpus) {
+    free(nd->kept_cpus);
+    nd->kept_cpus = nd->cpus;
+  }
   nd->cpus = NULL;
   nd->node.cpuset_allocated_cpus = 0;
   nd->node.nrt_cpu_amplification_ratio = -2;
@@ -3741,6 +4041,7 @@ static char* or_resv_begin(or_cluster* c, const int32_t* ids, int32_t n_ids, int
   char* m = (char*)calloc((size_t)(c->n_resv > 0 ? c->n_resv : 1), 1);
   for (int32_t j = 0; j < n_ids; j++)
     if (or_resv_usable(&c->resv[ids[j]])) m[ids[j]] = 1;
+  c->resv_m = m;
   or_restore(c, m, 0);
   *pod_requested = (int64_t*)malloc(sizeof(int64_t) * KE_NRES * (size_t)(N > 0 ? N : 1));
   for (int32_t i = 0; i < N; i++)
@@ -3756,6 +4057,7 @@ int32_t or_reservation_prescore(or_cluster* c, const ke_pod* pod, const int32_t*
   char* m = or_resv_begin(c, ids, n_ids, &pr);
   const int32_t pref = or_resv_prescore(c, pod, m, pr, NULL, 0, raw, nom);
   or_restore(c, NULL, 0);
+  c->resv_m = NULL;
   free(m);
   free(pr);
   return pref;
@@ -3767,6 +4069,7 @@ int32_t or_reservation_filter(or_cluster* c, const ke_pod* pod, const int32_t* i
   char* m = or_resv_begin(c, ids, n_ids, &pr);
   const int32_t ok = or_resv_filter_node(c, pod, m, pr, node);
   or_restore(c, NULL, 0);
+  c->resv_m = NULL;
   free(m);
   free(pr);
   return ok;
@@ -3811,6 +4114,7 @@ static int32_t or_resv_eval(or_cluster* c, const ke_pod* pod, int64_t now, eval_
     }
   }
   *best = b >= 0 ? (int32_t)bt : -1;
+  c->resv_m = NULL;
   free(m);
   free(pr);
   free(feasible);
@@ -3838,8 +4142,11 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
     for (int r = KE_NRES; r < KE_RES_COUNT; r++) scalar |= pods[p].requests[r] != 0;
     for (int r = 0; r < KE_PDR_COUNT; r++) scalar |= pods[p].device_requests[r] != 0;
     if (scalar) return KE_ERR_UNSUPPORTED;
+    /* a matched reservation holding a NUMA allocation or a cpuset on a NUMA-policy node: its allocate-from-
+     * reservation path (tryAllocateFromReservation in the hints) is not restated */
     for (int32_t j = c->moff[p]; j < c->moff[p + 1]; j++)
-      if (or_resv_usable(&c->resv[c->mids[j]]) &&
+      if (or_resv_usable(&c->resv[c->mids[j]]) && c->ralloc &&
+          (or_holds_of(&c->ralloc[c->mids[j]]) & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)) &&
           c->nodes[c->resv[c->mids[j]].node].node.numa_topology_policy != KE_NUMA_POLICY_NONE)
         return KE_ERR_UNSUPPORTED;
   }
@@ -3932,6 +4239,7 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
           if (r->allocatable[k] != 0) r->allocated[k] += pods[p].requests[k];
         r->allocated_pods++;
         c->last_resv[p] = 1 + nom[b];
+        or_owner_update(c, nom[b], &pods[p], rp.cpus, numa_alloc ? numa_alloc + (int64_t)p * 16 : NULL, mask, +1);
         or_restore(c, NULL, 0);
       }
     }
@@ -3981,6 +4289,7 @@ int or_pod_release(or_cluster* c, const ke_pod* pod, const ke_pod_allocation* a,
     for (int k = 0; k < KE_NRES; k++)
       if (r->allocatable[k] != 0) r->allocated[k] = r->allocated[k] - pod->requests[k] > 0 ? r->allocated[k] - pod->requests[k] : 0;
     if (r->allocated_pods > 0) r->allocated_pods--;
+    or_owner_update(c, ridx, pod, a->cpuset, a->numa, a->device_minors, -1);
     or_restore(c, NULL, 0);
   }
   if (node >= 0) {
@@ -3994,8 +4303,11 @@ int or_pod_release(or_cluster* c, const ke_pod* pod, const ke_pod_allocation* a,
         ke_node_resource* r = (ke_node_resource*)node_xres(n, pod->xres_id[e]);
         if (r) r->requested -= pod->xres_value[e];
       }
-    if (cpus_valid(n)) {
-      or_cpus* x = n->cpus;
+    const int parked = !n->cpus && n->kept_cpus; /* NRT deleted: the NodeAllocation is parked */
+    if (cpus_valid(n) || parked) {
+      or_cpus* x = parked ? n->kept_cpus : n->cpus;
+      ke_numa_zone* zones = parked ? n->kept_zone : n->zone;
+      const int32_t nz = parked ? n->n_kept_zone : n->n_zone;
       int used[ACC_MAX_CPUS], nu = 0;
       for (int cpu = 0; cpu < ACC_MAX_CPUS; cpu++) {
         if (!(a->cpuset[cpu >> 6] >> (cpu & 63) & 1) || !x->al.present[cpu]) continue;
@@ -4007,8 +4319,8 @@ int or_pod_release(or_cluster* c, const ke_pod* pod, const ke_pod_allocation* a,
         for (int k = 0; k < nu && !f; k++) f = used[k] == x->t.node[cpu];
         if (!f) used[nu++] = x->t.node[cpu];
       }
-      for (int z = 0; z < n->n_zone; z++) {
-        ke_numa_zone* zn = &n->zone[z];
+      for (int z = 0; z < nz; z++) {
+        ke_numa_zone* zn = &zones[z];
         for (int k = 0; k < nu; k++)
           if (used[k] == zn->id) {
             int16_t* cnt = nu > 1 ? &zn->shared_pods : &zn->single_pods;

@@ -47,6 +47,22 @@ int or_set_pod_device_hints(or_cluster* c, int32_t n, const ke_pod_device_hints*
 int or_gpu_templates_load(or_cluster* c, int32_t n, const ke_gpu_template* t);
 int or_node_device_flags(or_cluster* c, int32_t node, int32_t secondary_well_planned, int32_t gpu_model_key);
 int or_reservations_load(or_cluster* c, int32_t n, const ke_reservation* r);
+int or_reservations_load_ex(or_cluster* c, int32_t n, const ke_reservation* r, const ke_reservation_alloc* allocs);
+int or_reservation_allocs_get(const or_cluster* c, int32_t n, ke_reservation_alloc* out);
+/* RestoreReservation's state of reservation r as a matched reservation (golden entry, oracle.c) */
+typedef struct or_rsv_state {
+  uint64_t allocatable_cpus[4], allocated_cpus[4], remained_cpus[4];
+  int32_t numa_in; /* the reserve pod has NUMA resources (allocatable != nil) */
+  int32_t pad;
+  int64_t numa_allocatable[KE_MAX_NUMA * KE_NRES], numa_allocated[KE_MAX_NUMA * KE_NRES];
+  int64_t numa_remained[KE_MAX_NUMA * KE_NRES];
+  uint8_t numa_remained_has[KE_MAX_NUMA * KE_NRES];
+  uint64_t dev_allocatable_minors, dev_allocated_minors, dev_remained_minors;
+  int64_t dev_allocatable[KE_DEV_TYPES][KE_MAX_MINORS][KE_DKEYS];
+  int64_t dev_allocated[KE_DEV_TYPES][KE_MAX_MINORS][KE_DKEYS];
+  int64_t dev_remained[KE_DEV_TYPES][KE_MAX_MINORS][KE_DKEYS];
+} or_rsv_state;
+int or_restore_state(const or_cluster* c, int32_t r, or_rsv_state* out);
 int or_reservations_get(const or_cluster* c, int32_t n, ke_reservation* out);
 int or_pod_reservations(or_cluster* c, int32_t n_pods, const int32_t* offsets, const int32_t* ids);
 int or_last_reservations(const or_cluster* c, int32_t n, int32_t* out);

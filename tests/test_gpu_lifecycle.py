@@ -112,13 +112,55 @@ def test_node_delete_cpuset_numa_devices_parity(gpu):
     for h in (ev2, o2):
         for i in gone:
             h.delete_node(int(i))
-    dp = synth.make_ds_pods(200, synth.BASE_SEED + 1118) if hasattr(synth, "make_ds_pods") else None
-    if dp is not None:
-        c1, s1 = ev2.schedule(dp, synth.T0)
-        c0, s0 = o2.schedule(dp, synth.T0)
-        assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
-        assert np.array_equal(ev2.last_device_allocations, o2.last_device_allocations)
-        assert not np.isin(c1, gone).any()
+    dp = synth.make_ds_pods(200, synth.BASE_SEED + 1118)
+    c1, s1 = ev2.schedule(dp, synth.T0)
+    c0, s0 = o2.schedule(dp, synth.T0)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    assert np.array_equal(ev2.last_device_allocations, o2.last_device_allocations)
+    assert (ev2.last_device_allocations != 0).any()
+    assert not np.isin(c1, gone).any()
+
+
+def test_topology_delete_readd_keeps_allocation_parity(gpu):
+    """NRT deletes between queues, cpuset pods released during the gap, then bare NRT re-adds
+    (topology only, as the informer delivers them): the parked NodeAllocation comes back, so the next cpuset queue
+    never hands out a CPU beyond MaxRefCount and stays bit-exact with the oracle (cpusets, NUMA allocations)."""
+    from test_lifecycle import _bare
+    n = 500
+    cl = synth.make_cluster(n, synth.BASE_SEED + 1151, amplified_fraction=0.2)
+    zones, tabs = synth.make_numa_cpus(cl, synth.BASE_SEED + 1152)
+    cfg = synth.config(n)
+    ev, o = Evaluator(cfg), Oracle(cfg, n)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        synth.load_numa(h, zones)
+        synth.load_cpus(h, tabs)
+    pods = synth.make_numa_cpuset_pods(600, synth.BASE_SEED + 1153)
+    assert_schedule_equal(ev, o, pods, synth.T0)
+    a1, a0 = ev.last_allocations(), o.last_allocations()
+    cs_pods = np.flatnonzero((a1["node"] >= 0) & a1["cpuset"].any(axis=1))
+    assert len(cs_pods) >= 10
+    nodes = np.unique(a1["node"][cs_pods])[:30]
+    for h in (ev, o):
+        for i in nodes:
+            h.delete_topology(int(i))
+    for p in cs_pods[:8]:  # pod GC during the gap
+        ev.release(pods[p], a1[p], abi.RELEASE_DELETE)
+        o.release(pods[p], a0[p], abi.RELEASE_DELETE)
+    for i in nodes:
+        t, z = _bare(tabs[i][0], zones[i])
+        for h in (ev, o):
+            h.set_numa(int(i), z)
+            h.set_cpus(int(i), t, tabs[i][1])
+    more = synth.make_numa_cpuset_pods(600, synth.BASE_SEED + 1154, key_base=8_500_000_000)
+    assert_schedule_equal(ev, o, more, synth.T0)
+    assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
+    assert ev.check_records(synth.T0) == 0
+    for i in nodes:
+        cpus1, cpus0 = ev.node_state(int(i))[1], o.node_state(int(i))[1]
+        assert np.array_equal(cpus1["ref_count"], cpus0["ref_count"]), i
+        assert cpus1["ref_count"].max(initial=0) <= tabs[i][1], i
+    assert sum(int(ev.node_state(int(i))[1]["ref_count"].sum()) for i in nodes) > 0
 
 
 def test_refused_call_leaves_no_state(gpu):

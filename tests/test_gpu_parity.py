@@ -218,6 +218,35 @@ def test_schedule_large_cluster_prefix(gpu):
     assert ev.check_records(synth.T0) == 0
 
 
+@pytest.mark.parametrize("per_call", [5000, 100_000], ids=["driver-calls", "one-call"])
+def test_c3_full_queue_fixture(gpu, per_call):
+    """the headline run end to end -- all 100,000 pods of the config-3 queue on the 50k-node
+    cluster (1,563 pipelined batches: stale lists, helpers, k_patch), in the driver's 5,000-pod calls and in one
+    call -- against the oracle's full-queue fixture (tests/golden/make_c3_fixture.py), every placement and
+    score bit-exact, the rows and records exact afterwards."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_c3_fixture import build_inputs, inputs_digest
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "c3_placements.npz"))
+    cl, pods = build_inputs()
+    assert str(g["digest"]) == inputs_digest(cl, pods), "generator changed: regenerate the fixture"
+    ev = Evaluator(synth.config(cl.n_nodes))
+    synth.load_into(ev, cl)
+    chosen, score = [], []
+    for s in range(0, len(pods), per_call):
+        c, sc = ev.schedule(pods[s:s + per_call], synth.T0)
+        chosen.append(c)
+        score.append(sc)
+    chosen, score = np.concatenate(chosen), np.concatenate(score)
+    bad = np.flatnonzero((chosen != g["chosen"]) | (score != g["score"].astype(np.int32)))
+    assert len(bad) == 0, (len(bad), bad[:5].tolist())
+    assert (chosen >= 0).sum() > 90_000
+    dev, host = ev.debug_rows(synth.T0)
+    assert np.array_equal(dev, host)
+    assert ev.check_records(synth.T0) == 0
+
+
 # ---- the stale-list run's options: T-row helpers, progressive R+S, patched early eval -----------------
 @pytest.mark.parametrize("helpers,patch,ignore", [("0", "1", "0"), ("4", "0", "0"), ("4", "1", "1"), ("8", "1", "0")],
                          ids=["no-helpers", "no-patch", "helpers-ignored", "8-helpers"])

@@ -1,0 +1,85 @@
+"""Reservations whose reserve pods hold NUMA resources, cpusets and device instances (ke_reservations_load_ex,
+SURVEY.md §8f rank 3) on the GPU: every pod that does not match them sees the plugins' restore states -- the
+unmatched reservations' owners' part given back as NodeNUMAResource's reusableResources
+(nodenumaresource/reservation.go:111-120, node_allocation.go:221-243) and as DeviceShare's preemptible
+(deviceshare/reservation.go:99-108, device_cache.go:322-365) -- bit-exact with the oracle's restatement on eval
+matrices, schedules, cpusets, NUMA allocations, device minors and the reservation state."""
+import numpy as np
+import pytest
+
+from koordinator_amd import Evaluator, abi, synth
+from oracle.binding import Oracle
+from test_gpu_cpuset import assert_eval_equal, assert_schedule_equal
+
+pytestmark = pytest.mark.gpu
+
+
+def holding_cluster(n, seed, devices=False, frac=0.3):
+    cl = synth.make_cluster(n, synth.BASE_SEED + seed, amplified_fraction=0.2)
+    zones, tabs = synth.make_numa_cpus(cl, synth.BASE_SEED + seed + 1)
+    devs = synth.make_devices(n, synth.BASE_SEED + seed + 2) if devices else None
+    rs, al = synth.make_reservation_holdings(cl, synth.BASE_SEED + seed + 3, zones, tabs, devs, frac=frac)
+    cfg = synth.config(n)
+    ev, o = Evaluator(cfg), Oracle(cfg, n)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        synth.load_numa(h, zones)
+        synth.load_cpus(h, tabs)
+        if devs is not None:
+            synth.load_devices(h, devs)
+        h.reservations_load(rs, al)
+    return ev, o, cl, rs, al
+
+
+def test_holdings_generator_covers_every_kind():
+    _, _, _, rs, al = holding_cluster(300, 1301, devices=True)
+    h = rs["holds"]
+    for bit in (abi.RSV_HOLDS_NUMA, abi.RSV_HOLDS_CPUSET, abi.RSV_HOLDS_DEVICES):
+        assert ((h & bit) != 0).sum() >= 5, bit
+    assert ((rs["allocated_pods"] > 0) & (h != 0)).sum() >= 10
+    assert (al["owner_numa"] > 0).any() and al["owner_cpuset"].any() and (al["owner_device"] > 0).any()
+
+
+@pytest.mark.parametrize("seed", [1311, 1312])
+def test_holdings_unmatched_numa_cpuset_parity(gpu, seed):
+    """NUMA-policy nodes (every policy) and cpuset pods: the zones' availability with the unmatched reservations'
+    owners given back equals the oracle's restatement -- eval matrices, then a queue with Reserves."""
+    ev, o, *_ = holding_cluster(400, seed)
+    pods = synth.make_numa_cpuset_pods(500, synth.BASE_SEED + seed + 10)
+    assert_eval_equal(ev.eval(pods[:64], synth.T0), o.eval(pods[:64], synth.T0))
+    assert_schedule_equal(ev, o, pods, synth.T0)
+    assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
+    assert ev.check_records(synth.T0) == 0
+
+
+def test_holdings_unmatched_deviceshare_parity(gpu):
+    """DeviceShare pods: the instances the unmatched reservations' owners share with their reserve pods count once
+    (calcFreeWithPreemptible) -- raw scores, totals, placements and device minors equal the oracle's."""
+    ev, o, *_ = holding_cluster(400, 1321, devices=True, frac=0.5)
+    pods = synth.make_ds_pods(400, synth.BASE_SEED + 1322)
+    a, b = ev.eval(pods[:64], synth.T0), o.eval(pods[:64], synth.T0)
+    assert_eval_equal(a, b)
+    c1, s1 = ev.schedule(pods, synth.T0)
+    c0, s0 = o.schedule(pods, synth.T0)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    assert np.array_equal(ev.last_device_allocations, o.last_device_allocations)
+    assert ev.check_records(synth.T0) == 0
+
+
+def test_holdings_reload_and_release_parity(gpu):
+    """A queue, then releases, then a reloaded set with other holdings: the restore states follow every change."""
+    ev, o, cl, rs, al = holding_cluster(300, 1331, devices=True)
+    pods = synth.make_numa_cpuset_pods(300, synth.BASE_SEED + 1332)
+    assert_schedule_equal(ev, o, pods, synth.T0)
+    a1, a0 = ev.last_allocations(), o.last_allocations()
+    for p in np.flatnonzero(a1["node"] >= 0)[::3]:
+        ev.release(pods[p], a1[p], abi.RELEASE_DELETE)
+        o.release(pods[p], a0[p], abi.RELEASE_DELETE)
+    keep = np.arange(len(rs)) % 2 == 0
+    for h in (ev, o):
+        h.reservations_load(rs[keep], al[keep])
+    more = synth.make_numa_cpuset_pods(300, synth.BASE_SEED + 1333, key_base=6_500_000_000)
+    assert_eval_equal(ev.eval(more[:48], synth.T0), o.eval(more[:48], synth.T0))
+    assert_schedule_equal(ev, o, more, synth.T0)
+    assert ev.check_records(synth.T0) == 0
+    assert np.array_equal(ev.reservation_allocs_get(), o.reservation_allocs_get())

@@ -60,6 +60,64 @@ def test_node_topology_delete_clears_zones_and_cpus():
     ev.close()
 
 
+def _bare(tab, zones):
+    """the NRT re-add as the informer delivers it: topology only, no allocation"""
+    t = tab.copy()
+    t["ref_count"], t["exclusive"] = 0, 0
+    z = zones.copy()
+    z["has_allocated"], z["allocated"], z["cpuset_cpus"], z["numa_status"] = 0, 0, 0, 0
+    z["single_pods"], z["shared_pods"] = 0, 0
+    return t, z
+
+
+def test_topology_delete_keeps_node_allocation():
+    """the resource manager's NodeAllocation outlives an NRT delete (topology_options.go:84-88,
+    resource_manager.go keeps nodeAllocations): a bare NRT re-add finds the CPU ref counts / exclusivity and the
+    zones' allocation again, a release during the gap applies to them, and an NRT re-add that carries its own
+    allocation replaces them -- the product and the oracle alike."""
+    cl = synth.make_cluster(12, synth.BASE_SEED + 1208)
+    zones, tabs = synth.make_numa_cpus(cl, synth.BASE_SEED + 1209, cpuset_fraction=(0.6,), max_ref_choices=(2,))
+    ev, o = Evaluator(synth.config(12)), Oracle(synth.config(12), 12)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        synth.load_numa(h, zones)
+        synth.load_cpus(h, tabs)
+    before = [h.node_state(5) for h in (ev, o)]
+    assert (before[0][1]["ref_count"] > 0).any()
+    for h in (ev, o):
+        h.delete_topology(5)
+    # a cpuset pod bound to node 5 before the delete goes away during the gap: its CPUs lose one reference
+    busy = np.flatnonzero(before[0][1]["ref_count"] > 0)
+    gone = before[0][1]["cpu_id"][busy[:3]]
+    alloc = np.zeros(1, abi.POD_ALLOCATION_DTYPE)
+    alloc["node"] = 5
+    for c in gone:
+        alloc["cpuset"][0, c >> 6] |= np.uint64(1) << np.uint64(c & 63)
+    pod = synth.make_pods(1, synth.BASE_SEED + 1210)[0].copy()
+    pod["requests"][2:] = 0
+    for h in (ev, o):
+        h.release(pod, alloc[0], abi.RELEASE_DELETE)
+    t, z = _bare(*tabs[5][:1], zones[5])
+    for h in (ev, o):
+        h.set_numa(5, z)
+        h.set_cpus(5, t, tabs[5][1])
+    want = before[0][1]["ref_count"].copy()
+    want[busy[:3]] -= 1
+    for h, b in zip((ev, o), before):
+        node, cpus, zz, _ = h.node_state(5)
+        assert np.array_equal(cpus["ref_count"], want)
+        keep = want > 0
+        assert np.array_equal(cpus["exclusive"][keep], b[1]["exclusive"][keep])
+        assert np.array_equal(zz["has_allocated"], b[2]["has_allocated"])
+    assert np.array_equal(ev.node_state(5)[2], o.node_state(5)[2])
+    # a re-add carrying an allocation of its own is authoritative
+    for h in (ev, o):
+        h.delete_topology(5)
+        h.set_cpus(5, tabs[5][0], tabs[5][1])
+        assert np.array_equal(h.node_state(5)[1]["ref_count"], before[0][1]["ref_count"])
+    ev.close()
+
+
 @pytest.mark.parametrize("bit", [abi.RSV_HOLDS_NUMA, abi.RSV_HOLDS_CPUSET, abi.RSV_HOLDS_DEVICES,
                                  abi.RSV_OTHER_ALLOCATABLE])
 def test_reservation_holds_refused(bit):
@@ -90,15 +148,19 @@ def test_reservation_holds_refused(bit):
 
 
 def test_matched_refusals_precede_every_segment():
-    """the refusal of a matched reservation on a NUMA-policy node is an argument check, so a queue
-    with plain pods ahead of the matched one fails before the device (here absent: NO_DEVICE would come later)."""
+    """the refusal of a matched reservation holding NUMA resources on a NUMA-policy node is an
+    argument check, so a queue with plain pods ahead of the matched one fails before the device (here absent:
+    NO_DEVICE would come later).  A reservation holding nothing there is not refused."""
     cl = synth.make_cluster(8, synth.BASE_SEED + 1205)
     ev = Evaluator(synth.config(8))
     synth.load_into(ev, cl)
     node = abi.Node.from_buffer_copy(cl.nodes[2].tobytes())
     node.numa_topology_policy = abi.NUMA_POLICY_RESTRICTED
     ev.upsert_node(2, node)
-    ev.reservations_load([abi.Reservation(node=2, available=1), abi.Reservation(node=4, available=1)])
+    al = np.zeros(2, abi.RESERVATION_ALLOC_DTYPE)
+    al["numa"][0, 0] = 2000  # reservation 0 holds NUMA resources on the NUMA-policy node: its matched path is refused
+    rs = [abi.Reservation(node=2, available=1, holds=abi.RSV_HOLDS_NUMA), abi.Reservation(node=4, available=1)]
+    ev.reservations_load(rs, al)
     pods = synth.make_pods(6, synth.BASE_SEED + 1206)
     pods["requests"][:, 2:] = 0
     pods["has_other_requests"] = 0
@@ -117,6 +179,11 @@ def test_matched_refusals_precede_every_segment():
         assert e.value.code == abi.ERR_NO_DEVICE
         with pytest.raises(KoordEvalError) as e:  # without the NUMA-policy node: past the checks, no device here
             ev.schedule(pods, synth.T0, matches=[[], [], [], [], [1], []])
+        assert e.value.code == abi.ERR_NO_DEVICE
+        rs[0].holds = 0  # the same reservations holding nothing: past the checks
+        ev.reservations_load(rs)
+        with pytest.raises(KoordEvalError) as e:
+            ev.schedule(pods, synth.T0, matches=[[], [], [], [], [0, 1], []])
         assert e.value.code == abi.ERR_NO_DEVICE
     ev.close()
 

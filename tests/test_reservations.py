@@ -200,3 +200,90 @@ def test_reservation_filter_golden(case):
     pod["requests"][0][:2] = case["pod"]
     pod["reservation_matched"][0] = abi.RSV_AFFINITY
     assert o.reservation_filter(pod[0], [0], 0) == case["want"]
+
+
+def test_holdings_load_rules():
+    """ke_reservations_load_ex: the holds bits state what the records hold (a mismatch is KE_ERR_INVALID); holdings
+    without their records are refused (KE_ERR_UNSUPPORTED); the records come back with ke_reservation_allocs_get --
+    the product and the oracle alike."""
+    cl = synth.make_cluster(40, synth.BASE_SEED + 1341, amplified_fraction=0.2)
+    zones, tabs = synth.make_numa_cpus(cl, synth.BASE_SEED + 1342)
+    devs = synth.make_devices(40, synth.BASE_SEED + 1343)
+    rs, al = synth.make_reservation_holdings(cl, synth.BASE_SEED + 1344, zones, tabs, devs, frac=0.6)
+    assert len(rs) and (rs["holds"] != 0).any()
+    ev, o = Evaluator(synth.config(40)), Oracle(synth.config(40), 40)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        h.reservations_load(rs, al)
+    assert np.array_equal(ev.reservation_allocs_get(), al)
+    assert np.array_equal(o.reservation_allocs_get(), al)
+    i = int(np.flatnonzero(rs["holds"] != 0)[0])
+    bad = rs.copy()
+    bad["holds"][i] = 0
+    with pytest.raises(KoordEvalError) as e:
+        ev.reservations_load(bad, al)
+    assert e.value.code == abi.ERR_INVALID
+    with pytest.raises(RuntimeError, match=f"rc={abi.ERR_INVALID}"):
+        o.reservations_load(bad, al)
+    with pytest.raises(KoordEvalError) as e:
+        ev.reservations_load(rs)
+    assert e.value.code == abi.ERR_UNSUPPORTED
+    with pytest.raises(RuntimeError, match=f"rc={abi.ERR_UNSUPPORTED}"):
+        o.reservations_load(rs)
+    neg = al.copy()
+    neg["owner_numa"][i, 0] = -1
+    with pytest.raises(KoordEvalError) as e:
+        ev.reservations_load(rs, neg)
+    assert e.value.code == abi.ERR_INVALID
+    ev.close()
+
+
+RESTORE = json.load(open(os.path.join(HERE, "golden", "reservation_restore.json")))["cases"]
+
+
+def _cpus(ids):
+    w = np.zeros(4, np.uint64)
+    for c in ids:
+        w[c >> 6] |= np.uint64(1) << np.uint64(c & 63)
+    return w
+
+
+@pytest.mark.parametrize("case", RESTORE, ids=[c["name"] for c in RESTORE])
+def test_restore_state_golden(case):
+    """The oracle's RestoreReservation state of a matched reservation (or_restore_state) against the reference's own
+    TestRestoreReservation / Test_Plugin_ReservationRestore expectations (tests/golden/reservation_restore.json)."""
+    o = Oracle(synth.config(2), 2)
+    r = np.zeros(1, abi.RESERVATION_DTYPE)
+    a = np.zeros(1, abi.RESERVATION_ALLOC_DTYPE)
+    r["available"] = 1
+    r["allocatable"][0] = [4000, abi.GI if hasattr(abi, "GI") else 2**30]
+    if "reserve_cpuset" in case:
+        r["holds"] = abi.RSV_HOLDS_CPUSET
+        r["allocated_pods"] = len(case["owner_cpusets"])
+        a["cpuset"][0] = _cpus(case["reserve_cpuset"])
+        a["owner_cpuset"][0] = _cpus(sorted({c for s in case["owner_cpusets"] for c in s}))
+    else:
+        r["holds"] = abi.RSV_HOLDS_DEVICES
+        r["allocated_pods"] = 1
+        for m, v in case["reserve_gpu"].items():
+            a["device_minors"][0] |= np.uint64(1) << np.uint64(int(m))
+            a["device"][0, abi.DEV_GPU, int(m)] = v
+        for m, v in case["owner_gpu"].items():
+            a["owner_device_minors"][0] |= np.uint64(1) << np.uint64(int(m))
+            a["owner_device"][0, abi.DEV_GPU, int(m)] = v
+    o.reservations_load(r, a)
+    st = o.restore_state(0)
+    w = case["want"]
+    for k in ("allocatable_cpus", "allocated_cpus", "remained_cpus"):
+        if k in w:
+            assert np.array_equal(st[k], _cpus(w[k])), k
+    if "gpu_allocatable" in w:
+        for key, field in (("gpu_allocatable", "dev_allocatable"), ("gpu_allocated", "dev_allocated"),
+                           ("gpu_remained", "dev_remained")):
+            got = {str(m): st[field][abi.DEV_GPU, m].tolist() for m in range(16) if st[field][abi.DEV_GPU, m].any()}
+            assert got == w[key], key
+        # mergeReservationAllocations over the one matched reservation
+        assert {str(m): st["dev_allocatable"][0, m].tolist() for m in range(16) if st["dev_allocatable"][0, m].any()} \
+            == w["merged_matched_allocatable"]
+        assert {str(m): st["dev_allocated"][0, m].tolist() for m in range(16) if st["dev_allocated"][0, m].any()} \
+            == w["merged_matched_allocated"]
