@@ -158,6 +158,7 @@ def test_topology_delete_readd_keeps_allocation_parity(gpu):
     assert ev.check_records(synth.T0) == 0
     for i in nodes:
         cpus1, cpus0 = ev.node_state(int(i))[1], o.node_state(int(i))[1]
+        cpus1, cpus0 = np.sort(cpus1, order="cpu_id"), np.sort(cpus0, order="cpu_id")  # (table vs id order)
         assert np.array_equal(cpus1["ref_count"], cpus0["ref_count"]), i
         assert cpus1["ref_count"].max(initial=0) <= tabs[i][1], i
     assert sum(int(ev.node_state(int(i))[1]["ref_count"].sum()) for i in nodes) > 0
@@ -170,11 +171,13 @@ def test_refused_call_leaves_no_state(gpu):
     ev, o, cl = _plain(400, 1121)
     node = abi.Node.from_buffer_copy(cl.nodes[7].tobytes())
     node.numa_topology_policy = abi.NUMA_POLICY_BEST_EFFORT
-    rs = [abi.Reservation(node=7, available=1), abi.Reservation(node=9, available=1)]
+    rs = [abi.Reservation(node=7, available=1, holds=abi.RSV_HOLDS_NUMA), abi.Reservation(node=9, available=1)]
     rs[0].allocatable[0], rs[1].allocatable[0] = 4000, 4000
+    al = np.zeros(2, abi.RESERVATION_ALLOC_DTYPE)
+    al["numa"][0, 0] = 4000  # the reserve pod's NUMA resources: the matched path there is refused
     for h in (ev, o):
         h.upsert_node(7, node)
-        h.reservations_load(rs)
+        h.reservations_load(rs, al)
     pods = synth.make_pods(200, synth.BASE_SEED + 1122)
     pods["reservation_matched"][150] = abi.RSV_MATCHED
     pods["qos_class"][150] = abi.QOS_LS  # not a cpuset pod: refused for the reservation's node alone
