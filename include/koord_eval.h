@@ -206,6 +206,9 @@ typedef struct ke_numa_args {
 #define KE_REASON_NUMA_CPU_BIND_POLICY_CONFLICT 24 /* ErrCPUBindPolicyConflict (plugin.go:365-367) */
 #define KE_REASON_NUMA_SMT_ALIGNMENT 25 /* ErrSMTAlignmentError (plugin.go:369-373) */
 #define KE_REASON_NUMA_INSUFFICIENT_CPUS 26 /* allocateCPUSet: "not enough cpus available to satisfy request" */
+#define KE_REASON_RSV_INSUFFICIENT_CPUS 50 /* a pod with a reservation affinity whose matched reservations holding a
+                                              cpuset / NUMA resources satisfy none (tryAllocateFromReservation,
+                                              nodenumaresource/reservation.go:420-422: "Reservation(s) ...") */
 
 /* One logical CPU of a node: CPUTopology.CPUDetails (cpu_topology.go:24-105, built from the NRT's
  * CPU topology, topology_options.go:90-164) + NodeAllocation.allocatedCPUs (node_allocation.go:33-41)

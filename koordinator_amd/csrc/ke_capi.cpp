@@ -16,6 +16,8 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
                 int16_t* la, int16_t* numa, int16_t* ds, int16_t* total, int32_t* best);
 int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t* chosen, int32_t* score);
 int device_rsv_result(Context* ctx, int32_t* out4);
+int device_rsv_views(Context* ctx, const ke_pod& pod, int64_t now, const std::vector<RsvView>& views,
+                     std::vector<RsvViewOut>& out);
 int device_quota_sync(Context* ctx);
 int device_debug_rows(Context* ctx, int32_t n, Row* out);
 int device_set_profiling(Context* ctx, int32_t every);
@@ -115,10 +117,10 @@ static int check_matches(Context& c, const ke_pod* pods, int32_t n) {
     bool scalar = pods[p].has_other_requests || pods[p].has_unsupported_device_requests;
     for (int r = KE_NRES; r < KE_RES_COUNT; r++) scalar = scalar || pods[p].requests[r] != 0;
     for (int r = 0; r < KE_PDR_COUNT; r++) scalar = scalar || pods[p].device_requests[r] != 0;
-    if ((f & (PF_DS | PF_DS_HINT | PF_CPUSET)) || scalar)
-      return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations with device, cpuset or scalar requests");
-    if (pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE || (c.n_bind_nodes > 0 && pods[p].requests[KE_RES_CPU] > 0))
-      return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations with a NUMA policy or that may bind CPUs");
+    if ((f & (PF_DS | PF_DS_HINT)) || scalar)
+      return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations with device or scalar requests");
+    if (pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE)
+      return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations with a NUMA topology policy");
     if (c.dev && device_sharded(&c)) return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations in a sharded context");
     const int rc = resv_check(c, c.match_ids.data() + c.match_off[(size_t)p], cnt);
     if (rc) return rc;
@@ -762,8 +764,14 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
     const int32_t len = s1 - s0;
     const bool rsv = len == 1 && matched(s0);
     if (rsv) {
-      rc = resv_prepare(c, pods[s0], mids.data() + moff[(size_t)s0], moff[(size_t)s0 + 1] - moff[(size_t)s0],
-                        pods[s0].reservation_matched == KE_RSV_AFFINITY);
+      const int32_t* ids = mids.data() + moff[(size_t)s0];
+      const int32_t n_ids = moff[(size_t)s0 + 1] - moff[(size_t)s0];
+      resv_views(c, pods[s0], ids, n_ids);  // allocate-from-reservation trials on the current state first
+      if (!c.rsv_views.empty()) {
+        rc = device_rsv_views(&c, pods[s0], now_ns, c.rsv_views, c.rsv_view_out);
+        if (rc) return rc;
+      }
+      rc = resv_prepare(c, pods[s0], ids, n_ids, pods[s0].reservation_matched == KE_RSV_AFFINITY);
       if (rc) return rc;
     }
     // a device failure leaves the pods of earlier segments Reserved on the device and the context's state

@@ -69,6 +69,9 @@ struct AccLds {
   // ids < n_numa (the byte arrays are zero past them)
   int n_cpu, n_core, n_sock, n_numa;
   int bcast;  // lane 0's result for the wave
+  // takePreferredCPUs' preferredCPUs (cpu_accumulator.go:29-85), has_pref = 0: none (takeCPUs alone)
+  uint8_t pref[ACC_CPUS];
+  int has_pref;
 };
 
 __device__ __forceinline__ int acc_lane() { return (int)threadIdx.x; }

@@ -778,6 +778,55 @@ int resv_check(const Context& c, const int32_t* ids, int32_t n_ids) {
   return KE_OK;
 }
 
+// requestCPUBind of the pod on the node (util.go:121-138): its own cpuset state, else a node CPU bind policy
+// binding a whole-CPU request
+static bool pod_binds_on(const DevPod& dp, const NodeState& ns) {
+  if (dp.flags & PF_NUMA_SKIP) return false;
+  if (dp.flags & PF_CPU_RCB) return true;
+  return dp.req[0] != 0 && ns.node.cpu_bind_policy != KE_NODE_CPU_BIND_NONE && (dp.flags & PF_CPU_INT);
+}
+static bool resv_holds_cpu(const Context& c, int32_t i) {
+  return !c.resv_holds.empty() && (c.resv_holds[(size_t)i] & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET));
+}
+
+void resv_views(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids) {
+  c.rsv_views.clear();
+  c.rsv_view_resv.clear();
+  c.rsv_view_out.clear();
+  if (c.resv_alloc.empty()) return;
+  const DevPod dp = make_dev_pod(c.cfg, pod, pod_hints(c, pod), &c.tmpl);
+  std::vector<char> m(c.resv.size(), 0);
+  for (int32_t j = 0; j < n_ids; j++)
+    if (resv_usable(c.resv[(size_t)ids[j]])) m[(size_t)ids[j]] = 1;
+  std::vector<int32_t> nodes;
+  for (int32_t j = 0; j < n_ids; j++)
+    if (m[(size_t)ids[j]] && resv_holds_cpu(c, ids[j])) nodes.push_back(c.resv[(size_t)ids[j]].node);
+  std::sort(nodes.begin(), nodes.end());
+  nodes.erase(std::unique(nodes.begin(), nodes.end()), nodes.end());
+  for (int32_t node : nodes) {
+    const NodeState& ns = c.nodes[(size_t)node];
+    // a node with a NUMA policy: refused before (resv_check); a pod binding no CPUs there allocates no cpuset
+    if (ns.node.numa_topology_policy != KE_NUMA_POLICY_NONE || !pod_binds_on(dp, ns) || !cpus_valid(ns)) continue;
+    uint64_t merged[4] = {0, 0, 0, 0};  // mergedMatchedAllocatedCPUs: the matched ones' allocatable CPUs
+    for (int32_t i : c.resv_by_node[(size_t)node])
+      if (m[(size_t)i] && resv_holds_cpu(c, i))
+        for (int w = 0; w < 4; w++) merged[w] |= c.resv_alloc[(size_t)i].cpuset[w];
+    for (int32_t i : c.resv_by_node[(size_t)node]) {
+      if (!m[(size_t)i] || !resv_holds_cpu(c, i)) continue;
+      const ke_reservation_alloc& a = c.resv_alloc[(size_t)i];
+      RsvView v{};
+      v.node = node;
+      v.restricted = c.resv[(size_t)i].allocate_policy == KE_RSV_POLICY_RESTRICTED;
+      for (int w = 0; w < 4; w++) {
+        v.pref2[w] = a.cpuset[w] & ~a.owner_cpuset[w];  // remainedCPUs
+        v.pref[w] = merged[w] | v.pref2[w];
+      }
+      c.rsv_views.push_back(v);
+      c.rsv_view_resv.push_back(i);
+    }
+  }
+}
+
 int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids, bool affinity) {
   int rc = resv_check(c, ids, n_ids);  // (ke_schedule's argument checks ran it already: nothing below fails)
   if (rc) return rc;
@@ -785,6 +834,8 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
   c.rsv_pairs.clear();
   c.rsv_nominated.clear();
   c.rsv_nodes.clear();
+  c.rsv_ovr.clear();
+  const DevPod dp = make_dev_pod(c.cfg, pod, pod_hints(c, pod), &c.tmpl);
   std::vector<char> m(c.resv.size(), 0);
   for (int32_t j = 0; j < n_ids; j++)
     if (resv_usable(c.resv[(size_t)ids[j]])) m[(size_t)ids[j]] = 1;
@@ -811,10 +862,24 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
     int32_t mpods = 0;  // the snapshot's len(Pods) delta with this pod's matched reserve pods removed
     resv_delta(c, node, &m, true, mreq, mnz, &mpods);
     const int64_t pods_restored = (int64_t)ns.node.pod_count + mpods;
+    // NodeNUMAResource's FilterNominateReservation (plugin.go:448-504): a binding pod needs a valid CPU topology;
+    // under a reservation affinity a reservation holding a cpuset / NUMA resources needs its trial (k_rsv_views)
+    const bool binds = pod_binds_on(dp, ns);
+    auto view_of = [&](int32_t i) -> int {  // the trial of reservation i here: 1 ok, 0 failed, -1 none
+      for (size_t q = 0; q < c.rsv_views.size(); q++)
+        if (c.rsv_view_resv[q] == i && c.rsv_views[q].node == node) return c.rsv_view_out.size() > q ? c.rsv_view_out[q].ok : 0;
+      return -1;
+    };
+    auto numa_nominable = [&](int32_t i) {
+      if (!binds) return true;
+      if (!cpus_valid(ns)) return false;
+      return !(affinity && view_of(i) == 0);
+    };
     std::vector<int32_t> ok;
     for (int32_t i : mine)
       if (resv_nominable(c.resv[(size_t)i], pod, ns.node.allocatable, pod_requested, all_alloc, affinity, pods_restored,
-                         (int64_t)mine.size(), ns.node.allowed_pods))
+                         (int64_t)mine.size(), ns.node.allowed_pods) &&
+          numa_nominable(i))
         ok.push_back(i);
     // the Reservation Filter with a reservation affinity (plugin.go:316-318, 351-442): a node without matched
     // reservations fails, one with them passes when one of them fits (the same checks as the nomination's)
@@ -847,6 +912,34 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
     }
     c.rsv_pairs.push_back({node, (int16_t)(nom >= 0 ? resv_score(c.resv[(size_t)nom], pod) : 0), (int16_t)allowed, order});
     c.rsv_nominated.push_back(nom);
+    // NodeNUMAResource with the matched reservations first (plugin.go:381-397, 553-563): the Filter's trial
+    // (one satisfied; else "Reservation(s) ..." under an affinity, else the node's own) and Reserve's allocation
+    // (the nominated reservation's when it holds one and is satisfied; failing under an affinity)
+    if (binds && ns.node.numa_topology_policy == KE_NUMA_POLICY_NONE) {
+      RsvOvr o{};
+      o.node = node;
+      bool any_view = false, any_ok = false;
+      for (size_t q = 0; q < c.rsv_views.size(); q++)
+        if (c.rsv_views[q].node == node) {
+          any_view = true;
+          any_ok = any_ok || (c.rsv_view_out.size() > q && c.rsv_view_out[q].ok);
+        }
+      o.filter = (int8_t)(any_ok ? 1 : (any_view && affinity) ? 2 : 0);
+      const int nv = nom >= 0 ? view_of(nom) : -1;
+      if (nom < 0) o.reserve = (int8_t)(affinity ? 2 : 0);  // "no nominated reservation"
+      else if (nv == 1) {
+        o.reserve = 1;
+        for (size_t q = 0; q < c.rsv_views.size(); q++)
+          if (c.rsv_view_resv[q] == nom && c.rsv_views[q].node == node)
+            for (int w = 0; w < 4; w++) o.cpus[w] = c.rsv_view_out[q].cpus[w];
+      } else {
+        o.reserve = (int8_t)(nv == 0 && affinity ? 2 : 0);
+      }
+      if (o.filter || o.reserve) {
+        c.rsv_ovr.push_back(o);
+        ns.rsv_ovr = true;
+      }
+    }
     // the rows this pod sees: its matched reservations restored too, and left out of the plugins' unmatched states
     resv_delta(c, node, &m, true, ns.rv_req, ns.rv_nz, &ns.rv_pods);
     resv_plugin_restore(c, node, &m, ns);
@@ -912,11 +1005,18 @@ void resv_finish(Context& c, int32_t chosen_local, const ke_pod& pod, int32_t* a
       *assumed = 1 + c.rsv_nominated[j];
       resv_owner_update(c, c.rsv_nominated[j], pod, cpuset, numa, dev_minors, +1);
     }
-  for (int32_t node : c.rsv_nodes) resv_node_restore(c, node);
+  for (int32_t node : c.rsv_nodes) {
+    c.nodes[(size_t)node].rsv_ovr = false;
+    resv_node_restore(c, node);
+  }
   c.rsv_affinity = false;
   c.rsv_pairs.clear();
   c.rsv_nominated.clear();
   c.rsv_nodes.clear();
+  c.rsv_ovr.clear();
+  c.rsv_views.clear();
+  c.rsv_view_resv.clear();
+  c.rsv_view_out.clear();
 }
 
 // forgetPod -> RemoveAssignedPod (reservation_info.go:470-482)
@@ -1418,6 +1518,7 @@ void derive_row(const ke_config& cfg, const NodeState& ns, int64_t now, Row* row
   flags |= (uint32_t)n.numa_topology_policy * NF_NUMA_POLICY0;
   flags |= (uint32_t)n.cpu_bind_policy * NF_CPU_BIND0;
   if (cpus_valid(ns)) flags |= NF_CPUS_VALID;
+  if (ns.rsv_ovr) flags |= NF_RSV_CS;
   // GetNUMAAllocateStrategy (util.go:33-47): the node label, else NUMAScoringStrategy's type
   if (n.numa_allocate_strategy == KE_NUMA_ALLOCATE_MOST ||
       (n.numa_allocate_strategy == KE_NUMA_ALLOCATE_DEFAULT && cfg.numa.numa_strategy == KE_STRATEGY_MOST_ALLOCATED))

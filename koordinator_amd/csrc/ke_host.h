@@ -109,6 +109,7 @@ struct NodeState {
   int64_t rv_dev[KE_DEV_TYPES][KE_MAX_MINORS][KE_DKEYS] = {};
   uint64_t rv_dev_keys[KE_DKEYS] = {0, 0, 0};  // bit 16*type + minor per key present
   uint64_t rv_dev_minors = 0;
+  bool rsv_ovr = false;  // the current KE_RSV_MATCHED segment overrides this node's cpuset trial (NF_RSV_CS)
   // derived
   DirtyFlag dirty;              // row must be re-derived and uploaded
   int64_t valid_until = INT64_MAX;  // derived row is exact for now < valid_until
@@ -198,6 +199,11 @@ struct Context {
   std::vector<RsvPair> rsv_pairs;
   std::vector<int32_t> rsv_nominated;
   bool rsv_affinity = false;  // the segment's pod has a required reservation affinity
+  std::vector<RsvOvr> rsv_ovr;  // its allocate-from-reservation decisions per node (SoA::rovr)
+  // its allocate-from-reservation trials (resv_views -> k_rsv_views): per view the reservation and the outcome
+  std::vector<RsvView> rsv_views;
+  std::vector<int32_t> rsv_view_resv;
+  std::vector<RsvViewOut> rsv_view_out;
   std::vector<int32_t> last_resv;  // per pod of the last ke_schedule: 1 + the reservation assumed, 0 = none
   int32_t resv_gen = 0;            // ke_reservations_generation: bumped by every load_reservations
   // per-pod latency of the last ke_schedule (ke_last_pod_latencies): the call's entry on the host clock, and
@@ -297,6 +303,9 @@ int32_t resv_score(const ke_reservation& r, const ke_pod& pod);
 // the nominated-reservation path of one KE_RSV_MATCHED pod: rows with its matched restore, rsv_pairs /
 // rsv_nominated; resv_finish assumes the pod into the chosen node's nominated reservation (1 + index, 0)
 int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids, bool affinity);
+// the allocate-from-reservation trials a KE_RSV_MATCHED pod needs (into c.rsv_views / rsv_view_resv): per node of
+// its matched reservations holding a cpuset / NUMA resources where the pod binds CPUs, one per such reservation
+void resv_views(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids);
 // the refusals of resv_prepare, checked for every pod before a ke_schedule call schedules any
 int resv_check(const Context& c, const int32_t* ids, int32_t n_ids);
 void resv_finish(Context& c, int32_t chosen_local, const ke_pod& pod, int32_t* assumed, const uint64_t* cpuset = nullptr,

@@ -81,7 +81,15 @@ struct SoA {
   int64_t* dsx;
   const DevPodHint* ph;
   int8_t* vfo;
+  // a KE_RSV_MATCHED segment's allocate-from-reservation decisions (RsvOvr) for its NF_RSV_CS nodes
+  const RsvOvr* rovr;
+  int32_t n_rovr;
 };
+__device__ __forceinline__ const RsvOvr* rsv_ovr_of(const SoA& s, int64_t node) {
+  for (int q = 0; q < s.n_rovr; q++)
+    if (s.rovr[q].node == node) return &s.rovr[q];
+  return nullptr;
+}
 constexpr int DSB_MAX = 0, DSB_CNT = 64, DSB_CUT = 128, DSB_WORDS = 129;
 // kerr bits: an input the kernels refuse mid-call (the call returns KE_ERR_UNSUPPORTED)
 constexpr int32_t KERR_HINT_ROUTE = 2;  // a hinted pod reached a kernel instantiated without the hint path (H)
@@ -2387,6 +2395,14 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
       } else if (req == XB_FULL && ncpu % cs_cpc(cnt) != 0) {
         o.status = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
         o.reason = KE_REASON_NUMA_SMT_ALIGNMENT;
+      } else if (req != XB_NONE && eff_pol == KE_NUMA_POLICY_NONE && (nf & NF_RSV_CS) &&
+                 rsv_ovr_of(s, i) && rsv_ovr_of(s, i)->filter != 0) {
+        // the matched pod's reservations first (plugin.go:381-390): satisfied by one (k_rsv_views), or none under
+        // a reservation affinity ("Reservation(s) ...", reservation.go:420-422)
+        if (rsv_ovr_of(s, i)->filter == 2) {
+          o.status = KE_CODE_UNSCHEDULABLE;
+          o.reason = KE_REASON_RSV_INSUFFICIENT_CPUS;
+        }
       } else if (req != XB_NONE && eff_pol == KE_NUMA_POLICY_NONE &&
                  ncpu > (req == XB_FULL ? cs_full(cnt) : cs_spread(cnt))) {
         o.status = KE_CODE_UNSCHEDULABLE;
@@ -5471,11 +5487,13 @@ __device__ void reserve_row(const SoA& s, int64_t node, uint32_t nf, const DevPo
 // One takePreferredCPUs call (no preferred CPUs = takeCPUs, cpu_accumulator.go:29-85) over the CPUs of
 // `a.base` in NUMA id `zone` (-1 = all) not yet in `a.uni`, from the pre-pod exclusivity; adds the
 // result to a.uni.  needed <= 0 takes nothing.  All lanes (ke_cpuacc.h).
-__device__ bool cpuset_take(AccLds& a, int zone, int needed, int bind) {
+__device__ bool cpuset_take1(AccLds& a, int zone, int needed, int bind, int pref_sel) {
   if (needed <= 0) return true;
   const int L = threadIdx.x;
   for (int c = L; c < a.n_cpu; c += 64) {
-    a.alloc[c] = a.base[c] && !a.uni[c] && (zone < 0 || a.cpu[c].numa == zone);
+    // pref_sel: 0 every available CPU, 1 the preferred ones, 2 the others (availableCPUs.Difference(preferred))
+    const bool sel = pref_sel == 0 || (pref_sel == 1) == (a.pref[c] != 0);
+    a.alloc[c] = a.base[c] && !a.uni[c] && (zone < 0 || a.cpu[c].numa == zone) && sel;
     a.res[c] = 0;
   }
   for (int k = L; k < a.n_core; k += 64) a.ex_core[k] = a.ex_core0[k];
@@ -5486,6 +5504,24 @@ __device__ bool cpuset_take(AccLds& a, int zone, int needed, int bind) {
   for (int c = L; c < a.n_cpu; c += 64) a.uni[c] |= a.res[c];
   __syncthreads();
   return true;
+}
+__device__ bool cpuset_take(AccLds& a, int zone, int needed, int bind) {
+  if (!a.has_pref) return cpuset_take1(a, zone, needed, bind, 0);
+  // takePreferredCPUs: min(needed, |available ∩ preferred|) from the preferred ones, the rest from the others
+  int np = 0, before = 0;
+  for (int c = threadIdx.x; c < a.n_cpu; c += 64) {
+    np += a.base[c] && !a.uni[c] && (zone < 0 || a.cpu[c].numa == zone) && a.pref[c];
+    before += a.uni[c];
+  }
+  np = acc_wave_sum(np);
+  before = acc_wave_sum(before);
+  if (np > 0) {
+    if (!cpuset_take1(a, zone, min(needed, np), bind, 1)) return false;
+    int got = 0;
+    for (int c = threadIdx.x; c < a.n_cpu; c += 64) got += a.uni[c];
+    needed -= acc_wave_sum(got) - before;
+  }
+  return cpuset_take1(a, zone, needed, bind, np > 0 ? 2 : 0);
 }
 
 // allocateCPUSet (resource_manager.go:353-459) over the node's CPU table in LDS: getAvailableCPUs, the
@@ -5669,6 +5705,70 @@ __device__ void cpuset_commit_wave(const SoA& s, AccLds& a, CsrShared& sh, int l
   }
 }
 
+// The allocate-from-reservation trials of one KE_RSV_MATCHED pod (pods[0]) on the nodes of its matched reservations
+// that hold a cpuset / NUMA resources (nodenumaresource/reservation.go:270-424; the node has no NUMA policy, so
+// Allocate is allocateCPUSet alone): one workgroup per view, allocateCPUSet over the node's CPU table with
+// RefCount-- on the view's preferredCPUs (getAvailableCPUs(preferred), node_allocation.go:192-219) and
+// takePreferredCPUs; a Restricted reservation's view then needs numCPUsNeeded <= |remainedCPUs| and a second
+// allocation preferring only them, whose cpuset may not outgrow them.
+__global__ __launch_bounds__(64) void k_rsv_views(SoA s, const DevPod* __restrict__ pods, const RsvView* __restrict__ views,
+                                                  RsvViewOut* __restrict__ out) {
+  __shared__ AccLds a;
+  __shared__ int s_ok;
+  const RsvView v = views[blockIdx.x];
+  const DevPod pod = pods[0];
+  const int L = threadIdx.x;
+  const uint32_t nf = s.flags[v.node];
+  const int64_t ncpu = pod.req[0] / 1000;
+  bool ok = s.cpu != nullptr && (nf & NF_CPUS_VALID);
+  for (int pass = 0; pass < (v.restricted ? 2 : 1) && ok; pass++) {
+    const uint64_t* pw = pass ? v.pref2 : v.pref;
+    if (pass) {  // Restricted: numCPUsNeeded > reservedCPUs.Size() fails the reservation
+      int nrem = 0;
+      for (int w = 0; w < 4; w++) nrem += __popcll(v.pref2[w]);
+      if (ncpu > nrem) {
+        ok = false;
+        break;
+      }
+    }
+    const CpuRec* recs = s.cpu + (int64_t)v.node * CPU_SLOTS;
+    int top_cpu = 0, top_numa = 0;
+    for (int c = L; c < CPU_SLOTS; c += 64) {
+      CpuRec r = recs[c];
+      const bool p = (pw[c >> 6] >> (c & 63)) & 1;
+      if (p && r.ref > 0 && --r.ref == 0) r.excl = KE_CPU_EXCL_NONE;  // the CPU leaves allocateInfo at 0
+      a.cpu[c] = r;
+      a.alloc[c] = a.res[c] = a.base[c] = a.uni[c] = a.mark[c] = 0;
+      a.pref[c] = p;
+      if (r.flags & CR_VALID) top_cpu = c + 1, top_numa = max(top_numa, (int)r.numa + 1);
+    }
+    top_cpu = (int)wave_max_u32((uint32_t)top_cpu);
+    top_numa = (int)wave_max_u32((uint32_t)top_numa);
+    if (L == 0) a.n_cpu = top_cpu, a.n_numa = top_numa, a.has_pref = 1;
+    __syncthreads();
+    const int64_t zcpu[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bool took = cpuset_allocate(s, v.node, nf, pod, a, 0u, zcpu);
+    if (L == 0) s_ok = took;
+    __syncthreads();
+    ok = s_ok != 0;
+    if (ok && pass) {  // result.CPUSet.Size() > reservedCPUs.Size()
+      int n = 0, nrem = 0;
+      for (int c = L; c < a.n_cpu; c += 64) n += a.res[c];
+      n = acc_wave_sum(n);
+      for (int w = 0; w < 4; w++) nrem += __popcll(v.pref2[w]);
+      ok = n <= nrem;
+    }
+  }
+  uint64_t w4[4] = {0, 0, 0, 0};
+  if (ok)
+    for (int c = 0; c < CPU_SLOTS; c++)
+      if (a.res[c]) w4[c >> 6] |= 1ull << (c & 63);
+  if (L == 0) {
+    out[blockIdx.x].ok = ok ? 1 : 0;
+    for (int w = 0; w < 4; w++) out[blockIdx.x].cpus[w] = w4[w];
+  }
+}
+
 // A singleton batch of a pod that may bind CPUs, after k_select: selectHost's node, then Reserve in
 // profile order — LoadAware, NodeNUMAResource (the NUMA allocation on the affinity Admit picks and the
 // cpuset; a failed Allocate fails Reserve and the pod stays unplaced), DeviceShare.  One thread: the
@@ -5700,12 +5800,12 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
       for (int c = threadIdx.x; c < CPU_SLOTS; c += 64) {
         const CpuRec r = recs[c];
         a.cpu[c] = r;
-        a.alloc[c] = a.res[c] = a.base[c] = a.uni[c] = a.mark[c] = 0;
+        a.alloc[c] = a.res[c] = a.base[c] = a.uni[c] = a.mark[c] = a.pref[c] = 0;
         if (r.flags & CR_VALID) top_cpu = c + 1, top_numa = max(top_numa, (int)r.numa + 1);
       }
       top_cpu = (int)wave_max_u32((uint32_t)top_cpu);
       top_numa = (int)wave_max_u32((uint32_t)top_numa);
-      if (threadIdx.x == 0) a.n_cpu = top_cpu, a.n_numa = top_numa;
+      if (threadIdx.x == 0) a.n_cpu = top_cpu, a.n_numa = top_numa, a.has_pref = 0;
     }
     __syncthreads();
   }
@@ -5803,7 +5903,14 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
     }
   }
   __syncthreads();
-  if (sh.take) {  // the accumulator on the whole wave
+  // a KE_RSV_MATCHED pod on a node without a NUMA policy: NodeNUMAResource Reserve allocates from the nominated
+  // reservation first (allocateWithNominatedReservation, reservation.go:492-522), as k_rsv_views computed it
+  const RsvOvr* ro = (sh.take && sh.zmask == 0 && (sh.nf & NF_RSV_CS)) ? rsv_ovr_of(s, sh.node) : nullptr;
+  if (ro && ro->reserve != 0) {
+    for (int c = lane; c < CPU_SLOTS; c += 64) a.res[c] = (ro->cpus[c >> 6] >> (c & 63)) & 1;
+    __syncthreads();
+    if (lane == 0) ok = ro->reserve == 1;
+  } else if (sh.take) {  // the accumulator on the whole wave
     const bool took = cpuset_allocate(s, sh.node, sh.nf, pod, a, sh.zmask, sh.zcpu);
     if (lane == 0) ok = took;
   }
@@ -6027,6 +6134,10 @@ struct DeviceState {
   // the Reservation plugin of a singleton batch (k_rsv_pick): its pairs and result words
   RsvPair* d_rsv = nullptr;
   int64_t rsv_cap = 0;              // bytes
+  void* d_rsv_views = nullptr;      // k_rsv_views: views, outputs, the pod
+  int64_t rsv_views_cap = 0;
+  RsvOvr* d_rovr = nullptr;         // the segment's allocate-from-reservation decisions (SoA::rovr)
+  int64_t rovr_cap = 0;
   int32_t* d_rsv_out = nullptr;     // [4]
 };
 
@@ -6114,6 +6225,34 @@ int device_create(Context* ctx) {
   HIP_OK(hipMalloc(&d->d_aff, d->capacity));
   HIP_OK(hipMalloc(&d->d_split, sizeof(uint32_t) * GATH_WORDS_MAX * MAX_WORLD));
   HIP_OK(hipMalloc(&d->d_rsv_out, sizeof(int32_t) * 4));
+  HIP_OK(hipStreamSynchronize(d->stream));
+  return KE_OK;
+}
+
+int device_refresh(Context* ctx, int64_t now);
+// k_rsv_views for one KE_RSV_MATCHED pod: the allocate-from-reservation trials `views` on the current device
+// state (synchronous; the segment's device_schedule follows)
+int device_rsv_views(Context* ctx, const ke_pod& pod, int64_t now, const std::vector<RsvView>& views,
+                     std::vector<RsvViewOut>& out) {
+  DeviceState* d = ctx->dev;
+  out.assign(views.size(), RsvViewOut{});
+  if (views.empty()) return KE_OK;
+  HIP_OK(hipSetDevice(d->device));
+  int rc = device_refresh(ctx, now);  // the rows / CPU tables as the segment will see them
+  if (rc) return rc;
+  for (const RsvView& v : views)
+    if (v.node < 0 || v.node >= ctx->n_nodes) return fail(KE_ERR_DEVICE, "reservation view node out of range");
+  const DevPod dp = make_dev_pod(ctx->cfg, pod, pod_hints(*ctx, pod), &ctx->tmpl);
+  const size_t vb = sizeof(RsvView) * views.size(), ob = sizeof(RsvViewOut) * views.size();
+  rc = ensure((void**)&d->d_rsv_views, &d->rsv_views_cap, (int64_t)(vb + ob + sizeof(DevPod)));
+  if (rc) return rc;
+  uint8_t* base = (uint8_t*)d->d_rsv_views;
+  HIP_OK(hipMemcpyAsync(base, views.data(), vb, hipMemcpyHostToDevice, d->stream));
+  HIP_OK(hipMemcpyAsync(base + vb + ob, &dp, sizeof(DevPod), hipMemcpyHostToDevice, d->stream));
+  hipLaunchKernelGGL(k_rsv_views, dim3((unsigned)views.size()), dim3(64), 0, d->stream, d->soa,
+                     (const DevPod*)(base + vb + ob), (const RsvView*)base, (RsvViewOut*)(base + vb));
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(out.data(), base + vb, ob, hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipStreamSynchronize(d->stream));
   return KE_OK;
 }
@@ -6754,6 +6893,15 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
       HIP_OK(hipMemcpyAsync(d->d_rsv, ctx->rsv_pairs.data(), sizeof(RsvPair) * ctx->rsv_pairs.size(),
                             hipMemcpyHostToDevice, d->stream));
     HIP_OK(hipMemsetAsync(d->d_rsv_out, 0xFF, sizeof(int32_t) * 4, d->stream));
+  }
+  d->soa.n_rovr = 0;  // a matched pod's allocate-from-reservation decisions (NF_RSV_CS rows read them)
+  if (!ctx->rsv_ovr.empty()) {
+    rc = ensure((void**)&d->d_rovr, &d->rovr_cap, (int64_t)sizeof(RsvOvr) * (int64_t)ctx->rsv_ovr.size());
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(d->d_rovr, ctx->rsv_ovr.data(), sizeof(RsvOvr) * ctx->rsv_ovr.size(), hipMemcpyHostToDevice,
+                          d->stream));
+    d->soa.rovr = d->d_rovr;
+    d->soa.n_rovr = (int32_t)ctx->rsv_ovr.size();
   }
   const bool quota = !ctx->quotas.empty();  // ElasticQuota admission + Reserve in the Reserve kernels
   if (quota) {

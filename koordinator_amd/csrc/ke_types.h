@@ -57,6 +57,30 @@ enum NodeFlag : uint32_t {
   NF_CPU_BIND0 = 1u << 20,        // 2 bits: the node's CPU bind policy (KE_NODE_CPU_BIND_*)
   NF_CPUS_VALID = 1u << 22,       // the node has a valid CPU topology table (cpuset pods can bind)
   NF_CPU_NUMA_MOST = 1u << 23,    // GetNUMAAllocateStrategy == MostAllocated (cpu accumulator order)
+  NF_RSV_CS = 1u << 24,           // the current KE_RSV_MATCHED pod's allocate-from-reservation outcome on this node
+                                  // is in SoA::rovr (RsvOvr): it replaces the cpuset trial / allocation
+};
+// A KE_RSV_MATCHED pod's allocate-from-reservation trial on one node (k_rsv_views): takePreferredCPUs with
+// preferredCPUs `pref` (getAvailableCPUs(preferred): RefCount-- on each, nodenumaresource/reservation.go:303-339),
+// and for a Restricted reservation a second allocation with `pref2` = its remainedCPUs (:340-417).
+struct RsvView {
+  int32_t node;
+  int32_t restricted;  // 1: Restricted (numCPUsNeeded <= |pref2|, a second allocation on pref2)
+  uint64_t pref[4];
+  uint64_t pref2[4];
+};
+struct RsvViewOut {
+  int32_t ok, pad;
+  uint64_t cpus[4];
+};
+// The decisions the host takes from them per node (ke_host.cpp resv_prepare): the Filter's trial allocation
+// (0 = the node's own, 1 = satisfied from a reservation, 2 = "Reservation(s) ..." Unschedulable) and Reserve's
+// (0 = the node's own allocation, 1 = `cpus` from the nominated reservation, 2 = Reserve fails)
+struct RsvOvr {
+  int32_t node;
+  int8_t filter, reserve;
+  int16_t pad;
+  uint64_t cpus[4];
 };
 KE_HD inline int nf_cpu_bind(uint32_t f) { return (int)((f >> 20) & 3u); }
 KE_HD inline int nf_numa_policy(uint32_t f) { return (int)((f >> 16) & 3u); }

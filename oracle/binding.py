@@ -70,6 +70,7 @@ def load():
         "or_reservations_get": (C.c_int, [V, i32, V]),
         "or_reservations_load_ex": (C.c_int, [V, i32, V, V]),
         "or_restore_state": (C.c_int, [V, i32, V]),
+        "or_numa_reserve_from_rsv": (C.c_int, [V, V, i32, V, i32, i32, i32, V]),
         "or_reservation_allocs_get": (C.c_int, [V, i32, V]),
         "or_pod_reservations": (C.c_int, [V, i32, V, V]),
         "or_last_reservations": (C.c_int, [V, i32, V]),
@@ -296,6 +297,15 @@ class Oracle:
         if rc != 0:
             raise RuntimeError(f"oracle reservations_load rc={rc}")
         self._n_resv = len(r)
+
+    def numa_reserve_from_rsv(self, pod, node, ids, nom, required):
+        """NodeNUMAResource Reserve's allocate-from-reservation (or_numa_reserve_from_rsv): (code, cpuset words)."""
+        p = as_pod_array([pod] if isinstance(pod, abi.Pod) else np.asarray(pod).reshape(1))
+        ids = np.ascontiguousarray(ids, np.int32)
+        out = np.zeros(4, np.uint64)
+        rc = self.lib.or_numa_reserve_from_rsv(self.h, abi.ptr(p), int(node), abi.ptr(ids), len(ids), int(nom),
+                                               int(required), abi.ptr(out))
+        return rc, out
 
     def restore_state(self, r):
         """RestoreReservation's matched state of reservation r (or_restore_state): a RSV_STATE_DTYPE record."""

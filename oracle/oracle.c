@@ -494,14 +494,6 @@ static int64_t cpus_allocated_count(const or_node* n) {
   return k;
 }
 
-/* NodeAllocation.getAvailableCPUs (node_allocation.go:192-219) without preferred CPUs */
-static void cpus_available(const or_cpus* x, uint64_t* avail) {
-  memset(avail, 0, sizeof(uint64_t) * ACC_WORDS);
-  for (int c = 0; c < ACC_MAX_CPUS; c++)
-    if (x->t.valid[c] && !x->reserved[c] && !(x->al.present[c] && x->al.ref[c] >= x->max_ref))
-      avail[c >> 6] |= 1ull << (c & 63);
-}
-
 /* getCPUBindPolicy (util.go:101-119): the policy and whether it is required */
 static int cpu_bind_policy_of(const cpuset_state* st, int node_bind, int* required) {
   if (st->required != KE_CPU_BIND_UNSET) {
@@ -557,6 +549,11 @@ typedef struct numa_cs {
   int avail_total;
   int zcnt[KE_MAX_NUMA];
   uint64_t avail[ACC_WORDS];
+  /* ResourceOptions.preferredCPUs (reservations) and the allocateInfo getAvailableCPUs returns with them
+   * (RefCount-- per preferred CPU, dropped at 0); has_pref = 0: the node's own allocation, no preferred CPUs */
+  int has_pref;
+  uint64_t pref[ACC_WORDS];
+  acc_alloc al;
 } numa_cs;
 
 static int exact_cpusets = 0; /* hints / admit run the CPU accumulator itself instead of its counts */
@@ -568,7 +565,14 @@ static int popcount_set(const uint64_t* s) {
   return n;
 }
 
+static void numa_cs_build_pref(const or_cluster* c, const or_node* n, const ke_pod* pod, numa_cs* cs,
+                               const uint64_t* pref);
 static void numa_cs_build(const or_cluster* c, const or_node* n, const ke_pod* pod, numa_cs* cs) {
+  numa_cs_build_pref(c, n, pod, cs, NULL);
+}
+/* with ResourceOptions.preferredCPUs: getAvailableCPUs(preferredCPUs) (node_allocation.go:192-219) */
+static void numa_cs_build_pref(const or_cluster* c, const or_node* n, const ke_pod* pod, numa_cs* cs,
+                               const uint64_t* pref) {
   memset(cs, 0, sizeof *cs);
   cpuset_state st;
   cpuset_prefilter(c, pod, &st);
@@ -582,7 +586,20 @@ static void numa_cs_build(const or_cluster* c, const or_node* n, const ke_pod* p
   if (!cs->valid) return;
   const or_cpus* x = n->cpus;
   cs->cpc = acc_cpus_per_core(&x->t);
-  cpus_available(x, cs->avail);
+  cs->al = x->al;
+  if (pref) {
+    cs->has_pref = 1;
+    memcpy(cs->pref, pref, sizeof cs->pref);
+    for (int c1 = 0; c1 < ACC_MAX_CPUS; c1++)
+      if ((pref[c1 >> 6] >> (c1 & 63) & 1) && cs->al.present[c1] && --cs->al.ref[c1] == 0) {
+        cs->al.present[c1] = 0;
+        cs->al.excl[c1] = 0;
+      }
+  }
+  memset(cs->avail, 0, sizeof cs->avail);
+  for (int c1 = 0; c1 < ACC_MAX_CPUS; c1++)
+    if (x->t.valid[c1] && !x->reserved[c1] && !(cs->al.present[c1] && cs->al.ref[c1] >= x->max_ref))
+      cs->avail[c1 >> 6] |= 1ull << (c1 & 63);
   if (cs->required) { /* filterCPUsByRequiredCPUBindPolicy (:655-695) */
     uint64_t keep[ACC_WORDS] = {0};
     for (int c1 = 0; c1 < ACC_MAX_CPUS; c1++) {
@@ -639,7 +656,8 @@ static int cpuset_allocate_cs(const or_node* n, const numa_cs* cs, const numa_vi
     int k = popcount_set(az);
     const int want = (int)(dist[z][KE_RES_CPU] / 1000);
     if (want < k) k = want;
-    if (acc_take_preferred_cpus(&x->t, x->max_ref, az, NULL, &x->al, k, acc_bind(cs->bind), cs->excl, cs->numa_most, got) != 0)
+    if (acc_take_preferred_cpus(&x->t, x->max_ref, az, cs->has_pref ? cs->pref : NULL, &cs->al, k, acc_bind(cs->bind),
+                                cs->excl, cs->numa_most, got) != 0)
       return -1;
     for (int w = 0; w < ACC_WORDS; w++) result[w] |= got[w];
   }
@@ -650,8 +668,8 @@ static int cpuset_allocate_cs(const or_node* n, const numa_cs* cs, const numa_vi
   if (needed > 0) {
     uint64_t rest[ACC_WORDS], got[ACC_WORDS];
     for (int w = 0; w < ACC_WORDS; w++) rest[w] = cs->avail[w] & ~result[w];
-    if (acc_take_preferred_cpus(&x->t, x->max_ref, rest, NULL, &x->al, needed, acc_bind(cs->bind), cs->excl, cs->numa_most,
-                                got) != 0)
+    if (acc_take_preferred_cpus(&x->t, x->max_ref, rest, cs->has_pref ? cs->pref : NULL, &cs->al, needed,
+                                acc_bind(cs->bind), cs->excl, cs->numa_most, got) != 0)
       return -1;
     for (int w = 0; w < ACC_WORDS; w++) result[w] |= got[w];
   }
@@ -663,7 +681,7 @@ static int cpuset_allocate_cs(const or_node* n, const numa_cs* cs, const numa_vi
  * multiple of CPUs per core (whole cores are all a zone offers then); SpreadByPCPUs offers one CPU per
  * core.  Verified against cpuset_allocate_cs by tests/test_oracle_cpuset_numa.py. */
 static int cpuset_fits_cs(const or_node* n, const numa_cs* cs, const numa_view* v, const int64_t (*dist)[KE_NRES]) {
-  if (exact_cpusets) {
+  if (exact_cpusets || cs->has_pref) {
     uint64_t r[ACC_WORDS];
     return cpuset_allocate_cs(n, cs, v, dist, r) == 0;
   }
@@ -689,6 +707,69 @@ static int cpuset_allocate(const or_cluster* c, const or_node* n, const ke_pod* 
   numa_cs cs;
   numa_cs_build(c, n, pod, &cs);
   return cpuset_allocate_cs(n, &cs, NULL, NULL, result);
+}
+/* ... with ResourceOptions.preferredCPUs */
+static int cpuset_allocate_pref(const or_cluster* c, const or_node* n, const ke_pod* pod, const uint64_t* pref,
+                                uint64_t* result) {
+  numa_cs cs;
+  numa_cs_build_pref(c, n, pod, &cs, pref);
+  return cpuset_allocate_cs(n, &cs, NULL, NULL, result);
+}
+
+static int or_holds_of_idx(const or_cluster* c, int32_t r);
+
+/* NodeNUMAResource's allocate-from-reservation for a binding pod on a node without a NUMA policy
+ * (tryAllocateFromReservation, nodenumaresource/reservation.go:270-424; the hint is empty, so Allocate is
+ * allocateCPUSet alone and the NUMA restore states do not enter): over RestoreReservation's matched set --
+ * the pod's matched reservations (c->resv_m) on the node whose reserve pod holds NUMA resources or a cpuset
+ * -- or only reservation `only` (the nominated one, allocateWithNominatedReservation :492-522, and
+ * FilterNominateReservation, plugin.go:448-504), each with
+ *   preferredCPUs = mergedMatchedAllocatedCPUs (the matched reservations' allocatedCPUs, i.e. their
+ *                   allocatable CPUs: or_restore_state) ∪ its remainedCPUs;
+ *   Default / Aligned: one Allocate;  Restricted: that Allocate, then numCPUsNeeded <= |remainedCPUs|, then an
+ *   Allocate with preferredCPUs = remainedCPUs whose cpuset may not outgrow them.
+ * The first satisfied one (ascending index; Go ranges over a map, so only whether one is satisfied is the
+ * reference's -- the Filter's question) gives 1 and its cpuset; none: -1 with requiredFromReservation (the
+ * Filter's "Reservation(s) ..." Unschedulable), else 0 (nil: the node itself, tryAllocateFromNode).  An empty
+ * matched set gives 0 whatever the requirement. */
+static int or_numa_from_rsv(const or_cluster* c, const ke_pod* pod, int32_t node, int32_t only, int required,
+                            uint64_t* out) {
+  const or_node* n = &c->nodes[node];
+  uint64_t merged[ACC_WORDS] = {0};
+  int any = 0;
+  for (int32_t r = 0; c->resv_m && c->ralloc && r < c->n_resv; r++) {
+    if (!c->resv_m[r] || c->resv[r].node != node || !(or_holds_of_idx(c, r) & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)))
+      continue;
+    any = 1;
+    for (int w = 0; w < ACC_WORDS; w++) merged[w] |= c->ralloc[r].cpuset[w];
+  }
+  if (!any) return 0;
+  if (only >= 0 && !(c->resv_m[only] && c->resv[only].node == node &&
+                     (or_holds_of_idx(c, only) & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET))))
+    return 0; /* "nominated reservation doesn't reserve numa resource or cpuset" */
+  for (int32_t r = 0; r < c->n_resv; r++) {
+    if (only >= 0 ? r != only : !(c->resv_m[r] && c->resv[r].node == node &&
+                                  (or_holds_of_idx(c, r) & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET))))
+      continue;
+    const ke_reservation_alloc* a = &c->ralloc[r];
+    uint64_t rem[ACC_WORDS], pref[ACC_WORDS], got[ACC_WORDS];
+    for (int w = 0; w < ACC_WORDS; w++) {
+      rem[w] = a->cpuset[w] & ~a->owner_cpuset[w];
+      pref[w] = merged[w] | rem[w];
+    }
+    if (cpuset_allocate_pref(c, n, pod, pref, got) != 0) continue;
+    if (c->resv[r].allocate_policy == KE_RSV_POLICY_RESTRICTED) {
+      cpuset_state st;
+      cpuset_prefilter(c, pod, &st);
+      const int reserved = popcount_set(rem);
+      if (st.num_cpus > reserved) continue; /* numCPUsNeeded > reservedCPUs.Size() */
+      if (cpuset_allocate_pref(c, n, pod, rem, got) != 0) continue;
+      if (popcount_set(got) > reserved) continue;
+    }
+    memcpy(out, got, sizeof got);
+    return 1;
+  }
+  return required ? -1 : 0;
 }
 
 /* ---------------------------------------------------------------------------------------------- */
@@ -875,6 +956,13 @@ static int numa_filter_aff(const or_cluster* c, const ke_pod* pod, int32_t node,
     }
     if (required != KE_CPU_BIND_UNSET && policy == KE_NUMA_POLICY_NONE) { /* trial Allocate */
       uint64_t cs[ACC_WORDS];
+      /* from the matched reservations first (plugin.go:381-390), then the node (tryAllocateFromNode) */
+      const int fr = or_numa_from_rsv(c, pod, node, -1, pod->reservation_matched == KE_RSV_AFFINITY, cs);
+      if (fr < 0) {
+        *reason = KE_REASON_RSV_INSUFFICIENT_CPUS;
+        return KE_CODE_UNSCHEDULABLE;
+      }
+      if (fr > 0) return KE_CODE_SUCCESS;
       if (cpuset_allocate(c, n, pod, cs) != 0) {
         *reason = KE_REASON_NUMA_INSUFFICIENT_CPUS;
         return KE_CODE_UNSCHEDULABLE;
@@ -3158,6 +3246,8 @@ int or_restore_state(const or_cluster* c, int32_t r, or_rsv_state* out) {
   return KE_OK;
 }
 
+static uint8_t or_holds_of(const ke_reservation_alloc* a);
+static int or_holds_of_idx(const or_cluster* c, int32_t r) { return c->ralloc ? or_holds_of(&c->ralloc[r]) : 0; }
 static uint8_t or_holds_of(const ke_reservation_alloc* a) {
   uint8_t h = 0;
   for (int j = 0; j < KE_MAX_NUMA * KE_NRES; j++)
@@ -3371,7 +3461,14 @@ typedef struct reserve_plan {
   int excl;
 } reserve_plan;
 
-static int or_reserve_plan(const or_cluster* c, const ke_pod* pod, int32_t node, reserve_plan* rp) {
+static int or_numa_from_rsv(const or_cluster* c, const ke_pod* pod, int32_t node, int32_t only, int required,
+                            uint64_t* out);
+/* nom_r: the reservation the Reservation plugin nominated on the node for a KE_RSV_MATCHED pod (-1 = none; the
+ * pod's matched flags in c->resv_m): NodeNUMAResource Reserve allocates from it first
+ * (allocateWithNominatedReservation, nodenumaresource/reservation.go:492-522) -- a binding pod on a node without
+ * a NUMA policy; a binding pod with a reservation affinity and no nominated reservation fails ("no nominated
+ * reservation", :508-513) */
+static int or_reserve_plan(const or_cluster* c, const ke_pod* pod, int32_t node, reserve_plan* rp, int32_t nom_r) {
   const or_node* n = &c->nodes[node];
   memset(rp, 0, sizeof *rp);
   if (pod_requests_zero(pod)) return 0;
@@ -3381,6 +3478,15 @@ static int or_reserve_plan(const or_cluster* c, const ke_pod* pod, int32_t node,
   numa_cs_build(c, n, pod, &cs);
   rp->excl = cs.excl;
   if (cs.rcb && !cs.valid) return -1;
+  if (c->resv_m && cs.rcb && policy == KE_NUMA_POLICY_NONE) {
+    const int required = pod->reservation_matched == KE_RSV_AFFINITY;
+    if (nom_r < 0 && required) return -1;
+    if (nom_r >= 0) {
+      const int fr = or_numa_from_rsv(c, pod, node, nom_r, required, rp->cpus);
+      if (fr < 0) return -1;
+      if (fr > 0) return 0;
+    }
+  }
   numa_view v;
   int have = 0;
   if (policy > KE_NUMA_POLICY_NONE && n->n_zone > 0) {
@@ -3966,6 +4072,41 @@ int or_eval(const or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now
  * of `nodes` (feasible[i] != 0, NULL = every node) with the smallest order (first in node order) scores 1000.
  * pod_requested[i*KE_NRES + k]: NodeInfo Requested after the unmatched restore.  raw[i] = Score (before
  * NormalizeScore), nom[i] = the nominated reservation or -1.  Returns preferredNode or -1. */
+/* NodeNUMAResource's FilterNominateReservation (plugin.go:448-504): a pod that binds no CPUs on a node without a
+ * NUMA policy passes, a binding pod needs a valid CPU topology, a reservation outside RestoreReservation's matched
+ * set passes, else tryAllocateFromReservation over it alone -- which fails only under a reservation affinity. */
+static int or_numa_nominable(const or_cluster* c, const ke_pod* pod, int32_t node, int32_t r, int affinity) {
+  const or_node* n = &c->nodes[node];
+  if (pod_requests_zero(pod)) return 1;
+  cpuset_state st;
+  cpuset_prefilter(c, pod, &st);
+  int exclusive;
+  const int policy = effective_policy(n, pod, &exclusive);
+  const int rcb = request_cpu_bind(&st, pod, n->node.cpu_bind_policy);
+  if (rcb < 0) return 0;
+  if (!rcb && policy <= KE_NUMA_POLICY_NONE) return 1;
+  if (rcb && !cpus_valid(n)) return 0;
+  if (policy != KE_NUMA_POLICY_NONE) return 1; /* (a holding reservation here is refused: or_resv_supported) */
+  uint64_t got[ACC_WORDS];
+  return or_numa_from_rsv(c, pod, node, r, affinity, got) >= 0;
+}
+
+/* golden entry point: NodeNUMAResource Reserve's allocation from reservation `nom` for a binding pod matching
+ * reservations ids[] on `node` (allocateWithNominatedReservation -> tryAllocateFromReservation): 1 and the cpuset,
+ * 0 (nil: the node itself), -1 (Unschedulable under a reservation affinity). */
+int or_numa_reserve_from_rsv(or_cluster* c, const ke_pod* pod, int32_t node, const int32_t* ids, int32_t n_ids,
+                             int32_t nom, int32_t required, uint64_t* cpus) {
+  char* m = (char*)calloc((size_t)(c->n_resv > 0 ? c->n_resv : 1), 1);
+  for (int32_t j = 0; j < n_ids; j++)
+    if (or_resv_usable(&c->resv[ids[j]])) m[ids[j]] = 1;
+  c->resv_m = m;
+  memset(cpus, 0, sizeof(uint64_t) * ACC_WORDS);
+  const int r = or_numa_from_rsv(c, pod, node, nom, required, cpus);
+  c->resv_m = NULL;
+  free(m);
+  return r;
+}
+
 static int32_t or_resv_prescore(const or_cluster* c, const ke_pod* pod, const char* m, const int64_t* pod_requested,
                                 const uint8_t* feasible, int affinity, int64_t* raw, int32_t* nom) {
   const int32_t N = c->n;
@@ -3993,7 +4134,9 @@ static int32_t or_resv_prescore(const or_cluster* c, const ke_pod* pod, const ch
       if (!m[r] || c->resv[r].node != i) continue;
       n_matched++;
       only = r;
-      if (!or_resv_nominable(c, &c->resv[r], pod, i, &pod_requested[i * KE_NRES], all_alloc, affinity)) continue;
+      if (!or_resv_nominable(c, &c->resv[r], pod, i, &pod_requested[i * KE_NRES], all_alloc, affinity) ||
+          !or_numa_nominable(c, pod, i, r, affinity))
+        continue;
       n_ok++;
       if (first < 0) first = r;
       if (c->resv[r].order != 0 && (bo == 0 || c->resv[r].order < bo)) {
@@ -4137,8 +4280,8 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
     cpuset_prefilter(c, &pods[p], &st);
     ds_pod d;
     ds_prepare_pod(c, &pods[p], &d);
-    int scalar = pods[p].has_other_requests || !d.skip || st.rcb || (node_bind && pods[p].requests[KE_RES_CPU] > 0) ||
-                 pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE;
+    (void)node_bind;
+    int scalar = pods[p].has_other_requests || !d.skip || pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE;
     for (int r = KE_NRES; r < KE_RES_COUNT; r++) scalar |= pods[p].requests[r] != 0;
     for (int r = 0; r < KE_PDR_COUNT; r++) scalar |= pods[p].device_requests[r] != 0;
     if (scalar) return KE_ERR_UNSUPPORTED;
@@ -4202,7 +4345,17 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
     memset(&rp, 0, sizeof rp);
     ds_aff da = NO_AFF; /* the affinity the Filter stored, for DeviceShare's Reserve */
     if (b >= 0) da = ds_reserve_affinity(c, &pods[p], b);
-    if (b >= 0 && (or_reserve_plan(c, &pods[p], b, &rp) != 0 || !ds_reserve_feasible(c, &pods[p], b, da))) {
+    char* mflags = NULL; /* the matched flags again for NodeNUMAResource's Reserve */
+    if (b >= 0 && (n_ids > 0 || affinity)) {
+      mflags = (char*)calloc((size_t)(c->n_resv > 0 ? c->n_resv : 1), 1);
+      for (int32_t j = c->moff[p]; j < c->moff[p + 1]; j++)
+        if (or_resv_usable(&c->resv[c->mids[j]])) mflags[c->mids[j]] = 1;
+      c->resv_m = mflags;
+    }
+    const int plan = b >= 0 ? or_reserve_plan(c, &pods[p], b, &rp, mflags ? nom[b] : -1) : 0;
+    c->resv_m = NULL;
+    free(mflags);
+    if (b >= 0 && (plan != 0 || !ds_reserve_feasible(c, &pods[p], b, da))) {
       /* Reserve failed (Unreserve undoes the others): not placed */
       chosen[p] = -1;
       if (score) score[p] = -1;

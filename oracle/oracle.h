@@ -63,6 +63,8 @@ typedef struct or_rsv_state {
   int64_t dev_remained[KE_DEV_TYPES][KE_MAX_MINORS][KE_DKEYS];
 } or_rsv_state;
 int or_restore_state(const or_cluster* c, int32_t r, or_rsv_state* out);
+int or_numa_reserve_from_rsv(or_cluster* c, const ke_pod* pod, int32_t node, const int32_t* ids, int32_t n_ids,
+                             int32_t nom, int32_t required, uint64_t* cpus);
 int or_reservations_get(const or_cluster* c, int32_t n, ke_reservation* out);
 int or_pod_reservations(or_cluster* c, int32_t n_pods, const int32_t* offsets, const int32_t* ids);
 int or_last_reservations(const or_cluster* c, int32_t n, int32_t* out);

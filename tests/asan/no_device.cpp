@@ -13,6 +13,9 @@ int device_eval(Context*, int32_t, const ke_pod*, int64_t, uint8_t*, uint8_t*, i
                 int32_t*) { return none(); }
 int device_schedule(Context*, int32_t, const ke_pod*, int64_t, int32_t*, int32_t*) { return none(); }
 int device_rsv_result(Context*, int32_t*) { return none(); }
+int device_rsv_views(Context*, const ke_pod&, int64_t, const std::vector<RsvView>&, std::vector<RsvViewOut>&) {
+  return none();
+}
 int device_quota_sync(Context*) { return KE_OK; }
 int device_debug_rows(Context*, int32_t, Row*) { return none(); }
 int device_set_profiling(Context*, int32_t) { return none(); }

@@ -11,7 +11,15 @@ Go tests cannot run here; each case restates one test's objects and expectations
     1 (:105-124), allocated-pod-1 (assigned to it) 50 / 4Gi / 50 of minor 1 (:126-143).  The matched state
     (:157-209): allocatable = minor 1 100 / 8Gi / 100, allocated = 50 / 4Gi / 50, remained = 50 / 4Gi / 50, and
     mergedMatchedAllocatable / mergedMatchedAllocated the same two lists.
-Encoding: cpusets as CPU id lists; device amounts as [gpu-core, gpu-memory, gpu-memory-ratio] of GPU minors.
+  * pkg/scheduler/plugins/nodenumaresource/plugin_test.go:1086-1500 TestPlugin_Reserve, its allocate-from-reservation
+    cases without a NUMA affinity (:1226-1280): CPU topology buildCPUTopologyForTest(2, 1, 4, 2) -- CPU c in core
+    c / 2, NUMA node = socket = c / 8 -- MaxRefCount 1, the matched reservation's remainedCPUs added to the node
+    allocation under its UID (:1449-1466; the hand-built restore state holds no merged CPUs, so preferredCPUs =
+    remainedCPUs), a 4-CPU pod preferring FullPCPUs, the reservation nominated (:1480):
+    Default, remained 4-10 -> 4-7; Restricted, remained 4-10 -> 4-7; Restricted, remained 4-5, with a reservation
+    affinity -> Unschedulable "Reservation(s) not enough cpus available to satisfy request".
+Encoding: cpusets as CPU id lists; device amounts as [gpu-core, gpu-memory, gpu-memory-ratio] of GPU minors;
+reserve cases: policy 0 Default / 2 Restricted, want_code 1 (from the reservation) / -1 (Unschedulable).
 
 Run:  python tests/golden/make_restore_state_fixtures.py
 """
@@ -37,7 +45,19 @@ cases = [
               "merged_matched_allocated": {"1": [50, 4 * GI, 50]}}},
 ]
 
+SRC = "pkg/scheduler/plugins/nodenumaresource/plugin_test.go"
+reserve_cases = [
+    {"name": "reserve_from_reservation_default", "source": f"{SRC}:1226-1242", "topology": [2, 1, 4, 2],
+     "remained": [4, 5, 6, 7, 8, 9, 10], "policy": 0, "affinity": False, "num_cpus": 4, "want_code": 1,
+     "want_cpus": [4, 5, 6, 7]},
+    {"name": "reserve_from_reservation_restricted", "source": f"{SRC}:1243-1259", "topology": [2, 1, 4, 2],
+     "remained": [4, 5, 6, 7, 8, 9, 10], "policy": 2, "affinity": False, "num_cpus": 4, "want_code": 1,
+     "want_cpus": [4, 5, 6, 7]},
+    {"name": "reserve_from_reservation_restricted_fails", "source": f"{SRC}:1260-1277", "topology": [2, 1, 4, 2],
+     "remained": [4, 5], "policy": 2, "affinity": True, "num_cpus": 4, "want_code": -1, "want_cpus": []},
+]
+
 if __name__ == "__main__":
     with open(os.path.join(HERE, "reservation_restore.json"), "w") as f:
-        json.dump({"cases": cases}, f, indent=1)
+        json.dump({"cases": cases, "reserve_cases": reserve_cases}, f, indent=1)
     print(f"wrote {len(cases)} cases")

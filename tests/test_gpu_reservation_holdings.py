@@ -83,3 +83,80 @@ def test_holdings_reload_and_release_parity(gpu):
     assert_schedule_equal(ev, o, more, synth.T0)
     assert ev.check_records(synth.T0) == 0
     assert np.array_equal(ev.reservation_allocs_get(), o.reservation_allocs_get())
+
+
+def cpuset_matched_setup(n, seed, n_pods, affinity=0.3, tight_pods=0.0):
+    """Nodes without NUMA policies carrying CPU tables, reservations whose reserve pods hold cpusets (owner pods
+    holding part of them, every allocate policy), and a queue of cpuset pods of which ~40 % match the reservations
+    of a few owner groups (KE_RSV_MATCHED, or KE_RSV_AFFINITY for `affinity` of them).  `tight_pods`: that fraction
+    of the reservation nodes has its pod limit just at its pod count (fitsNode's pod check binds)."""
+    rng = np.random.default_rng(seed)
+    cl = synth.make_cluster(n, synth.BASE_SEED + seed, amplified_fraction=0.0)
+    zones, tabs = synth.make_numa_cpus(cl, synth.BASE_SEED + seed + 1, policy_weights=(1, 0, 0, 0))
+    rs, al = synth.make_reservation_holdings(cl, synth.BASE_SEED + seed + 2, zones, tabs, None, frac=0.5)
+    for i in np.unique(rs["node"]):
+        if rng.random() < tight_pods:
+            cl.nodes["allowed_pods"][i] = cl.nodes["pod_count"][i] + int(rng.integers(-1, 2))
+    cfg = synth.config(n)
+    ev, o = Evaluator(cfg), Oracle(cfg, n)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        synth.load_numa(h, zones)
+        synth.load_cpus(h, tabs)
+        h.reservations_load(rs, al)
+    pods = synth.make_cpuset_pods(n_pods, synth.BASE_SEED + seed + 3, cpuset_fraction=0.7)
+    grp = rng.integers(0, 8, len(rs))
+    matches = [[] for _ in range(n_pods)]
+    ok = (pods["numa_topology_policy"] == 0) & (pods["requests"][:, 2:] == 0).all(1) & (pods["has_other_requests"] == 0) \
+        & (pods["device_requests"] == 0).all(1)
+    for p in np.flatnonzero(ok & (rng.random(n_pods) < 0.4)):
+        pods["reservation_matched"][p] = abi.RSV_AFFINITY if rng.random() < affinity else abi.RSV_MATCHED
+        matches[p] = np.flatnonzero(grp == rng.integers(0, 8)).tolist()
+    return ev, o, pods, matches, rs
+
+
+def _holdings_equal(ev, o):
+    a, b = ev.reservations_get(), o.reservations_get()
+    assert np.array_equal(a["allocated"], b["allocated"]) and np.array_equal(a["allocated_pods"], b["allocated_pods"])
+    assert np.array_equal(ev.reservation_allocs_get(), o.reservation_allocs_get())
+
+
+@pytest.mark.parametrize("seed,affinity,tight", [(1361, 0.0, 0.0), (1362, 0.5, 0.0), (1363, 0.3, 0.4)],
+                         ids=["matched", "affinity", "pod-limits"])
+def test_matched_cpuset_from_reservations_parity(gpu, seed, affinity, tight):
+    """Cpuset pods matching reservations that hold cpusets (nodes without NUMA policies): NodeNUMAResource's Filter
+    tries the matched reservations first (k_rsv_views: takePreferredCPUs on the reservations' CPUs, the Restricted
+    policy's second allocation), the nomination filters them under an affinity, Reserve allocates from the
+    nominated one -- placements, scores, cpusets, reservation state and owner cpusets bit-exact with the oracle;
+    then Unreserve of part of them and a second queue."""
+    ev, o, pods, matches, rs = cpuset_matched_setup(300, seed, 300, affinity, tight)
+    c1, s1 = ev.schedule(pods, synth.T0, matches=matches)
+    c0, s0 = o.schedule(pods, synth.T0, matches=matches)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5].ravel().tolist()
+    assert np.array_equal(s1, s0)
+    diff = np.argwhere(np.any(ev.last_cpusets != o.last_cpusets, axis=1))
+    assert len(diff) == 0, diff[:5].ravel().tolist()
+    _holdings_equal(ev, o)
+    a1, a0 = ev.last_allocations(), o.last_allocations()
+    assert np.array_equal(a1["reservation"], a0["reservation"])
+    into = np.flatnonzero(a1["reservation"] > 0)
+    assert len(into) >= 5
+    held = [p for p in into if rs["holds"][a1["reservation"][p] - 1] & abi.RSV_HOLDS_CPUSET and a1["cpuset"][p].any()]
+    assert len(held) >= 2  # cpusets taken out of holding reservations
+    for p in into[::3]:
+        ev.unreserve(pods[p], int(p))
+        o.release(pods[p], a0[p], abi.RELEASE_UNRESERVE)
+    _holdings_equal(ev, o)
+    more = synth.make_cpuset_pods(200, synth.BASE_SEED + seed + 7, key_base=7_700_000_000)
+    m2 = [matches[p % len(matches)] if pods["reservation_matched"][p % len(matches)] else [] for p in range(len(more))]
+    more["reservation_matched"] = [pods["reservation_matched"][p % len(matches)] for p in range(len(more))]
+    more["numa_topology_policy"] = 0
+    more["device_requests"] = 0
+    more["has_other_requests"] = np.where(np.array([len(m) > 0 for m in m2]), 0, more["has_other_requests"])
+    more["requests"][:, 2:] = np.where(np.array([len(m) > 0 for m in m2])[:, None], 0, more["requests"][:, 2:])
+    c1, s1 = ev.schedule(more, synth.T0, matches=m2)
+    c0, s0 = o.schedule(more, synth.T0, matches=m2)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    assert np.array_equal(ev.last_cpusets, o.last_cpusets)
+    _holdings_equal(ev, o)
+    assert ev.check_records(synth.T0) == 0

@@ -287,3 +287,46 @@ def test_restore_state_golden(case):
             == w["merged_matched_allocatable"]
         assert {str(m): st["dev_allocated"][0, m].tolist() for m in range(16) if st["dev_allocated"][0, m].any()} \
             == w["merged_matched_allocated"]
+
+
+RESERVE = json.load(open(os.path.join(HERE, "golden", "reservation_restore.json")))["reserve_cases"]
+
+
+@pytest.mark.parametrize("case", RESERVE, ids=[c["name"] for c in RESERVE])
+def test_numa_reserve_from_reservation_golden(case):
+    """NodeNUMAResource Reserve's allocate-from-reservation (allocateWithNominatedReservation ->
+    tryAllocateFromReservation) in the oracle against TestPlugin_Reserve's reservation cases."""
+    sockets, nodes_per, cores_per, tpc = case["topology"]
+    n_cpu = sockets * nodes_per * cores_per * tpc
+    cl = synth.make_cluster(1, synth.BASE_SEED + 1351)
+    cl.nodes["allocatable"][0] = [96_000, 512 * 2**30]
+    cl.nodes["raw_allocatable"][0] = abi.ABSENT
+    cl.nodes["requested"][0] = 0
+    cl.nodes["cpu_bind_policy"][0] = 0
+    cl.nodes["numa_topology_policy"][0] = 0
+    cl.nodes["cpu_amplification_ratio"][0] = 0
+    o = Oracle(synth.config(1), 1)
+    synth.load_into(o, cl)
+    t = np.zeros(n_cpu, abi.CPU_DTYPE)
+    t["cpu_id"] = np.arange(n_cpu)
+    t["core_id"] = np.arange(n_cpu) // tpc
+    t["numa_id"] = np.arange(n_cpu) // (cores_per * tpc)
+    t["socket_id"] = np.arange(n_cpu) // (nodes_per * cores_per * tpc)
+    t["ref_count"][case["remained"]] = 1  # the reservation's remainedCPUs under its UID
+    o.set_cpus(0, t, 1)
+    r = np.zeros(1, abi.RESERVATION_DTYPE)
+    a = np.zeros(1, abi.RESERVATION_ALLOC_DTYPE)
+    r["available"], r["holds"], r["allocate_policy"] = 1, abi.RSV_HOLDS_CPUSET, case["policy"]
+    r["allocatable"][0] = [len(case["remained"]) * 1000, 2**30]
+    a["cpuset"][0] = _cpus(case["remained"])
+    o.reservations_load(r, a)
+    pod = synth.make_pods(1, synth.BASE_SEED + 1352)[0].copy()
+    pod["requests"][:] = 0
+    pod["limits"][:] = 0
+    pod["requests"][abi.RES_CPU] = pod["limits"][abi.RES_CPU] = case["num_cpus"] * 1000
+    pod["priority_class"], pod["qos_class"] = abi.PRIORITY_PROD, abi.QOS_LSR
+    pod["cpu_bind_required"], pod["cpu_bind_preferred"] = abi.CPU_BIND_UNSET, abi.CPU_BIND_FULL_PCPUS
+    pod["has_other_requests"], pod["device_requests"], pod["numa_topology_policy"] = 0, 0, 0
+    code, cpus = o.numa_reserve_from_rsv(pod, 0, [0], 0, case["affinity"])
+    assert code == case["want_code"]
+    assert np.array_equal(cpus, _cpus(case["want_cpus"]))
