@@ -876,14 +876,15 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
       return !(affinity && view_of(i) == 0);
     };
     std::vector<int32_t> ok;
+    bool fits_one = false;  // the Reservation Filter with a reservation affinity (plugin.go:316-318, 351-442): a
+                            // node without matched reservations fails, one with them passes when one of them fits
     for (int32_t i : mine)
       if (resv_nominable(c.resv[(size_t)i], pod, ns.node.allocatable, pod_requested, all_alloc, affinity, pods_restored,
-                         (int64_t)mine.size(), ns.node.allowed_pods) &&
-          numa_nominable(i))
-        ok.push_back(i);
-    // the Reservation Filter with a reservation affinity (plugin.go:316-318, 351-442): a node without matched
-    // reservations fails, one with them passes when one of them fits (the same checks as the nomination's)
-    const bool allowed = !affinity || !ok.empty();
+                         (int64_t)mine.size(), ns.node.allowed_pods)) {
+        fits_one = true;
+        if (numa_nominable(i)) ok.push_back(i);
+      }
+    const bool allowed = !affinity || fits_one;
     // NominateReservation (nominator.go:223-277): with an affinity and one matched reservation that one, else
     // the survivors: the only one, else the smallest order, else the best ScoreReservation (ties -> lowest
     // index: sort.Slice's insertion sort keeps them below 13 elements)

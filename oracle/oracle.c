@@ -3342,8 +3342,10 @@ static int or_resv_nominable(const or_cluster* c, const ke_reservation* r, const
   int32_t n_matched = 0;
   for (int32_t i = 0; i < c->n_resv; i++)
     if (c->resv[i].node == node && or_resv_usable(&c->resv[i]) && c->resv_m && c->resv_m[i]) n_matched++;
-  int node_fits = (int64_t)c->nodes[node].node.pod_count + c->nodes[node].rv_pods - n_matched + 1 <=
-                  (int64_t)c->nodes[node].node.allowed_pods;
+  /* (restoreMatchedReservation removed one reserve pod per matched reservation from Pods; the unmatched restore
+   * moves only Requested) */
+  const int64_t pods_restored = (int64_t)c->nodes[node].node.pod_count - n_matched;
+  int node_fits = pods_restored - n_matched + 1 <= (int64_t)c->nodes[node].node.allowed_pods;
   if (!(pod->requests[KE_RES_CPU] == 0 && pod->requests[KE_RES_MEMORY] == 0)) {
     for (int k = 0; k < KE_NRES; k++) {
       int64_t remained = r->allocatable[k] - r->allocated[k];
