@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--pipeline-fixup", action="store_true",
                     help="pipelined with exact lists from k_fixup (ke_set_pipeline 2, the round-3 schedule)")
     ap.add_argument("--profile-every", type=int, default=8, help="HIP-event-sample every n-th batch (0 = off)")
+    ap.add_argument("--sync", action="store_true", help="one ke_schedule call per step (no submit-ahead)")
     ap.add_argument("--stream-nodes", type=int, default=4_000_000,
                     help="B=1 streaming sweep size (N*row > 512 MB, past the 256 MB Infinity Cache); 0 = skip")
     return ap.parse_args()
@@ -296,8 +297,16 @@ def main():
     got_c, got_s = [], []
     barrier()
     t0 = time.perf_counter()
+    # the scheduler loop hands over slice s+1 (ke_schedule_submit) before collecting slice s (ke_schedule_wait): the
+    # host's argument checks, staging and launches of s+1 overlap the device's work on s (--sync: ke_schedule)
+    sl = lambda s: pods[s * slice_len:(s + 1) * slice_len]  # noqa: E731
+    nxt = None if a.sync or K == 0 else ev.submit(sl(0), synth.T0)
     for s in range(K):
-        chosen, score = ev.schedule(pods[s * slice_len:(s + 1) * slice_len], synth.T0)
+        if a.sync:
+            chosen, score = ev.schedule(sl(s), synth.T0)
+        else:
+            cur, nxt = nxt, (ev.submit(sl(s + 1), synth.T0) if s + 1 < K else None)
+            chosen, score = ev.wait(cur)
         got_c.append(chosen)
         got_s.append(score)
         placed += int((chosen >= 0).sum())
@@ -325,7 +334,8 @@ def main():
             "fixup_ms": mean("fixup_ms"), "resolve_ms": mean("resolve_ms"), "handoff_ms": mean("handoff_ms"),
             "rows_fetched": mean("rows_fetched"), "rows_changed": mean("rows_changed"),
             "spec_failed": mean("spec_failed_rounds"),
-            "resolve_phases": {k: float(np.mean([x["resolve_phases_ms"][k] for x in kss])) for k in kss[0]["resolve_phases_ms"]}}
+            "resolve_phases": {k: float(np.mean([x["resolve_phases_ms"][k] for x in kss])) for k in kss[0]["resolve_phases_ms"]},
+            "resolve_wave1": {k: float(np.mean([x["resolve_wave1_ms"][k] for x in kss])) for k in kss[0]["resolve_wave1_ms"]}}
     tag = f"config{a.config}_nodes{hi - lo}_batch{a.batch}_world{world}" + ("" if not a.no_pipeline else "_serial")
     out = {
         "metric": "pod-node Filter+Score evals/sec + p99 per-pod sched latency @50k nodes",
@@ -344,7 +354,8 @@ def main():
                    "pods_per_batch": a.batch, "plugins": "LoadAwareScheduling+NodeNUMAResource",
                    "args": "v1beta3 defaults, NodeMetricExpirationSeconds=3600",
                    "parallelism": f"node-shard x{world}" + (" (RCCL all-gather of per-shard top-k)" if world > 1 else ""),
-                   "nodes_per_rank": hi - lo, "pipelined": not a.no_pipeline},
+                   "nodes_per_rank": hi - lo, "pipelined": not a.no_pipeline,
+                   "calls": "ke_schedule per step" if a.sync else "ke_schedule_submit one step ahead + ke_schedule_wait"},
         # pod dequeue (the ke_schedule call's entry: every pod of a step is dequeued then) -> its
         # node selected (its batch's Reserve end); includes host staging and the wait behind earlier batches
         "p99_pod_latency_ms": float(np.percentile(np.concatenate(plat), 99)) if plat else None,
@@ -361,6 +372,7 @@ def main():
                       "records_fetched_per_batch": kagg["rows_fetched"], "rows_changed_per_batch": kagg["rows_changed"],
                       "spec_failed_rounds_per_batch": kagg["spec_failed"],
                       "resolve_phases": kagg["resolve_phases"],
+                      "resolve_wave1": kagg["resolve_wave1"],
                       "note": "per batch; 'select' includes the all-gather + merge when sharded"},
         "host_ms_per_step": {k: float(np.mean([h[k] for h in hs])) for k in hs[0]} if hs else None,
         "roofline": roofline(hi - lo, a.batch, kagg, dt / K, n_batches / K, not a.no_pipeline, tag,

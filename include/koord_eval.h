@@ -886,6 +886,20 @@ int ke_eval(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
 int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
                 int32_t* chosen, int32_t* score);
 
+/* ke_schedule in two halves, so a scheduler loop can hand over its next queue slice while the device still
+ * resolves the previous one (the same sequential semantics: a submitted call sees the Reserves of every call
+ * submitted before it).  ke_schedule_submit checks the arguments (a refused call returns its code and submits
+ * nothing), enqueues the call and returns a ticket; ke_schedule_wait(ticket) writes its chosen / score (as
+ * ke_schedule) and makes it "the last ke_schedule" of ke_last_allocations / ke_unreserve.  `pods` must stay valid
+ * until the wait.  Only a plain queue is enqueued behind a call in flight (no reservation-matched, NUMA-policy,
+ * quota, DeviceShare or cpuset pod, no NUMA state, unsharded, pipelined, no node row to re-derive); any other
+ * call first completes the calls in flight and runs at once (its outputs are kept for the wait).  Every other
+ * entry point except the ke_last_* statistics completes the calls in flight first; the statistics describe the
+ * last completed call.  Replaces nothing in the reference: scheduleOne's per-pod loop
+ * (frameworkext/framework_extender_factory.go:159-192) is sequential, and so are the submitted calls. */
+int ke_schedule_submit(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int64_t* ticket);
+int ke_schedule_wait(ke_ctx* ctx, int64_t ticket, int32_t* chosen, int32_t* score);
+
 /* Timing of the last ke_schedule call: device milliseconds of the whole queue, and per-batch
  * device service time (the batch's eval start -> its Reserve end) in milliseconds, n_batches entries. */
 int ke_last_schedule_stats(ke_ctx* ctx, double* total_ms, int32_t* n_batches,
@@ -1115,6 +1129,10 @@ int ke_debug_resolve_phases(ke_ctx* ctx, double* phases6);
  * prediction loop (wave 0), the T maxima on wave 1 (its own rows or the T-row helpers' hand-off, concurrent with
  * the loop), wave 0's R; then the fraction of T batches whose maxima came from the helpers. */
 int ke_debug_resolve_subphases(ke_ctx* ctx, double* sub5);
+/* The progressive S of wave 1 in the first round of a batch with helper T maxima (4 entries, ms per batch): its
+ * polls for the chunks' predictions, its record loads + Reserves of the chunks' slots, its rows, and its end after
+ * T's set-up. */
+int ke_debug_resolve_wave1(ke_ctx* ctx, double* w4);
 /* BestEffort (pod, node) pairs the last ke_eval / ke_schedule evaluated in the compacted full-merge
  * pass (no preferred merged hint). */
 int ke_debug_numa_deferred(ke_ctx* ctx, int64_t* n);

@@ -539,6 +539,8 @@ EXPORTS = {
     "ke_quotas_load": (C.c_int, [C.c_void_p, C.POINTER(QuotaArgs), C.c_void_p, i32]),
     "ke_quota_state": (C.c_int, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "ke_schedule": (C.c_int, [C.c_void_p, i32, C.c_void_p, i64, C.c_void_p, C.c_void_p]),
+    "ke_schedule_submit": (C.c_int, [C.c_void_p, i32, C.c_void_p, i64, C.c_void_p]),
+    "ke_schedule_wait": (C.c_int, [C.c_void_p, i64, C.c_void_p, C.c_void_p]),
     "ke_last_schedule_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(i32), C.c_void_p, i32]),
     "ke_set_profiling": (C.c_int, [C.c_void_p, i32]),
     "ke_last_kernel_stats": (C.c_int, [C.c_void_p] + [C.POINTER(C.c_double)] * 3 + [C.POINTER(i32)]),
@@ -550,6 +552,7 @@ EXPORTS = {
     "ke_last_resolve_split": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "ke_debug_resolve_phases": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ke_debug_resolve_subphases": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "ke_debug_resolve_wave1": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ke_debug_numa_deferred": (C.c_int, [C.c_void_p, C.POINTER(i64)]),
     "ke_debug_ds_cuts": (C.c_int, [C.c_void_p, C.POINTER(i32)]),
     "ke_debug_spec_failed": (C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <deque>
 #include <new>
 
 #include "ke_host.h"
@@ -33,9 +34,54 @@ bool device_sharded(const Context* ctx);
 
 using namespace ke;
 
+// A ke_schedule_submit call: its device work in flight (`fin` set), or completed with its outputs kept until
+// ke_schedule_wait collects them.
+struct AsyncCall {
+  int64_t ticket = 0;
+  int32_t n = 0;
+  const ke_pod* pods = nullptr;  // the caller's array (valid until its ke_schedule_wait)
+  int64_t now = 0;
+  bool device = false;  // enqueued by ke_schedule_submit (its release records are set when it is collected)
+  DevFinish fin;
+  int rc = KE_OK;
+  std::string msg;
+  std::vector<int32_t> chosen, score;
+};
+
 struct ke_ctx {
   Context c;
+  std::deque<AsyncCall> async;  // submitted, not yet collected (ticket order)
+  int64_t next_ticket = 1;
 };
+
+// A submitted call's completion (in submission order): waits for its device work, takes its outputs and statistics,
+// and queues its host mirror (the deferred LoadAware assign / NodeInfo.Requested of its placed pods).
+static void async_finish(ke_ctx* ctx, AsyncCall& a) {
+  if (!a.fin) return;
+  DevFinish f = std::move(a.fin);
+  a.fin = nullptr;
+  a.chosen.assign((size_t)a.n, -1);
+  a.score.assign((size_t)a.n, 0);
+  a.rc = f(a.chosen.data(), a.score.data());
+  if (a.rc) {
+    a.msg = last_error_cstr();
+    return;
+  }
+  Context& c = ctx->c;
+  const int32_t off = c.cfg.global_node_offset;
+  const int64_t base = c.pending_base;  // the completion copied the pods there
+  c.pending.reserve(c.pending.size() + (size_t)a.n);
+  for (int32_t i = 0; i < a.n; i++) {
+    const int32_t node = a.chosen[(size_t)i] - off;
+    if (a.chosen[(size_t)i] < 0 || node < 0 || node >= c.n_nodes) continue;
+    c.pending.push_back({node, a.now, base + i});
+  }
+}
+
+// Every call in flight completes (an entry point that reads or changes the state the submitted calls work on).
+static void async_drain(ke_ctx* ctx) {
+  for (AsyncCall& a : ctx->async) async_finish(ctx, a);
+}
 
 static int check_node(ke_ctx* ctx, int32_t node) {
   if (!ctx) return fail(KE_ERR_INVALID, "null context");
@@ -235,6 +281,7 @@ int ke_create(const ke_config* cfg, ke_ctx** out) {
 
 void ke_destroy(ke_ctx* ctx) {
   if (!ctx) return;
+  async_drain(ctx);
   device_destroy(&ctx->c);
   delete ctx;
 }
@@ -242,6 +289,7 @@ void ke_destroy(ke_ctx* ctx) {
 int32_t ke_num_nodes(ke_ctx* ctx) { return ctx ? ctx->c.n_nodes : 0; }
 
 int ke_node_resources_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_node_resource* res) {
+  if (ctx) async_drain(ctx);
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
@@ -255,6 +303,7 @@ int ke_node_resources_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_node_re
 }
 
 int ke_node_resources_get(ke_ctx* ctx, int32_t node, int32_t cap, ke_node_resource* res, int32_t* n) {
+  if (ctx) async_drain(ctx);
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
@@ -272,6 +321,7 @@ int ke_debug_ds_cuts(ke_ctx* ctx, int32_t* cuts) {
 }
 
 int ke_node_upsert(ke_ctx* ctx, int32_t node, const ke_node* n) {
+  if (ctx) async_drain(ctx);
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
@@ -295,6 +345,7 @@ int ke_node_upsert(ke_ctx* ctx, int32_t node, const ke_node* n) {
 }
 
 int ke_node_delete(ke_ctx* ctx, int32_t node) {
+  if (ctx) async_drain(ctx);
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);  // pending Reserves on it first: the object state stays (koord_eval.h)
   if (rc) return rc;
@@ -308,6 +359,7 @@ int ke_node_delete(ke_ctx* ctx, int32_t node) {
 }
 
 int ke_node_topology_delete(ke_ctx* ctx, int32_t node) {
+  if (ctx) async_drain(ctx);
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
@@ -326,6 +378,7 @@ int ke_node_topology_delete(ke_ctx* ctx, int32_t node) {
 }
 
 int ke_nodes_load(ke_ctx* ctx, int32_t n, const ke_node* nodes) {
+  if (ctx) async_drain(ctx);
   if (!ctx || n < 0 || (n > 0 && !nodes)) return fail(KE_ERR_INVALID, "ke_nodes_load arguments");
   if (ctx) flush_mirror(ctx->c);
   if (n > ctx->c.cfg.node_capacity) return fail(KE_ERR_INVALID, "more nodes than node_capacity");
@@ -337,6 +390,7 @@ int ke_nodes_load(ke_ctx* ctx, int32_t n, const ke_node* nodes) {
 }
 
 int ke_node_devices_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_device* devices) {
+  if (ctx) async_drain(ctx);
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
@@ -353,6 +407,7 @@ int ke_node_devices_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_device* d
 }
 
 int ke_node_device_flags(ke_ctx* ctx, int32_t node, int32_t secondary_well_planned, int32_t gpu_model_key) {
+  if (ctx) async_drain(ctx);
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
@@ -366,12 +421,14 @@ int ke_node_device_flags(ke_ctx* ctx, int32_t node, int32_t secondary_well_plann
 }
 
 int ke_set_pod_device_hints(ke_ctx* ctx, int32_t n, const ke_pod_device_hints* hints) {
+  if (ctx) async_drain(ctx);
   if (!ctx || n < 0 || (n > 0 && !hints)) return fail(KE_ERR_INVALID, "ke_set_pod_device_hints arguments");
   ctx->c.hints.assign(hints, hints + n);
   return KE_OK;
 }
 
 int ke_gpu_templates_load(ke_ctx* ctx, int32_t n, const ke_gpu_template* templates) {
+  if (ctx) async_drain(ctx);
   if (!ctx || n < 0 || (n > 0 && !templates)) return fail(KE_ERR_INVALID, "ke_gpu_templates_load arguments");
   for (int32_t i = 0; i < n; i++) {
     const int id = intern_model_key(ctx->c, templates[i].model_key);
@@ -382,6 +439,7 @@ int ke_gpu_templates_load(ke_ctx* ctx, int32_t n, const ke_gpu_template* templat
 }
 
 int ke_reservations_load(ke_ctx* ctx, int32_t n, const ke_reservation* reservations) {
+  if (ctx) async_drain(ctx);
   if (!ctx) return fail(KE_ERR_INVALID, "null context");
   flush_mirror(ctx->c);
   return load_reservations(ctx->c, n, reservations);
@@ -389,12 +447,14 @@ int ke_reservations_load(ke_ctx* ctx, int32_t n, const ke_reservation* reservati
 
 int ke_reservations_load_ex(ke_ctx* ctx, int32_t n, const ke_reservation* reservations,
                             const ke_reservation_alloc* allocs) {
+  if (ctx) async_drain(ctx);
   if (!ctx) return fail(KE_ERR_INVALID, "null context");
   flush_mirror(ctx->c);
   return load_reservations(ctx->c, n, reservations, allocs);
 }
 
 int ke_reservation_allocs_get(ke_ctx* ctx, int32_t n, ke_reservation_alloc* out) {
+  if (ctx) async_drain(ctx);
   if (!ctx || n < 0 || (n > 0 && !out) || n > (int32_t)ctx->c.resv.size())
     return fail(KE_ERR_INVALID, "ke_reservation_allocs_get arguments");
   for (int32_t i = 0; i < n; i++)
@@ -405,12 +465,14 @@ int ke_reservation_allocs_get(ke_ctx* ctx, int32_t n, ke_reservation_alloc* out)
 int32_t ke_reservations_generation(ke_ctx* ctx) { return ctx ? ctx->c.resv_gen : 0; }
 
 int ke_reservations_get(ke_ctx* ctx, int32_t n, ke_reservation* out) {
+  if (ctx) async_drain(ctx);
   if (!ctx || n < 0 || (n > 0 && !out) || n > (int32_t)ctx->c.resv.size()) return fail(KE_ERR_INVALID, "ke_reservations_get arguments");
   std::copy(ctx->c.resv.begin(), ctx->c.resv.begin() + n, out);
   return KE_OK;
 }
 
 int ke_pod_reservations(ke_ctx* ctx, int32_t n_pods, const int32_t* offsets, const int32_t* ids) {
+  if (ctx) async_drain(ctx);
   if (!ctx || n_pods < 0 || !offsets) return fail(KE_ERR_INVALID, "ke_pod_reservations arguments");
   Context& c = ctx->c;
   if (offsets[0] != 0) return fail(KE_ERR_INVALID, "ke_pod_reservations offsets[0] != 0");
@@ -425,6 +487,7 @@ int ke_pod_reservations(ke_ctx* ctx, int32_t n_pods, const int32_t* offsets, con
 }
 
 int ke_node_info_requested(ke_ctx* ctx, int32_t node, int64_t* requested, int64_t* non_zero) {
+  if (ctx) async_drain(ctx);
   int rc = check_node(ctx, node);
   if (rc) return rc;
   if (!requested || !non_zero) return fail(KE_ERR_INVALID, "ke_node_info_requested outputs");
@@ -441,6 +504,7 @@ int ke_node_info_requested(ke_ctx* ctx, int32_t node, int64_t* requested, int64_
 
 int ke_node_gpu_partitions(ke_ctx* ctx, int32_t node, int32_t has_table, int32_t honor, int32_t n,
                            const ke_gpu_partition* partitions) {
+  if (ctx) async_drain(ctx);
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
@@ -458,6 +522,7 @@ int ke_node_gpu_partitions(ke_ctx* ctx, int32_t node, int32_t has_table, int32_t
 }
 
 int ke_node_devices_delete(ke_ctx* ctx, int32_t node) {
+  if (ctx) async_drain(ctx);
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
@@ -471,6 +536,7 @@ int ke_node_devices_delete(ke_ctx* ctx, int32_t node) {
 }
 
 int ke_node_numa_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_numa_zone* zones) {
+  if (ctx) async_drain(ctx);
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
@@ -500,6 +566,7 @@ int ke_node_numa_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_numa_zone* z
 }
 
 int ke_node_cpus_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_cpu* cpus, int32_t max_ref_count) {
+  if (ctx) async_drain(ctx);
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
@@ -521,6 +588,7 @@ int ke_node_cpus_set(ke_ctx* ctx, int32_t node, int32_t n, const ke_cpu* cpus, i
 }
 
 int ke_quotas_load(ke_ctx* ctx, const ke_quota_args* args, const ke_quota* quotas, int32_t n) {
+  if (ctx) async_drain(ctx);
   if (!ctx || !args || n < 0 || n > KE_MAX_QUOTAS || (n > 0 && !quotas)) return fail(KE_ERR_INVALID, "ke_quotas_load arguments");
   if (args->n_hook_plugins) return fail(KE_ERR_UNSUPPORTED, "ElasticQuotaArgs.HookPlugins are not supported");
   if (args->enable_guarantee_usage) return fail(KE_ERR_UNSUPPORTED, "ElasticQuotaGuaranteeUsage is not supported");
@@ -547,6 +615,7 @@ int ke_quotas_load(ke_ctx* ctx, const ke_quota_args* args, const ke_quota* quota
 }
 
 int ke_quota_state(ke_ctx* ctx, int32_t q, int64_t* limit, uint8_t* limit_has, int64_t* used, int64_t* np_used) {
+  if (ctx) async_drain(ctx);
   if (!ctx || q < 0 || q >= (int32_t)ctx->c.quotas.size()) return fail(KE_ERR_NOT_FOUND, "ke_quota_state: no such quota");
   const int rc = device_quota_sync(&ctx->c);
   if (rc) return rc;
@@ -583,6 +652,7 @@ int ke_last_device_allocations(ke_ctx* ctx, int32_t n, uint64_t* minors) {
 }
 
 int ke_node_set_requested(ke_ctx* ctx, int32_t node, int64_t milli_cpu, int64_t memory) {
+  if (ctx) async_drain(ctx);
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
@@ -594,6 +664,7 @@ int ke_node_set_requested(ke_ctx* ctx, int32_t node, int64_t milli_cpu, int64_t 
 }
 
 int ke_node_set_cpuset_allocated(ke_ctx* ctx, int32_t node, int64_t cpus) {
+  if (ctx) async_drain(ctx);
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
@@ -605,6 +676,7 @@ int ke_node_set_cpuset_allocated(ke_ctx* ctx, int32_t node, int64_t cpus) {
 
 int ke_nodemetric_upsert(ke_ctx* ctx, int32_t node, const ke_node_metric* nm, int32_t n_pm, const ke_pod_metric* pm,
                          int32_t n_agg, const ke_aggregated_usage* agg) {
+  if (ctx) async_drain(ctx);
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
@@ -620,6 +692,7 @@ int ke_nodemetric_upsert(ke_ctx* ctx, int32_t node, const ke_node_metric* nm, in
 
 int ke_nodemetrics_load(ke_ctx* ctx, int32_t n, const ke_node_metric* nms, const int64_t* pm_offsets,
                         const ke_pod_metric* pod_metrics, const int64_t* agg_offsets, const ke_aggregated_usage* aggregated) {
+  if (ctx) async_drain(ctx);
   if (!ctx || n < 0 || (n > 0 && (!nms || !pm_offsets || !agg_offsets))) return fail(KE_ERR_INVALID, "nodemetrics_load");
   if (ctx) flush_mirror(ctx->c);
   for (int32_t i = 0; i < n; i++) {
@@ -633,6 +706,7 @@ int ke_nodemetrics_load(ke_ctx* ctx, int32_t n, const ke_node_metric* nms, const
 }
 
 int ke_nodemetric_delete(ke_ctx* ctx, int32_t node) {
+  if (ctx) async_drain(ctx);
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
@@ -646,6 +720,7 @@ int ke_nodemetric_delete(ke_ctx* ctx, int32_t node) {
 }
 
 int ke_pod_assign(ke_ctx* ctx, int32_t node, const ke_pod* pod, int64_t timestamp_ns) {
+  if (ctx) async_drain(ctx);
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
@@ -655,6 +730,7 @@ int ke_pod_assign(ke_ctx* ctx, int32_t node, const ke_pod* pod, int64_t timestam
 }
 
 int ke_pods_assign(ke_ctx* ctx, int32_t n, const int32_t* nodes, const ke_pod* pods, const int64_t* timestamps_ns) {
+  if (ctx) async_drain(ctx);
   if (!ctx || n < 0 || (n > 0 && (!nodes || !pods || !timestamps_ns))) return fail(KE_ERR_INVALID, "ke_pods_assign");
   if (ctx) flush_mirror(ctx->c);
   for (int32_t i = 0; i < n; i++) {
@@ -666,14 +742,16 @@ int ke_pods_assign(ke_ctx* ctx, int32_t n, const int32_t* nodes, const ke_pod* p
 }
 
 int ke_pod_unassign(ke_ctx* ctx, int32_t node, int64_t uid) {
+  if (ctx) async_drain(ctx);
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
-  auto& v = ctx->c.nodes[node].asg;
-  for (size_t i = 0; i < v.size(); i++) {
-    if (v[i].pod.uid == uid) {
-      v.erase(v.begin() + (long)i);
-      ctx->c.nodes[node].dirty = true;
+  NodeState& ns = ctx->c.nodes[node];
+  for (size_t i = 0; i < ns.asg_uid.size(); i++) {
+    if (ns.asg_uid[i] == uid) {
+      ns.asg.erase(ns.asg.begin() + (long)i);
+      ns.asg_uid.erase(ns.asg_uid.begin() + (long)i);
+      ns.dirty = true;
       break;
     }
   }
@@ -681,6 +759,7 @@ int ke_pod_unassign(ke_ctx* ctx, int32_t node, int64_t uid) {
 }
 
 int ke_estimate_pod(ke_ctx* ctx, const ke_pod* pod, int64_t* est) {
+  if (ctx) async_drain(ctx);
   if (!ctx || !pod || !est) return fail(KE_ERR_INVALID, "ke_estimate_pod arguments");
   uint8_t present[KE_NRES];
   estimate_pod(ctx->c.cfg.loadaware, *pod, est, present);
@@ -691,6 +770,7 @@ int ke_estimate_pod(ke_ctx* ctx, const ke_pod* pod, int64_t* est) {
 
 int ke_eval(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, uint8_t* status, uint8_t* reason,
             int16_t* la_score, int16_t* numa_score, int16_t* ds_score, int16_t* total, int32_t* best) {
+  if (ctx) async_drain(ctx);
   if (!ctx) return fail(KE_ERR_INVALID, "null context");
   if (ctx) flush_mirror(ctx->c);
   int rc = check_pods(pods, n_pods, &ctx->c);
@@ -704,7 +784,7 @@ int ke_eval(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, uin
   return device_eval(&ctx->c, n_pods, pods, now_ns, status, reason, la_score, numa_score, ds_score, total, best);
 }
 
-int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int32_t* chosen, int32_t* score) {
+static int schedule_sync(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int32_t* chosen, int32_t* score) {
   if (!ctx || (n_pods > 0 && !chosen)) return fail(KE_ERR_INVALID, "ke_schedule arguments");
   using clk = std::chrono::steady_clock;
   auto tp = clk::now();
@@ -825,7 +905,7 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
       // patched on the device: re-derived from this mirror)
       if (cpus) host_cpuset_reserve(ns, make_dev_pod(c.cfg, pods[p]), cs);
     }
-    c.host_ms[7] = std::chrono::duration<double, std::milli>(clk::now() - tp).count();
+    c.host_ms[7] += std::chrono::duration<double, std::milli>(clk::now() - tp).count();
     const bool whole = s0 == 0 && s1 == n_pods;  // one segment: the last_* outputs are already whole
     if (!whole) {
       c.last_dev_alloc.resize((size_t)len, 0);  // (a segment without DeviceShare batches reads none back)
@@ -878,6 +958,92 @@ int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns,
   return KE_OK;
 }
 
+int ke_schedule(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int32_t* chosen, int32_t* score) {
+  if (ctx) async_drain(ctx);
+  return schedule_sync(ctx, n_pods, pods, now_ns, chosen, score);
+}
+
+int ke_schedule_submit(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int64_t* ticket) {
+  if (!ctx || n_pods < 0 || (n_pods > 0 && !pods) || !ticket) return fail(KE_ERR_INVALID, "ke_schedule_submit arguments");
+  using clk = std::chrono::steady_clock;
+  Context& c = ctx->c;
+  int in_flight = 0;
+  for (const AsyncCall& a : ctx->async) in_flight += a.fin != nullptr;
+  // at most one call in flight behind which this one is enqueued (two sets of call buffers)
+  for (AsyncCall& a : ctx->async)
+    if (in_flight >= 2 && a.fin) async_finish(ctx, a), in_flight--;
+  // a plain queue: no reservation-matched, NUMA-policy or quota pod, no staged reservation lists
+  bool plain = c.dev && n_pods > 0 && c.match_off.empty() && c.quotas.empty() && !c.numa_enabled;
+  for (int32_t p = 0; p < n_pods && plain; p++)
+    plain = pods[p].reservation_matched == KE_RSV_NONE && pods[p].numa_topology_policy == KE_NUMA_POLICY_NONE &&
+            pods[p].quota == 0;
+  if (plain) {
+    const auto tp = clk::now();
+    int rc = check_pods(pods, n_pods, &c);
+    if (rc) return rc;
+    rc = check_cpuset(ctx, pods, n_pods);  // (stages the pods' records)
+    if (rc) return rc;
+    plain = device_async_ok(&c, n_pods);
+    if (plain && in_flight > 0 && device_refresh_pending(&c, now_ns)) {
+      async_drain(ctx);  // rows to derive from the host state: it must carry the Reserves of the calls in flight
+      in_flight = 0;
+    }
+    if (plain) {
+      c.call_entry = tp;
+      c.host_ms[0] = std::chrono::duration<double, std::milli>(clk::now() - tp).count();
+      if (in_flight > 0) device_swap_call_buffers(&c);  // (the call in flight keeps its own)
+      AsyncCall a;
+      a.ticket = ctx->next_ticket++;
+      a.n = n_pods;
+      a.pods = pods;
+      a.now = now_ns;
+      a.device = true;
+      rc = device_schedule_enqueue(&c, n_pods, pods, now_ns, true, &a.fin);
+      if (rc) return rc;
+      *ticket = a.ticket;
+      ctx->async.push_back(std::move(a));
+      return KE_OK;
+    }
+  }
+  // anything else runs now, after every call in flight
+  async_drain(ctx);
+  AsyncCall a;
+  a.ticket = ctx->next_ticket++;
+  a.n = n_pods;
+  a.pods = pods;
+  a.now = now_ns;
+  a.chosen.assign((size_t)n_pods, -1);
+  a.score.assign((size_t)n_pods, 0);
+  const int rc = schedule_sync(ctx, n_pods, pods, now_ns, a.chosen.data(), a.score.data());
+  if (rc) return rc;
+  *ticket = a.ticket;
+  ctx->async.push_back(std::move(a));
+  return KE_OK;
+}
+
+int ke_schedule_wait(ke_ctx* ctx, int64_t ticket, int32_t* chosen, int32_t* score) {
+  if (!ctx) return fail(KE_ERR_INVALID, "ke_schedule_wait arguments");
+  size_t i = 0;
+  while (i < ctx->async.size() && ctx->async[i].ticket != ticket) i++;
+  if (i == ctx->async.size()) return fail(KE_ERR_NOT_FOUND, "ke_schedule_wait: no such submitted call");
+  if (ctx->async[i].n > 0 && !chosen) return fail(KE_ERR_INVALID, "ke_schedule_wait arguments");
+  for (size_t j = 0; j <= i; j++) async_finish(ctx, ctx->async[j]);  // (in submission order)
+  AsyncCall a = std::move(ctx->async[i]);
+  ctx->async.erase(ctx->async.begin() + (long)i);
+  if (a.rc) return fail(a.rc, a.msg);
+  std::copy(a.chosen.begin(), a.chosen.end(), chosen);
+  if (score) std::copy(a.score.begin(), a.score.end(), score);
+  if (a.device) {  // release records of this call (ke_last_allocations / ke_unreserve): the last collected call
+    Context& c = ctx->c;
+    c.last_chosen = a.chosen;
+    c.last_uid.resize((size_t)a.n);
+    c.last_quota.assign((size_t)a.n, 0);
+    c.last_resv.assign((size_t)a.n, 0);
+    for (int32_t p = 0; p < a.n; p++) c.last_uid[(size_t)p] = a.pods[p].uid;
+  }
+  return KE_OK;
+}
+
 // the release record of position p of the last ke_schedule
 static ke_pod_allocation last_allocation(const Context& c, int32_t p) {
   ke_pod_allocation a{};
@@ -907,6 +1073,7 @@ int ke_last_allocations(ke_ctx* ctx, int32_t n, ke_pod_allocation* out) {
 }
 
 int ke_pod_release(ke_ctx* ctx, const ke_pod* pod, const ke_pod_allocation* alloc, int32_t mode) {
+  if (ctx) async_drain(ctx);
   if (!ctx || !pod || !alloc) return fail(KE_ERR_INVALID, "ke_pod_release arguments");
   if (mode != KE_RELEASE_UNRESERVE && mode != KE_RELEASE_DELETE) return fail(KE_ERR_INVALID, "ke_pod_release mode");
   int rc = validate_pod(*pod);
@@ -949,6 +1116,7 @@ int ke_pod_release(ke_ctx* ctx, const ke_pod* pod, const ke_pod_allocation* allo
 }
 
 int ke_unreserve(ke_ctx* ctx, const ke_pod* pod, int32_t queue_pos) {
+  if (ctx) async_drain(ctx);
   if (!ctx || !pod) return fail(KE_ERR_INVALID, "ke_unreserve arguments");
   Context& c = ctx->c;
   if (queue_pos < 0 || queue_pos >= (int32_t)c.last_chosen.size())
@@ -987,6 +1155,7 @@ int ke_last_schedule_stats(ke_ctx* ctx, double* total_ms, int32_t* n_batches, do
 }
 
 int ke_set_profiling(ke_ctx* ctx, int32_t sample_every) {
+  if (ctx) async_drain(ctx);
   if (!ctx) return fail(KE_ERR_INVALID, "null context");
   int rc = require_device(ctx);
   if (rc) return rc;
@@ -1018,6 +1187,7 @@ int ke_last_kernel_stats_ex(ke_ctx* ctx, double* ms4 /* [8] */, int32_t* samples
 }
 
 int ke_debug_replay_phases(ke_ctx* ctx, double* cyc8) {
+  if (ctx) async_drain(ctx);
   if (!ctx || !cyc8) return fail(KE_ERR_INVALID, "ke_debug_replay_phases arguments");
   int rc = require_device(ctx);
   if (rc) return rc;
@@ -1031,6 +1201,7 @@ int ke_debug_spec_failed(ke_ctx* ctx, double* per_batch) {
 }
 
 int ke_debug_check_records(ke_ctx* ctx, int64_t now_ns, int64_t* mismatched_nodes) {
+  if (ctx) async_drain(ctx);
   if (!ctx || !mismatched_nodes) return fail(KE_ERR_INVALID, "ke_debug_check_records arguments");
   flush_mirror(ctx->c);
   int rc = require_device(ctx);
@@ -1039,6 +1210,7 @@ int ke_debug_check_records(ke_ctx* ctx, int64_t now_ns, int64_t* mismatched_node
 }
 
 int ke_set_pipeline(ke_ctx* ctx, int32_t on) {
+  if (ctx) async_drain(ctx);
   if (!ctx) return fail(KE_ERR_INVALID, "null context");
   int rc = require_device(ctx);
   if (rc) return rc;
@@ -1070,8 +1242,15 @@ int ke_debug_resolve_subphases(ke_ctx* ctx, double* sub5) {
   return KE_OK;
 }
 
+int ke_debug_resolve_wave1(ke_ctx* ctx, double* w4) {
+  if (!ctx || !w4) return fail(KE_ERR_INVALID, "ke_debug_resolve_wave1 arguments");
+  for (int i = 0; i < 4; i++) w4[i] = ctx->c.kstat_resolve_wave1_ms[i];
+  return KE_OK;
+}
+
 int ke_bench_eval_kernel(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t now_ns, int32_t iters,
                          double* avg_ms) {
+  if (ctx) async_drain(ctx);
   if (!ctx || !avg_ms) return fail(KE_ERR_INVALID, "ke_bench_eval_kernel arguments");
   if (ctx) flush_mirror(ctx->c);
   int rc = check_pods(pods, n_pods);
@@ -1088,6 +1267,7 @@ int ke_comm_unique_id(uint8_t* id, int32_t id_bytes) {
 }
 
 int ke_shard_init(ke_ctx* ctx, int32_t rank, int32_t world, const uint8_t* id) {
+  if (ctx) async_drain(ctx);
   if (!ctx) return fail(KE_ERR_INVALID, "null context");
   int rc = require_device(ctx);
   if (rc) return rc;
@@ -1095,6 +1275,7 @@ int ke_shard_init(ke_ctx* ctx, int32_t rank, int32_t world, const uint8_t* id) {
 }
 
 int ke_shard_range(ke_ctx* ctx, int32_t* lo, int32_t* hi) {
+  if (ctx) async_drain(ctx);
   if (!ctx || !lo || !hi) return fail(KE_ERR_INVALID, "ke_shard_range arguments");
   int rc = require_device(ctx);
   if (rc) return rc;
@@ -1108,6 +1289,7 @@ int ke_shard_range(ke_ctx* ctx, int32_t* lo, int32_t* hi) {
 int ke_debug_node_state(ke_ctx* ctx, int32_t node, ke_node* out, int32_t cpu_cap, ke_cpu* cpus, int32_t* n_cpus,
                         int32_t zone_cap, ke_numa_zone* zones, int32_t* n_zones, int32_t dev_cap, ke_device* devs,
                         int32_t* n_devs) {
+  if (ctx) async_drain(ctx);
   int rc = check_node(ctx, node);
   if (ctx) flush_mirror(ctx->c);
   if (rc) return rc;
@@ -1125,6 +1307,7 @@ int ke_debug_node_state(ke_ctx* ctx, int32_t node, ke_node* out, int32_t cpu_cap
 int64_t ke_debug_usage_bound(int64_t total, int64_t thr) { return total > 0 ? max_used_within(total, thr) : 0; }
 
 int ke_debug_rows(ke_ctx* ctx, int32_t n, int64_t now_ns, void* device_rows, void* host_rows) {
+  if (ctx) async_drain(ctx);
   if (!ctx || n < 0 || n > ctx->c.n_nodes) return fail(KE_ERR_INVALID, "ke_debug_rows arguments");
   if (ctx) flush_mirror(ctx->c);
   if (device_rows) {

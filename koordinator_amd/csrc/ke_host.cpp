@@ -7,6 +7,7 @@
 #include "ke_host.h"
 
 #include <algorithm>
+#include <thread>
 #include <climits>
 #include <cstddef>
 #include <cmath>
@@ -1746,9 +1747,10 @@ void host_cpuset_reserve(NodeState& ns, const DevPod& dp, const uint64_t* set) {
 void host_release_node(const ke_config& cfg, bool ext, NodeState& ns, const ke_pod& pod, const ke_pod_allocation& a,
                        const ke_pod_device_hints* h) {
   // LoadAware podAssignCache.unAssign (pod_assign_cache.go:126-136)
-  for (size_t i = 0; i < ns.asg.size(); i++)
-    if (ns.asg[i].pod.uid == pod.uid) {
+  for (size_t i = 0; i < ns.asg_uid.size(); i++)
+    if (ns.asg_uid[i] == pod.uid) {
       ns.asg.erase(ns.asg.begin() + (long)i);
+      ns.asg_uid.erase(ns.asg_uid.begin() + (long)i);
       break;
     }
   // framework NodeInfo.RemovePod: Requested (and the FitPlus (NonZero)Requested by resource id)
@@ -1831,38 +1833,56 @@ void host_release_node(const ke_config& cfg, bool ext, NodeState& ns, const ke_p
 }
 
 void flush_mirror(Context& c) {
-  for (const Context::PendingAssign& a : c.pending) {
+  // the device rows already carry these Reserves: the nodes' dirty flags stay as they are
+  auto apply = [&c](const Context::PendingAssign& a) {
     NodeState& ns = c.nodes[a.node];
     const ke_pod& pod = c.pending_pods[(size_t)a.idx];
-    const bool was_dirty = ns.dirty;
-    host_assign(c.cfg, ns, pod, a.ts);
+    host_assign(c.cfg, ns, pod, a.ts, false);
     ns.node.requested[KE_RES_CPU] += pod.requests[KE_RES_CPU];
     ns.node.requested[KE_RES_MEMORY] += pod.requests[KE_RES_MEMORY];
     ns.node.pod_count++;  // NodeInfo.AddPod
     if (c.ext_enabled) host_ext_reserve(ns, pod);
-    ns.dirty = was_dirty;  // the device row already carries this Reserve
+  };
+  const size_t n = c.pending.size();
+  // a large mirror (a whole queue's placements, random nodes: cache-miss bound) on worker threads, each taking the
+  // nodes of one residue in queue order -- a node's entries stay in order and no two threads share a node
+  const unsigned hw = std::thread::hardware_concurrency();
+  const int T = n >= 2048 ? (int)std::min<unsigned>(4, hw > 1 ? hw : 1) : 1;
+  if (T > 1) {
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; t++)
+      th.emplace_back([&, t]() {
+        for (const Context::PendingAssign& a : c.pending)
+          if (a.node % T == t) apply(a);
+      });
+    for (const Context::PendingAssign& a : c.pending)
+      if (a.node % T == 0) apply(a);
+    for (std::thread& x : th) x.join();
+  } else {
+    for (const Context::PendingAssign& a : c.pending) apply(a);
   }
   c.pending.clear();
   c.pending_pods.clear();
 }
 
-void host_assign(const ke_config& cfg, NodeState& ns, const ke_pod& pod, int64_t timestamp_ns) {
+void host_assign(const ke_config& cfg, NodeState& ns, const ke_pod& pod, int64_t timestamp_ns, bool mark_dirty) {
   if (pod.is_terminated) return;  // pod_assign_cache.go:90
   AssignedPod info{};
   info.pod = pod;
   estimate_pod(cfg.loadaware, pod, info.est, info.est_present);
   info.has_est = info.est_present[0] || info.est_present[1];
-  for (auto& e : ns.asg) {
-    if (e.pod.uid == pod.uid) {  // existing entry: refresh pod + estimate, keep timestamp
-      info.ts = e.ts;
-      e = info;
-      ns.dirty = true;
+  for (size_t i = 0; i < ns.asg_uid.size(); i++) {
+    if (ns.asg_uid[i] == pod.uid) {  // existing entry: refresh pod + estimate, keep timestamp
+      info.ts = ns.asg[i].ts;
+      ns.asg[i] = info;
+      if (mark_dirty) ns.dirty = true;
       return;
     }
   }
   info.ts = pod.has_scheduled ? pod.scheduled_transition_ns : timestamp_ns;
   ns.asg.push_back(info);
-  ns.dirty = true;
+  ns.asg_uid.push_back(pod.uid);
+  if (mark_dirty) ns.dirty = true;
 }
 
 }  // namespace ke

@@ -4,6 +4,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <string>
 #include <utility>
@@ -70,6 +71,7 @@ struct NodeState {
   std::vector<ke_pod_metric> pm;
   std::vector<ke_aggregated_usage> agg;
   std::vector<AssignedPod> asg;
+  std::vector<int64_t> asg_uid;  // asg[i].pod.uid: the uid scans of assign / unassign read 8 B an entry
   // NodeResourceTopology NUMA zones + the resource manager's allocation on them
   std::vector<ke_numa_zone> zones;
   // CPU topology + cpuset allocations (TopologyOptions.CPUTopology / ReservedCPUs / MaxRefCount,
@@ -153,6 +155,7 @@ struct Context {
   double kstat_resolve_prologue_ms = 0, kstat_resolve_loop_ms = 0;
   double kstat_resolve_phase_ms[6] = {0, 0, 0, 0, 0, 0};
   double kstat_resolve_sub_ms[5] = {0, 0, 0, 0, 0};  // ke_debug_resolve_subphases
+  double kstat_resolve_wave1_ms[4] = {0, 0, 0, 0};  // ke_debug_resolve_wave1
   int64_t kstat_numa_deferred = 0;  // BestEffort pairs the last ke_eval / ke_schedule left to k_numa_fallback
   int32_t kstat_samples = 0;
   // Host mirror of the LoadAware / NodeInfo part of the last ke_schedule's Reserves (the device rows
@@ -264,9 +267,16 @@ int64_t max_used_within(int64_t total, int64_t thr);
 int64_t usage_percent(int64_t used, int64_t total);
 
 // host mirror of Reserve (podAssignCache.assign + NodeInfo.Requested += requests)
-void host_assign(const ke_config& cfg, NodeState& ns, const ke_pod& pod, int64_t timestamp_ns);
+void host_assign(const ke_config& cfg, NodeState& ns, const ke_pod& pod, int64_t timestamp_ns, bool mark_dirty = true);
 // apply Context::pending (placements whose device rows are already patched: dirty flags unchanged)
 void flush_mirror(Context& c);
+// ke_schedule_submit / ke_schedule_wait (ke_kernels.hip): a call's enqueue part returns its completion, which waits
+// for the call's device work, writes the placements / scores and the call's statistics
+using DevFinish = std::function<int(int32_t* chosen, int32_t* score)>;
+int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, bool want_score, DevFinish* fin);
+void device_swap_call_buffers(Context* ctx);
+bool device_refresh_pending(const Context* ctx, int64_t now);
+bool device_async_ok(const Context* ctx, int32_t n_pods);
 
 // DeviceShare
 int validate_devices(int32_t n, const ke_device* devs);

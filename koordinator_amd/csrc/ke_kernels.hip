@@ -3205,11 +3205,17 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_plain(SoA s, int lo, int hi
   const int base = *batch_base;
   const int p0 = group * EVAL_PPB;
   const int np = min(batch_pods, p0 + EVAL_PPB) - p0;
+  // the group's pods in LDS once per block: the estimates / requests as doubles, and (without the ext terms) the
+  // flags and integer estimates / cpu request fast_total reads -- no scalar-memory load (and its wait) per pod
   __shared__ double s_pd[EVAL_PPB][4];
+  __shared__ int64_t s_pi[EVAL_PPB][3];
+  __shared__ uint32_t s_pf[EVAL_PPB];
   if ((int)threadIdx.x < 4 * np) {
     const int q = threadIdx.x >> 2, c = threadIdx.x & 3;
     const DevPod& pp = pods[base + p0 + q];
     s_pd[q][c] = (double)(c < 2 ? pp.est[c] : pp.req[c - 2]);
+    if (!EXT && c < 3) s_pi[q][c] = c < 2 ? pp.est[c] : pp.req[0];
+    if (!EXT && c == 3) s_pf[q] = pp.flags;
   }
   __syncthreads();
   if (i >= hi) return;
@@ -3217,10 +3223,21 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_plain(SoA s, int lo, int hi
   rec_load_plain(s.rec + (int64_t)i * NUM_RW, f);
   if (EXT && (k.flags & AF_EXT)) ext_load(s, i, k, f);
   fast_adopt(f, k);
+  uint16_t* const out = scores + (int64_t)p0 * score_stride + i;
   for (int q = 0; q < np; q++) {
-    const DevPod& pod = pods[base + p0 + q];
     const double ed[2] = {s_pd[q][0], s_pd[q][1]}, rd[2] = {s_pd[q][2], s_pd[q][3]};
-    scores[(int64_t)(p0 + q) * score_stride + i] = (uint16_t)(fast_total<EXT>(f, pod, ed, rd, k) + 1);
+    int32_t t;
+    if constexpr (EXT) {
+      t = fast_total<EXT>(f, pods[base + p0 + q], ed, rd, k);
+    } else {
+      DevPod pl;  // (fast_total<false> reads these fields only)
+      pl.flags = s_pf[q];
+      pl.est[0] = s_pi[q][0];
+      pl.est[1] = s_pi[q][1];
+      pl.req[0] = s_pi[q][2];
+      t = fast_total<false>(f, pl, ed, rd, k);
+    }
+    out[(int64_t)q * score_stride] = (uint16_t)(t + 1);
   }
 }
 
@@ -3231,8 +3248,15 @@ __global__ __launch_bounds__(EVAL_BLOCK) void k_eval_plain(SoA s, int lo, int hi
 template <bool EXT>
 __global__ __launch_bounds__(64) void k_patch(SoA s, const DevPod* __restrict__ pods, const int32_t* __restrict__ batch_base,
                                               KArgs k, const int32_t* __restrict__ tlist, uint16_t* __restrict__ scores,
-                                              int64_t score_stride) {
+                                              int64_t score_stride, const int32_t* __restrict__ done_wait,
+                                              int32_t* __restrict__ err) {
   const int j = blockIdx.x, t = threadIdx.x;
+  {  // batch b-2's done flag (each one-wave workgroup polls it: no separate wait kernel ahead of this one)
+    __shared__ int32_t s_go;
+    if (t == 0) s_go = wait_at_least(done_wait, 1, err);
+    __syncthreads();
+    if (!s_go) return;  // (a timed-out hand-off: the host discards the queue)
+  }
   const int n = ld_sc1(tlist);
   if (t >= n) return;
   const int node = ld_sc1(tlist + 1 + t);
@@ -4678,34 +4702,6 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
       }
     }
   };
-  // rows j and j1 (j1 < 0: none) against the slots c < j: mrow without T (the progressive S)
-  auto s_rows = [&](int j, int j1) {
-    const bool has1 = !EXT && j1 >= 0;
-    const DevPod p = L.pod[j];
-    const double ed[2] = {L.pd[j][0], L.pd[j][1]}, rd[2] = {L.pd[j][2], L.pd[j][3]};
-    uint32_t kc = 0, kc1 = 0;
-    if (has1) {
-      const DevPod p1 = L.pod[j1];
-      const double ed1[2] = {L.pd[j1][0], L.pd[j1][1]}, rd1[2] = {L.pd[j1][2], L.pd[j1][3]};
-      if (sv && lane < j) kc = make_key(fast_total<EXT>(slot, p, ed, rd, k), snode);
-      if (sv && lane < j1) kc1 = make_key(fast_total<EXT>(slot, p1, ed1, rd1, k), snode);
-    } else if (sv && lane < j) {
-      kc = make_key(fast_total<EXT>(slot, p, ed, rd, k), snode);
-    }
-    kc = wave_max_u32(kc);
-    kc1 = has1 ? wave_max_u32(kc1) : 0u;
-    if (lane == 0) {
-      L.sp.mrow[j] = kc;
-      if (has1) L.sp.mrow[j1] = kc1;
-    }
-    if (EXT && j1 >= 0) {  // (the ext slots: one chain a pass)
-      const DevPod p1 = L.pod[j1];
-      const double ed1[2] = {L.pd[j1][0], L.pd[j1][1]}, rd1[2] = {L.pd[j1][2], L.pd[j1][3]};
-      uint32_t k1 = (sv && lane < j1) ? make_key(fast_total<EXT>(slot, p1, ed1, rd1, k), snode) : 0u;
-      k1 = wave_max_u32(k1);
-      if (lane == 0) L.sp.mrow[j1] = k1;
-    }
-  };
   int32_t o_node = -1, o_score = -1;  // wave 0, lane j: pod j's placement
   int start = 0, win = B, rounds = 0, fetched = 0;
   const bool stamp = wave == 0 && lane == 0;  // phase stamps of the first round (ke_debug_resolve_phases)
@@ -4757,8 +4753,17 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
       }
     } else if (prog) {
       // ---- progressive R + S (waves 1..NW-1): once pod hi-1 of a chunk [lo, hi) is predicted, its slots are
-      // reserved and the rows (prev, hi] -- pods whose slots c < j are all known -- evaluated against them
+      // reserved and evaluated against every later pod of the window
       adopt_t();
+      uint64_t w_wait = 0, w_res = 0, w_rows = 0, w_t = __builtin_amdgcn_s_memrealtime();  // wave 1's stamps
+      // slot-major: a chunk's 16 slots are held four times a wave (lane l: slot lo + l % 16, group
+      // g = 4 (wave - 1) + l / 16 of GW), and group g evaluates its slot c against the pods j = c + 1 + g + GW t:
+      // every pair (c, j > c) of the chunk is evaluated once its slot is known, max-reduced into mrow[j] with an
+      // LDS atomic -- rows wait for no later prediction, so after the loop only the last chunk's pairs remain
+      constexpr int GW = 4 * (NW - 1);
+      const int g = 4 * (wave - 1) + (lane >> 4);
+      NodeFast pslot;
+      int pnode = -1;
       for (int lo = start; lo < end; lo += PCH) {
         const int hi = min(end, lo + PCH);
         if (lane == 0) {  // an LDS wait on wave 0 of the same workgroup (co-resident by construction), bounded
@@ -4773,9 +4778,52 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
             __builtin_amdgcn_s_sleep(1);
           }
         }
-        reserve_lanes(lo, hi, true);
-        const int r0 = lo == start ? start : lo + 1, r1 = min(hi + 1, end);  // rows [r0, r1)
-        for (int j = r0 + wave - 1; j < r1; j += 2 * (NW - 1)) s_rows(j, j + NW - 1 < r1 ? j + NW - 1 : -1);
+        uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        w_wait += t1 - w_t;
+        // lane l adopts slot c = lo + l % 16 and reserves pod c on it (lo is a multiple of 16: the first round
+        // starts at pod 0); lanes [lo, hi) keep it as their own slot for V and the later rounds
+        const int c = lo + (lane & 15);
+        pnode = c < hi ? ((volatile int32_t*)L.sp.xnode)[c] : -1;
+        const bool pv = pnode >= 0;
+        if (pv) {
+          rec_load_plain(s.rec + (int64_t)pnode * NUM_RW, pslot);
+          if (ext) ext_load(s, pnode, k, pslot);
+          fast_adopt(pslot, k);
+          const DevPod pc = L.pod[c];
+          const double ed[2] = {L.pd[c][0], L.pd[c][1]}, rd[2] = {L.pd[c][2], L.pd[c][3]};
+          fast_reserve(pslot, pc, ed, rd);
+          if (ext) ext_fast_reserve(pslot, pc, k);
+        }
+        if (lane >= lo && lane < hi) {
+          snode = pnode;
+          sv = pv;
+          if (pv) slot = pslot;
+        }
+        w_t = __builtin_amdgcn_s_memrealtime();
+        w_res += w_t - t1;
+        constexpr int RS = EXT ? 1 : 2;  // chains a pass
+        for (int j = c + 1 + g; pv && j < end; j += RS * GW) {
+          const DevPod p = L.pod[j];
+          const double ed[2] = {L.pd[j][0], L.pd[j][1]}, rd[2] = {L.pd[j][2], L.pd[j][3]};
+          const uint32_t kc = make_key(fast_total<EXT>(pslot, p, ed, rd, k), pnode);
+          uint32_t kc1 = 0u;
+          const int j1 = j + GW;
+          if (RS == 2 && j1 < end) {
+            const DevPod p1 = L.pod[j1];
+            const double ed1[2] = {L.pd[j1][0], L.pd[j1][1]}, rd1[2] = {L.pd[j1][2], L.pd[j1][3]};
+            kc1 = make_key(fast_total<EXT>(pslot, p1, ed1, rd1, k), pnode);
+          }
+          if (kc) atomicMax(&L.sp.mrow[j], kc);
+          if (kc1) atomicMax(&L.sp.mrow[j1], kc1);
+        }
+        t1 = __builtin_amdgcn_s_memrealtime();
+        w_rows += t1 - w_t;
+        w_t = t1;
+      }
+      if (wave == 1 && lane == 0) {  // ke_debug_resolve_waves: wave 1's polls, record loads + Reserves, rows
+        pst[13] = w_wait;
+        pst[14] = w_res | (w_rows << 32);
+        pst[15] = w_t;
       }
     } else if (tin) {
       adopt_t();
@@ -5003,7 +5051,7 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
     }
   }
   if (has_t && tid < B) L.sp.tver[tid] = -1;  // no pod's T max computed yet (replay_spec)
-  if (tid < B) L.sp.xnode[tid] = XN_PENDING;
+  if (tid < B) L.sp.xnode[tid] = XN_PENDING, L.sp.mrow[tid] = 0u;  // (the progressive S max-reduces into mrow)
   if (pub_done && tid == 0) {  // (wave 0 issued every store of the previous batch)
     drain_stores();
     st_sc1(pub_done, 1);
@@ -5027,7 +5075,7 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
     const uint64_t t = __builtin_amdgcn_s_memrealtime();
     for (int u = 1; u < 6; u++) pstamps[PST * batch_index + u] = t;
     for (int u = 8; u < 12; u++) pstamps[PST * batch_index + u] = t;
-    pstamps[PST * batch_index + 12] = 0;
+    for (int u = 12; u < 16; u++) pstamps[PST * batch_index + u] = 0;
   }
   if constexpr (!DS && !NUMA && !QUOTA) {  // plain batch: the speculative replay on every wave
     __builtin_amdgcn_s_setprio(3);
@@ -6030,6 +6078,11 @@ struct PinnedVec {
   const T& operator[](size_t i) const { return p[i]; }
   T* begin() { return p; }
   T* end() { return p + n; }
+  void swap(PinnedVec& o) {
+    std::swap(p, o.p);
+    std::swap(n, o.n);
+    std::swap(cap, o.cap);
+  }
   const T* begin() const { return p; }
   const T* end() const { return p + n; }
 };
@@ -6111,6 +6164,24 @@ struct DeviceState {
   // double the score matrix)
   hipStream_t estream2 = nullptr;
   hipEvent_t ev_sel2 = nullptr;
+  std::vector<hipEvent_t> tev;  // device_schedule's events (pool): span, the call's end per stream, samples
+  // the other call's buffers of two in flight (ke_schedule_submit): swapped with the fields of the same name
+  struct CallBufs {
+    PinnedVec<DevPod> host_pods;
+    DevPod* d_pods = nullptr;
+    int64_t pods_cap = 0;
+    int32_t *d_chosen = nullptr, *d_chosen_score = nullptr;
+    uint64_t* d_stamps = nullptr;
+    uint64_t* d_devalloc = nullptr;
+    int64_t* d_numaalloc = nullptr;
+    int64_t out_cap = 0;
+    uint64_t* d_cpusets = nullptr;
+    int64_t cpusets_cap = 0;
+    int32_t* d_sched = nullptr;
+    int64_t sched_cap = 0;
+    PinnedVec<uint8_t> h_out;
+    std::vector<hipEvent_t> tev;
+  } alt;
   uint16_t* d_scores2 = nullptr;
   uint32_t* d_split2 = nullptr;
   uint32_t* d_stale = nullptr;      // [2][MAX_BATCH][KSTALE] stale-snapshot candidate lists
@@ -6291,6 +6362,11 @@ void device_destroy(Context* ctx) {
   if (d->estream) (void)hipStreamDestroy(d->estream);
   if (d->estream2) (void)hipStreamDestroy(d->estream2);
   if (d->ev_sel2) (void)hipEventDestroy(d->ev_sel2);
+  for (auto& e : d->tev) (void)hipEventDestroy(e);
+  for (auto& e : d->alt.tev) (void)hipEventDestroy(e);
+  for (void* p : {(void*)d->alt.d_pods, (void*)d->alt.d_chosen, (void*)d->alt.d_chosen_score, (void*)d->alt.d_stamps,
+                  (void*)d->alt.d_devalloc, (void*)d->alt.d_numaalloc, (void*)d->alt.d_cpusets, (void*)d->alt.d_sched})
+    if (p) (void)hipFree(p);
   if (d->stream) (void)hipStreamDestroy(d->stream);
   delete d;
   ctx->dev = nullptr;
@@ -6787,7 +6863,60 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
   return KE_OK;
 }
 
+// The other call's buffers become this context's (ke_schedule_submit with a call in flight; host_pods, the pods,
+// outputs, stamps, hand-off words, readback staging and events are per call).
+void device_swap_call_buffers(Context* ctx) {
+  DeviceState* d = ctx->dev;
+  DeviceState::CallBufs& a = d->alt;
+  d->host_pods.swap(a.host_pods);
+  std::swap(d->d_pods, a.d_pods);
+  std::swap(d->pods_cap, a.pods_cap);
+  std::swap(d->d_chosen, a.d_chosen);
+  std::swap(d->d_chosen_score, a.d_chosen_score);
+  std::swap(d->d_stamps, a.d_stamps);
+  std::swap(d->d_devalloc, a.d_devalloc);
+  std::swap(d->d_numaalloc, a.d_numaalloc);
+  std::swap(d->out_cap, a.out_cap);
+  std::swap(d->d_cpusets, a.d_cpusets);
+  std::swap(d->cpusets_cap, a.cpusets_cap);
+  std::swap(d->d_sched, a.d_sched);
+  std::swap(d->sched_cap, a.sched_cap);
+  d->h_out.swap(a.h_out);
+  d->tev.swap(a.tev);
+}
+
+// whether the next call's device_refresh would upload rows (derived from the host state, which lacks the Reserves
+// of a call still in flight) or change a device table
+bool device_refresh_pending(const Context* ctx, int64_t now) {
+  if (ctx->ptab_dirty || !(now < ctx->min_valid_until && ctx->n_nodes == ctx->clean_n_nodes)) return true;
+  if (g_dirty_epoch.load(std::memory_order_relaxed) == ctx->clean_epoch) return false;
+  for (int32_t i : ctx->dirty_list)  // (the incremental refresh visits these; a clean one derives nothing)
+    if (i < ctx->n_nodes && ctx->nodes[(size_t)i].dirty) return true;
+  return false;
+}
+
+// a plain queue (no DeviceShare / cpuset / hinted pod, no NUMA or quota state, unsharded, pipelined) runs without a
+// host round trip between its launches: it may be submitted behind a call in flight
+bool device_async_ok(const Context* ctx, int32_t n_pods) {
+  const DeviceState* d = ctx->dev;
+  if (!d || d->world > 1 || d->comm || !d->pipeline || d->numa_alloc || !ctx->quotas.empty() || ctx->n_nodes <= 0)
+    return false;
+  if (ctx->n_bind_nodes > 0 || !ctx->rsv_pairs.empty() || ctx->rsv_affinity || !ctx->rsv_ovr.empty()) return false;
+  if ((int64_t)ctx->staged.size() != n_pods) return false;
+  for (const DevPod& q : ctx->staged)
+    if (q.flags & (PF_DS | PF_CPUSET | PF_DS_HINT)) return false;
+  return true;
+}
+
 int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t* chosen, int32_t* score) {
+  DevFinish fin;
+  const int rc = device_schedule_enqueue(ctx, n_pods, pods, now, score != nullptr, &fin);
+  if (rc || !fin) return rc;
+  return fin(chosen, score);
+}
+
+int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, bool want_score,
+                            DevFinish* fin) {
   DeviceState* d = ctx->dev;
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
@@ -6954,22 +7083,24 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   HIP_OK(hipMemsetAsync(d_fst, 0, sizeof(uint64_t) * 2 * n_batches, d->stream));
   HIP_OK(hipMemsetAsync(d->soa.kerr, 0, sizeof(int32_t), d->stream));
   HIP_OK(hipMemsetAsync(d->d_parts_done, 0, sizeof(int32_t) * 2 * MAX_BATCH, d->stream));  // (an aborted launch's counts)
-  hipEvent_t e0, e1;
-  HIP_OK(hipEventCreate(&e0));
-  HIP_OK(hipEventCreate(&e1));
+  // sampled per-kernel HIP event pairs (ke_set_profiling) on the eval stream: eval, select
+  constexpr int PE = 4;  // eval start, eval end, select end, select start (after k_patch and its wait)
+  const int every = d->profile_every;
+  // the call's timing events (the whole span, the samples) come from the context's pool: creating them per call
+  // cost the host ~3 us an event
+  const size_t n_tev = 5 + (every > 0 ? (size_t)((n_batches + every - 1) / every) * PE : 0);
+  while (d->tev.size() < n_tev) {
+    hipEvent_t e;
+    HIP_OK(hipEventCreate(&e));
+    d->tev.push_back(e);
+  }
+  hipEvent_t e0 = d->tev[0], e1 = d->tev[1];
+  const hipEvent_t done_ev[3] = {d->tev[2], d->tev[3], d->tev[4]};  // the call's end on each stream
+  std::vector<hipEvent_t> ev(d->tev.begin() + 5, d->tev.begin() + (long)n_tev);
   HIP_OK(hipEventRecord(e0, d->stream));
   hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, d->stream, d->d_stamps);
   HIP_OK(hipEventRecord(d->ev_start, d->stream));
   HIP_OK(hipStreamWaitEvent(d->estream, d->ev_start, 0));
-  // sampled per-kernel HIP event pairs (ke_set_profiling) on the eval stream: eval, select
-  constexpr int PE = 4;  // eval start, eval end, select end, select start (after k_patch and its wait)
-  const int every = d->profile_every;
-  std::vector<hipEvent_t> ev;
-  if (every > 0) {
-    const int samples = (n_batches + every - 1) / every;
-    ev.resize((size_t)samples * PE);
-    for (auto& e : ev) HIP_OK(hipEventCreate(&e));
-  }
   const bool sharded = d->world > 1 || d->comm;
   uint64_t* estamps = d->d_stamps + (PST + 1) * ((int64_t)n_pods + 2);  // eval start of each batch
   constexpr int R = DeviceState::EV_RING;
@@ -7052,11 +7183,9 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
         }
       }
       if (prof) HIP_OK(hipEventRecord(pe[1], es));
-      if (pwait) {  // the nodes batch b-2 changed, once it is done (k_patch)
-        hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), d->excl_lds, es, nullptr, 0, pwait, d_err, nullptr);
+      if (pwait)  // the nodes batch b-2 changed, once it is done (k_patch waits for the flag)
         hipLaunchKernelGGL(((k.flags & AF_EXT) ? k_patch<true> : k_patch<false>), dim3((unsigned)bp), dim3(64), d->excl_lds, es,
-                           d->soa, d->d_pods, bbase, k, ptl, scores, d->capacity);
-      }
+                           d->soa, d->d_pods, bbase, k, ptl, scores, d->capacity, pwait, d_err);
       if (ds && sharded && !d->loopback)  // DefaultNormalizeScore's max over the feasible nodes of all ranks
         RCCL_OK(ncclAllReduce(d->d_dsmax, d->d_dsmax, 1, ncclUint32, ncclMax, d->comm, es));
       if (prof) HIP_OK(hipEventRecord(pe[3], es));
@@ -7232,7 +7361,9 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   HIP_OK(hipGetLastError());
   ctx->last_enqueue_ms = ctx->host_ms[4] = ms_since(host_t0);
   tp = clk::now();
+  const auto t_fl = clk::now();
   flush_mirror(*ctx);  // the previous call's deferred host mirror, while the device works
+  const double flush_ms = ms_since(t_fl);
   HIP_OK(hipEventRecord(e1, d->stream));
   // The call's outputs go to one page-locked staging area (async copies, no host wait) and are copied out after
   // the synchronisation; allocations none of the call's batches can make are not read back (zero).
@@ -7246,7 +7377,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     off = (off + bytes + 15) & ~(size_t)15;
     return o;
   };
-  const size_t o_chosen = take((size_t)out_bytes), o_score = take(score ? (size_t)out_bytes : 0),
+  const size_t o_chosen = take((size_t)out_bytes), o_score = take(want_score ? (size_t)out_bytes : 0),
                o_dev = take(any_ds ? 8 * np : 0), o_cs = take(any_cpu ? 32 * np : 0),
                o_vf = take(vf_out ? 2 * DS_MINORS * np : 0), o_numa = take(numa ? 8 * 16 * np : 0), o_err = take(8),
                o_fst = take(16 * nb), o_dcnt = take(numa ? 4 * nb : 0), o_st = take(8 * (nb + 1)),
@@ -7258,7 +7389,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     return KE_OK;
   };
   if ((rc = d2h(o_chosen, d->d_chosen, (size_t)out_bytes))) return rc;
-  if (score && (rc = d2h(o_score, d->d_chosen_score, (size_t)out_bytes))) return rc;
+  if (want_score && (rc = d2h(o_score, d->d_chosen_score, (size_t)out_bytes))) return rc;
   if (any_ds && (rc = d2h(o_dev, d->d_devalloc, 8 * np))) return rc;
   if (any_cpu && (rc = d2h(o_cs, d->d_cpusets, 32 * np))) return rc;
   if (vf_out && (rc = d2h(o_vf, d->d_vfo, 2 * DS_MINORS * np))) return rc;
@@ -7269,6 +7400,20 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   if ((rc = d2h(o_st, d->d_stamps, 8 * (nb + 1))) || (rc = d2h(o_pst, d->d_stamps + (n_pods + 2), 8 * PST * nb)) ||
       (rc = d2h(o_est, estamps, 8 * nb)))
     return rc;
+  // the call's end on every stream: its completion waits for these events, not for the streams (a submission
+  // behind it may already be queued on them)
+  HIP_OK(hipEventRecord(done_ev[0], d->stream));
+  HIP_OK(hipEventRecord(done_ev[1], d->estream));
+  if (d->estream2) HIP_OK(hipEventRecord(done_ev[2], d->estream2));
+  double enq_ms[5];
+  for (int i = 0; i < 5; i++) enq_ms[i] = ctx->host_ms[i];
+  const auto entry = ctx->call_entry;
+  *fin = [=, batches = std::move(batches), bases = std::move(bases), run_end = std::move(run_end),
+          ev = std::move(ev)](int32_t* chosen, int32_t* score) mutable -> int {
+  HIP_OK(hipSetDevice(d->device));
+  auto tp = clk::now();
+  for (int i = 0; i < 5; i++) ctx->host_ms[i] = enq_ms[i];
+  ctx->host_ms[7] = flush_ms;  // (ke_schedule adds its own part of the mirror)
   std::vector<uint64_t> st(nb + 1), pst(PST * nb), est(nb), fst(2 * nb);
   std::vector<uint32_t> dcnt(numa ? nb : 0);
   int32_t herr = 0, kerr = 0;
@@ -7276,12 +7421,12 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   // ke_schedule records which of them were placed)
   ctx->pending_base = (int64_t)ctx->pending_pods.size();
   ctx->pending_pods.insert(ctx->pending_pods.end(), pods, pods + n_pods);
-  HIP_OK(hipStreamSynchronize(d->stream));
-  HIP_OK(hipStreamSynchronize(d->estream));
-  if (d->estream2) HIP_OK(hipStreamSynchronize(d->estream2));
+  HIP_OK(hipEventSynchronize(done_ev[0]));
+  HIP_OK(hipEventSynchronize(done_ev[1]));
+  if (d->estream2) HIP_OK(hipEventSynchronize(done_ev[2]));
   const auto t_sync = clk::now();
   std::memcpy(chosen, h + o_chosen, (size_t)out_bytes);
-  if (score) std::memcpy(score, h + o_score, (size_t)out_bytes);
+  if (score && want_score) std::memcpy(score, h + o_score, (size_t)out_bytes);
   if (any_ds) {
     ctx->last_dev_alloc.resize(np);
     std::memcpy(ctx->last_dev_alloc.data(), h + o_dev, 8 * np);
@@ -7316,22 +7461,14 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   if (herr) {
     if (d->d_chg)  // an abandoned replay may have left bits set
       (void)hipMemset(d->d_chg, 0, sizeof(uint32_t) * (d->capacity + 31) / 32);
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    for (auto& e : ev) (void)hipEventDestroy(e);
     return fail(KE_ERR_DEVICE, "pipelined schedule: a device-side hand-off timed out (placements invalid)");
   }
   if (kerr & (KERR_HINT_ROUTE | KERR_LDS_WAIT)) {  // internal errors: the placements are not the reference's
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    for (auto& e : ev) (void)hipEventDestroy(e);
     return fail(KE_ERR_DEVICE, (kerr & KERR_LDS_WAIT) ? "internal: a replay LDS wait expired (placements invalid)"
                                                       : "internal: a hinted pod reached a kernel without the hint path");
   }
   float ms = 0;
   HIP_OK(hipEventElapsedTime(&ms, e0, e1));
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   ctx->last_total_ms = ms;
   ctx->last_pipelined = n_pipelined;
   // s_memrealtime ticks -> ms, calibrated against the event-timed span of the whole queue
@@ -7347,7 +7484,7 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
   // the device stamps placed on the host clock by aligning the last one with the return of the final
   // synchronisation (later than the true end: an upper bound)
   {
-    const double sync_ms = std::chrono::duration<double, std::milli>(t_sync - ctx->call_entry).count();
+    const double sync_ms = std::chrono::duration<double, std::milli>(t_sync - entry).count();
     ctx->last_pod_lat.resize((size_t)n_pods);
     for (int b = 0, p0 = 0; b < n_batches; b++) {  // (a DeviceShare batch cut and re-run covers its first part too)
       const double lat = sync_ms - (double)(st[n_batches] - st[b + 1]) * ms_per_tick;
@@ -7397,6 +7534,20 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     }
     for (int i = 0; i < 4; i++) ctx->kstat_resolve_sub_ms[i] = ns ? sub[i] * ms_per_tick / ns : 0;
     ctx->kstat_resolve_sub_ms[4] = nt ? (double)hits / nt : 0;
+    // the progressive S of wave 1 (batches with helper T maxima): its polls, record loads + Reserves, rows, and
+    // its end after the T set-up
+    double wv[4] = {0, 0, 0, 0};
+    int nw = 0;
+    for (int b = 0; b < n_batches; b++) {
+      const uint64_t* p = &pst[PST * (size_t)b];
+      if (!(p[1] > p[4]) || !in_run_t[(size_t)b] || p[15] <= p[8]) continue;
+      nw++;
+      wv[0] += (double)p[13];
+      wv[1] += (double)(p[14] & 0xffffffffu);
+      wv[2] += (double)(p[14] >> 32);
+      wv[3] += (double)(p[15] - p[8]);
+    }
+    for (int i = 0; i < 4; i++) ctx->kstat_resolve_wave1_ms[i] = nw ? wv[i] * ms_per_tick / nw : 0;
   }
   ctx->kstat_numa_deferred = 0;
   for (uint32_t c : dcnt) ctx->kstat_numa_deferred += c;
@@ -7439,12 +7590,13 @@ int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t no
     ctx->kstat_select_ms += b;
     ctx->kstat_samples++;
   }
-  for (auto& e : ev) (void)hipEventDestroy(e);
   if (ctx->kstat_samples) {
     ctx->kstat_eval_ms /= ctx->kstat_samples;
     ctx->kstat_select_ms /= ctx->kstat_samples;
   }
   ctx->host_ms[6] = ms_since(tp);
+  return KE_OK;
+  };
   return KE_OK;
 }
 

@@ -38,6 +38,7 @@ class Evaluator:
         self._check(self.lib.ke_create(C.byref(cfg), C.byref(h)))
         self.h = h
         self._last_n, self._last_out = 0, {}
+        self._inflight = {}  # ticket -> the submitted pod array (ke_schedule_submit reads it until the wait)
 
     # ---- plumbing --------------------------------------------------------------------------
     def _check(self, rc):
@@ -260,6 +261,27 @@ class Evaluator:
         self._last_n, self._last_out = len(pods), {}  # the per-pod allocations are read on first access
         return chosen, score
 
+    def submit(self, pods, now_ns):
+        """ke_schedule_submit: enqueue a queue slice behind the calls in flight; returns its ticket (wait() collects
+        it).  The pod array is kept alive here until then."""
+        pods = as_pod_array(pods)
+        t = C.c_int64()
+        self._check(self.lib.ke_schedule_submit(self.h, len(pods), abi.ptr(pods), int(now_ns), C.byref(t)))
+        self._inflight[t.value] = pods
+        return t.value
+
+    def wait(self, ticket):
+        """ke_schedule_wait: (chosen, score) of a submitted slice, as schedule() returns them."""
+        pods = self._inflight[ticket]
+        chosen = np.zeros(len(pods), np.int32)
+        score = np.zeros(len(pods), np.int32)
+        try:
+            self._check(self.lib.ke_schedule_wait(self.h, int(ticket), abi.ptr(chosen), abi.ptr(score)))
+        finally:
+            del self._inflight[ticket]
+        self._last_n, self._last_out = len(pods), {}
+        return chosen, score
+
     def _last(self, name, shape, dtype, fn):
         if name not in self._last_out:
             a = np.zeros(shape, dtype)
@@ -373,6 +395,8 @@ class Evaluator:
         self._check(self.lib.ke_debug_resolve_phases(self.h, abi.ptr(ph)))
         sub = np.zeros(5, np.float64)
         self._check(self.lib.ke_debug_resolve_subphases(self.h, abi.ptr(sub)))
+        w1 = np.zeros(4, np.float64)
+        self._check(self.lib.ke_debug_resolve_wave1(self.h, abi.ptr(w1)))
         return {"eval_ms": ms4[0], "select_ms": ms4[1], "fixup_ms": ms4[2], "resolve_ms": ms4[3], "samples": n.value,
                 "pipelined_batches": npipe.value, "enqueue_ms": ms4[4], "handoff_ms": ms4[5],
                 "rows_fetched": ms4[6], "rows_changed": ms4[7], "spec_failed_rounds": sf.value,
@@ -380,7 +404,8 @@ class Evaluator:
                 "resolve_phases_ms": dict(zip(["prologue", "spec_predict", "spec_reserve_eval", "spec_verify", "spec_later_rounds", "writeback",
                                                "sub_t_setup", "sub_predict_loop", "sub_t_rows_wave1", "sub_reserve_R",
                                                "t_helper_hit"],
-                                              ph.tolist() + sub.tolist()))}
+                                              ph.tolist() + sub.tolist())),
+                "resolve_wave1_ms": dict(zip(["wait", "reserve", "rows", "end"], w1.tolist()))}
 
     def bench_eval_kernel(self, pods, now_ns, iters):
         pods = as_pod_array(pods)
