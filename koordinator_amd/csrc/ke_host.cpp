@@ -7,7 +7,6 @@
 #include "ke_host.h"
 
 #include <algorithm>
-#include <thread>
 #include <climits>
 #include <cstddef>
 #include <cmath>
@@ -1843,23 +1842,18 @@ void flush_mirror(Context& c) {
     ns.node.pod_count++;  // NodeInfo.AddPod
     if (c.ext_enabled) host_ext_reserve(ns, pod);
   };
+  // random nodes: cache-miss bound, so the node records (vector headers) are prefetched 16 entries ahead and their
+  // assign-cache arrays 8 ahead (worker threads were measured slower: the allocator's locks)
   const size_t n = c.pending.size();
-  // a large mirror (a whole queue's placements, random nodes: cache-miss bound) on worker threads, each taking the
-  // nodes of one residue in queue order -- a node's entries stay in order and no two threads share a node
-  const unsigned hw = std::thread::hardware_concurrency();
-  const int T = n >= 2048 ? (int)std::min<unsigned>(4, hw > 1 ? hw : 1) : 1;
-  if (T > 1) {
-    std::vector<std::thread> th;
-    for (int t = 1; t < T; t++)
-      th.emplace_back([&, t]() {
-        for (const Context::PendingAssign& a : c.pending)
-          if (a.node % T == t) apply(a);
-      });
-    for (const Context::PendingAssign& a : c.pending)
-      if (a.node % T == 0) apply(a);
-    for (std::thread& x : th) x.join();
-  } else {
-    for (const Context::PendingAssign& a : c.pending) apply(a);
+  for (size_t k = 0; k < n; k++) {
+    if (k + 16 < n) __builtin_prefetch(&c.nodes[c.pending[k + 16].node].asg, 1);
+    if (k + 8 < n) {
+      const NodeState& q = c.nodes[c.pending[k + 8].node];
+      __builtin_prefetch(q.asg_uid.data(), 0);
+      __builtin_prefetch(q.asg.data() + q.asg.size(), 1);
+      __builtin_prefetch(&q.node.requested[0], 1);
+    }
+    apply(c.pending[k]);
   }
   c.pending.clear();
   c.pending_pods.clear();
@@ -1868,7 +1862,12 @@ void flush_mirror(Context& c) {
 void host_assign(const ke_config& cfg, NodeState& ns, const ke_pod& pod, int64_t timestamp_ns, bool mark_dirty) {
   if (pod.is_terminated) return;  // pod_assign_cache.go:90
   AssignedPod info{};
-  info.pod = pod;
+  info.pod.pod_key = pod.pod_key;
+  info.pod.custom_seconds_after_scheduled = pod.custom_seconds_after_scheduled;
+  info.pod.custom_seconds_after_initialized = pod.custom_seconds_after_initialized;
+  info.pod.initialized_transition_ns = pod.initialized_transition_ns;
+  info.pod.priority_class = pod.priority_class;
+  info.pod.has_initialized = pod.has_initialized;
   estimate_pod(cfg.loadaware, pod, info.est, info.est_present);
   info.has_est = info.est_present[0] || info.est_present[1];
   for (size_t i = 0; i < ns.asg_uid.size(); i++) {

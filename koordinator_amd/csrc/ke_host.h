@@ -16,8 +16,14 @@
 namespace ke {
 
 // One podAssignCache entry (pkg/scheduler/plugins/loadaware/pod_assign_cache.go:45-49).
+// podAssignCache's podAssignInfo (pod_assign_cache.go:41-47): the pod fields estimatedAssignedPodUsed reads
 struct AssignedPod {
-  ke_pod pod;
+  struct {
+    int64_t pod_key;
+    int64_t custom_seconds_after_scheduled, custom_seconds_after_initialized, initialized_transition_ns;
+    int32_t priority_class;
+    uint8_t has_initialized;
+  } pod;
   int64_t ts;
   int64_t est[KE_NRES];
   uint8_t est_present[KE_NRES];
