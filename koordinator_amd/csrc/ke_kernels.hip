@@ -3764,8 +3764,12 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
                                                          uint32_t* __restrict__ mcand = nullptr,
                                                          int32_t* __restrict__ mcnt = nullptr,
                                                          int32_t* __restrict__ parts_done = nullptr,
-                                                         int32_t* __restrict__ ready = nullptr) {
+                                                         int32_t* __restrict__ ready = nullptr,
+                                                         int32_t* __restrict__ started = nullptr) {
   uint32_t* const gath = cand;
+  // the batch's selection is under way (the other eval stream's next eval waits for this: its workgroups then find
+  // these resident instead of queueing behind the whole eval grid)
+  if (started && (blockIdx.x | blockIdx.y | threadIdx.x) == 0) st_sc1(started, 1);
   if (!DS && gridDim.y > 1) {
     const int part = select_part(lo, hi, gridDim.y);
     lo = min(hi, lo + (int)blockIdx.y * part);
@@ -7063,9 +7067,9 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
     if (e - b >= 2) run_end[b] = e;
     b = e;
   }
-  // device: bases [n+1], ready [n], done [n], error word, T-helper counts [n]; fixup stamps [2n]; the T
-  // helpers' lists and maxima (THelp)
-  const int64_t sched_words = 4 * ((int64_t)n_batches + 1) + 1;
+  // device: bases [n+1], ready [n], done [n], error word, T-helper counts [n], select-started flags [n]; fixup
+  // stamps [2n]; the T helpers' lists and maxima (THelp)
+  const int64_t sched_words = 5 * ((int64_t)n_batches + 1) + 1;
   constexpr int64_t THELP_WORDS = 2 * (1 + MAX_BATCH) + 2 * MAX_BATCH;
   rc = ensure((void**)&d->d_sched, &d->sched_cap,
               sizeof(int32_t) * sched_words + sizeof(uint64_t) * 2 * n_batches + 8 + sizeof(int32_t) * THELP_WORDS);
@@ -7075,6 +7079,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   int32_t* d_done = d_ready + n_batches + 1;
   int32_t* d_err = d_done + n_batches + 1;
   int32_t* d_tready = d_err + 1;
+  int32_t* d_sstart = d_tready + n_batches + 1;
   uint64_t* d_fst = reinterpret_cast<uint64_t*>(d->d_sched + ((sched_words + 1) & ~1LL));
   int32_t* d_tlist = reinterpret_cast<int32_t*>(d_fst + 2 * n_batches);
   uint32_t* d_tmx = reinterpret_cast<uint32_t*>(d_tlist + 2 * (1 + MAX_BATCH));
@@ -7114,7 +7119,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   bool published = false;
   auto eval_select = [&](int b, bool pipe, hipStream_t es, const int32_t* dwait = nullptr,
                          int32_t* rpub = nullptr, bool alt = false, const int32_t* pwait = nullptr,
-                         const int32_t* ptl = nullptr) -> int {
+                         const int32_t* ptl = nullptr, int32_t* sstart = nullptr) -> int {
     published = false;
     uint16_t* const scores = alt ? d->d_scores2 : d->d_scores;  // (the second eval stream's buffers)
     uint32_t* const split = alt ? d->d_split2 : d->d_split;
@@ -7194,7 +7199,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
         const bool rc = select_seg(slo, shi) <= SEL_RC * 512;
         auto sel = ds ? (rc ? k_select<true, SEL_RC> : k_select<true, 0>) : (rc ? k_select<false, SEL_RC> : k_select<false, 0>);
         hipLaunchKernelGGL(sel, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, es, scores, d->capacity, slo, shi, cand,
-                           cnt, d->d_dsraw, d->d_dsmax, k.wp_ds, kext, L, (int64_t)0, nullptr, nullptr, nullptr, pub);
+                           cnt, d->d_dsraw, d->d_dsmax, k.wp_ds, kext, L, (int64_t)0, nullptr, nullptr, nullptr, pub, sstart);
       };
       // a plain batch over many nodes: its pods' selections split over several workgroups each (>= 256
       // workgroups in all, parts of >= 4096 nodes), merged by k_merge
@@ -7211,7 +7216,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
         hipLaunchKernelGGL((rc ? k_select<false, SEL_RC> : k_select<false, 0>), dim3((unsigned)bp, (unsigned)parts),
                            dim3(SELECT_BLOCK), 0, es, scores, d->capacity, 0, (int)N, split,
                            reinterpret_cast<int32_t*>(split + MAX_BATCH * L), d->d_dsraw, d->d_dsmax, k.wp_ds,
-                           kext, L, (int64_t)gw, lists, lists_cnt, pdone, rpub);  // the last part merges
+                           kext, L, (int64_t)gw, lists, lists_cnt, pdone, rpub, sstart);  // the last part merges
         published = rpub != nullptr;
       } else if (!sharded) {
         select(0, N, lists, lists_cnt, ds ? nullptr : rpub);
@@ -7284,8 +7289,13 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
           hipStream_t es = alt ? d->estream2 : d->estream;
           // two eval streams: batch q's eval waits only for batch q-3, k_patch brings in batch q-2's changed nodes
           const bool patch = two_es && d->eval_patch && q - 2 >= r0;
-          rc = eval_select(q, true, es, q - (patch ? 3 : 2) >= r0 ? d_done + (q - (patch ? 3 : 2)) : nullptr, d_ready + q,
-                           alt, patch ? d_done + (q - 2) : nullptr, d_tlist + ((q - 2) & 1) * (1 + MAX_BATCH));
+          // with k_patch, batch q's eval waits for batch q-1's select to start (it followed k_patch(q-1), which
+          // waited for done[q-3]): the select's workgroups are resident before this eval's grid takes the CUs
+          const bool after_sel = two_es && d->eval_patch;
+          const int32_t* ew = after_sel ? (q - 1 >= r0 ? d_sstart + (q - 1) : nullptr)
+                                        : (q - 2 >= r0 ? d_done + (q - 2) : nullptr);
+          rc = eval_select(q, true, es, ew, d_ready + q, alt, patch ? d_done + (q - 2) : nullptr,
+                           d_tlist + ((q - 2) & 1) * (1 + MAX_BATCH), after_sel ? d_sstart + q : nullptr);
           if (rc) return rc;
           if (!published)
             hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), d->excl_lds, es, d_ready + q, (int32_t)batches[q].pods, nullptr,
