@@ -3767,9 +3767,6 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
                                                          int32_t* __restrict__ ready = nullptr,
                                                          int32_t* __restrict__ started = nullptr) {
   uint32_t* const gath = cand;
-  // the batch's selection is under way (the other eval stream's next eval waits for this: its workgroups then find
-  // these resident instead of queueing behind the whole eval grid)
-  if (started && (blockIdx.x | blockIdx.y | threadIdx.x) == 0) st_sc1(started, 1);
   if (!DS && gridDim.y > 1) {
     const int part = select_part(lo, hi, gridDim.y);
     lo = min(hi, lo + (int)blockIdx.y * part);
@@ -3777,6 +3774,9 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
     cand += (int64_t)blockIdx.y * ystride;
     cand_cnt += (int64_t)blockIdx.y * ystride;
   }
+  // this workgroup of the batch's selection is resident: the other eval stream's next eval waits for all of them,
+  // so its grid never holds the CUs a workgroup of this select still needs
+  if (started && threadIdx.x == 0) __hip_atomic_fetch_add(started, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __shared__ int16_t s_lut[DS ? MAX_DS_RAW + 1 : 1];
   __shared__ int32_t s_dscnt;
   DsNorm dn{DS ? dsraw + (int64_t)blockIdx.x * score_stride : dsraw, s_lut};
@@ -4230,7 +4230,7 @@ __global__ __launch_bounds__(FIX_BLOCK) void k_fixup(SoA s, const DevPod* __rest
 // slots from the replay's latency-bound waves.
 constexpr unsigned EXCL_LDS = 1024;
 __global__ void k_handoff(int32_t* __restrict__ ready, int32_t n, const int32_t* __restrict__ done_wait,
-                          int32_t* __restrict__ err, uint64_t* __restrict__ fstamp) {
+                          int32_t* __restrict__ err, uint64_t* __restrict__ fstamp, int32_t want) {
   if (threadIdx.x != 0) return;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   if (ready) __hip_atomic_store(ready, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -4238,7 +4238,7 @@ __global__ void k_handoff(int32_t* __restrict__ ready, int32_t n, const int32_t*
     fstamp[0] = t0;
     fstamp[1] = t0 + 1;
   }
-  if (done_wait) (void)wait_at_least(done_wait, 1, err);  // a timeout sets *err: the host discards the queue
+  if (done_wait) (void)wait_at_least(done_wait, want, err);  // a timeout sets *err: the host discards the queue
 }
 
 // --- resolve: one wavefront replays the batch sequentially -------------------------------------
@@ -4425,6 +4425,8 @@ struct THelp {
   int32_t* tready;  // [batch]: helpers done with the batch (relaxed agent adds)
   int H;            // helper workgroups (0: none)
   int ign;          // test hook: the Reserve workgroup ignores the helpers' maxima (its own rows after the barrier)
+  int32_t* resident;  // set by the Reserve workgroup when it starts: the run's first eval waits for it (a select
+                      // workgroup waiting for a done flag must never be what keeps the Reserve workgroup off the CUs)
 };
 
 struct ResLdsCore {
@@ -5018,7 +5020,7 @@ __device__ __forceinline__ void resolve_batch(ResLds& L, const ChgSet& C, const 
                                               int32_t* __restrict__ touched_cnt = nullptr,
                                               bool has_t = false, bool keep = false, int LS = KMAX,
                                               bool sorted = false, int32_t* __restrict__ pub_done = nullptr,
-                                              const THelp th = THelp{nullptr, nullptr, nullptr, 0, 0}) {
+                                              const THelp th = THelp{nullptr, nullptr, nullptr, 0, 0, nullptr}) {
   const int tid = threadIdx.x;
   constexpr int RES_THREADS = res_threads<NUMA>();
   if (tid == 0) pstamps[PST * batch_index] = __builtin_amdgcn_s_memrealtime();
@@ -5485,6 +5487,7 @@ __global__ __launch_bounds__(res_threads<false>()) void k_resolve_run(SoA s, con
   __shared__ ResLds L;
   __shared__ int32_t s_ok;
   const bool nofix = !QUOTA && stale != nullptr;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && th.resident) st_sc1(th.resident, 1);
   if (blockIdx.x > 0) {  // a T-row helper
     if (nofix) t_helper<EXT>(L, s, pods, bases, b0, nb, k, done, err, th, (int)blockIdx.x - 1, &s_ok);
     return;
@@ -7067,9 +7070,9 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
     if (e - b >= 2) run_end[b] = e;
     b = e;
   }
-  // device: bases [n+1], ready [n], done [n], error word, T-helper counts [n], select-started flags [n]; fixup
-  // stamps [2n]; the T helpers' lists and maxima (THelp)
-  const int64_t sched_words = 5 * ((int64_t)n_batches + 1) + 1;
+  // device: bases [n+1], ready [n], done [n], error word, T-helper counts [n], select-started counts [n], the
+  // Reserve kernels' residency flags [n] (by run start); fixup stamps [2n]; the T helpers' lists and maxima (THelp)
+  const int64_t sched_words = 6 * ((int64_t)n_batches + 1) + 1;
   constexpr int64_t THELP_WORDS = 2 * (1 + MAX_BATCH) + 2 * MAX_BATCH;
   rc = ensure((void**)&d->d_sched, &d->sched_cap,
               sizeof(int32_t) * sched_words + sizeof(uint64_t) * 2 * n_batches + 8 + sizeof(int32_t) * THELP_WORDS);
@@ -7080,6 +7083,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   int32_t* d_err = d_done + n_batches + 1;
   int32_t* d_tready = d_err + 1;
   int32_t* d_sstart = d_tready + n_batches + 1;
+  int32_t* d_rres = d_sstart + n_batches + 1;
   uint64_t* d_fst = reinterpret_cast<uint64_t*>(d->d_sched + ((sched_words + 1) & ~1LL));
   int32_t* d_tlist = reinterpret_cast<int32_t*>(d_fst + 2 * n_batches);
   uint32_t* d_tmx = reinterpret_cast<uint32_t*>(d_tlist + 2 * (1 + MAX_BATCH));
@@ -7119,7 +7123,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   bool published = false;
   auto eval_select = [&](int b, bool pipe, hipStream_t es, const int32_t* dwait = nullptr,
                          int32_t* rpub = nullptr, bool alt = false, const int32_t* pwait = nullptr,
-                         const int32_t* ptl = nullptr, int32_t* sstart = nullptr) -> int {
+                         const int32_t* ptl = nullptr, int32_t* sstart = nullptr, int32_t dwant = 1) -> int {
     published = false;
     uint16_t* const scores = alt ? d->d_scores2 : d->d_scores;  // (the second eval stream's buffers)
     uint32_t* const split = alt ? d->d_split2 : d->d_split;
@@ -7144,7 +7148,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
     // spinning on the flag would hold the CUs the other stream's select needs)
     const bool plain_rec = !cpu && !ds && !numa && use_record_eval(bp);
     const bool wait_kernel = dwait && (!plain_rec || alt || (d->estream2 != nullptr && !sharded) || hi <= lo);
-    if (wait_kernel) hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), d->excl_lds, es, nullptr, 0, dwait, d_err, nullptr);
+    if (wait_kernel) hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), d->excl_lds, es, nullptr, 0, dwait, d_err, nullptr, dwant);
     if (prof) HIP_OK(hipEventRecord(pe[0], es));
     const int L = pipe ? KSTALE : KMAX, kext = pipe ? KMAX : 0;
     uint32_t* lists = pipe ? d->d_stale + (size_t)(b & 1) * MAX_BATCH * KSTALE : d->d_cand;
@@ -7188,7 +7192,12 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
         }
       }
       if (prof) HIP_OK(hipEventRecord(pe[1], es));
-      if (pwait)  // the nodes batch b-2 changed, once it is done (k_patch waits for the flag)
+      // a plain batch over many nodes: its pods' selections split over several workgroups each (>= 256
+      // workgroups in all, parts of >= 4096 nodes), merged by k_merge
+      const int parts = ds ? 1 : select_parts(N, bp);
+      // the nodes batch b-2 changed, once it is done (k_patch waits for the flag; folding it into the split select
+      // was measured slower: 256 select workgroups spinning on the flag)
+      if (pwait)
         hipLaunchKernelGGL(((k.flags & AF_EXT) ? k_patch<true> : k_patch<false>), dim3((unsigned)bp), dim3(64), d->excl_lds, es,
                            d->soa, d->d_pods, bbase, k, ptl, scores, d->capacity, pwait, d_err);
       if (ds && sharded && !d->loopback)  // DefaultNormalizeScore's max over the feasible nodes of all ranks
@@ -7201,9 +7210,6 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
         hipLaunchKernelGGL(sel, dim3((unsigned)bp), dim3(SELECT_BLOCK), 0, es, scores, d->capacity, slo, shi, cand,
                            cnt, d->d_dsraw, d->d_dsmax, k.wp_ds, kext, L, (int64_t)0, nullptr, nullptr, nullptr, pub, sstart);
       };
-      // a plain batch over many nodes: its pods' selections split over several workgroups each (>= 256
-      // workgroups in all, parts of >= 4096 nodes), merged by k_merge
-      const int parts = ds ? 1 : select_parts(N, bp);
       if (argmax1) {  // d_cand[0] zeroed by k_batch_begin
         hipLaunchKernelGGL((ds ? k_argmax1<true> : k_argmax1<false>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
                            es, scores, 0, N, d->d_dsraw, d->d_dsmax, k.wp_ds, d->d_cand, d->d_cand_cnt);
@@ -7270,7 +7276,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
       const int r0 = b, e = run_end[b];
       const bool ext = (k.flags & AF_EXT) != 0;
       const bool fixup = quota || d->pipe_fixup;  // the replay_batch path (quota) needs exact lists
-      const THelp th{d_tlist, d_tmx, d_tready, fixup ? 0 : d->t_helpers, d->t_help_ignore};
+      const THelp th{d_tlist, d_tmx, d_tready, fixup ? 0 : d->t_helpers, d->t_help_ignore, d_rres + r0};
       hipLaunchKernelGGL((quota ? (ext ? k_resolve_run<true, true> : k_resolve_run<true, false>)
                                 : (ext ? k_resolve_run<false, true> : k_resolve_run<false, false>)), dim3(1 + th.H), dim3(res_threads<false>()), 0,
                          d->stream, d->soa, d->d_pods, d_bases, r0, e - r0, k, d->d_cand, d->d_cand_cnt, d->d_chosen,
@@ -7292,14 +7298,16 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
           // with k_patch, batch q's eval waits for batch q-1's select to start (it followed k_patch(q-1), which
           // waited for done[q-3]): the select's workgroups are resident before this eval's grid takes the CUs
           const bool after_sel = two_es && d->eval_patch;
-          const int32_t* ew = after_sel ? (q - 1 >= r0 ? d_sstart + (q - 1) : nullptr)
+          const int32_t* ew = after_sel ? (q - 1 >= r0 ? d_sstart + (q - 1) : d_rres + r0)
                                         : (q - 2 >= r0 ? d_done + (q - 2) : nullptr);
+          // (every workgroup of batch q-1's select counts itself in sstart[q-1])
+          const int32_t want = after_sel && q - 1 >= r0 ? batches[q - 1].pods * std::max(1, select_parts(N, batches[q - 1].pods)) : 1;
           rc = eval_select(q, true, es, ew, d_ready + q, alt, patch ? d_done + (q - 2) : nullptr,
-                           d_tlist + ((q - 2) & 1) * (1 + MAX_BATCH), after_sel ? d_sstart + q : nullptr);
+                           d_tlist + ((q - 2) & 1) * (1 + MAX_BATCH), after_sel ? d_sstart + q : nullptr, want);
           if (rc) return rc;
           if (!published)
             hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), d->excl_lds, es, d_ready + q, (int32_t)batches[q].pods, nullptr,
-                               d_err, nullptr);
+                               d_err, nullptr, 1);
           continue;
         }
         rc = eval_select(q, true, d->estream);
