@@ -81,6 +81,7 @@ static void async_finish(ke_ctx* ctx, AsyncCall& a) {
 // Every call in flight completes (an entry point that reads or changes the state the submitted calls work on).
 static void async_drain(ke_ctx* ctx) {
   for (AsyncCall& a : ctx->async) async_finish(ctx, a);
+  mirror_join(ctx->c);
 }
 
 static int check_node(ke_ctx* ctx, int32_t node) {
@@ -843,6 +844,7 @@ static int schedule_sync(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_
     if (s1 < n_pods && (s1 == s0 || !matched(s1))) s1++;  // a barrier pod ends its segment; a matched one is alone
     const int32_t len = s1 - s0;
     const bool rsv = len == 1 && matched(s0);
+    mirror_join(c);  // (the previous segment's host mirror thread: this one reads the node state)
     if (rsv) {
       const int32_t* ids = mids.data() + moff[(size_t)s0];
       const int32_t n_ids = moff[(size_t)s0 + 1] - moff[(size_t)s0];
@@ -894,6 +896,7 @@ static int schedule_sync(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_
       const uint64_t* cs = (int64_t)c.last_cpusets.size() >= (int64_t)(i + 1) * 4 ? &c.last_cpusets[(size_t)i * 4] : nullptr;
       const bool cpus = cs && (cs[0] | cs[1] | cs[2] | cs[3]);
       if (!dev && !numa && !cpus) continue;
+      mirror_join(c);  // (the earlier calls' mirror may still be running on its thread)
       NodeState& ns = c.nodes[node];
       const bool was_dirty = ns.dirty;
       if (dev)

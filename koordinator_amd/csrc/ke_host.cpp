@@ -1831,32 +1831,57 @@ void host_release_node(const ke_config& cfg, bool ext, NodeState& ns, const ke_p
   ns.dirty = true;
 }
 
-void flush_mirror(Context& c) {
-  // the device rows already carry these Reserves: the nodes' dirty flags stay as they are
-  auto apply = [&c](const Context::PendingAssign& a) {
+// the mirror of placements (node, timestamp, pods[idx]) onto the host node state: LoadAware assign cache and
+// NodeInfo.Requested / pod count (+ FitPlus requests).  The device rows already carry these Reserves: the nodes'
+// dirty flags stay as they are.  Random nodes: cache-miss bound, so the node records (vector headers) are
+// prefetched 16 entries ahead and their arrays 8 ahead.
+static void apply_mirror(Context& c, const std::vector<Context::PendingAssign>& pending, const std::vector<ke_pod>& pods) {
+  const size_t n = pending.size();
+  for (size_t k = 0; k < n; k++) {
+    if (k + 16 < n) __builtin_prefetch(&c.nodes[pending[k + 16].node].asg, 1);
+    if (k + 8 < n) {
+      const NodeState& q = c.nodes[pending[k + 8].node];
+      __builtin_prefetch(q.asg_uid.data(), 0);
+      __builtin_prefetch(q.asg.data() + q.asg.size(), 1);
+      __builtin_prefetch(&q.node.requested[0], 1);
+    }
+    const Context::PendingAssign& a = pending[k];
     NodeState& ns = c.nodes[a.node];
-    const ke_pod& pod = c.pending_pods[(size_t)a.idx];
+    const ke_pod& pod = pods[(size_t)a.idx];
     host_assign(c.cfg, ns, pod, a.ts, false);
     ns.node.requested[KE_RES_CPU] += pod.requests[KE_RES_CPU];
     ns.node.requested[KE_RES_MEMORY] += pod.requests[KE_RES_MEMORY];
     ns.node.pod_count++;  // NodeInfo.AddPod
     if (c.ext_enabled) host_ext_reserve(ns, pod);
-  };
-  // random nodes: cache-miss bound, so the node records (vector headers) are prefetched 16 entries ahead and their
-  // assign-cache arrays 8 ahead (worker threads were measured slower: the allocator's locks)
-  const size_t n = c.pending.size();
-  for (size_t k = 0; k < n; k++) {
-    if (k + 16 < n) __builtin_prefetch(&c.nodes[c.pending[k + 16].node].asg, 1);
-    if (k + 8 < n) {
-      const NodeState& q = c.nodes[c.pending[k + 8].node];
-      __builtin_prefetch(q.asg_uid.data(), 0);
-      __builtin_prefetch(q.asg.data() + q.asg.size(), 1);
-      __builtin_prefetch(&q.node.requested[0], 1);
-    }
-    apply(c.pending[k]);
   }
+}
+
+void mirror_join(Context& c) {
+  if (c.mirror_thread.joinable()) c.mirror_thread.join();
+}
+
+void flush_mirror(Context& c) {
+  mirror_join(c);
+  apply_mirror(c, c.pending, c.pending_pods);
   c.pending.clear();
   c.pending_pods.clear();
+}
+
+// The queued mirror on a host thread (the lists move to it; later placements queue anew).  It writes only the
+// nodes' assign caches, requested amounts and pod counts -- never a dirty flag or list -- and every reader of those
+// joins it first.  A worker per node residue was measured slower than this one thread (the allocator's locks).
+void flush_mirror_async(Context& c) {
+  mirror_join(c);
+  if (c.pending.empty()) return;
+  auto* pend = new std::vector<Context::PendingAssign>(std::move(c.pending));
+  auto* pods = new std::vector<ke_pod>(std::move(c.pending_pods));
+  c.pending.clear();
+  c.pending_pods.clear();
+  c.mirror_thread = std::thread([&c, pend, pods]() {
+    apply_mirror(c, *pend, *pods);
+    delete pend;
+    delete pods;
+  });
 }
 
 void host_assign(const ke_config& cfg, NodeState& ns, const ke_pod& pod, int64_t timestamp_ns, bool mark_dirty) {

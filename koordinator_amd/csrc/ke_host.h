@@ -7,6 +7,7 @@
 #include <functional>
 #include <map>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -175,6 +176,13 @@ struct Context {
   std::vector<PendingAssign> pending;
   std::vector<ke_pod> pending_pods;  // copies of scheduled pods, taken while the device runs the call
   int64_t pending_base = 0;          // pending_pods index of the current device_schedule segment's first pod
+  // flush_mirror_async: the mirror of earlier placements applied on a host thread while this one enqueues and
+  // waits; every reader of the host node state joins it first (mirror_join; flush_mirror joins)
+  std::thread mirror_thread;
+  ~Context() { if (mirror_thread.joinable()) mirror_thread.join(); }
+  Context() = default;
+  Context(const Context&) = delete;
+  Context& operator=(const Context&) = delete;
   // The DevPod records of the current call's pods, built once by the argument checks (check_cpuset) and
   // reused by upload_pods
   std::vector<DevPod> staged;
@@ -276,6 +284,8 @@ int64_t usage_percent(int64_t used, int64_t total);
 void host_assign(const ke_config& cfg, NodeState& ns, const ke_pod& pod, int64_t timestamp_ns, bool mark_dirty = true);
 // apply Context::pending (placements whose device rows are already patched: dirty flags unchanged)
 void flush_mirror(Context& c);
+void flush_mirror_async(Context& c);
+void mirror_join(Context& c);
 // ke_schedule_submit / ke_schedule_wait (ke_kernels.hip): a call's enqueue part returns its completion, which waits
 // for the call's device work, writes the placements / scores and the call's statistics
 using DevFinish = std::function<int(int32_t* chosen, int32_t* score)>;

@@ -6590,6 +6590,7 @@ int device_refresh(Context* ctx, int64_t now) {
   const bool no_expiry = now < ctx->min_valid_until && ctx->n_nodes == ctx->clean_n_nodes;
   const bool all_clean = no_expiry && g_dirty_epoch.load(std::memory_order_relaxed) == ctx->clean_epoch;
   const bool incremental = !all_clean && no_expiry;
+  if (!all_clean) mirror_join(*ctx);  // a row may be derived: the host mirror on its thread first
   if (!all_clean && !ctx->pending.empty()) {  // a row to derive needs the deferred host mirror first
     bool any = false;
     if (incremental)
@@ -7380,7 +7381,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   ctx->last_enqueue_ms = ctx->host_ms[4] = ms_since(host_t0);
   tp = clk::now();
   const auto t_fl = clk::now();
-  flush_mirror(*ctx);  // the previous call's deferred host mirror, while the device works
+  flush_mirror_async(*ctx);  // the earlier calls' deferred host mirror, on a host thread while the device works
   const double flush_ms = ms_since(t_fl);
   HIP_OK(hipEventRecord(e1, d->stream));
   // The call's outputs go to one page-locked staging area (async copies, no host wait) and are copied out after
