@@ -3684,8 +3684,8 @@ constexpr int SEL_COPIES = 8;   // histogram copies per wave (pass 2)
 __host__ __device__ inline int select_seg(int lo, int hi) { return ((hi - lo + SELECT_WAVES - 1) / SELECT_WAVES + 511) & ~511; }
 // workgroups per pod of a plain batch's split k_select over n nodes: >= 256 workgroups in all, parts of
 // >= 4096 nodes, at most MAX_WORLD (k_merge's fan-in)
-inline int select_parts(int64_t n, int bp) {
-  return std::max(1, std::min({8, (255 + bp) / bp, (int)(n / 4096)}));
+inline int select_parts(int64_t n, int bp, int L = 2 * 64) {
+  return std::max(1, std::min({8, (255 + bp) / bp, (int)(n / 4096), 1024 / L}));  // (the merge: parts x L <= 1024)
 }
 // node part of one of `parts` workgroups of a split k_select (512-aligned, like the shard ranges)
 __host__ __device__ inline int select_part(int lo, int hi, int parts) { return ((hi - lo + parts - 1) / parts + 511) & ~511; }
@@ -3742,6 +3742,7 @@ __device__ __forceinline__ uint32_t max_halves(uint32_t w) { return max(w & 0xFF
 // the per-shard lists of the node-sharded path, on one GPU (a batch of 64 pods then fills every CU).
 // L = list length (KMAX, or KSTALE for the pipelined schedule's stale lists); outputs use stride L.
 constexpr int KSTALE = 2 * KMAX;  // stale-snapshot list length of the pipelined schedule
+constexpr int KSTALE2 = 3 * KMAX;  // select-ahead list length (k_fixlist: up to KMAX of them are batch b-2's nodes)
 constexpr int gath_words(int L) { return MAX_BATCH * L + MAX_BATCH; }
 constexpr int GATH_WORDS_MAX = MAX_BATCH * KSTALE + MAX_BATCH;
 constexpr int MAX_WORLD = 8;
@@ -4217,6 +4218,73 @@ __global__ __launch_bounds__(FIX_BLOCK) void k_fixup(SoA s, const DevPod* __rest
       if (j == 0 && fstamp) fstamp[1] = __builtin_amdgcn_s_memrealtime();
     }
   }
+}
+
+// Select-ahead (round 5): batch b's eval waited for batch b-3's Reserve, its select ran right after it into top-
+// (k_j + 2 KMAX) lists; once batch b-2 is done, workgroup j drops b-2's changed nodes (THelp::tlist, written with
+// their records before the flag) from pod j's list, inserts their current keys, and publishes the top-(k_j + KMAX)
+// in descending key order as the Reserve kernel's stale list -- exact but for batch b-1's nodes, which the replay
+// holds as T slots.  (At most KMAX entries drop, so k_j + KMAX exact keys remain.)  A key of a node that batch
+// b-1 changes too may be torn (its record is being rewritten): the replay drops every T node's key anyway.
+constexpr int FIXL_BLOCK = KSTALE2 + KMAX;
+template <bool EXT>
+__global__ __launch_bounds__(FIXL_BLOCK) void k_fixlist(SoA s, const DevPod* __restrict__ pods,
+                                                        const int32_t* __restrict__ batch_base, KArgs k,
+                                                        const uint32_t* __restrict__ pre, const int32_t* __restrict__ pre_cnt,
+                                                        const int32_t* __restrict__ tlist, const int32_t* __restrict__ done_wait,
+                                                        uint32_t* __restrict__ stale, int32_t* __restrict__ stale_cnt,
+                                                        int32_t* __restrict__ ready, int32_t* __restrict__ err) {
+  __shared__ int32_t s_tn[KMAX];
+  __shared__ uint4 s_k[FIXL_BLOCK / 4];
+  __shared__ int32_t s_ok, s_nt;
+  const int j = blockIdx.x, kj = min(j + 1, KMAX);
+  const int t = threadIdx.x;
+  uint32_t key = 0;  // (read before the wait: the select before this kernel on the same stream wrote them)
+  if (t < KSTALE2 && t < pre_cnt[j]) key = pre[j * KSTALE2 + t];
+  DevPod pod;
+  if (t >= KSTALE2) pod = pods[*batch_base + j];
+  if (t == 0) {
+    s_ok = done_wait ? wait_at_least(done_wait, 1, err) : 1;
+    s_nt = done_wait ? ld_sc1(tlist) : 0;
+  }
+  __syncthreads();
+  if (!s_ok) return;  // (a timed-out hand-off: the host discards the queue)
+  const int nt = s_nt;
+  NodeFast n;
+  int node = -1;
+  if (t >= KSTALE2 && t - KSTALE2 < nt) {
+    node = ld_sc1(tlist + 1 + (t - KSTALE2));
+    rec_load<__HIP_MEMORY_SCOPE_AGENT>(s.rec + (int64_t)node * NUM_RW, n);
+    if (EXT && (k.flags & AF_EXT)) ext_load(s, node, k, n);
+    s_tn[t - KSTALE2] = node;
+  }
+  __syncthreads();
+  if (t < KSTALE2) {
+    if (key) {
+      const int kn = key_node(key);
+      for (int u = 0; u < nt; u++) key = s_tn[u] == kn ? 0u : key;  // broadcast reads
+    }
+  } else if (node >= 0) {
+    fast_adopt(n, k);
+    const double estd[2] = {(double)pod.est[0], (double)pod.est[1]}, reqd[2] = {(double)pod.req[0], (double)pod.req[1]};
+    key = make_key(fast_total<EXT>(n, pod, estd, reqd, k), node);
+  }
+  reinterpret_cast<uint32_t*>(s_k)[t] = key;
+  const int nz = __syncthreads_count(key != 0u);
+  const int out = min(nz, kj + KMAX);
+  if (key) {
+    int rank = 0;
+#pragma unroll 4
+    for (int u = 0; u < FIXL_BLOCK / 4; u++) {
+      const uint4 q = s_k[u];
+      rank += (int)(q.x > key) + (int)(q.y > key) + (int)(q.z > key) + (int)(q.w > key);
+    }
+    if (rank < out) st_sc1(stale + j * KSTALE + rank, key);  // sc1: read by the running Reserve kernel
+  }
+  if (t == 0) st_sc1(stale_cnt + j, out);
+  drain_stores();  // publish: every wave drains its sc1 stores before the barrier, then one counter add
+  __syncthreads();
+  if (t == 0) __hip_atomic_fetch_add(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Pipelined schedule without k_fixup (k_resolve_run's stale-list mode), where the eval / select kernels do not
@@ -6192,6 +6260,7 @@ struct DeviceState {
   uint16_t* d_scores2 = nullptr;
   uint32_t* d_split2 = nullptr;
   uint32_t* d_stale = nullptr;      // [2][MAX_BATCH][KSTALE] stale-snapshot candidate lists
+  uint32_t* d_pre = nullptr;        // [2][MAX_BATCH][KSTALE2] select-ahead lists before k_fixlist (+ counts after)
   uint32_t* d_chg = nullptr;        // changed-node bitmap of the replay when node ids exceed its LDS copy
   int64_t* d_trows = nullptr;       // [MAX_BATCH][NUM_RW] records the last resolved batch changed (node in RW_PAD)
   int32_t* d_tcnt = nullptr;        // their count
@@ -6207,6 +6276,8 @@ struct DeviceState {
   // the CU's LDS, from the device's per-CU LDS at device_create (EXCL_LDS at the 160 KB of gfx950)
   unsigned excl_lds = EXCL_LDS;
   bool eval_patch = true;           // two eval streams: evals wait for batch b-3, k_patch adds b-2 (KOORDEVAL_EVAL_PATCH)
+  bool select_ahead = true;         // ... and the select follows the eval at once, k_fixlist adds b-2 to the lists
+                                    // (KOORDEVAL_SELECT_AHEAD; 0: k_patch before the select)
   int t_helpers = 4;                // T-row helper workgroups of a stale-list run (THelp; KOORDEVAL_T_HELPERS)
   int t_help_ignore = 0;            // test hook (KOORDEVAL_T_HELPERS_IGNORE): the replay's own T rows every batch
   // the Reservation plugin of a singleton batch (k_rsv_pick): its pairs and result words
@@ -6257,6 +6328,7 @@ int device_create(Context* ctx) {
   HIP_OK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
   if (const char* e = std::getenv("KOORDEVAL_T_HELPERS")) d->t_helpers = std::max(0, std::min(8, std::atoi(e)));
   if (const char* e = std::getenv("KOORDEVAL_EVAL_PATCH")) d->eval_patch = std::atoi(e) != 0;
+  if (const char* e = std::getenv("KOORDEVAL_SELECT_AHEAD")) d->select_ahead = std::atoi(e) != 0;
   if (const char* e = std::getenv("KOORDEVAL_T_HELPERS_IGNORE")) d->t_help_ignore = std::atoi(e) != 0;
   HIP_OK(hipStreamCreateWithPriority(&d->stream, hipStreamNonBlocking, prio_hi));
   HIP_OK(hipStreamCreateWithPriority(&d->estream, hipStreamNonBlocking, prio_lo));
@@ -6283,6 +6355,7 @@ int device_create(Context* ctx) {
   HIP_OK(hipMalloc(&d->d_batch_base, sizeof(int32_t)));
   HIP_OK(hipMemsetAsync(d->d_batch_base, 0, sizeof(int32_t), d->stream));
   HIP_OK(hipMalloc(&d->d_stale, sizeof(uint32_t) * 2 * MAX_BATCH * KSTALE));
+  HIP_OK(hipMalloc(&d->d_pre, sizeof(uint32_t) * 2 * MAX_BATCH * (KSTALE2 + 1)));
   HIP_OK(hipMalloc(&d->d_stale_cnt, sizeof(int32_t) * 2 * MAX_BATCH));
   HIP_OK(hipMalloc(&d->d_trows, sizeof(int64_t) * MAX_BATCH * NUM_RW));
   HIP_OK(hipMalloc(&d->soa.rec, sizeof(int64_t) * NUM_RW * d->capacity));
@@ -6355,7 +6428,7 @@ void device_destroy(Context* ctx) {
                   d->d_dsraw,   d->d_dsmax,  d->d_devalloc,   d->d_dsrows,       d->soa.nf,   d->soa.nm,
                   d->d_numaalloc, d->d_numarows, d->d_defer, d->d_defer_cnt, d->soa.cs, d->soa.cpu,
                   d->d_cpurows, d->d_cpusets, d->d_aff, d->soa.qt, d->soa.qm, d->d_sched, d->d_stale,
-                  d->d_stale_cnt, d->d_trows, d->d_tcnt, d->d_parts_done, d->d_scores2, d->d_split2, d->d_chg, d->soa.rec, d->soa.pt, d->soa.kerr,
+                  d->d_stale_cnt, d->d_pre, d->d_trows, d->d_tcnt, d->d_parts_done, d->d_scores2, d->d_split2, d->d_chg, d->soa.rec, d->soa.pt, d->soa.kerr,
                   d->soa.xf, d->soa.xm, d->d_xrows, d->soa.dsx, d->d_ph, d->d_vfo, d->d_rsv, d->d_rsv_out};
   if (d->estream) (void)hipStreamSynchronize(d->estream);
   if (d->estream2) (void)hipStreamSynchronize(d->estream2);
@@ -7124,7 +7197,8 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   bool published = false;
   auto eval_select = [&](int b, bool pipe, hipStream_t es, const int32_t* dwait = nullptr,
                          int32_t* rpub = nullptr, bool alt = false, const int32_t* pwait = nullptr,
-                         const int32_t* ptl = nullptr, int32_t* sstart = nullptr, int32_t dwant = 1) -> int {
+                         const int32_t* ptl = nullptr, int32_t* sstart = nullptr, int32_t dwant = 1,
+                         bool pre = false) -> int {
     published = false;
     uint16_t* const scores = alt ? d->d_scores2 : d->d_scores;  // (the second eval stream's buffers)
     uint32_t* const split = alt ? d->d_split2 : d->d_split;
@@ -7151,9 +7225,12 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
     const bool wait_kernel = dwait && (!plain_rec || alt || (d->estream2 != nullptr && !sharded) || hi <= lo);
     if (wait_kernel) hipLaunchKernelGGL(k_handoff, dim3(1), dim3(64), d->excl_lds, es, nullptr, 0, dwait, d_err, nullptr, dwant);
     if (prof) HIP_OK(hipEventRecord(pe[0], es));
-    const int L = pipe ? KSTALE : KMAX, kext = pipe ? KMAX : 0;
-    uint32_t* lists = pipe ? d->d_stale + (size_t)(b & 1) * MAX_BATCH * KSTALE : d->d_cand;
-    int32_t* lists_cnt = pipe ? d->d_stale_cnt + (b & 1) * MAX_BATCH : d->d_cand_cnt;
+    // (select-ahead: top-(k_j + 2 KMAX) into the pre-fix buffer, k_fixlist makes the Reserve kernel's lists)
+    const int L = pre ? KSTALE2 : pipe ? KSTALE : KMAX, kext = pre ? 2 * KMAX : pipe ? KMAX : 0;
+    uint32_t* lists = pre ? d->d_pre + (size_t)(b & 1) * MAX_BATCH * KSTALE2
+                          : pipe ? d->d_stale + (size_t)(b & 1) * MAX_BATCH * KSTALE : d->d_cand;
+    int32_t* lists_cnt = pre ? reinterpret_cast<int32_t*>(d->d_pre + (size_t)2 * MAX_BATCH * KSTALE2) + (b & 1) * MAX_BATCH
+                             : pipe ? d->d_stale_cnt + (b & 1) * MAX_BATCH : d->d_cand_cnt;
     if (N > 0) {
       const bool single = bp == 1;
       if (hi > lo) {
@@ -7195,7 +7272,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
       if (prof) HIP_OK(hipEventRecord(pe[1], es));
       // a plain batch over many nodes: its pods' selections split over several workgroups each (>= 256
       // workgroups in all, parts of >= 4096 nodes), merged by k_merge
-      const int parts = ds ? 1 : select_parts(N, bp);
+      const int parts = ds ? 1 : select_parts(N, bp, L);
       // the nodes batch b-2 changed, once it is done (k_patch waits for the flag; folding it into the split select
       // was measured slower: 256 select workgroups spinning on the flag)
       if (pwait)
@@ -7278,15 +7355,16 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
       const bool ext = (k.flags & AF_EXT) != 0;
       const bool fixup = quota || d->pipe_fixup;  // the replay_batch path (quota) needs exact lists
       const THelp th{d_tlist, d_tmx, d_tready, fixup ? 0 : d->t_helpers, d->t_help_ignore, d_rres + r0};
+      // batches alternate between the eval streams -- unsharded only: a node-sharded batch's all-gather must run
+      // in the same order on every rank's communicator, which two streams of one rank would not guarantee
+      const bool two_es = !fixup && d->estream2 != nullptr && !sharded;
+      const bool ahead = two_es && d->eval_patch && d->select_ahead;  // (k_fixlist's lists: descending)
       hipLaunchKernelGGL((quota ? (ext ? k_resolve_run<true, true> : k_resolve_run<true, false>)
                                 : (ext ? k_resolve_run<false, true> : k_resolve_run<false, false>)), dim3(1 + th.H), dim3(res_threads<false>()), 0,
                          d->stream, d->soa, d->d_pods, d_bases, r0, e - r0, k, d->d_cand, d->d_cand_cnt, d->d_chosen,
                          d->d_chosen_score, ctx->cfg.global_node_offset, d->d_stamps, d->d_stamps + (n_pods + 2),
                          d->d_devalloc, d_ready, d_done, d_err, d->d_trows, d->d_tcnt, d->d_chg, N,
-                         fixup ? nullptr : d->d_stale, fixup ? nullptr : d->d_stale_cnt, (int)run_sorted(r0, e), th);
-      // batches alternate between the eval streams -- unsharded only: a node-sharded batch's all-gather must run
-      // in the same order on every rank's communicator, which two streams of one rank would not guarantee
-      const bool two_es = !fixup && d->estream2 != nullptr && !sharded;
+                         fixup ? nullptr : d->d_stale, fixup ? nullptr : d->d_stale_cnt, (int)(ahead || run_sorted(r0, e)), th);
       if (r0 > 0) HIP_OK(hipStreamWaitEvent(d->estream, d->ev_res[(r0 - 1) % R], 0));
       if (two_es) HIP_OK(hipStreamWaitEvent(d->estream2, r0 > 0 ? d->ev_res[(r0 - 1) % R] : d->ev_start, 0));
       for (int q = r0; q < e; q++) {
@@ -7294,6 +7372,22 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
         if (!fixup) {  // the stale lists go to the replay as they are; batch q's eval waits for batch q-2's done
           const bool alt = two_es && ((q - r0) & 1);
           hipStream_t es = alt ? d->estream2 : d->estream;
+          if (ahead) {
+            // select-ahead: batch q's eval waits for batch q-3 (the first two of the run for the Reserve kernel's
+            // residency: k_fixlist workgroups spinning on a done flag must never keep it off the CUs), its select
+            // follows at once, and k_fixlist brings in batch q-2's changed nodes and publishes the lists
+            const int32_t* ew = q - 3 >= r0 ? d_done + (q - 3) : q - 2 < r0 ? d_rres + r0 : nullptr;
+            rc = eval_select(q, true, es, ew, nullptr, alt, nullptr, nullptr, nullptr, 1, true);
+            if (rc) return rc;
+            const uint32_t* pre = d->d_pre + (size_t)(q & 1) * MAX_BATCH * KSTALE2;
+            const int32_t* pre_cnt = reinterpret_cast<const int32_t*>(d->d_pre + (size_t)2 * MAX_BATCH * KSTALE2) + (q & 1) * MAX_BATCH;
+            hipLaunchKernelGGL((ext ? k_fixlist<true> : k_fixlist<false>), dim3((unsigned)batches[q].pods), dim3(FIXL_BLOCK),
+                               0, es, d->soa, d->d_pods, d_bases + q, k, pre, pre_cnt,
+                               d_tlist + ((q - 2) & 1) * (1 + MAX_BATCH), q - 2 >= r0 ? d_done + (q - 2) : nullptr,
+                               d->d_stale + (size_t)(q & 1) * MAX_BATCH * KSTALE, d->d_stale_cnt + (q & 1) * MAX_BATCH,
+                               d_ready + q, d_err);
+            continue;
+          }
           // two eval streams: batch q's eval waits only for batch q-3, k_patch brings in batch q-2's changed nodes
           const bool patch = two_es && d->eval_patch && q - 2 >= r0;
           // with k_patch, batch q's eval waits for batch q-1's select to start (it followed k_patch(q-1), which
