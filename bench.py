@@ -11,7 +11,7 @@ one workgroup, per-batch time from in-kernel s_memrealtime stamps); eval and sel
 alternating eval streams (k_fixup too with --pipeline-fixup).  `roofline.achieved` = SURVEY.md §8(d)'s algorithmic bytes of a batch (N*S_row +
 B*S_pod + B*k*12) over that critical path; `roofline.replay` the replay's own bytes, `roofline.kernels`
 every kernel of a batch and `roofline.end_to_end` the whole step, each against 8 TB/s.
-`traffic` = HBM bytes from a prior rocprofv3 PMC pass of this workload (profiles/r04/pmc_bench.json).
+`traffic` = HBM bytes from a prior rocprofv3 PMC pass of this workload (profiles/r05/pmc_bench.json).
 
 cpu_baseline: the oracle (C restatement of the Go plugins, oracle/) scheduling a prefix of the same
 queue on the host's cores at 1 thread, 16 threads (upstream Parallelism) and every usable core.
@@ -98,10 +98,12 @@ def batch_bytes(n_nodes, b, fetched, changed, pipelined, fixup=False):
 
 def pmc_traffic(tag):
     """HBM bytes per launch by kernel from the committed PMC passes (tools/pmc_bench.sh, summarised by
-    tools/pmc_summary.py into profiles/r04/pmc_bench.json) of this workload.  Counter collection serialises
-    dispatches, which the persistent Reserve chain cannot run under, so the passes run the one-stream
-    schedule (tag suffix _serial): its k_eval_batch / k_select / k_resolve launches do the same work per batch."""
-    f = os.path.join(ROOT, "profiles", "r04", "pmc_bench.json")
+    tools/pmc_summary.py into profiles/r05/pmc_bench.json) of this workload.  Counter collection serialises
+    dispatches, which the persistent Reserve chain (and the eval streams' kernels that wait on its flags: k_handoff,
+    k_fixlist) cannot run under, so the passes run the one-stream schedule (tag suffix _serial): its k_eval_plain /
+    k_select / k_resolve launches do the same work per batch; k_fixlist moves <= 64 records + 64 x 256 keys per
+    batch (about 64 KB)."""
+    f = os.path.join(ROOT, "profiles", "r05", "pmc_bench.json")
     if not os.path.exists(f):
         return {}, None
     d = json.load(open(f))
