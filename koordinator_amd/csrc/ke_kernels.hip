@@ -4908,10 +4908,17 @@ __device__ __forceinline__ void replay_spec(ResLds& L, const ChgSet& C, const So
     __syncthreads();
     if (stamp && first) pst[1] = __builtin_amdgcn_s_memrealtime();
     if (prog) {
-      // the T maxima into the rows: the helpers' (wave 0 polled them), else evaluated here
-      for (int j = start + wave; j < end; j += NW) {
-        t_row(j);
-        if (lane == 0) L.sp.mrow[j] = max(L.sp.mrow[j], L.sp.tmx[j]);
+      // the T maxima into the rows: the helpers' (wave 0 polled them), else evaluated here.  With every row's
+      // maximum in (the usual case: the same LDS words on every wave, so the test is uniform) wave 0 merges
+      // them one lane a row
+      const bool in = lane >= start && lane < end;
+      if (!__ballot(in && L.sp.tver[lane] != tres)) {
+        if (wave == 0 && in) L.sp.mrow[lane] = max(L.sp.mrow[lane], L.sp.tmx[lane]);
+      } else {
+        for (int j = start + wave; j < end; j += NW) {
+          t_row(j);
+          if (lane == 0) L.sp.mrow[j] = max(L.sp.mrow[j], L.sp.tmx[j]);
+        }
       }
     } else {
       // ---- R (every wave): lane c in [start, end) adopts pod c's predicted node and reserves pod c on it
@@ -6234,6 +6241,12 @@ struct DeviceState {
   uint8_t* d_aff = nullptr;        // [capacity] NUMA affinity per node of a singleton batch's eval
   // pipelined schedule: eval + select run on `estream` one batch ahead of the Reserve chain on `stream`
   hipStream_t estream = nullptr;
+  // a call's staging copies (pod upload, bookkeeping words) and read-back run on `cstream`: the next call's uploads
+  // proceed while this one still runs, and the Reserve stream goes from one call's Reserve kernel to the next.
+  // Opt-in (KOORDEVAL_STAGING_STREAM=1): on the C3 bench it measured 78-85 G against 92 G with everything on `stream`
+  // (tools/_ab.sh, one box, alternated), so by default the staging work stays on `stream` (nullptr here)
+  hipStream_t cstream = nullptr;
+  hipEvent_t ev_setup = nullptr, ev_rend = nullptr;
   // a second eval stream with its own score matrix / part lists: consecutive batches of a stale-list run
   // alternate between the two, so batch b+1's eval overlaps batch b's select (nullptr: clusters too large to
   // double the score matrix)
@@ -6332,6 +6345,10 @@ int device_create(Context* ctx) {
   if (const char* e = std::getenv("KOORDEVAL_T_HELPERS_IGNORE")) d->t_help_ignore = std::atoi(e) != 0;
   HIP_OK(hipStreamCreateWithPriority(&d->stream, hipStreamNonBlocking, prio_hi));
   HIP_OK(hipStreamCreateWithPriority(&d->estream, hipStreamNonBlocking, prio_lo));
+  if (const char* e = std::getenv("KOORDEVAL_STAGING_STREAM"); e && std::atoi(e) != 0)
+    HIP_OK(hipStreamCreateWithPriority(&d->cstream, hipStreamNonBlocking, prio_lo));
+  HIP_OK(hipEventCreateWithFlags(&d->ev_setup, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&d->ev_rend, hipEventDisableTiming));
   for (int e = 0; e < DeviceState::EV_RING; e++) {
     HIP_OK(hipEventCreateWithFlags(&d->ev_res[e], hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&d->ev_sel[e], hipEventDisableTiming));
@@ -6440,6 +6457,9 @@ void device_destroy(Context* ctx) {
   }
   if (d->ev_start) (void)hipEventDestroy(d->ev_start);
   if (d->estream) (void)hipStreamDestroy(d->estream);
+  if (d->cstream) (void)hipStreamDestroy(d->cstream);
+  if (d->ev_setup) (void)hipEventDestroy(d->ev_setup);
+  if (d->ev_rend) (void)hipEventDestroy(d->ev_rend);
   if (d->estream2) (void)hipStreamDestroy(d->estream2);
   if (d->ev_sel2) (void)hipEventDestroy(d->ev_sel2);
   for (auto& e : d->tev) (void)hipEventDestroy(e);
@@ -6830,8 +6850,9 @@ int device_refresh(Context* ctx, int64_t now) {
   return KE_OK;
 }
 
-static int upload_pods(Context* ctx, int32_t n_pods, const ke_pod* pods) {
+static int upload_pods(Context* ctx, int32_t n_pods, const ke_pod* pods, hipStream_t ustream = nullptr) {
   DeviceState* d = ctx->dev;
+  if (!ustream) ustream = d->stream;
   PinnedVec<DevPod>& dp = d->host_pods;
   if (!dp.resize((size_t)n_pods)) return fail(KE_ERR_DEVICE, "hipHostMalloc of the pod staging buffer");
   std::vector<DevPodHint>& ph = d->host_ph;  // the hinted pods' records; DevPod::ring_bw = slot
@@ -6852,11 +6873,11 @@ static int upload_pods(Context* ctx, int32_t n_pods, const ke_pod* pods) {
   }
   int rc = ensure((void**)&d->d_pods, &d->pods_cap, sizeof(DevPod) * (int64_t)std::max(n_pods, 1));
   if (rc) return rc;
-  HIP_OK(hipMemcpyAsync(d->d_pods, dp.data(), sizeof(DevPod) * n_pods, hipMemcpyHostToDevice, d->stream));
+  HIP_OK(hipMemcpyAsync(d->d_pods, dp.data(), sizeof(DevPod) * n_pods, hipMemcpyHostToDevice, ustream));
   if (!ph.empty()) {
     rc = ensure((void**)&d->d_ph, &d->ph_cap, sizeof(DevPodHint) * (int64_t)ph.size());
     if (rc) return rc;
-    HIP_OK(hipMemcpyAsync(d->d_ph, ph.data(), sizeof(DevPodHint) * ph.size(), hipMemcpyHostToDevice, d->stream));
+    HIP_OK(hipMemcpyAsync(d->d_ph, ph.data(), sizeof(DevPodHint) * ph.size(), hipMemcpyHostToDevice, ustream));
   }
   d->soa.ph = d->d_ph;
   // no host wait: the kernels run on d->stream after the copies, and the eval stream waits for ev_start,
@@ -7012,7 +7033,8 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   ctx->last_pod_lat.clear();
   if (n_pods == 0) return KE_OK;
   tp = clk::now();
-  rc = upload_pods(ctx, n_pods, pods);
+  hipStream_t const cs = d->cstream ? d->cstream : d->stream;  // the call's staging stream
+  rc = upload_pods(ctx, n_pods, pods, cs);
   if (rc) return rc;
   ctx->host_ms[2] = ms_since(tp);
   tp = clk::now();
@@ -7073,7 +7095,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   }
   rc = ensure((void**)&d->d_cpusets, &d->cpusets_cap, sizeof(uint64_t) * 4 * (int64_t)n_pods);
   if (rc) return rc;
-  HIP_OK(hipMemsetAsync(d->d_cpusets, 0, sizeof(uint64_t) * 4 * n_pods, d->stream));
+  HIP_OK(hipMemsetAsync(d->d_cpusets, 0, sizeof(uint64_t) * 4 * n_pods, cs));
   bool any_hint = false;
   for (const DevPod& q : d->host_pods) any_hint = any_hint || (q.flags & PF_DS_HINT);
   d->soa.vfo = nullptr;
@@ -7161,11 +7183,12 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   uint64_t* d_fst = reinterpret_cast<uint64_t*>(d->d_sched + ((sched_words + 1) & ~1LL));
   int32_t* d_tlist = reinterpret_cast<int32_t*>(d_fst + 2 * n_batches);
   uint32_t* d_tmx = reinterpret_cast<uint32_t*>(d_tlist + 2 * (1 + MAX_BATCH));
-  HIP_OK(hipMemcpyAsync(d_bases, bases.data(), sizeof(int32_t) * (n_batches + 1), hipMemcpyHostToDevice, d->stream));
-  HIP_OK(hipMemsetAsync(d_ready, 0, sizeof(int32_t) * (sched_words - n_batches - 1), d->stream));
-  HIP_OK(hipMemsetAsync(d_fst, 0, sizeof(uint64_t) * 2 * n_batches, d->stream));
-  HIP_OK(hipMemsetAsync(d->soa.kerr, 0, sizeof(int32_t), d->stream));
-  HIP_OK(hipMemsetAsync(d->d_parts_done, 0, sizeof(int32_t) * 2 * MAX_BATCH, d->stream));  // (an aborted launch's counts)
+  // (the call's own words, on its staging stream; the error word and the split selects' counters stay zero
+  // between calls -- an aborted call resets them)
+  HIP_OK(hipMemcpyAsync(d_bases, bases.data(), sizeof(int32_t) * (n_batches + 1), hipMemcpyHostToDevice, cs));
+  HIP_OK(hipMemsetAsync(d_ready, 0, sizeof(int32_t) * (sched_words - n_batches - 1), cs));
+  HIP_OK(hipMemsetAsync(d_fst, 0, sizeof(uint64_t) * 2 * n_batches, cs));
+  HIP_OK(hipEventRecord(d->ev_setup, cs));
   // sampled per-kernel HIP event pairs (ke_set_profiling) on the eval stream: eval, select
   constexpr int PE = 4;  // eval start, eval end, select end, select start (after k_patch and its wait)
   const int every = d->profile_every;
@@ -7180,6 +7203,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   hipEvent_t e0 = d->tev[0], e1 = d->tev[1];
   const hipEvent_t done_ev[3] = {d->tev[2], d->tev[3], d->tev[4]};  // the call's end on each stream
   std::vector<hipEvent_t> ev(d->tev.begin() + 5, d->tev.begin() + (long)n_tev);
+  HIP_OK(hipStreamWaitEvent(d->stream, d->ev_setup, 0));
   HIP_OK(hipEventRecord(e0, d->stream));
   hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, d->stream, d->d_stamps);
   HIP_OK(hipEventRecord(d->ev_start, d->stream));
@@ -7478,6 +7502,8 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   flush_mirror_async(*ctx);  // the earlier calls' deferred host mirror, on a host thread while the device works
   const double flush_ms = ms_since(t_fl);
   HIP_OK(hipEventRecord(e1, d->stream));
+  HIP_OK(hipEventRecord(d->ev_rend, d->stream));  // the read-back on the staging stream after the Reserve chain
+  HIP_OK(hipStreamWaitEvent(cs, d->ev_rend, 0));
   // The call's outputs go to one page-locked staging area (async copies, no host wait) and are copied out after
   // the synchronisation; allocations none of the call's batches can make are not read back (zero).
   bool any_ds = false;
@@ -7498,7 +7524,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   if (!d->h_out.resize(off)) return fail(KE_ERR_DEVICE, "hipHostMalloc of the readback staging buffer");
   uint8_t* const h = d->h_out.data();
   auto d2h = [&](size_t o, const void* src, size_t bytes) -> int {
-    if (bytes) HIP_OK(hipMemcpyAsync(h + o, src, bytes, hipMemcpyDeviceToHost, d->stream));
+    if (bytes) HIP_OK(hipMemcpyAsync(h + o, src, bytes, hipMemcpyDeviceToHost, cs));
     return KE_OK;
   };
   if ((rc = d2h(o_chosen, d->d_chosen, (size_t)out_bytes))) return rc;
@@ -7515,7 +7541,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
     return rc;
   // the call's end on every stream: its completion waits for these events, not for the streams (a submission
   // behind it may already be queued on them)
-  HIP_OK(hipEventRecord(done_ev[0], d->stream));
+  HIP_OK(hipEventRecord(done_ev[0], cs));
   HIP_OK(hipEventRecord(done_ev[1], d->estream));
   if (d->estream2) HIP_OK(hipEventRecord(done_ev[2], d->estream2));
   double enq_ms[5];
@@ -7574,6 +7600,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   if (herr) {
     if (d->d_chg)  // an abandoned replay may have left bits set
       (void)hipMemset(d->d_chg, 0, sizeof(uint32_t) * (d->capacity + 31) / 32);
+    (void)hipMemset(d->d_parts_done, 0, sizeof(int32_t) * 2 * MAX_BATCH);  // (an aborted launch's counts)
     return fail(KE_ERR_DEVICE, "pipelined schedule: a device-side hand-off timed out (placements invalid)");
   }
   if (kerr & (KERR_HINT_ROUTE | KERR_LDS_WAIT)) {  // internal errors: the placements are not the reference's
