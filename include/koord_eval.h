@@ -805,7 +805,11 @@ int ke_reservations_get(ke_ctx* ctx, int32_t n, ke_reservation* out);
                              transformer.go:97-146) listed with ke_pod_reservations                          */
 #define KE_RSV_AFFINITY 2 /* a required reservation affinity: as KE_RSV_MATCHED, and the Reservation Filter
                              passes only nodes where a listed reservation fits (an empty list: unschedulable) */
-#define KE_RSV_IGNORED 3  /* reservation-ignored pod: refused                                               */
+#define KE_RSV_IGNORED 3  /* reservation-ignored pod (apis/extension/reservation.go:97-99): every available
+                             reservation of every node is matchedOrIgnored (its reserve pod leaves NodeInfo, no
+                             unmatched restore), no Reservation Filter / Score / Reserve; lists none.
+                             KE_ERR_UNSUPPORTED while a reservation holds NUMA resources, CPUs or devices
+                             (ke_reservation_alloc), and outside ke_schedule                                    */
 /* For each pod of the next ke_schedule call, the reservations (indices into the loaded set) it matches,
  * ids[offsets[p] .. offsets[p+1]) (with a reservation name in the affinity: only that one).  Only KE_RSV_MATCHED /
  * KE_RSV_AFFINITY pods may list any; the call consumes the lists.

@@ -97,9 +97,8 @@ static int check_pods(const ke_pod* pods, int32_t n, const Context* c = nullptr,
     if (rc) return rc;
     const uint8_t rm = pods[p].reservation_matched;
     if (rm > KE_RSV_IGNORED) return fail(KE_ERR_INVALID, "ke_pod.reservation_matched");
-    if (rm == KE_RSV_IGNORED) return fail(KE_ERR_UNSUPPORTED, "a reservation-ignored pod");
-    if ((rm == KE_RSV_MATCHED || rm == KE_RSV_AFFINITY) && !matched_ok)
-      return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations outside ke_schedule");
+    if (rm != KE_RSV_NONE && !matched_ok)
+      return fail(KE_ERR_UNSUPPORTED, "a pod matching / ignoring reservations outside ke_schedule");
     if (c) rc = validate_pod_hints(*c, pods[p]);
     else if (pods[p].device_hint) rc = fail(KE_ERR_INVALID, "ke_pod.device_hint without a context");
     if (rc) return rc;
@@ -157,6 +156,10 @@ static int check_matches(Context& c, const ke_pod* pods, int32_t n) {
     const uint8_t rm = pods[p].reservation_matched;
     if (rm != KE_RSV_MATCHED && rm != KE_RSV_AFFINITY) {
       if (cnt) return fail(KE_ERR_INVALID, "reservations listed for a pod that is not KE_RSV_MATCHED / AFFINITY");
+      if (rm == KE_RSV_IGNORED) {
+        const int rc = resv_ignore_check(c);
+        if (rc) return rc;
+      }
       continue;
     }
     if (!staged) return fail(KE_ERR_INVALID, "a KE_RSV_MATCHED / AFFINITY pod without ke_pod_reservations");
@@ -837,14 +840,19 @@ static int schedule_sync(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_
     return pods[p].reservation_matched == KE_RSV_AFFINITY ||
            (!moff.empty() && moff[(size_t)p + 1] > moff[(size_t)p]);
   };
+  // A run of KE_RSV_IGNORED pods is a segment of its own: its rows carry every reservation's matched restore.
+  auto ignored = [&](int32_t p) { return pods[p].reservation_matched == KE_RSV_IGNORED; };
   std::vector<int32_t> assumed((size_t)n_pods, 0);
   for (int32_t s0 = 0; s0 < n_pods || (n_pods == 0 && s0 == 0);) {
     int32_t s1 = s0;
-    while (s1 < n_pods && !barrier(s1) && !matched(s1)) s1++;
-    if (s1 < n_pods && (s1 == s0 || !matched(s1))) s1++;  // a barrier pod ends its segment; a matched one is alone
+    const bool ign = s0 < n_pods && ignored(s0);
+    while (s1 < n_pods && !barrier(s1) && !matched(s1) && ignored(s1) == ign) s1++;
+    // a barrier pod ends its segment; a matched one is alone
+    if (s1 < n_pods && (s1 == s0 || (!matched(s1) && barrier(s1) && ignored(s1) == ign))) s1++;
     const int32_t len = s1 - s0;
     const bool rsv = len == 1 && matched(s0);
     mirror_join(c);  // (the previous segment's host mirror thread: this one reads the node state)
+    if (ign) resv_ignore_begin(c);
     if (rsv) {
       const int32_t* ids = mids.data() + moff[(size_t)s0];
       const int32_t n_ids = moff[(size_t)s0 + 1] - moff[(size_t)s0];
@@ -862,9 +870,11 @@ static int schedule_sync(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_
     auto undo_rsv = [&]() {
       int32_t dummy = 0;
       if (rsv) resv_finish(c, -1, pods[s0], &dummy);
+      if (ign) resv_ignore_end(c);
     };
     rc = device_schedule(&c, len, pods + s0, now_ns, chosen + (n_pods ? s0 : 0), score ? score + s0 : nullptr);
     if (rc) return undo_rsv(), rc;
+    if (ign) resv_ignore_end(c);
     if (rsv) {
       const int32_t local = chosen[s0] < 0 ? -1 : chosen[s0] - off;
       int32_t pick[4] = {local, 0, 0, -1};  // no usable matched reservation: no Reservation score

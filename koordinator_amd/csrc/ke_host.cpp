@@ -778,6 +778,38 @@ int resv_check(const Context& c, const int32_t* ids, int32_t n_ids) {
   return KE_OK;
 }
 
+// A reservation-ignored pod (apis/extension/reservation.go:97-99) takes every available reservation of every node
+// as matchedOrIgnored (transformer.go:101-106, 181-199): restoreMatchedReservation removes each reserve pod from
+// NodeInfo and no unmatched restore is left; the Reservation plugin's Filter passes (filterWithReservations without
+// an affinity, plugin.go:350-353), PreScore / Score skip it (scoring.go:48-50) and Reserve assumes it into no
+// reservation (plugin.go:755-761).  NodeNUMAResource / DeviceShare allocate it from the node and the ignored
+// reservations' unallocated remainder (tryAllocateIgnoreReservation, nodenumaresource/reservation.go:437-490,
+// deviceshare/reservation.go:290-310): that remainder is restated only when no reservation holds NUMA resources,
+// CPUs or devices, where it is empty and the pod's rows are the matched restore alone.
+int resv_ignore_check(const Context& c) {
+  for (size_t i = 0; i < c.resv_holds.size(); i++)
+    if (c.resv_holds[i])
+      return fail(KE_ERR_UNSUPPORTED, "a reservation-ignored pod while a reservation holds NUMA resources, CPUs or "
+                                      "devices (tryAllocateIgnoreReservation over held resources)");
+  return KE_OK;
+}
+
+void resv_ignore_begin(Context& c) {
+  const std::vector<char> all(c.resv.size(), 1);
+  for (size_t node = 0; node < c.resv_by_node.size(); node++) {
+    if (c.resv_by_node[node].empty()) continue;
+    NodeState& ns = c.nodes[node];
+    resv_delta(c, (int32_t)node, &all, true, ns.rv_req, ns.rv_nz, &ns.rv_pods);
+    resv_plugin_restore(c, (int32_t)node, &all, ns);
+    ns.dirty = true;
+  }
+}
+
+void resv_ignore_end(Context& c) {
+  for (size_t node = 0; node < c.resv_by_node.size(); node++)
+    if (!c.resv_by_node[node].empty()) resv_node_restore(c, (int32_t)node);
+}
+
 // requestCPUBind of the pod on the node (util.go:121-138): its own cpuset state, else a node CPU bind policy
 // binding a whole-CPU request
 static bool pod_binds_on(const DevPod& dp, const NodeState& ns) {

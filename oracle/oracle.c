@@ -421,8 +421,8 @@ static int pod_is_cpuset(const ke_pod* pod) {
          pod->requests[KE_RES_CPU] > 0;
 }
 static int pod_unsupported(const ke_pod* pod) {
-  /* KE_RSV_MATCHED pods are checked by or_schedule (or_resv_supported); affinity / ignored are refused */
-  return pod->has_resource_spec || pod->has_unsupported_device_requests || pod->reservation_matched > KE_RSV_AFFINITY;
+  /* KE_RSV_MATCHED / AFFINITY / IGNORED pods are checked by or_schedule (or_resv_supported) */
+  return pod->has_resource_spec || pod->has_unsupported_device_requests || pod->reservation_matched > KE_RSV_IGNORED;
 }
 static int node_unsupported(const ke_node* n) {
   return n->numa_topology_policy < 0 || n->numa_topology_policy > KE_NUMA_POLICY_SINGLE_NUMA_NODE ||
@@ -4275,6 +4275,9 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
     const int32_t n_ids = c->moff && c->m_pods == n_pods ? c->moff[p + 1] - c->moff[p] : 0;
     if (pods[p].reservation_matched != KE_RSV_MATCHED && pods[p].reservation_matched != KE_RSV_AFFINITY) {
       if (n_ids) return KE_ERR_INVALID;
+      /* a reservation-ignored pod: tryAllocateIgnoreReservation's remainder of held resources is not restated */
+      for (int32_t r = 0; pods[p].reservation_matched == KE_RSV_IGNORED && c->ralloc && r < c->n_resv; r++)
+        if (or_holds_of(&c->ralloc[r])) return KE_ERR_UNSUPPORTED;
       continue;
     }
     if (!(c->moff && c->m_pods == n_pods)) return KE_ERR_INVALID;
@@ -4336,6 +4339,17 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
     const int32_t n_ids = c->moff && pods[p].reservation_matched ? c->moff[p + 1] - c->moff[p] : 0;
     if (n_ids > 0 || affinity) {
       b = or_resv_eval(c, &pods[p], now, o, c->moff ? c->mids + c->moff[p] : NULL, n_ids, affinity, &bs, nom);
+    } else if (pods[p].reservation_matched == KE_RSV_IGNORED) {
+      /* a reservation-ignored pod (transformer.go:101-106, 181-199): every available reservation matchedOrIgnored,
+       * restoreMatchedReservation for each; the Reservation plugin filters nothing (plugin.go:350-353), skips
+       * PreScore (scoring.go:48-50) and Reserve (plugin.go:755-761) */
+      char* all = (char*)malloc((size_t)(c->n_resv > 0 ? c->n_resv : 1));
+      memset(all, 1, (size_t)(c->n_resv > 0 ? c->n_resv : 1));
+      or_restore(c, all, 1);
+      b = eval_pod(c, &pods[p], now, o, &bs16);
+      bs = bs16;
+      or_restore(c, NULL, 0);
+      free(all);
     } else {
       b = eval_pod(c, &pods[p], now, o, &bs16);
       bs = bs16;

@@ -140,6 +140,54 @@ def test_matched_reservations_schedule_parity(gpu):
     assert ev.check_records(synth.T0) == 0
 
 
+def test_ignored_pods_small_case(gpu):
+    """KE_RSV_IGNORED on the device: the oracle test's three nodes (test_reservations.py ignored_case) -- two ignored
+    pods take the reserved CPUs, the plain twins fit nowhere."""
+    from test_reservations import ignored_case
+    cl, cfg, tables, rs, pods = ignored_case()
+    for v, want in ((abi.RSV_NONE, [-1, -1, -1]), (abi.RSV_IGNORED, [1, 1, -1])):
+        ev = Evaluator(cfg)
+        synth.load_into(ev, cl)
+        synth.load_node_resources(ev, tables)
+        ev.reservations_load(rs)
+        pods["reservation_matched"][:] = v
+        c, _ = ev.schedule(pods, synth.T0)
+        assert c.tolist() == want
+        assert ev.reservations_get()["allocated_pods"][0] == 0
+        assert ev.check_records(synth.T0) == 0
+        ev.close()
+
+
+def test_ignored_pods_between_matched_and_plain(gpu):
+    """Reservation-ignored pods (runs of them and single ones) between KE_RSV_MATCHED and plain pods of one queue:
+    every available reservation's matched restore for them, the unmatched restore for the plain pods, the
+    nominated-reservation path for the matched ones -- placements, totals, reservation state and release records
+    bit-exact with the oracle; the ignored pods go into no reservation."""
+    ev, o, pods, matches = _matched_setup(300, 981, 300)
+    rng = np.random.default_rng(982)
+    free = np.flatnonzero(pods["reservation_matched"] == abi.RSV_NONE)
+    ign = free[rng.random(len(free)) < 0.35]
+    ign = np.union1d(ign, free[(free >= 100) & (free < 140)])  # a long run
+    pods["reservation_matched"][ign] = abi.RSV_IGNORED
+    c1, s1 = ev.schedule(pods, synth.T0, matches=matches)
+    c0, s0 = o.schedule(pods, synth.T0, matches=matches)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5].ravel().tolist()
+    assert np.array_equal(s1, s0)
+    _resv_equal(ev, o)
+    a1, a0 = ev.last_allocations(), o.last_allocations()
+    assert np.array_equal(a1["reservation"], a0["reservation"])
+    assert (a1["reservation"][ign] == 0).all() and (c1[ign] >= 0).sum() >= 20
+    assert ev.check_records(synth.T0) == 0
+    for i in range(0, 300, 29):
+        assert ev.node_info_requested(i) == o.node_info_requested(i), i
+    more = synth.make_pods(120, synth.BASE_SEED + 983, key_base=8_800_000_000)
+    more["reservation_matched"][::2] = abi.RSV_IGNORED
+    c1, s1 = ev.schedule(more, synth.T0)
+    c0, s0 = o.schedule(more, synth.T0)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    ev.close()
+
+
 def test_matched_reservations_weight_one(gpu):
     """weight_reservation 1: the Reservation score mixes with the other plugins' totals instead of dominating;
     every matched pod matches all 40 reservations (several per node compete in NominateReservation)."""

@@ -93,8 +93,8 @@ def test_restore_rules_product_equals_oracle():
 
 
 def test_matched_pod_checks():
-    """KE_RSV_MATCHED needs ke_pod_reservations lists; affinity / ignored pods and ke_eval of a matched pod are
-    refused; lists for other pods or of another length are invalid (host checks, no device call)."""
+    """KE_RSV_MATCHED needs ke_pod_reservations lists; an affinity pod needs its list staged; ke_eval of a matched /
+    ignored pod is refused; lists for other pods or of another length are invalid (host checks, no device call)."""
     cfg = synth.config(4)
     ev = Evaluator(cfg)
     synth.load_into(ev, synth.make_cluster(4, synth.BASE_SEED + 903))
@@ -115,8 +115,14 @@ def test_matched_pod_checks():
     assert e.value.code == abi.ERR_NOT_FOUND
     pods["reservation_matched"][1] = abi.RSV_IGNORED
     with pytest.raises(KoordEvalError) as e:
-        ev.schedule(pods, synth.T0)
+        ev.schedule(pods, synth.T0, matches=[[], [0]])  # an ignored pod lists none
+    assert e.value.code == abi.ERR_INVALID
+    with pytest.raises(KoordEvalError) as e:
+        ev.eval(pods, synth.T0)  # outside ke_schedule
     assert e.value.code == abi.ERR_UNSUPPORTED
+    with pytest.raises(KoordEvalError) as e:
+        ev.schedule(pods, synth.T0)  # accepted by the checks: the device is what is missing here
+    assert e.value.code == abi.ERR_NO_DEVICE
     pods["reservation_matched"][1] = abi.RSV_AFFINITY
     with pytest.raises(KoordEvalError) as e:
         ev.schedule(pods, synth.T0)  # an affinity pod needs its (possibly empty) list staged
@@ -235,7 +241,54 @@ def test_holdings_load_rules():
     with pytest.raises(KoordEvalError) as e:
         ev.reservations_load(rs, neg)
     assert e.value.code == abi.ERR_INVALID
+    # a reservation-ignored pod while reservations hold NUMA resources / CPUs / devices: refused by both
+    pods = synth.make_pods(3, synth.BASE_SEED + 1345)
+    pods["reservation_matched"][2] = abi.RSV_IGNORED
+    with pytest.raises(KoordEvalError) as e:
+        ev.schedule(pods, synth.T0)
+    assert e.value.code == abi.ERR_UNSUPPORTED
+    with pytest.raises(RuntimeError, match=f"rc={abi.ERR_UNSUPPORTED}"):
+        o.schedule(pods, synth.T0)
     ev.close()
+
+
+def ignored_case():
+    """Three nodes with 1 CPU free each; node 1 also holds an 8-CPU reservation's reserve pod (Default policy).  Three
+    4-CPU pods."""
+    cl = synth.make_cluster(3, synth.BASE_SEED + 1401)
+    cl.nodes["requested"][:, 0] = cl.nodes["allocatable"][:, 0] - 1000
+    cl.nodes["requested"][:, 1] = cl.nodes["allocatable"][:, 1] // 2
+    cfg = synth.fit_config(synth.config(3))
+    tables = synth.make_node_resources(cl, 5, gpu_fraction=0, scarce_fraction=0)
+    r = abi.Reservation(node=1, available=1)
+    r.allocatable[0], r.allocatable[1] = 8000, 2**30
+    pods = synth.make_pods(3, synth.BASE_SEED + 1402)
+    pods["requests"][:, 0], pods["requests"][:, 1], pods["requests"][:, 2:] = 4000, 2**28, 0
+    pods["n_xres"] = 2
+    pods["xres_id"][:, 0], pods["xres_value"][:, 0] = abi.XRES_CPU, 4000
+    pods["xres_id"][:, 1], pods["xres_value"][:, 1] = abi.XRES_MEMORY, 2**28
+    return cl, cfg, tables, [r], pods
+
+
+def test_ignored_pods_use_the_reserved_capacity():
+    """KE_RSV_IGNORED (transformer.go:101-106): every available reservation is matchedOrIgnored, its reserve pod
+    leaves NodeInfo (transformer_test.go:1040 'pod has affinity and set reservation ignored': restored), the
+    Reservation Filter passes (plugin_test.go:651) and Reserve assumes nothing (plugin.go:755-761): two 4-CPU ignored
+    pods take node 1's 8 reserved CPUs, the third finds none, the reservation stays unallocated; the same pods not
+    ignored fit nowhere.  The oracle restatement (the GPU twin: test_gpu_reservations.py)."""
+    cl, cfg, tables, rs, pods = ignored_case()
+    for v, want in ((abi.RSV_NONE, [-1, -1, -1]), (abi.RSV_IGNORED, [1, 1, -1])):
+        o = Oracle(cfg, 3)
+        synth.load_into(o, cl)
+        synth.load_node_resources(o, tables)
+        o.reservations_load(rs)
+        pods["reservation_matched"][:] = v
+        c, _ = o.schedule(pods, synth.T0)
+        assert c.tolist() == want
+        assert o.reservations_get()["allocated_pods"][0] == 0 and (o.reservations_get()["allocated"][0] == 0).all()
+        assert o.last_allocations()["reservation"].tolist() == [0, 0, 0]
+        if v == abi.RSV_IGNORED:  # the two pods entered NodeInfo; the reserve pod is back for everyone else
+            assert o.node_info_requested(1)[0][0] == int(cl.nodes["requested"][1, 0]) + 8000
 
 
 RESTORE = json.load(open(os.path.join(HERE, "golden", "reservation_restore.json")))["cases"]
