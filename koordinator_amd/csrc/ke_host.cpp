@@ -1088,6 +1088,19 @@ int64_t max_used_within(int64_t total, int64_t thr) {
   int64_t lo = -USED_DOMAIN, hi = USED_DOMAIN;
   if (usage_percent(hi, total) <= thr) return hi;
   if (usage_percent(lo, total) > thr) return lo - 1;
+  // the boundary is near (thr + 0.5) * total / 100: step from there to the u with pct(u) <= thr < pct(u + 1),
+  // the same element the search below finds (the predicate is monotone); the search when that does not land
+  if (total > 0) {
+    const double g = std::floor(((double)thr + 0.5) * (double)total / 100.0);
+    if (g > (double)(-USED_DOMAIN + 8) && g < (double)(USED_DOMAIN - 8)) {
+      int64_t u = (int64_t)g;
+      for (int s = 0; s < 8; s++) {
+        if (usage_percent(u, total) > thr) u--;
+        else if (usage_percent(u + 1, total) <= thr) u++;
+        else return u;
+      }
+    }
+  }
   while (hi - lo > 1) {  // pct(lo) <= thr < pct(hi)
     int64_t mid = lo + (hi - lo) / 2;
     if (usage_percent(mid, total) <= thr) lo = mid;
@@ -1423,23 +1436,38 @@ static bool should_estimate(const ke_loadaware_args& a, const AssignedPod& info,
 static Terms compute_terms(const ke_loadaware_args& a, const NodeState& ns, bool prod, int64_t now, int64_t* valid_until) {
   Terms t;
   if (ns.asg.empty() && ns.pm.empty()) return t;
-  // buildPodMetricMap(nodeMetric, prod): name -> last PodMetricInfo (helper.go:154-170)
-  std::unordered_map<int64_t, const ke_pod_metric*> metrics;
-  metrics.reserve(ns.pm.size() * 2 + 1);
-  for (const auto& m : ns.pm) {
-    if (prod && m.priority_class != KE_PRIORITY_PROD) continue;
-    metrics[m.pod_key] = &m;
+  // buildPodMetricMap(nodeMetric, prod): name -> last PodMetricInfo (helper.go:154-170), as a key-sorted index
+  // (the last entry of a repeated key kept); `est` marks the estimatedPods among them
+  struct MetricRef {
+    int64_t key;
+    int32_t idx;
+  };
+  thread_local std::vector<MetricRef> metrics;
+  thread_local std::vector<uint8_t> est;
+  metrics.clear();
+  for (size_t i = 0; i < ns.pm.size(); i++) {
+    if (prod && ns.pm[i].priority_class != KE_PRIORITY_PROD) continue;
+    metrics.push_back({ns.pm[i].pod_key, (int32_t)i});
   }
+  std::stable_sort(metrics.begin(), metrics.end(), [](const MetricRef& x, const MetricRef& y) { return x.key < y.key; });
+  size_t w = 0;
+  for (size_t i = 0; i < metrics.size(); i++)
+    if (i + 1 == metrics.size() || metrics[i + 1].key != metrics[i].key) metrics[w++] = metrics[i];
+  metrics.resize(w);
+  est.assign(w, 0);
+  auto find_metric = [&](int64_t key) -> int64_t {
+    auto it = std::lower_bound(metrics.begin(), metrics.end(), key, [](const MetricRef& x, int64_t k) { return x.key < k; });
+    return it != metrics.end() && it->key == key ? it - metrics.begin() : -1;
+  };
   const bool has_ut = ns.nm.has_update_time;
   const int64_t ut = ns.nm.update_time_ns;
   const int64_t interval = ns.nm.report_interval_seconds != KE_ABSENT ? ns.nm.report_interval_seconds * NS : DEFAULT_REPORT_INTERVAL_NS;
   const bool score_agg = a.has_aggregated && a.agg_score_type != KE_AGG_NONE;
   const bool score_agg_missing = score_agg && target_aggregated(ns, a.agg_score_duration_ns, a.agg_score_type) == nullptr;
-  std::unordered_map<int64_t, bool> estimated;  // estimatedPods set
   for (const auto& info : ns.asg) {  // estimatedAssignedPodUsed (load_aware.go:315-358)
     if (prod && info.pod.priority_class != KE_PRIORITY_PROD) continue;
-    auto it = metrics.find(info.pod.pod_key);
-    const ke_pod_metric* m = it == metrics.end() ? nullptr : it->second;
+    const int64_t j = find_metric(info.pod.pod_key);
+    const ke_pod_metric* m = j < 0 ? nullptr : &ns.pm[(size_t)metrics[(size_t)j].idx];
     const bool static_cond = (m == nullptr || m->usage.n_keys == 0) || (has_ut ? info.ts > ut : true) ||
                              (has_ut && info.ts < ut && ut - info.ts < interval) || score_agg_missing;
     if (!static_cond) {
@@ -1454,14 +1482,14 @@ static Terms compute_terms(const ke_loadaware_args& a, const NodeState& ns, bool
         if (m && m->usage.present[r] && m->usage.value[r] > v) v = m->usage.value[r];
         t.assigned[r] += v;
       }
-      estimated[info.pod.pod_key] = true;
+      if (j >= 0) est[(size_t)j] = 1;  // estimatedPods (only its members with a metric are read below)
     }
   }
-  for (const auto& kv : metrics) {  // sumPodUsages (helper.go:172-186)
-    const bool is_est = estimated.count(kv.first) != 0;
+  for (size_t j = 0; j < metrics.size(); j++) {  // sumPodUsages (helper.go:172-186)
+    const ke_pod_metric& m = ns.pm[(size_t)metrics[j].idx];
     for (int r = 0; r < KE_NRES; r++) {
-      if (!kv.second->usage.present[r]) continue;
-      (is_est ? t.est_actual : t.other_actual)[r] += kv.second->usage.value[r];
+      if (!m.usage.present[r]) continue;
+      (est[j] ? t.est_actual : t.other_actual)[r] += m.usage.value[r];
     }
   }
   return t;

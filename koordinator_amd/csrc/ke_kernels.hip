@@ -6219,6 +6219,9 @@ struct DeviceState {
   int64_t ds_staging_cap = 0;
   PinnedVec<DevPod> host_pods;    // the last uploaded queue (batch segmentation), page-locked
   PinnedVec<uint8_t> h_out;       // ke_schedule's readback staging (placements, allocations, stamps)
+  PinnedVec<int64_t> h_refresh;   // device_refresh's row staging (every table's rows + indices, one sync)
+  PinnedVec<uint8_t> h_rsv;       // a matched pod's RsvPair / RsvOvr uploads
+  PinnedVec<int32_t> h_rsv_out;   // k_rsv_pick's result words, read back by the call's own copies
   std::vector<DevPodHint> host_ph;  // its hinted pods' records (the async upload reads them)
   // NUMA topology
   bool numa_alloc = false;         // soa.nf / soa.nm allocated
@@ -6428,8 +6431,9 @@ int device_rsv_views(Context* ctx, const ke_pod& pod, int64_t now, const std::ve
 // k_rsv_pick's result of the last device_schedule (a segment of one KE_RSV_MATCHED pod)
 int device_rsv_result(Context* ctx, int32_t* out4) {
   DeviceState* d = ctx->dev;
-  HIP_OK(hipMemcpyAsync(out4, d->d_rsv_out, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, d->stream));
-  HIP_OK(hipStreamSynchronize(d->stream));
+  // copied after k_rsv_pick on its stream, complete with the call (device_schedule waited for every stream)
+  if (d->h_rsv_out.size() < 4) return fail(KE_ERR_DEVICE, "no k_rsv_pick result staged");
+  for (int i = 0; i < 4; i++) out4[i] = d->h_rsv_out[i];
   return KE_OK;
 }
 
@@ -6772,81 +6776,89 @@ int device_refresh(Context* ctx, int64_t now) {
     ctx->clean_n_nodes = ctx->n_nodes;
     ctx->dirty_list.clear();  // every node < n_nodes is clean now
   }
-  if (!dsidx.empty()) {
-    const int64_t n = (int64_t)dsidx.size();
-    if (d->ds_staging_cap < n) {
-      if (d->d_dsrows) HIP_OK(hipFree(d->d_dsrows));
-      HIP_OK(hipMalloc(&d->d_dsrows, sizeof(int64_t) * DS_ROW_WORDS * n + sizeof(int32_t) * n));
-      d->ds_staging_cap = n;
+  // every table's rows and indices go through one page-locked staging area: async copies and scatters on the
+  // stream, one synchronisation at the end (the staging is reused by the next refresh)
+  static_assert(sizeof(Row) % sizeof(int64_t) == 0, "Row staged in int64 words");
+  auto words = [](size_t bytes) { return (bytes + sizeof(int64_t) - 1) / sizeof(int64_t); };
+  const size_t total = dsrows.size() + words(sizeof(int32_t) * dsidx.size()) + nrows.size() +
+                       words(sizeof(int32_t) * nidx.size()) + xrows.size() + words(sizeof(int32_t) * xidx.size()) +
+                       crows.size() + words(sizeof(int32_t) * cidx.size()) + words(sizeof(Row) * rows.size()) +
+                       words(sizeof(int32_t) * idx.size());
+  if (total == 0) return KE_OK;
+  if (!d->h_refresh.resize(total)) return fail(KE_ERR_DEVICE, "hipHostMalloc of the row staging");
+  size_t at = 0;
+  auto stage = [&](const void* src, size_t bytes) {  // -> the staged copy
+    void* dst = d->h_refresh.data() + at;
+    if (bytes) std::memcpy(dst, src, bytes);
+    at += words(bytes);
+    return dst;
+  };
+  // one table: rows (row_words int64 per node) + indices into its device staging buffer, then its scatter
+  auto table = [&](int64_t** dbuf, int64_t* cap, const std::vector<int64_t>& hrows, const std::vector<int32_t>& hidx,
+                   int64_t row_words, int32_t** didx) -> int {
+    const int64_t n = (int64_t)hidx.size();
+    if (*cap < n) {
+      if (*dbuf) HIP_OK(hipFree(*dbuf));
+      HIP_OK(hipMalloc(dbuf, sizeof(int64_t) * row_words * n + sizeof(int32_t) * n));
+      *cap = n;
     }
-    int32_t* didx = reinterpret_cast<int32_t*>(d->d_dsrows + DS_ROW_WORDS * n);
-    HIP_OK(hipMemcpyAsync(d->d_dsrows, dsrows.data(), sizeof(int64_t) * dsrows.size(), hipMemcpyHostToDevice, d->stream));
-    HIP_OK(hipMemcpyAsync(didx, dsidx.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, d->stream));
-    hipLaunchKernelGGL(k_scatter_ds, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, d->stream, d->soa, d->d_dsrows, didx,
-                       (int)n);
+    *didx = reinterpret_cast<int32_t*>(*dbuf + row_words * n);
+    HIP_OK(hipMemcpyAsync(*dbuf, stage(hrows.data(), sizeof(int64_t) * hrows.size()), sizeof(int64_t) * hrows.size(),
+                          hipMemcpyHostToDevice, d->stream));
+    HIP_OK(hipMemcpyAsync(*didx, stage(hidx.data(), sizeof(int32_t) * n), sizeof(int32_t) * n, hipMemcpyHostToDevice,
+                          d->stream));
+    return KE_OK;
+  };
+  int32_t* didx = nullptr;
+  if (!dsidx.empty()) {
+    const int n = (int)dsidx.size();
+    rc = table(&d->d_dsrows, &d->ds_staging_cap, dsrows, dsidx, DS_ROW_WORDS, &didx);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_scatter_ds, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, d->stream, d->soa, d->d_dsrows, didx, n);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipStreamSynchronize(d->stream));  // `dsrows` is a local host vector
   }
   if (!nidx.empty()) {
-    const int64_t n = (int64_t)nidx.size();
-    if (d->numa_staging_cap < n) {
-      if (d->d_numarows) HIP_OK(hipFree(d->d_numarows));
-      HIP_OK(hipMalloc(&d->d_numarows, sizeof(int64_t) * NUMA_ROW_WORDS * n + sizeof(int32_t) * n));
-      d->numa_staging_cap = n;
-    }
-    int32_t* didx = reinterpret_cast<int32_t*>(d->d_numarows + NUMA_ROW_WORDS * n);
-    HIP_OK(hipMemcpyAsync(d->d_numarows, nrows.data(), sizeof(int64_t) * nrows.size(), hipMemcpyHostToDevice, d->stream));
-    HIP_OK(hipMemcpyAsync(didx, nidx.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, d->stream));
+    const int n = (int)nidx.size();
+    rc = table(&d->d_numarows, &d->numa_staging_cap, nrows, nidx, NUMA_ROW_WORDS, &didx);
+    if (rc) return rc;
     hipLaunchKernelGGL(k_scatter_numa, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, d->stream, d->soa, d->d_numarows,
-                       didx, (int)n);
+                       didx, n);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipStreamSynchronize(d->stream));  // `nrows` is a local host vector
   }
   if (!xidx.empty()) {
-    const int64_t n = (int64_t)xidx.size();
-    if (d->ext_staging_cap < n) {
-      if (d->d_xrows) HIP_OK(hipFree(d->d_xrows));
-      HIP_OK(hipMalloc(&d->d_xrows, sizeof(int64_t) * XROW_WORDS * n + sizeof(int32_t) * n));
-      d->ext_staging_cap = n;
-    }
-    int32_t* didx = reinterpret_cast<int32_t*>(d->d_xrows + XROW_WORDS * n);
-    HIP_OK(hipMemcpyAsync(d->d_xrows, xrows.data(), sizeof(int64_t) * xrows.size(), hipMemcpyHostToDevice, d->stream));
-    HIP_OK(hipMemcpyAsync(didx, xidx.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, d->stream));
+    const int n = (int)xidx.size();
+    rc = table(&d->d_xrows, &d->ext_staging_cap, xrows, xidx, XROW_WORDS, &didx);
+    if (rc) return rc;
     hipLaunchKernelGGL(k_scatter_ext, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, d->stream, d->soa, d->d_xrows,
-                       didx, (int)n);
+                       didx, n);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipStreamSynchronize(d->stream));  // `xrows` is a local host vector
   }
   if (!cidx.empty()) {
-    const int64_t n = (int64_t)cidx.size();
-    if (d->cpu_staging_cap < n) {
-      if (d->d_cpurows) HIP_OK(hipFree(d->d_cpurows));
-      HIP_OK(hipMalloc(&d->d_cpurows, sizeof(int64_t) * CPU_ROW_WORDS * n + sizeof(int32_t) * n));
-      d->cpu_staging_cap = n;
-    }
-    int32_t* didx = reinterpret_cast<int32_t*>(d->d_cpurows + CPU_ROW_WORDS * n);
-    HIP_OK(hipMemcpyAsync(d->d_cpurows, crows.data(), sizeof(int64_t) * crows.size(), hipMemcpyHostToDevice, d->stream));
-    HIP_OK(hipMemcpyAsync(didx, cidx.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, d->stream));
-    hipLaunchKernelGGL(k_scatter_cpu, dim3((unsigned)n), dim3(CPU_SLOTS), 0, d->stream, d->soa, d->d_cpurows, didx, (int)n);
+    const int n = (int)cidx.size();
+    rc = table(&d->d_cpurows, &d->cpu_staging_cap, crows, cidx, CPU_ROW_WORDS, &didx);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_scatter_cpu, dim3((unsigned)n), dim3(CPU_SLOTS), 0, d->stream, d->soa, d->d_cpurows, didx, n);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipStreamSynchronize(d->stream));  // `crows` is a local host vector
   }
-  if (rows.empty()) return KE_OK;
-  HIP_OK(hipSetDevice(d->device));
-  const int64_t n = (int64_t)rows.size();
-  if (d->staging_cap < n) {
-    if (d->d_rows) HIP_OK(hipFree(d->d_rows));
-    if (d->d_idx) HIP_OK(hipFree(d->d_idx));
-    HIP_OK(hipMalloc(&d->d_rows, sizeof(Row) * n));
-    HIP_OK(hipMalloc(&d->d_idx, sizeof(int32_t) * n));
-    d->staging_cap = n;
+  if (!rows.empty()) {
+    HIP_OK(hipSetDevice(d->device));
+    const int64_t n = (int64_t)rows.size();
+    if (d->staging_cap < n) {
+      if (d->d_rows) HIP_OK(hipFree(d->d_rows));
+      if (d->d_idx) HIP_OK(hipFree(d->d_idx));
+      HIP_OK(hipMalloc(&d->d_rows, sizeof(Row) * n));
+      HIP_OK(hipMalloc(&d->d_idx, sizeof(int32_t) * n));
+      d->staging_cap = n;
+    }
+    HIP_OK(hipMemcpyAsync(d->d_rows, stage(rows.data(), sizeof(Row) * n), sizeof(Row) * n, hipMemcpyHostToDevice,
+                          d->stream));
+    HIP_OK(hipMemcpyAsync(d->d_idx, stage(idx.data(), sizeof(int32_t) * n), sizeof(int32_t) * n, hipMemcpyHostToDevice,
+                          d->stream));
+    hipLaunchKernelGGL(k_scatter_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, d->stream, d->soa, d->d_rows,
+                       d->d_idx, (int)n, make_kargs(ctx, now));
+    HIP_OK(hipGetLastError());
   }
-  HIP_OK(hipMemcpyAsync(d->d_rows, rows.data(), sizeof(Row) * n, hipMemcpyHostToDevice, d->stream));
-  HIP_OK(hipMemcpyAsync(d->d_idx, idx.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, d->stream));
-  hipLaunchKernelGGL(k_scatter_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, d->stream, d->soa, d->d_rows,
-                     d->d_idx, (int)n, make_kargs(ctx, now));
-  HIP_OK(hipGetLastError());
-  HIP_OK(hipStreamSynchronize(d->stream));  // `rows` is a local host vector
+  HIP_OK(hipStreamSynchronize(d->stream));  // (the staging is reused; the eval streams read the rows)
   return KE_OK;
 }
 
@@ -7121,17 +7133,27 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
       if (q.node < 0 || q.node >= ctx->n_nodes) return fail(KE_ERR_DEVICE, "reservation pair node out of range");
     rc = ensure((void**)&d->d_rsv, &d->rsv_cap, (int64_t)sizeof(RsvPair) * (int64_t)ctx->rsv_pairs.size());
     if (rc) return rc;
-    if (!ctx->rsv_pairs.empty())
-      HIP_OK(hipMemcpyAsync(d->d_rsv, ctx->rsv_pairs.data(), sizeof(RsvPair) * ctx->rsv_pairs.size(),
-                            hipMemcpyHostToDevice, d->stream));
+    if (!d->h_rsv_out.resize(4)) return fail(KE_ERR_DEVICE, "hipHostMalloc of the reservation staging");
+    for (int i = 0; i < 4; i++) d->h_rsv_out[i] = -1;
+  }
+  // the matched pod's pairs and allocate-from-reservation decisions, staged page-locked (the previous call's copies
+  // from this buffer completed with that call)
+  const size_t rsv_bytes = sizeof(RsvPair) * ctx->rsv_pairs.size(), ovr_bytes = sizeof(RsvOvr) * ctx->rsv_ovr.size();
+  if (rsv_bytes + ovr_bytes && !d->h_rsv.resize(rsv_bytes + ovr_bytes))
+    return fail(KE_ERR_DEVICE, "hipHostMalloc of the reservation staging");
+  if (!ctx->rsv_pairs.empty() || ctx->rsv_affinity) {
+    if (rsv_bytes) {
+      std::memcpy(d->h_rsv.data(), ctx->rsv_pairs.data(), rsv_bytes);
+      HIP_OK(hipMemcpyAsync(d->d_rsv, d->h_rsv.data(), rsv_bytes, hipMemcpyHostToDevice, d->stream));
+    }
     HIP_OK(hipMemsetAsync(d->d_rsv_out, 0xFF, sizeof(int32_t) * 4, d->stream));
   }
   d->soa.n_rovr = 0;  // a matched pod's allocate-from-reservation decisions (NF_RSV_CS rows read them)
   if (!ctx->rsv_ovr.empty()) {
     rc = ensure((void**)&d->d_rovr, &d->rovr_cap, (int64_t)sizeof(RsvOvr) * (int64_t)ctx->rsv_ovr.size());
     if (rc) return rc;
-    HIP_OK(hipMemcpyAsync(d->d_rovr, ctx->rsv_ovr.data(), sizeof(RsvOvr) * ctx->rsv_ovr.size(), hipMemcpyHostToDevice,
-                          d->stream));
+    std::memcpy(d->h_rsv.data() + rsv_bytes, ctx->rsv_ovr.data(), ovr_bytes);
+    HIP_OK(hipMemcpyAsync(d->d_rovr, d->h_rsv.data() + rsv_bytes, ovr_bytes, hipMemcpyHostToDevice, d->stream));
     d->soa.rovr = d->d_rovr;
     d->soa.n_rovr = (int32_t)ctx->rsv_ovr.size();
   }
@@ -7315,9 +7337,11 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
       if (argmax1) {  // d_cand[0] zeroed by k_batch_begin
         hipLaunchKernelGGL((ds ? k_argmax1<true> : k_argmax1<false>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
                            es, scores, 0, N, d->d_dsraw, d->d_dsmax, k.wp_ds, d->d_cand, d->d_cand_cnt);
-        if (!ctx->rsv_pairs.empty() || ctx->rsv_affinity)  // the pod's matched reservations: the Reservation plugin
+        if (!ctx->rsv_pairs.empty() || ctx->rsv_affinity) {  // the pod's matched reservations: the Reservation plugin
           hipLaunchKernelGGL(k_rsv_pick, dim3(1), dim3(64), 0, es, scores, d->d_rsv, (int)ctx->rsv_pairs.size(),
                              (int64_t)ctx->cfg.weight_reservation, (int)ctx->rsv_affinity, d->d_cand, d->d_rsv_out);
+          HIP_OK(hipMemcpyAsync(d->h_rsv_out.data(), d->d_rsv_out, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, es));
+        }
       } else if (!sharded && parts > 1) {
         const int gw = gath_words(L);
         const bool rc = select_seg(0, select_part(0, N, parts)) <= SEL_RC * 512;
