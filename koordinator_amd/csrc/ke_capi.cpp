@@ -157,7 +157,7 @@ static int check_matches(Context& c, const ke_pod* pods, int32_t n) {
     if (rm != KE_RSV_MATCHED && rm != KE_RSV_AFFINITY) {
       if (cnt) return fail(KE_ERR_INVALID, "reservations listed for a pod that is not KE_RSV_MATCHED / AFFINITY");
       if (rm == KE_RSV_IGNORED) {
-        const int rc = resv_ignore_check(c);
+        const int rc = resv_ignore_check(c, pods[p], c.staged[(size_t)p].flags);
         if (rc) return rc;
       }
       continue;

@@ -784,13 +784,25 @@ int resv_check(const Context& c, const int32_t* ids, int32_t n_ids) {
 // an affinity, plugin.go:350-353), PreScore / Score skip it (scoring.go:48-50) and Reserve assumes it into no
 // reservation (plugin.go:755-761).  NodeNUMAResource / DeviceShare allocate it from the node and the ignored
 // reservations' unallocated remainder (tryAllocateIgnoreReservation, nodenumaresource/reservation.go:437-490,
-// deviceshare/reservation.go:290-310): that remainder is restated only when no reservation holds NUMA resources,
-// CPUs or devices, where it is empty and the pod's rows are the matched restore alone.
-int resv_ignore_check(const Context& c) {
-  for (size_t i = 0; i < c.resv_holds.size(); i++)
-    if (c.resv_holds[i])
-      return fail(KE_ERR_UNSUPPORTED, "a reservation-ignored pod while a reservation holds NUMA resources, CPUs or "
-                                      "devices (tryAllocateIgnoreReservation over held resources)");
+// deviceshare/reservation.go:290-310): that remainder of held resources is not restated, so the pod is refused
+// where it would read it -- a DeviceShare pod while a reservation holds devices; a pod that may bind CPUs or has
+// its own NUMA policy while one holds NUMA resources or CPUs; any pod while one of those sits on a node with a
+// NUMA topology policy (its hints read the zones).  Elsewhere the held state is not read and the rows are exact.
+int resv_ignore_check(const Context& c, const ke_pod& pod, uint32_t pod_flags) {
+  bool dev = false, numa_cpu = false, on_policy_node = false;
+  for (size_t i = 0; i < c.resv_holds.size(); i++) {
+    const uint8_t h = c.resv_holds[i];
+    dev = dev || (h & KE_RSV_HOLDS_DEVICES);
+    if (h & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)) {
+      numa_cpu = true;
+      on_policy_node = on_policy_node || c.nodes[(size_t)c.resv[i].node].node.numa_topology_policy != KE_NUMA_POLICY_NONE;
+    }
+  }
+  const bool binds = (pod_flags & PF_CPUSET) || (c.n_bind_nodes > 0 && pod.requests[KE_RES_CPU] > 0);
+  if ((dev && (pod_flags & (PF_DS | PF_DS_HINT))) ||
+      (numa_cpu && (binds || pod.numa_topology_policy != KE_NUMA_POLICY_NONE)) || on_policy_node)
+    return fail(KE_ERR_UNSUPPORTED, "a reservation-ignored pod reading resources a reservation holds "
+                                    "(tryAllocateIgnoreReservation's remainder)");
   return KE_OK;
 }
 

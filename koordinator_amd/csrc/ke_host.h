@@ -336,7 +336,7 @@ void resv_views(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids
 int resv_check(const Context& c, const int32_t* ids, int32_t n_ids);
 // a run of KE_RSV_IGNORED pods: the rows with every usable reservation matchedOrIgnored (begin) and back to the
 // restore every other pod sees (end); resv_ignore_check is the refusal, checked before any segment runs
-int resv_ignore_check(const Context& c);
+int resv_ignore_check(const Context& c, const ke_pod& pod, uint32_t pod_flags);
 void resv_ignore_begin(Context& c);
 void resv_ignore_end(Context& c);
 void resv_finish(Context& c, int32_t chosen_local, const ke_pod& pod, int32_t* assumed, const uint64_t* cpuset = nullptr,

@@ -4275,9 +4275,27 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
     const int32_t n_ids = c->moff && c->m_pods == n_pods ? c->moff[p + 1] - c->moff[p] : 0;
     if (pods[p].reservation_matched != KE_RSV_MATCHED && pods[p].reservation_matched != KE_RSV_AFFINITY) {
       if (n_ids) return KE_ERR_INVALID;
-      /* a reservation-ignored pod: tryAllocateIgnoreReservation's remainder of held resources is not restated */
-      for (int32_t r = 0; pods[p].reservation_matched == KE_RSV_IGNORED && c->ralloc && r < c->n_resv; r++)
-        if (or_holds_of(&c->ralloc[r])) return KE_ERR_UNSUPPORTED;
+      /* a reservation-ignored pod reading held resources: tryAllocateIgnoreReservation's remainder is not restated
+       * (a DeviceShare pod and held devices; a pod binding CPUs or with a NUMA policy and held NUMA resources /
+       * CPUs; held NUMA resources / CPUs on a NUMA-policy node) */
+      if (pods[p].reservation_matched == KE_RSV_IGNORED && c->ralloc) {
+        int dev = 0, numa_cpu = 0, on_policy = 0;
+        for (int32_t r = 0; r < c->n_resv; r++) {
+          const int h = or_holds_of(&c->ralloc[r]);
+          dev |= (h & KE_RSV_HOLDS_DEVICES) != 0;
+          if (h & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)) {
+            numa_cpu = 1;
+            on_policy |= c->nodes[c->resv[r].node].node.numa_topology_policy != KE_NUMA_POLICY_NONE;
+          }
+        }
+        ds_pod d;
+        ds_prepare_pod(c, &pods[p], &d);
+        cpuset_state st;
+        cpuset_prefilter(c, &pods[p], &st);
+        const int binds = st.rcb || st.invalid || (node_bind && pods[p].requests[KE_RES_CPU] > 0);
+        if ((dev && !d.skip) || (numa_cpu && (binds || pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE)) || on_policy)
+          return KE_ERR_UNSUPPORTED;
+      }
       continue;
     }
     if (!(c->moff && c->m_pods == n_pods)) return KE_ERR_INVALID;

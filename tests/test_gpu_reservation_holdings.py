@@ -7,7 +7,7 @@ matrices, schedules, cpusets, NUMA allocations, device minors and the reservatio
 import numpy as np
 import pytest
 
-from koordinator_amd import Evaluator, abi, synth
+from koordinator_amd import Evaluator, KoordEvalError, abi, synth
 from oracle.binding import Oracle
 from test_gpu_cpuset import assert_eval_equal, assert_schedule_equal
 
@@ -85,7 +85,7 @@ def test_holdings_reload_and_release_parity(gpu):
     assert np.array_equal(ev.reservation_allocs_get(), o.reservation_allocs_get())
 
 
-def cpuset_matched_setup(n, seed, n_pods, affinity=0.3, tight_pods=0.0):
+def cpuset_matched_setup(n, seed, n_pods, affinity=0.3, tight_pods=0.0, node_bind=True):
     """Nodes without NUMA policies carrying CPU tables, reservations whose reserve pods hold cpusets (owner pods
     holding part of them, every allocate policy), and a queue of cpuset pods of which ~40 % match the reservations
     of a few owner groups (KE_RSV_MATCHED, or KE_RSV_AFFINITY for `affinity` of them).  `tight_pods`: that fraction
@@ -93,6 +93,8 @@ def cpuset_matched_setup(n, seed, n_pods, affinity=0.3, tight_pods=0.0):
     rng = np.random.default_rng(seed)
     cl = synth.make_cluster(n, synth.BASE_SEED + seed, amplified_fraction=0.0)
     zones, tabs = synth.make_numa_cpus(cl, synth.BASE_SEED + seed + 1, policy_weights=(1, 0, 0, 0))
+    if not node_bind:
+        cl.nodes["cpu_bind_policy"] = 0
     rs, al = synth.make_reservation_holdings(cl, synth.BASE_SEED + seed + 2, zones, tabs, None, frac=0.5)
     for i in np.unique(rs["node"]):
         if rng.random() < tight_pods:
@@ -160,3 +162,31 @@ def test_matched_cpuset_from_reservations_parity(gpu, seed, affinity, tight):
     assert np.array_equal(ev.last_cpusets, o.last_cpusets)
     _holdings_equal(ev, o)
     assert ev.check_records(synth.T0) == 0
+
+
+def test_ignored_pods_beside_held_cpusets(gpu):
+    """Reservation-ignored pods that read no held resource (no CPU binding: no cpuset pod, no node CPU bind policy;
+    no NUMA policy; nodes without NUMA policies) in a cluster whose reservations hold NUMA resources and cpusets, between
+    cpuset pods and matched cpuset pods: every reservation's matched restore for them, the held state for the rest --
+    placements, scores, cpusets and reservation state bit-exact with the oracle.  An ignored cpuset pod is refused by
+    both (tryAllocateIgnoreReservation's remainder of held CPUs is not restated)."""
+    ev, o, pods, matches, rs = cpuset_matched_setup(300, 1371, 300, affinity=0.0, node_bind=False)
+    cs = np.isin(pods["qos_class"], [abi.QOS_LSE, abi.QOS_LSR]) & (pods["priority_class"] == abi.PRIORITY_PROD)
+    free = np.flatnonzero((pods["reservation_matched"] == abi.RSV_NONE) & ~cs)
+    assert len(free) >= 40
+    pods["reservation_matched"][free[::2]] = abi.RSV_IGNORED
+    c1, s1 = ev.schedule(pods, synth.T0, matches=matches)
+    c0, s0 = o.schedule(pods, synth.T0, matches=matches)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5].ravel().tolist()
+    assert np.array_equal(s1, s0)
+    assert np.array_equal(ev.last_cpusets, o.last_cpusets)
+    _holdings_equal(ev, o)
+    assert (ev.last_allocations()["reservation"][free[::2]] == 0).all()
+    assert ev.check_records(synth.T0) == 0
+    bad = synth.make_cpuset_pods(4, synth.BASE_SEED + 1375, cpuset_fraction=1.0, key_base=7_900_000_000)
+    bad["reservation_matched"][1] = abi.RSV_IGNORED
+    with pytest.raises(KoordEvalError) as e:
+        ev.schedule(bad, synth.T0)
+    assert e.value.code == abi.ERR_UNSUPPORTED
+    with pytest.raises(RuntimeError, match=f"rc={abi.ERR_UNSUPPORTED}"):
+        o.schedule(bad, synth.T0)

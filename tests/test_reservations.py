@@ -241,14 +241,16 @@ def test_holdings_load_rules():
     with pytest.raises(KoordEvalError) as e:
         ev.reservations_load(rs, neg)
     assert e.value.code == abi.ERR_INVALID
-    # a reservation-ignored pod while reservations hold NUMA resources / CPUs / devices: refused by both
-    pods = synth.make_pods(3, synth.BASE_SEED + 1345)
-    pods["reservation_matched"][2] = abi.RSV_IGNORED
+    # a reservation-ignored pod that would read held resources (here a DeviceShare pod beside held devices): refused
+    # by both; one that reads none passes the checks (the product stops at the missing device)
+    ds = synth.make_ds_pods(3, synth.BASE_SEED + 1345)
+    ds["reservation_matched"][:] = abi.RSV_IGNORED
+    i_ds = int(np.flatnonzero((ds["device_requests"] != 0).any(1))[0])
     with pytest.raises(KoordEvalError) as e:
-        ev.schedule(pods, synth.T0)
+        ev.schedule(ds[i_ds:i_ds + 1], synth.T0)
     assert e.value.code == abi.ERR_UNSUPPORTED
     with pytest.raises(RuntimeError, match=f"rc={abi.ERR_UNSUPPORTED}"):
-        o.schedule(pods, synth.T0)
+        o.schedule(ds[i_ds:i_ds + 1], synth.T0)
     ev.close()
 
 
