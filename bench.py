@@ -178,7 +178,9 @@ def c3_parity(chosen, score, n_nodes, n_pods, config):
     g = np.load(f)
     if int(g["nodes"]) != n_nodes:
         return "unchecked (no fixture for this workload)"
-    m = min(n_pods, int(g["pods"]))
+    if n_pods != int(g["pods"]):  # synth.make_pods of another length is another queue, not a prefix
+        return f"unchecked (the fixture holds the {int(g['pods'])}-pod queue; this run's queue has {n_pods})"
+    m = n_pods
     ok = (chosen[:m] == g["chosen"][:m]) & (score[:m] == g["score"][:m].astype(np.int32))
     if ok.all():
         return f"bit-exact {m}/{int(g['pods'])} (placements + scores vs the oracle fixture)"
