@@ -838,8 +838,9 @@ int ke_reservations_get(ke_ctx* ctx, int32_t n, ke_reservation* out);
  * the restored NodeInfo (ke_node.pod_count with the matched reserve pods removed) minus the node's matched
  * reservations, plus one, within ke_node.allowed_pods.
  * Refused (KE_ERR_UNSUPPORTED, by ke_schedule's argument checks before any pod of the call is scheduled): such a
- * pod with DeviceShare requests, cpuset binding or a NUMA topology policy, a usable matched reservation holding NUMA
- * resources or a cpuset on a node with a NUMA topology policy, a sharded context; ke_eval of such a pod.  The lists
+ * pod with DeviceShare or scalar requests, one with a NUMA topology policy whose usable matched reservation holds
+ * NUMA resources or a cpuset, a usable matched reservation holding NUMA resources or a cpuset on a node with a NUMA
+ * topology policy, a sharded context; ke_eval of such a pod.  The lists
  * are consumed by the next ke_schedule call, a refused one included. */
 int ke_pod_reservations(ke_ctx* ctx, int32_t n_pods, const int32_t* offsets, const int32_t* ids);
 /* NodeInfo.Requested / NonZeroRequested (MilliCPU, Memory) of `node` as the plugins see it for a pod that

@@ -169,8 +169,17 @@ static int check_matches(Context& c, const ke_pod* pods, int32_t n) {
     for (int r = 0; r < KE_PDR_COUNT; r++) scalar = scalar || pods[p].device_requests[r] != 0;
     if ((f & (PF_DS | PF_DS_HINT)) || scalar)
       return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations with device or scalar requests");
-    if (pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE)
-      return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations with a NUMA topology policy");
+    // a pod with its own NUMA policy takes hints on every node: a matched reservation holding NUMA resources or
+    // CPUs would need them over its allocate-from-reservation trials (not restated); without such holdings its
+    // matched restore moves only NodeInfo.Requested, which the hints do not read
+    if (pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE && !c.resv_holds.empty())
+      for (int32_t j = c.match_off[(size_t)p]; j < c.match_off[(size_t)p + 1]; j++) {
+        const int32_t r = c.match_ids[(size_t)j];
+        if (r >= 0 && r < (int32_t)c.resv.size() && resv_usable(c.resv[(size_t)r]) &&
+            (c.resv_holds[(size_t)r] & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)))
+          return fail(KE_ERR_UNSUPPORTED, "a pod with a NUMA topology policy matching a reservation that holds NUMA "
+                                          "resources or CPUs");
+      }
     if (c.dev && device_sharded(&c)) return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations in a sharded context");
     const int rc = resv_check(c, c.match_ids.data() + c.match_off[(size_t)p], cnt);
     if (rc) return rc;

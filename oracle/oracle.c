@@ -4304,10 +4304,16 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
     ds_pod d;
     ds_prepare_pod(c, &pods[p], &d);
     (void)node_bind;
-    int scalar = pods[p].has_other_requests || !d.skip || pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE;
+    int scalar = pods[p].has_other_requests || !d.skip;
     for (int r = KE_NRES; r < KE_RES_COUNT; r++) scalar |= pods[p].requests[r] != 0;
     for (int r = 0; r < KE_PDR_COUNT; r++) scalar |= pods[p].device_requests[r] != 0;
     if (scalar) return KE_ERR_UNSUPPORTED;
+    /* a pod with its own NUMA policy matching a reservation that holds NUMA resources / CPUs: its hints over the
+     * allocate-from-reservation trials are not restated */
+    for (int32_t j = c->moff[p]; pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE && j < c->moff[p + 1]; j++)
+      if (or_resv_usable(&c->resv[c->mids[j]]) && c->ralloc &&
+          (or_holds_of(&c->ralloc[c->mids[j]]) & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)))
+        return KE_ERR_UNSUPPORTED;
     /* a matched reservation holding a NUMA allocation or a cpuset on a NUMA-policy node: its allocate-from-
      * reservation path (tryAllocateFromReservation in the hints) is not restated */
     for (int32_t j = c->moff[p]; j < c->moff[p + 1]; j++)

@@ -188,6 +188,60 @@ def test_ignored_pods_between_matched_and_plain(gpu):
     ev.close()
 
 
+def test_matched_pods_with_numa_policies(gpu):
+    """KE_RSV_MATCHED pods with their own NUMA topology policy (and cpuset / plain pods) on a cluster of NUMA-policy
+    nodes beside cpu / memory reservations (no holdings): the matched restore moves NodeInfo.Requested only, which
+    the hints do not read; the Reservation score and Reserve as for any matched pod -- placements, totals, NUMA
+    allocations and reservation state bit-exact with the oracle."""
+    n = 300
+    rng = np.random.default_rng(991)
+    cl = synth.make_cluster(n, synth.BASE_SEED + 991, amplified_fraction=0.2)
+    zones, tabs = synth.make_numa_cpus(cl, synth.BASE_SEED + 992)
+    rs, grp = [], []
+    for g in range(10):
+        for _ in range(int(rng.integers(2, 7))):
+            r = abi.Reservation(node=int(rng.integers(0, n)), available=1, allocate_once=int(rng.random() < 0.2),
+                                allocate_policy=int(rng.integers(0, 3)), allocated_pods=int(rng.choice([0, 1])),
+                                order=int(rng.choice([0, 0, 5])))
+            r.allocatable[0] = int(rng.choice([2000, 4000, 8000]))
+            r.allocatable[1] = int(rng.choice([4, 8, 16])) * 2**30
+            if r.allocated_pods:
+                r.allocated[0], r.allocated[1] = r.allocatable[0] // 2, r.allocatable[1] // 4
+            cl.nodes["requested"][r.node, 0] += r.allocatable[0]
+            cl.nodes["requested"][r.node, 1] += r.allocatable[1]
+            rs.append(r)
+            grp.append(g)
+    cfg = synth.config(n)
+    ev, o = Evaluator(cfg), Oracle(cfg, n)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        synth.load_numa(h, zones)
+        synth.load_cpus(h, tabs)
+        h.reservations_load(rs)
+    pods = synth.make_numa_cpuset_pods(300, synth.BASE_SEED + 993, policy_fraction=0.4)
+    grp = np.asarray(grp)
+    elig = ((pods["requests"][:, 2:] == 0).all(1) & (pods["has_other_requests"] == 0)
+            & (pods["device_requests"] == 0).all(1))
+    matches = [[] for _ in range(len(pods))]
+    for p in np.flatnonzero(elig & (rng.random(len(pods)) < 0.5)):
+        pods["reservation_matched"][p] = abi.RSV_MATCHED
+        matches[p] = np.flatnonzero(grp == rng.integers(0, 10)).tolist()
+    assert ((pods["reservation_matched"] == abi.RSV_MATCHED) & (pods["numa_topology_policy"] != 0)).sum() >= 10
+    c1, s1 = ev.schedule(pods, synth.T0, matches=matches)
+    c0, s0 = o.schedule(pods, synth.T0, matches=matches)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5].ravel().tolist()
+    assert np.array_equal(s1, s0)
+    assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
+    assert np.array_equal(ev.last_cpusets, o.last_cpusets)
+    _resv_equal(ev, o)
+    a1, a0 = ev.last_allocations(), o.last_allocations()
+    assert np.array_equal(a1["reservation"], a0["reservation"])
+    pol = (pods["numa_topology_policy"] != 0) & (a1["reservation"] > 0)
+    assert pol.sum() >= 2  # pods with their own NUMA policy went into reservations
+    assert ev.check_records(synth.T0) == 0
+    ev.close()
+
+
 def test_matched_reservations_weight_one(gpu):
     """weight_reservation 1: the Reservation score mixes with the other plugins' totals instead of dominating;
     every matched pod matches all 40 reservations (several per node compete in NominateReservation)."""
