@@ -810,8 +810,9 @@ int ke_reservations_get(ke_ctx* ctx, int32_t n, ke_reservation* out);
                              unmatched restore), no Reservation Filter / Score / Reserve; lists none.
                              KE_ERR_UNSUPPORTED outside ke_schedule and where it would read resources a
                              reservation holds (ke_reservation_alloc): a DeviceShare pod beside held devices, a
-                             pod binding CPUs / with a NUMA policy beside held NUMA resources or CPUs, any pod
-                             while those sit on a NUMA-policy node                                             */
+                             pod with a NUMA policy beside held NUMA resources or CPUs, any pod while those sit
+                             on a NUMA-policy node.  A CPU-binding pod allocates with the held CPUs preferred
+                             (tryAllocateIgnoreReservation)                                                     */
 /* For each pod of the next ke_schedule call, the reservations (indices into the loaded set) it matches,
  * ids[offsets[p] .. offsets[p+1]) (with a reservation name in the affinity: only that one).  Only KE_RSV_MATCHED /
  * KE_RSV_AFFINITY pods may list any; the call consumes the lists.

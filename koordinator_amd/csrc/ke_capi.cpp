@@ -850,18 +850,30 @@ static int schedule_sync(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_
            (!moff.empty() && moff[(size_t)p + 1] > moff[(size_t)p]);
   };
   // A run of KE_RSV_IGNORED pods is a segment of its own: its rows carry every reservation's matched restore.
+  // An ignored pod that may bind CPUs beside CPU-holding reservations is alone too (its trials read the state).
   auto ignored = [&](int32_t p) { return pods[p].reservation_matched == KE_RSV_IGNORED; };
+  auto ign_views = [&](int32_t p) { return ignored(p) && resv_ignore_needs_views(c, pods[p], c.staged[(size_t)p].flags); };
+  auto alone = [&](int32_t p) { return matched(p) || ign_views(p); };
   std::vector<int32_t> assumed((size_t)n_pods, 0);
   for (int32_t s0 = 0; s0 < n_pods || (n_pods == 0 && s0 == 0);) {
     int32_t s1 = s0;
     const bool ign = s0 < n_pods && ignored(s0);
-    while (s1 < n_pods && !barrier(s1) && !matched(s1) && ignored(s1) == ign) s1++;
+    while (s1 < n_pods && !barrier(s1) && !alone(s1) && ignored(s1) == ign) s1++;
     // a barrier pod ends its segment; a matched one is alone
-    if (s1 < n_pods && (s1 == s0 || (!matched(s1) && barrier(s1) && ignored(s1) == ign))) s1++;
+    if (s1 < n_pods && (s1 == s0 || (!alone(s1) && barrier(s1) && ignored(s1) == ign))) s1++;
     const int32_t len = s1 - s0;
     const bool rsv = len == 1 && matched(s0);
     mirror_join(c);  // (the previous segment's host mirror thread: this one reads the node state)
     if (ign) resv_ignore_begin(c);
+    if (ign && len == 1 && ign_views(s0)) {  // its trials on the current state, as the matched pods' below
+      flush_mirror(c);
+      resv_ignore_views(c, pods[s0]);
+      if (!c.rsv_views.empty()) {
+        rc = device_rsv_views(&c, pods[s0], now_ns, c.rsv_views, c.rsv_view_out);
+        if (rc) return resv_ignore_end(c), rc;
+      }
+      resv_ignore_ovr(c);
+    }
     if (rsv) {
       const int32_t* ids = mids.data() + moff[(size_t)s0];
       const int32_t n_ids = moff[(size_t)s0 + 1] - moff[(size_t)s0];

@@ -784,10 +784,11 @@ int resv_check(const Context& c, const int32_t* ids, int32_t n_ids) {
 // an affinity, plugin.go:350-353), PreScore / Score skip it (scoring.go:48-50) and Reserve assumes it into no
 // reservation (plugin.go:755-761).  NodeNUMAResource / DeviceShare allocate it from the node and the ignored
 // reservations' unallocated remainder (tryAllocateIgnoreReservation, nodenumaresource/reservation.go:437-490,
-// deviceshare/reservation.go:290-310): that remainder of held resources is not restated, so the pod is refused
-// where it would read it -- a DeviceShare pod while a reservation holds devices; a pod that may bind CPUs or has
-// its own NUMA policy while one holds NUMA resources or CPUs; any pod while one of those sits on a node with a
-// NUMA topology policy (its hints read the zones).  Elsewhere the held state is not read and the rows are exact.
+// deviceshare/reservation.go:290-310): for a pod binding CPUs on a node without a NUMA policy that remainder is
+// the held CPUs, tried as the preferred CPUs of one allocation (resv_ignore_views); the held NUMA amounts and
+// devices are not restated, so the pod is refused where it would read them -- a DeviceShare pod while a
+// reservation holds devices; a pod with its own NUMA policy while one holds NUMA resources or CPUs; any pod while
+// one of those sits on a node with a NUMA topology policy (its hints read the zones).
 int resv_ignore_check(const Context& c, const ke_pod& pod, uint32_t pod_flags) {
   bool dev = false, numa_cpu = false, on_policy_node = false;
   for (size_t i = 0; i < c.resv_holds.size(); i++) {
@@ -798,9 +799,8 @@ int resv_ignore_check(const Context& c, const ke_pod& pod, uint32_t pod_flags) {
       on_policy_node = on_policy_node || c.nodes[(size_t)c.resv[i].node].node.numa_topology_policy != KE_NUMA_POLICY_NONE;
     }
   }
-  const bool binds = (pod_flags & PF_CPUSET) || (c.n_bind_nodes > 0 && pod.requests[KE_RES_CPU] > 0);
-  if ((dev && (pod_flags & (PF_DS | PF_DS_HINT))) ||
-      (numa_cpu && (binds || pod.numa_topology_policy != KE_NUMA_POLICY_NONE)) || on_policy_node)
+  if ((dev && (pod_flags & (PF_DS | PF_DS_HINT))) || (numa_cpu && pod.numa_topology_policy != KE_NUMA_POLICY_NONE) ||
+      on_policy_node)
     return fail(KE_ERR_UNSUPPORTED, "a reservation-ignored pod reading resources a reservation holds "
                                     "(tryAllocateIgnoreReservation's remainder)");
   return KE_OK;
@@ -818,8 +818,69 @@ void resv_ignore_begin(Context& c) {
 }
 
 void resv_ignore_end(Context& c) {
+  for (const RsvOvr& o : c.rsv_ovr) c.nodes[(size_t)o.node].rsv_ovr = false;
+  c.rsv_ovr.clear();
+  c.rsv_views.clear();
+  c.rsv_view_resv.clear();
+  c.rsv_view_out.clear();
   for (size_t node = 0; node < c.resv_by_node.size(); node++)
     if (!c.resv_by_node[node].empty()) resv_node_restore(c, (int32_t)node);
+}
+
+static bool resv_holds_cpu(const Context& c, int32_t i);
+static bool pod_binds_on(const DevPod& dp, const NodeState& ns);
+
+bool resv_ignore_needs_views(const Context& c, const ke_pod& pod, uint32_t pod_flags) {
+  if (!((pod_flags & PF_CPUSET) || (c.n_bind_nodes > 0 && pod.requests[KE_RES_CPU] > 0))) return false;
+  for (size_t i = 0; i < c.resv_holds.size(); i++)
+    if (c.resv_holds[i] & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)) return true;
+  return false;
+}
+
+// tryAllocateIgnoreReservation for a reservation-ignored pod binding CPUs (nodenumaresource/reservation.go:437-490):
+// on every node without a NUMA policy whose usable reservations hold NUMA resources or CPUs (RestoreReservation's
+// matched set), one allocation with reservedCPUsFromIgnored = their allocatable CPUs (mergedMatchedAllocatedCPUs,
+// the remainedCPUs inside them) preferred and no required resources
+void resv_ignore_views(Context& c, const ke_pod& pod) {
+  c.rsv_views.clear();
+  c.rsv_view_resv.clear();
+  c.rsv_view_out.clear();
+  if (c.resv_alloc.empty()) return;
+  const DevPod dp = make_dev_pod(c.cfg, pod, pod_hints(c, pod), &c.tmpl);
+  for (size_t node = 0; node < c.resv_by_node.size(); node++) {
+    if (c.resv_by_node[node].empty()) continue;
+    const NodeState& ns = c.nodes[node];
+    if (ns.node.numa_topology_policy != KE_NUMA_POLICY_NONE || !pod_binds_on(dp, ns) || !cpus_valid(ns)) continue;
+    RsvView v{};
+    bool any = false;
+    for (int32_t i : c.resv_by_node[node])
+      if (resv_usable(c.resv[(size_t)i]) && resv_holds_cpu(c, i)) {
+        any = true;
+        for (int w = 0; w < 4; w++) v.pref[w] |= c.resv_alloc[(size_t)i].cpuset[w];
+      }
+    if (!any) continue;
+    v.node = (int32_t)node;
+    c.rsv_views.push_back(v);
+    c.rsv_view_resv.push_back(-1);
+  }
+}
+
+// the trials' outcome as the Filter's and Reserve's decisions (a failed allocation fails both: the status is
+// returned, plugin.go:384-387 and :554-558)
+void resv_ignore_ovr(Context& c) {
+  c.rsv_ovr.clear();
+  for (size_t q = 0; q < c.rsv_views.size(); q++) {
+    RsvOvr o{};
+    o.node = c.rsv_views[q].node;
+    const bool ok = c.rsv_view_out.size() > q && c.rsv_view_out[q].ok;
+    o.filter = o.reserve = (int8_t)(ok ? 1 : 2);
+    if (ok)
+      for (int w = 0; w < 4; w++) o.cpus[w] = c.rsv_view_out[q].cpus[w];
+    c.rsv_ovr.push_back(o);
+    NodeState& ns = c.nodes[(size_t)o.node];
+    ns.rsv_ovr = true;
+    ns.dirty = true;
+  }
 }
 
 // requestCPUBind of the pod on the node (util.go:121-138): its own cpuset state, else a node CPU bind policy

@@ -339,6 +339,12 @@ int resv_check(const Context& c, const int32_t* ids, int32_t n_ids);
 int resv_ignore_check(const Context& c, const ke_pod& pod, uint32_t pod_flags);
 void resv_ignore_begin(Context& c);
 void resv_ignore_end(Context& c);
+// a reservation-ignored pod that may bind CPUs beside reservations holding NUMA resources / CPUs: a segment of its
+// own, its allocate-ignoring-reservation trials (resv_ignore_views -> device_rsv_views) turned into the Filter /
+// Reserve decisions of those nodes (resv_ignore_ovr)
+bool resv_ignore_needs_views(const Context& c, const ke_pod& pod, uint32_t pod_flags);
+void resv_ignore_views(Context& c, const ke_pod& pod);
+void resv_ignore_ovr(Context& c);
 void resv_finish(Context& c, int32_t chosen_local, const ke_pod& pod, int32_t* assumed, const uint64_t* cpuset = nullptr,
                  const int64_t* numa = nullptr, uint64_t dev_minors = 0);
 void resv_forget(Context& c, int32_t idx, const ke_pod& pod, const ke_pod_allocation* a = nullptr);

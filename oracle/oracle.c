@@ -111,6 +111,7 @@ struct or_cluster {
   ke_reservation* resv;
   ke_reservation_alloc* ralloc; /* the reservations' NUMA / cpuset / device holdings (NULL: none) */
   const char* resv_m;           /* the matched flags of the pod being evaluated (or_resv_begin), NULL = none */
+  int ignored;                  /* the pod being evaluated / reserved is reservation-ignored (or_numa_ignored) */
   uint8_t* rcpu;                /* [reservation][cpu] owner counts (or_owner_update), NULL until first needed */
   int32_t n_resv;
   int32_t* moff;
@@ -717,6 +718,30 @@ static int cpuset_allocate_pref(const or_cluster* c, const or_node* n, const ke_
 }
 
 static int or_holds_of_idx(const or_cluster* c, int32_t r);
+static int or_resv_usable(const ke_reservation* r);
+
+/* tryAllocateIgnoreReservation for a reservation-ignored binding pod on a node without a NUMA policy
+ * (nodenumaresource/reservation.go:437-490; the hint is empty, so the held NUMA amounts do not enter): over
+ * RestoreReservation's matched set -- every usable reservation on the node whose reserve pod holds NUMA resources or
+ * a cpuset -- one Allocate with reservedCPUsFromIgnored (their allocatable CPUs, the remainedCPUs inside them)
+ * preferred and no required resources; its status is the Filter's (plugin.go:384-387) and Reserve's: 1 and the
+ * cpuset, or -1.  An empty set gives 0 (tryAllocateFromNode). */
+static int or_numa_ignored(const or_cluster* c, const ke_pod* pod, int32_t node, uint64_t* out) {
+  const or_node* n = &c->nodes[node];
+  uint64_t pref[ACC_WORDS] = {0}, got[ACC_WORDS];
+  int any = 0;
+  for (int32_t r = 0; c->ralloc && r < c->n_resv; r++) {
+    if (c->resv[r].node != node || !or_resv_usable(&c->resv[r]) ||
+        !(or_holds_of_idx(c, r) & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)))
+      continue;
+    any = 1;
+    for (int w = 0; w < ACC_WORDS; w++) pref[w] |= c->ralloc[r].cpuset[w];
+  }
+  if (!any) return 0;
+  if (cpuset_allocate_pref(c, n, pod, pref, got) != 0) return -1;
+  memcpy(out, got, sizeof got);
+  return 1;
+}
 
 /* NodeNUMAResource's allocate-from-reservation for a binding pod on a node without a NUMA policy
  * (tryAllocateFromReservation, nodenumaresource/reservation.go:270-424; the hint is empty, so Allocate is
@@ -957,7 +982,8 @@ static int numa_filter_aff(const or_cluster* c, const ke_pod* pod, int32_t node,
     if (required != KE_CPU_BIND_UNSET && policy == KE_NUMA_POLICY_NONE) { /* trial Allocate */
       uint64_t cs[ACC_WORDS];
       /* from the matched reservations first (plugin.go:381-390), then the node (tryAllocateFromNode) */
-      const int fr = or_numa_from_rsv(c, pod, node, -1, pod->reservation_matched == KE_RSV_AFFINITY, cs);
+      const int fr = c->ignored ? or_numa_ignored(c, pod, node, cs)
+                                : or_numa_from_rsv(c, pod, node, -1, pod->reservation_matched == KE_RSV_AFFINITY, cs);
       if (fr < 0) {
         *reason = KE_REASON_RSV_INSUFFICIENT_CPUS;
         return KE_CODE_UNSCHEDULABLE;
@@ -3480,6 +3506,11 @@ static int or_reserve_plan(const or_cluster* c, const ke_pod* pod, int32_t node,
   numa_cs_build(c, n, pod, &cs);
   rp->excl = cs.excl;
   if (cs.rcb && !cs.valid) return -1;
+  if (c->ignored && cs.rcb && policy == KE_NUMA_POLICY_NONE) {  /* allocateWithNominatedReservation, ignored */
+    const int fr = or_numa_ignored(c, pod, node, rp->cpus);
+    if (fr < 0) return -1;
+    if (fr > 0) return 0;
+  }
   if (c->resv_m && cs.rcb && policy == KE_NUMA_POLICY_NONE) {
     const int required = pod->reservation_matched == KE_RSV_AFFINITY;
     if (nom_r < 0 && required) return -1;
@@ -4275,9 +4306,9 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
     const int32_t n_ids = c->moff && c->m_pods == n_pods ? c->moff[p + 1] - c->moff[p] : 0;
     if (pods[p].reservation_matched != KE_RSV_MATCHED && pods[p].reservation_matched != KE_RSV_AFFINITY) {
       if (n_ids) return KE_ERR_INVALID;
-      /* a reservation-ignored pod reading held resources: tryAllocateIgnoreReservation's remainder is not restated
-       * (a DeviceShare pod and held devices; a pod binding CPUs or with a NUMA policy and held NUMA resources /
-       * CPUs; held NUMA resources / CPUs on a NUMA-policy node) */
+      /* a reservation-ignored pod reading held NUMA amounts / devices: tryAllocateIgnoreReservation's remainder of
+       * those is not restated (a DeviceShare pod and held devices; a pod with a NUMA policy and held NUMA
+       * resources / CPUs; held NUMA resources / CPUs on a NUMA-policy node) */
       if (pods[p].reservation_matched == KE_RSV_IGNORED && c->ralloc) {
         int dev = 0, numa_cpu = 0, on_policy = 0;
         for (int32_t r = 0; r < c->n_resv; r++) {
@@ -4293,7 +4324,8 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
         cpuset_state st;
         cpuset_prefilter(c, &pods[p], &st);
         const int binds = st.rcb || st.invalid || (node_bind && pods[p].requests[KE_RES_CPU] > 0);
-        if ((dev && !d.skip) || (numa_cpu && (binds || pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE)) || on_policy)
+        (void)binds; /* a binding pod allocates from the held CPUs (or_numa_ignored) */
+        if ((dev && !d.skip) || (numa_cpu && pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE) || on_policy)
           return KE_ERR_UNSUPPORTED;
       }
       continue;
@@ -4370,6 +4402,7 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
       char* all = (char*)malloc((size_t)(c->n_resv > 0 ? c->n_resv : 1));
       memset(all, 1, (size_t)(c->n_resv > 0 ? c->n_resv : 1));
       or_restore(c, all, 1);
+      c->ignored = 1;
       b = eval_pod(c, &pods[p], now, o, &bs16);
       bs = bs16;
       or_restore(c, NULL, 0);
@@ -4394,6 +4427,7 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
     }
     const int plan = b >= 0 ? or_reserve_plan(c, &pods[p], b, &rp, mflags ? nom[b] : -1) : 0;
     c->resv_m = NULL;
+    c->ignored = 0;
     free(mflags);
     if (b >= 0 && (plan != 0 || !ds_reserve_feasible(c, &pods[p], b, da))) {
       /* Reserve failed (Unreserve undoes the others): not placed */
