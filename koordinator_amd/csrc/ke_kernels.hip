@@ -6222,6 +6222,7 @@ struct DeviceState {
   PinnedVec<int64_t> h_refresh;   // device_refresh's row staging (every table's rows + indices, one sync)
   PinnedVec<uint8_t> h_rsv;       // a matched pod's RsvPair / RsvOvr uploads
   PinnedVec<int32_t> h_rsv_out;   // k_rsv_pick's result words, read back by the call's own copies
+  PinnedVec<int32_t> h_cut;       // a DeviceShare batch's cut word (async read-back, the next batch enqueued behind)
   std::vector<DevPodHint> host_ph;  // its hinted pods' records (the async upload reads them)
   // NUMA topology
   bool numa_alloc = false;         // soa.nf / soa.nm allocated
@@ -7237,6 +7238,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   // Batch b's eval + candidate lists on stream `es`.  pipe: stale top-(k_j + KMAX) lists into the run's
   // stale buffer (k_fixup makes them exact); else the exact top-k_j lists straight into d_cand.
   bool rerun = false;  // the current serial batch is the remainder of a DeviceShare batch that stopped early
+  int pre_b = -1;      // a serial batch whose eval + select is already enqueued (behind a DeviceShare cut check)
   // dwait (pipelined, stale lists): the eval first waits for that done flag -- in k_eval_plain itself, else a
   // k_handoff ahead of it; rpub: the select publishes the lists to the running Reserve kernel itself when it
   // can (split or one-workgroup select, unsharded) -- *published tells the caller
@@ -7475,7 +7477,8 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
     const int bp = batches[b].pods;
     const bool ds = batches[b].ds, cpu = batches[b].cpu;
     const int32_t* bbase = d_bases + b;
-    rc = eval_select(b, false, d->stream);
+    if (pre_b != b) rc = eval_select(b, false, d->stream);
+    pre_b = -1;
     if (rc) return rc;
     if (bp == 1) {  // one pod: the single-node Reserve (cpuset accumulator when it binds)
       int elo = 0, ehi = 0;  // nodes whose affinities this batch's eval stored in d_aff (binding batches)
@@ -7500,10 +7503,22 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
                          d->d_stamps, d->d_stamps + (n_pods + 2), b, d->d_devalloc, d->d_numaalloc, d->d_chg, N,
                          (int)run_sorted(b, b + 1));
       if (batches[b].cut) {  // a DeviceShare batch may stop early: re-run its remaining pods as batch b
-        int32_t cut = -1;
-        HIP_OK(hipMemcpyAsync(&cut, d->d_dsmax + DSB_CUT, sizeof(int32_t), hipMemcpyDeviceToHost, d->stream));
+        if (!d->h_cut.resize(1)) return fail(KE_ERR_DEVICE, "hipHostMalloc of the cut word");
+        HIP_OK(hipMemcpyAsync(d->h_cut.data(), d->d_dsmax + DSB_CUT, sizeof(int32_t), hipMemcpyDeviceToHost, d->stream));
+        // the next serial batch's eval + select go in behind the read-back, so the device keeps working while the
+        // host waits for the cut (without one they stand; with one the re-run batch overwrites what they wrote)
+        if (b + 1 < n_batches && run_end[b + 1] == 0) {
+          const bool keep = rerun;
+          rerun = false;
+          rc = eval_select(b + 1, false, d->stream);
+          rerun = keep;
+          if (rc) return rc;
+          pre_b = b + 1;
+        }
         HIP_OK(hipStreamSynchronize(d->stream));
+        const int32_t cut = d->h_cut[0];
         if (cut >= 0) {
+          pre_b = -1;
           if (cut <= bases[b] || cut >= bases[b] + bp) return fail(KE_ERR_DEVICE, "DeviceShare batch cut out of range");
           batches[b].pods = bases[b] + bp - cut;
           bases[b] = cut;
