@@ -731,18 +731,33 @@ int load_reservations(Context& c, int32_t n, const ke_reservation* rs, const ke_
 // The pod-count check of fitsNode (plugin.go:450-453) reads len(NodeInfo.Pods) of the snapshot NodeInfo, which
 // the BeforePreFilter restore already left without the matched reserve pods (restoreMatchedReservation ->
 // RemovePod, transformer.go:440), and subtracts len(matchedOrIgnored) once more: `pods_restored` is the former.
-static bool resv_nominable(const ke_reservation& r, const ke_pod& pod, const int64_t* alloc, const int64_t* pod_requested,
+static bool resv_nominable(const ke_reservation& r, const ke_pod& pod, const NodeState& ns, const int64_t* pod_requested,
                            const int64_t* all_allocated, bool affinity, int64_t pods_restored, int64_t n_matched,
                            int64_t allowed_pods) {
   bool shared = false;
   for (int k = 0; k < KE_NRES; k++) shared = shared || (r.allocatable[k] != 0 && pod.requests[k] != 0);
   if (!shared && !affinity) return false;
   bool node_fits = pods_restored - n_matched + 1 <= allowed_pods;
-  if (pod.requests[KE_RES_CPU] != 0 || pod.requests[KE_RES_MEMORY] != 0)
+  // the pod's other resources (ephemeral storage, scalars: its ke_pod.xres) -- a reservation holds none of them
+  // (KE_RSV_OTHER_ALLOCATABLE is refused), so their rRemained / allRAllocated are 0 and podRequested is the node's
+  bool other = false;
+  for (int e = 0; e < pod.n_xres; e++)
+    other = other || (pod.xres_id[e] != KE_XRES_CPU && pod.xres_id[e] != KE_XRES_MEMORY && pod.xres_value[e] != 0);
+  if (pod.requests[KE_RES_CPU] != 0 || pod.requests[KE_RES_MEMORY] != 0 || other) {  // else pods only (:455-460)
+    const int64_t* alloc = ns.node.allocatable;
     for (int k = 0; k < KE_NRES; k++) {
       const int64_t remained = r.allocatable[k] > r.allocated[k] ? r.allocatable[k] - r.allocated[k] : 0;  // GetAvailable
       if (pod.requests[k] > alloc[k] - (pod_requested[k] - remained - all_allocated[k])) node_fits = false;
     }
+    for (int e = 0; e < pod.n_xres; e++) {  // (plugin.go:487-495)
+      const int32_t id = pod.xres_id[e];
+      if (id == KE_XRES_CPU || id == KE_XRES_MEMORY || pod.xres_value[e] == 0) continue;
+      int64_t a = 0, q = 0;
+      for (const ke_node_resource& x : ns.xres)
+        if (x.id == id) a = x.allocatable, q = x.requested;
+      if (pod.xres_value[e] > a - q) node_fits = false;
+    }
+  }
   bool resv_fits = node_fits;
   if (r.allocate_policy == KE_RSV_POLICY_RESTRICTED) {
     resv_fits = true;
@@ -984,7 +999,7 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
     bool fits_one = false;  // the Reservation Filter with a reservation affinity (plugin.go:316-318, 351-442): a
                             // node without matched reservations fails, one with them passes when one of them fits
     for (int32_t i : mine)
-      if (resv_nominable(c.resv[(size_t)i], pod, ns.node.allocatable, pod_requested, all_alloc, affinity, pods_restored,
+      if (resv_nominable(c.resv[(size_t)i], pod, ns, pod_requested, all_alloc, affinity, pods_restored,
                          (int64_t)mine.size(), ns.node.allowed_pods)) {
         fits_one = true;
         if (numa_nominable(i)) ok.push_back(i);

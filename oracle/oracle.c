@@ -3372,12 +3372,24 @@ static int or_resv_nominable(const or_cluster* c, const ke_reservation* r, const
    * moves only Requested) */
   const int64_t pods_restored = (int64_t)c->nodes[node].node.pod_count - n_matched;
   int node_fits = pods_restored - n_matched + 1 <= (int64_t)c->nodes[node].node.allowed_pods;
-  if (!(pod->requests[KE_RES_CPU] == 0 && pod->requests[KE_RES_MEMORY] == 0)) {
+  /* the pod's ephemeral storage / scalar resources (ke_pod.xres): a reservation holds none of them, so rRemained and
+   * allRAllocated are 0 there and podRequested is the node's (plugin.go:487-495); without any request only the pod
+   * count is checked (:455-460) */
+  int other = 0;
+  for (int32_t e = 0; e < pod->n_xres; e++)
+    other |= pod->xres_id[e] != KE_XRES_CPU && pod->xres_id[e] != KE_XRES_MEMORY && pod->xres_value[e] != 0;
+  if (!(pod->requests[KE_RES_CPU] == 0 && pod->requests[KE_RES_MEMORY] == 0) || other) {
     for (int k = 0; k < KE_NRES; k++) {
       int64_t remained = r->allocatable[k] - r->allocated[k];
       if (remained < 0) remained = 0;
       const int64_t avail = c->nodes[node].node.allocatable[k] - (pod_requested[k] - remained - all_allocated[k]);
       if (pod->requests[k] > avail) node_fits = 0;
+    }
+    for (int32_t e = 0; e < pod->n_xres; e++) {
+      const int32_t id = pod->xres_id[e];
+      if (id == KE_XRES_CPU || id == KE_XRES_MEMORY || pod->xres_value[e] == 0) continue;
+      const ke_node_resource* x = node_xres(&c->nodes[node], id);
+      if (pod->xres_value[e] > (x ? x->allocatable - x->requested : 0)) node_fits = 0;
     }
   }
   int resv_fits = node_fits;

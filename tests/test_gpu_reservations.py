@@ -292,3 +292,32 @@ def test_reservation_affinity_schedule_parity(gpu):
     assert (a1["reservation"][placed_aff] > 0).all()  # an affinity pod is placed only into a reservation
     assert (c1[aff & np.array([len(m) == 0 for m in matches])] == -1).all()
     assert ev.check_records(synth.T0) == 0
+
+
+def test_fits_node_other_resources_on_the_device(gpu):
+    """The CPU test's single node (test_reservations.py::test_fits_node_checks_the_pods_other_resources) on the
+    device: a matched pod whose scalar does not fit is not nominated, with it free it is -- as the oracle."""
+    cl = synth.make_cluster(1, synth.BASE_SEED + 1412)
+    cfg = synth.config(1)
+    tab = np.zeros(3, abi.NODE_RESOURCE_DTYPE)
+    tab["id"] = [abi.XRES_CPU, abi.XRES_MEMORY, 5]
+    tab["allocatable"] = [cl.nodes["allocatable"][0, 0], cl.nodes["allocatable"][0, 1], 4]
+    tab["requested"] = [cl.nodes["requested"][0, 0], cl.nodes["requested"][0, 1], 4]
+    r = abi.Reservation(node=0, available=1)
+    r.allocatable[0] = 2000
+    pods = synth.make_pods(1, synth.BASE_SEED + 1412)
+    pods["requests"][0, 0], pods["requests"][0, 1], pods["requests"][0, 2:] = 1000, 2**28, 0
+    pods["has_other_requests"], pods["device_requests"], pods["numa_topology_policy"] = 0, 0, 0
+    pods["n_xres"] = 1
+    pods["xres_id"][0, 0], pods["xres_value"][0, 0] = 5, 1
+    pods["reservation_matched"] = abi.RSV_MATCHED
+    for used, into in ((4, 0), (3, 1)):
+        tab["requested"][2] = used
+        ev = Evaluator(cfg)
+        synth.load_into(ev, cl)
+        ev.set_resources(0, tab)
+        ev.reservations_load([r])
+        c, s = ev.schedule(pods, synth.T0, matches=[[0]])
+        assert c.tolist() == [0] and ev.last_allocations()["reservation"].tolist() == [into]
+        assert (s[0] >= 5000) == bool(into)
+        ev.close()

@@ -385,3 +385,35 @@ def test_numa_reserve_from_reservation_golden(case):
     code, cpus = o.numa_reserve_from_rsv(pod, 0, [0], 0, case["affinity"])
     assert code == case["want_code"]
     assert np.array_equal(cpus, _cpus(case["want_cpus"]))
+
+
+def test_fits_node_checks_the_pods_other_resources():
+    """fitsNode (reservation/plugin.go:447-497) checks every resource the pod requests, its scalars and ephemeral
+    storage included (a reservation holds none of them: the node's free amount decides), and with no request at all
+    only the pod count (:455-460).  One node, one cpu reservation, NodeResourcesFit's Filter off: a matched pod whose
+    scalar (id 5) does not fit on the node is not nominated (no Reservation score, assumed into nothing); with the
+    scalar free it is."""
+    cl = synth.make_cluster(1, synth.BASE_SEED + 1412)  # (a node LoadAware admits the pod on)
+    cfg = synth.config(1)
+    tab = np.zeros(3, abi.NODE_RESOURCE_DTYPE)
+    tab["id"] = [abi.XRES_CPU, abi.XRES_MEMORY, 5]
+    tab["allocatable"] = [cl.nodes["allocatable"][0, 0], cl.nodes["allocatable"][0, 1], 4]
+    tab["requested"] = [cl.nodes["requested"][0, 0], cl.nodes["requested"][0, 1], 4]
+    r = abi.Reservation(node=0, available=1)
+    r.allocatable[0] = 2000
+    pods = synth.make_pods(1, synth.BASE_SEED + 1412)
+    pods["requests"][0, 0], pods["requests"][0, 1], pods["requests"][0, 2:] = 1000, 2**28, 0
+    pods["has_other_requests"], pods["device_requests"], pods["numa_topology_policy"] = 0, 0, 0
+    pods["n_xres"] = 1
+    pods["xres_id"][0, 0], pods["xres_value"][0, 0] = 5, 1
+    pods["reservation_matched"] = abi.RSV_MATCHED
+    for used, into in ((4, 0), (3, 1)):
+        tab["requested"][2] = used
+        o = Oracle(cfg, 1)
+        synth.load_into(o, cl)
+        o.set_resources(0, tab)
+        o.reservations_load([r])
+        c, s = o.schedule(pods, synth.T0, matches=[[0]])
+        assert c.tolist() == [0]
+        assert o.last_allocations()["reservation"].tolist() == [into]
+        assert (s[0] >= 5000) == bool(into)
