@@ -839,7 +839,7 @@ int ke_reservations_get(ke_ctx* ctx, int32_t n, ke_reservation* out);
  * the restored NodeInfo (ke_node.pod_count with the matched reserve pods removed) minus the node's matched
  * reservations, plus one, within ke_node.allowed_pods.
  * Refused (KE_ERR_UNSUPPORTED, by ke_schedule's argument checks before any pod of the call is scheduled): such a
- * pod with DeviceShare or scalar requests, one with a NUMA topology policy whose usable matched reservation holds
+ * pod with DeviceShare requests or resources outside KE_RES_* / xres (has_other_requests), one with a NUMA topology policy whose usable matched reservation holds
  * NUMA resources or a cpuset, a usable matched reservation holding NUMA resources or a cpuset on a node with a NUMA
  * topology policy, a sharded context; ke_eval of such a pod.  The lists
  * are consumed by the next ke_schedule call, a refused one included. */

@@ -164,11 +164,12 @@ static int check_matches(Context& c, const ke_pod* pods, int32_t n) {
     }
     if (!staged) return fail(KE_ERR_INVALID, "a KE_RSV_MATCHED / AFFINITY pod without ke_pod_reservations");
     const uint32_t f = c.staged[(size_t)p].flags;
+    // (batch / mid resources, KE_RES_BATCH_* / KE_RES_MID_*: a reservation holds only cpu / memory, so they enter
+    // the Reservation plugin as the pod's other resources of fitsNode, its ke_pod.xres, and nothing else)
     bool scalar = pods[p].has_other_requests || pods[p].has_unsupported_device_requests;
-    for (int r = KE_NRES; r < KE_RES_COUNT; r++) scalar = scalar || pods[p].requests[r] != 0;
     for (int r = 0; r < KE_PDR_COUNT; r++) scalar = scalar || pods[p].device_requests[r] != 0;
     if ((f & (PF_DS | PF_DS_HINT)) || scalar)
-      return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations with device or scalar requests");
+      return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations with device requests or unnamed resources");
     // a pod with its own NUMA policy takes hints on every node: a matched reservation holding NUMA resources or
     // CPUs would need them over its allocate-from-reservation trials (not restated); without such holdings its
     // matched restore moves only NodeInfo.Requested, which the hints do not read

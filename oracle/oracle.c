@@ -4348,8 +4348,7 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
     ds_pod d;
     ds_prepare_pod(c, &pods[p], &d);
     (void)node_bind;
-    int scalar = pods[p].has_other_requests || !d.skip;
-    for (int r = KE_NRES; r < KE_RES_COUNT; r++) scalar |= pods[p].requests[r] != 0;
+    int scalar = pods[p].has_other_requests || !d.skip; /* (batch / mid resources: fitsNode's xres only) */
     for (int r = 0; r < KE_PDR_COUNT; r++) scalar |= pods[p].device_requests[r] != 0;
     if (scalar) return KE_ERR_UNSUPPORTED;
     /* a pod with its own NUMA policy matching a reservation that holds NUMA resources / CPUs: its hints over the

@@ -321,3 +321,27 @@ def test_fits_node_other_resources_on_the_device(gpu):
         assert c.tolist() == [0] and ev.last_allocations()["reservation"].tolist() == [into]
         assert (s[0] >= 5000) == bool(into)
         ev.close()
+
+
+def test_matched_batch_pods_parity(gpu):
+    """KE_RSV_MATCHED pods requesting batch / mid resources (KE_RES_BATCH_* / MID_*, LoadAware's translated names):
+    a reservation holds only cpu / memory, so they reach the Reservation plugin as fitsNode's other resources and
+    nothing else -- placements, totals and reservation state bit-exact with the oracle."""
+    ev, o, pods, matches = _matched_setup(300, 1001, 300)
+    rng = np.random.default_rng(1002)
+    lists = [m for m in matches if m]
+    batch = np.flatnonzero((pods["requests"][:, 2:] != 0).any(1) & (pods["numa_topology_policy"] == 0)
+                           & (pods["has_other_requests"] == 0) & (pods["device_requests"] == 0).all(1)
+                           & (pods["reservation_matched"] == abi.RSV_NONE))
+    assert len(batch) >= 10
+    for p in batch[::2]:
+        pods["reservation_matched"][p] = abi.RSV_MATCHED
+        matches[p] = lists[int(rng.integers(len(lists)))]
+    c1, s1 = ev.schedule(pods, synth.T0, matches=matches)
+    c0, s0 = o.schedule(pods, synth.T0, matches=matches)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5].ravel().tolist()
+    assert np.array_equal(s1, s0)
+    _resv_equal(ev, o)
+    assert np.array_equal(ev.last_allocations()["reservation"], o.last_allocations()["reservation"])
+    assert ev.check_records(synth.T0) == 0
+    ev.close()

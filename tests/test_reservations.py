@@ -128,7 +128,7 @@ def test_matched_pod_checks():
         ev.schedule(pods, synth.T0)  # an affinity pod needs its (possibly empty) list staged
     assert e.value.code == abi.ERR_INVALID
     pods["reservation_matched"][1] = abi.RSV_MATCHED
-    pods["requests"][1][abi.RES_BATCH_CPU] = 1000  # a scalar request
+    pods["has_other_requests"][1] = 1  # a resource outside the ABI's names
     with pytest.raises(KoordEvalError) as e:
         ev.schedule(pods, synth.T0, matches=[[], [0]])
     assert e.value.code == abi.ERR_UNSUPPORTED
