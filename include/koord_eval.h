@@ -841,7 +841,7 @@ int ke_reservations_get(ke_ctx* ctx, int32_t n, ke_reservation* out);
  * Refused (KE_ERR_UNSUPPORTED, by ke_schedule's argument checks before any pod of the call is scheduled): such a
  * pod with DeviceShare requests or resources outside KE_RES_* / xres (has_other_requests), one with a NUMA topology policy whose usable matched reservation holds
  * NUMA resources or a cpuset, a usable matched reservation holding NUMA resources or a cpuset on a node with a NUMA
- * topology policy, a sharded context; ke_eval of such a pod.  The lists
+ * topology policy; ke_eval of such a pod.  (Node-sharded contexts pick over every rank's pairs.)  The lists
  * are consumed by the next ke_schedule call, a refused one included. */
 int ke_pod_reservations(ke_ctx* ctx, int32_t n_pods, const int32_t* offsets, const int32_t* ids);
 /* NodeInfo.Requested / NonZeroRequested (MilliCPU, Memory) of `node` as the plugins see it for a pod that

@@ -181,7 +181,6 @@ static int check_matches(Context& c, const ke_pod* pods, int32_t n) {
           return fail(KE_ERR_UNSUPPORTED, "a pod with a NUMA topology policy matching a reservation that holds NUMA "
                                           "resources or CPUs");
       }
-    if (c.dev && device_sharded(&c)) return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations in a sharded context");
     const int rc = resv_check(c, c.match_ids.data() + c.match_off[(size_t)p], cnt);
     if (rc) return rc;
   }

@@ -3358,6 +3358,86 @@ __global__ __launch_bounds__(64) void k_rsv_pick(const uint16_t* __restrict__ sc
   }
 }
 
+// k_rsv_pick across node shards (the pod's reservation nodes may live on any rank; every rank replays the same
+// Reserve, so every rank needs the same winner): the same steps in stages over the pairs of this rank's node range
+// [lo, hi) (loopback: every node), each stage's word made global by an all-reduce between the launches --
+//   0: the smallest order != 0 of a feasible pair (MIN)        1: the smallest such node with it (MIN)
+//   2: mx over the feasible pairs, preferredNode at 1000 (MAX)  3: the best 64-bit key against the merged lists' top
+//   4: the winner's total and n from the rank that owns it (MAX) 5: cand[0] and the result words, as k_rsv_pick.
+struct RsvPickSt {
+  int64_t order;
+  int32_t node, mx;
+  uint64_t best;
+  int32_t wt, nw;
+};
+template <int S>
+__global__ __launch_bounds__(64) void k_rsv_stage(const uint16_t* __restrict__ scores, const RsvPair* __restrict__ pr,
+                                                  int K, int lo, int hi, int64_t w, int affinity,
+                                                  uint32_t* __restrict__ cand, RsvPickSt* __restrict__ st,
+                                                  int32_t* __restrict__ out) {
+  const int l = (int)threadIdx.x;
+  auto mine = [&](const RsvPair& q) { return q.node >= lo && q.node < hi && scores[q.node] != 0 && q.allowed != 0; };
+  const int32_t pref = S >= 2 ? (st->order == INT64_MAX ? -1 : st->node) : -1;
+  if constexpr (S == 0) {
+    int64_t bo = INT64_MAX;
+    for (int i = l; i < K; i += 64)
+      if (pr[i].order != 0 && mine(pr[i])) bo = min(bo, pr[i].order);
+    for (int m = 32; m; m >>= 1) bo = min(bo, (int64_t)__shfl_xor(bo, m));
+    if (l == 0) st->order = bo;
+  } else if constexpr (S == 1) {
+    int32_t bn = INT32_MAX;
+    for (int i = l; i < K; i += 64)
+      if (st->order != INT64_MAX && pr[i].order == st->order && mine(pr[i])) bn = min(bn, pr[i].node);
+    for (int m = 32; m; m >>= 1) bn = min(bn, __shfl_xor(bn, m));
+    if (l == 0) st->node = bn;
+  } else if constexpr (S == 2) {
+    int32_t mx = 0;
+    for (int i = l; i < K; i += 64)
+      if (mine(pr[i])) mx = max(mx, pr[i].node == pref ? 1000 : (int32_t)pr[i].raw);
+    for (int m = 32; m; m >>= 1) mx = max(mx, __shfl_xor(mx, m));
+    if (l == 0) st->mx = mx;
+  } else if constexpr (S == 3) {
+    const int32_t mx = st->mx;
+    uint64_t best = affinity ? 0u : cand[0];  // the merged lists' top: (total + 1) << KEY_IDX_BITS | (mask - node)
+    if (mx > 0 || affinity)
+      for (int i = l; i < K; i += 64) {
+        const RsvPair q = pr[i];
+        if (!mine(q)) continue;
+        const int64_t n = mx > 0 ? 100 * (int64_t)(q.node == pref ? 1000 : q.raw) / mx : 0;
+        const uint64_t key = ((uint64_t)(scores[q.node] + w * n) << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)q.node);
+        best = key > best ? key : best;
+      }
+    for (int m = 32; m; m >>= 1) {
+      const uint64_t o = __shfl_xor(best, m);
+      best = o > best ? o : best;
+    }
+    if (l == 0) st->best = best;
+  } else if constexpr (S == 4) {
+    const uint64_t best = st->best;
+    const int32_t win = best ? (int32_t)(KEY_IDX_MASK - (uint32_t)(best & KEY_IDX_MASK)) : -1;
+    int32_t nw = 0;
+    if (win >= 0 && st->mx > 0)
+      for (int i = l; i < K; i += 64)
+        if (pr[i].node == win && win >= lo && win < hi)
+          nw = (int32_t)(100 * (int64_t)(pr[i].node == pref ? 1000 : pr[i].raw) / st->mx);
+    for (int m = 32; m; m >>= 1) nw = max(nw, __shfl_xor(nw, m));
+    if (l == 0) {
+      st->wt = win >= lo && win < hi ? (int32_t)scores[win] : 0;
+      st->nw = nw;
+    }
+  } else {
+    if (l == 0) {
+      const uint64_t best = st->best;
+      const int32_t win = best ? (int32_t)(KEY_IDX_MASK - (uint32_t)(best & KEY_IDX_MASK)) : -1;
+      cand[0] = win >= 0 ? ((uint32_t)st->wt << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)win) : 0u;
+      out[0] = win;
+      out[1] = st->nw;
+      out[2] = st->mx;
+      out[3] = pref;
+    }
+  }
+}
+
 // The deferred BestEffort pairs of an eval launch: one wavefront per pair computes mergeFilteredHints
 // over the full provider lists (numa_best_effort_fallback's result), then lane 0 evaluates the pair
 // with it.  A DeviceShare pod's pair is deferred only on a node without a device cache (DeviceShare has
@@ -6305,6 +6385,7 @@ struct DeviceState {
   RsvOvr* d_rovr = nullptr;         // the segment's allocate-from-reservation decisions (SoA::rovr)
   int64_t rovr_cap = 0;
   int32_t* d_rsv_out = nullptr;     // [4]
+  RsvPickSt* d_rsv_st = nullptr;    // k_rsv_stage's words (node-sharded contexts)
 };
 
 // Contiguous node range of shard `rank`: 512-aligned chunks (k_select's 16-B loads stay aligned).
@@ -6397,6 +6478,7 @@ int device_create(Context* ctx) {
   HIP_OK(hipMalloc(&d->d_aff, d->capacity));
   HIP_OK(hipMalloc(&d->d_split, sizeof(uint32_t) * GATH_WORDS_MAX * MAX_WORLD));
   HIP_OK(hipMalloc(&d->d_rsv_out, sizeof(int32_t) * 4));
+  HIP_OK(hipMalloc(&d->d_rsv_st, sizeof(RsvPickSt)));
   HIP_OK(hipStreamSynchronize(d->stream));
   return KE_OK;
 }
@@ -6451,7 +6533,7 @@ void device_destroy(Context* ctx) {
                   d->d_numaalloc, d->d_numarows, d->d_defer, d->d_defer_cnt, d->soa.cs, d->soa.cpu,
                   d->d_cpurows, d->d_cpusets, d->d_aff, d->soa.qt, d->soa.qm, d->d_sched, d->d_stale,
                   d->d_stale_cnt, d->d_pre, d->d_trows, d->d_tcnt, d->d_parts_done, d->d_scores2, d->d_split2, d->d_chg, d->soa.rec, d->soa.pt, d->soa.kerr,
-                  d->soa.xf, d->soa.xm, d->d_xrows, d->soa.dsx, d->d_ph, d->d_vfo, d->d_rsv, d->d_rsv_out};
+                  d->soa.xf, d->soa.xm, d->d_xrows, d->soa.dsx, d->d_ph, d->d_vfo, d->d_rsv, d->d_rsv_out, d->d_rsv_st};
   if (d->estream) (void)hipStreamSynchronize(d->estream);
   if (d->estream2) (void)hipStreamSynchronize(d->estream2);
   for (void* p : ptrs)
@@ -7129,7 +7211,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   }
   KArgs k = make_kargs(ctx, now);
   if (!ctx->rsv_pairs.empty() || ctx->rsv_affinity) {  // one matched pod (ke_schedule's segment of its own)
-    if (n_pods != 1 || d->world > 1 || d->comm) return fail(KE_ERR_UNSUPPORTED, "matched reservations need an unsharded singleton");
+    if (n_pods != 1) return fail(KE_ERR_UNSUPPORTED, "matched reservations need a singleton segment");
     for (const RsvPair& q : ctx->rsv_pairs)
       if (q.node < 0 || q.node >= ctx->n_nodes) return fail(KE_ERR_DEVICE, "reservation pair node out of range");
     rc = ensure((void**)&d->d_rsv, &d->rsv_cap, (int64_t)sizeof(RsvPair) * (int64_t)ctx->rsv_pairs.size());
@@ -7371,6 +7453,27 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
         }
         hipLaunchKernelGGL(k_merge, dim3((unsigned)bp), dim3(MERGE_BLOCK), 0, es, d->d_gath, d->world, L, kext,
                            lists, lists_cnt);
+        if (!ctx->rsv_pairs.empty() || ctx->rsv_affinity) {  // a matched singleton: the Reservation plugin in stages
+          int rlo = 0, rhi = N;
+          if (!d->loopback) shard_range(N, d->rank, d->world, &rlo, &rhi);
+          const int K = (int)ctx->rsv_pairs.size();
+          const int64_t wr = (int64_t)ctx->cfg.weight_reservation;
+          const int aff = (int)ctx->rsv_affinity;
+          RsvPickSt* st = d->d_rsv_st;
+          const bool coll = !d->loopback && d->comm;
+          hipLaunchKernelGGL(k_rsv_stage<0>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out);
+          if (coll) RCCL_OK(ncclAllReduce(&st->order, &st->order, 1, ncclInt64, ncclMin, d->comm, es));
+          hipLaunchKernelGGL(k_rsv_stage<1>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out);
+          if (coll) RCCL_OK(ncclAllReduce(&st->node, &st->node, 1, ncclInt32, ncclMin, d->comm, es));
+          hipLaunchKernelGGL(k_rsv_stage<2>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out);
+          if (coll) RCCL_OK(ncclAllReduce(&st->mx, &st->mx, 1, ncclInt32, ncclMax, d->comm, es));
+          hipLaunchKernelGGL(k_rsv_stage<3>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out);
+          if (coll) RCCL_OK(ncclAllReduce(&st->best, &st->best, 1, ncclUint64, ncclMax, d->comm, es));
+          hipLaunchKernelGGL(k_rsv_stage<4>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out);
+          if (coll) RCCL_OK(ncclAllReduce(&st->wt, &st->wt, 2, ncclInt32, ncclMax, d->comm, es));  // wt, nw
+          hipLaunchKernelGGL(k_rsv_stage<5>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out);
+          HIP_OK(hipMemcpyAsync(d->h_rsv_out.data(), d->d_rsv_out, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, es));
+        }
       }
     } else {
       if (prof) HIP_OK(hipEventRecord(pe[1], es));

@@ -199,3 +199,16 @@ def test_ignored_pods_beside_held_cpusets(gpu):
     assert e.value.code == abi.ERR_UNSUPPORTED
     with pytest.raises(RuntimeError, match=f"rc={abi.ERR_UNSUPPORTED}"):
         o.schedule(bad, synth.T0)
+
+
+def test_matched_cpuset_sharded_loopback(gpu):
+    """Matched cpuset pods from CPU-holding reservations in a node-sharded context (loopback, 3 shards): the views,
+    the Filter / Reserve decisions and the staged Reservation pick -- bit-exact with the oracle."""
+    ev, o, pods, matches, rs = cpuset_matched_setup(300, 1381, 200, affinity=0.3)
+    ev.shard_init(0, 3, None)
+    c1, s1 = ev.schedule(pods, synth.T0, matches=matches)
+    c0, s0 = o.schedule(pods, synth.T0, matches=matches)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5].ravel().tolist()
+    assert np.array_equal(s1, s0)
+    assert np.array_equal(ev.last_cpusets, o.last_cpusets)
+    _holdings_equal(ev, o)

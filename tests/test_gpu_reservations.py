@@ -345,3 +345,21 @@ def test_matched_batch_pods_parity(gpu):
     assert np.array_equal(ev.last_allocations()["reservation"], o.last_allocations()["reservation"])
     assert ev.check_records(synth.T0) == 0
     ev.close()
+
+
+@pytest.mark.parametrize("world,affinity", [(2, 0.0), (3, 0.4), (8, 0.0)])
+def test_matched_reservations_sharded_loopback(gpu, world, affinity):
+    """Node-sharded contexts (loopback: every shard in this context) with matched and affinity pods: the
+    Reservation plugin runs in stages over each shard's pairs (k_rsv_stage; on real ranks an all-reduce between the
+    stages) against the merged lists' top -- placements, totals, reservation state bit-exact with the oracle."""
+    ev, o, pods, matches = _matched_setup(300, 1011 + world, 260, affinity=affinity)
+    ev.shard_init(0, world, None)
+    c1, s1 = ev.schedule(pods, synth.T0, matches=matches)
+    c0, s0 = o.schedule(pods, synth.T0, matches=matches)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5].ravel().tolist()
+    assert np.array_equal(s1, s0)
+    _resv_equal(ev, o)
+    a1 = ev.last_allocations()
+    assert np.array_equal(a1["reservation"], o.last_allocations()["reservation"])
+    assert (a1["reservation"] > 0).sum() >= 5
+    ev.close()
