@@ -4331,12 +4331,8 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
             on_policy |= c->nodes[c->resv[r].node].node.numa_topology_policy != KE_NUMA_POLICY_NONE;
           }
         }
-        ds_pod d;
+        ds_pod d; /* (a pod binding CPUs allocates from the held CPUs: or_numa_ignored) */
         ds_prepare_pod(c, &pods[p], &d);
-        cpuset_state st;
-        cpuset_prefilter(c, &pods[p], &st);
-        const int binds = st.rcb || st.invalid || (node_bind && pods[p].requests[KE_RES_CPU] > 0);
-        (void)binds; /* a binding pod allocates from the held CPUs (or_numa_ignored) */
         if ((dev && !d.skip) || (numa_cpu && pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE) || on_policy)
           return KE_ERR_UNSUPPORTED;
       }
