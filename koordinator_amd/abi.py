@@ -547,6 +547,7 @@ EXPORTS = {
     "ke_last_kernel_stats_ex": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(i32), C.POINTER(i32)]),
     "ke_set_pipeline": (C.c_int, [C.c_void_p, i32]),
     "ke_debug_replay_phases": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "ke_debug_kernel_phases": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p]),
     "ke_debug_check_records": (C.c_int, [C.c_void_p, i64, C.POINTER(i64)]),
     "ke_last_host_stats": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ke_last_resolve_split": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]),

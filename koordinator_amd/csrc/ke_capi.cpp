@@ -23,7 +23,7 @@ int device_quota_sync(Context* ctx);
 int device_debug_rows(Context* ctx, int32_t n, Row* out);
 int device_set_profiling(Context* ctx, int32_t every);
 int device_set_pipeline(Context* ctx, int32_t on);
-int device_replay_phases(Context* ctx, double* cyc8);
+int device_replay_phases(Context* ctx, int which, double* cyc8);
 int device_check_records(Context* ctx, int64_t now, int64_t* bad);
 int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t iters, double* avg_ms);
 int device_comm_unique_id(uint8_t* id);
@@ -1225,7 +1225,15 @@ int ke_debug_replay_phases(ke_ctx* ctx, double* cyc8) {
   if (!ctx || !cyc8) return fail(KE_ERR_INVALID, "ke_debug_replay_phases arguments");
   int rc = require_device(ctx);
   if (rc) return rc;
-  return device_replay_phases(&ctx->c, cyc8);
+  return device_replay_phases(&ctx->c, 0, cyc8);
+}
+
+int ke_debug_kernel_phases(ke_ctx* ctx, int32_t kernel, double* cyc8) {
+  if (ctx) async_drain(ctx);
+  if (!ctx || !cyc8 || kernel < 0 || kernel > 2) return fail(KE_ERR_INVALID, "ke_debug_kernel_phases arguments");
+  int rc = require_device(ctx);
+  if (rc) return rc;
+  return device_replay_phases(&ctx->c, kernel, cyc8);
 }
 
 int ke_debug_spec_failed(ke_ctx* ctx, double* per_batch) {

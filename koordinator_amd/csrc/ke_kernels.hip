@@ -415,7 +415,7 @@ __constant__ uint8_t NUMA_OFF[10] = {0, 0, 8, 36, 92, 162, 218, 246, 254, 255}; 
 // the per-pod replay loop, summed over every pod into g_rprof (ke_debug_replay_phases).  Off in the
 // product build (the macro expands to nothing).
 #ifdef KE_PROF_REPLAY
-__device__ unsigned long long g_rprof[8];
+__device__ unsigned long long g_rprof[3][8];  // per kernel: k_resolve, k_numa_fallback, k_cpuset_reserve
 #define RPROF_DECL uint64_t rp_[7] = {0, 0, 0, 0, 0, 0, 0}, rp_t = __builtin_amdgcn_s_memtime();
 #define RPROF(i)                                         \
   {                                                      \
@@ -423,15 +423,15 @@ __device__ unsigned long long g_rprof[8];
     rp_[i] += rp_n - rp_t;                               \
     rp_t = rp_n;                                         \
   }
-#define RPROF_FLUSH(npods)                                                           \
-  if (lane == 0) {                                                                   \
-    for (int u_ = 0; u_ < 7; u_++) atomicAdd(&g_rprof[u_], (unsigned long long)rp_[u_]); \
-    atomicAdd(&g_rprof[7], (unsigned long long)(npods));                             \
+#define RPROF_FLUSH(blk, npods)                                                           \
+  if (lane == 0) {                                                                        \
+    for (int u_ = 0; u_ < 7; u_++) atomicAdd(&g_rprof[blk][u_], (unsigned long long)rp_[u_]); \
+    atomicAdd(&g_rprof[blk][7], (unsigned long long)(npods));                             \
   }
 #else
 #define RPROF_DECL
 #define RPROF(i)
-#define RPROF_FLUSH(npods)
+#define RPROF_FLUSH(blk, npods)
 #endif
 
 // ---- GPUAllocator.Allocate (allocator_gpu.go:72-451) ------------------------------------------------
@@ -3651,7 +3651,7 @@ __global__ __launch_bounds__(64) void k_numa_fallback(SoA s, const DevPod* __res
     RPROF(2)
     if (!fb) fb = NFB_BEST_EFFORT << 8 | aff;
     if (lane == 0) fb_out[w] = fb;
-    RPROF_FLUSH(1)
+    RPROF_FLUSH(1, 1)
     __syncthreads();
   }
 }
@@ -5455,7 +5455,7 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
     chg = chg_n;
     RPROF(6)
   }
-  RPROF_FLUSH(B)
+  RPROF_FLUSH(0, B)
   if (lane < B) {
     chosen[base + lane] = o_node;
     chosen_score[base + lane] = o_score;
@@ -6176,7 +6176,7 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
       if (quota) quota_reserve_g(s, pod, qreq);  // ElasticQuota Reserve
     }
     RPROF(6)
-    RPROF_FLUSH(1)
+    RPROF_FLUSH(2, 1)
     chosen[base] = out_node;
     chosen_score[base] = out_score;
     dev_alloc[base] = alloc;
@@ -7882,20 +7882,23 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   return KE_OK;
 }
 
-// cycles per pod of each replay phase since the last call (diagnostic build only; zeros otherwise)
-int device_replay_phases(Context* ctx, double* cyc8) {
+// cycles per unit of each phase of kernel `which` (0 k_resolve per pod, 1 k_numa_fallback per deferred pair,
+// 2 k_cpuset_reserve per pod) since its last read (diagnostic build only; zeros otherwise)
+int device_replay_phases(Context* ctx, int which, double* cyc8) {
 #ifdef KE_PROF_REPLAY
   DeviceState* d = ctx->dev;
   HIP_OK(hipSetDevice(d->device));
   HIP_OK(hipDeviceSynchronize());
   unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  HIP_OK(hipMemcpyFromSymbol(v, HIP_SYMBOL(g_rprof), sizeof(v)));
+  const size_t off = sizeof(v) * (size_t)which;
+  HIP_OK(hipMemcpyFromSymbol(v, HIP_SYMBOL(g_rprof), sizeof(v), off));
   const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_rprof), z, sizeof(z)));
+  HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_rprof), z, sizeof(z), off));
   for (int i = 0; i < 7; i++) cyc8[i] = v[7] ? (double)v[i] / (double)v[7] : 0.0;
   cyc8[7] = (double)v[7];
 #else
   (void)ctx;
+  (void)which;
   for (int i = 0; i < 8; i++) cyc8[i] = 0.0;
 #endif
   return KE_OK;

@@ -24,7 +24,7 @@ int device_quota_sync(Context*) { return KE_OK; }
 int device_debug_rows(Context*, int32_t, Row*) { return none(); }
 int device_set_profiling(Context*, int32_t) { return none(); }
 int device_set_pipeline(Context*, int32_t) { return none(); }
-int device_replay_phases(Context*, double*) { return none(); }
+int device_replay_phases(Context*, int, double*) { return none(); }
 int device_check_records(Context*, int64_t, int64_t*) { return none(); }
 int device_bench_eval(Context*, int32_t, const ke_pod*, int64_t, int32_t, double*) { return none(); }
 int device_comm_unique_id(uint8_t*) { return none(); }

@@ -21,8 +21,8 @@ synth.load_numa(ev, zones)
 synth.load_cpus(ev, tables)
 ev.eval(pods[:0], synth.T0)
 cyc = np.zeros(8)
-ev.lib.ke_debug_replay_phases(ev.h, cyc.ctypes.data_as(C.c_void_p))
+ev.lib.ke_debug_kernel_phases(ev.h, 1, cyc.ctypes.data_as(C.c_void_p))
 ev.schedule(pods, synth.T0)
-ev.lib.ke_debug_replay_phases(ev.h, cyc.ctypes.data_as(C.c_void_p))
+ev.lib.ke_debug_kernel_phases(ev.h, 1, cyc.ctypes.data_as(C.c_void_p))
 print(json.dumps({"units": int(cyc[7]), "cycles_per_unit": dict(zip(["step0_search", "later_steps", "best_effort_merge", "setup", "step0_list", "-", "-"],
                                                                   cyc[:7].round(1).tolist()))}))

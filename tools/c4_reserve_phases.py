@@ -30,9 +30,9 @@ def main():
     synth.load_cpus(ev, tables)
     ev.eval(pods[:0], synth.T0)
     cyc = np.zeros(8)
-    ev.lib.ke_debug_replay_phases(ev.h, cyc.ctypes.data_as(C.c_void_p))  # reset
+    ev.lib.ke_debug_kernel_phases(ev.h, 2, cyc.ctypes.data_as(C.c_void_p))  # reset
     ev.schedule(pods, synth.T0)
-    ev.lib.ke_debug_replay_phases(ev.h, cyc.ctypes.data_as(C.c_void_p))
+    ev.lib.ke_debug_kernel_phases(ev.h, 2, cyc.ctypes.data_as(C.c_void_p))
     print(json.dumps({"pods": int(cyc[7]), "cycles_per_pod": dict(zip(PHASES, cyc[:7].round(1).tolist())),
                       "total_cycles_per_pod": float(cyc[:7].sum())}))
 
