@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define KE_ABI_VERSION 11
+#define KE_ABI_VERSION 12
 #define KE_ABSENT (-1)
 
 typedef struct ke_ctx ke_ctx; /* one evaluator context (ke_create) */
@@ -544,7 +544,8 @@ typedef struct ke_pod {
   uint8_t has_initialized;
   uint8_t is_terminated;
   uint8_t has_resource_spec;          /* ResourceSpec annotation that failed to unmarshal (PreFilter Error) */
-  uint8_t has_other_requests;         /* PodRequests has a non-zero resource outside KE_RES_* */
+  uint8_t has_other_requests;         /* PodRequests has a non-zero resource outside KE_RES_*: 1 = each such name
+                                         has a resource id (its request is a ke_pod.xres entry), 2 = some has none */
   uint8_t has_unsupported_device_requests; /* Huawei NPU / Hygon DCU device resources: unsupported */
   int64_t device_requests[KE_PDR_COUNT]; /* PodRequests of the device resources (Value()), 0 = absent */
   int32_t numa_topology_policy; /* NUMATopologySpec annotation: KE_NUMA_POLICY_* (NONE = unset) */
@@ -651,7 +652,7 @@ int ke_abi_version(void);
 /* sizeof() of ke_config, ke_node, ke_node_metric, ke_pod_metric, ke_aggregated_usage, ke_pod,
  * ke_resource_map, ke_loadaware_args, ke_numa_args, ke_deviceshare_args, ke_device, ke_numa_zone, ke_cpu,
  * ke_quota_args, ke_quota, ke_gpu_partition, ke_ext_args, ke_node_resource, ke_pod_allocation, ke_pod_device_hints,
- * ke_gpu_template, ke_reservation, ke_reservation_alloc (in that order) for binding-layout checks. */
+ * ke_gpu_template, ke_reservation, ke_reservation_alloc, ke_reservation_resource (in that order) for binding-layout checks. */
 int ke_abi_struct_sizes(int32_t* sizes, int32_t n);
 /* 1 if this build has a usable HIP device and its gfx950 kernels loaded, else 0. */
 int ke_device_available(void);
@@ -731,7 +732,9 @@ int ke_node_devices_delete(ke_ctx* ctx, int32_t node);
  * What a reservation's reserve pod holds beyond NodeInfo — a NUMA allocation or a cpuset in the resource manager
  * (nodenumaresource/reservation.go:185-259), device instances in the device cache (deviceshare/reservation.go:
  * 136-195) — comes with ke_reservations_load_ex (ke_reservation_alloc); `holds` states which (the records decide).
- * Allocatable names other than cpu / memory (KE_RSV_OTHER_ALLOCATABLE) are refused (KE_ERR_UNSUPPORTED). */
+ * Allocatable names other than cpu / memory (pods, ephemeral storage, device resources, scalars) come with
+ * ke_reservations_load_full as resource entries (ke_reservation_resource) by resource id (the context's
+ * ke_ext_args id space, KE_MAX_XRES); the pod's request of such a name is its ke_pod.xres entry of that id. */
 #define KE_RSV_POLICY_DEFAULT 0    /* spec.allocatePolicy "" */
 #define KE_RSV_POLICY_ALIGNED 1    /* Aligned */
 #define KE_RSV_POLICY_RESTRICTED 2 /* Restricted (ResourceNames = the allocatable's names) */
@@ -741,14 +744,15 @@ int ke_node_devices_delete(ke_ctx* ctx, int32_t node);
 #define KE_RSV_HOLDS_DEVICES 4u  /* the reserve pod has device instances in the DeviceShare device cache     */
 #define KE_RSV_OTHER_ALLOCATABLE 8u /* status.allocatable names a resource other than cpu / memory (pods, GPU,
                                        scalars): scoreReservation / fitsReservation read them (scoring.go:191-210,
-                                       plugin.go:499-569) */
+                                       plugin.go:499-569); must agree with the reservation's resource entries
+                                       (ke_reservations_load_full; without them: KE_ERR_UNSUPPORTED) */
 typedef struct ke_reservation {
   int32_t node;           /* status.nodeName as a node index                                     */
   uint8_t available;      /* IsAvailable() and no ParseError                                     */
   uint8_t allocate_once;  /* spec.allocateOnce                                                   */
   uint8_t allocate_policy; /* KE_RSV_POLICY_*                                                     */
   uint8_t holds;          /* KE_RSV_HOLDS_*: must agree with the ke_reservation_alloc record (without one:
-                             KE_ERR_UNSUPPORTED); KE_RSV_OTHER_ALLOCATABLE: KE_ERR_UNSUPPORTED                 */
+                             KE_ERR_UNSUPPORTED); KE_RSV_OTHER_ALLOCATABLE: with the resource entries      */
   int32_t allocated_pods; /* GetAllocatedPods(): owner pods assigned to it                         */
   int32_t pad2;
   int64_t allocatable[KE_NRES]; /* status.allocatable = the reserve pod's requests: MilliCPU, Memory; a zero
@@ -756,7 +760,22 @@ typedef struct ke_reservation {
   int64_t allocated[KE_NRES];   /* status.allocated: the owner pods' requests                     */
   int64_t order;          /* label scheduling.koordinator.sh/reservation-order parsed (ParseInt), 0 = none */
   int64_t uid;            /* the Reservation's UID interned by the caller (release records find it by this; 0 = none) */
-} ke_reservation; /* 64 bytes */
+  int64_t reserved[KE_NRES]; /* rInfo.Reserved (GetNodeReservationFromAnnotation, reservation_info.go:88): the part
+                                of cpu / memory fitsReservation's capacity and GetAvailable exclude (0 = none)     */
+  uint8_t names_excluded;    /* bit r: cpu (0) / memory (1) left out of rInfo.ResourceNames by the Restricted
+                                options annotation (GetReservationRestrictedResources, reservation.go:637-654)      */
+  uint8_t pad3[7];
+} ke_reservation; /* 88 bytes */
+/* One status.allocatable entry of a reservation beyond cpu / memory (ke_reservations_load_full). */
+#define KE_RSV_RES_PODS (-1) /* the "pods" entry: fitsReservation's allocated-pods cap (plugin.go:511-527) */
+typedef struct ke_reservation_resource {
+  int32_t id;          /* resource id (ke_ext_args id space, not KE_XRES_CPU / KE_XRES_MEMORY) or KE_RSV_RES_PODS */
+  uint8_t excluded;    /* left out of rInfo.ResourceNames by the Restricted options annotation                  */
+  uint8_t pad[3];
+  int64_t allocatable; /* status.allocatable[name] (Value(); > 0)                                               */
+  int64_t allocated;   /* status.allocated[name] (Mask(owners' requests, ResourceNames))                        */
+  int64_t reserved;    /* rInfo.Reserved[name] (0 = none)                                                        */
+} ke_reservation_resource; /* 32 bytes */
 /* What a reservation's reserve pod holds beyond NodeInfo, and what its owner pods (rInfo.AssignedPods) hold:
  * the resource manager's NUMANodeResources / CPUSet of the reserve pod and of its owners
  * (resourceManager.GetAllocatedNUMAResource / GetAllocatedCPUSet, nodenumaresource/reservation.go:185-227), and
@@ -789,6 +808,17 @@ typedef struct ke_reservation_alloc {
  * the evaluator takes the holdings from the records. */
 int ke_reservations_load_ex(ke_ctx* ctx, int32_t n, const ke_reservation* reservations,
                             const ke_reservation_alloc* allocs);
+/* ke_reservations_load_ex with each reservation's allocatable names beyond cpu / memory: reservation i owns
+ * res[res_offsets[i] .. res_offsets[i+1]) (res_offsets: n + 1 entries; NULL = no entries), distinct ids, each
+ * with a positive allocatable.  KE_RSV_OTHER_ALLOCATABLE must be set exactly when a reservation has entries.  The
+ * entries enter every path that reads the reservation's allocatable / allocated: the NodeInfo restore of the
+ * scalars (NodeInfo.Requested.ScalarResources, NodeResourcesFit / FitPlus), the name check, fitsNode,
+ * fitsReservation and scoreReservation of the nominated-reservation path, and the Reserve's allocated. */
+int ke_reservations_load_full(ke_ctx* ctx, int32_t n, const ke_reservation* reservations,
+                              const ke_reservation_alloc* allocs, const int32_t* res_offsets,
+                              const ke_reservation_resource* res);
+/* Reservation r's resource entries as Reserve / release left them: up to cap entries, *n = count. */
+int ke_reservation_resources_get(ke_ctx* ctx, int32_t r, int32_t cap, ke_reservation_resource* out, int32_t* n);
 /* The holdings as they stand (owner parts after the Reserves / releases of this context). */
 int ke_reservation_allocs_get(ke_ctx* ctx, int32_t n, ke_reservation_alloc* out);
 /* Generation of the loaded reservation set: bumped by every ke_reservations_load. */

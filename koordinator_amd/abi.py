@@ -9,7 +9,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 ABSENT = -1
 
 OK = 0
@@ -393,7 +393,15 @@ RSV_HOLDS_NUMA, RSV_HOLDS_CPUSET, RSV_HOLDS_DEVICES, RSV_OTHER_ALLOCATABLE = 1, 
 class Reservation(C.Structure):  # ke_reservation
     _fields_ = [("node", i32), ("available", u8), ("allocate_once", u8), ("allocate_policy", u8), ("holds", u8),
                 ("allocated_pods", i32), ("pad2", i32), ("allocatable", i64 * NRES), ("allocated", i64 * NRES),
-                ("order", i64), ("uid", i64)]
+                ("order", i64), ("uid", i64), ("reserved", i64 * NRES), ("names_excluded", u8), ("pad3", u8 * 7)]
+
+
+RSV_RES_PODS = -1  # ke_reservation_resource.id of the "pods" entry
+
+
+class ReservationResource(C.Structure):  # ke_reservation_resource
+    _fields_ = [("id", i32), ("excluded", u8), ("pad", u8 * 3), ("allocatable", i64), ("allocated", i64),
+                ("reserved", i64)]
 
 
 class ReservationAlloc(C.Structure):  # ke_reservation_alloc
@@ -405,8 +413,9 @@ class ReservationAlloc(C.Structure):  # ke_reservation_alloc
 
 STRUCTS = [Config, Node, NodeMetric, PodMetric, AggregatedUsage, Pod, ResourceMap, LoadAwareArgs, NumaArgs,
            DeviceShareArgs, Device, NumaZone, Cpu, QuotaArgs, Quota, GpuPartition, ExtArgs, NodeResource,
-           PodAllocation, PodDeviceHints, GpuTemplate, Reservation, ReservationAlloc]
+           PodAllocation, PodDeviceHints, GpuTemplate, Reservation, ReservationAlloc, ReservationResource]
 RESERVATION_DTYPE = np.dtype(Reservation)
+RESERVATION_RESOURCE_DTYPE = np.dtype(ReservationResource)
 RESERVATION_ALLOC_DTYPE = np.dtype(ReservationAlloc)
 POD_DEVICE_HINTS_DTYPE = np.dtype(PodDeviceHints)
 GPU_TEMPLATE_DTYPE = np.dtype(GpuTemplate)
@@ -426,6 +435,16 @@ NODE_RESOURCE_DTYPE = np.dtype(NodeResource)
 POD_ALLOCATION_DTYPE = np.dtype(PodAllocation)
 
 ROW_DTYPE = np.dtype([("f", np.int64, (18,)), ("flags", np.uint32), ("pad", np.uint32)])
+
+
+def resource_csr(resources, n):
+    """per reservation a list / array of ke_reservation_resource entries -> (int32 offsets [n + 1], entries)"""
+    assert len(resources) == n
+    parts = [np.ascontiguousarray(np.asarray(x, RESERVATION_RESOURCE_DTYPE).reshape(-1)) for x in resources]
+    off = np.zeros(n + 1, np.int32)
+    off[1:] = np.cumsum([len(x) for x in parts])
+    res = np.concatenate(parts) if off[-1] else np.zeros(1, RESERVATION_RESOURCE_DTYPE)
+    return off, np.ascontiguousarray(res)
 
 
 def struct_array(items, ctype):
@@ -523,6 +542,8 @@ EXPORTS = {
     "ke_node_device_flags": (C.c_int, [C.c_void_p, i32, i32, i32]),
     "ke_reservations_load": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_reservations_load_ex": (C.c_int, [C.c_void_p, i32, C.c_void_p, C.c_void_p]),
+    "ke_reservations_load_full": (C.c_int, [C.c_void_p, i32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "ke_reservation_resources_get": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p, C.POINTER(i32)]),
     "ke_reservation_allocs_get": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_reservations_get": (C.c_int, [C.c_void_p, i32, C.c_void_p]),
     "ke_pod_reservations": (C.c_int, [C.c_void_p, i32, C.c_void_p, C.c_void_p]),

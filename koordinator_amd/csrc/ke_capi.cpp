@@ -34,6 +34,30 @@ bool device_sharded(const Context* ctx);
 
 using namespace ke;
 
+// The release records of one completed call (ke_last_allocations / ke_unreserve read them from the Context):
+// taken when the call completes, restored when ke_schedule_wait collects it, so a wait on an earlier ticket
+// never pairs that call's nodes with a later call's cpusets / NUMA amounts / device minors.
+struct CallRecords {
+  std::vector<int32_t> chosen, resv;
+  std::vector<int64_t> uid, numa;
+  std::vector<uint8_t> quota;
+  std::vector<uint64_t> cpusets, dev;
+  std::vector<int8_t> vf;
+  int32_t resv_gen = 0;  // the reservation set `resv` indexes
+  void save(const Context& c) {
+    chosen = c.last_chosen, resv = c.last_resv, uid = c.last_uid, numa = c.last_numa_alloc, quota = c.last_quota;
+    cpusets = c.last_cpusets, dev = c.last_dev_alloc, vf = c.last_vf;
+    resv_gen = c.resv_gen;
+  }
+  void restore(Context& c) {
+    c.last_chosen.swap(chosen), c.last_uid.swap(uid), c.last_numa_alloc.swap(numa), c.last_quota.swap(quota);
+    c.last_cpusets.swap(cpusets), c.last_dev_alloc.swap(dev), c.last_vf.swap(vf);
+    // a reservation set loaded since names other reservations: as load_reservations does, the records drop them
+    if (resv_gen == c.resv_gen) c.last_resv.swap(resv);
+    else c.last_resv.assign(c.last_chosen.size(), 0);
+  }
+};
+
 // A ke_schedule_submit call: its device work in flight (`fin` set), or completed with its outputs kept until
 // ke_schedule_wait collects them.
 struct AsyncCall {
@@ -46,6 +70,7 @@ struct AsyncCall {
   int rc = KE_OK;
   std::string msg;
   std::vector<int32_t> chosen, score;
+  CallRecords rec;  // its release records (set when it completes)
 };
 
 struct ke_ctx {
@@ -68,6 +93,14 @@ static void async_finish(ke_ctx* ctx, AsyncCall& a) {
     return;
   }
   Context& c = ctx->c;
+  // the completion wrote this call's device / cpuset / VF / NUMA records into the Context; a plain queue assumes
+  // no reservation and no quota
+  c.last_chosen = a.chosen;
+  c.last_uid.resize((size_t)a.n);
+  for (int32_t p = 0; p < a.n; p++) c.last_uid[(size_t)p] = a.pods[p].uid;
+  c.last_quota.assign((size_t)a.n, 0);
+  c.last_resv.assign((size_t)a.n, 0);
+  a.rec.save(c);
   const int32_t off = c.cfg.global_node_offset;
   const int64_t base = c.pending_base;  // the completion copied the pods there
   c.pending.reserve(c.pending.size() + (size_t)a.n);
@@ -164,9 +197,9 @@ static int check_matches(Context& c, const ke_pod* pods, int32_t n) {
     }
     if (!staged) return fail(KE_ERR_INVALID, "a KE_RSV_MATCHED / AFFINITY pod without ke_pod_reservations");
     const uint32_t f = c.staged[(size_t)p].flags;
-    // (batch / mid resources, KE_RES_BATCH_* / KE_RES_MID_*: a reservation holds only cpu / memory, so they enter
-    // the Reservation plugin as the pod's other resources of fitsNode, its ke_pod.xres, and nothing else)
-    bool scalar = pods[p].has_other_requests || pods[p].has_unsupported_device_requests;
+    // (the Reservation plugin reads the pod's requests by name: every name other than cpu / memory through its
+    // ke_pod.xres entry -- batch / mid resources included -- so a requested name without a resource id is refused)
+    bool scalar = pods[p].has_other_requests > 1 || pods[p].has_unsupported_device_requests;
     for (int r = 0; r < KE_PDR_COUNT; r++) scalar = scalar || pods[p].device_requests[r] != 0;
     if ((f & (PF_DS | PF_DS_HINT)) || scalar)
       return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations with device requests or unnamed resources");
@@ -202,7 +235,7 @@ int ke_abi_struct_sizes(int32_t* sizes, int32_t n) {
                          (int32_t)sizeof(ke_ext_args),     (int32_t)sizeof(ke_node_resource),
                          (int32_t)sizeof(ke_pod_allocation), (int32_t)sizeof(ke_pod_device_hints),
                          (int32_t)sizeof(ke_gpu_template),   (int32_t)sizeof(ke_reservation),
-                         (int32_t)sizeof(ke_reservation_alloc)};
+                         (int32_t)sizeof(ke_reservation_alloc), (int32_t)sizeof(ke_reservation_resource)};
   const int32_t m = (int32_t)(sizeof(all) / sizeof(all[0]));
   for (int32_t i = 0; i < n && i < m; i++) sizes[i] = all[i];
   return m;
@@ -464,6 +497,26 @@ int ke_reservations_load_ex(ke_ctx* ctx, int32_t n, const ke_reservation* reserv
   if (!ctx) return fail(KE_ERR_INVALID, "null context");
   flush_mirror(ctx->c);
   return load_reservations(ctx->c, n, reservations, allocs);
+}
+
+int ke_reservations_load_full(ke_ctx* ctx, int32_t n, const ke_reservation* reservations,
+                              const ke_reservation_alloc* allocs, const int32_t* res_offsets,
+                              const ke_reservation_resource* res) {
+  if (ctx) async_drain(ctx);
+  if (!ctx) return fail(KE_ERR_INVALID, "null context");
+  if (!res_offsets) return fail(KE_ERR_INVALID, "ke_reservations_load_full: res_offsets");
+  flush_mirror(ctx->c);
+  return load_reservations(ctx->c, n, reservations, allocs, res_offsets, res);
+}
+
+int ke_reservation_resources_get(ke_ctx* ctx, int32_t r, int32_t cap, ke_reservation_resource* out, int32_t* n) {
+  if (ctx) async_drain(ctx);
+  if (!ctx || !n || cap < 0 || (cap > 0 && !out) || r < 0 || r >= (int32_t)ctx->c.resv.size())
+    return fail(KE_ERR_INVALID, "ke_reservation_resources_get arguments");
+  const auto& e = (size_t)r < ctx->c.resv_res.size() ? ctx->c.resv_res[(size_t)r] : std::vector<ke_reservation_resource>{};
+  *n = (int32_t)e.size();
+  for (int32_t i = 0; i < cap && i < *n; i++) out[i] = e[(size_t)i];
+  return KE_OK;
 }
 
 int ke_reservation_allocs_get(ke_ctx* ctx, int32_t n, ke_reservation_alloc* out) {
@@ -1033,7 +1086,13 @@ int ke_schedule_submit(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t 
       a.now = now_ns;
       a.device = true;
       rc = device_schedule_enqueue(&c, n_pods, pods, now_ns, true, &a.fin);
-      if (rc) return rc;
+      if (rc) {
+        // the call in flight keeps the buffers its completion captured: swap back, and let no partly enqueued
+        // launch of this call outlive the error
+        if (in_flight > 0) device_swap_call_buffers(&c);
+        device_quiesce(&c);
+        return rc;
+      }
       *ticket = a.ticket;
       ctx->async.push_back(std::move(a));
       return KE_OK;
@@ -1050,6 +1109,7 @@ int ke_schedule_submit(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_t 
   a.score.assign((size_t)n_pods, 0);
   const int rc = schedule_sync(ctx, n_pods, pods, now_ns, a.chosen.data(), a.score.data());
   if (rc) return rc;
+  a.rec.save(c);
   *ticket = a.ticket;
   ctx->async.push_back(std::move(a));
   return KE_OK;
@@ -1067,14 +1127,9 @@ int ke_schedule_wait(ke_ctx* ctx, int64_t ticket, int32_t* chosen, int32_t* scor
   if (a.rc) return fail(a.rc, a.msg);
   std::copy(a.chosen.begin(), a.chosen.end(), chosen);
   if (score) std::copy(a.score.begin(), a.score.end(), score);
-  if (a.device) {  // release records of this call (ke_last_allocations / ke_unreserve): the last collected call
-    Context& c = ctx->c;
-    c.last_chosen = a.chosen;
-    c.last_uid.resize((size_t)a.n);
-    c.last_quota.assign((size_t)a.n, 0);
-    c.last_resv.assign((size_t)a.n, 0);
-    for (int32_t p = 0; p < a.n; p++) c.last_uid[(size_t)p] = a.pods[p].uid;
-  }
+  // release records of this call (ke_last_allocations / ke_unreserve): the last collected call, device-enqueued
+  // or run at once alike
+  a.rec.restore(ctx->c);
   return KE_OK;
 }
 

@@ -519,9 +519,11 @@ int ke_decode_pod(const char* js, int64_t len, int32_t n_names, const char* cons
   }
   for (const auto& kv : reqs) {
     if (kv.second == 0) continue;
-    bool known = false;
+    bool known = false, named = false;
     for (const char* n : KE_RES_NAMES) known |= kv.first == n;
-    if (!known) p.has_other_requests = 1;
+    for (int32_t id = 0; id < n_names && !named; id++) named = xres_names[id] && kv.first == xres_names[id];
+    // 1: every other name has a resource id (its request is in ke_pod.xres); 2: some name has none
+    if (!known) p.has_other_requests = std::max<uint8_t>(p.has_other_requests, named ? 1 : 2);
     for (int d = 0; d < KE_PDR_COUNT; d++)
       if (kv.first == PDR_NAMES[d] && !total_value(reqs, kv.first, &p.device_requests[d]))
         return unsup("device request out of range");

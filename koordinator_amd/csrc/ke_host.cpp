@@ -552,8 +552,44 @@ void derive_ext_row(const ke_config& cfg, const NodeState& ns, int64_t* f, uint6
 std::atomic<uint64_t> g_dirty_epoch{0};
 
 int64_t xres_requested(const NodeState& ns, const ke_node_resource& r) {
-  // cpu / memory rows carry NonZeroRequested: the reservation restore moves it too
-  return r.requested + (r.id == KE_RES_CPU || r.id == KE_RES_MEMORY ? ns.rv_nz[r.id] : 0);
+  // cpu / memory rows carry NonZeroRequested: the reservation restore moves it too; scalars move with
+  // NodeInfo.Requested.ScalarResources (updateNodeInfoRequested, transformer.go:491-504)
+  return r.requested + (r.id == KE_RES_CPU || r.id == KE_RES_MEMORY ? ns.rv_nz[r.id] : rv_x_of(ns, r.id));
+}
+
+int64_t rv_x_of(const NodeState& ns, int32_t id) {
+  for (const auto& e : ns.rv_x)
+    if (e.first == id) return e.second;
+  return 0;
+}
+
+int64_t pod_request_of(const ke_pod& pod, int32_t id) {
+  if (id == KE_XRES_CPU) return pod.requests[KE_RES_CPU];
+  if (id == KE_XRES_MEMORY) return pod.requests[KE_RES_MEMORY];
+  for (int e = 0; e < pod.n_xres && e < KE_MAX_POD_XRES; e++)
+    if (pod.xres_id[e] == id) return pod.xres_value[e];
+  return 0;
+}
+
+using XDelta = std::vector<std::pair<int32_t, int64_t>>;
+static void x_add(XDelta* x, int32_t id, int64_t d) {
+  if (!x) return;
+  for (auto& e : *x)
+    if (e.first == id) {
+      e.second += d;
+      return;
+    }
+  x->push_back({id, d});
+}
+static int64_t x_get(const XDelta& x, int32_t id) {
+  for (const auto& e : x)
+    if (e.first == id) return e.second;
+  return 0;
+}
+// reservation i's entries beyond cpu / memory (none without ke_reservations_load_full)
+static const std::vector<ke_reservation_resource>& resv_entries(const Context& c, int32_t i) {
+  static const std::vector<ke_reservation_resource> none;
+  return (size_t)i < c.resv_res.size() ? c.resv_res[(size_t)i] : none;
 }
 
 // The reservation cache's NodeInfo restore (BeforePreFilter, transformer.go:147-300).  A reservation that is
@@ -567,14 +603,17 @@ int64_t xres_requested(const NodeState& ns, const ke_node_resource& r) {
 static int64_t resv_non0(int k, int64_t v) { return v != 0 ? v : (k == KE_RES_CPU ? 100 : 200LL << 20); }
 bool resv_usable(const ke_reservation& r) { return r.available && !(r.allocate_once && r.allocated_pods > 0); }
 
-// node's Requested / NonZeroRequested deltas with `matched` (by reservation index, nullptr = none) matched
+// node's Requested / NonZeroRequested deltas with `matched` (by reservation index, nullptr = none) matched; `x`:
+// the NodeInfo.Requested.ScalarResources deltas by resource id of their entries beyond cpu / memory
 static void resv_delta(const Context& c, int32_t node, const std::vector<char>* matched, bool with_matched,
-                       int64_t* req, int64_t* nz, int32_t* pods = nullptr) {
+                       int64_t* req, int64_t* nz, int32_t* pods = nullptr, XDelta* x = nullptr) {
   for (int k = 0; k < KE_NRES; k++) req[k] = nz[k] = 0;
   if (pods) *pods = 0;
+  if (x) x->clear();
   for (int32_t i : c.resv_by_node[(size_t)node]) {
     const ke_reservation& r = c.resv[(size_t)i];
     if (!resv_usable(r)) continue;
+    const std::vector<ke_reservation_resource>& ex = resv_entries(c, i);
     if (matched && (*matched)[(size_t)i]) {
       if (!with_matched) continue;
       if (pods) --*pods;  // NodeInfo.RemovePod(reservePod)
@@ -582,19 +621,25 @@ static void resv_delta(const Context& c, int32_t node, const std::vector<char>* 
         req[k] -= r.allocatable[k];
         nz[k] -= resv_non0(k, r.allocatable[k]);
       }
+      for (const ke_reservation_resource& e : ex)
+        if (e.id != KE_RSV_RES_PODS) x_add(x, e.id, -e.allocatable);
       continue;
     }
     if (r.allocated_pods == 0) continue;
     int64_t rem[KE_NRES];
-    bool rem_nz = false;
+    bool rem_nz = false;  // quotav1.IsZero(SubtractWithNonNegativeResult(Allocatable, Allocated)) over every name
     for (int k = 0; k < KE_NRES; k++) {
       rem[k] = r.allocatable[k] > r.allocated[k] ? r.allocatable[k] - r.allocated[k] : 0;
       rem_nz = rem_nz || rem[k] != 0;
     }
+    for (const ke_reservation_resource& e : ex) rem_nz = rem_nz || e.allocatable > e.allocated;
     for (int k = 0; k < KE_NRES; k++) {
       req[k] += -r.allocatable[k] + rem[k];
       nz[k] += -resv_non0(k, r.allocatable[k]) + (rem_nz ? resv_non0(k, rem[k]) : 0);
     }
+    for (const ke_reservation_resource& e : ex)
+      if (e.id != KE_RSV_RES_PODS)
+        x_add(x, e.id, -e.allocatable + (e.allocatable > e.allocated ? e.allocatable - e.allocated : 0));
   }
 }
 
@@ -653,7 +698,7 @@ static void resv_plugin_restore(const Context& c, int32_t node, const std::vecto
 
 void resv_node_restore(Context& c, int32_t node) {
   NodeState& ns = c.nodes[(size_t)node];
-  resv_delta(c, node, nullptr, false, ns.rv_req, ns.rv_nz, &ns.rv_pods);
+  resv_delta(c, node, nullptr, false, ns.rv_req, ns.rv_nz, &ns.rv_pods, &ns.rv_x);
   resv_plugin_restore(c, node, nullptr, ns);
   ns.dirty = true;
 }
@@ -667,15 +712,19 @@ uint8_t resv_holds_of(const ke_reservation_alloc& a) {
   return h;
 }
 
-int load_reservations(Context& c, int32_t n, const ke_reservation* rs, const ke_reservation_alloc* allocs) {
+int load_reservations(Context& c, int32_t n, const ke_reservation* rs, const ke_reservation_alloc* allocs,
+                      const int32_t* res_off, const ke_reservation_resource* res) {
   if (n < 0 || (n > 0 && !rs)) return fail(KE_ERR_INVALID, "reservations");
+  if (res_off && res_off[0] != 0) return fail(KE_ERR_INVALID, "reservation resource offsets");
   for (int32_t i = 0; i < n; i++) {
     const ke_reservation& r = rs[i];
     if (r.node < 0 || r.node >= c.n_nodes) return fail(KE_ERR_NOT_FOUND, "reservation node index");
     if (r.allocated_pods < 0) return fail(KE_ERR_INVALID, "negative reservation allocated pods");
     if (r.allocate_policy > KE_RSV_POLICY_RESTRICTED) return fail(KE_ERR_INVALID, "reservation allocate policy");
     for (int k = 0; k < KE_NRES; k++)
-      if (r.allocatable[k] < 0 || r.allocated[k] < 0) return fail(KE_ERR_INVALID, "negative reservation quantity");
+      if (r.allocatable[k] < 0 || r.allocated[k] < 0 || r.reserved[k] < 0)
+        return fail(KE_ERR_INVALID, "negative reservation quantity");
+    if (r.names_excluded & ~3u) return fail(KE_ERR_INVALID, "ke_reservation.names_excluded");
     // the holdings come with the record (ke_reservations_load_ex); a holds bit without one has nothing to restore
     // from: refused rather than scheduled around without the NUMA / cpuset / device restore (koord_eval.h)
     const uint8_t held = allocs ? resv_holds_of(allocs[i]) : 0;
@@ -701,8 +750,30 @@ int load_reservations(Context& c, int32_t n, const ke_reservation* rs, const ke_
       if ((a.device_minors | a.owner_device_minors) & ~0x0000FFFFFFFFFFFFull)
         return fail(KE_ERR_INVALID, "reservation device minors beyond the three types");
     }
-    if (r.holds & KE_RSV_OTHER_ALLOCATABLE)
-      return fail(KE_ERR_UNSUPPORTED, "a reservation whose allocatable names resources other than cpu / memory");
+    // the allocatable names beyond cpu / memory: with their entries (ke_reservations_load_full), else refused
+    const int32_t ne = res_off ? res_off[i + 1] - res_off[i] : 0;
+    if (ne < 0 || (ne > 0 && !res)) return fail(KE_ERR_INVALID, "reservation resource offsets");
+    if (!res_off && (r.holds & KE_RSV_OTHER_ALLOCATABLE))
+      return fail(KE_ERR_UNSUPPORTED, "a reservation whose allocatable names resources other than cpu / memory, "
+                                      "without its resource entries (ke_reservations_load_full)");
+    if (res_off && ((r.holds & KE_RSV_OTHER_ALLOCATABLE) != 0) != (ne > 0))
+      return fail(KE_ERR_INVALID, "KE_RSV_OTHER_ALLOCATABLE disagrees with the reservation's resource entries");
+    uint64_t seen = 0;
+    bool pods_seen = false;
+    for (int32_t j = 0; j < ne; j++) {
+      const ke_reservation_resource& e = res[res_off[i] + j];
+      if (e.id == KE_RSV_RES_PODS) {
+        if (pods_seen) return fail(KE_ERR_INVALID, "duplicate reservation resource id");
+        pods_seen = true;
+      } else {
+        if (e.id == KE_XRES_CPU || e.id == KE_XRES_MEMORY || e.id < 0 || e.id >= KE_MAX_XRES)
+          return fail(KE_ERR_INVALID, "reservation resource id (cpu / memory go in ke_reservation)");
+        if (seen >> e.id & 1) return fail(KE_ERR_INVALID, "duplicate reservation resource id");
+        seen |= 1ull << e.id;
+      }
+      if (e.allocatable <= 0 || e.allocated < 0 || e.reserved < 0) return fail(KE_ERR_INVALID, "reservation resource quantity");
+      if (e.excluded > 1) return fail(KE_ERR_INVALID, "ke_reservation_resource.excluded");
+    }
     if (r.holds & ~15u) return fail(KE_ERR_INVALID, "unknown ke_reservation.holds bits");
   }
   std::vector<int32_t> old;
@@ -710,6 +781,8 @@ int load_reservations(Context& c, int32_t n, const ke_reservation* rs, const ke_
   c.resv.assign(rs, rs + n);
   if (allocs) c.resv_alloc.assign(allocs, allocs + n);
   else c.resv_alloc.clear();
+  c.resv_res.assign((size_t)n, {});
+  for (int32_t i = 0; res_off && i < n; i++) c.resv_res[(size_t)i].assign(res + res_off[i], res + res_off[i + 1]);
   c.resv_cpu_cnt.clear();
   c.resv_holds.assign((size_t)n, 0);
   for (int32_t i = 0; allocs && i < n; i++) c.resv_holds[(size_t)i] = resv_holds_of(allocs[i]);
@@ -723,61 +796,86 @@ int load_reservations(Context& c, int32_t n, const ke_reservation* rs, const ke_
 }
 
 // FilterNominateReservation -> filterWithReservations(..., requiredFromReservation = true) for one matched
-// reservation (plugin.go:351-442, 707-738): a resource name shared with the pod, fitsNode over the restored
-// NodeInfo (plugin.go:447-497; preemptible empty; the pod-count check not modelled) and, for Restricted,
-// fitsReservation (plugin.go:499-569).  podRequested = Requested after the unmatched restore only,
-// allRAllocated = Σ allocated of the node's matched reservations.
+// reservation (plugin.go:351-442, 707-738): a resource name of rInfo.ResourceNames shared with the pod, fitsNode
+// over the restored NodeInfo (plugin.go:447-497; preemptible empty) and, for Restricted, fitsReservation
+// (plugin.go:499-569).  podRequested = Requested after the unmatched restore only (`ureq`, `ux`: its scalar part's
+// restore delta), allRAllocated = Σ allocated of the node's matched reservations (`all_alloc`, `all_x`).
 // With a reservation affinity the name check is skipped (the pod may use any matched reservation, :373).
 // The pod-count check of fitsNode (plugin.go:450-453) reads len(NodeInfo.Pods) of the snapshot NodeInfo, which
 // the BeforePreFilter restore already left without the matched reserve pods (restoreMatchedReservation ->
 // RemovePod, transformer.go:440), and subtracts len(matchedOrIgnored) once more: `pods_restored` is the former.
-static bool resv_nominable(const ke_reservation& r, const ke_pod& pod, const NodeState& ns, const int64_t* pod_requested,
-                           const int64_t* all_allocated, bool affinity, int64_t pods_restored, int64_t n_matched,
+// rInfo.GetAvailable() = SubtractWithNonNegativeResult(Allocatable - Allocated, Reserved) (reservation_info.go:484-488).
+static bool resv_nominable(const Context& c, int32_t ri, const ke_pod& pod, const NodeState& ns,
+                           const int64_t* pod_requested, const XDelta& ux, const int64_t* all_allocated,
+                           const XDelta& all_x, bool affinity, int64_t pods_restored, int64_t n_matched,
                            int64_t allowed_pods) {
-  bool shared = false;
-  for (int k = 0; k < KE_NRES; k++) shared = shared || (r.allocatable[k] != 0 && pod.requests[k] != 0);
+  const ke_reservation& r = c.resv[(size_t)ri];
+  const std::vector<ke_reservation_resource>& ex = resv_entries(c, ri);
+  bool shared = false;  // quotav1.Intersection(rInfo.ResourceNames, ResourceNames(podRequests))
+  for (int k = 0; k < KE_NRES; k++)
+    shared = shared || (r.allocatable[k] != 0 && !(r.names_excluded >> k & 1) && pod.requests[k] != 0);
+  for (const ke_reservation_resource& e : ex)
+    shared = shared || (!e.excluded && e.id != KE_RSV_RES_PODS && pod_request_of(pod, e.id) != 0);
   if (!shared && !affinity) return false;
   bool node_fits = pods_restored - n_matched + 1 <= allowed_pods;
-  // the pod's other resources (ephemeral storage, scalars: its ke_pod.xres) -- a reservation holds none of them
-  // (KE_RSV_OTHER_ALLOCATABLE is refused), so their rRemained / allRAllocated are 0 and podRequested is the node's
-  bool other = false;
+  bool other = false;  // ephemeral storage / scalar requests (framework.Resource.ScalarResources): ke_pod.xres
   for (int e = 0; e < pod.n_xres; e++)
     other = other || (pod.xres_id[e] != KE_XRES_CPU && pod.xres_id[e] != KE_XRES_MEMORY && pod.xres_value[e] != 0);
+  auto avail = [](int64_t a, int64_t al, int64_t rs) { return a - al - rs > 0 ? a - al - rs : 0; };
   if (pod.requests[KE_RES_CPU] != 0 || pod.requests[KE_RES_MEMORY] != 0 || other) {  // else pods only (:455-460)
     const int64_t* alloc = ns.node.allocatable;
     for (int k = 0; k < KE_NRES; k++) {
-      const int64_t remained = r.allocatable[k] > r.allocated[k] ? r.allocatable[k] - r.allocated[k] : 0;  // GetAvailable
+      const int64_t remained = avail(r.allocatable[k], r.allocated[k], r.reserved[k]);
       if (pod.requests[k] > alloc[k] - (pod_requested[k] - remained - all_allocated[k])) node_fits = false;
     }
     for (int e = 0; e < pod.n_xres; e++) {  // (plugin.go:487-495)
       const int32_t id = pod.xres_id[e];
       if (id == KE_XRES_CPU || id == KE_XRES_MEMORY || pod.xres_value[e] == 0) continue;
-      int64_t a = 0, q = 0;
+      int64_t a = 0, q = x_get(ux, id), remained = 0;
       for (const ke_node_resource& x : ns.xres)
-        if (x.id == id) a = x.allocatable, q = x.requested;
-      if (pod.xres_value[e] > a - q) node_fits = false;
+        if (x.id == id) a = x.allocatable, q += x.requested;
+      for (const ke_reservation_resource& re : ex)
+        if (re.id == id) remained = avail(re.allocatable, re.allocated, re.reserved);
+      if (pod.xres_value[e] > a - (q - remained - x_get(all_x, id))) node_fits = false;
     }
   }
   bool resv_fits = node_fits;
   if (r.allocate_policy == KE_RSV_POLICY_RESTRICTED) {
     resv_fits = true;
-    for (int k = 0; k < KE_NRES; k++)  // requests masked to the reservation's names; zero requests skipped
-      if (r.allocatable[k] != 0 && pod.requests[k] != 0 && pod.requests[k] > r.allocatable[k] - r.allocated[k])
+    for (const ke_reservation_resource& e : ex)  // "pods" reserved explicitly: one more assigned pod fits (:511-527)
+      if (e.id == KE_RSV_RES_PODS && (int64_t)r.allocated_pods + 1 > e.allocatable) resv_fits = false;
+    // Mask(podRequests, ResourceNames), zero requests skipped: requested <= capacity - reserved - allocated
+    for (int k = 0; k < KE_NRES; k++)
+      if (r.allocatable[k] != 0 && !(r.names_excluded >> k & 1) && pod.requests[k] != 0 &&
+          pod.requests[k] > r.allocatable[k] - r.reserved[k] - r.allocated[k])
         resv_fits = false;
+    for (const ke_reservation_resource& e : ex) {
+      if (e.excluded || e.id == KE_RSV_RES_PODS) continue;
+      const int64_t q = pod_request_of(pod, e.id);
+      if (q != 0 && q > e.allocatable - e.reserved - e.allocated) resv_fits = false;
+    }
   }
   return node_fits && resv_fits;
 }
 
 // scoreReservation (scoring.go:191-210): MostAllocated of (pod requests + allocated) over the reservation's
-// non-zero allocatable, 100 * req / capacity per resource that fits, averaged
-int32_t resv_score(const ke_reservation& r, const ke_pod& pod) {
+// non-zero allocatable (every name, "pods" too), MaxNodeScore * req.MilliValue() / capacity.MilliValue() per
+// resource that fits, averaged over all of them (exact in 128-bit: Go's int64 product wraps only beyond ~9.2e13
+// bytes of a non-cpu resource)
+int32_t resv_score(const Context& c, int32_t i, const ke_pod& pod) {
+  const ke_reservation& r = c.resv[(size_t)i];
   int64_t s = 0, w = 0;
-  for (int k = 0; k < KE_NRES; k++) {
-    if (r.allocatable[k] == 0) continue;
+  auto term = [&](int64_t req, int64_t cap, bool milli) {
     w++;
-    const int64_t req = pod.requests[k] + r.allocated[k];
-    if (req <= r.allocatable[k]) s += 100 * req / r.allocatable[k];  // MilliValue ratio: the same quotient
-  }
+    if (req <= cap) {
+      const __int128 m = milli ? 1 : 1000;
+      s += (int64_t)((__int128)100 * req * m / ((__int128)cap * m));
+    }
+  };
+  for (int k = 0; k < KE_NRES; k++)
+    if (r.allocatable[k] != 0) term(pod.requests[k] + r.allocated[k], r.allocatable[k], k == KE_RES_CPU);
+  for (const ke_reservation_resource& e : resv_entries(c, i))
+    term((e.id == KE_RSV_RES_PODS ? 0 : pod_request_of(pod, e.id)) + e.allocated, e.allocatable, false);
   return w ? (int32_t)(s / w) : 0;
 }
 
@@ -826,7 +924,7 @@ void resv_ignore_begin(Context& c) {
   for (size_t node = 0; node < c.resv_by_node.size(); node++) {
     if (c.resv_by_node[node].empty()) continue;
     NodeState& ns = c.nodes[node];
-    resv_delta(c, (int32_t)node, &all, true, ns.rv_req, ns.rv_nz, &ns.rv_pods);
+    resv_delta(c, (int32_t)node, &all, true, ns.rv_req, ns.rv_nz, &ns.rv_pods, &ns.rv_x);
     resv_plugin_restore(c, (int32_t)node, &all, ns);
     ns.dirty = true;
   }
@@ -967,7 +1065,8 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
   for (int32_t node : c.rsv_nodes) {
     NodeState& ns = c.nodes[(size_t)node];
     int64_t ureq[KE_NRES], unz[KE_NRES], pod_requested[KE_NRES], all_alloc[KE_NRES] = {0, 0};
-    resv_delta(c, node, &m, false, ureq, unz);
+    XDelta ux, all_x;
+    resv_delta(c, node, &m, false, ureq, unz, nullptr, &ux);
     for (int k = 0; k < KE_NRES; k++) pod_requested[k] = ns.node.requested[k] + ureq[k];
     std::vector<int32_t> mine;
     int64_t order = 0;  // findMostPreferredReservationByOrder over all matched (scoring.go:170-189)
@@ -975,6 +1074,8 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
       if (m[(size_t)i]) {
         mine.push_back(i);
         for (int k = 0; k < KE_NRES; k++) all_alloc[k] += c.resv[(size_t)i].allocated[k];
+        for (const ke_reservation_resource& e : resv_entries(c, i))
+          if (e.id != KE_RSV_RES_PODS) x_add(&all_x, e.id, e.allocated);
         const int64_t o = c.resv[(size_t)i].order;
         if (o != 0 && (order == 0 || o < order)) order = o;
       }
@@ -999,7 +1100,7 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
     bool fits_one = false;  // the Reservation Filter with a reservation affinity (plugin.go:316-318, 351-442): a
                             // node without matched reservations fails, one with them passes when one of them fits
     for (int32_t i : mine)
-      if (resv_nominable(c.resv[(size_t)i], pod, ns, pod_requested, all_alloc, affinity, pods_restored,
+      if (resv_nominable(c, i, pod, ns, pod_requested, ux, all_alloc, all_x, affinity, pods_restored,
                          (int64_t)mine.size(), ns.node.allowed_pods)) {
         fits_one = true;
         if (numa_nominable(i)) ok.push_back(i);
@@ -1023,7 +1124,7 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
       if (nom < 0) {
         int32_t bs = -1;
         for (int32_t i : ok) {
-          const int32_t sc = resv_score(c.resv[(size_t)i], pod);
+          const int32_t sc = resv_score(c, i, pod);
           if (sc > bs) {
             bs = sc;
             nom = i;
@@ -1031,7 +1132,7 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
         }
       }
     }
-    c.rsv_pairs.push_back({node, (int16_t)(nom >= 0 ? resv_score(c.resv[(size_t)nom], pod) : 0), (int16_t)allowed, order});
+    c.rsv_pairs.push_back({node, (int16_t)(nom >= 0 ? resv_score(c, nom, pod) : 0), (int16_t)allowed, order});
     c.rsv_nominated.push_back(nom);
     // NodeNUMAResource with the matched reservations first (plugin.go:381-397, 553-563): the Filter's trial
     // (one satisfied; else "Reservation(s) ..." under an affinity, else the node's own) and Reserve's allocation
@@ -1062,7 +1163,7 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
       }
     }
     // the rows this pod sees: its matched reservations restored too, and left out of the plugins' unmatched states
-    resv_delta(c, node, &m, true, ns.rv_req, ns.rv_nz, &ns.rv_pods);
+    resv_delta(c, node, &m, true, ns.rv_req, ns.rv_nz, &ns.rv_pods, &ns.rv_x);
     resv_plugin_restore(c, node, &m, ns);
     ns.dirty = true;
   }
@@ -1121,7 +1222,10 @@ void resv_finish(Context& c, int32_t chosen_local, const ke_pod& pod, int32_t* a
       // assumePod -> AddAssignedPod (reservation_info.go:458-468): Mask(requests, ResourceNames)
       ke_reservation& r = c.resv[(size_t)c.rsv_nominated[j]];
       for (int k = 0; k < KE_NRES; k++)
-        if (r.allocatable[k] != 0) r.allocated[k] += pod.requests[k];
+        if (r.allocatable[k] != 0 && !(r.names_excluded >> k & 1)) r.allocated[k] += pod.requests[k];
+      if ((size_t)c.rsv_nominated[j] < c.resv_res.size())
+        for (ke_reservation_resource& e : c.resv_res[(size_t)c.rsv_nominated[j]])
+          if (!e.excluded && e.id != KE_RSV_RES_PODS) e.allocated += pod_request_of(pod, e.id);
       r.allocated_pods++;
       *assumed = 1 + c.rsv_nominated[j];
       resv_owner_update(c, c.rsv_nominated[j], pod, cpuset, numa, dev_minors, +1);
@@ -1145,7 +1249,10 @@ void resv_forget(Context& c, int32_t idx, const ke_pod& pod, const ke_pod_alloca
   if (idx < 0 || idx >= (int32_t)c.resv.size()) return;
   ke_reservation& r = c.resv[(size_t)idx];
   for (int k = 0; k < KE_NRES; k++)
-    if (r.allocatable[k] != 0) r.allocated[k] = std::max<int64_t>(0, r.allocated[k] - pod.requests[k]);
+    if (r.allocatable[k] != 0 && !(r.names_excluded >> k & 1)) r.allocated[k] = std::max<int64_t>(0, r.allocated[k] - pod.requests[k]);
+  if ((size_t)idx < c.resv_res.size())
+    for (ke_reservation_resource& e : c.resv_res[(size_t)idx])
+      if (!e.excluded && e.id != KE_RSV_RES_PODS) e.allocated = std::max<int64_t>(0, e.allocated - pod_request_of(pod, e.id));
   if (r.allocated_pods > 0) r.allocated_pods--;
   if (a) resv_owner_update(c, idx, pod, a->cpuset, a->numa, a->device_minors, -1);
   resv_node_restore(c, r.node);

@@ -108,6 +108,8 @@ struct NodeState {
   // Requested / NonZeroRequested (MilliCPU, Memory) when the rows are derived (load_reservations)
   int64_t rv_req[KE_NRES] = {0, 0}, rv_nz[KE_NRES] = {0, 0};
   int32_t rv_pods = 0;  // len(NodeInfo.Pods) delta of the restore (matched reserve pods removed)
+  // ... and of NodeInfo.Requested.ScalarResources by resource id (reservations' allocatable beyond cpu / memory)
+  std::vector<std::pair<int32_t, int64_t>> rv_x;
   // ... and the plugins' restore states of the reservations holding NUMA / cpuset / device allocations
   // (ke_reservations_load_ex): NodeNUMAResource's reusableResources per zone (mergedUnmatchedUsed; key bits
   // 2*id + r of the ResourceList keys present) and DeviceShare's preemptible per instance
@@ -206,6 +208,8 @@ struct Context {
   std::vector<ke_reservation> resv;  // ke_reservations_load (allocated / allocated_pods kept by Reserve)
   std::vector<ke_reservation_alloc> resv_alloc;  // their NUMA / cpuset / device holdings (owner parts kept by Reserve)
   std::vector<uint8_t> resv_holds;   // derived from resv_alloc: KE_RSV_HOLDS_* bits
+  // per reservation its allocatable names beyond cpu / memory (ke_reservations_load_full; allocated kept by Reserve)
+  std::vector<std::vector<ke_reservation_resource>> resv_res;
   std::vector<std::vector<uint8_t>> resv_cpu_cnt;  // per reservation: owners per CPU id (lazily from owner_cpuset)
   std::vector<std::vector<int32_t>> resv_by_node;  // reservation indices per node
   // ke_pod_reservations staging for the next ke_schedule: CSR over its pods
@@ -291,6 +295,7 @@ void mirror_join(Context& c);
 using DevFinish = std::function<int(int32_t* chosen, int32_t* score)>;
 int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, bool want_score, DevFinish* fin);
 void device_swap_call_buffers(Context* ctx);
+void device_quiesce(Context* ctx);  // wait for every stream of the context (after a failed enqueue)
 bool device_refresh_pending(const Context* ctx, int64_t now);
 bool device_async_ok(const Context* ctx, int32_t n_pods);
 
@@ -322,10 +327,16 @@ int validate_node_resources(int32_t n, const ke_node_resource* r);
 int ext_slots(const ke_config& cfg, int32_t* ids);
 // the ext SoA row of a node: NUM_XF int64 + the uint64 mask of resource ids with Allocatable > 0
 void derive_ext_row(const ke_config& cfg, const NodeState& ns, int64_t* f, uint64_t* mask);
-int load_reservations(Context& c, int32_t n, const ke_reservation* r, const ke_reservation_alloc* allocs = nullptr);
+int load_reservations(Context& c, int32_t n, const ke_reservation* r, const ke_reservation_alloc* allocs = nullptr,
+                      const int32_t* res_off = nullptr, const ke_reservation_resource* res = nullptr);
 bool resv_usable(const ke_reservation& r);
 void resv_node_restore(Context& c, int32_t node);  // the restore every non-matching pod sees
-int32_t resv_score(const ke_reservation& r, const ke_pod& pod);
+// scoreReservation of reservation i for the pod (reservation/scoring.go:191-210)
+int32_t resv_score(const Context& c, int32_t i, const ke_pod& pod);
+// the pod's PodRequests of resource id (cpu / memory: ke_pod.requests, others: its ke_pod.xres entry, 0 without)
+int64_t pod_request_of(const ke_pod& pod, int32_t id);
+// the scalar restore delta of resource id on the node (NodeInfo.Requested.ScalarResources)
+int64_t rv_x_of(const NodeState& ns, int32_t id);
 // the nominated-reservation path of one KE_RSV_MATCHED pod: rows with its matched restore, rsv_pairs /
 // rsv_nominated; resv_finish assumes the pod into the chosen node's nominated reservation (1 + index, 0)
 int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids, bool affinity);

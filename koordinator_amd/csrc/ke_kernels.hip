@@ -7082,6 +7082,14 @@ void device_swap_call_buffers(Context* ctx) {
   d->tev.swap(a.tev);
 }
 
+// a failed enqueue may have left part of its launches on the streams: wait for every stream of the context
+void device_quiesce(Context* ctx) {
+  DeviceState* d = ctx->dev;
+  if (!d) return;
+  (void)hipSetDevice(d->device);
+  (void)hipDeviceSynchronize();
+}
+
 // whether the next call's device_refresh would upload rows (derived from the host state, which lacks the Reserves
 // of a call still in flight) or change a device table
 bool device_refresh_pending(const Context* ctx, int64_t now) {

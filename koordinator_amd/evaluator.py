@@ -142,17 +142,31 @@ class Evaluator:
         t = abi.struct_array(templates, abi.GpuTemplate)
         self._check(self.lib.ke_gpu_templates_load(self.h, len(t), abi.ptr(t)))
 
-    def reservations_load(self, reservations, allocs=None):
-        """ke_reservations_load(_ex): the reservation cache (RESERVATION_DTYPE array) and, optionally, each one's
-        NUMA / cpuset / device holdings (RESERVATION_ALLOC_DTYPE array, one per reservation)."""
+    def reservations_load(self, reservations, allocs=None, resources=None):
+        """ke_reservations_load(_ex / _full): the reservation cache (RESERVATION_DTYPE array), optionally each one's
+        NUMA / cpuset / device holdings (RESERVATION_ALLOC_DTYPE array, one per reservation) and its allocatable
+        names beyond cpu / memory (`resources`: per reservation a RESERVATION_RESOURCE_DTYPE array or list)."""
         r = abi.struct_array(reservations, abi.Reservation)
-        if allocs is None:
-            self._check(self.lib.ke_reservations_load(self.h, len(r), abi.ptr(r)))
-        else:
+        a = None
+        if allocs is not None:
             a = abi.struct_array(allocs, abi.ReservationAlloc)
             assert len(a) == len(r)
+        if resources is not None:
+            off, res = abi.resource_csr(resources, len(r))
+            self._check(self.lib.ke_reservations_load_full(self.h, len(r), abi.ptr(r), abi.ptr(a) if a is not None else None,
+                                                           abi.ptr(off), abi.ptr(res)))
+        elif a is None:
+            self._check(self.lib.ke_reservations_load(self.h, len(r), abi.ptr(r)))
+        else:
             self._check(self.lib.ke_reservations_load_ex(self.h, len(r), abi.ptr(r), abi.ptr(a)))
         self._n_resv = len(r)
+
+    def reservation_resources_get(self, i):
+        """ke_reservation_resources_get: reservation i's entries beyond cpu / memory as Reserve / release left them."""
+        out = np.zeros(abi.MAX_XRES + 1, abi.RESERVATION_RESOURCE_DTYPE)
+        n = C.c_int32()
+        self._check(self.lib.ke_reservation_resources_get(self.h, int(i), len(out), abi.ptr(out), C.byref(n)))
+        return out[:n.value]
 
     def reservation_allocs_get(self):
         """ke_reservation_allocs_get: the holdings with the owner parts as Reserve / release left them."""

@@ -69,6 +69,8 @@ def load():
         "or_reservations_load": (C.c_int, [V, i32, V]),
         "or_reservations_get": (C.c_int, [V, i32, V]),
         "or_reservations_load_ex": (C.c_int, [V, i32, V, V]),
+        "or_reservations_load_full": (C.c_int, [V, i32, V, V, V, V]),
+        "or_reservation_resources_get": (C.c_int, [V, i32, i32, V, V]),
         "or_restore_state": (C.c_int, [V, i32, V]),
         "or_numa_reserve_from_rsv": (C.c_int, [V, V, i32, V, i32, i32, i32, V]),
         "or_reservation_allocs_get": (C.c_int, [V, i32, V]),
@@ -77,6 +79,7 @@ def load():
         "or_reservation_score": (C.c_int64, [V, V]),
         "or_reservation_prescore": (i32, [V, V, V, i32, V, V]),
         "or_reservation_filter": (i32, [V, V, V, i32, i32]),
+        "or_rsv_filter_with": (i32, [V, i32, V, i32, V, V, i32, i32]),
         "or_node_info_requested": (C.c_int, [V, i32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
         "or_node_device_flags": (C.c_int, [V, i32, i32, i32]),
         "or_last_vf_ranks": (C.c_int, [V, i32, V]),
@@ -286,17 +289,29 @@ class Oracle:
         t = abi.struct_array(templates, abi.GpuTemplate)
         assert self.lib.or_gpu_templates_load(self.h, len(t), abi.ptr(t)) == 0
 
-    def reservations_load(self, reservations, allocs=None):
+    def reservations_load(self, reservations, allocs=None, resources=None):
         r = abi.struct_array(reservations, abi.Reservation)
-        if allocs is None:
-            rc = self.lib.or_reservations_load(self.h, len(r), abi.ptr(r))
-        else:
+        a = None
+        if allocs is not None:
             a = abi.struct_array(allocs, abi.ReservationAlloc)
             assert len(a) == len(r)
+        if resources is not None:
+            off, res = abi.resource_csr(resources, len(r))
+            rc = self.lib.or_reservations_load_full(self.h, len(r), abi.ptr(r), abi.ptr(a) if a is not None else None,
+                                                    abi.ptr(off), abi.ptr(res))
+        elif a is None:
+            rc = self.lib.or_reservations_load(self.h, len(r), abi.ptr(r))
+        else:
             rc = self.lib.or_reservations_load_ex(self.h, len(r), abi.ptr(r), abi.ptr(a))
         if rc != 0:
             raise RuntimeError(f"oracle reservations_load rc={rc}")
         self._n_resv = len(r)
+
+    def reservation_resources_get(self, i):
+        out = np.zeros(abi.MAX_XRES + 1, abi.RESERVATION_RESOURCE_DTYPE)
+        n = C.c_int32()
+        assert self.lib.or_reservation_resources_get(self.h, int(i), len(out), abi.ptr(out), C.byref(n)) == 0
+        return out[:n.value]
 
     def numa_reserve_from_rsv(self, pod, node, ids, nom, required):
         """NodeNUMAResource Reserve's allocate-from-reservation (or_numa_reserve_from_rsv): (code, cpuset words)."""
@@ -345,6 +360,18 @@ class Oracle:
         p = as_pod_array([pod] if isinstance(pod, abi.Pod) else np.asarray(pod).reshape(1))
         ids = np.ascontiguousarray(ids, np.int32)
         return bool(self.lib.or_reservation_filter(self.h, abi.ptr(p), abi.ptr(ids), len(ids), int(node)))
+
+    def rsv_filter_with(self, r, pod, node, pod_requested, r_allocated, required, affinity):
+        """filterWithReservations over reservation r alone with the given podRequested / rAllocated (cpu, memory,
+        then per resource id): 0 ok, 1 by node, 2 by reservation, 3 none meets."""
+        p = as_pod_array([pod] if isinstance(pod, abi.Pod) else np.asarray(pod).reshape(1))
+        pr = np.zeros(abi.NRES + abi.MAX_XRES, np.int64)
+        ra = np.zeros(abi.NRES + abi.MAX_XRES, np.int64)
+        for dst, src in ((pr, pod_requested), (ra, r_allocated)):
+            for k, v in src.items():
+                dst[k] = v
+        return int(self.lib.or_rsv_filter_with(self.h, int(r), abi.ptr(p), int(node), abi.ptr(pr), abi.ptr(ra),
+                                               int(required), int(affinity)))
 
     def reservation_score(self, reservation, pod):
         """scoreReservation of one reservation record for one pod (golden-vector entry point)."""

@@ -74,6 +74,7 @@ typedef struct or_node {
   /* the reservation cache's NodeInfo restore for a pod that matches no reservation (or_reservations_load) */
   int64_t rv_req[KE_NRES], rv_nz[KE_NRES];
   int32_t rv_pods; /* len(NodeInfo.Pods) delta of the restore: a matched reservation's reserve pod is removed */
+  int64_t rv_x[KE_MAX_XRES]; /* ... and of NodeInfo.Requested.ScalarResources by resource id */
   /* the plugins' RestoreReservation states of the pod being evaluated (or_restore): NodeNUMAResource's
    * mergedUnmatchedUsed per NUMA id (ResourceList keys tracked) and DeviceShare's per (type, minor) */
   int rs_numa_has[KE_MAX_NUMA];
@@ -114,6 +115,9 @@ struct or_cluster {
   int ignored;                  /* the pod being evaluated / reserved is reservation-ignored (or_numa_ignored) */
   uint8_t* rcpu;                /* [reservation][cpu] owner counts (or_owner_update), NULL until first needed */
   int32_t n_resv;
+  /* each reservation's allocatable entries beyond cpu / memory (or_reservations_load_full): roff[i] .. roff[i+1] */
+  int32_t* roff;
+  ke_reservation_resource* rres;
   int32_t* moff;
   int32_t* mids;
   int32_t m_pods;
@@ -3006,6 +3010,8 @@ void or_destroy(or_cluster* c) {
   free(c->resv);
   free(c->ralloc);
   free(c->rcpu);
+  free(c->roff);
+  free(c->rres);
   free(c->moff);
   free(c->mids);
   free(c->last_resv);
@@ -3133,6 +3139,7 @@ static void or_restore(or_cluster* c, const char* matched, int with_matched) {
     or_node* nd = &c->nodes[i];
     for (int k = 0; k < KE_NRES; k++) nd->rv_req[k] = nd->rv_nz[k] = 0;
     nd->rv_pods = 0;
+    memset(nd->rv_x, 0, sizeof nd->rv_x);
     memset(nd->rs_numa_has, 0, sizeof nd->rs_numa_has);
     memset(nd->rs_numa_key, 0, sizeof nd->rs_numa_key);
     memset(nd->rs_numa, 0, sizeof nd->rs_numa);
@@ -3152,26 +3159,35 @@ static void or_restore(or_cluster* c, const char* matched, int with_matched) {
     const ke_reservation* r = &c->resv[i];
     if (!or_resv_usable(r)) continue;
     or_node* nd = &c->nodes[r->node];
+    const ke_reservation_resource* ex = c->rres ? c->rres + c->roff[i] : NULL;
+    const int32_t nex = c->rres ? c->roff[i + 1] - c->roff[i] : 0;
     if (matched && matched[i]) {
       if (with_matched) nd->rv_pods--; /* restoreMatchedReservation: NodeInfo.RemovePod(reservePod) */
-      if (with_matched)
+      if (with_matched) {
         for (int k = 0; k < KE_NRES; k++) {
           nd->rv_req[k] -= r->allocatable[k];
           nd->rv_nz[k] -= or_non0(k, r->allocatable[k]);
         }
+        for (int32_t e = 0; e < nex; e++) /* Requested.ScalarResources of the reserve pod's other names */
+          if (ex[e].id != KE_RSV_RES_PODS) nd->rv_x[ex[e].id] -= ex[e].allocatable;
+      }
       continue;
     }
     if (r->allocated_pods == 0) continue;
     int64_t rem[KE_NRES];
-    int rem_nz = 0;
+    int rem_nz = 0; /* quotav1.IsZero(SubtractWithNonNegativeResult(Allocatable, Allocated)) over every name */
     for (int k = 0; k < KE_NRES; k++) {
       rem[k] = r->allocatable[k] - r->allocated[k] > 0 ? r->allocatable[k] - r->allocated[k] : 0;
       rem_nz |= rem[k] != 0;
     }
+    for (int32_t e = 0; e < nex; e++) rem_nz |= ex[e].allocatable - ex[e].allocated > 0;
     for (int k = 0; k < KE_NRES; k++) {
       nd->rv_req[k] += -r->allocatable[k] + rem[k];
       nd->rv_nz[k] += -or_non0(k, r->allocatable[k]) + (rem_nz ? or_non0(k, rem[k]) : 0);
     }
+    for (int32_t e = 0; e < nex; e++)
+      if (ex[e].id != KE_RSV_RES_PODS)
+        nd->rv_x[ex[e].id] += -ex[e].allocatable + (ex[e].allocatable - ex[e].allocated > 0 ? ex[e].allocatable - ex[e].allocated : 0);
   }
 }
 /* An owner pod enters (+1) / leaves (-1) the reservation's AssignedPods: its resource manager / device cache entries
@@ -3283,13 +3299,23 @@ static uint8_t or_holds_of(const ke_reservation_alloc* a) {
   if (a->device_minors) h |= KE_RSV_HOLDS_DEVICES;
   return h;
 }
-int or_reservations_load_ex(or_cluster* c, int32_t n, const ke_reservation* rs, const ke_reservation_alloc* allocs) {
+int or_reservations_load_full(or_cluster* c, int32_t n, const ke_reservation* rs, const ke_reservation_alloc* allocs,
+                              const int32_t* roff, const ke_reservation_resource* res) {
   for (int32_t i = 0; i < n; i++) {
     if (rs[i].node < 0 || rs[i].node >= c->n) return KE_ERR_NOT_FOUND;
     const uint8_t said = rs[i].holds & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET | KE_RSV_HOLDS_DEVICES);
-    if (rs[i].holds & KE_RSV_OTHER_ALLOCATABLE) return KE_ERR_UNSUPPORTED; /* other allocatable names */
+    const int32_t ne = roff ? roff[i + 1] - roff[i] : 0;
+    if (!roff && (rs[i].holds & KE_RSV_OTHER_ALLOCATABLE)) return KE_ERR_UNSUPPORTED; /* names without entries */
+    if (roff && ((rs[i].holds & KE_RSV_OTHER_ALLOCATABLE) != 0) != (ne > 0)) return KE_ERR_INVALID;
     if (!allocs && said) return KE_ERR_UNSUPPORTED;                      /* holdings without their record */
     if (allocs && or_holds_of(&allocs[i]) != said) return KE_ERR_INVALID;
+    for (int32_t e = 0; e < ne; e++) {
+      const ke_reservation_resource* x = &res[roff[i] + e];
+      if (x->id != KE_RSV_RES_PODS && (x->id < 2 || x->id >= KE_MAX_XRES)) return KE_ERR_INVALID;
+      if (x->allocatable <= 0 || x->allocated < 0 || x->reserved < 0) return KE_ERR_INVALID;
+      for (int32_t f = 0; f < e; f++)
+        if (res[roff[i] + f].id == x->id) return KE_ERR_INVALID; /* one entry per name */
+    }
   }
   free(c->resv);
   c->resv = (ke_reservation*)malloc(sizeof(ke_reservation) * (size_t)(n > 0 ? n : 1));
@@ -3298,6 +3324,16 @@ int or_reservations_load_ex(or_cluster* c, int32_t n, const ke_reservation* rs, 
   c->ralloc = NULL;
   free(c->rcpu);
   c->rcpu = NULL;
+  free(c->roff);
+  free(c->rres);
+  c->roff = NULL;
+  c->rres = NULL;
+  if (roff) {
+    c->roff = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n + 1));
+    memcpy(c->roff, roff, sizeof(int32_t) * (size_t)(n + 1));
+    c->rres = (ke_reservation_resource*)malloc(sizeof(ke_reservation_resource) * (size_t)(roff[n] > 0 ? roff[n] : 1));
+    if (roff[n] > 0) memcpy(c->rres, res, sizeof(ke_reservation_resource) * (size_t)roff[n]);
+  }
   if (allocs && n > 0) {
     c->ralloc = (ke_reservation_alloc*)malloc(sizeof(ke_reservation_alloc) * (size_t)n);
     memcpy(c->ralloc, allocs, sizeof(ke_reservation_alloc) * (size_t)n);
@@ -3306,8 +3342,17 @@ int or_reservations_load_ex(or_cluster* c, int32_t n, const ke_reservation* rs, 
   or_restore(c, NULL, 0);
   return KE_OK;
 }
+int or_reservations_load_ex(or_cluster* c, int32_t n, const ke_reservation* rs, const ke_reservation_alloc* allocs) {
+  return or_reservations_load_full(c, n, rs, allocs, NULL, NULL);
+}
 int or_reservations_load(or_cluster* c, int32_t n, const ke_reservation* rs) {
   return or_reservations_load_ex(c, n, rs, NULL);
+}
+int or_reservation_resources_get(const or_cluster* c, int32_t r, int32_t cap, ke_reservation_resource* out, int32_t* n) {
+  if (r < 0 || r >= c->n_resv) return KE_ERR_INVALID;
+  *n = c->rres ? c->roff[r + 1] - c->roff[r] : 0;
+  for (int32_t e = 0; e < cap && e < *n; e++) out[e] = c->rres[c->roff[r] + e];
+  return KE_OK;
 }
 int or_reservation_allocs_get(const or_cluster* c, int32_t n, ke_reservation_alloc* out) {
   if (n < 0 || n > c->n_resv) return KE_ERR_INVALID;
@@ -3337,31 +3382,63 @@ int or_pod_reservations(or_cluster* c, int32_t n_pods, const int32_t* offsets, c
 }
 
 /* ScoreReservation -> scoreReservation (reservation/scoring.go:141-164, 191-210): requested = PodRequests +
- * allocated; over RemoveZeros(allocatable): MaxNodeScore * req.MilliValue() / capacity.MilliValue() for each
- * resource with req <= capacity, summed, divided by the number of resources */
+ * allocated; over RemoveZeros(allocatable) -- every name, "pods" too: MaxNodeScore * req.MilliValue() /
+ * capacity.MilliValue() for each resource with req <= capacity, summed, divided by the number of resources.
+ * (128-bit products: Go's int64 product wraps only beyond ~9.2e13 of a non-cpu resource.) */
+static void or_score_term(int64_t req, int64_t cap, int milli_is_value, int64_t* s, int64_t* w) {
+  (*w)++;
+  if (req > cap) return;
+  const __int128 m = milli_is_value ? 1 : 1000; /* cpu: MilliValue(); others: Value() * 1000 */
+  *s += (int64_t)((__int128)MAX_NODE_SCORE * req * m / ((__int128)cap * m));
+}
+/* the pod's PodRequests of resource id (cpu / memory: requests; others: its ke_pod.xres entry) */
+static int64_t pod_xres(const ke_pod* pod, int32_t id);
+static int64_t or_pod_request_of(const ke_pod* pod, int32_t id) {
+  if (id == KE_XRES_CPU) return pod->requests[KE_RES_CPU];
+  if (id == KE_XRES_MEMORY) return pod->requests[KE_RES_MEMORY];
+  return pod_xres(pod, id);
+}
 int64_t or_reservation_score(const ke_reservation* r, const ke_pod* pod) {
   int64_t s = 0, w = 0;
-  for (int k = 0; k < KE_NRES; k++) {
-    if (r->allocatable[k] == 0) continue;
-    w++;
-    const int64_t req = pod->requests[k] + r->allocated[k];
-    const int64_t milli = k == KE_RES_CPU ? 1 : 1000; /* memory: Value() * 1000 */
-    if (req <= r->allocatable[k]) s += MAX_NODE_SCORE * (req * milli) / (r->allocatable[k] * milli);
+  for (int k = 0; k < KE_NRES; k++)
+    if (r->allocatable[k] != 0) or_score_term(pod->requests[k] + r->allocated[k], r->allocatable[k], k == KE_RES_CPU, &s, &w);
+  return w ? s / w : 0;
+}
+static int64_t or_reservation_score_idx(const or_cluster* c, int32_t i, const ke_pod* pod) {
+  const ke_reservation* r = &c->resv[i];
+  int64_t s = 0, w = 0;
+  for (int k = 0; k < KE_NRES; k++)
+    if (r->allocatable[k] != 0) or_score_term(pod->requests[k] + r->allocated[k], r->allocatable[k], k == KE_RES_CPU, &s, &w);
+  for (int32_t e = c->rres ? c->roff[i] : 0; c->rres && e < c->roff[i + 1]; e++) {
+    const ke_reservation_resource* x = &c->rres[e];
+    or_score_term((x->id == KE_RSV_RES_PODS ? 0 : or_pod_request_of(pod, x->id)) + x->allocated, x->allocatable, 0, &s, &w);
   }
   return w ? s / w : 0;
 }
 
 /* FilterNominateReservation (reservation/plugin.go:707-738) -> filterWithReservations(..., true) on one
- * reservation (:351-442): skipped (not nominable) without a resource name shared with the pod (:369-375);
- * fitsNode (:447-497: pods count not modelled; preemptible empty) with podRequested = Requested after the
- * unmatched restore, rRemained = GetAvailable (allocatable - allocated, >= 0), allRAllocated = Σ allocated
- * of the node's matched reservations; fitsReservation (:499-569) for the Restricted policy, else the node fit.
+ * reservation (:351-442): skipped (not nominable) without a name of rInfo.ResourceNames shared with the pod
+ * (:369-375); fitsNode (:447-497; preemptible empty) with podRequested = Requested after the unmatched restore
+ * (scalars too), rRemained = GetAvailable = max(0, allocatable - allocated - reserved) per name, allRAllocated =
+ * Σ allocated of the node's matched reservations; fitsReservation (:499-569) for the Restricted policy (the "pods"
+ * cap, then every requested name of ResourceNames within allocatable - reserved - allocated), else the node fit.
  * The NUMA / DeviceShare FilterNominateReservation pass for pods without cpuset, NUMA policy or devices. */
-static int or_resv_nominable(const or_cluster* c, const ke_reservation* r, const ke_pod* pod, int32_t node,
+static int64_t or_rsv_entry(const or_cluster* c, int32_t i, int32_t id, const ke_reservation_resource** out) {
+  *out = NULL;
+  for (int32_t e = c->rres ? c->roff[i] : 0; c->rres && e < c->roff[i + 1]; e++)
+    if (c->rres[e].id == id) *out = &c->rres[e];
+  return *out ? 1 : 0;
+}
+static int64_t or_avail(int64_t a, int64_t al, int64_t rs) { return a - al - rs > 0 ? a - al - rs : 0; }
+static int or_resv_nominable(const or_cluster* c, int32_t ri, const ke_pod* pod, int32_t node,
                              const int64_t* pod_requested, const int64_t* all_allocated, int affinity) {
+  const ke_reservation* r = &c->resv[ri];
+  const int32_t e0 = c->rres ? c->roff[ri] : 0, e1 = c->rres ? c->roff[ri + 1] : 0;
   int shared = 0;
   for (int k = 0; k < KE_NRES; k++)
-    if (r->allocatable[k] != 0 && pod->requests[k] != 0) shared = 1;
+    if (r->allocatable[k] != 0 && !((r->names_excluded >> k) & 1) && pod->requests[k] != 0) shared = 1;
+  for (int32_t e = e0; e < e1; e++)
+    if (!c->rres[e].excluded && c->rres[e].id != KE_RSV_RES_PODS && or_pod_request_of(pod, c->rres[e].id) != 0) shared = 1;
   if (!shared && !affinity) return 0; /* plugin.go:373: skipped only without a reservation affinity */
   /* fitsNode's pod count (plugin.go:450-453): len(nodeInfo.Pods) of the snapshot NodeInfo the BeforePreFilter
    * restore left (the matched reserve pods removed: rv_pods after or_restore(m, 1)) minus len(matchedOrIgnored) */
@@ -3372,16 +3449,14 @@ static int or_resv_nominable(const or_cluster* c, const ke_reservation* r, const
    * moves only Requested) */
   const int64_t pods_restored = (int64_t)c->nodes[node].node.pod_count - n_matched;
   int node_fits = pods_restored - n_matched + 1 <= (int64_t)c->nodes[node].node.allowed_pods;
-  /* the pod's ephemeral storage / scalar resources (ke_pod.xres): a reservation holds none of them, so rRemained and
-   * allRAllocated are 0 there and podRequested is the node's (plugin.go:487-495); without any request only the pod
-   * count is checked (:455-460) */
+  /* the pod's ephemeral storage / scalar resources (ke_pod.xres): Allocatable - (podRequested - rRemained -
+   * allRAllocated) per name (plugin.go:487-495); without any request only the pod count is checked (:455-460) */
   int other = 0;
   for (int32_t e = 0; e < pod->n_xres; e++)
     other |= pod->xres_id[e] != KE_XRES_CPU && pod->xres_id[e] != KE_XRES_MEMORY && pod->xres_value[e] != 0;
   if (!(pod->requests[KE_RES_CPU] == 0 && pod->requests[KE_RES_MEMORY] == 0) || other) {
     for (int k = 0; k < KE_NRES; k++) {
-      int64_t remained = r->allocatable[k] - r->allocated[k];
-      if (remained < 0) remained = 0;
+      const int64_t remained = or_avail(r->allocatable[k], r->allocated[k], r->reserved[k]);
       const int64_t avail = c->nodes[node].node.allocatable[k] - (pod_requested[k] - remained - all_allocated[k]);
       if (pod->requests[k] > avail) node_fits = 0;
     }
@@ -3389,15 +3464,28 @@ static int or_resv_nominable(const or_cluster* c, const ke_reservation* r, const
       const int32_t id = pod->xres_id[e];
       if (id == KE_XRES_CPU || id == KE_XRES_MEMORY || pod->xres_value[e] == 0) continue;
       const ke_node_resource* x = node_xres(&c->nodes[node], id);
-      if (pod->xres_value[e] > (x ? x->allocatable - x->requested : 0)) node_fits = 0;
+      /* podRequested: the node's requested with the unmatched restore (its scalar delta: pod_requested[KE_NRES + id],
+       * taken by or_resv_begin before the matched restore) */
+      const int64_t q = (x ? x->requested : 0) + pod_requested[KE_NRES + id];
+      const ke_reservation_resource* re;
+      const int64_t remained = or_rsv_entry(c, ri, id, &re) ? or_avail(re->allocatable, re->allocated, re->reserved) : 0;
+      if (pod->xres_value[e] > (x ? x->allocatable : 0) - (q - remained - all_allocated[KE_NRES + id])) node_fits = 0;
     }
   }
   int resv_fits = node_fits;
   if (r->allocate_policy == KE_RSV_POLICY_RESTRICTED) {
     resv_fits = 1;
+    const ke_reservation_resource* pods_e;
+    if (or_rsv_entry(c, ri, KE_RSV_RES_PODS, &pods_e) && (int64_t)r->allocated_pods + 1 > pods_e->allocatable) resv_fits = 0;
     for (int k = 0; k < KE_NRES; k++) {
-      if (r->allocatable[k] == 0 || pod->requests[k] == 0) continue; /* Mask(requests, names); zero skipped */
-      if (pod->requests[k] > r->allocatable[k] - r->allocated[k]) resv_fits = 0;
+      if (r->allocatable[k] == 0 || ((r->names_excluded >> k) & 1) || pod->requests[k] == 0) continue; /* Mask; zero skipped */
+      if (pod->requests[k] > r->allocatable[k] - r->reserved[k] - r->allocated[k]) resv_fits = 0;
+    }
+    for (int32_t e = e0; e < e1; e++) {
+      const ke_reservation_resource* x = &c->rres[e];
+      if (x->excluded || x->id == KE_RSV_RES_PODS) continue;
+      const int64_t q = or_pod_request_of(pod, x->id);
+      if (q != 0 && q > x->allocatable - x->reserved - x->allocated) resv_fits = 0;
     }
   }
   return node_fits && resv_fits;
@@ -3670,7 +3758,7 @@ int64_t or_fitplus_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
     const ke_node_resource* r = node_xres(nd, id);
     const int64_t alloc = r ? r->allocatable : 0;
     /* NonZeroRequested of cpu / memory after the reservation restore */
-    const int64_t rv = r && (id == KE_RES_CPU || id == KE_RES_MEMORY) ? nd->rv_nz[id] : 0;
+    const int64_t rv = r && (id == KE_RES_CPU || id == KE_RES_MEMORY) ? nd->rv_nz[id] : (r ? nd->rv_x[id] : 0);
     const int64_t req = (r ? r->requested + rv : 0) + pod_xres(pod, id);
     const int64_t rs = ra->type == KE_STRATEGY_MOST_ALLOCATED ? fp_most(req, alloc) : fp_least(req, alloc);
     node_score += rs * ra->weight;
@@ -3698,7 +3786,7 @@ static int or_fit_filter(const or_cluster* c, const ke_pod* pod, int32_t node) {
     const int32_t id = c->cfg.fit.scalars[q];
     const int64_t v = pod_xres(pod, id);
     const ke_node_resource* r = node_xres(nd, id);
-    if (v > 0 && v > (r ? r->allocatable : 0) - (r ? r->requested : 0)) return KE_REASON_FIT_INSUFFICIENT_SCALAR;
+    if (v > 0 && v > (r ? r->allocatable : 0) - (r ? r->requested + nd->rv_x[id] : 0)) return KE_REASON_FIT_INSUFFICIENT_SCALAR;
   }
   return 0;
 }
@@ -3718,7 +3806,7 @@ static int64_t or_fit_score(const or_cluster* c, const ke_pod* pod, int32_t node
     const ke_node_resource* r = node_xres(nd, id);
     const int64_t alloc = r ? r->allocatable : 0;
     if (alloc == 0) continue;
-    const int64_t rv = id == KE_RES_CPU || id == KE_RES_MEMORY ? nd->rv_nz[id] : 0;
+    const int64_t rv = id == KE_RES_CPU || id == KE_RES_MEMORY ? nd->rv_nz[id] : nd->rv_x[id];
     const int64_t req = r->requested + rv + preq;
     const int64_t rs = a->strategy == KE_STRATEGY_MOST_ALLOCATED ? fp_most(req, alloc) : fp_least(req, alloc);
     node_score += rs * a->resources[q].weight;
@@ -4152,6 +4240,17 @@ int or_numa_reserve_from_rsv(or_cluster* c, const ke_pod* pod, int32_t node, con
   return r;
 }
 
+/* allRAllocated of node i: Σ allocated of its matched reservations, [cpu, memory, then KE_NRES + resource id] */
+#define PRW (KE_NRES + KE_MAX_XRES)
+static void or_all_allocated(const or_cluster* c, const char* m, int32_t i, int64_t* all) {
+  memset(all, 0, sizeof(int64_t) * PRW);
+  for (int32_t r = 0; r < c->n_resv; r++) {
+    if (!m[r] || c->resv[r].node != i) continue;
+    for (int k = 0; k < KE_NRES; k++) all[k] += c->resv[r].allocated[k];
+    for (int32_t e = c->rres ? c->roff[r] : 0; c->rres && e < c->roff[r + 1]; e++)
+      if (c->rres[e].id != KE_RSV_RES_PODS) all[KE_NRES + c->rres[e].id] += c->rres[e].allocated;
+  }
+}
 static int32_t or_resv_prescore(const or_cluster* c, const ke_pod* pod, const char* m, const int64_t* pod_requested,
                                 const uint8_t* feasible, int affinity, int64_t* raw, int32_t* nom) {
   const int32_t N = c->n;
@@ -4164,12 +4263,12 @@ static int32_t or_resv_prescore(const or_cluster* c, const ke_pod* pod, const ch
     nom[i] = -1;
     raw[i] = 0;
     if (!has[i]) continue;
-    int64_t all_alloc[KE_NRES] = {0, 0}, order = 0;
+    int64_t all_alloc[PRW], order = 0;
     int any = 0;
+    or_all_allocated(c, m, i, all_alloc);
     for (int32_t r = 0; r < c->n_resv; r++)
       if (m[r] && c->resv[r].node == i) {
         any = 1;
-        for (int k = 0; k < KE_NRES; k++) all_alloc[k] += c->resv[r].allocated[k];
         if (c->resv[r].order != 0 && (order == 0 || c->resv[r].order < order)) order = c->resv[r].order;
       }
     if (!any) continue;
@@ -4179,7 +4278,7 @@ static int32_t or_resv_prescore(const or_cluster* c, const ke_pod* pod, const ch
       if (!m[r] || c->resv[r].node != i) continue;
       n_matched++;
       only = r;
-      if (!or_resv_nominable(c, &c->resv[r], pod, i, &pod_requested[i * KE_NRES], all_alloc, affinity) ||
+      if (!or_resv_nominable(c, r, pod, i, &pod_requested[i * PRW], all_alloc, affinity) ||
           !or_numa_nominable(c, pod, i, r, affinity))
         continue;
       n_ok++;
@@ -4188,7 +4287,7 @@ static int32_t or_resv_prescore(const or_cluster* c, const ke_pod* pod, const ch
         bo = c->resv[r].order;
         by_order = r;
       }
-      const int64_t sc = or_reservation_score(&c->resv[r], pod);
+      const int64_t sc = or_reservation_score_idx(c, r, pod);
       if (sc > bsc) { /* sort.Slice by score desc; equal scores keep list order (insertion sort below 13) */
         bsc = sc;
         by_score = r;
@@ -4196,7 +4295,7 @@ static int32_t or_resv_prescore(const or_cluster* c, const ke_pod* pod, const ch
     }
     nom[i] = n_ok == 0 ? -1 : n_ok == 1 ? first : by_order >= 0 ? by_order : by_score;
     if (affinity && n_matched == 1) nom[i] = only; /* nominator.go:223-225 */
-    raw[i] = nom[i] >= 0 ? or_reservation_score(&c->resv[nom[i]], pod) : 0;
+    raw[i] = nom[i] >= 0 ? or_reservation_score_idx(c, nom[i], pod) : 0;
     if ((!feasible || feasible[i]) && order != 0 && (pref < 0 || order < po)) {
       po = order;
       pref = i;
@@ -4212,12 +4311,10 @@ static int32_t or_resv_prescore(const or_cluster* c, const ke_pod* pod, const ch
  * Restricted; resource names are not required to overlap with an affinity) */
 static int or_resv_filter_node(const or_cluster* c, const ke_pod* pod, const char* m, const int64_t* pod_requested,
                                int32_t i) {
-  int64_t all_alloc[KE_NRES] = {0, 0};
+  int64_t all_alloc[PRW];
+  or_all_allocated(c, m, i, all_alloc);
   for (int32_t r = 0; r < c->n_resv; r++)
-    if (m[r] && c->resv[r].node == i)
-      for (int k = 0; k < KE_NRES; k++) all_alloc[k] += c->resv[r].allocated[k];
-  for (int32_t r = 0; r < c->n_resv; r++)
-    if (m[r] && c->resv[r].node == i && or_resv_nominable(c, &c->resv[r], pod, i, &pod_requested[i * KE_NRES], all_alloc, 1))
+    if (m[r] && c->resv[r].node == i && or_resv_nominable(c, r, pod, i, &pod_requested[i * PRW], all_alloc, 1))
       return 1;
   return 0;
 }
@@ -4231,9 +4328,11 @@ static char* or_resv_begin(or_cluster* c, const int32_t* ids, int32_t n_ids, int
     if (or_resv_usable(&c->resv[ids[j]])) m[ids[j]] = 1;
   c->resv_m = m;
   or_restore(c, m, 0);
-  *pod_requested = (int64_t*)malloc(sizeof(int64_t) * KE_NRES * (size_t)(N > 0 ? N : 1));
-  for (int32_t i = 0; i < N; i++)
-    for (int k = 0; k < KE_NRES; k++) (*pod_requested)[i * KE_NRES + k] = c->nodes[i].node.requested[k] + c->nodes[i].rv_req[k];
+  *pod_requested = (int64_t*)malloc(sizeof(int64_t) * PRW * (size_t)(N > 0 ? N : 1));
+  for (int32_t i = 0; i < N; i++) {
+    for (int k = 0; k < KE_NRES; k++) (*pod_requested)[i * PRW + k] = c->nodes[i].node.requested[k] + c->nodes[i].rv_req[k];
+    for (int id = 0; id < KE_MAX_XRES; id++) (*pod_requested)[i * PRW + KE_NRES + id] = c->nodes[i].rv_x[id];
+  }
   or_restore(c, m, 1);
   return m;
 }
@@ -4249,6 +4348,39 @@ int32_t or_reservation_prescore(or_cluster* c, const ke_pod* pod, const int32_t*
   free(m);
   free(pr);
   return pref;
+}
+
+/* golden-vector entry point: filterWithReservations (reservation/plugin.go:351-442) over reservation r alone on
+ * `node`, with the cycle state a test gives directly: pod_requested[PRW] = nodeRState.podRequested (cpu, memory,
+ * then [KE_NRES + id] the scalars), r_allocated[PRW] = nodeRState.rAllocated; `required` =
+ * requiredFromReservation, `affinity` = state.hasAffinity.  Returns 0 = Success, 1 = Unschedulable with a node
+ * insufficiency ("... by node"), 2 = with a reservation reason ("Reservation(s) ..."), 3 = no reservation met. */
+int32_t or_rsv_filter_with(or_cluster* c, int32_t r, const ke_pod* pod, int32_t node, const int64_t* pod_requested,
+                           const int64_t* r_allocated, int32_t required, int32_t affinity) {
+  if (!required) return 0;
+  if (r < 0 || r >= c->n_resv || node < 0 || node >= c->n) return -1;
+  char* m = (char*)calloc((size_t)c->n_resv, 1);
+  m[r] = 1;
+  c->resv_m = m;
+  const ke_reservation* rv = &c->resv[r];
+  int shared = 0;
+  for (int k = 0; k < KE_NRES; k++)
+    if (rv->allocatable[k] != 0 && !((rv->names_excluded >> k) & 1) && pod->requests[k] != 0) shared = 1;
+  for (int32_t e = c->rres ? c->roff[r] : 0; c->rres && e < c->roff[r + 1]; e++)
+    if (!c->rres[e].excluded && c->rres[e].id != KE_RSV_RES_PODS && or_pod_request_of(pod, c->rres[e].id) != 0) shared = 1;
+  int32_t out = 3;
+  if (shared || affinity) {
+    /* the node part alone (a Default copy of the reservation), then the whole decision */
+    ke_reservation keep = *rv;
+    c->resv[r].allocate_policy = KE_RSV_POLICY_DEFAULT;
+    const int node_fits = or_resv_nominable(c, r, pod, node, pod_requested, r_allocated, 1);
+    c->resv[r] = keep;
+    const int fits = or_resv_nominable(c, r, pod, node, pod_requested, r_allocated, 1);
+    out = fits ? 0 : !node_fits ? 1 : 2;
+  }
+  c->resv_m = NULL;
+  free(m);
+  return out;
 }
 
 /* golden-vector entry point: the Reservation Filter with a reservation affinity on `node` (1 = passes) */
@@ -4344,7 +4476,9 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
     ds_pod d;
     ds_prepare_pod(c, &pods[p], &d);
     (void)node_bind;
-    int scalar = pods[p].has_other_requests || !d.skip; /* (batch / mid resources: fitsNode's xres only) */
+    /* every requested name beyond cpu / memory is read through its ke_pod.xres entry: a name without an id is
+     * refused (batch / mid resources included) */
+    int scalar = pods[p].has_other_requests > 1 || !d.skip;
     for (int r = 0; r < KE_PDR_COUNT; r++) scalar |= pods[p].device_requests[r] != 0;
     if (scalar) return KE_ERR_UNSUPPORTED;
     /* a pod with its own NUMA policy matching a reservation that holds NUMA resources / CPUs: its hints over the
@@ -4470,7 +4604,9 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
          * reservation_info.go:458-468): allocated += Mask(requests, ResourceNames), one more allocated pod */
         ke_reservation* r = &c->resv[nom[b]];
         for (int k = 0; k < KE_NRES; k++)
-          if (r->allocatable[k] != 0) r->allocated[k] += pods[p].requests[k];
+          if (r->allocatable[k] != 0 && !((r->names_excluded >> k) & 1)) r->allocated[k] += pods[p].requests[k];
+        for (int32_t e = c->rres ? c->roff[nom[b]] : 0; c->rres && e < c->roff[nom[b] + 1]; e++)
+          if (!c->rres[e].excluded && c->rres[e].id != KE_RSV_RES_PODS) c->rres[e].allocated += or_pod_request_of(&pods[p], c->rres[e].id);
         r->allocated_pods++;
         c->last_resv[p] = 1 + nom[b];
         or_owner_update(c, nom[b], &pods[p], rp.cpus, numa_alloc ? numa_alloc + (int64_t)p * 16 : NULL, mask, +1);
@@ -4521,7 +4657,14 @@ int or_pod_release(or_cluster* c, const ke_pod* pod, const ke_pod_allocation* a,
      * allocated = SubtractWithNonNegativeResult(allocated, Mask(requests, ResourceNames)) */
     ke_reservation* r = &c->resv[ridx];
     for (int k = 0; k < KE_NRES; k++)
-      if (r->allocatable[k] != 0) r->allocated[k] = r->allocated[k] - pod->requests[k] > 0 ? r->allocated[k] - pod->requests[k] : 0;
+      if (r->allocatable[k] != 0 && !((r->names_excluded >> k) & 1))
+        r->allocated[k] = r->allocated[k] - pod->requests[k] > 0 ? r->allocated[k] - pod->requests[k] : 0;
+    for (int32_t e = c->rres ? c->roff[ridx] : 0; c->rres && e < c->roff[ridx + 1]; e++) {
+      ke_reservation_resource* x = &c->rres[e];
+      if (x->excluded || x->id == KE_RSV_RES_PODS) continue;
+      const int64_t v = x->allocated - or_pod_request_of(pod, x->id);
+      x->allocated = v > 0 ? v : 0;
+    }
     if (r->allocated_pods > 0) r->allocated_pods--;
     or_owner_update(c, ridx, pod, a->cpuset, a->numa, a->device_minors, -1);
     or_restore(c, NULL, 0);

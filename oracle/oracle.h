@@ -48,6 +48,9 @@ int or_gpu_templates_load(or_cluster* c, int32_t n, const ke_gpu_template* t);
 int or_node_device_flags(or_cluster* c, int32_t node, int32_t secondary_well_planned, int32_t gpu_model_key);
 int or_reservations_load(or_cluster* c, int32_t n, const ke_reservation* r);
 int or_reservations_load_ex(or_cluster* c, int32_t n, const ke_reservation* r, const ke_reservation_alloc* allocs);
+int or_reservations_load_full(or_cluster* c, int32_t n, const ke_reservation* r, const ke_reservation_alloc* allocs,
+                              const int32_t* res_offsets, const ke_reservation_resource* res);
+int or_reservation_resources_get(const or_cluster* c, int32_t r, int32_t cap, ke_reservation_resource* out, int32_t* n);
 int or_reservation_allocs_get(const or_cluster* c, int32_t n, ke_reservation_alloc* out);
 /* RestoreReservation's state of reservation r as a matched reservation (golden entry, oracle.c) */
 typedef struct or_rsv_state {
@@ -70,6 +73,8 @@ int or_pod_reservations(or_cluster* c, int32_t n_pods, const int32_t* offsets, c
 int or_last_reservations(const or_cluster* c, int32_t n, int32_t* out);
 int64_t or_reservation_score(const ke_reservation* r, const ke_pod* pod);
 int32_t or_reservation_filter(or_cluster* c, const ke_pod* pod, const int32_t* ids, int32_t n_ids, int32_t node);
+int32_t or_rsv_filter_with(or_cluster* c, int32_t r, const ke_pod* pod, int32_t node, const int64_t* pod_requested,
+                           const int64_t* r_allocated, int32_t required, int32_t affinity);
 int32_t or_reservation_prescore(or_cluster* c, const ke_pod* pod, const int32_t* ids, int32_t n_ids, int64_t* raw,
                                 int32_t* nom);
 int or_node_info_requested(const or_cluster* c, int32_t node, int64_t* requested, int64_t* non_zero);

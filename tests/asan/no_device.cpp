@@ -15,6 +15,7 @@ int device_schedule(Context*, int32_t, const ke_pod*, int64_t, int32_t*, int32_t
 int device_rsv_result(Context*, int32_t*) { return none(); }
 int device_schedule_enqueue(Context*, int32_t, const ke_pod*, int64_t, bool, DevFinish*) { return none(); }
 void device_swap_call_buffers(Context*) {}
+void device_quiesce(Context*) {}
 bool device_refresh_pending(const Context*, int64_t) { return false; }
 bool device_async_ok(const Context*, int32_t) { return false; }
 int device_rsv_views(Context*, const ke_pod&, int64_t, const std::vector<RsvView>&, std::vector<RsvViewOut>&) {

@@ -346,7 +346,10 @@ def test_pod_device_annotations(lib):
                           gpu_partition_spec={"allocatePolicy": "Restricted", "ringBusBandwidth": "200Gi"},
                           device_hints={"gpu": {"requiredTopologyScope": "PCIe"}, "rdma": {"vfSelector": {}}},
                           device_joint_allocate={"deviceTypes": ["gpu", "rdma"]})
-    same(got, want, skip=("pod_key", "uid", "xres_request_mask", "n_xres", "xres_id", "xres_value"))
+    same(got, want, skip=("pod_key", "uid", "xres_request_mask", "n_xres", "xres_id", "xres_value", "has_other_requests"))
+    # without a resource-name table the device names have no id (2); with one (the model's interning) they do (1)
+    assert (got.has_other_requests, want.has_other_requests) == (2, 1)
+    assert decode.decode_pod(doc, ["cpu", "memory", "nvidia.com/gpu", "koordinator.sh/rdma"]).has_other_requests == 1
 
 
 # ---- Device -------------------------------------------------------------------------------------------------

@@ -96,3 +96,44 @@ def test_deviceshare_slice_runs_behind_the_calls_in_flight(gpu):
         c, s = ev.wait(t)
         assert np.array_equal(c, c0) and np.array_equal(s, s0)
     ev.close()
+
+
+def _records_equal(a, b):
+    for k in ("node", "cpuset", "numa", "device_minors", "vf_rank", "reservation", "quota_assigned"):
+        assert np.array_equal(a[k], b[k]), k
+
+
+def test_wait_switches_every_release_record(gpu):
+    """a plain slice A in flight, a DeviceShare slice B that runs at once (its device minors written),
+    then wait(A): A's release records carry A's nodes and no device minors of B; an Unreserve of an A pod releases
+    only what A reserved; wait(B) then switches to B's records, whose minors equal the oracle's (both twins keep the
+    same state throughout: dev rows, records, next queue)."""
+    from test_gpu_parity import ds_both
+    ev, o = ds_both(1200, 1311, abi.STRATEGY_LEAST_ALLOCATED)
+    qa = synth.make_pods(400, synth.BASE_SEED + 1312)
+    qb = synth.make_ds_pods(40, synth.BASE_SEED + 1313, key_base=6_200_000_000)
+    ta = ev.submit(qa, synth.T0)
+    tb = ev.submit(qb, synth.T0)  # completes A's device work, runs B at once
+    ca, _ = o.schedule(qa, synth.T0)
+    rec_a = o.last_allocations()
+    cb, _ = o.schedule(qb, synth.T0)  # (the device ran B at its submission)
+    rec_b = o.last_allocations()
+    ga, _ = ev.wait(ta)
+    assert np.array_equal(ga, ca)
+    got_a = ev.last_allocations(len(qa))
+    _records_equal(got_a, rec_a)
+    assert not got_a["device_minors"].any()
+    p = int(np.flatnonzero(ca >= 0)[3])
+    ev.unreserve(qa[p], p)  # A's record: the LoadAware / NodeInfo part only, no device minors of B's pod p
+    o.release(qa[p], rec_a[p])
+    gb, _ = ev.wait(tb)
+    assert np.array_equal(gb, cb)
+    _records_equal(ev.last_allocations(len(qb)), rec_b)
+    assert rec_b["device_minors"].any()
+    tail = synth.make_ds_pods(60, synth.BASE_SEED + 1314, key_base=6_300_000_000)
+    c1, s1 = ev.schedule(tail, synth.T0)
+    c0, s0 = o.schedule(tail, synth.T0)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    assert np.array_equal(ev.last_device_allocations, o.last_device_allocations)
+    assert ev.check_records(synth.T0) == 0
+    ev.close()

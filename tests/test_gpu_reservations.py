@@ -363,3 +363,109 @@ def test_matched_reservations_sharded_loopback(gpu, world, affinity):
     assert np.array_equal(a1["reservation"], o.last_allocations()["reservation"])
     assert (a1["reservation"] > 0).sum() >= 5
     ev.close()
+
+
+def _general_setup(n, seed, n_pods):
+    """Reservations whose allocatable names batch-cpu / batch-memory / ephemeral storage / nvidia.com/gpu and
+    "pods" besides cpu / memory (ke_reservations_load_full; resource ids of synth.XRES), some with a reserved part
+    (the node-reservation annotation) or names left out of a Restricted one's ResourceNames, their reserve pods in
+    NodeInfo (cpu / memory and the scalar rows); NodeResourcesFit (Filter + Score over the scalars) and FitPlus in
+    the profile; about half of the eligible pods (batch and scalar requests included) match a group."""
+    rng = np.random.default_rng(seed)
+    cl = synth.make_cluster(n, synth.BASE_SEED + seed, amplified_fraction=0.2)
+    tables = synth.make_node_resources(cl, synth.BASE_SEED + seed + 1)
+    rs, ents, grp = [], [], []
+    for g in range(8):
+        for _ in range(int(rng.integers(2, 6))):
+            node = int(rng.integers(0, n))
+            r = abi.Reservation(node=node, available=int(rng.random() < 0.95), allocate_once=int(rng.random() < 0.2),
+                                allocate_policy=int(rng.integers(0, 3)), allocated_pods=int(rng.choice([0, 0, 1, 2])),
+                                order=int(rng.choice([0, 0, 0, 5, 9])))
+            r.allocatable[0] = int(rng.choice([0, 2000, 4000, 8000]))
+            r.allocatable[1] = int(rng.choice([0, 4, 8, 16])) * 2**30
+            if r.allocated_pods:
+                r.allocated[0], r.allocated[1] = r.allocatable[0] // 2, r.allocatable[1] // 4
+            if rng.random() < 0.15:
+                r.reserved[0] = r.allocatable[0] // 4
+            if r.allocate_policy == abi.RSV_POLICY_RESTRICTED and rng.random() < 0.2:
+                r.names_excluded = 1 << int(rng.integers(0, 2))
+            e = []
+            for rid, lo, hi, unit in ((2, 1, 8, 1000), (3, 1, 16, 2**30), (4, 1, 20, 2**30), (5, 1, 4, 1)):
+                if rng.random() < 0.45:
+                    a = int(rng.integers(lo, hi + 1)) * unit
+                    al = int(rng.choice([0, a // 2, a])) if r.allocated_pods else 0
+                    e.append((rid, a, al, int(rng.random() < 0.1) * (a // 4), int(rng.random() < 0.1)))
+            if rng.random() < 0.2:
+                e.append((abi.RSV_RES_PODS, int(rng.integers(1, 4)), 0, 0, 0))
+            x = np.zeros(len(e), abi.RESERVATION_RESOURCE_DTYPE)
+            for q, (rid, a, al, rsv, exc) in enumerate(e):
+                x[q]["id"], x[q]["allocatable"], x[q]["allocated"], x[q]["reserved"], x[q]["excluded"] = rid, a, al, rsv, exc
+            if len(e):
+                r.holds |= abi.RSV_OTHER_ALLOCATABLE
+            # the reserve pod is in NodeInfo: cpu / memory, and its scalars in the node's rows
+            cl.nodes["requested"][node, 0] += r.allocatable[0]
+            cl.nodes["requested"][node, 1] += r.allocatable[1]
+            t = tables[node]
+            for rid, a, _, _, _ in e:
+                if rid == abi.RSV_RES_PODS:
+                    continue
+                hit = np.flatnonzero(t["id"] == rid)
+                if len(hit):
+                    t["requested"][hit[0]] += a
+                else:
+                    row = np.zeros(1, abi.NODE_RESOURCE_DTYPE)
+                    row["id"], row["allocatable"], row["requested"] = rid, 2 * a, a
+                    t = np.concatenate([t, row])
+            tables[node] = t
+            rs.append(r)
+            ents.append(x)
+            grp.append(g)
+    cfg = synth.fit_config(synth.ext_config(synth.config(n)))
+    ev, o = Evaluator(cfg), Oracle(cfg, n)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        synth.load_node_resources(h, tables)
+        h.reservations_load(rs, resources=ents)
+    pods = synth.add_pod_xres(synth.make_pods(n_pods, synth.BASE_SEED + seed + 2), synth.BASE_SEED + seed + 3)
+    cpuset = np.isin(pods["qos_class"], [abi.QOS_LSE, abi.QOS_LSR]) & (pods["priority_class"] == abi.PRIORITY_PROD)
+    elig = ((pods["numa_topology_policy"] == 0) & (pods["has_other_requests"] <= 1)
+            & (pods["device_requests"] == 0).all(1) & ~cpuset)
+    grp = np.asarray(grp)
+    matches = [[] for _ in range(n_pods)]
+    for p in np.flatnonzero(elig & (rng.random(n_pods) < 0.5)):
+        pods["reservation_matched"][p] = abi.RSV_AFFINITY if rng.random() < 0.15 else abi.RSV_MATCHED
+        matches[p] = np.flatnonzero(grp == rng.integers(0, 8)).tolist()
+    return ev, o, pods, matches, rs
+
+
+def test_general_reservation_resources_parity(gpu):
+    """Reservations naming resources beyond cpu / memory (VERDICT r5 missing 2): the scalar NodeInfo restore every pod
+    sees (NodeResourcesFit's Filter / Score and FitPlus rows), and for matched pods the name check, fitsNode's scalars,
+    fitsReservation's pods cap / reserved / ResourceNames, scoreReservation over every name, Reserve's allocated per
+    name -- bit-exact with the oracle on placements, totals and reservation state; then Unreserve and a second queue."""
+    ev, o, pods, matches, rs = _general_setup(300, 1361, 240)
+    assert sum(1 for m in matches if m) > 40
+    c1, s1 = ev.schedule(pods, synth.T0, matches=matches)
+    c0, s0 = o.schedule(pods, synth.T0, matches=matches)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5].ravel().tolist()
+    assert np.array_equal(s1, s0)
+    _resv_equal(ev, o)
+    for i in range(len(rs)):
+        a, b = ev.reservation_resources_get(i), o.reservation_resources_get(i)
+        assert np.array_equal(a["allocated"], b["allocated"]), i
+    assert any((ev.reservation_resources_get(i)["allocated"] > 0).any() for i in range(len(rs)))
+    rec, rec0 = ev.last_allocations(), o.last_allocations()
+    assert np.array_equal(rec["reservation"], rec0["reservation"]) and (rec["reservation"] > 0).sum() > 5
+    for p in np.flatnonzero(rec["reservation"] > 0)[::3]:
+        ev.release(pods[p], rec[p])
+        o.release(pods[p], rec0[p])
+    _resv_equal(ev, o)
+    for i in range(len(rs)):
+        assert np.array_equal(ev.reservation_resources_get(i)["allocated"], o.reservation_resources_get(i)["allocated"])
+    more = synth.add_pod_xres(synth.make_pods(120, synth.BASE_SEED + 1365, key_base=9_950_000_000),
+                              synth.BASE_SEED + 1366)
+    c1, s1 = ev.schedule(more, synth.T0)
+    c0, s0 = o.schedule(more, synth.T0)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    assert ev.check_records(synth.T0) == 0
+    ev.close()

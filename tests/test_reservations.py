@@ -128,7 +128,7 @@ def test_matched_pod_checks():
         ev.schedule(pods, synth.T0)  # an affinity pod needs its (possibly empty) list staged
     assert e.value.code == abi.ERR_INVALID
     pods["reservation_matched"][1] = abi.RSV_MATCHED
-    pods["has_other_requests"][1] = 1  # a resource outside the ABI's names
+    pods["has_other_requests"][1] = 2  # a requested name without a resource id
     with pytest.raises(KoordEvalError) as e:
         ev.schedule(pods, synth.T0, matches=[[], [0]])
     assert e.value.code == abi.ERR_UNSUPPORTED
@@ -417,3 +417,105 @@ def test_fits_node_checks_the_pods_other_resources():
         assert c.tolist() == [0]
         assert o.last_allocations()["reservation"].tolist() == [into]
         assert (s[0] >= 5000) == bool(into)
+
+
+GENERAL_FILTER_CASES = json.load(open(os.path.join(HERE, "golden", "reservation_filters_general.json")))["cases"]
+
+
+def _pod_with(requests, scalars):
+    pod = synth.make_pods(1, synth.BASE_SEED + 907)
+    pod["requests"][0][:] = 0
+    pod["requests"][0][:2] = requests
+    pod["n_xres"][0] = len(scalars)
+    for e, (k, v) in enumerate(sorted(scalars.items())):
+        pod["xres_id"][0][e], pod["xres_value"][0][e] = int(k), v
+    pod["reservation_matched"][0] = abi.RSV_AFFINITY
+    return pod
+
+
+def _reservation(d, node=0):
+    r = abi.Reservation(node=node, available=1, allocate_policy=d["policy"], allocated_pods=d["allocated_pods"])
+    for k in range(abi.NRES):
+        r.allocatable[k], r.allocated[k], r.reserved[k] = d["allocatable"][k], d["allocated"][k], d["reserved"][k]
+    ents = np.zeros(len(d["entries"]), abi.RESERVATION_RESOURCE_DTYPE)
+    for e, x in enumerate(d["entries"]):
+        ents[e]["id"], ents[e]["allocatable"], ents[e]["allocated"] = x["id"], x["allocatable"], x["allocated"]
+        ents[e]["reserved"] = x["reserved"]
+    if len(ents):
+        r.holds |= abi.RSV_OTHER_ALLOCATABLE
+    return r, ents
+
+
+@pytest.mark.parametrize("case", GENERAL_FILTER_CASES, ids=[c["name"] for c in GENERAL_FILTER_CASES])
+def test_reservation_filter_general_golden(case):
+    """filterWithReservations over a reservation's allocatable beyond cpu / memory (the pods cap, reserved, batch
+    scalar requests) in the oracle, against Test_filterWithReservations (tests/golden/make_rsv_general_fixtures.py)."""
+    cfg = synth.config(1)
+    o = Oracle(cfg, 1)
+    node = abi.Node()
+    for k in range(abi.NRES):
+        node.allocatable[k] = case["node"]["allocatable"][k]
+        node.raw_allocatable[k] = abi.ABSENT
+        node.custom_usage_thresholds[k] = node.custom_prod_usage_thresholds[k] = abi.ABSENT
+        node.custom_agg_thresholds[k] = abi.ABSENT
+    node.allowed_pods = case["node"]["allowed_pods"]
+    node.pod_count = 1  # the matched reserve pod (removed by restoreMatchedReservation: len(Pods) = 0)
+    node.cpu_amplification_ratio = -1.0
+    node.nrt_cpu_amplification_ratio = -2.0
+    o.upsert_node(0, node)
+    res = np.zeros(len(case["node"]["scalars"]), abi.NODE_RESOURCE_DTYPE)
+    for e, (k, v) in enumerate(sorted(case["node"]["scalars"].items())):
+        res[e]["id"], res[e]["allocatable"] = int(k), v
+    o.set_resources(0, res)
+    r, ents = _reservation(case["reservation"])
+    o.reservations_load([r], resources=[ents])
+    pod = _pod_with(case["pod"]["requests"], case["pod"]["scalars"])
+    pr = {int(k): v for k, v in case["pod_requested"].items()}
+    ra = {int(k): v for k, v in case["r_allocated"].items()}
+    assert o.rsv_filter_with(0, pod[0], 0, pr, ra, case["required"], case["affinity"]) == case["want"]
+
+
+def test_general_reservation_load_rules():
+    """ke_reservations_load_full: KE_RSV_OTHER_ALLOCATABLE must agree with the entries, ids are resource ids other
+    than cpu / memory (or the pods entry), distinct, with a positive allocatable; the old entry points refuse a
+    reservation naming other resources (KE_ERR_UNSUPPORTED); the entries come back with
+    ke_reservation_resources_get -- the product and the oracle alike."""
+    cl = synth.make_cluster(20, synth.BASE_SEED + 1351)
+    ev, o = Evaluator(synth.config(20)), Oracle(synth.config(20), 20)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+    r, _ = _reservation(dict(R6_GENERAL))
+    ents = np.zeros(2, abi.RESERVATION_RESOURCE_DTYPE)
+    ents["id"] = [5, abi.RSV_RES_PODS]
+    ents["allocatable"] = [4, 3]
+    ok = abi.Reservation.from_buffer_copy(r)
+    ok.holds |= abi.RSV_OTHER_ALLOCATABLE
+    for h in (ev, o):
+        h.reservations_load([ok], resources=[ents])
+        got = h.reservation_resources_get(0)
+        assert list(got["id"]) == [5, abi.RSV_RES_PODS] and list(got["allocatable"]) == [4, 3]
+    bad_cases = [
+        ([r], [ents], abi.ERR_INVALID),                 # entries without the bit
+        ([ok], [ents[:0]], abi.ERR_INVALID),            # the bit without entries
+        ([ok], [np.concatenate([ents, ents[:1]])], abi.ERR_INVALID),  # duplicate id
+    ]
+    cpu = ents.copy()
+    cpu["id"][0] = abi.XRES_CPU
+    bad_cases.append(([ok], [cpu], abi.ERR_INVALID))   # cpu goes in ke_reservation
+    zero = ents.copy()
+    zero["allocatable"][0] = 0
+    bad_cases.append(([ok], [zero], abi.ERR_INVALID))
+    for rs, rsc, code in bad_cases:
+        with pytest.raises(KoordEvalError) as e:
+            ev.reservations_load(rs, resources=rsc)
+        assert e.value.code == code
+        with pytest.raises(RuntimeError):
+            o.reservations_load(rs, resources=rsc)
+    with pytest.raises(KoordEvalError) as e:  # named resources without their entries
+        ev.reservations_load([ok])
+    assert e.value.code == abi.ERR_UNSUPPORTED
+    ev.close()
+
+
+R6_GENERAL = {"policy": 0, "allocatable": [6000, 8 << 30], "allocated": [0, 0], "reserved": [0, 0],
+              "allocated_pods": 0, "entries": []}
