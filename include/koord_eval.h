@@ -209,6 +209,9 @@ typedef struct ke_numa_args {
 #define KE_REASON_RSV_INSUFFICIENT_CPUS 50 /* a pod with a reservation affinity whose matched reservations holding a
                                               cpuset / NUMA resources satisfy none (tryAllocateFromReservation,
                                               nodenumaresource/reservation.go:420-422: "Reservation(s) ...") */
+#define KE_REASON_RSV_INSUFFICIENT_DEVICES 51 /* a DeviceShare pod with a reservation affinity whose matched
+                                                 reservations holding devices satisfy none (tryAllocateFromReservation,
+                                                 deviceshare/reservation.go:283-285: "Reservation(s) Insufficient ...") */
 
 /* One logical CPU of a node: CPUTopology.CPUDetails (cpu_topology.go:24-105, built from the NRT's
  * CPU topology, topology_options.go:90-164) + NodeAllocation.allocatedCPUs (node_allocation.go:33-41)

@@ -85,6 +85,7 @@ def load():
         "or_last_vf_ranks": (C.c_int, [V, i32, V]),
         "or_ds_allocate": (C.c_int, [V, C.POINTER(abi.Pod), i32, i32, i32, V, V, V]),
         "or_ds_score_device": (i64, [V, i32, V, V, V, V, V, V]),
+        "or_ds_rsv_direct": (i32, [V, C.POINTER(abi.Pod), i32, i32, V, V, V, V, V, i32, i32, i32, i32, V, V, V]),
         "or_normalize_scores": (None, [V, i32]),
         "or_topology_merge": (C.c_int, [i32, C.c_uint32, i32, V, V, V, V, V, V, V, V, V]),
         "or_node_numa_set": (C.c_int, [V, i32, i32, V]),
@@ -396,6 +397,26 @@ class Oracle:
                                      abi.ptr(reason))
         return st, int(reason[0]), out, vf
 
+    def ds_rsv_direct(self, pod, node, matched, basic, m_alloc, m_allocd, mode=0, required=False, ignored=False,
+                      scored=False):
+        """DeviceShare's reservation restore state given directly (golden vectors of
+        deviceshare/reservation_test.go:225 and scoring_test.go:670): matched = [(policy, allocatable, allocated,
+        remained)], each deviceResources map {type: {minor: {key: value}}}.  mode 0 -> (code, reason, minors per type);
+        mode 1 -> scoreWithReservation of entry 0."""
+        n = len(matched)
+        pol = np.array([m[0] for m in matched] or [0], dtype=np.int32)
+        mm = np.concatenate([pack_dres(x) for m in matched for x in m[1:]]) if n else np.zeros(192, np.int64)
+        out = np.zeros(3, np.uint32)
+        score = np.zeros(1, np.int64)
+        reason = np.zeros(1, np.int32)
+        b, ma, md = pack_dres(basic), pack_dres(m_alloc), pack_dres(m_allocd)  # alive across the call
+        code = self.lib.or_ds_rsv_direct(self.h, C.byref(pod), int(node), n, abi.ptr(pol), abi.ptr(mm),
+                                         abi.ptr(b), abi.ptr(ma), abi.ptr(md), int(mode), int(required), int(ignored),
+                                         int(scored), abi.ptr(out), abi.ptr(score), abi.ptr(reason))
+        if mode == 1:
+            return int(score[0])
+        return int(code), int(reason[0]), [int(x) for x in out]
+
     def ds_score_device(self, dev_type, req, total, free):
         """each argument: (values[3], has[3])"""
         arrs = [np.ascontiguousarray(x, dtype) for pair in (req, total, free) for x, dtype in
@@ -517,6 +538,19 @@ def _quota_state(fn, h, q):
     if rc != 0:
         raise RuntimeError(f"quota state rc={rc}")
     return {"limit": limit, "limit_has": has.astype(bool), "used": used, "np_used": npu}
+
+
+def pack_dres(d):
+    """deviceResources per type -> the 192 int64 or_ds_rsv_direct reads: [type][minor][key 0..2, flags] (flags bit k:
+    key k present, bit 3: the minor is in the map)"""
+    w = np.zeros((abi.DEV_TYPES, 16, 4), np.int64)
+    for t, minors in (d or {}).items():
+        for m, keys in minors.items():
+            w[t, m, 3] |= 8
+            for k, v in keys.items():
+                w[t, m, k] = v
+                w[t, m, 3] |= 1 << k
+    return w.reshape(-1)
 
 
 def normalize_scores(scores):

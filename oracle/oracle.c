@@ -113,6 +113,7 @@ struct or_cluster {
   ke_reservation_alloc* ralloc; /* the reservations' NUMA / cpuset / device holdings (NULL: none) */
   const char* resv_m;           /* the matched flags of the pod being evaluated (or_resv_begin), NULL = none */
   int ignored;                  /* the pod being evaluated / reserved is reservation-ignored (or_numa_ignored) */
+  const int32_t* ds_nom;        /* per node the reservation nominated for the pod being scored / reserved (or NULL) */
   uint8_t* rcpu;                /* [reservation][cpu] owner counts (or_owner_update), NULL until first needed */
   int32_t n_resv;
   /* each reservation's allocatable entries beyond cpu / memory (or_reservations_load_full): roff[i] .. roff[i+1] */
@@ -1733,9 +1734,9 @@ static rl rl_sub_nonneg(rl a, rl b, int nk) {
       int64_t q = a.v[k] - (b.has[k] ? b.v[k] : 0);
       r.has[k] = 1;
       r.v[k] = q > 0 ? q : 0;
-    } else if (b.has[k]) {
+    } else if (b.has[k]) { /* a key only in b: zero */
       r.has[k] = 1;
-      r.v[k] = -b.v[k] > 0 ? -b.v[k] : 0;
+      r.v[k] = 0;
     }
   }
   return r;
@@ -1982,6 +1983,24 @@ static int sel_matches(const ke_label_selector* s, const ke_labels* l) {
   return 1;
 }
 
+/* deviceResources of every device type (map[DeviceType]map[minor]ResourceList): in[t] bit m = minor m present */
+typedef struct ds_dres {
+  uint16_t in[KE_DEV_TYPES];
+  rl r[KE_DEV_TYPES][KE_MAX_MINORS];
+} ds_dres;
+/* The allocator's arguments beyond the node's cache when DeviceShare allocates for a reservation-matched pod
+ * (AutopilotAllocator.Allocate / score, device_allocator.go:96-138,469-492): the whole preemptible map
+ * (calcFreeWithPreemptible, device_cache.go:322-348), requiredDeviceResources (has_req; per type restricted when the
+ * type has minors, :350-362), and defaultAllocateDevices' required / preferred minors (:364-382).  NULL: the plain
+ * path (preemptible = the node's mergedUnmatchedUsed, nd->rs_dev). */
+typedef struct ds_rview {
+  ds_dres pre;
+  int has_req;
+  ds_dres req;
+  uint16_t required[KE_DEV_TYPES], preferred[KE_DEV_TYPES];
+} ds_rview;
+static __thread const ds_rview* g_rv = NULL;
+
 /* one device type of a node's cache: minors in ascending order */
 typedef struct ds_view {
   int n;
@@ -2060,14 +2079,41 @@ static void ds_filtered_view_aff(const or_node* nd, const ds_pod* d, int t, ds_a
    * (mergedFreeDevices; the others keep deviceFree) */
   for (int i = 0; i < v->n; i++) {
     const int m = v->minor[i];
-    if (!nd->rs_dev_has[t][m]) continue;
     rl pre = rl_empty();
-    for (int k = 0; k < nk; k++) {
-      pre.has[k] = nd->rs_dev_key[t][m][k];
-      pre.v[k] = nd->rs_dev[t][m][k];
+    if (g_rv) { /* the reservation path's preemptible map replaces the node's */
+      if (!((g_rv->pre.in[t] >> m) & 1u)) continue;
+      pre = g_rv->pre.r[t][m];
+    } else {
+      if (!nd->rs_dev_has[t][m]) continue;
+      for (int k = 0; k < nk; k++) {
+        pre.has[k] = nd->rs_dev_key[t][m][k];
+        pre.v[k] = nd->rs_dev[t][m][k];
+      }
     }
     const rl remaining = rl_sub_nonneg(v->total[i], rl_sub_nonneg(v->used[i], pre, nk), nk);
     if (!rl_is_zero(remaining, nk)) v->free[i] = remaining;
+  }
+  /* requiredDeviceResources of the type (a Restricted reservation): only its minors, free = MinResourceList(free,
+   * required) -- the keys of both, the smaller value (pkg/util/resource.go:64-78) */
+  if (g_rv && g_rv->has_req && g_rv->req.in[t]) {
+    int n = 0;
+    for (int i = 0; i < v->n; i++) {
+      const int m = v->minor[i];
+      if (!((g_rv->req.in[t] >> m) & 1u)) continue;
+      const rl q = g_rv->req.r[t][m];
+      rl f = rl_empty();
+      for (int k = 0; k < nk; k++)
+        if (v->free[i].has[k] && q.has[k]) {
+          f.has[k] = 1;
+          f.v[k] = v->free[i].v[k] < q.v[k] ? v->free[i].v[k] : q.v[k];
+        }
+      v->minor[n] = m;
+      v->total[n] = v->total[i];
+      v->used[n] = v->used[i];
+      v->free[n] = f;
+      n++;
+    }
+    v->n = n;
   }
   int all_zero = 1;
   for (int i = 0; i < v->n; i++)
@@ -2196,11 +2242,14 @@ static int ds_allocate_x(const or_node* nd, const ds_pod* d, const ke_deviceshar
   if (!v->present) return 0;
   int order[KE_MAX_MINORS], pf[KE_MAX_MINORS];
   int64_t sc[KE_MAX_MINORS];
+  const uint16_t rpref = g_rv ? g_rv->preferred[t] : 0, rreq = g_rv ? g_rv->required[t] : 0;
   for (int i = 0; i < v->n; i++) {
     order[i] = i;
     sc[i] = scorer ? ds_score_device(scorer, t, req, &v->total[i], &v->free[i]) : 0;
     const ke_device* dv = nd ? dev_of(nd, t, v->minor[i]) : NULL;
     pf[i] = pref && dv && dv->has_topology && dv->pcie_rank >= 0 && dv->pcie_rank < 64 && ((pref >> dv->pcie_rank) & 1);
+    /* sortDeviceResourcesByMinor with a non-empty preferred set overwrites the PCIe flags (device_resources.go:187-193) */
+    if (rpref) pf[i] = (rpref >> v->minor[i]) & 1u;
   }
   for (int i = 1; i < v->n; i++) /* insertion sort: preferred, score desc, minor asc */
     for (int j = i; j > 0; j--) {
@@ -2214,6 +2263,7 @@ static int ds_allocate_x(const or_node* nd, const ds_pod* d, const ke_deviceshar
   int n = 0;
   for (int i = 0; i < v->n && n < max_count; i++) {
     const int k = order[i];
+    if (rreq && !((rreq >> v->minor[k]) & 1u)) continue; /* required.Len() > 0 && !required.Has(minor) */
     if (rl_is_zero(v->free[k], nk)) continue;
     if (!rl_leq(*req, v->free[k], nk)) continue;
     int r = -1;
@@ -2690,6 +2740,313 @@ static int ds_autopilot(const or_cluster* c, const or_node* nd, const ds_pod* d,
   return 0;
 }
 
+/* ---- DeviceShare allocate-from-reservation (deviceshare/reservation.go:35-450) ---------------------------------- */
+/* nodeReservationRestoreStateData of one node for the pod being scheduled: RestoreReservation's matched list (the
+ * usable matched reservations whose reserve pod holds device instances, in reservation index order), each with
+ * allocatable = nd.getUsed(reservePod), allocated = the owners' usage on those instances (appendAllocatedByHints),
+ * remained = subtractAllocated(copy(allocatable), allocated, false); mergeReservationAllocations' sums; and the
+ * basicPreemptible the plugin starts from (mergedUnmatchedUsed + the node's preemptible of preemption -- the latter
+ * only in golden tests). */
+#define DS_MAX_MATCHED 32
+typedef struct ds_ralloc {
+  int32_t r;      /* reservation index (-1 in golden tests) */
+  int32_t policy; /* KE_RSV_POLICY_* */
+  ds_dres allocatable, allocated, remained;
+} ds_ralloc;
+typedef struct ds_rstate {
+  int n;
+  ds_ralloc m[DS_MAX_MATCHED];
+  ds_dres basic, matched_allocatable, matched_allocated;
+} ds_rstate;
+
+/* deviceResources.append (device_resources.go:47-63) of one instance: util.AddResourceList (keys of both, summed) */
+static void dres_add(ds_dres* d, int t, int m, rl x) {
+  if ((d->in[t] >> m) & 1u) {
+    d->r[t][m] = rl_add(d->r[t][m], x, nkeys(t));
+  } else {
+    d->in[t] |= (uint16_t)(1u << m);
+    d->r[t][m] = x;
+  }
+}
+/* appendAllocated(dst, src) (device_resources.go:116-132) */
+static void dres_append(ds_dres* d, const ds_dres* src) {
+  for (int t = 0; t < KE_DEV_TYPES; t++)
+    for (int m = 0; m < KE_MAX_MINORS; m++)
+      if ((src->in[t] >> m) & 1u) dres_add(d, t, m, src->r[t][m]);
+}
+/* quotav1.Subtract: the keys of both, a - b (may go negative) */
+static rl rl_sub(rl a, rl b, int nk) {
+  rl r = rl_empty();
+  for (int k = 0; k < nk; k++) {
+    r.has[k] = a.has[k] || b.has[k];
+    r.v[k] = (a.has[k] ? a.v[k] : 0) - (b.has[k] ? b.v[k] : 0);
+  }
+  return r;
+}
+
+/* the preemptible / required / preferred the allocator gets for matched reservation `idx` (tryAllocateFromReservation,
+ * reservation.go:229-280 and scoreWithReservation :323-345): preemptible = basicPreemptible + mergedMatchedAllocated +
+ * remained (+ preemptibleInRR, empty: no preemption); preferred = the reservation's minors; Restricted: required =
+ * preferred and requiredDeviceResources = calcRequiredDeviceResources (:347-366) -- remained by the reservation's
+ * minors, or, with nothing remained, every reservation minor with an empty list.  idx = -1: the node's own
+ * allocation (Filter / Score / Reserve fallback): basicPreemptible + mergedMatchedAllocatable.  idx = -2:
+ * tryAllocateIgnoreReservation (:290-310): Σ remained + basicPreemptible + mergedMatchedAllocated. */
+static void ds_view_of(const ds_rstate* st, int idx, ds_rview* v) {
+  memset(v, 0, sizeof *v);
+  if (idx == -1) {
+    dres_append(&v->pre, &st->basic);
+    dres_append(&v->pre, &st->matched_allocatable);
+    return;
+  }
+  if (idx == -2) {
+    for (int i = 0; i < st->n; i++) dres_append(&v->pre, &st->m[i].remained);
+    dres_append(&v->pre, &st->basic);
+    dres_append(&v->pre, &st->matched_allocated);
+    return;
+  }
+  const ds_ralloc* a = &st->m[idx];
+  dres_append(&v->pre, &st->basic);
+  dres_append(&v->pre, &st->matched_allocated);
+  dres_append(&v->pre, &a->remained);
+  for (int t = 0; t < KE_DEV_TYPES; t++) v->preferred[t] = a->allocatable.in[t];
+  if (a->policy == KE_RSV_POLICY_RESTRICTED) {
+    v->has_req = 1;
+    int any = 0;
+    for (int t = 0; t < KE_DEV_TYPES; t++) {
+      v->required[t] = a->allocatable.in[t];
+      v->req.in[t] = a->allocatable.in[t] ? (uint16_t)(a->remained.in[t] & a->allocatable.in[t]) : 0;
+      for (int m = 0; m < KE_MAX_MINORS; m++)
+        if ((v->req.in[t] >> m) & 1u) v->req.r[t][m] = a->remained.r[t][m];
+      any |= v->req.in[t] != 0;
+    }
+    if (!any) /* no resources left: every reservation minor with an empty list */
+      for (int t = 0; t < KE_DEV_TYPES; t++) {
+        v->req.in[t] = a->allocatable.in[t];
+        for (int m = 0; m < KE_MAX_MINORS; m++) v->req.r[t][m] = rl_empty();
+      }
+  }
+}
+
+static int or_resv_usable(const ke_reservation* r);
+/* the owners' part of reservation alloc a that RestoreReservation reads: the instances the reserve pod holds,
+ * each with the keys of a non-zero owner amount */
+static void ds_rsv_parts(const ke_reservation_alloc* a, ds_dres* allocatable, ds_dres* allocated) {
+  memset(allocatable, 0, sizeof *allocatable);
+  memset(allocated, 0, sizeof *allocated);
+  for (int t = 0; t < KE_DEV_TYPES; t++) {
+    const int nk = nkeys(t);
+    for (int m = 0; m < KE_MAX_MINORS; m++) {
+      const uint64_t bit = 1ull << (16 * t + m);
+      if (!(a->device_minors & bit)) continue;
+      rl al = rl_empty(), ow = rl_empty();
+      for (int k = 0; k < nk; k++) {
+        al.has[k] = a->device[t][m][k] != 0;
+        al.v[k] = a->device[t][m][k];
+        ow.has[k] = a->owner_device[t][m][k] != 0;
+        ow.v[k] = a->owner_device[t][m][k];
+      }
+      dres_add(allocatable, t, m, al);
+      if ((a->owner_device_minors & bit) && !rl_is_zero(ow, nk)) dres_add(allocated, t, m, ow);
+    }
+  }
+}
+/* remained = subtractAllocated(copy(allocatable), allocated, false): quotav1.Subtract per allocated instance, an
+ * instance deleted when the result IsZero */
+static void ds_remained(const ds_dres* allocatable, const ds_dres* allocated, ds_dres* remained) {
+  *remained = *allocatable;
+  for (int t = 0; t < KE_DEV_TYPES; t++)
+    for (int m = 0; m < KE_MAX_MINORS; m++) {
+      if (!((allocated->in[t] >> m) & 1u)) continue;
+      const rl x = rl_sub(((remained->in[t] >> m) & 1u) ? remained->r[t][m] : rl_empty(), allocated->r[t][m], nkeys(t));
+      if (rl_is_zero(x, nkeys(t))) {
+        remained->in[t] &= (uint16_t)~(1u << m);
+      } else {
+        remained->in[t] |= (uint16_t)(1u << m);
+        remained->r[t][m] = x;
+      }
+    }
+}
+/* the restore state of `node` for a pod whose matched reservations are flagged in m[] (NULL: none) -- from the
+ * holdings, as RestoreReservation + mergeReservationAllocations build it (reservation.go:99-195) */
+static void ds_rstate_build(const or_cluster* c, int32_t node, const char* mflags, ds_rstate* st) {
+  memset(st, 0, sizeof *st);
+  if (!c->ralloc) return;
+  for (int32_t i = 0; i < c->n_resv; i++) {
+    const ke_reservation* r = &c->resv[i];
+    if (r->node != node || !or_resv_usable(r) || !c->ralloc[i].device_minors) continue;
+    const int matched = mflags && mflags[i];
+    if (!matched && r->allocated_pods == 0) continue; /* an unmatched one restores only with allocated pods */
+    ds_dres al, ow, rem;
+    ds_rsv_parts(&c->ralloc[i], &al, &ow);
+    ds_remained(&al, &ow, &rem);
+    if (matched) {
+      if (st->n >= DS_MAX_MATCHED) continue;
+      ds_ralloc* a = &st->m[st->n++];
+      a->r = i;
+      a->policy = r->allocate_policy;
+      a->allocatable = al;
+      a->allocated = ow;
+      a->remained = rem;
+      dres_append(&st->matched_allocatable, &al);
+      dres_append(&st->matched_allocated, &ow);
+    } else { /* mergedUnmatchedUsed += subtractAllocated(copy(allocatable), remained, true) */
+      ds_dres used = al;
+      for (int t = 0; t < KE_DEV_TYPES; t++)
+        for (int mm = 0; mm < KE_MAX_MINORS; mm++) {
+          if (!((rem.in[t] >> mm) & 1u)) continue;
+          const rl x = rl_sub_nonneg(((used.in[t] >> mm) & 1u) ? used.r[t][mm] : rl_empty(), rem.r[t][mm], nkeys(t));
+          if (rl_is_zero(x, nkeys(t))) used.in[t] &= (uint16_t)~(1u << mm);
+          else used.in[t] |= (uint16_t)(1u << mm), used.r[t][mm] = x;
+        }
+      dres_append(&st->basic, &used);
+    }
+  }
+}
+static int ds_rsv_find(const ds_rstate* st, int32_t r) {
+  for (int i = 0; i < st->n; i++)
+    if (st->m[i].r == r) return i;
+  return -1;
+}
+
+static int ds_autopilot(const or_cluster* c, const or_node* nd, const ds_pod* d, ds_aff a,
+                        const ke_deviceshare_args* scorer, int reserve, uint32_t* out, int8_t (*vf)[KE_MAX_MINORS],
+                        int* reason);
+/* AutopilotAllocator.Allocate under view v */
+static int ds_autopilot_view(const or_cluster* c, const or_node* nd, const ds_pod* d, const ds_rview* v,
+                             const ke_deviceshare_args* scorer, int reserve, uint32_t* out, int8_t (*vf)[KE_MAX_MINORS],
+                             int* reason) {
+  const ds_rview* keep = g_rv;
+  g_rv = v;
+  const int st = ds_autopilot(c, nd, d, NO_AFF, scorer, reserve, out, vf, reason);
+  g_rv = keep;
+  return st;
+}
+/* tryAllocateFromReservation (reservation.go:207-287) over the matched list (only >= 0: that entry alone): 1 = a
+ * reservation satisfied the pod (out = the allocation), 0 = none satisfied and not required (nil result), -1 =
+ * Unschedulable "Reservation(s) ..." (required).  A reservation-ignored pod: tryAllocateIgnoreReservation's status. */
+static int ds_from_rsv(const or_cluster* c, const or_node* nd, const ds_pod* d, const ds_rstate* st, int only,
+                       int required, int ignored, const ke_deviceshare_args* scorer, int reserve, uint32_t* out,
+                       int8_t (*vf)[KE_MAX_MINORS], int* reason) {
+  (void)ignored;
+  if (st->n == 0) return 0;
+  ds_rview v;
+  for (int i = 0; i < st->n; i++) {
+    if (only >= 0 && i != only) continue;
+    ds_view_of(st, i, &v);
+    int why = 0;
+    if (ds_autopilot_view(c, nd, d, &v, scorer, reserve, out, vf, &why) == KE_CODE_SUCCESS) return 1;
+  }
+  for (int t = 0; t < KE_DEV_TYPES; t++) out[t] = 0;
+  if (required) {
+    *reason = KE_REASON_RSV_INSUFFICIENT_DEVICES;
+    return -1;
+  }
+  return 0;
+}
+/* AutopilotAllocator.score (device_allocator.go:469-492) under view v: Σ scoreNode over the requested types the
+ * filtered nodeDevice keeps; a Prepare error scores 0 */
+static int64_t ds_score_view(const or_cluster* c, const or_node* nd, const ds_pod* d, const ds_rview* v) {
+  int inc[KE_DEV_TYPES], cnt[KE_DEV_TYPES], why = 0;
+  if (ds_node_prepare(nd, d, 0, inc, cnt, &why)) return 0;
+  const ds_rview* keep = g_rv;
+  g_rv = v;
+  int64_t s = 0;
+  for (int t = 0; t < KE_DEV_TYPES; t++) {
+    if (!inc[t]) continue;
+    ds_view dv;
+    ds_filtered_view_aff(nd, d, t, NO_AFF, &dv);
+    if (dv.present && dv.n > 0) s += ds_score_node(&c->cfg.deviceshare, t, &d->req[t], &dv);
+  }
+  g_rv = keep;
+  return s;
+}
+/* scoreWithReservation / ScoreReservation of matched entry i (scoring.go:113-153, reservation.go:323-345); -1: the
+ * node's own (Score's fallback, scoring.go:96-102) */
+static int64_t ds_rsv_score(const or_cluster* c, const or_node* nd, const ds_pod* d, const ds_rstate* st, int i) {
+  ds_rview v;
+  ds_view_of(st, i, &v);
+  return ds_score_view(c, nd, d, &v);
+}
+/* golden-vector entry point (Test_tryAllocateFromReservation, deviceshare/reservation_test.go:225-888;
+ * TestScoreReservation, scoring_test.go:670-1240): the restore state given directly.  Each deviceResources map is
+ * packed as 192 int64 [type][minor][4] = key values 0..2 and a flags word (bit k: key k present, bit 3: the minor is
+ * in the map); `matched` holds n x 3 of them (allocatable, allocated, remained) with policy[i].
+ *   mode 0: tryAllocateFromReservation over the n entries (required: requiredFromReservation; ignored: the pod is
+ *           reservation-ignored; scored: with the plugin's scorer) -> 0 success (out3 = minors per type), 1 nil
+ *           result, else the status code (Unschedulable "Reservation(s) ...": *reason = KE_REASON_RSV_*)
+ *   mode 1: scoreWithReservation of entry 0 -> 0 and *score */
+static void dres_unpack(const int64_t* w, ds_dres* d) {
+  memset(d, 0, sizeof *d);
+  for (int t = 0; t < KE_DEV_TYPES; t++)
+    for (int m = 0; m < KE_MAX_MINORS; m++) {
+      const int64_t* e = w + (t * KE_MAX_MINORS + m) * 4;
+      if (!((e[3] >> 3) & 1)) continue;
+      d->in[t] |= (uint16_t)(1u << m);
+      for (int k = 0; k < KE_DKEYS; k++) {
+        d->r[t][m].has[k] = (uint8_t)((e[3] >> k) & 1);
+        d->r[t][m].v[k] = d->r[t][m].has[k] ? e[k] : 0;
+      }
+    }
+}
+int32_t or_ds_rsv_direct(or_cluster* c, const ke_pod* pod, int32_t node, int32_t n, const int32_t* policy,
+                         const int64_t* matched, const int64_t* basic, const int64_t* m_alloc, const int64_t* m_allocd,
+                         int32_t mode, int32_t required, int32_t ignored, int32_t scored, uint32_t* out3,
+                         int64_t* score, int32_t* reason) {
+  static ds_rstate st;
+  memset(&st, 0, sizeof st);
+  if (n < 0 || n > DS_MAX_MATCHED) return KE_ERR_INVALID;
+  st.n = n;
+  for (int i = 0; i < n; i++) {
+    st.m[i].r = -1;
+    st.m[i].policy = policy[i];
+    dres_unpack(matched + (3 * i + 0) * 192, &st.m[i].allocatable);
+    dres_unpack(matched + (3 * i + 1) * 192, &st.m[i].allocated);
+    dres_unpack(matched + (3 * i + 2) * 192, &st.m[i].remained);
+  }
+  dres_unpack(basic, &st.basic);
+  dres_unpack(m_alloc, &st.matched_allocatable);
+  dres_unpack(m_allocd, &st.matched_allocated);
+  ds_pod d;
+  ds_prepare_pod(c, pod, &d);
+  const or_node* nd = &c->nodes[node];
+  *reason = 0;
+  for (int t = 0; t < KE_DEV_TYPES; t++) out3[t] = 0;
+  if (mode == 1) {
+    *score = n > 0 ? ds_rsv_score(c, nd, &d, &st, 0) : 0;
+    return 0;
+  }
+  int8_t vf[2][KE_MAX_MINORS];
+  int why = 0;
+  const ke_deviceshare_args* sc = scored ? &c->cfg.deviceshare : NULL;
+  if (n == 0) return 1;
+  if (ignored) {
+    ds_rview v;
+    ds_view_of(&st, -2, &v);
+    const int code = ds_autopilot_view(c, nd, &d, &v, sc, 0, out3, vf, &why);
+    *reason = why;
+    return code;
+  }
+  const int r = ds_from_rsv(c, nd, &d, &st, -1, required, 0, sc, 0, out3, vf, &why);
+  *reason = why;
+  return r == 1 ? 0 : r == 0 ? 1 : KE_CODE_UNSCHEDULABLE;
+}
+
+/* the pod's DeviceShare restore state on `node` when it is a reservation-matched (or ignored) DeviceShare pod: 1 and
+ * *st, else 0 (the plain path) */
+static int ds_pod_rstate(const or_cluster* c, const ke_pod* pod, const ds_pod* d, int32_t node, ds_rstate* st) {
+  if (d->skip || d->status || !c->ralloc) return 0;
+  if (c->ignored && pod->reservation_matched == KE_RSV_IGNORED) {
+    char* all = (char*)malloc((size_t)c->n_resv);
+    memset(all, 1, (size_t)c->n_resv);
+    ds_rstate_build(c, node, all, st);
+    free(all);
+    return st->n > 0;
+  }
+  if (!c->resv_m || (pod->reservation_matched != KE_RSV_MATCHED && pod->reservation_matched != KE_RSV_AFFINITY)) return 0;
+  ds_rstate_build(c, node, c->resv_m, st);
+  return st->n > 0;
+}
+
 /* Filter's trial allocation: *gpu = the GPU minors */
 static int ds_try_allocate(const or_cluster* c, const or_node* nd, const ds_pod* d, ds_aff a, uint32_t* gpu,
                            int* reason) {
@@ -2716,6 +3073,32 @@ int or_ds_filter(const or_cluster* c, const ke_pod* pod, int32_t node, int* reas
   if (!nd->has_dev_cache) return KE_CODE_SUCCESS;
   uint32_t gpu;
   int why = 0;
+  static __thread ds_rstate rs;
+  if (ds_pod_rstate(c, pod, &d, node, &rs)) {
+    /* tryAllocateFromReservation over the matched list (plugin.go:350-356): a satisfied reservation passes, none
+     * under a reservation affinity fails; else the node's own allocation with the matched reservations' allocatable
+     * preemptible (:358-364).  A reservation-ignored pod: tryAllocateIgnoreReservation's status. */
+    uint32_t out[KE_DEV_TYPES];
+    int8_t vf[2][KE_MAX_MINORS];
+    if (pod->reservation_matched == KE_RSV_IGNORED) { /* tryAllocateIgnoreReservation (reservation.go:221-223) */
+      ds_rview v;
+      ds_view_of(&rs, -2, &v);
+      const int st = ds_autopilot_view(c, nd, &d, &v, NULL, 0, out, vf, &why);
+      if (st) *reason = why;
+      return st;
+    }
+    const int r = ds_from_rsv(c, nd, &d, &rs, -1, pod->reservation_matched == KE_RSV_AFFINITY, 0, NULL, 0, out, vf, &why);
+    if (r == 1) return KE_CODE_SUCCESS;
+    if (r == -1) {
+      *reason = why;
+      return KE_CODE_UNSCHEDULABLE;
+    }
+    ds_rview v;
+    ds_view_of(&rs, -1, &v);
+    const int st = ds_autopilot_view(c, nd, &d, &v, NULL, 0, out, vf, &why);
+    if (st) *reason = why;
+    return st;
+  }
   const int st = ds_try_allocate(c, nd, &d, NO_AFF, &gpu, &why);
   if (st) *reason = why;
   return st;
@@ -2856,6 +3239,12 @@ int64_t or_ds_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
   const ds_aff a = numa_stored_affinity(c, pod, node, &aff) ? (ds_aff){aff != 0, aff} : NO_AFF;
   int inc[KE_DEV_TYPES], cnt[KE_DEV_TYPES], why = 0;
   if (ds_node_prepare(nd, &d, 0, inc, cnt, &why)) return 0; /* Prepare error: Score returns 0 with an error status */
+  static __thread ds_rstate rs;
+  if (ds_pod_rstate(c, pod, &d, node, &rs)) {
+    /* the nominated reservation's scoreWithNominatedReservation, else the node's own (scoring.go:83-102) */
+    const int i = c->ds_nom && pod->reservation_matched != KE_RSV_IGNORED ? ds_rsv_find(&rs, c->ds_nom[node]) : -1;
+    return ds_rsv_score(c, nd, &d, &rs, i);
+  }
   int64_t s = 0;
   for (int t = 0; t < KE_DEV_TYPES; t++) {
     if (!inc[t]) continue;
@@ -2891,6 +3280,28 @@ static void fill_gpu_total_mem(const ke_device* dev, rl* alloc) {
   }
 }
 
+/* DeviceShare Reserve's allocation (plugin.go:428-496): for a reservation-matched pod the nominated reservation's
+ * (allocateWithNominatedReservation, reservation.go:368-415) when it holds devices and satisfies the pod, else the
+ * node's own with the matched reservations' allocatable preemptible (plugin.go:482-487); for a reservation-ignored
+ * pod tryAllocateIgnoreReservation's (reservation.go:381-385); else on the stored NUMA affinity `a`. */
+static int ds_reserve_alloc(const or_cluster* c, const ke_pod* pod, const ds_pod* d, int32_t node, ds_aff a,
+                            uint32_t* out, int8_t (*vf)[KE_MAX_MINORS], int* why) {
+  const or_node* nd = &c->nodes[node];
+  static __thread ds_rstate rs;
+  if (ds_pod_rstate(c, pod, d, node, &rs)) {
+    ds_rview v;
+    if (pod->reservation_matched == KE_RSV_IGNORED) {
+      ds_view_of(&rs, -2, &v);
+      return ds_autopilot_view(c, nd, d, &v, &c->cfg.deviceshare, 1, out, vf, why);
+    }
+    const int i = c->ds_nom ? ds_rsv_find(&rs, c->ds_nom[node]) : -1;
+    if (i >= 0 && ds_from_rsv(c, nd, d, &rs, i, 0, 0, &c->cfg.deviceshare, 1, out, vf, why) == 1) return KE_CODE_SUCCESS;
+    ds_view_of(&rs, -1, &v);
+    return ds_autopilot_view(c, nd, d, &v, &c->cfg.deviceshare, 1, out, vf, why);
+  }
+  return ds_autopilot(c, nd, d, a, &c->cfg.deviceshare, 1, out, vf, why);
+}
+
 /* AutopilotAllocator.Allocate in Reserve (plugin.go:459-486) succeeds: with the alignment disabled nothing
  * checked the devices of a node whose NUMA Admit stored an affinity (Filter skipped, Allocate a no-op) */
 static int ds_reserve_feasible(const or_cluster* c, const ke_pod* pod, int32_t node, ds_aff a) {
@@ -2901,7 +3312,7 @@ static int ds_reserve_feasible(const or_cluster* c, const ke_pod* pod, int32_t n
   uint32_t out[KE_DEV_TYPES];
   int8_t vf[2][KE_MAX_MINORS];
   int why = 0;
-  return ds_autopilot(c, nd, &d, a, &c->cfg.deviceshare, 1, out, vf, &why) == KE_CODE_SUCCESS;
+  return ds_reserve_alloc(c, pod, &d, node, a, out, vf, &why) == KE_CODE_SUCCESS;
 }
 
 uint64_t or_ds_reserve(or_cluster* c, const ke_pod* pod, int32_t node) {
@@ -2919,7 +3330,7 @@ static uint64_t ds_reserve_on(or_cluster* c, const ke_pod* pod, int32_t node, ds
   int8_t vf[2][KE_MAX_MINORS];
   memset(vf, -1, sizeof vf);
   int why = 0;
-  if (ds_autopilot(c, nd, &d, a, &c->cfg.deviceshare, 1, out, vf, &why)) return 0; /* passed Filter */
+  if (ds_reserve_alloc(c, pod, &d, node, a, out, vf, &why)) return 0; /* passed Filter */
   uint64_t mask = 0;
   for (int t = 0; t < KE_DEV_TYPES; t++) {
     const int nk = nkeys(t);
@@ -4272,8 +4683,16 @@ static int32_t or_resv_prescore(const or_cluster* c, const ke_pod* pod, const ch
         if (c->resv[r].order != 0 && (order == 0 || c->resv[r].order < order)) order = c->resv[r].order;
       }
     if (!any) continue;
-    int32_t n_ok = 0, first = -1, by_order = -1, by_score = -1, n_matched = 0, only = -1;
-    int64_t bo = 0, bsc = -1;
+    /* DeviceShare's part of the nomination for a DeviceShare pod (FilterNominateReservation, plugin.go:371-426;
+     * ScoreReservation, scoring.go:113-153): over the node's matched reservations holding devices */
+    ds_pod d;
+    ds_prepare_pod(c, pod, &d);
+    static __thread ds_rstate rs;
+    const int ds_on = c->nodes[i].has_dev_cache && ds_pod_rstate(c, pod, &d, i, &rs);
+    int32_t n_ok = 0, first = -1, by_order = -1, n_matched = 0, only = -1;
+    int32_t okr[DS_MAX_MATCHED * 4];
+    int64_t ok_rs[DS_MAX_MATCHED * 4], ok_ds[DS_MAX_MATCHED * 4];
+    int64_t bo = 0;
     for (int32_t r = 0; r < c->n_resv; r++) {
       if (!m[r] || c->resv[r].node != i) continue;
       n_matched++;
@@ -4281,16 +4700,39 @@ static int32_t or_resv_prescore(const or_cluster* c, const ke_pod* pod, const ch
       if (!or_resv_nominable(c, r, pod, i, &pod_requested[i * PRW], all_alloc, affinity) ||
           !or_numa_nominable(c, pod, i, r, affinity))
         continue;
+      const int di = ds_on ? ds_rsv_find(&rs, r) : -1;
+      if (di >= 0) { /* tryAllocateFromReservation over it alone, required */
+        uint32_t out[KE_DEV_TYPES];
+        int8_t vf[2][KE_MAX_MINORS];
+        int why = 0;
+        if (ds_from_rsv(c, &c->nodes[i], &d, &rs, di, 1, 0, NULL, 0, out, vf, &why) != 1) continue;
+      }
+      if (n_ok < DS_MAX_MATCHED * 4) {
+        okr[n_ok] = r;
+        ok_rs[n_ok] = or_reservation_score_idx(c, r, pod);
+        ok_ds[n_ok] = di >= 0 ? ds_rsv_score(c, &c->nodes[i], &d, &rs, di) : 0;
+      }
       n_ok++;
       if (first < 0) first = r;
       if (c->resv[r].order != 0 && (bo == 0 || c->resv[r].order < bo)) {
         bo = c->resv[r].order;
         by_order = r;
       }
-      const int64_t sc = or_reservation_score_idx(c, r, pod);
-      if (sc > bsc) { /* sort.Slice by score desc; equal scores keep list order (insertion sort below 13) */
-        bsc = sc;
-        by_score = r;
+    }
+    /* prioritizeReservations (nominator.go:315-360): Σ of the plugins' ScoreReservation -- the Reservation plugin's
+     * raw, DeviceShare's normalized (DefaultReservationNormalizeScore over the list, normalize_score.go:24-52) --
+     * sort.Slice by score desc (equal scores keep list order: insertion sort below 13 elements) */
+    int32_t by_score = -1;
+    {
+      int64_t mx = 0, bsc = -1;
+      const int32_t n = n_ok < DS_MAX_MATCHED * 4 ? n_ok : DS_MAX_MATCHED * 4;
+      for (int32_t q = 0; q < n; q++) mx = ok_ds[q] > mx ? ok_ds[q] : mx;
+      for (int32_t q = 0; q < n; q++) {
+        const int64_t sc = ok_rs[q] + (mx > 0 ? 100 * ok_ds[q] / mx : ok_ds[q]);
+        if (sc > bsc) {
+          bsc = sc;
+          by_score = okr[q];
+        }
       }
     }
     nom[i] = n_ok == 0 ? -1 : n_ok == 1 ? first : by_order >= 0 ? by_order : by_score;
@@ -4419,6 +4861,19 @@ static int32_t or_resv_eval(or_cluster* c, const ke_pod* pod, int64_t now, eval_
   }
   int64_t* raw = (int64_t*)malloc(sizeof(int64_t) * (size_t)(N > 0 ? N : 1));
   (void)or_resv_prescore(c, pod, m, pr, feasible, affinity, raw, nom);
+  /* DeviceShare's Score reads the nominated reservation (scoring.go:83-102), and NormalizeScore runs over the nodes
+   * that passed every Filter, the Reservation Filter of a reservation affinity included */
+  ds_pod dsp;
+  ds_prepare_pod(c, pod, &dsp);
+  if (!dsp.skip && !dsp.status) {
+    c->ds_nom = nom;
+    for (int32_t i = 0; i < N; i++)
+      if (feasible[i] && c->nodes[i].has_dev_cache) o[i].ds = (int16_t)or_ds_score(c, pod, i);
+    c->ds_nom = NULL;
+  }
+  for (int32_t i = 0; i < N; i++)
+    if (!feasible[i] && o[i].status == KE_CODE_SUCCESS) o[i].status = KE_CODE_UNSCHEDULABLE;
+  normalize_and_total(c, o, N);
   int64_t mx = 0;
   for (int32_t i = 0; i < N; i++)
     if (feasible[i] && raw[i] > mx) mx = raw[i];
@@ -4454,18 +4909,21 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
        * those is not restated (a DeviceShare pod and held devices; a pod with a NUMA policy and held NUMA
        * resources / CPUs; held NUMA resources / CPUs on a NUMA-policy node) */
       if (pods[p].reservation_matched == KE_RSV_IGNORED && c->ralloc) {
-        int dev = 0, numa_cpu = 0, on_policy = 0;
+        int dev = 0, dev_on_policy = 0, numa_cpu = 0, on_policy = 0;
         for (int32_t r = 0; r < c->n_resv; r++) {
           const int h = or_holds_of(&c->ralloc[r]);
-          dev |= (h & KE_RSV_HOLDS_DEVICES) != 0;
+          const int pol = c->nodes[c->resv[r].node].node.numa_topology_policy != KE_NUMA_POLICY_NONE;
+          if (h & KE_RSV_HOLDS_DEVICES) dev = 1, dev_on_policy |= pol;
           if (h & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)) {
             numa_cpu = 1;
-            on_policy |= c->nodes[c->resv[r].node].node.numa_topology_policy != KE_NUMA_POLICY_NONE;
+            on_policy |= pol;
           }
         }
-        ds_pod d; /* (a pod binding CPUs allocates from the held CPUs: or_numa_ignored) */
+        ds_pod d; /* (a pod binding CPUs allocates from the held CPUs: or_numa_ignored; a DeviceShare pod from the
+                     held devices: tryAllocateIgnoreReservation) -- the held devices in NUMA hints are not restated */
         ds_prepare_pod(c, &pods[p], &d);
-        if ((dev && !d.skip) || (numa_cpu && pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE) || on_policy)
+        const int pod_pol = pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE;
+        if ((dev && !d.skip && (d.h || pod_pol || dev_on_policy)) || (numa_cpu && pod_pol) || on_policy)
           return KE_ERR_UNSUPPORTED;
       }
       continue;
@@ -4477,10 +4935,18 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
     ds_prepare_pod(c, &pods[p], &d);
     (void)node_bind;
     /* every requested name beyond cpu / memory is read through its ke_pod.xres entry: a name without an id is
-     * refused (batch / mid resources included) */
-    int scalar = pods[p].has_other_requests > 1 || !d.skip;
-    for (int r = 0; r < KE_PDR_COUNT; r++) scalar |= pods[p].device_requests[r] != 0;
-    if (scalar) return KE_ERR_UNSUPPORTED;
+     * refused (batch / mid resources included); a DeviceShare pod allocates from its matched reservations' devices
+     * (deviceshare/reservation.go:207-449) -- not with device hints / joint allocation, nor in NUMA hints (a pod
+     * with a NUMA policy, or a NUMA-policy node, beside a matched reservation holding devices) */
+    if (pods[p].has_other_requests > 1 || pods[p].has_unsupported_device_requests) return KE_ERR_UNSUPPORTED;
+    if (!d.skip && c->ralloc)
+      for (int32_t j = c->moff[p]; j < c->moff[p + 1]; j++) {
+        const int32_t r = c->mids[j];
+        if (!or_resv_usable(&c->resv[r]) || !(or_holds_of(&c->ralloc[r]) & KE_RSV_HOLDS_DEVICES)) continue;
+        if (d.h || pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE ||
+            c->nodes[c->resv[r].node].node.numa_topology_policy != KE_NUMA_POLICY_NONE)
+          return KE_ERR_UNSUPPORTED;
+      }
     /* a pod with its own NUMA policy matching a reservation that holds NUMA resources / CPUs: its hints over the
      * allocate-from-reservation trials are not restated */
     for (int32_t j = c->moff[p]; pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE && j < c->moff[p + 1]; j++)
@@ -4567,9 +5033,7 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
       c->resv_m = mflags;
     }
     const int plan = b >= 0 ? or_reserve_plan(c, &pods[p], b, &rp, mflags ? nom[b] : -1) : 0;
-    c->resv_m = NULL;
-    c->ignored = 0;
-    free(mflags);
+    c->ds_nom = mflags ? nom : NULL; /* DeviceShare Reserve: the nominated reservation (with resv_m / ignored) */
     if (b >= 0 && (plan != 0 || !ds_reserve_feasible(c, &pods[p], b, da))) {
       /* Reserve failed (Unreserve undoes the others): not placed */
       chosen[p] = -1;
@@ -4585,6 +5049,9 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
       or_pod_assign(c, b, &pods[p], now);
       or_reserve_apply(c, b, &rp, numa_alloc ? numa_alloc + (int64_t)p * 16 : NULL);
       mask = ds_reserve_on(c, &pods[p], b, da, (int8_t(*)[KE_MAX_MINORS])(c->last_vf + (int64_t)p * 2 * KE_MAX_MINORS));
+      c->resv_m = NULL;
+      c->ds_nom = NULL;
+      c->ignored = 0;
       c->nodes[b].node.requested[KE_RES_CPU] += pods[p].requests[KE_RES_CPU];
       c->nodes[b].node.requested[KE_RES_MEMORY] += pods[p].requests[KE_RES_MEMORY];
       c->nodes[b].node.pod_count++; /* NodeInfo.AddPod */
@@ -4614,6 +5081,10 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
       }
     }
     if (dev_alloc) dev_alloc[p] = mask;
+    c->resv_m = NULL;
+    c->ds_nom = NULL;
+    c->ignored = 0;
+    free(mflags);
   }
   free(o);
   free(nom);

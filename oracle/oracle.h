@@ -66,6 +66,10 @@ typedef struct or_rsv_state {
   int64_t dev_remained[KE_DEV_TYPES][KE_MAX_MINORS][KE_DKEYS];
 } or_rsv_state;
 int or_restore_state(const or_cluster* c, int32_t r, or_rsv_state* out);
+int32_t or_ds_rsv_direct(or_cluster* c, const ke_pod* pod, int32_t node, int32_t n, const int32_t* policy,
+                         const int64_t* matched, const int64_t* basic, const int64_t* m_alloc, const int64_t* m_allocd,
+                         int32_t mode, int32_t required, int32_t ignored, int32_t scored, uint32_t* out3,
+                         int64_t* score, int32_t* reason);
 int or_numa_reserve_from_rsv(or_cluster* c, const ke_pod* pod, int32_t node, const int32_t* ids, int32_t n_ids,
                              int32_t nom, int32_t required, uint64_t* cpus);
 int or_reservations_get(const or_cluster* c, int32_t n, ke_reservation* out);
