@@ -62,6 +62,7 @@ REASON_DS_JOINT_VIOLATION = 48
 REASON_DS_NO_MATCHED_TEMPLATE = 49
 REASON_RSV_INSUFFICIENT_CPUS = 50  # a required reservation affinity whose holding reservations satisfy none
 REASON_RSV_INSUFFICIENT_DEVICES = 51
+REASON_RSV_AFFINITY = 52  # the Reservation Filter of a reservation-affinity pod (reservation/plugin.go:316-318)
 REASON_FIT_TOO_MANY_PODS, REASON_FIT_INSUFFICIENT_CPU, REASON_FIT_INSUFFICIENT_MEMORY = 64, 65, 66
 REASON_FIT_INSUFFICIENT_SCALAR = 67
 # ke_pod.gpu_required_topology_scope (apiext.DeviceTopologyScope -> level)

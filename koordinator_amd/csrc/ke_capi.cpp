@@ -17,6 +17,8 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
                 int16_t* la, int16_t* numa, int16_t* ds, int16_t* total, int32_t* best);
 int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t* chosen, int32_t* score);
 int device_rsv_result(Context* ctx, int32_t* out4);
+int device_ds_views(Context* ctx, const ke_pod& pod, int64_t now, const std::vector<DsView>& views,
+                    std::vector<DsViewOut>& out);
 int device_rsv_views(Context* ctx, const ke_pod& pod, int64_t now, const std::vector<RsvView>& views,
                      std::vector<RsvViewOut>& out);
 int device_quota_sync(Context* ctx);
@@ -198,11 +200,24 @@ static int check_matches(Context& c, const ke_pod* pods, int32_t n) {
     if (!staged) return fail(KE_ERR_INVALID, "a KE_RSV_MATCHED / AFFINITY pod without ke_pod_reservations");
     const uint32_t f = c.staged[(size_t)p].flags;
     // (the Reservation plugin reads the pod's requests by name: every name other than cpu / memory through its
-    // ke_pod.xres entry -- batch / mid resources included -- so a requested name without a resource id is refused)
-    bool scalar = pods[p].has_other_requests > 1 || pods[p].has_unsupported_device_requests;
-    for (int r = 0; r < KE_PDR_COUNT; r++) scalar = scalar || pods[p].device_requests[r] != 0;
-    if ((f & (PF_DS | PF_DS_HINT)) || scalar)
-      return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations with device requests or unnamed resources");
+    // ke_pod.xres entry -- batch / mid resources and device resources included -- so a requested name without a
+    // resource id is refused)
+    if (pods[p].has_other_requests > 1 || pods[p].has_unsupported_device_requests)
+      return fail(KE_ERR_UNSUPPORTED, "a pod matching reservations with unnamed resources");
+    // a DeviceShare pod allocates from its matched reservations' devices (resv_ds_views) -- not with device hints /
+    // joint allocation, nor in NUMA hints (a pod with a NUMA policy, or a NUMA-policy node, beside a matched
+    // reservation holding devices)
+    if ((f & (PF_DS | PF_DS_HINT)) && !c.resv_holds.empty())
+      for (int32_t j = c.match_off[(size_t)p]; j < c.match_off[(size_t)p + 1]; j++) {
+        const int32_t r = c.match_ids[(size_t)j];
+        if (r < 0 || r >= (int32_t)c.resv.size() || !resv_usable(c.resv[(size_t)r]) ||
+            !(c.resv_holds[(size_t)r] & KE_RSV_HOLDS_DEVICES))
+          continue;
+        if ((f & PF_DS_HINT) || pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE ||
+            c.nodes[(size_t)c.resv[(size_t)r].node].node.numa_topology_policy != KE_NUMA_POLICY_NONE)
+          return fail(KE_ERR_UNSUPPORTED, "a DeviceShare pod with device hints or NUMA hints matching a reservation "
+                                          "that holds devices");
+      }
     // a pod with its own NUMA policy takes hints on every node: a matched reservation holding NUMA resources or
     // CPUs would need them over its allocate-from-reservation trials (not restated); without such holdings its
     // matched restore moves only NodeInfo.Requested, which the hints do not read
@@ -925,6 +940,11 @@ static int schedule_sync(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_
         rc = device_rsv_views(&c, pods[s0], now_ns, c.rsv_views, c.rsv_view_out);
         if (rc) return resv_ignore_end(c), rc;
       }
+      resv_ds_views(c, pods[s0], nullptr, 0);  // DeviceShare's ignore / own views (k_ds_views)
+      if (!c.ds_views.empty()) {
+        rc = device_ds_views(&c, pods[s0], now_ns, c.ds_views, c.ds_view_out);
+        if (rc) return resv_ignore_end(c), rc;
+      }
       resv_ignore_ovr(c);
     }
     if (rsv) {
@@ -934,6 +954,15 @@ static int schedule_sync(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_
       if (!c.rsv_views.empty()) {
         rc = device_rsv_views(&c, pods[s0], now_ns, c.rsv_views, c.rsv_view_out);
         if (rc) return rc;
+      }
+      resv_ds_views(c, pods[s0], ids, n_ids);  // DeviceShare's trials, on the rows with the pod's matched restore
+      if (!c.ds_views.empty()) {
+        rc = device_ds_views(&c, pods[s0], now_ns, c.ds_views, c.ds_view_out);
+        if (rc) {
+          for (const DsView& v : c.ds_views) resv_node_restore(c, v.node);
+          c.ds_views.clear();
+          return rc;
+        }
       }
       rc = resv_prepare(c, pods[s0], ids, n_ids, pods[s0].reservation_matched == KE_RSV_AFFINITY);
       if (rc) return rc;

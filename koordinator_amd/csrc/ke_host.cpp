@@ -912,8 +912,15 @@ int resv_ignore_check(const Context& c, const ke_pod& pod, uint32_t pod_flags) {
       on_policy_node = on_policy_node || c.nodes[(size_t)c.resv[i].node].node.numa_topology_policy != KE_NUMA_POLICY_NONE;
     }
   }
-  if ((dev && (pod_flags & (PF_DS | PF_DS_HINT))) || (numa_cpu && pod.numa_topology_policy != KE_NUMA_POLICY_NONE) ||
-      on_policy_node)
+  // a DeviceShare pod allocates from the held devices (resv_ds_views' ignore view) -- not with device hints, nor in
+  // NUMA hints (its own NUMA policy, or a device-holding reservation on a NUMA-policy node)
+  bool dev_on_policy = false;
+  for (size_t i = 0; i < c.resv_holds.size(); i++)
+    if (c.resv_holds[i] & KE_RSV_HOLDS_DEVICES)
+      dev_on_policy = dev_on_policy || c.nodes[(size_t)c.resv[i].node].node.numa_topology_policy != KE_NUMA_POLICY_NONE;
+  const bool ds = (pod_flags & (PF_DS | PF_DS_HINT)) != 0;
+  if ((dev && ds && ((pod_flags & PF_DS_HINT) || pod.numa_topology_policy != KE_NUMA_POLICY_NONE || dev_on_policy)) ||
+      (numa_cpu && pod.numa_topology_policy != KE_NUMA_POLICY_NONE) || on_policy_node)
     return fail(KE_ERR_UNSUPPORTED, "a reservation-ignored pod reading resources a reservation holds "
                                     "(tryAllocateIgnoreReservation's remainder)");
   return KE_OK;
@@ -936,6 +943,9 @@ void resv_ignore_end(Context& c) {
   c.rsv_views.clear();
   c.rsv_view_resv.clear();
   c.rsv_view_out.clear();
+  c.ds_views.clear();
+  c.ds_view_resv.clear();
+  c.ds_view_out.clear();
   for (size_t node = 0; node < c.resv_by_node.size(); node++)
     if (!c.resv_by_node[node].empty()) resv_node_restore(c, (int32_t)node);
 }
@@ -944,9 +954,12 @@ static bool resv_holds_cpu(const Context& c, int32_t i);
 static bool pod_binds_on(const DevPod& dp, const NodeState& ns);
 
 bool resv_ignore_needs_views(const Context& c, const ke_pod& pod, uint32_t pod_flags) {
-  if (!((pod_flags & PF_CPUSET) || (c.n_bind_nodes > 0 && pod.requests[KE_RES_CPU] > 0))) return false;
-  for (size_t i = 0; i < c.resv_holds.size(); i++)
-    if (c.resv_holds[i] & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)) return true;
+  const bool binds = (pod_flags & PF_CPUSET) || (c.n_bind_nodes > 0 && pod.requests[KE_RES_CPU] > 0);
+  const bool ds = (pod_flags & PF_DS) && !(pod_flags & PF_DS_INVALID);
+  for (size_t i = 0; i < c.resv_holds.size(); i++) {
+    if (binds && (c.resv_holds[i] & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET))) return true;
+    if (ds && (c.resv_holds[i] & KE_RSV_HOLDS_DEVICES)) return true;
+  }
   return false;
 }
 
@@ -980,19 +993,42 @@ void resv_ignore_views(Context& c, const ke_pod& pod) {
 
 // the trials' outcome as the Filter's and Reserve's decisions (a failed allocation fails both: the status is
 // returned, plugin.go:384-387 and :554-558)
+// DeviceShare (resv_ds_views with every reservation matchedOrIgnored): Filter and Reserve from the ignore view (-2,
+// tryAllocateIgnoreReservation, reservation.go:221-223, 381-385), Score from the node's own (-1: no nominated
+// reservation, scoring.go:96-102)
 void resv_ignore_ovr(Context& c) {
   c.rsv_ovr.clear();
+  auto ovr_of = [&](int32_t node) -> RsvOvr& {
+    for (RsvOvr& o : c.rsv_ovr)
+      if (o.node == node) return o;
+    c.rsv_ovr.emplace_back();
+    RsvOvr& o = c.rsv_ovr.back();
+    std::memset(&o, 0, sizeof o);
+    o.node = node;
+    NodeState& ns = c.nodes[(size_t)node];
+    ns.rsv_ovr = true;
+    ns.dirty = true;
+    return o;
+  };
   for (size_t q = 0; q < c.rsv_views.size(); q++) {
-    RsvOvr o{};
-    o.node = c.rsv_views[q].node;
+    RsvOvr& o = ovr_of(c.rsv_views[q].node);
     const bool ok = c.rsv_view_out.size() > q && c.rsv_view_out[q].ok;
     o.filter = o.reserve = (int8_t)(ok ? 1 : 2);
     if (ok)
       for (int w = 0; w < 4; w++) o.cpus[w] = c.rsv_view_out[q].cpus[w];
-    c.rsv_ovr.push_back(o);
-    NodeState& ns = c.nodes[(size_t)o.node];
-    ns.rsv_ovr = true;
-    ns.dirty = true;
+  }
+  for (size_t q = 0; q < c.ds_views.size() && q < c.ds_view_out.size(); q++) {
+    RsvOvr& o = ovr_of(c.ds_views[q].node);
+    const DsViewOut& v = c.ds_view_out[q];
+    o.ds_on = 1;
+    if (c.ds_view_resv[q] == -1) {
+      o.ds_raw = (int16_t)v.raw;
+    } else {
+      o.ds_st = (uint8_t)v.st;
+      o.ds_reason = (uint8_t)v.reason;
+      o.ds_res = (int8_t)(v.st == KE_CODE_SUCCESS && v.minors ? 1 : 2);
+      o.ds_minors = v.minors;
+    }
   }
 }
 
@@ -1041,6 +1077,160 @@ void resv_views(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids
       }
       c.rsv_views.push_back(v);
       c.rsv_view_resv.push_back(i);
+    }
+  }
+}
+
+// ---- DeviceShare allocate-from-reservation views (deviceshare/reservation.go:99-366) ------------------------------
+// A deviceResources map of one reservation part: per instance (bit 16*type + minor in `in`) the keys present
+// (bit in keys[k]) and their values -- the quotav1 ResourceList arithmetic of the reference, keys kept by union.
+struct HDres {
+  uint64_t in = 0;
+  uint64_t keys[KE_DKEYS] = {0, 0, 0};
+  int64_t v[KE_DEV_TYPES][KE_MAX_MINORS][KE_DKEYS] = {};
+};
+// deviceResources.append of one instance: util.AddResourceList (keys of both, summed)
+static void hd_add(HDres& d, int t, int m, const int64_t* val, uint32_t kb) {
+  const uint64_t bit = 1ull << (16 * t + m);
+  const bool had = (d.in & bit) != 0;
+  d.in |= bit;
+  for (int k = 0; k < KE_DKEYS; k++) {
+    if (!((kb >> k) & 1u)) continue;
+    d.v[t][m][k] = (had && (d.keys[k] & bit) ? d.v[t][m][k] : 0) + val[k];
+    d.keys[k] |= bit;
+  }
+}
+static void hd_append(HDres& d, const HDres& src) {  // appendAllocated (device_resources.go:116-132)
+  for (int t = 0; t < KE_DEV_TYPES; t++)
+    for (int m = 0; m < KE_MAX_MINORS; m++) {
+      const uint64_t bit = 1ull << (16 * t + m);
+      if (!(src.in & bit)) continue;
+      uint32_t kb = 0;
+      for (int k = 0; k < KE_DKEYS; k++) kb |= (uint32_t)((src.keys[k] & bit) != 0) << k;
+      hd_add(d, t, m, src.v[t][m], kb);
+    }
+}
+// RestoreReservation's parts of one reservation (reservation.go:157-172): allocatable = the reserve pod's instances
+// (keys with a non-zero amount), allocated = the owners' usage on them (appendAllocatedByHints), remained =
+// subtractAllocated(copy(allocatable), allocated, false) -- quotav1.Subtract per allocated instance, deleted IsZero
+static void hd_parts(const ke_reservation_alloc& a, HDres& al, HDres& ow, HDres& rem) {
+  al = HDres{};
+  ow = HDres{};
+  for (int t = 0; t < KE_DEV_TYPES; t++)
+    for (int m = 0; m < KE_MAX_MINORS; m++) {
+      const uint64_t bit = 1ull << (16 * t + m);
+      if (!(a.device_minors & bit)) continue;
+      uint32_t ka = 0, ko = 0;
+      for (int k = 0; k < KE_DKEYS; k++) {
+        ka |= (uint32_t)(a.device[t][m][k] != 0) << k;
+        ko |= (uint32_t)(a.owner_device[t][m][k] != 0) << k;
+      }
+      hd_add(al, t, m, a.device[t][m], ka);
+      if ((a.owner_device_minors & bit) && ko) hd_add(ow, t, m, a.owner_device[t][m], ko);
+    }
+  rem = al;
+  for (int t = 0; t < KE_DEV_TYPES; t++)
+    for (int m = 0; m < KE_MAX_MINORS; m++) {
+      const uint64_t bit = 1ull << (16 * t + m);
+      if (!(ow.in & bit)) continue;
+      bool zero = true;
+      for (int k = 0; k < KE_DKEYS; k++) {
+        const bool hr = (rem.in & bit) && (rem.keys[k] & bit), ho = (ow.keys[k] & bit) != 0;
+        if (!hr && !ho) continue;
+        rem.v[t][m][k] = (hr ? rem.v[t][m][k] : 0) - (ho ? ow.v[t][m][k] : 0);
+        rem.keys[k] |= bit;
+        zero = zero && rem.v[t][m][k] == 0;
+      }
+      if (zero) {  // the instance leaves the map
+        rem.in &= ~bit;
+        for (int k = 0; k < KE_DKEYS; k++) rem.keys[k] &= ~bit, rem.v[t][m][k] = 0;
+      } else {
+        rem.in |= bit;
+      }
+    }
+}
+static void hd_to_pre(const HDres& x, DsView& v) {
+  v.pre_in = x.in;
+  for (int k = 0; k < KE_DKEYS; k++) v.pre_keys[k] = x.keys[k];
+  std::memcpy(v.pre, x.v, sizeof v.pre);
+}
+
+void resv_ds_views(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids) {
+  c.ds_views.clear();
+  c.ds_view_resv.clear();
+  c.ds_view_out.clear();
+  if (c.resv_alloc.empty() || !c.ds_enabled) return;
+  const DevPod dp = make_dev_pod(c.cfg, pod, pod_hints(c, pod), &c.tmpl);
+  if (!(dp.flags & PF_DS) || (dp.flags & PF_DS_INVALID)) return;
+  const bool ignored = ids == nullptr;
+  std::vector<char> m(c.resv.size(), ignored ? 1 : 0);
+  for (int32_t j = 0; !ignored && j < n_ids; j++) m[(size_t)ids[j]] = 1;
+  flush_mirror(c);  // the rows re-derived below carry every earlier placement
+  for (size_t node = 0; node < c.resv_by_node.size(); node++) {
+    NodeState& ns = c.nodes[node];
+    if (c.resv_by_node[node].empty() || !ns.has_dev_cache) continue;
+    // RestoreReservation's matched list: the usable matched reservations holding devices, in index order
+    // (at most 32, as the restatement keeps them)
+    std::vector<int32_t> mine;
+    for (int32_t i : c.resv_by_node[node])
+      if (m[(size_t)i] && resv_usable(c.resv[(size_t)i]) && c.resv_alloc[(size_t)i].device_minors && mine.size() < 32)
+        mine.push_back(i);
+    if (mine.empty()) continue;
+    if (!ignored) {  // the rows this pod sees: its matched restore (resv_prepare applies the same)
+      resv_delta(c, (int32_t)node, &m, true, ns.rv_req, ns.rv_nz, &ns.rv_pods, &ns.rv_x);
+      resv_plugin_restore(c, (int32_t)node, &m, ns);
+      ns.dirty = true;
+    }
+    std::vector<HDres> al(mine.size()), ow(mine.size()), rem(mine.size());
+    HDres m_alloc, m_allocd, sum_rem;
+    for (size_t q = 0; q < mine.size(); q++) {
+      hd_parts(c.resv_alloc[(size_t)mine[q]], al[q], ow[q], rem[q]);
+      hd_append(m_alloc, al[q]);
+      hd_append(m_allocd, ow[q]);
+      hd_append(sum_rem, rem[q]);
+    }
+    auto push = [&](const HDres& extra, int32_t r) -> DsView& {
+      c.ds_views.emplace_back();
+      DsView& v = c.ds_views.back();
+      std::memset(&v, 0, sizeof v);
+      v.node = (int32_t)node;
+      hd_to_pre(extra, v);
+      c.ds_view_resv.push_back(r);
+      return v;
+    };
+    if (!ignored)
+      for (size_t q = 0; q < mine.size(); q++) {  // tryAllocateFromReservation's trial of each (reservation.go:229-280)
+        HDres extra = m_allocd;  // basicPreemptible (in the row) + mergedMatchedAllocated + remained
+        hd_append(extra, rem[q]);
+        DsView& v = push(extra, mine[q]);
+        const bool restricted = c.resv[(size_t)mine[q]].allocate_policy == KE_RSV_POLICY_RESTRICTED;
+        bool any = false;
+        for (int t = 0; t < KE_DEV_TYPES; t++) {
+          const uint16_t ain = (uint16_t)((al[q].in >> (16 * t)) & 0xFFFF);
+          v.pref[t] = ain;  // preferred = the reservation's minors
+          if (!restricted) continue;
+          v.rreq[t] = ain;  // required = preferred
+          v.cap_in[t] = ain ? (uint16_t)((rem[q].in >> (16 * t)) & ain) : 0;  // calcRequiredDeviceResources
+          any = any || v.cap_in[t] != 0;
+        }
+        if (restricted) {
+          if (any) {
+            for (int k = 0; k < KE_DKEYS; k++) {
+              uint64_t cb = 0;
+              for (int t = 0; t < KE_DEV_TYPES; t++) cb |= (uint64_t)v.cap_in[t] << (16 * t);
+              v.cap_keys[k] = rem[q].keys[k] & cb;
+            }
+            std::memcpy(v.cap, rem[q].v, sizeof v.cap);
+          } else {  // nothing remained: every reservation minor with an empty list
+            for (int t = 0; t < KE_DEV_TYPES; t++) v.cap_in[t] = v.rreq[t];
+          }
+        }
+      }
+    push(m_alloc, -1);  // the node's own allocation: basicPreemptible + mergedMatchedAllocatable (plugin.go:358-364)
+    if (ignored) {      // tryAllocateIgnoreReservation (reservation.go:290-310): Σ remained + mergedMatchedAllocated
+      HDres extra = sum_rem;
+      hd_append(extra, m_allocd);
+      push(extra, -2);
     }
   }
 }
@@ -1096,21 +1286,36 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
       if (!cpus_valid(ns)) return false;
       return !(affinity && view_of(i) == 0);
     };
+    // DeviceShare (a pod with device requests on a node with a cache entry and matched reservations holding devices):
+    // the k_ds_views outcomes of its trials -- per reservation (tryAllocateFromReservation over it alone) and the
+    // node's own (-1)
+    auto ds_view = [&](int32_t r) -> const DsViewOut* {
+      for (size_t q = 0; q < c.ds_views.size(); q++)
+        if (c.ds_view_resv[q] == r && c.ds_views[q].node == node) return c.ds_view_out.size() > q ? &c.ds_view_out[q] : nullptr;
+      return nullptr;
+    };
+    const DsViewOut* ds_own = ds_view(-1);
     std::vector<int32_t> ok;
+    std::vector<int64_t> ok_ds;
     bool fits_one = false;  // the Reservation Filter with a reservation affinity (plugin.go:316-318, 351-442): a
                             // node without matched reservations fails, one with them passes when one of them fits
     for (int32_t i : mine)
       if (resv_nominable(c, i, pod, ns, pod_requested, ux, all_alloc, all_x, affinity, pods_restored,
                          (int64_t)mine.size(), ns.node.allowed_pods)) {
         fits_one = true;
-        if (numa_nominable(i)) ok.push_back(i);
+        if (!numa_nominable(i)) continue;
+        // DeviceShare's FilterNominateReservation (plugin.go:371-426): a reservation holding devices satisfies the pod
+        const DsViewOut* dv = ds_own ? ds_view(i) : nullptr;
+        if (dv && dv->st != KE_CODE_SUCCESS) continue;
+        ok.push_back(i);
+        ok_ds.push_back(dv ? dv->raw : 0);
       }
     const bool allowed = !affinity || fits_one;
     // NominateReservation (nominator.go:223-277): with an affinity and one matched reservation that one, else
-    // the survivors: the only one, else the smallest order, else the best ScoreReservation (ties -> lowest
-    // index: sort.Slice's insertion sort keeps them below 13 elements)
+    // the survivors: the only one, else the smallest order, else the best Σ ScoreReservation -- the Reservation
+    // plugin's raw and DeviceShare's normalized (DefaultReservationNormalizeScore over the list) -- ties to the
+    // lowest index (sort.Slice's insertion sort keeps them below 13 elements)
     int32_t nom = -1;
-    if (affinity && mine.size() == 1) ok.assign(1, mine[0]);
     if (ok.size() == 1) nom = ok[0];
     if (ok.size() > 1) {
       int64_t bo = 0;
@@ -1122,24 +1327,68 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
         }
       }
       if (nom < 0) {
-        int32_t bs = -1;
-        for (int32_t i : ok) {
-          const int32_t sc = resv_score(c, i, pod);
+        int64_t mx = 0, bs = -1;
+        for (int64_t x : ok_ds) mx = std::max(mx, x);
+        for (size_t q = 0; q < ok.size(); q++) {
+          const int64_t sc = resv_score(c, ok[q], pod) + (mx > 0 ? 100 * ok_ds[q] / mx : ok_ds[q]);
           if (sc > bs) {
             bs = sc;
-            nom = i;
+            nom = ok[q];
           }
         }
       }
     }
-    c.rsv_pairs.push_back({node, (int16_t)(nom >= 0 ? resv_score(c, nom, pod) : 0), (int16_t)allowed, order});
+    if (affinity && mine.size() == 1) nom = mine[0];
+    RsvOvr o{};
+    o.node = node;
+    bool any_ovr = false;
+    // DeviceShare's Filter (tryAllocateFromReservation over the matched list: a satisfied reservation passes, none
+    // under an affinity fails, else the node's own), Score (the nominated reservation's view, else the node's own)
+    // and Reserve (the nominated one's allocation when it succeeds, else the node's own; failing: not placed)
+    bool reserve_fails = false;
+    if (ds_own) {
+      o.ds_on = 1;
+      const DsViewOut* pass = nullptr;
+      for (int32_t i : mine) {
+        const DsViewOut* dv = ds_view(i);
+        if (dv && dv->st == KE_CODE_SUCCESS) {
+          pass = dv;
+          break;
+        }
+      }
+      if (pass) {
+        o.ds_st = KE_CODE_SUCCESS;
+      } else if (affinity) {
+        o.ds_st = KE_CODE_UNSCHEDULABLE;
+        o.ds_reason = KE_REASON_RSV_INSUFFICIENT_DEVICES;
+      } else {
+        o.ds_st = (uint8_t)ds_own->st;
+        o.ds_reason = (uint8_t)ds_own->reason;
+      }
+      const DsViewOut* nv = nom >= 0 ? ds_view(nom) : nullptr;
+      o.ds_raw = (int16_t)(nv ? nv->raw : ds_own->raw);
+      const DsViewOut* rv = (nv && nv->st == KE_CODE_SUCCESS && nv->minors) ? nv : ds_own;
+      if (rv->st == KE_CODE_SUCCESS && rv->minors) {
+        o.ds_res = 1;
+        o.ds_minors = rv->minors;
+      } else {
+        o.ds_res = 2;
+        reserve_fails = o.ds_st == KE_CODE_SUCCESS;
+      }
+      any_ovr = true;
+    }
+    if (affinity) {
+      o.rfilter = (int8_t)(allowed ? 1 : 2);
+      any_ovr = true;
+    }
+    c.rsv_pairs.push_back({node, (int16_t)(nom >= 0 ? resv_score(c, nom, pod) : 0),
+                           (int16_t)((allowed ? RSV_PAIR_ALLOWED : 0) | (reserve_fails ? RSV_PAIR_RESERVE_FAILS : 0)),
+                           order});
     c.rsv_nominated.push_back(nom);
     // NodeNUMAResource with the matched reservations first (plugin.go:381-397, 553-563): the Filter's trial
     // (one satisfied; else "Reservation(s) ..." under an affinity, else the node's own) and Reserve's allocation
     // (the nominated reservation's when it holds one and is satisfied; failing under an affinity)
     if (binds && ns.node.numa_topology_policy == KE_NUMA_POLICY_NONE) {
-      RsvOvr o{};
-      o.node = node;
       bool any_view = false, any_ok = false;
       for (size_t q = 0; q < c.rsv_views.size(); q++)
         if (c.rsv_views[q].node == node) {
@@ -1157,10 +1406,11 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
       } else {
         o.reserve = (int8_t)(nv == 0 && affinity ? 2 : 0);
       }
-      if (o.filter || o.reserve) {
-        c.rsv_ovr.push_back(o);
-        ns.rsv_ovr = true;
-      }
+      any_ovr = any_ovr || o.filter || o.reserve;
+    }
+    if (any_ovr) {
+      c.rsv_ovr.push_back(o);
+      ns.rsv_ovr = true;
     }
     // the rows this pod sees: its matched reservations restored too, and left out of the plugins' unmatched states
     resv_delta(c, node, &m, true, ns.rv_req, ns.rv_nz, &ns.rv_pods, &ns.rv_x);
@@ -1242,6 +1492,9 @@ void resv_finish(Context& c, int32_t chosen_local, const ke_pod& pod, int32_t* a
   c.rsv_views.clear();
   c.rsv_view_resv.clear();
   c.rsv_view_out.clear();
+  c.ds_views.clear();
+  c.ds_view_resv.clear();
+  c.ds_view_out.clear();
 }
 
 // forgetPod -> RemoveAssignedPod (reservation_info.go:470-482)
@@ -2007,14 +2260,15 @@ void host_release_node(const ke_config& cfg, bool ext, NodeState& ns, const ke_p
       ns.asg_uid.erase(ns.asg_uid.begin() + (long)i);
       break;
     }
-  // framework NodeInfo.RemovePod: Requested (and the FitPlus (NonZero)Requested by resource id)
+  // framework NodeInfo.RemovePod: Requested and (NonZero)Requested by resource id (read by FitPlus -- whose device
+  // rows follow when `ext` -- and by the Reservation plugin's fitsNode)
+  (void)ext;
   ns.node.requested[KE_RES_CPU] -= pod.requests[KE_RES_CPU];
   ns.node.requested[KE_RES_MEMORY] -= pod.requests[KE_RES_MEMORY];
   ns.node.pod_count--;
-  if (ext)
-    for (int e = 0; e < pod.n_xres; e++)
-      for (ke_node_resource& r : ns.xres)
-        if (r.id == pod.xres_id[e]) r.requested -= pod.xres_value[e];
+  for (int e = 0; e < pod.n_xres; e++)
+    for (ke_node_resource& r : ns.xres)
+      if (r.id == pod.xres_id[e]) r.requested -= pod.xres_value[e];
   // NodeNUMAResource resourceManager.Release -> NodeAllocation.release (node_allocation.go:158-190); only a
   // node with a valid CPU topology recorded the allocation (Update, resource_manager.go:461-466).  While the
   // NRT is deleted the NodeAllocation lives on in the parked tables (ke_node_topology_delete).
@@ -2107,7 +2361,7 @@ static void apply_mirror(Context& c, const std::vector<Context::PendingAssign>& 
     ns.node.requested[KE_RES_CPU] += pod.requests[KE_RES_CPU];
     ns.node.requested[KE_RES_MEMORY] += pod.requests[KE_RES_MEMORY];
     ns.node.pod_count++;  // NodeInfo.AddPod
-    if (c.ext_enabled) host_ext_reserve(ns, pod);
+    host_ext_reserve(ns, pod);  // NodeInfo.Requested.ScalarResources (FitPlus and the Reservation plugin read them)
   }
 }
 

@@ -65,9 +65,11 @@ struct DirtyFlag {
 struct RsvPair {
   int32_t node;     // local node index
   int16_t raw;      // ScoreReservation of the nominated reservation (0 = none)
-  int16_t allowed;  // the Reservation plugin's Filter passes (always without a reservation affinity)
+  int16_t allowed;  // RSV_PAIR_* bits
   int64_t order;    // smallest reservation-order label of the matched reservations (0 = none)
 };
+constexpr int16_t RSV_PAIR_ALLOWED = 1;        // the Reservation plugin's Filter passes (always without an affinity)
+constexpr int16_t RSV_PAIR_RESERVE_FAILS = 2;  // DeviceShare's Reserve fails there (the pod is not placed)
 
 struct NodeState {
   bool valid = false;  // in the snapshot (ke_node_upsert .. ke_node_delete)
@@ -225,6 +227,12 @@ struct Context {
   std::vector<RsvView> rsv_views;
   std::vector<int32_t> rsv_view_resv;
   std::vector<RsvViewOut> rsv_view_out;
+  // its DeviceShare allocate-from-reservation views (resv_ds_views -> k_ds_views): per view the reservation (-1: the
+  // node's own allocation with the matched reservations' allocatable preemptible, -2: the ignored pod's
+  // tryAllocateIgnoreReservation) and the outcome
+  std::vector<DsView> ds_views;
+  std::vector<int32_t> ds_view_resv;
+  std::vector<DsViewOut> ds_view_out;
   std::vector<int32_t> last_resv;  // per pod of the last ke_schedule: 1 + the reservation assumed, 0 = none
   int32_t resv_gen = 0;            // ke_reservations_generation: bumped by every load_reservations
   // per-pod latency of the last ke_schedule (ke_last_pod_latencies): the call's entry on the host clock, and
@@ -343,6 +351,10 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
 // the allocate-from-reservation trials a KE_RSV_MATCHED pod needs (into c.rsv_views / rsv_view_resv): per node of
 // its matched reservations holding a cpuset / NUMA resources where the pod binds CPUs, one per such reservation
 void resv_views(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids);
+// the DeviceShare views of a reservation-matched DeviceShare pod (ids: its matched reservations) or, ids == nullptr,
+// of a reservation-ignored one: per node of its device-holding reservations one per such reservation in index order
+// and the node's own (-1); an ignored pod the node's own and the ignore view (-2).  Into c.ds_views / ds_view_resv.
+void resv_ds_views(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids);
 // the refusals of resv_prepare, checked for every pod before a ke_schedule call schedules any
 int resv_check(const Context& c, const int32_t* ids, int32_t n_ids);
 // a run of KE_RSV_IGNORED pods: the rows with every usable reservation matchedOrIgnored (begin) and back to the

@@ -295,7 +295,10 @@ struct DsInst {
 struct DsRaw {
   int64_t tv[3], uv[3];
 };
-__device__ __forceinline__ void ds_load(const SoA& s, int64_t i, int t, int m, const uint64_t msk[4], DsRaw& r) {
+// rv (k_ds_views): the view's preemptible beyond the row's restore leaves max(0, used - pre) (the caller's msk
+// carries the pre keys as used keys)
+__device__ __forceinline__ void ds_load(const SoA& s, int64_t i, int t, int m, const uint64_t msk[4], DsRaw& r,
+                                        const DsView* rv = nullptr) {
   const int nk = DS_NK[t];
 #pragma unroll
   for (int k = 0; k < 3; k++) {
@@ -303,13 +306,21 @@ __device__ __forceinline__ void ds_load(const SoA& s, int64_t i, int t, int m, c
     const bool hu = k < nk && ((msk[ds_hu_word(t)] >> ds_hu_bit(t, m, k)) & 1);
     r.tv[k] = ht ? dsf(s, DS_TBASE[t] + m * nk + k, i) : 0;
     r.uv[k] = hu ? dsf(s, DS_UBASE[t] + m * nk + k, i) : 0;
+    if (rv && k < nk && ((rv->pre_keys[k] >> (16 * t + m)) & 1)) {
+      const int64_t u = r.uv[k] - rv->pre[t][m][k];
+      r.uv[k] = u > 0 ? u : 0;
+    }
   }
 }
-__device__ __forceinline__ void ds_instance_from(const DsRaw& r, int t, int m, const uint64_t msk[4], DsInst& d) {
+// rv with the instance in cap_in (a Restricted reservation's requiredDeviceResources): free_orig =
+// MinResourceList(free_orig, cap) -- the keys of both, the smaller value (pkg/util/resource.go:64-78)
+__device__ __forceinline__ void ds_instance_from(const DsRaw& r, int t, int m, const uint64_t msk[4], DsInst& d,
+                                                 const DsView* rv = nullptr) {
   const int nk = DS_NK[t];
   int64_t up[3];
   uint32_t uh = 0;
   d.th = 0;
+  const bool capped = rv && ((rv->cap_in[t] >> m) & 1u);
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     d.tv[k] = 0;
@@ -320,11 +331,17 @@ __device__ __forceinline__ void ds_instance_from(const DsRaw& r, int t, int m, c
     const bool hu = (msk[ds_hu_word(t)] >> ds_hu_bit(t, m, k)) & 1;
     const int64_t tv = r.tv[k];
     const int64_t uv = r.uv[k];
-    const int64_t fo = ht ? (tv - uv > 0 ? tv - uv : 0) : 0;  // free_orig (used-only keys: 0)
-    up[k] = ht ? (tv - fo > 0 ? tv - fo : 0) : 0;            // used' (keys of total U used)
+    int64_t fo = ht ? (tv - uv > 0 ? tv - uv : 0) : 0;  // free_orig (used-only keys: 0)
+    bool fh = ht || hu;                                  // its keys
+    if (capped) {
+      const bool ch = (rv->cap_keys[k] >> (16 * t + m)) & 1;
+      fh = fh && ch;
+      fo = fh ? (fo < rv->cap[t][m][k] ? fo : rv->cap[t][m][k]) : 0;
+    }
+    up[k] = ht ? (tv - fo > 0 ? tv - fo : 0) : 0;  // used' = total - free_orig (keys of both)
     d.tv[k] = tv;
     d.th |= (uint32_t)ht << k;
-    uh |= (uint32_t)(ht || hu) << k;
+    uh |= (uint32_t)(ht || fh) << k;
   }
   bool up_zero = true;
 #pragma unroll
@@ -442,6 +459,7 @@ struct GpuMasks {
   uint32_t used;    // deviceUsedMinorsHash
   uint32_t sat;     // allocateFromScope: LessThanOrEqual(request, deviceFree) && in deviceTotal
   uint32_t dflt;    // defaultAllocateDevices: !IsZero(free') && LessThanOrEqual(request, free')
+  uint32_t pref;    // defaultAllocateDevices' preferred minors (a matched reservation's, k_ds_views; else 0)
 };
 
 // minors whose 4-bit rank in `w` equals r (SWAR nibble compare)
@@ -606,11 +624,12 @@ __device__ bool gpu_topology_feasible(const SoA& s, int64_t i, const DevPod& p, 
 
 // defaultAllocateDevices' choice among the satisfiable instances `ok`: (scoreDevice desc, minor asc)
 // (device_resources.go:171-208), the first `want`; without a scorer the lowest minors.
-__device__ __forceinline__ uint32_t default_pick(uint32_t ok, int want, const int64_t* score) {
+// `pref`: sortDeviceResourcesByMinor's preferred minors go first (device_resources.go:187-193)
+__device__ __forceinline__ uint32_t default_pick(uint32_t ok, int want, const int64_t* score, uint32_t pref = 0) {
   uint32_t take = 0;
   for (int c = 0; c < want && ok; c++) {
     int best = -1;
-    for (uint32_t r = ok; r; r &= r - 1) {
+    for (uint32_t r = (ok & pref) ? (ok & pref) : ok; r; r &= r - 1) {
       const int m = __builtin_ctz(r);
       if (best < 0 || (score && score[m] > score[best])) best = m;  // ascending minors: ties keep the lower
     }
@@ -659,7 +678,7 @@ __device__ int gpu_allocate(const SoA& s, int64_t i, uint64_t ex0, const DevPod&
     return KE_CODE_UNSCHEDULABLE;
   }
   if (__builtin_popcount(g.dflt) >= want) {  // defaultAllocateDevices
-    if (select) *minors = default_pick(g.dflt, want, dscore);
+    if (select) *minors = default_pick(g.dflt, want, dscore, g.pref);
     return 0;
   }
   *reason = KE_REASON_DS_INSUFFICIENT_GPU;
@@ -691,14 +710,20 @@ __device__ __forceinline__ uint32_t ds_allowed(const SoA& s, int64_t i, int t, D
 // the passing instances, their summed total / free' (scoreNode), scoreDevice per minor (`score`, optional),
 // and the used hash over realUsed (allocator_gpu.go:59-70: the original used minors outside the refined
 // total, the refined used' inside).
+// rv (k_ds_views): a reservation view -- the preemptible beyond the row's (ds_load), a Restricted reservation's
+// requiredDeviceResources (only the cap_in instances take part, their free capped: ds_instance_from), its required
+// minors (defaultAllocateDevices takes only those) and preferred minors (g.pref)
 __device__ __forceinline__ bool ds_type_view(const SoA& s, int64_t i, int t, const uint64_t msk[4], const DevPod& p,
                                              const KArgs& k, DsAff a, GpuMasks& g, int64_t (&tot)[3],
-                                             int64_t (&fre)[3], int64_t* score, uint32_t sel = 0xFFFFu) {
+                                             int64_t (&fre)[3], int64_t* score, uint32_t sel = 0xFFFFu,
+                                             const DsView* rv = nullptr) {
   const int nk = DS_NK[t];
   uint64_t ex = (msk[DSM_EXISTS] >> (16 * t)) & 0xFFFF;
-  const uint32_t allowed = (uint32_t)ex & ds_allowed(s, i, t, a) & sel;  // sel: a hint Selector's devices
+  const uint32_t keep = (rv && rv->cap_in[t]) ? (uint32_t)rv->cap_in[t] : 0xFFFFu;  // requiredDeviceResources
+  const uint32_t allowed = (uint32_t)ex & ds_allowed(s, i, t, a) & sel & keep;  // sel: a hint Selector's devices
   g.minors = (uint32_t)ex;
   g.total = g.used = g.sat = g.dflt = 0;
+  g.pref = rv ? (uint32_t)rv->pref[t] : 0u;
   uint32_t orig_used = 0, used_p = 0, tot_m = 0, sat = 0, dflt = 0;
   bool present = false;
 #pragma unroll
@@ -714,7 +739,7 @@ __device__ __forceinline__ bool ds_type_view(const SoA& s, int64_t i, int t, con
     }
 #pragma unroll
     for (int u = 0; u < GRP; u++)
-      if (ms[u] >= 0) ds_load(s, i, t, ms[u], msk, raw[u]);
+      if (ms[u] >= 0) ds_load(s, i, t, ms[u], msk, raw[u], rv);
 #pragma unroll
     for (int u = 0; u < GRP; u++) {
       const int m = ms[u];
@@ -723,8 +748,9 @@ __device__ __forceinline__ bool ds_type_view(const SoA& s, int64_t i, int t, con
 #pragma unroll
       for (int q = 0; q < 3; q++) hu = hu || (q < nk && ((msk[ds_hu_word(t)] >> ds_hu_bit(t, m, q)) & 1));
       orig_used |= (uint32_t)hu << m;
+      if (!((keep >> m) & 1u)) continue;  // outside requiredDeviceResources: not in the filtered view at all
       DsInst d;
-      ds_instance_from(raw[u], t, m, msk, d);
+      ds_instance_from(raw[u], t, m, msk, d, rv);
       const bool fz = ds_free_zero(d);
       present = present || !fz;
       if (!((allowed >> m) & 1u)) continue;
@@ -745,6 +771,7 @@ __device__ __forceinline__ bool ds_type_view(const SoA& s, int64_t i, int t, con
     }
   }
   present = present && allowed != 0;
+  if (rv && rv->rreq[t]) dflt &= (uint32_t)rv->rreq[t];  // required.Len() > 0 && !required.Has(minor)
   if (present) {
     g.dflt = dflt;
     g.sat = sat;
@@ -892,9 +919,11 @@ __device__ __forceinline__ void ds_filter_score(const SoA& s, int64_t i, const D
 // defaultAllocateDevices -- with the plugin's scorer.  The allocation (request + fillGPUTotalMem,
 // devicehandler_gpu.go:98-133) is added to `used` in the SoA (updateCacheUsed).  Returns the minors mask
 // (bit 16*type + minor).
+// ro: a reservation-matched / -ignored pod's Reserve on the node as k_ds_views decided it (RsvOvr.ds_res 1: the
+// minors of the nominated reservation's / the node's view; allocateWithNominatedReservation, reservation.go:368-415)
 template <bool H>
 __device__ __noinline__ uint64_t ds_reserve(const SoA& s, int64_t i, const DevPod& p, const KArgs& k, DsAff a,
-                                            int8_t* vf_out = nullptr) {
+                                            int8_t* vf_out = nullptr, const RsvOvr* ro = nullptr) {
   uint64_t msk[4], out = 0;
 #pragma unroll
   for (int w = 0; w < 4; w++) msk[w] = dsmask(s, w, i);
@@ -925,6 +954,8 @@ __device__ __noinline__ uint64_t ds_reserve(const SoA& s, int64_t i, const DevPo
         const int w = DSX_VFFREE + 16 * (t - 1) + m;
         s.dsx[w * s.stride + i] = (int64_t)(dsxw(s, w, i) & ~(1ull << hvf[t - 1][m]));
       }
+    } else if (ro && ro->ds_res) {
+      take = ro->ds_res == 1 ? (uint32_t)((ro->ds_minors >> (16 * t)) & 0xFFFFu) : 0u;
     } else {
       int64_t score[DS_MINORS];
       GpuMasks g;
@@ -2463,7 +2494,24 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
   }
   // ---- DeviceShare.Filter + raw Score  plugin.go:311-365, scoring.go:45-103 (Filter passes and Score
   // reads the devices of the affinity when the topology manager stored one)
-  if (ds_here && o.status == KE_CODE_SUCCESS) ds_filter_score<H>(s, i, p, k, o, stored, DsAff{stored && o.aff != 0, o.aff});
+  // a reservation-matched / -ignored pod on a node of its device-holding reservations: the allocate-from-reservation
+  // outcome k_ds_views computed (deviceshare/plugin.go:350-364, scoring.go:83-102; no NUMA policy on pod or node)
+  const RsvOvr* ro = (nf & NF_RSV_CS) ? rsv_ovr_of(s, i) : nullptr;
+  if (ds_here && o.status == KE_CODE_SUCCESS) {
+    if (ro && ro->ds_on) {
+      o.status = ro->ds_st;
+      o.reason = ro->ds_reason;
+      o.ds = ro->ds_raw;
+    } else {
+      ds_filter_score<H>(s, i, p, k, o, stored, DsAff{stored && o.aff != 0, o.aff});
+    }
+  }
+  // the Reservation Filter of a pod with a reservation affinity (reservation/plugin.go:316-318, 351-442): only the
+  // nodes of its matched reservations where one fits
+  if ((k.flags & AF_RSV_ONLY) && o.status == KE_CODE_SUCCESS && !(ro && ro->rfilter == 1)) {
+    o.status = KE_CODE_UNSCHEDULABLE;
+    o.reason = KE_REASON_RSV_AFFINITY;
+  }
   if (o.status != KE_CODE_SUCCESS) {
     o.total = -1;
     o.ds = 0;
@@ -3297,11 +3345,19 @@ __global__ __launch_bounds__(256) void k_argmax1(const uint16_t* __restrict__ sc
 // node or -1, its n, max, preferredNode or -1}.
 // With a reservation affinity only the pairs' allowed nodes pass the Reservation Filter: k_argmax1's winner
 // does not count and the others are infeasible.
+// A DeviceShare pod (dsraw != nullptr): a node's plugin total includes DeviceShare's normalized score, as in
+// k_argmax1.  A winner whose pair carries RSV_PAIR_RESERVE_FAILS is not placed (its DeviceShare Reserve fails).
 __global__ __launch_bounds__(64) void k_rsv_pick(const uint16_t* __restrict__ scores, const RsvPair* __restrict__ pr,
                                                  int K, int64_t w, int affinity, uint32_t* __restrict__ cand,
-                                                 int32_t* __restrict__ out) {
+                                                 int32_t* __restrict__ out, const uint16_t* __restrict__ dsraw,
+                                                 const uint32_t* __restrict__ dsmax1, int32_t wds) {
   const int l = (int)threadIdx.x;
-  auto feasible = [&](const RsvPair& q) { return scores[q.node] != 0 && q.allowed != 0; };
+  auto feasible = [&](const RsvPair& q) { return scores[q.node] != 0 && (q.allowed & RSV_PAIR_ALLOWED) != 0; };
+  auto total = [&](int32_t node) -> uint32_t {
+    uint32_t v = scores[node];
+    if (dsraw && v) v += (uint32_t)(wds * ds_norm((int32_t)dsraw[node] - 1, *dsmax1));
+    return v;
+  };
   int64_t bo = INT64_MAX;
   int32_t bn = INT32_MAX;
   for (int i = l; i < K; i += 64) {
@@ -3331,7 +3387,7 @@ __global__ __launch_bounds__(64) void k_rsv_pick(const uint16_t* __restrict__ sc
   if (mx > 0 || affinity)
     for (int i = l; i < K; i += 64) {
       const RsvPair q = pr[i];
-      const uint32_t v = scores[q.node];
+      const uint32_t v = total(q.node);
       if (!feasible(q)) continue;
       const int64_t n = mx > 0 ? 100 * (int64_t)(q.node == pref ? 1000 : q.raw) / mx : 0;
       const uint64_t key = ((uint64_t)(v + w * n) << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)q.node);
@@ -3342,16 +3398,18 @@ __global__ __launch_bounds__(64) void k_rsv_pick(const uint16_t* __restrict__ sc
     best = o > best ? o : best;
   }
   const int32_t win = best ? (int32_t)(KEY_IDX_MASK - (uint32_t)(best & KEY_IDX_MASK)) : -1;
-  int32_t nw = 0;  // the winner's n (0 unless it holds matched reservations)
-  if (win >= 0 && mx > 0)
+  int32_t nw = 0, fails = 0;  // the winner's n (0 unless it holds matched reservations), its Reserve failing
+  if (win >= 0)
     for (int i = l; i < K; i += 64) {
       const RsvPair q = pr[i];
-      if (q.node == win) nw = (int32_t)(100 * (int64_t)(q.node == pref ? 1000 : q.raw) / mx);
+      if (q.node == win && mx > 0) nw = (int32_t)(100 * (int64_t)(q.node == pref ? 1000 : q.raw) / mx);
+      if (q.node == win && (q.allowed & RSV_PAIR_RESERVE_FAILS)) fails = 1;
     }
-  for (int m = 32; m; m >>= 1) nw = max(nw, __shfl_xor(nw, m));
+  for (int m = 32; m; m >>= 1) nw = max(nw, __shfl_xor(nw, m)), fails = max(fails, __shfl_xor(fails, m));
   if (l == 0) {
-    cand[0] = win >= 0 ? ((uint32_t)scores[win] << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)win) : 0u;
-    out[0] = win;
+    const bool placed = win >= 0 && !fails;
+    cand[0] = placed ? (total(win) << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)win) : 0u;
+    out[0] = placed ? win : -1;
     out[1] = nw;
     out[2] = mx;
     out[3] = pref;
@@ -3374,9 +3432,17 @@ template <int S>
 __global__ __launch_bounds__(64) void k_rsv_stage(const uint16_t* __restrict__ scores, const RsvPair* __restrict__ pr,
                                                   int K, int lo, int hi, int64_t w, int affinity,
                                                   uint32_t* __restrict__ cand, RsvPickSt* __restrict__ st,
-                                                  int32_t* __restrict__ out) {
+                                                  int32_t* __restrict__ out, const uint16_t* __restrict__ dsraw,
+                                                  const uint32_t* __restrict__ dsmax1, int32_t wds) {
   const int l = (int)threadIdx.x;
-  auto mine = [&](const RsvPair& q) { return q.node >= lo && q.node < hi && scores[q.node] != 0 && q.allowed != 0; };
+  auto mine = [&](const RsvPair& q) {
+    return q.node >= lo && q.node < hi && scores[q.node] != 0 && (q.allowed & RSV_PAIR_ALLOWED) != 0;
+  };
+  auto total = [&](int32_t node) -> uint32_t {  // as k_rsv_pick
+    uint32_t v = scores[node];
+    if (dsraw && v) v += (uint32_t)(wds * ds_norm((int32_t)dsraw[node] - 1, *dsmax1));
+    return v;
+  };
   const int32_t pref = S >= 2 ? (st->order == INT64_MAX ? -1 : st->node) : -1;
   if constexpr (S == 0) {
     int64_t bo = INT64_MAX;
@@ -3404,7 +3470,7 @@ __global__ __launch_bounds__(64) void k_rsv_stage(const uint16_t* __restrict__ s
         const RsvPair q = pr[i];
         if (!mine(q)) continue;
         const int64_t n = mx > 0 ? 100 * (int64_t)(q.node == pref ? 1000 : q.raw) / mx : 0;
-        const uint64_t key = ((uint64_t)(scores[q.node] + w * n) << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)q.node);
+        const uint64_t key = ((uint64_t)(total(q.node) + w * n) << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)q.node);
         best = key > best ? key : best;
       }
     for (int m = 32; m; m >>= 1) {
@@ -3422,13 +3488,15 @@ __global__ __launch_bounds__(64) void k_rsv_stage(const uint16_t* __restrict__ s
           nw = (int32_t)(100 * (int64_t)(pr[i].node == pref ? 1000 : pr[i].raw) / st->mx);
     for (int m = 32; m; m >>= 1) nw = max(nw, __shfl_xor(nw, m));
     if (l == 0) {
-      st->wt = win >= lo && win < hi ? (int32_t)scores[win] : 0;
+      st->wt = win >= lo && win < hi ? (int32_t)total(win) : 0;
       st->nw = nw;
     }
   } else {
     if (l == 0) {
       const uint64_t best = st->best;
-      const int32_t win = best ? (int32_t)(KEY_IDX_MASK - (uint32_t)(best & KEY_IDX_MASK)) : -1;
+      int32_t win = best ? (int32_t)(KEY_IDX_MASK - (uint32_t)(best & KEY_IDX_MASK)) : -1;
+      for (int i = 0; win >= 0 && i < K; i++)  // (every rank holds every pair)
+        if (pr[i].node == win && (pr[i].allowed & RSV_PAIR_RESERVE_FAILS)) win = -1;
       cand[0] = win >= 0 ? ((uint32_t)st->wt << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)win) : 0u;
       out[0] = win;
       out[1] = st->nw;
@@ -4463,8 +4531,10 @@ __device__ __forceinline__ uint64_t ds_reserve_wave(const SoA& s, int64_t i, con
   uint64_t msk[4], out = 0;
 #pragma unroll
   for (int w = 0; w < 4; w++) msk[w] = dsmask(s, w, i);
-  if ((msk[DSM_EXISTS] & (DSX_TOPO | DSX_TABLE | DSX_HONOR)) || (p.flags & (PF_GPU_PART_SPEC | 7u * PF_GPU_SCOPE0))) {
-    if (lane == 0) out = ds_reserve<false>(s, i, p, k, DsAff{false, 0u});
+  const RsvOvr* ro = s.n_rovr ? rsv_ovr_of(s, i) : nullptr;  // a matched pod's Reserve from k_ds_views
+  if (ro && !ro->ds_res) ro = nullptr;
+  if (ro || (msk[DSM_EXISTS] & (DSX_TOPO | DSX_TABLE | DSX_HONOR)) || (p.flags & (PF_GPU_PART_SPEC | 7u * PF_GPU_SCOPE0))) {
+    if (lane == 0) out = ds_reserve<false>(s, i, p, k, DsAff{false, 0u}, nullptr, ro);
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(out >> 32), 0) << 32) |
            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)out, 0);
   }
@@ -5979,6 +6049,84 @@ __global__ __launch_bounds__(64) void k_rsv_views(SoA s, const DevPod* __restric
   }
 }
 
+// The DeviceShare allocate-from-reservation views of one reservation-matched / -ignored pod (pods[0]) on the nodes of
+// its device-holding reservations (deviceshare/reservation.go:207-366): one view per workgroup, its
+// lane 0 runs AutopilotAllocator over the node's row with the view's preemptible / requiredDeviceResources /
+// required and preferred minors (ds_type_view with rv) -- Prepare, the Filter's allocation without a scorer (the
+// first failing type's status in the order GPU, RDMA, FPGA), score (Σ scoreNode over the types the view keeps) and
+// the Reserve-phase allocation with the plugin's scorer (the minors; 0 when it fails).  Reads the SoA only.
+__global__ __launch_bounds__(64) void k_ds_views(SoA s, const DevPod* __restrict__ pods, const DsView* __restrict__ views,
+                                                 DsViewOut* __restrict__ out, KArgs k) {
+  if (threadIdx.x != 0) return;
+  const DsView* v = views + blockIdx.x;
+  const DevPod p = pods[0];
+  const int64_t i = v->node;
+  uint64_t msk[4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) msk[w] = dsmask(s, w, i);
+  for (int t = 0; t < 3; t++)  // the view's preemptible keys are used keys of their instances (calcFreeWithPreemptible)
+    for (int m = 0; m < DS_MINORS; m++) {
+      const int bit = 16 * t + m;
+      if (!((v->pre_in >> bit) & 1)) continue;
+      for (int q = 0; q < DS_NK[t]; q++)
+        if ((v->pre_keys[q] >> bit) & 1) msk[ds_hu_word(t)] |= 1ull << ds_hu_bit(t, m, q);
+    }
+  DsViewOut o;
+  o.st = KE_CODE_SUCCESS;
+  o.reason = KE_REASON_NONE;
+  o.raw = 0;
+  o.minors = 0;
+  for (int t = 0; t < 3; t++)  // Prepare: a requested type without devices
+    if (p.ds_cnt[t] && !((msk[DSM_EXISTS] >> (16 * t)) & 0xFFFF)) {
+      o.st = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE;
+      o.reason = KE_REASON_DS_INSUFFICIENT_GPU + t;
+      out[blockIdx.x] = o;
+      return;
+    }
+  int64_t raw = 0;
+  for (int t = 0; t < 3; t++) {
+    if (!p.ds_cnt[t]) continue;
+    GpuMasks g;
+    int64_t tot[3], fre[3];
+    const bool present = ds_type_view(s, i, t, msk, p, k, DsAff{false, 0u}, g, tot, fre, nullptr, 0xFFFFu, v);
+    if (o.st == KE_CODE_SUCCESS) {
+      int why = KE_REASON_DS_INSUFFICIENT_GPU + t;
+      int st = 0;
+      if (t == KE_DEV_GPU) {
+        uint32_t unused;
+        st = gpu_allocate(s, i, msk[DSM_EXISTS], p, g, false, nullptr, &unused, &why);
+      } else if (__builtin_popcount(g.dflt) < p.ds_cnt[t]) {
+        st = KE_CODE_UNSCHEDULABLE;
+      }
+      if (st) o.st = st, o.reason = why;
+    }
+    if (present) raw += ds_weighted(k, t, tot, fre, p);  // resourceAllocationScorer.scoreNode
+  }
+  o.raw = raw;
+  if (o.st == KE_CODE_SUCCESS) {
+    uint64_t minors = 0;
+    bool ok = true;
+    for (int t = 0; t < 3 && ok; t++) {
+      if (!p.ds_cnt[t]) continue;
+      int64_t score[DS_MINORS];
+      GpuMasks g;
+      int64_t tot[3], fre[3];
+      ds_type_view(s, i, t, msk, p, k, DsAff{false, 0u}, g, tot, fre, score, 0xFFFFu, v);
+      uint32_t take = 0;
+      if (t == KE_DEV_GPU) {
+        int why = 0;
+        ok = gpu_allocate(s, i, msk[DSM_EXISTS], p, g, true, score, &take, &why) == 0 && take != 0;
+      } else {
+        take = default_pick(g.dflt, p.ds_cnt[t], score, g.pref);
+        ok = __builtin_popcount(take) >= p.ds_cnt[t];
+      }
+      minors |= (uint64_t)take << (16 * t);
+    }
+    o.minors = ok ? minors : 0;
+  }
+  out[blockIdx.x] = o;
+}
+
 // A singleton batch of a pod that may bind CPUs, after k_select: selectHost's node, then Reserve in
 // profile order — LoadAware, NodeNUMAResource (the NUMA allocation on the affinity Admit picks and the
 // cpuset; a failed Allocate fails Reserve and the pod stays unplaced), DeviceShare.  One thread: the
@@ -6170,7 +6318,8 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
       RPROF(5)
       if (ds_here)
         alloc = ds_reserve<true>(s, node, pod, k, DsAff{stored && aff != 0 && !(k.flags & AF_DS_NO_NUMA), aff},
-                           s.vfo ? s.vfo + (int64_t)base * 2 * DS_MINORS : nullptr);
+                           s.vfo ? s.vfo + (int64_t)base * 2 * DS_MINORS : nullptr,
+                           (nf & NF_RSV_CS) ? rsv_ovr_of(s, node) : nullptr);
       out_node = (int32_t)node + global_offset;
       out_score = key_score(w);
       if (quota) quota_reserve_g(s, pod, qreq);  // ElasticQuota Reserve
@@ -6382,6 +6531,8 @@ struct DeviceState {
   int64_t rsv_cap = 0;              // bytes
   void* d_rsv_views = nullptr;      // k_rsv_views: views, outputs, the pod
   int64_t rsv_views_cap = 0;
+  void* d_ds_views = nullptr;       // k_ds_views: views, outputs, the pod
+  int64_t ds_views_cap = 0;
   RsvOvr* d_rovr = nullptr;         // the segment's allocate-from-reservation decisions (SoA::rovr)
   int64_t rovr_cap = 0;
   int32_t* d_rsv_out = nullptr;     // [4]
@@ -6511,6 +6662,36 @@ int device_rsv_views(Context* ctx, const ke_pod& pod, int64_t now, const std::ve
   return KE_OK;
 }
 
+static KArgs make_kargs(const Context* ctx, int64_t now);
+// k_ds_views for one reservation-matched / -ignored DeviceShare pod: its views on the current device state
+// (synchronous, like device_rsv_views)
+int device_ds_views(Context* ctx, const ke_pod& pod, int64_t now, const std::vector<DsView>& views,
+                    std::vector<DsViewOut>& out) {
+  DeviceState* d = ctx->dev;
+  out.assign(views.size(), DsViewOut{});
+  if (views.empty()) return KE_OK;
+  HIP_OK(hipSetDevice(d->device));
+  int rc = device_refresh(ctx, now);  // the rows as the segment will see them
+  if (rc) return rc;
+  if (!d->soa.ds) return fail(KE_ERR_DEVICE, "DeviceShare views without a device SoA");
+  for (const DsView& v : views)
+    if (v.node < 0 || v.node >= ctx->n_nodes) return fail(KE_ERR_DEVICE, "DeviceShare view node out of range");
+  const DevPod dp = make_dev_pod(ctx->cfg, pod, pod_hints(*ctx, pod), &ctx->tmpl);
+  const KArgs k = make_kargs(ctx, now);
+  const size_t vb = sizeof(DsView) * views.size(), ob = sizeof(DsViewOut) * views.size();
+  rc = ensure((void**)&d->d_ds_views, &d->ds_views_cap, (int64_t)(vb + ob + sizeof(DevPod)));
+  if (rc) return rc;
+  uint8_t* base = (uint8_t*)d->d_ds_views;
+  HIP_OK(hipMemcpyAsync(base, views.data(), vb, hipMemcpyHostToDevice, d->stream));
+  HIP_OK(hipMemcpyAsync(base + vb + ob, &dp, sizeof(DevPod), hipMemcpyHostToDevice, d->stream));
+  hipLaunchKernelGGL(k_ds_views, dim3((unsigned)views.size()), dim3(64), 0, d->stream, d->soa,
+                     (const DevPod*)(base + vb + ob), (const DsView*)base, (DsViewOut*)(base + vb), k);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(out.data(), base + vb, ob, hipMemcpyDeviceToHost, d->stream));
+  HIP_OK(hipStreamSynchronize(d->stream));
+  return KE_OK;
+}
+
 // k_rsv_pick's result of the last device_schedule (a segment of one KE_RSV_MATCHED pod)
 int device_rsv_result(Context* ctx, int32_t* out4) {
   DeviceState* d = ctx->dev;
@@ -6533,7 +6714,8 @@ void device_destroy(Context* ctx) {
                   d->d_numaalloc, d->d_numarows, d->d_defer, d->d_defer_cnt, d->soa.cs, d->soa.cpu,
                   d->d_cpurows, d->d_cpusets, d->d_aff, d->soa.qt, d->soa.qm, d->d_sched, d->d_stale,
                   d->d_stale_cnt, d->d_pre, d->d_trows, d->d_tcnt, d->d_parts_done, d->d_scores2, d->d_split2, d->d_chg, d->soa.rec, d->soa.pt, d->soa.kerr,
-                  d->soa.xf, d->soa.xm, d->d_xrows, d->soa.dsx, d->d_ph, d->d_vfo, d->d_rsv, d->d_rsv_out, d->d_rsv_st};
+                  d->soa.xf, d->soa.xm, d->d_xrows, d->soa.dsx, d->d_ph, d->d_vfo, d->d_rsv, d->d_rsv_out, d->d_rsv_st,
+                  d->d_rsv_views, d->d_ds_views, d->d_rovr};
   if (d->estream) (void)hipStreamSynchronize(d->estream);
   if (d->estream2) (void)hipStreamSynchronize(d->estream2);
   for (void* p : ptrs)
@@ -7218,6 +7400,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
     HIP_OK(hipMemsetAsync(d->d_defer_cnt, 0, sizeof(uint32_t) * n_batches, d->stream));
   }
   KArgs k = make_kargs(ctx, now);
+  if (ctx->rsv_affinity) k.flags |= AF_RSV_ONLY;  // the Reservation Filter: RsvOvr.rfilter of the pod's nodes
   if (!ctx->rsv_pairs.empty() || ctx->rsv_affinity) {  // one matched pod (ke_schedule's segment of its own)
     if (n_pods != 1) return fail(KE_ERR_UNSUPPORTED, "matched reservations need a singleton segment");
     for (const RsvPair& q : ctx->rsv_pairs)
@@ -7431,7 +7614,8 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
                            es, scores, 0, N, d->d_dsraw, d->d_dsmax, k.wp_ds, d->d_cand, d->d_cand_cnt);
         if (!ctx->rsv_pairs.empty() || ctx->rsv_affinity) {  // the pod's matched reservations: the Reservation plugin
           hipLaunchKernelGGL(k_rsv_pick, dim3(1), dim3(64), 0, es, scores, d->d_rsv, (int)ctx->rsv_pairs.size(),
-                             (int64_t)ctx->cfg.weight_reservation, (int)ctx->rsv_affinity, d->d_cand, d->d_rsv_out);
+                             (int64_t)ctx->cfg.weight_reservation, (int)ctx->rsv_affinity, d->d_cand, d->d_rsv_out,
+                             ds ? d->d_dsraw : nullptr, d->d_dsmax, k.wp_ds);
           HIP_OK(hipMemcpyAsync(d->h_rsv_out.data(), d->d_rsv_out, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, es));
         }
       } else if (!sharded && parts > 1) {
@@ -7468,18 +7652,19 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
           const int64_t wr = (int64_t)ctx->cfg.weight_reservation;
           const int aff = (int)ctx->rsv_affinity;
           RsvPickSt* st = d->d_rsv_st;
+          const uint16_t* rds = ds ? d->d_dsraw : nullptr;
           const bool coll = !d->loopback && d->comm;
-          hipLaunchKernelGGL(k_rsv_stage<0>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out);
+          hipLaunchKernelGGL(k_rsv_stage<0>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out, rds, d->d_dsmax, k.wp_ds);
           if (coll) RCCL_OK(ncclAllReduce(&st->order, &st->order, 1, ncclInt64, ncclMin, d->comm, es));
-          hipLaunchKernelGGL(k_rsv_stage<1>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out);
+          hipLaunchKernelGGL(k_rsv_stage<1>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out, rds, d->d_dsmax, k.wp_ds);
           if (coll) RCCL_OK(ncclAllReduce(&st->node, &st->node, 1, ncclInt32, ncclMin, d->comm, es));
-          hipLaunchKernelGGL(k_rsv_stage<2>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out);
+          hipLaunchKernelGGL(k_rsv_stage<2>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out, rds, d->d_dsmax, k.wp_ds);
           if (coll) RCCL_OK(ncclAllReduce(&st->mx, &st->mx, 1, ncclInt32, ncclMax, d->comm, es));
-          hipLaunchKernelGGL(k_rsv_stage<3>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out);
+          hipLaunchKernelGGL(k_rsv_stage<3>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out, rds, d->d_dsmax, k.wp_ds);
           if (coll) RCCL_OK(ncclAllReduce(&st->best, &st->best, 1, ncclUint64, ncclMax, d->comm, es));
-          hipLaunchKernelGGL(k_rsv_stage<4>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out);
+          hipLaunchKernelGGL(k_rsv_stage<4>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out, rds, d->d_dsmax, k.wp_ds);
           if (coll) RCCL_OK(ncclAllReduce(&st->wt, &st->wt, 2, ncclInt32, ncclMax, d->comm, es));  // wt, nw
-          hipLaunchKernelGGL(k_rsv_stage<5>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out);
+          hipLaunchKernelGGL(k_rsv_stage<5>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out, rds, d->d_dsmax, k.wp_ds);
           HIP_OK(hipMemcpyAsync(d->h_rsv_out.data(), d->d_rsv_out, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, es));
         }
       }

@@ -57,8 +57,9 @@ enum NodeFlag : uint32_t {
   NF_CPU_BIND0 = 1u << 20,        // 2 bits: the node's CPU bind policy (KE_NODE_CPU_BIND_*)
   NF_CPUS_VALID = 1u << 22,       // the node has a valid CPU topology table (cpuset pods can bind)
   NF_CPU_NUMA_MOST = 1u << 23,    // GetNUMAAllocateStrategy == MostAllocated (cpu accumulator order)
-  NF_RSV_CS = 1u << 24,           // the current KE_RSV_MATCHED pod's allocate-from-reservation outcome on this node
-                                  // is in SoA::rovr (RsvOvr): it replaces the cpuset trial / allocation
+  NF_RSV_CS = 1u << 24,           // the current KE_RSV_MATCHED / IGNORED pod's allocate-from-reservation outcome on
+                                  // this node is in SoA::rovr (RsvOvr): it replaces the cpuset trial / allocation,
+                                  // DeviceShare's Filter / Score / Reserve, or carries the Reservation Filter
 };
 // A KE_RSV_MATCHED pod's allocate-from-reservation trial on one node (k_rsv_views): takePreferredCPUs with
 // preferredCPUs `pref` (getAvailableCPUs(preferred): RefCount-- on each, nodenumaresource/reservation.go:303-339),
@@ -75,12 +76,45 @@ struct RsvViewOut {
 };
 // The decisions the host takes from them per node (ke_host.cpp resv_prepare): the Filter's trial allocation
 // (0 = the node's own, 1 = satisfied from a reservation, 2 = "Reservation(s) ..." Unschedulable) and Reserve's
-// (0 = the node's own allocation, 1 = `cpus` from the nominated reservation, 2 = Reserve fails)
+// (0 = the node's own allocation, 1 = `cpus` from the nominated reservation, 2 = Reserve fails).
+// DeviceShare (k_ds_views): ds_on = the Filter status / reason and raw Score below replace the node's own
+// (tryAllocateFromReservation / scoreWithNominatedReservation, deviceshare/plugin.go:350-364, scoring.go:83-102);
+// ds_res = Reserve's devices: 0 the node's own allocation, 1 `ds_minors` (bit 16*type + minor), 2 Reserve fails.
+// rfilter (a reservation affinity, AF_RSV_ONLY): 1 the Reservation Filter passes on the node (else it fails).
 struct RsvOvr {
   int32_t node;
   int8_t filter, reserve;
-  int16_t pad;
+  int8_t ds_on, ds_res;
+  uint8_t ds_st, ds_reason;
+  int8_t rfilter, pad;
+  int16_t ds_raw, pad2;
+  uint64_t ds_minors;
   uint64_t cpus[4];
+};
+// One DeviceShare allocate-from-reservation view of a node (k_ds_views): the allocator's arguments a
+// reservation-matched (or -ignored) pod sees beyond the node's row (AutopilotAllocator with preemptible /
+// requiredDeviceResources / required + preferred minors, deviceshare/reservation.go:207-366):
+//   pre:  the preemptible beyond the node's unmatched restore (already in the row's used), per instance and key
+//         (bit 16*type + minor in pre_in, keys in pre_keys[k]): the row's used becomes max(0, used - pre);
+//   cap:  requiredDeviceResources of a Restricted reservation: per type with cap_in bits only those instances,
+//         free = MinResourceList(free, cap) (keys of both);
+//   pref / rreq: defaultAllocateDevices' preferred minors (ordered first) and required minors (only these).
+struct DsView {
+  int32_t node;
+  int32_t pad;
+  uint16_t pref[3], rreq[3], cap_in[3];
+  uint16_t pad2;
+  uint64_t pre_in;
+  uint64_t pre_keys[3], cap_keys[3];
+  int64_t pre[3][16][3];
+  int64_t cap[3][16][3];
+};
+// its outcome: the Filter's allocation without a scorer (status, reason), AutopilotAllocator.score (raw) and the
+// Reserve-phase allocation with the plugin's scorer (minors, 0 when it fails)
+struct DsViewOut {
+  int32_t st, reason;
+  int64_t raw;
+  uint64_t minors;
 };
 KE_HD inline int nf_cpu_bind(uint32_t f) { return (int)((f >> 20) & 3u); }
 KE_HD inline int nf_numa_policy(uint32_t f) { return (int)((f >> 16) & 3u); }
@@ -321,6 +355,7 @@ enum ArgFlag : uint32_t {
   AF_EXT = 1u << 9,                 // NodeResourcesFitPlus / ScarceResourceAvoidance / NodeResourcesFit (ext SoA)
   AF_FIT_FILTER = 1u << 10,         // NodeResourcesFit's Filter in the profile
   AF_FIT_MOST = 1u << 11,           // NodeResourcesFit ScoringStrategy MostAllocated
+  AF_RSV_ONLY = 1u << 12,           // a reservation-affinity pod: only NF_RSV_CS nodes whose RsvOvr.rfilter is 1 pass
 };
 constexpr int NUM_XS = 8;  // ext slots: the resource ids NodeResourcesFitPlus / NodeResourcesFit read
 struct KArgs {

@@ -5146,11 +5146,11 @@ int or_pod_release(or_cluster* c, const ke_pod* pod, const ke_pod_allocation* a,
     n->node.requested[KE_RES_CPU] -= pod->requests[KE_RES_CPU];
     n->node.requested[KE_RES_MEMORY] -= pod->requests[KE_RES_MEMORY];
     n->node.pod_count--; /* NodeInfo.RemovePod */
-    if (c->cfg.ext.weight_fitplus > 0 || c->cfg.ext.weight_sra > 0 || c->cfg.fit.weight > 0 || c->cfg.fit.filter)
-      for (int32_t e = 0; e < pod->n_xres; e++) {
-        ke_node_resource* r = (ke_node_resource*)node_xres(n, pod->xres_id[e]);
-        if (r) r->requested -= pod->xres_value[e];
-      }
+    /* NodeInfo.RemovePod: Requested.ScalarResources by resource id, whichever plugins read them */
+    for (int32_t e = 0; e < pod->n_xres; e++) {
+      ke_node_resource* r = (ke_node_resource*)node_xres(n, pod->xres_id[e]);
+      if (r) r->requested -= pod->xres_value[e];
+    }
     const int parked = !n->cpus && n->kept_cpus; /* NRT deleted: the NodeAllocation is parked */
     if (cpus_valid(n) || parked) {
       or_cpus* x = parked ? n->kept_cpus : n->cpus;

@@ -86,3 +86,55 @@ def test_score_reservation(lib, case):
     assert s == case["want_score"], case["source"]
     if case["want_normalize"] is not None:  # DefaultReservationNormalizeScore over the one-entry list
         assert normalize_scores([s]) == [case["want_normalize"]], case["source"]
+
+
+def test_filter_nominate_reservation_full_cycle(lib):
+    """Test_Plugin_FilterNominateReservation (plugin_test.go:2681-2823) through the oracle's whole cycle (the GPU
+    twin: tests/test_gpu_ds_reservation.py): the affinity pod takes GPU 1 out of reservation-1, and fits nowhere
+    once allocated-pod-1 holds GPUs 1 and 2."""
+    import test_gpu_ds_reservation as g
+    for owned in (False, True):
+        o = Oracle(abi.default_config(1), 1)
+        g._filter_nominate_case(o, owned)
+        pod = model.make_pod(requests={"koordinator.sh/gpu": "100"})
+        pod.reservation_matched = abi.RSV_AFFINITY
+        pod.n_xres, pod.xres_id[0], pod.xres_value[0], pod.xres_request_mask = 1, g.KOORD_GPU, 100, 1 << g.KOORD_GPU
+        c, s = o.schedule([pod], cases.NOW, matches=[[0]])
+        a = o.last_allocations()
+        if owned:
+            assert c[0] == -1
+        else:
+            assert c[0] == 0 and a["reservation"][0] == 1 and int(a["device_minors"][0]) == 1 << 1
+            assert int(o.reservation_allocs_get()["owner_device"][0, abi.DEV_GPU, 1, 0]) == 100
+
+
+def test_ds_matched_checks_agree(lib):
+    """The refusals of the DeviceShare allocate-from-reservation path agree between the product's argument checks
+    and the oracle: a hinted DeviceShare pod (or one with a NUMA policy) matching a device-holding reservation is
+    refused; a plain DeviceShare pod passes the checks (the product then needs its device)."""
+    import ds_rsv_cases as dc
+    from koordinator_amd import Evaluator, KoordEvalError
+    (ev, o), pods, matches, rs = dc.setup(lambda cfg, n: [Evaluator(cfg), Oracle(cfg, n)], 60, 7201, 40, match=1.0,
+                                          affinity=0.0, ignored=0.0)
+    dsp = [p for p in range(len(pods)) if pods["device_requests"][p].any() and matches[p]
+           and any(rs["available"][r] for r in matches[p])]
+    p = dsp[0]
+    one = pods[p:p + 1].copy()
+    with pytest.raises(KoordEvalError) as e:
+        ev.schedule(one, cases.NOW, matches=[matches[p]])
+    assert e.value.code == abi.ERR_NO_DEVICE
+    one["numa_topology_policy"] = abi.NUMA_POLICY_BEST_EFFORT
+    with pytest.raises(KoordEvalError) as e:
+        ev.schedule(one, cases.NOW, matches=[matches[p]])
+    assert e.value.code == abi.ERR_UNSUPPORTED
+    with pytest.raises(RuntimeError, match=f"rc={abi.ERR_UNSUPPORTED}"):
+        o.schedule(one, cases.NOW, matches=[matches[p]])
+    one["numa_topology_policy"] = 0
+    one["reservation_matched"] = abi.RSV_IGNORED
+    one["numa_topology_policy"] = abi.NUMA_POLICY_RESTRICTED
+    with pytest.raises(KoordEvalError) as e:
+        ev.schedule(one, cases.NOW)
+    assert e.value.code == abi.ERR_UNSUPPORTED
+    with pytest.raises(RuntimeError, match=f"rc={abi.ERR_UNSUPPORTED}"):
+        o.schedule(one, cases.NOW, matches=[[]])
+    ev.close()
