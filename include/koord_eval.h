@@ -1122,6 +1122,22 @@ int ke_decode_device_flags(const char* device_json, int64_t device_len, const ch
  * resource manager's allocation state (zone allocations, RefCounts, NUMA status) is the scheduler's own: 0. */
 int ke_decode_nrt(const char* json, int64_t len, ke_node* node, int32_t zone_cap, ke_numa_zone* zones, int32_t* n_zones,
                   int32_t cpu_cap, ke_cpu* cpus, int32_t* n_cpus);
+/* Reservation (apis/scheduling/v1alpha1/reservation_types.go) as the reservation cache builds its ReservationInfo
+ * (frameworkext/reservation_info.go:87-130): available = scheduled (status.nodeName) and phase Available
+ * (util/reservation/reservation.go:238-240; a malformed restricted-options annotation, a ParseError, clears it);
+ * allocatable = ReservationRequests (status.allocatable when available, else the template's PodRequests,
+ * reservation.go:393-404) -- cpu / memory into *out, every other non-zero name into res[] by its index in
+ * xres_names ("pods" = KE_RSV_RES_PODS; a name without an id -> KE_ERR_UNSUPPORTED), *n_res entries;
+ * allocated = status.allocated masked by rInfo.ResourceNames (the Restricted options annotation narrows them:
+ * names_excluded / excluded); reserved = the node-reservation annotation (util/node.go:85-120); allocateOnce
+ * (default true), allocatePolicy, the reservation-order label, allocated_pods = len(status.currentOwners), uid =
+ * FNV-1a of metadata.uid.  *alloc (optional): the reserve pod's holdings from its device-allocated and
+ * resource-status annotations (the owner parts are the owner pods': 0 here); holds is derived from them and from
+ * the entries (KE_RSV_OTHER_ALLOCATABLE).  out->node is -1: the caller maps status.nodeName, copied NUL-terminated
+ * into node_name[name_cap], to its node index. */
+int ke_decode_reservation(const char* json, int64_t len, int32_t n_names, const char* const* xres_names,
+                          ke_reservation* out, ke_reservation_alloc* alloc, int32_t res_cap, ke_reservation_resource* res,
+                          int32_t* n_res, char* node_name, int32_t name_cap);
 
 /* ---- node sharding across GPUs (one process per GPU) ------------------------------------------
  * Replaces the upstream Parallelizer's fan-out of per-node Filter/Score over goroutines

@@ -537,6 +537,8 @@ EXPORTS = {
                                 C.POINTER(i32)]),
     "ke_decode_device": (C.c_int, [C.c_char_p, i64, i32, C.c_void_p, C.POINTER(i32), i32, C.c_void_p, C.POINTER(i32),
                                    C.POINTER(i32), C.POINTER(i32)]),
+    "ke_decode_reservation": (C.c_int, [C.c_char_p, i64, i32, C.c_void_p, C.POINTER(Reservation), C.c_void_p, i32,
+                                        C.c_void_p, C.POINTER(i32), C.c_char_p, i32]),
     "ke_node_resources_get": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p, C.POINTER(i32)]),
     "ke_label_id": (i32, [C.c_char_p]),
     "ke_set_pod_device_hints": (C.c_int, [C.c_void_p, i32, C.c_void_p]),

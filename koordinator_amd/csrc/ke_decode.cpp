@@ -1208,3 +1208,230 @@ int ke_decode_nrt(const char* js, int64_t len, ke_node* node, int32_t zone_cap, 
 }
 
 }  // extern "C"
+
+// ---- Reservation (apis/scheduling/v1alpha1/reservation_types.go) --------------------------------------------
+namespace {
+// a ResourceList's value by name as the reservation cache reads it: cpu MilliValue, every other name Value
+bool rl_get(const RL& rl, const std::string& name, int64_t* out) {
+  *out = 0;
+  auto it = rl.q.find(name);
+  if (it == rl.q.end()) return true;
+  int64_t v, m;
+  if (!nanos_value(it->second, &v, &m)) return false;
+  *out = name == "cpu" ? m : v;
+  return true;
+}
+const char* const DEV_TYPE_NAMES[KE_DEV_TYPES] = {"gpu", "rdma", "fpga"};
+const char* const DEV_KEY_NAMES[KE_DEV_TYPES][KE_DKEYS] = {
+    {"koordinator.sh/gpu-core", "koordinator.sh/gpu-memory", "koordinator.sh/gpu-memory-ratio"},
+    {"koordinator.sh/rdma", nullptr, nullptr},
+    {"koordinator.sh/fpga", nullptr, nullptr}};
+}  // namespace
+
+extern "C" {
+
+int ke_decode_reservation(const char* js, int64_t len, int32_t n_names, const char* const* xres_names, ke_reservation* out,
+                          ke_reservation_alloc* alloc, int32_t res_cap, ke_reservation_resource* res, int32_t* n_res,
+                          char* node_name, int32_t name_cap) {
+  if (!out || !n_res || res_cap < 0 || (res_cap && !res) || n_names < 0 || n_names > KE_MAX_XRES ||
+      (n_names && !xres_names) || name_cap < 0 || (name_cap && !node_name))
+    return bad("ke_decode_reservation arguments");
+  Value doc;
+  int rc = parse_doc(js, len, doc, "Reservation");
+  if (rc) return rc;
+  ke_reservation r{};
+  ke_reservation_alloc a{};
+  const Value* meta = doc.field("metadata");
+  const Value* spec = doc.field("spec");
+  const Value* status = doc.field("status");
+  std::map<std::string, std::string> ann, lab;
+  if ((rc = string_map(meta ? meta->field("annotations") : nullptr, ann, "metadata.annotations"))) return rc;
+  if ((rc = string_map(meta ? meta->field("labels") : nullptr, lab, "metadata.labels"))) return rc;
+  r.node = -1;
+  const std::string uid = str_or_empty(meta ? meta->field("uid") : nullptr);
+  r.uid = uid.empty() ? 0 : (int64_t)(fnv1a(uid) & (uint64_t)INT64_MAX);
+  // GetReservationNodeName = status.nodeName; IsReservationAvailable: scheduled and phase Available
+  // (util/reservation/reservation.go:238-240,263-265)
+  const std::string node = str_or_empty(status ? status->field("nodeName") : nullptr);
+  const std::string phase = str_or_empty(status ? status->field("phase") : nullptr);
+  bool available = !node.empty() && phase == "Available";
+  if (name_cap) {
+    if ((int64_t)node.size() + 1 > name_cap) return bad("status.nodeName longer than node_name");
+    std::memcpy(node_name, node.c_str(), node.size() + 1);
+  }
+  // spec.allocateOnce (default true, apis/extension/reservation.go:133-135), spec.allocatePolicy
+  const Value* once = spec ? spec->field("allocateOnce") : nullptr;
+  r.allocate_once = (!once || once->is_null()) ? 1 : (once->t == Value::BOOL ? (uint8_t)once->b : 2);
+  if (r.allocate_once > 1) return bad("spec.allocateOnce is not a boolean");
+  const std::string pol = str_or_empty(spec ? spec->field("allocatePolicy") : nullptr);
+  if (pol == "" || pol == "Default") r.allocate_policy = KE_RSV_POLICY_DEFAULT;
+  else if (pol == "Aligned") r.allocate_policy = KE_RSV_POLICY_ALIGNED;
+  else if (pol == "Restricted") r.allocate_policy = KE_RSV_POLICY_RESTRICTED;
+  else return unsup("allocate policy \"" + pol + "\"");
+  // the reservation-order label (findMostPreferredReservationByOrder, reservation/scoring.go:169-189): unparsable = none
+  if (const std::string* o = lookup(lab, "scheduling.koordinator.sh/reservation-order")) {
+    int64_t v;
+    if (parse_int64(*o, &v)) r.order = v;
+  }
+  // ReservationRequests (reservation.go:393-404): status.allocatable when available, else the template pod's
+  // PodRequests
+  std::map<std::string, __int128> alloc_q;
+  if (available) {
+    RL st;
+    if (!resource_list(status ? status->field("allocatable") : nullptr, st))
+      return st.overflow ? unsup("status.allocatable quantity out of range") : bad("status.allocatable");
+    alloc_q = st.q;
+  } else {
+    const Value* tspec = spec && spec->field("template") ? spec->field("template")->field("spec") : nullptr;
+    std::vector<Container> cs, ics;
+    if ((rc = containers(tspec ? tspec->field("containers") : nullptr, cs, "spec.template.spec.containers"))) return rc;
+    if ((rc = containers(tspec ? tspec->field("initContainers") : nullptr, ics, "spec.template.spec.initContainers"))) return rc;
+    RL overhead;
+    if (!resource_list(tspec ? tspec->field("overhead") : nullptr, overhead)) return bad("spec.template.spec.overhead");
+    alloc_q = pod_total(cs, ics, overhead, false);
+  }
+  RL allocatable, allocated;
+  allocatable.q = alloc_q;
+  if (!resource_list(status ? status->field("allocated") : nullptr, allocated))
+    return allocated.overflow ? unsup("status.allocated quantity out of range") : bad("status.allocated");
+  // rInfo.Reserved: the node-reservation annotation's resources, cpu = |reservedCPUs| when set (util/node.go:85-120)
+  RL reserved;
+  if (const std::string* s = lookup(ann, "node.koordinator.sh/reservation")) {
+    Value v;
+    std::string err;
+    if (!json::parse(s->c_str(), s->size(), v, err) || !v.is_obj()) return bad("node.koordinator.sh/reservation annotation");
+    if (!resource_list(v.field("resources"), reserved)) return bad("node.koordinator.sh/reservation resources");
+    std::vector<int> cpus;
+    const std::string rc_s = str_or_empty(v.field("reservedCPUs"));
+    if (!rc_s.empty()) {
+      if (!parse_cpuset(rc_s, cpus)) return bad("node.koordinator.sh/reservation reservedCPUs");
+      reserved.q["cpu"] = (__int128)cpus.size() * 1000000000;
+    }
+  }
+  // rInfo.ResourceNames: the allocatable's names, for Restricted narrowed by the restricted-options annotation
+  // (reservation_info.go:87-96, util/reservation/reservation.go:637-654); a malformed annotation is a ParseError
+  std::vector<std::string> keep;
+  bool restricted_opts = false;
+  if (r.allocate_policy == KE_RSV_POLICY_RESTRICTED) {
+    if (const std::string* s = lookup(ann, "scheduling.koordinator.sh/reservation-restricted-options")) {
+      Value v;
+      std::string err;
+      if (!s->empty()) {
+        if (!json::parse(s->c_str(), s->size(), v, err) || !v.is_obj()) {
+          available = false;  // ParseError: the reservation takes no part
+        } else if (const Value* rs = v.field("resources")) {
+          if (rs->t == Value::ARR)
+            for (const Value& x : rs->a)
+              if (x.t == Value::STR) keep.push_back(x.s);
+          restricted_opts = true;
+        }
+      }
+    }
+  }
+  auto excluded = [&](const std::string& name) {
+    if (!restricted_opts) return false;
+    bool any = false, in = false;  // (an options list matching none of the names keeps them all)
+    for (const auto& kv : alloc_q)
+      if (kv.second != 0)
+        for (const std::string& k : keep) any = any || k == kv.first;
+    for (const std::string& k : keep) in = in || k == name;
+    return any && !in;
+  };
+  r.available = available ? 1 : 0;
+  int32_t ne = 0;
+  for (const auto& kv : alloc_q) {
+    if (kv.second == 0) continue;  // a zero quantity: not a resource name of the reservation
+    int64_t av, al, rs;
+    if (!rl_get(allocatable, kv.first, &av) || !rl_get(allocated, kv.first, &al) || !rl_get(reserved, kv.first, &rs))
+      return unsup("reservation quantity out of range");
+    if (kv.first == "cpu" || kv.first == "memory") {
+      const int k = kv.first == "cpu" ? KE_RES_CPU : KE_RES_MEMORY;
+      r.allocatable[k] = av;
+      r.allocated[k] = excluded(kv.first) ? 0 : al;
+      r.reserved[k] = rs;
+      if (excluded(kv.first)) r.names_excluded |= (uint8_t)(1u << k);
+      continue;
+    }
+    int32_t id = kv.first == "pods" ? KE_RSV_RES_PODS : -2;
+    for (int32_t q = 0; q < n_names && id == -2; q++)
+      if (xres_names[q] && kv.first == xres_names[q]) id = q;
+    if (id == -2) return unsup("reservation allocatable \"" + kv.first + "\" without a resource id");
+    if (id == KE_XRES_CPU || id == KE_XRES_MEMORY) return bad("xres_names maps cpu / memory");
+    if (ne >= res_cap) return bad("more reservation resources than res_cap");
+    if (av <= 0) return unsup("reservation allocatable \"" + kv.first + "\" not positive");
+    ke_reservation_resource& e = res[ne++];
+    e = ke_reservation_resource{};
+    e.id = id;
+    e.excluded = excluded(kv.first) ? 1 : 0;
+    e.allocatable = av;
+    e.allocated = e.excluded ? 0 : al;
+    e.reserved = rs;
+  }
+  *n_res = ne;
+  // the reserve pod's holdings: its DeviceAllocations (device-allocated annotation, device_share.go:32,246-262) and
+  // its ResourceStatus (resource-status annotation: CPUSet + NUMANodeResources, numa_aware.go:83-94,257-268); the
+  // owner parts are the owner pods' own annotations (the caller's)
+  if (const std::string* s = lookup(ann, "scheduling.koordinator.sh/device-allocated")) {
+    Value v;
+    std::string err;
+    if (!json::parse(s->c_str(), s->size(), v, err) || !v.is_obj()) return bad("device-allocated annotation");
+    for (const auto& kv : v.o) {
+      int t = -1;
+      for (int q = 0; q < KE_DEV_TYPES; q++)
+        if (kv.first == DEV_TYPE_NAMES[q]) t = q;
+      if (t < 0) return unsup("device-allocated type \"" + kv.first + "\"");
+      if (kv.second.t != Value::ARR) return bad("device-allocated list");
+      for (const Value& d : kv.second.a) {
+        int64_t minor;
+        const Value* mv = d.field("minor");
+        if (!mv || !json::as_int64(*mv, &minor)) return bad("device-allocated minor");
+        if (minor < 0 || minor >= KE_MAX_MINORS) return unsup("device-allocated minor beyond 15");
+        RL rl;
+        if (!resource_list(d.field("resources"), rl)) return bad("device-allocated resources");
+        a.device_minors |= 1ull << (16 * t + minor);
+        for (int k = 0; k < KE_DKEYS; k++) {
+          if (!DEV_KEY_NAMES[t][k]) continue;
+          int64_t x;
+          if (!rl_get(rl, DEV_KEY_NAMES[t][k], &x)) return unsup("device-allocated quantity out of range");
+          a.device[t][minor][k] += x;
+        }
+      }
+    }
+  }
+  if (const std::string* s = lookup(ann, "scheduling.koordinator.sh/resource-status")) {
+    Value v;
+    std::string err;
+    if (!json::parse(s->c_str(), s->size(), v, err) || !v.is_obj()) return bad("resource-status annotation");
+    std::vector<int> cpus;
+    if (!parse_cpuset(str_or_empty(v.field("cpuset")), cpus)) return bad("resource-status cpuset");
+    for (int c : cpus) {
+      if (c >= KE_MAX_CPUS) return unsup("resource-status cpuset beyond the CPU id range");
+      a.cpuset[c >> 6] |= 1ull << (c & 63);
+    }
+    if (const Value* nr = v.field("numaNodeResources")) {
+      if (nr->t != Value::ARR && !nr->is_null()) return bad("resource-status numaNodeResources");
+      for (size_t q = 0; nr->t == Value::ARR && q < nr->a.size(); q++) {
+        const Value& z = nr->a[q];
+        int64_t id;
+        const Value* iv = z.field("node");
+        if (!iv || !json::as_int64(*iv, &id)) return bad("numaNodeResources node");
+        if (id < 0 || id >= KE_MAX_NUMA) return unsup("numaNodeResources node beyond the NUMA id range");
+        RL rl;
+        if (!resource_list(z.field("resources"), rl)) return bad("numaNodeResources resources");
+        int64_t cpu, mem;
+        if (!rl_get(rl, "cpu", &cpu) || !rl_get(rl, "memory", &mem)) return unsup("numaNodeResources quantity out of range");
+        a.numa[2 * id + KE_RES_CPU] += cpu;
+        a.numa[2 * id + KE_RES_MEMORY] += mem;
+      }
+    }
+  }
+  r.holds = (uint8_t)(resv_holds_of(a) | (ne > 0 ? KE_RSV_OTHER_ALLOCATABLE : 0u));
+  // allocated pods: status.currentOwners (the cache counts the assigned pods it tracks)
+  if (const Value* owners = status ? status->field("currentOwners") : nullptr)
+    if (owners->t == Value::ARR) r.allocated_pods = (int32_t)owners->a.size();
+  *out = r;
+  if (alloc) *alloc = a;
+  return KE_OK;
+}
+
+}  // extern "C"

@@ -8,6 +8,7 @@ boundary structs, through the C ABI (ke_decode_* in libkoordeval.so; no Python r
     zones, cpus = decode_nrt(nrt_json, node)       (patches the NRT-side fields of `node`)
     hints = decode_pod_device_hints(pod_json)       -> abi.PodDeviceHints or None (no hint annotations)
     well_planned, model_key = decode_device_flags(device_json, node_json)
+    rsv, alloc, resources, node_name = decode_reservation(reservation_json, xres_names)
 Objects may be given as dicts (serialised with json.dumps) or JSON text.
 """
 import ctypes as C
@@ -77,6 +78,23 @@ def decode_pod(obj, xres_names=()):
     p = abi.Pod()
     _check(lib, lib.ke_decode_pod(t, len(t), len(xres_names), names, C.byref(p)))
     return p
+
+
+def decode_reservation(obj, xres_names=()):
+    """Reservation -> (abi.Reservation with node = -1, RESERVATION_ALLOC_DTYPE record of the reserve pod's holdings,
+    RESERVATION_RESOURCE_DTYPE entries beyond cpu / memory, status.nodeName).  xres_names[id] = the resource name of
+    id (None = no name)."""
+    lib = _lib()
+    t = _text(obj)
+    names = (C.c_char_p * max(len(xres_names), 1))(*[n.encode() if n else None for n in xres_names])
+    r = abi.Reservation()
+    a = np.zeros(1, abi.RESERVATION_ALLOC_DTYPE)
+    res = np.zeros(abi.MAX_XRES + 1, abi.RESERVATION_RESOURCE_DTYPE)
+    n = abi.i32()
+    node = C.create_string_buffer(256)
+    _check(lib, lib.ke_decode_reservation(t, len(t), len(xres_names), names, C.byref(r), abi.ptr(a), len(res),
+                                          abi.ptr(res), C.byref(n), node, 256))
+    return r, a[0], res[:n.value].copy(), node.value.decode()
 
 
 def decode_device(obj, cap=3 * abi.MAX_MINORS, part_cap=abi.MAX_GPU_PARTITIONS):

@@ -858,16 +858,39 @@ def add_pod_xres(pods, seed, gpu_fraction=0.2, storage_fraction=0.5, scarce_frac
 
 
 # ---- reservations whose reserve pods hold NUMA resources, cpusets and devices ------------------------------------
+# resource ids of the device resource names (after XRES's 0..6): a reservation's allocatable names them when its
+# reserve pod holds devices (ReservationInfo.Allocatable = the reserve pod's requests)
+DEVICE_XRES = {"koordinator.sh/gpu-core": 10, "koordinator.sh/gpu-memory-ratio": 11, "koordinator.sh/gpu-memory": 12,
+               "koordinator.sh/rdma": 13}
+DEVICE_KEY_XRES = {(abi.DEV_GPU, 0): 10, (abi.DEV_GPU, 1): 12, (abi.DEV_GPU, 2): 11, (abi.DEV_RDMA, 0): 13}
+
+
+def device_resource_entries(a, owners=True):
+    """a reservation's allocatable entries of the device resources its reserve pod holds (RESERVATION_ALLOC record
+    `a`): per resource id the Σ over instances, allocated = the owners' Σ (ke_reservation_resource array)"""
+    sums = {}
+    for (ty, k), rid in DEVICE_KEY_XRES.items():
+        v = int(a["device"][ty, :, k].sum())
+        if v:
+            sums[rid] = (v, int(a["owner_device"][ty, :, k].sum()) if owners else 0)
+    e = np.zeros(len(sums), abi.RESERVATION_RESOURCE_DTYPE)
+    for q, rid in enumerate(sorted(sums)):
+        e[q]["id"], e[q]["allocatable"], e[q]["allocated"] = rid, sums[rid][0], sums[rid][1]
+    return e
+
+
 def make_reservation_holdings(cl, seed, zones=None, tabs=None, devices=None, frac=0.3, owner_fraction=0.6,
                               policies=(0, 1, 2)):
     """Reservations on a `frac` of the nodes whose reserve pods hold, where the node has them, a NUMA allocation on
     one or two zones, a cpuset out of the zones' free CPUs and a share of one GPU / RDMA instance, with owner pods
     (allocated_pods > 0 for `owner_fraction` of them) holding part of each.  Both are added to the node state the way
     the resource manager and the device cache count them (zone allocation, CPU ref counts, device used, NodeInfo
-    Requested / pod count).  Mutates cl.nodes, zones, tabs and devices; returns (RESERVATION_DTYPE array,
-    RESERVATION_ALLOC_DTYPE array)."""
+    Requested / pod count).  A reservation holding devices names their resources in its allocatable (the reserve
+    pod requests them): entries by DEVICE_XRES id, KE_RSV_OTHER_ALLOCATABLE.  Mutates cl.nodes, zones, tabs and
+    devices; returns (RESERVATION_DTYPE array, RESERVATION_ALLOC_DTYPE array, per reservation its
+    RESERVATION_RESOURCE_DTYPE entries)."""
     rng = np.random.default_rng(seed)
-    rs, al = [], []
+    rs, al, res = [], [], []
     for i in range(cl.n_nodes):
         if rng.random() >= frac:
             continue
@@ -961,7 +984,8 @@ def make_reservation_holdings(cl, seed, zones=None, tabs=None, devices=None, fra
                 continue
             cpu_total = cpu_total or int(rng.choice([2000, 4000]))
             mem_total = mem_total or int(rng.choice([2, 4])) * GI
-            r["holds"] = holds
+            e = device_resource_entries(a)
+            r["holds"] = holds | (abi.RSV_OTHER_ALLOCATABLE if len(e) else 0)
             r["allocatable"][:] = [cpu_total, mem_total]
             if owners:
                 r["allocated"][:] = [max(cpu_owned, 1000), max(mem_owned, GI)]
@@ -971,4 +995,5 @@ def make_reservation_holdings(cl, seed, zones=None, tabs=None, devices=None, fra
             cl.nodes["pod_count"][i] += 1 + int(r["allocated_pods"])
             rs.append(r)
             al.append(a)
-    return np.array(rs, abi.RESERVATION_DTYPE), np.array(al, abi.RESERVATION_ALLOC_DTYPE)
+            res.append(e)
+    return np.array(rs, abi.RESERVATION_DTYPE), np.array(al, abi.RESERVATION_ALLOC_DTYPE), res

@@ -9,11 +9,8 @@ from koordinator_amd import abi, synth
 
 GI = synth.GI
 GPU_MEM = synth.GPU_MEM
-# resource ids of the device names (synth.XRES keeps 0..6)
-DEV_IDS = {"koordinator.sh/gpu-core": 10, "koordinator.sh/gpu-memory": 12, "koordinator.sh/gpu-memory-ratio": 11,
-           "koordinator.sh/rdma": 13, "nvidia.com/gpu": 5}
-# (device type, device key) -> resource id
-KEY_ID = {(abi.DEV_GPU, 0): 10, (abi.DEV_GPU, 1): 12, (abi.DEV_GPU, 2): 11, (abi.DEV_RDMA, 0): 13}
+# (device type, device key) -> resource id (synth.DEVICE_XRES; synth.XRES keeps 0..6)
+KEY_ID = synth.DEVICE_KEY_XRES
 PDR_ID = {abi.PDR["koordinator.sh/gpu-core"]: 10, abi.PDR["koordinator.sh/gpu-memory"]: 12,
           abi.PDR["koordinator.sh/gpu-memory-ratio"]: 11, abi.PDR["koordinator.sh/rdma"]: 13,
           abi.PDR["nvidia.com/gpu"]: 5}
@@ -91,15 +88,7 @@ def make_ds_reservations(cl, devices, seed, n_groups=10, per_group=(2, 7), owner
             if owners:
                 r["allocated"][:] = [r["allocatable"][0] // 2, r["allocatable"][1] // 4]
             # the reservation's allocatable beyond cpu / memory: its device resources (the reserve pod's requests)
-            sums, osums = {}, {}
-            for (ty, k), rid in KEY_ID.items():
-                s = int(a["device"][ty, :, k].sum())
-                if s:
-                    sums[rid] = s
-                    osums[rid] = int(a["owner_device"][ty, :, k].sum())
-            e = np.zeros(len(sums), abi.RESERVATION_RESOURCE_DTYPE)
-            for q, rid in enumerate(sorted(sums)):
-                e[q]["id"], e[q]["allocatable"], e[q]["allocated"] = rid, sums[rid], osums[rid]
+            e = synth.device_resource_entries(a)
             cl.nodes["requested"][i, 0] += r["allocatable"][0] + (r["allocated"][0] if owners else 0)
             cl.nodes["requested"][i, 1] += r["allocatable"][1] + (r["allocated"][1] if owners else 0)
             cl.nodes["pod_count"][i] += 1 + int(r["allocated_pods"])

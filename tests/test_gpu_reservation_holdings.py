@@ -18,7 +18,7 @@ def holding_cluster(n, seed, devices=False, frac=0.3):
     cl = synth.make_cluster(n, synth.BASE_SEED + seed, amplified_fraction=0.2)
     zones, tabs = synth.make_numa_cpus(cl, synth.BASE_SEED + seed + 1)
     devs = synth.make_devices(n, synth.BASE_SEED + seed + 2) if devices else None
-    rs, al = synth.make_reservation_holdings(cl, synth.BASE_SEED + seed + 3, zones, tabs, devs, frac=frac)
+    rs, al, res = synth.make_reservation_holdings(cl, synth.BASE_SEED + seed + 3, zones, tabs, devs, frac=frac)
     cfg = synth.config(n)
     ev, o = Evaluator(cfg), Oracle(cfg, n)
     for h in (ev, o):
@@ -27,12 +27,12 @@ def holding_cluster(n, seed, devices=False, frac=0.3):
         synth.load_cpus(h, tabs)
         if devs is not None:
             synth.load_devices(h, devs)
-        h.reservations_load(rs, al)
-    return ev, o, cl, rs, al
+        h.reservations_load(rs, al, res)
+    return ev, o, cl, rs, al, res
 
 
 def test_holdings_generator_covers_every_kind():
-    _, _, _, rs, al = holding_cluster(300, 1301, devices=True)
+    _, _, _, rs, al, _ = holding_cluster(300, 1301, devices=True)
     h = rs["holds"]
     for bit in (abi.RSV_HOLDS_NUMA, abi.RSV_HOLDS_CPUSET, abi.RSV_HOLDS_DEVICES):
         assert ((h & bit) != 0).sum() >= 5, bit
@@ -68,7 +68,7 @@ def test_holdings_unmatched_deviceshare_parity(gpu):
 
 def test_holdings_reload_and_release_parity(gpu):
     """A queue, then releases, then a reloaded set with other holdings: the restore states follow every change."""
-    ev, o, cl, rs, al = holding_cluster(300, 1331, devices=True)
+    ev, o, cl, rs, al, res = holding_cluster(300, 1331, devices=True)
     pods = synth.make_numa_cpuset_pods(300, synth.BASE_SEED + 1332)
     assert_schedule_equal(ev, o, pods, synth.T0)
     a1, a0 = ev.last_allocations(), o.last_allocations()
@@ -77,7 +77,7 @@ def test_holdings_reload_and_release_parity(gpu):
         o.release(pods[p], a0[p], abi.RELEASE_DELETE)
     keep = np.arange(len(rs)) % 2 == 0
     for h in (ev, o):
-        h.reservations_load(rs[keep], al[keep])
+        h.reservations_load(rs[keep], al[keep], [res[i] for i in np.flatnonzero(keep)])
     more = synth.make_numa_cpuset_pods(300, synth.BASE_SEED + 1333, key_base=6_500_000_000)
     assert_eval_equal(ev.eval(more[:48], synth.T0), o.eval(more[:48], synth.T0))
     assert_schedule_equal(ev, o, more, synth.T0)
@@ -95,7 +95,7 @@ def cpuset_matched_setup(n, seed, n_pods, affinity=0.3, tight_pods=0.0, node_bin
     zones, tabs = synth.make_numa_cpus(cl, synth.BASE_SEED + seed + 1, policy_weights=(1, 0, 0, 0))
     if not node_bind:
         cl.nodes["cpu_bind_policy"] = 0
-    rs, al = synth.make_reservation_holdings(cl, synth.BASE_SEED + seed + 2, zones, tabs, None, frac=0.5)
+    rs, al, res = synth.make_reservation_holdings(cl, synth.BASE_SEED + seed + 2, zones, tabs, None, frac=0.5)
     for i in np.unique(rs["node"]):
         if rng.random() < tight_pods:
             cl.nodes["allowed_pods"][i] = cl.nodes["pod_count"][i] + int(rng.integers(-1, 2))
@@ -105,7 +105,7 @@ def cpuset_matched_setup(n, seed, n_pods, affinity=0.3, tight_pods=0.0, node_bin
         synth.load_into(h, cl)
         synth.load_numa(h, zones)
         synth.load_cpus(h, tabs)
-        h.reservations_load(rs, al)
+        h.reservations_load(rs, al, res)
     pods = synth.make_cpuset_pods(n_pods, synth.BASE_SEED + seed + 3, cpuset_fraction=0.7)
     grp = rng.integers(0, 8, len(rs))
     matches = [[] for _ in range(n_pods)]

@@ -215,22 +215,22 @@ def test_holdings_load_rules():
     cl = synth.make_cluster(40, synth.BASE_SEED + 1341, amplified_fraction=0.2)
     zones, tabs = synth.make_numa_cpus(cl, synth.BASE_SEED + 1342)
     devs = synth.make_devices(40, synth.BASE_SEED + 1343)
-    rs, al = synth.make_reservation_holdings(cl, synth.BASE_SEED + 1344, zones, tabs, devs, frac=0.6)
+    rs, al, res = synth.make_reservation_holdings(cl, synth.BASE_SEED + 1344, zones, tabs, devs, frac=0.6)
     assert len(rs) and (rs["holds"] != 0).any()
     ev, o = Evaluator(synth.config(40)), Oracle(synth.config(40), 40)
     for h in (ev, o):
         synth.load_into(h, cl)
-        h.reservations_load(rs, al)
+        h.reservations_load(rs, al, res)
     assert np.array_equal(ev.reservation_allocs_get(), al)
     assert np.array_equal(o.reservation_allocs_get(), al)
     i = int(np.flatnonzero(rs["holds"] != 0)[0])
     bad = rs.copy()
     bad["holds"][i] = 0
     with pytest.raises(KoordEvalError) as e:
-        ev.reservations_load(bad, al)
+        ev.reservations_load(bad, al, res)
     assert e.value.code == abi.ERR_INVALID
     with pytest.raises(RuntimeError, match=f"rc={abi.ERR_INVALID}"):
-        o.reservations_load(bad, al)
+        o.reservations_load(bad, al, res)
     with pytest.raises(KoordEvalError) as e:
         ev.reservations_load(rs)
     assert e.value.code == abi.ERR_UNSUPPORTED
@@ -239,10 +239,10 @@ def test_holdings_load_rules():
     neg = al.copy()
     neg["owner_numa"][i, 0] = -1
     with pytest.raises(KoordEvalError) as e:
-        ev.reservations_load(rs, neg)
+        ev.reservations_load(rs, neg, res)
     assert e.value.code == abi.ERR_INVALID
-    # a reservation-ignored pod that would read held resources (here a DeviceShare pod beside held devices): refused
-    # by both; one that reads none passes the checks (the product stops at the missing device)
+    # a reservation-ignored pod that would read held resources in NUMA hints (here a DeviceShare pod beside held
+    # devices and NUMA holdings on NUMA-policy nodes): refused by both
     ds = synth.make_ds_pods(3, synth.BASE_SEED + 1345)
     ds["reservation_matched"][:] = abi.RSV_IGNORED
     i_ds = int(np.flatnonzero((ds["device_requests"] != 0).any(1))[0])
