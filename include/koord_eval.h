@@ -1153,6 +1153,21 @@ int ke_comm_unique_id(uint8_t* id, int32_t id_bytes);
  * loopback mode: this context evaluates every shard itself and merges locally (single-GPU tests of
  * the sharded path); world == 1 with an id runs the sharded path over a 1-rank communicator. */
 int ke_shard_init(ke_ctx* ctx, int32_t rank, int32_t world, const uint8_t* id);
+/* ke_shard_init with the collectives carried by the caller on the host (e.g. a gloo process group) instead of
+ * RCCL: the same per-batch exchange -- the candidate lists' all-gather (op KE_COLL_ALL_GATHER: `count` words of this
+ * rank into recv[world * count], rank-major), DeviceShare's NormalizeScore max and the staged Reservation pick's
+ * reductions (KE_COLL_MAX / KE_COLL_MIN over `count` elements of dtype KE_COLL_*) -- each after the eval stream's
+ * work so far completes.  fn returns 0 on success.  Readiness / test path of the multi-process protocol. */
+#define KE_COLL_ALL_GATHER 0
+#define KE_COLL_MAX 1
+#define KE_COLL_MIN 2
+#define KE_COLL_U32 0
+#define KE_COLL_I32 1
+#define KE_COLL_I64 2
+#define KE_COLL_U64 3
+typedef int32_t (*ke_host_collective)(void* user, int32_t op, int32_t dtype, const void* send, void* recv,
+                                      int64_t count);
+int ke_shard_init_host(ke_ctx* ctx, int32_t rank, int32_t world, ke_host_collective fn, void* user);
 /* This rank's node range [lo, hi) for the current node count. */
 int ke_shard_range(ke_ctx* ctx, int32_t* lo, int32_t* hi);
 

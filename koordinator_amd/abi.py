@@ -62,6 +62,9 @@ REASON_DS_JOINT_VIOLATION = 48
 REASON_DS_NO_MATCHED_TEMPLATE = 49
 REASON_RSV_INSUFFICIENT_CPUS = 50  # a required reservation affinity whose holding reservations satisfy none
 REASON_RSV_INSUFFICIENT_DEVICES = 51
+COLL_ALL_GATHER, COLL_MAX, COLL_MIN = 0, 1, 2  # ke_host_collective ops
+COLL_U32, COLL_I32, COLL_I64, COLL_U64 = 0, 1, 2, 3  # ... and element types
+HOST_COLLECTIVE = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_int64)
 REASON_RSV_AFFINITY = 52  # the Reservation Filter of a reservation-affinity pod (reservation/plugin.go:316-318)
 REASON_FIT_TOO_MANY_PODS, REASON_FIT_INSUFFICIENT_CPU, REASON_FIT_INSUFFICIENT_MEMORY = 64, 65, 66
 REASON_FIT_INSUFFICIENT_SCALAR = 67
@@ -592,6 +595,7 @@ EXPORTS = {
                                       C.c_void_p, i32, C.c_void_p, C.c_void_p]),
     "ke_comm_unique_id": (C.c_int, [C.c_void_p, i32]),
     "ke_shard_init": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p]),
+    "ke_shard_init_host": (C.c_int, [C.c_void_p, i32, i32, C.c_void_p, C.c_void_p]),
     "ke_shard_range": (C.c_int, [C.c_void_p, C.POINTER(i32), C.POINTER(i32)]),
 }
 COMM_ID_BYTES = 128

@@ -30,6 +30,7 @@ int device_check_records(Context* ctx, int64_t now, int64_t* bad);
 int device_bench_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t iters, double* avg_ms);
 int device_comm_unique_id(uint8_t* id);
 int device_shard_init(Context* ctx, int rank, int world, const uint8_t* id);
+int device_shard_init_host(Context* ctx, int rank, int world, ke_host_collective fn, void* user);
 int device_shard_range(Context* ctx, int* lo, int* hi);
 bool device_sharded(const Context* ctx);
 }  // namespace ke
@@ -1398,6 +1399,14 @@ int ke_shard_init(ke_ctx* ctx, int32_t rank, int32_t world, const uint8_t* id) {
   int rc = require_device(ctx);
   if (rc) return rc;
   return device_shard_init(&ctx->c, rank, world, id);
+}
+
+int ke_shard_init_host(ke_ctx* ctx, int32_t rank, int32_t world, ke_host_collective fn, void* user) {
+  if (ctx) async_drain(ctx);
+  if (!ctx) return fail(KE_ERR_INVALID, "null context");
+  int rc = require_device(ctx);
+  if (rc) return rc;
+  return device_shard_init_host(&ctx->c, rank, world, fn, user);
 }
 
 int ke_shard_range(ke_ctx* ctx, int32_t* lo, int32_t* hi) {

@@ -6436,6 +6436,9 @@ struct DeviceState {
   int world = 1, rank = 0;
   bool loopback = false;
   ncclComm_t comm = nullptr;
+  // ke_shard_init_host: the caller's host collective carries the all-gather / all-reduces instead of RCCL
+  ke_host_collective host_fn = nullptr;
+  void* host_user = nullptr;
   uint32_t* d_gath = nullptr;  // [world][GATH_WORDS]
   uint32_t* d_split = nullptr; // [MAX_WORLD][GATH_WORDS]: the part lists of a split k_select (unsharded)
   // DeviceShare
@@ -6811,6 +6814,8 @@ int device_shard_init(Context* ctx, int rank, int world, const uint8_t* id) {
     RCCL_OK(ncclCommDestroy(d->comm));
     d->comm = nullptr;
   }
+  d->host_fn = nullptr;
+  d->host_user = nullptr;
   if (!d->d_gath) HIP_OK(hipMalloc(&d->d_gath, sizeof(uint32_t) * GATH_WORDS_MAX * MAX_WORLD));
   HIP_OK(hipMemsetAsync(d->d_gath, 0, sizeof(uint32_t) * GATH_WORDS_MAX * MAX_WORLD, d->stream));
   HIP_OK(hipStreamSynchronize(d->stream));
@@ -6825,7 +6830,52 @@ int device_shard_init(Context* ctx, int rank, int world, const uint8_t* id) {
   return KE_OK;
 }
 
-bool device_sharded(const Context* ctx) { return ctx->dev && (ctx->dev->world > 1 || ctx->dev->comm); }
+// ke_shard_init_host: the same sharded path, its collectives through the caller's host function (e.g. gloo)
+int device_shard_init_host(Context* ctx, int rank, int world, ke_host_collective fn, void* user) {
+  if (!fn) return fail(KE_ERR_INVALID, "ke_shard_init_host: null collective");
+  int rc = device_shard_init(ctx, rank, world, nullptr);
+  if (rc) return rc;
+  DeviceState* d = ctx->dev;
+  d->loopback = false;
+  d->host_fn = fn;
+  d->host_user = user;
+  return KE_OK;
+}
+
+// The shard collectives on the eval stream `es`: RCCL, or the host collective (the stream's work so far completes,
+// the words go through host memory and back before the next launch on `es`)
+static int coll_all_gather(DeviceState* d, uint32_t* mine, uint32_t* all, size_t count, hipStream_t es) {
+  if (d->host_fn) {
+    std::vector<uint32_t> snd(count), rcv(count * (size_t)d->world);
+    HIP_OK(hipStreamSynchronize(es));
+    HIP_OK(hipMemcpy(snd.data(), mine, sizeof(uint32_t) * count, hipMemcpyDeviceToHost));
+    if (d->host_fn(d->host_user, KE_COLL_ALL_GATHER, KE_COLL_U32, snd.data(), rcv.data(), (int64_t)count))
+      return fail(KE_ERR_DEVICE, "host all-gather failed");
+    HIP_OK(hipMemcpy(all, rcv.data(), sizeof(uint32_t) * rcv.size(), hipMemcpyHostToDevice));
+    return KE_OK;
+  }
+  RCCL_OK(ncclAllGather(mine, all, count, ncclUint32, d->comm, es));
+  return KE_OK;
+}
+static int coll_all_reduce(DeviceState* d, void* buf, size_t count, int dt, int op, hipStream_t es) {
+  const size_t w = (dt == KE_COLL_I64 || dt == KE_COLL_U64) ? 8 : 4;
+  if (d->host_fn) {
+    std::vector<uint8_t> snd(w * count), rcv(w * count);
+    HIP_OK(hipStreamSynchronize(es));
+    HIP_OK(hipMemcpy(snd.data(), buf, w * count, hipMemcpyDeviceToHost));
+    if (d->host_fn(d->host_user, op, dt, snd.data(), rcv.data(), (int64_t)count))
+      return fail(KE_ERR_DEVICE, "host all-reduce failed");
+    HIP_OK(hipMemcpy(buf, rcv.data(), w * count, hipMemcpyHostToDevice));
+    return KE_OK;
+  }
+  const ncclDataType_t t = dt == KE_COLL_U32 ? ncclUint32 : dt == KE_COLL_I32 ? ncclInt32 : dt == KE_COLL_I64 ? ncclInt64 : ncclUint64;
+  RCCL_OK(ncclAllReduce(buf, buf, count, t, op == KE_COLL_MAX ? ncclMax : ncclMin, d->comm, es));
+  return KE_OK;
+}
+
+bool device_sharded(const Context* ctx) {
+  return ctx->dev && (ctx->dev->world > 1 || ctx->dev->comm || ctx->dev->host_fn);
+}
 
 int device_shard_range(Context* ctx, int* lo, int* hi) {
   DeviceState* d = ctx->dev;
@@ -7286,7 +7336,7 @@ bool device_refresh_pending(const Context* ctx, int64_t now) {
 // host round trip between its launches: it may be submitted behind a call in flight
 bool device_async_ok(const Context* ctx, int32_t n_pods) {
   const DeviceState* d = ctx->dev;
-  if (!d || d->world > 1 || d->comm || !d->pipeline || d->numa_alloc || !ctx->quotas.empty() || ctx->n_nodes <= 0)
+  if (!d || d->world > 1 || d->comm || d->host_fn || !d->pipeline || d->numa_alloc || !ctx->quotas.empty() || ctx->n_nodes <= 0)
     return false;
   if (ctx->n_bind_nodes > 0 || !ctx->rsv_pairs.empty() || ctx->rsv_affinity || !ctx->rsv_ovr.empty()) return false;
   if ((int64_t)ctx->staged.size() != n_pods) return false;
@@ -7339,7 +7389,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   // DeviceShare pods share batches (exact: the replay checks each pod's normalisation max and stops the
   // batch where it may have moved) unless the nodes are sharded or carry NUMA policies (then
   // each is a singleton batch)
-  const bool ds_batch = !(d->world > 1 || d->comm) && !d->numa_alloc && ctx->n_nodes > 0;
+  const bool ds_batch = !(d->world > 1 || d->comm || d->host_fn) && !d->numa_alloc && ctx->n_nodes > 0;
   ctx->last_ds_cuts = 0;
   for (int32_t p = 0; p < n_pods;) {
     const uint32_t f = d->host_pods[p].flags;
@@ -7504,7 +7554,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, d->stream, d->d_stamps);
   HIP_OK(hipEventRecord(d->ev_start, d->stream));
   HIP_OK(hipStreamWaitEvent(d->estream, d->ev_start, 0));
-  const bool sharded = d->world > 1 || d->comm;
+  const bool sharded = d->world > 1 || d->comm || d->host_fn;
   uint64_t* estamps = d->d_stamps + (PST + 1) * ((int64_t)n_pods + 2);  // eval start of each batch
   constexpr int R = DeviceState::EV_RING;
   int n_pipelined = 0;
@@ -7599,8 +7649,10 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
       if (pwait)
         hipLaunchKernelGGL(((k.flags & AF_EXT) ? k_patch<true> : k_patch<false>), dim3((unsigned)bp), dim3(64), d->excl_lds, es,
                            d->soa, d->d_pods, bbase, k, ptl, scores, d->capacity, pwait, d_err);
-      if (ds && sharded && !d->loopback)  // DefaultNormalizeScore's max over the feasible nodes of all ranks
-        RCCL_OK(ncclAllReduce(d->d_dsmax, d->d_dsmax, 1, ncclUint32, ncclMax, d->comm, es));
+      if (ds && sharded && !d->loopback) {  // DefaultNormalizeScore's max over the feasible nodes of all ranks
+        const int crc = coll_all_reduce(d, d->d_dsmax, 1, KE_COLL_U32, KE_COLL_MAX, es);
+        if (crc) return crc;
+      }
       if (prof) HIP_OK(hipEventRecord(pe[3], es));
       auto select = [&](int slo, int shi, uint32_t* cand, int32_t* cnt, int32_t* pub) {
         // register-resident when a wave's segment fits SEL_RC steps, else streamed
@@ -7641,7 +7693,8 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
         }
         if (!d->loopback) {
           uint32_t* mine = d->d_gath + (int64_t)d->rank * gw;  // in place: send = own block of recv
-          RCCL_OK(ncclAllGather(mine, d->d_gath, gw, ncclUint32, d->comm, es));
+          const int crc = coll_all_gather(d, mine, d->d_gath, (size_t)gw, es);
+          if (crc) return crc;
         }
         hipLaunchKernelGGL(k_merge, dim3((unsigned)bp), dim3(MERGE_BLOCK), 0, es, d->d_gath, d->world, L, kext,
                            lists, lists_cnt);
@@ -7653,17 +7706,18 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
           const int aff = (int)ctx->rsv_affinity;
           RsvPickSt* st = d->d_rsv_st;
           const uint16_t* rds = ds ? d->d_dsraw : nullptr;
-          const bool coll = !d->loopback && d->comm;
+          const bool coll = !d->loopback && (d->comm || d->host_fn);
+          int crc = 0;
           hipLaunchKernelGGL(k_rsv_stage<0>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out, rds, d->d_dsmax, k.wp_ds);
-          if (coll) RCCL_OK(ncclAllReduce(&st->order, &st->order, 1, ncclInt64, ncclMin, d->comm, es));
+          if (coll && (crc = coll_all_reduce(d, &st->order, 1, KE_COLL_I64, KE_COLL_MIN, es))) return crc;
           hipLaunchKernelGGL(k_rsv_stage<1>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out, rds, d->d_dsmax, k.wp_ds);
-          if (coll) RCCL_OK(ncclAllReduce(&st->node, &st->node, 1, ncclInt32, ncclMin, d->comm, es));
+          if (coll && (crc = coll_all_reduce(d, &st->node, 1, KE_COLL_I32, KE_COLL_MIN, es))) return crc;
           hipLaunchKernelGGL(k_rsv_stage<2>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out, rds, d->d_dsmax, k.wp_ds);
-          if (coll) RCCL_OK(ncclAllReduce(&st->mx, &st->mx, 1, ncclInt32, ncclMax, d->comm, es));
+          if (coll && (crc = coll_all_reduce(d, &st->mx, 1, KE_COLL_I32, KE_COLL_MAX, es))) return crc;
           hipLaunchKernelGGL(k_rsv_stage<3>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out, rds, d->d_dsmax, k.wp_ds);
-          if (coll) RCCL_OK(ncclAllReduce(&st->best, &st->best, 1, ncclUint64, ncclMax, d->comm, es));
+          if (coll && (crc = coll_all_reduce(d, &st->best, 1, KE_COLL_U64, KE_COLL_MAX, es))) return crc;
           hipLaunchKernelGGL(k_rsv_stage<4>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out, rds, d->d_dsmax, k.wp_ds);
-          if (coll) RCCL_OK(ncclAllReduce(&st->wt, &st->wt, 2, ncclInt32, ncclMax, d->comm, es));  // wt, nw
+          if (coll && (crc = coll_all_reduce(d, &st->wt, 2, KE_COLL_I32, KE_COLL_MAX, es))) return crc;  // wt, nw
           hipLaunchKernelGGL(k_rsv_stage<5>, dim3(1), dim3(64), 0, es, scores, d->d_rsv, K, rlo, rhi, wr, aff, lists, st, d->d_rsv_out, rds, d->d_dsmax, k.wp_ds);
           HIP_OK(hipMemcpyAsync(d->h_rsv_out.data(), d->d_rsv_out, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, es));
         }

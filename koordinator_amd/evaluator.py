@@ -241,6 +241,30 @@ class Evaluator:
             buf = C.create_string_buffer(bytes(unique_id), abi.COMM_ID_BYTES)
         self._check(self.lib.ke_shard_init(self.h, rank, world, buf))
 
+    def shard_init_host(self, rank, world, collective):
+        """ke_shard_init_host: the sharded path with its collectives carried on the host by
+        collective(op, dtype, send: np.ndarray, world) -> np.ndarray (all-gather: world * len(send) elements
+        rank-major; max / min: len(send) elements), e.g. koordinator_amd.shard.gloo_collective()."""
+        dts = {abi.COLL_U32: np.uint32, abi.COLL_I32: np.int32, abi.COLL_I64: np.int64, abi.COLL_U64: np.uint64}
+
+        def cb(user, op, dtype, send, recv, count):
+            try:
+                dt = np.dtype(dts[dtype])
+                n = int(count)
+                src = np.frombuffer((C.c_uint8 * (n * dt.itemsize)).from_address(send), dtype=dt).copy()
+                out = np.ascontiguousarray(collective(int(op), dt, src, world), dtype=dt)
+                m = n * (world if op == abi.COLL_ALL_GATHER else 1)
+                assert out.size == m
+                C.memmove(recv, out.ctypes.data, m * dt.itemsize)
+                return 0
+            except Exception:  # the library fails the call (KE_ERR_DEVICE)
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        self._collective = abi.HOST_COLLECTIVE(cb)  # kept alive with the context
+        self._check(self.lib.ke_shard_init_host(self.h, rank, world, self._collective, None))
+
     def shard_range(self):
         lo, hi = abi.i32(), abi.i32()
         self._check(self.lib.ke_shard_range(self.h, C.byref(lo), C.byref(hi)))

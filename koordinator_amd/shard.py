@@ -59,3 +59,25 @@ def init_node_sharding(ev, rank, world, group=None):
         return
     uid = exchange_unique_id(rank, lambda: comm_unique_id(ev.lib), group)
     ev.shard_init(rank, world, uid)
+
+
+def gloo_collective(group=None):
+    """A host collective for Evaluator.shard_init_host over a torch.distributed process group (gloo: CPU
+    tensors): all-gather of uint32 words (as int32 bits), all-reduce MAX / MIN of 32 / 64-bit integers (as int64;
+    the library's 64-bit words stay below 2^63)."""
+    import torch
+    import torch.distributed as dist
+
+    def collective(op, dt, send, world):
+        if op == 0:  # all-gather, rank-major
+            t = torch.from_numpy(send.view(np.int32).copy())
+            outs = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(outs, t, group=group)
+            return np.concatenate([o.numpy() for o in outs]).view(np.int32).view(dt)
+        if dt == np.uint64 and (send >> np.uint64(63)).any():
+            raise ValueError("64-bit word beyond int64")
+        t = torch.from_numpy(send.astype(np.int64))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == 1 else dist.ReduceOp.MIN, group=group)
+        return t.numpy().astype(dt)
+
+    return collective

@@ -33,6 +33,7 @@ int device_check_records(Context*, int64_t, int64_t*) { return none(); }
 int device_bench_eval(Context*, int32_t, const ke_pod*, int64_t, int32_t, double*) { return none(); }
 int device_comm_unique_id(uint8_t*) { return none(); }
 int device_shard_init(Context*, int, int, const uint8_t*) { return none(); }
+int device_shard_init_host(Context*, int, int, ke_host_collective, void*) { return none(); }
 int device_shard_range(Context*, int*, int*) { return none(); }
 bool device_sharded(const Context*) { return false; }
 }  // namespace ke
