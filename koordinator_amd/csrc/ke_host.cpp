@@ -649,7 +649,12 @@ static void resv_delta(const Context& c, int32_t node, const std::vector<char>* 
 //   used = subtractAllocated(copy(allocatable), remained, true),  remained = allocatable - allocated
 // which per NUMA id / device instance and key is the owners' amount where the reserve pod holds that key (keys of
 // both lists kept, the ResourceList arithmetic of quotav1) -- the part the node allocation counts twice.
-static void resv_plugin_restore(const Context& c, int32_t node, const std::vector<char>* matched, NodeState& ns) {
+// ignored: a reservation-ignored pod's rows (every reservation matchedOrIgnored) -- NodeNUMAResource's reusable
+// resources are then mergedMatchedAllocatable, the reserve pods' whole NUMA allocations: the hint view
+// (GetTopologyHints, resource_manager.go:130-138) and tryAllocateIgnoreReservation's mergedMatchedAllocated + Σ
+// remained (nodenumaresource/reservation.go:437-490), equal in value
+static void resv_plugin_restore(const Context& c, int32_t node, const std::vector<char>* matched, NodeState& ns,
+                                bool ignored = false) {
   std::memset(ns.rv_numa, 0, sizeof ns.rv_numa);
   std::memset(ns.rv_dev, 0, sizeof ns.rv_dev);
   ns.rv_numa_keys = 0;
@@ -659,6 +664,18 @@ static void resv_plugin_restore(const Context& c, int32_t node, const std::vecto
   if (c.resv_alloc.empty()) return;
   for (int32_t i : c.resv_by_node[(size_t)node]) {
     const ke_reservation& r = c.resv[(size_t)i];
+    if (ignored && resv_usable(r)) {
+      const ke_reservation_alloc& a = c.resv_alloc[(size_t)i];
+      for (int id = 0; id < KE_MAX_NUMA; id++)
+        for (int q = 0; q < KE_NRES; q++) {
+          const int j = 2 * id + q;
+          if (a.numa[j] == 0) continue;
+          ns.rv_numa_zones |= (uint8_t)(1u << id);
+          ns.rv_numa_keys |= 1u << j;
+          ns.rv_numa[j] += a.numa[j];
+        }
+      continue;
+    }
     if (!resv_usable(r) || (matched && (*matched)[(size_t)i]) || r.allocated_pods == 0) continue;
     const ke_reservation_alloc& a = c.resv_alloc[(size_t)i];
     // NodeNUMAResource (RestoreReservation, reservation.go:196-209): only with the reserve pod's NUMA resources
@@ -898,11 +915,15 @@ int resv_check(const Context& c, const int32_t* ids, int32_t n_ids) {
 // reservation (plugin.go:755-761).  NodeNUMAResource / DeviceShare allocate it from the node and the ignored
 // reservations' unallocated remainder (tryAllocateIgnoreReservation, nodenumaresource/reservation.go:437-490,
 // deviceshare/reservation.go:290-310): for a pod binding CPUs on a node without a NUMA policy that remainder is
-// the held CPUs, tried as the preferred CPUs of one allocation (resv_ignore_views); the held NUMA amounts and
-// devices are not restated, so the pod is refused where it would read them -- a DeviceShare pod while a
-// reservation holds devices; a pod with its own NUMA policy while one holds NUMA resources or CPUs; any pod while
-// one of those sits on a node with a NUMA topology policy (its hints read the zones).
+// the held CPUs, tried as the preferred CPUs of one allocation (resv_ignore_views); for a pod binding no CPUs the
+// held NUMA amounts are reusable resources (resv_plugin_restore, ignored); for a DeviceShare pod the held devices
+// are views (resv_ds_views).  Refused: a binding pod with its own NUMA policy while a reservation holds NUMA
+// resources or CPUs, a binding pod while one of those sits on a NUMA-policy node (its hints over the held CPUs),
+// a DeviceShare pod with hints or a NUMA policy (pod or node) beside held devices.
 int resv_ignore_check(const Context& c, const ke_pod& pod, uint32_t pod_flags) {
+  // a pod binding no CPUs reads held NUMA amounts only as reusable resources, which its rows carry
+  // (resv_plugin_restore, ignored); a binding one's NUMA hints would trim them by the held CPUs (not restated)
+  const bool binds = (pod_flags & PF_CPUSET) || (c.n_bind_nodes > 0 && pod.requests[KE_RES_CPU] > 0);
   bool dev = false, numa_cpu = false, on_policy_node = false;
   for (size_t i = 0; i < c.resv_holds.size(); i++) {
     const uint8_t h = c.resv_holds[i];
@@ -920,7 +941,7 @@ int resv_ignore_check(const Context& c, const ke_pod& pod, uint32_t pod_flags) {
       dev_on_policy = dev_on_policy || c.nodes[(size_t)c.resv[i].node].node.numa_topology_policy != KE_NUMA_POLICY_NONE;
   const bool ds = (pod_flags & (PF_DS | PF_DS_HINT)) != 0;
   if ((dev && ds && ((pod_flags & PF_DS_HINT) || pod.numa_topology_policy != KE_NUMA_POLICY_NONE || dev_on_policy)) ||
-      (numa_cpu && pod.numa_topology_policy != KE_NUMA_POLICY_NONE) || on_policy_node)
+      (binds && ((numa_cpu && pod.numa_topology_policy != KE_NUMA_POLICY_NONE) || on_policy_node)))
     return fail(KE_ERR_UNSUPPORTED, "a reservation-ignored pod reading resources a reservation holds "
                                     "(tryAllocateIgnoreReservation's remainder)");
   return KE_OK;
@@ -932,7 +953,7 @@ void resv_ignore_begin(Context& c) {
     if (c.resv_by_node[node].empty()) continue;
     NodeState& ns = c.nodes[node];
     resv_delta(c, (int32_t)node, &all, true, ns.rv_req, ns.rv_nz, &ns.rv_pods, &ns.rv_x);
-    resv_plugin_restore(c, (int32_t)node, &all, ns);
+    resv_plugin_restore(c, (int32_t)node, &all, ns, true);
     ns.dirty = true;
   }
 }

@@ -3545,6 +3545,20 @@ static void or_dev_unmatched_used(or_node* nd, const ke_reservation_alloc* a) {
   }
 }
 
+/* a reservation-ignored pod's NodeNUMAResource reusable: mergedMatchedAllocatable over every reservation (the hint
+ * view, resource_manager.go:130-138), equal in value to tryAllocateIgnoreReservation's mergedMatchedAllocated + Σ
+ * remained (nodenumaresource/reservation.go:437-490) */
+static void or_numa_ignored_reusable(or_node* nd, const ke_reservation_alloc* a) {
+  for (int id = 0; id < KE_MAX_NUMA; id++)
+    for (int r = 0; r < KE_NRES; r++) {
+      if (a->numa[2 * id + r] == 0) continue;
+      nd->rs_numa_has[id] = 1;
+      nd->rs_numa_key[id][r] = 1;
+      nd->rs_numa[id][r] += a->numa[2 * id + r];
+    }
+}
+
+/* with_matched 2: a reservation-ignored pod's restore (every reservation matched, the NUMA reusable above) */
 static void or_restore(or_cluster* c, const char* matched, int with_matched) {
   for (int32_t i = 0; i < c->n; i++) {
     or_node* nd = &c->nodes[i];
@@ -3562,6 +3576,7 @@ static void or_restore(or_cluster* c, const char* matched, int with_matched) {
    * (transformer.go:195-199) */
   for (int32_t i = 0; c->ralloc && i < c->n_resv; i++) {
     const ke_reservation* r = &c->resv[i];
+    if (with_matched == 2 && or_resv_usable(r)) or_numa_ignored_reusable(&c->nodes[r->node], &c->ralloc[i]);
     if (!or_resv_usable(r) || (matched && matched[i]) || r->allocated_pods == 0) continue;
     or_numa_unmatched_used(&c->nodes[r->node], &c->ralloc[i]);
     or_dev_unmatched_used(&c->nodes[r->node], &c->ralloc[i]);
@@ -4905,9 +4920,11 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
     const int32_t n_ids = c->moff && c->m_pods == n_pods ? c->moff[p + 1] - c->moff[p] : 0;
     if (pods[p].reservation_matched != KE_RSV_MATCHED && pods[p].reservation_matched != KE_RSV_AFFINITY) {
       if (n_ids) return KE_ERR_INVALID;
-      /* a reservation-ignored pod reading held NUMA amounts / devices: tryAllocateIgnoreReservation's remainder of
-       * those is not restated (a DeviceShare pod and held devices; a pod with a NUMA policy and held NUMA
-       * resources / CPUs; held NUMA resources / CPUs on a NUMA-policy node) */
+      /* a reservation-ignored pod: tryAllocateIgnoreReservation's remainder is restated for a pod binding no CPUs
+       * (the held NUMA amounts reusable), a pod binding CPUs on nodes without a NUMA policy (the held CPUs) and a
+       * DeviceShare pod without hints beside held devices off NUMA-policy nodes; refused: a binding pod with a NUMA
+       * policy beside held NUMA resources / CPUs, a binding pod beside those on a NUMA-policy node (its hints over
+       * the held CPUs), a DeviceShare pod with hints or a NUMA policy (node or pod) beside held devices */
       if (pods[p].reservation_matched == KE_RSV_IGNORED && c->ralloc) {
         int dev = 0, dev_on_policy = 0, numa_cpu = 0, on_policy = 0;
         for (int32_t r = 0; r < c->n_resv; r++) {
@@ -4920,10 +4937,15 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
           }
         }
         ds_pod d; /* (a pod binding CPUs allocates from the held CPUs: or_numa_ignored; a DeviceShare pod from the
-                     held devices: tryAllocateIgnoreReservation) -- the held devices in NUMA hints are not restated */
+                     held devices: tryAllocateIgnoreReservation; a pod binding none reads the held NUMA amounts as
+                     reusable: or_numa_ignored_reusable) -- the held devices in NUMA hints and a binding pod's NUMA
+                     hints over held CPUs are not restated */
         ds_prepare_pod(c, &pods[p], &d);
         const int pod_pol = pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE;
-        if ((dev && !d.skip && (d.h || pod_pol || dev_on_policy)) || (numa_cpu && pod_pol) || on_policy)
+        cpuset_state cst;
+        cpuset_prefilter(c, &pods[p], &cst);
+        const int binds = cst.rcb || cst.invalid || (node_bind && pods[p].requests[KE_RES_CPU] > 0);
+        if ((dev && !d.skip && (d.h || pod_pol || dev_on_policy)) || (binds && ((numa_cpu && pod_pol) || on_policy)))
           return KE_ERR_UNSUPPORTED;
       }
       continue;
@@ -4998,6 +5020,7 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
     }
     int16_t bs16;
     int32_t bs, b;
+    int ign_restored = 0;
     const int affinity = pods[p].reservation_matched == KE_RSV_AFFINITY;
     const int32_t n_ids = c->moff && pods[p].reservation_matched ? c->moff[p + 1] - c->moff[p] : 0;
     if (n_ids > 0 || affinity) {
@@ -5008,11 +5031,11 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
        * PreScore (scoring.go:48-50) and Reserve (plugin.go:755-761) */
       char* all = (char*)malloc((size_t)(c->n_resv > 0 ? c->n_resv : 1));
       memset(all, 1, (size_t)(c->n_resv > 0 ? c->n_resv : 1));
-      or_restore(c, all, 1);
+      or_restore(c, all, 2);
       c->ignored = 1;
       b = eval_pod(c, &pods[p], now, o, &bs16);
       bs = bs16;
-      or_restore(c, NULL, 0);
+      ign_restored = 1; /* NodeNUMAResource's Reserve reads the same cycle state (the reusable NUMA view) */
       free(all);
     } else {
       b = eval_pod(c, &pods[p], now, o, &bs16);
@@ -5084,6 +5107,7 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
     c->resv_m = NULL;
     c->ds_nom = NULL;
     c->ignored = 0;
+    if (ign_restored) or_restore(c, NULL, 0);
     free(mflags);
   }
   free(o);

@@ -212,3 +212,43 @@ def test_matched_cpuset_sharded_loopback(gpu):
     assert np.array_equal(s1, s0)
     assert np.array_equal(ev.last_cpusets, o.last_cpusets)
     _holdings_equal(ev, o)
+
+
+@pytest.mark.parametrize("seed", [1391, 1392])
+def test_ignored_numa_pods_beside_held_numa(gpu, seed):
+    """Reservation-ignored pods binding no CPUs (nodes without a bind policy) in a cluster whose reservations hold
+    NUMA allocations and cpusets on nodes of every NUMA policy: their rows carry every reservation's matched restore,
+    NodeNUMAResource's reusable resources being the reserve pods' whole NUMA allocations (mergedMatchedAllocatable,
+    nodenumaresource/resource_manager.go:130-138; tryAllocateIgnoreReservation's mergedMatchedAllocated + Σ remained,
+    reservation.go:437-490) -- in the hints, the zones' distribution and Reserve.  Pods with their own NUMA policy among
+    them; cpuset pods between them.  Placements, scores, NUMA allocations, cpusets and reservation state bit-exact
+    with the oracle (the CPU twin: test_reservations.py::test_ignored_numa_pod_reuses_the_held_zone)."""
+    n = 400
+    cl = synth.make_cluster(n, synth.BASE_SEED + seed, amplified_fraction=0.2)
+    zones, tabs = synth.make_numa_cpus(cl, synth.BASE_SEED + seed + 1)
+    cl.nodes["cpu_bind_policy"] = 0
+    rs, al, res = synth.make_reservation_holdings(cl, synth.BASE_SEED + seed + 3, zones, tabs, None, frac=0.5)
+    cfg = synth.config(n)
+    ev, o = Evaluator(cfg), Oracle(cfg, n)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        synth.load_numa(h, zones)
+        synth.load_cpus(h, tabs)
+        h.reservations_load(rs, al, res)
+    pods = synth.make_numa_cpuset_pods(400, synth.BASE_SEED + seed + 10, cpuset_fraction=0.3, policy_fraction=0.3)
+    cs = np.isin(pods["qos_class"], [abi.QOS_LSE, abi.QOS_LSR]) & (pods["priority_class"] == abi.PRIORITY_PROD)
+    pods["numa_topology_policy"][cs] = 0
+    ign = np.flatnonzero(~cs)[::2]
+    pods["reservation_matched"][ign] = abi.RSV_IGNORED
+    assert len(ign) >= 100 and (pods["numa_topology_policy"][ign] != 0).sum() >= 20
+    assert_schedule_equal(ev, o, pods, synth.T0)
+    assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
+    assert np.array_equal(ev.last_cpusets, o.last_cpusets)
+    _holdings_equal(ev, o)
+    c = ev.last_allocations()["node"]
+    pol = cl.nodes["numa_topology_policy"] != 0
+    held = np.zeros(n, bool)
+    held[rs["node"][(rs["holds"] & abi.RSV_HOLDS_NUMA) != 0]] = True
+    on_held = [p for p in ign if c[p] >= 0 and held[c[p]] and pol[c[p]] and ev.last_numa_allocations[p].any()]
+    assert len(on_held) >= 3  # ignored pods given NUMA allocations on policy nodes with held zones
+    assert ev.check_records(synth.T0) == 0

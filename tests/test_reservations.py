@@ -519,3 +519,61 @@ def test_general_reservation_load_rules():
 
 R6_GENERAL = {"policy": 0, "allocatable": [6000, 8 << 30], "allocated": [0, 0], "reserved": [0, 0],
               "allocated_pods": 0, "entries": []}
+
+
+def ignored_numa_case():
+    """One SingleNUMANode node, two NUMA zones of 4 CPUs: zone 0 held whole by a reservation's reserve pod (its NUMA
+    allocation), zone 1 half used; a 3-CPU pod with no cpuset."""
+    from koordinator_amd import model
+    cl = synth.make_cluster(1, synth.BASE_SEED + 1431)
+    cl.nodes["allocatable"][0] = [8000, 64 * 2**30]
+    cl.nodes["raw_allocatable"][0] = abi.ABSENT
+    cl.nodes["requested"][0] = [6000, 4 * 2**30]
+    cl.nodes["numa_topology_policy"][0] = abi.NUMA_POLICY_SINGLE_NUMA_NODE
+    cl.nodes["cpu_bind_policy"][0] = 0
+    cl.nodes["cpu_amplification_ratio"][0] = 0
+    zones = model.make_zones([{"id": 0, "cpu": "4", "memory": "32Gi", "allocated": {"cpu": "4", "memory": "2Gi"}},
+                              {"id": 1, "cpu": "4", "memory": "32Gi", "allocated": {"cpu": "2", "memory": "2Gi"}}])
+    r = np.zeros(1, abi.RESERVATION_DTYPE)
+    a = np.zeros(1, abi.RESERVATION_ALLOC_DTYPE)
+    r["available"], r["holds"] = 1, abi.RSV_HOLDS_NUMA
+    r["allocatable"][0] = [4000, 2 * 2**30]
+    a["numa"][0, 0], a["numa"][0, 1] = 4000, 2 * 2**30
+    pods = synth.make_pods(2, synth.BASE_SEED + 1432)
+    pods["requests"][:, 0], pods["requests"][:, 1], pods["requests"][:, 2:] = 3000, 2**30, 0
+    pods["limits"][:] = 0
+    pods["qos_class"], pods["priority_class"] = abi.QOS_LS, abi.PRIORITY_PROD
+    pods["has_other_requests"], pods["device_requests"], pods["numa_topology_policy"] = 0, 0, 0
+    pods["n_xres"] = 0
+    return cl, zones, r, a, pods
+
+
+def test_ignored_numa_pod_reuses_the_held_zone():
+    """A reservation-ignored pod on a NUMA-policy node reads the held NUMA amounts as reusable (GetTopologyHints'
+    mergedUnmatchedUsed + mergedMatchedAllocatable, tryAllocateIgnoreReservation's mergedMatchedAllocated + Σ remained,
+    nodenumaresource/resource_manager.go:130-138, reservation.go:437-490): the 3-CPU pod fits zone 0 only when
+    ignored; a plain one fits no zone.  Oracle and product checks agree (the GPU twin:
+    test_gpu_reservation_holdings.py::test_ignored_numa_pods_beside_held_numa)."""
+    cl, zones, r, a, pods = ignored_numa_case()
+    for v, want in ((abi.RSV_NONE, -1), (abi.RSV_IGNORED, 0)):
+        o = Oracle(synth.config(1), 1)
+        synth.load_into(o, cl)
+        o.delete_nodemetric(0)  # (LoadAware passes without a NodeMetric)
+        o.set_numa(0, zones)
+        o.reservations_load(r, a)
+        one = pods[:1].copy()
+        one["reservation_matched"] = v
+        c, _ = o.schedule(one, synth.T0)
+        assert c[0] == want
+        if v == abi.RSV_IGNORED:
+            assert o.last_numa_allocations[0, 0] == 3000 and o.last_numa_allocations[0, 2] == 0  # zone 0's cpu
+    ev = Evaluator(synth.config(1))
+    synth.load_into(ev, cl)
+    ev.set_numa(0, zones)
+    ev.reservations_load(r, a)
+    one = pods[:1].copy()
+    one["reservation_matched"] = abi.RSV_IGNORED
+    with pytest.raises(KoordEvalError) as e:  # accepted by the checks: the device is what is missing here
+        ev.schedule(one, synth.T0)
+    assert e.value.code == abi.ERR_NO_DEVICE
+    ev.close()
