@@ -214,6 +214,9 @@ typedef struct ke_numa_args {
                                                  deviceshare/reservation.go:283-285: "Reservation(s) Insufficient ...") */
 #define KE_REASON_RSV_AFFINITY 52 /* a pod with a reservation affinity on a node where none of its matched reservations
                                      fits (the Reservation plugin's Filter, reservation/plugin.go:316-318, 351-442) */
+#define KE_REASON_RSV_INSUFFICIENT_NUMA 53 /* a pod with a reservation affinity under a NUMA policy whose matched
+                                              reservations cannot allocate on the merged affinity: "Reservation(s)
+                                              Insufficient NUMA <resource>" (nodenumaresource/reservation.go:420-422) */
 
 /* One logical CPU of a node: CPUTopology.CPUDetails (cpu_topology.go:24-105, built from the NRT's
  * CPU topology, topology_options.go:90-164) + NodeAllocation.allocatedCPUs (node_allocation.go:33-41)

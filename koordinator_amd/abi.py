@@ -66,6 +66,7 @@ COLL_ALL_GATHER, COLL_MAX, COLL_MIN = 0, 1, 2  # ke_host_collective ops
 COLL_U32, COLL_I32, COLL_I64, COLL_U64 = 0, 1, 2, 3  # ... and element types
 HOST_COLLECTIVE = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_int64)
 REASON_RSV_AFFINITY = 52  # the Reservation Filter of a reservation-affinity pod (reservation/plugin.go:316-318)
+REASON_RSV_INSUFFICIENT_NUMA = 53  # an affinity pod's reservations cannot allocate on the NUMA affinity
 REASON_FIT_TOO_MANY_PODS, REASON_FIT_INSUFFICIENT_CPU, REASON_FIT_INSUFFICIENT_MEMORY = 64, 65, 66
 REASON_FIT_INSUFFICIENT_SCALAR = 67
 # ke_pod.gpu_required_topology_scope (apiext.DeviceTopologyScope -> level)

@@ -21,6 +21,8 @@ int device_ds_views(Context* ctx, const ke_pod& pod, int64_t now, const std::vec
                     std::vector<DsViewOut>& out);
 int device_rsv_views(Context* ctx, const ke_pod& pod, int64_t now, const std::vector<RsvView>& views,
                      std::vector<RsvViewOut>& out);
+int device_numa_views(Context* ctx, const ke_pod& pod, int64_t now, const std::vector<NumaRsvView>& views,
+                      std::vector<NumaRsvOut>& out);
 int device_quota_sync(Context* ctx);
 int device_debug_rows(Context* ctx, int32_t n, Row* out);
 int device_set_profiling(Context* ctx, int32_t every);
@@ -219,17 +221,35 @@ static int check_matches(Context& c, const ke_pod* pods, int32_t n) {
           return fail(KE_ERR_UNSUPPORTED, "a DeviceShare pod with device hints or NUMA hints matching a reservation "
                                           "that holds devices");
       }
-    // a pod with its own NUMA policy takes hints on every node: a matched reservation holding NUMA resources or
-    // CPUs would need them over its allocate-from-reservation trials (not restated); without such holdings its
-    // matched restore moves only NodeInfo.Requested, which the hints do not read
-    if (pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE && !c.resv_holds.empty())
+    // under a NUMA policy (the pod's or the node's) a matched reservation holding NUMA resources or CPUs enters the
+    // hints through its allocate-from-reservation trials (k_numa_views) for a pod binding no CPUs without device
+    // requests; a binding pod's hints over the held CPUs and a DeviceShare pod's joint hints there are not restated,
+    // nor more than NV_MAX such reservations of the pod on one node
+    if (!c.resv_holds.empty()) {
+      const bool binds = (f & PF_CPUSET) || (c.n_bind_nodes > 0 && pods[p].requests[KE_RES_CPU] > 0);
+      const bool dev = (f & (PF_DS | PF_DS_HINT)) != 0;
+      std::vector<std::pair<int32_t, int32_t>> per_node;
       for (int32_t j = c.match_off[(size_t)p]; j < c.match_off[(size_t)p + 1]; j++) {
         const int32_t r = c.match_ids[(size_t)j];
-        if (r >= 0 && r < (int32_t)c.resv.size() && resv_usable(c.resv[(size_t)r]) &&
-            (c.resv_holds[(size_t)r] & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)))
-          return fail(KE_ERR_UNSUPPORTED, "a pod with a NUMA topology policy matching a reservation that holds NUMA "
-                                          "resources or CPUs");
+        if (r < 0 || r >= (int32_t)c.resv.size() || !resv_usable(c.resv[(size_t)r]) ||
+            !(c.resv_holds[(size_t)r] & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)))
+          continue;
+        const int32_t node = c.resv[(size_t)r].node;
+        const bool pol = pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE ||
+                         c.nodes[(size_t)node].node.numa_topology_policy != KE_NUMA_POLICY_NONE;
+        if (pol && (binds || dev))
+          return fail(KE_ERR_UNSUPPORTED, "a pod binding CPUs or requesting devices under a NUMA topology policy "
+                                          "matching a reservation that holds NUMA resources or CPUs");
+        bool seen = false;
+        for (auto& e : per_node)
+          if (e.first == node) seen = true, e.second++;
+        if (!seen) per_node.emplace_back(node, 1);
       }
+      for (auto& e : per_node)
+        if (e.second > NV_MAX)
+          return fail(KE_ERR_UNSUPPORTED, "more matched reservations holding NUMA resources / CPUs on a node than "
+                                          "NV_MAX");
+    }
     const int rc = resv_check(c, c.match_ids.data() + c.match_off[(size_t)p], cnt);
     if (rc) return rc;
   }
@@ -961,6 +981,17 @@ static int schedule_sync(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_
         rc = device_ds_views(&c, pods[s0], now_ns, c.ds_views, c.ds_view_out);
         if (rc) {
           for (const DsView& v : c.ds_views) resv_node_restore(c, v.node);
+          c.ds_views.clear();
+          return rc;
+        }
+      }
+      resv_numa_views(c, pods[s0], ids, n_ids);  // NodeNUMAResource's hints over the trials (NUMA policies)
+      if (!c.numa_views.empty()) {
+        rc = device_numa_views(&c, pods[s0], now_ns, c.numa_views, c.numa_view_out);
+        if (rc) {
+          for (const NumaRsvView& v : c.numa_views) resv_node_restore(c, v.node);
+          for (const DsView& v : c.ds_views) resv_node_restore(c, v.node);
+          c.numa_views.clear();
           c.ds_views.clear();
           return rc;
         }

@@ -691,7 +691,9 @@ static void resv_plugin_restore(const Context& c, int32_t node, const std::vecto
           const int j = 2 * id + r;
           if (a.numa[j] == 0 && a.owner_numa[j] == 0) continue;
           ns.rv_numa_keys |= 1u << j;
-          if (a.numa[j] != 0 && a.owner_numa[j] > 0) ns.rv_numa[j] += a.owner_numa[j];
+          // used = SubtractWithNonNegativeResult(allocatable, allocatable - allocated) = the owners' amount, also
+          // on ids / keys the reserve pod does not hold (an owner allocated from the node, assumed into it)
+          if (a.owner_numa[j] > 0) ns.rv_numa[j] += a.owner_numa[j];
         }
       }
     // DeviceShare (RestoreReservation, deviceshare/reservation.go:157-172): the owners' usage on the reserve pod's
@@ -899,11 +901,6 @@ int32_t resv_score(const Context& c, int32_t i, const ke_pod& pod) {
 int resv_check(const Context& c, const int32_t* ids, int32_t n_ids) {
   for (int32_t j = 0; j < n_ids; j++) {
     if (ids[j] < 0 || ids[j] >= (int32_t)c.resv.size()) return fail(KE_ERR_NOT_FOUND, "matched reservation index");
-    const ke_reservation& r = c.resv[(size_t)ids[j]];
-    if (resv_usable(r) && c.nodes[(size_t)r.node].node.numa_topology_policy != KE_NUMA_POLICY_NONE &&
-        !c.resv_holds.empty() && (c.resv_holds[(size_t)ids[j]] & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)))
-      return fail(KE_ERR_UNSUPPORTED, "a matched reservation holding NUMA resources / a cpuset on a node with a NUMA "
-                                      "topology policy");
   }
   return KE_OK;
 }
@@ -1256,6 +1253,80 @@ void resv_ds_views(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_
   }
 }
 
+// ---- NodeNUMAResource allocate-from-reservation views under a NUMA policy (nodenumaresource/reservation.go:270-424) ----
+// Per node of the pod's matched reservations holding NUMA resources / CPUs where the pod's or the node's NUMA policy
+// applies (the pod binds no CPUs: check_matches), RestoreReservation's matched set there (index order) and:
+//   the hint view (GetTopologyHints, resource_manager.go:136-138): reusable += mergedMatchedAllocatable;
+//   trial q (tryAllocateFromReservation, reservation.go:293-311): reusable += mergedMatchedAllocated + its remained;
+//   a Restricted trial's requiredResources (:353-357): its remained (quotav1.Subtract: signed, keys of both).
+void resv_numa_views(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids) {
+  c.numa_views.clear();
+  c.numa_view_ids.clear();
+  c.numa_view_out.clear();
+  if (c.resv_alloc.empty()) return;
+  const DevPod dp = make_dev_pod(c.cfg, pod, pod_hints(c, pod), &c.tmpl);
+  if (dp.flags & PF_NUMA_SKIP) return;
+  std::vector<char> m(c.resv.size(), 0);
+  for (int32_t j = 0; j < n_ids; j++)
+    if (resv_usable(c.resv[(size_t)ids[j]])) m[(size_t)ids[j]] = 1;
+  std::vector<int32_t> nodes;
+  for (int32_t j = 0; j < n_ids; j++)
+    if (m[(size_t)ids[j]] && resv_holds_cpu(c, ids[j])) nodes.push_back(c.resv[(size_t)ids[j]].node);
+  std::sort(nodes.begin(), nodes.end());
+  nodes.erase(std::unique(nodes.begin(), nodes.end()), nodes.end());
+  auto any_numa = [](const int64_t* v) {
+    for (int j = 0; j < KE_MAX_NUMA * KE_NRES; j++)
+      if (v[j]) return true;
+    return false;
+  };
+  for (int32_t node : nodes) {
+    NodeState& ns = c.nodes[(size_t)node];
+    if (pod.numa_topology_policy == KE_NUMA_POLICY_NONE && ns.node.numa_topology_policy == KE_NUMA_POLICY_NONE) continue;
+    std::vector<int32_t> mine;
+    for (int32_t i : c.resv_by_node[(size_t)node])
+      if (m[(size_t)i] && resv_holds_cpu(c, i) && mine.size() < (size_t)NV_MAX) mine.push_back(i);
+    if (mine.empty()) continue;
+    // the rows this pod sees: its matched restore (resv_prepare applies the same)
+    resv_delta(c, node, &m, true, ns.rv_req, ns.rv_nz, &ns.rv_pods, &ns.rv_x);
+    resv_plugin_restore(c, node, &m, ns);
+    ns.dirty = true;
+    c.numa_views.emplace_back();
+    NumaRsvView& v = c.numa_views.back();
+    std::memset(&v, 0, sizeof v);
+    v.node = node;
+    v.n = (int32_t)mine.size();
+    v.required = pod.reservation_matched == KE_RSV_AFFINITY;
+    for (const ke_numa_zone& z : ns.zones)
+      if (z.id >= 0 && z.id < KE_MAX_NUMA && (z.has_allocated & KE_NUMA_ALLOC_ENTRY)) v.entry |= 1u << z.id;
+    int64_t m_allocd[KE_MAX_NUMA * KE_NRES] = {};
+    uint32_t m_allocd_keys = 0;
+    for (int32_t i : mine) {
+      const ke_reservation_alloc& a = c.resv_alloc[(size_t)i];
+      for (int j = 0; j < KE_MAX_NUMA * KE_NRES; j++)
+        if (a.numa[j] != 0) v.hint_keys |= 1u << j, v.hint[j] += a.numa[j];  // mergedMatchedAllocatable
+      if (!any_numa(a.numa)) continue;
+      for (int j = 0; j < KE_MAX_NUMA * KE_NRES; j++)
+        if (a.owner_numa[j] != 0) m_allocd_keys |= 1u << j, m_allocd[j] += a.owner_numa[j];  // mergedMatchedAllocated
+    }
+    for (size_t q = 0; q < mine.size(); q++) {
+      const ke_reservation_alloc& a = c.resv_alloc[(size_t)mine[q]];
+      v.keys[q] = m_allocd_keys;
+      std::memcpy(v.reuse[q], m_allocd, sizeof m_allocd);
+      v.restricted[q] = c.resv[(size_t)mine[q]].allocate_policy == KE_RSV_POLICY_RESTRICTED;
+      v.has_req[q] = any_numa(a.numa);
+      if (!v.has_req[q]) continue;
+      for (int j = 0; j < KE_MAX_NUMA * KE_NRES; j++)
+        if (a.numa[j] != 0 || a.owner_numa[j] != 0) {  // remained = allocatable - allocated
+          v.req_keys[q] |= 1u << j;
+          v.req[q][j] = a.numa[j] - a.owner_numa[j];
+          v.keys[q] |= 1u << j;
+          v.reuse[q][j] += v.req[q][j];
+        }
+    }
+    c.numa_view_ids.push_back(mine);
+  }
+}
+
 int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids, bool affinity) {
   int rc = resv_check(c, ids, n_ids);  // (ke_schedule's argument checks ran it already: nothing below fails)
   if (rc) return rc;
@@ -1302,7 +1373,24 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
         if (c.rsv_view_resv[q] == i && c.rsv_views[q].node == node) return c.rsv_view_out.size() > q ? c.rsv_view_out[q].ok : 0;
       return -1;
     };
+    // under a NUMA policy (k_numa_views): with an affinity a reservation of the trials needs its allocation on the
+    // stored affinity; one outside RestoreReservation's matched set passes
+    int nvi = -1;
+    for (size_t q = 0; q < c.numa_views.size(); q++)
+      if (c.numa_views[q].node == node) nvi = (int)q;
+    const NumaRsvOut* nvo = nvi >= 0 && (size_t)nvi < c.numa_view_out.size() ? &c.numa_view_out[(size_t)nvi] : nullptr;
+    auto numa_trial = [&](int32_t i) -> int {  // the trial index of reservation i in the node's view set, or -1
+      if (nvi < 0) return -1;
+      const std::vector<int32_t>& t = c.numa_view_ids[(size_t)nvi];
+      for (size_t q = 0; q < t.size(); q++)
+        if (t[q] == i) return (int)q;
+      return -1;
+    };
     auto numa_nominable = [&](int32_t i) {
+      if (nvo) {
+        const int q = numa_trial(i);
+        return !(affinity && q >= 0 && !((nvo->ok >> q) & 1u));
+      }
       if (!binds) return true;
       if (!cpus_valid(ns)) return false;
       return !(affinity && view_of(i) == 0);
@@ -1402,8 +1490,32 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
       o.rfilter = (int8_t)(allowed ? 1 : 2);
       any_ovr = true;
     }
+    // NodeNUMAResource under a NUMA policy (k_numa_views): the Filter's outcome; Score and Reserve from the
+    // nominated reservation's allocation on the affinity (allocateWithNominatedReservation), else the node's own
+    // (tryAllocateFromNode); an error status there is a Score error (scoring.go:105-115)
+    bool score_err = false;
+    if (nvo) {
+      o.numa_on = 1;
+      o.numa_st = (uint8_t)nvo->st;
+      o.numa_reason = (uint8_t)nvo->reason;
+      o.numa_aff = (uint8_t)nvo->aff;
+      int use = -1;  // the trial, NV_MAX = the node's own
+      const int qn = nom >= 0 ? numa_trial(nom) : -1;
+      if (nom < 0 && affinity) score_err = true;  // "no nominated reservation"
+      else if (qn >= 0 && ((nvo->ok >> qn) & 1u)) use = qn;
+      else if (qn >= 0 && affinity) score_err = true;
+      else if ((nvo->ok >> NV_MAX) & 1u) use = NV_MAX;
+      else score_err = true;
+      if (nvo->st != KE_CODE_SUCCESS) score_err = false;  // (an infeasible node is not scored)
+      if (use >= 0) {
+        o.numa_score = (int16_t)nvo->score[use];
+        std::memcpy(o.numa_dist, nvo->dist[use], sizeof o.numa_dist);
+      }
+      any_ovr = true;
+    }
     c.rsv_pairs.push_back({node, (int16_t)(nom >= 0 ? resv_score(c, nom, pod) : 0),
-                           (int16_t)((allowed ? RSV_PAIR_ALLOWED : 0) | (reserve_fails ? RSV_PAIR_RESERVE_FAILS : 0)),
+                           (int16_t)((allowed ? RSV_PAIR_ALLOWED : 0) | (reserve_fails ? RSV_PAIR_RESERVE_FAILS : 0) |
+                                     (score_err ? RSV_PAIR_SCORE_ERROR : 0)),
                            order});
     c.rsv_nominated.push_back(nom);
     // NodeNUMAResource with the matched reservations first (plugin.go:381-397, 553-563): the Filter's trial
@@ -1516,6 +1628,9 @@ void resv_finish(Context& c, int32_t chosen_local, const ke_pod& pod, int32_t* a
   c.ds_views.clear();
   c.ds_view_resv.clear();
   c.ds_view_out.clear();
+  c.numa_views.clear();
+  c.numa_view_ids.clear();
+  c.numa_view_out.clear();
 }
 
 // forgetPod -> RemoveAssignedPod (reservation_info.go:470-482)

@@ -70,6 +70,7 @@ struct RsvPair {
 };
 constexpr int16_t RSV_PAIR_ALLOWED = 1;        // the Reservation plugin's Filter passes (always without an affinity)
 constexpr int16_t RSV_PAIR_RESERVE_FAILS = 2;  // DeviceShare's Reserve fails there (the pod is not placed)
+constexpr int16_t RSV_PAIR_SCORE_ERROR = 4;    // NodeNUMAResource's Score errs there: feasible, it fails the pod's cycle
 
 struct NodeState {
   bool valid = false;  // in the snapshot (ke_node_upsert .. ke_node_delete)
@@ -233,6 +234,11 @@ struct Context {
   std::vector<DsView> ds_views;
   std::vector<int32_t> ds_view_resv;
   std::vector<DsViewOut> ds_view_out;
+  // its NodeNUMAResource views under a NUMA policy (resv_numa_views -> k_numa_views): per node view set the
+  // reservations of its trials (index order) and the outcome
+  std::vector<NumaRsvView> numa_views;
+  std::vector<std::vector<int32_t>> numa_view_ids;
+  std::vector<NumaRsvOut> numa_view_out;
   std::vector<int32_t> last_resv;  // per pod of the last ke_schedule: 1 + the reservation assumed, 0 = none
   int32_t resv_gen = 0;            // ke_reservations_generation: bumped by every load_reservations
   // per-pod latency of the last ke_schedule (ke_last_pod_latencies): the call's entry on the host clock, and
@@ -355,6 +361,10 @@ void resv_views(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids
 // of a reservation-ignored one: per node of its device-holding reservations one per such reservation in index order
 // and the node's own (-1); an ignored pod the node's own and the ignore view (-2).  Into c.ds_views / ds_view_resv.
 void resv_ds_views(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids);
+// the NodeNUMAResource views of a reservation-matched pod binding no CPUs (ids: its matched reservations): per node of
+// its reservations holding NUMA resources / CPUs where a NUMA policy applies, one view set over them (k_numa_views).
+// Into c.numa_views / numa_view_ids; the rows of those nodes carry the pod's matched restore.
+void resv_numa_views(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids);
 // the refusals of resv_prepare, checked for every pod before a ke_schedule call schedules any
 int resv_check(const Context& c, const int32_t* ids, int32_t n_ids);
 // a run of KE_RSV_IGNORED pods: the rows with every usable reservation matchedOrIgnored (begin) and back to the

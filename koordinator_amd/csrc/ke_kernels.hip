@@ -2187,6 +2187,21 @@ __device__ __forceinline__ void numa_reserve(const SoA& s, int64_t i, uint32_t n
   numa_reserve_cs(s, i, nf, v, got, out, cs, cs, 0u, 0, out16);
 }
 
+// numa_reserve with an allocation given per NUMA id ([2*id + r], k_numa_views' choice for a reservation-matched pod)
+__device__ __noinline__ void numa_reserve_dist(const SoA& s, int64_t i, uint32_t nf, const NumaNode& v,
+                                               const int64_t* dist16, int64_t* out16) {
+  int64_t out[2][8];
+  uint32_t got[2] = {0, 0};
+  for (int z = 0; z < 8; z++)
+    for (int r = 0; r < 2; r++) {
+      out[r][z] = dist16[2 * z + r];
+      if (out[r][z] != 0) got[r] |= 1u << z;
+    }
+  int cs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if ((nf & NF_NUMA_AL_AMP) && ((got[0] | got[1]) & ~v.ak[0])) zone_cpusets(s, i, cs);  // a new entry
+  numa_reserve_cs(s, i, nf, v, got, out, cs, cs, 0u, 0, out16);
+}
+
 // `s`/`i` locate the node's DeviceShare state (read only for pods with PF_DS, and only when DS: the
 // batch replay never evaluates a DeviceShare pod — such a pod is alone in its batch).
 // NUMA: some node may carry a NUMA topology policy; `nv` holds node i's zones when its policy is set.
@@ -2448,7 +2463,20 @@ __device__ __forceinline__ EvalOut eval_pair(const NodeRegs& n, bool expired, co
   // (topology_hint.go:38-58); such a pair is never deferred (its batch runs no k_numa_fallback)
   const bool ds_here = DS && (p.flags & PF_DS) && (nf & NF_DS_CACHE);
   bool stored = false;  // the topology manager stored an affinity for the node
-  if (npol && o.status == KE_CODE_SUCCESS) {
+  // a reservation-matched pod on a node of its reservations holding NUMA resources / CPUs: the outcome k_numa_views
+  // computed over the allocate-from-reservation trials (RsvOvr.numa_on)
+  const RsvOvr* nro = (npol && (nf & NF_RSV_CS)) ? rsv_ovr_of(s, i) : nullptr;
+  if (nro && !nro->numa_on) nro = nullptr;
+  if (nro && o.status == KE_CODE_SUCCESS) {
+    if (nro->numa_st != KE_CODE_SUCCESS) {
+      o.status = nro->numa_st;
+      o.reason = nro->numa_reason;
+    } else {
+      o.aff = nro->numa_aff;
+      npol_score = nro->numa_score;
+      stored = true;
+    }
+  } else if (npol && o.status == KE_CODE_SUCCESS) {
     DsHints dh;
     dh.status = 0;
     dh.none = true;
@@ -3399,12 +3427,12 @@ __global__ __launch_bounds__(64) void k_rsv_pick(const uint16_t* __restrict__ sc
   }
   const int32_t win = best ? (int32_t)(KEY_IDX_MASK - (uint32_t)(best & KEY_IDX_MASK)) : -1;
   int32_t nw = 0, fails = 0;  // the winner's n (0 unless it holds matched reservations), its Reserve failing
-  if (win >= 0)
-    for (int i = l; i < K; i += 64) {
-      const RsvPair q = pr[i];
-      if (q.node == win && mx > 0) nw = (int32_t)(100 * (int64_t)(q.node == pref ? 1000 : q.raw) / mx);
-      if (q.node == win && (q.allowed & RSV_PAIR_RESERVE_FAILS)) fails = 1;
-    }
+  for (int i = l; i < K; i += 64) {
+    const RsvPair q = pr[i];
+    if (q.node == win && mx > 0) nw = (int32_t)(100 * (int64_t)(q.node == pref ? 1000 : q.raw) / mx);
+    if (q.node == win && (q.allowed & RSV_PAIR_RESERVE_FAILS)) fails = 1;
+    if ((q.allowed & RSV_PAIR_SCORE_ERROR) && feasible(q)) fails = 1;  // RunScorePlugins' error: no placement
+  }
   for (int m = 32; m; m >>= 1) nw = max(nw, __shfl_xor(nw, m)), fails = max(fails, __shfl_xor(fails, m));
   if (l == 0) {
     const bool placed = win >= 0 && !fails;
@@ -3486,6 +3514,8 @@ __global__ __launch_bounds__(64) void k_rsv_stage(const uint16_t* __restrict__ s
       for (int i = l; i < K; i += 64)
         if (pr[i].node == win && win >= lo && win < hi)
           nw = (int32_t)(100 * (int64_t)(pr[i].node == pref ? 1000 : pr[i].raw) / st->mx);
+    for (int i = l; i < K; i += 64)  // a feasible pair of this range whose Score errs: bit 30, carried by the MAX
+      if ((pr[i].allowed & RSV_PAIR_SCORE_ERROR) && mine(pr[i])) nw |= 1 << 30;
     for (int m = 32; m; m >>= 1) nw = max(nw, __shfl_xor(nw, m));
     if (l == 0) {
       st->wt = win >= lo && win < hi ? (int32_t)total(win) : 0;
@@ -3497,9 +3527,10 @@ __global__ __launch_bounds__(64) void k_rsv_stage(const uint16_t* __restrict__ s
       int32_t win = best ? (int32_t)(KEY_IDX_MASK - (uint32_t)(best & KEY_IDX_MASK)) : -1;
       for (int i = 0; win >= 0 && i < K; i++)  // (every rank holds every pair)
         if (pr[i].node == win && (pr[i].allowed & RSV_PAIR_RESERVE_FAILS)) win = -1;
+      if ((st->nw >> 30) & 1) win = -1;  // a Score error on some rank's feasible node
       cand[0] = win >= 0 ? ((uint32_t)st->wt << KEY_IDX_BITS) | (KEY_IDX_MASK - (uint32_t)win) : 0u;
       out[0] = win;
-      out[1] = st->nw;
+      out[1] = st->nw & ~(1 << 30);
       out[2] = st->mx;
       out[3] = pref;
     }
@@ -5487,7 +5518,12 @@ __device__ __forceinline__ void replay_batch(ResLds& L, const ChgSet& C, const S
         if (NUMA) {  // NodeNUMAResource Reserve: the zones of a NUMA-policy node
           int64_t* out16 = numa_alloc + (int64_t)(base + j) * 16;
           const int pol = pf_numa_policy(pod.flags) ? pf_numa_policy(pod.flags) : nf_numa_policy(mine.flags);
-          if (!(pod.flags & PF_NUMA_SKIP) && pol != KE_NUMA_POLICY_NONE) {
+          const RsvOvr* nro = (mine.flags & NF_RSV_CS) ? rsv_ovr_of(s, my_node) : nullptr;
+          if (!(pod.flags & PF_NUMA_SKIP) && pol != KE_NUMA_POLICY_NONE && nro && nro->numa_on) {
+            NumaNode nv;  // the nominated reservation's (or the node's own) allocation k_numa_views computed
+            numa_load(s, my_node, nv);
+            numa_reserve_dist(s, my_node, mine.flags, nv, nro->numa_dist, out16);
+          } else if (!(pod.flags & PF_NUMA_SKIP) && pol != KE_NUMA_POLICY_NONE) {
             NumaNode nv;
             numa_load(s, my_node, nv);
             const NumaPick pk = numa_admit<false>(s, my_node, mine.flags, pol, nv, pod, k);
@@ -6127,6 +6163,236 @@ __global__ __launch_bounds__(64) void k_ds_views(SoA s, const DevPod* __restrict
   out[blockIdx.x] = o;
 }
 
+// ---- NodeNUMAResource allocate-from-reservation under a NUMA policy (k_numa_views) ------------------------------
+// A view of node i's zones with `e` (keys ek: bit 2*id + r) added to the reusable resources of the NUMA ids with an
+// allocation entry (getAvailableNUMANodeResources, node_allocation.go:221-243): SubtractWithNonNegativeResult of the
+// row's allocated (its unmatched restore already subtracted) -- the allocated amounts al[r][id] and totalAvailable.
+__device__ __noinline__ void numa_view_reuse(const SoA& s, int64_t i, const NumaNode& base, uint32_t entry,
+                                             const int64_t* e, uint32_t ek, NumaNode& o, int64_t (&al)[2][8]) {
+  o = base;
+  for (int z = 0; z < 8; z++)
+    for (int r = 0; r < 2; r++) {
+      int64_t a = numa_al(s, i, base, z, r);
+      if (((entry >> z) & 1u) && ((ek >> (2 * z + r)) & 1u)) {
+        a -= e[2 * z + r];
+        a = a > 0 ? a : 0;
+        o.ak[r] |= 1u << z;
+      }
+      al[r][z] = ((o.ak[r] >> z) & 1u) ? a : 0;
+      const int64_t q = numa_cap(s, i, z, r) - al[r][z];
+      o.av[r][z] = q > 0 ? q : 0;
+    }
+  numa_perm(o, 0);
+  numa_perm(o, 1);
+}
+// totalAvailable = requiredResources (allocateResourcesByHint, resource_manager.go:226-254): its NUMA ids and keys,
+// signed (quotav1.Subtract); resourceNamesByNUMA = its keys
+__device__ __noinline__ void numa_view_req(const NumaNode& base, const int64_t* req, uint32_t rk, NumaNode& o) {
+  o = base;
+  o.ch[0] = o.ch[1] = o.ak[0] = o.ak[1] = 0;
+  for (int z = 0; z < 8; z++)
+    for (int r = 0; r < 2; r++) {
+      const bool key = (rk >> (2 * z + r)) & 1u;
+      if (key) o.ch[r] |= 1u << z;
+      o.av[r][z] = key ? req[2 * z + r] : 0;
+    }
+  numa_perm(o, 0);
+  numa_perm(o, 1);
+}
+
+// One workgroup per view set (a node of the matched pod's reservations holding NUMA resources / CPUs, the pod binding
+// no CPUs, a NUMA policy merged): the views in LDS; every lane takes masks of IterateBitMasks' order and asks the
+// Allocate of generateResourceHints (resource_manager.go:586-594): tryAllocateFromReservation over the trials (the
+// first satisfied one), else -- without a reservation affinity -- tryAllocateFromNode; lane 0 merges the hint lists
+// as numa_admit does (preferred scan, BestEffort's full fold) and runs Plugin.Allocate on the affinity
+// (topology_hint.go:78-118); lanes q <= n then record each trial's (and the node's own) allocation on it and the Score
+// calculateAllocatableAndRequested gives with its options (scoring.go:101-119, 141-186).  Reads the SoA only.
+__global__ __launch_bounds__(64) void k_numa_views(SoA s, const DevPod* __restrict__ pods,
+                                                   const NumaRsvView* __restrict__ views, NumaRsvOut* __restrict__ out,
+                                                   KArgs k) {
+  const NumaRsvView& w = views[blockIdx.x];
+  const DevPod p = pods[0];
+  const int64_t i = w.node;
+  const int n = min(w.n, NV_MAX);
+  const int lane = (int)threadIdx.x;
+  __shared__ NumaNode s_v[2 + 2 * NV_MAX];  // 0 hint, 1 node, 2 + q trial q, 2 + NV_MAX + q its requiredResources
+  __shared__ int64_t s_al[NV_MAX + 1][2][8];  // the allocated amounts of trial q / the node (NV_MAX)
+  __shared__ unsigned long long s_L[2][4];
+  __shared__ uint32_t s_aff;
+  __shared__ int32_t s_st, s_reason;
+  NodeRegs nr;
+  load_row(s, i, nr);
+  const uint32_t nf = nr.flags;
+  if (lane < 2 + 2 * NV_MAX) {
+    NumaNode base;
+    numa_load(s, i, base);
+    NumaNode o;
+    int64_t al[2][8];
+    if (lane == 0) {
+      numa_view_reuse(s, i, base, w.entry, w.hint, w.hint_keys, o, al);
+      s_v[0] = o;
+    } else if (lane == 1) {
+      s_v[1] = base;
+      for (int r = 0; r < 2; r++)
+        for (int z = 0; z < 8; z++) s_al[NV_MAX][r][z] = numa_al(s, i, base, z, r);
+    } else if (lane < 2 + n) {
+      const int q = lane - 2;
+      numa_view_reuse(s, i, base, w.entry, w.reuse[q], w.keys[q], o, al);
+      s_v[lane] = o;
+      for (int r = 0; r < 2; r++)
+        for (int z = 0; z < 8; z++) s_al[q][r][z] = al[r][z];
+    } else if (lane >= 2 + NV_MAX && lane < 2 + NV_MAX + n) {
+      const int q = lane - 2 - NV_MAX;
+      if (w.has_req[q]) numa_view_req(base, w.req[q], w.req_keys[q], o), s_v[lane] = o;
+    }
+  }
+  if (lane < 8) reinterpret_cast<unsigned long long*>(s_L)[lane] = 0ull;
+  __syncthreads();
+  // tryAllocateFromReservation's trial q with the hint m: Allocate on its view; a Restricted one's second Allocate
+  // over its requiredResources (a binding pod's CPU checks do not arise: the pod binds none)
+  auto trial = [&](int q, uint32_t m) -> bool {
+    if (!numa_fits(s_v[2 + q], m, p)) return false;
+    return !(w.restricted[q] && w.has_req[q]) || numa_fits(s_v[2 + NV_MAX + q], m, p);
+  };
+  auto allocate = [&](uint32_t m) -> bool {  // Plugin.Allocate / the hint pass's check on mask m (0: no hint)
+    if (!m) return true;
+    for (int q = 0; q < n; q++)
+      if (trial(q, m)) return true;
+    return !w.required && numa_fits(s_v[1], m, p);
+  };
+  const NumaNode& hv = s_v[0];
+  const uint32_t all = hv.zm;
+  bool present[2];
+  uint32_t lack[2];
+  numa_present_lack(hv, p, present, lack);
+  for (int e = lane; e < 255; e += 64) {  // generateResourceHints: the feasible masks per resource
+    const uint32_t m = NUMA_ORDER[e];
+    if (m & ~all) continue;
+    const bool in0 = present[0] && !(m & lack[0]), in1 = present[1] && !(m & lack[1]);
+    if ((!in0 && !in1) || !allocate(m)) continue;
+    const unsigned long long bit = 1ull << (m & 63u);
+    if (in0) atomicOr(&s_L[0][m >> 6], bit);
+    if (in1) atomicOr(&s_L[1][m >> 6], bit);
+  }
+  __syncthreads();
+  if (lane == 0) {
+    const int policy = pf_numa_policy(p.flags) ? pf_numa_policy(p.flags) : nf_numa_policy(nf);
+    const bool excl = (p.flags & PF_NUMA_EXCL_REQ) != 0;
+    const bool single = policy == KE_NUMA_POLICY_SINGLE_NUMA_NODE, restricted = policy == KE_NUMA_POLICY_RESTRICTED;
+    int st = KE_CODE_SUCCESS, reason = KE_REASON_NONE;
+    uint32_t aff = 0;
+    uint64_t L[2][4];
+    for (int r = 0; r < 2; r++)
+      for (int q = 0; q < 4; q++) L[r][q] = s_L[r][q];
+    const int R = (int)present[0] + (int)present[1];
+    if (all == 0) {  // topology_hint.go:31-41
+      st = KE_CODE_UNSCHEDULABLE_AND_UNRESOLVABLE, reason = KE_REASON_NUMA_MISSING_RESOURCES;
+    } else if (nf & NF_NUMA_OPT_ERR) {
+      st = KE_CODE_UNSCHEDULABLE, reason = KE_REASON_NUMA_HINT_UNALIGNED;
+    } else if (R == 0) {  // one preferred any-NUMA hint per provider
+      if (policy != KE_NUMA_POLICY_BEST_EFFORT && !exclusive_ok(hv, all, excl))
+        st = KE_CODE_UNSCHEDULABLE, reason = KE_REASON_NUMA_HINT_UNALIGNED;
+      else
+        aff = single ? 0u : all;
+    } else {
+      int minr[2] = {9, 9};
+      for (int e = 0; e < 255; e++) {
+        const uint32_t m = NUMA_ORDER[e];
+        for (int r = 0; r < 2; r++)
+          if (present[r] && bit256(L[r], m)) minr[r] = min(minr[r], __popc(m));
+      }
+      const bool empty0 = present[0] && minr[0] == 9, empty1 = present[1] && minr[1] == 9;
+      uint32_t best = all;
+      int32_t bsc = 0;
+      bool found = false;
+      if (!empty0 && !empty1)
+        for (int e = 0; e < 255; e++) {  // the preferred merged hints, IterateBitMasks order
+          const uint32_t m = NUMA_ORDER[e];
+          if ((m & ~all) || (single && __popc(m) != 1)) continue;
+          bool cand = true;
+          for (int r = 0; r < 2; r++)
+            if (present[r]) cand = cand && bit256(L[r], m) && (restricted || (int)__popc(m) == minr[r]);
+          if (!cand || !exclusive_ok(hv, m, excl)) continue;
+          const int32_t sc = R * numa_hint_score(s, i, hv, m, p, k);
+          if (!found || narrower(m, best) || (__popc(m) == __popc(best) && sc > bsc)) best = m, bsc = sc, found = true;
+        }
+      if (found) {
+        aff = (single && best == all) ? 0u : best;
+      } else if (policy != KE_NUMA_POLICY_BEST_EFFORT) {
+        st = KE_CODE_UNSCHEDULABLE, reason = KE_REASON_NUMA_HINT_UNALIGNED;
+      } else {  // mergeFilteredHints over every permutation of the lists
+        MergeLists ml;
+        ml.n = 0;
+        for (int r = 0; r < 2; r++) {
+          if (!present[r]) continue;
+          int c = 0;
+          if (minr[r] == 9) {
+            ml.m[ml.n][0] = 0, c = 1, ml.unsat[ml.n] = 1;
+          } else {
+            for (int e = 0; e < 255; e++)
+              if (bit256(L[r], NUMA_ORDER[e])) ml.m[ml.n][c++] = NUMA_ORDER[e];
+            ml.unsat[ml.n] = 0;
+          }
+          ml.len[ml.n] = c;
+          ml.ds[ml.n] = 0;
+          ml.n++;
+        }
+        DsHints dh;
+        dh.status = 0;
+        dh.none = true;
+        dh.copies = 0;
+        aff = merge_all_permutations(s, i, hv, p, k, ml, dh, excl);
+      }
+    }
+    if (st == KE_CODE_SUCCESS && !allocate(aff)) {
+      st = KE_CODE_UNSCHEDULABLE;
+      reason = w.required ? KE_REASON_RSV_INSUFFICIENT_NUMA : KE_REASON_NUMA_INSUFFICIENT_RESOURCES;
+    }
+    s_aff = aff;
+    s_st = st;
+    s_reason = reason;
+  }
+  __syncthreads();
+  const uint32_t aff = s_aff;
+  // per trial (lane q < n) and the node's own (lane NV_MAX): the allocation on the affinity and the Score with the
+  // options it used -- NUMA-scope allocatable / requested of the zones it touches, else the node's
+  bool ok = false;
+  if (lane < n || lane == NV_MAX) {
+    const int q = lane;
+    int64_t d[2][8] = {{0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0, 0}};
+    uint32_t got[2] = {0, 0};
+    if (q < n) {
+      ok = !aff || trial(q, aff);
+      if (ok && aff) numa_distribute<true>((w.restricted[q] && w.has_req[q]) ? s_v[2 + NV_MAX + q] : s_v[2 + q], aff, p,
+                                           got, d);
+    } else {
+      ok = !aff || numa_fits(s_v[1], aff, p);
+      if (ok && aff) numa_distribute<true>(s_v[1], aff, p, got, d);
+    }
+    const uint32_t zs = got[0] | got[1];
+    int64_t req[2] = {nr.nreq[0], nr.nreq[1]}, alloc[2] = {nr.nalloc[0], nr.nalloc[1]};
+    if (zs) {
+      req[0] = req[1] = alloc[0] = alloc[1] = 0;
+      for (int z = 0; z < 8; z++)
+        if ((zs >> z) & 1u)
+          for (int r = 0; r < 2; r++) {
+            alloc[r] += numa_cap(s, i, z, r);
+            req[r] += s_al[q < n ? q : NV_MAX][r][z];
+          }
+    }
+    out[blockIdx.x].score[q < n ? q : NV_MAX] = ok ? numa_scope_score((k.flags & AF_NUMA_MOST) != 0, req, alloc, p, k) : 0;
+    for (int z = 0; z < 8; z++)
+      for (int r = 0; r < 2; r++) out[blockIdx.x].dist[q < n ? q : NV_MAX][2 * z + r] = ok ? d[r][z] : 0;
+  }
+  const uint64_t okm = __ballot(ok);
+  if (lane == 0) {
+    out[blockIdx.x].st = s_st;
+    out[blockIdx.x].reason = s_reason;
+    out[blockIdx.x].aff = aff;
+    out[blockIdx.x].ok = (uint32_t)(okm & ((1ull << n) - 1ull)) | (((okm >> NV_MAX) & 1ull) ? 1u << NV_MAX : 0u);
+  }
+}
+
 // A singleton batch of a pod that may bind CPUs, after k_select: selectHost's node, then Reserve in
 // profile order — LoadAware, NodeNUMAResource (the NUMA allocation on the affinity Admit picks and the
 // cpuset; a failed Allocate fails Reserve and the pod stays unplaced), DeviceShare.  One thread: the
@@ -6210,7 +6476,16 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
     if (nsoa) numa_load(s, node, v);
     // DeviceShare's hints join the Admit of a pod with device requests (topology_hint.go:38-58)
     ds_here = DS && (pod.flags & PF_DS) && (nf & NF_DS_CACHE);
-    if (ok && npol) {  // the affinity the Filter's Admit stored and the allocation on it
+    const RsvOvr* nro = (ok && npol && !rcb && (nf & NF_RSV_CS)) ? rsv_ovr_of(s, node) : nullptr;
+    if (nro && nro->numa_on) {  // a reservation-matched pod: the allocation k_numa_views chose (RsvOvr.numa_dist)
+      aff = nro->numa_aff;
+      for (int z = 0; z < 8; z++)
+        for (int r = 0; r < 2; r++) {
+          dist[r][z] = nro->numa_dist[2 * z + r];
+          if (dist[r][z] != 0) got[r] |= 1u << z;
+        }
+      stored = true;
+    } else if (ok && npol) {  // the affinity the Filter's Admit stored and the allocation on it
       // this rank evaluated the node: its eval stored the affinity (a feasible node admitted, binding pods);
       // else (a node of another shard, a DeviceShare pod) Admit runs here
       const bool have = node >= eval_lo && node < eval_hi && !ds_here;
@@ -6536,6 +6811,8 @@ struct DeviceState {
   int64_t rsv_views_cap = 0;
   void* d_ds_views = nullptr;       // k_ds_views: views, outputs, the pod
   int64_t ds_views_cap = 0;
+  void* d_numa_views = nullptr;     // k_numa_views: views, outputs, the pod
+  int64_t numa_views_cap = 0;
   RsvOvr* d_rovr = nullptr;         // the segment's allocate-from-reservation decisions (SoA::rovr)
   int64_t rovr_cap = 0;
   int32_t* d_rsv_out = nullptr;     // [4]
@@ -6695,6 +6972,34 @@ int device_ds_views(Context* ctx, const ke_pod& pod, int64_t now, const std::vec
   return KE_OK;
 }
 
+int device_numa_views(Context* ctx, const ke_pod& pod, int64_t now, const std::vector<NumaRsvView>& views,
+                      std::vector<NumaRsvOut>& out) {
+  DeviceState* d = ctx->dev;
+  out.assign(views.size(), NumaRsvOut{});
+  if (views.empty()) return KE_OK;
+  HIP_OK(hipSetDevice(d->device));
+  int rc = device_refresh(ctx, now);  // the rows as the segment will see them
+  if (rc) return rc;
+  if (!d->soa.nf) return fail(KE_ERR_DEVICE, "NUMA views without a NUMA SoA");
+  for (const NumaRsvView& v : views)
+    if (v.node < 0 || v.node >= ctx->n_nodes || v.n < 0 || v.n > NV_MAX)
+      return fail(KE_ERR_DEVICE, "NUMA view node / trial count out of range");
+  const DevPod dp = make_dev_pod(ctx->cfg, pod, pod_hints(*ctx, pod), &ctx->tmpl);
+  const KArgs k = make_kargs(ctx, now);
+  const size_t vb = sizeof(NumaRsvView) * views.size(), ob = sizeof(NumaRsvOut) * views.size();
+  rc = ensure((void**)&d->d_numa_views, &d->numa_views_cap, (int64_t)(vb + ob + sizeof(DevPod)));
+  if (rc) return rc;
+  uint8_t* base = (uint8_t*)d->d_numa_views;
+  HIP_OK(hipMemcpyAsync(base, views.data(), vb, hipMemcpyHostToDevice, d->stream));
+  HIP_OK(hipMemcpyAsync(base + vb + ob, &dp, sizeof(DevPod), hipMemcpyHostToDevice, d->stream));
+  hipLaunchKernelGGL(k_numa_views, dim3((unsigned)views.size()), dim3(64), 0, d->stream, d->soa,
+                     (const DevPod*)(base + vb + ob), (const NumaRsvView*)base, (NumaRsvOut*)(base + vb), k);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(out.data(), base + vb, ob, hipMemcpyDeviceToHost, d->stream));
+  HIP_OK(hipStreamSynchronize(d->stream));
+  return KE_OK;
+}
+
 // k_rsv_pick's result of the last device_schedule (a segment of one KE_RSV_MATCHED pod)
 int device_rsv_result(Context* ctx, int32_t* out4) {
   DeviceState* d = ctx->dev;
@@ -6718,7 +7023,7 @@ void device_destroy(Context* ctx) {
                   d->d_cpurows, d->d_cpusets, d->d_aff, d->soa.qt, d->soa.qm, d->d_sched, d->d_stale,
                   d->d_stale_cnt, d->d_pre, d->d_trows, d->d_tcnt, d->d_parts_done, d->d_scores2, d->d_split2, d->d_chg, d->soa.rec, d->soa.pt, d->soa.kerr,
                   d->soa.xf, d->soa.xm, d->d_xrows, d->soa.dsx, d->d_ph, d->d_vfo, d->d_rsv, d->d_rsv_out, d->d_rsv_st,
-                  d->d_rsv_views, d->d_ds_views, d->d_rovr};
+                  d->d_rsv_views, d->d_ds_views, d->d_numa_views, d->d_rovr};
   if (d->estream) (void)hipStreamSynchronize(d->estream);
   if (d->estream2) (void)hipStreamSynchronize(d->estream2);
   for (void* p : ptrs)

@@ -81,15 +81,49 @@ struct RsvViewOut {
 // (tryAllocateFromReservation / scoreWithNominatedReservation, deviceshare/plugin.go:350-364, scoring.go:83-102);
 // ds_res = Reserve's devices: 0 the node's own allocation, 1 `ds_minors` (bit 16*type + minor), 2 Reserve fails.
 // rfilter (a reservation affinity, AF_RSV_ONLY): 1 the Reservation Filter passes on the node (else it fails).
+// NodeNUMAResource under a NUMA policy (k_numa_views, a pod binding no CPUs): numa_on = the Filter's status / reason /
+// affinity and the Score below replace the node's own (the hints over the allocate-from-reservation trials and the
+// nominated reservation's allocation, nodenumaresource/reservation.go:270-424, scoring.go:101-119); Reserve adds
+// numa_dist ([2*id + r]) to the zones.
 struct RsvOvr {
   int32_t node;
   int8_t filter, reserve;
   int8_t ds_on, ds_res;
   uint8_t ds_st, ds_reason;
-  int8_t rfilter, pad;
-  int16_t ds_raw, pad2;
+  int8_t rfilter, numa_on;
+  int16_t ds_raw, numa_score;
+  uint8_t numa_st, numa_reason, numa_aff, pad;
+  int32_t pad2;
   uint64_t ds_minors;
   uint64_t cpus[4];
+  int64_t numa_dist[16];
+};
+// The NodeNUMAResource allocate-from-reservation views of a node for a reservation-matched pod binding no CPUs under a
+// NUMA policy (k_numa_views; nodenumaresource/reservation.go:270-424, resource_manager.go:130-138, 195-254): beyond
+// the node's row (its unmatched restore applied), per NUMA id with an allocation entry (`entry`) the reusable amounts
+// [2*id + r] (keys: bit 2*id + r) of the hint view (mergedMatchedAllocatable) and of each trial q < n over
+// RestoreReservation's matched set in index order (mergedMatchedAllocated + its remained); a Restricted trial's
+// requiredResources (its remained, signed; has_req = the reserve pod holds NUMA amounts).
+constexpr int NV_MAX = 8;
+struct NumaRsvView {
+  int32_t node, n;
+  int32_t required;  // a reservation affinity: no allocation from the node itself
+  uint32_t entry;
+  uint32_t hint_keys;
+  uint32_t keys[NV_MAX], req_keys[NV_MAX];
+  uint8_t restricted[NV_MAX], has_req[NV_MAX];
+  int64_t hint[16];
+  int64_t reuse[NV_MAX][16];
+  int64_t req[NV_MAX][16];
+};
+// its outcome: the Filter (status, reason, the merged affinity -- 0 nil), and on that affinity per trial q (bit q of
+// ok; bit NV_MAX: the node's own) the allocation and the Score with the options it used
+struct NumaRsvOut {
+  int32_t st, reason;
+  uint32_t aff, ok;
+  int32_t score[NV_MAX + 1];
+  int32_t pad;
+  int64_t dist[NV_MAX + 1][16];
 };
 // One DeviceShare allocate-from-reservation view of a node (k_ds_views): the allocator's arguments a
 // reservation-matched (or -ignored) pod sees beyond the node's row (AutopilotAllocator with preemptible /

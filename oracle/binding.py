@@ -73,6 +73,8 @@ def load():
         "or_reservation_resources_get": (C.c_int, [V, i32, i32, V, V]),
         "or_restore_state": (C.c_int, [V, i32, V]),
         "or_numa_reserve_from_rsv": (C.c_int, [V, V, i32, V, i32, i32, i32, V]),
+        "or_numa_reserve_policy": (C.c_int, [V, V, i32, V, i32, i32, i32, C.c_uint32, V, V]),
+        "or_numa_reserve_ignored": (C.c_int, [V, V, i32, V]),
         "or_reservation_allocs_get": (C.c_int, [V, i32, V]),
         "or_pod_reservations": (C.c_int, [V, i32, V, V]),
         "or_last_reservations": (C.c_int, [V, i32, V]),
@@ -321,6 +323,24 @@ class Oracle:
         out = np.zeros(4, np.uint64)
         rc = self.lib.or_numa_reserve_from_rsv(self.h, abi.ptr(p), int(node), abi.ptr(ids), len(ids), int(nom),
                                                int(required), abi.ptr(out))
+        return rc, out
+
+    def numa_reserve_policy(self, pod, node, ids, nom, required, aff):
+        """NodeNUMAResource Reserve under a NUMA policy with a stored affinity (or_numa_reserve_policy):
+        (code, NUMA allocation [2*id + r], cpuset words)."""
+        p = as_pod_array([pod] if isinstance(pod, abi.Pod) else np.asarray(pod).reshape(1))
+        ids = np.ascontiguousarray(ids, np.int32)
+        dist = np.zeros(16, np.int64)
+        out = np.zeros(4, np.uint64)
+        rc = self.lib.or_numa_reserve_policy(self.h, abi.ptr(p), int(node), abi.ptr(ids), len(ids), int(nom),
+                                             int(required), int(aff), abi.ptr(dist), abi.ptr(out))
+        return rc, dist, out
+
+    def numa_reserve_ignored(self, pod, node):
+        """tryAllocateIgnoreReservation's Reserve on a node without a NUMA policy: (code, cpuset words)."""
+        p = as_pod_array([pod] if isinstance(pod, abi.Pod) else np.asarray(pod).reshape(1))
+        out = np.zeros(4, np.uint64)
+        rc = self.lib.or_numa_reserve_ignored(self.h, abi.ptr(p), int(node), abi.ptr(out))
         return rc, out
 
     def restore_state(self, r):

@@ -114,6 +114,8 @@ struct or_cluster {
   const char* resv_m;           /* the matched flags of the pod being evaluated (or_resv_begin), NULL = none */
   int ignored;                  /* the pod being evaluated / reserved is reservation-ignored (or_numa_ignored) */
   const int32_t* ds_nom;        /* per node the reservation nominated for the pod being scored / reserved (or NULL) */
+  const int32_t* numa_nom;      /* the same for NodeNUMAResource's Score (allocateWithNominatedReservation), or NULL */
+  const int8_t* numa_rok;       /* per reservation NodeNUMAResource's FilterNominateReservation under a NUMA policy (or NULL) */
   uint8_t* rcpu;                /* [reservation][cpu] owner counts (or_owner_update), NULL until first needed */
   int32_t n_resv;
   /* each reservation's allocatable entries beyond cpu / memory (or_reservations_load_full): roff[i] .. roff[i+1] */
@@ -1092,7 +1094,25 @@ static int zone_cpusets(const or_node* nd, int id, int given) {
 
 /* getResourceOptions -> amplifyNUMANodeResources (util.go:78-98) + getAvailableNUMANodeResources
  * (node_allocation.go:221-243).  Returns -1 on an amplification-ratio annotation error. */
+/* ResourceOptions beyond the node's own restore state, for NodeNUMAResource's allocate-from-reservation
+ * (nodenumaresource/reservation.go:270-424, resource_manager.go:130-138): reusableResources added to the restore
+ * state's (quotav1.Add per NUMA id: keys of both), requiredResources replacing totalAvailable
+ * (allocateResourcesByHint, resource_manager.go:226-254), preferredCPUs (numa_cs_build_pref). */
+typedef struct numa_opt {
+  int64_t reuse[KE_MAX_NUMA][KE_NRES];
+  uint8_t reuse_key[KE_MAX_NUMA][KE_NRES];
+  int has_req;
+  int64_t req[KE_MAX_NUMA][KE_NRES];
+  uint8_t req_key[KE_MAX_NUMA][KE_NRES];
+  int has_pref;
+  uint64_t pref[ACC_WORDS];
+} numa_opt;
+
+static int numa_view_build_opt(const or_node* nd, numa_view* v, const numa_cs* cs, const numa_opt* opt);
 static int numa_view_build(const or_node* nd, numa_view* v, const numa_cs* cs) {
+  return numa_view_build_opt(nd, v, cs, NULL);
+}
+static int numa_view_build_opt(const or_node* nd, numa_view* v, const numa_cs* cs, const numa_opt* opt) {
   memset(v, 0, sizeof *v);
   double ratio;
   int amplify_caps = 0;
@@ -1131,9 +1151,11 @@ static int numa_view_build(const or_node* nd, numa_view* v, const numa_cs* cs) {
        * restore state (or_restore) -- keys of both, floor 0 */
       const int zid = zn->id >= 0 && zn->id < KE_MAX_NUMA ? zn->id : -1;
       for (int r = 0; r < KE_NRES; r++) {
-        const int rk = zid >= 0 && nd->rs_numa_has[zid] && nd->rs_numa_key[zid][r];
-        const int64_t q = (has[r] ? al[r] : 0) - (rk ? nd->rs_numa[zid][r] : 0);
-        v->al_has[z][r] = has[r] || rk;
+        const int rk0 = zid >= 0 && nd->rs_numa_has[zid] && nd->rs_numa_key[zid][r];
+        const int rk1 = zid >= 0 && opt && opt->reuse_key[zid][r];
+        const int64_t reuse = (rk0 ? nd->rs_numa[zid][r] : 0) + (rk1 ? opt->reuse[zid][r] : 0);
+        const int64_t q = (has[r] ? al[r] : 0) - reuse;
+        v->al_has[z][r] = has[r] || rk0 || rk1;
         v->al[z][r] = v->al_has[z][r] && q > 0 ? q : 0;
       }
     }
@@ -1143,6 +1165,12 @@ static int numa_view_build(const or_node* nd, numa_view* v, const numa_cs* cs) {
       const int64_t q = v->cap_has[z][r] ? v->cap[z][r] - a : -a;
       v->av[z][r] = q > 0 ? q : 0;
     }
+    if (opt && opt->has_req) /* totalAvailable = requiredResources: its NUMA ids and keys, signed (quotav1.Subtract) */
+      for (int r = 0; r < KE_NRES; r++) {
+        const int in = zn->id >= 0 && zn->id < KE_MAX_NUMA && opt->req_key[zn->id][r];
+        v->av_has[z][r] = (uint8_t)in;
+        v->av[z][r] = in ? opt->req[zn->id][r] : 0;
+      }
     /* trimNUMANodeResources (resource_manager.go:166-192): a required bind policy caps a zone's cpu
      * at its CPUs that the policy leaves available */
     if (cs && cs->rcb && cs->required && v->av[z][KE_RES_CPU] != 0 && zn->id < KE_MAX_NUMA &&
@@ -1213,11 +1241,197 @@ static int numa_distribute(const numa_view* v, uint32_t mask, const ke_pod* pod,
   return ok;
 }
 
+/* ---- NodeNUMAResource's allocate-from-reservation under a NUMA policy (nodenumaresource/reservation.go:270-424) ---- */
+
+/* RestoreReservation's matched set on `node` (reservation.go:185-259): the pod's matched usable reservations there
+ * whose reserve pod holds NUMA resources or a cpuset (c->resv_m); ascending index.  Returns the count. */
+static int numa_rsv_matched(const or_cluster* c, int32_t node, int32_t* ids) {
+  int n = 0;
+  for (int32_t r = 0; c->resv_m && c->ralloc && r < c->n_resv; r++)
+    if (c->resv_m[r] && c->resv[r].node == node && or_resv_usable(&c->resv[r]) &&
+        (or_holds_of_idx(c, r) & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)) && n < 64)
+      ids[n++] = r;
+  return n;
+}
+
+static int numa_any(const int64_t* v16) {
+  for (int j = 0; j < KE_MAX_NUMA * KE_NRES; j++)
+    if (v16[j]) return 1;
+  return 0;
+}
+/* quotav1.Add of a NUMA map into o->reuse (keys of both: a non-zero amount is a key) */
+static void numa_opt_add(numa_opt* o, const int64_t* v16, const uint8_t* k16) {
+  for (int id = 0; id < KE_MAX_NUMA; id++)
+    for (int r = 0; r < KE_NRES; r++)
+      if (k16 ? k16[2 * id + r] : v16[2 * id + r] != 0) {
+        o->reuse_key[id][r] = 1;
+        o->reuse[id][r] += v16[2 * id + r];
+      }
+}
+/* reservationAlloc.allocated (Σ the owner pods' NUMA resources) and remained = quotav1.Subtract(allocatable,
+ * allocated) per NUMA id, keys of both; both nil without a NUMA allocation of the reserve pod (reservation.go:195-208) */
+static int numa_rsv_remained(const ke_reservation_alloc* a, int64_t* rem16, uint8_t* key16) {
+  memset(rem16, 0, sizeof(int64_t) * 2 * KE_MAX_NUMA);
+  memset(key16, 0, 2 * KE_MAX_NUMA);
+  if (!numa_any(a->numa)) return 0;
+  for (int j = 0; j < 2 * KE_MAX_NUMA; j++) {
+    key16[j] = a->numa[j] != 0 || a->owner_numa[j] != 0;
+    rem16[j] = a->numa[j] - a->owner_numa[j];
+  }
+  return 1;
+}
+static void cpus_remained(const ke_reservation_alloc* a, uint64_t* out) {
+  for (int w = 0; w < ACC_WORDS; w++) out[w] = a->cpuset[w] & ~a->owner_cpuset[w];
+}
+
+/* The views of the hint pass (GetTopologyHints, resource_manager.go:136-138): reusable = mergedUnmatchedUsed (the
+ * restore state) + mergedMatchedAllocatable, preferredCPUs = mergedMatchedRemainCPUs */
+static void numa_opt_hint(const or_cluster* c, const int32_t* M, int nM, numa_opt* o) {
+  memset(o, 0, sizeof *o);
+  o->has_pref = 1;
+  for (int q = 0; q < nM; q++) {
+    const ke_reservation_alloc* a = &c->ralloc[M[q]];
+    numa_opt_add(o, a->numa, NULL);
+    uint64_t rc[ACC_WORDS];
+    cpus_remained(a, rc);
+    for (int w = 0; w < ACC_WORDS; w++) o->pref[w] |= rc[w];
+  }
+}
+/* tryAllocateFromReservation's options for reservation r (reservation.go:293-311): reusable = mergedUnmatchedUsed +
+ * mergedMatchedAllocated + r's remained, preferredCPUs = mergedMatchedAllocatedCPUs ∪ r's remainedCPUs */
+static void numa_opt_rsv(const or_cluster* c, const int32_t* M, int nM, int32_t r, numa_opt* o) {
+  memset(o, 0, sizeof *o);
+  o->has_pref = 1;
+  for (int q = 0; q < nM; q++) {
+    const ke_reservation_alloc* a = &c->ralloc[M[q]];
+    if (numa_any(a->numa)) numa_opt_add(o, a->owner_numa, NULL);
+    for (int w = 0; w < ACC_WORDS; w++) o->pref[w] |= a->cpuset[w]; /* allocatedCPUs = the reserve pod's CPUs */
+  }
+  int64_t rem[2 * KE_MAX_NUMA];
+  uint8_t key[2 * KE_MAX_NUMA];
+  if (numa_rsv_remained(&c->ralloc[r], rem, key)) numa_opt_add(o, rem, key);
+  uint64_t rc[ACC_WORDS];
+  cpus_remained(&c->ralloc[r], rc);
+  for (int w = 0; w < ACC_WORDS; w++) o->pref[w] |= rc[w];
+}
+
+/* resourceManager.Allocate (resource_manager.go:195-224) with the hint `mask` (0 = nil) and options `o`:
+ * allocateResourcesByHint, then allocateCPUSet for a binding pod.  1 and the NUMA allocation (dist16[2*id + r]) and
+ * cpuset, or 0. */
+static int numa_alloc_try(const or_cluster* c, const or_node* nd, const ke_pod* pod, uint32_t mask, const numa_opt* o,
+                          int64_t* dist16, uint64_t* cpus) {
+  numa_cs cs;
+  numa_cs_build_pref(c, nd, pod, &cs, o && o->has_pref ? o->pref : NULL);
+  if (dist16) memset(dist16, 0, sizeof(int64_t) * 2 * KE_MAX_NUMA);
+  if (cpus) memset(cpus, 0, sizeof(uint64_t) * ACC_WORDS);
+  if (cs.rcb && !cs.valid) return 0;
+  numa_view v;
+  if (numa_view_build_opt(nd, &v, &cs, o) != 0) return 0;
+  int64_t out[KE_MAX_NUMA][KE_NRES];
+  memset(out, 0, sizeof out);
+  if (mask && !numa_distribute(&v, mask, pod, out, &cs)) return 0;
+  if (cs.rcb) {
+    uint64_t got[ACC_WORDS];
+    if (cpuset_allocate_cs(nd, &cs, &v, mask ? (const int64_t(*)[KE_NRES])out : NULL, got) != 0) return 0;
+    if (cpus) memcpy(cpus, got, sizeof got);
+  }
+  if (dist16)
+    for (int z = 0; z < v.n; z++)
+      if (v.id[z] >= 0 && v.id[z] < KE_MAX_NUMA)
+        for (int r = 0; r < KE_NRES; r++) dist16[2 * v.id[z] + r] = out[z][r];
+  return 1;
+}
+
+/* tryAllocateFromReservation (reservation.go:270-424) for a pod matching the reservations M[0..nM) of RestoreReservation's
+ * matched set on the node, over S[0..nS) (M itself, or the nominated / nominating one), with the hint `mask`:
+ * Default / Aligned: one Allocate; Restricted: that Allocate, numCPUsNeeded <= |remainedCPUs| for a binding pod, then an
+ * Allocate with requiredResources = remained and preferredCPUs = remainedCPUs whose cpuset may not outgrow them.  The
+ * first satisfied one in ascending index (Go ranges over a map: which one is the reference's choice only for one) gives
+ * 1, its options (*used) and its allocation; none: -1 under a reservation affinity, else 0 (nil: tryAllocateFromNode). */
+static int numa_from_rsv_try(const or_cluster* c, const ke_pod* pod, int32_t node, const int32_t* M, int nM,
+                             const int32_t* S, int nS, uint32_t mask, int required, numa_opt* used, int64_t* dist16,
+                             uint64_t* cpus) {
+  const or_node* nd = &c->nodes[node];
+  if (nM == 0) return 0;
+  for (int q = 0; q < nS; q++) {
+    const int32_t r = S[q];
+    numa_opt o1;
+    numa_opt_rsv(c, M, nM, r, &o1);
+    if (!numa_alloc_try(c, nd, pod, mask, &o1, dist16, cpus)) continue;
+    if (c->resv[r].allocate_policy == KE_RSV_POLICY_RESTRICTED) {
+      uint64_t rc[ACC_WORDS];
+      cpus_remained(&c->ralloc[r], rc);
+      const int reserved = popcount_set(rc);
+      cpuset_state st;
+      cpuset_prefilter(c, pod, &st);
+      numa_cs cs0;
+      numa_cs_build(c, nd, pod, &cs0);
+      if (cs0.rcb && st.num_cpus > reserved) continue;
+      numa_opt o2 = o1;
+      int64_t rem[2 * KE_MAX_NUMA];
+      uint8_t key[2 * KE_MAX_NUMA];
+      o2.has_req = numa_rsv_remained(&c->ralloc[r], rem, key);
+      for (int id = 0; id < KE_MAX_NUMA; id++)
+        for (int k = 0; k < KE_NRES; k++) {
+          o2.req[id][k] = rem[2 * id + k];
+          o2.req_key[id][k] = key[2 * id + k];
+        }
+      memcpy(o2.pref, rc, sizeof rc);
+      uint64_t got[ACC_WORDS];
+      if (!numa_alloc_try(c, nd, pod, mask, &o2, dist16, got)) continue;
+      if (popcount_set(got) > reserved) continue; /* (never: the take is numCPUsNeeded <= reserved) */
+      if (cpus) memcpy(cpus, got, sizeof got);
+    }
+    if (used) *used = o1;
+    return 1;
+  }
+  return required ? -1 : 0;
+}
+
+/* The Allocate of a matched pod under a NUMA policy on the node with the hint `mask` as Filter's hint generation and
+ * Plugin.Allocate run it (resource_manager.go:586-594, topology_hint.go:78-118): from one of the node's matched
+ * reservations, else (no reservation affinity) from the node.  1 = a hint / allocation, 0 = none. */
+static int numa_matched_alloc_ok(const or_cluster* c, const ke_pod* pod, int32_t node, const int32_t* M, int nM,
+                                 uint32_t mask) {
+  const int required = pod->reservation_matched == KE_RSV_AFFINITY;
+  const int r = numa_from_rsv_try(c, pod, node, M, nM, M, nM, mask, required, NULL, NULL, NULL);
+  if (r != 0) return r > 0;
+  return numa_alloc_try(c, &c->nodes[node], pod, mask, NULL, NULL, NULL);
+}
+
+/* allocateWithNominatedReservation (reservation.go:492-522) then tryAllocateFromNode (plugin.go:671-689) for a matched
+ * pod under a NUMA policy with the stored affinity: the nominated reservation nom (-1: none) -- Score and Reserve.
+ * 1 and the allocation (NUMA, cpuset) and the options it used (*used, for calculateAllocatableAndRequested), or 0 = an
+ * error status (no nominated reservation under an affinity; the reservation's or the node's Allocate failed). */
+static int numa_matched_alloc(const or_cluster* c, const ke_pod* pod, int32_t node, const int32_t* M, int nM,
+                              int32_t nom, uint32_t aff, numa_opt* used, int64_t* dist16, uint64_t* cpus) {
+  const int required = pod->reservation_matched == KE_RSV_AFFINITY;
+  if (nom < 0 && required) return 0; /* "no nominated reservation" */
+  int in = 0;
+  for (int q = 0; q < nM; q++) in |= M[q] == nom;
+  if (nom >= 0 && in) {
+    const int r = numa_from_rsv_try(c, pod, node, M, nM, &nom, 1, aff, required, used, dist16, cpus);
+    if (r < 0) return 0;
+    if (r > 0) return 1;
+  }
+  memset(used, 0, sizeof *used); /* tryAllocateFromNode: reusable = mergedUnmatchedUsed, no preferred CPUs */
+  return numa_alloc_try(c, &c->nodes[node], pod, aff, NULL, dist16, cpus);
+}
+
 typedef struct numa_hint {
   uint32_t mask; /* 0 = nil NUMANodeAffinity */
   int preferred, unsatisfied;
   int64_t score;
 } numa_hint;
+
+/* A matched pod's hint pass on a node with reservations in RestoreReservation's matched set (numa_admit): every
+ * mask's Allocate goes through tryAllocateFromReservation, then tryAllocateFromNode (resource_manager.go:586-594) */
+static __thread struct {
+  int on;
+  int32_t node;
+  int nM;
+  int32_t M[64];
+} g_trial;
 
 /* generateResourceHints (resource_manager.go:525-622) for a non-cpuset pod.  Per resource (cpu,
  * memory): the list of hints in IterateBitMasks order; present[r] = the resource has a list. */
@@ -1263,7 +1477,10 @@ static void numa_generate_hints(const or_cluster* c, const or_node* nd, const nu
       const int64_t score = numa_resource_score_as(&c->cfg.numa, c->cfg.numa.numa_strategy, req, total, podreq);
       int64_t out[KE_MAX_NUMA][KE_NRES];
       /* tryAllocateFromNode with the mask: allocateResourcesByHint, then allocateCPUSet */
-      if (numa_distribute(v, mask, pod, out, cs) && (!cs || !cs->rcb || cpuset_fits_cs(nd, cs, v, (const int64_t(*)[KE_NRES])out)))
+      const int fits = g_trial.on ? numa_matched_alloc_ok(c, pod, g_trial.node, g_trial.M, g_trial.nM, mask)
+                                  : numa_distribute(v, mask, pod, out, cs) &&
+                                        (!cs || !cs->rcb || cpuset_fits_cs(nd, cs, v, (const int64_t(*)[KE_NRES])out));
+      if (fits)
         for (int r = 0; r < KE_NRES; r++) { /* generator.generateHints per resource */
           if (!total_names[r]) continue;
           if (mask & lack[r]) continue;
@@ -1448,13 +1665,32 @@ static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod,
   uint8_t status[KE_MAX_NUMA] = {0};
   for (int z = 0; z < nd->n_zone; z++)
     if (nd->zone[z].id < nd->n_zone) status[nd->zone[z].id] = nd->zone[z].numa_status;
-  if (numa_view_build(nd, &v, cs) != 0) { /* GetPodTopologyHints error -> reasons -> Unschedulable */
+  /* a matched pod on a node of its reservations holding NUMA resources / CPUs: the hint view (mergedMatchedAllocatable
+   * reusable, mergedMatchedRemainCPUs preferred) and every mask's Allocate from the reservations first */
+  const int32_t node = (int32_t)(nd - c->nodes);
+  int32_t M[64];
+  const int nM = c->resv_m && !c->ignored ? numa_rsv_matched(c, node, M) : 0;
+  numa_opt oh;
+  numa_cs cs_h;
+  if (nM > 0) {
+    numa_opt_hint(c, M, nM, &oh);
+    numa_cs_build_pref(c, nd, pod, &cs_h, oh.pref);
+    cs = &cs_h;
+  }
+  if (numa_view_build_opt(nd, &v, cs, nM > 0 ? &oh : NULL) != 0) { /* GetPodTopologyHints error -> Unschedulable */
     *reason = KE_REASON_NUMA_HINT_UNALIGNED;
     return KE_CODE_UNSCHEDULABLE;
   }
   static __thread numa_hint store[KE_NRES * 255];
   int counts[KE_NRES], present[KE_NRES];
+  if (nM > 0) {
+    g_trial.on = 1;
+    g_trial.node = node;
+    g_trial.nM = nM;
+    memcpy(g_trial.M, M, sizeof(int32_t) * (size_t)nM);
+  }
   numa_generate_hints(c, nd, &v, pod, policy, store, counts, present, cs);
+  g_trial.on = 0;
   /* DeviceShare's hints (topology_hint.go:38-58): a provider error is an Admit reason
    * (accumulateProvidersHints, manager.go:110-125) */
   static __thread numa_hint ds_list[255];
@@ -1520,14 +1756,20 @@ static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod,
     *reason = KE_REASON_NUMA_HINT_UNALIGNED;
     return KE_CODE_UNSCHEDULABLE;
   }
-  /* allocateResources -> NodeNUMAResource.Allocate -> tryAllocateFromNode with the hint */
+  /* allocateResources -> NodeNUMAResource.Allocate -> tryAllocateFromReservation / tryAllocateFromNode with the hint */
   int64_t out[KE_MAX_NUMA][KE_NRES];
   memset(out, 0, sizeof out);
-  if (best.mask && !numa_distribute(&v, best.mask, pod, out, cs)) {
+  if (nM > 0) {
+    if (!numa_matched_alloc_ok(c, pod, node, M, nM, best.mask)) {
+      *reason = pod->reservation_matched == KE_RSV_AFFINITY ? KE_REASON_RSV_INSUFFICIENT_NUMA
+                                                            : KE_REASON_NUMA_INSUFFICIENT_RESOURCES;
+      return KE_CODE_UNSCHEDULABLE;
+    }
+  } else if (best.mask && !numa_distribute(&v, best.mask, pod, out, cs)) {
     *reason = KE_REASON_NUMA_INSUFFICIENT_RESOURCES;
     return KE_CODE_UNSCHEDULABLE;
   }
-  if (cs && cs->rcb && !cpuset_fits_cs(nd, cs, &v, (const int64_t(*)[KE_NRES])out)) {
+  if (nM == 0 && cs && cs->rcb && !cpuset_fits_cs(nd, cs, &v, (const int64_t(*)[KE_NRES])out)) {
     *reason = KE_REASON_NUMA_INSUFFICIENT_CPUS; /* "not enough cpus available to satisfy request" */
     return KE_CODE_UNSCHEDULABLE;
   }
@@ -1638,13 +1880,69 @@ static int numa_allocation(const or_node* nd, const ke_pod* pod, uint32_t affini
   return numa_distribute(v, affinity, pod, out, cs);
 }
 
-/* Plugin.Score  scoring.go:66-120 -> scoreWithAmplifiedCPUs :122-139 */
-int64_t or_numa_score(const or_cluster* c, const ke_pod* pod, int32_t node) {
+/* Plugin.Score  scoring.go:66-120 -> scoreWithAmplifiedCPUs :122-139.  *err (may be NULL): the Score returned an
+ * error status (a matched pod's allocateWithNominatedReservation / tryAllocateFromNode failed, scoring.go:105-115) */
+static int64_t numa_score_ex(const or_cluster* c, const ke_pod* pod, int32_t node, int* err);
+int64_t or_numa_score(const or_cluster* c, const ke_pod* pod, int32_t node) { return numa_score_ex(c, pod, node, NULL); }
+static int64_t numa_score_ex(const or_cluster* c, const ke_pod* pod, int32_t node, int* err) {
   const or_node* n = &c->nodes[node];
+  if (err) *err = 0;
   if (pod_requests_zero(pod)) return 0; /* state.skip */
   int exclusive;
   const int policy = effective_policy(n, pod, &exclusive);
   if (policy < 0) return 0;
+  int32_t M[64];
+  const int nM = policy != KE_NUMA_POLICY_NONE && c->resv_m && !c->ignored && c->numa_nom ? numa_rsv_matched(c, node, M) : 0;
+  if (nM > 0) {
+    /* a matched pod on a node of its reservations holding NUMA resources / CPUs: the allocation from the nominated
+     * reservation (else the node) on the stored affinity, calculateAllocatableAndRequested with the options it used */
+    numa_cs cs;
+    numa_cs_build(c, n, pod, &cs);
+    if (cs.rcb && !cs.valid) return 0;
+    uint32_t aff = 0;
+    int reason;
+    if (n->n_zone == 0 || numa_admit(c, n, pod, policy, exclusive, &aff, &reason, &cs) != KE_CODE_SUCCESS) return 0;
+    numa_opt used;
+    int64_t dist16[2 * KE_MAX_NUMA];
+    uint64_t pcpus[ACC_WORDS];
+    if (!numa_matched_alloc(c, pod, node, M, nM, c->numa_nom[node], aff, &used, dist16, pcpus)) {
+      if (err) *err = 1;
+      return 0;
+    }
+    numa_cs csu;
+    numa_cs_build_pref(c, n, pod, &csu, used.has_pref ? used.pref : NULL);
+    numa_view v;
+    if (numa_view_build_opt(n, &v, &csu, &used) != 0) return 0;
+    int64_t alloc[KE_NRES] = {0, 0}, req[KE_NRES] = {0, 0};
+    int any = 0;
+    for (int z = 0; z < v.n; z++) {
+      const int id = v.id[z];
+      if (id < 0 || id >= KE_MAX_NUMA || (dist16[2 * id] == 0 && dist16[2 * id + 1] == 0)) continue;
+      any = 1;
+      for (int r = 0; r < KE_NRES; r++) {
+        alloc[r] += v.cap_has[z][r] ? v.cap[z][r] : 0;
+        req[r] += v.has_alloc[z] ? v.al[z][r] : 0;
+      }
+    }
+    if (!any) {
+      req[0] = n->node.requested[KE_RES_CPU] + n->rv_req[KE_RES_CPU];
+      req[1] = n->node.requested[KE_RES_MEMORY] + n->rv_req[KE_RES_MEMORY];
+      alloc[0] = n->node.allocatable[KE_RES_CPU];
+      alloc[1] = n->node.allocatable[KE_RES_MEMORY];
+    }
+    int64_t podreq[KE_NRES] = {pod->requests[KE_RES_CPU], pod->requests[KE_RES_MEMORY]};
+    if (cs.rcb) { /* the node's allocated CPUs with preferredCPUs minus the pod's own released (scoring.go:180-185) */
+      int64_t k = 0;
+      for (int c1 = 0; n->cpus && c1 < ACC_MAX_CPUS; c1++) {
+        int ref = n->cpus->al.present[c1] ? n->cpus->al.ref[c1] : 0;
+        if (ref > 0 && used.has_pref && (used.pref[c1 >> 6] >> (c1 & 63) & 1) && !(pcpus[c1 >> 6] >> (c1 & 63) & 1)) ref--;
+        k += ref > 0;
+      }
+      req[0] = amplify(n->cpus ? k * 1000 : cpus_allocated_count(n) * 1000, v.ratio);
+      if (v.ratio > 1.0) podreq[KE_RES_CPU] = amplify(podreq[KE_RES_CPU], v.ratio);
+    }
+    return numa_resource_score(&c->cfg.numa, req, alloc, podreq);
+  }
   if (policy != KE_NUMA_POLICY_NONE) {
     /* the affinity the Filter's Admit stored, the allocation on it, calculateAllocatableAndRequested */
     uint32_t aff = 0;
@@ -4046,6 +4344,26 @@ static int or_reserve_plan(const or_cluster* c, const ke_pod* pod, int32_t node,
       if (fr > 0) return 0;
     }
   }
+  if (c->resv_m && !c->ignored && policy > KE_NUMA_POLICY_NONE && n->n_zone > 0) {
+    /* a matched pod on a node of its reservations holding NUMA resources / CPUs (plugin.go:552-566):
+     * allocateWithNominatedReservation, else tryAllocateFromNode, on the stored affinity */
+    int32_t M[64];
+    const int nM = numa_rsv_matched(c, node, M);
+    if (nM > 0) {
+      uint32_t aff = 0;
+      int reason;
+      if (numa_admit(c, n, pod, policy, exclusive, &aff, &reason, &cs) != KE_CODE_SUCCESS) return -1;
+      numa_opt used;
+      int64_t d16[2 * KE_MAX_NUMA];
+      uint64_t pc[ACC_WORDS];
+      if (!numa_matched_alloc(c, pod, node, M, nM, nom_r, aff, &used, d16, pc)) return -1;
+      for (int z = 0; z < n->n_zone; z++)
+        for (int r = 0; r < KE_NRES; r++)
+          rp->dist[z][r] = n->zone[z].id >= 0 && n->zone[z].id < KE_MAX_NUMA ? d16[2 * n->zone[z].id + r] : 0;
+      if (cs.rcb) memcpy(rp->cpus, pc, sizeof pc);
+      return 0;
+    }
+  }
   numa_view v;
   int have = 0;
   if (policy > KE_NUMA_POLICY_NONE && n->n_zone > 0) {
@@ -4645,7 +4963,7 @@ static int or_numa_nominable(const or_cluster* c, const ke_pod* pod, int32_t nod
   if (rcb < 0) return 0;
   if (!rcb && policy <= KE_NUMA_POLICY_NONE) return 1;
   if (rcb && !cpus_valid(n)) return 0;
-  if (policy != KE_NUMA_POLICY_NONE) return 1; /* (a holding reservation here is refused: or_resv_supported) */
+  if (policy != KE_NUMA_POLICY_NONE) return !c->numa_rok || c->numa_rok[r] != 0; /* (or_resv_eval's precomputation) */
   uint64_t got[ACC_WORDS];
   return or_numa_from_rsv(c, pod, node, r, affinity, got) >= 0;
 }
@@ -4664,6 +4982,34 @@ int or_numa_reserve_from_rsv(or_cluster* c, const ke_pod* pod, int32_t node, con
   c->resv_m = NULL;
   free(m);
   return r;
+}
+
+/* golden entry point: NodeNUMAResource Reserve under a NUMA policy for a pod matching reservations ids[] on `node`
+ * with the stored affinity `aff` (0 = nil) and the nominated reservation `nom` (allocateWithNominatedReservation ->
+ * tryAllocateFromReservation, then tryAllocateFromNode; plugin.go:552-566): 1 = from the reservation, 0 = from the
+ * node, -1 = Unschedulable; dist16[2*id + r] the NUMA allocation, cpus the cpuset. */
+int or_numa_reserve_policy(or_cluster* c, const ke_pod* pod, int32_t node, const int32_t* ids, int32_t n_ids,
+                           int32_t nom, int32_t required, uint32_t aff, int64_t* dist16, uint64_t* cpus) {
+  char* m = (char*)calloc((size_t)(c->n_resv > 0 ? c->n_resv : 1), 1);
+  for (int32_t j = 0; j < n_ids; j++)
+    if (or_resv_usable(&c->resv[ids[j]])) m[ids[j]] = 1;
+  c->resv_m = m;
+  int32_t M[64];
+  const int nM = numa_rsv_matched(c, node, M);
+  int in = 0;
+  for (int q = 0; q < nM; q++) in |= M[q] == nom;
+  int rc = in ? numa_from_rsv_try(c, pod, node, M, nM, &nom, 1, aff, required, NULL, dist16, cpus) : 0;
+  if (rc == 0) rc = numa_alloc_try(c, &c->nodes[node], pod, aff, NULL, dist16, cpus) ? 0 : -1;
+  c->resv_m = NULL;
+  free(m);
+  return rc;
+}
+
+/* golden entry point: NodeNUMAResource Reserve of a reservation-ignored pod on a node without a NUMA policy
+ * (tryAllocateIgnoreReservation, reservation.go:437-490): 1 and the cpuset, 0 (no holding reservation: the node), -1 */
+int or_numa_reserve_ignored(or_cluster* c, const ke_pod* pod, int32_t node, uint64_t* cpus) {
+  memset(cpus, 0, sizeof(uint64_t) * ACC_WORDS);
+  return or_numa_ignored(c, pod, node, cpus);
 }
 
 /* allRAllocated of node i: Σ allocated of its matched reservations, [cpu, memory, then KE_NRES + resource id] */
@@ -4863,6 +5209,29 @@ static int32_t or_resv_eval(or_cluster* c, const ke_pod* pod, int64_t now, eval_
   char* m = or_resv_begin(c, ids, n_ids, &pr);
   int16_t bs16;
   (void)eval_pod(c, pod, now, o, &bs16);
+  /* NodeNUMAResource's FilterNominateReservation under a NUMA policy (plugin.go:448-504) for a pod with a reservation
+   * affinity, in the cycle's restore state: tryAllocateFromReservation over the reservation alone on the stored
+   * affinity; a reservation outside RestoreReservation's matched set passes */
+  int8_t* rok = NULL;
+  if (affinity) {
+    rok = (int8_t*)malloc((size_t)(c->n_resv > 0 ? c->n_resv : 1));
+    memset(rok, 1, (size_t)(c->n_resv > 0 ? c->n_resv : 1));
+    for (int32_t r = 0; r < c->n_resv; r++) {
+      if (!m[r]) continue;
+      const int32_t i = c->resv[r].node;
+      int ex;
+      const int pol = effective_policy(&c->nodes[i], pod, &ex);
+      if (pol <= KE_NUMA_POLICY_NONE || pod_requests_zero(pod) || o[i].status != KE_CODE_SUCCESS) continue;
+      int32_t M[64];
+      const int nM = numa_rsv_matched(c, i, M);
+      int in = 0;
+      for (int q = 0; q < nM; q++) in |= M[q] == r;
+      if (!in) continue;
+      uint32_t aff = 0;
+      if (!numa_stored_affinity(c, pod, i, &aff)) aff = 0;
+      rok[r] = (int8_t)(numa_from_rsv_try(c, pod, i, M, nM, &r, 1, aff, 1, NULL, NULL, NULL) == 1);
+    }
+  }
   or_restore(c, NULL, 0);
   uint8_t* feasible = (uint8_t*)malloc((size_t)(N > 0 ? N : 1));
   for (int32_t i = 0; i < N; i++) feasible[i] = o[i].status == KE_CODE_SUCCESS;
@@ -4875,7 +5244,26 @@ static int32_t or_resv_eval(or_cluster* c, const ke_pod* pod, int64_t now, eval_
     free(has);
   }
   int64_t* raw = (int64_t*)malloc(sizeof(int64_t) * (size_t)(N > 0 ? N : 1));
+  c->numa_rok = rok;
   (void)or_resv_prescore(c, pod, m, pr, feasible, affinity, raw, nom);
+  c->numa_rok = NULL;
+  free(rok);
+  /* NodeNUMAResource's Score of a node with reservations in RestoreReservation's matched set under a NUMA policy reads
+   * the nominated reservation (scoring.go:101-119); an error status there fails the pod's cycle (RunScorePlugins) */
+  int score_err = 0;
+  or_restore(c, m, 1);
+  c->numa_nom = nom;
+  for (int32_t i = 0; i < N && !score_err; i++) {
+    if (!feasible[i]) continue;
+    int ex;
+    int32_t M[64];
+    if (effective_policy(&c->nodes[i], pod, &ex) <= KE_NUMA_POLICY_NONE || numa_rsv_matched(c, i, M) == 0) continue;
+    int err = 0;
+    o[i].numa = (int16_t)numa_score_ex(c, pod, i, &err);
+    score_err |= err;
+  }
+  c->numa_nom = NULL;
+  or_restore(c, NULL, 0);
   /* DeviceShare's Score reads the nominated reservation (scoring.go:83-102), and NormalizeScore runs over the nodes
    * that passed every Filter, the Reservation Filter of a reservation affinity included */
   ds_pod dsp;
@@ -4903,6 +5291,7 @@ static int32_t or_resv_eval(or_cluster* c, const ke_pod* pod, int64_t now, eval_
       b = i;
     }
   }
+  if (score_err) b = -1, bt = -1;
   *best = b >= 0 ? (int32_t)bt : -1;
   c->resv_m = NULL;
   free(m);
@@ -4955,7 +5344,6 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
     cpuset_prefilter(c, &pods[p], &st);
     ds_pod d;
     ds_prepare_pod(c, &pods[p], &d);
-    (void)node_bind;
     /* every requested name beyond cpu / memory is read through its ke_pod.xres entry: a name without an id is
      * refused (batch / mid resources included); a DeviceShare pod allocates from its matched reservations' devices
      * (deviceshare/reservation.go:207-449) -- not with device hints / joint allocation, nor in NUMA hints (a pod
@@ -4969,19 +5357,30 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
             c->nodes[c->resv[r].node].node.numa_topology_policy != KE_NUMA_POLICY_NONE)
           return KE_ERR_UNSUPPORTED;
       }
-    /* a pod with its own NUMA policy matching a reservation that holds NUMA resources / CPUs: its hints over the
-     * allocate-from-reservation trials are not restated */
-    for (int32_t j = c->moff[p]; pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE && j < c->moff[p + 1]; j++)
-      if (or_resv_usable(&c->resv[c->mids[j]]) && c->ralloc &&
-          (or_holds_of(&c->ralloc[c->mids[j]]) & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)))
-        return KE_ERR_UNSUPPORTED;
-    /* a matched reservation holding a NUMA allocation or a cpuset on a NUMA-policy node: its allocate-from-
-     * reservation path (tryAllocateFromReservation in the hints) is not restated */
-    for (int32_t j = c->moff[p]; j < c->moff[p + 1]; j++)
-      if (or_resv_usable(&c->resv[c->mids[j]]) && c->ralloc &&
-          (or_holds_of(&c->ralloc[c->mids[j]]) & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)) &&
-          c->nodes[c->resv[c->mids[j]].node].node.numa_topology_policy != KE_NUMA_POLICY_NONE)
-        return KE_ERR_UNSUPPORTED;
+    /* under a NUMA policy (the pod's or the node's) a matched reservation holding NUMA resources / CPUs enters the
+     * hints through its allocate-from-reservation trials (numa_admit) for a pod binding no CPUs without device
+     * requests; a binding pod's hints over the held CPUs and a DeviceShare pod's joint hints there are not restated,
+     * nor more than 8 such reservations of the pod on one node (the product's NV_MAX) */
+    if (c->ralloc) {
+      const int binds = st.rcb || st.invalid || (node_bind && pods[p].requests[KE_RES_CPU] > 0);
+      const int dev = !d.skip || d.h;
+      for (int32_t j = c->moff[p]; j < c->moff[p + 1]; j++) {
+        const int32_t r = c->mids[j];
+        if (!or_resv_usable(&c->resv[r]) || !(or_holds_of(&c->ralloc[r]) & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)))
+          continue;
+        const int32_t node = c->resv[r].node;
+        if ((pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE ||
+             c->nodes[node].node.numa_topology_policy != KE_NUMA_POLICY_NONE) && (binds || dev))
+          return KE_ERR_UNSUPPORTED;
+        int same = 0;
+        for (int32_t j2 = c->moff[p]; j2 < c->moff[p + 1]; j2++) {
+          const int32_t r2 = c->mids[j2];
+          same += or_resv_usable(&c->resv[r2]) && c->resv[r2].node == node &&
+                  (or_holds_of(&c->ralloc[r2]) & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET));
+        }
+        if (same > 8) return KE_ERR_UNSUPPORTED;
+      }
+    }
   }
   return KE_OK;
 }
@@ -5047,7 +5446,6 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
     reserve_plan rp;
     memset(&rp, 0, sizeof rp);
     ds_aff da = NO_AFF; /* the affinity the Filter stored, for DeviceShare's Reserve */
-    if (b >= 0) da = ds_reserve_affinity(c, &pods[p], b);
     char* mflags = NULL; /* the matched flags again for NodeNUMAResource's Reserve */
     if (b >= 0 && (n_ids > 0 || affinity)) {
       mflags = (char*)calloc((size_t)(c->n_resv > 0 ? c->n_resv : 1), 1);
@@ -5055,7 +5453,10 @@ int or_schedule(or_cluster* c, int32_t n_pods, const ke_pod* pods, int64_t now, 
         if (or_resv_usable(&c->resv[c->mids[j]])) mflags[c->mids[j]] = 1;
       c->resv_m = mflags;
     }
+    if (mflags) or_restore(c, mflags, 1); /* the cycle's restore state through Reserve (as the Filter saw it) */
+    if (b >= 0) da = ds_reserve_affinity(c, &pods[p], b);
     const int plan = b >= 0 ? or_reserve_plan(c, &pods[p], b, &rp, mflags ? nom[b] : -1) : 0;
+    if (mflags) or_restore(c, NULL, 0);
     c->ds_nom = mflags ? nom : NULL; /* DeviceShare Reserve: the nominated reservation (with resv_m / ignored) */
     if (b >= 0 && (plan != 0 || !ds_reserve_feasible(c, &pods[p], b, da))) {
       /* Reserve failed (Unreserve undoes the others): not placed */

@@ -72,6 +72,9 @@ int32_t or_ds_rsv_direct(or_cluster* c, const ke_pod* pod, int32_t node, int32_t
                          int64_t* score, int32_t* reason);
 int or_numa_reserve_from_rsv(or_cluster* c, const ke_pod* pod, int32_t node, const int32_t* ids, int32_t n_ids,
                              int32_t nom, int32_t required, uint64_t* cpus);
+int or_numa_reserve_policy(or_cluster* c, const ke_pod* pod, int32_t node, const int32_t* ids, int32_t n_ids,
+                           int32_t nom, int32_t required, uint32_t aff, int64_t* dist16, uint64_t* cpus);
+int or_numa_reserve_ignored(or_cluster* c, const ke_pod* pod, int32_t node, uint64_t* cpus);
 int or_reservations_get(const or_cluster* c, int32_t n, ke_reservation* out);
 int or_pod_reservations(or_cluster* c, int32_t n_pods, const int32_t* offsets, const int32_t* ids);
 int or_last_reservations(const or_cluster* c, int32_t n, int32_t* out);

@@ -24,6 +24,9 @@ int device_rsv_views(Context*, const ke_pod&, int64_t, const std::vector<RsvView
 int device_ds_views(Context*, const ke_pod&, int64_t, const std::vector<DsView>&, std::vector<DsViewOut>&) {
   return none();
 }
+int device_numa_views(Context*, const ke_pod&, int64_t, const std::vector<NumaRsvView>&, std::vector<NumaRsvOut>&) {
+  return none();
+}
 int device_quota_sync(Context*) { return KE_OK; }
 int device_debug_rows(Context*, int32_t, Row*) { return none(); }
 int device_set_profiling(Context*, int32_t) { return none(); }

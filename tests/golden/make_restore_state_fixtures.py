@@ -18,6 +18,8 @@ Go tests cannot run here; each case restates one test's objects and expectations
     remainedCPUs), a 4-CPU pod preferring FullPCPUs, the reservation nominated (:1480):
     Default, remained 4-10 -> 4-7; Restricted, remained 4-10 -> 4-7; Restricted, remained 4-5, with a reservation
     affinity -> Unschedulable "Reservation(s) not enough cpus available to satisfy request".
+  * the same test's cases under a pod NUMA policy with a stored affinity (:1268-1398) and its reservation-ignored
+    cpuset case (:1399-1433) -- policy_cases / ignored_cases below.
 Encoding: cpusets as CPU id lists; device amounts as [gpu-core, gpu-memory, gpu-memory-ratio] of GPU minors;
 reserve cases: policy 0 Default / 2 Restricted, want_code 1 (from the reservation) / -1 (Unschedulable).
 
@@ -57,7 +59,35 @@ reserve_cases = [
      "remained": [4, 5], "policy": 2, "affinity": True, "num_cpus": 4, "want_code": -1, "want_cpus": []},
 ]
 
+# TestPlugin_Reserve's allocate-from-reservation cases under the pod's NUMA policy (Restricted) with a stored affinity
+# (:1268-1398) and its reservation-ignored case (:1399-1433).  Node: NUMANodeResources cpu = CPUsPerNode per socket
+# (no memory key, :1466-1471); the reservation's reserve pod holds remainedCPUs and its `allocatable` NUMA amounts
+# (addCPUs + addPodAllocation, :1476-1494).  The hand-built restore state of the test carries no merged lists; the
+# holdings model restates it with the owners holding allocatable - remained (none where the test gives no remained) --
+# the amounts Reserve reads are the same.  Encoding: numa maps {id: cpu milli}; bind = requestCPUBind (a 4-CPU LSR
+# pod preferring FullPCPUs) else a LS pod; affinity_mask = the stored NUMANodeAffinity; required = the reservation
+# affinity; want_code 1 / 0 (from the node) / -1 (Unschedulable); want_numa {id: cpu milli}.
+policy_cases = [
+    {"name": "numa_cpuset_restricted", "source": f"{SRC}:1268-1297", "topology": [2, 1, 8, 2], "bind": True,
+     "remained_cpus": [4, 5, 6, 7, 8, 9, 10], "allocatable": {"0": 7000}, "remained": None, "policy": 2,
+     "required": True, "affinity_mask": 1, "want_code": 1, "want_cpus": [4, 5, 6, 7], "want_numa": {"0": 4000}},
+    {"name": "numa_cpuset_restricted_fails", "source": f"{SRC}:1299-1330", "topology": [2, 1, 4, 2], "bind": True,
+     "remained_cpus": [4, 5], "allocatable": {"0": 2000}, "remained": {"0": 2000}, "policy": 2,
+     "required": True, "affinity_mask": 1, "want_code": -1, "want_cpus": [], "want_numa": {}},
+    {"name": "numa_restricted", "source": f"{SRC}:1331-1364", "topology": [2, 1, 4, 2], "bind": False,
+     "remained_cpus": [], "allocatable": {"1": 7000}, "remained": {"1": 7000}, "policy": 2,
+     "required": True, "affinity_mask": 2, "want_code": 1, "want_cpus": [], "want_numa": {"1": 4000}},
+    {"name": "numa_restricted_fails", "source": f"{SRC}:1366-1397", "topology": [2, 1, 4, 2], "bind": False,
+     "remained_cpus": [], "allocatable": {"0": 2000}, "remained": {"0": 2000}, "policy": 2,
+     "required": True, "affinity_mask": 1, "want_code": -1, "want_cpus": [], "want_numa": {}},
+]
+ignored_cases = [
+    {"name": "ignored_pod_cpuset", "source": f"{SRC}:1399-1433", "topology": [2, 1, 4, 2],
+     "remained_cpus": [4, 5, 6, 7, 8, 9, 10], "num_cpus": 4, "want_code": 1, "want_cpus": [4, 5, 6, 7]},
+]
+
 if __name__ == "__main__":
     with open(os.path.join(HERE, "reservation_restore.json"), "w") as f:
-        json.dump({"cases": cases, "reserve_cases": reserve_cases}, f, indent=1)
+        json.dump({"cases": cases, "reserve_cases": reserve_cases, "policy_cases": policy_cases,
+                   "ignored_cases": ignored_cases}, f, indent=1)
     print(f"wrote {len(cases)} cases")

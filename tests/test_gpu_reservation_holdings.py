@@ -252,3 +252,92 @@ def test_ignored_numa_pods_beside_held_numa(gpu, seed):
     on_held = [p for p in ign if c[p] >= 0 and held[c[p]] and pol[c[p]] and ev.last_numa_allocations[p].any()]
     assert len(on_held) >= 3  # ignored pods given NUMA allocations on policy nodes with held zones
     assert ev.check_records(synth.T0) == 0
+
+
+def numa_matched_setup(n, seed, n_pods, affinity):
+    """Nodes of every NUMA policy without a CPU bind policy, reservations whose reserve pods hold NUMA amounts and
+    cpusets (owners holding part of them, every allocate policy), a queue where half of the pods binding no CPUs --
+    40 % of the queue carrying a NUMA policy of its own -- match the reservations of one of 8 owner groups
+    (KE_RSV_MATCHED, or KE_RSV_AFFINITY for `affinity` of them), between cpuset pods."""
+    rng = np.random.default_rng(seed)
+    cl = synth.make_cluster(n, synth.BASE_SEED + seed, amplified_fraction=0.2)
+    zones, tabs = synth.make_numa_cpus(cl, synth.BASE_SEED + seed + 1)
+    cl.nodes["cpu_bind_policy"] = 0
+    rs, al, res = synth.make_reservation_holdings(cl, synth.BASE_SEED + seed + 2, zones, tabs, None, frac=0.5)
+    cfg = synth.config(n)
+    ev, o = Evaluator(cfg), Oracle(cfg, n)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        synth.load_numa(h, zones)
+        synth.load_cpus(h, tabs)
+        h.reservations_load(rs, al, res)
+    pods = synth.make_numa_cpuset_pods(n_pods, synth.BASE_SEED + seed + 3, cpuset_fraction=0.3, policy_fraction=0.4)
+    cs = np.isin(pods["qos_class"], [abi.QOS_LSE, abi.QOS_LSR]) & (pods["priority_class"] == abi.PRIORITY_PROD)
+    grp = rng.integers(0, 8, len(rs))
+    matches = [[] for _ in range(n_pods)]
+    ok = ~cs & (pods["requests"][:, 2:] == 0).all(1) & (pods["has_other_requests"] == 0) \
+        & (pods["device_requests"] == 0).all(1)
+    for p in np.flatnonzero(ok & (rng.random(n_pods) < 0.5)):
+        pods["reservation_matched"][p] = abi.RSV_AFFINITY if rng.random() < affinity else abi.RSV_MATCHED
+        matches[p] = np.flatnonzero(grp == rng.integers(0, 8)).tolist()
+    return cl, ev, o, pods, matches, rs
+
+
+@pytest.mark.parametrize("seed,affinity", [(1401, 0.0), (1402, 0.5)], ids=["matched", "affinity"])
+def test_matched_numa_policy_from_reservations_parity(gpu, seed, affinity):
+    """Reservation-matched pods binding no CPUs under NUMA policies (the node's, or their own) on nodes of their
+    reservations holding NUMA amounts / cpusets: NodeNUMAResource's hints over the allocate-from-reservation trials
+    (k_numa_views: tryAllocateFromReservation per mask, then tryAllocateFromNode; nodenumaresource/resource_manager.go
+    :586-594, reservation.go:270-424), FilterNominateReservation under an affinity, the Score and Reserve from the
+    nominated reservation's allocation on the affinity (Restricted: over its remained) -- placements, scores, NUMA
+    allocations, cpusets and the reservation state bit-exact with the oracle; then Unreserve of part of them and a
+    second queue."""
+    cl, ev, o, pods, matches, rs = numa_matched_setup(400, seed, 300, affinity)
+    c1, s1 = ev.schedule(pods, synth.T0, matches=matches)
+    c0, s0 = o.schedule(pods, synth.T0, matches=matches)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5].ravel().tolist()
+    assert np.array_equal(s1, s0)
+    diff = np.argwhere(np.any(ev.last_numa_allocations != o.last_numa_allocations, axis=1))
+    assert len(diff) == 0, diff[:5].ravel().tolist()
+    assert np.array_equal(ev.last_cpusets, o.last_cpusets)
+    _holdings_equal(ev, o)
+    a1, a0 = ev.last_allocations(), o.last_allocations()
+    assert np.array_equal(a1["reservation"], a0["reservation"])
+    pol = cl.nodes["numa_topology_policy"] != 0
+    m = np.flatnonzero(pods["reservation_matched"] != 0)
+    numa_into = [p for p in m if a1["reservation"][p] > 0 and c1[p] >= 0 and pol[c1[p]] and
+                 ev.last_numa_allocations[p].any()]
+    assert len(numa_into) >= 10  # NUMA allocations taken out of holding reservations on policy nodes
+    assert sum(pods["numa_topology_policy"][p] != 0 for p in numa_into) >= 3  # pods with their own policy
+    assert ev.check_records(synth.T0) == 0
+    for p in np.flatnonzero(a1["reservation"] > 0)[::3]:
+        ev.unreserve(pods[p], int(p))
+        o.release(pods[p], a0[p], abi.RELEASE_UNRESERVE)
+    _holdings_equal(ev, o)
+    more = synth.make_numa_cpuset_pods(200, synth.BASE_SEED + seed + 7, cpuset_fraction=0.0, policy_fraction=0.4,
+                                       key_base=7_800_000_000)
+    m2 = [matches[p % len(matches)] for p in range(len(more))]
+    more["reservation_matched"] = [pods["reservation_matched"][p % len(matches)] for p in range(len(more))]
+    keep = np.array([len(x) > 0 for x in m2])
+    more["requests"][:, 2:] = np.where(keep[:, None], 0, more["requests"][:, 2:])
+    more["has_other_requests"] = np.where(keep, 0, more["has_other_requests"])
+    more["device_requests"] = np.where(keep[:, None], 0, more["device_requests"])
+    c1, s1 = ev.schedule(more, synth.T0, matches=m2)
+    c0, s0 = o.schedule(more, synth.T0, matches=m2)
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
+    assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
+    _holdings_equal(ev, o)
+    assert ev.check_records(synth.T0) == 0
+
+
+def test_matched_numa_policy_sharded_loopback(gpu):
+    """The same pods in a node-sharded context (loopback, 3 shards): the NUMA views, the staged Reservation pick
+    (a Score error on any rank's feasible node fails the pod) -- bit-exact with the oracle."""
+    cl, ev, o, pods, matches, rs = numa_matched_setup(300, 1403, 200, 0.3)
+    ev.shard_init(0, 3, None)
+    c1, s1 = ev.schedule(pods, synth.T0, matches=matches)
+    c0, s0 = o.schedule(pods, synth.T0, matches=matches)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5].ravel().tolist()
+    assert np.array_equal(s1, s0)
+    assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
+    _holdings_equal(ev, o)

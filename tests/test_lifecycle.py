@@ -152,9 +152,10 @@ def test_reservation_holds_refused(bit):
 
 
 def test_matched_refusals_precede_every_segment():
-    """the refusal of a matched reservation holding NUMA resources on a NUMA-policy node is an
-    argument check, so a queue with plain pods ahead of the matched one fails before the device (here absent:
-    NO_DEVICE would come later).  A reservation holding nothing there is not refused."""
+    """the refusal of a binding pod matching a reservation holding NUMA resources on a NUMA-policy
+    node is an argument check, so a queue with plain pods ahead of the matched one fails before the device (here
+    absent: NO_DEVICE would come later).  A reservation holding nothing there is not refused, nor the same pod
+    binding no CPUs (k_numa_views)."""
     cl = synth.make_cluster(8, synth.BASE_SEED + 1205)
     ev = Evaluator(synth.config(8))
     synth.load_into(ev, cl)
@@ -172,6 +173,8 @@ def test_matched_refusals_precede_every_segment():
     pods["numa_topology_policy"] = 0
     pods["qos_class"] = abi.QOS_LS
     pods["reservation_matched"][4] = abi.RSV_MATCHED
+    pods["qos_class"][4], pods["priority_class"][4] = abi.QOS_LSR, abi.PRIORITY_PROD  # binds CPUs
+    pods["requests"][4, abi.RES_CPU] = pods["limits"][4, abi.RES_CPU] = 2000
     with pytest.raises(KoordEvalError) as e:
         ev.schedule(pods, synth.T0, matches=[[], [], [], [], [0, 1], []])
     assert e.value.code == abi.ERR_UNSUPPORTED
@@ -183,6 +186,11 @@ def test_matched_refusals_precede_every_segment():
         assert e.value.code == abi.ERR_NO_DEVICE
         with pytest.raises(KoordEvalError) as e:  # without the NUMA-policy node: past the checks, no device here
             ev.schedule(pods, synth.T0, matches=[[], [], [], [], [1], []])
+        assert e.value.code == abi.ERR_NO_DEVICE
+        ls = pods.copy()
+        ls["qos_class"][4] = abi.QOS_LS  # binding no CPUs: past the checks
+        with pytest.raises(KoordEvalError) as e:
+            ev.schedule(ls, synth.T0, matches=[[], [], [], [], [0, 1], []])
         assert e.value.code == abi.ERR_NO_DEVICE
         rs[0].holds = 0  # the same reservations holding nothing: past the checks
         ev.reservations_load(rs)

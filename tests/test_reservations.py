@@ -387,6 +387,109 @@ def test_numa_reserve_from_reservation_golden(case):
     assert np.array_equal(cpus, _cpus(case["want_cpus"]))
 
 
+def _reserve_node(case, seed):
+    """One node as TestPlugin_Reserve builds it (plugin_test.go:1436-1494): allocatable 96 cpu / 512Gi, a CPU table of
+    buildCPUTopologyForTest(sockets, nodes/socket, cores/node, threads/core) with the reservation's remainedCPUs under
+    its UID (MaxRefCount 1), NUMA zones of CPUsPerNode cpu each (no memory key) holding the reserve pod's NUMA amounts."""
+    from koordinator_amd import model
+    sockets, nodes_per, cores_per, tpc = case["topology"]
+    n_cpu = sockets * nodes_per * cores_per * tpc
+    cl = synth.make_cluster(1, synth.BASE_SEED + seed)
+    cl.nodes["allocatable"][0] = [96_000, 512 * 2**30]
+    cl.nodes["raw_allocatable"][0] = abi.ABSENT
+    cl.nodes["requested"][0] = 0
+    cl.nodes["cpu_bind_policy"][0] = 0
+    cl.nodes["numa_topology_policy"][0] = 0
+    cl.nodes["cpu_amplification_ratio"][0] = 0
+    o = Oracle(synth.config(1), 1)
+    synth.load_into(o, cl)
+    t = np.zeros(n_cpu, abi.CPU_DTYPE)
+    t["cpu_id"] = np.arange(n_cpu)
+    t["core_id"] = np.arange(n_cpu) // tpc
+    t["numa_id"] = np.arange(n_cpu) // (cores_per * tpc)
+    t["socket_id"] = np.arange(n_cpu) // (nodes_per * cores_per * tpc)
+    t["ref_count"][case["remained_cpus"]] = 1
+    alloc = {int(k): v for k, v in (case.get("allocatable") or {}).items()}
+    per = n_cpu // (sockets * nodes_per)
+    zones = model.make_zones([{"id": z, "cpu": str(per), **({"allocated": {"cpu": f"{alloc[z]}m"}} if z in alloc else {})}
+                              for z in range(sockets * nodes_per)])
+    o.set_numa(0, zones)
+    o.set_cpus(0, t, 1)
+    return o
+
+
+POLICY = json.load(open(os.path.join(HERE, "golden", "reservation_restore.json")))["policy_cases"]
+
+
+@pytest.mark.parametrize("case", POLICY, ids=[c["name"] for c in POLICY])
+def test_numa_reserve_from_reservation_policy_golden(case):
+    """NodeNUMAResource Reserve under the pod's NUMA policy with a stored affinity (allocateWithNominatedReservation ->
+    tryAllocateFromReservation: the Restricted second Allocate over requiredResources = remained) in the oracle against
+    TestPlugin_Reserve's cases (plugin_test.go:1268-1398): code, cpuset and NUMA allocation."""
+    o = _reserve_node(case, 1391)
+    r = np.zeros(1, abi.RESERVATION_DTYPE)
+    a = np.zeros(1, abi.RESERVATION_ALLOC_DTYPE)
+    r["available"], r["allocate_policy"] = 1, case["policy"]
+    r["allocatable"][0] = [max(1, len(case["remained_cpus"])) * 1000, 2**30]
+    holds = 0
+    if case["remained_cpus"]:
+        a["cpuset"][0] = _cpus(case["remained_cpus"])
+        holds |= abi.RSV_HOLDS_CPUSET
+    for k, v in case["allocatable"].items():
+        a["numa"][0, 2 * int(k)] = v
+        holds |= abi.RSV_HOLDS_NUMA
+        if case["remained"] is not None:
+            a["owner_numa"][0, 2 * int(k)] = v - case["remained"].get(k, 0)
+    r["holds"] = holds
+    o.reservations_load(r, a)
+    pod = synth.make_pods(1, synth.BASE_SEED + 1392)[0].copy()
+    pod["requests"][:] = 0
+    pod["limits"][:] = 0
+    pod["requests"][abi.RES_CPU] = pod["limits"][abi.RES_CPU] = 4000
+    if case["bind"]:
+        pod["priority_class"], pod["qos_class"] = abi.PRIORITY_PROD, abi.QOS_LSR
+        pod["cpu_bind_required"], pod["cpu_bind_preferred"] = abi.CPU_BIND_UNSET, abi.CPU_BIND_FULL_PCPUS
+    else:
+        pod["priority_class"], pod["qos_class"] = abi.PRIORITY_PROD, abi.QOS_LS
+    pod["has_other_requests"], pod["device_requests"] = 0, 0
+    pod["numa_topology_policy"] = abi.NUMA_POLICY_RESTRICTED
+    code, dist, cpus = o.numa_reserve_policy(pod, 0, [0], 0, case["required"], case["affinity_mask"])
+    assert code == case["want_code"]
+    if code >= 0:
+        assert np.array_equal(cpus, _cpus(case["want_cpus"]))
+        want = np.zeros(16, np.int64)
+        for k, v in case["want_numa"].items():
+            want[2 * int(k)] = v
+        assert np.array_equal(dist, want), dist.tolist()
+
+
+IGNORED = json.load(open(os.path.join(HERE, "golden", "reservation_restore.json")))["ignored_cases"]
+
+
+@pytest.mark.parametrize("case", IGNORED, ids=[c["name"] for c in IGNORED])
+def test_numa_reserve_ignored_golden(case):
+    """A reservation-ignored binding pod's Reserve (tryAllocateIgnoreReservation: every held CPU preferred) in the
+    oracle against TestPlugin_Reserve's "succeed allocate for a reservation-ignored pod" (plugin_test.go:1399-1433)."""
+    o = _reserve_node(case, 1393)
+    r = np.zeros(1, abi.RESERVATION_DTYPE)
+    a = np.zeros(1, abi.RESERVATION_ALLOC_DTYPE)
+    r["available"], r["holds"] = 1, abi.RSV_HOLDS_CPUSET
+    r["allocatable"][0] = [len(case["remained_cpus"]) * 1000, 2**30]
+    a["cpuset"][0] = _cpus(case["remained_cpus"])
+    o.reservations_load(r, a)
+    pod = synth.make_pods(1, synth.BASE_SEED + 1394)[0].copy()
+    pod["requests"][:] = 0
+    pod["limits"][:] = 0
+    pod["requests"][abi.RES_CPU] = pod["limits"][abi.RES_CPU] = case["num_cpus"] * 1000
+    pod["priority_class"], pod["qos_class"] = abi.PRIORITY_PROD, abi.QOS_LSR
+    pod["cpu_bind_required"], pod["cpu_bind_preferred"] = abi.CPU_BIND_UNSET, abi.CPU_BIND_FULL_PCPUS
+    pod["has_other_requests"], pod["device_requests"], pod["numa_topology_policy"] = 0, 0, 0
+    pod["reservation_matched"] = abi.RSV_IGNORED
+    code, cpus = o.numa_reserve_ignored(pod, 0)
+    assert code == case["want_code"]
+    assert np.array_equal(cpus, _cpus(case["want_cpus"]))
+
+
 def test_fits_node_checks_the_pods_other_resources():
     """fitsNode (reservation/plugin.go:447-497) checks every resource the pod requests, its scalars and ephemeral
     storage included (a reservation holds none of them: the node's free amount decides), and with no request at all
