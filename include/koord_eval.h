@@ -1221,7 +1221,7 @@ int ke_debug_ds_cuts(ke_ctx* ctx, int32_t* cuts);
  * Reserve, next pod's changed flags — and the pod count (cyc8[7]); zeros in the product build. */
 int ke_debug_replay_phases(ke_ctx* ctx, double* cyc8);
 /* The same per phase of another kernel of the diagnostic build: kernel 0 k_resolve (per pod), 1 k_numa_fallback
- * (per deferred pair), 2 k_cpuset_reserve (per pod); each read clears that kernel's counters. */
+ * (per deferred pair), 2 k_cpuset_reserve (per pod), 3 k_select (per wave); each read clears that kernel's counters. */
 int ke_debug_kernel_phases(ke_ctx* ctx, int32_t kernel, double* cyc8);
 /* Speculative replay of plain batches: rounds per batch of the last ke_schedule that ended at a
  * failed prediction (0 = every pod of the batch took its best candidate not taken before). */

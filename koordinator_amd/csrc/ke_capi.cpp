@@ -1346,7 +1346,7 @@ int ke_debug_replay_phases(ke_ctx* ctx, double* cyc8) {
 
 int ke_debug_kernel_phases(ke_ctx* ctx, int32_t kernel, double* cyc8) {
   if (ctx) async_drain(ctx);
-  if (!ctx || !cyc8 || kernel < 0 || kernel > 2) return fail(KE_ERR_INVALID, "ke_debug_kernel_phases arguments");
+  if (!ctx || !cyc8 || kernel < 0 || kernel > 3) return fail(KE_ERR_INVALID, "ke_debug_kernel_phases arguments");
   int rc = require_device(ctx);
   if (rc) return rc;
   return device_replay_phases(&ctx->c, kernel, cyc8);

@@ -432,7 +432,7 @@ __constant__ uint8_t NUMA_OFF[10] = {0, 0, 8, 36, 92, 162, 218, 246, 254, 255}; 
 // the per-pod replay loop, summed over every pod into g_rprof (ke_debug_replay_phases).  Off in the
 // product build (the macro expands to nothing).
 #ifdef KE_PROF_REPLAY
-__device__ unsigned long long g_rprof[3][8];  // per kernel: k_resolve, k_numa_fallback, k_cpuset_reserve
+__device__ unsigned long long g_rprof[4][8];  // per kernel: k_resolve, k_numa_fallback, k_cpuset_reserve, k_select
 #define RPROF_DECL uint64_t rp_[7] = {0, 0, 0, 0, 0, 0, 0}, rp_t = __builtin_amdgcn_s_memtime();
 #define RPROF(i)                                         \
   {                                                      \
@@ -3863,8 +3863,14 @@ constexpr int SEL_COPIES = 8;   // histogram copies per wave (pass 2)
 __host__ __device__ inline int select_seg(int lo, int hi) { return ((hi - lo + SELECT_WAVES - 1) / SELECT_WAVES + 511) & ~511; }
 // workgroups per pod of a plain batch's split k_select over n nodes: >= 256 workgroups in all, parts of
 // >= 4096 nodes, at most MAX_WORLD (k_merge's fan-in)
+// (parts of >= 24576 nodes: at C3's 50k nodes two parts per pod measured 93.5 G against 92.1 G with four and 91.1 G
+// with one -- profiles/r06/ab_select_parts.txt; the split's merge tail costs more than the per-part pass saves.
+// KOORDEVAL_SELECT_PARTS = P, an A/B knob: at most P parts of >= 4096 nodes.)
 inline int select_parts(int64_t n, int bp, int L = 2 * 64) {
-  return std::max(1, std::min({8, (255 + bp) / bp, (int)(n / 4096), 1024 / L}));  // (the merge: parts x L <= 1024)
+  const char* e = std::getenv("KOORDEVAL_SELECT_PARTS");
+  const int cap = e ? std::max(1, std::min(8, std::atoi(e))) : 8;
+  const int64_t per = e ? 4096 : 24576;
+  return std::max(1, std::min({cap, (255 + bp) / bp, (int)(n / per), 1024 / L}));  // (the merge: parts x L <= 1024)
 }
 // node part of one of `parts` workgroups of a split k_select (512-aligned, like the shard ranges)
 __host__ __device__ inline int select_part(int lo, int hi, int parts) { return ((hi - lo + parts - 1) / parts + 511) & ~511; }
@@ -3947,6 +3953,7 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
                                                          int32_t* __restrict__ ready = nullptr,
                                                          int32_t* __restrict__ started = nullptr) {
   uint32_t* const gath = cand;
+  RPROF_DECL
   if (!DS && gridDim.y > 1) {
     const int part = select_part(lo, hi, gridDim.y);
     lo = min(hi, lo + (int)blockIdx.y * part);
@@ -4039,6 +4046,7 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
     at_max = wave_sum(at_max);
     if (lane == 0 && at_max) atomicAdd(&s_dscnt, at_max);
   }
+  RPROF(0)
   const uint32_t mx = wave_max_u32(max_halves(mx2));
   const int feas = wave_sum((int)((cnt2 & 0xFFFFu) + (cnt2 >> 16)));
   if (lane == 0) {
@@ -4052,6 +4060,7 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
     M = max(M, s_red[0][w]);
     F += s_red[1][w];
   }
+  RPROF(1)
   int thr = 0, need_ties = 0;  // select v > thr, plus the first need_ties with v == thr
   if (F > k) {
     // pass 2: per-wave histogram of d = M - v over the window d < 64.  An infeasible node (v = 0) has
@@ -4149,6 +4158,7 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
     }
     __syncthreads();
   }
+  RPROF(2)
   // pass 3: select (a step none of whose scores reaches vmin holds no selected node and no tie)
   const uint32_t vmin = (uint32_t)max(1, need_ties > 0 ? thr : thr + 1);
   uint32_t* const stage = reinterpret_cast<uint32_t*>(&s_hist[0][0][0]);  // (pass 3 reads no histogram)
@@ -4198,6 +4208,7 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
     }
   });
   __syncthreads();
+  RPROF(3)
   if (mcand && !DS) {  // the part's list in descending order (the merge ranks by binary search)
     const int n = s_out;
     if ((int)threadIdx.x < n) {
@@ -4217,7 +4228,11 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (DS || !mcand) return;
+  RPROF(4)
+  if (DS || !mcand) {
+    RPROF_FLUSH(3, 1)
+    return;
+  }
   // split select with the merge fused: the workgroup finishing pod j's last part merges the parts (k_merge's
   // work without its launch).  The lists went out as sc1 stores; every wave drains them before the barrier,
   // then one relaxed count (no agent-scope fence: on this part it would write back the XCD's L2,
@@ -4231,7 +4246,11 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
     if (s_last) parts_done[j] = 0;  // the next batch's count (stream order; no other workgroup touches it now)
   }
   __syncthreads();
-  if (!s_last) return;
+  RPROF(5)
+  if (!s_last) {
+    RPROF_FLUSH(3, 1)
+    return;
+  }
   __syncthreads();  // (the staging reads above, before the merge reuses the words)
   merge_lists<true, true>(gath, ystride, (int)gridDim.y, ostride, kext, j, reinterpret_cast<uint4*>(&s_hist[0][0][0]),
                           mcand, mcnt, ready != nullptr);
@@ -4240,6 +4259,8 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  RPROF(6)
+  RPROF_FLUSH(3, 1)
 }
 
 // --- node-sharded batches: merge of the per-shard candidate lists ---------------------------------

@@ -165,9 +165,10 @@ def test_topology_delete_readd_keeps_allocation_parity(gpu):
 
 
 def test_refused_call_leaves_no_state(gpu):
-    """a queue whose matched pod is refused (its reservation sits on a NUMA-policy node) fails in the
-    argument checks, before any pod is scheduled -- the plain pods ahead of it are not Reserved and the matched
-    restore is not left behind; the next queue equals an oracle that never saw the refused one."""
+    """a queue whose matched pod is refused (a pod binding CPUs whose reservation holds NUMA
+    resources on a NUMA-policy node) fails in the argument checks, before any pod is scheduled -- the plain pods ahead
+    of it are not Reserved and the matched restore is not left behind; the next queue equals an oracle that never
+    saw the refused one."""
     ev, o, cl = _plain(400, 1121)
     node = abi.Node.from_buffer_copy(cl.nodes[7].tobytes())
     node.numa_topology_policy = abi.NUMA_POLICY_BEST_EFFORT
@@ -180,7 +181,8 @@ def test_refused_call_leaves_no_state(gpu):
         h.reservations_load(rs, al)
     pods = synth.make_pods(200, synth.BASE_SEED + 1122)
     pods["reservation_matched"][150] = abi.RSV_MATCHED
-    pods["qos_class"][150] = abi.QOS_LS  # not a cpuset pod: refused for the reservation's node alone
+    pods["qos_class"][150], pods["priority_class"][150] = abi.QOS_LSR, abi.PRIORITY_PROD  # binds CPUs: refused
+    pods["requests"][150, abi.RES_CPU] = pods["limits"][150, abi.RES_CPU] = 2000
     pods["numa_topology_policy"][150] = 0
     pods["requests"][150, 2:] = 0
     pods["has_other_requests"][150] = 0
