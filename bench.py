@@ -11,7 +11,7 @@ one workgroup, per-batch time from in-kernel s_memrealtime stamps); eval and sel
 alternating eval streams (k_fixup too with --pipeline-fixup).  `roofline.achieved` = SURVEY.md §8(d)'s algorithmic bytes of a batch (N*S_row +
 B*S_pod + B*k*12) over that critical path; `roofline.replay` the replay's own bytes, `roofline.kernels`
 every kernel of a batch and `roofline.end_to_end` the whole step, each against 8 TB/s.
-`traffic` = HBM bytes from a prior rocprofv3 PMC pass of this workload (profiles/r05/pmc_bench.json).
+`traffic` = HBM bytes from a prior rocprofv3 PMC pass of this workload (profiles/r06/pmc_bench.json).
 
 cpu_baseline: the oracle (C restatement of the Go plugins, oracle/) scheduling a prefix of the same
 queue on the host's cores at 1 thread, 16 threads (upstream Parallelism) and every usable core.
@@ -98,13 +98,14 @@ def batch_bytes(n_nodes, b, fetched, changed, pipelined, fixup=False):
 
 def pmc_traffic(tag):
     """HBM bytes per launch by kernel from the committed PMC passes (tools/pmc_bench.sh, summarised by
-    tools/pmc_summary.py into profiles/r05/pmc_bench.json) of this workload.  Counter collection serialises
+    tools/pmc_summary.py into profiles/<round>/pmc_bench.json, the newest) of this workload.  Counter collection serialises
     dispatches, which the persistent Reserve chain (and the eval streams' kernels that wait on its flags: k_handoff,
     k_fixlist) cannot run under, so the passes run the one-stream schedule (tag suffix _serial): its k_eval_plain /
     k_select / k_resolve launches do the same work per batch; k_fixlist moves <= 64 records + 64 x 256 keys per
     batch (about 64 KB)."""
-    f = os.path.join(ROOT, "profiles", "r05", "pmc_bench.json")
-    if not os.path.exists(f):
+    f = next((x for x in (os.path.join(ROOT, "profiles", r, "pmc_bench.json") for r in ("r06", "r05")) if os.path.exists(x)),
+             None)  # (the newest round's passes)
+    if f is None:
         return {}, None
     d = json.load(open(f))
     w = d.get("workloads", {})
@@ -219,6 +220,11 @@ def roofline(n_nodes, b, ks, dt_step, batches_per_step, pipelined, tag, fixup=Fa
     return {"bound": "hbm", "kernel": "k_resolve_run (the Reserve chain: the batch's critical path)",
             "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS if ach else None,
             "traffic": pmc_sum, "traffic_source": src, "bytes_per_launch": alg, "launch_ms": crit_ms,
+            "batches_per_launch": batches_per_step,
+            "reproduce": "k_resolve_run is one persistent launch per ke_schedule call (one call per step): achieved = "
+                         "bytes_per_launch x batches_per_launch / (AverageNs of k_resolve_run in a rocprofv3 "
+                         "--kernel-trace --stats CSV of the same command); the profiler slows the pipeline, so compare "
+                         "with the bench line printed under it (profiles/r06/bench_under_rocprof.json)",
             "bytes_definition": "SURVEY.md §8(d) per B-pod batch: N*S_row + B*S_pod + B*k*12 "
                                 f"(S_row {sizes()[0]}, S_pod {sizes()[1]}, k {KMAX}); time = replay + hand-off per batch "
                                 "(in-kernel s_memrealtime); traffic = PMC HBM bytes of every kernel of a batch",

@@ -4229,7 +4229,7 @@ __global__ __launch_bounds__(SELECT_BLOCK) void k_select(const uint16_t* __restr
     if (threadIdx.x == 0) __hip_atomic_fetch_add(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   RPROF(4)
-  if (DS || !mcand) {
+  if (DS || !mcand || !parts_done) {  // (no parts_done: the parts stay sorted in place, k_fixlist<PARTS> merges)
     RPROF_FLUSH(3, 1)
     return;
   }
@@ -4426,23 +4426,62 @@ __global__ __launch_bounds__(FIX_BLOCK) void k_fixup(SoA s, const DevPod* __rest
 // in descending key order as the Reserve kernel's stale list -- exact but for batch b-1's nodes, which the replay
 // holds as T slots.  (At most KMAX entries drop, so k_j + KMAX exact keys remain.)  A key of a node that batch
 // b-1 changes too may be torn (its record is being rewritten): the replay drops every T node's key anyway.
+// PARTS (round 6): the split select left its parts' lists sorted in their blocks of the gather buffer (`pre`, `gw`
+// words apart) without merging them -- its sc1 drain, counter and last-arriver merge were its tail -- and this kernel
+// merges them before it waits (a key's rank is its position plus a binary search in every other part, as
+// merge_lists), so the merge is off the done[b-2] -> ready[b] lap.
 constexpr int FIXL_BLOCK = KSTALE2 + KMAX;
-template <bool EXT>
-__global__ __launch_bounds__(FIXL_BLOCK) void k_fixlist(SoA s, const DevPod* __restrict__ pods,
-                                                        const int32_t* __restrict__ batch_base, KArgs k,
-                                                        const uint32_t* __restrict__ pre, const int32_t* __restrict__ pre_cnt,
-                                                        const int32_t* __restrict__ tlist, const int32_t* __restrict__ done_wait,
-                                                        uint32_t* __restrict__ stale, int32_t* __restrict__ stale_cnt,
-                                                        int32_t* __restrict__ ready, int32_t* __restrict__ err) {
+constexpr int FIXL_PARTS_BLOCK = 1024;
+static_assert((1024 / KSTALE2) * KSTALE2 <= FIXL_PARTS_BLOCK, "every part of a select-ahead split fits a workgroup");
+template <bool EXT, bool PARTS = false>
+__global__ __launch_bounds__(PARTS ? FIXL_PARTS_BLOCK : FIXL_BLOCK) void k_fixlist(
+    SoA s, const DevPod* __restrict__ pods, const int32_t* __restrict__ batch_base, KArgs k,
+    const uint32_t* __restrict__ pre, const int32_t* __restrict__ pre_cnt, const int32_t* __restrict__ tlist,
+    const int32_t* __restrict__ done_wait, uint32_t* __restrict__ stale, int32_t* __restrict__ stale_cnt,
+    int32_t* __restrict__ ready, int32_t* __restrict__ err, int64_t gw = 0, int parts = 1) {
   __shared__ int32_t s_tn[KMAX];
   __shared__ uint4 s_k[FIXL_BLOCK / 4];
   __shared__ int32_t s_ok, s_nt;
+  __shared__ uint32_t s_pk[PARTS ? FIXL_PARTS_BLOCK : 1];  // the parts' lists (descending, zeros after each count)
+  __shared__ int32_t s_mcnt;
   const int j = blockIdx.x, kj = min(j + 1, KMAX);
   const int t = threadIdx.x;
   uint32_t key = 0;  // (read before the wait: the select before this kernel on the same stream wrote them)
-  if (t < KSTALE2 && t < pre_cnt[j]) key = pre[j * KSTALE2 + t];
+  if constexpr (PARTS) {
+    const int L = KSTALE2, r = t / L, c = t - r * L;
+    const int kx = kj + 2 * KMAX;  // the merged list's length (the select's k_j + kext)
+    uint32_t pk = 0;
+    if (r < parts) {
+      const uint32_t* blk = pre + (int64_t)r * gw;
+      if (c < (int)blk[MAX_BATCH * L + j]) pk = blk[j * L + c];
+      s_pk[t] = pk;
+    }
+    if (t < KSTALE2) reinterpret_cast<uint32_t*>(s_k)[t] = 0u;
+    const int nz = __syncthreads_count(pk != 0u);
+    if (t == 0) s_mcnt = min(nz, kx);
+    if (pk) {
+      int rank = c;  // the larger keys of its own part come first
+      for (int q = 0; q < parts; q++) {
+        if (q == r) continue;
+        const uint32_t* b = s_pk + q * L;
+        int lo = 0, hi = L;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (b[mid] > pk) lo = mid + 1;
+          else hi = mid;
+        }
+        rank += lo;
+      }
+      if (rank < kx) reinterpret_cast<uint32_t*>(s_k)[rank] = pk;
+    }
+    __syncthreads();
+    if (t < KSTALE2 && t < s_mcnt) key = reinterpret_cast<uint32_t*>(s_k)[t];
+    __syncthreads();  // (s_k is reused below; threads >= FIXL_BLOCK only join the barriers from here)
+  } else {
+    if (t < KSTALE2 && t < pre_cnt[j]) key = pre[j * KSTALE2 + t];
+  }
   DevPod pod;
-  if (t >= KSTALE2) pod = pods[*batch_base + j];
+  if (t >= KSTALE2 && t < FIXL_BLOCK) pod = pods[*batch_base + j];
   if (t == 0) {
     s_ok = done_wait ? wait_at_least(done_wait, 1, err) : 1;
     s_nt = done_wait ? ld_sc1(tlist) : 0;
@@ -4452,7 +4491,7 @@ __global__ __launch_bounds__(FIXL_BLOCK) void k_fixlist(SoA s, const DevPod* __r
   const int nt = s_nt;
   NodeFast n;
   int node = -1;
-  if (t >= KSTALE2 && t - KSTALE2 < nt) {
+  if (t >= KSTALE2 && t < FIXL_BLOCK && t - KSTALE2 < nt) {
     node = ld_sc1(tlist + 1 + (t - KSTALE2));
     rec_load<__HIP_MEMORY_SCOPE_AGENT>(s.rec + (int64_t)node * NUM_RW, n);
     if (EXT && (k.flags & AF_EXT)) ext_load(s, node, k, n);
@@ -4469,7 +4508,7 @@ __global__ __launch_bounds__(FIXL_BLOCK) void k_fixlist(SoA s, const DevPod* __r
     const double estd[2] = {(double)pod.est[0], (double)pod.est[1]}, reqd[2] = {(double)pod.req[0], (double)pod.req[1]};
     key = make_key(fast_total<EXT>(n, pod, estd, reqd, k), node);
   }
-  reinterpret_cast<uint32_t*>(s_k)[t] = key;
+  if (t < FIXL_BLOCK) reinterpret_cast<uint32_t*>(s_k)[t] = key;
   const int nz = __syncthreads_count(key != 0u);
   const int out = min(nz, kj + KMAX);
   if (key) {
@@ -6822,6 +6861,7 @@ struct DeviceState {
   unsigned excl_lds = EXCL_LDS;
   bool eval_patch = true;           // two eval streams: evals wait for batch b-3, k_patch adds b-2 (KOORDEVAL_EVAL_PATCH)
   bool select_ahead = true;         // ... and the select follows the eval at once, k_fixlist adds b-2 to the lists
+  bool fix_merge = true;            // ... a split select leaves its parts unmerged, k_fixlist<PARTS> merges them first
                                     // (KOORDEVAL_SELECT_AHEAD; 0: k_patch before the select)
   int t_helpers = 4;                // T-row helper workgroups of a stale-list run (THelp; KOORDEVAL_T_HELPERS)
   int t_help_ignore = 0;            // test hook (KOORDEVAL_T_HELPERS_IGNORE): the replay's own T rows every batch
@@ -6879,6 +6919,7 @@ int device_create(Context* ctx) {
   if (const char* e = std::getenv("KOORDEVAL_T_HELPERS")) d->t_helpers = std::max(0, std::min(8, std::atoi(e)));
   if (const char* e = std::getenv("KOORDEVAL_EVAL_PATCH")) d->eval_patch = std::atoi(e) != 0;
   if (const char* e = std::getenv("KOORDEVAL_SELECT_AHEAD")) d->select_ahead = std::atoi(e) != 0;
+  if (const char* e = std::getenv("KOORDEVAL_FIX_MERGE")) d->fix_merge = std::atoi(e) != 0;
   if (const char* e = std::getenv("KOORDEVAL_T_HELPERS_IGNORE")) d->t_help_ignore = std::atoi(e) != 0;
   HIP_OK(hipStreamCreateWithPriority(&d->stream, hipStreamNonBlocking, prio_hi));
   HIP_OK(hipStreamCreateWithPriority(&d->estream, hipStreamNonBlocking, prio_lo));
@@ -7999,10 +8040,12 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
       } else if (!sharded && parts > 1) {
         const int gw = gath_words(L);
         const bool rc = select_seg(0, select_part(0, N, parts)) <= SEL_RC * 512;
+        // (select-ahead: no parts_done -- the parts stay sorted in `split` and k_fixlist<PARTS> merges them)
         hipLaunchKernelGGL((rc ? k_select<false, SEL_RC> : k_select<false, 0>), dim3((unsigned)bp, (unsigned)parts),
                            dim3(SELECT_BLOCK), 0, es, scores, d->capacity, 0, (int)N, split,
                            reinterpret_cast<int32_t*>(split + MAX_BATCH * L), d->d_dsraw, d->d_dsmax, k.wp_ds,
-                           kext, L, (int64_t)gw, lists, lists_cnt, pdone, rpub, sstart);  // the last part merges
+                           kext, L, (int64_t)gw, lists, lists_cnt, (pre && d->fix_merge) ? nullptr : pdone, rpub,
+                           sstart);  // the last part merges
         published = rpub != nullptr;
       } else if (!sharded) {
         select(0, N, lists, lists_cnt, ds ? nullptr : rpub);
@@ -8107,11 +8150,20 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
             if (rc) return rc;
             const uint32_t* pre = d->d_pre + (size_t)(q & 1) * MAX_BATCH * KSTALE2;
             const int32_t* pre_cnt = reinterpret_cast<const int32_t*>(d->d_pre + (size_t)2 * MAX_BATCH * KSTALE2) + (q & 1) * MAX_BATCH;
-            hipLaunchKernelGGL((ext ? k_fixlist<true> : k_fixlist<false>), dim3((unsigned)batches[q].pods), dim3(FIXL_BLOCK),
-                               0, es, d->soa, d->d_pods, d_bases + q, k, pre, pre_cnt,
-                               d_tlist + ((q - 2) & 1) * (1 + MAX_BATCH), q - 2 >= r0 ? d_done + (q - 2) : nullptr,
-                               d->d_stale + (size_t)(q & 1) * MAX_BATCH * KSTALE, d->d_stale_cnt + (q & 1) * MAX_BATCH,
-                               d_ready + q, d_err);
+            const int sp = N > 0 && !batches[q].ds ? select_parts(N, batches[q].pods, KSTALE2) : 1;
+            if (d->fix_merge && sp > 1)  // the select left its parts unmerged in the split buffer: the fix merges them
+              hipLaunchKernelGGL((ext ? k_fixlist<true, true> : k_fixlist<false, true>), dim3((unsigned)batches[q].pods),
+                                 dim3(FIXL_PARTS_BLOCK), 0, es, d->soa, d->d_pods, d_bases + q, k,
+                                 alt ? d->d_split2 : d->d_split, nullptr, d_tlist + ((q - 2) & 1) * (1 + MAX_BATCH),
+                                 q - 2 >= r0 ? d_done + (q - 2) : nullptr,
+                                 d->d_stale + (size_t)(q & 1) * MAX_BATCH * KSTALE, d->d_stale_cnt + (q & 1) * MAX_BATCH,
+                                 d_ready + q, d_err, (int64_t)gath_words(KSTALE2), sp);
+            else
+              hipLaunchKernelGGL((ext ? k_fixlist<true> : k_fixlist<false>), dim3((unsigned)batches[q].pods), dim3(FIXL_BLOCK),
+                                 0, es, d->soa, d->d_pods, d_bases + q, k, pre, pre_cnt,
+                                 d_tlist + ((q - 2) & 1) * (1 + MAX_BATCH), q - 2 >= r0 ? d_done + (q - 2) : nullptr,
+                                 d->d_stale + (size_t)(q & 1) * MAX_BATCH * KSTALE, d->d_stale_cnt + (q & 1) * MAX_BATCH,
+                                 d_ready + q, d_err, (int64_t)0, 1);
             continue;
           }
           // two eval streams: batch q's eval waits only for batch q-3, k_patch brings in batch q-2's changed nodes

@@ -248,24 +248,26 @@ def test_c3_full_queue_fixture(gpu, per_call):
 
 
 # ---- the stale-list run's options: T-row helpers, progressive R+S, patched early eval -----------------
-@pytest.mark.parametrize("helpers,patch,ignore,ahead,parts", [("0", "1", "0", "1", "8"), ("4", "0", "0", "1", "8"),
-                                                              ("4", "1", "1", "1", "8"), ("8", "1", "0", "1", "8"),
-                                                              ("4", "1", "0", "0", "8"), ("0", "1", "0", "0", "8"),
-                                                              ("4", "1", "0", "1", "1")],
+@pytest.mark.parametrize("helpers,patch,ignore,ahead,parts,fixm",
+                         [("0", "1", "0", "1", "8", "1"), ("4", "0", "0", "1", "8", "1"), ("4", "1", "1", "1", "8", "1"),
+                          ("8", "1", "0", "1", "8", "1"), ("4", "1", "0", "0", "8", "1"), ("0", "1", "0", "0", "8", "1"),
+                          ("4", "1", "0", "1", "1", "1"), ("4", "1", "0", "1", "8", "0")],
                          ids=["no-helpers", "no-patch", "helpers-ignored", "8-helpers", "patch-then-select",
-                              "patch-then-select-no-helpers", "one-part-select"])
+                              "patch-then-select-no-helpers", "one-part-select", "merge-in-select"])
 @pytest.mark.parametrize("n_nodes,n_pods,seed", [(20_000, 3000, 71), (150, 2500, 72)])
-def test_stale_run_options_match_oracle(gpu, monkeypatch, n_nodes, n_pods, seed, helpers, patch, ignore, ahead, parts):
+def test_stale_run_options_match_oracle(gpu, monkeypatch, n_nodes, n_pods, seed, helpers, patch, ignore, ahead, parts,
+                                       fixm):
     """The stale-list run with its helper workgroups off / on (progressive R+S) / on but ignored (the replay's
     own T rows after the barrier), with the eval waiting for batch b-2 instead of batch b-3, and with batch b-2's
     changed nodes patched into the scores before the select (k_patch) instead of into the select-ahead lists
-    (k_fixlist): every variant places exactly as the oracle and leaves exact rows and records (KOORDEVAL_* are read
-    per device context)."""
+    (k_fixlist), with the split select's parts merged by k_fixlist or by the select's last part: every variant places
+    exactly as the oracle and leaves exact rows and records (KOORDEVAL_* are read per device context)."""
     monkeypatch.setenv("KOORDEVAL_T_HELPERS", helpers)
     monkeypatch.setenv("KOORDEVAL_EVAL_PATCH", patch)
     monkeypatch.setenv("KOORDEVAL_T_HELPERS_IGNORE", ignore)
     monkeypatch.setenv("KOORDEVAL_SELECT_AHEAD", ahead)
-    monkeypatch.setenv("KOORDEVAL_SELECT_PARTS", parts)  # (read once per process: the cap of the first context)
+    monkeypatch.setenv("KOORDEVAL_SELECT_PARTS", parts)  # 8: split selects at 20k nodes (parts of >= 4096 nodes)
+    monkeypatch.setenv("KOORDEVAL_FIX_MERGE", fixm)  # 0: the split select merges its parts, not k_fixlist
     cl = synth.make_cluster(n_nodes, synth.BASE_SEED + seed)
     pods = synth.make_pods(n_pods, synth.BASE_SEED + 100 + seed)
     ev, o = both(synth.config(n_nodes), cl)

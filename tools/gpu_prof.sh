@@ -9,9 +9,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gp
   python3 "$R/bench.py" --no-cpu-baseline --stream-nodes 0 --steps ${STEPS:-10} --warmup 1 ${BENCH_ARGS:-} > "$R/gpurun_out/$TAG/bench.log" 2>&1
 tail -1 "$R/gpurun_out/$TAG/bench.log"
 f=$(find "$R/gpurun_out/$TAG" -name "*kernel_trace.csv" | head -1)
-python3 "$R/tools/timeline.py" "$f" --json "$R/gpurun_out/$TAG/timeline.json" > /dev/null
+python3 "$R/tools/timeline.py" "$f" > "$R/gpurun_out/$TAG/timeline.txt"
 s=$(find "$R/gpurun_out/$TAG" -name "*kernel_stats.csv" | head -1)
 cut -d, -f1-4 "$s" | head -12
-python3 -c "import json;d=json.load(open('$R/gpurun_out/$TAG/timeline.json'));print({k:v for k,v in d.items() if k!='kernels'})"
-python3 -c "import json;d=json.load(open('$R/gpurun_out/$TAG/timeline.json'));[print(k, v) for k, v in d['gaps'].items()]"
+cat "$R/gpurun_out/$TAG/timeline.txt"
 gzip -f "$f"
