@@ -341,3 +341,29 @@ def test_matched_numa_policy_sharded_loopback(gpu):
     assert np.array_equal(s1, s0)
     assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
     _holdings_equal(ev, o)
+
+
+@pytest.mark.parametrize("order2,placed", [(1, False), (0, True)], ids=["r2-nominated", "r1-nominated"])
+def test_numa_score_error_parity(gpu, order2, placed):
+    """NodeNUMAResource's Score error on a feasible node (the nominated reservation's allocation and the node's own
+    both fail on the stored affinity) fails the pod's cycle although another node is feasible (RSV_PAIR_SCORE_ERROR
+    in k_rsv_pick); with the other reservation nominated the pod is placed -- as the oracle (the CPU twin:
+    test_reservations.py::test_numa_score_error_fails_the_pod)."""
+    from test_reservations import score_error_case
+    cl, full, empty, r, a, pods = score_error_case()
+    r["order"][1] = order2
+    cfg = synth.config(2)
+    ev, o = Evaluator(cfg), Oracle(cfg, 2)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        for i in range(2):
+            h.delete_nodemetric(i)
+        h.set_numa(0, full)
+        h.set_numa(1, empty)
+        h.reservations_load(r, a)
+    c1, s1 = ev.schedule(pods, synth.T0, matches=[[0, 1]])
+    c0, s0 = o.schedule(pods, synth.T0, matches=[[0, 1]])
+    assert np.array_equal(c1, c0) and np.array_equal(s1, s0), (c1, c0)
+    assert (c1[0] >= 0) == placed
+    assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
+    _holdings_equal(ev, o)

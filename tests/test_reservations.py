@@ -680,3 +680,66 @@ def test_ignored_numa_pod_reuses_the_held_zone():
         ev.schedule(one, synth.T0)
     assert e.value.code == abi.ERR_NO_DEVICE
     ev.close()
+
+
+def score_error_case():
+    """Two SingleNUMANode nodes of two 4-CPU zones.  Node 0's zones are full: zone 0 is reservation r1's reserve pod
+    (4 CPUs), zone 1 holds reservation r2's (1 CPU) and other pods.  Node 1 is empty.  A matched 3-CPU pod (no
+    affinity) has hints on node 0 only through r1 (zone 0); with r2 nominated (its order), Score's
+    allocateWithNominatedReservation fails on zone 0 and so does tryAllocateFromNode."""
+    from koordinator_amd import model
+    cl = synth.make_cluster(2, synth.BASE_SEED + 1441)
+    cl.nodes["allocatable"][:] = [8000, 64 * 2**30]
+    cl.nodes["raw_allocatable"][:] = abi.ABSENT
+    cl.nodes["requested"][0] = [3000, 0]  # (NodeInfo: fitsNode passes for both reservations)
+    cl.nodes["requested"][1] = [0, 0]
+    cl.nodes["numa_topology_policy"][:] = abi.NUMA_POLICY_SINGLE_NUMA_NODE
+    cl.nodes["cpu_bind_policy"][:] = 0
+    cl.nodes["cpu_amplification_ratio"][:] = 0
+    full = model.make_zones([{"id": 0, "cpu": "4", "memory": "32Gi", "allocated": {"cpu": "4"}},
+                             {"id": 1, "cpu": "4", "memory": "32Gi", "allocated": {"cpu": "4"}}])
+    empty = model.make_zones([{"id": 0, "cpu": "4", "memory": "32Gi"}, {"id": 1, "cpu": "4", "memory": "32Gi"}])
+    r = np.zeros(2, abi.RESERVATION_DTYPE)
+    a = np.zeros(2, abi.RESERVATION_ALLOC_DTYPE)
+    r["node"], r["available"], r["holds"] = 0, 1, abi.RSV_HOLDS_NUMA
+    r["allocatable"][0] = [4000, 2**30]
+    r["allocatable"][1] = [1000, 2**30]
+    a["numa"][0, 0] = 4000
+    a["numa"][1, 2] = 1000
+    pods = synth.make_pods(1, synth.BASE_SEED + 1442)
+    pods["requests"][:, 0], pods["requests"][:, 1], pods["requests"][:, 2:] = 3000, 2**30, 0
+    pods["limits"][:] = 0
+    pods["qos_class"], pods["priority_class"] = abi.QOS_LS, abi.PRIORITY_PROD
+    pods["has_other_requests"], pods["device_requests"], pods["numa_topology_policy"] = 0, 0, 0
+    pods["n_xres"] = 0
+    pods["reservation_matched"] = abi.RSV_MATCHED
+    return cl, full, empty, r, a, pods
+
+
+@pytest.mark.parametrize("order2,placed", [(1, False), (0, True)], ids=["r2-nominated", "r1-nominated"])
+def test_numa_score_error_fails_the_pod(order2, placed):
+    """NodeNUMAResource's Score returns an error status when the nominated reservation's allocation and the node's own
+    both fail on the stored affinity (scoring.go:105-115); RunScorePlugins' error fails the pod's cycle although
+    another node is feasible.  With r1 nominated instead (no order on r2: the Reservation score decides) the pod is
+    placed.  Oracle and product checks agree (the GPU twin: test_gpu_reservation_holdings.py::
+    test_numa_score_error_parity)."""
+    cl, full, empty, r, a, pods = score_error_case()
+    r["order"][1] = order2
+    o = Oracle(synth.config(2), 2)
+    synth.load_into(o, cl)
+    for i in range(2):
+        o.delete_nodemetric(i)
+    o.set_numa(0, full)
+    o.set_numa(1, empty)
+    o.reservations_load(r, a)
+    c, _ = o.schedule(pods, synth.T0, matches=[[0, 1]])
+    assert (c[0] >= 0) == placed, c
+    ev = Evaluator(synth.config(2))
+    synth.load_into(ev, cl)
+    ev.set_numa(0, full)
+    ev.set_numa(1, empty)
+    ev.reservations_load(r, a)
+    with pytest.raises(KoordEvalError) as e:  # accepted by the checks: the device is what is missing here
+        ev.schedule(pods, synth.T0, matches=[[0, 1]])
+    assert e.value.code == abi.ERR_NO_DEVICE
+    ev.close()
