@@ -222,9 +222,10 @@ static int check_matches(Context& c, const ke_pod* pods, int32_t n) {
                                           "that holds devices");
       }
     // under a NUMA policy (the pod's or the node's) a matched reservation holding NUMA resources or CPUs enters the
-    // hints through its allocate-from-reservation trials (k_numa_views) for a pod binding no CPUs without device
-    // requests; a binding pod's hints over the held CPUs and a DeviceShare pod's joint hints there are not restated,
-    // nor more than NV_MAX such reservations of the pod on one node
+    // hints through its allocate-from-reservation trials (k_numa_views) for a pod without device requests -- one
+    // binding CPUs too (whole CPUs, not under a required FullPCPUs policy: preferredCPUs taken first may split cores,
+    // which the per-view counts do not see); a DeviceShare pod's joint hints there are not restated, nor more than
+    // NV_MAX such reservations of the pod on one node
     if (!c.resv_holds.empty()) {
       const bool binds = (f & PF_CPUSET) || (c.n_bind_nodes > 0 && pods[p].requests[KE_RES_CPU] > 0);
       const bool dev = (f & (PF_DS | PF_DS_HINT)) != 0;
@@ -237,9 +238,13 @@ static int check_matches(Context& c, const ke_pod* pods, int32_t n) {
         const int32_t node = c.resv[(size_t)r].node;
         const bool pol = pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE ||
                          c.nodes[(size_t)node].node.numa_topology_policy != KE_NUMA_POLICY_NONE;
-        if (pol && (binds || dev))
-          return fail(KE_ERR_UNSUPPORTED, "a pod binding CPUs or requesting devices under a NUMA topology policy "
-                                          "matching a reservation that holds NUMA resources or CPUs");
+        const int preq = pf_cpu_required(f);
+        const bool full_req = preq == XB_FULL || (preq == XB_NONE && c.nodes[(size_t)node].node.cpu_bind_policy ==
+                                                                         KE_NODE_CPU_BIND_FULL_PCPUS_ONLY);
+        if (pol && (dev || (binds && (!(f & PF_CPU_INT) || full_req))))
+          return fail(KE_ERR_UNSUPPORTED, "a pod requesting devices, fractional CPUs or a required FullPCPUs binding "
+                                          "under a NUMA topology policy matching a reservation that holds NUMA "
+                                          "resources or CPUs");
         bool seen = false;
         for (auto& e : per_node)
           if (e.first == node) seen = true, e.second++;
@@ -998,6 +1003,15 @@ static int schedule_sync(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_
       }
       rc = resv_prepare(c, pods[s0], ids, n_ids, pods[s0].reservation_matched == KE_RSV_AFFINITY);
       if (rc) return rc;
+      if (!c.numa_cs_views.empty()) {  // a binding pod's cpuset of the nominated reservation (NUMA policies)
+        rc = device_rsv_views(&c, pods[s0], now_ns, c.numa_cs_views, c.numa_cs_out);
+        if (rc) {
+          int32_t dummy = 0;
+          resv_finish(c, -1, pods[s0], &dummy);
+          return rc;
+        }
+        resv_numa_cs_apply(c);
+      }
     }
     // a device failure leaves the pods of earlier segments Reserved on the device and the context's state
     // undefined (KE_ERR_DEVICE: rebuild the context); the matched-restore state is still undone so the

@@ -1077,8 +1077,11 @@ void resv_views(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids
   nodes.erase(std::unique(nodes.begin(), nodes.end()), nodes.end());
   for (int32_t node : nodes) {
     const NodeState& ns = c.nodes[(size_t)node];
-    // a node with a NUMA policy: refused before (resv_check); a pod binding no CPUs there allocates no cpuset
-    if (ns.node.numa_topology_policy != KE_NUMA_POLICY_NONE || !pod_binds_on(dp, ns) || !cpus_valid(ns)) continue;
+    // under a NUMA policy (the pod's or the node's) the trials are k_numa_views'; a pod binding no CPUs there
+    // allocates no cpuset
+    if (ns.node.numa_topology_policy != KE_NUMA_POLICY_NONE || pod.numa_topology_policy != KE_NUMA_POLICY_NONE ||
+        !pod_binds_on(dp, ns) || !cpus_valid(ns))
+      continue;
     uint64_t merged[4] = {0, 0, 0, 0};  // mergedMatchedAllocatedCPUs: the matched ones' allocatable CPUs
     for (int32_t i : c.resv_by_node[(size_t)node])
       if (m[(size_t)i] && resv_holds_cpu(c, i))
@@ -1323,8 +1326,44 @@ void resv_numa_views(Context& c, const ke_pod& pod, const int32_t* ids, int32_t 
           v.reuse[q][j] += v.req[q][j];
         }
     }
+    if (pod_binds_on(dp, ns) && cpus_valid(ns)) {  // the views' preferredCPUs (reservation.go:293-311, 340-357)
+      uint64_t allocd[4] = {0, 0, 0, 0};          // mergedMatchedAllocatedCPUs: the reserve pods' CPUs
+      for (int32_t i : mine)
+        for (int w = 0; w < 4; w++) allocd[w] |= c.resv_alloc[(size_t)i].cpuset[w];
+      for (size_t q = 0; q < mine.size(); q++) {
+        const ke_reservation_alloc& a = c.resv_alloc[(size_t)mine[q]];
+        int rem = 0;
+        for (int w = 0; w < 4; w++) {
+          const uint64_t rc = a.cpuset[w] & ~a.owner_cpuset[w];  // remainedCPUs
+          v.pref[NV_MAX][w] |= rc;                                // mergedMatchedRemainCPUs (the hint view)
+          v.pref[q][w] = allocd[w] | rc;
+          v.rpref[q][w] = rc;
+          rem += __builtin_popcountll(rc);
+        }
+        v.rem_cpus[q] = rem;
+      }
+    }
     c.numa_view_ids.push_back(mine);
   }
+}
+
+void resv_numa_cs_apply(Context& c) {
+  for (size_t j = 0; j < c.numa_cs_views.size(); j++) {
+    RsvOvr& o = c.rsv_ovr[(size_t)c.numa_cs_ovr[j]];
+    const bool ok = j < c.numa_cs_out.size() && c.numa_cs_out[j].ok;
+    if (ok) {
+      o.reserve = 1;
+      o.numa_score = (int16_t)c.numa_cs_out[j].score;
+      for (int w = 0; w < 4; w++) o.cpus[w] = c.numa_cs_out[j].cpus[w];
+    } else {  // (the Filter's counts admitted the trial: not reached while they agree with allocateCPUSet)
+      o.reserve = 2;
+      if (o.numa_st == KE_CODE_SUCCESS) c.rsv_pairs[(size_t)c.numa_cs_pair[j]].allowed |= RSV_PAIR_SCORE_ERROR;
+    }
+  }
+  c.numa_cs_views.clear();
+  c.numa_cs_ovr.clear();
+  c.numa_cs_pair.clear();
+  c.numa_cs_out.clear();
 }
 
 int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids, bool affinity) {
@@ -1511,6 +1550,29 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
         o.numa_score = (int16_t)nvo->score[use];
         std::memcpy(o.numa_dist, nvo->dist[use], sizeof o.numa_dist);
       }
+      if (use >= 0 && use < NV_MAX && binds && cpus_valid(ns)) {
+        // a binding pod: the cpuset of the nominated reservation's allocation and the Score it gives (k_rsv_views
+        // with the allocation's zones, resv_numa_cs_apply) -- a Restricted one's from its remainedCPUs
+        const NumaRsvView& nv = c.numa_views[(size_t)nvi];
+        RsvView v{};
+        v.node = node;
+        for (int w = 0; w < 4; w++) {
+          v.pref[w] = nv.restricted[use] ? nv.rpref[use][w] : nv.pref[use][w];
+          v.pref2[w] = nv.pref[use][w];
+        }
+        for (int z = 0; z < 8; z++)
+          if (nvo->dist[use][2 * z] != 0 || nvo->dist[use][2 * z + 1] != 0) {
+            v.zmask |= 1 << z;
+            v.zcpu[z] = nvo->dist[use][2 * z];
+          }
+        v.score_on = 1;
+        v.sreq1 = nvo->sreq1[use];
+        v.salloc[0] = nvo->salloc[use][0];
+        v.salloc[1] = nvo->salloc[use][1];
+        c.numa_cs_views.push_back(v);
+        c.numa_cs_ovr.push_back((int32_t)c.rsv_ovr.size());
+        c.numa_cs_pair.push_back((int32_t)c.rsv_pairs.size());
+      }
       any_ovr = true;
     }
     c.rsv_pairs.push_back({node, (int16_t)(nom >= 0 ? resv_score(c, nom, pod) : 0),
@@ -1521,7 +1583,7 @@ int resv_prepare(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_id
     // NodeNUMAResource with the matched reservations first (plugin.go:381-397, 553-563): the Filter's trial
     // (one satisfied; else "Reservation(s) ..." under an affinity, else the node's own) and Reserve's allocation
     // (the nominated reservation's when it holds one and is satisfied; failing under an affinity)
-    if (binds && ns.node.numa_topology_policy == KE_NUMA_POLICY_NONE) {
+    if (binds && ns.node.numa_topology_policy == KE_NUMA_POLICY_NONE && !nvo) {
       bool any_view = false, any_ok = false;
       for (size_t q = 0; q < c.rsv_views.size(); q++)
         if (c.rsv_views[q].node == node) {
@@ -1631,6 +1693,10 @@ void resv_finish(Context& c, int32_t chosen_local, const ke_pod& pod, int32_t* a
   c.numa_views.clear();
   c.numa_view_ids.clear();
   c.numa_view_out.clear();
+  c.numa_cs_views.clear();
+  c.numa_cs_ovr.clear();
+  c.numa_cs_pair.clear();
+  c.numa_cs_out.clear();
 }
 
 // forgetPod -> RemoveAssignedPod (reservation_info.go:470-482)

@@ -239,6 +239,11 @@ struct Context {
   std::vector<NumaRsvView> numa_views;
   std::vector<std::vector<int32_t>> numa_view_ids;
   std::vector<NumaRsvOut> numa_view_out;
+  // a binding pod's cpuset pass after the nomination (resv_prepare -> k_rsv_views with zones, resv_numa_cs_apply): per
+  // view the rsv_ovr / rsv_pairs entries it completes
+  std::vector<RsvView> numa_cs_views;
+  std::vector<int32_t> numa_cs_ovr, numa_cs_pair;
+  std::vector<RsvViewOut> numa_cs_out;
   std::vector<int32_t> last_resv;  // per pod of the last ke_schedule: 1 + the reservation assumed, 0 = none
   int32_t resv_gen = 0;            // ke_reservations_generation: bumped by every load_reservations
   // per-pod latency of the last ke_schedule (ke_last_pod_latencies): the call's entry on the host clock, and
@@ -361,10 +366,14 @@ void resv_views(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids
 // of a reservation-ignored one: per node of its device-holding reservations one per such reservation in index order
 // and the node's own (-1); an ignored pod the node's own and the ignore view (-2).  Into c.ds_views / ds_view_resv.
 void resv_ds_views(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids);
-// the NodeNUMAResource views of a reservation-matched pod binding no CPUs (ids: its matched reservations): per node of
-// its reservations holding NUMA resources / CPUs where a NUMA policy applies, one view set over them (k_numa_views).
-// Into c.numa_views / numa_view_ids; the rows of those nodes carry the pod's matched restore.
+// the NodeNUMAResource views of a reservation-matched pod (ids: its matched reservations): per node of its
+// reservations holding NUMA resources / CPUs where a NUMA policy applies, one view set over them (k_numa_views), with
+// the views' preferredCPUs for a pod binding CPUs there.  Into c.numa_views / numa_view_ids; the rows of those nodes
+// carry the pod's matched restore.
 void resv_numa_views(Context& c, const ke_pod& pod, const int32_t* ids, int32_t n_ids);
+// the cpuset pass's outcome (c.numa_cs_out, k_rsv_views over c.numa_cs_views after resv_prepare): Reserve's cpuset and
+// the Score of the nominated reservation's allocation; a failed one is a Score error
+void resv_numa_cs_apply(Context& c);
 // the refusals of resv_prepare, checked for every pod before a ke_schedule call schedules any
 int resv_check(const Context& c, const int32_t* ids, int32_t n_ids);
 // a run of KE_RSV_IGNORED pods: the rows with every usable reservation matchedOrIgnored (begin) and back to the

@@ -1416,6 +1416,27 @@ struct NumaCs {
 };
 __device__ __forceinline__ int cs_zc(const NumaCs& c, int z) { return cs_zone(c.zlo, c.zhi, z); }
 
+// the same from a CS_CNT word and the three CS_Z* word pairs (cs_fill's layout; a view's availability, k_numa_views)
+__device__ __forceinline__ NumaCs numa_cs_words(int64_t cnt, const int64_t (&z6)[6], uint32_t nf, const DevPod& p) {
+  NumaCs c;
+  const int preq = pf_cpu_required(p.flags), nb = nf_cpu_bind(nf);
+  int bind = preq;
+  c.req = true;
+  if (preq == XB_NONE) {
+    if (nb == KE_NODE_CPU_BIND_SPREAD_BY_PCPUS) bind = XB_SPREAD;
+    else if (nb == KE_NODE_CPU_BIND_FULL_PCPUS_ONLY) bind = XB_FULL;
+    else c.req = false, bind = pf_cpu_preferred(p.flags);
+  }
+  c.rcb = true;
+  c.full = c.req && bind == XB_FULL;
+  c.num = (int)(p.req[0] / 1000);
+  c.cpc = cs_cpc(cnt);
+  const int zw = !c.req ? 0 : (bind == XB_FULL ? 2 : 4);
+  c.total = !c.req ? cs_all(cnt) : (bind == XB_FULL ? cs_full(cnt) : cs_spread(cnt));
+  c.zlo = z6[zw];
+  c.zhi = z6[zw + 1];
+  return c;
+}
 __device__ __forceinline__ NumaCs numa_cs_load(const SoA& s, int64_t i, uint32_t nf, const DevPod& p) {
   NumaCs c;
   const int64_t cnt = s.cs[CS_CNT * s.stride + i];
@@ -6008,7 +6029,7 @@ struct CsrShared {
   int64_t node;
   int64_t zcpu[8];  // the NUMA allocation's cpu per id (cpuset_allocate's zones)
   uint32_t nf, zmask;
-  int take, cs_pass, commit, excl, cpc, max_ref;
+  int take, cs_pass, commit, excl, cpc, max_ref, numa_ovr;
   int cs_old[8], cs_add[8];  // allocated CPUs per NUMA id before the pod; newly allocated ones
   uint32_t used[8];          // NUMA ids (0..255) of the cpuset
   int zc[24];                // cs_fill's per-NUMA-id counts: available, in full cores, cores' lowest
@@ -6087,8 +6108,12 @@ __device__ void cpuset_commit_wave(const SoA& s, AccLds& a, CsrShared& sh, int l
 // RefCount-- on the view's preferredCPUs (getAvailableCPUs(preferred), node_allocation.go:192-219) and
 // takePreferredCPUs; a Restricted reservation's view then needs numCPUsNeeded <= |remainedCPUs| and a second
 // allocation preferring only them, whose cpuset may not outgrow them.
+// zmask != 0 or score_on (a pod binding CPUs under a NUMA policy, after k_numa_views and the nomination): one
+// allocation with `pref` over the zones of the trial's NUMA allocation, and with score_on the NodeNUMAResource Score of
+// it -- requested cpu = Amplify(the CPUs still referenced once `pref2`, the options' preferredCPUs, gives back those
+// not in the cpuset, x 1000) (scoring.go:101-119, 179-185).
 __global__ __launch_bounds__(64) void k_rsv_views(SoA s, const DevPod* __restrict__ pods, const RsvView* __restrict__ views,
-                                                  RsvViewOut* __restrict__ out) {
+                                                  RsvViewOut* __restrict__ out, KArgs k) {
   __shared__ AccLds a;
   __shared__ int s_ok;
   const RsvView v = views[blockIdx.x];
@@ -6122,8 +6147,7 @@ __global__ __launch_bounds__(64) void k_rsv_views(SoA s, const DevPod* __restric
     top_numa = (int)wave_max_u32((uint32_t)top_numa);
     if (L == 0) a.n_cpu = top_cpu, a.n_numa = top_numa, a.has_pref = 1;
     __syncthreads();
-    const int64_t zcpu[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const bool took = cpuset_allocate(s, v.node, nf, pod, a, 0u, zcpu);
+    const bool took = cpuset_allocate(s, v.node, nf, pod, a, (uint32_t)v.zmask, v.zcpu);
     if (L == 0) s_ok = took;
     __syncthreads();
     ok = s_ok != 0;
@@ -6139,8 +6163,26 @@ __global__ __launch_bounds__(64) void k_rsv_views(SoA s, const DevPod* __restric
   if (ok)
     for (int c = 0; c < CPU_SLOTS; c++)
       if (a.res[c]) w4[c >> 6] |= 1ull << (c & 63);
+  int32_t score = 0;
+  if (ok && v.score_on) {
+    const CpuRec* recs = s.cpu + (int64_t)v.node * CPU_SLOTS;
+    int held = 0;
+    for (int c = L; c < CPU_SLOTS; c += 64) {
+      const CpuRec r = recs[c];
+      int ref = (r.flags & CR_VALID) ? r.ref : 0;
+      if (ref > 0 && ((v.pref2[c >> 6] >> (c & 63)) & 1) && !((w4[c >> 6] >> (c & 63)) & 1)) ref--;
+      held += ref > 0;
+    }
+    held = acc_wave_sum(held);
+    const int64_t rs = s.cs[CS_RS * s.stride + v.node];
+    DevPod ps = pod;
+    ps.req[0] = amplify_bits(pod.req[0], rs);
+    const int64_t req[2] = {amplify_bits((int64_t)held * 1000, rs), v.sreq1}, alloc[2] = {v.salloc[0], v.salloc[1]};
+    score = numa_scope_score((k.flags & AF_NUMA_MOST) != 0, req, alloc, ps, k);
+  }
   if (L == 0) {
     out[blockIdx.x].ok = ok ? 1 : 0;
+    out[blockIdx.x].score = score;
     for (int w = 0; w < 4; w++) out[blockIdx.x].cpus[w] = w4[w];
   }
 }
@@ -6260,13 +6302,16 @@ __device__ __noinline__ void numa_view_req(const NumaNode& base, const int64_t* 
   numa_perm(o, 1);
 }
 
-// One workgroup per view set (a node of the matched pod's reservations holding NUMA resources / CPUs, the pod binding
-// no CPUs, a NUMA policy merged): the views in LDS; every lane takes masks of IterateBitMasks' order and asks the
-// Allocate of generateResourceHints (resource_manager.go:586-594): tryAllocateFromReservation over the trials (the
-// first satisfied one), else -- without a reservation affinity -- tryAllocateFromNode; lane 0 merges the hint lists
-// as numa_admit does (preferred scan, BestEffort's full fold) and runs Plugin.Allocate on the affinity
-// (topology_hint.go:78-118); lanes q <= n then record each trial's (and the node's own) allocation on it and the Score
-// calculateAllocatableAndRequested gives with its options (scoring.go:101-119, 141-186).  Reads the SoA only.
+// One workgroup per view set (a node of the matched pod's reservations holding NUMA resources / CPUs, a NUMA policy
+// merged): the views in LDS; every lane takes masks of IterateBitMasks' order and asks the Allocate of
+// generateResourceHints (resource_manager.go:586-594): tryAllocateFromReservation over the trials (the first satisfied
+// one), else -- without a reservation affinity -- tryAllocateFromNode; lane 0 merges the hint lists as numa_admit does
+// (preferred scan, BestEffort's full fold) and runs Plugin.Allocate on the affinity (topology_hint.go:78-118); lanes
+// q <= n then record each trial's (and the node's own) allocation on it and the Score calculateAllocatableAndRequested
+// gives with its options (scoring.go:101-119, 141-186).  A pod binding CPUs (round 6): every view has its own
+// availability counts (cs_fill with the view's preferredCPUs), trims its zones under a required bind policy and
+// checks allocateCPUSet's take by counts as numa_fits<CS>; its Score's cpu needs the cpuset, which the
+// cpuset pass (k_rsv_views with zones) adds to sreq1 / salloc.  Reads the SoA only.
 __global__ __launch_bounds__(64) void k_numa_views(SoA s, const DevPod* __restrict__ pods,
                                                    const NumaRsvView* __restrict__ views, NumaRsvOut* __restrict__ out,
                                                    KArgs k) {
@@ -6275,7 +6320,10 @@ __global__ __launch_bounds__(64) void k_numa_views(SoA s, const DevPod* __restri
   const int64_t i = w.node;
   const int n = min(w.n, NV_MAX);
   const int lane = (int)threadIdx.x;
-  __shared__ NumaNode s_v[2 + 2 * NV_MAX];  // 0 hint, 1 node, 2 + q trial q, 2 + NV_MAX + q its requiredResources
+  constexpr int NVW = 2 + 2 * NV_MAX;  // 0 hint, 1 node, 2 + q trial q, 2 + NV_MAX + q its requiredResources
+  __shared__ NumaNode s_v[NVW];
+  __shared__ NumaCs s_cs[NVW];
+  __shared__ uint8_t s_scr[NVW][CPU_SLOTS];
   __shared__ int64_t s_al[NV_MAX + 1][2][8];  // the allocated amounts of trial q / the node (NV_MAX)
   __shared__ unsigned long long s_L[2][4];
   __shared__ uint32_t s_aff;
@@ -6283,42 +6331,78 @@ __global__ __launch_bounds__(64) void k_numa_views(SoA s, const DevPod* __restri
   NodeRegs nr;
   load_row(s, i, nr);
   const uint32_t nf = nr.flags;
-  if (lane < 2 + 2 * NV_MAX) {
+  // requestCPUBind (util.go:121-138), as eval_pair; a binding pod's hint scores see its amplified cpu request
+  const bool rcb = s.cpu != nullptr && (nf & NF_CPUS_VALID) && !(p.flags & PF_NUMA_SKIP) &&
+                   ((p.flags & PF_CPU_RCB) || (p.req[0] != 0 && nf_cpu_bind(nf) != KE_NODE_CPU_BIND_NONE &&
+                                               (p.flags & PF_CPU_INT)));
+  DevPod ps = p;
+  if (rcb) ps.req[0] = amplify_bits(p.req[0], s.cs[CS_RS * s.stride + i]);
+  if (lane < NVW) {
+    NumaCs cs;
+    cs.rcb = false;
+    const bool used = lane < 2 || (lane < 2 + n) || (lane >= 2 + NV_MAX && lane < 2 + NV_MAX + n);
+    if (rcb && used) {
+      if (lane == 1) {
+        cs = numa_cs_load(s, i, nf, p);
+      } else {
+        const uint64_t* pr = lane == 0 ? w.pref[NV_MAX] : lane < 2 + NV_MAX ? w.pref[lane - 2] : w.rpref[lane - 2 - NV_MAX];
+        const int64_t c0 = s.cs[CS_CNT * s.stride + i];
+        int64_t cnt, z6[6];
+        cs_fill(s.cpu + i * CPU_SLOTS, cs_cpc(c0), cs_max_ref(c0), s_scr[lane], &cnt, z6, pr);
+        cs = numa_cs_words(cnt, z6, nf, p);
+      }
+    }
+    s_cs[lane] = cs;
     NumaNode base;
     numa_load(s, i, base);
     NumaNode o;
     int64_t al[2][8];
     if (lane == 0) {
       numa_view_reuse(s, i, base, w.entry, w.hint, w.hint_keys, o, al);
+      if (cs.rcb) numa_trim(o, cs);
       s_v[0] = o;
     } else if (lane == 1) {
-      s_v[1] = base;
+      o = base;
+      if (cs.rcb) numa_trim(o, cs);
+      s_v[1] = o;
       for (int r = 0; r < 2; r++)
         for (int z = 0; z < 8; z++) s_al[NV_MAX][r][z] = numa_al(s, i, base, z, r);
     } else if (lane < 2 + n) {
       const int q = lane - 2;
       numa_view_reuse(s, i, base, w.entry, w.reuse[q], w.keys[q], o, al);
+      if (cs.rcb) numa_trim(o, cs);
       s_v[lane] = o;
       for (int r = 0; r < 2; r++)
         for (int z = 0; z < 8; z++) s_al[q][r][z] = al[r][z];
     } else if (lane >= 2 + NV_MAX && lane < 2 + NV_MAX + n) {
+      // the Restricted trial's second Allocate: requiredResources when the reserve pod holds NUMA amounts, else the
+      // trial's own reusable view; trimmed by the remainedCPUs' availability
       const int q = lane - 2 - NV_MAX;
-      if (w.has_req[q]) numa_view_req(base, w.req[q], w.req_keys[q], o), s_v[lane] = o;
+      if (w.has_req[q]) numa_view_req(base, w.req[q], w.req_keys[q], o);
+      else numa_view_reuse(s, i, base, w.entry, w.reuse[q], w.keys[q], o, al);
+      if (cs.rcb) numa_trim(o, cs);
+      s_v[lane] = o;
     }
   }
   if (lane < 8) reinterpret_cast<unsigned long long*>(s_L)[lane] = 0ull;
   __syncthreads();
-  // tryAllocateFromReservation's trial q with the hint m: Allocate on its view; a Restricted one's second Allocate
-  // over its requiredResources (a binding pod's CPU checks do not arise: the pod binds none)
+  auto fits = [&](int v, uint32_t m) -> bool {  // Allocate on view v with the hint m (a binding pod: counts, §4e)
+    if (!rcb) return numa_fits(s_v[v], m, p);
+    return m ? numa_fits<true>(s_v[v], m, p, &s_cs[v]) : s_cs[v].total >= s_cs[v].num;
+  };
+  // tryAllocateFromReservation's trial q with the hint m: Allocate on its view; a Restricted one's
+  // numCPUsNeeded <= |remainedCPUs| (a binding pod) and second Allocate
   auto trial = [&](int q, uint32_t m) -> bool {
-    if (!numa_fits(s_v[2 + q], m, p)) return false;
-    return !(w.restricted[q] && w.has_req[q]) || numa_fits(s_v[2 + NV_MAX + q], m, p);
+    if (!fits(2 + q, m)) return false;
+    if (!w.restricted[q]) return true;
+    if (rcb && s_cs[2 + NV_MAX + q].num > w.rem_cpus[q]) return false;
+    return (!w.has_req[q] && !rcb) || fits(2 + NV_MAX + q, m);
   };
   auto allocate = [&](uint32_t m) -> bool {  // Plugin.Allocate / the hint pass's check on mask m (0: no hint)
-    if (!m) return true;
+    if (!m && !rcb) return true;
     for (int q = 0; q < n; q++)
       if (trial(q, m)) return true;
-    return !w.required && numa_fits(s_v[1], m, p);
+    return !w.required && fits(1, m);
   };
   const NumaNode& hv = s_v[0];
   const uint32_t all = hv.zm;
@@ -6373,7 +6457,7 @@ __global__ __launch_bounds__(64) void k_numa_views(SoA s, const DevPod* __restri
           for (int r = 0; r < 2; r++)
             if (present[r]) cand = cand && bit256(L[r], m) && (restricted || (int)__popc(m) == minr[r]);
           if (!cand || !exclusive_ok(hv, m, excl)) continue;
-          const int32_t sc = R * numa_hint_score(s, i, hv, m, p, k);
+          const int32_t sc = R * numa_hint_score(s, i, hv, m, ps, k);
           if (!found || narrower(m, best) || (__popc(m) == __popc(best) && sc > bsc)) best = m, bsc = sc, found = true;
         }
       if (found) {
@@ -6401,7 +6485,7 @@ __global__ __launch_bounds__(64) void k_numa_views(SoA s, const DevPod* __restri
         dh.status = 0;
         dh.none = true;
         dh.copies = 0;
-        aff = merge_all_permutations(s, i, hv, p, k, ml, dh, excl);
+        aff = merge_all_permutations(s, i, hv, ps, k, ml, dh, excl);
       }
     }
     if (st == KE_CODE_SUCCESS && !allocate(aff)) {
@@ -6421,13 +6505,11 @@ __global__ __launch_bounds__(64) void k_numa_views(SoA s, const DevPod* __restri
     const int q = lane;
     int64_t d[2][8] = {{0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0, 0}};
     uint32_t got[2] = {0, 0};
-    if (q < n) {
-      ok = !aff || trial(q, aff);
-      if (ok && aff) numa_distribute<true>((w.restricted[q] && w.has_req[q]) ? s_v[2 + NV_MAX + q] : s_v[2 + q], aff, p,
-                                           got, d);
-    } else {
-      ok = !aff || numa_fits(s_v[1], aff, p);
-      if (ok && aff) numa_distribute<true>(s_v[1], aff, p, got, d);
+    const int vv = q < n ? ((w.restricted[q] && (w.has_req[q] || rcb)) ? 2 + NV_MAX + q : 2 + q) : 1;
+    ok = (!aff && !rcb) || (q < n ? trial(q, aff) : fits(1, aff));
+    if (ok && aff) {
+      if (rcb) numa_distribute<true, true>(s_v[vv], aff, p, got, d, &s_cs[vv]);
+      else numa_distribute<true>(s_v[vv], aff, p, got, d);
     }
     const uint32_t zs = got[0] | got[1];
     int64_t req[2] = {nr.nreq[0], nr.nreq[1]}, alloc[2] = {nr.nalloc[0], nr.nalloc[1]};
@@ -6440,9 +6522,16 @@ __global__ __launch_bounds__(64) void k_numa_views(SoA s, const DevPod* __restri
             req[r] += s_al[q < n ? q : NV_MAX][r][z];
           }
     }
-    out[blockIdx.x].score[q < n ? q : NV_MAX] = ok ? numa_scope_score((k.flags & AF_NUMA_MOST) != 0, req, alloc, p, k) : 0;
+    const int oq = q < n ? q : NV_MAX;
+    // a binding pod: requested cpu = Amplify(the node's allocated CPUs * 1000) (scoring.go:179-185) -- the node's own
+    // here; a trial's gives its preferredCPUs back but for the pod's cpuset (the cpuset pass)
+    if (rcb) req[0] = amplify_bits(nr.csm, s.cs[CS_RS * s.stride + i]);
+    out[blockIdx.x].score[oq] = ok ? numa_scope_score((k.flags & AF_NUMA_MOST) != 0, req, alloc, rcb ? ps : p, k) : 0;
+    out[blockIdx.x].sreq1[oq] = req[1];
+    out[blockIdx.x].salloc[oq][0] = alloc[0];
+    out[blockIdx.x].salloc[oq][1] = alloc[1];
     for (int z = 0; z < 8; z++)
-      for (int r = 0; r < 2; r++) out[blockIdx.x].dist[q < n ? q : NV_MAX][2 * z + r] = ok ? d[r][z] : 0;
+      for (int r = 0; r < 2; r++) out[blockIdx.x].dist[oq][2 * z + r] = ok ? d[r][z] : 0;
   }
   const uint64_t okm = __ballot(ok);
   if (lane == 0) {
@@ -6516,6 +6605,7 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
     sh.cs_pass = 0;
     sh.commit = 0;
     sh.take = 0;
+    sh.numa_ovr = 0;
     for (int q = 0; q < 4; q++) sh.set[q] = 0;
     for (int z = 0; z < 8; z++) sh.cs_old[z] = sh.cs_add[z] = sh.used[z] = 0;
     for (int z = 0; z < 24; z++) sh.zc[z] = 0;
@@ -6536,8 +6626,10 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
     if (nsoa) numa_load(s, node, v);
     // DeviceShare's hints join the Admit of a pod with device requests (topology_hint.go:38-58)
     ds_here = DS && (pod.flags & PF_DS) && (nf & NF_DS_CACHE);
-    const RsvOvr* nro = (ok && npol && !rcb && (nf & NF_RSV_CS)) ? rsv_ovr_of(s, node) : nullptr;
+    const RsvOvr* nro = (ok && npol && (nf & NF_RSV_CS)) ? rsv_ovr_of(s, node) : nullptr;
+    sh.numa_ovr = 0;
     if (nro && nro->numa_on) {  // a reservation-matched pod: the allocation k_numa_views chose (RsvOvr.numa_dist)
+      sh.numa_ovr = 1;  // (a binding pod: its cpuset from the nominated reservation, RsvOvr.reserve / cpus)
       aff = nro->numa_aff;
       for (int z = 0; z < 8; z++)
         for (int r = 0; r < 2; r++) {
@@ -6598,7 +6690,7 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(SoA s, const DevPod* __re
   __syncthreads();
   // a KE_RSV_MATCHED pod on a node without a NUMA policy: NodeNUMAResource Reserve allocates from the nominated
   // reservation first (allocateWithNominatedReservation, reservation.go:492-522), as k_rsv_views computed it
-  const RsvOvr* ro = (sh.take && sh.zmask == 0 && (sh.nf & NF_RSV_CS)) ? rsv_ovr_of(s, sh.node) : nullptr;
+  const RsvOvr* ro = (sh.take && (sh.zmask == 0 || sh.numa_ovr) && (sh.nf & NF_RSV_CS)) ? rsv_ovr_of(s, sh.node) : nullptr;
   if (ro && ro->reserve != 0) {
     for (int c = lane; c < CPU_SLOTS; c += 64) a.res[c] = (ro->cpus[c >> 6] >> (c & 63)) & 1;
     __syncthreads();
@@ -6979,6 +7071,7 @@ int device_create(Context* ctx) {
 int device_refresh(Context* ctx, int64_t now);
 // k_rsv_views for one KE_RSV_MATCHED pod: the allocate-from-reservation trials `views` on the current device
 // state (synchronous; the segment's device_schedule follows)
+static KArgs make_kargs(const Context* ctx, int64_t now);
 int device_rsv_views(Context* ctx, const ke_pod& pod, int64_t now, const std::vector<RsvView>& views,
                      std::vector<RsvViewOut>& out) {
   DeviceState* d = ctx->dev;
@@ -6990,6 +7083,7 @@ int device_rsv_views(Context* ctx, const ke_pod& pod, int64_t now, const std::ve
   for (const RsvView& v : views)
     if (v.node < 0 || v.node >= ctx->n_nodes) return fail(KE_ERR_DEVICE, "reservation view node out of range");
   const DevPod dp = make_dev_pod(ctx->cfg, pod, pod_hints(*ctx, pod), &ctx->tmpl);
+  const KArgs k = make_kargs(ctx, now);
   const size_t vb = sizeof(RsvView) * views.size(), ob = sizeof(RsvViewOut) * views.size();
   rc = ensure((void**)&d->d_rsv_views, &d->rsv_views_cap, (int64_t)(vb + ob + sizeof(DevPod)));
   if (rc) return rc;
@@ -6997,14 +7091,13 @@ int device_rsv_views(Context* ctx, const ke_pod& pod, int64_t now, const std::ve
   HIP_OK(hipMemcpyAsync(base, views.data(), vb, hipMemcpyHostToDevice, d->stream));
   HIP_OK(hipMemcpyAsync(base + vb + ob, &dp, sizeof(DevPod), hipMemcpyHostToDevice, d->stream));
   hipLaunchKernelGGL(k_rsv_views, dim3((unsigned)views.size()), dim3(64), 0, d->stream, d->soa,
-                     (const DevPod*)(base + vb + ob), (const RsvView*)base, (RsvViewOut*)(base + vb));
+                     (const DevPod*)(base + vb + ob), (const RsvView*)base, (RsvViewOut*)(base + vb), k);
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(out.data(), base + vb, ob, hipMemcpyDeviceToHost, d->stream));
   HIP_OK(hipStreamSynchronize(d->stream));
   return KE_OK;
 }
 
-static KArgs make_kargs(const Context* ctx, int64_t now);
 // k_ds_views for one reservation-matched / -ignored DeviceShare pod: its views on the current device state
 // (synchronous, like device_rsv_views)
 int device_ds_views(Context* ctx, const ke_pod& pod, int64_t now, const std::vector<DsView>& views,

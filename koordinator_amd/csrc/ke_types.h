@@ -64,14 +64,22 @@ enum NodeFlag : uint32_t {
 // A KE_RSV_MATCHED pod's allocate-from-reservation trial on one node (k_rsv_views): takePreferredCPUs with
 // preferredCPUs `pref` (getAvailableCPUs(preferred): RefCount-- on each, nodenumaresource/reservation.go:303-339),
 // and for a Restricted reservation a second allocation with `pref2` = its remainedCPUs (:340-417).
+// zmask / zcpu (round 6, a pod binding CPUs under a NUMA policy, k_numa_views' allocation): allocateCPUSet per NUMA id
+// of the allocation (zmask: ids, zcpu: their cpu amounts) instead of over the node; with score_on the NodeNUMAResource
+// Score of the result (scoring.go:101-119, 180-185): requested cpu = Amplify(the node's allocated CPUs with `pref`'s
+// RefCount given back, but for the pod's own, x 1000), requested memory / allocatable = sreq1 / salloc (the zones' or
+// the node's, from k_numa_views).
 struct RsvView {
   int32_t node;
   int32_t restricted;  // 1: Restricted (numCPUsNeeded <= |pref2|, a second allocation on pref2)
   uint64_t pref[4];
   uint64_t pref2[4];
+  int32_t zmask, score_on;
+  int64_t zcpu[8];
+  int64_t sreq1, salloc[2];
 };
 struct RsvViewOut {
-  int32_t ok, pad;
+  int32_t ok, score;
   uint64_t cpus[4];
 };
 // The decisions the host takes from them per node (ke_host.cpp resv_prepare): the Filter's trial allocation
@@ -105,6 +113,10 @@ struct RsvOvr {
 // RestoreReservation's matched set in index order (mergedMatchedAllocated + its remained); a Restricted trial's
 // requiredResources (its remained, signed; has_req = the reserve pod holds NUMA amounts).
 constexpr int NV_MAX = 8;
+// A pod binding CPUs adds preferredCPUs: the hint view's mergedMatchedRemainCPUs (pref[NV_MAX]), each trial's
+// mergedMatchedAllocatedCPUs ∪ its remainedCPUs (pref[q]) and a Restricted trial's remainedCPUs (rpref[q], rem_cpus[q]
+// of them) -- getAvailableCPUs with RefCount given back, the per-NUMA-id counts of the CPUs allocateCPUSet may take
+// (cs_fill) and trimNUMANodeResources under a required bind policy.
 struct NumaRsvView {
   int32_t node, n;
   int32_t required;  // a reservation affinity: no allocation from the node itself
@@ -112,18 +124,25 @@ struct NumaRsvView {
   uint32_t hint_keys;
   uint32_t keys[NV_MAX], req_keys[NV_MAX];
   uint8_t restricted[NV_MAX], has_req[NV_MAX];
+  int32_t rem_cpus[NV_MAX];
   int64_t hint[16];
   int64_t reuse[NV_MAX][16];
   int64_t req[NV_MAX][16];
+  uint64_t pref[NV_MAX + 1][4];
+  uint64_t rpref[NV_MAX][4];
 };
 // its outcome: the Filter (status, reason, the merged affinity -- 0 nil), and on that affinity per trial q (bit q of
-// ok; bit NV_MAX: the node's own) the allocation and the Score with the options it used
+// ok; bit NV_MAX: the node's own) the allocation and the Score with the options it used (a binding pod's Score needs
+// its cpuset: sreq1 / salloc are calculateAllocatableAndRequested's memory requested and allocatable, the cpuset pass
+// -- k_rsv_views -- adds the cpu)
 struct NumaRsvOut {
   int32_t st, reason;
   uint32_t aff, ok;
   int32_t score[NV_MAX + 1];
   int32_t pad;
   int64_t dist[NV_MAX + 1][16];
+  int64_t sreq1[NV_MAX + 1];
+  int64_t salloc[NV_MAX + 1][2];
 };
 // One DeviceShare allocate-from-reservation view of a node (k_ds_views): the allocator's arguments a
 // reservation-matched (or -ignored) pod sees beyond the node's row (AutopilotAllocator with preemptible /
@@ -237,12 +256,19 @@ KE_HD inline int cs_zone(int64_t lo, int64_t hi, int z) { return (int)(((z < 4 ?
 KE_HD inline bool cpu_available(const CpuRec& r, int max_ref) {
   return (r.flags & CR_VALID) && !(r.flags & CR_RESERVED) && !(r.ref > 0 && r.ref >= max_ref);
 }
-// CS_CNT and the six CS_Z* words over one node's records; `core_n` is CPU_SLOTS bytes of scratch
-KE_HD inline void cs_fill(const CpuRec* recs, int cpc, int max_ref, uint8_t* core_n, int64_t* cnt, int64_t* z6) {
+// CS_CNT and the six CS_Z* words over one node's records; `core_n` is CPU_SLOTS bytes of scratch.  `pref`: a
+// view's preferredCPUs given back first (getAvailableCPUs(preferred): RefCount-- on each, node_allocation.go:192-219)
+KE_HD inline void cs_fill(const CpuRec* recs, int cpc, int max_ref, uint8_t* core_n, int64_t* cnt, int64_t* z6,
+                          const uint64_t* pref = nullptr) {
+  auto avail = [&](int c) {
+    CpuRec r = recs[c];
+    if (pref && ((pref[c >> 6] >> (c & 63)) & 1) && r.ref > 0) r.ref--;
+    return cpu_available(r, max_ref);
+  };
   for (int k = 0; k < CPU_SLOTS; k++) core_n[k] = 0;
   int all = 0;
   for (int c = 0; c < CPU_SLOTS; c++)
-    if (cpu_available(recs[c], max_ref)) core_n[recs[c].core]++, all++;
+    if (avail(c)) core_n[recs[c].core]++, all++;
   int full = 0, spread = 0;
   for (int k = 0; k < CPU_SLOTS; k++) {
     if (core_n[k] == cpc && cpc > 0) full += cpc;
@@ -251,7 +277,7 @@ KE_HD inline void cs_fill(const CpuRec* recs, int cpc, int max_ref, uint8_t* cor
   *cnt = cs_pack(full, spread, cpc, max_ref, all);
   for (int w = 0; w < 6; w++) z6[w] = 0;
   for (int c = 0; c < CPU_SLOTS; c++) {  // ascending ids: a core's first available CPU is its lowest
-    if (!cpu_available(recs[c], max_ref) || recs[c].numa >= 8) continue;
+    if (!avail(c) || recs[c].numa >= 8) continue;
     const int z = recs[c].numa, sh = 16 * (z & 3), hi = z >> 2;
     uint8_t& n = core_n[recs[c].core];
     z6[0 + hi] += (int64_t)1 << sh;                                  // available

@@ -5358,9 +5358,10 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
           return KE_ERR_UNSUPPORTED;
       }
     /* under a NUMA policy (the pod's or the node's) a matched reservation holding NUMA resources / CPUs enters the
-     * hints through its allocate-from-reservation trials (numa_admit) for a pod binding no CPUs without device
-     * requests; a binding pod's hints over the held CPUs and a DeviceShare pod's joint hints there are not restated,
-     * nor more than 8 such reservations of the pod on one node (the product's NV_MAX) */
+     * hints through its allocate-from-reservation trials (numa_admit) for a pod without device requests; refused: a
+     * DeviceShare pod's joint hints there, a binding pod with fractional CPUs or under a required FullPCPUs policy (the
+     * product counts a view's CPUs; preferredCPUs taken first may split cores there), more than 8 such reservations
+     * of the pod on one node (the product's NV_MAX) */
     if (c->ralloc) {
       const int binds = st.rcb || st.invalid || (node_bind && pods[p].requests[KE_RES_CPU] > 0);
       const int dev = !d.skip || d.h;
@@ -5369,8 +5370,11 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
         if (!or_resv_usable(&c->resv[r]) || !(or_holds_of(&c->ralloc[r]) & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)))
           continue;
         const int32_t node = c->resv[r].node;
+        const int rq = st.required == KE_CPU_BIND_FULL_PCPUS ? 1 : st.required == KE_CPU_BIND_SPREAD_BY_PCPUS ? 2 : 0;
+        const int full_req = rq == 1 || (rq == 0 && c->nodes[node].node.cpu_bind_policy == KE_NODE_CPU_BIND_FULL_PCPUS_ONLY);
         if ((pods[p].numa_topology_policy != KE_NUMA_POLICY_NONE ||
-             c->nodes[node].node.numa_topology_policy != KE_NUMA_POLICY_NONE) && (binds || dev))
+             c->nodes[node].node.numa_topology_policy != KE_NUMA_POLICY_NONE) &&
+            (dev || (binds && (pods[p].requests[KE_RES_CPU] % 1000 != 0 || full_req))))
           return KE_ERR_UNSUPPORTED;
         int same = 0;
         for (int32_t j2 = c->moff[p]; j2 < c->moff[p + 1]; j2++) {

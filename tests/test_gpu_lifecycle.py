@@ -181,7 +181,8 @@ def test_refused_call_leaves_no_state(gpu):
         h.reservations_load(rs, al)
     pods = synth.make_pods(200, synth.BASE_SEED + 1122)
     pods["reservation_matched"][150] = abi.RSV_MATCHED
-    pods["qos_class"][150], pods["priority_class"][150] = abi.QOS_LSR, abi.PRIORITY_PROD  # binds CPUs: refused
+    pods["qos_class"][150], pods["priority_class"][150] = abi.QOS_LSR, abi.PRIORITY_PROD  # binds CPUs
+    pods["cpu_bind_required"][150] = abi.CPU_BIND_FULL_PCPUS  # under a required FullPCPUs policy: refused
     pods["requests"][150, abi.RES_CPU] = pods["limits"][150, abi.RES_CPU] = 2000
     pods["numa_topology_policy"][150] = 0
     pods["requests"][150, 2:] = 0

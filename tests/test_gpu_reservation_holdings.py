@@ -367,3 +367,107 @@ def test_numa_score_error_parity(gpu, order2, placed):
     assert (c1[0] >= 0) == placed
     assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
     _holdings_equal(ev, o)
+
+
+def numa_bind_matched_setup(n, seed, n_pods, affinity):
+    """numa_matched_setup with CPU bind policies on the nodes (none / SpreadByPCPUs) and matched pods binding CPUs:
+    whole-CPU requests, the pods' required bind policies outside FullPCPUs (the refusal: preferredCPUs taken first may
+    split cores there), half of the queue matching the reservations of one of 8 owner groups."""
+    rng = np.random.default_rng(seed)
+    cl = synth.make_cluster(n, synth.BASE_SEED + seed, amplified_fraction=0.2)
+    zones, tabs = synth.make_numa_cpus(cl, synth.BASE_SEED + seed + 1, bind_weights=(0.6, 0.0, 0.4))
+    rs, al, res = synth.make_reservation_holdings(cl, synth.BASE_SEED + seed + 2, zones, tabs, None, frac=0.5)
+    cfg = synth.config(n)
+    ev, o = Evaluator(cfg), Oracle(cfg, n)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        synth.load_numa(h, zones)
+        synth.load_cpus(h, tabs)
+        h.reservations_load(rs, al, res)
+    pods = synth.make_numa_cpuset_pods(n_pods, synth.BASE_SEED + seed + 3, cpuset_fraction=0.5, policy_fraction=0.4)
+    pods["requests"][:, abi.RES_CPU] = np.maximum(1000, pods["requests"][:, abi.RES_CPU] // 1000 * 1000)
+    pods["limits"][:, abi.RES_CPU] = np.maximum(pods["limits"][:, abi.RES_CPU], pods["requests"][:, abi.RES_CPU])
+    pods["cpu_bind_required"][np.isin(pods["cpu_bind_required"], [abi.CPU_BIND_DEFAULT, abi.CPU_BIND_FULL_PCPUS])] = \
+        abi.CPU_BIND_SPREAD_BY_PCPUS
+    grp = rng.integers(0, 8, len(rs))
+    matches = [[] for _ in range(n_pods)]
+    ok = (pods["requests"][:, 2:] == 0).all(1) & (pods["has_other_requests"] == 0) & (pods["device_requests"] == 0).all(1)
+    for p in np.flatnonzero(ok & (rng.random(n_pods) < 0.5)):
+        pods["reservation_matched"][p] = abi.RSV_AFFINITY if rng.random() < affinity else abi.RSV_MATCHED
+        matches[p] = np.flatnonzero(grp == rng.integers(0, 8)).tolist()
+    return cl, ev, o, pods, matches, rs
+
+
+@pytest.mark.parametrize("seed,affinity", [(1421, 0.0), (1422, 0.5)], ids=["matched", "affinity"])
+def test_matched_binding_pods_numa_policy_parity(gpu, seed, affinity):
+    """Reservation-matched pods binding CPUs under NUMA policies on nodes of their reservations holding NUMA amounts /
+    cpusets: k_numa_views' views carry preferredCPUs (the hint view's mergedMatchedRemainCPUs, a trial's
+    mergedMatchedAllocatedCPUs + its remainedCPUs, a Restricted trial's remainedCPUs) -- per-view CPU availability,
+    trimNUMANodeResources, allocateCPUSet's take by counts -- and after the nomination the cpuset pass (k_rsv_views over
+    the allocation's zones) gives Reserve's cpuset and the Score's requested cpu (scoring.go:179-185).  Placements,
+    scores, NUMA allocations, cpusets and the reservation state bit-exact with the oracle (allocateCPUSet itself)."""
+    cl, ev, o, pods, matches, rs = numa_bind_matched_setup(300, seed, 250, affinity)
+    c1, s1 = ev.schedule(pods, synth.T0, matches=matches)
+    c0, s0 = o.schedule(pods, synth.T0, matches=matches)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5].ravel().tolist()
+    assert np.array_equal(s1, s0), np.argwhere(s1 != s0)[:5].ravel().tolist()
+    diff = np.argwhere(np.any(ev.last_numa_allocations != o.last_numa_allocations, axis=1))
+    assert len(diff) == 0, diff[:5].ravel().tolist()
+    diff = np.argwhere(np.any(ev.last_cpusets != o.last_cpusets, axis=1))
+    assert len(diff) == 0, diff[:5].ravel().tolist()
+    _holdings_equal(ev, o)
+    a1 = ev.last_allocations()
+    pol = cl.nodes["numa_topology_policy"] != 0
+    m = np.flatnonzero(pods["reservation_matched"] != 0)
+    into = [p for p in m if a1["reservation"][p] > 0 and c1[p] >= 0 and (pol[c1[p]] or pods["numa_topology_policy"][p])
+            and a1["cpuset"][p].any() and ev.last_numa_allocations[p].any()]
+    assert len(into) >= 10  # binding pods given cpusets and NUMA allocations out of holding reservations
+    assert ev.check_records(synth.T0) == 0
+
+
+def test_matched_binding_pod_full_pcpus_refused(gpu):
+    """A matched pod under a required FullPCPUs policy (its own, or the node's FullPCPUsOnly) beside a reservation
+    holding NUMA amounts / CPUs under a NUMA policy: KE_ERR_UNSUPPORTED from both (preferredCPUs taken first may
+    split cores there, which the per-view counts do not see)."""
+    cl, ev, o, pods, matches, rs = numa_bind_matched_setup(300, 1423, 60, 0.0)
+    pol = cl.nodes["numa_topology_policy"] != 0
+    holding = [r for r in range(len(rs)) if pol[rs["node"][r]] and rs["holds"][r] & (abi.RSV_HOLDS_NUMA | abi.RSV_HOLDS_CPUSET)
+               and rs["available"][r]]
+    assert holding
+    bad = pods[:1].copy()
+    bad["priority_class"], bad["qos_class"] = abi.PRIORITY_PROD, abi.QOS_LSR
+    bad["requests"][0, :] = 0
+    bad["requests"][0, abi.RES_CPU], bad["requests"][0, abi.RES_MEMORY] = 2000, 2**30
+    bad["cpu_bind_required"], bad["cpu_bind_preferred"] = abi.CPU_BIND_FULL_PCPUS, abi.CPU_BIND_FULL_PCPUS
+    bad["has_other_requests"], bad["device_requests"] = 0, 0
+    bad["reservation_matched"] = abi.RSV_MATCHED
+    with pytest.raises(KoordEvalError) as e:
+        ev.schedule(bad, synth.T0, matches=[[holding[0]]])
+    assert e.value.code == abi.ERR_UNSUPPORTED
+    with pytest.raises(RuntimeError, match=f"rc={abi.ERR_UNSUPPORTED}"):
+        o.schedule(bad, synth.T0, matches=[[holding[0]]])
+
+
+def test_numa_policy_golden_cases_through_schedule(gpu):
+    """TestPlugin_Reserve's NUMA-policy cases (plugin_test.go:1268-1398, tests/golden/reservation_restore.json) as
+    whole scheduling cycles of the matched pod on the test's node -- the binding pod's (preferring FullPCPUs)
+    included: GPU and oracle agree on placement, score, cpuset, NUMA allocation and reservation state; the binding
+    Restricted case takes the test's cpus 4-7 and 4 cpu on NUMA node 0 (:1268-1297)."""
+    from test_reservations import POLICY, _reserve_node, policy_reservation, policy_pod, _cpus
+    for case in POLICY:
+        hs = [_reserve_node(case, 1391, Evaluator(synth.config(1))), _reserve_node(case, 1391)]
+        r, a = policy_reservation(case)
+        pods = np.array([policy_pod(case)])
+        pods["reservation_matched"] = abi.RSV_AFFINITY if case["required"] else abi.RSV_MATCHED
+        out = []
+        for h in hs:
+            h.reservations_load(r, a)
+            c, s = h.schedule(pods, synth.T0, matches=[[0]])
+            out.append((c, s, h.last_cpusets.copy(), h.last_numa_allocations.copy(), h.last_allocations()["reservation"]))
+        for x, y in zip(*out):
+            assert np.array_equal(x, y), case["name"]
+        if case["name"] == "numa_cpuset_restricted":
+            c, s, cpus, numa, into = out[0]
+            assert c[0] == 0 and into[0] == 1
+            assert np.array_equal(cpus[0], _cpus(case["want_cpus"]))
+            assert numa[0][0] == 4000 and not numa[0][1:].any()

@@ -174,6 +174,7 @@ def test_matched_refusals_precede_every_segment():
     pods["qos_class"] = abi.QOS_LS
     pods["reservation_matched"][4] = abi.RSV_MATCHED
     pods["qos_class"][4], pods["priority_class"][4] = abi.QOS_LSR, abi.PRIORITY_PROD  # binds CPUs
+    pods["cpu_bind_required"][4] = abi.CPU_BIND_FULL_PCPUS  # under a required FullPCPUs policy: refused
     pods["requests"][4, abi.RES_CPU] = pods["limits"][4, abi.RES_CPU] = 2000
     with pytest.raises(KoordEvalError) as e:
         ev.schedule(pods, synth.T0, matches=[[], [], [], [], [0, 1], []])

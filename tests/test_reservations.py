@@ -387,7 +387,7 @@ def test_numa_reserve_from_reservation_golden(case):
     assert np.array_equal(cpus, _cpus(case["want_cpus"]))
 
 
-def _reserve_node(case, seed):
+def _reserve_node(case, seed, h=None):
     """One node as TestPlugin_Reserve builds it (plugin_test.go:1436-1494): allocatable 96 cpu / 512Gi, a CPU table of
     buildCPUTopologyForTest(sockets, nodes/socket, cores/node, threads/core) with the reservation's remainedCPUs under
     its UID (MaxRefCount 1), NUMA zones of CPUsPerNode cpu each (no memory key) holding the reserve pod's NUMA amounts."""
@@ -401,7 +401,7 @@ def _reserve_node(case, seed):
     cl.nodes["cpu_bind_policy"][0] = 0
     cl.nodes["numa_topology_policy"][0] = 0
     cl.nodes["cpu_amplification_ratio"][0] = 0
-    o = Oracle(synth.config(1), 1)
+    o = Oracle(synth.config(1), 1) if h is None else h
     synth.load_into(o, cl)
     t = np.zeros(n_cpu, abi.CPU_DTYPE)
     t["cpu_id"] = np.arange(n_cpu)
@@ -427,6 +427,21 @@ def test_numa_reserve_from_reservation_policy_golden(case):
     tryAllocateFromReservation: the Restricted second Allocate over requiredResources = remained) in the oracle against
     TestPlugin_Reserve's cases (plugin_test.go:1268-1398): code, cpuset and NUMA allocation."""
     o = _reserve_node(case, 1391)
+    r, a = policy_reservation(case)
+    o.reservations_load(r, a)
+    pod = policy_pod(case)
+    code, dist, cpus = o.numa_reserve_policy(pod, 0, [0], 0, case["required"], case["affinity_mask"])
+    assert code == case["want_code"]
+    if code >= 0:
+        assert np.array_equal(cpus, _cpus(case["want_cpus"]))
+        want = np.zeros(16, np.int64)
+        for k, v in case["want_numa"].items():
+            want[2 * int(k)] = v
+        assert np.array_equal(dist, want), dist.tolist()
+
+
+def policy_reservation(case):
+    """The reservation of a TestPlugin_Reserve NUMA-policy case: its reserve pod's remainedCPUs and NUMA amounts"""
     r = np.zeros(1, abi.RESERVATION_DTYPE)
     a = np.zeros(1, abi.RESERVATION_ALLOC_DTYPE)
     r["available"], r["allocate_policy"] = 1, case["policy"]
@@ -441,7 +456,11 @@ def test_numa_reserve_from_reservation_policy_golden(case):
         if case["remained"] is not None:
             a["owner_numa"][0, 2 * int(k)] = v - case["remained"].get(k, 0)
     r["holds"] = holds
-    o.reservations_load(r, a)
+    return r, a
+
+
+def policy_pod(case):
+    """Its pod: 4 CPUs, an LSR pod preferring FullPCPUs (bind) or an LS pod, under a Restricted NUMA policy"""
     pod = synth.make_pods(1, synth.BASE_SEED + 1392)[0].copy()
     pod["requests"][:] = 0
     pod["limits"][:] = 0
@@ -453,14 +472,7 @@ def test_numa_reserve_from_reservation_policy_golden(case):
         pod["priority_class"], pod["qos_class"] = abi.PRIORITY_PROD, abi.QOS_LS
     pod["has_other_requests"], pod["device_requests"] = 0, 0
     pod["numa_topology_policy"] = abi.NUMA_POLICY_RESTRICTED
-    code, dist, cpus = o.numa_reserve_policy(pod, 0, [0], 0, case["required"], case["affinity_mask"])
-    assert code == case["want_code"]
-    if code >= 0:
-        assert np.array_equal(cpus, _cpus(case["want_cpus"]))
-        want = np.zeros(16, np.int64)
-        for k, v in case["want_numa"].items():
-            want[2 * int(k)] = v
-        assert np.array_equal(dist, want), dist.tolist()
+    return pod
 
 
 IGNORED = json.load(open(os.path.join(HERE, "golden", "reservation_restore.json")))["ignored_cases"]
@@ -743,3 +755,20 @@ def test_numa_score_error_fails_the_pod(order2, placed):
         ev.schedule(pods, synth.T0, matches=[[0, 1]])
     assert e.value.code == abi.ERR_NO_DEVICE
     ev.close()
+
+
+def test_numa_policy_binding_case_through_schedule():
+    """TestPlugin_Reserve's binding Restricted case (plugin_test.go:1268-1297) as a whole scheduling cycle in the
+    oracle: the matched pod (preferring FullPCPUs, Restricted NUMA policy, reservation affinity) is placed into the
+    reservation with cpus 4-7 and 4 cpu on NUMA node 0 (the GPU twin:
+    test_gpu_reservation_holdings.py::test_numa_policy_golden_cases_through_schedule)."""
+    case = next(c for c in POLICY if c["name"] == "numa_cpuset_restricted")
+    o = _reserve_node(case, 1391)
+    r, a = policy_reservation(case)
+    o.reservations_load(r, a)
+    pods = np.array([policy_pod(case)])
+    pods["reservation_matched"] = abi.RSV_AFFINITY
+    c, _ = o.schedule(pods, synth.T0, matches=[[0]])
+    assert c.tolist() == [0] and o.last_allocations()["reservation"].tolist() == [1]
+    assert np.array_equal(o.last_cpusets[0], _cpus(case["want_cpus"]))
+    assert o.last_numa_allocations[0][0] == 4000 and not o.last_numa_allocations[0][1:].any()
