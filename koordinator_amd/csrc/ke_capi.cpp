@@ -966,12 +966,21 @@ static int schedule_sync(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_
         rc = device_rsv_views(&c, pods[s0], now_ns, c.rsv_views, c.rsv_view_out);
         if (rc) return resv_ignore_end(c), rc;
       }
+      if (!c.numa_views.empty()) {  // NUMA policies: the hints over tryAllocateIgnoreReservation (k_numa_views)
+        rc = device_numa_views(&c, pods[s0], now_ns, c.numa_views, c.numa_view_out);
+        if (rc) return resv_ignore_end(c), rc;
+      }
       resv_ds_views(c, pods[s0], nullptr, 0);  // DeviceShare's ignore / own views (k_ds_views)
       if (!c.ds_views.empty()) {
         rc = device_ds_views(&c, pods[s0], now_ns, c.ds_views, c.ds_view_out);
         if (rc) return resv_ignore_end(c), rc;
       }
       resv_ignore_ovr(c);
+      if (!c.numa_cs_views.empty()) {  // its cpuset and Score on the Filter's affinity
+        rc = device_rsv_views(&c, pods[s0], now_ns, c.numa_cs_views, c.numa_cs_out);
+        if (rc) return resv_ignore_end(c), rc;
+        resv_numa_cs_apply(c);
+      }
     }
     if (rsv) {
       const int32_t* ids = mids.data() + moff[(size_t)s0];

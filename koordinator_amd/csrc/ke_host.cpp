@@ -937,8 +937,18 @@ int resv_ignore_check(const Context& c, const ke_pod& pod, uint32_t pod_flags) {
     if (c.resv_holds[i] & KE_RSV_HOLDS_DEVICES)
       dev_on_policy = dev_on_policy || c.nodes[(size_t)c.resv[i].node].node.numa_topology_policy != KE_NUMA_POLICY_NONE;
   const bool ds = (pod_flags & (PF_DS | PF_DS_HINT)) != 0;
+  // a binding pod under a NUMA policy beside held NUMA resources / CPUs: tryAllocateIgnoreReservation in its hints
+  // (k_numa_views, resv_ignore_views) -- not with fractional CPUs or a required FullPCPUs binding (the pod's, or a
+  // FullPCPUsOnly node's among the holding ones: preferredCPUs taken first may split cores)
+  const int preq = pf_cpu_required(pod_flags);
+  bool full_req = preq == XB_FULL;
+  for (size_t i = 0; preq == XB_NONE && i < c.resv_holds.size(); i++)
+    if ((c.resv_holds[i] & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)) &&
+        c.nodes[(size_t)c.resv[i].node].node.cpu_bind_policy == KE_NODE_CPU_BIND_FULL_PCPUS_ONLY)
+      full_req = true;
+  const bool pol_here = (numa_cpu && pod.numa_topology_policy != KE_NUMA_POLICY_NONE) || on_policy_node;
   if ((dev && ds && ((pod_flags & PF_DS_HINT) || pod.numa_topology_policy != KE_NUMA_POLICY_NONE || dev_on_policy)) ||
-      (binds && ((numa_cpu && pod.numa_topology_policy != KE_NUMA_POLICY_NONE) || on_policy_node)))
+      (binds && pol_here && (!(pod_flags & PF_CPU_INT) || full_req)))
     return fail(KE_ERR_UNSUPPORTED, "a reservation-ignored pod reading resources a reservation holds "
                                     "(tryAllocateIgnoreReservation's remainder)");
   return KE_OK;
@@ -964,6 +974,13 @@ void resv_ignore_end(Context& c) {
   c.ds_views.clear();
   c.ds_view_resv.clear();
   c.ds_view_out.clear();
+  c.numa_views.clear();
+  c.numa_view_ids.clear();
+  c.numa_view_out.clear();
+  c.numa_cs_views.clear();
+  c.numa_cs_ovr.clear();
+  c.numa_cs_pair.clear();
+  c.numa_cs_out.clear();
   for (size_t node = 0; node < c.resv_by_node.size(); node++)
     if (!c.resv_by_node[node].empty()) resv_node_restore(c, (int32_t)node);
 }
@@ -985,16 +1002,45 @@ bool resv_ignore_needs_views(const Context& c, const ke_pod& pod, uint32_t pod_f
 // on every node without a NUMA policy whose usable reservations hold NUMA resources or CPUs (RestoreReservation's
 // matched set), one allocation with reservedCPUsFromIgnored = their allocatable CPUs (mergedMatchedAllocatedCPUs,
 // the remainedCPUs inside them) preferred and no required resources
+// Under a NUMA policy (the pod's or the node's) the same allocation is every mask's Allocate of its hints: one
+// k_numa_views set per such node (resv_ignore_ovr: the Filter, and the cpuset pass for Score / Reserve) -- the trial
+// prefers reservedCPUsFromIgnored, the hint view mergedMatchedRemainCPUs, and the reusable amounts are the rows' own
+// (the ignored restore, resv_plugin_restore).
 void resv_ignore_views(Context& c, const ke_pod& pod) {
   c.rsv_views.clear();
   c.rsv_view_resv.clear();
   c.rsv_view_out.clear();
+  c.numa_views.clear();
+  c.numa_view_ids.clear();
+  c.numa_view_out.clear();
   if (c.resv_alloc.empty()) return;
   const DevPod dp = make_dev_pod(c.cfg, pod, pod_hints(c, pod), &c.tmpl);
   for (size_t node = 0; node < c.resv_by_node.size(); node++) {
     if (c.resv_by_node[node].empty()) continue;
     const NodeState& ns = c.nodes[node];
-    if (ns.node.numa_topology_policy != KE_NUMA_POLICY_NONE || !pod_binds_on(dp, ns) || !cpus_valid(ns)) continue;
+    if (!pod_binds_on(dp, ns) || !cpus_valid(ns)) continue;
+    if (ns.node.numa_topology_policy != KE_NUMA_POLICY_NONE || pod.numa_topology_policy != KE_NUMA_POLICY_NONE) {
+      std::vector<int32_t> mine;
+      for (int32_t i : c.resv_by_node[node])
+        if (resv_usable(c.resv[(size_t)i]) && resv_holds_cpu(c, i)) mine.push_back(i);
+      if (mine.empty()) continue;
+      c.numa_views.emplace_back();
+      NumaRsvView& v = c.numa_views.back();
+      std::memset(&v, 0, sizeof v);
+      v.node = (int32_t)node;
+      v.n = 1;
+      v.required = 1;  // tryAllocateIgnoreReservation's status: no allocation from the node besides it
+      for (const ke_numa_zone& z : ns.zones)
+        if (z.id >= 0 && z.id < KE_MAX_NUMA && (z.has_allocated & KE_NUMA_ALLOC_ENTRY)) v.entry |= 1u << z.id;
+      for (int32_t i : mine)
+        for (int w = 0; w < 4; w++) {
+          const ke_reservation_alloc& a = c.resv_alloc[(size_t)i];
+          v.pref[NV_MAX][w] |= a.cpuset[w] & ~a.owner_cpuset[w];  // mergedMatchedRemainCPUs
+          v.pref[0][w] |= a.cpuset[w];                            // reservedCPUsFromIgnored
+        }
+      c.numa_view_ids.push_back({-2});
+      continue;
+    }
     RsvView v{};
     bool any = false;
     for (int32_t i : c.resv_by_node[node])
@@ -1034,6 +1080,43 @@ void resv_ignore_ovr(Context& c) {
     o.filter = o.reserve = (int8_t)(ok ? 1 : 2);
     if (ok)
       for (int w = 0; w < 4; w++) o.cpus[w] = c.rsv_view_out[q].cpus[w];
+  }
+  // NodeNUMAResource under a NUMA policy: the Filter's outcome over tryAllocateIgnoreReservation, then the cpuset pass
+  // (k_rsv_views over the allocation's zones) for Reserve's cpuset and the Score (resv_numa_cs_apply)
+  c.numa_cs_views.clear();
+  c.numa_cs_ovr.clear();
+  c.numa_cs_pair.clear();
+  c.numa_cs_out.clear();
+  for (size_t q = 0; q < c.numa_views.size() && q < c.numa_view_out.size(); q++) {
+    const NumaRsvOut& r = c.numa_view_out[q];
+    const NumaRsvView& nv = c.numa_views[q];
+    RsvOvr& o = ovr_of(nv.node);
+    o.numa_on = 1;
+    o.numa_st = (uint8_t)r.st;
+    o.numa_reason = (uint8_t)r.reason;
+    o.numa_aff = (uint8_t)r.aff;
+    std::memcpy(o.numa_dist, r.dist[0], sizeof o.numa_dist);
+    if (r.st != KE_CODE_SUCCESS) continue;
+    if (!(r.ok & 1u)) {  // (the Filter's Allocate on the affinity succeeded: not reached)
+      o.numa_st = KE_CODE_UNSCHEDULABLE;
+      o.numa_reason = KE_REASON_NUMA_INSUFFICIENT_CPUS;
+      continue;
+    }
+    RsvView v{};
+    v.node = nv.node;
+    for (int w = 0; w < 4; w++) v.pref[w] = v.pref2[w] = nv.pref[0][w];
+    for (int z = 0; z < 8; z++)
+      if (r.dist[0][2 * z] != 0 || r.dist[0][2 * z + 1] != 0) {
+        v.zmask |= 1 << z;
+        v.zcpu[z] = r.dist[0][2 * z];
+      }
+    v.score_on = 1;
+    v.sreq1 = r.sreq1[0];
+    v.salloc[0] = r.salloc[0][0];
+    v.salloc[1] = r.salloc[0][1];
+    c.numa_cs_views.push_back(v);
+    c.numa_cs_ovr.push_back((int32_t)(&o - c.rsv_ovr.data()));
+    c.numa_cs_pair.push_back(-1);
   }
   for (size_t q = 0; q < c.ds_views.size() && q < c.ds_view_out.size(); q++) {
     RsvOvr& o = ovr_of(c.ds_views[q].node);
@@ -1357,7 +1440,8 @@ void resv_numa_cs_apply(Context& c) {
       for (int w = 0; w < 4; w++) o.cpus[w] = c.numa_cs_out[j].cpus[w];
     } else {  // (the Filter's counts admitted the trial: not reached while they agree with allocateCPUSet)
       o.reserve = 2;
-      if (o.numa_st == KE_CODE_SUCCESS) c.rsv_pairs[(size_t)c.numa_cs_pair[j]].allowed |= RSV_PAIR_SCORE_ERROR;
+      if (c.numa_cs_pair[j] < 0) o.numa_st = KE_CODE_UNSCHEDULABLE, o.numa_reason = KE_REASON_NUMA_INSUFFICIENT_CPUS;
+      else if (o.numa_st == KE_CODE_SUCCESS) c.rsv_pairs[(size_t)c.numa_cs_pair[j]].allowed |= RSV_PAIR_SCORE_ERROR;
     }
   }
   c.numa_cs_views.clear();

@@ -1254,6 +1254,17 @@ static int numa_rsv_matched(const or_cluster* c, int32_t node, int32_t* ids) {
   return n;
 }
 
+/* the set a reservation-ignored pod sees there (every reservation matchedOrIgnored, transformer.go:101-106): the
+ * usable reservations on `node` holding NUMA resources or a cpuset, ascending index */
+static int numa_rsv_ignored(const or_cluster* c, int32_t node, int32_t* ids) {
+  int n = 0;
+  for (int32_t r = 0; c->ralloc && r < c->n_resv; r++)
+    if (c->resv[r].node == node && or_resv_usable(&c->resv[r]) &&
+        (or_holds_of_idx(c, r) & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)) && n < 64)
+      ids[n++] = r;
+  return n;
+}
+
 static int numa_any(const int64_t* v16) {
   for (int j = 0; j < KE_MAX_NUMA * KE_NRES; j++)
     if (v16[j]) return 1;
@@ -1295,6 +1306,20 @@ static void numa_opt_hint(const or_cluster* c, const int32_t* M, int nM, numa_op
     uint64_t rc[ACC_WORDS];
     cpus_remained(a, rc);
     for (int w = 0; w < ACC_WORDS; w++) o->pref[w] |= rc[w];
+  }
+}
+/* A reservation-ignored pod's options: the hint view's preferredCPUs mergedMatchedRemainCPUs; tryAllocateIgnoreReservation
+ * (reservation.go:437-490) prefers reservedCPUsFromIgnored = mergedMatchedAllocatedCPUs (the reserve pods' CPUs) ∪ Σ
+ * remainedCPUs.  Their reusable amounts (mergedMatchedAllocatable; mergedMatchedAllocated + Σ remained, equal in value)
+ * are the node's restore state already (or_numa_ignored_reusable): none added here. */
+static void numa_opt_ign(const or_cluster* c, const int32_t* M, int nM, int hint, numa_opt* o) {
+  memset(o, 0, sizeof *o);
+  o->has_pref = 1;
+  for (int q = 0; q < nM; q++) {
+    const ke_reservation_alloc* a = &c->ralloc[M[q]];
+    uint64_t rc[ACC_WORDS];
+    cpus_remained(a, rc);
+    for (int w = 0; w < ACC_WORDS; w++) o->pref[w] |= hint ? rc[w] : (a->cpuset[w] | rc[w]);
   }
 }
 /* tryAllocateFromReservation's options for reservation r (reservation.go:293-311): reusable = mergedUnmatchedUsed +
@@ -1393,6 +1418,11 @@ static int numa_from_rsv_try(const or_cluster* c, const ke_pod* pod, int32_t nod
  * reservations, else (no reservation affinity) from the node.  1 = a hint / allocation, 0 = none. */
 static int numa_matched_alloc_ok(const or_cluster* c, const ke_pod* pod, int32_t node, const int32_t* M, int nM,
                                  uint32_t mask) {
+  if (c->ignored) {  /* tryAllocateIgnoreReservation: its status, no fallback (reservation.go:282-284) */
+    numa_opt o;
+    numa_opt_ign(c, M, nM, 0, &o);
+    return numa_alloc_try(c, &c->nodes[node], pod, mask, &o, NULL, NULL);
+  }
   const int required = pod->reservation_matched == KE_RSV_AFFINITY;
   const int r = numa_from_rsv_try(c, pod, node, M, nM, M, nM, mask, required, NULL, NULL, NULL);
   if (r != 0) return r > 0;
@@ -1405,6 +1435,10 @@ static int numa_matched_alloc_ok(const or_cluster* c, const ke_pod* pod, int32_t
  * error status (no nominated reservation under an affinity; the reservation's or the node's Allocate failed). */
 static int numa_matched_alloc(const or_cluster* c, const ke_pod* pod, int32_t node, const int32_t* M, int nM,
                               int32_t nom, uint32_t aff, numa_opt* used, int64_t* dist16, uint64_t* cpus) {
+  if (c->ignored) {  /* allocateWithNominatedReservation of an ignored pod: tryAllocateIgnoreReservation (:504-506) */
+    numa_opt_ign(c, M, nM, 0, used);
+    return numa_alloc_try(c, &c->nodes[node], pod, aff, used, dist16, cpus);
+  }
   const int required = pod->reservation_matched == KE_RSV_AFFINITY;
   if (nom < 0 && required) return 0; /* "no nominated reservation" */
   int in = 0;
@@ -1669,11 +1703,15 @@ static int numa_admit(const or_cluster* c, const or_node* nd, const ke_pod* pod,
    * reusable, mergedMatchedRemainCPUs preferred) and every mask's Allocate from the reservations first */
   const int32_t node = (int32_t)(nd - c->nodes);
   int32_t M[64];
-  const int nM = c->resv_m && !c->ignored ? numa_rsv_matched(c, node, M) : 0;
+  /* a reservation-ignored pod binding CPUs: the hint view prefers the held remainedCPUs, every mask's Allocate is
+   * tryAllocateIgnoreReservation (a pod binding none reads the held amounts as reusable only: its rows) */
+  const int nM = c->resv_m && !c->ignored ? numa_rsv_matched(c, node, M)
+                 : c->ignored && cs && cs->rcb ? numa_rsv_ignored(c, node, M) : 0;
   numa_opt oh;
   numa_cs cs_h;
   if (nM > 0) {
-    numa_opt_hint(c, M, nM, &oh);
+    if (c->ignored) numa_opt_ign(c, M, nM, 1, &oh);
+    else numa_opt_hint(c, M, nM, &oh);
     numa_cs_build_pref(c, nd, pod, &cs_h, oh.pref);
     cs = &cs_h;
   }
@@ -1892,12 +1930,15 @@ static int64_t numa_score_ex(const or_cluster* c, const ke_pod* pod, int32_t nod
   const int policy = effective_policy(n, pod, &exclusive);
   if (policy < 0) return 0;
   int32_t M[64];
-  const int nM = policy != KE_NUMA_POLICY_NONE && c->resv_m && !c->ignored && c->numa_nom ? numa_rsv_matched(c, node, M) : 0;
+  numa_cs cs;
+  numa_cs_build(c, n, pod, &cs);
+  const int nM = policy == KE_NUMA_POLICY_NONE ? 0
+                 : c->resv_m && !c->ignored && c->numa_nom ? numa_rsv_matched(c, node, M)
+                 : c->ignored && cs.rcb ? numa_rsv_ignored(c, node, M) : 0;
   if (nM > 0) {
     /* a matched pod on a node of its reservations holding NUMA resources / CPUs: the allocation from the nominated
-     * reservation (else the node) on the stored affinity, calculateAllocatableAndRequested with the options it used */
-    numa_cs cs;
-    numa_cs_build(c, n, pod, &cs);
+     * reservation (else the node) on the stored affinity, calculateAllocatableAndRequested with the options it used;
+     * an ignored binding pod: tryAllocateIgnoreReservation's */
     if (cs.rcb && !cs.valid) return 0;
     uint32_t aff = 0;
     int reason;
@@ -1905,7 +1946,7 @@ static int64_t numa_score_ex(const or_cluster* c, const ke_pod* pod, int32_t nod
     numa_opt used;
     int64_t dist16[2 * KE_MAX_NUMA];
     uint64_t pcpus[ACC_WORDS];
-    if (!numa_matched_alloc(c, pod, node, M, nM, c->numa_nom[node], aff, &used, dist16, pcpus)) {
+    if (!numa_matched_alloc(c, pod, node, M, nM, c->ignored ? -1 : c->numa_nom[node], aff, &used, dist16, pcpus)) {
       if (err) *err = 1;
       return 0;
     }
@@ -4344,11 +4385,12 @@ static int or_reserve_plan(const or_cluster* c, const ke_pod* pod, int32_t node,
       if (fr > 0) return 0;
     }
   }
-  if (c->resv_m && !c->ignored && policy > KE_NUMA_POLICY_NONE && n->n_zone > 0) {
+  if (((c->resv_m && !c->ignored) || (c->ignored && cs.rcb)) && policy > KE_NUMA_POLICY_NONE && n->n_zone > 0) {
     /* a matched pod on a node of its reservations holding NUMA resources / CPUs (plugin.go:552-566):
-     * allocateWithNominatedReservation, else tryAllocateFromNode, on the stored affinity */
+     * allocateWithNominatedReservation, else tryAllocateFromNode, on the stored affinity; an ignored binding pod
+     * beside held NUMA resources / CPUs: tryAllocateIgnoreReservation */
     int32_t M[64];
-    const int nM = numa_rsv_matched(c, node, M);
+    const int nM = c->ignored ? numa_rsv_ignored(c, node, M) : numa_rsv_matched(c, node, M);
     if (nM > 0) {
       uint32_t aff = 0;
       int reason;
@@ -5334,7 +5376,18 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
         cpuset_state cst;
         cpuset_prefilter(c, &pods[p], &cst);
         const int binds = cst.rcb || cst.invalid || (node_bind && pods[p].requests[KE_RES_CPU] > 0);
-        if ((dev && !d.skip && (d.h || pod_pol || dev_on_policy)) || (binds && ((numa_cpu && pod_pol) || on_policy)))
+        /* a binding pod under a NUMA policy beside held NUMA resources / CPUs: tryAllocateIgnoreReservation in its
+         * hints (numa_admit) -- refused as for matched pods with fractional CPUs or a required FullPCPUs binding
+         * (the pod's, or a FullPCPUsOnly node's among those) */
+        int full_req = cst.required == KE_CPU_BIND_FULL_PCPUS;
+        for (int32_t r = 0; cst.required != KE_CPU_BIND_FULL_PCPUS && cst.required != KE_CPU_BIND_SPREAD_BY_PCPUS &&
+                            r < c->n_resv; r++)
+          if ((or_holds_of(&c->ralloc[r]) & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET)) &&
+              c->nodes[c->resv[r].node].node.cpu_bind_policy == KE_NODE_CPU_BIND_FULL_PCPUS_ONLY)
+            full_req = 1;
+        const int pol_here = (numa_cpu && pod_pol) || on_policy;
+        if ((dev && !d.skip && (d.h || pod_pol || dev_on_policy)) ||
+            (binds && pol_here && (pods[p].requests[KE_RES_CPU] % 1000 != 0 || full_req)))
           return KE_ERR_UNSUPPORTED;
       }
       continue;

@@ -169,8 +169,8 @@ def test_ignored_pods_beside_held_cpusets(gpu):
     policies), between cpuset pods and matched cpuset pods: every reservation's matched restore for them; an ignored
     cpuset pod allocates on a node with held CPUs through tryAllocateIgnoreReservation (one trial with every held
     CPU preferred, k_rsv_views; a failed trial fails Filter and Reserve), elsewhere from the node -- placements,
-    scores, cpusets and reservation state bit-exact with the oracle.  An ignored pod with a NUMA policy is refused by
-    both (the held NUMA amounts of its hints are not restated)."""
+    scores, cpusets and reservation state bit-exact with the oracle.  An ignored pod with a NUMA policy under a required
+    FullPCPUs binding is refused by both (preferredCPUs taken first may split cores)."""
     ev, o, pods, matches, rs = cpuset_matched_setup(300, 1371, 300, affinity=0.0, node_bind=False)
     cs = np.isin(pods["qos_class"], [abi.QOS_LSE, abi.QOS_LSR]) & (pods["priority_class"] == abi.PRIORITY_PROD)
     free = np.flatnonzero(pods["reservation_matched"] == abi.RSV_NONE)
@@ -194,6 +194,7 @@ def test_ignored_pods_beside_held_cpusets(gpu):
     bad = synth.make_cpuset_pods(4, synth.BASE_SEED + 1375, cpuset_fraction=1.0, key_base=7_900_000_000)
     bad["reservation_matched"][1] = abi.RSV_IGNORED
     bad["numa_topology_policy"][1] = abi.NUMA_POLICY_BEST_EFFORT
+    bad["cpu_bind_required"][1] = abi.CPU_BIND_FULL_PCPUS
     with pytest.raises(KoordEvalError) as e:
         ev.schedule(bad, synth.T0)
     assert e.value.code == abi.ERR_UNSUPPORTED
@@ -471,3 +472,43 @@ def test_numa_policy_golden_cases_through_schedule(gpu):
             assert c[0] == 0 and into[0] == 1
             assert np.array_equal(cpus[0], _cpus(case["want_cpus"]))
             assert numa[0][0] == 4000 and not numa[0][1:].any()
+
+
+@pytest.mark.parametrize("seed", [1431, 1432])
+def test_ignored_binding_pods_numa_policy_parity(gpu, seed):
+    """Reservation-ignored pods binding CPUs under NUMA policies (the node's or their own) beside reservations holding
+    NUMA amounts / cpusets: every mask's Allocate in their hints is tryAllocateIgnoreReservation (reservation.go:437-490:
+    reservedCPUsFromIgnored preferred, the held amounts reusable), the hint view prefers mergedMatchedRemainCPUs
+    (resource_manager.go:130-138); Score and Reserve from the same allocation (k_numa_views with one trial, then the
+    cpuset pass).  Placements, scores, NUMA allocations, cpusets and reservation state bit-exact with the oracle."""
+    n = 300
+    rng = np.random.default_rng(seed)
+    cl = synth.make_cluster(n, synth.BASE_SEED + seed, amplified_fraction=0.2)
+    zones, tabs = synth.make_numa_cpus(cl, synth.BASE_SEED + seed + 1, bind_weights=(0.6, 0.0, 0.4))
+    rs, al, res = synth.make_reservation_holdings(cl, synth.BASE_SEED + seed + 2, zones, tabs, None, frac=0.5)
+    cfg = synth.config(n)
+    ev, o = Evaluator(cfg), Oracle(cfg, n)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        synth.load_numa(h, zones)
+        synth.load_cpus(h, tabs)
+        h.reservations_load(rs, al, res)
+    pods = synth.make_numa_cpuset_pods(250, synth.BASE_SEED + seed + 3, cpuset_fraction=0.5, policy_fraction=0.4)
+    pods["requests"][:, abi.RES_CPU] = np.maximum(1000, pods["requests"][:, abi.RES_CPU] // 1000 * 1000)
+    pods["limits"][:, abi.RES_CPU] = np.maximum(pods["limits"][:, abi.RES_CPU], pods["requests"][:, abi.RES_CPU])
+    pods["cpu_bind_required"][np.isin(pods["cpu_bind_required"], [abi.CPU_BIND_DEFAULT, abi.CPU_BIND_FULL_PCPUS])] = \
+        abi.CPU_BIND_SPREAD_BY_PCPUS
+    ign = np.flatnonzero((pods["device_requests"] == 0).all(1) & (rng.random(250) < 0.5))
+    pods["reservation_matched"][ign] = abi.RSV_IGNORED
+    assert_schedule_equal(ev, o, pods, synth.T0)
+    assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
+    assert np.array_equal(ev.last_cpusets, o.last_cpusets)
+    _holdings_equal(ev, o)
+    c, a = ev.last_allocations()["node"], ev.last_allocations()
+    pol = cl.nodes["numa_topology_policy"] != 0
+    held = np.zeros(n, bool)
+    held[rs["node"][(rs["holds"] & (abi.RSV_HOLDS_NUMA | abi.RSV_HOLDS_CPUSET)) != 0]] = True
+    on_held = [p for p in ign if c[p] >= 0 and held[c[p]] and (pol[c[p]] or pods["numa_topology_policy"][p])
+               and a["cpuset"][p].any()]
+    assert len(on_held) >= 10  # ignored binding pods given cpusets on policy nodes with held CPUs
+    assert ev.check_records(synth.T0) == 0
