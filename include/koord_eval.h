@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define KE_ABI_VERSION 12
+#define KE_ABI_VERSION 13
 #define KE_ABSENT (-1)
 
 typedef struct ke_ctx ke_ctx; /* one evaluator context (ke_create) */
@@ -296,7 +296,8 @@ typedef struct ke_numa_zone {
 #define KE_PDR_GPU_MEMORY_RATIO 6 /* koordinator.sh/gpu-memory-ratio */
 #define KE_PDR_RDMA 7             /* koordinator.sh/rdma         */
 #define KE_PDR_FPGA 8             /* koordinator.sh/fpga         */
-#define KE_PDR_COUNT 9
+#define KE_PDR_HYGON_DCU 9        /* dcu.com/gpu (a GPU: ConvertDeviceRequest's x100, utils.go:206-212) */
+#define KE_PDR_COUNT 10
 /* DeviceShareArgs.ScoringStrategy (types.go:263-275, v1beta3/defaults.go:218-242): weights indexed
  * gpu-memory-ratio, gpu-memory, rdma, fpga; KE_ABSENT = not in Resources. */
 #define KE_DSW_GPU_MEMORY_RATIO 0
@@ -554,7 +555,7 @@ typedef struct ke_pod {
   uint8_t has_resource_spec;          /* ResourceSpec annotation that failed to unmarshal (PreFilter Error) */
   uint8_t has_other_requests;         /* PodRequests has a non-zero resource outside KE_RES_*: 1 = each such name
                                          has a resource id (its request is a ke_pod.xres entry), 2 = some has none */
-  uint8_t has_unsupported_device_requests; /* Huawei NPU / Hygon DCU device resources: unsupported */
+  uint8_t has_unsupported_device_requests; /* Huawei NPU device resources: unsupported */
   int64_t device_requests[KE_PDR_COUNT]; /* PodRequests of the device resources (Value()), 0 = absent */
   int32_t numa_topology_policy; /* NUMATopologySpec annotation: KE_NUMA_POLICY_* (NONE = unset) */
   int32_t numa_exclusive;       /* NUMATopologySpec.SingleNUMANodeExclusive: KE_NUMA_EXCLUSIVE_* */
@@ -805,7 +806,9 @@ typedef struct ke_reservation_alloc {
   int64_t numa[KE_MAX_NUMA * KE_NRES];       /* the reserve pod's NUMANodeResources: [2*id + r], 0 = none    */
   int64_t owner_numa[KE_MAX_NUMA * KE_NRES]; /* Σ the owner pods' NUMANodeResources                            */
   uint64_t cpuset[4];                        /* the reserve pod's CPUSet (bit c = CPU id c)                    */
-  uint64_t owner_cpuset[4];                  /* ∪ the owner pods' CPUSets                                      */
+  uint64_t owner_cpuset[4];                  /* ∪ the owner pods' CPUSets, taken as disjoint: each CPU counts
+                                                one owner (owners sharing a CPU under MaxRefCount > 1 are
+                                                parity-unpinned: releasing one would free the CPU for both) */
   uint64_t device_minors;                    /* bit 16*type + minor: instances the reserve pod holds           */
   uint64_t owner_device_minors;              /* bit 16*type + minor: instances an owner pod holds              */
   int64_t device[KE_DEV_TYPES][KE_MAX_MINORS][KE_DKEYS];       /* the reserve pod's used per instance, 0 = none */

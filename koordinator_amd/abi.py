@@ -9,7 +9,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 ABSENT = -1
 
 OK = 0
@@ -89,10 +89,11 @@ DKEY_RDMA = DKEY_FPGA = 0
 DKEYS = 3
 PDR = {"nvidia.com/gpu": 0, "amd.com/gpu": 1, "koordinator.sh/gpu": 2, "koordinator.sh/gpu.shared": 3,
        "koordinator.sh/gpu-core": 4, "koordinator.sh/gpu-memory": 5, "koordinator.sh/gpu-memory-ratio": 6,
-       "koordinator.sh/rdma": 7, "koordinator.sh/fpga": 8}
-PDR_COUNT = 9
-# device resources the DeviceShare ABI does not model (utils.go:38-52): Huawei NPU, Hygon DCU
-UNSUPPORTED_DEVICE_RESOURCES = {"huawei.com/npu-core", "huawei.com/npu-cpu", "huawei.com/npu-dvpp", "dcu.com/gpu"}
+       "koordinator.sh/rdma": 7, "koordinator.sh/fpga": 8, "dcu.com/gpu": 9}
+PDR_COUNT = 10
+PDR_GPU = (0, 1, 2, 3, 4, 5, 6, 9)  # the GPU device type's names (DeviceResourceNames[GPU], utils.go:54-69)
+# device resources the DeviceShare ABI does not model (utils.go:38-52): Huawei NPU
+UNSUPPORTED_DEVICE_RESOURCES = {"huawei.com/npu-core", "huawei.com/npu-cpu", "huawei.com/npu-dvpp"}
 DSW_GPU_MEMORY_RATIO, DSW_GPU_MEMORY, DSW_RDMA, DSW_FPGA = 0, 1, 2, 3
 
 RES_CPU, RES_MEMORY, RES_BATCH_CPU, RES_BATCH_MEMORY, RES_MID_CPU, RES_MID_MEMORY = range(6)

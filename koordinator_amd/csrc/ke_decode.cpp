@@ -374,9 +374,8 @@ const char* const KE_RES_NAMES[KE_RES_COUNT] = {"cpu", "memory", "kubernetes.io/
 const char* const PDR_NAMES[KE_PDR_COUNT] = {"nvidia.com/gpu", "amd.com/gpu", "koordinator.sh/gpu",
                                              "koordinator.sh/gpu.shared", "koordinator.sh/gpu-core",
                                              "koordinator.sh/gpu-memory", "koordinator.sh/gpu-memory-ratio",
-                                             "koordinator.sh/rdma", "koordinator.sh/fpga"};
-const char* const UNSUPPORTED_DEVICE[] = {"huawei.com/npu-core", "huawei.com/npu-cpu", "huawei.com/npu-dvpp",
-                                          "dcu.com/gpu"};
+                                             "koordinator.sh/rdma", "koordinator.sh/fpga", "dcu.com/gpu"};
+const char* const UNSUPPORTED_DEVICE[] = {"huawei.com/npu-core", "huawei.com/npu-cpu", "huawei.com/npu-dvpp"};
 
 struct Container {
   RL req, lim;
@@ -708,7 +707,7 @@ int ke_decode_pod(const char* js, int64_t len, int32_t n_names, const char* cons
     const std::string* hs = lookup(ann, "scheduling.koordinator.sh/device-allocate-hint");
     if (hs) json::parse(hs->data(), hs->size(), hints, err);
     bool gpu = false;
-    for (int d = 0; d < 7; d++) gpu |= p.device_requests[d] > 0;
+    for (int d = 0; d < KE_PDR_COUNT; d++) gpu |= d != KE_PDR_RDMA && d != KE_PDR_FPGA && p.device_requests[d] > 0;
     const Value* types = v.field("deviceTypes");
     if (types && types->t == Value::ARR)
       for (const Value& t : types->a) {

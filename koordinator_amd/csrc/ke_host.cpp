@@ -216,7 +216,8 @@ bool selector_matches(const ke_label_selector& sel, const std::vector<std::pair<
 // types without an ApplyForAll hint, in annotation order
 static int joint_list(const ke_pod_device_hints& h, const ke_pod& p, int* out) {
   bool req[KE_DEV_TYPES] = {false, p.device_requests[KE_PDR_RDMA] > 0, p.device_requests[KE_PDR_FPGA] > 0};
-  for (int i = 0; i < KE_PDR_RDMA; i++) req[KE_DEV_GPU] = req[KE_DEV_GPU] || p.device_requests[i] > 0;
+  for (int i = 0; i < KE_PDR_COUNT; i++)
+    req[KE_DEV_GPU] = req[KE_DEV_GPU] || (i != KE_PDR_RDMA && i != KE_PDR_FPGA && p.device_requests[i] > 0);
   int n = 0;
   for (int j = 0; j < h.joint_n && j < KE_DEV_TYPES; j++) {
     const int t = h.joint_types[j];
@@ -485,7 +486,7 @@ int validate_pod(const ke_pod& p) {
     return fail(KE_ERR_INVALID, "pod CPU bind / exclusive policy");
   if (p.priority_class < 0 || p.priority_class > KE_PRIORITY_FREE) return fail(KE_ERR_INVALID, "priority class");
   if (p.has_unsupported_device_requests)
-    return fail(KE_ERR_UNSUPPORTED, "Huawei NPU / Hygon DCU device requests are not implemented");
+    return fail(KE_ERR_UNSUPPORTED, "Huawei NPU device requests are not implemented");
   for (int i = 0; i < KE_PDR_COUNT; i++)
     if (p.device_requests[i] < 0) return fail(KE_ERR_INVALID, "negative device request");
   if (p.numa_topology_policy < KE_NUMA_POLICY_NONE || p.numa_topology_policy > KE_NUMA_POLICY_SINGLE_NUMA_NODE)
@@ -1892,16 +1893,17 @@ static bool percentage_ok(int64_t q) { return !(q > 100 && q % 100 != 0); }  // 
 
 static bool ds_prepare(const ke_pod& pod, DevPod& d, const ke_pod_device_hints* h) {
   const int64_t* q = pod.device_requests;
-  bool nv = q[KE_PDR_NVIDIA_GPU] > 0, amd = q[KE_PDR_AMD_GPU] > 0, kg = q[KE_PDR_KOORD_GPU] > 0;
+  // NvidiaGPU / AMDGPU / HygonDCU: whole devices, ConvertDeviceRequest's x100 (utils.go:190-212)
+  bool nv = q[KE_PDR_NVIDIA_GPU] > 0, amd = q[KE_PDR_AMD_GPU] > 0, dcu = q[KE_PDR_HYGON_DCU] > 0, kg = q[KE_PDR_KOORD_GPU] > 0;
   bool sh = q[KE_PDR_GPU_SHARED] > 0, co = q[KE_PDR_GPU_CORE] > 0, me = q[KE_PDR_GPU_MEMORY] > 0,
        ra = q[KE_PDR_GPU_MEMORY_RATIO] > 0;
-  const int kinds = nv + amd + kg + (sh || co || me || ra);
+  const int kinds = nv + amd + dcu + kg + (sh || co || me || ra);
   if (kinds > 1) return false;  // no ValidDeviceResourceCombinations entry mixes these
   int64_t core = 0, mem = 0, ratio = 0;
   bool h_core = false, h_mem = false, h_ratio = false, any_gpu = true;
   int64_t n = 1;
-  if (nv || amd) {
-    core = ratio = 100 * q[nv ? KE_PDR_NVIDIA_GPU : KE_PDR_AMD_GPU];
+  if (nv || amd || dcu) {
+    core = ratio = 100 * q[nv ? KE_PDR_NVIDIA_GPU : amd ? KE_PDR_AMD_GPU : KE_PDR_HYGON_DCU];
     h_core = h_ratio = true;
   } else if (kg) {
     if (!percentage_ok(q[KE_PDR_KOORD_GPU])) return false;

@@ -349,7 +349,7 @@ def _device_annotations(p, spec, hints, joint):
             p.gpu_required_topology_scope = abi.SCOPES.get(h["requiredTopologyScope"], abi.SCOPE_UNKNOWN)
     p.device_hints = bits
     if joint:  # parsePodDeviceShareExtensions: keep the requested types without an ApplyForAll hint
-        req = {"gpu": any(p.device_requests[i] for i in range(7)), "rdma": p.device_requests[abi.PDR["koordinator.sh/rdma"]] > 0,
+        req = {"gpu": any(p.device_requests[i] for i in abi.PDR_GPU), "rdma": p.device_requests[abi.PDR["koordinator.sh/rdma"]] > 0,
                "fpga": p.device_requests[abi.PDR["koordinator.sh/fpga"]] > 0}
         kept = [t for t in joint.get("deviceTypes", [])
                 if req.get(t) and ((hints or {}).get(t) or {}).get("allocateStrategy") != "ApplyForAll"]

@@ -2149,10 +2149,11 @@ static void ds_prepare_pod(const or_cluster* c, const ke_pod* pod, ds_pod* d) {
   if (pod->device_hint > 0 && c && pod->device_hint <= c->n_hints) h = &c->hints[pod->device_hint - 1];
   const int64_t* q = pod->device_requests;
   /* GPU combination flags (utils.go:38-52) */
-  enum { NV = 1, AMD = 2, KGPU = 4, SHARED = 8, CORE = 16, MEM = 32, RATIO = 64 };
+  enum { NV = 1, AMD = 2, KGPU = 4, SHARED = 8, CORE = 16, MEM = 32, RATIO = 64, DCU = 128 };
   int comb = 0;
   if (q[KE_PDR_NVIDIA_GPU] > 0) comb |= NV;
   if (q[KE_PDR_AMD_GPU] > 0) comb |= AMD;
+  if (q[KE_PDR_HYGON_DCU] > 0) comb |= DCU;
   if (q[KE_PDR_KOORD_GPU] > 0) comb |= KGPU;
   if (q[KE_PDR_GPU_SHARED] > 0) comb |= SHARED;
   if (q[KE_PDR_GPU_CORE] > 0) comb |= CORE;
@@ -2162,7 +2163,7 @@ static void ds_prepare_pod(const or_cluster* c, const ke_pod* pod, ds_pod* d) {
     int ok = 0;
     const int64_t core = q[KE_PDR_GPU_CORE], ratio = q[KE_PDR_GPU_MEMORY_RATIO], shared = q[KE_PDR_GPU_SHARED];
     if (comb == KGPU) ok = valid_percentage(q[KE_PDR_KOORD_GPU]);
-    else if (comb == NV || comb == AMD) ok = 1;
+    else if (comb == NV || comb == AMD || comb == DCU) ok = 1; /* ValidDeviceResourceCombinationsDefaultTrue */
     else if (comb == MEM || comb == RATIO || comb == (CORE | MEM) || comb == (CORE | RATIO))
       ok = (!(comb & CORE) || valid_percentage(core)) && (!(comb & RATIO) || valid_percentage(ratio));
     else if (comb == (SHARED | MEM) || comb == (SHARED | RATIO) || comb == (SHARED | CORE | MEM) ||
@@ -2176,8 +2177,8 @@ static void ds_prepare_pod(const or_cluster* c, const ke_pod* pod, ds_pod* d) {
     /* ConvertDeviceRequest: converted keys */
     int64_t c_core = 0, c_mem = 0, c_ratio = 0, c_shared = 0;
     int h_core = 0, h_mem = 0, h_ratio = 0, h_shared = 0;
-    if (comb == NV || comb == AMD) {
-      const int64_t n = q[comb == NV ? KE_PDR_NVIDIA_GPU : KE_PDR_AMD_GPU];
+    if (comb == NV || comb == AMD || comb == DCU) { /* utils.go:190-212 */
+      const int64_t n = q[comb == NV ? KE_PDR_NVIDIA_GPU : comb == AMD ? KE_PDR_AMD_GPU : KE_PDR_HYGON_DCU];
       c_core = c_ratio = n * 100;
       h_core = h_ratio = 1;
     } else if (comb == KGPU) {

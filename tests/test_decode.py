@@ -235,7 +235,7 @@ def _q(rng, kind):
 
 def random_pod(rng, i):
     names = ["cpu", "memory", "kubernetes.io/batch-cpu", "kubernetes.io/batch-memory", "nvidia.com/gpu",
-             "ephemeral-storage", "koordinator.sh/rdma"]
+             "ephemeral-storage", "koordinator.sh/rdma", "dcu.com/gpu", "huawei.com/npu-core"]
     def rl():
         return {n: str(_q(rng, n)) for n in names if rng.random() < (0.6 if n in ("cpu", "memory") else 0.15)}
     cs = [{"name": f"c{k}", "resources": {"requests": rl(), "limits": rl()}} for k in range(int(rng.integers(0, 3)))]
@@ -292,7 +292,7 @@ def random_pod(rng, i):
 def test_pod_random_vs_model(lib):
     rng = np.random.default_rng(11)
     xres = ["cpu", "memory", "kubernetes.io/batch-cpu", "kubernetes.io/batch-memory", "nvidia.com/gpu", "ephemeral-storage",
-            "koordinator.sh/rdma"]
+            "koordinator.sh/rdma", "dcu.com/gpu", "huawei.com/npu-core"]
     for name in xres:
         model.xres_id(name)
     table = sorted(model.XRES_IDS, key=model.XRES_IDS.get)
