@@ -6946,6 +6946,11 @@ struct DeviceState {
   hipEvent_t ev_res[EV_RING] = {};  // a batch's Reserve done (stream)
   hipEvent_t ev_sel[EV_RING] = {};  // a batch's candidate lists done (estream)
   hipEvent_t ev_start = nullptr;
+  // device_refresh's copies + scatters (no host wait since round 6): the next refresh waits on it before it reuses the
+  // staging; every reader of the rows runs on `stream` behind them or waits for an event recorded there after them
+  hipEvent_t ev_refresh = nullptr;
+  bool refresh_pending = false;
+  bool refresh_sync = false;        // KOORDEVAL_REFRESH_SYNC=1: the host waits for every refresh (A/B)
   bool pipeline = true;             // ke_set_pipeline
   bool pipe_fixup = false;          // ke_set_pipeline(2): exact lists from k_fixup for every run (else quota runs only)
   // dynamic LDS of the eval streams' LDS-free kernels: more than what a Reserve workgroup (ResLds) leaves free of
@@ -7012,6 +7017,7 @@ int device_create(Context* ctx) {
   if (const char* e = std::getenv("KOORDEVAL_EVAL_PATCH")) d->eval_patch = std::atoi(e) != 0;
   if (const char* e = std::getenv("KOORDEVAL_SELECT_AHEAD")) d->select_ahead = std::atoi(e) != 0;
   if (const char* e = std::getenv("KOORDEVAL_FIX_MERGE")) d->fix_merge = std::atoi(e) != 0;
+  if (const char* e = std::getenv("KOORDEVAL_REFRESH_SYNC")) d->refresh_sync = std::atoi(e) != 0;
   if (const char* e = std::getenv("KOORDEVAL_T_HELPERS_IGNORE")) d->t_help_ignore = std::atoi(e) != 0;
   HIP_OK(hipStreamCreateWithPriority(&d->stream, hipStreamNonBlocking, prio_hi));
   HIP_OK(hipStreamCreateWithPriority(&d->estream, hipStreamNonBlocking, prio_lo));
@@ -7024,6 +7030,7 @@ int device_create(Context* ctx) {
     HIP_OK(hipEventCreateWithFlags(&d->ev_sel[e], hipEventDisableTiming));
   }
   HIP_OK(hipEventCreateWithFlags(&d->ev_start, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&d->ev_refresh, hipEventDisableTiming));
   d->capacity = ((int64_t)ctx->cfg.node_capacity + 255) & ~255LL;
   d->soa.stride = d->capacity;
   HIP_OK(hipMalloc(&d->soa.f, sizeof(int64_t) * NUM_I64_FIELDS * d->capacity));
@@ -7188,6 +7195,7 @@ void device_destroy(Context* ctx) {
     if (d->ev_sel[e]) (void)hipEventDestroy(d->ev_sel[e]);
   }
   if (d->ev_start) (void)hipEventDestroy(d->ev_start);
+  if (d->ev_refresh) (void)hipEventDestroy(d->ev_refresh);
   if (d->estream) (void)hipStreamDestroy(d->estream);
   if (d->cstream) (void)hipStreamDestroy(d->cstream);
   if (d->ev_setup) (void)hipEventDestroy(d->ev_setup);
@@ -7560,6 +7568,10 @@ int device_refresh(Context* ctx, int64_t now) {
                        crows.size() + words(sizeof(int32_t) * cidx.size()) + words(sizeof(Row) * rows.size()) +
                        words(sizeof(int32_t) * idx.size());
   if (total == 0) return KE_OK;
+  if (d->refresh_pending) {  // the previous refresh's copies still read the staging / device staging buffers
+    HIP_OK(hipEventSynchronize(d->ev_refresh));
+    d->refresh_pending = false;
+  }
   if (!d->h_refresh.resize(total)) return fail(KE_ERR_DEVICE, "hipHostMalloc of the row staging");
   size_t at = 0;
   auto stage = [&](const void* src, size_t bytes) {  // -> the staged copy
@@ -7633,7 +7645,14 @@ int device_refresh(Context* ctx, int64_t now) {
                        d->d_idx, (int)n, make_kargs(ctx, now));
     HIP_OK(hipGetLastError());
   }
-  HIP_OK(hipStreamSynchronize(d->stream));  // (the staging is reused; the eval streams read the rows)
+  // no host wait: the staging is reused only after ev_refresh (above), and the kernels reading the rows run on
+  // `stream` after the scatters or wait for an event recorded there after them (device_schedule_enqueue's ev_start)
+  if (d->refresh_sync) {
+    HIP_OK(hipStreamSynchronize(d->stream));
+  } else {
+    HIP_OK(hipEventRecord(d->ev_refresh, d->stream));
+    d->refresh_pending = true;
+  }
   return KE_OK;
 }
 
