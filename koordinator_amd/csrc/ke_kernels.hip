@@ -6321,6 +6321,7 @@ __global__ __launch_bounds__(64) void k_numa_views(SoA s, const DevPod* __restri
   const int n = min(w.n, NV_MAX);
   const int lane = (int)threadIdx.x;
   constexpr int NVW = 2 + 2 * NV_MAX;  // 0 hint, 1 node, 2 + q trial q, 2 + NV_MAX + q its requiredResources
+  static_assert(NVW <= 64, "k_numa_views: one lane per view");
   __shared__ NumaNode s_v[NVW];
   __shared__ NumaCs s_cs[NVW];
   __shared__ uint8_t s_scr[NVW][CPU_SLOTS];

@@ -112,7 +112,7 @@ struct RsvOvr {
 // [2*id + r] (keys: bit 2*id + r) of the hint view (mergedMatchedAllocatable) and of each trial q < n over
 // RestoreReservation's matched set in index order (mergedMatchedAllocated + its remained); a Restricted trial's
 // requiredResources (its remained, signed; has_req = the reserve pod holds NUMA amounts).
-constexpr int NV_MAX = 8;
+constexpr int NV_MAX = 31;  // k_numa_views: 2 + 2 x NV_MAX lanes (hint, node, trials, their requiredResources) = the wave
 // A pod binding CPUs adds preferredCPUs: the hint view's mergedMatchedRemainCPUs (pref[NV_MAX]), each trial's
 // mergedMatchedAllocatedCPUs ∪ its remainedCPUs (pref[q]) and a Restricted trial's remainedCPUs (rpref[q], rem_cpus[q]
 // of them) -- getAvailableCPUs with RefCount given back, the per-NUMA-id counts of the CPUs allocateCPUSet may take

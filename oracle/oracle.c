@@ -5415,7 +5415,7 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
      * hints through its allocate-from-reservation trials (numa_admit) for a pod without device requests; refused: a
      * DeviceShare pod's joint hints there, a binding pod with fractional CPUs or under a required FullPCPUs policy (the
      * product counts a view's CPUs; preferredCPUs taken first may split cores there), more than 8 such reservations
-     * of the pod on one node (the product's NV_MAX) */
+     * of the pod on one node (the product's NV_MAX, 31) */
     if (c->ralloc) {
       const int binds = st.rcb || st.invalid || (node_bind && pods[p].requests[KE_RES_CPU] > 0);
       const int dev = !d.skip || d.h;
@@ -5436,7 +5436,7 @@ static int or_resv_supported(const or_cluster* c, int32_t n_pods, const ke_pod* 
           same += or_resv_usable(&c->resv[r2]) && c->resv[r2].node == node &&
                   (or_holds_of(&c->ralloc[r2]) & (KE_RSV_HOLDS_NUMA | KE_RSV_HOLDS_CPUSET));
         }
-        if (same > 8) return KE_ERR_UNSUPPORTED;
+        if (same > 31) return KE_ERR_UNSUPPORTED;
       }
     }
   }

@@ -512,3 +512,57 @@ def test_ignored_binding_pods_numa_policy_parity(gpu, seed):
                and a["cpuset"][p].any()]
     assert len(on_held) >= 10  # ignored binding pods given cpusets on policy nodes with held CPUs
     assert ev.check_records(synth.T0) == 0
+
+
+def many_per_node_setup(n, seed, n_pods, layers=12):
+    """`layers` rounds of reservation holdings on every node (each round's reserve pods hold NUMA amounts / cpusets out
+    of what the earlier rounds left), so a node carries up to `layers` NUMA/CPU-holding reservations; matched pods list
+    every reservation of three random nodes (more than 8 holding ones on a node: beyond the earlier NV_MAX of 8)."""
+    rng = np.random.default_rng(seed)
+    cl = synth.make_cluster(n, synth.BASE_SEED + seed, amplified_fraction=0.2)
+    zones, tabs = synth.make_numa_cpus(cl, synth.BASE_SEED + seed + 1)
+    cl.nodes["cpu_bind_policy"] = 0
+    rs, al, res = [], [], []
+    for layer in range(layers):
+        r, a, x = synth.make_reservation_holdings(cl, synth.BASE_SEED + seed + 10 + layer, zones, tabs, None, frac=1.0)
+        rs.append(r), al.append(a), res.extend(x)
+    rs, al = np.concatenate(rs), np.concatenate(al)
+    cfg = synth.config(n)
+    ev, o = Evaluator(cfg), Oracle(cfg, n)
+    for h in (ev, o):
+        synth.load_into(h, cl)
+        synth.load_numa(h, zones)
+        synth.load_cpus(h, tabs)
+        h.reservations_load(rs, al, res)
+    pods = synth.make_numa_cpuset_pods(n_pods, synth.BASE_SEED + seed + 3, cpuset_fraction=0.3, policy_fraction=0.4)
+    cs = np.isin(pods["qos_class"], [abi.QOS_LSE, abi.QOS_LSR]) & (pods["priority_class"] == abi.PRIORITY_PROD)
+    ok = ~cs & (pods["requests"][:, 2:] == 0).all(1) & (pods["has_other_requests"] == 0) \
+        & (pods["device_requests"] == 0).all(1)
+    matches = [[] for _ in range(n_pods)]
+    for p in np.flatnonzero(ok & (rng.random(n_pods) < 0.9)):
+        pods["reservation_matched"][p] = abi.RSV_MATCHED
+        nodes = rng.choice(n, 3, replace=False)
+        matches[p] = np.flatnonzero(np.isin(rs["node"], nodes)).tolist()
+    holds = (al["numa"] != 0).any(1) | (al["cpuset"] != 0).any(1)
+    per_node = np.bincount(rs["node"][holds & (rs["available"] != 0)], minlength=n)
+    return cl, ev, o, pods, matches, per_node, rs
+
+
+def test_matched_numa_policy_many_reservations_per_node(gpu):
+    """More than 8 (up to NV_MAX = 31) NUMA/CPU-holding matched reservations on one node under NUMA policies:
+    k_numa_views runs one lane per trial and per requiredResources view (2 + 2 x 31 lanes = the wave) -- placements,
+    scores, NUMA allocations, cpusets and reservation state bit-exact with the oracle."""
+    cl, ev, o, pods, matches, per_node, _ = many_per_node_setup(48, 1501, 160)
+    assert per_node.max() > 8
+    c1, s1 = ev.schedule(pods, synth.T0, matches=matches)
+    c0, s0 = o.schedule(pods, synth.T0, matches=matches)
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5].ravel().tolist()
+    assert np.array_equal(s1, s0)
+    assert np.array_equal(ev.last_numa_allocations, o.last_numa_allocations)
+    assert np.array_equal(ev.last_cpusets, o.last_cpusets)
+    _holdings_equal(ev, o)
+    a1, a0 = ev.last_allocations(), o.last_allocations()
+    assert np.array_equal(a1["reservation"], a0["reservation"])
+    into = np.flatnonzero(a1["reservation"] > 0)
+    assert len(into) >= 8 and (per_node[c1[into]] > 8).sum() >= 3  # placed into reservations of crowded nodes
+    assert ev.check_records(synth.T0) == 0

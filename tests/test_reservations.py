@@ -772,3 +772,22 @@ def test_numa_policy_binding_case_through_schedule():
     assert c.tolist() == [0] and o.last_allocations()["reservation"].tolist() == [1]
     assert np.array_equal(o.last_cpusets[0], _cpus(case["want_cpus"]))
     assert o.last_numa_allocations[0][0] == 4000 and not o.last_numa_allocations[0][1:].any()
+
+
+def test_numa_views_beyond_nv_max_refused(lib):
+    """More than NV_MAX = 31 NUMA/CPU-holding matched reservations of a pod on one node under a NUMA policy: refused by
+    the product's argument checks (before any device work) and by the oracle twin alike."""
+    from test_gpu_reservation_holdings import many_per_node_setup
+    from koordinator_amd import KoordEvalError
+    cl, ev, o, pods, matches, per_node, rs = many_per_node_setup(16, 1502, 60, layers=40)
+    node = int(np.argmax(per_node))
+    assert per_node[node] > 31
+    p = next(i for i, m in enumerate(matches) if m)
+    q = pods[p:p + 1].copy()
+    q["numa_topology_policy"] = abi.NUMA_POLICY_RESTRICTED
+    m = [np.flatnonzero(rs["node"] == node).tolist()]
+    with pytest.raises(KoordEvalError) as e:
+        ev.schedule(q, synth.T0, matches=m)
+    assert e.value.code == abi.ERR_UNSUPPORTED
+    with pytest.raises(RuntimeError):
+        o.schedule(q, synth.T0, matches=m)
