@@ -1219,6 +1219,10 @@ int ke_debug_numa_deferred(ke_ctx* ctx, int64_t* n);
 /* DeviceShare batches of the last ke_schedule that stopped early because a pod's NormalizeScore max may have
  * moved (their remaining pods were re-run as a new batch). */
 int ke_debug_ds_cuts(ke_ctx* ctx, int32_t* cuts);
+/* Reservation-matched pods of the last ke_schedule that ran fused behind their preceding plain segment (placed by
+ * that call: out2[0]) and those whose speculation a plain pod of the segment broke (run again alone: out2[1]);
+ * DESIGN.md §4k.  KOORDEVAL_RSV_FUSE=0 turns the fusion off. */
+int ke_debug_rsv_fused(ke_ctx* ctx, int64_t* out2);
 /* Diagnostic build only (-DKE_PROF_REPLAY): shader cycles per pod of the replay loop's phases since the
  * last call — best unchanged candidate, row fetch issue, re-evaluation, its wave max, decision / adoption,
  * Reserve, next pod's changed flags — and the pod count (cyc8[7]); zeros in the product build. */

@@ -586,6 +586,7 @@ EXPORTS = {
     "ke_debug_resolve_wave1": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ke_debug_numa_deferred": (C.c_int, [C.c_void_p, C.POINTER(i64)]),
     "ke_debug_ds_cuts": (C.c_int, [C.c_void_p, C.POINTER(i32)]),
+    "ke_debug_rsv_fused": (C.c_int, [C.c_void_p, C.POINTER(i64)]),
     "ke_debug_spec_failed": (C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
     "ke_bench_eval_kernel": (C.c_int, [C.c_void_p, i32, C.c_void_p, i64, i32, C.POINTER(C.c_double)]),
     "ke_row_bytes": (C.c_int, []),

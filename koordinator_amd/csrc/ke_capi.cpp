@@ -17,6 +17,8 @@ int device_eval(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, u
                 int16_t* la, int16_t* numa, int16_t* ds, int16_t* total, int32_t* best);
 int device_schedule(Context* ctx, int32_t n_pods, const ke_pod* pods, int64_t now, int32_t* chosen, int32_t* score);
 int device_rsv_result(Context* ctx, int32_t* out4);
+int device_rsv_gate(const Context* ctx);
+int device_refresh(Context* ctx, int64_t now, bool defer);
 int device_ds_views(Context* ctx, const ke_pod& pod, int64_t now, const std::vector<DsView>& views,
                     std::vector<DsViewOut>& out);
 int device_rsv_views(Context* ctx, const ke_pod& pod, int64_t now, const std::vector<RsvView>& views,
@@ -38,6 +40,12 @@ bool device_sharded(const Context* ctx);
 }  // namespace ke
 
 using namespace ke;
+
+// KOORDEVAL_RSV_FUSE=0: every reservation-matched pod is a segment of its own (the fused path's A/B)
+static const bool kFuseMatched = [] {
+  const char* e = std::getenv("KOORDEVAL_RSV_FUSE");
+  return !e || std::atoi(e) != 0;
+}();
 
 // The release records of one completed call (ke_last_allocations / ke_unreserve read them from the Context):
 // taken when the call completes, restored when ke_schedule_wait collects it, so a wait on an earlier ticket
@@ -398,6 +406,13 @@ int ke_node_resources_get(ke_ctx* ctx, int32_t node, int32_t cap, ke_node_resour
   const NodeState& ns = ctx->c.nodes[node];
   *n = (int32_t)ns.xres.size();
   for (int32_t e = 0; e < cap && e < *n; e++) res[e] = ns.xres[e];
+  return KE_OK;
+}
+
+int ke_debug_rsv_fused(ke_ctx* ctx, int64_t* out2) {
+  if (!ctx || !out2) return fail(KE_ERR_INVALID, "ke_debug_rsv_fused arguments");
+  out2[0] = ctx->c.last_rsv_fused;
+  out2[1] = ctx->c.last_rsv_fused_gated;
   return KE_OK;
 }
 
@@ -949,13 +964,14 @@ static int schedule_sync(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_
   auto ign_views = [&](int32_t p) { return ignored(p) && resv_ignore_needs_views(c, pods[p], c.staged[(size_t)p].flags); };
   auto alone = [&](int32_t p) { return matched(p) || ign_views(p); };
   std::vector<int32_t> assumed((size_t)n_pods, 0);
+  c.last_rsv_fused = c.last_rsv_fused_gated = 0;
   for (int32_t s0 = 0; s0 < n_pods || (n_pods == 0 && s0 == 0);) {
     int32_t s1 = s0;
     const bool ign = s0 < n_pods && ignored(s0);
     while (s1 < n_pods && !barrier(s1) && !alone(s1) && ignored(s1) == ign) s1++;
     // a barrier pod ends its segment; a matched one is alone
     if (s1 < n_pods && (s1 == s0 || (!alone(s1) && barrier(s1) && ignored(s1) == ign))) s1++;
-    const int32_t len = s1 - s0;
+    int32_t len = s1 - s0;
     const bool rsv = len == 1 && matched(s0);
     mirror_join(c);  // (the previous segment's host mirror thread: this one reads the node state)
     if (ign) resv_ignore_begin(c);
@@ -1030,9 +1046,89 @@ static int schedule_sync(ke_ctx* ctx, int32_t n_pods, const ke_pod* pods, int64_
       if (rsv) resv_finish(c, -1, pods[s0], &dummy);
       if (ign) resv_ignore_end(c);
     };
-    rc = device_schedule(&c, len, pods + s0, now_ns, chosen + (n_pods ? s0 : 0), score ? score + s0 : nullptr);
+    // A plain segment followed by a matched pod without allocate-from-reservation views or decisions (DESIGN.md §4k,
+    // "fused"): the pod's nomination and rows are taken now, on the state before the segment, and it runs last in the
+    // segment's call -- k_rsv_check gates it on the device when a plain pod of the segment took a node of its
+    // reservations, and the host then runs it as a segment of its own.
+    bool fuse = kFuseMatched && !ign && !rsv && len >= 1 && s1 < n_pods && pods[s1].reservation_matched == KE_RSV_MATCHED &&
+                matched(s1) && c.quotas.empty() && !device_sharded(&c) && (size_t)s1 < c.staged.size() &&
+                !(c.staged[(size_t)s1].flags & (PF_CPUSET | PF_DS | PF_DS_HINT));
+    if (fuse) {
+      rc = device_refresh(&c, now_ns, false);  // the segment's rows (no host wait)
+      if (rc) return rc;
+      const int32_t* ids = mids.data() + moff[(size_t)s1];
+      const int32_t n_ids = moff[(size_t)s1 + 1] - moff[(size_t)s1];
+      resv_views(c, pods[s1], ids, n_ids);
+      fuse = c.rsv_views.empty();
+      if (fuse) {
+        resv_ds_views(c, pods[s1], ids, n_ids);
+        fuse = c.ds_views.empty();
+      }
+      if (fuse) {
+        resv_numa_views(c, pods[s1], ids, n_ids);
+        fuse = c.numa_views.empty();
+      }
+      if (!fuse) {  // its own segment after all: the views' rows back as they were
+        for (const DsView& v : c.ds_views) resv_node_restore(c, v.node);
+        for (const NumaRsvView& v : c.numa_views) resv_node_restore(c, v.node);
+        int32_t dummy = 0;
+        resv_finish(c, -1, pods[s1], &dummy);
+      } else {
+        rc = resv_prepare(c, pods[s1], ids, n_ids, false);
+        if (rc) return rc;
+        if (!c.rsv_ovr.empty() || !c.numa_cs_views.empty()) {
+          int32_t dummy = 0;
+          resv_finish(c, -1, pods[s1], &dummy);
+          fuse = false;
+        }
+      }
+    }
+    c.rsv_fused = fuse;
+    rc = device_schedule(&c, fuse ? len + 1 : len, pods + s0, now_ns, chosen + (n_pods ? s0 : 0), score ? score + s0 : nullptr);
+    c.rsv_fused = false;
+    if (rc && fuse) {
+      int32_t dummy = 0;
+      resv_finish(c, -1, pods[s1], &dummy);
+    }
     if (rc) return undo_rsv(), rc;
     if (ign) resv_ignore_end(c);
+    if (fuse && device_rsv_gate(&c)) {
+      // a plain pod took a node of the fused pod's reservations: the pod placed nothing; its nomination and rows are
+      // undone and it runs next as a segment of its own (the call's per-pod outputs: the segment's only)
+      int32_t dummy = 0;
+      resv_finish(c, -1, pods[s1], &dummy);
+      chosen[s1] = -1;
+      auto cut = [&](auto& v, size_t per) {
+        if (v.size() > per * (size_t)len) v.resize(per * (size_t)len);
+      };
+      cut(c.last_dev_alloc, 1);
+      cut(c.last_cpusets, 4);
+      cut(c.last_vf, 2 * KE_MAX_MINORS);
+      cut(c.last_numa_alloc, (size_t)KE_MAX_NUMA * KE_NRES);
+      cut(c.last_pod_lat, 1);
+      if (!c.last_batch_ms.empty()) c.last_batch_ms.pop_back();
+      c.last_rsv_fused_gated++;
+      fuse = false;
+    } else if (fuse) {  // the Reservation plugin's outcome of the fused pod, as for a matched segment below
+      const int32_t local = chosen[s1] < 0 ? -1 : chosen[s1] - off;
+      int32_t pick[4] = {local, 0, 0, -1};
+      if (!c.rsv_pairs.empty()) rc = device_rsv_result(&c, pick);
+      if (!rc && local >= 0 && local != pick[0]) rc = fail(KE_ERR_DEVICE, "k_rsv_pick winner differs from the placement");
+      if (rc) {
+        int32_t dummy = 0;
+        resv_finish(c, -1, pods[s1], &dummy);
+        return rc;
+      }
+      if (local >= 0 && score) score[s1] = (int32_t)((int64_t)score[s1] + c.cfg.weight_reservation * (int64_t)pick[1]);
+      const size_t L = (size_t)len;
+      resv_finish(c, local, pods[s1], &assumed[(size_t)s1],
+                  c.last_cpusets.size() >= 4 * (L + 1) ? c.last_cpusets.data() + 4 * L : nullptr,
+                  c.last_numa_alloc.size() >= (L + 1) * KE_MAX_NUMA * KE_NRES ? c.last_numa_alloc.data() + L * KE_MAX_NUMA * KE_NRES : nullptr,
+                  c.last_dev_alloc.size() > L ? c.last_dev_alloc[L] : 0);
+      c.last_rsv_fused++;
+      len++;
+      s1++;
+    }
     if (rsv) {
       const int32_t local = chosen[s0] < 0 ? -1 : chosen[s0] - off;
       int32_t pick[4] = {local, 0, 0, -1};  // no usable matched reservation: no Reservation score

@@ -223,6 +223,8 @@ struct Context {
   std::vector<RsvPair> rsv_pairs;
   std::vector<int32_t> rsv_nominated;
   bool rsv_affinity = false;  // the segment's pod has a required reservation affinity
+  bool rsv_fused = false;
+  int64_t last_rsv_fused = 0, last_rsv_fused_gated = 0;  // fused matched pods placed / gated (statistics)     // the call's last pod is a matched pod fused behind plain pods (ke_schedule)
   std::vector<RsvOvr> rsv_ovr;  // its allocate-from-reservation decisions per node (SoA::rovr)
   // its allocate-from-reservation trials (resv_views -> k_rsv_views): per view the reservation and the outcome
   std::vector<RsvView> rsv_views;

@@ -3104,9 +3104,10 @@ __device__ __forceinline__ int32_t fast_total(const NodeFast& f, const DevPod& p
 // ---------------------------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------------------------
-__global__ void k_scatter_rows(SoA s, const Row* __restrict__ rows, const int32_t* __restrict__ idx, int n, KArgs k) {
+__global__ void k_scatter_rows(SoA s, const Row* __restrict__ rows, const int32_t* __restrict__ idx, int n, KArgs k,
+                               const int32_t* __restrict__ gate) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
+  if (t >= n || (gate && *gate)) return;
   const int64_t i = idx[t];
   const Row& r = rows[t];
 #pragma unroll
@@ -3396,6 +3397,30 @@ __global__ __launch_bounds__(256) void k_argmax1(const uint16_t* __restrict__ sc
 // does not count and the others are infeasible.
 // A DeviceShare pod (dsraw != nullptr): a node's plugin total includes DeviceShare's normalized score, as in
 // k_argmax1.  A winner whose pair carries RSV_PAIR_RESERVE_FAILS is not placed (its DeviceShare Reserve fails).
+// A reservation-matched pod fused behind the plain pods of its ke_schedule segment: its nomination and
+// rows were taken on the host before those pods ran, valid unless one of them was placed on a node of its reservations
+// (their Requested / pod count / assign cache feed fitsNode and the rows).  k_rsv_check sets *gate then; the gated
+// scatters keep the plain rows, k_rsv_gate_apply empties the pod's candidates (its Reserve places nothing) and the
+// host runs the pod again as a segment of its own.
+__global__ __launch_bounds__(256) void k_rsv_check(const int32_t* __restrict__ chosen, int n_prev,
+                                                   const RsvPair* __restrict__ pr, int K, int32_t global_offset,
+                                                   int32_t* __restrict__ gate) {
+  __shared__ int32_t hit;
+  if (threadIdx.x == 0) hit = 0;
+  __syncthreads();
+  for (int i = (int)threadIdx.x; i < n_prev; i += (int)blockDim.x) {
+    const int32_t c = chosen[i];
+    if (c < 0) continue;
+    for (int q = 0; q < K; q++)
+      if (pr[q].node + global_offset == c) hit = 1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *gate = hit;
+}
+__global__ void k_rsv_gate_apply(const int32_t* __restrict__ gate, int32_t* __restrict__ cand_cnt) {
+  if (threadIdx.x == 0 && *gate) cand_cnt[0] = 0;
+}
+
 __global__ __launch_bounds__(64) void k_rsv_pick(const uint16_t* __restrict__ scores, const RsvPair* __restrict__ pr,
                                                  int K, int64_t w, int affinity, uint32_t* __restrict__ cand,
                                                  int32_t* __restrict__ out, const uint16_t* __restrict__ dsraw,
@@ -6951,6 +6976,8 @@ struct DeviceState {
   // staging; every reader of the rows runs on `stream` behind them or waits for an event recorded there after them
   hipEvent_t ev_refresh = nullptr;
   bool refresh_pending = false;
+  std::vector<std::function<void(const int32_t*)>> deferred;  // device_refresh(defer): its scatters, gated
+  int32_t* d_rsv_gate = nullptr;    // k_rsv_check's word: a fused matched pod's speculation failed (1)
   bool refresh_sync = false;        // KOORDEVAL_REFRESH_SYNC=1: the host waits for every refresh (A/B)
   bool pipeline = true;             // ke_set_pipeline
   bool pipe_fixup = false;          // ke_set_pipeline(2): exact lists from k_fixup for every run (else quota runs only)
@@ -7076,7 +7103,8 @@ int device_create(Context* ctx) {
   return KE_OK;
 }
 
-int device_refresh(Context* ctx, int64_t now);
+int device_refresh(Context* ctx, int64_t now, bool defer = false);
+int device_refresh_flush(Context* ctx, const int32_t* gate);
 // k_rsv_views for one KE_RSV_MATCHED pod: the allocate-from-reservation trials `views` on the current device
 // state (synchronous; the segment's device_schedule follows)
 static KArgs make_kargs(const Context* ctx, int64_t now);
@@ -7172,6 +7200,12 @@ int device_rsv_result(Context* ctx, int32_t* out4) {
   return KE_OK;
 }
 
+// the fused matched pod's gate after its call: 1 = a plain pod of the call took a node of its reservations
+int device_rsv_gate(const Context* ctx) {
+  const DeviceState* d = ctx->dev;
+  return d->h_rsv_out.size() >= 5 ? d->h_rsv_out[4] : 0;
+}
+
 void device_destroy(Context* ctx) {
   DeviceState* d = ctx->dev;
   if (!d) return;
@@ -7186,7 +7220,7 @@ void device_destroy(Context* ctx) {
                   d->d_cpurows, d->d_cpusets, d->d_aff, d->soa.qt, d->soa.qm, d->d_sched, d->d_stale,
                   d->d_stale_cnt, d->d_pre, d->d_trows, d->d_tcnt, d->d_parts_done, d->d_scores2, d->d_split2, d->d_chg, d->soa.rec, d->soa.pt, d->soa.kerr,
                   d->soa.xf, d->soa.xm, d->d_xrows, d->soa.dsx, d->d_ph, d->d_vfo, d->d_rsv, d->d_rsv_out, d->d_rsv_st,
-                  d->d_rsv_views, d->d_ds_views, d->d_numa_views, d->d_rovr};
+                  d->d_rsv_views, d->d_ds_views, d->d_numa_views, d->d_rovr, d->d_rsv_gate};
   if (d->estream) (void)hipStreamSynchronize(d->estream);
   if (d->estream2) (void)hipStreamSynchronize(d->estream2);
   for (void* p : ptrs)
@@ -7359,9 +7393,10 @@ static KArgs make_kargs(const Context* ctx, int64_t now) {
 }
 
 constexpr int DS_ROW_WORDS = NUM_DS_FIELDS + NUM_DS_MASKS + NUM_DSX;  // device fields, masks, hint words
-__global__ void k_scatter_ds(SoA s, const int64_t* __restrict__ rows, const int32_t* __restrict__ idx, int n) {
+__global__ void k_scatter_ds(SoA s, const int64_t* __restrict__ rows, const int32_t* __restrict__ idx, int n,
+                             const int32_t* __restrict__ gate) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
+  if (t >= n || (gate && *gate)) return;
   const int64_t i = idx[t];
   const int64_t* r = rows + (int64_t)t * DS_ROW_WORDS;
   for (int f = 0; f < NUM_DS_FIELDS; f++) s.ds[f * s.stride + i] = r[f];
@@ -7384,9 +7419,10 @@ static int ensure_ds(Context* ctx) {
 
 constexpr int NUMA_ROW_WORDS = NUM_NUMA_FIELDS + 1;  // int64 fields + the mask word
 
-__global__ void k_scatter_numa(SoA s, const int64_t* __restrict__ rows, const int32_t* __restrict__ idx, int n) {
+__global__ void k_scatter_numa(SoA s, const int64_t* __restrict__ rows, const int32_t* __restrict__ idx, int n,
+                             const int32_t* __restrict__ gate) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
+  if (t >= n || (gate && *gate)) return;
   const int64_t i = idx[t];
   const int64_t* r = rows + (int64_t)t * NUMA_ROW_WORDS;
   for (int f = 0; f < NUM_NUMA_FIELDS; f++) s.nf[f * s.stride + i] = r[f];
@@ -7408,9 +7444,10 @@ static int ensure_numa(Context* ctx) {
 
 constexpr int XROW_WORDS = NUM_XF + 1;  // ext row: NUM_XF int64 + the mask
 
-__global__ void k_scatter_ext(SoA s, const int64_t* __restrict__ rows, const int32_t* __restrict__ idx, int n) {
+__global__ void k_scatter_ext(SoA s, const int64_t* __restrict__ rows, const int32_t* __restrict__ idx, int n,
+                             const int32_t* __restrict__ gate) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
+  if (t >= n || (gate && *gate)) return;
   const int64_t i = idx[t];
   const int64_t* r = rows + (int64_t)t * XROW_WORDS;
   for (int f = 0; f < NUM_XF; f++) s.xf[f * s.stride + i] = r[f];
@@ -7431,9 +7468,10 @@ static int ensure_ext(Context* ctx) {
 
 constexpr int CPU_ROW_WORDS = CPU_SLOTS + NUM_CS_FIELDS;  // records (one int64 each) + summary
 
-__global__ void k_scatter_cpu(SoA s, const int64_t* __restrict__ rows, const int32_t* __restrict__ idx, int n) {
+__global__ void k_scatter_cpu(SoA s, const int64_t* __restrict__ rows, const int32_t* __restrict__ idx, int n,
+                              const int32_t* __restrict__ gate) {
   const int t = blockIdx.x;
-  if (t >= n) return;
+  if (t >= n || (gate && *gate)) return;
   const int64_t i = idx[t];
   const int64_t* r = rows + (int64_t)t * CPU_ROW_WORDS;
   reinterpret_cast<int64_t*>(s.cpu + i * CPU_SLOTS)[threadIdx.x] = r[threadIdx.x];
@@ -7456,8 +7494,9 @@ static int ensure_cpu(Context* ctx) {
 }
 
 // Re-derive rows of dirty / time-expired nodes and scatter them into the SoA.
-int device_refresh(Context* ctx, int64_t now) {
+int device_refresh(Context* ctx, int64_t now, bool defer) {
   DeviceState* d = ctx->dev;
+  d->deferred.clear();
   int rc = ensure_ds(ctx);  // (first use marks the nodes dirty: before the checks below)
   if (rc) return rc;
   rc = ensure_numa(ctx);
@@ -7602,31 +7641,37 @@ int device_refresh(Context* ctx, int64_t now) {
     const int n = (int)dsidx.size();
     rc = table(&d->d_dsrows, &d->ds_staging_cap, dsrows, dsidx, DS_ROW_WORDS, &didx);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_scatter_ds, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, d->stream, d->soa, d->d_dsrows, didx, n);
-    HIP_OK(hipGetLastError());
+    const int64_t* rows = d->d_dsrows;
+    d->deferred.push_back([=](const int32_t* gate) {
+      hipLaunchKernelGGL(k_scatter_ds, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, d->stream, d->soa, rows, didx, n, gate);
+    });
   }
   if (!nidx.empty()) {
     const int n = (int)nidx.size();
     rc = table(&d->d_numarows, &d->numa_staging_cap, nrows, nidx, NUMA_ROW_WORDS, &didx);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_scatter_numa, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, d->stream, d->soa, d->d_numarows,
-                       didx, n);
-    HIP_OK(hipGetLastError());
+    const int64_t* rows = d->d_numarows;
+    d->deferred.push_back([=](const int32_t* gate) {
+      hipLaunchKernelGGL(k_scatter_numa, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, d->stream, d->soa, rows, didx, n, gate);
+    });
   }
   if (!xidx.empty()) {
     const int n = (int)xidx.size();
     rc = table(&d->d_xrows, &d->ext_staging_cap, xrows, xidx, XROW_WORDS, &didx);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_scatter_ext, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, d->stream, d->soa, d->d_xrows,
-                       didx, n);
-    HIP_OK(hipGetLastError());
+    const int64_t* rows = d->d_xrows;
+    d->deferred.push_back([=](const int32_t* gate) {
+      hipLaunchKernelGGL(k_scatter_ext, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, d->stream, d->soa, rows, didx, n, gate);
+    });
   }
   if (!cidx.empty()) {
     const int n = (int)cidx.size();
     rc = table(&d->d_cpurows, &d->cpu_staging_cap, crows, cidx, CPU_ROW_WORDS, &didx);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_scatter_cpu, dim3((unsigned)n), dim3(CPU_SLOTS), 0, d->stream, d->soa, d->d_cpurows, didx, n);
-    HIP_OK(hipGetLastError());
+    const int64_t* rows = d->d_cpurows;
+    d->deferred.push_back([=](const int32_t* gate) {
+      hipLaunchKernelGGL(k_scatter_cpu, dim3((unsigned)n), dim3(CPU_SLOTS), 0, d->stream, d->soa, rows, didx, n, gate);
+    });
   }
   if (!rows.empty()) {
     HIP_OK(hipSetDevice(d->device));
@@ -7642,10 +7687,27 @@ int device_refresh(Context* ctx, int64_t now) {
                           d->stream));
     HIP_OK(hipMemcpyAsync(d->d_idx, stage(idx.data(), sizeof(int32_t) * n), sizeof(int32_t) * n, hipMemcpyHostToDevice,
                           d->stream));
-    hipLaunchKernelGGL(k_scatter_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, d->stream, d->soa, d->d_rows,
-                       d->d_idx, (int)n, make_kargs(ctx, now));
-    HIP_OK(hipGetLastError());
+    const Row* rows_d = d->d_rows;
+    const int32_t* idx_d = d->d_idx;
+    const KArgs ka = make_kargs(ctx, now);
+    const int nn = (int)n;
+    d->deferred.push_back([=](const int32_t* gate) {
+      hipLaunchKernelGGL(k_scatter_rows, dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, d->stream, d->soa, rows_d, idx_d,
+                         nn, ka, gate);
+    });
   }
+  // defer (a fused reservation-matched pod): the copies are on the stream, the scatters wait for
+  // device_refresh_flush -- behind the segment's plain pods, gated by their k_rsv_check
+  if (defer) return KE_OK;
+  return device_refresh_flush(ctx, nullptr);
+}
+
+int device_refresh_flush(Context* ctx, const int32_t* gate) {
+  DeviceState* d = ctx->dev;
+  if (d->deferred.empty()) return KE_OK;
+  for (auto& f : d->deferred) f(gate);
+  d->deferred.clear();
+  HIP_OK(hipGetLastError());
   // no host wait: the staging is reused only after ev_refresh (above), and the kernels reading the rows run on
   // `stream` after the scatters or wait for an event recorded there after them (device_schedule_enqueue's ev_start)
   if (d->refresh_sync) {
@@ -7839,7 +7901,8 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
   auto tp = clk::now();
   HIP_OK(hipSetDevice(d->device));
-  int rc = device_refresh(ctx, now);
+  const bool fused = ctx->rsv_fused;  // the last pod: a matched pod behind plain ones (its rows' scatters deferred)
+  int rc = device_refresh(ctx, now, fused);
   if (rc) return rc;
   ctx->host_ms[1] = ms_since(tp);
   ctx->last_batch_ms.clear();
@@ -7873,14 +7936,15 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   ctx->last_ds_cuts = 0;
   for (int32_t p = 0; p < n_pods;) {
     const uint32_t f = d->host_pods[p].flags;
-    if ((f & PF_CPUSET) || ((f & PF_DS) && !ds_batch) || (f & PF_DS_HINT)) {  // hinted pods: singletons
+    if ((f & PF_CPUSET) || ((f & PF_DS) && !ds_batch) || (f & PF_DS_HINT) || (fused && p == n_pods - 1)) {
+      // hinted pods and a fused matched pod: singletons
       batches.push_back({1, (f & PF_DS) != 0, (f & PF_CPUSET) != 0, false, (f & PF_DS_HINT) != 0});
       p++;
       continue;
     }
     int bp = 0;
     bool has_ds = false, ds_pods = false;
-    while (p + bp < n_pods && bp < B) {
+    while (p + bp < n_pods && bp < B && !(fused && p + bp == n_pods - 1)) {
       const uint32_t g = d->host_pods[p + bp].flags;
       if ((g & PF_CPUSET) || ((g & PF_DS) && !ds_batch) || (g & PF_DS_HINT)) break;
       has_ds = has_ds || (g & PF_DS);
@@ -7932,14 +7996,18 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   KArgs k = make_kargs(ctx, now);
   if (ctx->rsv_affinity) k.flags |= AF_RSV_ONLY;  // the Reservation Filter: RsvOvr.rfilter of the pod's nodes
   if (!ctx->rsv_pairs.empty() || ctx->rsv_affinity) {  // one matched pod (ke_schedule's segment of its own)
-    if (n_pods != 1) return fail(KE_ERR_UNSUPPORTED, "matched reservations need a singleton segment");
+    if (n_pods != 1 && !fused) return fail(KE_ERR_UNSUPPORTED, "matched reservations need a singleton segment");
     for (const RsvPair& q : ctx->rsv_pairs)
       if (q.node < 0 || q.node >= ctx->n_nodes) return fail(KE_ERR_DEVICE, "reservation pair node out of range");
     rc = ensure((void**)&d->d_rsv, &d->rsv_cap, (int64_t)sizeof(RsvPair) * (int64_t)ctx->rsv_pairs.size());
     if (rc) return rc;
-    if (!d->h_rsv_out.resize(4)) return fail(KE_ERR_DEVICE, "hipHostMalloc of the reservation staging");
-    for (int i = 0; i < 4; i++) d->h_rsv_out[i] = -1;
   }
+  if (fused || !ctx->rsv_pairs.empty() || ctx->rsv_affinity) {
+    if (!d->h_rsv_out.resize(5)) return fail(KE_ERR_DEVICE, "hipHostMalloc of the reservation staging");
+    for (int i = 0; i < 4; i++) d->h_rsv_out[i] = -1;
+    d->h_rsv_out[4] = 0;  // the fused pod's gate (k_rsv_check)
+  }
+  if (fused && !d->d_rsv_gate) HIP_OK(hipMalloc(&d->d_rsv_gate, sizeof(int32_t)));
   // the matched pod's pairs and allocate-from-reservation decisions, staged page-locked (the previous call's copies
   // from this buffer completed with that call)
   const size_t rsv_bytes = sizeof(RsvPair) * ctx->rsv_pairs.size(), ovr_bytes = sizeof(RsvOvr) * ctx->rsv_ovr.size();
@@ -7980,7 +8048,9 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
   // pipelined runs: maximal stretches of plain batches (no DeviceShare / cpuset pod) in a
   // context without NUMA policies; run_end[b] > 0 marks the first batch of a run and holds its end
   // (a lone plain batch between singletons gains nothing from the second stream: it runs serially)
-  auto eligible = [&](int b) { return d->pipeline && N > 0 && !numa && !batches[b].ds && !batches[b].cpu; };
+  auto eligible = [&](int b) {
+    return d->pipeline && N > 0 && !numa && !batches[b].ds && !batches[b].cpu && !(fused && b == n_batches - 1);
+  };
   std::vector<int> run_end((size_t)n_batches, 0);
   for (int b = 0; b < n_batches;) {
     if (!eligible(b)) {
@@ -8144,7 +8214,8 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
       if (argmax1) {  // d_cand[0] zeroed by k_batch_begin
         hipLaunchKernelGGL((ds ? k_argmax1<true> : k_argmax1<false>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
                            es, scores, 0, N, d->d_dsraw, d->d_dsmax, k.wp_ds, d->d_cand, d->d_cand_cnt);
-        if (!ctx->rsv_pairs.empty() || ctx->rsv_affinity) {  // the pod's matched reservations: the Reservation plugin
+        if ((!ctx->rsv_pairs.empty() || ctx->rsv_affinity) && (!fused || b == n_batches - 1)) {
+          // the pod's matched reservations: the Reservation plugin
           hipLaunchKernelGGL(k_rsv_pick, dim3(1), dim3(64), 0, es, scores, d->d_rsv, (int)ctx->rsv_pairs.size(),
                              (int64_t)ctx->cfg.weight_reservation, (int)ctx->rsv_affinity, d->d_cand, d->d_rsv_out,
                              ds ? d->d_dsraw : nullptr, d->d_dsmax, k.wp_ds);
@@ -8318,9 +8389,20 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
     const int bp = batches[b].pods;
     const bool ds = batches[b].ds, cpu = batches[b].cpu;
     const int32_t* bbase = d_bases + b;
+    const bool fused_b = fused && b == n_batches - 1;
+    if (fused_b) {  // the fused matched pod: the speculation check, then its rows (gated) before its eval
+      hipLaunchKernelGGL(k_rsv_check, dim3(1), dim3(256), 0, d->stream, d->d_chosen, bases[b], d->d_rsv,
+                         (int)ctx->rsv_pairs.size(), ctx->cfg.global_node_offset, d->d_rsv_gate);
+      rc = device_refresh_flush(ctx, d->d_rsv_gate);
+      if (rc) return rc;
+    }
     if (pre_b != b) rc = eval_select(b, false, d->stream);
     pre_b = -1;
     if (rc) return rc;
+    if (fused_b) {
+      hipLaunchKernelGGL(k_rsv_gate_apply, dim3(1), dim3(64), 0, d->stream, d->d_rsv_gate, d->d_cand_cnt);
+      HIP_OK(hipMemcpyAsync(d->h_rsv_out.data() + 4, d->d_rsv_gate, sizeof(int32_t), hipMemcpyDeviceToHost, d->stream));
+    }
     if (bp == 1) {  // one pod: the single-node Reserve (cpuset accumulator when it binds)
       int elo = 0, ehi = 0;  // nodes whose affinities this batch's eval stored in d_aff (binding batches)
       if (cpu && numa) {
@@ -8348,7 +8430,7 @@ int device_schedule_enqueue(Context* ctx, int32_t n_pods, const ke_pod* pods, in
         HIP_OK(hipMemcpyAsync(d->h_cut.data(), d->d_dsmax + DSB_CUT, sizeof(int32_t), hipMemcpyDeviceToHost, d->stream));
         // the next serial batch's eval + select go in behind the read-back, so the device keeps working while the
         // host waits for the cut (without one they stand; with one the re-run batch overwrites what they wrote)
-        if (b + 1 < n_batches && run_end[b + 1] == 0) {
+        if (b + 1 < n_batches && run_end[b + 1] == 0 && !(fused && b + 1 == n_batches - 1)) {
           const bool keep = rerun;
           rerun = false;
           rc = eval_select(b + 1, false, d->stream);

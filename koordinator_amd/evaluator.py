@@ -390,6 +390,13 @@ class Evaluator:
     def set_profiling(self, sample_every):
         self._check(self.lib.ke_set_profiling(self.h, sample_every))
 
+    def rsv_fused(self):
+        """(fused, gated): matched pods of the last schedule placed behind their plain segment in its call, and those
+        a plain pod of the segment broke (run again alone) -- ke_debug_rsv_fused."""
+        out = (abi.i64 * 2)()
+        self._check(self.lib.ke_debug_rsv_fused(self.h, out))
+        return int(out[0]), int(out[1])
+
     def ds_cuts(self):
         """DeviceShare batches of the last schedule that stopped early (NormalizeScore max may have moved)."""
         n = abi.i32()

@@ -13,6 +13,8 @@ int device_eval(Context*, int32_t, const ke_pod*, int64_t, uint8_t*, uint8_t*, i
                 int32_t*) { return none(); }
 int device_schedule(Context*, int32_t, const ke_pod*, int64_t, int32_t*, int32_t*) { return none(); }
 int device_rsv_result(Context*, int32_t*) { return none(); }
+int device_rsv_gate(const Context*) { return 0; }
+int device_refresh(Context*, int64_t, bool) { return none(); }
 int device_schedule_enqueue(Context*, int32_t, const ke_pod*, int64_t, bool, DevFinish*) { return none(); }
 void device_swap_call_buffers(Context*) {}
 void device_quiesce(Context*) {}

@@ -469,3 +469,26 @@ def test_general_reservation_resources_parity(gpu):
     assert np.array_equal(c1, c0) and np.array_equal(s1, s0)
     assert ev.check_records(synth.T0) == 0
     ev.close()
+
+
+@pytest.mark.parametrize("n_nodes", [300, 24], ids=["spread", "crowded"])
+def test_fused_matched_pods_parity(gpu, n_nodes):
+    """Matched pods fused behind their plain segment: nomination and rows taken before the segment ran,
+    k_rsv_check gating the pod when a plain pod of the segment took a node of its reservations (then it runs again
+    alone).  On 300 nodes most matched pods run fused; on 24 nodes, most carrying reservations, plain pods keep taking
+    their nodes and the gate fires -- bit-exact with the oracle on placements, scores, reservation state and release
+    records either way."""
+    ev, o, pods, matches = _matched_setup(n_nodes, 977, 400)
+    c1, s1 = ev.schedule(pods, synth.T0, matches=matches)
+    c0, s0 = o.schedule(pods, synth.T0, matches=matches)
+    fused, gated = ev.rsv_fused()
+    assert np.array_equal(c1, c0), np.argwhere(c1 != c0)[:5].ravel().tolist()
+    assert np.array_equal(s1, s0)
+    _resv_equal(ev, o)
+    a1, a0 = ev.last_allocations(), o.last_allocations()
+    for k in ("node", "reservation"):
+        assert np.array_equal(a1[k], a0[k]), k
+    assert fused >= 10
+    if n_nodes == 24:
+        assert gated >= 1
+    assert ev.check_records(synth.T0) == 0

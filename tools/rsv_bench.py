@@ -3,8 +3,9 @@ reservations (the nominated-reservation path) against the same q
 
 N synthetic nodes (the config-3 generator) hold `--resv-nodes` x N reservations in owner groups of ~25 (Default /
 Aligned / Restricted, AllocateOnce, orders, partly allocated; the reserve pods counted in NodeInfo.Requested);
-`--matched` of the pods match one owner group's reservations.  Each matched pod is a segment of its own in
-ke_schedule (host nomination + k_rsv_pick), every other pod keeps the batched path.  Prints one JSON line:
+`--matched` of the pods match one owner group's reservations.  A matched pod runs in the call of the plain
+segment before it (its nomination and rows taken before that segment, gated by k_rsv_check; KOORDEVAL_RSV_FUSE=0: a
+segment of its own), every other pod keeps the batched path.  Prints one JSON line:
 evals/s with and without matched pods, the added cost per matched pod, and an oracle-checked prefix.
 Usage: python tools/rsv_bench.py [--nodes 50000] [--pods 12800] [--matched 0.05] ...
 """
@@ -75,20 +76,22 @@ def main():
         c, s = ev.schedule(q, synth.T0, matches=m)
         dt = time.perf_counter() - t0
         into = int((ev.last_allocations()["reservation"] > 0).sum())
+        fused = ev.rsv_fused()
         ev.close()
-        return dt, c, s, into
+        return dt, c, s, into, fused
 
     warm = Evaluator(cfg)  # kernels loaded, code paths exercised
     synth.load_into(warm, cl)
     warm.reservations_load(rs)
     warm.schedule(matched_pods[:64], synth.T0, matches=matches[:64])
     warm.close()
-    t_plain, _, _, _ = run(pods, None)
-    t_rsv, c1, s1, into = run(matched_pods, matches)
+    t_plain, _, _, _, _ = run(pods, None)
+    t_rsv, c1, s1, into, fused = run(matched_pods, matches)
     out = {"workload": f"{N} nodes x {P} pods, {len(rs)} reservations, {n_matched} matched pods",
            "evals_per_s_plain": P * N / t_plain, "evals_per_s_matched": P * N / t_rsv,
            "s_plain": t_plain, "s_matched": t_rsv,
-           "ms_per_matched_pod": (t_rsv - t_plain) * 1e3 / max(n_matched, 1), "placed_into_reservations": into}
+           "ms_per_matched_pod": (t_rsv - t_plain) * 1e3 / max(n_matched, 1), "placed_into_reservations": into,
+           "fused_matched_pods": {"fused": fused[0], "gated": fused[1]}}
     # one matched pod per ke_schedule call: the fixed cost of its segment, by host phase
     ev = Evaluator(cfg)
     synth.load_into(ev, cl)
