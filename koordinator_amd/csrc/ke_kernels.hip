@@ -6904,7 +6904,7 @@ struct DeviceState {
   int64_t ds_staging_cap = 0;
   PinnedVec<DevPod> host_pods;    // the last uploaded queue (batch segmentation), page-locked
   PinnedVec<uint8_t> h_out;       // ke_schedule's readback staging (placements, allocations, stamps)
-  PinnedVec<int64_t> h_refresh;   // device_refresh's row staging (every table's rows + indices, one sync)
+  PinnedVec<int64_t> h_refresh[2];  // device_refresh's row staging (every table's rows + indices), two in turn
   PinnedVec<uint8_t> h_rsv;       // a matched pod's RsvPair / RsvOvr uploads
   PinnedVec<int32_t> h_rsv_out;   // k_rsv_pick's result words, read back by the call's own copies
   PinnedVec<int32_t> h_cut;       // a DeviceShare batch's cut word (async read-back, the next batch enqueued behind)
@@ -6974,8 +6974,9 @@ struct DeviceState {
   hipEvent_t ev_start = nullptr;
   // device_refresh's copies + scatters (no host wait since round 6): the next refresh waits on it before it reuses the
   // staging; every reader of the rows runs on `stream` behind them or waits for an event recorded there after them
-  hipEvent_t ev_refresh = nullptr;
-  bool refresh_pending = false;
+  hipEvent_t ev_refresh[2] = {};  // the copies out of h_refresh[i] done
+  bool refresh_pending[2] = {};
+  int refresh_cur = 0;
   std::vector<std::function<void(const int32_t*)>> deferred;  // device_refresh(defer): its scatters, gated
   int32_t* d_rsv_gate = nullptr;    // k_rsv_check's word: a fused matched pod's speculation failed (1)
   bool refresh_sync = false;        // KOORDEVAL_REFRESH_SYNC=1: the host waits for every refresh (A/B)
@@ -7058,7 +7059,7 @@ int device_create(Context* ctx) {
     HIP_OK(hipEventCreateWithFlags(&d->ev_sel[e], hipEventDisableTiming));
   }
   HIP_OK(hipEventCreateWithFlags(&d->ev_start, hipEventDisableTiming));
-  HIP_OK(hipEventCreateWithFlags(&d->ev_refresh, hipEventDisableTiming));
+  for (hipEvent_t& e : d->ev_refresh) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   d->capacity = ((int64_t)ctx->cfg.node_capacity + 255) & ~255LL;
   d->soa.stride = d->capacity;
   HIP_OK(hipMalloc(&d->soa.f, sizeof(int64_t) * NUM_I64_FIELDS * d->capacity));
@@ -7230,7 +7231,8 @@ void device_destroy(Context* ctx) {
     if (d->ev_sel[e]) (void)hipEventDestroy(d->ev_sel[e]);
   }
   if (d->ev_start) (void)hipEventDestroy(d->ev_start);
-  if (d->ev_refresh) (void)hipEventDestroy(d->ev_refresh);
+  for (hipEvent_t e : d->ev_refresh)
+    if (e) (void)hipEventDestroy(e);
   if (d->estream) (void)hipStreamDestroy(d->estream);
   if (d->cstream) (void)hipStreamDestroy(d->cstream);
   if (d->ev_setup) (void)hipEventDestroy(d->ev_setup);
@@ -7608,14 +7610,18 @@ int device_refresh(Context* ctx, int64_t now, bool defer) {
                        crows.size() + words(sizeof(int32_t) * cidx.size()) + words(sizeof(Row) * rows.size()) +
                        words(sizeof(int32_t) * idx.size());
   if (total == 0) return KE_OK;
-  if (d->refresh_pending) {  // the previous refresh's copies still read the staging / device staging buffers
-    HIP_OK(hipEventSynchronize(d->ev_refresh));
-    d->refresh_pending = false;
+  // the staging of the refresh before the previous one: its copies are done before it is reused (two refreshes in a
+  // row -- a fused matched pod's -- do not wait for each other)
+  const int cur = d->refresh_cur ^= 1;
+  if (d->refresh_pending[cur]) {
+    HIP_OK(hipEventSynchronize(d->ev_refresh[cur]));
+    d->refresh_pending[cur] = false;
   }
-  if (!d->h_refresh.resize(total)) return fail(KE_ERR_DEVICE, "hipHostMalloc of the row staging");
+  PinnedVec<int64_t>& hstage = d->h_refresh[cur];
+  if (!hstage.resize(total)) return fail(KE_ERR_DEVICE, "hipHostMalloc of the row staging");
   size_t at = 0;
   auto stage = [&](const void* src, size_t bytes) {  // -> the staged copy
-    void* dst = d->h_refresh.data() + at;
+    void* dst = hstage.data() + at;
     if (bytes) std::memcpy(dst, src, bytes);
     at += words(bytes);
     return dst;
@@ -7713,8 +7719,8 @@ int device_refresh_flush(Context* ctx, const int32_t* gate) {
   if (d->refresh_sync) {
     HIP_OK(hipStreamSynchronize(d->stream));
   } else {
-    HIP_OK(hipEventRecord(d->ev_refresh, d->stream));
-    d->refresh_pending = true;
+    HIP_OK(hipEventRecord(d->ev_refresh[d->refresh_cur], d->stream));
+    d->refresh_pending[d->refresh_cur] = true;
   }
   return KE_OK;
 }
